@@ -1,0 +1,156 @@
+#!/usr/bin/env python3
+"""Headline benchmark: RCCL all-reduce bus bandwidth on the scheduler-chosen k-GPU subset.
+
+BASELINE.json metric: "RCCL all-reduce bus GB/s on scheduler-chosen k-GPU subset, k=1/2/4/8".
+
+    python bench.py --gpus N --steps K --warmup W          # N=1 runs in-process
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One *step* = one out-of-place RCCL all-reduce (bf16, sum) of ``--size-mb`` MiB per GPU over the
+subset the placement core picked from the node's discovered xGMI topology (rank r runs on
+``subset[r]``).  Exactly K steps are timed between barrier + ``torch.cuda.synchronize()`` on both
+sides; the max over ranks is reported.  ``value`` is busBW = algBW * 2(k-1)/k (nccl-tests
+convention) for k >= 2; at k = 1 busBW is 0 by definition, so ``value`` is the algBW of the
+single-rank RCCL all-reduce (BASELINE.md "k=1 reports algBW only").  Per-GPU message size is fixed
+as N grows ("weak" scaling).  Data is synthetic (exactly checked once before timing).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+METRIC = "RCCL all-reduce bus GB/s on scheduler-chosen k-GPU subset, k=1/2/4/8"
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--size-mb", type=float, default=2048.0, help="per-GPU message size in MiB (default 2 GiB)")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--backend", default="native", choices=["native", "torch"])
+    ap.add_argument("--inplace", action="store_true")
+    ap.add_argument("--probe", default=None, choices=[None, "quick", "full"], help="run the HIP link probe before placement")
+    ap.add_argument("--discovery", default="auto", choices=["auto", "amdsmi", "sysfs", "fake"])
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    args = parse(argv)
+    in_launcher = "WORLD_SIZE" in os.environ and "RANK" in os.environ
+    if args.gpus > 1 and not in_launcher:
+        # Re-launch under torch.distributed.run as a CHILD process (no exec; GPU untouched here).
+        port = _free_port()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + (argv if argv is not None else sys.argv[1:])
+        return subprocess.call(cmd)
+    if not in_launcher:
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from gpu_topology_on_k8s_amd.parallel.allreduce import AllReduceRunner, DistEnv, SubsetChoice, bus_factor, choose_subset
+
+    env = DistEnv.from_env()
+    if env.world != args.gpus:
+        print(f"bench: WORLD_SIZE={env.world} but --gpus={args.gpus}", file=sys.stderr)
+        return 2
+    dist.init_process_group(backend="nccl")
+    env.store = dist.distributed_c10d._get_default_store()
+
+    # --- placement: rank 0 picks the subset, everybody binds to subset[rank] ---------------------
+    if env.rank == 0:
+        choice = choose_subset(env.world, probe=args.probe, backend=args.discovery)
+        env.store.set("gtk/subset", choice.to_json())
+    choice = SubsetChoice.from_json(env.store.get("gtk/subset").decode())
+    device = choice.devices[env.rank]
+    torch.cuda.set_device(device)
+
+    nbytes = int(args.size_mb * (1 << 20))
+    runner = AllReduceRunner(env, device, nbytes, args.dtype, backend=args.backend, inplace=args.inplace)
+    wrong = torch.tensor([runner.check()], dtype=torch.int64, device=f"cuda:{device}")
+    dist.all_reduce(wrong)
+    if int(wrong.item()) != 0:
+        print(f"bench: all-reduce correctness check FAILED ({int(wrong.item())} wrong elements)", file=sys.stderr)
+        return 3
+
+    for _ in range(args.warmup):
+        runner.step()
+    runner.synchronize()
+
+    dist.barrier(device_ids=[device])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        runner.step()
+    runner.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    dist.barrier(device_ids=[device])
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ms_per_step = elapsed / max(1, args.steps) * 1e3
+    algbw = runner.nbytes / (ms_per_step / 1e3) / 1e9
+    busbw = algbw * bus_factor(env.world)
+    value = busbw if env.world > 1 else algbw
+    runner.close()
+    if env.rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GB/s",
+            "n_gpus": env.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (rank-dependent exact pattern, verified before timing)",
+            "config": {
+                "model": "rccl-allreduce",
+                "op": "sum",
+                "message_bytes_per_gpu": runner.nbytes,
+                "inplace": args.inplace,
+                "backend": args.backend,
+                "global_batch": None,
+                "seq_len": None,
+                "parallelism": f"dp{env.world}",
+                "subset": choice.devices,
+                "placement_score": choice.score,
+                "placement_ms": choice.placement_ms,
+                "worst_subset": choice.worst,
+                "worst_score": choice.worst_score,
+                "topology_source": choice.source,
+                "probed": choice.probed,
+            },
+            "value_kind": "busbw" if env.world > 1 else "algbw (busbw = 0 at k=1)",
+            "algbw_gbps": round(algbw, 3),
+            "busbw_gbps": round(busbw, 3),
+        }
+        print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,426 @@
+// HIP/CDNA4 link-cost probe kernels (gfx950) + pybind11 bindings.
+//
+// Reference: design.md:23-59 obtains the GPU-pair link class from NVML and leaves the bandwidth
+// weight as a TODO (design.md:47).  On MI355X every GPU pair is a direct xGMI link, so the link
+// class alone cannot rank placements; instead the device plugin measures the real link-cost matrix
+// at node start with the kernels below:
+//   K1 p2p read  : kernel on the reader GPU pulls a peer buffer over xGMI, staged through LDS by
+//                  LDS-DMA (global_load_lds_dwordx4) and stored to local HBM.
+//   K2 p2p write : kernel on the source GPU pushes local HBM into the peer buffer.
+//   K3 hbm copy  : self pair (k=1 baseline), same kernel with both pointers local.
+//   K4 mfma warm : v_mfma_f32_32x32x16_bf16 loop to lift clocks before timing, also reporting the
+//                  achieved dense bf16 rate.
+// The copy kernel exists in two staging forms (LDS-DMA and plain register staging) so the
+// rocprofv3 counter profile can show what LDS staging costs/buys on a pure stream (profiles/).
+//
+// Geometry (CDNA4): 256-thread blocks (4 wave64), each wave moves 64 lanes x 16 B = 1 KiB per
+// instruction; UNROLL=4 instructions in flight per lane -> 16 KiB LDS image per block, so up to
+// 8 blocks (32 waves, the CU maximum) are resident per CU inside the 160 KiB LDS.  Grid = CUs x 8
+// with a grid-stride loop: >>256 workgroups fills all 8 XCDs; a streaming copy has no reuse so no
+// XCD remap is needed (each byte is touched once).
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace py = pybind11;
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define HIP_CHECK(expr)                                                                          \
+  do {                                                                                           \
+    hipError_t _e = (expr);                                                                      \
+    if (_e != hipSuccess)                                                                        \
+      throw std::runtime_error(std::string(#expr " failed: ") + hipGetErrorString(_e) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__));                       \
+  } while (0)
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kUnroll = 4;
+constexpr int kTileVec = kBlock * kUnroll;  // 16-byte vectors per block-iteration (16 KiB)
+constexpr int kBlocksPerCU = 8;
+
+using gptr_t = const __attribute__((address_space(1))) void*;
+using lptr_t = __attribute__((address_space(3))) void*;
+
+// ---------------------------------------------------------------------------------------------
+// K1/K2/K3: LDS-DMA staged copy.  Each wave issues kUnroll global_load_lds_dwordx4 into its own
+// 1 KiB LDS slices (wave-uniform base + lane*16: the DMA's lane-linear rule), drains vmcnt, then
+// each lane stores back the 16 B its own lane fetched, so no cross-wave barrier is needed.
+template <bool kNonTemporal>
+__global__ __launch_bounds__(kBlock) void copy_lds_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                          size_t n_vec) {
+  __shared__ u32x4 lds[kTileVec];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const size_t n_full = (n_vec / kTileVec) * kTileVec;
+  for (size_t base = (size_t)blockIdx.x * kTileVec; base < n_full; base += (size_t)gridDim.x * kTileVec) {
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const size_t off = base + (size_t)u * kBlock + wave * 64;
+      __builtin_amdgcn_global_load_lds((gptr_t)(src + off + lane), (lptr_t)(lds + u * kBlock + wave * 64), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const size_t off = base + (size_t)u * kBlock + wave * 64 + lane;
+      u32x4 v = lds[u * kBlock + wave * 64 + lane];
+      if (kNonTemporal)
+        __builtin_nontemporal_store(v, dst + off);
+      else
+        dst[off] = v;
+    }
+  }
+  // tail (< one tile): plain per-thread copy
+  for (size_t i = n_full + (size_t)blockIdx.x * kBlock + threadIdx.x; i < n_vec; i += (size_t)gridDim.x * kBlock)
+    dst[i] = src[i];
+}
+
+// Register-staged variant of the same stream (kUnroll independent 16-B loads in flight per lane).
+template <bool kNonTemporal>
+__global__ __launch_bounds__(kBlock) void copy_reg_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                          size_t n_vec) {
+  const size_t n_full = (n_vec / kTileVec) * kTileVec;
+  for (size_t base = (size_t)blockIdx.x * kTileVec; base < n_full; base += (size_t)gridDim.x * kTileVec) {
+    u32x4 r[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) r[u] = src[base + (size_t)u * kBlock + threadIdx.x];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      if (kNonTemporal)
+        __builtin_nontemporal_store(r[u], dst + base + (size_t)u * kBlock + threadIdx.x);
+      else
+        dst[base + (size_t)u * kBlock + threadIdx.x] = r[u];
+    }
+  }
+  for (size_t i = n_full + (size_t)blockIdx.x * kBlock + threadIdx.x; i < n_vec; i += (size_t)gridDim.x * kBlock)
+    dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(kBlock) void fill_pattern_kernel(unsigned int* __restrict__ p, size_t n_words,
+                                                              unsigned int seed) {
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n_words; i += (size_t)gridDim.x * kBlock)
+    p[i] = (unsigned int)(i * 2654435761u) ^ seed;
+}
+
+// K4: MFMA warm-up.  Each wave keeps 4 independent 32x32 accumulators so back-to-back
+// v_mfma_f32_32x32x16_bf16 issue is not serialised on the dependent-accumulator latency.
+__global__ __launch_bounds__(kBlock) void mfma_warmup_kernel(float* __restrict__ out, int iters) {
+  bf16x8 a, b;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    a[i] = (__bf16)((threadIdx.x & 7) * 0.125f - 0.5f);
+    b[i] = (__bf16)(i * 0.0625f - 0.25f);
+  }
+  f32x16 acc0 = {}, acc1 = {}, acc2 = {}, acc3 = {};
+  for (int it = 0; it < iters; ++it) {
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc1, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc2, 0, 0, 0);
+    acc3 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc3, 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s += acc0[i] + acc1[i] + acc2[i] + acc3[i];
+  out[(size_t)blockIdx.x * kBlock + threadIdx.x] = s;
+}
+
+// ---------------------------------------------------------------------------------------------
+struct DeviceGuard {
+  int prev = 0;
+  explicit DeviceGuard(int dev) {
+    HIP_CHECK(hipGetDevice(&prev));
+    HIP_CHECK(hipSetDevice(dev));
+  }
+  ~DeviceGuard() { (void)hipSetDevice(prev); }
+};
+
+struct DevBuf {
+  void* p = nullptr;
+  int dev = -1;
+  size_t bytes = 0;
+  DevBuf(int d, size_t b) : dev(d), bytes(b) {
+    DeviceGuard g(d);
+    HIP_CHECK(hipMalloc(&p, b));
+  }
+  ~DevBuf() {
+    if (p) {
+      int prev = 0;
+      (void)hipGetDevice(&prev);
+      (void)hipSetDevice(dev);
+      (void)hipFree(p);
+      (void)hipSetDevice(prev);
+    }
+  }
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+};
+
+int num_cus(int dev) {
+  int cus = 0;
+  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  return std::max(cus, 1);
+}
+
+void enable_peer(int from, int to) {
+  if (from == to) return;
+  int can = 0;
+  HIP_CHECK(hipDeviceCanAccessPeer(&can, from, to));
+  if (!can) throw std::runtime_error("device " + std::to_string(from) + " cannot access peer " + std::to_string(to));
+  DeviceGuard g(from);
+  hipError_t e = hipDeviceEnablePeerAccess(to, 0);
+  if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+    throw std::runtime_error(std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(e));
+  (void)hipGetLastError();
+}
+
+void launch_copy(const std::string& kind, bool nt, const void* src, void* dst, size_t n_vec, int grid, hipStream_t s) {
+  auto* S = reinterpret_cast<const u32x4*>(src);
+  auto* D = reinterpret_cast<u32x4*>(dst);
+  if (kind == "lds") {
+    if (nt)
+      hipLaunchKernelGGL(copy_lds_kernel<true>, dim3(grid), dim3(kBlock), 0, s, S, D, n_vec);
+    else
+      hipLaunchKernelGGL(copy_lds_kernel<false>, dim3(grid), dim3(kBlock), 0, s, S, D, n_vec);
+  } else if (kind == "reg") {
+    if (nt)
+      hipLaunchKernelGGL(copy_reg_kernel<true>, dim3(grid), dim3(kBlock), 0, s, S, D, n_vec);
+    else
+      hipLaunchKernelGGL(copy_reg_kernel<false>, dim3(grid), dim3(kBlock), 0, s, S, D, n_vec);
+  } else if (kind == "sdma") {
+    HIP_CHECK(hipMemcpyAsync(dst, src, n_vec * 16, hipMemcpyDeviceToDevice, s));
+    return;
+  } else {
+    throw std::invalid_argument("kind must be lds|reg|sdma");
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
+// Verify a few windows of dst against the host-side pattern.
+bool verify_pattern(const DevBuf& dst, size_t n_words, unsigned int seed) {
+  const size_t win = std::min<size_t>(n_words, 1 << 16);
+  std::vector<size_t> starts = {0, n_words / 2 - std::min(n_words / 2, win / 2), n_words - win};
+  std::vector<unsigned int> h(win);
+  DeviceGuard g(dst.dev);
+  for (size_t st : starts) {
+    HIP_CHECK(hipMemcpy(h.data(), (const unsigned int*)dst.p + st, win * 4, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < win; ++i) {
+      unsigned int want = (unsigned int)((st + i) * 2654435761u) ^ seed;
+      if (h[i] != want) return false;
+    }
+  }
+  return true;
+}
+
+struct CopyResult {
+  int src, dst, exec, iters, grid;
+  size_t bytes;
+  std::string kind;
+  bool nontemporal, ok;
+  double ms_per_iter, gbps;
+};
+
+CopyResult copy_bw_impl(int src_dev, int dst_dev, int exec_dev, size_t bytes, int iters, int warmup,
+                        const std::string& kind, bool nontemporal, int blocks_per_cu) {
+  if (bytes < 16 || bytes % 16) throw std::invalid_argument("bytes must be a positive multiple of 16");
+  if (exec_dev != src_dev && exec_dev != dst_dev) throw std::invalid_argument("exec_dev must be src or dst");
+  if (iters < 1) throw std::invalid_argument("iters >= 1");
+  int ndev = 0;
+  HIP_CHECK(hipGetDeviceCount(&ndev));
+  for (int d : {src_dev, dst_dev})
+    if (d < 0 || d >= ndev) throw std::invalid_argument("device index out of range");
+  if (src_dev != dst_dev) enable_peer(exec_dev, exec_dev == src_dev ? dst_dev : src_dev);
+
+  DevBuf src(src_dev, bytes), dst(dst_dev, bytes);
+  const size_t n_vec = bytes / 16;
+  const unsigned int seed = 0x9e3779b9u ^ (unsigned)(src_dev * 131 + dst_dev);
+  {
+    DeviceGuard g(src_dev);
+    hipLaunchKernelGGL(fill_pattern_kernel, dim3(num_cus(src_dev) * 4), dim3(kBlock), 0, 0, (unsigned int*)src.p,
+                       bytes / 4, seed);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipDeviceSynchronize());
+  }
+  DeviceGuard g(exec_dev);
+  hipStream_t s;
+  HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  const int grid = num_cus(exec_dev) * std::max(1, blocks_per_cu);
+  hipEvent_t e0, e1;
+  HIP_CHECK(hipEventCreate(&e0));
+  HIP_CHECK(hipEventCreate(&e1));
+  float ms = 0.f;
+  try {
+    for (int i = 0; i < warmup; ++i) launch_copy(kind, nontemporal, src.p, dst.p, n_vec, grid, s);
+    HIP_CHECK(hipEventRecord(e0, s));
+    for (int i = 0; i < iters; ++i) launch_copy(kind, nontemporal, src.p, dst.p, n_vec, grid, s);
+    HIP_CHECK(hipEventRecord(e1, s));
+    HIP_CHECK(hipEventSynchronize(e1));
+    HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  } catch (...) {
+    (void)hipStreamSynchronize(s);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipStreamDestroy(s);
+    throw;
+  }
+  HIP_CHECK(hipEventDestroy(e0));
+  HIP_CHECK(hipEventDestroy(e1));
+  HIP_CHECK(hipStreamDestroy(s));
+  const bool ok = verify_pattern(dst, bytes / 4, seed);
+  const double sec = ms / 1e3 / iters;
+  // gbps = bytes copied per second (one direction over the link; for a self copy HBM moves 2x)
+  return CopyResult{src_dev, dst_dev, exec_dev, iters, grid, bytes, kind, nontemporal, ok, (double)ms / iters,
+                    (double)bytes / sec / 1e9};
+}
+
+py::dict to_dict(const CopyResult& c) {
+  py::dict r;
+  r["src"] = c.src;
+  r["dst"] = c.dst;
+  r["exec"] = c.exec;
+  r["bytes"] = c.bytes;
+  r["iters"] = c.iters;
+  r["kind"] = c.kind;
+  r["nontemporal"] = c.nontemporal;
+  r["grid"] = c.grid;
+  r["ms_per_iter"] = c.ms_per_iter;
+  r["gbps"] = c.gbps;
+  r["ok"] = c.ok;
+  return r;
+}
+
+py::dict copy_bw(int src_dev, int dst_dev, int exec_dev, size_t bytes, int iters, int warmup, const std::string& kind,
+                 bool nontemporal, int blocks_per_cu) {
+  CopyResult c;
+  {
+    py::gil_scoped_release nogil;
+    c = copy_bw_impl(src_dev, dst_dev, exec_dev, bytes, iters, warmup, kind, nontemporal, blocks_per_cu);
+  }
+  return to_dict(c);
+}
+
+py::dict mfma_warmup(int dev, double target_ms, int iters_per_launch) {
+  py::gil_scoped_release nogil_outer;
+  DeviceGuard g(dev);
+  const int grid = num_cus(dev) * 4;  // 16 waves per CU = 4 per SIMD
+  DevBuf out(dev, (size_t)grid * kBlock * sizeof(float));
+  hipEvent_t e0, e1;
+  HIP_CHECK(hipEventCreate(&e0));
+  HIP_CHECK(hipEventCreate(&e1));
+  int launches = 0;
+  float total_ms = 0.f;
+  auto t0 = std::chrono::steady_clock::now();
+  HIP_CHECK(hipEventRecord(e0, 0));
+  do {
+    hipLaunchKernelGGL(mfma_warmup_kernel, dim3(grid), dim3(kBlock), 0, 0, (float*)out.p, iters_per_launch);
+    HIP_CHECK(hipGetLastError());
+    ++launches;
+    HIP_CHECK(hipDeviceSynchronize());
+    total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  } while (total_ms < target_ms && launches < 100000);
+  // timed launch, clocks now lifted
+  HIP_CHECK(hipEventRecord(e0, 0));
+  hipLaunchKernelGGL(mfma_warmup_kernel, dim3(grid), dim3(kBlock), 0, 0, (float*)out.p, iters_per_launch);
+  HIP_CHECK(hipEventRecord(e1, 0));
+  HIP_CHECK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  HIP_CHECK(hipEventDestroy(e0));
+  HIP_CHECK(hipEventDestroy(e1));
+  const double flops = 2.0 * 32 * 32 * 16 * 4.0 * (double)iters_per_launch * (grid * (kBlock / 64));
+  py::gil_scoped_acquire gil;
+  py::dict r;
+  r["device"] = dev;
+  r["launches"] = launches;
+  r["warm_ms"] = total_ms;
+  r["timed_ms"] = ms;
+  r["tflops"] = flops / (ms / 1e3) / 1e12;
+  return r;
+}
+
+py::dict device_props(int dev) {
+  hipDeviceProp_t p;
+  HIP_CHECK(hipGetDeviceProperties(&p, dev));
+  char bus[64] = {0};
+  HIP_CHECK(hipDeviceGetPCIBusId(bus, sizeof(bus), dev));
+  py::dict r;
+  r["index"] = dev;
+  r["name"] = std::string(p.name);
+  r["gcn_arch"] = std::string(p.gcnArchName);
+  r["cus"] = p.multiProcessorCount;
+  r["total_mem"] = (size_t)p.totalGlobalMem;
+  r["lds_per_block"] = (size_t)p.sharedMemPerBlock;
+  r["clock_khz"] = p.clockRate;
+  r["mem_clock_khz"] = p.memoryClockRate;
+  r["mem_bus_width"] = p.memoryBusWidth;
+  r["l2_bytes"] = p.l2CacheSize;
+  r["pci_bus_id"] = std::string(bus);
+  r["warp_size"] = p.warpSize;
+  return r;
+}
+
+int device_count() {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+bool can_access_peer(int a, int b) {
+  if (a == b) return true;
+  int can = 0;
+  HIP_CHECK(hipDeviceCanAccessPeer(&can, a, b));
+  return can != 0;
+}
+
+// Full ordered-pair matrix: entry [i][j] = GB/s of moving data from device i to device j.
+// "read" executes on j (pull over the link), "write" on i (push).  Diagonal = local HBM copy.
+std::vector<std::vector<double>> probe_matrix(const std::vector<int>& devs, size_t bytes, int iters, int warmup,
+                                              const std::string& mode, const std::string& kind, bool nontemporal,
+                                              int blocks_per_cu) {
+  const size_t n = devs.size();
+  std::vector<std::vector<double>> m(n, std::vector<double>(n, 0.0));
+  for (size_t i = 0; i < n; ++i)
+    for (size_t j = 0; j < n; ++j) {
+      int s = devs[i], d = devs[j];
+      int ex = (mode == "write") ? s : d;
+      CopyResult r = copy_bw_impl(s, d, ex, bytes, iters, warmup, kind, nontemporal, blocks_per_cu);
+      if (!r.ok)
+        throw std::runtime_error("probe copy verification failed for pair " + std::to_string(s) + "->" + std::to_string(d));
+      m[i][j] = r.gbps;
+    }
+  return m;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_probe, m) {
+  m.doc() = "HIP/CDNA4 (gfx950) link probe kernels: LDS-DMA staged p2p/HBM copy, MFMA warm-up";
+  m.def("device_count", &device_count);
+  m.def("device_props", &device_props, py::arg("dev"));
+  m.def("can_access_peer", &can_access_peer, py::arg("a"), py::arg("b"));
+  m.def("copy_bw", &copy_bw, py::arg("src_dev"), py::arg("dst_dev"), py::arg("exec_dev"), py::arg("bytes"),
+        py::arg("iters") = 10, py::arg("warmup") = 2, py::arg("kind") = "lds", py::arg("nontemporal") = false,
+        py::arg("blocks_per_cu") = kBlocksPerCU);
+  m.def("mfma_warmup", &mfma_warmup, py::arg("dev"), py::arg("target_ms") = 50.0, py::arg("iters_per_launch") = 4096);
+  m.def("probe_matrix", &probe_matrix, py::arg("devs"), py::arg("bytes") = (size_t)256 << 20, py::arg("iters") = 5,
+        py::arg("warmup") = 1, py::arg("mode") = "read", py::arg("kind") = "lds", py::arg("nontemporal") = false,
+        py::arg("blocks_per_cu") = kBlocksPerCU, py::call_guard<py::gil_scoped_release>());
+  m.attr("BLOCK") = kBlock;
+  m.attr("UNROLL") = kUnroll;
+  m.attr("BLOCKS_PER_CU") = kBlocksPerCU;
+}

@@ -1,0 +1,528 @@
+// Native GPU topology discovery for MI355X nodes (pybind11 module `_topo`).
+//
+// Reference: design.md:23-59 — the device plugin queries the P2P link type of every GPU pair via
+// NVML (cgo FFI) at init; design.md:57-74 stores it in `map[uint]map[uint]gpuTopologyType`.
+// MI355X-native replacement:
+//   * amdsmi backend: amdsmi_topo_get_link_type (hops + INTERNAL/PCIE/XGMI), link weight,
+//     min/max link bandwidth, NUMA node, P2P accessibility, compute/memory partition, xGMI link
+//     status, enumeration info (render/card minors, HSA and HIP ids).  libamd_smi is dlopen'ed so
+//     the module (and the sysfs backend) still loads on hosts without amdsmi.
+//   * KFD sysfs backend: /sys/class/kfd/kfd/topology/nodes/*/{properties,io_links,p2p_links}.
+//     Takes a root path so tests can point it at a synthetic tree.
+// Both return the same dict schema, consumed by gpu_topology_on_k8s_amd/topology/discovery.py.
+#include <amd_smi/amdsmi.h>
+#include <dirent.h>
+#include <dlfcn.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace py = pybind11;
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// Common result model
+struct Dev {
+  int index = 0;
+  std::string uuid, bdf, partition = "SPX", memory_partition = "NPS1", model, gfx;
+  int numa = 0, render_minor = -1, card = -1, kfd_node = -1, hip_id = -1, physical = -1;
+  uint64_t vram = 0;
+  int xgmi_links_up = -1;
+  int cus = 0;
+  bool healthy = true;
+  uint64_t location = 0;  // domain<<16 | bdf: physical-package key
+};
+
+struct Result {
+  std::string source;
+  std::vector<Dev> devs;
+  std::vector<std::vector<int>> link_type, hops;  // link_type uses LinkType of model.py
+  std::vector<std::vector<double>> weight, min_bw, max_bw;
+  std::vector<std::vector<int>> p2p;
+  std::vector<std::string> warnings;
+};
+
+// LinkType values mirrored from gpu_topology_on_k8s_amd/topology/model.py
+enum : int { LT_SELF = 0, LT_INTERNAL = 1, LT_XGMI = 2, LT_PCIE = 3, LT_PCIE_SYS = 4, LT_UNKNOWN = 5 };
+
+void init_mats(Result& r) {
+  const size_t n = r.devs.size();
+  r.link_type.assign(n, std::vector<int>(n, LT_UNKNOWN));
+  r.hops.assign(n, std::vector<int>(n, 0));
+  r.weight.assign(n, std::vector<double>(n, 0.0));
+  r.min_bw.assign(n, std::vector<double>(n, 0.0));
+  r.max_bw.assign(n, std::vector<double>(n, 0.0));
+  r.p2p.assign(n, std::vector<int>(n, 0));
+  for (size_t i = 0; i < n; ++i) {
+    r.link_type[i][i] = LT_SELF;
+    r.p2p[i][i] = 1;
+  }
+}
+
+void assign_physical(Result& r) {
+  std::map<uint64_t, int> pkg;
+  for (auto& d : r.devs) {
+    auto it = pkg.find(d.location);
+    if (it == pkg.end()) it = pkg.emplace(d.location, (int)pkg.size()).first;
+    d.physical = it->second;
+  }
+  // XCPs of one package: INTERNAL links regardless of what the backend reported
+  for (size_t i = 0; i < r.devs.size(); ++i)
+    for (size_t j = 0; j < r.devs.size(); ++j)
+      if (i != j && r.devs[i].physical == r.devs[j].physical) {
+        r.link_type[i][j] = LT_INTERNAL;
+        r.hops[i][j] = 0;
+        r.p2p[i][j] = 1;
+      }
+}
+
+py::dict to_py(const Result& r) {
+  py::list gpus;
+  for (const auto& d : r.devs) {
+    py::dict g;
+    g["index"] = d.index;
+    g["uuid"] = d.uuid;
+    g["bdf"] = d.bdf;
+    g["numa"] = d.numa;
+    g["render_minor"] = d.render_minor;
+    g["card"] = d.card;
+    g["kfd_node"] = d.kfd_node;
+    g["hip_id"] = d.hip_id;
+    g["physical"] = d.physical;
+    g["partition"] = d.partition;
+    g["memory_partition"] = d.memory_partition;
+    g["model"] = d.model;
+    g["gfx"] = d.gfx;
+    g["vram_bytes"] = d.vram;
+    g["healthy"] = d.healthy;
+    g["xgmi_links_up"] = d.xgmi_links_up;
+    g["cus"] = d.cus;
+    gpus.append(g);
+  }
+  py::dict out;
+  out["source"] = r.source;
+  out["gpus"] = gpus;
+  out["link_type"] = r.link_type;
+  out["hops"] = r.hops;
+  out["weight"] = r.weight;
+  out["min_bw_mbps"] = r.min_bw;
+  out["max_bw_mbps"] = r.max_bw;
+  out["p2p"] = r.p2p;
+  out["warnings"] = r.warnings;
+  return out;
+}
+
+std::string fmt_bdf(uint64_t domain, uint64_t bus, uint64_t dev, uint64_t fn) {
+  char buf[32];
+  snprintf(buf, sizeof(buf), "%04llx:%02llx:%02llx.%llx", (unsigned long long)domain, (unsigned long long)bus,
+           (unsigned long long)dev, (unsigned long long)fn);
+  return buf;
+}
+
+// ------------------------------------------------------------------------------------------------
+// amdsmi backend (dlopen)
+struct AmdSmi {
+  void* h = nullptr;
+// decltype of the declared prototypes: no link-time dependency on libamd_smi
+  decltype(&amdsmi_init) init = nullptr;
+  decltype(&amdsmi_shut_down) shut_down = nullptr;
+  decltype(&amdsmi_get_socket_handles) get_socket_handles = nullptr;
+  decltype(&amdsmi_get_processor_handles) get_processor_handles = nullptr;
+  decltype(&amdsmi_get_processor_type) get_processor_type = nullptr;
+  decltype(&amdsmi_get_gpu_device_bdf) get_bdf = nullptr;
+  decltype(&amdsmi_get_gpu_device_uuid) get_uuid = nullptr;
+  decltype(&amdsmi_get_gpu_enumeration_info) get_enum = nullptr;
+  decltype(&amdsmi_topo_get_numa_node_number) get_numa = nullptr;
+  decltype(&amdsmi_topo_get_link_weight) get_weight = nullptr;
+  decltype(&amdsmi_get_minmax_bandwidth_between_processors) get_minmax = nullptr;
+  decltype(&amdsmi_topo_get_link_type) get_link_type = nullptr;
+  decltype(&amdsmi_is_P2P_accessible) is_p2p = nullptr;
+  decltype(&amdsmi_get_gpu_compute_partition) get_cpart = nullptr;
+  decltype(&amdsmi_get_gpu_memory_partition) get_mpart = nullptr;
+  decltype(&amdsmi_get_gpu_asic_info) get_asic = nullptr;
+  decltype(&amdsmi_get_gpu_memory_total) get_mem_total = nullptr;
+  decltype(&amdsmi_get_gpu_xgmi_link_status) get_xgmi_status = nullptr;
+
+  template <class F>
+  void bind(F& f, const char* sym, bool required) {
+    f = reinterpret_cast<F>(dlsym(h, sym));
+    if (!f && required) throw std::runtime_error(std::string("amdsmi symbol missing: ") + sym);
+  }
+
+  explicit AmdSmi(const std::string& path) {
+    h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+    if (!h) throw std::runtime_error(std::string("dlopen amdsmi failed: ") + dlerror());
+    bind(init, "amdsmi_init", true);
+    bind(shut_down, "amdsmi_shut_down", true);
+    bind(get_socket_handles, "amdsmi_get_socket_handles", true);
+    bind(get_processor_handles, "amdsmi_get_processor_handles", true);
+    bind(get_processor_type, "amdsmi_get_processor_type", true);
+    bind(get_bdf, "amdsmi_get_gpu_device_bdf", true);
+    bind(get_uuid, "amdsmi_get_gpu_device_uuid", false);
+    bind(get_enum, "amdsmi_get_gpu_enumeration_info", false);
+    bind(get_numa, "amdsmi_topo_get_numa_node_number", false);
+    bind(get_weight, "amdsmi_topo_get_link_weight", false);
+    bind(get_minmax, "amdsmi_get_minmax_bandwidth_between_processors", false);
+    bind(get_link_type, "amdsmi_topo_get_link_type", true);
+    bind(is_p2p, "amdsmi_is_P2P_accessible", false);
+    bind(get_cpart, "amdsmi_get_gpu_compute_partition", false);
+    bind(get_mpart, "amdsmi_get_gpu_memory_partition", false);
+    bind(get_asic, "amdsmi_get_gpu_asic_info", false);
+    bind(get_mem_total, "amdsmi_get_gpu_memory_total", false);
+    bind(get_xgmi_status, "amdsmi_get_gpu_xgmi_link_status", false);
+  }
+  ~AmdSmi() {
+    if (h) dlclose(h);
+  }
+};
+
+Result discover_amdsmi_impl(const std::string& lib) {
+  AmdSmi s(lib);
+  amdsmi_status_t st = s.init(AMDSMI_INIT_AMD_GPUS);
+  if (st != AMDSMI_STATUS_SUCCESS) throw std::runtime_error("amdsmi_init failed: status " + std::to_string((int)st));
+  struct Closer {
+    AmdSmi& s;
+    ~Closer() { s.shut_down(); }
+  } closer{s};
+
+  Result r;
+  r.source = "amdsmi";
+  uint32_t nsock = 0;
+  if (s.get_socket_handles(&nsock, nullptr) != AMDSMI_STATUS_SUCCESS) throw std::runtime_error("socket count");
+  std::vector<amdsmi_socket_handle> socks(nsock);
+  if (nsock && s.get_socket_handles(&nsock, socks.data()) != AMDSMI_STATUS_SUCCESS)
+    throw std::runtime_error("socket handles");
+  std::vector<amdsmi_processor_handle> handles;
+  for (auto sk : socks) {
+    uint32_t np = 0;
+    if (s.get_processor_handles(sk, &np, nullptr) != AMDSMI_STATUS_SUCCESS) continue;
+    std::vector<amdsmi_processor_handle> ph(np);
+    if (np && s.get_processor_handles(sk, &np, ph.data()) != AMDSMI_STATUS_SUCCESS) continue;
+    for (auto p : ph) {
+      processor_type_t t;
+      if (s.get_processor_type(p, &t) == AMDSMI_STATUS_SUCCESS && t == AMDSMI_PROCESSOR_TYPE_AMD_GPU) handles.push_back(p);
+    }
+  }
+  std::vector<Dev> devs(handles.size());
+  for (size_t i = 0; i < handles.size(); ++i) {
+    Dev& d = devs[i];
+    auto h = handles[i];
+    amdsmi_bdf_t bdf;
+    if (s.get_bdf(h, &bdf) == AMDSMI_STATUS_SUCCESS) {
+      d.bdf = fmt_bdf(bdf.domain_number, bdf.bus_number, bdf.device_number, bdf.function_number);
+      d.location = ((uint64_t)bdf.domain_number << 16) | ((uint64_t)bdf.bus_number << 8) | ((uint64_t)bdf.device_number << 3);
+    }
+    if (s.get_uuid) {
+      char buf[AMDSMI_MAX_STRING_LENGTH] = {0};
+      unsigned int len = sizeof(buf);
+      if (s.get_uuid(h, &len, buf) == AMDSMI_STATUS_SUCCESS) d.uuid = buf;
+    }
+    if (s.get_enum) {
+      amdsmi_enumeration_info_t e;
+      if (s.get_enum(h, &e) == AMDSMI_STATUS_SUCCESS) {
+        d.render_minor = (int)e.drm_render;
+        d.card = (int)e.drm_card;
+        d.kfd_node = (int)e.hsa_id;
+        d.hip_id = (int)e.hip_id;
+        if (d.uuid.empty()) d.uuid = e.hip_uuid;
+      }
+    }
+    if (s.get_numa) {
+      uint32_t nn = 0;
+      if (s.get_numa(h, &nn) == AMDSMI_STATUS_SUCCESS) d.numa = (int)nn;
+    }
+    if (s.get_cpart) {
+      char buf[64] = {0};
+      if (s.get_cpart(h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS && buf[0]) d.partition = buf;
+    }
+    if (s.get_mpart) {
+      char buf[64] = {0};
+      if (s.get_mpart(h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS && buf[0]) d.memory_partition = buf;
+    }
+    if (s.get_asic) {
+      amdsmi_asic_info_t a;
+      if (s.get_asic(h, &a) == AMDSMI_STATUS_SUCCESS) {
+        d.model = a.market_name;
+        if (a.num_of_compute_units != 0xFFFFFFFFu) d.cus = (int)a.num_of_compute_units;
+        if (a.target_graphics_version != 0xFFFFFFFFFFFFFFFFull) {
+          char gb[32];
+          snprintf(gb, sizeof(gb), "gfx%llx", (unsigned long long)a.target_graphics_version);
+          d.gfx = gb;
+        }
+      }
+    }
+    if (s.get_mem_total) {
+      uint64_t tot = 0;
+      if (s.get_mem_total(h, AMDSMI_MEM_TYPE_VRAM, &tot) == AMDSMI_STATUS_SUCCESS) d.vram = tot;
+    }
+    if (s.get_xgmi_status) {
+      amdsmi_xgmi_link_status_t ls;
+      if (s.get_xgmi_status(h, &ls) == AMDSMI_STATUS_SUCCESS) {
+        int up = 0;
+        for (uint32_t l = 0; l < ls.total_links && l < AMDSMI_MAX_NUM_XGMI_LINKS; ++l)
+          up += ls.status[l] == AMDSMI_XGMI_LINK_UP;
+        d.xgmi_links_up = up;
+      }
+    }
+  }
+  // Order by HIP id when available (so index == HIP ordinal with no HIP_VISIBLE_DEVICES)
+  std::vector<size_t> order(devs.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+    int ka = devs[a].hip_id >= 0 ? devs[a].hip_id : 1 << 20;
+    int kb = devs[b].hip_id >= 0 ? devs[b].hip_id : 1 << 20;
+    return ka < kb;
+  });
+  for (size_t i = 0; i < order.size(); ++i) {
+    r.devs.push_back(devs[order[i]]);
+    r.devs.back().index = (int)i;
+  }
+  init_mats(r);
+  const size_t n = r.devs.size();
+  for (size_t i = 0; i < n; ++i)
+    for (size_t j = 0; j < n; ++j) {
+      if (i == j) continue;
+      auto a = handles[order[i]], b = handles[order[j]];
+      uint64_t hops = 0;
+      amdsmi_link_type_t lt;
+      if (s.get_link_type(a, b, &hops, &lt) == AMDSMI_STATUS_SUCCESS) {
+        r.hops[i][j] = (int)hops;
+        switch (lt) {
+          case AMDSMI_LINK_TYPE_INTERNAL: r.link_type[i][j] = LT_INTERNAL; break;
+          case AMDSMI_LINK_TYPE_XGMI: r.link_type[i][j] = LT_XGMI; break;
+          case AMDSMI_LINK_TYPE_PCIE:
+            r.link_type[i][j] = (r.devs[i].numa != r.devs[j].numa) ? LT_PCIE_SYS : LT_PCIE;
+            break;
+          default: r.link_type[i][j] = LT_UNKNOWN;
+        }
+      } else {
+        r.warnings.push_back("link_type(" + std::to_string(i) + "," + std::to_string(j) + ") unavailable");
+      }
+      uint64_t w = 0;
+      if (s.get_weight && s.get_weight(a, b, &w) == AMDSMI_STATUS_SUCCESS) r.weight[i][j] = (double)w;
+      uint64_t mn = 0, mx = 0;
+      if (s.get_minmax && s.get_minmax(a, b, &mn, &mx) == AMDSMI_STATUS_SUCCESS) {
+        r.min_bw[i][j] = (double)mn;
+        r.max_bw[i][j] = (double)mx;
+      }
+      bool acc = false;
+      if (s.is_p2p && s.is_p2p(a, b, &acc) == AMDSMI_STATUS_SUCCESS) r.p2p[i][j] = acc ? 1 : 0;
+    }
+  assign_physical(r);
+  return r;
+}
+
+// ------------------------------------------------------------------------------------------------
+// KFD sysfs backend
+std::map<std::string, std::string> read_props(const std::string& path) {
+  std::map<std::string, std::string> m;
+  std::ifstream f(path);
+  std::string line;
+  while (std::getline(f, line)) {
+    std::istringstream ss(line);
+    std::string k, v;
+    if (ss >> k >> v) m[k] = v;
+  }
+  return m;
+}
+
+std::vector<std::string> list_dir(const std::string& path) {
+  std::vector<std::string> out;
+  DIR* d = opendir(path.c_str());
+  if (!d) return out;
+  while (auto* e = readdir(d)) {
+    std::string n = e->d_name;
+    if (n != "." && n != "..") out.push_back(n);
+  }
+  closedir(d);
+  std::sort(out.begin(), out.end(), [](const std::string& a, const std::string& b) {
+    bool na = !a.empty() && std::all_of(a.begin(), a.end(), ::isdigit);
+    bool nb = !b.empty() && std::all_of(b.begin(), b.end(), ::isdigit);
+    if (na && nb) return std::stoll(a) < std::stoll(b);
+    return a < b;
+  });
+  return out;
+}
+
+uint64_t as_u64(const std::map<std::string, std::string>& m, const std::string& k, uint64_t dflt = 0) {
+  auto it = m.find(k);
+  if (it == m.end()) return dflt;
+  try {
+    return std::stoull(it->second);
+  } catch (...) {
+    return dflt;
+  }
+}
+
+std::string read_first_line(const std::string& path) {
+  std::ifstream f(path);
+  std::string s;
+  std::getline(f, s);
+  return s;
+}
+
+struct KfdLink {
+  int from, to, type;
+  double weight, min_bw, max_bw;
+};
+
+Result discover_sysfs_impl(const std::string& root, const std::string& drm_root) {
+  Result r;
+  r.source = "sysfs";
+  const std::string nodes_dir = root + "/nodes";
+  auto nodes = list_dir(nodes_dir);
+  if (nodes.empty()) throw std::runtime_error("no KFD topology nodes under " + nodes_dir);
+  std::map<int, std::map<std::string, std::string>> props;
+  std::map<int, std::vector<KfdLink>> direct, indirect;
+  std::map<int, bool> is_cpu;
+  for (const auto& nd : nodes) {
+    int id = std::stoi(nd);
+    auto p = read_props(nodes_dir + "/" + nd + "/properties");
+    props[id] = p;
+    is_cpu[id] = as_u64(p, "simd_count") == 0;
+    for (const char* sub : {"io_links", "p2p_links"}) {
+      std::string ld = nodes_dir + "/" + nd + "/" + sub;
+      for (const auto& l : list_dir(ld)) {
+        auto lp = read_props(ld + "/" + l + "/properties");
+        KfdLink k{(int)as_u64(lp, "node_from", id), (int)as_u64(lp, "node_to", -1), (int)as_u64(lp, "type"),
+                  (double)as_u64(lp, "weight"), (double)as_u64(lp, "min_bandwidth"), (double)as_u64(lp, "max_bandwidth")};
+        (std::string(sub) == "io_links" ? direct : indirect)[id].push_back(k);
+      }
+    }
+  }
+  std::vector<int> gpu_nodes;
+  for (auto& kv : props)
+    if (!is_cpu[kv.first]) gpu_nodes.push_back(kv.first);
+  std::map<int, int> idx_of;
+  for (size_t i = 0; i < gpu_nodes.size(); ++i) {
+    int nid = gpu_nodes[i];
+    auto& p = props[nid];
+    Dev d;
+    d.index = (int)i;
+    d.kfd_node = nid;
+    d.hip_id = (int)i;
+    d.render_minor = (int)as_u64(p, "drm_render_minor", (uint64_t)-1);
+    uint64_t loc = as_u64(p, "location_id"), dom = as_u64(p, "domain");
+    d.bdf = fmt_bdf(dom, (loc >> 8) & 0xff, (loc >> 3) & 0x1f, loc & 0x7);
+    d.location = (dom << 16) | (loc & ~7ull);
+    uint64_t uid = as_u64(p, "unique_id");
+    if (uid) {
+      char b[40];
+      snprintf(b, sizeof(b), "GPU-%016llx", (unsigned long long)uid);
+      d.uuid = b;
+    }
+    uint64_t gtv = as_u64(p, "gfx_target_version");
+    if (gtv) {
+      char b[32];
+      snprintf(b, sizeof(b), "gfx%llu%llu%llx", (unsigned long long)(gtv / 10000), (unsigned long long)((gtv / 100) % 100),
+               (unsigned long long)(gtv % 100));
+      d.gfx = b;
+    }
+    d.cus = (int)(as_u64(p, "simd_count") / std::max<uint64_t>(1, as_u64(p, "simd_per_cu", 4)));
+    d.vram = as_u64(p, "local_mem_size");
+    d.model = d.gfx == "gfx950" ? "MI355X" : "";
+    // NUMA: the CPU node this GPU's PCIe io_link lands on
+    for (const auto& l : direct[nid])
+      if (is_cpu.count(l.to) && is_cpu[l.to]) {
+        d.numa = l.to;
+        break;
+      }
+    int up = 0;
+    for (const auto& l : direct[nid]) up += (l.type == 11);
+    d.xgmi_links_up = up;
+    if (!drm_root.empty() && d.render_minor >= 0) {
+      std::string dev = drm_root + "/renderD" + std::to_string(d.render_minor) + "/device/";
+      std::string cp = read_first_line(dev + "current_compute_partition");
+      std::string mp = read_first_line(dev + "current_memory_partition");
+      if (!cp.empty()) d.partition = cp;
+      if (!mp.empty()) d.memory_partition = mp;
+      // the card minor: first cardN directory under the device's drm/
+      for (const auto& c : list_dir(dev + "drm"))
+        if (c.rfind("card", 0) == 0) {
+          d.card = std::stoi(c.substr(4));
+          break;
+        }
+    }
+    idx_of[nid] = (int)i;
+    r.devs.push_back(d);
+  }
+  init_mats(r);
+  const size_t n = r.devs.size();
+  for (size_t i = 0; i < n; ++i) {
+    int nid = gpu_nodes[i];
+    for (size_t j = 0; j < n; ++j) {
+      if (i == j) continue;
+      int to = gpu_nodes[j];
+      const KfdLink* best = nullptr;
+      bool is_direct = false;
+      for (const auto& l : direct[nid])
+        if (l.to == to) {
+          best = &l;
+          is_direct = true;
+        }
+      if (!best)
+        for (const auto& l : indirect[nid])
+          if (l.to == to) best = &l;
+      if (best) {
+        r.weight[i][j] = best->weight;
+        r.min_bw[i][j] = best->min_bw;
+        r.max_bw[i][j] = best->max_bw;
+        r.p2p[i][j] = 1;
+        if (best->type == 11) {
+          r.link_type[i][j] = LT_XGMI;
+          r.hops[i][j] = is_direct ? 1 : 2;
+        } else {
+          bool cross = r.devs[i].numa != r.devs[j].numa;
+          r.link_type[i][j] = cross ? LT_PCIE_SYS : LT_PCIE;
+          r.hops[i][j] = cross ? 3 : 2;
+        }
+      } else {
+        bool cross = r.devs[i].numa != r.devs[j].numa;
+        r.link_type[i][j] = cross ? LT_PCIE_SYS : LT_PCIE;
+        r.hops[i][j] = cross ? 3 : 2;
+        r.warnings.push_back("no KFD link " + std::to_string(nid) + "->" + std::to_string(to) + ", assuming PCIe");
+      }
+    }
+  }
+  assign_physical(r);
+  return r;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_topo, m) {
+  m.doc() = "MI355X topology discovery: amdsmi (dlopen) and KFD sysfs backends";
+  m.def(
+      "discover_amdsmi",
+      [](const std::string& lib) {
+        Result r;
+        {
+          py::gil_scoped_release nogil;
+          r = discover_amdsmi_impl(lib);
+        }
+        return to_py(r);
+      },
+      py::arg("lib") = "libamd_smi.so");
+  m.def(
+      "discover_sysfs",
+      [](const std::string& root, const std::string& drm_root) {
+        Result r;
+        {
+          py::gil_scoped_release nogil;
+          r = discover_sysfs_impl(root, drm_root);
+        }
+        return to_py(r);
+      },
+      py::arg("root") = "/sys/class/kfd/kfd/topology", py::arg("drm_root") = "/sys/class/drm");
+  m.attr("HSA_IOLINK_TYPE_XGMI") = 11;
+  m.attr("HSA_IOLINK_TYPE_PCIEXPRESS") = 2;
+}

@@ -1,0 +1,162 @@
+"""Build every native component in-tree (no JIT cache, no pip install).
+
+    python -m gpu_topology_on_k8s_amd._native.build [--force] [--only _probe,_rccl] [-j 8]
+
+Targets (all land in ``gpu_topology_on_k8s_amd/_native/``):
+  _topo       C++  (g++)    amdsmi (dlopen) + KFD sysfs topology reader
+  _placement  C++  (g++)    branch-and-bound placement engine
+  _probe      HIP  (hipcc)  gfx950 link/HBM probe kernels + MFMA warm-up
+  _rccl       HIP  (hipcc)  RCCL all-reduce validator (librccl)
+  _fused      HIP  (hipcc)  PyTorch custom ops for the Llama-3 workload (torch headers)
+  bin/rccl_allreduce_bench  standalone validator binary
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shlex
+import subprocess
+import sys
+import sysconfig
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import List, Optional
+
+HERE = Path(__file__).resolve().parent
+REPO = HERE.parent.parent
+CSRC = REPO / "csrc"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+ARCH = os.environ.get("GTK_OFFLOAD_ARCH", "gfx950")
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def _py_includes() -> List[str]:
+    import pybind11
+
+    return [f"-I{sysconfig.get_paths()['include']}", f"-I{pybind11.get_include()}"]
+
+
+def _torch_flags() -> List[str]:
+    import torch
+    from torch.utils import cpp_extension as ce
+
+    inc = [f"-I{p}" for p in ce.include_paths()]
+    libdir = str(Path(torch.__file__).parent / "lib")
+    return inc + [
+        "-D__HIP_PLATFORM_AMD__=1",
+        "-DUSE_ROCM=1",
+        "-DTORCH_EXTENSION_NAME=_fused",
+        f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}",
+        f"-L{libdir}",
+        "-lc10",
+        "-ltorch",
+        "-ltorch_cpu",
+        "-ltorch_python",
+        "-lc10_hip",
+        "-ltorch_hip",
+        f"-Wl,-rpath,{libdir}",
+    ]
+
+
+@dataclass
+class Target:
+    name: str
+    sources: List[Path]
+    compiler: str  # "gxx" | "hipcc"
+    out: Path
+    extra: List[str] = field(default_factory=list)
+    deps: List[Path] = field(default_factory=list)
+    pybind: bool = True
+    torch: bool = False
+    shared: bool = True
+
+    def command(self) -> List[str]:
+        if self.compiler == "hipcc":
+            cmd = [str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-O3", "-std=c++17"]
+        else:
+            cmd = ["g++", "-O3", "-std=c++17", "-Wall", "-Wno-unused-function"]
+        if self.shared:
+            cmd += ["-shared", "-fPIC", "-fvisibility=hidden"]
+        cmd += [f"-I{ROCM / 'include'}", f"-I{CSRC}"]
+        if self.pybind:
+            cmd += _py_includes()
+        cmd += [str(s) for s in self.sources]
+        if self.torch:
+            cmd += _torch_flags()
+        cmd += self.extra
+        cmd += ["-o", str(self.out)]
+        return cmd
+
+    def up_to_date(self) -> bool:
+        if not self.out.exists():
+            return False
+        t = self.out.stat().st_mtime
+        inputs = list(self.sources) + list(self.deps) + [Path(__file__)]
+        return all(p.stat().st_mtime <= t for p in inputs if p.exists())
+
+
+def targets() -> List[Target]:
+    rocm_lib = str(ROCM / "lib")
+    return [
+        Target("_topo", [CSRC / "topo" / "topo_reader.cpp"], "gxx", HERE / f"_topo{EXT}", ["-ldl"]),
+        Target("_placement", [CSRC / "placement" / "engine.cpp"], "gxx", HERE / f"_placement{EXT}",
+               deps=[CSRC / "placement" / "engine.h"]),
+        Target("_probe", [CSRC / "probe" / "probe.hip"], "hipcc", HERE / f"_probe{EXT}"),
+        Target("_rccl", [CSRC / "rccl" / "rccl_module.hip"], "hipcc", HERE / f"_rccl{EXT}",
+               [f"-L{rocm_lib}", "-lrccl", f"-Wl,-rpath,{rocm_lib}"], deps=[CSRC / "rccl" / "rccl_core.h"]),
+        Target("rccl_allreduce_bench", [CSRC / "rccl" / "rccl_allreduce_bench.hip"], "hipcc",
+               HERE / "bin" / "rccl_allreduce_bench", [f"-L{rocm_lib}", "-lrccl", f"-Wl,-rpath,{rocm_lib}"],
+               deps=[CSRC / "rccl" / "rccl_core.h"], pybind=False, shared=False),
+        Target("_fused", sorted((CSRC / "ops").glob("*.hip")), "hipcc", HERE / f"_fused{EXT}",
+               deps=sorted((CSRC / "ops").glob("*.h")), pybind=True, torch=True),
+    ]
+
+
+def build_one(t: Target, force: bool = False, verbose: bool = False) -> str:
+    missing = [s for s in t.sources if not s.exists()]
+    if not t.sources or missing:
+        return f"skip {t.name} (no sources)"
+    if not force and t.up_to_date():
+        return f"ok   {t.name} (up to date)"
+    t.out.parent.mkdir(parents=True, exist_ok=True)
+    cmd = t.command()
+    if verbose:
+        print(" ".join(shlex.quote(c) for c in cmd), flush=True)
+    p = subprocess.run(cmd, capture_output=True, text=True)
+    if p.returncode != 0:
+        raise RuntimeError(f"build of {t.name} failed ({p.returncode}):\n{' '.join(cmd)}\n{p.stdout}\n{p.stderr}")
+    return f"built {t.name} -> {t.out.relative_to(REPO)}"
+
+
+def build(force: bool = False, only: Optional[List[str]] = None, jobs: int = 4, verbose: bool = False) -> List[str]:
+    ts = [t for t in targets() if not only or t.name in only]
+    msgs: List[str] = []
+    errors: List[str] = []
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        futs = {ex.submit(build_one, t, force, verbose): t for t in ts}
+        for f in cf.as_completed(futs):
+            try:
+                msgs.append(f.result())
+            except Exception as e:  # noqa: BLE001 - report all failures together
+                errors.append(str(e))
+    if errors:
+        raise RuntimeError("\n\n".join(errors))
+    return sorted(msgs)
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--only", default="")
+    ap.add_argument("-j", "--jobs", type=int, default=4)
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    only = [s for s in a.only.split(",") if s] or None
+    for m in build(a.force, only, a.jobs, a.verbose):
+        print(m)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,94 @@
+"""Python front-end of the HIP/CDNA4 link probe (``csrc/probe/probe.hip``).
+
+Seeds the link-cost matrix at node start (BASELINE.json north_star):
+
+    mfma_warmup (K4)  ->  p2p read (K1) for every ordered pair  ->  GB/s matrix  ->  cost matrix
+
+With one visible GPU only the diagonal (K3 HBM self-copy) is measurable; off-diagonal entries are
+left unmeasured (nan) and the cost model falls back to the discovered link class.
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from .._native import load
+from ..topology.model import Topology
+
+__all__ = ["device_count", "device_props", "warmup", "copy_bw", "measure_matrix", "probe_topology", "PROBE_PRESETS"]
+
+#: bytes per transfer / timed iterations; sizes exceed the 256 MiB Infinity Cache for "full".
+PROBE_PRESETS: Dict[str, Dict[str, int]] = {
+    "quick": {"bytes": 64 << 20, "iters": 3, "warmup": 1},
+    "full": {"bytes": 512 << 20, "iters": 10, "warmup": 2},
+}
+
+
+def _p():
+    return load("_probe")
+
+
+def device_count() -> int:
+    return int(_p().device_count())
+
+
+def device_props(dev: int) -> Dict[str, object]:
+    return dict(_p().device_props(dev))
+
+
+def warmup(dev: int, ms: float = 50.0) -> Dict[str, object]:
+    """K4: run MFMA until ``ms`` elapsed so the measured copies see lifted clocks."""
+    return dict(_p().mfma_warmup(dev, float(ms)))
+
+
+def copy_bw(src: int, dst: int, nbytes: int = 256 << 20, iters: int = 10, warmup_iters: int = 2, mode: str = "read",
+            kind: str = "lds", nontemporal: bool = False, blocks_per_cu: int = 8) -> Dict[str, object]:
+    exec_dev = dst if mode == "read" else src
+    return dict(_p().copy_bw(src, dst, exec_dev, int(nbytes), int(iters), int(warmup_iters), kind, bool(nontemporal), int(blocks_per_cu)))
+
+
+def measure_matrix(devs: Sequence[int], nbytes: int = 64 << 20, iters: int = 3, warmup_iters: int = 1, mode: str = "read",
+                   kind: str = "lds") -> np.ndarray:
+    return np.array(_p().probe_matrix(list(devs), int(nbytes), int(iters), int(warmup_iters), mode, kind), dtype=np.float64)
+
+
+def probe_topology(topo: Topology, preset: str = "quick", devs: Optional[List[int]] = None, mode: str = "read",
+                   kind: str = "lds", warm_ms: float = 50.0) -> Topology:
+    """Measure every visible pair and fold it into ``topo`` (in place; also returned)."""
+    cfg = PROBE_PRESETS[preset]
+    ndev = device_count()
+    if ndev == 0:
+        raise RuntimeError("no HIP devices visible: cannot probe")
+    devs = list(range(min(ndev, topo.n))) if devs is None else list(devs)
+    t0 = time.time()
+    w = warmup(devs[0], warm_ms)
+    bw = np.full((topo.n, topo.n), np.nan)
+    hbm = np.full(topo.n, np.nan)
+    for i in devs:
+        for j in devs:
+            if i != j and not bool(_p().can_access_peer(j if mode == "read" else i, i if mode == "read" else j)):
+                continue
+            r = copy_bw(i, j, cfg["bytes"], cfg["iters"], cfg["warmup"], mode=mode, kind=kind)
+            if not r["ok"]:
+                raise RuntimeError(f"probe verification failed for {i}->{j}")
+            if i == j:
+                hbm[i] = r["gbps"]
+            else:
+                bw[i, j] = r["gbps"]
+    topo.hbm_gbps = hbm
+    topo.set_measured_bw(
+        bw,
+        {
+            "method": f"p2p_{mode}_{kind}",
+            "preset": preset,
+            "bytes": cfg["bytes"],
+            "iters": cfg["iters"],
+            "devices": devs,
+            "mfma_warmup_tflops": round(float(w["tflops"]), 1),
+            "ts": int(time.time()),
+            "seconds": round(time.time() - t0, 3),
+        },
+    )
+    return topo

@@ -1,0 +1,175 @@
+"""RCCL all-reduce over xGMI on a scheduler-chosen device subset (one process per GPU).
+
+This is the placement validator of SURVEY.md §3.5 in its multi-process form, and the engine of the
+repo-root ``bench.py`` (BASELINE.json metric: "RCCL all-reduce bus GB/s on scheduler-chosen k-GPU
+subset").  Flow per job:
+
+1. ``torch.distributed`` (backend ``nccl`` = RCCL) provides the rendezvous store, barriers and the
+   max-over-ranks timing reduction.
+2. Rank 0 discovers the node topology (amdsmi, native) and runs the placement core to pick the
+   k-GPU subset; the choice travels to the other ranks through the store.  Every rank binds to
+   ``subset[rank]`` — this is what a pod sees after ``Allocate`` mounted its GROUP.
+3. The measured collective is a native RCCL communicator (``_rccl.Comm``, ncclCommInitRank with a
+   unique id shipped through the same store) issuing out-of-place ``ncclAllReduce`` (nccl-tests
+   semantics: algBW = bytes/t, busBW = algBW * 2(k-1)/k).  ``backend="torch"`` uses
+   ``dist.all_reduce`` instead, for cross-checking.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+log = logging.getLogger(__name__)
+
+__all__ = ["DistEnv", "choose_subset", "AllReduceRunner", "bus_factor"]
+
+
+def bus_factor(k: int) -> float:
+    return 2.0 * (k - 1) / k if k > 1 else 0.0
+
+
+@dataclass
+class DistEnv:
+    rank: int
+    world: int
+    local_rank: int
+    store: object = None
+
+    @classmethod
+    def from_env(cls) -> "DistEnv":
+        return cls(int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("LOCAL_RANK", "0")))
+
+
+@dataclass
+class SubsetChoice:
+    devices: List[int]
+    score: float
+    objective: float
+    source: str
+    worst: Optional[List[int]] = None
+    worst_score: Optional[float] = None
+    placement_ms: float = 0.0
+    probed: bool = False
+    extra: Dict[str, object] = field(default_factory=dict)
+
+    def to_json(self) -> str:
+        return json.dumps(self.__dict__)
+
+    @classmethod
+    def from_json(cls, s: str) -> "SubsetChoice":
+        return cls(**json.loads(s))
+
+
+def _visible_device_count() -> int:
+    import torch
+
+    return int(torch.cuda.device_count())
+
+
+def choose_subset(k: int, probe: Optional[str] = None, backend: str = "auto") -> SubsetChoice:
+    """Rank-0 side: discover the node, optionally probe links, run the placement core."""
+    from ..placement import PlacementPolicy, select, worst
+    from ..topology.discovery import DiscoveryError, discover, fake_topology
+
+    nvis = _visible_device_count()
+    t0 = time.perf_counter()
+    try:
+        topo = discover(backend)
+        source = topo.source
+        if topo.n != nvis:
+            log.warning("topology has %d devices but %d are visible to HIP; using a full-mesh model of the visible set", topo.n, nvis)
+            topo = fake_topology(nvis)
+            source = f"{source}->visible-mesh"
+    except DiscoveryError as e:
+        log.warning("topology discovery failed (%s); using a full-mesh model of %d visible devices", e, nvis)
+        topo = fake_topology(nvis)
+        source = "fallback-mesh"
+    probed = False
+    if probe:
+        from ..ops.probe import probe_topology
+
+        probe_topology(topo, preset=probe)
+        probed = True
+    t1 = time.perf_counter()
+    pl = select(topo, k, policy=PlacementPolicy())
+    ms = (time.perf_counter() - t1) * 1e3
+    w = worst(topo, k) if k < topo.n else None
+    return SubsetChoice(
+        devices=list(pl.ids),
+        score=round(pl.score, 4),
+        objective=round(pl.objective, 6),
+        source=source,
+        worst=list(w.ids) if w else None,
+        worst_score=round(w.score, 4) if w else None,
+        placement_ms=round(ms, 4),
+        probed=probed,
+        extra={"discovery_ms": round((t1 - t0) * 1e3, 2), "node_devices": topo.n},
+    )
+
+
+class AllReduceRunner:
+    """One rank's side of the measured all-reduce (native RCCL comm or torch.distributed)."""
+
+    def __init__(self, env: DistEnv, device: int, nbytes: int, dtype: str = "bf16", backend: str = "native", inplace: bool = False):
+        import torch
+
+        self.env, self.device, self.dtype, self.inplace = env, device, dtype, inplace
+        self.backend = backend
+        self.comm = None
+        self.tensor = None
+        if backend == "native":
+            from .._native import load
+
+            rccl = load("_rccl")
+            key = "gtk/rccl_uid"
+            if env.rank == 0:
+                uid = rccl.unique_id()
+                env.store.set(key, uid)
+            else:
+                uid = env.store.get(key)
+            self.comm = rccl.Comm(bytes(uid), env.world, env.rank, device)
+            self.comm.prepare(int(nbytes), dtype)
+            self.nbytes = int(self.comm.bytes)
+        elif backend == "torch":
+            tdt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[dtype]
+            esz = torch.empty((), dtype=tdt).element_size()
+            self.tensor = torch.ones(max(1, int(nbytes) // esz), dtype=tdt, device=f"cuda:{device}")
+            self.nbytes = self.tensor.numel() * esz
+        else:
+            raise ValueError(backend)
+
+    def check(self) -> int:
+        """Exact correctness check of one all-reduce; returns wrong elements on this rank."""
+        if self.comm is not None:
+            return int(self.comm.check(self.inplace))
+        import torch
+        import torch.distributed as dist
+
+        x = torch.full((4096,), float(self.env.rank + 1), dtype=self.tensor.dtype, device=self.tensor.device)
+        dist.all_reduce(x)
+        want = self.env.world * (self.env.world + 1) / 2
+        return int((x.float() != want).sum().item())
+
+    def step(self) -> None:
+        if self.comm is not None:
+            self.comm.step(self.inplace)
+        else:
+            import torch.distributed as dist
+
+            dist.all_reduce(self.tensor)
+
+    def synchronize(self) -> None:
+        if self.comm is not None:
+            self.comm.synchronize()
+        import torch
+
+        torch.cuda.synchronize(self.device)
+
+    def close(self) -> None:
+        if self.comm is not None:
+            self.comm.destroy()
+            self.comm = None

@@ -1,0 +1,253 @@
+"""Exact, topology-aware GPU-subset selection and the 0..10 affinity score.
+
+Reference behaviour:
+  * ``design.md:131-190`` — subset selection: req==1 picks one free GPU; req>=2 seeds with the
+    closest free pair and grows it Prim-style.  ``design.md:188-190`` documents that a tie on the
+    seed pair can lock in a worse set.  This module replaces the greedy with an *exact* search over
+    all C(n,k) free subsets (n<=8 on an MI355X node: at most 70 subsets), so the tie flaw cannot
+    occur.  The greedy is kept in :mod:`.legacy` for parity tests.
+  * ``design.md:192-217`` — score in 0..10.  The reference formula is inverted w.r.t. its own mark
+    table; here the score is ``10 / max(1, J)`` of a *cost* objective ``J`` where
+    lower is better, so a set of nominal xGMI links with no fragmentation penalty scores 10 and the
+    score falls monotonically as cost rises.  The literal formula lives in :mod:`.legacy`.
+  * Gaia Singular (paper p.5 Alg. 3, ``gaia.md:38-52``): a 1-GPU request prefers a GPU whose
+    sibling is already used.  Generalised here as an anti-fragmentation term: allocating into a
+    group (NUMA domain; physical GPU when partitioned) that is still *pristine* costs ``w_frag``.
+
+The objective for a candidate set S (|S| = k) is::
+
+    J(S) = comm(S) + w_span * span(S) + w_frag * frag(S) + w_fit * fit(S) + w_access * acc(S)
+
+    comm  = mean pairwise link cost (1.0 = one nominal xGMI link; 1.0 for k == 1)
+    span  = sum over levels of (#groups touched - #groups minimally needed to host k free devices)
+    frag  = sum over levels of #pristine groups left partially used
+    fit   = sum over levels and touched groups of free_after/size  (best-fit packing)
+    acc   = mean per-device access cost (CPU/NUMA affinity hint, design.md:144-145, Gaia B6)
+
+The C++ engine (``csrc/placement/engine.cpp``) implements the same objective with branch-and-bound;
+``tests/test_placement_native.py`` checks both agree.
+"""
+from __future__ import annotations
+
+import itertools
+import math
+import random
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..topology.model import Topology
+
+__all__ = ["PlacementPolicy", "Placement", "Problem", "select", "evaluate", "score_from_objective", "NoFeasiblePlacement"]
+
+EPS = 1e-9
+
+
+class NoFeasiblePlacement(RuntimeError):
+    pass
+
+
+@dataclass(frozen=True)
+class PlacementPolicy:
+    w_span: float = 0.5
+    w_frag: float = 0.25
+    w_fit: float = 0.05
+    w_access: float = 0.1
+    tie_break: str = "first"  # "first" (deterministic, lowest ids) | "random"
+    exact_limit: int = 200_000  # max subsets enumerated exactly; above -> greedy + local search
+
+    def to_dict(self) -> Dict[str, object]:
+        return dict(
+            w_span=self.w_span, w_frag=self.w_frag, w_fit=self.w_fit, w_access=self.w_access,
+            tie_break=self.tie_break, exact_limit=self.exact_limit,
+        )
+
+
+@dataclass
+class Placement:
+    ids: Tuple[int, ...]
+    objective: float
+    score: float  # 0..10, higher is better
+    comm: float
+    terms: Dict[str, float] = field(default_factory=dict)
+    exact: bool = True
+
+    @property
+    def k8s_score(self) -> int:
+        """Integer score for ``HostPriority.score`` (0..MaxExtenderPriority=10)."""
+        return int(max(0, min(10, round(self.score))))
+
+
+@dataclass
+class Problem:
+    """Everything the objective needs, in flat arrays (mirrors the C++ engine's input)."""
+
+    cost: np.ndarray  # n x n
+    free: np.ndarray  # bool[n]
+    levels: List[np.ndarray]  # group id per device, innermost level first
+    access: np.ndarray  # float[n]
+
+    @classmethod
+    def from_topology(cls, topo: Topology, used: Sequence[int] = (), access: Optional[Sequence[float]] = None) -> "Problem":
+        n = topo.n
+        free = topo.healthy_mask().copy()
+        for u in used:
+            if 0 <= int(u) < n:
+                free[int(u)] = False
+        levels = []
+        phys = topo.physical
+        if len(set(phys.tolist())) < n:  # partitioned: XCP -> physical GPU level is meaningful
+            levels.append(phys)
+        levels.append(topo.numa)
+        acc = np.zeros(n) if access is None else np.asarray(access, dtype=np.float64)
+        return cls(cost=np.asarray(topo.cost, dtype=np.float64), free=free, levels=levels, access=acc)
+
+    @property
+    def n(self) -> int:
+        return len(self.free)
+
+
+def score_from_objective(j: float) -> float:
+    return 10.0 / max(1.0, j)
+
+
+def _level_stats(p: Problem):
+    """Per level: (group ids array, {g: size}, {g: free_count})."""
+    out = []
+    for lv in p.levels:
+        size: Dict[int, int] = {}
+        fre: Dict[int, int] = {}
+        for i, g in enumerate(lv.tolist()):
+            size[g] = size.get(g, 0) + 1
+            fre[g] = fre.get(g, 0) + (1 if p.free[i] else 0)
+        out.append((lv, size, fre))
+    return out
+
+
+def _min_groups(free_counts: Sequence[int], k: int) -> int:
+    s = 0
+    for i, c in enumerate(sorted(free_counts, reverse=True)):
+        s += c
+        if s >= k:
+            return i + 1
+    return len(free_counts)
+
+
+def evaluate(p: Problem, ids: Sequence[int], policy: PlacementPolicy = PlacementPolicy(), _stats=None) -> Tuple[float, Dict[str, float]]:
+    ids = list(ids)
+    k = len(ids)
+    if k >= 2:
+        sub = p.cost[np.ix_(ids, ids)]
+        comm = float(sub.sum() / (k * (k - 1)))
+    else:
+        comm = 1.0
+    stats = _stats if _stats is not None else _level_stats(p)
+    span = frag = fit = 0.0
+    for lv, size, fre in stats:
+        take: Dict[int, int] = {}
+        for i in ids:
+            g = int(lv[i])
+            take[g] = take.get(g, 0) + 1
+        span += len(take) - _min_groups(list(fre.values()), k)
+        for g, t in take.items():
+            after = fre[g] - t
+            if fre[g] == size[g] and after > 0:
+                frag += 1
+            fit += after / size[g]
+    acc = float(np.mean(p.access[ids])) if k else 0.0
+    j = comm + policy.w_span * span + policy.w_frag * frag + policy.w_fit * fit + policy.w_access * acc
+    return j, {"comm": comm, "span": span, "frag": frag, "fit": fit, "access": acc}
+
+
+def _greedy_local(p: Problem, k: int, policy: PlacementPolicy, stats) -> Tuple[List[int], float]:
+    """Heuristic for very large n (CPX: 64 XCPs): greedy growth from every seed + 1-swap descent."""
+    free_ids = [i for i in range(p.n) if p.free[i]]
+    best: Optional[List[int]] = None
+    best_j = math.inf
+    for seed in free_ids:
+        cur = [seed]
+        while len(cur) < k:
+            cand = None
+            cj = math.inf
+            for c in free_ids:
+                if c in cur:
+                    continue
+                j, _ = evaluate(p, cur + [c], policy, stats)
+                if j < cj - EPS:
+                    cj, cand = j, c
+            cur.append(cand)
+        cur_j, _ = evaluate(p, cur, policy, stats)
+        improved = True
+        while improved:
+            improved = False
+            outside = [c for c in free_ids if c not in cur]
+            for a_pos in range(len(cur)):
+                for b in outside:
+                    trial = cur.copy()
+                    trial[a_pos] = b
+                    tj, _ = evaluate(p, trial, policy, stats)
+                    if tj < cur_j - EPS:
+                        cur, cur_j, improved = trial, tj, True
+                        break
+                if improved:
+                    break
+        if cur_j < best_j - EPS or (abs(cur_j - best_j) <= EPS and sorted(cur) < sorted(best)):
+            best, best_j = sorted(cur), cur_j
+    assert best is not None
+    return best, best_j
+
+
+def select(
+    topo_or_problem,
+    k: int,
+    used: Sequence[int] = (),
+    policy: PlacementPolicy = PlacementPolicy(),
+    access: Optional[Sequence[float]] = None,
+    rng: Optional[random.Random] = None,
+) -> Placement:
+    """Choose ``k`` free devices minimising :func:`evaluate`'s objective."""
+    p = topo_or_problem if isinstance(topo_or_problem, Problem) else Problem.from_topology(topo_or_problem, used, access)
+    if k <= 0:
+        raise ValueError("k must be >= 1")
+    free_ids = [i for i in range(p.n) if p.free[i]]
+    if len(free_ids) < k:
+        raise NoFeasiblePlacement(f"need {k} free devices, have {len(free_ids)}")
+    stats = _level_stats(p)
+    n_subsets = math.comb(len(free_ids), k)
+    if n_subsets <= policy.exact_limit:
+        best_j = math.inf
+        ties: List[Tuple[int, ...]] = []
+        for comb in itertools.combinations(free_ids, k):
+            j, _ = evaluate(p, comb, policy, stats)
+            if j < best_j - EPS:
+                best_j, ties = j, [comb]
+            elif j <= best_j + EPS:
+                ties.append(comb)
+        if policy.tie_break == "random" and len(ties) > 1:
+            choice = (rng or random).choice(ties)
+        else:
+            choice = ties[0]
+        exact = True
+    else:
+        lst, best_j = _greedy_local(p, k, policy, stats)
+        choice = tuple(lst)
+        exact = False
+    j, terms = evaluate(p, choice, policy, stats)
+    return Placement(ids=tuple(int(c) for c in choice), objective=j, score=score_from_objective(j), comm=terms["comm"], terms=terms, exact=exact)
+
+
+def worst(topo: Topology, k: int, used: Sequence[int] = (), policy: PlacementPolicy = PlacementPolicy()) -> Placement:
+    """Highest-objective subset (the "worst-topology placement" of BASELINE config 5)."""
+    p = Problem.from_topology(topo, used)
+    stats = _level_stats(p)
+    free_ids = [i for i in range(p.n) if p.free[i]]
+    if len(free_ids) < k:
+        raise NoFeasiblePlacement(f"need {k} free devices, have {len(free_ids)}")
+    bj, bc = -math.inf, None
+    for comb in itertools.combinations(free_ids, k):
+        j, _ = evaluate(p, comb, policy, stats)
+        if j > bj + EPS:
+            bj, bc = j, comb
+    j, terms = evaluate(p, bc, policy, stats)
+    return Placement(ids=tuple(bc), objective=j, score=score_from_objective(j), comm=terms["comm"], terms=terms)

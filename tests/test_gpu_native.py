@@ -1,0 +1,124 @@
+"""GPU tests of the native layer (run on a real MI355X via gpurun: ``pytest -m gpu``)."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def probe_mod():
+    from gpu_topology_on_k8s_amd._native import load
+
+    p = load("_probe")
+    assert p.device_count() >= 1, "no HIP device visible"
+    return p
+
+
+def test_device_is_gfx950(probe_mod):
+    props = probe_mod.device_props(0)
+    assert props["gcn_arch"].startswith("gfx950"), props
+    assert props["warp_size"] == 64
+    assert props["cus"] >= 256
+
+
+def test_mfma_warmup_rate(probe_mod):
+    from gpu_topology_on_k8s_amd.ops.probe import warmup
+
+    r = warmup(0, 30.0)
+    # dense bf16 peak ~2.5 PF; a 4-accumulator issue loop must at least clear 25% of it
+    assert r["tflops"] > 600, r
+
+
+@pytest.mark.parametrize("kind", ["lds", "reg", "sdma"])
+def test_hbm_copy_kernels(probe_mod, kind):
+    from gpu_topology_on_k8s_amd.ops.probe import copy_bw
+
+    r = copy_bw(0, 0, 512 << 20, iters=5, warmup_iters=1, kind=kind)
+    assert r["ok"], r
+    assert r["gbps"] > 1000, r  # 2x traffic: >2 TB/s of HBM
+
+
+def test_copy_odd_size_tail(probe_mod):
+    from gpu_topology_on_k8s_amd.ops.probe import copy_bw
+
+    r = copy_bw(0, 0, (3 << 20) + 16 * 37, iters=1, warmup_iters=0, kind="lds")
+    assert r["ok"], r
+
+
+def test_discover_real_node():
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
+
+    t = discover("auto")
+    assert t.n >= 1
+    assert all(g.gfx.startswith("gfx95") for g in t.gpus), [g.gfx for g in t.gpus]
+    assert all(g.render_minor >= 128 for g in t.gpus)
+    print(t.render())
+    print(json.dumps(t.to_dict()["gpus"][0]))
+
+
+def test_sysfs_backend_on_real_node():
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
+
+    if not os.path.isdir("/sys/class/kfd/kfd/topology/nodes"):
+        pytest.skip("no KFD sysfs in this container")
+    t = discover("sysfs")
+    assert t.n >= 1
+    assert t.gpus[0].gfx == "gfx950"
+
+
+def test_probe_topology_single_gpu():
+    from gpu_topology_on_k8s_amd.ops.probe import probe_topology
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
+
+    t = discover("auto")
+    probe_topology(t, preset="quick")
+    assert np.isfinite(t.hbm_gbps[0]) and t.hbm_gbps[0] > 500
+    assert t.probe["method"] == "p2p_read_lds"
+
+
+def test_rccl_single_rank_allreduce_exact():
+    from gpu_topology_on_k8s_amd._native import load
+
+    rccl = load("_rccl")
+    for dt in ("bf16", "fp32"):
+        pts = rccl.local_sweep([0], [4096, 1 << 20, 64 << 20], dt, 3, 1, False, True)
+        assert all(p["wrong"] == 0 for p in pts), pts
+        assert all(p["busbw_gbps"] == 0.0 for p in pts)
+
+
+def test_rccl_comm_api_single_rank():
+    from gpu_topology_on_k8s_amd._native import load
+
+    rccl = load("_rccl")
+    c = rccl.Comm(rccl.unique_id(), 1, 0, 0)
+    c.prepare(8 << 20, "bf16")
+    assert c.check(False) == 0
+    c.step(False)
+    c.synchronize()
+    c.destroy()
+
+
+def test_rccl_cli_binary():
+    from gpu_topology_on_k8s_amd._native import binary
+
+    p = subprocess.run([str(binary("rccl_allreduce_bench")), "--devices", "0", "--min", "1K", "--max", "16M", "--factor", "16", "--json"],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    lines = [json.loads(l) for l in p.stdout.strip().splitlines() if l.startswith("{")]  # RCCL prints a banner
+    assert lines[-1]["summary"] and lines[-1]["wrong"] == 0
+
+
+def test_bench_py_single_gpu():
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "5", "--warmup", "2", "--size-mb", "64"],
+                       capture_output=True, text=True, timeout=600, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-4000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == 1 and out["value"] > 0 and out["config"]["subset"] == [0]
