@@ -1,0 +1,317 @@
+// Branch-and-bound placement engine (see engine.h for the objective and the reference mapping).
+#include "placement/engine.h"
+
+#include <algorithm>
+#include <cmath>
+#include <functional>
+#include <limits>
+#include <map>
+#include <numeric>
+#include <stdexcept>
+
+namespace gtk {
+
+Engine::Engine(const Problem& p, const Policy& pol) : p_(p), pol_(pol) {
+  if (p_.n < 0) throw std::invalid_argument("n < 0");
+  const size_t n = (size_t)p_.n;
+  if (p_.cost.size() != n * n) throw std::invalid_argument("cost must be n*n");
+  if (p_.free.size() != n) throw std::invalid_argument("free must have n entries");
+  if (p_.access.empty()) p_.access.assign(n, 0.0);
+  if (p_.access.size() != n) throw std::invalid_argument("access must have n entries");
+  for (const auto& raw : p_.levels) {
+    if (raw.size() != n) throw std::invalid_argument("every level needs n group ids");
+    Level lv;
+    std::map<int, int> dense;
+    lv.gid.resize(n);
+    for (size_t i = 0; i < n; ++i) {
+      auto it = dense.find(raw[i]);
+      if (it == dense.end()) it = dense.emplace(raw[i], (int)dense.size()).first;
+      lv.gid[i] = it->second;
+    }
+    lv.size.assign(dense.size(), 0);
+    lv.free.assign(dense.size(), 0);
+    for (size_t i = 0; i < n; ++i) {
+      lv.size[lv.gid[i]] += 1;
+      lv.free[lv.gid[i]] += p_.free[i] ? 1 : 0;
+    }
+    lv_.push_back(std::move(lv));
+  }
+}
+
+int Engine::min_groups(const Level& lv, int k) const {
+  std::vector<int> f = lv.free;
+  std::sort(f.begin(), f.end(), std::greater<int>());
+  int s = 0;
+  for (size_t i = 0; i < f.size(); ++i) {
+    s += f[i];
+    if (s >= k) return (int)i + 1;
+  }
+  return (int)f.size();
+}
+
+double Engine::evaluate(const std::vector<int>& ids, Terms* terms) const {
+  const int k = (int)ids.size();
+  const int n = p_.n;
+  Terms t;
+  if (k >= 2) {
+    double s = 0;
+    for (int a = 0; a < k; ++a)
+      for (int b = a + 1; b < k; ++b) s += p_.cost[(size_t)ids[a] * n + ids[b]];
+    t.comm = 2.0 * s / ((double)k * (k - 1));
+  } else {
+    t.comm = 1.0;
+  }
+  for (const auto& lv : lv_) {
+    std::map<int, int> take;
+    for (int i : ids) take[lv.gid[i]] += 1;
+    t.span += (double)take.size() - min_groups(lv, k);
+    for (const auto& kv : take) {
+      const int g = kv.first;
+      const int after = lv.free[g] - kv.second;
+      if (lv.free[g] == lv.size[g] && after > 0) t.frag += 1;
+      t.fit += (double)after / lv.size[g];
+    }
+  }
+  double acc = 0;
+  for (int i : ids) acc += p_.access[i];
+  t.access = k ? acc / k : 0.0;
+  if (terms) *terms = t;
+  return t.comm + pol_.w_span * t.span + pol_.w_frag * t.frag + pol_.w_fit * t.fit + pol_.w_access * t.access;
+}
+
+void Engine::greedy(int k, const std::vector<int>& F, std::vector<int>* best, double* best_j) const {
+  // Greedy growth from every seed, then first-improvement 1-swap descent (core._greedy_local).
+  for (int seed : F) {
+    std::vector<int> cur{seed};
+    while ((int)cur.size() < k) {
+      int cand = -1;
+      double cj = std::numeric_limits<double>::infinity();
+      for (int c : F) {
+        if (std::find(cur.begin(), cur.end(), c) != cur.end()) continue;
+        cur.push_back(c);
+        double j = evaluate(cur, nullptr);
+        cur.pop_back();
+        if (j < cj - kEps) {
+          cj = j;
+          cand = c;
+        }
+      }
+      cur.push_back(cand);
+    }
+    double cur_j = evaluate(cur, nullptr);
+    bool improved = true;
+    while (improved) {
+      improved = false;
+      for (size_t a = 0; a < cur.size() && !improved; ++a) {
+        for (int b : F) {
+          if (std::find(cur.begin(), cur.end(), b) != cur.end()) continue;
+          std::vector<int> trial = cur;
+          trial[a] = b;
+          double tj = evaluate(trial, nullptr);
+          if (tj < cur_j - kEps) {
+            cur = trial;
+            cur_j = tj;
+            improved = true;
+            break;
+          }
+        }
+      }
+    }
+    std::sort(cur.begin(), cur.end());
+    if (cur_j < *best_j - kEps || (std::fabs(cur_j - *best_j) <= kEps && (best->empty() || cur < *best))) {
+      *best = cur;
+      *best_j = cur_j;
+    }
+  }
+}
+
+Result Engine::select(int k, uint64_t node_limit) const {
+  Result res;
+  if (k <= 0) throw std::invalid_argument("k must be >= 1");
+  const int n = p_.n;
+  std::vector<int> F;
+  for (int i = 0; i < n; ++i)
+    if (p_.free[i]) F.push_back(i);
+  const int m = (int)F.size();
+  if (m < k) return res;  // infeasible
+
+  // ---- global bounds helpers
+  // suffix-sorted access: amin_suffix[s][r] would be O(m^2); a global minimum is enough here.
+  double amin = std::numeric_limits<double>::infinity();
+  for (int i : F) amin = std::min(amin, p_.access[i]);
+  // pre[c][t] = sum of the t cheapest links from F[c] to other free devices: every device of a
+  // completion R (|R| = r) pays at least half of its r-1 cheapest links inside R.
+  std::vector<std::vector<double>> pre(m, std::vector<double>(m, 0.0));
+  {
+    std::vector<double> row;
+    for (int a = 0; a < m; ++a) {
+      row.clear();
+      for (int b = 0; b < m; ++b)
+        if (b != a) row.push_back(p_.cost[(size_t)F[a] * n + F[b]]);
+      std::sort(row.begin(), row.end());
+      for (size_t t = 0; t < row.size(); ++t) pre[a][t + 1] = pre[a][t] + row[t];
+    }
+  }
+  std::vector<int> mg(lv_.size());
+  for (size_t l = 0; l < lv_.size(); ++l) mg[l] = min_groups(lv_[l], k);
+  const double pairs_k = k >= 2 ? 0.5 * k * (k - 1) : 1.0;
+
+  // ---- DFS state
+  std::vector<int> chosen;  // positions into F
+  chosen.reserve(k);
+  std::vector<std::vector<int>> take(lv_.size());
+  std::vector<int> touched(lv_.size(), 0);
+  for (size_t l = 0; l < lv_.size(); ++l) take[l].assign(lv_[l].size.size(), 0);
+  std::vector<std::vector<double>> cross(k + 1, std::vector<double>(m, 0.0));  // cross[d][c] = sum cost(F[c], P_d)
+  std::vector<double> scratch(m);
+
+  double best_j = std::numeric_limits<double>::infinity();
+  std::vector<int> best_pos;
+  uint64_t nodes = 0, leaves = 0;
+  bool aborted = false;
+
+  // Leaf objective from the incremental state.
+  auto leaf_objective = [&](double pairsum, double accsum) {
+    double comm = k >= 2 ? pairsum / pairs_k : 1.0;
+    double span = 0, frag = 0, fit = 0;
+    for (size_t l = 0; l < lv_.size(); ++l) {
+      span += touched[l] - mg[l];
+      const auto& lv = lv_[l];
+      // walk the touched groups once: use the chosen devices' groups, dedup by marking
+      for (size_t ci = 0; ci < chosen.size(); ++ci) {
+        int g = lv.gid[F[chosen[ci]]];
+        bool first = true;
+        for (size_t cj = 0; cj < ci; ++cj)
+          if (lv.gid[F[chosen[cj]]] == g) {
+            first = false;
+            break;
+          }
+        if (!first) continue;
+        int after = lv.free[g] - take[l][g];
+        if (lv.free[g] == lv.size[g] && after > 0) frag += 1;
+        fit += (double)after / lv.size[g];
+      }
+    }
+    return comm + pol_.w_span * span + pol_.w_frag * frag + pol_.w_fit * fit + pol_.w_access * (accsum / k);
+  };
+
+  // Large search spaces: seed the incumbent with greedy + 1-swap so pruning bites from the start.
+  // (Ties then resolve to the greedy set rather than the lexicographically first optimum.)
+  double log_comb = std::lgamma(m + 1.0) - std::lgamma(k + 1.0) - std::lgamma(m - k + 1.0);
+  if (log_comb > std::log(2.0e5)) {
+    std::vector<int> g;
+    double gj = std::numeric_limits<double>::infinity();
+    greedy(k, F, &g, &gj);
+    best_j = gj;
+    for (int dev : g) best_pos.push_back((int)(std::lower_bound(F.begin(), F.end(), dev) - F.begin()));
+  }
+
+  std::function<void(int, double, double)> dfs = [&](int start, double pairsum, double accsum) {
+    if (aborted) return;
+    const int d = (int)chosen.size();
+    if (d == k) {
+      ++leaves;
+      double j = leaf_objective(pairsum, accsum);
+      if (j < best_j - kEps) {
+        best_j = j;
+        best_pos = chosen;
+      }
+      return;
+    }
+    if (++nodes > node_limit) {
+      aborted = true;
+      return;
+    }
+    const int r = k - d;
+    // lower bound over completions drawn from F[start..m)
+    if (std::isfinite(best_j)) {
+      double comm_lb = 1.0;
+      if (k >= 2) {
+        int cnt = m - start;
+        for (int c = 0; c < cnt; ++c) scratch[c] = cross[d][start + c] + 0.5 * pre[start + c][r - 1];
+        std::nth_element(scratch.begin(), scratch.begin() + (r - 1), scratch.begin() + cnt);
+        double add = 0;
+        for (int c = 0; c < r; ++c) add += scratch[c];
+        // nth_element leaves the r smallest in [0, r) in arbitrary order
+        comm_lb = (pairsum + std::max(add, 0.0)) / pairs_k;
+      }
+      double span_lb = 0;
+      for (size_t l = 0; l < lv_.size(); ++l) span_lb += std::max(0, touched[l] - mg[l]);
+      double lb = comm_lb + pol_.w_span * span_lb + pol_.w_access * ((accsum + r * amin) / k);
+      if (lb >= best_j - kEps) return;
+    }
+    for (int c = start; c <= m - r; ++c) {
+      const int dev = F[c];
+      // push
+      chosen.push_back(c);
+      for (size_t l = 0; l < lv_.size(); ++l) {
+        int g = lv_[l].gid[dev];
+        if (take[l][g]++ == 0) touched[l] += 1;
+      }
+      const double add_pairs = cross[d][c];
+      if (d + 1 < k) {
+        const double* row = &p_.cost[(size_t)dev * n];
+        for (int q = c + 1; q < m; ++q) cross[d + 1][q] = cross[d][q] + row[F[q]];
+      }
+      dfs(c + 1, pairsum + add_pairs, accsum + p_.access[dev]);
+      // pop
+      for (size_t l = 0; l < lv_.size(); ++l) {
+        int g = lv_[l].gid[dev];
+        if (--take[l][g] == 0) touched[l] -= 1;
+      }
+      chosen.pop_back();
+      if (aborted) return;
+    }
+  };
+  dfs(0, 0.0, 0.0);
+
+  std::vector<int> ids;
+  for (int pos : best_pos) ids.push_back(F[pos]);
+  res.exact = !aborted;
+  if (aborted && best_pos.size() != (size_t)k) {
+    double gj = std::numeric_limits<double>::infinity();
+    std::vector<int> g;
+    greedy(k, F, &g, &gj);
+    ids = g;
+  }
+  res.ids = ids;
+  res.objective = evaluate(ids, &res.terms);
+  res.feasible = true;
+  res.nodes = nodes;
+  res.leaves = leaves;
+  return res;
+}
+
+Result Engine::worst(int k) const {
+  Result res;
+  const int n = p_.n;
+  std::vector<int> F;
+  for (int i = 0; i < n; ++i)
+    if (p_.free[i]) F.push_back(i);
+  const int m = (int)F.size();
+  if (k <= 0 || m < k) return res;
+  std::vector<int> idx(k);
+  std::iota(idx.begin(), idx.end(), 0);
+  double bj = -std::numeric_limits<double>::infinity();
+  std::vector<int> cur(k), best;
+  while (true) {
+    for (int i = 0; i < k; ++i) cur[i] = F[idx[i]];
+    double j = evaluate(cur, nullptr);
+    ++res.leaves;
+    if (j > bj + kEps) {
+      bj = j;
+      best = cur;
+    }
+    int i = k - 1;
+    while (i >= 0 && idx[i] == m - k + i) --i;
+    if (i < 0) break;
+    ++idx[i];
+    for (int q = i + 1; q < k; ++q) idx[q] = idx[q - 1] + 1;
+  }
+  res.ids = best;
+  res.objective = evaluate(best, &res.terms);
+  res.feasible = true;
+  return res;
+}
+
+}  // namespace gtk

@@ -5,6 +5,7 @@
 Targets (all land in ``gpu_topology_on_k8s_amd/_native/``):
   _topo       C++  (g++)    amdsmi (dlopen) + KFD sysfs topology reader
   _placement  C++  (g++)    branch-and-bound placement engine
+  bin/engine_selftest       ASan/UBSan host build of the engine checked against brute force
   _probe      HIP  (hipcc)  gfx950 link/HBM probe kernels + MFMA warm-up
   _rccl       HIP  (hipcc)  RCCL all-reduce validator (librccl)
   _fused      HIP  (hipcc)  PyTorch custom ops for the Llama-3 workload (torch headers)
@@ -100,8 +101,12 @@ def targets() -> List[Target]:
     rocm_lib = str(ROCM / "lib")
     return [
         Target("_topo", [CSRC / "topo" / "topo_reader.cpp"], "gxx", HERE / f"_topo{EXT}", ["-ldl"]),
-        Target("_placement", [CSRC / "placement" / "engine.cpp"], "gxx", HERE / f"_placement{EXT}",
-               deps=[CSRC / "placement" / "engine.h"]),
+        Target("_placement", [CSRC / "placement" / "engine.cpp", CSRC / "placement" / "engine_module.cpp"], "gxx",
+               HERE / f"_placement{EXT}", deps=[CSRC / "placement" / "engine.h"]),
+        # host-only sanitizer build of the engine; run by tests/test_placement_native.py
+        Target("engine_selftest", [CSRC / "placement" / "engine.cpp", CSRC / "placement" / "engine_selftest.cpp"], "gxx",
+               HERE / "bin" / "engine_selftest", ["-g", "-O1", "-fsanitize=address,undefined", "-fno-omit-frame-pointer"],
+               deps=[CSRC / "placement" / "engine.h"], pybind=False, shared=False),
         Target("_probe", [CSRC / "probe" / "probe.hip"], "hipcc", HERE / f"_probe{EXT}"),
         Target("_rccl", [CSRC / "rccl" / "rccl_module.hip"], "hipcc", HERE / f"_rccl{EXT}",
                [f"-L{rocm_lib}", "-lrccl", f"-Wl,-rpath,{rocm_lib}"], deps=[CSRC / "rccl" / "rccl_core.h"]),

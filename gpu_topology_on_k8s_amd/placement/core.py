@@ -55,13 +55,18 @@ class PlacementPolicy:
     w_fit: float = 0.05
     w_access: float = 0.1
     tie_break: str = "first"  # "first" (deterministic, lowest ids) | "random"
-    exact_limit: int = 200_000  # max subsets enumerated exactly; above -> greedy + local search
+    exact_limit: int = 200_000  # Python path: max subsets enumerated exactly; above -> greedy + local search
+    node_limit: int = 2_000_000  # native path: branch-and-bound node budget; above -> greedy + local search
 
     def to_dict(self) -> Dict[str, object]:
         return dict(
             w_span=self.w_span, w_frag=self.w_frag, w_fit=self.w_fit, w_access=self.w_access,
-            tie_break=self.tie_break, exact_limit=self.exact_limit,
+            tie_break=self.tie_break, exact_limit=self.exact_limit, node_limit=self.node_limit,
         )
+
+    @classmethod
+    def from_dict(cls, d: Dict[str, object]) -> "PlacementPolicy":
+        return cls(**{k: v for k, v in d.items() if k in cls.__dataclass_fields__})
 
 
 @dataclass
@@ -198,6 +203,30 @@ def _greedy_local(p: Problem, k: int, policy: PlacementPolicy, stats) -> Tuple[L
     return best, best_j
 
 
+def _native_engine():
+    from .._native import NativeUnavailable, load
+
+    try:
+        return load("_placement")
+    except NativeUnavailable:
+        return None
+
+
+def _select_native(mod, p: Problem, k: int, policy: PlacementPolicy) -> Placement:
+    r = mod.select(
+        np.ascontiguousarray(p.cost, dtype=np.float64), np.ascontiguousarray(p.free, dtype=bool),
+        [lv.astype(np.int64).tolist() for lv in p.levels], np.ascontiguousarray(p.access, dtype=np.float64), int(k),
+        policy.w_span, policy.w_frag, policy.w_fit, policy.w_access, int(policy.node_limit),
+    )
+    if not r["feasible"]:
+        raise NoFeasiblePlacement(f"need {k} free devices")
+    terms = dict(r["terms"])
+    terms["search_nodes"] = float(r["nodes"])
+    terms["search_us"] = float(r["micros"])
+    return Placement(ids=tuple(int(i) for i in r["ids"]), objective=float(r["objective"]), score=score_from_objective(r["objective"]),
+                     comm=terms["comm"], terms=terms, exact=bool(r["exact"]))
+
+
 def select(
     topo_or_problem,
     k: int,
@@ -205,14 +234,30 @@ def select(
     policy: PlacementPolicy = PlacementPolicy(),
     access: Optional[Sequence[float]] = None,
     rng: Optional[random.Random] = None,
+    engine: str = "auto",
 ) -> Placement:
-    """Choose ``k`` free devices minimising :func:`evaluate`'s objective."""
+    """Choose ``k`` free devices minimising :func:`evaluate`'s objective.
+
+    ``engine``: ``native`` = C++ branch-and-bound (``csrc/placement/engine.cpp``), ``python`` = the
+    enumeration below, ``auto`` = native when built (deterministic tie-break only; random
+    tie-breaking needs the full tie list, which only the Python path collects).
+    """
     p = topo_or_problem if isinstance(topo_or_problem, Problem) else Problem.from_topology(topo_or_problem, used, access)
     if k <= 0:
         raise ValueError("k must be >= 1")
     free_ids = [i for i in range(p.n) if p.free[i]]
     if len(free_ids) < k:
         raise NoFeasiblePlacement(f"need {k} free devices, have {len(free_ids)}")
+    if engine not in ("auto", "native", "python"):
+        raise ValueError(engine)
+    if engine != "python" and policy.tie_break != "random":
+        mod = _native_engine()
+        if mod is not None:
+            return _select_native(mod, p, k, policy)
+        if engine == "native":
+            from .._native import load
+
+            load("_placement")  # raises NativeUnavailable with the build command
     stats = _level_stats(p)
     n_subsets = math.comb(len(free_ids), k)
     if n_subsets <= policy.exact_limit:

@@ -1,0 +1,77 @@
+"""Native discovery (``_topo``) against synthetic KFD sysfs trees, and the discovery front-end."""
+import numpy as np
+import pytest
+
+from gpu_topology_on_k8s_amd._native import available, load
+from gpu_topology_on_k8s_amd.topology import fixtures as fx
+from gpu_topology_on_k8s_amd.topology.discovery import DiscoveryError, discover, fake_topology, from_native
+from gpu_topology_on_k8s_amd.topology.model import LinkType
+
+needs_topo = pytest.mark.skipif(not available("_topo"), reason="_topo not built")
+
+
+@needs_topo
+def test_sysfs_full_mesh(tmp_path):
+    p = fx.write_fake_kfd_sysfs(str(tmp_path))
+    d = load("_topo").discover_sysfs(p["kfd"], p["drm"])
+    assert d["source"] == "sysfs"
+    assert len(d["gpus"]) == 8
+    g0 = d["gpus"][0]
+    assert g0["gfx"] == "gfx950" and g0["model"] == "MI355X"
+    assert g0["render_minor"] == 128 and g0["card"] == 0
+    assert g0["xgmi_links_up"] == 7 and g0["cus"] == 256
+    t = from_native(d, node_name="n1")
+    assert (t.link_type[~np.eye(8, dtype=bool)] == int(LinkType.XGMI)).all()
+    assert (t.hops[~np.eye(8, dtype=bool)] == 1).all()
+    assert t.numa.tolist() == [0, 0, 0, 0, 1, 1, 1, 1]
+    assert not d["warnings"]
+
+
+@needs_topo
+def test_sysfs_missing_xgmi_link_falls_back_to_pcie(tmp_path):
+    p = fx.write_fake_kfd_sysfs(str(tmp_path), missing_links=[(0, 5)])
+    t = from_native(load("_topo").discover_sysfs(p["kfd"], p["drm"]))
+    assert LinkType(int(t.link_type[0, 5])) == LinkType.PCIE_SYS
+    assert t.cost[0, 5] > t.cost[0, 1]
+    assert t.gpus[0].xgmi_links_up == 6
+
+
+@needs_topo
+def test_sysfs_cpx_partitions(tmp_path):
+    p = fx.write_fake_kfd_sysfs(str(tmp_path), partitions_per_gpu=8)
+    t = from_native(load("_topo").discover_sysfs(p["kfd"], p["drm"]))
+    assert t.n == 64
+    assert t.physical.tolist() == [i // 8 for i in range(64)]
+    assert all(g.partition == "CPX" for g in t.gpus)
+    assert LinkType(int(t.link_type[0, 1])) == LinkType.INTERNAL
+    assert LinkType(int(t.link_type[0, 8])) == LinkType.XGMI
+
+
+@needs_topo
+def test_sysfs_empty_root_raises(tmp_path):
+    with pytest.raises(RuntimeError):
+        load("_topo").discover_sysfs(str(tmp_path), str(tmp_path))
+
+
+@needs_topo
+def test_amdsmi_missing_library_raises():
+    with pytest.raises(RuntimeError):
+        load("_topo").discover_amdsmi("libdefinitely_not_amdsmi.so")
+
+
+def test_discover_fake_backend():
+    t = discover("fake", fake_n=2)
+    assert t.n == 2 and t.source == "fake"
+    assert fake_topology(8).numa.tolist() == [0] * 4 + [1] * 4
+
+
+@needs_topo
+def test_discover_sysfs_via_frontend(tmp_path):
+    p = fx.write_fake_kfd_sysfs(str(tmp_path), n_gpus=4, sockets=1)
+    t = discover("sysfs", sysfs_root=p["kfd"], drm_root=p["drm"], node_name="x")
+    assert t.n == 4 and t.node_name == "x"
+
+
+def test_discover_never_silently_fakes(tmp_path):
+    with pytest.raises(DiscoveryError):
+        discover("sysfs", sysfs_root=str(tmp_path / "nope"), drm_root=str(tmp_path))

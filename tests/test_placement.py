@@ -1,0 +1,225 @@
+"""Placement core: exact search == brute force, score properties, native engine == Python, legacy formulas."""
+import itertools
+import math
+import os
+import random
+import subprocess
+import time
+
+import numpy as np
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from gpu_topology_on_k8s_amd._native import available, binary
+from gpu_topology_on_k8s_amd.placement import (
+    NoFeasiblePlacement, PlacementPolicy, Problem, design_farthest_single, design_greedy_select, evaluate,
+    legacy_score, legacy_score_of_set, select, worst,
+)
+from gpu_topology_on_k8s_amd.placement.legacy import legacy_mark, legacy_score_literal
+from gpu_topology_on_k8s_amd.topology import fixtures as fx
+from gpu_topology_on_k8s_amd.topology.model import RefLinkClass
+
+needs_native = pytest.mark.skipif(not available("_placement"), reason="_placement not built")
+
+
+def _random_problem(rng: np.random.Generator, n: int) -> Problem:
+    c = rng.uniform(0.25, 4.0, size=(n, n))
+    c = np.triu(c, 1)
+    c = c + c.T
+    free = rng.random(n) > 0.25
+    levels = [np.array([0 if i < n // 2 else 1 for i in range(n)])]
+    if rng.random() < 0.5:
+        levels.insert(0, np.arange(n) // 2)
+    access = np.where(rng.random(n) < 0.5, 0.0, rng.uniform(0, 2, n))
+    return Problem(cost=c, free=free, levels=levels, access=access)
+
+
+def _brute(p: Problem, k: int, policy=PlacementPolicy()):
+    free_ids = [i for i in range(p.n) if p.free[i]]
+    best, bj = None, math.inf
+    for comb in itertools.combinations(free_ids, k):
+        j, _ = evaluate(p, comb, policy)
+        if j < bj - 1e-9:
+            best, bj = comb, j
+    return best, bj
+
+
+@settings(max_examples=60, deadline=None)
+@given(st.integers(min_value=2, max_value=10), st.integers(min_value=0, max_value=2**31 - 1))
+def test_python_exact_matches_bruteforce(n, seed):
+    rng = np.random.default_rng(seed)
+    p = _random_problem(rng, n)
+    nfree = int(p.free.sum())
+    for k in range(1, nfree + 1):
+        pl = select(p, k, engine="python")
+        ids, bj = _brute(p, k)
+        assert pl.ids == ids
+        assert pl.objective == pytest.approx(bj)
+
+
+@needs_native
+@settings(max_examples=80, deadline=None)
+@given(st.integers(min_value=2, max_value=12), st.integers(min_value=0, max_value=2**31 - 1))
+def test_native_engine_matches_python(n, seed):
+    rng = np.random.default_rng(seed)
+    p = _random_problem(rng, n)
+    for k in range(1, int(p.free.sum()) + 1):
+        a = select(p, k, engine="native")
+        b = select(p, k, engine="python")
+        assert a.exact
+        assert a.ids == b.ids, (k, a, b)
+        assert a.objective == pytest.approx(b.objective)
+        for key in ("comm", "span", "frag", "fit", "access"):
+            assert a.terms[key] == pytest.approx(b.terms[key])
+
+
+@needs_native
+def test_native_engine_sanitizer_selftest():
+    """ASan/UBSan host build of the engine vs brute force."""
+    exe = binary("engine_selftest")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1")
+    env.pop("LD_PRELOAD", None)
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "0 failures" in p.stdout
+
+
+def test_score_range_and_direction():
+    t = fx.f7_mi355x(link_gbps=76.5)
+    for k in range(1, 9):
+        pl = select(t, k)
+        assert 0 <= pl.score <= 10
+        assert 0 <= pl.k8s_score <= 10
+    # a degraded link makes every set containing it score lower
+    bw = t.bw_gbps.copy()
+    bw[0, 1] = bw[1, 0] = 10.0
+    t.set_measured_bw(bw)
+    p = Problem.from_topology(t)
+    j_bad, _ = evaluate(p, (0, 1))
+    j_ok, _ = evaluate(p, (0, 2))
+    assert j_bad > j_ok
+    assert select(t, 2).ids != (0, 1)
+
+
+def test_full_mesh_four_gpu_picks_one_numa_domain():
+    t = fx.f7_mi355x()
+    assert select(t, 4).ids in ((0, 1, 2, 3), (4, 5, 6, 7))
+
+
+def test_two_concurrent_four_gpu_pods_are_disjoint_numa_halves():
+    """BASELINE config 4: two 4-GPU pods land on disjoint NUMA halves."""
+    t = fx.f7_mi355x(link_gbps=76.5, noise=0.02, seed=5)
+    a = select(t, 4)
+    b = select(t, 4, used=a.ids)
+    assert not set(a.ids) & set(b.ids)
+    assert {t.gpus[i].numa for i in a.ids} != {t.gpus[i].numa for i in b.ids}
+    assert len({t.gpus[i].numa for i in a.ids}) == 1 and len({t.gpus[i].numa for i in b.ids}) == 1
+
+
+def test_singular_packing_on_mi355x():
+    """Gaia Singular generalised: a 1-GPU request goes next to an existing allocation."""
+    t = fx.f7_mi355x()
+    first = select(t, 1).ids
+    second = select(t, 1, used=first).ids
+    assert t.gpus[first[0]].numa == t.gpus[second[0]].numa
+    # after 3 single pods on NUMA0, a 4-GPU request still finds the pristine NUMA1
+    used = []
+    for _ in range(3):
+        used += list(select(t, 1, used=used).ids)
+    assert {t.gpus[i].numa for i in used} == {0}
+    assert select(t, 4, used=used).ids == (4, 5, 6, 7)
+
+
+def test_cpx_whole_package_first():
+    t = fx.f8_mi355x_cpx()
+    pl = select(t, 8)
+    assert len({t.gpus[i].physical for i in pl.ids}) == 1
+    pl2 = select(t, 8, used=pl.ids)
+    assert len({t.gpus[i].physical for i in pl2.ids}) == 1
+    assert not set(pl.ids) & set(pl2.ids)
+
+
+@needs_native
+def test_cpx_large_requests_are_fast():
+    t = fx.f8_mi355x_cpx(link_gbps=76.5, noise=0.05, seed=2)
+    for k in (2, 4, 8, 16, 32):
+        t0 = time.perf_counter()
+        pl = select(t, k, used=[0, 9, 18])
+        dt = time.perf_counter() - t0
+        assert len(pl.ids) == k and not {0, 9, 18} & set(pl.ids)
+        assert dt < 5.0, (k, dt)
+
+
+def test_infeasible():
+    t = fx.f7_mi355x()
+    with pytest.raises(NoFeasiblePlacement):
+        select(t, 5, used=[0, 1, 2, 3])
+    with pytest.raises(ValueError):
+        select(t, 0)
+
+
+def test_unhealthy_devices_are_never_chosen():
+    t = fx.f7_mi355x()
+    t.gpus[0].healthy = False
+    t.gpus[1].healthy = False
+    assert not {0, 1} & set(select(t, 4).ids)
+    assert not {0, 1} & set(select(t, 6).ids)
+
+
+def test_random_tie_break_spreads():
+    t = fx.f7_mi355x()
+    rng = random.Random(1)
+    pol = PlacementPolicy(tie_break="random")
+    seen = {select(t, 1, policy=pol, rng=rng).ids for _ in range(200)}
+    assert len(seen) > 1
+
+
+def test_worst_is_worse_than_best():
+    t = fx.f7_mi355x(link_gbps=76.5, noise=0.1, seed=9)
+    for k in (2, 4, 6):
+        assert worst(t, k).objective >= select(t, k).objective
+
+
+# ------------------------------------------------------------------ reference (legacy) formulas
+def test_design_example_score():
+    """design.md:213-217: marks 1,1,1,2,3,3 -> 10*(1-11/36) = 6.94."""
+    assert legacy_score([1, 1, 1, 2, 3, 3]) == pytest.approx(6.944, abs=1e-3)
+    assert legacy_score([]) == 10.0  # single GPU
+    # the literal typed formula multiplies by len -> negative nonsense
+    assert legacy_score_literal([1, 1, 1, 2, 3, 3]) < 0
+
+
+def test_legacy_marks():
+    assert legacy_mark(RefLinkClass.SYS) == 1
+    assert legacy_mark(RefLinkClass.PSB) == 6
+    with pytest.raises(ValueError):
+        legacy_mark(RefLinkClass.NV3)
+
+
+def test_legacy_score_of_f1_set():
+    t = fx.f1_nvlink_host()
+    s = legacy_score_of_set(t, [0, 2, 4])  # all PHB (mark 3)
+    assert s == pytest.approx(10 * (1 - 9 / 18))
+
+
+def test_design_greedy_and_tie_flaw():
+    t = fx.f1_nvlink_host()
+    ids = design_greedy_select(t.cost, [], 2)
+    assert t.ref_class[ids[0], ids[1]] == int(RefLinkClass.NV3)
+    assert design_greedy_select(t.cost, [], 1) == [0]
+    assert design_greedy_select(t.cost, list(range(7)), 2) == []
+    # tie flaw (design.md:188-190): greedy can lock in a worse 3-set than the exact search
+    d = np.array([[0, 1, 5, 5], [1, 0, 5, 5], [5, 5, 0, 1], [5, 5, 1, 0]], float)
+    d[0, 2] = d[2, 0] = 1.2
+    g = design_greedy_select(d, [], 3)
+    gsum = sum(d[a, b] for a, b in itertools.combinations(g, 2))
+    best = min(sum(d[a, b] for a, b in itertools.combinations(c, 2)) for c in itertools.combinations(range(4), 3))
+    assert gsum >= best
+
+
+def test_design_farthest_single():
+    t = fx.f1_nvlink_host()
+    i = design_farthest_single(t.cost, [])
+    assert i is not None and 0 <= i < 8
+    assert design_farthest_single(t.cost, list(range(8))) is None
