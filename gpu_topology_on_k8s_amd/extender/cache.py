@@ -1,0 +1,264 @@
+"""Extender node cache: topology per node + device usage rebuilt from pod annotations.
+
+Reference: ``design.md:234`` "update the pod annotation and record the running pod on the device";
+the diagram's device report carries ``isUsed``.  Here the *pod annotations are the source of truth*
+(SURVEY.md §2.A A13, §5.3 (c)): usage of a node = union of ``ALIYUN_COM_GPU_GROUP`` over its
+bound, non-terminal pods whose assignment is either confirmed (``ASSIGNED=true``, written by the
+device plugin at Allocate) or still within the assume TTL (``ASSIGNED=false`` and
+``now - ASSUME_TIME <= ttl``).  An expired assumption releases its devices (§5.3 (b)), and an
+extender restart loses nothing because it rebuilds from the apiserver.
+
+An in-memory *overlay* records binds this process made but that the apiserver view may not show yet
+(watch lag / list cache), so two back-to-back binds on one node never overlap.  Pods that consume
+the resource but carry no GROUP (scheduled around the extender) are counted as ``unknown`` usage:
+their device ids are unknown, so only feasibility is reduced.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, Iterable, List, Optional, Set, Tuple
+
+from ..k8s.annotations import Contract, PodAssignment, decode_node_annotations
+from ..k8s.api import KubeAPI
+from ..k8s.objects import annotations as obj_annotations
+from ..k8s.objects import labels as obj_labels
+from ..k8s.objects import meta, pod_gpu_request, pod_is_terminal, pod_key, pod_node
+from ..topology.model import Topology
+
+log = logging.getLogger(__name__)
+
+__all__ = ["Alloc", "NodeState", "ClusterCache"]
+
+
+@dataclass
+class Alloc:
+    pod: str
+    ids: Tuple[int, ...]
+    assigned: bool
+    assume_time: float
+    source: str = "annotation"  # annotation | overlay
+
+
+@dataclass
+class NodeState:
+    name: str
+    topology: Optional[Topology] = None
+    labels: Dict[str, str] = field(default_factory=dict)
+    node_rv: str = ""
+    allocs: Dict[str, Alloc] = field(default_factory=dict)
+    unknown: int = 0  # devices held by pods without a GROUP annotation
+    capacity: int = -1  # node.status.allocatable[resource] (-1 = unknown)
+    synced_at: float = 0.0
+    lock: threading.RLock = field(default_factory=threading.RLock, repr=False)
+
+    def used(self, now: float, ttl: float) -> Set[int]:
+        out: Set[int] = set()
+        for a in self.allocs.values():
+            if a.assigned or (now - a.assume_time) <= ttl:
+                out.update(a.ids)
+        return out
+
+    def free_count(self, now: float, ttl: float) -> int:
+        if self.topology is None:
+            return 0
+        healthy = sum(1 for g in self.topology.gpus if g.healthy)
+        return max(0, healthy - len(self.used(now, ttl) & {g.index for g in self.topology.gpus if g.healthy}) - self.unknown)
+
+
+class ClusterCache:
+    def __init__(self, api: KubeAPI, contract: Contract = Contract(), assume_ttl: float = 300.0,
+                 resync_s: float = 5.0, clock: Callable[[], float] = time.time,
+                 resource_aliases: Iterable[str] = ()):
+        self.api = api
+        self.contract = contract
+        self.ttl = float(assume_ttl)
+        self.resync_s = float(resync_s)
+        self.clock = clock
+        self.resources = [contract.resource_name] + [r for r in resource_aliases if r != contract.resource_name]
+        self._nodes: Dict[str, NodeState] = {}
+        self._overlay: Dict[str, Dict[str, Alloc]] = {}  # node -> pod -> alloc (binds made here)
+        self._lock = threading.RLock()
+        self._last_full = 0.0
+        self.overlay_grace = 30.0  # seconds a bind made here may stay invisible in the apiserver view
+
+    # ------------------------------------------------------------------ node objects
+    def _state(self, name: str) -> NodeState:
+        with self._lock:
+            st = self._nodes.get(name)
+            if st is None:
+                st = self._nodes[name] = NodeState(name=name)
+            return st
+
+    def update_node_object(self, node: dict) -> NodeState:
+        name = meta(node).get("name", "")
+        st = self._state(name)
+        with st.lock:
+            rv = meta(node).get("resourceVersion", "")
+            if st.topology is None or rv != st.node_rv or not rv:
+                try:
+                    st.topology = decode_node_annotations(obj_annotations(node), self.contract, node_name=name)
+                except Exception as e:  # malformed annotation: treat as unknown topology
+                    log.warning("node %s: bad topology annotation: %s", name, e)
+                    st.topology = None
+                st.node_rv = rv
+            st.labels = dict(obj_labels(node))
+            alloc = ((node.get("status") or {}).get("allocatable") or {})
+            st.capacity = -1
+            for r in self.resources:
+                if r in alloc:
+                    try:
+                        st.capacity = int(float(alloc[r]))
+                    except ValueError:
+                        pass
+                    break
+        return st
+
+    # ------------------------------------------------------------------ pods -> usage
+    def _pod_alloc(self, pod: dict) -> Tuple[Optional[Alloc], int]:
+        """(alloc, unknown_devices) of one pod already filtered to a node."""
+        if pod_is_terminal(pod):
+            return None, 0
+        pa = PodAssignment.from_annotations(obj_annotations(pod))
+        if pa is None:
+            try:
+                req = pod_gpu_request(pod, self.resources)
+            except ValueError:
+                req = 0
+            return None, req
+        return Alloc(pod=pod_key(pod), ids=tuple(pa.group), assigned=pa.assigned, assume_time=float(pa.assume_time)), 0
+
+    def _rebuild(self, st: NodeState, pods: List[dict]) -> None:
+        allocs: Dict[str, Alloc] = {}
+        unknown = 0
+        seen = set()
+        for p in pods:
+            seen.add(pod_key(p))
+            a, u = self._pod_alloc(p)
+            unknown += u
+            if a is not None:
+                allocs[a.pod] = a
+        now = self.clock()
+        with self._lock:
+            ov = self._overlay.get(st.name, {})
+            for key in list(ov):
+                a = ov[key]
+                if key in seen:
+                    del ov[key]  # the apiserver view has the pod: it is authoritative from now on
+                elif now - a.assume_time > min(self.ttl, self.overlay_grace):
+                    del ov[key]  # never showed up (deleted right after bind)
+                else:
+                    allocs[key] = a
+        st.allocs = allocs
+        st.unknown = unknown
+        st.synced_at = now
+
+    def refresh_node(self, name: str) -> NodeState:
+        """Authoritative re-read of one node and its pods (used before every bind)."""
+        node = self.api.get_node(name)
+        st = self.update_node_object(node)
+        pods = self.api.list_pods(node_name=name)
+        with st.lock:
+            self._rebuild(st, pods)
+        return st
+
+    def sync_all(self) -> None:
+        nodes = self.api.list_nodes()
+        pods = self.api.list_pods()
+        by_node: Dict[str, List[dict]] = {}
+        for p in pods:
+            n = pod_node(p)
+            if n:
+                by_node.setdefault(n, []).append(p)
+        names = set()
+        for node in nodes:
+            st = self.update_node_object(node)
+            names.add(st.name)
+            with st.lock:
+                self._rebuild(st, by_node.get(st.name, []))
+        with self._lock:
+            for gone in set(self._nodes) - names:
+                del self._nodes[gone]
+            self._last_full = self.clock()
+
+    def maybe_sync(self) -> None:
+        if self.clock() - self._last_full >= self.resync_s:
+            self.sync_all()
+
+    def get(self, name: str, node_obj: Optional[dict] = None) -> NodeState:
+        """Cached state of a node; refreshed from ``node_obj`` when the scheduler passed full nodes."""
+        if node_obj is not None:
+            st = self.update_node_object(node_obj)
+        else:
+            st = self._state(name)
+        if st.synced_at == 0.0 or self.clock() - st.synced_at >= self.resync_s:
+            try:
+                self.refresh_node(name)
+            except Exception as e:
+                log.warning("refresh of node %s failed: %s", name, e)
+        return st
+
+    # ------------------------------------------------------------------ writes made by this process
+    def assume(self, node: str, pod: str, ids: Iterable[int], at: Optional[float] = None) -> None:
+        a = Alloc(pod=pod, ids=tuple(int(i) for i in ids), assigned=False, assume_time=at if at is not None else self.clock(),
+                  source="overlay")
+        with self._lock:
+            self._overlay.setdefault(node, {})[pod] = a
+        st = self._state(node)
+        with st.lock:
+            st.allocs[pod] = a
+
+    def forget(self, node: str, pod: str) -> None:
+        with self._lock:
+            self._overlay.get(node, {}).pop(pod, None)
+        st = self._state(node)
+        with st.lock:
+            st.allocs.pop(pod, None)
+
+    # ------------------------------------------------------------------ watch events (fake / informer)
+    def on_event(self, event: str, kind: str, obj: dict) -> None:
+        if kind == "Node":
+            if event == "DELETED":
+                with self._lock:
+                    self._nodes.pop(meta(obj).get("name", ""), None)
+            else:
+                self.update_node_object(obj)
+            return
+        if kind != "Pod":
+            return
+        node = pod_node(obj)
+        if not node:
+            return
+        st = self._state(node)
+        key = pod_key(obj)
+        with st.lock:
+            if event == "DELETED" or pod_is_terminal(obj):
+                st.allocs.pop(key, None)
+                with self._lock:
+                    self._overlay.get(node, {}).pop(key, None)
+                return
+            a, _ = self._pod_alloc(obj)
+            if a is not None:
+                st.allocs[key] = a
+
+    def nodes(self) -> List[NodeState]:
+        with self._lock:
+            return list(self._nodes.values())
+
+    def snapshot(self) -> Dict[str, dict]:
+        now = self.clock()
+        out = {}
+        for st in self.nodes():
+            with st.lock:
+                out[st.name] = {
+                    "devices": st.topology.n if st.topology else 0,
+                    "used": sorted(st.used(now, self.ttl)),
+                    "unknown": st.unknown,
+                    "free": st.free_count(now, self.ttl),
+                    "allocs": {k: {"ids": list(a.ids), "assigned": a.assigned, "assume_time": a.assume_time, "source": a.source}
+                               for k, a in st.allocs.items()},
+                    "labels": st.labels,
+                }
+        return out

@@ -1,0 +1,173 @@
+"""HTTP front-end of the extender (kube-scheduler extender v1 JSON over aiohttp).
+
+Reference endpoint (``design.md:98-100``): ``http://127.0.0.1:32743/gputopology-scheduler`` with
+``/sort`` (prioritize) and ``/bind``.  Served here under the same prefix and port by default:
+
+  POST {prefix}/sort        ExtenderArgs -> HostPriorityList           (reference verb name)
+  POST {prefix}/prioritize  alias of /sort
+  POST {prefix}/filter      ExtenderArgs -> ExtenderFilterResult       (optional)
+  POST {prefix}/bind        ExtenderBindingArgs -> ExtenderBindingResult
+  GET  {prefix}/healthz, /metrics (Prometheus text), /version, /debug/nodes (cache snapshot)
+
+kube-scheduler marshals Go structs without json tags, so request keys are capitalised (``Pod``,
+``Nodes``, ``NodeNames``, ``PodName`` ...); Go's decoder matches keys case-insensitively, so the
+responses use the same capitalised names.  Lower-case request keys are accepted too.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import time
+from concurrent.futures import ThreadPoolExecutor
+from typing import Any, Dict, List, Optional, Tuple
+
+from aiohttp import web
+
+from .. import __version__
+from .scheduler import TopologyExtender
+
+log = logging.getLogger(__name__)
+
+__all__ = ["make_app", "run", "DEFAULT_PORT", "DEFAULT_PREFIX"]
+
+DEFAULT_PORT = 32743
+DEFAULT_PREFIX = "/gputopology-scheduler"
+EXTENDER_KEY = web.AppKey("extender", TopologyExtender)
+
+
+def _get(d: Dict[str, Any], key: str, default=None):
+    if key in d:
+        return d[key]
+    lk = key.lower()
+    for k, v in d.items():
+        if k.lower() == lk:
+            return v
+    return default
+
+
+def _candidates(args: Dict[str, Any]) -> Tuple[List[str], Optional[Dict[str, dict]], bool]:
+    """(node names, {name: node object} when full nodes were sent, whether NodeNames mode)."""
+    names = _get(args, "NodeNames")
+    if names is not None:
+        return list(names), None, True
+    nodes = _get(args, "Nodes") or {}
+    items = _get(nodes, "items") or []
+    objs = {((n.get("metadata") or {}).get("name", "")): n for n in items}
+    return list(objs), objs, False
+
+
+def make_app(ext: TopologyExtender, prefix: str = DEFAULT_PREFIX, workers: int = 8) -> web.Application:
+    pool = ThreadPoolExecutor(max_workers=workers, thread_name_prefix="extender")
+    prefix = "/" + prefix.strip("/") if prefix.strip("/") else ""
+
+    async def run_blocking(fn, *a):
+        return await asyncio.get_running_loop().run_in_executor(pool, fn, *a)
+
+    async def body(request: web.Request) -> Dict[str, Any]:
+        try:
+            return await request.json(loads=json.loads)
+        except Exception as e:
+            raise web.HTTPBadRequest(text=f"invalid JSON: {e}")
+
+    async def prioritize(request: web.Request) -> web.Response:
+        args = await body(request)
+        pod = _get(args, "Pod") or {}
+        names, objs, _ = _candidates(args)
+        try:
+            res = await run_blocking(ext.prioritize, pod, names, objs)
+            ext.metrics.request("prioritize", "ok")
+        except Exception as e:  # never fail scheduling because of the extender: score 0
+            log.exception("prioritize failed")
+            ext.metrics.request("prioritize", "error")
+            res = [(n, 0) for n in names]
+            return web.json_response([{"Host": h, "Score": s} for h, s in res], headers={"X-Extender-Error": str(e)[:200]})
+        return web.json_response([{"Host": h, "Score": s} for h, s in res])
+
+    async def filter_(request: web.Request) -> web.Response:
+        args = await body(request)
+        pod = _get(args, "Pod") or {}
+        names, objs, names_mode = _candidates(args)
+        try:
+            ok, failed = await run_blocking(ext.filter, pod, names, objs)
+        except Exception as e:
+            log.exception("filter failed")
+            ext.metrics.request("filter", "error")
+            return web.json_response({"Nodes": None, "NodeNames": None, "FailedNodes": {}, "FailedAndUnresolvableNodes": {},
+                                      "Error": str(e)})
+        ext.metrics.request("filter", "ok")
+        out: Dict[str, Any] = {"FailedNodes": failed, "FailedAndUnresolvableNodes": {}, "Error": ""}
+        if names_mode:
+            out["NodeNames"] = ok
+            out["Nodes"] = None
+        else:
+            out["Nodes"] = {"metadata": {}, "items": [objs[n] for n in ok]}
+            out["NodeNames"] = None
+        return web.json_response(out)
+
+    async def bind(request: web.Request) -> web.Response:
+        args = await body(request)
+        try:
+            d = await run_blocking(ext.bind, _get(args, "PodNamespace", "default"), _get(args, "PodName"), _get(args, "PodUID", ""),
+                                   _get(args, "Node"))
+            ext.metrics.request("bind", "ok")
+            out = {"Error": ""}
+            if d is not None:
+                out["Devices"] = list(d.ids)  # extra field, ignored by kube-scheduler
+            return web.json_response(out)
+        except Exception as e:
+            log.warning("bind failed: %s", e)
+            ext.metrics.request("bind", "error")
+            return web.json_response({"Error": str(e)})
+
+    async def healthz(request: web.Request) -> web.Response:
+        return web.Response(text="ok")
+
+    async def metrics(request: web.Request) -> web.Response:
+        return web.Response(body=ext.metrics.exposition(), content_type="text/plain", charset="utf-8")
+
+    async def version(request: web.Request) -> web.Response:
+        return web.json_response({"version": __version__, "policy": ext.cfg.policy_name, "resource": ext.cfg.contract.resource_name})
+
+    async def debug_nodes(request: web.Request) -> web.Response:
+        return web.json_response(await run_blocking(ext.cache.snapshot))
+
+    async def on_cleanup(app):
+        pool.shutdown(wait=False, cancel_futures=True)
+
+    app = web.Application(client_max_size=64 << 20)
+    app.router.add_post(f"{prefix}/sort", prioritize)
+    app.router.add_post(f"{prefix}/prioritize", prioritize)
+    app.router.add_post(f"{prefix}/filter", filter_)
+    app.router.add_post(f"{prefix}/bind", bind)
+    for p in (f"{prefix}/healthz", "/healthz"):
+        app.router.add_get(p, healthz)
+    app.router.add_get(f"{prefix}/metrics", metrics)
+    app.router.add_get("/metrics", metrics)
+    app.router.add_get(f"{prefix}/version", version)
+    app.router.add_get(f"{prefix}/debug/nodes", debug_nodes)
+    app.on_cleanup.append(on_cleanup)
+    app[EXTENDER_KEY] = ext
+    return app
+
+
+def run(ext: TopologyExtender, host: str = "0.0.0.0", port: int = DEFAULT_PORT, prefix: str = DEFAULT_PREFIX,
+        resync_period: float = 5.0) -> None:
+    app = make_app(ext, prefix)
+
+    async def resync_loop(app):
+        async def loop():
+            while True:
+                try:
+                    await asyncio.get_running_loop().run_in_executor(None, ext.cache.sync_all)
+                except Exception as e:
+                    log.warning("cache resync failed: %s", e)
+                await asyncio.sleep(resync_period)
+
+        task = asyncio.create_task(loop())
+        yield
+        task.cancel()
+
+    app.cleanup_ctx.append(resync_loop)
+    log.info("extender listening on %s:%d%s (policy=%s)", host, port, prefix, ext.cfg.policy_name)
+    web.run_app(app, host=host, port=port, access_log=None, print=None)

@@ -1,0 +1,220 @@
+"""Wire contracts carried by Kubernetes objects — kept byte-compatible.
+
+Node annotations (written by the device plugin, read by the extender):
+  * ``GPU_<ABBR>_<i>_<j>: <description>`` — one per unordered device pair, ``design.md:76-82``
+    (e.g. ``GPU_SYS_0_1: Cross CPU socket``).  On MI355X the abbreviations are the AMD link classes
+    (``GPU_XGMI_0_1: xGMI 1 hop``, ``GPU_INTERNAL_0_1``, ``GPU_PCIE_..``, ``GPU_SYS_..``); the
+    reference's NVML abbreviations (SYS/NODE/PHB/PXB/PIX/PSB/NV#) are still parsed.
+  * ``<prefix>/topology`` — one JSON document with the full model (measured GB/s matrix, cost,
+    NUMA, partitions, probe metadata).  This answers the reference's weight TODO (``design.md:47``).
+
+Pod annotations (written by the extender at bind, flipped by the device plugin at Allocate):
+  * ``ALIYUN_COM_GPU_GROUP: 0,1,2,3`` — node-local device indices (``design.md:231``)
+  * ``ALIYUN_COM_GPU_ASSIGNED: false|true`` (``design.md:227,243``)
+  * ``ALIYUN_COM_GPU_ASSUME_TIME: <unix seconds>`` (``design.md:229,245``)
+  * ``gpu-id: 0,2`` — the diagram's alias (``imgs/gpu_topology_on_k8s.png`` step 4), read-only.
+"""
+from __future__ import annotations
+
+import json
+import re
+import time
+from dataclasses import dataclass
+from typing import Dict, List, Mapping, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..topology.model import LinkType, RefLinkClass, Topology
+
+__all__ = [
+    "ANN_GROUP", "ANN_ASSIGNED", "ANN_ASSUME_TIME", "ANN_GPU_ID_ALIAS", "Contract", "PodAssignment",
+    "encode_node_annotations", "decode_node_annotations", "pair_annotations", "parse_pair_annotations",
+    "parse_group", "format_group",
+]
+
+ANN_GROUP = "ALIYUN_COM_GPU_GROUP"
+ANN_ASSIGNED = "ALIYUN_COM_GPU_ASSIGNED"
+ANN_ASSUME_TIME = "ALIYUN_COM_GPU_ASSUME_TIME"
+ANN_GPU_ID_ALIAS = "gpu-id"
+
+DEFAULT_PREFIX = "gputopology.amd.com"
+DEFAULT_RESOURCE = "amd.com/gpu"
+COMPAT_RESOURCE = "aliyun.com/gpu"  # design.md:86,105 (aliyun.com/gpu-count in the prose/diagram)
+
+_PAIR_RE = re.compile(r"^GPU_([A-Z0-9]+)_(\d+)_(\d+)$")
+
+
+@dataclass(frozen=True)
+class Contract:
+    """Names that make up the cluster-state contract (configurable)."""
+
+    resource_name: str = DEFAULT_RESOURCE
+    prefix: str = DEFAULT_PREFIX
+
+    @property
+    def topology_key(self) -> str:
+        return f"{self.prefix}/topology"
+
+    @property
+    def probe_time_key(self) -> str:
+        return f"{self.prefix}/probe-time"
+
+    @property
+    def cpuset_key(self) -> str:
+        """Pod annotation: recommended NUMA node(s) / cpuset for the kubelet CPU manager (Gaia B6)."""
+        return f"{self.prefix}/numa-nodes"
+
+    @property
+    def score_key(self) -> str:
+        return f"{self.prefix}/placement-score"
+
+    @property
+    def label_model(self) -> str:
+        """Node label for heterogeneous-cluster quota (Gaia B7)."""
+        return f"{self.prefix}/gpu-model"
+
+    @property
+    def label_partition(self) -> str:
+        return f"{self.prefix}/compute-partition"
+
+    @property
+    def label_gfx(self) -> str:
+        return f"{self.prefix}/gfx"
+
+    @property
+    def pod_model_key(self) -> str:
+        """Pod annotation/label selecting a GPU model (pods without it accept any single model)."""
+        return f"{self.prefix}/gpu-model"
+
+
+# ------------------------------------------------------------------------------ node annotations
+def _pair_abbr_desc(t: Topology, i: int, j: int) -> Tuple[str, str]:
+    if t.ref_class is not None and int(t.ref_class[i, j]) > 0:
+        rc = RefLinkClass(int(t.ref_class[i, j]))
+        return rc.name, rc.desc
+    lt = LinkType(int(t.link_type[i, j]))
+    if lt == LinkType.XGMI:
+        h = int(t.hops[i, j])
+        return lt.abbr, f"xGMI {h} hop" + ("s" if h != 1 else "")
+    return lt.abbr, lt.desc
+
+
+def pair_annotations(t: Topology) -> Dict[str, str]:
+    """``GPU_<ABBR>_<i>_<j>`` for every unordered pair (none for a single GPU, design.md:17-19)."""
+    out: Dict[str, str] = {}
+    for i, j in t.pairs():
+        abbr, desc = _pair_abbr_desc(t, i, j)
+        out[f"GPU_{abbr}_{i}_{j}"] = desc
+    return out
+
+
+def parse_pair_annotations(ann: Mapping[str, str]) -> Dict[Tuple[int, int], str]:
+    """``{(i, j): ABBR}`` from ``GPU_<ABBR>_<i>_<j>`` keys (AMD or reference abbreviations)."""
+    out: Dict[Tuple[int, int], str] = {}
+    for k in ann:
+        m = _PAIR_RE.match(k)
+        if m:
+            i, j = int(m.group(2)), int(m.group(3))
+            out[(min(i, j), max(i, j))] = m.group(1)
+    return out
+
+
+def encode_node_annotations(t: Topology, contract: Contract = Contract(), with_pairs: bool = True) -> Dict[str, str]:
+    ann = {contract.topology_key: t.to_json()}
+    ts = t.probe.get("ts") if t.probe else None
+    if ts:
+        ann[contract.probe_time_key] = str(int(ts))
+    if with_pairs:
+        ann.update(pair_annotations(t))
+    return ann
+
+
+def topology_from_pairs(pairs: Dict[Tuple[int, int], str], n: Optional[int] = None) -> Topology:
+    """Rebuild a class-only model from pair annotations alone (a node written by a reference plugin)."""
+    if n is None:
+        n = 1 + max([max(p) for p in pairs] or [0])
+    abbrs = {a.name for a in RefLinkClass}
+    if pairs and all(v in abbrs for v in pairs.values()):
+        m = [["PHB"] * n for _ in range(n)]
+        for (i, j), a in pairs.items():
+            m[i][j] = m[j][i] = a
+        return Topology.from_ref_matrix(m, node_name="")
+    from ..topology.model import GPUInfo
+
+    lt = np.full((n, n), int(LinkType.UNKNOWN), dtype=np.int32)
+    for (i, j), a in pairs.items():
+        try:
+            v = int(LinkType.from_abbr(a))
+        except KeyError:
+            v = int(LinkType.UNKNOWN)
+        lt[i, j] = lt[j, i] = v
+    return Topology(gpus=[GPUInfo(index=i) for i in range(n)], link_type=lt, hops=np.ones((n, n), dtype=np.int32), source="pair-annotations")
+
+
+def decode_node_annotations(ann: Mapping[str, str], contract: Contract = Contract(), node_name: str = "") -> Optional[Topology]:
+    """Topology from a node's annotations: the JSON model if present, else the pair annotations."""
+    raw = ann.get(contract.topology_key)
+    if raw:
+        t = Topology.from_json(raw)
+        if node_name:
+            t.node_name = node_name
+        return t
+    pairs = parse_pair_annotations(ann)
+    if pairs:
+        t = topology_from_pairs(pairs)
+        t.node_name = node_name
+        return t
+    return None
+
+
+# ------------------------------------------------------------------------------- pod annotations
+def parse_group(s: Optional[str]) -> Optional[List[int]]:
+    if s is None:
+        return None
+    s = s.strip()
+    if not s:
+        return []
+    return [int(x) for x in s.split(",") if x.strip() != ""]
+
+
+def format_group(ids: Sequence[int]) -> str:
+    return ",".join(str(int(i)) for i in ids)
+
+
+@dataclass
+class PodAssignment:
+    """The allocation state a pod carries in its annotations."""
+
+    group: List[int]
+    assigned: bool
+    assume_time: int
+
+    @classmethod
+    def from_annotations(cls, ann: Optional[Mapping[str, str]]) -> Optional["PodAssignment"]:
+        ann = ann or {}
+        g = parse_group(ann.get(ANN_GROUP))
+        if g is None:
+            g = parse_group(ann.get(ANN_GPU_ID_ALIAS))  # diagram alias, read-only
+        if g is None:
+            return None
+        assigned = str(ann.get(ANN_ASSIGNED, "false")).lower() == "true"
+        try:
+            at = int(ann.get(ANN_ASSUME_TIME, "0"))
+        except ValueError:
+            at = 0
+        return cls(group=g, assigned=assigned, assume_time=at)
+
+    def to_annotations(self) -> Dict[str, str]:
+        return {
+            ANN_GROUP: format_group(self.group),
+            ANN_ASSIGNED: "true" if self.assigned else "false",
+            ANN_ASSUME_TIME: str(int(self.assume_time)),
+        }
+
+    @classmethod
+    def assumed(cls, ids: Sequence[int], now: Optional[float] = None) -> "PodAssignment":
+        return cls(group=list(ids), assigned=False, assume_time=int(now if now is not None else time.time()))
+
+
+def dumps_compact(obj) -> str:
+    return json.dumps(obj, separators=(",", ":"))

@@ -1,0 +1,170 @@
+"""Kubernetes API access: the interface the extender and device plugin use, and a thin REST client.
+
+The reference talks to the apiserver to annotate nodes (``design.md:76-82``), patch pod annotations
+(``design.md:223-246``), list pods and bind (``design.md:119``).  :class:`KubeAPI` is exactly that
+surface.  :class:`RestKubeAPI` speaks the real REST API (in-cluster service account or kubeconfig-
+less explicit URL/token); :class:`~.fake.FakeAPIServer` implements the same interface in memory for
+tests and the in-process cluster simulation, and can also be served over HTTP so the REST client is
+exercised on the wire.
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+from typing import Any, Dict, List, Optional
+from urllib.parse import quote
+
+__all__ = ["ApiError", "Conflict", "NotFound", "KubeAPI", "RestKubeAPI"]
+
+Obj = Dict[str, Any]
+
+
+class ApiError(RuntimeError):
+    def __init__(self, code: int, message: str = ""):
+        super().__init__(f"{code}: {message}")
+        self.code = code
+        self.message = message
+
+
+class Conflict(ApiError):
+    def __init__(self, message: str = "conflict"):
+        super().__init__(409, message)
+
+
+class NotFound(ApiError):
+    def __init__(self, message: str = "not found"):
+        super().__init__(404, message)
+
+
+def raise_for(code: int, message: str) -> None:
+    if code == 404:
+        raise NotFound(message)
+    if code == 409:
+        raise Conflict(message)
+    raise ApiError(code, message)
+
+
+class KubeAPI:
+    """Subset of the Kubernetes API used by this framework."""
+
+    def get_node(self, name: str) -> Obj:
+        raise NotImplementedError
+
+    def list_nodes(self, label_selector: Optional[str] = None) -> List[Obj]:
+        raise NotImplementedError
+
+    def patch_node(self, name: str, annotations: Optional[Dict[str, Optional[str]]] = None,
+                   labels: Optional[Dict[str, Optional[str]]] = None) -> Obj:
+        """JSON merge patch of node metadata (a ``None`` value deletes the key)."""
+        raise NotImplementedError
+
+    def get_pod(self, namespace: str, name: str) -> Obj:
+        raise NotImplementedError
+
+    def list_pods(self, node_name: Optional[str] = None, namespace: Optional[str] = None) -> List[Obj]:
+        raise NotImplementedError
+
+    def patch_pod_annotations(self, namespace: str, name: str, annotations: Dict[str, Optional[str]],
+                              resource_version: Optional[str] = None) -> Obj:
+        """Merge-patch pod annotations; with ``resource_version`` the patch is conditional (409 on mismatch)."""
+        raise NotImplementedError
+
+    def bind_pod(self, namespace: str, name: str, uid: str, node: str) -> None:
+        raise NotImplementedError
+
+
+def _selector_q(label_selector: Optional[str]) -> str:
+    return f"?labelSelector={quote(label_selector)}" if label_selector else ""
+
+
+class RestKubeAPI(KubeAPI):
+    """Minimal REST client (``requests``): JSON merge patches, pods/binding subresource."""
+
+    SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+    def __init__(self, base_url: str, token: Optional[str] = None, ca_file: Optional[str] = None, verify: bool = True,
+                 timeout: float = 10.0):
+        import requests
+
+        self.base = base_url.rstrip("/")
+        self.timeout = timeout
+        self._local = threading.local()
+        self._requests = requests
+        self._headers = {"Accept": "application/json"}
+        if token:
+            self._headers["Authorization"] = f"Bearer {token}"
+        self._verify = ca_file if (verify and ca_file) else verify
+
+    @classmethod
+    def in_cluster(cls) -> "RestKubeAPI":
+        host, port = os.environ.get("KUBERNETES_SERVICE_HOST"), os.environ.get("KUBERNETES_SERVICE_PORT", "443")
+        if not host:
+            raise RuntimeError("not running in a cluster (KUBERNETES_SERVICE_HOST unset); pass --apiserver")
+        with open(os.path.join(cls.SA_DIR, "token")) as f:
+            token = f.read().strip()
+        if ":" in host and not host.startswith("["):
+            host = f"[{host}]"
+        return cls(f"https://{host}:{port}", token=token, ca_file=os.path.join(cls.SA_DIR, "ca.crt"))
+
+    def _session(self):
+        s = getattr(self._local, "s", None)
+        if s is None:
+            s = self._requests.Session()
+            s.headers.update(self._headers)
+            self._local.s = s
+        return s
+
+    def _do(self, method: str, path: str, body: Any = None, content_type: str = "application/json") -> Obj:
+        headers = {}
+        data = None
+        if body is not None:
+            headers["Content-Type"] = content_type
+            data = json.dumps(body)
+        r = self._session().request(method, self.base + path, data=data, headers=headers, timeout=self.timeout, verify=self._verify)
+        if r.status_code >= 400:
+            try:
+                msg = r.json().get("message", r.text)
+            except ValueError:
+                msg = r.text
+            raise_for(r.status_code, msg)
+        return r.json() if r.content else {}
+
+    def get_node(self, name: str) -> Obj:
+        return self._do("GET", f"/api/v1/nodes/{quote(name)}")
+
+    def list_nodes(self, label_selector: Optional[str] = None) -> List[Obj]:
+        return self._do("GET", "/api/v1/nodes" + _selector_q(label_selector)).get("items", [])
+
+    def patch_node(self, name, annotations=None, labels=None) -> Obj:
+        md: Obj = {}
+        if annotations is not None:
+            md["annotations"] = annotations
+        if labels is not None:
+            md["labels"] = labels
+        return self._do("PATCH", f"/api/v1/nodes/{quote(name)}", {"metadata": md}, "application/merge-patch+json")
+
+    def get_pod(self, namespace: str, name: str) -> Obj:
+        return self._do("GET", f"/api/v1/namespaces/{quote(namespace)}/pods/{quote(name)}")
+
+    def list_pods(self, node_name: Optional[str] = None, namespace: Optional[str] = None) -> List[Obj]:
+        path = f"/api/v1/namespaces/{quote(namespace)}/pods" if namespace else "/api/v1/pods"
+        if node_name:
+            path += "?fieldSelector=" + quote(f"spec.nodeName={node_name}")
+        return self._do("GET", path).get("items", [])
+
+    def patch_pod_annotations(self, namespace, name, annotations, resource_version=None) -> Obj:
+        md: Obj = {"annotations": annotations}
+        if resource_version is not None:
+            md["resourceVersion"] = str(resource_version)
+        return self._do("PATCH", f"/api/v1/namespaces/{quote(namespace)}/pods/{quote(name)}", {"metadata": md},
+                        "application/merge-patch+json")
+
+    def bind_pod(self, namespace: str, name: str, uid: str, node: str) -> None:
+        body = {
+            "apiVersion": "v1",
+            "kind": "Binding",
+            "metadata": {"name": name, "namespace": namespace, **({"uid": uid} if uid else {})},
+            "target": {"apiVersion": "v1", "kind": "Node", "name": node},
+        }
+        self._do("POST", f"/api/v1/namespaces/{quote(namespace)}/pods/{quote(name)}/binding", body)

@@ -1,0 +1,321 @@
+"""In-memory Kubernetes apiserver (same :class:`~.api.KubeAPI` surface) with fault injection.
+
+Used by the test-suite and by the in-process cluster simulation (``sim/``) because this
+environment has no kind/kubectl/docker.  Semantics that matter for
+correctness are modelled: ``resourceVersion`` bumps on every write, conditional patches return
+409, binding a pod that already has a node returns 409, JSON merge patch (``None`` deletes), and
+watchers get ADDED/MODIFIED/DELETED events.  :meth:`FakeAPIServer.inject` makes the next N calls of
+an operation fail with a given HTTP code (apiserver 409/500).
+
+:func:`serve_http` exposes the fake over the REST paths :class:`~.api.RestKubeAPI` uses, so the REST
+client is tested on the wire as well.
+"""
+from __future__ import annotations
+
+import copy
+import json
+import threading
+import time
+import uuid
+from collections import defaultdict
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from typing import Any, Callable, Dict, List, Optional, Tuple
+from urllib.parse import parse_qs, unquote, urlparse
+
+from .api import ApiError, Conflict, KubeAPI, NotFound, raise_for
+from .objects import meta
+
+__all__ = ["FakeAPIServer", "serve_http"]
+
+Obj = Dict[str, Any]
+Watcher = Callable[[str, str, Obj], None]  # (event, kind, object)
+
+
+def _merge(dst: Obj, patch: Obj) -> Obj:
+    """RFC 7386 JSON merge patch."""
+    for k, v in patch.items():
+        if v is None:
+            dst.pop(k, None)
+        elif isinstance(v, dict) and isinstance(dst.get(k), dict):
+            _merge(dst[k], v)
+        else:
+            dst[k] = copy.deepcopy(v)
+    return dst
+
+
+def _match_labels(obj: Obj, selector: Optional[str]) -> bool:
+    if not selector:
+        return True
+    lb = meta(obj).get("labels") or {}
+    for term in selector.split(","):
+        term = term.strip()
+        if not term:
+            continue
+        if "!=" in term:
+            k, v = term.split("!=", 1)
+            if lb.get(k.strip()) == v.strip():
+                return False
+        elif "=" in term:
+            k, v = term.split("=", 1)
+            if lb.get(k.strip().rstrip("=")) != v.strip().lstrip("="):
+                return False
+        elif lb.get(term) is None:
+            return False
+    return True
+
+
+class FakeAPIServer(KubeAPI):
+    def __init__(self):
+        self._lock = threading.RLock()
+        self._rv = 0
+        self.nodes: Dict[str, Obj] = {}
+        self.pods: Dict[Tuple[str, str], Obj] = {}
+        self._faults: Dict[str, List[Tuple[int, int]]] = defaultdict(list)  # op -> [(code, remaining)]
+        self._watchers: List[Watcher] = []
+        self.calls: Dict[str, int] = defaultdict(int)
+        self.latency_s = 0.0
+
+    # ------------------------------------------------------------------ infrastructure
+    def _next_rv(self) -> str:
+        self._rv += 1
+        return str(self._rv)
+
+    def inject(self, op: str, code: int = 500, times: int = 1) -> None:
+        """Make the next ``times`` calls of ``op`` (method name, e.g. ``bind_pod``) fail with ``code``."""
+        with self._lock:
+            self._faults[op].append((code, times))
+
+    def _enter(self, op: str) -> None:
+        self.calls[op] += 1
+        if self.latency_s:
+            time.sleep(self.latency_s)
+        q = self._faults.get(op)
+        if q:
+            code, left = q[0]
+            if left <= 1:
+                q.pop(0)
+            else:
+                q[0] = (code, left - 1)
+            raise_for(code, f"injected fault on {op}")
+
+    def watch(self, fn: Watcher) -> None:
+        with self._lock:
+            self._watchers.append(fn)
+
+    def _emit(self, event: str, kind: str, obj: Obj) -> None:
+        for w in list(self._watchers):
+            w(event, kind, copy.deepcopy(obj))
+
+    # ------------------------------------------------------------------ object creation (tests/sim)
+    def create_node(self, node: Obj) -> Obj:
+        with self._lock:
+            node = copy.deepcopy(node)
+            md = meta(node)
+            md.setdefault("uid", str(uuid.uuid4()))
+            md["resourceVersion"] = self._next_rv()
+            self.nodes[md["name"]] = node
+            self._emit("ADDED", "Node", node)
+            return copy.deepcopy(node)
+
+    def create_pod(self, pod: Obj) -> Obj:
+        with self._lock:
+            pod = copy.deepcopy(pod)
+            md = meta(pod)
+            md.setdefault("namespace", "default")
+            md.setdefault("uid", str(uuid.uuid4()))
+            md.setdefault("creationTimestamp", time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()))
+            key = (md["namespace"], md["name"])
+            if key in self.pods:
+                raise Conflict(f"pod {key} exists")
+            md["resourceVersion"] = self._next_rv()
+            self.pods[key] = pod
+            self._emit("ADDED", "Pod", pod)
+            return copy.deepcopy(pod)
+
+    def delete_pod(self, namespace: str, name: str) -> None:
+        with self._lock:
+            pod = self.pods.pop((namespace, name), None)
+            if pod is None:
+                raise NotFound(f"pod {namespace}/{name}")
+            self._emit("DELETED", "Pod", pod)
+
+    def set_pod_phase(self, namespace: str, name: str, phase: str) -> Obj:
+        with self._lock:
+            pod = self._pod(namespace, name)
+            pod.setdefault("status", {})["phase"] = phase
+            meta(pod)["resourceVersion"] = self._next_rv()
+            self._emit("MODIFIED", "Pod", pod)
+            return copy.deepcopy(pod)
+
+    def update_node_status(self, name: str, capacity: Dict[str, str], allocatable: Optional[Dict[str, str]] = None) -> Obj:
+        """What the kubelet does after ListAndWatch (diagram step 2)."""
+        with self._lock:
+            node = self._node(name)
+            st = node.setdefault("status", {})
+            st.setdefault("capacity", {}).update(capacity)
+            st.setdefault("allocatable", {}).update(allocatable if allocatable is not None else capacity)
+            meta(node)["resourceVersion"] = self._next_rv()
+            self._emit("MODIFIED", "Node", node)
+            return copy.deepcopy(node)
+
+    # ------------------------------------------------------------------ KubeAPI
+    def _node(self, name: str) -> Obj:
+        n = self.nodes.get(name)
+        if n is None:
+            raise NotFound(f"node {name}")
+        return n
+
+    def _pod(self, namespace: str, name: str) -> Obj:
+        p = self.pods.get((namespace, name))
+        if p is None:
+            raise NotFound(f"pod {namespace}/{name}")
+        return p
+
+    def get_node(self, name: str) -> Obj:
+        with self._lock:
+            self._enter("get_node")
+            return copy.deepcopy(self._node(name))
+
+    def list_nodes(self, label_selector: Optional[str] = None) -> List[Obj]:
+        with self._lock:
+            self._enter("list_nodes")
+            return [copy.deepcopy(n) for n in self.nodes.values() if _match_labels(n, label_selector)]
+
+    def patch_node(self, name, annotations=None, labels=None) -> Obj:
+        with self._lock:
+            self._enter("patch_node")
+            node = self._node(name)
+            md: Obj = {}
+            if annotations is not None:
+                md["annotations"] = annotations
+            if labels is not None:
+                md["labels"] = labels
+            _merge(node, {"metadata": md})
+            meta(node)["resourceVersion"] = self._next_rv()
+            self._emit("MODIFIED", "Node", node)
+            return copy.deepcopy(node)
+
+    def get_pod(self, namespace: str, name: str) -> Obj:
+        with self._lock:
+            self._enter("get_pod")
+            return copy.deepcopy(self._pod(namespace, name))
+
+    def list_pods(self, node_name: Optional[str] = None, namespace: Optional[str] = None) -> List[Obj]:
+        with self._lock:
+            self._enter("list_pods")
+            out = []
+            for (ns, _), p in self.pods.items():
+                if namespace and ns != namespace:
+                    continue
+                if node_name is not None and (p.get("spec") or {}).get("nodeName", "") != node_name:
+                    continue
+                out.append(copy.deepcopy(p))
+            return out
+
+    def patch_pod_annotations(self, namespace, name, annotations, resource_version=None) -> Obj:
+        with self._lock:
+            self._enter("patch_pod_annotations")
+            pod = self._pod(namespace, name)
+            if resource_version is not None and str(resource_version) != meta(pod).get("resourceVersion"):
+                raise Conflict(f"pod {namespace}/{name}: resourceVersion {resource_version} is stale")
+            _merge(pod, {"metadata": {"annotations": annotations}})
+            meta(pod)["resourceVersion"] = self._next_rv()
+            self._emit("MODIFIED", "Pod", pod)
+            return copy.deepcopy(pod)
+
+    def bind_pod(self, namespace: str, name: str, uid: str, node: str) -> None:
+        with self._lock:
+            self._enter("bind_pod")
+            pod = self._pod(namespace, name)
+            if uid and meta(pod).get("uid") != uid:
+                raise Conflict(f"pod {namespace}/{name}: uid mismatch")
+            if (pod.get("spec") or {}).get("nodeName"):
+                raise Conflict(f"pod {namespace}/{name} is already assigned to node {pod['spec']['nodeName']}")
+            self._node(node)
+            pod.setdefault("spec", {})["nodeName"] = node
+            pod.setdefault("status", {})["phase"] = "Pending"
+            meta(pod)["resourceVersion"] = self._next_rv()
+            self._emit("MODIFIED", "Pod", pod)
+
+
+# ---------------------------------------------------------------------------------------- HTTP
+class _Handler(BaseHTTPRequestHandler):
+    api: FakeAPIServer = None  # type: ignore[assignment]
+    token: Optional[str] = None
+
+    def log_message(self, *a):  # quiet
+        pass
+
+    def _send(self, code: int, body: Obj) -> None:
+        data = json.dumps(body).encode()
+        self.send_response(code)
+        self.send_header("Content-Type", "application/json")
+        self.send_header("Content-Length", str(len(data)))
+        self.end_headers()
+        self.wfile.write(data)
+
+    def _body(self) -> Obj:
+        n = int(self.headers.get("Content-Length") or 0)
+        return json.loads(self.rfile.read(n) or b"{}")
+
+    def _route(self, method: str) -> None:
+        if self.token and self.headers.get("Authorization") != f"Bearer {self.token}":
+            return self._send(401, {"kind": "Status", "code": 401, "message": "Unauthorized"})
+        u = urlparse(self.path)
+        parts = [unquote(p) for p in u.path.strip("/").split("/")]
+        q = parse_qs(u.query)
+        try:
+            if parts[:2] != ["api", "v1"]:
+                raise NotFound(u.path)
+            rest = parts[2:]
+            if rest == ["nodes"] and method == "GET":
+                return self._send(200, {"kind": "NodeList", "items": self.api.list_nodes((q.get("labelSelector") or [None])[0])})
+            if len(rest) == 2 and rest[0] == "nodes":
+                if method == "GET":
+                    return self._send(200, self.api.get_node(rest[1]))
+                if method == "PATCH":
+                    md = self._body().get("metadata", {})
+                    return self._send(200, self.api.patch_node(rest[1], md.get("annotations"), md.get("labels")))
+            node_name = None
+            fs = (q.get("fieldSelector") or [""])[0]
+            if fs.startswith("spec.nodeName="):
+                node_name = fs.split("=", 1)[1]
+            if rest == ["pods"] and method == "GET":
+                return self._send(200, {"kind": "PodList", "items": self.api.list_pods(node_name=node_name)})
+            if len(rest) >= 3 and rest[0] == "namespaces" and rest[2] == "pods":
+                ns = rest[1]
+                if len(rest) == 3 and method == "GET":
+                    return self._send(200, {"kind": "PodList", "items": self.api.list_pods(node_name=node_name, namespace=ns)})
+                if len(rest) == 4:
+                    if method == "GET":
+                        return self._send(200, self.api.get_pod(ns, rest[3]))
+                    if method == "PATCH":
+                        md = self._body().get("metadata", {})
+                        return self._send(200, self.api.patch_pod_annotations(ns, rest[3], md.get("annotations") or {},
+                                                                            md.get("resourceVersion")))
+                if len(rest) == 5 and rest[4] == "binding" and method == "POST":
+                    b = self._body()
+                    self.api.bind_pod(ns, rest[3], (b.get("metadata") or {}).get("uid", ""), b["target"]["name"])
+                    return self._send(201, {"kind": "Status", "status": "Success", "code": 201})
+            raise NotFound(f"{method} {u.path}")
+        except ApiError as e:
+            return self._send(e.code, {"kind": "Status", "status": "Failure", "code": e.code, "message": e.message})
+
+    def do_GET(self):
+        self._route("GET")
+
+    def do_PATCH(self):
+        self._route("PATCH")
+
+    def do_POST(self):
+        self._route("POST")
+
+
+def serve_http(api: FakeAPIServer, host: str = "127.0.0.1", port: int = 0, token: Optional[str] = None):
+    """Serve ``api`` over HTTP in a daemon thread; returns ``(server, base_url)``.  ``server.shutdown()`` stops it."""
+    handler = type("FakeKubeHandler", (_Handler,), {"api": api, "token": token})
+    srv = ThreadingHTTPServer((host, port), handler)
+    srv.daemon_threads = True
+    t = threading.Thread(target=srv.serve_forever, name="fake-apiserver", daemon=True)
+    t.start()
+    return srv, f"http://{host}:{srv.server_address[1]}"

@@ -303,7 +303,9 @@ class Topology:
                     c[i, j] = RefLinkClass(int(self.ref_class[i, j])).nominal_cost()
                 else:
                     c[i, j] = default_link_cost(LinkType(int(self.link_type[i, j])), int(self.hops[i, j]))
-        c = np.maximum(c, c.T)
+        # quantised to the 1e-6 grid the JSON annotation carries, so the device plugin and the
+        # extender (which decodes the annotation) see bit-identical costs and break ties identically
+        c = np.round(np.maximum(c, c.T), 6)
         self.cost = c
         return c
 
