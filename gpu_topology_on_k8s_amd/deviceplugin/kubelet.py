@@ -1,0 +1,199 @@
+"""A fake kubelet device manager speaking the real ``v1beta1`` gRPC protocol (SURVEY.md §4 "fake kubelet").
+
+It serves ``Registration`` on ``<dir>/kubelet.sock``; when a plugin registers it dials the plugin's
+endpoint, consumes ``ListAndWatch`` (updating the node's capacity/allocatable in the fake
+apiserver, as the real kubelet does — diagram step 2), and on pod admission calls
+``GetPreferredAllocation`` + ``Allocate`` exactly like the kubelet's device manager.  ``restart()``
+wipes the socket directory like a kubelet restart so plugin re-registration can be tested.
+"""
+from __future__ import annotations
+
+import glob
+import logging
+import os
+import threading
+import time
+from concurrent import futures
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import grpc
+
+from ..k8s.objects import meta, pod_gpu_request, pod_key
+from . import proto as pb
+
+log = logging.getLogger(__name__)
+
+__all__ = ["FakeKubelet", "AdmissionError"]
+
+
+class AdmissionError(RuntimeError):
+    pass
+
+
+@dataclass
+class _Plugin:
+    resource: str
+    endpoint: str
+    channel: grpc.Channel
+    options: object
+    devices: Dict[str, str] = field(default_factory=dict)  # id -> health
+    ready: threading.Event = field(default_factory=threading.Event)
+    thread: Optional[threading.Thread] = None
+
+
+class FakeKubelet:
+    def __init__(self, socket_dir: str, node_name: str = "", api=None):
+        self.socket_dir = socket_dir
+        self.node_name = node_name
+        self.api = api
+        self.plugins: Dict[str, _Plugin] = {}
+        self.allocated: Dict[str, Dict[str, Tuple[str, ...]]] = {}  # resource -> pod key -> ids
+        self.responses: Dict[str, object] = {}  # pod key -> AllocateResponse
+        self._server: Optional[grpc.Server] = None
+        self._lock = threading.RLock()
+        self._stop = threading.Event()
+
+    @property
+    def socket(self) -> str:
+        return os.path.join(self.socket_dir, "kubelet.sock")
+
+    # ------------------------------------------------------------------ Registration service
+    def Register(self, request, context):
+        if request.version != pb.VERSION:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"unsupported version {request.version}")
+        ep = os.path.join(self.socket_dir, request.endpoint)
+        ch = grpc.insecure_channel(f"unix://{ep}")
+        old = self.plugins.get(request.resource_name)
+        p = _Plugin(resource=request.resource_name, endpoint=ep, channel=ch, options=request.options)
+        with self._lock:
+            self.plugins[request.resource_name] = p
+            self.allocated.setdefault(request.resource_name, {})
+        if old is not None:
+            old.channel.close()
+        p.thread = threading.Thread(target=self._watch, args=(p,), name=f"kubelet-law-{request.resource_name}", daemon=True)
+        p.thread.start()
+        return pb.Empty()
+
+    def _stub(self, p: _Plugin, method: str):
+        req, res, stream = pb.METHODS[f"/{pb.DEVICE_PLUGIN_SERVICE}/{method}"]
+        mk = p.channel.unary_stream if stream else p.channel.unary_unary
+        return mk(f"/{pb.DEVICE_PLUGIN_SERVICE}/{method}", request_serializer=req.SerializeToString,
+                  response_deserializer=res.FromString)
+
+    def _watch(self, p: _Plugin) -> None:
+        try:
+            for resp in self._stub(p, "ListAndWatch")(pb.Empty()):
+                with self._lock:
+                    p.devices = {d.ID: d.health for d in resp.devices}
+                p.ready.set()
+                self._update_capacity(p)
+                if self._stop.is_set():
+                    break
+        except grpc.RpcError as e:
+            if not self._stop.is_set():
+                log.info("ListAndWatch for %s ended: %s", p.resource, e.code())
+
+    def _update_capacity(self, p: _Plugin) -> None:
+        if self.api is None or not self.node_name or not hasattr(self.api, "update_node_status"):
+            return
+        healthy = sum(1 for h in p.devices.values() if h == pb.HEALTHY)
+        try:
+            self.api.update_node_status(self.node_name, {p.resource: str(len(p.devices))}, {p.resource: str(healthy)})
+        except Exception as e:  # pragma: no cover
+            log.warning("capacity update failed: %s", e)
+
+    # ------------------------------------------------------------------ lifecycle
+    def start(self) -> None:
+        os.makedirs(self.socket_dir, exist_ok=True)
+        try:
+            os.unlink(self.socket)
+        except FileNotFoundError:
+            pass
+        self._stop.clear()
+        self._server = grpc.server(futures.ThreadPoolExecutor(max_workers=4, thread_name_prefix="kubelet"))
+        h = grpc.unary_unary_rpc_method_handler(self.Register, request_deserializer=pb.RegisterRequest.FromString,
+                                                response_serializer=pb.Empty.SerializeToString)
+        self._server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(pb.REGISTRATION_SERVICE, {"Register": h}),))
+        self._server.add_insecure_port(f"unix://{self.socket}")
+        self._server.start()
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._server is not None:
+            self._server.stop(grace=0).wait()
+            self._server = None
+        for p in list(self.plugins.values()):
+            p.channel.close()
+
+    def restart(self) -> None:
+        """Like a kubelet restart: stop, wipe every socket in the directory, start again."""
+        self.stop()
+        for s in glob.glob(os.path.join(self.socket_dir, "*.sock")):
+            os.unlink(s)
+        with self._lock:
+            self.plugins.clear()
+        self.start()
+
+    def wait_for(self, resource: str, timeout: float = 10.0) -> _Plugin:
+        t0 = time.time()
+        while time.time() - t0 < timeout:
+            p = self.plugins.get(resource)
+            if p is not None and p.ready.wait(timeout=0.05):
+                return p
+            time.sleep(0.02)
+        raise TimeoutError(f"plugin for {resource} did not register/advertise within {timeout}s")
+
+    # ------------------------------------------------------------------ device manager
+    def options(self, resource: str):
+        return self._stub(self.plugins[resource], "GetDevicePluginOptions")(pb.Empty(), timeout=5)
+
+    def available(self, resource: str) -> List[str]:
+        p = self.plugins[resource]
+        with self._lock:
+            used = {i for ids in self.allocated.get(resource, {}).values() for i in ids}
+            return sorted((d for d, h in p.devices.items() if h == pb.HEALTHY and d not in used), key=int)
+
+    def admit(self, pod: dict, resource: str, container_split: Optional[Sequence[int]] = None):
+        """Allocate devices for ``pod``: GetPreferredAllocation (if offered) then Allocate."""
+        key = pod_key(pod)
+        p = self.plugins.get(resource)
+        k = pod_gpu_request(pod, [resource] + [r for r in self.plugins if r != resource])
+        if k == 0:
+            return None
+        if p is None:
+            raise AdmissionError(f"no device plugin registered for {resource}")
+        with self._lock:
+            avail = self.available(resource)
+            if len(avail) < k:
+                raise AdmissionError(f"UnexpectedAdmissionError: requested {k}, available {len(avail)}")
+            chosen: List[str] = avail[:k]
+            if getattr(p.options, "get_preferred_allocation_available", False):
+                req = pb.PreferredAllocationRequest()
+                req.container_requests.add(available_deviceIDs=avail, allocation_size=k)
+                pref = self._stub(p, "GetPreferredAllocation")(req, timeout=5)
+                ids = list(pref.container_responses[0].deviceIDs)
+                if len(ids) == k and set(ids) <= set(avail):
+                    chosen = ids
+            split = list(container_split or [k])
+            areq = pb.AllocateRequest()
+            pos = 0
+            for n in split:
+                areq.container_requests.add(devices_ids=chosen[pos:pos + n])
+                pos += n
+            resp = self._stub(p, "Allocate")(areq, timeout=10)
+            self.allocated[resource][key] = tuple(chosen)
+            self.responses[key] = resp
+        if self.api is not None and hasattr(self.api, "set_pod_phase"):
+            md = meta(pod)
+            try:
+                self.api.set_pod_phase(md.get("namespace", "default"), md["name"], "Running")
+            except Exception:  # pragma: no cover
+                pass
+        return resp
+
+    def release(self, pod: dict) -> None:
+        key = pod_key(pod)
+        with self._lock:
+            for res in self.allocated.values():
+                res.pop(key, None)

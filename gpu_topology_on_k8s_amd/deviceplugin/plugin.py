@@ -1,0 +1,378 @@
+"""kubelet device plugin advertising the MI355X devices of one node.
+
+Reference behaviour:
+  * ``design.md:57-82`` — at init, read the GPU-pair topology and publish it as node annotations
+    ``GPU_<ABBR>_<i>_<j>``.  Here the node additionally gets one JSON annotation with the measured
+    cost model and labels for the GPU model / partition mode (heterogeneous quota, Gaia B7).
+  * ``design.md:84-86`` — advertise the extended resource through ``ListAndWatch``.  Each device is
+    reported with its NUMA node (``TopologyInfo``) and live health.
+  * ``design.md:236-246`` — ``Allocate`` finds the pod the devices belong to through the pod
+    annotations, injects the devices and flips ``ALIYUN_COM_GPU_ASSIGNED=true`` with a fresh
+    ``ALIYUN_COM_GPU_ASSUME_TIME``.  Instead of ``NVIDIA_VISIBLE_DEVICES`` for nvidia-docker, the
+    container gets the ROCm device nodes: ``/dev/kfd`` plus ``/dev/dri/renderD<minor>`` (and
+    ``card<N>``) of each allocated device — plain containerd, no runtime hook.
+  * ``GetPreferredAllocation`` (kubelet API, not in the 2019 design) returns the extender's GROUP so
+    the kubelet allocates exactly the annotated devices; without an annotated pod it runs the
+    placement core itself.
+
+Pod <-> Allocate association (the kubelet does not say which pod it is allocating for, SURVEY §7.3
+#4): pending pods on this node with ``ASSIGNED=false`` are matched by exact device set first, then
+by size with the oldest ``ASSUME_TIME`` (the design's implicit scheme); a pod scheduled around the
+extender (no GROUP) is annotated with what the kubelet gave it so the extender sees the usage.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import threading
+import time
+from concurrent import futures
+from typing import Callable, Dict, Iterable, List, Optional, Sequence, Set, Tuple
+
+import grpc
+
+from ..k8s.annotations import ANN_ASSIGNED, ANN_ASSUME_TIME, ANN_GROUP, Contract, PodAssignment, encode_node_annotations, format_group
+from ..k8s.api import Conflict, KubeAPI
+from ..k8s.objects import annotations as obj_annotations
+from ..k8s.objects import meta, pod_gpu_request, pod_is_terminal, pod_phase
+from ..placement import PlacementPolicy
+from ..placement.core import select_with
+from ..topology.model import Topology
+from . import proto as pb
+
+log = logging.getLogger(__name__)
+
+__all__ = ["DevicePluginServer", "PluginConfig"]
+
+#: pod annotation whose ``KEY=VALUE`` lines are passed into the container (RCCL / NCCL tuning only)
+RCCL_ENV_ANNOTATION_SUFFIX = "rccl-env"
+_ENV_PREFIXES = ("NCCL_", "RCCL_", "HSA_", "HIP_", "GPU_MAX_HW_QUEUES")
+
+
+class PluginConfig:
+    def __init__(self, resource_name: str = "amd.com/gpu", socket_dir: str = pb.DEVICE_PLUGIN_PATH,
+                 socket_name: str = "amd-gpu-topology.sock", kubelet_socket: Optional[str] = None, dev_root: str = "/dev",
+                 node_name: str = "", contract: Optional[Contract] = None, health_interval: float = 5.0,
+                 publish_node: bool = True, pass_rccl_env: bool = True, policy: PlacementPolicy = PlacementPolicy(),
+                 resource_aliases: Sequence[str] = ("aliyun.com/gpu", "aliyun.com/gpu-count")):
+        self.resource_name = resource_name
+        self.socket_dir = socket_dir
+        self.socket_name = socket_name
+        self.kubelet_socket = kubelet_socket or os.path.join(socket_dir, "kubelet.sock")
+        self.dev_root = dev_root
+        self.node_name = node_name
+        self.contract = contract or Contract(resource_name=resource_name)
+        self.health_interval = health_interval
+        self.publish_node = publish_node
+        self.pass_rccl_env = pass_rccl_env
+        self.policy = policy
+        self.resource_aliases = tuple(resource_aliases)
+
+    @property
+    def socket_path(self) -> str:
+        return os.path.join(self.socket_dir, self.socket_name)
+
+
+class DevicePluginServer:
+    def __init__(self, topology: Topology, config: Optional[PluginConfig] = None, api: Optional[KubeAPI] = None,
+                 health_fn: Optional[Callable[[Topology], Dict[int, bool]]] = None, clock: Callable[[], float] = time.time):
+        self.cfg = config or PluginConfig()
+        self.topology = topology
+        self.api = api
+        self.health_fn = health_fn
+        self.clock = clock
+        self._health: Dict[int, bool] = {g.index: bool(g.healthy) for g in topology.gpus}
+        self._cond = threading.Condition()
+        self._version = 0
+        self._server: Optional[grpc.Server] = None
+        self._stop = threading.Event()
+        self._threads: List[threading.Thread] = []
+        self._alloc_lock = threading.Lock()
+        self.allocations: List[Tuple[str, Tuple[int, ...]]] = []  # (pod key or "", ids) log
+        self.registered = 0
+
+    # ------------------------------------------------------------------ device view
+    def devices(self) -> List[pb.Device]:
+        out = []
+        for g in self.topology.gpus:
+            d = pb.Device(ID=g.device_id, health=pb.HEALTHY if self._health.get(g.index, True) else pb.UNHEALTHY)
+            d.topology.nodes.add(ID=int(g.numa))
+            out.append(d)
+        return out
+
+    def set_health(self, index: int, healthy: bool) -> None:
+        """Fault injection / health monitor entry: re-advertise through every ListAndWatch stream."""
+        with self._cond:
+            if self._health.get(index) == healthy:
+                return
+            self._health[index] = healthy
+            self.topology.gpus[index].healthy = healthy
+            self._version += 1
+            self._cond.notify_all()
+        log.warning("device %d is now %s", index, "Healthy" if healthy else "Unhealthy")
+        self._publish_node()
+
+    def update_topology(self, topo: Topology) -> None:
+        """New probe results / partition change: re-publish and re-advertise."""
+        with self._cond:
+            self.topology = topo
+            self._health = {g.index: bool(g.healthy) for g in topo.gpus}
+            self._version += 1
+            self._cond.notify_all()
+        self._publish_node()
+
+    # ------------------------------------------------------------------ node publication (A5, B7)
+    def _publish_node(self) -> None:
+        if not (self.api is not None and self.cfg.publish_node and self.cfg.node_name):
+            return
+        t = self.topology
+        c = self.cfg.contract
+        models = sorted({g.model for g in t.gpus})
+        labels = {
+            c.label_model: models[0] if len(models) == 1 else "mixed",
+            c.label_partition: t.gpus[0].partition if t.gpus else "",
+            c.label_gfx: t.gpus[0].gfx if t.gpus else "",
+        }
+        try:
+            self.api.patch_node(self.cfg.node_name, annotations=encode_node_annotations(t, c), labels=labels)
+        except Exception as e:
+            log.warning("publishing topology on node %s failed: %s", self.cfg.node_name, e)
+
+    # ------------------------------------------------------------------ gRPC handlers
+    def GetDevicePluginOptions(self, request, context):
+        return pb.DevicePluginOptions(pre_start_required=False, get_preferred_allocation_available=True)
+
+    def ListAndWatch(self, request, context):
+        last = -1
+        while not self._stop.is_set() and context.is_active():
+            with self._cond:
+                if self._version == last:
+                    self._cond.wait(timeout=0.5)
+                    if self._version == last:
+                        continue
+                last = self._version
+                devs = self.devices()
+            yield pb.ListAndWatchResponse(devices=devs)
+
+    def GetPreferredAllocation(self, request, context):
+        resp = pb.PreferredAllocationResponse()
+        pending = self._pending_assumed()
+        for creq in request.container_requests:
+            avail = [int(x) for x in creq.available_deviceIDs]
+            must = [int(x) for x in creq.must_include_deviceIDs]
+            size = int(creq.allocation_size)
+            ids = None
+            for _, pa, _ in pending:
+                g = set(pa.group)
+                if len(g) == size and g <= set(avail) and set(must) <= g:
+                    ids = sorted(g)
+                    break
+            if ids is None:
+                ids = list(select_with(self.topology, size, avail, must, self.cfg.policy))
+            resp.container_responses.add(deviceIDs=[str(i) for i in ids])
+        return resp
+
+    def Allocate(self, request, context):
+        resp = pb.AllocateResponse()
+        all_ids: List[int] = []
+        for creq in request.container_requests:
+            ids = [int(x) for x in creq.devices_ids]
+            bad = [i for i in ids if i < 0 or i >= self.topology.n]
+            if bad:
+                context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"unknown device ids {bad}")
+            unhealthy = [i for i in ids if not self._health.get(i, True)]
+            if unhealthy:
+                context.abort(grpc.StatusCode.FAILED_PRECONDITION, f"devices {unhealthy} are unhealthy")
+            all_ids.extend(ids)
+        with self._alloc_lock:
+            pod = self._claim_pod(sorted(set(all_ids)))
+        extra_env = self._rccl_env(pod) if pod is not None else {}
+        for creq in request.container_requests:
+            ids = [int(x) for x in creq.devices_ids]
+            resp.container_responses.append(self._container_response(ids, extra_env))
+        self.allocations.append((f"{meta(pod).get('namespace')}/{meta(pod).get('name')}" if pod else "", tuple(sorted(all_ids))))
+        return resp
+
+    def PreStartContainer(self, request, context):
+        return pb.PreStartContainerResponse()
+
+    # ------------------------------------------------------------------ Allocate helpers
+    def _container_response(self, ids: Sequence[int], extra_env: Dict[str, str]) -> pb.ContainerAllocateResponse:
+        r = pb.ContainerAllocateResponse()
+        root = self.cfg.dev_root.rstrip("/")
+        r.devices.add(container_path="/dev/kfd", host_path=f"{root}/kfd", permissions="rw")
+        numa: Set[int] = set()
+        for i in ids:
+            g = self.topology.gpus[i]
+            minor = g.render_minor if g.render_minor >= 0 else 128 + i
+            r.devices.add(container_path=f"/dev/dri/renderD{minor}", host_path=f"{root}/dri/renderD{minor}", permissions="rw")
+            if g.card >= 0:
+                r.devices.add(container_path=f"/dev/dri/card{g.card}", host_path=f"{root}/dri/card{g.card}", permissions="rw")
+            numa.add(int(g.numa))
+        r.envs["GTK_GPU_GROUP"] = format_group(ids)
+        r.envs["GTK_NUMA_NODES"] = ",".join(str(x) for x in sorted(numa))
+        for k, v in extra_env.items():
+            r.envs[k] = v
+        r.annotations["gputopology.amd.com/devices"] = format_group(ids)
+        return r
+
+    def _rccl_env(self, pod: dict) -> Dict[str, str]:
+        if not self.cfg.pass_rccl_env:
+            return {}
+        raw = obj_annotations(pod).get(f"{self.cfg.contract.prefix}/{RCCL_ENV_ANNOTATION_SUFFIX}", "")
+        env = {}
+        for line in raw.replace(";", "\n").splitlines():
+            if "=" not in line:
+                continue
+            k, v = line.split("=", 1)
+            k = k.strip()
+            if k.startswith(_ENV_PREFIXES):
+                env[k] = v.strip()
+        return env
+
+    def _node_pods(self) -> List[dict]:
+        if self.api is None or not self.cfg.node_name:
+            return []
+        try:
+            return [p for p in self.api.list_pods(node_name=self.cfg.node_name) if not pod_is_terminal(p)]
+        except Exception as e:
+            log.warning("listing pods on %s failed: %s", self.cfg.node_name, e)
+            return []
+
+    def _pending_assumed(self) -> List[Tuple[dict, PodAssignment, float]]:
+        out = []
+        for p in self._node_pods():
+            pa = PodAssignment.from_annotations(obj_annotations(p))
+            if pa is not None and not pa.assigned and pod_phase(p) == "Pending":
+                out.append((p, pa, float(pa.assume_time)))
+        out.sort(key=lambda x: (x[2], meta(x[0]).get("creationTimestamp", ""), meta(x[0]).get("name", "")))
+        return out
+
+    def _claim_pod(self, ids: List[int]) -> Optional[dict]:
+        """Find the pod these devices are for and flip it to ASSIGNED=true (conditional patch)."""
+        if self.api is None or not self.cfg.node_name:
+            return None
+        for attempt in range(5):
+            cands = self._pending_assumed()
+            exact = [c for c in cands if sorted(set(c[1].group)) == ids]
+            sized = [c for c in cands if len(set(c[1].group)) == len(ids)]
+            pod: Optional[dict] = None
+            if exact:
+                pod = exact[0][0]
+            elif sized:
+                pod = sized[0][0]  # oldest ASSUME_TIME with the same count (design's implicit rule)
+                log.warning("kubelet allocated %s but pod %s was assumed %s; recording what the kubelet chose",
+                            ids, meta(pod).get("name"), sized[0][1].group)
+            else:
+                pod = self._unannotated_pod(len(ids))
+                if pod is None:
+                    log.warning("no pending pod on %s matches allocation %s", self.cfg.node_name, ids)
+                    return None
+            now = int(self.clock())
+            ann = {ANN_GROUP: format_group(ids), ANN_ASSIGNED: "true", ANN_ASSUME_TIME: str(now)}
+            md = meta(pod)
+            try:
+                return self.api.patch_pod_annotations(md.get("namespace", "default"), md["name"], ann,
+                                                      resource_version=md.get("resourceVersion"))
+            except Conflict:
+                continue  # someone else touched the pod: re-read and retry
+            except Exception as e:
+                log.warning("flipping %s/%s to ASSIGNED=true failed: %s", md.get("namespace"), md.get("name"), e)
+                return pod
+        return None
+
+    def _unannotated_pod(self, k: int) -> Optional[dict]:
+        names = (self.cfg.resource_name,) + tuple(a for a in self.cfg.resource_aliases if a != self.cfg.resource_name)
+        cands = []
+        for p in self._node_pods():
+            if PodAssignment.from_annotations(obj_annotations(p)) is not None or pod_phase(p) != "Pending":
+                continue
+            try:
+                if pod_gpu_request(p, names) == k:
+                    cands.append(p)
+            except ValueError:
+                continue
+        cands.sort(key=lambda p: (meta(p).get("creationTimestamp", ""), meta(p).get("name", "")))
+        return cands[0] if cands else None
+
+    # ------------------------------------------------------------------ lifecycle
+    def _handlers(self):
+        svc = pb.DEVICE_PLUGIN_SERVICE
+        h = {}
+        for path, (req, res, stream) in pb.METHODS.items():
+            if not path.startswith(f"/{svc}/"):
+                continue
+            name = path.rsplit("/", 1)[1]
+            fn = getattr(self, name)
+            mk = grpc.unary_stream_rpc_method_handler if stream else grpc.unary_unary_rpc_method_handler
+            h[name] = mk(fn, request_deserializer=req.FromString, response_serializer=res.SerializeToString)
+        return grpc.method_handlers_generic_handler(svc, h)
+
+    def serve(self) -> None:
+        os.makedirs(self.cfg.socket_dir, exist_ok=True)
+        try:
+            os.unlink(self.cfg.socket_path)
+        except FileNotFoundError:
+            pass
+        self._server = grpc.server(futures.ThreadPoolExecutor(max_workers=16, thread_name_prefix="devplugin"))
+        self._server.add_generic_rpc_handlers((self._handlers(),))
+        self._server.add_insecure_port(f"unix://{self.cfg.socket_path}")
+        self._server.start()
+        log.info("device plugin serving %s on %s", self.cfg.resource_name, self.cfg.socket_path)
+
+    def register(self, timeout: float = 10.0) -> None:
+        with grpc.insecure_channel(f"unix://{self.cfg.kubelet_socket}") as ch:
+            grpc.channel_ready_future(ch).result(timeout=timeout)
+            call = ch.unary_unary(f"/{pb.REGISTRATION_SERVICE}/Register", request_serializer=pb.RegisterRequest.SerializeToString,
+                                  response_deserializer=pb.Empty.FromString)
+            call(pb.RegisterRequest(version=pb.VERSION, endpoint=self.cfg.socket_name, resource_name=self.cfg.resource_name,
+                                    options=pb.DevicePluginOptions(pre_start_required=False,
+                                                                   get_preferred_allocation_available=True)),
+                 timeout=timeout)
+        self.registered += 1
+        log.info("registered %s with kubelet at %s", self.cfg.resource_name, self.cfg.kubelet_socket)
+
+    def start(self, register: bool = True) -> None:
+        self._stop.clear()
+        self._publish_node()
+        self.serve()
+        if register:
+            self.register()
+        self._threads = [threading.Thread(target=self._monitor, name="devplugin-monitor", daemon=True)]
+        for t in self._threads:
+            t.start()
+
+    def _monitor(self) -> None:
+        """Health polling + kubelet restart detection (the kubelet wipes plugin sockets on restart)."""
+        next_health = 0.0
+        while not self._stop.wait(0.2):
+            if not os.path.exists(self.cfg.socket_path):
+                log.warning("plugin socket %s vanished (kubelet restart?): re-serving and re-registering", self.cfg.socket_path)
+                try:
+                    if self._server is not None:
+                        self._server.stop(grace=0)
+                    self.serve()
+                    self.register()
+                except Exception as e:
+                    log.warning("re-registration failed, will retry: %s", e)
+            if self.health_fn is not None and time.monotonic() >= next_health:
+                next_health = time.monotonic() + self.cfg.health_interval
+                try:
+                    for idx, ok in self.health_fn(self.topology).items():
+                        self.set_health(int(idx), bool(ok))
+                except Exception as e:
+                    log.warning("health check failed: %s", e)
+
+    def stop(self) -> None:
+        self._stop.set()
+        with self._cond:
+            self._cond.notify_all()
+        if self._server is not None:
+            self._server.stop(grace=0.5).wait()
+            self._server = None
+        for t in self._threads:
+            t.join(timeout=2)
+        try:
+            os.unlink(self.cfg.socket_path)
+        except FileNotFoundError:
+            pass

@@ -296,3 +296,36 @@ def worst(topo: Topology, k: int, used: Sequence[int] = (), policy: PlacementPol
             bj, bc = j, comb
     j, terms = evaluate(p, bc, policy, stats)
     return Placement(ids=tuple(bc), objective=j, score=score_from_objective(j), comm=terms["comm"], terms=terms)
+
+
+def select_with(topo: Topology, k: int, available: Sequence[int], must_include: Sequence[int] = (),
+                policy: PlacementPolicy = PlacementPolicy()) -> Tuple[int, ...]:
+    """Best ``k`` devices drawn from ``available`` that contain ``must_include`` (kubelet
+    ``GetPreferredAllocation`` semantics).  Devices outside ``available`` are treated as used."""
+    avail = sorted({int(a) for a in available})
+    must = sorted({int(m) for m in must_include})
+    if not set(must) <= set(avail):
+        raise NoFeasiblePlacement(f"must-include devices {must} are not all available")
+    if len(avail) < k or len(must) > k:
+        raise NoFeasiblePlacement(f"need {k} of {len(avail)} available devices (must include {must})")
+    used = [i for i in range(topo.n) if i not in set(avail)]
+    if not must:
+        return select(topo, k, used=used, policy=policy).ids
+    p = Problem.from_topology(topo, used)
+    rest = [a for a in avail if a not in set(must) and p.free[a]]
+    r = k - len(must)
+    stats = _level_stats(p)
+    if math.comb(len(rest), r) <= policy.exact_limit:
+        best, bj = None, math.inf
+        for comb in itertools.combinations(rest, r):
+            cand = tuple(sorted(must + list(comb)))
+            j, _ = evaluate(p, cand, policy, stats)
+            if j < bj - EPS:
+                best, bj = cand, j
+        assert best is not None
+        return best
+    cur = list(must)  # greedy growth around the mandatory devices
+    while len(cur) < k:
+        c = min((x for x in rest if x not in cur), key=lambda x: evaluate(p, cur + [x], policy, stats)[0])
+        cur.append(c)
+    return tuple(sorted(cur))

@@ -1,0 +1,189 @@
+"""Device plugin against the fake kubelet over real gRPC unix sockets (SURVEY.md §4 "Unit: device plugin")."""
+import shutil
+import tempfile
+import time
+
+import grpc
+import pytest
+
+from gpu_topology_on_k8s_amd.deviceplugin import DevicePluginServer, FakeKubelet, PluginConfig
+from gpu_topology_on_k8s_amd.deviceplugin import proto as pb
+from gpu_topology_on_k8s_amd.extender import ExtenderConfig, TopologyExtender
+from gpu_topology_on_k8s_amd.k8s import ANN_ASSIGNED, ANN_ASSUME_TIME, ANN_GROUP, Contract, FakeAPIServer, PodAssignment
+from gpu_topology_on_k8s_amd.k8s.objects import make_node, make_pod
+from gpu_topology_on_k8s_amd.topology import fixtures as fx
+
+RES = "amd.com/gpu"
+
+
+@pytest.fixture
+def sockdir():
+    d = tempfile.mkdtemp(prefix="gtkdp", dir="/tmp")  # unix socket paths must stay < 108 bytes
+    yield d
+    shutil.rmtree(d, ignore_errors=True)
+
+
+@pytest.fixture
+def node(sockdir):
+    api = FakeAPIServer()
+    api.create_node(make_node("n1"))
+    kubelet = FakeKubelet(sockdir, node_name="n1", api=api)
+    kubelet.start()
+    topo = fx.f7_mi355x()
+    plugin = DevicePluginServer(topo, PluginConfig(resource_name=RES, socket_dir=sockdir, node_name="n1"), api=api)
+    plugin.start()
+    kubelet.wait_for(RES)
+    yield api, kubelet, plugin, topo
+    plugin.stop()
+    kubelet.stop()
+
+
+def _wait(pred, timeout=5.0):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        if pred():
+            return True
+        time.sleep(0.02)
+    return False
+
+
+def test_register_and_list_and_watch(node):
+    api, kubelet, plugin, topo = node
+    p = kubelet.plugins[RES]
+    assert sorted(p.devices, key=int) == [str(i) for i in range(8)]
+    assert set(p.devices.values()) == {pb.HEALTHY}
+    opts = kubelet.options(RES)
+    assert opts.get_preferred_allocation_available and not opts.pre_start_required
+    n = api.get_node("n1")
+    assert n["status"]["capacity"][RES] == "8"  # kubelet published capacity (diagram step 2)
+    c = Contract(resource_name=RES)
+    assert n["metadata"]["annotations"]["GPU_XGMI_0_1"] == "xGMI 1 hop"  # design.md:76-82 shape
+    assert c.topology_key in n["metadata"]["annotations"]
+    assert n["metadata"]["labels"][c.label_model] == "MI355X"
+
+
+def test_device_numa_topology_reported(node):
+    _, _, plugin, _ = node
+    devs = plugin.devices()
+    assert [d.topology.nodes[0].ID for d in devs] == [0, 0, 0, 0, 1, 1, 1, 1]
+
+
+def test_health_change_is_streamed(node):
+    api, kubelet, plugin, _ = node
+    plugin.set_health(5, False)
+    assert _wait(lambda: kubelet.plugins[RES].devices.get("5") == pb.UNHEALTHY)
+    assert _wait(lambda: api.get_node("n1")["status"]["allocatable"][RES] == "7")
+    assert "5" not in kubelet.available(RES)
+    plugin.set_health(5, True)
+    assert _wait(lambda: kubelet.plugins[RES].devices.get("5") == pb.HEALTHY)
+
+
+def test_allocate_follows_extender_group_and_flips_assigned(node):
+    """design.md:236-246: Allocate reads GROUP, injects devices, sets ASSIGNED=true + fresh ASSUME_TIME."""
+    api, kubelet, plugin, topo = node
+    ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+    pod = api.create_pod(make_pod("train", gpus=4))
+    d = ext.bind("default", "train", pod["metadata"]["uid"], "n1")
+    pod = api.get_pod("default", "train")
+    resp = kubelet.admit(pod, RES)
+    assert kubelet.allocated[RES]["default/train"] == tuple(str(i) for i in d.ids)  # preferred == GROUP
+    c = resp.container_responses[0]
+    paths = [x.container_path for x in c.devices]
+    assert paths[0] == "/dev/kfd"
+    for i in d.ids:
+        assert f"/dev/dri/renderD{128 + i}" in paths and f"/dev/dri/card{i}" in paths
+    assert all(x.permissions == "rw" for x in c.devices)
+    assert c.envs["GTK_GPU_GROUP"] == ",".join(map(str, d.ids))
+    assert "NVIDIA_VISIBLE_DEVICES" not in c.envs
+    ann = api.get_pod("default", "train")["metadata"]["annotations"]
+    assert ann[ANN_ASSIGNED] == "true" and ann[ANN_GROUP] == ",".join(map(str, d.ids))
+    assert int(ann[ANN_ASSUME_TIME]) > 0
+
+
+def test_preferred_allocation_without_pod_uses_placement_core(node):
+    _, kubelet, plugin, _ = node
+    req = pb.PreferredAllocationRequest()
+    req.container_requests.add(available_deviceIDs=[str(i) for i in range(8)], allocation_size=4)
+    req.container_requests.add(available_deviceIDs=["1", "2", "5", "6"], must_include_deviceIDs=["5"], allocation_size=2)
+    resp = kubelet._stub(kubelet.plugins[RES], "GetPreferredAllocation")(req, timeout=5)
+    assert list(resp.container_responses[0].deviceIDs) in (["0", "1", "2", "3"], ["4", "5", "6", "7"])
+    assert list(resp.container_responses[1].deviceIDs) == ["5", "6"]
+
+
+def test_allocate_for_pod_scheduled_around_extender(node):
+    api, kubelet, plugin, _ = node
+    pod = api.create_pod(make_pod("legacy", gpus=2, node="n1"))
+    kubelet.admit(pod, RES)
+    ann = api.get_pod("default", "legacy")["metadata"]["annotations"]
+    pa = PodAssignment.from_annotations(ann)
+    assert pa.assigned and len(pa.group) == 2  # recorded so the extender sees the usage
+
+
+def test_allocate_rejects_unknown_and_unhealthy(node):
+    _, kubelet, plugin, _ = node
+    stub = kubelet._stub(kubelet.plugins[RES], "Allocate")
+    req = pb.AllocateRequest()
+    req.container_requests.add(devices_ids=["42"])
+    with pytest.raises(grpc.RpcError) as ei:
+        stub(req, timeout=5)
+    assert ei.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+    plugin.set_health(0, False)
+    req = pb.AllocateRequest()
+    req.container_requests.add(devices_ids=["0"])
+    with pytest.raises(grpc.RpcError) as ei:
+        stub(req, timeout=5)
+    assert ei.value.code() == grpc.StatusCode.FAILED_PRECONDITION
+
+
+def test_multi_container_pod(node):
+    api, kubelet, plugin, _ = node
+    ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+    pod = make_pod("mc", gpus=0, containers=2)
+    for c in pod["spec"]["containers"]:
+        c["resources"] = {"limits": {RES: "2"}}
+    pod = api.create_pod(pod)
+    d = ext.bind("default", "mc", pod["metadata"]["uid"], "n1")
+    assert len(d.ids) == 4
+    resp = kubelet.admit(api.get_pod("default", "mc"), RES, container_split=[2, 2])
+    assert len(resp.container_responses) == 2
+    assert PodAssignment.from_annotations(api.get_pod("default", "mc")["metadata"]["annotations"]).assigned
+
+
+def test_rccl_env_passthrough(node):
+    api, kubelet, plugin, _ = node
+    c = Contract(resource_name=RES)
+    pod = api.create_pod(make_pod("env", gpus=1, node="n1", annotations={
+        f"{c.prefix}/rccl-env": "NCCL_MIN_NCHANNELS=32\nLD_PRELOAD=/evil.so\nRCCL_MSCCL_ENABLE=0",
+        **PodAssignment.assumed([3], 1).to_annotations()}))
+    resp = kubelet.admit(pod, RES)
+    envs = resp.container_responses[0].envs
+    assert envs["NCCL_MIN_NCHANNELS"] == "32" and envs["RCCL_MSCCL_ENABLE"] == "0"
+    assert "LD_PRELOAD" not in envs  # only RCCL/HIP tuning variables pass
+
+
+def test_kubelet_restart_triggers_reregistration(node):
+    api, kubelet, plugin, _ = node
+    assert plugin.registered == 1
+    kubelet.restart()
+    assert _wait(lambda: plugin.registered >= 2, timeout=10)
+    kubelet.wait_for(RES)
+    assert len(kubelet.plugins[RES].devices) == 8
+
+
+def test_health_fn_polling(sockdir):
+    api = FakeAPIServer()
+    api.create_node(make_node("n2"))
+    kubelet = FakeKubelet(sockdir, node_name="n2", api=api)
+    kubelet.start()
+    state = {2: True}
+    plugin = DevicePluginServer(fx.f7_mi355x(n=4), PluginConfig(resource_name=RES, socket_dir=sockdir, node_name="n2",
+                                                                 health_interval=0.05),
+                                api=api, health_fn=lambda t: dict(state))
+    plugin.start()
+    try:
+        kubelet.wait_for(RES)
+        state[2] = False  # e.g. amdsmi reports an xGMI/RAS fault
+        assert _wait(lambda: kubelet.plugins[RES].devices.get("2") == pb.UNHEALTHY)
+    finally:
+        plugin.stop()
+        kubelet.stop()
