@@ -1,0 +1,275 @@
+"""In-process Kubernetes cluster: fake apiserver + mini kube-scheduler + extender (HTTP) + per-node
+fake kubelet and real device plugin over gRPC (SURVEY.md §4 "Integration: cluster in a process",
+§7.1 step 8).
+
+It drives the reference's 7-step flow end to end (``imgs/gpu_topology_on_k8s.png``):
+  1-2. each node's device plugin registers with its kubelet, ListAndWatch -> node capacity;
+       the plugin publishes the topology annotations (design.md:76-86);
+  3.   the mini scheduler filters by extended-resource fit (the default scheduler's job,
+       design.md:117), then POSTs ``{prefix}/sort`` to the extender and picks the best node;
+  4-5. it POSTs ``{prefix}/bind``; the extender writes GROUP/ASSIGNED/ASSUME_TIME and binds;
+  6-7. the node's kubelet admits the pod: GetPreferredAllocation + Allocate over gRPC; the plugin
+       flips ASSIGNED=true and returns the device nodes.
+Used for BASELINE config 1 (2 fake GPUs, 1-GPU pod), config 4 (two concurrent 4-GPU pods),
+restart recovery, fault injection and the scheduling-latency benchmark.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import shutil
+import tempfile
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import requests
+from aiohttp import web
+
+from ..deviceplugin import DevicePluginServer, FakeKubelet, PluginConfig
+from ..extender import ExtenderConfig, TopologyExtender
+from ..extender.server import DEFAULT_PREFIX, make_app
+from ..k8s import Contract, FakeAPIServer, PodAssignment
+from ..k8s.objects import annotations as obj_annotations
+from ..k8s.objects import make_node, make_pod, meta, pod_gpu_request, pod_is_terminal, pod_key, pod_node
+from ..placement import PlacementPolicy
+from ..topology.model import Topology
+
+log = logging.getLogger(__name__)
+
+__all__ = ["SimCluster", "ScheduleResult", "HttpExtender"]
+
+
+class HttpExtender:
+    """Run the aiohttp extender app on 127.0.0.1:<ephemeral> in a background event-loop thread."""
+
+    def __init__(self, ext: TopologyExtender, prefix: str = DEFAULT_PREFIX):
+        self.ext = ext
+        self.prefix = prefix
+        self.port = 0
+        self._loop: Optional[asyncio.AbstractEventLoop] = None
+        self._runner: Optional[web.AppRunner] = None
+        self._ready = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+
+    @property
+    def url(self) -> str:
+        return f"http://127.0.0.1:{self.port}{self.prefix}"
+
+    def start(self) -> None:
+        def run():
+            self._loop = asyncio.new_event_loop()
+            asyncio.set_event_loop(self._loop)
+
+            async def up():
+                self._runner = web.AppRunner(make_app(self.ext, self.prefix), access_log=None)
+                await self._runner.setup()
+                site = web.TCPSite(self._runner, "127.0.0.1", 0)
+                await site.start()
+                self.port = site._server.sockets[0].getsockname()[1]  # type: ignore[union-attr]
+
+            self._loop.run_until_complete(up())
+            self._ready.set()
+            self._loop.run_forever()
+
+        self._thread = threading.Thread(target=run, name="sim-extender", daemon=True)
+        self._thread.start()
+        if not self._ready.wait(10):
+            raise RuntimeError("extender HTTP server did not start")
+
+    def stop(self) -> None:
+        if self._loop is None:
+            return
+
+        async def down():
+            if self._runner is not None:
+                await self._runner.cleanup()
+
+        asyncio.run_coroutine_threadsafe(down(), self._loop).result(10)
+        self._loop.call_soon_threadsafe(self._loop.stop)
+        if self._thread is not None:
+            self._thread.join(5)
+        self._loop = None
+
+
+@dataclass
+class ScheduleResult:
+    pod: str
+    node: Optional[str]
+    devices: Tuple[int, ...] = ()
+    score: int = 0
+    error: str = ""
+    sched_ms: float = 0.0  # filter + sort + bind (the paper's "scheduling time", Fig. 10)
+    admit_ms: float = 0.0  # kubelet GetPreferredAllocation + Allocate
+    allocated: Tuple[int, ...] = ()
+
+
+@dataclass
+class _Node:
+    name: str
+    topology: Topology
+    sockdir: str
+    kubelet: FakeKubelet
+    plugin: DevicePluginServer
+
+
+class SimCluster:
+    def __init__(self, nodes: Dict[str, Topology], resource: str = "amd.com/gpu", policy_name: str = "exact",
+                 policy: PlacementPolicy = PlacementPolicy(), assume_ttl: float = 300.0, use_filter: bool = True,
+                 node_labels: Optional[Dict[str, Dict[str, str]]] = None):
+        self.resource = resource
+        self.contract = Contract(resource_name=resource)
+        self.api = FakeAPIServer()
+        self.ext_cfg = ExtenderConfig(contract=self.contract, policy_name=policy_name, policy=policy, assume_ttl=assume_ttl,
+                                      resync_s=0.0)
+        self.use_filter = use_filter
+        self._root = tempfile.mkdtemp(prefix="gtksim", dir="/tmp")
+        self.nodes: Dict[str, _Node] = {}
+        self._topologies = dict(nodes)
+        self._labels = node_labels or {}
+        self.extender: Optional[TopologyExtender] = None
+        self.http: Optional[HttpExtender] = None
+        self._session = requests.Session()
+        self.history: List[ScheduleResult] = []
+
+    # ------------------------------------------------------------------ lifecycle
+    def start(self) -> "SimCluster":
+        for i, (name, topo) in enumerate(self._topologies.items()):
+            self.api.create_node(make_node(name, labels=self._labels.get(name)))
+            sockdir = os.path.join(self._root, f"n{i}")
+            kubelet = FakeKubelet(sockdir, node_name=name, api=self.api)
+            kubelet.start()
+            plugin = DevicePluginServer(topo, PluginConfig(resource_name=self.resource, socket_dir=sockdir, node_name=name,
+                                                           contract=self.contract), api=self.api)
+            plugin.start()
+            kubelet.wait_for(self.resource)
+            self.nodes[name] = _Node(name, topo, sockdir, kubelet, plugin)
+        self.start_extender()
+        return self
+
+    def start_extender(self) -> None:
+        self.extender = TopologyExtender(self.api, self.ext_cfg)
+        self.http = HttpExtender(self.extender)
+        self.http.start()
+
+    def restart_extender(self) -> None:
+        """Stateless restart: the new process rebuilds from annotations."""
+        if self.http is not None:
+            self.http.stop()
+        self.start_extender()
+
+    def stop(self) -> None:
+        if self.http is not None:
+            self.http.stop()
+        for n in self.nodes.values():
+            n.plugin.stop()
+            n.kubelet.stop()
+        shutil.rmtree(self._root, ignore_errors=True)
+
+    def __enter__(self) -> "SimCluster":
+        return self.start()
+
+    def __exit__(self, *exc) -> None:
+        self.stop()
+
+    # ------------------------------------------------------------------ workload
+    def submit(self, name: str, gpus: int, namespace: str = "default", **kw) -> dict:
+        return self.api.create_pod(make_pod(name, gpus=gpus, namespace=namespace, resource=self.resource, **kw))
+
+    def complete(self, name: str, namespace: str = "default", phase: str = "Succeeded") -> None:
+        pod = self.api.get_pod(namespace, name)
+        self.api.set_pod_phase(namespace, name, phase)
+        n = self.nodes.get(pod_node(pod))
+        if n is not None:
+            n.kubelet.release(pod)
+
+    def delete(self, name: str, namespace: str = "default") -> None:
+        pod = self.api.get_pod(namespace, name)
+        self.api.delete_pod(namespace, name)
+        n = self.nodes.get(pod_node(pod))
+        if n is not None:
+            n.kubelet.release(pod)
+
+    # ------------------------------------------------------------------ mini kube-scheduler
+    def _fits(self, pod: dict) -> List[str]:
+        """Default NodeResourcesFit on the extended resource (design.md:117)."""
+        k = pod_gpu_request(pod, [self.resource])
+        pods = self.api.list_pods()
+        out = []
+        for node in self.api.list_nodes():
+            name = meta(node)["name"]
+            alloc = int(float(((node.get("status") or {}).get("allocatable") or {}).get(self.resource, 0)))
+            used = sum(pod_gpu_request(p, [self.resource]) for p in pods if pod_node(p) == name and not pod_is_terminal(p))
+            if k == 0 or alloc - used >= k:
+                out.append(name)
+        return out
+
+    def _post(self, verb: str, body: dict):
+        assert self.http is not None
+        r = self._session.post(f"{self.http.url}/{verb}", json=body, timeout=30)
+        r.raise_for_status()
+        return r.json()
+
+    def schedule_one(self, pod: dict, admit: bool = True) -> ScheduleResult:
+        key = pod_key(pod)
+        t0 = time.perf_counter()
+        cands = self._fits(pod)
+        res = ScheduleResult(pod=key, node=None)
+        if cands and self.use_filter:
+            fr = self._post("filter", {"Pod": pod, "NodeNames": cands})
+            cands = fr.get("NodeNames") or []
+        if not cands:
+            res.error = "no feasible node"
+            res.sched_ms = (time.perf_counter() - t0) * 1e3
+            self.history.append(res)
+            return res
+        prio = self._post("sort", {"Pod": pod, "NodeNames": cands})
+        best = max(prio, key=lambda h: (h["Score"], -cands.index(h["Host"])))
+        md = meta(pod)
+        br = self._post("bind", {"PodName": md["name"], "PodNamespace": md.get("namespace", "default"), "PodUID": md.get("uid", ""),
+                                 "Node": best["Host"]})
+        res.sched_ms = (time.perf_counter() - t0) * 1e3
+        if br.get("Error"):
+            res.error = br["Error"]
+            self.history.append(res)
+            return res
+        res.node = best["Host"]
+        res.score = int(best["Score"])
+        res.devices = tuple(br.get("Devices") or ())
+        if admit:
+            t1 = time.perf_counter()
+            bound = self.api.get_pod(md.get("namespace", "default"), md["name"])
+            self.nodes[res.node].kubelet.admit(bound, self.resource)
+            res.admit_ms = (time.perf_counter() - t1) * 1e3
+            res.allocated = tuple(int(i) for i in self.nodes[res.node].kubelet.allocated[self.resource][key])
+        self.history.append(res)
+        return res
+
+    def pending(self) -> List[dict]:
+        return [p for p in self.api.list_pods() if not pod_node(p) and not pod_is_terminal(p)]
+
+    def schedule_pending(self, admit: bool = True, concurrent: bool = False) -> List[ScheduleResult]:
+        pods = sorted(self.pending(), key=lambda p: (meta(p).get("creationTimestamp", ""), int(meta(p).get("resourceVersion", 0))))
+        if not concurrent:
+            return [self.schedule_one(p, admit) for p in pods]
+        out: Dict[str, ScheduleResult] = {}
+
+        def go(p):
+            out[pod_key(p)] = self.schedule_one(p, admit)
+
+        ts = [threading.Thread(target=go, args=(p,)) for p in pods]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        return [out[pod_key(p)] for p in pods]
+
+    # ------------------------------------------------------------------ views
+    def assignment(self, name: str, namespace: str = "default") -> Optional[PodAssignment]:
+        return PodAssignment.from_annotations(obj_annotations(self.api.get_pod(namespace, name)))
+
+    def used_devices(self, node: str) -> List[int]:
+        assert self.extender is not None
+        return sorted(self.extender.cache.refresh_node(node).used(time.time(), self.ext_cfg.assume_ttl))
