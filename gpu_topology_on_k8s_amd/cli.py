@@ -1,0 +1,182 @@
+"""``python -m gpu_topology_on_k8s_amd <command>`` — operator tool.
+
+  topo      discover the node (amdsmi / sysfs / fake) and print the matrix, JSON or annotations
+  probe     run the HIP link probe (MFMA warm-up + LDS-staged copies) and print GB/s / cost
+  select    run the placement core on a topology (file, discovery or fake) for k devices
+  config    emit the scheduler config: ``scheduler`` (KubeSchedulerConfiguration), ``policy``
+            (the reference's legacy Policy JSON, design.md:92-113) or ``manifests`` (deploy YAML)
+  validate  RCCL all-reduce over the allocated devices (GTK_GPU_GROUP or --devices): the
+            placement validator of SURVEY.md §3.5 (flow step 8)
+  sim       run a small in-process cluster and print the scheduling decisions
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+from typing import List, Optional
+
+import yaml
+
+
+def _topology(a):
+    from .topology.discovery import discover
+    from .topology.model import Topology
+
+    if getattr(a, "topology", None):
+        with open(a.topology) as f:
+            return Topology.from_json(f.read())
+    return discover(a.discovery, fake_n=a.fake_gpus)
+
+
+def _ints(s: Optional[str]) -> List[int]:
+    return [int(x) for x in s.split(",") if x.strip()] if s else []
+
+
+def cmd_topo(a) -> int:
+    from .k8s.annotations import Contract, encode_node_annotations
+
+    t = _topology(a)
+    if a.output == "json":
+        print(t.to_json(indent=None))
+    elif a.output == "annotations":
+        print(json.dumps(encode_node_annotations(t, Contract(resource_name=a.resource_name)), indent=1))
+    else:
+        print(f"{t.n} devices via {t.source}")
+        print(t.render())
+    return 0
+
+
+def cmd_probe(a) -> int:
+    from .ops.probe import probe_topology
+
+    t = _topology(a)
+    probe_topology(t, preset=a.preset, mode=a.mode)
+    print(t.render())
+    print(json.dumps({"probe": t.probe, "hbm_gbps": [None if x != x else round(float(x), 1) for x in t.hbm_gbps]}))
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(t.to_json())
+    return 0
+
+
+def cmd_select(a) -> int:
+    from .placement import PlacementPolicy, select, worst
+    from .placement.gaia import gaia_schedule, tree_from_topology
+
+    t = _topology(a)
+    used = _ints(a.used)
+    if a.policy == "gaia":
+        ids = gaia_schedule(tree_from_topology(t, used), a.k)
+        print(json.dumps({"ids": ids, "policy": "gaia"}))
+        return 0
+    pl = select(t, a.k, used=used, policy=PlacementPolicy())
+    out = {"ids": list(pl.ids), "score": round(pl.score, 4), "objective": round(pl.objective, 6), "exact": pl.exact,
+           "terms": {k: round(v, 6) for k, v in pl.terms.items()}}
+    if a.worst:
+        w = worst(t, a.k, used=used)
+        out["worst"] = {"ids": list(w.ids), "score": round(w.score, 4)}
+    print(json.dumps(out))
+    return 0
+
+
+def cmd_config(a) -> int:
+    from .config import legacy_policy, render_manifests, scheduler_configuration
+
+    if a.kind == "policy":
+        print(json.dumps(legacy_policy(a.resource_name, with_filter=a.filter), indent=2))
+    elif a.kind == "scheduler":
+        print(yaml.safe_dump(scheduler_configuration(a.resource_name, with_filter=a.filter), sort_keys=False), end="")
+    else:
+        print(render_manifests(a.resource_name, image=a.image), end="")
+    return 0
+
+
+def cmd_validate(a) -> int:
+    from ._native import load
+
+    devs = _ints(a.devices) or _ints(os.environ.get("GTK_GPU_GROUP", ""))
+    if not devs:
+        import torch
+
+        devs = list(range(torch.cuda.device_count()))
+    rccl = load("_rccl")
+    sizes = rccl.size_sweep(a.min_bytes, a.max_bytes, a.factor)
+    pts = rccl.local_sweep(devs, sizes, a.dtype, a.iters, a.warmup, False, True)
+    wrong = sum(p["wrong"] for p in pts)
+    peak = max(pts, key=lambda p: p["busbw_gbps"] if len(devs) > 1 else p["algbw_gbps"])
+    for p in pts:
+        print(json.dumps({"k": len(devs), "devices": devs, **p}))
+    print(json.dumps({"summary": True, "k": len(devs), "devices": devs, "wrong": wrong, "peak_bytes": peak["bytes"],
+                      "peak_algbw_gbps": round(peak["algbw_gbps"], 2), "peak_busbw_gbps": round(peak["busbw_gbps"], 2)}))
+    return 1 if wrong else 0
+
+
+def cmd_sim(a) -> int:
+    from .sim import SimCluster
+    from .topology import fixtures as fx
+
+    with SimCluster({f"node{i}": fx.f7_mi355x(link_gbps=76.5, noise=0.03, seed=i) for i in range(a.nodes)},
+                    policy_name=a.policy) as c:
+        for i, k in enumerate(_ints(a.pods)):
+            c.submit(f"pod{i}-{k}gpu", k)
+        for r in c.schedule_pending():
+            print(json.dumps({"pod": r.pod, "node": r.node, "devices": list(r.allocated), "score": r.score,
+                              "sched_ms": round(r.sched_ms, 3), "admit_ms": round(r.admit_ms, 3), "error": r.error}))
+    return 0
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="gtk", description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    sub = ap.add_subparsers(dest="cmd", required=True)
+
+    def disc(p):
+        p.add_argument("--discovery", default="auto", choices=["auto", "amdsmi", "sysfs", "fake"])
+        p.add_argument("--fake-gpus", type=int, default=None)
+        p.add_argument("--topology", default="", help="topology JSON file instead of discovery")
+
+    p = sub.add_parser("topo")
+    disc(p)
+    p.add_argument("--output", default="table", choices=["table", "json", "annotations"])
+    p.add_argument("--resource-name", default="amd.com/gpu")
+    p.set_defaults(fn=cmd_topo)
+    p = sub.add_parser("probe")
+    disc(p)
+    p.add_argument("--preset", default="quick", choices=["quick", "full"])
+    p.add_argument("--mode", default="read", choices=["read", "write"])
+    p.add_argument("--out", default="")
+    p.set_defaults(fn=cmd_probe)
+    p = sub.add_parser("select")
+    disc(p)
+    p.add_argument("-k", type=int, required=True)
+    p.add_argument("--used", default="")
+    p.add_argument("--policy", default="exact", choices=["exact", "gaia"])
+    p.add_argument("--worst", action="store_true")
+    p.set_defaults(fn=cmd_select)
+    p = sub.add_parser("config")
+    p.add_argument("kind", choices=["scheduler", "policy", "manifests"])
+    p.add_argument("--resource-name", default="amd.com/gpu")
+    p.add_argument("--filter", action="store_true")
+    p.add_argument("--image", default="rocm/gpu-topology-k8s:latest")
+    p.set_defaults(fn=cmd_config)
+    p = sub.add_parser("validate")
+    p.add_argument("--devices", default="")
+    p.add_argument("--min-bytes", type=int, default=1 << 20)
+    p.add_argument("--max-bytes", type=int, default=1 << 30)
+    p.add_argument("--factor", type=int, default=4)
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    p.add_argument("--iters", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.set_defaults(fn=cmd_validate)
+    p = sub.add_parser("sim")
+    p.add_argument("--nodes", type=int, default=2)
+    p.add_argument("--pods", default="4,4,2,1,1,8")
+    p.add_argument("--policy", default="exact", choices=["exact", "gaia", "design"])
+    p.set_defaults(fn=cmd_sim)
+    a = ap.parse_args(argv)
+    return a.fn(a)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,82 @@
+"""Device-plugin daemon (DaemonSet entry point).
+
+    python -m gpu_topology_on_k8s_amd.deviceplugin --resource-name amd.com/gpu --probe quick
+
+Bring-up: discover the node (amdsmi, KFD sysfs fallback), optionally seed the
+link-cost matrix with the HIP probe (MFMA warm-up + LDS-staged p2p reads), publish the topology
+annotations, serve the kubelet ``v1beta1`` API and register.  Health is re-polled from the same
+discovery backend.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import signal
+import sys
+import threading
+
+from ..k8s.annotations import Contract
+from ..topology.discovery import discover
+from .plugin import DevicePluginServer, PluginConfig
+from .proto import DEVICE_PLUGIN_PATH
+
+
+def make_api(apiserver: str, token: str):
+    from ..k8s.api import RestKubeAPI
+
+    if apiserver == "none":
+        return None
+    if apiserver:
+        return RestKubeAPI(apiserver, token=token or None, verify=False)
+    if os.environ.get("KUBERNETES_SERVICE_HOST"):
+        return RestKubeAPI.in_cluster()
+    return None
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--resource-name", default="amd.com/gpu")
+    ap.add_argument("--annotation-prefix", default="gputopology.amd.com")
+    ap.add_argument("--socket-dir", default=DEVICE_PLUGIN_PATH)
+    ap.add_argument("--socket-name", default="amd-gpu-topology.sock")
+    ap.add_argument("--node-name", default=os.environ.get("NODE_NAME", ""))
+    ap.add_argument("--discovery", default="auto", choices=["auto", "amdsmi", "sysfs", "fake"])
+    ap.add_argument("--fake-gpus", type=int, default=None, help="fake backend device count (kind / CPU-only nodes)")
+    ap.add_argument("--probe", default="off", choices=["off", "quick", "full"])
+    ap.add_argument("--apiserver", default="", help="apiserver URL; default in-cluster; 'none' disables annotations")
+    ap.add_argument("--token", default="")
+    ap.add_argument("--dev-root", default="/dev")
+    ap.add_argument("--health-interval", type=float, default=10.0)
+    ap.add_argument("--log-level", default="INFO")
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=a.log_level, format='{"ts":"%(asctime)s","lvl":"%(levelname)s","mod":"%(name)s","msg":"%(message)s"}')
+    log = logging.getLogger("gtk.deviceplugin")
+
+    topo = discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus)
+    if a.probe != "off" and a.discovery != "fake":
+        from ..ops.probe import probe_topology
+
+        probe_topology(topo, preset=a.probe)
+        log.info("probe: %s", topo.probe)
+    log.info("topology:\n%s", topo.render())
+
+    def health(t):
+        fresh = discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus)
+        return {g.index: bool(g.healthy) for g in fresh.gpus if g.index < t.n}
+
+    cfg = PluginConfig(resource_name=a.resource_name, socket_dir=a.socket_dir, socket_name=a.socket_name, dev_root=a.dev_root,
+                       node_name=a.node_name, contract=Contract(resource_name=a.resource_name, prefix=a.annotation_prefix),
+                       health_interval=a.health_interval)
+    plugin = DevicePluginServer(topo, cfg, api=make_api(a.apiserver, a.token), health_fn=health if a.discovery != "fake" else None)
+    plugin.start()
+    done = threading.Event()
+    for sig in (signal.SIGINT, signal.SIGTERM):
+        signal.signal(sig, lambda *_: done.set())
+    done.wait()
+    plugin.stop()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

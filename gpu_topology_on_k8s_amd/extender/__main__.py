@@ -1,0 +1,46 @@
+"""Scheduler-extender daemon.
+
+    python -m gpu_topology_on_k8s_amd.extender --port 32743 --policy exact
+
+Serves ``/gputopology-scheduler/{sort,prioritize,filter,bind}`` (design.md:98-100) against the
+in-cluster apiserver (or ``--apiserver URL``).
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import sys
+
+from ..k8s.annotations import Contract
+from ..placement import PlacementPolicy
+from .scheduler import ExtenderConfig, TopologyExtender
+from .server import DEFAULT_PORT, DEFAULT_PREFIX, run
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=DEFAULT_PORT)
+    ap.add_argument("--url-prefix", default=DEFAULT_PREFIX)
+    ap.add_argument("--resource-name", default="amd.com/gpu")
+    ap.add_argument("--annotation-prefix", default="gputopology.amd.com")
+    ap.add_argument("--policy", default="exact", choices=["exact", "gaia", "design"])
+    ap.add_argument("--tie-break", default="first", choices=["first", "random"])
+    ap.add_argument("--assume-ttl", type=float, default=300.0)
+    ap.add_argument("--resync", type=float, default=5.0)
+    ap.add_argument("--apiserver", default="")
+    ap.add_argument("--token", default="")
+    ap.add_argument("--log-level", default="INFO")
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=a.log_level, format='{"ts":"%(asctime)s","lvl":"%(levelname)s","mod":"%(name)s","msg":"%(message)s"}')
+    from ..k8s.api import RestKubeAPI
+
+    api = RestKubeAPI(a.apiserver, token=a.token or None, verify=False) if a.apiserver else RestKubeAPI.in_cluster()
+    cfg = ExtenderConfig(contract=Contract(resource_name=a.resource_name, prefix=a.annotation_prefix), policy_name=a.policy,
+                         policy=PlacementPolicy(tie_break=a.tie_break), assume_ttl=a.assume_ttl, resync_s=a.resync)
+    run(TopologyExtender(api, cfg), a.host, a.port, a.url_prefix, resync_period=a.resync)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,75 @@
+"""Scheduler config generators, deploy manifests and the operator CLI."""
+import json
+import subprocess
+import sys
+
+import yaml
+
+from gpu_topology_on_k8s_amd.config import legacy_policy, render_manifests, scheduler_configuration
+
+
+def test_legacy_policy_matches_reference():
+    """design.md:92-113, field for field."""
+    p = legacy_policy("aliyun.com/gpu")
+    assert p["kind"] == "Policy" and p["apiVersion"] == "v1"
+    (e,) = p["extenders"]
+    assert e == {
+        "urlPrefix": "http://127.0.0.1:32743/gputopology-scheduler",
+        "PrioritizeVerb": "sort",
+        "bindVerb": "bind",
+        "enableHttps": False,
+        "nodeCacheCapable": True,
+        "managedResources": [{"name": "aliyun.com/gpu", "ignoredByScheduler": False}],
+        "ignorable": False,
+    }
+    assert "filterVerb" not in e  # design.md:117: no filter in the reference
+
+
+def test_scheduler_configuration():
+    c = scheduler_configuration("amd.com/gpu", extra_resources=["aliyun.com/gpu"])
+    assert c["apiVersion"] == "kubescheduler.config.k8s.io/v1"
+    e = c["extenders"][0]
+    assert e["prioritizeVerb"] == "sort" and e["bindVerb"] == "bind" and e["filterVerb"] == "filter"
+    assert [m["name"] for m in e["managedResources"]] == ["amd.com/gpu", "aliyun.com/gpu"]
+
+
+def test_manifests_are_valid_yaml():
+    docs = list(yaml.safe_load_all(render_manifests()))
+    kinds = [d["kind"] for d in docs]
+    assert kinds == ["ServiceAccount", "ClusterRole", "ClusterRoleBinding", "DaemonSet", "Deployment", "Service", "ConfigMap"]
+    ds = docs[3]
+    c = ds["spec"]["template"]["spec"]["containers"][0]
+    assert "gpu_topology_on_k8s_amd.deviceplugin" in c["command"]
+    assert {"name": "device-plugins", "mountPath": "/var/lib/kubelet/device-plugins"} in c["volumeMounts"]
+    cm = docs[-1]
+    assert yaml.safe_load(cm["data"]["scheduler-config.yaml"])["kind"] == "KubeSchedulerConfiguration"
+
+
+def _cli(*args):
+    p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd", *args], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    return p.stdout
+
+
+def test_cli_topo_select_config():
+    out = _cli("topo", "--discovery", "fake", "--fake-gpus", "8", "--output", "json")
+    assert json.loads(out)["gpus"][7]["index"] == 7
+    ann = json.loads(_cli("topo", "--discovery", "fake", "--fake-gpus", "2", "--output", "annotations"))
+    assert ann["GPU_XGMI_0_1"] == "xGMI 1 hop"
+    sel = json.loads(_cli("select", "--discovery", "fake", "--fake-gpus", "8", "-k", "4", "--used", "0", "--worst"))
+    assert sel["ids"] == [4, 5, 6, 7] and sel["worst"]["score"] < sel["score"]
+    g = json.loads(_cli("select", "--discovery", "fake", "--fake-gpus", "8", "-k", "2", "--policy", "gaia"))
+    assert len(g["ids"]) == 2
+    assert json.loads(_cli("config", "policy"))["kind"] == "Policy"
+
+
+def test_cli_sim():
+    lines = [json.loads(l) for l in _cli("sim", "--nodes", "1", "--pods", "4,4").splitlines()]
+    assert {tuple(l["devices"]) for l in lines} == {(0, 1, 2, 3), (4, 5, 6, 7)}
+
+
+def test_committed_deploy_files_are_current():
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent / "deploy"
+    assert (root / "gpu-topology.yaml").read_text() == render_manifests()
