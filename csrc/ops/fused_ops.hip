@@ -1,0 +1,594 @@
+// Fused elementwise / normalisation / loss / optimizer kernels for the Llama-3 DP validation
+// workload (BASELINE config 5: "Llama-3-8B DP all-reduce training on the allocated set").
+//
+// The reference has no model code; these kernels exist because the validation
+// workload's non-GEMM ops are HBM-bound and a bf16 Llama step on MI355X would otherwise spend its
+// time in chains of small PyTorch elementwise kernels.  GEMMs stay on hipBLASLt (plain library
+// GEMMs); everything between them is one pass over HBM here:
+//   rmsnorm_fwd / rmsnorm_bwd   wave-per-row, 16-B vector loads, no LDS (D=4096 -> 8 x 16 B per lane),
+//                               bwd keeps per-lane dW partials in registers across rows
+//   rope_split_fwd / _bwd       QKV GEMM output [T, (H+2Hkv)*Dh] -> q/k/v in [B, heads, S, Dh] with
+//                               RoPE applied to q,k in the same pass (and the exact inverse)
+//   swiglu_fwd / swiglu_bwd     gate|up GEMM output [T, 2F] -> silu(g)*u, and its gradient
+//   xent_fwd / xent_bwd         fused log-softmax cross-entropy over V=128256, gradient written
+//                               in place over the bf16 logits (saves a T x V fp32 tensor)
+//   adamw_step / sq_norm        one flat-buffer AdamW over bf16 params + fp32 master/m/v, and the
+//                               global gradient-norm reduction for clipping
+// All math in fp32, bf16 storage.  Wave size 64 everywhere (gfx950).
+#include <hip/hip_runtime.h>
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+
+#include <cstdint>
+
+namespace {
+
+typedef unsigned short u16;
+typedef u16 u16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float((uint32_t)v << 16); }
+__device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_BF16(t) TORCH_CHECK((t).is_cuda() && (t).scalar_type() == at::kBFloat16 && (t).is_contiguous(), #t " must be a contiguous bf16 GPU tensor")
+#define CHECK_F32(t) TORCH_CHECK((t).is_cuda() && (t).scalar_type() == at::kFloat && (t).is_contiguous(), #t " must be a contiguous fp32 GPU tensor")
+
+const u16* bp(const at::Tensor& t) { return reinterpret_cast<const u16*>(t.data_ptr()); }
+u16* bpm(at::Tensor& t) { return reinterpret_cast<u16*>(t.data_ptr()); }
+
+// =============================================================================== RMSNorm
+// One wave per row; lane l owns vectors c = i*64 + l (8 bf16 each).  NV = ceil(D / 512).
+template <int NV>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ w,
+                                                          u16* __restrict__ y, float* __restrict__ rstd, int M, int D,
+                                                          float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nvec = D >> 3;
+  const u16x8* xr = reinterpret_cast<const u16x8*>(x + (size_t)row * D);
+  u16x8 v[NV];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = i * 64 + lane;
+    if (c < nvec) {
+      v[i] = xr[c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float f = bf2f(v[i][j]);
+        ss += f * f;
+      }
+    }
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / (float)D + eps);
+  if (lane == 0) rstd[row] = r;
+  const u16x8* wr = reinterpret_cast<const u16x8*>(w);
+  u16x8* yr = reinterpret_cast<u16x8*>(y + (size_t)row * D);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = i * 64 + lane;
+    if (c < nvec) {
+      u16x8 wv = wr[c], o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(v[i][j]) * r * bf2f(wv[j]));
+      yr[c] = o;
+    }
+  }
+}
+
+// dx = r*g - x*r^3*mean(g*x), g = dy*w ;  dW partial[wave] = sum_rows dy*x*r  (fp32, reduced later)
+template <int NV>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const u16* __restrict__ dy, const u16* __restrict__ x,
+                                                          const u16* __restrict__ w, const float* __restrict__ rstd,
+                                                          u16* __restrict__ dx, float* __restrict__ dw_part, int M, int D) {
+  const int lane = threadIdx.x & 63;
+  const int gwave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nwaves = gridDim.x * 4;
+  const int nvec = D >> 3;
+  const u16x8* wr = reinterpret_cast<const u16x8*>(w);
+  float dwacc[NV][8];
+  u16x8 wv[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = i * 64 + lane;
+    if (c < nvec) wv[i] = wr[c];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dwacc[i][j] = 0.f;
+  }
+  for (int row = gwave; row < M; row += nwaves) {
+    const u16x8* xr = reinterpret_cast<const u16x8*>(x + (size_t)row * D);
+    const u16x8* dyr = reinterpret_cast<const u16x8*>(dy + (size_t)row * D);
+    const float r = rstd[row];
+    u16x8 xv[NV], gv[NV];
+    float dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = i * 64 + lane;
+      if (c < nvec) {
+        xv[i] = xr[c];
+        gv[i] = dyr[c];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xf = bf2f(xv[i][j]), dyf = bf2f(gv[i][j]);
+          dot += dyf * bf2f(wv[i][j]) * xf;
+          dwacc[i][j] += dyf * xf * r;
+        }
+      }
+    }
+    dot = wave_sum(dot);
+    const float k = r * r * r * dot / (float)D;
+    u16x8* dxr = reinterpret_cast<u16x8*>(dx + (size_t)row * D);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = i * 64 + lane;
+      if (c < nvec) {
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(r * bf2f(gv[i][j]) * bf2f(wv[i][j]) - bf2f(xv[i][j]) * k);
+        dxr[c] = o;
+      }
+    }
+  }
+  float* part = dw_part + (size_t)gwave * D;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = i * 64 + lane;
+    if (c < nvec) {
+      f32x4 a = {dwacc[i][0], dwacc[i][1], dwacc[i][2], dwacc[i][3]};
+      f32x4 b = {dwacc[i][4], dwacc[i][5], dwacc[i][6], dwacc[i][7]};
+      reinterpret_cast<f32x4*>(part)[2 * c] = a;
+      reinterpret_cast<f32x4*>(part)[2 * c + 1] = b;
+    }
+  }
+}
+
+// column sums of [P, D] fp32 partials -> bf16 [D]
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, u16* __restrict__ out, int P, int D) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= D) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += part[(size_t)p * D + col];
+  out[col] = f2bf(s);
+}
+
+template <int NV>
+void rmsnorm_fwd_launch(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, at::Tensor& rstd, int M, int D, float eps) {
+  hipLaunchKernelGGL(rmsnorm_fwd_kernel<NV>, dim3((M + 3) / 4), dim3(256), 0, cur_stream(), bp(x), bp(w), bpm(y),
+                     rstd.data_ptr<float>(), M, D, eps);
+}
+
+std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const at::Tensor& w, double eps) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  const int D = (int)x.size(-1);
+  TORCH_CHECK(D % 8 == 0 && D <= 8192 && w.numel() == D, "rmsnorm: D must be a multiple of 8, <= 8192, and match w");
+  const int M = (int)(x.numel() / D);
+  auto y = at::empty_like(x);
+  auto rstd = at::empty({M}, x.options().dtype(at::kFloat));
+  if (M == 0) return {y, rstd};
+  const int nv = (D + 511) / 512;
+  if (nv <= 1) rmsnorm_fwd_launch<1>(x, w, y, rstd, M, D, (float)eps);
+  else if (nv <= 2) rmsnorm_fwd_launch<2>(x, w, y, rstd, M, D, (float)eps);
+  else if (nv <= 4) rmsnorm_fwd_launch<4>(x, w, y, rstd, M, D, (float)eps);
+  else if (nv <= 8) rmsnorm_fwd_launch<8>(x, w, y, rstd, M, D, (float)eps);
+  else rmsnorm_fwd_launch<16>(x, w, y, rstd, M, D, (float)eps);
+  return {y, rstd};
+}
+
+template <int NV>
+void rmsnorm_bwd_launch(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, const at::Tensor& rstd, at::Tensor& dx,
+                        at::Tensor& part, int grid, int M, int D) {
+  hipLaunchKernelGGL(rmsnorm_bwd_kernel<NV>, dim3(grid), dim3(256), 0, cur_stream(), bp(dy), bp(x), bp(w),
+                     rstd.data_ptr<float>(), bpm(dx), part.data_ptr<float>(), M, D);
+}
+
+std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, const at::Tensor& rstd) {
+  CHECK_BF16(dy);
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_F32(rstd);
+  const int D = (int)x.size(-1);
+  const int M = (int)(x.numel() / D);
+  TORCH_CHECK(dy.numel() == x.numel() && rstd.numel() == M, "rmsnorm_bwd: shape mismatch");
+  auto dx = at::empty_like(x);
+  auto dw = at::empty({D}, w.options());
+  // enough waves to fill the chip (>= 4 per CU), but each wave gets several rows so dW partials stay small
+  int grid = std::max(1, std::min((M + 3) / 4, 1024));
+  auto part = at::empty({(int64_t)grid * 4, D}, x.options().dtype(at::kFloat));
+  if (M > 0) {
+    const int nv = (D + 511) / 512;
+    if (nv <= 1) rmsnorm_bwd_launch<1>(dy, x, w, rstd, dx, part, grid, M, D);
+    else if (nv <= 2) rmsnorm_bwd_launch<2>(dy, x, w, rstd, dx, part, grid, M, D);
+    else if (nv <= 4) rmsnorm_bwd_launch<4>(dy, x, w, rstd, dx, part, grid, M, D);
+    else if (nv <= 8) rmsnorm_bwd_launch<8>(dy, x, w, rstd, dx, part, grid, M, D);
+    else rmsnorm_bwd_launch<16>(dy, x, w, rstd, dx, part, grid, M, D);
+  } else {
+    part.zero_();
+  }
+  hipLaunchKernelGGL(colsum_kernel, dim3((D + 255) / 256), dim3(256), 0, cur_stream(), part.data_ptr<float>(), bpm(dw),
+                     grid * 4, D);
+  return {dx, dw};
+}
+
+// =============================================================================== RoPE + QKV split
+// qkv: [B*S, (H + 2*Hkv) * Dh] (token-major, the fused QKV GEMM output).  Outputs q [B,H,S,Dh],
+// k [B,Hkv,S,Dh], v [B,Hkv,S,Dh].  Rotation (HF/Llama "rotate_half"): for i < Dh/2
+//   out[i] = x[i]*cos - x[i+Dh/2]*sin ; out[i+Dh/2] = x[i+Dh/2]*cos + x[i]*sin
+// cos/sin tables: fp32 [S_max, Dh/2].  One thread = 8 consecutive pairs of one (token, head).
+// Backward (inverse=true) maps dq/dk/dv back to dqkv with the transposed rotation (sin -> -sin).
+template <bool kInverse>
+__global__ __launch_bounds__(256) void rope_split_kernel(u16* __restrict__ qkv, u16* __restrict__ q, u16* __restrict__ k,
+                                                         u16* __restrict__ v, const float* __restrict__ cosb,
+                                                         const float* __restrict__ sinb, int B, int S, int H, int Hkv,
+                                                         int Dh, int pos_offset) {
+  const int half = Dh >> 1;
+  const int vec_per_head = half >> 3;  // threads per head (each covers 8 pairs)
+  const int heads = H + 2 * Hkv;
+  const size_t total = (size_t)B * S * heads * vec_per_head;
+  for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
+    const int vi = (int)(idx % vec_per_head);
+    size_t t = idx / vec_per_head;
+    const int hh = (int)(t % heads);
+    t /= heads;  // token index
+    const int s = (int)(t % S);
+    const int b = (int)(t / S);
+    u16* src = qkv + t * (size_t)heads * Dh + (size_t)hh * Dh;
+    u16* dst;
+    if (hh < H)
+      dst = q + (((size_t)b * H + hh) * S + s) * Dh;
+    else if (hh < H + Hkv)
+      dst = k + (((size_t)b * Hkv + (hh - H)) * S + s) * Dh;
+    else
+      dst = v + (((size_t)b * Hkv + (hh - H - Hkv)) * S + s) * Dh;
+    const int i0 = vi * 8;
+    u16* fa = kInverse ? dst : src;  // read side
+    u16* ta = kInverse ? src : dst;  // write side
+    u16x8 lo = *reinterpret_cast<const u16x8*>(fa + i0);
+    u16x8 hi = *reinterpret_cast<const u16x8*>(fa + half + i0);
+    if (hh >= H + Hkv) {  // V: plain copy
+      *reinterpret_cast<u16x8*>(ta + i0) = lo;
+      *reinterpret_cast<u16x8*>(ta + half + i0) = hi;
+      continue;
+    }
+    const float* cr = cosb + (size_t)(s + pos_offset) * half + i0;
+    const float* sr = sinb + (size_t)(s + pos_offset) * half + i0;
+    f32x4 c0 = *reinterpret_cast<const f32x4*>(cr), c1 = *reinterpret_cast<const f32x4*>(cr + 4);
+    f32x4 s0 = *reinterpret_cast<const f32x4*>(sr), s1 = *reinterpret_cast<const f32x4*>(sr + 4);
+    u16x8 olo, ohi;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float c = j < 4 ? c0[j] : c1[j - 4];
+      const float sn = (j < 4 ? s0[j] : s1[j - 4]) * (kInverse ? -1.f : 1.f);
+      const float a = bf2f(lo[j]), bb = bf2f(hi[j]);
+      olo[j] = f2bf(a * c - bb * sn);
+      ohi[j] = f2bf(bb * c + a * sn);
+    }
+    *reinterpret_cast<u16x8*>(ta + i0) = olo;
+    *reinterpret_cast<u16x8*>(ta + half + i0) = ohi;
+  }
+}
+
+int grid_for(size_t work, int per_block = 256) {
+  size_t g = (work + per_block - 1) / per_block;
+  return (int)std::max<size_t>(1, std::min<size_t>(g, 256 * 16));  // >> 256 CUs, grid-stride beyond
+}
+
+std::vector<at::Tensor> rope_split_fwd(const at::Tensor& qkv, const at::Tensor& cosb, const at::Tensor& sinb, int64_t B,
+                                       int64_t S, int64_t H, int64_t Hkv, int64_t Dh, int64_t pos_offset) {
+  CHECK_BF16(qkv);
+  CHECK_F32(cosb);
+  CHECK_F32(sinb);
+  TORCH_CHECK(Dh % 16 == 0, "head dim must be a multiple of 16");
+  TORCH_CHECK(qkv.numel() == B * S * (H + 2 * Hkv) * Dh, "qkv shape mismatch");
+  TORCH_CHECK(cosb.size(-1) == Dh / 2 && cosb.size(0) >= S + pos_offset && sinb.sizes() == cosb.sizes(), "rope table shape");
+  auto opt = qkv.options();
+  auto q = at::empty({B, H, S, Dh}, opt), k = at::empty({B, Hkv, S, Dh}, opt), v = at::empty({B, Hkv, S, Dh}, opt);
+  const size_t work = (size_t)B * S * (H + 2 * Hkv) * (Dh / 16);
+  if (work)
+    hipLaunchKernelGGL(rope_split_kernel<false>, dim3(grid_for(work)), dim3(256), 0, cur_stream(),
+                       const_cast<u16*>(bp(qkv)), bpm(q), bpm(k), bpm(v), cosb.data_ptr<float>(), sinb.data_ptr<float>(),
+                       (int)B, (int)S, (int)H, (int)Hkv, (int)Dh, (int)pos_offset);
+  return {q, k, v};
+}
+
+at::Tensor rope_split_bwd(const at::Tensor& dq, const at::Tensor& dk, const at::Tensor& dv, const at::Tensor& cosb,
+                          const at::Tensor& sinb, int64_t pos_offset) {
+  CHECK_BF16(dq);
+  CHECK_BF16(dk);
+  CHECK_BF16(dv);
+  const int64_t B = dq.size(0), H = dq.size(1), S = dq.size(2), Dh = dq.size(3), Hkv = dk.size(1);
+  auto dqkv = at::empty({B * S, (H + 2 * Hkv) * Dh}, dq.options());
+  const size_t work = (size_t)B * S * (H + 2 * Hkv) * (Dh / 16);
+  if (work)
+    hipLaunchKernelGGL(rope_split_kernel<true>, dim3(grid_for(work)), dim3(256), 0, cur_stream(), bpm(dqkv),
+                       const_cast<u16*>(bp(dq)), const_cast<u16*>(bp(dk)), const_cast<u16*>(bp(dv)), cosb.data_ptr<float>(),
+                       sinb.data_ptr<float>(), (int)B, (int)S, (int)H, (int)Hkv, (int)Dh, (int)pos_offset);
+  return dqkv;
+}
+
+// =============================================================================== SwiGLU
+// gu: [T, 2F] = [gate | up]; h = silu(g) * u : [T, F]
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const u16* __restrict__ gu, u16* __restrict__ h, size_t T, int F) {
+  const int fv = F >> 3;
+  const size_t total = T * fv;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const size_t t = i / fv;
+    const int c = (int)(i % fv);
+    const u16x8 g = reinterpret_cast<const u16x8*>(gu + t * 2 * F)[c];
+    const u16x8 u = reinterpret_cast<const u16x8*>(gu + t * 2 * F + F)[c];
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gf = bf2f(g[j]);
+      o[j] = f2bf(gf / (1.f + __expf(-gf)) * bf2f(u[j]));
+    }
+    reinterpret_cast<u16x8*>(h + t * F)[c] = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const u16* __restrict__ dh, const u16* __restrict__ gu,
+                                                         u16* __restrict__ dgu, size_t T, int F) {
+  const int fv = F >> 3;
+  const size_t total = T * fv;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const size_t t = i / fv;
+    const int c = (int)(i % fv);
+    const u16x8 g = reinterpret_cast<const u16x8*>(gu + t * 2 * F)[c];
+    const u16x8 u = reinterpret_cast<const u16x8*>(gu + t * 2 * F + F)[c];
+    const u16x8 d = reinterpret_cast<const u16x8*>(dh + t * F)[c];
+    u16x8 og, ou;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gf = bf2f(g[j]), uf = bf2f(u[j]), df = bf2f(d[j]);
+      const float sg = 1.f / (1.f + __expf(-gf));
+      const float silu = gf * sg;
+      ou[j] = f2bf(df * silu);
+      og[j] = f2bf(df * uf * sg * (1.f + gf * (1.f - sg)));
+    }
+    reinterpret_cast<u16x8*>(dgu + t * 2 * F)[c] = og;
+    reinterpret_cast<u16x8*>(dgu + t * 2 * F + F)[c] = ou;
+  }
+}
+
+at::Tensor swiglu_fwd(const at::Tensor& gu) {
+  CHECK_BF16(gu);
+  const int64_t F2 = gu.size(-1);
+  TORCH_CHECK(F2 % 16 == 0, "swiglu: 2F must be a multiple of 16");
+  const int F = (int)(F2 / 2);
+  const size_t T = gu.numel() / F2;
+  auto sizes = gu.sizes().vec();
+  sizes.back() = F;
+  auto h = at::empty(sizes, gu.options());
+  if (T) hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid_for(T * (F / 8))), dim3(256), 0, cur_stream(), bp(gu), bpm(h), T, F);
+  return h;
+}
+
+at::Tensor swiglu_bwd(const at::Tensor& dh, const at::Tensor& gu) {
+  CHECK_BF16(dh);
+  CHECK_BF16(gu);
+  const int F = (int)(gu.size(-1) / 2);
+  const size_t T = gu.numel() / (2 * F);
+  TORCH_CHECK((size_t)dh.numel() == T * F, "swiglu_bwd: shape mismatch");
+  auto dgu = at::empty_like(gu);
+  if (T) hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(T * (F / 8))), dim3(256), 0, cur_stream(), bp(dh), bp(gu), bpm(dgu), T, F);
+  return dgu;
+}
+
+// =============================================================================== cross-entropy
+// One 256-thread block per row; online (max, sum-exp) over 16-B vectors, block reduce through LDS.
+__device__ __forceinline__ void online_merge(float& m, float& s, float m2, float s2) {
+  const float mx = fmaxf(m, m2);
+  s = (m == -INFINITY ? 0.f : s * __expf(m - mx)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mx));
+  m = mx;
+}
+
+__global__ __launch_bounds__(256) void xent_fwd_kernel(const u16* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                       float* __restrict__ loss, float* __restrict__ lse, int V,
+                                                       int64_t ignore_index) {
+  __shared__ float sm[4], ss[4];
+  const int row = blockIdx.x;
+  const u16x8* lr = reinterpret_cast<const u16x8*>(logits + (size_t)row * V);
+  const int nvec = V >> 3;
+  float m = -INFINITY, s = 0.f;
+  for (int c = threadIdx.x; c < nvec; c += 256) {
+    const u16x8 x = lr[c];
+    float lm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lm = fmaxf(lm, bf2f(x[j]));
+    float ls = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ls += __expf(bf2f(x[j]) - lm);
+    online_merge(m, s, lm, ls);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float m2 = __shfl_xor(m, off, 64), s2 = __shfl_xor(s, off, 64);
+    online_merge(m, s, m2, s2);
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sm[wave] = m;
+    ss[wave] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = sm[0], Ssum = ss[0];
+    for (int w = 1; w < 4; ++w) online_merge(M, Ssum, sm[w], ss[w]);
+    const float l = M + __logf(Ssum);
+    lse[row] = l;
+    const int64_t y = labels[row];
+    loss[row] = (y == ignore_index || y < 0 || y >= V) ? 0.f : l - bf2f(logits[(size_t)row * V + y]);
+  }
+}
+
+// dlogits = (softmax - onehot) * scale, written over the logits (scale = dL/dloss_mean per valid row)
+__global__ __launch_bounds__(256) void xent_bwd_kernel(u16* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                       const float* __restrict__ lse, const float* __restrict__ gscale,
+                                                       int V, int64_t ignore_index) {
+  const int row = blockIdx.x;
+  const int64_t y = labels[row];
+  const bool ignored = (y == ignore_index || y < 0 || y >= V);
+  const float l = lse[row];
+  const float sc = ignored ? 0.f : gscale[0];
+  u16x8* lr = reinterpret_cast<u16x8*>(logits + (size_t)row * V);
+  const int nvec = V >> 3;
+  for (int c = threadIdx.x; c < nvec; c += 256) {
+    const u16x8 x = lr[c];
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = c * 8 + j;
+      const float p = __expf(bf2f(x[j]) - l);
+      o[j] = f2bf((p - (col == y ? 1.f : 0.f)) * sc);
+    }
+    lr[c] = o;
+  }
+}
+
+std::vector<at::Tensor> xent_fwd(const at::Tensor& logits, const at::Tensor& labels, int64_t ignore_index) {
+  CHECK_BF16(logits);
+  TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous(), "labels must be int64 GPU");
+  const int V = (int)logits.size(-1);
+  TORCH_CHECK(V % 8 == 0, "vocab must be a multiple of 8");
+  const int64_t T = logits.numel() / V;
+  TORCH_CHECK(labels.numel() == T, "labels/logits mismatch");
+  auto loss = at::empty({T}, logits.options().dtype(at::kFloat));
+  auto lse = at::empty({T}, logits.options().dtype(at::kFloat));
+  if (T) hipLaunchKernelGGL(xent_fwd_kernel, dim3((unsigned)T), dim3(256), 0, cur_stream(), bp(logits), labels.data_ptr<int64_t>(),
+                            loss.data_ptr<float>(), lse.data_ptr<float>(), V, ignore_index);
+  return {loss, lse};
+}
+
+void xent_bwd_inplace(at::Tensor& logits, const at::Tensor& labels, const at::Tensor& lse, const at::Tensor& gscale,
+                      int64_t ignore_index) {
+  CHECK_BF16(logits);
+  CHECK_F32(lse);
+  CHECK_F32(gscale);
+  const int V = (int)logits.size(-1);
+  const int64_t T = logits.numel() / V;
+  if (T) hipLaunchKernelGGL(xent_bwd_kernel, dim3((unsigned)T), dim3(256), 0, cur_stream(), bpm(logits), labels.data_ptr<int64_t>(),
+                            lse.data_ptr<float>(), gscale.data_ptr<float>(), V, ignore_index);
+}
+
+// =============================================================================== optimizer
+// Flat-buffer AdamW (decoupled weight decay).  8 elements per thread per iteration: two 16-B loads
+// each of master/m/v, one 16-B load of the bf16 gradient; writes master/m/v and the bf16 weight.
+// hp: device fp32 [lr, beta1, beta2, eps, weight_decay, grad_scale, bias_c1, bias_c2] so a captured
+// graph replays with updated hyper-parameters.
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, float* __restrict__ m, float* __restrict__ v,
+                                                    const u16* __restrict__ g, u16* __restrict__ w, const float* __restrict__ hp,
+                                                    size_t n) {
+  const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4], gs = hp[5], bc1 = hp[6], bc2 = hp[7];
+  const size_t nv = n >> 3;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (size_t)gridDim.x * 256) {
+    f32x4 p0 = reinterpret_cast<f32x4*>(master)[2 * i], p1 = reinterpret_cast<f32x4*>(master)[2 * i + 1];
+    f32x4 m0 = reinterpret_cast<f32x4*>(m)[2 * i], m1 = reinterpret_cast<f32x4*>(m)[2 * i + 1];
+    f32x4 v0 = reinterpret_cast<f32x4*>(v)[2 * i], v1 = reinterpret_cast<f32x4*>(v)[2 * i + 1];
+    const u16x8 gv = reinterpret_cast<const u16x8*>(g)[i];
+    u16x8 wo;
+    float p[8], mm[8], vv[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      p[j] = p0[j], p[j + 4] = p1[j];
+      mm[j] = m0[j], mm[j + 4] = m1[j];
+      vv[j] = v0[j], vv[j + 4] = v1[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gr = bf2f(gv[j]) * gs;
+      mm[j] = b1 * mm[j] + (1.f - b1) * gr;
+      vv[j] = b2 * vv[j] + (1.f - b2) * gr * gr;
+      const float upd = (mm[j] / bc1) / (sqrtf(vv[j] / bc2) + eps);
+      p[j] = p[j] - lr * (upd + wd * p[j]);
+      wo[j] = f2bf(p[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      p0[j] = p[j], p1[j] = p[j + 4];
+      m0[j] = mm[j], m1[j] = mm[j + 4];
+      v0[j] = vv[j], v1[j] = vv[j + 4];
+    }
+    reinterpret_cast<f32x4*>(master)[2 * i] = p0;
+    reinterpret_cast<f32x4*>(master)[2 * i + 1] = p1;
+    reinterpret_cast<f32x4*>(m)[2 * i] = m0;
+    reinterpret_cast<f32x4*>(m)[2 * i + 1] = m1;
+    reinterpret_cast<f32x4*>(v)[2 * i] = v0;
+    reinterpret_cast<f32x4*>(v)[2 * i + 1] = v1;
+    reinterpret_cast<u16x8*>(w)[i] = wo;
+  }
+}
+
+// sum of squares of a bf16 buffer -> per-block partials (fp32)
+__global__ __launch_bounds__(256) void sqnorm_kernel(const u16* __restrict__ g, float* __restrict__ part, size_t n) {
+  __shared__ float red[4];
+  float s = 0.f;
+  const size_t nv = n >> 3;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (size_t)gridDim.x * 256) {
+    const u16x8 x = reinterpret_cast<const u16x8*>(g)[i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float f = bf2f(x[j]);
+      s += f * f;
+    }
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+void adamw_step(at::Tensor& master, at::Tensor& m, at::Tensor& v, const at::Tensor& g, at::Tensor& w, const at::Tensor& hp) {
+  CHECK_F32(master);
+  CHECK_F32(m);
+  CHECK_F32(v);
+  CHECK_BF16(g);
+  CHECK_BF16(w);
+  CHECK_F32(hp);
+  const size_t n = master.numel();
+  TORCH_CHECK(n % 8 == 0 && (size_t)m.numel() == n && (size_t)v.numel() == n && (size_t)g.numel() == n && (size_t)w.numel() == n,
+              "adamw: flat buffers must have equal sizes, a multiple of 8");
+  TORCH_CHECK(hp.numel() >= 8, "adamw: hp needs 8 entries");
+  if (n) hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n / 8)), dim3(256), 0, cur_stream(), master.data_ptr<float>(),
+                            m.data_ptr<float>(), v.data_ptr<float>(), bp(g), bpm(w), hp.data_ptr<float>(), n);
+}
+
+at::Tensor sq_norm(const at::Tensor& g) {
+  CHECK_BF16(g);
+  const size_t n = g.numel();
+  TORCH_CHECK(n % 8 == 0, "sq_norm: size must be a multiple of 8");
+  const int grid = 1024;
+  auto part = at::zeros({grid}, g.options().dtype(at::kFloat));
+  if (n) hipLaunchKernelGGL(sqnorm_kernel, dim3(grid), dim3(256), 0, cur_stream(), bp(g), part.data_ptr<float>(), n);
+  return part.sum();
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_fused, m) {
+  m.doc() = "gfx950 fused kernels for the Llama-3 DP validation workload";
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("rope_split_fwd", &rope_split_fwd);
+  m.def("rope_split_bwd", &rope_split_bwd);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("xent_fwd", &xent_fwd);
+  m.def("xent_bwd_inplace", &xent_bwd_inplace);
+  m.def("adamw_step", &adamw_step);
+  m.def("sq_norm", &sq_norm);
+}

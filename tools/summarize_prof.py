@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 CSV output (kernel stats + PMC counter collections) into one markdown file.
+
+    python tools/summarize_prof.py gpurun_out/prof_probe gpurun_out/pmc_lds gpurun_out/pmc_mem ... > profiles/x/SUMMARY.md
+
+PMC rows are aggregated per kernel name (sum over dispatches); derived metrics:
+  * LDS bank-conflict ratio = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
+  * HBM bytes = (TCC_EA0_RDREQ + TCC_EA0_WRREQ) * 64  (MI355X_MICROARCH: FETCH counts 64 B per request;
+    wide streaming reads are 128-B requests tallied at 64 B, so reads are doubled for dwordx4 streams)
+  * effective clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel wall time
+  * MFMA-busy / SQ-busy raw cycle ratio (normalisation of SQ_BUSY_CYCLES on gfx950 is uncalibrated)
+"""
+from __future__ import annotations
+
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "")
+    if "(" in name:
+        name = name[: name.index("(")]
+    return name.replace("void ", "")[:70]
+
+
+def stats_tables(d: str):
+    out = []
+    for f in sorted(glob.glob(os.path.join(d, "*kernel_stats.csv"))):
+        rows = list(csv.DictReader(open(f)))
+        out.append(f"### Kernel stats: `{os.path.relpath(f)}`\n")
+        out.append("| kernel | calls | avg µs | min µs | max µs | % time |\n|---|---|---|---|---|---|")
+        for r in rows:
+            out.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | {float(r['MinNs'])/1e3:.1f} | "
+                       f"{float(r['MaxNs'])/1e3:.1f} | {float(r['Percentage']):.1f} |")
+        out.append("")
+    return out
+
+
+def pmc_tables(d: str):
+    out = []
+    for f in sorted(glob.glob(os.path.join(d, "*counter_collection.csv"))):
+        agg = defaultdict(lambda: defaultdict(float))
+        meta = {}
+        wall = defaultdict(float)
+        seen = set()
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            did = (r["Dispatch_Id"], k)
+            if did not in seen:
+                seen.add(did)
+                wall[k] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+                agg[k]["_dispatches"] += 1
+            meta[k] = (r["Grid_Size"], r["Workgroup_Size"], r["LDS_Block_Size"], r["VGPR_Count"], r["Accum_VGPR_Count"], r["SGPR_Count"])
+        counters = sorted({c for v in agg.values() for c in v if not c.startswith("_")})
+        out.append(f"### PMC: `{os.path.relpath(f)}`\n")
+        out.append("| kernel | dispatches | grid | wg | LDS B | VGPR | AGPR | SGPR | " + " | ".join(counters) + " | derived |")
+        out.append("|" + "---|" * (9 + len(counters)))
+        for k, v in agg.items():
+            der = []
+            if v.get("SQ_LDS_IDX_ACTIVE"):
+                der.append(f"LDS conflict {v.get('SQ_LDS_BANK_CONFLICT', 0) / v['SQ_LDS_IDX_ACTIVE'] * 100:.2f}%")
+            if "TCC_EA0_RDREQ_sum" in v and wall[k] > 0:
+                rd = v["TCC_EA0_RDREQ_sum"] * 64 * 2  # 128-B requests counted at 64 B for wide streams
+                wr = v.get("TCC_EA0_WRREQ_sum", 0) * 64
+                der.append(f"HBM ≈{(rd + wr) / wall[k] / 1e9:.0f} GB/s (rd {rd/1e9:.2f} GB, wr {wr/1e9:.2f} GB)")
+            if v.get("GRBM_GUI_ACTIVE") and wall[k] > 0:
+                der.append(f"clk ≈{v['GRBM_GUI_ACTIVE'] / 8 / wall[k] / 1e9:.2f} GHz")
+            if v.get("SQ_VALU_MFMA_BUSY_CYCLES") and v.get("SQ_BUSY_CYCLES"):
+                der.append(f"MFMA-busy/SQ-busy cycles {v['SQ_VALU_MFMA_BUSY_CYCLES'] / v['SQ_BUSY_CYCLES']:.2f} (raw ratio)")
+            m = meta[k]
+            out.append(f"| {k} | {int(v['_dispatches'])} | {m[0]} | {m[1]} | {m[2]} | {m[3]} | {m[4]} | {m[5]} | "
+                       + " | ".join(f"{v.get(c, 0):.3g}" for c in counters) + f" | {'; '.join(der)} |")
+        out.append("")
+    return out
+
+
+def main(dirs):
+    lines = ["# rocprofv3 summary", ""]
+    for d in dirs:
+        lines += stats_tables(d) + pmc_tables(d)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
