@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""BASELINE config 5: Llama-3-8B DP training tokens/s on the scheduler-chosen subset vs the worst one.
+
+    python bench/train_llama.py --gpus 8 --model llama3-8b --batch 2 --seq 4096 --steps 10 [--out f.json]
+
+For each placement (``best`` = placement core's choice, ``worst`` = highest-objective subset of the
+same size) one ``torch.distributed.run`` job of ``--gpus`` ranks is started as a child process
+(nothing here touches the GPU).  With k equal to the node's device count both placements are the
+whole node and only ``best`` runs.  Random-init weights, synthetic tokens.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run(placement: str, a) -> dict:
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_port()}", "-m", "gpu_topology_on_k8s_amd.models.train", "--model", a.model, "--batch", str(a.batch),
+           "--seq", str(a.seq), "--steps", str(a.steps), "--warmup", str(a.warmup), "--placement", placement,
+           "--bucket-mb", str(a.bucket_mb), "--attn", a.attn] + (["--checkpoint"] if a.checkpoint else [])
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    p = subprocess.run(cmd, capture_output=True, text=True, cwd=REPO, env=env, timeout=a.timeout)
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    if p.returncode != 0 or not lines:
+        sys.stderr.write(p.stderr[-6000:])
+        raise SystemExit(f"{placement} run failed with exit code {p.returncode}")
+    return json.loads(lines[-1])
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--batch", type=int, default=2)
+    ap.add_argument("--seq", type=int, default=4096)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--bucket-mb", type=float, default=256.0)
+    ap.add_argument("--attn", default="sdpa")
+    ap.add_argument("--checkpoint", action="store_true")
+    ap.add_argument("--timeout", type=int, default=1500)
+    ap.add_argument("--placements", default="best,worst")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    res = {}
+    for pl in a.placements.split(","):
+        r = run(pl, a)
+        res[pl] = r
+        print(json.dumps(r), flush=True)
+        if pl == "best" and not r.get("worst_devices"):
+            break  # k == node size: best == worst
+    summary = {
+        "metric": "Llama DP tokens/s, scheduler-chosen vs worst placement",
+        "model": a.model, "n_gpus": a.gpus, "seq_len": a.seq, "global_batch": a.batch * a.gpus,
+        "best_tokens_per_s": res["best"]["tokens_per_s"], "best_devices": res["best"]["devices"],
+        "worst_tokens_per_s": res.get("worst", {}).get("tokens_per_s"), "worst_devices": res.get("worst", {}).get("devices"),
+        "mfu": res["best"]["mfu"], "max_mem_gb": res["best"]["max_mem_gb"], "data": "synthetic tokens, random-init weights",
+    }
+    if summary["worst_tokens_per_s"]:
+        summary["speedup_vs_worst"] = summary["best_tokens_per_s"] / summary["worst_tokens_per_s"]
+    print(json.dumps(summary), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump({"summary": summary, "runs": res}, f, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,212 @@
+"""Llama-3 decoder (random init) for the placement-validation workload (BASELINE config 5).
+
+"Single pod requests 8 MI355X; Llama-3-8B DP all-reduce training on the allocated set, tokens/sec vs
+worst-topology placement."  The reference has no model code; this is the workload
+that turns a placement into a measurable training throughput.
+
+MI355X-first layout:
+  * every parameter is a view into ONE flat bf16 buffer and every gradient a view into ONE flat bf16
+    gradient buffer (:class:`FlatParams`): the data-parallel engine all-reduces contiguous buckets of
+    that buffer straight from the backward hooks, and the optimizer is one fused AdamW launch over
+    the whole buffer (fp32 master + moments: 14 B/param read + 14 B/param written per step);
+  * fused QKV and gate|up projections -> hipBLASLt GEMMs; everything between GEMMs is a fused HIP
+    kernel (RMSNorm, RoPE + head split, SwiGLU, cross-entropy with in-place dlogits);
+  * Llama-3-8B = 8.03 B params: 16 GB bf16 weights + 16 GB bf16 grads + 96 GB fp32 master/m/v =
+    128 GB, leaving ~160 GB of the 288 GB HBM for activations, so DP alone suffices (no TP/PP/SP).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import asdict, dataclass
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from ..ops import fused
+
+__all__ = ["LlamaConfig", "FlatParams", "Llama", "smoke_step"]
+
+
+@dataclass(frozen=True)
+class LlamaConfig:
+    dim: int = 4096
+    n_layers: int = 32
+    n_heads: int = 32
+    n_kv_heads: int = 8
+    vocab: int = 128256
+    ffn_dim: int = 14336
+    rope_theta: float = 500000.0
+    norm_eps: float = 1e-5
+    max_seq: int = 8192
+
+    @property
+    def head_dim(self) -> int:
+        return self.dim // self.n_heads
+
+    @classmethod
+    def llama3_8b(cls) -> "LlamaConfig":
+        return cls()
+
+    @classmethod
+    def tiny(cls) -> "LlamaConfig":
+        return cls(dim=256, n_layers=2, n_heads=4, n_kv_heads=2, vocab=1024, ffn_dim=512, max_seq=512)
+
+    @classmethod
+    def named(cls, name: str) -> "LlamaConfig":
+        table = {
+            "llama3-8b": cls.llama3_8b(),
+            "tiny": cls.tiny(),
+            "llama3-1b": cls(dim=2048, n_layers=16, n_heads=32, n_kv_heads=8, vocab=128256, ffn_dim=8192),
+        }
+        return table[name]
+
+    def param_shapes(self) -> List[Tuple[str, Tuple[int, ...]]]:
+        D, Dh, H, Hkv = self.dim, self.head_dim, self.n_heads, self.n_kv_heads
+        shapes: List[Tuple[str, Tuple[int, ...]]] = [("tok_emb", (self.vocab, D))]
+        for i in range(self.n_layers):
+            shapes += [
+                (f"l{i}.attn_norm", (D,)),
+                (f"l{i}.wqkv", ((H + 2 * Hkv) * Dh, D)),
+                (f"l{i}.wo", (D, H * Dh)),
+                (f"l{i}.ffn_norm", (D,)),
+                (f"l{i}.w13", (2 * self.ffn_dim, D)),
+                (f"l{i}.w2", (D, self.ffn_dim)),
+            ]
+        shapes += [("norm", (D,)), ("lm_head", (self.vocab, D))]
+        return shapes
+
+    def num_params(self) -> int:
+        return sum(math.prod(s) for _, s in self.param_shapes())
+
+    def flops_per_token(self, seq: int) -> float:
+        """Training FLOPs per token: 6 N (dense) + 12 L S D (causal attention fwd+bwd, halved for causality)."""
+        return 6.0 * self.num_params() + 6.0 * self.n_layers * seq * self.dim
+
+    def to_dict(self) -> Dict[str, object]:
+        return asdict(self)
+
+
+_ALIGN = 64  # elements: keeps every parameter view 128-B aligned for 16-B vector kernels
+
+
+class FlatParams:
+    """All parameters as views of one flat bf16 buffer, gradients as views of one flat grad buffer."""
+
+    def __init__(self, shapes: List[Tuple[str, Tuple[int, ...]]], device, dtype=torch.bfloat16):
+        self.names = [n for n, _ in shapes]
+        self.shapes = {n: s for n, s in shapes}
+        self.offsets: Dict[str, int] = {}
+        off = 0
+        for n, s in shapes:
+            self.offsets[n] = off
+            off += (math.prod(s) + _ALIGN - 1) // _ALIGN * _ALIGN
+        self.numel = off
+        self.data = torch.zeros(off, dtype=dtype, device=device)
+        self.grad = torch.zeros(off, dtype=dtype, device=device)
+        self.params: Dict[str, torch.nn.Parameter] = {}
+        for n, s in shapes:
+            o, k = self.offsets[n], math.prod(s)
+            p = torch.nn.Parameter(self.data[o:o + k].view(s))
+            p.grad = self.grad[o:o + k].view(s)
+            self.params[n] = p
+
+    def attach_grads(self) -> None:
+        """(Re)bind every ``param.grad`` to its view of the flat gradient buffer."""
+        for n, p in self.params.items():
+            o, k = self.offsets[n], math.prod(self.shapes[n])
+            p.grad = self.grad[o:o + k].view(self.shapes[n])
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+
+    def span(self, name: str) -> Tuple[int, int]:
+        o = self.offsets[name]
+        return o, o + math.prod(self.shapes[name])
+
+
+class Llama(torch.nn.Module):
+    def __init__(self, cfg: LlamaConfig, device="cuda", seed: int = 0, checkpoint: bool = False, attn: str = "sdpa"):
+        super().__init__()
+        self.cfg = cfg
+        self.checkpoint = checkpoint
+        self.attn = attn
+        self.flat = FlatParams(cfg.param_shapes(), device)
+        for n, p in self.flat.params.items():
+            self.register_parameter(n.replace(".", "_"), p)
+        self._init(seed)
+        cos, sin = fused.rope_tables(cfg.max_seq, cfg.head_dim, cfg.rope_theta, device=device)
+        self.register_buffer("rope_cos", cos, persistent=False)
+        self.register_buffer("rope_sin", sin, persistent=False)
+
+    @torch.no_grad()
+    def _init(self, seed: int) -> None:
+        dev = self.flat.data.device
+        g = torch.Generator(device=dev).manual_seed(seed)  # same seed + device type => identical replicas
+        std = 0.02
+        out_std = std / math.sqrt(2 * self.cfg.n_layers)
+        for n, p in self.flat.params.items():
+            if n.endswith("norm"):
+                p.fill_(1.0)
+                continue
+            s = out_std if (n.endswith(".wo") or n.endswith(".w2")) else std
+            flat = p.view(-1)
+            step = 1 << 26  # bounded fp32 scratch (256 MB) per chunk
+            for i in range(0, flat.numel(), step):
+                m = min(step, flat.numel() - i)
+                flat[i:i + m].copy_(torch.randn(m, generator=g, dtype=torch.float32, device=dev).mul_(s))
+
+    def P(self, name: str) -> torch.nn.Parameter:
+        return self.flat.params[name]
+
+    # ---------------------------------------------------------------- blocks
+    def _attention(self, q, k, v):
+        if self.attn == "sdpa":
+            return F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=q.size(1) != k.size(1))
+        # explicit GQA expansion (fallback when the SDPA backend lacks native GQA)
+        rep = q.size(1) // k.size(1)
+        if rep > 1:
+            k = k.repeat_interleave(rep, dim=1)
+            v = v.repeat_interleave(rep, dim=1)
+        return F.scaled_dot_product_attention(q, k, v, is_causal=True)
+
+    def _layer(self, i: int, x: torch.Tensor, B: int, S: int) -> torch.Tensor:
+        cfg = self.cfg
+        H, Hkv, Dh = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
+        h = fused.rmsnorm(x, self.P(f"l{i}.attn_norm"), cfg.norm_eps)
+        qkv = F.linear(h, self.P(f"l{i}.wqkv"))
+        q, k, v = fused.rope_split(qkv, self.rope_cos, self.rope_sin, B, S, H, Hkv, Dh)
+        o = self._attention(q, k, v)  # [B, H, S, Dh]
+        o = o.transpose(1, 2).reshape(B * S, H * Dh)
+        x = x + F.linear(o, self.P(f"l{i}.wo"))
+        h = fused.rmsnorm(x, self.P(f"l{i}.ffn_norm"), cfg.norm_eps)
+        x = x + F.linear(fused.swiglu(F.linear(h, self.P(f"l{i}.w13"))), self.P(f"l{i}.w2"))
+        return x
+
+    def forward(self, tokens: torch.Tensor, labels: Optional[torch.Tensor] = None) -> torch.Tensor:
+        B, S = tokens.shape
+        x = F.embedding(tokens.reshape(-1), self.P("tok_emb"))  # [B*S, D]
+        for i in range(self.cfg.n_layers):
+            if self.checkpoint and self.training:
+                x = torch.utils.checkpoint.checkpoint(self._layer, i, x, B, S, use_reentrant=False)
+            else:
+                x = self._layer(i, x, B, S)
+        x = fused.rmsnorm(x, self.P("norm"), self.cfg.norm_eps)
+        logits = F.linear(x, self.P("lm_head"))  # [B*S, V]
+        if labels is None:
+            return logits.view(B, S, -1)
+        return fused.cross_entropy(logits, labels.reshape(-1))
+
+
+def smoke_step(device: str = "cuda:0") -> float:
+    """One tiny forward+backward on ``device`` through the HIP kernels (``__graft_entry__.smoke``)."""
+    torch.manual_seed(0)
+    cfg = LlamaConfig.tiny()
+    model = Llama(cfg, device=device)
+    tokens = torch.randint(0, cfg.vocab, (2, 64), device=device)
+    loss = model(tokens, torch.roll(tokens, -1, dims=1))
+    loss.backward()
+    torch.cuda.synchronize()
+    g = model.flat.grad.float()
+    assert torch.isfinite(g).all() and g.abs().sum() > 0
+    return float(loss.item())

@@ -1,0 +1,162 @@
+"""Llama-3 data-parallel training on the scheduler-chosen devices (BASELINE config 5).
+
+    python -m torch.distributed.run --nproc-per-node K --master-addr 127.0.0.1 \
+        -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 2 --seq 4096 --steps 10 --placement best
+
+One process per GPU; rank 0 discovers the node, runs the placement core for the k-subset (``best``)
+or its worst-scoring alternative (``worst``), and every rank binds to ``subset[rank]`` — what the pod
+would see after the device plugin's Allocate.  A step = forward + backward with bucketed RCCL
+gradient all-reduce overlapped with backward + global-norm clip + fused AdamW.  Reports tokens/s
+(whole job) and model FLOP utilisation against the 2.5 PF/s dense bf16 peak per GPU.
+Runs on CPU with the gloo backend for tests (tiny model).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from typing import Dict, Optional
+
+import torch
+import torch.distributed as dist
+
+from .llama import Llama, LlamaConfig
+from .optim import FlatAdamW
+from ..parallel.dp import BucketedAllReduce, broadcast_params
+
+__all__ = ["train", "main"]
+
+PEAK_BF16_FLOPS = 2.5e15  # MI355X dense bf16 (MI355X_MICROARCH.md), per GPU
+
+
+def _init_dist(device_kind: str) -> Dict[str, int]:
+    if "RANK" not in os.environ:
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    if not dist.is_initialized():
+        dist.init_process_group(backend="nccl" if device_kind == "cuda" else "gloo")
+    return {"rank": rank, "world": world, "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}
+
+
+def _choose_device(env, placement: str, discovery: str) -> Dict[str, object]:
+    """Rank 0 places the job; the choice travels through the store."""
+    store = dist.distributed_c10d._get_default_store()
+    if env["rank"] == 0:
+        from ..parallel.allreduce import choose_subset
+
+        ch = choose_subset(env["world"], backend=discovery)
+        devices = ch.devices if placement == "best" or not ch.worst else ch.worst
+        info = {"devices": devices, "best": ch.devices, "best_score": ch.score, "worst": ch.worst,
+                "worst_score": ch.worst_score, "source": ch.source}
+        store.set("gtk/train_placement", json.dumps(info))
+    return json.loads(store.get("gtk/train_placement").decode())
+
+
+def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int = 3, warmup: int = 1, device_kind: str = "cuda",
+          placement: str = "best", discovery: str = "auto", bucket_mb: float = 256.0, checkpoint: bool = False, lr: float = 3e-4,
+          attn: str = "sdpa", seed: int = 0, log: bool = True) -> Dict[str, object]:
+    env = _init_dist(device_kind)
+    if device_kind == "cuda":
+        pl = _choose_device(env, placement, discovery)
+        dev = int(pl["devices"][env["rank"]])
+        torch.cuda.set_device(dev)
+        device = torch.device("cuda", dev)
+    else:
+        pl = {"devices": [], "best": [], "worst": None, "source": "cpu"}
+        device = torch.device("cpu")
+    cfg = LlamaConfig.named(model_name)
+    model = Llama(cfg, device=device, seed=seed, checkpoint=checkpoint, attn=attn)
+    broadcast_params(model.flat)
+    ar = BucketedAllReduce(model.flat, bucket_mb=bucket_mb)
+    opt = FlatAdamW(model.flat, lr=lr)
+    gen = torch.Generator(device="cpu").manual_seed(1234 + env["rank"])
+
+    def batch_tokens():
+        t = torch.randint(0, cfg.vocab, (batch, seq + 1), generator=gen)
+        t = t.to(device, non_blocking=True)
+        return t[:, :-1], t[:, 1:]
+
+    def step() -> torch.Tensor:
+        x, y = batch_tokens()
+        model.flat.zero_grad()
+        loss = model(x, y)
+        loss.backward()
+        ar.finish()
+        opt.step(grad_scale=ar.grad_scale)
+        return loss.detach()
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+
+    losses = []
+    for _ in range(warmup):
+        losses.append(step())
+    sync()
+    dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        losses.append(step())
+    sync()
+    dt = time.perf_counter() - t0
+    dist.barrier()
+    t = torch.tensor([dt], dtype=torch.float64, device=device if device.type == "cuda" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    tokens = env["world"] * batch * seq * steps
+    tps = tokens / dt
+    mfu = tps * cfg.flops_per_token(seq) / (PEAK_BF16_FLOPS * env["world"]) if device.type == "cuda" else None
+    out = {
+        "metric": "Llama DP training tokens/s on the scheduler-chosen subset",
+        "model": model_name,
+        "params": cfg.num_params(),
+        "n_gpus": env["world"],
+        "placement": placement,
+        "devices": pl["devices"],
+        "best_devices": pl.get("best"),
+        "worst_devices": pl.get("worst"),
+        "global_batch": batch * env["world"],
+        "seq_len": seq,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": dt / max(1, steps) * 1e3,
+        "tokens_per_s": tps,
+        "mfu": mfu,
+        "loss_first": float(losses[0]),
+        "loss_last": float(losses[-1]),
+        "buckets": ar.stats["buckets"],
+        "bucket_mb": bucket_mb,
+        "max_mem_gb": (torch.cuda.max_memory_allocated(device) / 1e9) if device.type == "cuda" else None,
+    }
+    if log and env["rank"] == 0:
+        print(json.dumps(out), flush=True)
+    ar.remove()
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--model", default="llama3-8b", choices=["llama3-8b", "llama3-1b", "tiny"])
+    ap.add_argument("--batch", type=int, default=2)
+    ap.add_argument("--seq", type=int, default=4096)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
+    ap.add_argument("--placement", default="best", choices=["best", "worst"])
+    ap.add_argument("--discovery", default="auto")
+    ap.add_argument("--bucket-mb", type=float, default=256.0)
+    ap.add_argument("--checkpoint", action="store_true")
+    ap.add_argument("--attn", default="sdpa", choices=["sdpa", "sdpa-expand"])
+    a = ap.parse_args(argv)
+    train(a.model, a.batch, a.seq, a.steps, a.warmup, a.device, a.placement, a.discovery, a.bucket_mb, a.checkpoint, attn=a.attn)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

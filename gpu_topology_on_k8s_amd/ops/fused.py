@@ -1,0 +1,163 @@
+"""Autograd front-end of the fused HIP kernels (``csrc/ops/fused_ops.hip``) + PyTorch references.
+
+GPU tensors always take the HIP path and fail loudly (``NativeUnavailable``) when the extension is
+missing; CPU tensors take the reference path (used by the CPU test-suite and as the fp32 numerics
+oracle of ``tests/test_fused_gpu.py``).
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+
+from .._native import load
+
+__all__ = [
+    "rmsnorm", "rmsnorm_ref", "rope_tables", "rope_split", "rope_split_ref", "swiglu", "swiglu_ref", "cross_entropy",
+    "cross_entropy_ref", "hip",
+]
+
+
+def hip():
+    return load("_fused")
+
+
+# ------------------------------------------------------------------------------------ RMSNorm
+def rmsnorm_ref(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()).to(x.dtype)
+
+
+class _RMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        x = x.contiguous()
+        y, rstd = hip().rmsnorm_fwd(x, w, float(eps))
+        ctx.save_for_backward(x, w, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, rstd = ctx.saved_tensors
+        dx, dw = hip().rmsnorm_bwd(dy.contiguous(), x, w, rstd)
+        return dx, dw, None
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
+    if x.is_cuda:
+        return _RMSNorm.apply(x, w, eps)
+    return rmsnorm_ref(x, w, eps)
+
+
+# ------------------------------------------------------------------------------------ RoPE
+def rope_tables(seq: int, head_dim: int, theta: float = 500000.0, device=None,
+                scaling: dict | None = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """fp32 cos/sin tables [seq, head_dim/2] (Llama-3 RoPE; optional llama3 frequency scaling)."""
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling:  # Llama-3.1 style long-context scaling
+        factor, lo, hi, orig = scaling["factor"], scaling["low_freq_factor"], scaling["high_freq_factor"], scaling["original_max_position_embeddings"]
+        wavelen = 2 * torch.pi / inv
+        smooth = ((orig / wavelen) - lo) / (hi - lo)
+        scaled = torch.where(wavelen > orig / lo, inv / factor, inv)
+        mid = (wavelen <= orig / lo) & (wavelen >= orig / hi)
+        inv = torch.where(mid, (1 - smooth) * inv / factor + smooth * inv, scaled)
+    t = torch.arange(seq, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    return f.cos().float().to(device), f.sin().float().to(device)
+
+
+def rope_split_ref(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, B: int, S: int, H: int, Hkv: int, Dh: int,
+                   pos_offset: int = 0):
+    x = qkv.view(B, S, H + 2 * Hkv, Dh).float()
+    c = cos[pos_offset:pos_offset + S].view(1, S, 1, Dh // 2)
+    s = sin[pos_offset:pos_offset + S].view(1, S, 1, Dh // 2)
+
+    def rot(t):
+        a, b = t[..., : Dh // 2], t[..., Dh // 2:]
+        return torch.cat([a * c - b * s, b * c + a * s], dim=-1)
+
+    q = rot(x[:, :, :H]).to(qkv.dtype).transpose(1, 2).contiguous()
+    k = rot(x[:, :, H:H + Hkv]).to(qkv.dtype).transpose(1, 2).contiguous()
+    v = x[:, :, H + Hkv:].to(qkv.dtype).transpose(1, 2).contiguous()
+    return q, k, v
+
+
+class _RopeSplit(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, B, S, H, Hkv, Dh, pos_offset):
+        q, k, v = hip().rope_split_fwd(qkv.contiguous(), cos, sin, B, S, H, Hkv, Dh, pos_offset)
+        ctx.save_for_backward(cos, sin)
+        ctx.meta = (pos_offset, qkv.shape)
+        return q, k, v
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        cos, sin = ctx.saved_tensors
+        pos_offset, shape = ctx.meta
+        dqkv = hip().rope_split_bwd(dq.contiguous(), dk.contiguous(), dv.contiguous(), cos, sin, pos_offset)
+        return dqkv.view(shape), None, None, None, None, None, None, None, None
+
+
+def rope_split(qkv, cos, sin, B, S, H, Hkv, Dh, pos_offset: int = 0):
+    """Fused QKV split + RoPE: [B*S, (H+2Hkv)*Dh] -> q [B,H,S,Dh], k/v [B,Hkv,S,Dh]."""
+    if qkv.is_cuda:
+        return _RopeSplit.apply(qkv, cos, sin, B, S, H, Hkv, Dh, pos_offset)
+    return rope_split_ref(qkv, cos, sin, B, S, H, Hkv, Dh, pos_offset)
+
+
+# ------------------------------------------------------------------------------------ SwiGLU
+def swiglu_ref(gu: torch.Tensor) -> torch.Tensor:
+    g, u = gu.float().chunk(2, dim=-1)
+    return (torch.nn.functional.silu(g) * u).to(gu.dtype)
+
+
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        gu = gu.contiguous()
+        ctx.save_for_backward(gu)
+        return hip().swiglu_fwd(gu)
+
+    @staticmethod
+    def backward(ctx, dh):
+        (gu,) = ctx.saved_tensors
+        return hip().swiglu_bwd(dh.contiguous(), gu)
+
+
+def swiglu(gu: torch.Tensor) -> torch.Tensor:
+    if gu.is_cuda:
+        return _SwiGLU.apply(gu)
+    return swiglu_ref(gu)
+
+
+# ------------------------------------------------------------------------------------ loss
+def cross_entropy_ref(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
+    return torch.nn.functional.cross_entropy(logits.float().view(-1, logits.size(-1)), labels.view(-1), ignore_index=ignore_index)
+
+
+class _CrossEntropy(torch.autograd.Function):
+    """Mean token cross-entropy; backward overwrites the (no longer needed) bf16 logits with dlogits."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index):
+        V = logits.size(-1)
+        lg = logits.contiguous().view(-1, V)
+        lb = labels.contiguous().view(-1)
+        loss_rows, lse = hip().xent_fwd(lg, lb, int(ignore_index))
+        nvalid = (lb != ignore_index).sum().clamp_min(1).float()
+        ctx.lg, ctx.lb, ctx.lse, ctx.nvalid, ctx.ii, ctx.shape = lg, lb, lse, nvalid, int(ignore_index), logits.shape
+        return loss_rows.sum() / nvalid
+
+    @staticmethod
+    def backward(ctx, g):
+        scale = (g.float() / ctx.nvalid).reshape(1).contiguous()
+        lg = ctx.lg
+        hip().xent_bwd_inplace(lg, ctx.lb, ctx.lse, scale, ctx.ii)
+        ctx.lg = None
+        return lg.view(ctx.shape), None, None
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
+    if logits.is_cuda:
+        return _CrossEntropy.apply(logits, labels, ignore_index)
+    return cross_entropy_ref(logits, labels, ignore_index)
