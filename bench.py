@@ -41,7 +41,8 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--size-mb", type=float, default=2048.0, help="per-GPU message size in MiB (default 2 GiB)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
-    ap.add_argument("--backend", default="native", choices=["native", "torch"])
+    ap.add_argument("--backend", default="native", choices=["native", "torch", "cpu"],
+                    help="native = RCCL communicator from csrc/rccl; torch = dist.all_reduce; cpu = gloo (control-path tests)")
     ap.add_argument("--inplace", action="store_true")
     ap.add_argument("--probe", default=None, choices=[None, "quick", "full"], help="run the HIP link probe before placement")
     ap.add_argument("--discovery", default="auto", choices=["auto", "amdsmi", "sysfs", "fake"])
@@ -71,20 +72,29 @@ def main(argv=None) -> int:
     if env.world != args.gpus:
         print(f"bench: WORLD_SIZE={env.world} but --gpus={args.gpus}", file=sys.stderr)
         return 2
-    dist.init_process_group(backend="nccl")
+    cpu = args.backend == "cpu"
+    dist.init_process_group(backend="gloo" if cpu else "nccl")
     env.store = dist.distributed_c10d._get_default_store()
 
     # --- placement: rank 0 picks the subset, everybody binds to subset[rank] ---------------------
     if env.rank == 0:
-        choice = choose_subset(env.world, probe=args.probe, backend=args.discovery)
+        choice = choose_subset(env.world, probe=args.probe, backend=args.discovery, visible=env.world if cpu else None)
         env.store.set("gtk/subset", choice.to_json())
     choice = SubsetChoice.from_json(env.store.get("gtk/subset").decode())
     device = choice.devices[env.rank]
-    torch.cuda.set_device(device)
+    tdev = "cpu" if cpu else f"cuda:{device}"
+    barrier_kw = {} if cpu else {"device_ids": [device]}
+
+    def gpu_sync():
+        if not cpu:
+            torch.cuda.synchronize()
+
+    if not cpu:
+        torch.cuda.set_device(device)
 
     nbytes = int(args.size_mb * (1 << 20))
     runner = AllReduceRunner(env, device, nbytes, args.dtype, backend=args.backend, inplace=args.inplace)
-    wrong = torch.tensor([runner.check()], dtype=torch.int64, device=f"cuda:{device}")
+    wrong = torch.tensor([runner.check()], dtype=torch.int64, device=tdev)
     dist.all_reduce(wrong)
     if int(wrong.item()) != 0:
         print(f"bench: all-reduce correctness check FAILED ({int(wrong.item())} wrong elements)", file=sys.stderr)
@@ -94,17 +104,17 @@ def main(argv=None) -> int:
         runner.step()
     runner.synchronize()
 
-    dist.barrier(device_ids=[device])
-    torch.cuda.synchronize()
+    dist.barrier(**barrier_kw)
+    gpu_sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         runner.step()
     runner.synchronize()
-    torch.cuda.synchronize()
+    gpu_sync()
     elapsed = time.perf_counter() - t0
-    dist.barrier(device_ids=[device])
+    dist.barrier(**barrier_kw)
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
+    t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     ms_per_step = elapsed / max(1, args.steps) * 1e3

@@ -70,12 +70,14 @@ def _visible_device_count() -> int:
     return int(torch.cuda.device_count())
 
 
-def choose_subset(k: int, probe: Optional[str] = None, backend: str = "auto") -> SubsetChoice:
-    """Rank-0 side: discover the node, optionally probe links, run the placement core."""
+def choose_subset(k: int, probe: Optional[str] = None, backend: str = "auto", visible: Optional[int] = None) -> SubsetChoice:
+    """Rank-0 side: discover the node, optionally probe links, run the placement core.
+
+    ``visible`` overrides the HIP device count (CPU/gloo runs model a mesh of that many devices)."""
     from ..placement import PlacementPolicy, select, worst
     from ..topology.discovery import DiscoveryError, discover, fake_topology
 
-    nvis = _visible_device_count()
+    nvis = _visible_device_count() if visible is None else int(visible)
     t0 = time.perf_counter()
     try:
         topo = discover(backend)
@@ -134,10 +136,13 @@ class AllReduceRunner:
             self.comm = rccl.Comm(bytes(uid), env.world, env.rank, device)
             self.comm.prepare(int(nbytes), dtype)
             self.nbytes = int(self.comm.bytes)
-        elif backend == "torch":
+        elif backend in ("torch", "cpu"):
             tdt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[dtype]
+            if backend == "cpu" and tdt != torch.float32:
+                tdt = torch.float32  # gloo reduces fp32 natively
             esz = torch.empty((), dtype=tdt).element_size()
-            self.tensor = torch.ones(max(1, int(nbytes) // esz), dtype=tdt, device=f"cuda:{device}")
+            dev = "cpu" if backend == "cpu" else f"cuda:{device}"
+            self.tensor = torch.ones(max(1, int(nbytes) // esz), dtype=tdt, device=dev)
             self.nbytes = self.tensor.numel() * esz
         else:
             raise ValueError(backend)
@@ -165,6 +170,8 @@ class AllReduceRunner:
     def synchronize(self) -> None:
         if self.comm is not None:
             self.comm.synchronize()
+        if self.backend == "cpu":
+            return
         import torch
 
         torch.cuda.synchronize(self.device)
