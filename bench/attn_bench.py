@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""HIP MFMA flash attention vs torch SDPA (ROCm library kernels) at the Llama-3-8B training shape.
+
+    python bench/attn_bench.py [--b 2 --s 4096 --h 32 --hkv 8 --iters 10]
+
+Random gaussian bf16 inputs (guide rule 25: never zeros).  FLOPs counted as causal:
+fwd 2 * 2 * B*H*S*S*D / 2, bwd 2.5x fwd.
+"""
+import argparse
+import json
+import time
+
+import torch
+import torch.nn.functional as F
+
+from gpu_topology_on_k8s_amd.ops import fused
+
+
+def timeit(fn, iters):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--b", type=int, default=2)
+    ap.add_argument("--s", type=int, default=4096)
+    ap.add_argument("--h", type=int, default=32)
+    ap.add_argument("--hkv", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    B, S, H, Hkv, Dh = a.b, a.s, a.h, a.hkv, 128
+    q = torch.randn(B, H, S, Dh, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, S, Dh, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, S, Dh, device="cuda", dtype=torch.bfloat16)
+    do = torch.randn(B, S, H, Dh, device="cuda", dtype=torch.bfloat16)
+    fwd_flops = 2 * 2 * B * H * S * S * Dh / 2
+    res = {"shape": {"B": B, "S": S, "H": H, "Hkv": Hkv, "D": Dh}}
+    hip = fused.hip()
+    o, lse = hip.attn_fwd(q, k, v, Dh ** -0.5)
+    t = timeit(lambda: hip.attn_fwd(q, k, v, Dh ** -0.5), a.iters)
+    res["hip_fwd_ms"] = t * 1e3
+    res["hip_fwd_tflops"] = fwd_flops / t / 1e12
+    t = timeit(lambda: hip.attn_bwd(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
+    res["hip_bwd_ms"] = t * 1e3
+    res["hip_bwd_tflops"] = 2.5 * fwd_flops / t / 1e12
+    try:
+        t = timeit(lambda: F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True), a.iters)
+        res["sdpa_fwd_ms"] = t * 1e3
+        res["sdpa_fwd_tflops"] = fwd_flops / t / 1e12
+        qq, kk, vv = (x.clone().requires_grad_(True) for x in (q, k, v))
+        out = F.scaled_dot_product_attention(qq, kk, vv, is_causal=True, enable_gqa=True)
+        g = do.transpose(1, 2).contiguous()
+        t = timeit(lambda: torch.autograd.grad(out, (qq, kk, vv), g, retain_graph=True), a.iters)
+        res["sdpa_bwd_ms"] = t * 1e3
+        res["sdpa_bwd_tflops"] = 2.5 * fwd_flops / t / 1e12
+    except Exception as e:  # pragma: no cover
+        res["sdpa_error"] = str(e)[:300]
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

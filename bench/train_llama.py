@@ -49,7 +49,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--bucket-mb", type=float, default=256.0)
-    ap.add_argument("--attn", default="sdpa")
+    ap.add_argument("--attn", default="hip", choices=["hip", "sdpa", "sdpa-expand"])
     ap.add_argument("--checkpoint", action="store_true")
     ap.add_argument("--timeout", type=int, default=1500)
     ap.add_argument("--placements", default="best,worst")

@@ -1,0 +1,414 @@
+// Causal GQA flash attention for gfx950 (MFMA 32x32x16 bf16), forward and backward.
+//
+// Part of the Llama-3 validation workload (BASELINE config 5); replaces the SDPA dispatch (whose
+// ROCm flash path is Triton-compiled) with hand-written CDNA4 code.  Head dim 128, bf16 I/O,
+// fp32 accumulation and softmax.
+//
+// Forward (one 256-thread workgroup = 4 waves = 128 queries of one (batch, q-head); KV tiles of 64):
+//   * "swapped" QK^T: each wave computes S^T = K . Q^T, so the accumulator holds one QUERY per lane
+//     (lane & 31) and 16 keys per 32-key sub-tile in registers; the row max / row sum need only
+//     in-lane reductions plus one exchange with lane ^ 32.
+//   * that accumulator, rounded to bf16, IS the B operand of O^T += V^T . P^T (§3 "accumulator as the
+//     next MFMA's operand"), with V^T fragments gathered by ds_read_b64_tr_b16 from the row-major V
+//     tile: no P round trip through LDS.
+//   * K and V tiles share one XOR-swizzled LDS image ((b) of guide T10): 16-B chunk ch of row r at
+//     256*r + 16*(ch ^ (((r&3)<<2) | ((r>>2)&3))) — conflict-free for both the ds_read_b128 row reads
+//     of K and the transposed reads of V.
+//   * register-staged K/V prefetch: the next tile's global loads are issued before this tile's MFMAs
+//     and written to LDS after the barrier (guide T14).  Query blocks are launched heaviest-first.
+//   * output O is written token-major [B, S, H, D] (what the o-projection GEMM consumes) and the
+//     row log-sum-exp in log2 units for the backward.
+// Backward (one workgroup = 4 waves = 128 keys of one (batch, kv-head); sweeps every q-head of the
+// GQA group x 32-query slices, so dK/dV never need a cross-workgroup sum):
+//   * key on the lane for S = Q.K^T and dP = dO.V^T; P and dS accumulators feed dV^T += dO^T.P and
+//     dK^T += Q^T.dS directly as B operands (dO^T, Q^T by transposed LDS reads);
+//   * dS crosses LDS once (a [key][query] image written with 8-B stores, read transposed) for
+//     dQ = dS.K, summed over workgroups with fp32 atomics (one register = 128 contiguous bytes).
+#include <hip/hip_runtime.h>
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+
+#include <cmath>
+#include <cstdint>
+
+namespace gtk_attn {
+
+typedef unsigned short u16;
+typedef u16 u16x8 __attribute__((ext_vector_type(8)));
+typedef u16 u16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int D = 128;
+constexpr int BQ = 128;  // forward: queries per workgroup
+constexpr int BK = 64;   // forward: keys per tile
+constexpr int KB = 128;  // backward: keys per workgroup
+constexpr int QT = 32;   // backward: queries per slice
+
+#define LDS_AS __attribute__((address_space(3)))
+
+__device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float((uint32_t)v << 16); }
+__device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
+
+// byte offset of 16-B chunk `ch` of row `row` in a [rows][128 x bf16] swizzled image
+__device__ __forceinline__ int swz(int row, int ch) { return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3))); }
+// accumulator register -> row of a 32x32 MFMA tile (lane half hh)
+__device__ __forceinline__ int crow(int reg, int hh) { return (reg & 3) + 8 * (reg >> 2) + 4 * hh; }
+
+__device__ __forceinline__ bf16x8 lds_b128(const char* base, int off) { return *reinterpret_cast<const bf16x8*>(base + off); }
+
+__device__ __forceinline__ s16x4 lds_tr(const char* base, int off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(base + off));
+}
+
+// Transposed A fragment of a 32x32x16 MFMA whose k index walks ROWS of a [rows][128] swizzled image
+// and whose output row walks COLUMNS: element j of lane (r, hh) = img[row_of(j)][col0 + r] where
+// rows are r_lo + {0..3} (j < 4) and r_hi + {0..3} (j >= 4).  r_lo/r_hi are per-half (caller adds 4*hh).
+__device__ __forceinline__ bf16x8 tr_frag(const char* img, int lane, int r_lo, int r_hi, int col0) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int col = col0 + 16 * (g & 1);  // first column this 16-lane group delivers
+  const int ch = (col >> 3) + (p >> 1);
+  s16x4 lo = lds_tr(img, swz(r_lo + q, ch) + 8 * (p & 1));
+  s16x4 hi = lds_tr(img, swz(r_hi + q, ch) + 8 * (p & 1));
+  bf16x8 out;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    out[j] = __builtin_bit_cast(__bf16, lo[j]);
+    out[j + 4] = __builtin_bit_cast(__bf16, hi[j]);
+  }
+  return out;
+}
+
+__device__ __forceinline__ bf16x8 pack8(const f32x16& acc, int base) {
+  bf16x8 out;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = (__bf16)acc[base + j];
+  return out;
+}
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// ==================================================================================== forward
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
+                                                          const u16* __restrict__ v, u16* __restrict__ o,
+                                                          float* __restrict__ lse2, int H, int Hkv, int S, float c) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * BK * D * 2];  // K image | V image
+  char* kimg = smem;
+  char* vimg = smem + BK * D * 2;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, hh = lane >> 5;
+  const int nqb = gridDim.x;
+  const int qb = nqb - 1 - blockIdx.x;  // heaviest (most keys) first
+  const int bh = blockIdx.y, b = bh / H, hq = bh % H, hk = hq / (H / Hkv);
+  const u16* qp = q + ((size_t)(b * H + hq) * S) * D;
+  const u16* kp = k + ((size_t)(b * Hkv + hk) * S) * D;
+  const u16* vp = v + ((size_t)(b * Hkv + hk) * S) * D;
+  const int q0 = qb * BQ + w * 32;
+  const int myq = q0 + r;
+
+  bf16x8 qf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + (size_t)myq * D + 16 * s + 8 * hh);
+
+  f32x16 oacc[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) oacc[dt] = f32x16{};
+  float m = -INFINITY, l = 0.f;
+
+  const int ntiles = (qb * BQ + BQ) / BK;
+  u16x8 stk[4], stv[4];
+  const int srow = t >> 4, sch = t & 15;
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const size_t row = (size_t)kt * BK + i * 16 + srow;
+      stk[i] = *reinterpret_cast<const u16x8*>(kp + row * D + sch * 8);
+      stv[i] = *reinterpret_cast<const u16x8*>(vp + row * D + sch * 8);
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      *reinterpret_cast<u16x8*>(kimg + swz(i * 16 + srow, sch)) = stk[i];
+      *reinterpret_cast<u16x8*>(vimg + swz(i * 16 + srow, sch)) = stv[i];
+    }
+  };
+
+  gload(0);
+  lstore();
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    if (kt + 1 < ntiles) gload(kt + 1);  // in flight under this tile's MFMAs (T14)
+    const int key0 = kt * BK;
+    if (key0 <= q0 + 31) {  // wave-uniform: some key of this tile is visible to some query of this wave
+      f32x16 s0 = f32x16{}, s1 = f32x16{};
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        s0 = mfma(lds_b128(kimg, swz(r, 2 * s + hh)), qf[s], s0);
+        s1 = mfma(lds_b128(kimg, swz(32 + r, 2 * s + hh)), qf[s], s1);
+      }
+      const bool diag = key0 + BK - 1 > q0;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float x0 = s0[i] * c, x1 = s1[i] * c;
+        if (diag) {
+          const int k0i = key0 + crow(i, hh);
+          if (k0i > myq) x0 = -INFINITY;
+          if (k0i + 32 > myq) x1 = -INFINITY;
+        }
+        s0[i] = x0;
+        s1[i] = x1;
+        mx = fmaxf(mx, fmaxf(x0, x1));
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m, mx);
+      const float alpha = exp2f(m - mnew);
+      float rs = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        s0[i] = exp2f(s0[i] - mnew);
+        s1[i] = exp2f(s1[i] - mnew);
+        rs += s0[i] + s1[i];
+      }
+      rs += __shfl_xor(rs, 32, 64);
+      l = l * alpha + rs;
+      m = mnew;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+      const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 8), p10 = pack8(s1, 0), p11 = pack8(s1, 8);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int col0 = 32 * dt;
+        oacc[dt] = mfma(tr_frag(vimg, lane, 0 + 4 * hh, 8 + 4 * hh, col0), p00, oacc[dt]);
+        oacc[dt] = mfma(tr_frag(vimg, lane, 16 + 4 * hh, 24 + 4 * hh, col0), p01, oacc[dt]);
+        oacc[dt] = mfma(tr_frag(vimg, lane, 32 + 4 * hh, 40 + 4 * hh, col0), p10, oacc[dt]);
+        oacc[dt] = mfma(tr_frag(vimg, lane, 48 + 4 * hh, 56 + 4 * hh, col0), p11, oacc[dt]);
+      }
+    }
+    __syncthreads();  // every wave is done with this tile's image
+    if (kt + 1 < ntiles) {
+      lstore();
+      __syncthreads();
+    }
+  }
+  const float inv = 1.f / l;
+  u16* orow = o + (((size_t)b * S + myq) * (size_t)(H) + hq) * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u16x4 v4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v4[e] = f2bf(oacc[dt][4 * g4 + e] * inv);
+      *reinterpret_cast<u16x4*>(orow + 32 * dt + 8 * g4 + 4 * hh) = v4;
+    }
+  if (hh == 0) lse2[(size_t)(b * H + hq) * S + myq] = m + log2f(l);
+}
+
+// ==================================================================================== backward
+// delta[b, h, q] = sum_d dO[b, q, h, d] * O[b, q, h, d]   (one 16-lane group per row)
+__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
+                                                           float* __restrict__ delta, int B, int H, int S) {
+  const int row = blockIdx.x * 16 + (threadIdx.x >> 4);  // row = (b*S + s)*H + h
+  const int i = threadIdx.x & 15;
+  if (row >= B * S * H) return;
+  const u16x8 a = reinterpret_cast<const u16x8*>(dout + (size_t)row * D)[i];
+  const u16x8 bb = reinterpret_cast<const u16x8*>(out + (size_t)row * D)[i];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += bf2f(a[j]) * bf2f(bb[j]);
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) s += __shfl_xor(s, off, 16);
+  if (i == 0) {
+    const int h = row % H, bs = row / H, sidx = bs % S, bidx = bs / S;
+    delta[((size_t)bidx * H + h) * S + sidx] = s;
+  }
+}
+
+__global__ __launch_bounds__(256, 1) void attn_bwd_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
+                                                          const u16* __restrict__ v, const u16* __restrict__ dout,
+                                                          const float* __restrict__ lse2, const float* __restrict__ delta,
+                                                          float* __restrict__ dqacc, u16* __restrict__ dk, u16* __restrict__ dv,
+                                                          int H, int Hkv, int S, float c, float scale) {
+  // K image | V image | Q slice | dO slice | dS^T image [key][query] (64-B rows) | lse | delta
+  __shared__ __attribute__((aligned(16))) char smem[KB * D * 2 * 2 + QT * D * 2 * 2 + KB * QT * 2 + QT * 4 * 2];
+  char* kimg = smem;
+  char* vimg = kimg + KB * D * 2;
+  char* qimg = vimg + KB * D * 2;
+  char* doimg = qimg + QT * D * 2;
+  char* dsimg = doimg + QT * D * 2;
+  float* slse = reinterpret_cast<float*>(dsimg + KB * QT * 2);
+  float* sdel = slse + QT;
+
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, hh = lane >> 5;
+  const int kb = blockIdx.x;  // key block (low blocks see the most queries: launched first)
+  const int bk = blockIdx.y, b = bk / Hkv, hk = bk % Hkv, G = H / Hkv;
+  const u16* kp = k + ((size_t)(b * Hkv + hk) * S + (size_t)kb * KB) * D;
+  const u16* vp = v + ((size_t)(b * Hkv + hk) * S + (size_t)kb * KB) * D;
+  // stage this workgroup's K and V (128 x 128 each) once
+  for (int idx = t; idx < KB * 16; idx += 256) {
+    const int row = idx >> 4, ch = idx & 15;
+    *reinterpret_cast<u16x8*>(kimg + swz(row, ch)) = *reinterpret_cast<const u16x8*>(kp + (size_t)row * D + ch * 8);
+    *reinterpret_cast<u16x8*>(vimg + swz(row, ch)) = *reinterpret_cast<const u16x8*>(vp + (size_t)row * D + ch * 8);
+  }
+  f32x16 dvt[4], dkt[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dvt[dt] = dkt[dt] = f32x16{};
+  const int mykey = kb * KB + w * 32 + r;  // key held on this lane
+  const int krow = w * 32 + r;             // its row in the K/V image
+
+  const int qt0 = (kb * KB) / QT;
+  const int nqt = S / QT;
+  for (int hi = 0; hi < G; ++hi) {
+    const int hq = hk * G + hi;
+    const u16* qp = q + ((size_t)(b * H + hq) * S) * D;
+    for (int qt = qt0; qt < nqt; ++qt) {
+      const int qbase = qt * QT;
+      __syncthreads();  // previous slice fully consumed (and K/V staged on the first pass)
+      for (int idx = t; idx < QT * 16; idx += 256) {
+        const int row = idx >> 4, ch = idx & 15;
+        *reinterpret_cast<u16x8*>(qimg + swz(row, ch)) = *reinterpret_cast<const u16x8*>(qp + (size_t)(qbase + row) * D + ch * 8);
+        *reinterpret_cast<u16x8*>(doimg + swz(row, ch)) =
+            *reinterpret_cast<const u16x8*>(dout + (((size_t)b * S + qbase + row) * H + hq) * D + ch * 8);
+      }
+      if (t < QT) slse[t] = lse2[((size_t)b * H + hq) * S + qbase + t];
+      else if (t < 2 * QT) sdel[t - QT] = delta[((size_t)b * H + hq) * S + qbase + t - QT];
+      __syncthreads();
+
+      // S = Q.K^T and dP = dO.V^T with the key on the lane (rows = queries crow(i, hh))
+      f32x16 sacc = f32x16{}, dpacc = f32x16{};
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const bf16x8 kb8 = lds_b128(kimg, swz(krow, 2 * s + hh));
+        const bf16x8 vb8 = lds_b128(vimg, swz(krow, 2 * s + hh));
+        sacc = mfma(lds_b128(qimg, swz(r, 2 * s + hh)), kb8, sacc);
+        dpacc = mfma(lds_b128(doimg, swz(r, 2 * s + hh)), vb8, dpacc);
+      }
+      f32x16 p, ds;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qi = crow(i, hh);
+        const float pv = (mykey > qbase + qi) ? 0.f : exp2f(sacc[i] * c - slse[qi]);
+        p[i] = pv;
+        ds[i] = pv * (dpacc[i] - sdel[qi]);
+      }
+      const bf16x8 p0 = pack8(p, 0), p1 = pack8(p, 8), d0 = pack8(ds, 0), d1 = pack8(ds, 8);
+      // dV^T += dO^T . P ; dK^T += Q^T . dS   (k = query: rows 16t + 8(j>>2) + 4hh + (j&3))
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dvt[dt] = mfma(tr_frag(doimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), p0, dvt[dt]);
+        dvt[dt] = mfma(tr_frag(doimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), p1, dvt[dt]);
+        dkt[dt] = mfma(tr_frag(qimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), d0, dkt[dt]);
+        dkt[dt] = mfma(tr_frag(qimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), d1, dkt[dt]);
+      }
+      // dS^T image: row = key (krow), 64-B rows of 32 queries; regs 4g..4g+3 = queries 8g + 4hh + 0..3
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u16x4 v4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v4[e] = f2bf(ds[4 * g + e]);
+        *reinterpret_cast<u16x4*>(dsimg + krow * 64 + 2 * (8 * g + 4 * hh)) = v4;
+      }
+      __syncthreads();
+      // dQ[q][d] = sum_key dS[q][key] K[key][d]; wave w owns d columns 32w..32w+31, k = 128 keys
+      f32x16 dq = f32x16{};
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        // A[row q = r][k = key 16s + 8hh + j] = dS^T[key][q]: transposed read of the dS image
+        const int gq = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
+        const int qcol = 16 * (gq & 1);  // first query column of this 16-lane group
+        const int kr = 16 * s + 8 * hh + qq;
+        s16x4 lo = lds_tr(dsimg, kr * 64 + 2 * (qcol + 4 * pp));
+        s16x4 hi4 = lds_tr(dsimg, (kr + 4) * 64 + 2 * (qcol + 4 * pp));
+        bf16x8 a;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] = __builtin_bit_cast(__bf16, lo[j]);
+          a[j + 4] = __builtin_bit_cast(__bf16, hi4[j]);
+        }
+        // B[k = key 16s + 8hh + j][col = d 32w + r] = K[key][d]: transposed read of the K image
+        const bf16x8 bkf = tr_frag(kimg, lane, 16 * s + 8 * hh, 16 * s + 8 * hh + 4, 32 * w);
+        dq = mfma(a, bkf, dq);
+      }
+      float* dqrow = dqacc + ((size_t)(b * H + hq) * S + qbase) * D + 32 * w + r;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) atomicAdd(dqrow + (size_t)crow(i, hh) * D, dq[i]);
+    }
+  }
+  // dK = scale * dK^T^T, dV = dV^T^T : lane = key, regs = d rows (crow) -> 8-B stores per 4 d
+  u16* dkrow = dk + ((size_t)(b * Hkv + hk) * S + mykey) * D;
+  u16* dvrow = dv + ((size_t)(b * Hkv + hk) * S + mykey) * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u16x4 a4, b4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a4[e] = f2bf(dkt[dt][4 * g4 + e] * scale);
+        b4[e] = f2bf(dvt[dt][4 * g4 + e]);
+      }
+      *reinterpret_cast<u16x4*>(dkrow + 32 * dt + 8 * g4 + 4 * hh) = a4;
+      *reinterpret_cast<u16x4*>(dvrow + 32 * dt + 8 * g4 + 4 * hh) = b4;
+    }
+}
+
+__global__ __launch_bounds__(256) void scale_cast_kernel(const float* __restrict__ x, u16* __restrict__ y, float s, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) y[i] = f2bf(x[i] * s);
+}
+
+// ==================================================================================== host
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+const u16* bp(const at::Tensor& t) { return reinterpret_cast<const u16*>(t.data_ptr()); }
+u16* bpm(at::Tensor& t) { return reinterpret_cast<u16*>(t.data_ptr()); }
+
+void check_qkv(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
+  for (const at::Tensor* x : {&q, &k, &v})
+    TORCH_CHECK(x->is_cuda() && x->scalar_type() == at::kBFloat16 && x->is_contiguous() && x->dim() == 4,
+                "attention: q/k/v must be contiguous bf16 [B, heads, S, D] GPU tensors");
+  TORCH_CHECK(q.size(3) == D && k.size(3) == D && v.size(3) == D, "attention: head dim must be 128");
+  TORCH_CHECK(k.sizes() == v.sizes() && q.size(0) == k.size(0) && q.size(2) == k.size(2), "attention: shape mismatch");
+  TORCH_CHECK(q.size(1) % k.size(1) == 0, "attention: q heads must be a multiple of kv heads");
+  TORCH_CHECK(q.size(2) % BQ == 0, "attention: sequence length must be a multiple of 128");
+}
+
+std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale) {
+  check_qkv(q, k, v);
+  const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
+  auto o = at::empty({B, S, H, D}, q.options());
+  auto lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+  const float c = (float)(scale * 1.4426950408889634);
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(S / BQ, B * H), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bpm(o),
+                     lse.data_ptr<float>(), H, Hkv, S, c);
+  return {o, lse};
+}
+
+std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                 const at::Tensor& out, const at::Tensor& lse, double scale) {
+  check_qkv(q, k, v);
+  const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
+  TORCH_CHECK(dout.is_contiguous() && out.is_contiguous() && dout.numel() == q.numel() && out.numel() == q.numel(),
+              "attention bwd: dout/out must be contiguous [B, S, H, D]");
+  auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+  auto dqacc = at::zeros({B, H, S, D}, q.options().dtype(at::kFloat));
+  auto dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
+  const int rows = B * S * H;
+  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
+                     delta.data_ptr<float>(), B, H, S);
+  const float c = (float)(scale * 1.4426950408889634);
+  hipLaunchKernelGGL(attn_bwd_kernel, dim3(S / KB, B * Hkv), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
+                     lse.data_ptr<float>(), delta.data_ptr<float>(), dqacc.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c,
+                     (float)scale);
+  const size_t n = dq.numel();
+  hipLaunchKernelGGL(scale_cast_kernel, dim3((unsigned)std::min<size_t>((n + 255) / 256, 4096)), dim3(256), 0, cur_stream(),
+                     dqacc.data_ptr<float>(), bpm(dq), (float)scale, n);
+  return {dq, dk, dv};
+}
+
+}  // namespace gtk_attn

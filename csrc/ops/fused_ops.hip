@@ -157,13 +157,25 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const u16* __restrict_
   }
 }
 
-// column sums of [P, D] fp32 partials -> bf16 [D]
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, u16* __restrict__ out, int P, int D) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= D) return;
+// Column sums of [P, D] fp32 partials.  Grid (ceil(D/64), kColSplit): each block owns 64 columns
+// (one 256-B coalesced row segment per wave-instruction) and a 1/kColSplit slice of the rows; its 4
+// waves stride the slice, combine through LDS, and one fp32 atomic per column per block lands in acc.
+constexpr int kColSplit = 8;
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, float* __restrict__ acc, int P, int D) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(size_t)p * D + col];
-  out[col] = f2bf(s);
+  if (col < D)
+    for (int p = blockIdx.y * 4 + wave; p < P; p += kColSplit * 4) s += part[(size_t)p * D + col];
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && col < D) atomicAdd(acc + col, red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
+}
+
+__global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restrict__ x, u16* __restrict__ y, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) y[i] = f2bf(x[i]);
 }
 
 template <int NV>
@@ -207,8 +219,8 @@ std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, c
   TORCH_CHECK(dy.numel() == x.numel() && rstd.numel() == M, "rmsnorm_bwd: shape mismatch");
   auto dx = at::empty_like(x);
   auto dw = at::empty({D}, w.options());
-  // enough waves to fill the chip (>= 4 per CU), but each wave gets several rows so dW partials stay small
-  int grid = std::max(1, std::min((M + 3) / 4, 1024));
+  // 1024 waves (4 per CU) fill the chip; each takes M/1024 rows so the dW partials stay at 16 MB
+  int grid = std::max(1, std::min((M + 3) / 4, 256));
   auto part = at::empty({(int64_t)grid * 4, D}, x.options().dtype(at::kFloat));
   if (M > 0) {
     const int nv = (D + 511) / 512;
@@ -220,8 +232,10 @@ std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, c
   } else {
     part.zero_();
   }
-  hipLaunchKernelGGL(colsum_kernel, dim3((D + 255) / 256), dim3(256), 0, cur_stream(), part.data_ptr<float>(), bpm(dw),
-                     grid * 4, D);
+  auto acc = at::zeros({D}, x.options().dtype(at::kFloat));
+  hipLaunchKernelGGL(colsum_kernel, dim3((D + 63) / 64, kColSplit), dim3(256), 0, cur_stream(), part.data_ptr<float>(),
+                     acc.data_ptr<float>(), grid * 4, D);
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((D + 255) / 256), dim3(256), 0, cur_stream(), acc.data_ptr<float>(), bpm(dw), D);
   return {dx, dw};
 }
 
@@ -579,7 +593,15 @@ at::Tensor sq_norm(const at::Tensor& g) {
 
 }  // namespace
 
+namespace gtk_attn {  // csrc/ops/attention.hip
+std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale);
+std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                 const at::Tensor& out, const at::Tensor& lse, double scale);
+}  // namespace gtk_attn
+
 PYBIND11_MODULE(_fused, m) {
+  m.def("attn_fwd", &gtk_attn::attn_fwd, "causal GQA flash attention forward (bf16, D=128): -> (o [B,S,H,D], lse2 [B,H,S])");
+  m.def("attn_bwd", &gtk_attn::attn_bwd, "flash attention backward: -> (dq, dk, dv)");
   m.doc() = "gfx950 fused kernels for the Llama-3 DP validation workload";
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);

@@ -126,7 +126,7 @@ class FlatParams:
 
 
 class Llama(torch.nn.Module):
-    def __init__(self, cfg: LlamaConfig, device="cuda", seed: int = 0, checkpoint: bool = False, attn: str = "sdpa"):
+    def __init__(self, cfg: LlamaConfig, device="cuda", seed: int = 0, checkpoint: bool = False, attn: str = "hip"):
         super().__init__()
         self.cfg = cfg
         self.checkpoint = checkpoint
@@ -161,14 +161,18 @@ class Llama(torch.nn.Module):
 
     # ---------------------------------------------------------------- blocks
     def _attention(self, q, k, v):
-        if self.attn == "sdpa":
-            return F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=q.size(1) != k.size(1))
-        # explicit GQA expansion (fallback when the SDPA backend lacks native GQA)
-        rep = q.size(1) // k.size(1)
-        if rep > 1:
-            k = k.repeat_interleave(rep, dim=1)
-            v = v.repeat_interleave(rep, dim=1)
-        return F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        """q [B,H,S,Dh], k/v [B,Hkv,S,Dh] -> [B,S,H,Dh] (token-major, what the o-projection reads)."""
+        if self.attn == "hip" and (not q.is_cuda or fused.flash_attention_supported(q, k)):
+            return fused.attention(q, k, v)  # HIP MFMA flash attention (PyTorch reference on CPU)
+        if self.attn in ("hip", "sdpa"):  # library SDPA: A/B baseline, or shapes the HIP kernel does not cover
+            o = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=q.size(1) != k.size(1))
+        else:  # "sdpa-expand": explicit GQA expansion for SDPA backends without native GQA
+            rep = q.size(1) // k.size(1)
+            if rep > 1:
+                k = k.repeat_interleave(rep, dim=1)
+                v = v.repeat_interleave(rep, dim=1)
+            o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        return o.transpose(1, 2)
 
     def _layer(self, i: int, x: torch.Tensor, B: int, S: int) -> torch.Tensor:
         cfg = self.cfg
@@ -176,8 +180,7 @@ class Llama(torch.nn.Module):
         h = fused.rmsnorm(x, self.P(f"l{i}.attn_norm"), cfg.norm_eps)
         qkv = F.linear(h, self.P(f"l{i}.wqkv"))
         q, k, v = fused.rope_split(qkv, self.rope_cos, self.rope_sin, B, S, H, Hkv, Dh)
-        o = self._attention(q, k, v)  # [B, H, S, Dh]
-        o = o.transpose(1, 2).reshape(B * S, H * Dh)
+        o = self._attention(q, k, v).reshape(B * S, H * Dh)  # [B, S, H, Dh] -> [B*S, H*Dh]
         x = x + F.linear(o, self.P(f"l{i}.wo"))
         h = fused.rmsnorm(x, self.P(f"l{i}.ffn_norm"), cfg.norm_eps)
         x = x + F.linear(fused.swiglu(F.linear(h, self.P(f"l{i}.w13"))), self.P(f"l{i}.w2"))

@@ -57,7 +57,7 @@ def _choose_device(env, placement: str, discovery: str) -> Dict[str, object]:
 
 def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int = 3, warmup: int = 1, device_kind: str = "cuda",
           placement: str = "best", discovery: str = "auto", bucket_mb: float = 256.0, checkpoint: bool = False, lr: float = 3e-4,
-          attn: str = "sdpa", seed: int = 0, log: bool = True) -> Dict[str, object]:
+          attn: str = "hip", seed: int = 0, log: bool = True) -> Dict[str, object]:
     env = _init_dist(device_kind)
     if device_kind == "cuda":
         pl = _choose_device(env, placement, discovery)
@@ -150,7 +150,7 @@ def main(argv=None) -> int:
     ap.add_argument("--discovery", default="auto")
     ap.add_argument("--bucket-mb", type=float, default=256.0)
     ap.add_argument("--checkpoint", action="store_true")
-    ap.add_argument("--attn", default="sdpa", choices=["sdpa", "sdpa-expand"])
+    ap.add_argument("--attn", default="hip", choices=["hip", "sdpa", "sdpa-expand"])
     a = ap.parse_args(argv)
     train(a.model, a.batch, a.seq, a.steps, a.warmup, a.device, a.placement, a.discovery, a.bucket_mb, a.checkpoint, attn=a.attn)
     if dist.is_initialized():

@@ -14,7 +14,7 @@ from .._native import load
 
 __all__ = [
     "rmsnorm", "rmsnorm_ref", "rope_tables", "rope_split", "rope_split_ref", "swiglu", "swiglu_ref", "cross_entropy",
-    "cross_entropy_ref", "hip",
+    "cross_entropy_ref", "hip", "attention", "attention_ref", "flash_attention_supported",
 ]
 
 
@@ -161,3 +161,47 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int 
     if logits.is_cuda:
         return _CrossEntropy.apply(logits, labels, ignore_index)
     return cross_entropy_ref(logits, labels, ignore_index)
+
+
+# ------------------------------------------------------------------------------------ attention
+def attention_ref(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | None = None) -> torch.Tensor:
+    """fp32 causal GQA attention: q [B,H,S,D], k/v [B,Hkv,S,D] -> o [B,S,H,D] (same dtype as q)."""
+    B, H, S, Dh = q.shape
+    rep = H // k.size(1)
+    kf = k.float().repeat_interleave(rep, dim=1)
+    vf = v.float().repeat_interleave(rep, dim=1)
+    sc = (scale if scale is not None else Dh ** -0.5)
+    s = torch.matmul(q.float(), kf.transpose(-1, -2)) * sc
+    mask = torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1)
+    p = torch.softmax(s.masked_fill(mask, float("-inf")), dim=-1)
+    return torch.matmul(p, vf).transpose(1, 2).to(q.dtype).contiguous()
+
+
+class _FlashAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, scale):
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        o, lse = hip().attn_fwd(q, k, v, float(scale))
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.scale = float(scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        dq, dk, dv = hip().attn_bwd(do.contiguous(), q, k, v, o, lse, ctx.scale)
+        return dq, dk, dv, None
+
+
+def flash_attention_supported(q: torch.Tensor, k: torch.Tensor) -> bool:
+    return q.is_cuda and q.dtype == torch.bfloat16 and q.size(-1) == 128 and q.size(2) % 128 == 0 and q.size(1) % k.size(1) == 0
+
+
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | None = None) -> torch.Tensor:
+    """Causal GQA attention -> [B, S, H, D]; the HIP flash kernel on GPU (head dim 128, S % 128 == 0)."""
+    sc = scale if scale is not None else q.size(-1) ** -0.5
+    if q.is_cuda:
+        if not flash_attention_supported(q, k):
+            raise ValueError("HIP flash attention needs bf16, head dim 128 and S % 128 == 0")
+        return _FlashAttention.apply(q, k, v, sc)
+    return attention_ref(q, k, v, sc)
