@@ -8,12 +8,15 @@ fwd 2 * 2 * B*H*S*S*D / 2, bwd 2.5x fwd.
 """
 import argparse
 import json
+import os
+import sys
 import time
 
 import torch
 import torch.nn.functional as F
 
-from gpu_topology_on_k8s_amd.ops import fused
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gpu_topology_on_k8s_amd.ops import fused  # noqa: E402
 
 
 def timeit(fn, iters):

@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""Gaia experiments 1-4 through the whole stack: placement tables + mean scheduling time.
+
+    python bench/sched_bench.py [--reps 500] [--out profiles/sched/sched_bench.json]
+
+Paper p.6-7: each request is submitted REPS times from a fixed node state (Fig. 7 tree: SOC ->
+{PXB{GPU0 c2, GPU1 c2}, PIX{GPU2 c1, GPU3 c1}}) and the chosen GPU sets are tallied (Tables I-IV);
+Fig. 10 reports the mean scheduling time (2.53-3.56 s with Gaia on k8s 1.9).  Here every repetition
+is a real pass through the in-process cluster: mini-scheduler -> HTTP extender (filter, sort, bind)
+-> apiserver annotations -> kubelet GetPreferredAllocation + Allocate over gRPC -> device plugin.
+``sched_ms`` covers filter+sort+bind (the paper's scheduling time); ``admit_ms`` the kubelet side.
+Exp. 2 (fractional 0.5/0.4/0.1 GPUs) has no Kubernetes extended-resource form (integers only), so it
+is reported from the placement core's Fragment policy directly.
+A second section times the exact policy on an 8x MI355X node (the case this framework targets).
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import json
+import os
+import random
+import statistics
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from gpu_topology_on_k8s_amd.k8s import PodAssignment  # noqa: E402
+from gpu_topology_on_k8s_amd.placement import PlacementPolicy, gaia_schedule  # noqa: E402
+from gpu_topology_on_k8s_amd.sim import SimCluster  # noqa: E402
+from gpu_topology_on_k8s_amd.topology import fixtures as fx  # noqa: E402
+from gpu_topology_on_k8s_amd.topology.model import GPUInfo, LinkType, Topology  # noqa: E402
+
+PAPER_SCHED_S = {"exp1": (2.53, 2.66), "exp2": (None, 3.45), "exp3": (2.64, 3.02), "exp4": (2.58, 3.56)}  # (k8s, Gaia), Fig. 10
+
+
+def fig7_topology() -> Topology:
+    tr = fx.f4_tree()
+    cost = np.array([[tr.pair_cost(i, j) for j in range(4)] for i in range(4)], float)
+    return Topology(gpus=[GPUInfo(index=i, numa=[0, 0, 1, 1][i], model="P4") for i in range(4)],
+                    link_type=np.full((4, 4), int(LinkType.PCIE)), hops=np.ones((4, 4), int), cost=cost, node_name="p4")
+
+
+def run_exp(name: str, k: int, pre_used, reps: int, policy: str = "gaia", topo_fn=fig7_topology):
+    tally = collections.Counter()
+    sched, admit = [], []
+    pol = PlacementPolicy(tie_break="random")
+    with SimCluster({"node": topo_fn()}, policy_name=policy, policy=pol) as c:
+        c.extender.cfg.seed = 0
+        for i in range(reps):
+            pods = []
+            if pre_used:
+                p = c.api.create_pod(__import__("gpu_topology_on_k8s_amd.k8s.objects", fromlist=["make_pod"]).make_pod(
+                    f"busy{i}", gpus=len(pre_used), node="node", annotations=PodAssignment(list(pre_used), True, 1).to_annotations()))
+                pods.append(("busy", p))
+            c.submit(f"req{i}", k)
+            (r,) = c.schedule_pending(admit=True)
+            tally[tuple(r.allocated)] += 1
+            sched.append(r.sched_ms)
+            admit.append(r.admit_ms)
+            c.delete(f"req{i}")
+            if pre_used:
+                c.api.delete_pod("default", f"busy{i}")
+    return {
+        "experiment": name, "request_gpus": k, "used_before": list(pre_used), "reps": reps, "policy": policy,
+        "table": {",".join(f"gpu{g}" for g in s): n for s, n in sorted(tally.items())},
+        "sched_ms_mean": statistics.mean(sched), "sched_ms_p50": statistics.median(sched),
+        "sched_ms_p99": sorted(sched)[int(0.99 * (len(sched) - 1))], "admit_ms_mean": statistics.mean(admit),
+        "paper_sched_s": PAPER_SCHED_S.get(name.split("-")[0]),
+    }
+
+
+def exp2_fragments(reps: int):
+    tally = collections.Counter()
+    for _ in range(reps):
+        t = fx.f4_tree()
+        t.mark_used([2], 0.5)
+        a = gaia_schedule(t, 0.4, commit=True)
+        b = gaia_schedule(t, 0.1, commit=True)
+        tally[(tuple(a), tuple(b))] += 1
+    return {"experiment": "exp2", "reps": reps, "table": {f"0.4->gpu{a[0]}, 0.1->gpu{b[0]}": n for (a, b), n in tally.items()},
+            "note": "fractional GPUs have no k8s extended-resource form; placement core only (MI355X: XCP partitions)"}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--reps", type=int, default=500)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    random.seed(0)
+    results = [
+        run_exp("exp1-1gpu", 1, (), a.reps),
+        run_exp("exp1-2gpu", 2, (), a.reps),
+        exp2_fragments(a.reps),
+        run_exp("exp3", 1, (2,), a.reps),
+        run_exp("exp4", 2, (2,), a.reps),
+        run_exp("mi355x-exact-4gpu", 4, (), max(50, a.reps // 5), policy="exact", topo_fn=lambda: fx.f7_mi355x(76.5, 0.03, 1)),
+        run_exp("mi355x-exact-1gpu-after-2", 1, (0, 1), max(50, a.reps // 5), policy="exact", topo_fn=lambda: fx.f7_mi355x(76.5, 0.03, 1)),
+    ]
+    for r in results:
+        print(json.dumps(r))
+    if a.out:
+        os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(results, f, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

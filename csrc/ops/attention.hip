@@ -38,6 +38,7 @@ typedef u16 u16x8 __attribute__((ext_vector_type(8)));
 typedef u16 u16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -63,6 +64,13 @@ __device__ __forceinline__ s16x4 lds_tr(const char* base, int off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(base + off));
 }
 
+// Two transposed 4-element reads -> one bf16x8 MFMA operand.  Whole-vector bit casts only: on ROCm
+// 7.2 (clang 22) a per-element __builtin_bit_cast(__bf16, v[j]) of the tr-read result is folded to
+// element 0 for every j (one ds_read_b64_tr_b16 + v_perm broadcast in the .s), silently wrong.
+__device__ __forceinline__ bf16x8 cat8(s16x4 lo, s16x4 hi) {
+  return __builtin_shufflevector(__builtin_bit_cast(bf16x4, lo), __builtin_bit_cast(bf16x4, hi), 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 // Transposed A fragment of a 32x32x16 MFMA whose k index walks ROWS of a [rows][128] swizzled image
 // and whose output row walks COLUMNS: element j of lane (r, hh) = img[row_of(j)][col0 + r] where
 // rows are r_lo + {0..3} (j < 4) and r_hi + {0..3} (j >= 4).  r_lo/r_hi are per-half (caller adds 4*hh).
@@ -72,13 +80,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* img, int lane, int r_lo, i
   const int ch = (col >> 3) + (p >> 1);
   s16x4 lo = lds_tr(img, swz(r_lo + q, ch) + 8 * (p & 1));
   s16x4 hi = lds_tr(img, swz(r_hi + q, ch) + 8 * (p & 1));
-  bf16x8 out;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    out[j] = __builtin_bit_cast(__bf16, lo[j]);
-    out[j + 4] = __builtin_bit_cast(__bf16, hi[j]);
-  }
-  return out;
+  return cat8(lo, hi);
 }
 
 __device__ __forceinline__ bf16x8 pack8(const f32x16& acc, int base) {
@@ -95,7 +97,8 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 // ==================================================================================== forward
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
                                                           const u16* __restrict__ v, u16* __restrict__ o,
-                                                          float* __restrict__ lse2, int H, int Hkv, int S, float c) {
+                                                          float* __restrict__ lse2, int H, int Hkv, int S, float c,
+                                                          float* __restrict__ dbg) {
   __shared__ __attribute__((aligned(16))) char smem[2 * BK * D * 2];  // K image | V image
   char* kimg = smem;
   char* vimg = smem + BK * D * 2;
@@ -149,6 +152,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const u16* __restrict_
       for (int s = 0; s < 8; ++s) {
         s0 = mfma(lds_b128(kimg, swz(r, 2 * s + hh)), qf[s], s0);
         s1 = mfma(lds_b128(kimg, swz(32 + r, 2 * s + hh)), qf[s], s1);
+      }
+      if (dbg != nullptr && kt == 0) {  // debug: raw S^T accumulators of the first KV tile
+        float* d = dbg + ((((size_t)bh * nqb + qb) * 4 + w) * 64 + lane) * 32;
+        for (int i = 0; i < 16; ++i) {
+          d[i] = s0[i];
+          d[16 + i] = s1[i];
+        }
       }
       const bool diag = key0 + BK - 1 > q0;
       float mx = -INFINITY;
@@ -324,14 +334,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(const u16* __restrict_
         const int gq = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
         const int qcol = 16 * (gq & 1);  // first query column of this 16-lane group
         const int kr = 16 * s + 8 * hh + qq;
-        s16x4 lo = lds_tr(dsimg, kr * 64 + 2 * (qcol + 4 * pp));
-        s16x4 hi4 = lds_tr(dsimg, (kr + 4) * 64 + 2 * (qcol + 4 * pp));
-        bf16x8 a;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          a[j] = __builtin_bit_cast(__bf16, lo[j]);
-          a[j + 4] = __builtin_bit_cast(__bf16, hi4[j]);
-        }
+        const bf16x8 a = cat8(lds_tr(dsimg, kr * 64 + 2 * (qcol + 4 * pp)), lds_tr(dsimg, (kr + 4) * 64 + 2 * (qcol + 4 * pp)));
         // B[k = key 16s + 8hh + j][col = d 32w + r] = K[key][d]: transposed read of the K image
         const bf16x8 bkf = tr_frag(kimg, lane, 16 * s + 8 * hh, 16 * s + 8 * hh + 4, 32 * w);
         dq = mfma(a, bkf, dq);
@@ -359,6 +362,18 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(const u16* __restrict_
     }
 }
 
+// debug: stage a [64][128] bf16 tile into the swizzled image, return what tr_frag delivers per lane
+__global__ __launch_bounds__(64) void tr_probe_kernel(const u16* __restrict__ tile, u16* __restrict__ out, int t, int col0) {
+  __shared__ __attribute__((aligned(16))) char img[BK * D * 2];
+  const int lane = threadIdx.x, hh = lane >> 5;
+  for (int idx = lane; idx < BK * 16; idx += 64) {
+    const int row = idx >> 4, ch = idx & 15;
+    *reinterpret_cast<u16x8*>(img + swz(row, ch)) = *reinterpret_cast<const u16x8*>(tile + row * D + ch * 8);
+  }
+  __syncthreads();
+  *reinterpret_cast<bf16x8*>(out + lane * 8) = tr_frag(img, lane, 16 * t + 4 * hh, 16 * t + 8 + 4 * hh, col0);
+}
+
 __global__ __launch_bounds__(256) void scale_cast_kernel(const float* __restrict__ x, u16* __restrict__ y, float s, size_t n) {
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) y[i] = f2bf(x[i] * s);
 }
@@ -378,15 +393,34 @@ void check_qkv(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
   TORCH_CHECK(q.size(2) % BQ == 0, "attention: sequence length must be a multiple of 128");
 }
 
-std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale) {
+std::vector<at::Tensor> attn_fwd_impl(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale, bool debug) {
   check_qkv(q, k, v);
   const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
   auto o = at::empty({B, S, H, D}, q.options());
   auto lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+  at::Tensor dbg;
+  if (debug) dbg = at::zeros({B * H, S / BQ, 4, 64, 32}, q.options().dtype(at::kFloat));
   const float c = (float)(scale * 1.4426950408889634);
   hipLaunchKernelGGL(attn_fwd_kernel, dim3(S / BQ, B * H), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bpm(o),
-                     lse.data_ptr<float>(), H, Hkv, S, c);
+                     lse.data_ptr<float>(), H, Hkv, S, c, debug ? dbg.data_ptr<float>() : nullptr);
+  if (debug) return {o, lse, dbg};
   return {o, lse};
+}
+
+std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale) {
+  return attn_fwd_impl(q, k, v, scale, false);
+}
+
+at::Tensor attn_tr_probe(const at::Tensor& tile, int64_t t, int64_t col0) {
+  TORCH_CHECK(tile.is_cuda() && tile.scalar_type() == at::kBFloat16 && tile.is_contiguous() && tile.numel() == BK * D);
+  TORCH_CHECK(t >= 0 && t < 4 && col0 >= 0 && col0 <= 96 && col0 % 32 == 0);
+  auto out = at::empty({64, 8}, tile.options());
+  hipLaunchKernelGGL(tr_probe_kernel, dim3(1), dim3(64), 0, cur_stream(), bp(tile), bpm(out), (int)t, (int)col0);
+  return out;
+}
+
+std::vector<at::Tensor> attn_fwd_debug(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale) {
+  return attn_fwd_impl(q, k, v, scale, true);
 }
 
 std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,

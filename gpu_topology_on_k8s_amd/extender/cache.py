@@ -82,7 +82,10 @@ class ClusterCache:
         self._overlay: Dict[str, Dict[str, Alloc]] = {}  # node -> pod -> alloc (binds made here)
         self._lock = threading.RLock()
         self._last_full = 0.0
-        self.overlay_grace = 30.0  # seconds a bind made here may stay invisible in the apiserver view
+        self.overlay_grace = 30.0  # seconds a bind made here may stay invisible in a lagging (cached) view
+        self.consistent_lists = True  # apiserver LISTs without resourceVersion are quorum reads
+        self._epoch = 0
+        self._overlay_epoch: Dict[Tuple[str, str], int] = {}
 
     # ------------------------------------------------------------------ node objects
     def _state(self, name: str) -> NodeState:
@@ -130,7 +133,13 @@ class ClusterCache:
             return None, req
         return Alloc(pod=pod_key(pod), ids=tuple(pa.group), assigned=pa.assigned, assume_time=float(pa.assume_time)), 0
 
-    def _rebuild(self, st: NodeState, pods: List[dict]) -> None:
+    def _next_epoch(self) -> int:
+        with self._lock:
+            self._epoch += 1
+            return self._epoch
+
+    def _rebuild(self, st: NodeState, pods: List[dict], list_epoch: int) -> None:
+        """``list_epoch``: value of the epoch counter taken just before the pods were listed."""
         allocs: Dict[str, Alloc] = {}
         unknown = 0
         seen = set()
@@ -147,10 +156,15 @@ class ClusterCache:
                 a = ov[key]
                 if key in seen:
                     del ov[key]  # the apiserver view has the pod: it is authoritative from now on
+                elif list_epoch > self._overlay_epoch.get((st.name, key), 0) and self.consistent_lists:
+                    del ov[key]  # listed (quorum read) after the bind and absent: the pod is gone
                 elif now - a.assume_time > min(self.ttl, self.overlay_grace):
-                    del ov[key]  # never showed up (deleted right after bind)
+                    del ov[key]  # cached/lagging lists: give up after the grace period
                 else:
                     allocs[key] = a
+            for key in set(self._overlay_epoch) - {(st.name, k) for k in ov}:
+                if key[0] == st.name:
+                    del self._overlay_epoch[key]
         st.allocs = allocs
         st.unknown = unknown
         st.synced_at = now
@@ -159,12 +173,14 @@ class ClusterCache:
         """Authoritative re-read of one node and its pods (used before every bind)."""
         node = self.api.get_node(name)
         st = self.update_node_object(node)
+        epoch = self._next_epoch()
         pods = self.api.list_pods(node_name=name)
         with st.lock:
-            self._rebuild(st, pods)
+            self._rebuild(st, pods, epoch)
         return st
 
     def sync_all(self) -> None:
+        epoch = self._next_epoch()
         nodes = self.api.list_nodes()
         pods = self.api.list_pods()
         by_node: Dict[str, List[dict]] = {}
@@ -177,7 +193,7 @@ class ClusterCache:
             st = self.update_node_object(node)
             names.add(st.name)
             with st.lock:
-                self._rebuild(st, by_node.get(st.name, []))
+                self._rebuild(st, by_node.get(st.name, []), epoch)
         with self._lock:
             for gone in set(self._nodes) - names:
                 del self._nodes[gone]
@@ -206,6 +222,7 @@ class ClusterCache:
                   source="overlay")
         with self._lock:
             self._overlay.setdefault(node, {})[pod] = a
+            self._overlay_epoch[(node, pod)] = self._next_epoch()
         st = self._state(node)
         with st.lock:
             st.allocs[pod] = a
