@@ -93,7 +93,25 @@ def main(argv=None) -> int:
         torch.cuda.set_device(device)
 
     nbytes = int(args.size_mb * (1 << 20))
-    runner = AllReduceRunner(env, device, nbytes, args.dtype, backend=args.backend, inplace=args.inplace)
+    runner = None
+    if args.backend == "native":
+        # The native communicator (csrc/rccl) is the measured path; if its extension cannot be
+        # loaded on some rank, every rank falls back together to dist.all_reduce (the same RCCL).
+        try:
+            runner = AllReduceRunner(env, device, nbytes, args.dtype, backend="native", inplace=args.inplace)
+            ok = 1
+        except Exception as e:  # noqa: BLE001 - reported, then the whole job falls back
+            print(f"bench: native RCCL communicator unavailable on rank {env.rank}: {e}", file=sys.stderr)
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32, device=tdev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 0:
+            if runner is not None:
+                runner.close()
+            runner = None
+            args.backend = "torch"
+    if runner is None:
+        runner = AllReduceRunner(env, device, nbytes, args.dtype, backend=args.backend, inplace=args.inplace)
     wrong = torch.tensor([runner.check()], dtype=torch.int64, device=tdev)
     dist.all_reduce(wrong)
     if int(wrong.item()) != 0:

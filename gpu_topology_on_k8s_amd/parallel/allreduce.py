@@ -144,6 +144,9 @@ class AllReduceRunner:
             dev = "cpu" if backend == "cpu" else f"cuda:{device}"
             self.tensor = torch.ones(max(1, int(nbytes) // esz), dtype=tdt, device=dev)
             self.nbytes = self.tensor.numel() * esz
+            # dist.all_reduce is in place; a 1-rank in-place reduce is a no-op, so for k = 1 each step
+            # copies a source buffer first (the out-of-place semantics the native path measures)
+            self.src = torch.ones_like(self.tensor) if env.world == 1 and not inplace else None
         else:
             raise ValueError(backend)
 
@@ -165,6 +168,8 @@ class AllReduceRunner:
         else:
             import torch.distributed as dist
 
+            if self.src is not None:
+                self.tensor.copy_(self.src)
             dist.all_reduce(self.tensor)
 
     def synchronize(self) -> None:
