@@ -53,6 +53,8 @@ def main():
     t = timeit(lambda: hip.attn_bwd(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
     res["hip_bwd_ms"] = t * 1e3
     res["hip_bwd_tflops"] = 2.5 * fwd_flops / t / 1e12
+    t = timeit(lambda: hip.attn_bwd_atomic(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
+    res["hip_bwd_v1_atomic_ms"] = t * 1e3
     try:
         t = timeit(lambda: F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True), a.iters)
         res["sdpa_fwd_ms"] = t * 1e3

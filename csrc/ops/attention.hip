@@ -378,6 +378,193 @@ __global__ __launch_bounds__(256) void scale_cast_kernel(const float* __restrict
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) y[i] = f2bf(x[i] * s);
 }
 
+// ============================================================================ backward v2 (split)
+// Kernel 1 — dK, dV.  One workgroup = 4 waves = 128 keys of one (batch, kv-head); sweeps every
+// q-head of the GQA group x 32-query slices.  Key on the lane: S = Q.K^T and dP = dO.V^T land with
+// queries in registers, so P and dS feed dV^T += dO^T.P and dK^T += Q^T.dS as B operands directly.
+// No dQ here (kernel 2), hence no atomics and no dS image; K|V|Q|dO images = exactly 80 KiB, so two
+// workgroups share a CU.  Q/dO of the next slice are prefetched into registers under the MFMAs.
+// Per-query constants (lse, delta) come from lane r of the slice via a lane shuffle.
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
+                                                               const u16* __restrict__ v, const u16* __restrict__ dout,
+                                                               const float* __restrict__ lse2, const float* __restrict__ delta,
+                                                               u16* __restrict__ dk, u16* __restrict__ dv, int H, int Hkv, int S,
+                                                               float c, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[KB * D * 2 * 2 + QT * D * 2 * 2];
+  char* kimg = smem;
+  char* vimg = kimg + KB * D * 2;
+  char* qimg = vimg + KB * D * 2;
+  char* doimg = qimg + QT * D * 2;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, hh = lane >> 5;
+  const int kb = blockIdx.x, bk = blockIdx.y, b = bk / Hkv, hk = bk % Hkv, G = H / Hkv;
+  const u16* kp = k + ((size_t)(b * Hkv + hk) * S + (size_t)kb * KB) * D;
+  const u16* vp = v + ((size_t)(b * Hkv + hk) * S + (size_t)kb * KB) * D;
+  for (int idx = t; idx < KB * 16; idx += 256) {
+    const int row = idx >> 4, ch = idx & 15;
+    *reinterpret_cast<u16x8*>(kimg + swz(row, ch)) = *reinterpret_cast<const u16x8*>(kp + (size_t)row * D + ch * 8);
+    *reinterpret_cast<u16x8*>(vimg + swz(row, ch)) = *reinterpret_cast<const u16x8*>(vp + (size_t)row * D + ch * 8);
+  }
+  f32x16 dvt[4], dkt[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dvt[dt] = dkt[dt] = f32x16{};
+  const int krow = w * 32 + r, mykey = kb * KB + krow, kmin = kb * KB + w * 32;
+  const int qt0 = (kb * KB) / QT, nqt = S / QT - qt0, nslice = G * nqt;
+  // slice staging: thread t owns rows (t >> 4) and (t >> 4) + 16, chunk t & 15, of Q and dO
+  const int srow = t >> 4, sch = t & 15;
+  u16x8 pq0, pq1, pd0, pd1;
+  auto gload = [&](int idx) {
+    const int hq = hk * G + idx / nqt, qbase = (qt0 + idx % nqt) * QT;
+    const u16* qp = q + ((size_t)(b * H + hq) * S + qbase) * D;
+    pq0 = *reinterpret_cast<const u16x8*>(qp + (size_t)srow * D + sch * 8);
+    pq1 = *reinterpret_cast<const u16x8*>(qp + (size_t)(srow + 16) * D + sch * 8);
+    const u16* dp = dout + (((size_t)b * S + qbase) * H + hq) * D;
+    pd0 = *reinterpret_cast<const u16x8*>(dp + (size_t)srow * H * D + sch * 8);
+    pd1 = *reinterpret_cast<const u16x8*>(dp + (size_t)(srow + 16) * H * D + sch * 8);
+  };
+  auto lstore = [&]() {
+    *reinterpret_cast<u16x8*>(qimg + swz(srow, sch)) = pq0;
+    *reinterpret_cast<u16x8*>(qimg + swz(srow + 16, sch)) = pq1;
+    *reinterpret_cast<u16x8*>(doimg + swz(srow, sch)) = pd0;
+    *reinterpret_cast<u16x8*>(doimg + swz(srow + 16, sch)) = pd1;
+  };
+  gload(0);
+  lstore();
+  __syncthreads();
+  for (int idx = 0; idx < nslice; ++idx) {
+    const int hq = hk * G + idx / nqt, qbase = (qt0 + idx % nqt) * QT;
+    const size_t rowoff = ((size_t)b * H + hq) * S + qbase + r;
+    const float lse_r = lse2[rowoff], del_r = delta[rowoff];  // query qbase + r (lane r of each half)
+    if (qbase + QT - 1 >= kmin) {  // wave-uniform: some query of the slice sees a key of this wave
+      f32x16 sacc = f32x16{}, dpacc = f32x16{};
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        sacc = mfma(lds_b128(qimg, swz(r, 2 * s + hh)), lds_b128(kimg, swz(krow, 2 * s + hh)), sacc);
+        dpacc = mfma(lds_b128(doimg, swz(r, 2 * s + hh)), lds_b128(vimg, swz(krow, 2 * s + hh)), dpacc);
+      }
+      f32x16 p, ds;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qi = crow(i, hh);
+        const float lq = __shfl(lse_r, qi, 64), dq_ = __shfl(del_r, qi, 64);
+        const float pv = (mykey > qbase + qi) ? 0.f : exp2f(sacc[i] * c - lq);
+        p[i] = pv;
+        ds[i] = pv * (dpacc[i] - dq_);
+      }
+      const bf16x8 p0 = pack8(p, 0), p1 = pack8(p, 8), d0 = pack8(ds, 0), d1 = pack8(ds, 8);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dvt[dt] = mfma(tr_frag(doimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), p0, dvt[dt]);
+        dvt[dt] = mfma(tr_frag(doimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), p1, dvt[dt]);
+        dkt[dt] = mfma(tr_frag(qimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), d0, dkt[dt]);
+        dkt[dt] = mfma(tr_frag(qimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), d1, dkt[dt]);
+      }
+    }
+    __syncthreads();
+    if (idx + 1 < nslice) {  // synchronous staging: the co-resident workgroup covers its latency
+      gload(idx + 1);
+      lstore();
+      __syncthreads();
+    }
+  }
+  u16* dkrow = dk + ((size_t)(b * Hkv + hk) * S + mykey) * D;
+  u16* dvrow = dv + ((size_t)(b * Hkv + hk) * S + mykey) * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u16x4 a4, b4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a4[e] = f2bf(dkt[dt][4 * g4 + e] * scale);
+        b4[e] = f2bf(dvt[dt][4 * g4 + e]);
+      }
+      *reinterpret_cast<u16x4*>(dkrow + 32 * dt + 8 * g4 + 4 * hh) = a4;
+      *reinterpret_cast<u16x4*>(dvrow + 32 * dt + 8 * g4 + 4 * hh) = b4;
+    }
+}
+
+// Kernel 2 — dQ.  Forward-shaped: one workgroup = 4 waves = 128 queries of one (batch, q-head),
+// query on the lane.  Per 64-key tile: S^T = K.Q^T and dP^T = V.dO^T (Q, dO fragments in registers),
+// dS^T = P^T * (dP^T - delta), and dQ^T += K^T.dS^T with K^T gathered by transposed LDS reads and the
+// dS^T accumulator as the B operand — dQ is summed in registers, written once.
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
+                                                             const u16* __restrict__ v, const u16* __restrict__ dout,
+                                                             const float* __restrict__ lse2, const float* __restrict__ delta,
+                                                             u16* __restrict__ dq, int H, int Hkv, int S, float c, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * BK * D * 2];
+  char* kimg = smem;
+  char* vimg = smem + BK * D * 2;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, hh = lane >> 5;
+  const int nqb = gridDim.x, qb = nqb - 1 - blockIdx.x;
+  const int bh = blockIdx.y, b = bh / H, hq = bh % H, hk = hq / (H / Hkv);
+  const u16* kp = k + ((size_t)(b * Hkv + hk) * S) * D;
+  const u16* vp = v + ((size_t)(b * Hkv + hk) * S) * D;
+  const int q0 = qb * BQ + w * 32, myq = q0 + r;
+  const u16* qrow = q + ((size_t)(b * H + hq) * S + myq) * D;
+  const u16* dorow = dout + (((size_t)b * S + myq) * H + hq) * D;
+  bf16x8 qf[8], df[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    qf[s] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s + 8 * hh);
+    df[s] = *reinterpret_cast<const bf16x8*>(dorow + 16 * s + 8 * hh);
+  }
+  const float lse_q = lse2[(size_t)(b * H + hq) * S + myq], del_q = delta[(size_t)(b * H + hq) * S + myq];
+  f32x16 dqt[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dqt[dt] = f32x16{};
+  const int ntiles = (qb * BQ + BQ) / BK;
+  const int srow = t >> 4, sch = t & 15;
+  for (int kt = 0; kt < ntiles; ++kt) {
+    __syncthreads();  // previous tile consumed
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const size_t row = (size_t)kt * BK + i * 16 + srow;
+      *reinterpret_cast<u16x8*>(kimg + swz(i * 16 + srow, sch)) = *reinterpret_cast<const u16x8*>(kp + row * D + sch * 8);
+      *reinterpret_cast<u16x8*>(vimg + swz(i * 16 + srow, sch)) = *reinterpret_cast<const u16x8*>(vp + row * D + sch * 8);
+    }
+    __syncthreads();
+    const int key0 = kt * BK;
+    if (key0 > q0 + 31) continue;  // wave-uniform: no visible key in this tile (barriers stay matched)
+    f32x16 s0 = f32x16{}, s1 = f32x16{}, e0 = f32x16{}, e1 = f32x16{};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const bf16x8 k0 = lds_b128(kimg, swz(r, 2 * s + hh)), k1 = lds_b128(kimg, swz(32 + r, 2 * s + hh));
+      const bf16x8 v0 = lds_b128(vimg, swz(r, 2 * s + hh)), v1 = lds_b128(vimg, swz(32 + r, 2 * s + hh));
+      s0 = mfma(k0, qf[s], s0);
+      s1 = mfma(k1, qf[s], s1);
+      e0 = mfma(v0, df[s], e0);
+      e1 = mfma(v1, df[s], e1);
+    }
+    const bool diag = key0 + BK - 1 > q0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int kk = key0 + crow(i, hh);
+      const float p0 = (diag && kk > myq) ? 0.f : exp2f(s0[i] * c - lse_q);
+      const float p1 = (diag && kk + 32 > myq) ? 0.f : exp2f(s1[i] * c - lse_q);
+      s0[i] = p0 * (e0[i] - del_q);
+      s1[i] = p1 * (e1[i] - del_q);
+    }
+    const bf16x8 d00 = pack8(s0, 0), d01 = pack8(s0, 8), d10 = pack8(s1, 0), d11 = pack8(s1, 8);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      dqt[dt] = mfma(tr_frag(kimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), d00, dqt[dt]);
+      dqt[dt] = mfma(tr_frag(kimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), d01, dqt[dt]);
+      dqt[dt] = mfma(tr_frag(kimg, lane, 32 + 4 * hh, 40 + 4 * hh, 32 * dt), d10, dqt[dt]);
+      dqt[dt] = mfma(tr_frag(kimg, lane, 48 + 4 * hh, 56 + 4 * hh, 32 * dt), d11, dqt[dt]);
+    }
+  }
+  u16* out = dq + ((size_t)(b * H + hq) * S + myq) * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u16x4 a4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a4[e] = f2bf(dqt[dt][4 * g4 + e] * scale);
+      *reinterpret_cast<u16x4*>(out + 32 * dt + 8 * g4 + 4 * hh) = a4;
+    }
+}
+
 // ==================================================================================== host
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 const u16* bp(const at::Tensor& t) { return reinterpret_cast<const u16*>(t.data_ptr()); }
@@ -425,6 +612,26 @@ std::vector<at::Tensor> attn_fwd_debug(const at::Tensor& q, const at::Tensor& k,
 
 std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                  const at::Tensor& out, const at::Tensor& lse, double scale) {
+  check_qkv(q, k, v);
+  const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
+  TORCH_CHECK(dout.is_contiguous() && out.is_contiguous() && dout.numel() == q.numel() && out.numel() == q.numel(),
+              "attention bwd: dout/out must be contiguous [B, S, H, D]");
+  auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+  auto dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
+  const int rows = B * S * H;
+  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
+                     delta.data_ptr<float>(), B, H, S);
+  const float c = (float)(scale * 1.4426950408889634);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(S / KB, B * Hkv), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
+                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(S / BQ, B * H), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
+                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
+  return {dq, dk, dv};
+}
+
+// v1: one fused kernel, dQ summed across key blocks with fp32 atomics (kept for A/B)
+std::vector<at::Tensor> attn_bwd_atomic(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                        const at::Tensor& out, const at::Tensor& lse, double scale) {
   check_qkv(q, k, v);
   const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
   TORCH_CHECK(dout.is_contiguous() && out.is_contiguous() && dout.numel() == q.numel() && out.numel() == q.numel(),
