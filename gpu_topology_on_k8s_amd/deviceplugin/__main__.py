@@ -69,11 +69,12 @@ def main(argv=None) -> int:
                        node_name=a.node_name, contract=Contract(resource_name=a.resource_name, prefix=a.annotation_prefix),
                        health_interval=a.health_interval)
     plugin = DevicePluginServer(topo, cfg, api=make_api(a.apiserver, a.token), health_fn=health if a.discovery != "fake" else None)
-    plugin.start()
     done = threading.Event()
-    for sig in (signal.SIGINT, signal.SIGTERM):
+    for sig in (signal.SIGINT, signal.SIGTERM):  # installed before serving: a stop never races start-up
         signal.signal(sig, lambda *_: done.set())
-    done.wait()
+    plugin.start()
+    while not done.wait(1.0):
+        pass
     plugin.stop()
     return 0
 

@@ -204,12 +204,20 @@ class ClusterCache:
             self.sync_all()
 
     def get(self, name: str, node_obj: Optional[dict] = None) -> NodeState:
-        """Cached state of a node; refreshed from ``node_obj`` when the scheduler passed full nodes."""
-        if node_obj is not None:
-            st = self.update_node_object(node_obj)
-        else:
-            st = self._state(name)
-        if st.synced_at == 0.0 or self.clock() - st.synced_at >= self.resync_s:
+        """Cached state of a node for scoring/filtering.
+
+        A stale cache is refreshed with ONE cluster-wide sync (list nodes + list pods: two API calls
+        however many candidates the scheduler sends), not per node; ``bind`` does its own
+        authoritative per-node refresh under the node lock.  ``node_obj`` (scheduler sent full
+        Node objects) refreshes the node's topology/labels without an API call.
+        """
+        if self.clock() - self._last_full >= self.resync_s or name not in self._nodes:
+            try:
+                self.sync_all()
+            except Exception as e:
+                log.warning("cache sync failed: %s", e)
+        st = self.update_node_object(node_obj) if node_obj is not None else self._state(name)
+        if st.synced_at == 0.0:  # node unknown to the last sync (e.g. just created): read it directly
             try:
                 self.refresh_node(name)
             except Exception as e:

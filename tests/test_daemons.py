@@ -1,0 +1,109 @@
+"""The two daemons as shipped (``python -m ...deviceplugin`` / ``python -m ...extender``) in subprocesses,
+talking to an in-test fake kubelet (gRPC, unix socket) and the fake apiserver over HTTP."""
+import os
+import shutil
+import signal
+import socket
+import subprocess
+import sys
+import tempfile
+import time
+
+import pytest
+import requests
+
+from gpu_topology_on_k8s_amd.deviceplugin import FakeKubelet
+from gpu_topology_on_k8s_amd.k8s import Contract, FakeAPIServer, serve_http
+from gpu_topology_on_k8s_amd.k8s.annotations import encode_node_annotations
+from gpu_topology_on_k8s_amd.k8s.objects import make_node, make_pod
+from gpu_topology_on_k8s_amd.topology import fixtures as fx
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _wait(pred, timeout=30.0):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        if pred():
+            return True
+        time.sleep(0.05)
+    return False
+
+
+def _spawn(args):
+    env = dict(os.environ, PYTHONPATH=REPO)
+    return subprocess.Popen([sys.executable, "-m", *args], cwd=REPO, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                            text=True)
+
+
+def _stop(p):
+    if p.poll() is None:
+        p.send_signal(signal.SIGTERM)
+        try:
+            p.wait(timeout=20)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    return p.returncode
+
+
+def test_device_plugin_daemon_registers_and_publishes():
+    api = FakeAPIServer()
+    api.create_node(make_node("worker-1"))
+    srv, url = serve_http(api)
+    sockdir = tempfile.mkdtemp(prefix="gtkd", dir="/tmp")
+    kubelet = FakeKubelet(sockdir, node_name="worker-1", api=api)
+    kubelet.start()
+    p = _spawn(["gpu_topology_on_k8s_amd.deviceplugin", "--discovery", "fake", "--fake-gpus", "4", "--apiserver", url,
+                "--node-name", "worker-1", "--socket-dir", sockdir, "--resource-name", "aliyun.com/gpu", "--log-level", "WARNING"])
+    try:
+        plugin = kubelet.wait_for("aliyun.com/gpu", timeout=60)
+        assert sorted(plugin.devices) == ["0", "1", "2", "3"]
+        node = api.get_node("worker-1")
+        assert "GPU_XGMI_0_1" in node["metadata"]["annotations"]
+        assert node["status"]["capacity"]["aliyun.com/gpu"] == "4"
+        pod = api.create_pod(make_pod("p", gpus=2, node="worker-1", resource="aliyun.com/gpu"))
+        resp = kubelet.admit(pod, "aliyun.com/gpu")
+        assert resp.container_responses[0].devices[0].container_path == "/dev/kfd"
+    finally:
+        rc = _stop(p)
+        kubelet.stop()
+        srv.shutdown()
+        shutil.rmtree(sockdir, ignore_errors=True)
+    assert rc == 0, p.stdout.read() if p.stdout else ""
+
+
+def test_extender_daemon_serves_the_reference_endpoint():
+    api = FakeAPIServer()
+    c = Contract()
+    api.create_node(make_node("n1", annotations=encode_node_annotations(fx.f7_mi355x(), c), capacity={c.resource_name: "8"}))
+    srv, url = serve_http(api)
+    port = _free_port()
+    p = _spawn(["gpu_topology_on_k8s_amd.extender", "--apiserver", url, "--port", str(port), "--host", "127.0.0.1",
+                "--log-level", "WARNING"])
+    base = f"http://127.0.0.1:{port}/gputopology-scheduler"
+    try:
+        def up():
+            try:
+                return requests.get(base + "/healthz", timeout=1).ok
+            except requests.RequestException:
+                return False
+
+        assert _wait(up, 60), "extender did not come up"
+        pod = api.create_pod(make_pod("train", gpus=4))
+        hp = requests.post(base + "/sort", json={"Pod": pod, "NodeNames": ["n1"]}, timeout=10).json()
+        assert hp[0]["Host"] == "n1" and hp[0]["Score"] >= 1
+        br = requests.post(base + "/bind", json={"PodName": "train", "PodNamespace": "default",
+                                                 "PodUID": pod["metadata"]["uid"], "Node": "n1"}, timeout=10).json()
+        assert br["Error"] == "" and len(br["Devices"]) == 4
+        assert api.get_pod("default", "train")["spec"]["nodeName"] == "n1"
+        assert "gtk_extender_binds_total" in requests.get(base + "/metrics", timeout=5).text
+    finally:
+        _stop(p)
+        srv.shutdown()

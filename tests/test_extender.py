@@ -29,7 +29,7 @@ def _cluster(nodes=("n1",), topo_fn=fx.f7_mi355x, **cfg):
         api.create_node(make_node(n, labels={c.label_model: "MI355X"}, annotations=encode_node_annotations(t, c),
                                   capacity={c.resource_name: str(t.n)}))
     clock = Clock()
-    ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0, **cfg), clock=clock)
+    ext = TopologyExtender(api, ExtenderConfig(**{"resync_s": 0.0, **cfg}), clock=clock)
     return api, ext, clock
 
 
@@ -282,3 +282,18 @@ def test_http_sort_bind_filter_wire_format():
 
     _http(ext, flow)
     assert api.get_pod("default", "p")["spec"]["nodeName"] == "n2"
+
+
+def test_prioritize_over_many_nodes_uses_constant_api_calls():
+    """nodeCacheCapable: a 64-node prioritize costs one cluster-wide sync, not 2 calls per node."""
+    names = tuple(f"n{i}" for i in range(64))
+    api, ext, clock = _cluster(nodes=names, resync_s=5.0)
+    pod = _submit(api, "p", 4)
+    before = sum(api.calls.values())
+    res = ext.prioritize(pod, list(names))
+    used = sum(api.calls.values()) - before
+    assert len(res) == 64 and all(s > 0 for _, s in res)
+    assert used <= 2, dict(api.calls)
+    before = sum(api.calls.values())
+    ext.prioritize(pod, list(names))  # fresh cache: no API traffic at all
+    assert sum(api.calls.values()) == before
