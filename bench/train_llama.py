@@ -6,7 +6,11 @@
 For each placement (``best`` = placement core's choice, ``worst`` = highest-objective subset of the
 same size) one ``torch.distributed.run`` job of ``--gpus`` ranks is started as a child process
 (nothing here touches the GPU).  With k equal to the node's device count both placements are the
-whole node and only ``best`` runs.  Random-init weights, synthetic tokens.
+whole node; the worst *link class* is then emulated with ``p2p-off``: the scheduler's devices with
+RCCL peer-to-peer disabled (``NCCL_P2P_DISABLE=1``), so every collective is staged through host
+memory — the PHB/SYS class the reference's worst placement lands on (BASELINE config 5 compares
+NVLink-pair vs cross-socket PCIe).  It is labelled as an emulation in the summary.  Random-init
+weights, synthetic tokens.
 """
 from __future__ import annotations
 
@@ -26,12 +30,17 @@ def _port() -> int:
         return s.getsockname()[1]
 
 
+EMULATIONS = {"p2p-off": ("best", {"NCCL_P2P_DISABLE": "1"})}
+
+
 def run(placement: str, a) -> dict:
+    placement, extra_env = EMULATIONS.get(placement, (placement, {}))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1",
            f"--master-port={_port()}", "-m", "gpu_topology_on_k8s_amd.models.train", "--model", a.model, "--batch", str(a.batch),
            "--seq", str(a.seq), "--steps", str(a.steps), "--warmup", str(a.warmup), "--placement", placement,
            "--bucket-mb", str(a.bucket_mb), "--attn", a.attn] + (["--checkpoint"] if a.checkpoint else [])
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""),
+               **extra_env)
     p = subprocess.run(cmd, capture_output=True, text=True, cwd=REPO, env=env, timeout=a.timeout)
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     if p.returncode != 0 or not lines:
@@ -52,21 +61,28 @@ def main() -> int:
     ap.add_argument("--attn", default="hip", choices=["hip", "sdpa", "sdpa-expand"])
     ap.add_argument("--checkpoint", action="store_true")
     ap.add_argument("--timeout", type=int, default=1500)
-    ap.add_argument("--placements", default="best,worst")
+    ap.add_argument("--placements", default="best,worst", help="comma list of best, worst, p2p-off (emulated worst link class)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     res = {}
     for pl in a.placements.split(","):
+        if pl == "worst" and "best" in res and not res["best"].get("worst_devices"):
+            pl = "p2p-off"  # k == node size: best == worst device set; emulate the worst link class instead
+        if pl in res:
+            continue
         r = run(pl, a)
+        r["placement"] = pl
         res[pl] = r
         print(json.dumps(r), flush=True)
-        if pl == "best" and not r.get("worst_devices"):
-            break  # k == node size: best == worst
+    worst_kind = "worst" if "worst" in res else ("p2p-off" if "p2p-off" in res else None)
+    worst = res.get(worst_kind, {}) if worst_kind else {}
+    if worst_kind == "p2p-off":
+        worst_kind = "emulated: same devices, NCCL_P2P_DISABLE=1 (host-staged collectives)"
     summary = {
         "metric": "Llama DP tokens/s, scheduler-chosen vs worst placement",
         "model": a.model, "n_gpus": a.gpus, "seq_len": a.seq, "global_batch": a.batch * a.gpus,
         "best_tokens_per_s": res["best"]["tokens_per_s"], "best_devices": res["best"]["devices"],
-        "worst_tokens_per_s": res.get("worst", {}).get("tokens_per_s"), "worst_devices": res.get("worst", {}).get("devices"),
+        "worst_tokens_per_s": worst.get("tokens_per_s"), "worst_devices": worst.get("devices"), "worst_kind": worst_kind,
         "mfu": res["best"]["mfu"], "max_mem_gb": res["best"]["max_mem_gb"], "data": "synthetic tokens, random-init weights",
     }
     if summary["worst_tokens_per_s"]:

@@ -18,12 +18,13 @@
 //     and written to LDS after the barrier (guide T14).  Query blocks are launched heaviest-first.
 //   * output O is written token-major [B, S, H, D] (what the o-projection GEMM consumes) and the
 //     row log-sum-exp in log2 units for the backward.
-// Backward (one workgroup = 4 waves = 128 keys of one (batch, kv-head); sweeps every q-head of the
-// GQA group x 32-query slices, so dK/dV never need a cross-workgroup sum):
-//   * key on the lane for S = Q.K^T and dP = dO.V^T; P and dS accumulators feed dV^T += dO^T.P and
-//     dK^T += Q^T.dS directly as B operands (dO^T, Q^T by transposed LDS reads);
-//   * dS crosses LDS once (a [key][query] image written with 8-B stores, read transposed) for
-//     dQ = dS.K, summed over workgroups with fp32 atomics (one register = 128 contiguous bytes).
+// Backward v2 (attn_bwd): delta = rowsum(dO*O), then two kernels with no cross-workgroup sums:
+//   * dK/dV: one workgroup = 128 keys of one (batch, kv-head), sweeping every q-head of the GQA group
+//     x 32-query slices; key on the lane for S = Q.K^T and dP = dO.V^T, whose P / dS accumulators
+//     feed dV^T += dO^T.P and dK^T += Q^T.dS as B operands (dO^T, Q^T by transposed LDS reads).
+//   * dQ: forward-shaped (query on the lane), dQ^T += K^T.dS^T accumulated in registers.
+// Backward v1 (attn_bwd_atomic, kept for A/B): one fused kernel, dS through an LDS [key][query]
+// image and dQ summed across key blocks with fp32 atomics — 1.8x slower at the Llama shape.
 #include <hip/hip_runtime.h>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
@@ -89,6 +90,9 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& acc, int base) {
   for (int j = 0; j < 8; ++j) out[j] = (__bf16)acc[base + j];
   return out;
 }
+
+// raw v_exp_f32 (2^x): no denormal range reduction — softmax terms below 2^-126 are 0 either way
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -176,21 +180,26 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const u16* __restrict_
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(m, mx);
-      const float alpha = exp2f(m - mnew);
       float rs = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        s0[i] = exp2f(s0[i] - mnew);
-        s1[i] = exp2f(s1[i] - mnew);
+        s0[i] = fexp2(s0[i] - mnew);
+        s1[i] = fexp2(s1[i] - mnew);
         rs += s0[i] + s1[i];
       }
       rs += __shfl_xor(rs, 32, 64);
-      l = l * alpha + rs;
+      // Exact skip: when no query row of the wave raised its max, alpha == 1 for every lane and the
+      // 64-register O rescale is a no-op (most tiles after the first few).
+      if (__any(mnew > m)) {
+        const float alpha = fexp2(m - mnew);
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+      }
+      l += rs;
       m = mnew;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
       const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 8), p10 = pack8(s1, 0), p11 = pack8(s1, 8);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
@@ -304,7 +313,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(const u16* __restrict_
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int qi = crow(i, hh);
-        const float pv = (mykey > qbase + qi) ? 0.f : exp2f(sacc[i] * c - slse[qi]);
+        const float pv = (mykey > qbase + qi) ? 0.f : fexp2(sacc[i] * c - slse[qi]);
         p[i] = pv;
         ds[i] = pv * (dpacc[i] - sdel[qi]);
       }
@@ -446,7 +455,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const u16* __rest
       for (int i = 0; i < 16; ++i) {
         const int qi = crow(i, hh);
         const float lq = __shfl(lse_r, qi, 64), dq_ = __shfl(del_r, qi, 64);
-        const float pv = (mykey > qbase + qi) ? 0.f : exp2f(sacc[i] * c - lq);
+        const float pv = (mykey > qbase + qi) ? 0.f : fexp2(sacc[i] * c - lq);
         p[i] = pv;
         ds[i] = pv * (dpacc[i] - dq_);
       }
@@ -539,8 +548,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const u16* __restri
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int kk = key0 + crow(i, hh);
-      const float p0 = (diag && kk > myq) ? 0.f : exp2f(s0[i] * c - lse_q);
-      const float p1 = (diag && kk + 32 > myq) ? 0.f : exp2f(s1[i] * c - lse_q);
+      const float p0 = (diag && kk > myq) ? 0.f : fexp2(s0[i] * c - lse_q);
+      const float p1 = (diag && kk + 32 > myq) ? 0.f : fexp2(s1[i] * c - lse_q);
       s0[i] = p0 * (e0[i] - del_q);
       s1[i] = p1 * (e1[i] - del_q);
     }
