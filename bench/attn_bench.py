@@ -50,6 +50,9 @@ def main():
     t = timeit(lambda: hip.attn_fwd(q, k, v, Dh ** -0.5), a.iters)
     res["hip_fwd_ms"] = t * 1e3
     res["hip_fwd_tflops"] = fwd_flops / t / 1e12
+    if hasattr(hip, "attn_fwd_v1"):
+        t = timeit(lambda: hip.attn_fwd_v1(q, k, v, Dh ** -0.5), a.iters)
+        res["hip_fwd_v1_ms"] = t * 1e3
     t = timeit(lambda: hip.attn_bwd(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
     res["hip_bwd_ms"] = t * 1e3
     res["hip_bwd_tflops"] = 2.5 * fwd_flops / t / 1e12

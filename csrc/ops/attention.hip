@@ -94,6 +94,11 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& acc, int base) {
 // raw v_exp_f32 (2^x): no denormal range reduction — softmax terms below 2^-126 are 0 either way
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// 16-byte LDS-DMA: lane i's 16 bytes from g land at lds_base + 16 i (lds_base wave-uniform, -> M0)
+__device__ __forceinline__ void glds16(const u16* g, char* lds_base) {
+  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g, (LDS_AS void*)lds_base, 16, 0, 0);
+}
+
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -215,6 +220,181 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const u16* __restrict_
       lstore();
       __syncthreads();
     }
+  }
+  const float inv = 1.f / l;
+  u16* orow = o + (((size_t)b * S + myq) * (size_t)(H) + hq) * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u16x4 v4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v4[e] = f2bf(oacc[dt][4 * g4 + e] * inv);
+      *reinterpret_cast<u16x4*>(orow + 32 * dt + 8 * g4 + 4 * hh) = v4;
+    }
+  if (hh == 0) lse2[(size_t)(b * H + hq) * S + myq] = m + log2f(l);
+}
+
+// XCD-aware (batch*head) order: workgroups are dealt round-robin over the 8 XCDs (id % 8), so map
+// consecutive ids of one XCD to consecutive heads — the q-heads of a GQA group (which read the same
+// K/V) then run on one XCD and share its L2.  Identity when the head count is not a multiple of 8.
+__device__ __forceinline__ int xcd_head(int id, int n) { return (n & 7) ? id : (id & 7) * (n >> 3) + (id >> 3); }
+
+// Forward v2: same math as attn_fwd_kernel, restructured for the CDNA4 pipes.
+//   * grid (B*H, S/128): x = head fastest, so dispatch order is heaviest query block first across
+//     ALL heads (LPT order for the causal triangle), heads XCD-grouped (xcd_head).
+//   * K/V double-buffered in LDS (2 x 32 KiB), ONE barrier per tile.  The next tile arrives by
+//     LDS-DMA (buffer_load ... lds through a wave-uniform descriptor, swizzle on the source offset)
+//     into the other buffer, issued after QK^T and retired before the barrier: no staging
+//     registers, no ds_write pass, per-tile addressing in one scalar.
+//   * K fragments read 8 ahead of the QK^T chain (sched_group_barrier), not one pair at a time.
+//   * scale folded into the exponent: p = 2^(s*c - m) with one v_fma + v_exp per score; the max is
+//     taken on raw scores (c > 0) with v_max3.  Only the last two tiles of a block can need the
+//     causal mask or be invisible to a wave: the main loop is branch-free, those two are peeled.
+__device__ __forceinline__ float max3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));  // no IEEE canonicalising v_max per operand
+  return r;
+}
+
+__global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
+                                                           const u16* __restrict__ v, u16* __restrict__ o,
+                                                           float* __restrict__ lse2, int H, int Hkv, int S, float c) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BK * D * 2];  // [buf][K image | V image]
+  const int t = threadIdx.x, lane = t & 63, r = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int nqb = gridDim.y;
+  const int qb = nqb - 1 - blockIdx.y;  // heaviest first
+  const int bh = xcd_head(blockIdx.x, gridDim.x), b = bh / H, hq = bh % H, hk = hq / (H / Hkv);
+  const u16* qp = q + ((size_t)(b * H + hq) * S) * D;
+  const size_t kvoff = ((size_t)(b * Hkv + hk) * S) * D;
+  const int q0 = qb * BQ + w * 32;
+  const int myq = q0 + r;
+
+  bf16x8 qf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + (size_t)myq * D + 16 * s + 8 * hh);
+
+  f32x16 oacc[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) oacc[dt] = f32x16{};
+  float m = -INFINITY, l = 0.f;  // m in units of log2 (score * c)
+
+  const int ntiles = (qb * BQ + BQ) / BK;
+  // LDS-DMA staging: wave w fills rows 16w .. 16w+15 of the K and V images with 4 + 4
+  // buffer_load_dwordx4 ... lds (1 KiB = 4 rows each).  The destination is lane-linear, so the XOR
+  // swizzle goes on the SOURCE: lane (row R, slot p) fetches chunk p ^ f(R), so that
+  // swz(R, chunk) == 256 R + 16 p.  Descriptors from wave-uniform values only (no waterfall).
+  const uint32_t kvbytes = (uint32_t)((size_t)S * D * 2);
+  const auto krsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(k + kvoff), 0, kvbytes, 0x00020000);
+  const auto vrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(v + kvoff), 0, kvbytes, 0x00020000);
+  uint32_t voff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int R = 16 * w + 4 * i + (lane >> 4);
+    voff[i] = (uint32_t)(R * D * 2 + 16 * ((lane & 15) ^ (((R & 3) << 2) | ((R >> 2) & 3))));
+  }
+  auto gload = [&](int kt, char* img) {
+    const uint32_t soff = (uint32_t)kt * (BK * D * 2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(krsrc, (LDS_AS void*)(img + (16 * w + 4 * i) * 256), 16, voff[i], soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(vrsrc, (LDS_AS void*)(img + BK * D * 2 + (16 * w + 4 * i) * 256), 16, voff[i],
+                                               soff, 0, 0);
+    }
+  };
+
+  // one KV tile: QK^T, DMA of the next tile, online softmax, PV.  `masked` (compile-time at each
+  // call) adds the causal mask for the wave's diagonal tiles.
+  auto tile = [&](int kt, bool masked) {
+    char* kimg = smem + (kt & 1) * (2 * BK * D * 2);
+    char* vimg = kimg + BK * D * 2;
+    const int key0 = kt * BK;
+    f32x16 s0 = f32x16{}, s1 = f32x16{};
+    {
+      bf16x8 kf0[8], kf1[8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        kf0[s] = lds_b128(kimg, swz(r, 2 * s + hh));
+        kf1[s] = lds_b128(kimg, swz(32 + r, 2 * s + hh));
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        s0 = mfma(kf0[s], qf[s], s0);
+        s1 = mfma(kf1[s], qf[s], s1);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // 8 reads ahead, then read/MFMA pairs
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x8, 8, 0);
+    }
+    if (kt + 1 < ntiles) gload(kt + 1, smem + ((kt + 1) & 1) * (2 * BK * D * 2));  // lands under softmax + PV
+    if (masked) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int k0i = key0 + crow(i, hh);
+        if (k0i > myq) s0[i] = -INFINITY;
+        if (k0i + 32 > myq) s1[i] = -INFINITY;
+      }
+    }
+    float mx = max3(s0[0], s1[0], s0[1]);
+#pragma unroll
+    for (int i = 1; i < 16; ++i) mx = max3(mx, s1[i], i + 1 < 16 ? s0[i + 1] : s1[i]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx * c);
+    float rs = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      s0[i] = fexp2(fmaf(s0[i], c, -mnew));
+      s1[i] = fexp2(fmaf(s1[i], c, -mnew));
+      rs += s0[i] + s1[i];
+    }
+    rs += __shfl_xor(rs, 32, 64);
+    if (__any(mnew > m)) {  // exact skip: no row max moved => alpha == 1 everywhere
+      const float alpha = fexp2(m - mnew);
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+    }
+    l += rs;
+    m = mnew;
+    const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 8), p10 = pack8(s1, 0), p11 = pack8(s1, 8);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int col0 = 32 * dt;
+      oacc[dt] = mfma(tr_frag(vimg, lane, 0 + 4 * hh, 8 + 4 * hh, col0), p00, oacc[dt]);
+      oacc[dt] = mfma(tr_frag(vimg, lane, 16 + 4 * hh, 24 + 4 * hh, col0), p01, oacc[dt]);
+      oacc[dt] = mfma(tr_frag(vimg, lane, 32 + 4 * hh, 40 + 4 * hh, col0), p10, oacc[dt]);
+      oacc[dt] = mfma(tr_frag(vimg, lane, 48 + 4 * hh, 56 + 4 * hh, col0), p11, oacc[dt]);
+    }
+  };
+  auto sync = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of the next tile has landed ...
+    __syncthreads();                                    // ... and everyone's is visible
+  };
+
+  gload(0, smem);
+  sync();
+  // tiles 0 .. ntiles-3 lie entirely below every query of the block: no mask, no visibility test
+  int kt = 0;
+  for (; kt < ntiles - 2; ++kt) {
+    tile(kt, false);
+    sync();
+  }
+  // the block's diagonal: tile ntiles-2 covers keys [128 qb, 128 qb + 64), ntiles-1 the next 64
+  for (; kt < ntiles; ++kt) {
+    const int key0 = kt * BK;
+    if (key0 <= q0 + 31) {
+      tile(kt, key0 + BK - 1 > q0);
+    } else if (kt + 1 < ntiles) {
+      gload(kt + 1, smem + ((kt + 1) & 1) * (2 * BK * D * 2));
+    }
+    sync();
   }
   const float inv = 1.f / l;
   u16* orow = o + (((size_t)b * S + myq) * (size_t)(H) + hq) * D;
@@ -604,6 +784,18 @@ std::vector<at::Tensor> attn_fwd_impl(const at::Tensor& q, const at::Tensor& k, 
 }
 
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale) {
+  check_qkv(q, k, v);
+  const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
+  auto o = at::empty({B, S, H, D}, q.options());
+  auto lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+  const float c = (float)(scale * 1.4426950408889634);
+  hipLaunchKernelGGL(attn_fwd2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bpm(o),
+                     lse.data_ptr<float>(), H, Hkv, S, c);
+  return {o, lse};
+}
+
+// v1 forward (two barriers per tile, single LDS buffer), kept for A/B
+std::vector<at::Tensor> attn_fwd_v1(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale) {
   return attn_fwd_impl(q, k, v, scale, false);
 }
 
