@@ -240,6 +240,43 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const u16* __restrict_
 // K/V) then run on one XCD and share its L2.  Identity when the head count is not a multiple of 8.
 __device__ __forceinline__ int xcd_head(int id, int n) { return (n & 7) ? id : (id & 7) * (n >> 3) + (id >> 3); }
 
+// LDS-DMA staging of one [BK=64][128] K tile and V tile into the swizzled images (K at img, V at
+// img + 16 KiB) by a 4-wave workgroup: wave w fills rows 16w .. 16w+15 with 4 + 4
+// buffer_load_dwordx4 ... lds (1 KiB = 4 rows each).  The destination is lane-linear, so the XOR
+// swizzle goes on the SOURCE offset: lane (row R, slot p) fetches chunk p ^ f(R), which makes
+// swz(R, chunk) == 256 R + 16 p.  Descriptors are built from wave-uniform values only (no
+// waterfall loops); the per-tile step is one scalar offset.
+struct KVStage {
+  __amdgpu_buffer_rsrc_t krs, vrs;
+  uint32_t voff[4];
+  int w;
+  __device__ __forceinline__ KVStage(const u16* kbase, const u16* vbase, int S, int w_, int lane) : w(w_) {
+    const uint32_t bytes = (uint32_t)((size_t)S * D * 2);
+    krs = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, 0, bytes, 0x00020000);
+    vrs = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, 0, bytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int R = 16 * w + 4 * i + (lane >> 4);
+      voff[i] = (uint32_t)(R * D * 2 + 16 * ((lane & 15) ^ (((R & 3) << 2) | ((R >> 2) & 3))));
+    }
+  }
+  __device__ __forceinline__ void load(int kt, char* img) const {
+    const uint32_t soff = (uint32_t)kt * (BK * D * 2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (LDS_AS void*)(img + (16 * w + 4 * i) * 256), 16, voff[i], soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (LDS_AS void*)(img + BK * D * 2 + (16 * w + 4 * i) * 256), 16, voff[i], soff,
+                                               0, 0);
+    }
+  }
+};
+
+// every wave's outstanding LDS-DMA has landed, then a barrier makes it visible to the workgroup
+__device__ __forceinline__ void dma_sync() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 // Forward v2: same math as attn_fwd_kernel, restructured for the CDNA4 pipes.
 //   * grid (B*H, S/128): x = head fastest, so dispatch order is heaviest query block first across
 //     ALL heads (LPT order for the causal triangle), heads XCD-grouped (xcd_head).
@@ -281,28 +318,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict
   float m = -INFINITY, l = 0.f;  // m in units of log2 (score * c)
 
   const int ntiles = (qb * BQ + BQ) / BK;
-  // LDS-DMA staging: wave w fills rows 16w .. 16w+15 of the K and V images with 4 + 4
-  // buffer_load_dwordx4 ... lds (1 KiB = 4 rows each).  The destination is lane-linear, so the XOR
-  // swizzle goes on the SOURCE: lane (row R, slot p) fetches chunk p ^ f(R), so that
-  // swz(R, chunk) == 256 R + 16 p.  Descriptors from wave-uniform values only (no waterfall).
-  const uint32_t kvbytes = (uint32_t)((size_t)S * D * 2);
-  const auto krsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(k + kvoff), 0, kvbytes, 0x00020000);
-  const auto vrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(v + kvoff), 0, kvbytes, 0x00020000);
-  uint32_t voff[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int R = 16 * w + 4 * i + (lane >> 4);
-    voff[i] = (uint32_t)(R * D * 2 + 16 * ((lane & 15) ^ (((R & 3) << 2) | ((R >> 2) & 3))));
-  }
-  auto gload = [&](int kt, char* img) {
-    const uint32_t soff = (uint32_t)kt * (BK * D * 2);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(krsrc, (LDS_AS void*)(img + (16 * w + 4 * i) * 256), 16, voff[i], soff, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(vrsrc, (LDS_AS void*)(img + BK * D * 2 + (16 * w + 4 * i) * 256), 16, voff[i],
-                                               soff, 0, 0);
-    }
-  };
+  const KVStage stage(k + kvoff, v + kvoff, S, w, lane);
+  auto gload = [&](int kt, char* img) { stage.load(kt, img); };
 
   // one KV tile: QK^T, DMA of the next tile, online softmax, PV.  `masked` (compile-time at each
   // call) adds the causal mask for the wave's diagonal tiles.
@@ -373,18 +390,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict
       oacc[dt] = mfma(tr_frag(vimg, lane, 48 + 4 * hh, 56 + 4 * hh, col0), p11, oacc[dt]);
     }
   };
-  auto sync = [&]() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of the next tile has landed ...
-    __syncthreads();                                    // ... and everyone's is visible
-  };
-
   gload(0, smem);
-  sync();
+  dma_sync();
   // tiles 0 .. ntiles-3 lie entirely below every query of the block: no mask, no visibility test
   int kt = 0;
   for (; kt < ntiles - 2; ++kt) {
     tile(kt, false);
-    sync();
+    dma_sync();
   }
   // the block's diagonal: tile ntiles-2 covers keys [128 qb, 128 qb + 64), ntiles-1 the next 64
   for (; kt < ntiles; ++kt) {
@@ -394,7 +406,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict
     } else if (kt + 1 < ntiles) {
       gload(kt + 1, smem + ((kt + 1) & 1) * (2 * BK * D * 2));
     }
-    sync();
+    dma_sync();
   }
   const float inv = 1.f / l;
   u16* orow = o + (((size_t)b * S + myq) * (size_t)(H) + hq) * D;
@@ -754,6 +766,228 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const u16* __restri
     }
 }
 
+// dK/dV v3.  Same decomposition as attn_bwd_dkdv_kernel (one workgroup = 128 keys of one (batch,
+// kv-head), sweeping every q-head of the GQA group x 32-query slices, key on the lane), with the
+// slice stream made asynchronous and the LDS footprint cut so two workgroups still share a CU:
+//   * each lane's K row (the B operand of S = Q.K^T) lives in registers for the whole kernel
+//     (32 VGPRs), so only the V image stays in LDS (32 KiB);
+//   * Q, dO, lse and delta of a slice arrive by LDS-DMA into a double buffer (2 x 16.5 KiB), issued
+//     one slice ahead: one barrier per slice, no staging registers, no ds_write pass;
+//   * lse / delta are read per accumulator quad with ds_read_b128 (crow(4g..4g+3) are 4 consecutive
+//     queries) instead of 32 cross-lane shuffles;
+//   * only the first KB/QT slices of each q-head touch the block's diagonal: mask code runs there only.
+constexpr int SL_Q = 0, SL_DO = QT * D * 2, SL_LSE = 2 * QT * D * 2, SL_DEL = SL_LSE + 256, SL_BYTES = SL_DEL + 256;
+
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv3_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
+                                                                const u16* __restrict__ v, const u16* __restrict__ dout,
+                                                                const float* __restrict__ lse2, const float* __restrict__ delta,
+                                                                u16* __restrict__ dk, u16* __restrict__ dv, int H, int Hkv,
+                                                                int S, float c, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * SL_BYTES];  // slice double buffer
+  char* sbuf = smem;
+  const int t = threadIdx.x, lane = t & 63, r = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int kb = blockIdx.y;  // grid (B*Hkv, S/KB): key block 0 (the most query slices) of every head dispatches first
+  const int bk = xcd_head(blockIdx.x, gridDim.x), b = bk / Hkv, hk = bk % Hkv, G = H / Hkv;
+  const size_t kvoff = ((size_t)(b * Hkv + hk) * S + (size_t)kb * KB) * D;
+  const int krow = w * 32 + r, mykey = kb * KB + krow, kmin = kb * KB + w * 32;
+  bf16x8 kf[8], vf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    kf[s] = *reinterpret_cast<const bf16x8*>(k + kvoff + (size_t)krow * D + 16 * s + 8 * hh);
+    vf[s] = *reinterpret_cast<const bf16x8*>(v + kvoff + (size_t)krow * D + 16 * s + 8 * hh);
+  }
+  f32x16 dvt[4], dkt[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dvt[dt] = dkt[dt] = f32x16{};
+  const int qt0 = (kb * KB) / QT, nqt = S / QT - qt0, nslice = G * nqt;
+
+  // slice DMA: wave w brings rows 8w .. 8w+7 of the Q and dO images (2 + 2 x 1 KiB); waves 0 / 1 the
+  // 64 lse / delta values starting at the slice (the upper 32 are the next slice's or out of range).
+  const uint32_t qbytes = (uint32_t)((size_t)H * S * D * 2), dbytes = (uint32_t)((size_t)S * H * D * 2);
+  const auto qrs = __builtin_amdgcn_make_buffer_rsrc((void*)(q + (size_t)b * H * S * D), 0, qbytes, 0x00020000);
+  const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)(dout + (size_t)b * S * H * D), 0, dbytes, 0x00020000);
+  const auto lrs = __builtin_amdgcn_make_buffer_rsrc((void*)((w == 0 ? lse2 : delta) + (size_t)b * H * S), 0,
+                                                     (uint32_t)((size_t)H * S * 4), 0x00020000);
+  uint32_t qv[2], dvo[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int R = 8 * w + 4 * i + (lane >> 4);
+    const uint32_t ch16 = 16 * ((lane & 15) ^ (((R & 3) << 2) | ((R >> 2) & 3)));
+    qv[i] = (uint32_t)(R * D * 2) + ch16;
+    dvo[i] = (uint32_t)(R * H * D * 2) + ch16;
+  }
+  auto sload = [&](int idx, char* buf) {
+    const int hq = hk * G + idx / nqt, qbase = (qt0 + idx % nqt) * QT;
+    const uint32_t qs = (uint32_t)(((size_t)hq * S + qbase) * D * 2), ds = (uint32_t)(((size_t)qbase * H + hq) * D * 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (LDS_AS void*)(buf + SL_Q + (8 * w + 4 * i) * 256), 16, qv[i], qs, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, (LDS_AS void*)(buf + SL_DO + (8 * w + 4 * i) * 256), 16, dvo[i], ds, 0, 0);
+    }
+    if (w < 2)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, (LDS_AS void*)(buf + (w == 0 ? SL_LSE : SL_DEL)), 4, 4 * lane,
+                                               (uint32_t)(((size_t)hq * S + qbase) * 4), 0, 0);
+  };
+
+  auto slice = [&](int idx, char* buf, bool masked) {
+    const int qbase = (qt0 + idx % nqt) * QT;
+    const char* qimg = buf + SL_Q;
+    const char* doimg = buf + SL_DO;
+    f32x16 sacc = f32x16{}, dpacc = f32x16{};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      sacc = mfma(lds_b128(qimg, swz(r, 2 * s + hh)), kf[s], sacc);
+      dpacc = mfma(lds_b128(doimg, swz(r, 2 * s + hh)), vf[s], dpacc);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {  // accumulator quad g holds queries 8g + 4hh + {0..3}
+      const f32x4 lq = *reinterpret_cast<const f32x4*>(buf + SL_LSE + 4 * (8 * g + 4 * hh));
+      const f32x4 dq_ = *reinterpret_cast<const f32x4*>(buf + SL_DEL + 4 * (8 * g + 4 * hh));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * g + e;
+        float pv = fexp2(fmaf(sacc[i], c, -lq[e]));
+        if (masked && mykey > qbase + crow(i, hh)) pv = 0.f;
+        sacc[i] = pv;
+        dpacc[i] = pv * (dpacc[i] - dq_[e]);
+      }
+    }
+    const bf16x8 p0 = pack8(sacc, 0), p1 = pack8(sacc, 8), d0 = pack8(dpacc, 0), d1 = pack8(dpacc, 8);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      dvt[dt] = mfma(tr_frag(doimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), p0, dvt[dt]);
+      dvt[dt] = mfma(tr_frag(doimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), p1, dvt[dt]);
+      dkt[dt] = mfma(tr_frag(qimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), d0, dkt[dt]);
+      dkt[dt] = mfma(tr_frag(qimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), d1, dkt[dt]);
+    }
+  };
+
+  sload(0, sbuf);
+  dma_sync();
+  for (int idx = 0; idx < nslice; ++idx) {
+    char* buf = sbuf + (idx & 1) * SL_BYTES;
+    if (idx + 1 < nslice) sload(idx + 1, sbuf + ((idx + 1) & 1) * SL_BYTES);  // buffer free since the last barrier
+    const int j = idx % nqt;  // scalar
+    if (j >= KB / QT) {
+      slice(idx, buf, false);  // every query of the slice is past the block's last key
+    } else if ((qt0 + j) * QT + QT - 1 >= kmin) {  // diagonal slice that reaches this wave's keys
+      slice(idx, buf, true);
+    }
+    dma_sync();
+  }
+  u16* dkrow = dk + ((size_t)(b * Hkv + hk) * S + mykey) * D;
+  u16* dvrow = dv + ((size_t)(b * Hkv + hk) * S + mykey) * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u16x4 a4, b4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a4[e] = f2bf(dkt[dt][4 * g4 + e] * scale);
+        b4[e] = f2bf(dvt[dt][4 * g4 + e]);
+      }
+      *reinterpret_cast<u16x4*>(dkrow + 32 * dt + 8 * g4 + 4 * hh) = a4;
+      *reinterpret_cast<u16x4*>(dvrow + 32 * dt + 8 * g4 + 4 * hh) = b4;
+    }
+}
+
+// dQ v2: attn_bwd_dq_kernel restructured like forward v2 — LDS-DMA double-buffered K/V tiles with
+// one barrier per tile, the block's diagonal tiles peeled out of a branch-free main loop, LPT +
+// XCD-grouped grid (B*H, S/128).  (Forcing the fragment reads ahead with sched_group_barrier spills
+// inside the loop here: Q, dO, 4 accumulators and dQ^T already hold 192 VGPRs.)
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
+                                                              const u16* __restrict__ v, const u16* __restrict__ dout,
+                                                              const float* __restrict__ lse2, const float* __restrict__ delta,
+                                                              u16* __restrict__ dq, int H, int Hkv, int S, float c, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BK * D * 2];  // [buf][K image | V image]
+  const int t = threadIdx.x, lane = t & 63, r = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int nqb = gridDim.y, qb = nqb - 1 - blockIdx.y;
+  const int bh = xcd_head(blockIdx.x, gridDim.x), b = bh / H, hq = bh % H, hk = hq / (H / Hkv);
+  const size_t kvoff = ((size_t)(b * Hkv + hk) * S) * D;
+  const int q0 = qb * BQ + w * 32, myq = q0 + r;
+  const u16* qrow = q + ((size_t)(b * H + hq) * S + myq) * D;
+  const u16* dorow = dout + (((size_t)b * S + myq) * H + hq) * D;
+  bf16x8 qf[8], df[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    qf[s] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s + 8 * hh);
+    df[s] = *reinterpret_cast<const bf16x8*>(dorow + 16 * s + 8 * hh);
+  }
+  const float lse_q = lse2[(size_t)(b * H + hq) * S + myq], del_q = delta[(size_t)(b * H + hq) * S + myq];
+  f32x16 dqt[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dqt[dt] = f32x16{};
+  const int ntiles = (qb * BQ + BQ) / BK;
+  const KVStage stage(k + kvoff, v + kvoff, S, w, lane);
+
+  auto tile = [&](int kt, bool masked) {
+    char* kimg = smem + (kt & 1) * (2 * BK * D * 2);
+    char* vimg = kimg + BK * D * 2;
+    const int key0 = kt * BK;
+    f32x16 s0 = f32x16{}, s1 = f32x16{}, e0 = f32x16{}, e1 = f32x16{};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const bf16x8 k0 = lds_b128(kimg, swz(r, 2 * s + hh)), k1 = lds_b128(kimg, swz(32 + r, 2 * s + hh));
+      const bf16x8 v0 = lds_b128(vimg, swz(r, 2 * s + hh)), v1 = lds_b128(vimg, swz(32 + r, 2 * s + hh));
+      s0 = mfma(k0, qf[s], s0);
+      s1 = mfma(k1, qf[s], s1);
+      e0 = mfma(v0, df[s], e0);
+      e1 = mfma(v1, df[s], e1);
+    }
+    if (kt + 1 < ntiles) stage.load(kt + 1, smem + ((kt + 1) & 1) * (2 * BK * D * 2));  // lands under the dQ MFMAs
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float p0 = fexp2(fmaf(s0[i], c, -lse_q));
+      float p1 = fexp2(fmaf(s1[i], c, -lse_q));
+      if (masked) {
+        const int kk = key0 + crow(i, hh);
+        if (kk > myq) p0 = 0.f;
+        if (kk + 32 > myq) p1 = 0.f;
+      }
+      s0[i] = p0 * (e0[i] - del_q);
+      s1[i] = p1 * (e1[i] - del_q);
+    }
+    const bf16x8 d00 = pack8(s0, 0), d01 = pack8(s0, 8), d10 = pack8(s1, 0), d11 = pack8(s1, 8);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      dqt[dt] = mfma(tr_frag(kimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), d00, dqt[dt]);
+      dqt[dt] = mfma(tr_frag(kimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), d01, dqt[dt]);
+      dqt[dt] = mfma(tr_frag(kimg, lane, 32 + 4 * hh, 40 + 4 * hh, 32 * dt), d10, dqt[dt]);
+      dqt[dt] = mfma(tr_frag(kimg, lane, 48 + 4 * hh, 56 + 4 * hh, 32 * dt), d11, dqt[dt]);
+    }
+  };
+
+  stage.load(0, smem);
+  dma_sync();
+  int kt = 0;
+  for (; kt < ntiles - 2; ++kt) {
+    tile(kt, false);
+    dma_sync();
+  }
+  for (; kt < ntiles; ++kt) {
+    const int key0 = kt * BK;
+    if (key0 <= q0 + 31) {
+      tile(kt, key0 + BK - 1 > q0);
+    } else if (kt + 1 < ntiles) {
+      stage.load(kt + 1, smem + ((kt + 1) & 1) * (2 * BK * D * 2));
+    }
+    dma_sync();
+  }
+  u16* out = dq + ((size_t)(b * H + hq) * S + myq) * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u16x4 a4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a4[e] = f2bf(dqt[dt][4 * g4 + e] * scale);
+      *reinterpret_cast<u16x4*>(out + 32 * dt + 8 * g4 + 4 * hh) = a4;
+    }
+}
+
 // ==================================================================================== host
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 const u16* bp(const at::Tensor& t) { return reinterpret_cast<const u16*>(t.data_ptr()); }
@@ -767,6 +1001,7 @@ void check_qkv(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
   TORCH_CHECK(k.sizes() == v.sizes() && q.size(0) == k.size(0) && q.size(2) == k.size(2), "attention: shape mismatch");
   TORCH_CHECK(q.size(1) % k.size(1) == 0, "attention: q heads must be a multiple of kv heads");
   TORCH_CHECK(q.size(2) % BQ == 0, "attention: sequence length must be a multiple of 128");
+  TORCH_CHECK(q.size(1) * q.size(2) * D * 2 < (int64_t(1) << 31), "attention: per-batch q/dO bytes must fit the 32-bit buffer offsets");
 }
 
 std::vector<at::Tensor> attn_fwd_impl(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale, bool debug) {
@@ -817,6 +1052,24 @@ std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, co
   const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
   TORCH_CHECK(dout.is_contiguous() && out.is_contiguous() && dout.numel() == q.numel() && out.numel() == q.numel(),
               "attention bwd: dout/out must be contiguous [B, S, H, D]");
+  auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+  auto dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
+  const int rows = B * S * H;
+  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
+                     delta.data_ptr<float>(), B, H, S);
+  const float c = (float)(scale * 1.4426950408889634);
+  hipLaunchKernelGGL(attn_bwd_dkdv3_kernel, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
+                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
+  hipLaunchKernelGGL(attn_bwd_dq2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
+                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
+  return {dq, dk, dv};
+}
+
+// v2 backward (kept for A/B): dK/dV with synchronous slice staging, dQ with two barriers per tile
+std::vector<at::Tensor> attn_bwd_v2(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                    const at::Tensor& out, const at::Tensor& lse, double scale) {
+  check_qkv(q, k, v);
+  const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
   auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
   auto dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
   const int rows = B * S * H;

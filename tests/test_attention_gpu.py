@@ -18,7 +18,7 @@ def fused():
     return f
 
 
-CASES = [(1, 4, 2, 128), (2, 8, 2, 256), (1, 32, 8, 512), (1, 2, 2, 384)]
+CASES = [(1, 4, 2, 128), (2, 8, 2, 256), (1, 32, 8, 512), (1, 2, 2, 384), (2, 8, 2, 1024)]
 
 
 @pytest.mark.parametrize("B,H,Hkv,S", CASES)
@@ -56,6 +56,25 @@ def test_attention_backward(fused, B, H, Hkv, S):
     assert _rel(qh.grad, qf.grad) < 2e-2, _rel(qh.grad, qf.grad)
     assert _rel(kh.grad, kf.grad) < 2e-2, _rel(kh.grad, kf.grad)
     assert _rel(vh.grad, vf.grad) < 2e-2, _rel(vh.grad, vf.grad)
+
+
+def test_attention_kernel_generations_agree(fused):
+    """Forward v2 vs v1 and backward v3 (LDS-DMA pipelines) vs v2: same math, same numbers (up to
+    fp32 summation order)."""
+    torch.manual_seed(3)
+    B, H, Hkv, S = 2, 8, 2, 768
+    q = torch.randn(B, H, S, 128, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
+    do = torch.randn(B, S, H, 128, device="cuda", dtype=torch.bfloat16)
+    hip = fused.hip()
+    o2, l2 = hip.attn_fwd(q, k, v, 128 ** -0.5)
+    o1, l1 = hip.attn_fwd_v1(q, k, v, 128 ** -0.5)
+    assert _rel(o2, o1) < 5e-3 and torch.allclose(l2, l1, atol=1e-3)
+    g3 = hip.attn_bwd(do, q, k, v, o2, l2, 128 ** -0.5)
+    g2 = hip.attn_bwd_v2(do, q, k, v, o2, l2, 128 ** -0.5)
+    for a, b in zip(g3, g2):
+        assert _rel(a, b) < 5e-3, _rel(a, b)
 
 
 def test_attention_causality(fused):
