@@ -23,6 +23,7 @@ import torch
 import torch.distributed as dist
 
 from .llama import Llama, LlamaConfig
+from .gemm_tuning import setup_gemm_tuning
 from .optim import FlatAdamW
 from ..parallel.dp import BucketedAllReduce, broadcast_params
 
@@ -57,16 +58,19 @@ def _choose_device(env, placement: str, discovery: str) -> Dict[str, object]:
 
 def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int = 3, warmup: int = 1, device_kind: str = "cuda",
           placement: str = "best", discovery: str = "auto", bucket_mb: float = 256.0, checkpoint: bool = False, lr: float = 3e-4,
-          attn: str = "hip", seed: int = 0, log: bool = True) -> Dict[str, object]:
+          attn: str = "hip", seed: int = 0, log: bool = True, gemm_tuning: str = "auto",
+          gemm_table: Optional[str] = None) -> Dict[str, object]:
     env = _init_dist(device_kind)
     if device_kind == "cuda":
         pl = _choose_device(env, placement, discovery)
         dev = int(pl["devices"][env["rank"]])
         torch.cuda.set_device(dev)
         device = torch.device("cuda", dev)
+        gemm_mode = setup_gemm_tuning(gemm_tuning, gemm_table, env["rank"])
     else:
         pl = {"devices": [], "best": [], "worst": None, "source": "cpu"}
         device = torch.device("cpu")
+        gemm_mode = "off"
     cfg = LlamaConfig.named(model_name)
     model = Llama(cfg, device=device, seed=seed, checkpoint=checkpoint, attn=attn)
     broadcast_params(model.flat)
@@ -130,6 +134,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "loss_last": float(losses[-1]),
         "buckets": ar.stats["buckets"],
         "bucket_mb": bucket_mb,
+        "gemm_tuning": gemm_mode,
         "max_mem_gb": (torch.cuda.max_memory_allocated(device) / 1e9) if device.type == "cuda" else None,
     }
     if log and env["rank"] == 0:
@@ -151,8 +156,12 @@ def main(argv=None) -> int:
     ap.add_argument("--bucket-mb", type=float, default=256.0)
     ap.add_argument("--checkpoint", action="store_true")
     ap.add_argument("--attn", default="hip", choices=["hip", "sdpa", "sdpa-expand"])
+    ap.add_argument("--gemm-tuning", default="auto", choices=["auto", "off", "use", "tune"],
+                    help="TunableOp library-GEMM selection (models/gemm_tuning.py)")
+    ap.add_argument("--gemm-table", default=None, help="TunableOp results table (default: the shipped MI355X table)")
     a = ap.parse_args(argv)
-    train(a.model, a.batch, a.seq, a.steps, a.warmup, a.device, a.placement, a.discovery, a.bucket_mb, a.checkpoint, attn=a.attn)
+    train(a.model, a.batch, a.seq, a.steps, a.warmup, a.device, a.placement, a.discovery, a.bucket_mb, a.checkpoint, attn=a.attn,
+          gemm_tuning=a.gemm_tuning, gemm_table=a.gemm_table)
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0
