@@ -18,7 +18,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import asdict, dataclass
-from typing import Dict, List, Optional, Tuple
+from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -90,8 +90,24 @@ class LlamaConfig:
 _ALIGN = 64  # elements: keeps every parameter view 128-B aligned for 16-B vector kernels
 
 
+class _ReadyHandle:
+    def __init__(self, hooks: List[Callable], fn: Callable):
+        self._hooks, self._fn = hooks, fn
+
+    def remove(self) -> None:
+        if self._fn in self._hooks:
+            self._hooks.remove(self._fn)
+
+
 class FlatParams:
-    """All parameters as views of one flat bf16 buffer, gradients as views of one flat grad buffer."""
+    """All parameters as views of one flat bf16 buffer, gradients as views of one flat grad buffer.
+
+    Projection weights can be marked *direct* (:class:`_FlatLinear`): their weight-gradient GEMM
+    writes ``dW = dY^T X`` straight into the flat gradient view (``torch.mm(out=)``, ``addmm_`` when
+    accumulating) instead of allocating a temporary that AccumulateGrad then adds in — no add
+    kernel, no 16 GB zero-fill per step.  Readiness of a direct gradient is announced through
+    :meth:`add_ready_hook` (the data-parallel bucket countdown), since no AccumulateGrad runs.
+    """
 
     def __init__(self, shapes: List[Tuple[str, Tuple[int, ...]]], device, dtype=torch.bfloat16):
         self.names = [n for n, _ in shapes]
@@ -110,6 +126,34 @@ class FlatParams:
             p = torch.nn.Parameter(self.data[o:o + k].view(s))
             p.grad = self.grad[o:o + k].view(s)
             self.params[n] = p
+        self.direct: Dict[str, bool] = {}  # name -> "fresh" (not yet written since zero_grad)
+        self._ready: Dict[str, List[Callable]] = {}
+
+    def mark_direct(self, name: str) -> None:
+        self.direct[name] = True
+
+    def add_ready_hook(self, name: str, fn: Callable) -> _ReadyHandle:
+        hooks = self._ready.setdefault(name, [])
+        hooks.append(fn)
+        return _ReadyHandle(hooks, fn)
+
+    def write_grad(self, name: str, dy: torch.Tensor, x: torch.Tensor) -> None:
+        """Weight gradient of ``y = x W^T`` into the flat buffer: ``W.grad (+)= dy^T x``."""
+        view = self.params[name].grad
+        if self.direct[name]:
+            torch.mm(dy.t(), x, out=view)
+            self.direct[name] = False
+        else:
+            view.addmm_(dy.t(), x)
+        for fn in list(self._ready.get(name, ())):
+            fn(self.params[name])
+
+    def fill_unwritten(self) -> None:
+        """Zero the gradients of direct parameters that received none since :meth:`zero_grad`."""
+        for n, fresh in self.direct.items():
+            if fresh:
+                o, e = self.span(n)
+                self.grad[o:e].zero_()
 
     def attach_grads(self) -> None:
         """(Re)bind every ``param.grad`` to its view of the flat gradient buffer."""
@@ -118,11 +162,36 @@ class FlatParams:
             p.grad = self.grad[o:o + k].view(self.shapes[n])
 
     def zero_grad(self) -> None:
-        self.grad.zero_()
+        if not self.direct:
+            self.grad.zero_()
+            return
+        for n in self.names:  # direct gradients are overwritten by their first GEMM instead
+            if n not in self.direct:
+                o, e = self.span(n)
+                self.grad[o:e].zero_()
+        for n in self.direct:
+            self.direct[n] = True
 
     def span(self, name: str) -> Tuple[int, int]:
         o = self.offsets[name]
         return o, o + math.prod(self.shapes[name])
+
+
+class _FlatLinear(torch.autograd.Function):
+    """``y = x W^T`` whose weight gradient is written in place into the flat buffer."""
+
+    @staticmethod
+    def forward(ctx, x, w, flat, name):
+        ctx.save_for_backward(x, w)
+        ctx.flat, ctx.name = flat, name
+        return F.linear(x, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = dy.mm(w) if ctx.needs_input_grad[0] else None
+        ctx.flat.write_grad(ctx.name, dy, x)
+        return dx, None, None, None
 
 
 class Llama(torch.nn.Module):
@@ -134,6 +203,8 @@ class Llama(torch.nn.Module):
         self.flat = FlatParams(cfg.param_shapes(), device)
         for n, p in self.flat.params.items():
             self.register_parameter(n.replace(".", "_"), p)
+            if p.dim() == 2 and n != "tok_emb":
+                self.flat.mark_direct(n)
         self._init(seed)
         cos, sin = fused.rope_tables(cfg.max_seq, cfg.head_dim, cfg.rope_theta, device=device)
         self.register_buffer("rope_cos", cos, persistent=False)
@@ -159,6 +230,9 @@ class Llama(torch.nn.Module):
     def P(self, name: str) -> torch.nn.Parameter:
         return self.flat.params[name]
 
+    def _linear(self, x: torch.Tensor, name: str) -> torch.Tensor:
+        return _FlatLinear.apply(x, self.flat.params[name].detach(), self.flat, name)
+
     # ---------------------------------------------------------------- blocks
     def _attention(self, q, k, v):
         """q [B,H,S,Dh], k/v [B,Hkv,S,Dh] -> [B,S,H,Dh] (token-major, what the o-projection reads)."""
@@ -178,12 +252,12 @@ class Llama(torch.nn.Module):
         cfg = self.cfg
         H, Hkv, Dh = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
         h = fused.rmsnorm(x, self.P(f"l{i}.attn_norm"), cfg.norm_eps)
-        qkv = F.linear(h, self.P(f"l{i}.wqkv"))
+        qkv = self._linear(h, f"l{i}.wqkv")
         q, k, v = fused.rope_split(qkv, self.rope_cos, self.rope_sin, B, S, H, Hkv, Dh)
         o = self._attention(q, k, v).reshape(B * S, H * Dh)  # [B, S, H, Dh] -> [B*S, H*Dh]
-        x = x + F.linear(o, self.P(f"l{i}.wo"))
+        x = x + self._linear(o, f"l{i}.wo")
         h = fused.rmsnorm(x, self.P(f"l{i}.ffn_norm"), cfg.norm_eps)
-        x = x + F.linear(fused.swiglu(F.linear(h, self.P(f"l{i}.w13"))), self.P(f"l{i}.w2"))
+        x = x + self._linear(fused.swiglu(self._linear(h, f"l{i}.w13")), f"l{i}.w2")
         return x
 
     def forward(self, tokens: torch.Tensor, labels: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -195,7 +269,7 @@ class Llama(torch.nn.Module):
             else:
                 x = self._layer(i, x, B, S)
         x = fused.rmsnorm(x, self.P("norm"), self.cfg.norm_eps)
-        logits = F.linear(x, self.P("lm_head"))  # [B*S, V]
+        logits = self._linear(x, "lm_head")  # [B*S, V]
         if labels is None:
             return logits.view(B, S, -1)
         return fused.cross_entropy(logits, labels.reshape(-1))

@@ -81,8 +81,12 @@ class BucketedAllReduce:
         self._hooks = []
         self.stats = {"buckets": len(self.buckets), "bucket_mb": bucket_mb, "launches": 0, "comm_bytes": 0}
         if overlap and self.world > 1:
+            direct = getattr(flat, "direct", {})
             for n, p in flat.params.items():
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(n)))
+                if n in direct:  # weight-gradient GEMM writes the flat buffer itself (models/llama.py _FlatLinear)
+                    self._hooks.append(flat.add_ready_hook(n, self._make_hook(n)))
+                else:
+                    self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(n)))
         self.reset()
 
     def _make_hook(self, name: str):
@@ -108,6 +112,8 @@ class BucketedAllReduce:
 
     def finish(self) -> None:
         """After ``loss.backward()``: launch stragglers (params without grads), wait for everything."""
+        if hasattr(self.flat, "fill_unwritten"):
+            self.flat.fill_unwritten()  # a direct gradient nobody wrote this step is zero, not stale
         if self.world > 1:
             for b in self.buckets:
                 if b.work is None:

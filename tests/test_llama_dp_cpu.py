@@ -46,6 +46,43 @@ def test_forward_backward_accumulates_into_flat_grad():
     assert all(p.grad.data_ptr() == m.flat.grad[m.flat.span(n)[0]:].data_ptr() for n, p in m.flat.params.items())
 
 
+def test_direct_weight_grads_match_autograd_and_accumulate():
+    """Projection weight gradients written in place by the GEMM (models/llama.py _FlatLinear) equal
+    plain autograd's, a second backward without zero_grad accumulates, zero_grad restarts."""
+    cfg = LlamaConfig.tiny()
+    m = Llama(cfg, device="cpu", seed=3)
+    assert "lm_head" in m.flat.direct and "l0.wqkv" in m.flat.direct and "tok_emb" not in m.flat.direct
+    tok = torch.randint(0, cfg.vocab, (2, 16), generator=torch.Generator().manual_seed(5))
+    lab = torch.roll(tok, -1, 1)
+    m.flat.zero_grad()
+    m(tok, lab).backward()
+    g1 = m.flat.grad.float().clone()
+    # reference: the same math with every weight an ordinary autograd leaf
+    ref = {n: p.detach().float().clone().requires_grad_(True) for n, p in m.flat.params.items()}
+    x = torch.nn.functional.embedding(tok.reshape(-1), ref["tok_emb"])
+    B, S = tok.shape
+    H, Hkv, Dh = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
+    cos, sin = fused.rope_tables(cfg.max_seq, Dh, cfg.rope_theta)
+    for i in range(cfg.n_layers):
+        h = fused.rmsnorm_ref(x, ref[f"l{i}.attn_norm"], cfg.norm_eps)
+        q, k, v = fused.rope_split_ref(h @ ref[f"l{i}.wqkv"].t(), cos, sin, B, S, H, Hkv, Dh)
+        o = fused.attention_ref(q, k, v).reshape(B * S, H * Dh)
+        x = x + o @ ref[f"l{i}.wo"].t()
+        h = fused.rmsnorm_ref(x, ref[f"l{i}.ffn_norm"], cfg.norm_eps)
+        x = x + fused.swiglu_ref(h @ ref[f"l{i}.w13"].t()) @ ref[f"l{i}.w2"].t()
+    logits = fused.rmsnorm_ref(x, ref["norm"], cfg.norm_eps) @ ref["lm_head"].t()
+    torch.nn.functional.cross_entropy(logits.float(), lab.reshape(-1)).backward()
+    for n in ("lm_head", "l0.wqkv", "l1.w2", "l0.wo"):
+        o_, e_ = m.flat.span(n)
+        got, want = g1[o_:e_].view_as(ref[n]), ref[n].grad
+        assert (got - want).norm() / want.norm() < 5e-2, n
+    m(tok, lab).backward()  # no zero_grad: accumulate
+    assert torch.allclose(m.flat.grad.float(), 2 * g1, rtol=2e-2, atol=1e-4)
+    m.flat.zero_grad()
+    m(tok, lab).backward()
+    assert torch.allclose(m.flat.grad.float(), g1, rtol=1e-2, atol=1e-5)
+
+
 def test_reference_ops_match_definitions():
     x = torch.randn(4, 64, dtype=torch.bfloat16)
     w = torch.rand(64, dtype=torch.bfloat16) + 0.5
