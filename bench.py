@@ -27,6 +27,11 @@ import time
 
 METRIC = "RCCL all-reduce bus GB/s on scheduler-chosen k-GPU subset, k=1/2/4/8"
 
+# (minCTAs, maxCTAs) of ncclConfig_t tried by the tuning pass; (0, 0) = RCCL's own channel count.
+# A k-subset of the xGMI full mesh has k-1 links per GPU; more channels put more rings/CTAs on
+# them, and which count saturates the links depends on k, so it is measured on the node.
+TUNE_CANDIDATES = [(0, 0), (32, 128), (64, 128), (112, 128)]
+
 
 def _free_port() -> int:
     with socket.socket() as s:
@@ -46,7 +51,63 @@ def parse(argv=None):
     ap.add_argument("--inplace", action="store_true")
     ap.add_argument("--probe", default=None, choices=[None, "quick", "full"], help="run the HIP link probe before placement")
     ap.add_argument("--discovery", default="auto", choices=["auto", "amdsmi", "sysfs", "fake"])
+    ap.add_argument("--ctas", default="auto",
+                    help="RCCL channel (CTA) bounds of the measured communicator: 'auto' = short tuning pass over "
+                         f"{TUNE_CANDIDATES} at k >= 2 (untimed, before warmup), 'tune' = that pass at any k, "
+                         "'default' = RCCL's choice, or MIN[:MAX]")
+    ap.add_argument("--tune-steps", type=int, default=3, help="timed all-reduces per candidate in the tuning pass")
     return ap.parse_args(argv)
+
+
+def parse_ctas(spec: str):
+    if spec in ("auto", "tune", "default"):
+        return None
+    lo, _, hi = spec.partition(":")
+    return (int(lo), int(hi or 0))
+
+
+def tune_ctas(env, device, nbytes, args, tdev, barrier_kw):
+    """Untimed pass: one communicator per TUNE_CANDIDATES entry, ``--tune-steps`` all-reduces of the
+    full message each (max over ranks); returns the fastest (min, max) and the table.  Every rank
+    builds every candidate (init is collective) and agrees on the winner through an all-reduce."""
+    import torch
+    import torch.distributed as dist
+
+    from gpu_topology_on_k8s_amd.parallel.allreduce import AllReduceRunner
+
+    table = []
+    best, best_ms = None, float("inf")
+    for i, cand in enumerate(TUNE_CANDIDATES):
+        try:
+            r = AllReduceRunner(env, device, nbytes, args.dtype, backend="native", inplace=args.inplace,
+                                ctas=cand if cand != (0, 0) else None, tag=f"/tune{i}")
+            ok = 1
+        except Exception as e:  # noqa: BLE001 - skipped by every rank together
+            print(f"bench: ctas {cand} unavailable on rank {env.rank}: {e}", file=sys.stderr)
+            r, ok = None, 0
+        flag = torch.tensor([ok], dtype=torch.int32, device=tdev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 0:
+            if r is not None:
+                r.close()
+            continue
+        r.step()
+        r.synchronize()
+        dist.barrier(**barrier_kw)
+        t0 = time.perf_counter()
+        for _ in range(max(1, args.tune_steps)):
+            r.step()
+        r.synchronize()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=tdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item()) / max(1, args.tune_steps) * 1e3
+        r.close()
+        table.append({"ctas": list(cand), "ms_per_step": round(ms, 4)})
+        if ms < best_ms:
+            best, best_ms = cand, ms
+    if best is None or best == (0, 0):
+        return None, table
+    return best, table
 
 
 def main(argv=None) -> int:
@@ -93,12 +154,17 @@ def main(argv=None) -> int:
         torch.cuda.set_device(device)
 
     nbytes = int(args.size_mb * (1 << 20))
+    ctas = parse_ctas(args.ctas)
+    tuning = None
+    if args.backend == "native" and (args.ctas == "tune" or (args.ctas == "auto" and env.world > 1)):
+        ctas, tuning = tune_ctas(env, device, nbytes, args, tdev, barrier_kw)
     runner = None
     if args.backend == "native":
         # The native communicator (csrc/rccl) is the measured path; if its extension cannot be
         # loaded on some rank, every rank falls back together to dist.all_reduce (the same RCCL).
         try:
-            runner = AllReduceRunner(env, device, nbytes, args.dtype, backend="native", inplace=args.inplace)
+            runner = AllReduceRunner(env, device, nbytes, args.dtype, backend="native", inplace=args.inplace,
+                                     ctas=ctas, tag="/final")
             ok = 1
         except Exception as e:  # noqa: BLE001 - reported, then the whole job falls back
             print(f"bench: native RCCL communicator unavailable on rank {env.rank}: {e}", file=sys.stderr)
@@ -170,7 +236,9 @@ def main(argv=None) -> int:
                 "worst_score": choice.worst_score,
                 "topology_source": choice.source,
                 "probed": choice.probed,
+                "rccl_ctas": list(ctas) if ctas else "rccl-default",
             },
+            "ctas_tuning": tuning,
             "value_kind": "busbw" if env.world > 1 else "algbw (busbw = 0 at k=1)",
             "algbw_gbps": round(algbw, 3),
             "busbw_gbps": round(busbw, 3),

@@ -18,7 +18,9 @@ namespace {
 
 class Comm {
  public:
-  Comm(py::bytes uid, int nranks, int rank, int device) {
+  // min_ctas / max_ctas > 0 go through ncclCommInitRankConfig (ncclConfig_t.minCTAs/maxCTAs =
+  // the communicator's channel count bounds); bench.py tunes them per subset size on the node.
+  Comm(py::bytes uid, int nranks, int rank, int device, int min_ctas, int max_ctas) {
     std::string s = uid;
     if (s.size() != sizeof(ncclUniqueId)) throw std::invalid_argument("unique id must be NCCL_UNIQUE_ID_BYTES long");
     ncclUniqueId id;
@@ -28,7 +30,16 @@ class Comm {
     st_.nranks = nranks;
     py::gil_scoped_release nogil;
     st_.set_device();
-    NCCL_CHECK(ncclCommInitRank(&st_.comm, nranks, id, rank));
+    if (min_ctas > 0 || max_ctas > 0) {
+      ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+      if (min_ctas > 0) cfg.minCTAs = min_ctas;
+      if (max_ctas > 0) cfg.maxCTAs = max_ctas;
+      NCCL_CHECK(ncclCommInitRankConfig(&st_.comm, nranks, id, rank, &cfg));
+    } else {
+      NCCL_CHECK(ncclCommInitRank(&st_.comm, nranks, id, rank));
+    }
+    min_ctas_ = min_ctas;
+    max_ctas_ = max_ctas;
     RCCL_HIP_CHECK(hipStreamCreateWithFlags(&st_.stream, hipStreamNonBlocking));
   }
   ~Comm() { st_.release(); }
@@ -64,12 +75,15 @@ class Comm {
   int rank() const { return st_.rank; }
   int nranks() const { return st_.nranks; }
   int device() const { return st_.device; }
+  int min_ctas() const { return min_ctas_; }
+  int max_ctas() const { return max_ctas_; }
   void destroy() { st_.release(); }
 
  private:
   RankState st_;
   ncclDataType_t t_ = ncclBfloat16;
   size_t elem_ = 2, count_ = 0;
+  int min_ctas_ = 0, max_ctas_ = 0;
 };
 
 py::bytes unique_id() {
@@ -117,7 +131,8 @@ PYBIND11_MODULE(_rccl, m) {
   m.def("local_sweep", &local_sweep, py::arg("devs"), py::arg("sizes"), py::arg("dtype") = "bf16", py::arg("iters") = 20,
         py::arg("warmup") = 5, py::arg("inplace") = false, py::arg("check") = true);
   py::class_<Comm>(m, "Comm")
-      .def(py::init<py::bytes, int, int, int>(), py::arg("uid"), py::arg("nranks"), py::arg("rank"), py::arg("device"))
+      .def(py::init<py::bytes, int, int, int, int, int>(), py::arg("uid"), py::arg("nranks"), py::arg("rank"),
+           py::arg("device"), py::arg("min_ctas") = 0, py::arg("max_ctas") = 0)
       .def("prepare", &Comm::prepare, py::arg("bytes"), py::arg("dtype") = "bf16",
            py::call_guard<py::gil_scoped_release>())
       .def("step", &Comm::step, py::arg("inplace") = false, py::call_guard<py::gil_scoped_release>())
@@ -127,5 +142,7 @@ PYBIND11_MODULE(_rccl, m) {
       .def_property_readonly("bytes", &Comm::bytes)
       .def_property_readonly("rank", &Comm::rank)
       .def_property_readonly("nranks", &Comm::nranks)
-      .def_property_readonly("device", &Comm::device);
+      .def_property_readonly("device", &Comm::device)
+      .def_property_readonly("min_ctas", &Comm::min_ctas)
+      .def_property_readonly("max_ctas", &Comm::max_ctas);
 }

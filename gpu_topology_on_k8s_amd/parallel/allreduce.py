@@ -116,7 +116,11 @@ def choose_subset(k: int, probe: Optional[str] = None, backend: str = "auto", vi
 class AllReduceRunner:
     """One rank's side of the measured all-reduce (native RCCL comm or torch.distributed)."""
 
-    def __init__(self, env: DistEnv, device: int, nbytes: int, dtype: str = "bf16", backend: str = "native", inplace: bool = False):
+    def __init__(self, env: DistEnv, device: int, nbytes: int, dtype: str = "bf16", backend: str = "native", inplace: bool = False,
+                 ctas: Optional[Sequence[int]] = None, tag: str = ""):
+        """``ctas = (min, max)`` bounds the RCCL communicator's channel (CTA) count through
+        ``ncclConfig_t`` (0 = RCCL's own choice); ``tag`` keeps the unique-id store key of several
+        communicators built one after another (bench.py's tuning pass) apart."""
         import torch
 
         self.env, self.device, self.dtype, self.inplace = env, device, dtype, inplace
@@ -127,13 +131,14 @@ class AllReduceRunner:
             from .._native import load
 
             rccl = load("_rccl")
-            key = "gtk/rccl_uid"
+            key = f"gtk/rccl_uid{tag}"
             if env.rank == 0:
                 uid = rccl.unique_id()
                 env.store.set(key, uid)
             else:
                 uid = env.store.get(key)
-            self.comm = rccl.Comm(bytes(uid), env.world, env.rank, device)
+            mn, mx = (int(ctas[0]), int(ctas[1])) if ctas else (0, 0)
+            self.comm = rccl.Comm(bytes(uid), env.world, env.rank, device, mn, mx)
             self.comm.prepare(int(nbytes), dtype)
             self.nbytes = int(self.comm.bytes)
         elif backend in ("torch", "cpu"):

@@ -36,3 +36,12 @@ def test_bench_two_ranks_gloo():
 def test_bench_single_rank_cpu():
     out = _bench("--backend", "cpu", "--steps", "2", "--warmup", "1", "--size-mb", "1")
     assert out["n_gpus"] == 1 and out["busbw_gbps"] == 0.0 and out["value"] == out["algbw_gbps"]
+
+
+def test_parse_ctas():
+    sys.path.insert(0, REPO)
+    import bench
+
+    assert bench.parse_ctas("auto") is None and bench.parse_ctas("default") is None
+    assert bench.parse_ctas("64") == (64, 0) and bench.parse_ctas("32:64") == (32, 64)
+    assert (0, 0) in bench.TUNE_CANDIDATES

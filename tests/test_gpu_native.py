@@ -105,6 +105,27 @@ def test_rccl_comm_api_single_rank():
     c.destroy()
 
 
+def test_rccl_comm_config_ctas():
+    """ncclCommInitRankConfig path (minCTAs/maxCTAs) builds a working communicator."""
+    from gpu_topology_on_k8s_amd._native import load
+
+    rccl = load("_rccl")
+    c = rccl.Comm(rccl.unique_id(), 1, 0, 0, 32, 64)
+    assert (c.min_ctas, c.max_ctas) == (32, 64)
+    c.prepare(8 << 20, "bf16")
+    assert c.check(False) == 0
+    c.destroy()
+
+
+def test_bench_py_ctas_tuning_pass():
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup", "1", "--size-mb", "64",
+                        "--ctas", "tune"], capture_output=True, text=True, timeout=600, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-4000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert len(out["ctas_tuning"]) >= 1 and all(r["ms_per_step"] > 0 for r in out["ctas_tuning"])
+    assert out["value"] > 0
+
+
 def test_rccl_cli_binary():
     from gpu_topology_on_k8s_amd._native import binary
 
