@@ -49,7 +49,10 @@ def parse(argv=None):
     ap.add_argument("--backend", default="native", choices=["native", "torch", "cpu"],
                     help="native = RCCL communicator from csrc/rccl; torch = dist.all_reduce; cpu = gloo (control-path tests)")
     ap.add_argument("--inplace", action="store_true")
-    ap.add_argument("--probe", default=None, choices=[None, "quick", "full"], help="run the HIP link probe before placement")
+    ap.add_argument("--probe", default="auto", choices=["auto", "off", "quick", "full"],
+                    help="HIP link probe (K4 warm-up + K1 p2p read of every ordered pair) before placement, in a child "
+                         "process of rank 0; 'auto' = quick on GPUs, off for --backend cpu; a failed probe falls back "
+                         "to the discovered link classes")
     ap.add_argument("--discovery", default="auto", choices=["auto", "amdsmi", "sysfs", "fake"])
     ap.add_argument("--ctas", default="auto",
                     help="RCCL channel (CTA) bounds of the measured communicator: 'auto' = short tuning pass over "
@@ -127,7 +130,8 @@ def main(argv=None) -> int:
     import torch.distributed as dist
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    from gpu_topology_on_k8s_amd.parallel.allreduce import AllReduceRunner, DistEnv, SubsetChoice, bus_factor, choose_subset
+    from gpu_topology_on_k8s_amd.parallel.allreduce import (AllReduceRunner, DistEnv, SubsetChoice, bus_factor, choose_subset,
+                                                             probe_node)
 
     env = DistEnv.from_env()
     if env.world != args.gpus:
@@ -139,7 +143,13 @@ def main(argv=None) -> int:
 
     # --- placement: rank 0 picks the subset, everybody binds to subset[rank] ---------------------
     if env.rank == 0:
-        choice = choose_subset(env.world, probe=args.probe, backend=args.discovery, visible=env.world if cpu else None)
+        preset = {"auto": None if cpu else "quick", "off": None}.get(args.probe, args.probe)
+        topo = None
+        if preset:
+            topo, msg = probe_node(preset, backend=args.discovery)
+            if topo is None:
+                print(f"bench: link probe unavailable ({msg}); placing on discovered link classes", file=sys.stderr)
+        choice = choose_subset(env.world, backend=args.discovery, visible=env.world if cpu else None, topology=topo)
         env.store.set("gtk/subset", choice.to_json())
     choice = SubsetChoice.from_json(env.store.get("gtk/subset").decode())
     device = choice.devices[env.rank]
@@ -239,6 +249,7 @@ def main(argv=None) -> int:
                 "rccl_ctas": list(ctas) if ctas else "rccl-default",
             },
             "ctas_tuning": tuning,
+            "link_probe": choice.extra.get("probe"),
             "value_kind": "busbw" if env.world > 1 else "algbw (busbw = 0 at k=1)",
             "algbw_gbps": round(algbw, 3),
             "busbw_gbps": round(busbw, 3),

@@ -25,7 +25,7 @@ from typing import Dict, List, Optional, Sequence
 
 log = logging.getLogger(__name__)
 
-__all__ = ["DistEnv", "choose_subset", "AllReduceRunner", "bus_factor"]
+__all__ = ["DistEnv", "choose_subset", "probe_node", "probe_summary", "AllReduceRunner", "bus_factor"]
 
 
 def bus_factor(k: int) -> float:
@@ -70,17 +70,73 @@ def _visible_device_count() -> int:
     return int(torch.cuda.device_count())
 
 
-def choose_subset(k: int, probe: Optional[str] = None, backend: str = "auto", visible: Optional[int] = None) -> SubsetChoice:
+def probe_node(preset: str = "quick", backend: str = "auto", timeout: float = 240.0):
+    """Node-start link probe in a CHILD process: discovery + K4 warm-up + K1 p2p
+    read over every visible ordered pair, written as topology JSON.  A child keeps the probe's HIP
+    contexts on every device (and any failure) out of the caller, which goes on to build its RCCL
+    communicator on one device.  Returns ``(Topology | None, message)``."""
+    import subprocess
+    import sys
+    import tempfile
+
+    from ..topology.model import Topology
+
+    fd, path = tempfile.mkstemp(prefix="gtk_probe_", suffix=".json")
+    os.close(fd)
+    cmd = [sys.executable, "-m", "gpu_topology_on_k8s_amd", "probe", "--preset", preset, "--discovery", backend, "--out", path]
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=root)
+        if p.returncode != 0:
+            return None, f"probe exited {p.returncode}: {(p.stderr or p.stdout).strip()[-400:]}"
+        with open(path) as f:
+            return Topology.from_json(f.read()), "ok"
+    except subprocess.TimeoutExpired:
+        return None, f"probe timed out after {timeout:.0f}s"
+    except (OSError, ValueError, KeyError) as e:
+        return None, f"probe output unreadable: {e}"
+    finally:
+        try:
+            os.unlink(path)
+        except OSError:
+            pass
+
+
+def probe_summary(topo, subset: Sequence[int]) -> Dict[str, object]:
+    """Compact view of the measured link matrix for the bench JSON line."""
+    import numpy as np
+
+    out: Dict[str, object] = {"meta": topo.probe}
+    if topo.hbm_gbps is not None:
+        out["hbm_copy_gbps"] = [None if not np.isfinite(v) else round(float(v), 1) for v in topo.hbm_gbps]
+    bw = topo.bw_gbps
+    if bw is None:
+        return out
+    off = [float(bw[i, j]) for i in range(topo.n) for j in range(topo.n) if i != j and np.isfinite(bw[i, j])]
+    if off:
+        out["link_read_gbps"] = {"pairs": len(off), "min": round(min(off), 1), "median": round(float(np.median(off)), 1),
+                                 "max": round(max(off), 1)}
+        out["matrix_gbps"] = [[None if (i == j or not np.isfinite(bw[i, j])) else round(float(bw[i, j]), 1) for j in range(topo.n)]
+                              for i in range(topo.n)]
+        sub = [float(bw[i, j]) for i in subset for j in subset if i != j and np.isfinite(bw[i, j])]
+        if sub:
+            out["subset_link_read_gbps"] = {"min": round(min(sub), 1), "max": round(max(sub), 1)}
+    return out
+
+
+def choose_subset(k: int, probe: Optional[str] = None, backend: str = "auto", visible: Optional[int] = None,
+                  topology=None) -> SubsetChoice:
     """Rank-0 side: discover the node, optionally probe links, run the placement core.
 
-    ``visible`` overrides the HIP device count (CPU/gloo runs model a mesh of that many devices)."""
+    ``visible`` overrides the HIP device count (CPU/gloo runs model a mesh of that many devices);
+    ``topology`` is an already discovered (and probed) node, e.g. from :func:`probe_node`."""
     from ..placement import PlacementPolicy, select, worst
     from ..topology.discovery import DiscoveryError, discover, fake_topology
 
     nvis = _visible_device_count() if visible is None else int(visible)
     t0 = time.perf_counter()
     try:
-        topo = discover(backend)
+        topo = topology if topology is not None else discover(backend)
         source = topo.source
         if topo.n != nvis:
             log.warning("topology has %d devices but %d are visible to HIP; using a full-mesh model of the visible set", topo.n, nvis)
@@ -90,8 +146,8 @@ def choose_subset(k: int, probe: Optional[str] = None, backend: str = "auto", vi
         log.warning("topology discovery failed (%s); using a full-mesh model of %d visible devices", e, nvis)
         topo = fake_topology(nvis)
         source = "fallback-mesh"
-    probed = False
-    if probe:
+    probed = bool(topo.probe)
+    if probe and not probed:
         from ..ops.probe import probe_topology
 
         probe_topology(topo, preset=probe)
@@ -109,7 +165,8 @@ def choose_subset(k: int, probe: Optional[str] = None, backend: str = "auto", vi
         worst_score=round(w.score, 4) if w else None,
         placement_ms=round(ms, 4),
         probed=probed,
-        extra={"discovery_ms": round((t1 - t0) * 1e3, 2), "node_devices": topo.n},
+        extra={"discovery_ms": round((t1 - t0) * 1e3, 2), "node_devices": topo.n,
+               **({"probe": probe_summary(topo, pl.ids)} if probed else {})},
     )
 
 

@@ -45,3 +45,32 @@ def test_parse_ctas():
     assert bench.parse_ctas("auto") is None and bench.parse_ctas("default") is None
     assert bench.parse_ctas("64") == (64, 0) and bench.parse_ctas("32:64") == (32, 64)
     assert (0, 0) in bench.TUNE_CANDIDATES
+
+
+def test_choose_subset_uses_probed_topology():
+    """A probed node (measured GB/s) steers the k=2 choice to the fastest pair and is summarised."""
+    import numpy as np
+
+    sys.path.insert(0, REPO)
+    from gpu_topology_on_k8s_amd.parallel.allreduce import choose_subset, probe_summary
+    from gpu_topology_on_k8s_amd.topology.discovery import fake_topology
+
+    topo = fake_topology(4)
+    bw = np.full((4, 4), 50.0)
+    bw[2, 3] = bw[3, 2] = 70.0  # one faster link
+    np.fill_diagonal(bw, np.nan)
+    topo.set_measured_bw(bw, {"method": "p2p_read_lds", "preset": "quick"})
+    ch = choose_subset(2, visible=4, topology=topo)
+    assert sorted(ch.devices) == [2, 3] and ch.probed
+    s = ch.extra["probe"]
+    assert s["link_read_gbps"]["pairs"] == 12 and s["link_read_gbps"]["max"] == 70.0
+    assert s["subset_link_read_gbps"] == {"min": 70.0, "max": 70.0}
+    assert probe_summary(topo, [0, 1])["subset_link_read_gbps"]["max"] == 50.0
+
+
+def test_probe_node_failure_is_reported_not_raised():
+    sys.path.insert(0, REPO)
+    from gpu_topology_on_k8s_amd.parallel.allreduce import probe_node
+
+    topo, msg = probe_node("quick", backend="fake", timeout=120)
+    assert topo is None and "probe" in msg
