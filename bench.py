@@ -59,7 +59,68 @@ def parse(argv=None):
                          f"{TUNE_CANDIDATES} at k >= 2 (untimed, before warmup), 'tune' = that pass at any k, "
                          "'default' = RCCL's choice, or MIN[:MAX]")
     ap.add_argument("--tune-steps", type=int, default=3, help="timed all-reduces per candidate in the tuning pass")
+    ap.add_argument("--sweep", default="auto",
+                    help="after the headline timing: exact-checked size sweep MIN:MAX:FACTOR (nccl-tests style, "
+                         "BASELINE.md target 3, peak busBW reported); 'auto' = 8:16G:8 on GPUs, 8:1M:8 for "
+                         "--backend cpu; or 'off'")
     return ap.parse_args(argv)
+
+
+def parse_size(s: str) -> int:
+    s = s.strip().upper()
+    mult = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30}.get(s[-1:], 1)
+    return int(float(s[:-1] if mult > 1 else s) * mult)
+
+
+def sweep_sizes(spec: str, cpu: bool = False):
+    if spec == "off":
+        return []
+    if spec == "auto":
+        spec = "8:1M:8" if cpu else "8:16G:8"
+    lo, hi, fac = spec.split(":")
+    lo, hi, fac = parse_size(lo), parse_size(hi), max(2, int(fac))
+    out, b = [], lo
+    while b <= hi:
+        out.append(b)
+        b *= fac
+    if out and out[-1] < hi:
+        out.append(hi)
+    return out
+
+
+def run_sweep(runner, sizes, env, tdev, barrier_kw, gpu_sync):
+    """Every size: exact check, 1 warmup, then enough timed all-reduces for ~>=20 ms (max over
+    ranks).  Returns nccl-tests style rows plus the peak busBW (algBW at k = 1)."""
+    import torch
+    import torch.distributed as dist
+
+    from gpu_topology_on_k8s_amd.parallel.allreduce import bus_factor
+
+    rows = []
+    for b in sizes:
+        runner.resize(b)
+        wrong = torch.tensor([runner.check()], dtype=torch.int64, device=tdev)
+        dist.all_reduce(wrong)
+        runner.step()
+        runner.synchronize()
+        iters = 20 if b < (64 << 20) else (5 if b < (1 << 30) else 2)
+        dist.barrier(**barrier_kw)
+        gpu_sync()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            runner.step()
+        runner.synchronize()
+        gpu_sync()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=tdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        us = float(t.item()) / iters * 1e6
+        alg = runner.nbytes / (us * 1e-6) / 1e9
+        rows.append({"bytes": runner.nbytes, "time_us": round(us, 2), "algbw_gbps": round(alg, 3),
+                     "busbw_gbps": round(alg * bus_factor(env.world), 3), "wrong": int(wrong.item())})
+    key = "busbw_gbps" if env.world > 1 else "algbw_gbps"
+    peak = max(rows, key=lambda r: r[key]) if rows else None
+    return {"rows": rows, "peak": {"bytes": peak["bytes"], key: peak[key]} if peak else None,
+            "all_exact": all(r["wrong"] == 0 for r in rows)}
 
 
 def parse_ctas(spec: str):
@@ -212,9 +273,14 @@ def main(argv=None) -> int:
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     ms_per_step = elapsed / max(1, args.steps) * 1e3
-    algbw = runner.nbytes / (ms_per_step / 1e3) / 1e9
+    algbw = runner.nbytes / (ms_per_step / 1e3) / 1e9  # headline size (the sweep below resizes)
     busbw = algbw * bus_factor(env.world)
     value = busbw if env.world > 1 else algbw
+    headline_bytes = runner.nbytes
+    sweep = None
+    sizes = sweep_sizes(args.sweep, cpu=cpu)
+    if sizes:
+        sweep = run_sweep(runner, sizes, env, tdev, barrier_kw, gpu_sync)
     runner.close()
     if env.rank == 0:
         out = {
@@ -233,7 +299,7 @@ def main(argv=None) -> int:
             "config": {
                 "model": "rccl-allreduce",
                 "op": "sum",
-                "message_bytes_per_gpu": runner.nbytes,
+                "message_bytes_per_gpu": headline_bytes,
                 "inplace": args.inplace,
                 "backend": args.backend,
                 "global_batch": None,
@@ -250,6 +316,7 @@ def main(argv=None) -> int:
             },
             "ctas_tuning": tuning,
             "link_probe": choice.extra.get("probe"),
+            "size_sweep": sweep,
             "value_kind": "busbw" if env.world > 1 else "algbw (busbw = 0 at k=1)",
             "algbw_gbps": round(algbw, 3),
             "busbw_gbps": round(busbw, 3),

@@ -212,6 +212,20 @@ class AllReduceRunner:
         else:
             raise ValueError(backend)
 
+    def resize(self, nbytes: int) -> None:
+        """Re-target the runner to ``nbytes`` per rank (the size sweep after the headline timing)."""
+        if self.comm is not None:
+            self.comm.prepare(int(nbytes), self.dtype)
+            self.nbytes = int(self.comm.bytes)
+            return
+        import torch
+
+        esz = self.tensor.element_size()
+        self.tensor = torch.ones(max(1, int(nbytes) // esz), dtype=self.tensor.dtype, device=self.tensor.device)
+        self.nbytes = self.tensor.numel() * esz
+        if self.src is not None:
+            self.src = torch.ones_like(self.tensor)
+
     def check(self) -> int:
         """Exact correctness check of one all-reduce; returns wrong elements on this rank."""
         if self.comm is not None:

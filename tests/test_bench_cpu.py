@@ -31,6 +31,9 @@ def test_bench_two_ranks_gloo():
     assert len(set(out["config"]["subset"])) == 2
     assert out["value"] > 0 and abs(out["busbw_gbps"] - out["algbw_gbps"]) < 1e-3 * out["algbw_gbps"] + 1e-6  # 2(k-1)/k = 1
     assert out["config"]["parallelism"] == "dp2"
+    assert out["config"]["message_bytes_per_gpu"] == 1 << 20
+    sw = out["size_sweep"]
+    assert sw["all_exact"] and [r["bytes"] for r in sw["rows"]][:2] == [8, 64] and sw["peak"]["busbw_gbps"] > 0
 
 
 def test_bench_single_rank_cpu():
@@ -74,3 +77,14 @@ def test_probe_node_failure_is_reported_not_raised():
 
     topo, msg = probe_node("quick", backend="fake", timeout=120)
     assert topo is None and "probe" in msg
+
+
+def test_sweep_sizes():
+    sys.path.insert(0, REPO)
+    import bench
+
+    assert bench.sweep_sizes("off") == []
+    full = bench.sweep_sizes("auto")
+    assert full[0] == 8 and full[-1] == 16 << 30 and full[-2] == 8 << 30
+    assert bench.sweep_sizes("auto", cpu=True)[-1] == 1 << 20
+    assert bench.sweep_sizes("1K:4K:2") == [1024, 2048, 4096]

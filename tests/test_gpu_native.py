@@ -143,3 +143,6 @@ def test_bench_py_single_gpu():
     line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
     out = json.loads(line)
     assert out["n_gpus"] == 1 and out["value"] > 0 and out["config"]["subset"] == [0]
+    assert out["config"]["message_bytes_per_gpu"] == 64 << 20
+    sw = out["size_sweep"]  # 8 B .. 16 GiB, every size exactly checked
+    assert sw["all_exact"] and sw["rows"][-1]["bytes"] == 16 << 30 and sw["peak"]["algbw_gbps"] > 0
