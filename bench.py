@@ -210,6 +210,8 @@ def main(argv=None) -> int:
             topo, msg = probe_node(preset, backend=args.discovery)
             if topo is None:
                 print(f"bench: link probe unavailable ({msg}); placing on discovered link classes", file=sys.stderr)
+            elif msg != "ok":
+                print(f"bench: link probe: {msg}", file=sys.stderr)
         choice = choose_subset(env.world, backend=args.discovery, visible=env.world if cpu else None, topology=topo)
         env.store.set("gtk/subset", choice.to_json())
     choice = SubsetChoice.from_json(env.store.get("gtk/subset").decode())
@@ -283,6 +285,7 @@ def main(argv=None) -> int:
         sweep = run_sweep(runner, sizes, env, tdev, barrier_kw, gpu_sync)
     runner.close()
     if env.rank == 0:
+        bound = (choice.extra.get("probe") or {}).get("subset_ingress_bound_gbps")  # K5/K1 ceiling of busBW
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -318,6 +321,7 @@ def main(argv=None) -> int:
             "link_probe": choice.extra.get("probe"),
             "size_sweep": sweep,
             "value_kind": "busbw" if env.world > 1 else "algbw (busbw = 0 at k=1)",
+            "busbw_vs_probe_bound": round(busbw / bound, 4) if bound else None,
             "algbw_gbps": round(algbw, 3),
             "busbw_gbps": round(busbw, 3),
         }

@@ -10,6 +10,8 @@
 //   K3 hbm copy  : self pair (k=1 baseline), same kernel with both pointers local.
 //   K4 mfma warm : v_mfma_f32_32x32x16_bf16 loop to lift clocks before timing, also reporting the
 //                  achieved dense bf16 rate.
+//   K5 gather    : one kernel on the reader pulls from all of its peers at once -> aggregate xGMI
+//                  ingress per GPU, the bound a ring all-reduce's busBW is measured against.
 // The copy kernel exists in two staging forms (LDS-DMA and plain register staging) so the
 // rocprofv3 counter profile can show what LDS staging costs/buys on a pure stream (profiles/).
 //
@@ -26,6 +28,7 @@
 #include <chrono>
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -58,14 +61,14 @@ using lptr_t = __attribute__((address_space(3))) void*;
 // K1/K2/K3: LDS-DMA staged copy.  Each wave issues kUnroll global_load_lds_dwordx4 into its own
 // 1 KiB LDS slices (wave-uniform base + lane*16: the DMA's lane-linear rule), drains vmcnt, then
 // each lane stores back the 16 B its own lane fetched, so no cross-wave barrier is needed.
+// `blk`/`nblk` let one launch split its grid over several streams (K5 gather below).
 template <bool kNonTemporal>
-__global__ __launch_bounds__(kBlock) void copy_lds_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
-                                                          size_t n_vec) {
-  __shared__ u32x4 lds[kTileVec];
+__device__ __forceinline__ void copy_lds_stream(const u32x4* __restrict__ src, u32x4* __restrict__ dst, size_t n_vec,
+                                                u32x4* lds, size_t blk, size_t nblk) {
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const size_t n_full = (n_vec / kTileVec) * kTileVec;
-  for (size_t base = (size_t)blockIdx.x * kTileVec; base < n_full; base += (size_t)gridDim.x * kTileVec) {
+  for (size_t base = blk * kTileVec; base < n_full; base += nblk * kTileVec) {
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const size_t off = base + (size_t)u * kBlock + wave * 64;
@@ -83,8 +86,29 @@ __global__ __launch_bounds__(kBlock) void copy_lds_kernel(const u32x4* __restric
     }
   }
   // tail (< one tile): plain per-thread copy
-  for (size_t i = n_full + (size_t)blockIdx.x * kBlock + threadIdx.x; i < n_vec; i += (size_t)gridDim.x * kBlock)
-    dst[i] = src[i];
+  for (size_t i = n_full + blk * kBlock + threadIdx.x; i < n_vec; i += nblk * kBlock) dst[i] = src[i];
+}
+
+template <bool kNonTemporal>
+__global__ __launch_bounds__(kBlock) void copy_lds_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                          size_t n_vec) {
+  __shared__ u32x4 lds[kTileVec];
+  copy_lds_stream<kNonTemporal>(src, dst, n_vec, lds, blockIdx.x, gridDim.x);
+}
+
+// K5 gather: one launch on the reader pulls from up to kMaxSrc peers at once (ingress over all of
+// its xGMI links together).  Block b serves source b % nsrc, so every source gets gridDim/nsrc
+// blocks spread over all XCDs; source s lands in dst[s * n_vec ...].
+constexpr int kMaxSrc = 16;
+struct SrcSet {
+  const u32x4* p[kMaxSrc];
+};
+
+__global__ __launch_bounds__(kBlock) void gather_lds_kernel(SrcSet srcs, int nsrc, u32x4* __restrict__ dst,
+                                                            size_t n_vec) {
+  __shared__ u32x4 lds[kTileVec];
+  const int s = blockIdx.x % nsrc;
+  copy_lds_stream<true>(srcs.p[s], dst + (size_t)s * n_vec, n_vec, lds, blockIdx.x / nsrc, gridDim.x / nsrc);
 }
 
 // Register-staged variant of the same stream (kUnroll independent 16-B loads in flight per lane).
@@ -284,6 +308,87 @@ CopyResult copy_bw_impl(int src_dev, int dst_dev, int exec_dev, size_t bytes, in
                     (double)bytes / sec / 1e9};
 }
 
+// K5: aggregate ingress of `dst_dev` reading `bytes` from every device in `srcs` concurrently.
+// A source equal to dst_dev is a local stream (one buffer per entry), which lets a 1-GPU box check
+// the kernel's segment indexing; on a node the sources are the peers.
+py::dict gather_bw(int dst_dev, const std::vector<int>& srcs, size_t bytes, int iters, int warmup, int blocks_per_cu) {
+  if (srcs.empty() || srcs.size() > (size_t)kMaxSrc) throw std::invalid_argument("1..16 source devices");
+  if (bytes < 16 || bytes % 16) throw std::invalid_argument("bytes must be a positive multiple of 16");
+  if (iters < 1) throw std::invalid_argument("iters >= 1");
+  int ndev = 0;
+  HIP_CHECK(hipGetDeviceCount(&ndev));
+  if (dst_dev < 0 || dst_dev >= ndev) throw std::invalid_argument("device index out of range");
+  for (int d : srcs) {
+    if (d < 0 || d >= ndev) throw std::invalid_argument("source device index out of range");
+  }
+  double ms_total = 0.0;
+  bool ok = true;
+  const int nsrc = (int)srcs.size();
+  {
+    py::gil_scoped_release nogil;
+    for (int d : srcs) enable_peer(dst_dev, d);
+    std::vector<std::unique_ptr<DevBuf>> src_bufs;
+    SrcSet set{};
+    for (int i = 0; i < nsrc; ++i) {
+      src_bufs.emplace_back(new DevBuf(srcs[i], bytes));
+      DeviceGuard g(srcs[i]);
+      hipLaunchKernelGGL(fill_pattern_kernel, dim3(num_cus(srcs[i]) * 4), dim3(kBlock), 0, 0,
+                         (unsigned int*)src_bufs.back()->p, bytes / 4, 0x51ed27u ^ (unsigned)(srcs[i] * 977));
+      HIP_CHECK(hipGetLastError());
+      HIP_CHECK(hipDeviceSynchronize());
+      set.p[i] = reinterpret_cast<const u32x4*>(src_bufs.back()->p);
+    }
+    DevBuf dst(dst_dev, bytes * (size_t)nsrc);
+    DeviceGuard g(dst_dev);
+    hipStream_t st;
+    HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    const int per = std::max(1, num_cus(dst_dev) * std::max(1, blocks_per_cu) / nsrc);
+    const int grid = per * nsrc;  // a multiple of nsrc: every source gets the same block count
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    for (int i = 0; i < warmup; ++i)
+      hipLaunchKernelGGL(gather_lds_kernel, dim3(grid), dim3(kBlock), 0, st, set, nsrc, (u32x4*)dst.p, bytes / 16);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipEventRecord(e0, st));
+    for (int i = 0; i < iters; ++i)
+      hipLaunchKernelGGL(gather_lds_kernel, dim3(grid), dim3(kBlock), 0, st, set, nsrc, (u32x4*)dst.p, bytes / 16);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipEventRecord(e1, st));
+    HIP_CHECK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    ms_total = ms;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipStreamDestroy(st);
+    // verify every segment against its source's pattern (windows, as for the pairwise probe)
+    const size_t words = bytes / 4, win = std::min<size_t>(words, 1 << 14);
+    std::vector<unsigned int> h(win);
+    for (int i = 0; i < nsrc && ok; ++i) {
+      const unsigned int seed = 0x51ed27u ^ (unsigned)(srcs[i] * 977);
+      for (size_t st0 : {(size_t)0, words - win}) {
+        HIP_CHECK(hipMemcpy(h.data(), (const unsigned int*)dst.p + (size_t)i * words + st0, win * 4, hipMemcpyDeviceToHost));
+        for (size_t k = 0; k < win; ++k)
+          if (h[k] != ((unsigned int)((st0 + k) * 2654435761u) ^ seed)) {
+            ok = false;
+            break;
+          }
+      }
+    }
+  }
+  const double sec = ms_total / 1e3 / iters;
+  py::dict r;
+  r["dst"] = dst_dev;
+  r["srcs"] = srcs;
+  r["bytes_per_src"] = bytes;
+  r["iters"] = iters;
+  r["ms_per_iter"] = ms_total / iters;
+  r["gbps"] = (double)bytes * nsrc / sec / 1e9;
+  r["ok"] = ok;
+  return r;
+}
+
 py::dict to_dict(const CopyResult& c) {
   py::dict r;
   r["src"] = c.src;
@@ -416,6 +521,8 @@ PYBIND11_MODULE(_probe, m) {
   m.def("copy_bw", &copy_bw, py::arg("src_dev"), py::arg("dst_dev"), py::arg("exec_dev"), py::arg("bytes"),
         py::arg("iters") = 10, py::arg("warmup") = 2, py::arg("kind") = "lds", py::arg("nontemporal") = false,
         py::arg("blocks_per_cu") = kBlocksPerCU);
+  m.def("gather_bw", &gather_bw, py::arg("dst_dev"), py::arg("srcs"), py::arg("bytes") = (size_t)64 << 20,
+        py::arg("iters") = 3, py::arg("warmup") = 1, py::arg("blocks_per_cu") = kBlocksPerCU);
   m.def("mfma_warmup", &mfma_warmup, py::arg("dev"), py::arg("target_ms") = 50.0, py::arg("iters_per_launch") = 4096);
   m.def("probe_matrix", &probe_matrix, py::arg("devs"), py::arg("bytes") = (size_t)256 << 20, py::arg("iters") = 5,
         py::arg("warmup") = 1, py::arg("mode") = "read", py::arg("kind") = "lds", py::arg("nontemporal") = false,

@@ -53,11 +53,18 @@ def cmd_probe(a) -> int:
 
     t = _topology(a)
     probe_topology(t, preset=a.preset, mode=a.mode)
-    print(t.render())
-    print(json.dumps({"probe": t.probe, "hbm_gbps": [None if x != x else round(float(x), 1) for x in t.hbm_gbps]}))
-    if a.out:
+    if a.out:  # written before the ingress stage, so a failure there keeps the pairwise matrix
         with open(a.out, "w") as f:
             f.write(t.to_json())
+    if a.ingress:
+        from .ops.probe import measure_ingress
+
+        measure_ingress(t, t.probe.get("devices", list(range(t.n))), preset=a.preset)
+        if a.out:
+            with open(a.out, "w") as f:
+                f.write(t.to_json())
+    print(t.render())
+    print(json.dumps({"probe": t.probe, "hbm_gbps": [None if x != x else round(float(x), 1) for x in t.hbm_gbps]}))
     return 0
 
 
@@ -145,6 +152,7 @@ def main(argv=None) -> int:
     disc(p)
     p.add_argument("--preset", default="quick", choices=["quick", "full"])
     p.add_argument("--mode", default="read", choices=["read", "write"])
+    p.add_argument("--ingress", action="store_true", help="also measure each GPU's all-peer ingress (K5 gather)")
     p.add_argument("--out", default="")
     p.set_defaults(fn=cmd_probe)
     p = sub.add_parser("select")

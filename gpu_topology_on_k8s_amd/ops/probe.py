@@ -17,7 +17,8 @@ import numpy as np
 from .._native import load
 from ..topology.model import Topology
 
-__all__ = ["device_count", "device_props", "warmup", "copy_bw", "measure_matrix", "probe_topology", "PROBE_PRESETS"]
+__all__ = ["device_count", "device_props", "warmup", "copy_bw", "gather_bw", "measure_matrix", "measure_ingress",
+           "probe_topology", "ingress_bound", "PROBE_PRESETS"]
 
 #: bytes per transfer / timed iterations; sizes exceed the 256 MiB Infinity Cache for "full".
 PROBE_PRESETS: Dict[str, Dict[str, int]] = {
@@ -47,6 +48,48 @@ def copy_bw(src: int, dst: int, nbytes: int = 256 << 20, iters: int = 10, warmup
             kind: str = "lds", nontemporal: bool = False, blocks_per_cu: int = 8) -> Dict[str, object]:
     exec_dev = dst if mode == "read" else src
     return dict(_p().copy_bw(src, dst, exec_dev, int(nbytes), int(iters), int(warmup_iters), kind, bool(nontemporal), int(blocks_per_cu)))
+
+
+def gather_bw(dst: int, srcs: Sequence[int], nbytes: int = 64 << 20, iters: int = 3, warmup_iters: int = 1) -> Dict[str, object]:
+    """K5: one kernel on ``dst`` reads ``nbytes`` from every device in ``srcs`` at once (aggregate ingress)."""
+    return dict(_p().gather_bw(int(dst), [int(s) for s in srcs], int(nbytes), int(iters), int(warmup_iters)))
+
+
+def measure_ingress(topo: Topology, devs: Sequence[int], preset: str = "quick") -> List[Optional[float]]:
+    """Aggregate ingress GB/s of every device in ``devs`` reading from all the others concurrently
+    (K5); stored in ``topo.probe["ingress_all_gbps"]`` (None where fewer than two devices)."""
+    cfg = PROBE_PRESETS[preset]
+    out: List[Optional[float]] = [None] * topo.n
+    for d in devs:
+        peers = [s for s in devs if s != d and bool(_p().can_access_peer(d, s))]
+        if not peers:
+            continue
+        r = gather_bw(d, peers, cfg["bytes"], cfg["iters"], cfg["warmup"])
+        if not r["ok"]:
+            raise RuntimeError(f"ingress probe verification failed on device {d}")
+        out[d] = round(float(r["gbps"]), 2)
+    topo.probe = dict(topo.probe, ingress_all_gbps=out)
+    return out
+
+
+def ingress_bound(topo: Topology, subset: Sequence[int]) -> Optional[float]:
+    """Probe-derived ceiling of an all-reduce's busBW on ``subset``: each member's ingress over its
+    |subset|-1 links (sum of the measured pairwise reads, capped by its measured all-peer ingress),
+    minimum over members.  busBW = bytes each GPU sends / time, so it cannot exceed this."""
+    subset = list(subset)
+    if len(subset) < 2 or topo.bw_gbps is None:
+        return None
+    ing = (topo.probe or {}).get("ingress_all_gbps") or [None] * topo.n
+    best = None
+    for d in subset:
+        links = [float(topo.bw_gbps[s, d]) for s in subset if s != d]
+        if not all(np.isfinite(links)):
+            return None
+        cap = sum(links)
+        if ing[d] is not None:
+            cap = min(cap, float(ing[d]))
+        best = cap if best is None else min(best, cap)
+    return best
 
 
 def measure_matrix(devs: Sequence[int], nbytes: int = 64 << 20, iters: int = 3, warmup_iters: int = 1, mode: str = "read",

@@ -83,14 +83,17 @@ def probe_node(preset: str = "quick", backend: str = "auto", timeout: float = 24
 
     fd, path = tempfile.mkstemp(prefix="gtk_probe_", suffix=".json")
     os.close(fd)
-    cmd = [sys.executable, "-m", "gpu_topology_on_k8s_amd", "probe", "--preset", preset, "--discovery", backend, "--out", path]
+    cmd = [sys.executable, "-m", "gpu_topology_on_k8s_amd", "probe", "--preset", preset, "--discovery", backend, "--out", path,
+           "--ingress"]
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     try:
         p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=root)
-        if p.returncode != 0:
-            return None, f"probe exited {p.returncode}: {(p.stderr or p.stdout).strip()[-400:]}"
-        with open(path) as f:
-            return Topology.from_json(f.read()), "ok"
+        err = f"probe exited {p.returncode}: {(p.stderr or p.stdout).strip()[-400:]}"
+        text = open(path).read() if os.path.getsize(path) else ""
+        if not text:
+            return None, err
+        # the pairwise matrix is on disk before the ingress stage runs: keep it if only that failed
+        return Topology.from_json(text), ("ok" if p.returncode == 0 else "pairwise only; ingress stage failed: " + err)
     except subprocess.TimeoutExpired:
         return None, f"probe timed out after {timeout:.0f}s"
     except (OSError, ValueError, KeyError) as e:
@@ -121,6 +124,14 @@ def probe_summary(topo, subset: Sequence[int]) -> Dict[str, object]:
         sub = [float(bw[i, j]) for i in subset for j in subset if i != j and np.isfinite(bw[i, j])]
         if sub:
             out["subset_link_read_gbps"] = {"min": round(min(sub), 1), "max": round(max(sub), 1)}
+    ing = (topo.probe or {}).get("ingress_all_gbps")
+    if ing:
+        out["ingress_all_gbps"] = ing
+    from ..ops.probe import ingress_bound
+
+    bound = ingress_bound(topo, subset)
+    if bound is not None:
+        out["subset_ingress_bound_gbps"] = round(bound, 1)
     return out
 
 

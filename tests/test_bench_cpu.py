@@ -88,3 +88,22 @@ def test_sweep_sizes():
     assert full[0] == 8 and full[-1] == 16 << 30 and full[-2] == 8 << 30
     assert bench.sweep_sizes("auto", cpu=True)[-1] == 1 << 20
     assert bench.sweep_sizes("1K:4K:2") == [1024, 2048, 4096]
+
+
+def test_ingress_bound():
+    import numpy as np
+
+    sys.path.insert(0, REPO)
+    from gpu_topology_on_k8s_amd.ops.probe import ingress_bound
+    from gpu_topology_on_k8s_amd.topology.discovery import fake_topology
+
+    topo = fake_topology(4)
+    assert ingress_bound(topo, [0, 1]) is None  # nothing measured
+    bw = np.full((4, 4), 60.0)
+    np.fill_diagonal(bw, np.nan)
+    topo.set_measured_bw(bw, {"method": "p2p_read_lds"})
+    assert ingress_bound(topo, [0]) is None
+    assert ingress_bound(topo, [0, 1]) == 60.0
+    assert ingress_bound(topo, [0, 1, 2, 3]) == 180.0  # 3 links per member
+    topo.probe["ingress_all_gbps"] = [150.0, 170.0, None, 175.0]  # shared fabric caps member 0
+    assert ingress_bound(topo, [0, 1, 2, 3]) == 150.0

@@ -52,6 +52,23 @@ def test_copy_odd_size_tail(probe_mod):
     assert r["ok"], r
 
 
+def test_gather_kernel_segments(probe_mod):
+    """K5 gather: three source buffers streamed by one launch land in their own dst segments (the
+    sources are local here; on a node they are the peers, same kernel); odd size exercises tails."""
+    r = probe_mod.gather_bw(0, [0, 0, 0], (16 << 20) + 4112, 2, 1)
+    assert r["ok"] and r["gbps"] > 100 and r["bytes_per_src"] == (16 << 20) + 4112
+
+
+def test_probe_cli_ingress_single_gpu(tmp_path):
+    out = tmp_path / "topo.json"
+    p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd", "probe", "--preset", "quick", "--ingress", "--out", str(out)],
+                       capture_output=True, text=True, timeout=300, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads(out.read_text())
+    assert d["probe"]["ingress_all_gbps"][0] is None  # one GPU: no peers to gather from
+    assert d["hbm_gbps"][0] > 1000
+
+
 def test_discover_real_node():
     from gpu_topology_on_k8s_amd.topology.discovery import discover
 
