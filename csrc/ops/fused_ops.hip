@@ -606,6 +606,10 @@ std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, co
                                  const at::Tensor& out, const at::Tensor& lse, double scale);
 }  // namespace gtk_attn
 
+namespace gtk_xpose {  // csrc/ops/transpose.hip
+at::Tensor transpose_bf16(const at::Tensor& x);
+}  // namespace gtk_xpose
+
 PYBIND11_MODULE(_fused, m) {
   m.def("attn_fwd", &gtk_attn::attn_fwd, "causal GQA flash attention forward (bf16, D=128): -> (o [B,S,H,D], lse2 [B,H,S])");
   m.def("attn_fwd_v1", &gtk_attn::attn_fwd_v1, "v1 forward (single-buffered LDS, two barriers per tile; A/B reference)");
@@ -625,4 +629,5 @@ PYBIND11_MODULE(_fused, m) {
   m.def("xent_bwd_inplace", &xent_bwd_inplace);
   m.def("adamw_step", &adamw_step);
   m.def("sq_norm", &sq_norm);
+  m.def("transpose_bf16", &gtk_xpose::transpose_bf16, "contiguous [R, C] bf16 -> [C, R] (R, C multiples of 64)");
 }

@@ -11,6 +11,10 @@ MI355X-first layout:
     the whole buffer (fp32 master + moments: 14 B/param read + 14 B/param written per step);
   * fused QKV and gate|up projections -> hipBLASLt GEMMs; everything between GEMMs is a fused HIP
     kernel (RMSNorm, RoPE + head split, SwiGLU, cross-entropy with in-place dlogits);
+  * backward GEMMs in the forward GEMM's "NT" layout (``gemm_layout="nt"``): dgrad as
+    ``dy (W^T)^T`` and wgrad as ``(dy^T)(x^T)^T``, the operands transposed by the LDS-tiled HIP
+    kernel (``ops.fused.transpose``) — hipBLASLt runs NT 10-40 % faster than the NN / TN layouts
+    autograd would hand it (bench/gemm_layout_bench.py);
   * Llama-3-8B = 8.03 B params: 16 GB bf16 weights + 16 GB bf16 grads + 96 GB fp32 master/m/v =
     128 GB, leaving ~160 GB of the 288 GB HBM for activations, so DP alone suffices (no TP/PP/SP).
 """
@@ -137,14 +141,21 @@ class FlatParams:
         hooks.append(fn)
         return _ReadyHandle(hooks, fn)
 
-    def write_grad(self, name: str, dy: torch.Tensor, x: torch.Tensor) -> None:
-        """Weight gradient of ``y = x W^T`` into the flat buffer: ``W.grad (+)= dy^T x``."""
+    def write_grad(self, name: str, dy: torch.Tensor, x: torch.Tensor, nt: bool = False) -> None:
+        """Weight gradient of ``y = x W^T`` into the flat buffer: ``W.grad (+)= dy^T x``.
+
+        ``nt``: compute it as ``(dy^T)(x^T)^T`` from transposed copies, the GEMM layout hipBLASLt runs
+        fastest (both operands contiguous along the token dimension being reduced)."""
         view = self.params[name].grad
+        if nt:
+            a, b = fused.transpose(dy), fused.transpose(x).t()
+        else:
+            a, b = dy.t(), x
         if self.direct[name]:
-            torch.mm(dy.t(), x, out=view)
+            torch.mm(a, b, out=view)
             self.direct[name] = False
         else:
-            view.addmm_(dy.t(), x)
+            view.addmm_(a, b)
         for fn in list(self._ready.get(name, ())):
             fn(self.params[name])
 
@@ -181,25 +192,31 @@ class _FlatLinear(torch.autograd.Function):
     """``y = x W^T`` whose weight gradient is written in place into the flat buffer."""
 
     @staticmethod
-    def forward(ctx, x, w, flat, name):
+    def forward(ctx, x, w, flat, name, nt):
         ctx.save_for_backward(x, w)
-        ctx.flat, ctx.name = flat, name
+        ctx.flat, ctx.name, ctx.nt = flat, name, nt
         return F.linear(x, w)
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        dx = dy.mm(w) if ctx.needs_input_grad[0] else None
-        ctx.flat.write_grad(ctx.name, dy, x)
-        return dx, None, None, None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = F.linear(dy, fused.transpose(w)) if ctx.nt else dy.mm(w)  # NT: dy (W^T)^T
+        ctx.flat.write_grad(ctx.name, dy, x, nt=ctx.nt)
+        return dx, None, None, None, None
 
 
 class Llama(torch.nn.Module):
-    def __init__(self, cfg: LlamaConfig, device="cuda", seed: int = 0, checkpoint: bool = False, attn: str = "hip"):
+    def __init__(self, cfg: LlamaConfig, device="cuda", seed: int = 0, checkpoint: bool = False, attn: str = "hip",
+                 gemm_layout: str = "nt"):
         super().__init__()
+        if gemm_layout not in ("nt", "native"):
+            raise ValueError("gemm_layout must be 'nt' or 'native'")
         self.cfg = cfg
         self.checkpoint = checkpoint
         self.attn = attn
+        self.gemm_layout = gemm_layout
         self.flat = FlatParams(cfg.param_shapes(), device)
         for n, p in self.flat.params.items():
             self.register_parameter(n.replace(".", "_"), p)
@@ -231,7 +248,8 @@ class Llama(torch.nn.Module):
         return self.flat.params[name]
 
     def _linear(self, x: torch.Tensor, name: str) -> torch.Tensor:
-        return _FlatLinear.apply(x, self.flat.params[name].detach(), self.flat, name)
+        nt = self.gemm_layout == "nt"
+        return _FlatLinear.apply(x, self.flat.params[name].detach(), self.flat, name, nt)
 
     # ---------------------------------------------------------------- blocks
     def _attention(self, q, k, v):

@@ -14,12 +14,21 @@ from .._native import load
 
 __all__ = [
     "rmsnorm", "rmsnorm_ref", "rope_tables", "rope_split", "rope_split_ref", "swiglu", "swiglu_ref", "cross_entropy",
-    "cross_entropy_ref", "hip", "attention", "attention_ref", "flash_attention_supported",
+    "cross_entropy_ref", "hip", "attention", "attention_ref", "flash_attention_supported", "transpose",
 ]
 
 
 def hip():
     return load("_fused")
+
+
+# ------------------------------------------------------------------------------------ transpose
+def transpose(x: torch.Tensor) -> torch.Tensor:
+    """Contiguous ``x.t()``: the LDS-tiled HIP kernel for bf16 GPU matrices whose dims are multiples of
+    64 (every Llama-3 dim), torch's copy otherwise.  Puts backward-GEMM operands into the NT layout."""
+    if x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and x.size(0) % 64 == 0 and x.size(1) % 64 == 0:
+        return hip().transpose_bf16(x.contiguous())
+    return x.t().contiguous()
 
 
 # ------------------------------------------------------------------------------------ RMSNorm

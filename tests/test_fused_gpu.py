@@ -129,6 +129,35 @@ def test_adamw_and_sqnorm(hip):
     assert math.isclose(sq.item(), g.float().pow(2).sum().item(), rel_tol=1e-4)
 
 
+@pytest.mark.parametrize("R,C", [(64, 64), (128, 4096), (4096, 192), (16384, 6144), (640, 128256)])
+def test_transpose_kernel_exact(hip, R, C):
+    x = torch.randn(R, C, device="cuda", dtype=torch.bfloat16)
+    y = hip.transpose_bf16(x)
+    assert y.shape == (C, R) and torch.equal(y, x.t().contiguous())
+
+
+def test_transpose_wrapper_fallback_shapes():
+    from gpu_topology_on_k8s_amd.ops import fused
+
+    x = torch.randn(100, 72, device="cuda", dtype=torch.bfloat16)  # not multiples of 64: torch copy
+    assert torch.equal(fused.transpose(x), x.t().contiguous())
+
+
+def test_llama_nt_layout_matches_native_gpu():
+    """NT backward GEMMs (HIP transposes + hipBLASLt NT) vs the native layout on the GPU."""
+    from gpu_topology_on_k8s_amd.models import Llama, LlamaConfig
+
+    cfg = LlamaConfig.tiny()
+    tok = torch.randint(0, cfg.vocab, (2, 128), device="cuda")
+    grads = {}
+    for layout in ("native", "nt"):
+        m = Llama(cfg, device="cuda", seed=3, gemm_layout=layout)
+        m.flat.zero_grad()
+        m(tok, torch.roll(tok, -1, 1)).backward()
+        grads[layout] = m.flat.grad.float().clone()
+    assert _rel(grads["nt"], grads["native"]) < 1e-2
+
+
 def test_llama_model_gpu_matches_cpu_reference():
     """Full tiny model: HIP kernels + hipBLASLt on GPU vs the PyTorch reference path on CPU."""
     from gpu_topology_on_k8s_amd.models import Llama, LlamaConfig

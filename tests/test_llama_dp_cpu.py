@@ -83,6 +83,21 @@ def test_direct_weight_grads_match_autograd_and_accumulate():
     assert torch.allclose(m.flat.grad.float(), g1, rtol=1e-2, atol=1e-5)
 
 
+def test_nt_gemm_layout_matches_native():
+    """Backward GEMMs in NT layout (transposed operands) give the native layout's gradients."""
+    cfg = LlamaConfig.tiny()
+    tok = torch.randint(0, cfg.vocab, (2, 16), generator=torch.Generator().manual_seed(7))
+    grads = {}
+    for layout in ("native", "nt"):
+        m = Llama(cfg, device="cpu", seed=3, gemm_layout=layout)
+        m.flat.zero_grad()
+        m(tok, torch.roll(tok, -1, 1)).backward()
+        grads[layout] = m.flat.grad.float().clone()
+    assert torch.allclose(grads["nt"], grads["native"], rtol=1e-2, atol=1e-5)
+    with pytest.raises(ValueError):
+        Llama(cfg, device="cpu", gemm_layout="tn")
+
+
 def test_reference_ops_match_definitions():
     x = torch.randn(4, 64, dtype=torch.bfloat16)
     w = torch.rand(64, dtype=torch.bfloat16) + 0.5
