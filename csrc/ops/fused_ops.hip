@@ -379,6 +379,56 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const u16* __restrict__
   }
 }
 
+// Backward with a second, transposed copy of the gradient: dguT [2F, T] is the A operand of the
+// w13 weight-gradient GEMM in NT layout (dW13 = dguT . hT^T), written here from the LDS tile instead
+// of by a separate transpose pass (saves re-reading the 2*T*F gradient).  One 256-thread block =
+// 64 tokens x 64 features: each thread computes 2 x 8 features of the gate AND up halves, stores
+// them row-major, stages both tiles in LDS (XOR-swizzled exactly like csrc/ops/transpose.hip) and
+// writes 2 x 8 tokens of a transposed row per tile.  T and F must be multiples of 64.
+__global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const u16* __restrict__ dh, const u16* __restrict__ gu,
+                                                           u16* __restrict__ dgu, u16* __restrict__ dguT, int T, int F) {
+  __shared__ u16x8 tile[2][64][8];  // [gate | up][token][feature vector]
+  const int t = threadIdx.x;
+  const size_t r0 = (size_t)blockIdx.y * 64, c0 = (size_t)blockIdx.x * 64;
+  const size_t F2 = 2 * (size_t)F;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (t >> 3) + 32 * i, v = t & 7;
+    const size_t row = r0 + r;
+    const u16x8 g = *reinterpret_cast<const u16x8*>(gu + row * F2 + c0 + 8 * v);
+    const u16x8 u = *reinterpret_cast<const u16x8*>(gu + row * F2 + F + c0 + 8 * v);
+    const u16x8 d = *reinterpret_cast<const u16x8*>(dh + row * F + c0 + 8 * v);
+    u16x8 og, ou;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gf = bf2f(g[j]), uf = bf2f(u[j]), df = bf2f(d[j]);
+      const float sg = 1.f / (1.f + __expf(-gf));
+      const float silu = gf * sg;  // same expression order as swiglu_bwd_kernel: identical rounding
+      ou[j] = f2bf(df * silu);
+      og[j] = f2bf(df * uf * sg * (1.f + gf * (1.f - sg)));
+    }
+    *reinterpret_cast<u16x8*>(dgu + row * F2 + c0 + 8 * v) = og;
+    *reinterpret_cast<u16x8*>(dgu + row * F2 + F + c0 + 8 * v) = ou;
+    tile[0][r][v ^ ((r >> 3) & 7)] = og;
+    tile[1][r][v ^ ((r >> 3) & 7)] = ou;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const u16* lds = reinterpret_cast<const u16*>(&tile[h][0][0]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = t + 256 * i;
+      const int c = idx >> 3, p = idx & 7;
+      const int pv = (c >> 3) ^ p;
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = lds[(8 * p + j) * 64 + pv * 8 + (c & 7)];
+      *reinterpret_cast<u16x8*>(dguT + ((size_t)h * F + c0 + c) * T + r0 + 8 * p) = o;
+    }
+  }
+}
+
 at::Tensor swiglu_fwd(const at::Tensor& gu) {
   CHECK_BF16(gu);
   const int64_t F2 = gu.size(-1);
@@ -401,6 +451,20 @@ at::Tensor swiglu_bwd(const at::Tensor& dh, const at::Tensor& gu) {
   auto dgu = at::empty_like(gu);
   if (T) hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(T * (F / 8))), dim3(256), 0, cur_stream(), bp(dh), bp(gu), bpm(dgu), T, F);
   return dgu;
+}
+
+std::vector<at::Tensor> swiglu_bwd_t(const at::Tensor& dh, const at::Tensor& gu) {
+  CHECK_BF16(dh);
+  CHECK_BF16(gu);
+  TORCH_CHECK(gu.dim() == 2, "swiglu_bwd_t: gu must be [T, 2F]");
+  const int64_t T = gu.size(0), F = gu.size(1) / 2;
+  TORCH_CHECK(dh.numel() == T * F, "swiglu_bwd_t: shape mismatch");
+  TORCH_CHECK(T % 64 == 0 && F % 64 == 0 && T / 64 <= 65535, "swiglu_bwd_t: T and F must be multiples of 64");
+  auto dgu = at::empty_like(gu);
+  auto dguT = at::empty({2 * F, T}, gu.options());
+  if (T && F) hipLaunchKernelGGL(swiglu_bwd_t_kernel, dim3((unsigned)(F / 64), (unsigned)(T / 64)), dim3(256), 0, cur_stream(), bp(dh),
+                           bp(gu), bpm(dgu), bpm(dguT), (int)T, (int)F);
+  return {dgu, dguT};
 }
 
 // =============================================================================== cross-entropy
@@ -625,6 +689,7 @@ PYBIND11_MODULE(_fused, m) {
   m.def("rope_split_bwd", &rope_split_bwd);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("swiglu_bwd_t", &swiglu_bwd_t, "swiglu backward -> (dgu [T, 2F], dgu^T [2F, T]); T, F multiples of 64");
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd_inplace", &xent_bwd_inplace);
   m.def("adamw_step", &adamw_step);

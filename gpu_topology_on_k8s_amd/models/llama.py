@@ -141,14 +141,16 @@ class FlatParams:
         hooks.append(fn)
         return _ReadyHandle(hooks, fn)
 
-    def write_grad(self, name: str, dy: torch.Tensor, x: torch.Tensor, nt: bool = False) -> None:
+    def write_grad(self, name: str, dy: torch.Tensor, x: torch.Tensor, nt: bool = False,
+                   dy_t: Optional[torch.Tensor] = None) -> None:
         """Weight gradient of ``y = x W^T`` into the flat buffer: ``W.grad (+)= dy^T x``.
 
         ``nt``: compute it as ``(dy^T)(x^T)^T`` from transposed copies, the GEMM layout hipBLASLt runs
-        fastest (both operands contiguous along the token dimension being reduced)."""
+        fastest (both operands contiguous along the token dimension being reduced); ``dy_t`` is a
+        transposed copy the producer of ``dy`` already wrote (SwiGLU backward)."""
         view = self.params[name].grad
         if nt:
-            a, b = fused.transpose(dy), fused.transpose(x).t()
+            a, b = (dy_t if dy_t is not None else fused.transpose(dy)), fused.transpose(x).t()
         else:
             a, b = dy.t(), x
         if self.direct[name]:
@@ -204,6 +206,33 @@ class _FlatLinear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = F.linear(dy, fused.transpose(w)) if ctx.nt else dy.mm(w)  # NT: dy (W^T)^T
         ctx.flat.write_grad(ctx.name, dy, x, nt=ctx.nt)
+        return dx, None, None, None, None
+
+
+class _FlatLinearSwiGLU(torch.autograd.Function):
+    """``silu(g) * u`` of ``[g | u] = x W13^T``: the gate|up projection and SwiGLU as one node, so the
+    backward gets d[g | u] AND its transpose from one HIP kernel (``fused.swiglu_bwd_t``) and feeds
+    the transpose straight to the NT weight-gradient GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, w, flat, name, nt):
+        gu = F.linear(x, w)
+        ctx.save_for_backward(x, w, gu)
+        ctx.flat, ctx.name, ctx.nt = flat, name, nt
+        return fused.hip().swiglu_fwd(gu) if gu.is_cuda else fused.swiglu_ref(gu)
+
+    @staticmethod
+    def backward(ctx, da):
+        x, w, gu = ctx.saved_tensors
+        if ctx.nt:
+            dgu, dgu_t = fused.swiglu_bwd_t(da, gu)
+        else:
+            dgu = fused.hip().swiglu_bwd(da.contiguous(), gu) if gu.is_cuda else fused.swiglu_bwd_ref(da, gu)
+            dgu_t = None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = F.linear(dgu, fused.transpose(w)) if ctx.nt else dgu.mm(w)
+        ctx.flat.write_grad(ctx.name, dgu, x, nt=ctx.nt, dy_t=dgu_t)
         return dx, None, None, None, None
 
 
@@ -275,7 +304,8 @@ class Llama(torch.nn.Module):
         o = self._attention(q, k, v).reshape(B * S, H * Dh)  # [B, S, H, Dh] -> [B*S, H*Dh]
         x = x + self._linear(o, f"l{i}.wo")
         h = fused.rmsnorm(x, self.P(f"l{i}.ffn_norm"), cfg.norm_eps)
-        x = x + self._linear(fused.swiglu(self._linear(h, f"l{i}.w13")), f"l{i}.w2")
+        a = _FlatLinearSwiGLU.apply(h, self.flat.params[f"l{i}.w13"].detach(), self.flat, f"l{i}.w13", self.gemm_layout == "nt")
+        x = x + self._linear(a, f"l{i}.w2")
         return x
 
     def forward(self, tokens: torch.Tensor, labels: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -14,7 +14,8 @@ from .._native import load
 
 __all__ = [
     "rmsnorm", "rmsnorm_ref", "rope_tables", "rope_split", "rope_split_ref", "swiglu", "swiglu_ref", "cross_entropy",
-    "cross_entropy_ref", "hip", "attention", "attention_ref", "flash_attention_supported", "transpose",
+    "cross_entropy_ref", "hip", "attention", "attention_ref", "flash_attention_supported", "transpose", "swiglu_bwd_ref",
+    "swiglu_bwd_t",
 ]
 
 
@@ -118,6 +119,24 @@ def rope_split(qkv, cos, sin, B, S, H, Hkv, Dh, pos_offset: int = 0):
 def swiglu_ref(gu: torch.Tensor) -> torch.Tensor:
     g, u = gu.float().chunk(2, dim=-1)
     return (torch.nn.functional.silu(g) * u).to(gu.dtype)
+
+
+def swiglu_bwd_ref(dh: torch.Tensor, gu: torch.Tensor) -> torch.Tensor:
+    """d[gate | up] of ``silu(g) * u`` (fp32 math, ``gu``'s dtype out)."""
+    g, u = gu.float().chunk(2, dim=-1)
+    d = dh.float()
+    sg = torch.sigmoid(g)
+    return torch.cat([d * u * sg * (1 + g * (1 - sg)), d * g * sg], dim=-1).to(gu.dtype)
+
+
+def swiglu_bwd_t(dh: torch.Tensor, gu: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """SwiGLU backward returning ``(dgu [T, 2F], dgu^T [2F, T])``: the HIP kernel writes the transposed
+    copy from its LDS tile (T, F multiples of 64); elsewhere the reference plus a transpose."""
+    if gu.is_cuda and gu.dim() == 2 and gu.size(0) % 64 == 0 and (gu.size(1) // 2) % 64 == 0:
+        dgu, dgu_t = hip().swiglu_bwd_t(dh.contiguous(), gu.contiguous())
+        return dgu, dgu_t
+    dgu = hip().swiglu_bwd(dh.contiguous(), gu.contiguous()) if gu.is_cuda else swiglu_bwd_ref(dh, gu)
+    return dgu, transpose(dgu)
 
 
 class _SwiGLU(torch.autograd.Function):

@@ -15,6 +15,12 @@ def hip():
     return load_hip()  # raises (fails loudly) if the extension is missing
 
 
+def fused_swiglu_bwd_ref(dh, gu):
+    from gpu_topology_on_k8s_amd.ops.fused import swiglu_bwd_ref
+
+    return swiglu_bwd_ref(dh.cpu(), gu.cpu()).cuda()
+
+
 def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
@@ -134,6 +140,17 @@ def test_transpose_kernel_exact(hip, R, C):
     x = torch.randn(R, C, device="cuda", dtype=torch.bfloat16)
     y = hip.transpose_bf16(x)
     assert y.shape == (C, R) and torch.equal(y, x.t().contiguous())
+
+
+@pytest.mark.parametrize("T,F", [(64, 64), (256, 14336), (4096, 192)])
+def test_swiglu_bwd_t_matches_bwd_and_transpose(hip, T, F):
+    gu = torch.randn(T, 2 * F, device="cuda", dtype=torch.bfloat16)
+    dh = torch.randn(T, F, device="cuda", dtype=torch.bfloat16)
+    dgu, dgu_t = hip.swiglu_bwd_t(dh, gu)
+    ref = hip.swiglu_bwd(dh, gu)  # same math; allow a rare 1-ulp difference from FMA contraction
+    assert (dgu.float() - ref.float()).abs().max().item() <= 1e-2 * ref.float().abs().max().item()
+    assert _rel(dgu, fused_swiglu_bwd_ref(dh, gu)) < 1e-2
+    assert dgu_t.shape == (2 * F, T) and torch.equal(dgu_t, dgu.t().contiguous())
 
 
 def test_transpose_wrapper_fallback_shapes():

@@ -98,6 +98,15 @@ def test_nt_gemm_layout_matches_native():
         Llama(cfg, device="cpu", gemm_layout="tn")
 
 
+def test_swiglu_bwd_ref_matches_autograd():
+    gu = torch.randn(8, 64, dtype=torch.float64, requires_grad=True)
+    dh = torch.randn(8, 32, dtype=torch.float64)
+    fused.swiglu_ref(gu).backward(dh)
+    assert torch.allclose(fused.swiglu_bwd_ref(dh, gu.detach()).double(), gu.grad, rtol=1e-5, atol=1e-6)
+    dgu, dgu_t = fused.swiglu_bwd_t(dh, gu.detach())
+    assert torch.equal(dgu_t, dgu.t().contiguous())
+
+
 def test_reference_ops_match_definitions():
     x = torch.randn(4, 64, dtype=torch.bfloat16)
     w = torch.rand(64, dtype=torch.bfloat16) + 0.5
