@@ -54,6 +54,9 @@ def parse(argv=None):
                          "process of rank 0; 'auto' = quick on GPUs, off for --backend cpu; a failed probe falls back "
                          "to the discovered link classes")
     ap.add_argument("--discovery", default="auto", choices=["auto", "amdsmi", "sysfs", "fake"])
+    ap.add_argument("--via", default="k8s", choices=["k8s", "direct"],
+                    help="k8s = place the k-GPU pod through device plugin (gRPC) + extender (HTTP) + kubelet Allocate "
+                         "in process; direct = call the placement core")
     ap.add_argument("--ctas", default="auto",
                     help="RCCL channel (CTA) bounds of the measured communicator: 'auto' = short tuning pass over "
                          f"{TUNE_CANDIDATES} at k >= 2 (untimed, before warmup), 'tune' = that pass at any k, "
@@ -212,7 +215,8 @@ def main(argv=None) -> int:
                 print(f"bench: link probe unavailable ({msg}); placing on discovered link classes", file=sys.stderr)
             elif msg != "ok":
                 print(f"bench: link probe: {msg}", file=sys.stderr)
-        choice = choose_subset(env.world, backend=args.discovery, visible=env.world if cpu else None, topology=topo)
+        choice = choose_subset(env.world, backend=args.discovery, visible=env.world if cpu else None, topology=topo,
+                               via_k8s=args.via == "k8s")
         env.store.set("gtk/subset", choice.to_json())
     choice = SubsetChoice.from_json(env.store.get("gtk/subset").decode())
     device = choice.devices[env.rank]
@@ -319,6 +323,7 @@ def main(argv=None) -> int:
             },
             "ctas_tuning": tuning,
             "link_probe": choice.extra.get("probe"),
+            "k8s_placement": choice.extra.get("k8s"),
             "size_sweep": sweep,
             "value_kind": "busbw" if env.world > 1 else "algbw (busbw = 0 at k=1)",
             "busbw_vs_probe_bound": round(busbw / bound, 4) if bound else None,

@@ -135,8 +135,29 @@ def probe_summary(topo, subset: Sequence[int]) -> Dict[str, object]:
     return out
 
 
+def schedule_via_k8s(topo, k: int, node: str = "") -> Dict[str, object]:
+    """Place a k-GPU pod through the whole Kubernetes path, in process (``sim.SimCluster``, CPU only):
+    the device plugin publishes ``topo`` on a fake apiserver and registers with a fake kubelet over
+    gRPC; the mini scheduler calls the extender's ``/filter``, ``/sort`` and ``/bind`` over HTTP;
+    the kubelet admits the pod through ``GetPreferredAllocation`` + ``Allocate``.  Returns the
+    allocated devices, the pod's GROUP annotation and the flow's latencies."""
+    from ..sim import SimCluster
+
+    name = node or topo.node_name or "node0"
+    with SimCluster({name: topo}) as c:
+        c.submit("allreduce-bench", k)
+        r = c.schedule_pending()[0]
+        if r.error or not r.allocated:
+            raise RuntimeError(f"k8s flow did not place the pod: {r.error or 'no devices allocated'}")
+        pa = c.assignment("allreduce-bench")
+        return {"devices": [int(i) for i in r.allocated], "node": r.node, "extender_score": r.score,
+                "group_annotation": ",".join(str(i) for i in pa.group) if pa else None,
+                "assigned": bool(pa.assigned) if pa else None,
+                "sched_ms": round(r.sched_ms, 3), "admit_ms": round(r.admit_ms, 3)}
+
+
 def choose_subset(k: int, probe: Optional[str] = None, backend: str = "auto", visible: Optional[int] = None,
-                  topology=None) -> SubsetChoice:
+                  topology=None, via_k8s: bool = False) -> SubsetChoice:
     """Rank-0 side: discover the node, optionally probe links, run the placement core.
 
     ``visible`` overrides the HIP device count (CPU/gloo runs model a mesh of that many devices);
@@ -167,17 +188,33 @@ def choose_subset(k: int, probe: Optional[str] = None, backend: str = "auto", vi
     pl = select(topo, k, policy=PlacementPolicy())
     ms = (time.perf_counter() - t1) * 1e3
     w = worst(topo, k) if k < topo.n else None
+    devices, score, objective = list(pl.ids), pl.score, pl.objective
+    k8s: Optional[Dict[str, object]] = None
+    if via_k8s:
+        try:
+            k8s = schedule_via_k8s(topo, k)
+        except Exception as e:  # noqa: BLE001 - the direct placement stands in, and says so
+            log.warning("k8s flow failed (%s); using the placement core directly", e)
+            k8s = {"error": str(e)}
+        else:
+            if sorted(k8s["devices"]) != sorted(devices):
+                from ..placement.core import Problem, evaluate, score_from_objective
+
+                objective, _ = evaluate(Problem.from_topology(topo, []), k8s["devices"], PlacementPolicy())
+                score = score_from_objective(objective)
+            devices = list(k8s["devices"])
     return SubsetChoice(
-        devices=list(pl.ids),
-        score=round(pl.score, 4),
-        objective=round(pl.objective, 6),
+        devices=devices,
+        score=round(score, 4),
+        objective=round(objective, 6),
         source=source,
         worst=list(w.ids) if w else None,
         worst_score=round(w.score, 4) if w else None,
         placement_ms=round(ms, 4),
         probed=probed,
         extra={"discovery_ms": round((t1 - t0) * 1e3, 2), "node_devices": topo.n,
-               **({"probe": probe_summary(topo, pl.ids)} if probed else {})},
+               **({"probe": probe_summary(topo, devices)} if probed else {}),
+               **({"k8s": k8s} if k8s is not None else {})},
     )
 
 

@@ -32,12 +32,16 @@ def test_bench_two_ranks_gloo():
     assert out["value"] > 0 and abs(out["busbw_gbps"] - out["algbw_gbps"]) < 1e-3 * out["algbw_gbps"] + 1e-6  # 2(k-1)/k = 1
     assert out["config"]["parallelism"] == "dp2"
     assert out["config"]["message_bytes_per_gpu"] == 1 << 20
+    k8s = out["k8s_placement"]  # placed through device plugin + extender + kubelet Allocate
+    assert k8s["devices"] == out["config"]["subset"] and k8s["assigned"] is True
+    assert k8s["group_annotation"] == ",".join(str(i) for i in out["config"]["subset"])
     sw = out["size_sweep"]
     assert sw["all_exact"] and [r["bytes"] for r in sw["rows"]][:2] == [8, 64] and sw["peak"]["busbw_gbps"] > 0
 
 
 def test_bench_single_rank_cpu():
-    out = _bench("--backend", "cpu", "--steps", "2", "--warmup", "1", "--size-mb", "1")
+    out = _bench("--backend", "cpu", "--steps", "2", "--warmup", "1", "--size-mb", "1", "--via", "direct")
+    assert out["k8s_placement"] is None
     assert out["n_gpus"] == 1 and out["busbw_gbps"] == 0.0 and out["value"] == out["algbw_gbps"]
 
 
