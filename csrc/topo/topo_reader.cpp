@@ -36,7 +36,10 @@ struct Dev {
   std::string uuid, bdf, partition = "SPX", memory_partition = "NPS1", model, gfx;
   int numa = 0, render_minor = -1, card = -1, kfd_node = -1, hip_id = -1, physical = -1;
   uint64_t vram = 0;
-  int xgmi_links_up = -1;
+  int xgmi_links_up = -1, xgmi_links_total = -1;
+  // RAS signals for the device plugin's health monitor (-1 = not readable: unsupported / no root)
+  int64_t ecc_correctable = -1, ecc_uncorrectable = -1, ecc_deferred = -1;
+  int bad_pages = -1, bad_page_threshold = -1;
   int cus = 0;
   bool healthy = true;
   uint64_t location = 0;  // domain<<16 | bdf: physical-package key
@@ -105,6 +108,12 @@ py::dict to_py(const Result& r) {
     g["vram_bytes"] = d.vram;
     g["healthy"] = d.healthy;
     g["xgmi_links_up"] = d.xgmi_links_up;
+    g["xgmi_links_total"] = d.xgmi_links_total;
+    g["ecc_correctable"] = d.ecc_correctable;
+    g["ecc_uncorrectable"] = d.ecc_uncorrectable;
+    g["ecc_deferred"] = d.ecc_deferred;
+    g["bad_pages"] = d.bad_pages;
+    g["bad_page_threshold"] = d.bad_page_threshold;
     g["cus"] = d.cus;
     gpus.append(g);
   }
@@ -151,6 +160,9 @@ struct AmdSmi {
   decltype(&amdsmi_get_gpu_asic_info) get_asic = nullptr;
   decltype(&amdsmi_get_gpu_memory_total) get_mem_total = nullptr;
   decltype(&amdsmi_get_gpu_xgmi_link_status) get_xgmi_status = nullptr;
+  decltype(&amdsmi_get_gpu_total_ecc_count) get_ecc_total = nullptr;
+  decltype(&amdsmi_get_gpu_bad_page_info) get_bad_pages = nullptr;
+  decltype(&amdsmi_get_gpu_bad_page_threshold) get_bad_page_threshold = nullptr;
 
   template <class F>
   void bind(F& f, const char* sym, bool required) {
@@ -179,6 +191,9 @@ struct AmdSmi {
     bind(get_asic, "amdsmi_get_gpu_asic_info", false);
     bind(get_mem_total, "amdsmi_get_gpu_memory_total", false);
     bind(get_xgmi_status, "amdsmi_get_gpu_xgmi_link_status", false);
+    bind(get_ecc_total, "amdsmi_get_gpu_total_ecc_count", false);
+    bind(get_bad_pages, "amdsmi_get_gpu_bad_page_info", false);
+    bind(get_bad_page_threshold, "amdsmi_get_gpu_bad_page_threshold", false);
   }
   ~AmdSmi() {
     if (h) dlclose(h);
@@ -271,7 +286,24 @@ Result discover_amdsmi_impl(const std::string& lib) {
         for (uint32_t l = 0; l < ls.total_links && l < AMDSMI_MAX_NUM_XGMI_LINKS; ++l)
           up += ls.status[l] == AMDSMI_XGMI_LINK_UP;
         d.xgmi_links_up = up;
+        d.xgmi_links_total = (int)std::min<uint32_t>(ls.total_links, AMDSMI_MAX_NUM_XGMI_LINKS);
       }
+    }
+    if (s.get_ecc_total) {
+      amdsmi_error_count_t ec;
+      if (s.get_ecc_total(h, &ec) == AMDSMI_STATUS_SUCCESS) {
+        d.ecc_correctable = (int64_t)ec.correctable_count;
+        d.ecc_uncorrectable = (int64_t)ec.uncorrectable_count;
+        d.ecc_deferred = (int64_t)ec.deferred_count;
+      }
+    }
+    if (s.get_bad_pages) {
+      uint32_t np = 0;
+      if (s.get_bad_pages(h, &np, nullptr) == AMDSMI_STATUS_SUCCESS) d.bad_pages = (int)np;
+    }
+    if (s.get_bad_page_threshold) {
+      uint32_t th = 0;
+      if (s.get_bad_page_threshold(h, &th) == AMDSMI_STATUS_SUCCESS) d.bad_page_threshold = (int)th;
     }
   }
   // Order by HIP id when available (so index == HIP ordinal with no HIP_VISIBLE_DEVICES)
@@ -439,12 +471,36 @@ Result discover_sysfs_impl(const std::string& root, const std::string& drm_root)
     int up = 0;
     for (const auto& l : direct[nid]) up += (l.type == 11);
     d.xgmi_links_up = up;
+    d.xgmi_links_total = up;  // KFD lists only links that trained; amdsmi reports the down ones
     if (!drm_root.empty() && d.render_minor >= 0) {
       std::string dev = drm_root + "/renderD" + std::to_string(d.render_minor) + "/device/";
       std::string cp = read_first_line(dev + "current_compute_partition");
       std::string mp = read_first_line(dev + "current_memory_partition");
       if (!cp.empty()) d.partition = cp;
       if (!mp.empty()) d.memory_partition = mp;
+      // RAS: amdgpu's per-block ras/<block>_err_count files ("ue: N" / "ce: M"), summed, and the
+      // retired-page list ras/gpu_vram_bad_pages (one line per page)
+      const std::string ras = dev + "ras/";
+      for (const auto& f : list_dir(ras)) {
+        if (f.size() < 10 || f.compare(f.size() - 10, 10, "_err_count") != 0) continue;
+        std::ifstream in(ras + f);
+        std::string key;
+        uint64_t v = 0;
+        while (in >> key >> v) {
+          if (key == "ue:") d.ecc_uncorrectable = std::max<int64_t>(d.ecc_uncorrectable, 0) + (int64_t)v;
+          if (key == "ce:") d.ecc_correctable = std::max<int64_t>(d.ecc_correctable, 0) + (int64_t)v;
+        }
+      }
+      {
+        std::ifstream bp(ras + "gpu_vram_bad_pages");
+        if (bp) {
+          int n = 0;
+          std::string line;
+          while (std::getline(bp, line))
+            if (!line.empty()) ++n;
+          d.bad_pages = n;
+        }
+      }
       // the card minor: first cardN directory under the device's drm/
       for (const auto& c : list_dir(dev + "drm"))
         if (c.rfind("card", 0) == 0) {

@@ -18,6 +18,7 @@ import threading
 
 from ..k8s.annotations import Contract
 from ..topology.discovery import discover
+from .health import HealthMonitor
 from .plugin import DevicePluginServer, PluginConfig
 from .proto import DEVICE_PLUGIN_PATH
 
@@ -61,9 +62,7 @@ def main(argv=None) -> int:
         log.info("probe: %s", topo.probe)
     log.info("topology:\n%s", topo.render())
 
-    def health(t):
-        fresh = discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus)
-        return {g.index: bool(g.healthy) for g in fresh.gpus if g.index < t.n}
+    health = HealthMonitor(topo, lambda: discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus))
 
     cfg = PluginConfig(resource_name=a.resource_name, socket_dir=a.socket_dir, socket_name=a.socket_name, dev_root=a.dev_root,
                        node_name=a.node_name, contract=Contract(resource_name=a.resource_name, prefix=a.annotation_prefix),

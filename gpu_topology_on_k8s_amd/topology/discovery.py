@@ -45,6 +45,12 @@ def from_native(d: Dict[str, object], node_name: str = "", ref_gbps: float = DEF
                 vram_bytes=int(g.get("vram_bytes", 0)),
                 healthy=bool(g.get("healthy", True)),
                 xgmi_links_up=int(g.get("xgmi_links_up", -1)),
+                xgmi_links_total=int(g.get("xgmi_links_total", -1)),
+                ecc_correctable=int(g.get("ecc_correctable", -1)),
+                ecc_uncorrectable=int(g.get("ecc_uncorrectable", -1)),
+                ecc_deferred=int(g.get("ecc_deferred", -1)),
+                bad_pages=int(g.get("bad_pages", -1)),
+                bad_page_threshold=int(g.get("bad_page_threshold", -1)),
             )
         )
     lt = np.array(d["link_type"], dtype=np.int32)

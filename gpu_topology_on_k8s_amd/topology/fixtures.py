@@ -123,12 +123,15 @@ def write_fake_kfd_sysfs(
     xgmi: bool = True,
     missing_links: Sequence[tuple] = (),
     compute_partition: Optional[str] = None,
+    ras: Optional[Dict[int, Dict[str, object]]] = None,
 ) -> Dict[str, str]:
     """Write a KFD topology tree + DRM tree for an MI355X node under ``root``.
 
     Returns ``{"kfd": <topology root>, "drm": <drm root>}``.  KFD node ids: CPUs first
     (0..sockets-1) then one node per schedulable GPU/XCP, as the amdgpu driver enumerates them.
     ``missing_links`` drops direct xGMI io_links between GPU indices (a degraded node).
+    ``ras`` writes amdgpu RAS files for device index ``d``: ``{"umc": (ue, ce), "gfx": (ue, ce),
+    "bad_pages": n}`` -> ``ras/<block>_err_count`` and ``ras/gpu_vram_bad_pages``.
     """
     kfd = os.path.join(root, "kfd", "topology")
     drm = os.path.join(root, "drm")
@@ -183,6 +186,15 @@ def write_fake_kfd_sysfs(
             f.write(part + "\n")
         with open(os.path.join(dev, "current_memory_partition"), "w") as f:
             f.write("NPS1\n")
+        for key, val in ((ras or {}).get(d) or {}).items():
+            os.makedirs(os.path.join(dev, "ras"), exist_ok=True)
+            if key == "bad_pages":
+                with open(os.path.join(dev, "ras", "gpu_vram_bad_pages"), "w") as f:
+                    f.writelines(f"0x{0x1000 + i:08x} : 0x00001000 : R\n" for i in range(int(val)))
+            else:
+                ue, ce = val
+                with open(os.path.join(dev, "ras", f"{key}_err_count"), "w") as f:
+                    f.write(f"ue: {ue}\nce: {ce}\n")
     return {"kfd": kfd, "drm": drm}
 
 

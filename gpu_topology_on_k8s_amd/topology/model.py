@@ -191,6 +191,13 @@ class GPUInfo:
     healthy: bool = True
     xgmi_links_up: int = -1
     cpu_affinity: str = ""  # cpulist string, e.g. "0-63"
+    # RAS signals read by discovery (amdsmi / amdgpu sysfs); -1 = not readable on this node
+    xgmi_links_total: int = -1
+    ecc_correctable: int = -1
+    ecc_uncorrectable: int = -1
+    ecc_deferred: int = -1
+    bad_pages: int = -1
+    bad_page_threshold: int = -1
 
     def __post_init__(self) -> None:
         if self.physical < 0:

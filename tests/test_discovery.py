@@ -28,6 +28,17 @@ def test_sysfs_full_mesh(tmp_path):
 
 
 @needs_topo
+def test_sysfs_ras_counters(tmp_path):
+    """amdgpu ras/<block>_err_count files are summed per device; retired pages counted; absent = -1."""
+    p = fx.write_fake_kfd_sysfs(str(tmp_path), ras={1: {"umc": (2, 5), "gfx": (1, 0), "bad_pages": 3}})
+    t = from_native(load("_topo").discover_sysfs(p["kfd"], p["drm"]))
+    g1, g0 = t.gpus[1], t.gpus[0]
+    assert (g1.ecc_uncorrectable, g1.ecc_correctable, g1.bad_pages) == (3, 5, 3)
+    assert (g0.ecc_uncorrectable, g0.ecc_correctable, g0.bad_pages) == (-1, -1, -1)
+    assert g0.xgmi_links_total == g0.xgmi_links_up == 7
+
+
+@needs_topo
 def test_sysfs_missing_xgmi_link_falls_back_to_pcie(tmp_path):
     p = fx.write_fake_kfd_sysfs(str(tmp_path), missing_links=[(0, 5)])
     t = from_native(load("_topo").discover_sysfs(p["kfd"], p["drm"]))

@@ -80,6 +80,21 @@ def test_discover_real_node():
     print(json.dumps(t.to_dict()["gpus"][0]))
 
 
+def test_health_monitor_on_real_node():
+    """RAS signals come back as integers (-1 where the node does not expose them to this user) and
+    a freshly started monitor calls every device Healthy."""
+    from gpu_topology_on_k8s_amd.deviceplugin.health import HealthMonitor
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
+
+    t = discover("auto")
+    for g in t.gpus:
+        assert all(isinstance(v, int) for v in (g.ecc_uncorrectable, g.ecc_correctable, g.bad_pages, g.xgmi_links_total))
+    mon = HealthMonitor(t, lambda: discover("auto"))
+    assert all(mon(t).values()), mon.reasons
+    print({g.index: (g.ecc_uncorrectable, g.ecc_correctable, g.bad_pages, g.bad_page_threshold, g.xgmi_links_up,
+                     g.xgmi_links_total) for g in t.gpus})
+
+
 def test_sysfs_backend_on_real_node():
     from gpu_topology_on_k8s_amd.topology.discovery import discover
 

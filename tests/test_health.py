@@ -1,0 +1,66 @@
+"""Device health from RAS signals (deviceplugin/health.py): the policy, the
+monitor's transitions, and the plugin re-advertising a device that turns Unhealthy."""
+import dataclasses
+
+from gpu_topology_on_k8s_amd.deviceplugin.health import HealthMonitor, HealthPolicy, device_problems
+from gpu_topology_on_k8s_amd.topology.discovery import fake_topology
+from gpu_topology_on_k8s_amd.topology.model import GPUInfo
+
+
+def _gpu(**kw):
+    base = dict(index=0, ecc_uncorrectable=3, ecc_correctable=10, bad_pages=2, bad_page_threshold=64, xgmi_links_up=7)
+    base.update(kw)
+    return GPUInfo(**base)
+
+
+def test_policy_signals():
+    base = _gpu()
+    assert device_problems(_gpu(), base) == []
+    assert device_problems(_gpu(ecc_correctable=500), base) == []  # correctable errors alone are not fatal
+    assert "uncorrectable" in device_problems(_gpu(ecc_uncorrectable=4), base)[0]
+    assert "retired pages" in device_problems(_gpu(bad_pages=64), base)[0]
+    assert "xGMI" in device_problems(_gpu(xgmi_links_up=6), base)[0]
+    assert device_problems(_gpu(healthy=False), base)
+    # unreadable signals (-1) never count as failures
+    assert device_problems(_gpu(ecc_uncorrectable=-1, bad_pages=-1, xgmi_links_up=-1), base) == []
+    assert device_problems(_gpu(ecc_uncorrectable=9), _gpu(ecc_uncorrectable=-1)) == []
+    assert device_problems(_gpu(xgmi_links_up=6), base, HealthPolicy(xgmi_links=False)) == []
+
+
+def test_monitor_transitions_and_vanished_device():
+    topo = fake_topology(4)
+    for g in topo.gpus:
+        g.ecc_uncorrectable, g.xgmi_links_up = 0, 3
+    state = {"topo": topo}
+
+    def rediscover():
+        return state["topo"]
+
+    mon = HealthMonitor(topo, rediscover)
+    assert mon(topo) == {0: True, 1: True, 2: True, 3: True}
+    bad = fake_topology(4)
+    for g in bad.gpus:
+        g.ecc_uncorrectable, g.xgmi_links_up = 0, 3
+    bad.gpus[2] = dataclasses.replace(bad.gpus[2], ecc_uncorrectable=1)
+    bad.gpus[3] = dataclasses.replace(bad.gpus[3], xgmi_links_up=2)
+    state["topo"] = bad
+    assert mon(topo) == {0: True, 1: True, 2: False, 3: False}
+    assert "uncorrectable" in mon.reasons[2][0] and "xGMI" in mon.reasons[3][0]
+    state["topo"] = topo  # links retrain, counters as at start
+    assert all(mon(topo).values()) and mon.reasons[3] == []
+    shrunk = fake_topology(3)
+    for g in shrunk.gpus:
+        g.ecc_uncorrectable, g.xgmi_links_up = 0, 3
+    state["topo"] = shrunk
+    res = mon(topo)
+    assert res[3] is False and "vanished" in mon.reasons[3][0]
+
+
+def test_json_roundtrip_keeps_ras_fields():
+    from gpu_topology_on_k8s_amd.topology.model import Topology
+
+    t = fake_topology(2)
+    t.gpus[1].ecc_uncorrectable = 5
+    t.gpus[1].bad_page_threshold = 64
+    u = Topology.from_json(t.to_json())
+    assert u.gpus[1].ecc_uncorrectable == 5 and u.gpus[1].bad_page_threshold == 64
