@@ -39,6 +39,7 @@ def run(placement: str, a) -> dict:
            f"--master-port={_port()}", "-m", "gpu_topology_on_k8s_amd.models.train", "--model", a.model, "--batch", str(a.batch),
            "--seq", str(a.seq), "--steps", str(a.steps), "--warmup", str(a.warmup), "--placement", placement,
            "--bucket-mb", str(a.bucket_mb), "--attn", a.attn, "--gemm-tuning", a.gemm_tuning, "--gemm-layout", a.gemm_layout]
+           + (["--overlap-transposes"] if a.overlap_transposes else [])
            + (["--checkpoint"] if a.checkpoint else []) + (["--gemm-table", a.gemm_table] if a.gemm_table else []))
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""),
                **extra_env)
@@ -64,6 +65,7 @@ def main() -> int:
     ap.add_argument("--gemm-tuning", default="auto", choices=["auto", "off", "use", "tune"])
     ap.add_argument("--gemm-table", default="")
     ap.add_argument("--gemm-layout", default="nt", choices=["nt", "native"])
+    ap.add_argument("--overlap-transposes", action="store_true")
     ap.add_argument("--timeout", type=int, default=1500)
     ap.add_argument("--placements", default="best,worst", help="comma list of best, worst, p2p-off (emulated worst link class)")
     ap.add_argument("--out", default="")

@@ -14,7 +14,9 @@ MI355X-first layout:
   * backward GEMMs in the forward GEMM's "NT" layout (``gemm_layout="nt"``): dgrad as
     ``dy (W^T)^T`` and wgrad as ``(dy^T)(x^T)^T``, the operands transposed by the LDS-tiled HIP
     kernel (``ops.fused.transpose``) — hipBLASLt runs NT 10-40 % faster than the NN / TN layouts
-    autograd would hand it (bench/gemm_layout_bench.py);
+    autograd would hand it (bench/gemm_layout_bench.py).  ``overlap_transposes`` makes ``x^T`` and
+    ``W^T`` in the forward on a side HIP stream instead; measured on MI355X it does not pay (22.8k
+    vs 23.0k tok/s, +18 GB): the hipBLASLt GEMMs hold every CU, so the transposes only contend;
   * Llama-3-8B = 8.03 B params: 16 GB bf16 weights + 16 GB bf16 grads + 96 GB fp32 master/m/v =
     128 GB, leaving ~160 GB of the 288 GB HBM for activations, so DP alone suffices (no TP/PP/SP).
 """
@@ -141,16 +143,17 @@ class FlatParams:
         hooks.append(fn)
         return _ReadyHandle(hooks, fn)
 
-    def write_grad(self, name: str, dy: torch.Tensor, x: torch.Tensor, nt: bool = False,
-                   dy_t: Optional[torch.Tensor] = None) -> None:
+    def write_grad(self, name: str, dy: torch.Tensor, x: Optional[torch.Tensor], nt: bool = False,
+                   dy_t: Optional[torch.Tensor] = None, x_t: Optional[torch.Tensor] = None) -> None:
         """Weight gradient of ``y = x W^T`` into the flat buffer: ``W.grad (+)= dy^T x``.
 
         ``nt``: compute it as ``(dy^T)(x^T)^T`` from transposed copies, the GEMM layout hipBLASLt runs
-        fastest (both operands contiguous along the token dimension being reduced); ``dy_t`` is a
-        transposed copy the producer of ``dy`` already wrote (SwiGLU backward)."""
+        fastest (both operands contiguous along the token dimension being reduced); ``dy_t`` / ``x_t``
+        are transposed copies made elsewhere (SwiGLU backward; the forward's side stream)."""
         view = self.params[name].grad
         if nt:
-            a, b = (dy_t if dy_t is not None else fused.transpose(dy)), fused.transpose(x).t()
+            a = dy_t if dy_t is not None else fused.transpose(dy)
+            b = (x_t if x_t is not None else fused.transpose(x)).t()
         else:
             a, b = dy.t(), x
         if self.direct[name]:
@@ -190,23 +193,81 @@ class FlatParams:
         return o, o + math.prod(self.shapes[name])
 
 
+_SIDE_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def _side_stream(device: torch.device) -> "torch.cuda.Stream":
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _SIDE_STREAMS.get(idx)
+    if s is None:
+        s = _SIDE_STREAMS[idx] = torch.cuda.Stream(device=idx)
+    return s
+
+
+class _NTOperands:
+    """``x^T`` and ``W^T`` of one forward GEMM for its NT-layout backward GEMMs.
+
+    Default: made in backward on the main stream, just before their GEMMs.  ``overlap``: issued in
+    the FORWARD on a side HIP stream right after the producer of ``x`` (memory-bound transposes
+    under the compute-bound forward GEMMs), ``x^T`` kept instead of ``x``.  Measured at Llama-3-8B
+    b4 x 4096 on one MI355X: 22.8k tok/s with overlap vs 23.0k without, and +18 GB peak (all W^T
+    live through backward) -- the GEMMs hold every CU, so the side stream only contends."""
+
+    def __init__(self, x: torch.Tensor, w: torch.Tensor, overlap: bool):
+        self.event = None
+        if overlap and x.is_cuda:
+            main = torch.cuda.current_stream(x.device)
+            side = _side_stream(x.device)
+            side.wait_stream(main)  # x (and the optimizer's last write of w) are complete
+            with torch.cuda.stream(side):
+                self.x_t, self.w_t = fused.transpose(x), fused.transpose(w)
+            x.record_stream(side)  # x may be freed by the caller while the side stream still reads it
+            w.record_stream(side)
+            self.event = torch.cuda.Event()
+            self.event.record(side)
+            self.x, self.w = None, None
+        else:
+            self.x_t = self.w_t = None
+            self.x, self.w = x, w
+
+    def get(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        """-> (x^T, W^T), ready for use on the current stream."""
+        if self.event is not None:
+            main = torch.cuda.current_stream(self.x_t.device)
+            main.wait_event(self.event)
+            self.x_t.record_stream(main)  # allocated on the side stream, consumed on the main one
+            self.w_t.record_stream(main)
+            self.event = None
+        elif self.x_t is None:
+            self.x_t, self.w_t = fused.transpose(self.x), fused.transpose(self.w)
+            self.x = self.w = None
+        return self.x_t, self.w_t
+
+
 class _FlatLinear(torch.autograd.Function):
     """``y = x W^T`` whose weight gradient is written in place into the flat buffer."""
 
     @staticmethod
-    def forward(ctx, x, w, flat, name, nt):
-        ctx.save_for_backward(x, w)
+    def forward(ctx, x, w, flat, name, nt, overlap):
         ctx.flat, ctx.name, ctx.nt = flat, name, nt
+        if nt:
+            ctx.ops = _NTOperands(x, w, overlap)
+        else:
+            ctx.save_for_backward(x, w)
         return F.linear(x, w)
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dx = F.linear(dy, fused.transpose(w)) if ctx.nt else dy.mm(w)  # NT: dy (W^T)^T
-        ctx.flat.write_grad(ctx.name, dy, x, nt=ctx.nt)
-        return dx, None, None, None, None
+        if ctx.nt:
+            x_t, w_t = ctx.ops.get()
+            ctx.ops = None
+            dx = F.linear(dy, w_t) if ctx.needs_input_grad[0] else None  # dy (W^T)^T
+            ctx.flat.write_grad(ctx.name, dy, None, nt=True, x_t=x_t)
+        else:
+            x, w = ctx.saved_tensors
+            dx = dy.mm(w) if ctx.needs_input_grad[0] else None
+            ctx.flat.write_grad(ctx.name, dy, x)
+        return dx, None, None, None, None, None
 
 
 class _FlatLinearSwiGLU(torch.autograd.Function):
@@ -215,30 +276,36 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
     the transpose straight to the NT weight-gradient GEMM."""
 
     @staticmethod
-    def forward(ctx, x, w, flat, name, nt):
+    def forward(ctx, x, w, flat, name, nt, overlap):
         gu = F.linear(x, w)
-        ctx.save_for_backward(x, w, gu)
         ctx.flat, ctx.name, ctx.nt = flat, name, nt
+        if nt:
+            ctx.ops = _NTOperands(x, w, overlap)
+            ctx.save_for_backward(gu)
+        else:
+            ctx.save_for_backward(gu, x, w)
         return fused.hip().swiglu_fwd(gu) if gu.is_cuda else fused.swiglu_ref(gu)
 
     @staticmethod
     def backward(ctx, da):
-        x, w, gu = ctx.saved_tensors
+        gu = ctx.saved_tensors[0]
         if ctx.nt:
             dgu, dgu_t = fused.swiglu_bwd_t(da, gu)
+            x_t, w_t = ctx.ops.get()
+            ctx.ops = None
+            dx = F.linear(dgu, w_t) if ctx.needs_input_grad[0] else None
+            ctx.flat.write_grad(ctx.name, dgu, None, nt=True, dy_t=dgu_t, x_t=x_t)
         else:
+            _, x, w = ctx.saved_tensors
             dgu = fused.hip().swiglu_bwd(da.contiguous(), gu) if gu.is_cuda else fused.swiglu_bwd_ref(da, gu)
-            dgu_t = None
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dx = F.linear(dgu, fused.transpose(w)) if ctx.nt else dgu.mm(w)
-        ctx.flat.write_grad(ctx.name, dgu, x, nt=ctx.nt, dy_t=dgu_t)
-        return dx, None, None, None, None
+            dx = dgu.mm(w) if ctx.needs_input_grad[0] else None
+            ctx.flat.write_grad(ctx.name, dgu, x)
+        return dx, None, None, None, None, None
 
 
 class Llama(torch.nn.Module):
     def __init__(self, cfg: LlamaConfig, device="cuda", seed: int = 0, checkpoint: bool = False, attn: str = "hip",
-                 gemm_layout: str = "nt"):
+                 gemm_layout: str = "nt", overlap_transposes: bool = False):
         super().__init__()
         if gemm_layout not in ("nt", "native"):
             raise ValueError("gemm_layout must be 'nt' or 'native'")
@@ -246,6 +313,7 @@ class Llama(torch.nn.Module):
         self.checkpoint = checkpoint
         self.attn = attn
         self.gemm_layout = gemm_layout
+        self.overlap_transposes = overlap_transposes
         self.flat = FlatParams(cfg.param_shapes(), device)
         for n, p in self.flat.params.items():
             self.register_parameter(n.replace(".", "_"), p)
@@ -278,7 +346,7 @@ class Llama(torch.nn.Module):
 
     def _linear(self, x: torch.Tensor, name: str) -> torch.Tensor:
         nt = self.gemm_layout == "nt"
-        return _FlatLinear.apply(x, self.flat.params[name].detach(), self.flat, name, nt)
+        return _FlatLinear.apply(x, self.flat.params[name].detach(), self.flat, name, nt, self.overlap_transposes)
 
     # ---------------------------------------------------------------- blocks
     def _attention(self, q, k, v):
@@ -304,7 +372,8 @@ class Llama(torch.nn.Module):
         o = self._attention(q, k, v).reshape(B * S, H * Dh)  # [B, S, H, Dh] -> [B*S, H*Dh]
         x = x + self._linear(o, f"l{i}.wo")
         h = fused.rmsnorm(x, self.P(f"l{i}.ffn_norm"), cfg.norm_eps)
-        a = _FlatLinearSwiGLU.apply(h, self.flat.params[f"l{i}.w13"].detach(), self.flat, f"l{i}.w13", self.gemm_layout == "nt")
+        a = _FlatLinearSwiGLU.apply(h, self.flat.params[f"l{i}.w13"].detach(), self.flat, f"l{i}.w13", self.gemm_layout == "nt",
+                                    self.overlap_transposes)
         x = x + self._linear(a, f"l{i}.w2")
         return x
 

@@ -59,7 +59,7 @@ def _choose_device(env, placement: str, discovery: str) -> Dict[str, object]:
 def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int = 3, warmup: int = 1, device_kind: str = "cuda",
           placement: str = "best", discovery: str = "auto", bucket_mb: float = 256.0, checkpoint: bool = False, lr: float = 3e-4,
           attn: str = "hip", seed: int = 0, log: bool = True, gemm_tuning: str = "auto",
-          gemm_table: Optional[str] = None, gemm_layout: str = "nt") -> Dict[str, object]:
+          gemm_table: Optional[str] = None, gemm_layout: str = "nt", overlap_transposes: bool = False) -> Dict[str, object]:
     env = _init_dist(device_kind)
     if device_kind == "cuda":
         pl = _choose_device(env, placement, discovery)
@@ -72,7 +72,8 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         device = torch.device("cpu")
         gemm_mode = "off"
     cfg = LlamaConfig.named(model_name)
-    model = Llama(cfg, device=device, seed=seed, checkpoint=checkpoint, attn=attn, gemm_layout=gemm_layout)
+    model = Llama(cfg, device=device, seed=seed, checkpoint=checkpoint, attn=attn, gemm_layout=gemm_layout,
+                  overlap_transposes=overlap_transposes)
     broadcast_params(model.flat)
     ar = BucketedAllReduce(model.flat, bucket_mb=bucket_mb)
     opt = FlatAdamW(model.flat, lr=lr)
@@ -136,6 +137,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "bucket_mb": bucket_mb,
         "gemm_tuning": gemm_mode,
         "gemm_layout": gemm_layout,
+        "overlap_transposes": overlap_transposes,
         "max_mem_gb": (torch.cuda.max_memory_allocated(device) / 1e9) if device.type == "cuda" else None,
     }
     if log and env["rank"] == 0:
@@ -162,9 +164,12 @@ def main(argv=None) -> int:
     ap.add_argument("--gemm-table", default=None, help="TunableOp results table (default: the shipped MI355X table)")
     ap.add_argument("--gemm-layout", default="nt", choices=["nt", "native"],
                     help="backward GEMM operand layout: nt = transposed operands (HIP transpose kernel), native = as autograd issues them")
+    ap.add_argument("--overlap-transposes", action="store_true",
+                    help="make the NT operands' transposes on a side stream in forward (measured: no gain on MI355X)")
     a = ap.parse_args(argv)
     train(a.model, a.batch, a.seq, a.steps, a.warmup, a.device, a.placement, a.discovery, a.bucket_mb, a.checkpoint, attn=a.attn,
-          gemm_tuning=a.gemm_tuning, gemm_table=a.gemm_table, gemm_layout=a.gemm_layout)
+          gemm_tuning=a.gemm_tuning, gemm_table=a.gemm_table, gemm_layout=a.gemm_layout,
+          overlap_transposes=a.overlap_transposes)
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0

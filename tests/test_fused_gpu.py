@@ -167,12 +167,16 @@ def test_llama_nt_layout_matches_native_gpu():
     cfg = LlamaConfig.tiny()
     tok = torch.randint(0, cfg.vocab, (2, 128), device="cuda")
     grads = {}
-    for layout in ("native", "nt"):
-        m = Llama(cfg, device="cuda", seed=3, gemm_layout=layout)
-        m.flat.zero_grad()
-        m(tok, torch.roll(tok, -1, 1)).backward()
-        grads[layout] = m.flat.grad.float().clone()
-    assert _rel(grads["nt"], grads["native"]) < 1e-2
+    for layout, overlap in (("native", False), ("nt", False), ("nt", True)):
+        m = Llama(cfg, device="cuda", seed=3, gemm_layout=layout, overlap_transposes=overlap)
+        for _ in range(2):  # a weight update between steps: the side stream must see the new weights
+            m.flat.zero_grad()
+            m(tok, torch.roll(tok, -1, 1)).backward()
+            with torch.no_grad():
+                m.flat.data.add_(m.flat.grad, alpha=-1e-2)
+        grads[(layout, overlap)] = m.flat.grad.float().clone()
+    assert _rel(grads[("nt", False)], grads[("native", False)]) < 1e-2
+    assert torch.equal(grads[("nt", True)], grads[("nt", False)])  # same kernels, only the stream differs
 
 
 def test_llama_model_gpu_matches_cpu_reference():
