@@ -56,6 +56,9 @@ def main():
     t = timeit(lambda: hip.attn_bwd(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
     res["hip_bwd_ms"] = t * 1e3
     res["hip_bwd_tflops"] = 2.5 * fwd_flops / t / 1e12
+    if hasattr(hip, "attn_bwd_v3"):
+        t = timeit(lambda: hip.attn_bwd_v3(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
+        res["hip_bwd_v3_ms"] = t * 1e3
     if hasattr(hip, "attn_bwd_v2"):
         t = timeit(lambda: hip.attn_bwd_v2(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
         res["hip_bwd_v2_ms"] = t * 1e3

@@ -893,6 +893,186 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv3_kernel(const u16* __res
     }
 }
 
+// dK/dV v4: dK/dV v3 software-pipelined across query slices.  PMC on v3 (profiles/r01_attention):
+// the MFMA pipe is busy ~27 % of the time and the kernel issues ~13 VALU per MFMA, because at one
+// wave per SIMD the softmax/dS VALU block of a slice sits between its S/dP MFMAs and its dV/dK
+// MFMAs with nothing to overlap it.  v4 defers each slice's dV^T/dK^T MFMAs by one slice: slice i's
+// softmax/dS VALU runs interleaved (sched_group_barrier) with slice i-1's dV/dK MFMAs, which need
+// only slice i-1's packed bf16 P/dS (16 VGPRs carried across iterations; a second S/dP accumulator
+// set would spill).  Slices rotate through a 3-buffer LDS ring (i-1 read by the deferred dV/dK
+// products, i by S/dP, i+1 in flight by LDS-DMA), still one barrier per slice.  Diagonal slices (the
+// first KB/QT of each q-head) and slices a wave skips take the unfused path.
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv4_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
+                                                                const u16* __restrict__ v, const u16* __restrict__ dout,
+                                                                const float* __restrict__ lse2, const float* __restrict__ delta,
+                                                                u16* __restrict__ dk, u16* __restrict__ dv, int H, int Hkv,
+                                                                int S, float c, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[3 * SL_BYTES];  // slice ring
+  const int t = threadIdx.x, lane = t & 63, r = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int kb = blockIdx.y;
+  const int bk = xcd_head(blockIdx.x, gridDim.x), b = bk / Hkv, hk = bk % Hkv, G = H / Hkv;
+  const size_t kvoff = ((size_t)(b * Hkv + hk) * S + (size_t)kb * KB) * D;
+  const int krow = w * 32 + r, mykey = kb * KB + krow, kmin = kb * KB + w * 32;
+  bf16x8 kf[8], vf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    kf[s] = *reinterpret_cast<const bf16x8*>(k + kvoff + (size_t)krow * D + 16 * s + 8 * hh);
+    vf[s] = *reinterpret_cast<const bf16x8*>(v + kvoff + (size_t)krow * D + 16 * s + 8 * hh);
+  }
+  f32x16 dvt[4], dkt[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dvt[dt] = dkt[dt] = f32x16{};
+  const int qt0 = (kb * KB) / QT, nqt = S / QT - qt0, nslice = G * nqt;
+
+  const uint32_t qbytes = (uint32_t)((size_t)H * S * D * 2), dbytes = (uint32_t)((size_t)S * H * D * 2);
+  const auto qrs = __builtin_amdgcn_make_buffer_rsrc((void*)(q + (size_t)b * H * S * D), 0, qbytes, 0x00020000);
+  const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)(dout + (size_t)b * S * H * D), 0, dbytes, 0x00020000);
+  const auto lrs = __builtin_amdgcn_make_buffer_rsrc((void*)((w == 0 ? lse2 : delta) + (size_t)b * H * S), 0,
+                                                     (uint32_t)((size_t)H * S * 4), 0x00020000);
+  uint32_t qv[2], dvo[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int R = 8 * w + 4 * i + (lane >> 4);
+    const uint32_t ch16 = 16 * ((lane & 15) ^ (((R & 3) << 2) | ((R >> 2) & 3)));
+    qv[i] = (uint32_t)(R * D * 2) + ch16;
+    dvo[i] = (uint32_t)(R * H * D * 2) + ch16;
+  }
+  auto ring = [&](int idx) -> char* { return smem + (idx % 3) * SL_BYTES; };
+  auto sload = [&](int idx) {
+    char* buf = ring(idx);
+    const int hq = hk * G + idx / nqt, qbase = (qt0 + idx % nqt) * QT;
+    const uint32_t qs = (uint32_t)(((size_t)hq * S + qbase) * D * 2), ds = (uint32_t)(((size_t)qbase * H + hq) * D * 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (LDS_AS void*)(buf + SL_Q + (8 * w + 4 * i) * 256), 16, qv[i], qs, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, (LDS_AS void*)(buf + SL_DO + (8 * w + 4 * i) * 256), 16, dvo[i], ds, 0, 0);
+    }
+    if (w < 2)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, (LDS_AS void*)(buf + (w == 0 ? SL_LSE : SL_DEL)), 4, 4 * lane,
+                                               (uint32_t)(((size_t)hq * S + qbase) * 4), 0, 0);
+  };
+  // slice state: does this wave compute slice idx at all, and does it need the causal mask there
+  auto active = [&](int idx) {
+    const int j = idx % nqt;
+    return j >= KB / QT || (qt0 + j) * QT + QT - 1 >= kmin;
+  };
+  auto masked = [&](int idx) { return idx % nqt < KB / QT; };
+
+  // S and dP of one slice (key on the lane, 32 queries in registers)
+  auto sdp = [&](const char* buf, f32x16& sacc, f32x16& dpacc) {
+    const char* qimg = buf + SL_Q;
+    const char* doimg = buf + SL_DO;
+    sacc = f32x16{};
+    dpacc = f32x16{};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      sacc = mfma(lds_b128(qimg, swz(r, 2 * s + hh)), kf[s], sacc);
+      dpacc = mfma(lds_b128(doimg, swz(r, 2 * s + hh)), vf[s], dpacc);
+    }
+  };
+  struct Packs {  // bf16 B operands of dV^T (P) and dK^T (dS) for one slice
+    bf16x8 p0, p1, d0, d1;
+  };
+  // dV^T += dO^T.P and dK^T += Q^T.dS (dO^T, Q^T by transposed LDS reads of the slice's images)
+  auto dvdk = [&](const char* buf, const Packs& pk) {
+    const char* qimg = buf + SL_Q;
+    const char* doimg = buf + SL_DO;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      dvt[dt] = mfma(tr_frag(doimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), pk.p0, dvt[dt]);
+      dvt[dt] = mfma(tr_frag(doimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), pk.p1, dvt[dt]);
+      dkt[dt] = mfma(tr_frag(qimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), pk.d0, dkt[dt]);
+      dkt[dt] = mfma(tr_frag(qimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), pk.d1, dkt[dt]);
+    }
+  };
+
+  // Iteration idx, one basic block: S/dP of slice idx (MFMA); then its softmax/dS (VALU) interleaved
+  // with the dV/dK MFMAs of slice idx-1, whose bf16 operands (16 VGPRs) were packed one iteration
+  // earlier.  No branches: a slice this wave would skip (all its queries precede the wave's keys)
+  // runs with P = 0 (adds exact zeros), the causal mask is a select, and the first iteration's
+  // deferred products use zero packs.  With one MFMA path the accumulators stay put: v3's two
+  // inlined paths made the register allocator copy all 128 dK/dV accumulators VGPR -> AGPR on
+  // every slice (v_accvgpr_write x 128 in the .s).
+  Packs prev{};
+  {  // ring(2) is what the first iteration's deferred (zero-pack) products read: make it zeros, not
+     // whatever bits the LDS held (0 x NaN would poison the accumulators)
+    u16x8* z = reinterpret_cast<u16x8*>(smem + 2 * SL_BYTES);
+    for (int i = t; i < SL_BYTES / 16; i += 256) z[i] = u16x8{};
+  }
+  __syncthreads();
+  sload(0);
+  dma_sync();
+  // One slice; `rb` = ring slot of slice idx, a constant at every call site (the loop is unrolled by
+  // the ring length), so every LDS address is a hoisted per-lane offset plus an immediate.
+  auto step = [&](int idx, const int rb) {
+    // ring slot rb landed at the last barrier; slot (rb+1)%3 = slice idx-2's, read by the dV/dK
+    // products of the previous step, takes slice idx+1; slot (rb+2)%3 (slice idx-1) stays intact
+    if (idx + 1 < nslice) sload(idx + 1);
+    const int j = idx % nqt;
+    const int qbase = (qt0 + j) * QT;
+    const bool dead = !active(idx);  // wave-uniform
+    const int kill_from = dead ? -(1 << 30) : (masked(idx) ? qbase : 1 << 30);  // key - query > kill_from -> P = 0
+    const char* buf = smem + rb * SL_BYTES;
+    f32x16 sacc, dpacc;
+    sdp(buf, sacc, dpacc);
+    __builtin_amdgcn_sched_barrier(0);
+    Packs cur;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 lq = *reinterpret_cast<const f32x4*>(buf + SL_LSE + 4 * (8 * g + 4 * hh));
+      const f32x4 dq_ = *reinterpret_cast<const f32x4*>(buf + SL_DEL + 4 * (8 * g + 4 * hh));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * g + e;
+        float pv = fexp2(fmaf(sacc[i], c, -lq[e]));
+        pv = (mykey - crow(i, hh) > kill_from) ? 0.f : pv;
+        sacc[i] = pv;
+        dpacc[i] = pv * (dpacc[i] - dq_[e]);
+      }
+    }
+    cur = Packs{pack8(sacc, 0), pack8(sacc, 8), pack8(dpacc, 0), pack8(dpacc, 8)};
+    dvdk(smem + ((rb + 2) % 3) * SL_BYTES, prev);  // slice idx-1; at idx = 0 zero packs on zeros
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {  // {1 dV/dK MFMA, 2 transposed reads, 12 softmax VALU} x 16
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    prev = cur;
+    dma_sync();
+  };
+  int idx = 0;
+  for (; idx + 3 <= nslice; idx += 3) {
+    step(idx, 0);
+    step(idx + 1, 1);
+    step(idx + 2, 2);
+  }
+  if (idx < nslice) step(idx, 0);
+  if (idx + 1 < nslice) step(idx + 1, 1);
+  switch ((nslice - 1) % 3) {  // the last slice's deferred dV/dK products
+    case 0: dvdk(smem, prev); break;
+    case 1: dvdk(smem + SL_BYTES, prev); break;
+    default: dvdk(smem + 2 * SL_BYTES, prev); break;
+  }
+  u16* dkrow = dk + ((size_t)(b * Hkv + hk) * S + mykey) * D;
+  u16* dvrow = dv + ((size_t)(b * Hkv + hk) * S + mykey) * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u16x4 a4, b4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a4[e] = f2bf(dkt[dt][4 * g4 + e] * scale);
+        b4[e] = f2bf(dvt[dt][4 * g4 + e]);
+      }
+      *reinterpret_cast<u16x4*>(dkrow + 32 * dt + 8 * g4 + 4 * hh) = a4;
+      *reinterpret_cast<u16x4*>(dvrow + 32 * dt + 8 * g4 + 4 * hh) = b4;
+    }
+}
+
 // dQ v2: attn_bwd_dq_kernel restructured like forward v2 — LDS-DMA double-buffered K/V tiles with
 // one barrier per tile, the block's diagonal tiles peeled out of a branch-free main loop, LPT +
 // XCD-grouped grid (B*H, S/128).  (Forcing the fragment reads ahead with sched_group_barrier spills
@@ -1046,6 +1226,27 @@ std::vector<at::Tensor> attn_fwd_debug(const at::Tensor& q, const at::Tensor& k,
   return attn_fwd_impl(q, k, v, scale, true);
 }
 
+// v3 dK/dV (kept for A/B: v4 must match it bit for bit) + dQ v2
+std::vector<at::Tensor> attn_bwd_v3(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                    const at::Tensor& out, const at::Tensor& lse, double scale) {
+  check_qkv(q, k, v);
+  const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
+  TORCH_CHECK(dout.is_contiguous() && out.is_contiguous() && dout.numel() == q.numel() && out.numel() == q.numel(),
+              "attention bwd: dout/out must be contiguous [B, S, H, D]");
+  auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+  auto dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
+  const int rows = B * S * H;
+  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
+                     delta.data_ptr<float>(), B, H, S);
+  const float c = (float)(scale * 1.4426950408889634);
+  hipLaunchKernelGGL(attn_bwd_dkdv3_kernel, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
+                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
+  hipLaunchKernelGGL(attn_bwd_dq2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
+                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
+  return {dq, dk, dv};
+}
+
+// default backward: delta, dK/dV v4 (software-pipelined slices), dQ v2
 std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                  const at::Tensor& out, const at::Tensor& lse, double scale) {
   check_qkv(q, k, v);
@@ -1058,7 +1259,7 @@ std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, co
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
                      delta.data_ptr<float>(), B, H, S);
   const float c = (float)(scale * 1.4426950408889634);
-  hipLaunchKernelGGL(attn_bwd_dkdv3_kernel, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
+  hipLaunchKernelGGL(attn_bwd_dkdv4_kernel, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
                      lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
   hipLaunchKernelGGL(attn_bwd_dq2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
                      lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);

@@ -668,6 +668,8 @@ std::vector<at::Tensor> attn_bwd_atomic(const at::Tensor& dout, const at::Tensor
                                         const at::Tensor& out, const at::Tensor& lse, double scale);
 std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                  const at::Tensor& out, const at::Tensor& lse, double scale);
+std::vector<at::Tensor> attn_bwd_v3(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                    const at::Tensor& out, const at::Tensor& lse, double scale);
 }  // namespace gtk_attn
 
 namespace gtk_xpose {  // csrc/ops/transpose.hip
@@ -680,6 +682,7 @@ PYBIND11_MODULE(_fused, m) {
   m.def("attn_bwd", &gtk_attn::attn_bwd, "flash attention backward: -> (dq, dk, dv)");
   m.def("attn_fwd_debug", &gtk_attn::attn_fwd_debug, "forward + raw S^T accumulators of the first KV tile (tests)");
   m.def("attn_tr_probe", &gtk_attn::attn_tr_probe, "transposed-fragment gather of a [64][128] tile (tests)");
+  m.def("attn_bwd_v3", &gtk_attn::attn_bwd_v3, "v3 backward (dK/dV not pipelined across slices; A/B reference for v4)");
   m.def("attn_bwd_v2", &gtk_attn::attn_bwd_v2, "v2 backward (synchronous dK/dV slice staging; A/B reference)");
   m.def("attn_bwd_atomic", &gtk_attn::attn_bwd_atomic, "v1 fused backward with fp32 dQ atomics (A/B reference)");
   m.doc() = "gfx950 fused kernels for the Llama-3 DP validation workload";

@@ -72,9 +72,27 @@ def test_attention_kernel_generations_agree(fused):
     o1, l1 = hip.attn_fwd_v1(q, k, v, 128 ** -0.5)
     assert _rel(o2, o1) < 5e-3 and torch.allclose(l2, l1, atol=1e-3)
     g3 = hip.attn_bwd(do, q, k, v, o2, l2, 128 ** -0.5)
-    g2 = hip.attn_bwd_v2(do, q, k, v, o2, l2, 128 ** -0.5)
+    g2 = hip.attn_bwd_v2(do, q, k, v, o2, l2, 128 ** -0.5)  # v4 default vs v2
     for a, b in zip(g3, g2):
         assert _rel(a, b) < 5e-3, _rel(a, b)
+
+
+@pytest.mark.parametrize("B,H,Hkv,S", [(2, 8, 2, 768), (1, 4, 4, 128), (1, 32, 8, 1024), (2, 4, 1, 384)])
+def test_attention_bwd_v4_matches_v3(fused, B, H, Hkv, S):
+    """dK/dV v4 (the default: slices software-pipelined through a 3-buffer ring, branch-free) does
+    v3's arithmetic in v3's order: identical bits, including the all-diagonal S=128 case, MHA
+    (G=1), G=4 and G=8, and slice counts that are not multiples of the ring length."""
+    torch.manual_seed(5)
+    q = torch.randn(B, H, S, 128, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
+    do = torch.randn(B, S, H, 128, device="cuda", dtype=torch.bfloat16)
+    hip = fused.hip()
+    o, lse = hip.attn_fwd(q, k, v, 128 ** -0.5)
+    g3 = hip.attn_bwd_v3(do, q, k, v, o, lse, 128 ** -0.5)
+    g4 = hip.attn_bwd(do, q, k, v, o, lse, 128 ** -0.5)
+    for name, a, b in zip(("dq", "dk", "dv"), g4, g3):
+        assert torch.equal(a, b), (name, _rel(a, b))
 
 
 def test_attention_causality(fused):
