@@ -286,7 +286,11 @@ def main(argv=None) -> int:
     sweep = None
     sizes = sweep_sizes(args.sweep, cpu=cpu)
     if sizes:
-        sweep = run_sweep(runner, sizes, env, tdev, barrier_kw, gpu_sync)
+        try:  # supplementary: a failure here (e.g. no memory for 2 x 16 GiB) must not cost the headline
+            sweep = run_sweep(runner, sizes, env, tdev, barrier_kw, gpu_sync)
+        except Exception as e:  # noqa: BLE001 - every rank runs the same sizes, so all land here together
+            print(f"bench: size sweep aborted on rank {env.rank}: {e}", file=sys.stderr)
+            sweep = {"error": str(e)[:300]}
     runner.close()
     if env.rank == 0:
         bound = (choice.extra.get("probe") or {}).get("subset_ingress_bound_gbps")  # K5/K1 ceiling of busBW
