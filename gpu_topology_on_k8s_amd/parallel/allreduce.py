@@ -70,7 +70,7 @@ def _visible_device_count() -> int:
     return int(torch.cuda.device_count())
 
 
-def probe_node(preset: str = "quick", backend: str = "auto", timeout: float = 240.0):
+def probe_node(preset: str = "quick", backend: str = "auto", timeout: float = 150.0):
     """Node-start link probe in a CHILD process: discovery + K4 warm-up + K1 p2p
     read over every visible ordered pair, written as topology JSON.  A child keeps the probe's HIP
     contexts on every device (and any failure) out of the caller, which goes on to build its RCCL
@@ -135,7 +135,30 @@ def probe_summary(topo, subset: Sequence[int]) -> Dict[str, object]:
     return out
 
 
-def schedule_via_k8s(topo, k: int, node: str = "") -> Dict[str, object]:
+def schedule_via_k8s(topo, k: int, node: str = "", timeout: float = 60.0) -> Dict[str, object]:
+    """:func:`_schedule_via_k8s` in a daemon thread, bounded by ``timeout`` seconds (raises on expiry):
+    the in-process cluster opens sockets and servers, and a stuck one must not stall the job."""
+    import threading
+
+    box: Dict[str, object] = {}
+
+    def run():
+        try:
+            box["ok"] = _schedule_via_k8s(topo, k, node)
+        except Exception as e:  # noqa: BLE001 - re-raised in the caller's thread
+            box["err"] = e
+
+    th = threading.Thread(target=run, name="gtk-k8s-flow", daemon=True)
+    th.start()
+    th.join(timeout)
+    if th.is_alive():
+        raise TimeoutError(f"k8s flow did not finish within {timeout:.0f}s")
+    if "err" in box:
+        raise box["err"]  # type: ignore[misc]
+    return box["ok"]  # type: ignore[return-value]
+
+
+def _schedule_via_k8s(topo, k: int, node: str = "") -> Dict[str, object]:
     """Place a k-GPU pod through the whole Kubernetes path, in process (``sim.SimCluster``, CPU only):
     the device plugin publishes ``topo`` on a fake apiserver and registers with a fake kubelet over
     gRPC; the mini scheduler calls the extender's ``/filter``, ``/sort`` and ``/bind`` over HTTP;
