@@ -1,0 +1,10 @@
+#!/bin/bash
+# Whole-tree GPU check: GPU test suite, smoke(), headline bench, bench kernel profile.
+cd "${GRAFT_REPO_ROOT:-.}" || exit 1
+source tools/gpu_steps.sh
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench_k1 300 python3 bench.py
+step prof_bench 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench_full -o bench -- python3 bench.py --steps 20 --warmup 5
+echo "== done"
