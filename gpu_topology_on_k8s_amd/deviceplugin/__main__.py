@@ -56,10 +56,17 @@ def main(argv=None) -> int:
 
     topo = discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus)
     if a.probe != "off" and a.discovery != "fake":
-        from ..ops.probe import probe_topology
+        # in a child process: the plugin lives as long as the node and must not hold HIP contexts
+        # and probe buffers on every GPU it hands out to pods
+        from ..ops.probe import probe_in_child
 
-        probe_topology(topo, preset=a.probe)
-        log.info("probe: %s", topo.probe)
+        probed, msg = probe_in_child(a.probe, backend=a.discovery)
+        if probed is not None and probed.n == topo.n:
+            probed.node_name = topo.node_name
+            topo = probed
+            log.info("probe (%s): %s", msg, topo.probe)
+        else:
+            log.warning("link probe unavailable (%s); publishing discovered link classes", msg)
     log.info("topology:\n%s", topo.render())
 
     health = HealthMonitor(topo, lambda: discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus))

@@ -9,8 +9,12 @@ left unmeasured (nan) and the cost model falls back to the discovered link class
 """
 from __future__ import annotations
 
+import os
+import subprocess
+import sys
+import tempfile
 import time
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -18,7 +22,7 @@ from .._native import load
 from ..topology.model import Topology
 
 __all__ = ["device_count", "device_props", "warmup", "copy_bw", "gather_bw", "measure_matrix", "measure_ingress",
-           "probe_topology", "ingress_bound", "PROBE_PRESETS"]
+           "probe_topology", "probe_in_child", "ingress_bound", "PROBE_PRESETS"]
 
 #: bytes per transfer / timed iterations; sizes exceed the 256 MiB Infinity Cache for "full".
 PROBE_PRESETS: Dict[str, Dict[str, int]] = {
@@ -135,3 +139,37 @@ def probe_topology(topo: Topology, preset: str = "quick", devs: Optional[List[in
         },
     )
     return topo
+
+
+def probe_in_child(preset: str = "quick", backend: str = "auto", timeout: float = 150.0,
+                   ingress: bool = True) -> Tuple[Optional[Topology], str]:
+    """Discovery + K4 warm-up + K1 p2p read of every visible ordered pair (+ K5 ingress) in a CHILD
+    process (``gtk probe --out``), returned as a probed :class:`Topology`.
+
+    Long-lived callers (the device-plugin DaemonSet, rank 0 of the bench) must not keep HIP contexts
+    and probe buffers on every GPU of the node: the child takes them and exits, and a failure there
+    (fault, timeout) cannot take the caller down.  The pairwise matrix is written before the ingress
+    stage runs, so an ingress failure still returns it.  Returns ``(Topology | None, message)``."""
+    fd, path = tempfile.mkstemp(prefix="gtk_probe_", suffix=".json")
+    os.close(fd)
+    cmd = [sys.executable, "-m", "gpu_topology_on_k8s_amd", "probe", "--preset", preset, "--discovery", backend, "--out", path]
+    if ingress:
+        cmd.append("--ingress")
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=root)
+        err = f"probe exited {p.returncode}: {(p.stderr or p.stdout).strip()[-400:]}"
+        with open(path) as f:
+            text = f.read()
+        if not text:
+            return None, err
+        return Topology.from_json(text), ("ok" if p.returncode == 0 else "pairwise only; ingress stage failed: " + err)
+    except subprocess.TimeoutExpired:
+        return None, f"probe timed out after {timeout:.0f}s"
+    except (OSError, ValueError, KeyError) as e:
+        return None, f"probe output unreadable: {e}"
+    finally:
+        try:
+            os.unlink(path)
+        except OSError:
+            pass

@@ -71,38 +71,10 @@ def _visible_device_count() -> int:
 
 
 def probe_node(preset: str = "quick", backend: str = "auto", timeout: float = 150.0):
-    """Node-start link probe in a CHILD process: discovery + K4 warm-up + K1 p2p
-    read over every visible ordered pair, written as topology JSON.  A child keeps the probe's HIP
-    contexts on every device (and any failure) out of the caller, which goes on to build its RCCL
-    communicator on one device.  Returns ``(Topology | None, message)``."""
-    import subprocess
-    import sys
-    import tempfile
+    """Node-start link probe in a child process (:func:`ops.probe.probe_in_child`)."""
+    from ..ops.probe import probe_in_child
 
-    from ..topology.model import Topology
-
-    fd, path = tempfile.mkstemp(prefix="gtk_probe_", suffix=".json")
-    os.close(fd)
-    cmd = [sys.executable, "-m", "gpu_topology_on_k8s_amd", "probe", "--preset", preset, "--discovery", backend, "--out", path,
-           "--ingress"]
-    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    try:
-        p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=root)
-        err = f"probe exited {p.returncode}: {(p.stderr or p.stdout).strip()[-400:]}"
-        text = open(path).read() if os.path.getsize(path) else ""
-        if not text:
-            return None, err
-        # the pairwise matrix is on disk before the ingress stage runs: keep it if only that failed
-        return Topology.from_json(text), ("ok" if p.returncode == 0 else "pairwise only; ingress stage failed: " + err)
-    except subprocess.TimeoutExpired:
-        return None, f"probe timed out after {timeout:.0f}s"
-    except (OSError, ValueError, KeyError) as e:
-        return None, f"probe output unreadable: {e}"
-    finally:
-        try:
-            os.unlink(path)
-        except OSError:
-            pass
+    return probe_in_child(preset, backend=backend, timeout=timeout)
 
 
 def probe_summary(topo, subset: Sequence[int]) -> Dict[str, object]:

@@ -178,3 +178,39 @@ def test_bench_py_single_gpu():
     assert out["config"]["message_bytes_per_gpu"] == 64 << 20
     sw = out["size_sweep"]  # 8 B .. 16 GiB, every size exactly checked
     assert sw["all_exact"] and sw["rows"][-1]["bytes"] == 16 << 30 and sw["peak"]["algbw_gbps"] > 0
+
+
+def test_device_plugin_daemon_probes_in_child_on_real_node():
+    """DaemonSet entry on the real node with --probe quick: the probe runs in a child process, the
+    published topology annotation carries its measurements, and the plugin registers."""
+    import shutil
+    import signal
+    import tempfile
+
+    from gpu_topology_on_k8s_amd.deviceplugin import FakeKubelet
+    from gpu_topology_on_k8s_amd.k8s import Contract, FakeAPIServer, serve_http
+    from gpu_topology_on_k8s_amd.k8s.objects import make_node
+
+    api = FakeAPIServer()
+    api.create_node(make_node("gpu-node"))
+    srv, url = serve_http(api)
+    sockdir = tempfile.mkdtemp(prefix="gtkd", dir="/tmp")
+    kubelet = FakeKubelet(sockdir, node_name="gpu-node", api=api)
+    kubelet.start()
+    p = subprocess.Popen([sys.executable, "-m", "gpu_topology_on_k8s_amd.deviceplugin", "--discovery", "auto", "--probe", "quick",
+                          "--apiserver", url, "--node-name", "gpu-node", "--socket-dir", sockdir, "--log-level", "INFO"],
+                         cwd=REPO, env=dict(os.environ, PYTHONPATH=REPO), stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    try:
+        plugin = kubelet.wait_for("amd.com/gpu", timeout=120)
+        assert len(plugin.devices) >= 1
+        ann = api.get_node("gpu-node")["metadata"]["annotations"]
+        topo = json.loads(ann[Contract().topology_key])
+        assert topo["probe"]["method"] == "p2p_read_lds" and topo["hbm_gbps"][0] > 1000
+    finally:
+        if p.poll() is None:
+            p.send_signal(signal.SIGTERM)
+            p.wait(timeout=30)
+        kubelet.stop()
+        srv.shutdown()
+        shutil.rmtree(sockdir, ignore_errors=True)
+    assert p.returncode == 0, p.stdout.read() if p.stdout else ""
