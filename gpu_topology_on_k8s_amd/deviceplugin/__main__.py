@@ -49,6 +49,10 @@ def main(argv=None) -> int:
     ap.add_argument("--token", default="")
     ap.add_argument("--dev-root", default="/dev")
     ap.add_argument("--health-interval", type=float, default=10.0)
+    ap.add_argument("--reprobe-interval", type=float, default=0.0,
+                    help="re-measure the links (child process) every N s while no pod holds a device; 0 = never")
+    ap.add_argument("--reprobe-tolerance", type=float, default=0.15,
+                    help="republish the topology when a measured pair moved by more than this fraction")
     ap.add_argument("--log-level", default="INFO")
     a = ap.parse_args(argv)
     logging.basicConfig(level=a.log_level, format='{"ts":"%(asctime)s","lvl":"%(levelname)s","mod":"%(name)s","msg":"%(message)s"}')
@@ -73,8 +77,16 @@ def main(argv=None) -> int:
 
     cfg = PluginConfig(resource_name=a.resource_name, socket_dir=a.socket_dir, socket_name=a.socket_name, dev_root=a.dev_root,
                        node_name=a.node_name, contract=Contract(resource_name=a.resource_name, prefix=a.annotation_prefix),
-                       health_interval=a.health_interval)
-    plugin = DevicePluginServer(topo, cfg, api=make_api(a.apiserver, a.token), health_fn=health if a.discovery != "fake" else None)
+                       health_interval=a.health_interval, reprobe_interval=a.reprobe_interval,
+                       reprobe_tolerance=a.reprobe_tolerance)
+    reprobe = None
+    if a.reprobe_interval > 0 and a.discovery != "fake":
+        from ..ops.probe import probe_in_child
+
+        def reprobe():
+            return probe_in_child(a.probe if a.probe != "off" else "quick", backend=a.discovery)[0]
+    plugin = DevicePluginServer(topo, cfg, api=make_api(a.apiserver, a.token), health_fn=health if a.discovery != "fake" else None,
+                                reprobe_fn=reprobe)
     done = threading.Event()
     for sig in (signal.SIGINT, signal.SIGTERM):  # installed before serving: a stop never races start-up
         signal.signal(sig, lambda *_: done.set())

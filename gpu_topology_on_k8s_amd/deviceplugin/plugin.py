@@ -54,7 +54,8 @@ class PluginConfig:
                  socket_name: str = "amd-gpu-topology.sock", kubelet_socket: Optional[str] = None, dev_root: str = "/dev",
                  node_name: str = "", contract: Optional[Contract] = None, health_interval: float = 5.0,
                  publish_node: bool = True, pass_rccl_env: bool = True, policy: PlacementPolicy = PlacementPolicy(),
-                 resource_aliases: Sequence[str] = ("aliyun.com/gpu", "aliyun.com/gpu-count")):
+                 resource_aliases: Sequence[str] = ("aliyun.com/gpu", "aliyun.com/gpu-count"),
+                 reprobe_interval: float = 0.0, reprobe_tolerance: float = 0.15):
         self.resource_name = resource_name
         self.socket_dir = socket_dir
         self.socket_name = socket_name
@@ -67,6 +68,10 @@ class PluginConfig:
         self.pass_rccl_env = pass_rccl_env
         self.policy = policy
         self.resource_aliases = tuple(resource_aliases)
+        # re-measure the links every `reprobe_interval` s while no pod holds a device (0 = never);
+        # republish when any measured pair moved by more than `reprobe_tolerance` (relative)
+        self.reprobe_interval = reprobe_interval
+        self.reprobe_tolerance = reprobe_tolerance
 
     @property
     def socket_path(self) -> str:
@@ -75,11 +80,15 @@ class PluginConfig:
 
 class DevicePluginServer:
     def __init__(self, topology: Topology, config: Optional[PluginConfig] = None, api: Optional[KubeAPI] = None,
-                 health_fn: Optional[Callable[[Topology], Dict[int, bool]]] = None, clock: Callable[[], float] = time.time):
+                 health_fn: Optional[Callable[[Topology], Dict[int, bool]]] = None, clock: Callable[[], float] = time.time,
+                 reprobe_fn: Optional[Callable[[], Optional[Topology]]] = None):
         self.cfg = config or PluginConfig()
         self.topology = topology
         self.api = api
         self.health_fn = health_fn
+        self.reprobe_fn = reprobe_fn
+        self.reprobes = 0  # completed re-measurements
+        self.republished = 0  # ... of which changed the published matrix
         self.clock = clock
         self._health: Dict[int, bool] = {g.index: bool(g.healthy) for g in topology.gpus}
         self._cond = threading.Condition()
@@ -120,6 +129,58 @@ class DevicePluginServer:
             self._version += 1
             self._cond.notify_all()
         self._publish_node()
+
+    # ------------------------------------------------------------------ link re-measurement
+    def node_idle(self) -> bool:
+        """No live pod on this node holds (or is assumed to hold) a device — the only time a probe may
+        run, since it saturates every xGMI link.  Unknown (no apiserver) counts as busy."""
+        if self.api is None or not self.cfg.node_name:
+            return False
+        try:
+            pods = [p for p in self.api.list_pods(node_name=self.cfg.node_name) if not pod_is_terminal(p)]
+        except Exception as e:
+            log.warning("listing pods on %s failed: %s", self.cfg.node_name, e)
+            return False
+        return all(PodAssignment.from_annotations(obj_annotations(p)) is None for p in pods)
+
+    @staticmethod
+    def link_change(old: Topology, new: Topology) -> float:
+        """Largest relative change of a measured pair between two probes (inf if the measured set differs)."""
+        import numpy as np
+
+        if old.bw_gbps is None or new.bw_gbps is None or old.n != new.n:
+            return float("inf")
+        a, b = old.bw_gbps, new.bw_gbps
+        fa, fb = np.isfinite(a), np.isfinite(b)
+        np.fill_diagonal(fa, False)
+        np.fill_diagonal(fb, False)
+        if (fa != fb).any():
+            return float("inf")
+        if not fa.any():
+            return 0.0
+        return float(np.max(np.abs(b[fa] - a[fa]) / np.maximum(a[fa], 1e-9)))
+
+    def reprobe(self) -> bool:
+        """One re-measurement (caller checked idleness); republish if the links moved.  -> republished."""
+        if self.reprobe_fn is None:
+            return False
+        new = self.reprobe_fn()
+        self.reprobes += 1
+        if new is None or new.n != self.topology.n:
+            log.warning("link re-probe produced no usable topology")
+            return False
+        delta = self.link_change(self.topology, new)
+        if delta <= self.cfg.reprobe_tolerance:
+            log.info("link re-probe: largest change %.1f%% (within tolerance)", 100 * delta)
+            return False
+        for g in new.gpus:  # health is the RAS monitor's call, not the probe's
+            g.healthy = self._health.get(g.index, True)
+        new.node_name = self.topology.node_name
+        log.warning("link re-probe: largest change %s; republishing the measured matrix",
+                    "in the measured set" if delta == float("inf") else f"{100 * delta:.1f}%")
+        self.update_topology(new)
+        self.republished += 1
+        return True
 
     # ------------------------------------------------------------------ node publication (A5, B7)
     def _publish_node(self) -> None:
@@ -343,8 +404,10 @@ class DevicePluginServer:
             t.start()
 
     def _monitor(self) -> None:
-        """Health polling + kubelet restart detection (the kubelet wipes plugin sockets on restart)."""
+        """Health polling, idle-time link re-probes, kubelet restart detection (the kubelet wipes
+        plugin sockets on restart)."""
         next_health = 0.0
+        next_probe = time.monotonic() + self.cfg.reprobe_interval
         while not self._stop.wait(0.2):
             if not os.path.exists(self.cfg.socket_path):
                 log.warning("plugin socket %s vanished (kubelet restart?): re-serving and re-registering", self.cfg.socket_path)
@@ -362,6 +425,13 @@ class DevicePluginServer:
                         self.set_health(int(idx), bool(ok))
                 except Exception as e:
                     log.warning("health check failed: %s", e)
+            if self.reprobe_fn is not None and self.cfg.reprobe_interval > 0 and time.monotonic() >= next_probe:
+                next_probe = time.monotonic() + self.cfg.reprobe_interval
+                try:
+                    if self.node_idle():
+                        self.reprobe()
+                except Exception as e:
+                    log.warning("link re-probe failed: %s", e)
 
     def stop(self) -> None:
         self._stop.set()

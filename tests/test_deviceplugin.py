@@ -187,3 +187,62 @@ def test_health_fn_polling(sockdir):
     finally:
         plugin.stop()
         kubelet.stop()
+
+
+def _measured(n=4, bw=60.0, degrade=None):
+    import numpy as np
+
+    t = fx.f7_mi355x(n=n)
+    m = np.full((t.n, t.n), bw)
+    np.fill_diagonal(m, np.nan)
+    if degrade:
+        i, j, f = degrade
+        m[i, j] = m[j, i] = bw * f
+    t.set_measured_bw(m, {"method": "p2p_read_lds", "preset": "quick"})
+    return t
+
+
+def test_reprobe_republishes_only_when_idle_and_changed():
+    """Idle-time link re-probe: a degraded pair measured while no pod holds a device
+    is republished on the node; a re-probe within tolerance or a busy node changes nothing."""
+    import json
+
+    api = FakeAPIServer()
+    api.create_node(make_node("n1"))
+    base = _measured()
+    results = [_measured(bw=61.0), _measured(degrade=(0, 3, 0.5))]
+    plug = DevicePluginServer(base, PluginConfig(node_name="n1", reprobe_tolerance=0.15), api=api,
+                              reprobe_fn=lambda: results.pop(0))
+    plug._publish_node()
+    assert plug.node_idle()
+    assert plug.reprobe() is False  # +1.7 %: within tolerance
+    assert plug.reprobe() is True  # pair (0,3) at half speed
+    topo = json.loads(api.get_node("n1")["metadata"]["annotations"][Contract().topology_key])
+    assert topo["bw_gbps"][0][3] == 30.0 and plug.republished == 1 and plug.reprobes == 2
+    # a pod holding devices makes the node busy: the monitor must not probe
+    api.create_pod(make_pod("busy", gpus=2, node="n1", annotations=PodAssignment.assumed((0, 1), 1).to_annotations()))
+    assert not plug.node_idle()
+    assert DevicePluginServer.link_change(base, _measured()) == 0.0
+
+
+def test_reprobe_runs_from_the_monitor_loop():
+    api = FakeAPIServer()
+    api.create_node(make_node("n2"))
+    calls = []
+
+    def fn():
+        calls.append(1)
+        return _measured(degrade=(1, 2, 0.3))
+
+    sockdir = tempfile.mkdtemp(prefix="gtkp", dir="/tmp")
+    plug = DevicePluginServer(_measured(), PluginConfig(node_name="n2", socket_dir=sockdir, reprobe_interval=0.3), api=api,
+                              reprobe_fn=fn)
+    try:
+        plug.start(register=False)
+        t0 = time.time()
+        while plug.republished == 0 and time.time() - t0 < 10:
+            time.sleep(0.1)
+        assert calls and plug.republished >= 1
+    finally:
+        plug.stop()
+        shutil.rmtree(sockdir, ignore_errors=True)
