@@ -84,10 +84,44 @@ def exp2_fragments(reps: int):
             "note": "fractional GPUs have no k8s extended-resource form; placement core only (MI355X: XCP partitions)"}
 
 
+def scale_prioritize(n_nodes: int, pods: int = 20, k: int = 4):
+    """kube-scheduler's sort fan-out on a large cluster: one pending k-GPU pod x every node, repeated
+    for `pods` same-size pods (no binds in between), extender called in process (no HTTP) so the
+    numbers are the extender's own cost.  Decision cache off vs on (the LRU of scheduler.py)."""
+    import time
+
+    from gpu_topology_on_k8s_amd.extender import ExtenderConfig, TopologyExtender
+    from gpu_topology_on_k8s_amd.k8s import Contract, FakeAPIServer
+    from gpu_topology_on_k8s_amd.k8s.annotations import encode_node_annotations
+    from gpu_topology_on_k8s_amd.k8s.objects import make_node, make_pod
+
+    api = FakeAPIServer()
+    c = Contract()
+    names = [f"node{i}" for i in range(n_nodes)]
+    for i, n in enumerate(names):
+        t = fx.f7_mi355x(76.5, 0.03, i)
+        api.create_node(make_node(n, labels={c.label_model: "MI355X"}, annotations=encode_node_annotations(t, c),
+                                  capacity={c.resource_name: "8"}))
+    out = {"experiment": f"scale-prioritize-{n_nodes}-nodes", "nodes": n_nodes, "request_gpus": k, "pods": pods}
+    for cache in (0, 4096):
+        ext = TopologyExtender(api, ExtenderConfig(resync_s=60.0, decision_cache=cache))
+        ms = []
+        for i in range(pods):
+            pod = api.create_pod(make_pod(f"p{cache}-{i}", gpus=k))
+            t0 = time.perf_counter()
+            ext.prioritize(pod, names)
+            ms.append((time.perf_counter() - t0) * 1e3)
+        key = "cache_on" if cache else "cache_off"
+        out[key] = {"first_ms": round(ms[0], 2), "steady_ms_mean": round(statistics.mean(ms[1:]), 2),
+                    "steady_us_per_node": round(1e3 * statistics.mean(ms[1:]) / n_nodes, 2)}
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--reps", type=int, default=500)
     ap.add_argument("--out", default="")
+    ap.add_argument("--scale-nodes", type=int, default=1024, help="cluster size of the sort fan-out experiment (0: skip)")
     a = ap.parse_args()
     random.seed(0)
     results = [
@@ -99,6 +133,8 @@ def main() -> int:
         run_exp("mi355x-exact-4gpu", 4, (), max(50, a.reps // 5), policy="exact", topo_fn=lambda: fx.f7_mi355x(76.5, 0.03, 1)),
         run_exp("mi355x-exact-1gpu-after-2", 1, (0, 1), max(50, a.reps // 5), policy="exact", topo_fn=lambda: fx.f7_mi355x(76.5, 0.03, 1)),
     ]
+    if a.scale_nodes:
+        results.append(scale_prioritize(a.scale_nodes))
     for r in results:
         print(json.dumps(r))
     if a.out:

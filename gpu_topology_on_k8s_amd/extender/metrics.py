@@ -25,6 +25,12 @@ class ExtenderMetrics:
         self.select_us = Histogram("gtk_extender_select_microseconds", "placement search time at bind",
                                    buckets=(10, 30, 100, 300, 1000, 3000, 1e4, 3e4, 1e5, 1e6), registry=self.registry)
 
+        self.decision_cache = Counter("gtk_extender_decision_cache_total", "placement decisions served from / added to the cache",
+                                      ["result"], registry=self.registry)
+
+    def cache(self, hit: bool) -> None:
+        self.decision_cache.labels(result="hit" if hit else "miss").inc()
+
     def observe(self, verb: str, seconds: float) -> None:
         self.latency.labels(verb).observe(seconds)
 

@@ -23,6 +23,7 @@ import logging
 import random
 import threading
 import time
+from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -56,6 +57,7 @@ class ExtenderConfig:
     require_model_match: bool = True
     bind_retries: int = 3
     seed: Optional[int] = None
+    decision_cache: int = 4096  # LRU entries; 0 disables (random tie-breaks are never cached)
 
 
 @dataclass
@@ -79,6 +81,11 @@ class TopologyExtender:
         self.metrics = metrics or ExtenderMetrics()
         self._rng = random.Random(self.cfg.seed)
         self._bind_lock = threading.Lock()
+        # Placement decisions are a pure function of (node topology object, used set, healthy set, k)
+        # under a deterministic policy: kube-scheduler asks sort for every pending pod x candidate
+        # node, and on a large cluster most nodes have not changed since the last pod of the same size.
+        self._cache: "OrderedDict[tuple, Tuple[Tuple[int, ...], float, float, Topology]]" = OrderedDict()
+        self._cache_lock = threading.Lock()
 
     # ------------------------------------------------------------------ helpers
     @property
@@ -102,6 +109,28 @@ class TopologyExtender:
             if have != want:
                 return False, f"pod wants GPU model {want}, node has {have or 'unknown'}"
         return True, ""
+
+    def _cacheable(self) -> bool:
+        return self.cfg.decision_cache > 0 and self.cfg.policy.tie_break != "random"
+
+    def _choose_cached(self, t: Topology, used: Sequence[int], k: int) -> Tuple[Tuple[int, ...], float, float]:
+        if not self._cacheable():
+            return self._choose(t, used, k)
+        # the Topology object is replaced whenever the node annotation changes (new resourceVersion)
+        key = (id(t), tuple(used), tuple(g.healthy for g in t.gpus), k, self.cfg.policy_name)
+        with self._cache_lock:
+            hit = self._cache.get(key)
+            if hit is not None and hit[3] is t:
+                self._cache.move_to_end(key)
+                self.metrics.cache(True)
+                return hit[:3]
+        res = self._choose(t, used, k)  # NoFeasiblePlacement propagates uncached
+        with self._cache_lock:
+            self._cache[key] = res + (t,)  # keeps t alive, so id(t) cannot be reused while cached
+            while len(self._cache) > self.cfg.decision_cache:
+                self._cache.popitem(last=False)
+        self.metrics.cache(False)
+        return res
 
     def _choose(self, t: Topology, used: Sequence[int], k: int) -> Tuple[Tuple[int, ...], float, float]:
         """(ids, score 0..10, objective) under the configured policy; raises NoFeasiblePlacement."""
@@ -141,7 +170,7 @@ class TopologyExtender:
                 return None, f"insufficient free devices: need {k}, free {st.free_count(now, self.cfg.assume_ttl)}"
             t0 = time.perf_counter()
             try:
-                ids, score, obj = self._choose(st.topology, used, k)
+                ids, score, obj = self._choose_cached(st.topology, used, k)
             except NoFeasiblePlacement as e:
                 return None, str(e)
             us = (time.perf_counter() - t0) * 1e6

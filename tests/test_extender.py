@@ -297,3 +297,25 @@ def test_prioritize_over_many_nodes_uses_constant_api_calls():
     before = sum(api.calls.values())
     ext.prioritize(pod, list(names))  # fresh cache: no API traffic at all
     assert sum(api.calls.values()) == before
+
+
+def test_decision_cache_hits_and_invalidates():
+    """Repeated sort calls for same-size pods on unchanged nodes are served from the LRU cache; a bind
+    (new used set) misses and still yields a disjoint, correct set; random tie-breaks never cache."""
+    api, ext, _ = _cluster(nodes=("n1", "n2"))
+    p1, p2 = _submit(api, "a", 4), _submit(api, "b", 4)
+    first = ext.prioritize(p1, ["n1", "n2"])
+    assert ext.prioritize(p2, ["n1", "n2"]) == first
+    assert ext.metrics.decision_cache.labels(result="hit")._value.get() >= 2
+    d1 = _bind(api, ext, "a")  # bind re-evaluates: cached decision for (n1, {}, 4)
+    d2 = _bind(api, ext, "b")  # used set changed -> miss -> the other half
+    assert not set(d1.ids) & set(d2.ids)
+    p3 = _submit(api, "c", 4)
+    cached = ext.prioritize(p3, ["n1", "n2"])
+    ext.cfg.decision_cache = 0  # same extender state, cache off: same answer
+    assert cached == ext.prioritize(p3, ["n1", "n2"]) and cached[0][1] == 0  # n1 is full now
+
+    from gpu_topology_on_k8s_amd.placement import PlacementPolicy
+
+    _, rnd, _ = _cluster(policy=PlacementPolicy(tie_break="random"))
+    assert not rnd._cacheable()
