@@ -17,6 +17,7 @@ import sys
 import threading
 
 from ..k8s.annotations import Contract
+from ..placement import PlacementPolicy
 from ..topology.discovery import discover
 from .health import HealthMonitor
 from .plugin import DevicePluginServer, PluginConfig
@@ -53,6 +54,8 @@ def main(argv=None) -> int:
                     help="re-measure the links (child process) every N s while no pod holds a device; 0 = never")
     ap.add_argument("--reprobe-tolerance", type=float, default=0.15,
                     help="republish the topology when a measured pair moved by more than this fraction")
+    ap.add_argument("--partition-aware", default="on", choices=["on", "off"],
+                    help="GetPreferredAllocation on CPX/DPX/QPX nodes: group XCPs by physical GPU (on) or not (off)")
     ap.add_argument("--log-level", default="INFO")
     a = ap.parse_args(argv)
     logging.basicConfig(level=a.log_level, format='{"ts":"%(asctime)s","lvl":"%(levelname)s","mod":"%(name)s","msg":"%(message)s"}')
@@ -78,7 +81,8 @@ def main(argv=None) -> int:
     cfg = PluginConfig(resource_name=a.resource_name, socket_dir=a.socket_dir, socket_name=a.socket_name, dev_root=a.dev_root,
                        node_name=a.node_name, contract=Contract(resource_name=a.resource_name, prefix=a.annotation_prefix),
                        health_interval=a.health_interval, reprobe_interval=a.reprobe_interval,
-                       reprobe_tolerance=a.reprobe_tolerance)
+                       reprobe_tolerance=a.reprobe_tolerance,
+                       policy=PlacementPolicy(partition_aware=a.partition_aware == "on"))
     reprobe = None
     if a.reprobe_interval > 0 and a.discovery != "fake":
         from ..ops.probe import probe_in_child

@@ -27,6 +27,8 @@ def main(argv=None) -> int:
     ap.add_argument("--policy", default="exact", choices=["exact", "gaia", "design"])
     ap.add_argument("--tie-break", default="first", choices=["first", "random"])
     ap.add_argument("--assume-ttl", type=float, default=300.0)
+    ap.add_argument("--partition-aware", default="on", choices=["on", "off"],
+                    help="CPX/DPX/QPX nodes: group XCPs by physical GPU (on) or treat each as a stand-alone GPU (off)")
     ap.add_argument("--resync", type=float, default=5.0)
     ap.add_argument("--apiserver", default="")
     ap.add_argument("--token", default="")
@@ -37,7 +39,7 @@ def main(argv=None) -> int:
 
     api = RestKubeAPI(a.apiserver, token=a.token or None, verify=False) if a.apiserver else RestKubeAPI.in_cluster()
     cfg = ExtenderConfig(contract=Contract(resource_name=a.resource_name, prefix=a.annotation_prefix), policy_name=a.policy,
-                         policy=PlacementPolicy(tie_break=a.tie_break), assume_ttl=a.assume_ttl, resync_s=a.resync)
+                         policy=PlacementPolicy(tie_break=a.tie_break, partition_aware=a.partition_aware == "on"), assume_ttl=a.assume_ttl, resync_s=a.resync)
     run(TopologyExtender(api, cfg), a.host, a.port, a.url_prefix, resync_period=a.resync)
     return 0
 

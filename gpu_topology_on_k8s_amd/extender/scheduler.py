@@ -153,7 +153,7 @@ class TopologyExtender:
             raise NoFeasiblePlacement(f"{name}: no {k}-device placement")
         from ..placement.core import Problem, evaluate, score_from_objective
 
-        j, _ = evaluate(Problem.from_topology(t, used), ids, self.cfg.policy)
+        j, _ = evaluate(Problem.from_topology(t, used, partition_aware=self.cfg.policy.partition_aware), ids, self.cfg.policy)
         return tuple(sorted(int(i) for i in ids)), score_from_objective(j), j
 
     def _node_eval(self, pod: Dict[str, Any], name: str, node_obj: Optional[dict], k: int) -> Tuple[Optional[Decision], str]:

@@ -57,11 +57,16 @@ class PlacementPolicy:
     tie_break: str = "first"  # "first" (deterministic, lowest ids) | "random"
     exact_limit: int = 200_000  # Python path: max subsets enumerated exactly; above -> greedy + local search
     node_limit: int = 2_000_000  # native path: branch-and-bound node budget; above -> greedy + local search
+    # CPX/DPX/QPX nodes: treat the XCPs of one physical GPU as a group (pack multi-XCP requests onto
+    # one package, keep whole packages pristine) and keep their cheap on-package links.  False =
+    # every device is a stand-alone GPU behind xGMI (A/B baseline; SURVEY.md §5.6 --partition-aware)
+    partition_aware: bool = True
 
     def to_dict(self) -> Dict[str, object]:
         return dict(
             w_span=self.w_span, w_frag=self.w_frag, w_fit=self.w_fit, w_access=self.w_access,
             tie_break=self.tie_break, exact_limit=self.exact_limit, node_limit=self.node_limit,
+            partition_aware=self.partition_aware,
         )
 
     @classmethod
@@ -94,7 +99,8 @@ class Problem:
     access: np.ndarray  # float[n]
 
     @classmethod
-    def from_topology(cls, topo: Topology, used: Sequence[int] = (), access: Optional[Sequence[float]] = None) -> "Problem":
+    def from_topology(cls, topo: Topology, used: Sequence[int] = (), access: Optional[Sequence[float]] = None,
+                      partition_aware: bool = True) -> "Problem":
         n = topo.n
         free = topo.healthy_mask().copy()
         for u in used:
@@ -102,11 +108,19 @@ class Problem:
                 free[int(u)] = False
         levels = []
         phys = topo.physical
-        if len(set(phys.tolist())) < n:  # partitioned: XCP -> physical GPU level is meaningful
+        cost = np.asarray(topo.cost, dtype=np.float64)
+        partitioned = len(set(phys.tolist())) < n
+        if partitioned and partition_aware:  # XCP -> physical GPU level is meaningful
             levels.append(phys)
+        elif partitioned:  # partition-blind: on-package pairs priced like the node's xGMI pairs
+            same = (phys[:, None] == phys[None, :]) & ~np.eye(n, dtype=bool)
+            cross = ~(phys[:, None] == phys[None, :])
+            if cross.any():
+                cost = cost.copy()
+                cost[same] = float(np.median(cost[cross]))
         levels.append(topo.numa)
         acc = np.zeros(n) if access is None else np.asarray(access, dtype=np.float64)
-        return cls(cost=np.asarray(topo.cost, dtype=np.float64), free=free, levels=levels, access=acc)
+        return cls(cost=cost, free=free, levels=levels, access=acc)
 
     @property
     def n(self) -> int:
@@ -242,7 +256,8 @@ def select(
     enumeration below, ``auto`` = native when built (deterministic tie-break only; random
     tie-breaking needs the full tie list, which only the Python path collects).
     """
-    p = topo_or_problem if isinstance(topo_or_problem, Problem) else Problem.from_topology(topo_or_problem, used, access)
+    p = (topo_or_problem if isinstance(topo_or_problem, Problem)
+         else Problem.from_topology(topo_or_problem, used, access, partition_aware=policy.partition_aware))
     if k <= 0:
         raise ValueError("k must be >= 1")
     free_ids = [i for i in range(p.n) if p.free[i]]
@@ -284,7 +299,7 @@ def select(
 
 def worst(topo: Topology, k: int, used: Sequence[int] = (), policy: PlacementPolicy = PlacementPolicy()) -> Placement:
     """Highest-objective subset (the "worst-topology placement" of BASELINE config 5)."""
-    p = Problem.from_topology(topo, used)
+    p = Problem.from_topology(topo, used, partition_aware=policy.partition_aware)
     stats = _level_stats(p)
     free_ids = [i for i in range(p.n) if p.free[i]]
     if len(free_ids) < k:
@@ -311,7 +326,7 @@ def select_with(topo: Topology, k: int, available: Sequence[int], must_include: 
     used = [i for i in range(topo.n) if i not in set(avail)]
     if not must:
         return select(topo, k, used=used, policy=policy).ids
-    p = Problem.from_topology(topo, used)
+    p = Problem.from_topology(topo, used, partition_aware=policy.partition_aware)
     rest = [a for a in avail if a not in set(must) and p.free[a]]
     r = k - len(must)
     stats = _level_stats(p)

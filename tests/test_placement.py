@@ -223,3 +223,21 @@ def test_design_farthest_single():
     i = design_farthest_single(t.cost, [])
     assert i is not None and 0 <= i < 8
     assert design_farthest_single(t.cost, list(range(8))) is None
+
+
+def test_partition_aware_switch_on_cpx_node():
+    """--partition-aware: with XCP grouping a 2-XCP request lands on one package (cheap
+    on-package links); partition-blind treats every XCP as a stand-alone xGMI device."""
+    from gpu_topology_on_k8s_amd.placement import PlacementPolicy, select
+    from gpu_topology_on_k8s_amd.placement.core import Problem
+    from gpu_topology_on_k8s_amd.topology.model import Topology
+
+    t = Topology.full_mesh(n=2, partitions_per_gpu=4, numa_split=1)  # 2 GPUs x 4 XCPs
+    aware = select(t, 2, used=[1, 2, 3], policy=PlacementPolicy(partition_aware=True))
+    assert t.physical[list(aware.ids)].tolist() == [1, 1]
+    blind_p = Problem.from_topology(t, [1, 2, 3], partition_aware=False)
+    same = t.physical[:, None] == t.physical[None, :]
+    off = ~np.eye(t.n, dtype=bool)
+    assert np.allclose(blind_p.cost[same & off], blind_p.cost[~same].mean())  # on-package pairs priced as xGMI
+    assert len(blind_p.levels) == 1  # NUMA only, no package level
+    assert PlacementPolicy.from_dict(PlacementPolicy(partition_aware=False).to_dict()).partition_aware is False
