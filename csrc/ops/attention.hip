@@ -294,6 +294,16 @@ __device__ __forceinline__ float max3(float a, float b, float c) {
   return r;
 }
 
+// Running-max slack (log2 units, guide T13): the max used for the exponent is only raised when a
+// row's max exceeds it by more than kMaxSlack, so P <= 2^kMaxSlack (exact after the final 1/l) and
+// the O rescale, 64 multiplies per wave, runs on a few early tiles instead of on most tiles.
+constexpr float kMaxSlack = 8.f;
+
+__device__ __forceinline__ float xhalf_max(float x) {  // max(x[lane], x[lane ^ 32])
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+}
+
 __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
                                                            const u16* __restrict__ v, u16* __restrict__ o,
                                                            float* __restrict__ lse2, int H, int Hkv, int S, float c) {
@@ -360,8 +370,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict
     float mx = max3(s0[0], s1[0], s0[1]);
 #pragma unroll
     for (int i = 1; i < 16; ++i) mx = max3(mx, s1[i], i + 1 < 16 ? s0[i + 1] : s1[i]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mnew = fmaxf(m, mx * c);
+    const float mrow = xhalf_max(mx) * c;
+    // per row (a row's frame must depend on its own visible scores only: causality is bitwise);
+    // the wave-uniform `resc` only gates the rescale branch, alpha == 1 exactly on unmoved rows
+    const float mnew = mrow > m + kMaxSlack ? mrow : m;
+    const bool resc = __any(mnew != m);
     float rs = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -370,7 +383,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict
       rs += s0[i] + s1[i];
     }
     rs += __shfl_xor(rs, 32, 64);
-    if (__any(mnew > m)) {  // exact skip: no row max moved => alpha == 1 everywhere
+    if (resc) {  // alpha == 1 everywhere otherwise
       const float alpha = fexp2(m - mnew);
       l *= alpha;
 #pragma unroll

@@ -95,6 +95,30 @@ def test_attention_bwd_v4_matches_v3(fused, B, H, Hkv, S):
         assert torch.equal(a, b), (name, _rel(a, b))
 
 
+@pytest.mark.parametrize("B,H,Hkv,S", [(2, 8, 2, 768), (1, 4, 4, 128), (1, 2, 2, 640)])
+@pytest.mark.parametrize("spike", [False, True])
+def test_attention_forward_max_slack(fused, B, H, Hkv, S, spike):
+    """The forward raises its running max only past a slack (P <= 2^8 before 1/l).  `spike` plants
+    large keys late in the sequence so the max jumps after many tiles and the O/l rescale path runs
+    mid-sequence; outputs and log-sum-exp must stay exact against fp32 and the v1 kernel (which
+    rescales on every increase)."""
+    torch.manual_seed(6)
+    q = torch.randn(B, H, S, 128, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
+    if spike:
+        k[:, :, S // 2 :: 97] *= 8
+        k[:, :, S - 70] = q[:, 0, S - 1].unsqueeze(1) * 4
+    hip = fused.hip()
+    o2, l2 = hip.attn_fwd(q, k, v, 128 ** -0.5)
+    o1, l1 = hip.attn_fwd_v1(q, k, v, 128 ** -0.5)
+    ref = fused.attention_ref(q, k, v)
+    assert torch.isfinite(o2).all() and torch.isfinite(l2).all()
+    assert _rel(o2, ref) < 1e-2, _rel(o2, ref)
+    assert _rel(o2, o1) < 5e-3, _rel(o2, o1)
+    assert torch.allclose(l2, l1, atol=1e-3, rtol=1e-5), (l2 - l1).abs().max().item()
+
+
 def test_attention_causality(fused):
     """Changing future keys/values must not change earlier outputs."""
     torch.manual_seed(2)
