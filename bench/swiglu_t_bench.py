@@ -40,6 +40,12 @@ def main():
         "transpose_dgu_ms": timeit(lambda: hip.transpose_bf16(dgu)),
         "swiglu_bwd_t_ms": timeit(lambda: hip.swiglu_bwd_t(dh, gu)),
     }
+    for name, (r, c) in {"x": (T, 4096), "ffn": (T, F), "gu": (T, 2 * F), "wqkv": (T, 6144)}.items():
+        x = torch.randn(r, c, device="cuda", dtype=torch.bfloat16)
+        ms = timeit(lambda: hip.transpose_bf16(x))
+        out[f"transpose_{name}_ms"] = ms
+        out[f"transpose_{name}_tbps"] = 2 * r * c * 2 / 1e9 / ms
+        del x
     gb = (3 * T * F * 2 + 2 * T * F * 2) / 1e9  # read gu + dh, write dgu
     out["swiglu_bwd_tbps"] = gb / out["swiglu_bwd_ms"]
     out["swiglu_bwd_t_tbps"] = (gb + 2 * T * F * 2 / 1e9) / out["swiglu_bwd_t_ms"]

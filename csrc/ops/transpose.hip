@@ -15,7 +15,8 @@
 //          them into 16 B and writes out[c][8p..8p+7].  In one instruction a wave's lanes take 8
 //          columns x 8 row-groups; the swizzle puts the 8 row-groups on 8 different 16-B slots, so
 //          the 64 lanes touch 32 distinct banks (lane pairs share a dword): no conflicts.
-// R and C must be multiples of 64 (all Llama-3 dims are); other shapes take torch's copy.
+// R and C must be multiples of 64; multiples of 128 (all Llama-3 dims) take the 128x128 kernel below.
+// Other shapes take torch's copy.
 #include <hip/hip_runtime.h>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
@@ -52,6 +53,46 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const u16* __restri
   }
 }
 
+// 128x128 tile per 256-thread block (the path for every Llama-3 shape: all dims are multiples of
+// 128).  The 64x64 tile reads 128-B row segments and keeps only 2 x 16 B per thread in flight, so it
+// is latency bound at ~4.2 TB/s (profiles/r01_xpose).  Here each thread issues 8 independent 16-B
+// loads before touching LDS, input row segments are 256 B and output row segments 256 B.
+//   LDS  : [128 rows][16 vectors], vector v of row r at slot v ^ ((r>>3)&15): 32 KiB.
+//   store: output row c (input column), vector p = input rows 8p..8p+7.  16 lanes write one 256-B
+//          output row segment, a wave 4 of them.  ds_read_u16 banks like ds_read_b32 (two groups
+//          of 32 lanes, dword mod 32), so the lanes are ordered to give each 32-lane group 8 p
+//          values x 4 columns: slots (c>>3) ^ p are 8 distinct 4-dword groups, the 4 columns two
+//          dwords of each (lane pairs share one): no bank conflicts.
+constexpr int kBig = 128;
+
+__global__ __launch_bounds__(256) void transpose128_bf16_kernel(const u16* __restrict__ x, u16* __restrict__ y, int R,
+                                                                int C) {
+  __shared__ u16x8 tile[kBig][16];
+  const int t = threadIdx.x;
+  const size_t r0 = (size_t)blockIdx.y * kBig, c0 = (size_t)blockIdx.x * kBig;
+  const int v = t & 15;
+  u16x8 in[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) in[i] = *reinterpret_cast<const u16x8*>(x + (r0 + (t >> 4) + 16 * i) * C + c0 + 8 * v);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = (t >> 4) + 16 * i;
+    tile[r][v ^ ((r >> 3) & 15)] = in[i];
+  }
+  __syncthreads();
+  const u16* lds = reinterpret_cast<const u16*>(&tile[0][0]);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int idx = t + 256 * i, lane = idx & 63;
+    const int c = 4 * (idx >> 6) + ((lane >> 3) & 3), p = (lane & 7) + 8 * (lane >> 5);
+    const int slot = (c >> 3) ^ p;
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = lds[(8 * p + j) * kBig + slot * 8 + (c & 7)];
+    *reinterpret_cast<u16x8*>(y + (c0 + c) * R + r0 + 8 * p) = o;
+  }
+}
+
 at::Tensor transpose_bf16(const at::Tensor& x) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 2,
               "transpose_bf16: x must be a contiguous 2-D bf16 GPU tensor");
@@ -60,6 +101,12 @@ at::Tensor transpose_bf16(const at::Tensor& x) {
   TORCH_CHECK(R / kTile <= 65535, "transpose_bf16: too many rows for the grid");
   auto y = at::empty({C, R}, x.options());
   if (R == 0 || C == 0) return y;
+  if (R % kBig == 0 && C % kBig == 0) {
+    hipLaunchKernelGGL(transpose128_bf16_kernel, dim3((unsigned)(C / kBig), (unsigned)(R / kBig)), dim3(256), 0,
+                       at::hip::getCurrentHIPStream().stream(), reinterpret_cast<const u16*>(x.data_ptr()),
+                       reinterpret_cast<u16*>(y.data_ptr()), (int)R, (int)C);
+    return y;
+  }
   hipLaunchKernelGGL(transpose_bf16_kernel, dim3((unsigned)(C / kTile), (unsigned)(R / kTile)), dim3(256), 0,
                      at::hip::getCurrentHIPStream().stream(), reinterpret_cast<const u16*>(x.data_ptr()),
                      reinterpret_cast<u16*>(y.data_ptr()), (int)R, (int)C);

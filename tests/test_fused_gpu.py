@@ -135,14 +135,14 @@ def test_adamw_and_sqnorm(hip):
     assert math.isclose(sq.item(), g.float().pow(2).sum().item(), rel_tol=1e-4)
 
 
-@pytest.mark.parametrize("R,C", [(64, 64), (128, 4096), (4096, 192), (16384, 6144), (640, 128256)])
+@pytest.mark.parametrize("R,C", [(64, 64), (128, 4096), (4096, 192), (192, 384), (16384, 6144), (640, 128256)])
 def test_transpose_kernel_exact(hip, R, C):
     x = torch.randn(R, C, device="cuda", dtype=torch.bfloat16)
     y = hip.transpose_bf16(x)
     assert y.shape == (C, R) and torch.equal(y, x.t().contiguous())
 
 
-@pytest.mark.parametrize("T,F", [(64, 64), (256, 14336), (4096, 192)])
+@pytest.mark.parametrize("T,F", [(64, 64), (192, 128), (256, 14336), (4096, 192), (64, 384), (16384, 256)])
 def test_swiglu_bwd_t_matches_bwd_and_transpose(hip, T, F):
     gu = torch.randn(T, 2 * F, device="cuda", dtype=torch.bfloat16)
     dh = torch.randn(T, F, device="cuda", dtype=torch.bfloat16)
