@@ -338,6 +338,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict
     char* vimg = kimg + BK * D * 2;
     const int key0 = kt * BK;
     f32x16 s0 = f32x16{}, s1 = f32x16{};
+    __builtin_amdgcn_s_setprio(1);  // MFMA phases outrank the other wave's softmax VALU (ping-pong)
     {
       bf16x8 kf0[8], kf1[8];
 #pragma unroll
@@ -358,6 +359,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict
       }
       __builtin_amdgcn_sched_group_barrier(0x8, 8, 0);
     }
+    __builtin_amdgcn_s_setprio(0);
     if (kt + 1 < ntiles) gload(kt + 1, smem + ((kt + 1) & 1) * (2 * BK * D * 2));  // lands under softmax + PV
     if (masked) {
 #pragma unroll
@@ -394,6 +396,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict
     l += rs;
     m = mnew;
     const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 8), p10 = pack8(s1, 0), p11 = pack8(s1, 8);
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       const int col0 = 32 * dt;
@@ -402,6 +405,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict
       oacc[dt] = mfma(tr_frag(vimg, lane, 32 + 4 * hh, 40 + 4 * hh, col0), p10, oacc[dt]);
       oacc[dt] = mfma(tr_frag(vimg, lane, 48 + 4 * hh, 56 + 4 * hh, col0), p11, oacc[dt]);
     }
+    __builtin_amdgcn_s_setprio(0);
   };
   gload(0, smem);
   dma_sync();
@@ -1121,6 +1125,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(const u16* __restr
     char* vimg = kimg + BK * D * 2;
     const int key0 = kt * BK;
     f32x16 s0 = f32x16{}, s1 = f32x16{}, e0 = f32x16{}, e1 = f32x16{};
+    __builtin_amdgcn_s_setprio(1);  // MFMA phases outrank the other wave's VALU phase (ping-pong)
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const bf16x8 k0 = lds_b128(kimg, swz(r, 2 * s + hh)), k1 = lds_b128(kimg, swz(32 + r, 2 * s + hh));
@@ -1130,6 +1135,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(const u16* __restr
       e0 = mfma(v0, df[s], e0);
       e1 = mfma(v1, df[s], e1);
     }
+    __builtin_amdgcn_s_setprio(0);
     if (kt + 1 < ntiles) stage.load(kt + 1, smem + ((kt + 1) & 1) * (2 * BK * D * 2));  // lands under the dQ MFMAs
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -1144,6 +1150,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(const u16* __restr
       s1[i] = p1 * (e1[i] - del_q);
     }
     const bf16x8 d00 = pack8(s0, 0), d01 = pack8(s0, 8), d10 = pack8(s1, 0), d11 = pack8(s1, 8);
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       dqt[dt] = mfma(tr_frag(kimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), d00, dqt[dt]);
@@ -1151,6 +1158,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(const u16* __restr
       dqt[dt] = mfma(tr_frag(kimg, lane, 32 + 4 * hh, 40 + 4 * hh, 32 * dt), d10, dqt[dt]);
       dqt[dt] = mfma(tr_frag(kimg, lane, 48 + 4 * hh, 56 + 4 * hh, 32 * dt), d11, dqt[dt]);
     }
+    __builtin_amdgcn_s_setprio(0);
   };
 
   stage.load(0, smem);
