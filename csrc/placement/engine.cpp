@@ -125,7 +125,7 @@ void Engine::greedy(int k, const std::vector<int>& F, std::vector<int>* best, do
   }
 }
 
-Result Engine::select(int k, uint64_t node_limit) const {
+Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_ties) const {
   Result res;
   if (k <= 0) throw std::invalid_argument("k must be >= 1");
   const int n = p_.n;
@@ -167,6 +167,7 @@ Result Engine::select(int k, uint64_t node_limit) const {
 
   double best_j = std::numeric_limits<double>::infinity();
   std::vector<int> best_pos;
+  std::vector<std::vector<int>> tie_pos;
   uint64_t nodes = 0, leaves = 0;
   bool aborted = false;
 
@@ -198,7 +199,7 @@ Result Engine::select(int k, uint64_t node_limit) const {
   // Large search spaces: seed the incumbent with greedy + 1-swap so pruning bites from the start.
   // (Ties then resolve to the greedy set rather than the lexicographically first optimum.)
   double log_comb = std::lgamma(m + 1.0) - std::lgamma(k + 1.0) - std::lgamma(m - k + 1.0);
-  if (log_comb > std::log(2.0e5)) {
+  if (log_comb > std::log(2.0e5)) {  // (with collect_ties the DFS re-finds the seed and lists it)
     std::vector<int> g;
     double gj = std::numeric_limits<double>::infinity();
     greedy(k, F, &g, &gj);
@@ -215,6 +216,9 @@ Result Engine::select(int k, uint64_t node_limit) const {
       if (j < best_j - kEps) {
         best_j = j;
         best_pos = chosen;
+        if (collect_ties) tie_pos.assign(1, chosen);
+      } else if (collect_ties && j <= best_j + kEps && tie_pos.size() < max_ties) {
+        tie_pos.push_back(chosen);
       }
       return;
     }
@@ -238,7 +242,7 @@ Result Engine::select(int k, uint64_t node_limit) const {
       double span_lb = 0;
       for (size_t l = 0; l < lv_.size(); ++l) span_lb += std::max(0, touched[l] - mg[l]);
       double lb = comm_lb + pol_.w_span * span_lb + pol_.w_access * ((accsum + r * amin) / k);
-      if (lb >= best_j - kEps) return;
+      if (collect_ties ? lb > best_j + kEps : lb >= best_j - kEps) return;
     }
     for (int c = start; c <= m - r; ++c) {
       const int dev = F[c];
@@ -277,6 +281,17 @@ Result Engine::select(int k, uint64_t node_limit) const {
   res.ids = ids;
   res.objective = evaluate(ids, &res.terms);
   res.feasible = true;
+  if (collect_ties) {
+    if (aborted || tie_pos.empty()) {
+      res.ties.assign(1, ids);
+    } else {
+      for (const auto& t : tie_pos) {
+        std::vector<int> s;
+        for (int pos : t) s.push_back(F[pos]);
+        res.ties.push_back(std::move(s));
+      }
+    }
+  }
   res.nodes = nodes;
   res.leaves = leaves;
   return res;

@@ -50,6 +50,9 @@ struct Result {
   bool feasible = false;
   uint64_t nodes = 0;     // search-tree nodes expanded
   uint64_t leaves = 0;    // complete subsets evaluated
+  // select(collect_ties=true): every subset within kEps of the optimum, in lexicographic order (what
+  // a random tie-break draws from: Gaia Table I splits 1-GPU requests between equal cousins).
+  std::vector<std::vector<int>> ties;
 };
 
 class Engine {
@@ -58,7 +61,9 @@ class Engine {
 
   // Exact (branch and bound) unless more than `node_limit` nodes are needed, in which case the
   // best set found by greedy growth + 1-swap descent is returned with exact=false.
-  Result select(int k, uint64_t node_limit) const;
+  // With `collect_ties` the bound prunes only strictly worse branches and the optima (at most
+  // `max_ties`) come back in Result::ties.
+  Result select(int k, uint64_t node_limit, bool collect_ties = false, size_t max_ties = 65536) const;
   // Highest-objective subset (exhaustive; intended for n <= ~24) — "worst placement" baseline.
   Result worst(int k) const;
   // Objective of an arbitrary set.

@@ -73,7 +73,7 @@ PYBIND11_MODULE(_placement, m) {
       [](py::array_t<double, py::array::c_style | py::array::forcecast> cost,
          py::array_t<bool, py::array::c_style | py::array::forcecast> free_mask, const std::vector<std::vector<int>>& levels,
          py::array_t<double, py::array::c_style | py::array::forcecast> access, int k, double w_span, double w_frag,
-         double w_fit, double w_access, uint64_t node_limit) {
+         double w_fit, double w_access, uint64_t node_limit, bool collect_ties) {
         Problem p = make_problem(cost, free_mask, levels, access);
         Result r;
         double us = 0;
@@ -81,14 +81,16 @@ PYBIND11_MODULE(_placement, m) {
           py::gil_scoped_release nogil;
           auto t0 = std::chrono::steady_clock::now();
           Engine e(p, make_policy(w_span, w_frag, w_fit, w_access));
-          r = e.select(k, node_limit);
+          r = e.select(k, node_limit, collect_ties);
           us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
         }
-        return to_dict(r, us);
+        py::dict d = to_dict(r, us);
+        if (collect_ties) d["ties"] = r.ties;
+        return d;
       },
       py::arg("cost"), py::arg("free"), py::arg("levels"), py::arg("access"), py::arg("k"), py::arg("w_span") = 0.5,
       py::arg("w_frag") = 0.25, py::arg("w_fit") = 0.05, py::arg("w_access") = 0.1,
-      py::arg("node_limit") = (uint64_t)2000000);
+      py::arg("node_limit") = (uint64_t)2000000, py::arg("collect_ties") = false);
   m.def(
       "worst",
       [](py::array_t<double, py::array::c_style | py::array::forcecast> cost,

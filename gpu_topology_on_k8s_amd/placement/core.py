@@ -226,14 +226,20 @@ def _native_engine():
         return None
 
 
-def _select_native(mod, p: Problem, k: int, policy: PlacementPolicy) -> Placement:
-    r = mod.select(
-        np.ascontiguousarray(p.cost, dtype=np.float64), np.ascontiguousarray(p.free, dtype=bool),
-        [lv.astype(np.int64).tolist() for lv in p.levels], np.ascontiguousarray(p.access, dtype=np.float64), int(k),
-        policy.w_span, policy.w_frag, policy.w_fit, policy.w_access, int(policy.node_limit),
-    )
+def _select_native(mod, p: Problem, k: int, policy: PlacementPolicy, rng: Optional[random.Random] = None) -> Placement:
+    args = (np.ascontiguousarray(p.cost, dtype=np.float64), np.ascontiguousarray(p.free, dtype=bool),
+            [lv.astype(np.int64).tolist() for lv in p.levels], np.ascontiguousarray(p.access, dtype=np.float64))
+    w = (policy.w_span, policy.w_frag, policy.w_fit, policy.w_access)
+    ties = policy.tie_break == "random"
+    r = mod.select(*args, int(k), *w, int(policy.node_limit), ties)
     if not r["feasible"]:
         raise NoFeasiblePlacement(f"need {k} free devices")
+    if ties and len(r["ties"]) > 1:
+        # same draw as the Python enumeration: lexicographic tie list, one rng.choice
+        pick = list((rng or random).choice(r["ties"]))
+        if pick != list(r["ids"]):
+            e = mod.evaluate(*args, pick, *w)
+            r = dict(r, ids=pick, objective=e["objective"], terms=e["terms"])
     terms = dict(r["terms"])
     terms["search_nodes"] = float(r["nodes"])
     terms["search_us"] = float(r["micros"])
@@ -253,8 +259,9 @@ def select(
     """Choose ``k`` free devices minimising :func:`evaluate`'s objective.
 
     ``engine``: ``native`` = C++ branch-and-bound (``csrc/placement/engine.cpp``), ``python`` = the
-    enumeration below, ``auto`` = native when built (deterministic tie-break only; random
-    tie-breaking needs the full tie list, which only the Python path collects).
+    enumeration below, ``auto`` = native when built.  A random tie-break asks the engine for the
+    full lexicographic tie list (ties are pruned only when strictly worse) and draws from it exactly
+    as the enumeration does, so both engines return the same set for the same rng state.
     """
     p = (topo_or_problem if isinstance(topo_or_problem, Problem)
          else Problem.from_topology(topo_or_problem, used, access, partition_aware=policy.partition_aware))
@@ -265,10 +272,10 @@ def select(
         raise NoFeasiblePlacement(f"need {k} free devices, have {len(free_ids)}")
     if engine not in ("auto", "native", "python"):
         raise ValueError(engine)
-    if engine != "python" and policy.tie_break != "random":
+    if engine != "python":
         mod = _native_engine()
         if mod is not None:
-            return _select_native(mod, p, k, policy)
+            return _select_native(mod, p, k, policy, rng)
         if engine == "native":
             from .._native import load
 

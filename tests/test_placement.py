@@ -75,6 +75,44 @@ def test_native_engine_matches_python(n, seed):
 
 
 @needs_native
+@settings(max_examples=60, deadline=None)
+@given(st.integers(min_value=2, max_value=10), st.integers(min_value=0, max_value=2**31 - 1))
+def test_native_random_tie_break_matches_python(n, seed):
+    """Random tie-break on the native engine: same tie list, same draw as the Python enumeration.
+    Costs are quantised to a few classes so most requests have many optima (the mesh case)."""
+    rng = np.random.default_rng(seed)
+    p = _random_problem(rng, n)
+    c = np.triu(rng.integers(1, 3, size=(n, n)).astype(float), 1)
+    p = Problem(cost=c + c.T, free=p.free, levels=p.levels, access=np.zeros(n))
+    pol = PlacementPolicy(tie_break="random")
+    for k in range(1, int(p.free.sum()) + 1):
+        a = select(p, k, policy=pol, rng=random.Random(seed + k), engine="native")
+        b = select(p, k, policy=pol, rng=random.Random(seed + k), engine="python")
+        assert a.ids == b.ids, (k, a, b)
+        assert a.objective == pytest.approx(b.objective)
+
+
+@needs_native
+def test_native_tie_list_on_mi355x_mesh():
+    """Full xGMI mesh, nothing used: every 2-subset is optimal, listed lexicographically."""
+    import gpu_topology_on_k8s_amd.placement.core as core
+
+    t = fx.f7_mi355x(link_gbps=76.5)
+    p = Problem.from_topology(t)
+    mod = core._native_engine()
+    r = mod.select(p.cost, p.free, [lv.astype(np.int64).tolist() for lv in p.levels], p.access, 2, collect_ties=True)
+    py_ties = []
+    best = math.inf
+    for comb in itertools.combinations(range(8), 2):
+        j, _ = evaluate(p, comb)
+        if j < best - 1e-9:
+            best, py_ties = j, [list(comb)]
+        elif j <= best + 1e-9:
+            py_ties.append(list(comb))
+    assert r["ties"] == py_ties
+
+
+@needs_native
 def test_native_engine_sanitizer_selftest():
     """ASan/UBSan host build of the engine vs brute force."""
     exe = binary("engine_selftest")
