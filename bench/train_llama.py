@@ -39,7 +39,7 @@ def run(placement: str, a) -> dict:
            f"--master-port={_port()}", "-m", "gpu_topology_on_k8s_amd.models.train", "--model", a.model, "--batch", str(a.batch),
            "--seq", str(a.seq), "--steps", str(a.steps), "--warmup", str(a.warmup), "--placement", placement,
            "--bucket-mb", str(a.bucket_mb), "--attn", a.attn, "--gemm-tuning", a.gemm_tuning, "--gemm-layout", a.gemm_layout]
-           + (["--overlap-transposes"] if a.overlap_transposes else [])
+           + (["--overlap-transposes"] if a.overlap_transposes else []) + (["--zero1"] if a.zero1 else [])
            + (["--checkpoint"] if a.checkpoint else []) + (["--gemm-table", a.gemm_table] if a.gemm_table else []))
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""),
                **extra_env)
@@ -66,6 +66,7 @@ def main() -> int:
     ap.add_argument("--gemm-table", default="")
     ap.add_argument("--gemm-layout", default="nt", choices=["nt", "native"])
     ap.add_argument("--overlap-transposes", action="store_true")
+    ap.add_argument("--zero1", action="store_true", help="ZeRO-1: sharded AdamW, reduce-scatter grads / all-gather weights")
     ap.add_argument("--timeout", type=int, default=1500)
     ap.add_argument("--placements", default="best,worst", help="comma list of best, worst, p2p-off (emulated worst link class)")
     ap.add_argument("--out", default="")
@@ -89,7 +90,7 @@ def main() -> int:
         "model": a.model, "n_gpus": a.gpus, "seq_len": a.seq, "global_batch": a.batch * a.gpus,
         "best_tokens_per_s": res["best"]["tokens_per_s"], "best_devices": res["best"]["devices"],
         "worst_tokens_per_s": worst.get("tokens_per_s"), "worst_devices": worst.get("devices"), "worst_kind": worst_kind,
-        "mfu": res["best"]["mfu"], "max_mem_gb": res["best"]["max_mem_gb"], "data": "synthetic tokens, random-init weights",
+        "mfu": res["best"]["mfu"], "max_mem_gb": res["best"]["max_mem_gb"], "zero1": a.zero1, "data": "synthetic tokens, random-init weights",
     }
     if summary["worst_tokens_per_s"]:
         summary["speedup_vs_worst"] = summary["best_tokens_per_s"] / summary["worst_tokens_per_s"]

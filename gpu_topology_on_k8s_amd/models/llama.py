@@ -314,6 +314,9 @@ class Llama(torch.nn.Module):
         self.attn = attn
         self.gemm_layout = gemm_layout
         self.overlap_transposes = overlap_transposes
+        # called with a parameter name before its first use in forward (ZeRO-1: wait for that
+        # bucket's weight all-gather, parallel/dp.py BucketedAllReduce.wait_param)
+        self.param_ready: Optional[Callable[[str], None]] = None
         self.flat = FlatParams(cfg.param_shapes(), device)
         for n, p in self.flat.params.items():
             self.register_parameter(n.replace(".", "_"), p)
@@ -342,11 +345,13 @@ class Llama(torch.nn.Module):
                 flat[i:i + m].copy_(torch.randn(m, generator=g, dtype=torch.float32, device=dev).mul_(s))
 
     def P(self, name: str) -> torch.nn.Parameter:
+        if self.param_ready is not None:
+            self.param_ready(name)
         return self.flat.params[name]
 
     def _linear(self, x: torch.Tensor, name: str) -> torch.Tensor:
         nt = self.gemm_layout == "nt"
-        return _FlatLinear.apply(x, self.flat.params[name].detach(), self.flat, name, nt, self.overlap_transposes)
+        return _FlatLinear.apply(x, self.P(name).detach(), self.flat, name, nt, self.overlap_transposes)
 
     # ---------------------------------------------------------------- blocks
     def _attention(self, q, k, v):
@@ -372,7 +377,7 @@ class Llama(torch.nn.Module):
         o = self._attention(q, k, v).reshape(B * S, H * Dh)  # [B, S, H, Dh] -> [B*S, H*Dh]
         x = x + self._linear(o, f"l{i}.wo")
         h = fused.rmsnorm(x, self.P(f"l{i}.ffn_norm"), cfg.norm_eps)
-        a = _FlatLinearSwiGLU.apply(h, self.flat.params[f"l{i}.w13"].detach(), self.flat, f"l{i}.w13", self.gemm_layout == "nt",
+        a = _FlatLinearSwiGLU.apply(h, self.P(f"l{i}.w13").detach(), self.flat, f"l{i}.w13", self.gemm_layout == "nt",
                                     self.overlap_transposes)
         x = x + self._linear(a, f"l{i}.w2")
         return x

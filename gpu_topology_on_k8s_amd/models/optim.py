@@ -5,13 +5,18 @@ gradient that live in :class:`~.llama.FlatParams`.  The step reads 14 B and writ
 — HBM-bound by construction, so it is one grid-stride kernel over the whole 8 B-element buffer
 instead of one launch per tensor.  Hyper-parameters are a device tensor so nothing syncs the host.
 Optional global-norm clipping uses one more fused pass (``sq_norm``) and stays on the device.
+
+``shards`` (ZeRO-1, :class:`~..parallel.dp.BucketedAllReduce` with ``zero1=True``): the optimizer
+owns only those flat-buffer ranges — its master/m/v hold their concatenation, one kernel launch per
+range, and the clipping norm is the all-reduced sum of every rank's shard norms.
 """
 from __future__ import annotations
 
 import math
-from typing import Optional
+from typing import List, Optional, Sequence, Tuple
 
 import torch
+import torch.distributed as dist
 
 from ..ops import fused
 
@@ -20,11 +25,17 @@ __all__ = ["FlatAdamW"]
 
 class FlatAdamW:
     def __init__(self, flat, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8, weight_decay: float = 0.1,
-                 clip_norm: Optional[float] = 1.0):
+                 clip_norm: Optional[float] = 1.0, shards: Optional[Sequence[Tuple[int, int]]] = None, group=None):
         self.flat = flat
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.clip_norm = clip_norm
-        self.master = flat.data.float()
+        self.group = group
+        self.sharded = shards is not None
+        self.shards: List[Tuple[int, int]] = list(shards) if shards is not None else [(0, flat.numel)]
+        if self.sharded:
+            self.master = torch.cat([flat.data[s:e].float() for s, e in self.shards])
+        else:
+            self.master = flat.data.float()
         self.m = torch.zeros_like(self.master)
         self.v = torch.zeros_like(self.master)
         self.t = 0
@@ -39,25 +50,35 @@ class FlatAdamW:
         b1, b2 = self.betas
         gs = torch.tensor(grad_scale, dtype=torch.float32, device=self.hp.device)
         if self.clip_norm is not None:
-            if self.flat.grad.is_cuda:
-                sq = fused.hip().sq_norm(self.flat.grad)
-            else:
-                sq = self.flat.grad.float().pow(2).sum()
+            sq = None
+            for g in self._views(self.flat.grad):
+                part = fused.hip().sq_norm(g) if g.is_cuda else g.float().pow(2).sum()
+                sq = part if sq is None else sq + part
+            if self.sharded and dist.is_initialized() and dist.get_world_size(self.group) > 1:
+                dist.all_reduce(sq, group=self.group)
             norm = sq.sqrt() * grad_scale
             gs = gs * torch.clamp(self.clip_norm / (norm + 1e-6), max=1.0)
         vals = torch.tensor([self.lr, b1, b2, self.eps, self.wd, 0.0, 1 - b1 ** self.t, 1 - b2 ** self.t], dtype=torch.float32)
         self.hp.copy_(vals, non_blocking=True)
         self.hp[5:6].copy_(gs.reshape(1))
-        if self.flat.data.is_cuda:
-            fused.hip().adamw_step(self.master, self.m, self.v, self.flat.grad, self.flat.data, self.hp)
-        else:
-            self._step_ref()
+        o = 0
+        for (s, e), g, d in zip(self.shards, self._views(self.flat.grad), self._views(self.flat.data)):
+            n = e - s
+            st = (self.master[o:o + n], self.m[o:o + n], self.v[o:o + n])
+            if d.is_cuda:
+                fused.hip().adamw_step(*st, g, d, self.hp)
+            else:
+                self._step_ref(*st, g, d)
+            o += n
 
-    def _step_ref(self) -> None:
+    def _views(self, buf: torch.Tensor):
+        return [buf[s:e] for s, e in self.shards]
+
+    def _step_ref(self, master, m, v, grad, data) -> None:
         lr, b1, b2, eps, wd, gs, bc1, bc2 = self.hp.tolist()
-        g = self.flat.grad.float() * gs
-        self.m.mul_(b1).add_(g, alpha=1 - b1)
-        self.v.mul_(b2).addcmul_(g, g, value=1 - b2)
-        upd = (self.m / bc1) / ((self.v / bc2).sqrt() + eps)
-        self.master.sub_(lr * (upd + wd * self.master))
-        self.flat.data.copy_(self.master.to(self.flat.data.dtype))
+        g = grad.float() * gs
+        m.mul_(b1).add_(g, alpha=1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        upd = (m / bc1) / ((v / bc2).sqrt() + eps)
+        master.sub_(lr * (upd + wd * master))
+        data.copy_(master.to(data.dtype))

@@ -59,7 +59,8 @@ def _choose_device(env, placement: str, discovery: str) -> Dict[str, object]:
 def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int = 3, warmup: int = 1, device_kind: str = "cuda",
           placement: str = "best", discovery: str = "auto", bucket_mb: float = 256.0, checkpoint: bool = False, lr: float = 3e-4,
           attn: str = "hip", seed: int = 0, log: bool = True, gemm_tuning: str = "auto",
-          gemm_table: Optional[str] = None, gemm_layout: str = "nt", overlap_transposes: bool = False) -> Dict[str, object]:
+          gemm_table: Optional[str] = None, gemm_layout: str = "nt", overlap_transposes: bool = False,
+          zero1: bool = False) -> Dict[str, object]:
     env = _init_dist(device_kind)
     if device_kind == "cuda":
         pl = _choose_device(env, placement, discovery)
@@ -75,8 +76,10 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
     model = Llama(cfg, device=device, seed=seed, checkpoint=checkpoint, attn=attn, gemm_layout=gemm_layout,
                   overlap_transposes=overlap_transposes)
     broadcast_params(model.flat)
-    ar = BucketedAllReduce(model.flat, bucket_mb=bucket_mb)
-    opt = FlatAdamW(model.flat, lr=lr)
+    ar = BucketedAllReduce(model.flat, bucket_mb=bucket_mb, zero1=zero1)
+    opt = FlatAdamW(model.flat, lr=lr, shards=ar.shards() if zero1 else None)
+    if zero1:
+        model.param_ready = ar.wait_param
     gen = torch.Generator(device="cpu").manual_seed(1234 + env["rank"])
 
     def batch_tokens():
@@ -91,6 +94,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         loss.backward()
         ar.finish()
         opt.step(grad_scale=ar.grad_scale)
+        ar.gather_params()  # zero1: overlaps the next forward; no-op otherwise
         return loss.detach()
 
     def sync():
@@ -100,12 +104,14 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
     losses = []
     for _ in range(warmup):
         losses.append(step())
+    ar.wait_all_params()
     sync()
     dist.barrier()
     sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         losses.append(step())
+    ar.wait_all_params()
     sync()
     dt = time.perf_counter() - t0
     dist.barrier()
@@ -134,6 +140,8 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "loss_first": float(losses[0]),
         "loss_last": float(losses[-1]),
         "buckets": ar.stats["buckets"],
+        "zero1": zero1,
+        "optimizer_state_gb": opt.state_bytes() / 1e9,
         "bucket_mb": bucket_mb,
         "gemm_tuning": gemm_mode,
         "gemm_layout": gemm_layout,
@@ -166,10 +174,12 @@ def main(argv=None) -> int:
                     help="backward GEMM operand layout: nt = transposed operands (HIP transpose kernel), native = as autograd issues them")
     ap.add_argument("--overlap-transposes", action="store_true",
                     help="make the NT operands' transposes on a side stream in forward (measured: no gain on MI355X)")
+    ap.add_argument("--zero1", action="store_true",
+                    help="shard the optimizer over the ranks: reduce-scatter grads, all-gather weights (ZeRO-1)")
     a = ap.parse_args(argv)
     train(a.model, a.batch, a.seq, a.steps, a.warmup, a.device, a.placement, a.discovery, a.bucket_mb, a.checkpoint, attn=a.attn,
           gemm_tuning=a.gemm_tuning, gemm_table=a.gemm_table, gemm_layout=a.gemm_layout,
-          overlap_transposes=a.overlap_transposes)
+          overlap_transposes=a.overlap_transposes, zero1=a.zero1)
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0

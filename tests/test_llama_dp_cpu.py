@@ -204,16 +204,79 @@ def test_bucketed_allreduce_two_ranks_gloo():
         assert res[r]["tiled"]
 
 
-def test_train_entry_cpu_single_rank():
+def _zero1_worker(rank, world, port, q):
+    """Same data, same seed: ZeRO-1 (reduce-scatter grads, sharded AdamW, async all-gather waited per
+    bucket in the next forward) must track the all-reduce + full AdamW run step for step."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = LlamaConfig.tiny()
+    runs = {}
+    for zero1 in (False, True):
+        m = Llama(cfg, device="cpu", seed=7)
+        ar = BucketedAllReduce(m.flat, bucket_mb=0.05, first_bucket_mb=0.01, zero1=zero1)
+        opt = FlatAdamW(m.flat, lr=1e-3, shards=ar.shards() if zero1 else None)
+        if zero1:
+            m.param_ready = ar.wait_param
+        gen = torch.Generator().manual_seed(100 + rank)
+        losses = []
+        for _ in range(3):
+            tok = torch.randint(0, cfg.vocab, (2, 16), generator=gen)
+            m.flat.zero_grad()
+            loss = m(tok, torch.roll(tok, -1, 1))
+            loss.backward()
+            ar.finish()
+            opt.step(grad_scale=ar.grad_scale)
+            ar.gather_params()
+            losses.append(float(loss))
+        ar.wait_all_params()
+        runs[zero1] = (m.flat.data.float().clone(), losses, opt.master.numel(), len(ar.buckets))
+        ar.remove()
+    full, sharded = runs[False], runs[True]
+    ck = torch.tensor([sharded[0].sum().item()])
+    gathered = [torch.zeros(1) for _ in range(world)]
+    dist.all_gather(gathered, ck)
+    q.put((rank, {
+        "max_diff": float((full[0] - sharded[0]).abs().max()),
+        "loss_diff": max(abs(a - b) for a, b in zip(full[1], sharded[1])),
+        "state_ratio": sharded[2] / full[2],
+        "buckets": sharded[3],
+        "replicas_equal": all(abs(g.item() - gathered[0].item()) < 1e-6 for g in gathered),
+    }))
+    dist.destroy_process_group()
+
+
+def test_zero1_matches_allreduce_two_ranks_gloo():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_zero1_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert res[r]["buckets"] > 3
+        assert res[r]["state_ratio"] == pytest.approx(1 / world)
+        assert res[r]["replicas_equal"], res
+        assert res[r]["loss_diff"] < 1e-2, res
+        assert res[r]["max_diff"] < 2e-2, res  # bf16 weights; reduction order differs (RS vs AR)
+
+
+@pytest.mark.parametrize("zero1", [False, True])
+def test_train_entry_cpu_single_rank(zero1):
     from gpu_topology_on_k8s_amd.models.train import train
 
     if dist.is_initialized():
         pytest.skip("process group already initialised")
     os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     try:
-        out = train("tiny", batch=2, seq=32, steps=2, warmup=1, device_kind="cpu", log=False)
+        out = train("tiny", batch=2, seq=32, steps=2, warmup=1, device_kind="cpu", log=False, zero1=zero1)
     finally:
         dist.destroy_process_group()
         for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
             os.environ.pop(k, None)
     assert out["tokens_per_s"] > 0 and out["steps"] == 2 and math.isfinite(out["loss_last"])
+    assert out["zero1"] == zero1 and out["optimizer_state_gb"] > 0
