@@ -40,12 +40,22 @@ class FlatAdamW:
         self.v = torch.zeros_like(self.master)
         self.t = 0
         self.hp = torch.zeros(8, dtype=torch.float32, device=flat.data.device)
+        self._deferred = []  # events the next step's writes must wait for (async checkpoint copies)
+
+    def defer_until(self, event) -> None:
+        """Make the next :meth:`step` (on its stream) wait for ``event`` before it writes."""
+        self._deferred.append(event)
 
     def state_bytes(self) -> int:
         return 3 * self.master.numel() * 4
 
     @torch.no_grad()
     def step(self, grad_scale: float = 1.0) -> None:
+        if self._deferred:
+            cur = torch.cuda.current_stream(self.hp.device)
+            for ev in self._deferred:
+                cur.wait_event(ev)
+            self._deferred.clear()
         self.t += 1
         b1, b2 = self.betas
         gs = torch.tensor(grad_scale, dtype=torch.float32, device=self.hp.device)

@@ -25,6 +25,7 @@ import torch.distributed as dist
 from .llama import Llama, LlamaConfig
 from .gemm_tuning import setup_gemm_tuning
 from .optim import FlatAdamW
+from .checkpoint import CheckpointWriter, load_checkpoint
 from ..parallel.dp import BucketedAllReduce, broadcast_params
 
 __all__ = ["train", "main"]
@@ -60,7 +61,8 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
           placement: str = "best", discovery: str = "auto", bucket_mb: float = 256.0, checkpoint: bool = False, lr: float = 3e-4,
           attn: str = "hip", seed: int = 0, log: bool = True, gemm_tuning: str = "auto",
           gemm_table: Optional[str] = None, gemm_layout: str = "nt", overlap_transposes: bool = False,
-          zero1: bool = False) -> Dict[str, object]:
+          zero1: bool = False, save_dir: Optional[str] = None, save_every: int = 0, resume: Optional[str] = None,
+          keep: int = 2) -> Dict[str, object]:
     env = _init_dist(device_kind)
     if device_kind == "cuda":
         pl = _choose_device(env, placement, discovery)
@@ -81,6 +83,14 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
     if zero1:
         model.param_ready = ar.wait_param
     gen = torch.Generator(device="cpu").manual_seed(1234 + env["rank"])
+    start_step, resumed = 0, None
+    if resume:
+        meta = load_checkpoint(resume, model, opt, gen)
+        start_step, resumed = int(meta["step"]), meta["path"]
+    ckpt = CheckpointWriter(save_dir, model, opt, model_name=model_name, keep=keep, zero1=zero1) if save_dir else None
+    if ckpt is not None and save_every > 0:
+        ckpt.prepare()
+    done = [start_step]
 
     def batch_tokens():
         t = torch.randint(0, cfg.vocab, (batch, seq + 1), generator=gen)
@@ -95,6 +105,10 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         ar.finish()
         opt.step(grad_scale=ar.grad_scale)
         ar.gather_params()  # zero1: overlaps the next forward; no-op otherwise
+        done[0] += 1
+        if ckpt is not None and save_every > 0 and done[0] % save_every == 0:
+            ar.wait_all_params()
+            ckpt.save(done[0], gen)
         return loss.detach()
 
     def sync():
@@ -118,6 +132,10 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
     t = torch.tensor([dt], dtype=torch.float64, device=device if device.type == "cuda" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
+    if ckpt is not None:
+        if not ckpt.has(done[0]):
+            ckpt.save(done[0], gen)
+        ckpt.close()
     tokens = env["world"] * batch * seq * steps
     tps = tokens / dt
     mfu = tps * cfg.flops_per_token(seq) / (PEAK_BF16_FLOPS * env["world"]) if device.type == "cuda" else None
@@ -146,6 +164,11 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "gemm_tuning": gemm_mode,
         "gemm_layout": gemm_layout,
         "overlap_transposes": overlap_transposes,
+        "step_start": start_step,
+        "step_end": done[0],
+        "resumed_from": resumed,
+        "checkpoints_saved": ckpt.saved if ckpt is not None else [],
+        "checkpoint_stats": ckpt.stats if ckpt is not None else None,
         "max_mem_gb": (torch.cuda.max_memory_allocated(device) / 1e9) if device.type == "cuda" else None,
     }
     if log and env["rank"] == 0:
@@ -176,10 +199,16 @@ def main(argv=None) -> int:
                     help="make the NT operands' transposes on a side stream in forward (measured: no gain on MI355X)")
     ap.add_argument("--zero1", action="store_true",
                     help="shard the optimizer over the ranks: reduce-scatter grads, all-gather weights (ZeRO-1)")
+    ap.add_argument("--save-dir", default=None, help="write checkpoints here (async; at the end, and every --save-every steps)")
+    ap.add_argument("--save-every", type=int, default=0, help="checkpoint interval in optimizer steps (0 = only at the end)")
+    ap.add_argument("--keep", type=int, default=2, help="committed checkpoints to keep")
+    ap.add_argument("--resume", default=None,
+                    help="checkpoint root (its latest) or step directory; any world size / --zero1 setting")
     a = ap.parse_args(argv)
     train(a.model, a.batch, a.seq, a.steps, a.warmup, a.device, a.placement, a.discovery, a.bucket_mb, a.checkpoint, attn=a.attn,
           gemm_tuning=a.gemm_tuning, gemm_table=a.gemm_table, gemm_layout=a.gemm_layout,
-          overlap_transposes=a.overlap_transposes, zero1=a.zero1)
+          overlap_transposes=a.overlap_transposes, zero1=a.zero1, save_dir=a.save_dir, save_every=a.save_every,
+          resume=a.resume, keep=a.keep)
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0

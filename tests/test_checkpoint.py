@@ -1,0 +1,187 @@
+"""Training checkpoints (models/checkpoint.py): async sharded save, exact resume, and resharding
+across world sizes / ZeRO-1 settings.  CPU: single process and gloo at world_size 2 (127.0.0.1)."""
+import json
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+from safetensors import safe_open
+
+from gpu_topology_on_k8s_amd.models import CheckpointWriter, FlatAdamW, Llama, LlamaConfig, load_checkpoint
+from gpu_topology_on_k8s_amd.models.checkpoint import latest_checkpoint, read_optimizer_ranges
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _steps(m, opt, gen, n, cfg):
+    for _ in range(n):
+        tok = torch.randint(0, cfg.vocab, (2, 16), generator=gen)
+        m.flat.zero_grad()
+        m(tok, torch.roll(tok, -1, 1)).backward()
+        opt.step()
+
+
+def test_save_resume_single_process_is_exact(tmp_path):
+    cfg = LlamaConfig.tiny()
+    m = Llama(cfg, device="cpu", seed=1)
+    opt = FlatAdamW(m.flat, lr=1e-3)
+    gen = torch.Generator().manual_seed(5)
+    _steps(m, opt, gen, 2, cfg)
+    w = CheckpointWriter(str(tmp_path), m, opt, model_name="tiny")
+    w.save(2, gen)
+    w.close()
+    _steps(m, opt, gen, 2, cfg)  # continuous run: steps 3, 4
+    want = m.flat.data.clone()
+
+    m2 = Llama(cfg, device="cpu", seed=99)  # different init: everything must come from the file
+    opt2 = FlatAdamW(m2.flat, lr=1e-3)
+    gen2 = torch.Generator().manual_seed(0)
+    meta = load_checkpoint(str(tmp_path), m2, opt2, gen2)
+    assert meta["step"] == 2 and opt2.t == 2 and meta["path"] == latest_checkpoint(str(tmp_path))
+    _steps(m2, opt2, gen2, 2, cfg)
+    assert torch.equal(m2.flat.data, want)
+
+
+def test_keep_prunes_and_latest_points_at_newest(tmp_path):
+    cfg = LlamaConfig.tiny()
+    m = Llama(cfg, device="cpu")
+    opt = FlatAdamW(m.flat)
+    w = CheckpointWriter(str(tmp_path), m, opt, keep=2)
+    for s in (1, 2, 3):
+        w.save(s)
+    w.close()
+    dirs = sorted(d for d in os.listdir(tmp_path) if d.startswith("step_"))
+    assert dirs == ["step_000002", "step_000003"]
+    assert open(tmp_path / "latest").read() == "step_000003"
+    assert not [d for d in os.listdir(tmp_path) if d.endswith(".tmp")]
+    meta = json.load(open(tmp_path / "step_000003" / "meta.json"))
+    assert meta["numel"] == m.flat.numel and meta["layout"][0][0] == m.flat.names[0]
+
+
+def test_layout_mismatch_is_refused(tmp_path):
+    m = Llama(LlamaConfig.tiny(), device="cpu")
+    w = CheckpointWriter(str(tmp_path), m, FlatAdamW(m.flat))
+    w.save(1)
+    w.close()
+    import dataclasses
+    cfg = dataclasses.replace(LlamaConfig.tiny(), n_layers=3)
+    other = Llama(cfg, device="cpu")
+    with pytest.raises(ValueError, match="layout"):
+        load_checkpoint(str(tmp_path), other, FlatAdamW(other.flat))
+    with pytest.raises(FileNotFoundError):
+        load_checkpoint(str(tmp_path / "nothing"), m)
+
+
+def test_optimizer_ranges_reshard(tmp_path):
+    """State written as 3 uneven shards reads back for any other tiling of the buffer."""
+    n = 1000
+    full = {k: torch.randn(n) for k in ("master", "m", "v")}
+    shards = [[(0, 100), (700, 1000)], [(100, 450)], [(450, 700)]]
+    from safetensors.torch import save_file
+    for r, sh in enumerate(shards):
+        t = {k: torch.cat([full[k][s:e] for s, e in sh]) for k in full}
+        t["shards"] = torch.tensor(sh, dtype=torch.int64)
+        save_file(t, str(tmp_path / f"optim_rank{r}.safetensors"))
+    for ranges in ([(0, n)], [(0, 500)], [(500, 1000)], [(50, 120), (600, 990)]):
+        got = read_optimizer_ranges(str(tmp_path), ranges)
+        for k in full:
+            assert torch.equal(got[k], torch.cat([full[k][s:e] for s, e in ranges]))
+    with pytest.raises(ValueError, match="cover"):
+        read_optimizer_ranges(str(tmp_path), [(0, n + 10)])
+
+
+def _worker(rank, world, port, root, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from gpu_topology_on_k8s_amd.models.train import train
+    import torch.distributed as dist
+
+    kw = dict(batch=2, seq=16, warmup=0, device_kind="cpu", log=False, zero1=True, bucket_mb=0.05)
+    a = train("tiny", steps=4, save_dir=os.path.join(root, "a"), **kw)
+    b1 = train("tiny", steps=2, save_dir=os.path.join(root, "b"), save_every=1, **kw)
+    b2 = train("tiny", steps=2, save_dir=os.path.join(root, "b"), resume=os.path.join(root, "b"), **kw)
+    q.put((rank, {"a": a["step_end"], "b1": b1["checkpoints_saved"], "b2": (b2["step_start"], b2["step_end"]),
+                  "loss_a": a["loss_last"], "loss_b": b2["loss_last"]}))
+    dist.destroy_process_group()
+
+
+def test_zero1_two_ranks_resume_matches_continuous_and_reshards_to_one(tmp_path):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert res[r]["a"] == 4 and res[r]["b1"] == [1, 2] and res[r]["b2"] == (2, 4)
+        assert res[r]["loss_a"] == res[r]["loss_b"]
+    da, db = latest_checkpoint(str(tmp_path / "a")), latest_checkpoint(str(tmp_path / "b"))
+    assert da.endswith("step_000004") and db.endswith("step_000004")
+    # each ZeRO-1 rank wrote only its own shard
+    assert sorted(f for f in os.listdir(da) if f.startswith("optim")) == ["optim_rank0.safetensors", "optim_rank1.safetensors"]
+    with safe_open(os.path.join(da, "weights.safetensors"), "pt") as fa, safe_open(os.path.join(db, "weights.safetensors"), "pt") as fb:
+        assert torch.equal(fa.get_tensor("flat"), fb.get_tensor("flat"))  # resumed run == continuous run
+    # reshard: the 2-rank ZeRO-1 state resumes into one unsharded optimizer (world 1)
+    m = Llama(LlamaConfig.tiny(), device="cpu", seed=3)
+    opt = FlatAdamW(m.flat)
+    meta = load_checkpoint(da, m, opt)
+    assert meta["world"] == 2 and meta["zero1"] and opt.t == 4
+    for fn in ("optim_rank0.safetensors", "optim_rank1.safetensors"):
+        with safe_open(os.path.join(da, fn), "pt") as f:
+            o = 0
+            master = f.get_tensor("master")
+            for s, e in f.get_tensor("shards").tolist():
+                assert torch.equal(opt.master[s:e], master[o:o + e - s])
+                o += e - s
+
+
+@pytest.mark.gpu
+def test_async_checkpoint_on_gpu_resumes_exactly(tmp_path):
+    """HIP path: pinned async snapshot on a side stream while the next steps run (fused AdamW
+    kernel, HIP attention), then an exact resume into a fresh model on the device."""
+    from gpu_topology_on_k8s_amd.ops import fused
+
+    fused.hip()  # fail loudly if the extension is missing
+    dev = torch.device("cuda", 0)
+    cfg = LlamaConfig.tiny()
+    m = Llama(cfg, device=dev, seed=1)
+    opt = FlatAdamW(m.flat, lr=1e-3)
+    gen = torch.Generator().manual_seed(5)
+
+    def steps(m, opt, gen, n):
+        for _ in range(n):
+            tok = torch.randint(0, cfg.vocab, (2, 64), generator=gen).to(dev)
+            m.flat.zero_grad()
+            m(tok, torch.roll(tok, -1, 1)).backward()
+            opt.step()
+
+    steps(m, opt, gen, 2)
+    snap = (m.flat.data.clone(), opt.master.clone(), opt.v.clone())
+    w = CheckpointWriter(str(tmp_path), m, opt, model_name="tiny")
+    w.save(2, gen)  # returns before the file is written
+    steps(m, opt, gen, 2)  # these steps overwrite the state while the writer runs
+    w.close()
+    torch.cuda.synchronize()
+    want = m.flat.data.clone()
+    d = latest_checkpoint(str(tmp_path))
+    with safe_open(os.path.join(d, "weights.safetensors"), "pt") as f:
+        assert torch.equal(f.get_tensor("flat"), snap[0].cpu())  # the snapshot, not later state
+    with safe_open(os.path.join(d, "optim_rank0.safetensors"), "pt") as f:
+        assert torch.equal(f.get_tensor("master"), snap[1].cpu()) and torch.equal(f.get_tensor("v"), snap[2].cpu())
+    m2 = Llama(cfg, device=dev, seed=7)
+    opt2 = FlatAdamW(m2.flat, lr=1e-3)
+    gen2 = torch.Generator()
+    load_checkpoint(str(tmp_path), m2, opt2, gen2)
+    steps(m2, opt2, gen2, 2)
+    torch.cuda.synchronize()
+    assert torch.equal(m2.flat.data, want)
