@@ -49,6 +49,9 @@ def parse(argv=None):
     ap.add_argument("--backend", default="native", choices=["native", "torch", "cpu"],
                     help="native = RCCL communicator from csrc/rccl; torch = dist.all_reduce; cpu = gloo (control-path tests)")
     ap.add_argument("--inplace", action="store_true")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="small-message latency of hipGraph-captured vs eager all-reduces after the sweep "
+                         "(auto = only at k = 1, where it has been run on MI355X; k >= 2 capture is opt-in)")
     ap.add_argument("--probe", default="auto", choices=["auto", "off", "quick", "full"],
                     help="HIP link probe (K4 warm-up + K1 p2p read of every ordered pair) before placement, in a child "
                          "process of rank 0; 'auto' = quick on GPUs, off for --backend cpu; a failed probe falls back "
@@ -124,6 +127,41 @@ def run_sweep(runner, sizes, env, tdev, barrier_kw, gpu_sync):
     peak = max(rows, key=lambda r: r[key]) if rows else None
     return {"rows": rows, "peak": {"bytes": peak["bytes"], key: peak[key]} if peak else None,
             "all_exact": all(r["wrong"] == 0 for r in rows)}
+
+
+def run_graph_latency(runner, sizes, env, tdev, barrier_kw, gpu_sync, ops: int = 32, replays: int = 8):
+    """Launch-bound small messages: ``ops`` out-of-place all-reduces captured into one hipGraph
+    (native ``Comm.capture``) and replayed, against the same ``ops`` enqueued one call at a time.
+    µs per all-reduce, max over ranks; the graph's result is exact-checked (``Comm.verify``)."""
+    import torch
+    import torch.distributed as dist
+
+    def timed(fn, n):
+        dist.barrier(**barrier_kw)
+        gpu_sync()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        runner.synchronize()
+        gpu_sync()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=tdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    rows = []
+    c = runner.comm
+    for b in sizes:
+        runner.resize(b)
+        eager_us = timed(runner.step, ops * replays) / (ops * replays) * 1e6
+        c.capture(ops, False)
+        c.replay()
+        runner.synchronize()
+        graph_us = timed(c.replay, replays) / (ops * replays) * 1e6
+        wrong = torch.tensor([c.verify()], dtype=torch.int64, device=tdev)
+        dist.all_reduce(wrong)
+        rows.append({"bytes": runner.nbytes, "eager_us": round(eager_us, 2), "graph_us": round(graph_us, 2),
+                     "speedup": round(eager_us / graph_us, 2) if graph_us > 0 else None, "wrong": int(wrong.item())})
+    return {"ops_per_graph": ops, "rows": rows, "all_exact": all(r["wrong"] == 0 for r in rows)}
 
 
 def parse_ctas(spec: str):
@@ -291,6 +329,14 @@ def main(argv=None) -> int:
         except Exception as e:  # noqa: BLE001 - every rank runs the same sizes, so all land here together
             print(f"bench: size sweep aborted on rank {env.rank}: {e}", file=sys.stderr)
             sweep = {"error": str(e)[:300]}
+    graph = None
+    want_graph = args.graph == "on" or (args.graph == "auto" and env.world == 1)
+    if want_graph and sizes and runner.comm is not None and not args.inplace:
+        try:  # supplementary, like the sweep
+            graph = run_graph_latency(runner, [8, 4096, 65536, 1 << 20], env, tdev, barrier_kw, gpu_sync)
+        except Exception as e:  # noqa: BLE001
+            print(f"bench: graph latency aborted on rank {env.rank}: {e}", file=sys.stderr)
+            graph = {"error": str(e)[:300]}
     runner.close()
     if env.rank == 0:
         bound = (choice.extra.get("probe") or {}).get("subset_ingress_bound_gbps")  # K5/K1 ceiling of busBW
@@ -329,6 +375,7 @@ def main(argv=None) -> int:
             "link_probe": choice.extra.get("probe"),
             "k8s_placement": choice.extra.get("k8s"),
             "size_sweep": sweep,
+            "graph_latency": graph,
             "value_kind": "busbw" if env.world > 1 else "algbw (busbw = 0 at k=1)",
             "busbw_vs_probe_bound": round(busbw / bound, 4) if bound else None,
             "algbw_gbps": round(algbw, 3),

@@ -6,6 +6,9 @@
 //                                     rank builds a Comm on its chosen device (ncclCommInitRank).
 // Comm.step() enqueues one out-of-place all-reduce on the Comm's stream and returns immediately so
 // a Python-side timing loop (bench.py) brackets exactly K of them with barrier + synchronize.
+// Comm.capture(n) records n back-to-back all-reduces into one hipGraph and Comm.replay() launches
+// it: small messages are launch-bound (a few µs of host enqueue per call), and a graph replays the
+// whole chain with one launch — the latency a graph-captured training step sees.
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -42,9 +45,13 @@ class Comm {
     max_ctas_ = max_ctas;
     RCCL_HIP_CHECK(hipStreamCreateWithFlags(&st_.stream, hipStreamNonBlocking));
   }
-  ~Comm() { st_.release(); }
+  ~Comm() {
+    drop_graph();
+    st_.release();
+  }
 
   void prepare(size_t bytes, const std::string& dtype) {
+    drop_graph();
     t_ = parse_dtype(dtype, &elem_);
     count_ = std::max<size_t>(1, bytes / elem_);
     st_.ensure(count_ * elem_);
@@ -71,15 +78,74 @@ class Comm {
     return st_.check(count_, t_, inplace);
   }
 
+  // Capture n all-reduces of the prepared buffer into one executable graph (every rank of the
+  // communicator must capture the same n).  One eager call first so RCCL's lazy per-size setup
+  // (channels, proxy buffers) happens outside the capture.
+  void capture(int n, bool inplace) {
+    if (!count_) throw std::runtime_error("prepare() first");
+    if (n < 1) throw std::invalid_argument("capture needs n >= 1");
+    drop_graph();
+    st_.set_device();
+    st_.allreduce(count_, t_, inplace);
+    RCCL_HIP_CHECK(hipStreamSynchronize(st_.stream));
+    hipGraph_t g = nullptr;
+    RCCL_HIP_CHECK(hipStreamBeginCapture(st_.stream, hipStreamCaptureModeThreadLocal));
+    try {
+      for (int i = 0; i < n; ++i) st_.allreduce(count_, t_, inplace);
+    } catch (...) {
+      (void)hipStreamEndCapture(st_.stream, &g);
+      if (g) (void)hipGraphDestroy(g);
+      throw;
+    }
+    RCCL_HIP_CHECK(hipStreamEndCapture(st_.stream, &g));
+    hipError_t e = hipGraphInstantiate(&exec_, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) {
+      exec_ = nullptr;
+      throw std::runtime_error(std::string("hipGraphInstantiate failed: ") + hipGetErrorString(e));
+    }
+    graph_n_ = n;
+  }
+
+  void replay() {
+    if (!exec_) throw std::runtime_error("capture() first");
+    st_.set_device();
+    RCCL_HIP_CHECK(hipGraphLaunch(exec_, st_.stream));
+  }
+
+  int graph_ops() const { return graph_n_; }
+
+  // Exact check of the receive buffer as it stands (no new all-reduce): after out-of-place graph
+  // replays of prepare()'s fill it must hold the same sums as one eager call.
+  unsigned long long verify() {
+    if (!count_) throw std::runtime_error("prepare() first");
+    return st_.check(count_, t_, false);
+  }
+
   size_t bytes() const { return count_ * elem_; }
   int rank() const { return st_.rank; }
   int nranks() const { return st_.nranks; }
   int device() const { return st_.device; }
   int min_ctas() const { return min_ctas_; }
   int max_ctas() const { return max_ctas_; }
-  void destroy() { st_.release(); }
+  void destroy() {
+    drop_graph();
+    st_.release();
+  }
 
  private:
+  void drop_graph() {
+    if (exec_) {
+      (void)hipSetDevice(st_.device);
+      (void)hipStreamSynchronize(st_.stream);
+      (void)hipGraphExecDestroy(exec_);
+    }
+    exec_ = nullptr;
+    graph_n_ = 0;
+  }
+  hipGraphExec_t exec_ = nullptr;
+  int graph_n_ = 0;
+
   RankState st_;
   ncclDataType_t t_ = ncclBfloat16;
   size_t elem_ = 2, count_ = 0;
@@ -136,6 +202,10 @@ PYBIND11_MODULE(_rccl, m) {
       .def("prepare", &Comm::prepare, py::arg("bytes"), py::arg("dtype") = "bf16",
            py::call_guard<py::gil_scoped_release>())
       .def("step", &Comm::step, py::arg("inplace") = false, py::call_guard<py::gil_scoped_release>())
+      .def("capture", &Comm::capture, py::arg("n"), py::arg("inplace") = false, py::call_guard<py::gil_scoped_release>())
+      .def("replay", &Comm::replay, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("graph_ops", &Comm::graph_ops)
+      .def("verify", &Comm::verify, py::call_guard<py::gil_scoped_release>())
       .def("synchronize", &Comm::synchronize, py::call_guard<py::gil_scoped_release>())
       .def("check", &Comm::check, py::arg("inplace") = false, py::call_guard<py::gil_scoped_release>())
       .def("destroy", &Comm::destroy, py::call_guard<py::gil_scoped_release>())

@@ -149,6 +149,28 @@ def test_rccl_comm_config_ctas():
     c.destroy()
 
 
+def test_rccl_comm_graph_capture_replay():
+    """n all-reduces captured into one hipGraph replay exactly (out-of-place result checked), the
+    graph is dropped on re-prepare, and replay without a capture fails loudly."""
+    from gpu_topology_on_k8s_amd._native import load
+
+    rccl = load("_rccl")
+    c = rccl.Comm(rccl.unique_id(), 1, 0, 0, 0, 0)
+    for nbytes in (8, 4096, 1 << 20, 64 << 20):
+        c.prepare(nbytes, "bf16")
+        c.capture(16, False)
+        assert c.graph_ops == 16
+        for _ in range(3):
+            c.replay()
+        c.synchronize()
+        assert c.verify() == 0
+    c.prepare(4096, "bf16")
+    assert c.graph_ops == 0
+    with pytest.raises(RuntimeError):
+        c.replay()
+    c.destroy()
+
+
 def test_bench_py_ctas_tuning_pass():
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup", "1", "--size-mb", "64",
                         "--ctas", "tune"], capture_output=True, text=True, timeout=600, cwd=REPO)
@@ -178,6 +200,8 @@ def test_bench_py_single_gpu():
     assert out["config"]["message_bytes_per_gpu"] == 64 << 20
     sw = out["size_sweep"]  # 8 B .. 16 GiB, every size exactly checked
     assert sw["all_exact"] and sw["rows"][-1]["bytes"] == 16 << 30 and sw["peak"]["algbw_gbps"] > 0
+    g = out["graph_latency"]  # hipGraph-captured vs eager small all-reduces, exact
+    assert g["all_exact"] and len(g["rows"]) == 4 and all(r["graph_us"] > 0 for r in g["rows"]), g
 
 
 def test_device_plugin_daemon_probes_in_child_on_real_node():
