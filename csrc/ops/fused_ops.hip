@@ -51,10 +51,13 @@ u16* bpm(at::Tensor& t) { return reinterpret_cast<u16*>(t.data_ptr()); }
 
 // =============================================================================== RMSNorm
 // One wave per row; lane l owns vectors c = i*64 + l (8 bf16 each).  NV = ceil(D / 512).
-template <int NV>
+// ADD: h = bf16(x + res) is formed in registers, written once (the residual stream) and normalised
+// in the same pass — the separate add kernel and its re-read of h disappear.
+template <int NV, bool ADD = false>
 __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ w,
                                                           u16* __restrict__ y, float* __restrict__ rstd, int M, int D,
-                                                          float eps) {
+                                                          float eps, const u16* __restrict__ res = nullptr,
+                                                          u16* __restrict__ h = nullptr) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -67,6 +70,12 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const u16* __restrict_
     const int c = i * 64 + lane;
     if (c < nvec) {
       v[i] = xr[c];
+      if constexpr (ADD) {
+        const u16x8 rv = reinterpret_cast<const u16x8*>(res + (size_t)row * D)[c];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = f2bf(bf2f(v[i][j]) + bf2f(rv[j]));
+        reinterpret_cast<u16x8*>(h + (size_t)row * D)[c] = v[i];
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float f = bf2f(v[i][j]);
@@ -92,10 +101,13 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const u16* __restrict_
 }
 
 // dx = r*g - x*r^3*mean(g*x), g = dy*w ;  dW partial[wave] = sum_rows dy*x*r  (fp32, reduced later)
-template <int NV>
+// ACC: dx += dres (the residual stream's own gradient) before the single bf16 rounding — replaces
+// autograd's separate accumulate kernel for the fused add+norm.
+template <int NV, bool ACC = false>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const u16* __restrict__ dy, const u16* __restrict__ x,
                                                           const u16* __restrict__ w, const float* __restrict__ rstd,
-                                                          u16* __restrict__ dx, float* __restrict__ dw_part, int M, int D) {
+                                                          u16* __restrict__ dx, float* __restrict__ dw_part, int M, int D,
+                                                          const u16* __restrict__ dres = nullptr) {
   const int lane = threadIdx.x & 63;
   const int gwave = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int nwaves = gridDim.x * 4;
@@ -114,7 +126,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const u16* __restrict_
     const u16x8* xr = reinterpret_cast<const u16x8*>(x + (size_t)row * D);
     const u16x8* dyr = reinterpret_cast<const u16x8*>(dy + (size_t)row * D);
     const float r = rstd[row];
-    u16x8 xv[NV], gv[NV];
+    u16x8 xv[NV], gv[NV], dv[ACC ? NV : 1];
     float dot = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
@@ -122,6 +134,8 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const u16* __restrict_
       if (c < nvec) {
         xv[i] = xr[c];
         gv[i] = dyr[c];
+        // issued with x/dy so the residual gradient's latency hides under the same wait
+        if constexpr (ACC) dv[i] = reinterpret_cast<const u16x8*>(dres + (size_t)row * D)[c];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float xf = bf2f(xv[i][j]), dyf = bf2f(gv[i][j]);
@@ -138,8 +152,14 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const u16* __restrict_
       const int c = i * 64 + lane;
       if (c < nvec) {
         u16x8 o;
+        if constexpr (ACC) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = f2bf(r * bf2f(gv[i][j]) * bf2f(wv[i][j]) - bf2f(xv[i][j]) * k);
+          for (int j = 0; j < 8; ++j)
+            o[j] = f2bf(r * bf2f(gv[i][j]) * bf2f(wv[i][j]) - bf2f(xv[i][j]) * k + bf2f(dv[i][j]));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = f2bf(r * bf2f(gv[i][j]) * bf2f(wv[i][j]) - bf2f(xv[i][j]) * k);
+        }
         dxr[c] = o;
       }
     }
@@ -184,6 +204,35 @@ void rmsnorm_fwd_launch(const at::Tensor& x, const at::Tensor& w, at::Tensor& y,
                      rstd.data_ptr<float>(), M, D, eps);
 }
 
+template <int NV>
+void add_rmsnorm_fwd_launch(const at::Tensor& x, const at::Tensor& r, const at::Tensor& w, at::Tensor& h, at::Tensor& y,
+                            at::Tensor& rstd, int M, int D, float eps) {
+  hipLaunchKernelGGL((rmsnorm_fwd_kernel<NV, true>), dim3((M + 3) / 4), dim3(256), 0, cur_stream(), bp(x), bp(w), bpm(y),
+                     rstd.data_ptr<float>(), M, D, eps, bp(r), bpm(h));
+}
+
+// h = x + r (bf16), y = rmsnorm(h) * w in one pass; returns {h, y, rstd}.
+std::vector<at::Tensor> add_rmsnorm_fwd(const at::Tensor& x, const at::Tensor& r, const at::Tensor& w, double eps) {
+  CHECK_BF16(x);
+  CHECK_BF16(r);
+  CHECK_BF16(w);
+  const int D = (int)x.size(-1);
+  TORCH_CHECK(D % 8 == 0 && D <= 8192 && w.numel() == D, "add_rmsnorm: D must be a multiple of 8, <= 8192, and match w");
+  TORCH_CHECK(r.sizes() == x.sizes(), "add_rmsnorm: x and r shapes differ");
+  const int M = (int)(x.numel() / D);
+  auto h = at::empty_like(x);
+  auto y = at::empty_like(x);
+  auto rstd = at::empty({M}, x.options().dtype(at::kFloat));
+  if (M == 0) return {h, y, rstd};
+  const int nv = (D + 511) / 512;
+  if (nv <= 1) add_rmsnorm_fwd_launch<1>(x, r, w, h, y, rstd, M, D, (float)eps);
+  else if (nv <= 2) add_rmsnorm_fwd_launch<2>(x, r, w, h, y, rstd, M, D, (float)eps);
+  else if (nv <= 4) add_rmsnorm_fwd_launch<4>(x, r, w, h, y, rstd, M, D, (float)eps);
+  else if (nv <= 8) add_rmsnorm_fwd_launch<8>(x, r, w, h, y, rstd, M, D, (float)eps);
+  else add_rmsnorm_fwd_launch<16>(x, r, w, h, y, rstd, M, D, (float)eps);
+  return {h, y, rstd};
+}
+
 std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const at::Tensor& w, double eps) {
   CHECK_BF16(x);
   CHECK_BF16(w);
@@ -204,12 +253,33 @@ std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const at::Tensor& w, do
 
 template <int NV>
 void rmsnorm_bwd_launch(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, const at::Tensor& rstd, at::Tensor& dx,
-                        at::Tensor& part, int grid, int M, int D) {
-  hipLaunchKernelGGL(rmsnorm_bwd_kernel<NV>, dim3(grid), dim3(256), 0, cur_stream(), bp(dy), bp(x), bp(w),
-                     rstd.data_ptr<float>(), bpm(dx), part.data_ptr<float>(), M, D);
+                        at::Tensor& part, int grid, int M, int D, const u16* dres) {
+  if (dres)
+    hipLaunchKernelGGL((rmsnorm_bwd_kernel<NV, true>), dim3(grid), dim3(256), 0, cur_stream(), bp(dy), bp(x), bp(w),
+                       rstd.data_ptr<float>(), bpm(dx), part.data_ptr<float>(), M, D, dres);
+  else
+    hipLaunchKernelGGL((rmsnorm_bwd_kernel<NV, false>), dim3(grid), dim3(256), 0, cur_stream(), bp(dy), bp(x), bp(w),
+                       rstd.data_ptr<float>(), bpm(dx), part.data_ptr<float>(), M, D, nullptr);
 }
 
+std::vector<at::Tensor> rmsnorm_bwd_impl(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, const at::Tensor& rstd,
+                                         const u16* dres);
+
 std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, const at::Tensor& rstd) {
+  return rmsnorm_bwd_impl(dy, x, w, rstd, nullptr);
+}
+
+// Backward of add_rmsnorm: dx = rmsnorm_bwd(dy) + dres, where dres is the gradient that reached h
+// through the residual stream; the same dx is the gradient of both x and r.
+std::vector<at::Tensor> add_rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tensor& w, const at::Tensor& rstd,
+                                        const at::Tensor& dres) {
+  CHECK_BF16(dres);
+  TORCH_CHECK(dres.numel() == h.numel(), "add_rmsnorm_bwd: dres shape mismatch");
+  return rmsnorm_bwd_impl(dy, h, w, rstd, bp(dres));
+}
+
+std::vector<at::Tensor> rmsnorm_bwd_impl(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, const at::Tensor& rstd,
+                                         const u16* dres) {
   CHECK_BF16(dy);
   CHECK_BF16(x);
   CHECK_BF16(w);
@@ -224,11 +294,11 @@ std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, c
   auto part = at::empty({(int64_t)grid * 4, D}, x.options().dtype(at::kFloat));
   if (M > 0) {
     const int nv = (D + 511) / 512;
-    if (nv <= 1) rmsnorm_bwd_launch<1>(dy, x, w, rstd, dx, part, grid, M, D);
-    else if (nv <= 2) rmsnorm_bwd_launch<2>(dy, x, w, rstd, dx, part, grid, M, D);
-    else if (nv <= 4) rmsnorm_bwd_launch<4>(dy, x, w, rstd, dx, part, grid, M, D);
-    else if (nv <= 8) rmsnorm_bwd_launch<8>(dy, x, w, rstd, dx, part, grid, M, D);
-    else rmsnorm_bwd_launch<16>(dy, x, w, rstd, dx, part, grid, M, D);
+    if (nv <= 1) rmsnorm_bwd_launch<1>(dy, x, w, rstd, dx, part, grid, M, D, dres);
+    else if (nv <= 2) rmsnorm_bwd_launch<2>(dy, x, w, rstd, dx, part, grid, M, D, dres);
+    else if (nv <= 4) rmsnorm_bwd_launch<4>(dy, x, w, rstd, dx, part, grid, M, D, dres);
+    else if (nv <= 8) rmsnorm_bwd_launch<8>(dy, x, w, rstd, dx, part, grid, M, D, dres);
+    else rmsnorm_bwd_launch<16>(dy, x, w, rstd, dx, part, grid, M, D, dres);
   } else {
     part.zero_();
   }
@@ -688,6 +758,8 @@ PYBIND11_MODULE(_fused, m) {
   m.doc() = "gfx950 fused kernels for the Llama-3 DP validation workload";
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("add_rmsnorm_fwd", &add_rmsnorm_fwd);
+  m.def("add_rmsnorm_bwd", &add_rmsnorm_bwd);
   m.def("rope_split_fwd", &rope_split_fwd);
   m.def("rope_split_bwd", &rope_split_bwd);
   m.def("swiglu_fwd", &swiglu_fwd);

@@ -305,7 +305,7 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
 
 class Llama(torch.nn.Module):
     def __init__(self, cfg: LlamaConfig, device="cuda", seed: int = 0, checkpoint: bool = False, attn: str = "hip",
-                 gemm_layout: str = "nt", overlap_transposes: bool = False):
+                 gemm_layout: str = "nt", overlap_transposes: bool = False, fuse_residual: bool = True):
         super().__init__()
         if gemm_layout not in ("nt", "native"):
             raise ValueError("gemm_layout must be 'nt' or 'native'")
@@ -314,6 +314,7 @@ class Llama(torch.nn.Module):
         self.attn = attn
         self.gemm_layout = gemm_layout
         self.overlap_transposes = overlap_transposes
+        self.fuse_residual = fuse_residual  # residual add inside the RMSNorm kernels (fwd and bwd)
         # called with a parameter name before its first use in forward (ZeRO-1: wait for that
         # bucket's weight all-gather, parallel/dp.py BucketedAllReduce.wait_param)
         self.param_ready: Optional[Callable[[str], None]] = None
@@ -368,29 +369,40 @@ class Llama(torch.nn.Module):
             o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
         return o.transpose(1, 2)
 
-    def _layer(self, i: int, x: torch.Tensor, B: int, S: int) -> torch.Tensor:
+    def _norm(self, x: torch.Tensor, r: Optional[torch.Tensor], name: str):
+        """``(x + r, rmsnorm(x + r))`` — the residual add fused into the norm kernel; ``r=None``
+        is a plain norm of ``x`` (first layer)."""
+        if r is None:
+            return x, fused.rmsnorm(x, self.P(name), self.cfg.norm_eps)
+        if self.fuse_residual:
+            return fused.add_rmsnorm(x, r, self.P(name), self.cfg.norm_eps)
+        x = x + r
+        return x, fused.rmsnorm(x, self.P(name), self.cfg.norm_eps)
+
+    def _layer(self, i: int, x: torch.Tensor, B: int, S: int, r: Optional[torch.Tensor] = None):
+        """One block; returns ``(x, r)``: the residual stream and the block's last branch output, which
+        the next block's (or the final) norm adds in its own kernel."""
         cfg = self.cfg
         H, Hkv, Dh = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
-        h = fused.rmsnorm(x, self.P(f"l{i}.attn_norm"), cfg.norm_eps)
+        x, h = self._norm(x, r, f"l{i}.attn_norm")
         qkv = self._linear(h, f"l{i}.wqkv")
         q, k, v = fused.rope_split(qkv, self.rope_cos, self.rope_sin, B, S, H, Hkv, Dh)
         o = self._attention(q, k, v).reshape(B * S, H * Dh)  # [B, S, H, Dh] -> [B*S, H*Dh]
-        x = x + self._linear(o, f"l{i}.wo")
-        h = fused.rmsnorm(x, self.P(f"l{i}.ffn_norm"), cfg.norm_eps)
+        x, h = self._norm(x, self._linear(o, f"l{i}.wo"), f"l{i}.ffn_norm")
         a = _FlatLinearSwiGLU.apply(h, self.P(f"l{i}.w13").detach(), self.flat, f"l{i}.w13", self.gemm_layout == "nt",
                                     self.overlap_transposes)
-        x = x + self._linear(a, f"l{i}.w2")
-        return x
+        return x, self._linear(a, f"l{i}.w2")
 
     def forward(self, tokens: torch.Tensor, labels: Optional[torch.Tensor] = None) -> torch.Tensor:
         B, S = tokens.shape
         x = F.embedding(tokens.reshape(-1), self.P("tok_emb"))  # [B*S, D]
+        r = None
         for i in range(self.cfg.n_layers):
             if self.checkpoint and self.training:
-                x = torch.utils.checkpoint.checkpoint(self._layer, i, x, B, S, use_reentrant=False)
+                x, r = torch.utils.checkpoint.checkpoint(self._layer, i, x, B, S, r, use_reentrant=False)
             else:
-                x = self._layer(i, x, B, S)
-        x = fused.rmsnorm(x, self.P("norm"), self.cfg.norm_eps)
+                x, r = self._layer(i, x, B, S, r)
+        _, x = self._norm(x, r, "norm")
         logits = self._linear(x, "lm_head")  # [B*S, V]
         if labels is None:
             return logits.view(B, S, -1)

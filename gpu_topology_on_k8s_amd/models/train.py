@@ -62,7 +62,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
           attn: str = "hip", seed: int = 0, log: bool = True, gemm_tuning: str = "auto",
           gemm_table: Optional[str] = None, gemm_layout: str = "nt", overlap_transposes: bool = False,
           zero1: bool = False, save_dir: Optional[str] = None, save_every: int = 0, resume: Optional[str] = None,
-          keep: int = 2) -> Dict[str, object]:
+          keep: int = 2, fuse_residual: bool = True) -> Dict[str, object]:
     env = _init_dist(device_kind)
     if device_kind == "cuda":
         pl = _choose_device(env, placement, discovery)
@@ -76,7 +76,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         gemm_mode = "off"
     cfg = LlamaConfig.named(model_name)
     model = Llama(cfg, device=device, seed=seed, checkpoint=checkpoint, attn=attn, gemm_layout=gemm_layout,
-                  overlap_transposes=overlap_transposes)
+                  overlap_transposes=overlap_transposes, fuse_residual=fuse_residual)
     broadcast_params(model.flat)
     ar = BucketedAllReduce(model.flat, bucket_mb=bucket_mb, zero1=zero1)
     opt = FlatAdamW(model.flat, lr=lr, shards=ar.shards() if zero1 else None)
@@ -164,6 +164,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "gemm_tuning": gemm_mode,
         "gemm_layout": gemm_layout,
         "overlap_transposes": overlap_transposes,
+        "fuse_residual": fuse_residual,
         "step_start": start_step,
         "step_end": done[0],
         "resumed_from": resumed,
@@ -204,11 +205,13 @@ def main(argv=None) -> int:
     ap.add_argument("--keep", type=int, default=2, help="committed checkpoints to keep")
     ap.add_argument("--resume", default=None,
                     help="checkpoint root (its latest) or step directory; any world size / --zero1 setting")
+    ap.add_argument("--no-fuse-residual", action="store_true",
+                    help="separate residual-add kernels instead of the fused add+RMSNorm (A/B)")
     a = ap.parse_args(argv)
     train(a.model, a.batch, a.seq, a.steps, a.warmup, a.device, a.placement, a.discovery, a.bucket_mb, a.checkpoint, attn=a.attn,
           gemm_tuning=a.gemm_tuning, gemm_table=a.gemm_table, gemm_layout=a.gemm_layout,
           overlap_transposes=a.overlap_transposes, zero1=a.zero1, save_dir=a.save_dir, save_every=a.save_every,
-          resume=a.resume, keep=a.keep)
+          resume=a.resume, keep=a.keep, fuse_residual=not a.no_fuse_residual)
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0

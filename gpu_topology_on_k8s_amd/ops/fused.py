@@ -59,6 +59,40 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> torch.Tensor
     return rmsnorm_ref(x, w, eps)
 
 
+class _AddRMSNorm(torch.autograd.Function):
+    """``h = x + r; y = rmsnorm(h) * w`` as one node: the residual add lives in the norm kernel
+    (forward) and the residual-stream gradient is accumulated inside the norm's backward kernel."""
+
+    @staticmethod
+    def forward(ctx, x, r, w, eps):
+        h, y, rstd = hip().add_rmsnorm_fwd(x.contiguous(), r.contiguous(), w, float(eps))
+        ctx.save_for_backward(h, w, rstd)
+        return h, y
+
+    @staticmethod
+    def backward(ctx, dh, dy):
+        h, w, rstd = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros_like(h)
+        if dh is None:
+            dx, dw = hip().rmsnorm_bwd(dy.contiguous(), h, w, rstd)
+        else:
+            dx, dw = hip().add_rmsnorm_bwd(dy.contiguous(), h, w, rstd, dh.contiguous())
+        return dx, dx, dw, None
+
+
+def add_rmsnorm_ref(x: torch.Tensor, r: torch.Tensor, w: torch.Tensor, eps: float):
+    h = x + r
+    return h, rmsnorm_ref(h, w, eps)
+
+
+def add_rmsnorm(x: torch.Tensor, r: torch.Tensor, w: torch.Tensor, eps: float = 1e-5):
+    """``(h, y)`` with ``h = x + r`` (the new residual stream) and ``y = rmsnorm(h) * w``."""
+    if x.is_cuda:
+        return _AddRMSNorm.apply(x, r, w, eps)
+    return add_rmsnorm_ref(x, r, w, eps)
+
+
 # ------------------------------------------------------------------------------------ RoPE
 def rope_tables(seq: int, head_dim: int, theta: float = 500000.0, device=None,
                 scaling: dict | None = None) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -41,6 +41,46 @@ def test_rmsnorm_fwd_bwd(hip, M, D):
     assert _rel(dw, wf.grad) < 1e-2
 
 
+@pytest.mark.parametrize("M,D", [(1, 4096), (513, 4096), (33, 1000), (8, 8192)])
+def test_add_rmsnorm_fwd_bwd(hip, M, D):
+    """Fused residual add + RMSNorm vs fp32 autograd of h = x + r, y = rmsnorm(h) * w, with a
+    gradient arriving on both outputs (dh from the residual stream, dy from the branch)."""
+    torch.manual_seed(2)
+    x = torch.randn(M, D, device="cuda", dtype=torch.bfloat16)
+    r = torch.randn(M, D, device="cuda", dtype=torch.bfloat16)
+    w = (torch.rand(D, device="cuda") + 0.5).to(torch.bfloat16)
+    dy = torch.randn(M, D, device="cuda", dtype=torch.bfloat16)
+    dh = torch.randn(M, D, device="cuda", dtype=torch.bfloat16)
+    h, y, rstd = hip.add_rmsnorm_fwd(x, r, w, 1e-5)
+    assert torch.equal(h, x + r)  # bf16 residual stream, bit-identical to the separate add
+    xf, rf, wf = (t.float().requires_grad_(True) for t in (x, r, w))
+    hf = xf + rf
+    ref = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-5) * wf
+    assert _rel(y, ref) < 5e-3
+    torch.autograd.backward([ref, hf], [dy.float(), dh.float()])
+    dx, dw = hip.add_rmsnorm_bwd(dy, h, w, rstd, dh)
+    assert _rel(dx, xf.grad) < 1e-2 and torch.equal(xf.grad, rf.grad)
+    assert _rel(dw, wf.grad) < 1e-2
+
+
+def test_llama_fused_residual_matches_unfused_gpu():
+    """Whole tiny model: add+RMSNorm in one kernel (default) vs separate adds — same loss and
+    gradients to bf16 rounding."""
+    from gpu_topology_on_k8s_amd.models import Llama, LlamaConfig
+
+    cfg = LlamaConfig.tiny()
+    tok = torch.randint(0, cfg.vocab, (2, 128), device="cuda")
+    out = {}
+    for fuse in (False, True):
+        m = Llama(cfg, device="cuda", seed=3, fuse_residual=fuse)
+        m.flat.zero_grad()
+        loss = m(tok, torch.roll(tok, -1, 1))
+        loss.backward()
+        out[fuse] = (loss.item(), m.flat.grad.float().clone())
+    assert abs(out[True][0] - out[False][0]) < 1e-3
+    assert _rel(out[True][1], out[False][1]) < 1e-2
+
+
 @pytest.mark.parametrize("B,S,H,Hkv,Dh", [(2, 128, 32, 8, 128), (1, 77, 4, 2, 64), (1, 16, 8, 8, 32)])
 def test_rope_split_fwd_bwd(hip, B, S, H, Hkv, Dh):
     from gpu_topology_on_k8s_amd.ops.fused import rope_split_ref, rope_tables
