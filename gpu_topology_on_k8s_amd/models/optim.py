@@ -50,7 +50,9 @@ class FlatAdamW:
         return 3 * self.master.numel() * 4
 
     @torch.no_grad()
-    def step(self, grad_scale: float = 1.0) -> None:
+    def step(self, grad_scale: float = 1.0, sq: Optional[torch.Tensor] = None) -> None:
+        """``sq``: this rank's precomputed sum of squared gradients over its shards (the
+        data-parallel reducer's overlapped per-bucket norms); computed here when ``None``."""
         if self._deferred:
             cur = torch.cuda.current_stream(self.hp.device)
             for ev in self._deferred:
@@ -60,8 +62,7 @@ class FlatAdamW:
         b1, b2 = self.betas
         gs = torch.tensor(grad_scale, dtype=torch.float32, device=self.hp.device)
         if self.clip_norm is not None:
-            sq = None
-            for g in self._views(self.flat.grad):
+            for g in ([] if sq is not None else self._views(self.flat.grad)):
                 part = fused.hip().sq_norm(g) if g.is_cuda else g.float().pow(2).sum()
                 sq = part if sq is None else sq + part
             if self.sharded and dist.is_initialized() and dist.get_world_size(self.group) > 1:

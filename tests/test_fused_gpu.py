@@ -271,3 +271,35 @@ def test_smoke_step_and_training_gpu():
     from gpu_topology_on_k8s_amd.models.llama import smoke_step
 
     assert math.isfinite(smoke_step("cuda:0"))
+
+
+def test_overlapped_bucket_norm_matches_direct_gpu():
+    """Per-bucket squared norms computed on a side stream as buckets complete (parallel/dp.py
+    overlap_norm, installed even at world 1) equal the serial norm of the whole gradient, and a
+    clipped AdamW step fed with them matches the one that computes the norm itself."""
+    from gpu_topology_on_k8s_amd.models import FlatAdamW, Llama, LlamaConfig
+    from gpu_topology_on_k8s_amd.parallel.dp import BucketedAllReduce
+
+    cfg = LlamaConfig.tiny()
+    tok = torch.randint(0, cfg.vocab, (2, 128), device="cuda")
+    res = {}
+    for overlap in (True, False):
+        m = Llama(cfg, device="cuda", seed=3)
+        ar = BucketedAllReduce(m.flat, bucket_mb=0.05, first_bucket_mb=0.01, overlap_norm=overlap)
+        opt = FlatAdamW(m.flat, lr=1e-3, clip_norm=0.1)  # small clip: the norm decides the step
+        for _ in range(2):
+            m.flat.zero_grad()
+            m(tok, torch.roll(tok, -1, 1)).backward()
+            ar.finish()
+            sq = ar.sq_norm()
+            if overlap:
+                assert sq is not None and len(ar.buckets) > 3
+                want = m.flat.grad.float().pow(2).sum()
+                assert abs(sq.item() - want.item()) <= 1e-4 * want.item()
+            else:
+                assert sq is None
+            opt.step(grad_scale=ar.grad_scale, sq=sq)
+        torch.cuda.synchronize()
+        res[overlap] = m.flat.data.float().clone()
+        ar.remove()
+    assert _rel(res[True], res[False]) < 1e-3
