@@ -5,9 +5,9 @@ annotations.  The config-5 workload (``models/train.py``) is a
 job on the devices the extender placed it on, so it needs the usual save/resume:
 
     <dir>/step_000100/meta.json                 step, Adam t, flat layout, world, zero1   (rank 0)
-    <dir>/step_000100/weights.safetensors       "flat": bf16 [numel]                      (rank 0)
-    <dir>/step_000100/optim_rank{r}.safetensors "master"/"m"/"v": fp32 concatenation of the
-                                                rank's flat ranges, "shards": int64 [n, 2]
+    <dir>/step_000100/state_rank{r}.safetensors "flat" (bf16 weights), "master"/"m"/"v" (fp32):
+                                                the concatenation of the rank's flat ranges,
+                                                "shards": int64 [n, 2] = those ranges
     <dir>/step_000100/rng_rank{r}.safetensors   the rank's data-generator state
     <dir>/latest                                name of the newest committed step directory
 
@@ -22,9 +22,10 @@ Layout choices for MI355X:
   continues.  The commit (barrier, ``meta.json``, rename, ``latest``) runs on the main thread at the
   next :meth:`CheckpointWriter.save` or :meth:`CheckpointWriter.close`, so no collective is ever
   issued from the writer thread.
-- **ZeRO-1 shards are written by their owners.**  With ``--zero1`` each rank holds 1/W of the fp32
-  state (12 GB per GPU at W=8 for Llama-3-8B) and writes only that; without it every rank holds
-  the same state and only rank 0 writes.
+- **Every rank writes 1/W.**  With ``--zero1`` each rank writes the weights and fp32 state of its
+  own shards; without it the (replicated) state is split into W contiguous ranges, one per rank.
+  Either way a rank writes ~14 B x params / W (14 GB per GPU for Llama-3-8B at W=8) — no single
+  112 GB writer.
 - **Reshardable.**  Every optimizer file records the flat ranges it holds, and resume reads
   exactly the ranges the *new* layout owns (``safe_open(...).get_slice``, no full loads), so a job
   can resume on a different world size or switch ZeRO-1 on or off — what happens when the extender
@@ -45,13 +46,14 @@ import torch
 import torch.distributed as dist
 from safetensors import safe_open
 
-__all__ = ["CheckpointWriter", "write_safetensors", "load_checkpoint", "latest_checkpoint", "read_optimizer_ranges"]
+__all__ = ["CheckpointWriter", "write_safetensors", "read_ranges", "load_checkpoint", "latest_checkpoint", "read_optimizer_ranges"]
 
-FORMAT = 1
+FORMAT = 2
 
 
 _ST_DTYPES = {torch.float32: "F32", torch.bfloat16: "BF16", torch.float16: "F16", torch.int64: "I64",
               torch.int32: "I32", torch.uint8: "U8", torch.int8: "I8"}
+_ST_NAMES = {v: k for k, v in _ST_DTYPES.items()}
 
 
 def write_safetensors(path: str, tensors: Dict[str, torch.Tensor]) -> None:
@@ -79,6 +81,22 @@ def write_safetensors(path: str, tensors: Dict[str, torch.Tensor]) -> None:
         for t in order:
             if t.numel():
                 f.write(memoryview(t.reshape(-1).view(torch.uint8).numpy()))
+
+
+def _concat_offsets(shards) -> List[Tuple[int, int, int]]:
+    """(start, end, offset in the concatenation) for each shard."""
+    out, o = [], 0
+    for a, b in shards:
+        out.append((a, b, o))
+        o += b - a
+    return out
+
+
+def _to_concat(base, s: int) -> int:
+    for a, b, o in base:
+        if a <= s < b:
+            return o + s - a
+    raise ValueError(f"flat offset {s} is not in this rank's shards")
 
 
 def _rank_world() -> Tuple[int, int]:
@@ -120,15 +138,34 @@ class CheckpointWriter:
         os.makedirs(root, exist_ok=True)
 
     # -- snapshot ------------------------------------------------------------------------------
-    def _host(self, key: str, src: torch.Tensor) -> torch.Tensor:
-        """Device→host copy of ``src`` into a reused (pinned on GPU) buffer."""
-        if not src.is_cuda:
-            return src.detach().clone()
-        buf = self._pinned.get(key)
-        if buf is None or buf.numel() != src.numel() or buf.dtype != src.dtype:
-            buf = torch.empty(src.numel(), dtype=src.dtype, pin_memory=True)
-            self._pinned[key] = buf
-        buf.copy_(src.reshape(-1), non_blocking=True)
+    def write_ranges(self) -> List[Tuple[int, int]]:
+        """The flat-buffer ranges this rank writes: its ZeRO-1 shards, or (replicated state) a 1/W
+        contiguous slice, so every rank writes ~(2 + 12) B x params / W and no rank is the 112 GB
+        single writer of an 8 B-parameter model."""
+        if self.opt.sharded:
+            return [tuple(r) for r in self.opt.shards]
+        n = self.model.flat.numel
+        chunk = -(-n // (self.world * 8)) * 8
+        s, e = min(n, self.rank * chunk), min(n, (self.rank + 1) * chunk)
+        return [(s, e)] if e > s else []
+
+    def _gather(self, key: str, src: torch.Tensor, ranges, base) -> torch.Tensor:
+        """Device->host copy of ``src``'s ``ranges`` (concatenated) into a reused pinned buffer.
+        ``base`` maps a flat offset to ``src``'s index: 0 for the flat buffer, else the shard
+        concatenation offsets of the optimizer state."""
+        total = sum(e - s for s, e in ranges)
+        if src.is_cuda:
+            buf = self._pinned.get(key)
+            if buf is None or buf.numel() != total or buf.dtype != src.dtype:
+                buf = torch.empty(total, dtype=src.dtype, pin_memory=True)
+                self._pinned[key] = buf
+        else:
+            buf = torch.empty(total, dtype=src.dtype)
+        o = 0
+        for s, e in ranges:
+            i = s if base == 0 else _to_concat(base, s)
+            buf[o:o + e - s].copy_(src[i:i + e - s], non_blocking=src.is_cuda)
+            o += e - s
         return buf
 
     def prepare(self) -> None:
@@ -136,14 +173,10 @@ class CheckpointWriter:
         timed loop, instead of inside the first save."""
         if not self.model.flat.data.is_cuda:
             return
-        srcs = {"master": self.opt.master, "m": self.opt.m, "v": self.opt.v}
-        if self.rank == 0:
-            srcs["flat"] = self.model.flat.data
-        if not (self.opt.sharded or self.rank == 0):
-            srcs = {k: v for k, v in srcs.items() if k == "flat"}
-        for k, t in srcs.items():
+        total = sum(e - s for s, e in self.write_ranges())
+        for k, t in (("flat", self.model.flat.data), ("master", self.opt.master), ("m", self.opt.m), ("v", self.opt.v)):
             if k not in self._pinned:
-                self._pinned[k] = torch.empty(t.numel(), dtype=t.dtype, pin_memory=True)
+                self._pinned[k] = torch.empty(total, dtype=t.dtype, pin_memory=True)
 
     def _snapshot(self, gen: Optional[torch.Generator]) -> Tuple[Dict[str, Dict[str, torch.Tensor]], Optional[torch.cuda.Event]]:
         flat, opt = self.model.flat, self.opt
@@ -158,16 +191,15 @@ class CheckpointWriter:
             ctx = torch.cuda.stream(self._stream)
         else:
             ctx = _nullctx()
+        ranges = self.write_ranges()
         with ctx:
-            if self.rank == 0:
-                files["weights.safetensors"] = {"flat": self._host("flat", flat.data)}
-            if opt.sharded or self.rank == 0:
-                files[f"optim_rank{self.rank}.safetensors"] = {
-                    "master": self._host("master", opt.master),
-                    "m": self._host("m", opt.m),
-                    "v": self._host("v", opt.v),
-                    "shards": torch.tensor(opt.shards, dtype=torch.int64).reshape(-1, 2),
-                }
+            st = {"flat": self._gather("flat", flat.data, ranges, 0)}
+            # optimizer state is stored as the concatenation of opt.shards; map ranges into it
+            base = _concat_offsets(opt.shards)
+            for k in ("master", "m", "v"):
+                st[k] = self._gather(k, getattr(opt, k), ranges, base)
+            st["shards"] = torch.tensor(ranges, dtype=torch.int64).reshape(-1, 2)
+            files[f"state_rank{self.rank}.safetensors"] = st
         if dev.type == "cuda":
             ev = torch.cuda.Event()
             ev.record(self._stream)
@@ -282,17 +314,20 @@ class _nullctx:
         return False
 
 
-def read_optimizer_ranges(ckpt_dir: str, ranges: Sequence[Tuple[int, int]], keys=("master", "m", "v")) -> Dict[str, torch.Tensor]:
-    """The fp32 optimizer state of the flat ``ranges`` (concatenated in order), gathered from
-    whichever saved rank files hold them — independent of the world size they were written at."""
+def read_ranges(ckpt_dir: str, ranges: Sequence[Tuple[int, int]], keys=("master", "m", "v")) -> Dict[str, torch.Tensor]:
+    """``keys`` over the flat ``ranges`` (concatenated in order), gathered from whichever saved
+    rank files hold them — independent of the world size and ZeRO-1 setting they were written at."""
     total = sum(e - s for s, e in ranges)
-    out = {k: torch.empty(total, dtype=torch.float32) for k in keys}
+    out: Dict[str, torch.Tensor] = {}
     filled = 0
-    files = sorted(f for f in os.listdir(ckpt_dir) if f.startswith("optim_rank") and f.endswith(".safetensors"))
+    files = sorted(f for f in os.listdir(ckpt_dir) if f.startswith("state_rank") and f.endswith(".safetensors"))
     for fn in files:
         with safe_open(os.path.join(ckpt_dir, fn), framework="pt") as f:
             saved = f.get_tensor("shards").tolist()
             slices = {k: f.get_slice(k) for k in keys}
+            for k in keys:
+                if k not in out:
+                    out[k] = torch.empty(total, dtype=_ST_NAMES[slices[k].get_dtype()])
             off = 0
             for s, e in saved:
                 o = 0
@@ -304,9 +339,13 @@ def read_optimizer_ranges(ckpt_dir: str, ranges: Sequence[Tuple[int, int]], keys
                         filled += hi - lo
                     o += we - ws
                 off += e - s
-    if filled != total:
-        raise ValueError(f"{ckpt_dir}: saved optimizer ranges cover {filled} of the {total} elements requested")
+    if filled != total or len(out) != len(keys):
+        raise ValueError(f"{ckpt_dir}: saved ranges cover {filled} of the {total} elements requested")
     return out
+
+
+def read_optimizer_ranges(ckpt_dir: str, ranges: Sequence[Tuple[int, int]]) -> Dict[str, torch.Tensor]:
+    return read_ranges(ckpt_dir, ranges, ("master", "m", "v"))
 
 
 def load_checkpoint(path: str, model, opt=None, gen: Optional[torch.Generator] = None) -> Dict[str, object]:
@@ -322,8 +361,7 @@ def load_checkpoint(path: str, model, opt=None, gen: Optional[torch.Generator] =
     flat = model.flat
     if meta["numel"] != flat.numel or meta["layout"] != _layout(flat):
         raise ValueError(f"{d}: flat parameter layout does not match this model ({meta['model']!r})")
-    with safe_open(os.path.join(d, "weights.safetensors"), framework="pt") as f:
-        w = f.get_tensor("flat")
+    w = read_ranges(d, [(0, flat.numel)], ("flat",))["flat"]
     with torch.no_grad():
         flat.data.copy_(w.to(flat.data.dtype), non_blocking=False)
     if opt is not None:

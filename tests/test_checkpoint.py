@@ -10,7 +10,7 @@ import torch.multiprocessing as mp
 from safetensors import safe_open
 
 from gpu_topology_on_k8s_amd.models import CheckpointWriter, FlatAdamW, Llama, LlamaConfig, load_checkpoint
-from gpu_topology_on_k8s_amd.models.checkpoint import latest_checkpoint, read_optimizer_ranges
+from gpu_topology_on_k8s_amd.models.checkpoint import latest_checkpoint, read_optimizer_ranges, read_ranges
 
 
 def _free_port():
@@ -87,7 +87,7 @@ def test_optimizer_ranges_reshard(tmp_path):
     for r, sh in enumerate(shards):
         t = {k: torch.cat([full[k][s:e] for s, e in sh]) for k in full}
         t["shards"] = torch.tensor(sh, dtype=torch.int64)
-        save_file(t, str(tmp_path / f"optim_rank{r}.safetensors"))
+        save_file(t, str(tmp_path / f"state_rank{r}.safetensors"))
     for ranges in ([(0, n)], [(0, 500)], [(500, 1000)], [(50, 120), (600, 990)]):
         got = read_optimizer_ranges(str(tmp_path), ranges)
         for k in full:
@@ -105,9 +105,28 @@ def _worker(rank, world, port, root, q):
     a = train("tiny", steps=4, save_dir=os.path.join(root, "a"), **kw)
     b1 = train("tiny", steps=2, save_dir=os.path.join(root, "b"), save_every=1, **kw)
     b2 = train("tiny", steps=2, save_dir=os.path.join(root, "b"), resume=os.path.join(root, "b"), **kw)
+    # replicated (no ZeRO-1): each rank writes half of the state; resume is exact too
+    kw["zero1"] = False
+    train("tiny", steps=3, save_dir=os.path.join(root, "c"), **kw)
+    train("tiny", steps=1, save_dir=os.path.join(root, "d"), **kw)
+    train("tiny", steps=2, save_dir=os.path.join(root, "d"), resume=os.path.join(root, "d"), **kw)
     q.put((rank, {"a": a["step_end"], "b1": b1["checkpoints_saved"], "b2": (b2["step_start"], b2["step_end"]),
                   "loss_a": a["loss_last"], "loss_b": b2["loss_last"]}))
     dist.destroy_process_group()
+
+
+def test_replicated_state_is_split_over_ranks(tmp_path):
+    """Without ZeRO-1 every rank writes a 1/W slice (8-aligned) of weights and optimizer state."""
+    m = Llama(LlamaConfig.tiny(), device="cpu")
+    opt = FlatAdamW(m.flat)
+    n = m.flat.numel
+    spans = []
+    for r in range(3):
+        w = CheckpointWriter.__new__(CheckpointWriter)
+        w.model, w.opt, w.rank, w.world = m, opt, r, 3
+        spans += w.write_ranges()
+    assert spans[0][0] == 0 and spans[-1][1] == n and all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    assert all(s % 8 == 0 for s, _ in spans)
 
 
 def test_zero1_two_ranks_resume_matches_continuous_and_reshards_to_one(tmp_path):
@@ -127,16 +146,23 @@ def test_zero1_two_ranks_resume_matches_continuous_and_reshards_to_one(tmp_path)
         assert res[r]["loss_a"] == res[r]["loss_b"]
     da, db = latest_checkpoint(str(tmp_path / "a")), latest_checkpoint(str(tmp_path / "b"))
     assert da.endswith("step_000004") and db.endswith("step_000004")
-    # each ZeRO-1 rank wrote only its own shard
-    assert sorted(f for f in os.listdir(da) if f.startswith("optim")) == ["optim_rank0.safetensors", "optim_rank1.safetensors"]
-    with safe_open(os.path.join(da, "weights.safetensors"), "pt") as fa, safe_open(os.path.join(db, "weights.safetensors"), "pt") as fb:
-        assert torch.equal(fa.get_tensor("flat"), fb.get_tensor("flat"))  # resumed run == continuous run
+    # each ZeRO-1 rank wrote only its own shard (weights and optimizer state)
+    assert sorted(f for f in os.listdir(da) if f.startswith("state")) == ["state_rank0.safetensors", "state_rank1.safetensors"]
+    numel = json.load(open(os.path.join(da, "meta.json")))["numel"]
+    wa = read_ranges(da, [(0, numel)], ("flat",))["flat"]
+    wb = read_ranges(db, [(0, numel)], ("flat",))["flat"]
+    assert wa.dtype == torch.bfloat16 and torch.equal(wa, wb)  # resumed run == continuous run
+    dc, dd = latest_checkpoint(str(tmp_path / "c")), latest_checkpoint(str(tmp_path / "d"))
+    assert sorted(f for f in os.listdir(dc) if f.startswith("state")) == ["state_rank0.safetensors", "state_rank1.safetensors"]
+    keys = ("flat", "master", "m", "v")
+    sc, sd = read_ranges(dc, [(0, numel)], keys), read_ranges(dd, [(0, numel)], keys)
+    assert all(torch.equal(sc[k], sd[k]) for k in keys)
     # reshard: the 2-rank ZeRO-1 state resumes into one unsharded optimizer (world 1)
     m = Llama(LlamaConfig.tiny(), device="cpu", seed=3)
     opt = FlatAdamW(m.flat)
     meta = load_checkpoint(da, m, opt)
     assert meta["world"] == 2 and meta["zero1"] and opt.t == 4
-    for fn in ("optim_rank0.safetensors", "optim_rank1.safetensors"):
+    for fn in ("state_rank0.safetensors", "state_rank1.safetensors"):
         with safe_open(os.path.join(da, fn), "pt") as f:
             o = 0
             master = f.get_tensor("master")
@@ -174,10 +200,9 @@ def test_async_checkpoint_on_gpu_resumes_exactly(tmp_path):
     torch.cuda.synchronize()
     want = m.flat.data.clone()
     d = latest_checkpoint(str(tmp_path))
-    with safe_open(os.path.join(d, "weights.safetensors"), "pt") as f:
-        assert torch.equal(f.get_tensor("flat"), snap[0].cpu())  # the snapshot, not later state
-    with safe_open(os.path.join(d, "optim_rank0.safetensors"), "pt") as f:
-        assert torch.equal(f.get_tensor("master"), snap[1].cpu()) and torch.equal(f.get_tensor("v"), snap[2].cpu())
+    st = read_ranges(d, [(0, m.flat.numel)], ("flat", "master", "v"))
+    assert torch.equal(st["flat"], snap[0].cpu())  # the snapshot, not later state
+    assert torch.equal(st["master"], snap[1].cpu()) and torch.equal(st["v"], snap[2].cpu())
     m2 = Llama(cfg, device=dev, seed=7)
     opt2 = FlatAdamW(m2.flat, lr=1e-3)
     gen2 = torch.Generator()
