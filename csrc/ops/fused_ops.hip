@@ -289,7 +289,9 @@ std::vector<at::Tensor> rmsnorm_bwd_impl(const at::Tensor& dy, const at::Tensor&
   TORCH_CHECK(dy.numel() == x.numel() && rstd.numel() == M, "rmsnorm_bwd: shape mismatch");
   auto dx = at::empty_like(x);
   auto dw = at::empty({D}, w.options());
-  // 1024 waves (4 per CU) fill the chip; each takes M/1024 rows so the dW partials stay at 16 MB
+  // 1024 waves (4 per CU) fill the chip; each takes M/1024 rows so the dW partials stay at 16 MB.
+  // 2048 waves measured slower for the fused (ACC) variant at [16384, 4096]: 160.4 vs 143.5 us
+  // (bench/norm_bench.py; the plain variant went 197 -> 171 us incl. its separate add).
   int grid = std::max(1, std::min((M + 3) / 4, 256));
   auto part = at::empty({(int64_t)grid * 4, D}, x.options().dtype(at::kFloat));
   if (M > 0) {
