@@ -257,7 +257,7 @@ def main(argv=None) -> int:
                                via_k8s=args.via == "k8s")
         env.store.set("gtk/subset", choice.to_json())
     choice = SubsetChoice.from_json(env.store.get("gtk/subset").decode())
-    device = choice.devices[env.rank]
+    device = choice.hip_devices[env.rank]  # HIP ordinal of node device choice.devices[rank] (PCI-address map)
     tdev = "cpu" if cpu else f"cuda:{device}"
     barrier_kw = {} if cpu else {"device_ids": [device]}
 
@@ -363,6 +363,7 @@ def main(argv=None) -> int:
                 "seq_len": None,
                 "parallelism": f"dp{env.world}",
                 "subset": choice.devices,
+                "hip_devices": choice.hip_devices,
                 "placement_score": choice.score,
                 "placement_ms": choice.placement_ms,
                 "worst_subset": choice.worst,

@@ -79,8 +79,10 @@ double Engine::evaluate(const std::vector<int>& ids, Terms* terms) const {
   return t.comm + pol_.w_span * t.span + pol_.w_frag * t.frag + pol_.w_fit * t.fit + pol_.w_access * t.access;
 }
 
-void Engine::greedy(int k, const std::vector<int>& F, std::vector<int>* best, double* best_j) const {
+void Engine::greedy(int k, const std::vector<int>& F, std::vector<int>* best, double* best_j, bool maximise) const {
   // Greedy growth from every seed, then first-improvement 1-swap descent (core._greedy_local).
+  // `maximise` flips the direction (worst-placement search): sgn*J is minimised either way.
+  const double sgn = maximise ? -1.0 : 1.0;
   for (int seed : F) {
     std::vector<int> cur{seed};
     while ((int)cur.size() < k) {
@@ -89,7 +91,7 @@ void Engine::greedy(int k, const std::vector<int>& F, std::vector<int>* best, do
       for (int c : F) {
         if (std::find(cur.begin(), cur.end(), c) != cur.end()) continue;
         cur.push_back(c);
-        double j = evaluate(cur, nullptr);
+        double j = sgn * evaluate(cur, nullptr);
         cur.pop_back();
         if (j < cj - kEps) {
           cj = j;
@@ -98,7 +100,7 @@ void Engine::greedy(int k, const std::vector<int>& F, std::vector<int>* best, do
       }
       cur.push_back(cand);
     }
-    double cur_j = evaluate(cur, nullptr);
+    double cur_j = sgn * evaluate(cur, nullptr);
     bool improved = true;
     while (improved) {
       improved = false;
@@ -107,7 +109,7 @@ void Engine::greedy(int k, const std::vector<int>& F, std::vector<int>* best, do
           if (std::find(cur.begin(), cur.end(), b) != cur.end()) continue;
           std::vector<int> trial = cur;
           trial[a] = b;
-          double tj = evaluate(trial, nullptr);
+          double tj = sgn * evaluate(trial, nullptr);
           if (tj < cur_j - kEps) {
             cur = trial;
             cur_j = tj;
@@ -118,9 +120,11 @@ void Engine::greedy(int k, const std::vector<int>& F, std::vector<int>* best, do
       }
     }
     std::sort(cur.begin(), cur.end());
-    if (cur_j < *best_j - kEps || (std::fabs(cur_j - *best_j) <= kEps && (best->empty() || cur < *best))) {
+    // best_j is kept in the caller's sign convention (a real objective value)
+    const double bj = sgn * *best_j;
+    if (cur_j < bj - kEps || (std::fabs(cur_j - bj) <= kEps && (best->empty() || cur < *best))) {
       *best = cur;
-      *best_j = cur_j;
+      *best_j = sgn * cur_j;
     }
   }
 }
@@ -202,7 +206,7 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
   if (log_comb > std::log(2.0e5)) {  // (with collect_ties the DFS re-finds the seed and lists it)
     std::vector<int> g;
     double gj = std::numeric_limits<double>::infinity();
-    greedy(k, F, &g, &gj);
+    greedy(k, F, &g, &gj, false);
     best_j = gj;
     for (int dev : g) best_pos.push_back((int)(std::lower_bound(F.begin(), F.end(), dev) - F.begin()));
   }
@@ -275,7 +279,7 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
   if (aborted && best_pos.size() != (size_t)k) {
     double gj = std::numeric_limits<double>::infinity();
     std::vector<int> g;
-    greedy(k, F, &g, &gj);
+    greedy(k, F, &g, &gj, false);
     ids = g;
   }
   res.ids = ids;
@@ -297,7 +301,10 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
   return res;
 }
 
-Result Engine::worst(int k) const {
+Result Engine::worst(int k, uint64_t node_limit) const {
+  // Exhaustive when C(m, k) fits the budget (lexicographic, first strict maximum: the same set as
+  // itertools.combinations + first-maximum in core.worst); otherwise greedy ascent + 1-swap from
+  // every seed with exact=false.  CPX nodes (64 XCPs, k=8: C(64,8) ~ 4.4e9) take the second path.
   Result res;
   const int n = p_.n;
   std::vector<int> F;
@@ -305,23 +312,31 @@ Result Engine::worst(int k) const {
     if (p_.free[i]) F.push_back(i);
   const int m = (int)F.size();
   if (k <= 0 || m < k) return res;
-  std::vector<int> idx(k);
-  std::iota(idx.begin(), idx.end(), 0);
-  double bj = -std::numeric_limits<double>::infinity();
-  std::vector<int> cur(k), best;
-  while (true) {
-    for (int i = 0; i < k; ++i) cur[i] = F[idx[i]];
-    double j = evaluate(cur, nullptr);
-    ++res.leaves;
-    if (j > bj + kEps) {
-      bj = j;
-      best = cur;
+  const double log_comb = std::lgamma(m + 1.0) - std::lgamma(k + 1.0) - std::lgamma(m - k + 1.0);
+  std::vector<int> best;
+  if (log_comb <= std::log((double)std::max<uint64_t>(node_limit, 1))) {
+    std::vector<int> idx(k);
+    std::iota(idx.begin(), idx.end(), 0);
+    double bj = -std::numeric_limits<double>::infinity();
+    std::vector<int> cur(k);
+    while (true) {
+      for (int i = 0; i < k; ++i) cur[i] = F[idx[i]];
+      double j = evaluate(cur, nullptr);
+      ++res.leaves;
+      if (j > bj + kEps) {
+        bj = j;
+        best = cur;
+      }
+      int i = k - 1;
+      while (i >= 0 && idx[i] == m - k + i) --i;
+      if (i < 0) break;
+      ++idx[i];
+      for (int q = i + 1; q < k; ++q) idx[q] = idx[q - 1] + 1;
     }
-    int i = k - 1;
-    while (i >= 0 && idx[i] == m - k + i) --i;
-    if (i < 0) break;
-    ++idx[i];
-    for (int q = i + 1; q < k; ++q) idx[q] = idx[q - 1] + 1;
+  } else {
+    double bj = -std::numeric_limits<double>::infinity();
+    greedy(k, F, &best, &bj, /*maximise=*/true);
+    res.exact = false;
   }
   res.ids = best;
   res.objective = evaluate(best, &res.terms);

@@ -64,8 +64,9 @@ class Engine {
   // With `collect_ties` the bound prunes only strictly worse branches and the optima (at most
   // `max_ties`) come back in Result::ties.
   Result select(int k, uint64_t node_limit, bool collect_ties = false, size_t max_ties = 65536) const;
-  // Highest-objective subset (exhaustive; intended for n <= ~24) — "worst placement" baseline.
-  Result worst(int k) const;
+  // Highest-objective subset ("worst placement" baseline of BASELINE config 5): exhaustive when
+  // C(free, k) <= node_limit, else greedy ascent + 1-swap (exact=false).
+  Result worst(int k, uint64_t node_limit = 2000000) const;
   // Objective of an arbitrary set.
   double evaluate(const std::vector<int>& ids, Terms* terms) const;
 
@@ -77,7 +78,7 @@ class Engine {
     int min_groups_k = 0;      // groups needed to host k (filled per query)
   };
   int min_groups(const Level& lv, int k) const;
-  void greedy(int k, const std::vector<int>& free_ids, std::vector<int>* best, double* best_j) const;
+  void greedy(int k, const std::vector<int>& free_ids, std::vector<int>* best, double* best_j, bool maximise) const;
 
   Problem p_;
   Policy pol_;

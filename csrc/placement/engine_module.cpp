@@ -96,13 +96,22 @@ PYBIND11_MODULE(_placement, m) {
       [](py::array_t<double, py::array::c_style | py::array::forcecast> cost,
          py::array_t<bool, py::array::c_style | py::array::forcecast> free_mask, const std::vector<std::vector<int>>& levels,
          py::array_t<double, py::array::c_style | py::array::forcecast> access, int k, double w_span, double w_frag,
-         double w_fit, double w_access) {
+         double w_fit, double w_access, uint64_t node_limit) {
         Problem p = make_problem(cost, free_mask, levels, access);
-        Engine e(p, make_policy(w_span, w_frag, w_fit, w_access));
-        return to_dict(e.worst(k), 0.0);
+        Result r;
+        double us = 0;
+        {
+          py::gil_scoped_release nogil;
+          auto t0 = std::chrono::steady_clock::now();
+          Engine e(p, make_policy(w_span, w_frag, w_fit, w_access));
+          r = e.worst(k, node_limit);
+          us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        }
+        return to_dict(r, us);
       },
       py::arg("cost"), py::arg("free"), py::arg("levels"), py::arg("access"), py::arg("k"), py::arg("w_span") = 0.5,
-      py::arg("w_frag") = 0.25, py::arg("w_fit") = 0.05, py::arg("w_access") = 0.1);
+      py::arg("w_frag") = 0.25, py::arg("w_fit") = 0.05, py::arg("w_access") = 0.1,
+      py::arg("node_limit") = (uint64_t)2000000);
   m.def(
       "evaluate",
       [](py::array_t<double, py::array::c_style | py::array::forcecast> cost,

@@ -10,15 +10,16 @@
 
 using namespace gtk;
 
-static double brute(const Engine& e, const std::vector<int>& F, int k, std::vector<int>* best) {
+static double brute(const Engine& e, const std::vector<int>& F, int k, std::vector<int>* best, bool maximise = false) {
   const int m = (int)F.size();
   std::vector<int> idx(k);
   for (int i = 0; i < k; ++i) idx[i] = i;
+  const double sgn = maximise ? -1.0 : 1.0;
   double bj = INFINITY;
   std::vector<int> cur(k);
   while (true) {
     for (int i = 0; i < k; ++i) cur[i] = F[idx[i]];
-    double j = e.evaluate(cur, nullptr);
+    double j = sgn * e.evaluate(cur, nullptr);
     if (j < bj - kEps) {
       bj = j;
       *best = cur;
@@ -29,7 +30,7 @@ static double brute(const Engine& e, const std::vector<int>& F, int k, std::vect
     ++idx[i];
     for (int q = i + 1; q < k; ++q) idx[q] = idx[q - 1] + 1;
   }
-  return bj;
+  return sgn * bj;
 }
 
 int main() {
@@ -67,6 +68,14 @@ int main() {
       if (!r.exact || r.ids != bb || std::fabs(r.objective - bj) > 1e-9) {
         ++failures;
         std::printf("MISMATCH n=%d k=%d bnb_j=%.12f brute_j=%.12f\n", n, k, r.objective, bj);
+      }
+      std::vector<int> wb;
+      double wj = brute(e, F, k, &wb, /*maximise=*/true);
+      Result w = e.worst(k, 50000000ull);
+      ++cases;
+      if (!w.exact || w.ids != wb || std::fabs(w.objective - wj) > 1e-9) {
+        ++failures;
+        std::printf("WORST MISMATCH n=%d k=%d worst_j=%.12f brute_j=%.12f\n", n, k, w.objective, wj);
       }
     }
   }

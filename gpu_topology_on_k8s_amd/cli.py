@@ -100,14 +100,42 @@ def cmd_config(a) -> int:
     return 0
 
 
+def validate_devices(a, env=None) -> List[int]:
+    """HIP ordinals to validate: ``--devices`` (ordinals) as given; else the pod's node-local GROUP
+    (``--group`` or ``GTK_GPU_GROUP``) resolved through ``GTK_GPU_BDFS`` / ``--topology`` by PCI
+    address (:func:`topology.identity.resolve_group`); else every visible device."""
+    from .topology.identity import ENV_BDFS, group_from_env, hip_device_bdfs, resolve_group
+
+    if a.devices:
+        return _ints(a.devices)
+    env = os.environ if env is None else env
+    group, bdfs = group_from_env(env)
+    if a.group:
+        group = _ints(a.group)
+        bdfs = [b for b in (a.bdfs or "").split(",") if b.strip()]
+    elif a.bdfs:
+        bdfs = [b for b in a.bdfs.split(",") if b.strip()]
+    vis = hip_device_bdfs() if a.visible_bdfs is None else [b for b in a.visible_bdfs.split(",") if b.strip()]
+    if not group:
+        return list(range(len(vis)))
+    topo = None
+    if a.topology:
+        from .topology.model import Topology
+
+        with open(a.topology) as f:
+            topo = Topology.from_json(f.read())
+    if bdfs and len(bdfs) != len(group):
+        raise SystemExit(f"{ENV_BDFS} has {len(bdfs)} entries for GROUP {group}")
+    return resolve_group(group, bdfs=bdfs or None, topology=topo, visible_bdfs=vis)
+
+
 def cmd_validate(a) -> int:
     from ._native import load
 
-    devs = _ints(a.devices) or _ints(os.environ.get("GTK_GPU_GROUP", ""))
-    if not devs:
-        import torch
-
-        devs = list(range(torch.cuda.device_count()))
+    devs = validate_devices(a)
+    if a.resolve_only:
+        print(json.dumps({"hip_devices": devs}))
+        return 0
     rccl = load("_rccl")
     sizes = rccl.size_sweep(a.min_bytes, a.max_bytes, a.factor)
     pts = rccl.local_sweep(devs, sizes, a.dtype, a.iters, a.warmup, False, True)
@@ -169,7 +197,12 @@ def main(argv=None) -> int:
     p.add_argument("--image", default="rocm/gpu-topology-k8s:latest")
     p.set_defaults(fn=cmd_config)
     p = sub.add_parser("validate")
-    p.add_argument("--devices", default="")
+    p.add_argument("--devices", default="", help="HIP ordinals (skips GROUP resolution)")
+    p.add_argument("--group", default="", help="node-local device indices (default: $GTK_GPU_GROUP)")
+    p.add_argument("--bdfs", default="", help="PCI addresses of --group, same order (default: $GTK_GPU_BDFS)")
+    p.add_argument("--topology", default="", help="node topology JSON mapping GROUP indices to PCI addresses")
+    p.add_argument("--visible-bdfs", default=None, help=argparse.SUPPRESS)  # tests: stand-in for hipDeviceGetPCIBusId
+    p.add_argument("--resolve-only", action="store_true", help="print the HIP ordinals and exit")
     p.add_argument("--min-bytes", type=int, default=1 << 20)
     p.add_argument("--max-bytes", type=int, default=1 << 30)
     p.add_argument("--factor", type=int, default=4)

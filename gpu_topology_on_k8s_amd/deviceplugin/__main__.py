@@ -20,7 +20,7 @@ from ..k8s.annotations import Contract
 from ..placement import PlacementPolicy
 from ..topology.discovery import discover
 from .health import HealthMonitor
-from .plugin import DevicePluginServer, PluginConfig
+from .plugin import DevicePluginServer, PluginConfig, startup_topology
 from .proto import DEVICE_PLUGIN_PATH
 
 
@@ -48,7 +48,12 @@ def main(argv=None) -> int:
     ap.add_argument("--probe", default="off", choices=["off", "quick", "full"])
     ap.add_argument("--apiserver", default="", help="apiserver URL; default in-cluster; 'none' disables annotations")
     ap.add_argument("--token", default="")
-    ap.add_argument("--dev-root", default="/dev")
+    ap.add_argument("--dev-root", default="/dev", help="where the ROCm device nodes live (a placeholder dir on kind)")
+    ap.add_argument("--device-specs", default="auto", choices=["auto", "strict", "stub"],
+                    help="Allocate DeviceSpecs: strict = kfd + render/card nodes, fail if missing; stub = only nodes "
+                         "that exist under --dev-root (kind / fake GPUs); auto = stub for --discovery fake, else strict")
+    ap.add_argument("--metrics-port", type=int, default=0, help="serve Prometheus /metrics on this port (0 = off)")
+    ap.add_argument("--metrics-host", default="0.0.0.0")
     ap.add_argument("--health-interval", type=float, default=10.0)
     ap.add_argument("--reprobe-interval", type=float, default=0.0,
                     help="re-measure the links (child process) every N s while no pod holds a device; 0 = never")
@@ -62,24 +67,27 @@ def main(argv=None) -> int:
     log = logging.getLogger("gtk.deviceplugin")
 
     topo = discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus)
+    api = make_api(a.apiserver, a.token)
+    contract = Contract(resource_name=a.resource_name, prefix=a.annotation_prefix)
+    probe_fn = None
     if a.probe != "off" and a.discovery != "fake":
         # in a child process: the plugin lives as long as the node and must not hold HIP contexts
         # and probe buffers on every GPU it hands out to pods
         from ..ops.probe import probe_in_child
 
-        probed, msg = probe_in_child(a.probe, backend=a.discovery)
-        if probed is not None and probed.n == topo.n:
-            probed.node_name = topo.node_name
-            topo = probed
-            log.info("probe (%s): %s", msg, topo.probe)
-        else:
-            log.warning("link probe unavailable (%s); publishing discovered link classes", msg)
-    log.info("topology:\n%s", topo.render())
+        def probe_fn():
+            probed, msg = probe_in_child(a.probe, backend=a.discovery)
+            log.info("probe: %s", msg)
+            return probed
+    names = (a.resource_name, "aliyun.com/gpu", "aliyun.com/gpu-count")
+    topo, how = startup_topology(topo, api, a.node_name, contract, names, probe_fn)
+    log.info("link matrix: %s; topology:\n%s", how, topo.render())
 
     health = HealthMonitor(topo, lambda: discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus))
 
+    specs = a.device_specs if a.device_specs != "auto" else ("stub" if a.discovery == "fake" else "strict")
     cfg = PluginConfig(resource_name=a.resource_name, socket_dir=a.socket_dir, socket_name=a.socket_name, dev_root=a.dev_root,
-                       node_name=a.node_name, contract=Contract(resource_name=a.resource_name, prefix=a.annotation_prefix),
+                       node_name=a.node_name, contract=contract, device_specs=specs,
                        health_interval=a.health_interval, reprobe_interval=a.reprobe_interval,
                        reprobe_tolerance=a.reprobe_tolerance,
                        policy=PlacementPolicy(partition_aware=a.partition_aware == "on"))
@@ -89,8 +97,11 @@ def main(argv=None) -> int:
 
         def reprobe():
             return probe_in_child(a.probe if a.probe != "off" else "quick", backend=a.discovery)[0]
-    plugin = DevicePluginServer(topo, cfg, api=make_api(a.apiserver, a.token), health_fn=health if a.discovery != "fake" else None,
-                                reprobe_fn=reprobe)
+    plugin = DevicePluginServer(topo, cfg, api=api, health_fn=health if a.discovery != "fake" else None, reprobe_fn=reprobe)
+    if a.metrics_port:
+        from .metrics import serve_metrics
+
+        serve_metrics(plugin.metrics, a.metrics_host, a.metrics_port)
     done = threading.Event()
     for sig in (signal.SIGINT, signal.SIGTERM):  # installed before serving: a stop never races start-up
         signal.signal(sig, lambda *_: done.set())

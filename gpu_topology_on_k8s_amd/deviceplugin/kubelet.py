@@ -182,6 +182,11 @@ class FakeKubelet:
                 areq.container_requests.add(devices_ids=chosen[pos:pos + n])
                 pos += n
             resp = self._stub(p, "Allocate")(areq, timeout=10)
+            # what containerd does next: every DeviceSpec must name a device node that exists on the
+            # host, or the container is never created (BASELINE config 1 on a kind node)
+            missing = [d.host_path for c in resp.container_responses for d in c.devices if not os.path.exists(d.host_path)]
+            if missing:
+                raise AdmissionError(f"CreateContainerError: device nodes do not exist on the node: {missing}")
             self.allocated[resource][key] = tuple(chosen)
             self.responses[key] = resp
         if self.api is not None and hasattr(self.api, "set_pod_phase"):

@@ -30,23 +30,93 @@ from concurrent import futures
 from typing import Callable, Dict, Iterable, List, Optional, Sequence, Set, Tuple
 
 import grpc
+import numpy as np
 
-from ..k8s.annotations import ANN_ASSIGNED, ANN_ASSUME_TIME, ANN_GROUP, Contract, PodAssignment, encode_node_annotations, format_group
+from ..k8s.annotations import (ANN_ASSIGNED, ANN_ASSUME_TIME, ANN_GROUP, Contract, PodAssignment, decode_node_annotations,
+                               encode_node_annotations, format_group)
 from ..k8s.api import Conflict, KubeAPI
+from ..k8s.events import record_event
 from ..k8s.objects import annotations as obj_annotations
 from ..k8s.objects import meta, pod_gpu_request, pod_is_terminal, pod_phase
-from ..placement import PlacementPolicy
+from ..placement import NoFeasiblePlacement, PlacementPolicy
 from ..placement.core import select_with
+from ..topology.cpus import format_cpulist, parse_cpulist
+from ..topology.identity import ENV_BDFS, ENV_GROUP
 from ..topology.model import Topology
 from . import proto as pb
+from .metrics import PluginMetrics
 
 log = logging.getLogger(__name__)
 
-__all__ = ["DevicePluginServer", "PluginConfig"]
+__all__ = ["DevicePluginServer", "PluginConfig", "placeholder_dev_tree", "node_is_idle", "startup_topology"]
 
 #: pod annotation whose ``KEY=VALUE`` lines are passed into the container (RCCL / NCCL tuning only)
 RCCL_ENV_ANNOTATION_SUFFIX = "rccl-env"
 _ENV_PREFIXES = ("NCCL_", "RCCL_", "HSA_", "HIP_", "GPU_MAX_HW_QUEUES")
+
+
+def node_is_idle(api: KubeAPI, node_name: str, resource_names: Sequence[str]) -> bool:
+    """True when no live pod on ``node_name`` holds a device: neither an annotated GROUP (assumed or
+    allocated) nor a device request scheduled around the extender.  Any API error counts as busy."""
+    try:
+        pods = [p for p in api.list_pods(node_name=node_name) if not pod_is_terminal(p)]
+    except Exception as e:
+        log.warning("listing pods on %s failed: %s", node_name, e)
+        return False
+    for p in pods:
+        if PodAssignment.from_annotations(obj_annotations(p)) is not None:
+            return False
+        try:
+            if pod_gpu_request(p, resource_names) > 0:
+                return False
+        except ValueError:
+            return False
+    return True
+
+
+def startup_topology(discovered: Topology, api: Optional[KubeAPI], node_name: str, contract: Contract,
+                     resource_names: Sequence[str], probe_fn: Optional[Callable[[], Optional[Topology]]]) -> Tuple[Topology, str]:
+    """The topology a (re)starting plugin publishes, and how it was obtained.
+
+    A plugin restart or upgrade on a node running jobs must not saturate every xGMI link under live
+    training (and publish contention-skewed costs): while any pod holds a device the measured matrix
+    already on the node annotation is carried over onto the fresh discovery (same devices, same PCI
+    addresses) and no probe runs.  The probe runs only on an idle node (or with no apiserver at all,
+    where the operator's ``--probe`` is the only signal)."""
+    if probe_fn is None:
+        return discovered, "probe off"
+    if api is not None and node_name and not node_is_idle(api, node_name, resource_names):
+        prev = None
+        try:
+            prev = decode_node_annotations(obj_annotations(api.get_node(node_name)), contract, node_name=node_name)
+        except Exception as e:  # noqa: BLE001 - unreadable annotation: nothing to reuse
+            log.warning("reading the published topology of %s failed: %s", node_name, e)
+        if prev is not None and prev.n == discovered.n and [g.bdf for g in prev.gpus] == [g.bdf for g in discovered.gpus] \
+                and prev.bw_gbps is not None and np.isfinite(prev.bw_gbps).any():
+            discovered.hbm_gbps = prev.hbm_gbps
+            discovered.set_measured_bw(prev.bw_gbps, dict(prev.probe, reused=True))
+            return discovered, "reused the published matrix (devices in use: probe skipped)"
+        return discovered, "devices in use and no compatible published matrix: probe skipped, link classes only"
+    probed = probe_fn()
+    if probed is not None and probed.n == discovered.n:
+        probed.node_name = discovered.node_name
+        return probed, "probed"
+    return discovered, "probe unavailable: link classes only"
+
+
+def placeholder_dev_tree(root: str, topo: Topology) -> str:
+    """Create empty stand-ins for ``kfd`` and every device's ``dri/renderD*`` / ``dri/card*`` under
+    ``root`` (the ``--dev-root`` of a kind node or the cluster simulation, where no real ROCm device
+    nodes exist but the Allocate -> container path must still be exercised end to end)."""
+    os.makedirs(os.path.join(root, "dri"), exist_ok=True)
+    names = ["kfd"]
+    for i, g in enumerate(topo.gpus):
+        names.append(f"dri/renderD{g.render_minor if g.render_minor >= 0 else 128 + i}")
+        if g.card >= 0:
+            names.append(f"dri/card{g.card}")
+    for n in names:
+        open(os.path.join(root, n), "a").close()
+    return root
 
 
 class PluginConfig:
@@ -55,7 +125,7 @@ class PluginConfig:
                  node_name: str = "", contract: Optional[Contract] = None, health_interval: float = 5.0,
                  publish_node: bool = True, pass_rccl_env: bool = True, policy: PlacementPolicy = PlacementPolicy(),
                  resource_aliases: Sequence[str] = ("aliyun.com/gpu", "aliyun.com/gpu-count"),
-                 reprobe_interval: float = 0.0, reprobe_tolerance: float = 0.15):
+                 reprobe_interval: float = 0.0, reprobe_tolerance: float = 0.15, device_specs: str = "strict"):
         self.resource_name = resource_name
         self.socket_dir = socket_dir
         self.socket_name = socket_name
@@ -72,6 +142,13 @@ class PluginConfig:
         # republish when any measured pair moved by more than `reprobe_tolerance` (relative)
         self.reprobe_interval = reprobe_interval
         self.reprobe_tolerance = reprobe_tolerance
+        # Allocate's DeviceSpecs: "strict" = /dev/kfd + every device's render/card node, Allocate fails
+        # if one is missing on the node (a container must never start without its GPU); "stub" = only
+        # the nodes that exist under dev_root (a kind node with fake GPUs has none: envs + annotations
+        # only, BASELINE config 1)
+        if device_specs not in ("strict", "stub"):
+            raise ValueError(f"device_specs must be strict|stub, got {device_specs!r}")
+        self.device_specs = device_specs
 
     @property
     def socket_path(self) -> str:
@@ -97,8 +174,11 @@ class DevicePluginServer:
         self._stop = threading.Event()
         self._threads: List[threading.Thread] = []
         self._alloc_lock = threading.Lock()
+        self._probing = False  # set (under _alloc_lock) while an idle-time re-probe owns the links
         self.allocations: List[Tuple[str, Tuple[int, ...]]] = []  # (pod key or "", ids) log
         self.registered = 0
+        self.metrics = PluginMetrics()
+        self.metrics.set_topology(topology)
 
     # ------------------------------------------------------------------ device view
     def devices(self) -> List[pb.Device]:
@@ -119,6 +199,11 @@ class DevicePluginServer:
             self._version += 1
             self._cond.notify_all()
         log.warning("device %d is now %s", index, "Healthy" if healthy else "Unhealthy")
+        self.metrics.health(index, healthy)
+        if self.api is not None and self.cfg.node_name and not healthy:
+            record_event(self.api, {"kind": "Node", "metadata": {"name": self.cfg.node_name}}, "GPUUnhealthy",
+                         f"device {index} ({self.topology.gpus[index].bdf or 'no bdf'}) is Unhealthy", "Warning",
+                         component="gpu-topology-device-plugin", host=self.cfg.node_name)
         self._publish_node()
 
     def update_topology(self, topo: Topology) -> None:
@@ -128,6 +213,7 @@ class DevicePluginServer:
             self._health = {g.index: bool(g.healthy) for g in topo.gpus}
             self._version += 1
             self._cond.notify_all()
+        self.metrics.set_topology(topo)
         self._publish_node()
 
     # ------------------------------------------------------------------ link re-measurement
@@ -136,18 +222,14 @@ class DevicePluginServer:
         run, since it saturates every xGMI link.  Unknown (no apiserver) counts as busy."""
         if self.api is None or not self.cfg.node_name:
             return False
-        try:
-            pods = [p for p in self.api.list_pods(node_name=self.cfg.node_name) if not pod_is_terminal(p)]
-        except Exception as e:
-            log.warning("listing pods on %s failed: %s", self.cfg.node_name, e)
-            return False
-        return all(PodAssignment.from_annotations(obj_annotations(p)) is None for p in pods)
+        return node_is_idle(self.api, self.cfg.node_name, self._resource_names())
+
+    def _resource_names(self) -> Tuple[str, ...]:
+        return (self.cfg.resource_name,) + tuple(a for a in self.cfg.resource_aliases if a != self.cfg.resource_name)
 
     @staticmethod
     def link_change(old: Topology, new: Topology) -> float:
         """Largest relative change of a measured pair between two probes (inf if the measured set differs)."""
-        import numpy as np
-
         if old.bw_gbps is None or new.bw_gbps is None or old.n != new.n:
             return float("inf")
         a, b = old.bw_gbps, new.bw_gbps
@@ -161,17 +243,38 @@ class DevicePluginServer:
         return float(np.max(np.abs(b[fa] - a[fa]) / np.maximum(a[fa], 1e-9)))
 
     def reprobe(self) -> bool:
-        """One re-measurement (caller checked idleness); republish if the links moved.  -> republished."""
+        """One idle-time re-measurement; republish if the links moved.  -> republished.
+
+        While it runs ``Allocate`` is refused (UNAVAILABLE: the kubelet retries), so no container
+        starts on links the probe is saturating; idleness is checked under the same lock before and
+        again after the probe, and a result taken while a pod arrived is dropped (its traffic would
+        skew the matrix)."""
         if self.reprobe_fn is None:
             return False
-        new = self.reprobe_fn()
+        with self._alloc_lock:
+            if not self.node_idle():
+                self.metrics.reprobes.labels("busy").inc()
+                return False
+            self._probing = True
+        try:
+            new = self.reprobe_fn()
+        finally:
+            with self._alloc_lock:
+                self._probing = False
+                still_idle = self.node_idle()
         self.reprobes += 1
+        if not still_idle:
+            log.warning("link re-probe: a pod claimed devices during the probe; discarding the measurement")
+            self.metrics.reprobes.labels("discarded").inc()
+            return False
         if new is None or new.n != self.topology.n:
             log.warning("link re-probe produced no usable topology")
+            self.metrics.reprobes.labels("failed").inc()
             return False
         delta = self.link_change(self.topology, new)
         if delta <= self.cfg.reprobe_tolerance:
             log.info("link re-probe: largest change %.1f%% (within tolerance)", 100 * delta)
+            self.metrics.reprobes.labels("unchanged").inc()
             return False
         for g in new.gpus:  # health is the RAS monitor's call, not the probe's
             g.healthy = self._health.get(g.index, True)
@@ -180,6 +283,7 @@ class DevicePluginServer:
                     "in the measured set" if delta == float("inf") else f"{100 * delta:.1f}%")
         self.update_topology(new)
         self.republished += 1
+        self.metrics.reprobes.labels("republished").inc()
         return True
 
     # ------------------------------------------------------------------ node publication (A5, B7)
@@ -194,9 +298,13 @@ class DevicePluginServer:
             c.label_partition: t.gpus[0].partition if t.gpus else "",
             c.label_gfx: t.gpus[0].gfx if t.gpus else "",
         }
+        ann = encode_node_annotations(t, c)
+        self.metrics.annotation_bytes.set(sum(len(k) + len(v) for k, v in ann.items()))
         try:
-            self.api.patch_node(self.cfg.node_name, annotations=encode_node_annotations(t, c), labels=labels)
+            self.api.patch_node(self.cfg.node_name, annotations=ann, labels=labels)
+            self.metrics.node_publishes.labels("ok").inc()
         except Exception as e:
+            self.metrics.node_publishes.labels("error").inc()
             log.warning("publishing topology on node %s failed: %s", self.cfg.node_name, e)
 
     # ------------------------------------------------------------------ gRPC handlers
@@ -227,51 +335,108 @@ class DevicePluginServer:
                 g = set(pa.group)
                 if len(g) == size and g <= set(avail) and set(must) <= g:
                     ids = sorted(g)
+                    self.metrics.preferred.labels("annotation").inc()
                     break
             if ids is None:
-                ids = list(select_with(self.topology, size, avail, must, self.cfg.policy))
+                ids = self._preferred_fallback(size, avail, must)
             resp.container_responses.add(deviceIDs=[str(i) for i in ids])
         return resp
 
+    def _preferred_fallback(self, size: int, avail: Sequence[int], must: Sequence[int]) -> List[int]:
+        """No annotated pod matches: run the placement core over the healthy available devices.  A
+        placement error never fails admission (the kubelet would reject the pod): the answer then
+        degrades to must-include first, then the lowest available ids."""
+        healthy = [a for a in avail if 0 <= a < self.topology.n and self._health.get(a, True)]
+        try:
+            ids = list(select_with(self.topology, size, healthy, must, self.cfg.policy))
+            self.metrics.preferred.labels("placement").inc()
+            return ids
+        except (NoFeasiblePlacement, ValueError, AssertionError) as e:
+            log.warning("GetPreferredAllocation: placement failed (%s); answering in id order", e)
+            self.metrics.preferred.labels("fallback").inc()
+            out = [m for m in must if m in avail][:size]
+            out += [a for a in sorted(avail, key=lambda a: (a not in healthy, a)) if a not in out][: size - len(out)]
+            return sorted(out)
+
+    def _refuse(self, context, code, msg: str, outcome: str) -> None:
+        self.metrics.allocations.labels(outcome).inc()
+        if self.api is not None and self.cfg.node_name:
+            record_event(self.api, {"kind": "Node", "metadata": {"name": self.cfg.node_name}}, "FailedGPUAllocate", msg,
+                         "Warning", component="gpu-topology-device-plugin", host=self.cfg.node_name)
+        context.abort(code, msg)
+
     def Allocate(self, request, context):
+        t0 = time.perf_counter()
         resp = pb.AllocateResponse()
         all_ids: List[int] = []
         for creq in request.container_requests:
             ids = [int(x) for x in creq.devices_ids]
             bad = [i for i in ids if i < 0 or i >= self.topology.n]
             if bad:
-                context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"unknown device ids {bad}")
+                self._refuse(context, grpc.StatusCode.INVALID_ARGUMENT, f"unknown device ids {bad}", "invalid")
             unhealthy = [i for i in ids if not self._health.get(i, True)]
             if unhealthy:
-                context.abort(grpc.StatusCode.FAILED_PRECONDITION, f"devices {unhealthy} are unhealthy")
+                self._refuse(context, grpc.StatusCode.FAILED_PRECONDITION, f"devices {unhealthy} are unhealthy", "unhealthy")
             all_ids.extend(ids)
+        missing = self._missing_device_nodes(all_ids)
+        if missing:
+            self._refuse(context, grpc.StatusCode.FAILED_PRECONDITION, f"device nodes missing on this node: {missing}", "missing")
         with self._alloc_lock:
+            if self._probing:
+                self.metrics.allocations.labels("probing").inc()
+                context.abort(grpc.StatusCode.UNAVAILABLE, "link probe in progress; retry")
             pod = self._claim_pod(sorted(set(all_ids)))
         extra_env = self._rccl_env(pod) if pod is not None else {}
         for creq in request.container_requests:
             ids = [int(x) for x in creq.devices_ids]
             resp.container_responses.append(self._container_response(ids, extra_env))
         self.allocations.append((f"{meta(pod).get('namespace')}/{meta(pod).get('name')}" if pod else "", tuple(sorted(all_ids))))
+        self.metrics.allocations.labels("ok").inc()
+        self.metrics.allocated_devices.inc(len(all_ids))
+        self.metrics.allocate_seconds.observe(time.perf_counter() - t0)
         return resp
 
     def PreStartContainer(self, request, context):
         return pb.PreStartContainerResponse()
 
     # ------------------------------------------------------------------ Allocate helpers
-    def _container_response(self, ids: Sequence[int], extra_env: Dict[str, str]) -> pb.ContainerAllocateResponse:
-        r = pb.ContainerAllocateResponse()
+    def device_nodes(self, ids: Sequence[int]) -> List[Tuple[str, str]]:
+        """(container path, host path) of every device node the container needs for ``ids``."""
         root = self.cfg.dev_root.rstrip("/")
-        r.devices.add(container_path="/dev/kfd", host_path=f"{root}/kfd", permissions="rw")
-        numa: Set[int] = set()
+        out = [("/dev/kfd", f"{root}/kfd")]
         for i in ids:
             g = self.topology.gpus[i]
             minor = g.render_minor if g.render_minor >= 0 else 128 + i
-            r.devices.add(container_path=f"/dev/dri/renderD{minor}", host_path=f"{root}/dri/renderD{minor}", permissions="rw")
+            out.append((f"/dev/dri/renderD{minor}", f"{root}/dri/renderD{minor}"))
             if g.card >= 0:
-                r.devices.add(container_path=f"/dev/dri/card{g.card}", host_path=f"{root}/dri/card{g.card}", permissions="rw")
+                out.append((f"/dev/dri/card{g.card}", f"{root}/dri/card{g.card}"))
+        return out
+
+    def _missing_device_nodes(self, ids: Sequence[int]) -> List[str]:
+        if self.cfg.device_specs != "strict":
+            return []
+        return [h for _, h in self.device_nodes(ids) if not os.path.exists(h)]
+
+    def _container_response(self, ids: Sequence[int], extra_env: Dict[str, str]) -> pb.ContainerAllocateResponse:
+        r = pb.ContainerAllocateResponse()
+        for cpath, hpath in self.device_nodes(ids):
+            if self.cfg.device_specs == "stub" and not os.path.exists(hpath):
+                continue  # kind / fake GPUs: never hand containerd a host path the node does not have
+            r.devices.add(container_path=cpath, host_path=hpath, permissions="rw")
+        numa: Set[int] = set()
+        cpus: List[str] = []
+        for i in ids:
+            g = self.topology.gpus[i]
             numa.add(int(g.numa))
-        r.envs["GTK_GPU_GROUP"] = format_group(ids)
+            if g.cpu_affinity:
+                cpus.append(g.cpu_affinity)
+        r.envs[ENV_GROUP] = format_group(ids)
+        # PCI addresses in GROUP order: HIP renumbers the container's devices 0..k-1, so tools inside
+        # the pod map GROUP -> HIP ordinal by address (topology/identity.py, `gtk validate`)
+        r.envs[ENV_BDFS] = ",".join(self.topology.gpus[i].bdf for i in ids)
         r.envs["GTK_NUMA_NODES"] = ",".join(str(x) for x in sorted(numa))
+        if cpus:
+            r.envs["GTK_CPUSET"] = format_cpulist(parse_cpulist(",".join(cpus)))
         for k, v in extra_env.items():
             r.envs[k] = v
         r.annotations["gputopology.amd.com/devices"] = format_group(ids)
@@ -343,7 +508,7 @@ class DevicePluginServer:
         return None
 
     def _unannotated_pod(self, k: int) -> Optional[dict]:
-        names = (self.cfg.resource_name,) + tuple(a for a in self.cfg.resource_aliases if a != self.cfg.resource_name)
+        names = self._resource_names()
         cands = []
         for p in self._node_pods():
             if PodAssignment.from_annotations(obj_annotations(p)) is not None or pod_phase(p) != "Pending":
@@ -391,6 +556,7 @@ class DevicePluginServer:
                                                                    get_preferred_allocation_available=True)),
                  timeout=timeout)
         self.registered += 1
+        self.metrics.registrations.inc()
         log.info("registered %s with kubelet at %s", self.cfg.resource_name, self.cfg.kubelet_socket)
 
     def start(self, register: bool = True) -> None:
@@ -400,14 +566,22 @@ class DevicePluginServer:
         if register:
             self.register()
         self._threads = [threading.Thread(target=self._monitor, name="devplugin-monitor", daemon=True)]
+        if self.reprobe_fn is not None and self.cfg.reprobe_interval > 0:
+            # its own thread: a probe takes minutes and must not stall health polling / re-registration
+            self._threads.append(threading.Thread(target=self._reprobe_loop, name="devplugin-reprobe", daemon=True))
         for t in self._threads:
             t.start()
 
+    def _reprobe_loop(self) -> None:
+        while not self._stop.wait(self.cfg.reprobe_interval):
+            try:
+                self.reprobe()
+            except Exception as e:
+                log.warning("link re-probe failed: %s", e)
+
     def _monitor(self) -> None:
-        """Health polling, idle-time link re-probes, kubelet restart detection (the kubelet wipes
-        plugin sockets on restart)."""
+        """Health polling and kubelet restart detection (the kubelet wipes plugin sockets on restart)."""
         next_health = 0.0
-        next_probe = time.monotonic() + self.cfg.reprobe_interval
         while not self._stop.wait(0.2):
             if not os.path.exists(self.cfg.socket_path):
                 log.warning("plugin socket %s vanished (kubelet restart?): re-serving and re-registering", self.cfg.socket_path)
@@ -425,13 +599,6 @@ class DevicePluginServer:
                         self.set_health(int(idx), bool(ok))
                 except Exception as e:
                     log.warning("health check failed: %s", e)
-            if self.reprobe_fn is not None and self.cfg.reprobe_interval > 0 and time.monotonic() >= next_probe:
-                next_probe = time.monotonic() + self.cfg.reprobe_interval
-                try:
-                    if self.node_idle():
-                        self.reprobe()
-                except Exception as e:
-                    log.warning("link re-probe failed: %s", e)
 
     def stop(self) -> None:
         self._stop.set()

@@ -40,6 +40,7 @@ class Alloc:
     assigned: bool
     assume_time: float
     source: str = "annotation"  # annotation | overlay
+    cpuset: str = ""  # cores recommended to the pod at bind (<prefix>/cpuset)
 
 
 @dataclass
@@ -49,16 +50,31 @@ class NodeState:
     labels: Dict[str, str] = field(default_factory=dict)
     node_rv: str = ""
     allocs: Dict[str, Alloc] = field(default_factory=dict)
-    unknown: int = 0  # devices held by pods without a GROUP annotation
+    unknown_pods: Dict[str, int] = field(default_factory=dict)  # pod -> devices held without a GROUP annotation
     capacity: int = -1  # node.status.allocatable[resource] (-1 = unknown)
     synced_at: float = 0.0
     lock: threading.RLock = field(default_factory=threading.RLock, repr=False)
+
+    @property
+    def unknown(self) -> int:
+        """Devices held by pods without a GROUP annotation (ids unknown: only feasibility shrinks)."""
+        return sum(self.unknown_pods.values())
 
     def used(self, now: float, ttl: float) -> Set[int]:
         out: Set[int] = set()
         for a in self.allocs.values():
             if a.assigned or (now - a.assume_time) <= ttl:
                 out.update(a.ids)
+        return out
+
+    def claimed_cpus(self, now: float, ttl: float) -> Set[int]:
+        """Cores recommended to the live pods of this node (their cpuset annotations)."""
+        from ..topology.cpus import parse_cpulist
+
+        out: Set[int] = set()
+        for a in self.allocs.values():
+            if a.cpuset and (a.assigned or (now - a.assume_time) <= ttl):
+                out |= parse_cpulist(a.cpuset)
         return out
 
     def free_count(self, now: float, ttl: float) -> int:
@@ -86,6 +102,8 @@ class ClusterCache:
         self.consistent_lists = True  # apiserver LISTs without resourceVersion are quorum reads
         self._epoch = 0
         self._overlay_epoch: Dict[Tuple[str, str], int] = {}
+        self.informer = None
+        self._pending_pod_list: Optional[List[dict]] = None
 
     # ------------------------------------------------------------------ node objects
     def _state(self, name: str) -> NodeState:
@@ -131,7 +149,8 @@ class ClusterCache:
             except ValueError:
                 req = 0
             return None, req
-        return Alloc(pod=pod_key(pod), ids=tuple(pa.group), assigned=pa.assigned, assume_time=float(pa.assume_time)), 0
+        return Alloc(pod=pod_key(pod), ids=tuple(pa.group), assigned=pa.assigned, assume_time=float(pa.assume_time),
+                     cpuset=obj_annotations(pod).get(self.contract.cpuset_key, "")), 0
 
     def _next_epoch(self) -> int:
         with self._lock:
@@ -141,12 +160,13 @@ class ClusterCache:
     def _rebuild(self, st: NodeState, pods: List[dict], list_epoch: int) -> None:
         """``list_epoch``: value of the epoch counter taken just before the pods were listed."""
         allocs: Dict[str, Alloc] = {}
-        unknown = 0
+        unknown: Dict[str, int] = {}
         seen = set()
         for p in pods:
             seen.add(pod_key(p))
             a, u = self._pod_alloc(p)
-            unknown += u
+            if u:
+                unknown[pod_key(p)] = u
             if a is not None:
                 allocs[a.pod] = a
         now = self.clock()
@@ -166,7 +186,7 @@ class ClusterCache:
                 if key[0] == st.name:
                     del self._overlay_epoch[key]
         st.allocs = allocs
-        st.unknown = unknown
+        st.unknown_pods = unknown
         st.synced_at = now
 
     def refresh_node(self, name: str) -> NodeState:
@@ -179,45 +199,85 @@ class ClusterCache:
             self._rebuild(st, pods, epoch)
         return st
 
-    def sync_all(self) -> None:
-        epoch = self._next_epoch()
-        nodes = self.api.list_nodes()
-        pods = self.api.list_pods()
+    def replace_nodes(self, nodes: List[dict]) -> None:
+        """A full node LIST: update every node, forget the ones that are gone."""
+        names = set()
+        for node in nodes:
+            names.add(self.update_node_object(node).name)
+        with self._lock:
+            for gone in set(self._nodes) - names:
+                del self._nodes[gone]
+
+    def replace_pods(self, pods: List[dict], epoch: Optional[int] = None) -> None:
+        """A full pod LIST: rebuild every known node's usage from it."""
+        epoch = self._next_epoch() if epoch is None else epoch
         by_node: Dict[str, List[dict]] = {}
         for p in pods:
             n = pod_node(p)
             if n:
                 by_node.setdefault(n, []).append(p)
-        names = set()
-        for node in nodes:
-            st = self.update_node_object(node)
-            names.add(st.name)
+        for st in self.nodes():
             with st.lock:
                 self._rebuild(st, by_node.get(st.name, []), epoch)
+
+    def sync_all(self) -> None:
+        """Cluster-wide LIST of nodes + pods (polling mode, or the informer's safety resync).
+        Takes node locks one at a time and never while holding one (callers must not either)."""
+        epoch = self._next_epoch()
+        nodes = self.api.list_nodes()
+        pods = self.api.list_pods()
+        self.replace_nodes(nodes)
+        self.replace_pods(pods, epoch)
         with self._lock:
-            for gone in set(self._nodes) - names:
-                del self._nodes[gone]
             self._last_full = self.clock()
 
     def maybe_sync(self) -> None:
-        if self.clock() - self._last_full >= self.resync_s:
+        if self.informer is None and self.clock() - self._last_full >= self.resync_s:
             self.sync_all()
 
-    def get(self, name: str, node_obj: Optional[dict] = None) -> NodeState:
+    # ------------------------------------------------------------------ informer (LIST+WATCH)
+    def attach_informer(self, informer) -> None:
+        """Drive this cache from a :class:`~..k8s.informer.Informer`: its LISTs replace the view, its
+        WATCH events patch it, and :meth:`get` stops polling once it has synced."""
+        self.informer = informer
+
+    def on_list(self, kind: str, items: List[dict]) -> None:
+        if kind == "Node":
+            self.replace_nodes(items)
+            with self._lock:
+                pods = self._pending_pod_list
+                self._pending_pod_list = None
+            if pods is not None:  # pods listed before their nodes existed here
+                self.replace_pods(pods)
+        elif kind == "Pod":
+            if not self._nodes:
+                with self._lock:
+                    self._pending_pod_list = items
+            self.replace_pods(items)
+        with self._lock:
+            self._last_full = self.clock()
+
+    def informed(self) -> bool:
+        return self.informer is not None and self.informer.synced
+
+    def get(self, name: str, node_obj: Optional[dict] = None, sync: bool = True) -> NodeState:
         """Cached state of a node for scoring/filtering.
 
-        A stale cache is refreshed with ONE cluster-wide sync (list nodes + list pods: two API calls
-        however many candidates the scheduler sends), not per node; ``bind`` does its own
-        authoritative per-node refresh under the node lock.  ``node_obj`` (scheduler sent full
-        Node objects) refreshes the node's topology/labels without an API call.
+        With a synced informer this never calls the apiserver.  Otherwise a stale cache is
+        refreshed with ONE cluster-wide sync (list nodes + list pods: two API calls however many
+        candidates the scheduler sends), not per node.  ``sync=False`` (bind, which refreshes its
+        node itself and holds the node lock) never syncs: :meth:`sync_all` takes every node's lock,
+        so calling it under one can deadlock two binds on different nodes.  ``node_obj`` (scheduler
+        sent full Node objects) refreshes the node's topology/labels without an API call.
         """
-        if self.clock() - self._last_full >= self.resync_s or name not in self._nodes:
+        stale = self.clock() - self._last_full >= self.resync_s or name not in self._nodes
+        if sync and stale and not self.informed():
             try:
                 self.sync_all()
             except Exception as e:
                 log.warning("cache sync failed: %s", e)
         st = self.update_node_object(node_obj) if node_obj is not None else self._state(name)
-        if st.synced_at == 0.0:  # node unknown to the last sync (e.g. just created): read it directly
+        if sync and st.synced_at == 0.0:  # node unknown to the last sync (e.g. just created): read it directly
             try:
                 self.refresh_node(name)
             except Exception as e:
@@ -225,9 +285,9 @@ class ClusterCache:
         return st
 
     # ------------------------------------------------------------------ writes made by this process
-    def assume(self, node: str, pod: str, ids: Iterable[int], at: Optional[float] = None) -> None:
+    def assume(self, node: str, pod: str, ids: Iterable[int], at: Optional[float] = None, cpuset: str = "") -> None:
         a = Alloc(pod=pod, ids=tuple(int(i) for i in ids), assigned=False, assume_time=at if at is not None else self.clock(),
-                  source="overlay")
+                  source="overlay", cpuset=cpuset)
         with self._lock:
             self._overlay.setdefault(node, {})[pod] = a
             self._overlay_epoch[(node, pod)] = self._next_epoch()
@@ -261,12 +321,23 @@ class ClusterCache:
         with st.lock:
             if event == "DELETED" or pod_is_terminal(obj):
                 st.allocs.pop(key, None)
+                st.unknown_pods.pop(key, None)
                 with self._lock:
                     self._overlay.get(node, {}).pop(key, None)
                 return
-            a, _ = self._pod_alloc(obj)
+            a, u = self._pod_alloc(obj)
             if a is not None:
-                st.allocs[key] = a
+                st.allocs[key] = a  # the apiserver has the assignment: authoritative over the overlay
+                st.unknown_pods.pop(key, None)
+                with self._lock:
+                    self._overlay.get(node, {}).pop(key, None)
+            else:
+                if u:
+                    st.unknown_pods[key] = u
+                else:
+                    st.unknown_pods.pop(key, None)
+                if key in st.allocs and st.allocs[key].source == "annotation":
+                    del st.allocs[key]  # GROUP removed (bind rollback)
 
     def nodes(self) -> List[NodeState]:
         with self._lock:

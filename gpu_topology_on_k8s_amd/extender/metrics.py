@@ -1,11 +1,19 @@
 """Prometheus metrics of the extender: per-verb latency histograms, chosen-score
-histogram, bind count.  Uses a private registry so several extenders can live in one process
-(tests, cluster simulation)."""
+histogram, bind count, and cluster fragmentation gauges computed from the node cache at scrape
+time.  Uses a private registry so several extenders can live in one process (tests, cluster
+simulation).
+
+Fragmentation index of a node = 1 - (free devices in its fullest group) / (free devices), where a
+group is a physical GPU on partitioned nodes and a NUMA domain otherwise: 0 when every free device
+sits in one group (the next large request gets a compact set), toward 1 as free devices scatter.
+The cluster index weights nodes by free devices.  ``gtk_extender_placeable_nodes{k}`` counts the
+nodes that can still host a k-device pod."""
 from __future__ import annotations
 
 from typing import TYPE_CHECKING
 
 from prometheus_client import CollectorRegistry, Counter, Histogram, generate_latest
+from prometheus_client.core import GaugeMetricFamily
 
 if TYPE_CHECKING:  # pragma: no cover
     from .scheduler import Decision
@@ -28,6 +36,14 @@ class ExtenderMetrics:
         self.decision_cache = Counter("gtk_extender_decision_cache_total", "placement decisions served from / added to the cache",
                                       ["result"], registry=self.registry)
 
+        self._cache = None
+
+    def attach_cache(self, cache, ttl: float, clock) -> None:
+        """Export fragmentation gauges from ``cache`` (an :class:`~.cache.ClusterCache`) at scrape time."""
+        if self._cache is None:
+            self.registry.register(_FragmentationCollector(cache, ttl, clock))
+        self._cache = cache
+
     def cache(self, hit: bool) -> None:
         self.decision_cache.labels(result="hit" if hit else "miss").inc()
 
@@ -46,3 +62,51 @@ class ExtenderMetrics:
 
     def exposition(self) -> bytes:
         return generate_latest(self.registry)
+
+
+def node_fragmentation(topology, used, unknown: int = 0):
+    """(free devices, fragmentation index in [0, 1], largest free group) of one node."""
+    if topology is None:
+        return 0, 0.0, 0
+    partitioned = len({g.physical for g in topology.gpus}) < topology.n
+    groups = {}
+    free = 0
+    for g in topology.gpus:
+        if g.healthy and g.index not in used:
+            key = g.physical if partitioned else g.numa
+            groups[key] = groups.get(key, 0) + 1
+            free += 1
+    free = max(0, free - unknown)
+    if free == 0:
+        return 0, 0.0, 0
+    big = min(free, max(groups.values()))
+    return free, 1.0 - big / free, big
+
+
+class _FragmentationCollector:
+    def __init__(self, cache, ttl: float, clock):
+        self.cache, self.ttl, self.clock = cache, ttl, clock
+
+    def collect(self):
+        node_g = GaugeMetricFamily("gtk_extender_node_fragmentation", "1 - largest free group / free devices", labels=["node"])
+        free_g = GaugeMetricFamily("gtk_extender_node_free_devices", "schedulable free devices", labels=["node"])
+        place_g = GaugeMetricFamily("gtk_extender_placeable_nodes", "nodes with at least k free devices", labels=["k"])
+        cluster_g = GaugeMetricFamily("gtk_extender_cluster_fragmentation", "free-device weighted fragmentation index")
+        now = self.clock()
+        tot_free = tot_big = 0
+        counts = {1: 0, 2: 0, 4: 0, 8: 0}
+        for st in self.cache.nodes():
+            with st.lock:
+                if st.topology is None:
+                    continue
+                free, frag, big = node_fragmentation(st.topology, st.used(now, self.ttl), st.unknown)
+            node_g.add_metric([st.name], frag)
+            free_g.add_metric([st.name], free)
+            tot_free += free
+            tot_big += big
+            for k in counts:
+                counts[k] += free >= k
+        for k, c in counts.items():
+            place_g.add_metric([str(k)], c)
+        cluster_g.add_metric([], (1.0 - tot_big / tot_free) if tot_free else 0.0)
+        yield from (node_g, free_g, place_g, cluster_g)

@@ -9,17 +9,26 @@ Reference (``design.md:88-234``):
     ``ALIYUN_COM_GPU_ASSIGNED=false``, ``ALIYUN_COM_GPU_ASSUME_TIME=<now>`` and bind
     (``design.md:119,223-232``).
 
-This implementation adds (SURVEY.md §2.A A8, §2.B B6/B7):
+This implementation adds (SURVEY.md §2.A A8, A16, §2.B B3/B6/B7):
   * an optional filter verb that rejects nodes with no topology, too few free devices, or the wrong
     GPU model (heterogeneous-cluster quota, Gaia B7);
-  * a NUMA hint annotation (Gaia B6 CPU binding) and the placement score on the pod;
+  * node scores normalised over the candidate set: the best feasible node gets 10 and every other
+    loses one point per ``score_resolution`` of relative objective gap, so a measured degraded link
+    (a fraction of a percent of an 8-GPU set's mean cost) still decides between nodes;
+  * CPU affinity (``design.md:135-147`` tie-break, Gaia B6): the devices' local cores already
+    recommended to other pods raise their access cost, and bind writes the chosen devices' local
+    cores (``<prefix>/cpuset``) and NUMA nodes on the pod;
+  * fractional requests (Gaia Fragment, Alg. 2) as XCP partitions of ONE physical GPU on
+    CPX/DPX/QPX nodes, selected by the ``<prefix>/gpu-fraction`` pod annotation;
   * per-node locking + an assume overlay so concurrent binds never overlap (BASELINE config 4);
   * three selectable policies: ``exact`` (default, :func:`placement.select`), ``gaia`` (cost-tree
-    Alg. 1-4) and ``design`` (the reference's greedy/Prim, for parity experiments).
+    Alg. 1-4) and ``design`` (the reference's greedy/Prim, for parity experiments);
+  * k8s Events on bind success / failure, and binds refused for pods this extender does not manage.
 """
 from __future__ import annotations
 
 import logging
+import math
 import random
 import threading
 import time
@@ -29,19 +38,21 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 from ..k8s.annotations import ANN_ASSIGNED, ANN_ASSUME_TIME, ANN_GROUP, Contract, PodAssignment
 from ..k8s.api import ApiError, KubeAPI
+from ..k8s.events import record_event
 from ..k8s.objects import annotations as obj_annotations
 from ..k8s.objects import labels as obj_labels
 from ..k8s.objects import meta, pod_gpu_request, pod_key
-from ..placement import NoFeasiblePlacement, PlacementPolicy, select
+from ..placement import NoFeasiblePlacement, PlacementPolicy, place_fraction, select
 from ..placement.gaia import gaia_schedule, tree_from_topology
 from ..placement.legacy import design_greedy_select
+from ..topology.cpus import access_costs, recommended_cpuset
 from ..topology.model import Topology
 from .cache import ClusterCache, NodeState
 from .metrics import ExtenderMetrics
 
 log = logging.getLogger(__name__)
 
-__all__ = ["ExtenderConfig", "TopologyExtender", "Decision"]
+__all__ = ["ExtenderConfig", "TopologyExtender", "Decision", "normalized_scores"]
 
 MAX_EXTENDER_PRIORITY = 10  # k8s.io/kube-scheduler/extender/v1 MaxExtenderPriority
 
@@ -58,6 +69,12 @@ class ExtenderConfig:
     bind_retries: int = 3
     seed: Optional[int] = None
     decision_cache: int = 4096  # LRU entries; 0 disables (random tie-breaks are never cached)
+    # relative objective gap worth one score point below the best candidate (prioritize)
+    score_resolution: float = 0.005
+    cpu_affinity: bool = True  # access term from the devices' local cores (A16 / Gaia B6)
+    # pods whose spec.schedulerName is not listed are refused at bind (empty = any scheduler)
+    scheduler_names: Tuple[str, ...] = ()
+    events: bool = True
 
 
 @dataclass
@@ -68,6 +85,22 @@ class Decision:
     objective: float
     policy: str
     micros: float
+    cpuset: str = ""
+
+
+def normalized_scores(objectives: Dict[str, float], resolution: float = 0.005) -> Dict[str, int]:
+    """Node scores for one pod: 10 for the lowest objective, one point less per ``resolution`` of
+    relative gap (rounded up, so any strictly worse node scores strictly lower), never below 1 (a
+    feasible node always beats an infeasible one, which scores 0)."""
+    if not objectives:
+        return {}
+    best = min(objectives.values())
+    out = {}
+    for n, j in objectives.items():
+        gap = (j - best) / max(abs(best), 1e-12)
+        pts = 0 if gap <= 1e-9 else math.ceil(gap / resolution - 1e-9)
+        out[n] = int(max(1, MAX_EXTENDER_PRIORITY - pts))
+    return out
 
 
 class TopologyExtender:
@@ -79,11 +112,13 @@ class TopologyExtender:
         self.cache = ClusterCache(api, self.cfg.contract, self.cfg.assume_ttl, self.cfg.resync_s, clock=clock,
                                   resource_aliases=self.cfg.resource_aliases)
         self.metrics = metrics or ExtenderMetrics()
+        self.metrics.attach_cache(self.cache, self.cfg.assume_ttl, clock)
         self._rng = random.Random(self.cfg.seed)
         self._bind_lock = threading.Lock()
-        # Placement decisions are a pure function of (node topology object, used set, healthy set, k)
-        # under a deterministic policy: kube-scheduler asks sort for every pending pod x candidate
-        # node, and on a large cluster most nodes have not changed since the last pod of the same size.
+        # Placement decisions are a pure function of (node topology object, used set, healthy set,
+        # access costs, k, fraction) under a deterministic policy: kube-scheduler asks sort for every
+        # pending pod x candidate node, and on a large cluster most nodes have not changed since the
+        # last pod of the same size.
         self._cache: "OrderedDict[tuple, Tuple[Tuple[int, ...], float, float, Topology]]" = OrderedDict()
         self._cache_lock = threading.Lock()
 
@@ -94,6 +129,16 @@ class TopologyExtender:
 
     def request_of(self, pod: Dict[str, Any]) -> int:
         return pod_gpu_request(pod, self.resources)
+
+    def fraction_of(self, pod: Dict[str, Any]) -> Optional[float]:
+        """``<prefix>/gpu-fraction`` (0 < m < 1) or None; malformed values raise ValueError."""
+        raw = obj_annotations(pod).get(self.cfg.contract.fraction_key)
+        if raw is None or str(raw).strip() == "":
+            return None
+        m = float(raw)
+        if not 0.0 < m < 1.0:
+            raise ValueError(f"{self.cfg.contract.fraction_key} must be in (0, 1), got {raw!r}")
+        return m
 
     def _model_ok(self, pod: Dict[str, Any], st: NodeState) -> Tuple[bool, str]:
         """Heterogeneous-cluster quota (Gaia B7): a pod never receives a mix of GPU models, and a
@@ -113,18 +158,20 @@ class TopologyExtender:
     def _cacheable(self) -> bool:
         return self.cfg.decision_cache > 0 and self.cfg.policy.tie_break != "random"
 
-    def _choose_cached(self, t: Topology, used: Sequence[int], k: int) -> Tuple[Tuple[int, ...], float, float]:
+    def _choose_cached(self, t: Topology, used: Sequence[int], k: int, access=None,
+                       fraction: Optional[float] = None) -> Tuple[Tuple[int, ...], float, float]:
         if not self._cacheable():
-            return self._choose(t, used, k)
+            return self._choose(t, used, k, access, fraction)
         # the Topology object is replaced whenever the node annotation changes (new resourceVersion)
-        key = (id(t), tuple(used), tuple(g.healthy for g in t.gpus), k, self.cfg.policy_name)
+        acc_key = None if access is None else tuple(round(float(x), 9) for x in access)
+        key = (id(t), tuple(used), tuple(g.healthy for g in t.gpus), k, self.cfg.policy_name, acc_key, fraction)
         with self._cache_lock:
             hit = self._cache.get(key)
             if hit is not None and hit[3] is t:
                 self._cache.move_to_end(key)
                 self.metrics.cache(True)
                 return hit[:3]
-        res = self._choose(t, used, k)  # NoFeasiblePlacement propagates uncached
+        res = self._choose(t, used, k, access, fraction)  # NoFeasiblePlacement propagates uncached
         with self._cache_lock:
             self._cache[key] = res + (t,)  # keeps t alive, so id(t) cannot be reused while cached
             while len(self._cache) > self.cfg.decision_cache:
@@ -132,13 +179,19 @@ class TopologyExtender:
         self.metrics.cache(False)
         return res
 
-    def _choose(self, t: Topology, used: Sequence[int], k: int) -> Tuple[Tuple[int, ...], float, float]:
-        """(ids, score 0..10, objective) under the configured policy; raises NoFeasiblePlacement."""
+    def _choose(self, t: Topology, used: Sequence[int], k: int, access=None,
+                fraction: Optional[float] = None) -> Tuple[Tuple[int, ...], float, float]:
+        """(ids, absolute score 0..10, objective) under the configured policy; raises NoFeasiblePlacement."""
+        from ..placement.core import Problem, evaluate, score_from_objective
+
         name = self.cfg.policy_name
-        if name == "exact":
-            pl = select(t, k, used=used, policy=self.cfg.policy, rng=self._rng)
+        if fraction is not None:
+            ids = place_fraction(t, k, used, access)
+            name = "fragment"
+        elif name == "exact":
+            pl = select(t, k, used=used, policy=self.cfg.policy, rng=self._rng, access=access)
             return pl.ids, pl.score, pl.objective
-        if name == "gaia":
+        elif name == "gaia":
             tree = tree_from_topology(t, used=[u for u in used])
             for g in t.gpus:
                 if not g.healthy and g.index not in used:
@@ -151,30 +204,54 @@ class TopologyExtender:
             raise ValueError(f"unknown policy {name!r}")
         if len(ids) != k:
             raise NoFeasiblePlacement(f"{name}: no {k}-device placement")
-        from ..placement.core import Problem, evaluate, score_from_objective
-
-        j, _ = evaluate(Problem.from_topology(t, used, partition_aware=self.cfg.policy.partition_aware), ids, self.cfg.policy)
+        j, _ = evaluate(Problem.from_topology(t, used, access, partition_aware=self.cfg.policy.partition_aware), ids,
+                        self.cfg.policy)
         return tuple(sorted(int(i) for i in ids)), score_from_objective(j), j
 
-    def _node_eval(self, pod: Dict[str, Any], name: str, node_obj: Optional[dict], k: int) -> Tuple[Optional[Decision], str]:
-        st = self.cache.get(name, node_obj)
+    def _eval_state(self, pod: Dict[str, Any], name: str, st: NodeState, k: int) -> Tuple[Optional[Decision], str]:
+        """Decision for ``pod`` on the node state ``st`` as cached now.  Never calls the apiserver,
+        so it may run under the node lock (bind)."""
         with st.lock:
-            if st.topology is None:
+            t = st.topology
+            if t is None:
                 return None, "node has no GPU topology annotation"
             ok, why = self._model_ok(pod, st)
             if not ok:
                 return None, why
+            try:
+                fraction = self.fraction_of(pod)
+            except ValueError as e:
+                return None, str(e)
+            if fraction is not None:
+                sizes = {}
+                for g in t.gpus:
+                    sizes[g.physical] = sizes.get(g.physical, 0) + 1
+                per_gpu = max(sizes.values()) if sizes else 1
+                if per_gpu <= 1:
+                    return None, "fractional GPU requests need a partitioned (CPX/DPX/QPX) node"
+                need = max(1, math.ceil(fraction * per_gpu - 1e-9))
+                if need != k:
+                    return None, (f"gpu-fraction {fraction} is {need} of {per_gpu} partitions per GPU on this node, "
+                                  f"but the pod requests {k} devices")
             now = self.clock()
             used = sorted(st.used(now, self.cfg.assume_ttl))
-            if st.free_count(now, self.cfg.assume_ttl) < k:
-                return None, f"insufficient free devices: need {k}, free {st.free_count(now, self.cfg.assume_ttl)}"
+            free = st.free_count(now, self.cfg.assume_ttl)
+            if free < k:
+                return None, f"insufficient free devices: need {k}, free {free}"
+            access = access_costs(t, st.claimed_cpus(now, self.cfg.assume_ttl)) if self.cfg.cpu_affinity else None
             t0 = time.perf_counter()
             try:
-                ids, score, obj = self._choose_cached(st.topology, used, k)
+                ids, score, obj = self._choose_cached(t, used, k, access, fraction)
             except NoFeasiblePlacement as e:
                 return None, str(e)
             us = (time.perf_counter() - t0) * 1e6
-            return Decision(node=name, ids=ids, score=score, objective=obj, policy=self.cfg.policy_name, micros=us), ""
+            return Decision(node=name, ids=ids, score=score, objective=obj,
+                            policy="fragment" if fraction is not None else self.cfg.policy_name, micros=us,
+                            cpuset=recommended_cpuset(t, ids)), ""
+
+    def _node_eval(self, pod: Dict[str, Any], name: str, node_obj: Optional[dict], k: int) -> Tuple[Optional[Decision], str]:
+        st = self.cache.get(name, node_obj)  # may sync the cache: never call with a node lock held
+        return self._eval_state(pod, name, st, k)
 
     # ------------------------------------------------------------------ verbs
     def filter(self, pod: Dict[str, Any], node_names: Sequence[str], node_objs: Optional[Dict[str, dict]] = None):
@@ -196,27 +273,27 @@ class TopologyExtender:
         return ok, failed
 
     def prioritize(self, pod: Dict[str, Any], node_names: Sequence[str], node_objs: Optional[Dict[str, dict]] = None):
-        """-> [(host, score 0..10)].  Infeasible nodes score 0 (the reference has no filter verb)."""
+        """-> [(host, score 0..10)]: infeasible nodes 0 (the reference has no filter verb), feasible
+        nodes :func:`normalized_scores` of their best placement's objective."""
         t0 = time.perf_counter()
         k = self.request_of(pod)
-        out: List[Tuple[str, int]] = []
+        objs: Dict[str, float] = {}
         for n in node_names:
             if k == 0:
-                out.append((n, 0))
                 continue
             d, _ = self._node_eval(pod, n, (node_objs or {}).get(n), k)
-            if d is None:
-                out.append((n, 0))
-            else:
-                s = int(max(0, min(MAX_EXTENDER_PRIORITY, round(d.score))))
-                out.append((n, max(1, s)))  # feasible nodes always beat infeasible ones
+            if d is not None:
+                objs[n] = d.objective
                 self.metrics.score(d.score)
+        norm = normalized_scores(objs, self.cfg.score_resolution)
+        out = [(n, norm.get(n, 0)) for n in node_names]
         self.metrics.observe("prioritize", time.perf_counter() - t0)
         return out
 
     def bind(self, namespace: str, name: str, uid: str, node: str) -> Optional[Decision]:
         """Choose the device set on ``node``, annotate the pod, bind it.  Raises on failure."""
         t0 = time.perf_counter()
+        pod: Optional[Dict[str, Any]] = None
         try:
             pod = self.api.get_pod(namespace, name)
             k = self.request_of(pod)
@@ -230,12 +307,18 @@ class TopologyExtender:
                                     micros=0.0) if ids else None
                 raise ApiError(409, f"pod {namespace}/{name} is already bound to {bound_to}")
             if k == 0:
-                self.api.bind_pod(namespace, name, uid, node)
-                return None
-            st = self.cache.get(node)
+                # kube-scheduler only delegates binding of pods that request a managed resource; any
+                # other bind request did not come from it and is refused
+                raise ApiError(400, f"pod {namespace}/{name} requests none of {self.resources}: not managed by this extender")
+            sched = (pod.get("spec") or {}).get("schedulerName") or "default-scheduler"
+            if self.cfg.scheduler_names and sched not in self.cfg.scheduler_names:
+                raise ApiError(403, f"pod {namespace}/{name} uses scheduler {sched!r}, not one of {list(self.cfg.scheduler_names)}")
+            # refresh (2 API calls) BEFORE taking the node lock; the decision below uses only cached
+            # state, so a bind never holds one node's lock while waiting for another's
+            self.cache.refresh_node(node)
+            st = self.cache.get(node, sync=False)
             with st.lock:  # serialise select+annotate+bind per node
-                self.cache.refresh_node(node)
-                d, why = self._node_eval(pod, node, None, k)
+                d, why = self._eval_state(pod, node, st, k)
                 if d is None:
                     raise NoFeasiblePlacement(f"bind {namespace}/{name} on {node}: {why}")
                 key = pod_key(pod)
@@ -244,22 +327,34 @@ class TopologyExtender:
                 ann = pa.to_annotations()
                 t = st.topology
                 numa = sorted({t.gpus[i].numa for i in d.ids}) if t is not None else []
-                ann[self.cfg.contract.cpuset_key] = ",".join(str(x) for x in numa)
+                ann[self.cfg.contract.numa_key] = ",".join(str(x) for x in numa)
+                if d.cpuset:
+                    ann[self.cfg.contract.cpuset_key] = d.cpuset
                 ann[self.cfg.contract.score_key] = f"{d.score:.3f}"
-                self.cache.assume(node, key, d.ids, now)
+                self.cache.assume(node, key, d.ids, now, cpuset=d.cpuset)
                 try:
                     self._patch_with_retry(namespace, name, ann)
                     self.api.bind_pod(namespace, name, uid, node)
                 except Exception:
                     self.cache.forget(node, key)
                     try:  # roll back the annotation so a retry starts clean
-                        self.api.patch_pod_annotations(namespace, name, {ANN_GROUP: None, ANN_ASSIGNED: None, ANN_ASSUME_TIME: None})
+                        self.api.patch_pod_annotations(namespace, name, {ANN_GROUP: None, ANN_ASSIGNED: None, ANN_ASSUME_TIME: None,
+                                                                         self.cfg.contract.cpuset_key: None})
                     except Exception as e2:  # pragma: no cover - best effort
                         log.warning("rollback of %s/%s annotations failed: %s", namespace, name, e2)
                     raise
                 self.metrics.bound(d)
                 log.info("bound %s to %s devices %s score %.2f (%s)", key, node, list(d.ids), d.score, d.policy)
+                if self.cfg.events:
+                    record_event(self.api, pod, "GPUTopologyBound",
+                                 f"assigned devices {list(d.ids)} on {node} (score {d.score:.2f}, {d.policy})",
+                                 component="gpu-topology-extender")
                 return d
+        except Exception as e:
+            if self.cfg.events and pod is not None:
+                record_event(self.api, pod, "FailedGPUTopologyBind", f"bind to {node} failed: {e}", "Warning",
+                             component="gpu-topology-extender")
+            raise
         finally:
             self.metrics.observe("bind", time.perf_counter() - t0)
 

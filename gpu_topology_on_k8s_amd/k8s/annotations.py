@@ -60,9 +60,20 @@ class Contract:
         return f"{self.prefix}/probe-time"
 
     @property
-    def cpuset_key(self) -> str:
-        """Pod annotation: recommended NUMA node(s) / cpuset for the kubelet CPU manager (Gaia B6)."""
+    def numa_key(self) -> str:
+        """Pod annotation: NUMA node(s) of the assigned devices (Gaia B6)."""
         return f"{self.prefix}/numa-nodes"
+
+    @property
+    def cpuset_key(self) -> str:
+        """Pod annotation: recommended cpuset = the assigned devices' local cores (Gaia B6 CPU binding)."""
+        return f"{self.prefix}/cpuset"
+
+    @property
+    def fraction_key(self) -> str:
+        """Pod annotation: a fraction 0<m<1 of ONE physical GPU, served as ceil(m * partitions) XCPs
+        of one package on a CPX/DPX/QPX node (Gaia Fragment, paper Alg. 2)."""
+        return f"{self.prefix}/gpu-fraction"
 
     @property
     def score_key(self) -> str:

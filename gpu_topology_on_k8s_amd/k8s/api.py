@@ -12,10 +12,10 @@ from __future__ import annotations
 import json
 import os
 import threading
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, Iterator, List, Optional, Tuple
 from urllib.parse import quote
 
-__all__ = ["ApiError", "Conflict", "NotFound", "KubeAPI", "RestKubeAPI"]
+__all__ = ["ApiError", "Conflict", "NotFound", "Gone", "KubeAPI", "RestKubeAPI"]
 
 Obj = Dict[str, Any]
 
@@ -37,9 +37,18 @@ class NotFound(ApiError):
         super().__init__(404, message)
 
 
+class Gone(ApiError):
+    """410: a watch's resourceVersion fell out of the apiserver's window; relist."""
+
+    def __init__(self, message: str = "gone"):
+        super().__init__(410, message)
+
+
 def raise_for(code: int, message: str) -> None:
     if code == 404:
         raise NotFound(message)
+    if code == 410:
+        raise Gone(message)
     if code == 409:
         raise Conflict(message)
     raise ApiError(code, message)
@@ -71,6 +80,19 @@ class KubeAPI:
         raise NotImplementedError
 
     def bind_pod(self, namespace: str, name: str, uid: str, node: str) -> None:
+        raise NotImplementedError
+
+    def create_event(self, namespace: str, event: Obj) -> Obj:
+        """POST a core/v1 Event (see :func:`.events.record_event`)."""
+        raise NotImplementedError
+
+    def list_with_version(self, kind: str, node_name: Optional[str] = None) -> Tuple[List[Obj], str]:
+        """(items, list resourceVersion) of ``kind`` in {"Node", "Pod"}: the LIST half of an informer."""
+        raise NotImplementedError
+
+    def watch_stream(self, kind: str, resource_version: str, timeout: float = 60.0,
+                     stop: Optional[threading.Event] = None) -> Iterator[Tuple[str, Obj]]:
+        """(event type, object) after ``resource_version`` until ``timeout``: the WATCH half."""
         raise NotImplementedError
 
 
@@ -168,3 +190,36 @@ class RestKubeAPI(KubeAPI):
             "target": {"apiVersion": "v1", "kind": "Node", "name": node},
         }
         self._do("POST", f"/api/v1/namespaces/{quote(namespace)}/pods/{quote(name)}/binding", body)
+
+    def create_event(self, namespace: str, event: Obj) -> Obj:
+        return self._do("POST", f"/api/v1/namespaces/{quote(namespace)}/events", event)
+
+    _KIND_PATH = {"Node": "/api/v1/nodes", "Pod": "/api/v1/pods"}
+
+    def list_with_version(self, kind: str, node_name: Optional[str] = None) -> Tuple[List[Obj], str]:
+        path = self._KIND_PATH[kind]
+        if node_name and kind == "Pod":
+            path += "?fieldSelector=" + quote(f"spec.nodeName={node_name}")
+        d = self._do("GET", path)
+        return d.get("items", []), str((d.get("metadata") or {}).get("resourceVersion", ""))
+
+    def watch_stream(self, kind: str, resource_version: str, timeout: float = 60.0,
+                     stop: Optional[threading.Event] = None) -> Iterator[Tuple[str, Obj]]:
+        """``GET {path}?watch=1&resourceVersion=..&timeoutSeconds=..&allowWatchBookmarks=true`` read
+        line by line; BOOKMARKs are yielded (they carry only a resourceVersion), an ERROR 410 raises
+        :class:`Gone`."""
+        url = (f"{self.base}{self._KIND_PATH[kind]}?watch=1&allowWatchBookmarks=true"
+               f"&resourceVersion={quote(str(resource_version))}&timeoutSeconds={int(max(1, timeout))}")
+        with self._session().get(url, stream=True, timeout=(self.timeout, timeout + 30), verify=self._verify) as r:
+            if r.status_code >= 400:
+                raise_for(r.status_code, r.text[:300])
+            for line in r.iter_lines():
+                if stop is not None and stop.is_set():
+                    return
+                if not line:
+                    continue
+                ev = json.loads(line)
+                t, obj = ev.get("type", ""), ev.get("object") or {}
+                if t == "ERROR":
+                    raise_for(int(obj.get("code", 500)), str(obj.get("message", "watch error")))
+                yield t, obj

@@ -17,12 +17,12 @@ import json
 import threading
 import time
 import uuid
-from collections import defaultdict
+from collections import defaultdict, deque
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
-from typing import Any, Callable, Dict, List, Optional, Tuple
+from typing import Any, Callable, Dict, Iterator, List, Optional, Tuple
 from urllib.parse import parse_qs, unquote, urlparse
 
-from .api import ApiError, Conflict, KubeAPI, NotFound, raise_for
+from .api import ApiError, Conflict, Gone, KubeAPI, NotFound, raise_for
 from .objects import meta
 
 __all__ = ["FakeAPIServer", "serve_http"]
@@ -65,13 +65,17 @@ def _match_labels(obj: Obj, selector: Optional[str]) -> bool:
 
 
 class FakeAPIServer(KubeAPI):
-    def __init__(self):
+    def __init__(self, history: int = 100_000):
         self._lock = threading.RLock()
+        self._changed = threading.Condition(self._lock)
         self._rv = 0
         self.nodes: Dict[str, Obj] = {}
         self.pods: Dict[Tuple[str, str], Obj] = {}
+        self.events: List[Obj] = []
         self._faults: Dict[str, List[Tuple[int, int]]] = defaultdict(list)  # op -> [(code, remaining)]
         self._watchers: List[Watcher] = []
+        # watch cache: (rv, type, kind, object) of every change; a watch older than the window gets 410
+        self._history: "deque[Tuple[int, str, str, Obj]]" = deque(maxlen=history)
         self.calls: Dict[str, int] = defaultdict(int)
         self.latency_s = 0.0
 
@@ -103,8 +107,50 @@ class FakeAPIServer(KubeAPI):
             self._watchers.append(fn)
 
     def _emit(self, event: str, kind: str, obj: Obj) -> None:
+        self._history.append((int(meta(obj).get("resourceVersion") or self._rv), event, kind, copy.deepcopy(obj)))
+        self._changed.notify_all()
         for w in list(self._watchers):
             w(event, kind, copy.deepcopy(obj))
+
+    # ------------------------------------------------------------------ LIST+WATCH (informers)
+    def list_with_version(self, kind: str, node_name: Optional[str] = None) -> Tuple[List[Obj], str]:
+        """(items, list resourceVersion): what ``GET /api/v1/{nodes,pods}`` returns."""
+        with self._lock:
+            items = self.list_nodes() if kind == "Node" else self.list_pods(node_name=node_name)
+            return items, str(self._rv)
+
+    def watch_stream(self, kind: str, resource_version: str, timeout: float = 60.0,
+                     stop: Optional[threading.Event] = None) -> Iterator[Tuple[str, Obj]]:
+        """Changes of ``kind`` after ``resource_version``, blocking up to ``timeout`` s for new ones
+        (``GET ...?watch=1``).  Raises :class:`Gone` when the window no longer reaches back that far."""
+        self.calls[f"watch_{kind}"] += 1
+        since = int(resource_version or 0)
+        deadline = time.monotonic() + timeout
+        with self._lock:
+            if self._history and since < self._history[0][0] - 1 and len(self._history) == self._history.maxlen:
+                raise Gone(f"resourceVersion {since} is too old")
+        while stop is None or not stop.is_set():
+            with self._lock:
+                batch = [(t, o) for rv, t, k, o in self._history if rv > since and k == kind]
+                if self._history:
+                    since = max(since, self._history[-1][0])
+                if not batch:
+                    left = deadline - time.monotonic()
+                    if left <= 0:
+                        return
+                    self._changed.wait(min(left, 0.25))
+                    continue
+            for t, o in batch:
+                yield t, copy.deepcopy(o)
+
+    def create_event(self, namespace: str, event: Obj) -> Obj:
+        with self._lock:
+            self._enter("create_event")
+            ev = copy.deepcopy(event)
+            meta(ev).setdefault("namespace", namespace)
+            meta(ev)["resourceVersion"] = self._next_rv()
+            self.events.append(ev)
+            return copy.deepcopy(ev)
 
     # ------------------------------------------------------------------ object creation (tests/sim)
     def create_node(self, node: Obj) -> Obj:
@@ -137,6 +183,7 @@ class FakeAPIServer(KubeAPI):
             pod = self.pods.pop((namespace, name), None)
             if pod is None:
                 raise NotFound(f"pod {namespace}/{name}")
+            meta(pod)["resourceVersion"] = self._next_rv()
             self._emit("DELETED", "Pod", pod)
 
     def set_pod_phase(self, namespace: str, name: str, phase: str) -> Obj:
@@ -268,8 +315,13 @@ class _Handler(BaseHTTPRequestHandler):
             if parts[:2] != ["api", "v1"]:
                 raise NotFound(u.path)
             rest = parts[2:]
+            watch = (q.get("watch") or ["0"])[0] in ("1", "true")
+            if rest in (["nodes"], ["pods"]) and method == "GET" and watch:
+                return self._watch("Node" if rest == ["nodes"] else "Pod", (q.get("resourceVersion") or ["0"])[0],
+                                   float((q.get("timeoutSeconds") or ["60"])[0]))
             if rest == ["nodes"] and method == "GET":
-                return self._send(200, {"kind": "NodeList", "items": self.api.list_nodes((q.get("labelSelector") or [None])[0])})
+                items, rv = self.api.list_with_version("Node")
+                return self._send(200, {"kind": "NodeList", "metadata": {"resourceVersion": rv}, "items": items})
             if len(rest) == 2 and rest[0] == "nodes":
                 if method == "GET":
                     return self._send(200, self.api.get_node(rest[1]))
@@ -281,7 +333,10 @@ class _Handler(BaseHTTPRequestHandler):
             if fs.startswith("spec.nodeName="):
                 node_name = fs.split("=", 1)[1]
             if rest == ["pods"] and method == "GET":
-                return self._send(200, {"kind": "PodList", "items": self.api.list_pods(node_name=node_name)})
+                items, rv = self.api.list_with_version("Pod", node_name=node_name)
+                return self._send(200, {"kind": "PodList", "metadata": {"resourceVersion": rv}, "items": items})
+            if len(rest) == 3 and rest[0] == "namespaces" and rest[2] == "events" and method == "POST":
+                return self._send(201, self.api.create_event(rest[1], self._body()))
             if len(rest) >= 3 and rest[0] == "namespaces" and rest[2] == "pods":
                 ns = rest[1]
                 if len(rest) == 3 and method == "GET":
@@ -300,6 +355,28 @@ class _Handler(BaseHTTPRequestHandler):
             raise NotFound(f"{method} {u.path}")
         except ApiError as e:
             return self._send(e.code, {"kind": "Status", "status": "Failure", "code": e.code, "message": e.message})
+
+    def _watch(self, kind: str, rv: str, timeout: float) -> None:
+        """Watch response: one JSON ``{"type", "object"}`` per line until ``timeoutSeconds`` (HTTP/1.0,
+        body ends when the connection closes, as a chunked watch does for a streaming client)."""
+        try:
+            stream = self.api.watch_stream(kind, rv, timeout)
+            first = next(stream, None)
+        except Gone as e:
+            return self._send(200, {"type": "ERROR", "object": {"kind": "Status", "code": 410, "reason": "Expired",
+                                                                "message": e.message}})
+        self.send_response(200)
+        self.send_header("Content-Type", "application/json")
+        self.end_headers()
+        try:
+            if first is not None:
+                self.wfile.write((json.dumps({"type": first[0], "object": first[1]}) + "\n").encode())
+                self.wfile.flush()
+                for t, o in stream:
+                    self.wfile.write((json.dumps({"type": t, "object": o}) + "\n").encode())
+                    self.wfile.flush()
+        except (BrokenPipeError, ConnectionResetError):
+            pass
 
     def do_GET(self):
         self._route("GET")

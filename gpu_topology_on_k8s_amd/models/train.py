@@ -50,9 +50,10 @@ def _choose_device(env, placement: str, discovery: str) -> Dict[str, object]:
         from ..parallel.allreduce import choose_subset
 
         ch = choose_subset(env["world"], backend=discovery)
-        devices = ch.devices if placement == "best" or not ch.worst else ch.worst
-        info = {"devices": devices, "best": ch.devices, "best_score": ch.score, "worst": ch.worst,
-                "worst_score": ch.worst_score, "source": ch.source}
+        use_worst = placement == "worst" and ch.worst
+        devices = ch.worst if use_worst else ch.devices  # node-local topology indices (GROUP numbering)
+        info = {"devices": devices, "hip_devices": ch.worst_hip if use_worst else ch.hip_devices, "best": ch.devices,
+                "best_score": ch.score, "worst": ch.worst, "worst_score": ch.worst_score, "source": ch.source}
         store.set("gtk/train_placement", json.dumps(info))
     return json.loads(store.get("gtk/train_placement").decode())
 
@@ -66,7 +67,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
     env = _init_dist(device_kind)
     if device_kind == "cuda":
         pl = _choose_device(env, placement, discovery)
-        dev = int(pl["devices"][env["rank"]])
+        dev = int(pl["hip_devices"][env["rank"]])
         torch.cuda.set_device(dev)
         device = torch.device("cuda", dev)
         gemm_mode = setup_gemm_tuning(gemm_tuning, gemm_table, env["rank"])

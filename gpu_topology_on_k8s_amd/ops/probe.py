@@ -9,6 +9,7 @@ left unmeasured (nan) and the cost model falls back to the discovered link class
 """
 from __future__ import annotations
 
+import logging
 import os
 import subprocess
 import sys
@@ -19,7 +20,10 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from .._native import load
+from ..topology.identity import DeviceMap
 from ..topology.model import Topology
+
+log = logging.getLogger(__name__)
 
 __all__ = ["device_count", "device_props", "warmup", "copy_bw", "gather_bw", "measure_matrix", "measure_ingress",
            "probe_topology", "probe_in_child", "ingress_bound", "PROBE_PRESETS"]
@@ -59,16 +63,31 @@ def gather_bw(dst: int, srcs: Sequence[int], nbytes: int = 64 << 20, iters: int 
     return dict(_p().gather_bw(int(dst), [int(s) for s in srcs], int(nbytes), int(iters), int(warmup_iters)))
 
 
-def measure_ingress(topo: Topology, devs: Sequence[int], preset: str = "quick") -> List[Optional[float]]:
-    """Aggregate ingress GB/s of every device in ``devs`` reading from all the others concurrently
-    (K5); stored in ``topo.probe["ingress_all_gbps"]`` (None where fewer than two devices)."""
+def _device_map(topo: Topology, dmap: Optional[DeviceMap]) -> DeviceMap:
+    if dmap is not None:
+        return dmap
+    m = DeviceMap.for_topology(topo)
+    if not m.by_bdf and m.n_visible != topo.n:
+        log.warning("topology has %d devices, HIP sees %d and no PCI address matches: probing HIP ordinals "
+                    "0..%d as topology indices", topo.n, m.n_visible, len(m.hip_of_index) - 1)
+    return m
+
+
+def measure_ingress(topo: Topology, devs: Sequence[int], preset: str = "quick",
+                    dmap: Optional[DeviceMap] = None) -> List[Optional[float]]:
+    """Aggregate ingress GB/s of every topology device in ``devs`` reading from all the others
+    concurrently (K5); stored in ``topo.probe["ingress_all_gbps"]`` (None where fewer than two
+    devices).  Topology indices are turned into HIP ordinals by PCI address (:class:`DeviceMap`)."""
     cfg = PROBE_PRESETS[preset]
+    m = _device_map(topo, dmap)
+    devs = [d for d in devs if d in m.hip_of_index]
     out: List[Optional[float]] = [None] * topo.n
     for d in devs:
-        peers = [s for s in devs if s != d and bool(_p().can_access_peer(d, s))]
+        hd = m.hip(d)
+        peers = [m.hip(s) for s in devs if s != d and bool(_p().can_access_peer(hd, m.hip(s)))]
         if not peers:
             continue
-        r = gather_bw(d, peers, cfg["bytes"], cfg["iters"], cfg["warmup"])
+        r = gather_bw(hd, peers, cfg["bytes"], cfg["iters"], cfg["warmup"])
         if not r["ok"]:
             raise RuntimeError(f"ingress probe verification failed on device {d}")
         out[d] = round(float(r["gbps"]), 2)
@@ -102,22 +121,30 @@ def measure_matrix(devs: Sequence[int], nbytes: int = 64 << 20, iters: int = 3, 
 
 
 def probe_topology(topo: Topology, preset: str = "quick", devs: Optional[List[int]] = None, mode: str = "read",
-                   kind: str = "lds", warm_ms: float = 50.0) -> Topology:
-    """Measure every visible pair and fold it into ``topo`` (in place; also returned)."""
+                   kind: str = "lds", warm_ms: float = 50.0, dmap: Optional[DeviceMap] = None) -> Topology:
+    """Measure every visible pair and fold it into ``topo`` (in place; also returned).
+
+    ``devs`` are *topology indices* (default: every device this process can reach).  Each is run on
+    the HIP ordinal with the same PCI address, so a probe under ``HIP_VISIBLE_DEVICES`` or inside a
+    pod writes its numbers into the right rows of the node matrix."""
     cfg = PROBE_PRESETS[preset]
     ndev = device_count()
     if ndev == 0:
         raise RuntimeError("no HIP devices visible: cannot probe")
-    devs = list(range(min(ndev, topo.n))) if devs is None else list(devs)
+    m = _device_map(topo, dmap)
+    devs = m.visible_indices() if devs is None else [d for d in devs if d in m.hip_of_index]
+    if not devs:
+        raise RuntimeError("none of the requested topology devices is visible to HIP")
     t0 = time.time()
-    w = warmup(devs[0], warm_ms)
+    w = warmup(m.hip(devs[0]), warm_ms)
     bw = np.full((topo.n, topo.n), np.nan)
     hbm = np.full(topo.n, np.nan)
     for i in devs:
         for j in devs:
-            if i != j and not bool(_p().can_access_peer(j if mode == "read" else i, i if mode == "read" else j)):
+            hi, hj = m.hip(i), m.hip(j)
+            if i != j and not bool(_p().can_access_peer(hj if mode == "read" else hi, hi if mode == "read" else hj)):
                 continue
-            r = copy_bw(i, j, cfg["bytes"], cfg["iters"], cfg["warmup"], mode=mode, kind=kind)
+            r = copy_bw(hi, hj, cfg["bytes"], cfg["iters"], cfg["warmup"], mode=mode, kind=kind)
             if not r["ok"]:
                 raise RuntimeError(f"probe verification failed for {i}->{j}")
             if i == j:
@@ -133,6 +160,8 @@ def probe_topology(topo: Topology, preset: str = "quick", devs: Optional[List[in
             "bytes": cfg["bytes"],
             "iters": cfg["iters"],
             "devices": devs,
+            "hip_ordinals": [m.hip(d) for d in devs],
+            "device_map": "bdf" if m.by_bdf else "identity",
             "mfma_warmup_tflops": round(float(w["tflops"]), 1),
             "ts": int(time.time()),
             "seconds": round(time.time() - t0, 3),

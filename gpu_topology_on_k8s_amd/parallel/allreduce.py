@@ -54,6 +54,8 @@ class SubsetChoice:
     worst_score: Optional[float] = None
     placement_ms: float = 0.0
     probed: bool = False
+    hip_devices: List[int] = field(default_factory=list)  # HIP ordinal of devices[r] in this process
+    worst_hip: Optional[List[int]] = None
     extra: Dict[str, object] = field(default_factory=dict)
 
     def to_json(self) -> str:
@@ -151,38 +153,74 @@ def _schedule_via_k8s(topo, k: int, node: str = "") -> Dict[str, object]:
                 "sched_ms": round(r.sched_ms, 3), "admit_ms": round(r.admit_ms, 3)}
 
 
+def visible_view(topo, nvis: int, visible_bdfs: Optional[Sequence[str]] = None):
+    """(placement topology, DeviceMap, source suffix) for a process that sees ``nvis`` HIP devices.
+
+    The node model keeps its indices (the ``ALIYUN_COM_GPU_GROUP`` numbering) and measured links; the
+    devices this process cannot reach (``HIP_VISIBLE_DEVICES``, a pod's device cgroup) are marked
+    unavailable in a *copy*, so placement and the in-process k8s flow only pick reachable devices,
+    and the map turns the chosen indices into HIP ordinals by PCI address.  Without any address
+    match (fake/fixture topologies) the first ``nvis`` indices are taken as ordinals 0..nvis-1; a
+    model smaller than what HIP sees is replaced by a full mesh of the visible devices."""
+    import copy
+
+    from ..topology.discovery import fake_topology
+    from ..topology.identity import DeviceMap
+
+    if visible_bdfs is not None:
+        dmap = DeviceMap.for_topology(topo, visible_bdfs)
+        nvis = len(visible_bdfs)
+    else:
+        dmap = DeviceMap.identity(min(topo.n, nvis))
+        dmap.n_topology, dmap.n_visible = topo.n, nvis
+    suffix = "" if dmap.by_bdf or topo.n == nvis else "->visible-prefix"
+    if not dmap.by_bdf and topo.n < nvis:
+        log.warning("topology has %d devices but %d are visible to HIP; using a full-mesh model of the visible set", topo.n, nvis)
+        return fake_topology(nvis), DeviceMap.identity(nvis), "->visible-mesh"
+    hidden = dmap.hidden_indices()
+    if hidden:
+        topo = copy.deepcopy(topo)
+        for i in hidden:
+            topo.gpus[i].healthy = False
+    return topo, dmap, suffix
+
+
 def choose_subset(k: int, probe: Optional[str] = None, backend: str = "auto", visible: Optional[int] = None,
-                  topology=None, via_k8s: bool = False) -> SubsetChoice:
+                  topology=None, via_k8s: bool = False, visible_bdfs: Optional[Sequence[str]] = None) -> SubsetChoice:
     """Rank-0 side: discover the node, optionally probe links, run the placement core.
 
-    ``visible`` overrides the HIP device count (CPU/gloo runs model a mesh of that many devices);
-    ``topology`` is an already discovered (and probed) node, e.g. from :func:`probe_node`."""
+    ``visible`` overrides the HIP device count (CPU/gloo runs model a mesh of that many devices, with
+    no PCI addresses); otherwise the visible devices' PCI addresses (``visible_bdfs``, queried from
+    HIP when None) map the node's topology indices onto HIP ordinals (:func:`visible_view`).
+    ``topology`` is an already discovered (and probed) node, e.g. from :func:`probe_node`.
+    ``devices`` of the result are node-local topology indices (what GROUP carries); ``hip_devices``
+    are what each rank binds to."""
     from ..placement import PlacementPolicy, select, worst
     from ..topology.discovery import DiscoveryError, discover, fake_topology
+    from ..topology.identity import DeviceMap, hip_device_bdfs
 
-    nvis = _visible_device_count() if visible is None else int(visible)
+    if visible is None and visible_bdfs is None:
+        visible_bdfs = hip_device_bdfs()
+    nvis = len(visible_bdfs) if visible is None else int(visible)
     t0 = time.perf_counter()
     try:
-        topo = topology if topology is not None else discover(backend)
-        source = topo.source
-        if topo.n != nvis:
-            log.warning("topology has %d devices but %d are visible to HIP; using a full-mesh model of the visible set", topo.n, nvis)
-            topo = fake_topology(nvis)
-            source = f"{source}->visible-mesh"
+        node = topology if topology is not None else discover(backend)
+        topo, dmap, suffix = visible_view(node, nvis, visible_bdfs if visible is None else None)
+        source = node.source + suffix
     except DiscoveryError as e:
         log.warning("topology discovery failed (%s); using a full-mesh model of %d visible devices", e, nvis)
-        topo = fake_topology(nvis)
-        source = "fallback-mesh"
+        topo, dmap, source = fake_topology(nvis), DeviceMap.identity(nvis), "fallback-mesh"
     probed = bool(topo.probe)
     if probe and not probed:
         from ..ops.probe import probe_topology
 
-        probe_topology(topo, preset=probe)
+        probe_topology(topo, preset=probe, dmap=dmap)
         probed = True
     t1 = time.perf_counter()
     pl = select(topo, k, policy=PlacementPolicy())
     ms = (time.perf_counter() - t1) * 1e3
-    w = worst(topo, k) if k < topo.n else None
+    n_avail = int(topo.healthy_mask().sum())
+    w = worst(topo, k) if k < n_avail else None
     devices, score, objective = list(pl.ids), pl.score, pl.objective
     k8s: Optional[Dict[str, object]] = None
     if via_k8s:
@@ -207,7 +245,10 @@ def choose_subset(k: int, probe: Optional[str] = None, backend: str = "auto", vi
         worst_score=round(w.score, 4) if w else None,
         placement_ms=round(ms, 4),
         probed=probed,
-        extra={"discovery_ms": round((t1 - t0) * 1e3, 2), "node_devices": topo.n,
+        hip_devices=[dmap.hip(i) for i in devices],
+        worst_hip=[dmap.hip(i) for i in w.ids] if w else None,
+        extra={"discovery_ms": round((t1 - t0) * 1e3, 2), "node_devices": topo.n, "visible_devices": nvis,
+               "device_map": dmap.to_dict(), "worst_exact": bool(w.exact) if w else None,
                **({"probe": probe_summary(topo, devices)} if probed else {}),
                **({"k8s": k8s} if k8s is not None else {})},
     )

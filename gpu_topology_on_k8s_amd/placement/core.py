@@ -39,7 +39,8 @@ import numpy as np
 
 from ..topology.model import Topology
 
-__all__ = ["PlacementPolicy", "Placement", "Problem", "select", "evaluate", "score_from_objective", "NoFeasiblePlacement"]
+__all__ = ["PlacementPolicy", "Placement", "Problem", "select", "worst", "select_with", "place_fraction", "evaluate",
+           "score_from_objective", "NoFeasiblePlacement"]
 
 EPS = 1e-9
 
@@ -304,20 +305,74 @@ def select(
     return Placement(ids=tuple(int(c) for c in choice), objective=j, score=score_from_objective(j), comm=terms["comm"], terms=terms, exact=exact)
 
 
-def worst(topo: Topology, k: int, used: Sequence[int] = (), policy: PlacementPolicy = PlacementPolicy()) -> Placement:
-    """Highest-objective subset (the "worst-topology placement" of BASELINE config 5)."""
+def _greedy_ascent(p: Problem, k: int, policy: PlacementPolicy, stats) -> List[int]:
+    """Python twin of the engine's maximising greedy (growth from every seed + 1-swap ascent)."""
+    free_ids = [i for i in range(p.n) if p.free[i]]
+    best: Optional[List[int]] = None
+    best_j = -math.inf
+    for seed in free_ids:
+        cur = [seed]
+        while len(cur) < k:
+            cand, cj = None, -math.inf
+            for c in free_ids:
+                if c not in cur:
+                    j, _ = evaluate(p, cur + [c], policy, stats)
+                    if j > cj + EPS:
+                        cj, cand = j, c
+            cur.append(cand)
+        cur_j, _ = evaluate(p, cur, policy, stats)
+        improved = True
+        while improved:
+            improved = False
+            for a_pos in range(len(cur)):
+                for b in (c for c in free_ids if c not in cur):
+                    trial = cur.copy()
+                    trial[a_pos] = b
+                    tj, _ = evaluate(p, trial, policy, stats)
+                    if tj > cur_j + EPS:
+                        cur, cur_j, improved = trial, tj, True
+                        break
+                if improved:
+                    break
+        cur = sorted(cur)
+        if cur_j > best_j + EPS or (abs(cur_j - best_j) <= EPS and cur < best):
+            best, best_j = cur, cur_j
+    assert best is not None
+    return best
+
+
+def worst(topo: Topology, k: int, used: Sequence[int] = (), policy: PlacementPolicy = PlacementPolicy(),
+          engine: str = "auto") -> Placement:
+    """Highest-objective subset (the "worst-topology placement" of BASELINE config 5).
+
+    Exhaustive while C(free, k) fits the budget (``node_limit`` natively, ``exact_limit`` in
+    Python), otherwise greedy ascent + 1-swap (``exact=False``): a CPX node (64 XCPs, k=8) is
+    C(64,8) ~ 4.4e9 subsets, which must never be enumerated in a request or a bench start-up."""
     p = Problem.from_topology(topo, used, partition_aware=policy.partition_aware)
-    stats = _level_stats(p)
     free_ids = [i for i in range(p.n) if p.free[i]]
     if len(free_ids) < k:
         raise NoFeasiblePlacement(f"need {k} free devices, have {len(free_ids)}")
-    bj, bc = -math.inf, None
-    for comb in itertools.combinations(free_ids, k):
-        j, _ = evaluate(p, comb, policy, stats)
-        if j > bj + EPS:
-            bj, bc = j, comb
+    mod = _native_engine() if engine != "python" else None
+    if mod is not None:
+        args = (np.ascontiguousarray(p.cost, dtype=np.float64), np.ascontiguousarray(p.free, dtype=bool),
+                [lv.astype(np.int64).tolist() for lv in p.levels], np.ascontiguousarray(p.access, dtype=np.float64))
+        r = mod.worst(*args, int(k), policy.w_span, policy.w_frag, policy.w_fit, policy.w_access, int(policy.exact_limit))
+        terms = dict(r["terms"])
+        terms["search_us"] = float(r["micros"])
+        return Placement(ids=tuple(int(i) for i in r["ids"]), objective=float(r["objective"]),
+                         score=score_from_objective(r["objective"]), comm=terms["comm"], terms=terms, exact=bool(r["exact"]))
+    stats = _level_stats(p)
+    if math.comb(len(free_ids), k) <= policy.exact_limit:
+        bj, bc = -math.inf, None
+        for comb in itertools.combinations(free_ids, k):
+            j, _ = evaluate(p, comb, policy, stats)
+            if j > bj + EPS:
+                bj, bc = j, comb
+        exact = True
+    else:
+        bc, exact = tuple(_greedy_ascent(p, k, policy, stats)), False
     j, terms = evaluate(p, bc, policy, stats)
-    return Placement(ids=tuple(bc), objective=j, score=score_from_objective(j), comm=terms["comm"], terms=terms)
+    return Placement(ids=tuple(bc), objective=j, score=score_from_objective(j), comm=terms["comm"], terms=terms, exact=exact)
 
 
 def select_with(topo: Topology, k: int, available: Sequence[int], must_include: Sequence[int] = (),
@@ -351,3 +406,33 @@ def select_with(topo: Topology, k: int, available: Sequence[int], must_include: 
         c = min((x for x in rest if x not in cur), key=lambda x: evaluate(p, cur + [x], policy, stats)[0])
         cur.append(c)
     return tuple(sorted(cur))
+
+
+def place_fraction(topo: Topology, k: int, used: Sequence[int] = (), access: Optional[Sequence[float]] = None) -> Tuple[int, ...]:
+    """A fraction of ONE physical GPU as ``k`` of its XCP partitions (Gaia Fragment, paper p.4-5 Alg. 2;
+    ``gaia_gpu_topology_scheduler.md:32``), the MI355X-native form of a 0<m<1 request: CPX/DPX/QPX
+    hardware partitions instead of API interception.
+
+    Candidates are packages already partly in use with >= k free XCPs; the best fit (fewest XCPs
+    left over, the author's note on Alg. 2: "closest to m, so the fragment waste is smallest")
+    wins.  Without one, the first pristine package is opened.  Ties break on mean access cost, then
+    package id.  Raises :class:`NoFeasiblePlacement` when no package can host ``k``."""
+    phys = topo.physical
+    healthy = topo.healthy_mask()
+    usedset = {int(u) for u in used}
+    acc = np.zeros(topo.n) if access is None else np.asarray(access, dtype=np.float64)
+    pk: Dict[int, List[int]] = {}
+    for i in range(topo.n):
+        pk.setdefault(int(phys[i]), []).append(i)
+    partial, pristine = [], []
+    for g, members in sorted(pk.items()):
+        free = [i for i in members if healthy[i] and i not in usedset]
+        if len(free) < k:
+            continue
+        take = free[:k]
+        key = (len(free) - k, float(np.mean(acc[take])), g)
+        (pristine if len(free) == len(members) else partial).append((key, take))
+    pool = partial or pristine
+    if not pool:
+        raise NoFeasiblePlacement(f"no physical GPU has {k} free partitions")
+    return tuple(min(pool)[1])

@@ -30,7 +30,7 @@ import json
 from urllib.parse import urlsplit
 from aiohttp import web
 
-from ..deviceplugin import DevicePluginServer, FakeKubelet, PluginConfig
+from ..deviceplugin import DevicePluginServer, FakeKubelet, PluginConfig, placeholder_dev_tree
 from ..extender import ExtenderConfig, TopologyExtender
 from ..extender.server import DEFAULT_PREFIX, make_app
 from ..k8s import Contract, FakeAPIServer, PodAssignment
@@ -185,8 +185,9 @@ class _Node:
 class SimCluster:
     def __init__(self, nodes: Dict[str, Topology], resource: str = "amd.com/gpu", policy_name: str = "exact",
                  policy: PlacementPolicy = PlacementPolicy(), assume_ttl: float = 300.0, use_filter: bool = True,
-                 node_labels: Optional[Dict[str, Dict[str, str]]] = None):
+                 node_labels: Optional[Dict[str, Dict[str, str]]] = None, device_specs: str = "strict"):
         self.resource = resource
+        self.device_specs = device_specs
         self.contract = Contract(resource_name=resource)
         self.api = FakeAPIServer()
         self.ext_cfg = ExtenderConfig(contract=self.contract, policy_name=policy_name, policy=policy, assume_ttl=assume_ttl,
@@ -208,8 +209,14 @@ class SimCluster:
             sockdir = os.path.join(self._root, f"n{i}")
             kubelet = FakeKubelet(sockdir, node_name=name, api=self.api)
             kubelet.start()
+            if self.device_specs == "strict":  # a node with (placeholder) ROCm device nodes
+                dev_root = placeholder_dev_tree(os.path.join(self._root, f"dev{i}"), topo)
+            else:  # a kind node: no /dev/kfd, no render nodes
+                dev_root = os.path.join(self._root, f"dev{i}")
+                os.makedirs(dev_root, exist_ok=True)
             plugin = DevicePluginServer(topo, PluginConfig(resource_name=self.resource, socket_dir=sockdir, node_name=name,
-                                                           contract=self.contract), api=self.api)
+                                                           contract=self.contract, dev_root=dev_root,
+                                                           device_specs=self.device_specs), api=self.api)
             plugin.start()
             kubelet.wait_for(self.resource)
             self.nodes[name] = _Node(name, topo, sockdir, kubelet, plugin)

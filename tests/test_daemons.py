@@ -60,8 +60,12 @@ def test_device_plugin_daemon_registers_and_publishes():
     sockdir = tempfile.mkdtemp(prefix="gtkd", dir="/tmp")
     kubelet = FakeKubelet(sockdir, node_name="worker-1", api=api)
     kubelet.start()
+    mport = _free_port()
+    devroot = os.path.join(sockdir, "dev")  # a kind node: no ROCm device nodes at all
+    os.makedirs(devroot)
     p = _spawn(["gpu_topology_on_k8s_amd.deviceplugin", "--discovery", "fake", "--fake-gpus", "4", "--apiserver", url,
-                "--node-name", "worker-1", "--socket-dir", sockdir, "--resource-name", "aliyun.com/gpu", "--log-level", "WARNING"])
+                "--node-name", "worker-1", "--socket-dir", sockdir, "--resource-name", "aliyun.com/gpu", "--log-level", "WARNING",
+                "--dev-root", devroot, "--metrics-port", str(mport), "--metrics-host", "127.0.0.1"])
     try:
         plugin = kubelet.wait_for("aliyun.com/gpu", timeout=60)
         assert sorted(plugin.devices) == ["0", "1", "2", "3"]
@@ -69,8 +73,13 @@ def test_device_plugin_daemon_registers_and_publishes():
         assert "GPU_XGMI_0_1" in node["metadata"]["annotations"]
         assert node["status"]["capacity"]["aliyun.com/gpu"] == "4"
         pod = api.create_pod(make_pod("p", gpus=2, node="worker-1", resource="aliyun.com/gpu"))
-        resp = kubelet.admit(pod, "aliyun.com/gpu")
-        assert resp.container_responses[0].devices[0].container_path == "/dev/kfd"
+        resp = kubelet.admit(pod, "aliyun.com/gpu")  # the fake kubelet rejects host paths that do not exist
+        c = resp.container_responses[0]
+        assert list(c.devices) == []  # --discovery fake => stub DeviceSpecs: envs + annotations only (BASELINE config 1)
+        assert c.envs["GTK_GPU_GROUP"] and len(c.envs["GTK_GPU_BDFS"].split(",")) == 2
+        scrape = lambda: requests.get(f"http://127.0.0.1:{mport}/metrics", timeout=5).text  # noqa: E731
+        assert _wait(lambda: "gtk_plugin_registrations_total 1.0" in scrape(), 10)  # counted once Register returns
+        assert 'gtk_plugin_allocations_total{outcome="ok"} 1.0' in scrape()
     finally:
         rc = _stop(p)
         kubelet.stop()

@@ -6,7 +6,9 @@ import time
 import grpc
 import pytest
 
-from gpu_topology_on_k8s_amd.deviceplugin import DevicePluginServer, FakeKubelet, PluginConfig
+import os
+
+from gpu_topology_on_k8s_amd.deviceplugin import DevicePluginServer, FakeKubelet, PluginConfig, placeholder_dev_tree
 from gpu_topology_on_k8s_amd.deviceplugin import proto as pb
 from gpu_topology_on_k8s_amd.extender import ExtenderConfig, TopologyExtender
 from gpu_topology_on_k8s_amd.k8s import ANN_ASSIGNED, ANN_ASSUME_TIME, ANN_GROUP, Contract, FakeAPIServer, PodAssignment
@@ -30,7 +32,8 @@ def node(sockdir):
     kubelet = FakeKubelet(sockdir, node_name="n1", api=api)
     kubelet.start()
     topo = fx.f7_mi355x()
-    plugin = DevicePluginServer(topo, PluginConfig(resource_name=RES, socket_dir=sockdir, node_name="n1"), api=api)
+    dev = placeholder_dev_tree(os.path.join(sockdir, "dev"), topo)
+    plugin = DevicePluginServer(topo, PluginConfig(resource_name=RES, socket_dir=sockdir, node_name="n1", dev_root=dev), api=api)
     plugin.start()
     kubelet.wait_for(RES)
     yield api, kubelet, plugin, topo
@@ -93,7 +96,9 @@ def test_allocate_follows_extender_group_and_flips_assigned(node):
     for i in d.ids:
         assert f"/dev/dri/renderD{128 + i}" in paths and f"/dev/dri/card{i}" in paths
     assert all(x.permissions == "rw" for x in c.devices)
+    assert all(x.host_path.startswith(plugin.cfg.dev_root) and os.path.exists(x.host_path) for x in c.devices)
     assert c.envs["GTK_GPU_GROUP"] == ",".join(map(str, d.ids))
+    assert c.envs["GTK_GPU_BDFS"] == ",".join(topo.gpus[i].bdf for i in d.ids)  # GROUP -> HIP ordinal inside the pod
     assert "NVIDIA_VISIBLE_DEVICES" not in c.envs
     ann = api.get_pod("default", "train")["metadata"]["annotations"]
     assert ann[ANN_ASSIGNED] == "true" and ann[ANN_GROUP] == ",".join(map(str, d.ids))

@@ -61,7 +61,7 @@ def test_bind_writes_reference_annotations():
     assert ann[ANN_GROUP] == ",".join(map(str, d.ids))
     assert ann[ANN_ASSIGNED] == "false"
     assert ann[ANN_ASSUME_TIME] == str(int(clock.t))
-    assert ann[Contract().cpuset_key] in ("0", "1")  # both devices in one NUMA domain
+    assert ann[Contract().numa_key] in ("0", "1")  # both devices in one NUMA domain
 
 
 def test_config4_two_concurrent_four_gpu_pods_disjoint():
@@ -171,11 +171,22 @@ def test_transient_patch_errors_are_retried():
     assert len(_bind(api, ext, "a").ids) == 2
 
 
-def test_zero_gpu_pod_is_just_bound():
-    api, ext, _ = _cluster()
+def test_bind_refuses_unmanaged_pods():
+    """/bind must not place pods that kube-scheduler would never delegate to the extender
+    (no managed resource) or that belong to another scheduler."""
+    from gpu_topology_on_k8s_amd.k8s.api import ApiError
+
+    api, ext, _ = _cluster(scheduler_names=("default-scheduler",))
     _submit(api, "web", 0)
-    assert _bind(api, ext, "web") is None
-    assert api.get_pod("default", "web")["spec"]["nodeName"] == "n1"
+    with pytest.raises(ApiError) as ei:
+        _bind(api, ext, "web")
+    assert ei.value.code == 400 and "not managed" in str(ei.value)
+    assert not api.get_pod("default", "web")["spec"].get("nodeName")
+    _submit(api, "other", 2, scheduler_name="volcano")
+    with pytest.raises(ApiError) as ei:
+        _bind(api, ext, "other")
+    assert ei.value.code == 403
+    assert any(e["reason"] == "FailedGPUTopologyBind" and e["involvedObject"]["name"] == "web" for e in api.events)
 
 
 def test_model_quota_gaia_b7():
