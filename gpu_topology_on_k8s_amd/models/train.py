@@ -63,7 +63,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
           attn: str = "hip", seed: int = 0, log: bool = True, gemm_tuning: str = "auto",
           gemm_table: Optional[str] = None, gemm_layout: str = "nt", overlap_transposes: bool = False,
           zero1: bool = False, save_dir: Optional[str] = None, save_every: int = 0, resume: Optional[str] = None,
-          keep: int = 2, fuse_residual: bool = True, overlap_norm: bool = False) -> Dict[str, object]:
+          keep: int = 2, fuse_residual: bool = True, overlap_norm: bool = False, same_data: bool = False) -> Dict[str, object]:
     env = _init_dist(device_kind)
     if device_kind == "cuda":
         pl = _choose_device(env, placement, discovery)
@@ -83,7 +83,9 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
     opt = FlatAdamW(model.flat, lr=lr, shards=ar.shards() if zero1 else None)
     if zero1:
         model.param_ready = ar.wait_param
-    gen = torch.Generator(device="cpu").manual_seed(1234 + env["rank"])
+    # same_data: every rank draws rank 0's batches, so the averaged gradient equals the 1-rank
+    # gradient and a k-rank run must reproduce the 1-rank losses (the DP correctness check)
+    gen = torch.Generator(device="cpu").manual_seed(1234 + (0 if same_data else env["rank"]))
     start_step, resumed = 0, None
     if resume:
         meta = load_checkpoint(resume, model, opt, gen)
@@ -158,6 +160,8 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "mfu": mfu,
         "loss_first": float(losses[0]),
         "loss_last": float(losses[-1]),
+        "losses": [float(x) for x in losses],
+        "same_data": same_data,
         "buckets": ar.stats["buckets"],
         "zero1": zero1,
         "optimizer_state_gb": opt.state_bytes() / 1e9,
@@ -209,6 +213,8 @@ def main(argv=None) -> int:
                     help="checkpoint root (its latest) or step directory; any world size / --zero1 setting")
     ap.add_argument("--no-fuse-residual", action="store_true",
                     help="separate residual-add kernels instead of the fused add+RMSNorm (A/B)")
+    ap.add_argument("--same-data", action="store_true",
+                    help="every rank trains on rank 0's batches (k-rank losses must equal the 1-rank run)")
     ap.add_argument("--overlap-norm", action="store_true",
                     help="clipping norm per bucket on a side stream as buckets complete (measured no gain at world 1)")
     a = ap.parse_args(argv)
@@ -216,7 +222,7 @@ def main(argv=None) -> int:
           gemm_tuning=a.gemm_tuning, gemm_table=a.gemm_table, gemm_layout=a.gemm_layout,
           overlap_transposes=a.overlap_transposes, zero1=a.zero1, save_dir=a.save_dir, save_every=a.save_every,
           resume=a.resume, keep=a.keep, fuse_residual=not a.no_fuse_residual,
-          overlap_norm=a.overlap_norm)
+          overlap_norm=a.overlap_norm, same_data=a.same_data)
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0

@@ -1,0 +1,114 @@
+"""GPU, k >= 2: the multi-device paths the 8-GPU scaling run depends on (VERDICT r1 "next" #2).
+
+Every test here needs at least two visible MI355X and skips with the reason on a 1-GPU box; on the
+8-GPU node they localise a failure of the scaling curve to one component: the p2p probe kernels
+across a real xGMI pair (K1 read, K2 write), the all-peer gather (K5), the RCCL communicator at
+k=2 (bench.py, native backend, exact check, busBW bounded by the probe), hipGraph capture at k=2,
+and 2-rank Llama DP / ZeRO-1 against the 1-rank run.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _ndev() -> int:
+    import torch
+
+    return int(torch.cuda.device_count())  # counts without initialising HIP on this image
+
+
+needs2 = pytest.mark.skipif(_ndev() < 2, reason="needs >= 2 visible GPUs (single-GPU box)")
+
+
+def _run(args, timeout=900, env=None):
+    e = dict(os.environ, **(env or {}))
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    p = subprocess.run([sys.executable, *args], capture_output=True, text=True, timeout=timeout, cwd=REPO, env=e)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    return json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+
+
+@needs2
+@pytest.mark.parametrize("mode", ["read", "write"])
+def test_p2p_pair_copy(mode):
+    from gpu_topology_on_k8s_amd.ops import probe
+
+    assert probe.device_props(0)["pci_bus_id"] != probe.device_props(1)["pci_bus_id"]
+    r = probe.copy_bw(0, 1, 256 << 20, iters=3, warmup_iters=1, mode=mode)
+    assert r["ok"] and r["gbps"] > 10, r
+    back = probe.copy_bw(1, 0, 256 << 20, iters=3, warmup_iters=1, mode=mode)
+    assert back["ok"] and back["gbps"] > 10, back
+
+
+@needs2
+def test_gather_over_real_peers_beats_one_link():
+    from gpu_topology_on_k8s_amd.ops import probe
+
+    n = _ndev()
+    peers = list(range(1, n))
+    single = max(probe.copy_bw(s, 0, 64 << 20, iters=3, warmup_iters=1)["gbps"] for s in peers)
+    g = probe.gather_bw(0, peers, 64 << 20, iters=3, warmup_iters=1)
+    assert g["ok"], g
+    assert g["gbps"] >= 0.9 * single, (g, single)
+
+
+@needs2
+def test_probe_matrix_all_pairs():
+    from gpu_topology_on_k8s_amd.ops.probe import probe_topology
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
+
+    t = probe_topology(discover("auto"), preset="quick")
+    assert t.probe["device_map"] == "bdf"
+    n = len(t.probe["devices"])
+    import numpy as np
+
+    off = t.bw_gbps[np.ix_(t.probe["devices"], t.probe["devices"])][~np.eye(n, dtype=bool)]
+    assert np.isfinite(off).all() and (off > 10).all()
+
+
+@needs2
+def test_bench_two_gpus_native_exact_and_bounded():
+    out = _run(["bench.py", "--gpus", "2", "--steps", "5", "--warmup", "2", "--size-mb", "256", "--sweep", "8:64M:64",
+                "--ctas", "default"])
+    assert out["n_gpus"] == 2 and out["value_kind"] == "busbw" and out["config"]["backend"] == "native"
+    assert out["size_sweep"]["all_exact"]
+    assert len(set(out["config"]["hip_devices"])) == 2
+    bound = (out["link_probe"] or {}).get("subset_ingress_bound_gbps")
+    if bound:
+        assert out["busbw_gbps"] <= 1.10 * bound, (out["busbw_gbps"], bound)
+
+
+@needs2
+def test_bench_two_gpus_graph_capture():
+    out = _run(["bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--size-mb", "16", "--sweep", "8:4K:8",
+                "--graph", "on", "--ctas", "default", "--probe", "off"])
+    g = out["graph_latency"]
+    assert g and g.get("all_exact"), g
+
+
+@needs2
+def test_bench_two_gpus_ctas_tuning():
+    out = _run(["bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--size-mb", "64", "--sweep", "off", "--probe", "off"])
+    assert out["ctas_tuning"] and all(r["ms_per_step"] > 0 for r in out["ctas_tuning"])
+
+
+@needs2
+@pytest.mark.parametrize("zero1", [False, True])
+def test_two_rank_dp_matches_one_rank(zero1):
+    """Same data on both ranks: the averaged gradient is the 1-rank gradient, so the losses agree."""
+    base = ["--model", "tiny", "--batch", "2", "--seq", "128", "--steps", "2", "--warmup", "1", "--same-data",
+            "--gemm-tuning", "off"] + (["--zero1"] if zero1 else [])
+    one = _run(["-m", "gpu_topology_on_k8s_amd.models.train", *base])
+    two = _run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1",
+                "--master-port=29611", "-m", "gpu_topology_on_k8s_amd.models.train", *base])
+    assert two["n_gpus"] == 2 and len(two["losses"]) == len(one["losses"]) == 3
+    for a, b in zip(one["losses"], two["losses"]):
+        assert abs(a - b) <= 2e-2 * max(1.0, abs(a)), (one["losses"], two["losses"])
