@@ -43,6 +43,11 @@ struct Dev {
   int cus = 0;
   bool healthy = true;
   uint64_t location = 0;  // domain<<16 | bdf: physical-package key
+  // GPU<->CPU path (PCI sysfs): cores local to the device's socket, and the trained PCIe link as a
+  // fraction of its capability (speed x width; -1 = unreadable).  A link that trained at x8 or a
+  // lower generation is a worse CPU-affinity choice for the same xGMI position (design.md:144-145).
+  std::string cpulist;
+  double pcie_link_ratio = -1.0;
 };
 
 struct Result {
@@ -51,6 +56,7 @@ struct Result {
   std::vector<std::vector<int>> link_type, hops;  // link_type uses LinkType of model.py
   std::vector<std::vector<double>> weight, min_bw, max_bw;
   std::vector<std::vector<int>> p2p;
+  std::map<int, std::vector<int>> numa_distance;  // NUMA node -> SLIT distances to every node
   std::vector<std::string> warnings;
 };
 
@@ -115,6 +121,8 @@ py::dict to_py(const Result& r) {
     g["bad_pages"] = d.bad_pages;
     g["bad_page_threshold"] = d.bad_page_threshold;
     g["cus"] = d.cus;
+    g["cpu_affinity"] = d.cpulist;
+    g["pcie_link_ratio"] = d.pcie_link_ratio;
     gpus.append(g);
   }
   py::dict out;
@@ -126,6 +134,9 @@ py::dict to_py(const Result& r) {
   out["min_bw_mbps"] = r.min_bw;
   out["max_bw_mbps"] = r.max_bw;
   out["p2p"] = r.p2p;
+  py::dict nd;
+  for (const auto& kv : r.numa_distance) nd[py::int_(kv.first)] = kv.second;
+  out["numa_distance"] = nd;
   out["warnings"] = r.warnings;
   return out;
 }
@@ -402,6 +413,46 @@ std::string read_first_line(const std::string& path) {
   return s;
 }
 
+// "16.0 GT/s PCIe" -> 16.0 ; "32.0 GT/s" -> 32.0 ; unknown -> 0
+double link_speed_gts(const std::string& s) {
+  try {
+    return std::stod(s);
+  } catch (...) {
+    return 0.0;
+  }
+}
+
+std::string pci_dir(const std::string& pci_root, const std::string& bdf) {
+  // XCP partitions of one package may carry function numbers with no PCI function behind them:
+  // fall back to function 0 of the same bus/device
+  std::string p = pci_root + "/" + bdf;
+  if (!read_first_line(p + "/vendor").empty() || bdf.size() < 2) return p;
+  return pci_root + "/" + bdf.substr(0, bdf.size() - 1) + "0";
+}
+
+// Local cpulist + PCIe link ratio per device, NUMA SLIT distances per node.
+void read_host_affinity(Result& r, const std::string& pci_root, const std::string& node_root) {
+  for (auto& d : r.devs) {
+    if (d.bdf.empty() || pci_root.empty()) continue;
+    const std::string dir = pci_dir(pci_root, d.bdf);
+    d.cpulist = read_first_line(dir + "/local_cpulist");
+    double cs = link_speed_gts(read_first_line(dir + "/current_link_speed"));
+    double ms = link_speed_gts(read_first_line(dir + "/max_link_speed"));
+    double cw = link_speed_gts(read_first_line(dir + "/current_link_width"));
+    double mw = link_speed_gts(read_first_line(dir + "/max_link_width"));
+    if (cs > 0 && ms > 0 && cw > 0 && mw > 0) d.pcie_link_ratio = std::min(1.0, (cs * cw) / (ms * mw));
+  }
+  if (node_root.empty()) return;
+  for (const auto& e : list_dir(node_root)) {
+    if (e.rfind("node", 0) != 0 || e.size() < 5 || !std::all_of(e.begin() + 4, e.end(), ::isdigit)) continue;
+    std::istringstream ss(read_first_line(node_root + "/" + e + "/distance"));
+    std::vector<int> dist;
+    int v;
+    while (ss >> v) dist.push_back(v);
+    if (!dist.empty()) r.numa_distance[std::stoi(e.substr(4))] = dist;
+  }
+}
+
 struct KfdLink {
   int from, to, type;
   double weight, min_bw, max_bw;
@@ -559,26 +610,30 @@ PYBIND11_MODULE(_topo, m) {
   m.doc() = "MI355X topology discovery: amdsmi (dlopen) and KFD sysfs backends";
   m.def(
       "discover_amdsmi",
-      [](const std::string& lib) {
+      [](const std::string& lib, const std::string& pci_root, const std::string& node_root) {
         Result r;
         {
           py::gil_scoped_release nogil;
           r = discover_amdsmi_impl(lib);
+          read_host_affinity(r, pci_root, node_root);
         }
         return to_py(r);
       },
-      py::arg("lib") = "libamd_smi.so");
+      py::arg("lib") = "libamd_smi.so", py::arg("pci_root") = "/sys/bus/pci/devices",
+      py::arg("node_root") = "/sys/devices/system/node");
   m.def(
       "discover_sysfs",
-      [](const std::string& root, const std::string& drm_root) {
+      [](const std::string& root, const std::string& drm_root, const std::string& pci_root, const std::string& node_root) {
         Result r;
         {
           py::gil_scoped_release nogil;
           r = discover_sysfs_impl(root, drm_root);
+          read_host_affinity(r, pci_root, node_root);
         }
         return to_py(r);
       },
-      py::arg("root") = "/sys/class/kfd/kfd/topology", py::arg("drm_root") = "/sys/class/drm");
+      py::arg("root") = "/sys/class/kfd/kfd/topology", py::arg("drm_root") = "/sys/class/drm",
+      py::arg("pci_root") = "/sys/bus/pci/devices", py::arg("node_root") = "/sys/devices/system/node");
   m.attr("HSA_IOLINK_TYPE_XGMI") = 11;
   m.attr("HSA_IOLINK_TYPE_PCIEXPRESS") = 2;
 }

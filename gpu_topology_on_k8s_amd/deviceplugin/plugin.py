@@ -40,7 +40,7 @@ from ..k8s.objects import annotations as obj_annotations
 from ..k8s.objects import meta, pod_gpu_request, pod_is_terminal, pod_phase
 from ..placement import NoFeasiblePlacement, PlacementPolicy
 from ..placement.core import select_with
-from ..topology.cpus import format_cpulist, parse_cpulist
+from ..topology.cpus import recommended_cpuset
 from ..topology.identity import ENV_BDFS, ENV_GROUP
 from ..topology.model import Topology
 from . import proto as pb
@@ -423,20 +423,15 @@ class DevicePluginServer:
             if self.cfg.device_specs == "stub" and not os.path.exists(hpath):
                 continue  # kind / fake GPUs: never hand containerd a host path the node does not have
             r.devices.add(container_path=cpath, host_path=hpath, permissions="rw")
-        numa: Set[int] = set()
-        cpus: List[str] = []
-        for i in ids:
-            g = self.topology.gpus[i]
-            numa.add(int(g.numa))
-            if g.cpu_affinity:
-                cpus.append(g.cpu_affinity)
+        numa = {int(self.topology.gpus[i].numa) for i in ids}
         r.envs[ENV_GROUP] = format_group(ids)
         # PCI addresses in GROUP order: HIP renumbers the container's devices 0..k-1, so tools inside
         # the pod map GROUP -> HIP ordinal by address (topology/identity.py, `gtk validate`)
         r.envs[ENV_BDFS] = ",".join(self.topology.gpus[i].bdf for i in ids)
         r.envs["GTK_NUMA_NODES"] = ",".join(str(x) for x in sorted(numa))
-        if cpus:
-            r.envs["GTK_CPUSET"] = format_cpulist(parse_cpulist(",".join(cpus)))
+        cpuset = recommended_cpuset(self.topology, ids)  # Gaia B6: the devices' local core slices
+        if cpuset:
+            r.envs["GTK_CPUSET"] = cpuset
         for k, v in extra_env.items():
             r.envs[k] = v
         r.annotations["gputopology.amd.com/devices"] = format_group(ids)

@@ -16,6 +16,7 @@ their device ids are unknown, so only feasibility is reduced.
 from __future__ import annotations
 
 import logging
+import math
 import threading
 import time
 from dataclasses import dataclass, field
@@ -53,6 +54,7 @@ class NodeState:
     unknown_pods: Dict[str, int] = field(default_factory=dict)  # pod -> devices held without a GROUP annotation
     capacity: int = -1  # node.status.allocatable[resource] (-1 = unknown)
     synced_at: float = 0.0
+    list_epoch: int = -1  # epoch of the newest pod LIST applied (older LISTs arriving late are stale)
     lock: threading.RLock = field(default_factory=threading.RLock, repr=False)
 
     @property
@@ -65,16 +67,6 @@ class NodeState:
         for a in self.allocs.values():
             if a.assigned or (now - a.assume_time) <= ttl:
                 out.update(a.ids)
-        return out
-
-    def claimed_cpus(self, now: float, ttl: float) -> Set[int]:
-        """Cores recommended to the live pods of this node (their cpuset annotations)."""
-        from ..topology.cpus import parse_cpulist
-
-        out: Set[int] = set()
-        for a in self.allocs.values():
-            if a.cpuset and (a.assigned or (now - a.assume_time) <= ttl):
-                out |= parse_cpulist(a.cpuset)
         return out
 
     def free_count(self, now: float, ttl: float) -> int:
@@ -158,7 +150,13 @@ class ClusterCache:
             return self._epoch
 
     def _rebuild(self, st: NodeState, pods: List[dict], list_epoch: int) -> None:
-        """``list_epoch``: value of the epoch counter taken just before the pods were listed."""
+        """``list_epoch``: value of the epoch counter taken just before the pods were listed.  Called
+        with ``st.lock`` held.  A LIST older than the one already applied is dropped: concurrent
+        refreshes can finish out of order, and the older one may predate a bind the newer one
+        already made authoritative (its overlay entry is gone)."""
+        if list_epoch < st.list_epoch:
+            return
+        st.list_epoch = list_epoch
         allocs: Dict[str, Alloc] = {}
         unknown: Dict[str, int] = {}
         seen = set()
@@ -174,9 +172,13 @@ class ClusterCache:
             ov = self._overlay.get(st.name, {})
             for key in list(ov):
                 a = ov[key]
+                after_bind = list_epoch > self._overlay_epoch.get((st.name, key), 0)
                 if key in seen:
-                    del ov[key]  # the apiserver view has the pod: it is authoritative from now on
-                elif list_epoch > self._overlay_epoch.get((st.name, key), 0) and self.consistent_lists:
+                    if after_bind:  # a LIST started after the bind: authoritative from now on
+                        del ov[key]
+                    # else: this LIST shows the pod, but a LIST started before the bind may still be
+                    # applied after it; keep the entry so such a stale view cannot drop the devices
+                elif after_bind and self.consistent_lists:
                     del ov[key]  # listed (quorum read) after the bind and absent: the pod is gone
                 elif now - a.assume_time > min(self.ttl, self.overlay_grace):
                     del ov[key]  # cached/lagging lists: give up after the grace period
@@ -290,10 +292,20 @@ class ClusterCache:
                   source="overlay", cpuset=cpuset)
         with self._lock:
             self._overlay.setdefault(node, {})[pod] = a
-            self._overlay_epoch[(node, pod)] = self._next_epoch()
+            # pending until :meth:`bound`: a LIST taken while the pod is still unbound does not show
+            # it on the node and must not drop the assumption (the refresh before a concurrent bind
+            # on the same node runs outside the node lock)
+            self._overlay_epoch[(node, pod)] = math.inf
         st = self._state(node)
         with st.lock:
             st.allocs[pod] = a
+
+    def bound(self, node: str, pod: str) -> None:
+        """The binding of an assumed pod was accepted: a LIST started after this point must show the
+        pod on the node, so one that does not proves the pod is gone."""
+        with self._lock:
+            if (node, pod) in self._overlay_epoch:
+                self._overlay_epoch[(node, pod)] = self._next_epoch()
 
     def forget(self, node: str, pod: str) -> None:
         with self._lock:
@@ -353,7 +365,8 @@ class ClusterCache:
                     "used": sorted(st.used(now, self.ttl)),
                     "unknown": st.unknown,
                     "free": st.free_count(now, self.ttl),
-                    "allocs": {k: {"ids": list(a.ids), "assigned": a.assigned, "assume_time": a.assume_time, "source": a.source}
+                    "allocs": {k: {"ids": list(a.ids), "assigned": a.assigned, "assume_time": a.assume_time, "source": a.source,
+                                   "cpuset": a.cpuset}
                                for k, a in st.allocs.items()},
                     "labels": st.labels,
                 }

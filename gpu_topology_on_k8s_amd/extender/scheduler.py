@@ -15,9 +15,9 @@ This implementation adds:
   * node scores normalised over the candidate set: the best feasible node gets 10 and every other
     loses one point per ``score_resolution`` of relative objective gap, so a measured degraded link
     (a fraction of a percent of an 8-GPU set's mean cost) still decides between nodes;
-  * CPU affinity (``design.md:135-147`` tie-break, Gaia B6): the devices' local cores already
-    recommended to other pods raise their access cost, and bind writes the chosen devices' local
-    cores (``<prefix>/cpuset``) and NUMA nodes on the pod;
+  * CPU affinity (``design.md:135-147`` tie-break, Gaia B6): a degraded PCIe host link, a slow HBM
+    stack and the SLIT distance from the pod's preferred NUMA node raise a device's access cost, and
+    bind writes the chosen devices' core slices (``<prefix>/cpuset``) and NUMA nodes on the pod;
   * fractional requests (Gaia Fragment, Alg. 2) as XCP partitions of ONE physical GPU on
     CPX/DPX/QPX nodes, selected by the ``<prefix>/gpu-fraction`` pod annotation;
   * per-node locking + an assume overlay so concurrent binds never overlap (BASELINE config 4);
@@ -140,6 +140,16 @@ class TopologyExtender:
             raise ValueError(f"{self.cfg.contract.fraction_key} must be in (0, 1), got {raw!r}")
         return m
 
+    def numa_preference(self, pod: Dict[str, Any]) -> Optional[List[int]]:
+        """NUMA node(s) the pod's host threads run on (``<prefix>/numa-preference: "1"``), if stated."""
+        raw = obj_annotations(pod).get(self.cfg.contract.numa_pref_key)
+        if not raw:
+            return None
+        try:
+            return [int(x) for x in str(raw).split(",") if x.strip()]
+        except ValueError:
+            return None
+
     def _model_ok(self, pod: Dict[str, Any], st: NodeState) -> Tuple[bool, str]:
         """Heterogeneous-cluster quota (Gaia B7): a pod never receives a mix of GPU models, and a
         pod asking for a model (annotation or label) only lands on nodes advertising it."""
@@ -238,7 +248,7 @@ class TopologyExtender:
             free = st.free_count(now, self.cfg.assume_ttl)
             if free < k:
                 return None, f"insufficient free devices: need {k}, free {free}"
-            access = access_costs(t, st.claimed_cpus(now, self.cfg.assume_ttl)) if self.cfg.cpu_affinity else None
+            access = access_costs(t, self.numa_preference(pod)) if self.cfg.cpu_affinity else None
             t0 = time.perf_counter()
             try:
                 ids, score, obj = self._choose_cached(t, used, k, access, fraction)
@@ -335,6 +345,7 @@ class TopologyExtender:
                 try:
                     self._patch_with_retry(namespace, name, ann)
                     self.api.bind_pod(namespace, name, uid, node)
+                    self.cache.bound(node, key)
                 except Exception:
                     self.cache.forget(node, key)
                     try:  # roll back the annotation so a retry starts clean

@@ -29,7 +29,7 @@ from ..topology.model import LinkType, RefLinkClass, Topology
 __all__ = [
     "ANN_GROUP", "ANN_ASSIGNED", "ANN_ASSUME_TIME", "ANN_GPU_ID_ALIAS", "Contract", "PodAssignment",
     "encode_node_annotations", "decode_node_annotations", "pair_annotations", "parse_pair_annotations",
-    "parse_group", "format_group",
+    "parse_group", "format_group", "package_pair_annotations", "annotations_size",
 ]
 
 ANN_GROUP = "ALIYUN_COM_GPU_GROUP"
@@ -68,6 +68,11 @@ class Contract:
     def cpuset_key(self) -> str:
         """Pod annotation: recommended cpuset = the assigned devices' local cores (Gaia B6 CPU binding)."""
         return f"{self.prefix}/cpuset"
+
+    @property
+    def numa_pref_key(self) -> str:
+        """Pod annotation: NUMA node(s) the pod's host threads live on (CPU-affinity tie-break input)."""
+        return f"{self.prefix}/numa-preference"
 
     @property
     def fraction_key(self) -> str:
@@ -130,14 +135,39 @@ def parse_pair_annotations(ann: Mapping[str, str]) -> Dict[Tuple[int, int], str]
     return out
 
 
+def package_pair_annotations(t: Topology) -> Dict[str, str]:
+    """Partitioned (CPX/DPX/QPX) nodes: one ``GPUPKG_<ABBR>_<p>_<q>`` key per pair of *physical*
+    GPUs instead of one ``GPU_<ABBR>_<i>_<j>`` per XCP pair (64 XCPs = 2016 keys, ~50 KB of the
+    apiserver's 256 KiB per-object annotation budget).  The different prefix keeps readers of the
+    reference contract from taking package ids for device ids."""
+    first: Dict[int, int] = {}
+    for g in t.gpus:
+        first.setdefault(g.physical, g.index)
+    pk = sorted(first)
+    out: Dict[str, str] = {}
+    for a in range(len(pk)):
+        for b in range(a + 1, len(pk)):
+            abbr, desc = _pair_abbr_desc(t, first[pk[a]], first[pk[b]])
+            out[f"GPUPKG_{abbr}_{pk[a]}_{pk[b]}"] = desc
+    return out
+
+
 def encode_node_annotations(t: Topology, contract: Contract = Contract(), with_pairs: bool = True) -> Dict[str, str]:
-    ann = {contract.topology_key: t.to_json()}
+    """Node annotations: the compact v2 model (topology/codec.py) + the reference's pair keys
+    (per device on whole-GPU nodes, per physical GPU on partitioned nodes)."""
+    ann = {contract.topology_key: t.to_wire()}
     ts = t.probe.get("ts") if t.probe else None
     if ts:
         ann[contract.probe_time_key] = str(int(ts))
     if with_pairs:
-        ann.update(pair_annotations(t))
+        partitioned = len({g.physical for g in t.gpus}) < t.n
+        ann.update(package_pair_annotations(t) if partitioned else pair_annotations(t))
     return ann
+
+
+def annotations_size(ann: Mapping[str, str]) -> int:
+    """Bytes the apiserver counts against its 256 KiB per-object annotation limit (keys + values)."""
+    return sum(len(k.encode()) + len(v.encode()) for k, v in ann.items())
 
 
 def topology_from_pairs(pairs: Dict[Tuple[int, int], str], n: Optional[int] = None) -> Topology:

@@ -1,39 +1,45 @@
 """CPU lists (Linux ``cpulist`` format, e.g. ``0-47,96-143``) and the GPU<->CPU affinity terms.
 
 Reference: ``design.md:135-147`` breaks a 1-GPU tie by CPU affinity, and Gaia binds each GPU to its
-nearest CPU cores (paper p.3 §III.A, ``gaia_gpu_topology_scheduler.md:44-46``).  On an MI355X node
-each OAM hangs off one socket: ``/sys/bus/pci/devices/<bdf>/local_cpulist`` names the cores that
-reach it without crossing the socket interconnect (read by ``csrc/topo/topo_reader.cpp`` into
-``GPUInfo.cpu_affinity``).  Two placement inputs come from it:
+nearest CPU cores (paper p.3 §III.A "GPU and CPU core are automatically bound",
+``gaia_gpu_topology_scheduler.md:44-46``).  On an MI355X node each OAM hangs off one socket.
+Discovery (``csrc/topo/topo_reader.cpp``) reads, per device, ``/sys/bus/pci/devices/<bdf>/
+local_cpulist`` (``GPUInfo.cpu_affinity``) and the trained PCIe link against its capability
+(``GPUInfo.pcie_link_ratio``), and per node the NUMA SLIT distances (``Topology.numa_distance``).
 
-* :func:`access_costs` — the per-device ``access`` term of the placement objective: how crowded the
-  device's local cores already are (cores recommended to pods bound on the node, from their
-  ``<prefix>/cpuset`` annotations), plus a slow-HBM penalty from the k=1 self-copy probe.  A 1-GPU
-  request whose candidates tie on links and packing therefore goes to the GPU whose socket has the
-  most spare cores.
-* :func:`recommended_cpuset` — the cpuset written on the pod at bind (Gaia B6 "GPU and CPU core are
-  automatically bound"): the union of the chosen devices' local cores, for the kubelet CPU manager
-  or the workload's own pinning (``GTK_CPUSET`` in the container).
+* :func:`access_costs` — the per-device ``access`` term of the placement objective for one pod:
+  a degraded host link (PCIe trained below x16 / its generation) and a slow HBM stack (k=1 self-copy
+  probe) cost extra, and a pod that names the NUMA node its host threads live on
+  (``<prefix>/numa-preference``) pays the SLIT distance to each device's socket.  Devices tied on
+  links and packing (the ``design.md:135-147`` case) are then ordered by CPU affinity.
+* :func:`device_core_slices` / :func:`recommended_cpuset` — Gaia B6 binding: the local cores of a
+  socket are split evenly among the devices attached to it (SMT siblings stay together: every range
+  of the cpulist is cut at the same fractions), and a pod is recommended the union of its devices'
+  slices (``<prefix>/cpuset`` on the pod, ``GTK_CPUSET`` in the container).
 """
 from __future__ import annotations
 
-from typing import Iterable, List, Optional, Sequence, Set
+from typing import Dict, Iterable, List, Optional, Sequence, Set, Tuple
 
 import numpy as np
 
-__all__ = ["parse_cpulist", "format_cpulist", "recommended_cpuset", "access_costs"]
+__all__ = ["parse_cpulist", "format_cpulist", "device_core_slices", "recommended_cpuset", "access_costs"]
+
+
+def _ranges(s: str) -> List[Tuple[int, int]]:
+    out = []
+    for part in (s or "").replace(" ", "").split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.append((int(a), int(b or a)))
+    return out
 
 
 def parse_cpulist(s: str) -> Set[int]:
     out: Set[int] = set()
-    for part in (s or "").replace(" ", "").split(","):
-        if not part:
-            continue
-        if "-" in part:
-            a, b = part.split("-", 1)
-            out.update(range(int(a), int(b) + 1))
-        else:
-            out.add(int(part))
+    for a, b in _ranges(s):
+        out.update(range(a, b + 1))
     return out
 
 
@@ -53,33 +59,69 @@ def format_cpulist(cpus: Iterable[int]) -> str:
     return ",".join(runs)
 
 
+def device_core_slices(topo) -> Dict[int, Set[int]]:
+    """Disjoint core slice per device: devices sharing a ``local_cpulist`` split each of its ranges
+    into equal consecutive chunks in device order (chunk sizes differ by at most one core)."""
+    groups: Dict[str, List[int]] = {}
+    for g in topo.gpus:
+        if g.cpu_affinity:
+            groups.setdefault(g.cpu_affinity, []).append(g.index)
+    out: Dict[int, Set[int]] = {g.index: set() for g in topo.gpus}
+    for cpulist, devs in groups.items():
+        m = len(devs)
+        for a, b in _ranges(cpulist):
+            n = b - a + 1
+            for j, d in enumerate(devs):
+                lo, hi = a + (n * j) // m, a + (n * (j + 1)) // m
+                out[d].update(range(lo, hi))
+    return out
+
+
 def recommended_cpuset(topo, ids: Sequence[int]) -> str:
-    """Union of the local cores of ``ids`` ('' when discovery could not read them)."""
+    """Union of the core slices of ``ids`` ('' when discovery could not read the cpulists)."""
+    sl = device_core_slices(topo)
     cpus: Set[int] = set()
     for i in ids:
-        cpus |= parse_cpulist(topo.gpus[int(i)].cpu_affinity)
+        cpus |= sl.get(int(i), set())
     return format_cpulist(cpus)
 
 
-def access_costs(topo, claimed_cpus: Optional[Iterable[int]] = None) -> Optional[np.ndarray]:
-    """Per-device access cost in [0, ~2]: ``claimed`` = fraction of the device's local cores already
-    recommended to other pods, ``hbm`` = relative HBM self-copy shortfall against the node median
-    (a degraded stack).  None when neither signal exists (the objective's access term is then 0)."""
+def access_costs(topo, prefer_numa: Optional[Sequence[int]] = None) -> Optional[np.ndarray]:
+    """Per-device access cost (0 = ideal) or None when no signal exists (the term is then 0).
+
+    ``pcie``   1 - trained/capable PCIe (speed x width): 0.5 for a Gen5 link trained at x8;
+    ``hbm``    relative HBM self-copy shortfall against the node median (k=1 probe);
+    ``numa``   2 x (SLIT distance from the preferred NUMA node(s) - 10) / 10: 0 local, 4.4 remote on
+               a 2-socket EPYC (SLIT 32), so with the default weights a stated preference outweighs
+               anti-fragmentation packing (``w_frag``); without SLIT data a remote socket costs 2.
+    """
     n = topo.n
     cost = np.zeros(n)
     have = False
-    claimed = set(int(c) for c in (claimed_cpus or ()))
     for g in topo.gpus:
-        local = parse_cpulist(g.cpu_affinity)
-        if local:
+        r = float(getattr(g, "pcie_link_ratio", -1.0))
+        if 0.0 < r <= 1.0:
             have = True
-            cost[g.index] += len(local & claimed) / len(local)
+            cost[g.index] += 1.0 - r
     hbm = getattr(topo, "hbm_gbps", None)
     if hbm is not None:
         h = np.asarray(hbm, dtype=np.float64)
         ok = np.isfinite(h) & (h > 0)
         if ok.sum() >= 2:
-            med = float(np.median(h[ok]))
             have = True
+            med = float(np.median(h[ok]))
             cost[ok] += np.maximum(0.0, med / h[ok] - 1.0)
+    if prefer_numa:
+        have = True
+        slit = getattr(topo, "numa_distance", None) or {}
+        for g in topo.gpus:
+            best = None
+            for p in prefer_numa:
+                row = slit.get(int(p)) if isinstance(slit, dict) else None
+                if row is not None and 0 <= g.numa < len(row):
+                    d = 2.0 * (row[g.numa] - 10) / 10.0
+                else:
+                    d = 0.0 if g.numa == int(p) else 2.0
+                best = d if best is None else min(best, d)
+            cost[g.index] += max(0.0, best or 0.0)
     return cost if have else None

@@ -51,6 +51,8 @@ def from_native(d: Dict[str, object], node_name: str = "", ref_gbps: float = DEF
                 ecc_deferred=int(g.get("ecc_deferred", -1)),
                 bad_pages=int(g.get("bad_pages", -1)),
                 bad_page_threshold=int(g.get("bad_page_threshold", -1)),
+                cpu_affinity=str(g.get("cpu_affinity") or ""),
+                pcie_link_ratio=float(g.get("pcie_link_ratio", -1.0)),
             )
         )
     lt = np.array(d["link_type"], dtype=np.int32)
@@ -59,6 +61,9 @@ def from_native(d: Dict[str, object], node_name: str = "", ref_gbps: float = DEF
     hops = np.maximum(hops, hops.T)
     weight = np.array(d.get("weight") or np.zeros_like(lt), dtype=np.float64)
     t = Topology(gpus=gpus, link_type=lt, hops=hops, weight=weight, node_name=node_name, source=str(d.get("source", "native")), ref_gbps=ref_gbps)
+    nd = d.get("numa_distance") or {}
+    if nd:
+        t.numa_distance = {int(k): [int(x) for x in v] for k, v in nd.items()}
     mx = d.get("max_bw_mbps")
     if mx is not None:
         t.probe.setdefault("amdsmi_max_bw_mbps", mx)
@@ -81,6 +86,8 @@ def discover(
     amdsmi_lib: str = "libamd_smi.so",
     ref_gbps: float = DEFAULT_REF_GBPS,
     fake_n: Optional[int] = None,
+    pci_root: str = "/sys/bus/pci/devices",
+    node_root: str = "/sys/devices/system/node",
 ) -> Topology:
     """Discover the node topology.  ``auto`` = amdsmi, then KFD sysfs; never silently fake."""
     node_name = node_name or os.environ.get("NODE_NAME", "") or os.uname().nodename
@@ -92,9 +99,9 @@ def discover(
         try:
             topo_mod = load("_topo")
             if b == "amdsmi":
-                d = topo_mod.discover_amdsmi(amdsmi_lib)
+                d = topo_mod.discover_amdsmi(amdsmi_lib, pci_root, node_root)
             elif b == "sysfs":
-                d = topo_mod.discover_sysfs(sysfs_root, drm_root)
+                d = topo_mod.discover_sysfs(sysfs_root, drm_root, pci_root, node_root)
             else:
                 raise DiscoveryError(f"unknown backend {b!r}")
             if not d["gpus"]:

@@ -124,10 +124,12 @@ def write_fake_kfd_sysfs(
     missing_links: Sequence[tuple] = (),
     compute_partition: Optional[str] = None,
     ras: Optional[Dict[int, Dict[str, object]]] = None,
+    degraded_pcie: Sequence[int] = (),
 ) -> Dict[str, str]:
     """Write a KFD topology tree + DRM tree for an MI355X node under ``root``.
 
-    Returns ``{"kfd": <topology root>, "drm": <drm root>}``.  KFD node ids: CPUs first
+    Returns ``{"kfd": <topology root>, "drm": <drm root>, "pci": <PCI devices root>, "node": <NUMA root>}``
+    (PCI: ``local_cpulist`` and PCIe link files of each package's function 0; NUMA: SLIT rows).  KFD node ids: CPUs first
     (0..sockets-1) then one node per schedulable GPU/XCP, as the amdgpu driver enumerates them.
     ``missing_links`` drops direct xGMI io_links between GPU indices (a degraded node).
     ``ras`` writes amdgpu RAS files for device index ``d``: ``{"umc": (ue, ce), "gfx": (ue, ce),
@@ -135,6 +137,14 @@ def write_fake_kfd_sysfs(
     """
     kfd = os.path.join(root, "kfd", "topology")
     drm = os.path.join(root, "drm")
+    pci = os.path.join(root, "pci")
+    numa_root = os.path.join(root, "node")
+    cores = 48
+    for c in range(sockets):
+        nd = os.path.join(numa_root, f"node{c}")
+        os.makedirs(nd, exist_ok=True)
+        with open(os.path.join(nd, "distance"), "w") as f:
+            f.write(" ".join("10" if c == o else "32" for o in range(sockets)) + "\n")
     nodes = os.path.join(kfd, "nodes")
     per_sock = max(1, n_gpus // sockets)
     total = n_gpus * partitions_per_gpu
@@ -180,6 +190,15 @@ def write_fake_kfd_sysfs(
                 {"type": typ, "node_from": nid, "node_to": to, "weight": w, "min_bandwidth": 0,
                  "max_bandwidth": 76800 if typ == _KFD_IOLINK_XGMI else 64000},
             )
+        if xcp == 0:
+            pdir = os.path.join(pci, f"0000:{bus:02x}:00.0")
+            os.makedirs(pdir, exist_ok=True)
+            a, tot = sock * cores, sockets * cores
+            for name, val in (("vendor", "0x1002"), ("local_cpulist", f"{a}-{a + cores - 1},{a + tot}-{a + tot + cores - 1}"),
+                              ("current_link_speed", "32.0 GT/s PCIe"), ("max_link_speed", "32.0 GT/s PCIe"),
+                              ("current_link_width", str(8 if phys in degraded_pcie else 16)), ("max_link_width", "16")):
+                with open(os.path.join(pdir, name), "w") as f:
+                    f.write(val + "\n")
         dev = os.path.join(drm, f"renderD{128 + d}", "device")
         os.makedirs(os.path.join(dev, "drm", f"card{d}"), exist_ok=True)
         with open(os.path.join(dev, "current_compute_partition"), "w") as f:
@@ -195,7 +214,7 @@ def write_fake_kfd_sysfs(
                 ue, ce = val
                 with open(os.path.join(dev, "ras", f"{key}_err_count"), "w") as f:
                     f.write(f"ue: {ue}\nce: {ce}\n")
-    return {"kfd": kfd, "drm": drm}
+    return {"kfd": kfd, "drm": drm, "pci": pci, "node": numa_root}
 
 
 def cost_matrix_stats(t: Topology) -> Dict[str, float]:

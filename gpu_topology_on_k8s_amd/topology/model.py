@@ -190,7 +190,8 @@ class GPUInfo:
     vram_bytes: int = 0
     healthy: bool = True
     xgmi_links_up: int = -1
-    cpu_affinity: str = ""  # cpulist string, e.g. "0-63"
+    cpu_affinity: str = ""  # local_cpulist of the device's PCI function, e.g. "0-47,96-143"
+    pcie_link_ratio: float = -1.0  # trained / capable PCIe (speed x width); -1 = unknown
     # RAS signals read by discovery (amdsmi / amdgpu sysfs); -1 = not readable on this node
     xgmi_links_total: int = -1
     ecc_correctable: int = -1
@@ -207,6 +208,19 @@ class GPUInfo:
     def device_id(self) -> str:
         """Device-plugin ``Device.ID``; stable across restarts (the index, as the reference uses)."""
         return str(self.index)
+
+
+def _numa_distance(raw) -> Optional[Dict[int, List[int]]]:
+    if not raw:
+        return None
+    return {int(k): [int(x) for x in v] for k, v in raw.items()}
+
+
+def _quantize_bw(bw: np.ndarray) -> np.ndarray:
+    """Measured GB/s on the f16 grid the node annotation carries (topology/codec.py): 0.05 %
+    resolution, far below probe noise, and the plugin and the extender then derive identical costs."""
+    with np.errstate(over="ignore"):
+        return bw.astype(np.float16).astype(np.float64)
 
 
 def _as_matrix(x, n: int, dtype, fill) -> np.ndarray:
@@ -240,6 +254,7 @@ class Topology:
     probe: Dict[str, object] = field(default_factory=dict)
     ref_class: Optional[np.ndarray] = None  # optional RefLinkClass matrix (reference fixtures)
     hbm_gbps: Optional[np.ndarray] = None  # per-device self-copy bandwidth (k=1 probe)
+    numa_distance: Optional[Dict[int, List[int]]] = None  # NUMA node -> SLIT distances (sysfs)
 
     def __post_init__(self) -> None:
         n = len(self.gpus)
@@ -247,7 +262,7 @@ class Topology:
         self.hops = _as_matrix(self.hops, n, np.int32, 1)
         if self.weight is not None:
             self.weight = _as_matrix(self.weight, n, np.float64, 0.0)
-        self.bw_gbps = _as_matrix(self.bw_gbps, n, np.float64, np.nan)
+        self.bw_gbps = _quantize_bw(_as_matrix(self.bw_gbps, n, np.float64, np.nan))
         if self.ref_class is not None:
             self.ref_class = _as_matrix(self.ref_class, n, np.int32, 0)
         for i in range(n):
@@ -317,7 +332,7 @@ class Topology:
         return c
 
     def set_measured_bw(self, bw: np.ndarray, probe_meta: Optional[Dict[str, object]] = None) -> None:
-        self.bw_gbps = _as_matrix(bw, self.n, np.float64, np.nan)
+        self.bw_gbps = _quantize_bw(_as_matrix(bw, self.n, np.float64, np.nan))
         if probe_meta:
             self.probe = dict(probe_meta)
         self.recompute_cost()
@@ -371,13 +386,25 @@ class Topology:
             d["ref_class"] = self.ref_class.tolist()
         if self.hbm_gbps is not None:
             d["hbm_gbps"] = [None if not np.isfinite(v) else float(v) for v in self.hbm_gbps]
+        if self.numa_distance:
+            d["numa_distance"] = {str(k): list(v) for k, v in self.numa_distance.items()}
         return d
 
     def to_json(self, **kw) -> str:
         return json.dumps(self.to_dict(), separators=(",", ":"), **kw)
 
+    def to_wire(self) -> str:
+        """Compact v2 JSON for the node annotation (:mod:`.codec`)."""
+        from .codec import encode_v2
+
+        return json.dumps(encode_v2(self), separators=(",", ":"))
+
     @classmethod
     def from_dict(cls, d: Dict[str, object]) -> "Topology":
+        if int(d.get("version", 1)) >= 2:
+            from .codec import decode_v2
+
+            return decode_v2(d)
         gpus = [GPUInfo(**g) for g in d["gpus"]]
 
         def m(a):
@@ -399,6 +426,7 @@ class Topology:
             probe=dict(d.get("probe") or {}),
             ref_class=None if d.get("ref_class") is None else np.array(d["ref_class"], dtype=np.int32),
             hbm_gbps=None if hbm is None else np.array([np.nan if v is None else v for v in hbm], dtype=np.float64),
+            numa_distance=_numa_distance(d.get("numa_distance")),
         )
 
     @classmethod
@@ -416,13 +444,22 @@ class Topology:
         seed: int = 0,
         node_name: str = "mi355x-node",
         partitions_per_gpu: int = 1,
+        cores_per_socket: int = 48,
     ) -> "Topology":
         """Synthetic 8x MI355X full xGMI mesh (fixture F7) or its CPX variant (F8).
 
         ``numa_split`` sockets split the GPUs evenly (0-3 / 4-7 on a 2-socket host).  With
         ``partitions_per_gpu > 1`` every physical GPU exposes that many XCP devices; XCPs of the same
-        GPU are joined by INTERNAL links.
+        GPU are joined by INTERNAL links.  Each socket has ``cores_per_socket`` cores with SMT
+        (socket s: ``s*C..(s+1)*C-1`` plus siblings ``+S*C``), SLIT 10 local / 32 remote.
         """
+        sockets = max(1, numa_split)
+        total_cores = sockets * cores_per_socket
+
+        def cpulist(sock: int) -> str:
+            a = sock * cores_per_socket
+            return f"{a}-{a + cores_per_socket - 1},{a + total_cores}-{a + total_cores + cores_per_socket - 1}"
+
         rng = np.random.default_rng(seed)
         total = n * partitions_per_gpu
         per_numa = max(1, n // max(1, numa_split))
@@ -443,6 +480,8 @@ class Topology:
                     partition=part_name,
                     vram_bytes=(288 * 10**9) // partitions_per_gpu,
                     xgmi_links_up=n - 1,
+                    cpu_affinity=cpulist(min(phys // per_numa, max(0, numa_split - 1))) if cores_per_socket else "",
+                    pcie_link_ratio=1.0,
                 )
             )
         lt = np.full((total, total), int(LinkType.XGMI), dtype=np.int32)
@@ -461,7 +500,8 @@ class Topology:
                         continue
                     base = link_gbps * (4.0 if lt[i, j] == int(LinkType.INTERNAL) else 1.0)
                     bw[i, j] = base * (1.0 + noise * rng.uniform(-1, 1))
-        return cls(gpus=gpus, link_type=lt, hops=hops, bw_gbps=bw, node_name=node_name, source="fake")
+        slit = {s: [10 if s == t else 32 for t in range(sockets)] for s in range(sockets)}
+        return cls(gpus=gpus, link_type=lt, hops=hops, bw_gbps=bw, node_name=node_name, source="fake", numa_distance=slit)
 
     @classmethod
     def from_ref_matrix(

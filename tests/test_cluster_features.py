@@ -1,0 +1,419 @@
+"""Round-2 cluster behaviour (VERDICT r1 "next" #3-#10): bounded worst-placement search,
+start-up probe reuse on busy nodes, compact node annotations, CPU affinity, the kind/stub Allocate
+path, normalised node scores, LIST+WATCH informer, plugin metrics/events, Gaia Fragment via XCPs,
+and the cross-node bind deadlock."""
+import itertools
+import math
+import threading
+import time
+
+import numpy as np
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from gpu_topology_on_k8s_amd.deviceplugin import DevicePluginServer, PluginConfig
+from gpu_topology_on_k8s_amd.deviceplugin.plugin import node_is_idle, startup_topology
+from gpu_topology_on_k8s_amd.extender import ExtenderConfig, TopologyExtender
+from gpu_topology_on_k8s_amd.extender.scheduler import normalized_scores
+from gpu_topology_on_k8s_amd.k8s import Contract, FakeAPIServer, PodAssignment, serve_http
+from gpu_topology_on_k8s_amd.k8s.annotations import annotations_size, decode_node_annotations, encode_node_annotations
+from gpu_topology_on_k8s_amd.k8s.api import RestKubeAPI
+from gpu_topology_on_k8s_amd.k8s.informer import Informer
+from gpu_topology_on_k8s_amd.k8s.objects import make_node, make_pod
+from gpu_topology_on_k8s_amd.parallel.allreduce import choose_subset
+from gpu_topology_on_k8s_amd.placement import PlacementPolicy, Problem, evaluate, place_fraction, select, worst
+from gpu_topology_on_k8s_amd.sim import SimCluster
+from gpu_topology_on_k8s_amd.topology import fixtures as fx
+from gpu_topology_on_k8s_amd.topology.cpus import access_costs, device_core_slices, format_cpulist, parse_cpulist, recommended_cpuset
+from gpu_topology_on_k8s_amd.topology.discovery import fake_topology
+from gpu_topology_on_k8s_amd.topology.model import Topology
+
+C = Contract()
+
+
+def _probed(t, base=70.0, degrade=None, noise=0.0, seed=0):
+    rng = np.random.default_rng(seed)
+    n = t.n
+    bw = np.where(t.link_type == 1, 4 * base, base) * (1 + noise * rng.uniform(-1, 1, (n, n)))
+    np.fill_diagonal(bw, np.nan)
+    if degrade:
+        i, j, f = degrade
+        bw[i, j] = bw[j, i] = base * f
+    t.set_measured_bw(bw, {"method": "p2p_read_lds", "preset": "quick", "ts": 1700000000})
+    return t
+
+
+# ---------------------------------------------------------------------------------- #3 worst()
+def test_worst_bounded_on_cpx_and_choose_subset_fast():
+    t = fx.f8_mi355x_cpx()
+    t0 = time.perf_counter()
+    w = worst(t, 8)
+    assert time.perf_counter() - t0 < 0.1 and not w.exact and len(set(w.ids)) == 8
+    assert w.objective > select(t, 8).objective
+    t0 = time.perf_counter()
+    ch = choose_subset(8, topology=t, visible=64)
+    assert time.perf_counter() - t0 < 1.0 and ch.worst is not None and ch.extra["worst_exact"] is False
+
+
+@settings(max_examples=40, deadline=None)
+@given(n=st.integers(2, 9), k=st.integers(1, 5), seed=st.integers(0, 10_000))
+def test_worst_and_select_match_brute_force(n, k, seed):
+    k = min(k, n)
+    rng = np.random.default_rng(seed)
+    t = fake_topology(n)
+    bw = rng.uniform(40, 80, (n, n))
+    bw = (bw + bw.T) / 2
+    np.fill_diagonal(bw, np.nan)
+    t.set_measured_bw(bw)
+    p = Problem.from_topology(t)
+    js = {c: evaluate(p, c)[0] for c in itertools.combinations(range(n), k)}
+    hi, lo = max(js.values()), min(js.values())
+    for eng in ("native", "python"):
+        assert abs(worst(t, k, engine=eng).objective - hi) < 1e-9
+    assert abs(select(t, k).objective - lo) < 1e-9
+
+
+# ---------------------------------------------------------------------------------- #4 start-up probe
+def _busy_node_api(topo, busy=True):
+    api = FakeAPIServer()
+    api.create_node(make_node("n1", annotations=encode_node_annotations(topo, C)))
+    if busy:
+        api.create_pod(make_pod("train", gpus=2, node="n1", annotations=PodAssignment(group=[0, 1], assigned=True, assume_time=1)
+                                .to_annotations()))
+    return api
+
+
+def test_startup_reuses_published_matrix_on_busy_node():
+    published = _probed(fx.f7_mi355x(), degrade=(2, 5, 0.6))
+    api = _busy_node_api(published)
+    calls = []
+    fresh = fx.f7_mi355x()
+    topo, how = startup_topology(fresh, api, "n1", C, ("amd.com/gpu",), lambda: calls.append(1))
+    assert calls == [] and "reused" in how
+    assert topo.bw_gbps[2, 5] == pytest.approx(42.0) and topo.probe["reused"] is True
+    # republished by the plugin as it was measured
+    plug = DevicePluginServer(topo, PluginConfig(node_name="n1"), api=api)
+    plug._publish_node()
+    again = decode_node_annotations(api.get_node("n1")["metadata"]["annotations"], C)
+    assert np.array_equal(np.nan_to_num(again.bw_gbps), np.nan_to_num(published.bw_gbps))
+
+
+def test_startup_probes_idle_node_and_counts_unannotated_holders():
+    api = _busy_node_api(fx.f7_mi355x(), busy=False)
+    probed = _probed(fx.f7_mi355x())
+    topo, how = startup_topology(fx.f7_mi355x(), api, "n1", C, ("amd.com/gpu",), lambda: probed)
+    assert how == "probed" and topo is probed
+    api.create_pod(make_pod("around", gpus=1, node="n1"))  # no GROUP, still holds a device
+    assert not node_is_idle(api, "n1", ("amd.com/gpu",))
+
+
+# ---------------------------------------------------------------------------------- #5 annotation size
+def test_cpx_node_annotations_fit_and_decode_to_same_placements():
+    t = _probed(fx.f8_mi355x_cpx(), noise=0.05, seed=3)
+    n = t.n
+    rng = np.random.default_rng(1)
+    t.weight = np.where(t.link_type == 1, 10, 15).astype(float)
+    np.fill_diagonal(t.weight, 0)
+    t.probe["amdsmi_max_bw_mbps"] = np.where(t.link_type == 1, 0, 64000).tolist()
+    t.probe["ingress_all_gbps"] = [round(float(x), 2) for x in rng.uniform(400, 500, n)]
+    t.hbm_gbps = rng.uniform(3000, 3300, n)
+    for g in t.gpus:
+        g.uuid = f"{int(rng.integers(1 << 62)):016x}-{g.index}"
+    ann = encode_node_annotations(t, C)
+    assert annotations_size(ann) < 64 * 1024
+    assert not any(k.startswith("GPU_") for k in ann)  # per-package keys on a partitioned node
+    assert sum(k.startswith("GPUPKG_") for k in ann) == 28
+    u = decode_node_annotations(ann, C)
+    assert np.array_equal(u.cost, t.cost) and np.array_equal(u.weight, t.weight)
+    assert u.probe["amdsmi_max_bw_mbps"] == t.probe["amdsmi_max_bw_mbps"]
+    for k in (1, 2, 4, 8, 12):
+        assert select(u, k, used=[0, 9]).ids == select(t, k, used=[0, 9]).ids
+
+
+def test_v1_json_still_decodes():
+    t = fx.f7_mi355x(link_gbps=70.0, noise=0.05)
+    u = decode_node_annotations({C.topology_key: t.to_json()}, C)
+    assert np.array_equal(u.cost, t.cost)
+
+
+# ---------------------------------------------------------------------------------- #6 CPU affinity
+def test_cpulist_roundtrip_and_slices():
+    assert format_cpulist(parse_cpulist("0-3,8,10-11")) == "0-3,8,10-11"
+    t = fx.f7_mi355x()
+    sl = device_core_slices(t)
+    assert format_cpulist(sl[0]) == "0-11,96-107" and format_cpulist(sl[7]) == "84-95,180-191"
+    assert not set().union(*[sl[i] & sl[j] for i in range(8) for j in range(i + 1, 8)])
+    assert recommended_cpuset(t, [0, 1]) == "0-23,96-119"
+
+
+def test_req1_tie_broken_by_cpu_affinity():
+    """design.md:135-147: among equally good single GPUs, the better CPU affinity wins."""
+    t = fx.f7_mi355x()
+    assert select(t, 1).ids == (0,)
+    assert select(t, 1, access=access_costs(t, prefer_numa=[1])).ids == (4,)
+    t.gpus[0].pcie_link_ratio = 0.5  # host link trained at x8
+    assert select(t, 1, access=access_costs(t)).ids == (1,)
+
+
+def test_extender_writes_exact_cpuset_and_honours_numa_preference():
+    api = FakeAPIServer()
+    api.create_node(make_node("n1", labels={C.label_model: "MI355X"}, annotations=encode_node_annotations(fx.f7_mi355x(), C),
+                              capacity={C.resource_name: "8"}))
+    ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+    pod = api.create_pod(make_pod("a", gpus=2))
+    d = ext.bind("default", "a", pod["metadata"]["uid"], "n1")
+    ann = api.get_pod("default", "a")["metadata"]["annotations"]
+    assert d.ids == (0, 1) and ann[C.cpuset_key] == "0-23,96-119" and ann[C.numa_key] == "0"
+    pod = api.create_pod(make_pod("b", gpus=1, annotations={C.numa_pref_key: "1"}))
+    d = ext.bind("default", "b", pod["metadata"]["uid"], "n1")
+    assert d.ids[0] >= 4 and api.get_pod("default", "b")["metadata"]["annotations"][C.cpuset_key] == \
+        format_cpulist(device_core_slices(fx.f7_mi355x())[d.ids[0]])
+
+
+# ---------------------------------------------------------------------------------- #7 kind / stub
+def test_config1_kind_node_two_fake_gpus_stub_allocate():
+    """BASELINE config 1: 2 fake GPUs on a node without ROCm device nodes; a 1-GPU pod is admitted
+    (the fake kubelet rejects any DeviceSpec whose host path is missing, as containerd would)."""
+    with SimCluster({"kind-worker": fake_topology(2, node_name="kind-worker")}, device_specs="stub") as c:
+        c.submit("p", 1)
+        r = c.schedule_pending()[0]
+        assert r.error == "" and r.node == "kind-worker" and len(r.allocated) == 1
+        resp = c.nodes["kind-worker"].kubelet.responses["default/p"]
+        cr = resp.container_responses[0]
+        assert list(cr.devices) == [] and cr.envs["GTK_GPU_GROUP"] == str(r.allocated[0])
+        assert c.assignment("p").assigned
+
+
+def test_strict_specs_refuse_missing_device_nodes(tmp_path):
+    import grpc
+
+    plug = DevicePluginServer(fx.f7_mi355x(n=2), PluginConfig(dev_root=str(tmp_path), node_name="n1"), api=FakeAPIServer())
+    plug.api.create_node(make_node("n1"))
+
+    class Ctx:
+        def abort(self, code, msg):
+            raise RuntimeError((code, msg))
+
+    from gpu_topology_on_k8s_amd.deviceplugin import proto as pb
+
+    req = pb.AllocateRequest()
+    req.container_requests.add(devices_ids=["0"])
+    with pytest.raises(RuntimeError) as ei:
+        plug.Allocate(req, Ctx())
+    assert ei.value.args[0][0] == grpc.StatusCode.FAILED_PRECONDITION and "kfd" in ei.value.args[0][1]
+    assert any(e["reason"] == "FailedGPUAllocate" for e in plug.api.events)
+    assert 'gtk_plugin_allocations_total{outcome="missing"} 1.0' in plug.metrics.exposition().decode()
+
+
+# ---------------------------------------------------------------------------------- #8 node scores
+def test_normalized_scores():
+    s = normalized_scores({"a": 1.0, "b": 1.004, "c": 1.2, "d": 1.0})
+    assert s["a"] == s["d"] == 10 and s["b"] == 9 and s["c"] == 1
+    assert normalized_scores({}) == {}
+
+
+def test_degraded_link_loses_the_8gpu_pod():
+    nodes = {"degraded": _probed(fx.f7_mi355x(), degrade=(2, 6, 0.9)), "pristine": _probed(fx.f7_mi355x())}
+    for name, t in nodes.items():
+        t.node_name = name
+    with SimCluster(nodes) as c:
+        pod = c.submit("big", 8)
+        prio = {h["Host"]: h["Score"] for h in c._post("sort", {"Pod": pod, "NodeNames": ["degraded", "pristine"]})}
+        assert prio["pristine"] > prio["degraded"] >= 1
+        r = c.schedule_pending()[0]
+        assert r.node == "pristine" and len(r.allocated) == 8
+
+
+# ---------------------------------------------------------------------------------- #9 informer
+def _rest_cluster(nodes=64):
+    api = FakeAPIServer()
+    t = fx.f7_mi355x()
+    ann = encode_node_annotations(t, C)
+    for i in range(nodes):
+        api.create_node(make_node(f"n{i}", labels={C.label_model: "MI355X"}, annotations=ann, capacity={C.resource_name: "8"}))
+    srv, url = serve_http(api)
+    return api, srv, RestKubeAPI(url, verify=False)
+
+
+def test_informer_keeps_prioritize_free_of_lists():
+    api, srv, rest = _rest_cluster(64)
+    ext = TopologyExtender(rest, ExtenderConfig(resync_s=0.0))
+    inf = Informer(rest, ext.cache.on_list, ext.cache.on_event, watch_timeout=5.0)
+    ext.cache.attach_informer(inf)
+    inf.start()
+    try:
+        assert inf.wait_synced(20)
+        names = [f"n{i}" for i in range(64)]
+        pod = api.create_pod(make_pod("p", gpus=4))
+        before = dict(api.calls)
+        res = dict(ext.prioritize(pod, names))
+        assert all(v == 10 for v in res.values())
+        assert api.calls.get("list_pods", 0) == before.get("list_pods", 0)
+        assert api.calls.get("list_nodes", 0) == before.get("list_nodes", 0)
+        # a pod bound by someone else arrives through the WATCH stream
+        api.create_pod(make_pod("other", gpus=8, node="n3", annotations=PodAssignment(list(range(8)), True, 1).to_annotations()))
+        deadline = time.time() + 10
+        while time.time() < deadline and dict(ext.prioritize(pod, ["n3"]))["n3"] != 0:
+            time.sleep(0.05)
+        assert dict(ext.prioritize(pod, ["n3"]))["n3"] == 0
+        api.delete_pod("default", "other")
+        deadline = time.time() + 10
+        while time.time() < deadline and dict(ext.prioritize(pod, ["n3"]))["n3"] == 0:
+            time.sleep(0.05)
+        assert dict(ext.prioritize(pod, ["n3"]))["n3"] == 10
+        assert api.calls.get("list_pods", 0) == before.get("list_pods", 0)
+        assert inf.events["Pod"] >= 2
+    finally:
+        inf.stop()
+        srv.shutdown()
+
+
+def test_informer_relists_after_gone():
+    api = FakeAPIServer(history=4)
+    api.create_node(make_node("n0"))
+    seen = {"lists": 0}
+
+    def on_list(kind, items):
+        seen["lists"] += 1
+
+    inf = Informer(api, on_list, lambda *a: None, kinds=("Pod",), watch_timeout=0.2, backoff=0.05)
+    inf.start()
+    try:
+        assert inf.wait_synced(5)
+        for i in range(20):  # overflow the 4-entry window while the watch may lag
+            api.create_pod(make_pod(f"p{i}", gpus=0))
+        time.sleep(0.5)
+        assert inf.lists["Pod"] >= 1 and inf.events["Pod"] + 0 >= 0
+    finally:
+        inf.stop()
+
+
+# ---------------------------------------------------------------------------------- ADVICE: deadlock
+def test_concurrent_binds_across_nodes_do_not_deadlock():
+    api = FakeAPIServer()
+    for n in ("a", "b", "c"):
+        api.create_node(make_node(n, labels={C.label_model: "MI355X"}, annotations=encode_node_annotations(fx.f7_mi355x(), C),
+                                  capacity={C.resource_name: "8"}))
+    ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+    api.latency_s = 0.002  # widen the race window
+    pods = [(f"p{i}", "abc"[i % 3]) for i in range(18)]
+    for name, _ in pods:
+        api.create_pod(make_pod(name, gpus=1))
+    errs = []
+
+    def go(name, node):
+        try:
+            pod = api.get_pod("default", name)
+            ext.bind("default", name, pod["metadata"]["uid"], node)
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+
+    ts = [threading.Thread(target=go, args=p, daemon=True) for p in pods]
+    [t.start() for t in ts]
+    [t.join(30) for t in ts]
+    assert not any(t.is_alive() for t in ts), "binds deadlocked"
+    assert not errs
+    for n in "abc":
+        used = [PodAssignment.from_annotations(p["metadata"]["annotations"]).group[0] for p in api.list_pods(node_name=n)]
+        assert len(used) == 6 and len(set(used)) == 6
+
+
+# ---------------------------------------------------------------------------------- ADVICE: re-probe
+def test_reprobe_discards_measurement_when_a_pod_arrives():
+    api = FakeAPIServer()
+    api.create_node(make_node("n1"))
+
+    def probe():
+        api.create_pod(make_pod("late", gpus=1, node="n1", annotations=PodAssignment([0], False, 1).to_annotations()))
+        return _probed(fx.f7_mi355x(n=4), degrade=(0, 1, 0.3))
+
+    plug = DevicePluginServer(_probed(fx.f7_mi355x(n=4)), PluginConfig(node_name="n1"), api=api, reprobe_fn=probe)
+    assert plug.reprobe() is False and plug.republished == 0
+    assert 'gtk_plugin_reprobes_total{result="discarded"} 1.0' in plug.metrics.exposition().decode()
+
+
+def test_allocate_refused_while_probing(tmp_path):
+    import grpc
+
+    from gpu_topology_on_k8s_amd.deviceplugin import placeholder_dev_tree
+    from gpu_topology_on_k8s_amd.deviceplugin import proto as pb
+
+    t = fx.f7_mi355x(n=2)
+    plug = DevicePluginServer(t, PluginConfig(dev_root=placeholder_dev_tree(str(tmp_path), t)))
+    plug._probing = True
+
+    class Ctx:
+        def abort(self, code, msg):
+            raise RuntimeError(code)
+
+    req = pb.AllocateRequest()
+    req.container_requests.add(devices_ids=["1"])
+    with pytest.raises(RuntimeError) as ei:
+        plug.Allocate(req, Ctx())
+    assert ei.value.args[0] == grpc.StatusCode.UNAVAILABLE
+    plug._probing = False
+    assert len(plug.Allocate(req, Ctx()).container_responses) == 1
+
+
+def test_preferred_allocation_survives_unhealthy_available_device():
+    plug = DevicePluginServer(fx.f7_mi355x(n=4), PluginConfig())
+    plug.set_health(2, False)
+    ids = plug._preferred_fallback(2, [0, 2, 3], [])
+    assert len(ids) == 2 and 2 not in ids
+    ids = plug._preferred_fallback(3, [0, 2, 3], [2])  # impossible healthy answer: degrade, never raise
+    assert sorted(ids) == [0, 2, 3]
+
+
+# ---------------------------------------------------------------------------------- #10 fractions
+def test_place_fraction_best_fit():
+    t = Topology.full_mesh(n=4, numa_split=1, partitions_per_gpu=10)
+    used = list(range(20, 25))  # 0.5 of gpu2 taken
+    assert place_fraction(t, 4, used) == (25, 26, 27, 28)
+    assert place_fraction(t, 1, used + [25, 26, 27, 28]) == (29,)
+    assert place_fraction(t, 6, used) == (0, 1, 2, 3, 4, 5)  # does not fit gpu2: open a pristine package
+
+
+def test_table2_fragment_through_the_cluster():
+    """Gaia Table II on a 4-GPU node exposing 10 XCPs per GPU: after 0.5 of gpu2 is taken, a 0.4-GPU
+    pod and then a 0.1-GPU pod both land on gpu2 (best fit), through /filter, /sort, /bind,
+    GetPreferredAllocation and Allocate."""
+    t = Topology.full_mesh(n=4, numa_split=1, partitions_per_gpu=10, node_name="p4")
+    for rep in range(3):
+        with SimCluster({"p4": t}) as c:
+            c.api.create_pod(make_pod("half", gpus=5, node="p4", annotations=PodAssignment(list(range(20, 25)), True, 1)
+                                      .to_annotations()))
+            c.submit("f04", 4, annotations={C.fraction_key: "0.4"})
+            r = c.schedule_pending()[0]
+            assert r.error == "" and set(r.allocated) <= set(range(20, 30)) and len(r.allocated) == 4
+            c.submit("f01", 1, annotations={C.fraction_key: "0.1"})
+            r = c.schedule_pending()[0]
+            assert r.allocated == (29,)
+            c.submit("bad", 2, annotations={C.fraction_key: "0.4"})  # 0.4 of a 10-XCP GPU is 4 partitions
+            r = c.schedule_pending()[0]
+            assert r.node is None
+
+
+def test_fraction_refused_on_whole_gpu_node():
+    api = FakeAPIServer()
+    api.create_node(make_node("n1", annotations=encode_node_annotations(fx.f7_mi355x(), C), capacity={C.resource_name: "8"}))
+    ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+    pod = api.create_pod(make_pod("f", gpus=1, annotations={C.fraction_key: "0.5"}))
+    ok, failed = ext.filter(pod, ["n1"])
+    assert ok == [] and "partitioned" in failed["n1"]
+
+
+# ---------------------------------------------------------------------------------- metrics
+def test_fragmentation_gauges():
+    api = FakeAPIServer()
+    api.create_node(make_node("n1", labels={C.label_model: "MI355X"}, annotations=encode_node_annotations(fx.f7_mi355x(), C),
+                              capacity={C.resource_name: "8"}))
+    ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+    for name, ids in (("a", [0, 1, 2]), ("b", [4])):
+        api.create_pod(make_pod(name, gpus=len(ids), node="n1", annotations=PodAssignment(ids, True, 1).to_annotations()))
+    ext.cache.sync_all()
+    text = ext.metrics.exposition().decode()
+    # free: {3} on NUMA0, {5,6,7} on NUMA1 -> 1 - 3/4
+    assert 'gtk_extender_node_fragmentation{node="n1"} 0.25' in text
+    assert 'gtk_extender_node_free_devices{node="n1"} 4.0' in text
+    assert 'gtk_extender_placeable_nodes{k="8"} 0.0' in text and 'gtk_extender_placeable_nodes{k="4"} 1.0' in text

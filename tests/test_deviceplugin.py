@@ -222,8 +222,10 @@ def test_reprobe_republishes_only_when_idle_and_changed():
     assert plug.node_idle()
     assert plug.reprobe() is False  # +1.7 %: within tolerance
     assert plug.reprobe() is True  # pair (0,3) at half speed
-    topo = json.loads(api.get_node("n1")["metadata"]["annotations"][Contract().topology_key])
-    assert topo["bw_gbps"][0][3] == 30.0 and plug.republished == 1 and plug.reprobes == 2
+    from gpu_topology_on_k8s_amd.topology.model import Topology
+
+    topo = Topology.from_json(api.get_node("n1")["metadata"]["annotations"][Contract().topology_key])
+    assert topo.bw_gbps[0][3] == 30.0 and plug.republished == 1 and plug.reprobes == 2
     # a pod holding devices makes the node busy: the monitor must not probe
     api.create_pod(make_pod("busy", gpus=2, node="n1", annotations=PodAssignment.assumed((0, 1), 1).to_annotations()))
     assert not plug.node_idle()

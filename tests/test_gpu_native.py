@@ -228,8 +228,10 @@ def test_device_plugin_daemon_probes_in_child_on_real_node():
         plugin = kubelet.wait_for("amd.com/gpu", timeout=120)
         assert len(plugin.devices) >= 1
         ann = api.get_node("gpu-node")["metadata"]["annotations"]
-        topo = json.loads(ann[Contract().topology_key])
-        assert topo["probe"]["method"] == "p2p_read_lds" and topo["hbm_gbps"][0] > 1000
+        from gpu_topology_on_k8s_amd.topology.model import Topology
+
+        topo = Topology.from_json(ann[Contract().topology_key])
+        assert topo.probe["method"] == "p2p_read_lds" and topo.hbm_gbps[0] > 1000
     finally:
         if p.poll() is None:
             p.send_signal(signal.SIGTERM)
