@@ -91,6 +91,20 @@ def cmd_select(a) -> int:
 def cmd_config(a) -> int:
     from .config import legacy_policy, render_manifests, scheduler_configuration
 
+    if a.kind == "kind":
+        from .config import render_kind
+
+        out = render_kind(a.resource_name, image=a.image)
+        if a.out_dir:
+            os.makedirs(a.out_dir, exist_ok=True)
+            for name, text in out.items():
+                with open(os.path.join(a.out_dir, name), "w") as f:
+                    f.write(text)
+                if name.endswith(".sh"):
+                    os.chmod(os.path.join(a.out_dir, name), 0o755)
+        else:
+            print(out["gpu-topology-kind.yaml"], end="")
+        return 0
     if a.kind == "policy":
         print(json.dumps(legacy_policy(a.resource_name, with_filter=a.filter), indent=2))
     elif a.kind == "scheduler":
@@ -191,7 +205,8 @@ def main(argv=None) -> int:
     p.add_argument("--worst", action="store_true")
     p.set_defaults(fn=cmd_select)
     p = sub.add_parser("config")
-    p.add_argument("kind", choices=["scheduler", "policy", "manifests"])
+    p.add_argument("kind", choices=["scheduler", "policy", "manifests", "kind"])
+    p.add_argument("--out-dir", default="", help="kind: write every file of deploy/kind/ here")
     p.add_argument("--resource-name", default="amd.com/gpu")
     p.add_argument("--filter", action="store_true")
     p.add_argument("--image", default="rocm/gpu-topology-k8s:latest")

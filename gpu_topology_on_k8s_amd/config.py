@@ -7,8 +7,10 @@
 * :func:`scheduler_configuration` — the same extender as a ``KubeSchedulerConfiguration``
   (``kubescheduler.config.k8s.io/v1``) ``extenders:`` stanza for current clusters, optionally with
   the ``filter`` verb this framework adds.
-* :func:`render_manifests` — DaemonSet (device plugin), Deployment + Service (extender), RBAC and
-  the scheduler ConfigMap, as one multi-document YAML (``deploy/``).
+* :func:`render_manifests` — DaemonSet (device plugin, Prometheus ``/metrics`` on :32744), Deployment
+  (extender on the control-plane host network, listening on 127.0.0.1 only: kube-scheduler calls it
+  on loopback and ``/bind`` is unauthenticated, so no Service exposes it), RBAC and the scheduler
+  ConfigMap, as one multi-document YAML (``deploy/``).
 """
 from __future__ import annotations
 
@@ -20,9 +22,10 @@ import yaml
 from .extender.server import DEFAULT_PORT, DEFAULT_PREFIX
 from .k8s.annotations import COMPAT_RESOURCE, DEFAULT_RESOURCE
 
-__all__ = ["legacy_policy", "scheduler_configuration", "render_manifests", "extender_url"]
+__all__ = ["legacy_policy", "scheduler_configuration", "render_manifests", "render_kind", "extender_url"]
 
 NAMESPACE = "kube-system"
+PLUGIN_METRICS_PORT = 32744
 IMAGE = "rocm/gpu-topology-k8s:latest"
 
 
@@ -112,7 +115,8 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
                             "image": image,
                             "command": ["python3", "-m", "gpu_topology_on_k8s_amd.deviceplugin",
                                         f"--resource-name={resource}", f"--probe={probe}", "--discovery=auto",
-                                        "--reprobe-interval=3600"],
+                                        "--reprobe-interval=3600", f"--metrics-port={PLUGIN_METRICS_PORT}"],
+                            "ports": [{"containerPort": PLUGIN_METRICS_PORT, "name": "metrics"}],
                             "env": [{"name": "NODE_NAME", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}},
                                     {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}],
                             "securityContext": {"privileged": True},
@@ -150,21 +154,14 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
                             "name": "extender",
                             "image": image,
                             "command": ["python3", "-m", "gpu_topology_on_k8s_amd.extender", f"--resource-name={resource}",
-                                        f"--port={DEFAULT_PORT}", f"--policy={policy}"],
-                            "ports": [{"containerPort": DEFAULT_PORT, "name": "http"}],
-                            "readinessProbe": {"httpGet": {"path": "/healthz", "port": DEFAULT_PORT}},
-                            "livenessProbe": {"httpGet": {"path": "/healthz", "port": DEFAULT_PORT}},
+                                        "--host=127.0.0.1", f"--port={DEFAULT_PORT}", f"--policy={policy}", "--informer=on",
+                                        "--scheduler-names=default-scheduler"],
+                            "readinessProbe": {"httpGet": {"host": "127.0.0.1", "path": "/healthz", "port": DEFAULT_PORT}},
+                            "livenessProbe": {"httpGet": {"host": "127.0.0.1", "path": "/healthz", "port": DEFAULT_PORT}},
                         }],
                     },
                 },
             },
-        },
-        {
-            "apiVersion": "v1",
-            "kind": "Service",
-            "metadata": {"name": "gpu-topology-scheduler-extender", "namespace": namespace, "labels": labels},
-            "spec": {"selector": {"name": "gpu-topology-scheduler-extender"},
-                     "ports": [{"port": DEFAULT_PORT, "targetPort": DEFAULT_PORT, "name": "http"}]},
         },
         {
             "apiVersion": "v1",
@@ -177,3 +174,80 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
         },
     ]
     return yaml.safe_dump_all(docs, sort_keys=False)
+
+
+def render_kind(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, fake_gpus: int = 2) -> Dict[str, str]:
+    """BASELINE config 1 — a kind cluster whose worker advertises ``fake_gpus`` fake CPU-backed GPUs
+    and a pod that requests one.  Files (``deploy/kind/``):
+
+    * ``kind-config.yaml`` — 1 control plane + 1 worker; the scheduler config is mounted into the
+      control-plane node and passed to kube-scheduler (``--config``) through a kubeadm patch;
+    * ``gpu-topology-kind.yaml`` — the manifests of :func:`render_manifests` with the device plugin in
+      fake-discovery / stub-DeviceSpec mode: a kind node has no ``/dev/kfd`` or render nodes, so
+      Allocate returns envs + annotations only and containerd never sees a missing host path;
+    * ``pod-1gpu.yaml`` — the test pod; ``up.sh`` wires it together (needs docker + kind + kubectl).
+    """
+    docs = list(yaml.safe_load_all(render_manifests(resource, image=image, probe="off")))
+    for d in docs:
+        if d["kind"] == "DaemonSet":
+            spec = d["spec"]["template"]["spec"]
+            spec["nodeSelector"] = {"gputopology.amd.com/fake-gpus": "true"}
+            c = spec["containers"][0]
+            c["command"] = ["python3", "-m", "gpu_topology_on_k8s_amd.deviceplugin", f"--resource-name={resource}", "--discovery=fake",
+                            f"--fake-gpus={fake_gpus}", "--probe=off", "--device-specs=stub", f"--metrics-port={PLUGIN_METRICS_PORT}"]
+            c.pop("securityContext", None)
+            c["volumeMounts"] = [m for m in c["volumeMounts"] if m["name"] == "device-plugins"]
+            spec["volumes"] = [v for v in spec["volumes"] if v["name"] == "device-plugins"]
+    kind_cfg = {
+        "kind": "Cluster",
+        "apiVersion": "kind.x-k8s.io/v1alpha4",
+        "nodes": [
+            {
+                "role": "control-plane",
+                "extraMounts": [{"hostPath": "./scheduler-config.yaml", "containerPath": "/etc/kubernetes/gpu-topology/scheduler-config.yaml",
+                                 "readOnly": True}],
+                "kubeadmConfigPatches": [yaml.safe_dump({
+                    "kind": "ClusterConfiguration",
+                    "scheduler": {
+                        "extraArgs": {"config": "/etc/kubernetes/gpu-topology/scheduler-config.yaml"},
+                        "extraVolumes": [{"name": "gpu-topology", "hostPath": "/etc/kubernetes/gpu-topology",
+                                          "mountPath": "/etc/kubernetes/gpu-topology", "readOnly": True, "pathType": "Directory"}],
+                    },
+                }, sort_keys=False)],
+            },
+            {"role": "worker", "labels": {"gputopology.amd.com/fake-gpus": "true"}},
+        ],
+    }
+    pod = {
+        "apiVersion": "v1",
+        "kind": "Pod",
+        "metadata": {"name": "gpu-topology-smoke", "namespace": "default"},
+        "spec": {
+            "restartPolicy": "Never",
+            "containers": [{"name": "c", "image": "busybox:1.36", "command": ["sh", "-c", "env | grep GTK_ && sleep 5"],
+                            "resources": {"limits": {resource: "1"}}}],
+        },
+    }
+    up = "\n".join([
+        "#!/usr/bin/env bash",
+        "# BASELINE config 1: kind + 2 fake GPUs; the pod must reach Succeeded with GTK_GPU_GROUP set.",
+        "set -euo pipefail",
+        'cd "$(dirname "$0")"',
+        "kind create cluster --name gpu-topology --config kind-config.yaml",
+        f"kind load docker-image --name gpu-topology {image}",
+        "kubectl apply -f gpu-topology-kind.yaml",
+        "kubectl -n kube-system rollout status ds/amd-gpu-topology-device-plugin --timeout=180s",
+        "kubectl -n kube-system rollout status deploy/gpu-topology-scheduler-extender --timeout=180s",
+        "kubectl apply -f pod-1gpu.yaml",
+        "kubectl wait --for=jsonpath='{.status.phase}'=Succeeded pod/gpu-topology-smoke --timeout=180s",
+        "kubectl get pod gpu-topology-smoke -o jsonpath='{.metadata.annotations}'; echo",
+        "kubectl logs gpu-topology-smoke",
+        "",
+    ])
+    return {
+        "kind-config.yaml": yaml.safe_dump(kind_cfg, sort_keys=False),
+        "scheduler-config.yaml": yaml.safe_dump(scheduler_configuration(resource), sort_keys=False),
+        "gpu-topology-kind.yaml": yaml.safe_dump_all(docs, sort_keys=False),
+        "pod-1gpu.yaml": yaml.safe_dump(pod, sort_keys=False),
+        "up.sh": up,
+    }

@@ -19,7 +19,9 @@ from .server import DEFAULT_PORT, DEFAULT_PREFIX, run
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--host", default="127.0.0.1",
+                    help="listen address; kube-scheduler calls the extender on loopback (design.md:98), and /bind "
+                         "is unauthenticated, so do not expose it beyond the node without TLS + auth in front")
     ap.add_argument("--port", type=int, default=DEFAULT_PORT)
     ap.add_argument("--url-prefix", default=DEFAULT_PREFIX)
     ap.add_argument("--resource-name", default="amd.com/gpu")
@@ -29,7 +31,11 @@ def main(argv=None) -> int:
     ap.add_argument("--assume-ttl", type=float, default=300.0)
     ap.add_argument("--partition-aware", default="on", choices=["on", "off"],
                     help="CPX/DPX/QPX nodes: group XCPs by physical GPU (on) or treat each as a stand-alone GPU (off)")
-    ap.add_argument("--resync", type=float, default=5.0)
+    ap.add_argument("--resync", type=float, default=5.0, help="polling period without the informer")
+    ap.add_argument("--informer", default="on", choices=["on", "off"],
+                    help="keep the node/pod view current with LIST+WATCH (on) or by polling every --resync s (off)")
+    ap.add_argument("--scheduler-names", default="",
+                    help="comma list of spec.schedulerName values whose pods may be bound (empty = any)")
     ap.add_argument("--apiserver", default="")
     ap.add_argument("--token", default="")
     ap.add_argument("--log-level", default="INFO")
@@ -39,8 +45,17 @@ def main(argv=None) -> int:
 
     api = RestKubeAPI(a.apiserver, token=a.token or None, verify=False) if a.apiserver else RestKubeAPI.in_cluster()
     cfg = ExtenderConfig(contract=Contract(resource_name=a.resource_name, prefix=a.annotation_prefix), policy_name=a.policy,
-                         policy=PlacementPolicy(tie_break=a.tie_break, partition_aware=a.partition_aware == "on"), assume_ttl=a.assume_ttl, resync_s=a.resync)
-    run(TopologyExtender(api, cfg), a.host, a.port, a.url_prefix, resync_period=a.resync)
+                         policy=PlacementPolicy(tie_break=a.tie_break, partition_aware=a.partition_aware == "on"),
+                         assume_ttl=a.assume_ttl, resync_s=a.resync,
+                         scheduler_names=tuple(x.strip() for x in a.scheduler_names.split(",") if x.strip()))
+    ext = TopologyExtender(api, cfg)
+    if a.informer == "on":
+        from ..k8s.informer import Informer
+
+        inf = Informer(api, ext.cache.on_list, ext.cache.on_event)
+        ext.cache.attach_informer(inf)
+        inf.start()
+    run(ext, a.host, a.port, a.url_prefix, resync_period=a.resync)
     return 0
 
 

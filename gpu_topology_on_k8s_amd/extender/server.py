@@ -151,17 +151,20 @@ def make_app(ext: TopologyExtender, prefix: str = DEFAULT_PREFIX, workers: int =
     return app
 
 
-def run(ext: TopologyExtender, host: str = "0.0.0.0", port: int = DEFAULT_PORT, prefix: str = DEFAULT_PREFIX,
+def run(ext: TopologyExtender, host: str = "127.0.0.1", port: int = DEFAULT_PORT, prefix: str = DEFAULT_PREFIX,
         resync_period: float = 5.0) -> None:
+    """Serve until interrupted.  Without an informer the cache is re-listed every ``resync_period``
+    seconds off the request path; with one, WATCH events keep it current and nothing polls."""
     app = make_app(ext, prefix)
 
     async def resync_loop(app):
         async def loop():
             while True:
-                try:
-                    await asyncio.get_running_loop().run_in_executor(None, ext.cache.sync_all)
-                except Exception as e:
-                    log.warning("cache resync failed: %s", e)
+                if ext.cache.informer is None:
+                    try:
+                        await asyncio.get_running_loop().run_in_executor(None, ext.cache.sync_all)
+                    except Exception as e:
+                        log.warning("cache resync failed: %s", e)
                 await asyncio.sleep(resync_period)
 
         task = asyncio.create_task(loop())

@@ -110,14 +110,21 @@ def _layout(flat) -> List[list]:
 
 
 def latest_checkpoint(root: str) -> Optional[str]:
-    """The newest committed step directory under ``root`` (``None`` if there is none)."""
+    """The newest committed step directory under ``root`` (``None`` if there is none).
+
+    ``latest`` names it; if that directory is incomplete (a crash while an existing step was being
+    replaced), the step's moved-aside ``.step_N.old`` or else the newest complete ``step_N`` is used."""
     p = os.path.join(root, "latest")
     if not os.path.exists(p):
         return None
     with open(p) as f:
         name = f.read().strip()
-    d = os.path.join(root, name)
-    return d if os.path.exists(os.path.join(d, "meta.json")) else None
+    for d in (os.path.join(root, name), os.path.join(root, f".{name}.old")):
+        if os.path.exists(os.path.join(d, "meta.json")):
+            return d
+    done = sorted((x for x in os.listdir(root) if x.startswith("step_") and x[5:].isdigit()
+                   and os.path.exists(os.path.join(root, x, "meta.json"))), key=lambda x: int(x[5:]))
+    return os.path.join(root, done[-1]) if done else None
 
 
 class CheckpointWriter:
@@ -279,11 +286,19 @@ class CheckpointWriter:
         if self.rank == 0:
             final = os.path.join(self.root, f"step_{step:06d}")
             os.replace(os.path.join(tmp, "meta.part.json"), os.path.join(tmp, "meta.json"))
-            shutil.rmtree(final, ignore_errors=True)
+            # re-saving an existing step (a resumed run): move the old directory aside first, so a
+            # crash at any point leaves `latest` naming a complete directory (old or new)
+            old = None
+            if os.path.exists(final):
+                old = os.path.join(self.root, f".step_{step:06d}.old")
+                shutil.rmtree(old, ignore_errors=True)
+                os.replace(final, old)
             os.replace(tmp, final)
             with open(os.path.join(self.root, "latest.tmp"), "w") as f:
                 f.write(os.path.basename(final))
             os.replace(os.path.join(self.root, "latest.tmp"), os.path.join(self.root, "latest"))
+            if old is not None:
+                shutil.rmtree(old, ignore_errors=True)
             self._prune()
         self.saved.append(step)
         if dist.is_initialized():
@@ -292,8 +307,9 @@ class CheckpointWriter:
     def _prune(self) -> None:
         if self.keep <= 0:
             return
-        steps = sorted(d for d in os.listdir(self.root) if d.startswith("step_") and
-                       os.path.exists(os.path.join(self.root, d, "meta.json")))
+        # numeric order: the zero padding stops sorting lexicographically past step 999999
+        steps = sorted((d for d in os.listdir(self.root) if d.startswith("step_") and d[5:].isdigit() and
+                        os.path.exists(os.path.join(self.root, d, "meta.json"))), key=lambda d: int(d[5:]))
         for d in steps[:-self.keep]:
             shutil.rmtree(os.path.join(self.root, d), ignore_errors=True)
 

@@ -111,3 +111,15 @@ def test_ingress_bound():
     assert ingress_bound(topo, [0, 1, 2, 3]) == 180.0  # 3 links per member
     topo.probe["ingress_all_gbps"] = [150.0, 170.0, None, 175.0]  # shared fabric caps member 0
     assert ingress_bound(topo, [0, 1, 2, 3]) == 150.0
+
+
+def test_bench_eight_ranks_gloo_dry_run():
+    """The N=8 driver run, rehearsed on CPU: 8 ranks, an 8-device fake node placed through the full
+    k8s flow (k = n: no worst subset), the store protocol with 8 ranks, max-over-ranks timing."""
+    out = _bench("--gpus", "8", "--backend", "cpu", "--discovery", "fake", "--steps", "2", "--warmup", "1", "--size-mb", "1",
+                 "--sweep", "8:64K:64", timeout=900)
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8"
+    assert sorted(out["config"]["subset"]) == list(range(8)) and out["config"]["worst_subset"] is None
+    assert out["k8s_placement"]["assigned"] is True and len(out["k8s_placement"]["devices"]) == 8
+    assert abs(out["busbw_gbps"] - out["algbw_gbps"] * 2 * 7 / 8) <= 1e-2 * out["busbw_gbps"] + 2e-3  # 3-decimal rounding
+    assert out["size_sweep"]["all_exact"] and out["value_kind"] == "busbw"

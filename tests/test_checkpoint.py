@@ -210,3 +210,22 @@ def test_async_checkpoint_on_gpu_resumes_exactly(tmp_path):
     steps(m2, opt2, gen2, 2)
     torch.cuda.synchronize()
     assert torch.equal(m2.flat.data, want)
+
+
+def test_latest_survives_crash_while_replacing_a_step(tmp_path):
+    """re-saving an existing step moves it aside first; `latest` must never dangle."""
+    import json as _json
+
+    from gpu_topology_on_k8s_amd.models.checkpoint import latest_checkpoint
+
+    root = tmp_path
+    for s in (999999, 1000000):
+        d = root / f"step_{s:06d}"
+        d.mkdir()
+        (d / "meta.json").write_text(_json.dumps({"step": s}))
+    (root / "latest").write_text("step_1000000")
+    assert latest_checkpoint(str(root)).endswith("step_1000000")
+    (root / "step_1000000").rename(root / ".step_1000000.old")  # crash between the two renames
+    assert latest_checkpoint(str(root)).endswith(".step_1000000.old")
+    (root / ".step_1000000.old" / "meta.json").unlink()
+    assert latest_checkpoint(str(root)).endswith("step_999999")  # numeric, not lexicographic

@@ -36,7 +36,9 @@ def test_scheduler_configuration():
 def test_manifests_are_valid_yaml():
     docs = list(yaml.safe_load_all(render_manifests()))
     kinds = [d["kind"] for d in docs]
-    assert kinds == ["ServiceAccount", "ClusterRole", "ClusterRoleBinding", "DaemonSet", "Deployment", "Service", "ConfigMap"]
+    assert kinds == ["ServiceAccount", "ClusterRole", "ClusterRoleBinding", "DaemonSet", "Deployment", "ConfigMap"]
+    ext = docs[4]["spec"]["template"]["spec"]["containers"][0]
+    assert "--host=127.0.0.1" in ext["command"] and "ports" not in ext  # /bind is never exposed off-node
     ds = docs[3]
     c = ds["spec"]["template"]["spec"]["containers"][0]
     assert "gpu_topology_on_k8s_amd.deviceplugin" in c["command"]
@@ -73,3 +75,21 @@ def test_committed_deploy_files_are_current():
 
     root = Path(__file__).resolve().parent.parent / "deploy"
     assert (root / "gpu-topology.yaml").read_text() == render_manifests()
+    from gpu_topology_on_k8s_amd.config import render_kind
+
+    for name, text in render_kind().items():
+        assert (root / "kind" / name).read_text() == text, name
+
+
+def test_kind_manifests_config1():
+    from gpu_topology_on_k8s_amd.config import render_kind
+
+    files = render_kind()
+    docs = list(yaml.safe_load_all(files["gpu-topology-kind.yaml"]))
+    ds = [d for d in docs if d["kind"] == "DaemonSet"][0]
+    c = ds["spec"]["template"]["spec"]["containers"][0]
+    assert "--device-specs=stub" in c["command"] and "--discovery=fake" in c["command"] and "--fake-gpus=2" in c["command"]
+    assert all(v["name"] == "device-plugins" for v in ds["spec"]["template"]["spec"]["volumes"])
+    kc = yaml.safe_load(files["kind-config.yaml"])
+    assert [n["role"] for n in kc["nodes"]] == ["control-plane", "worker"]
+    assert yaml.safe_load(files["pod-1gpu.yaml"])["spec"]["containers"][0]["resources"]["limits"]["amd.com/gpu"] == "1"
