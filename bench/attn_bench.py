@@ -62,8 +62,6 @@ def main():
     if hasattr(hip, "attn_bwd_v2"):
         t = timeit(lambda: hip.attn_bwd_v2(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
         res["hip_bwd_v2_ms"] = t * 1e3
-    t = timeit(lambda: hip.attn_bwd_atomic(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
-    res["hip_bwd_v1_atomic_ms"] = t * 1e3
     try:
         t = timeit(lambda: F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True), a.iters)
         res["sdpa_fwd_ms"] = t * 1e3

@@ -18,13 +18,14 @@
 //     and written to LDS after the barrier (guide T14).  Query blocks are launched heaviest-first.
 //   * output O is written token-major [B, S, H, D] (what the o-projection GEMM consumes) and the
 //     row log-sum-exp in log2 units for the backward.
-// Backward v2 (attn_bwd): delta = rowsum(dO*O), then two kernels with no cross-workgroup sums:
-//   * dK/dV: one workgroup = 128 keys of one (batch, kv-head), sweeping every q-head of the GQA group
-//     x 32-query slices; key on the lane for S = Q.K^T and dP = dO.V^T, whose P / dS accumulators
-//     feed dV^T += dO^T.P and dK^T += Q^T.dS as B operands (dO^T, Q^T by transposed LDS reads).
+// Backward (attn_bwd): delta = rowsum(dO*O), then two kernels with no cross-workgroup sums:
+//   * dK/dV (v4): one workgroup = 128 keys of one (batch, kv-head), sweeping every q-head of the GQA
+//     group x 32-query slices; key on the lane for S = Q.K^T and dP = dO.V^T, whose P / dS
+//     accumulators feed dV^T += dO^T.P and dK^T += Q^T.dS as B operands (dO^T, Q^T by transposed LDS
+//     reads); software-pipelined slices.  v3 (attn_bwd_v3) is kept as the bit-identity oracle.
 //   * dQ: forward-shaped (query on the lane), dQ^T += K^T.dS^T accumulated in registers.
-// Backward v1 (attn_bwd_atomic, kept for A/B): one fused kernel, dS through an LDS [key][query]
-// image and dQ summed across key blocks with fp32 atomics — 1.8x slower at the Llama shape.
+// Earlier generations (forward v1 with one LDS buffer, backward v1 with fp32 dQ atomics, backward v2
+// with synchronous slice staging) were measured, retired, and live in git history before round 2.
 #include <hip/hip_runtime.h>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
@@ -104,136 +105,6 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 }
 
 // ==================================================================================== forward
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
-                                                          const u16* __restrict__ v, u16* __restrict__ o,
-                                                          float* __restrict__ lse2, int H, int Hkv, int S, float c,
-                                                          float* __restrict__ dbg) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * BK * D * 2];  // K image | V image
-  char* kimg = smem;
-  char* vimg = smem + BK * D * 2;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, hh = lane >> 5;
-  const int nqb = gridDim.x;
-  const int qb = nqb - 1 - blockIdx.x;  // heaviest (most keys) first
-  const int bh = blockIdx.y, b = bh / H, hq = bh % H, hk = hq / (H / Hkv);
-  const u16* qp = q + ((size_t)(b * H + hq) * S) * D;
-  const u16* kp = k + ((size_t)(b * Hkv + hk) * S) * D;
-  const u16* vp = v + ((size_t)(b * Hkv + hk) * S) * D;
-  const int q0 = qb * BQ + w * 32;
-  const int myq = q0 + r;
-
-  bf16x8 qf[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + (size_t)myq * D + 16 * s + 8 * hh);
-
-  f32x16 oacc[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) oacc[dt] = f32x16{};
-  float m = -INFINITY, l = 0.f;
-
-  const int ntiles = (qb * BQ + BQ) / BK;
-  u16x8 stk[4], stv[4];
-  const int srow = t >> 4, sch = t & 15;
-  auto gload = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const size_t row = (size_t)kt * BK + i * 16 + srow;
-      stk[i] = *reinterpret_cast<const u16x8*>(kp + row * D + sch * 8);
-      stv[i] = *reinterpret_cast<const u16x8*>(vp + row * D + sch * 8);
-    }
-  };
-  auto lstore = [&]() {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      *reinterpret_cast<u16x8*>(kimg + swz(i * 16 + srow, sch)) = stk[i];
-      *reinterpret_cast<u16x8*>(vimg + swz(i * 16 + srow, sch)) = stv[i];
-    }
-  };
-
-  gload(0);
-  lstore();
-  __syncthreads();
-  for (int kt = 0; kt < ntiles; ++kt) {
-    if (kt + 1 < ntiles) gload(kt + 1);  // in flight under this tile's MFMAs (T14)
-    const int key0 = kt * BK;
-    if (key0 <= q0 + 31) {  // wave-uniform: some key of this tile is visible to some query of this wave
-      f32x16 s0 = f32x16{}, s1 = f32x16{};
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        s0 = mfma(lds_b128(kimg, swz(r, 2 * s + hh)), qf[s], s0);
-        s1 = mfma(lds_b128(kimg, swz(32 + r, 2 * s + hh)), qf[s], s1);
-      }
-      if (dbg != nullptr && kt == 0) {  // debug: raw S^T accumulators of the first KV tile
-        float* d = dbg + ((((size_t)bh * nqb + qb) * 4 + w) * 64 + lane) * 32;
-        for (int i = 0; i < 16; ++i) {
-          d[i] = s0[i];
-          d[16 + i] = s1[i];
-        }
-      }
-      const bool diag = key0 + BK - 1 > q0;
-      float mx = -INFINITY;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float x0 = s0[i] * c, x1 = s1[i] * c;
-        if (diag) {
-          const int k0i = key0 + crow(i, hh);
-          if (k0i > myq) x0 = -INFINITY;
-          if (k0i + 32 > myq) x1 = -INFINITY;
-        }
-        s0[i] = x0;
-        s1[i] = x1;
-        mx = fmaxf(mx, fmaxf(x0, x1));
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx);
-      float rs = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        s0[i] = fexp2(s0[i] - mnew);
-        s1[i] = fexp2(s1[i] - mnew);
-        rs += s0[i] + s1[i];
-      }
-      rs += __shfl_xor(rs, 32, 64);
-      // Exact skip: when no query row of the wave raised its max, alpha == 1 for every lane and the
-      // 64-register O rescale is a no-op (most tiles after the first few).
-      if (__any(mnew > m)) {
-        const float alpha = fexp2(m - mnew);
-        l *= alpha;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
-      }
-      l += rs;
-      m = mnew;
-      const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 8), p10 = pack8(s1, 0), p11 = pack8(s1, 8);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int col0 = 32 * dt;
-        oacc[dt] = mfma(tr_frag(vimg, lane, 0 + 4 * hh, 8 + 4 * hh, col0), p00, oacc[dt]);
-        oacc[dt] = mfma(tr_frag(vimg, lane, 16 + 4 * hh, 24 + 4 * hh, col0), p01, oacc[dt]);
-        oacc[dt] = mfma(tr_frag(vimg, lane, 32 + 4 * hh, 40 + 4 * hh, col0), p10, oacc[dt]);
-        oacc[dt] = mfma(tr_frag(vimg, lane, 48 + 4 * hh, 56 + 4 * hh, col0), p11, oacc[dt]);
-      }
-    }
-    __syncthreads();  // every wave is done with this tile's image
-    if (kt + 1 < ntiles) {
-      lstore();
-      __syncthreads();
-    }
-  }
-  const float inv = 1.f / l;
-  u16* orow = o + (((size_t)b * S + myq) * (size_t)(H) + hq) * D;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      u16x4 v4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v4[e] = f2bf(oacc[dt][4 * g4 + e] * inv);
-      *reinterpret_cast<u16x4*>(orow + 32 * dt + 8 * g4 + 4 * hh) = v4;
-    }
-  if (hh == 0) lse2[(size_t)(b * H + hq) * S + myq] = m + log2f(l);
-}
 
 // XCD-aware (batch*head) order: workgroups are dealt round-robin over the 8 XCDs (id % 8), so map
 // consecutive ids of one XCD to consecutive heads — the q-heads of a GQA group (which read the same
@@ -459,331 +330,9 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const u16* __restrict
   }
 }
 
-__global__ __launch_bounds__(256, 1) void attn_bwd_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
-                                                          const u16* __restrict__ v, const u16* __restrict__ dout,
-                                                          const float* __restrict__ lse2, const float* __restrict__ delta,
-                                                          float* __restrict__ dqacc, u16* __restrict__ dk, u16* __restrict__ dv,
-                                                          int H, int Hkv, int S, float c, float scale) {
-  // K image | V image | Q slice | dO slice | dS^T image [key][query] (64-B rows) | lse | delta
-  __shared__ __attribute__((aligned(16))) char smem[KB * D * 2 * 2 + QT * D * 2 * 2 + KB * QT * 2 + QT * 4 * 2];
-  char* kimg = smem;
-  char* vimg = kimg + KB * D * 2;
-  char* qimg = vimg + KB * D * 2;
-  char* doimg = qimg + QT * D * 2;
-  char* dsimg = doimg + QT * D * 2;
-  float* slse = reinterpret_cast<float*>(dsimg + KB * QT * 2);
-  float* sdel = slse + QT;
-
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, hh = lane >> 5;
-  const int kb = blockIdx.x;  // key block (low blocks see the most queries: launched first)
-  const int bk = blockIdx.y, b = bk / Hkv, hk = bk % Hkv, G = H / Hkv;
-  const u16* kp = k + ((size_t)(b * Hkv + hk) * S + (size_t)kb * KB) * D;
-  const u16* vp = v + ((size_t)(b * Hkv + hk) * S + (size_t)kb * KB) * D;
-  // stage this workgroup's K and V (128 x 128 each) once
-  for (int idx = t; idx < KB * 16; idx += 256) {
-    const int row = idx >> 4, ch = idx & 15;
-    *reinterpret_cast<u16x8*>(kimg + swz(row, ch)) = *reinterpret_cast<const u16x8*>(kp + (size_t)row * D + ch * 8);
-    *reinterpret_cast<u16x8*>(vimg + swz(row, ch)) = *reinterpret_cast<const u16x8*>(vp + (size_t)row * D + ch * 8);
-  }
-  f32x16 dvt[4], dkt[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) dvt[dt] = dkt[dt] = f32x16{};
-  const int mykey = kb * KB + w * 32 + r;  // key held on this lane
-  const int krow = w * 32 + r;             // its row in the K/V image
-
-  const int qt0 = (kb * KB) / QT;
-  const int nqt = S / QT;
-  for (int hi = 0; hi < G; ++hi) {
-    const int hq = hk * G + hi;
-    const u16* qp = q + ((size_t)(b * H + hq) * S) * D;
-    for (int qt = qt0; qt < nqt; ++qt) {
-      const int qbase = qt * QT;
-      __syncthreads();  // previous slice fully consumed (and K/V staged on the first pass)
-      for (int idx = t; idx < QT * 16; idx += 256) {
-        const int row = idx >> 4, ch = idx & 15;
-        *reinterpret_cast<u16x8*>(qimg + swz(row, ch)) = *reinterpret_cast<const u16x8*>(qp + (size_t)(qbase + row) * D + ch * 8);
-        *reinterpret_cast<u16x8*>(doimg + swz(row, ch)) =
-            *reinterpret_cast<const u16x8*>(dout + (((size_t)b * S + qbase + row) * H + hq) * D + ch * 8);
-      }
-      if (t < QT) slse[t] = lse2[((size_t)b * H + hq) * S + qbase + t];
-      else if (t < 2 * QT) sdel[t - QT] = delta[((size_t)b * H + hq) * S + qbase + t - QT];
-      __syncthreads();
-
-      // S = Q.K^T and dP = dO.V^T with the key on the lane (rows = queries crow(i, hh))
-      f32x16 sacc = f32x16{}, dpacc = f32x16{};
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const bf16x8 kb8 = lds_b128(kimg, swz(krow, 2 * s + hh));
-        const bf16x8 vb8 = lds_b128(vimg, swz(krow, 2 * s + hh));
-        sacc = mfma(lds_b128(qimg, swz(r, 2 * s + hh)), kb8, sacc);
-        dpacc = mfma(lds_b128(doimg, swz(r, 2 * s + hh)), vb8, dpacc);
-      }
-      f32x16 p, ds;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qi = crow(i, hh);
-        const float pv = (mykey > qbase + qi) ? 0.f : fexp2(sacc[i] * c - slse[qi]);
-        p[i] = pv;
-        ds[i] = pv * (dpacc[i] - sdel[qi]);
-      }
-      const bf16x8 p0 = pack8(p, 0), p1 = pack8(p, 8), d0 = pack8(ds, 0), d1 = pack8(ds, 8);
-      // dV^T += dO^T . P ; dK^T += Q^T . dS   (k = query: rows 16t + 8(j>>2) + 4hh + (j&3))
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        dvt[dt] = mfma(tr_frag(doimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), p0, dvt[dt]);
-        dvt[dt] = mfma(tr_frag(doimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), p1, dvt[dt]);
-        dkt[dt] = mfma(tr_frag(qimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), d0, dkt[dt]);
-        dkt[dt] = mfma(tr_frag(qimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), d1, dkt[dt]);
-      }
-      // dS^T image: row = key (krow), 64-B rows of 32 queries; regs 4g..4g+3 = queries 8g + 4hh + 0..3
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u16x4 v4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v4[e] = f2bf(ds[4 * g + e]);
-        *reinterpret_cast<u16x4*>(dsimg + krow * 64 + 2 * (8 * g + 4 * hh)) = v4;
-      }
-      __syncthreads();
-      // dQ[q][d] = sum_key dS[q][key] K[key][d]; wave w owns d columns 32w..32w+31, k = 128 keys
-      f32x16 dq = f32x16{};
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        // A[row q = r][k = key 16s + 8hh + j] = dS^T[key][q]: transposed read of the dS image
-        const int gq = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
-        const int qcol = 16 * (gq & 1);  // first query column of this 16-lane group
-        const int kr = 16 * s + 8 * hh + qq;
-        const bf16x8 a = cat8(lds_tr(dsimg, kr * 64 + 2 * (qcol + 4 * pp)), lds_tr(dsimg, (kr + 4) * 64 + 2 * (qcol + 4 * pp)));
-        // B[k = key 16s + 8hh + j][col = d 32w + r] = K[key][d]: transposed read of the K image
-        const bf16x8 bkf = tr_frag(kimg, lane, 16 * s + 8 * hh, 16 * s + 8 * hh + 4, 32 * w);
-        dq = mfma(a, bkf, dq);
-      }
-      float* dqrow = dqacc + ((size_t)(b * H + hq) * S + qbase) * D + 32 * w + r;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) atomicAdd(dqrow + (size_t)crow(i, hh) * D, dq[i]);
-    }
-  }
-  // dK = scale * dK^T^T, dV = dV^T^T : lane = key, regs = d rows (crow) -> 8-B stores per 4 d
-  u16* dkrow = dk + ((size_t)(b * Hkv + hk) * S + mykey) * D;
-  u16* dvrow = dv + ((size_t)(b * Hkv + hk) * S + mykey) * D;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      u16x4 a4, b4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        a4[e] = f2bf(dkt[dt][4 * g4 + e] * scale);
-        b4[e] = f2bf(dvt[dt][4 * g4 + e]);
-      }
-      *reinterpret_cast<u16x4*>(dkrow + 32 * dt + 8 * g4 + 4 * hh) = a4;
-      *reinterpret_cast<u16x4*>(dvrow + 32 * dt + 8 * g4 + 4 * hh) = b4;
-    }
-}
-
-// debug: stage a [64][128] bf16 tile into the swizzled image, return what tr_frag delivers per lane
-__global__ __launch_bounds__(64) void tr_probe_kernel(const u16* __restrict__ tile, u16* __restrict__ out, int t, int col0) {
-  __shared__ __attribute__((aligned(16))) char img[BK * D * 2];
-  const int lane = threadIdx.x, hh = lane >> 5;
-  for (int idx = lane; idx < BK * 16; idx += 64) {
-    const int row = idx >> 4, ch = idx & 15;
-    *reinterpret_cast<u16x8*>(img + swz(row, ch)) = *reinterpret_cast<const u16x8*>(tile + row * D + ch * 8);
-  }
-  __syncthreads();
-  *reinterpret_cast<bf16x8*>(out + lane * 8) = tr_frag(img, lane, 16 * t + 4 * hh, 16 * t + 8 + 4 * hh, col0);
-}
-
-__global__ __launch_bounds__(256) void scale_cast_kernel(const float* __restrict__ x, u16* __restrict__ y, float s, size_t n) {
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) y[i] = f2bf(x[i] * s);
-}
-
 // ============================================================================ backward v2 (split)
-// Kernel 1 — dK, dV.  One workgroup = 4 waves = 128 keys of one (batch, kv-head); sweeps every
-// q-head of the GQA group x 32-query slices.  Key on the lane: S = Q.K^T and dP = dO.V^T land with
-// queries in registers, so P and dS feed dV^T += dO^T.P and dK^T += Q^T.dS as B operands directly.
-// No dQ here (kernel 2), hence no atomics and no dS image; K|V|Q|dO images = exactly 80 KiB, so two
-// workgroups share a CU.  Q/dO of the next slice are prefetched into registers under the MFMAs.
-// Per-query constants (lse, delta) come from lane r of the slice via a lane shuffle.
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
-                                                               const u16* __restrict__ v, const u16* __restrict__ dout,
-                                                               const float* __restrict__ lse2, const float* __restrict__ delta,
-                                                               u16* __restrict__ dk, u16* __restrict__ dv, int H, int Hkv, int S,
-                                                               float c, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[KB * D * 2 * 2 + QT * D * 2 * 2];
-  char* kimg = smem;
-  char* vimg = kimg + KB * D * 2;
-  char* qimg = vimg + KB * D * 2;
-  char* doimg = qimg + QT * D * 2;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, hh = lane >> 5;
-  const int kb = blockIdx.x, bk = blockIdx.y, b = bk / Hkv, hk = bk % Hkv, G = H / Hkv;
-  const u16* kp = k + ((size_t)(b * Hkv + hk) * S + (size_t)kb * KB) * D;
-  const u16* vp = v + ((size_t)(b * Hkv + hk) * S + (size_t)kb * KB) * D;
-  for (int idx = t; idx < KB * 16; idx += 256) {
-    const int row = idx >> 4, ch = idx & 15;
-    *reinterpret_cast<u16x8*>(kimg + swz(row, ch)) = *reinterpret_cast<const u16x8*>(kp + (size_t)row * D + ch * 8);
-    *reinterpret_cast<u16x8*>(vimg + swz(row, ch)) = *reinterpret_cast<const u16x8*>(vp + (size_t)row * D + ch * 8);
-  }
-  f32x16 dvt[4], dkt[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) dvt[dt] = dkt[dt] = f32x16{};
-  const int krow = w * 32 + r, mykey = kb * KB + krow, kmin = kb * KB + w * 32;
-  const int qt0 = (kb * KB) / QT, nqt = S / QT - qt0, nslice = G * nqt;
-  // slice staging: thread t owns rows (t >> 4) and (t >> 4) + 16, chunk t & 15, of Q and dO
-  const int srow = t >> 4, sch = t & 15;
-  u16x8 pq0, pq1, pd0, pd1;
-  auto gload = [&](int idx) {
-    const int hq = hk * G + idx / nqt, qbase = (qt0 + idx % nqt) * QT;
-    const u16* qp = q + ((size_t)(b * H + hq) * S + qbase) * D;
-    pq0 = *reinterpret_cast<const u16x8*>(qp + (size_t)srow * D + sch * 8);
-    pq1 = *reinterpret_cast<const u16x8*>(qp + (size_t)(srow + 16) * D + sch * 8);
-    const u16* dp = dout + (((size_t)b * S + qbase) * H + hq) * D;
-    pd0 = *reinterpret_cast<const u16x8*>(dp + (size_t)srow * H * D + sch * 8);
-    pd1 = *reinterpret_cast<const u16x8*>(dp + (size_t)(srow + 16) * H * D + sch * 8);
-  };
-  auto lstore = [&]() {
-    *reinterpret_cast<u16x8*>(qimg + swz(srow, sch)) = pq0;
-    *reinterpret_cast<u16x8*>(qimg + swz(srow + 16, sch)) = pq1;
-    *reinterpret_cast<u16x8*>(doimg + swz(srow, sch)) = pd0;
-    *reinterpret_cast<u16x8*>(doimg + swz(srow + 16, sch)) = pd1;
-  };
-  gload(0);
-  lstore();
-  __syncthreads();
-  for (int idx = 0; idx < nslice; ++idx) {
-    const int hq = hk * G + idx / nqt, qbase = (qt0 + idx % nqt) * QT;
-    const size_t rowoff = ((size_t)b * H + hq) * S + qbase + r;
-    const float lse_r = lse2[rowoff], del_r = delta[rowoff];  // query qbase + r (lane r of each half)
-    if (qbase + QT - 1 >= kmin) {  // wave-uniform: some query of the slice sees a key of this wave
-      f32x16 sacc = f32x16{}, dpacc = f32x16{};
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        sacc = mfma(lds_b128(qimg, swz(r, 2 * s + hh)), lds_b128(kimg, swz(krow, 2 * s + hh)), sacc);
-        dpacc = mfma(lds_b128(doimg, swz(r, 2 * s + hh)), lds_b128(vimg, swz(krow, 2 * s + hh)), dpacc);
-      }
-      f32x16 p, ds;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qi = crow(i, hh);
-        const float lq = __shfl(lse_r, qi, 64), dq_ = __shfl(del_r, qi, 64);
-        const float pv = (mykey > qbase + qi) ? 0.f : fexp2(sacc[i] * c - lq);
-        p[i] = pv;
-        ds[i] = pv * (dpacc[i] - dq_);
-      }
-      const bf16x8 p0 = pack8(p, 0), p1 = pack8(p, 8), d0 = pack8(ds, 0), d1 = pack8(ds, 8);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        dvt[dt] = mfma(tr_frag(doimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), p0, dvt[dt]);
-        dvt[dt] = mfma(tr_frag(doimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), p1, dvt[dt]);
-        dkt[dt] = mfma(tr_frag(qimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), d0, dkt[dt]);
-        dkt[dt] = mfma(tr_frag(qimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), d1, dkt[dt]);
-      }
-    }
-    __syncthreads();
-    if (idx + 1 < nslice) {  // synchronous staging: the co-resident workgroup covers its latency
-      gload(idx + 1);
-      lstore();
-      __syncthreads();
-    }
-  }
-  u16* dkrow = dk + ((size_t)(b * Hkv + hk) * S + mykey) * D;
-  u16* dvrow = dv + ((size_t)(b * Hkv + hk) * S + mykey) * D;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      u16x4 a4, b4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        a4[e] = f2bf(dkt[dt][4 * g4 + e] * scale);
-        b4[e] = f2bf(dvt[dt][4 * g4 + e]);
-      }
-      *reinterpret_cast<u16x4*>(dkrow + 32 * dt + 8 * g4 + 4 * hh) = a4;
-      *reinterpret_cast<u16x4*>(dvrow + 32 * dt + 8 * g4 + 4 * hh) = b4;
-    }
-}
 
-// Kernel 2 — dQ.  Forward-shaped: one workgroup = 4 waves = 128 queries of one (batch, q-head),
-// query on the lane.  Per 64-key tile: S^T = K.Q^T and dP^T = V.dO^T (Q, dO fragments in registers),
-// dS^T = P^T * (dP^T - delta), and dQ^T += K^T.dS^T with K^T gathered by transposed LDS reads and the
-// dS^T accumulator as the B operand — dQ is summed in registers, written once.
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
-                                                             const u16* __restrict__ v, const u16* __restrict__ dout,
-                                                             const float* __restrict__ lse2, const float* __restrict__ delta,
-                                                             u16* __restrict__ dq, int H, int Hkv, int S, float c, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * BK * D * 2];
-  char* kimg = smem;
-  char* vimg = smem + BK * D * 2;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, hh = lane >> 5;
-  const int nqb = gridDim.x, qb = nqb - 1 - blockIdx.x;
-  const int bh = blockIdx.y, b = bh / H, hq = bh % H, hk = hq / (H / Hkv);
-  const u16* kp = k + ((size_t)(b * Hkv + hk) * S) * D;
-  const u16* vp = v + ((size_t)(b * Hkv + hk) * S) * D;
-  const int q0 = qb * BQ + w * 32, myq = q0 + r;
-  const u16* qrow = q + ((size_t)(b * H + hq) * S + myq) * D;
-  const u16* dorow = dout + (((size_t)b * S + myq) * H + hq) * D;
-  bf16x8 qf[8], df[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    qf[s] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s + 8 * hh);
-    df[s] = *reinterpret_cast<const bf16x8*>(dorow + 16 * s + 8 * hh);
-  }
-  const float lse_q = lse2[(size_t)(b * H + hq) * S + myq], del_q = delta[(size_t)(b * H + hq) * S + myq];
-  f32x16 dqt[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) dqt[dt] = f32x16{};
-  const int ntiles = (qb * BQ + BQ) / BK;
-  const int srow = t >> 4, sch = t & 15;
-  for (int kt = 0; kt < ntiles; ++kt) {
-    __syncthreads();  // previous tile consumed
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const size_t row = (size_t)kt * BK + i * 16 + srow;
-      *reinterpret_cast<u16x8*>(kimg + swz(i * 16 + srow, sch)) = *reinterpret_cast<const u16x8*>(kp + row * D + sch * 8);
-      *reinterpret_cast<u16x8*>(vimg + swz(i * 16 + srow, sch)) = *reinterpret_cast<const u16x8*>(vp + row * D + sch * 8);
-    }
-    __syncthreads();
-    const int key0 = kt * BK;
-    if (key0 > q0 + 31) continue;  // wave-uniform: no visible key in this tile (barriers stay matched)
-    f32x16 s0 = f32x16{}, s1 = f32x16{}, e0 = f32x16{}, e1 = f32x16{};
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const bf16x8 k0 = lds_b128(kimg, swz(r, 2 * s + hh)), k1 = lds_b128(kimg, swz(32 + r, 2 * s + hh));
-      const bf16x8 v0 = lds_b128(vimg, swz(r, 2 * s + hh)), v1 = lds_b128(vimg, swz(32 + r, 2 * s + hh));
-      s0 = mfma(k0, qf[s], s0);
-      s1 = mfma(k1, qf[s], s1);
-      e0 = mfma(v0, df[s], e0);
-      e1 = mfma(v1, df[s], e1);
-    }
-    const bool diag = key0 + BK - 1 > q0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int kk = key0 + crow(i, hh);
-      const float p0 = (diag && kk > myq) ? 0.f : fexp2(s0[i] * c - lse_q);
-      const float p1 = (diag && kk + 32 > myq) ? 0.f : fexp2(s1[i] * c - lse_q);
-      s0[i] = p0 * (e0[i] - del_q);
-      s1[i] = p1 * (e1[i] - del_q);
-    }
-    const bf16x8 d00 = pack8(s0, 0), d01 = pack8(s0, 8), d10 = pack8(s1, 0), d11 = pack8(s1, 8);
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      dqt[dt] = mfma(tr_frag(kimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), d00, dqt[dt]);
-      dqt[dt] = mfma(tr_frag(kimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), d01, dqt[dt]);
-      dqt[dt] = mfma(tr_frag(kimg, lane, 32 + 4 * hh, 40 + 4 * hh, 32 * dt), d10, dqt[dt]);
-      dqt[dt] = mfma(tr_frag(kimg, lane, 48 + 4 * hh, 56 + 4 * hh, 32 * dt), d11, dqt[dt]);
-    }
-  }
-  u16* out = dq + ((size_t)(b * H + hq) * S + myq) * D;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      u16x4 a4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) a4[e] = f2bf(dqt[dt][4 * g4 + e] * scale);
-      *reinterpret_cast<u16x4*>(out + 32 * dt + 8 * g4 + 4 * hh) = a4;
-    }
-}
-
-// dK/dV v3.  Same decomposition as attn_bwd_dkdv_kernel (one workgroup = 128 keys of one (batch,
+// dK/dV v3.  The split dK/dV decomposition (one workgroup = 128 keys of one (batch,
 // kv-head), sweeping every q-head of the GQA group x 32-query slices, key on the lane), with the
 // slice stream made asynchronous and the LDS footprint cut so two workgroups still share a CU:
 //   * each lane's K row (the B operand of S = Q.K^T) lives in registers for the whole kernel
@@ -1090,7 +639,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv4_kernel(const u16* __res
     }
 }
 
-// dQ v2: attn_bwd_dq_kernel restructured like forward v2 — LDS-DMA double-buffered K/V tiles with
+// dQ v2: the forward-shaped dQ kernel restructured like forward v2 — LDS-DMA double-buffered K/V tiles with
 // one barrier per tile, the block's diagonal tiles peeled out of a branch-free main loop, LPT +
 // XCD-grouped grid (B*H, S/128).  (Forcing the fragment reads ahead with sched_group_barrier spills
 // inside the loop here: Q, dO, 4 accumulators and dQ^T already hold 192 VGPRs.)
@@ -1205,20 +754,6 @@ void check_qkv(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
   TORCH_CHECK(q.size(1) * q.size(2) * D * 2 < (int64_t(1) << 31), "attention: per-batch q/dO bytes must fit the 32-bit buffer offsets");
 }
 
-std::vector<at::Tensor> attn_fwd_impl(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale, bool debug) {
-  check_qkv(q, k, v);
-  const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
-  auto o = at::empty({B, S, H, D}, q.options());
-  auto lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
-  at::Tensor dbg;
-  if (debug) dbg = at::zeros({B * H, S / BQ, 4, 64, 32}, q.options().dtype(at::kFloat));
-  const float c = (float)(scale * 1.4426950408889634);
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3(S / BQ, B * H), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bpm(o),
-                     lse.data_ptr<float>(), H, Hkv, S, c, debug ? dbg.data_ptr<float>() : nullptr);
-  if (debug) return {o, lse, dbg};
-  return {o, lse};
-}
-
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale) {
   check_qkv(q, k, v);
   const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
@@ -1228,23 +763,6 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
   hipLaunchKernelGGL(attn_fwd2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bpm(o),
                      lse.data_ptr<float>(), H, Hkv, S, c);
   return {o, lse};
-}
-
-// v1 forward (two barriers per tile, single LDS buffer), kept for A/B
-std::vector<at::Tensor> attn_fwd_v1(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale) {
-  return attn_fwd_impl(q, k, v, scale, false);
-}
-
-at::Tensor attn_tr_probe(const at::Tensor& tile, int64_t t, int64_t col0) {
-  TORCH_CHECK(tile.is_cuda() && tile.scalar_type() == at::kBFloat16 && tile.is_contiguous() && tile.numel() == BK * D);
-  TORCH_CHECK(t >= 0 && t < 4 && col0 >= 0 && col0 <= 96 && col0 % 32 == 0);
-  auto out = at::empty({64, 8}, tile.options());
-  hipLaunchKernelGGL(tr_probe_kernel, dim3(1), dim3(64), 0, cur_stream(), bp(tile), bpm(out), (int)t, (int)col0);
-  return out;
-}
-
-std::vector<at::Tensor> attn_fwd_debug(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale) {
-  return attn_fwd_impl(q, k, v, scale, true);
 }
 
 // v3 dK/dV (kept for A/B: v4 must match it bit for bit) + dQ v2
@@ -1284,47 +802,6 @@ std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, co
                      lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
   hipLaunchKernelGGL(attn_bwd_dq2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
                      lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
-  return {dq, dk, dv};
-}
-
-// v2 backward (kept for A/B): dK/dV with synchronous slice staging, dQ with two barriers per tile
-std::vector<at::Tensor> attn_bwd_v2(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                    const at::Tensor& out, const at::Tensor& lse, double scale) {
-  check_qkv(q, k, v);
-  const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
-  auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
-  auto dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
-  const int rows = B * S * H;
-  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
-                     delta.data_ptr<float>(), B, H, S);
-  const float c = (float)(scale * 1.4426950408889634);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(S / KB, B * Hkv), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
-                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(S / BQ, B * H), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
-                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
-  return {dq, dk, dv};
-}
-
-// v1: one fused kernel, dQ summed across key blocks with fp32 atomics (kept for A/B)
-std::vector<at::Tensor> attn_bwd_atomic(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                        const at::Tensor& out, const at::Tensor& lse, double scale) {
-  check_qkv(q, k, v);
-  const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
-  TORCH_CHECK(dout.is_contiguous() && out.is_contiguous() && dout.numel() == q.numel() && out.numel() == q.numel(),
-              "attention bwd: dout/out must be contiguous [B, S, H, D]");
-  auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
-  auto dqacc = at::zeros({B, H, S, D}, q.options().dtype(at::kFloat));
-  auto dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
-  const int rows = B * S * H;
-  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
-                     delta.data_ptr<float>(), B, H, S);
-  const float c = (float)(scale * 1.4426950408889634);
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3(S / KB, B * Hkv), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
-                     lse.data_ptr<float>(), delta.data_ptr<float>(), dqacc.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c,
-                     (float)scale);
-  const size_t n = dq.numel();
-  hipLaunchKernelGGL(scale_cast_kernel, dim3((unsigned)std::min<size_t>((n + 255) / 256, 4096)), dim3(256), 0, cur_stream(),
-                     dqacc.data_ptr<float>(), bpm(dq), (float)scale, n);
   return {dq, dk, dv};
 }
 

@@ -731,13 +731,6 @@ at::Tensor sq_norm(const at::Tensor& g) {
 
 namespace gtk_attn {  // csrc/ops/attention.hip
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale);
-std::vector<at::Tensor> attn_fwd_debug(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale);
-std::vector<at::Tensor> attn_bwd_v2(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                    const at::Tensor& out, const at::Tensor& lse, double scale);
-std::vector<at::Tensor> attn_fwd_v1(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale);
-at::Tensor attn_tr_probe(const at::Tensor& tile, int64_t t, int64_t col0);
-std::vector<at::Tensor> attn_bwd_atomic(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                        const at::Tensor& out, const at::Tensor& lse, double scale);
 std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                  const at::Tensor& out, const at::Tensor& lse, double scale);
 std::vector<at::Tensor> attn_bwd_v3(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
@@ -750,13 +743,8 @@ at::Tensor transpose_bf16(const at::Tensor& x);
 
 PYBIND11_MODULE(_fused, m) {
   m.def("attn_fwd", &gtk_attn::attn_fwd, "causal GQA flash attention forward (bf16, D=128): -> (o [B,S,H,D], lse2 [B,H,S])");
-  m.def("attn_fwd_v1", &gtk_attn::attn_fwd_v1, "v1 forward (single-buffered LDS, two barriers per tile; A/B reference)");
   m.def("attn_bwd", &gtk_attn::attn_bwd, "flash attention backward: -> (dq, dk, dv)");
-  m.def("attn_fwd_debug", &gtk_attn::attn_fwd_debug, "forward + raw S^T accumulators of the first KV tile (tests)");
-  m.def("attn_tr_probe", &gtk_attn::attn_tr_probe, "transposed-fragment gather of a [64][128] tile (tests)");
   m.def("attn_bwd_v3", &gtk_attn::attn_bwd_v3, "v3 backward (dK/dV not pipelined across slices; A/B reference for v4)");
-  m.def("attn_bwd_v2", &gtk_attn::attn_bwd_v2, "v2 backward (synchronous dK/dV slice staging; A/B reference)");
-  m.def("attn_bwd_atomic", &gtk_attn::attn_bwd_atomic, "v1 fused backward with fp32 dQ atomics (A/B reference)");
   m.doc() = "gfx950 fused kernels for the Llama-3 DP validation workload";
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);

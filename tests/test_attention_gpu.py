@@ -1,4 +1,6 @@
 """HIP MFMA flash attention (csrc/ops/attention.hip) vs a plain PyTorch fp32 reference (``pytest -m gpu``)."""
+import math
+
 import pytest
 import torch
 
@@ -58,25 +60,6 @@ def test_attention_backward(fused, B, H, Hkv, S):
     assert _rel(vh.grad, vf.grad) < 2e-2, _rel(vh.grad, vf.grad)
 
 
-def test_attention_kernel_generations_agree(fused):
-    """Forward v2 vs v1 and backward v3 (LDS-DMA pipelines) vs v2: same math, same numbers (up to
-    fp32 summation order)."""
-    torch.manual_seed(3)
-    B, H, Hkv, S = 2, 8, 2, 768
-    q = torch.randn(B, H, S, 128, device="cuda", dtype=torch.bfloat16)
-    k = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
-    v = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
-    do = torch.randn(B, S, H, 128, device="cuda", dtype=torch.bfloat16)
-    hip = fused.hip()
-    o2, l2 = hip.attn_fwd(q, k, v, 128 ** -0.5)
-    o1, l1 = hip.attn_fwd_v1(q, k, v, 128 ** -0.5)
-    assert _rel(o2, o1) < 5e-3 and torch.allclose(l2, l1, atol=1e-3)
-    g3 = hip.attn_bwd(do, q, k, v, o2, l2, 128 ** -0.5)
-    g2 = hip.attn_bwd_v2(do, q, k, v, o2, l2, 128 ** -0.5)  # v4 default vs v2
-    for a, b in zip(g3, g2):
-        assert _rel(a, b) < 5e-3, _rel(a, b)
-
-
 @pytest.mark.parametrize("B,H,Hkv,S", [(2, 8, 2, 768), (1, 4, 4, 128), (1, 32, 8, 1024), (2, 4, 1, 384)])
 def test_attention_bwd_v4_matches_v3(fused, B, H, Hkv, S):
     """dK/dV v4 (the default: slices software-pipelined through a 3-buffer ring, branch-free) does
@@ -100,8 +83,7 @@ def test_attention_bwd_v4_matches_v3(fused, B, H, Hkv, S):
 def test_attention_forward_max_slack(fused, B, H, Hkv, S, spike):
     """The forward raises its running max only past a slack (P <= 2^8 before 1/l).  `spike` plants
     large keys late in the sequence so the max jumps after many tiles and the O/l rescale path runs
-    mid-sequence; outputs and log-sum-exp must stay exact against fp32 and the v1 kernel (which
-    rescales on every increase)."""
+    mid-sequence; outputs and the log-sum-exp must match an fp32 reference."""
     torch.manual_seed(6)
     q = torch.randn(B, H, S, 128, device="cuda", dtype=torch.bfloat16)
     k = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
@@ -111,12 +93,15 @@ def test_attention_forward_max_slack(fused, B, H, Hkv, S, spike):
         k[:, :, S - 70] = q[:, 0, S - 1].unsqueeze(1) * 4
     hip = fused.hip()
     o2, l2 = hip.attn_fwd(q, k, v, 128 ** -0.5)
-    o1, l1 = hip.attn_fwd_v1(q, k, v, 128 ** -0.5)
     ref = fused.attention_ref(q, k, v)
     assert torch.isfinite(o2).all() and torch.isfinite(l2).all()
     assert _rel(o2, ref) < 1e-2, _rel(o2, ref)
-    assert _rel(o2, o1) < 5e-3, _rel(o2, o1)
-    assert torch.allclose(l2, l1, atol=1e-3, rtol=1e-5), (l2 - l1).abs().max().item()
+    # log-sum-exp of the causal scores, log2 units (what the backward consumes)
+    kf = k.float().repeat_interleave(H // Hkv, dim=1)
+    sc = torch.einsum("bhqd,bhkd->bhqk", q.float(), kf) * 128 ** -0.5
+    sc = sc.masked_fill(torch.ones(S, S, dtype=torch.bool, device="cuda").triu(1), float("-inf"))
+    lse_ref = torch.logsumexp(sc, dim=-1) / math.log(2.0)
+    assert torch.allclose(l2, lse_ref, atol=2e-3, rtol=1e-5), (l2 - lse_ref).abs().max().item()
 
 
 def test_attention_causality(fused):

@@ -1,0 +1,37 @@
+#!/usr/bin/env bash
+# One gpurun call per invocation:  gpurun --timeout 1200 -- 'bash tools/gpu_suite.sh <mode> <outdir>'
+#   suite    pytest -m gpu, smoke(), headline bench (k=1)
+#   bench    headline bench only (the driver's command line)
+#   profile  rocprofv3 --kernel-trace --stats of the headline bench and of the link probe
+# Every GPU step has its own time limit; the first failing step ends the call (exit status kept).
+set -uo pipefail
+mode=${1:-suite}
+out=${2:-gpurun_out/run}
+mkdir -p "$out"
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+
+step() {  # step <name> <seconds> <command...>
+  local name=$1 secs=$2; shift 2
+  echo "[gpu_suite] $name"
+  timeout -k 10 "$secs" "$@" > "$out/$name.log" 2>&1
+  local rc=$?
+  tail -3 "$out/$name.log"
+  if [ $rc -ne 0 ]; then echo "[gpu_suite] $name failed rc=$rc"; exit $rc; fi
+}
+
+case "$mode" in
+  suite)
+    step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+    step smoke 300 python -u -c 'import __graft_entry__ as g; g.smoke()'
+    step bench_k1 600 python -u bench.py --gpus 1 --steps 20 --warmup 5
+    ;;
+  bench)
+    step bench_k1 600 python -u bench.py --gpus 1 --steps 20 --warmup 5
+    ;;
+  profile)
+    step prof_bench 600 rocprofv3 --kernel-trace --stats -d "$out/prof_bench" -o run -- python3 bench.py --steps 5 --warmup 2 --sweep off
+    step prof_probe 600 rocprofv3 --kernel-trace --stats -d "$out/prof_probe" -o run -- python3 -m gpu_topology_on_k8s_amd probe --preset full
+    ;;
+  *) echo "unknown mode $mode"; exit 2 ;;
+esac
+echo "[gpu_suite] done"
