@@ -43,13 +43,14 @@ def _init_dist(device_kind: str) -> Dict[str, int]:
     return {"rank": rank, "world": world, "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}
 
 
-def _choose_device(env, placement: str, discovery: str) -> Dict[str, object]:
-    """Rank 0 places the job; the choice travels through the store."""
+def _choose_device(env, placement: str, discovery: str, visible: Optional[int] = None) -> Dict[str, object]:
+    """Rank 0 places the job; the choice travels through the store.  ``visible`` models a node of
+    that many devices without HIP (CPU dry runs of the best-vs-worst harness on a fake node)."""
     store = dist.distributed_c10d._get_default_store()
     if env["rank"] == 0:
         from ..parallel.allreduce import choose_subset
 
-        ch = choose_subset(env["world"], backend=discovery)
+        ch = choose_subset(env["world"], backend=discovery, visible=visible)
         use_worst = placement == "worst" and ch.worst
         devices = ch.worst if use_worst else ch.devices  # node-local topology indices (GROUP numbering)
         info = {"devices": devices, "hip_devices": ch.worst_hip if use_worst else ch.hip_devices, "best": ch.devices,
@@ -72,7 +73,10 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         device = torch.device("cuda", dev)
         gemm_mode = setup_gemm_tuning(gemm_tuning, gemm_table, env["rank"])
     else:
-        pl = {"devices": [], "best": [], "worst": None, "source": "cpu"}
+        if discovery == "fake":  # placement on a fake node (GTK_FAKE_GPUS devices), ranks stay on the CPU
+            pl = _choose_device(env, placement, discovery, visible=int(os.environ.get("GTK_FAKE_GPUS", "8")))
+        else:
+            pl = {"devices": [], "best": [], "worst": None, "source": "cpu"}
         device = torch.device("cpu")
         gemm_mode = "off"
     cfg = LlamaConfig.named(model_name)
@@ -151,6 +155,8 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "devices": pl["devices"],
         "best_devices": pl.get("best"),
         "worst_devices": pl.get("worst"),
+        "best_score": pl.get("best_score"),
+        "worst_score": pl.get("worst_score"),
         "global_batch": batch * env["world"],
         "seq_len": seq,
         "steps": steps,

@@ -280,3 +280,25 @@ def test_train_entry_cpu_single_rank(zero1):
             os.environ.pop(k, None)
     assert out["tokens_per_s"] > 0 and out["steps"] == 2 and math.isfinite(out["loss_last"])
     assert out["zero1"] == zero1 and out["optimizer_state_gb"] > 0
+
+
+def test_best_vs_worst_harness_cpu_dry_run(tmp_path):
+    """bench/train_llama.py (BASELINE config 5 / Gaia Exp. 6) end to end on CPU: two 2-rank gloo jobs
+    placed on a fake 8-device node, best and worst being different real device sets (k < n)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "r.json"
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(repo, "bench", "train_llama.py"), "--gpus", "2", "--device", "cpu",
+                        "--discovery", "fake", "--model", "tiny", "--batch", "1", "--seq", "64", "--steps", "2", "--warmup", "1",
+                        "--attn", "sdpa", "--gemm-tuning", "off", "--out", str(out)],
+                       capture_output=True, text=True, timeout=600, cwd=repo, env=dict(env, GTK_FAKE_GPUS="8"))
+    assert p.returncode == 0, p.stderr[-4000:]
+    s = json.loads(out.read_text())["summary"]
+    assert s["worst_kind"] == "worst" and s["best_devices"] != s["worst_devices"]
+    assert len(s["best_devices"]) == 2 and s["best_tokens_per_s"] > 0 and s["worst_tokens_per_s"] > 0
+    assert s["best_score"] > s["worst_score"]
