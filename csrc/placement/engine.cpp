@@ -34,22 +34,25 @@ Engine::Engine(const Problem& p, const Policy& pol) : p_(p), pol_(pol) {
       lv.size[lv.gid[i]] += 1;
       lv.free[lv.gid[i]] += p_.free[i] ? 1 : 0;
     }
+    lv.sorted_free = lv.free;
+    std::sort(lv.sorted_free.begin(), lv.sorted_free.end(), std::greater<int>());
     lv_.push_back(std::move(lv));
   }
 }
 
 int Engine::min_groups(const Level& lv, int k) const {
-  std::vector<int> f = lv.free;
-  std::sort(f.begin(), f.end(), std::greater<int>());
+  // lv.sorted_free: free counts in descending order (fixed for the problem)
   int s = 0;
-  for (size_t i = 0; i < f.size(); ++i) {
-    s += f[i];
+  for (size_t i = 0; i < lv.sorted_free.size(); ++i) {
+    s += lv.sorted_free[i];
     if (s >= k) return (int)i + 1;
   }
-  return (int)f.size();
+  return (int)lv.sorted_free.size();
 }
 
 double Engine::evaluate(const std::vector<int>& ids, Terms* terms) const {
+  // Allocation-free: k is small, so groups are de-duplicated by an O(k^2) scan instead of a map
+  // (the greedy / 1-swap searches of CPX-sized problems call this ~1e5 times per request).
   const int k = (int)ids.size();
   const int n = p_.n;
   Terms t;
@@ -62,15 +65,24 @@ double Engine::evaluate(const std::vector<int>& ids, Terms* terms) const {
     t.comm = 1.0;
   }
   for (const auto& lv : lv_) {
-    std::map<int, int> take;
-    for (int i : ids) take[lv.gid[i]] += 1;
-    t.span += (double)take.size() - min_groups(lv, k);
-    for (const auto& kv : take) {
-      const int g = kv.first;
-      const int after = lv.free[g] - kv.second;
+    int touched = 0;
+    for (int a = 0; a < k; ++a) {
+      const int g = lv.gid[ids[a]];
+      bool first = true;
+      for (int b = 0; b < a; ++b)
+        if (lv.gid[ids[b]] == g) {
+          first = false;
+          break;
+        }
+      if (!first) continue;
+      int take = 1;
+      for (int b = a + 1; b < k; ++b) take += lv.gid[ids[b]] == g;
+      ++touched;
+      const int after = lv.free[g] - take;
       if (lv.free[g] == lv.size[g] && after > 0) t.frag += 1;
       t.fit += (double)after / lv.size[g];
     }
+    t.span += (double)touched - min_groups(lv, k);
   }
   double acc = 0;
   for (int i : ids) acc += p_.access[i];

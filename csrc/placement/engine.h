@@ -75,7 +75,7 @@ class Engine {
     std::vector<int> gid;      // dense group id per device
     std::vector<int> size;     // devices per group
     std::vector<int> free;     // free devices per group
-    int min_groups_k = 0;      // groups needed to host k (filled per query)
+    std::vector<int> sorted_free;  // `free`, descending (min_groups)
   };
   int min_groups(const Level& lv, int k) const;
   void greedy(int k, const std::vector<int>& free_ids, std::vector<int>* best, double* best_j, bool maximise) const;

@@ -53,7 +53,7 @@ def test_worst_bounded_on_cpx_and_choose_subset_fast():
     assert w.objective > select(t, 8).objective
     t0 = time.perf_counter()
     ch = choose_subset(8, topology=t, visible=64)
-    assert time.perf_counter() - t0 < 1.0 and ch.worst is not None and ch.extra["worst_exact"] is False
+    assert time.perf_counter() - t0 < 0.1 and ch.worst is not None and ch.extra["worst_exact"] is False
 
 
 @settings(max_examples=40, deadline=None)
