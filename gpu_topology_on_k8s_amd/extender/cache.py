@@ -95,7 +95,6 @@ class ClusterCache:
         self._epoch = 0
         self._overlay_epoch: Dict[Tuple[str, str], int] = {}
         self.informer = None
-        self._pending_pod_list: Optional[List[dict]] = None
 
     # ------------------------------------------------------------------ node objects
     def _state(self, name: str) -> NodeState:
@@ -218,9 +217,12 @@ class ClusterCache:
             n = pod_node(p)
             if n:
                 by_node.setdefault(n, []).append(p)
-        for st in self.nodes():
+        with self._lock:
+            names = set(self._nodes) | set(by_node)  # a pod LIST may land before the node LIST
+        for name in names:
+            st = self._state(name)
             with st.lock:
-                self._rebuild(st, by_node.get(st.name, []), epoch)
+                self._rebuild(st, by_node.get(name, []), epoch)
 
     def sync_all(self) -> None:
         """Cluster-wide LIST of nodes + pods (polling mode, or the informer's safety resync).
@@ -246,15 +248,7 @@ class ClusterCache:
     def on_list(self, kind: str, items: List[dict]) -> None:
         if kind == "Node":
             self.replace_nodes(items)
-            with self._lock:
-                pods = self._pending_pod_list
-                self._pending_pod_list = None
-            if pods is not None:  # pods listed before their nodes existed here
-                self.replace_pods(pods)
         elif kind == "Pod":
-            if not self._nodes:
-                with self._lock:
-                    self._pending_pod_list = items
             self.replace_pods(items)
         with self._lock:
             self._last_full = self.clock()
@@ -279,7 +273,9 @@ class ClusterCache:
             except Exception as e:
                 log.warning("cache sync failed: %s", e)
         st = self.update_node_object(node_obj) if node_obj is not None else self._state(name)
-        if sync and st.synced_at == 0.0:  # node unknown to the last sync (e.g. just created): read it directly
+        # node unknown to the last sync (e.g. just created): read it directly.  An informer's view is
+        # authoritative: a node it has not delivered yet simply has no topology for now
+        if sync and st.synced_at == 0.0 and not self.informed():
             try:
                 self.refresh_node(name)
             except Exception as e:
