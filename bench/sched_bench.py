@@ -9,9 +9,12 @@ Fig. 10 reports the mean scheduling time (2.53-3.56 s with Gaia on k8s 1.9).  He
 is a real pass through the in-process cluster: mini-scheduler -> HTTP extender (filter, sort, bind)
 -> apiserver annotations -> kubelet GetPreferredAllocation + Allocate over gRPC -> device plugin.
 ``sched_ms`` covers filter+sort+bind (the paper's scheduling time); ``admit_ms`` the kubelet side.
-Exp. 2 (fractional 0.5/0.4/0.1 GPUs) has no Kubernetes extended-resource form (integers only), so it
-is reported from the placement core's Fragment policy directly.
-A second section times the exact policy on an 8x MI355X node (the case this framework targets).
+Exp. 2 (fractional 0.5/0.4/0.1 GPUs) runs twice: through the placement core's Fragment policy on
+the Fig. 7 tree, and through the cluster as XCP partitions of one GPU (``<prefix>/gpu-fraction``
+on a 4-GPU node exposing 10 partitions per GPU: 0.4 GPU = 4 partitions).
+A second section times the exact policy on an 8x MI355X node (the case this framework targets), and
+the sort fan-out over a 1024-node cluster with the polling cache and with the LIST+WATCH informer
+(counting the LIST calls the steady state makes).
 """
 from __future__ import annotations
 
@@ -84,6 +87,35 @@ def exp2_fragments(reps: int):
             "note": "fractional GPUs have no k8s extended-resource form; placement core only (MI355X: XCP partitions)"}
 
 
+def exp2_xcp_cluster(reps: int):
+    """Gaia Table II through /filter, /sort, /bind, GetPreferredAllocation and Allocate: 0.5 of gpu2
+    is held (5 of its 10 partitions), then a 0.4-GPU pod, then a 0.1-GPU pod."""
+    from gpu_topology_on_k8s_amd.k8s import Contract
+    from gpu_topology_on_k8s_amd.k8s.objects import make_pod
+
+    c0 = Contract()
+    tally = collections.Counter()
+    sched = []
+    t = Topology.full_mesh(n=4, numa_split=1, partitions_per_gpu=10, node_name="p4")
+    with SimCluster({"p4": t}) as c:
+        for i in range(reps):
+            c.api.create_pod(make_pod(f"half{i}", gpus=5, node="p4", annotations=PodAssignment(list(range(20, 25)), True, 1)
+                                      .to_annotations()))
+            c.submit(f"a{i}", 4, annotations={c0.fraction_key: "0.4"})
+            (ra,) = c.schedule_pending()
+            c.submit(f"b{i}", 1, annotations={c0.fraction_key: "0.1"})
+            (rb,) = c.schedule_pending()
+            gpu = lambda r: sorted({d // 10 for d in r.allocated})  # noqa: E731
+            tally[(tuple(gpu(ra)), tuple(gpu(rb)))] += 1
+            sched += [ra.sched_ms, rb.sched_ms]
+            for n in (f"a{i}", f"b{i}"):
+                c.delete(n)
+            c.api.delete_pod("default", f"half{i}")
+    return {"experiment": "exp2-xcp-cluster", "reps": reps, "partitions_per_gpu": 10,
+            "table": {f"0.4->gpu{','.join(map(str, a))}, 0.1->gpu{','.join(map(str, b))}": n for (a, b), n in tally.items()},
+            "sched_ms_mean": statistics.mean(sched), "paper_sched_s": PAPER_SCHED_S["exp2"]}
+
+
 def scale_prioritize(n_nodes: int, pods: int = 20, k: int = 4):
     """kube-scheduler's sort fan-out on a large cluster: one pending k-GPU pod x every node, repeated
     for `pods` same-size pods (no binds in between), extender called in process (no HTTP) so the
@@ -103,17 +135,32 @@ def scale_prioritize(n_nodes: int, pods: int = 20, k: int = 4):
         api.create_node(make_node(n, labels={c.label_model: "MI355X"}, annotations=encode_node_annotations(t, c),
                                   capacity={c.resource_name: "8"}))
     out = {"experiment": f"scale-prioritize-{n_nodes}-nodes", "nodes": n_nodes, "request_gpus": k, "pods": pods}
-    for cache in (0, 4096):
-        ext = TopologyExtender(api, ExtenderConfig(resync_s=60.0, decision_cache=cache))
+    from gpu_topology_on_k8s_amd.k8s.informer import Informer
+
+    for mode, cache in (("cache_off", 0), ("cache_on", 4096), ("informer", 4096)):
+        ext = TopologyExtender(api, ExtenderConfig(resync_s=60.0 if mode != "informer" else 0.0, decision_cache=cache))
+        inf = None
+        sync_ms = None
+        if mode == "informer":
+            t0 = time.perf_counter()
+            inf = Informer(api, ext.cache.on_list, ext.cache.on_event, watch_timeout=30.0)
+            ext.cache.attach_informer(inf)
+            inf.start()
+            inf.wait_synced(60)
+            sync_ms = round((time.perf_counter() - t0) * 1e3, 2)
         ms = []
+        lists_before = api.calls.get("list_pods", 0) + api.calls.get("list_nodes", 0)
         for i in range(pods):
-            pod = api.create_pod(make_pod(f"p{cache}-{i}", gpus=k))
+            pod = api.create_pod(make_pod(f"p{mode}-{i}", gpus=k))
             t0 = time.perf_counter()
             ext.prioritize(pod, names)
             ms.append((time.perf_counter() - t0) * 1e3)
-        key = "cache_on" if cache else "cache_off"
-        out[key] = {"first_ms": round(ms[0], 2), "steady_ms_mean": round(statistics.mean(ms[1:]), 2),
-                    "steady_us_per_node": round(1e3 * statistics.mean(ms[1:]) / n_nodes, 2)}
+        lists = api.calls.get("list_pods", 0) + api.calls.get("list_nodes", 0) - lists_before
+        out[mode] = {"first_ms": round(ms[0], 2), "steady_ms_mean": round(statistics.mean(ms[1:]), 2),
+                     "steady_us_per_node": round(1e3 * statistics.mean(ms[1:]) / n_nodes, 2), "list_calls": lists}
+        if sync_ms is not None:
+            out[mode]["initial_sync_ms"] = sync_ms
+            inf.stop()
     return out
 
 
@@ -128,6 +175,7 @@ def main() -> int:
         run_exp("exp1-1gpu", 1, (), a.reps),
         run_exp("exp1-2gpu", 2, (), a.reps),
         exp2_fragments(a.reps),
+        exp2_xcp_cluster(max(20, a.reps // 10)),
         run_exp("exp3", 1, (2,), a.reps),
         run_exp("exp4", 2, (2,), a.reps),
         run_exp("mi355x-exact-4gpu", 4, (), max(50, a.reps // 5), policy="exact", topo_fn=lambda: fx.f7_mi355x(76.5, 0.03, 1)),

@@ -256,8 +256,7 @@ class TopologyExtender:
                 return None, str(e)
             us = (time.perf_counter() - t0) * 1e6
             return Decision(node=name, ids=ids, score=score, objective=obj,
-                            policy="fragment" if fraction is not None else self.cfg.policy_name, micros=us,
-                            cpuset=recommended_cpuset(t, ids)), ""
+                            policy="fragment" if fraction is not None else self.cfg.policy_name, micros=us), ""
 
     def _node_eval(self, pod: Dict[str, Any], name: str, node_obj: Optional[dict], k: int) -> Tuple[Optional[Decision], str]:
         st = self.cache.get(name, node_obj)  # may sync the cache: never call with a node lock held
@@ -331,6 +330,7 @@ class TopologyExtender:
                 d, why = self._eval_state(pod, node, st, k)
                 if d is None:
                     raise NoFeasiblePlacement(f"bind {namespace}/{name} on {node}: {why}")
+                d.cpuset = recommended_cpuset(st.topology, d.ids)
                 key = pod_key(pod)
                 now = self.clock()
                 pa = PodAssignment.assumed(d.ids, now)

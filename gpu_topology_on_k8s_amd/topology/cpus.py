@@ -62,6 +62,10 @@ def format_cpulist(cpus: Iterable[int]) -> str:
 def device_core_slices(topo) -> Dict[int, Set[int]]:
     """Disjoint core slice per device: devices sharing a ``local_cpulist`` split each of its ranges
     into equal consecutive chunks in device order (chunk sizes differ by at most one core)."""
+    key = tuple(g.cpu_affinity for g in topo.gpus)
+    memo = getattr(topo, "_core_slices", None)
+    if memo is not None and memo[0] == key:
+        return memo[1]
     groups: Dict[str, List[int]] = {}
     for g in topo.gpus:
         if g.cpu_affinity:
@@ -74,6 +78,10 @@ def device_core_slices(topo) -> Dict[int, Set[int]]:
             for j, d in enumerate(devs):
                 lo, hi = a + (n * j) // m, a + (n * (j + 1)) // m
                 out[d].update(range(lo, hi))
+    try:
+        topo._core_slices = (key, out)
+    except AttributeError:  # pragma: no cover - slotted stand-ins
+        pass
     return out
 
 
