@@ -115,7 +115,7 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
                             "image": image,
                             "command": ["python3", "-m", "gpu_topology_on_k8s_amd.deviceplugin",
                                         f"--resource-name={resource}", f"--probe={probe}", "--discovery=auto",
-                                        "--reprobe-interval=3600", f"--metrics-port={PLUGIN_METRICS_PORT}"],
+                                        "--reprobe-interval=3600", "--prestart-validate", f"--metrics-port={PLUGIN_METRICS_PORT}"],
                             "ports": [{"containerPort": PLUGIN_METRICS_PORT, "name": "metrics"}],
                             "env": [{"name": "NODE_NAME", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}},
                                     {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}],

@@ -52,6 +52,8 @@ def main(argv=None) -> int:
     ap.add_argument("--device-specs", default="auto", choices=["auto", "strict", "stub"],
                     help="Allocate DeviceSpecs: strict = kfd + render/card nodes, fail if missing; stub = only nodes "
                          "that exist under --dev-root (kind / fake GPUs); auto = stub for --discovery fake, else strict")
+    ap.add_argument("--prestart-validate", action="store_true",
+                    help="validate every placement with an RCCL all-reduce over the container's devices before it starts")
     ap.add_argument("--metrics-port", type=int, default=0, help="serve Prometheus /metrics on this port (0 = off)")
     ap.add_argument("--metrics-host", default="0.0.0.0")
     ap.add_argument("--health-interval", type=float, default=10.0)
@@ -87,7 +89,7 @@ def main(argv=None) -> int:
 
     specs = a.device_specs if a.device_specs != "auto" else ("stub" if a.discovery == "fake" else "strict")
     cfg = PluginConfig(resource_name=a.resource_name, socket_dir=a.socket_dir, socket_name=a.socket_name, dev_root=a.dev_root,
-                       node_name=a.node_name, contract=contract, device_specs=specs,
+                       node_name=a.node_name, contract=contract, device_specs=specs, prestart_validate=a.prestart_validate,
                        health_interval=a.health_interval, reprobe_interval=a.reprobe_interval,
                        reprobe_tolerance=a.reprobe_tolerance,
                        policy=PlacementPolicy(partition_aware=a.partition_aware == "on"))

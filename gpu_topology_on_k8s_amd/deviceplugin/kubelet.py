@@ -187,6 +187,16 @@ class FakeKubelet:
             missing = [d.host_path for c in resp.container_responses for d in c.devices if not os.path.exists(d.host_path)]
             if missing:
                 raise AdmissionError(f"CreateContainerError: device nodes do not exist on the node: {missing}")
+            if getattr(p.options, "pre_start_required", False):
+                # the kubelet calls PreStartContainer per container before starting it; an error
+                # there fails the container start
+                pos = 0
+                for n in split:
+                    try:
+                        self._stub(p, "PreStartContainer")(pb.PreStartContainerRequest(devices_ids=chosen[pos:pos + n]), timeout=300)
+                    except grpc.RpcError as e:
+                        raise AdmissionError(f"PreStartContainer failed: {e.details()}") from e
+                    pos += n
             self.allocated[resource][key] = tuple(chosen)
             self.responses[key] = resp
         if self.api is not None and hasattr(self.api, "set_pod_phase"):

@@ -37,6 +37,10 @@ class PluginMetrics:
         self.reprobes = Counter("gtk_plugin_reprobes_total", "idle-time link re-measurements by result", ["result"], registry=r)
         self.node_publishes = Counter("gtk_plugin_node_publishes_total", "node annotation PATCHes by outcome", ["outcome"],
                                       registry=r)
+        self.validations = Counter("gtk_plugin_placement_validations_total", "PreStartContainer RCCL validations by result",
+                                   ["result"], registry=r)
+        self.validate_seconds = Histogram("gtk_plugin_placement_validation_seconds", "PreStartContainer validation time",
+                                          buckets=(0.5, 1, 2, 5, 10, 30, 60, 120), registry=r)
         self.annotation_bytes = Gauge("gtk_plugin_topology_annotation_bytes", "encoded size of the published node annotations",
                                       registry=r)
 

@@ -22,6 +22,7 @@ extender (no GROUP) is annotated with what the kubelet gave it so the extender s
 """
 from __future__ import annotations
 
+import json
 import logging
 import os
 import threading
@@ -125,7 +126,8 @@ class PluginConfig:
                  node_name: str = "", contract: Optional[Contract] = None, health_interval: float = 5.0,
                  publish_node: bool = True, pass_rccl_env: bool = True, policy: PlacementPolicy = PlacementPolicy(),
                  resource_aliases: Sequence[str] = ("aliyun.com/gpu", "aliyun.com/gpu-count"),
-                 reprobe_interval: float = 0.0, reprobe_tolerance: float = 0.15, device_specs: str = "strict"):
+                 reprobe_interval: float = 0.0, reprobe_tolerance: float = 0.15, device_specs: str = "strict",
+                 prestart_validate: bool = False, validate_timeout: float = 120.0):
         self.resource_name = resource_name
         self.socket_dir = socket_dir
         self.socket_name = socket_name
@@ -149,6 +151,11 @@ class PluginConfig:
         if device_specs not in ("strict", "stub"):
             raise ValueError(f"device_specs must be strict|stub, got {device_specs!r}")
         self.device_specs = device_specs
+        # flow step 8: before the container starts, an RCCL all-reduce over exactly
+        # the allocated devices (kubelet PreStartContainer) validates the placement; the measured
+        # bus bandwidth is recorded on the pod
+        self.prestart_validate = prestart_validate
+        self.validate_timeout = validate_timeout
 
     @property
     def socket_path(self) -> str:
@@ -158,8 +165,10 @@ class PluginConfig:
 class DevicePluginServer:
     def __init__(self, topology: Topology, config: Optional[PluginConfig] = None, api: Optional[KubeAPI] = None,
                  health_fn: Optional[Callable[[Topology], Dict[int, bool]]] = None, clock: Callable[[], float] = time.time,
-                 reprobe_fn: Optional[Callable[[], Optional[Topology]]] = None):
+                 reprobe_fn: Optional[Callable[[], Optional[Topology]]] = None,
+                 validate_fn: Optional[Callable[[Sequence[int]], Dict[str, object]]] = None):
         self.cfg = config or PluginConfig()
+        self.validate_fn = validate_fn or self._validate_in_child
         self.topology = topology
         self.api = api
         self.health_fn = health_fn
@@ -309,7 +318,7 @@ class DevicePluginServer:
 
     # ------------------------------------------------------------------ gRPC handlers
     def GetDevicePluginOptions(self, request, context):
-        return pb.DevicePluginOptions(pre_start_required=False, get_preferred_allocation_available=True)
+        return pb.DevicePluginOptions(pre_start_required=self.cfg.prestart_validate, get_preferred_allocation_available=True)
 
     def ListAndWatch(self, request, context):
         last = -1
@@ -397,7 +406,70 @@ class DevicePluginServer:
         return resp
 
     def PreStartContainer(self, request, context):
+        """Placement validation (flow step 8): an exact-checked RCCL all-reduce over the container's
+        devices, in a child process (the plugin never holds HIP contexts).  A failure fails the
+        container start (the kubelet retries it) and is recorded as an Event; a success writes the
+        measured bandwidth on the pod.  A no-op unless ``prestart_validate``."""
+        if not self.cfg.prestart_validate:
+            return pb.PreStartContainerResponse()
+        ids = sorted({int(x) for x in request.devices_ids})
+        t0 = time.perf_counter()
+        try:
+            res = self.validate_fn(ids)
+        except Exception as e:  # noqa: BLE001 - reported to the kubelet below
+            res = {"ok": False, "error": str(e)}
+        self.metrics.validate_seconds.observe(time.perf_counter() - t0)
+        ok = bool(res.get("ok")) and int(res.get("wrong", 0)) == 0
+        self.metrics.validations.labels("ok" if ok else "failed").inc()
+        pod = self._assigned_pod(ids)
+        if not ok:
+            msg = f"RCCL validation of devices {ids} failed: {res.get('error') or str(res.get('wrong')) + ' wrong elements'}"
+            record_event(self.api, pod if pod is not None else {"kind": "Node", "metadata": {"name": self.cfg.node_name}},
+                         "FailedGPUPlacementValidation", msg, "Warning", component="gpu-topology-device-plugin",
+                         host=self.cfg.node_name)
+            context.abort(grpc.StatusCode.FAILED_PRECONDITION, msg)
+        if pod is not None and self.api is not None:
+            md = meta(pod)
+            ann = {self.cfg.contract.validated_key: json.dumps(
+                {k: res[k] for k in ("k", "peak_bytes", "peak_algbw_gbps", "peak_busbw_gbps") if k in res}, separators=(",", ":"))}
+            try:
+                self.api.patch_pod_annotations(md.get("namespace", "default"), md["name"], ann)
+            except Exception as e:  # noqa: BLE001 - the validation passed; the record is best effort
+                log.warning("recording validation on %s failed: %s", md.get("name"), e)
         return pb.PreStartContainerResponse()
+
+    def _assigned_pod(self, ids: Sequence[int]) -> Optional[dict]:
+        """The live pod on this node whose confirmed GROUP is exactly ``ids`` (newest ASSUME_TIME)."""
+        best = None
+        for p in self._node_pods():
+            pa = PodAssignment.from_annotations(obj_annotations(p))
+            if pa is not None and pa.assigned and sorted(set(pa.group)) == list(ids):
+                if best is None or pa.assume_time >= best[1]:
+                    best = (p, pa.assume_time)
+        return best[0] if best else None
+
+    def _validate_in_child(self, ids: Sequence[int]) -> Dict[str, object]:
+        """``gtk validate`` over ``ids`` (node indices, resolved to HIP ordinals by PCI address) in a
+        child process: 1 MiB..64 MiB bf16 all-reduces, exact-checked; returns its summary line."""
+        import subprocess
+        import sys
+
+        bdfs = ",".join(self.topology.gpus[i].bdf for i in ids)
+        cmd = [sys.executable, "-m", "gpu_topology_on_k8s_amd", "validate", "--group", ",".join(map(str, ids)),
+               "--min-bytes", str(1 << 20), "--max-bytes", str(64 << 20), "--factor", "8", "--iters", "5", "--warmup", "2"]
+        if all(self.topology.gpus[i].bdf for i in ids):
+            cmd += ["--bdfs", bdfs]
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        try:
+            p = subprocess.run(cmd, capture_output=True, text=True, timeout=self.cfg.validate_timeout, cwd=root)
+        except subprocess.TimeoutExpired:
+            return {"ok": False, "error": f"validation timed out after {self.cfg.validate_timeout:.0f}s"}
+        lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{"summary"')]
+        if not lines:
+            return {"ok": False, "error": f"validate exited {p.returncode}: {(p.stderr or p.stdout).strip()[-300:]}"}
+        out = json.loads(lines[-1])
+        out["ok"] = p.returncode == 0
+        return out
 
     # ------------------------------------------------------------------ Allocate helpers
     def device_nodes(self, ids: Sequence[int]) -> List[Tuple[str, str]]:
@@ -547,7 +619,7 @@ class DevicePluginServer:
             call = ch.unary_unary(f"/{pb.REGISTRATION_SERVICE}/Register", request_serializer=pb.RegisterRequest.SerializeToString,
                                   response_deserializer=pb.Empty.FromString)
             call(pb.RegisterRequest(version=pb.VERSION, endpoint=self.cfg.socket_name, resource_name=self.cfg.resource_name,
-                                    options=pb.DevicePluginOptions(pre_start_required=False,
+                                    options=pb.DevicePluginOptions(pre_start_required=self.cfg.prestart_validate,
                                                                    get_preferred_allocation_available=True)),
                  timeout=timeout)
         self.registered += 1

@@ -70,6 +70,12 @@ class Contract:
         return f"{self.prefix}/cpuset"
 
     @property
+    def validated_key(self) -> str:
+        """Pod annotation: the RCCL all-reduce that validated the placement before the container
+        started (device plugin PreStartContainer): k, peak size, algBW / busBW."""
+        return f"{self.prefix}/validated-allreduce"
+
+    @property
     def numa_pref_key(self) -> str:
         """Pod annotation: NUMA node(s) the pod's host threads live on (CPU-affinity tie-break input)."""
         return f"{self.prefix}/numa-preference"

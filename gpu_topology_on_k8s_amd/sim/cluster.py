@@ -185,9 +185,12 @@ class _Node:
 class SimCluster:
     def __init__(self, nodes: Dict[str, Topology], resource: str = "amd.com/gpu", policy_name: str = "exact",
                  policy: PlacementPolicy = PlacementPolicy(), assume_ttl: float = 300.0, use_filter: bool = True,
-                 node_labels: Optional[Dict[str, Dict[str, str]]] = None, device_specs: str = "strict"):
+                 node_labels: Optional[Dict[str, Dict[str, str]]] = None, device_specs: str = "strict",
+                 prestart_validate: bool = False, validate_fn=None):
         self.resource = resource
         self.device_specs = device_specs
+        self.prestart_validate = prestart_validate
+        self.validate_fn = validate_fn
         self.contract = Contract(resource_name=resource)
         self.api = FakeAPIServer()
         self.ext_cfg = ExtenderConfig(contract=self.contract, policy_name=policy_name, policy=policy, assume_ttl=assume_ttl,
@@ -216,7 +219,9 @@ class SimCluster:
                 os.makedirs(dev_root, exist_ok=True)
             plugin = DevicePluginServer(topo, PluginConfig(resource_name=self.resource, socket_dir=sockdir, node_name=name,
                                                            contract=self.contract, dev_root=dev_root,
-                                                           device_specs=self.device_specs), api=self.api)
+                                                           device_specs=self.device_specs,
+                                                           prestart_validate=self.prestart_validate),
+                                        api=self.api, validate_fn=self.validate_fn)
             plugin.start()
             kubelet.wait_for(self.resource)
             self.nodes[name] = _Node(name, topo, sockdir, kubelet, plugin)

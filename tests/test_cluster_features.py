@@ -417,3 +417,36 @@ def test_fragmentation_gauges():
     assert 'gtk_extender_node_fragmentation{node="n1"} 0.25' in text
     assert 'gtk_extender_node_free_devices{node="n1"} 4.0' in text
     assert 'gtk_extender_placeable_nodes{k="8"} 0.0' in text and 'gtk_extender_placeable_nodes{k="4"} 1.0' in text
+
+
+# ---------------------------------------------------------------------------------- flow step 8
+def test_prestart_validation_records_busbw_on_the_pod():
+    """PreStartContainer runs the placement validator on exactly the allocated devices; its result
+    lands on the pod, and a failing validation fails the container start with an Event."""
+    import json as _json
+
+    from gpu_topology_on_k8s_amd.deviceplugin import AdmissionError
+
+    seen = []
+
+    def fake_validate(ids):
+        seen.append(list(ids))
+        if len(ids) == 3:
+            return {"ok": False, "wrong": 17}
+        return {"ok": True, "wrong": 0, "k": len(ids), "peak_bytes": 64 << 20, "peak_algbw_gbps": 60.0,
+                "peak_busbw_gbps": 60.0 * 2 * (len(ids) - 1) / len(ids)}
+
+    with SimCluster({"n1": fx.f7_mi355x()}, prestart_validate=True, validate_fn=fake_validate) as c:
+        assert c.nodes["n1"].kubelet.options(C.resource_name).pre_start_required
+        c.submit("pair", 2)
+        r = c.schedule_pending()[0]
+        assert r.error == "" and seen == [sorted(r.allocated)]
+        v = _json.loads(c.api.get_pod("default", "pair")["metadata"]["annotations"][C.validated_key])
+        assert v["k"] == 2 and v["peak_busbw_gbps"] == 60.0
+        c.submit("bad", 3)
+        with pytest.raises(AdmissionError, match="validation"):
+            c.schedule_pending()
+        assert any(e["reason"] == "FailedGPUPlacementValidation" for e in c.api.events)
+        text = c.nodes["n1"].plugin.metrics.exposition().decode()
+        assert 'gtk_plugin_placement_validations_total{result="ok"} 1.0' in text
+        assert 'gtk_plugin_placement_validations_total{result="failed"} 1.0' in text

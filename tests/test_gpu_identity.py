@@ -93,3 +93,20 @@ def test_bench_under_hip_visible_devices_keeps_probe():
     cfg = out["config"]
     assert cfg["probed"] is True and "mesh" not in cfg["topology_source"], cfg
     assert cfg["hip_devices"] == [0] and out["link_probe"]["hbm_copy_gbps"][cfg["subset"][0]] > 500
+
+
+def test_prestart_validation_on_real_node():
+    """Flow step 8 on MI355X: kubelet PreStartContainer -> the plugin runs `gtk validate` in a child
+    over the allocated device (GROUP -> HIP ordinal by PCI address) and records RCCL's result."""
+    from gpu_topology_on_k8s_amd.k8s import Contract
+    from gpu_topology_on_k8s_amd.sim import SimCluster
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
+
+    t = discover("auto")
+    t.node_name = "gpu-node"
+    with SimCluster({"gpu-node": t}, prestart_validate=True) as c:
+        c.submit("validated", 1)
+        r = c.schedule_pending()[0]
+        assert r.error == "" and len(r.allocated) == 1
+        v = json.loads(c.api.get_pod("default", "validated")["metadata"]["annotations"][Contract().validated_key])
+        assert v["k"] == 1 and v["peak_algbw_gbps"] > 100
