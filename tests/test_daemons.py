@@ -116,3 +116,57 @@ def test_extender_daemon_serves_the_reference_endpoint():
     finally:
         _stop(p)
         srv.shutdown()
+
+
+def test_both_daemons_config4_through_shipped_processes():
+    """BASELINE config 4 with the shipped entry points only: the device-plugin daemon (fake 8-GPU node,
+    stub DeviceSpecs) publishes to the apiserver and registers with the kubelet; the extender daemon
+    (LIST+WATCH informer) answers /filter, /sort and /bind; two 4-GPU pods land on disjoint NUMA halves
+    and the kubelet admits both."""
+    api = FakeAPIServer()
+    api.create_node(make_node("worker-1"))
+    srv, url = serve_http(api)
+    sockdir = tempfile.mkdtemp(prefix="gtkd", dir="/tmp")
+    devroot = os.path.join(sockdir, "dev")
+    os.makedirs(devroot)
+    kubelet = FakeKubelet(sockdir, node_name="worker-1", api=api)
+    kubelet.start()
+    port = _free_port()
+    plug = _spawn(["gpu_topology_on_k8s_amd.deviceplugin", "--discovery", "fake", "--fake-gpus", "8", "--apiserver", url,
+                   "--node-name", "worker-1", "--socket-dir", sockdir, "--dev-root", devroot, "--log-level", "WARNING"])
+    ext = _spawn(["gpu_topology_on_k8s_amd.extender", "--apiserver", url, "--port", str(port), "--log-level", "WARNING"])
+    base = f"http://127.0.0.1:{port}/gputopology-scheduler"
+    try:
+        kubelet.wait_for("amd.com/gpu", timeout=60)
+
+        def up():
+            try:
+                return requests.get(base + "/healthz", timeout=1).ok
+            except requests.RequestException:
+                return False
+
+        assert _wait(up, 60), "extender did not come up"
+        assert _wait(lambda: requests.post(base + "/filter", json={"Pod": make_pod("probe", gpus=8), "NodeNames": ["worker-1"]},
+                                           timeout=5).json()["NodeNames"] == ["worker-1"], 30)  # informer saw the topology
+        got = []
+        for name in ("a", "b"):
+            pod = api.create_pod(make_pod(name, gpus=4))
+            names = requests.post(base + "/filter", json={"Pod": pod, "NodeNames": ["worker-1"]}, timeout=10).json()["NodeNames"]
+            hp = requests.post(base + "/sort", json={"Pod": pod, "NodeNames": names}, timeout=10).json()
+            br = requests.post(base + "/bind", json={"PodName": name, "PodNamespace": "default", "PodUID": pod["metadata"]["uid"],
+                                                     "Node": hp[0]["Host"]}, timeout=10).json()
+            assert br["Error"] == "", br
+            kubelet.admit(api.get_pod("default", name), "amd.com/gpu")
+            got.append(set(br["Devices"]))
+        assert {frozenset(g) for g in got} == {frozenset(range(4)), frozenset(range(4, 8))}
+        for name in ("a", "b"):
+            ann = api.get_pod("default", name)["metadata"]["annotations"]
+            assert ann["ALIYUN_COM_GPU_ASSIGNED"] == "true" and ann[Contract().cpuset_key]
+        assert any(e["reason"] == "GPUTopologyBound" for e in api.events)
+    finally:
+        _stop(ext)
+        rc = _stop(plug)
+        kubelet.stop()
+        srv.shutdown()
+        shutil.rmtree(sockdir, ignore_errors=True)
+    assert rc == 0
