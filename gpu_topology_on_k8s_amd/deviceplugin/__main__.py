@@ -19,7 +19,7 @@ import threading
 from ..k8s.annotations import Contract
 from ..placement import PlacementPolicy
 from ..topology.discovery import discover
-from .health import HealthMonitor
+from .health import HealthMonitor, HealthPolicy
 from .plugin import DevicePluginServer, PluginConfig, startup_topology
 from .proto import DEVICE_PLUGIN_PATH
 
@@ -52,6 +52,9 @@ def main(argv=None) -> int:
     ap.add_argument("--device-specs", default="auto", choices=["auto", "strict", "stub"],
                     help="Allocate DeviceSpecs: strict = kfd + render/card nodes, fail if missing; stub = only nodes "
                          "that exist under --dev-root (kind / fake GPUs); auto = stub for --discovery fake, else strict")
+    ap.add_argument("--xgmi-link-loss", default="degrade", choices=["degrade", "unhealthy"],
+                    help="a GPU whose xGMI link drops: degrade = republish the pair at its new link class and keep the "
+                         "GPU schedulable; unhealthy = advertise the GPU Unhealthy")
     ap.add_argument("--prestart-validate", action="store_true",
                     help="validate every placement with an RCCL all-reduce over the container's devices before it starts")
     ap.add_argument("--metrics-port", type=int, default=0, help="serve Prometheus /metrics on this port (0 = off)")
@@ -85,7 +88,8 @@ def main(argv=None) -> int:
     topo, how = startup_topology(topo, api, a.node_name, contract, names, probe_fn)
     log.info("link matrix: %s; topology:\n%s", how, topo.render())
 
-    health = HealthMonitor(topo, lambda: discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus))
+    health = HealthMonitor(topo, lambda: discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus),
+                           HealthPolicy(xgmi_links=a.xgmi_link_loss == "unhealthy"))
 
     specs = a.device_specs if a.device_specs != "auto" else ("stub" if a.discovery == "fake" else "strict")
     cfg = PluginConfig(resource_name=a.resource_name, socket_dir=a.socket_dir, socket_name=a.socket_name, dev_root=a.dev_root,

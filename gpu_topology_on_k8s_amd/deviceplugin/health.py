@@ -14,12 +14,21 @@ look at, read by discovery (``csrc/topo/topo_reader.cpp``: amdsmi, or amdgpu sys
 
 A device that recovers (e.g. links retrain) becomes Healthy again on the next poll.  Signals a node
 cannot read (``-1``: unsupported, or no root) are ignored rather than treated as failures.
+
+A lost xGMI link need not take the GPU out of service (``HealthPolicy(xgmi_links=False)``, the
+daemon's ``--xgmi-link-loss degrade``): :meth:`HealthMonitor.relink` rebuilds the published model
+with the re-discovered link class and hop count of every pair that changed, drops those pairs'
+stale probe measurements, and the plugin republishes it — the extender then prices the pair at its
+new class (e.g. PCIe across sockets, 8x a nominal xGMI link) and steers multi-GPU sets around it.
 """
 from __future__ import annotations
 
+import copy
 import logging
 from dataclasses import dataclass
-from typing import Callable, Dict, List, Tuple
+from typing import Callable, Dict, List, Optional, Tuple
+
+import numpy as np
 
 from ..topology.model import GPUInfo, Topology
 
@@ -59,6 +68,7 @@ class HealthMonitor:
         self.discover_fn = discover_fn
         self.policy = policy
         self.reasons: Dict[int, List[str]] = {}
+        self.last: Optional[Topology] = None  # the latest re-discovery
 
     def evaluate(self, fresh: Topology) -> Dict[int, Tuple[bool, List[str]]]:
         now = {g.index: g for g in fresh.gpus}
@@ -69,8 +79,29 @@ class HealthMonitor:
             out[idx] = (not probs, probs)
         return out
 
+    def relink(self, current: Topology) -> Optional[Topology]:
+        """``current`` with the link class / hops of the last re-discovery wherever they changed (and
+        those pairs' measurements dropped), or None when no pair changed."""
+        fresh = self.last
+        if fresh is None or fresh.n != current.n:
+            return None
+        changed = (fresh.link_type != current.link_type) | (fresh.hops != current.hops)
+        np.fill_diagonal(changed, False)
+        if not changed.any():
+            return None
+        new = copy.deepcopy(current)
+        new.link_type = fresh.link_type.copy()
+        new.hops = fresh.hops.copy()
+        bw = new.bw_gbps.copy()
+        bw[changed] = np.nan
+        pairs = [(int(i), int(j)) for i, j in zip(*np.nonzero(np.triu(changed)))]
+        log.warning("link class changed for pairs %s: republishing without their stale measurements", pairs)
+        new.set_measured_bw(bw, dict(new.probe, relinked=pairs) if new.probe else {"relinked": pairs})
+        return new
+
     def __call__(self, topo: Topology) -> Dict[int, bool]:
-        res = self.evaluate(self.discover_fn())
+        self.last = self.discover_fn()
+        res = self.evaluate(self.last)
         for idx, (ok, probs) in res.items():
             if probs != self.reasons.get(idx, []):
                 if probs:

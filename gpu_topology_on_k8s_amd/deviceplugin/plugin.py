@@ -664,6 +664,16 @@ class DevicePluginServer:
                 try:
                     for idx, ok in self.health_fn(self.topology).items():
                         self.set_health(int(idx), bool(ok))
+                    relink = getattr(self.health_fn, "relink", None)
+                    new = relink(self.topology) if relink is not None else None
+                    if new is not None:  # a link retrained at another class / went down: republish
+                        for g in new.gpus:
+                            g.healthy = self._health.get(g.index, True)
+                        self.update_topology(new)
+                        if self.api is not None and self.cfg.node_name:
+                            record_event(self.api, {"kind": "Node", "metadata": {"name": self.cfg.node_name}}, "GPULinkChanged",
+                                         f"link class changed for pairs {new.probe.get('relinked')}", "Warning",
+                                         component="gpu-topology-device-plugin", host=self.cfg.node_name)
                 except Exception as e:
                     log.warning("health check failed: %s", e)
 

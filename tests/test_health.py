@@ -64,3 +64,35 @@ def test_json_roundtrip_keeps_ras_fields():
     t.gpus[1].bad_page_threshold = 64
     u = Topology.from_json(t.to_json())
     assert u.gpus[1].ecc_uncorrectable == 5 and u.gpus[1].bad_page_threshold == 64
+
+
+def test_link_loss_degrade_republishes_pair_class():
+    """--xgmi-link-loss degrade: the GPU stays Healthy, the re-discovered pair class is republished and
+    its stale measurement dropped, so the extender prices the pair as PCIe and avoids it."""
+    import numpy as np
+
+    from gpu_topology_on_k8s_amd.deviceplugin import DevicePluginServer, PluginConfig
+    from gpu_topology_on_k8s_amd.k8s import Contract, FakeAPIServer
+    from gpu_topology_on_k8s_amd.k8s.annotations import decode_node_annotations
+    from gpu_topology_on_k8s_amd.k8s.objects import make_node
+    from gpu_topology_on_k8s_amd.placement import select
+    from gpu_topology_on_k8s_amd.topology import fixtures as fx
+    from gpu_topology_on_k8s_amd.topology.model import LinkType
+
+    topo = fx.f7_mi355x(link_gbps=70.0)
+    fresh = fx.f7_mi355x(link_gbps=70.0)
+    fresh.link_type[0, 5] = fresh.link_type[5, 0] = int(LinkType.PCIE_SYS)
+    fresh.hops[0, 5] = fresh.hops[5, 0] = 3
+    fresh.gpus[0].xgmi_links_up = fresh.gpus[5].xgmi_links_up = 6
+    mon = HealthMonitor(topo, lambda: fresh, HealthPolicy(xgmi_links=False))
+    api = FakeAPIServer()
+    api.create_node(make_node("n1"))
+    plug = DevicePluginServer(topo, PluginConfig(node_name="n1"), api=api, health_fn=mon)
+    assert all(mon(topo).values())  # nobody goes Unhealthy
+    new = mon.relink(plug.topology)
+    assert new is not None and new.probe["relinked"] == [(0, 5)] and np.isnan(new.bw_gbps[0, 5])
+    plug.update_topology(new)
+    pub = decode_node_annotations(api.get_node("n1")["metadata"]["annotations"], Contract())
+    assert LinkType(int(pub.link_type[0, 5])) == LinkType.PCIE_SYS and pub.cost[0, 5] > 4 * pub.cost[0, 1]
+    assert set(select(pub, 2, used=[1, 2, 3, 4, 6, 7]).ids) == {0, 5}  # only pair left: still schedulable
+    assert mon.relink(new) is None  # nothing changed since
