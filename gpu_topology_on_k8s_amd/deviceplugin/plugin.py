@@ -92,8 +92,9 @@ def startup_topology(discovered: Topology, api: Optional[KubeAPI], node_name: st
             prev = decode_node_annotations(obj_annotations(api.get_node(node_name)), contract, node_name=node_name)
         except Exception as e:  # noqa: BLE001 - unreadable annotation: nothing to reuse
             log.warning("reading the published topology of %s failed: %s", node_name, e)
-        if prev is not None and prev.n == discovered.n and [g.bdf for g in prev.gpus] == [g.bdf for g in discovered.gpus] \
-                and prev.bw_gbps is not None and np.isfinite(prev.bw_gbps).any():
+        measured = prev is not None and ((prev.bw_gbps is not None and np.isfinite(prev.bw_gbps).any())
+                                         or (prev.hbm_gbps is not None and np.isfinite(prev.hbm_gbps).any()))
+        if measured and prev.n == discovered.n and [g.bdf for g in prev.gpus] == [g.bdf for g in discovered.gpus]:
             discovered.hbm_gbps = prev.hbm_gbps
             discovered.set_measured_bw(prev.bw_gbps, dict(prev.probe, reused=True))
             return discovered, "reused the published matrix (devices in use: probe skipped)"

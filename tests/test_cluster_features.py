@@ -269,24 +269,37 @@ def test_informer_keeps_prioritize_free_of_lists():
         srv.shutdown()
 
 
-def test_informer_relists_after_gone():
+def test_watch_gone_over_http_and_informer_relist():
+    """A watch from a resourceVersion the apiserver's window no longer holds gets ERROR 410 on the
+    wire; RestKubeAPI raises Gone and the informer relists instead of missing events."""
+    from gpu_topology_on_k8s_amd.k8s.api import Gone
+
     api = FakeAPIServer(history=4)
     api.create_node(make_node("n0"))
-    seen = {"lists": 0}
-
-    def on_list(kind, items):
-        seen["lists"] += 1
-
-    inf = Informer(api, on_list, lambda *a: None, kinds=("Pod",), watch_timeout=0.2, backoff=0.05)
-    inf.start()
+    for i in range(10):
+        api.create_pod(make_pod(f"p{i}", gpus=0))
+    srv, url = serve_http(api)
+    rest = RestKubeAPI(url, verify=False)
     try:
-        assert inf.wait_synced(5)
-        for i in range(20):  # overflow the 4-entry window while the watch may lag
-            api.create_pod(make_pod(f"p{i}", gpus=0))
-        time.sleep(0.5)
-        assert inf.lists["Pod"] >= 1 and inf.events["Pod"] + 0 >= 0
+        with pytest.raises(Gone):
+            list(rest.watch_stream("Pod", "1", timeout=2))
+        items, rv = rest.list_with_version("Pod")
+        assert len(items) == 10 and int(rv) >= 11
+        seen = []
+        inf = Informer(rest, lambda k, items: seen.append(("list", k, len(items))), lambda t, k, o: seen.append((t, k)),
+                       kinds=("Pod",), watch_timeout=1.0, backoff=0.05)
+        inf.start()
+        try:
+            assert inf.wait_synced(10)
+            api.create_pod(make_pod("late", gpus=0))
+            deadline = time.time() + 10
+            while time.time() < deadline and ("ADDED", "Pod") not in seen:
+                time.sleep(0.05)
+            assert ("ADDED", "Pod") in seen and inf.lists["Pod"] >= 1
+        finally:
+            inf.stop()
     finally:
-        inf.stop()
+        srv.shutdown()
 
 
 # ---------------------------------------------------------------------------------- ADVICE: deadlock
