@@ -26,8 +26,30 @@ def short(name: str) -> str:
     return name.replace("void ", "")[:70]
 
 
-def stats_tables(d: str):
+def db_tables(d: str):
+    """rocprofv3 >= 7 writes a rocpd SQLite database (``*.db``) by default: its ``kernels`` view has
+    one row per dispatch (start/end in ns)."""
+    import sqlite3
+
     out = []
+    for f in sorted(glob.glob(os.path.join(d, "*.db"))):
+        c = sqlite3.connect(f)
+        cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+        if not {"name", "start", "end"} <= set(cols):
+            continue
+        rows = c.execute("select name, count(*), avg(end - start), min(end - start), max(end - start), sum(end - start) "
+                         "from kernels group by name order by sum(end - start) desc").fetchall()
+        total = sum(r[5] for r in rows) or 1
+        out.append(f"### Kernel stats: `{os.path.relpath(f)}`\n")
+        out.append("| kernel | calls | avg µs | min µs | max µs | % time |\n|---|---|---|---|---|---|")
+        for name, n, avg, mn, mx, tot in rows:
+            out.append(f"| {short(name)} | {n} | {avg / 1e3:.1f} | {mn / 1e3:.1f} | {mx / 1e3:.1f} | {100 * tot / total:.1f} |")
+        out.append("")
+    return out
+
+
+def stats_tables(d: str):
+    out = db_tables(d)
     for f in sorted(glob.glob(os.path.join(d, "*kernel_stats.csv"))):
         rows = list(csv.DictReader(open(f)))
         out.append(f"### Kernel stats: `{os.path.relpath(f)}`\n")
