@@ -99,3 +99,67 @@ def test_sysfs_host_affinity(tmp_path):
     c = fx.write_fake_kfd_sysfs(str(tmp_path / "cpx"), partitions_per_gpu=8)
     tc = from_native(load("_topo").discover_sysfs(c["kfd"], c["drm"], c["pci"], c["node"]))
     assert tc.gpus[9].cpu_affinity == "0-47,96-143"  # XCP function 1: read through function 0
+
+
+# ------------------------------------------------------------------ amdsmi backend on a stand-in library
+def _fake_amdsmi():
+    from gpu_topology_on_k8s_amd._native import binary
+
+    try:
+        return str(binary("libfake_amdsmi.so"))
+    except Exception:
+        pytest.skip("fake_amdsmi not built")
+
+
+def _amdsmi_node(monkeypatch, tmp_path, **env):
+    for k in ("FAKE_AMDSMI_GPUS", "FAKE_AMDSMI_PARTITIONS", "FAKE_AMDSMI_HIP_ORDER", "FAKE_AMDSMI_DOWN"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(f"FAKE_AMDSMI_{k.upper()}", str(v))
+    return discover("amdsmi", amdsmi_lib=_fake_amdsmi(), pci_root=str(tmp_path), node_root=str(tmp_path))
+
+
+@needs_topo
+def test_amdsmi_backend_eight_gpu_mesh(monkeypatch, tmp_path):
+    """The pairwise half of the amdsmi reader (what bench.py's rank 0 runs on the 8-GPU node)."""
+    t = _amdsmi_node(monkeypatch, tmp_path)
+    off = ~np.eye(8, dtype=bool)
+    assert t.n == 8 and t.source == "amdsmi"
+    assert (t.link_type[off] == int(LinkType.XGMI)).all() and (t.hops[off] == 1).all()
+    assert (t.weight[off] == 15).all() and t.probe["amdsmi_max_bw_mbps"][0][1] == 76800
+    assert t.numa.tolist() == [0] * 4 + [1] * 4 and all(g.xgmi_links_up == 7 for g in t.gpus)
+    assert all(g.gfx == "gfx950" and g.model == "MI355X" and g.render_minor == 128 + i for i, g in enumerate(t.gpus))
+    assert len({g.bdf for g in t.gpus}) == 8
+
+
+@needs_topo
+def test_amdsmi_backend_orders_by_hip_id_and_maps_bdfs(monkeypatch, tmp_path):
+    t = _amdsmi_node(monkeypatch, tmp_path, hip_order="3,2,1,0,4,5,6,7")
+    assert [g.bdf for g in t.gpus][:4] == ["0000:35:00.0", "0000:25:00.0", "0000:15:00.0", "0000:05:00.0"]
+    from gpu_topology_on_k8s_amd.parallel.allreduce import choose_subset
+
+    ch = choose_subset(2, topology=t, visible_bdfs=["0000:45:00.0", "0000:55:00.0"])  # HIP_VISIBLE_DEVICES=4,5
+    assert ch.devices == [4, 5] and ch.hip_devices == [0, 1]
+
+
+@needs_topo
+def test_amdsmi_backend_down_link(monkeypatch, tmp_path):
+    t = _amdsmi_node(monkeypatch, tmp_path, down="2-6")
+    assert LinkType(int(t.link_type[2, 6])) == LinkType.PCIE_SYS and t.hops[2, 6] == 2
+    assert t.gpus[2].xgmi_links_up == 6 and t.gpus[6].xgmi_links_up == 6 and t.gpus[0].xgmi_links_up == 7
+    assert t.cost[2, 6] > t.cost[2, 5]
+    from gpu_topology_on_k8s_amd.placement import select
+
+    assert set(select(t, 2, used=[0, 1, 3, 4, 5]).ids) in ({2, 7}, {6, 7})  # the down pair is avoided
+
+
+@needs_topo
+def test_amdsmi_backend_cpx(monkeypatch, tmp_path):
+    t = _amdsmi_node(monkeypatch, tmp_path, partitions=8)
+    assert t.n == 64 and t.physical.tolist() == [i // 8 for i in range(64)]
+    assert all(g.partition == "CPX" for g in t.gpus)
+    assert LinkType(int(t.link_type[0, 1])) == LinkType.INTERNAL and LinkType(int(t.link_type[0, 8])) == LinkType.XGMI
+    from gpu_topology_on_k8s_amd.k8s.annotations import annotations_size, encode_node_annotations
+
+    ann = encode_node_annotations(t)
+    assert annotations_size(ann) < 64 * 1024 and sum(k.startswith("GPUPKG_") for k in ann) == 28
