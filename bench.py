@@ -57,6 +57,9 @@ def parse(argv=None):
                          "process of rank 0; 'auto' = quick on GPUs, off for --backend cpu; a failed probe falls back "
                          "to the discovered link classes")
     ap.add_argument("--discovery", default="auto", choices=["auto", "amdsmi", "sysfs", "fake"])
+    ap.add_argument("--cpu-visible", type=int, default=0,
+                    help="--backend cpu: devices the job may place on (default: one per rank); e.g. 8 rehearses an "
+                         "N<8 job on a whole 8-GPU node")
     ap.add_argument("--via", default="k8s", choices=["k8s", "direct"],
                     help="k8s = place the k-GPU pod through device plugin (gRPC) + extender (HTTP) + kubelet Allocate "
                          "in process; direct = call the placement core")
@@ -253,7 +256,7 @@ def main(argv=None) -> int:
                 print(f"bench: link probe unavailable ({msg}); placing on discovered link classes", file=sys.stderr)
             elif msg != "ok":
                 print(f"bench: link probe: {msg}", file=sys.stderr)
-        choice = choose_subset(env.world, backend=args.discovery, visible=env.world if cpu else None, topology=topo,
+        choice = choose_subset(env.world, backend=args.discovery, visible=(args.cpu_visible or env.world) if cpu else None, topology=topo,
                                via_k8s=args.via == "k8s")
         env.store.set("gtk/subset", choice.to_json())
     choice = SubsetChoice.from_json(env.store.get("gtk/subset").decode())

@@ -83,14 +83,17 @@ def discover(
     node_name: str = "",
     sysfs_root: str = "/sys/class/kfd/kfd/topology",
     drm_root: str = "/sys/class/drm",
-    amdsmi_lib: str = "libamd_smi.so",
+    amdsmi_lib: Optional[str] = None,
     ref_gbps: float = DEFAULT_REF_GBPS,
     fake_n: Optional[int] = None,
     pci_root: str = "/sys/bus/pci/devices",
     node_root: str = "/sys/devices/system/node",
 ) -> Topology:
-    """Discover the node topology.  ``auto`` = amdsmi, then KFD sysfs; never silently fake."""
+    """Discover the node topology.  ``auto`` = amdsmi, then KFD sysfs; never silently fake.
+    ``amdsmi_lib`` defaults to ``$GTK_AMDSMI_LIB`` or ``libamd_smi.so`` (the CPU tests point it at the
+    stand-in ``bin/libfake_amdsmi.so``)."""
     node_name = node_name or os.environ.get("NODE_NAME", "") or os.uname().nodename
+    amdsmi_lib = amdsmi_lib or os.environ.get("GTK_AMDSMI_LIB", "") or "libamd_smi.so"
     if backend == "fake":
         return fake_topology(fake_n, node_name=node_name)
     errors = []

@@ -123,3 +123,23 @@ def test_bench_eight_ranks_gloo_dry_run():
     assert out["k8s_placement"]["assigned"] is True and len(out["k8s_placement"]["devices"]) == 8
     assert abs(out["busbw_gbps"] - out["algbw_gbps"] * 2 * 7 / 8) <= 1e-2 * out["busbw_gbps"] + 2e-3  # 3-decimal rounding
     assert out["size_sweep"]["all_exact"] and out["value_kind"] == "busbw"
+
+
+def test_bench_four_ranks_on_amdsmi_discovered_node():
+    """N=4 of an 8-GPU node discovered through the amdsmi reader (stand-in library): placement picks a
+    4-subset of the 8 real-shaped devices, with a worst subset, through the k8s flow."""
+    from gpu_topology_on_k8s_amd._native import binary
+
+    lib = str(binary("libfake_amdsmi.so"))
+    env = dict(os.environ, GTK_AMDSMI_LIB=lib)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "4", "--backend", "cpu", "--discovery", "amdsmi",
+                        "--steps", "2", "--warmup", "1", "--size-mb", "1", "--sweep", "off", "--cpu-visible", "8"],
+                       capture_output=True, text=True, timeout=600, cwd=REPO, env=env)
+    assert p.returncode == 0, p.stderr[-4000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    cfg = out["config"]
+    assert cfg["topology_source"].startswith("amdsmi") and len(cfg["subset"]) == 4
+    assert cfg["worst_subset"] is not None and cfg["worst_score"] < cfg["placement_score"]
+    assert out["k8s_placement"]["assigned"] is True
