@@ -7,10 +7,10 @@
 * :func:`scheduler_configuration` — the same extender as a ``KubeSchedulerConfiguration``
   (``kubescheduler.config.k8s.io/v1``) ``extenders:`` stanza for current clusters, optionally with
   the ``filter`` verb this framework adds.
-* :func:`render_manifests` — DaemonSet (device plugin, Prometheus ``/metrics`` on :32744), Deployment
-  (extender on the control-plane host network, listening on 127.0.0.1 only: kube-scheduler calls it
-  on loopback and ``/bind`` is unauthenticated, so no Service exposes it), RBAC and the scheduler
-  ConfigMap, as one multi-document YAML (``deploy/``).
+* :func:`render_manifests` — DaemonSet (device plugin, Prometheus ``/metrics`` on :32744), DaemonSet
+  (extender on every control-plane node's host network, listening on 127.0.0.1 only: each
+  kube-scheduler replica calls its own node's extender on loopback, and ``/bind`` is unauthenticated,
+  so no Service exposes it), RBAC and the scheduler ConfigMap, as one multi-document YAML (``deploy/``).
 """
 from __future__ import annotations
 
@@ -137,10 +137,12 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
         },
         {
             "apiVersion": "apps/v1",
-            "kind": "Deployment",
+            # one extender per control-plane node: every kube-scheduler replica calls ITS node's
+            # 127.0.0.1:32743 (design.md:98); leader election keeps one scheduler (hence one extender)
+            # active, and a new leader's extender rebuilds its state from the pod annotations
+            "kind": "DaemonSet",
             "metadata": {"name": "gpu-topology-scheduler-extender", "namespace": namespace, "labels": labels},
             "spec": {
-                "replicas": 1,
                 "selector": {"matchLabels": {"name": "gpu-topology-scheduler-extender"}},
                 "template": {
                     "metadata": {"labels": {"name": "gpu-topology-scheduler-extender", **labels}},
@@ -189,7 +191,7 @@ def render_kind(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, fake_gpus:
     """
     docs = list(yaml.safe_load_all(render_manifests(resource, image=image, probe="off")))
     for d in docs:
-        if d["kind"] == "DaemonSet":
+        if d["kind"] == "DaemonSet" and d["metadata"]["name"] == "amd-gpu-topology-device-plugin":
             spec = d["spec"]["template"]["spec"]
             spec["nodeSelector"] = {"gputopology.amd.com/fake-gpus": "true"}
             c = spec["containers"][0]
@@ -237,7 +239,7 @@ def render_kind(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, fake_gpus:
         f"kind load docker-image --name gpu-topology {image}",
         "kubectl apply -f gpu-topology-kind.yaml",
         "kubectl -n kube-system rollout status ds/amd-gpu-topology-device-plugin --timeout=180s",
-        "kubectl -n kube-system rollout status deploy/gpu-topology-scheduler-extender --timeout=180s",
+        "kubectl -n kube-system rollout status ds/gpu-topology-scheduler-extender --timeout=180s",
         "kubectl apply -f pod-1gpu.yaml",
         "kubectl wait --for=jsonpath='{.status.phase}'=Succeeded pod/gpu-topology-smoke --timeout=180s",
         "kubectl get pod gpu-topology-smoke -o jsonpath='{.metadata.annotations}'; echo",

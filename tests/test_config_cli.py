@@ -36,7 +36,8 @@ def test_scheduler_configuration():
 def test_manifests_are_valid_yaml():
     docs = list(yaml.safe_load_all(render_manifests()))
     kinds = [d["kind"] for d in docs]
-    assert kinds == ["ServiceAccount", "ClusterRole", "ClusterRoleBinding", "DaemonSet", "Deployment", "ConfigMap"]
+    assert kinds == ["ServiceAccount", "ClusterRole", "ClusterRoleBinding", "DaemonSet", "DaemonSet", "ConfigMap"]
+    assert docs[4]["spec"]["template"]["spec"]["nodeSelector"] == {"node-role.kubernetes.io/control-plane": ""}
     ext = docs[4]["spec"]["template"]["spec"]["containers"][0]
     assert "--host=127.0.0.1" in ext["command"] and "ports" not in ext  # /bind is never exposed off-node
     ds = docs[3]
@@ -86,7 +87,7 @@ def test_kind_manifests_config1():
 
     files = render_kind()
     docs = list(yaml.safe_load_all(files["gpu-topology-kind.yaml"]))
-    ds = [d for d in docs if d["kind"] == "DaemonSet"][0]
+    ds = [d for d in docs if d["kind"] == "DaemonSet" and d["metadata"]["name"] == "amd-gpu-topology-device-plugin"][0]
     c = ds["spec"]["template"]["spec"]["containers"][0]
     assert "--device-specs=stub" in c["command"] and "--discovery=fake" in c["command"] and "--fake-gpus=2" in c["command"]
     assert all(v["name"] == "device-plugins" for v in ds["spec"]["template"]["spec"]["volumes"])
