@@ -113,7 +113,10 @@ def main(argv=None) -> int:
         signal.signal(sig, lambda *_: done.set())
     plugin.start()
     while not done.wait(1.0):
-        pass
+        if plugin.layout_change.is_set():  # partition switch / device hot-(un)plug: restart cleanly
+            log.warning("exiting for a restart: %s", plugin.layout_change_reason)
+            plugin.stop()
+            return 75  # EX_TEMPFAIL: the DaemonSet restarts the container, which re-discovers
     plugin.stop()
     return 0
 

@@ -79,6 +79,24 @@ class HealthMonitor:
             out[idx] = (not probs, probs)
         return out
 
+    def layout_changed(self) -> Optional[str]:
+        """Why the device set itself changed since start (compute/memory partition switch, devices
+        added or removed), or None.  The advertised device IDs no longer describe the node then: the
+        plugin exits so its DaemonSet restarts it, and the new process re-discovers, re-probes (when
+        idle) and re-registers with the kubelet."""
+        fresh = self.last
+        if fresh is None:
+            return None
+        before = [(g.bdf, g.partition, g.memory_partition) for g in self.base.values()]
+        now = [(g.bdf, g.partition, g.memory_partition) for g in fresh.gpus]
+        if len(before) != len(now):
+            return f"device count {len(before)} -> {len(now)}"
+        diff = [i for i, (a, b) in enumerate(zip(before, now)) if a != b]
+        if diff:
+            i = diff[0]
+            return f"device {i}: {before[i]} -> {now[i]}" + (f" (+{len(diff) - 1} more)" if len(diff) > 1 else "")
+        return None
+
     def relink(self, current: Topology) -> Optional[Topology]:
         """``current`` with the link class / hops of the last re-discovery wherever they changed (and
         those pairs' measurements dropped), or None when no pair changed."""

@@ -189,6 +189,10 @@ class DevicePluginServer:
         self.registered = 0
         self.metrics = PluginMetrics()
         self.metrics.set_topology(topology)
+        # set when re-discovery finds a different device set (partition switch, hot removal): the
+        # daemon exits for a clean restart instead of advertising stale device IDs
+        self.layout_change = threading.Event()
+        self.layout_change_reason = ""
 
     # ------------------------------------------------------------------ device view
     def devices(self) -> List[pb.Device]:
@@ -665,6 +669,17 @@ class DevicePluginServer:
                 try:
                     for idx, ok in self.health_fn(self.topology).items():
                         self.set_health(int(idx), bool(ok))
+                    changed = getattr(self.health_fn, "layout_changed", lambda: None)()
+                    if changed:
+                        if not self.layout_change.is_set():
+                            log.warning("device layout changed (%s): restart required", changed)
+                            self.layout_change_reason = changed
+                            if self.api is not None and self.cfg.node_name:
+                                record_event(self.api, {"kind": "Node", "metadata": {"name": self.cfg.node_name}},
+                                             "GPULayoutChanged", f"{changed}; device plugin restarting", "Warning",
+                                             component="gpu-topology-device-plugin", host=self.cfg.node_name)
+                            self.layout_change.set()
+                        continue
                     relink = getattr(self.health_fn, "relink", None)
                     new = relink(self.topology) if relink is not None else None
                     if new is not None:  # a link retrained at another class / went down: republish

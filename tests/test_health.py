@@ -96,3 +96,34 @@ def test_link_loss_degrade_republishes_pair_class():
     assert LinkType(int(pub.link_type[0, 5])) == LinkType.PCIE_SYS and pub.cost[0, 5] > 4 * pub.cost[0, 1]
     assert set(select(pub, 2, used=[1, 2, 3, 4, 6, 7]).ids) == {0, 5}  # only pair left: still schedulable
     assert mon.relink(new) is None  # nothing changed since
+
+
+def test_partition_switch_requests_restart():
+    """a compute-partition switch (SPX -> CPX) changes the device set; the plugin flags a
+    restart (the daemon exits 75 so the DaemonSet restarts it) instead of advertising stale IDs."""
+    import time
+
+    from gpu_topology_on_k8s_amd.deviceplugin import DevicePluginServer, PluginConfig
+    from gpu_topology_on_k8s_amd.k8s import FakeAPIServer
+    from gpu_topology_on_k8s_amd.k8s.objects import make_node
+    from gpu_topology_on_k8s_amd.topology import fixtures as fx
+
+    state = {"topo": fx.f7_mi355x()}
+    mon = HealthMonitor(fx.f7_mi355x(), lambda: state["topo"])
+    assert mon(fx.f7_mi355x()) and mon.layout_changed() is None
+    state["topo"] = fx.f8_mi355x_cpx()
+    mon(fx.f7_mi355x())
+    assert "device count 8 -> 64" in mon.layout_changed()
+    api = FakeAPIServer()
+    api.create_node(make_node("n1"))
+    import tempfile
+
+    d = tempfile.mkdtemp(prefix="gtkh", dir="/tmp")
+    plug = DevicePluginServer(fx.f7_mi355x(), PluginConfig(node_name="n1", socket_dir=d, health_interval=0.05), api=api,
+                              health_fn=HealthMonitor(fx.f7_mi355x(), lambda: state["topo"]))
+    plug.start(register=False)
+    try:
+        assert plug.layout_change.wait(5) and "64" in plug.layout_change_reason
+        assert any(e["reason"] == "GPULayoutChanged" for e in api.events)
+    finally:
+        plug.stop()
