@@ -14,6 +14,9 @@
 //                               in place over the bf16 logits (saves a T x V fp32 tensor)
 //   adamw_step / sq_norm        one flat-buffer AdamW over bf16 params + fp32 master/m/v, and the
 //                               global gradient-norm reduction for clipping
+//   adamw_step_dev /            the graph-capturable pair: step count, bias corrections and the
+//   sq_norm_parts               clipping factor live on the device (2 launches per optimizer step)
+//   mnist_synth                 the MNIST workload's synthetic batch, one launch, device-indexed
 // All math in fp32, bf16 storage.  Wave size 64 everywhere (gfx950).
 #include <hip/hip_runtime.h>
 #include <torch/extension.h>
@@ -640,10 +643,9 @@ void xent_bwd_inplace(at::Tensor& logits, const at::Tensor& labels, const at::Te
 // each of master/m/v, one 16-B load of the bf16 gradient; writes master/m/v and the bf16 weight.
 // hp: device fp32 [lr, beta1, beta2, eps, weight_decay, grad_scale, bias_c1, bias_c2] so a captured
 // graph replays with updated hyper-parameters.
-__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, float* __restrict__ m, float* __restrict__ v,
-                                                    const u16* __restrict__ g, u16* __restrict__ w, const float* __restrict__ hp,
-                                                    size_t n) {
-  const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4], gs = hp[5], bc1 = hp[6], bc2 = hp[7];
+__device__ __forceinline__ void adamw_body(float* __restrict__ master, float* __restrict__ m, float* __restrict__ v,
+                                           const u16* __restrict__ g, u16* __restrict__ w, size_t n, float lr, float b1,
+                                           float b2, float eps, float wd, float gs, float bc1, float bc2) {
   const size_t nv = n >> 3;
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (size_t)gridDim.x * 256) {
     f32x4 p0 = reinterpret_cast<f32x4*>(master)[2 * i], p1 = reinterpret_cast<f32x4*>(master)[2 * i + 1];
@@ -683,6 +685,38 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, 
   }
 }
 
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, float* __restrict__ m, float* __restrict__ v,
+                                                    const u16* __restrict__ g, u16* __restrict__ w, const float* __restrict__ hp,
+                                                    size_t n) {
+  adamw_body(master, m, v, g, w, n, hp[0], hp[1], hp[2], hp[3], hp[4], hp[5], hp[6], hp[7]);
+}
+
+// Graph-mode AdamW: everything the host used to compute per step is derived on the device, so one
+// captured launch replays correctly forever (``FlatAdamW(capturable=True)``).
+//   hp   = [lr, beta1, beta2, eps, weight_decay, grad_scale, clip_norm (<= 0: off), -]
+//   part = sqnorm partials of the gradient (``sq_norm_parts``); every block reduces them itself
+//   t    = optimizer step count AFTER this step (``sq_norm_parts`` advanced it in stream order)
+// Bias corrections 1 - beta^t and the clipping factor min(1, clip / ||g * grad_scale||) follow.
+__global__ __launch_bounds__(256) void adamw_dev_kernel(float* __restrict__ master, float* __restrict__ m, float* __restrict__ v,
+                                                        const u16* __restrict__ g, u16* __restrict__ w, const float* __restrict__ hp,
+                                                        const float* __restrict__ part, int nparts, const float* __restrict__ tptr,
+                                                        size_t n) {
+  __shared__ float red[4];
+  const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4], gscale = hp[5], clip = hp[6];
+  float gs = gscale;
+  if (nparts > 0 && clip > 0.f) {
+    float s = 0.f;
+    for (int i = threadIdx.x; i < nparts; i += 256) s += part[i];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    const float norm = sqrtf(red[0] + red[1] + red[2] + red[3]) * gscale;
+    gs = gscale * fminf(1.f, clip / (norm + 1e-6f));
+  }
+  const float t = tptr[0];
+  adamw_body(master, m, v, g, w, n, lr, b1, b2, eps, wd, gs, 1.f - powf(b1, t), 1.f - powf(b2, t));
+}
+
 // sum of squares of a bf16 buffer -> per-block partials (fp32)
 __global__ __launch_bounds__(256) void sqnorm_kernel(const u16* __restrict__ g, float* __restrict__ part, size_t n) {
   __shared__ float red[4];
@@ -717,6 +751,122 @@ void adamw_step(at::Tensor& master, at::Tensor& m, at::Tensor& v, const at::Tens
                             m.data_ptr<float>(), v.data_ptr<float>(), bp(g), bpm(w), hp.data_ptr<float>(), n);
 }
 
+// sqnorm + (optionally) the step counter: block 0 / thread 0 adds 1 to ``tick`` — nothing else in
+// this kernel reads it; the AdamW kernel after it in stream order does.
+__global__ __launch_bounds__(256) void sqnorm_tick_kernel(const u16* __restrict__ g, float* __restrict__ part, size_t n,
+                                                          float* __restrict__ tick) {
+  __shared__ float red[4];
+  float s = 0.f;
+  const size_t nv = n >> 3;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (size_t)gridDim.x * 256) {
+    const u16x8 x = reinterpret_cast<const u16x8*>(g)[i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float f = bf2f(x[j]);
+      s += f * f;
+    }
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+    if (tick != nullptr && blockIdx.x == 0) tick[0] = tick[0] + 1.f;
+  }
+}
+
+// ============================================================================ synthetic MNIST
+// One block per image: label = hash(seed, step, image) % classes, pixel = (prototype[label] +
+// noise * N(0,1) - mean) / std in bf16, N(0,1) by Box-Muller from a counter-based hash of
+// (seed, step, pixel index).  ``step`` is read from the device (the optimizer's step counter), so a
+// captured graph draws a fresh batch every replay with no host involvement.  Reference:
+// ``models/mnist.py synth_reference`` (same hash in numpy).
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) { return mix32(a ^ mix32(b ^ mix32(c))); }
+
+__global__ __launch_bounds__(256) void mnist_synth_kernel(const float* __restrict__ proto, u16* __restrict__ x,
+                                                          int64_t* __restrict__ y, const float* __restrict__ tptr, uint32_t seed,
+                                                          int classes, int pixels, float noise, float mean, float inv_std) {
+  const int b = blockIdx.x;
+  const uint32_t step = (uint32_t)tptr[0];
+  const uint32_t lab = hash3(seed, step, 0x9e3779b9U ^ (uint32_t)b) % (uint32_t)classes;
+  if (threadIdx.x == 0) y[b] = (int64_t)lab;
+  const float* pr = proto + (size_t)lab * pixels;
+  u16* xo = x + (size_t)b * pixels;
+  for (int p = threadIdx.x * 2; p < pixels; p += 512) {
+    const uint32_t h1 = hash3(seed ^ 0x85ebca6bU, step, (uint32_t)b * (uint32_t)pixels + (uint32_t)p);
+    const uint32_t h2 = mix32(h1 ^ 0x27d4eb2fU);
+    const float u1 = (float)((h1 >> 8) + 1u) * (1.f / 16777216.f);  // (0, 1]
+    const float u2 = (float)(h2 >> 8) * (1.f / 16777216.f);         // [0, 1)
+    const float r = sqrtf(-2.f * logf(u1));
+    const float a = 6.28318530718f * u2;
+    xo[p] = f2bf((pr[p] + noise * r * cosf(a) - mean) * inv_std);
+    if (p + 1 < pixels) xo[p + 1] = f2bf((pr[p + 1] + noise * r * sinf(a) - mean) * inv_std);
+  }
+}
+
+std::vector<at::Tensor> mnist_synth(const at::Tensor& proto, int64_t batch, const at::Tensor& step, int64_t seed, double noise,
+                                    double mean, double std_) {
+  CHECK_F32(proto);
+  CHECK_F32(step);
+  TORCH_CHECK(proto.dim() == 4 && proto.size(1) == 1, "prototypes must be [classes, 1, H, W]");
+  TORCH_CHECK(batch > 0 && batch < (1 << 24), "batch out of range");
+  const int classes = (int)proto.size(0), H = (int)proto.size(2), W = (int)proto.size(3), pixels = H * W;
+  auto x = at::empty({batch, 1, H, W}, proto.options().dtype(at::kBFloat16));
+  auto y = at::empty({batch}, proto.options().dtype(at::kLong));
+  hipLaunchKernelGGL(mnist_synth_kernel, dim3((unsigned)batch), dim3(256), 0, cur_stream(), proto.data_ptr<float>(), bpm(x),
+                     y.data_ptr<int64_t>(), step.data_ptr<float>(), (uint32_t)seed, classes, pixels, (float)noise, (float)mean,
+                     (float)(1.0 / std_));
+  return {x, y};
+}
+
+at::Tensor sq_norm_parts(const at::Tensor& g, c10::optional<at::Tensor> tick) {
+  CHECK_BF16(g);
+  const size_t n = g.numel();
+  TORCH_CHECK(n % 8 == 0, "sq_norm_parts: size must be a multiple of 8");
+  float* tk = nullptr;
+  if (tick.has_value()) {
+    CHECK_F32(*tick);
+    tk = tick->data_ptr<float>();
+  }
+  const int grid = (int)std::max<size_t>(1, std::min<size_t>((n / 8 + 255) / 256, 1024));
+  auto part = at::empty({grid}, g.options().dtype(at::kFloat));  // every slot written
+  hipLaunchKernelGGL(sqnorm_tick_kernel, dim3(grid), dim3(256), 0, cur_stream(), bp(g), part.data_ptr<float>(), n, tk);
+  return part;
+}
+
+void adamw_step_dev(at::Tensor& master, at::Tensor& m, at::Tensor& v, const at::Tensor& g, at::Tensor& w, const at::Tensor& hp,
+                    c10::optional<at::Tensor> part, const at::Tensor& t) {
+  CHECK_F32(master);
+  CHECK_F32(m);
+  CHECK_F32(v);
+  CHECK_BF16(g);
+  CHECK_BF16(w);
+  CHECK_F32(hp);
+  CHECK_F32(t);
+  const size_t n = master.numel();
+  TORCH_CHECK(n % 8 == 0 && (size_t)m.numel() == n && (size_t)v.numel() == n && (size_t)g.numel() == n && (size_t)w.numel() == n,
+              "adamw: flat buffers must have equal sizes, a multiple of 8");
+  TORCH_CHECK(hp.numel() >= 7, "adamw_step_dev: hp needs 7 entries");
+  const float* pp = nullptr;
+  int np = 0;
+  if (part.has_value()) {
+    CHECK_F32(*part);
+    pp = part->data_ptr<float>();
+    np = (int)part->numel();
+  }
+  if (n) hipLaunchKernelGGL(adamw_dev_kernel, dim3(grid_for(n / 8)), dim3(256), 0, cur_stream(), master.data_ptr<float>(),
+                            m.data_ptr<float>(), v.data_ptr<float>(), bp(g), bpm(w), hp.data_ptr<float>(), pp, np,
+                            t.data_ptr<float>(), n);
+}
+
 at::Tensor sq_norm(const at::Tensor& g) {
   CHECK_BF16(g);
   const size_t n = g.numel();
@@ -728,6 +878,15 @@ at::Tensor sq_norm(const at::Tensor& g) {
 }
 
 }  // namespace
+
+namespace gtk_mnist {  // csrc/ops/mnist_conv.hip
+at::Tensor conv1_fwd(const at::Tensor& x, const at::Tensor& w1, const at::Tensor& b1);
+std::vector<at::Tensor> conv2_pool_fwd(const at::Tensor& h1, const at::Tensor& w2, const at::Tensor& b2, const at::Tensor& step,
+                                       int64_t seed, double p_drop);
+void conv_bwd(const at::Tensor& dp, const at::Tensor& code, const at::Tensor& x, const at::Tensor& h1, const at::Tensor& w1,
+              const at::Tensor& b1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& gw1, at::Tensor& gb1, at::Tensor& gw2,
+              at::Tensor& gb2, double p_drop, bool accumulate);
+}  // namespace gtk_mnist
 
 namespace gtk_attn {  // csrc/ops/attention.hip
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale);
@@ -759,5 +918,11 @@ PYBIND11_MODULE(_fused, m) {
   m.def("xent_bwd_inplace", &xent_bwd_inplace);
   m.def("adamw_step", &adamw_step);
   m.def("sq_norm", &sq_norm);
+  m.def("sq_norm_parts", &sq_norm_parts, "sum-of-squares partials of a bf16 buffer; optionally advance a step counter");
+  m.def("adamw_step_dev", &adamw_step_dev, "AdamW with device-side bias correction and clipping (graph-capturable)");
+  m.def("mnist_synth", &mnist_synth, "synthetic MNIST batch on the device, indexed by a device step counter");
+  m.def("mnist_conv1_fwd", &gtk_mnist::conv1_fwd, "MNIST conv1 + ReLU, NHWC bf16");
+  m.def("mnist_conv2_pool_fwd", &gtk_mnist::conv2_pool_fwd, "MNIST conv2 + ReLU + 2x2 max-pool + dropout (MFMA)");
+  m.def("mnist_conv_bwd", &gtk_mnist::conv_bwd, "MNIST conv stack backward into the flat gradient (MFMA)");
   m.def("transpose_bf16", &gtk_xpose::transpose_bf16, "contiguous [R, C] bf16 -> [C, R] (R, C multiples of 64)");
 }

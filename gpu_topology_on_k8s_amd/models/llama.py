@@ -164,6 +164,13 @@ class FlatParams:
         for fn in list(self._ready.get(name, ())):
             fn(self.params[name])
 
+    def mark_written(self, name: str) -> None:
+        """A kernel wrote ``name``'s gradient into the flat buffer itself (not through
+        :meth:`write_grad`): clear its fresh flag and announce readiness (data-parallel buckets)."""
+        self.direct[name] = False
+        for fn in list(self._ready.get(name, ())):
+            fn(self.params[name])
+
     def fill_unwritten(self) -> None:
         """Zero the gradients of direct parameters that received none since :meth:`zero_grad`."""
         for n, fresh in self.direct.items():

@@ -9,6 +9,10 @@ Optional global-norm clipping uses one more fused pass (``sq_norm``) and stays o
 ``shards`` (ZeRO-1, :class:`~..parallel.dp.BucketedAllReduce` with ``zero1=True``): the optimizer
 owns only those flat-buffer ranges — its master/m/v hold their concatenation, one kernel launch per
 range, and the clipping norm is the all-reduced sum of every rank's shard norms.
+
+``capturable=True``: the step count and every hyper-parameter stay on the device (bias corrections
+computed there), so a whole training step including :meth:`step` can be captured into a hipGraph and
+replayed (``models/train.py --graph``); the host mirror ``t`` is advanced by :meth:`note_replay`.
 """
 from __future__ import annotations
 
@@ -25,7 +29,8 @@ __all__ = ["FlatAdamW"]
 
 class FlatAdamW:
     def __init__(self, flat, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8, weight_decay: float = 0.1,
-                 clip_norm: Optional[float] = 1.0, shards: Optional[Sequence[Tuple[int, int]]] = None, group=None):
+                 clip_norm: Optional[float] = 1.0, shards: Optional[Sequence[Tuple[int, int]]] = None, group=None,
+                 capturable: bool = False):
         self.flat = flat
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.clip_norm = clip_norm
@@ -38,9 +43,34 @@ class FlatAdamW:
             self.master = flat.data.float()
         self.m = torch.zeros_like(self.master)
         self.v = torch.zeros_like(self.master)
-        self.t = 0
         self.hp = torch.zeros(8, dtype=torch.float32, device=flat.data.device)
+        self.capturable = capturable
+        self.t_dev = torch.zeros(1, dtype=torch.float32, device=flat.data.device) if capturable else None
+        self._t = 0
+        self.hp_dev = None
+        if capturable:
+            b1, b2 = betas
+            self.hp[:5].copy_(torch.tensor([lr, b1, b2, eps, weight_decay], dtype=torch.float32))
+            # fused path (GPU, unsharded): [lr, b1, b2, eps, wd, grad_scale, clip_norm, -] for adamw_step_dev
+            self.hp_dev = torch.tensor([lr, b1, b2, eps, weight_decay, 1.0, clip_norm if clip_norm else -1.0, 0.0],
+                                       dtype=torch.float32).to(flat.data.device)
+            self._hp_scale = 1.0
         self._deferred = []  # events the next step's writes must wait for (async checkpoint copies)
+
+    @property
+    def t(self) -> int:
+        """Optimizer steps taken (host view; checkpoints record it)."""
+        return self._t
+
+    @t.setter
+    def t(self, value: int) -> None:
+        self._t = int(value)
+        if self.t_dev is not None:
+            self.t_dev.fill_(float(self._t))
+
+    def note_replay(self, n: int = 1) -> None:
+        """A captured :meth:`step` ran ``n`` more times on the device: advance the host mirror."""
+        self._t += n
 
     def defer_until(self, event) -> None:
         """Make the next :meth:`step` (on its stream) wait for ``event`` before it writes."""
@@ -58,7 +88,10 @@ class FlatAdamW:
             for ev in self._deferred:
                 cur.wait_event(ev)
             self._deferred.clear()
-        self.t += 1
+        if self.capturable:
+            self._step_device(grad_scale, sq)
+            return
+        self._t += 1
         b1, b2 = self.betas
         gs = torch.tensor(grad_scale, dtype=torch.float32, device=self.hp.device)
         if self.clip_norm is not None:
@@ -72,6 +105,54 @@ class FlatAdamW:
         vals = torch.tensor([self.lr, b1, b2, self.eps, self.wd, 0.0, 1 - b1 ** self.t, 1 - b2 ** self.t], dtype=torch.float32)
         self.hp.copy_(vals, non_blocking=True)
         self.hp[5:6].copy_(gs.reshape(1))
+        o = 0
+        for (s, e), g, d in zip(self.shards, self._views(self.flat.grad), self._views(self.flat.data)):
+            n = e - s
+            st = (self.master[o:o + n], self.m[o:o + n], self.v[o:o + n])
+            if d.is_cuda:
+                fused.hip().adamw_step(*st, g, d, self.hp)
+            else:
+                self._step_ref(*st, g, d)
+            o += n
+
+    def _clip_sq(self, sq: Optional[torch.Tensor]) -> torch.Tensor:
+        for g in ([] if sq is not None else self._views(self.flat.grad)):
+            part = fused.hip().sq_norm(g) if g.is_cuda else g.float().pow(2).sum()
+            sq = part if sq is None else sq + part
+        if self.sharded and dist.is_initialized() and dist.get_world_size(self.group) > 1:
+            dist.all_reduce(sq, group=self.group)
+        return sq
+
+    def _step_device(self, grad_scale: float, sq: Optional[torch.Tensor]) -> None:
+        """Host-sync-free step: no host->device copies, so it captures.  On a GPU without shards it
+        is two HIP launches — ``sq_norm_parts`` (clipping partials, step counter += 1) and
+        ``adamw_step_dev`` (bias corrections and clip factor derived in-kernel)."""
+        g, d = self.flat.grad, self.flat.data
+        if d.is_cuda and not self.sharded and sq is None:
+            hip = fused.hip()
+            if grad_scale != self._hp_scale:  # constant per run (1/world): set once, persists across replays
+                self.hp_dev[5:6].fill_(grad_scale)
+                self._hp_scale = grad_scale
+            if self.clip_norm is not None:
+                part = hip.sq_norm_parts(g, self.t_dev)
+            else:
+                part = None
+                self.t_dev.add_(1.0)
+            if not torch.cuda.is_current_stream_capturing():
+                self._t += 1
+            hip.adamw_step_dev(self.master, self.m, self.v, g, d, self.hp_dev, part, self.t_dev)
+            return
+        b1, b2 = self.betas
+        self.t_dev.add_(1.0)
+        if not (self.t_dev.is_cuda and torch.cuda.is_current_stream_capturing()):
+            self._t += 1
+        self.hp[6:7].copy_(1.0 - torch.pow(b1, self.t_dev))
+        self.hp[7:8].copy_(1.0 - torch.pow(b2, self.t_dev))
+        if self.clip_norm is not None:
+            norm = self._clip_sq(sq).sqrt() * grad_scale
+            self.hp[5:6].copy_((torch.clamp(self.clip_norm / (norm + 1e-6), max=1.0) * grad_scale).reshape(1))
+        else:
+            self.hp[5:6].fill_(grad_scale)
         o = 0
         for (s, e), g, d in zip(self.shards, self._views(self.flat.grad), self._views(self.flat.data)):
             n = e - s

@@ -1,7 +1,9 @@
-"""Llama-3 data-parallel training on the scheduler-chosen devices (BASELINE config 5).
+"""Data-parallel training on the scheduler-chosen devices: Llama-3 (BASELINE config 5) and the Gaia
+paper's MNIST CNN (Exp. 6, ``models/mnist.py``).
 
     python -m torch.distributed.run --nproc-per-node K --master-addr 127.0.0.1 \
         -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 2 --seq 4096 --steps 10 --placement best
+    ... -m gpu_topology_on_k8s_amd.models.train --model mnist-cnn --batch 64 --steps 200   # images/s, epoch time
 
 One process per GPU; rank 0 discovers the node, runs the placement core for the k-subset (``best``)
 or its worst-scoring alternative (``worst``), and every rank binds to ``subset[rank]`` — what the pod
@@ -9,6 +11,10 @@ would see after the device plugin's Allocate.  A step = forward + backward with 
 gradient all-reduce overlapped with backward + global-norm clip + fused AdamW.  Reports tokens/s
 (whole job) and model FLOP utilisation against the 2.5 PF/s dense bf16 peak per GPU.
 Runs on CPU with the gloo backend for tests (tiny model).
+
+``--graph on`` captures the whole step (device-side batch synthesis, forward, backward, gradient
+all-reduce, clipping, capturable AdamW) into one hipGraph after the warmup and replays it: the mode
+for launch-bound models such as the MNIST CNN ('auto' = on for MNIST at world 1 on a GPU).
 """
 from __future__ import annotations
 
@@ -23,6 +29,7 @@ import torch
 import torch.distributed as dist
 
 from .llama import Llama, LlamaConfig
+from .mnist import EPOCH_IMAGES, MnistCNN, MnistConfig
 from .gemm_tuning import setup_gemm_tuning
 from .optim import FlatAdamW
 from .checkpoint import CheckpointWriter, load_checkpoint
@@ -64,7 +71,8 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
           attn: str = "hip", seed: int = 0, log: bool = True, gemm_tuning: str = "auto",
           gemm_table: Optional[str] = None, gemm_layout: str = "nt", overlap_transposes: bool = False,
           zero1: bool = False, save_dir: Optional[str] = None, save_every: int = 0, resume: Optional[str] = None,
-          keep: int = 2, fuse_residual: bool = True, overlap_norm: bool = False, same_data: bool = False) -> Dict[str, object]:
+          keep: int = 2, fuse_residual: bool = True, overlap_norm: bool = False, same_data: bool = False,
+          graph: str = "auto", conv: str = "hip") -> Dict[str, object]:
     env = _init_dist(device_kind)
     if device_kind == "cuda":
         pl = _choose_device(env, placement, discovery)
@@ -79,17 +87,38 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
             pl = {"devices": [], "best": [], "worst": None, "source": "cpu"}
         device = torch.device("cpu")
         gemm_mode = "off"
-    cfg = LlamaConfig.named(model_name)
-    model = Llama(cfg, device=device, seed=seed, checkpoint=checkpoint, attn=attn, gemm_layout=gemm_layout,
-                  overlap_transposes=overlap_transposes, fuse_residual=fuse_residual)
+    mnist = model_name.startswith("mnist")
+    use_graph = graph == "on" or (graph == "auto" and mnist and device.type == "cuda" and env["world"] == 1)
+    if use_graph and device.type != "cuda":
+        raise ValueError("--graph on needs a GPU")
+    if use_graph and zero1:
+        raise ValueError("--graph does not capture ZeRO-1's per-bucket weight all-gathers")
+    data_seed = 1234 + (0 if same_data else env["rank"])
+    if mnist:
+        cfg = MnistConfig.named(model_name)
+        model = MnistCNN(cfg, device=device, seed=seed, conv=conv)
+        items_per_step, unit, flops_per_item = batch, "images", cfg.flops_per_image()
+    else:
+        cfg = LlamaConfig.named(model_name)
+        model = Llama(cfg, device=device, seed=seed, checkpoint=checkpoint, attn=attn, gemm_layout=gemm_layout,
+                      overlap_transposes=overlap_transposes, fuse_residual=fuse_residual)
+        items_per_step, unit, flops_per_item = batch * seq, "tokens", cfg.flops_per_token(seq)
     broadcast_params(model.flat)
     ar = BucketedAllReduce(model.flat, bucket_mb=bucket_mb, zero1=zero1, overlap_norm=overlap_norm)
-    opt = FlatAdamW(model.flat, lr=lr, shards=ar.shards() if zero1 else None)
+    opt = FlatAdamW(model.flat, lr=lr, shards=ar.shards() if zero1 else None, capturable=use_graph)
     if zero1:
         model.param_ready = ar.wait_param
+    if mnist and use_graph:
+        model.step_counter = opt.t_dev  # dropout hash keyed by the device step count (advances per replay)
     # same_data: every rank draws rank 0's batches, so the averaged gradient equals the 1-rank
-    # gradient and a k-rank run must reproduce the 1-rank losses (the DP correctness check)
-    gen = torch.Generator(device="cpu").manual_seed(1234 + (0 if same_data else env["rank"]))
+    # gradient and a k-rank run must reproduce the 1-rank losses (the DP correctness check).
+    # MNIST batches are synthesised on the device; in graph mode by the mnist_synth kernel, indexed
+    # by the optimizer's device step counter (dropout masks from the graph-safe default generator).
+    if mnist and use_graph:
+        torch.cuda.manual_seed(data_seed)
+        gen = None
+    else:
+        gen = torch.Generator(device=device if mnist else "cpu").manual_seed(data_seed)
     start_step, resumed = 0, None
     if resume:
         meta = load_checkpoint(resume, model, opt, gen)
@@ -100,11 +129,15 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
     done = [start_step]
 
     def batch_tokens():
+        if mnist and use_graph:  # one HIP launch, indexed by the optimizer's device step counter
+            return model.synthetic_batch_dev(batch, opt.t_dev, seed=data_seed)
+        if mnist:
+            return model.synthetic_batch(batch, gen)
         t = torch.randint(0, cfg.vocab, (batch, seq + 1), generator=gen)
         t = t.to(device, non_blocking=True)
         return t[:, :-1], t[:, 1:]
 
-    def step() -> torch.Tensor:
+    def body() -> torch.Tensor:
         x, y = batch_tokens()
         model.flat.zero_grad()
         loss = model(x, y)
@@ -112,20 +145,43 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         ar.finish()
         opt.step(grad_scale=ar.grad_scale, sq=ar.sq_norm())
         ar.gather_params()  # zero1: overlaps the next forward; no-op otherwise
+        return loss.detach()
+
+    captured = {}
+
+    def capture() -> None:
+        """After the eager warmup (library handles, workspaces and autotuning exist): record one
+        whole step into a hipGraph; it is not executed here."""
+        torch.cuda.synchronize(device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            captured["loss"] = body()
+        captured["g"] = g
+        torch.cuda.synchronize(device)
+
+    def step() -> torch.Tensor:
+        if "g" in captured:
+            captured["g"].replay()
+            opt.note_replay()
+            loss = captured["loss"].clone()
+        else:
+            loss = body()
         done[0] += 1
         if ckpt is not None and save_every > 0 and done[0] % save_every == 0:
             ar.wait_all_params()
             ckpt.save(done[0], gen)
-        return loss.detach()
+        return loss
 
     def sync():
         if device.type == "cuda":
             torch.cuda.synchronize(device)
 
     losses = []
-    for _ in range(warmup):
+    for _ in range(max(warmup, 1) if use_graph else warmup):
         losses.append(step())
     ar.wait_all_params()
+    if use_graph:
+        capture()
     sync()
     dist.barrier()
     sync()
@@ -143,12 +199,16 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         if not ckpt.has(done[0]):
             ckpt.save(done[0], gen)
         ckpt.close()
-    tokens = env["world"] * batch * seq * steps
-    tps = tokens / dt
-    mfu = tps * cfg.flops_per_token(seq) / (PEAK_BF16_FLOPS * env["world"]) if device.type == "cuda" else None
+    items = env["world"] * items_per_step * steps
+    tps = items / dt
+    mfu = tps * flops_per_item / (PEAK_BF16_FLOPS * env["world"]) if device.type == "cuda" else None
     out = {
-        "metric": "Llama DP training tokens/s on the scheduler-chosen subset",
+        "metric": (f"{'MNIST CNN' if mnist else 'Llama'} DP training {unit}/s on the scheduler-chosen subset"),
         "model": model_name,
+        "throughput": tps,
+        "throughput_unit": f"{unit}/s",
+        "graph": use_graph,
+        "conv": getattr(model, "conv", None),
         "params": cfg.num_params(),
         "n_gpus": env["world"],
         "placement": placement,
@@ -158,11 +218,13 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "best_score": pl.get("best_score"),
         "worst_score": pl.get("worst_score"),
         "global_batch": batch * env["world"],
-        "seq_len": seq,
+        "seq_len": None if mnist else seq,
         "steps": steps,
         "warmup": warmup,
         "ms_per_step": dt / max(1, steps) * 1e3,
-        "tokens_per_s": tps,
+        "tokens_per_s": None if mnist else tps,
+        "images_per_s": tps if mnist else None,
+        "epoch_s": EPOCH_IMAGES / tps if mnist else None,  # one 60k-image MNIST epoch at the measured rate
         "mfu": mfu,
         "loss_first": float(losses[0]),
         "loss_last": float(losses[-1]),
@@ -192,7 +254,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--model", default="llama3-8b", choices=["llama3-8b", "llama3-1b", "tiny"])
+    ap.add_argument("--model", default="llama3-8b", choices=["llama3-8b", "llama3-1b", "tiny", "mnist-cnn"])
     ap.add_argument("--batch", type=int, default=2)
     ap.add_argument("--seq", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=5)
@@ -221,6 +283,10 @@ def main(argv=None) -> int:
                     help="separate residual-add kernels instead of the fused add+RMSNorm (A/B)")
     ap.add_argument("--same-data", action="store_true",
                     help="every rank trains on rank 0's batches (k-rank losses must equal the 1-rank run)")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="capture the whole step into one hipGraph after warmup (auto: MNIST at world 1 on a GPU)")
+    ap.add_argument("--conv", default="hip", choices=["hip", "torch"],
+                    help="MNIST convolution stack: hip = csrc/ops/mnist_conv.hip (MFMA), torch = MIOpen via F.conv2d")
     ap.add_argument("--overlap-norm", action="store_true",
                     help="clipping norm per bucket on a side stream as buckets complete (measured no gain at world 1)")
     a = ap.parse_args(argv)
@@ -228,7 +294,7 @@ def main(argv=None) -> int:
           gemm_tuning=a.gemm_tuning, gemm_table=a.gemm_table, gemm_layout=a.gemm_layout,
           overlap_transposes=a.overlap_transposes, zero1=a.zero1, save_dir=a.save_dir, save_every=a.save_every,
           resume=a.resume, keep=a.keep, fuse_residual=not a.no_fuse_residual,
-          overlap_norm=a.overlap_norm, same_data=a.same_data)
+          overlap_norm=a.overlap_norm, same_data=a.same_data, graph=a.graph, conv=a.conv)
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0

@@ -4,7 +4,7 @@ Every test here needs at least two visible MI355X and skips with the reason on a
 8-GPU node they localise a failure of the scaling curve to one component: the p2p probe kernels
 across a real xGMI pair (K1 read, K2 write), the all-peer gather (K5), the RCCL communicator at
 k=2 (bench.py, native backend, exact check, busBW bounded by the probe), hipGraph capture at k=2,
-and 2-rank Llama DP / ZeRO-1 against the 1-rank run.
+and 2-rank Llama DP / ZeRO-1 and MNIST DP against the 1-rank run.
 """
 import json
 import os
@@ -110,5 +110,18 @@ def test_two_rank_dp_matches_one_rank(zero1):
     two = _run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1",
                 "--master-port=29611", "-m", "gpu_topology_on_k8s_amd.models.train", *base])
     assert two["n_gpus"] == 2 and len(two["losses"]) == len(one["losses"]) == 3
+    for a, b in zip(one["losses"], two["losses"]):
+        assert abs(a - b) <= 2e-2 * max(1.0, abs(a)), (one["losses"], two["losses"])
+
+
+@needs2
+def test_two_rank_mnist_dp_matches_one_rank():
+    """The Gaia Exp. 6 workload at k=2: one 2.4 MB gradient all-reduce per step over RCCL."""
+    base = ["--model", "mnist-cnn", "--batch", "64", "--steps", "5", "--warmup", "1", "--same-data", "--graph", "off",
+            "--gemm-tuning", "off"]
+    one = _run(["-m", "gpu_topology_on_k8s_amd.models.train", *base])
+    two = _run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1",
+                "--master-port=29613", "-m", "gpu_topology_on_k8s_amd.models.train", *base])
+    assert two["n_gpus"] == 2 and two["images_per_s"] > 0
     for a, b in zip(one["losses"], two["losses"]):
         assert abs(a - b) <= 2e-2 * max(1.0, abs(a)), (one["losses"], two["losses"])
