@@ -34,6 +34,9 @@ typedef unsigned short u16;
 typedef u16 u16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+#define LDS_AS __attribute__((address_space(3)))
 
 constexpr int IMG = 28, H1 = 26, C1 = 32, H2 = 24, C2 = 64, HP = 12;
 constexpr int WIN_PER_IMG = HP * HP;      // 144 pooling windows
@@ -49,6 +52,18 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ bf16x8 as_bf(u16x8 v) { return __builtin_bit_cast(bf16x8, v); }
+
+// 16x16x32 operand whose k index walks the ROWS of a row-major LDS image [k][cols] (ds_read_b64_tr_b16,
+// cdna_hip_programming.md T10): lane l = 16g + 4q + p reads rows row0 + 8g + q (+4), columns
+// col0 + 4p .. +3, and receives column col0 + (l & 15) for k = 8g .. 8g+7.  Whole-vector casts only
+// (a per-element bit cast of a tr-read result miscompiles on this toolchain).  EXEC must be full.
+__device__ __forceinline__ bf16x8 tr_frag16(const u16* img, int stride, int row0, int col0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const u16* a = img + (row0 + 8 * g + q) * stride + col0 + 4 * p;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a + 4 * stride));
+  return __builtin_shufflevector(__builtin_bit_cast(bf16x4, lo), __builtin_bit_cast(bf16x4, hi), 0, 1, 2, 3, 4, 5, 6, 7);
+}
 
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
@@ -173,43 +188,88 @@ __device__ __forceinline__ void dy2_frag(const u16* __restrict__ dp, const uint8
 }
 
 // ------------------------------------------------------ conv2 dgrad + conv1 wgrad partials (MFMA)
-constexpr int WTS = C2 + 8;   // LDS row stride of the transposed conv2.w: [tap][ci][co]
 constexpr int DG_ROWS = 4;    // input rows of h1 per workgroup (one per wave)
 constexpr int DYW = 34;       // dy2 tile columns: x = -2 .. 31 (zero outside 0..23)
 constexpr int DYC = C2 + 8;   // dy2 tile channel stride (pad)
+constexpr int XROWS = DG_ROWS + 2;
 
-// Workgroup = (image b, input rows 4g .. 4g+3); wave w owns input row 4g + w, as two 16-pixel m-tiles
-// (x = 0..31, 26 valid).  The dy2 rows it needs (4g-2 .. 4g+3) are rebuilt once from the pooled
-// gradient and code bytes into a zero-bordered LDS tile, so every A fragment is one 16-byte LDS read.
+// Workgroup = (image b, input rows 4g .. 4g+3); wave w owns input row 4g + w as two 16-pixel m-tiles
+// (x = 0..31, 26 valid).  Everything the workgroup reads is staged once, with every global load
+// issued before the first LDS write: conv2.w row-major (its k index, the output channel, walks rows:
+// transposed reads give the B operand), the dy2 rows 4g-2 .. 4g+3 rebuilt from the pooled gradient
+// and code bytes into a zero-bordered tile (A operand: one 16-byte read), and the h1 / x rows the
+// epilogue needs for conv1's ReLU mask and weight gradient.
 __global__ __launch_bounds__(256) void conv2_dgrad_kernel(const u16* __restrict__ dp, const uint8_t* __restrict__ code,
                                                           const u16* __restrict__ w2, const u16* __restrict__ h1,
                                                           const u16* __restrict__ x, float* __restrict__ part1, float dscale) {
-  __shared__ __attribute__((aligned(16))) u16 wt[9 * C1 * WTS];
-  __shared__ __attribute__((aligned(16))) u16 dyl[(DG_ROWS + 2) * DYW * DYC];
+  __shared__ __attribute__((aligned(16))) u16 ws[C2 * W2S];
+  __shared__ __attribute__((aligned(16))) u16 dyl[XROWS * DYW * DYC];
+  __shared__ __attribute__((aligned(16))) u16 h1t[DG_ROWS * H1 * C1];
+  __shared__ __attribute__((aligned(16))) u16 xt[XROWS * IMG + 8];
   __shared__ float red[4][P1];
   constexpr int GROUPS = (H1 + DG_ROWS - 1) / DG_ROWS;  // 7
   const int b = blockIdx.x / GROUPS, yi0 = (blockIdx.x - b * GROUPS) * DG_ROWS;
-  for (int i = threadIdx.x; i < C2 * (KW2 / 8); i += 256) {
-    const int co = i / (KW2 / 8), ch = i - co * (KW2 / 8), tap = ch >> 2, ci0 = (ch & 3) * 8;
-    const u16x8 v = reinterpret_cast<const u16x8*>(w2)[i];
+  constexpr int WCH = C2 * (KW2 / 8) / 256;         // 9 conv2.w chunks per thread
+  constexpr int DTASK = XROWS * DYW * 8;            // 1632 dy2 tasks
+  constexpr int DPT = (DTASK + 255) / 256;          // 7 per thread
+  constexpr int HTASK = DG_ROWS * H1 * 4;           // 416 h1 chunks
+  const int nrows = min(DG_ROWS, H1 - yi0);
+  u16x8 wv[WCH];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) wt[(tap * C1 + ci0 + j) * WTS + co] = v[j];
-  }
-  for (int i = threadIdx.x; i < (DG_ROWS + 2) * DYW * 8; i += 256) {
+  for (int k = 0; k < WCH; ++k) wv[k] = reinterpret_cast<const u16x8*>(w2)[threadIdx.x + 256 * k];
+  uint64_t cc[DPT];
+  u16x8 dd[DPT];
+#pragma unroll
+  for (int k = 0; k < DPT; ++k) {
+    const int i = threadIdx.x + 256 * k;
     const int ry = i / (DYW * 8), rem = i - ry * (DYW * 8), xs = rem >> 3, co0 = (rem & 7) * 8;
     const int y = yi0 - 2 + ry, xx = xs - 2;
-    u16x8 u = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    if (y >= 0 && y < H2 && xx >= 0 && xx < H2) {
-      float v[8];
-      dy2_frag(dp, code, b, y, xx, co0, dscale, v);
+    cc[k] = 0;
+    dd[k] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (i < DTASK && y >= 0 && y < H2 && xx >= 0 && xx < H2) {
+      const size_t o = (size_t)((b * HP + (y >> 1)) * HP + (xx >> 1)) * C2 + co0;
+      cc[k] = *reinterpret_cast<const uint64_t*>(code + o);
+      dd[k] = *reinterpret_cast<const u16x8*>(dp + o);
+    }
+  }
+  u16x8 hv[2];
+  const u16* h1b = h1 + ((size_t)b * H1 + yi0) * H1 * C1;  // rows yi0 .. yi0+3 are contiguous
 #pragma unroll
-      for (int j = 0; j < 8; ++j) u[j] = f2bf(v[j]);
+  for (int k = 0; k < 2; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    hv[k] = (i < HTASK && i < nrows * H1 * 4) ? reinterpret_cast<const u16x8*>(h1b)[i] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  uint32_t xv = 0;  // x rows yi0 .. yi0+5 (two bf16 per thread; rows past 27 are never read)
+  const int xe = yi0 * IMG + 2 * threadIdx.x;
+  if (threadIdx.x < XROWS * IMG / 2 && xe < IMG * IMG)
+    xv = *reinterpret_cast<const uint32_t*>(x + (size_t)b * IMG * IMG + xe);
+#pragma unroll
+  for (int k = 0; k < WCH; ++k) {
+    const int i = threadIdx.x + 256 * k, co = i / (KW2 / 8), ch = i - co * (KW2 / 8);
+    *reinterpret_cast<u16x8*>(&ws[co * W2S + ch * 8]) = wv[k];
+  }
+#pragma unroll
+  for (int k = 0; k < DPT; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    if (i >= DTASK) break;
+    const int ry = i / (DYW * 8), rem = i - ry * (DYW * 8), xs = rem >> 3, co0 = (rem & 7) * 8;
+    const int y = yi0 - 2 + ry, xx = xs - 2, q = (y & 1) * 2 + (xx & 1);
+    u16x8 u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t c = (uint32_t)(cc[k] >> (8 * j)) & 0xffu;  // 0 (never passes) outside the map
+      u[j] = f2bf(((c & 3u) == (uint32_t)q && (c & 12u) == 12u) ? bf2f(dd[k][j]) * dscale : 0.f);
     }
     *reinterpret_cast<u16x8*>(&dyl[(ry * DYW + xs) * DYC + co0]) = u;
   }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    if (i < HTASK) reinterpret_cast<u16x8*>(h1t)[i] = hv[k];
+  }
+  if (threadIdx.x < XROWS * IMG / 2) reinterpret_cast<uint32_t*>(xt)[threadIdx.x] = xv;
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 15, h = lane >> 4;
-  const int yi = yi0 + wave;
   f32x4 acc[2][2];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
@@ -228,33 +288,31 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(const u16* __restrict_
         a[mt] = as_bf(*reinterpret_cast<const u16x8*>(&dyl[(arow + mt * 16 + r - kx + 2) * DYC + co0]));
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
-        const bf16x8 bf = as_bf(*reinterpret_cast<const u16x8*>(&wt[(t * C1 + nt * 16 + r) * WTS + co0]));
+        const bf16x8 bf = tr_frag16(ws, W2S, kc * 32, t * C1 + nt * 16, lane);  // B[k = co][n = ci]
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) acc[mt][nt] = mfma16(a[mt], bf, acc[mt][nt]);
       }
     }
   }
-  // lane: channel ci = nt*16 + r, pixels (yi, x = 16mt + 4h + reg)
+  // lane: channel ci = nt*16 + r, pixels (yi0 + wave, x = 16mt + 4h + reg)
   float w1acc[2][10];
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
     for (int t = 0; t < 10; ++t) w1acc[nt][t] = 0.f;
-  if (yi < H1) {
+  if (wave < nrows) {
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg) {
         const int xi = mt * 16 + 4 * h + reg;
         if (xi >= H1) continue;
-        const u16* xp = x + (size_t)b * IMG * IMG + yi * IMG + xi;
         float xin[9];
 #pragma unroll
-        for (int t = 0; t < 9; ++t) xin[t] = bf2f(xp[(t / 3) * IMG + t % 3]);
-        const size_t gp = ((size_t)b * H1 + yi) * H1 + xi;
+        for (int t = 0; t < 9; ++t) xin[t] = bf2f(xt[(wave + t / 3) * IMG + xi + t % 3]);
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
-          const float dz = bf2f(h1[gp * C1 + nt * 16 + r]) > 0.f ? acc[mt][nt][reg] : 0.f;
+          const float dz = bf2f(h1t[(wave * H1 + xi) * C1 + nt * 16 + r]) > 0.f ? acc[mt][nt][reg] : 0.f;
 #pragma unroll
           for (int t = 0; t < 9; ++t) w1acc[nt][t] += dz * xin[t];
           w1acc[nt][9] += dz;
@@ -278,28 +336,30 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(const u16* __restrict_
 }
 
 // ------------------------------------------------------------------- conv2 wgrad partials (MFMA)
-constexpr int DYS = 40;  // LDS row stride (elements) of dy2^T rows (32 pixels + pad)
-constexpr int HTS = 40;  // ... of the shifted h1^T rows
+constexpr int DYN = C2 + 8;          // dy2 row image [x 32][co]: row stride (elements)
+constexpr int HNR = 34;              // h1 rows per ky in the image: x = 0..33 (26..33 zero)
+constexpr int HNS = C1 + 8;          // h1 image [ky][x][ci]: row stride (elements)
 constexpr int HCHUNKS = 3 * H1 * 4;  // 312 16-byte chunks of h1 per output row (rows y..y+2)
+constexpr int WG_BUF = 32 * DYN + 3 * HNR * HNS;  // one stage: dy2 image + h1 image
 
-// Workgroup = a run of consecutive output rows (b, y); per row, K = 24 pixels (padded to 32).  The
-// next row's code bytes, pooled gradient and h1 chunks are loaded into registers while the MFMAs of
-// the current row run, then written transposed into LDS.
+// Workgroup = a run of consecutive output rows (b, y); per row, K = 24 pixels (padded to 32).  dy2 and
+// the three h1 rows it meets are staged row-major exactly as they sit in memory (16-byte writes) and
+// both MFMA operands, whose k index is the pixel, are read transposed (tr_frag16); a tap's column
+// shift kx is a row offset of the h1 image.  Two LDS stages: the next row's loads are in flight during
+// this row's MFMAs and one barrier per row suffices.
 __global__ __launch_bounds__(256) void conv2_wgrad_kernel(const u16* __restrict__ dp, const uint8_t* __restrict__ code,
                                                           const u16* __restrict__ h1, float* __restrict__ part2, float dscale,
                                                           int nrows, int rows_per_wg) {
-  __shared__ __attribute__((aligned(16))) u16 dyT[C2 * DYS];          // [co][x]
-  __shared__ __attribute__((aligned(16))) u16 hT[9 * C1 * HTS];       // [ky][shift][ci][x]
+  __shared__ __attribute__((aligned(16))) u16 img[2 * WG_BUF];
   __shared__ float dbp[192][9];
-  for (int i = threadIdx.x; i < C2 * DYS; i += 256) dyT[i] = 0;
-  for (int i = threadIdx.x; i < 9 * C1 * HTS; i += 256) hT[i] = 0;
+  for (int i = threadIdx.x; i < 2 * WG_BUF; i += 256) img[i] = 0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 15, h = lane >> 4;
   f32x4 acc[18];
 #pragma unroll
   for (int n = 0; n < 18; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
   float db[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int row0 = blockIdx.x * rows_per_wg, row1 = min(nrows, row0 + rows_per_wg);
-  // this thread's staging tasks: one dy2 (x, 8-channel chunk) if < 192; h1 chunks tid and tid + 256
+  // staging tasks: one dy2 (x, 8-channel chunk) if tid < 192; h1 chunks tid and tid + 256
   const int dx = threadIdx.x >> 3, dco0 = (threadIdx.x & 7) * 8;
   uint64_t c8 = 0;
   u16x8 d8 = u16x8{0, 0, 0, 0, 0, 0, 0, 0}, hv0 = d8, hv1 = d8;
@@ -310,46 +370,43 @@ __global__ __launch_bounds__(256) void conv2_wgrad_kernel(const u16* __restrict_
       c8 = *reinterpret_cast<const uint64_t*>(code + (size_t)win * C2 + dco0);
       d8 = *reinterpret_cast<const u16x8*>(dp + (size_t)win * C2 + dco0);
     }
-    const size_t base = ((size_t)b * H1 + y) * H1 * C1;  // h1 row y of image b; chunk i -> (ky, x, ci0)
+    const size_t base = ((size_t)b * H1 + y) * H1 * C1;  // chunk i of rows y..y+2 -> (ky, x, ci0)
     hv0 = *reinterpret_cast<const u16x8*>(h1 + base + (size_t)threadIdx.x * 8);
     if (threadIdx.x + 256 < HCHUNKS) hv1 = *reinterpret_cast<const u16x8*>(h1 + base + (size_t)(threadIdx.x + 256) * 8);
   };
-  auto store_h = [&](int i, const u16x8& v) {
-    const int ky = i / (H1 * 4), rem = i - ky * (H1 * 4), xx = rem >> 2, ci0 = (rem & 3) * 8;
-#pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      const int xd = xx - s;
-      if (xd >= 0 && xd < 32) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) hT[((ky * 3 + s) * C1 + ci0 + j) * HTS + xd] = v[j];
-      }
-    }
+  auto store_h = [&](u16* hn, int i, const u16x8& v) {
+    const int ky = i / (H1 * 4), rem = i - ky * (H1 * 4);
+    *reinterpret_cast<u16x8*>(&hn[(ky * HNR + (rem >> 2)) * HNS + (rem & 3) * 8]) = v;
   };
   if (row0 < row1) load_row(row0);
   __syncthreads();
-  for (int gr = row0; gr < row1; ++gr) {
+  for (int gr = row0, st = 0; gr < row1; ++gr, st ^= 1) {
+    u16* dyn = img + st * WG_BUF;
+    u16* hn = dyn + 32 * DYN;
     const int y = gr - (gr / H2) * H2;
-    if (threadIdx.x < 192) {  // dy2 row, written transposed
+    if (threadIdx.x < 192) {
       const int q = (y & 1) * 2 + (dx & 1);
+      u16x8 u;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const uint32_t c = (uint32_t)(c8 >> (8 * j)) & 0xffu;
         const float v = ((c & 3u) == (uint32_t)q && (c & 12u) == 12u) ? bf2f(d8[j]) * dscale : 0.f;
         db[j] += v;
-        dyT[(dco0 + j) * DYS + dx] = f2bf(v);
+        u[j] = f2bf(v);
       }
+      *reinterpret_cast<u16x8*>(&dyn[dx * DYN + dco0]) = u;
     }
-    store_h(threadIdx.x, hv0);
-    if (threadIdx.x + 256 < HCHUNKS) store_h(threadIdx.x + 256, hv1);
+    store_h(hn, threadIdx.x, hv0);
+    if (threadIdx.x + 256 < HCHUNKS) store_h(hn, threadIdx.x + 256, hv1);
     __syncthreads();
     if (gr + 1 < row1) load_row(gr + 1);  // in flight during the MFMAs below
-    const bf16x8 a = as_bf(*reinterpret_cast<const u16x8*>(&dyT[(wave * 16 + r) * DYS + h * 8]));
+    const bf16x8 a = tr_frag16(dyn, DYN, 0, wave * 16, lane);
 #pragma unroll
     for (int n = 0; n < 18; ++n) {
-      const bf16x8 bf = as_bf(*reinterpret_cast<const u16x8*>(&hT[((n >> 1) * C1 + (n & 1) * 16 + r) * HTS + h * 8]));
+      const int t = n >> 1;
+      const bf16x8 bf = tr_frag16(hn + (t / 3) * HNR * HNS, HNS, t % 3, (n & 1) * 16, lane);
       acc[n] = mfma16(a, bf, acc[n]);
     }
-    __syncthreads();
   }
   float* out = part2 + (size_t)blockIdx.x * P2;
 #pragma unroll
@@ -386,11 +443,14 @@ __global__ __launch_bounds__(256) void conv_grad_reduce_kernel(const float* __re
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (col < P2 + P1) {
     int k = sl;
-    for (; k + 12 < n; k += 16) {
-      s0 += src[(size_t)k * stride];
-      s1 += src[(size_t)(k + 4) * stride];
-      s2 += src[(size_t)(k + 8) * stride];
-      s3 += src[(size_t)(k + 12) * stride];
+    for (; k + 28 < n; k += 32) {  // 8 independent loads in flight per round
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(k + 4 * u) * stride];
+      s0 += v[0] + v[4];
+      s1 += v[1] + v[5];
+      s2 += v[2] + v[6];
+      s3 += v[3] + v[7];
     }
     for (; k < n; k += 4) s0 += src[(size_t)k * stride];
   }

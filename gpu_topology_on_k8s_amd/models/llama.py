@@ -188,12 +188,32 @@ class FlatParams:
         if not self.direct:
             self.grad.zero_()
             return
-        for n in self.names:  # direct gradients are overwritten by their first GEMM instead
-            if n not in self.direct:
-                o, e = self.span(n)
-                self.grad[o:e].zero_()
+        for o, e in self._zero_runs():  # direct gradients are overwritten by their first writer instead
+            self.grad[o:e].zero_()
         for n in self.direct:
             self.direct[n] = True
+
+    def _zero_runs(self) -> List[Tuple[int, int]]:
+        """Maximal runs of consecutive non-direct parameters (alignment padding included): one fill
+        kernel per run instead of one per parameter."""
+        key = tuple(sorted(self.direct))
+        if getattr(self, "_runs_key", None) != key:
+            runs: List[Tuple[int, int]] = []
+            for n in self.names:
+                o = self.offsets[n]
+                e = self.span(n)[1]
+                if n in self.direct:
+                    continue
+                if runs and runs[-1][1] >= o - (_ALIGN - 1) and self._only_padding(runs[-1][1], o):
+                    runs[-1] = (runs[-1][0], e)
+                else:
+                    runs.append((o, e))
+            self._runs, self._runs_key = runs, key
+        return self._runs
+
+    def _only_padding(self, a: int, b: int) -> bool:
+        """True when no parameter starts in [a, b) (the gap is alignment padding, zero anyway)."""
+        return all(not (a <= self.offsets[n] < b) for n in self.names)
 
     def span(self, name: str) -> Tuple[int, int]:
         o = self.offsets[name]
