@@ -886,6 +886,10 @@ std::vector<at::Tensor> conv2_pool_fwd(const at::Tensor& h1, const at::Tensor& w
 void conv_bwd(const at::Tensor& dp, const at::Tensor& code, const at::Tensor& x, const at::Tensor& h1, const at::Tensor& w1,
               const at::Tensor& b1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& gw1, at::Tensor& gb1, at::Tensor& gw2,
               at::Tensor& gb2, double p_drop, bool accumulate);
+std::vector<at::Tensor> relu_dropout_fwd(const at::Tensor& h, const at::Tensor& step, int64_t seed, double p_drop);
+at::Tensor relu_dropout_bwd(const at::Tensor& dy, const at::Tensor& mask, at::Tensor& gb, double p_drop, bool accumulate);
+std::vector<at::Tensor> xent10_fwd(const at::Tensor& logits, const at::Tensor& labels);
+at::Tensor xent10_bwd(const at::Tensor& dlog, const at::Tensor& g, at::Tensor& gb, bool accumulate);
 }  // namespace gtk_mnist
 
 namespace gtk_attn {  // csrc/ops/attention.hip
@@ -924,5 +928,9 @@ PYBIND11_MODULE(_fused, m) {
   m.def("mnist_conv1_fwd", &gtk_mnist::conv1_fwd, "MNIST conv1 + ReLU, NHWC bf16");
   m.def("mnist_conv2_pool_fwd", &gtk_mnist::conv2_pool_fwd, "MNIST conv2 + ReLU + 2x2 max-pool + dropout (MFMA)");
   m.def("mnist_conv_bwd", &gtk_mnist::conv_bwd, "MNIST conv stack backward into the flat gradient (MFMA)");
+  m.def("mnist_relu_dropout_fwd", &gtk_mnist::relu_dropout_fwd, "ReLU + hash dropout, keep mask");
+  m.def("mnist_relu_dropout_bwd", &gtk_mnist::relu_dropout_bwd, "ReLU/dropout backward + bias gradient");
+  m.def("mnist_xent10_fwd", &gtk_mnist::xent10_fwd, "10-class softmax cross-entropy: mean loss + unscaled gradient");
+  m.def("mnist_xent10_bwd", &gtk_mnist::xent10_bwd, "scaled logits gradient + bias gradient");
   m.def("transpose_bf16", &gtk_xpose::transpose_bf16, "contiguous [R, C] bf16 -> [C, R] (R, C multiples of 64)");
 }

@@ -469,6 +469,108 @@ __global__ __launch_bounds__(256) void conv_grad_reduce_kernel(const float* __re
   *dst = f2bf(s);
 }
 
+// ------------------------------------------------------------------------ classifier head glue
+// fc1 -> ReLU -> dropout -> fc2 -> softmax cross-entropy around two library GEMMs per direction:
+// each kernel below replaces 2-5 framework launches (elementwise, bias reduction, fills, casts).
+constexpr int HID = 128, NCLS = 10;
+
+// h [B,128] bf16 (fc1 output incl. bias) -> y = keep && h > 0 ? h / (1-p) : 0, code bit0 = keep && h > 0
+__global__ __launch_bounds__(256) void relu_dropout_fwd_kernel(const u16* __restrict__ hin, u16* __restrict__ y,
+                                                               uint8_t* __restrict__ mask, const float* __restrict__ tptr,
+                                                               uint32_t seed, uint32_t drop_thresh, float keep_scale, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t step = (uint32_t)tptr[0];
+  const float v = bf2f(hin[i]);
+  const bool pass = v > 0.f && (hash3(seed, step, (uint32_t)i) >> 8) >= drop_thresh;
+  y[i] = f2bf(pass ? v * keep_scale : 0.f);
+  mask[i] = pass ? 1 : 0;
+}
+
+// dh = mask ? dy / (1-p) : 0, and fc1's bias gradient = column sums of dh (into the flat buffer).
+// Block = 64 columns x 16 row slices.
+__global__ __launch_bounds__(1024) void relu_dropout_bwd_kernel(const u16* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                                u16* __restrict__ dh, u16* __restrict__ gb, float keep_scale,
+                                                                int rows, int accumulate) {
+  __shared__ float red[16][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), sl = threadIdx.x >> 6;
+  float s = 0.f;
+  for (int r = sl; r < rows; r += 16) {
+    const size_t i = (size_t)r * HID + c;
+    const float v = mask[i] ? bf2f(dy[i]) * keep_scale : 0.f;
+    const u16 vb = f2bf(v);
+    dh[i] = vb;
+    s += bf2f(vb);  // the bias gradient of exactly the dh the weight-gradient GEMM sees
+  }
+  red[sl][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (sl == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][threadIdx.x & 63];
+    if (accumulate) t += bf2f(gb[c]);
+    gb[c] = f2bf(t);
+  }
+}
+
+// Softmax cross-entropy over 10 classes, mean over rows, one block: loss and the unscaled gradient
+// dlog = (softmax - onehot) / B in one pass (the backward only scales it).
+__global__ __launch_bounds__(256) void xent10_fwd_kernel(const u16* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                         float* __restrict__ loss, float* __restrict__ dlog, int rows) {
+  __shared__ float red[4];
+  float s = 0.f;
+  const float inv = 1.f / (float)rows;
+  for (int r = threadIdx.x; r < rows; r += 256) {
+    float z[NCLS], m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < NCLS; ++k) {
+      z[k] = bf2f(logits[(size_t)r * NCLS + k]);
+      m = fmaxf(m, z[k]);
+    }
+    float e = 0.f;
+#pragma unroll
+    for (int k = 0; k < NCLS; ++k) {
+      z[k] = __expf(z[k] - m);
+      e += z[k];
+    }
+    const int lab = (int)labels[r];
+    const float lse = m + __logf(e), ie = 1.f / e;
+    s += lse - bf2f(logits[(size_t)r * NCLS + lab]);
+#pragma unroll
+    for (int k = 0; k < NCLS; ++k) dlog[(size_t)r * NCLS + k] = (z[k] * ie - (k == lab ? 1.f : 0.f)) * inv;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) loss[0] = (red[0] + red[1] + red[2] + red[3]) * inv;
+}
+
+// dlogits = g * dlog (bf16) and fc2's bias gradient = column sums of it (into the flat buffer).
+__global__ __launch_bounds__(256) void xent10_bwd_kernel(const float* __restrict__ dlog, const float* __restrict__ g,
+                                                         u16* __restrict__ dlogits, u16* __restrict__ gb, int rows,
+                                                         int accumulate) {
+  __shared__ float red[25][NCLS];
+  const float gs = g[0];
+  const int c = threadIdx.x % NCLS, sl = threadIdx.x / NCLS;  // 25 slices x 10 columns (250 threads)
+  float s = 0.f;
+  if (sl < 25) {
+    for (int r = sl; r < rows; r += 25) {
+      const u16 vb = f2bf(dlog[(size_t)r * NCLS + c] * gs);
+      dlogits[(size_t)r * NCLS + c] = vb;
+      s += bf2f(vb);
+    }
+    red[sl][c] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < NCLS) {
+    float t = 0.f;
+    for (int k = 0; k < 25; ++k) t += red[k][threadIdx.x];
+    if (accumulate) t += bf2f(gb[threadIdx.x]);
+    gb[threadIdx.x] = f2bf(t);
+  }
+}
+
 #define CHECK_BF16(t) TORCH_CHECK((t).is_cuda() && (t).scalar_type() == at::kBFloat16 && (t).is_contiguous(), #t " must be a contiguous bf16 GPU tensor")
 
 void check_w(const at::Tensor& w1, const at::Tensor& b1, const at::Tensor& w2, const at::Tensor& b2) {
@@ -551,6 +653,60 @@ void conv_bwd(const at::Tensor& dp, const at::Tensor& code, const at::Tensor& x,
   static_assert(P2 % 64 == 0 && P1 % 64 == 0, "reduce blocks must not straddle the two partial sets");
   hipLaunchKernelGGL(conv_grad_reduce_kernel, dim3((P2 + P1) / 64), dim3(256), 0, st, part1.data_ptr<float>(), n1,
                      part2.data_ptr<float>(), n2, bpm(gw1), bpm(gb1), bpm(gw2), bpm(gb2), accumulate ? 1 : 0);
+}
+
+}  // namespace gtk_mnist
+
+namespace gtk_mnist {
+
+std::vector<at::Tensor> relu_dropout_fwd(const at::Tensor& h, const at::Tensor& step, int64_t seed, double p_drop) {
+  CHECK_BF16(h);
+  TORCH_CHECK(h.dim() == 2 && h.size(1) == HID, "fc1 output must be [B,128]");
+  TORCH_CHECK(step.is_cuda() && step.scalar_type() == at::kFloat, "step must be a fp32 GPU tensor");
+  const int n = (int)h.numel();
+  auto y = at::empty_like(h);
+  auto mask = at::empty(h.sizes(), h.options().dtype(at::kByte));
+  hipLaunchKernelGGL(relu_dropout_fwd_kernel, dim3((n + 255) / 256), dim3(256), 0, cur_stream(), bp(h), bpm(y),
+                     mask.data_ptr<uint8_t>(), step.data_ptr<float>(), (uint32_t)seed, drop_threshold(p_drop),
+                     (float)(1.0 / (1.0 - p_drop)), n);
+  return {y, mask};
+}
+
+at::Tensor relu_dropout_bwd(const at::Tensor& dy, const at::Tensor& mask, at::Tensor& gb, double p_drop, bool accumulate) {
+  CHECK_BF16(dy);
+  CHECK_BF16(gb);
+  TORCH_CHECK(dy.dim() == 2 && dy.size(1) == HID && mask.numel() == dy.numel() && mask.scalar_type() == at::kByte &&
+              mask.is_contiguous() && gb.numel() == HID, "relu_dropout_bwd: shapes");
+  auto dh = at::empty_like(dy);
+  hipLaunchKernelGGL(relu_dropout_bwd_kernel, dim3(HID / 64), dim3(1024), 0, cur_stream(), bp(dy), mask.data_ptr<uint8_t>(),
+                     bpm(dh), bpm(gb), (float)(1.0 / (1.0 - p_drop)), (int)dy.size(0), accumulate ? 1 : 0);
+  return dh;
+}
+
+std::vector<at::Tensor> xent10_fwd(const at::Tensor& logits, const at::Tensor& labels) {
+  CHECK_BF16(logits);
+  TORCH_CHECK(logits.dim() == 2 && logits.size(1) == NCLS, "logits must be [B,10]");
+  TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous() &&
+              labels.numel() == logits.size(0), "labels must be int64 [B]");
+  const int rows = (int)logits.size(0);
+  auto loss = at::empty({}, logits.options().dtype(at::kFloat));
+  auto dlog = at::empty({rows, NCLS}, logits.options().dtype(at::kFloat));
+  hipLaunchKernelGGL(xent10_fwd_kernel, dim3(1), dim3(256), 0, cur_stream(), bp(logits), labels.data_ptr<int64_t>(),
+                     loss.data_ptr<float>(), dlog.data_ptr<float>(), rows);
+  return {loss, dlog};
+}
+
+at::Tensor xent10_bwd(const at::Tensor& dlog, const at::Tensor& g, at::Tensor& gb, bool accumulate) {
+  TORCH_CHECK(dlog.is_cuda() && dlog.scalar_type() == at::kFloat && dlog.is_contiguous() && dlog.dim() == 2 &&
+              dlog.size(1) == NCLS, "dlog must be fp32 [B,10]");
+  TORCH_CHECK(g.is_cuda() && g.scalar_type() == at::kFloat && g.numel() == 1, "g must be a fp32 GPU scalar");
+  CHECK_BF16(gb);
+  TORCH_CHECK(gb.numel() == NCLS, "fc2 bias gradient must have 10 entries");
+  const int rows = (int)dlog.size(0);
+  auto dlogits = at::empty({rows, NCLS}, dlog.options().dtype(at::kBFloat16));
+  hipLaunchKernelGGL(xent10_bwd_kernel, dim3(1), dim3(256), 0, cur_stream(), dlog.data_ptr<float>(), g.data_ptr<float>(),
+                     bpm(dlogits), bpm(gb), rows, accumulate ? 1 : 0);
+  return dlogits;
 }
 
 }  // namespace gtk_mnist

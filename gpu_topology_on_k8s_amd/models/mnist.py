@@ -16,6 +16,9 @@ bound by launch latency, not by MFMA throughput or HBM.  The design therefore mi
 * batches are synthesised on the device (no host->device copy per step);
 * the whole step — batch synthesis, forward, backward, gradient all-reduce, clipping, AdamW — is
   captured once into a hipGraph and replayed (``models/train.py --graph``), one host launch per step;
+* the classifier head is two library GEMMs per direction around four HIP kernels (ReLU+dropout and
+  softmax cross-entropy, forward and backward, each also producing a bias gradient), with the
+  weight-gradient GEMMs writing the flat buffer (no zero fills, no AccumulateGrad adds);
 * the convolution stack is five hand-written HIP launches (``csrc/ops/mnist_conv.hip``): conv1+ReLU;
   conv2+ReLU+2x2 max-pool+dropout as one MFMA implicit GEMM whose accumulator rows are the pooling
   windows; backward as an MFMA dgrad that rebuilds dy2 from the pooled gradient and folds conv1's
@@ -93,14 +96,14 @@ class _ConvStack(torch.autograd.Function):
     writes the four conv gradients straight into the flat buffer (no autograd accumulation)."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, model):
+    def forward(ctx, x, w1, b1, w2, b2, model, step):
         from ..ops import fused
 
         hip = fused.hip()
         p_drop = model.cfg.p1 if model.training else 0.0
         x = x.reshape(x.shape[0], model.cfg.image, model.cfg.image)
         h1 = hip.mnist_conv1_fwd(x, w1.detach(), b1.detach())
-        p, code = hip.mnist_conv2_pool_fwd(h1, w2.detach(), b2.detach(), model.dropout_step(), model.drop_seed, p_drop)
+        p, code = hip.mnist_conv2_pool_fwd(h1, w2.detach(), b2.detach(), step, model.drop_seed, p_drop)
         ctx.save_for_backward(x, h1, code)
         ctx.model, ctx.p_drop = model, p_drop
         return p.view(p.shape[0], -1)
@@ -117,7 +120,57 @@ class _ConvStack(torch.autograd.Function):
         fused.hip().mnist_conv_bwd(dp.contiguous(), code, x, h1, *w, *g, ctx.p_drop, not fresh)
         for n in _CONV_PARAMS:
             flat.mark_written(n)
-        return None, None, None, None, None, None
+        return None, None, None, None, None, None, None
+
+
+_HEAD_PARAMS = ("fc1.w", "fc1.b", "fc2.w", "fc2.b")
+
+
+class _Head(torch.autograd.Function):
+    """fc1 -> ReLU -> dropout -> fc2 -> mean softmax cross-entropy.  Library GEMMs (bias in the
+    epilogue) plus four HIP kernels (``relu_dropout`` fwd/bwd, ``xent10`` fwd/bwd) that also produce
+    the bias gradients; weight gradients are GEMMs into the flat buffer (``mm(out=)``), so neither
+    an AccumulateGrad add nor a zero fill runs."""
+
+    @staticmethod
+    def forward(ctx, feats, w1, b1, w2, b2, labels, model, step):
+        from ..ops import fused
+
+        hip = fused.hip()
+        p_drop = model.cfg.p2 if model.training else 0.0
+        w1, b1, w2, b2 = w1.detach(), b1.detach(), w2.detach(), b2.detach()
+        h = torch.addmm(b1, feats, w1.t())
+        h2, mask = hip.mnist_relu_dropout_fwd(h, step, model.drop_seed ^ 0x5BD1E995, p_drop)
+        logits = torch.addmm(b2, h2, w2.t())
+        loss, dlog = hip.mnist_xent10_fwd(logits, labels)
+        ctx.save_for_backward(feats, h2, mask, dlog)
+        ctx.model, ctx.p_drop = model, p_drop
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        from ..ops import fused
+
+        hip = fused.hip()
+        feats, h2, mask, dlog = ctx.saved_tensors
+        flat = ctx.model.flat
+        P = flat.params
+        acc = not flat.direct["fc1.w"]
+        dlogits = hip.mnist_xent10_bwd(dlog, g.float().reshape(1).contiguous(), P["fc2.b"].grad, acc)
+        if acc:
+            P["fc2.w"].grad.addmm_(dlogits.t(), h2)
+        else:
+            torch.mm(dlogits.t(), h2, out=P["fc2.w"].grad)
+        dh2 = dlogits.mm(P["fc2.w"].detach())
+        dh = hip.mnist_relu_dropout_bwd(dh2, mask, P["fc1.b"].grad, ctx.p_drop, acc)
+        if acc:
+            P["fc1.w"].grad.addmm_(dh.t(), feats)
+        else:
+            torch.mm(dh.t(), feats, out=P["fc1.w"].grad)
+        dfeats = dh.mm(P["fc1.w"].detach())
+        for n in _HEAD_PARAMS:
+            flat.mark_written(n)
+        return dfeats, None, None, None, None, None, None, None
 
 
 class MnistCNN(torch.nn.Module):
@@ -133,7 +186,7 @@ class MnistCNN(torch.nn.Module):
         dev = self.flat.data.device
         self.conv = conv if dev.type == "cuda" else "torch"
         if self.conv == "hip":
-            for n in _CONV_PARAMS:  # gradients written by the HIP backward, not by autograd
+            for n in _CONV_PARAMS + _HEAD_PARAMS:  # gradients written by the HIP backward, not by autograd
                 self.flat.mark_direct(n)
         # dropout of the HIP path: counter-based hash of (seed, step, element); ``step_counter`` is
         # the optimizer's device step count when set (graph mode), else a per-forward counter
@@ -180,11 +233,13 @@ class MnistCNN(torch.nn.Module):
         self._own_step.add_(1.0)
         return self._own_step
 
-    def conv_features(self, x: torch.Tensor) -> torch.Tensor:
-        """[B,1,28,28] -> pooled features [B, 9216] in NHWC order (fc1's input)."""
+    def conv_features(self, x: torch.Tensor, step: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """[B,1,28,28] -> pooled features [B, 9216] in NHWC order (fc1's input).  ``step``: the
+        dropout counter value of this forward (drawn here when not given)."""
         c = self.cfg
         if self.conv == "hip" and x.is_cuda:
-            return _ConvStack.apply(x, *(self.P(n) for n in _CONV_PARAMS), self)
+            return _ConvStack.apply(x, *(self.P(n) for n in _CONV_PARAMS), self,
+                                    step if step is not None else self.dropout_step())
         w1 = self.P("conv1.w").permute(0, 3, 1, 2)  # channels-last storage -> OIHW
         w2 = self.P("conv2.w").permute(0, 3, 1, 2)
         h = F.relu(F.conv2d(x, w1, self.P("conv1.b")))
@@ -194,6 +249,10 @@ class MnistCNN(torch.nn.Module):
 
     def forward(self, x: torch.Tensor, labels: Optional[torch.Tensor] = None) -> torch.Tensor:
         c = self.cfg
+        if self.conv == "hip" and x.is_cuda and labels is not None:
+            step = self.dropout_step()
+            feats = self.conv_features(x, step)
+            return _Head.apply(feats, *(self.P(n) for n in _HEAD_PARAMS), labels, self, step)
         h = self.conv_features(x)
         h = F.dropout(F.relu(F.linear(h, self.P("fc1.w"), self.P("fc1.b"))), c.p2, self.training)
         logits = F.linear(h, self.P("fc2.w"), self.P("fc2.b"))

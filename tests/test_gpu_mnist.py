@@ -166,3 +166,29 @@ def test_hip_conv_training_beats_library_conv():
     assert hip_conv["conv"] == "hip" and torch_conv["conv"] == "torch"
     assert hip_conv["loss_last"] < 0.5 * hip_conv["loss_first"]
     assert hip_conv["ms_per_step"] < torch_conv["ms_per_step"]
+
+
+def test_hip_head_matches_fp32_reference():
+    """fc1 -> ReLU -> fc2 -> cross-entropy through the HIP head (eval: no dropout) against fp32."""
+    import torch.nn.functional as F
+
+    from gpu_topology_on_k8s_amd.models.mnist import MnistCNN
+
+    m = MnistCNN(device="cuda", seed=6)
+    m.eval()
+    x, y = m.synthetic_batch(48, torch.Generator(device="cuda").manual_seed(7))
+    m.flat.zero_grad()
+    loss = m(x, y)
+    loss.backward()
+    P = {n: m.flat.params[n].detach().float().clone().requires_grad_(True) for n in ("fc1.w", "fc1.b", "fc2.w", "fc2.b")}
+    feats = m.conv_features(x).detach().float()
+    h = F.relu(feats @ P["fc1.w"].t() + P["fc1.b"])
+    ref = F.cross_entropy(h @ P["fc2.w"].t() + P["fc2.b"], y)
+    ref.backward()
+    assert abs(float(loss) - float(ref)) < 2e-2 * max(1.0, float(ref)), (float(loss), float(ref))
+    for n, t in P.items():
+        e = (m.flat.params[n].grad.float() - t.grad).norm() / t.grad.norm()
+        print(n, float(e))
+        assert e < 3e-2, (n, float(e))
+    # conv gradients flowed through the head's dfeats
+    assert m.flat.params["conv2.w"].grad.float().abs().sum() > 0
