@@ -1,18 +1,19 @@
 // MNIST CNN convolution stack on gfx950 (models/mnist.py, the Gaia paper's Exp. 6 workload).
 //
 // conv1 (1->32, 3x3) + ReLU, conv2 (32->64, 3x3) + ReLU + 2x2 max-pool + dropout, and their backward,
-// as five launches instead of MIOpen's ~45 (layout transposes, casts, bias reductions, naive conv1):
+// as four launches instead of MIOpen's ~45 (layout transposes, casts, bias reductions, naive conv1):
 //
 //   conv1_fwd        FMA, one thread per (pixel, 8 channels); writes h1 NHWC bf16
 //   conv2_pool_fwd   MFMA implicit GEMM, M = output pixels ordered so that a lane's four accumulator
 //                    rows are one 2x2 pooling window (pool = max over the lane's registers, no
 //                    shuffles); epilogue adds bias, ReLU, pools, applies dropout from a counter-based
 //                    hash, writes the pooled map and one code byte per element (argmax | pos | keep)
-//   conv2_dgrad      MFMA implicit GEMM over the 9 taps x 64 output channels; dy2 is never stored: the
+//   conv2_bwd        one launch, two block roles running concurrently:
+//   - dgrad          MFMA implicit GEMM over the 9 taps x 64 output channels; dy2 is never stored: the
 //                    A fragment is rebuilt from the pooled gradient and the code bytes; the epilogue
 //                    applies conv1's ReLU mask and accumulates conv1's weight/bias gradient in
 //                    registers (dz1 is never stored either) -> per-workgroup partials
-//   conv2_wgrad      MFMA, M = 64 output channels, N = 9 taps x 32 input channels, K = output pixels
+//   - wgrad          MFMA, M = 64 output channels, N = 9 taps x 32 input channels, K = output pixels
 //                    of one row (24, padded to 32); dy2 and three column-shifted copies of the h1 rows
 //                    are staged transposed in LDS so every fragment is one 16-byte LDS read
 //   conv_grad_reduce sums the partials in a fixed order (deterministic) into the flat bf16 gradient
@@ -199,16 +200,21 @@ constexpr int XROWS = DG_ROWS + 2;
 // transposed reads give the B operand), the dy2 rows 4g-2 .. 4g+3 rebuilt from the pooled gradient
 // and code bytes into a zero-bordered tile (A operand: one 16-byte read), and the h1 / x rows the
 // epilogue needs for conv1's ReLU mask and weight gradient.
-__global__ __launch_bounds__(256) void conv2_dgrad_kernel(const u16* __restrict__ dp, const uint8_t* __restrict__ code,
-                                                          const u16* __restrict__ w2, const u16* __restrict__ h1,
-                                                          const u16* __restrict__ x, float* __restrict__ part1, float dscale) {
-  __shared__ __attribute__((aligned(16))) u16 ws[C2 * W2S];
-  __shared__ __attribute__((aligned(16))) u16 dyl[XROWS * DYW * DYC];
-  __shared__ __attribute__((aligned(16))) u16 h1t[DG_ROWS * H1 * C1];
-  __shared__ __attribute__((aligned(16))) u16 xt[XROWS * IMG + 8];
-  __shared__ float red[4][P1];
+constexpr int DG_LDS_WS = C2 * W2S * 2, DG_LDS_DY = XROWS * DYW * DYC * 2, DG_LDS_H1 = DG_ROWS * H1 * C1 * 2,
+              DG_LDS_X = (XROWS * IMG + 8) * 2;
+constexpr int DG_LDS = DG_LDS_WS + DG_LDS_DY + DG_LDS_H1 + DG_LDS_X + 4 * P1 * 4;
+
+__device__ __forceinline__ void conv2_dgrad_block(const u16* __restrict__ dp, const uint8_t* __restrict__ code,
+                                                  const u16* __restrict__ w2, const u16* __restrict__ h1,
+                                                  const u16* __restrict__ x, float* __restrict__ part1, float dscale, int blk,
+                                                  char* smem) {
+  u16* ws = reinterpret_cast<u16*>(smem);
+  u16* dyl = reinterpret_cast<u16*>(smem + DG_LDS_WS);
+  u16* h1t = reinterpret_cast<u16*>(smem + DG_LDS_WS + DG_LDS_DY);
+  u16* xt = reinterpret_cast<u16*>(smem + DG_LDS_WS + DG_LDS_DY + DG_LDS_H1);
+  float (*red)[P1] = reinterpret_cast<float (*)[P1]>(smem + DG_LDS_WS + DG_LDS_DY + DG_LDS_H1 + DG_LDS_X);
   constexpr int GROUPS = (H1 + DG_ROWS - 1) / DG_ROWS;  // 7
-  const int b = blockIdx.x / GROUPS, yi0 = (blockIdx.x - b * GROUPS) * DG_ROWS;
+  const int b = blk / GROUPS, yi0 = (blk - b * GROUPS) * DG_ROWS;
   constexpr int WCH = C2 * (KW2 / 8) / 256;         // 9 conv2.w chunks per thread
   constexpr int DTASK = XROWS * DYW * 8;            // 1632 dy2 tasks
   constexpr int DPT = (DTASK + 255) / 256;          // 7 per thread
@@ -332,7 +338,7 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(const u16* __restrict_
     }
   __syncthreads();
   for (int i = threadIdx.x; i < P1; i += 256)
-    part1[(size_t)blockIdx.x * P1 + i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    part1[(size_t)blk * P1 + i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
 }
 
 // ------------------------------------------------------------------- conv2 wgrad partials (MFMA)
@@ -347,18 +353,20 @@ constexpr int WG_BUF = 32 * DYN + 3 * HNR * HNS;  // one stage: dy2 image + h1 i
 // both MFMA operands, whose k index is the pixel, are read transposed (tr_frag16); a tap's column
 // shift kx is a row offset of the h1 image.  Two LDS stages: the next row's loads are in flight during
 // this row's MFMAs and one barrier per row suffices.
-__global__ __launch_bounds__(256) void conv2_wgrad_kernel(const u16* __restrict__ dp, const uint8_t* __restrict__ code,
-                                                          const u16* __restrict__ h1, float* __restrict__ part2, float dscale,
-                                                          int nrows, int rows_per_wg) {
-  __shared__ __attribute__((aligned(16))) u16 img[2 * WG_BUF];
-  __shared__ float dbp[192][9];
+constexpr int WG_LDS = 2 * WG_BUF * 2 + 192 * 9 * 4;
+
+__device__ __forceinline__ void conv2_wgrad_block(const u16* __restrict__ dp, const uint8_t* __restrict__ code,
+                                                  const u16* __restrict__ h1, float* __restrict__ part2, float dscale, int nrows,
+                                                  int rows_per_wg, int blk, char* smem) {
+  u16* img = reinterpret_cast<u16*>(smem);
+  float (*dbp)[9] = reinterpret_cast<float (*)[9]>(smem + 2 * WG_BUF * 2);
   for (int i = threadIdx.x; i < 2 * WG_BUF; i += 256) img[i] = 0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 15, h = lane >> 4;
   f32x4 acc[18];
 #pragma unroll
   for (int n = 0; n < 18; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
   float db[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int row0 = blockIdx.x * rows_per_wg, row1 = min(nrows, row0 + rows_per_wg);
+  const int row0 = blk * rows_per_wg, row1 = min(nrows, row0 + rows_per_wg);
   // staging tasks: one dy2 (x, 8-channel chunk) if tid < 192; h1 chunks tid and tid + 256
   const int dx = threadIdx.x >> 3, dco0 = (threadIdx.x & 7) * 8;
   uint64_t c8 = 0;
@@ -408,7 +416,7 @@ __global__ __launch_bounds__(256) void conv2_wgrad_kernel(const u16* __restrict_
       acc[n] = mfma16(a, bf, acc[n]);
     }
   }
-  float* out = part2 + (size_t)blockIdx.x * P2;
+  float* out = part2 + (size_t)blk * P2;
 #pragma unroll
   for (int n = 0; n < 18; ++n)
 #pragma unroll
@@ -424,6 +432,19 @@ __global__ __launch_bounds__(256) void conv2_wgrad_kernel(const u16* __restrict_
     for (int xx = 0; xx < H2; ++xx) s += dbp[xx * 8 + chunk][j];
     out[NW2 + threadIdx.x] = s;
   }
+}
+
+// Both backward GEMMs in one launch (they are independent): blocks [0, n2) compute conv2's weight
+// gradient, blocks [n2, n2 + n1) the data gradient + conv1's weight gradient, concurrently.
+__global__ __launch_bounds__(256) void conv2_bwd_kernel(const u16* __restrict__ dp, const uint8_t* __restrict__ code,
+                                                        const u16* __restrict__ w2, const u16* __restrict__ h1,
+                                                        const u16* __restrict__ x, float* __restrict__ part1,
+                                                        float* __restrict__ part2, float dscale, int nrows, int rows_per_wg, int n2) {
+  __shared__ __attribute__((aligned(16))) char smem[DG_LDS > WG_LDS ? DG_LDS : WG_LDS];
+  if ((int)blockIdx.x < n2)
+    conv2_wgrad_block(dp, code, h1, part2, dscale, nrows, rows_per_wg, blockIdx.x, smem);
+  else
+    conv2_dgrad_block(dp, code, w2, h1, x, part1, dscale, blockIdx.x - n2, smem);
 }
 
 // ------------------------------------------------------------------------ partials -> gradient
@@ -646,10 +667,8 @@ void conv_bwd(const at::Tensor& dp, const at::Tensor& code, const at::Tensor& x,
   auto part1 = at::empty({n1, P1}, opts);
   auto part2 = at::empty({n2, P2}, opts);
   hipStream_t st = cur_stream();
-  hipLaunchKernelGGL(conv2_dgrad_kernel, dim3(n1), dim3(256), 0, st, bp(dp), code.data_ptr<uint8_t>(), bp(w2), bp(h1), bp(x),
-                     part1.data_ptr<float>(), dscale);
-  hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(n2), dim3(256), 0, st, bp(dp), code.data_ptr<uint8_t>(), bp(h1),
-                     part2.data_ptr<float>(), dscale, nrows, rows_per_wg);
+  hipLaunchKernelGGL(conv2_bwd_kernel, dim3(n2 + n1), dim3(256), 0, st, bp(dp), code.data_ptr<uint8_t>(), bp(w2), bp(h1), bp(x),
+                     part1.data_ptr<float>(), part2.data_ptr<float>(), dscale, nrows, rows_per_wg, n2);
   static_assert(P2 % 64 == 0 && P1 % 64 == 0, "reduce blocks must not straddle the two partial sets");
   hipLaunchKernelGGL(conv_grad_reduce_kernel, dim3((P2 + P1) / 64), dim3(256), 0, st, part1.data_ptr<float>(), n1,
                      part2.data_ptr<float>(), n2, bpm(gw1), bpm(gb1), bpm(gw2), bpm(gb2), accumulate ? 1 : 0);
