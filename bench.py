@@ -68,6 +68,9 @@ def parse(argv=None):
                          f"{TUNE_CANDIDATES} at k >= 2 (untimed, before warmup), 'tune' = that pass at any k, "
                          "'default' = RCCL's choice, or MIN[:MAX]")
     ap.add_argument("--tune-steps", type=int, default=3, help="timed all-reduces per candidate in the tuning pass")
+    ap.add_argument("--rccl-log", default="auto", choices=["auto", "on", "off"],
+                    help="capture RCCL's INIT/GRAPH log (per-rank file under /tmp) and report the transports and "
+                         "channel counts it chose; auto = on for k >= 2")
     ap.add_argument("--sweep", default="auto",
                     help="after the headline timing: exact-checked size sweep MIN:MAX:FACTOR (nccl-tests style, "
                          "BASELINE.md target 3, peak busBW reported); 'auto' = 8:16G:8 on GPUs, 8:1M:8 for "
@@ -230,6 +233,13 @@ def main(argv=None) -> int:
     if not in_launcher:
         os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    rccl_log = None
+    if args.backend != "cpu" and (args.rccl_log == "on" or (args.rccl_log == "auto" and args.gpus > 1)) \
+            and "NCCL_DEBUG" not in os.environ:
+        from gpu_topology_on_k8s_amd.parallel.allreduce import rccl_log_env
+
+        rccl_log = f"/tmp/gtk_rccl_{os.environ.get('MASTER_PORT', '0')}_{os.environ.get('RANK', '0')}"
+        os.environ.update(rccl_log_env(rccl_log))  # before any communicator exists
 
     import torch
     import torch.distributed as dist
@@ -341,6 +351,17 @@ def main(argv=None) -> int:
             print(f"bench: graph latency aborted on rank {env.rank}: {e}", file=sys.stderr)
             graph = {"error": str(e)[:300]}
     runner.close()
+    rccl = None
+    if rccl_log and env.rank == 0:
+        from gpu_topology_on_k8s_amd.parallel.allreduce import rccl_log_summary
+
+        path = f"{rccl_log}.{os.getpid()}"
+        try:
+            with open(path) as f:
+                rccl = rccl_log_summary(f.read())
+            rccl["log"] = path
+        except OSError as e:
+            rccl = {"error": str(e)[:200]}
     if env.rank == 0:
         bound = (choice.extra.get("probe") or {}).get("subset_ingress_bound_gbps")  # K5/K1 ceiling of busBW
         out = {
@@ -380,6 +401,7 @@ def main(argv=None) -> int:
             "k8s_placement": choice.extra.get("k8s"),
             "size_sweep": sweep,
             "graph_latency": graph,
+            "rccl": rccl,
             "value_kind": "busbw" if env.world > 1 else "algbw (busbw = 0 at k=1)",
             "busbw_vs_probe_bound": round(busbw / bound, 4) if bound else None,
             "algbw_gbps": round(algbw, 3),

@@ -25,11 +25,49 @@ from typing import Dict, List, Optional, Sequence
 
 log = logging.getLogger(__name__)
 
-__all__ = ["DistEnv", "choose_subset", "probe_node", "probe_summary", "AllReduceRunner", "bus_factor"]
+__all__ = ["DistEnv", "choose_subset", "probe_node", "probe_summary", "AllReduceRunner", "bus_factor", "rccl_log_env",
+           "rccl_log_summary"]
 
 
 def bus_factor(k: int) -> float:
     return 2.0 * (k - 1) / k if k > 1 else 0.0
+
+
+def rccl_log_env(path_prefix: str) -> Dict[str, str]:
+    """Environment that makes RCCL write its init/graph log to ``<prefix>.<pid>`` (set before the
+    first communicator is created): the transport of every ring edge and the channel counts RCCL
+    chose on this node."""
+    return {"NCCL_DEBUG": "INFO", "NCCL_DEBUG_SUBSYS": "INIT,GRAPH", "NCCL_DEBUG_FILE": f"{path_prefix}.%p"}
+
+
+_RE_COMM = None
+
+
+def rccl_log_summary(text: str) -> Dict[str, object]:
+    """What RCCL decided, from its INFO log: communicators (rank count), channel counts, and how
+    every channel edge is carried (``P2P/IPC``, ``P2P/direct pointer``, ``SHM``, ``NET``...)."""
+    import re
+
+    global _RE_COMM
+    if _RE_COMM is None:
+        _RE_COMM = (re.compile(r"nRanks (\d+)"), re.compile(r"(\d+) coll channels"),
+                    re.compile(r"Channel \d+/\d+ : \S+ -> \S+ via (.+?)(?: comm 0x\S+)?\s*$"), None)
+    r_ranks, r_coll, r_via, _ = _RE_COMM
+    comms, channels, via, version = [], [], {}, None
+    for line in text.splitlines():
+        m = r_ranks.search(line)
+        if m and "comm 0x" in line:
+            comms.append(int(m.group(1)))
+        m = r_coll.search(line)
+        if m:
+            channels.append(int(m.group(1)))
+        m = r_via.search(line)
+        if m:
+            via[m.group(1)] = via.get(m.group(1), 0) + 1
+        if version is None and "version" in line and ("RCCL" in line or "NCCL" in line):
+            version = line.split("INFO", 1)[-1].strip()[:80]
+    return {"communicators": len(comms), "nranks": sorted(set(comms)), "coll_channels": sorted(set(channels)),
+            "edges_via": via, "version": version}
 
 
 @dataclass

@@ -143,3 +143,22 @@ def test_bench_four_ranks_on_amdsmi_discovered_node():
     assert cfg["topology_source"].startswith("amdsmi") and len(cfg["subset"]) == 4
     assert cfg["worst_subset"] is not None and cfg["worst_score"] < cfg["placement_score"]
     assert out["k8s_placement"]["assigned"] is True
+
+
+def test_rccl_log_summary_parses_transports():
+    """bench.py reports how RCCL carried every ring edge (k >= 2) from its INFO log."""
+    from gpu_topology_on_k8s_amd.parallel.allreduce import rccl_log_env, rccl_log_summary
+
+    env = rccl_log_env("/tmp/x")
+    assert env["NCCL_DEBUG"] == "INFO" and env["NCCL_DEBUG_FILE"].endswith(".%p")
+    text = "\n".join([
+        "node:123:123 [0] NCCL INFO RCCL version 2.27.7-HEAD:abc",
+        "node:123:130 [0] NCCL INFO comm 0x5555 rank 0 nRanks 2 nNodes 1 localRanks 2 localRank 0 MNNVL 0",
+        "node:123:130 [0] NCCL INFO Channel 00/32 : 0[0] -> 1[1] via P2P/IPC",
+        "node:123:130 [0] NCCL INFO Channel 01/32 : 0[0] -> 1[1] via P2P/IPC",
+        "node:123:130 [0] NCCL INFO Channel 00/0 : 0[2a000] -> 1[3a000] via P2P/direct pointer comm 0x5555",
+        "node:123:130 [0] NCCL INFO 32 coll channels, 32 collnet channels, 0 nvls channels, 32 p2p channels, 2 p2p channels per peer",
+    ])
+    s = rccl_log_summary(text)
+    assert s["communicators"] == 1 and s["nranks"] == [2] and s["coll_channels"] == [32]
+    assert s["edges_via"]["P2P/IPC"] == 2 and "RCCL version 2.27.7" in s["version"]

@@ -240,3 +240,23 @@ def test_device_plugin_daemon_probes_in_child_on_real_node():
         srv.shutdown()
         shutil.rmtree(sockdir, ignore_errors=True)
     assert p.returncode == 0, p.stdout.read() if p.stdout else ""
+
+
+def test_bench_py_reports_rccl_log():
+    """--rccl-log on: RCCL's own INIT log is captured and summarised in the JSON line (on the 8-GPU
+    node this shows the xGMI transport of every ring edge)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if not k.startswith("NCCL_DEBUG")}
+    p = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--size-mb", "16", "--sweep", "off",
+                        "--graph", "off", "--probe", "off", "--rccl-log", "on"], capture_output=True, text=True, timeout=600,
+                       cwd=repo, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    r = out["rccl"]
+    assert r and "error" not in r, r
+    assert r["communicators"] >= 1 and r["nranks"] == [1] and r["version"], r
