@@ -28,7 +28,7 @@ import os
 import threading
 import time
 from concurrent import futures
-from typing import Callable, Dict, Iterable, List, Optional, Sequence, Set, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import grpc
 import numpy as np

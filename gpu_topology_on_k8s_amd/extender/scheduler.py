@@ -41,7 +41,7 @@ from ..k8s.api import ApiError, KubeAPI
 from ..k8s.events import record_event
 from ..k8s.objects import annotations as obj_annotations
 from ..k8s.objects import labels as obj_labels
-from ..k8s.objects import meta, pod_gpu_request, pod_key
+from ..k8s.objects import pod_gpu_request, pod_key
 from ..placement import NoFeasiblePlacement, PlacementPolicy, place_fraction, select
 from ..placement.gaia import gaia_schedule, tree_from_topology
 from ..placement.legacy import design_greedy_select

@@ -16,7 +16,6 @@ replayed (``models/train.py --graph``); the host mirror ``t`` is advanced by :me
 """
 from __future__ import annotations
 
-import math
 from typing import List, Optional, Sequence, Tuple
 
 import torch

@@ -25,7 +25,6 @@ length splits into 8-element-multiple chunks for any world size up to 8.
 """
 from __future__ import annotations
 
-import math
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional

@@ -32,7 +32,7 @@ import random
 from dataclasses import dataclass, field
 from typing import Dict, Iterable, List, Optional, Sequence
 
-from ..topology.model import LinkType, RefLinkClass, Topology
+from ..topology.model import LinkType, Topology
 
 __all__ = ["TreeNode", "CostTree", "gaia_schedule", "fragment", "singular", "link", "tree_from_topology", "tree_from_spec"]
 
