@@ -50,6 +50,20 @@ def _init_dist(device_kind: str) -> Dict[str, int]:
     return {"rank": rank, "world": world, "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}
 
 
+def _pod_devices(env, visible_bdfs=None) -> Dict[str, object]:
+    """Inside a pod: train on the devices the device plugin allocated (``GTK_GPU_GROUP`` node-local
+    indices, ``GTK_GPU_BDFS`` their PCI addresses; ``design.md:239``), rank r on GROUP[r], mapped to
+    this container's HIP ordinals by PCI address (:func:`topology.identity.resolve_group`)."""
+    from ..topology.identity import ENV_GROUP, group_from_env, resolve_group
+
+    group, bdfs = group_from_env()
+    if len(group) != env["world"]:
+        raise ValueError(f"{ENV_GROUP}={group} allocates {len(group)} devices for a job of {env['world']} ranks")
+    hip = resolve_group(group, bdfs=bdfs or None, visible_bdfs=visible_bdfs)
+    return {"devices": group, "hip_devices": hip, "best": group, "best_score": None, "worst": None, "worst_score": None,
+            "source": "pod-allocation"}
+
+
 def _choose_device(env, placement: str, discovery: str, visible: Optional[int] = None) -> Dict[str, object]:
     """Rank 0 places the job; the choice travels through the store.  ``visible`` models a node of
     that many devices without HIP (CPU dry runs of the best-vs-worst harness on a fake node)."""
@@ -67,14 +81,22 @@ def _choose_device(env, placement: str, discovery: str, visible: Optional[int] =
 
 
 def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int = 3, warmup: int = 1, device_kind: str = "cuda",
-          placement: str = "best", discovery: str = "auto", bucket_mb: float = 256.0, checkpoint: bool = False, lr: float = 3e-4,
+          placement: str = "auto", discovery: str = "auto", bucket_mb: float = 256.0, checkpoint: bool = False, lr: float = 3e-4,
           attn: str = "hip", seed: int = 0, log: bool = True, gemm_tuning: str = "auto",
           gemm_table: Optional[str] = None, gemm_layout: str = "nt", overlap_transposes: bool = False,
           zero1: bool = False, save_dir: Optional[str] = None, save_every: int = 0, resume: Optional[str] = None,
           keep: int = 2, fuse_residual: bool = True, overlap_norm: bool = False, same_data: bool = False,
           graph: str = "auto", conv: str = "hip") -> Dict[str, object]:
     env = _init_dist(device_kind)
-    if device_kind == "cuda":
+    if placement == "auto":  # inside a pod the allocation decides; on a bare node, the placement core
+        placement = "pod" if os.environ.get("GTK_GPU_GROUP") else "best"
+    if device_kind == "cuda" and placement == "pod":
+        pl = _pod_devices(env)
+        dev = int(pl["hip_devices"][env["rank"]])
+        torch.cuda.set_device(dev)
+        device = torch.device("cuda", dev)
+        gemm_mode = setup_gemm_tuning(gemm_tuning, gemm_table, env["rank"])
+    elif device_kind == "cuda":
         pl = _choose_device(env, placement, discovery)
         dev = int(pl["hip_devices"][env["rank"]])
         torch.cuda.set_device(dev)
@@ -213,6 +235,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "n_gpus": env["world"],
         "placement": placement,
         "devices": pl["devices"],
+        "placement_source": pl.get("source"),
         "best_devices": pl.get("best"),
         "worst_devices": pl.get("worst"),
         "best_score": pl.get("best_score"),
@@ -260,7 +283,9 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
-    ap.add_argument("--placement", default="best", choices=["best", "worst"])
+    ap.add_argument("--placement", default="auto", choices=["auto", "best", "worst", "pod"],
+                    help="pod = the devices Allocate gave this container (GTK_GPU_GROUP/GTK_GPU_BDFS); best/worst = "
+                         "run the placement core on the node; auto = pod when GTK_GPU_GROUP is set, else best")
     ap.add_argument("--discovery", default="auto")
     ap.add_argument("--bucket-mb", type=float, default=256.0)
     ap.add_argument("--checkpoint", action="store_true")

@@ -110,3 +110,28 @@ def test_prestart_validation_on_real_node():
         assert r.error == "" and len(r.allocated) == 1
         v = json.loads(c.api.get_pod("default", "validated")["metadata"]["annotations"][Contract().validated_key])
         assert v["k"] == 1 and v["peak_algbw_gbps"] > 100
+
+
+def test_pod_flow_then_training_on_the_allocated_device():
+    """Flow steps 1-7 on the real node, then the workload inside the 'container': the device plugin's
+    Allocate envs (GTK_GPU_GROUP/GTK_GPU_BDFS) decide where the MNIST job trains (design.md:239)."""
+    from gpu_topology_on_k8s_amd.sim import SimCluster
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
+
+    t = discover("auto")
+    t.node_name = "gpu-node"
+    with SimCluster({"gpu-node": t}) as c:
+        c.submit("trainer", 1)
+        r = c.schedule_pending()[0]
+        assert r.error == "" and len(r.allocated) == 1
+        resp = c.nodes["gpu-node"].kubelet.responses["default/trainer"]
+        envs = dict(resp.container_responses[0].envs)
+    assert envs["GTK_GPU_GROUP"] == str(r.allocated[0]) and envs["GTK_GPU_BDFS"]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update({k: envs[k] for k in ("GTK_GPU_GROUP", "GTK_GPU_BDFS")})
+    p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd.models.train", "--model", "mnist-cnn", "--batch", "64",
+                        "--steps", "20", "--warmup", "2", "--gemm-tuning", "off"], capture_output=True, text=True, cwd=REPO,
+                       timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["devices"] == [r.allocated[0]] and out["images_per_s"] > 0

@@ -122,3 +122,18 @@ def test_choose_subset_under_visible_devices():
 def test_choose_subset_cpu_visible_count_identity():
     ch = choose_subset(2, visible=4, topology=_node(4))
     assert ch.hip_devices == ch.devices
+
+
+def test_training_in_a_pod_uses_the_allocated_group(monkeypatch):
+    """design.md:239: the workload runs on the devices Allocate handed to the container — rank r on
+    GROUP[r], resolved to this container's HIP ordinals by PCI address."""
+    from gpu_topology_on_k8s_amd.models.train import _pod_devices
+
+    monkeypatch.setenv("GTK_GPU_GROUP", "6,2")
+    monkeypatch.setenv("GTK_GPU_BDFS", "0000:c5:00.0,0000:15:00.0")
+    pl = _pod_devices({"rank": 0, "world": 2}, visible_bdfs=["0000:15:00.0", "0000:c5:00.0"])
+    assert pl["devices"] == [6, 2] and pl["hip_devices"] == [1, 0] and pl["source"] == "pod-allocation"
+    import pytest
+
+    with pytest.raises(ValueError):
+        _pod_devices({"rank": 0, "world": 4}, visible_bdfs=["0000:15:00.0", "0000:c5:00.0"])
