@@ -126,7 +126,9 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
                       overlap_transposes=overlap_transposes, fuse_residual=fuse_residual)
         items_per_step, unit, flops_per_item = batch * seq, "tokens", cfg.flops_per_token(seq)
     broadcast_params(model.flat)
-    ar = BucketedAllReduce(model.flat, bucket_mb=bucket_mb, zero1=zero1, overlap_norm=overlap_norm)
+    # graph mode issues the gradient collectives after backward (inside the captured step), not from
+    # autograd hooks mid-backward: one capture-friendly sequence
+    ar = BucketedAllReduce(model.flat, bucket_mb=bucket_mb, zero1=zero1, overlap_norm=overlap_norm, overlap=not use_graph)
     opt = FlatAdamW(model.flat, lr=lr, shards=ar.shards() if zero1 else None, capturable=use_graph)
     if zero1:
         model.param_ready = ar.wait_param

@@ -125,3 +125,16 @@ def test_two_rank_mnist_dp_matches_one_rank():
     assert two["n_gpus"] == 2 and two["images_per_s"] > 0
     for a, b in zip(one["losses"], two["losses"]):
         assert abs(a - b) <= 2e-2 * max(1.0, abs(a)), (one["losses"], two["losses"])
+
+
+@needs2
+def test_two_rank_mnist_graph_matches_one_rank():
+    """Whole-step hipGraph at k=2: the gradient all-reduce (RCCL) is captured with the step."""
+    base = ["--model", "mnist-cnn", "--batch", "64", "--steps", "6", "--warmup", "2", "--same-data", "--graph", "on",
+            "--gemm-tuning", "off"]
+    one = _run(["-m", "gpu_topology_on_k8s_amd.models.train", *base])
+    two = _run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1",
+                "--master-port=29617", "-m", "gpu_topology_on_k8s_amd.models.train", *base])
+    assert two["graph"] and two["n_gpus"] == 2
+    for a, b in zip(one["losses"], two["losses"]):
+        assert abs(a - b) <= 2e-2 * max(1.0, abs(a)), (one["losses"], two["losses"])
