@@ -68,6 +68,10 @@ def parse(argv=None):
                          f"{TUNE_CANDIDATES} at k >= 2 (untimed, before warmup), 'tune' = that pass at any k, "
                          "'default' = RCCL's choice, or MIN[:MAX]")
     ap.add_argument("--tune-steps", type=int, default=3, help="timed all-reduces per candidate in the tuning pass")
+    ap.add_argument("--ab-worst", default="auto", choices=["auto", "on", "off"],
+                    help="after the headline: time the same all-reduce on the WORST k-subset the placement core found "
+                         "(a second communicator on those devices) and report the placement gain; auto = whenever a "
+                         "distinct worst subset exists (k < devices on the node)")
     ap.add_argument("--rccl-log", default="auto", choices=["auto", "on", "off"],
                     help="capture RCCL's INIT/GRAPH log (per-rank file under /tmp) and report the transports and "
                          "channel counts it chose; auto = on for k >= 2")
@@ -221,6 +225,51 @@ def tune_ctas(env, device, nbytes, args, tdev, barrier_kw):
     return best, table
 
 
+def measure_worst(env, choice, nbytes, args, tdev, barrier_kw, backend, ctas):
+    """The placement A/B inside the north-star run: rank r builds a second communicator on
+    ``choice.worst_hip[r]`` (the worst-scoring k-subset of the same node), checks it exactly and times
+    ``min(K, 20)`` all-reduces of the headline size (max over ranks)."""
+    import torch
+    import torch.distributed as dist
+
+    from gpu_topology_on_k8s_amd.parallel.allreduce import AllReduceRunner, bus_factor
+
+    wdev = int((choice.worst_hip or choice.worst)[env.rank])
+    ok, r = 1, None
+    try:
+        r = AllReduceRunner(env, wdev, nbytes, args.dtype, backend=backend, inplace=args.inplace, ctas=ctas, tag="/worst")
+    except Exception as e:  # noqa: BLE001 - every rank learns it through the flag below
+        print(f"bench: worst-subset communicator unavailable on rank {env.rank}: {e}", file=sys.stderr)
+        ok = 0
+    flag = torch.tensor([ok], dtype=torch.int32, device=tdev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 0:
+        if r is not None:
+            r.close()
+        return {"subset": choice.worst, "error": "communicator unavailable"}
+    try:
+        wrong = torch.tensor([r.check()], dtype=torch.int64, device=tdev)
+        dist.all_reduce(wrong)
+        for _ in range(max(1, args.warmup // 2)):
+            r.step()
+        r.synchronize()
+        steps = max(1, min(args.steps, 20))
+        dist.barrier(**barrier_kw)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            r.step()
+        r.synchronize()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=tdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item()) / steps * 1e3
+        alg = r.nbytes / (ms / 1e3) / 1e9
+        return {"subset": choice.worst, "hip_devices": choice.worst_hip, "score": choice.worst_score, "steps": steps,
+                "ms_per_step": round(ms, 4), "algbw_gbps": round(alg, 3), "busbw_gbps": round(alg * bus_factor(env.world), 3),
+                "exact": int(wrong.item()) == 0}
+    finally:
+        r.close()
+
+
 def main(argv=None) -> int:
     args = parse(argv)
     in_launcher = "WORLD_SIZE" in os.environ and "RANK" in os.environ
@@ -350,6 +399,19 @@ def main(argv=None) -> int:
         except Exception as e:  # noqa: BLE001
             print(f"bench: graph latency aborted on rank {env.rank}: {e}", file=sys.stderr)
             graph = {"error": str(e)[:300]}
+    worst_ab = None
+    want_ab = args.ab_worst == "on" or (args.ab_worst == "auto" and bool(choice.worst))
+    # a second communicator on other devices: the native RCCL comm (takes its device) or gloo on the CPU;
+    # the torch backend's process group is bound to this rank's device
+    if want_ab and choice.worst and (cpu or (choice.worst_hip and runner.comm is not None)):
+        try:  # supplementary, like the sweep: a failure is reported, never costs the headline
+            worst_ab = measure_worst(env, choice, headline_bytes, args, tdev, barrier_kw, args.backend, ctas)
+        except Exception as e:  # noqa: BLE001 - every rank runs the same steps
+            print(f"bench: worst-subset A/B aborted on rank {env.rank}: {e}", file=sys.stderr)
+            worst_ab = {"subset": choice.worst, "error": str(e)[:300]}
+        finally:
+            if not cpu:
+                torch.cuda.set_device(device)  # the second communicator switched this thread's device
     runner.close()
     rccl = None
     if rccl_log and env.rank == 0:
@@ -402,6 +464,9 @@ def main(argv=None) -> int:
             "size_sweep": sweep,
             "graph_latency": graph,
             "rccl": rccl,
+            "worst_subset_ab": worst_ab,
+            "placement_gain": (round(value / worst_ab[("busbw_gbps" if env.world > 1 else "algbw_gbps")], 4)
+                               if worst_ab and worst_ab.get(("busbw_gbps" if env.world > 1 else "algbw_gbps")) else None),
             "value_kind": "busbw" if env.world > 1 else "algbw (busbw = 0 at k=1)",
             "busbw_vs_probe_bound": round(busbw / bound, 4) if bound else None,
             "algbw_gbps": round(algbw, 3),

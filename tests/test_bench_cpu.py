@@ -143,6 +143,11 @@ def test_bench_four_ranks_on_amdsmi_discovered_node():
     assert cfg["topology_source"].startswith("amdsmi") and len(cfg["subset"]) == 4
     assert cfg["worst_subset"] is not None and cfg["worst_score"] < cfg["placement_score"]
     assert out["k8s_placement"]["assigned"] is True
+    # the placement A/B of the same run: a second communicator timed on the worst 4-subset
+    ab = out["worst_subset_ab"]
+    assert ab and "error" not in ab, ab
+    assert ab["subset"] == cfg["worst_subset"] and ab["exact"] and ab["busbw_gbps"] > 0
+    assert out["placement_gain"] is not None and out["placement_gain"] > 0
 
 
 def test_rccl_log_summary_parses_transports():
