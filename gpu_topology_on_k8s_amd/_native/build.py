@@ -90,6 +90,20 @@ class Target:
         cmd += ["-o", str(self.out)]
         return cmd
 
+    def compile_flags(self) -> List[str]:
+        """Per-object compile command prefix (multi-source hipcc targets: one object per source)."""
+        cmd = [str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
+               f"-I{ROCM / 'include'}", f"-I{CSRC}"]
+        if self.pybind:
+            cmd += _py_includes()
+        if self.torch:
+            cmd += [f for f in _torch_flags() if f.startswith(("-I", "-D"))]
+        return cmd
+
+    def link_flags(self) -> List[str]:
+        flags = [f for f in _torch_flags() if not f.startswith(("-I", "-D"))] if self.torch else []
+        return flags + [f for f in self.extra if not f.startswith(("-I", "-D"))]
+
     def up_to_date(self) -> bool:
         if not self.out.exists():
             return False
@@ -121,12 +135,50 @@ def targets() -> List[Target]:
     ]
 
 
-def build_one(t: Target, force: bool = False, verbose: bool = False) -> str:
+OBJ = HERE / "obj"  # per-source objects of multi-source hipcc targets (git- and gpurun-ignored)
+
+
+def _run(cmd: List[str], what: str, verbose: bool) -> None:
+    if verbose:
+        print(" ".join(shlex.quote(c) for c in cmd), flush=True)
+    p = subprocess.run(cmd, capture_output=True, text=True)
+    if p.returncode != 0:
+        raise RuntimeError(f"build of {what} failed ({p.returncode}):\n{' '.join(cmd)}\n{p.stdout}\n{p.stderr}")
+
+
+def _build_objects(t: Target, force: bool, verbose: bool, jobs: int) -> str:
+    """Multi-source hipcc target: compile every source to its own object in parallel (only the
+    sources changed since their object was built), then link.  The gfx950 device code of each
+    translation unit is self-contained, so no relocatable device code is needed."""
+    odir = OBJ / t.name
+    odir.mkdir(parents=True, exist_ok=True)
+    dep_t = max([p.stat().st_mtime for p in list(t.deps) + [Path(__file__)] if p.exists()] or [0.0])
+    flags = t.compile_flags()
+
+    def one(src: Path) -> Path:
+        obj = odir / (src.stem + ".o")
+        if force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, dep_t):
+            _run(flags + ["-c", str(src), "-o", str(obj)], f"{t.name}:{src.name}", verbose)
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(t.sources)))) as ex:
+        objs = list(ex.map(one, t.sources))
+    if not force and t.out.exists() and all(o.stat().st_mtime <= t.out.stat().st_mtime for o in objs) and t.up_to_date():
+        return f"ok   {t.name} (up to date)"
+    t.out.parent.mkdir(parents=True, exist_ok=True)
+    _run([str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-shared", "-fPIC"] + [str(o) for o in objs]
+         + t.link_flags() + ["-o", str(t.out)], t.name, verbose)
+    return f"built {t.name} -> {t.out.relative_to(REPO)} ({len(objs)} objects)"
+
+
+def build_one(t: Target, force: bool = False, verbose: bool = False, jobs: int = 4) -> str:
     missing = [s for s in t.sources if not s.exists()]
     if not t.sources or missing:
         return f"skip {t.name} (no sources)"
     if not force and t.up_to_date():
         return f"ok   {t.name} (up to date)"
+    if t.compiler == "hipcc" and t.shared and len(t.sources) > 1:
+        return _build_objects(t, force, verbose, jobs)
     t.out.parent.mkdir(parents=True, exist_ok=True)
     cmd = t.command()
     if verbose:
@@ -142,7 +194,7 @@ def build(force: bool = False, only: Optional[List[str]] = None, jobs: int = 4, 
     msgs: List[str] = []
     errors: List[str] = []
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        futs = {ex.submit(build_one, t, force, verbose): t for t in ts}
+        futs = {ex.submit(build_one, t, force, verbose, jobs): t for t in ts}
         for f in cf.as_completed(futs):
             try:
                 msgs.append(f.result())
