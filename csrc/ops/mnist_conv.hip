@@ -104,7 +104,9 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const u16* __restrict__ 
 }
 
 // ------------------------------------------------------------------- conv2 + pool forward (MFMA)
-constexpr int W2S = KW2 + 8;  // LDS row stride of conv2.w per output channel (pad: spreads banks)
+// LDS row stride of conv2.w per output channel: 152 dwords makes the forward's ds_read_b128 B reads
+// conflict-free (every 16-lane b128 group covers the 64 banks once; was 41 % conflict cycles at 148)
+constexpr int W2S = KW2 + 16;
 
 __global__ __launch_bounds__(256) void conv2_pool_fwd_kernel(const u16* __restrict__ h1, const u16* __restrict__ w2,
                                                              const u16* __restrict__ b2, u16* __restrict__ p,
@@ -190,8 +192,11 @@ __device__ __forceinline__ void dy2_frag(const u16* __restrict__ dp, const uint8
 
 // ------------------------------------------------------ conv2 dgrad + conv1 wgrad partials (MFMA)
 constexpr int DG_ROWS = 4;    // input rows of h1 per workgroup (one per wave)
-constexpr int DYW = 34;       // dy2 tile columns: x = -2 .. 31 (zero outside 0..23)
-constexpr int DYC = C2 + 8;   // dy2 tile channel stride (pad)
+// dy2 tile columns x = -2 .. 25 (zero outside 0..23).  Padded pixels x >= 26 of a wave's second
+// m-tile read up to 6 columns past a row (into the next row, or past the tile into the h1 tile): finite
+// values that only reach their own discarded output rows (MFMA rows are independent).
+constexpr int DYW = 28;
+constexpr int DYC = C2 + 16;  // 40 dwords: the A fragment's ds_read_b128 groups are conflict-free
 constexpr int XROWS = DG_ROWS + 2;
 
 // Workgroup = (image b, input rows 4g .. 4g+3); wave w owns input row 4g + w as two 16-pixel m-tiles
@@ -290,8 +295,8 @@ __device__ __forceinline__ void conv2_dgrad_block(const u16* __restrict__ dp, co
       const int co0 = kc * 32 + h * 8;
       bf16x8 a[2];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)  // dy2 column xi - kx, tile column xi - kx + 2 <= 33
-        a[mt] = as_bf(*reinterpret_cast<const u16x8*>(&dyl[(arow + mt * 16 + r - kx + 2) * DYC + co0]));
+      for (int mt = 0; mt < 2; ++mt)  // dy2 column xi - kx at tile column xi - kx + 2
+        a[mt] = as_bf(*reinterpret_cast<const u16x8*>(&dyl[(arow + mt * 16 + r - kx + 2) * DYC + co0]));  // <= 5 rows past
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
         const bf16x8 bf = tr_frag16(ws, W2S, kc * 32, t * C1 + nt * 16, lane);  // B[k = co][n = ci]

@@ -94,3 +94,18 @@ def test_kind_manifests_config1():
     kc = yaml.safe_load(files["kind-config.yaml"])
     assert [n["role"] for n in kc["nodes"]] == ["control-plane", "worker"]
     assert yaml.safe_load(files["pod-1gpu.yaml"])["spec"]["containers"][0]["resources"]["limits"]["amd.com/gpu"] == "1"
+
+
+def test_console_scripts_resolve():
+    """setup.cfg console scripts (gtk, gtk-device-plugin, gtk-extender) point at real callables."""
+    import configparser
+    import importlib
+    import os
+
+    cfg = configparser.ConfigParser()
+    cfg.read(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "setup.cfg"))
+    lines = [l.strip() for l in cfg["options.entry_points"]["console_scripts"].splitlines() if l.strip()]
+    assert {l.split("=")[0].strip() for l in lines} == {"gtk", "gtk-device-plugin", "gtk-extender"}
+    for l in lines:
+        mod, fn = l.split("=")[1].strip().split(":")
+        assert callable(getattr(importlib.import_module(mod), fn))
