@@ -122,12 +122,15 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
                             "securityContext": {"privileged": True},
                             "volumeMounts": [
                                 {"name": "device-plugins", "mountPath": "/var/lib/kubelet/device-plugins"},
+                                # kubelet pod-resources API: which pod holds which device (GROUP reconcile)
+                                {"name": "pod-resources", "mountPath": "/var/lib/kubelet/pod-resources", "readOnly": True},
                                 {"name": "sys", "mountPath": "/sys", "readOnly": True},
                                 {"name": "dev", "mountPath": "/dev"},
                             ],
                         }],
                         "volumes": [
                             {"name": "device-plugins", "hostPath": {"path": "/var/lib/kubelet/device-plugins"}},
+                            {"name": "pod-resources", "hostPath": {"path": "/var/lib/kubelet/pod-resources"}},
                             {"name": "sys", "hostPath": {"path": "/sys"}},
                             {"name": "dev", "hostPath": {"path": "/dev"}},
                         ],
@@ -198,8 +201,8 @@ def render_kind(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, fake_gpus:
             c["command"] = ["python3", "-m", "gpu_topology_on_k8s_amd.deviceplugin", f"--resource-name={resource}", "--discovery=fake",
                             f"--fake-gpus={fake_gpus}", "--probe=off", "--device-specs=stub", f"--metrics-port={PLUGIN_METRICS_PORT}"]
             c.pop("securityContext", None)
-            c["volumeMounts"] = [m for m in c["volumeMounts"] if m["name"] == "device-plugins"]
-            spec["volumes"] = [v for v in spec["volumes"] if v["name"] == "device-plugins"]
+            c["volumeMounts"] = [m for m in c["volumeMounts"] if m["name"] in ("device-plugins", "pod-resources")]
+            spec["volumes"] = [v for v in spec["volumes"] if v["name"] in ("device-plugins", "pod-resources")]
     kind_cfg = {
         "kind": "Cluster",
         "apiVersion": "kind.x-k8s.io/v1alpha4",

@@ -60,6 +60,10 @@ def main(argv=None) -> int:
     ap.add_argument("--metrics-port", type=int, default=0, help="serve Prometheus /metrics on this port (0 = off)")
     ap.add_argument("--metrics-host", default="0.0.0.0")
     ap.add_argument("--health-interval", type=float, default=10.0)
+    ap.add_argument("--pod-resources-socket", default="/var/lib/kubelet/pod-resources/kubelet.sock",
+                    help="kubelet pod-resources API; GROUP annotations are reconciled against it ('' = off)")
+    ap.add_argument("--reconcile-interval", type=float, default=10.0,
+                    help="seconds between pod-resources reconciliation passes (0 = off)")
     ap.add_argument("--reprobe-interval", type=float, default=0.0,
                     help="re-measure the links (child process) every N s while no pod holds a device; 0 = never")
     ap.add_argument("--reprobe-tolerance", type=float, default=0.15,
@@ -95,7 +99,8 @@ def main(argv=None) -> int:
     cfg = PluginConfig(resource_name=a.resource_name, socket_dir=a.socket_dir, socket_name=a.socket_name, dev_root=a.dev_root,
                        node_name=a.node_name, contract=contract, device_specs=specs, prestart_validate=a.prestart_validate,
                        health_interval=a.health_interval, reprobe_interval=a.reprobe_interval,
-                       reprobe_tolerance=a.reprobe_tolerance,
+                       reprobe_tolerance=a.reprobe_tolerance, pod_resources_socket=a.pod_resources_socket,
+                       reconcile_interval=a.reconcile_interval,
                        policy=PlacementPolicy(partition_aware=a.partition_aware == "on"))
     reprobe = None
     if a.reprobe_interval > 0 and a.discovery != "fake":

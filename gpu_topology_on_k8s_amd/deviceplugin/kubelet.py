@@ -20,6 +20,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import grpc
 
 from ..k8s.objects import meta, pod_gpu_request, pod_key
+from .podresources import build_response, pod_resources_handler
 from . import proto as pb
 
 log = logging.getLogger(__name__)
@@ -43,8 +44,11 @@ class _Plugin:
 
 
 class FakeKubelet:
-    def __init__(self, socket_dir: str, node_name: str = "", api=None):
+    def __init__(self, socket_dir: str, node_name: str = "", api=None, pod_resources_socket: Optional[str] = None):
         self.socket_dir = socket_dir
+        # the pod-resources API (v1 PodResourcesLister.List) lives in its own directory on a real
+        # node (/var/lib/kubelet/pod-resources/kubelet.sock); here a subdirectory of socket_dir
+        self.pod_resources_socket = pod_resources_socket or os.path.join(socket_dir, "pod-resources", "kubelet.sock")
         self.node_name = node_name
         self.api = api
         self.plugins: Dict[str, _Plugin] = {}
@@ -114,9 +118,22 @@ class FakeKubelet:
         self._server = grpc.server(futures.ThreadPoolExecutor(max_workers=4, thread_name_prefix="kubelet"))
         h = grpc.unary_unary_rpc_method_handler(self.Register, request_deserializer=pb.RegisterRequest.FromString,
                                                 response_serializer=pb.Empty.SerializeToString)
-        self._server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(pb.REGISTRATION_SERVICE, {"Register": h}),))
+        self._server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(pb.REGISTRATION_SERVICE, {"Register": h}),
+                                               pod_resources_handler(self.list_pod_resources)))
         self._server.add_insecure_port(f"unix://{self.socket}")
+        os.makedirs(os.path.dirname(self.pod_resources_socket), exist_ok=True)
+        try:
+            os.unlink(self.pod_resources_socket)
+        except FileNotFoundError:
+            pass
+        self._server.add_insecure_port(f"unix://{self.pod_resources_socket}")
         self._server.start()
+
+    def list_pod_resources(self):
+        """What the device manager recorded: pod -> resource -> device IDs (PodResourcesLister.List)."""
+        with self._lock:
+            triples = [(key, res, list(ids)) for res, per in self.allocated.items() for key, ids in per.items()]
+        return build_response(triples)
 
     def stop(self) -> None:
         self._stop.set()

@@ -41,6 +41,8 @@ class PluginMetrics:
                                    ["result"], registry=r)
         self.validate_seconds = Histogram("gtk_plugin_placement_validation_seconds", "PreStartContainer validation time",
                                           buckets=(0.5, 1, 2, 5, 10, 30, 60, 120), registry=r)
+        self.reconciled = Counter("gtk_plugin_reconciled_pods_total",
+                                  "pod GROUP annotations corrected to the kubelet's pod-resources truth", registry=r)
         self.annotation_bytes = Gauge("gtk_plugin_topology_annotation_bytes", "encoded size of the published node annotations",
                                       registry=r)
 

@@ -45,6 +45,7 @@ from ..topology.cpus import recommended_cpuset
 from ..topology.identity import ENV_BDFS, ENV_GROUP
 from ..topology.model import Topology
 from . import proto as pb
+from .podresources import POD_RESOURCES_SOCKET, list_pod_resources
 from .metrics import PluginMetrics
 
 log = logging.getLogger(__name__)
@@ -128,7 +129,8 @@ class PluginConfig:
                  publish_node: bool = True, pass_rccl_env: bool = True, policy: PlacementPolicy = PlacementPolicy(),
                  resource_aliases: Sequence[str] = ("aliyun.com/gpu", "aliyun.com/gpu-count"),
                  reprobe_interval: float = 0.0, reprobe_tolerance: float = 0.15, device_specs: str = "strict",
-                 prestart_validate: bool = False, validate_timeout: float = 120.0):
+                 prestart_validate: bool = False, validate_timeout: float = 120.0,
+                 pod_resources_socket: Optional[str] = POD_RESOURCES_SOCKET, reconcile_interval: float = 10.0):
         self.resource_name = resource_name
         self.socket_dir = socket_dir
         self.socket_name = socket_name
@@ -157,6 +159,11 @@ class PluginConfig:
         # bus bandwidth is recorded on the pod
         self.prestart_validate = prestart_validate
         self.validate_timeout = validate_timeout
+        # Allocate has no pod identity: two same-size pods assumed on one node can be admitted in the
+        # other order, leaving their GROUP annotations swapped.  Every `reconcile_interval` s the
+        # annotations are corrected to the kubelet's pod-resources API (None / "" = off)
+        self.pod_resources_socket = pod_resources_socket or ""
+        self.reconcile_interval = reconcile_interval
 
     @property
     def socket_path(self) -> str:
@@ -579,6 +586,47 @@ class DevicePluginServer:
                 return pod
         return None
 
+    def reconcile(self) -> int:
+        """Make every GPU pod's ``ALIYUN_COM_GPU_GROUP`` on this node equal the devices the kubelet
+        actually gave it (pod-resources ``List``): the annotation is what the extender's view is built
+        from, so a swapped pair would let it place a new pod on a device that is in use.  Returns the
+        number of pods corrected."""
+        sock = self.cfg.pod_resources_socket
+        if self.api is None or not self.cfg.node_name or not sock or not os.path.exists(sock):
+            return 0
+        try:
+            truth = list_pod_resources(sock)
+        except Exception as e:  # noqa: BLE001 - kubelet restarting: next pass
+            log.debug("pod-resources List failed: %s", e)
+            return 0
+        names = self._resource_names()
+        fixed = 0
+        for p in self._node_pods():
+            md = meta(p)
+            key = f"{md.get('namespace', 'default')}/{md.get('name')}"
+            ids = sorted({int(i) for r in names for i in truth.get(key, {}).get(r, []) if str(i).isdigit()})
+            if not ids:
+                continue  # not admitted yet (or not ours)
+            pa = PodAssignment.from_annotations(obj_annotations(p))
+            if pa is not None and pa.assigned and sorted(set(pa.group)) == ids:
+                continue
+            ann = {ANN_GROUP: format_group(ids), ANN_ASSIGNED: "true"}
+            if pa is None:
+                ann[ANN_ASSUME_TIME] = str(int(self.clock()))
+            try:
+                self.api.patch_pod_annotations(md.get("namespace", "default"), md["name"], ann,
+                                               resource_version=md.get("resourceVersion"))
+            except Exception as e:  # noqa: BLE001 - conflict or apiserver error: next pass
+                log.info("reconciling %s failed (%s); retrying next pass", key, e)
+                continue
+            fixed += 1
+            self.metrics.reconciled.inc()
+            log.warning("pod %s: GROUP %s -> %s (kubelet pod-resources)", key, pa.group if pa else None, ids)
+            record_event(self.api, p, "GPUAllocationReconciled",
+                         f"GROUP {format_group(pa.group) if pa else '-'} -> {format_group(ids)} (kubelet pod-resources)",
+                         "Normal", component="gpu-topology-device-plugin", host=self.cfg.node_name)
+        return fixed
+
     def _unannotated_pod(self, k: int) -> Optional[dict]:
         names = self._resource_names()
         cands = []
@@ -653,8 +701,14 @@ class DevicePluginServer:
 
     def _monitor(self) -> None:
         """Health polling and kubelet restart detection (the kubelet wipes plugin sockets on restart)."""
-        next_health = 0.0
+        next_health = next_reconcile = 0.0
         while not self._stop.wait(0.2):
+            if self.cfg.reconcile_interval > 0 and time.monotonic() >= next_reconcile:
+                next_reconcile = time.monotonic() + self.cfg.reconcile_interval
+                try:
+                    self.reconcile()
+                except Exception as e:  # noqa: BLE001
+                    log.warning("reconcile failed: %s", e)
             if not os.path.exists(self.cfg.socket_path):
                 log.warning("plugin socket %s vanished (kubelet restart?): re-serving and re-registering", self.cfg.socket_path)
                 try:

@@ -186,8 +186,10 @@ class SimCluster:
     def __init__(self, nodes: Dict[str, Topology], resource: str = "amd.com/gpu", policy_name: str = "exact",
                  policy: PlacementPolicy = PlacementPolicy(), assume_ttl: float = 300.0, use_filter: bool = True,
                  node_labels: Optional[Dict[str, Dict[str, str]]] = None, device_specs: str = "strict",
-                 prestart_validate: bool = False, validate_fn=None):
+                 prestart_validate: bool = False, validate_fn=None, reconcile_interval: float = 0.0):
         self.resource = resource
+        # the plugins' pod-resources reconcile loop (0 = only when reconcile() is called: deterministic tests)
+        self.reconcile_interval = reconcile_interval
         self.device_specs = device_specs
         self.prestart_validate = prestart_validate
         self.validate_fn = validate_fn
@@ -220,7 +222,9 @@ class SimCluster:
             plugin = DevicePluginServer(topo, PluginConfig(resource_name=self.resource, socket_dir=sockdir, node_name=name,
                                                            contract=self.contract, dev_root=dev_root,
                                                            device_specs=self.device_specs,
-                                                           prestart_validate=self.prestart_validate),
+                                                           prestart_validate=self.prestart_validate,
+                                                           pod_resources_socket=kubelet.pod_resources_socket,
+                                                           reconcile_interval=self.reconcile_interval),
                                         api=self.api, validate_fn=self.validate_fn)
             plugin.start()
             kubelet.wait_for(self.resource)
@@ -347,6 +351,10 @@ class SimCluster:
     # ------------------------------------------------------------------ views
     def assignment(self, name: str, namespace: str = "default") -> Optional[PodAssignment]:
         return PodAssignment.from_annotations(obj_annotations(self.api.get_pod(namespace, name)))
+
+    def reconcile(self) -> int:
+        """One pod-resources reconciliation pass on every node (pods corrected)."""
+        return sum(n.plugin.reconcile() for n in self.nodes.values())
 
     def used_devices(self, node: str) -> List[int]:
         assert self.extender is not None

@@ -90,7 +90,7 @@ def test_kind_manifests_config1():
     ds = [d for d in docs if d["kind"] == "DaemonSet" and d["metadata"]["name"] == "amd-gpu-topology-device-plugin"][0]
     c = ds["spec"]["template"]["spec"]["containers"][0]
     assert "--device-specs=stub" in c["command"] and "--discovery=fake" in c["command"] and "--fake-gpus=2" in c["command"]
-    assert all(v["name"] == "device-plugins" for v in ds["spec"]["template"]["spec"]["volumes"])
+    assert {v["name"] for v in ds["spec"]["template"]["spec"]["volumes"]} == {"device-plugins", "pod-resources"}
     kc = yaml.safe_load(files["kind-config.yaml"])
     assert [n["role"] for n in kc["nodes"]] == ["control-plane", "worker"]
     assert yaml.safe_load(files["pod-1gpu.yaml"])["spec"]["containers"][0]["resources"]["limits"]["amd.com/gpu"] == "1"
