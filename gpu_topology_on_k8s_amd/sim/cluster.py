@@ -186,8 +186,12 @@ class SimCluster:
     def __init__(self, nodes: Dict[str, Topology], resource: str = "amd.com/gpu", policy_name: str = "exact",
                  policy: PlacementPolicy = PlacementPolicy(), assume_ttl: float = 300.0, use_filter: bool = True,
                  node_labels: Optional[Dict[str, Dict[str, str]]] = None, device_specs: str = "strict",
-                 prestart_validate: bool = False, validate_fn=None, reconcile_interval: float = 0.0):
+                 prestart_validate: bool = False, validate_fn=None, reconcile_interval: float = 0.0,
+                 informer: bool = False):
         self.resource = resource
+        # drive the extender's cache by LIST+WATCH (production mode) instead of a LIST per request
+        self.use_informer = informer
+        self.informer = None
         # the plugins' pod-resources reconcile loop (0 = only when reconcile() is called: deterministic tests)
         self.reconcile_interval = reconcile_interval
         self.device_specs = device_specs
@@ -234,19 +238,33 @@ class SimCluster:
 
     def start_extender(self) -> None:
         self.extender = TopologyExtender(self.api, self.ext_cfg)
+        if self.use_informer:
+            from ..k8s.informer import Informer
+
+            self.informer = Informer(self.api, self.extender.cache.on_list, self.extender.cache.on_event, watch_timeout=5.0,
+                                     backoff=0.1)
+            self.extender.cache.attach_informer(self.informer)
+            self.informer.start()
+            self.informer.wait_synced(10.0)
         self.http = HttpExtender(self.extender)
         self.http.start()
 
-    def restart_extender(self) -> None:
-        """Stateless restart (SURVEY §5.3 (c)): the new process rebuilds from annotations."""
+    def _stop_extender(self) -> None:
         if self.http is not None:
             self.http.stop()
+            self.http = None
+        if self.informer is not None:
+            self.informer.stop()
+            self.informer = None
+
+    def restart_extender(self) -> None:
+        """Stateless restart (SURVEY §5.3 (c)): the new process rebuilds from annotations."""
+        self._stop_extender()
         self.start_extender()
 
     def stop(self) -> None:
         self._client.close()
-        if self.http is not None:
-            self.http.stop()
+        self._stop_extender()
         for n in self.nodes.values():
             n.plugin.stop()
             n.kubelet.stop()

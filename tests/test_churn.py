@@ -32,10 +32,10 @@ def _check(c, live, request):
         assert c.used_devices(node) == sorted(ids), (node, c.used_devices(node), sorted(ids))
 
 
-@pytest.mark.parametrize("seed", [11, 12, 13])
-def test_random_churn_keeps_allocations_consistent(seed):
+@pytest.mark.parametrize("seed,informer", [(11, False), (12, False), (13, False), (21, True), (22, True)])
+def test_random_churn_keeps_allocations_consistent(seed, informer):
     rng = random.Random(seed)
-    with SimCluster({f"n{i}": fx.f7_mi355x() for i in range(3)}) as c:
+    with SimCluster({f"n{i}": fx.f7_mi355x() for i in range(3)}, informer=informer) as c:
         live, request, nxt = {}, {}, 0
         for _ in range(36):
             op = rng.random()
