@@ -102,3 +102,41 @@ def test_out_of_order_admission_is_reconciled_from_pod_resources():
         if swapped:
             assert any(e["reason"] == "GPUAllocationReconciled" for e in c.api.events)
         assert pod_key(c.api.get_pod("default", "a")) == "default/a"
+
+
+@pytest.mark.parametrize("seed", [31, 32])
+def test_random_churn_on_cpx_nodes_with_fractions(seed):
+    """CPX nodes (8 packages x 8 XCPs): whole-XCP-count pods and Gaia fractions (gpu-fraction, one
+    package, best fit) churn together; besides the invariants above, every fraction stays inside one
+    package."""
+    from gpu_topology_on_k8s_amd.k8s import Contract
+
+    C = Contract()
+    rng = random.Random(seed)
+    with SimCluster({"c0": fx.f8_mi355x_cpx(), "c1": fx.f8_mi355x_cpx()}) as c:
+        live, request, frac, nxt = {}, {}, set(), 0
+        for _ in range(30):
+            if rng.random() < 0.6:
+                for _ in range(rng.randint(1, 4)):
+                    name = f"p{nxt}"
+                    nxt += 1
+                    if rng.random() < 0.5:
+                        f = rng.choice([0.125, 0.25, 0.5])
+                        c.submit(name, int(f * 8), annotations={C.fraction_key: str(f)})
+                        frac.add(f"default/{name}")
+                        request[f"default/{name}"] = int(f * 8)
+                    else:
+                        k = rng.choice([1, 2, 8, 16])
+                        c.submit(name, k)
+                        request[f"default/{name}"] = k
+                for r in c.schedule_pending(concurrent=rng.random() < 0.3):
+                    if r.node and r.allocated:
+                        live[r.pod] = r.node
+            elif live:
+                key = rng.choice(sorted(live))
+                c.complete(key.split("/")[1])
+                live.pop(key)
+            _check(c, live, request)
+            for key in frac & set(live):
+                ids = c.nodes[live[key]].kubelet.allocated[c.resource][key]
+                assert len({int(i) // 8 for i in ids}) == 1, (key, ids)
