@@ -10,10 +10,14 @@ exercised on the wire.
 from __future__ import annotations
 
 import json
+import logging
 import os
 import threading
+import time
 from typing import Any, Dict, Iterator, List, Optional, Tuple
 from urllib.parse import quote
+
+log = logging.getLogger(__name__)
 
 __all__ = ["ApiError", "Conflict", "NotFound", "Gone", "KubeAPI", "RestKubeAPI"]
 
@@ -105,8 +109,12 @@ class RestKubeAPI(KubeAPI):
 
     SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
 
+    #: projected service-account tokens rotate (the kubelet rewrites the file well before expiry):
+    #: a long-running daemon re-reads the file at most this often, and immediately after a 401
+    TOKEN_REFRESH_S = 60.0
+
     def __init__(self, base_url: str, token: Optional[str] = None, ca_file: Optional[str] = None, verify: bool = True,
-                 timeout: float = 10.0):
+                 timeout: float = 10.0, token_file: Optional[str] = None):
         import requests
 
         self.base = base_url.rstrip("/")
@@ -114,8 +122,9 @@ class RestKubeAPI(KubeAPI):
         self._local = threading.local()
         self._requests = requests
         self._headers = {"Accept": "application/json"}
-        if token:
-            self._headers["Authorization"] = f"Bearer {token}"
+        self._token_file = token_file
+        self._token = token or ""
+        self._token_read = time.monotonic()
         self._verify = ca_file if (verify and ca_file) else verify
 
     @classmethod
@@ -123,11 +132,27 @@ class RestKubeAPI(KubeAPI):
         host, port = os.environ.get("KUBERNETES_SERVICE_HOST"), os.environ.get("KUBERNETES_SERVICE_PORT", "443")
         if not host:
             raise RuntimeError("not running in a cluster (KUBERNETES_SERVICE_HOST unset); pass --apiserver")
-        with open(os.path.join(cls.SA_DIR, "token")) as f:
+        tf = os.path.join(cls.SA_DIR, "token")
+        with open(tf) as f:
             token = f.read().strip()
         if ":" in host and not host.startswith("["):
             host = f"[{host}]"
-        return cls(f"https://{host}:{port}", token=token, ca_file=os.path.join(cls.SA_DIR, "ca.crt"))
+        return cls(f"https://{host}:{port}", token=token, ca_file=os.path.join(cls.SA_DIR, "ca.crt"), token_file=tf)
+
+    def _bearer(self, force: bool = False) -> str:
+        """The current token, re-read from ``token_file`` when stale (or ``force``: after a 401)."""
+        if self._token_file and (force or time.monotonic() - self._token_read > self.TOKEN_REFRESH_S):
+            try:
+                with open(self._token_file) as f:
+                    self._token = f.read().strip()
+            except OSError as e:
+                log.warning("re-reading %s failed: %s", self._token_file, e)
+            self._token_read = time.monotonic()
+        return self._token
+
+    def _auth(self, force: bool = False) -> Dict[str, str]:
+        tok = self._bearer(force)
+        return {"Authorization": f"Bearer {tok}"} if tok else {}
 
     def _session(self):
         s = getattr(self._local, "s", None)
@@ -138,12 +163,16 @@ class RestKubeAPI(KubeAPI):
         return s
 
     def _do(self, method: str, path: str, body: Any = None, content_type: str = "application/json") -> Obj:
-        headers = {}
+        headers = self._auth()
         data = None
         if body is not None:
             headers["Content-Type"] = content_type
             data = json.dumps(body)
         r = self._session().request(method, self.base + path, data=data, headers=headers, timeout=self.timeout, verify=self._verify)
+        if r.status_code == 401 and self._token_file:  # rotated token: re-read once and retry
+            headers.update(self._auth(force=True))
+            r = self._session().request(method, self.base + path, data=data, headers=headers, timeout=self.timeout,
+                                        verify=self._verify)
         if r.status_code >= 400:
             try:
                 msg = r.json().get("message", r.text)
@@ -210,7 +239,8 @@ class RestKubeAPI(KubeAPI):
         :class:`Gone`."""
         url = (f"{self.base}{self._KIND_PATH[kind]}?watch=1&allowWatchBookmarks=true"
                f"&resourceVersion={quote(str(resource_version))}&timeoutSeconds={int(max(1, timeout))}")
-        with self._session().get(url, stream=True, timeout=(self.timeout, timeout + 30), verify=self._verify) as r:
+        with self._session().get(url, stream=True, timeout=(self.timeout, timeout + 30), verify=self._verify,
+                                 headers=self._auth()) as r:
             if r.status_code >= 400:
                 raise_for(r.status_code, r.text[:300])
             for line in r.iter_lines():

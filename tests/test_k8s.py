@@ -160,3 +160,24 @@ def test_in_cluster_requires_env(monkeypatch):
     monkeypatch.delenv("KUBERNETES_SERVICE_HOST", raising=False)
     with pytest.raises(RuntimeError):
         RestKubeAPI.in_cluster()
+
+
+def test_rest_client_rereads_a_rotated_token(tmp_path):
+    """Projected service-account tokens rotate: after a 401 the client re-reads its token file once
+    and retries (and re-reads it anyway once it is older than TOKEN_REFRESH_S)."""
+    api = FakeAPIServer()
+    api.create_node(make_node("n1"))
+    srv, url = serve_http(api, token="new-token")
+    try:
+        tf = tmp_path / "token"
+        tf.write_text("old-token\n")
+        rest = RestKubeAPI(url, token="old-token", token_file=str(tf))
+        tf.write_text("new-token\n")  # the kubelet rotated it
+        assert rest.get_node("n1")["metadata"]["name"] == "n1"
+        assert rest._token == "new-token"
+        static = RestKubeAPI(url, token="old-token")  # no file: nothing to re-read, the 401 stands
+        with pytest.raises(ApiError) as ei:
+            static.get_node("n1")
+        assert ei.value.code == 401
+    finally:
+        srv.shutdown()
