@@ -164,6 +164,34 @@ def scale_prioritize(n_nodes: int, pods: int = 20, k: int = 4):
     return out
 
 
+def cpx_select(reps: int = 5):
+    """The exact placement core on a CPX node (8 packages x 8 XCPs = 64 devices): median time per
+    request size and used fraction, and whether the branch-and-bound finished exactly (symmetry
+    breaking over interchangeable XCPs; before it, k = 16 took 364 ms and gave up exactness)."""
+    import time
+
+    from gpu_topology_on_k8s_amd.placement import select
+
+    t = fx.f8_mi355x_cpx()
+    rng = random.Random(7)
+    rows = []
+    for k in (1, 2, 4, 8, 16, 32):
+        for frac in (0.0, 0.25, 0.5):
+            ts, exact = [], True
+            for _ in range(reps):
+                used = rng.sample(range(64), int(64 * frac))
+                if 64 - len(used) < k:
+                    continue
+                t0 = time.perf_counter()
+                pl = select(t, k, used=used)
+                ts.append((time.perf_counter() - t0) * 1e3)
+                exact &= pl.exact
+            if ts:
+                rows.append({"k": k, "used_fraction": frac, "median_ms": round(statistics.median(ts), 3),
+                             "max_ms": round(max(ts), 3), "exact": exact})
+    return {"experiment": "cpx-64xcp-select", "reps": reps, "rows": rows}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--reps", type=int, default=500)
@@ -181,6 +209,7 @@ def main() -> int:
         run_exp("mi355x-exact-4gpu", 4, (), max(50, a.reps // 5), policy="exact", topo_fn=lambda: fx.f7_mi355x(76.5, 0.03, 1)),
         run_exp("mi355x-exact-1gpu-after-2", 1, (0, 1), max(50, a.reps // 5), policy="exact", topo_fn=lambda: fx.f7_mi355x(76.5, 0.03, 1)),
     ]
+    results.append(cpx_select())
     if a.scale_nodes:
         results.append(scale_prioritize(a.scale_nodes))
     for r in results:

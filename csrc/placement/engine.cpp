@@ -91,17 +91,31 @@ double Engine::evaluate(const std::vector<int>& ids, Terms* terms) const {
   return t.comm + pol_.w_span * t.span + pol_.w_frag * t.frag + pol_.w_fit * t.fit + pol_.w_access * t.access;
 }
 
-void Engine::greedy(int k, const std::vector<int>& F, std::vector<int>* best, double* best_j, bool maximise) const {
+void Engine::greedy(int k, const std::vector<int>& F, std::vector<int>* best, double* best_j, bool maximise,
+                    const std::vector<int>* cls) const {
   // Greedy growth from every seed, then first-improvement 1-swap descent (core._greedy_local).
   // `maximise` flips the direction (worst-placement search): sgn*J is minimised either way.
   const double sgn = maximise ? -1.0 : 1.0;
+  // candidate filter under symmetry: a device is worth trying only if every lower-id member of its
+  // class is already in the set (the others give the same objective as that member)
+  auto skip = [&](const std::vector<int>& cur, int c) {
+    if (std::find(cur.begin(), cur.end(), c) != cur.end()) return true;
+    if (cls == nullptr) return false;
+    const int cc = (*cls)[c];
+    for (int d : F) {
+      if (d >= c) break;
+      if ((*cls)[d] == cc && std::find(cur.begin(), cur.end(), d) == cur.end()) return true;
+    }
+    return false;
+  };
   for (int seed : F) {
+    if (cls != nullptr && skip(std::vector<int>{}, seed)) continue;  // one seed per class
     std::vector<int> cur{seed};
     while ((int)cur.size() < k) {
       int cand = -1;
       double cj = std::numeric_limits<double>::infinity();
       for (int c : F) {
-        if (std::find(cur.begin(), cur.end(), c) != cur.end()) continue;
+        if (skip(cur, c)) continue;
         cur.push_back(c);
         double j = sgn * evaluate(cur, nullptr);
         cur.pop_back();
@@ -118,7 +132,7 @@ void Engine::greedy(int k, const std::vector<int>& F, std::vector<int>* best, do
       improved = false;
       for (size_t a = 0; a < cur.size() && !improved; ++a) {
         for (int b : F) {
-          if (std::find(cur.begin(), cur.end(), b) != cur.end()) continue;
+          if (skip(cur, b)) continue;
           std::vector<int> trial = cur;
           trial[a] = b;
           double tj = sgn * evaluate(trial, nullptr);
@@ -172,6 +186,38 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
   for (size_t l = 0; l < lv_.size(); ++l) mg[l] = min_groups(lv_[l], k);
   const double pairs_k = k >= 2 ? 0.5 * k * (k - 1) : 1.0;
 
+  // ---- exact symmetry breaking.  Free devices a and b are interchangeable when they sit in the same
+  // group at every level, have the same access cost and the same link cost to every other free
+  // device: swapping them maps any set onto one with the same objective.  The XCPs of one package on
+  // a CPX node (64 devices, 8 classes of 8) are the case that matters: without this, C(64,16) sets.
+  // Only canonical sets are searched — within a class, the chosen members are a prefix of the class
+  // in id order — which keeps the first (lexicographically smallest) optimum of the full enumeration.
+  // Off when collecting ties: a random tie-break must see every optimal set (Gaia Table I).
+  std::vector<int> prev_same(m, -1);
+  if (!collect_ties) {
+    auto same = [&](int a, int b) {  // positions into F
+      const int i = F[a], j = F[b];
+      for (const auto& lv : lv_)
+        if (lv.gid[i] != lv.gid[j]) return false;
+      if (std::fabs(p_.access[i] - p_.access[j]) > 1e-12 * std::max(1.0, std::fabs(p_.access[i]))) return false;
+      const double* ri = &p_.cost[(size_t)i * n];
+      const double* rj = &p_.cost[(size_t)j * n];
+      for (int c = 0; c < m; ++c) {
+        const int x = F[c];
+        if (x == i || x == j) continue;
+        if (std::fabs(ri[x] - rj[x]) > 1e-12 * std::max(1.0, std::fabs(ri[x]))) return false;
+      }
+      return true;
+    };
+    for (int a = 1; a < m; ++a)
+      for (int b = a - 1; b >= 0; --b)
+        if (same(b, a)) {  // exact equality is transitive: the nearest equal one is the class predecessor
+          prev_same[a] = b;
+          break;
+        }
+  }
+  std::vector<char> inset(m, 0);
+
   // ---- DFS state
   std::vector<int> chosen;  // positions into F
   chosen.reserve(k);
@@ -213,12 +259,38 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
   };
 
   // Large search spaces: seed the incumbent with greedy + 1-swap so pruning bites from the start.
-  // (Ties then resolve to the greedy set rather than the lexicographically first optimum.)
-  double log_comb = std::lgamma(m + 1.0) - std::lgamma(k + 1.0) - std::lgamma(m - k + 1.0);
-  if (log_comb > std::log(2.0e5)) {  // (with collect_ties the DFS re-finds the seed and lists it)
+  // (Ties then resolve to the greedy set rather than the lexicographically first optimum.)  The size
+  // that matters is the number of CANONICAL k-sets: count vectors over the symmetry classes.
+  double log_space;
+  {
+    std::vector<int> class_size;
+    for (int a = 0; a < m; ++a) {
+      if (prev_same[a] < 0) class_size.push_back(1);
+      else {
+        int root = a;
+        while (prev_same[root] >= 0) root = prev_same[root];
+        int idx = 0;  // class index = number of roots before `root`
+        for (int b = 0; b < root; ++b) idx += prev_same[b] < 0;
+        class_size[idx] += 1;
+      }
+    }
+    std::vector<double> ways(k + 1, 0.0);  // ways[t] = canonical t-sets over the classes so far
+    ways[0] = 1.0;
+    for (int sz : class_size)
+      for (int t = k; t >= 1; --t)
+        for (int c = 1; c <= std::min(sz, t); ++c) ways[t] += ways[t - c];
+    log_space = std::log(std::max(1.0, ways[k]));
+  }
+  std::vector<int> cls_of(n, -1);  // symmetry class per device id (root position in F)
+  for (int a = 0; a < m; ++a) {
+    int root = a;
+    while (prev_same[root] >= 0) root = prev_same[root];
+    cls_of[F[a]] = root;
+  }
+  if (log_space > std::log(2.0e5)) {  // (with collect_ties the DFS re-finds the seed and lists it)
     std::vector<int> g;
     double gj = std::numeric_limits<double>::infinity();
-    greedy(k, F, &g, &gj, false);
+    greedy(k, F, &g, &gj, false, &cls_of);
     best_j = gj;
     for (int dev : g) best_pos.push_back((int)(std::lower_bound(F.begin(), F.end(), dev) - F.begin()));
   }
@@ -261,9 +333,11 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
       if (collect_ties ? lb > best_j + kEps : lb >= best_j - kEps) return;
     }
     for (int c = start; c <= m - r; ++c) {
+      if (prev_same[c] >= 0 && !inset[prev_same[c]]) continue;  // non-canonical: its class predecessor was skipped
       const int dev = F[c];
       // push
       chosen.push_back(c);
+      inset[c] = 1;
       for (size_t l = 0; l < lv_.size(); ++l) {
         int g = lv_[l].gid[dev];
         if (take[l][g]++ == 0) touched[l] += 1;
@@ -280,6 +354,7 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
         if (--take[l][g] == 0) touched[l] -= 1;
       }
       chosen.pop_back();
+      inset[c] = 0;
       if (aborted) return;
     }
   };
@@ -291,7 +366,7 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
   if (aborted && best_pos.size() != (size_t)k) {
     double gj = std::numeric_limits<double>::infinity();
     std::vector<int> g;
-    greedy(k, F, &g, &gj, false);
+    greedy(k, F, &g, &gj, false, &cls_of);
     ids = g;
   }
   res.ids = ids;

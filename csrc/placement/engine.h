@@ -78,7 +78,10 @@ class Engine {
     std::vector<int> sorted_free;  // `free`, descending (min_groups)
   };
   int min_groups(const Level& lv, int k) const;
-  void greedy(int k, const std::vector<int>& free_ids, std::vector<int>* best, double* best_j, bool maximise) const;
+  // `cls` (optional, class id per device id, -1 = not free): interchangeable devices share a class, and
+  // only the first not-yet-chosen member of each class is tried (identical objective otherwise).
+  void greedy(int k, const std::vector<int>& free_ids, std::vector<int>* best, double* best_j, bool maximise,
+              const std::vector<int>* cls = nullptr) const;
 
   Problem p_;
   Policy pol_;
