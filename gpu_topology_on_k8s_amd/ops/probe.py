@@ -74,23 +74,36 @@ def _device_map(topo: Topology, dmap: Optional[DeviceMap]) -> DeviceMap:
 
 
 def measure_ingress(topo: Topology, devs: Sequence[int], preset: str = "quick",
-                    dmap: Optional[DeviceMap] = None) -> List[Optional[float]]:
+                    dmap: Optional[DeviceMap] = None, by_package: bool = True) -> List[Optional[float]]:
     """Aggregate ingress GB/s of every topology device in ``devs`` reading from all the others
     concurrently (K5); stored in ``topo.probe["ingress_all_gbps"]`` (None where fewer than two
-    devices).  Topology indices are turned into HIP ordinals by PCI address (:class:`DeviceMap`)."""
+    devices).  Topology indices are turned into HIP ordinals by PCI address (:class:`DeviceMap`).
+    On a partitioned node (``by_package``) the first XCP of each package gathers from the first XCP
+    of every other package and the number is shared by the package's XCPs (8 gathers on a CPX node,
+    not 64 x 63-way)."""
     cfg = PROBE_PRESETS[preset]
     m = _device_map(topo, dmap)
     devs = [d for d in devs if d in m.hip_of_index]
     out: List[Optional[float]] = [None] * topo.n
-    for d in devs:
+    phys = topo.physical
+    rep_of = {d: d for d in devs}
+    if by_package and len(set(phys.tolist())) < topo.n:
+        first: Dict[int, int] = {}
+        for d in devs:
+            first.setdefault(int(phys[d]), d)
+        rep_of = {d: first[int(phys[d])] for d in devs}
+    reps = sorted(set(rep_of.values()))
+    for d in reps:
         hd = m.hip(d)
-        peers = [m.hip(s) for s in devs if s != d and bool(_p().can_access_peer(hd, m.hip(s)))]
+        peers = [m.hip(s) for s in reps if s != d and bool(_p().can_access_peer(hd, m.hip(s)))]
         if not peers:
             continue
         r = gather_bw(hd, peers, cfg["bytes"], cfg["iters"], cfg["warmup"])
         if not r["ok"]:
             raise RuntimeError(f"ingress probe verification failed on device {d}")
         out[d] = round(float(r["gbps"]), 2)
+    for d in devs:
+        out[d] = out[rep_of[d]]
     topo.probe = dict(topo.probe, ingress_all_gbps=out)
     return out
 
@@ -120,13 +133,49 @@ def measure_matrix(devs: Sequence[int], nbytes: int = 64 << 20, iters: int = 3, 
     return np.array(_p().probe_matrix(list(devs), int(nbytes), int(iters), int(warmup_iters), mode, kind), dtype=np.float64)
 
 
+def _probe_pairs(topo: Topology, devs: Sequence[int], by_package: bool):
+    """Ordered (src, dst) pairs to measure, and for a partitioned node the representative pair of
+    every device pair (None when each pair is measured).
+
+    On a CPX/DPX/QPX node the XCPs of one package share that package's xGMI links and HBM, so the
+    node is measured per PACKAGE pair (first visible XCP of each; plus one on-package pair and one
+    self-copy per package) and every XCP pair takes its packages' number: 8 x 8 measurements instead
+    of 64 x 64 on a CPX node, and XCPs of one package stay exactly interchangeable for the placement
+    engine's symmetry breaking (measured noise would otherwise tell them apart)."""
+    phys = topo.physical
+    partitioned = len(set(phys.tolist())) < topo.n
+    if not (by_package and partitioned):
+        return [(i, j) for i in devs for j in devs], None
+    members: Dict[int, List[int]] = {}
+    for d in devs:
+        members.setdefault(int(phys[d]), []).append(d)
+    first = {p: ms[0] for p, ms in members.items()}
+    second = {p: ms[1] for p, ms in members.items() if len(ms) > 1}
+    pairs = [(first[p], first[p]) for p in first]
+    pairs += [(first[p], second[p]) for p in second]
+    pairs += [(first[p], first[q]) for p in first for q in first if p != q]
+    rep = {}
+    for i in devs:
+        for j in devs:
+            p, q = int(phys[i]), int(phys[j])
+            if i == j:
+                rep[(i, j)] = (first[p], first[p])
+            elif p == q:
+                rep[(i, j)] = (first[p], second.get(p, first[p]))
+            else:
+                rep[(i, j)] = (first[p], first[q])
+    return pairs, rep
+
+
 def probe_topology(topo: Topology, preset: str = "quick", devs: Optional[List[int]] = None, mode: str = "read",
-                   kind: str = "lds", warm_ms: float = 50.0, dmap: Optional[DeviceMap] = None) -> Topology:
+                   kind: str = "lds", warm_ms: float = 50.0, dmap: Optional[DeviceMap] = None,
+                   by_package: bool = True) -> Topology:
     """Measure every visible pair and fold it into ``topo`` (in place; also returned).
 
     ``devs`` are *topology indices* (default: every device this process can reach).  Each is run on
     the HIP ordinal with the same PCI address, so a probe under ``HIP_VISIBLE_DEVICES`` or inside a
-    pod writes its numbers into the right rows of the node matrix."""
+    pod writes its numbers into the right rows of the node matrix.  ``by_package``: on a partitioned
+    node measure package pairs and share the numbers among their XCPs (:func:`_probe_pairs`)."""
     cfg = PROBE_PRESETS[preset]
     ndev = device_count()
     if ndev == 0:
@@ -139,18 +188,26 @@ def probe_topology(topo: Topology, preset: str = "quick", devs: Optional[List[in
     w = warmup(m.hip(devs[0]), warm_ms)
     bw = np.full((topo.n, topo.n), np.nan)
     hbm = np.full(topo.n, np.nan)
-    for i in devs:
-        for j in devs:
-            hi, hj = m.hip(i), m.hip(j)
-            if i != j and not bool(_p().can_access_peer(hj if mode == "read" else hi, hi if mode == "read" else hj)):
-                continue
-            r = copy_bw(hi, hj, cfg["bytes"], cfg["iters"], cfg["warmup"], mode=mode, kind=kind)
-            if not r["ok"]:
-                raise RuntimeError(f"probe verification failed for {i}->{j}")
-            if i == j:
-                hbm[i] = r["gbps"]
-            else:
-                bw[i, j] = r["gbps"]
+    pairs, rep = _probe_pairs(topo, devs, by_package)
+    for i, j in pairs:
+        hi, hj = m.hip(i), m.hip(j)
+        if i != j and not bool(_p().can_access_peer(hj if mode == "read" else hi, hi if mode == "read" else hj)):
+            continue
+        r = copy_bw(hi, hj, cfg["bytes"], cfg["iters"], cfg["warmup"], mode=mode, kind=kind)
+        if not r["ok"]:
+            raise RuntimeError(f"probe verification failed for {i}->{j}")
+        if i == j:
+            hbm[i] = r["gbps"]
+        else:
+            bw[i, j] = r["gbps"]
+    if rep is not None:  # partitioned node: every XCP pair takes its packages' measurement
+        for i in devs:
+            hbm[i] = hbm[rep[(i, i)][0]] if np.isnan(hbm[i]) else hbm[i]
+        for i in devs:
+            for j in devs:
+                if i != j and np.isnan(bw[i, j]):
+                    a, b = rep[(i, j)]
+                    bw[i, j] = bw[a, b]
     topo.hbm_gbps = hbm
     topo.set_measured_bw(
         bw,
@@ -162,6 +219,8 @@ def probe_topology(topo: Topology, preset: str = "quick", devs: Optional[List[in
             "devices": devs,
             "hip_ordinals": [m.hip(d) for d in devs],
             "device_map": "bdf" if m.by_bdf else "identity",
+            "pairs_measured": len(pairs),
+            "granularity": "package" if rep is not None else "device",
             "mfma_warmup_tflops": round(float(w["tflops"]), 1),
             "ts": int(time.time()),
             "seconds": round(time.time() - t0, 3),

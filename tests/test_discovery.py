@@ -163,3 +163,23 @@ def test_amdsmi_backend_cpx(monkeypatch, tmp_path):
 
     ann = encode_node_annotations(t)
     assert annotations_size(ann) < 64 * 1024 and sum(k.startswith("GPUPKG_") for k in ann) == 28
+
+
+def test_probe_pairs_per_package_on_cpx():
+    """A CPX node is probed per package pair (72 copies instead of 4096) and every XCP pair takes its
+    packages' number, so the XCPs of a package stay interchangeable for the placement engine."""
+    from gpu_topology_on_k8s_amd.ops.probe import _probe_pairs
+    from gpu_topology_on_k8s_amd.topology import fixtures as fx
+
+    t = fx.f8_mi355x_cpx()
+    pairs, rep = _probe_pairs(t, list(range(64)), by_package=True)
+    assert len(pairs) == 8 + 8 + 56 and len(set(pairs)) == len(pairs)
+    phys = t.physical
+    for (i, j), (a, b) in rep.items():
+        assert (a, b) in pairs
+        assert phys[a] == phys[i] and phys[b] == phys[j]
+        assert (i == j) == (a == b)
+    full, none = _probe_pairs(t, list(range(64)), by_package=False)
+    assert none is None and len(full) == 64 * 64
+    flat, r8 = _probe_pairs(fx.f7_mi355x(), list(range(8)), by_package=True)  # unpartitioned: every pair
+    assert r8 is None and len(flat) == 64
