@@ -57,12 +57,17 @@ double Engine::evaluate(const std::vector<int>& ids, Terms* terms) const {
   const int n = p_.n;
   Terms t;
   if (k >= 2) {
-    double s = 0;
+    double s = 0, mx = -std::numeric_limits<double>::infinity();
     for (int a = 0; a < k; ++a)
-      for (int b = a + 1; b < k; ++b) s += p_.cost[(size_t)ids[a] * n + ids[b]];
+      for (int b = a + 1; b < k; ++b) {
+        const double c = p_.cost[(size_t)ids[a] * n + ids[b]];
+        s += c;
+        mx = std::max(mx, c);
+      }
     t.comm = 2.0 * s / ((double)k * (k - 1));
+    t.bott = mx;
   } else {
-    t.comm = 1.0;
+    t.comm = t.bott = 1.0;
   }
   for (const auto& lv : lv_) {
     int touched = 0;
@@ -88,7 +93,7 @@ double Engine::evaluate(const std::vector<int>& ids, Terms* terms) const {
   for (int i : ids) acc += p_.access[i];
   t.access = k ? acc / k : 0.0;
   if (terms) *terms = t;
-  return t.comm + pol_.w_span * t.span + pol_.w_frag * t.frag + pol_.w_fit * t.fit + pol_.w_access * t.access;
+  return t.comm + pol_.w_bottleneck * (t.bott - t.comm) + pol_.w_span * t.span + pol_.w_frag * t.frag + pol_.w_fit * t.fit + pol_.w_access * t.access;
 }
 
 void Engine::greedy(int k, const std::vector<int>& F, std::vector<int>* best, double* best_j, bool maximise,
@@ -225,6 +230,7 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
   std::vector<int> touched(lv_.size(), 0);
   for (size_t l = 0; l < lv_.size(); ++l) take[l].assign(lv_[l].size.size(), 0);
   std::vector<std::vector<double>> cross(k + 1, std::vector<double>(m, 0.0));  // cross[d][c] = sum cost(F[c], P_d)
+  std::vector<std::vector<double>> xmax(k + 1, std::vector<double>(m, 0.0));   // xmax[d][c] = max cost(F[c], P_d)
   std::vector<double> scratch(m);
 
   double best_j = std::numeric_limits<double>::infinity();
@@ -234,8 +240,10 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
   bool aborted = false;
 
   // Leaf objective from the incremental state.
-  auto leaf_objective = [&](double pairsum, double accsum) {
+  const double wb = pol_.w_bottleneck;
+  auto leaf_objective = [&](double pairsum, double pairmax, double accsum) {
     double comm = k >= 2 ? pairsum / pairs_k : 1.0;
+    double bott = k >= 2 ? pairmax : 1.0;
     double span = 0, frag = 0, fit = 0;
     for (size_t l = 0; l < lv_.size(); ++l) {
       span += touched[l] - mg[l];
@@ -255,7 +263,8 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
         fit += (double)after / lv.size[g];
       }
     }
-    return comm + pol_.w_span * span + pol_.w_frag * frag + pol_.w_fit * fit + pol_.w_access * (accsum / k);
+    return comm + wb * (bott - comm) + pol_.w_span * span + pol_.w_frag * frag + pol_.w_fit * fit +
+           pol_.w_access * (accsum / k);
   };
 
   // Large search spaces: seed the incumbent with greedy + 1-swap so pruning bites from the start.
@@ -295,12 +304,12 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
     for (int dev : g) best_pos.push_back((int)(std::lower_bound(F.begin(), F.end(), dev) - F.begin()));
   }
 
-  std::function<void(int, double, double)> dfs = [&](int start, double pairsum, double accsum) {
+  std::function<void(int, double, double, double)> dfs = [&](int start, double pairsum, double pairmax, double accsum) {
     if (aborted) return;
     const int d = (int)chosen.size();
     if (d == k) {
       ++leaves;
-      double j = leaf_objective(pairsum, accsum);
+      double j = leaf_objective(pairsum, pairmax, accsum);
       if (j < best_j - kEps) {
         best_j = j;
         best_pos = chosen;
@@ -317,7 +326,7 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
     const int r = k - d;
     // lower bound over completions drawn from F[start..m)
     if (std::isfinite(best_j)) {
-      double comm_lb = 1.0;
+      double comm_lb = 1.0, bott_lb = 1.0;
       if (k >= 2) {
         int cnt = m - start;
         for (int c = 0; c < cnt; ++c) scratch[c] = cross[d][start + c] + 0.5 * pre[start + c][r - 1];
@@ -326,10 +335,11 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
         for (int c = 0; c < r; ++c) add += scratch[c];
         // nth_element leaves the r smallest in [0, r) in arbitrary order
         comm_lb = (pairsum + std::max(add, 0.0)) / pairs_k;
+        bott_lb = std::max(pairmax, comm_lb);  // the costliest pair is at least the mean
       }
       double span_lb = 0;
       for (size_t l = 0; l < lv_.size(); ++l) span_lb += std::max(0, touched[l] - mg[l]);
-      double lb = comm_lb + pol_.w_span * span_lb + pol_.w_access * ((accsum + r * amin) / k);
+      double lb = (1.0 - wb) * comm_lb + wb * bott_lb + pol_.w_span * span_lb + pol_.w_access * ((accsum + r * amin) / k);
       if (collect_ties ? lb > best_j + kEps : lb >= best_j - kEps) return;
     }
     for (int c = start; c <= m - r; ++c) {
@@ -343,11 +353,15 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
         if (take[l][g]++ == 0) touched[l] += 1;
       }
       const double add_pairs = cross[d][c];
+      const double new_max = d > 0 ? std::max(pairmax, xmax[d][c]) : pairmax;
       if (d + 1 < k) {
         const double* row = &p_.cost[(size_t)dev * n];
-        for (int q = c + 1; q < m; ++q) cross[d + 1][q] = cross[d][q] + row[F[q]];
+        for (int q = c + 1; q < m; ++q) {
+          cross[d + 1][q] = cross[d][q] + row[F[q]];
+          xmax[d + 1][q] = d > 0 ? std::max(xmax[d][q], row[F[q]]) : row[F[q]];
+        }
       }
-      dfs(c + 1, pairsum + add_pairs, accsum + p_.access[dev]);
+      dfs(c + 1, pairsum + add_pairs, new_max, accsum + p_.access[dev]);
       // pop
       for (size_t l = 0; l < lv_.size(); ++l) {
         int g = lv_[l].gid[dev];
@@ -358,7 +372,7 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
       if (aborted) return;
     }
   };
-  dfs(0, 0.0, 0.0);
+  dfs(0, 0.0, -std::numeric_limits<double>::infinity(), 0.0);
 
   std::vector<int> ids;
   for (int pos : best_pos) ids.push_back(F[pos]);

@@ -8,8 +8,10 @@
 // devices (C(64,8) ~ 4.4e9 subsets), which is why the engine is native and prunes with bounds.
 //
 // Objective (identical to core.evaluate):
-//   J(S) = comm + w_span*span + w_frag*frag + w_fit*fit + w_access*acc
+//   J(S) = comm + w_bottleneck*(bott - comm) + w_span*span + w_frag*frag + w_fit*fit + w_access*acc
 //   comm = mean unordered-pair cost of S (1.0 when |S| == 1)
+//   bott = costliest pair of S (== comm when |S| <= 2 or every link is alike): a ring collective runs
+//          at its slowest link, which the mean dilutes (one half-bandwidth link in a 4-set is +1/6)
 //   span = sum_levels (#groups touched - #groups minimally needed for k free devices)
 //   frag = sum_levels #pristine groups left partially used
 //   fit  = sum_levels sum_touched free_after/size
@@ -27,7 +29,7 @@ namespace gtk {
 constexpr double kEps = 1e-9;
 
 struct Policy {
-  double w_span = 0.5, w_frag = 0.25, w_fit = 0.05, w_access = 0.1;
+  double w_span = 0.5, w_frag = 0.25, w_fit = 0.05, w_access = 0.1, w_bottleneck = 0.4;  // w_bottleneck in [0, 1]
 };
 
 struct Problem {
@@ -39,7 +41,7 @@ struct Problem {
 };
 
 struct Terms {
-  double comm = 0, span = 0, frag = 0, fit = 0, access = 0;
+  double comm = 0, bott = 0, span = 0, frag = 0, fit = 0, access = 0;
 };
 
 struct Result {

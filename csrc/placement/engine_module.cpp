@@ -47,6 +47,7 @@ py::dict to_dict(const Result& r, double us) {
   d["micros"] = us;
   py::dict t;
   t["comm"] = r.terms.comm;
+  t["bottleneck"] = r.terms.bott;
   t["span"] = r.terms.span;
   t["frag"] = r.terms.frag;
   t["fit"] = r.terms.fit;
@@ -55,8 +56,10 @@ py::dict to_dict(const Result& r, double us) {
   return d;
 }
 
-Policy make_policy(double w_span, double w_frag, double w_fit, double w_access) {
+Policy make_policy(double w_span, double w_frag, double w_fit, double w_access, double w_bottleneck) {
+  if (!(w_bottleneck >= 0.0 && w_bottleneck <= 1.0)) throw std::invalid_argument("w_bottleneck must be in [0, 1]");
   Policy pol;
+  pol.w_bottleneck = w_bottleneck;
   pol.w_span = w_span;
   pol.w_frag = w_frag;
   pol.w_fit = w_fit;
@@ -73,14 +76,14 @@ PYBIND11_MODULE(_placement, m) {
       [](py::array_t<double, py::array::c_style | py::array::forcecast> cost,
          py::array_t<bool, py::array::c_style | py::array::forcecast> free_mask, const std::vector<std::vector<int>>& levels,
          py::array_t<double, py::array::c_style | py::array::forcecast> access, int k, double w_span, double w_frag,
-         double w_fit, double w_access, uint64_t node_limit, bool collect_ties) {
+         double w_fit, double w_access, uint64_t node_limit, bool collect_ties, double w_bottleneck) {
         Problem p = make_problem(cost, free_mask, levels, access);
         Result r;
         double us = 0;
         {
           py::gil_scoped_release nogil;
           auto t0 = std::chrono::steady_clock::now();
-          Engine e(p, make_policy(w_span, w_frag, w_fit, w_access));
+          Engine e(p, make_policy(w_span, w_frag, w_fit, w_access, w_bottleneck));
           r = e.select(k, node_limit, collect_ties);
           us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
         }
@@ -90,20 +93,21 @@ PYBIND11_MODULE(_placement, m) {
       },
       py::arg("cost"), py::arg("free"), py::arg("levels"), py::arg("access"), py::arg("k"), py::arg("w_span") = 0.5,
       py::arg("w_frag") = 0.25, py::arg("w_fit") = 0.05, py::arg("w_access") = 0.1,
-      py::arg("node_limit") = (uint64_t)2000000, py::arg("collect_ties") = false);
+      py::arg("node_limit") = (uint64_t)2000000, py::arg("collect_ties") = false,
+      py::arg("w_bottleneck") = 0.4);
   m.def(
       "worst",
       [](py::array_t<double, py::array::c_style | py::array::forcecast> cost,
          py::array_t<bool, py::array::c_style | py::array::forcecast> free_mask, const std::vector<std::vector<int>>& levels,
          py::array_t<double, py::array::c_style | py::array::forcecast> access, int k, double w_span, double w_frag,
-         double w_fit, double w_access, uint64_t node_limit) {
+         double w_fit, double w_access, uint64_t node_limit, double w_bottleneck) {
         Problem p = make_problem(cost, free_mask, levels, access);
         Result r;
         double us = 0;
         {
           py::gil_scoped_release nogil;
           auto t0 = std::chrono::steady_clock::now();
-          Engine e(p, make_policy(w_span, w_frag, w_fit, w_access));
+          Engine e(p, make_policy(w_span, w_frag, w_fit, w_access, w_bottleneck));
           r = e.worst(k, node_limit);
           us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
         }
@@ -111,15 +115,15 @@ PYBIND11_MODULE(_placement, m) {
       },
       py::arg("cost"), py::arg("free"), py::arg("levels"), py::arg("access"), py::arg("k"), py::arg("w_span") = 0.5,
       py::arg("w_frag") = 0.25, py::arg("w_fit") = 0.05, py::arg("w_access") = 0.1,
-      py::arg("node_limit") = (uint64_t)2000000);
+      py::arg("node_limit") = (uint64_t)2000000, py::arg("w_bottleneck") = 0.4);
   m.def(
       "evaluate",
       [](py::array_t<double, py::array::c_style | py::array::forcecast> cost,
          py::array_t<bool, py::array::c_style | py::array::forcecast> free_mask, const std::vector<std::vector<int>>& levels,
          py::array_t<double, py::array::c_style | py::array::forcecast> access, const std::vector<int>& ids,
-         double w_span, double w_frag, double w_fit, double w_access) {
+         double w_span, double w_frag, double w_fit, double w_access, double w_bottleneck) {
         Problem p = make_problem(cost, free_mask, levels, access);
-        Engine e(p, make_policy(w_span, w_frag, w_fit, w_access));
+        Engine e(p, make_policy(w_span, w_frag, w_fit, w_access, w_bottleneck));
         Result r;
         r.ids = ids;
         r.objective = e.evaluate(ids, &r.terms);
@@ -127,6 +131,6 @@ PYBIND11_MODULE(_placement, m) {
         return to_dict(r, 0.0);
       },
       py::arg("cost"), py::arg("free"), py::arg("levels"), py::arg("access"), py::arg("ids"), py::arg("w_span") = 0.5,
-      py::arg("w_frag") = 0.25, py::arg("w_fit") = 0.05, py::arg("w_access") = 0.1);
+      py::arg("w_frag") = 0.25, py::arg("w_fit") = 0.05, py::arg("w_access") = 0.1, py::arg("w_bottleneck") = 0.4);
   m.attr("EPS") = kEps;
 }

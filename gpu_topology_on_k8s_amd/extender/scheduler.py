@@ -43,6 +43,7 @@ from ..k8s.objects import annotations as obj_annotations
 from ..k8s.objects import labels as obj_labels
 from ..k8s.objects import pod_gpu_request, pod_key
 from ..placement import NoFeasiblePlacement, PlacementPolicy, place_fraction, select
+from ..placement.core import node_packing_term
 from ..placement.gaia import gaia_schedule, tree_from_topology
 from ..placement.legacy import design_greedy_select
 from ..topology.cpus import access_costs, recommended_cpuset
@@ -86,6 +87,7 @@ class Decision:
     policy: str
     micros: float
     cpuset: str = ""
+    rank: float = float("nan")  # objective + node-level packing term: what nodes are compared by
 
 
 def normalized_scores(objectives: Dict[str, float], resolution: float = 0.005) -> Dict[str, int]:
@@ -255,8 +257,9 @@ class TopologyExtender:
             except NoFeasiblePlacement as e:
                 return None, str(e)
             us = (time.perf_counter() - t0) * 1e6
+            rank = obj + node_packing_term(free, k, t.n, self.cfg.policy)
             return Decision(node=name, ids=ids, score=score, objective=obj,
-                            policy="fragment" if fraction is not None else self.cfg.policy_name, micros=us), ""
+                            policy="fragment" if fraction is not None else self.cfg.policy_name, micros=us, rank=rank), ""
 
     def _node_eval(self, pod: Dict[str, Any], name: str, node_obj: Optional[dict], k: int) -> Tuple[Optional[Decision], str]:
         st = self.cache.get(name, node_obj)  # may sync the cache: never call with a node lock held
@@ -292,7 +295,7 @@ class TopologyExtender:
                 continue
             d, _ = self._node_eval(pod, n, (node_objs or {}).get(n), k)
             if d is not None:
-                objs[n] = d.objective
+                objs[n] = d.rank if d.rank == d.rank else d.objective
                 self.metrics.score(d.score)
         norm = normalized_scores(objs, self.cfg.score_resolution)
         out = [(n, norm.get(n, 0)) for n in node_names]

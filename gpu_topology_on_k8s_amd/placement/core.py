@@ -16,9 +16,12 @@ Reference behaviour:
 
 The objective for a candidate set S (|S| = k) is::
 
-    J(S) = comm(S) + w_span * span(S) + w_frag * frag(S) + w_fit * fit(S) + w_access * acc(S)
+    J(S) = comm(S) + w_bottleneck * (bott(S) - comm(S)) + w_span * span(S) + w_frag * frag(S)
+           + w_fit * fit(S) + w_access * acc(S)
 
     comm  = mean pairwise link cost (1.0 = one nominal xGMI link; 1.0 for k == 1)
+    bott  = costliest pair in S: a ring all-reduce runs at its slowest link, which the mean dilutes
+            (one half-bandwidth link in a 4-set moves the mean by 1/6); equal to comm on uniform sets
     span  = sum over levels of (#groups touched - #groups minimally needed to host k free devices)
     frag  = sum over levels of #pristine groups left partially used
     fit   = sum over levels and touched groups of free_after/size  (best-fit packing)
@@ -40,7 +43,7 @@ import numpy as np
 from ..topology.model import Topology
 
 __all__ = ["PlacementPolicy", "Placement", "Problem", "select", "worst", "select_with", "place_fraction", "evaluate",
-           "score_from_objective", "NoFeasiblePlacement"]
+           "score_from_objective", "node_packing_term", "NoFeasiblePlacement"]
 
 EPS = 1e-9
 
@@ -55,9 +58,14 @@ class PlacementPolicy:
     w_frag: float = 0.25
     w_fit: float = 0.05
     w_access: float = 0.1
+    w_bottleneck: float = 0.4  # in [0, 1]: blend of mean and worst link (bench/cluster_trace.py)
     tie_break: str = "first"  # "first" (deterministic, lowest ids) | "random"
     exact_limit: int = 200_000  # Python path: max subsets enumerated exactly; above -> greedy + local search
     node_limit: int = 2_000_000  # native path: branch-and-bound node budget; above -> greedy + local search
+    # across nodes (the extender's ranking, not the subset search): breaking a pristine node costs
+    # w_frag and every device left free on the chosen node w_node_fit / node size — node-level best fit,
+    # so small jobs do not scatter over empty nodes that 8-GPU jobs need (bench/cluster_trace.py)
+    w_node_fit: float = 0.2
     # CPX/DPX/QPX nodes: treat the XCPs of one physical GPU as a group (pack multi-XCP requests onto
     # one package, keep whole packages pristine) and keep their cheap on-package links.  False =
     # every device is a stand-alone GPU behind xGMI (A/B baseline; SURVEY.md §5.6 --partition-aware)
@@ -65,7 +73,8 @@ class PlacementPolicy:
 
     def to_dict(self) -> Dict[str, object]:
         return dict(
-            w_span=self.w_span, w_frag=self.w_frag, w_fit=self.w_fit, w_access=self.w_access,
+            w_span=self.w_span, w_frag=self.w_frag, w_fit=self.w_fit, w_access=self.w_access, w_bottleneck=self.w_bottleneck,
+            w_node_fit=self.w_node_fit,
             tie_break=self.tie_break, exact_limit=self.exact_limit, node_limit=self.node_limit,
             partition_aware=self.partition_aware,
         )
@@ -128,6 +137,15 @@ class Problem:
         return len(self.free)
 
 
+def node_packing_term(free_before: int, k: int, size: int, policy: PlacementPolicy = PlacementPolicy()) -> float:
+    """Node-level packing cost of putting k devices on a node with ``free_before`` of ``size`` free:
+    the same anti-fragmentation (pristine group broken) and best-fit terms as inside a node, one level
+    up.  A constant for every subset of one node, so it only ranks nodes against each other."""
+    after = free_before - k
+    broken = 1.0 if free_before == size and after > 0 else 0.0
+    return policy.w_frag * broken + policy.w_node_fit * after / max(1, size)
+
+
 def score_from_objective(j: float) -> float:
     return 10.0 / max(1.0, j)
 
@@ -160,8 +178,9 @@ def evaluate(p: Problem, ids: Sequence[int], policy: PlacementPolicy = Placement
     if k >= 2:
         sub = p.cost[np.ix_(ids, ids)]
         comm = float(sub.sum() / (k * (k - 1)))
+        bott = float(max(sub[a, b] for a in range(k) for b in range(a + 1, k)))
     else:
-        comm = 1.0
+        comm = bott = 1.0
     stats = _stats if _stats is not None else _level_stats(p)
     span = frag = fit = 0.0
     for lv, size, fre in stats:
@@ -176,8 +195,9 @@ def evaluate(p: Problem, ids: Sequence[int], policy: PlacementPolicy = Placement
                 frag += 1
             fit += after / size[g]
     acc = float(np.mean(p.access[ids])) if k else 0.0
-    j = comm + policy.w_span * span + policy.w_frag * frag + policy.w_fit * fit + policy.w_access * acc
-    return j, {"comm": comm, "span": span, "frag": frag, "fit": fit, "access": acc}
+    j = (comm + policy.w_bottleneck * (bott - comm) + policy.w_span * span + policy.w_frag * frag
+         + policy.w_fit * fit + policy.w_access * acc)
+    return j, {"comm": comm, "bottleneck": bott, "span": span, "frag": frag, "fit": fit, "access": acc}
 
 
 def _greedy_local(p: Problem, k: int, policy: PlacementPolicy, stats) -> Tuple[List[int], float]:
@@ -232,14 +252,14 @@ def _select_native(mod, p: Problem, k: int, policy: PlacementPolicy, rng: Option
             [lv.astype(np.int64).tolist() for lv in p.levels], np.ascontiguousarray(p.access, dtype=np.float64))
     w = (policy.w_span, policy.w_frag, policy.w_fit, policy.w_access)
     ties = policy.tie_break == "random"
-    r = mod.select(*args, int(k), *w, int(policy.node_limit), ties)
+    r = mod.select(*args, int(k), *w, int(policy.node_limit), ties, w_bottleneck=policy.w_bottleneck)
     if not r["feasible"]:
         raise NoFeasiblePlacement(f"need {k} free devices")
     if ties and len(r["ties"]) > 1:
         # same draw as the Python enumeration: lexicographic tie list, one rng.choice
         pick = list((rng or random).choice(r["ties"]))
         if pick != list(r["ids"]):
-            e = mod.evaluate(*args, pick, *w)
+            e = mod.evaluate(*args, pick, *w, w_bottleneck=policy.w_bottleneck)
             r = dict(r, ids=pick, objective=e["objective"], terms=e["terms"])
     terms = dict(r["terms"])
     terms["search_nodes"] = float(r["nodes"])
@@ -356,7 +376,8 @@ def worst(topo: Topology, k: int, used: Sequence[int] = (), policy: PlacementPol
     if mod is not None:
         args = (np.ascontiguousarray(p.cost, dtype=np.float64), np.ascontiguousarray(p.free, dtype=bool),
                 [lv.astype(np.int64).tolist() for lv in p.levels], np.ascontiguousarray(p.access, dtype=np.float64))
-        r = mod.worst(*args, int(k), policy.w_span, policy.w_frag, policy.w_fit, policy.w_access, int(policy.exact_limit))
+        r = mod.worst(*args, int(k), policy.w_span, policy.w_frag, policy.w_fit, policy.w_access, int(policy.exact_limit),
+                      w_bottleneck=policy.w_bottleneck)
         terms = dict(r["terms"])
         terms["search_us"] = float(r["micros"])
         return Placement(ids=tuple(int(i) for i in r["ids"]), objective=float(r["objective"]),
