@@ -81,7 +81,7 @@ def make_cluster(n_nodes: int, degraded: int, seed: int, kind: str = "mi355x") -
             out.append(t)
         return out
     for i in range(n_nodes):
-        t = Topology.full_mesh(n=8, numa_split=2, link_gbps=153.0, noise=0.05, seed=seed * 1000 + i, node_name=f"node{i}")
+        t = Topology.full_mesh(n=8, numa_split=2, link_gbps=76.5, noise=0.05, seed=seed * 1000 + i, node_name=f"node{i}")
         bw = np.array(t.bw_gbps, dtype=float)
         pairs = [(a, b) for a in range(8) for b in range(a + 1, 8)]
         for idx in rng.choice(len(pairs), size=degraded, replace=False):

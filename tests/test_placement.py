@@ -279,3 +279,22 @@ def test_partition_aware_switch_on_cpx_node():
     assert np.allclose(blind_p.cost[same & off], blind_p.cost[~same].mean())  # on-package pairs priced as xGMI
     assert len(blind_p.levels) == 1  # NUMA only, no package level
     assert PlacementPolicy.from_dict(PlacementPolicy(partition_aware=False).to_dict()).partition_aware is False
+
+
+@pytest.mark.parametrize("engine", ["python", "native"])
+def test_bottleneck_term_avoids_a_slow_link_a_ring_cannot_skip(engine):
+    """GPUs 5-7 are taken; links 0-1 and 0-2 run at a third of nominal.  Every ring over {0,1,2,3}
+    uses one of them.  The mean pair cost alone (+2/3) keeps the job inside NUMA half 0-3 (crossing
+    to GPU 4 costs w_span + w_frag = 0.75); the bottleneck term moves it to {1,2,3,4}."""
+    if engine == "native" and not available("_placement"):
+        pytest.skip("_placement not built")
+    t = fx.f7_mi355x(link_gbps=76.5)  # cost 1.0 per nominal link
+    bw = np.array(t.bw_gbps, dtype=float)
+    for a, b in ((0, 1), (0, 2)):
+        bw[a, b] = bw[b, a] = bw[a, b] / 3.0
+    t.set_measured_bw(bw, {"method": "synthetic"})
+    used = [5, 6, 7]
+    assert set(select(t, 4, used=used, policy=PlacementPolicy(w_bottleneck=0.0), engine=engine).ids) == {0, 1, 2, 3}
+    pl = select(t, 4, used=used, policy=PlacementPolicy(), engine=engine)
+    assert set(pl.ids) == {1, 2, 3, 4}
+    assert pl.terms["bottleneck"] == pytest.approx(pl.comm)
