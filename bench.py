@@ -75,6 +75,9 @@ def parse(argv=None):
     ap.add_argument("--rccl-log", default="auto", choices=["auto", "on", "off"],
                     help="capture RCCL's INIT/GRAPH log (per-rank file under /tmp) and report the transports and "
                          "channel counts it chose; auto = on for k >= 2")
+    ap.add_argument("--fp32-check", type=int, default=1,
+                    help="after the headline (bf16): the same size as an fp32 sum, exact-checked and timed (BASELINE.md "
+                         "target 3 names both dtypes); 0 = skip")
     ap.add_argument("--sweep", default="auto",
                     help="after the headline timing: exact-checked size sweep MIN:MAX:FACTOR (nccl-tests style, "
                          "BASELINE.md target 3, peak busBW reported); 'auto' = 8:16G:8 on GPUs, 8:1M:8 for "
@@ -137,6 +140,39 @@ def run_sweep(runner, sizes, env, tdev, barrier_kw, gpu_sync):
     peak = max(rows, key=lambda r: r[key]) if rows else None
     return {"rows": rows, "peak": {"bytes": peak["bytes"], key: peak[key]} if peak else None,
             "all_exact": all(r["wrong"] == 0 for r in rows)}
+
+
+def run_other_dtype(runner, nbytes, dtype, env, tdev, barrier_kw, gpu_sync, steps):
+    """BASELINE.md target 3 names bf16 AND fp32 sums: the same communicator re-prepared for ``dtype``
+    at the headline size, exact-checked, then ``steps`` timed all-reduces (max over ranks)."""
+    import torch
+    import torch.distributed as dist
+
+    from gpu_topology_on_k8s_amd.parallel.allreduce import bus_factor
+
+    prev = runner.dtype
+    runner.dtype = dtype
+    try:
+        runner.resize(nbytes)
+        wrong = torch.tensor([runner.check()], dtype=torch.int64, device=tdev)
+        dist.all_reduce(wrong)
+        runner.step()
+        runner.synchronize()
+        dist.barrier(**barrier_kw)
+        gpu_sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            runner.step()
+        runner.synchronize()
+        gpu_sync()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=tdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    finally:
+        runner.dtype = prev
+    ms = float(t.item()) / steps * 1e3
+    alg = runner.nbytes / (ms / 1e3) / 1e9
+    return {"dtype": dtype, "bytes": runner.nbytes, "steps": steps, "ms_per_step": round(ms, 4),
+            "algbw_gbps": round(alg, 3), "busbw_gbps": round(alg * bus_factor(env.world), 3), "exact": int(wrong.item()) == 0}
 
 
 def run_graph_latency(runner, sizes, env, tdev, barrier_kw, gpu_sync, ops: int = 32, replays: int = 8):
@@ -391,6 +427,13 @@ def main(argv=None) -> int:
         except Exception as e:  # noqa: BLE001 - every rank runs the same sizes, so all land here together
             print(f"bench: size sweep aborted on rank {env.rank}: {e}", file=sys.stderr)
             sweep = {"error": str(e)[:300]}
+    other = None
+    if args.fp32_check and runner.comm is not None and args.dtype != "fp32":
+        try:  # supplementary, like the sweep
+            other = run_other_dtype(runner, headline_bytes, "fp32", env, tdev, barrier_kw, gpu_sync, max(1, min(args.steps, 20)))
+        except Exception as e:  # noqa: BLE001
+            print(f"bench: fp32 all-reduce aborted on rank {env.rank}: {e}", file=sys.stderr)
+            other = {"dtype": "fp32", "error": str(e)[:300]}
     graph = None
     want_graph = args.graph == "on" or (args.graph == "auto" and env.world == 1)
     if want_graph and sizes and runner.comm is not None and not args.inplace:
@@ -462,6 +505,7 @@ def main(argv=None) -> int:
             "link_probe": choice.extra.get("probe"),
             "k8s_placement": choice.extra.get("k8s"),
             "size_sweep": sweep,
+            "fp32_headline": other,
             "graph_latency": graph,
             "rccl": rccl,
             "worst_subset_ab": worst_ab,
