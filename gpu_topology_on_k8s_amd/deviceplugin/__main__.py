@@ -24,13 +24,13 @@ from .plugin import DevicePluginServer, PluginConfig, startup_topology
 from .proto import DEVICE_PLUGIN_PATH
 
 
-def make_api(apiserver: str, token: str):
+def make_api(apiserver: str, token: str, ca_file: str = "", insecure: bool = False):
     from ..k8s.api import RestKubeAPI
 
     if apiserver == "none":
         return None
     if apiserver:
-        return RestKubeAPI(apiserver, token=token or None, verify=False)
+        return RestKubeAPI(apiserver, token=token or None, ca_file=ca_file or None, verify=not insecure)
     if os.environ.get("KUBERNETES_SERVICE_HOST"):
         return RestKubeAPI.in_cluster()
     return None
@@ -48,6 +48,9 @@ def main(argv=None) -> int:
     ap.add_argument("--probe", default="off", choices=["off", "quick", "full"])
     ap.add_argument("--apiserver", default="", help="apiserver URL; default in-cluster; 'none' disables annotations")
     ap.add_argument("--token", default="")
+    ap.add_argument("--ca-file", default="", help="CA bundle that signs --apiserver's certificate (default: system CAs)")
+    ap.add_argument("--insecure-skip-tls-verify", action="store_true",
+                    help="do not verify --apiserver's certificate (test clusters only: the bearer token goes to whoever answers)")
     ap.add_argument("--dev-root", default="/dev", help="where the ROCm device nodes live (a placeholder dir on kind)")
     ap.add_argument("--device-specs", default="auto", choices=["auto", "strict", "stub"],
                     help="Allocate DeviceSpecs: strict = kfd + render/card nodes, fail if missing; stub = only nodes "
@@ -76,7 +79,7 @@ def main(argv=None) -> int:
     log = logging.getLogger("gtk.deviceplugin")
 
     topo = discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus)
-    api = make_api(a.apiserver, a.token)
+    api = make_api(a.apiserver, a.token, a.ca_file, a.insecure_skip_tls_verify)
     contract = Contract(resource_name=a.resource_name, prefix=a.annotation_prefix)
     probe_fn = None
     if a.probe != "off" and a.discovery != "fake":

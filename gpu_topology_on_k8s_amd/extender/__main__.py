@@ -38,12 +38,16 @@ def main(argv=None) -> int:
                     help="comma list of spec.schedulerName values whose pods may be bound (empty = any)")
     ap.add_argument("--apiserver", default="")
     ap.add_argument("--token", default="")
+    ap.add_argument("--ca-file", default="", help="CA bundle that signs --apiserver's certificate (default: system CAs)")
+    ap.add_argument("--insecure-skip-tls-verify", action="store_true",
+                    help="do not verify --apiserver's certificate (test clusters only: the bearer token goes to whoever answers)")
     ap.add_argument("--log-level", default="INFO")
     a = ap.parse_args(argv)
     logging.basicConfig(level=a.log_level, format='{"ts":"%(asctime)s","lvl":"%(levelname)s","mod":"%(name)s","msg":"%(message)s"}')
     from ..k8s.api import RestKubeAPI
 
-    api = RestKubeAPI(a.apiserver, token=a.token or None, verify=False) if a.apiserver else RestKubeAPI.in_cluster()
+    api = (RestKubeAPI(a.apiserver, token=a.token or None, ca_file=a.ca_file or None, verify=not a.insecure_skip_tls_verify)
+           if a.apiserver else RestKubeAPI.in_cluster())
     cfg = ExtenderConfig(contract=Contract(resource_name=a.resource_name, prefix=a.annotation_prefix), policy_name=a.policy,
                          policy=PlacementPolicy(tie_break=a.tie_break, partition_aware=a.partition_aware == "on"),
                          assume_ttl=a.assume_ttl, resync_s=a.resync,
