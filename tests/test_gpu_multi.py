@@ -83,7 +83,10 @@ def test_bench_two_gpus_native_exact_and_bounded():
     assert len(set(out["config"]["hip_devices"])) == 2
     bound = (out["link_probe"] or {}).get("subset_ingress_bound_gbps")
     if bound:
-        assert out["busbw_gbps"] <= 1.10 * bound, (out["busbw_gbps"], bound)
+        # the bound comes from the READ probe (64 MiB, 3 iterations); RCCL pushes with writes, which
+        # may run somewhat faster on a link, so only a gross excess (a wrong bus factor, a ring that
+        # is not where the placement put it) fails here
+        assert out["busbw_gbps"] <= 1.5 * bound, (out["busbw_gbps"], bound)
 
 
 @needs2
