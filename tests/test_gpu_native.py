@@ -65,7 +65,12 @@ def test_probe_cli_ingress_single_gpu(tmp_path):
                        capture_output=True, text=True, timeout=300, cwd=REPO)
     assert p.returncode == 0, p.stderr[-3000:]
     d = json.loads(out.read_text())
-    assert d["probe"]["ingress_all_gbps"][0] is None  # one GPU: no peers to gather from
+    import torch
+
+    if torch.cuda.device_count() == 1:
+        assert d["probe"]["ingress_all_gbps"][0] is None  # one GPU: no peers to gather from
+    else:
+        assert all(x is not None and x > 0 for x in d["probe"]["ingress_all_gbps"])
     assert d["hbm_gbps"][0] > 1000
 
 
@@ -196,7 +201,7 @@ def test_bench_py_single_gpu():
     assert p.returncode == 0, p.stderr[-4000:]
     line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
     out = json.loads(line)
-    assert out["n_gpus"] == 1 and out["value"] > 0 and out["config"]["subset"] == [0]
+    assert out["n_gpus"] == 1 and out["value"] > 0 and len(out["config"]["subset"]) == 1  # [0] on a 1-GPU box
     assert out["config"]["message_bytes_per_gpu"] == 64 << 20
     sw = out["size_sweep"]  # 8 B .. 16 GiB, every size exactly checked
     assert sw["all_exact"] and sw["rows"][-1]["bytes"] == 16 << 30 and sw["peak"]["algbw_gbps"] > 0
