@@ -56,6 +56,25 @@ class NodeState:
     synced_at: float = 0.0
     list_epoch: int = -1  # epoch of the newest pod LIST applied (older LISTs arriving late are stale)
     lock: threading.RLock = field(default_factory=threading.RLock, repr=False)
+    # Every change of topology / labels / capacity / usage bumps `version` and clears `memo`, where the
+    # extender keeps its per-pod-shape decisions for this node (sort fans out every pending pod over
+    # every node; most nodes have not changed since the previous pod of the same shape).
+    version: int = 0
+    memo: Dict[tuple, tuple] = field(default_factory=dict, repr=False)
+
+    def bump(self) -> None:
+        """Call with ``lock`` held after any change that can alter a placement on this node."""
+        self.version += 1
+        self.memo.clear()
+
+    def valid_until(self, now: float, ttl: float) -> float:
+        """Time after which :meth:`used` can shrink on its own: the earliest expiry of a live
+        unconfirmed assumption (``inf`` when none)."""
+        t = math.inf
+        for a in self.allocs.values():
+            if not a.assigned and now - a.assume_time <= ttl:
+                t = min(t, a.assume_time + ttl)
+        return t
 
     @property
     def unknown(self) -> int:
@@ -109,6 +128,9 @@ class ClusterCache:
         st = self._state(name)
         with st.lock:
             rv = meta(node).get("resourceVersion", "")
+            labels = dict(obj_labels(node))
+            if st.topology is None or rv != st.node_rv or not rv or labels != st.labels:
+                st.bump()
             if st.topology is None or rv != st.node_rv or not rv:
                 try:
                     st.topology = decode_node_annotations(obj_annotations(node), self.contract, node_name=name)
@@ -116,7 +138,7 @@ class ClusterCache:
                     log.warning("node %s: bad topology annotation: %s", name, e)
                     st.topology = None
                 st.node_rv = rv
-            st.labels = dict(obj_labels(node))
+            st.labels = labels
             alloc = ((node.get("status") or {}).get("allocatable") or {})
             st.capacity = -1
             for r in self.resources:
@@ -189,6 +211,7 @@ class ClusterCache:
         st.allocs = allocs
         st.unknown_pods = unknown
         st.synced_at = now
+        st.bump()
 
     def refresh_node(self, name: str) -> NodeState:
         """Authoritative re-read of one node and its pods (used before every bind)."""
@@ -295,6 +318,7 @@ class ClusterCache:
         st = self._state(node)
         with st.lock:
             st.allocs[pod] = a
+            st.bump()
 
     def bound(self, node: str, pod: str) -> None:
         """The binding of an assumed pod was accepted: a LIST started after this point must show the
@@ -309,6 +333,7 @@ class ClusterCache:
         st = self._state(node)
         with st.lock:
             st.allocs.pop(pod, None)
+            st.bump()
 
     # ------------------------------------------------------------------ watch events (fake / informer)
     def on_event(self, event: str, kind: str, obj: dict) -> None:
@@ -327,6 +352,7 @@ class ClusterCache:
         st = self._state(node)
         key = pod_key(obj)
         with st.lock:
+            st.bump()
             if event == "DELETED" or pod_is_terminal(obj):
                 st.allocs.pop(key, None)
                 st.unknown_pods.pop(key, None)

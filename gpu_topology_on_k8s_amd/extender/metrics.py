@@ -36,6 +36,7 @@ class ExtenderMetrics:
         self.decision_cache = Counter("gtk_extender_decision_cache_total", "placement decisions served from / added to the cache",
                                       ["result"], registry=self.registry)
 
+        self._hit, self._miss = self.decision_cache.labels(result="hit"), self.decision_cache.labels(result="miss")
         self._cache = None
 
     def attach_cache(self, cache, ttl: float, clock) -> None:
@@ -44,8 +45,8 @@ class ExtenderMetrics:
             self.registry.register(_FragmentationCollector(cache, ttl, clock))
         self._cache = cache
 
-    def cache(self, hit: bool) -> None:
-        self.decision_cache.labels(result="hit" if hit else "miss").inc()
+    def cache(self, hit: bool, n: int = 1) -> None:
+        (self._hit if hit else self._miss).inc(n)
 
     def observe(self, verb: str, seconds: float) -> None:
         self.latency.labels(verb).observe(seconds)

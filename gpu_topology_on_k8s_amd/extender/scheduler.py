@@ -27,6 +27,7 @@ This implementation adds:
 """
 from __future__ import annotations
 
+import dataclasses
 import logging
 import math
 import random
@@ -152,10 +153,9 @@ class TopologyExtender:
         except ValueError:
             return None
 
-    def _model_ok(self, pod: Dict[str, Any], st: NodeState) -> Tuple[bool, str]:
+    def _model_ok(self, want: Optional[str], st: NodeState) -> Tuple[bool, str]:
         """Heterogeneous-cluster quota (Gaia B7): a pod never receives a mix of GPU models, and a
-        pod asking for a model (annotation or label) only lands on nodes advertising it."""
-        want = obj_annotations(pod).get(self.cfg.contract.pod_model_key) or obj_labels(pod).get(self.cfg.contract.pod_model_key)
+        pod asking for a model (``want``: its annotation or label) only lands on nodes advertising it."""
         t = st.topology
         models = {g.model for g in t.gpus} if t is not None else set()
         node_model = st.labels.get(self.cfg.contract.label_model)
@@ -220,50 +220,77 @@ class TopologyExtender:
                         self.cfg.policy)
         return tuple(sorted(int(i) for i in ids)), score_from_objective(j), j
 
-    def _eval_state(self, pod: Dict[str, Any], name: str, st: NodeState, k: int) -> Tuple[Optional[Decision], str]:
-        """Decision for ``pod`` on the node state ``st`` as cached now.  Never calls the apiserver,
-        so it may run under the node lock (bind)."""
-        with st.lock:
-            t = st.topology
-            if t is None:
-                return None, "node has no GPU topology annotation"
-            ok, why = self._model_ok(pod, st)
-            if not ok:
-                return None, why
-            try:
-                fraction = self.fraction_of(pod)
-            except ValueError as e:
-                return None, str(e)
-            if fraction is not None:
-                sizes = {}
-                for g in t.gpus:
-                    sizes[g.physical] = sizes.get(g.physical, 0) + 1
-                per_gpu = max(sizes.values()) if sizes else 1
-                if per_gpu <= 1:
-                    return None, "fractional GPU requests need a partitioned (CPX/DPX/QPX) node"
-                need = max(1, math.ceil(fraction * per_gpu - 1e-9))
-                if need != k:
-                    return None, (f"gpu-fraction {fraction} is {need} of {per_gpu} partitions per GPU on this node, "
-                                  f"but the pod requests {k} devices")
-            now = self.clock()
-            used = sorted(st.used(now, self.cfg.assume_ttl))
-            free = st.free_count(now, self.cfg.assume_ttl)
-            if free < k:
-                return None, f"insufficient free devices: need {k}, free {free}"
-            access = access_costs(t, self.numa_preference(pod)) if self.cfg.cpu_affinity else None
-            t0 = time.perf_counter()
-            try:
-                ids, score, obj = self._choose_cached(t, used, k, access, fraction)
-            except NoFeasiblePlacement as e:
-                return None, str(e)
-            us = (time.perf_counter() - t0) * 1e6
-            rank = obj + node_packing_term(free, k, t.n, self.cfg.policy)
-            return Decision(node=name, ids=ids, score=score, objective=obj,
-                            policy="fragment" if fraction is not None else self.cfg.policy_name, micros=us, rank=rank), ""
+    def _pod_shape(self, pod: Dict[str, Any], k: int) -> Tuple[Optional[tuple], str]:
+        """What a placement depends on from the pod: (k, fraction, NUMA preference, GPU model), parsed
+        once per request; (None, reason) for a malformed fraction."""
+        try:
+            fraction = self.fraction_of(pod)
+        except ValueError as e:
+            return None, str(e)
+        numa = self.numa_preference(pod)
+        want = obj_annotations(pod).get(self.cfg.contract.pod_model_key) or obj_labels(pod).get(self.cfg.contract.pod_model_key)
+        return (k, fraction, tuple(numa) if numa else None, want), ""
 
-    def _node_eval(self, pod: Dict[str, Any], name: str, node_obj: Optional[dict], k: int) -> Tuple[Optional[Decision], str]:
+    def _eval_state(self, pod: Dict[str, Any], name: str, st: NodeState, k: int,
+                    shape: Optional[tuple] = None) -> Tuple[Optional[Decision], str]:
+        """Decision for ``pod`` on the node state ``st`` as cached now.  Never calls the apiserver,
+        so it may run under the node lock (bind).  Memoised per node on the pod's shape (k, fraction,
+        NUMA preference, GPU model) until the node state changes or a live assumption expires."""
+        if shape is None:
+            shape, why = self._pod_shape(pod, k)
+            if shape is None:
+                return None, why
+        _, fraction, numa, want = shape
+        with st.lock:
+            now = self.clock()
+            if self._cacheable():
+                hit = st.memo.get(shape)
+                if hit is not None and hit[0] <= now <= hit[1]:
+                    self.metrics.cache(True)
+                    return hit[2], hit[3]
+            d, why = self._eval_state_uncached(st, name, k, fraction, numa, want, now)
+            if self._cacheable():
+                st.memo[shape] = (now, st.valid_until(now, self.cfg.assume_ttl), d, why)
+            return d, why
+
+    def _eval_state_uncached(self, st: NodeState, name: str, k: int, fraction: Optional[float], numa, want,
+                             now: float) -> Tuple[Optional[Decision], str]:
+        t = st.topology
+        if t is None:
+            return None, "node has no GPU topology annotation"
+        ok, why = self._model_ok(want, st)
+        if not ok:
+            return None, why
+        if fraction is not None:
+            sizes = {}
+            for g in t.gpus:
+                sizes[g.physical] = sizes.get(g.physical, 0) + 1
+            per_gpu = max(sizes.values()) if sizes else 1
+            if per_gpu <= 1:
+                return None, "fractional GPU requests need a partitioned (CPX/DPX/QPX) node"
+            need = max(1, math.ceil(fraction * per_gpu - 1e-9))
+            if need != k:
+                return None, (f"gpu-fraction {fraction} is {need} of {per_gpu} partitions per GPU on this node, "
+                              f"but the pod requests {k} devices")
+        used = sorted(st.used(now, self.cfg.assume_ttl))
+        free = st.free_count(now, self.cfg.assume_ttl)
+        if free < k:
+            return None, f"insufficient free devices: need {k}, free {free}"
+        access = access_costs(t, numa) if self.cfg.cpu_affinity else None
+        t0 = time.perf_counter()
+        try:
+            ids, score, obj = self._choose_cached(t, used, k, access, fraction)
+        except NoFeasiblePlacement as e:
+            return None, str(e)
+        us = (time.perf_counter() - t0) * 1e6
+        rank = obj + node_packing_term(free, k, t.n, self.cfg.policy)
+        return Decision(node=name, ids=ids, score=score, objective=obj,
+                        policy="fragment" if fraction is not None else self.cfg.policy_name, micros=us, rank=rank), ""
+
+    def _node_eval(self, pod: Dict[str, Any], name: str, node_obj: Optional[dict], k: int,
+                   shape: Optional[tuple] = None) -> Tuple[Optional[Decision], str]:
         st = self.cache.get(name, node_obj)  # may sync the cache: never call with a node lock held
-        return self._eval_state(pod, name, st, k)
+        return self._eval_state(pod, name, st, k, shape)
 
     # ------------------------------------------------------------------ verbs
     def filter(self, pod: Dict[str, Any], node_names: Sequence[str], node_objs: Optional[Dict[str, dict]] = None):
@@ -272,11 +299,15 @@ class TopologyExtender:
         k = self.request_of(pod)
         ok: List[str] = []
         failed: Dict[str, str] = {}
+        shape, bad = self._pod_shape(pod, k) if k else (None, "")
         for n in node_names:
             if k == 0:
                 ok.append(n)
                 continue
-            d, why = self._node_eval(pod, n, (node_objs or {}).get(n), k)
+            if shape is None:
+                failed[n] = bad
+                continue
+            d, why = self._node_eval(pod, n, (node_objs or {}).get(n), k, shape)
             if d is None:
                 failed[n] = why
             else:
@@ -290,10 +321,11 @@ class TopologyExtender:
         t0 = time.perf_counter()
         k = self.request_of(pod)
         objs: Dict[str, float] = {}
+        shape, _ = self._pod_shape(pod, k) if k else (None, "")
         for n in node_names:
-            if k == 0:
+            if shape is None:
                 continue
-            d, _ = self._node_eval(pod, n, (node_objs or {}).get(n), k)
+            d, _ = self._node_eval(pod, n, (node_objs or {}).get(n), k, shape)
             if d is not None:
                 objs[n] = d.rank if d.rank == d.rank else d.objective
                 self.metrics.score(d.score)
@@ -333,7 +365,7 @@ class TopologyExtender:
                 d, why = self._eval_state(pod, node, st, k)
                 if d is None:
                     raise NoFeasiblePlacement(f"bind {namespace}/{name} on {node}: {why}")
-                d.cpuset = recommended_cpuset(st.topology, d.ids)
+                d = dataclasses.replace(d, cpuset=recommended_cpuset(st.topology, d.ids))  # memo entries stay unshared
                 key = pod_key(pod)
                 now = self.clock()
                 pa = PodAssignment.assumed(d.ids, now)

@@ -35,6 +35,7 @@ class Informer:
         self.backoff = backoff
         self._stop = threading.Event()
         self._synced = {k: threading.Event() for k in self.kinds}
+        self._all_synced = False
         self._threads: List[threading.Thread] = []
         self.lists: Dict[str, int] = {k: 0 for k in self.kinds}  # LIST calls made (relists after the first)
         self.events: Dict[str, int] = {k: 0 for k in self.kinds}
@@ -42,7 +43,11 @@ class Informer:
 
     @property
     def synced(self) -> bool:
-        return all(e.is_set() for e in self._synced.values())
+        # sync flags are only ever set, so once every kind has listed the answer stays True (this is
+        # read once per candidate node on the extender's sort path)
+        if not self._all_synced:
+            self._all_synced = all(e.is_set() for e in self._synced.values())
+        return self._all_synced
 
     def wait_synced(self, timeout: float = 30.0) -> bool:
         for e in self._synced.values():
