@@ -208,10 +208,11 @@ class ClusterCache:
             for key in set(self._overlay_epoch) - {(st.name, k) for k in ov}:
                 if key[0] == st.name:
                     del self._overlay_epoch[key]
+        if allocs != st.allocs or unknown != st.unknown_pods:  # a resync that changes nothing keeps the memo
+            st.bump()
         st.allocs = allocs
         st.unknown_pods = unknown
         st.synced_at = now
-        st.bump()
 
     def refresh_node(self, name: str) -> NodeState:
         """Authoritative re-read of one node and its pods (used before every bind)."""

@@ -330,3 +330,32 @@ def test_decision_cache_hits_and_invalidates():
 
     _, rnd, _ = _cluster(policy=PlacementPolicy(tie_break="random"))
     assert not rnd._cacheable()
+
+
+def test_node_memo_tracks_state_version_and_assumption_expiry():
+    """The per-node memo answers a same-shape pod without re-evaluating; any usage change (bind,
+    watch event) or the expiry of a live assumption invalidates it, and pod shapes never mix."""
+    api, ext, clock = _cluster(assume_ttl=60.0)
+    st = ext.cache.get("n1")
+    a = _submit(api, "a", 4)
+    ext.prioritize(a, ["n1"])
+    v0, memo0 = st.version, dict(st.memo)
+    assert len(memo0) == 1
+    ext.prioritize(_submit(api, "a2", 4), ["n1"])
+    assert st.version == v0 and st.memo == memo0  # served from the memo
+    ext.prioritize(_submit(api, "pinned", 4, annotations={Contract().numa_pref_key: "1"}), ["n1"])
+    assert len(st.memo) == 2  # a NUMA preference is another shape
+    _bind(api, ext, "a")
+    assert st.version > v0
+    b = _submit(api, "b", 4)
+    ok, _ = ext.filter(b, ["n1"])
+    assert ok == ["n1"]
+    _submit(api, "c", 1)
+    assert ext.filter(api.get_pod("default", "c"), ["n1"])[0] == ["n1"]
+    _submit(api, "big", 8)
+    assert ext.filter(api.get_pod("default", "big"), ["n1"])[0] == []  # 4 assumed
+    clock.t += 61  # the assumption of "a" expires without any state change
+    assert ext.filter(api.get_pod("default", "big"), ["n1"])[0] == ["n1"]
+    v1 = st.version
+    ext.cache.on_event("MODIFIED", "Pod", api.get_pod("default", "a"))
+    assert st.version > v1 and not st.memo
