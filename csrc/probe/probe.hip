@@ -132,6 +132,29 @@ __global__ __launch_bounds__(kBlock) void copy_reg_kernel(const u32x4* __restric
     dst[i] = src[i];
 }
 
+// Contiguous-chunk variant: block b streams its own 1/grid slice of the buffer (each workgroup walks
+// one DRAM region, instead of the whole grid sweeping one window together), U independent 16-B
+// loads in flight per lane, non-temporal loads and stores.
+template <int U>
+__global__ __launch_bounds__(kBlock) void copy_chunk_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                            size_t n_vec) {
+  const size_t tile = (size_t)kBlock * U;
+  const size_t n_tiles = n_vec / tile;
+  const size_t per = (n_tiles + gridDim.x - 1) / gridDim.x;
+  const size_t t0 = (size_t)blockIdx.x * per;
+  const size_t t1 = std::min(n_tiles, t0 + per);
+  for (size_t t = t0; t < t1; ++t) {
+    const size_t base = t * tile + threadIdx.x;
+    u32x4 r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) r[u] = __builtin_nontemporal_load(src + base + (size_t)u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; ++u) __builtin_nontemporal_store(r[u], dst + base + (size_t)u * kBlock);
+  }
+  for (size_t i = n_tiles * tile + (size_t)blockIdx.x * kBlock + threadIdx.x; i < n_vec; i += (size_t)gridDim.x * kBlock)
+    dst[i] = src[i];
+}
+
 __global__ __launch_bounds__(kBlock) void fill_pattern_kernel(unsigned int* __restrict__ p, size_t n_words,
                                                               unsigned int seed) {
   for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n_words; i += (size_t)gridDim.x * kBlock)
@@ -222,11 +245,15 @@ void launch_copy(const std::string& kind, bool nt, const void* src, void* dst, s
       hipLaunchKernelGGL(copy_reg_kernel<true>, dim3(grid), dim3(kBlock), 0, s, S, D, n_vec);
     else
       hipLaunchKernelGGL(copy_reg_kernel<false>, dim3(grid), dim3(kBlock), 0, s, S, D, n_vec);
+  } else if (kind == "chunk") {
+    hipLaunchKernelGGL(copy_chunk_kernel<8>, dim3(grid), dim3(kBlock), 0, s, S, D, n_vec);
+  } else if (kind == "chunk4") {
+    hipLaunchKernelGGL(copy_chunk_kernel<4>, dim3(grid), dim3(kBlock), 0, s, S, D, n_vec);
   } else if (kind == "sdma") {
     HIP_CHECK(hipMemcpyAsync(dst, src, n_vec * 16, hipMemcpyDeviceToDevice, s));
     return;
   } else {
-    throw std::invalid_argument("kind must be lds|reg|sdma");
+    throw std::invalid_argument("kind must be lds|reg|chunk|chunk4|sdma");
   }
   HIP_CHECK(hipGetLastError());
 }
