@@ -10,6 +10,9 @@
 //   FAKE_AMDSMI_PARTITIONS  XCPs per package (1 = SPX, 8 = CPX)
 //   FAKE_AMDSMI_HIP_ORDER   comma list: HIP id of each enumerated processor (default identity)
 //   FAKE_AMDSMI_DOWN        "a-b": the xGMI link between packages a and b is down (PCIe, 2 hops)
+//   FAKE_AMDSMI_EVENTS_FILE GPU event script: every line "<processor index> <event id> <message>" is
+//                           delivered once by amdsmi_get_gpu_event_notification (lines appended while
+//                           a watcher runs arrive on its next poll)
 // Built by gpu_topology_on_k8s_amd/_native/build.py (target fake_amdsmi); never loaded in production.
 #include <amd_smi/amdsmi.h>
 
@@ -17,7 +20,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <chrono>
+#include <fstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -248,6 +255,62 @@ amdsmi_status_t amdsmi_get_gpu_bad_page_info(amdsmi_processor_handle h, uint32_t
 amdsmi_status_t amdsmi_get_gpu_bad_page_threshold(amdsmi_processor_handle h, uint32_t* threshold) {
   if (idx(h) < 0 || !threshold) return AMDSMI_STATUS_INVAL;
   *threshold = 128;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+// ---- GPU event notification: scripted through FAKE_AMDSMI_EVENTS_FILE
+namespace {
+std::vector<uint64_t> g_evt_mask;
+size_t g_evt_delivered = 0;
+
+bool next_events(uint32_t cap, uint32_t* n, amdsmi_evt_notification_data_t* data) {
+  const char* path = std::getenv("FAKE_AMDSMI_EVENTS_FILE");
+  *n = 0;
+  if (!path) return false;
+  std::ifstream f(path);
+  std::string line;
+  size_t lineno = 0;
+  while (*n < cap && std::getline(f, line)) {
+    if (lineno++ < g_evt_delivered || line.empty()) continue;
+    ++g_evt_delivered;
+    int dev = -1, id = 0, off = 0;
+    if (std::sscanf(line.c_str(), "%d %d %n", &dev, &id, &off) < 2 || dev < 0 || dev >= g_node.n()) continue;
+    if (dev >= (int)g_evt_mask.size() || !(g_evt_mask[dev] & AMDSMI_EVENT_MASK_FROM_INDEX(id))) continue;
+    amdsmi_evt_notification_data_t& d = data[(*n)++];
+    d.processor_handle = reinterpret_cast<amdsmi_processor_handle>((intptr_t)dev + 1);
+    d.event = (amdsmi_evt_notification_type_t)id;
+    std::snprintf(d.message, sizeof(d.message), "%s", line.c_str() + off);
+  }
+  return *n > 0;
+}
+}  // namespace
+
+amdsmi_status_t amdsmi_init_gpu_event_notification(amdsmi_processor_handle h) {
+  if (!g_init || idx(h) < 0) return AMDSMI_STATUS_INVAL;
+  if ((int)g_evt_mask.size() < g_node.n()) g_evt_mask.assign(g_node.n(), 0);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_set_gpu_event_notification_mask(amdsmi_processor_handle h, uint64_t mask) {
+  if (idx(h) < 0 || (int)g_evt_mask.size() <= idx(h)) return AMDSMI_STATUS_INVAL;
+  g_evt_mask[idx(h)] = mask;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_event_notification(int timeout_ms, uint32_t* num_elem, amdsmi_evt_notification_data_t* data) {
+  if (!num_elem || !data) return AMDSMI_STATUS_INVAL;
+  const uint32_t cap = *num_elem;
+  const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(std::max(0, timeout_ms));
+  while (!next_events(cap, num_elem, data)) {
+    if (std::chrono::steady_clock::now() >= until) return AMDSMI_STATUS_NO_DATA;
+    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  }
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_stop_gpu_event_notification(amdsmi_processor_handle h) {
+  if (idx(h) < 0) return AMDSMI_STATUS_INVAL;
+  if (idx(h) < (int)g_evt_mask.size()) g_evt_mask[idx(h)] = 0;
   return AMDSMI_STATUS_SUCCESS;
 }
 

@@ -23,6 +23,7 @@
 #include <sstream>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <vector>
 
 namespace py = pybind11;
@@ -174,6 +175,10 @@ struct AmdSmi {
   decltype(&amdsmi_get_gpu_total_ecc_count) get_ecc_total = nullptr;
   decltype(&amdsmi_get_gpu_bad_page_info) get_bad_pages = nullptr;
   decltype(&amdsmi_get_gpu_bad_page_threshold) get_bad_page_threshold = nullptr;
+  decltype(&amdsmi_init_gpu_event_notification) evt_init = nullptr;
+  decltype(&amdsmi_set_gpu_event_notification_mask) evt_mask = nullptr;
+  decltype(&amdsmi_get_gpu_event_notification) evt_get = nullptr;
+  decltype(&amdsmi_stop_gpu_event_notification) evt_stop = nullptr;
 
   template <class F>
   void bind(F& f, const char* sym, bool required) {
@@ -205,6 +210,10 @@ struct AmdSmi {
     bind(get_ecc_total, "amdsmi_get_gpu_total_ecc_count", false);
     bind(get_bad_pages, "amdsmi_get_gpu_bad_page_info", false);
     bind(get_bad_page_threshold, "amdsmi_get_gpu_bad_page_threshold", false);
+    bind(evt_init, "amdsmi_init_gpu_event_notification", false);
+    bind(evt_mask, "amdsmi_set_gpu_event_notification_mask", false);
+    bind(evt_get, "amdsmi_get_gpu_event_notification", false);
+    bind(evt_stop, "amdsmi_stop_gpu_event_notification", false);
   }
   ~AmdSmi() {
     if (h) dlclose(h);
@@ -363,6 +372,102 @@ Result discover_amdsmi_impl(const std::string& lib) {
   assign_physical(r);
   return r;
 }
+
+// ------------------------------------------------------------------------------------------------
+// GPU event notification (amdsmi): resets, VM faults, thermal throttling as they happen, instead of
+// waiting for the next RAS poll (SURVEY.md §5.3 failure detection).  The device plugin polls this
+// on its own thread; events name the device by PCI address.
+const char* event_name(amdsmi_evt_notification_type_t e) {
+  switch (e) {
+    case AMDSMI_EVT_NOTIF_VMFAULT: return "VMFAULT";
+    case AMDSMI_EVT_NOTIF_THERMAL_THROTTLE: return "THERMAL_THROTTLE";
+    case AMDSMI_EVT_NOTIF_GPU_PRE_RESET: return "GPU_PRE_RESET";
+    case AMDSMI_EVT_NOTIF_GPU_POST_RESET: return "GPU_POST_RESET";
+    case AMDSMI_EVT_NOTIF_MIGRATE_START: return "MIGRATE_START";
+    case AMDSMI_EVT_NOTIF_MIGRATE_END: return "MIGRATE_END";
+    case AMDSMI_EVT_NOTIF_PAGE_FAULT_START: return "PAGE_FAULT_START";
+    case AMDSMI_EVT_NOTIF_PAGE_FAULT_END: return "PAGE_FAULT_END";
+    case AMDSMI_EVT_NOTIF_QUEUE_EVICTION: return "QUEUE_EVICTION";
+    case AMDSMI_EVT_NOTIF_QUEUE_RESTORE: return "QUEUE_RESTORE";
+    case AMDSMI_EVT_NOTIF_UNMAP_FROM_GPU: return "UNMAP_FROM_GPU";
+    case AMDSMI_EVT_NOTIF_PROCESS_START: return "PROCESS_START";
+    case AMDSMI_EVT_NOTIF_PROCESS_END: return "PROCESS_END";
+    default: return "NONE";
+  }
+}
+
+class EventWatcher {
+ public:
+  EventWatcher(const std::string& lib, const std::vector<std::string>& kinds) : s_(lib) {
+    if (!s_.evt_init || !s_.evt_mask || !s_.evt_get || !s_.evt_stop)
+      throw std::runtime_error("this amdsmi has no GPU event notification API");
+    uint64_t mask = 0;
+    for (const auto& k : kinds) {
+      int id = -1;
+      for (int e = AMDSMI_EVT_NOTIF_FIRST; e <= AMDSMI_EVT_NOTIF_LAST; ++e)
+        if (k == event_name((amdsmi_evt_notification_type_t)e)) id = e;
+      if (id < 0) throw std::invalid_argument("unknown GPU event kind: " + k);
+      mask |= AMDSMI_EVENT_MASK_FROM_INDEX(id);
+    }
+    if (s_.init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) throw std::runtime_error("amdsmi_init failed");
+    inited_ = true;
+    uint32_t nsock = 0;
+    if (s_.get_socket_handles(&nsock, nullptr) != AMDSMI_STATUS_SUCCESS) throw std::runtime_error("socket count");
+    std::vector<amdsmi_socket_handle> socks(nsock);
+    if (nsock && s_.get_socket_handles(&nsock, socks.data()) != AMDSMI_STATUS_SUCCESS) throw std::runtime_error("socket handles");
+    for (auto sk : socks) {
+      uint32_t np = 0;
+      if (s_.get_processor_handles(sk, &np, nullptr) != AMDSMI_STATUS_SUCCESS) continue;
+      std::vector<amdsmi_processor_handle> ph(np);
+      if (np && s_.get_processor_handles(sk, &np, ph.data()) != AMDSMI_STATUS_SUCCESS) continue;
+      for (auto p : ph) {
+        processor_type_t t;
+        if (s_.get_processor_type(p, &t) != AMDSMI_STATUS_SUCCESS || t != AMDSMI_PROCESSOR_TYPE_AMD_GPU) continue;
+        amdsmi_bdf_t b;
+        std::string bdf;
+        if (s_.get_bdf(p, &b) == AMDSMI_STATUS_SUCCESS) bdf = fmt_bdf(b.domain_number, b.bus_number, b.device_number, b.function_number);
+        if (s_.evt_init(p) != AMDSMI_STATUS_SUCCESS) continue;  // e.g. no permission on this device
+        handles_.push_back(p);
+        bdfs_.push_back(bdf);
+        if (s_.evt_mask(p, mask) != AMDSMI_STATUS_SUCCESS) throw std::runtime_error("event mask on " + bdf);
+      }
+    }
+    if (handles_.empty()) throw std::runtime_error("no GPU accepted event notification");
+  }
+  ~EventWatcher() { close(); }
+
+  // Events collected for up to timeout_ms (returns early when some arrive): (bdf, kind, message).
+  std::vector<std::tuple<std::string, std::string, std::string>> poll(int timeout_ms, uint32_t max_events) {
+    std::vector<std::tuple<std::string, std::string, std::string>> out;
+    if (handles_.empty()) return out;
+    std::vector<amdsmi_evt_notification_data_t> buf(std::max<uint32_t>(1, max_events));
+    uint32_t n = (uint32_t)buf.size();
+    amdsmi_status_t st = s_.evt_get(timeout_ms, &n, buf.data());
+    if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_NO_DATA) return out;
+    for (uint32_t i = 0; i < n && i < buf.size(); ++i) {
+      std::string bdf;
+      for (size_t j = 0; j < handles_.size(); ++j)
+        if (handles_[j] == buf[i].processor_handle) bdf = bdfs_[j];
+      buf[i].message[AMDSMI_MAX_STRING_LENGTH - 1] = 0;
+      out.emplace_back(bdf, event_name(buf[i].event), std::string(buf[i].message));
+    }
+    return out;
+  }
+
+  void close() {
+    for (auto p : handles_) s_.evt_stop(p);
+    handles_.clear();
+    if (inited_) s_.shut_down();
+    inited_ = false;
+  }
+  const std::vector<std::string>& bdfs() const { return bdfs_; }
+
+ private:
+  AmdSmi s_;
+  bool inited_ = false;
+  std::vector<amdsmi_processor_handle> handles_;
+  std::vector<std::string> bdfs_;
+};
 
 // ------------------------------------------------------------------------------------------------
 // KFD sysfs backend
@@ -634,6 +739,21 @@ PYBIND11_MODULE(_topo, m) {
       },
       py::arg("root") = "/sys/class/kfd/kfd/topology", py::arg("drm_root") = "/sys/class/drm",
       py::arg("pci_root") = "/sys/bus/pci/devices", py::arg("node_root") = "/sys/devices/system/node");
+  py::class_<EventWatcher>(m, "EventWatcher")
+      .def(py::init<const std::string&, const std::vector<std::string>&>(), py::arg("lib") = "libamd_smi.so",
+           py::arg("kinds") = std::vector<std::string>{"GPU_PRE_RESET", "GPU_POST_RESET", "VMFAULT", "THERMAL_THROTTLE"})
+      .def("poll",
+           [](EventWatcher& w, int timeout_ms, uint32_t max_events) {
+             std::vector<std::tuple<std::string, std::string, std::string>> ev;
+             {
+               py::gil_scoped_release nogil;
+               ev = w.poll(timeout_ms, max_events);
+             }
+             return ev;
+           },
+           py::arg("timeout_ms") = 1000, py::arg("max_events") = 64)
+      .def("close", &EventWatcher::close)
+      .def_property_readonly("bdfs", &EventWatcher::bdfs);
   m.attr("HSA_IOLINK_TYPE_XGMI") = 11;
   m.attr("HSA_IOLINK_TYPE_PCIEXPRESS") = 2;
 }

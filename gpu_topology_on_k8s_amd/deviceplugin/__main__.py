@@ -73,6 +73,9 @@ def main(argv=None) -> int:
                     help="republish the topology when a measured pair moved by more than this fraction")
     ap.add_argument("--partition-aware", default="on", choices=["on", "off"],
                     help="GetPreferredAllocation on CPX/DPX/QPX nodes: group XCPs by physical GPU (on) or not (off)")
+    ap.add_argument("--gpu-events", default="auto", choices=["auto", "off"],
+                    help="amdsmi GPU event notification (reset / VM fault / thermal throttle) on its own thread; "
+                         "auto = on wherever amdsmi offers it")
     ap.add_argument("--log-level", default="INFO")
     a = ap.parse_args(argv)
     logging.basicConfig(level=a.log_level, format='{"ts":"%(asctime)s","lvl":"%(levelname)s","mod":"%(name)s","msg":"%(message)s"}')
@@ -105,13 +108,19 @@ def main(argv=None) -> int:
                        reprobe_tolerance=a.reprobe_tolerance, pod_resources_socket=a.pod_resources_socket,
                        reconcile_interval=a.reconcile_interval,
                        policy=PlacementPolicy(partition_aware=a.partition_aware == "on"))
+    events = None
+    if a.gpu_events == "auto" and a.discovery in ("auto", "amdsmi"):
+        from .events import GpuEventWatcher
+
+        events = GpuEventWatcher.try_open()
     reprobe = None
-    if a.reprobe_interval > 0 and a.discovery != "fake":
+    if (a.reprobe_interval > 0 or events is not None) and a.discovery != "fake":
         from ..ops.probe import probe_in_child
 
         def reprobe():
             return probe_in_child(a.probe if a.probe != "off" else "quick", backend=a.discovery)[0]
     plugin = DevicePluginServer(topo, cfg, api=api, health_fn=health if a.discovery != "fake" else None, reprobe_fn=reprobe)
+    plugin.event_source = events
     if a.metrics_port:
         from .metrics import serve_metrics
 

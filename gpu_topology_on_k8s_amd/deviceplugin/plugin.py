@@ -200,6 +200,10 @@ class DevicePluginServer:
         # daemon exits for a clean restart instead of advertising stale device IDs
         self.layout_change = threading.Event()
         self.layout_change_reason = ""
+        # devices held Unhealthy by a GPU event (reset in progress) whatever the RAS poll says
+        self._holds: Dict[int, str] = {}
+        self._reprobe_now = threading.Event()  # a GPU reset finished: re-measure as soon as the node is idle
+        self.event_source = None  # deviceplugin.events.GpuEventWatcher (amdsmi event notification)
 
     # ------------------------------------------------------------------ device view
     def devices(self) -> List[pb.Device]:
@@ -686,18 +690,70 @@ class DevicePluginServer:
         if register:
             self.register()
         self._threads = [threading.Thread(target=self._monitor, name="devplugin-monitor", daemon=True)]
-        if self.reprobe_fn is not None and self.cfg.reprobe_interval > 0:
+        if self.reprobe_fn is not None and (self.cfg.reprobe_interval > 0 or self.event_source is not None):
             # its own thread: a probe takes minutes and must not stall health polling / re-registration
             self._threads.append(threading.Thread(target=self._reprobe_loop, name="devplugin-reprobe", daemon=True))
+        if self.event_source is not None:
+            self._threads.append(threading.Thread(target=self.event_source.run, args=(self, self._stop),
+                                                  name="devplugin-gpu-events", daemon=True))
         for t in self._threads:
             t.start()
 
     def _reprobe_loop(self) -> None:
-        while not self._stop.wait(self.cfg.reprobe_interval):
+        """Every ``reprobe_interval`` s (0 = never), or as soon as a finished GPU reset asks for it (the
+        reset may have retrained links) and the node is idle."""
+        interval = self.cfg.reprobe_interval if self.cfg.reprobe_interval > 0 else float("inf")
+        deadline = time.monotonic() + interval
+        while not self._stop.is_set():
+            if not self._reprobe_now.is_set() and time.monotonic() < deadline:
+                self._reprobe_now.wait(min(1.0, deadline - time.monotonic()))
+                continue
+            if self._reprobe_now.is_set() and not self.node_idle():
+                self._stop.wait(5.0)  # keep the request; retry once the node drains
+                continue
+            self._reprobe_now.clear()
+            deadline = time.monotonic() + interval
             try:
                 self.reprobe()
             except Exception as e:
                 log.warning("link re-probe failed: %s", e)
+
+    # ------------------------------------------------------------------ GPU events (amdsmi notification)
+    def gpu_event(self, index: int, kind: str, message: str = "") -> None:
+        """One amdsmi GPU event for device ``index`` (SURVEY.md §5.3 failure detection, between RAS polls):
+        ``GPU_PRE_RESET`` holds the device Unhealthy at once (a reset kills every queue on it);
+        ``GPU_POST_RESET`` releases the hold — the next RAS pass decides — and asks for a link
+        re-measurement once the node is idle; ``VMFAULT`` / ``THERMAL_THROTTLE`` are counted and
+        recorded as Node events (a VM fault is a workload's bug, throttling a cooling problem: neither
+        takes the device out of service)."""
+        if not 0 <= index < self.topology.n:
+            return
+        self.metrics.gpu_events.labels(kind).inc()
+        bdf = self.topology.gpus[index].bdf or "no bdf"
+        node = {"kind": "Node", "metadata": {"name": self.cfg.node_name}}
+        if kind == "GPU_PRE_RESET":
+            self._holds[index] = "GPU reset in progress"
+            log.warning("device %d (%s): GPU reset starting: %s", index, bdf, message)
+            self.set_health(index, False)
+            reason, note = "GPUReset", f"device {index} ({bdf}) is resetting; held Unhealthy"
+        elif kind == "GPU_POST_RESET":
+            self._holds.pop(index, None)
+            log.warning("device %d (%s): GPU reset finished: %s", index, bdf, message)
+            if self.health_fn is None:
+                self.set_health(index, True)
+            self._reprobe_now.set()
+            reason, note = "GPUResetDone", f"device {index} ({bdf}) finished a reset; links re-measured when idle"
+        elif kind == "VMFAULT":
+            log.warning("device %d (%s): VM fault: %s", index, bdf, message)
+            reason, note = "GPUVMFault", f"device {index} ({bdf}): GPU VM fault: {message[:200]}"
+        elif kind == "THERMAL_THROTTLE":
+            log.warning("device %d (%s): thermal throttling: %s", index, bdf, message)
+            reason, note = "GPUThermalThrottle", f"device {index} ({bdf}) is thermally throttled: {message[:200]}"
+        else:
+            return
+        if self.api is not None and self.cfg.node_name:
+            record_event(self.api, node, reason, note, "Normal" if kind == "GPU_POST_RESET" else "Warning",
+                         component="gpu-topology-device-plugin", host=self.cfg.node_name)
 
     def _monitor(self) -> None:
         """Health polling and kubelet restart detection (the kubelet wipes plugin sockets on restart)."""
@@ -722,7 +778,7 @@ class DevicePluginServer:
                 next_health = time.monotonic() + self.cfg.health_interval
                 try:
                     for idx, ok in self.health_fn(self.topology).items():
-                        self.set_health(int(idx), bool(ok))
+                        self.set_health(int(idx), bool(ok) and int(idx) not in self._holds)
                     changed = getattr(self.health_fn, "layout_changed", lambda: None)()
                     if changed:
                         if not self.layout_change.is_set():

@@ -265,3 +265,22 @@ def test_bench_py_reports_rccl_log():
     r = out["rccl"]
     assert r and "error" not in r, r
     assert r["communicators"] >= 1 and r["nranks"] == [1] and r["version"], r
+
+
+def test_gpu_event_watcher_on_real_node():
+    """amdsmi GPU event notification as the device plugin opens it: every GPU subscribed, a short poll
+    returns (no reset is expected on the box), close releases the event files."""
+    from gpu_topology_on_k8s_amd._native import load
+    from gpu_topology_on_k8s_amd.topology.identity import hip_device_bdfs
+
+    try:
+        w = load("_topo").EventWatcher("libamd_smi.so", ["GPU_PRE_RESET", "GPU_POST_RESET", "VMFAULT", "THERMAL_THROTTLE"])
+    except RuntimeError as e:
+        pytest.skip(f"event notification unavailable to this user: {e}")
+    try:
+        assert w.bdfs and set(b.lower() for b in hip_device_bdfs()) <= set(b.lower() for b in w.bdfs)
+        ev = w.poll(100, 16)
+        assert isinstance(ev, list)
+        print(json.dumps({"bdfs": w.bdfs, "events": ev}))
+    finally:
+        w.close()
