@@ -52,9 +52,11 @@ def main(argv=None) -> int:
     ap.add_argument("--insecure-skip-tls-verify", action="store_true",
                     help="do not verify --apiserver's certificate (test clusters only: the bearer token goes to whoever answers)")
     ap.add_argument("--dev-root", default="/dev", help="where the ROCm device nodes live (a placeholder dir on kind)")
-    ap.add_argument("--device-specs", default="auto", choices=["auto", "strict", "stub"],
+    ap.add_argument("--cdi-dir", default="/var/run/cdi", help="--device-specs cdi: where the CDI spec is written")
+    ap.add_argument("--device-specs", default="auto", choices=["auto", "strict", "stub", "cdi"],
                     help="Allocate DeviceSpecs: strict = kfd + render/card nodes, fail if missing; stub = only nodes "
-                         "that exist under --dev-root (kind / fake GPUs); auto = stub for --discovery fake, else strict")
+                         "that exist under --dev-root (kind / fake GPUs); cdi = CDI device names resolved by the spec written to "
+                         "--cdi-dir (CDI-enabled runtimes); auto = stub for --discovery fake, else strict")
     ap.add_argument("--xgmi-link-loss", default="degrade", choices=["degrade", "unhealthy"],
                     help="a GPU whose xGMI link drops: degrade = republish the pair at its new link class and keep the "
                          "GPU schedulable; unhealthy = advertise the GPU Unhealthy")
@@ -106,7 +108,7 @@ def main(argv=None) -> int:
                        node_name=a.node_name, contract=contract, device_specs=specs, prestart_validate=a.prestart_validate,
                        health_interval=a.health_interval, reprobe_interval=a.reprobe_interval,
                        reprobe_tolerance=a.reprobe_tolerance, pod_resources_socket=a.pod_resources_socket,
-                       reconcile_interval=a.reconcile_interval,
+                       reconcile_interval=a.reconcile_interval, cdi_dir=a.cdi_dir,
                        policy=PlacementPolicy(partition_aware=a.partition_aware == "on"))
     events = None
     if a.gpu_events == "auto" and a.discovery in ("auto", "amdsmi"):

@@ -44,8 +44,11 @@ class _Plugin:
 
 
 class FakeKubelet:
-    def __init__(self, socket_dir: str, node_name: str = "", api=None, pod_resources_socket: Optional[str] = None):
+    def __init__(self, socket_dir: str, node_name: str = "", api=None, pod_resources_socket: Optional[str] = None,
+                 cdi_dir: Optional[str] = None):
         self.socket_dir = socket_dir
+        # a CDI-enabled runtime resolves Allocate's cdi_devices against the specs in this directory
+        self.cdi_dir = cdi_dir
         # the pod-resources API (v1 PodResourcesLister.List) lives in its own directory on a real
         # node (/var/lib/kubelet/pod-resources/kubelet.sock); here a subdirectory of socket_dir
         self.pod_resources_socket = pod_resources_socket or os.path.join(socket_dir, "pod-resources", "kubelet.sock")
@@ -202,6 +205,9 @@ class FakeKubelet:
             # what containerd does next: every DeviceSpec must name a device node that exists on the
             # host, or the container is never created (BASELINE config 1 on a kind node)
             missing = [d.host_path for c in resp.container_responses for d in c.devices if not os.path.exists(d.host_path)]
+            for c in resp.container_responses:
+                for cd in c.cdi_devices:
+                    missing += self._cdi_missing(cd.name)
             if missing:
                 raise AdmissionError(f"CreateContainerError: device nodes do not exist on the node: {missing}")
             if getattr(p.options, "pre_start_required", False):
@@ -223,6 +229,26 @@ class FakeKubelet:
             except Exception:  # pragma: no cover
                 pass
         return resp
+
+    def _cdi_missing(self, name: str) -> List[str]:
+        """What a CDI runtime would fail on for device ``name`` (``vendor/class=dev``): no spec of that
+        kind, no such device, or a device node the spec names that is absent on the host."""
+        import glob
+        import json
+
+        kind, _, dev = name.partition("=")
+        for path in sorted(glob.glob(os.path.join(self.cdi_dir or "/nonexistent", "*.json"))):
+            with open(path) as f:
+                spec = json.load(f)
+            if spec.get("kind") != kind:
+                continue
+            for d in spec.get("devices", []):
+                if d.get("name") == dev:
+                    nodes = list(d.get("containerEdits", {}).get("deviceNodes", []))
+                    nodes += spec.get("containerEdits", {}).get("deviceNodes", [])
+                    return [n.get("hostPath") or n["path"] for n in nodes if not os.path.exists(n.get("hostPath") or n["path"])]
+            return [f"CDI device {name} not in {path}"]
+        return [f"unresolvable CDI device {name}"]
 
     def release(self, pod: dict) -> None:
         key = pod_key(pod)

@@ -130,7 +130,8 @@ class PluginConfig:
                  resource_aliases: Sequence[str] = ("aliyun.com/gpu", "aliyun.com/gpu-count"),
                  reprobe_interval: float = 0.0, reprobe_tolerance: float = 0.15, device_specs: str = "strict",
                  prestart_validate: bool = False, validate_timeout: float = 120.0,
-                 pod_resources_socket: Optional[str] = POD_RESOURCES_SOCKET, reconcile_interval: float = 10.0):
+                 pod_resources_socket: Optional[str] = POD_RESOURCES_SOCKET, reconcile_interval: float = 10.0,
+                 cdi_dir: str = "/var/run/cdi", cdi_kind: str = "amd.com/gpu"):
         self.resource_name = resource_name
         self.socket_dir = socket_dir
         self.socket_name = socket_name
@@ -150,10 +151,13 @@ class PluginConfig:
         # Allocate's DeviceSpecs: "strict" = /dev/kfd + every device's render/card node, Allocate fails
         # if one is missing on the node (a container must never start without its GPU); "stub" = only
         # the nodes that exist under dev_root (a kind node with fake GPUs has none: envs + annotations
-        # only, BASELINE config 1)
-        if device_specs not in ("strict", "stub"):
-            raise ValueError(f"device_specs must be strict|stub, got {device_specs!r}")
+        # only, BASELINE config 1); "cdi" = CDI names (``cdi_kind=<index>``) resolved by the spec the
+        # plugin writes into ``cdi_dir`` (deviceplugin/cdi.py): the runtime injects the nodes
+        if device_specs not in ("strict", "stub", "cdi"):
+            raise ValueError(f"device_specs must be strict|stub|cdi, got {device_specs!r}")
         self.device_specs = device_specs
+        self.cdi_dir = cdi_dir
+        self.cdi_kind = cdi_kind
         # flow step 8: before the container starts, an RCCL all-reduce over exactly
         # the allocated devices (kubelet PreStartContainer) validates the placement; the measured
         # bus bandwidth is recorded on the pod
@@ -239,6 +243,7 @@ class DevicePluginServer:
             self._version += 1
             self._cond.notify_all()
         self.metrics.set_topology(topo)
+        self.write_cdi_spec()
         self._publish_node()
 
     # ------------------------------------------------------------------ link re-measurement
@@ -507,7 +512,12 @@ class DevicePluginServer:
 
     def _container_response(self, ids: Sequence[int], extra_env: Dict[str, str]) -> pb.ContainerAllocateResponse:
         r = pb.ContainerAllocateResponse()
-        for cpath, hpath in self.device_nodes(ids):
+        if self.cfg.device_specs == "cdi":
+            from .cdi import cdi_name
+
+            for i in ids:
+                r.cdi_devices.add(name=cdi_name(self.cfg.cdi_kind, i))
+        for cpath, hpath in ([] if self.cfg.device_specs == "cdi" else self.device_nodes(ids)):
             if self.cfg.device_specs == "stub" and not os.path.exists(hpath):
                 continue  # kind / fake GPUs: never hand containerd a host path the node does not have
             r.devices.add(container_path=cpath, host_path=hpath, permissions="rw")
@@ -683,8 +693,19 @@ class DevicePluginServer:
         self.metrics.registrations.inc()
         log.info("registered %s with kubelet at %s", self.cfg.resource_name, self.cfg.kubelet_socket)
 
+    def write_cdi_spec(self) -> Optional[str]:
+        """(``device_specs == "cdi"``) the CDI spec of the advertised devices -> its path."""
+        if self.cfg.device_specs != "cdi":
+            return None
+        from .cdi import build_spec, write_spec
+
+        path = write_spec(build_spec(self.topology, self.cfg.cdi_kind, self.cfg.dev_root), self.cfg.cdi_dir)
+        log.info("CDI spec for %d devices written to %s", self.topology.n, path)
+        return path
+
     def start(self, register: bool = True) -> None:
         self._stop.clear()
+        self.write_cdi_spec()
         self._publish_node()
         self.serve()
         if register:

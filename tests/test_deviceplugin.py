@@ -253,3 +253,45 @@ def test_reprobe_runs_from_the_monitor_loop():
     finally:
         plug.stop()
         shutil.rmtree(sockdir, ignore_errors=True)
+
+
+def test_cdi_mode_allocates_by_cdi_name_and_writes_the_spec(sockdir):
+    """--device-specs cdi: Allocate returns `amd.com/gpu=<GROUP index>` names, no DeviceSpecs; the spec
+    the plugin wrote resolves every name to existing render/card nodes plus the common /dev/kfd."""
+    import json
+
+    api = FakeAPIServer()
+    api.create_node(make_node("n1"))
+    cdi = os.path.join(sockdir, "cdi")
+    kubelet = FakeKubelet(sockdir, node_name="n1", api=api, cdi_dir=cdi)
+    kubelet.start()
+    topo = fx.f7_mi355x()
+    dev = placeholder_dev_tree(os.path.join(sockdir, "dev"), topo)
+    plugin = DevicePluginServer(topo, PluginConfig(resource_name=RES, socket_dir=sockdir, node_name="n1", dev_root=dev,
+                                                   device_specs="cdi", cdi_dir=cdi), api=api)
+    plugin.start()
+    try:
+        kubelet.wait_for(RES)
+        spec = json.load(open(os.path.join(cdi, "amd.com-gpu.json")))
+        assert spec["kind"] == "amd.com/gpu" and len(spec["devices"]) == 8
+        assert spec["containerEdits"]["deviceNodes"][0]["path"] == "/dev/kfd"
+        ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+        pod = api.create_pod(make_pod("cdi", gpus=2))
+        d = ext.bind("default", "cdi", pod["metadata"]["uid"], "n1")
+        resp = kubelet.admit(api.get_pod("default", "cdi"), RES)
+        c = resp.container_responses[0]
+        assert [x.name for x in c.cdi_devices] == [f"amd.com/gpu={i}" for i in d.ids] and len(c.devices) == 0
+        assert c.envs["GTK_GPU_GROUP"] == ",".join(map(str, d.ids))
+        # a runtime with the spec gone cannot create the container
+        os.unlink(os.path.join(cdi, "amd.com-gpu.json"))
+        from gpu_topology_on_k8s_amd.deviceplugin.kubelet import AdmissionError
+
+        with pytest.raises(AdmissionError, match="unresolvable CDI"):
+            kubelet.admit(api.create_pod(make_pod("cdi2", gpus=1)), RES)
+        plugin.update_topology(topo)  # republish rewrites the spec
+        assert os.path.exists(os.path.join(cdi, "amd.com-gpu.json"))
+    finally:
+        plugin.stop()
+        kubelet.stop()
+    with pytest.raises(ValueError):
+        PluginConfig(device_specs="nvidia")
