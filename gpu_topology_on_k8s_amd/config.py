@@ -6,7 +6,7 @@
   removed in Kubernetes 1.23, so this is only for old clusters.
 * :func:`scheduler_configuration` — the same extender as a ``KubeSchedulerConfiguration``
   (``kubescheduler.config.k8s.io/v1``) ``extenders:`` stanza for current clusters, optionally with
-  the ``filter`` verb this framework adds.
+  the ``filter`` and ``preempt`` verbs this framework adds.
 * :func:`render_manifests` — DaemonSet (device plugin, Prometheus ``/metrics`` on :32744), DaemonSet
   (extender on every control-plane node's host network, listening on 127.0.0.1 only: each
   kube-scheduler replica calls its own node's extender on loopback, and ``/bind`` is unauthenticated,
@@ -50,7 +50,7 @@ def legacy_policy(resource: str = COMPAT_RESOURCE, url: Optional[str] = None, wi
 
 def scheduler_configuration(resource: str = DEFAULT_RESOURCE, url: Optional[str] = None, with_filter: bool = True,
                             scheduler_name: str = "default-scheduler", weight: int = 5,
-                            extra_resources: Optional[List[str]] = None) -> Dict[str, Any]:
+                            extra_resources: Optional[List[str]] = None, with_preempt: bool = True) -> Dict[str, Any]:
     managed = [{"name": r, "ignoredByScheduler": False} for r in [resource] + list(extra_resources or [])]
     ext: Dict[str, Any] = {
         "urlPrefix": url or extender_url(),
@@ -65,6 +65,8 @@ def scheduler_configuration(resource: str = DEFAULT_RESOURCE, url: Optional[str]
     }
     if with_filter:
         ext["filterVerb"] = "filter"
+    if with_preempt:  # topology-aware victim selection (extender/scheduler.py TopologyExtender.preempt)
+        ext["preemptVerb"] = "preempt"
     return {
         "apiVersion": "kubescheduler.config.k8s.io/v1",
         "kind": "KubeSchedulerConfiguration",

@@ -42,6 +42,7 @@ class Alloc:
     assume_time: float
     source: str = "annotation"  # annotation | overlay
     cpuset: str = ""  # cores recommended to the pod at bind (<prefix>/cpuset)
+    uid: str = ""  # pod UID (preemption victims are named by UID)
 
 
 @dataclass
@@ -52,6 +53,7 @@ class NodeState:
     node_rv: str = ""
     allocs: Dict[str, Alloc] = field(default_factory=dict)
     unknown_pods: Dict[str, int] = field(default_factory=dict)  # pod -> devices held without a GROUP annotation
+    unknown_uids: Dict[str, str] = field(default_factory=dict)  # pod UID -> pod key of unknown_pods
     capacity: int = -1  # node.status.allocatable[resource] (-1 = unknown)
     synced_at: float = 0.0
     list_epoch: int = -1  # epoch of the newest pod LIST applied (older LISTs arriving late are stale)
@@ -163,7 +165,7 @@ class ClusterCache:
                 req = 0
             return None, req
         return Alloc(pod=pod_key(pod), ids=tuple(pa.group), assigned=pa.assigned, assume_time=float(pa.assume_time),
-                     cpuset=obj_annotations(pod).get(self.contract.cpuset_key, "")), 0
+                     cpuset=obj_annotations(pod).get(self.contract.cpuset_key, ""), uid=str(meta(pod).get("uid", ""))), 0
 
     def _next_epoch(self) -> int:
         with self._lock:
@@ -180,12 +182,14 @@ class ClusterCache:
         st.list_epoch = list_epoch
         allocs: Dict[str, Alloc] = {}
         unknown: Dict[str, int] = {}
+        unknown_uids: Dict[str, str] = {}
         seen = set()
         for p in pods:
             seen.add(pod_key(p))
             a, u = self._pod_alloc(p)
             if u:
                 unknown[pod_key(p)] = u
+                unknown_uids[str(meta(p).get("uid", ""))] = pod_key(p)
             if a is not None:
                 allocs[a.pod] = a
         now = self.clock()
@@ -212,6 +216,7 @@ class ClusterCache:
             st.bump()
         st.allocs = allocs
         st.unknown_pods = unknown
+        st.unknown_uids = unknown_uids
         st.synced_at = now
 
     def refresh_node(self, name: str) -> NodeState:
@@ -307,9 +312,10 @@ class ClusterCache:
         return st
 
     # ------------------------------------------------------------------ writes made by this process
-    def assume(self, node: str, pod: str, ids: Iterable[int], at: Optional[float] = None, cpuset: str = "") -> None:
+    def assume(self, node: str, pod: str, ids: Iterable[int], at: Optional[float] = None, cpuset: str = "",
+               uid: str = "") -> None:
         a = Alloc(pod=pod, ids=tuple(int(i) for i in ids), assigned=False, assume_time=at if at is not None else self.clock(),
-                  source="overlay", cpuset=cpuset)
+                  source="overlay", cpuset=cpuset, uid=uid)
         with self._lock:
             self._overlay.setdefault(node, {})[pod] = a
             # pending until :meth:`bound`: a LIST taken while the pod is still unbound does not show
@@ -369,6 +375,7 @@ class ClusterCache:
             else:
                 if u:
                     st.unknown_pods[key] = u
+                    st.unknown_uids[str(meta(obj).get("uid", ""))] = key
                 else:
                     st.unknown_pods.pop(key, None)
                 if key in st.allocs and st.allocs[key].source == "annotation":

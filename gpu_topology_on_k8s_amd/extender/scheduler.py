@@ -42,7 +42,7 @@ from ..k8s.api import ApiError, KubeAPI
 from ..k8s.events import record_event
 from ..k8s.objects import annotations as obj_annotations
 from ..k8s.objects import labels as obj_labels
-from ..k8s.objects import pod_gpu_request, pod_key
+from ..k8s.objects import meta, pod_gpu_request, pod_key
 from ..placement import NoFeasiblePlacement, PlacementPolicy, place_fraction, select
 from ..placement.core import node_packing_term
 from ..placement.gaia import gaia_schedule, tree_from_topology
@@ -376,7 +376,7 @@ class TopologyExtender:
                 if d.cpuset:
                     ann[self.cfg.contract.cpuset_key] = d.cpuset
                 ann[self.cfg.contract.score_key] = f"{d.score:.3f}"
-                self.cache.assume(node, key, d.ids, now, cpuset=d.cpuset)
+                self.cache.assume(node, key, d.ids, now, cpuset=d.cpuset, uid=uid or str(meta(pod).get("uid", "")))
                 try:
                     self._patch_with_retry(namespace, name, ann)
                     self.api.bind_pod(namespace, name, uid, node)
@@ -403,6 +403,73 @@ class TopologyExtender:
             raise
         finally:
             self.metrics.observe("bind", time.perf_counter() - t0)
+
+    def preempt(self, pod: Dict[str, Any], victims: Dict[str, Tuple[List[str], int]],
+                max_subsets: int = 4096) -> Dict[str, Tuple[List[str], int]]:
+        """kube-scheduler extender ``preemptVerb``: refine the scheduler's victims per candidate node.
+
+        kube-scheduler picks victims by priority and resource counts only; any lower-priority pods that
+        together free k devices qualify, wherever those devices sit.  Here, per node, the victims that
+        hold no GROUP devices (chosen for CPU/memory, or holding devices without an annotation) are kept
+        as proposed, and among the GROUP holders the extender keeps the smallest subset whose devices,
+        together with the free ones, host the pod — and among those the one whose best placement has
+        the lowest objective (evicting the two pods on one NUMA half beats evicting one on each).
+        Nodes where even all victims do not make the pod placeable are dropped.  ``victims``:
+        node -> (victim pod UIDs, NumPDBViolations); the PDB count is passed through (fewer victims
+        can only violate fewer budgets)."""
+        import itertools
+
+        t0 = time.perf_counter()
+        k = self.request_of(pod)
+        out: Dict[str, Tuple[List[str], int]] = {}
+        shape, _ = self._pod_shape(pod, k) if k else (None, "")
+        for node, (uids, pdb) in victims.items():
+            if k == 0:
+                out[node] = (list(uids), pdb)
+                continue
+            if shape is None:
+                continue
+            st = self.cache.get(node)
+            with st.lock:
+                t = st.topology
+                if t is None:
+                    continue
+                now = self.clock()
+                live = {a.uid: a for a in st.allocs.values()
+                        if a.uid and (a.assigned or now - a.assume_time <= self.cfg.assume_ttl)}
+                gpu = [u for u in uids if u in live]
+                keep = [u for u in uids if u not in live]
+                freed_unknown = sum(st.unknown_pods.get(st.unknown_uids.get(u, ""), 0) for u in keep)
+                used = st.used(now, self.cfg.assume_ttl)
+                healthy = {g.index for g in t.gpus if g.healthy}
+                _, fraction, numa, _ = shape
+                access = access_costs(t, numa) if self.cfg.cpu_affinity else None
+                best = None
+                tried = 0
+                for r in range(0, len(gpu) + 1):
+                    for sub in itertools.combinations(gpu, r):
+                        tried += 1
+                        if tried > max_subsets:
+                            break
+                        freed = set().union(*(live[u].ids for u in sub)) if sub else set()
+                        still = sorted((used - freed) & set(range(t.n)))
+                        free = len(healthy) - len(set(still) & healthy) - max(0, st.unknown - freed_unknown)
+                        if free < k:
+                            continue
+                        try:
+                            _, _, obj = self._choose_cached(t, still, k, access, fraction)
+                        except NoFeasiblePlacement:
+                            continue
+                        if best is None or obj < best[0] - 1e-12:
+                            best = (obj, list(sub))
+                    if best is not None or tried > max_subsets:
+                        break  # the smallest victim count that works (or the search budget) decides
+                if best is None:
+                    continue
+                chosen = set(best[1])
+                out[node] = ([u for u in uids if u in chosen or u in keep], pdb)
+        self.metrics.observe("preempt", time.perf_counter() - t0)
+        return out
 
     def _patch_with_retry(self, namespace: str, name: str, ann: Dict[str, str]) -> None:
         last: Optional[Exception] = None

@@ -7,6 +7,7 @@ Reference endpoint (``design.md:98-100``): ``http://127.0.0.1:32743/gputopology-
   POST {prefix}/prioritize  alias of /sort
   POST {prefix}/filter      ExtenderArgs -> ExtenderFilterResult       (optional)
   POST {prefix}/bind        ExtenderBindingArgs -> ExtenderBindingResult
+  POST {prefix}/preempt     ExtenderPreemptionArgs -> ExtenderPreemptionResult (topology-aware victims)
   GET  {prefix}/healthz, /metrics (Prometheus text), /version, /debug/nodes (cache snapshot)
 
 kube-scheduler marshals Go structs without json tags, so request keys are capitalised (``Pod``,
@@ -119,6 +120,26 @@ def make_app(ext: TopologyExtender, prefix: str = DEFAULT_PREFIX, workers: int =
             ext.metrics.request("bind", "error")
             return web.json_response({"Error": str(e)})
 
+    async def preempt(request: web.Request) -> web.Response:
+        args = await body(request)
+        pod = _get(args, "Pod") or {}
+        victims: Dict[str, Tuple[List[str], int]] = {}
+        meta_v = _get(args, "NodeNameToMetaVictims") or {}
+        full_v = _get(args, "NodeNameToVictims") or {}
+        for node, v in list(full_v.items()) + list(meta_v.items()):
+            pods = _get(v or {}, "Pods") or []
+            uids = [str(_get(p, "UID") or ((_get(p, "metadata") or {}).get("uid", ""))) for p in pods]
+            victims[node] = ([u for u in uids if u], int(_get(v or {}, "NumPDBViolations", 0) or 0))
+        try:
+            res = await run_blocking(ext.preempt, pod, victims)
+            ext.metrics.request("preempt", "ok")
+        except Exception as e:  # the scheduler's own victims stand
+            log.exception("preempt failed")
+            ext.metrics.request("preempt", "error")
+            res = victims
+        return web.json_response({"NodeNameToMetaVictims": {
+            n: {"Pods": [{"UID": u} for u in uids], "NumPDBViolations": pdb} for n, (uids, pdb) in res.items()}})
+
     async def healthz(request: web.Request) -> web.Response:
         return web.Response(text="ok")
 
@@ -139,6 +160,7 @@ def make_app(ext: TopologyExtender, prefix: str = DEFAULT_PREFIX, workers: int =
     app.router.add_post(f"{prefix}/prioritize", prioritize)
     app.router.add_post(f"{prefix}/filter", filter_)
     app.router.add_post(f"{prefix}/bind", bind)
+    app.router.add_post(f"{prefix}/preempt", preempt)
     for p in (f"{prefix}/healthz", "/healthz"):
         app.router.add_get(p, healthz)
     app.router.add_get(f"{prefix}/metrics", metrics)

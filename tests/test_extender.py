@@ -359,3 +359,60 @@ def test_node_memo_tracks_state_version_and_assumption_expiry():
     v1 = st.version
     ext.cache.on_event("MODIFIED", "Pod", api.get_pod("default", "a"))
     assert st.version > v1 and not st.memo
+
+
+def _running(api, ext, name, k):
+    """A bound, Allocate-confirmed pod holding k devices."""
+    pod = _submit(api, name, k)
+    d = ext.bind("default", name, pod["metadata"]["uid"], "n1")
+    api.patch_pod_annotations("default", name, {ANN_ASSIGNED: "true"})
+    return api.get_pod("default", name), d
+
+
+def test_preempt_keeps_the_smallest_victim_set_with_the_best_topology():
+    """kube-scheduler proposes every lower-priority pod; a 4-GPU pod needs only the two 2-GPU pods of
+    one NUMA half gone.  The extender keeps those two, drops the rest, and keeps non-GPU victims."""
+    api, ext, _ = _cluster()
+    held = [_running(api, ext, f"p{i}", 2) for i in range(4)]  # 0-1, 2-3 | 4-5, 6-7 (or similar)
+    uids = [p["metadata"]["uid"] for p, _ in held]
+    cpu_only = api.create_pod(make_pod("cpu-only", gpus=0))["metadata"]["uid"]
+    pod = _submit(api, "big", 4)
+    res = ext.preempt(pod, {"n1": (uids + [cpu_only], 1)})
+    kept, pdb = res["n1"]
+    assert pdb == 1 and cpu_only in kept
+    gpu_kept = [u for u in kept if u != cpu_only]
+    assert len(gpu_kept) == 2
+    freed = set()
+    for (p, d) in held:
+        if p["metadata"]["uid"] in gpu_kept:
+            freed |= set(d.ids)
+    numa = {fx.f7_mi355x().gpus[i].numa for i in freed}
+    assert len(freed) == 4 and len(numa) == 1  # a whole NUMA half, not one pair from each side
+
+
+def test_preempt_drops_nodes_where_victims_do_not_suffice():
+    api, ext, _ = _cluster()
+    held = [_running(api, ext, f"q{i}", 4) for i in range(2)]
+    pod = _submit(api, "all8", 8)
+    one = held[0][0]["metadata"]["uid"]
+    assert ext.preempt(pod, {"n1": ([one], 0)}) == {}
+    both = [p["metadata"]["uid"] for p, _ in held]
+    assert sorted(ext.preempt(pod, {"n1": (both, 0)})["n1"][0]) == sorted(both)
+
+
+def test_http_preempt_wire_format():
+    api, ext, _ = _cluster()
+    held = [_running(api, ext, f"w{i}", 4) for i in range(2)]
+    pod = _submit(api, "want4", 4)
+    args = {"Pod": pod, "NodeNameToMetaVictims": {"n1": {"Pods": [{"UID": p["metadata"]["uid"]} for p, _ in held],
+                                                          "NumPDBViolations": 0}}}
+
+    async def go():
+        async with TestClient(TestServer(make_app(ext))) as client:
+            r = await client.post("/gputopology-scheduler/preempt", json=args)
+            return r.status, await r.json()
+
+    status, body = asyncio.run(go())
+    assert status == 200
+    pods = body["NodeNameToMetaVictims"]["n1"]["Pods"]
+    assert len(pods) == 1 and body["NodeNameToMetaVictims"]["n1"]["NumPDBViolations"] == 0
