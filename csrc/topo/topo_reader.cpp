@@ -51,9 +51,19 @@ struct Dev {
   double pcie_link_ratio = -1.0;
 };
 
+// RDMA NIC (RoCE / InfiniBand verbs device) and its PCIe distance class to every GPU: multi-node
+// RCCL traffic should leave through the NIC behind the GPU's own PCIe switch.
+struct Nic {
+  std::string name, bdf, netdev, state;
+  int numa = -1;
+  double rate_gbps = 0.0;
+};
+
 struct Result {
   std::string source;
   std::vector<Dev> devs;
+  std::vector<Nic> nics;
+  std::vector<std::vector<int>> gpu_nic;  // [gpu][nic] PCIe class: 1 PIX, 2 PXB, 3 PHB, 4 NODE, 5 SYS, 0 unknown
   std::vector<std::vector<int>> link_type, hops;  // link_type uses LinkType of model.py
   std::vector<std::vector<double>> weight, min_bw, max_bw;
   std::vector<std::vector<int>> p2p;
@@ -138,6 +148,19 @@ py::dict to_py(const Result& r) {
   py::dict nd;
   for (const auto& kv : r.numa_distance) nd[py::int_(kv.first)] = kv.second;
   out["numa_distance"] = nd;
+  py::list nics;
+  for (const auto& n : r.nics) {
+    py::dict d;
+    d["name"] = n.name;
+    d["bdf"] = n.bdf;
+    d["netdev"] = n.netdev;
+    d["state"] = n.state;
+    d["numa"] = n.numa;
+    d["rate_gbps"] = n.rate_gbps;
+    nics.append(d);
+  }
+  out["nics"] = nics;
+  out["gpu_nic"] = r.gpu_nic;
   out["warnings"] = r.warnings;
   return out;
 }
@@ -558,6 +581,62 @@ void read_host_affinity(Result& r, const std::string& pci_root, const std::strin
   }
 }
 
+// PCI path of a device below /sys/devices: ["pci0000:00", "0000:00:01.1", ..., "<bdf>"] (empty if unknown)
+std::vector<std::string> pci_path(const std::string& link) {
+  char buf[4096];
+  if (!realpath(link.c_str(), buf)) return {};
+  std::vector<std::string> parts;
+  std::stringstream ss(buf);
+  std::string item;
+  bool in = false;
+  while (std::getline(ss, item, '/')) {
+    if (!in && item.rfind("pci", 0) == 0 && item.find(':') != std::string::npos) in = true;
+    if (in && !item.empty()) parts.push_back(item);
+  }
+  return parts;
+}
+
+// The reference's PCIe taxonomy (design.md:31-47, nvidia-smi topo -m) for a GPU-NIC pair:
+// PIX = behind one PCIe switch, PXB = several bridges below the same root port, PHB = through the host
+// bridge, NODE = different root complexes of one NUMA node, SYS = across sockets.
+int pcie_class(const std::vector<std::string>& a, const std::vector<std::string>& b, int numa_a, int numa_b) {
+  if (a.empty() || b.empty()) return 0;
+  if (a[0] != b[0]) return numa_a >= 0 && numa_a == numa_b ? 4 : 5;
+  size_t l = 0;
+  while (l < a.size() && l < b.size() && a[l] == b[l]) ++l;
+  if (l <= 1) return 3;
+  if (a.size() - l <= 2 && b.size() - l <= 2) return 1;
+  return 2;
+}
+
+void read_nics(Result& r, const std::string& pci_root, const std::string& ib_root) {
+  if (ib_root.empty()) return;
+  std::vector<std::vector<std::string>> nic_paths;
+  for (const auto& name : list_dir(ib_root)) {
+    if (name.empty() || name[0] == '.') continue;
+    const std::string dev = ib_root + "/" + name + "/device";
+    auto path = pci_path(dev);
+    if (path.empty()) continue;
+    Nic n;
+    n.name = name;
+    n.bdf = path.back();
+    const std::string numa = read_first_line(dev + "/numa_node");
+    if (!numa.empty()) n.numa = std::atoi(numa.c_str());
+    n.state = read_first_line(ib_root + "/" + name + "/ports/1/state");  // e.g. "4: ACTIVE"
+    n.rate_gbps = std::atof(read_first_line(ib_root + "/" + name + "/ports/1/rate").c_str());  // "400 Gb/sec (4X NDR)"
+    for (const auto& nd : list_dir(dev + "/net"))
+      if (!nd.empty() && nd[0] != '.') n.netdev = nd;
+    r.nics.push_back(n);
+    nic_paths.push_back(path);
+  }
+  r.gpu_nic.assign(r.devs.size(), std::vector<int>(r.nics.size(), 0));
+  for (size_t g = 0; g < r.devs.size(); ++g) {
+    if (r.devs[g].bdf.empty() || pci_root.empty()) continue;
+    auto gp = pci_path(pci_dir(pci_root, r.devs[g].bdf));
+    for (size_t i = 0; i < r.nics.size(); ++i) r.gpu_nic[g][i] = pcie_class(gp, nic_paths[i], r.devs[g].numa, r.nics[i].numa);
+  }
+}
+
 struct KfdLink {
   int from, to, type;
   double weight, min_bw, max_bw;
@@ -715,30 +794,34 @@ PYBIND11_MODULE(_topo, m) {
   m.doc() = "MI355X topology discovery: amdsmi (dlopen) and KFD sysfs backends";
   m.def(
       "discover_amdsmi",
-      [](const std::string& lib, const std::string& pci_root, const std::string& node_root) {
+      [](const std::string& lib, const std::string& pci_root, const std::string& node_root, const std::string& ib_root) {
         Result r;
         {
           py::gil_scoped_release nogil;
           r = discover_amdsmi_impl(lib);
           read_host_affinity(r, pci_root, node_root);
+          read_nics(r, pci_root, ib_root);
         }
         return to_py(r);
       },
       py::arg("lib") = "libamd_smi.so", py::arg("pci_root") = "/sys/bus/pci/devices",
-      py::arg("node_root") = "/sys/devices/system/node");
+      py::arg("node_root") = "/sys/devices/system/node", py::arg("ib_root") = "/sys/class/infiniband");
   m.def(
       "discover_sysfs",
-      [](const std::string& root, const std::string& drm_root, const std::string& pci_root, const std::string& node_root) {
+      [](const std::string& root, const std::string& drm_root, const std::string& pci_root, const std::string& node_root,
+         const std::string& ib_root) {
         Result r;
         {
           py::gil_scoped_release nogil;
           r = discover_sysfs_impl(root, drm_root);
           read_host_affinity(r, pci_root, node_root);
+          read_nics(r, pci_root, ib_root);
         }
         return to_py(r);
       },
       py::arg("root") = "/sys/class/kfd/kfd/topology", py::arg("drm_root") = "/sys/class/drm",
-      py::arg("pci_root") = "/sys/bus/pci/devices", py::arg("node_root") = "/sys/devices/system/node");
+      py::arg("pci_root") = "/sys/bus/pci/devices", py::arg("node_root") = "/sys/devices/system/node",
+      py::arg("ib_root") = "/sys/class/infiniband");
   py::class_<EventWatcher>(m, "EventWatcher")
       .def(py::init<const std::string&, const std::vector<std::string>&>(), py::arg("lib") = "libamd_smi.so",
            py::arg("kinds") = std::vector<std::string>{"GPU_PRE_RESET", "GPU_POST_RESET", "VMFAULT", "THERMAL_THROTTLE"})

@@ -75,6 +75,8 @@ def main(argv=None) -> int:
                     help="republish the topology when a measured pair moved by more than this fraction")
     ap.add_argument("--partition-aware", default="on", choices=["on", "off"],
                     help="GetPreferredAllocation on CPX/DPX/QPX nodes: group XCPs by physical GPU (on) or not (off)")
+    ap.add_argument("--nic-env", default="on", choices=["on", "off"],
+                    help="Allocate sets NCCL_IB_HCA / GTK_NICS to the RDMA NICs behind the allocated GPUs' PCIe switches")
     ap.add_argument("--gpu-events", default="auto", choices=["auto", "off"],
                     help="amdsmi GPU event notification (reset / VM fault / thermal throttle) on its own thread; "
                          "auto = on wherever amdsmi offers it")
@@ -108,7 +110,7 @@ def main(argv=None) -> int:
                        node_name=a.node_name, contract=contract, device_specs=specs, prestart_validate=a.prestart_validate,
                        health_interval=a.health_interval, reprobe_interval=a.reprobe_interval,
                        reprobe_tolerance=a.reprobe_tolerance, pod_resources_socket=a.pod_resources_socket,
-                       reconcile_interval=a.reconcile_interval, cdi_dir=a.cdi_dir,
+                       reconcile_interval=a.reconcile_interval, cdi_dir=a.cdi_dir, nic_env=a.nic_env == "on",
                        policy=PlacementPolicy(partition_aware=a.partition_aware == "on"))
     events = None
     if a.gpu_events == "auto" and a.discovery in ("auto", "amdsmi"):

@@ -131,7 +131,7 @@ class PluginConfig:
                  reprobe_interval: float = 0.0, reprobe_tolerance: float = 0.15, device_specs: str = "strict",
                  prestart_validate: bool = False, validate_timeout: float = 120.0,
                  pod_resources_socket: Optional[str] = POD_RESOURCES_SOCKET, reconcile_interval: float = 10.0,
-                 cdi_dir: str = "/var/run/cdi", cdi_kind: str = "amd.com/gpu"):
+                 cdi_dir: str = "/var/run/cdi", cdi_kind: str = "amd.com/gpu", nic_env: bool = True):
         self.resource_name = resource_name
         self.socket_dir = socket_dir
         self.socket_name = socket_name
@@ -158,6 +158,9 @@ class PluginConfig:
         self.device_specs = device_specs
         self.cdi_dir = cdi_dir
         self.cdi_kind = cdi_kind
+        # multi-node RCCL: NCCL_IB_HCA = the RDMA NICs behind the allocated GPUs' own PCIe switches
+        # (Topology.nearest_nics); a pod's RCCL env annotation still overrides it
+        self.nic_env = nic_env
         # flow step 8: before the container starts, an RCCL all-reduce over exactly
         # the allocated devices (kubelet PreStartContainer) validates the placement; the measured
         # bus bandwidth is recorded on the pod
@@ -530,6 +533,10 @@ class DevicePluginServer:
         cpuset = recommended_cpuset(self.topology, ids)  # Gaia B6: the devices' local core slices
         if cpuset:
             r.envs["GTK_CPUSET"] = cpuset
+        nics = self.topology.nearest_nics(ids) if self.cfg.nic_env else []
+        if nics:
+            r.envs["GTK_NICS"] = ",".join(nics)
+            r.envs["NCCL_IB_HCA"] = "=" + ",".join(nics)  # exact-name match
         for k, v in extra_env.items():
             r.envs[k] = v
         r.annotations["gputopology.amd.com/devices"] = format_group(ids)

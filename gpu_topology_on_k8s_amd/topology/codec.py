@@ -92,6 +92,9 @@ def encode_v2(topo) -> Dict[str, Any]:
         d["hbm_gbps"] = [None if not math.isfinite(v) else round(float(v), 1) for v in topo.hbm_gbps]
     if topo.numa_distance:
         d["numa_distance"] = {str(k): list(v) for k, v in topo.numa_distance.items()}
+    if topo.nics:
+        d["nics"] = topo.nics
+        d["gpu_nic"] = topo.gpu_nic
     # cost only when it is not derivable (fixtures with explicit costs)
     probe_copy = _decode_no_cost(d)
     if not np.array_equal(np.round(probe_copy.cost, 6), np.round(topo.cost, 6)):
@@ -139,4 +142,6 @@ def decode_v2(d: Dict[str, Any]):
         ref_class=None if rc is None else rc.astype(np.int32),
         hbm_gbps=None if hbm is None else np.array([np.nan if v is None else v for v in hbm], dtype=np.float64),
         numa_distance={int(k): [int(x) for x in v] for k, v in d["numa_distance"].items()} if d.get("numa_distance") else None,
+        nics=d.get("nics") or None,
+        gpu_nic=d.get("gpu_nic") or None,
     )

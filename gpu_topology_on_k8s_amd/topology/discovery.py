@@ -64,6 +64,9 @@ def from_native(d: Dict[str, object], node_name: str = "", ref_gbps: float = DEF
     nd = d.get("numa_distance") or {}
     if nd:
         t.numa_distance = {int(k): [int(x) for x in v] for k, v in nd.items()}
+    if d.get("nics"):
+        t.nics = [dict(x) for x in d["nics"]]
+        t.gpu_nic = [[int(c) for c in row] for row in d.get("gpu_nic") or []]
     mx = d.get("max_bw_mbps")
     if mx is not None:
         t.probe.setdefault("amdsmi_max_bw_mbps", mx)
@@ -88,6 +91,7 @@ def discover(
     fake_n: Optional[int] = None,
     pci_root: str = "/sys/bus/pci/devices",
     node_root: str = "/sys/devices/system/node",
+    ib_root: str = "/sys/class/infiniband",
 ) -> Topology:
     """Discover the node topology.  ``auto`` = amdsmi, then KFD sysfs; never silently fake.
     ``amdsmi_lib`` defaults to ``$GTK_AMDSMI_LIB`` or ``libamd_smi.so`` (the CPU tests point it at the
@@ -102,9 +106,9 @@ def discover(
         try:
             topo_mod = load("_topo")
             if b == "amdsmi":
-                d = topo_mod.discover_amdsmi(amdsmi_lib, pci_root, node_root)
+                d = topo_mod.discover_amdsmi(amdsmi_lib, pci_root, node_root, ib_root)
             elif b == "sysfs":
-                d = topo_mod.discover_sysfs(sysfs_root, drm_root, pci_root, node_root)
+                d = topo_mod.discover_sysfs(sysfs_root, drm_root, pci_root, node_root, ib_root)
             else:
                 raise DiscoveryError(f"unknown backend {b!r}")
             if not d["gpus"]:

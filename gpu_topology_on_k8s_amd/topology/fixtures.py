@@ -125,6 +125,7 @@ def write_fake_kfd_sysfs(
     compute_partition: Optional[str] = None,
     ras: Optional[Dict[int, Dict[str, object]]] = None,
     degraded_pcie: Sequence[int] = (),
+    nics: bool = False,
 ) -> Dict[str, str]:
     """Write a KFD topology tree + DRM tree for an MI355X node under ``root``.
 
@@ -134,6 +135,9 @@ def write_fake_kfd_sysfs(
     ``missing_links`` drops direct xGMI io_links between GPU indices (a degraded node).
     ``ras`` writes amdgpu RAS files for device index ``d``: ``{"umc": (ue, ce), "gfx": (ue, ce),
     "bad_pages": n}`` -> ``ras/<block>_err_count`` and ``ras/gpu_vram_bad_pages``.
+    ``nics`` lays the PCI devices out as a ``/sys/devices`` hierarchy (one root complex per socket, one
+    PCIe switch per package carrying the GPU and an RDMA NIC ``ionic_<package>``, ``pci/<bdf>`` as
+    symlinks into it) and adds an ``ib`` root like ``/sys/class/infiniband``.
     """
     kfd = os.path.join(root, "kfd", "topology")
     drm = os.path.join(root, "drm")
@@ -192,6 +196,24 @@ def write_fake_kfd_sysfs(
             )
         if xcp == 0:
             pdir = os.path.join(pci, f"0000:{bus:02x}:00.0")
+            if nics:
+                sw = _pcie_switch(root, sock, phys)
+                pdir = os.path.join(sw, f"0000:{bus + 1:02x}:00.0", f"0000:{bus:02x}:00.0")
+                os.makedirs(pdir, exist_ok=True)
+                os.makedirs(pci, exist_ok=True)
+                os.symlink(pdir, os.path.join(pci, f"0000:{bus:02x}:00.0"))
+                nbus = bus + 2
+                ndir = os.path.join(sw, f"0000:{bus + 1:02x}:01.0", f"0000:{nbus:02x}:00.0")
+                os.makedirs(os.path.join(ndir, "net", f"enp{nbus}s0"), exist_ok=True)
+                with open(os.path.join(ndir, "numa_node"), "w") as f:
+                    f.write(f"{sock}\n")
+                os.symlink(ndir, os.path.join(pci, f"0000:{nbus:02x}:00.0"))
+                ib = os.path.join(root, "infiniband", f"ionic_{phys}")
+                os.makedirs(os.path.join(ib, "ports", "1"), exist_ok=True)
+                os.symlink(ndir, os.path.join(ib, "device"))
+                for name, val in (("state", "4: ACTIVE"), ("rate", "400 Gb/sec (4X NDR)")):
+                    with open(os.path.join(ib, "ports", "1", name), "w") as f:
+                        f.write(val + "\n")
             os.makedirs(pdir, exist_ok=True)
             a, tot = sock * cores, sockets * cores
             for name, val in (("vendor", "0x1002"), ("local_cpulist", f"{a}-{a + cores - 1},{a + tot}-{a + tot + cores - 1}"),
@@ -214,7 +236,15 @@ def write_fake_kfd_sysfs(
                 ue, ce = val
                 with open(os.path.join(dev, "ras", f"{key}_err_count"), "w") as f:
                     f.write(f"ue: {ue}\nce: {ce}\n")
-    return {"kfd": kfd, "drm": drm, "pci": pci, "node": numa_root}
+    return {"kfd": kfd, "drm": drm, "pci": pci, "node": numa_root, "ib": os.path.join(root, "infiniband")}
+
+
+def _pcie_switch(root: str, sock: int, phys: int) -> str:
+    """Upstream port of package ``phys``'s PCIe switch: root complex of socket ``sock`` -> root port
+    -> switch upstream port (downstream ports 00.0 = GPU, 01.0 = NIC are its children)."""
+    rc = 0x80 * sock
+    up_bus = 0x05 + 0x10 * phys - 2
+    return os.path.join(root, "devices", f"pci0000:{rc:02x}", f"0000:{rc:02x}:{phys + 1:02x}.1", f"0000:{up_bus:02x}:00.0")
 
 
 def cost_matrix_stats(t: Topology) -> Dict[str, float]:

@@ -255,6 +255,10 @@ class Topology:
     ref_class: Optional[np.ndarray] = None  # optional RefLinkClass matrix (reference fixtures)
     hbm_gbps: Optional[np.ndarray] = None  # per-device self-copy bandwidth (k=1 probe)
     numa_distance: Optional[Dict[int, List[int]]] = None  # NUMA node -> SLIT distances (sysfs)
+    # RDMA NICs ({name, bdf, netdev, state, numa, rate_gbps}) and the PCIe class of every GPU-NIC pair
+    # ([gpu][nic]: 1 PIX, 2 PXB, 3 PHB, 4 NODE, 5 SYS, 0 unknown — the reference's taxonomy, design.md:31-47)
+    nics: Optional[List[Dict[str, object]]] = None
+    gpu_nic: Optional[List[List[int]]] = None
 
     def __post_init__(self) -> None:
         n = len(self.gpus)
@@ -388,7 +392,30 @@ class Topology:
             d["hbm_gbps"] = [None if not np.isfinite(v) else float(v) for v in self.hbm_gbps]
         if self.numa_distance:
             d["numa_distance"] = {str(k): list(v) for k, v in self.numa_distance.items()}
+        if self.nics:
+            d["nics"] = self.nics
+            d["gpu_nic"] = self.gpu_nic
         return d
+
+    def nearest_nics(self, ids: Sequence[int]) -> List[str]:
+        """Names of the RDMA NICs closest (PCIe class) to each device of ``ids``, active ports first,
+        in device order without repeats: what RCCL should use for inter-node traffic of those GPUs."""
+        if not self.nics or not self.gpu_nic:
+            return []
+        out: List[str] = []
+        for i in ids:
+            row = self.gpu_nic[int(i)] if int(i) < len(self.gpu_nic) else []
+            cands = [(c, "ACTIVE" not in str(self.nics[j].get("state", "")).upper(), j) for j, c in enumerate(row) if c > 0]
+            if not cands:
+                continue
+            best = min(cands)
+            for c, down, j in sorted(cands):
+                if (c, down) != best[:2]:
+                    break
+                name = str(self.nics[j]["name"])
+                if name not in out:
+                    out.append(name)
+        return out
 
     def to_json(self, **kw) -> str:
         return json.dumps(self.to_dict(), separators=(",", ":"), **kw)
@@ -427,6 +454,8 @@ class Topology:
             ref_class=None if d.get("ref_class") is None else np.array(d["ref_class"], dtype=np.int32),
             hbm_gbps=None if hbm is None else np.array([np.nan if v is None else v for v in hbm], dtype=np.float64),
             numa_distance=_numa_distance(d.get("numa_distance")),
+            nics=d.get("nics") or None,
+            gpu_nic=d.get("gpu_nic") or None,
         )
 
     @classmethod

@@ -295,3 +295,32 @@ def test_cdi_mode_allocates_by_cdi_name_and_writes_the_spec(sockdir):
         kubelet.stop()
     with pytest.raises(ValueError):
         PluginConfig(device_specs="nvidia")
+
+
+def test_allocate_sets_nccl_ib_hca_to_the_gpus_own_nics(sockdir, tmp_path):
+    """Multi-node RCCL: Allocate points NCCL_IB_HCA at the NIC behind each allocated GPU's PCIe switch."""
+    from gpu_topology_on_k8s_amd._native import available, load
+    from gpu_topology_on_k8s_amd.topology.discovery import from_native
+
+    if not available("_topo"):
+        pytest.skip("_topo not built")
+    p = fx.write_fake_kfd_sysfs(str(tmp_path), nics=True)
+    topo = from_native(load("_topo").discover_sysfs(p["kfd"], p["drm"], p["pci"], p["node"], p["ib"]))
+    api = FakeAPIServer()
+    api.create_node(make_node("n1"))
+    kubelet = FakeKubelet(sockdir, node_name="n1", api=api)
+    kubelet.start()
+    dev = placeholder_dev_tree(os.path.join(sockdir, "dev"), topo)
+    plugin = DevicePluginServer(topo, PluginConfig(resource_name=RES, socket_dir=sockdir, node_name="n1", dev_root=dev), api=api)
+    plugin.start()
+    try:
+        kubelet.wait_for(RES)
+        ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+        pod = api.create_pod(make_pod("mn", gpus=2))
+        d = ext.bind("default", "mn", pod["metadata"]["uid"], "n1")
+        c = kubelet.admit(api.get_pod("default", "mn"), RES).container_responses[0]
+        want = [f"ionic_{topo.gpus[i].physical}" for i in d.ids]
+        assert c.envs["GTK_NICS"] == ",".join(want) and c.envs["NCCL_IB_HCA"] == "=" + ",".join(want)
+    finally:
+        plugin.stop()
+        kubelet.stop()

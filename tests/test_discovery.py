@@ -5,7 +5,7 @@ import pytest
 from gpu_topology_on_k8s_amd._native import available, load
 from gpu_topology_on_k8s_amd.topology import fixtures as fx
 from gpu_topology_on_k8s_amd.topology.discovery import DiscoveryError, discover, fake_topology, from_native
-from gpu_topology_on_k8s_amd.topology.model import LinkType
+from gpu_topology_on_k8s_amd.topology.model import LinkType, Topology
 
 needs_topo = pytest.mark.skipif(not available("_topo"), reason="_topo not built")
 
@@ -183,3 +183,26 @@ def test_probe_pairs_per_package_on_cpx():
     assert none is None and len(full) == 64 * 64
     flat, r8 = _probe_pairs(fx.f7_mi355x(), list(range(8)), by_package=True)  # unpartitioned: every pair
     assert r8 is None and len(flat) == 64
+
+
+@needs_topo
+def test_sysfs_nics_pcie_classes_and_nearest(tmp_path):
+    """RDMA NICs from /sys/class/infiniband and the reference's PCIe taxonomy per GPU-NIC pair: the NIC on
+    the GPU's own switch is PIX, the same socket's others PHB, the other socket's SYS."""
+    p = fx.write_fake_kfd_sysfs(str(tmp_path), nics=True)
+    t = from_native(load("_topo").discover_sysfs(p["kfd"], p["drm"], p["pci"], p["node"], p["ib"]))
+    assert [n["name"] for n in t.nics] == [f"ionic_{i}" for i in range(8)]
+    assert t.nics[0]["rate_gbps"] == 400.0 and "ACTIVE" in t.nics[0]["state"] and t.nics[0]["netdev"]
+    assert t.gpu_nic[0][0] == 1 and t.gpu_nic[0][1] == 3 and t.gpu_nic[0][4] == 5
+    assert t.nearest_nics([1, 6]) == ["ionic_1", "ionic_6"]
+    # survives the node annotation codec
+    back = Topology.from_json(t.to_wire())
+    assert back.nearest_nics([3]) == ["ionic_3"] and back.gpu_nic == t.gpu_nic
+    # a down port loses to an active one of the same class
+    t.nics[2]["state"] = "1: DOWN"
+    t.gpu_nic[2][3] = 1
+    assert t.nearest_nics([2]) == ["ionic_3"]
+    # no NIC tree: nothing
+    q = fx.write_fake_kfd_sysfs(str(tmp_path / "plain"))
+    t2 = from_native(load("_topo").discover_sysfs(q["kfd"], q["drm"], q["pci"], q["node"], str(tmp_path / "none")))
+    assert not t2.nics and t2.nearest_nics([0]) == []

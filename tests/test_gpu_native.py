@@ -284,3 +284,14 @@ def test_gpu_event_watcher_on_real_node():
         print(json.dumps({"bdfs": w.bdfs, "events": ev}))
     finally:
         w.close()
+
+
+def test_nic_discovery_on_real_node():
+    """RDMA NICs of the box (if any) with their PCIe class to each GPU; the classes are well-formed."""
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
+
+    t = discover("auto")
+    print(json.dumps({"nics": t.nics, "gpu_nic": t.gpu_nic, "nearest": t.nearest_nics(range(t.n)) if t.nics else []}))
+    if t.nics:
+        assert len(t.gpu_nic) == t.n and all(len(row) == len(t.nics) for row in t.gpu_nic)
+        assert all(0 <= c <= 5 for row in t.gpu_nic for c in row)
