@@ -20,6 +20,7 @@
 #include <cstdint>
 #include <fstream>
 #include <map>
+#include <mutex>
 #include <sstream>
 #include <stdexcept>
 #include <string>
@@ -243,7 +244,13 @@ struct AmdSmi {
   }
 };
 
+// amdsmi_init / amdsmi_shut_down keep a process-wide reference count and handle table: the device
+// plugin's health pass (discovery) and its GPU-event thread must not interleave them.  Every amdsmi
+// session in this module runs under this lock (an event poll holds it for at most its timeout).
+std::mutex g_amdsmi_mu;
+
 Result discover_amdsmi_impl(const std::string& lib) {
+  std::lock_guard<std::mutex> guard(g_amdsmi_mu);
   AmdSmi s(lib);
   amdsmi_status_t st = s.init(AMDSMI_INIT_AMD_GPUS);
   if (st != AMDSMI_STATUS_SUCCESS) throw std::runtime_error("amdsmi_init failed: status " + std::to_string((int)st));
@@ -422,6 +429,45 @@ const char* event_name(amdsmi_evt_notification_type_t e) {
 class EventWatcher {
  public:
   EventWatcher(const std::string& lib, const std::vector<std::string>& kinds) : s_(lib) {
+    std::lock_guard<std::mutex> guard(g_amdsmi_mu);
+    try {
+      open_locked(kinds);
+    } catch (...) {
+      close_locked();  // a half-open session: stop what was subscribed, drop the amdsmi reference
+      throw;
+    }
+  }
+
+  ~EventWatcher() { close(); }
+
+  // Events collected for up to timeout_ms (returns early when some arrive): (bdf, kind, message).
+  std::vector<std::tuple<std::string, std::string, std::string>> poll(int timeout_ms, uint32_t max_events) {
+    std::vector<std::tuple<std::string, std::string, std::string>> out;
+    std::lock_guard<std::mutex> guard(g_amdsmi_mu);
+    if (handles_.empty()) return out;
+    std::vector<amdsmi_evt_notification_data_t> buf(std::max<uint32_t>(1, max_events));
+    uint32_t n = (uint32_t)buf.size();
+    amdsmi_status_t st = s_.evt_get(timeout_ms, &n, buf.data());
+    if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_NO_DATA) return out;
+    for (uint32_t i = 0; i < n && i < buf.size(); ++i) {
+      std::string bdf;
+      for (size_t j = 0; j < handles_.size(); ++j)
+        if (handles_[j] == buf[i].processor_handle) bdf = bdfs_[j];
+      buf[i].message[AMDSMI_MAX_STRING_LENGTH - 1] = 0;
+      out.emplace_back(bdf, event_name(buf[i].event), std::string(buf[i].message));
+    }
+    return out;
+  }
+
+  void close() {
+    std::lock_guard<std::mutex> guard(g_amdsmi_mu);
+    close_locked();
+  }
+  const std::vector<std::string>& bdfs() const { return bdfs_; }
+
+
+ private:
+  void open_locked(const std::vector<std::string>& kinds) {
     if (!s_.evt_init || !s_.evt_mask || !s_.evt_get || !s_.evt_stop)
       throw std::runtime_error("this amdsmi has no GPU event notification API");
     uint64_t mask = 0;
@@ -457,35 +503,14 @@ class EventWatcher {
     }
     if (handles_.empty()) throw std::runtime_error("no GPU accepted event notification");
   }
-  ~EventWatcher() { close(); }
-
-  // Events collected for up to timeout_ms (returns early when some arrive): (bdf, kind, message).
-  std::vector<std::tuple<std::string, std::string, std::string>> poll(int timeout_ms, uint32_t max_events) {
-    std::vector<std::tuple<std::string, std::string, std::string>> out;
-    if (handles_.empty()) return out;
-    std::vector<amdsmi_evt_notification_data_t> buf(std::max<uint32_t>(1, max_events));
-    uint32_t n = (uint32_t)buf.size();
-    amdsmi_status_t st = s_.evt_get(timeout_ms, &n, buf.data());
-    if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_NO_DATA) return out;
-    for (uint32_t i = 0; i < n && i < buf.size(); ++i) {
-      std::string bdf;
-      for (size_t j = 0; j < handles_.size(); ++j)
-        if (handles_[j] == buf[i].processor_handle) bdf = bdfs_[j];
-      buf[i].message[AMDSMI_MAX_STRING_LENGTH - 1] = 0;
-      out.emplace_back(bdf, event_name(buf[i].event), std::string(buf[i].message));
-    }
-    return out;
-  }
-
-  void close() {
+  void close_locked() {
     for (auto p : handles_) s_.evt_stop(p);
     handles_.clear();
     if (inited_) s_.shut_down();
     inited_ = false;
   }
-  const std::vector<std::string>& bdfs() const { return bdfs_; }
 
- private:
+
   AmdSmi s_;
   bool inited_ = false;
   std::vector<amdsmi_processor_handle> handles_;
