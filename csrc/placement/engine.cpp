@@ -38,6 +38,30 @@ Engine::Engine(const Problem& p, const Policy& pol) : p_(p), pol_(pol) {
     std::sort(lv.sorted_free.begin(), lv.sorted_free.end(), std::greater<int>());
     lv_.push_back(std::move(lv));
   }
+  if (!p_.nic.empty()) {
+    if (p_.nic.size() != n) throw std::invalid_argument("nic must be empty or have n entries");
+    std::vector<int> seen;
+    for (size_t i = 0; i < n; ++i)
+      if (p_.free[i] && p_.nic[i] >= 0 && std::find(seen.begin(), seen.end(), p_.nic[i]) == seen.end()) seen.push_back(p_.nic[i]);
+    nic_domains_free_ = (int)seen.size();
+  }
+}
+
+double Engine::nic_deficit(const int* ids, int k) const {
+  if (p_.nic.empty() || pol_.w_nic == 0.0) return 0.0;
+  int touched = 0;
+  for (int a = 0; a < k; ++a) {
+    const int d = p_.nic[ids[a]];
+    if (d < 0) continue;
+    bool first = true;
+    for (int b = 0; b < a; ++b)
+      if (p_.nic[ids[b]] == d) {
+        first = false;
+        break;
+      }
+    touched += first;
+  }
+  return (double)std::max(0, std::min(k, nic_domains_free_) - touched);
 }
 
 int Engine::min_groups(const Level& lv, int k) const {
@@ -92,8 +116,9 @@ double Engine::evaluate(const std::vector<int>& ids, Terms* terms) const {
   double acc = 0;
   for (int i : ids) acc += p_.access[i];
   t.access = k ? acc / k : 0.0;
+  t.nicdef = k ? nic_deficit(ids.data(), k) : 0.0;
   if (terms) *terms = t;
-  return t.comm + pol_.w_bottleneck * (t.bott - t.comm) + pol_.w_span * t.span + pol_.w_frag * t.frag + pol_.w_fit * t.fit + pol_.w_access * t.access;
+  return t.comm + pol_.w_nic * t.nicdef + pol_.w_bottleneck * (t.bott - t.comm) + pol_.w_span * t.span + pol_.w_frag * t.frag + pol_.w_fit * t.fit + pol_.w_access * t.access;
 }
 
 void Engine::greedy(int k, const std::vector<int>& F, std::vector<int>* best, double* best_j, bool maximise,
@@ -205,6 +230,7 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
       for (const auto& lv : lv_)
         if (lv.gid[i] != lv.gid[j]) return false;
       if (std::fabs(p_.access[i] - p_.access[j]) > 1e-12 * std::max(1.0, std::fabs(p_.access[i]))) return false;
+      if (!p_.nic.empty() && p_.nic[i] != p_.nic[j]) return false;
       const double* ri = &p_.cost[(size_t)i * n];
       const double* rj = &p_.cost[(size_t)j * n];
       for (int c = 0; c < m; ++c) {
@@ -263,8 +289,20 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
         fit += (double)after / lv.size[g];
       }
     }
+    double nicdef = 0.0;
+    if (!p_.nic.empty()) {
+      int small[64];
+      std::vector<int> big;
+      int* ids = small;
+      if (k > 64) {
+        big.resize(k);
+        ids = big.data();
+      }
+      for (int i = 0; i < k; ++i) ids[i] = F[chosen[i]];
+      nicdef = nic_deficit(ids, k);
+    }
     return comm + wb * (bott - comm) + pol_.w_span * span + pol_.w_frag * frag + pol_.w_fit * fit +
-           pol_.w_access * (accsum / k);
+           pol_.w_access * (accsum / k) + pol_.w_nic * nicdef;
   };
 
   // Large search spaces: seed the incumbent with greedy + 1-swap so pruning bites from the start.

@@ -16,6 +16,8 @@
 //   frag = sum_levels #pristine groups left partially used
 //   fit  = sum_levels sum_touched free_after/size
 //   acc  = mean access cost of S
+//   + w_nic * nicdef (only with Problem::nic): NIC domains (device -> its nearest RDMA NIC) a
+//     multi-node pod could use but S leaves out, min(k, domains with a free device) - domains touched
 // Enumeration is lexicographic over free device ids and a candidate replaces the incumbent only if
 // it is better by more than kEps, so the result equals itertools.combinations + first-minimum.
 #pragma once
@@ -30,6 +32,7 @@ constexpr double kEps = 1e-9;
 
 struct Policy {
   double w_span = 0.5, w_frag = 0.25, w_fit = 0.05, w_access = 0.1, w_bottleneck = 0.4;  // w_bottleneck in [0, 1]
+  double w_nic = 1.0;
 };
 
 struct Problem {
@@ -38,10 +41,11 @@ struct Problem {
   std::vector<uint8_t> free;              // n
   std::vector<std::vector<int>> levels;   // per level: group id per device (any ints)
   std::vector<double> access;             // n
+  std::vector<int> nic;                   // empty, or n: NIC domain per device (-1 = none)
 };
 
 struct Terms {
-  double comm = 0, bott = 0, span = 0, frag = 0, fit = 0, access = 0;
+  double comm = 0, bott = 0, span = 0, frag = 0, fit = 0, access = 0, nicdef = 0;
 };
 
 struct Result {
@@ -80,6 +84,7 @@ class Engine {
     std::vector<int> sorted_free;  // `free`, descending (min_groups)
   };
   int min_groups(const Level& lv, int k) const;
+  double nic_deficit(const int* ids, int k) const;  // ids: device ids
   // `cls` (optional, class id per device id, -1 = not free): interchangeable devices share a class, and
   // only the first not-yet-chosen member of each class is tried (identical objective otherwise).
   void greedy(int k, const std::vector<int>& free_ids, std::vector<int>* best, double* best_j, bool maximise,
@@ -88,6 +93,7 @@ class Engine {
   Problem p_;
   Policy pol_;
   std::vector<Level> lv_;
+  int nic_domains_free_ = 0;  // NIC domains with at least one free device
 };
 
 }  // namespace gtk

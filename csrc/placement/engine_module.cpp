@@ -52,14 +52,16 @@ py::dict to_dict(const Result& r, double us) {
   t["frag"] = r.terms.frag;
   t["fit"] = r.terms.fit;
   t["access"] = r.terms.access;
+  t["nic_deficit"] = r.terms.nicdef;
   d["terms"] = t;
   return d;
 }
 
-Policy make_policy(double w_span, double w_frag, double w_fit, double w_access, double w_bottleneck) {
+Policy make_policy(double w_span, double w_frag, double w_fit, double w_access, double w_bottleneck, double w_nic = 1.0) {
   if (!(w_bottleneck >= 0.0 && w_bottleneck <= 1.0)) throw std::invalid_argument("w_bottleneck must be in [0, 1]");
   Policy pol;
   pol.w_bottleneck = w_bottleneck;
+  pol.w_nic = w_nic;
   pol.w_span = w_span;
   pol.w_frag = w_frag;
   pol.w_fit = w_fit;
@@ -76,14 +78,16 @@ PYBIND11_MODULE(_placement, m) {
       [](py::array_t<double, py::array::c_style | py::array::forcecast> cost,
          py::array_t<bool, py::array::c_style | py::array::forcecast> free_mask, const std::vector<std::vector<int>>& levels,
          py::array_t<double, py::array::c_style | py::array::forcecast> access, int k, double w_span, double w_frag,
-         double w_fit, double w_access, uint64_t node_limit, bool collect_ties, double w_bottleneck) {
+         double w_fit, double w_access, uint64_t node_limit, bool collect_ties, double w_bottleneck,
+         const std::vector<int>& nic, double w_nic) {
         Problem p = make_problem(cost, free_mask, levels, access);
+        p.nic = nic;
         Result r;
         double us = 0;
         {
           py::gil_scoped_release nogil;
           auto t0 = std::chrono::steady_clock::now();
-          Engine e(p, make_policy(w_span, w_frag, w_fit, w_access, w_bottleneck));
+          Engine e(p, make_policy(w_span, w_frag, w_fit, w_access, w_bottleneck, w_nic));
           r = e.select(k, node_limit, collect_ties);
           us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
         }
@@ -94,20 +98,22 @@ PYBIND11_MODULE(_placement, m) {
       py::arg("cost"), py::arg("free"), py::arg("levels"), py::arg("access"), py::arg("k"), py::arg("w_span") = 0.5,
       py::arg("w_frag") = 0.25, py::arg("w_fit") = 0.05, py::arg("w_access") = 0.1,
       py::arg("node_limit") = (uint64_t)2000000, py::arg("collect_ties") = false,
-      py::arg("w_bottleneck") = 0.4);
+      py::arg("w_bottleneck") = 0.4, py::arg("nic") = std::vector<int>{}, py::arg("w_nic") = 1.0);
   m.def(
       "worst",
       [](py::array_t<double, py::array::c_style | py::array::forcecast> cost,
          py::array_t<bool, py::array::c_style | py::array::forcecast> free_mask, const std::vector<std::vector<int>>& levels,
          py::array_t<double, py::array::c_style | py::array::forcecast> access, int k, double w_span, double w_frag,
-         double w_fit, double w_access, uint64_t node_limit, double w_bottleneck) {
+         double w_fit, double w_access, uint64_t node_limit, double w_bottleneck,
+         const std::vector<int>& nic, double w_nic) {
         Problem p = make_problem(cost, free_mask, levels, access);
+        p.nic = nic;
         Result r;
         double us = 0;
         {
           py::gil_scoped_release nogil;
           auto t0 = std::chrono::steady_clock::now();
-          Engine e(p, make_policy(w_span, w_frag, w_fit, w_access, w_bottleneck));
+          Engine e(p, make_policy(w_span, w_frag, w_fit, w_access, w_bottleneck, w_nic));
           r = e.worst(k, node_limit);
           us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
         }
@@ -115,15 +121,18 @@ PYBIND11_MODULE(_placement, m) {
       },
       py::arg("cost"), py::arg("free"), py::arg("levels"), py::arg("access"), py::arg("k"), py::arg("w_span") = 0.5,
       py::arg("w_frag") = 0.25, py::arg("w_fit") = 0.05, py::arg("w_access") = 0.1,
-      py::arg("node_limit") = (uint64_t)2000000, py::arg("w_bottleneck") = 0.4);
+      py::arg("node_limit") = (uint64_t)2000000, py::arg("w_bottleneck") = 0.4, py::arg("nic") = std::vector<int>{},
+      py::arg("w_nic") = 1.0);
   m.def(
       "evaluate",
       [](py::array_t<double, py::array::c_style | py::array::forcecast> cost,
          py::array_t<bool, py::array::c_style | py::array::forcecast> free_mask, const std::vector<std::vector<int>>& levels,
          py::array_t<double, py::array::c_style | py::array::forcecast> access, const std::vector<int>& ids,
-         double w_span, double w_frag, double w_fit, double w_access, double w_bottleneck) {
+         double w_span, double w_frag, double w_fit, double w_access, double w_bottleneck,
+         const std::vector<int>& nic, double w_nic) {
         Problem p = make_problem(cost, free_mask, levels, access);
-        Engine e(p, make_policy(w_span, w_frag, w_fit, w_access, w_bottleneck));
+        p.nic = nic;
+        Engine e(p, make_policy(w_span, w_frag, w_fit, w_access, w_bottleneck, w_nic));
         Result r;
         r.ids = ids;
         r.objective = e.evaluate(ids, &r.terms);
@@ -131,6 +140,7 @@ PYBIND11_MODULE(_placement, m) {
         return to_dict(r, 0.0);
       },
       py::arg("cost"), py::arg("free"), py::arg("levels"), py::arg("access"), py::arg("ids"), py::arg("w_span") = 0.5,
-      py::arg("w_frag") = 0.25, py::arg("w_fit") = 0.05, py::arg("w_access") = 0.1, py::arg("w_bottleneck") = 0.4);
+      py::arg("w_frag") = 0.25, py::arg("w_fit") = 0.05, py::arg("w_access") = 0.1, py::arg("w_bottleneck") = 0.4,
+      py::arg("nic") = std::vector<int>{}, py::arg("w_nic") = 1.0);
   m.attr("EPS") = kEps;
 }

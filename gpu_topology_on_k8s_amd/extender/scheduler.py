@@ -171,19 +171,19 @@ class TopologyExtender:
         return self.cfg.decision_cache > 0 and self.cfg.policy.tie_break != "random"
 
     def _choose_cached(self, t: Topology, used: Sequence[int], k: int, access=None,
-                       fraction: Optional[float] = None) -> Tuple[Tuple[int, ...], float, float]:
+                       fraction: Optional[float] = None, multi: bool = False) -> Tuple[Tuple[int, ...], float, float]:
         if not self._cacheable():
-            return self._choose(t, used, k, access, fraction)
+            return self._choose(t, used, k, access, fraction, multi)
         # the Topology object is replaced whenever the node annotation changes (new resourceVersion)
         acc_key = None if access is None else tuple(round(float(x), 9) for x in access)
-        key = (id(t), tuple(used), tuple(g.healthy for g in t.gpus), k, self.cfg.policy_name, acc_key, fraction)
+        key = (id(t), tuple(used), tuple(g.healthy for g in t.gpus), k, self.cfg.policy_name, acc_key, fraction, multi)
         with self._cache_lock:
             hit = self._cache.get(key)
             if hit is not None and hit[3] is t:
                 self._cache.move_to_end(key)
                 self.metrics.cache(True)
                 return hit[:3]
-        res = self._choose(t, used, k, access, fraction)  # NoFeasiblePlacement propagates uncached
+        res = self._choose(t, used, k, access, fraction, multi)  # NoFeasiblePlacement propagates uncached
         with self._cache_lock:
             self._cache[key] = res + (t,)  # keeps t alive, so id(t) cannot be reused while cached
             while len(self._cache) > self.cfg.decision_cache:
@@ -192,7 +192,7 @@ class TopologyExtender:
         return res
 
     def _choose(self, t: Topology, used: Sequence[int], k: int, access=None,
-                fraction: Optional[float] = None) -> Tuple[Tuple[int, ...], float, float]:
+                fraction: Optional[float] = None, multi: bool = False) -> Tuple[Tuple[int, ...], float, float]:
         """(ids, absolute score 0..10, objective) under the configured policy; raises NoFeasiblePlacement."""
         from ..placement.core import Problem, evaluate, score_from_objective
 
@@ -201,7 +201,7 @@ class TopologyExtender:
             ids = place_fraction(t, k, used, access)
             name = "fragment"
         elif name == "exact":
-            pl = select(t, k, used=used, policy=self.cfg.policy, rng=self._rng, access=access)
+            pl = select(t, k, used=used, policy=self.cfg.policy, rng=self._rng, access=access, nic_aware=multi)
             return pl.ids, pl.score, pl.objective
         elif name == "gaia":
             tree = tree_from_topology(t, used=[u for u in used])
@@ -216,8 +216,8 @@ class TopologyExtender:
             raise ValueError(f"unknown policy {name!r}")
         if len(ids) != k:
             raise NoFeasiblePlacement(f"{name}: no {k}-device placement")
-        j, _ = evaluate(Problem.from_topology(t, used, access, partition_aware=self.cfg.policy.partition_aware), ids,
-                        self.cfg.policy)
+        j, _ = evaluate(Problem.from_topology(t, used, access, partition_aware=self.cfg.policy.partition_aware, nic_aware=multi),
+                        ids, self.cfg.policy)
         return tuple(sorted(int(i) for i in ids)), score_from_objective(j), j
 
     def _pod_shape(self, pod: Dict[str, Any], k: int) -> Tuple[Optional[tuple], str]:
@@ -229,7 +229,19 @@ class TopologyExtender:
             return None, str(e)
         numa = self.numa_preference(pod)
         want = obj_annotations(pod).get(self.cfg.contract.pod_model_key) or obj_labels(pod).get(self.cfg.contract.pod_model_key)
-        return (k, fraction, tuple(numa) if numa else None, want), ""
+        return (k, fraction, tuple(numa) if numa else None, want, self.multi_node(pod)), ""
+
+    def multi_node(self, pod: Dict[str, Any]) -> bool:
+        """A member of a multi-node job: ``<prefix>/multi-node: "true"``, or it requests an RDMA
+        resource (any resource name containing ``rdma``)."""
+        if str(obj_annotations(pod).get(self.cfg.contract.multi_node_key, "")).strip().lower() in ("1", "true", "yes"):
+            return True
+        for c in ((pod.get("spec") or {}).get("containers") or []):
+            res = c.get("resources") or {}
+            for part in ("limits", "requests"):
+                if any("rdma" in str(name).lower() for name in (res.get(part) or {})):
+                    return True
+        return False
 
     def _eval_state(self, pod: Dict[str, Any], name: str, st: NodeState, k: int,
                     shape: Optional[tuple] = None) -> Tuple[Optional[Decision], str]:
@@ -240,7 +252,7 @@ class TopologyExtender:
             shape, why = self._pod_shape(pod, k)
             if shape is None:
                 return None, why
-        _, fraction, numa, want = shape
+        _, fraction, numa, want, multi = shape
         with st.lock:
             now = self.clock()
             if self._cacheable():
@@ -248,13 +260,13 @@ class TopologyExtender:
                 if hit is not None and hit[0] <= now <= hit[1]:
                     self.metrics.cache(True)
                     return hit[2], hit[3]
-            d, why = self._eval_state_uncached(st, name, k, fraction, numa, want, now)
+            d, why = self._eval_state_uncached(st, name, k, fraction, numa, want, now, multi)
             if self._cacheable():
                 st.memo[shape] = (now, st.valid_until(now, self.cfg.assume_ttl), d, why)
             return d, why
 
     def _eval_state_uncached(self, st: NodeState, name: str, k: int, fraction: Optional[float], numa, want,
-                             now: float) -> Tuple[Optional[Decision], str]:
+                             now: float, multi: bool = False) -> Tuple[Optional[Decision], str]:
         t = st.topology
         if t is None:
             return None, "node has no GPU topology annotation"
@@ -279,7 +291,7 @@ class TopologyExtender:
         access = access_costs(t, numa) if self.cfg.cpu_affinity else None
         t0 = time.perf_counter()
         try:
-            ids, score, obj = self._choose_cached(t, used, k, access, fraction)
+            ids, score, obj = self._choose_cached(t, used, k, access, fraction, multi)
         except NoFeasiblePlacement as e:
             return None, str(e)
         us = (time.perf_counter() - t0) * 1e6
@@ -442,7 +454,7 @@ class TopologyExtender:
                 freed_unknown = sum(st.unknown_pods.get(st.unknown_uids.get(u, ""), 0) for u in keep)
                 used = st.used(now, self.cfg.assume_ttl)
                 healthy = {g.index for g in t.gpus if g.healthy}
-                _, fraction, numa, _ = shape
+                _, fraction, numa, _, multi = shape
                 access = access_costs(t, numa) if self.cfg.cpu_affinity else None
                 best = None
                 tried = 0
@@ -457,7 +469,7 @@ class TopologyExtender:
                         if free < k:
                             continue
                         try:
-                            _, _, obj = self._choose_cached(t, still, k, access, fraction)
+                            _, _, obj = self._choose_cached(t, still, k, access, fraction, multi)
                         except NoFeasiblePlacement:
                             continue
                         if best is None or obj < best[0] - 1e-12:

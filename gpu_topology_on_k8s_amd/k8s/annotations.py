@@ -81,6 +81,12 @@ class Contract:
         return f"{self.prefix}/numa-preference"
 
     @property
+    def multi_node_key(self) -> str:
+        """Pod annotation ``"true"``: the pod is one member of a multi-node job, so its devices should
+        cover as many RDMA NIC domains as possible (placement ``w_nic`` term)."""
+        return f"{self.prefix}/multi-node"
+
+    @property
     def fraction_key(self) -> str:
         """Pod annotation: a fraction 0<m<1 of ONE physical GPU, served as ceil(m * partitions) XCPs
         of one package on a CPX/DPX/QPX node (Gaia Fragment, paper Alg. 2)."""

@@ -26,6 +26,10 @@ The objective for a candidate set S (|S| = k) is::
     frag  = sum over levels of #pristine groups left partially used
     fit   = sum over levels and touched groups of free_after/size  (best-fit packing)
     acc   = mean per-device access cost (CPU/NUMA affinity hint, design.md:144-145, Gaia B6)
+    + w_nic * nicdef, multi-node pods only (``Problem.nic``): NIC domains (device -> its nearest RDMA
+      NIC) the set leaves out, min(k, domains with a free device) - domains touched.  A 2-GPU pod of
+      a multi-node job on a node with one NIC per socket gets twice the network bandwidth across the
+      sockets; on a full xGMI mesh that costs its collectives nothing
 
 The C++ engine (``csrc/placement/engine.cpp``) implements the same objective with branch-and-bound;
 ``tests/test_placement_native.py`` checks both agree.
@@ -59,6 +63,7 @@ class PlacementPolicy:
     w_fit: float = 0.05
     w_access: float = 0.1
     w_bottleneck: float = 0.4  # in [0, 1]: blend of mean and worst link (bench/cluster_trace.py)
+    w_nic: float = 1.0  # per NIC domain a multi-node pod leaves unused (only with Problem.nic)
     tie_break: str = "first"  # "first" (deterministic, lowest ids) | "random"
     exact_limit: int = 200_000  # Python path: max subsets enumerated exactly; above -> greedy + local search
     node_limit: int = 2_000_000  # native path: branch-and-bound node budget; above -> greedy + local search
@@ -73,7 +78,7 @@ class PlacementPolicy:
 
     def to_dict(self) -> Dict[str, object]:
         return dict(
-            w_span=self.w_span, w_frag=self.w_frag, w_fit=self.w_fit, w_access=self.w_access, w_bottleneck=self.w_bottleneck,
+            w_span=self.w_span, w_frag=self.w_frag, w_fit=self.w_fit, w_access=self.w_access, w_bottleneck=self.w_bottleneck, w_nic=self.w_nic,
             w_node_fit=self.w_node_fit,
             tie_break=self.tie_break, exact_limit=self.exact_limit, node_limit=self.node_limit,
             partition_aware=self.partition_aware,
@@ -107,10 +112,11 @@ class Problem:
     free: np.ndarray  # bool[n]
     levels: List[np.ndarray]  # group id per device, innermost level first
     access: np.ndarray  # float[n]
+    nic: Optional[np.ndarray] = None  # int[n]: NIC domain per device (-1 none); None = not a multi-node pod
 
     @classmethod
     def from_topology(cls, topo: Topology, used: Sequence[int] = (), access: Optional[Sequence[float]] = None,
-                      partition_aware: bool = True) -> "Problem":
+                      partition_aware: bool = True, nic_aware: bool = False) -> "Problem":
         n = topo.n
         free = topo.healthy_mask().copy()
         for u in used:
@@ -130,11 +136,25 @@ class Problem:
                 cost[same] = float(np.median(cost[cross]))
         levels.append(topo.numa)
         acc = np.zeros(n) if access is None else np.asarray(access, dtype=np.float64)
-        return cls(cost=cost, free=free, levels=levels, access=acc)
+        return cls(cost=cost, free=free, levels=levels, access=acc, nic=nic_domains(topo) if nic_aware else None)
 
     @property
     def n(self) -> int:
         return len(self.free)
+
+
+def nic_domains(topo: Topology) -> Optional[np.ndarray]:
+    """NIC domain per device: the index of its nearest RDMA NIC (``Topology.nearest_nics``), -1 when
+    it has none; None when the node published no NICs."""
+    if not topo.nics or not topo.gpu_nic:
+        return None
+    names = [str(x["name"]) for x in topo.nics]
+    out = np.full(topo.n, -1, dtype=np.int64)
+    for i in range(topo.n):
+        near = topo.nearest_nics([i])
+        if near:
+            out[i] = names.index(near[0])
+    return out
 
 
 def node_packing_term(free_before: int, k: int, size: int, policy: PlacementPolicy = PlacementPolicy()) -> float:
@@ -195,9 +215,14 @@ def evaluate(p: Problem, ids: Sequence[int], policy: PlacementPolicy = Placement
                 frag += 1
             fit += after / size[g]
     acc = float(np.mean(p.access[ids])) if k else 0.0
+    nicdef = 0.0
+    if p.nic is not None and k:
+        domains = {int(d) for d, f in zip(p.nic, p.free) if f and d >= 0}
+        touched = {int(p.nic[i]) for i in ids if p.nic[i] >= 0}
+        nicdef = float(max(0, min(k, len(domains)) - len(touched)))
     j = (comm + policy.w_bottleneck * (bott - comm) + policy.w_span * span + policy.w_frag * frag
-         + policy.w_fit * fit + policy.w_access * acc)
-    return j, {"comm": comm, "bottleneck": bott, "span": span, "frag": frag, "fit": fit, "access": acc}
+         + policy.w_fit * fit + policy.w_access * acc + policy.w_nic * nicdef)
+    return j, {"comm": comm, "bottleneck": bott, "nic_deficit": nicdef, "span": span, "frag": frag, "fit": fit, "access": acc}
 
 
 def _greedy_local(p: Problem, k: int, policy: PlacementPolicy, stats) -> Tuple[List[int], float]:
@@ -252,14 +277,16 @@ def _select_native(mod, p: Problem, k: int, policy: PlacementPolicy, rng: Option
             [lv.astype(np.int64).tolist() for lv in p.levels], np.ascontiguousarray(p.access, dtype=np.float64))
     w = (policy.w_span, policy.w_frag, policy.w_fit, policy.w_access)
     ties = policy.tie_break == "random"
-    r = mod.select(*args, int(k), *w, int(policy.node_limit), ties, w_bottleneck=policy.w_bottleneck)
+    nic = [] if p.nic is None else [int(x) for x in p.nic]
+    r = mod.select(*args, int(k), *w, int(policy.node_limit), ties, w_bottleneck=policy.w_bottleneck, nic=nic,
+                   w_nic=policy.w_nic)
     if not r["feasible"]:
         raise NoFeasiblePlacement(f"need {k} free devices")
     if ties and len(r["ties"]) > 1:
         # same draw as the Python enumeration: lexicographic tie list, one rng.choice
         pick = list((rng or random).choice(r["ties"]))
         if pick != list(r["ids"]):
-            e = mod.evaluate(*args, pick, *w, w_bottleneck=policy.w_bottleneck)
+            e = mod.evaluate(*args, pick, *w, w_bottleneck=policy.w_bottleneck, nic=nic, w_nic=policy.w_nic)
             r = dict(r, ids=pick, objective=e["objective"], terms=e["terms"])
     terms = dict(r["terms"])
     terms["search_nodes"] = float(r["nodes"])
@@ -276,16 +303,19 @@ def select(
     access: Optional[Sequence[float]] = None,
     rng: Optional[random.Random] = None,
     engine: str = "auto",
+    nic_aware: bool = False,
 ) -> Placement:
     """Choose ``k`` free devices minimising :func:`evaluate`'s objective.
 
+    ``nic_aware``: the pod is part of a multi-node job, so the set should also cover as many RDMA NIC
+    domains as it can (the ``w_nic`` term; no effect on nodes without published NICs).
     ``engine``: ``native`` = C++ branch-and-bound (``csrc/placement/engine.cpp``), ``python`` = the
     enumeration below, ``auto`` = native when built.  A random tie-break asks the engine for the
     full lexicographic tie list (ties are pruned only when strictly worse) and draws from it exactly
     as the enumeration does, so both engines return the same set for the same rng state.
     """
     p = (topo_or_problem if isinstance(topo_or_problem, Problem)
-         else Problem.from_topology(topo_or_problem, used, access, partition_aware=policy.partition_aware))
+         else Problem.from_topology(topo_or_problem, used, access, partition_aware=policy.partition_aware, nic_aware=nic_aware))
     if k <= 0:
         raise ValueError("k must be >= 1")
     free_ids = [i for i in range(p.n) if p.free[i]]

@@ -416,3 +416,22 @@ def test_http_preempt_wire_format():
     assert status == 200
     pods = body["NodeNameToMetaVictims"]["n1"]["Pods"]
     assert len(pods) == 1 and body["NodeNameToMetaVictims"]["n1"]["NumPDBViolations"] == 0
+
+
+def test_multi_node_pod_binds_across_nic_domains():
+    def topo():
+        t = fx.f7_mi355x()
+        t.nics = [{"name": "mlx5_0", "state": "4: ACTIVE"}, {"name": "mlx5_1", "state": "4: ACTIVE"}]
+        t.gpu_nic = [[1, 5] if i < 4 else [5, 1] for i in range(8)]
+        return t
+
+    api, ext, _ = _cluster(topo_fn=topo)
+    _submit(api, "mn", 2, annotations={Contract().multi_node_key: "true"})
+    d = _bind(api, ext, "mn")
+    assert {i // 4 for i in d.ids} == {0, 1}
+    _submit(api, "local", 2)
+    d2 = _bind(api, ext, "local")
+    assert len({i // 4 for i in d2.ids}) == 1
+    rdma = api.create_pod(make_pod("rdma", gpus=2))
+    rdma["spec"]["containers"][0]["resources"]["limits"]["rdma/hca"] = "1"
+    assert ext.multi_node(rdma) and not ext.multi_node(api.get_pod("default", "local"))

@@ -298,3 +298,28 @@ def test_bottleneck_term_avoids_a_slow_link_a_ring_cannot_skip(engine):
     pl = select(t, 4, used=used, policy=PlacementPolicy(), engine=engine)
     assert set(pl.ids) == {1, 2, 3, 4}
     assert pl.terms["bottleneck"] == pytest.approx(pl.comm)
+
+
+def _two_nic_node():
+    """F7 with one RDMA NIC per socket (like the MI355X gpurun box): GPUs 0-3 -> nic0, 4-7 -> nic1."""
+    t = fx.f7_mi355x()
+    t.nics = [{"name": "mlx5_0", "state": "4: ACTIVE"}, {"name": "mlx5_1", "state": "4: ACTIVE"}]
+    t.gpu_nic = [[1, 5] if i < 4 else [5, 1] for i in range(8)]
+    return t
+
+
+@pytest.mark.parametrize("engine", ["python", "native"])
+def test_multi_node_pod_spreads_over_nic_domains(engine):
+    """A 2-GPU member of a multi-node job gets one GPU per NIC domain (twice the network bandwidth);
+    a single-node pod stays in one NUMA half.  On a node without NICs the flag changes nothing."""
+    if engine == "native" and not available("_placement"):
+        pytest.skip("_placement not built")
+    t = _two_nic_node()
+    local = select(t, 2, engine=engine)
+    assert {i // 4 for i in local.ids} == {0} or {i // 4 for i in local.ids} == {1}
+    multi = select(t, 2, engine=engine, nic_aware=True)
+    assert {i // 4 for i in multi.ids} == {0, 1} and multi.terms["nic_deficit"] == 0
+    # only one domain left with free devices: nothing to spread over, no penalty
+    half = select(t, 2, used=[4, 5, 6, 7], engine=engine, nic_aware=True)
+    assert set(half.ids) <= {0, 1, 2, 3} and half.terms["nic_deficit"] == 0
+    assert select(fx.f7_mi355x(), 2, engine=engine, nic_aware=True).ids == select(fx.f7_mi355x(), 2, engine=engine).ids
