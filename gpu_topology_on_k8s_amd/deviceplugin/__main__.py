@@ -19,6 +19,7 @@ import threading
 from ..k8s.annotations import Contract
 from ..placement import PlacementPolicy
 from ..topology.discovery import discover
+from ..topology.shares import time_slice
 from .health import HealthMonitor, HealthPolicy
 from .plugin import DevicePluginServer, PluginConfig, startup_topology
 from .proto import DEVICE_PLUGIN_PATH
@@ -80,12 +81,18 @@ def main(argv=None) -> int:
     ap.add_argument("--gpu-events", default="auto", choices=["auto", "off"],
                     help="amdsmi GPU event notification (reset / VM fault / thermal throttle) on its own thread; "
                          "auto = on wherever amdsmi offers it")
+    ap.add_argument("--time-slices", type=int, default=1,
+                    help="advertise every (SPX) GPU as this many time slices: Gaia fractional requests on unpartitioned "
+                         "nodes (a pod holding j slices holds j/S of one GPU; topology/shares.py); 1 = whole GPUs")
     ap.add_argument("--log-level", default="INFO")
     a = ap.parse_args(argv)
     logging.basicConfig(level=a.log_level, format='{"ts":"%(asctime)s","lvl":"%(levelname)s","mod":"%(name)s","msg":"%(message)s"}')
     log = logging.getLogger("gtk.deviceplugin")
 
-    topo = discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus)
+    def node_topology():
+        return time_slice(discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus), a.time_slices)
+
+    topo = node_topology()
     api = make_api(a.apiserver, a.token, a.ca_file, a.insecure_skip_tls_verify)
     contract = Contract(resource_name=a.resource_name, prefix=a.annotation_prefix)
     probe_fn = None
@@ -97,13 +104,12 @@ def main(argv=None) -> int:
         def probe_fn():
             probed, msg = probe_in_child(a.probe, backend=a.discovery)
             log.info("probe: %s", msg)
-            return probed
+            return None if probed is None else time_slice(probed, a.time_slices)
     names = (a.resource_name, "aliyun.com/gpu", "aliyun.com/gpu-count")
     topo, how = startup_topology(topo, api, a.node_name, contract, names, probe_fn)
     log.info("link matrix: %s; topology:\n%s", how, topo.render())
 
-    health = HealthMonitor(topo, lambda: discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus),
-                           HealthPolicy(xgmi_links=a.xgmi_link_loss == "unhealthy"))
+    health = HealthMonitor(topo, node_topology, HealthPolicy(xgmi_links=a.xgmi_link_loss == "unhealthy"))
 
     specs = a.device_specs if a.device_specs != "auto" else ("stub" if a.discovery == "fake" else "strict")
     cfg = PluginConfig(resource_name=a.resource_name, socket_dir=a.socket_dir, socket_name=a.socket_name, dev_root=a.dev_root,
@@ -122,7 +128,8 @@ def main(argv=None) -> int:
         from ..ops.probe import probe_in_child
 
         def reprobe():
-            return probe_in_child(a.probe if a.probe != "off" else "quick", backend=a.discovery)[0]
+            probed = probe_in_child(a.probe if a.probe != "off" else "quick", backend=a.discovery)[0]
+            return None if probed is None else time_slice(probed, a.time_slices)
     plugin = DevicePluginServer(topo, cfg, api=api, health_fn=health if a.discovery != "fake" else None, reprobe_fn=reprobe)
     plugin.event_source = events
     if a.metrics_port:

@@ -32,7 +32,7 @@ def cdi_name(kind: str, index: int) -> str:
 def _nodes(topo: Topology, i: int, dev_root: str) -> List[Dict[str, object]]:
     g = topo.gpus[i]
     root = dev_root.rstrip("/")
-    minor = g.render_minor if g.render_minor >= 0 else 128 + i
+    minor = g.render_node
     out: List[Dict[str, object]] = [{"path": f"/dev/dri/renderD{minor}", "hostPath": f"{root}/dri/renderD{minor}"}]
     if g.card >= 0:
         out.append({"path": f"/dev/dri/card{g.card}", "hostPath": f"{root}/dri/card{g.card}"})

@@ -42,8 +42,9 @@ from ..k8s.objects import meta, pod_gpu_request, pod_is_terminal, pod_phase
 from ..placement import NoFeasiblePlacement, PlacementPolicy
 from ..placement.core import select_with
 from ..topology.cpus import recommended_cpuset
-from ..topology.identity import ENV_BDFS, ENV_GROUP
+from ..topology.identity import ENV_BDFS, ENV_FRACTION, ENV_GROUP, ENV_SLICES
 from ..topology.model import Topology
+from ..topology.shares import physical_group, share_fractions, slices_per_gpu
 from . import proto as pb
 from .podresources import POD_RESOURCES_SOCKET, list_pod_resources
 from .metrics import PluginMetrics
@@ -113,8 +114,8 @@ def placeholder_dev_tree(root: str, topo: Topology) -> str:
     nodes exist but the Allocate -> container path must still be exercised end to end)."""
     os.makedirs(os.path.join(root, "dri"), exist_ok=True)
     names = ["kfd"]
-    for i, g in enumerate(topo.gpus):
-        names.append(f"dri/renderD{g.render_minor if g.render_minor >= 0 else 128 + i}")
+    for g in topo.gpus:
+        names.append(f"dri/renderD{g.render_node}")
         if g.card >= 0:
             names.append(f"dri/card{g.card}")
     for n in names:
@@ -478,10 +479,11 @@ class DevicePluginServer:
         import subprocess
         import sys
 
-        bdfs = ",".join(self.topology.gpus[i].bdf for i in ids)
+        ids = physical_group(self.topology, ids)  # time slices of one GPU validate that GPU once
+        bdfs = ",".join(self.topology.gpus[self._first_slice(i)].bdf for i in ids)
         cmd = [sys.executable, "-m", "gpu_topology_on_k8s_amd", "validate", "--group", ",".join(map(str, ids)),
                "--min-bytes", str(1 << 20), "--max-bytes", str(64 << 20), "--factor", "8", "--iters", "5", "--warmup", "2"]
-        if all(self.topology.gpus[i].bdf for i in ids):
+        if all(self.topology.gpus[self._first_slice(i)].bdf for i in ids):
             cmd += ["--bdfs", bdfs]
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         try:
@@ -496,17 +498,22 @@ class DevicePluginServer:
         return out
 
     # ------------------------------------------------------------------ Allocate helpers
+    def _first_slice(self, physical: int) -> int:
+        """Topology index of the first device of physical GPU ``physical`` (itself on an SPX node)."""
+        return next(g.index for g in self.topology.gpus if g.physical == physical)
+
     def device_nodes(self, ids: Sequence[int]) -> List[Tuple[str, str]]:
-        """(container path, host path) of every device node the container needs for ``ids``."""
+        """(container path, host path) of every device node the container needs for ``ids``, each
+        once (time slices of one GPU share its render/card nodes)."""
         root = self.cfg.dev_root.rstrip("/")
         out = [("/dev/kfd", f"{root}/kfd")]
         for i in ids:
             g = self.topology.gpus[i]
-            minor = g.render_minor if g.render_minor >= 0 else 128 + i
+            minor = g.render_node
             out.append((f"/dev/dri/renderD{minor}", f"{root}/dri/renderD{minor}"))
             if g.card >= 0:
                 out.append((f"/dev/dri/card{g.card}", f"{root}/dri/card{g.card}"))
-        return out
+        return list(dict.fromkeys(out))
 
     def _missing_device_nodes(self, ids: Sequence[int]) -> List[str]:
         if self.cfg.device_specs != "strict":
@@ -525,10 +532,20 @@ class DevicePluginServer:
                 continue  # kind / fake GPUs: never hand containerd a host path the node does not have
             r.devices.add(container_path=cpath, host_path=hpath, permissions="rw")
         numa = {int(self.topology.gpus[i].numa) for i in ids}
-        r.envs[ENV_GROUP] = format_group(ids)
-        # PCI addresses in GROUP order: HIP renumbers the container's devices 0..k-1, so tools inside
-        # the pod map GROUP -> HIP ordinal by address (topology/identity.py, `gtk validate`)
-        r.envs[ENV_BDFS] = ",".join(self.topology.gpus[i].bdf for i in ids)
+        if slices_per_gpu(self.topology) > 1:
+            # time slices (topology/shares.py): the container sees the physical GPUs behind them, and
+            # its share of each (GTK_GPU_FRACTION, in GROUP order) caps its HBM cooperatively
+            frac = share_fractions(self.topology, ids)
+            group = sorted(frac)
+            r.envs[ENV_GROUP] = format_group(group)
+            r.envs[ENV_BDFS] = ",".join(self.topology.gpus[self._first_slice(p)].bdf for p in group)
+            r.envs[ENV_FRACTION] = ",".join(f"{frac[p]:.4g}" for p in group)
+            r.envs[ENV_SLICES] = format_group(ids)
+        else:
+            r.envs[ENV_GROUP] = format_group(ids)
+            # PCI addresses in GROUP order: HIP renumbers the container's devices 0..k-1, so tools inside
+            # the pod map GROUP -> HIP ordinal by address (topology/identity.py, `gtk validate`)
+            r.envs[ENV_BDFS] = ",".join(self.topology.gpus[i].bdf for i in ids)
         r.envs["GTK_NUMA_NODES"] = ",".join(str(x) for x in sorted(numa))
         cpuset = recommended_cpuset(self.topology, ids)  # Gaia B6: the devices' local core slices
         if cpuset:
@@ -759,16 +776,21 @@ class DevicePluginServer:
         self.metrics.gpu_events.labels(kind).inc()
         bdf = self.topology.gpus[index].bdf or "no bdf"
         node = {"kind": "Node", "metadata": {"name": self.cfg.node_name}}
+        # the time slices of a GPU (topology/shares.py) are one device: a reset takes all of them
+        same = ([g.index for g in self.topology.gpus if g.physical == self.topology.gpus[index].physical]
+                if slices_per_gpu(self.topology) > 1 else [index])
         if kind == "GPU_PRE_RESET":
-            self._holds[index] = "GPU reset in progress"
             log.warning("device %d (%s): GPU reset starting: %s", index, bdf, message)
-            self.set_health(index, False)
+            for i in same:
+                self._holds[i] = "GPU reset in progress"
+                self.set_health(i, False)
             reason, note = "GPUReset", f"device {index} ({bdf}) is resetting; held Unhealthy"
         elif kind == "GPU_POST_RESET":
-            self._holds.pop(index, None)
             log.warning("device %d (%s): GPU reset finished: %s", index, bdf, message)
-            if self.health_fn is None:
-                self.set_health(index, True)
+            for i in same:
+                self._holds.pop(i, None)
+                if self.health_fn is None:
+                    self.set_health(i, True)
             self._reprobe_now.set()
             reason, note = "GPUResetDone", f"device {index} ({bdf}) finished a reset; links re-measured when idle"
         elif kind == "VMFAULT":

@@ -19,7 +19,8 @@ This implementation adds:
     stack and the SLIT distance from the pod's preferred NUMA node raise a device's access cost, and
     bind writes the chosen devices' core slices (``<prefix>/cpuset``) and NUMA nodes on the pod;
   * fractional requests (Gaia Fragment, Alg. 2) as XCP partitions of ONE physical GPU on
-    CPX/DPX/QPX nodes, selected by the ``<prefix>/gpu-fraction`` pod annotation;
+    CPX/DPX/QPX nodes, or as time slices of one GPU on a node whose device plugin runs with
+    ``--time-slices`` (topology/shares.py), selected by the ``<prefix>/gpu-fraction`` pod annotation;
   * per-node locking + an assume overlay so concurrent binds never overlap (BASELINE config 4);
   * three selectable policies: ``exact`` (default, :func:`placement.select`), ``gaia`` (cost-tree
     Alg. 1-4) and ``design`` (the reference's greedy/Prim, for parity experiments);
@@ -279,7 +280,7 @@ class TopologyExtender:
                 sizes[g.physical] = sizes.get(g.physical, 0) + 1
             per_gpu = max(sizes.values()) if sizes else 1
             if per_gpu <= 1:
-                return None, "fractional GPU requests need a partitioned (CPX/DPX/QPX) node"
+                return None, "fractional GPU requests need a partitioned (CPX/DPX/QPX) or time-sliced node"
             need = max(1, math.ceil(fraction * per_gpu - 1e-9))
             if need != k:
                 return None, (f"gpu-fraction {fraction} is {need} of {per_gpu} partitions per GPU on this node, "

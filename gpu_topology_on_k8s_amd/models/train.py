@@ -54,14 +54,26 @@ def _pod_devices(env, visible_bdfs=None) -> Dict[str, object]:
     """Inside a pod: train on the devices the device plugin allocated (``GTK_GPU_GROUP`` node-local
     indices, ``GTK_GPU_BDFS`` their PCI addresses; ``design.md:239``), rank r on GROUP[r], mapped to
     this container's HIP ordinals by PCI address (:func:`topology.identity.resolve_group`)."""
-    from ..topology.identity import ENV_GROUP, group_from_env, resolve_group
+    from ..topology.identity import ENV_GROUP, fractions_from_env, group_from_env, resolve_group
 
     group, bdfs = group_from_env()
     if len(group) != env["world"]:
         raise ValueError(f"{ENV_GROUP}={group} allocates {len(group)} devices for a job of {env['world']} ranks")
     hip = resolve_group(group, bdfs=bdfs or None, visible_bdfs=visible_bdfs)
+    fr = fractions_from_env()
     return {"devices": group, "hip_devices": hip, "best": group, "best_score": None, "worst": None, "worst_score": None,
-            "source": "pod-allocation"}
+            "source": "pod-allocation", "fractions": fr if len(fr) == len(group) else None}
+
+
+def apply_share_cap(pl: Dict[str, object], rank: int, dev: int) -> Optional[float]:
+    """On a time-sliced node (``GTK_GPU_FRACTION``, topology/shares.py) hold this process to its
+    share of the GPU's HBM: the caching allocator refuses to grow past ``fraction * capacity``.  The
+    slices of a GPU share its CUs, so this is the cooperative part of the share; returns the cap."""
+    fr = pl.get("fractions")
+    if not fr or float(fr[rank]) >= 1.0:
+        return None
+    torch.cuda.set_per_process_memory_fraction(float(fr[rank]), dev)
+    return float(fr[rank])
 
 
 def _choose_device(env, placement: str, discovery: str, visible: Optional[int] = None) -> Dict[str, object]:
@@ -94,6 +106,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         pl = _pod_devices(env)
         dev = int(pl["hip_devices"][env["rank"]])
         torch.cuda.set_device(dev)
+        pl["hbm_cap_fraction"] = apply_share_cap(pl, env["rank"], dev)
         device = torch.device("cuda", dev)
         gemm_mode = setup_gemm_tuning(gemm_tuning, gemm_table, env["rank"])
     elif device_kind == "cuda":
@@ -238,6 +251,8 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "placement": placement,
         "devices": pl["devices"],
         "placement_source": pl.get("source"),
+        "gpu_fractions": pl.get("fractions"),
+        "hbm_cap_fraction": pl.get("hbm_cap_fraction"),
         "best_devices": pl.get("best"),
         "worst_devices": pl.get("worst"),
         "best_score": pl.get("best_score"),

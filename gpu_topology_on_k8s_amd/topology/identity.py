@@ -24,11 +24,16 @@ from typing import Dict, List, Optional, Sequence
 
 log = logging.getLogger(__name__)
 
-__all__ = ["normalize_bdf", "hip_device_bdfs", "DeviceMap", "resolve_group", "ENV_GROUP", "ENV_BDFS"]
+__all__ = ["normalize_bdf", "hip_device_bdfs", "DeviceMap", "resolve_group", "ENV_GROUP", "ENV_BDFS", "ENV_FRACTION",
+           "ENV_SLICES", "fractions_from_env"]
 
 #: container env written by Allocate: node-local indices (GROUP order) and their PCI addresses
 ENV_GROUP = "GTK_GPU_GROUP"
 ENV_BDFS = "GTK_GPU_BDFS"
+#: on a time-sliced node (topology/shares.py): the share of each GROUP GPU the pod holds, and the
+#: slice ids the kubelet allocated (GROUP then names the physical GPUs behind them)
+ENV_FRACTION = "GTK_GPU_FRACTION"
+ENV_SLICES = "GTK_GPU_SLICES"
 
 _BDF_RE = re.compile(r"^(?:([0-9a-fA-F]{1,8}):)?([0-9a-fA-F]{1,2}):([0-9a-fA-F]{1,2})\.([0-7])$")
 
@@ -174,3 +179,9 @@ def group_from_env(env: Optional[Dict[str, str]] = None):
     g = [int(x) for x in env.get(ENV_GROUP, "").split(",") if x.strip()]
     b = [x.strip() for x in env.get(ENV_BDFS, "").split(",") if x.strip()]
     return g, b
+
+
+def fractions_from_env(env: Optional[Dict[str, str]] = None) -> List[float]:
+    """The pod's share of each GROUP GPU (``GTK_GPU_FRACTION``; empty when it holds whole GPUs)."""
+    env = os.environ if env is None else env
+    return [float(x) for x in env.get(ENV_FRACTION, "").split(",") if x.strip()]

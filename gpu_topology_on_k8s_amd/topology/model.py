@@ -199,10 +199,21 @@ class GPUInfo:
     ecc_deferred: int = -1
     bad_pages: int = -1
     bad_page_threshold: int = -1
+    # > 1: this device is one of `shares` time slices of GPU `physical` (topology/shares.py); the
+    # slices of a GPU share its CUs and HBM, so a pod holding j of them holds j/shares of the GPU
+    shares: int = 1
 
     def __post_init__(self) -> None:
         if self.physical < 0:
             self.physical = self.index
+
+    @property
+    def render_node(self) -> int:
+        """``/dev/dri/renderD<minor>`` of this device; without a discovered one (fake / fixture
+        devices) 128 + index, the physical GPU's for a time slice (slices share their GPU's node)."""
+        if self.render_minor >= 0:
+            return self.render_minor
+        return 128 + (self.physical if self.shares > 1 else self.index)
 
     @property
     def device_id(self) -> str:

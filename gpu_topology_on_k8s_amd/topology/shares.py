@@ -1,0 +1,114 @@
+"""Time-sliced GPU shares: Gaia's vGPU (fractional requests) on unpartitioned (SPX) nodes.
+
+Gaia serves a request for 0 < m < 1 of a GPU by its Fragment algorithm (paper p.4-5 Alg. 2,
+``reference/gaia_gpu_topology_scheduler.md:32``): the fraction lands on the GPU whose remaining share
+fits it most tightly, and the paper's Table II packs 0.5, 0.4 and 0.1 onto one GPU.  On MI355X the
+hardware form of that is XCP partitioning (CPX/DPX/QPX, ``placement.core.place_fraction``), but a node
+left in SPX mode — the default — has no partitions.  This module gives such a node the same shape in
+software: every physical GPU is advertised as ``S`` *time slices* (device ``i*S + j`` is slice ``j``
+of GPU ``i``), so
+
+* the kubelet counts shares (``amd.com/gpu: 4`` on an ``S = 10`` node is 0.4 of one GPU) and the
+  pod-annotation contract (``ALIYUN_COM_GPU_GROUP`` = slice ids) stays as it is;
+* the extender's Fragment path (``<prefix>/gpu-fraction`` + ``place_fraction``) packs fractions onto
+  the best-fitting GPU exactly as it packs XCPs of one package;
+* Allocate maps slices back to the physical GPU (its render/card nodes once) and tells the container
+  its share (``GTK_GPU_FRACTION``).  Slices of one GPU run concurrently on the same CUs: the share is
+  a scheduling quantity plus a cooperative HBM cap (``torch.cuda.set_per_process_memory_fraction`` in
+  the training entry point, ``models/train.py``), not hardware isolation — CPX/DPX partitions are the
+  isolated form.
+
+Slices of one GPU are linked ``INTERNAL`` at the GPU's own HBM bandwidth (they share the device);
+slices of different GPUs inherit the physical pair's link class, hops, amdsmi weight and measured
+bandwidth.
+"""
+from __future__ import annotations
+
+import copy
+import dataclasses
+from typing import Dict, List, Sequence
+
+import numpy as np
+
+from .model import GPUInfo, LinkType, Topology
+
+__all__ = ["time_slice", "slices_per_gpu", "physical_group", "share_fractions"]
+
+
+def slices_per_gpu(topo: Topology) -> int:
+    """``S`` of a time-sliced node (1 for a node whose devices are whole GPUs or XCPs)."""
+    return max((int(g.shares) for g in topo.gpus), default=1)
+
+
+def time_slice(topo: Topology, slices: int) -> Topology:
+    """``topo`` with every GPU advertised as ``slices`` time slices (``slices <= 1``: ``topo`` itself).
+
+    Only whole GPUs can be sliced: a partitioned node (CPX/DPX/QPX) already exposes hardware
+    fractions, and slicing its XCPs would need a third hierarchy level the placement core does not
+    model, so that raises ``ValueError``."""
+    s = int(slices)
+    if s <= 1:
+        return topo
+    if slices_per_gpu(topo) > 1:
+        raise ValueError("topology is already time-sliced")
+    if any(g.physical != g.index for g in topo.gpus):
+        raise ValueError("time slicing needs an unpartitioned (SPX) node; this one exposes XCP partitions")
+    n = topo.n
+    phys = np.repeat(np.arange(n), s)  # virtual device -> physical GPU
+    gpus: List[GPUInfo] = []
+    for v, p in enumerate(phys):
+        g = topo.gpus[int(p)]
+        gpus.append(dataclasses.replace(g, index=v, physical=int(p), shares=s,
+                                        uuid=f"{g.uuid}-s{v % s}" if g.uuid else "",
+                                        vram_bytes=int(g.vram_bytes) // s))
+    same = phys[:, None] == phys[None, :]
+
+    def expand(m):
+        return None if m is None else np.asarray(m)[np.ix_(phys, phys)].copy()
+
+    lt = expand(topo.link_type)
+    lt[same] = int(LinkType.INTERNAL)
+    hops = expand(topo.hops)
+    hops[same] = 0
+    weight = expand(topo.weight)
+    if weight is not None:
+        weight[same] = 0.0
+    bw = expand(topo.bw_gbps)
+    hbm = None if topo.hbm_gbps is None else np.asarray(topo.hbm_gbps, dtype=np.float64)[phys]
+    if hbm is not None:  # slices of one GPU exchange data through its own HBM
+        bw[same] = np.broadcast_to(hbm[:, None], bw.shape)[same]
+    else:
+        bw[same] = np.nan
+    probe: Dict[str, object] = copy.deepcopy(topo.probe or {})
+    mx = probe.get("amdsmi_max_bw_mbps")
+    if mx is not None and np.asarray(mx).shape == (n, n):
+        probe["amdsmi_max_bw_mbps"] = expand(np.asarray(mx, dtype=np.float64)).tolist()
+    ing = probe.get("ingress_all_gbps")
+    if isinstance(ing, list) and len(ing) == n:
+        probe["ingress_all_gbps"] = [ing[int(p)] for p in phys]
+    probe["time_slices"] = s
+    out = Topology(
+        gpus=gpus, link_type=lt, hops=hops, weight=weight, bw_gbps=bw,
+        cost=None if topo.ref_class is None else expand(topo.cost),
+        ref_gbps=topo.ref_gbps, node_name=topo.node_name, source=topo.source, probe=probe,
+        ref_class=expand(topo.ref_class), hbm_gbps=hbm,
+        numa_distance=copy.deepcopy(topo.numa_distance), nics=copy.deepcopy(topo.nics),
+        gpu_nic=None if topo.gpu_nic is None else [list(topo.gpu_nic[int(p)]) for p in phys],
+    )
+    if out.ref_class is not None:  # fixtures priced by reference class: same GPU = the cheapest pair
+        out.cost[same & ~np.eye(out.n, dtype=bool)] = 0.0
+    return out
+
+
+def physical_group(topo: Topology, ids: Sequence[int]) -> List[int]:
+    """Physical GPUs (ascending, each once) behind the devices ``ids``."""
+    return sorted({int(topo.gpus[int(i)].physical) for i in ids})
+
+
+def share_fractions(topo: Topology, ids: Sequence[int]) -> Dict[int, float]:
+    """Physical GPU -> fraction of it that the time slices ``ids`` hold (slices / S)."""
+    held: Dict[int, int] = {}
+    for i in set(int(x) for x in ids):
+        held[int(topo.gpus[i].physical)] = held.get(int(topo.gpus[i].physical), 0) + 1
+    s = slices_per_gpu(topo)
+    return {p: min(1.0, c / s) for p, c in held.items()}

@@ -170,3 +170,36 @@ def test_both_daemons_config4_through_shipped_processes():
         srv.shutdown()
         shutil.rmtree(sockdir, ignore_errors=True)
     assert rc == 0
+
+
+def test_device_plugin_daemon_time_slices():
+    """``--time-slices 4`` on a 2-GPU node: the kubelet sees 8 devices, the node annotation carries the
+    slices, and a 2-slice pod gets one GPU's device nodes with GTK_GPU_FRACTION=0.5."""
+    from gpu_topology_on_k8s_amd.k8s.annotations import decode_node_annotations
+    from gpu_topology_on_k8s_amd.topology.shares import slices_per_gpu
+
+    api = FakeAPIServer()
+    api.create_node(make_node("worker-1"))
+    srv, url = serve_http(api)
+    sockdir = tempfile.mkdtemp(prefix="gtkd", dir="/tmp")
+    kubelet = FakeKubelet(sockdir, node_name="worker-1", api=api)
+    kubelet.start()
+    devroot = os.path.join(sockdir, "dev")
+    os.makedirs(devroot)
+    p = _spawn(["gpu_topology_on_k8s_amd.deviceplugin", "--discovery", "fake", "--fake-gpus", "2", "--time-slices", "4",
+                "--apiserver", url, "--node-name", "worker-1", "--socket-dir", sockdir, "--dev-root", devroot,
+                "--log-level", "WARNING"])
+    try:
+        plugin = kubelet.wait_for("amd.com/gpu", timeout=60)
+        assert sorted(plugin.devices, key=int) == [str(i) for i in range(8)]
+        topo = decode_node_annotations(api.get_node("worker-1")["metadata"]["annotations"], Contract())
+        assert topo.n == 8 and slices_per_gpu(topo) == 4
+        pod = api.create_pod(make_pod("half", gpus=2, node="worker-1"))
+        c = kubelet.admit(pod, "amd.com/gpu").container_responses[0]
+        assert c.envs["GTK_GPU_FRACTION"] == "0.5" and len(c.envs["GTK_GPU_GROUP"].split(",")) == 1
+    finally:
+        rc = _stop(p)
+        kubelet.stop()
+        srv.shutdown()
+        shutil.rmtree(sockdir, ignore_errors=True)
+    assert rc == 0, p.stdout.read() if p.stdout else ""

@@ -1,0 +1,76 @@
+"""GPU: time-sliced shares (topology/shares.py) on the real MI355X, which runs in SPX mode.
+
+The node is discovered through amdsmi and advertised as 4 slices per GPU; two pods asking for half a
+GPU each go through the whole flow (extender /filter /sort /bind, GetPreferredAllocation, Allocate),
+land on the same physical GPU, and then train concurrently on it with their HBM caps."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_STRIP = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")
+
+
+def _pod_env(envs):
+    env = {k: v for k, v in os.environ.items() if k not in _STRIP}
+    env.update({k: envs[k] for k in ("GTK_GPU_GROUP", "GTK_GPU_BDFS", "GTK_GPU_FRACTION")})
+    return env
+
+
+def test_two_half_gpu_pods_share_the_real_gpu_and_train_concurrently():
+    from gpu_topology_on_k8s_amd.k8s import Contract
+    from gpu_topology_on_k8s_amd.sim import SimCluster
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
+    from gpu_topology_on_k8s_amd.topology.shares import physical_group, time_slice
+
+    t = discover("auto")
+    t.node_name = "gpu-node"
+    v = time_slice(t, 4)
+    envs = []
+    with SimCluster({"gpu-node": v}) as c:
+        for name in ("half-a", "half-b"):
+            c.submit(name, 2, annotations={Contract().fraction_key: "0.5"})
+            r = c.schedule_pending()[0]
+            assert r.error == "" and len(r.allocated) == 2 and physical_group(v, r.allocated) == [0], r
+            envs.append(dict(c.nodes["gpu-node"].kubelet.responses[f"default/{name}"].container_responses[0].envs))
+    assert [e["GTK_GPU_FRACTION"] for e in envs] == ["0.5", "0.5"]
+    assert envs[0]["GTK_GPU_GROUP"] == envs[1]["GTK_GPU_GROUP"] == "0" and envs[0]["GTK_GPU_SLICES"] != envs[1]["GTK_GPU_SLICES"]
+    cmd = [sys.executable, "-m", "gpu_topology_on_k8s_amd.models.train", "--model", "mnist-cnn", "--batch", "64", "--steps", "200",
+           "--warmup", "5", "--gemm-tuning", "off"]
+    procs = [subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=REPO, env=_pod_env(e))
+             for e in envs]
+    outs = []
+    for p in procs:
+        so, se = p.communicate(timeout=300)
+        assert p.returncode == 0, se[-3000:]
+        outs.append(json.loads([ln for ln in so.splitlines() if ln.startswith("{")][-1]))
+    for o in outs:
+        assert o["devices"] == [0] and o["gpu_fractions"] == [0.5] and o["hbm_cap_fraction"] == 0.5 and o["throughput"] > 0
+    print(json.dumps({"shared_gpu_images_per_s": [round(o["throughput"]) for o in outs]}))
+
+
+def test_share_cap_bounds_the_caching_allocator():
+    """A quarter share: allocating 30 % of the GPU's HBM fails, 20 % succeeds."""
+    code = r"""
+import torch
+from gpu_topology_on_k8s_amd.models.train import apply_share_cap
+assert apply_share_cap({"fractions": [0.25]}, 0, 0) == 0.25
+cap = torch.cuda.get_device_properties(0).total_memory
+x = torch.empty(int(0.20 * cap), dtype=torch.uint8, device="cuda")
+del x
+torch.cuda.empty_cache()
+try:
+    torch.empty(int(0.30 * cap), dtype=torch.uint8, device="cuda")
+    print("NOCAP")
+except torch.OutOfMemoryError:
+    print("CAPPED")
+"""
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=REPO, timeout=120,
+                       env={k: v for k, v in os.environ.items() if k not in _STRIP})
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.stdout.strip().splitlines()[-1] == "CAPPED"

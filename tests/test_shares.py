@@ -1,0 +1,120 @@
+"""Time-sliced GPU shares (topology/shares.py): Gaia's fractional requests (paper p.4-5 Alg. 2,
+Table II; ``gaia_gpu_topology_scheduler.md:32``) on unpartitioned SPX nodes, through the model, the
+annotation codec, the placement core, the device plugin and the whole cluster."""
+import numpy as np
+import pytest
+
+from gpu_topology_on_k8s_amd.deviceplugin import DevicePluginServer, PluginConfig
+from gpu_topology_on_k8s_amd.deviceplugin import proto as pb
+from gpu_topology_on_k8s_amd.k8s import Contract, PodAssignment
+from gpu_topology_on_k8s_amd.k8s.annotations import decode_node_annotations, encode_node_annotations
+from gpu_topology_on_k8s_amd.placement import PlacementPolicy, place_fraction, select
+from gpu_topology_on_k8s_amd.sim import SimCluster
+from gpu_topology_on_k8s_amd.k8s.objects import make_pod
+from gpu_topology_on_k8s_amd.topology import fixtures as fx
+from gpu_topology_on_k8s_amd.topology.identity import fractions_from_env, resolve_group
+from gpu_topology_on_k8s_amd.topology.model import LinkType, Topology
+from gpu_topology_on_k8s_amd.topology.shares import physical_group, share_fractions, slices_per_gpu, time_slice
+
+C = Contract()
+
+
+def _probed_f7(n=4):
+    t = fx.f7_mi355x(n=n)
+    bw = np.full((n, n), 70.0)
+    bw[0, 1] = bw[1, 0] = 35.0  # one degraded link
+    np.fill_diagonal(bw, np.nan)
+    t.hbm_gbps = np.full(n, 3200.0)
+    t.set_measured_bw(bw, {"method": "test", "ingress_all_gbps": [200.0] * n})
+    return t
+
+
+def test_time_slice_shape_links_and_costs():
+    t = _probed_f7()
+    v = time_slice(t, 4)
+    assert v.n == 16 and slices_per_gpu(v) == 4
+    assert list(v.physical) == [i // 4 for i in range(16)]
+    assert all(g.vram_bytes == t.gpus[0].vram_bytes // 4 for g in v.gpus)
+    assert len({g.uuid for g in v.gpus}) == 16 and all(g.bdf == t.gpus[g.physical].bdf for g in v.gpus)
+    assert v.link_type[0, 1] == LinkType.INTERNAL and v.link_type[0, 4] == t.link_type[0, 1]
+    # slices of one GPU exchange through its HBM: far cheaper than any link; the degraded link stays degraded
+    assert v.cost[0, 1] < v.cost[0, 8] and v.cost[0, 4] == pytest.approx(t.cost[0, 1])
+    assert v.cost[0, 4] > v.cost[0, 8]
+    assert v.probe["ingress_all_gbps"] == [200.0] * 16 and v.probe["time_slices"] == 4
+    assert time_slice(t, 1) is t
+
+
+def test_time_slice_refuses_partitioned_and_double_slicing():
+    with pytest.raises(ValueError, match="SPX"):
+        time_slice(fx.f8_mi355x_cpx(), 2)
+    with pytest.raises(ValueError, match="already"):
+        time_slice(time_slice(fx.f7_mi355x(n=2), 2), 2)
+
+
+def test_sliced_node_annotation_round_trip_keeps_placements():
+    v = time_slice(_probed_f7(), 10)
+    back = decode_node_annotations(encode_node_annotations(v, C), C)
+    assert back.n == 40 and slices_per_gpu(back) == 10 and list(back.physical) == list(v.physical)
+    np.testing.assert_allclose(back.cost, v.cost)
+    used = list(range(20, 25))
+    assert place_fraction(back, 4, used) == place_fraction(v, 4, used) == (25, 26, 27, 28)
+
+
+def test_whole_gpu_request_on_a_sliced_node_takes_one_gpu():
+    v = time_slice(fx.f7_mi355x(n=4), 4)
+    pl = select(v, 4, used=[0], policy=PlacementPolicy(partition_aware=True))
+    assert len(physical_group(v, pl.ids)) == 1 and 0 not in physical_group(v, pl.ids)
+
+
+def test_share_fractions():
+    v = time_slice(fx.f7_mi355x(n=2), 10)
+    assert share_fractions(v, [10, 11, 12, 13]) == {1: pytest.approx(0.4)}
+    assert share_fractions(v, list(range(10)) + [15]) == {0: 1.0, 1: pytest.approx(0.1)}
+
+
+def test_allocate_maps_slices_to_the_physical_gpu(tmp_path):
+    t = fx.f7_mi355x(n=2)
+    v = time_slice(t, 10)
+    plug = DevicePluginServer(v, PluginConfig(device_specs="stub", dev_root=str(tmp_path)))
+    assert len(plug.devices()) == 20
+    req = pb.AllocateRequest()
+    req.container_requests.add(devices_ids=["11", "12", "13", "14"])
+    r = plug.Allocate(req, None).container_responses[0]
+    envs = dict(r.envs)
+    assert envs["GTK_GPU_GROUP"] == "1" and envs["GTK_GPU_BDFS"] == t.gpus[1].bdf
+    assert envs["GTK_GPU_FRACTION"] == "0.4" and envs["GTK_GPU_SLICES"] == "11,12,13,14"
+    assert fractions_from_env(envs) == [0.4]
+    nodes = plug.device_nodes([11, 12, 13, 14])
+    assert len(nodes) == len(set(nodes)) == 1 + 1 + (1 if t.gpus[1].card >= 0 else 0)
+    # inside the container: the one physical GPU it sees is HIP 0
+    assert resolve_group([1], bdfs=[t.gpus[1].bdf], visible_bdfs=[t.gpus[1].bdf]) == [0]
+
+
+def test_table2_fragment_through_the_cluster_on_a_time_sliced_spx_node():
+    """Gaia Table II on a 4-GPU SPX node advertised as 10 time slices per GPU: after 0.5 of gpu2 is
+    taken, a 0.4-GPU pod and then a 0.1-GPU pod both land on gpu2 (best fit) through /filter, /sort,
+    /bind, GetPreferredAllocation and Allocate, and the containers get gpu2 with their shares."""
+    v = time_slice(Topology.full_mesh(n=4, numa_split=1, node_name="p4"), 10)
+    with SimCluster({"p4": v}) as c:
+        c.api.create_pod(make_pod("half", gpus=5, node="p4",
+                                  annotations=PodAssignment(list(range(20, 25)), True, 1).to_annotations()))
+        c.submit("f04", 4, annotations={C.fraction_key: "0.4"})
+        r = c.schedule_pending()[0]
+        assert r.error == "" and set(r.allocated) <= set(range(25, 30)) and len(r.allocated) == 4
+        envs = dict(c.nodes["p4"].kubelet.responses["default/f04"].container_responses[0].envs)
+        assert envs["GTK_GPU_GROUP"] == "2" and envs["GTK_GPU_FRACTION"] == "0.4"
+        c.submit("f01", 1, annotations={C.fraction_key: "0.1"})
+        r = c.schedule_pending()[0]
+        assert r.allocated == (29,)
+        c.submit("whole", 10)  # a whole GPU on the same node: all slices of one untouched GPU
+        r = c.schedule_pending()[0]
+        assert r.error == "" and len(physical_group(v, r.allocated)) == 1 and 2 not in physical_group(v, r.allocated)
+
+
+def test_gpu_reset_holds_every_slice_of_the_gpu():
+    v = time_slice(fx.f7_mi355x(n=2), 4)
+    plug = DevicePluginServer(v, PluginConfig())
+    plug.gpu_event(5, "GPU_PRE_RESET", "test")
+    assert [d.health for d in plug.devices()] == [pb.HEALTHY] * 4 + [pb.UNHEALTHY] * 4
+    plug.gpu_event(5, "GPU_POST_RESET", "test")
+    assert all(d.health == pb.HEALTHY for d in plug.devices())
