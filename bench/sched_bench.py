@@ -87,16 +87,22 @@ def exp2_fragments(reps: int):
             "note": "fractional GPUs have no k8s extended-resource form; placement core only (MI355X: XCP partitions)"}
 
 
-def exp2_xcp_cluster(reps: int):
+def exp2_xcp_cluster(reps: int, node: str = "xcp"):
     """Gaia Table II through /filter, /sort, /bind, GetPreferredAllocation and Allocate: 0.5 of gpu2
-    is held (5 of its 10 partitions), then a 0.4-GPU pod, then a 0.1-GPU pod."""
+    is held (5 of its 10 partitions), then a 0.4-GPU pod, then a 0.1-GPU pod.  ``node``: ``xcp`` = 10
+    hardware partitions per GPU, ``slices`` = an SPX node whose device plugin advertises 10 time
+    slices per GPU (topology/shares.py)."""
     from gpu_topology_on_k8s_amd.k8s import Contract
     from gpu_topology_on_k8s_amd.k8s.objects import make_pod
+    from gpu_topology_on_k8s_amd.topology.shares import time_slice
 
     c0 = Contract()
     tally = collections.Counter()
     sched = []
-    t = Topology.full_mesh(n=4, numa_split=1, partitions_per_gpu=10, node_name="p4")
+    if node == "xcp":
+        t = Topology.full_mesh(n=4, numa_split=1, partitions_per_gpu=10, node_name="p4")
+    else:
+        t = time_slice(Topology.full_mesh(n=4, numa_split=1, node_name="p4"), 10)
     with SimCluster({"p4": t}) as c:
         for i in range(reps):
             c.api.create_pod(make_pod(f"half{i}", gpus=5, node="p4", annotations=PodAssignment(list(range(20, 25)), True, 1)
@@ -111,7 +117,8 @@ def exp2_xcp_cluster(reps: int):
             for n in (f"a{i}", f"b{i}"):
                 c.delete(n)
             c.api.delete_pod("default", f"half{i}")
-    return {"experiment": "exp2-xcp-cluster", "reps": reps, "partitions_per_gpu": 10,
+    return {"experiment": "exp2-xcp-cluster" if node == "xcp" else "exp2-timeslice-cluster", "reps": reps,
+            "partitions_per_gpu" if node == "xcp" else "slices_per_gpu": 10,
             "table": {f"0.4->gpu{','.join(map(str, a))}, 0.1->gpu{','.join(map(str, b))}": n for (a, b), n in tally.items()},
             "sched_ms_mean": statistics.mean(sched), "paper_sched_s": PAPER_SCHED_S["exp2"]}
 
@@ -204,6 +211,7 @@ def main() -> int:
         run_exp("exp1-2gpu", 2, (), a.reps),
         exp2_fragments(a.reps),
         exp2_xcp_cluster(max(20, a.reps // 10)),
+        exp2_xcp_cluster(max(20, a.reps // 10), node="slices"),
         run_exp("exp3", 1, (2,), a.reps),
         run_exp("exp4", 2, (2,), a.reps),
         run_exp("mi355x-exact-4gpu", 4, (), max(50, a.reps // 5), policy="exact", topo_fn=lambda: fx.f7_mi355x(76.5, 0.03, 1)),

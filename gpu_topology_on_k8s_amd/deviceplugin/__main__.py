@@ -84,6 +84,8 @@ def main(argv=None) -> int:
     ap.add_argument("--time-slices", type=int, default=1,
                     help="advertise every (SPX) GPU as this many time slices: Gaia fractional requests on unpartitioned "
                          "nodes (a pod holding j slices holds j/S of one GPU; topology/shares.py); 1 = whole GPUs")
+    ap.add_argument("--share-cu-mask", default="on", choices=["on", "off"],
+                    help="--time-slices: confine a pod holding part of a GPU to its slices' compute units (HSA_CU_MASK)")
     ap.add_argument("--log-level", default="INFO")
     a = ap.parse_args(argv)
     logging.basicConfig(level=a.log_level, format='{"ts":"%(asctime)s","lvl":"%(levelname)s","mod":"%(name)s","msg":"%(message)s"}')
@@ -117,6 +119,7 @@ def main(argv=None) -> int:
                        health_interval=a.health_interval, reprobe_interval=a.reprobe_interval,
                        reprobe_tolerance=a.reprobe_tolerance, pod_resources_socket=a.pod_resources_socket,
                        reconcile_interval=a.reconcile_interval, cdi_dir=a.cdi_dir, nic_env=a.nic_env == "on",
+                       share_cu_mask=a.share_cu_mask == "on",
                        policy=PlacementPolicy(partition_aware=a.partition_aware == "on"))
     events = None
     if a.gpu_events == "auto" and a.discovery in ("auto", "amdsmi"):

@@ -44,7 +44,7 @@ from ..placement.core import select_with
 from ..topology.cpus import recommended_cpuset
 from ..topology.identity import ENV_BDFS, ENV_FRACTION, ENV_GROUP, ENV_SLICES
 from ..topology.model import Topology
-from ..topology.shares import physical_group, share_fractions, slices_per_gpu
+from ..topology.shares import cu_mask_env, physical_group, share_fractions, slices_per_gpu
 from . import proto as pb
 from .podresources import POD_RESOURCES_SOCKET, list_pod_resources
 from .metrics import PluginMetrics
@@ -132,7 +132,8 @@ class PluginConfig:
                  reprobe_interval: float = 0.0, reprobe_tolerance: float = 0.15, device_specs: str = "strict",
                  prestart_validate: bool = False, validate_timeout: float = 120.0,
                  pod_resources_socket: Optional[str] = POD_RESOURCES_SOCKET, reconcile_interval: float = 10.0,
-                 cdi_dir: str = "/var/run/cdi", cdi_kind: str = "amd.com/gpu", nic_env: bool = True):
+                 cdi_dir: str = "/var/run/cdi", cdi_kind: str = "amd.com/gpu", nic_env: bool = True,
+                 share_cu_mask: bool = True):
         self.resource_name = resource_name
         self.socket_dir = socket_dir
         self.socket_name = socket_name
@@ -162,6 +163,9 @@ class PluginConfig:
         # multi-node RCCL: NCCL_IB_HCA = the RDMA NICs behind the allocated GPUs' own PCIe switches
         # (Topology.nearest_nics); a pod's RCCL env annotation still overrides it
         self.nic_env = nic_env
+        # time-sliced nodes (topology/shares.py): confine a pod holding part of a GPU to its slices'
+        # compute units (HSA_CU_MASK); off = slices share every CU (temporal sharing only)
+        self.share_cu_mask = share_cu_mask
         # flow step 8: before the container starts, an RCCL all-reduce over exactly
         # the allocated devices (kubelet PreStartContainer) validates the placement; the measured
         # bus bandwidth is recorded on the pod
@@ -532,6 +536,7 @@ class DevicePluginServer:
                 continue  # kind / fake GPUs: never hand containerd a host path the node does not have
             r.devices.add(container_path=cpath, host_path=hpath, permissions="rw")
         numa = {int(self.topology.gpus[i].numa) for i in ids}
+        mask = ""
         if slices_per_gpu(self.topology) > 1:
             # time slices (topology/shares.py): the container sees the physical GPUs behind them, and
             # its share of each (GTK_GPU_FRACTION, in GROUP order) caps its HBM cooperatively
@@ -541,6 +546,7 @@ class DevicePluginServer:
             r.envs[ENV_BDFS] = ",".join(self.topology.gpus[self._first_slice(p)].bdf for p in group)
             r.envs[ENV_FRACTION] = ",".join(f"{frac[p]:.4g}" for p in group)
             r.envs[ENV_SLICES] = format_group(ids)
+            mask = cu_mask_env(self.topology, ids) if self.cfg.share_cu_mask else ""
         else:
             r.envs[ENV_GROUP] = format_group(ids)
             # PCI addresses in GROUP order: HIP renumbers the container's devices 0..k-1, so tools inside
@@ -556,6 +562,8 @@ class DevicePluginServer:
             r.envs["NCCL_IB_HCA"] = "=" + ",".join(nics)  # exact-name match
         for k, v in extra_env.items():
             r.envs[k] = v
+        if mask:  # after the pod's own RCCL/HSA env: its queues run on its slices' CUs, disjoint from its neighbours'
+            r.envs["HSA_CU_MASK"] = mask
         r.annotations["gputopology.amd.com/devices"] = format_group(ids)
         return r
 

@@ -53,6 +53,7 @@ def from_native(d: Dict[str, object], node_name: str = "", ref_gbps: float = DEF
                 bad_page_threshold=int(g.get("bad_page_threshold", -1)),
                 cpu_affinity=str(g.get("cpu_affinity") or ""),
                 pcie_link_ratio=float(g.get("pcie_link_ratio", -1.0)),
+                cus=int(g.get("cus", -1)),
             )
         )
     lt = np.array(d["link_type"], dtype=np.int32)

@@ -202,6 +202,7 @@ class GPUInfo:
     # > 1: this device is one of `shares` time slices of GPU `physical` (topology/shares.py); the
     # slices of a GPU share its CUs and HBM, so a pod holding j of them holds j/shares of the GPU
     shares: int = 1
+    cus: int = -1  # compute units of the physical GPU (KFD simd_count / simd_per_cu); -1 = unknown
 
     def __post_init__(self) -> None:
         if self.physical < 0:

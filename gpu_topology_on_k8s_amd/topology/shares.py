@@ -13,10 +13,14 @@ of GPU ``i``), so
 * the extender's Fragment path (``<prefix>/gpu-fraction`` + ``place_fraction``) packs fractions onto
   the best-fitting GPU exactly as it packs XCPs of one package;
 * Allocate maps slices back to the physical GPU (its render/card nodes once) and tells the container
-  its share (``GTK_GPU_FRACTION``).  Slices of one GPU run concurrently on the same CUs: the share is
-  a scheduling quantity plus a cooperative HBM cap (``torch.cuda.set_per_process_memory_fraction`` in
-  the training entry point, ``models/train.py``), not hardware isolation — CPX/DPX partitions are the
-  isolated form.
+  its share (``GTK_GPU_FRACTION``).  Slice ``j`` of a GPU owns the ``j``-th ``1/S`` of its compute
+  units, and Allocate hands a pod holding part of a GPU ``HSA_CU_MASK`` with its slices' CUs, so the
+  ROCm runtime creates every queue of the container on those CUs only: pods sharing a GPU run on
+  disjoint CUs (spatial sharing; on MI355X a half mask gives 53 % of the MFMA rate, a quarter 27 %,
+  ``profiles/r02_cumask/``).  Like the HBM cap this is cooperative — a container can rewrite its own
+  environment — so it keeps well-behaved neighbours apart rather than confining a hostile one.  HBM is shared: the training entry point caps its caching allocator at
+  the share (``torch.cuda.set_per_process_memory_fraction``, ``models/train.py``).  CPX/DPX
+  partitions remain the form with isolated HBM and L2.
 
 Slices of one GPU are linked ``INTERNAL`` at the GPU's own HBM bandwidth (they share the device);
 slices of different GPUs inherit the physical pair's link class, hops, amdsmi weight and measured
@@ -32,7 +36,10 @@ import numpy as np
 
 from .model import GPUInfo, LinkType, Topology
 
-__all__ = ["time_slice", "slices_per_gpu", "physical_group", "share_fractions"]
+__all__ = ["time_slice", "slices_per_gpu", "physical_group", "share_fractions", "slice_cus", "cu_mask_env"]
+
+#: compute units of an MI355X (8 XCDs x 32) when discovery could not read the count
+DEFAULT_CUS = 256
 
 
 def slices_per_gpu(topo: Topology) -> int:
@@ -112,3 +119,41 @@ def share_fractions(topo: Topology, ids: Sequence[int]) -> Dict[int, float]:
         held[int(topo.gpus[i].physical)] = held.get(int(topo.gpus[i].physical), 0) + 1
     s = slices_per_gpu(topo)
     return {p: min(1.0, c / s) for p, c in held.items()}
+
+
+def slice_cus(topo: Topology, index: int) -> List[int]:
+    """Compute units owned by time slice ``index``: the ``j``-th of ``S`` equal runs of its GPU's CUs."""
+    g = topo.gpus[int(index)]
+    s = max(1, int(g.shares))
+    c = int(g.cus) if int(g.cus) > 0 else DEFAULT_CUS
+    j = sum(1 for h in topo.gpus[:int(index)] if h.physical == g.physical)
+    return list(range(j * c // s, (j + 1) * c // s))
+
+
+def _ranges(xs: Sequence[int]) -> str:
+    out, xs = [], sorted(xs)
+    i = 0
+    while i < len(xs):
+        j = i
+        while j + 1 < len(xs) and xs[j + 1] == xs[j] + 1:
+            j += 1
+        out.append(str(xs[i]) if i == j else f"{xs[i]}-{xs[j]}")
+        i = j + 1
+    return ",".join(out)
+
+
+def cu_mask_env(topo: Topology, ids: Sequence[int]) -> str:
+    """``HSA_CU_MASK`` for a container holding the time slices ``ids`` ("" when it holds only whole
+    GPUs): ``<ordinal>:<cu list>`` per partly held GPU, ``;``-separated, where the ordinal is the GPU's
+    position among the container's GPUs (the ROCm runtime enumerates them in PCI order, which is the
+    order of the physical indices)."""
+    if slices_per_gpu(topo) <= 1:
+        return ""
+    frac = share_fractions(topo, ids)
+    parts = []
+    for ordinal, p in enumerate(sorted(frac)):
+        if frac[p] >= 1.0:
+            continue
+        cus = sorted({c for i in ids if topo.gpus[int(i)].physical == p for c in slice_cus(topo, int(i))})
+        parts.append(f"{ordinal}:{_ranges(cus)}")
+    return ";".join(parts)

@@ -74,3 +74,55 @@ except torch.OutOfMemoryError:
                        env={k: v for k, v in os.environ.items() if k not in _STRIP})
     assert p.returncode == 0, p.stderr[-2000:]
     assert p.stdout.strip().splitlines()[-1] == "CAPPED"
+
+
+_MFMA = r"""
+import json
+from gpu_topology_on_k8s_amd.ops import probe
+w = probe.warmup(0, {ms})
+print(json.dumps({{"tflops": float(w["tflops"])}}))
+"""
+
+
+def _mfma_rate(env, ms=300.0):
+    return subprocess.Popen([sys.executable, "-c", _MFMA.format(ms=ms)], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                            text=True, cwd=REPO, env=env)
+
+
+def _rate(p):
+    so, se = p.communicate(timeout=120)
+    assert p.returncode == 0, se[-2000:]
+    return json.loads(so.strip().splitlines()[-1])["tflops"]
+
+
+def test_cu_masked_shares_split_the_compute_units():
+    """A 0.25 and a 0.75 pod on the real GPU (4 slices): Allocate gives them disjoint HSA_CU_MASKs;
+    each alone gets about its share of the MFMA rate, and running together neither slows the other."""
+    from gpu_topology_on_k8s_amd.k8s import Contract
+    from gpu_topology_on_k8s_amd.sim import SimCluster
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
+    from gpu_topology_on_k8s_amd.topology.shares import time_slice
+
+    t = discover("auto")
+    t.node_name = "gpu-node"
+    v = time_slice(t, 4)
+    envs = {}
+    with SimCluster({"gpu-node": v}) as c:
+        for name, k, m in (("quarter", 1, "0.25"), ("three-quarters", 3, "0.75")):
+            c.submit(name, k, annotations={Contract().fraction_key: m})
+            r = c.schedule_pending()[0]
+            assert r.error == "", r
+            envs[name] = dict(c.nodes["gpu-node"].kubelet.responses[f"default/{name}"].container_responses[0].envs)
+    cus = t.gpus[0].cus if t.gpus[0].cus > 0 else 256
+    assert envs["quarter"]["HSA_CU_MASK"] == f"0:0-{cus // 4 - 1}"
+    assert envs["three-quarters"]["HSA_CU_MASK"] == f"0:{cus // 4}-{cus - 1}"
+    base = {k: v for k, v in os.environ.items() if k not in _STRIP and k != "HSA_CU_MASK"}
+    full = _rate(_mfma_rate(base))
+    alone = {n: _rate(_mfma_rate(dict(base, HSA_CU_MASK=e["HSA_CU_MASK"]))) for n, e in envs.items()}
+    procs = {n: _mfma_rate(dict(base, HSA_CU_MASK=e["HSA_CU_MASK"]), ms=4000.0) for n, e in envs.items()}
+    together = {n: _rate(p) for n, p in procs.items()}
+    print(json.dumps({"cus": cus, "full_tflops": round(full), "alone_tflops": {n: round(x) for n, x in alone.items()},
+                      "concurrent_tflops": {n: round(x) for n, x in together.items()}}))
+    assert 0.15 < alone["quarter"] / full < 0.4 and 0.6 < alone["three-quarters"] / full < 0.95
+    for n in envs:
+        assert together[n] > 0.8 * alone[n], (n, together, alone)

@@ -118,3 +118,29 @@ def test_gpu_reset_holds_every_slice_of_the_gpu():
     assert [d.health for d in plug.devices()] == [pb.HEALTHY] * 4 + [pb.UNHEALTHY] * 4
     plug.gpu_event(5, "GPU_POST_RESET", "test")
     assert all(d.health == pb.HEALTHY for d in plug.devices())
+
+
+def test_slice_compute_units_and_cu_mask():
+    from gpu_topology_on_k8s_amd.topology.shares import cu_mask_env, slice_cus
+
+    v = time_slice(fx.f7_mi355x(n=2), 4)  # fixtures carry no CU count: MI355X's 256
+    assert slice_cus(v, 0) == list(range(0, 64)) and slice_cus(v, 7) == list(range(192, 256))
+    assert cu_mask_env(v, [5, 6]) == "0:64-191"  # the pod sees GPU 1 as its only device
+    assert cu_mask_env(v, [0, 2]) == "0:0-63,128-191"
+    assert cu_mask_env(v, [0, 1, 2, 3, 7]) == "1:192-255"  # GPU 0 whole (no mask), a quarter of GPU 1
+    assert cu_mask_env(fx.f7_mi355x(n=2), [0]) == ""
+    v8 = time_slice(Topology.full_mesh(n=1), 8)
+    v8.gpus[0].cus = 240  # e.g. a part with harvested CUs: runs of 30
+    assert slice_cus(v8, 0) == list(range(0, 30))
+
+
+def test_allocate_sets_cu_mask_after_pod_env(tmp_path):
+    from gpu_topology_on_k8s_amd.k8s.objects import make_pod as mk
+
+    v = time_slice(fx.f7_mi355x(n=2), 4)
+    plug = DevicePluginServer(v, PluginConfig(device_specs="stub", dev_root=str(tmp_path)))
+    pod = mk("p", gpus=2, annotations={f"{C.prefix}/rccl-env": "HSA_CU_MASK=0:0-255;NCCL_MIN_NCHANNELS=8"})
+    r = plug._container_response([4, 5], plug._rccl_env(pod))
+    assert r.envs["HSA_CU_MASK"] == "0:0-127" and r.envs["NCCL_MIN_NCHANNELS"] == "8"
+    off = DevicePluginServer(v, PluginConfig(device_specs="stub", dev_root=str(tmp_path), share_cu_mask=False))
+    assert "HSA_CU_MASK" not in off._container_response([4, 5], {}).envs

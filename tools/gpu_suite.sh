@@ -32,6 +32,17 @@ case "$mode" in
     step prof_bench 600 rocprofv3 --kernel-trace --stats -d "$out/prof_bench" -o run -- python3 bench.py --steps 5 --warmup 2 --sweep off
     step prof_probe 600 rocprofv3 --kernel-trace --stats -d "$out/prof_probe" -o run -- python3 -m gpu_topology_on_k8s_amd probe --preset full
     ;;
+  cumask)
+    # MFMA rate and HBM copy under HSA_CU_MASK (the time-sliced shares' spatial split, profiles/r02_cumask)
+    for m in "" "0:0-127" "0:0-63" "0:0-31,128-159"; do
+      echo "mask=[$m]" >> "$out/cumask.log"
+      HSA_CU_MASK="$m" timeout -k 10 60 python -c 'import json
+from gpu_topology_on_k8s_amd.ops import probe
+w = probe.warmup(0, 200.0)
+c = probe.copy_bw(0, 0, 512 << 20, 5, 1)
+print(json.dumps({"tflops": round(float(w["tflops"]), 1), "hbm_copy_gbps": round(float(c["gbps"]), 1)}))' >> "$out/cumask.log" 2>&1 || exit 1
+    done
+    ;;
   *) echo "unknown mode $mode"; exit 2 ;;
 esac
 echo "[gpu_suite] done"
