@@ -183,6 +183,15 @@ __global__ __launch_bounds__(kBlock) void mfma_warmup_kernel(float* __restrict__
   out[(size_t)blockIdx.x * kBlock + threadIdx.x] = s;
 }
 
+// Where a workgroup runs: its XCD (HW_REG_XCC_ID[3:0]) and the low half of HW_REG_HW_ID (wave, SIMD,
+// CU, SH, SE).  Lane 0 writes one word per workgroup with an ordinary vector store.  Shows how a queue
+// CU mask (HSA_CU_MASK, time-sliced shares in topology/shares.py) spreads over the 8 XCDs.
+__global__ __launch_bounds__(64) void xcc_census_kernel(unsigned int* __restrict__ out) {
+  const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xFu;  // hwreg(HW_REG_XCC_ID, 0, 4)
+  const unsigned hw = __builtin_amdgcn_s_getreg((15 << 11) | 4);          // hwreg(HW_REG_HW_ID, 0, 16)
+  if (threadIdx.x == 0) out[blockIdx.x] = (xcc << 16) | (hw & 0xFFFFu);
+}
+
 // ---------------------------------------------------------------------------------------------
 struct DeviceGuard {
   int prev = 0;
@@ -538,6 +547,26 @@ std::vector<std::vector<double>> probe_matrix(const std::vector<int>& devs, size
   return m;
 }
 
+// XCDs the workgroups of one census launch ran on (on the null stream: the process's own CU mask,
+// e.g. HSA_CU_MASK), as {xcc: workgroups}.
+py::dict xcc_census(int dev, int blocks) {
+  std::vector<unsigned int> host(blocks);
+  {
+    py::gil_scoped_release nogil;
+    DeviceGuard g(dev);
+    DevBuf out(dev, (size_t)blocks * sizeof(unsigned int));
+    hipLaunchKernelGGL(xcc_census_kernel, dim3(blocks), dim3(64), 0, 0, (unsigned int*)out.p);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpy(host.data(), out.p, (size_t)blocks * sizeof(unsigned int), hipMemcpyDeviceToHost));
+  }
+  py::dict r;
+  for (unsigned int w : host) {
+    py::int_ k((int)(w >> 16));
+    r[k] = (r.contains(k) ? r[k].cast<int>() : 0) + 1;
+  }
+  return r;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_probe, m) {
@@ -554,6 +583,7 @@ PYBIND11_MODULE(_probe, m) {
   m.def("probe_matrix", &probe_matrix, py::arg("devs"), py::arg("bytes") = (size_t)256 << 20, py::arg("iters") = 5,
         py::arg("warmup") = 1, py::arg("mode") = "read", py::arg("kind") = "lds", py::arg("nontemporal") = false,
         py::arg("blocks_per_cu") = kBlocksPerCU, py::call_guard<py::gil_scoped_release>());
+  m.def("xcc_census", &xcc_census, py::arg("dev"), py::arg("blocks") = 4096);
   m.attr("BLOCK") = kBlock;
   m.attr("UNROLL") = kUnroll;
   m.attr("BLOCKS_PER_CU") = kBlocksPerCU;

@@ -17,7 +17,8 @@ of GPU ``i``), so
   units, and Allocate hands a pod holding part of a GPU ``HSA_CU_MASK`` with its slices' CUs, so the
   ROCm runtime creates every queue of the container on those CUs only: pods sharing a GPU run on
   disjoint CUs (spatial sharing; on MI355X a half mask gives 53 % of the MFMA rate, a quarter 27 %,
-  ``profiles/r02_cumask/``).  Like the HBM cap this is cooperative — a container can rewrite its own
+  ``profiles/r02_cumask/``; the mask is applied symmetrically over the 8 XCDs, so the pods share the
+  L2s).  Like the HBM cap this is cooperative — a container can rewrite its own
   environment — so it keeps well-behaved neighbours apart rather than confining a hostile one.  HBM is shared: the training entry point caps its caching allocator at
   the share (``torch.cuda.set_per_process_memory_fraction``, ``models/train.py``).  CPX/DPX
   partitions remain the form with isolated HBM and L2.
@@ -90,9 +91,10 @@ def time_slice(topo: Topology, slices: int) -> Topology:
     mx = probe.get("amdsmi_max_bw_mbps")
     if mx is not None and np.asarray(mx).shape == (n, n):
         probe["amdsmi_max_bw_mbps"] = expand(np.asarray(mx, dtype=np.float64)).tolist()
-    ing = probe.get("ingress_all_gbps")
-    if isinstance(ing, list) and len(ing) == n:
-        probe["ingress_all_gbps"] = [ing[int(p)] for p in phys]
+    for key in ("ingress_all_gbps",):  # per-device lists follow their GPU
+        vals = probe.get(key)
+        if isinstance(vals, list) and len(vals) == n:
+            probe[key] = [vals[int(p)] for p in phys]
     probe["time_slices"] = s
     out = Topology(
         gpus=gpus, link_type=lt, hops=hops, weight=weight, bw_gbps=bw,
@@ -122,7 +124,10 @@ def share_fractions(topo: Topology, ids: Sequence[int]) -> Dict[int, float]:
 
 
 def slice_cus(topo: Topology, index: int) -> List[int]:
-    """Compute units owned by time slice ``index``: the ``j``-th of ``S`` equal runs of its GPU's CUs."""
+    """Compute units owned by time slice ``index``: the ``j``-th of ``S`` equal runs of its GPU's CU
+    indices.  On MI355X the runtime applies a queue CU mask symmetrically over the 8 XCDs (workgroups
+    are dealt to every XCD whatever the mask: ``tests/test_gpu_shares.py``), so any ``c`` indices are
+    ``c`` CUs spread over all XCDs, and a slice cannot own an XCD's L2; equal runs are as good as any."""
     g = topo.gpus[int(index)]
     s = max(1, int(g.shares))
     c = int(g.cus) if int(g.cus) > 0 else DEFAULT_CUS

@@ -126,3 +126,32 @@ def test_cu_masked_shares_split_the_compute_units():
     assert 0.15 < alone["quarter"] / full < 0.4 and 0.6 < alone["three-quarters"] / full < 0.95
     for n in envs:
         assert together[n] > 0.8 * alone[n], (n, together, alone)
+
+
+_CENSUS = r"""
+import json
+from gpu_topology_on_k8s_amd._native import load
+print(json.dumps({str(k): v for k, v in load("_probe").xcc_census(0, 4096).items()}))
+"""
+
+
+def test_cu_masks_are_symmetric_over_the_xcds():
+    """What a share's HSA_CU_MASK does to workgroup placement: with every slice mask of a 4-slice
+    share, as with none, the census kernel finds 1/8 of the workgroups on each of the 8 XCDs — the
+    runtime keeps CUs on every XCD, so slices split each XCD's CUs and share the L2s (which is why
+    slice_cus uses plain index runs)."""
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
+    from gpu_topology_on_k8s_amd.topology.shares import cu_mask_env, time_slice
+
+    v = time_slice(discover("auto"), 4)
+    rows = []
+    for mask in [""] + [cu_mask_env(v, [j]) for j in range(4)]:
+        env = {k: val for k, val in os.environ.items() if k not in _STRIP and k != "HSA_CU_MASK"}
+        if mask:
+            env["HSA_CU_MASK"] = mask
+        p = subprocess.run([sys.executable, "-c", _CENSUS], capture_output=True, text=True, cwd=REPO, timeout=120, env=env)
+        assert p.returncode == 0, p.stderr[-2000:]
+        got = {int(k): n for k, n in json.loads(p.stdout.strip().splitlines()[-1]).items()}
+        rows.append({"mask": mask, "workgroups_per_xcd": got})
+        assert sorted(got) == list(range(8)) and set(got.values()) == {512}, (mask, got)
+    print(json.dumps(rows))
