@@ -465,7 +465,7 @@ def main(argv=None) -> int:
             with open(path) as f:
                 rccl = rccl_log_summary(f.read())
             rccl["log"] = path
-        except OSError as e:
+        except Exception as e:  # noqa: BLE001 - supplementary: never costs the headline line
             rccl = {"error": str(e)[:200]}
     if env.rank == 0:
         bound = (choice.extra.get("probe") or {}).get("subset_ingress_bound_gbps")  # K5/K1 ceiling of busBW
