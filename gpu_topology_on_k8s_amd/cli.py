@@ -26,8 +26,14 @@ def _topology(a):
 
     if getattr(a, "topology", None):
         with open(a.topology) as f:
-            return Topology.from_json(f.read())
-    return discover(a.discovery, fake_n=a.fake_gpus)
+            t = Topology.from_json(f.read())
+    else:
+        t = discover(a.discovery, fake_n=a.fake_gpus)
+    if getattr(a, "time_slices", 1) > 1:  # what a device plugin run with --time-slices advertises
+        from .topology.shares import time_slice
+
+        t = time_slice(t, a.time_slices)
+    return t
 
 
 def _ints(s: Optional[str]) -> List[int]:
@@ -74,6 +80,25 @@ def cmd_select(a) -> int:
 
     t = _topology(a)
     used = _ints(a.used)
+    if a.fraction:
+        # a fraction of ONE GPU: XCP partitions (CPX/DPX/QPX) or time slices, Gaia Fragment best fit
+        import math
+
+        from .placement import place_fraction
+        from .topology.shares import cu_mask_env, share_fractions
+
+        per = max(int((t.physical == p).sum()) for p in set(t.physical.tolist()))
+        k = max(1, math.ceil(a.fraction * per - 1e-9))
+        ids = place_fraction(t, k, used)
+        out = {"ids": list(ids), "policy": "fragment", "devices_per_gpu": per,
+               "gpu": int(t.gpus[ids[0]].physical), "share": round(share_fractions(t, ids)[int(t.gpus[ids[0]].physical)], 4)}
+        if cu_mask_env(t, ids):
+            out["hsa_cu_mask"] = cu_mask_env(t, ids)
+        print(json.dumps(out))
+        return 0
+    if a.k <= 0:
+        print("gtk select: give -k N (devices) or --fraction m", file=sys.stderr)
+        return 2
     if a.policy == "gaia":
         ids = gaia_schedule(tree_from_topology(t, used), a.k)
         print(json.dumps({"ids": ids, "policy": "gaia"}))
@@ -184,6 +209,7 @@ def main(argv=None) -> int:
         p.add_argument("--discovery", default="auto", choices=["auto", "amdsmi", "sysfs", "fake"])
         p.add_argument("--fake-gpus", type=int, default=None)
         p.add_argument("--topology", default="", help="topology JSON file instead of discovery")
+        p.add_argument("--time-slices", type=int, default=1, help="view every GPU as this many time slices (device plugin --time-slices)")
 
     p = sub.add_parser("topo")
     disc(p)
@@ -199,7 +225,9 @@ def main(argv=None) -> int:
     p.set_defaults(fn=cmd_probe)
     p = sub.add_parser("select")
     disc(p)
-    p.add_argument("-k", type=int, required=True)
+    p.add_argument("-k", type=int, default=0)
+    p.add_argument("--fraction", type=float, default=0.0,
+                   help="0 < m < 1 of one GPU (Gaia Fragment) on a partitioned or --time-slices node, instead of -k")
     p.add_argument("--used", default="")
     p.add_argument("--policy", default="exact", choices=["exact", "gaia"])
     p.add_argument("--worst", action="store_true")

@@ -64,6 +64,8 @@ def test_cli_topo_select_config():
     g = json.loads(_cli("select", "--discovery", "fake", "--fake-gpus", "8", "-k", "2", "--policy", "gaia"))
     assert len(g["ids"]) == 2
     assert json.loads(_cli("config", "policy"))["kind"] == "Policy"
+    fr = json.loads(_cli("select", "--discovery", "fake", "--fake-gpus", "4", "--time-slices", "4", "--fraction", "0.25", "--used", "8,9"))
+    assert fr["gpu"] == 2 and fr["ids"] == [10] and fr["share"] == 0.25 and fr["hsa_cu_mask"] == "0:128-191"
 
 
 def test_cli_sim():
