@@ -113,6 +113,22 @@ def cmd_select(a) -> int:
     return 0
 
 
+def cmd_defrag(a) -> int:
+    """Plan the fewest pod moves after which a k-GPU pod fits (placement/defrag.py) from the
+    apiserver's nodes and pods; prints the plan, changes nothing."""
+    from .deviceplugin.__main__ import make_api
+    from .extender import ExtenderConfig, TopologyExtender
+    from .k8s.annotations import Contract
+
+    api = make_api(a.apiserver, a.token, a.ca_file, a.insecure_skip_tls_verify)
+    if api is None:
+        print("gtk defrag: no apiserver (--apiserver URL, or run in a cluster)", file=sys.stderr)
+        return 2
+    ext = TopologyExtender(api, ExtenderConfig(contract=Contract(resource_name=a.resource_name), resync_s=0.0, events=False))
+    print(json.dumps({"gpus": a.k, "plan": ext.defrag(a.k, a.max_moves)}))
+    return 0
+
+
 def cmd_config(a) -> int:
     from .config import legacy_policy, render_manifests, scheduler_configuration
 
@@ -232,6 +248,15 @@ def main(argv=None) -> int:
     p.add_argument("--policy", default="exact", choices=["exact", "gaia"])
     p.add_argument("--worst", action="store_true")
     p.set_defaults(fn=cmd_select)
+    p = sub.add_parser("defrag", help="plan pod moves that make a k-GPU pod placeable (read-only)")
+    p.add_argument("-k", type=int, default=8)
+    p.add_argument("--max-moves", type=int, default=3)
+    p.add_argument("--apiserver", default="")
+    p.add_argument("--token", default="")
+    p.add_argument("--ca-file", default="")
+    p.add_argument("--insecure-skip-tls-verify", action="store_true")
+    p.add_argument("--resource-name", default="amd.com/gpu")
+    p.set_defaults(fn=cmd_defrag)
     p = sub.add_parser("config")
     p.add_argument("kind", choices=["scheduler", "policy", "manifests", "kind"])
     p.add_argument("--out-dir", default="", help="kind: write every file of deploy/kind/ here")

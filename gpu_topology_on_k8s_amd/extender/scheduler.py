@@ -484,6 +484,29 @@ class TopologyExtender:
         self.metrics.observe("preempt", time.perf_counter() - t0)
         return out
 
+    def defrag(self, k: int, max_moves: int = 3) -> Optional[Dict[str, object]]:
+        """Operator view (``GET <prefix>/defrag?gpus=k``, ``gtk defrag``): the fewest pod moves after
+        which a ``k``-device pod fits well on some node (:func:`placement.defrag.plan_defrag`), planned
+        on the cache's current view.  Nodes carrying pods whose devices are unknown (no GROUP
+        annotation) are left out: their used sets are not exact."""
+        from ..placement.defrag import plan_defrag
+
+        if not self.cache.informed():
+            self.cache.sync_all()
+        now = self.clock()
+        nodes: Dict[str, Topology] = {}
+        pods: Dict[str, Dict[str, Tuple[int, ...]]] = {}
+        for st in self.cache.nodes():
+            name = st.name
+            with st.lock:
+                if st.topology is None or st.unknown:
+                    continue
+                nodes[name] = st.topology
+                pods[name] = {a.pod: tuple(a.ids) for a in st.allocs.values()
+                              if a.assigned or now - a.assume_time <= self.cfg.assume_ttl}
+        plan = plan_defrag(nodes, pods, k, self.cfg.policy, max_moves=max_moves)
+        return None if plan is None else plan.to_dict()
+
     def _patch_with_retry(self, namespace: str, name: str, ann: Dict[str, str]) -> None:
         last: Optional[Exception] = None
         for attempt in range(max(1, self.cfg.bind_retries)):

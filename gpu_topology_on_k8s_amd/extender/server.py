@@ -8,7 +8,8 @@ Reference endpoint (``design.md:98-100``): ``http://127.0.0.1:32743/gputopology-
   POST {prefix}/filter      ExtenderArgs -> ExtenderFilterResult       (optional)
   POST {prefix}/bind        ExtenderBindingArgs -> ExtenderBindingResult
   POST {prefix}/preempt     ExtenderPreemptionArgs -> ExtenderPreemptionResult (topology-aware victims)
-  GET  {prefix}/healthz, /metrics (Prometheus text), /version, /debug/nodes (cache snapshot)
+  GET  {prefix}/healthz, /metrics (Prometheus text), /version, /debug/nodes (cache snapshot),
+       /defrag?gpus=k (the fewest pod moves after which a k-GPU pod fits well: placement/defrag.py)
 
 kube-scheduler marshals Go structs without json tags, so request keys are capitalised (``Pod``,
 ``Nodes``, ``NodeNames``, ``PodName`` ...); Go's decoder matches keys case-insensitively, so the
@@ -149,6 +150,14 @@ def make_app(ext: TopologyExtender, prefix: str = DEFAULT_PREFIX, workers: int =
     async def version(request: web.Request) -> web.Response:
         return web.json_response({"version": __version__, "policy": ext.cfg.policy_name, "resource": ext.cfg.contract.resource_name})
 
+    async def defrag(request: web.Request) -> web.Response:
+        try:
+            k = int(request.query.get("gpus", "8"))
+            moves = int(request.query.get("max_moves", "3"))
+        except ValueError:
+            return web.json_response({"error": "gpus and max_moves must be integers"}, status=400)
+        return web.json_response({"gpus": k, "plan": await run_blocking(ext.defrag, k, moves)})
+
     async def debug_nodes(request: web.Request) -> web.Response:
         return web.json_response(await run_blocking(ext.cache.snapshot))
 
@@ -167,6 +176,7 @@ def make_app(ext: TopologyExtender, prefix: str = DEFAULT_PREFIX, workers: int =
     app.router.add_get("/metrics", metrics)
     app.router.add_get(f"{prefix}/version", version)
     app.router.add_get(f"{prefix}/debug/nodes", debug_nodes)
+    app.router.add_get(f"{prefix}/defrag", defrag)
     app.on_cleanup.append(on_cleanup)
     app[EXTENDER_KEY] = ext
     return app
