@@ -151,7 +151,7 @@ def cmd_config(a) -> int:
     elif a.kind == "scheduler":
         print(yaml.safe_dump(scheduler_configuration(a.resource_name, with_filter=a.filter), sort_keys=False), end="")
     else:
-        print(render_manifests(a.resource_name, image=a.image), end="")
+        print(render_manifests(a.resource_name, image=a.image, time_slices=a.time_slices), end="")
     return 0
 
 
@@ -263,6 +263,7 @@ def main(argv=None) -> int:
     p.add_argument("--resource-name", default="amd.com/gpu")
     p.add_argument("--filter", action="store_true")
     p.add_argument("--image", default="rocm/gpu-topology-k8s:latest")
+    p.add_argument("--time-slices", type=int, default=1, help="manifests: device plugin --time-slices (fractional GPUs on SPX nodes)")
     p.set_defaults(fn=cmd_config)
     p = sub.add_parser("validate")
     p.add_argument("--devices", default="", help="HIP ordinals (skips GROUP resolution)")

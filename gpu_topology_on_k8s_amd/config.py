@@ -76,7 +76,9 @@ def scheduler_configuration(resource: str = DEFAULT_RESOURCE, url: Optional[str]
 
 
 def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, namespace: str = NAMESPACE,
-                     probe: str = "quick", policy: str = "exact") -> str:
+                     probe: str = "quick", policy: str = "exact", time_slices: int = 1) -> str:
+    """The DaemonSets, RBAC and scheduler config.  ``time_slices > 1``: the device plugin advertises
+    every GPU as that many time slices (fractional pods; topology/shares.py)."""
     sa = "gpu-topology"
     labels = {"app.kubernetes.io/part-of": "gpu-topology-amd"}
     docs: List[Dict[str, Any]] = [
@@ -117,7 +119,8 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
                             "image": image,
                             "command": ["python3", "-m", "gpu_topology_on_k8s_amd.deviceplugin",
                                         f"--resource-name={resource}", f"--probe={probe}", "--discovery=auto",
-                                        "--reprobe-interval=3600", "--prestart-validate", f"--metrics-port={PLUGIN_METRICS_PORT}"],
+                                        "--reprobe-interval=3600", "--prestart-validate", f"--metrics-port={PLUGIN_METRICS_PORT}"]
+                                       + ([f"--time-slices={int(time_slices)}"] if int(time_slices) > 1 else []),
                             "ports": [{"containerPort": PLUGIN_METRICS_PORT, "name": "metrics"}],
                             "env": [{"name": "NODE_NAME", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}},
                                     {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}],

@@ -68,6 +68,15 @@ def test_cli_topo_select_config():
     assert fr["gpu"] == 2 and fr["ids"] == [10] and fr["share"] == 0.25 and fr["hsa_cu_mask"] == "0:128-191"
 
 
+def test_manifests_time_slices():
+    from gpu_topology_on_k8s_amd.config import render_manifests
+
+    docs = list(yaml.safe_load_all(render_manifests(time_slices=4)))
+    ds = [d for d in docs if d and d["kind"] == "DaemonSet" and "device-plugin" in d["metadata"]["name"]][0]
+    assert "--time-slices=4" in ds["spec"]["template"]["spec"]["containers"][0]["command"]
+    assert "--time-slices" not in render_manifests()
+
+
 def test_cli_sim():
     lines = [json.loads(l) for l in _cli("sim", "--nodes", "1", "--pods", "4,4").splitlines()]
     assert {tuple(l["devices"]) for l in lines} == {(0, 1, 2, 3), (4, 5, 6, 7)}
