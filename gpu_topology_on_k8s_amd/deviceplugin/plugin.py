@@ -529,7 +529,9 @@ class DevicePluginServer:
         if self.cfg.device_specs == "cdi":
             from .cdi import cdi_name
 
-            for i in ids:
+            # one name per physical device: time slices of a GPU share its nodes (topology/shares.py)
+            for i in dict.fromkeys(self._first_slice(self.topology.gpus[i].physical) if self.topology.gpus[i].shares > 1 else i
+                                   for i in ids):
                 r.cdi_devices.add(name=cdi_name(self.cfg.cdi_kind, i))
         for cpath, hpath in ([] if self.cfg.device_specs == "cdi" else self.device_nodes(ids)):
             if self.cfg.device_specs == "stub" and not os.path.exists(hpath):

@@ -144,3 +144,13 @@ def test_allocate_sets_cu_mask_after_pod_env(tmp_path):
     assert r.envs["HSA_CU_MASK"] == "0:0-127" and r.envs["NCCL_MIN_NCHANNELS"] == "8"
     off = DevicePluginServer(v, PluginConfig(device_specs="stub", dev_root=str(tmp_path), share_cu_mask=False))
     assert "HSA_CU_MASK" not in off._container_response([4, 5], {}).envs
+
+
+def test_cdi_mode_names_each_physical_gpu_once(tmp_path):
+    v = time_slice(fx.f7_mi355x(n=2), 4)
+    plug = DevicePluginServer(v, PluginConfig(device_specs="cdi", cdi_dir=str(tmp_path)))
+    r = plug._container_response([4, 5, 6], {})
+    assert [d.name for d in r.cdi_devices] == ["amd.com/gpu=4"] and r.envs["GTK_GPU_GROUP"] == "1"
+    r = plug._container_response([2, 3, 4], {})
+    assert [d.name for d in r.cdi_devices] == ["amd.com/gpu=0", "amd.com/gpu=4"]
+    assert r.envs["GTK_GPU_FRACTION"] == "0.5,0.25" and r.envs["HSA_CU_MASK"] == "0:128-255;1:0-63"
