@@ -140,3 +140,54 @@ def test_random_churn_on_cpx_nodes_with_fractions(seed):
             for key in frac & set(live):
                 ids = c.nodes[live[key]].kubelet.allocated[c.resource][key]
                 assert len({int(i) // 8 for i in ids}) == 1, (key, ids)
+
+
+@pytest.mark.parametrize("seed", [41, 42])
+def test_random_churn_on_time_sliced_nodes(seed):
+    """SPX nodes advertised as 4 time slices per GPU (topology/shares.py): fractional pods, whole-GPU
+    pods (4 slices each) and multi-GPU pods churn together; besides the invariants above every
+    fraction stays on one GPU, and every container got its share and disjoint CU masks."""
+    from gpu_topology_on_k8s_amd.k8s import Contract
+    from gpu_topology_on_k8s_amd.topology.shares import time_slice
+
+    C = Contract()
+    rng = random.Random(seed)
+    with SimCluster({"s0": time_slice(fx.f7_mi355x(), 4), "s1": time_slice(fx.f7_mi355x(), 4)}) as c:
+        live, request, frac, nxt = {}, {}, set(), 0
+        for _ in range(30):
+            if rng.random() < 0.6:
+                for _ in range(rng.randint(1, 4)):
+                    name = f"p{nxt}"
+                    nxt += 1
+                    if rng.random() < 0.5:
+                        f = rng.choice([0.25, 0.5, 0.75])
+                        c.submit(name, int(f * 4), annotations={C.fraction_key: str(f)})
+                        frac.add(f"default/{name}")
+                        request[f"default/{name}"] = int(f * 4)
+                    else:
+                        k = 4 * rng.choice([1, 2, 4])
+                        c.submit(name, k)
+                        request[f"default/{name}"] = k
+                for r in c.schedule_pending(concurrent=rng.random() < 0.3):
+                    if r.node and r.allocated:
+                        live[r.pod] = r.node
+            elif live:
+                key = rng.choice(sorted(live))
+                c.complete(key.split("/")[1])
+                live.pop(key)
+            _check(c, live, request)
+            masks = {}
+            for key in frac & set(live):
+                node = live[key]
+                ids = c.nodes[node].kubelet.allocated[c.resource][key]
+                gpus = {int(i) // 4 for i in ids}
+                assert len(gpus) == 1, (key, ids)
+                envs = dict(c.nodes[node].kubelet.responses[key].container_responses[0].envs)
+                assert float(envs["GTK_GPU_FRACTION"]) == request[key] / 4
+                cus = set()
+                for part in envs["HSA_CU_MASK"].split(":")[1].split(","):
+                    lo, _, hi = part.partition("-")
+                    cus |= set(range(int(lo), int(hi or lo) + 1))
+                prev = masks.setdefault((node, gpus.pop()), set())
+                assert not (prev & cus), (key, envs["HSA_CU_MASK"])  # neighbours on one GPU never share a CU
+                prev |= cus
