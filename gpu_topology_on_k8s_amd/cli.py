@@ -125,7 +125,7 @@ def cmd_defrag(a) -> int:
         print("gtk defrag: no apiserver (--apiserver URL, or run in a cluster)", file=sys.stderr)
         return 2
     ext = TopologyExtender(api, ExtenderConfig(contract=Contract(resource_name=a.resource_name), resync_s=0.0, events=False))
-    print(json.dumps({"gpus": a.k, "plan": ext.defrag(a.k, a.max_moves)}))
+    print(json.dumps({"gpus": a.k, "plan": ext.defrag(a.k, a.max_moves, a.min_score)}))
     return 0
 
 
@@ -251,6 +251,7 @@ def main(argv=None) -> int:
     p = sub.add_parser("defrag", help="plan pod moves that make a k-GPU pod placeable (read-only)")
     p.add_argument("-k", type=int, default=8)
     p.add_argument("--max-moves", type=int, default=3)
+    p.add_argument("--min-score", type=float, default=0.0, help="only placements scoring at least this (0..10) count")
     p.add_argument("--apiserver", default="")
     p.add_argument("--token", default="")
     p.add_argument("--ca-file", default="")

@@ -484,7 +484,7 @@ class TopologyExtender:
         self.metrics.observe("preempt", time.perf_counter() - t0)
         return out
 
-    def defrag(self, k: int, max_moves: int = 3) -> Optional[Dict[str, object]]:
+    def defrag(self, k: int, max_moves: int = 3, min_score: float = 0.0) -> Optional[Dict[str, object]]:
         """Operator view (``GET <prefix>/defrag?gpus=k``, ``gtk defrag``): the fewest pod moves after
         which a ``k``-device pod fits well on some node (:func:`placement.defrag.plan_defrag`), planned
         on the cache's current view.  Nodes carrying pods whose devices are unknown (no GROUP
@@ -504,7 +504,7 @@ class TopologyExtender:
                 nodes[name] = st.topology
                 pods[name] = {a.pod: tuple(a.ids) for a in st.allocs.values()
                               if a.assigned or now - a.assume_time <= self.cfg.assume_ttl}
-        plan = plan_defrag(nodes, pods, k, self.cfg.policy, max_moves=max_moves)
+        plan = plan_defrag(nodes, pods, k, self.cfg.policy, max_moves=max_moves, min_score=min_score)
         return None if plan is None else plan.to_dict()
 
     def _patch_with_retry(self, namespace: str, name: str, ann: Dict[str, str]) -> None:

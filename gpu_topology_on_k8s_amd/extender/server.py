@@ -154,9 +154,10 @@ def make_app(ext: TopologyExtender, prefix: str = DEFAULT_PREFIX, workers: int =
         try:
             k = int(request.query.get("gpus", "8"))
             moves = int(request.query.get("max_moves", "3"))
+            min_score = float(request.query.get("min_score", "0"))
         except ValueError:
-            return web.json_response({"error": "gpus and max_moves must be integers"}, status=400)
-        return web.json_response({"gpus": k, "plan": await run_blocking(ext.defrag, k, moves)})
+            return web.json_response({"error": "gpus, max_moves and min_score must be numbers"}, status=400)
+        return web.json_response({"gpus": k, "plan": await run_blocking(ext.defrag, k, moves, min_score)})
 
     async def debug_nodes(request: web.Request) -> web.Response:
         return web.json_response(await run_blocking(ext.cache.snapshot))

@@ -71,12 +71,14 @@ def _place(t: Topology, k: int, used: Sequence[int], policy: PlacementPolicy):
 
 def plan_defrag(nodes: Dict[str, Topology], pods: Dict[str, Dict[str, Tuple[int, ...]]], k: int,
                 policy: Optional[PlacementPolicy] = None, max_moves: int = 3,
-                movable: Optional[Sequence[str]] = None) -> Optional[DefragPlan]:
+                movable: Optional[Sequence[str]] = None, min_score: float = 0.0) -> Optional[DefragPlan]:
     """The cheapest plan that makes a ``k``-device pod placeable, or None.
 
     ``nodes``: node -> topology; ``pods``: node -> {pod key: device ids it holds} (every pod holding
-    devices, so the used sets are exact); ``movable``: pod keys that may be moved (default: all).
-    A plan with no moves means the pod already fits (its best node is returned)."""
+    devices, so the used sets are exact); ``movable``: pod keys that may be moved (default: all);
+    ``min_score``: a placement only counts when its 0..10 score reaches this (e.g. the score of a
+    NUMA-local set, so moves are planned for *good* placements, not just any).  A plan with no moves
+    means the pod already fits (its best node is returned)."""
     policy = policy or PlacementPolicy()
     movable_set = None if movable is None else set(movable)
     names = [n for n in sorted(nodes) if _whole_devices(nodes[n])]
@@ -88,9 +90,12 @@ def plan_defrag(nodes: Dict[str, Topology], pods: Dict[str, Dict[str, Tuple[int,
             return True
         return (p.moved_devices, len(p.moves), p.objective) < (best.moved_devices, len(best.moves), best.objective)
 
+    def good(pl) -> bool:
+        return pl is not None and pl.score >= min_score - 1e-9
+
     for n in names:  # already placeable: no moves
         pl = _place(nodes[n], k, used[n], policy)
-        if pl is not None:
+        if good(pl):
             cand = DefragPlan(n, tuple(pl.ids), pl.objective, pl.score)
             if better(cand):
                 best = cand
@@ -106,7 +111,7 @@ def plan_defrag(nodes: Dict[str, Topology], pods: Dict[str, Dict[str, Tuple[int,
                 break
             freed = {i for _, ids in sub for i in ids}
             pl = _place(t, k, used[n] - freed, policy)
-            if pl is None:
+            if not good(pl):
                 continue
             # re-place the moved pods on the other nodes, largest first, each on its best node
             trial = {m: set(u) for m, u in used.items() if m != n}

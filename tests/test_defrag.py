@@ -91,3 +91,16 @@ def test_extender_endpoint_and_cli():
         srv.shutdown()
     assert p.returncode == 0, p.stderr
     assert json.loads(p.stdout)["plan"]["node"] == "n0"
+
+
+def test_min_score_plans_for_a_numa_local_set():
+    """Two 1-GPU pods, one on each NUMA half of n0: a 4-GPU pod fits (1,2,3,5) but spans both halves;
+    asking for the score of a NUMA-local set moves one small pod to n1 and frees 0-3."""
+    from gpu_topology_on_k8s_amd.placement import select
+
+    pods = {"n0": {"a": (0,), "b": (4,)}, "n1": {"c": tuple(range(6))}}
+    assert plan_defrag(_nodes(), pods, 4).moves == []
+    local = select(fx.f7_mi355x(), 4).score
+    plan = plan_defrag(_nodes(), pods, 4, min_score=local)
+    assert plan.node == "n0" and plan.moved_devices == 1 and plan.score >= local
+    assert {fx.f7_mi355x().gpus[i].numa for i in plan.ids} == {plan.moves[0].src_ids[0] // 4}
