@@ -155,3 +155,21 @@ def test_cu_masks_are_symmetric_over_the_xcds():
         rows.append({"mask": mask, "workgroups_per_xcd": got})
         assert sorted(got) == list(range(8)) and set(got.values()) == {512}, (mask, got)
     print(json.dumps(rows))
+
+
+def test_prestart_validation_of_a_fractional_pod():
+    """Flow step 8 for a 0.5 pod on the time-sliced real node: the RCCL validation runs once over the
+    physical GPU behind the pod's two slices and is recorded on the pod."""
+    from gpu_topology_on_k8s_amd.k8s import Contract
+    from gpu_topology_on_k8s_amd.sim import SimCluster
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
+    from gpu_topology_on_k8s_amd.topology.shares import time_slice
+
+    t = discover("auto")
+    t.node_name = "gpu-node"
+    with SimCluster({"gpu-node": time_slice(t, 4)}, prestart_validate=True) as c:
+        c.submit("half", 2, annotations={Contract().fraction_key: "0.5"})
+        r = c.schedule_pending()[0]
+        assert r.error == "" and len(r.allocated) == 2
+        v = json.loads(c.api.get_pod("default", "half")["metadata"]["annotations"][Contract().validated_key])
+        assert v["k"] == 1 and v["peak_algbw_gbps"] > 100
