@@ -129,6 +129,48 @@ def cmd_defrag(a) -> int:
     return 0
 
 
+def cmd_status(a) -> int:
+    """Per-node GPU view from the apiserver, as the extender sees it: devices, used, free,
+    fragmentation index, and the best placement score for each request size (or '-' if none fits)."""
+    from .deviceplugin.__main__ import make_api
+    from .extender import ExtenderConfig, TopologyExtender
+    from .extender.metrics import node_fragmentation
+    from .k8s.annotations import Contract
+    from .topology.shares import slices_per_gpu
+
+    api = make_api(a.apiserver, a.token, a.ca_file, a.insecure_skip_tls_verify)
+    if api is None:
+        print("gtk status: no apiserver (--apiserver URL, or run in a cluster)", file=sys.stderr)
+        return 2
+    ext = TopologyExtender(api, ExtenderConfig(contract=Contract(resource_name=a.resource_name), resync_s=0.0, events=False))
+    ext.cache.sync_all()
+    sizes = _ints(a.sizes)
+    rows = []
+    now = ext.clock()
+    for st in sorted(ext.cache.nodes(), key=lambda s: s.name):
+        with st.lock:
+            t = st.topology
+            if t is None:
+                continue
+            used = st.used(now, ext.cfg.assume_ttl)
+            free, frag, _ = node_fragmentation(t, used, st.unknown)
+            row = {"node": st.name, "devices": t.n, "per_gpu": slices_per_gpu(t) if slices_per_gpu(t) > 1 else 1,
+                   "used": len(used) + st.unknown, "free": free, "fragmentation": round(frag, 3), "best_score": {}}
+        for k in sizes:
+            d, _ = ext._eval_state({"metadata": {"name": "status", "namespace": "default"}, "spec": {}}, st.name, st, k)
+            row["best_score"][str(k)] = None if d is None else round(d.score, 2)
+        rows.append(row)
+    if a.output == "json":
+        print(json.dumps(rows))
+        return 0
+    head = f"{'NODE':<20}{'DEV':>5}{'USED':>6}{'FREE':>6}{'FRAG':>7}  " + "  ".join(f"k={k:<4}" for k in sizes)
+    print(head)
+    for r in rows:
+        cells = "  ".join(f"{('-' if r['best_score'][str(k)] is None else format(r['best_score'][str(k)], '.2f')):<6}" for k in sizes)
+        print(f"{r['node']:<20}{r['devices']:>5}{r['used']:>6}{r['free']:>6}{r['fragmentation']:>7.3f}  {cells}")
+    return 0
+
+
 def cmd_config(a) -> int:
     from .config import legacy_policy, render_manifests, scheduler_configuration
 
@@ -258,6 +300,15 @@ def main(argv=None) -> int:
     p.add_argument("--insecure-skip-tls-verify", action="store_true")
     p.add_argument("--resource-name", default="amd.com/gpu")
     p.set_defaults(fn=cmd_defrag)
+    p = sub.add_parser("status", help="per-node GPU usage, fragmentation and best placement score per size (read-only)")
+    p.add_argument("--sizes", default="1,2,4,8")
+    p.add_argument("--output", default="table", choices=["table", "json"])
+    p.add_argument("--apiserver", default="")
+    p.add_argument("--token", default="")
+    p.add_argument("--ca-file", default="")
+    p.add_argument("--insecure-skip-tls-verify", action="store_true")
+    p.add_argument("--resource-name", default="amd.com/gpu")
+    p.set_defaults(fn=cmd_status)
     p = sub.add_parser("config")
     p.add_argument("kind", choices=["scheduler", "policy", "manifests", "kind"])
     p.add_argument("--out-dir", default="", help="kind: write every file of deploy/kind/ here")

@@ -104,3 +104,23 @@ def test_min_score_plans_for_a_numa_local_set():
     plan = plan_defrag(_nodes(), pods, 4, min_score=local)
     assert plan.node == "n0" and plan.moved_devices == 1 and plan.score >= local
     assert {fx.f7_mi355x().gpus[i].numa for i in plan.ids} == {plan.moves[0].src_ids[0] // 4}
+
+
+def test_gtk_status_reports_usage_and_scores():
+    api = FakeAPIServer()
+    for n in ("n0", "n1"):
+        api.create_node(make_node(n, annotations=encode_node_annotations(fx.f7_mi355x(), C), capacity={C.resource_name: "8"}))
+    api.create_pod(make_pod("a", gpus=2, node="n0", annotations=PodAssignment([0, 4], True, 1).to_annotations()))
+    srv, url = serve_http(api)
+    try:
+        p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd", "status", "--apiserver", url, "--output", "json"],
+                           capture_output=True, text=True, timeout=120)
+        q = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd", "status", "--apiserver", url],
+                           capture_output=True, text=True, timeout=120)
+    finally:
+        srv.shutdown()
+    assert p.returncode == 0, p.stderr
+    rows = {r["node"]: r for r in json.loads(p.stdout)}
+    assert rows["n0"]["used"] == 2 and rows["n0"]["free"] == 6 and rows["n1"]["free"] == 8
+    assert rows["n0"]["best_score"]["8"] is None and rows["n1"]["best_score"]["8"] is not None
+    assert q.returncode == 0 and q.stdout.splitlines()[0].startswith("NODE") and "n1" in q.stdout
