@@ -46,7 +46,11 @@ def _init_dist(device_kind: str) -> Dict[str, int]:
         os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     if not dist.is_initialized():
-        dist.init_process_group(backend="nccl" if device_kind == "cuda" else "gloo")
+        # rehearsal (GTK_REHEARSE_ON_ONE_GPU=1): every rank on the one visible GPU, collectives over
+        # gloo (RCCL refuses two ranks on one device) — the multi-rank DP / ZeRO-1 GPU code paths run
+        # on a single-GPU box; production runs one rank per GPU over RCCL
+        rehearse = device_kind == "cuda" and os.environ.get("GTK_REHEARSE_ON_ONE_GPU") == "1"
+        dist.init_process_group(backend="gloo" if rehearse or device_kind != "cuda" else "nccl")
     return {"rank": rank, "world": world, "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}
 
 
@@ -108,6 +112,11 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         torch.cuda.set_device(dev)
         pl["hbm_cap_fraction"] = apply_share_cap(pl, env["rank"], dev)
         device = torch.device("cuda", dev)
+        gemm_mode = setup_gemm_tuning(gemm_tuning, gemm_table, env["rank"])
+    elif device_kind == "cuda" and os.environ.get("GTK_REHEARSE_ON_ONE_GPU") == "1":
+        pl = {"devices": [0] * env["world"], "hip_devices": [0] * env["world"], "best": [0], "worst": None, "source": "rehearsal"}
+        torch.cuda.set_device(0)
+        device = torch.device("cuda", 0)
         gemm_mode = setup_gemm_tuning(gemm_tuning, gemm_table, env["rank"])
     elif device_kind == "cuda":
         pl = _choose_device(env, placement, discovery)
