@@ -97,15 +97,22 @@ def time_slice(topo: Topology, slices: int) -> Topology:
             probe[key] = [vals[int(p)] for p in phys]
     probe["time_slices"] = s
     out = Topology(
-        gpus=gpus, link_type=lt, hops=hops, weight=weight, bw_gbps=bw,
-        cost=None if topo.ref_class is None else expand(topo.cost),
+        gpus=gpus, link_type=lt, hops=hops, weight=weight, bw_gbps=bw, cost=None,
         ref_gbps=topo.ref_gbps, node_name=topo.node_name, source=topo.source, probe=probe,
         ref_class=expand(topo.ref_class), hbm_gbps=hbm,
         numa_distance=copy.deepcopy(topo.numa_distance), nics=copy.deepcopy(topo.nics),
         gpu_nic=None if topo.gpu_nic is None else [list(topo.gpu_nic[int(p)]) for p in phys],
     )
-    if out.ref_class is not None:  # fixtures priced by reference class: same GPU = the cheapest pair
-        out.cost[same & ~np.eye(out.n, dtype=bool)] = 0.0
+    derived = copy.deepcopy(topo)
+    derived.recompute_cost()
+    if not np.allclose(derived.cost, topo.cost):
+        # explicitly priced topology (fixtures, reference trees): keep its pair costs between GPUs;
+        # slices of one GPU stay at the cheapest cost the recomputation gave them
+        cross = ~same
+        cost = out.cost.copy()
+        cost[cross] = expand(topo.cost)[cross]
+        out.cost = np.round(np.maximum(cost, cost.T), 6)
+        out.validate()
     return out
 
 

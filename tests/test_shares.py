@@ -154,3 +154,19 @@ def test_cdi_mode_names_each_physical_gpu_once(tmp_path):
     r = plug._container_response([2, 3, 4], {})
     assert [d.name for d in r.cdi_devices] == ["amd.com/gpu=0", "amd.com/gpu=4"]
     assert r.envs["GTK_GPU_FRACTION"] == "0.5,0.25" and r.envs["HSA_CU_MASK"] == "0:128-255;1:0-63"
+
+
+def test_time_slice_keeps_explicit_pair_costs():
+    """A topology priced explicitly (the paper's PCIe tree, F4 costs) keeps those costs between GPUs;
+    slices of one GPU are the cheapest pairs."""
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench"))
+    import cluster_trace as ct
+
+    t = ct._tree_node(0)
+    v = time_slice(t, 2)
+    for a in range(8):
+        for b in range(8):
+            if a != b:
+                assert v.cost[2 * a, 2 * b + 1] == pytest.approx(t.cost[a, b])
+    assert v.cost[0, 1] < v.cost[0, 2]
