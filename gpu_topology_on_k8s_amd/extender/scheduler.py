@@ -144,6 +144,23 @@ class TopologyExtender:
             raise ValueError(f"{self.cfg.contract.fraction_key} must be in (0, 1), got {raw!r}")
         return m
 
+    def memory_of(self, pod: Dict[str, Any]) -> Optional[int]:
+        """``<prefix>/gpu-memory`` in bytes ("96Gi", "100G", "1e11") or None; malformed values raise ValueError."""
+        raw = obj_annotations(pod).get(self.cfg.contract.memory_key)
+        if raw is None or str(raw).strip() == "":
+            return None
+        txt = str(raw).strip()
+        units = {"Ki": 2**10, "Mi": 2**20, "Gi": 2**30, "Ti": 2**40, "K": 10**3, "M": 10**6, "G": 10**9, "T": 10**12}
+        mult = 1
+        for u in sorted(units, key=len, reverse=True):
+            if txt.endswith(u):
+                txt, mult = txt[: -len(u)], units[u]
+                break
+        b = int(float(txt) * mult)
+        if b <= 0:
+            raise ValueError(f"{self.cfg.contract.memory_key} must be positive, got {raw!r}")
+        return b
+
     def numa_preference(self, pod: Dict[str, Any]) -> Optional[List[int]]:
         """NUMA node(s) the pod's host threads run on (``<prefix>/numa-preference: "1"``), if stated."""
         raw = obj_annotations(pod).get(self.cfg.contract.numa_pref_key)
@@ -226,11 +243,14 @@ class TopologyExtender:
         once per request; (None, reason) for a malformed fraction."""
         try:
             fraction = self.fraction_of(pod)
+            mem = self.memory_of(pod)
         except ValueError as e:
             return None, str(e)
+        if mem is not None and fraction is None:
+            fraction = 0.0  # a memory-sized share of one GPU: the Fragment path, sized by HBM below
         numa = self.numa_preference(pod)
         want = obj_annotations(pod).get(self.cfg.contract.pod_model_key) or obj_labels(pod).get(self.cfg.contract.pod_model_key)
-        return (k, fraction, tuple(numa) if numa else None, want, self.multi_node(pod)), ""
+        return (k, fraction, tuple(numa) if numa else None, want, self.multi_node(pod), mem), ""
 
     def multi_node(self, pod: Dict[str, Any]) -> bool:
         """A member of a multi-node job: ``<prefix>/multi-node: "true"``, or it requests an RDMA
@@ -253,7 +273,7 @@ class TopologyExtender:
             shape, why = self._pod_shape(pod, k)
             if shape is None:
                 return None, why
-        _, fraction, numa, want, multi = shape
+        _, fraction, numa, want, multi, mem = shape
         with st.lock:
             now = self.clock()
             if self._cacheable():
@@ -261,13 +281,13 @@ class TopologyExtender:
                 if hit is not None and hit[0] <= now <= hit[1]:
                     self.metrics.cache(True)
                     return hit[2], hit[3]
-            d, why = self._eval_state_uncached(st, name, k, fraction, numa, want, now, multi)
+            d, why = self._eval_state_uncached(st, name, k, fraction, numa, want, now, multi, mem)
             if self._cacheable():
                 st.memo[shape] = (now, st.valid_until(now, self.cfg.assume_ttl), d, why)
             return d, why
 
     def _eval_state_uncached(self, st: NodeState, name: str, k: int, fraction: Optional[float], numa, want,
-                             now: float, multi: bool = False) -> Tuple[Optional[Decision], str]:
+                             now: float, multi: bool = False, mem: Optional[int] = None) -> Tuple[Optional[Decision], str]:
         t = st.topology
         if t is None:
             return None, "node has no GPU topology annotation"
@@ -279,11 +299,27 @@ class TopologyExtender:
             for g in t.gpus:
                 sizes[g.physical] = sizes.get(g.physical, 0) + 1
             per_gpu = max(sizes.values()) if sizes else 1
-            if per_gpu <= 1:
+            if per_gpu <= 1 and mem is not None and fraction == 0.0:
+                # whole GPUs: a memory size only has to fit one device, then it is an ordinary request
+                if any(0 < g.vram_bytes < mem for g in t.gpus):
+                    return None, f"gpu-memory {mem} B exceeds a device on this node"
+                fraction = None
+            elif per_gpu <= 1:
                 return None, "fractional GPU requests need a partitioned (CPX/DPX/QPX) or time-sliced node"
+        if fraction is not None:
             need = max(1, math.ceil(fraction * per_gpu - 1e-9))
+            what = f"gpu-fraction {fraction}"
+            if mem is not None:
+                dev_mem = min((g.vram_bytes for g in t.gpus if g.vram_bytes > 0), default=0)
+                if dev_mem <= 0:
+                    return None, "node does not publish device memory sizes: gpu-memory cannot be sized"
+                need_mem = math.ceil(mem / dev_mem - 1e-9)
+                if need_mem > per_gpu:
+                    return None, f"gpu-memory {mem} B exceeds one GPU on this node ({per_gpu} x {dev_mem} B)"
+                if need_mem > need:
+                    need, what = need_mem, f"gpu-memory {mem} B ({dev_mem} B per device)"
             if need != k:
-                return None, (f"gpu-fraction {fraction} is {need} of {per_gpu} partitions per GPU on this node, "
+                return None, (f"{what} is {need} of {per_gpu} partitions per GPU on this node, "
                               f"but the pod requests {k} devices")
         used = sorted(st.used(now, self.cfg.assume_ttl))
         free = st.free_count(now, self.cfg.assume_ttl)
@@ -455,7 +491,9 @@ class TopologyExtender:
                 freed_unknown = sum(st.unknown_pods.get(st.unknown_uids.get(u, ""), 0) for u in keep)
                 used = st.used(now, self.cfg.assume_ttl)
                 healthy = {g.index for g in t.gpus if g.healthy}
-                _, fraction, numa, _, multi = shape
+                _, fraction, numa, _, multi, mem = shape
+                if fraction == 0.0 and mem is not None and len({g.physical for g in t.gpus}) == t.n:
+                    fraction = None  # memory-sized request on whole GPUs: an ordinary placement
                 access = access_costs(t, numa) if self.cfg.cpu_affinity else None
                 best = None
                 tried = 0

@@ -87,6 +87,12 @@ class Contract:
         return f"{self.prefix}/multi-node"
 
     @property
+    def memory_key(self) -> str:
+        """Pod annotation: GPU memory the pod needs on ONE GPU ("96Gi", "100G", bytes), served like a
+        fraction: the fewest partitions / time slices of one GPU whose HBM covers it."""
+        return f"{self.prefix}/gpu-memory"
+
+    @property
     def fraction_key(self) -> str:
         """Pod annotation: a fraction 0<m<1 of ONE physical GPU, served as ceil(m * partitions) XCPs
         of one package on a CPX/DPX/QPX node (Gaia Fragment, paper Alg. 2)."""

@@ -170,3 +170,28 @@ def test_time_slice_keeps_explicit_pair_costs():
             if a != b:
                 assert v.cost[2 * a, 2 * b + 1] == pytest.approx(t.cost[a, b])
     assert v.cost[0, 1] < v.cost[0, 2]
+
+
+def test_gpu_memory_sizes_the_share():
+    """``gpu-memory`` sizes a share by HBM: on a 4-slice MI355X node (72 GB per slice) 100 GB needs
+    2 slices of one GPU; the pod must ask for that count; on whole-GPU nodes it only has to fit."""
+    from gpu_topology_on_k8s_amd.extender import ExtenderConfig, TopologyExtender
+    from gpu_topology_on_k8s_amd.k8s import FakeAPIServer
+    from gpu_topology_on_k8s_amd.k8s.objects import make_node
+
+    api = FakeAPIServer()
+    api.create_node(make_node("s", annotations=encode_node_annotations(time_slice(fx.f7_mi355x(), 4), C),
+                              capacity={C.resource_name: "32"}))
+    api.create_node(make_node("w", annotations=encode_node_annotations(fx.f7_mi355x(), C), capacity={C.resource_name: "8"}))
+    ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+    two = api.create_pod(make_pod("m2", gpus=2, annotations={C.memory_key: "100G"}))
+    ok, failed = ext.filter(two, ["s", "w"])
+    assert ok == ["s", "w"]  # on w it is simply two whole GPUs (each holds 100 GB)
+    d = ext.bind("default", "m2", two["metadata"]["uid"], "s")
+    assert len(physical_group(ext.cache.get("s").topology, d.ids)) == 1 and d.policy == "fragment"
+    bad = api.create_pod(make_pod("m1", gpus=1, annotations={C.memory_key: "100G"}))
+    ok, failed = ext.filter(bad, ["s", "w"])
+    assert ok == ["w"] and "2 of 4" in failed["s"]
+    big = api.create_pod(make_pod("huge", gpus=1, annotations={C.memory_key: "400Gi"}))
+    ok, failed = ext.filter(big, ["s", "w"])
+    assert ok == [] and "exceeds" in failed["w"] and "exceeds" in failed["s"]
