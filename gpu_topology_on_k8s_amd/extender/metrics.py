@@ -93,6 +93,9 @@ class _FragmentationCollector:
         free_g = GaugeMetricFamily("gtk_extender_node_free_devices", "schedulable free devices", labels=["node"])
         place_g = GaugeMetricFamily("gtk_extender_placeable_nodes", "nodes with at least k free devices", labels=["k"])
         cluster_g = GaugeMetricFamily("gtk_extender_cluster_fragmentation", "free-device weighted fragmentation index")
+        share_g = GaugeMetricFamily("gtk_extender_gpu_share_used",
+                                    "fraction of a physical GPU's partitions / time slices held (partitioned or time-sliced nodes)",
+                                    labels=["node", "gpu"])
         now = self.clock()
         tot_free = tot_big = 0
         counts = {1: 0, 2: 0, 4: 0, 8: 0}
@@ -100,7 +103,15 @@ class _FragmentationCollector:
             with st.lock:
                 if st.topology is None:
                     continue
-                free, frag, big = node_fragmentation(st.topology, st.used(now, self.ttl), st.unknown)
+                used = st.used(now, self.ttl)
+                free, frag, big = node_fragmentation(st.topology, used, st.unknown)
+                per: dict = {}
+                for g in st.topology.gpus:
+                    n_all, n_used = per.get(g.physical, (0, 0))
+                    per[g.physical] = (n_all + 1, n_used + (g.index in used))
+            if any(n > 1 for n, _ in per.values()):
+                for gpu, (n, u) in sorted(per.items()):
+                    share_g.add_metric([st.name, str(gpu)], u / n)
             node_g.add_metric([st.name], frag)
             free_g.add_metric([st.name], free)
             tot_free += free
@@ -110,4 +121,4 @@ class _FragmentationCollector:
         for k, c in counts.items():
             place_g.add_metric([str(k)], c)
         cluster_g.add_metric([], (1.0 - tot_big / tot_free) if tot_free else 0.0)
-        yield from (node_g, free_g, place_g, cluster_g)
+        yield from (node_g, free_g, place_g, cluster_g, share_g)

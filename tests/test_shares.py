@@ -195,3 +195,19 @@ def test_gpu_memory_sizes_the_share():
     big = api.create_pod(make_pod("huge", gpus=1, annotations={C.memory_key: "400Gi"}))
     ok, failed = ext.filter(big, ["s", "w"])
     assert ok == [] and "exceeds" in failed["w"] and "exceeds" in failed["s"]
+
+
+def test_share_gauge_per_gpu():
+    from gpu_topology_on_k8s_amd.extender import ExtenderConfig, TopologyExtender
+    from gpu_topology_on_k8s_amd.k8s import FakeAPIServer
+    from gpu_topology_on_k8s_amd.k8s.objects import make_node
+
+    api = FakeAPIServer()
+    api.create_node(make_node("s", annotations=encode_node_annotations(time_slice(fx.f7_mi355x(n=2), 4), C),
+                              capacity={C.resource_name: "8"}))
+    api.create_pod(make_pod("q", gpus=3, node="s", annotations=PodAssignment([4, 5, 6], True, 1).to_annotations()))
+    ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+    ext.cache.sync_all()
+    text = ext.metrics.exposition().decode()
+    assert 'gtk_extender_gpu_share_used{gpu="1",node="s"} 0.75' in text
+    assert 'gtk_extender_gpu_share_used{gpu="0",node="s"} 0.0' in text
