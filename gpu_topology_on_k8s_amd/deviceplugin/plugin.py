@@ -228,19 +228,34 @@ class DevicePluginServer:
 
     def set_health(self, index: int, healthy: bool) -> None:
         """Fault injection / health monitor entry: re-advertise through every ListAndWatch stream."""
+        self.set_health_many({index: healthy})
+
+    def set_health_many(self, states: Dict[int, bool]) -> None:
+        """Apply several health changes at once: one ListAndWatch update, one node publish and one
+        Event per newly unhealthy physical GPU (the time slices of a GPU flip together)."""
+        changed: Dict[int, bool] = {}
         with self._cond:
-            if self._health.get(index) == healthy:
+            for index, healthy in states.items():
+                if self._health.get(index) == healthy:
+                    continue
+                self._health[index] = healthy
+                self.topology.gpus[index].healthy = healthy
+                changed[index] = healthy
+            if not changed:
                 return
-            self._health[index] = healthy
-            self.topology.gpus[index].healthy = healthy
             self._version += 1
             self._cond.notify_all()
-        log.warning("device %d is now %s", index, "Healthy" if healthy else "Unhealthy")
-        self.metrics.health(index, healthy)
-        if self.api is not None and self.cfg.node_name and not healthy:
-            record_event(self.api, {"kind": "Node", "metadata": {"name": self.cfg.node_name}}, "GPUUnhealthy",
-                         f"device {index} ({self.topology.gpus[index].bdf or 'no bdf'}) is Unhealthy", "Warning",
-                         component="gpu-topology-device-plugin", host=self.cfg.node_name)
+        reported = set()
+        for index, healthy in sorted(changed.items()):
+            log.warning("device %d is now %s", index, "Healthy" if healthy else "Unhealthy")
+            self.metrics.health(index, healthy)
+            g = self.topology.gpus[index]
+            if self.api is not None and self.cfg.node_name and not healthy and g.physical not in reported:
+                reported.add(g.physical)
+                devs = sorted(i for i in changed if self.topology.gpus[i].physical == g.physical)
+                record_event(self.api, {"kind": "Node", "metadata": {"name": self.cfg.node_name}}, "GPUUnhealthy",
+                             f"device{'s' if len(devs) > 1 else ''} {format_group(devs)} ({g.bdf or 'no bdf'}) Unhealthy",
+                             "Warning", component="gpu-topology-device-plugin", host=self.cfg.node_name)
         self._publish_node()
 
     def update_topology(self, topo: Topology) -> None:
@@ -793,14 +808,14 @@ class DevicePluginServer:
             log.warning("device %d (%s): GPU reset starting: %s", index, bdf, message)
             for i in same:
                 self._holds[i] = "GPU reset in progress"
-                self.set_health(i, False)
+            self.set_health_many({i: False for i in same})
             reason, note = "GPUReset", f"device {index} ({bdf}) is resetting; held Unhealthy"
         elif kind == "GPU_POST_RESET":
             log.warning("device %d (%s): GPU reset finished: %s", index, bdf, message)
             for i in same:
                 self._holds.pop(i, None)
-                if self.health_fn is None:
-                    self.set_health(i, True)
+            if self.health_fn is None:
+                self.set_health_many({i: True for i in same})
             self._reprobe_now.set()
             reason, note = "GPUResetDone", f"device {index} ({bdf}) finished a reset; links re-measured when idle"
         elif kind == "VMFAULT":
@@ -837,8 +852,8 @@ class DevicePluginServer:
             if self.health_fn is not None and time.monotonic() >= next_health:
                 next_health = time.monotonic() + self.cfg.health_interval
                 try:
-                    for idx, ok in self.health_fn(self.topology).items():
-                        self.set_health(int(idx), bool(ok) and int(idx) not in self._holds)
+                    self.set_health_many({int(idx): bool(ok) and int(idx) not in self._holds
+                                          for idx, ok in self.health_fn(self.topology).items()})
                     changed = getattr(self.health_fn, "layout_changed", lambda: None)()
                     if changed:
                         if not self.layout_change.is_set():

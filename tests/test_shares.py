@@ -211,3 +211,18 @@ def test_share_gauge_per_gpu():
     text = ext.metrics.exposition().decode()
     assert 'gtk_extender_gpu_share_used{gpu="1",node="s"} 0.75' in text
     assert 'gtk_extender_gpu_share_used{gpu="0",node="s"} 0.0' in text
+
+
+def test_reset_of_a_sliced_gpu_is_one_event_and_one_publish():
+    from gpu_topology_on_k8s_amd.k8s import FakeAPIServer
+    from gpu_topology_on_k8s_amd.k8s.objects import make_node
+
+    api = FakeAPIServer()
+    api.create_node(make_node("n"))
+    plug = DevicePluginServer(time_slice(fx.f7_mi355x(n=2), 4), PluginConfig(node_name="n"), api=api)
+    calls = []
+    orig = api.patch_node
+    api.patch_node = lambda *a, **k: (calls.append(1), orig(*a, **k))[1]
+    plug.gpu_event(6, "GPU_PRE_RESET", "test")
+    resets = [e for e in api.events if e["reason"] == "GPUUnhealthy"]
+    assert len(resets) == 1 and "4,5,6,7" in resets[0]["message"] and len(calls) == 1
