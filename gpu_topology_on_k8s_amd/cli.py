@@ -191,7 +191,8 @@ def cmd_config(a) -> int:
     if a.kind == "policy":
         print(json.dumps(legacy_policy(a.resource_name, with_filter=a.filter), indent=2))
     elif a.kind == "scheduler":
-        print(yaml.safe_dump(scheduler_configuration(a.resource_name, with_filter=a.filter), sort_keys=False), end="")
+        print(yaml.safe_dump(scheduler_configuration(a.resource_name, with_filter=a.filter, tls_dir=a.tls_dir or None),
+                             sort_keys=False), end="")
     else:
         print(render_manifests(a.resource_name, image=a.image, time_slices=a.time_slices), end="")
     return 0
@@ -316,6 +317,7 @@ def main(argv=None) -> int:
     p.add_argument("--filter", action="store_true")
     p.add_argument("--image", default="rocm/gpu-topology-k8s:latest")
     p.add_argument("--time-slices", type=int, default=1, help="manifests: device plugin --time-slices (fractional GPUs on SPX nodes)")
+    p.add_argument("--tls-dir", default="", help="scheduler: call the extender over mutual TLS with tls.crt/tls.key/ca.crt from here")
     p.set_defaults(fn=cmd_config)
     p = sub.add_parser("validate")
     p.add_argument("--devices", default="", help="HIP ordinals (skips GROUP resolution)")

@@ -50,10 +50,13 @@ def legacy_policy(resource: str = COMPAT_RESOURCE, url: Optional[str] = None, wi
 
 def scheduler_configuration(resource: str = DEFAULT_RESOURCE, url: Optional[str] = None, with_filter: bool = True,
                             scheduler_name: str = "default-scheduler", weight: int = 5,
-                            extra_resources: Optional[List[str]] = None, with_preempt: bool = True) -> Dict[str, Any]:
+                            extra_resources: Optional[List[str]] = None, with_preempt: bool = True,
+                            tls_dir: Optional[str] = None) -> Dict[str, Any]:
+    """``tls_dir``: call the extender over mutual TLS (its ``--tls-cert/--tls-key/--client-ca``) with
+    the scheduler's client certificate ``tls.crt``/``tls.key`` and the CA ``ca.crt`` from that directory."""
     managed = [{"name": r, "ignoredByScheduler": False} for r in [resource] + list(extra_resources or [])]
     ext: Dict[str, Any] = {
-        "urlPrefix": url or extender_url(),
+        "urlPrefix": url or (extender_url().replace("http://", "https://", 1) if tls_dir else extender_url()),
         "prioritizeVerb": "sort",
         "bindVerb": "bind",
         "weight": weight,
@@ -63,6 +66,10 @@ def scheduler_configuration(resource: str = DEFAULT_RESOURCE, url: Optional[str]
         "ignorable": False,
         "httpTimeout": "30s",
     }
+    if tls_dir:
+        d = tls_dir.rstrip("/")
+        ext["enableHTTPS"] = True
+        ext["tlsConfig"] = {"certFile": f"{d}/tls.crt", "keyFile": f"{d}/tls.key", "caFile": f"{d}/ca.crt"}
     if with_filter:
         ext["filterVerb"] = "filter"
     if with_preempt:  # topology-aware victim selection (extender/scheduler.py TopologyExtender.preempt)

@@ -41,6 +41,11 @@ def main(argv=None) -> int:
     ap.add_argument("--ca-file", default="", help="CA bundle that signs --apiserver's certificate (default: system CAs)")
     ap.add_argument("--insecure-skip-tls-verify", action="store_true",
                     help="do not verify --apiserver's certificate (test clusters only: the bearer token goes to whoever answers)")
+    ap.add_argument("--tls-cert", default="", help="serve HTTPS with this certificate (PEM)")
+    ap.add_argument("--tls-key", default="", help="private key of --tls-cert (PEM)")
+    ap.add_argument("--client-ca", default="",
+                    help="require callers to present a certificate signed by this CA (mutual TLS; kube-scheduler's "
+                         "extender tlsConfig.certFile/keyFile) — needed before serving beyond loopback")
     ap.add_argument("--log-level", default="INFO")
     a = ap.parse_args(argv)
     logging.basicConfig(level=a.log_level, format='{"ts":"%(asctime)s","lvl":"%(levelname)s","mod":"%(name)s","msg":"%(message)s"}')
@@ -59,7 +64,18 @@ def main(argv=None) -> int:
         inf = Informer(api, ext.cache.on_list, ext.cache.on_event)
         ext.cache.attach_informer(inf)
         inf.start()
-    run(ext, a.host, a.port, a.url_prefix, resync_period=a.resync)
+    ssl_context = None
+    if a.tls_cert or a.tls_key:
+        from .server import tls_context
+
+        ssl_context = tls_context(a.tls_cert, a.tls_key, a.client_ca)
+    elif a.client_ca:
+        print("--client-ca needs --tls-cert and --tls-key", file=sys.stderr)
+        return 2
+    if a.host not in ("127.0.0.1", "localhost", "::1") and not a.client_ca:
+        logging.getLogger("gtk.extender").warning(
+            "listening on %s without --client-ca: /bind is reachable by anything that can reach this address", a.host)
+    run(ext, a.host, a.port, a.url_prefix, resync_period=a.resync, ssl_context=ssl_context)
     return 0
 
 

@@ -183,8 +183,23 @@ def make_app(ext: TopologyExtender, prefix: str = DEFAULT_PREFIX, workers: int =
     return app
 
 
+def tls_context(cert_file: str, key_file: str, client_ca: str = ""):
+    """Server TLS for the extender; with ``client_ca`` every caller must present a certificate that CA
+    signed (mutual TLS: kube-scheduler's extender ``tlsConfig.certFile/keyFile``), which is what makes
+    ``/bind`` safe to serve beyond loopback."""
+    import ssl
+
+    ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+    ctx.minimum_version = ssl.TLSVersion.TLSv1_2
+    ctx.load_cert_chain(cert_file, key_file)
+    if client_ca:
+        ctx.load_verify_locations(client_ca)
+        ctx.verify_mode = ssl.CERT_REQUIRED
+    return ctx
+
+
 def run(ext: TopologyExtender, host: str = "127.0.0.1", port: int = DEFAULT_PORT, prefix: str = DEFAULT_PREFIX,
-        resync_period: float = 5.0) -> None:
+        resync_period: float = 5.0, ssl_context=None) -> None:
     """Serve until interrupted.  Without an informer the cache is re-listed every ``resync_period``
     seconds off the request path; with one, WATCH events keep it current and nothing polls."""
     app = make_app(ext, prefix)
@@ -204,5 +219,6 @@ def run(ext: TopologyExtender, host: str = "127.0.0.1", port: int = DEFAULT_PORT
         task.cancel()
 
     app.cleanup_ctx.append(resync_loop)
-    log.info("extender listening on %s:%d%s (policy=%s)", host, port, prefix, ext.cfg.policy_name)
-    web.run_app(app, host=host, port=port, access_log=None, print=None)
+    log.info("extender listening on %s://%s:%d%s (policy=%s)", "https" if ssl_context else "http", host, port, prefix,
+             ext.cfg.policy_name)
+    web.run_app(app, host=host, port=port, access_log=None, print=None, ssl_context=ssl_context)

@@ -77,6 +77,15 @@ def test_manifests_time_slices():
     assert "--time-slices" not in render_manifests()
 
 
+def test_scheduler_config_mutual_tls():
+    from gpu_topology_on_k8s_amd.config import scheduler_configuration
+
+    ext = scheduler_configuration(tls_dir="/etc/gtk/tls")["extenders"][0]
+    assert ext["enableHTTPS"] is True and ext["urlPrefix"].startswith("https://127.0.0.1:32743")
+    assert ext["tlsConfig"] == {"certFile": "/etc/gtk/tls/tls.crt", "keyFile": "/etc/gtk/tls/tls.key", "caFile": "/etc/gtk/tls/ca.crt"}
+    assert scheduler_configuration()["extenders"][0]["enableHTTPS"] is False
+
+
 def test_cli_sim():
     lines = [json.loads(l) for l in _cli("sim", "--nodes", "1", "--pods", "4,4").splitlines()]
     assert {tuple(l["devices"]) for l in lines} == {(0, 1, 2, 3), (4, 5, 6, 7)}

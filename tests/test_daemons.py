@@ -203,3 +203,50 @@ def test_device_plugin_daemon_time_slices():
         srv.shutdown()
         shutil.rmtree(sockdir, ignore_errors=True)
     assert rc == 0, p.stdout.read() if p.stdout else ""
+
+
+def _pki(d):
+    """A CA, a server certificate for 127.0.0.1 and a client certificate, with the openssl CLI."""
+    def run(*args):
+        subprocess.run(["openssl", *args], check=True, capture_output=True, cwd=d)
+
+    run("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", "ca.key", "-out", "ca.crt", "-days", "2", "-subj", "/CN=test-ca")
+    with open(os.path.join(d, "san.cnf"), "w") as f:
+        f.write("subjectAltName=IP:127.0.0.1\n")
+    for name, ext in (("server", ["-extfile", "san.cnf"]), ("client", [])):
+        run("req", "-newkey", "rsa:2048", "-nodes", "-keyout", f"{name}.key", "-out", f"{name}.csr", "-subj", f"/CN={name}")
+        run("x509", "-req", "-in", f"{name}.csr", "-CA", "ca.crt", "-CAkey", "ca.key", "-CAcreateserial", "-out", f"{name}.crt",
+            "-days", "2", *ext)
+    return {n: os.path.join(d, n) for n in ("ca.crt", "server.crt", "server.key", "client.crt", "client.key")}
+
+
+@pytest.mark.skipif(shutil.which("openssl") is None, reason="openssl CLI not available")
+def test_extender_daemon_mutual_tls():
+    """--tls-cert/--tls-key/--client-ca: the extender serves HTTPS and only answers callers whose
+    certificate the CA signed (kube-scheduler's extender tlsConfig), so /bind may leave loopback."""
+    api = FakeAPIServer()
+    srv, url = serve_http(api)
+    d = tempfile.mkdtemp(prefix="gtkpki", dir="/tmp")
+    pki = _pki(d)
+    port = _free_port()
+    ext = _spawn(["gpu_topology_on_k8s_amd.extender", "--apiserver", url, "--port", str(port), "--log-level", "WARNING",
+                  "--tls-cert", pki["server.crt"], "--tls-key", pki["server.key"], "--client-ca", pki["ca.crt"]])
+    base = f"https://127.0.0.1:{port}/gputopology-scheduler"
+    try:
+        def up():
+            try:
+                return requests.get(base + "/healthz", timeout=1, verify=pki["ca.crt"],
+                                    cert=(pki["client.crt"], pki["client.key"])).ok
+            except requests.RequestException:
+                return False
+
+        assert _wait(up, 60), "extender did not come up over TLS"
+        with pytest.raises(requests.exceptions.ConnectionError):  # no client certificate: handshake refused / closed
+            requests.get(base + "/healthz", timeout=5, verify=pki["ca.crt"])
+        with pytest.raises(requests.RequestException):
+            requests.post(base.replace("https", "http") + "/bind", json={}, timeout=5)  # plain HTTP is not served
+    finally:
+        rc = _stop(ext)
+        srv.shutdown()
+        shutil.rmtree(d, ignore_errors=True)
+    assert rc == 0, ext.stdout.read() if ext.stdout else ""
