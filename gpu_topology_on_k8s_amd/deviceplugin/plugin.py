@@ -350,6 +350,7 @@ class DevicePluginServer:
             c.label_model: models[0] if len(models) == 1 else "mixed",
             c.label_partition: t.gpus[0].partition if t.gpus else "",
             c.label_gfx: t.gpus[0].gfx if t.gpus else "",
+            c.label_slices: str(max((int((t.physical == p).sum()) for p in set(t.physical.tolist())), default=1)),
         }
         ann = encode_node_annotations(t, c)
         self.metrics.annotation_bytes.set(sum(len(k) + len(v) for k, v in ann.items()))

@@ -116,6 +116,12 @@ class Contract:
         return f"{self.prefix}/gfx"
 
     @property
+    def label_slices(self) -> str:
+        """Node label: devices per physical GPU (time slices or XCP partitions; "1" = whole GPUs), so
+        fractional pods can select shared nodes with a nodeSelector."""
+        return f"{self.prefix}/devices-per-gpu"
+
+    @property
     def pod_model_key(self) -> str:
         """Pod annotation/label selecting a GPU model (pods without it accept any single model)."""
         return f"{self.prefix}/gpu-model"

@@ -226,3 +226,15 @@ def test_reset_of_a_sliced_gpu_is_one_event_and_one_publish():
     plug.gpu_event(6, "GPU_PRE_RESET", "test")
     resets = [e for e in api.events if e["reason"] == "GPUUnhealthy"]
     assert len(resets) == 1 and "4,5,6,7" in resets[0]["message"] and len(calls) == 1
+
+
+def test_node_label_devices_per_gpu():
+    from gpu_topology_on_k8s_amd.k8s import FakeAPIServer
+    from gpu_topology_on_k8s_amd.k8s.objects import make_node
+
+    api = FakeAPIServer()
+    for name, topo in (("s", time_slice(fx.f7_mi355x(n=2), 4)), ("w", fx.f7_mi355x(n=2)), ("c", fx.f8_mi355x_cpx())):
+        api.create_node(make_node(name))
+        DevicePluginServer(topo, PluginConfig(node_name=name), api=api)._publish_node()
+    labels = {n: api.get_node(n)["metadata"]["labels"][C.label_slices] for n in ("s", "w", "c")}
+    assert labels == {"s": "4", "w": "1", "c": "8"}
