@@ -37,6 +37,26 @@ def make_api(apiserver: str, token: str, ca_file: str = "", insecure: bool = Fal
     return None
 
 
+def node_time_slices(api, node_name: str, contract: Contract, default: int) -> int:
+    """Time slices for this node: the operator's node label ``<prefix>/time-slices`` when set (one
+    DaemonSet serves a cluster where only some nodes are shared), else ``--time-slices``."""
+    if api is None or not node_name:
+        return default
+    try:
+        labels = (api.get_node(node_name).get("metadata") or {}).get("labels") or {}
+    except Exception as e:  # noqa: BLE001 - the flag still applies
+        logging.getLogger("gtk.deviceplugin").warning("reading node %s labels failed: %s", node_name, e)
+        return default
+    raw = labels.get(contract.time_slices_label)
+    if raw is None:
+        return default
+    try:
+        return max(1, int(raw))
+    except ValueError:
+        logging.getLogger("gtk.deviceplugin").warning("ignoring %s=%r (not an integer)", contract.time_slices_label, raw)
+        return default
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--resource-name", default="amd.com/gpu")
@@ -83,7 +103,8 @@ def main(argv=None) -> int:
                          "auto = on wherever amdsmi offers it")
     ap.add_argument("--time-slices", type=int, default=1,
                     help="advertise every (SPX) GPU as this many time slices: Gaia fractional requests on unpartitioned "
-                         "nodes (a pod holding j slices holds j/S of one GPU; topology/shares.py); 1 = whole GPUs")
+                         "nodes (a pod holding j slices holds j/S of one GPU; topology/shares.py); 1 = whole GPUs. "
+                         "The node label <annotation-prefix>/time-slices overrides it per node")
     ap.add_argument("--share-cu-mask", default="on", choices=["on", "off"],
                     help="--time-slices: confine a pod holding part of a GPU to its slices' compute units (HSA_CU_MASK)")
     ap.add_argument("--log-level", default="INFO")
@@ -91,12 +112,14 @@ def main(argv=None) -> int:
     logging.basicConfig(level=a.log_level, format='{"ts":"%(asctime)s","lvl":"%(levelname)s","mod":"%(name)s","msg":"%(message)s"}')
     log = logging.getLogger("gtk.deviceplugin")
 
+    api = make_api(a.apiserver, a.token, a.ca_file, a.insecure_skip_tls_verify)
+    contract = Contract(resource_name=a.resource_name, prefix=a.annotation_prefix)
+    a.time_slices = node_time_slices(api, a.node_name, contract, a.time_slices)
+
     def node_topology():
         return time_slice(discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus), a.time_slices)
 
     topo = node_topology()
-    api = make_api(a.apiserver, a.token, a.ca_file, a.insecure_skip_tls_verify)
-    contract = Contract(resource_name=a.resource_name, prefix=a.annotation_prefix)
     probe_fn = None
     if a.probe != "off" and a.discovery != "fake":
         # in a child process: the plugin lives as long as the node and must not hold HIP contexts

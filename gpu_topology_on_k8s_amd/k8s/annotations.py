@@ -116,6 +116,11 @@ class Contract:
         return f"{self.prefix}/gfx"
 
     @property
+    def time_slices_label(self) -> str:
+        """Node label set by the operator: advertise this node's GPUs as that many time slices."""
+        return f"{self.prefix}/time-slices"
+
+    @property
     def label_slices(self) -> str:
         """Node label: devices per physical GPU (time slices or XCP partitions; "1" = whole GPUs), so
         fractional pods can select shared nodes with a nodeSelector."""

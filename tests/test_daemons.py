@@ -173,20 +173,20 @@ def test_both_daemons_config4_through_shipped_processes():
 
 
 def test_device_plugin_daemon_time_slices():
-    """``--time-slices 4`` on a 2-GPU node: the kubelet sees 8 devices, the node annotation carries the
-    slices, and a 2-slice pod gets one GPU's device nodes with GTK_GPU_FRACTION=0.5."""
+    """A node labelled ``gputopology.amd.com/time-slices=4`` (no flag): the kubelet sees 8 devices, the node
+    annotation carries the slices, and a 2-slice pod gets one GPU's device nodes with GTK_GPU_FRACTION=0.5."""
     from gpu_topology_on_k8s_amd.k8s.annotations import decode_node_annotations
     from gpu_topology_on_k8s_amd.topology.shares import slices_per_gpu
 
     api = FakeAPIServer()
-    api.create_node(make_node("worker-1"))
+    api.create_node(make_node("worker-1", labels={"gputopology.amd.com/time-slices": "4"}))  # the operator's per-node choice
     srv, url = serve_http(api)
     sockdir = tempfile.mkdtemp(prefix="gtkd", dir="/tmp")
     kubelet = FakeKubelet(sockdir, node_name="worker-1", api=api)
     kubelet.start()
     devroot = os.path.join(sockdir, "dev")
     os.makedirs(devroot)
-    p = _spawn(["gpu_topology_on_k8s_amd.deviceplugin", "--discovery", "fake", "--fake-gpus", "2", "--time-slices", "4",
+    p = _spawn(["gpu_topology_on_k8s_amd.deviceplugin", "--discovery", "fake", "--fake-gpus", "2",
                 "--apiserver", url, "--node-name", "worker-1", "--socket-dir", sockdir, "--dev-root", devroot,
                 "--log-level", "WARNING"])
     try:
