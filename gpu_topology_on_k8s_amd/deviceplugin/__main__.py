@@ -166,8 +166,15 @@ def main(argv=None) -> int:
     for sig in (signal.SIGINT, signal.SIGTERM):  # installed before serving: a stop never races start-up
         signal.signal(sig, lambda *_: done.set())
     plugin.start()
+    ticks = 0
     while not done.wait(1.0):
-        if plugin.layout_change.is_set():  # partition switch / device hot-(un)plug: restart cleanly
+        ticks += 1
+        if ticks % 30 == 0 and api is not None:  # the operator relabelled the node's time slices
+            want = node_time_slices(api, a.node_name, contract, a.time_slices)
+            if want != a.time_slices:
+                plugin.layout_change_reason = f"time slices per GPU {a.time_slices} -> {want} (node label)"
+                plugin.layout_change.set()
+        if plugin.layout_change.is_set():  # partition switch / device hot-(un)plug / new slicing: restart cleanly
             log.warning("exiting for a restart: %s", plugin.layout_change_reason)
             plugin.stop()
             return 75  # EX_TEMPFAIL: the DaemonSet restarts the container, which re-discovers

@@ -197,6 +197,10 @@ def test_device_plugin_daemon_time_slices():
         pod = api.create_pod(make_pod("half", gpus=2, node="worker-1"))
         c = kubelet.admit(pod, "amd.com/gpu").container_responses[0]
         assert c.envs["GTK_GPU_FRACTION"] == "0.5" and len(c.envs["GTK_GPU_GROUP"].split(",")) == 1
+        # the operator relabels the node: the plugin exits for a restart (EX_TEMPFAIL) with the new slicing
+        api.patch_node("worker-1", labels={"gputopology.amd.com/time-slices": "2"})
+        assert p.wait(timeout=60) == 75
+        return
     finally:
         rc = _stop(p)
         kubelet.stop()
