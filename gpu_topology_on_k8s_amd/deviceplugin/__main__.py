@@ -105,6 +105,8 @@ def main(argv=None) -> int:
                     help="advertise every (SPX) GPU as this many time slices: Gaia fractional requests on unpartitioned "
                          "nodes (a pod holding j slices holds j/S of one GPU; topology/shares.py); 1 = whole GPUs. "
                          "The node label <annotation-prefix>/time-slices overrides it per node")
+    ap.add_argument("--label-check-interval", type=float, default=30.0,
+                    help="seconds between checks of the node's time-slices label (a change restarts the plugin once idle)")
     ap.add_argument("--share-cu-mask", default="on", choices=["on", "off"],
                     help="--time-slices: confine a pod holding part of a GPU to its slices' compute units (HSA_CU_MASK)")
     ap.add_argument("--log-level", default="INFO")
@@ -169,11 +171,17 @@ def main(argv=None) -> int:
     ticks = 0
     while not done.wait(1.0):
         ticks += 1
-        if ticks % 30 == 0 and api is not None:  # the operator relabelled the node's time slices
+        if ticks % max(1, int(a.label_check_interval)) == 0 and api is not None:  # the operator relabelled the node's time slices
             want = node_time_slices(api, a.node_name, contract, a.time_slices)
             if want != a.time_slices:
-                plugin.layout_change_reason = f"time slices per GPU {a.time_slices} -> {want} (node label)"
-                plugin.layout_change.set()
+                # device IDs change with the slicing: switch only when no pod holds a device, or the
+                # running pods' GROUP annotations would name devices of the old layout
+                if plugin.node_idle():
+                    plugin.layout_change_reason = f"time slices per GPU {a.time_slices} -> {want} (node label)"
+                    plugin.layout_change.set()
+                elif ticks % 300 == 0:
+                    log.warning("time slices per GPU %d -> %d requested by the node label; waiting until no pod holds a device",
+                                a.time_slices, want)
         if plugin.layout_change.is_set():  # partition switch / device hot-(un)plug / new slicing: restart cleanly
             log.warning("exiting for a restart: %s", plugin.layout_change_reason)
             plugin.stop()

@@ -186,7 +186,7 @@ def test_device_plugin_daemon_time_slices():
     kubelet.start()
     devroot = os.path.join(sockdir, "dev")
     os.makedirs(devroot)
-    p = _spawn(["gpu_topology_on_k8s_amd.deviceplugin", "--discovery", "fake", "--fake-gpus", "2",
+    p = _spawn(["gpu_topology_on_k8s_amd.deviceplugin", "--discovery", "fake", "--fake-gpus", "2", "--label-check-interval", "2",
                 "--apiserver", url, "--node-name", "worker-1", "--socket-dir", sockdir, "--dev-root", devroot,
                 "--log-level", "WARNING"])
     try:
@@ -197,8 +197,12 @@ def test_device_plugin_daemon_time_slices():
         pod = api.create_pod(make_pod("half", gpus=2, node="worker-1"))
         c = kubelet.admit(pod, "amd.com/gpu").container_responses[0]
         assert c.envs["GTK_GPU_FRACTION"] == "0.5" and len(c.envs["GTK_GPU_GROUP"].split(",")) == 1
-        # the operator relabels the node: the plugin exits for a restart (EX_TEMPFAIL) with the new slicing
+        # the operator relabels the node: the plugin waits while a pod holds devices, then exits for a
+        # restart (EX_TEMPFAIL) with the new slicing
         api.patch_node("worker-1", labels={"gputopology.amd.com/time-slices": "2"})
+        with pytest.raises(subprocess.TimeoutExpired):
+            p.wait(timeout=6)
+        api.delete_pod("default", "half")
         assert p.wait(timeout=60) == 75
         return
     finally:
