@@ -136,8 +136,6 @@ def cmd_status(a) -> int:
     from .extender import ExtenderConfig, TopologyExtender
     from .extender.metrics import node_fragmentation
     from .k8s.annotations import Contract
-    from .topology.shares import slices_per_gpu
-
     api = make_api(a.apiserver, a.token, a.ca_file, a.insecure_skip_tls_verify)
     if api is None:
         print("gtk status: no apiserver (--apiserver URL, or run in a cluster)", file=sys.stderr)
@@ -154,8 +152,13 @@ def cmd_status(a) -> int:
                 continue
             used = st.used(now, ext.cfg.assume_ttl)
             free, frag, _ = node_fragmentation(t, used, st.unknown)
-            row = {"node": st.name, "devices": t.n, "per_gpu": slices_per_gpu(t) if slices_per_gpu(t) > 1 else 1,
+            per_gpu = max((int((t.physical == p).sum()) for p in set(t.physical.tolist())), default=1)
+            row = {"node": st.name, "devices": t.n, "per_gpu": per_gpu,
                    "used": len(used) + st.unknown, "free": free, "fragmentation": round(frag, 3), "best_score": {}}
+            if per_gpu > 1:  # partitioned / time-sliced: the share of every physical GPU in use
+                row["gpu_share_used"] = {str(p): round(sum(1 for g in t.gpus if g.physical == p and g.index in used) /
+                                                       sum(1 for g in t.gpus if g.physical == p), 3)
+                                         for p in sorted(set(t.physical.tolist()))}
         for k in sizes:
             d, _ = ext._eval_state({"metadata": {"name": "status", "namespace": "default"}, "spec": {}}, st.name, st, k)
             row["best_score"][str(k)] = None if d is None else round(d.score, 2)

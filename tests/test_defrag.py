@@ -124,3 +124,19 @@ def test_gtk_status_reports_usage_and_scores():
     assert rows["n0"]["used"] == 2 and rows["n0"]["free"] == 6 and rows["n1"]["free"] == 8
     assert rows["n0"]["best_score"]["8"] is None and rows["n1"]["best_score"]["8"] is not None
     assert q.returncode == 0 and q.stdout.splitlines()[0].startswith("NODE") and "n1" in q.stdout
+    assert "gpu_share_used" not in rows["n0"]
+
+
+def test_gtk_status_shares_on_a_sliced_node():
+    api = FakeAPIServer()
+    api.create_node(make_node("s", annotations=encode_node_annotations(time_slice(fx.f7_mi355x(n=2), 4), C),
+                              capacity={C.resource_name: "8"}))
+    api.create_pod(make_pod("q", gpus=1, node="s", annotations=PodAssignment([5], True, 1).to_annotations()))
+    srv, url = serve_http(api)
+    try:
+        p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd", "status", "--apiserver", url, "--output", "json",
+                            "--sizes", "1,4"], capture_output=True, text=True, timeout=120)
+    finally:
+        srv.shutdown()
+    (row,) = json.loads(p.stdout)
+    assert row["per_gpu"] == 4 and row["gpu_share_used"] == {"0": 0.0, "1": 0.25}
