@@ -139,7 +139,10 @@ class Sim:
         return None if best is None else (best[1], best[2])
 
 
-def run(topos: List[Topology], trace, policy: str, slices: int) -> Dict[str, object]:
+def run(topos: List[Topology], trace, policy: str, slices: int, share_slowdown: float = 1.0) -> Dict[str, object]:
+    """``share_slowdown``: run-time factor of a fractional job that starts on a GPU another job already
+    shares (HBM and L2 stay shared under the CU masks: 1.13 measured on MI355X next to a Llama job,
+    ``bench/share_neighbor.py``)."""
     sim = Sim(topos, policy, slices)
     n_gpus = sum(t.n for t in topos)
     events: List[Tuple[float, int, str, int]] = []
@@ -151,6 +154,7 @@ def run(topos: List[Topology], trace, policy: str, slices: int) -> Dict[str, obj
     where: Dict[int, Tuple[int, Tuple[int, ...]]] = {}
     start: Dict[int, float] = {}
     held = 0.0  # GPU-minutes allocated (a whole GPU for a 0.25 job under `whole`)
+    runtime: Dict[int, float] = {}
     now = 0.0
     jobs = {j["id"]: j for j in trace}
     while events:
@@ -177,11 +181,15 @@ def run(topos: List[Topology], trace, policy: str, slices: int) -> Dict[str, obj
                 still.append(p)
                 continue
             n, ids = pl
+            node = sim.nodes[n]
+            shared = len(ids) < slices and node.gpu_load(ids[0] // slices) > 0
             sim.nodes[n].slot_used |= set(ids)
             where[p] = (n, ids)
             start[p] = now
-            held += len(ids) / slices * jobs[p]["base"]
-            heapq.heappush(events, (now + jobs[p]["base"], seq, "finish", p))
+            rt = jobs[p]["base"] * (share_slowdown if shared else 1.0)
+            runtime[p] = rt
+            held += len(ids) / slices * rt
+            heapq.heappush(events, (now + rt, seq, "finish", p))
             seq += 1
         pending = still
     makespan = now
@@ -189,7 +197,7 @@ def run(topos: List[Topology], trace, policy: str, slices: int) -> Dict[str, obj
     frac = [start[j["id"]] - j["arrive"] for j in trace if j["k"] < 1]
     w8 = [start[j["id"]] - j["arrive"] for j in trace if j["k"] == 8]
     useful = sum(j["k"] * j["base"] for j in trace)
-    jct = [w + j["base"] for w, j in zip(waits, trace)]
+    jct = [w + runtime[j["id"]] for w, j in zip(waits, trace)]
     return {"policy": policy, "goodput": round(useful / (n_gpus * makespan), 4), "allocated": round(held / (n_gpus * makespan), 4),
             "makespan_h": round(makespan / 60, 2), "jct_mean_min": round(statistics.mean(jct), 2),
             "wait_mean_min": round(statistics.mean(waits), 2), "wait_frac_mean_min": round(statistics.mean(frac), 2) if frac else None,
@@ -205,6 +213,8 @@ def main() -> int:
                          "where goodput is the share of the cluster doing useful work)")
     ap.add_argument("--mean-min", type=float, default=60.0)
     ap.add_argument("--slices", type=int, default=4, help="time slices per GPU on shared nodes")
+    ap.add_argument("--share-slowdown", type=float, default=1.13,
+                    help="run-time factor of a fractional job that starts next to another on its GPU (measured: 1.13)")
     ap.add_argument("--seeds", default="1,2,3")
     ap.add_argument("--policies", default=",".join(POLICIES))
     ap.add_argument("--out", default="")
@@ -217,7 +227,7 @@ def main() -> int:
                      for i in range(a.nodes)]
             trace = make_trace(a.jobs, 8 * a.nodes, load, a.mean_min, seed)
             for pol in a.policies.split(","):
-                r = run(topos, trace, pol, a.slices)
+                r = run(topos, trace, pol, a.slices, a.share_slowdown)
                 r["seed"], r["load"] = seed, load
                 print(json.dumps(r), flush=True)
                 results.append(r)
