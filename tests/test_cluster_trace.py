@@ -91,3 +91,18 @@ def test_share_trace_sharing_beats_whole_gpus_under_a_backlog():
     sim.nodes[a[0]].slot_used |= set(a[1])
     b = sim.place(0.25)  # best fit: onto the half-used GPU, not a fresh one
     assert b[0] == a[0] and {i // 4 for i in b[1]} == {i // 4 for i in a[1]}
+
+
+def test_bench_scripts_compile_and_document_themselves():
+    """Every bench/ script (GPU-only ones included: share_mnist, share_neighbor, train_llama...) byte-
+    compiles and prints its usage without a GPU."""
+    import glob
+    import py_compile
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for path in sorted(glob.glob(os.path.join(root, "bench", "*.py"))):
+        py_compile.compile(path, doraise=True)
+    for name in ("share_mnist.py", "share_neighbor.py", "share_trace.py"):
+        p = subprocess.run([sys.executable, os.path.join(root, "bench", name), "--help"], capture_output=True, text=True, timeout=60)
+        assert p.returncode == 0 and "usage" in p.stdout.lower(), (name, p.stderr[-500:])
