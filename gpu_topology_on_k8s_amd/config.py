@@ -245,6 +245,19 @@ def render_kind(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, fake_gpus:
                             "resources": {"limits": {resource: "1"}}}],
         },
     }
+    half = {  # a fractional pod (Gaia Fragment): half of one GPU on a time-sliced node (docs/SHARES.md)
+        "apiVersion": "v1",
+        "kind": "Pod",
+        "metadata": {"name": "gpu-topology-half", "namespace": "default",
+                     "annotations": {"gputopology.amd.com/gpu-fraction": "0.5"}},
+        "spec": {
+            "restartPolicy": "Never",
+            "nodeSelector": {"gputopology.amd.com/devices-per-gpu": "2"},
+            "containers": [{"name": "c", "image": "busybox:1.36",
+                            "command": ["sh", "-c", "env | grep -E 'GTK_|HSA_CU_MASK' && sleep 5"],
+                            "resources": {"limits": {resource: "1"}}}],
+        },
+    }
     up = "\n".join([
         "#!/usr/bin/env bash",
         "# BASELINE config 1: kind + 2 fake GPUs; the pod must reach Succeeded with GTK_GPU_GROUP set.",
@@ -266,5 +279,7 @@ def render_kind(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, fake_gpus:
         "scheduler-config.yaml": yaml.safe_dump(scheduler_configuration(resource), sort_keys=False),
         "gpu-topology-kind.yaml": yaml.safe_dump_all(docs, sort_keys=False),
         "pod-1gpu.yaml": yaml.safe_dump(pod, sort_keys=False),
+        # after `kubectl label node <worker> gputopology.amd.com/time-slices=2` (the plugin restarts with 2 slices per GPU)
+        "pod-half-gpu.yaml": yaml.safe_dump(half, sort_keys=False),
         "up.sh": up,
     }
