@@ -88,6 +88,10 @@ def cmd_select(a) -> int:
         from .topology.shares import cu_mask_env, share_fractions
 
         per = max(int((t.physical == p).sum()) for p in set(t.physical.tolist()))
+        if per <= 1:
+            print("gtk select: --fraction needs a partitioned (CPX/DPX/QPX) or time-sliced node (--time-slices S)",
+                  file=sys.stderr)
+            return 2
         k = max(1, math.ceil(a.fraction * per - 1e-9))
         ids = place_fraction(t, k, used)
         out = {"ids": list(ids), "policy": "fragment", "devices_per_gpu": per,

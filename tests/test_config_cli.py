@@ -66,6 +66,9 @@ def test_cli_topo_select_config():
     assert json.loads(_cli("config", "policy"))["kind"] == "Policy"
     fr = json.loads(_cli("select", "--discovery", "fake", "--fake-gpus", "4", "--time-slices", "4", "--fraction", "0.25", "--used", "8,9"))
     assert fr["gpu"] == 2 and fr["ids"] == [10] and fr["share"] == 0.25 and fr["hsa_cu_mask"] == "0:128-191"
+    p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd", "select", "--discovery", "fake", "--fake-gpus", "4",
+                        "--fraction", "0.5"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2 and "time-sliced" in p.stderr
 
 
 def test_manifests_time_slices():
