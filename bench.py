@@ -82,7 +82,49 @@ def parse(argv=None):
                     help="after the headline timing: exact-checked size sweep MIN:MAX:FACTOR (nccl-tests style, "
                          "BASELINE.md target 3, peak busBW reported); 'auto' = 8:16G:8 on GPUs, 8:1M:8 for "
                          "--backend cpu; or 'off'")
+    ap.add_argument("--ring-probe", default="auto", choices=["auto", "on", "off"],
+                    help="K6 concurrent ring probe of the chosen subset (child process of rank 0, before any rank "
+                         "touches its GPU): the busBW ceiling 'busbw_vs_probe_bound' divides by; auto = on at k >= 2 "
+                         "when the link probe ran")
+    ap.add_argument("--cpu-bind", default="auto", choices=["auto", "env", "off"],
+                    help="Gaia B6: pin each rank to GTK_CPUSET (a pod's Allocate env) narrowed to its own device's core "
+                         "slice, or to that slice on a bare node (auto); env = GTK_CPUSET only; off")
+    ap.add_argument("--budget-s", type=float, default=300.0,
+                    help="wall-clock budget: a supplementary phase (tuning, sweep, fp32, graph, worst-subset A/B) is "
+                         "skipped when its predicted cost would overrun it; the headline is never skipped; 0 = no limit")
     return ap.parse_args(argv)
+
+
+class Phases:
+    """Per-phase wall time (``phase_s`` in the JSON line) and the ``--budget-s`` gate.  Decisions to
+    skip a phase are agreed by every rank (MIN all-reduce), so no rank enters a collective alone."""
+
+    def __init__(self, budget_s: float):
+        self.t0 = time.perf_counter()
+        self.budget = float(budget_s)
+        self.s = {}
+        self.skipped = []
+
+    def elapsed(self) -> float:
+        return time.perf_counter() - self.t0
+
+    def run(self, name, fn, *a, **kw):
+        t = time.perf_counter()
+        try:
+            return fn(*a, **kw)
+        finally:
+            self.s[name] = round(self.s.get(name, 0.0) + time.perf_counter() - t, 3)
+
+    def allow(self, name: str, predicted_s: float, agree=None) -> bool:
+        ok = self.budget <= 0 or self.elapsed() + max(0.0, predicted_s) <= self.budget
+        if agree is not None:
+            ok = agree(ok)
+        if not ok:
+            self.skipped.append({"phase": name, "predicted_s": round(predicted_s, 2), "elapsed_s": round(self.elapsed(), 2)})
+        return ok
+
+    def report(self) -> dict:
+        return dict(self.s, total=round(self.elapsed(), 3))
 
 
 def parse_size(s: str) -> int:
@@ -306,6 +348,17 @@ def measure_worst(env, choice, nbytes, args, tdev, barrier_kw, backend, ctas):
         r.close()
 
 
+def _sweep_cost(sizes, algbw_gbps: float) -> float:
+    """Predicted seconds of :func:`run_sweep` from the headline algBW (its iteration counts, plus a
+    per-size overhead for the exact check and the warm-up op)."""
+    bw = max(algbw_gbps, 1e-3) * 1e9
+    t = 0.0
+    for b in sizes:
+        iters = 20 if b < (64 << 20) else (5 if b < (1 << 30) else 2)
+        t += (iters + 2) * b / bw + 0.05
+    return t
+
+
 def main(argv=None) -> int:
     args = parse(argv)
     in_launcher = "WORLD_SIZE" in os.environ and "RANK" in os.environ
@@ -317,7 +370,12 @@ def main(argv=None) -> int:
         return subprocess.call(cmd)
     if not in_launcher:
         os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    # Cross-process GPU memory sharing (RCCL's P2P/IPC transport between the ranks' processes, k >= 2):
+    # the amdgpu host driver of these nodes exports IPC handles only as dma-bufs, and the ROCr runtime
+    # uses them only with the legacy KFD IPC path off; with it on, hipIpcGetMemHandle fails with
+    # "invalid argument" and RCCL cannot open its peers' buffers.  Set before HIP initialises.
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    ph = Phases(args.budget_s)
     rccl_log = None
     if args.backend != "cpu" and (args.rccl_log == "on" or (args.rccl_log == "auto" and args.gpus > 1)) \
             and "NCCL_DEBUG" not in os.environ:
@@ -332,6 +390,7 @@ def main(argv=None) -> int:
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from gpu_topology_on_k8s_amd.parallel.allreduce import (AllReduceRunner, DistEnv, SubsetChoice, bus_factor, choose_subset,
                                                              probe_node)
+    from gpu_topology_on_k8s_amd.topology.cpus import bind_workload
 
     env = DistEnv.from_env()
     if env.world != args.gpus:
@@ -342,26 +401,47 @@ def main(argv=None) -> int:
     env.store = dist.distributed_c10d._get_default_store()
 
     # --- placement: rank 0 picks the subset, everybody binds to subset[rank] ---------------------
+    ring = None
     if env.rank == 0:
         preset = {"auto": None if cpu else "quick", "off": None}.get(args.probe, args.probe)
         topo = None
         if preset:
-            topo, msg = probe_node(preset, backend=args.discovery)
+            # the probe seeds the placement's cost matrix (scheduler-chosen subset): part of the
+            # headline's definition, so it is bounded by the budget but never skipped
+            tmo = 150.0 if args.budget_s <= 0 else max(30.0, min(150.0, args.budget_s / 3))
+            topo, msg = ph.run("probe", probe_node, preset, backend=args.discovery, timeout=tmo)
             if topo is None:
                 print(f"bench: link probe unavailable ({msg}); placing on discovered link classes", file=sys.stderr)
             elif msg != "ok":
                 print(f"bench: link probe: {msg}", file=sys.stderr)
-        choice = choose_subset(env.world, backend=args.discovery, visible=(args.cpu_visible or env.world) if cpu else None, topology=topo,
-                               via_k8s=args.via == "k8s")
+        choice = ph.run("place", choose_subset, env.world, backend=args.discovery,
+                        visible=(args.cpu_visible or env.world) if cpu else None, topology=topo, via_k8s=args.via == "k8s")
+        want_ring = args.ring_probe == "on" or (args.ring_probe == "auto" and env.world > 1 and choice.probed)
+        if want_ring and not cpu and ph.allow("ring", 15.0):
+            from gpu_topology_on_k8s_amd.ops.probe import ring_in_child
+
+            # before any rank opens its GPU: the K6 child has the subset's links to itself
+            ring, msg = ph.run("ring", ring_in_child, choice.hip_devices, preset or "quick")
+            if ring is None:
+                print(f"bench: ring probe unavailable ({msg})", file=sys.stderr)
+                ring = {"error": msg[-300:]}
         env.store.set("gtk/subset", choice.to_json())
     choice = SubsetChoice.from_json(env.store.get("gtk/subset").decode())
     device = choice.hip_devices[env.rank]  # HIP ordinal of node device choice.devices[rank] (PCI-address map)
     tdev = "cpu" if cpu else f"cuda:{device}"
     barrier_kw = {} if cpu else {"device_ids": [device]}
+    own = (choice.extra.get("cpusets") or [""] * env.world)[env.rank]
+    cpu_rep = ph.run("cpu_bind", bind_workload, args.cpu_bind, own)
+    env.store.set(f"gtk/cpuset/{env.rank}", json.dumps(cpu_rep))
 
     def gpu_sync():
         if not cpu:
             torch.cuda.synchronize()
+
+    def agree(ok: bool) -> bool:
+        f = torch.tensor([1 if ok else 0], dtype=torch.int32, device=tdev)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        return bool(int(f.item()))
 
     if not cpu:
         torch.cuda.set_device(device)
@@ -370,8 +450,11 @@ def main(argv=None) -> int:
     ctas = parse_ctas(args.ctas)
     tuning = None
     if args.backend == "native" and (args.ctas == "tune" or (args.ctas == "auto" and env.world > 1)):
-        ctas, tuning = tune_ctas(env, device, nbytes, args, tdev, barrier_kw)
+        pred = len(TUNE_CANDIDATES) * (3.0 + (args.tune_steps + 1) * nbytes / 50e9)
+        if ph.allow("tune", pred, agree):
+            ctas, tuning = ph.run("tune", tune_ctas, env, device, nbytes, args, tdev, barrier_kw)
     runner = None
+    t_comm = time.perf_counter()
     if args.backend == "native":
         # The native communicator (csrc/rccl) is the measured path; if its extension cannot be
         # loaded on some rank, every rank falls back together to dist.all_reduce (the same RCCL).
@@ -391,26 +474,34 @@ def main(argv=None) -> int:
             args.backend = "torch"
     if runner is None:
         runner = AllReduceRunner(env, device, nbytes, args.dtype, backend=args.backend, inplace=args.inplace)
-    wrong = torch.tensor([runner.check()], dtype=torch.int64, device=tdev)
+    comm_s = time.perf_counter() - t_comm
+    ph.s["comm"] = round(comm_s, 3)
+    wrong = torch.tensor([ph.run("check", runner.check)], dtype=torch.int64, device=tdev)
     dist.all_reduce(wrong)
     if int(wrong.item()) != 0:
         print(f"bench: all-reduce correctness check FAILED ({int(wrong.item())} wrong elements)", file=sys.stderr)
         return 3
 
-    for _ in range(args.warmup):
-        runner.step()
-    runner.synchronize()
+    def warm():
+        for _ in range(args.warmup):
+            runner.step()
+        runner.synchronize()
 
-    dist.barrier(**barrier_kw)
-    gpu_sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        runner.step()
-    runner.synchronize()
-    gpu_sync()
-    elapsed = time.perf_counter() - t0
-    dist.barrier(**barrier_kw)
+    ph.run("warmup", warm)
 
+    def headline():
+        dist.barrier(**barrier_kw)
+        gpu_sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            runner.step()
+        runner.synchronize()
+        gpu_sync()
+        el = time.perf_counter() - t0
+        dist.barrier(**barrier_kw)
+        return el
+
+    elapsed = ph.run("headline", headline)
     t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -419,26 +510,29 @@ def main(argv=None) -> int:
     busbw = algbw * bus_factor(env.world)
     value = busbw if env.world > 1 else algbw
     headline_bytes = runner.nbytes
+    step_s = ms_per_step / 1e3
     sweep = None
     sizes = sweep_sizes(args.sweep, cpu=cpu)
-    if sizes:
+    if sizes and ph.allow("sweep", _sweep_cost(sizes, algbw), agree):
         try:  # supplementary: a failure here (e.g. no memory for 2 x 16 GiB) must not cost the headline
-            sweep = run_sweep(runner, sizes, env, tdev, barrier_kw, gpu_sync)
+            sweep = ph.run("sweep", run_sweep, runner, sizes, env, tdev, barrier_kw, gpu_sync)
         except Exception as e:  # noqa: BLE001 - every rank runs the same sizes, so all land here together
             print(f"bench: size sweep aborted on rank {env.rank}: {e}", file=sys.stderr)
             sweep = {"error": str(e)[:300]}
     other = None
-    if args.fp32_check and runner.comm is not None and args.dtype != "fp32":
+    fp32_steps = max(1, min(args.steps, 20))
+    if args.fp32_check and runner.comm is not None and args.dtype != "fp32" \
+            and ph.allow("fp32", (fp32_steps + 2) * step_s + 1.0, agree):
         try:  # supplementary, like the sweep
-            other = run_other_dtype(runner, headline_bytes, "fp32", env, tdev, barrier_kw, gpu_sync, max(1, min(args.steps, 20)))
+            other = ph.run("fp32", run_other_dtype, runner, headline_bytes, "fp32", env, tdev, barrier_kw, gpu_sync, fp32_steps)
         except Exception as e:  # noqa: BLE001
             print(f"bench: fp32 all-reduce aborted on rank {env.rank}: {e}", file=sys.stderr)
             other = {"dtype": "fp32", "error": str(e)[:300]}
     graph = None
     want_graph = args.graph == "on" or (args.graph == "auto" and env.world == 1)
-    if want_graph and sizes and runner.comm is not None and not args.inplace:
+    if want_graph and sizes and runner.comm is not None and not args.inplace and ph.allow("graph", 3.0, agree):
         try:  # supplementary, like the sweep
-            graph = run_graph_latency(runner, [8, 4096, 65536, 1 << 20], env, tdev, barrier_kw, gpu_sync)
+            graph = ph.run("graph", run_graph_latency, runner, [8, 4096, 65536, 1 << 20], env, tdev, barrier_kw, gpu_sync)
         except Exception as e:  # noqa: BLE001
             print(f"bench: graph latency aborted on rank {env.rank}: {e}", file=sys.stderr)
             graph = {"error": str(e)[:300]}
@@ -446,9 +540,10 @@ def main(argv=None) -> int:
     want_ab = args.ab_worst == "on" or (args.ab_worst == "auto" and bool(choice.worst))
     # a second communicator on other devices: the native RCCL comm (takes its device) or gloo on the CPU;
     # the torch backend's process group is bound to this rank's device
-    if want_ab and choice.worst and (cpu or (choice.worst_hip and runner.comm is not None)):
+    if want_ab and choice.worst and (cpu or (choice.worst_hip and runner.comm is not None)) \
+            and ph.allow("ab_worst", comm_s + (max(1, args.warmup // 2) + min(args.steps, 20) + 1) * step_s, agree):
         try:  # supplementary, like the sweep: a failure is reported, never costs the headline
-            worst_ab = measure_worst(env, choice, headline_bytes, args, tdev, barrier_kw, args.backend, ctas)
+            worst_ab = ph.run("ab_worst", measure_worst, env, choice, headline_bytes, args, tdev, barrier_kw, args.backend, ctas)
         except Exception as e:  # noqa: BLE001 - every rank runs the same steps
             print(f"bench: worst-subset A/B aborted on rank {env.rank}: {e}", file=sys.stderr)
             worst_ab = {"subset": choice.worst, "error": str(e)[:300]}
@@ -468,7 +563,16 @@ def main(argv=None) -> int:
         except Exception as e:  # noqa: BLE001 - supplementary: never costs the headline line
             rccl = {"error": str(e)[:200]}
     if env.rank == 0:
-        bound = (choice.extra.get("probe") or {}).get("subset_ingress_bound_gbps")  # K5/K1 ceiling of busBW
+        probe = choice.extra.get("probe") or {}
+        ingress = probe.get("subset_ingress_bound_gbps")  # K5/K1: one GPU's ingress, others idle
+        ring_bound = (ring or {}).get("ring_bound_gbps")  # K6: every member loaded at once
+        bound = ring_bound or ingress
+        binds = []
+        for r in range(env.world):
+            try:
+                binds.append(json.loads(env.store.get(f"gtk/cpuset/{r}").decode()))
+            except Exception as e:  # noqa: BLE001 - reported, never costs the line
+                binds.append({"applied": False, "reason": str(e)[:100]})
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -501,8 +605,13 @@ def main(argv=None) -> int:
                 "probed": choice.probed,
                 "rccl_ctas": list(ctas) if ctas else "rccl-default",
             },
+            "phase_s": ph.report(),
+            "skipped_phases": ph.skipped,
+            "budget_s": args.budget_s,
+            "cpuset_applied": [{k: b.get(k) for k in ("applied", "source", "cpus", "n", "reason")} for b in binds],
             "ctas_tuning": tuning,
             "link_probe": choice.extra.get("probe"),
+            "ring_probe": ring,
             "k8s_placement": choice.extra.get("k8s"),
             "size_sweep": sweep,
             "fp32_headline": other,
@@ -513,6 +622,7 @@ def main(argv=None) -> int:
                                if worst_ab and worst_ab.get(("busbw_gbps" if env.world > 1 else "algbw_gbps")) else None),
             "value_kind": "busbw" if env.world > 1 else "algbw (busbw = 0 at k=1)",
             "busbw_vs_probe_bound": round(busbw / bound, 4) if bound else None,
+            "probe_bound_kind": "k6-ring" if ring_bound else ("k5-ingress" if ingress else None),
             "algbw_gbps": round(algbw, 3),
             "busbw_gbps": round(busbw, 3),
         }

@@ -11,7 +11,11 @@
 //   K4 mfma warm : v_mfma_f32_32x32x16_bf16 loop to lift clocks before timing, also reporting the
 //                  achieved dense bf16 rate.
 //   K5 gather    : one kernel on the reader pulls from all of its peers at once -> aggregate xGMI
-//                  ingress per GPU, the bound a ring all-reduce's busBW is measured against.
+//                  ingress per GPU with every other GPU idle.
+//   K6 ring      : every member of a subset runs the K5 gather from its peers at the same time
+//                  (ingress and egress of every GPU loaded together, as under a ring all-reduce):
+//                  the slowest member's ingress is the bound a ring all-reduce's busBW is measured
+//                  against.
 // The copy kernel exists in two staging forms (LDS-DMA and plain register staging) so the
 // rocprofv3 counter profile can show what LDS staging costs/buys on a pure stream (profiles/).
 //
@@ -425,6 +429,139 @@ py::dict gather_bw(int dst_dev, const std::vector<int>& srcs, size_t bytes, int 
   return r;
 }
 
+// K6 ring: every member of a subset gathers from its peers AT THE SAME TIME, so each GPU's xGMI
+// ingress and egress are loaded together, as they are under a ring all-reduce (K1 loads one
+// direction of one idle link; K5 loads one GPU's ingress with every other GPU idle).  Member m runs
+// the K5 gather kernel on its own stream of devs[m], pulling the source buffer of every member in
+// peers[m] into its own inbox; launches are interleaved across members so they overlap from the
+// first iteration.  A member's rate is the bytes it received / its own stream time; the subset's
+// ring bound is the slowest member (a ring all-reduce's busBW is every member's ingress rate, so
+// the slowest one caps it).  Members may repeat a device: on one GPU that checks the indexing.
+py::dict ring_bw(const std::vector<int>& devs, const std::vector<std::vector<int>>& peers, size_t bytes, int iters,
+                 int warmup, int blocks_per_cu) {
+  const int k = (int)devs.size();
+  if (k < 2 || k > kMaxSrc + 1) throw std::invalid_argument("2..17 ring members");
+  if ((int)peers.size() != k) throw std::invalid_argument("one peer list per member");
+  if (bytes < 16 || bytes % 16) throw std::invalid_argument("bytes must be a positive multiple of 16");
+  if (iters < 1) throw std::invalid_argument("iters >= 1");
+  int ndev = 0;
+  HIP_CHECK(hipGetDeviceCount(&ndev));
+  for (int d : devs)
+    if (d < 0 || d >= ndev) throw std::invalid_argument("device index out of range");
+  for (int m = 0; m < k; ++m) {
+    if (peers[m].empty() || peers[m].size() > (size_t)kMaxSrc) throw std::invalid_argument("1..16 peers per member");
+    for (int p : peers[m])
+      if (p < 0 || p >= k || p == m) throw std::invalid_argument("peers are other members' indices");
+  }
+  auto seed_of = [](int m) { return 0x6a09e667u ^ (unsigned)(m * 7919 + 1); };
+  std::vector<double> ms_member(k, 0.0);
+  double wall_ms = 0.0;
+  bool ok = true;
+  {
+    py::gil_scoped_release nogil;
+    for (int m = 0; m < k; ++m)
+      for (int p : peers[m]) enable_peer(devs[m], devs[p]);
+    std::vector<std::unique_ptr<DevBuf>> src, inbox;
+    for (int m = 0; m < k; ++m) {
+      src.emplace_back(new DevBuf(devs[m], bytes));
+      inbox.emplace_back(new DevBuf(devs[m], bytes * peers[m].size()));
+      DeviceGuard g(devs[m]);
+      hipLaunchKernelGGL(fill_pattern_kernel, dim3(num_cus(devs[m]) * 4), dim3(kBlock), 0, 0, (unsigned int*)src[m]->p,
+                         bytes / 4, seed_of(m));
+      HIP_CHECK(hipGetLastError());
+      HIP_CHECK(hipDeviceSynchronize());
+    }
+    std::vector<SrcSet> sets(k);
+    std::vector<int> grid(k);
+    std::vector<hipStream_t> st(k, nullptr);
+    std::vector<hipEvent_t> e0(k, nullptr), e1(k, nullptr);
+    for (int m = 0; m < k; ++m) {
+      const int ns = (int)peers[m].size();
+      for (int i = 0; i < ns; ++i) sets[m].p[i] = reinterpret_cast<const u32x4*>(src[peers[m][i]]->p);
+      // members sharing a device split its CUs, so the self-test does not oversubscribe one GPU
+      int share = 0;
+      for (int d : devs) share += (d == devs[m]);
+      const int per = std::max(1, num_cus(devs[m]) * std::max(1, blocks_per_cu) / (ns * share));
+      grid[m] = per * ns;
+      DeviceGuard g(devs[m]);
+      HIP_CHECK(hipStreamCreateWithFlags(&st[m], hipStreamNonBlocking));
+      HIP_CHECK(hipEventCreate(&e0[m]));
+      HIP_CHECK(hipEventCreate(&e1[m]));
+    }
+    auto launch_round = [&]() {
+      for (int m = 0; m < k; ++m) {
+        DeviceGuard g(devs[m]);
+        hipLaunchKernelGGL(gather_lds_kernel, dim3(grid[m]), dim3(kBlock), 0, st[m], sets[m], (int)peers[m].size(),
+                           (u32x4*)inbox[m]->p, bytes / 16);
+        HIP_CHECK(hipGetLastError());
+      }
+    };
+    auto sync_all = [&]() {
+      for (int m = 0; m < k; ++m) {
+        DeviceGuard g(devs[m]);
+        HIP_CHECK(hipStreamSynchronize(st[m]));
+      }
+    };
+    for (int i = 0; i < warmup; ++i) launch_round();
+    sync_all();
+    auto t0 = std::chrono::steady_clock::now();
+    for (int m = 0; m < k; ++m) {
+      DeviceGuard g(devs[m]);
+      HIP_CHECK(hipEventRecord(e0[m], st[m]));
+    }
+    for (int i = 0; i < iters; ++i) launch_round();
+    for (int m = 0; m < k; ++m) {
+      DeviceGuard g(devs[m]);
+      HIP_CHECK(hipEventRecord(e1[m], st[m]));
+    }
+    sync_all();
+    wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    for (int m = 0; m < k; ++m) {
+      DeviceGuard g(devs[m]);
+      float ms = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&ms, e0[m], e1[m]));
+      ms_member[m] = ms;
+      (void)hipEventDestroy(e0[m]);
+      (void)hipEventDestroy(e1[m]);
+      (void)hipStreamDestroy(st[m]);
+    }
+    // every inbox segment holds its peer's pattern (head and tail windows)
+    const size_t words = bytes / 4, win = std::min<size_t>(words, 1 << 14);
+    std::vector<unsigned int> h(win);
+    for (int m = 0; m < k && ok; ++m) {
+      DeviceGuard g(devs[m]);
+      for (size_t i = 0; i < peers[m].size() && ok; ++i) {
+        const unsigned int seed = seed_of(peers[m][i]);
+        for (size_t st0 : {(size_t)0, words - win}) {
+          HIP_CHECK(hipMemcpy(h.data(), (const unsigned int*)inbox[m]->p + i * words + st0, win * 4, hipMemcpyDeviceToHost));
+          for (size_t w = 0; w < win; ++w)
+            if (h[w] != ((unsigned int)((st0 + w) * 2654435761u) ^ seed)) {
+              ok = false;
+              break;
+            }
+        }
+      }
+    }
+  }
+  py::dict r;
+  std::vector<double> gbps(k);
+  double bound = 0.0;
+  for (int m = 0; m < k; ++m) {
+    gbps[m] = (double)bytes * peers[m].size() * iters / (ms_member[m] / 1e3) / 1e9;
+    bound = (m == 0) ? gbps[m] : std::min(bound, gbps[m]);
+  }
+  r["devs"] = devs;
+  r["peers"] = peers;
+  r["bytes_per_peer"] = bytes;
+  r["iters"] = iters;
+  r["ms_member"] = ms_member;
+  r["wall_ms"] = wall_ms;
+  r["ingress_gbps"] = gbps;
+  r["bound_gbps"] = bound;
+  r["ok"] = ok;
+  return r;
+}
+
 py::dict to_dict(const CopyResult& c) {
   py::dict r;
   r["src"] = c.src;
@@ -579,6 +716,8 @@ PYBIND11_MODULE(_probe, m) {
         py::arg("blocks_per_cu") = kBlocksPerCU);
   m.def("gather_bw", &gather_bw, py::arg("dst_dev"), py::arg("srcs"), py::arg("bytes") = (size_t)64 << 20,
         py::arg("iters") = 3, py::arg("warmup") = 1, py::arg("blocks_per_cu") = kBlocksPerCU);
+  m.def("ring_bw", &ring_bw, py::arg("devs"), py::arg("peers"), py::arg("bytes") = (size_t)64 << 20, py::arg("iters") = 3,
+        py::arg("warmup") = 1, py::arg("blocks_per_cu") = kBlocksPerCU);
   m.def("mfma_warmup", &mfma_warmup, py::arg("dev"), py::arg("target_ms") = 50.0, py::arg("iters_per_launch") = 4096);
   m.def("probe_matrix", &probe_matrix, py::arg("devs"), py::arg("bytes") = (size_t)256 << 20, py::arg("iters") = 5,
         py::arg("warmup") = 1, py::arg("mode") = "read", py::arg("kind") = "lds", py::arg("nontemporal") = false,

@@ -2,6 +2,7 @@
 
   topo      discover the node (amdsmi / sysfs / fake) and print the matrix, JSON or annotations
   probe     run the HIP link probe (MFMA warm-up + LDS-staged copies) and print GB/s / cost
+  ring      K6: every member of a subset pulls from its peers at once; the busBW ceiling of a ring
   select    run the placement core on a topology (file, discovery or fake) for k devices
   config    emit the scheduler config: ``scheduler`` (KubeSchedulerConfiguration), ``policy``
             (the reference's legacy Policy JSON, design.md:92-113) or ``manifests`` (deploy YAML)
@@ -71,6 +72,19 @@ def cmd_probe(a) -> int:
                 f.write(t.to_json())
     print(t.render())
     print(json.dumps({"probe": t.probe, "hbm_gbps": [None if x != x else round(float(x), 1) for x in t.hbm_gbps]}))
+    return 0
+
+
+def cmd_ring(a) -> int:
+    """K6 concurrent ring probe over HIP ordinals (``--devices``) or a node-local GROUP resolved by
+    PCI address; prints one JSON line with ``ring_bound_gbps``."""
+    from .ops.probe import measure_ring
+
+    devs = validate_devices(a)
+    if len(devs) < 2:
+        print("gtk ring: needs at least 2 devices", file=sys.stderr)
+        return 2
+    print(json.dumps(measure_ring(devs, preset=a.preset, patterns=[p for p in a.patterns.split(",") if p])))
     return 0
 
 
@@ -289,6 +303,15 @@ def main(argv=None) -> int:
     p.add_argument("--ingress", action="store_true", help="also measure each GPU's all-peer ingress (K5 gather)")
     p.add_argument("--out", default="")
     p.set_defaults(fn=cmd_probe)
+    p = sub.add_parser("ring", help="K6: concurrent ring-pattern probe of a device subset (busBW ceiling)")
+    p.add_argument("--devices", default="", help="HIP ordinals (skips GROUP resolution)")
+    p.add_argument("--group", default="", help="node-local device indices (default: $GTK_GPU_GROUP)")
+    p.add_argument("--bdfs", default="", help="PCI addresses of --group, same order (default: $GTK_GPU_BDFS)")
+    p.add_argument("--topology", default="", help="node topology JSON mapping GROUP indices to PCI addresses")
+    p.add_argument("--visible-bdfs", default=None, help=argparse.SUPPRESS)
+    p.add_argument("--preset", default="quick", choices=["quick", "full"])
+    p.add_argument("--patterns", default="all,ring", help="K6 peer patterns: all (every link of the subset), ring (pred+succ)")
+    p.set_defaults(fn=cmd_ring)
     p = sub.add_parser("select")
     disc(p)
     p.add_argument("-k", type=int, default=0)

@@ -94,6 +94,12 @@ def main(argv=None) -> int:
                     help="re-measure the links (child process) every N s while no pod holds a device; 0 = never")
     ap.add_argument("--reprobe-tolerance", type=float, default=0.15,
                     help="republish the topology when a measured pair moved by more than this fraction")
+    ap.add_argument("--probe-mark-seconds", type=float, default=300.0,
+                    help="a re-probe marks the node <prefix>/probing for at most this long; the extender skips it meanwhile")
+    ap.add_argument("--probe-settle-seconds", type=float, default=2.0,
+                    help="after marking, wait this long for binds already in flight before re-checking that the node is idle")
+    ap.add_argument("--probe-yield-seconds", type=float, default=20.0,
+                    help="an Allocate arriving mid-probe cancels it and waits at most this long for the GPUs to be released")
     ap.add_argument("--partition-aware", default="on", choices=["on", "off"],
                     help="GetPreferredAllocation on CPX/DPX/QPX nodes: group XCPs by physical GPU (on) or not (off)")
     ap.add_argument("--nic-env", default="on", choices=["on", "off"],
@@ -143,6 +149,8 @@ def main(argv=None) -> int:
                        node_name=a.node_name, contract=contract, device_specs=specs, prestart_validate=a.prestart_validate,
                        health_interval=a.health_interval, reprobe_interval=a.reprobe_interval,
                        reprobe_tolerance=a.reprobe_tolerance, pod_resources_socket=a.pod_resources_socket,
+                       probe_mark_s=a.probe_mark_seconds, probe_settle_s=a.probe_settle_seconds,
+                       probe_yield_s=a.probe_yield_seconds,
                        reconcile_interval=a.reconcile_interval, cdi_dir=a.cdi_dir, nic_env=a.nic_env == "on",
                        share_cu_mask=a.share_cu_mask == "on",
                        policy=PlacementPolicy(partition_aware=a.partition_aware == "on"))
@@ -155,8 +163,10 @@ def main(argv=None) -> int:
     if (a.reprobe_interval > 0 or events is not None) and a.discovery != "fake":
         from ..ops.probe import probe_in_child
 
-        def reprobe():
-            probed = probe_in_child(a.probe if a.probe != "off" else "quick", backend=a.discovery)[0]
+        def reprobe(cancel=None):
+            # an Allocate arriving mid-probe sets `cancel`: the probe child is killed and the pod's
+            # container starts on released links (plugin.reprobe)
+            probed = probe_in_child(a.probe if a.probe != "off" else "quick", backend=a.discovery, cancel=cancel)[0]
             return None if probed is None else time_slice(probed, a.time_slices)
     plugin = DevicePluginServer(topo, cfg, api=api, health_fn=health if a.discovery != "fake" else None, reprobe_fn=reprobe)
     plugin.event_source = events

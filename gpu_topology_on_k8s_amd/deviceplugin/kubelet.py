@@ -57,6 +57,7 @@ class FakeKubelet:
         self.plugins: Dict[str, _Plugin] = {}
         self.allocated: Dict[str, Dict[str, Tuple[str, ...]]] = {}  # resource -> pod key -> ids
         self.responses: Dict[str, object] = {}  # pod key -> AllocateResponse
+        self.rejected: List[Tuple[str, str]] = []  # (pod key, reason) of pods whose admission failed
         self._server: Optional[grpc.Server] = None
         self._lock = threading.RLock()
         self._stop = threading.Event()
@@ -174,34 +175,54 @@ class FakeKubelet:
             used = {i for ids in self.allocated.get(resource, {}).values() for i in ids}
             return sorted((d for d, h in p.devices.items() if h == pb.HEALTHY and d not in used), key=int)
 
-    def admit(self, pod: dict, resource: str, container_split: Optional[Sequence[int]] = None):
-        """Allocate devices for ``pod``: GetPreferredAllocation (if offered) then Allocate."""
+    def _reject(self, pod: dict, msg: str) -> AdmissionError:
+        """Pod admission failed: like the real kubelet, the pod is terminal (``Failed``, reason
+        ``UnexpectedAdmissionError``) and is never retried on this node; a bare pod is lost."""
+        self.rejected.append((pod_key(pod), msg))
+        if self.api is not None and hasattr(self.api, "set_pod_phase"):
+            md = meta(pod)
+            try:
+                self.api.set_pod_phase(md.get("namespace", "default"), md["name"], "Failed", reason="UnexpectedAdmissionError",
+                                       message=msg)
+            except Exception:  # pragma: no cover
+                pass
+        return AdmissionError(f"UnexpectedAdmissionError: {msg}")
+
+    def admit(self, pod: dict, resource: str, container_split: Optional[Sequence[int]] = None,
+              allocate_timeout: float = 10.0):
+        """Allocate devices for ``pod``: GetPreferredAllocation (if offered) then Allocate.  Any error
+        of either call, or too few devices, rejects the pod for good (:meth:`_reject`) as the kubelet's
+        device manager does; a missing device node or a failed PreStartContainer only fails the
+        container start (retried by the kubelet), so the pod stays Pending."""
         key = pod_key(pod)
         p = self.plugins.get(resource)
         k = pod_gpu_request(pod, [resource] + [r for r in self.plugins if r != resource])
         if k == 0:
             return None
         if p is None:
-            raise AdmissionError(f"no device plugin registered for {resource}")
+            raise self._reject(pod, f"no device plugin registered for {resource}")
         with self._lock:
             avail = self.available(resource)
             if len(avail) < k:
-                raise AdmissionError(f"UnexpectedAdmissionError: requested {k}, available {len(avail)}")
+                raise self._reject(pod, f"requested {k} of {resource}, available {len(avail)}")
             chosen: List[str] = avail[:k]
-            if getattr(p.options, "get_preferred_allocation_available", False):
-                req = pb.PreferredAllocationRequest()
-                req.container_requests.add(available_deviceIDs=avail, allocation_size=k)
-                pref = self._stub(p, "GetPreferredAllocation")(req, timeout=5)
-                ids = list(pref.container_responses[0].deviceIDs)
-                if len(ids) == k and set(ids) <= set(avail):
-                    chosen = ids
-            split = list(container_split or [k])
-            areq = pb.AllocateRequest()
-            pos = 0
-            for n in split:
-                areq.container_requests.add(devices_ids=chosen[pos:pos + n])
-                pos += n
-            resp = self._stub(p, "Allocate")(areq, timeout=10)
+            try:
+                if getattr(p.options, "get_preferred_allocation_available", False):
+                    req = pb.PreferredAllocationRequest()
+                    req.container_requests.add(available_deviceIDs=avail, allocation_size=k)
+                    pref = self._stub(p, "GetPreferredAllocation")(req, timeout=5)
+                    ids = list(pref.container_responses[0].deviceIDs)
+                    if len(ids) == k and set(ids) <= set(avail):
+                        chosen = ids
+                split = list(container_split or [k])
+                areq = pb.AllocateRequest()
+                pos = 0
+                for n in split:
+                    areq.container_requests.add(devices_ids=chosen[pos:pos + n])
+                    pos += n
+                resp = self._stub(p, "Allocate")(areq, timeout=allocate_timeout)
+            except grpc.RpcError as e:
+                raise self._reject(pod, f"device plugin call failed: {e.code()}: {e.details()}") from e
             # what containerd does next: every DeviceSpec must name a device node that exists on the
             # host, or the container is never created (BASELINE config 1 on a kind node)
             missing = [d.host_path for c in resp.container_responses for d in c.devices if not os.path.exists(d.host_path)]

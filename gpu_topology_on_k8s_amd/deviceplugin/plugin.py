@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import json
 import logging
+import math
 import os
 import threading
 import time
@@ -133,7 +134,8 @@ class PluginConfig:
                  prestart_validate: bool = False, validate_timeout: float = 120.0,
                  pod_resources_socket: Optional[str] = POD_RESOURCES_SOCKET, reconcile_interval: float = 10.0,
                  cdi_dir: str = "/var/run/cdi", cdi_kind: str = "amd.com/gpu", nic_env: bool = True,
-                 share_cu_mask: bool = True):
+                 share_cu_mask: bool = True, probe_mark_s: float = 300.0, probe_settle_s: float = 2.0,
+                 probe_yield_s: float = 20.0):
         self.resource_name = resource_name
         self.socket_dir = socket_dir
         self.socket_name = socket_name
@@ -150,6 +152,12 @@ class PluginConfig:
         # republish when any measured pair moved by more than `reprobe_tolerance` (relative)
         self.reprobe_interval = reprobe_interval
         self.reprobe_tolerance = reprobe_tolerance
+        # a re-probe marks the node `<prefix>/probing` for at most `probe_mark_s` (the extender skips
+        # it), waits `probe_settle_s` for binds already in flight, and an Allocate arriving mid-probe
+        # waits at most `probe_yield_s` for the cancelled probe to release the GPUs
+        self.probe_mark_s = probe_mark_s
+        self.probe_settle_s = probe_settle_s
+        self.probe_yield_s = probe_yield_s
         # Allocate's DeviceSpecs: "strict" = /dev/kfd + every device's render/card node, Allocate fails
         # if one is missing on the node (a container must never start without its GPU); "stub" = only
         # the nodes that exist under dev_root (a kind node with fake GPUs has none: envs + annotations
@@ -203,7 +211,9 @@ class DevicePluginServer:
         self._stop = threading.Event()
         self._threads: List[threading.Thread] = []
         self._alloc_lock = threading.Lock()
+        self._alloc_cond = threading.Condition(self._alloc_lock)  # Allocate waits here for a probe to yield
         self._probing = False  # set (under _alloc_lock) while an idle-time re-probe owns the links
+        self._cancel = threading.Event()  # set by an Allocate arriving mid-probe: the probe stops
         self.allocations: List[Tuple[str, Tuple[int, ...]]] = []  # (pod key or "", ids) log
         self.registered = 0
         self.metrics = PluginMetrics()
@@ -295,27 +305,75 @@ class DevicePluginServer:
             return 0.0
         return float(np.max(np.abs(b[fa] - a[fa]) / np.maximum(a[fa], 1e-9)))
 
+    def _mark_probing(self, until: Optional[float]) -> bool:
+        """Set (``until`` = deadline) or clear (None) the node's ``<prefix>/probing`` mark, which the
+        extender's filter, sort and bind honour.  -> whether the apiserver took it."""
+        if self.api is None or not self.cfg.node_name:
+            return False
+        try:
+            self.api.patch_node(self.cfg.node_name, annotations={
+                self.cfg.contract.probing_key: None if until is None else str(int(math.ceil(until)))})
+            return True
+        except Exception as e:  # noqa: BLE001 - an unmarked node is never probed; a stale mark expires
+            log.warning("%s the probing mark on %s failed: %s", "clearing" if until is None else "setting",
+                        self.cfg.node_name, e)
+            return False
+
+    def _call_reprobe(self):
+        """``reprobe_fn(cancel=event)`` when it takes a cancel event (the child-process probe kills its
+        child when an Allocate arrives), else ``reprobe_fn()``."""
+        import inspect
+
+        try:
+            takes_cancel = "cancel" in inspect.signature(self.reprobe_fn).parameters
+        except (TypeError, ValueError):
+            takes_cancel = False
+        return self.reprobe_fn(cancel=self._cancel) if takes_cancel else self.reprobe_fn()
+
     def reprobe(self) -> bool:
         """One idle-time re-measurement; republish if the links moved.  -> republished.
 
-        While it runs ``Allocate`` is refused (UNAVAILABLE: the kubelet retries), so no container
-        starts on links the probe is saturating; idleness is checked under the same lock before and
-        again after the probe, and a result taken while a pod arrived is dropped (its traffic would
-        skew the matrix)."""
+        The kubelet never retries a failed ``Allocate`` (the pod is rejected for good), so a probe must
+        not refuse one.  Instead (``design.md:236-246``: Allocate hands a pod its devices):
+          1. the node is marked ``<prefix>/probing: <deadline>``, so the extender stops choosing it;
+          2. after ``probe_settle_s`` (a bind already past the extender's check lands in that window)
+             the node must still be idle, or the mark is cleared and nothing runs;
+          3. an ``Allocate`` arriving while the probe runs cancels it (the probe child is killed) and
+             waits, at most ``probe_yield_s``, for the links to be released, then proceeds;
+          4. the mark is cleared; a cancelled probe, or one a pod arrived during, is discarded (its
+             traffic would skew the matrix)."""
         if self.reprobe_fn is None:
             return False
-        with self._alloc_lock:
-            if not self.node_idle():
-                self.metrics.reprobes.labels("busy").inc()
-                return False
-            self._probing = True
+        if not self.node_idle():
+            self.metrics.reprobes.labels("busy").inc()
+            return False
+        if not self._mark_probing(self.clock() + self.cfg.probe_mark_s):
+            self.metrics.reprobes.labels("unmarked").inc()
+            return False
         try:
-            new = self.reprobe_fn()
+            if self.cfg.probe_settle_s > 0 and self._stop.wait(self.cfg.probe_settle_s):
+                return False
+            with self._alloc_cond:
+                if not self.node_idle():
+                    self.metrics.reprobes.labels("busy").inc()
+                    return False
+                self._cancel = threading.Event()
+                self._probing = True
+            try:
+                new = self._call_reprobe()
+            finally:
+                with self._alloc_cond:
+                    self._probing = False
+                    cancelled = self._cancel.is_set()
+                    still_idle = self.node_idle()
+                    self._alloc_cond.notify_all()
         finally:
-            with self._alloc_lock:
-                self._probing = False
-                still_idle = self.node_idle()
+            self._mark_probing(None)
         self.reprobes += 1
+        if cancelled:
+            log.warning("link re-probe: cancelled by an Allocate; the measurement is discarded")
+            self.metrics.reprobes.labels("cancelled").inc()
+            return False
         if not still_idle:
             log.warning("link re-probe: a pod claimed devices during the probe; discarding the measurement")
             self.metrics.reprobes.labels("discarded").inc()
@@ -435,10 +493,18 @@ class DevicePluginServer:
         missing = self._missing_device_nodes(all_ids)
         if missing:
             self._refuse(context, grpc.StatusCode.FAILED_PRECONDITION, f"device nodes missing on this node: {missing}", "missing")
-        with self._alloc_lock:
+        with self._alloc_cond:
             if self._probing:
-                self.metrics.allocations.labels("probing").inc()
-                context.abort(grpc.StatusCode.UNAVAILABLE, "link probe in progress; retry")
+                # never refuse (the kubelet would reject the pod for good): the probe yields — its
+                # child is killed — and the container starts once the links are released
+                self._cancel.set()
+                self.metrics.allocations.labels("probe_yield").inc()
+                deadline = time.monotonic() + self.cfg.probe_yield_s
+                while self._probing and time.monotonic() < deadline:
+                    self._alloc_cond.wait(deadline - time.monotonic())
+                if self._probing:
+                    log.warning("Allocate of %s: the link probe did not yield within %.0fs; allocating anyway",
+                                sorted(set(all_ids)), self.cfg.probe_yield_s)
             pod = self._claim_pod(sorted(set(all_ids)))
         extra_env = self._rccl_env(pod) if pod is not None else {}
         for creq in request.container_requests:

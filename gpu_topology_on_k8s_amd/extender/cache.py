@@ -22,7 +22,7 @@ import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, Iterable, List, Optional, Set, Tuple
 
-from ..k8s.annotations import Contract, PodAssignment, decode_node_annotations
+from ..k8s.annotations import Contract, PodAssignment, decode_node_annotations, probing_until
 from ..k8s.api import KubeAPI
 from ..k8s.objects import annotations as obj_annotations
 from ..k8s.objects import labels as obj_labels
@@ -55,6 +55,7 @@ class NodeState:
     unknown_pods: Dict[str, int] = field(default_factory=dict)  # pod -> devices held without a GROUP annotation
     unknown_uids: Dict[str, str] = field(default_factory=dict)  # pod UID -> pod key of unknown_pods
     capacity: int = -1  # node.status.allocatable[resource] (-1 = unknown)
+    probing_until: float = 0.0  # the device plugin's re-probe mark (<prefix>/probing): skip the node until then
     synced_at: float = 0.0
     list_epoch: int = -1  # epoch of the newest pod LIST applied (older LISTs arriving late are stale)
     lock: threading.RLock = field(default_factory=threading.RLock, repr=False)
@@ -141,6 +142,7 @@ class ClusterCache:
                     st.topology = None
                 st.node_rv = rv
             st.labels = labels
+            st.probing_until = probing_until(obj_annotations(node), self.contract)
             alloc = ((node.get("status") or {}).get("allocatable") or {})
             st.capacity = -1
             for r in self.resources:

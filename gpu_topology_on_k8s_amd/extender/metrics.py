@@ -36,6 +36,9 @@ class ExtenderMetrics:
         self.decision_cache = Counter("gtk_extender_decision_cache_total", "placement decisions served from / added to the cache",
                                       ["result"], registry=self.registry)
 
+        self.probing_skips = Counter("gtk_extender_probing_skips_total",
+                                     "node evaluations skipped because the node's device plugin is re-probing its links",
+                                     registry=self.registry)
         self._hit, self._miss = self.decision_cache.labels(result="hit"), self.decision_cache.labels(result="miss")
         self._cache = None
 

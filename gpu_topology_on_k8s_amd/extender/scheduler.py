@@ -276,6 +276,11 @@ class TopologyExtender:
         _, fraction, numa, want, multi, mem = shape
         with st.lock:
             now = self.clock()
+            if st.probing_until > now:
+                # the device plugin is re-measuring the node's links (deviceplugin/plugin.py reprobe):
+                # a pod placed now would share them with the probe; not memoised (the mark expires)
+                self.metrics.probing_skips.inc()
+                return None, f"link probe in progress on this node (until {int(st.probing_until)})"
             if self._cacheable():
                 hit = st.memo.get(shape)
                 if hit is not None and hit[0] <= now <= hit[1]:

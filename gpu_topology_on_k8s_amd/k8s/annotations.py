@@ -29,7 +29,7 @@ from ..topology.model import LinkType, RefLinkClass, Topology
 __all__ = [
     "ANN_GROUP", "ANN_ASSIGNED", "ANN_ASSUME_TIME", "ANN_GPU_ID_ALIAS", "Contract", "PodAssignment",
     "encode_node_annotations", "decode_node_annotations", "pair_annotations", "parse_pair_annotations",
-    "parse_group", "format_group", "package_pair_annotations", "annotations_size",
+    "parse_group", "format_group", "package_pair_annotations", "annotations_size", "probing_until",
 ]
 
 ANN_GROUP = "ALIYUN_COM_GPU_GROUP"
@@ -58,6 +58,14 @@ class Contract:
     @property
     def probe_time_key(self) -> str:
         return f"{self.prefix}/probe-time"
+
+    @property
+    def probing_key(self) -> str:
+        """Node annotation set by the device plugin while an idle-time link re-probe owns the node's
+        xGMI links: the unix time until which the extender's filter / sort / bind skip the node (a
+        pod admitted mid-probe would share the links with the probe, and a crashed plugin's mark
+        expires on its own)."""
+        return f"{self.prefix}/probing"
 
     @property
     def numa_key(self) -> str:
@@ -192,6 +200,15 @@ def encode_node_annotations(t: Topology, contract: Contract = Contract(), with_p
         partitioned = len({g.physical for g in t.gpus}) < t.n
         ann.update(package_pair_annotations(t) if partitioned else pair_annotations(t))
     return ann
+
+
+def probing_until(ann: Mapping[str, str], contract: Contract = Contract()) -> float:
+    """Deadline of a node's re-probe mark (``<prefix>/probing``), 0 when absent or malformed."""
+    raw = ann.get(contract.probing_key)
+    try:
+        return float(raw) if raw not in (None, "") else 0.0
+    except (TypeError, ValueError):
+        return 0.0
 
 
 def annotations_size(ann: Mapping[str, str]) -> int:

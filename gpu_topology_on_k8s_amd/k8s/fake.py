@@ -186,10 +186,13 @@ class FakeAPIServer(KubeAPI):
             meta(pod)["resourceVersion"] = self._next_rv()
             self._emit("DELETED", "Pod", pod)
 
-    def set_pod_phase(self, namespace: str, name: str, phase: str) -> Obj:
+    def set_pod_phase(self, namespace: str, name: str, phase: str, reason: str = "", message: str = "") -> Obj:
         with self._lock:
             pod = self._pod(namespace, name)
-            pod.setdefault("status", {})["phase"] = phase
+            st = pod.setdefault("status", {})
+            st["phase"] = phase
+            if reason:  # e.g. the kubelet's UnexpectedAdmissionError
+                st["reason"], st["message"] = reason, message
             meta(pod)["resourceVersion"] = self._next_rv()
             self._emit("MODIFIED", "Pod", pod)
             return copy.deepcopy(pod)

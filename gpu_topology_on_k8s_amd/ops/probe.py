@@ -26,7 +26,8 @@ from ..topology.model import Topology
 log = logging.getLogger(__name__)
 
 __all__ = ["device_count", "device_props", "warmup", "copy_bw", "gather_bw", "measure_matrix", "measure_ingress",
-           "probe_topology", "probe_in_child", "ingress_bound", "PROBE_PRESETS"]
+           "probe_topology", "probe_in_child", "ingress_bound", "ring_peers", "ring_bw", "measure_ring", "ring_in_child",
+           "PROBE_PRESETS"]
 
 #: bytes per transfer / timed iterations; sizes exceed the 256 MiB Infinity Cache for "full".
 PROBE_PRESETS: Dict[str, Dict[str, int]] = {
@@ -61,6 +62,62 @@ def copy_bw(src: int, dst: int, nbytes: int = 256 << 20, iters: int = 10, warmup
 def gather_bw(dst: int, srcs: Sequence[int], nbytes: int = 64 << 20, iters: int = 3, warmup_iters: int = 1) -> Dict[str, object]:
     """K5: one kernel on ``dst`` reads ``nbytes`` from every device in ``srcs`` at once (aggregate ingress)."""
     return dict(_p().gather_bw(int(dst), [int(s) for s in srcs], int(nbytes), int(iters), int(warmup_iters)))
+
+
+def ring_peers(k: int, pattern: str = "all") -> List[List[int]]:
+    """Member indices each of ``k`` ring members pulls from in K6: ``all`` = every other member (the
+    union of the rings RCCL lays over a full mesh: every link of the subset, both directions);
+    ``ring`` = predecessor and successor of one bidirectional ring (2 links per member, 1 at k = 2)."""
+    if k < 2:
+        raise ValueError("a ring needs at least 2 members")
+    if pattern == "all":
+        return [[p for p in range(k) if p != m] for m in range(k)]
+    if pattern == "ring":
+        return [sorted({(m - 1) % k, (m + 1) % k} - {m}) for m in range(k)]
+    raise ValueError(f"pattern must be all|ring, got {pattern!r}")
+
+
+def ring_bw(devs: Sequence[int], pattern: str = "all", nbytes: int = 64 << 20, iters: int = 3,
+            warmup_iters: int = 1) -> Dict[str, object]:
+    """K6: every member (HIP ordinal ``devs[m]``) gathers from its ``pattern`` peers at the same time;
+    ``bound_gbps`` = the slowest member's ingress (the ceiling of a ring all-reduce's busBW)."""
+    r = dict(_p().ring_bw([int(d) for d in devs], ring_peers(len(devs), pattern), int(nbytes), int(iters), int(warmup_iters)))
+    r["pattern"] = pattern
+    return r
+
+
+def measure_ring(devs: Sequence[int], preset: str = "quick", patterns: Sequence[str] = ("all", "ring")) -> Dict[str, object]:
+    """K6 over the HIP ordinals ``devs`` for each pattern; ``ring_bound_gbps`` is the ``all`` pattern's
+    bound (every link of the subset loaded at once: what RCCL's rings do together on a full mesh)."""
+    cfg = PROBE_PRESETS[preset]
+    out: Dict[str, object] = {"devices": [int(d) for d in devs], "preset": preset, "bytes_per_peer": cfg["bytes"]}
+    for pat in patterns:
+        r = ring_bw(devs, pat, cfg["bytes"], cfg["iters"], cfg["warmup"])
+        if not r["ok"]:
+            raise RuntimeError(f"ring probe ({pat}) verification failed on devices {list(devs)}")
+        out[pat] = {"ingress_gbps": [round(float(x), 2) for x in r["ingress_gbps"]], "bound_gbps": round(float(r["bound_gbps"]), 2),
+                    "wall_ms": round(float(r["wall_ms"]), 3), "ms_member": [round(float(x), 3) for x in r["ms_member"]]}
+    if "all" in out:
+        out["ring_bound_gbps"] = out["all"]["bound_gbps"]
+    return out
+
+
+def ring_in_child(devs: Sequence[int], preset: str = "quick", timeout: float = 120.0) -> Tuple[Optional[Dict[str, object]], str]:
+    """:func:`measure_ring` in a child process (``gtk ring --devices``): the caller keeps no HIP
+    context or buffers on the subset's GPUs.  Returns ``(result | None, message)``."""
+    import json
+
+    cmd = [sys.executable, "-m", "gpu_topology_on_k8s_amd", "ring", "--devices", ",".join(str(int(d)) for d in devs),
+           "--preset", preset]
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=root)
+    except subprocess.TimeoutExpired:
+        return None, f"ring probe timed out after {timeout:.0f}s"
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return None, f"ring probe exited {p.returncode}: {(p.stderr or p.stdout).strip()[-400:]}"
+    return json.loads(lines[-1]), "ok"
 
 
 def _device_map(topo: Topology, dmap: Optional[DeviceMap]) -> DeviceMap:
@@ -230,14 +287,17 @@ def probe_topology(topo: Topology, preset: str = "quick", devs: Optional[List[in
 
 
 def probe_in_child(preset: str = "quick", backend: str = "auto", timeout: float = 150.0,
-                   ingress: bool = True) -> Tuple[Optional[Topology], str]:
+                   ingress: bool = True, cancel=None) -> Tuple[Optional[Topology], str]:
     """Discovery + K4 warm-up + K1 p2p read of every visible ordered pair (+ K5 ingress) in a CHILD
     process (``gtk probe --out``), returned as a probed :class:`Topology`.
 
     Long-lived callers (the device-plugin DaemonSet, rank 0 of the bench) must not keep HIP contexts
     and probe buffers on every GPU of the node: the child takes them and exits, and a failure there
     (fault, timeout) cannot take the caller down.  The pairwise matrix is written before the ingress
-    stage runs, so an ingress failure still returns it.  Returns ``(Topology | None, message)``."""
+    stage runs, so an ingress failure still returns it.  ``cancel`` (a ``threading.Event``): once set,
+    the child is killed and reaped — its GPU memory and queues are gone when this returns — and the
+    result is ``(None, "cancelled")`` (the device plugin yields its links to an arriving pod this
+    way).  Returns ``(Topology | None, message)``."""
     fd, path = tempfile.mkstemp(prefix="gtk_probe_", suffix=".json")
     os.close(fd)
     cmd = [sys.executable, "-m", "gpu_topology_on_k8s_amd", "probe", "--preset", preset, "--discovery", backend, "--out", path]
@@ -245,15 +305,28 @@ def probe_in_child(preset: str = "quick", backend: str = "auto", timeout: float 
         cmd.append("--ingress")
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     try:
-        p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=root)
-        err = f"probe exited {p.returncode}: {(p.stderr or p.stdout).strip()[-400:]}"
+        p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=root)
+        deadline = time.monotonic() + timeout
+        out = err_text = ""
+        while True:
+            try:
+                out, err_text = p.communicate(timeout=0.2)
+                break
+            except subprocess.TimeoutExpired:
+                if cancel is not None and cancel.is_set():
+                    p.kill()
+                    p.communicate()
+                    return None, "cancelled"
+                if time.monotonic() >= deadline:
+                    p.kill()
+                    p.communicate()
+                    return None, f"probe timed out after {timeout:.0f}s"
+        err = f"probe exited {p.returncode}: {(err_text or out).strip()[-400:]}"
         with open(path) as f:
             text = f.read()
         if not text:
             return None, err
         return Topology.from_json(text), ("ok" if p.returncode == 0 else "pairwise only; ingress stage failed: " + err)
-    except subprocess.TimeoutExpired:
-        return None, f"probe timed out after {timeout:.0f}s"
     except (OSError, ValueError, KeyError) as e:
         return None, f"probe output unreadable: {e}"
     finally:

@@ -66,8 +66,11 @@ def rccl_log_summary(text: str) -> Dict[str, object]:
             via[m.group(1)] = via.get(m.group(1), 0) + 1
         if version is None and "version" in line and ("RCCL" in line or "NCCL" in line):
             version = line.split("INFO", 1)[-1].strip()[:80]
+    # intra-node rings must ride xGMI peer access (P2P/IPC, P2P/direct pointer); SHM (host staging,
+    # e.g. under NCCL_P2P_DISABLE=1) or NET on a single node means the placement's links were bypassed
+    non_p2p = {k: v for k, v in via.items() if not k.startswith("P2P")}
     return {"communicators": len(comms), "nranks": sorted(set(comms)), "coll_channels": sorted(set(channels)),
-            "edges_via": via, "version": version}
+            "edges_via": via, "non_p2p_edges": non_p2p, "p2p_only": bool(via) and not non_p2p, "version": version}
 
 
 @dataclass
@@ -274,6 +277,10 @@ def choose_subset(k: int, probe: Optional[str] = None, backend: str = "auto", vi
                 objective, _ = evaluate(Problem.from_topology(topo, []), k8s["devices"], PlacementPolicy())
                 score = score_from_objective(objective)
             devices = list(k8s["devices"])
+    from ..topology.cpus import recommended_cpuset
+
+    # Gaia B6: each rank's share of the node's cores = the slice of its own device (bind_workload)
+    cpusets = [recommended_cpuset(topo, [d]) for d in devices]
     return SubsetChoice(
         devices=devices,
         score=round(score, 4),
@@ -286,7 +293,7 @@ def choose_subset(k: int, probe: Optional[str] = None, backend: str = "auto", vi
         hip_devices=[dmap.hip(i) for i in devices],
         worst_hip=[dmap.hip(i) for i in w.ids] if w else None,
         extra={"discovery_ms": round((t1 - t0) * 1e3, 2), "node_devices": topo.n, "visible_devices": nvis,
-               "device_map": dmap.to_dict(), "worst_exact": bool(w.exact) if w else None,
+               "device_map": dmap.to_dict(), "worst_exact": bool(w.exact) if w else None, "cpusets": cpusets,
                **({"probe": probe_summary(topo, devices)} if probed else {}),
                **({"k8s": k8s} if k8s is not None else {})},
     )

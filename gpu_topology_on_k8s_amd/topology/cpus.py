@@ -16,14 +16,19 @@ local_cpulist`` (``GPUInfo.cpu_affinity``) and the trained PCIe link against its
   socket are split evenly among the devices attached to it (SMT siblings stay together: every range
   of the cpulist is cut at the same fractions), and a pod is recommended the union of its devices'
   slices (``<prefix>/cpuset`` on the pod, ``GTK_CPUSET`` in the container).
+* :func:`apply_cpuset` — the binding itself: the training entry point, ``gtk validate`` and
+  ``bench.py`` pin their threads to ``GTK_CPUSET`` (or their own device's slice) intersected with
+  the container's allowed CPUs, and size the intra-op thread pools to it.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Iterable, List, Optional, Sequence, Set, Tuple
 
 import numpy as np
 
-__all__ = ["parse_cpulist", "format_cpulist", "device_core_slices", "recommended_cpuset", "access_costs"]
+__all__ = ["parse_cpulist", "format_cpulist", "device_core_slices", "recommended_cpuset", "apply_cpuset", "bind_workload",
+           "access_costs"]
 
 
 def _ranges(s: str) -> List[Tuple[int, int]]:
@@ -92,6 +97,78 @@ def recommended_cpuset(topo, ids: Sequence[int]) -> str:
     for i in ids:
         cpus |= sl.get(int(i), set())
     return format_cpulist(cpus)
+
+
+def _tasks() -> List[int]:
+    """Thread ids of this process (``/proc/self/task``); just this thread where procfs is absent."""
+    try:
+        return [int(t) for t in os.listdir("/proc/self/task")]
+    except OSError:
+        return [0]
+
+
+def apply_cpuset(spec: Optional[str], source: str = "GTK_CPUSET", threads: bool = True,
+                 allowed: Optional[Set[int]] = None, setter=None) -> Dict[str, object]:
+    """Gaia B6 in the workload: pin this process to ``spec ∩`` the CPUs it may use, and size the
+    intra-op thread pools to the result.
+
+    ``spec`` is a cpulist (the pod's ``GTK_CPUSET`` from Allocate, or the recommended slice of the
+    process's own device).  The intersection with ``os.sched_getaffinity(0)`` respects the container's
+    cgroup cpuset: a recommendation disjoint from it (the kubelet CPU manager gave the pod other
+    cores) is reported and not applied.  Every existing thread of the process is moved (threads made
+    later inherit the mask), then OpenMP / torch intra-op threads are set to the core count.
+    Returns ``{"applied", "source", "requested", "cpus", "n", "reason"}`` for the JSON report lines.
+    ``allowed`` / ``setter`` stand in for the OS calls in tests."""
+    want = parse_cpulist(spec or "")
+    have = set(os.sched_getaffinity(0)) if allowed is None else set(allowed)
+    rep: Dict[str, object] = {"applied": False, "source": source, "requested": format_cpulist(want), "cpus": "", "n": 0,
+                              "reason": ""}
+    if not want:
+        rep["reason"] = "no cpuset given"
+        return rep
+    eff = want & have
+    if not eff:
+        rep["reason"] = f"disjoint from the CPUs this process may use ({format_cpulist(have)})"
+        return rep
+    set_aff = setter or os.sched_setaffinity
+    moved = 0
+    for tid in _tasks() if setter is None else [0]:
+        try:
+            set_aff(tid, eff)
+            moved += 1
+        except OSError:  # a thread that exited meanwhile
+            continue
+    if moved == 0:
+        rep["reason"] = "sched_setaffinity failed"
+        return rep
+    if threads:
+        os.environ["OMP_NUM_THREADS"] = str(len(eff))
+        import sys
+
+        if "torch" in sys.modules:
+            sys.modules["torch"].set_num_threads(len(eff))
+    rep.update(applied=True, cpus=format_cpulist(eff), n=len(eff), threads_moved=moved)
+    return rep
+
+
+def bind_workload(mode: str = "auto", own: str = "", env: Optional[Dict[str, str]] = None, **kw) -> Dict[str, object]:
+    """The cpuset a workload process pins itself to, applied (:func:`apply_cpuset`).
+
+    ``mode``: ``off``; ``env`` = the pod's ``GTK_CPUSET`` only; ``auto`` = ``GTK_CPUSET`` narrowed to
+    ``own`` (the slice of this rank's own device, :func:`recommended_cpuset`) where they overlap — a
+    k-GPU pod is given the union of its devices' slices, and each rank takes its device's part — else
+    ``GTK_CPUSET``, else ``own`` (a bare-node run has no pod allocation)."""
+    env = os.environ if env is None else env
+    if mode == "off":
+        return {"applied": False, "source": "off", "requested": "", "cpus": "", "n": 0, "reason": "--cpu-bind off"}
+    pod = env.get("GTK_CPUSET", "")
+    if mode == "env":
+        return apply_cpuset(pod, "GTK_CPUSET", **kw)
+    if pod and own and parse_cpulist(pod) & parse_cpulist(own):
+        return apply_cpuset(format_cpulist(parse_cpulist(pod) & parse_cpulist(own)), "GTK_CPUSET&device-slice", **kw)
+    if pod:
+        return apply_cpuset(pod, "GTK_CPUSET", **kw)
+    return apply_cpuset(own, "device-slice", **kw)
 
 
 def access_costs(topo, prefer_numa: Optional[Sequence[int]] = None) -> Optional[np.ndarray]:

@@ -123,6 +123,21 @@ def test_bench_eight_ranks_gloo_dry_run():
     assert out["k8s_placement"]["assigned"] is True and len(out["k8s_placement"]["devices"]) == 8
     assert abs(out["busbw_gbps"] - out["algbw_gbps"] * 2 * 7 / 8) <= 1e-2 * out["busbw_gbps"] + 2e-3  # 3-decimal rounding
     assert out["size_sweep"]["all_exact"] and out["value_kind"] == "busbw"
+    ph = out["phase_s"]  # the first 8-GPU run explains itself: where its wall time went
+    for key in ("place", "comm", "check", "warmup", "headline", "sweep", "total"):
+        assert key in ph and ph[key] >= 0, ph
+    assert ph["total"] >= ph["headline"] and out["skipped_phases"] == []
+    assert len(out["cpuset_applied"]) == 8 and all("applied" in b for b in out["cpuset_applied"])
+
+
+def test_bench_tiny_budget_keeps_the_headline():
+    """--budget-s far below any phase's cost: every supplementary phase is skipped by all ranks
+    together, and the headline line still comes out, measured."""
+    out = _bench("--gpus", "2", "--backend", "cpu", "--steps", "2", "--warmup", "1", "--size-mb", "1", "--budget-s", "0.001")
+    assert out["value"] > 0 and out["steps"] == 2 and out["phase_s"]["headline"] > 0
+    skipped = {s["phase"] for s in out["skipped_phases"]}
+    assert "sweep" in skipped and out["size_sweep"] is None
+    assert "ab_worst" not in out["phase_s"] and "sweep" not in out["phase_s"]
 
 
 def test_bench_four_ranks_on_amdsmi_discovered_node():
@@ -167,3 +182,20 @@ def test_rccl_log_summary_parses_transports():
     s = rccl_log_summary(text)
     assert s["communicators"] == 1 and s["nranks"] == [2] and s["coll_channels"] == [32]
     assert s["edges_via"]["P2P/IPC"] == 2 and "RCCL version 2.27.7" in s["version"]
+    assert s["p2p_only"] is True and s["non_p2p_edges"] == {}
+
+
+def test_rccl_log_summary_flags_a_broken_transport():
+    """What an NCCL_P2P_DISABLE=1 run logs: ring edges through host shared memory.  The summary says
+    the ring left xGMI peer access, which the k >= 2 GPU test asserts against."""
+    from gpu_topology_on_k8s_amd.parallel.allreduce import rccl_log_summary
+
+    text = "\n".join([
+        "node:9:9 [0] NCCL INFO comm 0x77 rank 0 nRanks 2 nNodes 1 localRanks 2 localRank 0 MNNVL 0",
+        "node:9:9 [0] NCCL INFO Channel 00/02 : 0[0] -> 1[1] via SHM/direct/direct",
+        "node:9:9 [0] NCCL INFO Channel 01/02 : 0[0] -> 1[1] via SHM/direct/direct",
+        "node:9:9 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[1] via P2P/IPC",
+    ])
+    s = rccl_log_summary(text)
+    assert s["p2p_only"] is False and s["non_p2p_edges"] == {"SHM/direct/direct": 2}
+    assert rccl_log_summary("")["p2p_only"] is False  # no edges logged proves nothing

@@ -32,8 +32,15 @@ def test_mfma_warmup_rate(probe_mod):
     from gpu_topology_on_k8s_amd.ops.probe import warmup
 
     r = warmup(0, 30.0)
-    # dense bf16 peak ~2.5 PF; a 4-accumulator issue loop must at least clear 25% of it
-    assert r["tflops"] > 600, r
+    # dense bf16 peak ~2.5 PF; the 4-accumulator issue loop measured 2.03-2.09 PF (r02 driver smoke,
+    # BENCH_r02): the floor sits at ~75 % of that, so a 25 % regression fails
+    print(json.dumps({"mfma_tflops": round(r["tflops"], 1)}))
+    assert r["tflops"] > 1600, r
+
+
+# copy GB/s floors at 512 MiB (HBM moves twice that): ~75 % of what r02 measured for each form
+# (K3 LDS-DMA and register staging ~2.8 TB/s copy, the runtime blit ~2.4 TB/s; profiles/r02_copy)
+COPY_FLOOR_GBPS = {"lds": 2000.0, "reg": 2000.0, "sdma": 1700.0}
 
 
 @pytest.mark.parametrize("kind", ["lds", "reg", "sdma"])
@@ -42,7 +49,8 @@ def test_hbm_copy_kernels(probe_mod, kind):
 
     r = copy_bw(0, 0, 512 << 20, iters=5, warmup_iters=1, kind=kind)
     assert r["ok"], r
-    assert r["gbps"] > 1000, r  # 2x traffic: >2 TB/s of HBM
+    print(json.dumps({"kind": kind, "copy_gbps": round(r["gbps"], 1)}))
+    assert r["gbps"] > COPY_FLOOR_GBPS[kind], r
 
 
 def test_copy_odd_size_tail(probe_mod):
@@ -59,6 +67,31 @@ def test_gather_kernel_segments(probe_mod):
     assert r["ok"] and r["gbps"] > 100 and r["bytes_per_src"] == (16 << 20) + 4112
 
 
+@pytest.mark.parametrize("members,pattern", [(3, "all"), (4, "ring"), (2, "all")])
+def test_ring_kernel_segments(probe_mod, members, pattern):
+    """K6: every member gathers from its peers at once, each into its own inbox segments.  Here every
+    member lives on device 0 (its own source buffer and inbox); on a node they are the subset's GPUs,
+    same launches.  The odd size exercises the tails; each segment is checked against its peer."""
+    from gpu_topology_on_k8s_amd.ops.probe import ring_bw, ring_peers
+
+    r = ring_bw([0] * members, pattern, (8 << 20) + 4112, iters=2, warmup_iters=1)
+    assert r["ok"], r
+    assert r["peers"] == ring_peers(members, pattern)
+    assert len(r["ingress_gbps"]) == members and min(r["ingress_gbps"]) == pytest.approx(r["bound_gbps"])
+    assert r["bound_gbps"] > 50 and r["wall_ms"] > 0
+    print(json.dumps({"members": members, "pattern": pattern, "bound_gbps": round(r["bound_gbps"], 1)}))
+
+
+def test_ring_probe_child_cli():
+    """The bench's K6 path: ``gtk ring`` in a child process returns ring_bound_gbps (2 members on the
+    one device here)."""
+    from gpu_topology_on_k8s_amd.ops.probe import ring_in_child
+
+    r, msg = ring_in_child([0, 0], "quick", timeout=240)
+    assert r is not None, msg
+    assert r["ring_bound_gbps"] > 50 and r["all"]["bound_gbps"] == r["ring_bound_gbps"] and "ring" in r
+
+
 def test_probe_cli_ingress_single_gpu(tmp_path):
     out = tmp_path / "topo.json"
     p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd", "probe", "--preset", "quick", "--ingress", "--out", str(out)],
@@ -71,7 +104,7 @@ def test_probe_cli_ingress_single_gpu(tmp_path):
         assert d["probe"]["ingress_all_gbps"][0] is None  # one GPU: no peers to gather from
     else:
         assert all(x is not None and x > 0 for x in d["probe"]["ingress_all_gbps"])
-    assert d["hbm_gbps"][0] > 1000
+    assert d["hbm_gbps"][0] > 2000  # quick preset, 64 MiB self copy: ~3.2 TB/s measured (r02)
 
 
 def test_discover_real_node():
@@ -236,7 +269,7 @@ def test_device_plugin_daemon_probes_in_child_on_real_node():
         from gpu_topology_on_k8s_amd.topology.model import Topology
 
         topo = Topology.from_json(ann[Contract().topology_key])
-        assert topo.probe["method"] == "p2p_read_lds" and topo.hbm_gbps[0] > 1000
+        assert topo.probe["method"] == "p2p_read_lds" and topo.hbm_gbps[0] > 2000
     finally:
         if p.poll() is None:
             p.send_signal(signal.SIGTERM)
