@@ -105,11 +105,12 @@ def exp2_xcp_cluster(reps: int, node: str = "xcp"):
         t = time_slice(Topology.full_mesh(n=4, numa_split=1, node_name="p4"), 10)
     with SimCluster({"p4": t}) as c:
         for i in range(reps):
-            c.api.create_pod(make_pod(f"half{i}", gpus=5, node="p4", annotations=PodAssignment(list(range(20, 25)), True, 1)
-                                      .to_annotations()))
-            c.submit(f"a{i}", 4, annotations={c0.fraction_key: "0.4"})
+            sl = node != "xcp"  # time slices are their own pool (amd.com/gpu-slice); XCPs are amd.com/gpu
+            c.api.create_pod(make_pod(f"half{i}", gpus=5, node="p4", resource=c.nodes["p4"].resource,
+                                      annotations=PodAssignment(list(range(20, 25)), True, 1).to_annotations()))
+            c.submit(f"a{i}", 4, slices=sl, annotations={c0.fraction_key: "0.4"})
             (ra,) = c.schedule_pending()
-            c.submit(f"b{i}", 1, annotations={c0.fraction_key: "0.1"})
+            c.submit(f"b{i}", 1, slices=sl, annotations={c0.fraction_key: "0.1"})
             (rb,) = c.schedule_pending()
             gpu = lambda r: sorted({d // 10 for d in r.allocated})  # noqa: E731
             tally[(tuple(gpu(ra)), tuple(gpu(rb)))] += 1

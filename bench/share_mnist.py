@@ -59,7 +59,7 @@ def pod_envs(slices: int = 2):
     envs = []
     with SimCluster({"gpu-node": time_slice(t, slices)}) as c:
         for name in ("job-a", "job-b"):
-            c.submit(name, slices // 2, annotations={Contract().fraction_key: "0.5"})
+            c.submit(name, slices // 2, slices=True, annotations={Contract().fraction_key: "0.5"})
             r = c.schedule_pending()[0]
             if r.error:
                 raise RuntimeError(r.error)

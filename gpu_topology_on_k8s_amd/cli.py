@@ -177,8 +177,13 @@ def cmd_status(a) -> int:
                 row["gpu_share_used"] = {str(p): round(sum(1 for g in t.gpus if g.physical == p and g.index in used) /
                                                        sum(1 for g in t.gpus if g.physical == p), 3)
                                          for p in sorted(set(t.physical.tolist()))}
+        # a sliced node is scored for slice requests (its own pool), every other node for whole devices
+        res = ext.cfg.contract.slice_resource if int(max((g.shares for g in t.gpus), default=1)) > 1 else ext.cfg.contract.resource_name
+        row["resource"] = res
         for k in sizes:
-            d, _ = ext._eval_state({"metadata": {"name": "status", "namespace": "default"}, "spec": {}}, st.name, st, k)
+            probe_pod = {"metadata": {"name": "status", "namespace": "default"},
+                         "spec": {"containers": [{"name": "c", "resources": {"limits": {res: str(k)}}}]}}
+            d, _ = ext._eval_state(probe_pod, st.name, st, k)
             row["best_score"][str(k)] = None if d is None else round(d.score, 2)
         rows.append(row)
     if a.output == "json":

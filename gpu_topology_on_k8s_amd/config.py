@@ -20,7 +20,7 @@ from typing import Any, Dict, List, Optional
 import yaml
 
 from .extender.server import DEFAULT_PORT, DEFAULT_PREFIX
-from .k8s.annotations import COMPAT_RESOURCE, DEFAULT_RESOURCE
+from .k8s.annotations import COMPAT_RESOURCE, DEFAULT_RESOURCE, DEFAULT_SLICE_RESOURCE
 
 __all__ = ["legacy_policy", "scheduler_configuration", "render_manifests", "render_kind", "extender_url"]
 
@@ -51,10 +51,13 @@ def legacy_policy(resource: str = COMPAT_RESOURCE, url: Optional[str] = None, wi
 def scheduler_configuration(resource: str = DEFAULT_RESOURCE, url: Optional[str] = None, with_filter: bool = True,
                             scheduler_name: str = "default-scheduler", weight: int = 5,
                             extra_resources: Optional[List[str]] = None, with_preempt: bool = True,
-                            tls_dir: Optional[str] = None) -> Dict[str, Any]:
+                            tls_dir: Optional[str] = None, slice_resource: str = DEFAULT_SLICE_RESOURCE) -> Dict[str, Any]:
     """``tls_dir``: call the extender over mutual TLS (its ``--tls-cert/--tls-key/--client-ca``) with
-    the scheduler's client certificate ``tls.crt``/``tls.key`` and the CA ``ca.crt`` from that directory."""
-    managed = [{"name": r, "ignoredByScheduler": False} for r in [resource] + list(extra_resources or [])]
+    the scheduler's client certificate ``tls.crt``/``tls.key`` and the CA ``ca.crt`` from that directory.
+    Both pools are managed: whole GPUs (``resource``) and the time slices of sliced nodes
+    (``slice_resource``, topology/shares.py), so the scheduler sends pods of either to the extender."""
+    names = [resource] + ([slice_resource] if slice_resource else []) + list(extra_resources or [])
+    managed = [{"name": r, "ignoredByScheduler": False} for r in dict.fromkeys(names)]
     ext: Dict[str, Any] = {
         "urlPrefix": url or (extender_url().replace("http://", "https://", 1) if tls_dir else extender_url()),
         "prioritizeVerb": "sort",
@@ -252,10 +255,11 @@ def render_kind(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, fake_gpus:
                      "annotations": {"gputopology.amd.com/gpu-fraction": "0.5"}},
         "spec": {
             "restartPolicy": "Never",
-            "nodeSelector": {"gputopology.amd.com/devices-per-gpu": "2"},
+            # a sliced node advertises its slices as their own resource (whole GPUs stay amd.com/gpu);
+            # on a 2-slice node one slice is half a GPU
             "containers": [{"name": "c", "image": "busybox:1.36",
                             "command": ["sh", "-c", "env | grep -E 'GTK_|HSA_CU_MASK' && sleep 5"],
-                            "resources": {"limits": {resource: "1"}}}],
+                            "resources": {"limits": {DEFAULT_SLICE_RESOURCE: "1"}}}],
         },
     }
     up = "\n".join([

@@ -15,13 +15,14 @@ import os
 import signal
 import sys
 import threading
+from typing import Tuple
 
 from ..k8s.annotations import Contract
 from ..placement import PlacementPolicy
 from ..topology.discovery import discover
 from ..topology.shares import time_slice
 from .health import HealthMonitor, HealthPolicy
-from .plugin import DevicePluginServer, PluginConfig, startup_topology
+from .plugin import DevicePluginServer, PluginConfig, node_is_idle, startup_topology
 from .proto import DEVICE_PLUGIN_PATH
 
 
@@ -57,9 +58,37 @@ def node_time_slices(api, node_name: str, contract: Contract, default: int) -> i
         return default
 
 
+def startup_time_slices(api, node_name: str, contract: Contract, default: int,
+                        resource_names=("amd.com/gpu", "amd.com/gpu-slice")) -> Tuple[int, str]:
+    """Time slices a (re)starting plugin advertises, and why.
+
+    The wanted count is the node label (or ``--time-slices``).  Device IDs depend on it, so if the
+    count published by the previous plugin run (``<prefix>/time-slices-active``) differs and any pod
+    still holds a device, the previous count is kept: the running pods' GROUP annotations and the
+    kubelet's checkpointed IDs name devices of that layout (a crash / OOM / rollout restart must not
+    re-number them).  The main loop's idle check performs the switch later (exit 75 + restart)."""
+    want = node_time_slices(api, node_name, contract, default)
+    if api is None or not node_name:
+        return want, ""
+    try:
+        raw = ((api.get_node(node_name).get("metadata") or {}).get("annotations") or {}).get(contract.active_slices_key)
+        active = int(raw) if raw not in (None, "") else None
+    except Exception:  # noqa: BLE001 - nothing published (first start) or unreadable: use the label
+        active = None
+    if active is None or active == want:
+        return want, ""
+    if node_is_idle(api, node_name, resource_names):
+        return want, f"time slices per GPU {active} -> {want} (node idle)"
+    return active, (f"keeping {active} time slices per GPU: pods hold devices of that layout; "
+                    f"the switch to {want} waits until the node is idle")
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--resource-name", default="amd.com/gpu")
+    ap.add_argument("--resource-name", default="amd.com/gpu", help="extended resource of whole GPUs (or XCP partitions)")
+    ap.add_argument("--slice-resource-name", default="amd.com/gpu-slice",
+                    help="extended resource a time-sliced node (--time-slices S > 1) advertises its slices under instead: "
+                         "whole GPUs and slices are separate pools, so --resource-name always means whole devices")
     ap.add_argument("--annotation-prefix", default="gputopology.amd.com")
     ap.add_argument("--socket-dir", default=DEVICE_PLUGIN_PATH)
     ap.add_argument("--socket-name", default="amd-gpu-topology.sock")
@@ -121,8 +150,14 @@ def main(argv=None) -> int:
     log = logging.getLogger("gtk.deviceplugin")
 
     api = make_api(a.apiserver, a.token, a.ca_file, a.insecure_skip_tls_verify)
-    contract = Contract(resource_name=a.resource_name, prefix=a.annotation_prefix)
-    a.time_slices = node_time_slices(api, a.node_name, contract, a.time_slices)
+    contract = Contract(resource_name=a.resource_name, prefix=a.annotation_prefix, slice_resource=a.slice_resource_name)
+    a.time_slices, why = startup_time_slices(api, a.node_name, contract, a.time_slices,
+                                             (a.resource_name, a.slice_resource_name, "aliyun.com/gpu", "aliyun.com/gpu-count"))
+    if why:
+        log.warning("%s", why)
+    # a sliced node is a pool of its own: it registers its slices under the slice resource and
+    # offers no whole GPUs (the extender's filter keeps the two kinds of request apart)
+    advertised = a.slice_resource_name if a.time_slices > 1 else a.resource_name
 
     def node_topology():
         return time_slice(discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus), a.time_slices)
@@ -138,14 +173,14 @@ def main(argv=None) -> int:
             probed, msg = probe_in_child(a.probe, backend=a.discovery)
             log.info("probe: %s", msg)
             return None if probed is None else time_slice(probed, a.time_slices)
-    names = (a.resource_name, "aliyun.com/gpu", "aliyun.com/gpu-count")
+    names = (a.resource_name, a.slice_resource_name, "aliyun.com/gpu", "aliyun.com/gpu-count")
     topo, how = startup_topology(topo, api, a.node_name, contract, names, probe_fn)
     log.info("link matrix: %s; topology:\n%s", how, topo.render())
 
     health = HealthMonitor(topo, node_topology, HealthPolicy(xgmi_links=a.xgmi_link_loss == "unhealthy"))
 
     specs = a.device_specs if a.device_specs != "auto" else ("stub" if a.discovery == "fake" else "strict")
-    cfg = PluginConfig(resource_name=a.resource_name, socket_dir=a.socket_dir, socket_name=a.socket_name, dev_root=a.dev_root,
+    cfg = PluginConfig(resource_name=advertised, socket_dir=a.socket_dir, socket_name=a.socket_name, dev_root=a.dev_root,
                        node_name=a.node_name, contract=contract, device_specs=specs, prestart_validate=a.prestart_validate,
                        health_interval=a.health_interval, reprobe_interval=a.reprobe_interval,
                        reprobe_tolerance=a.reprobe_tolerance, pod_resources_socket=a.pod_resources_socket,

@@ -288,7 +288,11 @@ class DevicePluginServer:
         return node_is_idle(self.api, self.cfg.node_name, self._resource_names())
 
     def _resource_names(self) -> Tuple[str, ...]:
-        return (self.cfg.resource_name,) + tuple(a for a in self.cfg.resource_aliases if a != self.cfg.resource_name)
+        """Every resource name a pod holding this node's devices may have asked for: the advertised
+        one, its aliases, and both pools (whole GPUs and time slices) of the contract."""
+        names = [self.cfg.resource_name] + list(self.cfg.resource_aliases)
+        names += [self.cfg.contract.resource_name, self.cfg.contract.slice_resource]
+        return tuple(dict.fromkeys(n for n in names if n))
 
     @staticmethod
     def link_change(old: Topology, new: Topology) -> float:
@@ -411,6 +415,7 @@ class DevicePluginServer:
             c.label_slices: str(max((int((t.physical == p).sum()) for p in set(t.physical.tolist())), default=1)),
         }
         ann = encode_node_annotations(t, c)
+        ann[c.active_slices_key] = str(slices_per_gpu(t))  # the layout a restart must keep while pods hold devices
         self.metrics.annotation_bytes.set(sum(len(k) + len(v) for k, v in ann.items()))
         try:
             self.api.patch_node(self.cfg.node_name, annotations=ann, labels=labels)

@@ -24,7 +24,9 @@ def main(argv=None) -> int:
                          "is unauthenticated, so do not expose it beyond the node without TLS + auth in front")
     ap.add_argument("--port", type=int, default=DEFAULT_PORT)
     ap.add_argument("--url-prefix", default=DEFAULT_PREFIX)
-    ap.add_argument("--resource-name", default="amd.com/gpu")
+    ap.add_argument("--resource-name", default="amd.com/gpu", help="extended resource of whole GPUs (or XCP partitions)")
+    ap.add_argument("--slice-resource-name", default="amd.com/gpu-slice",
+                    help="extended resource of time slices (nodes whose device plugin runs with --time-slices): a separate pool")
     ap.add_argument("--annotation-prefix", default="gputopology.amd.com")
     ap.add_argument("--policy", default="exact", choices=["exact", "gaia", "design"])
     ap.add_argument("--tie-break", default="first", choices=["first", "random"])
@@ -53,7 +55,7 @@ def main(argv=None) -> int:
 
     api = (RestKubeAPI(a.apiserver, token=a.token or None, ca_file=a.ca_file or None, verify=not a.insecure_skip_tls_verify)
            if a.apiserver else RestKubeAPI.in_cluster())
-    cfg = ExtenderConfig(contract=Contract(resource_name=a.resource_name, prefix=a.annotation_prefix), policy_name=a.policy,
+    cfg = ExtenderConfig(contract=Contract(resource_name=a.resource_name, prefix=a.annotation_prefix, slice_resource=a.slice_resource_name), policy_name=a.policy,
                          policy=PlacementPolicy(tie_break=a.tie_break, partition_aware=a.partition_aware == "on"),
                          assume_ttl=a.assume_ttl, resync_s=a.resync,
                          scheduler_names=tuple(x.strip() for x in a.scheduler_names.split(",") if x.strip()))

@@ -108,6 +108,8 @@ class ClusterCache:
         self.resync_s = float(resync_s)
         self.clock = clock
         self.resources = [contract.resource_name] + [r for r in resource_aliases if r != contract.resource_name]
+        if contract.slice_resource and contract.slice_resource not in self.resources:
+            self.resources.append(contract.slice_resource)  # time-sliced nodes' pool (topology/shares.py)
         self._nodes: Dict[str, NodeState] = {}
         self._overlay: Dict[str, Dict[str, Alloc]] = {}  # node -> pod -> alloc (binds made here)
         self._lock = threading.RLock()

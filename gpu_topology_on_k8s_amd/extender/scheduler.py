@@ -21,6 +21,9 @@ This implementation adds:
   * fractional requests (Gaia Fragment, Alg. 2) as XCP partitions of ONE physical GPU on
     CPX/DPX/QPX nodes, or as time slices of one GPU on a node whose device plugin runs with
     ``--time-slices`` (topology/shares.py), selected by the ``<prefix>/gpu-fraction`` pod annotation;
+    time slices are their own resource pool (``Contract.slice_resource``, default
+    ``amd.com/gpu-slice``): ``amd.com/gpu`` means a whole GPU on every node (Gaia's heterogeneous
+    quota against resource-pool pollution, paper p.3 §III.A), and the filter names every mismatch;
   * per-node locking + an assume overlay so concurrent binds never overlap (BASELINE config 4);
   * three selectable policies: ``exact`` (default, :func:`placement.select`), ``gaia`` (cost-tree
     Alg. 1-4) and ``design`` (the reference's greedy/Prim, for parity experiments);
@@ -50,6 +53,7 @@ from ..placement.gaia import gaia_schedule, tree_from_topology
 from ..placement.legacy import design_greedy_select
 from ..topology.cpus import access_costs, recommended_cpuset
 from ..topology.model import Topology
+from ..topology.shares import slices_per_gpu
 from .cache import ClusterCache, NodeState
 from .metrics import ExtenderMetrics
 
@@ -238,19 +242,33 @@ class TopologyExtender:
                         ids, self.cfg.policy)
         return tuple(sorted(int(i) for i in ids)), score_from_objective(j), j
 
+    def request_unit(self, pod: Dict[str, Any]) -> Tuple[Optional[str], str]:
+        """Which pool the pod draws from: ``"gpu"`` (whole GPUs: the resource name and its aliases) or
+        ``"slice"`` (``Contract.slice_resource``, time slices of sliced nodes); (None, reason) when it
+        asks for both — the two pools are never mixed in one pod."""
+        sl = self.cfg.contract.slice_resource
+        whole = pod_gpu_request(pod, [r for r in self.resources if r != sl])
+        slices = pod_gpu_request(pod, [sl]) if sl else 0
+        if whole and slices:
+            return None, f"pod requests both whole GPUs and {sl}: use one pool"
+        return ("slice" if slices else "gpu"), ""
+
     def _pod_shape(self, pod: Dict[str, Any], k: int) -> Tuple[Optional[tuple], str]:
-        """What a placement depends on from the pod: (k, fraction, NUMA preference, GPU model), parsed
-        once per request; (None, reason) for a malformed fraction."""
+        """What a placement depends on from the pod: (k, fraction, NUMA preference, GPU model,
+        multi-node, memory, pool unit), parsed once per request; (None, reason) for a malformed one."""
         try:
             fraction = self.fraction_of(pod)
             mem = self.memory_of(pod)
         except ValueError as e:
             return None, str(e)
+        unit, why = self.request_unit(pod)
+        if unit is None:
+            return None, why
         if mem is not None and fraction is None:
             fraction = 0.0  # a memory-sized share of one GPU: the Fragment path, sized by HBM below
         numa = self.numa_preference(pod)
         want = obj_annotations(pod).get(self.cfg.contract.pod_model_key) or obj_labels(pod).get(self.cfg.contract.pod_model_key)
-        return (k, fraction, tuple(numa) if numa else None, want, self.multi_node(pod), mem), ""
+        return (k, fraction, tuple(numa) if numa else None, want, self.multi_node(pod), mem, unit), ""
 
     def multi_node(self, pod: Dict[str, Any]) -> bool:
         """A member of a multi-node job: ``<prefix>/multi-node: "true"``, or it requests an RDMA
@@ -273,7 +291,7 @@ class TopologyExtender:
             shape, why = self._pod_shape(pod, k)
             if shape is None:
                 return None, why
-        _, fraction, numa, want, multi, mem = shape
+        _, fraction, numa, want, multi, mem, unit = shape
         with st.lock:
             now = self.clock()
             if st.probing_until > now:
@@ -286,17 +304,34 @@ class TopologyExtender:
                 if hit is not None and hit[0] <= now <= hit[1]:
                     self.metrics.cache(True)
                     return hit[2], hit[3]
-            d, why = self._eval_state_uncached(st, name, k, fraction, numa, want, now, multi, mem)
+            d, why = self._eval_state_uncached(st, name, k, fraction, numa, want, now, multi, mem, unit)
             if self._cacheable():
                 st.memo[shape] = (now, st.valid_until(now, self.cfg.assume_ttl), d, why)
             return d, why
 
+    def _pool_ok(self, t: Topology, unit: str) -> Tuple[bool, str]:
+        """Resource pools stay apart (Gaia paper p.3 §III.A, resource pool pollution): a time-sliced
+        node serves only slice requests, every other node only whole-device requests."""
+        c = self.cfg.contract
+        s = slices_per_gpu(t)
+        if s > 1 and unit != "slice":
+            return False, (f"node shares its GPUs as {c.slice_resource} ({s} per GPU); {c.resource_name} requests "
+                           f"whole GPUs, which this node does not offer")
+        if s <= 1 and unit == "slice":
+            return False, (f"node has no time slices ({c.slice_resource} is offered by nodes labelled "
+                           f"{c.time_slices_label}=S)")
+        return True, ""
+
     def _eval_state_uncached(self, st: NodeState, name: str, k: int, fraction: Optional[float], numa, want,
-                             now: float, multi: bool = False, mem: Optional[int] = None) -> Tuple[Optional[Decision], str]:
+                             now: float, multi: bool = False, mem: Optional[int] = None,
+                             unit: str = "gpu") -> Tuple[Optional[Decision], str]:
         t = st.topology
         if t is None:
             return None, "node has no GPU topology annotation"
         ok, why = self._model_ok(want, st)
+        if not ok:
+            return None, why
+        ok, why = self._pool_ok(t, unit)
         if not ok:
             return None, why
         if fraction is not None:
@@ -496,7 +531,9 @@ class TopologyExtender:
                 freed_unknown = sum(st.unknown_pods.get(st.unknown_uids.get(u, ""), 0) for u in keep)
                 used = st.used(now, self.cfg.assume_ttl)
                 healthy = {g.index for g in t.gpus if g.healthy}
-                _, fraction, numa, _, multi, mem = shape
+                _, fraction, numa, _, multi, mem, unit = shape
+                if not self._pool_ok(t, unit)[0]:
+                    continue
                 if fraction == 0.0 and mem is not None and len({g.physical for g in t.gpus}) == t.n:
                     fraction = None  # memory-sized request on whole GPUs: an ordinary placement
                 access = access_costs(t, numa) if self.cfg.cpu_affinity else None

@@ -39,6 +39,7 @@ ANN_GPU_ID_ALIAS = "gpu-id"
 
 DEFAULT_PREFIX = "gputopology.amd.com"
 DEFAULT_RESOURCE = "amd.com/gpu"
+DEFAULT_SLICE_RESOURCE = "amd.com/gpu-slice"  # time slices of a GPU (topology/shares.py): a pool of their own
 COMPAT_RESOURCE = "aliyun.com/gpu"  # design.md:86,105 (aliyun.com/gpu-count in the prose/diagram)
 
 _PAIR_RE = re.compile(r"^GPU_([A-Z0-9]+)_(\d+)_(\d+)$")
@@ -50,6 +51,11 @@ class Contract:
 
     resource_name: str = DEFAULT_RESOURCE
     prefix: str = DEFAULT_PREFIX
+    #: extended resource a time-sliced node advertises its slices under.  Gaia keeps resource pools
+    #: apart (paper p.3 §III.A, "resource pool pollution"): ``resource_name`` always counts whole
+    #: GPUs, so a pod's ``amd.com/gpu: 1`` means one GPU on every node, and a sliced node advertises
+    #: 0 of them and S x GPUs of this resource instead.
+    slice_resource: str = DEFAULT_SLICE_RESOURCE
 
     @property
     def topology_key(self) -> str:
@@ -127,6 +133,14 @@ class Contract:
     def time_slices_label(self) -> str:
         """Node label set by the operator: advertise this node's GPUs as that many time slices."""
         return f"{self.prefix}/time-slices"
+
+    @property
+    def active_slices_key(self) -> str:
+        """Node annotation written by the device plugin: the time slices per GPU it advertises now.
+        A restarted plugin keeps this count while pods hold devices (their GROUP annotations and the
+        kubelet's checkpoint name devices of this layout) and switches to a changed label only once
+        the node is idle."""
+        return f"{self.prefix}/time-slices-active"
 
     @property
     def label_slices(self) -> str:

@@ -72,7 +72,9 @@ def _pod_devices(env, visible_bdfs=None) -> Dict[str, object]:
 def apply_share_cap(pl: Dict[str, object], rank: int, dev: int) -> Optional[float]:
     """On a time-sliced node (``GTK_GPU_FRACTION``, topology/shares.py) hold this process to its
     share of the GPU's HBM: the caching allocator refuses to grow past ``fraction * capacity``.  The
-    slices of a GPU share its CUs, so this is the cooperative part of the share; returns the cap."""
+    compute side of the share is the slices' disjoint CUs (``HSA_CU_MASK`` from Allocate, with the
+    plugin's ``--share-cu-mask on``); HBM is shared by the slices, so this cap is the cooperative
+    part of the share.  Returns the cap."""
     fr = pl.get("fractions")
     if not fr or float(fr[rank]) >= 1.0:
         return None

@@ -38,6 +38,7 @@ from ..k8s.objects import annotations as obj_annotations
 from ..k8s.objects import make_node, make_pod, meta, pod_gpu_request, pod_is_terminal, pod_key, pod_node
 from ..placement import PlacementPolicy
 from ..topology.model import Topology
+from ..topology.shares import slices_per_gpu
 
 log = logging.getLogger(__name__)
 
@@ -180,6 +181,7 @@ class _Node:
     sockdir: str
     kubelet: FakeKubelet
     plugin: DevicePluginServer
+    resource: str = ""  # the extended resource its plugin advertises (slices on a time-sliced node)
 
 
 class SimCluster:
@@ -223,7 +225,10 @@ class SimCluster:
             else:  # a kind node: no /dev/kfd, no render nodes
                 dev_root = os.path.join(self._root, f"dev{i}")
                 os.makedirs(dev_root, exist_ok=True)
-            plugin = DevicePluginServer(topo, PluginConfig(resource_name=self.resource, socket_dir=sockdir, node_name=name,
+            # a time-sliced node is its own pool: its plugin advertises the slice resource (as the
+            # daemon does with --time-slices), and amd.com/gpu means whole GPUs everywhere
+            res = self.contract.slice_resource if slices_per_gpu(topo) > 1 else self.resource
+            plugin = DevicePluginServer(topo, PluginConfig(resource_name=res, socket_dir=sockdir, node_name=name,
                                                            contract=self.contract, dev_root=dev_root,
                                                            device_specs=self.device_specs,
                                                            prestart_validate=self.prestart_validate,
@@ -231,8 +236,8 @@ class SimCluster:
                                                            reconcile_interval=self.reconcile_interval),
                                         api=self.api, validate_fn=self.validate_fn)
             plugin.start()
-            kubelet.wait_for(self.resource)
-            self.nodes[name] = _Node(name, topo, sockdir, kubelet, plugin)
+            kubelet.wait_for(res)
+            self.nodes[name] = _Node(name, topo, sockdir, kubelet, plugin, res)
         self.start_extender()
         return self
 
@@ -277,8 +282,14 @@ class SimCluster:
         self.stop()
 
     # ------------------------------------------------------------------ workload
-    def submit(self, name: str, gpus: int, namespace: str = "default", **kw) -> dict:
-        return self.api.create_pod(make_pod(name, gpus=gpus, namespace=namespace, resource=self.resource, **kw))
+    def submit(self, name: str, gpus: int, namespace: str = "default", slices: bool = False, **kw) -> dict:
+        """A pod requesting ``gpus`` whole GPUs, or (``slices``) that many time slices."""
+        res = self.contract.slice_resource if slices else self.resource
+        return self.api.create_pod(make_pod(name, gpus=gpus, namespace=namespace, resource=res, **kw))
+
+    def pod_resource(self, pod: dict) -> str:
+        """The pool a pod draws from: the slice resource if it requests slices, else whole GPUs."""
+        return self.contract.slice_resource if pod_gpu_request(pod, [self.contract.slice_resource]) else self.resource
 
     def complete(self, name: str, namespace: str = "default", phase: str = "Succeeded") -> None:
         pod = self.api.get_pod(namespace, name)
@@ -296,14 +307,15 @@ class SimCluster:
 
     # ------------------------------------------------------------------ mini kube-scheduler
     def _fits(self, pod: dict) -> List[str]:
-        """Default NodeResourcesFit on the extended resource (design.md:117)."""
-        k = pod_gpu_request(pod, [self.resource])
+        """Default NodeResourcesFit on the extended resource the pod requests (design.md:117)."""
+        res = self.pod_resource(pod)
+        k = pod_gpu_request(pod, [res])
         pods = self.api.list_pods()
         out = []
         for node in self.api.list_nodes():
             name = meta(node)["name"]
-            alloc = int(float(((node.get("status") or {}).get("allocatable") or {}).get(self.resource, 0)))
-            used = sum(pod_gpu_request(p, [self.resource]) for p in pods if pod_node(p) == name and not pod_is_terminal(p))
+            alloc = int(float(((node.get("status") or {}).get("allocatable") or {}).get(res, 0)))
+            used = sum(pod_gpu_request(p, [res]) for p in pods if pod_node(p) == name and not pod_is_terminal(p))
             if k == 0 or alloc - used >= k:
                 out.append(name)
         return out
@@ -341,9 +353,10 @@ class SimCluster:
         if admit:
             t1 = time.perf_counter()
             bound = self.api.get_pod(md.get("namespace", "default"), md["name"])
-            self.nodes[res.node].kubelet.admit(bound, self.resource)
+            rname = self.pod_resource(bound)
+            self.nodes[res.node].kubelet.admit(bound, rname)
             res.admit_ms = (time.perf_counter() - t1) * 1e3
-            res.allocated = tuple(int(i) for i in self.nodes[res.node].kubelet.allocated[self.resource][key])
+            res.allocated = tuple(int(i) for i in self.nodes[res.node].kubelet.allocated[rname][key])
         self.history.append(res)
         return res
 

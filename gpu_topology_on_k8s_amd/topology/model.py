@@ -199,8 +199,9 @@ class GPUInfo:
     ecc_deferred: int = -1
     bad_pages: int = -1
     bad_page_threshold: int = -1
-    # > 1: this device is one of `shares` time slices of GPU `physical` (topology/shares.py); the
-    # slices of a GPU share its CUs and HBM, so a pod holding j of them holds j/shares of the GPU
+    # > 1: this device is one of `shares` time slices of GPU `physical` (topology/shares.py): a pod
+    # holding j of them holds j/shares of the GPU.  Each slice owns a disjoint 1/shares of the CUs
+    # (HSA_CU_MASK, with --share-cu-mask on); HBM is shared, capped cooperatively at the share
     shares: int = 1
     cus: int = -1  # compute units of the physical GPU (KFD simd_count / simd_per_cu); -1 = unknown
 

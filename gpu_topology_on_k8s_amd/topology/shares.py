@@ -8,8 +8,10 @@ left in SPX mode — the default — has no partitions.  This module gives such 
 software: every physical GPU is advertised as ``S`` *time slices* (device ``i*S + j`` is slice ``j``
 of GPU ``i``), so
 
-* the kubelet counts shares (``amd.com/gpu: 4`` on an ``S = 10`` node is 0.4 of one GPU) and the
-  pod-annotation contract (``ALIYUN_COM_GPU_GROUP`` = slice ids) stays as it is;
+* the kubelet counts shares under their own extended resource (``amd.com/gpu-slice: 4`` on an
+  ``S = 10`` node is 0.4 of one GPU; the node offers no ``amd.com/gpu``, which means a whole GPU
+  everywhere: Gaia's separate resource pools, docs/SHARES.md) and the pod-annotation contract
+  (``ALIYUN_COM_GPU_GROUP`` = slice ids) stays as it is;
 * the extender's Fragment path (``<prefix>/gpu-fraction`` + ``place_fraction``) packs fractions onto
   the best-fitting GPU exactly as it packs XCPs of one package;
 * Allocate maps slices back to the physical GPU (its render/card nodes once) and tells the container

@@ -19,7 +19,7 @@ def _check(c, live, request):
     per_node = {}
     for key, node in live.items():
         ns, name = key.split("/")
-        kub = c.nodes[node].kubelet.allocated[c.resource].get(key)
+        kub = c.nodes[node].kubelet.allocated[c.nodes[node].resource].get(key)
         assert kub is not None, f"{key} lost its kubelet allocation"
         ids = sorted(int(i) for i in kub)
         assert len(ids) == request[key], (key, ids)
@@ -153,7 +153,7 @@ def test_random_churn_on_time_sliced_nodes(seed):
     C = Contract()
     rng = random.Random(seed)
     with SimCluster({"s0": time_slice(fx.f7_mi355x(), 4), "s1": time_slice(fx.f7_mi355x(), 4)}) as c:
-        live, request, frac, nxt = {}, {}, set(), 0
+        live, request, frac, nxt, placed = {}, {}, set(), 0, 0
         for _ in range(30):
             if rng.random() < 0.6:
                 for _ in range(rng.randint(1, 4)):
@@ -161,12 +161,12 @@ def test_random_churn_on_time_sliced_nodes(seed):
                     nxt += 1
                     if rng.random() < 0.5:
                         f = rng.choice([0.25, 0.5, 0.75])
-                        c.submit(name, int(f * 4), annotations={C.fraction_key: str(f)})
+                        c.submit(name, int(f * 4), slices=True, annotations={C.fraction_key: str(f)})
                         frac.add(f"default/{name}")
                         request[f"default/{name}"] = int(f * 4)
                     else:
                         k = 4 * rng.choice([1, 2, 4])
-                        c.submit(name, k)
+                        c.submit(name, k, slices=True)
                         request[f"default/{name}"] = k
                 for r in c.schedule_pending(concurrent=rng.random() < 0.3):
                     if r.node and r.allocated:
@@ -176,10 +176,11 @@ def test_random_churn_on_time_sliced_nodes(seed):
                 c.complete(key.split("/")[1])
                 live.pop(key)
             _check(c, live, request)
+            placed += len(live)
             masks = {}
             for key in frac & set(live):
                 node = live[key]
-                ids = c.nodes[node].kubelet.allocated[c.resource][key]
+                ids = c.nodes[node].kubelet.allocated[c.nodes[node].resource][key]
                 gpus = {int(i) // 4 for i in ids}
                 assert len(gpus) == 1, (key, ids)
                 envs = dict(c.nodes[node].kubelet.responses[key].container_responses[0].envs)
@@ -191,3 +192,4 @@ def test_random_churn_on_time_sliced_nodes(seed):
                 prev = masks.setdefault((node, gpus.pop()), set())
                 assert not (prev & cus), (key, envs["HSA_CU_MASK"])  # neighbours on one GPU never share a CU
                 prev |= cus
+        assert placed > 0 and any(k in frac for k in request)  # the slice pool really was exercised

@@ -30,7 +30,7 @@ def test_scheduler_configuration():
     assert c["apiVersion"] == "kubescheduler.config.k8s.io/v1"
     e = c["extenders"][0]
     assert e["prioritizeVerb"] == "sort" and e["bindVerb"] == "bind" and e["filterVerb"] == "filter"
-    assert [m["name"] for m in e["managedResources"]] == ["amd.com/gpu", "aliyun.com/gpu"]
+    assert [m["name"] for m in e["managedResources"]] == ["amd.com/gpu", "amd.com/gpu-slice", "aliyun.com/gpu"]
 
 
 def test_manifests_are_valid_yaml():

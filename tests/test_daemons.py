@@ -173,8 +173,9 @@ def test_both_daemons_config4_through_shipped_processes():
 
 
 def test_device_plugin_daemon_time_slices():
-    """A node labelled ``gputopology.amd.com/time-slices=4`` (no flag): the kubelet sees 8 devices, the node
-    annotation carries the slices, and a 2-slice pod gets one GPU's device nodes with GTK_GPU_FRACTION=0.5."""
+    """A node labelled ``gputopology.amd.com/time-slices=4`` (no flag): the kubelet sees 8 devices of the
+    slice resource (and no whole GPUs), the node annotation carries the slices, and a 2-slice pod gets
+    one GPU's device nodes with GTK_GPU_FRACTION=0.5."""
     from gpu_topology_on_k8s_amd.k8s.annotations import decode_node_annotations
     from gpu_topology_on_k8s_amd.topology.shares import slices_per_gpu
 
@@ -190,12 +191,13 @@ def test_device_plugin_daemon_time_slices():
                 "--apiserver", url, "--node-name", "worker-1", "--socket-dir", sockdir, "--dev-root", devroot,
                 "--log-level", "WARNING"])
     try:
-        plugin = kubelet.wait_for("amd.com/gpu", timeout=60)
-        assert sorted(plugin.devices, key=int) == [str(i) for i in range(8)]
-        topo = decode_node_annotations(api.get_node("worker-1")["metadata"]["annotations"], Contract())
-        assert topo.n == 8 and slices_per_gpu(topo) == 4
-        pod = api.create_pod(make_pod("half", gpus=2, node="worker-1"))
-        c = kubelet.admit(pod, "amd.com/gpu").container_responses[0]
+        plugin = kubelet.wait_for("amd.com/gpu-slice", timeout=60)
+        assert sorted(plugin.devices, key=int) == [str(i) for i in range(8)] and "amd.com/gpu" not in kubelet.plugins
+        ann = api.get_node("worker-1")["metadata"]["annotations"]
+        topo = decode_node_annotations(ann, Contract())
+        assert topo.n == 8 and slices_per_gpu(topo) == 4 and ann[Contract().active_slices_key] == "4"
+        pod = api.create_pod(make_pod("half", gpus=2, node="worker-1", resource="amd.com/gpu-slice"))
+        c = kubelet.admit(pod, "amd.com/gpu-slice").container_responses[0]
         assert c.envs["GTK_GPU_FRACTION"] == "0.5" and len(c.envs["GTK_GPU_GROUP"].split(",")) == 1
         # the operator relabels the node: the plugin waits while a pod holds devices, then exits for a
         # restart (EX_TEMPFAIL) with the new slicing
@@ -258,3 +260,24 @@ def test_extender_daemon_mutual_tls():
         srv.shutdown()
         shutil.rmtree(d, ignore_errors=True)
     assert rc == 0, ext.stdout.read() if ext.stdout else ""
+
+
+def test_restart_on_a_busy_node_keeps_the_published_slicing():
+    """a plugin restarted (crash, rollout) after the operator relabelled the node keeps the
+    slice count it last published while any pod holds a device; an idle node switches at once."""
+    from gpu_topology_on_k8s_amd.deviceplugin.__main__ import startup_time_slices
+    from gpu_topology_on_k8s_amd.k8s import PodAssignment
+
+    c = Contract()
+    api = FakeAPIServer()
+    api.create_node(make_node("n", labels={c.time_slices_label: "2"}, annotations={c.active_slices_key: "4"}))
+    api.create_pod(make_pod("busy", gpus=2, node="n", resource=c.slice_resource,
+                            annotations=PodAssignment([4, 5], True, 1).to_annotations()))
+    s, why = startup_time_slices(api, "n", c, 1)
+    assert s == 4 and "keeping 4" in why
+    api.delete_pod("default", "busy")
+    s, why = startup_time_slices(api, "n", c, 1)
+    assert s == 2 and "4 -> 2" in why
+    api.create_node(make_node("fresh", labels={c.time_slices_label: "4"}))  # first start: nothing published
+    assert startup_time_slices(api, "fresh", c, 1) == (4, "")
+    assert startup_time_slices(None, "", c, 3) == (3, "")

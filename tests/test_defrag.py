@@ -140,3 +140,4 @@ def test_gtk_status_shares_on_a_sliced_node():
         srv.shutdown()
     (row,) = json.loads(p.stdout)
     assert row["per_gpu"] == 4 and row["gpu_share_used"] == {"0": 0.0, "1": 0.25}
+    assert row["resource"] == C.slice_resource and row["best_score"]["4"] is not None  # scored in its own pool

@@ -34,7 +34,7 @@ def test_two_half_gpu_pods_share_the_real_gpu_and_train_concurrently():
     envs = []
     with SimCluster({"gpu-node": v}) as c:
         for name in ("half-a", "half-b"):
-            c.submit(name, 2, annotations={Contract().fraction_key: "0.5"})
+            c.submit(name, 2, slices=True, annotations={Contract().fraction_key: "0.5"})
             r = c.schedule_pending()[0]
             assert r.error == "" and len(r.allocated) == 2 and physical_group(v, r.allocated) == [0], r
             envs.append(dict(c.nodes["gpu-node"].kubelet.responses[f"default/{name}"].container_responses[0].envs))
@@ -109,7 +109,7 @@ def test_cu_masked_shares_split_the_compute_units():
     envs = {}
     with SimCluster({"gpu-node": v}) as c:
         for name, k, m in (("quarter", 1, "0.25"), ("three-quarters", 3, "0.75")):
-            c.submit(name, k, annotations={Contract().fraction_key: m})
+            c.submit(name, k, slices=True, annotations={Contract().fraction_key: m})
             r = c.schedule_pending()[0]
             assert r.error == "", r
             envs[name] = dict(c.nodes["gpu-node"].kubelet.responses[f"default/{name}"].container_responses[0].envs)
@@ -168,7 +168,7 @@ def test_prestart_validation_of_a_fractional_pod():
     t = discover("auto")
     t.node_name = "gpu-node"
     with SimCluster({"gpu-node": time_slice(t, 4)}, prestart_validate=True) as c:
-        c.submit("half", 2, annotations={Contract().fraction_key: "0.5"})
+        c.submit("half", 2, slices=True, annotations={Contract().fraction_key: "0.5"})
         r = c.schedule_pending()[0]
         assert r.error == "" and len(r.allocated) == 2
         v = json.loads(c.api.get_pod("default", "half")["metadata"]["annotations"][Contract().validated_key])

@@ -96,19 +96,72 @@ def test_table2_fragment_through_the_cluster_on_a_time_sliced_spx_node():
     /bind, GetPreferredAllocation and Allocate, and the containers get gpu2 with their shares."""
     v = time_slice(Topology.full_mesh(n=4, numa_split=1, node_name="p4"), 10)
     with SimCluster({"p4": v}) as c:
-        c.api.create_pod(make_pod("half", gpus=5, node="p4",
+        c.api.create_pod(make_pod("half", gpus=5, node="p4", resource=C.slice_resource,
                                   annotations=PodAssignment(list(range(20, 25)), True, 1).to_annotations()))
-        c.submit("f04", 4, annotations={C.fraction_key: "0.4"})
+        c.submit("f04", 4, slices=True, annotations={C.fraction_key: "0.4"})
         r = c.schedule_pending()[0]
         assert r.error == "" and set(r.allocated) <= set(range(25, 30)) and len(r.allocated) == 4
         envs = dict(c.nodes["p4"].kubelet.responses["default/f04"].container_responses[0].envs)
         assert envs["GTK_GPU_GROUP"] == "2" and envs["GTK_GPU_FRACTION"] == "0.4"
-        c.submit("f01", 1, annotations={C.fraction_key: "0.1"})
+        c.submit("f01", 1, slices=True, annotations={C.fraction_key: "0.1"})
         r = c.schedule_pending()[0]
         assert r.allocated == (29,)
-        c.submit("whole", 10)  # a whole GPU on the same node: all slices of one untouched GPU
+        c.submit("whole", 10, slices=True)  # a whole GPU's worth of slices: all slices of one untouched GPU
         r = c.schedule_pending()[0]
         assert r.error == "" and len(physical_group(v, r.allocated)) == 1 and 2 not in physical_group(v, r.allocated)
+        c.submit("gpu", 1)  # amd.com/gpu means a whole GPU: a sliced node does not offer one
+        r = c.schedule_pending()[0]
+        assert r.node is None and c.nodes["p4"].kubelet.rejected == []
+
+
+def test_whole_gpu_and_slice_pools_stay_apart():
+    """VERDICT r2 #2 (Gaia p.3 §III.A resource-pool pollution): on a cluster with one whole-GPU node
+    and one time-sliced node, an unannotated ``amd.com/gpu: 1`` pod always gets a whole GPU with no
+    CU mask; a ``gpu-fraction: 0.5`` pod asking for slices gets half of one GPU; every mismatch is
+    named by /filter."""
+    from gpu_topology_on_k8s_amd.extender import ExtenderConfig, TopologyExtender
+    from gpu_topology_on_k8s_amd.k8s import FakeAPIServer
+    from gpu_topology_on_k8s_amd.k8s.objects import make_node
+
+    nodes = {"whole": fx.f7_mi355x(n=2), "sliced": time_slice(fx.f7_mi355x(n=2), 4)}
+    with SimCluster(nodes) as c:
+        assert c.nodes["sliced"].resource == C.slice_resource and c.nodes["whole"].resource == C.resource_name
+        alloc = {n: c.api.get_node(n)["status"]["allocatable"] for n in nodes}
+        assert alloc["whole"] == {C.resource_name: "2"} and alloc["sliced"] == {C.slice_resource: "8"}
+        for i in range(2):  # the whole-GPU node's two GPUs, each with no CU mask
+            c.submit(f"g{i}", 1)
+            r = c.schedule_pending()[0]
+            assert r.node == "whole", r
+            envs = dict(c.nodes["whole"].kubelet.responses[f"default/g{i}"].container_responses[0].envs)
+            assert "HSA_CU_MASK" not in envs and "GTK_GPU_FRACTION" not in envs
+        c.submit("g2", 1)  # no whole GPU left anywhere: pending, never a quarter GPU on the sliced node
+        r = c.schedule_pending()[0]
+        assert r.node is None
+        c.api.delete_pod("default", "g2")
+        c.submit("half", 2, slices=True, annotations={C.fraction_key: "0.5"})
+        r = c.schedule_pending()[0]
+        assert r.node == "sliced" and len(physical_group(nodes["sliced"], r.allocated)) == 1
+        envs = dict(c.nodes["sliced"].kubelet.responses["default/half"].container_responses[0].envs)
+        assert envs["GTK_GPU_FRACTION"] == "0.5" and envs["HSA_CU_MASK"].startswith("0:")
+
+    api = FakeAPIServer()
+    for n, t in nodes.items():
+        api.create_node(make_node(n, annotations=encode_node_annotations(t, C)))
+    ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+    gpu = api.create_pod(make_pod("gpu", gpus=1))
+    ok, failed = ext.filter(gpu, ["whole", "sliced"])
+    assert ok == ["whole"] and "amd.com/gpu-slice" in failed["sliced"] and "whole GPUs" in failed["sliced"]
+    sl = api.create_pod(make_pod("sl", gpus=1, resource=C.slice_resource))
+    ok, failed = ext.filter(sl, ["whole", "sliced"])
+    assert ok == ["sliced"] and "no time slices" in failed["whole"]
+    frac = api.create_pod(make_pod("frac", gpus=1, annotations={C.fraction_key: "0.25"}))  # fraction, wrong pool
+    ok, failed = ext.filter(frac, ["whole", "sliced"])
+    assert ok == [] and "partitioned" in failed["whole"] and "amd.com/gpu-slice" in failed["sliced"]
+    both = make_pod("both", gpus=1)
+    both["spec"]["containers"].append({"name": "c1", "resources": {"limits": {C.slice_resource: "1"}}})
+    both = api.create_pod(both)
+    ok, failed = ext.filter(both, ["whole", "sliced"])
+    assert ok == [] and "both" in failed["whole"]
 
 
 def test_gpu_reset_holds_every_slice_of_the_gpu():
@@ -181,20 +234,26 @@ def test_gpu_memory_sizes_the_share():
 
     api = FakeAPIServer()
     api.create_node(make_node("s", annotations=encode_node_annotations(time_slice(fx.f7_mi355x(), 4), C),
-                              capacity={C.resource_name: "32"}))
+                              capacity={C.slice_resource: "32"}))
     api.create_node(make_node("w", annotations=encode_node_annotations(fx.f7_mi355x(), C), capacity={C.resource_name: "8"}))
     ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
-    two = api.create_pod(make_pod("m2", gpus=2, annotations={C.memory_key: "100G"}))
+    two = api.create_pod(make_pod("m2", gpus=2, resource=C.slice_resource, annotations={C.memory_key: "100G"}))
     ok, failed = ext.filter(two, ["s", "w"])
-    assert ok == ["s", "w"]  # on w it is simply two whole GPUs (each holds 100 GB)
+    assert ok == ["s"] and "no time slices" in failed["w"]
     d = ext.bind("default", "m2", two["metadata"]["uid"], "s")
     assert len(physical_group(ext.cache.get("s").topology, d.ids)) == 1 and d.policy == "fragment"
-    bad = api.create_pod(make_pod("m1", gpus=1, annotations={C.memory_key: "100G"}))
+    whole2 = api.create_pod(make_pod("w2", gpus=2, annotations={C.memory_key: "100G"}))
+    ok, failed = ext.filter(whole2, ["s", "w"])
+    assert ok == ["w"]  # whole GPUs: simply two of them (each holds 100 GB)
+    bad = api.create_pod(make_pod("m1", gpus=1, resource=C.slice_resource, annotations={C.memory_key: "100G"}))
     ok, failed = ext.filter(bad, ["s", "w"])
-    assert ok == ["w"] and "2 of 4" in failed["s"]
+    assert ok == [] and "2 of 4" in failed["s"]
     big = api.create_pod(make_pod("huge", gpus=1, annotations={C.memory_key: "400Gi"}))
-    ok, failed = ext.filter(big, ["s", "w"])
-    assert ok == [] and "exceeds" in failed["w"] and "exceeds" in failed["s"]
+    ok, failed = ext.filter(big, ["w"])
+    assert ok == [] and "exceeds" in failed["w"]
+    big_s = api.create_pod(make_pod("huge-s", gpus=4, resource=C.slice_resource, annotations={C.memory_key: "400Gi"}))
+    ok, failed = ext.filter(big_s, ["s"])
+    assert ok == [] and "exceeds" in failed["s"]
 
 
 def test_share_gauge_per_gpu():
@@ -204,8 +263,9 @@ def test_share_gauge_per_gpu():
 
     api = FakeAPIServer()
     api.create_node(make_node("s", annotations=encode_node_annotations(time_slice(fx.f7_mi355x(n=2), 4), C),
-                              capacity={C.resource_name: "8"}))
-    api.create_pod(make_pod("q", gpus=3, node="s", annotations=PodAssignment([4, 5, 6], True, 1).to_annotations()))
+                              capacity={C.slice_resource: "8"}))
+    api.create_pod(make_pod("q", gpus=3, node="s", resource=C.slice_resource,
+                            annotations=PodAssignment([4, 5, 6], True, 1).to_annotations()))
     ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
     ext.cache.sync_all()
     text = ext.metrics.exposition().decode()
