@@ -63,7 +63,7 @@ def main(argv=None) -> int:
     if a.informer == "on":
         from ..k8s.informer import Informer
 
-        inf = Informer(api, ext.cache.on_list, ext.cache.on_event)
+        inf = Informer(api, ext.cache.on_list, ext.cache.on_event, begin_list=ext.cache.begin_list)
         ext.cache.attach_informer(inf)
         inf.start()
     ssl_context = None

@@ -278,11 +278,18 @@ class ClusterCache:
         WATCH events patch it, and :meth:`get` stops polling once it has synced."""
         self.informer = informer
 
-    def on_list(self, kind: str, items: List[dict]) -> None:
+    def begin_list(self, kind: str) -> Optional[int]:
+        """Informer hook, called just before a LIST request: the epoch that LIST is applied under.
+        Taking it after the LIST returned would let a bind that completed (:meth:`bound`) between
+        the request and its arrival look older than the LIST, so the LIST — which cannot show that
+        pod — would drop the bind's overlay entry and free its devices until the WATCH event."""
+        return self._next_epoch() if kind == "Pod" else None
+
+    def on_list(self, kind: str, items: List[dict], epoch: Optional[int] = None) -> None:
         if kind == "Node":
             self.replace_nodes(items)
         elif kind == "Pod":
-            self.replace_pods(items)
+            self.replace_pods(items, epoch)
         with self._lock:
             self._last_full = self.clock()
 

@@ -7,6 +7,10 @@ client-go's reflector does: LIST (remember the list ``resourceVersion``), hand t
 ``on_list``, then WATCH from that version and hand every change to ``on_event``; a watch that times
 out is resumed from the last seen version, a 410 Gone (window expired) or any error relists after a
 back-off.  ``synced`` is set once every kind has been listed.
+
+``begin_list(kind)`` (optional) is called just BEFORE each LIST request and its return value is
+passed to ``on_list(kind, items, token)``: a consumer that also writes state between the LIST request
+and its arrival (the extender's bind overlay) can order the two (extender/cache.py epochs).
 """
 from __future__ import annotations
 
@@ -25,10 +29,12 @@ Obj = Dict[str, object]
 
 
 class Informer:
-    def __init__(self, api: KubeAPI, on_list: Callable[[str, List[Obj]], None], on_event: Callable[[str, str, Obj], None],
-                 kinds: Sequence[str] = ("Node", "Pod"), watch_timeout: float = 300.0, backoff: float = 1.0):
+    def __init__(self, api: KubeAPI, on_list: Callable[..., None], on_event: Callable[[str, str, Obj], None],
+                 kinds: Sequence[str] = ("Node", "Pod"), watch_timeout: float = 300.0, backoff: float = 1.0,
+                 begin_list: Optional[Callable[[str], object]] = None):
         self.api = api
         self.on_list = on_list
+        self.begin_list = begin_list
         self.on_event = on_event
         self.kinds = tuple(kinds)
         self.watch_timeout = watch_timeout
@@ -74,9 +80,13 @@ class Informer:
         while not self._stop.is_set():
             try:
                 if rv is None:
+                    token = self.begin_list(kind) if self.begin_list is not None else None
                     items, rv = self.api.list_with_version(kind)
                     self.lists[kind] += 1
-                    self.on_list(kind, items)
+                    if self.begin_list is not None:
+                        self.on_list(kind, items, token)
+                    else:
+                        self.on_list(kind, items)
                     self._synced[kind].set()
                 for t, obj in self.api.watch_stream(kind, rv, self.watch_timeout, self._stop):
                     if self._stop.is_set():

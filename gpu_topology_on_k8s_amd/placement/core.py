@@ -392,13 +392,17 @@ def _greedy_ascent(p: Problem, k: int, policy: PlacementPolicy, stats) -> List[i
 
 
 def worst(topo: Topology, k: int, used: Sequence[int] = (), policy: PlacementPolicy = PlacementPolicy(),
-          engine: str = "auto") -> Placement:
-    """Highest-objective subset (the "worst-topology placement" of BASELINE config 5).
+          engine: str = "auto", access: Optional[Sequence[float]] = None, nic_aware: bool = False) -> Placement:
+    """Highest-objective subset (the "worst-topology placement" of BASELINE config 5), scored by
+    exactly the objective :func:`select` minimises for the same pod (``access``, and the NIC-coverage
+    term when ``nic_aware``: a multi-node job's A/B must not drop the term its placement used).
 
-    Exhaustive while C(free, k) fits the budget (``node_limit`` natively, ``exact_limit`` in
-    Python), otherwise greedy ascent + 1-swap (``exact=False``): a CPX node (64 XCPs, k=8) is
-    C(64,8) ~ 4.4e9 subsets, which must never be enumerated in a request or a bench start-up."""
-    p = Problem.from_topology(topo, used, partition_aware=policy.partition_aware)
+    Exhaustive while C(free, k) <= ``exact_limit`` in both engines (the native engine then walks every
+    subset, so the bound is the same subset budget the Python enumeration uses, not the
+    branch-and-bound ``node_limit`` of :func:`select`), otherwise greedy ascent + 1-swap
+    (``exact=False``): a CPX node (64 XCPs, k=8) is C(64,8) ~ 4.4e9 subsets, which must never be
+    enumerated in a request or a bench start-up."""
+    p = Problem.from_topology(topo, used, access, partition_aware=policy.partition_aware, nic_aware=nic_aware)
     free_ids = [i for i in range(p.n) if p.free[i]]
     if len(free_ids) < k:
         raise NoFeasiblePlacement(f"need {k} free devices, have {len(free_ids)}")
@@ -406,8 +410,9 @@ def worst(topo: Topology, k: int, used: Sequence[int] = (), policy: PlacementPol
     if mod is not None:
         args = (np.ascontiguousarray(p.cost, dtype=np.float64), np.ascontiguousarray(p.free, dtype=bool),
                 [lv.astype(np.int64).tolist() for lv in p.levels], np.ascontiguousarray(p.access, dtype=np.float64))
+        nic = [] if p.nic is None else [int(x) for x in p.nic]
         r = mod.worst(*args, int(k), policy.w_span, policy.w_frag, policy.w_fit, policy.w_access, int(policy.exact_limit),
-                      w_bottleneck=policy.w_bottleneck)
+                      w_bottleneck=policy.w_bottleneck, nic=nic, w_nic=policy.w_nic)
         terms = dict(r["terms"])
         terms["search_us"] = float(r["micros"])
         return Placement(ids=tuple(int(i) for i in r["ids"]), objective=float(r["objective"]),

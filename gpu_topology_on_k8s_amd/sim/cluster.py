@@ -247,6 +247,7 @@ class SimCluster:
             from ..k8s.informer import Informer
 
             self.informer = Informer(self.api, self.extender.cache.on_list, self.extender.cache.on_event, watch_timeout=5.0,
+                                     begin_list=self.extender.cache.begin_list,
                                      backoff=0.1)
             self.extender.cache.attach_informer(self.informer)
             self.informer.start()

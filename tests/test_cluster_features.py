@@ -239,7 +239,7 @@ def _rest_cluster(nodes=64):
 def test_informer_keeps_prioritize_free_of_lists():
     api, srv, rest = _rest_cluster(64)
     ext = TopologyExtender(rest, ExtenderConfig(resync_s=0.0))
-    inf = Informer(rest, ext.cache.on_list, ext.cache.on_event, watch_timeout=5.0)
+    inf = Informer(rest, ext.cache.on_list, ext.cache.on_event, watch_timeout=5.0, begin_list=ext.cache.begin_list)
     ext.cache.attach_informer(inf)
     inf.start()
     try:
@@ -465,3 +465,45 @@ def test_prestart_validation_records_busbw_on_the_pod():
         text = c.nodes["n1"].plugin.metrics.exposition().decode()
         assert 'gtk_plugin_placement_validations_total{result="ok"} 1.0' in text
         assert 'gtk_plugin_placement_validations_total{result="failed"} 1.0' in text
+
+
+def test_relist_racing_a_bind_keeps_the_binds_devices():
+    """ADVICE r2 (cache.py on_list): a bind that completes between an informer relist's LIST request
+    and its arrival must survive the relist.  The LIST cannot show the pod (it was unbound when
+    listed); with the epoch taken before the request, the cache knows the LIST predates the bind."""
+    def scenario(use_hook):
+        api = FakeAPIServer()
+        api.create_node(make_node("n", annotations=encode_node_annotations(fx.f7_mi355x(), C), capacity={C.resource_name: "8"}))
+        api.create_pod(make_pod("p", gpus=2))
+        ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+        cache = ext.cache
+        cache.sync_all()
+        token = cache.begin_list("Pod") if use_hook else None
+        items = api.list_pods()  # the relist's LIST: p is not on any node yet
+        d = ext.bind("default", "p", "", "n")  # ... the bind completes before the LIST arrives
+        if use_hook:
+            cache.on_list("Pod", items, token)
+        else:
+            cache.on_list("Pod", items)  # round-2 behaviour: epoch taken after the LIST returned
+        return set(d.ids), cache.get("n", sync=False).used(time.time(), 300.0)
+
+    ids, used = scenario(True)
+    assert ids <= used, (ids, used)
+    ids, used = scenario(False)
+    assert not (ids & used)  # the race the hook closes: the devices looked free until the WATCH event
+
+
+def test_worst_scores_the_nic_term_like_select():
+    """for a multi-node member the A/B 'worst' subset is scored with the same NIC
+    term select() uses, in both engines, and both agree with brute force over that objective."""
+    t = fx.f7_mi355x()
+    # two RDMA NICs, each behind the PCIe switches of one NUMA half (GPUs 0-3 / 4-7)
+    t.nics = [{"name": "mlx5_0", "numa": 0}, {"name": "mlx5_1", "numa": 1}]
+    t.gpu_nic = [[5 if g < 4 else 1, 1 if g < 4 else 5] for g in range(8)]
+    p = Problem.from_topology(t, nic_aware=True)
+    js = {c: evaluate(p, c)[0] for c in itertools.combinations(range(8), 2)}
+    hi = max(js.values())
+    for eng in ("native", "python"):
+        w = worst(t, 2, engine=eng, nic_aware=True)
+        assert abs(w.objective - hi) < 1e-9, (eng, w, hi)
+    assert worst(t, 2, nic_aware=True).objective > worst(t, 2).objective - 1e-12
