@@ -47,6 +47,7 @@ def run(placement: str, a) -> dict:
            + (["--overlap-transposes"] if a.overlap_transposes else []) + (["--zero1"] if a.zero1 else [])
            + (["--checkpoint"] if a.checkpoint else []) + (["--gemm-table", a.gemm_table] if a.gemm_table else [])
            + ["--graph", a.graph])
+    # dma-buf IPC handles for RCCL's P2P/IPC transport between the ranks (see bench.py main())
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""),
                **extra_env)
     p = subprocess.run(cmd, capture_output=True, text=True, cwd=REPO, env=env, timeout=a.timeout)

@@ -255,8 +255,11 @@ def validate_devices(a, env=None) -> List[int]:
 
 def cmd_validate(a) -> int:
     from ._native import load
+    from .topology.cpus import bind_workload
 
     devs = validate_devices(a)
+    # Gaia B6: the validator's host threads (RCCL proxies) on the pod's cores (GTK_CPUSET from Allocate)
+    cpu_rep = bind_workload(a.cpu_bind, "")
     if a.resolve_only:
         print(json.dumps({"hip_devices": devs}))
         return 0
@@ -268,7 +271,8 @@ def cmd_validate(a) -> int:
     for p in pts:
         print(json.dumps({"k": len(devs), "devices": devs, **p}))
     print(json.dumps({"summary": True, "k": len(devs), "devices": devs, "wrong": wrong, "peak_bytes": peak["bytes"],
-                      "peak_algbw_gbps": round(peak["algbw_gbps"], 2), "peak_busbw_gbps": round(peak["busbw_gbps"], 2)}))
+                      "peak_algbw_gbps": round(peak["algbw_gbps"], 2), "peak_busbw_gbps": round(peak["busbw_gbps"], 2),
+                      "cpuset_applied": {k: cpu_rep.get(k) for k in ("applied", "source", "cpus", "n", "reason")}}))
     return 1 if wrong else 0
 
 
@@ -367,6 +371,7 @@ def main(argv=None) -> int:
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
     p.add_argument("--iters", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--cpu-bind", default="env", choices=["env", "off"], help="pin to GTK_CPUSET (the pod's cores) or not")
     p.set_defaults(fn=cmd_validate)
     p = sub.add_parser("sim")
     p.add_argument("--nodes", type=int, default=2)

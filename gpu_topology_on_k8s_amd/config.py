@@ -133,6 +133,9 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
                                        + ([f"--time-slices={int(time_slices)}"] if int(time_slices) > 1 else []),
                             "ports": [{"containerPort": PLUGIN_METRICS_PORT, "name": "metrics"}],
                             "env": [{"name": "NODE_NAME", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}},
+                                    # the probe / validator children share GPU buffers across processes;
+                                    # the amdgpu host driver exports IPC handles only as dma-bufs, which ROCr
+                                    # uses with the legacy KFD IPC path off (docs/OPERATIONS.md "IPC")
                                     {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}],
                             "securityContext": {"privileged": True},
                             "volumeMounts": [

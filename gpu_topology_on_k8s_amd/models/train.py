@@ -34,6 +34,7 @@ from .gemm_tuning import setup_gemm_tuning
 from .optim import FlatAdamW
 from .checkpoint import CheckpointWriter, load_checkpoint
 from ..parallel.dp import BucketedAllReduce, broadcast_params
+from ..topology.cpus import bind_workload
 
 __all__ = ["train", "main"]
 
@@ -93,7 +94,9 @@ def _choose_device(env, placement: str, discovery: str, visible: Optional[int] =
         use_worst = placement == "worst" and ch.worst
         devices = ch.worst if use_worst else ch.devices  # node-local topology indices (GROUP numbering)
         info = {"devices": devices, "hip_devices": ch.worst_hip if use_worst else ch.hip_devices, "best": ch.devices,
-                "best_score": ch.score, "worst": ch.worst, "worst_score": ch.worst_score, "source": ch.source}
+                "best_score": ch.score, "worst": ch.worst, "worst_score": ch.worst_score, "source": ch.source,
+                # Gaia B6: each rank's share of the node's cores, the slice of its own device
+                "cpusets": ch.extra.get("worst_cpusets") if use_worst else ch.extra.get("cpusets")}
         store.set("gtk/train_placement", json.dumps(info))
     return json.loads(store.get("gtk/train_placement").decode())
 
@@ -104,7 +107,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
           gemm_table: Optional[str] = None, gemm_layout: str = "nt", overlap_transposes: bool = False,
           zero1: bool = False, save_dir: Optional[str] = None, save_every: int = 0, resume: Optional[str] = None,
           keep: int = 2, fuse_residual: bool = True, overlap_norm: bool = False, same_data: bool = False,
-          graph: str = "auto", conv: str = "hip") -> Dict[str, object]:
+          graph: str = "auto", conv: str = "hip", cpu_bind: str = "auto") -> Dict[str, object]:
     env = _init_dist(device_kind)
     if placement == "auto":  # inside a pod the allocation decides; on a bare node, the placement core
         placement = "pod" if os.environ.get("GTK_GPU_GROUP") else "best"
@@ -133,6 +136,14 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
             pl = {"devices": [], "best": [], "worst": None, "source": "cpu"}
         device = torch.device("cpu")
         gemm_mode = "off"
+    # Gaia B6 (paper p.3 "GPU and CPU core are automatically bound"): pin this rank to GTK_CPUSET (the
+    # pod's Allocate env) narrowed to its own device's core slice, or to that slice on a bare node,
+    # before the model, the optimizer and the data path start their host threads
+    own = ""
+    cs = pl.get("cpusets")
+    if cs and env["rank"] < len(cs):
+        own = cs[env["rank"]] or ""
+    cpu_rep = bind_workload(cpu_bind if device_kind == "cuda" else ("env" if cpu_bind == "auto" else cpu_bind), own)
     mnist = model_name.startswith("mnist")
     use_graph = graph == "on" or (graph == "auto" and mnist and device.type == "cuda" and env["world"] == 1)
     if use_graph and device.type != "cuda":
@@ -296,6 +307,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "checkpoints_saved": ckpt.saved if ckpt is not None else [],
         "checkpoint_stats": ckpt.stats if ckpt is not None else None,
         "max_mem_gb": (torch.cuda.max_memory_allocated(device) / 1e9) if device.type == "cuda" else None,
+        "cpuset_applied": {k: cpu_rep.get(k) for k in ("applied", "source", "cpus", "n", "reason")},
     }
     if log and env["rank"] == 0:
         print(json.dumps(out), flush=True)
@@ -340,6 +352,9 @@ def main(argv=None) -> int:
                     help="capture the whole step into one hipGraph after warmup (auto: MNIST at world 1 on a GPU)")
     ap.add_argument("--conv", default="hip", choices=["hip", "torch"],
                     help="MNIST convolution stack: hip = csrc/ops/mnist_conv.hip (MFMA), torch = MIOpen via F.conv2d")
+    ap.add_argument("--cpu-bind", default="auto", choices=["auto", "env", "off"],
+                    help="Gaia B6: pin this rank to GTK_CPUSET narrowed to its device's core slice (auto; on a bare node the "
+                         "slice alone), GTK_CPUSET only (env), or leave the threads unbound (off)")
     ap.add_argument("--overlap-norm", action="store_true",
                     help="clipping norm per bucket on a side stream as buckets complete (measured no gain at world 1)")
     a = ap.parse_args(argv)
@@ -347,7 +362,7 @@ def main(argv=None) -> int:
           gemm_tuning=a.gemm_tuning, gemm_table=a.gemm_table, gemm_layout=a.gemm_layout,
           overlap_transposes=a.overlap_transposes, zero1=a.zero1, save_dir=a.save_dir, save_every=a.save_every,
           resume=a.resume, keep=a.keep, fuse_residual=not a.no_fuse_residual,
-          overlap_norm=a.overlap_norm, same_data=a.same_data, graph=a.graph, conv=a.conv)
+          overlap_norm=a.overlap_norm, same_data=a.same_data, graph=a.graph, conv=a.conv, cpu_bind=a.cpu_bind)
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0

@@ -294,6 +294,7 @@ def choose_subset(k: int, probe: Optional[str] = None, backend: str = "auto", vi
         worst_hip=[dmap.hip(i) for i in w.ids] if w else None,
         extra={"discovery_ms": round((t1 - t0) * 1e3, 2), "node_devices": topo.n, "visible_devices": nvis,
                "device_map": dmap.to_dict(), "worst_exact": bool(w.exact) if w else None, "cpusets": cpusets,
+               "worst_cpusets": [recommended_cpuset(topo, [d]) for d in w.ids] if w else None,
                **({"probe": probe_summary(topo, devices)} if probed else {}),
                **({"k8s": k8s} if k8s is not None else {})},
     )
