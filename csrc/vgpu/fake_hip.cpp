@@ -1,0 +1,59 @@
+// Stand-in HIP runtime (host-only) for CPU tests of libgtk_vgpu.so: the allocation entry points the
+// guard intercepts, backed by tiny host allocations (the requested size is only bookkept), a current
+// device from $FAKE_HIP_DEVICE and a 64 GiB device.  Built as bin/fake_hip/libamdhip64.so so the
+// guard's fallback lookup (a runtime loaded RTLD_LOCAL, found by name among the loaded objects) is
+// exercised exactly as with the PyTorch wheel's bundled runtime.
+#include <cstdlib>
+#include <cstring>
+
+extern "C" {
+
+typedef int hipError_t;
+static const unsigned long long kTotal = 64ull << 30;
+
+__attribute__((visibility("default"))) hipError_t hipGetDevice(int* d) {
+  const char* e = std::getenv("FAKE_HIP_DEVICE");
+  *d = e ? std::atoi(e) : 0;
+  return 0;
+}
+
+static hipError_t fake_alloc(void** p, size_t n) {
+  if (!p) return 1;
+  *p = std::malloc(16 + (n & 7));  // distinct pointers; the size itself is never touched
+  return *p ? 0 : 2;
+}
+
+__attribute__((visibility("default"))) hipError_t hipMalloc(void** p, size_t n) { return fake_alloc(p, n); }
+__attribute__((visibility("default"))) hipError_t hipExtMallocWithFlags(void** p, size_t n, unsigned int) {
+  return fake_alloc(p, n);
+}
+__attribute__((visibility("default"))) hipError_t hipMallocManaged(void** p, size_t n, unsigned int) { return fake_alloc(p, n); }
+__attribute__((visibility("default"))) hipError_t hipMallocAsync(void** p, size_t n, void*) { return fake_alloc(p, n); }
+__attribute__((visibility("default"))) hipError_t hipMallocFromPoolAsync(void** p, size_t n, void*, void*) {
+  return fake_alloc(p, n);
+}
+__attribute__((visibility("default"))) hipError_t hipMallocPitch(void** p, size_t* pitch, size_t w, size_t h) {
+  if (pitch) *pitch = (w + 255) & ~(size_t)255;
+  return fake_alloc(p, w * h);
+}
+__attribute__((visibility("default"))) hipError_t hipFree(void* p) {
+  std::free(p);
+  return 0;
+}
+__attribute__((visibility("default"))) hipError_t hipFreeAsync(void* p, void*) {
+  std::free(p);
+  return 0;
+}
+__attribute__((visibility("default"))) hipError_t hipMemCreate(void** h, size_t n, const void*, unsigned long long) {
+  return fake_alloc(h, n);
+}
+__attribute__((visibility("default"))) hipError_t hipMemRelease(void* h) {
+  std::free(h);
+  return 0;
+}
+__attribute__((visibility("default"))) hipError_t hipMemGetInfo(size_t* f, size_t* t) {
+  if (f) *f = kTotal;
+  if (t) *t = kTotal;
+  return 0;
+}
+}

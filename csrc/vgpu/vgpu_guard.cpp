@@ -1,0 +1,335 @@
+// libgtk_vgpu.so — the container-side tier of a time-sliced GPU share (Gaia's two-tier vGPU).
+//
+// Reference: the Gaia paper (p.3 §III.A "GPU resource virtualization") splits a GPU into vGPUs in
+// its device plugin and enforces each vGPU's limits inside the container by intercepting the GPU API
+// (GaiaGPU's interception library).  On MI355X the device plugin already gives a pod holding part of
+// a GPU its slices' compute units (HSA_CU_MASK, topology/shares.py) and its HBM share
+// (GTK_GPU_FRACTION); both were cooperative: a container could rewrite its environment, and only the
+// framework's own training entry point capped its allocator.  This library, which Allocate mounts
+// into the container and preloads (deviceplugin/plugin.py, --share-guard), makes them hold for any
+// HIP program in the pod:
+//
+//   * HBM: every device allocation of the process (hipMalloc, hipExtMallocWithFlags, hipMallocManaged,
+//     hipMallocPitch, hipMallocAsync, hipMallocFromPoolAsync, hipMemCreate) is counted against the
+//     device's limit and refused with hipErrorOutOfMemory beyond it; frees give it back; hipMemGetInfo
+//     reports the share as the device's total, so caching allocators size themselves to it.
+//   * CUs: HSA_CU_MASK is set from the mounted config before the program's own code runs (a
+//     constructor of a preloaded library runs before main and before any HIP call, and the ROCr
+//     runtime reads the variable when it initialises), whatever the container's environment says.
+//
+// The config is the read-only file ``$GTK_VGPU_CONFIG`` (default /etc/gtk-vgpu.conf) the plugin
+// writes per allocation:
+//     hbm_limit <HIP ordinal> <bytes>
+//     cu_mask <HSA_CU_MASK value>
+// No file: the library is inert (pure pass-through).  Limits are per process, like GaiaGPU's.
+//
+// The real HIP entry points are found with dlsym(RTLD_NEXT); when the runtime was loaded RTLD_LOCAL
+// (the PyTorch wheel's bundled libamdhip64, brought in by Python's extension loader) RTLD_NEXT does
+// not see it, so the loaded objects are searched for libamdhip64 and it is re-opened RTLD_NOLOAD.
+// Host-only C++ (g++): no device code, no HIP headers (the few types needed are ABI-identical
+// stand-ins), no link against any HIP library.
+#include <dlfcn.h>
+#include <link.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+
+namespace {
+
+typedef int hipError_t;  // enum hipError_t: int-sized
+constexpr hipError_t kSuccess = 0;
+constexpr hipError_t kOutOfMemory = 2;  // hipErrorOutOfMemory
+constexpr int kMaxDev = 64;
+
+struct State {
+  std::mutex mu;
+  bool active = false;
+  long long limit[kMaxDev];  // bytes; < 0 = no limit on that ordinal
+  long long used[kMaxDev];
+  std::unordered_map<void*, std::pair<int, size_t>> ptrs;
+  std::unordered_map<unsigned long long, std::pair<int, size_t>> handles;  // hipMemCreate handles
+  std::string cu_mask;
+  State() {
+    for (int i = 0; i < kMaxDev; ++i) limit[i] = -1, used[i] = 0;
+  }
+};
+
+State& st() {
+  static State* s = new State();  // never destroyed: frees may arrive from other libraries' destructors
+  return *s;
+}
+
+void* hip_runtime_handle() {
+  static void* h = nullptr;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    dl_iterate_phdr(
+        [](struct dl_phdr_info* info, size_t, void*) -> int {
+          if (info->dlpi_name && std::strstr(info->dlpi_name, "libamdhip64")) {
+            h = dlopen(info->dlpi_name, RTLD_NOW | RTLD_NOLOAD);
+            return h != nullptr;
+          }
+          return 0;
+        },
+        nullptr);
+  });
+  return h;
+}
+
+template <typename Fn>
+Fn real(const char* name) {
+  void* p = dlsym(RTLD_NEXT, name);
+  if (!p) {
+    void* h = hip_runtime_handle();
+    if (h) p = dlsym(h, name);
+  }
+  if (!p) {
+    std::fprintf(stderr, "gtk-vgpu: cannot resolve %s in the HIP runtime\n", name);
+    std::abort();
+  }
+  return reinterpret_cast<Fn>(p);
+}
+
+#define REAL(name, type)                              \
+  static type real_fn = nullptr;                      \
+  if (!real_fn) real_fn = real<type>(#name);
+
+int current_device() {
+  typedef hipError_t (*F)(int*);
+  REAL(hipGetDevice, F);
+  int d = 0;
+  if (real_fn(&d) != kSuccess || d < 0 || d >= kMaxDev) return 0;
+  return d;
+}
+
+// reserve `bytes` on `dev`; false if the share would be exceeded
+bool reserve(int dev, size_t bytes) {
+  State& s = st();
+  if (!s.active || dev < 0 || dev >= kMaxDev || s.limit[dev] < 0) return true;
+  std::lock_guard<std::mutex> g(s.mu);
+  if (s.used[dev] + (long long)bytes > s.limit[dev]) return false;
+  s.used[dev] += (long long)bytes;
+  return true;
+}
+
+void unreserve(int dev, size_t bytes) {
+  State& s = st();
+  if (!s.active || dev < 0 || dev >= kMaxDev || s.limit[dev] < 0) return;
+  std::lock_guard<std::mutex> g(s.mu);
+  s.used[dev] -= (long long)bytes;
+  if (s.used[dev] < 0) s.used[dev] = 0;
+}
+
+void track(void* p, int dev, size_t bytes) {
+  State& s = st();
+  if (!s.active || !p) return;
+  std::lock_guard<std::mutex> g(s.mu);
+  s.ptrs[p] = {dev, bytes};
+}
+
+void untrack(void* p) {
+  State& s = st();
+  if (!s.active || !p) return;
+  int dev = -1;
+  size_t bytes = 0;
+  {
+    std::lock_guard<std::mutex> g(s.mu);
+    auto it = s.ptrs.find(p);
+    if (it == s.ptrs.end()) return;
+    dev = it->second.first;
+    bytes = it->second.second;
+    s.ptrs.erase(it);
+  }
+  unreserve(dev, bytes);
+}
+
+// one allocation through `call` (which performs the real allocation into *ptr)
+template <typename Call>
+hipError_t guarded(void** ptr, size_t bytes, Call call) {
+  const int dev = current_device();
+  if (!reserve(dev, bytes)) {
+    if (ptr) *ptr = nullptr;
+    return kOutOfMemory;
+  }
+  hipError_t e = call();
+  if (e != kSuccess || !ptr || !*ptr) {
+    unreserve(dev, bytes);
+    return e;
+  }
+  track(*ptr, dev, bytes);
+  return e;
+}
+
+__attribute__((constructor)) void load_config() {
+  const char* path = std::getenv("GTK_VGPU_CONFIG");
+  if (!path || !*path) path = "/etc/gtk-vgpu.conf";
+  FILE* f = std::fopen(path, "r");
+  if (!f) return;  // no share to enforce: pass-through
+  State& s = st();
+  char line[4096];
+  while (std::fgets(line, sizeof line, f)) {
+    char key[64] = {0}, val[4000] = {0};
+    int dev = -1;
+    long long bytes = -1;
+    if (std::sscanf(line, "hbm_limit %d %lld", &dev, &bytes) == 2) {
+      if (dev >= 0 && dev < kMaxDev && bytes >= 0) s.limit[dev] = bytes;
+    } else if (std::sscanf(line, "%63s %3999s", key, val) == 2 && std::strcmp(key, "cu_mask") == 0) {
+      s.cu_mask = val;
+    }
+  }
+  std::fclose(f);
+  s.active = true;
+  if (!s.cu_mask.empty()) setenv("HSA_CU_MASK", s.cu_mask.c_str(), 1);  // before ROCr initialises
+  setenv("GTK_VGPU_ACTIVE", "1", 1);  // lets the workload report that the guard is in force
+}
+
+}  // namespace
+
+extern "C" {
+
+__attribute__((visibility("default"))) hipError_t hipMalloc(void** ptr, size_t size) {
+  typedef hipError_t (*F)(void**, size_t);
+  REAL(hipMalloc, F);
+  return guarded(ptr, size, [&] { return real_fn(ptr, size); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipExtMallocWithFlags(void** ptr, size_t size, unsigned int flags) {
+  typedef hipError_t (*F)(void**, size_t, unsigned int);
+  REAL(hipExtMallocWithFlags, F);
+  return guarded(ptr, size, [&] { return real_fn(ptr, size, flags); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipMallocManaged(void** ptr, size_t size, unsigned int flags) {
+  typedef hipError_t (*F)(void**, size_t, unsigned int);
+  REAL(hipMallocManaged, F);
+  return guarded(ptr, size, [&] { return real_fn(ptr, size, flags); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipMallocAsync(void** ptr, size_t size, void* stream) {
+  typedef hipError_t (*F)(void**, size_t, void*);
+  REAL(hipMallocAsync, F);
+  return guarded(ptr, size, [&] { return real_fn(ptr, size, stream); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipMallocFromPoolAsync(void** ptr, size_t size, void* pool, void* stream) {
+  typedef hipError_t (*F)(void**, size_t, void*, void*);
+  REAL(hipMallocFromPoolAsync, F);
+  return guarded(ptr, size, [&] { return real_fn(ptr, size, pool, stream); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipMallocPitch(void** ptr, size_t* pitch, size_t width, size_t height) {
+  typedef hipError_t (*F)(void**, size_t*, size_t, size_t);
+  REAL(hipMallocPitch, F);
+  // the pitch is not known before the call: reserve the unpadded size, then settle to pitch*height
+  const int dev = current_device();
+  const size_t want = width * height;
+  if (!reserve(dev, want)) {
+    if (ptr) *ptr = nullptr;
+    return kOutOfMemory;
+  }
+  hipError_t e = real_fn(ptr, pitch, width, height);
+  if (e != kSuccess || !ptr || !*ptr) {
+    unreserve(dev, want);
+    return e;
+  }
+  const size_t got = (pitch ? *pitch : width) * height;
+  if (got > want && !reserve(dev, got - want)) {
+    typedef hipError_t (*G)(void*);
+    REAL(hipFree, G);
+    real_fn(*ptr);
+    *ptr = nullptr;
+    unreserve(dev, want);
+    return kOutOfMemory;
+  }
+  track(*ptr, dev, got > want ? got : want);
+  return e;
+}
+
+__attribute__((visibility("default"))) hipError_t hipFree(void* ptr) {
+  typedef hipError_t (*F)(void*);
+  REAL(hipFree, F);
+  hipError_t e = real_fn(ptr);
+  if (e == kSuccess) untrack(ptr);
+  return e;
+}
+
+__attribute__((visibility("default"))) hipError_t hipFreeAsync(void* ptr, void* stream) {
+  typedef hipError_t (*F)(void*, void*);
+  REAL(hipFreeAsync, F);
+  hipError_t e = real_fn(ptr, stream);
+  if (e == kSuccess) untrack(ptr);
+  return e;
+}
+
+// hipMemCreate(hipMemGenericAllocationHandle_t* handle, size_t size, const hipMemAllocationProp* prop,
+// unsigned long long flags): the handle is an opaque pointer-sized value
+__attribute__((visibility("default"))) hipError_t hipMemCreate(void** handle, size_t size, const void* prop,
+                                                                unsigned long long flags) {
+  typedef hipError_t (*F)(void**, size_t, const void*, unsigned long long);
+  REAL(hipMemCreate, F);
+  const int dev = current_device();
+  if (!reserve(dev, size)) return kOutOfMemory;
+  hipError_t e = real_fn(handle, size, prop, flags);
+  if (e != kSuccess || !handle) {
+    unreserve(dev, size);
+    return e;
+  }
+  State& s = st();
+  if (s.active) {
+    std::lock_guard<std::mutex> g(s.mu);
+    s.handles[(unsigned long long)(*handle)] = {dev, size};
+  }
+  return e;
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemRelease(void* handle) {
+  typedef hipError_t (*F)(void*);
+  REAL(hipMemRelease, F);
+  hipError_t e = real_fn(handle);
+  State& s = st();
+  if (e == kSuccess && s.active) {
+    int dev = -1;
+    size_t bytes = 0;
+    {
+      std::lock_guard<std::mutex> g(s.mu);
+      auto it = s.handles.find((unsigned long long)handle);
+      if (it != s.handles.end()) {
+        dev = it->second.first;
+        bytes = it->second.second;
+        s.handles.erase(it);
+      }
+    }
+    if (dev >= 0) unreserve(dev, bytes);
+  }
+  return e;
+}
+
+// the share is the device's size as far as this process can tell
+__attribute__((visibility("default"))) hipError_t hipMemGetInfo(size_t* free_b, size_t* total_b) {
+  typedef hipError_t (*F)(size_t*, size_t*);
+  REAL(hipMemGetInfo, F);
+  hipError_t e = real_fn(free_b, total_b);
+  State& s = st();
+  const int dev = current_device();
+  if (e != kSuccess || !s.active || s.limit[dev] < 0) return e;
+  std::lock_guard<std::mutex> g(s.mu);
+  const long long left = s.limit[dev] - s.used[dev];
+  if (total_b && (long long)*total_b > s.limit[dev]) *total_b = (size_t)s.limit[dev];
+  if (free_b && (long long)*free_b > left) *free_b = (size_t)(left > 0 ? left : 0);
+  return e;
+}
+
+// introspection for tests and the workload's report: bytes in use / limit on `dev` (-1: no limit)
+__attribute__((visibility("default"))) long long gtk_vgpu_used(int dev) {
+  return (dev >= 0 && dev < kMaxDev) ? st().used[dev] : -1;
+}
+
+__attribute__((visibility("default"))) long long gtk_vgpu_limit(int dev) {
+  return (dev >= 0 && dev < kMaxDev) ? st().limit[dev] : -1;
+}
+
+}  // extern "C"

@@ -11,6 +11,8 @@ Targets (all land in ``gpu_topology_on_k8s_amd/_native/``):
   _rccl       HIP  (hipcc)  RCCL all-reduce validator (librccl)
   _fused      HIP  (hipcc)  PyTorch custom ops for the Llama-3 workload (torch headers)
   bin/rccl_allreduce_bench  standalone validator binary
+  bin/libgtk_vgpu.so        C++  (g++)    HIP allocation guard preloaded into time-sliced pods (csrc/vgpu)
+  bin/fake_hip/libamdhip64.so             stand-in HIP runtime for CPU tests of the guard
 """
 from __future__ import annotations
 
@@ -130,6 +132,12 @@ def targets() -> List[Target]:
         Target("rccl_allreduce_bench", [CSRC / "rccl" / "rccl_allreduce_bench.hip"], "hipcc",
                HERE / "bin" / "rccl_allreduce_bench", [f"-L{rocm_lib}", "-lrccl", f"-Wl,-rpath,{rocm_lib}"],
                deps=[CSRC / "rccl" / "rccl_core.h"], pybind=False, shared=False),
+        # container-side tier of a time-sliced share (Gaia vGPU): HBM cap + forced CU mask, preloaded into
+        # the pod by Allocate (--share-guard); host-only C++, resolves the real HIP entry points at run time
+        Target("vgpu_guard", [CSRC / "vgpu" / "vgpu_guard.cpp"], "gxx", HERE / "bin" / "libgtk_vgpu.so",
+               ["-fvisibility=hidden", "-ldl", "-pthread"], pybind=False),
+        Target("fake_hip", [CSRC / "vgpu" / "fake_hip.cpp"], "gxx", HERE / "bin" / "fake_hip" / "libamdhip64.so",
+               ["-fvisibility=default"], pybind=False),
         Target("_fused", sorted((CSRC / "ops").glob("*.hip")), "hipcc", HERE / f"_fused{EXT}",
                deps=sorted((CSRC / "ops").glob("*.h")), pybind=True, torch=True),
     ]

@@ -144,11 +144,15 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
                                 {"name": "pod-resources", "mountPath": "/var/lib/kubelet/pod-resources", "readOnly": True},
                                 {"name": "sys", "mountPath": "/sys", "readOnly": True},
                                 {"name": "dev", "mountPath": "/dev"},
+                                # time-sliced shares: the vGPU guard library + per-allocation configs the
+                                # plugin writes here are bind-mounted into pods by Allocate (host path = this path)
+                                {"name": "vgpu-guard", "mountPath": "/var/lib/gtk-vgpu"},
                             ],
                         }],
                         "volumes": [
                             {"name": "device-plugins", "hostPath": {"path": "/var/lib/kubelet/device-plugins"}},
                             {"name": "pod-resources", "hostPath": {"path": "/var/lib/kubelet/pod-resources"}},
+                            {"name": "vgpu-guard", "hostPath": {"path": "/var/lib/gtk-vgpu", "type": "DirectoryOrCreate"}},
                             {"name": "sys", "hostPath": {"path": "/sys"}},
                             {"name": "dev", "hostPath": {"path": "/dev"}},
                         ],

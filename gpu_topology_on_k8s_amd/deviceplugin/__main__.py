@@ -142,6 +142,12 @@ def main(argv=None) -> int:
                          "The node label <annotation-prefix>/time-slices overrides it per node")
     ap.add_argument("--label-check-interval", type=float, default=30.0,
                     help="seconds between checks of the node's time-slices label (a change restarts the plugin once idle)")
+    ap.add_argument("--share-guard", default="env", choices=["off", "env", "preload"],
+                    help="--time-slices: mount and preload libgtk_vgpu.so into pods holding part of a GPU, which caps their HIP "
+                         "allocations at the share's HBM and forces their CU mask (env = LD_PRELOAD; preload = an "
+                         "/etc/ld.so.preload mount as well; off = cooperative shares)")
+    ap.add_argument("--share-guard-dir", default="/var/lib/gtk-vgpu",
+                    help="host directory (hostPath, same path inside the DaemonSet) for the guard library and per-allocation configs")
     ap.add_argument("--share-cu-mask", default="on", choices=["on", "off"],
                     help="--time-slices: confine a pod holding part of a GPU to its slices' compute units (HSA_CU_MASK)")
     ap.add_argument("--log-level", default="INFO")
@@ -187,7 +193,7 @@ def main(argv=None) -> int:
                        probe_mark_s=a.probe_mark_seconds, probe_settle_s=a.probe_settle_seconds,
                        probe_yield_s=a.probe_yield_seconds,
                        reconcile_interval=a.reconcile_interval, cdi_dir=a.cdi_dir, nic_env=a.nic_env == "on",
-                       share_cu_mask=a.share_cu_mask == "on",
+                       share_cu_mask=a.share_cu_mask == "on", share_guard=a.share_guard, guard_dir=a.share_guard_dir,
                        policy=PlacementPolicy(partition_aware=a.partition_aware == "on"))
     events = None
     if a.gpu_events == "auto" and a.discovery in ("auto", "amdsmi"):

@@ -226,6 +226,8 @@ class FakeKubelet:
             # what containerd does next: every DeviceSpec must name a device node that exists on the
             # host, or the container is never created (BASELINE config 1 on a kind node)
             missing = [d.host_path for c in resp.container_responses for d in c.devices if not os.path.exists(d.host_path)]
+            # bind-mount sources must exist too (the runtime fails the container otherwise)
+            missing += [m.host_path for c in resp.container_responses for m in c.mounts if not os.path.exists(m.host_path)]
             for c in resp.container_responses:
                 for cd in c.cdi_devices:
                     missing += self._cdi_missing(cd.name)

@@ -135,7 +135,8 @@ class PluginConfig:
                  pod_resources_socket: Optional[str] = POD_RESOURCES_SOCKET, reconcile_interval: float = 10.0,
                  cdi_dir: str = "/var/run/cdi", cdi_kind: str = "amd.com/gpu", nic_env: bool = True,
                  share_cu_mask: bool = True, probe_mark_s: float = 300.0, probe_settle_s: float = 2.0,
-                 probe_yield_s: float = 20.0):
+                 probe_yield_s: float = 20.0, share_guard: str = "off", guard_dir: str = "/var/lib/gtk-vgpu",
+                 guard_lib: Optional[str] = None):
         self.resource_name = resource_name
         self.socket_dir = socket_dir
         self.socket_name = socket_name
@@ -174,6 +175,17 @@ class PluginConfig:
         # time-sliced nodes (topology/shares.py): confine a pod holding part of a GPU to its slices'
         # compute units (HSA_CU_MASK); off = slices share every CU (temporal sharing only)
         self.share_cu_mask = share_cu_mask
+        # the container-side tier of a time-sliced share (csrc/vgpu/vgpu_guard.cpp, Gaia's two-tier
+        # vGPU): a pod holding part of a GPU gets libgtk_vgpu.so mounted and preloaded, which caps its
+        # HIP allocations at the share's HBM and forces its HSA_CU_MASK.  "env" = LD_PRELOAD in the
+        # container env; "preload" = also an /etc/ld.so.preload mount (survives an env override);
+        # "off" = cooperative only.  `guard_dir` is a host directory the plugin writes the library and
+        # the per-allocation configs to (a hostPath mounted at the same path into the DaemonSet)
+        if share_guard not in ("off", "env", "preload"):
+            raise ValueError(f"share_guard must be off|env|preload, got {share_guard!r}")
+        self.share_guard = share_guard
+        self.guard_dir = guard_dir
+        self.guard_lib = guard_lib
         # flow step 8: before the container starts, an RCCL all-reduce over exactly
         # the allocated devices (kubelet PreStartContainer) validates the placement; the measured
         # bus bandwidth is recorded on the pod
@@ -214,6 +226,7 @@ class DevicePluginServer:
         self._alloc_cond = threading.Condition(self._alloc_lock)  # Allocate waits here for a probe to yield
         self._probing = False  # set (under _alloc_lock) while an idle-time re-probe owns the links
         self._cancel = threading.Event()  # set by an Allocate arriving mid-probe: the probe stops
+        self._guard_ready = False  # install_guard() put libgtk_vgpu.so into cfg.guard_dir
         self.allocations: List[Tuple[str, Tuple[int, ...]]] = []  # (pod key or "", ids) log
         self.registered = 0
         self.metrics = PluginMetrics()
@@ -653,8 +666,83 @@ class DevicePluginServer:
             r.envs[k] = v
         if mask:  # after the pod's own RCCL/HSA env: its queues run on its slices' CUs, disjoint from its neighbours'
             r.envs["HSA_CU_MASK"] = mask
+        if slices_per_gpu(self.topology) > 1 and self._guard_ready:
+            self._guard_container(r, ids, mask)
         r.annotations["gputopology.amd.com/devices"] = format_group(ids)
         return r
+
+    # ------------------------------------------------------------------ share guard (vGPU container tier)
+    GUARD_LIB_IN_CONTAINER = "/usr/local/lib/gtk-vgpu/libgtk_vgpu.so"
+    GUARD_CONF_IN_CONTAINER = "/etc/gtk-vgpu.conf"
+
+    def install_guard(self) -> bool:
+        """Copy the guard library into ``guard_dir`` (atomically: a running pod keeps the file it
+        mapped).  -> ready.  A missing library leaves shares cooperative and says so."""
+        self._guard_ready = False
+        if self.cfg.share_guard == "off" or slices_per_gpu(self.topology) <= 1:
+            return False
+        import shutil
+
+        src = self.cfg.guard_lib
+        if src is None:
+            from .._native import NativeUnavailable, binary
+
+            try:
+                src = str(binary("libgtk_vgpu.so"))
+            except NativeUnavailable as e:
+                log.warning("share guard requested but unavailable (%s): time-sliced shares stay cooperative", e)
+                return False
+        try:
+            os.makedirs(os.path.join(self.cfg.guard_dir, "alloc"), exist_ok=True)
+            dst = os.path.join(self.cfg.guard_dir, "libgtk_vgpu.so")
+            tmp = f"{dst}.tmp{os.getpid()}"
+            shutil.copyfile(src, tmp)
+            os.chmod(tmp, 0o755)
+            os.replace(tmp, dst)
+            with open(os.path.join(self.cfg.guard_dir, "ld.so.preload"), "w") as f:
+                f.write(self.GUARD_LIB_IN_CONTAINER + "\n")
+        except OSError as e:
+            log.warning("installing the share guard into %s failed (%s): shares stay cooperative", self.cfg.guard_dir, e)
+            return False
+        self._guard_ready = True
+        return True
+
+    def guard_config(self, ids: Sequence[int], mask: str) -> str:
+        """The guard's config for a container holding the time slices ``ids``: per partly held GPU (its
+        HIP ordinal in the container: position among the held physical GPUs) the HBM of the slices it
+        holds, and the CU mask Allocate computed."""
+        frac = share_fractions(self.topology, ids)
+        lines = ["# gtk-vgpu: written by the device plugin at Allocate (deviceplugin/plugin.py)"]
+        for ordinal, p in enumerate(sorted(frac)):
+            if frac[p] >= 1.0:
+                continue
+            held = [self.topology.gpus[int(i)] for i in ids if self.topology.gpus[int(i)].physical == p]
+            hbm = sum(int(g.vram_bytes) for g in held)
+            if hbm > 0:
+                lines.append(f"hbm_limit {ordinal} {hbm}")
+        if mask:
+            lines.append(f"cu_mask {mask}")
+        return "\n".join(lines) + "\n"
+
+    def _guard_container(self, r: pb.ContainerAllocateResponse, ids: Sequence[int], mask: str) -> None:
+        frac = share_fractions(self.topology, ids)
+        if all(f >= 1.0 for f in frac.values()):
+            return  # whole GPUs only: nothing to guard
+        conf = os.path.join(self.cfg.guard_dir, "alloc", "slices-" + "-".join(str(int(i)) for i in sorted(set(ids))) + ".conf")
+        tmp = f"{conf}.tmp{os.getpid()}"
+        with open(tmp, "w") as f:
+            f.write(self.guard_config(ids, mask))
+        os.replace(tmp, conf)
+        r.mounts.add(container_path=self.GUARD_LIB_IN_CONTAINER, host_path=os.path.join(self.cfg.guard_dir, "libgtk_vgpu.so"),
+                     read_only=True)
+        r.mounts.add(container_path=self.GUARD_CONF_IN_CONTAINER, host_path=conf, read_only=True)
+        r.envs["GTK_VGPU_CONFIG"] = self.GUARD_CONF_IN_CONTAINER
+        if self.cfg.share_guard == "preload":
+            r.mounts.add(container_path="/etc/ld.so.preload", host_path=os.path.join(self.cfg.guard_dir, "ld.so.preload"),
+                         read_only=True)
+        else:
+            r.envs["LD_PRELOAD"] = self.GUARD_LIB_IN_CONTAINER
+        self.metrics.guarded.inc()
 
     def _rccl_env(self, pod: dict) -> Dict[str, str]:
         if not self.cfg.pass_rccl_env:
@@ -826,6 +914,7 @@ class DevicePluginServer:
 
     def start(self, register: bool = True) -> None:
         self._stop.clear()
+        self.install_guard()
         self.write_cdi_spec()
         self._publish_node()
         self.serve()

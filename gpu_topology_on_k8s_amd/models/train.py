@@ -308,6 +308,8 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "checkpoint_stats": ckpt.stats if ckpt is not None else None,
         "max_mem_gb": (torch.cuda.max_memory_allocated(device) / 1e9) if device.type == "cuda" else None,
         "cpuset_applied": {k: cpu_rep.get(k) for k in ("applied", "source", "cpus", "n", "reason")},
+        # a time-sliced share's container tier (libgtk_vgpu.so preloaded by Allocate) in force in this process
+        "share_guard": os.environ.get("GTK_VGPU_ACTIVE") == "1",
     }
     if log and env["rank"] == 0:
         print(json.dumps(out), flush=True)

@@ -189,7 +189,7 @@ class SimCluster:
                  policy: PlacementPolicy = PlacementPolicy(), assume_ttl: float = 300.0, use_filter: bool = True,
                  node_labels: Optional[Dict[str, Dict[str, str]]] = None, device_specs: str = "strict",
                  prestart_validate: bool = False, validate_fn=None, reconcile_interval: float = 0.0,
-                 informer: bool = False):
+                 informer: bool = False, share_guard: str = "env"):
         self.resource = resource
         # drive the extender's cache by LIST+WATCH (production mode) instead of a LIST per request
         self.use_informer = informer
@@ -197,6 +197,7 @@ class SimCluster:
         # the plugins' pod-resources reconcile loop (0 = only when reconcile() is called: deterministic tests)
         self.reconcile_interval = reconcile_interval
         self.device_specs = device_specs
+        self.share_guard = share_guard  # time-sliced nodes: the vGPU guard mounted into partial-GPU pods
         self.prestart_validate = prestart_validate
         self.validate_fn = validate_fn
         self.contract = Contract(resource_name=resource)
@@ -233,7 +234,9 @@ class SimCluster:
                                                            device_specs=self.device_specs,
                                                            prestart_validate=self.prestart_validate,
                                                            pod_resources_socket=kubelet.pod_resources_socket,
-                                                           reconcile_interval=self.reconcile_interval),
+                                                           reconcile_interval=self.reconcile_interval,
+                                                           share_guard=self.share_guard,
+                                                           guard_dir=os.path.join(self._root, f"vgpu{i}")),
                                         api=self.api, validate_fn=self.validate_fn)
             plugin.start()
             kubelet.wait_for(res)

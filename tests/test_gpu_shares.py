@@ -173,3 +173,52 @@ def test_prestart_validation_of_a_fractional_pod():
         assert r.error == "" and len(r.allocated) == 2
         v = json.loads(c.api.get_pod("default", "half")["metadata"]["annotations"][Contract().validated_key])
         assert v["k"] == 1 and v["peak_algbw_gbps"] > 100
+
+
+_GUARD_CHILD = r"""
+import json, os, torch
+from gpu_topology_on_k8s_amd.ops.probe import warmup
+free, total = torch.cuda.mem_get_info(0)
+x = torch.empty(12 << 30, dtype=torch.uint8, device="cuda")
+try:
+    y = torch.empty(8 << 30, dtype=torch.uint8, device="cuda")
+    over_refused = False
+except torch.OutOfMemoryError:
+    over_refused = True
+del x
+torch.cuda.empty_cache()
+z = torch.empty(15 << 30, dtype=torch.uint8, device="cuda")  # fits again once the 12 GiB went back
+del z
+torch.cuda.empty_cache()
+r = warmup(0, 30.0)
+print(json.dumps({"total": total, "free": free, "over_refused": over_refused, "mask": os.environ.get("HSA_CU_MASK"),
+                  "active": os.environ.get("GTK_VGPU_ACTIVE"), "tflops": r["tflops"]}))
+"""
+
+
+def test_vgpu_guard_caps_torch_and_forces_the_cu_mask(tmp_path):
+    """The container tier of a share on the real GPU: a torch process with libgtk_vgpu.so preloaded and
+    a 16 GiB / 64-CU share sees 16 GiB, cannot allocate past it, and runs on 64 CUs even though its own
+    environment asks for all 256 (the container rewrote HSA_CU_MASK)."""
+    from gpu_topology_on_k8s_amd._native import binary
+
+    conf = tmp_path / "gtk-vgpu.conf"
+    conf.write_text(f"hbm_limit 0 {16 << 30}\ncu_mask 0:0-63\n")
+    env = {k: v for k, v in os.environ.items() if k not in _STRIP}
+    env.update(GTK_VGPU_CONFIG=str(conf), HSA_CU_MASK="0:0-255")
+    guard = str(binary("libgtk_vgpu.so"))
+    env["LD_PRELOAD"] = (env["LD_PRELOAD"] + ":" if env.get("LD_PRELOAD") else "") + guard  # keep what is preloaded
+    p = subprocess.run([sys.executable, "-c", _GUARD_CHILD], capture_output=True, text=True, timeout=240, cwd=REPO, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    g = json.loads(p.stdout.strip().splitlines()[-1])
+    base_env = {k: v for k, v in os.environ.items() if k not in _STRIP}
+    base_env.pop("HSA_CU_MASK", None)
+    q = subprocess.run([sys.executable, "-c", "import json; from gpu_topology_on_k8s_amd.ops.probe import warmup;"
+                        "print(json.dumps(warmup(0, 30.0)))"], capture_output=True, text=True, timeout=240, cwd=REPO, env=base_env)
+    assert q.returncode == 0, q.stderr[-3000:]
+    full = json.loads(q.stdout.strip().splitlines()[-1])["tflops"]
+    print(json.dumps({"guarded": g, "full_tflops": full}))
+    assert g["active"] == "1" and g["mask"] == "0:0-63"
+    assert g["total"] == 16 << 30 and g["free"] <= 16 << 30
+    assert g["over_refused"] is True
+    assert 0.15 * full < g["tflops"] < 0.40 * full, (g["tflops"], full)  # 64 of 256 CUs (27 % measured in r02)

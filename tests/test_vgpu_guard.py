@@ -1,0 +1,129 @@
+"""The container-side tier of a time-sliced share (Gaia two-tier vGPU, paper p.3 §III.A):
+``libgtk_vgpu.so`` preloaded into a pod caps every HIP allocation at the share's HBM and forces the
+share's HSA_CU_MASK whatever the container's environment says.  CPU tests run it against a stand-in
+HIP runtime named ``libamdhip64.so`` (csrc/vgpu/fake_hip.cpp), loaded both ways a real process loads
+HIP: RTLD_LOCAL (the PyTorch wheel's bundled runtime, found by the guard's fallback lookup) and
+RTLD_GLOBAL (found by RTLD_NEXT)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from gpu_topology_on_k8s_amd._native import binary
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GiB = 1 << 30
+
+CHILD = r"""
+import ctypes, json, os, sys
+mode = ctypes.RTLD_GLOBAL if sys.argv[2] == "global" else ctypes.RTLD_LOCAL
+ctypes.CDLL(sys.argv[1], mode=mode)           # the 'HIP runtime' the application links
+g = ctypes.CDLL(None)                          # symbols as the application resolves them
+vp = ctypes.c_void_p
+def malloc(n, fn="hipMalloc"):
+    p = vp()
+    if fn == "hipMallocPitch":
+        pitch = ctypes.c_size_t()
+        return g.hipMallocPitch(ctypes.byref(p), ctypes.byref(pitch), ctypes.c_size_t(n), ctypes.c_size_t(1)), p
+    args = {"hipMalloc": (), "hipExtMallocWithFlags": (ctypes.c_uint(0),), "hipMallocManaged": (ctypes.c_uint(1),),
+            "hipMallocAsync": (vp(),)}[fn]
+    return getattr(g, fn)(ctypes.byref(p), ctypes.c_size_t(n), *args), p
+GiB = 1 << 30
+out = {"env_mask": os.environ.get("HSA_CU_MASK"), "active": os.environ.get("GTK_VGPU_ACTIVE")}
+e1, p1 = malloc(6 * GiB)
+e2, p2 = malloc(3 * GiB, "hipExtMallocWithFlags")    # 6 + 3 > 8: refused
+e3, p3 = malloc(2 * GiB, "hipMallocManaged")
+g.gtk_vgpu_used.restype = ctypes.c_longlong
+used_after = g.gtk_vgpu_used(0)
+free_, total = ctypes.c_size_t(), ctypes.c_size_t()
+g.hipMemGetInfo(ctypes.byref(free_), ctypes.byref(total))
+g.hipFree(p1)
+e4, p4 = malloc(5 * GiB, "hipMallocAsync")          # fits again once 6 GiB came back
+e5, p5 = malloc(1 << 20, "hipMallocPitch")
+os.environ["FAKE_HIP_DEVICE"] = "1"                 # no limit configured on ordinal 1
+e6, p6 = malloc(40 * GiB)
+out.update(e=[e1, e2, e3, e4, e5, e6], p2_null=not p2.value, used_after=used_after, free=free_.value, total=total.value,
+           used_end=g.gtk_vgpu_used(0))
+print(json.dumps(out))
+"""
+
+
+def _run(tmp_path, mode, config=True, env_mask="0:0-255"):
+    fake = os.path.join(os.path.dirname(str(binary("libgtk_vgpu.so"))), "fake_hip", "libamdhip64.so")
+    conf = tmp_path / "gtk-vgpu.conf"
+    if config:
+        conf.write_text(f"# written by the device plugin at Allocate\nhbm_limit 0 {8 * GiB}\ncu_mask 0:64-127\n")
+    env = dict(os.environ, GTK_VGPU_CONFIG=str(conf), HSA_CU_MASK=env_mask, FAKE_HIP_DEVICE="0")
+    guard = str(binary("libgtk_vgpu.so"))
+    env["LD_PRELOAD"] = (env["LD_PRELOAD"] + ":" if env.get("LD_PRELOAD") else "") + guard  # keep what is preloaded already
+    p = subprocess.run([sys.executable, "-c", CHILD, fake, mode], capture_output=True, text=True, timeout=60, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("mode", ["local", "global"])
+def test_guard_caps_hbm_and_forces_the_cu_mask(tmp_path, mode):
+    out = _run(tmp_path, mode)
+    assert out["active"] == "1" and out["env_mask"] == "0:64-127"  # the container's own value is overridden
+    e1, e2, e3, e4, e5, e6 = out["e"]
+    assert e1 == 0 and e2 == 2 and out["p2_null"]  # hipErrorOutOfMemory past the share
+    assert e3 == 0 and out["used_after"] == 8 * GiB  # exactly at the share is fine
+    assert out["total"] == 8 * GiB and out["free"] == 0  # hipMemGetInfo reports the share
+    assert e4 == 0 and e5 == 0 and e6 == 0  # freed memory returns; other ordinals are not limited
+    assert out["used_end"] == 7 * GiB + (1 << 20)  # 2 (managed) + 5 (async) GiB + one pitched 1 MiB row
+
+
+def test_guard_without_config_is_a_pass_through(tmp_path):
+    out = _run(tmp_path, "local", config=False)
+    assert out["active"] is None and out["env_mask"] == "0:0-255"
+    assert out["e"] == [0, 0, 0, 0, 0, 0] and out["total"] == 64 * GiB
+
+
+def test_allocate_mounts_the_guard_for_a_partial_gpu_only():
+    """Through the cluster: a 0.5-GPU pod on a 4-slice node gets the guard library and its config
+    mounted read-only and preloaded; the config caps ordinal 0 at its two slices' HBM and carries the
+    same CU mask as the env; a pod holding whole GPUs' worth of slices gets no guard."""
+    from gpu_topology_on_k8s_amd.k8s import Contract
+    from gpu_topology_on_k8s_amd.sim import SimCluster
+    from gpu_topology_on_k8s_amd.topology import fixtures as fx
+    from gpu_topology_on_k8s_amd.topology.shares import time_slice
+
+    C = Contract()
+    v = time_slice(fx.f7_mi355x(n=2), 4)
+    with SimCluster({"s": v}) as c:
+        c.submit("half", 2, slices=True, annotations={C.fraction_key: "0.5"})
+        r = c.schedule_pending()[0]
+        assert r.node == "s", r
+        resp = c.nodes["s"].kubelet.responses["default/half"].container_responses[0]
+        envs = dict(resp.envs)
+        mounts = {m.container_path: (m.host_path, m.read_only) for m in resp.mounts}
+        assert envs["LD_PRELOAD"] == "/usr/local/lib/gtk-vgpu/libgtk_vgpu.so" and envs["GTK_VGPU_CONFIG"] == "/etc/gtk-vgpu.conf"
+        lib, ro = mounts["/usr/local/lib/gtk-vgpu/libgtk_vgpu.so"]
+        assert ro and os.path.getsize(lib) == os.path.getsize(str(binary("libgtk_vgpu.so")))
+        conf, ro = mounts["/etc/gtk-vgpu.conf"]
+        text = open(conf).read()
+        assert ro and f"hbm_limit 0 {2 * (288_000_000_000 // 4)}" in text and f"cu_mask {envs['HSA_CU_MASK']}" in text
+        c.submit("whole", 4, slices=True)  # a whole GPU's worth of slices: no share to guard
+        r = c.schedule_pending()[0]
+        resp = c.nodes["s"].kubelet.responses["default/whole"].container_responses[0]
+        assert r.node == "s" and not resp.mounts and "LD_PRELOAD" not in dict(resp.envs)
+        assert "gtk_plugin_guarded_containers_total 1.0" in c.nodes["s"].plugin.metrics.exposition().decode()
+
+
+def test_preload_mode_mounts_ld_so_preload(tmp_path):
+    from gpu_topology_on_k8s_amd.deviceplugin import DevicePluginServer, PluginConfig
+    from gpu_topology_on_k8s_amd.topology import fixtures as fx
+    from gpu_topology_on_k8s_amd.topology.shares import time_slice
+
+    v = time_slice(fx.f7_mi355x(n=2), 4)
+    plug = DevicePluginServer(v, PluginConfig(device_specs="stub", dev_root=str(tmp_path), share_guard="preload",
+                                              guard_dir=str(tmp_path / "g")))
+    assert plug.install_guard()
+    r = plug._container_response([0], {})
+    mounts = {m.container_path: m.host_path for m in r.mounts}
+    assert open(mounts["/etc/ld.so.preload"]).read().strip() == "/usr/local/lib/gtk-vgpu/libgtk_vgpu.so"
+    assert "LD_PRELOAD" not in dict(r.envs)
+    whole = DevicePluginServer(fx.f7_mi355x(n=2), PluginConfig(share_guard="env", guard_dir=str(tmp_path / "w")))
+    assert whole.install_guard() is False  # whole-GPU nodes: nothing to guard

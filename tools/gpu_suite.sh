@@ -32,6 +32,12 @@ case "$mode" in
     step prof_bench 600 rocprofv3 --kernel-trace --stats -d "$out/prof_bench" -o run -- python3 bench.py --steps 5 --warmup 2 --sweep off
     step prof_probe 600 rocprofv3 --kernel-trace --stats -d "$out/prof_probe" -o run -- python3 -m gpu_topology_on_k8s_amd probe --preset full
     ;;
+  ring)
+    # K6 concurrent ring probe: kernel stats, then LDS and memory counters, each pass in its own run
+    step prof_ring 300 rocprofv3 --kernel-trace --stats -d "$out/prof_ring" -o run -- python3 -m gpu_topology_on_k8s_amd ring --devices 0,0,0 --preset full
+    step pmc_ring_lds 120 timeout -s KILL 90 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES --kernel-trace -d "$out/pmc_ring_lds" -o run -- python3 -m gpu_topology_on_k8s_amd ring --devices 0,0,0 --preset full --patterns all
+    step pmc_ring_mem 120 timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum --kernel-trace -d "$out/pmc_ring_mem" -o run -- python3 -m gpu_topology_on_k8s_amd ring --devices 0,0,0 --preset full --patterns all
+    ;;
   cumask)
     # MFMA rate and HBM copy under HSA_CU_MASK (the time-sliced shares' spatial split, profiles/r02_cumask)
     for m in "" "0:0-127" "0:0-63" "0:0-31,128-159"; do

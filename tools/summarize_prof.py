@@ -61,14 +61,32 @@ def stats_tables(d: str):
     return out
 
 
+def _db_counter_rows(f: str):
+    """rocpd database: the ``counters_collection`` view, one row per (dispatch, counter), mapped onto
+    the CSV column names the aggregation below reads."""
+    import sqlite3
+
+    c = sqlite3.connect(f)
+    cols = [r[1] for r in c.execute("pragma table_info(counters_collection)")]
+    if "counter_name" not in cols:
+        return []
+    q = ("select kernel_name, counter_name, value, dispatch_id, start, end, grid_size, workgroup_size, lds_block_size, "
+         "vgpr_count, accum_vgpr_count, sgpr_count from counters_collection")
+    keys = ("Kernel_Name", "Counter_Name", "Counter_Value", "Dispatch_Id", "Start_Timestamp", "End_Timestamp", "Grid_Size",
+            "Workgroup_Size", "LDS_Block_Size", "VGPR_Count", "Accum_VGPR_Count", "SGPR_Count")
+    return [dict(zip(keys, r)) for r in c.execute(q)]
+
+
 def pmc_tables(d: str):
     out = []
-    for f in sorted(glob.glob(os.path.join(d, "*counter_collection.csv"))):
+    sources = [(f, list(csv.DictReader(open(f)))) for f in sorted(glob.glob(os.path.join(d, "*counter_collection.csv")))]
+    sources += [(f, rows) for f in sorted(glob.glob(os.path.join(d, "*.db"))) for rows in [_db_counter_rows(f)] if rows]
+    for f, rows in sources:
         agg = defaultdict(lambda: defaultdict(float))
         meta = {}
         wall = defaultdict(float)
         seen = set()
-        for r in csv.DictReader(open(f)):
+        for r in rows:
             k = short(r["Kernel_Name"])
             agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
             did = (r["Dispatch_Id"], k)
