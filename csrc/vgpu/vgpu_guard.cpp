@@ -21,7 +21,12 @@
 // writes per allocation:
 //     hbm_limit <HIP ordinal> <bytes>
 //     cu_mask <HSA_CU_MASK value>
-// No file: the library is inert (pure pass-through).  Limits are per process, like GaiaGPU's.
+//     acct <path>                  (optional) pod-wide accounting file, shared read-write
+// No file: the library is inert (pure pass-through).  Without ``acct`` the limit holds per process.
+// With it, every process of the pod that maps the file draws from one budget: the file is a table of
+// per-process slots (bytes in use per device); a process owns its slot by holding an fcntl write lock
+// on the slot's first byte, so the kernel drops a crashed process's usage with its lock — whatever PID
+// namespace the pod's containers live in — and the next process reuses the slot.
 //
 // The real HIP entry points are found with dlsym(RTLD_NEXT); when the runtime was loaded RTLD_LOCAL
 // (the PyTorch wheel's bundled libamdhip64, brought in by Python's extension loader) RTLD_NEXT does
@@ -29,8 +34,15 @@
 // Host-only C++ (g++): no device code, no HIP headers (the few types needed are ABI-identical
 // stand-ins), no link against any HIP library.
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <link.h>
+#include <sys/file.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
+#include <cstddef>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -45,9 +57,27 @@ constexpr hipError_t kSuccess = 0;
 constexpr hipError_t kOutOfMemory = 2;  // hipErrorOutOfMemory
 constexpr int kMaxDev = 64;
 
+// pod-wide accounting table (the `acct` file)
+constexpr int kSlots = 128;
+constexpr uint64_t kMagic = 0x67746b7667707531ull;  // "gtkvgpu1"
+struct Slot {
+  int32_t pid;
+  int32_t reserved;
+  int64_t used[kMaxDev];
+};
+struct Table {
+  uint64_t magic;
+  uint64_t nslots;
+  Slot slot[kSlots];
+};
+
 struct State {
   std::mutex mu;
   bool active = false;
+  int acct_fd = -1;          // shared accounting file (pod-wide budget), -1 = per process
+  Table* table = nullptr;
+  int mine = -1;             // this process's slot
+  pid_t mine_pid = 0;        // the process that claimed `mine` (a forked child claims its own)
   long long limit[kMaxDev];  // bytes; < 0 = no limit on that ordinal
   long long used[kMaxDev];
   std::unordered_map<void*, std::pair<int, size_t>> ptrs;
@@ -106,11 +136,67 @@ int current_device() {
   return d;
 }
 
-// reserve `bytes` on `dev`; false if the share would be exceeded
+off_t slot_offset(int i) { return (off_t)(offsetof(Table, slot) + (size_t)i * sizeof(Slot)); }
+
+// another process holds slot i (its fcntl lock); our own lock never shows up in F_GETLK
+bool slot_alive(int fd, int i) {
+  struct flock fl{};
+  fl.l_type = F_WRLCK;
+  fl.l_whence = SEEK_SET;
+  fl.l_start = slot_offset(i);
+  fl.l_len = 1;
+  if (fcntl(fd, F_GETLK, &fl) != 0) return true;  // unknown: count it
+  return fl.l_type != F_UNLCK;
+}
+
+// call with s.mu and the file's flock held: make sure this process owns a slot of the table
+bool own_slot(State& s) {
+  if (s.mine >= 0 && s.mine_pid == getpid()) return true;
+  for (int i = 0; i < kSlots; ++i) {
+    if (slot_alive(s.acct_fd, i)) continue;  // another live process's
+    struct flock fl{};
+    fl.l_type = F_WRLCK;
+    fl.l_whence = SEEK_SET;
+    fl.l_start = slot_offset(i);
+    fl.l_len = 1;
+    if (fcntl(s.acct_fd, F_SETLK, &fl) != 0) continue;
+    Slot& sl = s.table->slot[i];
+    sl.pid = (int32_t)getpid();
+    for (int d = 0; d < kMaxDev; ++d) sl.used[d] = 0;  // a dead owner's bytes died with it
+    s.mine = i;
+    s.mine_pid = getpid();
+    return true;
+  }
+  return false;  // table full: this process falls back to its own budget
+}
+
+struct FileLock {  // whole-table critical section across the pod's processes
+  int fd;
+  explicit FileLock(int f) : fd(f) {
+    if (fd >= 0) flock(fd, LOCK_EX);
+  }
+  ~FileLock() {
+    if (fd >= 0) flock(fd, LOCK_UN);
+  }
+};
+
+// reserve `bytes` on `dev`; false if the share would be exceeded (pod-wide with an acct file)
 bool reserve(int dev, size_t bytes) {
   State& s = st();
   if (!s.active || dev < 0 || dev >= kMaxDev || s.limit[dev] < 0) return true;
   std::lock_guard<std::mutex> g(s.mu);
+  if (s.table) {
+    FileLock fl(s.acct_fd);
+    if (own_slot(s)) {
+      long long total = 0;
+      for (int i = 0; i < kSlots; ++i)
+        if (i == s.mine || slot_alive(s.acct_fd, i)) total += s.table->slot[i].used[dev];
+      if (total + (long long)bytes > s.limit[dev]) return false;
+      s.table->slot[s.mine].used[dev] += (long long)bytes;
+      s.used[dev] += (long long)bytes;
+      return true;
+    }
+  }
   if (s.used[dev] + (long long)bytes > s.limit[dev]) return false;
   s.used[dev] += (long long)bytes;
   return true;
@@ -120,8 +206,57 @@ void unreserve(int dev, size_t bytes) {
   State& s = st();
   if (!s.active || dev < 0 || dev >= kMaxDev || s.limit[dev] < 0) return;
   std::lock_guard<std::mutex> g(s.mu);
+  if (s.table && s.mine >= 0 && s.mine_pid == getpid()) {
+    FileLock fl(s.acct_fd);
+    int64_t& u = s.table->slot[s.mine].used[dev];
+    u -= (long long)bytes;
+    if (u < 0) u = 0;
+  }
   s.used[dev] -= (long long)bytes;
   if (s.used[dev] < 0) s.used[dev] = 0;
+}
+
+// bytes in use on `dev` by the whole pod (acct file) or this process
+long long pod_used(int dev) {
+  State& s = st();
+  if (!s.table) return s.used[dev];
+  FileLock fl(s.acct_fd);
+  long long total = 0;
+  for (int i = 0; i < kSlots; ++i)
+    if ((i == s.mine && s.mine_pid == getpid()) || slot_alive(s.acct_fd, i)) total += s.table->slot[i].used[dev];
+  return total;
+}
+
+void open_acct(State& s, const char* path) {
+  int fd = open(path, O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+  if (fd < 0) {
+    std::fprintf(stderr, "gtk-vgpu: accounting file %s unavailable; limits hold per process\n", path);
+    return;
+  }
+  {
+    FileLock fl(fd);
+    struct stat sb{};
+    if (fstat(fd, &sb) != 0 || (sb.st_size < (off_t)sizeof(Table) && ftruncate(fd, sizeof(Table)) != 0)) {
+      close(fd);
+      return;
+    }
+  }
+  void* m = mmap(nullptr, sizeof(Table), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  if (m == MAP_FAILED) {
+    close(fd);
+    return;
+  }
+  Table* t = static_cast<Table*>(m);
+  {
+    FileLock fl(fd);
+    if (t->magic != kMagic) {  // a fresh (or foreign) file: format it
+      std::memset(t, 0, sizeof(Table));
+      t->magic = kMagic;
+      t->nslots = kSlots;
+    }
+  }
+  s.acct_fd = fd;
+  s.table = t;
 }
 
 void track(void* p, int dev, size_t bytes) {
@@ -179,6 +314,8 @@ __attribute__((constructor)) void load_config() {
       if (dev >= 0 && dev < kMaxDev && bytes >= 0) s.limit[dev] = bytes;
     } else if (std::sscanf(line, "%63s %3999s", key, val) == 2 && std::strcmp(key, "cu_mask") == 0) {
       s.cu_mask = val;
+    } else if (std::sscanf(line, "%63s %3999s", key, val) == 2 && std::strcmp(key, "acct") == 0) {
+      open_acct(s, val);
     }
   }
   std::fclose(f);
@@ -317,7 +454,7 @@ __attribute__((visibility("default"))) hipError_t hipMemGetInfo(size_t* free_b, 
   const int dev = current_device();
   if (e != kSuccess || !s.active || s.limit[dev] < 0) return e;
   std::lock_guard<std::mutex> g(s.mu);
-  const long long left = s.limit[dev] - s.used[dev];
+  const long long left = s.limit[dev] - pod_used(dev);
   if (total_b && (long long)*total_b > s.limit[dev]) *total_b = (size_t)s.limit[dev];
   if (free_b && (long long)*free_b > left) *free_b = (size_t)(left > 0 ? left : 0);
   return e;
@@ -326,6 +463,13 @@ __attribute__((visibility("default"))) hipError_t hipMemGetInfo(size_t* free_b, 
 // introspection for tests and the workload's report: bytes in use / limit on `dev` (-1: no limit)
 __attribute__((visibility("default"))) long long gtk_vgpu_used(int dev) {
   return (dev >= 0 && dev < kMaxDev) ? st().used[dev] : -1;
+}
+
+// bytes in use on `dev` by every live process sharing the accounting file (= gtk_vgpu_used without one)
+__attribute__((visibility("default"))) long long gtk_vgpu_pod_used(int dev) {
+  if (dev < 0 || dev >= kMaxDev) return -1;
+  std::lock_guard<std::mutex> g(st().mu);
+  return pod_used(dev);
 }
 
 __attribute__((visibility("default"))) long long gtk_vgpu_limit(int dev) {

@@ -674,6 +674,7 @@ class DevicePluginServer:
     # ------------------------------------------------------------------ share guard (vGPU container tier)
     GUARD_LIB_IN_CONTAINER = "/usr/local/lib/gtk-vgpu/libgtk_vgpu.so"
     GUARD_CONF_IN_CONTAINER = "/etc/gtk-vgpu.conf"
+    GUARD_ACCT_IN_CONTAINER = "/var/run/gtk-vgpu.acct"  # pod-wide budget: one accounting table per allocation
 
     def install_guard(self) -> bool:
         """Copy the guard library into ``guard_dir`` (atomically: a running pod keeps the file it
@@ -707,10 +708,11 @@ class DevicePluginServer:
         self._guard_ready = True
         return True
 
-    def guard_config(self, ids: Sequence[int], mask: str) -> str:
+    def guard_config(self, ids: Sequence[int], mask: str, acct: bool = True) -> str:
         """The guard's config for a container holding the time slices ``ids``: per partly held GPU (its
         HIP ordinal in the container: position among the held physical GPUs) the HBM of the slices it
-        holds, and the CU mask Allocate computed."""
+        holds, the CU mask Allocate computed, and the accounting file every process of the pod shares
+        (one budget for the pod, not per process)."""
         frac = share_fractions(self.topology, ids)
         lines = ["# gtk-vgpu: written by the device plugin at Allocate (deviceplugin/plugin.py)"]
         for ordinal, p in enumerate(sorted(frac)):
@@ -722,20 +724,29 @@ class DevicePluginServer:
                 lines.append(f"hbm_limit {ordinal} {hbm}")
         if mask:
             lines.append(f"cu_mask {mask}")
+        if acct:
+            lines.append(f"acct {self.GUARD_ACCT_IN_CONTAINER}")
         return "\n".join(lines) + "\n"
 
     def _guard_container(self, r: pb.ContainerAllocateResponse, ids: Sequence[int], mask: str) -> None:
         frac = share_fractions(self.topology, ids)
         if all(f >= 1.0 for f in frac.values()):
             return  # whole GPUs only: nothing to guard
-        conf = os.path.join(self.cfg.guard_dir, "alloc", "slices-" + "-".join(str(int(i)) for i in sorted(set(ids))) + ".conf")
+        base = os.path.join(self.cfg.guard_dir, "alloc", "slices-" + "-".join(str(int(i)) for i in sorted(set(ids))))
+        conf, acct = base + ".conf", base + ".acct"
         tmp = f"{conf}.tmp{os.getpid()}"
         with open(tmp, "w") as f:
             f.write(self.guard_config(ids, mask))
         os.replace(tmp, conf)
+        # a fresh accounting table for this allocation (these devices are exclusively the new pod's, so
+        # nothing of a previous pod on them can still be running); world-writable: any container user
+        fd = os.open(acct, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o666)
+        os.fchmod(fd, 0o666)
+        os.close(fd)
         r.mounts.add(container_path=self.GUARD_LIB_IN_CONTAINER, host_path=os.path.join(self.cfg.guard_dir, "libgtk_vgpu.so"),
                      read_only=True)
         r.mounts.add(container_path=self.GUARD_CONF_IN_CONTAINER, host_path=conf, read_only=True)
+        r.mounts.add(container_path=self.GUARD_ACCT_IN_CONTAINER, host_path=acct, read_only=False)
         r.envs["GTK_VGPU_CONFIG"] = self.GUARD_CONF_IN_CONTAINER
         if self.cfg.share_guard == "preload":
             r.mounts.add(container_path="/etc/ld.so.preload", host_path=os.path.join(self.cfg.guard_dir, "ld.so.preload"),

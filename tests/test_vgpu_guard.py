@@ -105,6 +105,8 @@ def test_allocate_mounts_the_guard_for_a_partial_gpu_only():
         conf, ro = mounts["/etc/gtk-vgpu.conf"]
         text = open(conf).read()
         assert ro and f"hbm_limit 0 {2 * (288_000_000_000 // 4)}" in text and f"cu_mask {envs['HSA_CU_MASK']}" in text
+        acct, ro = mounts["/var/run/gtk-vgpu.acct"]  # the pod's shared budget, writable by any container user
+        assert not ro and "acct /var/run/gtk-vgpu.acct" in text and os.stat(acct).st_mode & 0o666 == 0o666
         c.submit("whole", 4, slices=True)  # a whole GPU's worth of slices: no share to guard
         r = c.schedule_pending()[0]
         resp = c.nodes["s"].kubelet.responses["default/whole"].container_responses[0]
@@ -127,3 +129,51 @@ def test_preload_mode_mounts_ld_so_preload(tmp_path):
     assert "LD_PRELOAD" not in dict(r.envs)
     whole = DevicePluginServer(fx.f7_mi355x(n=2), PluginConfig(share_guard="env", guard_dir=str(tmp_path / "w")))
     assert whole.install_guard() is False  # whole-GPU nodes: nothing to guard
+
+
+HOLDER = r"""
+import ctypes, sys
+ctypes.CDLL(sys.argv[1], mode=ctypes.RTLD_LOCAL)
+g = ctypes.CDLL(None)
+p = ctypes.c_void_p()
+print(g.hipMalloc(ctypes.byref(p), ctypes.c_size_t(6 << 30)), flush=True)
+sys.stdin.readline()          # hold the 6 GiB until told to go; exit WITHOUT freeing (a crash)
+"""
+
+PROBE = r"""
+import ctypes, json, sys
+ctypes.CDLL(sys.argv[1], mode=ctypes.RTLD_LOCAL)
+g = ctypes.CDLL(None)
+g.gtk_vgpu_pod_used.restype = ctypes.c_longlong
+res = []
+for n in [int(x) for x in sys.argv[2].split(",")]:
+    p = ctypes.c_void_p()
+    res.append(g.hipMalloc(ctypes.byref(p), ctypes.c_size_t(n << 30)))
+free_, total = ctypes.c_size_t(), ctypes.c_size_t()
+g.hipMemGetInfo(ctypes.byref(free_), ctypes.byref(total))
+print(json.dumps({"e": res, "pod_used": g.gtk_vgpu_pod_used(0), "free": free_.value}))
+"""
+
+
+def test_pod_wide_budget_across_processes_and_crash_release(tmp_path):
+    """With an ``acct`` file every process of the pod draws from one budget; a process that dies
+    holding memory gives it back (its slot lock dies with it)."""
+    fake = os.path.join(os.path.dirname(str(binary("libgtk_vgpu.so"))), "fake_hip", "libamdhip64.so")
+    conf = tmp_path / "gtk-vgpu.conf"
+    conf.write_text(f"hbm_limit 0 {8 * GiB}\nacct {tmp_path / 'pod.acct'}\n")
+    env = dict(os.environ, GTK_VGPU_CONFIG=str(conf), FAKE_HIP_DEVICE="0")
+    env["LD_PRELOAD"] = (env["LD_PRELOAD"] + ":" if env.get("LD_PRELOAD") else "") + str(binary("libgtk_vgpu.so"))
+    holder = subprocess.Popen([sys.executable, "-c", HOLDER, fake], stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
+    try:
+        assert holder.stdout.readline().strip() == "0"  # 6 of 8 GiB taken by another process of the pod
+        p = subprocess.run([sys.executable, "-c", PROBE, fake, "3,2"], capture_output=True, text=True, timeout=60, env=env)
+        assert p.returncode == 0, p.stderr
+        out = json.loads(p.stdout.strip().splitlines()[-1])
+        assert out["e"] == [2, 0] and out["pod_used"] == 8 * GiB and out["free"] == 0
+    finally:
+        holder.stdin.write("go\n")
+        holder.stdin.flush()
+        holder.wait(timeout=30)
+    p = subprocess.run([sys.executable, "-c", PROBE, fake, "5"], capture_output=True, text=True, timeout=60, env=env)
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["e"] == [0] and out["pod_used"] == 5 * GiB  # the dead processes' bytes are gone
