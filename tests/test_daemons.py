@@ -187,9 +187,10 @@ def test_device_plugin_daemon_time_slices():
     kubelet.start()
     devroot = os.path.join(sockdir, "dev")
     os.makedirs(devroot)
+    guard_dir = os.path.join(sockdir, "vgpu")
     p = _spawn(["gpu_topology_on_k8s_amd.deviceplugin", "--discovery", "fake", "--fake-gpus", "2", "--label-check-interval", "2",
                 "--apiserver", url, "--node-name", "worker-1", "--socket-dir", sockdir, "--dev-root", devroot,
-                "--log-level", "WARNING"])
+                "--share-guard-dir", guard_dir, "--log-level", "WARNING"])
     try:
         plugin = kubelet.wait_for("amd.com/gpu-slice", timeout=60)
         assert sorted(plugin.devices, key=int) == [str(i) for i in range(8)] and "amd.com/gpu" not in kubelet.plugins
@@ -199,6 +200,11 @@ def test_device_plugin_daemon_time_slices():
         pod = api.create_pod(make_pod("half", gpus=2, node="worker-1", resource="amd.com/gpu-slice"))
         c = kubelet.admit(pod, "amd.com/gpu-slice").container_responses[0]
         assert c.envs["GTK_GPU_FRACTION"] == "0.5" and len(c.envs["GTK_GPU_GROUP"].split(",")) == 1
+        # the daemon's default --share-guard env: the vGPU guard mounted and preloaded (host paths exist)
+        m = {x.container_path: x.host_path for x in c.mounts}
+        assert c.envs["LD_PRELOAD"] == "/usr/local/lib/gtk-vgpu/libgtk_vgpu.so"
+        assert m["/usr/local/lib/gtk-vgpu/libgtk_vgpu.so"] == os.path.join(guard_dir, "libgtk_vgpu.so")
+        assert all(os.path.exists(h) for h in m.values())
         # the operator relabels the node: the plugin waits while a pod holds devices, then exits for a
         # restart (EX_TEMPFAIL) with the new slicing
         api.patch_node("worker-1", labels={"gputopology.amd.com/time-slices": "2"})
