@@ -36,6 +36,7 @@
 #include <dlfcn.h>
 #include <fcntl.h>
 #include <link.h>
+#include <pthread.h>
 #include <sys/file.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -124,9 +125,8 @@ Fn real(const char* name) {
   return reinterpret_cast<Fn>(p);
 }
 
-#define REAL(name, type)                              \
-  static type real_fn = nullptr;                      \
-  if (!real_fn) real_fn = real<type>(#name);
+// resolved once per entry point; a function-local static is initialised thread-safely
+#define REAL(name, type) static const type real_fn = real<type>(#name);
 
 int current_device() {
   typedef hipError_t (*F)(int*);
@@ -266,20 +266,27 @@ void track(void* p, int dev, size_t bytes) {
   s.ptrs[p] = {dev, bytes};
 }
 
-void untrack(void* p) {
+// forget `p` BEFORE the runtime frees it: once freed, the address can be handed to another thread's
+// allocation, whose entry a late erase would destroy.  -> (device, bytes), or (-1, 0) if untracked
+std::pair<int, size_t> untrack(void* p) {
   State& s = st();
-  if (!s.active || !p) return;
-  int dev = -1;
-  size_t bytes = 0;
-  {
-    std::lock_guard<std::mutex> g(s.mu);
-    auto it = s.ptrs.find(p);
-    if (it == s.ptrs.end()) return;
-    dev = it->second.first;
-    bytes = it->second.second;
-    s.ptrs.erase(it);
+  if (!s.active || !p) return {-1, 0};
+  std::lock_guard<std::mutex> g(s.mu);
+  auto it = s.ptrs.find(p);
+  if (it == s.ptrs.end()) return {-1, 0};
+  auto v = it->second;
+  s.ptrs.erase(it);
+  return v;
+}
+
+// the free went through: give the bytes back; it failed: the allocation is still live
+void settle_free(void* p, std::pair<int, size_t> v, hipError_t e) {
+  if (v.first < 0) return;
+  if (e == kSuccess) {
+    unreserve(v.first, v.second);
+  } else {
+    track(p, v.first, v.second);
   }
-  unreserve(dev, bytes);
 }
 
 // one allocation through `call` (which performs the real allocation into *ptr)
@@ -320,6 +327,17 @@ __attribute__((constructor)) void load_config() {
   }
   std::fclose(f);
   s.active = true;
+  // fork: no thread may hold the lock across it, and the child starts with a budget of its own (HIP
+  // state, and so device memory, does not survive a fork); with an acct file it claims its own slot
+  pthread_atfork([] { st().mu.lock(); }, [] { st().mu.unlock(); },
+                 [] {
+                   State& c = st();
+                   c.mu.unlock();
+                   for (int d = 0; d < kMaxDev; ++d) c.used[d] = 0;
+                   c.ptrs.clear();
+                   c.handles.clear();
+                   c.mine = -1;
+                 });
   if (!s.cu_mask.empty()) setenv("HSA_CU_MASK", s.cu_mask.c_str(), 1);  // before ROCr initialises
   setenv("GTK_VGPU_ACTIVE", "1", 1);  // lets the workload report that the guard is in force
 }
@@ -389,16 +407,18 @@ __attribute__((visibility("default"))) hipError_t hipMallocPitch(void** ptr, siz
 __attribute__((visibility("default"))) hipError_t hipFree(void* ptr) {
   typedef hipError_t (*F)(void*);
   REAL(hipFree, F);
+  auto v = untrack(ptr);
   hipError_t e = real_fn(ptr);
-  if (e == kSuccess) untrack(ptr);
+  settle_free(ptr, v, e);
   return e;
 }
 
 __attribute__((visibility("default"))) hipError_t hipFreeAsync(void* ptr, void* stream) {
   typedef hipError_t (*F)(void*, void*);
   REAL(hipFreeAsync, F);
+  auto v = untrack(ptr);
   hipError_t e = real_fn(ptr, stream);
-  if (e == kSuccess) untrack(ptr);
+  settle_free(ptr, v, e);
   return e;
 }
 
@@ -426,21 +446,26 @@ __attribute__((visibility("default"))) hipError_t hipMemCreate(void** handle, si
 __attribute__((visibility("default"))) hipError_t hipMemRelease(void* handle) {
   typedef hipError_t (*F)(void*);
   REAL(hipMemRelease, F);
-  hipError_t e = real_fn(handle);
   State& s = st();
-  if (e == kSuccess && s.active) {
-    int dev = -1;
-    size_t bytes = 0;
-    {
-      std::lock_guard<std::mutex> g(s.mu);
-      auto it = s.handles.find((unsigned long long)handle);
-      if (it != s.handles.end()) {
-        dev = it->second.first;
-        bytes = it->second.second;
-        s.handles.erase(it);
-      }
+  int dev = -1;
+  size_t bytes = 0;
+  if (s.active) {  // forget the handle before the runtime can reuse its value
+    std::lock_guard<std::mutex> g(s.mu);
+    auto it = s.handles.find((unsigned long long)handle);
+    if (it != s.handles.end()) {
+      dev = it->second.first;
+      bytes = it->second.second;
+      s.handles.erase(it);
     }
-    if (dev >= 0) unreserve(dev, bytes);
+  }
+  hipError_t e = real_fn(handle);
+  if (dev >= 0) {
+    if (e == kSuccess) {
+      unreserve(dev, bytes);
+    } else {
+      std::lock_guard<std::mutex> g(s.mu);
+      s.handles[(unsigned long long)handle] = {dev, bytes};
+    }
   }
   return e;
 }
@@ -462,7 +487,9 @@ __attribute__((visibility("default"))) hipError_t hipMemGetInfo(size_t* free_b, 
 
 // introspection for tests and the workload's report: bytes in use / limit on `dev` (-1: no limit)
 __attribute__((visibility("default"))) long long gtk_vgpu_used(int dev) {
-  return (dev >= 0 && dev < kMaxDev) ? st().used[dev] : -1;
+  if (dev < 0 || dev >= kMaxDev) return -1;
+  std::lock_guard<std::mutex> g(st().mu);
+  return st().used[dev];
 }
 
 // bytes in use on `dev` by every live process sharing the accounting file (= gtk_vgpu_used without one)

@@ -138,6 +138,18 @@ def targets() -> List[Target]:
                ["-fvisibility=hidden", "-ldl", "-pthread"], pybind=False),
         Target("fake_hip", [CSRC / "vgpu" / "fake_hip.cpp"], "gxx", HERE / "bin" / "fake_hip" / "libamdhip64.so",
                ["-fvisibility=default"], pybind=False),
+        # the guard under ThreadSanitizer and under ASan/UBSan (host code only), stressed by many threads
+        # against the stand-in runtime (tests/test_vgpu_guard.py)
+        Target("vgpu_selftest_tsan", [CSRC / "vgpu" / "vgpu_guard.cpp", CSRC / "vgpu" / "vgpu_selftest.cpp"], "gxx",
+               HERE / "bin" / "vgpu_selftest_tsan",
+               ["-g", "-O1", "-fsanitize=thread", "-pthread", "-ldl", f"-L{HERE / 'bin' / 'fake_hip'}", "-l:libamdhip64.so",
+                "-Wl,--disable-new-dtags", f"-Wl,-rpath,{HERE / 'bin' / 'fake_hip'}"], deps=[HERE / "bin" / "fake_hip" / "libamdhip64.so"],
+               pybind=False, shared=False),
+        Target("vgpu_selftest_asan", [CSRC / "vgpu" / "vgpu_guard.cpp", CSRC / "vgpu" / "vgpu_selftest.cpp"], "gxx",
+               HERE / "bin" / "vgpu_selftest_asan",
+               ["-g", "-O1", "-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-pthread", "-ldl",
+                f"-L{HERE / 'bin' / 'fake_hip'}", "-l:libamdhip64.so", "-Wl,--disable-new-dtags", f"-Wl,-rpath,{HERE / 'bin' / 'fake_hip'}"],
+               deps=[HERE / "bin" / "fake_hip" / "libamdhip64.so"], pybind=False, shared=False),
         Target("_fused", sorted((CSRC / "ops").glob("*.hip")), "hipcc", HERE / f"_fused{EXT}",
                deps=sorted((CSRC / "ops").glob("*.h")), pybind=True, torch=True),
     ]
@@ -201,13 +213,18 @@ def build(force: bool = False, only: Optional[List[str]] = None, jobs: int = 4, 
     ts = [t for t in targets() if not only or t.name in only]
     msgs: List[str] = []
     errors: List[str] = []
+    # targets that link another target's output (the guard self-tests link the stand-in runtime) wait
+    # for a first wave of everything else
+    outs = {t.out for t in targets()}
+    waves = [[t for t in ts if not (set(t.deps) & outs)], [t for t in ts if set(t.deps) & outs]]
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        futs = {ex.submit(build_one, t, force, verbose, jobs): t for t in ts}
-        for f in cf.as_completed(futs):
-            try:
-                msgs.append(f.result())
-            except Exception as e:  # noqa: BLE001 - report all failures together
-                errors.append(str(e))
+        for wave in waves:
+            futs = {ex.submit(build_one, t, force, verbose, jobs): t for t in wave}
+            for f in cf.as_completed(futs):
+                try:
+                    msgs.append(f.result())
+                except Exception as e:  # noqa: BLE001 - report all failures together
+                    errors.append(str(e))
     if errors:
         raise RuntimeError("\n\n".join(errors))
     return sorted(msgs)
