@@ -521,9 +521,9 @@ class TopologyExtender:
             st = self.cache.get(node)
             with st.lock:
                 t = st.topology
-                if t is None:
-                    continue
                 now = self.clock()
+                if t is None or st.probing_until > now:  # a node being re-probed is not a candidate either
+                    continue
                 live = {a.uid: a for a in st.allocs.values()
                         if a.uid and (a.assigned or now - a.assume_time <= self.cfg.assume_ttl)}
                 gpu = [u for u in uids if u in live]

@@ -1,6 +1,7 @@
 """Scheduler extender: verbs, assume cache / TTL, concurrency, model quota, HTTP wire format."""
 import asyncio
 import threading
+import time
 
 import pytest
 from aiohttp.test_utils import TestClient, TestServer
@@ -398,6 +399,10 @@ def test_preempt_drops_nodes_where_victims_do_not_suffice():
     assert ext.preempt(pod, {"n1": ([one], 0)}) == {}
     both = [p["metadata"]["uid"] for p, _ in held]
     assert sorted(ext.preempt(pod, {"n1": (both, 0)})["n1"][0]) == sorted(both)
+    # a node under a re-probe mark offers no preemption either (deviceplugin/plugin.py reprobe)
+    api.patch_node("n1", annotations={Contract().probing_key: str(int(time.time()) + 300)})
+    ext.cache.refresh_node("n1")
+    assert ext.preempt(pod, {"n1": (both, 0)}) == {}
 
 
 def test_http_preempt_wire_format():
