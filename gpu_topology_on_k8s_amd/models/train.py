@@ -79,6 +79,11 @@ def apply_share_cap(pl: Dict[str, object], rank: int, dev: int) -> Optional[floa
     fr = pl.get("fractions")
     if not fr or float(fr[rank]) >= 1.0:
         return None
+    if os.environ.get("GTK_VGPU_ACTIVE") == "1":
+        # the vGPU guard (libgtk_vgpu.so, preloaded by Allocate) already enforces the share and reports
+        # it as the device's total through hipMemGetInfo, which is what the allocator's memory
+        # fraction is taken of: capping again would leave fraction x share
+        return float(fr[rank])
     torch.cuda.set_per_process_memory_fraction(float(fr[rank]), dev)
     return float(fr[rank])
 

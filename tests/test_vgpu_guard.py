@@ -197,3 +197,19 @@ def test_guard_under_sanitizers(tmp_path, sanitizer, pod_wide):
     assert p.returncode == 0, (p.stdout[-1000:], p.stderr[-4000:])
     out = json.loads(p.stdout.strip().splitlines()[-1])
     assert out["ok"] > 0 and out["oom"] > 0
+
+
+def test_training_entry_does_not_cap_twice_under_the_guard(monkeypatch):
+    """torch's memory fraction is taken of hipMemGetInfo's total, which the guard already reports as
+    the share: with the guard in force the cooperative cap must not be applied on top of it."""
+    import torch
+
+    from gpu_topology_on_k8s_amd.models import train as tr
+
+    calls = []
+    monkeypatch.setattr(torch.cuda, "set_per_process_memory_fraction", lambda f, d: calls.append((f, d)))
+    monkeypatch.setenv("GTK_VGPU_ACTIVE", "1")
+    assert tr.apply_share_cap({"fractions": [0.25]}, 0, 0) == 0.25 and calls == []
+    monkeypatch.delenv("GTK_VGPU_ACTIVE")
+    assert tr.apply_share_cap({"fractions": [0.25]}, 0, 0) == 0.25 and calls == [(0.25, 0)]
+    assert tr.apply_share_cap({"fractions": [1.0]}, 0, 0) is None
