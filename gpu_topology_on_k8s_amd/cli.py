@@ -9,6 +9,8 @@
   validate  RCCL all-reduce over the allocated devices (GTK_GPU_GROUP or --devices): the
             placement validator of SURVEY.md §3.5 (flow step 8)
   sim       run a small in-process cluster and print the scheduling decisions
+  doctor    node / pod readiness checks (device nodes, discovery, extensions, IPC mode, CPU affinity,
+            a pod's GROUP, cpuset and share guard), one JSON line each; --gpu adds HIP checks
 """
 from __future__ import annotations
 
@@ -373,6 +375,13 @@ def main(argv=None) -> int:
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--cpu-bind", default="env", choices=["env", "off"], help="pin to GTK_CPUSET (the pod's cores) or not")
     p.set_defaults(fn=cmd_validate)
+    p = sub.add_parser("doctor", help="node / pod readiness checks (JSON lines); exit 1 on any failure")
+    p.add_argument("--discovery", default="auto", choices=["auto", "amdsmi", "sysfs", "fake"])
+    p.add_argument("--fake-gpus", type=int, default=None)
+    p.add_argument("--gpu", action="store_true", help="also initialise HIP: device count, gfx950, MFMA warm-up")
+    p.add_argument("--dev-root", default="/dev")
+    p.add_argument("--plugin-dir", default="/var/lib/kubelet/device-plugins")
+    p.set_defaults(fn=lambda a: __import__("gpu_topology_on_k8s_amd.doctor", fromlist=["main"]).main(a))
     p = sub.add_parser("sim")
     p.add_argument("--nodes", type=int, default=2)
     p.add_argument("--pods", default="4,4,2,1,1,8")
