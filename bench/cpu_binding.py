@@ -40,7 +40,7 @@ def _read(path: str) -> str:
         return f.read().strip()
 
 
-def child(cpus: str) -> dict:
+def child(cpus: str, workload: str = "micro") -> dict:
     """Runs in the pinned child: affinity first, then torch."""
     from gpu_topology_on_k8s_amd.topology.cpus import format_cpulist, parse_cpulist
 
@@ -55,6 +55,11 @@ def child(cpus: str) -> dict:
     torch.cuda.set_device(0)
     nb = 256 << 20
     out = {"cpus": format_cpulist(os.sched_getaffinity(0)), "n_cpus": len(os.sched_getaffinity(0))}
+    if workload == "llama8b":  # the flagship step: GPU-bound, so binding should cost nothing here
+        r = train("llama3-8b", batch=2, seq=4096, steps=4, warmup=2, placement="best", log=False, cpu_bind="off")
+        out["llama8b_ms_per_step"] = round(r["ms_per_step"], 2)
+        out["llama8b_tokens_per_s"] = round(r.get("tokens_per_s", 2 * 4096 / (r["ms_per_step"] / 1e3)), 1)
+        return out
 
     def copy_gbps(src, dst, iters):
         dst.copy_(src, non_blocking=True)
@@ -101,13 +106,15 @@ def gpu_pci() -> str:
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--child", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--workload", default="micro", choices=["micro", "llama8b"],
+                    help="micro: copies + launch-bound steps; llama8b: the Llama-3-8B training step (local/remote only)")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--ncpus", type=int, default=16, help="CPUs per pinned configuration (the box's CPU share)")
     ap.add_argument("--out", default="")
     ap.add_argument("--timeout", type=float, default=240.0, help="seconds per child")
     a = ap.parse_args()
     if a.child is not None:
-        print(json.dumps(child(a.child)), flush=True)
+        print(json.dumps(child(a.child, a.workload)), flush=True)
         return 0
 
     from gpu_topology_on_k8s_amd.topology.cpus import format_cpulist, parse_cpulist
@@ -127,16 +134,19 @@ def main() -> int:
     remote = sorted(allowed & nodes[remote_node])[: a.ncpus] if remote_node is not None else []
     configs = {"local": format_cpulist(local), "remote": format_cpulist(remote), "unbound": ""}
     configs = {k: v for k, v in configs.items() if k == "unbound" or v}
+    if a.workload == "llama8b":
+        configs.pop("unbound", None)
     meta = {"gpu_bdf": bdf, "gpu_numa": gpu_numa, "gpu_local_cpulist": format_cpulist(local_list),
             "numa_nodes": {n: format_cpulist(c) for n, c in nodes.items()}, "allowed": format_cpulist(allowed),
-            "remote_numa": remote_node, "configs": configs, "reps": a.reps}
+            "remote_numa": remote_node, "configs": configs, "reps": a.reps, "workload": a.workload}
     print(json.dumps({"meta": meta}), flush=True)
     runs = {k: [] for k in configs}
     for rep in range(a.reps):
         order = list(configs) if rep % 2 == 0 else list(reversed(list(configs)))  # interleaved: no drift bias
         for name in order:
-            p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", configs[name]], capture_output=True, text=True,
-                               timeout=a.timeout, cwd=REPO)
+            print(json.dumps({"rep": rep, "config": name, "starting": True}), flush=True)
+            p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", configs[name], "--workload", a.workload],
+                               capture_output=True, text=True, timeout=a.timeout, cwd=REPO)
             if p.returncode != 0:
                 print(f"child {name} failed: {p.stderr[-1500:]}", file=sys.stderr)
                 return 1
@@ -144,7 +154,7 @@ def main() -> int:
             runs[name].append(r)
             print(json.dumps({"rep": rep, "config": name, **r}), flush=True)
     keys = ["pinned_h2d_gbps", "pinned_d2h_gbps", "pageable_h2d_gbps", "pin_alloc_1g_ms", "llama_tiny_ms_per_step",
-            "mnist_eager_ms_per_step"]
+            "mnist_eager_ms_per_step"] if a.workload == "micro" else ["llama8b_ms_per_step", "llama8b_tokens_per_s"]
     summary = {name: {k: round(statistics.median(r[k] for r in rs), 4) for k in keys} for name, rs in runs.items()}
     if "local" in summary and "remote" in summary:
         summary["remote_vs_local"] = {k: round(summary["remote"][k] / summary["local"][k], 4) for k in keys}
