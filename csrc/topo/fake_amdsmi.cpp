@@ -13,6 +13,14 @@
 //   FAKE_AMDSMI_EVENTS_FILE GPU event script: every line "<processor index> <event id> <message>" is
 //                           delivered once by amdsmi_get_gpu_event_notification (lines appended while
 //                           a watcher runs arrive on its next poll)
+//   FAKE_AMDSMI_STATE       partition state file ("<xcps> <memory mode> <pending memory mode>"): when
+//                           set, it overrides FAKE_AMDSMI_PARTITIONS at every amdsmi_init, and the
+//                           partition setters write it, so a switch shows on the next session (as a
+//                           real compute-partition switch re-enumerates the processors); a memory mode
+//                           is pending until amdsmi_gpu_driver_reload, as on hardware
+//   FAKE_AMDSMI_SET_STATUS  status every partition setter / the driver reload returns instead of acting
+//                           (e.g. 10 = AMDSMI_STATUS_NO_PERM: the plugin is not privileged)
+// Partition rules mirror MI300-class parts: SPX/DPX/QPX/CPX (no TPX), NPS1 always, NPS4 with CPX only.
 // Built by gpu_topology_on_k8s_amd/_native/build.py (target fake_amdsmi); never loaded in production.
 #include <amd_smi/amdsmi.h>
 
@@ -31,6 +39,7 @@ namespace {
 
 struct Node {
   int pkgs = 8, parts = 1, down_a = -1, down_b = -1;
+  std::string mem = "NPS1", mem_pending;
   std::vector<int> hip;
   int n() const { return pkgs * parts; }
 };
@@ -43,10 +52,32 @@ int env_int(const char* k, int d) {
   return v && *v ? std::atoi(v) : d;
 }
 
+void read_state() {
+  const char* path = std::getenv("FAKE_AMDSMI_STATE");
+  if (!path) return;
+  std::ifstream f(path);
+  int parts = 0;
+  std::string mem, pending;
+  if (f >> parts >> mem) {
+    g_node.parts = parts;
+    g_node.mem = mem;
+    if (f >> pending && pending != "-") g_node.mem_pending = pending;
+  }
+}
+
+bool write_state(int parts, const std::string& mem, const std::string& pending) {
+  const char* path = std::getenv("FAKE_AMDSMI_STATE");
+  if (!path) return false;
+  std::ofstream f(path, std::ios::trunc);
+  f << parts << " " << mem << " " << (pending.empty() ? "-" : pending) << "\n";
+  return bool(f);
+}
+
 void load() {
   g_node = Node{};
   g_node.pkgs = env_int("FAKE_AMDSMI_GPUS", 8);
   g_node.parts = env_int("FAKE_AMDSMI_PARTITIONS", 1);
+  read_state();
   const int n = g_node.n();
   g_node.hip.resize(n);
   for (int i = 0; i < n; ++i) g_node.hip[i] = i;
@@ -206,8 +237,78 @@ amdsmi_status_t amdsmi_get_gpu_compute_partition(amdsmi_processor_handle h, char
 
 amdsmi_status_t amdsmi_get_gpu_memory_partition(amdsmi_processor_handle h, char* memory_partition, uint32_t len) {
   if (idx(h) < 0 || !memory_partition || len < 5) return AMDSMI_STATUS_INVAL;
-  std::snprintf(memory_partition, len, "NPS1");
+  std::snprintf(memory_partition, len, "%s", g_node.mem.c_str());
   return AMDSMI_STATUS_SUCCESS;
+}
+
+// ---- partition control (no TPX; NPS4 only together with CPX)
+amdsmi_status_t amdsmi_get_gpu_accelerator_partition_profile_config(amdsmi_processor_handle h,
+                                                                    amdsmi_accelerator_partition_profile_config_t* cfg) {
+  if (idx(h) < 0 || !cfg) return AMDSMI_STATUS_INVAL;
+  const amdsmi_accelerator_partition_type_t types[] = {AMDSMI_ACCELERATOR_PARTITION_SPX, AMDSMI_ACCELERATOR_PARTITION_DPX,
+                                                       AMDSMI_ACCELERATOR_PARTITION_QPX, AMDSMI_ACCELERATOR_PARTITION_CPX};
+  const uint32_t parts[] = {1, 2, 4, 8};
+  cfg->num_profiles = 4;
+  cfg->default_profile_index = 0;
+  for (uint32_t i = 0; i < 4; ++i) {
+    amdsmi_accelerator_partition_profile_t& p = cfg->profiles[i];
+    p.profile_type = types[i];
+    p.num_partitions = parts[i];
+    p.profile_index = i;
+    p.memory_caps.nps_cap_mask = 0;
+    p.memory_caps.nps_flags.nps1_cap = 1;
+    p.memory_caps.nps_flags.nps4_cap = parts[i] == 8;
+  }
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_memory_partition_config(amdsmi_processor_handle h, amdsmi_memory_partition_config_t* cfg) {
+  if (idx(h) < 0 || !cfg) return AMDSMI_STATUS_INVAL;
+  cfg->partition_caps.nps_cap_mask = 0;
+  cfg->partition_caps.nps_flags.nps1_cap = 1;
+  cfg->partition_caps.nps_flags.nps4_cap = 1;
+  cfg->mp_mode = g_node.mem == "NPS4" ? AMDSMI_MEMORY_PARTITION_NPS4 : AMDSMI_MEMORY_PARTITION_NPS1;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_set_gpu_compute_partition(amdsmi_processor_handle h, amdsmi_compute_partition_type_t t) {
+  if (idx(h) < 0) return AMDSMI_STATUS_INVAL;
+  if (const char* st = std::getenv("FAKE_AMDSMI_SET_STATUS")) return (amdsmi_status_t)std::atoi(st);
+  int parts = 0;
+  switch (t) {
+    case AMDSMI_COMPUTE_PARTITION_SPX: parts = 1; break;
+    case AMDSMI_COMPUTE_PARTITION_DPX: parts = 2; break;
+    case AMDSMI_COMPUTE_PARTITION_QPX: parts = 4; break;
+    case AMDSMI_COMPUTE_PARTITION_CPX: parts = 8; break;
+    default: return AMDSMI_STATUS_SETTING_UNAVAILABLE;
+  }
+  if (g_node.mem == "NPS4" && parts != 8) return AMDSMI_STATUS_SETTING_UNAVAILABLE;
+  return write_state(parts, g_node.mem, g_node.mem_pending) ? AMDSMI_STATUS_SUCCESS : AMDSMI_STATUS_NOT_SUPPORTED;
+}
+
+amdsmi_status_t amdsmi_set_gpu_memory_partition(amdsmi_processor_handle h, amdsmi_memory_partition_type_t t) {
+  if (idx(h) < 0) return AMDSMI_STATUS_INVAL;
+  if (const char* st = std::getenv("FAKE_AMDSMI_SET_STATUS")) return (amdsmi_status_t)std::atoi(st);
+  // the session's view: a compute switch written by an earlier session is what the state file holds
+  Node cur = g_node;
+  read_state();
+  const int parts = g_node.parts;
+  g_node = cur;
+  std::string m;
+  if (t == AMDSMI_MEMORY_PARTITION_NPS1) m = "NPS1";
+  else if (t == AMDSMI_MEMORY_PARTITION_NPS4 && parts == 8) m = "NPS4";
+  else return AMDSMI_STATUS_SETTING_UNAVAILABLE;
+  return write_state(parts, g_node.mem, m == g_node.mem ? "" : m) ? AMDSMI_STATUS_SUCCESS : AMDSMI_STATUS_NOT_SUPPORTED;
+}
+
+amdsmi_status_t amdsmi_gpu_driver_reload(void) {
+  if (const char* st = std::getenv("FAKE_AMDSMI_SET_STATUS")) return (amdsmi_status_t)std::atoi(st);
+  Node cur = g_node;
+  read_state();
+  const int parts = g_node.parts;
+  const std::string mem = g_node.mem_pending.empty() ? g_node.mem : g_node.mem_pending;
+  g_node = cur;
+  return write_state(parts, mem, "") ? AMDSMI_STATUS_SUCCESS : AMDSMI_STATUS_NOT_SUPPORTED;
 }
 
 amdsmi_status_t amdsmi_get_gpu_asic_info(amdsmi_processor_handle h, amdsmi_asic_info_t* info) {

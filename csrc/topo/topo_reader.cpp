@@ -18,8 +18,10 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstring>
 #include <fstream>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <sstream>
 #include <stdexcept>
@@ -203,6 +205,12 @@ struct AmdSmi {
   decltype(&amdsmi_set_gpu_event_notification_mask) evt_mask = nullptr;
   decltype(&amdsmi_get_gpu_event_notification) evt_get = nullptr;
   decltype(&amdsmi_stop_gpu_event_notification) evt_stop = nullptr;
+  // partition control (topology/partition.py): read the modes a package offers, switch them
+  decltype(&amdsmi_get_gpu_accelerator_partition_profile_config) get_profiles = nullptr;
+  decltype(&amdsmi_get_gpu_memory_partition_config) get_mpart_cfg = nullptr;
+  decltype(&amdsmi_set_gpu_compute_partition) set_cpart = nullptr;
+  decltype(&amdsmi_set_gpu_memory_partition) set_mpart = nullptr;
+  decltype(&amdsmi_gpu_driver_reload) driver_reload = nullptr;
 
   template <class F>
   void bind(F& f, const char* sym, bool required) {
@@ -238,6 +246,11 @@ struct AmdSmi {
     bind(evt_mask, "amdsmi_set_gpu_event_notification_mask", false);
     bind(evt_get, "amdsmi_get_gpu_event_notification", false);
     bind(evt_stop, "amdsmi_stop_gpu_event_notification", false);
+    bind(get_profiles, "amdsmi_get_gpu_accelerator_partition_profile_config", false);
+    bind(get_mpart_cfg, "amdsmi_get_gpu_memory_partition_config", false);
+    bind(set_cpart, "amdsmi_set_gpu_compute_partition", false);
+    bind(set_mpart, "amdsmi_set_gpu_memory_partition", false);
+    bind(driver_reload, "amdsmi_gpu_driver_reload", false);
   }
   ~AmdSmi() {
     if (h) dlclose(h);
@@ -401,6 +414,169 @@ Result discover_amdsmi_impl(const std::string& lib) {
     }
   assign_physical(r);
   return r;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Partition control: the hardware tier of Gaia's GPU virtualization (paper p.3 §III.A; SURVEY.md B3,
+// B8: on MI355X a fraction of a GPU is an XCP of a CPX/DPX/QPX package, with NPS memory partitions).
+// Discovery reads the modes; these read what each package OFFERS and switch it.  Partition settings
+// belong to the package, so each call goes through the first processor (XCP) of every socket.
+const char* accel_name(amdsmi_accelerator_partition_type_t t) {
+  switch (t) {
+    case AMDSMI_ACCELERATOR_PARTITION_SPX: return "SPX";
+    case AMDSMI_ACCELERATOR_PARTITION_DPX: return "DPX";
+    case AMDSMI_ACCELERATOR_PARTITION_TPX: return "TPX";
+    case AMDSMI_ACCELERATOR_PARTITION_QPX: return "QPX";
+    case AMDSMI_ACCELERATOR_PARTITION_CPX: return "CPX";
+    default: return "";
+  }
+}
+
+bool compute_type(const std::string& m, amdsmi_compute_partition_type_t* t) {
+  static const std::map<std::string, amdsmi_compute_partition_type_t> k = {
+      {"SPX", AMDSMI_COMPUTE_PARTITION_SPX}, {"DPX", AMDSMI_COMPUTE_PARTITION_DPX}, {"TPX", AMDSMI_COMPUTE_PARTITION_TPX},
+      {"QPX", AMDSMI_COMPUTE_PARTITION_QPX}, {"CPX", AMDSMI_COMPUTE_PARTITION_CPX}};
+  auto it = k.find(m);
+  if (it == k.end()) return false;
+  *t = it->second;
+  return true;
+}
+
+bool memory_type(const std::string& m, amdsmi_memory_partition_type_t* t) {
+  static const std::map<std::string, amdsmi_memory_partition_type_t> k = {
+      {"NPS1", AMDSMI_MEMORY_PARTITION_NPS1}, {"NPS2", AMDSMI_MEMORY_PARTITION_NPS2},
+      {"NPS4", AMDSMI_MEMORY_PARTITION_NPS4}, {"NPS8", AMDSMI_MEMORY_PARTITION_NPS8}};
+  auto it = k.find(m);
+  if (it == k.end()) return false;
+  *t = it->second;
+  return true;
+}
+
+std::vector<std::string> nps_modes(amdsmi_nps_caps_t c) {
+  std::vector<std::string> out;
+  if (c.nps_flags.nps1_cap) out.push_back("NPS1");
+  if (c.nps_flags.nps2_cap) out.push_back("NPS2");
+  if (c.nps_flags.nps4_cap) out.push_back("NPS4");
+  if (c.nps_flags.nps8_cap) out.push_back("NPS8");
+  return out;
+}
+
+// one amdsmi session: the first GPU processor of every socket (= package), in socket order
+struct Session {
+  AmdSmi s;
+  std::vector<amdsmi_processor_handle> pkg;
+  std::vector<int> xcps;  // GPU processors per package
+  explicit Session(const std::string& lib) : s(lib) {
+    amdsmi_status_t st = s.init(AMDSMI_INIT_AMD_GPUS);
+    if (st != AMDSMI_STATUS_SUCCESS) throw std::runtime_error("amdsmi_init failed: status " + std::to_string((int)st));
+    uint32_t nsock = 0;
+    if (s.get_socket_handles(&nsock, nullptr) != AMDSMI_STATUS_SUCCESS) {
+      s.shut_down();
+      throw std::runtime_error("socket count");
+    }
+    std::vector<amdsmi_socket_handle> socks(nsock);
+    if (nsock) s.get_socket_handles(&nsock, socks.data());
+    for (uint32_t k = 0; k < nsock; ++k) {
+      uint32_t np = 0;
+      if (s.get_processor_handles(socks[k], &np, nullptr) != AMDSMI_STATUS_SUCCESS || np == 0) continue;
+      std::vector<amdsmi_processor_handle> ph(np);
+      if (s.get_processor_handles(socks[k], &np, ph.data()) != AMDSMI_STATUS_SUCCESS) continue;
+      amdsmi_processor_handle first = nullptr;
+      int n = 0;
+      for (auto p : ph) {
+        processor_type_t t;
+        if (s.get_processor_type(p, &t) == AMDSMI_STATUS_SUCCESS && t == AMDSMI_PROCESSOR_TYPE_AMD_GPU) {
+          if (!first) first = p;
+          ++n;
+        }
+      }
+      if (first) {
+        pkg.push_back(first);
+        xcps.push_back(n);
+      }
+    }
+  }
+  ~Session() { s.shut_down(); }
+  std::string bdf(amdsmi_processor_handle h) {
+    amdsmi_bdf_t b;
+    if (s.get_bdf(h, &b) != AMDSMI_STATUS_SUCCESS) return "";
+    return fmt_bdf(b.domain_number, b.bus_number, b.device_number, 0);  // the package: function 0
+  }
+};
+
+struct PartInfo {
+  std::string bdf, compute, memory;
+  int xcps = 0;
+  std::vector<std::string> compute_modes, memory_modes;
+};
+
+std::vector<PartInfo> partition_info_impl(const std::string& lib) {
+  std::lock_guard<std::mutex> guard(g_amdsmi_mu);
+  Session ss(lib);
+  AmdSmi& s = ss.s;
+  std::vector<PartInfo> out;
+  for (size_t k = 0; k < ss.pkg.size(); ++k) {
+    auto h = ss.pkg[k];
+    PartInfo p;
+    p.bdf = ss.bdf(h);
+    p.xcps = ss.xcps[k];
+    char buf[64] = {0};
+    if (s.get_cpart && s.get_cpart(h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) p.compute = buf;
+    buf[0] = 0;
+    if (s.get_mpart && s.get_mpart(h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) p.memory = buf;
+    if (s.get_profiles) {
+      // a few KiB per profile: on the heap, not the stack
+      auto cfg = std::make_unique<amdsmi_accelerator_partition_profile_config_t>();
+      std::memset(cfg.get(), 0, sizeof(*cfg));
+      if (s.get_profiles(h, cfg.get()) == AMDSMI_STATUS_SUCCESS)
+        for (uint32_t i = 0; i < cfg->num_profiles && i < AMDSMI_MAX_ACCELERATOR_PROFILE; ++i) {
+          const char* n = accel_name(cfg->profiles[i].profile_type);
+          if (*n && std::find(p.compute_modes.begin(), p.compute_modes.end(), n) == p.compute_modes.end())
+            p.compute_modes.push_back(n);
+        }
+    }
+    if (s.get_mpart_cfg) {
+      amdsmi_memory_partition_config_t mc;
+      std::memset(&mc, 0, sizeof(mc));
+      if (s.get_mpart_cfg(h, &mc) == AMDSMI_STATUS_SUCCESS) p.memory_modes = nps_modes(mc.partition_caps);
+    }
+    out.push_back(p);
+  }
+  return out;
+}
+
+// One step of a partition change on every package: ("compute"|"memory", mode) -> per package
+// (bdf, amdsmi status).  A fresh session per step: a compute-partition switch re-enumerates the
+// package's processors, so handles of an earlier session are not reused.
+std::vector<std::pair<std::string, int>> set_partition_step_impl(const std::string& lib, const std::string& what,
+                                                                 const std::string& mode) {
+  std::lock_guard<std::mutex> guard(g_amdsmi_mu);
+  Session ss(lib);
+  AmdSmi& s = ss.s;
+  std::vector<std::pair<std::string, int>> out;
+  if (what == "compute") {
+    amdsmi_compute_partition_type_t t;
+    if (!compute_type(mode, &t)) throw std::invalid_argument("unknown compute partition " + mode);
+    if (!s.set_cpart) throw std::runtime_error("amdsmi_set_gpu_compute_partition not available in " + lib);
+    for (auto h : ss.pkg) out.emplace_back(ss.bdf(h), (int)s.set_cpart(h, t));
+  } else if (what == "memory") {
+    amdsmi_memory_partition_type_t t;
+    if (!memory_type(mode, &t)) throw std::invalid_argument("unknown memory partition " + mode);
+    if (!s.set_mpart) throw std::runtime_error("amdsmi_set_gpu_memory_partition not available in " + lib);
+    for (auto h : ss.pkg) out.emplace_back(ss.bdf(h), (int)s.set_mpart(h, t));
+  } else {
+    throw std::invalid_argument("step must be 'compute' or 'memory'");
+  }
+  return out;
+}
+
+// amdgpu driver reload (a memory-partition change takes effect only after it; every GPU process of
+// the node must be gone).  -> amdsmi status
+int driver_reload_impl(const std::string& lib) {
+  std::lock_guard<std::mutex> guard(g_amdsmi_mu);
+  Session ss(lib);
+  if (!ss.s.driver_reload) throw std::runtime_error("amdsmi_gpu_driver_reload not available in " + lib);
+  return (int)ss.s.driver_reload();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -847,6 +1023,44 @@ PYBIND11_MODULE(_topo, m) {
       py::arg("root") = "/sys/class/kfd/kfd/topology", py::arg("drm_root") = "/sys/class/drm",
       py::arg("pci_root") = "/sys/bus/pci/devices", py::arg("node_root") = "/sys/devices/system/node",
       py::arg("ib_root") = "/sys/class/infiniband");
+  m.def(
+      "partition_info",
+      [](const std::string& lib) {
+        std::vector<PartInfo> v;
+        {
+          py::gil_scoped_release nogil;
+          v = partition_info_impl(lib);
+        }
+        py::list out;
+        for (const auto& p : v) {
+          py::dict d;
+          d["bdf"] = p.bdf;
+          d["compute"] = p.compute;
+          d["memory"] = p.memory;
+          d["xcps"] = p.xcps;
+          d["compute_modes"] = p.compute_modes;
+          d["memory_modes"] = p.memory_modes;
+          out.append(d);
+        }
+        return out;
+      },
+      py::arg("lib") = "libamd_smi.so",
+      "per package (socket order): current compute / memory partition, XCPs, and the modes it offers (read-only)");
+  m.def(
+      "set_partition_step",
+      [](const std::string& lib, const std::string& what, const std::string& mode) {
+        py::gil_scoped_release nogil;
+        return set_partition_step_impl(lib, what, mode);
+      },
+      py::arg("lib"), py::arg("what"), py::arg("mode"),
+      "switch every package's compute or memory partition; -> [(package bdf, amdsmi status)]");
+  m.def(
+      "driver_reload",
+      [](const std::string& lib) {
+        py::gil_scoped_release nogil;
+        return driver_reload_impl(lib);
+      },
+      py::arg("lib"), "reload the amdgpu driver (completes a memory-partition change); -> amdsmi status");
   py::class_<EventWatcher>(m, "EventWatcher")
       .def(py::init<const std::string&, const std::vector<std::string>&>(), py::arg("lib") = "libamd_smi.so",
            py::arg("kinds") = std::vector<std::string>{"GPU_PRE_RESET", "GPU_POST_RESET", "VMFAULT", "THERMAL_THROTTLE"})

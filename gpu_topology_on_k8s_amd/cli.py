@@ -43,6 +43,30 @@ def _ints(s: Optional[str]) -> List[int]:
     return [int(x) for x in s.split(",") if x.strip()] if s else []
 
 
+def cmd_partition(a) -> int:
+    """``gtk partition show`` (read-only) / ``gtk partition set --compute CPX [--memory NPS4] --yes``."""
+    from .topology.partition import PartitionError, apply_partition, partition_info
+
+    if a.action == "show":
+        for p in partition_info():
+            print(json.dumps(p))
+        return 0
+    if not (a.compute or a.memory):
+        print("partition set: give --compute and/or --memory", file=sys.stderr)
+        return 2
+    if not a.yes:
+        print("partition set re-partitions every GPU of this node (device IDs change, running GPU processes break): "
+              "stop them and pass --yes", file=sys.stderr)
+        return 2
+    try:
+        r = apply_partition(a.compute, a.memory, reload_driver=a.reload_driver)
+    except PartitionError as e:
+        print(f"partition set: {e}", file=sys.stderr)
+        return 1
+    print(json.dumps({k: r[k] for k in ("ok", "reason", "steps", "reload_required", "reloaded")}))
+    return 0 if r["ok"] else 1
+
+
 def cmd_topo(a) -> int:
     from .k8s.annotations import Contract, encode_node_annotations
 
@@ -222,7 +246,8 @@ def cmd_config(a) -> int:
         print(yaml.safe_dump(scheduler_configuration(a.resource_name, with_filter=a.filter, tls_dir=a.tls_dir or None),
                              sort_keys=False), end="")
     else:
-        print(render_manifests(a.resource_name, image=a.image, time_slices=a.time_slices), end="")
+        print(render_manifests(a.resource_name, image=a.image, time_slices=a.time_slices,
+                               partition_control=a.partition_control), end="")
     return 0
 
 
@@ -358,6 +383,8 @@ def main(argv=None) -> int:
     p.add_argument("--filter", action="store_true")
     p.add_argument("--image", default="rocm/gpu-topology-k8s:latest")
     p.add_argument("--time-slices", type=int, default=1, help="manifests: device plugin --time-slices (fractional GPUs on SPX nodes)")
+    p.add_argument("--partition-control", action="store_true",
+                   help="manifests: device plugin --partition-control on (switches partition modes on node labels; /sys writable)")
     p.add_argument("--tls-dir", default="", help="scheduler: call the extender over mutual TLS with tls.crt/tls.key/ca.crt from here")
     p.set_defaults(fn=cmd_config)
     p = sub.add_parser("validate")
@@ -382,6 +409,13 @@ def main(argv=None) -> int:
     p.add_argument("--dev-root", default="/dev")
     p.add_argument("--plugin-dir", default="/var/lib/kubelet/device-plugins")
     p.set_defaults(fn=lambda a: __import__("gpu_topology_on_k8s_amd.doctor", fromlist=["main"]).main(a))
+    p = sub.add_parser("partition", help="GPU compute / memory partition modes: show, or set (root; the node must be idle)")
+    p.add_argument("action", choices=["show", "set"])
+    p.add_argument("--compute", default=None, help="set: SPX | DPX | QPX | CPX")
+    p.add_argument("--memory", default=None, help="set: NPS1 | NPS2 | NPS4 | NPS8")
+    p.add_argument("--reload-driver", action="store_true", help="set: reload amdgpu to complete a memory-partition change")
+    p.add_argument("--yes", action="store_true", help="set: really change the hardware (every GPU process must be stopped)")
+    p.set_defaults(fn=cmd_partition)
     p = sub.add_parser("sim")
     p.add_argument("--nodes", type=int, default=2)
     p.add_argument("--pods", default="4,4,2,1,1,8")

@@ -86,9 +86,11 @@ def scheduler_configuration(resource: str = DEFAULT_RESOURCE, url: Optional[str]
 
 
 def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, namespace: str = NAMESPACE,
-                     probe: str = "quick", policy: str = "exact", time_slices: int = 1) -> str:
+                     probe: str = "quick", policy: str = "exact", time_slices: int = 1, partition_control: bool = False) -> str:
     """The DaemonSets, RBAC and scheduler config.  ``time_slices > 1``: the device plugin advertises
-    every GPU as that many time slices (fractional pods; topology/shares.py)."""
+    every GPU as that many time slices (fractional pods; topology/shares.py).  ``partition_control``:
+    the plugin switches compute / memory partition modes on the node labels' request
+    (deviceplugin/repartition.py), which writes the GPUs' sysfs, so /sys is mounted writable."""
     sa = "gpu-topology"
     labels = {"app.kubernetes.io/part-of": "gpu-topology-amd"}
     docs: List[Dict[str, Any]] = [
@@ -130,7 +132,8 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
                             "command": ["python3", "-m", "gpu_topology_on_k8s_amd.deviceplugin",
                                         f"--resource-name={resource}", f"--probe={probe}", "--discovery=auto",
                                         "--reprobe-interval=3600", "--prestart-validate", f"--metrics-port={PLUGIN_METRICS_PORT}"]
-                                       + ([f"--time-slices={int(time_slices)}"] if int(time_slices) > 1 else []),
+                                       + ([f"--time-slices={int(time_slices)}"] if int(time_slices) > 1 else [])
+                                       + (["--partition-control=on"] if partition_control else []),
                             "ports": [{"containerPort": PLUGIN_METRICS_PORT, "name": "metrics"}],
                             "env": [{"name": "NODE_NAME", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}},
                                     # the probe / validator children share GPU buffers across processes;
@@ -142,7 +145,7 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
                                 {"name": "device-plugins", "mountPath": "/var/lib/kubelet/device-plugins"},
                                 # kubelet pod-resources API: which pod holds which device (GROUP reconcile)
                                 {"name": "pod-resources", "mountPath": "/var/lib/kubelet/pod-resources", "readOnly": True},
-                                {"name": "sys", "mountPath": "/sys", "readOnly": True},
+                                {"name": "sys", "mountPath": "/sys", "readOnly": not partition_control},
                                 {"name": "dev", "mountPath": "/dev"},
                                 # time-sliced shares: the vGPU guard library + per-allocation configs the
                                 # plugin writes here are bind-mounted into pods by Allocate (host path = this path)

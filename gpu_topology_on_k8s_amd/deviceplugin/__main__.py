@@ -15,6 +15,7 @@ import os
 import signal
 import sys
 import threading
+import time
 from typing import Tuple
 
 from ..k8s.annotations import Contract
@@ -150,6 +151,14 @@ def main(argv=None) -> int:
                     help="host directory (hostPath, same path inside the DaemonSet) for the guard library and per-allocation configs")
     ap.add_argument("--share-cu-mask", default="on", choices=["on", "off"],
                     help="--time-slices: confine a pod holding part of a GPU to its slices' compute units (HSA_CU_MASK)")
+    ap.add_argument("--partition-control", default="off", choices=["off", "on"],
+                    help="switch the GPUs' compute / memory partition mode to what the node labels "
+                         "<annotation-prefix>/compute-partition-request (SPX|DPX|QPX|CPX) and "
+                         "memory-partition-request (NPS1|NPS4...) ask for, once no pod holds a device "
+                         "(needs a privileged DaemonSet; deviceplugin/repartition.py)")
+    ap.add_argument("--partition-driver-reload", action="store_true",
+                    help="--partition-control: reload the amdgpu driver to complete a memory-partition change "
+                         "(otherwise the new NPS mode waits for a reload by the operator)")
     ap.add_argument("--log-level", default="INFO")
     a = ap.parse_args(argv)
     logging.basicConfig(level=a.log_level, format='{"ts":"%(asctime)s","lvl":"%(levelname)s","mod":"%(name)s","msg":"%(message)s"}')
@@ -157,6 +166,23 @@ def main(argv=None) -> int:
 
     api = make_api(a.apiserver, a.token, a.ca_file, a.insecure_skip_tls_verify)
     contract = Contract(resource_name=a.resource_name, prefix=a.annotation_prefix, slice_resource=a.slice_resource_name)
+    names = (a.resource_name, a.slice_resource_name, "aliyun.com/gpu", "aliyun.com/gpu-count")
+    partition_control = a.partition_control == "on" and a.discovery in ("auto", "amdsmi") and api is not None
+
+    def repartition_pass(idle_fn, wait):
+        from .repartition import repartition
+
+        outcome, msg = repartition(api, a.node_name, contract, idle_fn, reload_driver=a.partition_driver_reload,
+                                   settle_s=a.probe_settle_seconds, wait=wait)
+        if outcome in ("ok", "failed", "invalid"):
+            (log.warning if outcome != "ok" else log.info)("partition request: %s: %s", outcome, msg)
+        return outcome, msg
+
+    if partition_control:  # before discovery: the first registration already shows the new layout
+        try:
+            repartition_pass(lambda: node_is_idle(api, a.node_name, names), lambda s: (time.sleep(s), False)[1])
+        except Exception as e:  # noqa: BLE001 - the node keeps its layout; the loop tries again
+            log.warning("partition request at start-up failed: %s", e)
     a.time_slices, why = startup_time_slices(api, a.node_name, contract, a.time_slices,
                                              (a.resource_name, a.slice_resource_name, "aliyun.com/gpu", "aliyun.com/gpu-count"))
     if why:
@@ -179,7 +205,6 @@ def main(argv=None) -> int:
             probed, msg = probe_in_child(a.probe, backend=a.discovery)
             log.info("probe: %s", msg)
             return None if probed is None else time_slice(probed, a.time_slices)
-    names = (a.resource_name, a.slice_resource_name, "aliyun.com/gpu", "aliyun.com/gpu-count")
     topo, how = startup_topology(topo, api, a.node_name, contract, names, probe_fn)
     log.info("link matrix: %s; topology:\n%s", how, topo.render())
 
@@ -233,6 +258,17 @@ def main(argv=None) -> int:
                 elif ticks % 300 == 0:
                     log.warning("time slices per GPU %d -> %d requested by the node label; waiting until no pod holds a device",
                                 a.time_slices, want)
+        if partition_control and ticks % max(1, int(a.label_check_interval)) == 0 and not plugin.layout_change.is_set():
+            try:
+                outcome, msg = repartition_pass(plugin.node_idle, done.wait)
+            except Exception as e:  # noqa: BLE001 - reported; the next pass tries again
+                outcome, msg = "error", str(e)
+                log.warning("partition request: %s", e)
+            if outcome == "ok":
+                plugin.layout_change_reason = f"GPU partitions {msg} (node label)"
+                plugin.layout_change.set()
+            elif outcome == "busy" and ticks % 300 == 0:
+                log.warning("partition request: %s", msg)
         if plugin.layout_change.is_set():  # partition switch / device hot-(un)plug / new slicing: restart cleanly
             log.warning("exiting for a restart: %s", plugin.layout_change_reason)
             plugin.stop()

@@ -1,0 +1,99 @@
+"""Operator-requested hardware repartitioning of a node (``--partition-control on``).
+
+The operator labels a node ``<prefix>/compute-partition-request=CPX`` (and optionally
+``<prefix>/memory-partition-request=NPS4``).  The device plugin owns the node's GPUs, so it makes
+the switch itself.  Device IDs, and with them every pod's GROUP annotation, change with the partition
+mode, so the switch follows the rules of a time-slice relabel (``__main__.py``) and of an idle-time
+re-probe (``plugin.reprobe``):
+
+1. it happens only while no pod holds a device of the node;
+2. the node is marked ``<prefix>/probing: <deadline>`` first, so the extender's filter, sort, bind
+   and preempt skip it.  After a settle window, for binds already past the extender, the node must
+   still be idle;
+3. the switch itself is :func:`topology.partition.apply_partition` (amdsmi, needs root);
+4. the mark is cleared, and a Kubernetes Event records the outcome.  A refused switch (no
+   permission, a mode the package does not offer) is recorded as ``<prefix>/partition-change-failed``
+   on the node and is not tried again until the label asks for something else.
+
+On success the plugin exits 75, like any layout change, and its restart discovers the new layout.
+At start-up the switch runs before discovery, so the first registration already shows the new
+layout.
+"""
+from __future__ import annotations
+
+import logging
+import math
+import time
+from typing import Callable, Optional, Tuple
+
+from ..k8s.annotations import Contract
+from ..k8s.events import record_event
+from ..topology.partition import PartitionError, apply_partition, normalise, partition_info
+
+log = logging.getLogger("gtk.deviceplugin.partition")
+
+__all__ = ["partition_request", "repartition"]
+
+
+def partition_request(api, node_name: str, contract: Contract) -> Tuple[Optional[str], Optional[str], dict]:
+    """(compute, memory, node) the node's labels ask for; (None, None, node) without a request."""
+    node = api.get_node(node_name)
+    labels = (node.get("metadata") or {}).get("labels") or {}
+    return (labels.get(contract.partition_request_label) or None, labels.get(contract.memory_partition_request_label) or None,
+            node)
+
+
+def _event(api, node_name: str, reason: str, msg: str, type_: str) -> None:
+    record_event(api, {"kind": "Node", "metadata": {"name": node_name}}, reason, msg, type_,
+                 component="gpu-topology-device-plugin", host=node_name)
+
+
+def repartition(api, node_name: str, contract: Contract, idle_fn: Callable[[], bool], lib: Optional[str] = None,
+                reload_driver: bool = False, settle_s: float = 2.0, mark_s: float = 600.0,
+                wait: Callable[[float], bool] = lambda s: (time.sleep(s), False)[1],
+                clock: Callable[[], float] = time.time) -> Tuple[str, str]:
+    """One reconciliation pass.  -> (outcome, message), outcome one of
+    ``none`` (no request), ``same`` (already there), ``invalid``, ``skipped`` (this request failed
+    before), ``busy`` (pods hold devices), ``stopped`` (``wait`` returned True), ``ok``, ``failed``."""
+    if api is None or not node_name:
+        return "none", "no apiserver"
+    want_c, want_m, node = partition_request(api, node_name, contract)
+    if want_c is None and want_m is None:
+        return "none", ""
+    try:
+        want_c, want_m = normalise(want_c, want_m)
+    except PartitionError as e:
+        return "invalid", str(e)
+    tag = f"{want_c or '-'}/{want_m or '-'}"
+    info = partition_info(lib)
+    if all((not want_c or p["compute"] == want_c) and (not want_m or p["memory"] == want_m) for p in info):
+        ann = (node.get("metadata") or {}).get("annotations") or {}
+        if contract.partition_failed_key in ann:
+            api.patch_node(node_name, annotations={contract.partition_failed_key: None})
+        return "same", f"already {tag}"
+    failed = ((node.get("metadata") or {}).get("annotations") or {}).get(contract.partition_failed_key, "")
+    if failed.startswith(tag + ":"):
+        return "skipped", f"{tag} failed before ({failed[len(tag) + 1:].strip()}); change the label to try again"
+    if not idle_fn():
+        return "busy", f"{tag} requested; waiting until no pod holds a device"
+    api.patch_node(node_name, annotations={contract.probing_key: str(int(math.ceil(clock() + mark_s)))})
+    try:
+        if settle_s > 0 and wait(settle_s):
+            return "stopped", ""
+        if not idle_fn():
+            return "busy", f"{tag} requested; a pod arrived while the node was being marked"
+        before = f"{info[0]['compute']}/{info[0]['memory']}" if info else "?"
+        log.warning("switching GPU partitions %s -> %s (node idle)", before, tag)
+        try:
+            res = apply_partition(want_c, want_m, lib=lib, reload_driver=reload_driver)
+        except PartitionError as e:
+            res = {"ok": False, "reason": str(e)}
+        if res["ok"]:
+            api.patch_node(node_name, annotations={contract.partition_failed_key: None})
+            _event(api, node_name, "GPUPartitionChanged", f"GPU partitions {before} -> {tag}", "Normal")
+            return "ok", f"{before} -> {tag}"
+        api.patch_node(node_name, annotations={contract.partition_failed_key: f"{tag}: {res['reason']}"[:1000]})
+        _event(api, node_name, "FailedGPUPartitionChange", f"{before} -> {tag}: {res['reason']}", "Warning")
+        return "failed", res["reason"]
+    finally:
+        api.patch_node(node_name, annotations={contract.probing_key: None})

@@ -9,7 +9,9 @@ DaemonSet's init step, an operator, or a pod's entry point can act on it.  Node 
 * ``native``                    the in-tree extensions and the vGPU guard are built;
 * ``ipc-mode``                  ``HSA_ENABLE_IPC_MODE_LEGACY=0`` for cross-process GPU memory (RCCL P2P/IPC);
 * ``cpu-affinity``              every GPU's local cores intersect this process's allowed CPUs (Gaia B6);
-* ``device-plugin-dir``         the kubelet's device-plugin socket directory is writable.
+* ``device-plugin-dir``         the kubelet's device-plugin socket directory is writable;
+* ``partition``                 each package's compute / memory partition mode and the modes it offers
+                                (amdsmi, read-only; what ``--partition-control`` may switch to).
 
 Pod checks (when ``GTK_GPU_GROUP`` is set, i.e. inside a container Allocate configured):
 
@@ -95,6 +97,26 @@ def check_cpu_affinity(topo, allowed=None) -> Check:
     return _c("cpu-affinity", "ok", f"every device's local cores intersect the allowed CPUs ({len(allowed)})")
 
 
+def check_partition(backend: str) -> Check:
+    if backend not in ("auto", "amdsmi"):
+        return _c("partition", "skip", f"--discovery {backend}: partition modes are read through amdsmi")
+    from .topology.partition import partition_info
+
+    try:
+        info = partition_info()
+    except Exception as e:  # noqa: BLE001 - no amdsmi here: not a failure of the node
+        return _c("partition", "skip", f"amdsmi unavailable: {str(e)[:200]}")
+    if not info:
+        return _c("partition", "warn", "amdsmi lists no GPU packages")
+    modes = sorted({f"{p['compute']}/{p['memory']}" for p in info})
+    offers = sorted({m for p in info for m in p["compute_modes"]}, key=lambda m: "SDTQC".index(m[0]) if m[0] in "SDTQC" else 9)
+    nps = sorted({m for p in info for m in p["memory_modes"]})
+    return _c("partition", "ok" if len(modes) == 1 else "warn",
+              f"{len(info)} package(s) in {', '.join(modes)}" + ("" if len(modes) == 1 else " (mixed modes)")
+              + f"; offered: {','.join(offers) or '?'} / {','.join(nps) or '?'}",
+              packages=info)
+
+
 def check_plugin_dir(path: str) -> Check:
     if not os.path.isdir(path):
         return _c("device-plugin-dir", "skip", f"{path} absent (not a kubelet node, or not mounted)")
@@ -164,6 +186,7 @@ def run_checks(backend: str = "auto", fake_n: Optional[int] = None, gpu: bool = 
     checks += found
     if topo is not None:
         checks.append(check_cpu_affinity(topo, allowed))
+        checks.append(check_partition(backend))
     checks += check_native()
     checks.append(check_ipc(env))
     checks.append(check_plugin_dir(plugin_dir))

@@ -126,6 +126,25 @@ class Contract:
         return f"{self.prefix}/compute-partition"
 
     @property
+    def partition_request_label(self) -> str:
+        """Node label set by the operator: the compute partition mode (SPX/DPX/QPX/CPX) the device
+        plugin should put the node's GPUs in, once no pod holds a device (``--partition-control``).
+        ``label_partition`` is what the plugin publishes; this is what the operator asks for."""
+        return f"{self.prefix}/compute-partition-request"
+
+    @property
+    def memory_partition_request_label(self) -> str:
+        """Node label set by the operator: the memory partition mode (NPS1/NPS2/NPS4/NPS8) to apply
+        with the compute partition request."""
+        return f"{self.prefix}/memory-partition-request"
+
+    @property
+    def partition_failed_key(self) -> str:
+        """Node annotation written by the device plugin when a requested partition change failed:
+        ``<compute>/<memory>: <reason>``; the plugin does not retry that request until the label changes."""
+        return f"{self.prefix}/partition-change-failed"
+
+    @property
     def label_gfx(self) -> str:
         return f"{self.prefix}/gfx"
 

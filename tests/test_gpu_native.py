@@ -133,6 +133,21 @@ def test_health_monitor_on_real_node():
                      g.xgmi_links_total) for g in t.gpus})
 
 
+def test_partition_modes_read_on_real_node():
+    """Read-only (no setter runs on a shared box, and it needs root): amdsmi's per-package partition
+    report agrees with discovery, and an SPX package is one device."""
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
+    from gpu_topology_on_k8s_amd.topology.partition import COMPUTE_XCPS, partition_info
+
+    t = discover("amdsmi")
+    info = partition_info()
+    print(json.dumps(info))
+    assert len(info) == len(set(t.physical.tolist()))
+    assert info[0]["compute"] == t.gpus[0].partition and info[0]["memory"] == t.gpus[0].memory_partition
+    assert info[0]["xcps"] == COMPUTE_XCPS.get(info[0]["compute"], info[0]["xcps"])
+    assert not info[0]["compute_modes"] or info[0]["compute"] in info[0]["compute_modes"]
+
+
 def test_sysfs_backend_on_real_node():
     from gpu_topology_on_k8s_amd.topology.discovery import discover
 
