@@ -203,6 +203,19 @@ def cmd_status(a) -> int:
                 row["gpu_share_used"] = {str(p): round(sum(1 for g in t.gpus if g.physical == p and g.index in used) /
                                                        sum(1 for g in t.gpus if g.physical == p), 3)
                                          for p in sorted(set(t.physical.tolist()))}
+        row["partition"] = f"{t.gpus[0].partition}/{t.gpus[0].memory_partition}" if t.gpus else ""
+        row["probing"] = bool(getattr(st, "probing_until", 0.0) > now)  # re-probe / repartition: the extender skips it
+        try:  # the operator's partition request and a refusal the plugin recorded
+            md = api.get_node(st.name).get("metadata") or {}
+            c = ext.cfg.contract
+            req = [(md.get("labels") or {}).get(k) for k in (c.partition_request_label, c.memory_partition_request_label)]
+            if any(req):
+                row["partition_request"] = "/".join(x or "-" for x in req)
+            failed = (md.get("annotations") or {}).get(c.partition_failed_key)
+            if failed:
+                row["partition_change_failed"] = failed
+        except Exception:  # noqa: BLE001 - the node vanished meanwhile: the row stands without it
+            pass
         # a sliced node is scored for slice requests (its own pool), every other node for whole devices
         res = ext.cfg.contract.slice_resource if int(max((g.shares for g in t.gpus), default=1)) > 1 else ext.cfg.contract.resource_name
         row["resource"] = res

@@ -110,6 +110,8 @@ def test_gtk_status_reports_usage_and_scores():
     api = FakeAPIServer()
     for n in ("n0", "n1"):
         api.create_node(make_node(n, annotations=encode_node_annotations(fx.f7_mi355x(), C), capacity={C.resource_name: "8"}))
+    api.patch_node("n1", labels={C.partition_request_label: "CPX"},
+                   annotations={C.partition_failed_key: "CPX/-: compute partition CPX: 0000:05:00.0: permission denied"})
     api.create_pod(make_pod("a", gpus=2, node="n0", annotations=PodAssignment([0, 4], True, 1).to_annotations()))
     srv, url = serve_http(api)
     try:
@@ -125,6 +127,8 @@ def test_gtk_status_reports_usage_and_scores():
     assert rows["n0"]["best_score"]["8"] is None and rows["n1"]["best_score"]["8"] is not None
     assert q.returncode == 0 and q.stdout.splitlines()[0].startswith("NODE") and "n1" in q.stdout
     assert "gpu_share_used" not in rows["n0"]
+    assert rows["n0"]["partition"] == "SPX/NPS1" and not rows["n0"]["probing"] and "partition_request" not in rows["n0"]
+    assert rows["n1"]["partition_request"] == "CPX/-" and "permission" in rows["n1"]["partition_change_failed"]
 
 
 def test_gtk_status_shares_on_a_sliced_node():
