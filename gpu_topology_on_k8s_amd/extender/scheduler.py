@@ -59,7 +59,12 @@ from .metrics import ExtenderMetrics
 
 log = logging.getLogger(__name__)
 
-__all__ = ["ExtenderConfig", "TopologyExtender", "Decision", "normalized_scores"]
+__all__ = ["ExtenderConfig", "TopologyExtender", "Decision", "MalformedPod", "normalized_scores"]
+
+
+class MalformedPod(ValueError):
+    """The pod's GPU request cannot be read (a quantity that is not a non-negative integer, a
+    container that is not an object): the verbs answer without scoring or binding it."""
 
 MAX_EXTENDER_PRIORITY = 10  # k8s.io/kube-scheduler/extender/v1 MaxExtenderPriority
 
@@ -136,7 +141,12 @@ class TopologyExtender:
         return self.cache.resources
 
     def request_of(self, pod: Dict[str, Any]) -> int:
-        return pod_gpu_request(pod, self.resources)
+        """Devices the pod asks for; a quantity that is not a non-negative integer raises
+        :class:`MalformedPod` (the verbs answer it without scoring or binding the pod)."""
+        try:
+            return pod_gpu_request(pod, self.resources)
+        except ValueError as e:
+            raise MalformedPod(f"malformed GPU request: {e}") from None
 
     def fraction_of(self, pod: Dict[str, Any]) -> Optional[float]:
         """``<prefix>/gpu-fraction`` (0 < m < 1) or None; malformed values raise ValueError."""
@@ -160,7 +170,10 @@ class TopologyExtender:
             if txt.endswith(u):
                 txt, mult = txt[: -len(u)], units[u]
                 break
-        b = int(float(txt) * mult)
+        v = float(txt) * mult
+        if not (v == v and v != float("inf")):  # nan / inf: no HBM share can be sized from it
+            raise ValueError(f"{self.cfg.contract.memory_key} must be a finite size, got {raw!r}")
+        b = int(v)
         if b <= 0:
             raise ValueError(f"{self.cfg.contract.memory_key} must be positive, got {raw!r}")
         return b
@@ -259,9 +272,9 @@ class TopologyExtender:
         try:
             fraction = self.fraction_of(pod)
             mem = self.memory_of(pod)
+            unit, why = self.request_unit(pod)
         except ValueError as e:
             return None, str(e)
-        unit, why = self.request_unit(pod)
         if unit is None:
             return None, why
         if mem is not None and fraction is None:
@@ -275,10 +288,13 @@ class TopologyExtender:
         resource (any resource name containing ``rdma``)."""
         if str(obj_annotations(pod).get(self.cfg.contract.multi_node_key, "")).strip().lower() in ("1", "true", "yes"):
             return True
-        for c in ((pod.get("spec") or {}).get("containers") or []):
-            res = c.get("resources") or {}
+        spec = pod.get("spec")
+        cs = spec.get("containers") if isinstance(spec, dict) else None
+        for c in cs if isinstance(cs, list) else []:
+            res = c.get("resources") if isinstance(c, dict) else None
             for part in ("limits", "requests"):
-                if any("rdma" in str(name).lower() for name in (res.get(part) or {})):
+                vals = res.get(part) if isinstance(res, dict) else None
+                if isinstance(vals, dict) and any("rdma" in str(name).lower() for name in vals):
                     return True
         return False
 
@@ -385,7 +401,10 @@ class TopologyExtender:
     def filter(self, pod: Dict[str, Any], node_names: Sequence[str], node_objs: Optional[Dict[str, dict]] = None):
         """-> (passing node names, {failed node: reason})."""
         t0 = time.perf_counter()
-        k = self.request_of(pod)
+        try:
+            k = self.request_of(pod)
+        except MalformedPod as e:
+            return [], {n: str(e) for n in node_names}
         ok: List[str] = []
         failed: Dict[str, str] = {}
         shape, bad = self._pod_shape(pod, k) if k else (None, "")
@@ -408,7 +427,10 @@ class TopologyExtender:
         """-> [(host, score 0..10)]: infeasible nodes 0 (the reference has no filter verb), feasible
         nodes :func:`normalized_scores` of their best placement's objective."""
         t0 = time.perf_counter()
-        k = self.request_of(pod)
+        try:
+            k = self.request_of(pod)
+        except MalformedPod:
+            return [(n, 0) for n in node_names]
         objs: Dict[str, float] = {}
         shape, _ = self._pod_shape(pod, k) if k else (None, "")
         for n in node_names:
@@ -509,7 +531,10 @@ class TopologyExtender:
         import itertools
 
         t0 = time.perf_counter()
-        k = self.request_of(pod)
+        try:
+            k = self.request_of(pod)
+        except MalformedPod:
+            return dict(victims)  # not ours to judge: kube-scheduler's own victims stand
         out: Dict[str, Tuple[List[str], int]] = {}
         shape, _ = self._pod_shape(pod, k) if k else (None, "")
         for node, (uids, pdb) in victims.items():

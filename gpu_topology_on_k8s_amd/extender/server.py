@@ -37,7 +37,9 @@ DEFAULT_PREFIX = "/gputopology-scheduler"
 EXTENDER_KEY = web.AppKey("extender", TopologyExtender)
 
 
-def _get(d: Dict[str, Any], key: str, default=None):
+def _get(d: Any, key: str, default=None):
+    if not isinstance(d, dict):
+        return default
     if key in d:
         return d[key]
     lk = key.lower()
@@ -47,14 +49,23 @@ def _get(d: Dict[str, Any], key: str, default=None):
     return default
 
 
+def _obj(x: Any) -> Dict[str, Any]:
+    """A JSON object from the request, or {} for anything else (null, a list, a scalar)."""
+    return x if isinstance(x, dict) else {}
+
+
 def _candidates(args: Dict[str, Any]) -> Tuple[List[str], Optional[Dict[str, dict]], bool]:
-    """(node names, {name: node object} when full nodes were sent, whether NodeNames mode)."""
+    """(node names, {name: node object} when full nodes were sent, whether NodeNames mode).  Entries
+    that are not node names / node objects are dropped: the pod is scored on the rest."""
     names = _get(args, "NodeNames")
     if names is not None:
-        return list(names), None, True
-    nodes = _get(args, "Nodes") or {}
-    items = _get(nodes, "items") or []
-    objs = {((n.get("metadata") or {}).get("name", "")): n for n in items}
+        return [n for n in (names if isinstance(names, list) else []) if isinstance(n, str) and n], None, True
+    items = _get(_obj(_get(args, "Nodes")), "items")
+    objs: Dict[str, dict] = {}
+    for n in items if isinstance(items, list) else []:
+        name = _get(_obj(_get(n, "metadata")), "name")
+        if isinstance(name, str) and name:
+            objs[name] = n
     return list(objs), objs, False
 
 
@@ -67,13 +78,16 @@ def make_app(ext: TopologyExtender, prefix: str = DEFAULT_PREFIX, workers: int =
 
     async def body(request: web.Request) -> Dict[str, Any]:
         try:
-            return await request.json(loads=json.loads)
+            args = await request.json(loads=json.loads)
         except Exception as e:
             raise web.HTTPBadRequest(text=f"invalid JSON: {e}")
+        if not isinstance(args, dict):
+            raise web.HTTPBadRequest(text="the extender arguments must be a JSON object")
+        return args
 
     async def prioritize(request: web.Request) -> web.Response:
         args = await body(request)
-        pod = _get(args, "Pod") or {}
+        pod = _obj(_get(args, "Pod"))
         names, objs, _ = _candidates(args)
         try:
             res = await run_blocking(ext.prioritize, pod, names, objs)
@@ -87,7 +101,7 @@ def make_app(ext: TopologyExtender, prefix: str = DEFAULT_PREFIX, workers: int =
 
     async def filter_(request: web.Request) -> web.Response:
         args = await body(request)
-        pod = _get(args, "Pod") or {}
+        pod = _obj(_get(args, "Pod"))
         names, objs, names_mode = _candidates(args)
         try:
             ok, failed = await run_blocking(ext.filter, pod, names, objs)
@@ -109,6 +123,12 @@ def make_app(ext: TopologyExtender, prefix: str = DEFAULT_PREFIX, workers: int =
     async def bind(request: web.Request) -> web.Response:
         args = await body(request)
         try:
+            for key in ("PodName", "Node"):
+                if not isinstance(_get(args, key), str) or not _get(args, key):
+                    raise ValueError(f"ExtenderBindingArgs.{key} must be a non-empty string")
+            for key in ("PodNamespace", "PodUID"):
+                if not isinstance(_get(args, key, ""), str):
+                    raise ValueError(f"ExtenderBindingArgs.{key} must be a string")
             d = await run_blocking(ext.bind, _get(args, "PodNamespace", "default"), _get(args, "PodName"), _get(args, "PodUID", ""),
                                    _get(args, "Node"))
             ext.metrics.request("bind", "ok")
@@ -123,14 +143,18 @@ def make_app(ext: TopologyExtender, prefix: str = DEFAULT_PREFIX, workers: int =
 
     async def preempt(request: web.Request) -> web.Response:
         args = await body(request)
-        pod = _get(args, "Pod") or {}
+        pod = _obj(_get(args, "Pod"))
         victims: Dict[str, Tuple[List[str], int]] = {}
-        meta_v = _get(args, "NodeNameToMetaVictims") or {}
-        full_v = _get(args, "NodeNameToVictims") or {}
+        meta_v = _obj(_get(args, "NodeNameToMetaVictims"))
+        full_v = _obj(_get(args, "NodeNameToVictims"))
         for node, v in list(full_v.items()) + list(meta_v.items()):
-            pods = _get(v or {}, "Pods") or []
-            uids = [str(_get(p, "UID") or ((_get(p, "metadata") or {}).get("uid", ""))) for p in pods]
-            victims[node] = ([u for u in uids if u], int(_get(v or {}, "NumPDBViolations", 0) or 0))
+            pods = _get(v, "Pods")
+            uids = [str(_get(p, "UID") or _get(_obj(_get(p, "metadata")), "uid", "")) for p in (pods if isinstance(pods, list) else [])]
+            try:
+                pdb = int(_get(v, "NumPDBViolations", 0) or 0)
+            except (TypeError, ValueError):
+                pdb = 0
+            victims[node] = ([u for u in uids if u and u != "None"], pdb)
         try:
             res = await run_blocking(ext.preempt, pod, victims)
             ext.metrics.request("preempt", "ok")

@@ -44,11 +44,12 @@ def pod_is_terminal(p: Obj) -> bool:
 def parse_quantity(q: Any) -> int:
     """Integer extended-resource quantity ("4", 4, "4.0"); fractions are not allowed by k8s for
     extended resources, so anything else is rejected."""
-    if isinstance(q, (int, float)):
-        v = float(q)
-    else:
-        v = float(str(q).strip())
-    if v != int(v) or v < 0:
+    try:
+        v = float(q) if isinstance(q, (int, float)) and not isinstance(q, bool) else float(str(q).strip())
+        ok = v == v and abs(v) != float("inf") and v == int(v) and v >= 0
+    except (TypeError, ValueError, OverflowError):
+        ok = False
+    if not ok:
         raise ValueError(f"extended resources must be non-negative integers, got {q!r}")
     return int(v)
 
@@ -57,19 +58,24 @@ def pod_gpu_request(p: Obj, resource_names: Iterable[str]) -> int:
     """Devices requested by a pod: sum over containers of limits (or requests) of the resource;
     init containers run sequentially, so the pod needs max(sum(containers), max(init))."""
     names = list(resource_names)
-    spec = p.get("spec") or {}
+    spec = p.get("spec") if isinstance(p, dict) else None
+    spec = spec if isinstance(spec, dict) else {}
 
     def one(c: Obj) -> int:
-        res = c.get("resources") or {}
+        res = c.get("resources") if isinstance(c, dict) else None
         for section in ("limits", "requests"):
-            vals = res.get(section) or {}
-            for n in names:
+            vals = res.get(section) if isinstance(res, dict) else None
+            for n in names if isinstance(vals, dict) else ():
                 if n in vals:
                     return parse_quantity(vals[n])
         return 0
 
-    main = sum(one(c) for c in spec.get("containers") or [])
-    init = max([one(c) for c in spec.get("initContainers") or []] or [0])
+    def containers(key: str) -> list:
+        cs = spec.get(key)
+        return cs if isinstance(cs, list) else []
+
+    main = sum(one(c) for c in containers("containers"))
+    init = max([one(c) for c in containers("initContainers")] or [0])
     return max(main, init)
 
 
