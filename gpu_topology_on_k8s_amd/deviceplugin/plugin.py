@@ -457,8 +457,8 @@ class DevicePluginServer:
         resp = pb.PreferredAllocationResponse()
         pending = self._pending_assumed()
         for creq in request.container_requests:
-            avail = [int(x) for x in creq.available_deviceIDs]
-            must = [int(x) for x in creq.must_include_deviceIDs]
+            avail = self._ids(context, creq.available_deviceIDs)
+            must = self._ids(context, creq.must_include_deviceIDs)
             size = int(creq.allocation_size)
             ids = None
             for _, pa, _ in pending:
@@ -488,6 +488,15 @@ class DevicePluginServer:
             out += [a for a in sorted(avail, key=lambda a: (a not in healthy, a)) if a not in out][: size - len(out)]
             return sorted(out)
 
+    def _ids(self, context, raw) -> List[int]:
+        """Device IDs of a kubelet request: the decimal indices ListAndWatch advertised; anything else
+        is refused as INVALID_ARGUMENT (not an UNKNOWN error out of int())."""
+        try:
+            return [int(x) for x in raw]
+        except (TypeError, ValueError):
+            self._refuse(context, grpc.StatusCode.INVALID_ARGUMENT, f"device ids {list(raw)} are not this plugin's", "invalid")
+            raise  # context.abort raised already; a stub context that does not must not go on either
+
     def _refuse(self, context, code, msg: str, outcome: str) -> None:
         self.metrics.allocations.labels(outcome).inc()
         if self.api is not None and self.cfg.node_name:
@@ -500,7 +509,7 @@ class DevicePluginServer:
         resp = pb.AllocateResponse()
         all_ids: List[int] = []
         for creq in request.container_requests:
-            ids = [int(x) for x in creq.devices_ids]
+            ids = self._ids(context, creq.devices_ids)
             bad = [i for i in ids if i < 0 or i >= self.topology.n]
             if bad:
                 self._refuse(context, grpc.StatusCode.INVALID_ARGUMENT, f"unknown device ids {bad}", "invalid")
@@ -541,7 +550,7 @@ class DevicePluginServer:
         measured bandwidth on the pod.  A no-op unless ``prestart_validate``."""
         if not self.cfg.prestart_validate:
             return pb.PreStartContainerResponse()
-        ids = sorted({int(x) for x in request.devices_ids})
+        ids = sorted(set(self._ids(context, request.devices_ids)))
         t0 = time.perf_counter()
         try:
             res = self.validate_fn(ids)

@@ -221,3 +221,21 @@ def test_fake_kubelet_rejects_for_good_on_an_allocate_error(tmp_path):
         st = c.api.get_pod("default", "x")["status"]
         assert st["phase"] == "Failed" and st["reason"] == "UnexpectedAdmissionError"
         assert c.nodes["a"].kubelet.rejected and c.nodes["a"].kubelet.rejected[0][0] == "default/x"
+
+
+def test_device_ids_that_are_not_indices_are_refused_as_invalid_argument(tmp_path):
+    """The kubelet only sends IDs that ListAndWatch advertised; anything else is INVALID_ARGUMENT,
+    never an UNKNOWN error out of the handler."""
+    t = fx.f7_mi355x(n=4)
+    plug = DevicePluginServer(t, PluginConfig(node_name="n1", dev_root=placeholder_dev_tree(str(tmp_path), t)))
+    bad = pb.AllocateRequest(container_requests=[pb.ContainerAllocateRequest(devices_ids=["0", "gpu-1"])])
+    with pytest.raises(RuntimeError) as e:
+        plug.Allocate(bad, Ctx())
+    assert e.value.args[0] == grpc.StatusCode.INVALID_ARGUMENT and "gpu-1" in e.value.args[1]
+    pref = pb.PreferredAllocationRequest(container_requests=[pb.ContainerPreferredAllocationRequest(
+        available_deviceIDs=["0", "x"], must_include_deviceIDs=[], allocation_size=1)])
+    with pytest.raises(RuntimeError) as e:
+        plug.GetPreferredAllocation(pref, Ctx())
+    assert e.value.args[0] == grpc.StatusCode.INVALID_ARGUMENT
+    ok = plug.Allocate(pb.AllocateRequest(container_requests=[pb.ContainerAllocateRequest(devices_ids=["2"])]), Ctx())
+    assert ok.container_responses[0].envs["GTK_GPU_GROUP"] == "2"
