@@ -628,10 +628,18 @@ class DevicePluginServer:
                 out.append((f"/dev/dri/card{g.card}", f"{root}/dri/card{g.card}"))
         return list(dict.fromkeys(out))
 
+    @staticmethod
+    def _optional_node(container_path: str) -> bool:
+        """ROCm compute needs ``/dev/kfd`` and the render nodes; a ``card<N>`` (primary / display) node
+        is handed over when the node has it, and its absence never refuses a pod.  Found on MI355X:
+        a container given only ``renderD128`` had no ``card16`` although amdsmi names it
+        (``bench/plugin_soak.py``), and strict mode refused every Allocate there."""
+        return container_path.startswith("/dev/dri/card")
+
     def _missing_device_nodes(self, ids: Sequence[int]) -> List[str]:
         if self.cfg.device_specs != "strict":
             return []
-        return [h for _, h in self.device_nodes(ids) if not os.path.exists(h)]
+        return [h for c, h in self.device_nodes(ids) if not self._optional_node(c) and not os.path.exists(h)]
 
     def _container_response(self, ids: Sequence[int], extra_env: Dict[str, str]) -> pb.ContainerAllocateResponse:
         r = pb.ContainerAllocateResponse()
@@ -643,8 +651,8 @@ class DevicePluginServer:
                                    for i in ids):
                 r.cdi_devices.add(name=cdi_name(self.cfg.cdi_kind, i))
         for cpath, hpath in ([] if self.cfg.device_specs == "cdi" else self.device_nodes(ids)):
-            if self.cfg.device_specs == "stub" and not os.path.exists(hpath):
-                continue  # kind / fake GPUs: never hand containerd a host path the node does not have
+            if (self.cfg.device_specs == "stub" or self._optional_node(cpath)) and not os.path.exists(hpath):
+                continue  # kind / fake GPUs, or an absent card node: never hand containerd a missing host path
             r.devices.add(container_path=cpath, host_path=hpath, permissions="rw")
         numa = {int(self.topology.gpus[i].numa) for i in ids}
         mask = ""

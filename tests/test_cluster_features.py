@@ -507,3 +507,26 @@ def test_worst_scores_the_nic_term_like_select():
         w = worst(t, 2, engine=eng, nic_aware=True)
         assert abs(w.objective - hi) < 1e-9, (eng, w, hi)
     assert worst(t, 2, nic_aware=True).objective > worst(t, 2).objective - 1e-12
+
+
+def test_strict_specs_do_not_require_card_nodes(tmp_path):
+    """kfd + render nodes are what ROCm compute needs; a card node the node lacks is left out, not
+    refused (an MI355X container with only renderD128 had no card16: bench/plugin_soak.py)."""
+    t = fx.f7_mi355x(n=2)
+    (tmp_path / "dri").mkdir()
+    (tmp_path / "kfd").write_text("")
+    for g in t.gpus:
+        (tmp_path / "dri" / f"renderD{g.render_node}").write_text("")
+    assert all(g.card >= 0 for g in t.gpus)
+    plug = DevicePluginServer(t, PluginConfig(dev_root=str(tmp_path), node_name="n1", device_specs="strict"), api=FakeAPIServer())
+    plug.api.create_node(make_node("n1"))
+    from gpu_topology_on_k8s_amd.deviceplugin import proto as pb
+
+    req = pb.AllocateRequest()
+    req.container_requests.add(devices_ids=["1"])
+    r = plug.Allocate(req, None).container_responses[0]
+    paths = sorted(d.container_path for d in r.devices)
+    assert paths == ["/dev/dri/renderD%d" % t.gpus[1].render_node, "/dev/kfd"]
+    (tmp_path / "dri" / f"card{t.gpus[1].card}").write_text("")
+    r = plug.Allocate(req, None).container_responses[0]
+    assert f"/dev/dri/card{t.gpus[1].card}" in [d.container_path for d in r.devices]
