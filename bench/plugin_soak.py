@@ -74,6 +74,9 @@ def main() -> int:
     ap.add_argument("--reprobe-interval", type=float, default=4.0)
     ap.add_argument("--max-idle", type=float, default=8.0, help="longest idle gap between pods (s)")
     ap.add_argument("--hold", type=float, default=0.5, help="longest time a pod holds its device (s)")
+    ap.add_argument("--time-slices", type=int, default=1,
+                    help="S > 1: the node advertises amd.com/gpu-slice; pods take 1..S slices, several at once, "
+                         "and partial-GPU pods get the vGPU guard mounted")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--out", default="")
     a = ap.parse_args()
@@ -96,37 +99,59 @@ def main() -> int:
             "--metrics-port", str(mport), "--metrics-host", "127.0.0.1", "--log-level", "WARNING"]
     if a.discovery == "fake":
         args += ["--fake-gpus", "2", "--device-specs", "stub", "--dev-root", sockdir]
+    resource = "amd.com/gpu"
+    if a.time_slices > 1:
+        resource = "amd.com/gpu-slice"
+        args += ["--time-slices", str(a.time_slices), "--share-guard", "env", "--share-guard-dir", os.path.join(sockdir, "vgpu")]
     log_path = os.path.join(sockdir, "daemon.log")
     logf = open(log_path, "w")
     daemon = subprocess.Popen(args, cwd=REPO, env=dict(os.environ, PYTHONPATH=REPO), stdout=logf, stderr=subprocess.STDOUT)
-    lat, rejected, admitted, samples = [], 0, 0, []
+    lat, rejected, admitted, guarded, samples = [], 0, 0, 0, []
     rc = None
     try:
-        plugin = kubelet.wait_for("amd.com/gpu", timeout=300)
+        plugin = kubelet.wait_for(resource, timeout=300)
         devs = sorted(plugin.devices, key=int)
         t0 = time.time()
         samples.append({"t": 0.0, **_proc_stats(daemon.pid), **_metrics(mport)})
         print(json.dumps({"registered": devs, **samples[-1]}), flush=True)
         i, last = 0, t0
+        live: list = []  # (name, slices) of pods holding devices
+
+        def finish(name):
+            kubelet.release(api.get_pod("default", name))  # the container ends: its devices go back
+            api.delete_pod("default", name)
+
         while time.time() - t0 < a.seconds:
-            time.sleep(rng.uniform(0.0, a.max_idle))  # idle: a re-probe may start now
-            pod = api.create_pod(make_pod(f"p{i}", gpus=1, node="soak-node"))
+            if not live:
+                time.sleep(rng.uniform(0.0, a.max_idle))  # idle: a re-probe may start now
+            want = 1 if a.time_slices <= 1 else rng.randint(1, a.time_slices)
+            free = len(kubelet.available(resource))
+            if want > free:  # full: the oldest pod ends first
+                finish(live.pop(0)[0])
+                continue
+            pod = api.create_pod(make_pod(f"p{i}", gpus=want, node="soak-node", resource=resource))
             ts = time.perf_counter()
             try:
-                kubelet.admit(pod, "amd.com/gpu")
+                resp = kubelet.admit(pod, resource)
                 admitted += 1
+                envs = resp.container_responses[0].envs
+                guarded += int("LD_PRELOAD" in envs)
+                live.append((f"p{i}", want))
             except AdmissionError as e:
                 rejected += 1
                 print(json.dumps({"rejected": f"p{i}", "error": str(e)[:200]}), flush=True)
+                api.delete_pod("default", f"p{i}")
             lat.append((time.perf_counter() - ts) * 1e3)
             time.sleep(rng.uniform(0.0, a.hold))
-            kubelet.release(api.get_pod("default", f"p{i}"))  # the container ends: its device goes back
-            api.delete_pod("default", f"p{i}")
+            while live and (a.time_slices <= 1 or rng.random() < 0.5):
+                finish(live.pop(0)[0])
             i += 1
             if time.time() - last >= 10:
                 last = time.time()
                 samples.append({"t": round(last - t0, 1), "pods": i, **_proc_stats(daemon.pid), **_metrics(mport)})
                 print(json.dumps(samples[-1]), flush=True)
+        for name, _ in live:
+            finish(name)
         samples.append({"t": round(time.time() - t0, 1), "pods": i, **_proc_stats(daemon.pid), **_metrics(mport)})
     finally:
         if daemon.poll() is None:
@@ -152,7 +177,8 @@ def main() -> int:
     allocs = {label(k): int(v) for k, v in last.items() if k.startswith("gtk_plugin_allocations_total{")}
     q = sorted(lat)
     out = {
-        "discovery": a.discovery, "probe": a.probe, "seconds": a.seconds, "pods": len(lat), "admitted": admitted,
+        "discovery": a.discovery, "probe": a.probe, "time_slices": a.time_slices, "seconds": a.seconds, "pods": len(lat),
+        "admitted": admitted, "guarded": guarded,
         "rejected": rejected, "allocate_ms": {"p50": round(statistics.median(q), 2) if q else None,
                                               "p99": round(q[int(0.99 * (len(q) - 1))], 2) if q else None,
                                               "max": round(q[-1], 2) if q else None},
