@@ -86,8 +86,8 @@ def repartition(api, node_name: str, contract: Contract, idle_fn: Callable[[], b
         log.warning("switching GPU partitions %s -> %s (node idle)", before, tag)
         try:
             res = apply_partition(want_c, want_m, lib=lib, reload_driver=reload_driver)
-        except PartitionError as e:
-            res = {"ok": False, "reason": str(e)}
+        except Exception as e:  # noqa: BLE001 - PartitionError, or amdsmi without the setters: recorded, not retried
+            res = {"ok": False, "reason": str(e)[:500]}
         if res["ok"]:
             api.patch_node(node_name, annotations={contract.partition_failed_key: None})
             _event(api, node_name, "GPUPartitionChanged", f"GPU partitions {before} -> {tag}", "Normal")
