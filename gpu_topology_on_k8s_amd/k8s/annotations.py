@@ -311,11 +311,18 @@ class PodAssignment:
 
     @classmethod
     def from_annotations(cls, ann: Optional[Mapping[str, str]]) -> Optional["PodAssignment"]:
-        ann = ann or {}
-        g = parse_group(ann.get(ANN_GROUP))
-        if g is None:
-            g = parse_group(ann.get(ANN_GPU_ID_ALIAS))  # diagram alias, read-only
-        if g is None:
+        """The assignment a pod carries, or None.  A GROUP that is not a list of device indices
+        ("a,b", "-1", a non-string) is no assignment: any user can annotate their own pod, and one such
+        pod must not stop the extender from reading its node or the plugin from admitting pods (the pod
+        then counts by its resource request, like any pod without a GROUP)."""
+        ann = ann if isinstance(ann, Mapping) else {}
+        try:
+            g = parse_group(ann.get(ANN_GROUP))
+            if g is None:
+                g = parse_group(ann.get(ANN_GPU_ID_ALIAS))  # diagram alias, read-only
+        except (ValueError, AttributeError, TypeError):
+            return None
+        if g is None or any(i < 0 for i in g):
             return None
         assigned = str(ann.get(ANN_ASSIGNED, "false")).lower() == "true"
         try:

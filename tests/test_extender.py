@@ -440,3 +440,19 @@ def test_multi_node_pod_binds_across_nic_domains():
     rdma = api.create_pod(make_pod("rdma", gpus=2))
     rdma["spec"]["containers"][0]["resources"]["limits"]["rdma/hca"] = "1"
     assert ext.multi_node(rdma) and not ext.multi_node(api.get_pod("default", "local"))
+
+
+def test_a_pod_with_a_garbage_group_annotation_does_not_break_its_node():
+    """Any user can annotate their own pod: a GROUP that is not a device list must not stop the
+    extender from reading the node (the pod counts by its request, like a pod without a GROUP)."""
+    api, ext, _ = _cluster()
+    for i, bad in enumerate(("x,1", "-1", "1,,2,a", "0x1")):
+        api.create_pod(make_pod(f"odd{i}", gpus=1, node="n1", annotations={ANN_GROUP: bad, ANN_ASSIGNED: "true"}))
+    assert PodAssignment.from_annotations({ANN_GROUP: "x,1"}) is None
+    assert PodAssignment.from_annotations({ANN_GROUP: "1,,2"}).group == [1, 2]  # empty entries are skipped
+    _submit(api, "p", 4)
+    d = _bind(api, ext, "p")
+    assert d is not None and len(d.ids) == 4
+    _submit(api, "big", 8)
+    with pytest.raises(Exception):
+        _bind(api, ext, "big", "n1")  # 4 (p) + 3 unreadable-but-counted + "1,,2" holding 1,2: no room for 8
