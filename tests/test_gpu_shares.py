@@ -222,3 +222,40 @@ def test_vgpu_guard_caps_torch_and_forces_the_cu_mask(tmp_path):
     assert g["total"] == 16 << 30 and g["free"] <= 16 << 30
     assert g["over_refused"] is True
     assert 0.15 * full < g["tflops"] < 0.40 * full, (g["tflops"], full)  # 64 of 256 CUs (27 % measured in r02)
+
+
+def test_doctor_inside_a_guarded_half_gpu_pod(tmp_path):
+    """A whole pod start on the real GPU: the device plugin (real discovery, 2 time slices, guard on)
+    allocates slice 0; a process gets exactly what the container would (the Allocate envs, the guard
+    preloaded from its mount, the mounted config with the accounting file) and runs `gtk doctor --gpu`:
+    GROUP maps to its HIP device by PCI address, the share is guarded, and the MFMA warm-up runs on
+    half the CUs."""
+    from gpu_topology_on_k8s_amd.deviceplugin import DevicePluginServer, PluginConfig
+    from gpu_topology_on_k8s_amd.deviceplugin import proto as pb
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
+    from gpu_topology_on_k8s_amd.topology.shares import time_slice
+
+    t = time_slice(discover("auto"), 2)
+    plug = DevicePluginServer(t, PluginConfig(device_specs="stub", dev_root=str(tmp_path), share_guard="env",
+                                              guard_dir=str(tmp_path / "vgpu")))
+    assert plug.install_guard()
+    req = pb.AllocateRequest()
+    req.container_requests.add(devices_ids=["0"])
+    r = plug.Allocate(req, None).container_responses[0]
+    mounts = {m.container_path: m.host_path for m in r.mounts}
+    conf = tmp_path / "pod.conf"  # the mounted config, its container paths pointed at the host files
+    conf.write_text(open(mounts[r.envs["GTK_VGPU_CONFIG"]]).read().replace(plug.GUARD_ACCT_IN_CONTAINER,
+                                                                           mounts[plug.GUARD_ACCT_IN_CONTAINER]))
+    env = {k: v for k, v in os.environ.items() if k not in _STRIP}
+    env.update({k: v for k, v in r.envs.items() if k not in ("LD_PRELOAD", "GTK_VGPU_CONFIG")})
+    env["GTK_VGPU_CONFIG"] = str(conf)
+    guard = mounts[r.envs["LD_PRELOAD"]]
+    env["LD_PRELOAD"] = (env["LD_PRELOAD"] + ":" if env.get("LD_PRELOAD") else "") + guard
+    p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd", "doctor", "--gpu"], capture_output=True, text=True,
+                       timeout=240, cwd=REPO, env=env)
+    print(p.stdout)
+    checks = {c["name"]: c for c in (json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")) if "name" in c}
+    assert checks["pod-group"]["status"] == "ok" and checks["pod-group"]["hip_devices"] == [0], checks["pod-group"]
+    assert checks["pod-share"]["status"] == "ok", checks["pod-share"]
+    assert checks["mfma"]["status"] in ("ok", "warn") and 0.3 * 2000 < checks["mfma"]["tflops"] < 0.7 * 2400, checks["mfma"]
+    assert p.returncode == 0, p.stderr[-2000:]
