@@ -19,6 +19,7 @@ def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--mib", type=int, default=2048)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--sweep", action="store_true", help="dense sweep of dst-src gaps (4 KiB .. 64 MiB, both orders)")
     a = ap.parse_args()
     import torch
 
@@ -44,8 +45,15 @@ def main() -> int:
     pad = 64 << 20
     big = torch.empty(2 * n + pad, dtype=torch.uint8, device="cuda")
     big[:n].fill_(1)
-    for off in [0, 256, 4096, 65536, 1 << 20, (1 << 20) + 4096, 2 << 20, (2 << 20) + 256 * 1024, 3 << 20, 16 << 20,
-                (16 << 20) + 8192, 32 << 20]:
+    offs = [0, 256, 4096, 65536, 1 << 20, (1 << 20) + 4096, 2 << 20, (2 << 20) + 256 * 1024, 3 << 20, 16 << 20,
+            (16 << 20) + 8192, 32 << 20]
+    if a.sweep:
+        import random
+
+        rng = random.Random(1)
+        offs = sorted(set([k << 12 for k in range(0, 64)] + [k << 16 for k in range(0, 64)] + [k << 20 for k in range(0, 64)]
+                          + [rng.randrange(0, 64 << 20) & ~4095 for _ in range(64)]))
+    for off in offs:
         src, dst = big[:n], big[n + off:2 * n + off]
         rows.append({"layout": "one-alloc", "gap": off, "dst_minus_src": dst.data_ptr() - src.data_ptr(),
                      "algbw_gbps": round(timed(src, dst), 1)})
