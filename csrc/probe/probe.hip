@@ -16,6 +16,8 @@
 //                  (ingress and egress of every GPU loaded together, as under a ring all-reduce):
 //                  the slowest member's ingress is the bound a ring all-reduce's busBW is measured
 //                  against.
+//   IPC read     : the K1 kernel on a buffer another process exported with hipIpcGetMemHandle (the
+//                  mapping RCCL's P2P transport gives a rank of its peers' buffers).
 // The copy kernel exists in two staging forms (LDS-DMA and plain register staging) so the
 // rocprofv3 counter profile can show what LDS staging costs/buys on a pure stream (profiles/).
 //
@@ -704,6 +706,77 @@ py::dict xcc_census(int dev, int blocks) {
   return r;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Cross-process reads through HIP IPC: the mapping RCCL's P2P transport gives a rank of its peers'
+// buffers (hipIpcGetMemHandle in the owner, hipIpcOpenMemHandle in the reader).  One process
+// exports a patterned buffer; another opens the handle and streams it into a buffer of its own with
+// the K1 LDS-DMA kernel, then verifies the pattern.  On one GPU both sides share the device, which
+// runs the IPC export / import path (the HSA_ENABLE_IPC_MODE_LEGACY=0 dma-buf handles) and the
+// kernel on an imported mapping; on a node the reader is a peer GPU.
+class IpcBuffer {
+ public:
+  IpcBuffer(int dev, size_t bytes, unsigned int seed) : buf_(dev, bytes), seed_(seed) {
+    if (bytes < 16 || bytes % 16) throw std::invalid_argument("bytes must be a positive multiple of 16");
+    DeviceGuard g(dev);
+    hipLaunchKernelGGL(fill_pattern_kernel, dim3(num_cus(dev) * 4), dim3(kBlock), 0, 0, (unsigned int*)buf_.p, bytes / 4, seed);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipIpcGetMemHandle(&h_, buf_.p));
+  }
+  py::bytes handle() const { return py::bytes(reinterpret_cast<const char*>(&h_), sizeof(h_)); }
+  size_t bytes() const { return buf_.bytes; }
+  unsigned int seed() const { return seed_; }
+
+ private:
+  DevBuf buf_;
+  unsigned int seed_;
+  hipIpcMemHandle_t h_{};
+};
+
+py::dict ipc_read_bw(const py::bytes& handle, int dev, size_t bytes, unsigned int seed, int iters, int warmup,
+                     int blocks_per_cu) {
+  const std::string raw = handle;
+  if (raw.size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("not a hipIpcMemHandle_t");
+  if (bytes < 16 || bytes % 16) throw std::invalid_argument("bytes must be a positive multiple of 16");
+  if (iters < 1) throw std::invalid_argument("iters >= 1");
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, raw.data(), sizeof(h));
+  DeviceGuard g(dev);
+  void* src = nullptr;
+  HIP_CHECK(hipIpcOpenMemHandle(&src, h, hipIpcMemLazyEnablePeerAccess));
+  struct Closer {
+    void* p;
+    ~Closer() { (void)hipIpcCloseMemHandle(p); }
+  } closer{src};
+  DevBuf dst(dev, bytes);
+  const size_t n_vec = bytes / 16;
+  const int grid = num_cus(dev) * std::max(1, blocks_per_cu);
+  hipStream_t s;
+  HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipEvent_t e0, e1;
+  HIP_CHECK(hipEventCreate(&e0));
+  HIP_CHECK(hipEventCreate(&e1));
+  for (int i = 0; i < warmup; ++i) launch_copy("lds", true, src, dst.p, n_vec, grid, s);
+  HIP_CHECK(hipEventRecord(e0, s));
+  for (int i = 0; i < iters; ++i) launch_copy("lds", true, src, dst.p, n_vec, grid, s);
+  HIP_CHECK(hipEventRecord(e1, s));
+  HIP_CHECK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  HIP_CHECK(hipEventDestroy(e0));
+  HIP_CHECK(hipEventDestroy(e1));
+  HIP_CHECK(hipStreamDestroy(s));
+  const bool ok = verify_pattern(dst, bytes / 4, seed);
+  py::dict d;
+  d["dev"] = dev;
+  d["bytes"] = bytes;
+  d["iters"] = iters;
+  d["ms_per_iter"] = ms / iters;
+  d["gbps"] = (double)bytes / (ms / 1e3 / iters) / 1e9;
+  d["ok"] = ok;
+  return d;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_probe, m) {
@@ -723,6 +796,14 @@ PYBIND11_MODULE(_probe, m) {
         py::arg("warmup") = 1, py::arg("mode") = "read", py::arg("kind") = "lds", py::arg("nontemporal") = false,
         py::arg("blocks_per_cu") = kBlocksPerCU, py::call_guard<py::gil_scoped_release>());
   m.def("xcc_census", &xcc_census, py::arg("dev"), py::arg("blocks") = 4096);
+  py::class_<IpcBuffer>(m, "IpcBuffer")
+      .def(py::init<int, size_t, unsigned int>(), py::arg("dev"), py::arg("bytes"), py::arg("seed") = 0x5eedu)
+      .def("handle", &IpcBuffer::handle)
+      .def_property_readonly("bytes", &IpcBuffer::bytes)
+      .def_property_readonly("seed", &IpcBuffer::seed);
+  m.def("ipc_read_bw", &ipc_read_bw, py::arg("handle"), py::arg("dev"), py::arg("bytes"), py::arg("seed"),
+        py::arg("iters") = 5, py::arg("warmup") = 1, py::arg("blocks_per_cu") = kBlocksPerCU,
+        "open another process's buffer by its IPC handle and stream it into a local one (K1 kernel); verified");
   m.attr("BLOCK") = kBlock;
   m.attr("UNROLL") = kUnroll;
   m.attr("BLOCKS_PER_CU") = kBlocksPerCU;

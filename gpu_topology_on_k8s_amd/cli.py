@@ -114,6 +114,42 @@ def cmd_ring(a) -> int:
     return 0
 
 
+def cmd_ipc(a) -> int:
+    """Cross-process GPU memory through HIP IPC, the mapping RCCL's P2P transport uses between ranks.
+    This process exports a patterned buffer on ``--device``. A child opens the handle on
+    ``--reader-device`` and streams it into its own buffer with the K1 LDS-DMA kernel, then verifies
+    it. Prints one JSON line, and exits 1 when the export, the import or the check fails."""
+    import subprocess
+
+    from ._native import load
+
+    probe = load("_probe")
+    if a.read:  # the child side
+        r = probe.ipc_read_bw(bytes.fromhex(a.read), a.reader_device, a.bytes, a.seed, a.iters)
+        print(json.dumps(dict(r)))
+        return 0 if r["ok"] else 1
+    out = {"ipc_mode_legacy": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY"), "bytes": a.bytes, "device": a.device,
+           "reader_device": a.reader_device}
+    try:
+        buf = probe.IpcBuffer(a.device, a.bytes, a.seed)
+    except RuntimeError as e:
+        out.update(ok=False, stage="export (hipIpcGetMemHandle)", error=str(e)[:300])
+        print(json.dumps(out))
+        return 1
+    p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd", "ipc", "--read", buf.handle().hex(), "--bytes",
+                        str(a.bytes), "--seed", str(a.seed), "--reader-device", str(a.reader_device), "--iters", str(a.iters)],
+                       capture_output=True, text=True, timeout=a.timeout)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        out.update(ok=False, stage="import (hipIpcOpenMemHandle) / read", error=(p.stderr or p.stdout)[-300:])
+        print(json.dumps(out))
+        return 1
+    r = json.loads(lines[-1])
+    out.update(ok=bool(r["ok"]), read_gbps=round(r["gbps"], 1), ms_per_iter=round(r["ms_per_iter"], 4))
+    print(json.dumps(out))
+    return 0 if out["ok"] else 1
+
+
 def cmd_select(a) -> int:
     from .placement import PlacementPolicy, select, worst
     from .placement.gaia import gaia_schedule, tree_from_topology
@@ -361,6 +397,15 @@ def main(argv=None) -> int:
     p.add_argument("--preset", default="quick", choices=["quick", "full"])
     p.add_argument("--patterns", default="all,ring", help="K6 peer patterns: all (every link of the subset), ring (pred+succ)")
     p.set_defaults(fn=cmd_ring)
+    p = sub.add_parser("ipc", help="cross-process GPU memory through HIP IPC (RCCL's P2P mapping), read by the K1 kernel")
+    p.add_argument("--device", type=int, default=0, help="HIP ordinal that owns (exports) the buffer")
+    p.add_argument("--reader-device", type=int, default=0, help="HIP ordinal of the reading process (a peer on a node)")
+    p.add_argument("--bytes", type=int, default=256 << 20)
+    p.add_argument("--seed", type=int, default=0x5EED)
+    p.add_argument("--iters", type=int, default=5)
+    p.add_argument("--timeout", type=float, default=180.0)
+    p.add_argument("--read", default="", help=argparse.SUPPRESS)
+    p.set_defaults(fn=cmd_ipc)
     p = sub.add_parser("select")
     disc(p)
     p.add_argument("-k", type=int, default=0)

@@ -343,3 +343,20 @@ def test_nic_discovery_on_real_node():
     if t.nics:
         assert len(t.gpu_nic) == t.n and all(len(row) == len(t.nics) for row in t.gpu_nic)
         assert all(0 <= c <= 5 for row in t.gpu_nic for c in row)
+
+
+def test_ipc_read_across_processes():
+    """HIP IPC between two processes, the mapping RCCL's P2P transport gives a rank of its peers'
+    buffers: one process exports a patterned buffer, a child opens the handle and streams it with the
+    K1 LDS-DMA kernel, verified.  With HSA_ENABLE_IPC_MODE_LEGACY=0 (what bench.py, the manifests and
+    the Dockerfile set) the export is a dma-buf handle; the legacy KFD path is run too and reported."""
+    base = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    runs = {}
+    for mode in ("0", "1"):
+        p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd", "ipc", "--bytes", str(256 << 20)],
+                           capture_output=True, text=True, timeout=300, cwd=REPO, env=dict(base, HSA_ENABLE_IPC_MODE_LEGACY=mode))
+        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        runs[mode] = (p.returncode, json.loads(lines[-1]) if lines else {"stderr": p.stderr[-500:]})
+    print(json.dumps(runs))
+    rc, out = runs["0"]
+    assert rc == 0 and out["ok"] and out["read_gbps"] > 1000, out
