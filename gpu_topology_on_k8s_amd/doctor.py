@@ -19,7 +19,8 @@ Pod checks (when ``GTK_GPU_GROUP`` is set, i.e. inside a container Allocate conf
 * ``pod-cpuset``                ``GTK_CPUSET`` is usable here (not disjoint from the allowed CPUs);
 * ``pod-share``                 a partial-GPU pod has its CU mask and the vGPU guard in force.
 
-``--gpu`` adds the checks that initialise HIP (device count, gfx950, an MFMA warm-up); without it
+``--gpu`` adds the checks that initialise HIP (device count, gfx950, an MFMA warm-up, an exact RCCL
+all-reduce over the visible devices); without it
 the command never touches a GPU, so it is safe on a node whose GPUs are busy.
 """
 from __future__ import annotations
@@ -172,6 +173,15 @@ def check_gpu() -> List[Check]:
     w = probe.warmup(0, 20.0)
     out.append(_c("mfma", "ok" if w["tflops"] > 1000 else "warn", f"{w['tflops']:.0f} TF/s dense bf16 on device 0",
                   tflops=round(float(w["tflops"]), 1)))
+    try:  # RCCL loads and sums exactly (one rank per visible device; cross-device links: `gtk validate`)
+        from ._native import load
+
+        pts = load("_rccl").local_sweep(list(range(n)), [1 << 20], "bf16", 1, 1, False, True)
+        wrong = sum(int(p["wrong"]) for p in pts)
+        out.append(_c("rccl", "ok" if wrong == 0 else "fail",
+                      f"{n}-rank all-reduce of 1 MiB bf16: {'exact' if wrong == 0 else f'{wrong} wrong elements'}"))
+    except Exception as e:  # noqa: BLE001 - the check's result
+        out.append(_c("rccl", "fail", str(e)[:300]))
     return out
 
 
