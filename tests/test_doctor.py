@@ -56,3 +56,16 @@ def test_cli_exit_status_and_json_lines():
                        capture_output=True, text=True, timeout=120, cwd=REPO, env=env)
     lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert p.returncode == 1 and lines[-1]["status"] == "fail"  # no /dev/kfd, no GPUs in this container
+
+
+def test_ipc_cli_reports_a_failed_export_as_json():
+    """`gtk ipc` without a usable GPU: one JSON line naming the failed stage, exit 1 (on MI355X it
+    reads a peer process's buffer: tests/test_gpu_native.py::test_ipc_read_across_processes)."""
+    import torch
+
+    if torch.cuda.is_available():
+        return
+    p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd", "ipc", "--bytes", "1048576"], capture_output=True,
+                       text=True, timeout=120, cwd=REPO)
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert p.returncode == 1 and out["ok"] is False and out["stage"].startswith("export")
