@@ -287,3 +287,16 @@ def test_restart_on_a_busy_node_keeps_the_published_slicing():
     api.create_node(make_node("fresh", labels={c.time_slices_label: "4"}))  # first start: nothing published
     assert startup_time_slices(api, "fresh", c, 1) == (4, "")
     assert startup_time_slices(None, "", c, 3) == (3, "")
+
+
+def test_plugin_soak_harness_on_a_fake_node():
+    """bench/plugin_soak.py (run on MI355X with re-probes: profiles/r03_soak/): the shipped daemon under
+    pod churn, here on a fake 2-GPU node sliced in two, with concurrent partial-GPU pods."""
+    import json
+
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench", "plugin_soak.py"), "--discovery", "fake", "--probe", "off",
+                        "--seconds", "4", "--max-idle", "0.3", "--hold", "0.2", "--time-slices", "2"],
+                       capture_output=True, text=True, timeout=180, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith('{"discovery"')][-1])
+    assert out["rejected"] == 0 and out["admitted"] >= 3 and out["guarded"] >= 1 and out["daemon_exit"] == 0
