@@ -31,7 +31,10 @@ import torch.nn.functional as F
 
 from ..ops import fused
 
-__all__ = ["LlamaConfig", "FlatParams", "Llama", "smoke_step"]
+__all__ = ["LlamaConfig", "FlatParams", "Llama", "smoke_step", "PROJECTIONS"]
+
+#: the projections of a block (and the head), as named in the parameters
+PROJECTIONS = ("wqkv", "wo", "w13", "w2", "lm_head")
 
 
 @dataclass(frozen=True)
@@ -240,9 +243,10 @@ class _NTOperands:
     b4 x 4096 on one MI355X: 22.8k tok/s with overlap vs 23.0k without, and +18 GB peak (all W^T
     live through backward) -- the GEMMs hold every CU, so the side stream only contends."""
 
-    def __init__(self, x: torch.Tensor, w: torch.Tensor, overlap: bool):
+    def __init__(self, x: torch.Tensor, w: torch.Tensor, overlap: bool, dgrad_nn: bool = False):
         self.event = None
-        if overlap and x.is_cuda:
+        self.dgrad_nn = dgrad_nn  # dgrad reads W as is (NN): no W^T is made
+        if overlap and x.is_cuda and not dgrad_nn:
             main = torch.cuda.current_stream(x.device)
             side = _side_stream(x.device)
             side.wait_stream(main)  # x (and the optimizer's last write of w) are complete
@@ -258,7 +262,12 @@ class _NTOperands:
             self.x, self.w = x, w
 
     def get(self) -> Tuple[torch.Tensor, torch.Tensor]:
-        """-> (x^T, W^T), ready for use on the current stream."""
+        """-> (x^T, W^T), ready for use on the current stream (``W`` itself with ``dgrad_nn``)."""
+        if self.dgrad_nn:
+            if self.x_t is None:
+                self.x_t = fused.transpose(self.x)
+                self.x = None
+            return self.x_t, self.w
         if self.event is not None:
             main = torch.cuda.current_stream(self.x_t.device)
             main.wait_event(self.event)
@@ -275,10 +284,10 @@ class _FlatLinear(torch.autograd.Function):
     """``y = x W^T`` whose weight gradient is written in place into the flat buffer."""
 
     @staticmethod
-    def forward(ctx, x, w, flat, name, nt, overlap):
-        ctx.flat, ctx.name, ctx.nt = flat, name, nt
+    def forward(ctx, x, w, flat, name, nt, overlap, dgrad_nn=False):
+        ctx.flat, ctx.name, ctx.nt, ctx.dgrad_nn = flat, name, nt, dgrad_nn
         if nt:
-            ctx.ops = _NTOperands(x, w, overlap)
+            ctx.ops = _NTOperands(x, w, overlap, dgrad_nn)
         else:
             ctx.save_for_backward(x, w)
         return F.linear(x, w)
@@ -288,13 +297,18 @@ class _FlatLinear(torch.autograd.Function):
         if ctx.nt:
             x_t, w_t = ctx.ops.get()
             ctx.ops = None
-            dx = F.linear(dy, w_t) if ctx.needs_input_grad[0] else None  # dy (W^T)^T
+            if not ctx.needs_input_grad[0]:
+                dx = None
+            elif ctx.dgrad_nn:
+                dx = dy.mm(w_t)  # w_t is W here: dy W (NN)
+            else:
+                dx = F.linear(dy, w_t)  # dy (W^T)^T
             ctx.flat.write_grad(ctx.name, dy, None, nt=True, x_t=x_t)
         else:
             x, w = ctx.saved_tensors
             dx = dy.mm(w) if ctx.needs_input_grad[0] else None
             ctx.flat.write_grad(ctx.name, dy, x)
-        return dx, None, None, None, None, None
+        return dx, None, None, None, None, None, None
 
 
 class _FlatLinearSwiGLU(torch.autograd.Function):
@@ -303,11 +317,11 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
     the transpose straight to the NT weight-gradient GEMM."""
 
     @staticmethod
-    def forward(ctx, x, w, flat, name, nt, overlap):
+    def forward(ctx, x, w, flat, name, nt, overlap, dgrad_nn=False):
         gu = F.linear(x, w)
-        ctx.flat, ctx.name, ctx.nt = flat, name, nt
+        ctx.flat, ctx.name, ctx.nt, ctx.dgrad_nn = flat, name, nt, dgrad_nn
         if nt:
-            ctx.ops = _NTOperands(x, w, overlap)
+            ctx.ops = _NTOperands(x, w, overlap, dgrad_nn)
             ctx.save_for_backward(gu)
         else:
             ctx.save_for_backward(gu, x, w)
@@ -320,22 +334,34 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
             dgu, dgu_t = fused.swiglu_bwd_t(da, gu)
             x_t, w_t = ctx.ops.get()
             ctx.ops = None
-            dx = F.linear(dgu, w_t) if ctx.needs_input_grad[0] else None
+            if not ctx.needs_input_grad[0]:
+                dx = None
+            elif ctx.dgrad_nn:
+                dx = dgu.mm(w_t)  # w_t is W here (NN)
+            else:
+                dx = F.linear(dgu, w_t)
             ctx.flat.write_grad(ctx.name, dgu, None, nt=True, dy_t=dgu_t, x_t=x_t)
         else:
             _, x, w = ctx.saved_tensors
             dgu = fused.hip().swiglu_bwd(da.contiguous(), gu) if gu.is_cuda else fused.swiglu_bwd_ref(da, gu)
             dx = dgu.mm(w) if ctx.needs_input_grad[0] else None
             ctx.flat.write_grad(ctx.name, dgu, x)
-        return dx, None, None, None, None, None
+        return dx, None, None, None, None, None, None
 
 
 class Llama(torch.nn.Module):
     def __init__(self, cfg: LlamaConfig, device="cuda", seed: int = 0, checkpoint: bool = False, attn: str = "hip",
-                 gemm_layout: str = "nt", overlap_transposes: bool = False, fuse_residual: bool = True):
+                 gemm_layout: str = "nt", overlap_transposes: bool = False, fuse_residual: bool = True,
+                 dgrad_nn: Tuple[str, ...] = ()):
         super().__init__()
         if gemm_layout not in ("nt", "native"):
             raise ValueError("gemm_layout must be 'nt' or 'native'")
+        bad = set(dgrad_nn) - set(PROJECTIONS)
+        if bad:
+            raise ValueError(f"dgrad_nn: unknown projections {sorted(bad)} (of {PROJECTIONS})")
+        # projections whose input gradient is dy W (NN) instead of dy (W^T)^T: no W^T per step, for
+        # the shapes where hipBLASLt's NN kernel costs less than the NT one plus the transpose
+        self.dgrad_nn = frozenset(dgrad_nn)
         self.cfg = cfg
         self.checkpoint = checkpoint
         self.attn = attn
@@ -379,7 +405,8 @@ class Llama(torch.nn.Module):
 
     def _linear(self, x: torch.Tensor, name: str) -> torch.Tensor:
         nt = self.gemm_layout == "nt"
-        return _FlatLinear.apply(x, self.P(name).detach(), self.flat, name, nt, self.overlap_transposes)
+        return _FlatLinear.apply(x, self.P(name).detach(), self.flat, name, nt, self.overlap_transposes,
+                                 name.rsplit(".", 1)[-1] in self.dgrad_nn)
 
     # ---------------------------------------------------------------- blocks
     def _attention(self, q, k, v):
@@ -417,7 +444,7 @@ class Llama(torch.nn.Module):
         o = self._attention(q, k, v).reshape(B * S, H * Dh)  # [B, S, H, Dh] -> [B*S, H*Dh]
         x, h = self._norm(x, self._linear(o, f"l{i}.wo"), f"l{i}.ffn_norm")
         a = _FlatLinearSwiGLU.apply(h, self.P(f"l{i}.w13").detach(), self.flat, f"l{i}.w13", self.gemm_layout == "nt",
-                                    self.overlap_transposes)
+                                    self.overlap_transposes, "w13" in self.dgrad_nn)
         return x, self._linear(a, f"l{i}.w2")
 
     def forward(self, tokens: torch.Tensor, labels: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -110,6 +110,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
           placement: str = "auto", discovery: str = "auto", bucket_mb: float = 256.0, checkpoint: bool = False, lr: float = 3e-4,
           attn: str = "hip", seed: int = 0, log: bool = True, gemm_tuning: str = "auto",
           gemm_table: Optional[str] = None, gemm_layout: str = "nt", overlap_transposes: bool = False,
+          dgrad_nn: str = "",
           zero1: bool = False, save_dir: Optional[str] = None, save_every: int = 0, resume: Optional[str] = None,
           keep: int = 2, fuse_residual: bool = True, overlap_norm: bool = False, same_data: bool = False,
           graph: str = "auto", conv: str = "hip", cpu_bind: str = "auto") -> Dict[str, object]:
@@ -163,7 +164,8 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
     else:
         cfg = LlamaConfig.named(model_name)
         model = Llama(cfg, device=device, seed=seed, checkpoint=checkpoint, attn=attn, gemm_layout=gemm_layout,
-                      overlap_transposes=overlap_transposes, fuse_residual=fuse_residual)
+                      overlap_transposes=overlap_transposes, fuse_residual=fuse_residual,
+                      dgrad_nn=tuple(p for p in dgrad_nn.split(",") if p))
         items_per_step, unit, flops_per_item = batch * seq, "tokens", cfg.flops_per_token(seq)
     broadcast_params(model.flat)
     # graph mode issues the gradient collectives after backward (inside the captured step), not from
@@ -304,6 +306,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "gemm_tuning": gemm_mode,
         "gemm_layout": gemm_layout,
         "overlap_transposes": overlap_transposes,
+        "dgrad_nn": dgrad_nn,
         "fuse_residual": fuse_residual,
         "overlap_norm": ar.overlap_norm,
         "step_start": start_step,
@@ -342,6 +345,9 @@ def main(argv=None) -> int:
     ap.add_argument("--gemm-table", default=None, help="TunableOp results table (default: the shipped MI355X table)")
     ap.add_argument("--gemm-layout", default="nt", choices=["nt", "native"],
                     help="backward GEMM operand layout: nt = transposed operands (HIP transpose kernel), native = as autograd issues them")
+    ap.add_argument("--dgrad-nn", default="",
+                    help="comma list of projections (wqkv,wo,w13,w2,lm_head) whose input gradient uses the NN GEMM dy W "
+                         "instead of NT with a per-step W^T (gemm layout nt)")
     ap.add_argument("--overlap-transposes", action="store_true",
                     help="make the NT operands' transposes on a side stream in forward (measured: no gain on MI355X)")
     ap.add_argument("--zero1", action="store_true",
@@ -367,7 +373,7 @@ def main(argv=None) -> int:
     a = ap.parse_args(argv)
     train(a.model, a.batch, a.seq, a.steps, a.warmup, a.device, a.placement, a.discovery, a.bucket_mb, a.checkpoint, attn=a.attn,
           gemm_tuning=a.gemm_tuning, gemm_table=a.gemm_table, gemm_layout=a.gemm_layout,
-          overlap_transposes=a.overlap_transposes, zero1=a.zero1, save_dir=a.save_dir, save_every=a.save_every,
+          overlap_transposes=a.overlap_transposes, dgrad_nn=a.dgrad_nn, zero1=a.zero1, save_dir=a.save_dir, save_every=a.save_every,
           resume=a.resume, keep=a.keep, fuse_residual=not a.no_fuse_residual,
           overlap_norm=a.overlap_norm, same_data=a.same_data, graph=a.graph, conv=a.conv, cpu_bind=a.cpu_bind)
     if dist.is_initialized():

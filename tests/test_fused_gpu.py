@@ -248,6 +248,13 @@ def test_llama_nt_layout_matches_native_gpu():
         grads[(layout, overlap)] = m.flat.grad.float().clone()
     assert _rel(grads[("nt", False)], grads[("native", False)]) < 1e-2
     assert torch.equal(grads[("nt", True)], grads[("nt", False)])  # same kernels, only the stream differs
+    m = Llama(cfg, device="cuda", seed=3, gemm_layout="nt", dgrad_nn=("wqkv", "wo", "w13", "w2", "lm_head"))
+    for _ in range(2):
+        m.flat.zero_grad()
+        m(tok, torch.roll(tok, -1, 1)).backward()
+        with torch.no_grad():
+            m.flat.data.add_(m.flat.grad, alpha=-1e-2)
+    assert _rel(m.flat.grad.float(), grads[("native", False)]) < 1e-2  # NN input gradients, NT weight gradients
 
 
 def test_llama_model_gpu_matches_cpu_reference():

@@ -94,8 +94,15 @@ def test_nt_gemm_layout_matches_native():
         m(tok, torch.roll(tok, -1, 1)).backward()
         grads[layout] = m.flat.grad.float().clone()
     assert torch.allclose(grads["nt"], grads["native"], rtol=1e-2, atol=1e-5)
+    # NN input gradients for some projections (no W^T): the same gradients
+    m = Llama(cfg, device="cpu", seed=3, gemm_layout="nt", dgrad_nn=("w13", "w2", "lm_head"))
+    m.flat.zero_grad()
+    m(tok, torch.roll(tok, -1, 1)).backward()
+    assert torch.allclose(m.flat.grad.float(), grads["native"], rtol=1e-2, atol=1e-5)
     with pytest.raises(ValueError):
         Llama(cfg, device="cpu", gemm_layout="tn")
+    with pytest.raises(ValueError):
+        Llama(cfg, device="cpu", dgrad_nn=("w4",))
 
 
 def test_swiglu_bwd_ref_matches_autograd():
