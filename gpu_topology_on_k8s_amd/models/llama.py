@@ -16,7 +16,10 @@ MI355X-first layout:
     kernel (``ops.fused.transpose``) — hipBLASLt runs NT 10-40 % faster than the NN / TN layouts
     autograd would hand it (bench/gemm_layout_bench.py).  ``overlap_transposes`` makes ``x^T`` and
     ``W^T`` in the forward on a side HIP stream instead; measured on MI355X it does not pay (22.8k
-    vs 23.0k tok/s, +18 GB): the hipBLASLt GEMMs hold every CU, so the transposes only contend;
+    vs 23.0k tok/s, +18 GB): the hipBLASLt GEMMs hold every CU, so the transposes only contend.
+    ``dgrad_nn`` computes the input gradient as ``dy W`` (NN, no per-step ``W^T``) for the named
+    projections; on MI355X every projection was slower that way, 1.4-4.7 ms per step each, even with
+    the NN shapes tuned (profiles/r03_layout/SUMMARY.md), so it is an A/B knob, off by default;
   * Llama-3-8B = 8.03 B params: 16 GB bf16 weights + 16 GB bf16 grads + 96 GB fp32 master/m/v =
     128 GB, leaving ~160 GB of the 288 GB HBM for activations, so DP alone suffices (no TP/PP/SP).
 """
