@@ -271,6 +271,9 @@ def main(argv=None) -> int:
                 log.warning("partition request: %s", msg)
         if plugin.layout_change.is_set():  # partition switch / device hot-(un)plug / new slicing: restart cleanly
             log.warning("exiting for a restart: %s", plugin.layout_change_reason)
+            # the published layout is stale until the restarted plugin publishes the new one (and
+            # clears this mark): the extender keeps away from the node meanwhile
+            plugin._mark_probing(time.time() + a.probe_mark_seconds)
             plugin.stop()
             return 75  # EX_TEMPFAIL: the DaemonSet restarts the container, which re-discovers
     plugin.stop()

@@ -940,11 +940,26 @@ class DevicePluginServer:
         log.info("CDI spec for %d devices written to %s", self.topology.n, path)
         return path
 
+    def _clear_stale_mark(self) -> None:
+        """At start-up, after the node's topology is published: drop a ``<prefix>/probing`` mark the
+        previous run left (it marks the node before exiting for a layout change, so the extender
+        keeps away until this run has published the new layout)."""
+        if self.api is None or not self.cfg.node_name:
+            return
+        try:
+            ann = (self.api.get_node(self.cfg.node_name).get("metadata") or {}).get("annotations") or {}
+        except Exception:  # noqa: BLE001 - a mark left in place expires at its deadline
+            return
+        if self.cfg.contract.probing_key in ann:
+            log.info("clearing the probing mark of the previous run (new layout published)")
+            self._mark_probing(None)
+
     def start(self, register: bool = True) -> None:
         self._stop.clear()
         self.install_guard()
         self.write_cdi_spec()
         self._publish_node()
+        self._clear_stale_mark()
         self.serve()
         if register:
             self.register()

@@ -11,13 +11,14 @@ re-probe (``plugin.reprobe``):
    and preempt skip it.  After a settle window, for binds already past the extender, the node must
    still be idle;
 3. the switch itself is :func:`topology.partition.apply_partition` (amdsmi, needs root);
-4. the mark is cleared, and a Kubernetes Event records the outcome.  A refused switch (no
-   permission, a mode the package does not offer) is recorded as ``<prefix>/partition-change-failed``
-   on the node and is not tried again until the label asks for something else.
-
-On success the plugin exits 75, like any layout change, and its restart discovers the new layout.
-At start-up the switch runs before discovery, so the first registration already shows the new
-layout.
+4. a Kubernetes Event records the outcome.  A refused switch (no permission, a mode the package
+   does not offer) clears the mark and is recorded as ``<prefix>/partition-change-failed`` on the
+   node; it is not tried again until the label asks for something else.  After a switch the mark
+   stays: the node's published layout is the old one until the plugin restarts (exit 75, like any
+   layout change) and publishes the new one, and the restarted plugin clears it then
+   (``DevicePluginServer._clear_stale_mark``; the mark's deadline covers a plugin that never
+   comes back).  At start-up the switch runs before discovery, so the first registration already
+   shows the new layout.
 """
 from __future__ import annotations
 
@@ -77,6 +78,7 @@ def repartition(api, node_name: str, contract: Contract, idle_fn: Callable[[], b
     if not idle_fn():
         return "busy", f"{tag} requested; waiting until no pod holds a device"
     api.patch_node(node_name, annotations={contract.probing_key: str(int(math.ceil(clock() + mark_s)))})
+    switched = False
     try:
         if settle_s > 0 and wait(settle_s):
             return "stopped", ""
@@ -89,6 +91,7 @@ def repartition(api, node_name: str, contract: Contract, idle_fn: Callable[[], b
         except Exception as e:  # noqa: BLE001 - PartitionError, or amdsmi without the setters: recorded, not retried
             res = {"ok": False, "reason": str(e)[:500]}
         if res["ok"]:
+            switched = True
             api.patch_node(node_name, annotations={contract.partition_failed_key: None})
             _event(api, node_name, "GPUPartitionChanged", f"GPU partitions {before} -> {tag}", "Normal")
             return "ok", f"{before} -> {tag}"
@@ -96,4 +99,5 @@ def repartition(api, node_name: str, contract: Contract, idle_fn: Callable[[], b
         _event(api, node_name, "FailedGPUPartitionChange", f"{before} -> {tag}: {res['reason']}", "Warning")
         return "failed", res["reason"]
     finally:
-        api.patch_node(node_name, annotations={contract.probing_key: None})
+        if not switched:  # after a switch the restarted plugin clears it, once the new layout is published
+            api.patch_node(node_name, annotations={contract.probing_key: None})

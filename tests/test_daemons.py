@@ -212,6 +212,8 @@ def test_device_plugin_daemon_time_slices():
             p.wait(timeout=6)
         api.delete_pod("default", "half")
         assert p.wait(timeout=60) == 75
+        # the old layout stays published until the restart: the extender is told to keep away
+        assert Contract().probing_key in api.get_node("worker-1")["metadata"]["annotations"]
         return
     finally:
         rc = _stop(p)

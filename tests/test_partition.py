@@ -36,6 +36,20 @@ def _stop(p):
     return p.returncode
 
 
+def _wait_for(pred, timeout=60.0):
+    import time
+
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        try:
+            if pred():
+                return True
+        except Exception:  # noqa: BLE001 - not there yet
+            pass
+        time.sleep(0.1)
+    return False
+
+
 def _lib():
     from gpu_topology_on_k8s_amd._native import binary
 
@@ -119,7 +133,9 @@ def test_repartition_pass_marks_the_node_and_records_the_outcome(node):
 
     assert repartition(api, "w", c, idle, settle_s=0.01) == ("ok", "SPX/NPS1 -> CPX/-")
     assert marks[-1]  # the extender was told to keep away while the switch ran
-    assert c.probing_key not in (api.get_node("w")["metadata"].get("annotations") or {})
+    # ... and still is: the published layout is stale until the restarted plugin publishes the new one
+    assert c.probing_key in api.get_node("w")["metadata"]["annotations"]
+    api.patch_node("w", annotations={c.probing_key: None})  # what the restarted plugin does
     assert any(e["reason"] == "GPUPartitionChanged" for e in api.events)
     assert repartition(api, "w", c, idle)[0] == "same"
     # a busy node waits; a refused switch is recorded once and not retried until the label changes
@@ -133,6 +149,7 @@ def test_repartition_pass_marks_the_node_and_records_the_outcome(node):
         assert repartition(api, "w", c, idle, settle_s=0)[0] == "skipped"
     finally:
         del os.environ["FAKE_AMDSMI_SET_STATUS"]
+    assert c.probing_key not in api.get_node("w")["metadata"]["annotations"]  # a refusal clears the mark
     api.patch_node("w", labels={c.partition_request_label: "DPX"})
     assert repartition(api, "w", c, idle, settle_s=0)[0] == "ok"
     assert c.partition_failed_key not in api.get_node("w")["metadata"]["annotations"]
@@ -173,6 +190,13 @@ def test_device_plugin_daemon_repartitions_on_the_node_label(node):
         api.delete_pod("default", "x")
         assert p.wait(timeout=60) == 75
         assert node["state"].read_text().split()[0] == "1"
+        assert c.probing_key in api.get_node("worker-1")["metadata"]["annotations"]  # until the restart publishes SPX
+        p = _spawn(["gpu_topology_on_k8s_amd.deviceplugin", "--discovery", "amdsmi", "--partition-control", "on",
+                    "--gpu-events", "off", "--device-specs", "stub", "--apiserver", url, "--node-name", "worker-1",
+                    "--socket-dir", sockdir, "--dev-root", devroot, "--log-level", "WARNING"])
+        assert _wait_for(lambda: len(kubelet.plugins.get("amd.com/gpu").devices) == 2 if "amd.com/gpu" in kubelet.plugins else False)
+        md = api.get_node("worker-1")["metadata"]
+        assert md["labels"][c.label_partition] == "SPX" and c.probing_key not in md["annotations"]
         assert [e["reason"] for e in api.events if "Partition" in e["reason"]] == ["GPUPartitionChanged"] * 2
     finally:
         _stop(p)
