@@ -173,7 +173,8 @@ def main(argv=None) -> int:
         from .repartition import repartition
 
         outcome, msg = repartition(api, a.node_name, contract, idle_fn, reload_driver=a.partition_driver_reload,
-                                   settle_s=a.probe_settle_seconds, wait=wait)
+                                   settle_s=a.probe_settle_seconds, wait=wait,
+                                   time_slices=node_time_slices(api, a.node_name, contract, a.time_slices))
         if outcome in ("ok", "failed", "invalid"):
             (log.warning if outcome != "ok" else log.info)("partition request: %s: %s", outcome, msg)
         return outcome, msg
@@ -187,6 +188,15 @@ def main(argv=None) -> int:
                                              (a.resource_name, a.slice_resource_name, "aliyun.com/gpu", "aliyun.com/gpu-count"))
     if why:
         log.warning("%s", why)
+    if a.time_slices > 1:
+        try:
+            parts = discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus)
+            if any(g.physical != g.index for g in parts.gpus):
+                log.error("time slices (%d per GPU) need SPX GPUs, and this node is partitioned (%s): advertising its "
+                          "XCPs unsliced", a.time_slices, parts.gpus[0].partition)
+                a.time_slices = 1
+        except Exception as e:  # noqa: BLE001 - discovery fails again below, with its own error
+            log.warning("discovery before slicing failed: %s", e)
     # a sliced node is a pool of its own: it registers its slices under the slice resource and
     # offers no whole GPUs (the extender's filter keeps the two kinds of request apart)
     advertised = a.slice_resource_name if a.time_slices > 1 else a.resource_name

@@ -50,7 +50,7 @@ def _event(api, node_name: str, reason: str, msg: str, type_: str) -> None:
 
 
 def repartition(api, node_name: str, contract: Contract, idle_fn: Callable[[], bool], lib: Optional[str] = None,
-                reload_driver: bool = False, settle_s: float = 2.0, mark_s: float = 600.0,
+                reload_driver: bool = False, settle_s: float = 2.0, mark_s: float = 600.0, time_slices: int = 1,
                 wait: Callable[[float], bool] = lambda s: (time.sleep(s), False)[1],
                 clock: Callable[[], float] = time.time) -> Tuple[str, str]:
     """One reconciliation pass.  -> (outcome, message), outcome one of
@@ -75,6 +75,13 @@ def repartition(api, node_name: str, contract: Contract, idle_fn: Callable[[], b
     failed = ((node.get("metadata") or {}).get("annotations") or {}).get(contract.partition_failed_key, "")
     if failed.startswith(tag + ":"):
         return "skipped", f"{tag} failed before ({failed[len(tag) + 1:].strip()}); change the label to try again"
+    if want_c and want_c != "SPX" and time_slices > 1:
+        # time slices split whole (SPX) GPUs; the two kinds of fraction are not stacked
+        why = (f"the node is time-sliced ({time_slices} per GPU, {contract.time_slices_label}): remove that label "
+               "before asking for XCP partitions")
+        api.patch_node(node_name, annotations={contract.partition_failed_key: f"{tag}: {why}"})
+        _event(api, node_name, "FailedGPUPartitionChange", f"{tag}: {why}", "Warning")
+        return "failed", why
     if not idle_fn():
         return "busy", f"{tag} requested; waiting until no pod holds a device"
     api.patch_node(node_name, annotations={contract.probing_key: str(int(math.ceil(clock() + mark_s)))})

@@ -233,3 +233,36 @@ def test_manifests_with_partition_control_mount_sys_writable():
     assert "--partition-control=on" not in off["command"] and "--partition-control=on" in on["command"]
     sys_mount = lambda c: next(m for m in c["volumeMounts"] if m["name"] == "sys")  # noqa: E731
     assert sys_mount(off)["readOnly"] is True and sys_mount(on)["readOnly"] is False
+
+
+def test_partitions_and_time_slices_are_not_stacked(node):
+    """A time-sliced node refuses an XCP partition request (recorded, no hardware touched); a
+    partitioned node started with --time-slices advertises its XCPs unsliced instead of crashing."""
+    from gpu_topology_on_k8s_amd.deviceplugin.repartition import repartition
+
+    c = Contract()
+    api = FakeAPIServer()
+    api.create_node(make_node("w", labels={c.partition_request_label: "CPX", c.time_slices_label: "4"}))
+    out, msg = repartition(api, "w", c, lambda: True, settle_s=0, time_slices=4)
+    assert out == "failed" and "time-sliced" in msg and node["state"].read_text().split()[0] == "1"
+    assert api.get_node("w")["metadata"]["annotations"][c.partition_failed_key].startswith("CPX/-: ")
+    assert repartition(api, "w", c, lambda: True, time_slices=4)[0] == "skipped"
+
+    from gpu_topology_on_k8s_amd.deviceplugin import FakeKubelet
+
+    node["state"].write_text("8 NPS1 -\n")  # the node is CPX already
+    srv, url = serve_http(api)
+    sockdir = tempfile.mkdtemp(prefix="gtkq", dir="/tmp")
+    kubelet = FakeKubelet(sockdir, node_name="w", api=api)
+    kubelet.start()
+    p = _spawn(["gpu_topology_on_k8s_amd.deviceplugin", "--discovery", "amdsmi", "--gpu-events", "off", "--device-specs", "stub",
+                "--apiserver", url, "--node-name", "w", "--socket-dir", sockdir, "--dev-root", sockdir, "--log-level", "ERROR"])
+    try:
+        plug = kubelet.wait_for("amd.com/gpu", timeout=60)  # the XCPs, as whole devices of their own
+        assert len(plug.devices) == 16 and "amd.com/gpu-slice" not in kubelet.plugins
+        assert p.poll() is None
+    finally:
+        _stop(p)
+        kubelet.stop()
+        srv.shutdown()
+        shutil.rmtree(sockdir, ignore_errors=True)
