@@ -269,11 +269,16 @@ def main(argv=None) -> int:
                     log.warning("time slices per GPU %d -> %d requested by the node label; waiting until no pod holds a device",
                                 a.time_slices, want)
         if partition_control and ticks % max(1, int(a.label_check_interval)) == 0 and not plugin.layout_change.is_set():
-            try:
-                outcome, msg = repartition_pass(plugin.node_idle, done.wait)
-            except Exception as e:  # noqa: BLE001 - reported; the next pass tries again
-                outcome, msg = "error", str(e)
-                log.warning("partition request: %s", e)
+            if not plugin.maintenance.acquire(blocking=False):
+                outcome, msg = "busy", "a link re-probe holds the GPUs"
+            else:
+                try:
+                    outcome, msg = repartition_pass(plugin.node_idle, done.wait)
+                except Exception as e:  # noqa: BLE001 - reported; the next pass tries again
+                    outcome, msg = "error", str(e)
+                    log.warning("partition request: %s", e)
+                finally:
+                    plugin.maintenance.release()
             if outcome == "ok":
                 plugin.layout_change_reason = f"GPU partitions {msg} (node label)"
                 plugin.layout_change.set()

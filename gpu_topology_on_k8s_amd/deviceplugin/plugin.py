@@ -224,6 +224,9 @@ class DevicePluginServer:
         self._threads: List[threading.Thread] = []
         self._alloc_lock = threading.Lock()
         self._alloc_cond = threading.Condition(self._alloc_lock)  # Allocate waits here for a probe to yield
+        # one maintenance operation on the GPUs at a time: an idle-time re-probe (a HIP child on every
+        # GPU) and a partition switch (deviceplugin/repartition.py) must never overlap
+        self.maintenance = threading.Lock()
         self._probing = False  # set (under _alloc_lock) while an idle-time re-probe owns the links
         self._cancel = threading.Event()  # set by an Allocate arriving mid-probe: the probe stops
         self._guard_ready = False  # install_guard() put libgtk_vgpu.so into cfg.guard_dir
@@ -361,6 +364,15 @@ class DevicePluginServer:
              traffic would skew the matrix)."""
         if self.reprobe_fn is None:
             return False
+        if not self.maintenance.acquire(blocking=False):  # a partition switch holds the GPUs
+            self.metrics.reprobes.labels("busy").inc()
+            return False
+        try:
+            return self._reprobe_locked()
+        finally:
+            self.maintenance.release()
+
+    def _reprobe_locked(self) -> bool:
         if not self.node_idle():
             self.metrics.reprobes.labels("busy").inc()
             return False

@@ -239,3 +239,20 @@ def test_device_ids_that_are_not_indices_are_refused_as_invalid_argument(tmp_pat
     assert e.value.args[0] == grpc.StatusCode.INVALID_ARGUMENT
     ok = plug.Allocate(pb.AllocateRequest(container_requests=[pb.ContainerAllocateRequest(devices_ids=["2"])]), Ctx())
     assert ok.container_responses[0].envs["GTK_GPU_GROUP"] == "2"
+
+
+def test_reprobe_never_overlaps_another_maintenance_operation(tmp_path):
+    """A partition switch (deviceplugin/repartition.py) holds ``plugin.maintenance``; a re-probe that
+    comes due meanwhile is skipped, not run against GPUs being reconfigured."""
+    api = FakeAPIServer()
+    api.create_node(make_node("n1"))
+    t = _probed(fx.f7_mi355x(n=4))
+    probe = BlockingProbe(_probed(fx.f7_mi355x(n=4)))
+    probe.release.set()
+    plug = DevicePluginServer(t, PluginConfig(node_name="n1", dev_root=placeholder_dev_tree(str(tmp_path), t), probe_settle_s=0.0),
+                              api=api, reprobe_fn=probe)
+    with plug.maintenance:
+        assert plug.reprobe() is False and not probe.started.is_set()
+    assert 'gtk_plugin_reprobes_total{result="busy"} 1.0' in plug.metrics.exposition().decode()
+    plug.reprobe()
+    assert probe.started.is_set()
