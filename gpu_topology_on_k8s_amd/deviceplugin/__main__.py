@@ -279,6 +279,8 @@ def main(argv=None) -> int:
                     log.warning("partition request: %s", e)
                 finally:
                     plugin.maintenance.release()
+            if outcome not in ("none", "same"):
+                plugin.metrics.partition_changes.labels(outcome).inc()
             if outcome == "ok":
                 plugin.layout_change_reason = f"GPU partitions {msg} (node label)"
                 plugin.layout_change.set()

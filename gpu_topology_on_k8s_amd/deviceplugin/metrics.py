@@ -35,6 +35,9 @@ class PluginMetrics:
         self.link_gbps = Gauge("gtk_plugin_link_read_gbps", "measured p2p read GB/s over the published matrix", ["stat"],
                                registry=r)
         self.reprobes = Counter("gtk_plugin_reprobes_total", "idle-time link re-measurements by result", ["result"], registry=r)
+        self.partition_changes = Counter("gtk_plugin_partition_changes_total",
+                                         "operator-requested GPU partition switches by outcome (ok, failed, skipped, busy)",
+                                         ["outcome"], registry=r)
         self.guarded = Counter("gtk_plugin_guarded_containers_total",
                                "containers holding part of a GPU given the vGPU guard (HBM cap + forced CU mask)", registry=r)
         self.gpu_events = Counter("gtk_plugin_gpu_events_total", "amdsmi GPU event notifications by kind", ["kind"], registry=r)
