@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--h", type=int, default=32)
     ap.add_argument("--hkv", type=int, default=8)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--ab", type=int, default=0,
+                    help="interleaved A/B of the backward variants: N rounds, one call of each per round, "
+                         "event-timed, medians (clock drift hits every variant alike)")
     a = ap.parse_args()
     B, S, H, Hkv, Dh = a.b, a.s, a.h, a.hkv, 128
     q = torch.randn(B, H, S, Dh, device="cuda", dtype=torch.bfloat16)
@@ -56,12 +59,29 @@ def main():
     t = timeit(lambda: hip.attn_bwd(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
     res["hip_bwd_ms"] = t * 1e3
     res["hip_bwd_tflops"] = 2.5 * fwd_flops / t / 1e12
+    if hasattr(hip, "attn_bwd_v4"):
+        t = timeit(lambda: hip.attn_bwd_v4(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
+        res["hip_bwd_v4_ms"] = t * 1e3
     if hasattr(hip, "attn_bwd_v3"):
         t = timeit(lambda: hip.attn_bwd_v3(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
         res["hip_bwd_v3_ms"] = t * 1e3
     if hasattr(hip, "attn_bwd_v2"):
         t = timeit(lambda: hip.attn_bwd_v2(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
         res["hip_bwd_v2_ms"] = t * 1e3
+    if a.ab:
+        variants = {n: getattr(hip, n) for n in ("attn_bwd", "attn_bwd_v4", "attn_bwd_v3") if hasattr(hip, n)}
+        times = {n: [] for n in variants}
+        for fn in variants.values():
+            fn(do, q, k, v, o, lse, Dh ** -0.5)
+        for _ in range(a.ab):
+            for n, fn in variants.items():
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn(do, q, k, v, o, lse, Dh ** -0.5)
+                e1.record()
+                times[n].append((e0, e1))
+        torch.cuda.synchronize()
+        res["ab_median_ms"] = {n: sorted(x.elapsed_time(y) for x, y in ts)[len(ts) // 2] for n, ts in times.items()}
     try:
         t = timeit(lambda: F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True), a.iters)
         res["sdpa_fwd_ms"] = t * 1e3

@@ -639,6 +639,183 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv4_kernel(const u16* __res
     }
 }
 
+// dK/dV v5: v4 with its LDS operands read AHEAD, into registers, before the next slice's LDS-DMA
+// is issued.  The v4 ISA (hipcc -S, ROCm 7.2) showed one wave per SIMD (460 VGPR+AGPR) waiting on
+// every fragment: each MFMA sat behind its own `ds_read; s_waitcnt lgkmcnt(0)`, and the compiler put
+// an `s_waitcnt vmcnt(0)` (the next slice's DMA) in front of the first transposed read of the
+// previous slot, since it cannot prove that read disjoint from the DMA target.  Here a step
+//   1. reads everything it will consume from LDS: the previous slice's dO^T / Q^T fragments (the
+//      deferred dV/dK products), this slice's lse / delta and its Q / dO fragments;
+//   2. only then issues the next slice's LDS-DMA (nothing after it reads LDS until the barrier);
+//   3. runs S and dP, then the softmax / dS VALU interleaved with the deferred dV/dK MFMAs, whose
+//      operands are all in registers already.
+// Same MFMAs in the same order per accumulator as v4, so the results are bit-identical.
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv5_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
+                                                                const u16* __restrict__ v, const u16* __restrict__ dout,
+                                                                const float* __restrict__ lse2, const float* __restrict__ delta,
+                                                                u16* __restrict__ dk, u16* __restrict__ dv, int H, int Hkv,
+                                                                int S, float c, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[3 * SL_BYTES];  // slice ring
+  const int t = threadIdx.x, lane = t & 63, r = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int kb = blockIdx.y;
+  const int bk = xcd_head(blockIdx.x, gridDim.x), b = bk / Hkv, hk = bk % Hkv, G = H / Hkv;
+  const size_t kvoff = ((size_t)(b * Hkv + hk) * S + (size_t)kb * KB) * D;
+  const int krow = w * 32 + r, mykey = kb * KB + krow, kmin = kb * KB + w * 32;
+  bf16x8 kf[8], vf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    kf[s] = *reinterpret_cast<const bf16x8*>(k + kvoff + (size_t)krow * D + 16 * s + 8 * hh);
+    vf[s] = *reinterpret_cast<const bf16x8*>(v + kvoff + (size_t)krow * D + 16 * s + 8 * hh);
+  }
+  f32x16 dvt[4], dkt[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dvt[dt] = dkt[dt] = f32x16{};
+  const int qt0 = (kb * KB) / QT, nqt = S / QT - qt0, nslice = G * nqt;
+
+  const uint32_t qbytes = (uint32_t)((size_t)H * S * D * 2), dbytes = (uint32_t)((size_t)S * H * D * 2);
+  const auto qrs = __builtin_amdgcn_make_buffer_rsrc((void*)(q + (size_t)b * H * S * D), 0, qbytes, 0x00020000);
+  const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)(dout + (size_t)b * S * H * D), 0, dbytes, 0x00020000);
+  const auto lrs = __builtin_amdgcn_make_buffer_rsrc((void*)((w == 0 ? lse2 : delta) + (size_t)b * H * S), 0,
+                                                     (uint32_t)((size_t)H * S * 4), 0x00020000);
+  uint32_t qv[2], dvo[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int R = 8 * w + 4 * i + (lane >> 4);
+    const uint32_t ch16 = 16 * ((lane & 15) ^ (((R & 3) << 2) | ((R >> 2) & 3)));
+    qv[i] = (uint32_t)(R * D * 2) + ch16;
+    dvo[i] = (uint32_t)(R * H * D * 2) + ch16;
+  }
+  auto sload = [&](int idx, char* buf) {
+    const int hq = hk * G + idx / nqt, qbase = (qt0 + idx % nqt) * QT;
+    const uint32_t qs = (uint32_t)(((size_t)hq * S + qbase) * D * 2), ds = (uint32_t)(((size_t)qbase * H + hq) * D * 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (LDS_AS void*)(buf + SL_Q + (8 * w + 4 * i) * 256), 16, qv[i], qs, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, (LDS_AS void*)(buf + SL_DO + (8 * w + 4 * i) * 256), 16, dvo[i], ds, 0, 0);
+    }
+    if (w < 2)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, (LDS_AS void*)(buf + (w == 0 ? SL_LSE : SL_DEL)), 4, 4 * lane,
+                                               (uint32_t)(((size_t)hq * S + qbase) * 4), 0, 0);
+  };
+  auto active = [&](int idx) {
+    const int j = idx % nqt;
+    return j >= KB / QT || (qt0 + j) * QT + QT - 1 >= kmin;
+  };
+  auto masked = [&](int idx) { return idx % nqt < KB / QT; };
+  struct Packs {
+    bf16x8 p0, p1, d0, d1;
+  };
+
+  Packs prev{};
+  {  // the first step's deferred products read ring(2): zeros, not stale LDS bits
+    u16x8* z = reinterpret_cast<u16x8*>(smem + 2 * SL_BYTES);
+    for (int i = t; i < SL_BYTES / 16; i += 256) z[i] = u16x8{};
+  }
+  __syncthreads();
+  sload(0, smem);
+  dma_sync();
+  auto step = [&](int idx, const int rb) {
+    const char* buf = smem + rb * SL_BYTES;
+    const char* pbuf = smem + ((rb + 2) % 3) * SL_BYTES;  // slice idx-1 (its deferred dV/dK products)
+    // (1) every LDS operand of this step, while no DMA is outstanding
+    bf16x8 ta[16];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      ta[4 * dt + 0] = tr_frag(pbuf + SL_DO, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt);
+      ta[4 * dt + 1] = tr_frag(pbuf + SL_DO, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt);
+      ta[4 * dt + 2] = tr_frag(pbuf + SL_Q, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt);
+      ta[4 * dt + 3] = tr_frag(pbuf + SL_Q, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt);
+    }
+    f32x4 lq[4], dq[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      lq[g] = *reinterpret_cast<const f32x4*>(buf + SL_LSE + 4 * (8 * g + 4 * hh));
+      dq[g] = *reinterpret_cast<const f32x4*>(buf + SL_DEL + 4 * (8 * g + 4 * hh));
+    }
+    bf16x8 qa[8], da[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      qa[s] = lds_b128(buf + SL_Q, swz(r, 2 * s + hh));
+      da[s] = lds_b128(buf + SL_DO, swz(r, 2 * s + hh));
+    }
+    // (2) the next slice lands in slot (rb+1)%3 = slice idx-2's, read for the last time last step
+    if (idx + 1 < nslice) sload(idx + 1, smem + ((rb + 1) % 3) * SL_BYTES);
+    const int j = idx % nqt;
+    const int qbase = (qt0 + j) * QT;
+    const bool dead = !active(idx);
+    const int kill_from = dead ? -(1 << 30) : (masked(idx) ? qbase : 1 << 30);
+    // (3) S and dP
+    f32x16 sacc = f32x16{}, dpacc = f32x16{};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      sacc = mfma(qa[s], kf[s], sacc);
+      dpacc = mfma(da[s], vf[s], dpacc);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // (4) softmax / dS of this slice under the deferred dV/dK MFMAs of the previous one
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * g + e;
+        float pv = fexp2(fmaf(sacc[i], c, -lq[g][e]));
+        pv = (mykey - crow(i, hh) > kill_from) ? 0.f : pv;
+        sacc[i] = pv;
+        dpacc[i] = pv * (dpacc[i] - dq[g][e]);
+      }
+    const Packs cur{pack8(sacc, 0), pack8(sacc, 8), pack8(dpacc, 0), pack8(dpacc, 8)};
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      dvt[dt] = mfma(ta[4 * dt + 0], prev.p0, dvt[dt]);
+      dvt[dt] = mfma(ta[4 * dt + 1], prev.p1, dvt[dt]);
+      dkt[dt] = mfma(ta[4 * dt + 2], prev.d0, dkt[dt]);
+      dkt[dt] = mfma(ta[4 * dt + 3], prev.d1, dkt[dt]);
+    }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {  // {1 dV/dK MFMA, 7 softmax VALU} x 16
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    prev = cur;
+    dma_sync();
+  };
+  int idx = 0;
+  for (; idx + 3 <= nslice; idx += 3) {
+    step(idx, 0);
+    step(idx + 1, 1);
+    step(idx + 2, 2);
+  }
+  if (idx < nslice) step(idx, 0);
+  if (idx + 1 < nslice) step(idx + 1, 1);
+  {  // the last slice's deferred dV/dK products
+    const char* pbuf = smem + ((nslice - 1) % 3) * SL_BYTES;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      dvt[dt] = mfma(tr_frag(pbuf + SL_DO, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), prev.p0, dvt[dt]);
+      dvt[dt] = mfma(tr_frag(pbuf + SL_DO, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), prev.p1, dvt[dt]);
+      dkt[dt] = mfma(tr_frag(pbuf + SL_Q, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), prev.d0, dkt[dt]);
+      dkt[dt] = mfma(tr_frag(pbuf + SL_Q, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), prev.d1, dkt[dt]);
+    }
+  }
+  u16* dkrow = dk + ((size_t)(b * Hkv + hk) * S + mykey) * D;
+  u16* dvrow = dv + ((size_t)(b * Hkv + hk) * S + mykey) * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u16x4 a4, b4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a4[e] = f2bf(dkt[dt][4 * g4 + e] * scale);
+        b4[e] = f2bf(dvt[dt][4 * g4 + e]);
+      }
+      *reinterpret_cast<u16x4*>(dkrow + 32 * dt + 8 * g4 + 4 * hh) = a4;
+      *reinterpret_cast<u16x4*>(dvrow + 32 * dt + 8 * g4 + 4 * hh) = b4;
+    }
+}
+
 // dQ v2: the forward-shaped dQ kernel restructured like forward v2 — LDS-DMA double-buffered K/V tiles with
 // one barrier per tile, the block's diagonal tiles peeled out of a branch-free main loop, LPT +
 // XCD-grouped grid (B*H, S/128).  (Forcing the fragment reads ahead with sched_group_barrier spills
@@ -785,7 +962,27 @@ std::vector<at::Tensor> attn_bwd_v3(const at::Tensor& dout, const at::Tensor& q,
   return {dq, dk, dv};
 }
 
-// default backward: delta, dK/dV v4 (software-pipelined slices), dQ v2
+// v4 dK/dV (LDS operands read at their use, under the next slice's DMA) + dQ v2: A/B reference for v5
+std::vector<at::Tensor> attn_bwd_v4(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                    const at::Tensor& out, const at::Tensor& lse, double scale) {
+  check_qkv(q, k, v);
+  const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
+  TORCH_CHECK(dout.is_contiguous() && out.is_contiguous() && dout.numel() == q.numel() && out.numel() == q.numel(),
+              "attention bwd: dout/out must be contiguous [B, S, H, D]");
+  auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+  auto dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
+  const int rows = B * S * H;
+  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
+                     delta.data_ptr<float>(), B, H, S);
+  const float c = (float)(scale * 1.4426950408889634);
+  hipLaunchKernelGGL(attn_bwd_dkdv4_kernel, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
+                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
+  hipLaunchKernelGGL(attn_bwd_dq2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
+                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
+  return {dq, dk, dv};
+}
+
+// default backward: delta, dK/dV v5 (software-pipelined slices, operands read ahead of the DMA), dQ v2
 std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                  const at::Tensor& out, const at::Tensor& lse, double scale) {
   check_qkv(q, k, v);
@@ -798,7 +995,7 @@ std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, co
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
                      delta.data_ptr<float>(), B, H, S);
   const float c = (float)(scale * 1.4426950408889634);
-  hipLaunchKernelGGL(attn_bwd_dkdv4_kernel, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
+  hipLaunchKernelGGL(attn_bwd_dkdv5_kernel, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
                      lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
   hipLaunchKernelGGL(attn_bwd_dq2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
                      lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);

@@ -896,6 +896,8 @@ namespace gtk_attn {  // csrc/ops/attention.hip
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale);
 std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                  const at::Tensor& out, const at::Tensor& lse, double scale);
+std::vector<at::Tensor> attn_bwd_v4(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                    const at::Tensor& out, const at::Tensor& lse, double scale);
 std::vector<at::Tensor> attn_bwd_v3(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                     const at::Tensor& out, const at::Tensor& lse, double scale);
 }  // namespace gtk_attn
@@ -907,6 +909,7 @@ at::Tensor transpose_bf16(const at::Tensor& x);
 PYBIND11_MODULE(_fused, m) {
   m.def("attn_fwd", &gtk_attn::attn_fwd, "causal GQA flash attention forward (bf16, D=128): -> (o [B,S,H,D], lse2 [B,H,S])");
   m.def("attn_bwd", &gtk_attn::attn_bwd, "flash attention backward: -> (dq, dk, dv)");
+  m.def("attn_bwd_v4", &gtk_attn::attn_bwd_v4, "v4 backward (dK/dV LDS operands read at their use; A/B reference for the default v5)");
   m.def("attn_bwd_v3", &gtk_attn::attn_bwd_v3, "v3 backward (dK/dV not pipelined across slices; A/B reference for v4)");
   m.doc() = "gfx950 fused kernels for the Llama-3 DP validation workload";
   m.def("rmsnorm_fwd", &rmsnorm_fwd);

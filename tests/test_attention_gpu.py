@@ -62,8 +62,9 @@ def test_attention_backward(fused, B, H, Hkv, S):
 
 @pytest.mark.parametrize("B,H,Hkv,S", [(2, 8, 2, 768), (1, 4, 4, 128), (1, 32, 8, 1024), (2, 4, 1, 384)])
 def test_attention_bwd_v4_matches_v3(fused, B, H, Hkv, S):
-    """dK/dV v4 (the default: slices software-pipelined through a 3-buffer ring, branch-free) does
-    v3's arithmetic in v3's order: identical bits, including the all-diagonal S=128 case, MHA
+    """dK/dV v4 (slices software-pipelined through a 3-buffer ring, branch-free) and v5 (the default:
+    v4 with every LDS operand read before the next slice's DMA) do v3's arithmetic in v3's order:
+    identical bits, including the all-diagonal S=128 case, MHA
     (G=1), G=4 and G=8, and slice counts that are not multiples of the ring length."""
     torch.manual_seed(5)
     q = torch.randn(B, H, S, 128, device="cuda", dtype=torch.bfloat16)
@@ -73,9 +74,12 @@ def test_attention_bwd_v4_matches_v3(fused, B, H, Hkv, S):
     hip = fused.hip()
     o, lse = hip.attn_fwd(q, k, v, 128 ** -0.5)
     g3 = hip.attn_bwd_v3(do, q, k, v, o, lse, 128 ** -0.5)
-    g4 = hip.attn_bwd(do, q, k, v, o, lse, 128 ** -0.5)
-    for name, a, b in zip(("dq", "dk", "dv"), g4, g3):
+    g5 = hip.attn_bwd(do, q, k, v, o, lse, 128 ** -0.5)  # the default, v5: operands read ahead of the DMA
+    for name, a, b in zip(("dq", "dk", "dv"), g5, g3):
         assert torch.equal(a, b), (name, _rel(a, b))
+    g4 = hip.attn_bwd_v4(do, q, k, v, o, lse, 128 ** -0.5)  # v4: operands read at their use
+    for name, a, b in zip(("dq", "dk", "dv"), g4, g3):
+        assert torch.equal(a, b), (name, "v4", _rel(a, b))
 
 
 @pytest.mark.parametrize("B,H,Hkv,S", [(2, 8, 2, 768), (1, 4, 4, 128), (1, 2, 2, 640)])
