@@ -10,9 +10,10 @@ BASELINE.json metric: "RCCL all-reduce bus GB/s on scheduler-chosen k-GPU subset
 One *step* = one out-of-place RCCL all-reduce (bf16, sum) of ``--size-mb`` MiB per GPU over the
 subset the placement core picked from the node's discovered xGMI topology (rank r runs on
 ``subset[r]``).  Exactly K steps are timed between barrier + ``torch.cuda.synchronize()`` on both
-sides; the max over ranks is reported.  ``value`` is busBW = algBW * 2(k-1)/k (nccl-tests
-convention) for k >= 2; at k = 1 busBW is 0 by definition, so ``value`` is the algBW of the
-single-rank RCCL all-reduce (BASELINE.md "k=1 reports algBW only").  Per-GPU message size is fixed
+sides; the max over ranks is reported.  ``busbw_gbps`` is the per-rank busBW = algBW * 2(k-1)/k
+(nccl-tests convention); ``value`` is the whole-job aggregate the bench contract asks for, the
+busBW of all k ranks summed (k * busbw_gbps) for k >= 2.  At k = 1 busBW is 0 by definition, so
+``value`` is the algBW of the single-rank RCCL all-reduce (BASELINE.md "k=1 reports algBW only").  Per-GPU message size is fixed
 as N grows ("weak" scaling).  Data is synthetic (exactly checked once before timing).
 """
 from __future__ import annotations
@@ -508,7 +509,9 @@ def main(argv=None) -> int:
     ms_per_step = elapsed / max(1, args.steps) * 1e3
     algbw = runner.nbytes / (ms_per_step / 1e3) / 1e9  # headline size (the sweep below resizes)
     busbw = algbw * bus_factor(env.world)
-    value = busbw if env.world > 1 else algbw
+    # whole-job aggregate (the bench contract): every rank's busBW summed, i.e. k x the per-rank
+    # nccl-tests busBW (busbw_gbps below); at k = 1 busBW is 0 and the one rank's algBW is the value
+    value = busbw * env.world if env.world > 1 else algbw
     headline_bytes = runner.nbytes
     step_s = ms_per_step / 1e3
     sweep = None
@@ -618,9 +621,11 @@ def main(argv=None) -> int:
             "graph_latency": graph,
             "rccl": rccl,
             "worst_subset_ab": worst_ab,
-            "placement_gain": (round(value / worst_ab[("busbw_gbps" if env.world > 1 else "algbw_gbps")], 4)
+            "placement_gain": (round((busbw if env.world > 1 else algbw)
+                                     / worst_ab[("busbw_gbps" if env.world > 1 else "algbw_gbps")], 4)
                                if worst_ab and worst_ab.get(("busbw_gbps" if env.world > 1 else "algbw_gbps")) else None),
-            "value_kind": "busbw" if env.world > 1 else "algbw (busbw = 0 at k=1)",
+            "value_kind": ("aggregate busbw (k x per-rank busbw_gbps)" if env.world > 1
+                           else "algbw (busbw = 0 at k=1)"),
             "busbw_vs_probe_bound": round(busbw / bound, 4) if bound else None,
             "probe_bound_kind": "k6-ring" if ring_bound else ("k5-ingress" if ingress else None),
             "algbw_gbps": round(algbw, 3),

@@ -30,6 +30,7 @@ def test_bench_two_ranks_gloo():
     assert out["higher_is_better"] is True and out["scaling"] == "weak"
     assert len(set(out["config"]["subset"])) == 2
     assert out["value"] > 0 and abs(out["busbw_gbps"] - out["algbw_gbps"]) < 1e-3 * out["algbw_gbps"] + 1e-6  # 2(k-1)/k = 1
+    assert abs(out["value"] - 2 * out["busbw_gbps"]) <= 1e-2 * out["value"] + 2e-3  # whole-job aggregate of 2 ranks
     assert out["config"]["parallelism"] == "dp2"
     assert out["config"]["message_bytes_per_gpu"] == 1 << 20
     k8s = out["k8s_placement"]  # placed through device plugin + extender + kubelet Allocate
@@ -122,7 +123,8 @@ def test_bench_eight_ranks_gloo_dry_run():
     assert sorted(out["config"]["subset"]) == list(range(8)) and out["config"]["worst_subset"] is None
     assert out["k8s_placement"]["assigned"] is True and len(out["k8s_placement"]["devices"]) == 8
     assert abs(out["busbw_gbps"] - out["algbw_gbps"] * 2 * 7 / 8) <= 1e-2 * out["busbw_gbps"] + 2e-3  # 3-decimal rounding
-    assert out["size_sweep"]["all_exact"] and out["value_kind"] == "busbw"
+    assert out["size_sweep"]["all_exact"] and out["value_kind"].startswith("aggregate busbw")
+    assert abs(out["value"] - 8 * out["busbw_gbps"]) <= 1e-2 * out["value"] + 2e-2  # every rank's busBW summed
     ph = out["phase_s"]  # the first 8-GPU run explains itself: where its wall time went
     for key in ("place", "comm", "check", "warmup", "headline", "sweep", "total"):
         assert key in ph and ph[key] >= 0, ph

@@ -115,7 +115,7 @@ def test_ring_probe_bounded_by_its_links():
 def test_bench_two_gpus_native_exact_and_bounded():
     out = _run(["bench.py", "--gpus", "2", "--steps", "5", "--warmup", "2", "--size-mb", "256", "--sweep", "8:64M:64",
                 "--ctas", "default"])
-    assert out["n_gpus"] == 2 and out["value_kind"] == "busbw" and out["config"]["backend"] == "native"
+    assert out["n_gpus"] == 2 and out["value_kind"].startswith("aggregate busbw") and out["config"]["backend"] == "native"
     assert out["size_sweep"]["all_exact"]
     assert len(set(out["config"]["hip_devices"])) == 2
     # RCCL's own log: every ring edge rides xGMI peer access (no SHM / host staging, no NET)
