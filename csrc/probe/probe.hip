@@ -726,12 +726,136 @@ class IpcBuffer {
   py::bytes handle() const { return py::bytes(reinterpret_cast<const char*>(&h_), sizeof(h_)); }
   size_t bytes() const { return buf_.bytes; }
   unsigned int seed() const { return seed_; }
+  // After a peer wrote into this buffer through its mapping (K2 over IPC): does it hold pattern(seed)?
+  bool holds(unsigned int seed) const {
+    py::gil_scoped_release nogil;
+    return verify_pattern(buf_, buf_.bytes / 4, seed);
+  }
 
  private:
   DevBuf buf_;
   unsigned int seed_;
   hipIpcMemHandle_t h_{};
 };
+
+// Opens another process's buffers by handle for the lifetime of the object.
+struct IpcMappings {
+  std::vector<void*> p;
+  IpcMappings(const std::vector<py::bytes>& handles, int dev) {
+    DeviceGuard g(dev);
+    for (const py::bytes& hb : handles) {
+      const std::string raw = hb;
+      if (raw.size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("not a hipIpcMemHandle_t");
+      hipIpcMemHandle_t h;
+      std::memcpy(&h, raw.data(), sizeof(h));
+      void* q = nullptr;
+      HIP_CHECK(hipIpcOpenMemHandle(&q, h, hipIpcMemLazyEnablePeerAccess));
+      p.push_back(q);
+    }
+  }
+  ~IpcMappings() {
+    for (void* q : p) (void)hipIpcCloseMemHandle(q);
+  }
+  IpcMappings(const IpcMappings&) = delete;
+  IpcMappings& operator=(const IpcMappings&) = delete;
+};
+
+// Event-timed `iters` launches of `launch` on a fresh non-blocking stream (after `warmup` untimed).
+template <class F>
+float time_launches(F launch, int iters, int warmup) {
+  hipStream_t s;
+  HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipEvent_t e0, e1;
+  HIP_CHECK(hipEventCreate(&e0));
+  HIP_CHECK(hipEventCreate(&e1));
+  for (int i = 0; i < warmup; ++i) launch(s);
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipEventRecord(e0, s));
+  for (int i = 0; i < iters; ++i) launch(s);
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipEventRecord(e1, s));
+  HIP_CHECK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipStreamDestroy(s);
+  return ms;
+}
+
+// K2 over IPC: the writer's kernel pushes a local patterned buffer into another process's buffer
+// through the imported mapping (remote stores, the direction RCCL's P2P write protocol uses).  The
+// owner checks the result (IpcBuffer.holds), since only it knows the write has landed in its memory.
+py::dict ipc_write_bw(const py::bytes& handle, int dev, size_t bytes, unsigned int seed, int iters, int warmup,
+                      int blocks_per_cu) {
+  if (bytes < 16 || bytes % 16) throw std::invalid_argument("bytes must be a positive multiple of 16");
+  if (iters < 1) throw std::invalid_argument("iters >= 1");
+  IpcMappings map({handle}, dev);
+  float ms = 0.f;
+  {
+    py::gil_scoped_release nogil;
+    DeviceGuard g(dev);
+    DevBuf src(dev, bytes);
+    hipLaunchKernelGGL(fill_pattern_kernel, dim3(num_cus(dev) * 4), dim3(kBlock), 0, 0, (unsigned int*)src.p, bytes / 4, seed);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipDeviceSynchronize());
+    const int grid = num_cus(dev) * std::max(1, blocks_per_cu);
+    ms = time_launches([&](hipStream_t s) { launch_copy("lds", true, src.p, map.p[0], bytes / 16, grid, s); }, iters, warmup);
+  }
+  py::dict d;
+  d["dev"] = dev;
+  d["bytes"] = bytes;
+  d["iters"] = iters;
+  d["ms_per_iter"] = ms / iters;
+  d["gbps"] = (double)bytes / (ms / 1e3 / iters) / 1e9;
+  return d;
+}
+
+// K5 over IPC: one gather launch pulls every imported buffer at once (segment i of the inbox from
+// handle i, as a rank's ingress from all of its peers); each segment is verified against seeds[i].
+py::dict ipc_gather_bw(const std::vector<py::bytes>& handles, int dev, size_t bytes, const std::vector<unsigned int>& seeds,
+                       int iters, int warmup, int blocks_per_cu) {
+  const int nsrc = (int)handles.size();
+  if (nsrc < 1 || nsrc > kMaxSrc) throw std::invalid_argument("1..16 handles");
+  if (seeds.size() != handles.size()) throw std::invalid_argument("one seed per handle");
+  if (bytes < 16 || bytes % 16) throw std::invalid_argument("bytes must be a positive multiple of 16");
+  if (iters < 1) throw std::invalid_argument("iters >= 1");
+  IpcMappings map(handles, dev);
+  float ms = 0.f;
+  bool ok = true;
+  {
+    py::gil_scoped_release nogil;
+    DeviceGuard g(dev);
+    SrcSet set{};
+    for (int i = 0; i < nsrc; ++i) set.p[i] = reinterpret_cast<const u32x4*>(map.p[i]);
+    DevBuf inbox(dev, bytes * (size_t)nsrc);
+    const int per = std::max(1, num_cus(dev) * std::max(1, blocks_per_cu) / nsrc);
+    const int grid = per * nsrc;  // every source gets the same block count
+    ms = time_launches([&](hipStream_t s) {
+      hipLaunchKernelGGL(gather_lds_kernel, dim3(grid), dim3(kBlock), 0, s, set, nsrc, (u32x4*)inbox.p, bytes / 16);
+    }, iters, warmup);
+    const size_t words = bytes / 4, win = std::min<size_t>(words, 1 << 14);
+    std::vector<unsigned int> h(win);
+    for (int i = 0; i < nsrc && ok; ++i)
+      for (size_t st0 : {(size_t)0, words / 2 - std::min(words / 2, win / 2), words - win}) {
+        HIP_CHECK(hipMemcpy(h.data(), (const unsigned int*)inbox.p + (size_t)i * words + st0, win * 4, hipMemcpyDeviceToHost));
+        for (size_t w = 0; w < win; ++w)
+          if (h[w] != ((unsigned int)((st0 + w) * 2654435761u) ^ seeds[i])) {
+            ok = false;
+            break;
+          }
+      }
+  }
+  py::dict d;
+  d["dev"] = dev;
+  d["segments"] = nsrc;
+  d["bytes_per_segment"] = bytes;
+  d["iters"] = iters;
+  d["ms_per_iter"] = ms / iters;
+  d["gbps"] = (double)bytes * nsrc / (ms / 1e3 / iters) / 1e9;
+  d["ok"] = ok;
+  return d;
+}
 
 py::dict ipc_read_bw(const py::bytes& handle, int dev, size_t bytes, unsigned int seed, int iters, int warmup,
                      int blocks_per_cu) {
@@ -799,8 +923,15 @@ PYBIND11_MODULE(_probe, m) {
   py::class_<IpcBuffer>(m, "IpcBuffer")
       .def(py::init<int, size_t, unsigned int>(), py::arg("dev"), py::arg("bytes"), py::arg("seed") = 0x5eedu)
       .def("handle", &IpcBuffer::handle)
+      .def("holds", &IpcBuffer::holds, py::arg("seed"), "does the buffer hold pattern(seed)? (after a peer's IPC write)")
       .def_property_readonly("bytes", &IpcBuffer::bytes)
       .def_property_readonly("seed", &IpcBuffer::seed);
+  m.def("ipc_write_bw", &ipc_write_bw, py::arg("handle"), py::arg("dev"), py::arg("bytes"), py::arg("seed"),
+        py::arg("iters") = 5, py::arg("warmup") = 1, py::arg("blocks_per_cu") = kBlocksPerCU,
+        "K2 over IPC: push pattern(seed) into another process's buffer through its handle (owner verifies)");
+  m.def("ipc_gather_bw", &ipc_gather_bw, py::arg("handles"), py::arg("dev"), py::arg("bytes"), py::arg("seeds"),
+        py::arg("iters") = 5, py::arg("warmup") = 1, py::arg("blocks_per_cu") = kBlocksPerCU,
+        "K5 over IPC: one gather launch over every imported buffer; each segment verified");
   m.def("ipc_read_bw", &ipc_read_bw, py::arg("handle"), py::arg("dev"), py::arg("bytes"), py::arg("seed"),
         py::arg("iters") = 5, py::arg("warmup") = 1, py::arg("blocks_per_cu") = kBlocksPerCU,
         "open another process's buffer by its IPC handle and stream it into a local one (K1 kernel); verified");

@@ -116,38 +116,65 @@ def cmd_ring(a) -> int:
 
 def cmd_ipc(a) -> int:
     """Cross-process GPU memory through HIP IPC, the mapping RCCL's P2P transport uses between ranks.
-    This process exports a patterned buffer on ``--device``. A child opens the handle on
-    ``--reader-device`` and streams it into its own buffer with the K1 LDS-DMA kernel, then verifies
-    it. Prints one JSON line, and exits 1 when the export, the import or the check fails."""
+    This process exports patterned buffers on ``--device``; a child opens the handles on
+    ``--reader-device`` and runs a probe kernel on the mappings (``--mode``):
+
+    * ``read``   (K1) streams one buffer into its own with the LDS-DMA kernel and verifies it;
+    * ``write``  (K2) pushes its own pattern into the exported buffer (remote stores); the owner
+      verifies what landed in its memory;
+    * ``gather`` (K5) pulls ``--segments`` exported buffers in one launch, each segment verified.
+
+    Prints one JSON line, and exits 1 when the export, the import or a check fails."""
     import subprocess
 
     from ._native import load
 
     probe = load("_probe")
-    if a.read:  # the child side
-        r = probe.ipc_read_bw(bytes.fromhex(a.read), a.reader_device, a.bytes, a.seed, a.iters)
-        print(json.dumps(dict(r)))
+    if a.child:  # the importing side
+        handles = [bytes.fromhex(h) for h in a.handles.split(",")]
+        seeds = [int(s) for s in a.seeds.split(",")]
+        if a.child == "read":
+            r = dict(probe.ipc_read_bw(handles[0], a.reader_device, a.bytes, seeds[0], a.iters))
+        elif a.child == "write":
+            r = dict(probe.ipc_write_bw(handles[0], a.reader_device, a.bytes, seeds[0], a.iters), ok=True)
+        else:
+            r = dict(probe.ipc_gather_bw(handles, a.reader_device, a.bytes, seeds, a.iters))
+        print(json.dumps(r))
         return 0 if r["ok"] else 1
-    out = {"ipc_mode_legacy": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY"), "bytes": a.bytes, "device": a.device,
-           "reader_device": a.reader_device}
+    nbuf = a.segments if a.mode == "gather" else 1
+    if not 1 <= nbuf <= 16:
+        print("gtk ipc: --segments must be 1..16", file=sys.stderr)
+        return 2
+    out = {"mode": a.mode, "ipc_mode_legacy": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY"), "bytes": a.bytes,
+           "device": a.device, "reader_device": a.reader_device}
+    if a.mode == "gather":
+        out["segments"] = nbuf
+    seeds = [(a.seed + 7919 * i) & 0xFFFFFFFF for i in range(nbuf)]
     try:
-        buf = probe.IpcBuffer(a.device, a.bytes, a.seed)
+        bufs = [probe.IpcBuffer(a.device, a.bytes, s) for s in seeds]
     except RuntimeError as e:
         out.update(ok=False, stage="export (hipIpcGetMemHandle)", error=str(e)[:300])
         print(json.dumps(out))
         return 1
-    p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd", "ipc", "--read", buf.handle().hex(), "--bytes",
-                        str(a.bytes), "--seed", str(a.seed), "--reader-device", str(a.reader_device), "--iters", str(a.iters)],
+    # the writer pushes a pattern the exported buffer does not already hold, so a no-op write fails
+    child_seeds = [s ^ 0xA5A5A5A5 for s in seeds] if a.mode == "write" else seeds
+    p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd", "ipc", "--child", a.mode,
+                        "--handles", ",".join(b.handle().hex() for b in bufs), "--seeds", ",".join(map(str, child_seeds)),
+                        "--bytes", str(a.bytes), "--reader-device", str(a.reader_device), "--iters", str(a.iters)],
                        capture_output=True, text=True, timeout=a.timeout)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     if p.returncode != 0 or not lines:
-        out.update(ok=False, stage="import (hipIpcOpenMemHandle) / read", error=(p.stderr or p.stdout)[-300:])
+        out.update(ok=False, stage=f"import (hipIpcOpenMemHandle) / {a.mode}", error=(p.stderr or p.stdout)[-300:])
         print(json.dumps(out))
         return 1
     r = json.loads(lines[-1])
-    out.update(ok=bool(r["ok"]), read_gbps=round(r["gbps"], 1), ms_per_iter=round(r["ms_per_iter"], 4))
+    ok = bool(r["ok"])
+    if a.mode == "write":
+        ok = ok and bufs[0].holds(child_seeds[0])
+    out.update(ok=ok, ms_per_iter=round(r["ms_per_iter"], 4))
+    out[{"read": "read_gbps", "write": "write_gbps", "gather": "ingress_gbps"}[a.mode]] = round(r["gbps"], 1)
     print(json.dumps(out))
-    return 0 if out["ok"] else 1
+    return 0 if ok else 1
 
 
 def cmd_select(a) -> int:
@@ -397,14 +424,19 @@ def main(argv=None) -> int:
     p.add_argument("--preset", default="quick", choices=["quick", "full"])
     p.add_argument("--patterns", default="all,ring", help="K6 peer patterns: all (every link of the subset), ring (pred+succ)")
     p.set_defaults(fn=cmd_ring)
-    p = sub.add_parser("ipc", help="cross-process GPU memory through HIP IPC (RCCL's P2P mapping), read by the K1 kernel")
-    p.add_argument("--device", type=int, default=0, help="HIP ordinal that owns (exports) the buffer")
-    p.add_argument("--reader-device", type=int, default=0, help="HIP ordinal of the reading process (a peer on a node)")
+    p = sub.add_parser("ipc", help="cross-process GPU memory through HIP IPC (RCCL's P2P mapping): K1 read, K2 write "
+                                   "or K5 gather kernels on the imported mappings")
+    p.add_argument("--mode", default="read", choices=["read", "write", "gather"])
+    p.add_argument("--segments", type=int, default=7, help="--mode gather: exported buffers pulled in one launch (1..16)")
+    p.add_argument("--device", type=int, default=0, help="HIP ordinal that owns (exports) the buffers")
+    p.add_argument("--reader-device", type=int, default=0, help="HIP ordinal of the importing process (a peer on a node)")
     p.add_argument("--bytes", type=int, default=256 << 20)
     p.add_argument("--seed", type=int, default=0x5EED)
     p.add_argument("--iters", type=int, default=5)
     p.add_argument("--timeout", type=float, default=180.0)
-    p.add_argument("--read", default="", help=argparse.SUPPRESS)
+    p.add_argument("--child", default="", choices=["", "read", "write", "gather"], help=argparse.SUPPRESS)
+    p.add_argument("--handles", default="", help=argparse.SUPPRESS)
+    p.add_argument("--seeds", default="", help=argparse.SUPPRESS)
     p.set_defaults(fn=cmd_ipc)
     p = sub.add_parser("select")
     disc(p)

@@ -360,3 +360,20 @@ def test_ipc_read_across_processes():
     print(json.dumps(runs))
     rc, out = runs["0"]
     assert rc == 0 and out["ok"] and out["read_gbps"] > 1000, out
+
+
+@pytest.mark.parametrize("mode,key", [("write", "write_gbps"), ("gather", "ingress_gbps")])
+def test_ipc_write_and_gather_across_processes(mode, key):
+    """K2 and K5 on imported HIP IPC mappings (the remote-pointer paths of the probe kernels; on a node
+    the importer is a peer GPU).  write: the child's K2 kernel stores a pattern the exported buffer
+    did not hold, and the OWNER verifies it in its own memory.  gather: one K5 launch pulls 7 exported
+    buffers (a rank's 7 xGMI peers on a full node), each segment verified against its own seed."""
+    base = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd", "ipc", "--mode", mode, "--bytes", str(128 << 20)],
+                       capture_output=True, text=True, timeout=300, cwd=REPO, env=dict(base, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    out = json.loads(lines[-1]) if lines else {"stderr": p.stderr[-500:]}
+    print(json.dumps(out))
+    assert p.returncode == 0 and out["ok"] and out[key] > 1000, out
+    if mode == "gather":
+        assert out["segments"] == 7
