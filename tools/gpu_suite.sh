@@ -38,6 +38,17 @@ case "$mode" in
     step pmc_ring_lds 120 timeout -s KILL 90 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES --kernel-trace -d "$out/pmc_ring_lds" -o run -- python3 -m gpu_topology_on_k8s_amd ring --devices 0,0,0 --preset full --patterns all
     step pmc_ring_mem 120 timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum --kernel-trace -d "$out/pmc_ring_mem" -o run -- python3 -m gpu_topology_on_k8s_amd ring --devices 0,0,0 --preset full --patterns all
     ;;
+  ipc)
+    # K1 read, K2 write and K5 gather on imported HIP IPC mappings (one JSON line each)
+    for m in read write gather; do
+      step "ipc_$m" 120 python -u -m gpu_topology_on_k8s_amd ipc --mode "$m" --bytes $((256 << 20))
+    done
+    ;;
+  llama)
+    # the config-5 workload on the current tree: Llama-3-8B b4 x 4096 step, then its kernel trace
+    step llama8b_b4 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
+    step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
+    ;;
   cumask)
     # MFMA rate and HBM copy under HSA_CU_MASK (the time-sliced shares' spatial split, profiles/r02_cumask)
     for m in "" "0:0-127" "0:0-63" "0:0-31,128-159"; do
