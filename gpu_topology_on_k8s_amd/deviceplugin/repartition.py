@@ -55,7 +55,8 @@ def repartition(api, node_name: str, contract: Contract, idle_fn: Callable[[], b
                 clock: Callable[[], float] = time.time) -> Tuple[str, str]:
     """One reconciliation pass.  -> (outcome, message), outcome one of
     ``none`` (no request), ``same`` (already there), ``invalid``, ``skipped`` (this request failed
-    before), ``busy`` (pods hold devices), ``stopped`` (``wait`` returned True), ``ok``, ``failed``."""
+    before), ``unavailable`` (amdsmi reports no package: nothing recorded, the next pass asks again),
+    ``busy`` (pods hold devices), ``stopped`` (``wait`` returned True), ``ok``, ``failed``."""
     if api is None or not node_name:
         return "none", "no apiserver"
     want_c, want_m, node = partition_request(api, node_name, contract)
@@ -67,6 +68,8 @@ def repartition(api, node_name: str, contract: Contract, idle_fn: Callable[[], b
         return "invalid", str(e)
     tag = f"{want_c or '-'}/{want_m or '-'}"
     info = partition_info(lib)
+    if not info:  # not "already there": there is nothing to compare (amdsmi down or no GPU visible)
+        return "unavailable", f"{tag} requested; amdsmi reports no GPU packages"
     if all((not want_c or p["compute"] == want_c) and (not want_m or p["memory"] == want_m) for p in info):
         ann = (node.get("metadata") or {}).get("annotations") or {}
         if contract.partition_failed_key in ann:

@@ -157,6 +157,21 @@ def test_repartition_pass_marks_the_node_and_records_the_outcome(node):
     assert repartition(api, "w", c, idle)[0] == "invalid"
 
 
+def test_repartition_without_packages_is_not_already_there(node, monkeypatch):
+    """amdsmi reporting no package (driver down, no GPU visible) is not "already in the mode": the
+    pass says so, records nothing on the node and asks again next time."""
+    from gpu_topology_on_k8s_amd.deviceplugin import repartition as rp
+
+    c = Contract()
+    api = FakeAPIServer()
+    api.create_node(make_node("w", labels={c.partition_request_label: "CPX"}))
+    monkeypatch.setattr(rp, "partition_info", lambda lib=None: [])
+    out, msg = rp.repartition(api, "w", c, lambda: True, settle_s=0)
+    assert out == "unavailable" and "no GPU packages" in msg
+    ann = api.get_node("w")["metadata"].get("annotations") or {}
+    assert c.partition_failed_key not in ann and c.probing_key not in ann
+
+
 def test_device_plugin_daemon_repartitions_on_the_node_label(node):
     """The shipped daemon with --partition-control on: a node labelled CPX registers 16 XCPs of a
     2-package node at start-up; relabelled SPX while a pod holds an XCP, the plugin waits, and once
