@@ -362,8 +362,8 @@ def test_ipc_read_across_processes():
     assert rc == 0 and out["ok"] and out["read_gbps"] > 1000, out
 
 
-@pytest.mark.parametrize("mode,key", [("write", "write_gbps"), ("gather", "ingress_gbps")])
-def test_ipc_write_and_gather_across_processes(mode, key):
+@pytest.mark.parametrize("mode,key,floor", [("write", "write_gbps", 2000.0), ("gather", "ingress_gbps", 1500.0)])
+def test_ipc_write_and_gather_across_processes(mode, key, floor):
     """K2 and K5 on imported HIP IPC mappings (the remote-pointer paths of the probe kernels; on a node
     the importer is a peer GPU).  write: the child's K2 kernel stores a pattern the exported buffer
     did not hold, and the OWNER verifies it in its own memory.  gather: one K5 launch pulls 7 exported
@@ -374,6 +374,7 @@ def test_ipc_write_and_gather_across_processes(mode, key):
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     out = json.loads(lines[-1]) if lines else {"stderr": p.stderr[-500:]}
     print(json.dumps(out))
-    assert p.returncode == 0 and out["ok"] and out[key] > 1000, out
+    # floors at ~60 % of MI355X (profiles/r03_llama2/ipc.jsonl: write 3446, gather 2412 GB/s)
+    assert p.returncode == 0 and out["ok"] and out[key] > floor, out
     if mode == "gather":
         assert out["segments"] == 7
