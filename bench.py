@@ -93,6 +93,10 @@ def parse(argv=None):
     ap.add_argument("--budget-s", type=float, default=300.0,
                     help="wall-clock budget: a supplementary phase (tuning, sweep, fp32, graph, worst-subset A/B) is "
                          "skipped when its predicted cost would overrun it; the headline is never skipped; 0 = no limit")
+    ap.add_argument("--watchdog-s", type=float, default=None,
+                    help="a rank still running after this many seconds (default: budget + 300; 0 = off) reports the "
+                         "phase it is stuck in (rank 0: a JSON line with value null), dumps every thread's stack and "
+                         "exits 124, so a hung collective ends the run with a diagnosis instead of a silent kill")
     return ap.parse_args(argv)
 
 
@@ -105,15 +109,18 @@ class Phases:
         self.budget = float(budget_s)
         self.s = {}
         self.skipped = []
+        self.current = "setup"  # the phase in progress (the watchdog's report)
 
     def elapsed(self) -> float:
         return time.perf_counter() - self.t0
 
     def run(self, name, fn, *a, **kw):
         t = time.perf_counter()
+        prev, self.current = self.current, name
         try:
             return fn(*a, **kw)
         finally:
+            self.current = prev
             self.s[name] = round(self.s.get(name, 0.0) + time.perf_counter() - t, 3)
 
     def allow(self, name: str, predicted_s: float, agree=None) -> bool:
@@ -126,6 +133,39 @@ class Phases:
 
     def report(self) -> dict:
         return dict(self.s, total=round(self.elapsed(), 3))
+
+
+def start_watchdog(seconds: float, ph: Phases, rank: int, world: int, args, exit_fn=os._exit, out=None, err=None):
+    """Arm a timer that ends a hung run with a diagnosis: the phase in progress (rank 0 prints the
+    bench's JSON line with ``value: null`` and an ``error``), every thread's stack, exit code 124.
+    A collective that never completes cannot be interrupted from Python, so the process exits
+    (``os._exit``) instead of unwinding.  Returns the timer (``cancel()`` it once the line is out) or
+    None when ``seconds <= 0``."""
+    import faulthandler
+    import threading
+
+    if seconds is None or seconds <= 0:
+        return None
+
+    def fire():
+        o = out or sys.stdout
+        e = err or sys.stderr
+        msg = f"watchdog: rank {rank} still in phase '{ph.current}' after {ph.elapsed():.0f} s"
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+                              "warmup": args.warmup, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                              "dtype": args.dtype, "error": msg, "phase_s": ph.report()}), file=o, flush=True)
+        print(f"bench: {msg}; thread stacks follow", file=e, flush=True)
+        try:
+            faulthandler.dump_traceback(file=e, all_threads=True)
+        except (AttributeError, ValueError, OSError):  # a stream without a file descriptor
+            pass
+        exit_fn(124)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
 
 
 def parse_size(s: str) -> int:
@@ -377,6 +417,8 @@ def main(argv=None) -> int:
     # "invalid argument" and RCCL cannot open its peers' buffers.  Set before HIP initialises.
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     ph = Phases(args.budget_s)
+    wd_s = args.watchdog_s if args.watchdog_s is not None else (args.budget_s + 300.0 if args.budget_s > 0 else 0.0)
+    watchdog = start_watchdog(wd_s, ph, int(os.environ.get("RANK", "0")), args.gpus, args)
     rccl_log = None
     if args.backend != "cpu" and (args.rccl_log == "on" or (args.rccl_log == "auto" and args.gpus > 1)) \
             and "NCCL_DEBUG" not in os.environ:
@@ -456,6 +498,7 @@ def main(argv=None) -> int:
             ctas, tuning = ph.run("tune", tune_ctas, env, device, nbytes, args, tdev, barrier_kw)
     runner = None
     t_comm = time.perf_counter()
+    ph.current = "comm"
     if args.backend == "native":
         # The native communicator (csrc/rccl) is the measured path; if its extension cannot be
         # loaded on some rank, every rank falls back together to dist.all_reduce (the same RCCL).
@@ -477,6 +520,7 @@ def main(argv=None) -> int:
         runner = AllReduceRunner(env, device, nbytes, args.dtype, backend=args.backend, inplace=args.inplace)
     comm_s = time.perf_counter() - t_comm
     ph.s["comm"] = round(comm_s, 3)
+    ph.current = "setup"
     wrong = torch.tensor([ph.run("check", runner.check)], dtype=torch.int64, device=tdev)
     dist.all_reduce(wrong)
     if int(wrong.item()) != 0:
@@ -631,7 +675,11 @@ def main(argv=None) -> int:
             "algbw_gbps": round(algbw, 3),
             "busbw_gbps": round(busbw, 3),
         }
+        if watchdog is not None:
+            watchdog.cancel()
         print(json.dumps(out), flush=True)
+    if watchdog is not None:
+        watchdog.cancel()
     dist.destroy_process_group()
     return 0
 

@@ -201,3 +201,36 @@ def test_rccl_log_summary_flags_a_broken_transport():
     s = rccl_log_summary(text)
     assert s["p2p_only"] is False and s["non_p2p_edges"] == {"SHM/direct/direct": 2}
     assert rccl_log_summary("")["p2p_only"] is False  # no edges logged proves nothing
+
+
+def test_watchdog_reports_the_stuck_phase_and_exits():
+    """A hung collective cannot be interrupted from Python: the watchdog prints rank 0's JSON line with
+    value null and the phase in progress, dumps the thread stacks and exits 124 (here into buffers,
+    with the exit captured)."""
+    import io
+    import threading
+    import time as _time
+
+    sys.path.insert(0, REPO)
+    import bench
+
+    args = bench.parse(["--steps", "3", "--warmup", "1"])
+    ph = bench.Phases(300.0)
+    out, err, codes = io.StringIO(), io.StringIO(), []
+    done = threading.Event()
+
+    def fake_exit(code):
+        codes.append(code)
+        done.set()
+
+    stuck = threading.Thread(target=lambda: ph.run("headline", done.wait, 30), daemon=True)
+    stuck.start()
+    _time.sleep(0.05)
+    t = bench.start_watchdog(0.2, ph, 0, 8, args, exit_fn=fake_exit, out=out, err=err)
+    assert done.wait(10) and codes == [124]
+    line = json.loads(out.getvalue().strip().splitlines()[-1])
+    assert line["value"] is None and line["n_gpus"] == 8 and "'headline'" in line["error"]
+    assert line["metric"] == "RCCL all-reduce bus GB/s on scheduler-chosen k-GPU subset, k=1/2/4/8"
+    assert "thread stacks follow" in err.getvalue()
+    t.cancel()
+    assert bench.start_watchdog(0, ph, 0, 1, args) is None
