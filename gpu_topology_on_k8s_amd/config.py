@@ -135,6 +135,14 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
                                        + ([f"--time-slices={int(time_slices)}"] if int(time_slices) > 1 else [])
                                        + (["--partition-control=on"] if partition_control else []),
                             "ports": [{"containerPort": PLUGIN_METRICS_PORT, "name": "metrics"}],
+                            # /healthz fails when the gRPC server is down, the monitor loop is wedged or
+                            # re-registration keeps failing (DevicePluginServer.liveness); start-up (discovery,
+                            # link probe, a requested partition switch) gets up to 15 min before liveness counts
+                            "startupProbe": {"httpGet": {"path": "/healthz", "port": PLUGIN_METRICS_PORT},
+                                             "periodSeconds": 10, "failureThreshold": 90},
+                            "livenessProbe": {"httpGet": {"path": "/healthz", "port": PLUGIN_METRICS_PORT},
+                                              "periodSeconds": 30, "failureThreshold": 4},
+                            "resources": {"requests": {"cpu": "100m", "memory": "256Mi"}, "limits": {"memory": "2Gi"}},
                             "env": [{"name": "NODE_NAME", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}},
                                     # the probe / validator children share GPU buffers across processes;
                                     # the amdgpu host driver exports IPC handles only as dma-bufs, which ROCr
@@ -188,6 +196,7 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
                                         "--scheduler-names=default-scheduler"],
                             "readinessProbe": {"httpGet": {"host": "127.0.0.1", "path": "/healthz", "port": DEFAULT_PORT}},
                             "livenessProbe": {"httpGet": {"host": "127.0.0.1", "path": "/healthz", "port": DEFAULT_PORT}},
+                            "resources": {"requests": {"cpu": "200m", "memory": "256Mi"}, "limits": {"memory": "2Gi"}},
                         }],
                     },
                 },

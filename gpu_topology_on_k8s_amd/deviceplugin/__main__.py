@@ -246,6 +246,7 @@ def main(argv=None) -> int:
             return None if probed is None else time_slice(probed, a.time_slices)
     plugin = DevicePluginServer(topo, cfg, api=api, health_fn=health if a.discovery != "fake" else None, reprobe_fn=reprobe)
     plugin.event_source = events
+    plugin.metrics.liveness = plugin.liveness  # /healthz: the DaemonSet's livenessProbe
     if a.metrics_port:
         from .metrics import serve_metrics
 

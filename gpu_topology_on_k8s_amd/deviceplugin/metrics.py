@@ -87,6 +87,16 @@ class _Handler(BaseHTTPRequestHandler):
         if self.path.split("?")[0] == "/metrics":
             body, ctype = self.metrics.exposition(), "text/plain; version=0.0.4; charset=utf-8"
         elif self.path.split("?")[0] == "/healthz":
+            live = getattr(self.metrics, "liveness", None)
+            ok, why = live() if live is not None else (True, "ok")
+            if not ok:  # the DaemonSet's livenessProbe restarts a wedged plugin
+                body = why.encode()
+                self.send_response(503)
+                self.send_header("Content-Type", "text/plain")
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+                return
             body, ctype = b"ok", "text/plain"
         else:
             self.send_response(404)

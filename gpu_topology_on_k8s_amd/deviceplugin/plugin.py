@@ -242,6 +242,11 @@ class DevicePluginServer:
         self._holds: Dict[int, str] = {}
         self._reprobe_now = threading.Event()  # a GPU reset finished: re-measure as soon as the node is idle
         self.event_source = None  # deviceplugin.events.GpuEventWatcher (amdsmi event notification)
+        # liveness (/healthz): the monitor loop's last pass, and since when re-registration has failed
+        self._monitor_beat: Optional[float] = None
+        self._register_failing_since: Optional[float] = None
+        self._started = False
+        self._register_required = True
 
     # ------------------------------------------------------------------ device view
     def devices(self) -> List[pb.Device]:
@@ -966,6 +971,23 @@ class DevicePluginServer:
             log.info("clearing the probing mark of the previous run (new layout published)")
             self._mark_probing(None)
 
+    def liveness(self, monitor_stall_s: float = 120.0, register_fail_s: float = 300.0) -> Tuple[bool, str]:
+        """What ``/healthz`` answers (the DaemonSet's livenessProbe): (ok, reason).  Not alive when the
+        gRPC server is down, the monitor loop (health polling, re-registration after a kubelet restart)
+        has not passed for ``monitor_stall_s`` — a driver call that never returns wedges it — or
+        re-registration has failed for ``register_fail_s``.  The kubelet then restarts the container,
+        which starts over from discovery; the pods' devices and annotations are untouched."""
+        if not self._started:
+            return False, "not started"
+        if self._server is None:
+            return False, "gRPC server not running"
+        now = time.monotonic()
+        if self._monitor_beat is not None and now - self._monitor_beat > monitor_stall_s:
+            return False, f"monitor loop stalled for {now - self._monitor_beat:.0f}s"
+        if self._register_failing_since is not None and now - self._register_failing_since > register_fail_s:
+            return False, f"re-registration with the kubelet failing for {now - self._register_failing_since:.0f}s"
+        return True, "ok"
+
     def start(self, register: bool = True) -> None:
         self._stop.clear()
         self.install_guard()
@@ -973,8 +995,11 @@ class DevicePluginServer:
         self._publish_node()
         self._clear_stale_mark()
         self.serve()
+        self._register_required = register
         if register:
             self.register()
+        self._started = True
+        self._monitor_beat = time.monotonic()
         self._threads = [threading.Thread(target=self._monitor, name="devplugin-monitor", daemon=True)]
         if self.reprobe_fn is not None and (self.cfg.reprobe_interval > 0 or self.event_source is not None):
             # its own thread: a probe takes minutes and must not stall health polling / re-registration
@@ -1050,6 +1075,7 @@ class DevicePluginServer:
         """Health polling and kubelet restart detection (the kubelet wipes plugin sockets on restart)."""
         next_health = next_reconcile = 0.0
         while not self._stop.wait(0.2):
+            self._monitor_beat = time.monotonic()
             if self.cfg.reconcile_interval > 0 and time.monotonic() >= next_reconcile:
                 next_reconcile = time.monotonic() + self.cfg.reconcile_interval
                 try:
@@ -1062,8 +1088,12 @@ class DevicePluginServer:
                     if self._server is not None:
                         self._server.stop(grace=0)
                     self.serve()
-                    self.register()
+                    if self._register_required:
+                        self.register()
+                    self._register_failing_since = None
                 except Exception as e:
+                    if self._register_failing_since is None:
+                        self._register_failing_since = time.monotonic()
                     log.warning("re-registration failed, will retry: %s", e)
             if self.health_fn is not None and time.monotonic() >= next_health:
                 next_health = time.monotonic() + self.cfg.health_interval
@@ -1095,6 +1125,7 @@ class DevicePluginServer:
                     log.warning("health check failed: %s", e)
 
     def stop(self) -> None:
+        self._started = False
         self._stop.set()
         with self._cond:
             self._cond.notify_all()

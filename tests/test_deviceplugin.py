@@ -324,3 +324,57 @@ def test_allocate_sets_nccl_ib_hca_to_the_gpus_own_nics(sockdir, tmp_path):
     finally:
         plugin.stop()
         kubelet.stop()
+
+
+def test_liveness_reports_a_wedged_monitor_and_failing_registration(sockdir):
+    """/healthz is the DaemonSet's livenessProbe: 200 while the plugin serves; 503 with the reason when
+    the monitor loop is stuck (here in a health poll that never returns, as a hung driver call would
+    be) or re-registration after a kubelet restart keeps failing, so the kubelet restarts the plugin."""
+    import threading
+
+    import requests
+
+    from gpu_topology_on_k8s_amd.deviceplugin import serve_metrics
+
+    api = FakeAPIServer()
+    api.create_node(make_node("n3"))
+    kubelet = FakeKubelet(sockdir, node_name="n3", api=api)
+    kubelet.start()
+    release = threading.Event()
+    wedge = threading.Event()
+
+    def health(t):
+        if wedge.is_set():
+            release.wait(30)  # a driver call that does not come back
+        return {g.index: True for g in t.gpus}
+
+    plugin = DevicePluginServer(fx.f7_mi355x(n=4), PluginConfig(resource_name=RES, socket_dir=sockdir, node_name="n3",
+                                                                 health_interval=0.05), api=api, health_fn=health)
+    plugin.metrics.liveness = plugin.liveness
+    srv, base = serve_metrics(plugin.metrics)
+    try:
+        assert requests.get(base + "/healthz", timeout=5).status_code == 503  # not started yet
+        plugin.start()
+        kubelet.wait_for(RES)
+        r = requests.get(base + "/healthz", timeout=5)
+        assert r.status_code == 200 and r.text == "ok"
+        wedge.set()
+        time.sleep(0.3)
+        ok, why = plugin.liveness(monitor_stall_s=0.1)
+        assert not ok and "monitor loop stalled" in why
+        release.set()
+        wedge.clear()
+        assert _wait(lambda: plugin.liveness(monitor_stall_s=0.1)[0], timeout=5)
+        # the kubelet goes away for good: the socket vanishes and registration keeps failing
+        kubelet.stop()
+        os.unlink(plugin.cfg.socket_path)
+        assert _wait(lambda: plugin._register_failing_since is not None, timeout=20)
+        ok, why = plugin.liveness(register_fail_s=0.0)
+        assert not ok and "re-registration" in why
+        assert plugin.liveness(register_fail_s=3600)[0]  # within the grace period it is still alive
+    finally:
+        release.set()
+        srv.shutdown()
+        plugin.stop()
+        kubelet.stop()
+    assert not plugin.liveness()[0]  # stopped
