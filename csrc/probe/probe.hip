@@ -189,6 +189,45 @@ __global__ __launch_bounds__(kBlock) void mfma_warmup_kernel(float* __restrict__
   out[(size_t)blockIdx.x * kBlock + threadIdx.x] = s;
 }
 
+// K4r: the same loop on random operands.  Eight distinct pseudo-random A and B fragments per lane
+// (uniform in [-1, 1), from a hash of lane and index) are cycled, so consecutive MFMAs see new
+// operand bits as a GEMM's do.  The bit toggling draws more power than K4's near-constant operands;
+// the rate it reaches is the MFMA ceiling a GEMM or an attention kernel on real data can approach.
+__device__ __forceinline__ __bf16 rand_bf16(unsigned int x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return (__bf16)((float)(x >> 8) * (1.0f / 8388608.0f) - 1.0f);
+}
+
+__global__ __launch_bounds__(kBlock) void mfma_warmup_random_kernel(float* __restrict__ out, int iters) {
+  bf16x8 a[8], b[8];
+  const unsigned int seed = (blockIdx.x * kBlock + threadIdx.x) * 131u;
+#pragma unroll
+  for (int f = 0; f < 8; ++f)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a[f][i] = rand_bf16(seed + 16u * f + i);
+      b[f][i] = rand_bf16(~(seed + 16u * f + i));
+    }
+  f32x16 acc0 = {}, acc1 = {}, acc2 = {}, acc3 = {};
+  for (int it = 0; it < iters; it += 2) {
+#pragma unroll
+    for (int f = 0; f < 8; f += 4) {
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[f], b[f + 1], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[f + 1], b[f + 2], acc1, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[f + 2], b[f + 3], acc2, 0, 0, 0);
+      acc3 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[f + 3], b[f], acc3, 0, 0, 0);
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s += acc0[i] + acc1[i] + acc2[i] + acc3[i];
+  out[(size_t)blockIdx.x * kBlock + threadIdx.x] = s;
+}
+
 // Where a workgroup runs: its XCD (HW_REG_XCC_ID[3:0]) and the low half of HW_REG_HW_ID (wave, SIMD,
 // CU, SH, SE).  Lane 0 writes one word per workgroup with an ordinary vector store.  Shows how a queue
 // CU mask (HSA_CU_MASK, time-sliced shares in topology/shares.py) spreads over the 8 XCDs.
@@ -590,9 +629,11 @@ py::dict copy_bw(int src_dev, int dst_dev, int exec_dev, size_t bytes, int iters
   return to_dict(c);
 }
 
-py::dict mfma_warmup(int dev, double target_ms, int iters_per_launch) {
+py::dict mfma_warmup(int dev, double target_ms, int iters_per_launch, bool random_operands) {
   py::gil_scoped_release nogil_outer;
   DeviceGuard g(dev);
+  if (iters_per_launch < 2 || iters_per_launch % 2) throw std::invalid_argument("iters_per_launch: a positive even number");
+  auto* kern = random_operands ? mfma_warmup_random_kernel : mfma_warmup_kernel;
   const int grid = num_cus(dev) * 4;  // 16 waves per CU = 4 per SIMD
   DevBuf out(dev, (size_t)grid * kBlock * sizeof(float));
   hipEvent_t e0, e1;
@@ -603,7 +644,7 @@ py::dict mfma_warmup(int dev, double target_ms, int iters_per_launch) {
   auto t0 = std::chrono::steady_clock::now();
   HIP_CHECK(hipEventRecord(e0, 0));
   do {
-    hipLaunchKernelGGL(mfma_warmup_kernel, dim3(grid), dim3(kBlock), 0, 0, (float*)out.p, iters_per_launch);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, 0, (float*)out.p, iters_per_launch);
     HIP_CHECK(hipGetLastError());
     ++launches;
     HIP_CHECK(hipDeviceSynchronize());
@@ -611,7 +652,7 @@ py::dict mfma_warmup(int dev, double target_ms, int iters_per_launch) {
   } while (total_ms < target_ms && launches < 100000);
   // timed launch, clocks now lifted
   HIP_CHECK(hipEventRecord(e0, 0));
-  hipLaunchKernelGGL(mfma_warmup_kernel, dim3(grid), dim3(kBlock), 0, 0, (float*)out.p, iters_per_launch);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, 0, (float*)out.p, iters_per_launch);
   HIP_CHECK(hipEventRecord(e1, 0));
   HIP_CHECK(hipEventSynchronize(e1));
   float ms = 0.f;
@@ -626,6 +667,7 @@ py::dict mfma_warmup(int dev, double target_ms, int iters_per_launch) {
   r["warm_ms"] = total_ms;
   r["timed_ms"] = ms;
   r["tflops"] = flops / (ms / 1e3) / 1e12;
+  r["random_operands"] = random_operands;
   return r;
 }
 
@@ -915,7 +957,8 @@ PYBIND11_MODULE(_probe, m) {
         py::arg("iters") = 3, py::arg("warmup") = 1, py::arg("blocks_per_cu") = kBlocksPerCU);
   m.def("ring_bw", &ring_bw, py::arg("devs"), py::arg("peers"), py::arg("bytes") = (size_t)64 << 20, py::arg("iters") = 3,
         py::arg("warmup") = 1, py::arg("blocks_per_cu") = kBlocksPerCU);
-  m.def("mfma_warmup", &mfma_warmup, py::arg("dev"), py::arg("target_ms") = 50.0, py::arg("iters_per_launch") = 4096);
+  m.def("mfma_warmup", &mfma_warmup, py::arg("dev"), py::arg("target_ms") = 50.0, py::arg("iters_per_launch") = 4096,
+        py::arg("random_operands") = false);
   m.def("probe_matrix", &probe_matrix, py::arg("devs"), py::arg("bytes") = (size_t)256 << 20, py::arg("iters") = 5,
         py::arg("warmup") = 1, py::arg("mode") = "read", py::arg("kind") = "lds", py::arg("nontemporal") = false,
         py::arg("blocks_per_cu") = kBlocksPerCU, py::call_guard<py::gil_scoped_release>());

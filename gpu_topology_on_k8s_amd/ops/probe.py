@@ -48,9 +48,10 @@ def device_props(dev: int) -> Dict[str, object]:
     return dict(_p().device_props(dev))
 
 
-def warmup(dev: int, ms: float = 50.0) -> Dict[str, object]:
-    """K4: run MFMA until ``ms`` elapsed so the measured copies see lifted clocks."""
-    return dict(_p().mfma_warmup(dev, float(ms)))
+def warmup(dev: int, ms: float = 50.0, random_operands: bool = False) -> Dict[str, object]:
+    """K4: run MFMA until ``ms`` elapsed so the measured copies see lifted clocks.  ``random_operands``:
+    cycle pseudo-random bf16 fragments instead (the power-limited MFMA rate real GEMM data sees)."""
+    return dict(_p().mfma_warmup(dev, float(ms), 4096, bool(random_operands)))
 
 
 def copy_bw(src: int, dst: int, nbytes: int = 256 << 20, iters: int = 10, warmup_iters: int = 2, mode: str = "read",

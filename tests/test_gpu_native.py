@@ -38,6 +38,17 @@ def test_mfma_warmup_rate(probe_mod):
     assert r["tflops"] > 1600, r
 
 
+def test_mfma_random_operands_rate(probe_mod):
+    """K4r: the same MFMA loop on cycled pseudo-random operands (the bit toggling of real GEMM data)
+    runs below K4's rate on near-constant operands; it is the ceiling hipBLASLt and the attention
+    kernels see on training data (profiles/r03_gemm_cold)."""
+    from gpu_topology_on_k8s_amd.ops.probe import warmup
+
+    r = warmup(0, 100.0, random_operands=True)
+    print(json.dumps({"mfma_random_tflops": round(r["tflops"], 1)}))
+    assert r["random_operands"] and r["tflops"] > 800, r
+
+
 # copy GB/s floors at 512 MiB (HBM moves twice that): ~75 % of what r02 measured for each form
 # (K3 LDS-DMA and register staging ~2.8 TB/s copy, the runtime blit ~2.4 TB/s; profiles/r02_copy)
 COPY_FLOOR_GBPS = {"lds": 2000.0, "reg": 2000.0, "sdma": 1700.0}
