@@ -15,7 +15,10 @@
 //     reports the share as the device's total, so caching allocators size themselves to it.
 //   * CUs: HSA_CU_MASK is set from the mounted config before the program's own code runs (a
 //     constructor of a preloaded library runs before main and before any HIP call, and the ROCr
-//     runtime reads the variable when it initialises), whatever the container's environment says.
+//     runtime reads the variable when it initialises), whatever the container's environment says;
+//     and set again at the first intercepted HIP call (the calls a program makes first: hipInit,
+//     hipGetDeviceCount, hipSetDevice, hipGetDevice, the allocators), in case the program itself
+//     rewrote it before initialising the runtime.
 //
 // The config is the read-only file ``$GTK_VGPU_CONFIG`` (default /etc/gtk-vgpu.conf) the plugin
 // writes per allocation:
@@ -47,6 +50,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -127,6 +131,14 @@ Fn real(const char* name) {
 
 // resolved once per entry point; a function-local static is initialised thread-safely
 #define REAL(name, type) static const type real_fn = real<type>(#name);
+
+// The runtime reads HSA_CU_MASK once, when the process's first HIP call initialises it.  A program may
+// have rewritten the variable after the constructor below set it (Python's os.environ before
+// `import torch`), so every intercepted entry point sets it back once, before its first call into the
+// runtime: if that call is the one that initialises it, the runtime reads the share's mask.
+std::atomic<bool> g_mask_reasserted{false};
+
+void reassert_cu_mask();
 
 int current_device() {
   typedef hipError_t (*F)(int*);
@@ -342,41 +354,56 @@ __attribute__((constructor)) void load_config() {
   setenv("GTK_VGPU_ACTIVE", "1", 1);  // lets the workload report that the guard is in force
 }
 
+void reassert_cu_mask() {
+  if (g_mask_reasserted.load(std::memory_order_acquire)) return;
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  if (g_mask_reasserted.load(std::memory_order_relaxed)) return;
+  if (s.active && !s.cu_mask.empty()) setenv("HSA_CU_MASK", s.cu_mask.c_str(), 1);
+  g_mask_reasserted.store(true, std::memory_order_release);
+}
+
 }  // namespace
 
 extern "C" {
 
 __attribute__((visibility("default"))) hipError_t hipMalloc(void** ptr, size_t size) {
+  reassert_cu_mask();
   typedef hipError_t (*F)(void**, size_t);
   REAL(hipMalloc, F);
   return guarded(ptr, size, [&] { return real_fn(ptr, size); });
 }
 
 __attribute__((visibility("default"))) hipError_t hipExtMallocWithFlags(void** ptr, size_t size, unsigned int flags) {
+  reassert_cu_mask();
   typedef hipError_t (*F)(void**, size_t, unsigned int);
   REAL(hipExtMallocWithFlags, F);
   return guarded(ptr, size, [&] { return real_fn(ptr, size, flags); });
 }
 
 __attribute__((visibility("default"))) hipError_t hipMallocManaged(void** ptr, size_t size, unsigned int flags) {
+  reassert_cu_mask();
   typedef hipError_t (*F)(void**, size_t, unsigned int);
   REAL(hipMallocManaged, F);
   return guarded(ptr, size, [&] { return real_fn(ptr, size, flags); });
 }
 
 __attribute__((visibility("default"))) hipError_t hipMallocAsync(void** ptr, size_t size, void* stream) {
+  reassert_cu_mask();
   typedef hipError_t (*F)(void**, size_t, void*);
   REAL(hipMallocAsync, F);
   return guarded(ptr, size, [&] { return real_fn(ptr, size, stream); });
 }
 
 __attribute__((visibility("default"))) hipError_t hipMallocFromPoolAsync(void** ptr, size_t size, void* pool, void* stream) {
+  reassert_cu_mask();
   typedef hipError_t (*F)(void**, size_t, void*, void*);
   REAL(hipMallocFromPoolAsync, F);
   return guarded(ptr, size, [&] { return real_fn(ptr, size, pool, stream); });
 }
 
 __attribute__((visibility("default"))) hipError_t hipMallocPitch(void** ptr, size_t* pitch, size_t width, size_t height) {
+  reassert_cu_mask();
   typedef hipError_t (*F)(void**, size_t*, size_t, size_t);
   REAL(hipMallocPitch, F);
   // the pitch is not known before the call: reserve the unpadded size, then settle to pitch*height
@@ -405,6 +432,7 @@ __attribute__((visibility("default"))) hipError_t hipMallocPitch(void** ptr, siz
 }
 
 __attribute__((visibility("default"))) hipError_t hipFree(void* ptr) {
+  reassert_cu_mask();
   typedef hipError_t (*F)(void*);
   REAL(hipFree, F);
   auto v = untrack(ptr);
@@ -414,6 +442,7 @@ __attribute__((visibility("default"))) hipError_t hipFree(void* ptr) {
 }
 
 __attribute__((visibility("default"))) hipError_t hipFreeAsync(void* ptr, void* stream) {
+  reassert_cu_mask();
   typedef hipError_t (*F)(void*, void*);
   REAL(hipFreeAsync, F);
   auto v = untrack(ptr);
@@ -426,6 +455,7 @@ __attribute__((visibility("default"))) hipError_t hipFreeAsync(void* ptr, void* 
 // unsigned long long flags): the handle is an opaque pointer-sized value
 __attribute__((visibility("default"))) hipError_t hipMemCreate(void** handle, size_t size, const void* prop,
                                                                 unsigned long long flags) {
+  reassert_cu_mask();
   typedef hipError_t (*F)(void**, size_t, const void*, unsigned long long);
   REAL(hipMemCreate, F);
   const int dev = current_device();
@@ -444,6 +474,7 @@ __attribute__((visibility("default"))) hipError_t hipMemCreate(void** handle, si
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemRelease(void* handle) {
+  reassert_cu_mask();
   typedef hipError_t (*F)(void*);
   REAL(hipMemRelease, F);
   State& s = st();
@@ -472,6 +503,7 @@ __attribute__((visibility("default"))) hipError_t hipMemRelease(void* handle) {
 
 // the share is the device's size as far as this process can tell
 __attribute__((visibility("default"))) hipError_t hipMemGetInfo(size_t* free_b, size_t* total_b) {
+  reassert_cu_mask();
   typedef hipError_t (*F)(size_t*, size_t*);
   REAL(hipMemGetInfo, F);
   hipError_t e = real_fn(free_b, total_b);
@@ -483,6 +515,36 @@ __attribute__((visibility("default"))) hipError_t hipMemGetInfo(size_t* free_b, 
   if (total_b && (long long)*total_b > s.limit[dev]) *total_b = (size_t)s.limit[dev];
   if (free_b && (long long)*free_b > left) *free_b = (size_t)(left > 0 ? left : 0);
   return e;
+}
+
+// The calls a program usually makes first (torch: hipGetDeviceCount), which initialise the runtime:
+// pass-through after the mask is set back.
+__attribute__((visibility("default"))) hipError_t hipInit(unsigned int flags) {
+  reassert_cu_mask();
+  typedef hipError_t (*F)(unsigned int);
+  REAL(hipInit, F);
+  return real_fn(flags);
+}
+
+__attribute__((visibility("default"))) hipError_t hipGetDeviceCount(int* count) {
+  reassert_cu_mask();
+  typedef hipError_t (*F)(int*);
+  REAL(hipGetDeviceCount, F);
+  return real_fn(count);
+}
+
+__attribute__((visibility("default"))) hipError_t hipSetDevice(int dev) {
+  reassert_cu_mask();
+  typedef hipError_t (*F)(int);
+  REAL(hipSetDevice, F);
+  return real_fn(dev);
+}
+
+__attribute__((visibility("default"))) hipError_t hipGetDevice(int* dev) {
+  reassert_cu_mask();
+  typedef hipError_t (*F)(int*);
+  REAL(hipGetDevice, F);
+  return real_fn(dev);
 }
 
 // introspection for tests and the workload's report: bytes in use / limit on `dev` (-1: no limit)

@@ -224,6 +224,34 @@ def test_vgpu_guard_caps_torch_and_forces_the_cu_mask(tmp_path):
     assert 0.15 * full < g["tflops"] < 0.40 * full, (g["tflops"], full)  # 64 of 256 CUs (27 % measured in r02)
 
 
+def test_vgpu_guard_holds_against_an_in_process_rewrite(tmp_path):
+    """The program itself sets HSA_CU_MASK to every CU after the guard loaded and before torch brings up
+    the runtime (Python's os.environ, then `import torch`): the guard sets the share's mask back at the
+    first HIP call, so the MFMA loop still runs on the share's 64 CUs."""
+    from gpu_topology_on_k8s_amd._native import binary
+
+    conf = tmp_path / "gtk-vgpu.conf"
+    conf.write_text(f"hbm_limit 0 {16 << 30}\ncu_mask 0:0-63\n")
+    env = {k: v for k, v in os.environ.items() if k not in _STRIP}
+    env.pop("HSA_CU_MASK", None)
+    env.update(GTK_VGPU_CONFIG=str(conf))
+    env["LD_PRELOAD"] = (env["LD_PRELOAD"] + ":" if env.get("LD_PRELOAD") else "") + str(binary("libgtk_vgpu.so"))
+    child = ("import json, os\nos.environ['HSA_CU_MASK'] = '0:0-255'\nimport torch\n"
+             "from gpu_topology_on_k8s_amd.ops.probe import warmup\ntorch.cuda.init()\n"
+             "print(json.dumps({'tflops': warmup(0, 30.0)['tflops']}))")
+    p = subprocess.run([sys.executable, "-c", child], capture_output=True, text=True, timeout=240, cwd=REPO, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    g = json.loads(p.stdout.strip().splitlines()[-1])
+    base_env = {k: v for k, v in os.environ.items() if k not in _STRIP}
+    base_env.pop("HSA_CU_MASK", None)
+    q = subprocess.run([sys.executable, "-c", "import json; from gpu_topology_on_k8s_amd.ops.probe import warmup;"
+                        "print(json.dumps(warmup(0, 30.0)))"], capture_output=True, text=True, timeout=240, cwd=REPO, env=base_env)
+    assert q.returncode == 0, q.stderr[-3000:]
+    full = json.loads(q.stdout.strip().splitlines()[-1])["tflops"]
+    print(json.dumps({"rewritten_then_guarded_tflops": g["tflops"], "full_tflops": full}))
+    assert 0.15 * full < g["tflops"] < 0.40 * full, (g["tflops"], full)
+
+
 def test_doctor_inside_a_guarded_half_gpu_pod(tmp_path):
     """A whole pod start on the real GPU: the device plugin (real discovery, 2 time slices, guard on)
     allocates slice 0; a process gets exactly what the container would (the Allocate envs, the guard

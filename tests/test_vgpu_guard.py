@@ -75,6 +75,42 @@ def test_guard_caps_hbm_and_forces_the_cu_mask(tmp_path, mode):
     assert out["used_end"] == 7 * GiB + (1 << 20)  # 2 (managed) + 5 (async) GiB + one pitched 1 MiB row
 
 
+REWRITE_CHILD = r"""
+import ctypes, json, os, sys
+os.environ["HSA_CU_MASK"] = "0:0-255"          # the program rewrites the mask before any HIP call
+rt = ctypes.CDLL(sys.argv[1], mode=ctypes.RTLD_GLOBAL if sys.argv[2] == "global" else ctypes.RTLD_LOCAL)
+g = ctypes.CDLL(None) if "libgtk_vgpu" in os.environ.get("LD_PRELOAD", "") else rt  # as the application resolves it
+n = ctypes.c_int()
+getattr(g, sys.argv[3])(*([ctypes.byref(n)] if sys.argv[3] in ("hipGetDeviceCount", "hipGetDevice") else [ctypes.c_int(0)]))
+rt.fake_hip_init_mask.restype = ctypes.c_char_p
+print(json.dumps({"init_mask": rt.fake_hip_init_mask().decode()}))
+"""
+
+
+@pytest.mark.parametrize("mode,first", [("local", "hipGetDeviceCount"), ("global", "hipSetDevice"), ("local", "hipGetDevice")])
+def test_guard_sets_the_mask_back_before_the_runtime_initialises(tmp_path, mode, first):
+    """A program that rewrites HSA_CU_MASK in its own environment (Python's os.environ before
+    `import torch`) after the guard's constructor ran: the guard sets the share's mask back at the
+    first intercepted HIP call, before forwarding it, so the runtime initialises with the share's mask
+    (the stand-in runtime records what it read at its first call, as ROCr reads the variable once)."""
+    fake = os.path.join(os.path.dirname(str(binary("libgtk_vgpu.so"))), "fake_hip", "libamdhip64.so")
+    conf = tmp_path / "gtk-vgpu.conf"
+    conf.write_text(f"hbm_limit 0 {8 * GiB}\ncu_mask 0:64-127\n")
+    env = dict(os.environ, GTK_VGPU_CONFIG=str(conf), FAKE_HIP_DEVICE="0")
+    guard = str(binary("libgtk_vgpu.so"))
+    env["LD_PRELOAD"] = (env["LD_PRELOAD"] + ":" if env.get("LD_PRELOAD") else "") + guard
+    p = subprocess.run([sys.executable, "-c", REWRITE_CHILD, fake, mode, first], capture_output=True, text=True, timeout=60,
+                       env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert json.loads(p.stdout.strip().splitlines()[-1])["init_mask"] == "0:64-127"
+    # without the guard the runtime would have read the program's own value
+    env.pop("LD_PRELOAD")
+    q = subprocess.run([sys.executable, "-c", REWRITE_CHILD, fake, mode, first], capture_output=True, text=True, timeout=60,
+                       env=env)
+    assert q.returncode == 0, q.stderr[-2000:]
+    assert json.loads(q.stdout.strip().splitlines()[-1])["init_mask"] == "0:0-255"
+
+
 def test_guard_without_config_is_a_pass_through(tmp_path):
     out = _run(tmp_path, "local", config=False)
     assert out["active"] is None and out["env_mask"] == "0:0-255"
