@@ -650,6 +650,12 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv4_kernel(const u16* __res
 //   3. runs S and dP, then the softmax / dS VALU interleaved with the deferred dV/dK MFMAs, whose
 //      operands are all in registers already.
 // Same MFMAs in the same order per accumulator as v4, so the results are bit-identical.
+// kSFirst: read this slice's Q / dO rows (and lse / delta) first, start S / dP on them, and issue the
+// previous slice's 32 transposed reads BETWEEN those MFMAs.  In the v5 order all 56 reads of a step
+// were issued before its first MFMA; a wave has at most 15 LDS reads in flight (4-bit lgkmcnt), so
+// the MFMA pipe idled while the LDS drained ~40 of them (`s_waitcnt lgkmcnt(14)` after 56 reads in
+// the ISA).  Same MFMAs in the same order: bit-identical.
+template <bool kSFirst>
 __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv5_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
                                                                 const u16* __restrict__ v, const u16* __restrict__ dout,
                                                                 const float* __restrict__ lse2, const float* __restrict__ delta,
@@ -719,38 +725,63 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv5_kernel(const u16* __res
     const char* buf = smem + rb * SL_BYTES;
     const char* pbuf = smem + ((rb + 2) % 3) * SL_BYTES;  // slice idx-1 (its deferred dV/dK products)
     // (1) every LDS operand of this step, while no DMA is outstanding
-    bf16x8 ta[16];
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      ta[4 * dt + 0] = tr_frag(pbuf + SL_DO, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt);
-      ta[4 * dt + 1] = tr_frag(pbuf + SL_DO, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt);
-      ta[4 * dt + 2] = tr_frag(pbuf + SL_Q, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt);
-      ta[4 * dt + 3] = tr_frag(pbuf + SL_Q, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt);
-    }
+    bf16x8 ta[16], qa[8], da[8];
     f32x4 lq[4], dq[4];
+    auto read_t = [&]() {  // the previous slice's dO^T / Q^T (the deferred dV / dK products)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      lq[g] = *reinterpret_cast<const f32x4*>(buf + SL_LSE + 4 * (8 * g + 4 * hh));
-      dq[g] = *reinterpret_cast<const f32x4*>(buf + SL_DEL + 4 * (8 * g + 4 * hh));
-    }
-    bf16x8 qa[8], da[8];
+      for (int dt = 0; dt < 4; ++dt) {
+        ta[4 * dt + 0] = tr_frag(pbuf + SL_DO, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt);
+        ta[4 * dt + 1] = tr_frag(pbuf + SL_DO, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt);
+        ta[4 * dt + 2] = tr_frag(pbuf + SL_Q, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt);
+        ta[4 * dt + 3] = tr_frag(pbuf + SL_Q, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt);
+      }
+    };
+    auto read_s = [&]() {  // this slice's Q / dO rows (S and dP), then lse / delta (the softmax)
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      qa[s] = lds_b128(buf + SL_Q, swz(r, 2 * s + hh));
-      da[s] = lds_b128(buf + SL_DO, swz(r, 2 * s + hh));
-    }
-    // (2) the next slice lands in slot (rb+1)%3 = slice idx-2's, read for the last time last step
-    if (idx + 1 < nslice) sload(idx + 1, smem + ((rb + 1) % 3) * SL_BYTES);
+      for (int s = 0; s < 8; ++s) {
+        qa[s] = lds_b128(buf + SL_Q, swz(r, 2 * s + hh));
+        da[s] = lds_b128(buf + SL_DO, swz(r, 2 * s + hh));
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        lq[g] = *reinterpret_cast<const f32x4*>(buf + SL_LSE + 4 * (8 * g + 4 * hh));
+        dq[g] = *reinterpret_cast<const f32x4*>(buf + SL_DEL + 4 * (8 * g + 4 * hh));
+      }
+    };
     const int j = idx % nqt;
     const int qbase = (qt0 + j) * QT;
     const bool dead = !active(idx);
     const int kill_from = dead ? -(1 << 30) : (masked(idx) ? qbase : 1 << 30);
-    // (3) S and dP
     f32x16 sacc = f32x16{}, dpacc = f32x16{};
+    if (kSFirst) {
+      // (2') S and dP as soon as this slice's rows are in, the previous slice's 32 transposed reads
+      // issued between their MFMAs ({1 MFMA, 2 LDS reads} x 16), then the next slice's DMA: every
+      // LDS read of the step still precedes it
+      read_s();
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      sacc = mfma(qa[s], kf[s], sacc);
-      dpacc = mfma(da[s], vf[s], dpacc);
+      for (int s = 0; s < 8; ++s) {
+        sacc = mfma(qa[s], kf[s], sacc);
+        dpacc = mfma(da[s], vf[s], dpacc);
+      }
+      read_t();
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (idx + 1 < nslice) sload(idx + 1, smem + ((rb + 1) % 3) * SL_BYTES);
+    } else {
+      read_t();
+      read_s();
+      // (2) the next slice lands in slot (rb+1)%3 = slice idx-2's, read for the last time last step
+      if (idx + 1 < nslice) sload(idx + 1, smem + ((rb + 1) % 3) * SL_BYTES);
+      // (3) S and dP
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        sacc = mfma(qa[s], kf[s], sacc);
+        dpacc = mfma(da[s], vf[s], dpacc);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     // (4) softmax / dS of this slice under the deferred dV/dK MFMAs of the previous one
@@ -983,8 +1014,8 @@ std::vector<at::Tensor> attn_bwd_v4(const at::Tensor& dout, const at::Tensor& q,
 }
 
 // default backward: delta, dK/dV v5 (software-pipelined slices, operands read ahead of the DMA), dQ v2
-std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                 const at::Tensor& out, const at::Tensor& lse, double scale) {
+std::vector<at::Tensor> attn_bwd_order(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                       const at::Tensor& out, const at::Tensor& lse, double scale, bool s_first) {
   check_qkv(q, k, v);
   const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
   TORCH_CHECK(dout.is_contiguous() && out.is_contiguous() && dout.numel() == q.numel() && out.numel() == q.numel(),
@@ -995,11 +1026,26 @@ std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, co
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
                      delta.data_ptr<float>(), B, H, S);
   const float c = (float)(scale * 1.4426950408889634);
-  hipLaunchKernelGGL(attn_bwd_dkdv5_kernel, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
-                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
+  if (s_first)
+    hipLaunchKernelGGL(attn_bwd_dkdv5_kernel<true>, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v),
+                       bp(dout), lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
+  else
+    hipLaunchKernelGGL(attn_bwd_dkdv5_kernel<false>, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v),
+                       bp(dout), lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
   hipLaunchKernelGGL(attn_bwd_dq2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
                      lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
   return {dq, dk, dv};
+}
+
+std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                 const at::Tensor& out, const at::Tensor& lse, double scale) {
+  return attn_bwd_order(dout, q, k, v, out, lse, scale, true);
+}
+
+// v5 with the previous slice's transposed reads issued first (the round-3 order): A/B reference
+std::vector<at::Tensor> attn_bwd_v5t(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                     const at::Tensor& out, const at::Tensor& lse, double scale) {
+  return attn_bwd_order(dout, q, k, v, out, lse, scale, false);
 }
 
 }  // namespace gtk_attn

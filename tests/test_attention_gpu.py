@@ -77,6 +77,9 @@ def test_attention_bwd_v4_matches_v3(fused, B, H, Hkv, S):
     g5 = hip.attn_bwd(do, q, k, v, o, lse, 128 ** -0.5)  # the default, v5: operands read ahead of the DMA
     for name, a, b in zip(("dq", "dk", "dv"), g5, g3):
         assert torch.equal(a, b), (name, _rel(a, b))
+    g5t = hip.attn_bwd_v5t(do, q, k, v, o, lse, 128 ** -0.5)  # v5 with the transposed reads first
+    for name, a, b in zip(("dq", "dk", "dv"), g5t, g3):
+        assert torch.equal(a, b), (name, "v5t", _rel(a, b))
     g4 = hip.attn_bwd_v4(do, q, k, v, o, lse, 128 ** -0.5)  # v4: operands read at their use
     for name, a, b in zip(("dq", "dk", "dv"), g4, g3):
         assert torch.equal(a, b), (name, "v4", _rel(a, b))
