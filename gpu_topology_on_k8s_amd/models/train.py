@@ -113,7 +113,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
           dgrad_nn: str = "",
           zero1: bool = False, save_dir: Optional[str] = None, save_every: int = 0, resume: Optional[str] = None,
           keep: int = 2, fuse_residual: bool = True, overlap_norm: bool = False, same_data: bool = False,
-          graph: str = "auto", conv: str = "hip", cpu_bind: str = "auto") -> Dict[str, object]:
+          graph: str = "auto", conv: str = "hip", cpu_bind: str = "auto", repeat_batch: bool = False) -> Dict[str, object]:
     env = _init_dist(device_kind)
     if placement == "auto":  # inside a pod the allocation decides; on a bare node, the placement core
         placement = "pod" if os.environ.get("GTK_GPU_GROUP") else "best"
@@ -193,14 +193,18 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
     if ckpt is not None and save_every > 0:
         ckpt.prepare()
     done = [start_step]
+    first: Dict[str, object] = {}
 
     def batch_tokens():
         if mnist and use_graph:  # one HIP launch, indexed by the optimizer's device step counter
             return model.synthetic_batch_dev(batch, opt.t_dev, seed=data_seed)
         if mnist:
             return model.synthetic_batch(batch, gen)
-        t = torch.randint(0, cfg.vocab, (batch, seq + 1), generator=gen)
-        t = t.to(device, non_blocking=True)
+        if repeat_batch and "t" in first:  # memorisation check: the same tokens every step
+            t = first["t"]
+        else:
+            t = torch.randint(0, cfg.vocab, (batch, seq + 1), generator=gen)
+            t = first["t"] = t.to(device, non_blocking=True)
         return t[:, :-1], t[:, 1:]
 
     def body() -> torch.Tensor:
@@ -299,6 +303,8 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "loss_last": float(losses[-1]),
         "losses": [float(x) for x in losses],
         "same_data": same_data,
+        "repeat_batch": repeat_batch,
+        "lr": lr,
         "buckets": ar.stats["buckets"],
         "zero1": zero1,
         "optimizer_state_gb": opt.state_bytes() / 1e9,
@@ -370,12 +376,17 @@ def main(argv=None) -> int:
                          "slice alone), GTK_CPUSET only (env), or leave the threads unbound (off)")
     ap.add_argument("--overlap-norm", action="store_true",
                     help="clipping norm per bucket on a side stream as buckets complete (measured no gain at world 1)")
+    ap.add_argument("--repeat-batch", action="store_true",
+                    help="train on the first batch at every step: uniform random tokens carry nothing to learn, one "
+                         "repeated batch does, so the loss must fall (end-to-end check of forward, backward and AdamW)")
+    ap.add_argument("--lr", type=float, default=3e-4)
     a = ap.parse_args(argv)
-    train(a.model, a.batch, a.seq, a.steps, a.warmup, a.device, a.placement, a.discovery, a.bucket_mb, a.checkpoint, attn=a.attn,
+    train(a.model, a.batch, a.seq, a.steps, a.warmup, a.device, a.placement, a.discovery, a.bucket_mb, a.checkpoint, lr=a.lr, attn=a.attn,
           gemm_tuning=a.gemm_tuning, gemm_table=a.gemm_table, gemm_layout=a.gemm_layout,
           overlap_transposes=a.overlap_transposes, dgrad_nn=a.dgrad_nn, zero1=a.zero1, save_dir=a.save_dir, save_every=a.save_every,
           resume=a.resume, keep=a.keep, fuse_residual=not a.no_fuse_residual,
-          overlap_norm=a.overlap_norm, same_data=a.same_data, graph=a.graph, conv=a.conv, cpu_bind=a.cpu_bind)
+          overlap_norm=a.overlap_norm, same_data=a.same_data, graph=a.graph, conv=a.conv, cpu_bind=a.cpu_bind,
+          repeat_batch=a.repeat_batch)
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0

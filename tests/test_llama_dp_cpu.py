@@ -289,6 +289,26 @@ def test_train_entry_cpu_single_rank(zero1):
     assert out["zero1"] == zero1 and out["optimizer_state_gb"] > 0
 
 
+def test_train_repeat_batch_memorises():
+    """--repeat-batch: one batch at every step must be learnt (forward, backward and AdamW end to end);
+    the same run on the GPU at the Llama-3-8B shape is profiles/r03_learn/."""
+    from gpu_topology_on_k8s_amd.models.train import train
+
+    if dist.is_initialized():
+        pytest.skip("process group already initialised")
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    try:
+        out = train("tiny", batch=2, seq=32, steps=25, warmup=0, device_kind="cpu", log=False, lr=3e-3,
+                    repeat_batch=True)
+    finally:
+        dist.destroy_process_group()
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+            os.environ.pop(k, None)
+    losses = out["losses"]
+    assert out["repeat_batch"] and len(losses) == 25
+    assert losses[-1] < 0.5 * losses[0], losses
+
+
 def test_best_vs_worst_harness_cpu_dry_run(tmp_path):
     """bench/train_llama.py (BASELINE config 5 / Gaia Exp. 6) end to end on CPU: two 2-rank gloo jobs
     placed on a fake 8-device node, best and worst being different real device sets (k < n)."""

@@ -49,6 +49,12 @@ case "$mode" in
     step llama8b_b4 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
     step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
     ;;
+  learn)
+    # end-to-end learning at the config-5 shape: one repeated batch must be memorised, fresh uniform
+    # tokens cannot be learnt below ln(vocab) (profiles/r03_learn)
+    step learn_repeat 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 40 --warmup 0 --repeat-batch
+    step learn_random 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 40 --warmup 0
+    ;;
   cumask)
     # MFMA rate and HBM copy under HSA_CU_MASK (the time-sliced shares' spatial split, profiles/r02_cumask)
     for m in "" "0:0-127" "0:0-63" "0:0-31,128-159"; do
