@@ -180,25 +180,26 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const u16* __restrict_
   }
 }
 
-// Column sums of [P, D] fp32 partials.  Grid (ceil(D/64), kColSplit): each block owns 64 columns
-// (one 256-B coalesced row segment per wave-instruction) and a 1/kColSplit slice of the rows; its 4
-// waves stride the slice, combine through LDS, and one fp32 atomic per column per block lands in acc.
-constexpr int kColSplit = 8;
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, float* __restrict__ acc, int P, int D) {
-  __shared__ float red[4][64];
+// dW = column sums of the [P, D] fp32 partials, written as bf16 in one launch.  Each block owns 64
+// columns (one 256-B coalesced row segment per wave-instruction); its 16 waves stride the rows and
+// combine through LDS in a fixed order: no atomics, so dW is bitwise reproducible run to run.
+constexpr int kColWaves = 16;
+__global__ __launch_bounds__(64 * kColWaves) void colsum_bf16_kernel(const float* __restrict__ part, u16* __restrict__ dw,
+                                                                     int P, int D) {
+  __shared__ float red[kColWaves][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + lane;
   float s = 0.f;
   if (col < D)
-    for (int p = blockIdx.y * 4 + wave; p < P; p += kColSplit * 4) s += part[(size_t)p * D + col];
+    for (int p = wave; p < P; p += kColWaves) s += part[(size_t)p * D + col];
   red[wave][lane] = s;
   __syncthreads();
-  if (wave == 0 && col < D) atomicAdd(acc + col, red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
-}
-
-__global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restrict__ x, u16* __restrict__ y, int n) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) y[i] = f2bf(x[i]);
+  if (wave == 0 && col < D) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < kColWaves; ++i) t += red[i][lane];
+    dw[col] = f2bf(t);
+  }
 }
 
 template <int NV>
@@ -307,10 +308,8 @@ std::vector<at::Tensor> rmsnorm_bwd_impl(const at::Tensor& dy, const at::Tensor&
   } else {
     part.zero_();
   }
-  auto acc = at::zeros({D}, x.options().dtype(at::kFloat));
-  hipLaunchKernelGGL(colsum_kernel, dim3((D + 63) / 64, kColSplit), dim3(256), 0, cur_stream(), part.data_ptr<float>(),
-                     acc.data_ptr<float>(), grid * 4, D);
-  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((D + 255) / 256), dim3(256), 0, cur_stream(), acc.data_ptr<float>(), bpm(dw), D);
+  hipLaunchKernelGGL(colsum_bf16_kernel, dim3((D + 63) / 64), dim3(64 * kColWaves), 0, cur_stream(), part.data_ptr<float>(),
+                     bpm(dw), grid * 4, D);
   return {dx, dw};
 }
 

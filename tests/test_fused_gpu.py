@@ -63,6 +63,21 @@ def test_add_rmsnorm_fwd_bwd(hip, M, D):
     assert _rel(dw, wf.grad) < 1e-2
 
 
+def test_rmsnorm_weight_grad_is_deterministic(hip):
+    """dW is reduced in a fixed order (no atomics): bit-identical launch to launch at the Llama-3-8B
+    shape [16384, 4096], and exact against an fp64 column sum of the same bf16 operands to bf16 rounding."""
+    torch.manual_seed(3)
+    M, D = 16384, 4096
+    x = torch.randn(M, D, device="cuda", dtype=torch.bfloat16)
+    w = (torch.rand(D, device="cuda") + 0.5).to(torch.bfloat16)
+    dy = torch.randn(M, D, device="cuda", dtype=torch.bfloat16)
+    _, rstd = hip.rmsnorm_fwd(x, w, 1e-5)
+    dws = [hip.rmsnorm_bwd(dy, x, w, rstd)[1] for _ in range(3)]
+    assert all(torch.equal(dws[0], d) for d in dws[1:])
+    ref = (dy.double() * x.double() * rstd.double()[:, None]).sum(0)
+    assert _rel(dws[0], ref) < 4e-3
+
+
 def test_llama_fused_residual_matches_unfused_gpu():
     """Whole tiny model: add+RMSNorm in one kernel (default) vs separate adds — same loss and
     gradients to bf16 rounding."""
