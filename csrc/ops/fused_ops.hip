@@ -180,24 +180,27 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const u16* __restrict_
   }
 }
 
-// dW = column sums of the [P, D] fp32 partials, written as bf16 in one launch.  Each block owns 64
-// columns (one 256-B coalesced row segment per wave-instruction); its 16 waves stride the rows and
-// combine through LDS in a fixed order: no atomics, so dW is bitwise reproducible run to run.
-constexpr int kColWaves = 16;
+// dW = column sums of the [P, D] fp32 partials, written as bf16 in one launch.  Each block owns 16
+// columns so that D = 4096 gives 256 blocks, one per CU; a wave-instruction reads 4 rows x 64 B.  The
+// 64 row streams of a block (16 waves x 4 lane groups) combine through LDS in a fixed order: no
+// atomics, so dW is bitwise reproducible run to run.
+constexpr int kColWaves = 16, kColW = 16;
 __global__ __launch_bounds__(64 * kColWaves) void colsum_bf16_kernel(const float* __restrict__ part, u16* __restrict__ dw,
                                                                      int P, int D) {
-  __shared__ float red[kColWaves][64];
+  constexpr int kStreams = kColWaves * (64 / kColW);
+  __shared__ float red[kStreams][kColW];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + lane;
+  const int c = lane % kColW, stream = wave * (64 / kColW) + lane / kColW;
+  const int col = blockIdx.x * kColW + c;
   float s = 0.f;
   if (col < D)
-    for (int p = wave; p < P; p += kColWaves) s += part[(size_t)p * D + col];
-  red[wave][lane] = s;
+    for (int p = stream; p < P; p += kStreams) s += part[(size_t)p * D + col];
+  red[stream][c] = s;
   __syncthreads();
-  if (wave == 0 && col < D) {
+  if (threadIdx.x < kColW && col < D) {
     float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < kColWaves; ++i) t += red[i][lane];
+#pragma unroll 8
+    for (int i = 0; i < kStreams; ++i) t += red[i][c];
     dw[col] = f2bf(t);
   }
 }
@@ -308,7 +311,7 @@ std::vector<at::Tensor> rmsnorm_bwd_impl(const at::Tensor& dy, const at::Tensor&
   } else {
     part.zero_();
   }
-  hipLaunchKernelGGL(colsum_bf16_kernel, dim3((D + 63) / 64), dim3(64 * kColWaves), 0, cur_stream(), part.data_ptr<float>(),
+  hipLaunchKernelGGL(colsum_bf16_kernel, dim3((D + kColW - 1) / kColW), dim3(64 * kColWaves), 0, cur_stream(), part.data_ptr<float>(),
                      bpm(dw), grid * 4, D);
   return {dx, dw};
 }
