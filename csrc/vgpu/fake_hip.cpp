@@ -1,88 +1,151 @@
-// Stand-in HIP runtime (host-only) for CPU tests of libgtk_vgpu.so: the allocation entry points the
-// guard intercepts, backed by tiny host allocations (the requested size is only bookkept), a current
-// device from $FAKE_HIP_DEVICE and a 64 GiB device.  Built as bin/fake_hip/libamdhip64.so so the
-// guard's fallback lookup (a runtime loaded RTLD_LOCAL, found by name among the loaded objects) is
-// exercised exactly as with the PyTorch wheel's bundled runtime.  Like ROCr, it reads HSA_CU_MASK
-// once, at the first call into it (its "initialisation"); fake_hip_init_mask() returns what it read.
+// Stand-in HIP runtime (host-only) for CPU tests of libgtk_vgpu.so.  Layered like the real one: every
+// entry point initialises the stand-in ROCr (fake_hsa.cpp, linked as libhsa-runtime64.so) through
+// hsa_init, device allocations come from the current GPU's global pool (hsa_amd_memory_pool_allocate),
+// host allocations from the CPU pool, hipMemCreate from hsa_amd_vmem_handle_create, and a stream is
+// an HSA queue on the current GPU.  Built as bin/fake_hip/libamdhip64.so so the guard's fallback
+// lookup (a runtime loaded RTLD_LOCAL, found by name among the loaded objects) is exercised exactly
+// as with the PyTorch wheel's bundled runtime.  The current device comes from $FAKE_HIP_DEVICE; the
+// device has 64 GiB.
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
 #include <cstdlib>
 #include <cstring>
 
 extern "C" {
+// the stand-in ROCr's test hooks
+const char* fake_hsa_init_mask();
+const char* fake_hsa_queue_mask(const hsa_queue_t* q);
+uint64_t fake_hsa_gpu_pool(int gpu);
+uint64_t fake_hsa_cpu_pool();
+uint64_t fake_hsa_gpu_agent(int gpu);
 
 typedef int hipError_t;
 static const unsigned long long kTotal = 64ull << 30;
-static char g_init_mask[4096] = "(never initialised)";
-static int g_inited = 0;
+static const hipError_t kOk = 0, kInvalid = 1, kOom = 2;
 
-static void fake_init() {
-  if (g_inited) return;
-  g_inited = 1;
-  const char* m = std::getenv("HSA_CU_MASK");
-  std::strncpy(g_init_mask, m ? m : "", sizeof(g_init_mask) - 1);
+struct hipExtent {
+  size_t width, height, depth;
+};
+struct hipPitchedPtr {
+  void* ptr;
+  size_t pitch, xsize, ysize;
+};
+
+static int cur() {
+  const char* e = std::getenv("FAKE_HIP_DEVICE");
+  return e ? std::atoi(e) : 0;
 }
 
-__attribute__((visibility("default"))) const char* fake_hip_init_mask() { return g_init_mask; }
+static void init() { hsa_init(); }
+
+static hipError_t status(hsa_status_t s) {
+  return s == HSA_STATUS_SUCCESS ? kOk : s == HSA_STATUS_ERROR_OUT_OF_RESOURCES ? kOom : kInvalid;
+}
+
+static hipError_t dev_alloc(void** p, size_t n) {
+  init();
+  if (!p) return kInvalid;
+  hipError_t e = status(hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t{fake_hsa_gpu_pool(cur())}, n, 0, p));
+  if (e != kOk) *p = nullptr;
+  return e;
+}
+
+__attribute__((visibility("default"))) const char* fake_hip_init_mask() { return fake_hsa_init_mask(); }
+__attribute__((visibility("default"))) const char* fake_hip_stream_mask(void* stream) {
+  return fake_hsa_queue_mask(static_cast<const hsa_queue_t*>(stream));
+}
 
 __attribute__((visibility("default"))) hipError_t hipInit(unsigned int) {
-  fake_init();
-  return 0;
+  init();
+  return kOk;
 }
 __attribute__((visibility("default"))) hipError_t hipGetDeviceCount(int* n) {
-  fake_init();
+  init();
   if (n) *n = 2;
-  return 0;
+  return kOk;
 }
 __attribute__((visibility("default"))) hipError_t hipSetDevice(int) {
-  fake_init();
-  return 0;
+  init();
+  return kOk;
 }
-
 __attribute__((visibility("default"))) hipError_t hipGetDevice(int* d) {
-  fake_init();
-  const char* e = std::getenv("FAKE_HIP_DEVICE");
-  *d = e ? std::atoi(e) : 0;
-  return 0;
+  init();
+  *d = cur();
+  return kOk;
+}
+__attribute__((visibility("default"))) hipError_t hipRuntimeGetVersion(int* v) {
+  init();
+  if (v) *v = 70200000;
+  return kOk;
+}
+__attribute__((visibility("default"))) hipError_t hipDeviceGetAttribute(int* v, int, int) {
+  init();
+  if (v) *v = 256;
+  return kOk;
 }
 
-static hipError_t fake_alloc(void** p, size_t n) {
-  fake_init();
-  if (!p) return 1;
-  *p = std::malloc(16 + (n & 7));  // distinct pointers; the size itself is never touched
-  return *p ? 0 : 2;
-}
-
-__attribute__((visibility("default"))) hipError_t hipMalloc(void** p, size_t n) { return fake_alloc(p, n); }
-__attribute__((visibility("default"))) hipError_t hipExtMallocWithFlags(void** p, size_t n, unsigned int) {
-  return fake_alloc(p, n);
-}
-__attribute__((visibility("default"))) hipError_t hipMallocManaged(void** p, size_t n, unsigned int) { return fake_alloc(p, n); }
-__attribute__((visibility("default"))) hipError_t hipMallocAsync(void** p, size_t n, void*) { return fake_alloc(p, n); }
-__attribute__((visibility("default"))) hipError_t hipMallocFromPoolAsync(void** p, size_t n, void*, void*) {
-  return fake_alloc(p, n);
-}
+__attribute__((visibility("default"))) hipError_t hipMalloc(void** p, size_t n) { return dev_alloc(p, n); }
+__attribute__((visibility("default"))) hipError_t hipExtMallocWithFlags(void** p, size_t n, unsigned int) { return dev_alloc(p, n); }
+__attribute__((visibility("default"))) hipError_t hipMallocManaged(void** p, size_t n, unsigned int) { return dev_alloc(p, n); }
+__attribute__((visibility("default"))) hipError_t hipMallocAsync(void** p, size_t n, void*) { return dev_alloc(p, n); }
+__attribute__((visibility("default"))) hipError_t hipMallocFromPoolAsync(void** p, size_t n, void*, void*) { return dev_alloc(p, n); }
 __attribute__((visibility("default"))) hipError_t hipMallocPitch(void** p, size_t* pitch, size_t w, size_t h) {
-  if (pitch) *pitch = (w + 255) & ~(size_t)255;
-  return fake_alloc(p, w * h);
+  const size_t pw = (w + 255) & ~(size_t)255;
+  if (pitch) *pitch = pw;
+  return dev_alloc(p, pw * h);
+}
+__attribute__((visibility("default"))) hipError_t hipMalloc3D(hipPitchedPtr* pp, hipExtent ext) {
+  if (!pp) return kInvalid;
+  const size_t pw = (ext.width + 255) & ~(size_t)255;
+  pp->pitch = pw;
+  pp->xsize = ext.width;
+  pp->ysize = ext.height;
+  return dev_alloc(&pp->ptr, pw * ext.height * (ext.depth ? ext.depth : 1));
+}
+__attribute__((visibility("default"))) hipError_t hipHostMalloc(void** p, size_t n, unsigned int) {
+  init();
+  if (!p) return kInvalid;
+  return status(hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t{fake_hsa_cpu_pool()}, n, 0, p));
 }
 __attribute__((visibility("default"))) hipError_t hipFree(void* p) {
-  std::free(p);
-  return 0;
+  init();
+  return p ? status(hsa_amd_memory_pool_free(p)) : kOk;
 }
-__attribute__((visibility("default"))) hipError_t hipFreeAsync(void* p, void*) {
-  std::free(p);
-  return 0;
-}
+__attribute__((visibility("default"))) hipError_t hipFreeAsync(void* p, void*) { return hipFree(p); }
+__attribute__((visibility("default"))) hipError_t hipHostFree(void* p) { return hipFree(p); }
 __attribute__((visibility("default"))) hipError_t hipMemCreate(void** h, size_t n, const void*, unsigned long long) {
-  return fake_alloc(h, n);
+  init();
+  hsa_amd_vmem_alloc_handle_t vh{0};
+  hipError_t e = status(hsa_amd_vmem_handle_create(hsa_amd_memory_pool_t{fake_hsa_gpu_pool(cur())}, n, MEMORY_TYPE_NONE, 0, &vh));
+  if (h) *h = e == kOk ? reinterpret_cast<void*>(vh.handle) : nullptr;
+  return e;
 }
 __attribute__((visibility("default"))) hipError_t hipMemRelease(void* h) {
-  std::free(h);
-  return 0;
+  return status(hsa_amd_vmem_handle_release(hsa_amd_vmem_alloc_handle_t{reinterpret_cast<uint64_t>(h)}));
 }
 __attribute__((visibility("default"))) hipError_t hipMemGetInfo(size_t* f, size_t* t) {
-  fake_init();
+  init();
   if (f) *f = kTotal;
   if (t) *t = kTotal;
-  return 0;
+  return kOk;
+}
+
+// a stream is an HSA queue on the current device (its handle is the queue's address here)
+__attribute__((visibility("default"))) hipError_t hipStreamCreate(void** stream) {
+  init();
+  hsa_queue_t* q = nullptr;
+  hipError_t e = status(hsa_queue_create(hsa_agent_t{fake_hsa_gpu_agent(cur())}, 4096, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr,
+                                         0, 0, &q));
+  if (stream) *stream = q;
+  return e;
+}
+__attribute__((visibility("default"))) hipError_t hipExtStreamCreateWithCUMask(void** stream, uint32_t count, const uint32_t* mask) {
+  hipError_t e = hipStreamCreate(stream);
+  if (e != kOk) return e;
+  return status(hsa_amd_queue_cu_set_mask(static_cast<hsa_queue_t*>(*stream), count * 32, mask));  // words -> bits
+}
+__attribute__((visibility("default"))) hipError_t hipStreamDestroy(void* stream) {
+  return status(hsa_queue_destroy(static_cast<hsa_queue_t*>(stream)));
 }
 }

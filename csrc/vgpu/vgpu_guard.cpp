@@ -7,21 +7,26 @@
 // (GTK_GPU_FRACTION); both were cooperative: a container could rewrite its environment, and only the
 // framework's own training entry point capped its allocator.  This library, which Allocate mounts
 // into the container and preloads (deviceplugin/plugin.py, --share-guard), makes them hold for any
-// HIP program in the pod:
+// HIP program in the pod.  It enforces at the ROCr (HSA) runtime, the layer every HIP entry point
+// ends in, not at a list of HIP calls:
 //
-//   * HBM: every device allocation of the process (hipMalloc, hipExtMallocWithFlags, hipMallocManaged,
-//     hipMallocPitch, hipMallocAsync, hipMallocFromPoolAsync, hipMemCreate) is counted against the
-//     device's limit and refused with hipErrorOutOfMemory beyond it; frees give it back; hipMemGetInfo
-//     reports the share as the device's total, so caching allocators size themselves to it.
-//   * CUs: HSA_CU_MASK is set from the mounted config before the program's own code runs (a
-//     constructor of a preloaded library runs before main and before any HIP call, and the ROCr
-//     runtime reads the variable when it initialises), whatever the container's environment says;
-//     and set again at the first intercepted HIP call (the calls a program makes first: hipInit,
-//     hipGetDeviceCount, hipSetDevice, hipGetDevice, the allocators), in case the program itself
-//     rewrote it before initialising the runtime.
+//   * HBM: every device-memory pool allocation of the process (hsa_amd_memory_pool_allocate on a
+//     GPU's global pool, hsa_amd_vmem_handle_create) is counted against the device's limit and
+//     refused with HSA_STATUS_ERROR_OUT_OF_RESOURCES beyond it (HIP turns that into
+//     hipErrorOutOfMemory).  So hipMalloc, hipMallocPitch/3D/Array, hipMallocAsync pools, hipMemCreate
+//     and the runtime's own device allocations are all charged, once.  Host pools are not counted.
+//     hipMemGetInfo reports the share as the device's total, so caching allocators size themselves
+//     to it.
+//   * CUs: HSA_CU_MASK is set from the mounted config in the constructor (before main), and set back
+//     again in hsa_init, which every HIP program passes through whatever its first HIP call is, in
+//     case the program rewrote it meanwhile.  Independently of the environment, every queue the
+//     runtime creates (hsa_queue_create) gets the share's mask applied, and a program's own
+//     hsa_amd_queue_cu_set_mask (hipExtStreamCreateWithCUMask) is intersected with it: no queue of the
+//     process can run on a CU outside the share.
 //
-// The config is the read-only file ``$GTK_VGPU_CONFIG`` (default /etc/gtk-vgpu.conf) the plugin
-// writes per allocation:
+// The config is the read-only file the plugin mounts at /etc/gtk-vgpu.conf.  When that file exists it
+// is the only one read: $GTK_VGPU_CONFIG (which the pod spec could override) is honoured only where
+// no config is mounted (tests, hand-run jobs).  Format:
 //     hbm_limit <HIP ordinal> <bytes>
 //     cu_mask <HSA_CU_MASK value>
 //     acct <path>                  (optional) pod-wide accounting file, shared read-write
@@ -31,13 +36,15 @@
 // on the slot's first byte, so the kernel drops a crashed process's usage with its lock — whatever PID
 // namespace the pod's containers live in — and the next process reuses the slot.
 //
-// The real HIP entry points are found with dlsym(RTLD_NEXT); when the runtime was loaded RTLD_LOCAL
-// (the PyTorch wheel's bundled libamdhip64, brought in by Python's extension loader) RTLD_NEXT does
-// not see it, so the loaded objects are searched for libamdhip64 and it is re-opened RTLD_NOLOAD.
-// Host-only C++ (g++): no device code, no HIP headers (the few types needed are ABI-identical
-// stand-ins), no link against any HIP library.
+// The real entry points are found with dlsym(RTLD_NEXT); when the runtime was loaded RTLD_LOCAL (the
+// PyTorch wheel's bundled libamdhip64 and its libhsa-runtime64, brought in by Python's extension
+// loader) RTLD_NEXT does not see it, so the loaded objects are searched for the library by name and it
+// is re-opened RTLD_NOLOAD.  Host-only C++ (g++): the HSA headers for the types, no device code, no
+// link against any ROCm library.
 #include <dlfcn.h>
 #include <fcntl.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <link.h>
 #include <pthread.h>
 #include <sys/file.h>
@@ -54,12 +61,16 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <vector>
+
+#ifndef GTK_VGPU_FIXED_CONF
+#define GTK_VGPU_FIXED_CONF "/etc/gtk-vgpu.conf"
+#endif
 
 namespace {
 
 typedef int hipError_t;  // enum hipError_t: int-sized
 constexpr hipError_t kSuccess = 0;
-constexpr hipError_t kOutOfMemory = 2;  // hipErrorOutOfMemory
 constexpr int kMaxDev = 64;
 
 // pod-wide accounting table (the `acct` file)
@@ -85,9 +96,11 @@ struct State {
   pid_t mine_pid = 0;        // the process that claimed `mine` (a forked child claims its own)
   long long limit[kMaxDev];  // bytes; < 0 = no limit on that ordinal
   long long used[kMaxDev];
-  std::unordered_map<void*, std::pair<int, size_t>> ptrs;
-  std::unordered_map<unsigned long long, std::pair<int, size_t>> handles;  // hipMemCreate handles
-  std::string cu_mask;
+  std::unordered_map<void*, std::pair<int, size_t>> ptrs;                  // pool allocations
+  std::unordered_map<uint64_t, std::pair<int, size_t>> handles;            // vmem handles
+  std::string cu_mask;                                                     // HSA_CU_MASK value
+  std::vector<std::vector<uint32_t>> mask_bits;                            // per ordinal; empty = all CUs
+  std::unordered_map<const hsa_queue_t*, int> queues;                      // queue -> GPU ordinal
   State() {
     for (int i = 0; i < kMaxDev; ++i) limit[i] = -1, used[i] = 0;
   }
@@ -98,54 +111,134 @@ State& st() {
   return *s;
 }
 
-void* hip_runtime_handle() {
-  static void* h = nullptr;
-  static std::once_flag once;
-  std::call_once(once, [] {
-    dl_iterate_phdr(
-        [](struct dl_phdr_info* info, size_t, void*) -> int {
-          if (info->dlpi_name && std::strstr(info->dlpi_name, "libamdhip64")) {
-            h = dlopen(info->dlpi_name, RTLD_NOW | RTLD_NOLOAD);
-            return h != nullptr;
-          }
-          return 0;
-        },
-        nullptr);
-  });
-  return h;
+// the loaded object whose path contains `stem`, re-opened without loading anything new
+void* loaded_library(const char* stem) {
+  struct Q {
+    const char* stem;
+    void* h;
+  } q{stem, nullptr};
+  dl_iterate_phdr(
+      [](struct dl_phdr_info* info, size_t, void* data) -> int {
+        Q* q = static_cast<Q*>(data);
+        if (info->dlpi_name && std::strstr(info->dlpi_name, q->stem)) {
+          q->h = dlopen(info->dlpi_name, RTLD_NOW | RTLD_NOLOAD);
+          return q->h != nullptr;
+        }
+        return 0;
+      },
+      &q);
+  return q.h;
 }
 
 template <typename Fn>
-Fn real(const char* name) {
+Fn real(const char* name, const char* stem) {
   void* p = dlsym(RTLD_NEXT, name);
   if (!p) {
-    void* h = hip_runtime_handle();
+    void* h = loaded_library(stem);
     if (h) p = dlsym(h, name);
   }
   if (!p) {
-    std::fprintf(stderr, "gtk-vgpu: cannot resolve %s in the HIP runtime\n", name);
+    std::fprintf(stderr, "gtk-vgpu: cannot resolve %s in %s\n", name, stem);
     std::abort();
   }
   return reinterpret_cast<Fn>(p);
 }
 
 // resolved once per entry point; a function-local static is initialised thread-safely
-#define REAL(name, type) static const type real_fn = real<type>(#name);
+#define REAL_HIP(name, type) static const type real_fn = real<type>(#name, "libamdhip64");
+#define REAL_HSA(name) static const auto real_fn = real<decltype(&::name)>(#name, "libhsa-runtime64");
 
-// The runtime reads HSA_CU_MASK once, when the process's first HIP call initialises it.  A program may
-// have rewritten the variable after the constructor below set it (Python's os.environ before
-// `import torch`), so every intercepted entry point sets it back once, before its first call into the
-// runtime: if that call is the one that initialises it, the runtime reads the share's mask.
-std::atomic<bool> g_mask_reasserted{false};
+// HSA_CU_MASK syntax: "<ordinal>:<cu>[-<cu>][,...]" parts separated by ';'
+std::vector<std::vector<uint32_t>> parse_mask(const std::string& v) {
+  std::vector<std::vector<uint32_t>> out;
+  size_t i = 0;
+  while (i < v.size()) {
+    size_t end = v.find(';', i);
+    if (end == std::string::npos) end = v.size();
+    std::string part = v.substr(i, end - i);
+    i = end + 1;
+    size_t colon = part.find(':');
+    if (colon == std::string::npos) continue;
+    int dev = std::atoi(part.c_str());
+    if (dev < 0 || dev >= kMaxDev) continue;
+    if ((int)out.size() <= dev) out.resize(dev + 1);
+    std::vector<uint32_t>& bits = out[dev];
+    const char* c = part.c_str() + colon + 1;
+    while (*c) {
+      char* e = nullptr;
+      long a = std::strtol(c, &e, 10);
+      if (e == c) break;
+      long b = a;
+      c = e;
+      if (*c == '-') {
+        b = std::strtol(c + 1, &e, 10);
+        c = e;
+      }
+      for (long cu = a; cu <= b && cu >= 0 && cu < 4096; ++cu) {
+        if ((long)bits.size() * 32 <= cu) bits.resize(cu / 32 + 1, 0u);
+        bits[cu / 32] |= 1u << (cu % 32);
+      }
+      if (*c == ',') ++c;
+    }
+  }
+  return out;
+}
 
-void reassert_cu_mask();
+// GPU agents in ROCr's enumeration order (HSA_CU_MASK's and HIP's ordinals) and each one's global
+// memory pools.  Built once, on the first queue or allocation, from the real runtime.
+struct Agents {
+  std::vector<uint64_t> gpus;                       // ordinal -> agent handle
+  std::unordered_map<uint64_t, int> pool_ordinal;   // GPU global pool handle -> ordinal
+};
 
-int current_device() {
-  typedef hipError_t (*F)(int*);
-  REAL(hipGetDevice, F);
-  int d = 0;
-  if (real_fn(&d) != kSuccess || d < 0 || d >= kMaxDev) return 0;
-  return d;
+Agents& agents() {
+  static Agents* a = new Agents();
+  static std::once_flag once;
+  std::call_once(once, [] {
+    REAL_HSA(hsa_iterate_agents);
+    real_fn(
+        [](hsa_agent_t ag, void* data) -> hsa_status_t {
+          static const auto info = real<decltype(&::hsa_agent_get_info)>("hsa_agent_get_info", "libhsa-runtime64");
+          static const auto pools =
+              real<decltype(&::hsa_amd_agent_iterate_memory_pools)>("hsa_amd_agent_iterate_memory_pools", "libhsa-runtime64");
+          Agents* a = static_cast<Agents*>(data);
+          hsa_device_type_t type{};
+          if (info(ag, HSA_AGENT_INFO_DEVICE, &type) != HSA_STATUS_SUCCESS || type != HSA_DEVICE_TYPE_GPU) return HSA_STATUS_SUCCESS;
+          a->gpus.push_back(ag.handle);
+          struct Ctx {
+            Agents* a;
+            int ordinal;
+          } ctx{a, (int)a->gpus.size() - 1};
+          pools(
+              ag,
+              [](hsa_amd_memory_pool_t pool, void* d) -> hsa_status_t {
+                static const auto pinfo =
+                    real<decltype(&::hsa_amd_memory_pool_get_info)>("hsa_amd_memory_pool_get_info", "libhsa-runtime64");
+                Ctx* c = static_cast<Ctx*>(d);
+                hsa_amd_segment_t seg{};
+                if (pinfo(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) == HSA_STATUS_SUCCESS && seg == HSA_AMD_SEGMENT_GLOBAL)
+                  c->a->pool_ordinal[pool.handle] = c->ordinal;
+                return HSA_STATUS_SUCCESS;
+              },
+              &ctx);
+          return HSA_STATUS_SUCCESS;
+        },
+        a);
+  });
+  return *a;
+}
+
+int pool_ordinal(hsa_amd_memory_pool_t pool) {
+  const Agents& a = agents();
+  auto it = a.pool_ordinal.find(pool.handle);
+  return it == a.pool_ordinal.end() ? -1 : it->second;
+}
+
+int agent_ordinal(hsa_agent_t agent) {
+  const Agents& a = agents();
+  for (size_t i = 0; i < a.gpus.size(); ++i)
+    if (a.gpus[i] == agent.handle) return (int)i;
+  return -1;
 }
 
 off_t slot_offset(int i) { return (off_t)(offsetof(Table, slot) + (size_t)i * sizeof(Slot)); }
@@ -271,15 +364,9 @@ void open_acct(State& s, const char* path) {
   s.table = t;
 }
 
-void track(void* p, int dev, size_t bytes) {
-  State& s = st();
-  if (!s.active || !p) return;
-  std::lock_guard<std::mutex> g(s.mu);
-  s.ptrs[p] = {dev, bytes};
-}
-
-// forget `p` BEFORE the runtime frees it: once freed, the address can be handed to another thread's
-// allocation, whose entry a late erase would destroy.  -> (device, bytes), or (-1, 0) if untracked
+// ordinal of the share's device a pointer was allocated on; (-1, 0) if untracked.  Forget `p` BEFORE
+// the runtime frees it: once freed, the address can be handed to another thread's allocation, whose
+// entry a late erase would destroy.
 std::pair<int, size_t> untrack(void* p) {
   State& s = st();
   if (!s.active || !p) return {-1, 0};
@@ -291,36 +378,21 @@ std::pair<int, size_t> untrack(void* p) {
   return v;
 }
 
-// the free went through: give the bytes back; it failed: the allocation is still live
-void settle_free(void* p, std::pair<int, size_t> v, hipError_t e) {
-  if (v.first < 0) return;
-  if (e == kSuccess) {
-    unreserve(v.first, v.second);
-  } else {
-    track(p, v.first, v.second);
-  }
+void set_cu_mask_env() {
+  State& s = st();
+  if (s.active && !s.cu_mask.empty()) setenv("HSA_CU_MASK", s.cu_mask.c_str(), 1);
 }
 
-// one allocation through `call` (which performs the real allocation into *ptr)
-template <typename Call>
-hipError_t guarded(void** ptr, size_t bytes, Call call) {
-  const int dev = current_device();
-  if (!reserve(dev, bytes)) {
-    if (ptr) *ptr = nullptr;
-    return kOutOfMemory;
-  }
-  hipError_t e = call();
-  if (e != kSuccess || !ptr || !*ptr) {
-    unreserve(dev, bytes);
-    return e;
-  }
-  track(*ptr, dev, bytes);
-  return e;
+const char* config_path() {
+  // the plugin's mount wins over anything the pod's environment says
+  if (access(GTK_VGPU_FIXED_CONF, R_OK) == 0) return GTK_VGPU_FIXED_CONF;
+  const char* env = std::getenv("GTK_VGPU_CONFIG");
+  return (env && *env) ? env : nullptr;
 }
 
 __attribute__((constructor)) void load_config() {
-  const char* path = std::getenv("GTK_VGPU_CONFIG");
-  if (!path || !*path) path = "/etc/gtk-vgpu.conf";
+  const char* path = config_path();
+  if (!path) return;
   FILE* f = std::fopen(path, "r");
   if (!f) return;  // no share to enforce: pass-through
   State& s = st();
@@ -333,13 +405,14 @@ __attribute__((constructor)) void load_config() {
       if (dev >= 0 && dev < kMaxDev && bytes >= 0) s.limit[dev] = bytes;
     } else if (std::sscanf(line, "%63s %3999s", key, val) == 2 && std::strcmp(key, "cu_mask") == 0) {
       s.cu_mask = val;
+      s.mask_bits = parse_mask(s.cu_mask);
     } else if (std::sscanf(line, "%63s %3999s", key, val) == 2 && std::strcmp(key, "acct") == 0) {
       open_acct(s, val);
     }
   }
   std::fclose(f);
   s.active = true;
-  // fork: no thread may hold the lock across it, and the child starts with a budget of its own (HIP
+  // fork: no thread may hold the lock across it, and the child starts with a budget of its own (HSA
   // state, and so device memory, does not survive a fork); with an acct file it claims its own slot
   pthread_atfork([] { st().mu.lock(); }, [] { st().mu.unlock(); },
                  [] {
@@ -348,203 +421,193 @@ __attribute__((constructor)) void load_config() {
                    for (int d = 0; d < kMaxDev; ++d) c.used[d] = 0;
                    c.ptrs.clear();
                    c.handles.clear();
+                   c.queues.clear();
                    c.mine = -1;
                  });
-  if (!s.cu_mask.empty()) setenv("HSA_CU_MASK", s.cu_mask.c_str(), 1);  // before ROCr initialises
+  set_cu_mask_env();  // before ROCr initialises
   setenv("GTK_VGPU_ACTIVE", "1", 1);  // lets the workload report that the guard is in force
 }
 
-void reassert_cu_mask() {
-  if (g_mask_reasserted.load(std::memory_order_acquire)) return;
+// the share's CU bits of `ordinal`, intersected with `want` (nullptr = all CUs); empty = no restriction
+std::vector<uint32_t> share_mask(int ordinal, const uint32_t* want, uint32_t want_bits) {
   State& s = st();
-  std::lock_guard<std::mutex> g(s.mu);
-  if (g_mask_reasserted.load(std::memory_order_relaxed)) return;
-  if (s.active && !s.cu_mask.empty()) setenv("HSA_CU_MASK", s.cu_mask.c_str(), 1);
-  g_mask_reasserted.store(true, std::memory_order_release);
+  if (!s.active || ordinal < 0 || ordinal >= (int)s.mask_bits.size() || s.mask_bits[ordinal].empty()) return {};
+  std::vector<uint32_t> m = s.mask_bits[ordinal];
+  if (want) {
+    bool any = false;
+    for (size_t w = 0; w < m.size(); ++w) {
+      const uint32_t x = m[w] & (w < want_bits / 32 ? want[w] : 0u);
+      any |= x != 0;
+      if (any) break;
+    }
+    if (any)  // an empty intersection would stop the queue: the share's own mask applies instead
+      for (size_t w = 0; w < m.size(); ++w) m[w] &= (w < want_bits / 32 ? want[w] : 0u);
+  }
+  return m;
 }
 
 }  // namespace
 
 extern "C" {
 
-__attribute__((visibility("default"))) hipError_t hipMalloc(void** ptr, size_t size) {
-  reassert_cu_mask();
-  typedef hipError_t (*F)(void**, size_t);
-  REAL(hipMalloc, F);
-  return guarded(ptr, size, [&] { return real_fn(ptr, size); });
+// ---------------------------------------------------------------- ROCr: initialisation and queues
+
+// Every HIP program initialises ROCr through here, whatever its first HIP call: the share's mask is
+// put back into the environment ROCr is about to read.
+__attribute__((visibility("default"))) hsa_status_t hsa_init() {
+  set_cu_mask_env();
+  REAL_HSA(hsa_init);
+  return real_fn();
 }
 
-__attribute__((visibility("default"))) hipError_t hipExtMallocWithFlags(void** ptr, size_t size, unsigned int flags) {
-  reassert_cu_mask();
-  typedef hipError_t (*F)(void**, size_t, unsigned int);
-  REAL(hipExtMallocWithFlags, F);
-  return guarded(ptr, size, [&] { return real_fn(ptr, size, flags); });
+__attribute__((visibility("default"))) hsa_status_t hsa_queue_create(
+    hsa_agent_t agent, uint32_t size, hsa_queue_type32_t type, void (*callback)(hsa_status_t, hsa_queue_t*, void*),
+    void* data, uint32_t private_segment_size, uint32_t group_segment_size, hsa_queue_t** queue) {
+  REAL_HSA(hsa_queue_create);
+  hsa_status_t e = real_fn(agent, size, type, callback, data, private_segment_size, group_segment_size, queue);
+  State& s = st();
+  if (e != HSA_STATUS_SUCCESS || !queue || !*queue || !s.active || s.mask_bits.empty()) return e;
+  const int ord = agent_ordinal(agent);
+  std::vector<uint32_t> m = share_mask(ord, nullptr, 0);
+  if (m.empty()) return e;
+  {
+    std::lock_guard<std::mutex> g(s.mu);
+    s.queues[*queue] = ord;
+  }
+  static const auto set_mask = real<decltype(&::hsa_amd_queue_cu_set_mask)>("hsa_amd_queue_cu_set_mask", "libhsa-runtime64");
+  const hsa_status_t me = set_mask(*queue, (uint32_t)(m.size() * 32), m.data());
+  if (me != HSA_STATUS_SUCCESS && me != HSA_STATUS_INFO_BREAK)
+    std::fprintf(stderr, "gtk-vgpu: applying the share's CU mask to a queue failed (%d)\n", (int)me);
+  return e;
 }
 
-__attribute__((visibility("default"))) hipError_t hipMallocManaged(void** ptr, size_t size, unsigned int flags) {
-  reassert_cu_mask();
-  typedef hipError_t (*F)(void**, size_t, unsigned int);
-  REAL(hipMallocManaged, F);
-  return guarded(ptr, size, [&] { return real_fn(ptr, size, flags); });
+__attribute__((visibility("default"))) hsa_status_t hsa_queue_destroy(hsa_queue_t* queue) {
+  State& s = st();
+  if (s.active && queue) {
+    std::lock_guard<std::mutex> g(s.mu);
+    s.queues.erase(queue);
+  }
+  REAL_HSA(hsa_queue_destroy);
+  return real_fn(queue);
 }
 
-__attribute__((visibility("default"))) hipError_t hipMallocAsync(void** ptr, size_t size, void* stream) {
-  reassert_cu_mask();
-  typedef hipError_t (*F)(void**, size_t, void*);
-  REAL(hipMallocAsync, F);
-  return guarded(ptr, size, [&] { return real_fn(ptr, size, stream); });
+// A program's own CU mask (hipExtStreamCreateWithCUMask) is narrowed to the share.
+__attribute__((visibility("default"))) hsa_status_t hsa_amd_queue_cu_set_mask(const hsa_queue_t* queue,
+                                                                               uint32_t num_cu_mask_count,
+                                                                               const uint32_t* cu_mask) {
+  REAL_HSA(hsa_amd_queue_cu_set_mask);
+  State& s = st();
+  int ord = -1;
+  if (s.active && queue) {
+    std::lock_guard<std::mutex> g(s.mu);
+    auto it = s.queues.find(queue);
+    if (it != s.queues.end()) ord = it->second;
+  }
+  std::vector<uint32_t> m = share_mask(ord, cu_mask, num_cu_mask_count);
+  if (m.empty()) return real_fn(queue, num_cu_mask_count, cu_mask);
+  return real_fn(queue, (uint32_t)(m.size() * 32), m.data());
 }
 
-__attribute__((visibility("default"))) hipError_t hipMallocFromPoolAsync(void** ptr, size_t size, void* pool, void* stream) {
-  reassert_cu_mask();
-  typedef hipError_t (*F)(void**, size_t, void*, void*);
-  REAL(hipMallocFromPoolAsync, F);
-  return guarded(ptr, size, [&] { return real_fn(ptr, size, pool, stream); });
-}
+// ---------------------------------------------------------------- ROCr: device memory
 
-__attribute__((visibility("default"))) hipError_t hipMallocPitch(void** ptr, size_t* pitch, size_t width, size_t height) {
-  reassert_cu_mask();
-  typedef hipError_t (*F)(void**, size_t*, size_t, size_t);
-  REAL(hipMallocPitch, F);
-  // the pitch is not known before the call: reserve the unpadded size, then settle to pitch*height
-  const int dev = current_device();
-  const size_t want = width * height;
-  if (!reserve(dev, want)) {
+__attribute__((visibility("default"))) hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t size,
+                                                                                  uint32_t flags, void** ptr) {
+  REAL_HSA(hsa_amd_memory_pool_allocate);
+  State& s = st();
+  if (!s.active) return real_fn(pool, size, flags, ptr);
+  const int dev = pool_ordinal(pool);
+  if (!reserve(dev, size)) {
     if (ptr) *ptr = nullptr;
-    return kOutOfMemory;
+    return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
   }
-  hipError_t e = real_fn(ptr, pitch, width, height);
-  if (e != kSuccess || !ptr || !*ptr) {
-    unreserve(dev, want);
-    return e;
-  }
-  const size_t got = (pitch ? *pitch : width) * height;
-  if (got > want && !reserve(dev, got - want)) {
-    typedef hipError_t (*G)(void*);
-    REAL(hipFree, G);
-    real_fn(*ptr);
-    *ptr = nullptr;
-    unreserve(dev, want);
-    return kOutOfMemory;
-  }
-  track(*ptr, dev, got > want ? got : want);
-  return e;
-}
-
-__attribute__((visibility("default"))) hipError_t hipFree(void* ptr) {
-  reassert_cu_mask();
-  typedef hipError_t (*F)(void*);
-  REAL(hipFree, F);
-  auto v = untrack(ptr);
-  hipError_t e = real_fn(ptr);
-  settle_free(ptr, v, e);
-  return e;
-}
-
-__attribute__((visibility("default"))) hipError_t hipFreeAsync(void* ptr, void* stream) {
-  reassert_cu_mask();
-  typedef hipError_t (*F)(void*, void*);
-  REAL(hipFreeAsync, F);
-  auto v = untrack(ptr);
-  hipError_t e = real_fn(ptr, stream);
-  settle_free(ptr, v, e);
-  return e;
-}
-
-// hipMemCreate(hipMemGenericAllocationHandle_t* handle, size_t size, const hipMemAllocationProp* prop,
-// unsigned long long flags): the handle is an opaque pointer-sized value
-__attribute__((visibility("default"))) hipError_t hipMemCreate(void** handle, size_t size, const void* prop,
-                                                                unsigned long long flags) {
-  reassert_cu_mask();
-  typedef hipError_t (*F)(void**, size_t, const void*, unsigned long long);
-  REAL(hipMemCreate, F);
-  const int dev = current_device();
-  if (!reserve(dev, size)) return kOutOfMemory;
-  hipError_t e = real_fn(handle, size, prop, flags);
-  if (e != kSuccess || !handle) {
+  hsa_status_t e = real_fn(pool, size, flags, ptr);
+  if (dev < 0 || dev >= kMaxDev || s.limit[dev] < 0) return e;
+  if (e != HSA_STATUS_SUCCESS || !ptr || !*ptr) {
     unreserve(dev, size);
     return e;
   }
-  State& s = st();
-  if (s.active) {
-    std::lock_guard<std::mutex> g(s.mu);
-    s.handles[(unsigned long long)(*handle)] = {dev, size};
+  std::lock_guard<std::mutex> g(s.mu);
+  s.ptrs[*ptr] = {dev, size};
+  return e;
+}
+
+__attribute__((visibility("default"))) hsa_status_t hsa_amd_memory_pool_free(void* ptr) {
+  REAL_HSA(hsa_amd_memory_pool_free);
+  auto v = untrack(ptr);
+  hsa_status_t e = real_fn(ptr);
+  if (v.first >= 0) {
+    if (e == HSA_STATUS_SUCCESS) {
+      unreserve(v.first, v.second);
+    } else {  // the free failed: the allocation is still live
+      std::lock_guard<std::mutex> g(st().mu);
+      st().ptrs[ptr] = v;
+    }
   }
   return e;
 }
 
-__attribute__((visibility("default"))) hipError_t hipMemRelease(void* handle) {
-  reassert_cu_mask();
-  typedef hipError_t (*F)(void*);
-  REAL(hipMemRelease, F);
+// physical memory behind the virtual-memory API (hipMemCreate, expandable caching-allocator segments)
+__attribute__((visibility("default"))) hsa_status_t hsa_amd_vmem_handle_create(hsa_amd_memory_pool_t pool, size_t size,
+                                                                                hsa_amd_memory_type_t type, uint64_t flags,
+                                                                                hsa_amd_vmem_alloc_handle_t* handle) {
+  REAL_HSA(hsa_amd_vmem_handle_create);
   State& s = st();
-  int dev = -1;
-  size_t bytes = 0;
+  if (!s.active) return real_fn(pool, size, type, flags, handle);
+  const int dev = pool_ordinal(pool);
+  if (!reserve(dev, size)) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  hsa_status_t e = real_fn(pool, size, type, flags, handle);
+  if (dev < 0 || dev >= kMaxDev || s.limit[dev] < 0) return e;
+  if (e != HSA_STATUS_SUCCESS || !handle) {
+    unreserve(dev, size);
+    return e;
+  }
+  std::lock_guard<std::mutex> g(s.mu);
+  s.handles[handle->handle] = {dev, size};
+  return e;
+}
+
+__attribute__((visibility("default"))) hsa_status_t hsa_amd_vmem_handle_release(hsa_amd_vmem_alloc_handle_t handle) {
+  REAL_HSA(hsa_amd_vmem_handle_release);
+  State& s = st();
+  std::pair<int, size_t> v{-1, 0};
   if (s.active) {  // forget the handle before the runtime can reuse its value
     std::lock_guard<std::mutex> g(s.mu);
-    auto it = s.handles.find((unsigned long long)handle);
+    auto it = s.handles.find(handle.handle);
     if (it != s.handles.end()) {
-      dev = it->second.first;
-      bytes = it->second.second;
+      v = it->second;
       s.handles.erase(it);
     }
   }
-  hipError_t e = real_fn(handle);
-  if (dev >= 0) {
-    if (e == kSuccess) {
-      unreserve(dev, bytes);
+  hsa_status_t e = real_fn(handle);
+  if (v.first >= 0) {
+    if (e == HSA_STATUS_SUCCESS) {
+      unreserve(v.first, v.second);
     } else {
       std::lock_guard<std::mutex> g(s.mu);
-      s.handles[(unsigned long long)handle] = {dev, bytes};
+      s.handles[handle.handle] = v;
     }
   }
   return e;
 }
 
+// ---------------------------------------------------------------- HIP: what the process is told
+
 // the share is the device's size as far as this process can tell
 __attribute__((visibility("default"))) hipError_t hipMemGetInfo(size_t* free_b, size_t* total_b) {
-  reassert_cu_mask();
   typedef hipError_t (*F)(size_t*, size_t*);
-  REAL(hipMemGetInfo, F);
+  REAL_HIP(hipMemGetInfo, F);
   hipError_t e = real_fn(free_b, total_b);
   State& s = st();
-  const int dev = current_device();
-  if (e != kSuccess || !s.active || s.limit[dev] < 0) return e;
+  if (e != kSuccess || !s.active) return e;
+  typedef hipError_t (*G)(int*);
+  static const G get_device = real<G>("hipGetDevice", "libamdhip64");
+  int dev = 0;
+  if (get_device(&dev) != kSuccess || dev < 0 || dev >= kMaxDev || s.limit[dev] < 0) return e;
   std::lock_guard<std::mutex> g(s.mu);
   const long long left = s.limit[dev] - pod_used(dev);
   if (total_b && (long long)*total_b > s.limit[dev]) *total_b = (size_t)s.limit[dev];
   if (free_b && (long long)*free_b > left) *free_b = (size_t)(left > 0 ? left : 0);
   return e;
-}
-
-// The calls a program usually makes first (torch: hipGetDeviceCount), which initialise the runtime:
-// pass-through after the mask is set back.
-__attribute__((visibility("default"))) hipError_t hipInit(unsigned int flags) {
-  reassert_cu_mask();
-  typedef hipError_t (*F)(unsigned int);
-  REAL(hipInit, F);
-  return real_fn(flags);
-}
-
-__attribute__((visibility("default"))) hipError_t hipGetDeviceCount(int* count) {
-  reassert_cu_mask();
-  typedef hipError_t (*F)(int*);
-  REAL(hipGetDeviceCount, F);
-  return real_fn(count);
-}
-
-__attribute__((visibility("default"))) hipError_t hipSetDevice(int dev) {
-  reassert_cu_mask();
-  typedef hipError_t (*F)(int);
-  REAL(hipSetDevice, F);
-  return real_fn(dev);
-}
-
-__attribute__((visibility("default"))) hipError_t hipGetDevice(int* dev) {
-  reassert_cu_mask();
-  typedef hipError_t (*F)(int*);
-  REAL(hipGetDevice, F);
-  return real_fn(dev);
 }
 
 // introspection for tests and the workload's report: bytes in use / limit on `dev` (-1: no limit)
@@ -563,6 +626,12 @@ __attribute__((visibility("default"))) long long gtk_vgpu_pod_used(int dev) {
 
 __attribute__((visibility("default"))) long long gtk_vgpu_limit(int dev) {
   return (dev >= 0 && dev < kMaxDev) ? st().limit[dev] : -1;
+}
+
+// queues of this process the share's mask was applied to
+__attribute__((visibility("default"))) int gtk_vgpu_masked_queues() {
+  std::lock_guard<std::mutex> g(st().mu);
+  return (int)st().queues.size();
 }
 
 }  // extern "C"

@@ -11,8 +11,9 @@ Targets (all land in ``gpu_topology_on_k8s_amd/_native/``):
   _rccl       HIP  (hipcc)  RCCL all-reduce validator (librccl)
   _fused      HIP  (hipcc)  PyTorch custom ops for the Llama-3 workload (torch headers)
   bin/rccl_allreduce_bench  standalone validator binary
-  bin/libgtk_vgpu.so        C++  (g++)    HIP allocation guard preloaded into time-sliced pods (csrc/vgpu)
+  bin/libgtk_vgpu.so        C++  (g++)    ROCr-level HBM/CU guard preloaded into time-sliced pods (csrc/vgpu)
   bin/fake_hip/libamdhip64.so             stand-in HIP runtime for CPU tests of the guard
+  bin/fake_hip/libhsa-runtime64.so        stand-in ROCr runtime under it
 """
 from __future__ import annotations
 
@@ -136,19 +137,25 @@ def targets() -> List[Target]:
         # the pod by Allocate (--share-guard); host-only C++, resolves the real HIP entry points at run time
         Target("vgpu_guard", [CSRC / "vgpu" / "vgpu_guard.cpp"], "gxx", HERE / "bin" / "libgtk_vgpu.so",
                ["-fvisibility=hidden", "-ldl", "-pthread"], pybind=False),
+        # stand-in ROCr + HIP runtimes for CPU tests of the guard, layered like the real pair (the HIP
+        # stand-in links the ROCr one as libhsa-runtime64.so, found next to it)
+        Target("fake_hsa", [CSRC / "vgpu" / "fake_hsa.cpp"], "gxx", HERE / "bin" / "fake_hip" / "libhsa-runtime64.so",
+               ["-fvisibility=default", "-pthread", "-Wl,-soname,libhsa-runtime64.so"], pybind=False),
         Target("fake_hip", [CSRC / "vgpu" / "fake_hip.cpp"], "gxx", HERE / "bin" / "fake_hip" / "libamdhip64.so",
-               ["-fvisibility=default"], pybind=False),
+               ["-fvisibility=default", f"-L{HERE / 'bin' / 'fake_hip'}", "-l:libhsa-runtime64.so", "-Wl,--disable-new-dtags", "-Wl,-rpath,$ORIGIN"],
+               deps=[HERE / "bin" / "fake_hip" / "libhsa-runtime64.so"], pybind=False),
         # the guard under ThreadSanitizer and under ASan/UBSan (host code only), stressed by many threads
-        # against the stand-in runtime (tests/test_vgpu_guard.py)
+        # against the stand-in runtimes (tests/test_vgpu_guard.py)
         Target("vgpu_selftest_tsan", [CSRC / "vgpu" / "vgpu_guard.cpp", CSRC / "vgpu" / "vgpu_selftest.cpp"], "gxx",
                HERE / "bin" / "vgpu_selftest_tsan",
                ["-g", "-O1", "-fsanitize=thread", "-pthread", "-ldl", f"-L{HERE / 'bin' / 'fake_hip'}", "-l:libamdhip64.so",
-                "-Wl,--disable-new-dtags", f"-Wl,-rpath,{HERE / 'bin' / 'fake_hip'}"], deps=[HERE / "bin" / "fake_hip" / "libamdhip64.so"],
-               pybind=False, shared=False),
+                "-l:libhsa-runtime64.so", "-Wl,--disable-new-dtags", f"-Wl,-rpath,{HERE / 'bin' / 'fake_hip'}"],
+               deps=[HERE / "bin" / "fake_hip" / "libamdhip64.so"], pybind=False, shared=False),
         Target("vgpu_selftest_asan", [CSRC / "vgpu" / "vgpu_guard.cpp", CSRC / "vgpu" / "vgpu_selftest.cpp"], "gxx",
                HERE / "bin" / "vgpu_selftest_asan",
                ["-g", "-O1", "-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-pthread", "-ldl",
-                f"-L{HERE / 'bin' / 'fake_hip'}", "-l:libamdhip64.so", "-Wl,--disable-new-dtags", f"-Wl,-rpath,{HERE / 'bin' / 'fake_hip'}"],
+                f"-L{HERE / 'bin' / 'fake_hip'}", "-l:libamdhip64.so", "-l:libhsa-runtime64.so", "-Wl,--disable-new-dtags",
+                f"-Wl,-rpath,{HERE / 'bin' / 'fake_hip'}"],
                deps=[HERE / "bin" / "fake_hip" / "libamdhip64.so"], pybind=False, shared=False),
         Target("_fused", sorted((CSRC / "ops").glob("*.hip")), "hipcc", HERE / f"_fused{EXT}",
                deps=sorted((CSRC / "ops").glob("*.h")), pybind=True, torch=True),
@@ -213,10 +220,15 @@ def build(force: bool = False, only: Optional[List[str]] = None, jobs: int = 4, 
     ts = [t for t in targets() if not only or t.name in only]
     msgs: List[str] = []
     errors: List[str] = []
-    # targets that link another target's output (the guard self-tests link the stand-in runtime) wait
-    # for a first wave of everything else
-    outs = {t.out for t in targets()}
-    waves = [[t for t in ts if not (set(t.deps) & outs)], [t for t in ts if set(t.deps) & outs]]
+    # targets that link another target's output (the stand-in HIP runtime links the stand-in ROCr, the
+    # guard self-tests link both) are built in a later wave than what they link: topological layers
+    producer = {t.out: t for t in targets()}
+
+    def depth(t: Target) -> int:
+        return 1 + max((depth(producer[d]) for d in t.deps if d in producer), default=-1)
+
+    layers = [depth(t) for t in ts]
+    waves = [[t for t, d in zip(ts, layers) if d == k] for k in range(max(layers, default=-1) + 1)]
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         for wave in waves:
             futs = {ex.submit(build_one, t, force, verbose, jobs): t for t in wave}

@@ -143,10 +143,11 @@ def main(argv=None) -> int:
                          "The node label <annotation-prefix>/time-slices overrides it per node")
     ap.add_argument("--label-check-interval", type=float, default=30.0,
                     help="seconds between checks of the node's time-slices label (a change restarts the plugin once idle)")
-    ap.add_argument("--share-guard", default="env", choices=["off", "env", "preload"],
+    ap.add_argument("--share-guard", default="preload", choices=["off", "env", "preload"],
                     help="--time-slices: mount and preload libgtk_vgpu.so into pods holding part of a GPU, which caps their HIP "
-                         "allocations at the share's HBM and forces their CU mask (env = LD_PRELOAD; preload = an "
-                         "/etc/ld.so.preload mount as well; off = cooperative shares)")
+                         "allocations at the share's HBM and forces their CU mask (preload = an /etc/ld.so.preload mount plus "
+                         "LD_PRELOAD, which survives a container that overrides its env; env = LD_PRELOAD only; "
+                         "off = cooperative shares)")
     ap.add_argument("--share-guard-dir", default="/var/lib/gtk-vgpu",
                     help="host directory (hostPath, same path inside the DaemonSet) for the guard library and per-allocation configs")
     ap.add_argument("--share-cu-mask", default="on", choices=["on", "off"],
@@ -169,11 +170,11 @@ def main(argv=None) -> int:
     names = (a.resource_name, a.slice_resource_name, "aliyun.com/gpu", "aliyun.com/gpu-count")
     partition_control = a.partition_control == "on" and a.discovery in ("auto", "amdsmi") and api is not None
 
-    def repartition_pass(idle_fn, wait):
+    def repartition_pass(idle_fn, wait, hold=None):
         from .repartition import repartition
 
         outcome, msg = repartition(api, a.node_name, contract, idle_fn, reload_driver=a.partition_driver_reload,
-                                   settle_s=a.probe_settle_seconds, wait=wait,
+                                   settle_s=a.probe_settle_seconds, wait=wait, hold=hold,
                                    time_slices=node_time_slices(api, a.node_name, contract, a.time_slices))
         if outcome in ("ok", "failed", "invalid"):
             (log.warning if outcome != "ok" else log.info)("partition request: %s: %s", outcome, msg)
@@ -188,15 +189,25 @@ def main(argv=None) -> int:
                                              (a.resource_name, a.slice_resource_name, "aliyun.com/gpu", "aliyun.com/gpu-count"))
     if why:
         log.warning("%s", why)
+    # Slicing needs SPX GPUs.  On a partitioned node the label's count cannot apply: the plugin
+    # advertises the XCPs unsliced, and the label check below compares the label against what it
+    # *could* apply (1), not against the label itself, so it never restarts for a count it cannot
+    # honour (an exit-75 loop every label-check interval).
+    partitioned = False
     if a.time_slices > 1:
         try:
             parts = discover(a.discovery, node_name=a.node_name, fake_n=a.fake_gpus)
-            if any(g.physical != g.index for g in parts.gpus):
+            partitioned = any(g.physical != g.index for g in parts.gpus)
+            if partitioned:
                 log.error("time slices (%d per GPU) need SPX GPUs, and this node is partitioned (%s): advertising its "
                           "XCPs unsliced", a.time_slices, parts.gpus[0].partition)
                 a.time_slices = 1
         except Exception as e:  # noqa: BLE001 - discovery fails again below, with its own error
             log.warning("discovery before slicing failed: %s", e)
+
+    def applicable_slices(want: int) -> int:
+        return 1 if partitioned else want
+    unapplied_warned = False
     # a sliced node is a pool of its own: it registers its slices under the slice resource and
     # offers no whole GPUs (the extender's filter keeps the two kinds of request apart)
     advertised = a.slice_resource_name if a.time_slices > 1 else a.resource_name
@@ -259,7 +270,12 @@ def main(argv=None) -> int:
     while not done.wait(1.0):
         ticks += 1
         if ticks % max(1, int(a.label_check_interval)) == 0 and api is not None:  # the operator relabelled the node's time slices
-            want = node_time_slices(api, a.node_name, contract, a.time_slices)
+            label = node_time_slices(api, a.node_name, contract, a.time_slices)
+            want = applicable_slices(label)
+            if want != label and not unapplied_warned:
+                log.warning("node label asks for %d time slices per GPU; a partitioned node cannot be sliced, "
+                            "so its XCPs stay unsliced (switch the node to SPX to apply the label)", label)
+                unapplied_warned = True
             if want != a.time_slices:
                 # device IDs change with the slicing: switch only when no pod holds a device, or the
                 # running pods' GROUP annotations would name devices of the old layout
@@ -274,7 +290,7 @@ def main(argv=None) -> int:
                 outcome, msg = "busy", "a link re-probe holds the GPUs"
             else:
                 try:
-                    outcome, msg = repartition_pass(plugin.node_idle, done.wait)
+                    outcome, msg = repartition_pass(plugin.node_idle, done.wait, plugin.allocation_hold)
                 except Exception as e:  # noqa: BLE001 - reported; the next pass tries again
                     outcome, msg = "error", str(e)
                     log.warning("partition request: %s", e)

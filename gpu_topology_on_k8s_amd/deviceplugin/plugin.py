@@ -22,6 +22,8 @@ extender (no GROUP) is annotated with what the kubelet gave it so the extender s
 """
 from __future__ import annotations
 
+import contextlib
+import itertools
 import json
 import logging
 import math
@@ -202,6 +204,18 @@ class PluginConfig:
         return os.path.join(self.socket_dir, self.socket_name)
 
 
+class AllocationHold:
+    """State shared by a partition switch and the Allocate calls it holds (``allocation_hold``)."""
+
+    def __init__(self) -> None:
+        self.waiters = 0  # Allocate calls waiting for the switch
+        self.started = False  # the switch passed its last idle check and runs amdsmi steps
+        self.switched = False  # ... and changed the package's modes
+
+    def contended(self) -> bool:
+        return self.waiters > 0
+
+
 class DevicePluginServer:
     def __init__(self, topology: Topology, config: Optional[PluginConfig] = None, api: Optional[KubeAPI] = None,
                  health_fn: Optional[Callable[[Topology], Dict[int, bool]]] = None, clock: Callable[[], float] = time.time,
@@ -229,6 +243,9 @@ class DevicePluginServer:
         self.maintenance = threading.Lock()
         self._probing = False  # set (under _alloc_lock) while an idle-time re-probe owns the links
         self._cancel = threading.Event()  # set by an Allocate arriving mid-probe: the probe stops
+        self._guard_seq = itertools.count(1)  # unique per-allocation guard files (_guard_files)
+        self._hold: Optional["AllocationHold"] = None  # a partition switch holds Allocate (allocation_hold)
+        self._stale_layout = ""  # set when a switch changed the device layout: Allocate refuses until the restart
         self._guard_ready = False  # install_guard() put libgtk_vgpu.so into cfg.guard_dir
         self.allocations: List[Tuple[str, Tuple[int, ...]]] = []  # (pod key or "", ids) log
         self.registered = 0
@@ -343,6 +360,25 @@ class DevicePluginServer:
             log.warning("%s the probing mark on %s failed: %s", "clearing" if until is None else "setting",
                         self.cfg.node_name, e)
             return False
+
+    @contextlib.contextmanager
+    def allocation_hold(self):
+        """Hold Allocate while a partition switch (deviceplugin/repartition.py) may run.  The yielded
+        :class:`AllocationHold` tells the switch whether an Allocate is waiting (it then abandons the
+        switch, and the Allocate proceeds on the unchanged layout); the switch sets ``started`` and
+        ``switched``.  An Allocate held across a switch that changed the layout is refused: its device
+        IDs name the old layout, and the plugin restarts to advertise the new one."""
+        h = AllocationHold()
+        with self._alloc_cond:
+            self._hold = h
+        try:
+            yield h
+        finally:
+            with self._alloc_cond:
+                self._hold = None
+                if h.switched:
+                    self._stale_layout = "the node's GPUs were repartitioned; the plugin restarts with new device IDs"
+                self._alloc_cond.notify_all()
 
     def _call_reprobe(self):
         """``reprobe_fn(cancel=event)`` when it takes a cancel event (the child-process probe kills its
@@ -538,6 +574,21 @@ class DevicePluginServer:
         if missing:
             self._refuse(context, grpc.StatusCode.FAILED_PRECONDITION, f"device nodes missing on this node: {missing}", "missing")
         with self._alloc_cond:
+            if self._hold is not None:
+                h = self._hold
+                h.waiters += 1
+                self.metrics.allocations.labels("switch_wait").inc()
+                try:
+                    while self._hold is h:
+                        self._alloc_cond.wait(1.0)
+                finally:
+                    h.waiters -= 1
+            if self._stale_layout:
+                self._alloc_cond.release()  # _refuse aborts the RPC (raises); never hold the lock across it
+                try:
+                    self._refuse(context, grpc.StatusCode.UNAVAILABLE, self._stale_layout, "stale_layout")
+                finally:
+                    self._alloc_cond.acquire()
             if self._probing:
                 # never refuse (the kubelet would reject the pod for good): the probe yields — its
                 # child is killed — and the container starts once the links are released
@@ -766,28 +817,77 @@ class DevicePluginServer:
         frac = share_fractions(self.topology, ids)
         if all(f >= 1.0 for f in frac.values()):
             return  # whole GPUs only: nothing to guard
-        base = os.path.join(self.cfg.guard_dir, "alloc", "slices-" + "-".join(str(int(i)) for i in sorted(set(ids))))
-        conf, acct = base + ".conf", base + ".acct"
-        tmp = f"{conf}.tmp{os.getpid()}"
-        with open(tmp, "w") as f:
-            f.write(self.guard_config(ids, mask))
-        os.replace(tmp, conf)
-        # a fresh accounting table for this allocation (these devices are exclusively the new pod's, so
-        # nothing of a previous pod on them can still be running); world-writable: any container user
-        fd = os.open(acct, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o666)
-        os.fchmod(fd, 0o666)
-        os.close(fd)
+        conf, acct = self._guard_files(ids, mask)
         r.mounts.add(container_path=self.GUARD_LIB_IN_CONTAINER, host_path=os.path.join(self.cfg.guard_dir, "libgtk_vgpu.so"),
                      read_only=True)
         r.mounts.add(container_path=self.GUARD_CONF_IN_CONTAINER, host_path=conf, read_only=True)
         r.mounts.add(container_path=self.GUARD_ACCT_IN_CONTAINER, host_path=acct, read_only=False)
         r.envs["GTK_VGPU_CONFIG"] = self.GUARD_CONF_IN_CONTAINER
-        if self.cfg.share_guard == "preload":
+        if self.cfg.share_guard == "preload":  # loaded by every process whatever its env says
             r.mounts.add(container_path="/etc/ld.so.preload", host_path=os.path.join(self.cfg.guard_dir, "ld.so.preload"),
                          read_only=True)
-        else:
-            r.envs["LD_PRELOAD"] = self.GUARD_LIB_IN_CONTAINER
+        # and LD_PRELOAD in both modes: the dynamic loader maps the library once either way
+        r.envs["LD_PRELOAD"] = self.GUARD_LIB_IN_CONTAINER
         self.metrics.guarded.inc()
+
+    def _guard_files(self, ids: Sequence[int], mask: str) -> Tuple[str, str]:
+        """A config and an accounting table of their own for this allocation.  The names are unique:
+        a process of an earlier holder of these slices (a terminating pod, a sidecar that keeps its
+        devices) may still map its own table, and truncating a mapped file would SIGBUS it and wipe the
+        pod's budget.  Older files of the same slices are removed once no process holds a
+        slot lock in their table (every live guarded process holds one): by then the kubelet has handed
+        the slices to this allocation, so the pod that owned them is gone."""
+        d = os.path.join(self.cfg.guard_dir, "alloc")
+        os.makedirs(d, exist_ok=True)
+        key = "slices-" + "-".join(str(int(i)) for i in sorted(set(ids)))
+        seq = next(self._guard_seq)  # itertools.count: atomic under the GIL
+        base = os.path.join(d, f"{key}.{time.time_ns():x}.{os.getpid():x}.{seq}")
+        conf, acct = base + ".conf", base + ".acct"
+        tmp = f"{conf}.tmp"
+        with open(tmp, "w") as f:
+            f.write(self.guard_config(ids, mask))
+        os.replace(tmp, conf)
+        fd = os.open(acct, os.O_RDWR | os.O_CREAT | os.O_EXCL, 0o666)  # world-writable: any container user
+        os.fchmod(fd, 0o666)
+        os.close(fd)
+        self._gc_guard_files(d, set(int(i) for i in ids), keep=base)
+        return conf, acct
+
+    @staticmethod
+    def _acct_in_use(path: str) -> bool:
+        """Some process holds a record lock in the table (a live guarded process owns a slot)."""
+        import fcntl
+
+        try:
+            fd = os.open(path, os.O_RDWR)
+        except OSError:
+            return False
+        try:
+            fcntl.lockf(fd, fcntl.LOCK_EX | fcntl.LOCK_NB, 0, 0)  # the whole file, no wait
+        except OSError:
+            return True
+        finally:
+            os.close(fd)  # closing drops the probe lock
+        return False
+
+    def _gc_guard_files(self, d: str, ids: set, keep: str) -> None:
+        for name in os.listdir(d):
+            if not name.endswith(".acct") or not name.startswith("slices-"):
+                continue
+            base = os.path.join(d, name[:-5])
+            if base == keep:
+                continue
+            try:
+                old = {int(x) for x in name.split(".", 1)[0][len("slices-"):].split("-")}
+            except ValueError:
+                continue
+            if not old & ids or self._acct_in_use(base + ".acct"):
+                continue
+            for ext in (".acct", ".conf"):
+                try:
+                    os.unlink(base + ext)
+                except FileNotFoundError:
+                    pass
 
     def _rccl_env(self, pod: dict) -> Dict[str, str]:
         if not self.cfg.pass_rccl_env:

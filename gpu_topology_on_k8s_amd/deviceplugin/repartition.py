@@ -22,10 +22,11 @@ re-probe (``plugin.reprobe``):
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import math
 import time
-from typing import Callable, Optional, Tuple
+from typing import Callable, ContextManager, Optional, Tuple
 
 from ..k8s.annotations import Contract
 from ..k8s.events import record_event
@@ -52,11 +53,19 @@ def _event(api, node_name: str, reason: str, msg: str, type_: str) -> None:
 def repartition(api, node_name: str, contract: Contract, idle_fn: Callable[[], bool], lib: Optional[str] = None,
                 reload_driver: bool = False, settle_s: float = 2.0, mark_s: float = 600.0, time_slices: int = 1,
                 wait: Callable[[float], bool] = lambda s: (time.sleep(s), False)[1],
-                clock: Callable[[], float] = time.time) -> Tuple[str, str]:
+                clock: Callable[[], float] = time.time, hold: Optional[Callable[[], ContextManager]] = None
+                ) -> Tuple[str, str]:
     """One reconciliation pass.  -> (outcome, message), outcome one of
     ``none`` (no request), ``same`` (already there), ``invalid``, ``skipped`` (this request failed
     before), ``unavailable`` (amdsmi reports no package: nothing recorded, the next pass asks again),
-    ``busy`` (pods hold devices), ``stopped`` (``wait`` returned True), ``ok``, ``failed``."""
+    ``busy`` (pods hold devices), ``stopped`` (``wait`` returned True), ``ok``, ``failed``.
+
+    ``hold`` (``DevicePluginServer.allocation_hold``) holds the plugin's Allocate from the moment the
+    node is marked until the switch is over.  An Allocate that arrives meanwhile (a bind already past
+    the extender, or a pod that bypassed it) makes the node busy: the switch is abandoned before it
+    starts (or the driver reload is held back) and the Allocate proceeds on the old layout.  One that
+    arrives while an amdsmi step is already running waits for it, and is then refused, because its
+    device IDs name the old layout (the kubelet fails the pod; the plugin restarts)."""
     if api is None or not node_name:
         return "none", "no apiserver"
     want_c, want_m, node = partition_request(api, node_name, contract)
@@ -90,16 +99,27 @@ def repartition(api, node_name: str, contract: Contract, idle_fn: Callable[[], b
     api.patch_node(node_name, annotations={contract.probing_key: str(int(math.ceil(clock() + mark_s)))})
     switched = False
     try:
-        if settle_s > 0 and wait(settle_s):
-            return "stopped", ""
-        if not idle_fn():
-            return "busy", f"{tag} requested; a pod arrived while the node was being marked"
-        before = f"{info[0]['compute']}/{info[0]['memory']}" if info else "?"
-        log.warning("switching GPU partitions %s -> %s (node idle)", before, tag)
-        try:
-            res = apply_partition(want_c, want_m, lib=lib, reload_driver=reload_driver)
-        except Exception as e:  # noqa: BLE001 - PartitionError, or amdsmi without the setters: recorded, not retried
-            res = {"ok": False, "reason": str(e)[:500]}
+        with (hold() if hold is not None else contextlib.nullcontext()) as h:
+            def still_idle() -> bool:
+                return idle_fn() and not (h is not None and h.contended())
+
+            if settle_s > 0 and wait(settle_s):
+                return "stopped", ""
+            if not still_idle():
+                return "busy", f"{tag} requested; a pod arrived while the node was being marked"
+            before = f"{info[0]['compute']}/{info[0]['memory']}" if info else "?"
+            log.warning("switching GPU partitions %s -> %s (node idle)", before, tag)
+            if h is not None:
+                h.started = True
+            try:
+                res = apply_partition(want_c, want_m, lib=lib, reload_driver=reload_driver, before_reload=still_idle)
+            except Exception as e:  # noqa: BLE001 - PartitionError, or amdsmi without the setters: recorded, not retried
+                res = {"ok": False, "reason": str(e)[:500]}
+            if h is not None:
+                # a memory step may have been applied even when a later step failed: any change of
+                # the package's modes makes the old device IDs stale
+                h.switched = bool(res["ok"] or any(st.get("set") in ("compute", "memory") and all(
+                    p.get("status") == "ok" for p in st.get("packages", [])) for st in res.get("steps", [])))
         if res["ok"]:
             switched = True
             api.patch_node(node_name, annotations={contract.partition_failed_key: None})

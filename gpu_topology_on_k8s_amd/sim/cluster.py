@@ -189,7 +189,7 @@ class SimCluster:
                  policy: PlacementPolicy = PlacementPolicy(), assume_ttl: float = 300.0, use_filter: bool = True,
                  node_labels: Optional[Dict[str, Dict[str, str]]] = None, device_specs: str = "strict",
                  prestart_validate: bool = False, validate_fn=None, reconcile_interval: float = 0.0,
-                 informer: bool = False, share_guard: str = "env"):
+                 informer: bool = False, share_guard: str = "preload"):
         self.resource = resource
         # drive the extender's cache by LIST+WATCH (production mode) instead of a LIST per request
         self.use_informer = informer

@@ -21,7 +21,7 @@ extender stops binding there.  Switching needs root (the privileged DaemonSet). 
 from __future__ import annotations
 
 import os
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 from .._native import load
 
@@ -92,10 +92,12 @@ def _check_offered(info: Sequence[dict], compute: Optional[str], memory: Optiona
 
 
 def apply_partition(compute: Optional[str] = None, memory: Optional[str] = None, lib: Optional[str] = None,
-                    reload_driver: bool = False) -> dict:
+                    reload_driver: bool = False, before_reload: Optional[Callable[[], bool]] = None) -> dict:
     """Switch every package to ``compute`` / ``memory`` (None = keep).  The caller guarantees that no
     process uses the GPUs.  -> ``{"ok", "steps", "before", "after", "reason", "reload_required"}``;
-    ``ok`` is False (with ``reason``) when amdsmi refused a step.  Nothing is retried."""
+    ``ok`` is False (with ``reason``) when amdsmi refused a step.  Nothing is retried.
+    ``before_reload`` is asked right before a driver reload (the most disruptive step); False stops
+    the switch there (the caller saw a pod claim a device since its own idle check)."""
     compute, memory = normalise(compute, memory)
     lib = amdsmi_lib(lib)
     mod = load("_topo")
@@ -124,6 +126,11 @@ def apply_partition(compute: Optional[str] = None, memory: Optional[str] = None,
                 out["ok"] = False
                 out["reason"] = (f"memory partition {mode} is pending an amdgpu driver reload "
                                  "(allow it with --partition-driver-reload, or reload the driver by hand)")
+                break
+            if before_reload is not None and not before_reload():
+                out["ok"] = False
+                out["reason"] = f"memory partition {mode} set; the driver reload was held back: the node is no longer idle"
+                out["reload_required"] = True
                 break
             code = int(mod.driver_reload(lib))
             out["steps"].append({"set": "driver-reload", "status": status_name(code)})

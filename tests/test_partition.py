@@ -271,13 +271,114 @@ def test_partitions_and_time_slices_are_not_stacked(node):
     kubelet = FakeKubelet(sockdir, node_name="w", api=api)
     kubelet.start()
     p = _spawn(["gpu_topology_on_k8s_amd.deviceplugin", "--discovery", "amdsmi", "--gpu-events", "off", "--device-specs", "stub",
-                "--apiserver", url, "--node-name", "w", "--socket-dir", sockdir, "--dev-root", sockdir, "--log-level", "ERROR"])
+                "--apiserver", url, "--node-name", "w", "--socket-dir", sockdir, "--dev-root", sockdir, "--log-level", "ERROR",
+                "--label-check-interval", "1"])
     try:
         plug = kubelet.wait_for("amd.com/gpu", timeout=60)  # the XCPs, as whole devices of their own
         assert len(plug.devices) == 16 and "amd.com/gpu-slice" not in kubelet.plugins
-        assert p.poll() is None
+        # several label checks later the plugin is still serving: the label's count it cannot apply
+        # on a partitioned node is not a layout change (exit-75 restart loop)
+        import time
+
+        time.sleep(4.5)
+        assert p.poll() is None, p.stdout.read() if p.poll() is not None else ""
+        from gpu_topology_on_k8s_amd.k8s.annotations import probing_until
+
+        assert probing_until(api.get_node("w")["metadata"].get("annotations") or {}, c) < time.time()
     finally:
         _stop(p)
         kubelet.stop()
         srv.shutdown()
         shutil.rmtree(sockdir, ignore_errors=True)
+
+
+class _Ctx:
+    def abort(self, code, msg):
+        raise RuntimeError(code, msg)
+
+
+def _held_plugin(tmp_path):
+    from gpu_topology_on_k8s_amd.deviceplugin import DevicePluginServer, PluginConfig, placeholder_dev_tree
+    from gpu_topology_on_k8s_amd.topology import fixtures as fx
+
+    api = FakeAPIServer()
+    api.create_node(make_node("w", labels={Contract().partition_request_label: "CPX"}))
+    t = fx.f7_mi355x(n=2)
+    plug = DevicePluginServer(t, PluginConfig(node_name="w", dev_root=placeholder_dev_tree(str(tmp_path), t)), api=api)
+    return api, plug
+
+
+def _alloc_req(*ids):
+    from gpu_topology_on_k8s_amd.deviceplugin import proto as pb
+
+    req = pb.AllocateRequest()
+    req.container_requests.add(devices_ids=[str(i) for i in ids])
+    return req
+
+
+def test_allocate_during_the_settle_window_abandons_the_switch(node, tmp_path):
+    """ADVICE r3 (repartition.py:100): an Allocate that arrives while a switch is pending (a bind
+    that outlived the settle window, or a pod that bypassed the extender) is held, makes the node
+    busy, and then proceeds on the unchanged layout; no amdsmi step runs."""
+    import threading
+    import time
+
+    from gpu_topology_on_k8s_amd.deviceplugin.repartition import repartition
+
+    api, plug = _held_plugin(tmp_path)
+    out = {}
+    th = threading.Thread(target=lambda: out.setdefault("r", repartition(
+        api, "w", Contract(), lambda: True, settle_s=0.6, hold=plug.allocation_hold)))
+    th.start()
+    t0 = time.time()
+    while plug._hold is None:
+        assert time.time() - t0 < 5
+        time.sleep(0.01)
+    resp = plug.Allocate(_alloc_req(1), _Ctx())  # waits for the pass to give up, then succeeds
+    th.join(5)
+    assert len(resp.container_responses) == 1
+    assert out["r"][0] == "busy"
+    assert node["state"].read_text().split()[0] == "1"  # still SPX: amdsmi never ran
+    assert Contract().probing_key not in (api.get_node("w")["metadata"].get("annotations") or {})
+
+
+def test_allocate_held_across_a_switch_is_refused_not_given_stale_devices(node, tmp_path, monkeypatch):
+    """An Allocate that arrives once the amdsmi steps run cannot stop them: it waits for the switch and
+    is refused (UNAVAILABLE), since its device IDs name the old layout."""
+    import threading
+    import time
+
+    import grpc
+
+    from gpu_topology_on_k8s_amd.deviceplugin import repartition as rp
+
+    api, plug = _held_plugin(tmp_path)
+    started = threading.Event()
+    real = rp.apply_partition
+
+    def slow_apply(*a, **kw):
+        started.set()
+        time.sleep(0.5)
+        return real(*a, **kw)
+
+    monkeypatch.setattr(rp, "apply_partition", slow_apply)
+    out = {}
+    th = threading.Thread(target=lambda: out.setdefault("r", rp.repartition(
+        api, "w", Contract(), lambda: True, settle_s=0, hold=plug.allocation_hold)))
+    th.start()
+    assert started.wait(5)
+    with pytest.raises(RuntimeError) as ei:
+        plug.Allocate(_alloc_req(0), _Ctx())
+    th.join(5)
+    assert out["r"][0] == "ok"
+    assert ei.value.args[0] == grpc.StatusCode.UNAVAILABLE and "repartitioned" in ei.value.args[1]
+    assert 'gtk_plugin_allocations_total{outcome="switch_wait"} 1.0' in plug.metrics.exposition().decode()
+
+
+def test_driver_reload_is_held_back_when_the_node_stops_being_idle(node):
+    """The last idle check sits right before the amdgpu reload (the most disruptive step)."""
+    r = apply_partition("CPX")
+    assert r["ok"]
+    r = apply_partition("CPX", "NPS4", reload_driver=True, before_reload=lambda: False)
+    assert not r["ok"] and r["reload_required"] and "held back" in r["reason"]
+    assert not any(s["set"] == "driver-reload" for s in r["steps"])
