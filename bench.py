@@ -674,6 +674,15 @@ def main(argv=None) -> int:
             "probe_bound_kind": "k6-ring" if ring_bound else ("k5-ingress" if ingress else None),
             "algbw_gbps": round(algbw, 3),
             "busbw_gbps": round(busbw, 3),
+            # k >= 2 values are aggregate busBW (k x the per-rank nccl-tests busBW); k = 1 has no bus
+            # traffic (busBW = 0) and reports one rank's algBW, an HBM copy rate.  The two are different
+            # quantities: nothing should divide one by the other
+            "aggregate_busbw_gbps": round(busbw * env.world, 3) if env.world > 1 else None,
+            "per_rank_busbw_gbps": round(busbw, 3) if env.world > 1 else None,
+            "scaling_comparable": env.world > 1,
+            "scaling_note": ("comparable across k >= 2 only: aggregate busBW over xGMI" if env.world > 1 else
+                             "k=1: algBW of one rank's all-reduce = the HIP runtime's HBM device copy, not a bus rate; "
+                             "not comparable to the k>=2 aggregate busBW values"),
         }
         if watchdog is not None:
             watchdog.cancel()

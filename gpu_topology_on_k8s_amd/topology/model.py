@@ -351,7 +351,9 @@ class Topology:
     def set_measured_bw(self, bw: np.ndarray, probe_meta: Optional[Dict[str, object]] = None) -> None:
         self.bw_gbps = _quantize_bw(_as_matrix(bw, self.n, np.float64, np.nan))
         if probe_meta:
-            self.probe = dict(probe_meta)
+            # what discovery read from amdsmi is not the probe's to drop (ops/checks.py rates links by it)
+            keep = {k: v for k, v in (self.probe or {}).items() if k == "amdsmi_max_bw_mbps"}
+            self.probe = {**keep, **dict(probe_meta)}
         self.recompute_cost()
 
     # ------------------------------------------------------------------ pair views

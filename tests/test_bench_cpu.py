@@ -44,6 +44,9 @@ def test_bench_single_rank_cpu():
     out = _bench("--backend", "cpu", "--steps", "2", "--warmup", "1", "--size-mb", "1", "--via", "direct")
     assert out["k8s_placement"] is None
     assert out["n_gpus"] == 1 and out["busbw_gbps"] == 0.0 and out["value"] == out["algbw_gbps"]
+    # the k=1 point says it is a copy rate, not comparable to k>=2 aggregate busBW
+    assert out["scaling_comparable"] is False and "not comparable" in out["scaling_note"]
+    assert out["aggregate_busbw_gbps"] is None and out["per_rank_busbw_gbps"] is None
 
 
 def test_parse_ctas():
@@ -125,6 +128,8 @@ def test_bench_eight_ranks_gloo_dry_run():
     assert abs(out["busbw_gbps"] - out["algbw_gbps"] * 2 * 7 / 8) <= 1e-2 * out["busbw_gbps"] + 2e-3  # 3-decimal rounding
     assert out["size_sweep"]["all_exact"] and out["value_kind"].startswith("aggregate busbw")
     assert abs(out["value"] - 8 * out["busbw_gbps"]) <= 1e-2 * out["value"] + 2e-2  # every rank's busBW summed
+    assert out["scaling_comparable"] is True and out["aggregate_busbw_gbps"] == out["value"]
+    assert out["per_rank_busbw_gbps"] == out["busbw_gbps"]
     ph = out["phase_s"]  # the first 8-GPU run explains itself: where its wall time went
     for key in ("place", "comm", "check", "warmup", "headline", "sweep", "total"):
         assert key in ph and ph[key] >= 0, ph

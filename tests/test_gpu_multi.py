@@ -36,12 +36,22 @@ def _run(args, timeout=900, env=None):
     return json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
 
 
-def _pair_floor(rates):
-    """A link that trained down (or a copy that fell off xGMI onto host staging) runs far below its
-    siblings: every pair must reach half the median pair of the same node and 20 GB/s outright."""
-    import statistics
+def _topo():
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
 
-    return max(20.0, 0.5 * statistics.median(rates))
+    return discover("auto")
+
+
+def _hip_to_topo(t):
+    """HIP ordinal -> topology index (by PCI address; identity when the node shows all its GPUs)."""
+    from gpu_topology_on_k8s_amd.ops import probe
+
+    bdf = {g.bdf.lower(): g.index for g in t.gpus if g.bdf}
+    out = {}
+    for h in range(_ndev()):
+        b = str(probe.device_props(h).get("pci_bus_id", "")).lower()
+        out[h] = bdf.get(b, h)
+    return out
 
 
 @needs2
@@ -58,21 +68,36 @@ def test_p2p_pair_copy(mode):
                 r = probe.copy_bw(a, b, 256 << 20, iters=3, warmup_iters=1, mode=mode)
                 assert r["ok"], r
                 res[(a, b)] = r["gbps"]
-    floor = _pair_floor(list(res.values()))
-    print(json.dumps({"mode": mode, "floor": round(floor, 1), "pairs": {f"{a}->{b}": round(v, 1) for (a, b), v in res.items()}}))
-    assert all(v >= floor for v in res.values()), (floor, res)
+    # absolute floors: half the link's amdsmi-rated per-direction rate AND half the median,
+    # so links that all fell to host staging fail even though they match each other
+    from gpu_topology_on_k8s_amd.ops.checks import check_pairs, pair_floors
+
+    t = _topo()
+    h2t = _hip_to_topo(t)
+    rates = {(h2t[a], h2t[b]): v for (a, b), v in res.items()}
+    floors = pair_floors(t, rates)
+    print(json.dumps({"mode": mode, "amdsmi_max_bw_mbps": t.probe.get("amdsmi_max_bw_mbps"),
+                      "pairs": {f"{a}->{b}": [round(v, 1), round(floors[(a, b)], 1)] for (a, b), v in rates.items()}}))
+    probs = check_pairs(t, rates)
+    assert not probs, probs
 
 
 @needs2
 def test_gather_over_real_peers_beats_one_link():
     from gpu_topology_on_k8s_amd.ops import probe
 
+    from gpu_topology_on_k8s_amd.ops.checks import check_gather
+
     n = _ndev()
     peers = list(range(1, n))
-    single = max(probe.copy_bw(s, 0, 64 << 20, iters=3, warmup_iters=1)["gbps"] for s in peers)
+    single = [probe.copy_bw(s, 0, 64 << 20, iters=3, warmup_iters=1)["gbps"] for s in peers]
     g = probe.gather_bw(0, peers, 64 << 20, iters=3, warmup_iters=1)
     assert g["ok"], g
-    assert g["gbps"] >= 0.9 * single, (g, single)
+    print(json.dumps({"gather_gbps": g["gbps"], "single_gbps": single}))
+    # all k-1 links at once: at least half of (k-1) x the median single read (a gather that
+    # serialises its sources reaches about one link's worth)
+    probs = check_gather(g["gbps"], single)
+    assert not probs, probs
 
 
 @needs2
@@ -80,13 +105,13 @@ def test_probe_matrix_all_pairs():
     from gpu_topology_on_k8s_amd.ops.probe import probe_topology
     from gpu_topology_on_k8s_amd.topology.discovery import discover
 
+    from gpu_topology_on_k8s_amd.ops.checks import check_pairs, matrix_rates
+
     t = probe_topology(discover("auto"), preset="quick")
     assert t.probe["device_map"] == "bdf"
-    n = len(t.probe["devices"])
-    import numpy as np
-
-    off = t.bw_gbps[np.ix_(t.probe["devices"], t.probe["devices"])][~np.eye(n, dtype=bool)]
-    assert np.isfinite(off).all() and (off >= _pair_floor(list(off))).all(), off
+    assert "amdsmi_max_bw_mbps" in t.probe  # discovery's rated link rates survive the probe
+    probs = check_pairs(t, matrix_rates(t, t.probe["devices"]))
+    assert not probs, probs
 
 
 @needs2
@@ -104,9 +129,11 @@ def test_ring_probe_bounded_by_its_links():
     r = measure_ring([t.probe["hip_ordinals"][devs.index(d)] for d in devs], "quick")
     pair_sum = ingress_bound(t, devs)
     print(json.dumps({"ring": r, "pair_sum_bound": pair_sum}))
+    from gpu_topology_on_k8s_amd.ops.checks import check_ring
+
     assert pair_sum is not None and np.isfinite(pair_sum)
-    assert r["ring_bound_gbps"] <= 1.1 * pair_sum, (r, pair_sum)
-    assert r["ring_bound_gbps"] >= 0.3 * pair_sum, (r, pair_sum)
+    probs = check_ring(r["ring_bound_gbps"], pair_sum)  # 0.6x..1.1x the pair-sum bound
+    assert not probs, probs
     if len(devs) > 3:
         assert r["ring"]["bound_gbps"] <= 1.05 * r["all"]["bound_gbps"], r
 

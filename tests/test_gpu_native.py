@@ -46,7 +46,8 @@ def test_mfma_random_operands_rate(probe_mod):
 
     r = warmup(0, 100.0, random_operands=True)
     print(json.dumps({"mfma_random_tflops": round(r["tflops"], 1)}))
-    assert r["random_operands"] and r["tflops"] > 800, r
+    # 1.76-1.88 PF/s measured (r03); ~75 % of that, so a 25 % regression fails
+    assert r["random_operands"] and r["tflops"] > 1300, r
 
 
 # copy GB/s floors at 512 MiB (HBM moves twice that): ~75 % of what r02 measured for each form
@@ -75,7 +76,15 @@ def test_gather_kernel_segments(probe_mod):
     """K5 gather: three source buffers streamed by one launch land in their own dst segments (the
     sources are local here; on a node they are the peers, same kernel); odd size exercises tails."""
     r = probe_mod.gather_bw(0, [0, 0, 0], (16 << 20) + 4112, 2, 1)
-    assert r["ok"] and r["gbps"] > 100 and r["bytes_per_src"] == (16 << 20) + 4112
+    assert r["ok"] and r["bytes_per_src"] == (16 << 20) + 4112
+
+
+def test_gather_kernel_rate(probe_mod):
+    """K5 at the size it was measured at (7 sources x 256 MiB: 2.41 TB/s copy, r03); the floor is ~75 %
+    of that, so a gather that serialises or stalls its sources fails here on one GPU."""
+    r = probe_mod.gather_bw(0, [0] * 7, 256 << 20, 3, 1)
+    print(json.dumps({"gather_gbps": round(r["gbps"], 1)}))
+    assert r["ok"] and r["gbps"] > 1800, r
 
 
 @pytest.mark.parametrize("members,pattern", [(3, "all"), (4, "ring"), (2, "all")])
@@ -91,6 +100,16 @@ def test_ring_kernel_segments(probe_mod, members, pattern):
     assert len(r["ingress_gbps"]) == members and min(r["ingress_gbps"]) == pytest.approx(r["bound_gbps"])
     assert r["bound_gbps"] > 50 and r["wall_ms"] > 0
     print(json.dumps({"members": members, "pattern": pattern, "bound_gbps": round(r["bound_gbps"], 1)}))
+
+
+def test_ring_kernel_rate():
+    """K6 with 3 members at 512 MiB, every member gathering from the other two at once: 951-977 GB/s per
+    member measured (r03_ring); floor ~75 % of it."""
+    from gpu_topology_on_k8s_amd.ops.probe import ring_bw
+
+    r = ring_bw([0, 0, 0], "all", 512 << 20, iters=3, warmup_iters=1)
+    print(json.dumps({"ring3_bound_gbps": round(r["bound_gbps"], 1), "ingress": [round(x, 1) for x in r["ingress_gbps"]]}))
+    assert r["ok"] and r["bound_gbps"] > 700, r
 
 
 def test_ring_probe_child_cli():
@@ -370,7 +389,7 @@ def test_ipc_read_across_processes():
         runs[mode] = (p.returncode, json.loads(lines[-1]) if lines else {"stderr": p.stderr[-500:]})
     print(json.dumps(runs))
     rc, out = runs["0"]
-    assert rc == 0 and out["ok"] and out["read_gbps"] > 1000, out
+    assert rc == 0 and out["ok"] and out["read_gbps"] > 2500, out  # 3442 measured (r03); ~75 %
 
 
 @pytest.mark.parametrize("mode,key,floor", [("write", "write_gbps", 2000.0), ("gather", "ingress_gbps", 1500.0)])

@@ -252,6 +252,64 @@ def test_vgpu_guard_holds_against_an_in_process_rewrite(tmp_path):
     assert 0.15 * full < g["tflops"] < 0.40 * full, (g["tflops"], full)
 
 
+_FIRST_CALL_CHILD = r"""
+import ctypes, json, os, sys
+os.environ["HSA_CU_MASK"] = "0:0-255"             # the program widens its own mask first
+hip = ctypes.CDLL("libamdhip64.so")               # the runtime the framework's extensions link
+v = ctypes.c_int()
+first = sys.argv[1]
+if first == "hipRuntimeGetVersion":
+    hip.hipRuntimeGetVersion(ctypes.byref(v))
+else:
+    hip.hipDeviceGetAttribute(ctypes.byref(v), ctypes.c_int(63), ctypes.c_int(0))  # any attribute
+class Extent(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_size_t), ("height", ctypes.c_size_t), ("depth", ctypes.c_size_t)]
+class Pitched(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("pitch", ctypes.c_size_t), ("xsize", ctypes.c_size_t), ("ysize", ctypes.c_size_t)]
+big, small = Pitched(), Pitched()
+e_big = hip.hipMalloc3D(ctypes.byref(big), Extent(1 << 20, 20 << 10, 1))     # 20 GiB of 3D array: past the share
+e_small = hip.hipMalloc3D(ctypes.byref(small), Extent(1 << 20, 1 << 10, 1))  # 1 GiB: inside it
+g = ctypes.CDLL(None)
+g.gtk_vgpu_used.restype = ctypes.c_longlong
+used = g.gtk_vgpu_used(0)
+hip.hipFree(ctypes.c_void_p(small.ptr))
+from gpu_topology_on_k8s_amd.ops.probe import warmup
+r = warmup(0, 30.0)
+print(json.dumps({"e_big": e_big, "e_small": e_small, "used_with_small": used, "tflops": r["tflops"],
+                  "masked_queues": g.gtk_vgpu_masked_queues()}))
+"""
+
+
+@pytest.mark.parametrize("first", ["hipRuntimeGetVersion", "hipDeviceGetAttribute"])
+def test_vgpu_guard_holds_whatever_the_first_hip_call(tmp_path, first):
+    """VERDICT r3 next #5, on the real runtime: the program rewrites HSA_CU_MASK and its first HIP call
+    is one no list of 'first calls' names.  The guard works at ROCr (hsa_init, hsa_queue_create, the
+    pool allocator), so the MFMA loop still runs on the share's 64 of 256 CUs, a hipMalloc3D past the
+    16 GiB share is refused and one inside it is charged."""
+    from gpu_topology_on_k8s_amd._native import binary
+
+    conf = tmp_path / "gtk-vgpu.conf"
+    conf.write_text(f"hbm_limit 0 {16 << 30}\ncu_mask 0:0-63\n")
+    env = {k: v for k, v in os.environ.items() if k not in _STRIP}
+    env.pop("HSA_CU_MASK", None)
+    env.update(GTK_VGPU_CONFIG=str(conf))
+    env["LD_PRELOAD"] = (env["LD_PRELOAD"] + ":" if env.get("LD_PRELOAD") else "") + str(binary("libgtk_vgpu.so"))
+    p = subprocess.run([sys.executable, "-c", _FIRST_CALL_CHILD, first], capture_output=True, text=True, timeout=240, cwd=REPO,
+                       env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    g = json.loads(p.stdout.strip().splitlines()[-1])
+    base_env = {k: v for k, v in os.environ.items() if k not in _STRIP}
+    base_env.pop("HSA_CU_MASK", None)
+    q = subprocess.run([sys.executable, "-c", "import json; from gpu_topology_on_k8s_amd.ops.probe import warmup;"
+                        "print(json.dumps(warmup(0, 30.0)))"], capture_output=True, text=True, timeout=240, cwd=REPO, env=base_env)
+    assert q.returncode == 0, q.stderr[-3000:]
+    full = json.loads(q.stdout.strip().splitlines()[-1])["tflops"]
+    print(json.dumps({"first": first, "guarded": g, "full_tflops": full}))
+    assert g["e_big"] == 2 and g["e_small"] == 0  # hipErrorOutOfMemory past the share
+    assert g["used_with_small"] >= 1 << 30 and g["masked_queues"] > 0
+    assert 0.15 * full < g["tflops"] < 0.40 * full, (g["tflops"], full)
+
+
 def test_doctor_inside_a_guarded_half_gpu_pod(tmp_path):
     """A whole pod start on the real GPU: the device plugin (real discovery, 2 time slices, guard on)
     allocates slice 0; a process gets exactly what the container would (the Allocate envs, the guard
