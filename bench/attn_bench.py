@@ -69,7 +69,8 @@ def main():
         t = timeit(lambda: hip.attn_bwd_v2(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
         res["hip_bwd_v2_ms"] = t * 1e3
     if a.ab:
-        variants = {n: getattr(hip, n) for n in ("attn_bwd", "attn_bwd_v5t", "attn_bwd_v4", "attn_bwd_v3") if hasattr(hip, n)}
+        variants = {n: getattr(hip, n) for n in ("attn_bwd", "attn_bwd_dq_alias", "attn_bwd_v5t", "attn_bwd_v4", "attn_bwd_v3")
+                    if hasattr(hip, n)}
         times = {n: [] for n in variants}
         for fn in variants.values():
             fn(do, q, k, v, o, lse, Dh ** -0.5)
@@ -82,6 +83,17 @@ def main():
                 times[n].append((e0, e1))
         torch.cuda.synchronize()
         res["ab_median_ms"] = {n: sorted(x.elapsed_time(y) for x, y in ts)[len(ts) // 2] for n, ts in times.items()}
+        fvars = {n: getattr(hip, n) for n in ("attn_fwd", "attn_fwd_noalias") if hasattr(hip, n)}
+        ftimes = {n: [] for n in fvars}
+        for _ in range(a.ab):
+            for n, fn in fvars.items():
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn(q, k, v, Dh ** -0.5)
+                e1.record()
+                ftimes[n].append((e0, e1))
+        torch.cuda.synchronize()
+        res["ab_fwd_median_ms"] = {n: sorted(x.elapsed_time(y) for x, y in ts)[len(ts) // 2] for n, ts in ftimes.items()}
     try:
         t = timeit(lambda: F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True), a.iters)
         res["sdpa_fwd_ms"] = t * 1e3

@@ -142,9 +142,12 @@ struct KVStage {
   }
 };
 
-// every wave's outstanding LDS-DMA has landed, then a barrier makes it visible to the workgroup
+// Every wave's outstanding LDS-DMA has landed AND every LDS read it issued has returned, then a
+// barrier: after it, the tile just staged is visible to the workgroup and the tile just read may be
+// overwritten by the next DMA.  Both halves of that contract are spelled out here rather than left to
+// the barrier's fence lowering or to the compiler's LDS-DMA alias analysis.
 __device__ __forceinline__ void dma_sync() {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 }
 
@@ -293,6 +296,155 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict
       tile(kt, key0 + BK - 1 > q0);
     } else if (kt + 1 < ntiles) {
       gload(kt + 1, smem + ((kt + 1) & 1) * (2 * BK * D * 2));
+    }
+    dma_sync();
+  }
+  const float inv = 1.f / l;
+  u16* orow = o + (((size_t)b * S + myq) * (size_t)(H) + hq) * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u16x4 v4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v4[e] = f2bf(oacc[dt][4 * g4 + e] * inv);
+      *reinterpret_cast<u16x4*>(orow + 32 * dt + 8 * g4 + 4 * hh) = v4;
+    }
+  if (hh == 0) lse2[(size_t)(b * H + hq) * S + myq] = m + log2f(l);
+}
+
+// ---- forward with the tile's LDS images as __restrict__ parameters (the default since round 4).
+// fwd2's tile reads the K/V images of buffer kt&1 and issues the DMA of tile kt+1 into buffer
+// (kt+1)&1, both through pointers into ONE __shared__ array with a run-time index, so the compiler
+// cannot prove the DMA target disjoint from the images and inserts `s_waitcnt vmcnt(0)` before the
+// first transposed V read: every tile waited mid-way for the next tile's DMA.  Passing the three
+// images as __restrict__ parameters of an inlined function gives their accesses scoped-noalias
+// metadata, the LDS-DMA wait tracking sees the reads and the DMA as disjoint, and the wait goes; the
+// DMA now lands under the softmax AND the PV MFMAs.  Correctness does not rest on that analysis: the
+// only orderings the double buffer needs (tile kt+1 staged before it is read; tile kt's reads
+// returned before its buffer is refilled) are dma_sync()'s explicit vmcnt(0) lgkmcnt(0) + barrier at
+// the end of every tile.  Same instructions and order of arithmetic as fwd2: bit-identical output.
+template <bool kMasked>
+__device__ __forceinline__ void fwd_tile_na(const char* __restrict__ kimg, const char* __restrict__ vimg,
+                                            char* __restrict__ nimg, bool prefetch, const KVStage& stage, int kt,
+                                            const bf16x8 (&qf)[8], f32x16 (&oacc)[4], float& m, float& l, int lane, int r,
+                                            int hh, int myq, float c) {
+  const int key0 = kt * BK;
+  f32x16 s0 = f32x16{}, s1 = f32x16{};
+  __builtin_amdgcn_s_setprio(1);
+  {
+    bf16x8 kf0[8], kf1[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      kf0[s] = lds_b128(kimg, swz(r, 2 * s + hh));
+      kf1[s] = lds_b128(kimg, swz(32 + r, 2 * s + hh));
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      s0 = mfma(kf0[s], qf[s], s0);
+      s1 = mfma(kf1[s], qf[s], s1);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x8, 8, 0);
+  }
+  __builtin_amdgcn_s_setprio(0);
+  if (prefetch) stage.load(kt + 1, nimg);  // lands under softmax + PV
+  if (kMasked) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int k0i = key0 + crow(i, hh);
+      if (k0i > myq) s0[i] = -INFINITY;
+      if (k0i + 32 > myq) s1[i] = -INFINITY;
+    }
+  }
+  float mx = max3(s0[0], s1[0], s0[1]);
+#pragma unroll
+  for (int i = 1; i < 16; ++i) mx = max3(mx, s1[i], i + 1 < 16 ? s0[i + 1] : s1[i]);
+  const float mrow = xhalf_max(mx) * c;
+  const float mnew = mrow > m + kMaxSlack ? mrow : m;
+  const bool resc = __any(mnew != m);
+  float rs = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    s0[i] = fexp2(fmaf(s0[i], c, -mnew));
+    s1[i] = fexp2(fmaf(s1[i], c, -mnew));
+    rs += s0[i] + s1[i];
+  }
+  rs += __shfl_xor(rs, 32, 64);
+  if (resc) {
+    const float alpha = fexp2(m - mnew);
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+  }
+  l += rs;
+  m = mnew;
+  const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 8), p10 = pack8(s1, 0), p11 = pack8(s1, 8);
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const int col0 = 32 * dt;
+    oacc[dt] = mfma(tr_frag(vimg, lane, 0 + 4 * hh, 8 + 4 * hh, col0), p00, oacc[dt]);
+    oacc[dt] = mfma(tr_frag(vimg, lane, 16 + 4 * hh, 24 + 4 * hh, col0), p01, oacc[dt]);
+    oacc[dt] = mfma(tr_frag(vimg, lane, 32 + 4 * hh, 40 + 4 * hh, col0), p10, oacc[dt]);
+    oacc[dt] = mfma(tr_frag(vimg, lane, 48 + 4 * hh, 56 + 4 * hh, col0), p11, oacc[dt]);
+  }
+  __builtin_amdgcn_s_setprio(0);
+}
+
+__global__ __launch_bounds__(256, 2) void attn_fwd2n_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
+                                                            const u16* __restrict__ v, u16* __restrict__ o,
+                                                            float* __restrict__ lse2, int H, int Hkv, int S, float c) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BK * D * 2];  // [buf][K image | V image]
+  const int t = threadIdx.x, lane = t & 63, r = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int nqb = gridDim.y;
+  const int qb = nqb - 1 - blockIdx.y;  // heaviest first
+  const int bh = xcd_head(blockIdx.x, gridDim.x), b = bh / H, hq = bh % H, hk = hq / (H / Hkv);
+  const u16* qp = q + ((size_t)(b * H + hq) * S) * D;
+  const size_t kvoff = ((size_t)(b * Hkv + hk) * S) * D;
+  const int q0 = qb * BQ + w * 32;
+  const int myq = q0 + r;
+
+  bf16x8 qf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + (size_t)myq * D + 16 * s + 8 * hh);
+
+  f32x16 oacc[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) oacc[dt] = f32x16{};
+  float m = -INFINITY, l = 0.f;
+
+  const int ntiles = (qb * BQ + BQ) / BK;
+  const KVStage stage(k + kvoff, v + kvoff, S, w, lane);
+  auto tile = [&](int kt, bool masked) {
+    const char* kimg = smem + (kt & 1) * (2 * BK * D * 2);
+    char* nimg = smem + ((kt + 1) & 1) * (2 * BK * D * 2);
+    if (masked)
+      fwd_tile_na<true>(kimg, kimg + BK * D * 2, nimg, kt + 1 < ntiles, stage, kt, qf, oacc, m, l, lane, r, hh, myq, c);
+    else
+      fwd_tile_na<false>(kimg, kimg + BK * D * 2, nimg, kt + 1 < ntiles, stage, kt, qf, oacc, m, l, lane, r, hh, myq, c);
+  };
+  stage.load(0, smem);
+  dma_sync();
+  int kt = 0;
+  for (; kt < ntiles - 2; ++kt) {
+    tile(kt, false);
+    dma_sync();
+  }
+  for (; kt < ntiles; ++kt) {
+    const int key0 = kt * BK;
+    if (key0 <= q0 + 31) {
+      tile(kt, key0 + BK - 1 > q0);
+    } else if (kt + 1 < ntiles) {
+      stage.load(kt + 1, smem + ((kt + 1) & 1) * (2 * BK * D * 2));
     }
     dma_sync();
   }
@@ -946,6 +1098,112 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(const u16* __restr
     }
 }
 
+// ---- dQ with the tile's LDS images as __restrict__ parameters (the default since round 4): the same
+// change as attn_fwd2n_kernel.  dq2's wait sat before the first transposed K read of the dQ MFMAs.
+template <bool kMasked>
+__device__ __forceinline__ void dq_tile_na(const char* __restrict__ kimg, const char* __restrict__ vimg,
+                                           char* __restrict__ nimg, bool prefetch, const KVStage& stage, int kt,
+                                           const bf16x8 (&qf)[8], const bf16x8 (&df)[8], f32x16 (&dqt)[4], float lse_q,
+                                           float del_q, int lane, int r, int hh, int myq, float c) {
+  const int key0 = kt * BK;
+  f32x16 s0 = f32x16{}, s1 = f32x16{}, e0 = f32x16{}, e1 = f32x16{};
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const bf16x8 k0 = lds_b128(kimg, swz(r, 2 * s + hh)), k1 = lds_b128(kimg, swz(32 + r, 2 * s + hh));
+    const bf16x8 v0 = lds_b128(vimg, swz(r, 2 * s + hh)), v1 = lds_b128(vimg, swz(32 + r, 2 * s + hh));
+    s0 = mfma(k0, qf[s], s0);
+    s1 = mfma(k1, qf[s], s1);
+    e0 = mfma(v0, df[s], e0);
+    e1 = mfma(v1, df[s], e1);
+  }
+  __builtin_amdgcn_s_setprio(0);
+  if (prefetch) stage.load(kt + 1, nimg);  // lands under the dQ MFMAs
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float p0 = fexp2(fmaf(s0[i], c, -lse_q));
+    float p1 = fexp2(fmaf(s1[i], c, -lse_q));
+    if (kMasked) {
+      const int kk = key0 + crow(i, hh);
+      if (kk > myq) p0 = 0.f;
+      if (kk + 32 > myq) p1 = 0.f;
+    }
+    s0[i] = p0 * (e0[i] - del_q);
+    s1[i] = p1 * (e1[i] - del_q);
+  }
+  const bf16x8 d00 = pack8(s0, 0), d01 = pack8(s0, 8), d10 = pack8(s1, 0), d11 = pack8(s1, 8);
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    dqt[dt] = mfma(tr_frag(kimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), d00, dqt[dt]);
+    dqt[dt] = mfma(tr_frag(kimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), d01, dqt[dt]);
+    dqt[dt] = mfma(tr_frag(kimg, lane, 32 + 4 * hh, 40 + 4 * hh, 32 * dt), d10, dqt[dt]);
+    dqt[dt] = mfma(tr_frag(kimg, lane, 48 + 4 * hh, 56 + 4 * hh, 32 * dt), d11, dqt[dt]);
+  }
+  __builtin_amdgcn_s_setprio(0);
+}
+
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq2n_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
+                                                               const u16* __restrict__ v, const u16* __restrict__ dout,
+                                                               const float* __restrict__ lse2, const float* __restrict__ delta,
+                                                               u16* __restrict__ dq, int H, int Hkv, int S, float c, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BK * D * 2];  // [buf][K image | V image]
+  const int t = threadIdx.x, lane = t & 63, r = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int nqb = gridDim.y, qb = nqb - 1 - blockIdx.y;
+  const int bh = xcd_head(blockIdx.x, gridDim.x), b = bh / H, hq = bh % H, hk = hq / (H / Hkv);
+  const size_t kvoff = ((size_t)(b * Hkv + hk) * S) * D;
+  const int q0 = qb * BQ + w * 32, myq = q0 + r;
+  const u16* qrow = q + ((size_t)(b * H + hq) * S + myq) * D;
+  const u16* dorow = dout + (((size_t)b * S + myq) * H + hq) * D;
+  bf16x8 qf[8], df[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    qf[s] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s + 8 * hh);
+    df[s] = *reinterpret_cast<const bf16x8*>(dorow + 16 * s + 8 * hh);
+  }
+  const float lse_q = lse2[(size_t)(b * H + hq) * S + myq], del_q = delta[(size_t)(b * H + hq) * S + myq];
+  f32x16 dqt[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dqt[dt] = f32x16{};
+  const int ntiles = (qb * BQ + BQ) / BK;
+  const KVStage stage(k + kvoff, v + kvoff, S, w, lane);
+  auto tile = [&](int kt, bool masked) {
+    const char* kimg = smem + (kt & 1) * (2 * BK * D * 2);
+    char* nimg = smem + ((kt + 1) & 1) * (2 * BK * D * 2);
+    if (masked)
+      dq_tile_na<true>(kimg, kimg + BK * D * 2, nimg, kt + 1 < ntiles, stage, kt, qf, df, dqt, lse_q, del_q, lane, r, hh, myq, c);
+    else
+      dq_tile_na<false>(kimg, kimg + BK * D * 2, nimg, kt + 1 < ntiles, stage, kt, qf, df, dqt, lse_q, del_q, lane, r, hh, myq, c);
+  };
+  stage.load(0, smem);
+  dma_sync();
+  int kt = 0;
+  for (; kt < ntiles - 2; ++kt) {
+    tile(kt, false);
+    dma_sync();
+  }
+  for (; kt < ntiles; ++kt) {
+    const int key0 = kt * BK;
+    if (key0 <= q0 + 31) {
+      tile(kt, key0 + BK - 1 > q0);
+    } else if (kt + 1 < ntiles) {
+      stage.load(kt + 1, smem + ((kt + 1) & 1) * (2 * BK * D * 2));
+    }
+    dma_sync();
+  }
+  u16* out = dq + ((size_t)(b * H + hq) * S + myq) * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u16x4 a4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a4[e] = f2bf(dqt[dt][4 * g4 + e] * scale);
+      *reinterpret_cast<u16x4*>(out + 32 * dt + 8 * g4 + 4 * hh) = a4;
+    }
+}
+
 // ==================================================================================== host
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 const u16* bp(const at::Tensor& t) { return reinterpret_cast<const u16*>(t.data_ptr()); }
@@ -962,15 +1220,32 @@ void check_qkv(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
   TORCH_CHECK(q.size(1) * q.size(2) * D * 2 < (int64_t(1) << 31), "attention: per-batch q/dO bytes must fit the 32-bit buffer offsets");
 }
 
-std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale) {
+std::vector<at::Tensor> attn_fwd_variant(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale,
+                                         bool noalias) {
   check_qkv(q, k, v);
   const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
   auto o = at::empty({B, S, H, D}, q.options());
   auto lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
   const float c = (float)(scale * 1.4426950408889634);
-  hipLaunchKernelGGL(attn_fwd2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bpm(o),
-                     lse.data_ptr<float>(), H, Hkv, S, c);
+  if (noalias)
+    hipLaunchKernelGGL(attn_fwd2n_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bpm(o),
+                       lse.data_ptr<float>(), H, Hkv, S, c);
+  else
+    hipLaunchKernelGGL(attn_fwd2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bpm(o),
+                       lse.data_ptr<float>(), H, Hkv, S, c);
   return {o, lse};
+}
+
+// default forward: fwd2.  fwd2n (no mid-tile DMA wait) computes the same bits but measured 1.4-2 %
+// slower on MI355X (profiles/r04_attn: the wait costs nothing -- the DMA has landed during the
+// softmax -- and fwd2n spills 9 VGPRs in its peeled diagonal tiles)
+std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale) {
+  return attn_fwd_variant(q, k, v, scale, false);
+}
+
+// fwd2n (LDS images as __restrict__ tile parameters, no mid-tile DMA wait): A/B reference, bit-identical
+std::vector<at::Tensor> attn_fwd_noalias(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale) {
+  return attn_fwd_variant(q, k, v, scale, true);
 }
 
 // v3 dK/dV (kept for A/B: v4 must match it bit for bit) + dQ v2
@@ -1015,7 +1290,8 @@ std::vector<at::Tensor> attn_bwd_v4(const at::Tensor& dout, const at::Tensor& q,
 
 // default backward: delta, dK/dV v5 (software-pipelined slices, operands read ahead of the DMA), dQ v2
 std::vector<at::Tensor> attn_bwd_order(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                       const at::Tensor& out, const at::Tensor& lse, double scale, bool s_first) {
+                                       const at::Tensor& out, const at::Tensor& lse, double scale, bool s_first,
+                                       bool dq_noalias = true) {
   check_qkv(q, k, v);
   const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
   TORCH_CHECK(dout.is_contiguous() && out.is_contiguous() && dout.numel() == q.numel() && out.numel() == q.numel(),
@@ -1032,14 +1308,25 @@ std::vector<at::Tensor> attn_bwd_order(const at::Tensor& dout, const at::Tensor&
   else
     hipLaunchKernelGGL(attn_bwd_dkdv5_kernel<false>, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v),
                        bp(dout), lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
-  hipLaunchKernelGGL(attn_bwd_dq2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
-                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
+  if (dq_noalias)
+    hipLaunchKernelGGL(attn_bwd_dq2n_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
+                       lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
+  else
+    hipLaunchKernelGGL(attn_bwd_dq2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
+                       lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
   return {dq, dk, dv};
 }
 
 std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                  const at::Tensor& out, const at::Tensor& lse, double scale) {
   return attn_bwd_order(dout, q, k, v, out, lse, scale, true);
+}
+
+// default order with the round-3 dQ (dq2: one-array images, mid-tile DMA wait): A/B reference, bit-identical.
+// The default dQ is dq2n: 1.2 % faster whole backward at B 4 x 4096, equal at B 2 (profiles/r04_attn)
+std::vector<at::Tensor> attn_bwd_dq_alias(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                          const at::Tensor& out, const at::Tensor& lse, double scale) {
+  return attn_bwd_order(dout, q, k, v, out, lse, scale, true, false);
 }
 
 // v5 with the previous slice's transposed reads issued first (the round-3 order): A/B reference

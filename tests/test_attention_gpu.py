@@ -158,9 +158,34 @@ def test_attention_is_deterministic_at_the_training_shape(fused):
     hip = fused.hip()
     o, lse = hip.attn_fwd(q, k, v, 128 ** -0.5)
     g = hip.attn_bwd(do, q, k, v, o, lse, 128 ** -0.5)
-    for _ in range(2):
+    for _ in range(4):
         o2, lse2 = hip.attn_fwd(q, k, v, 128 ** -0.5)
         assert torch.equal(o2, o) and torch.equal(lse2, lse)
         g2 = hip.attn_bwd(do, q, k, v, o, lse, 128 ** -0.5)
         for name, a, b in zip(("dq", "dk", "dv"), g2, g):
             assert torch.equal(a, b), name
+    # the A/B variants (fwd2n without the mid-tile DMA wait; the round-3 dQ dq2 with it): same bits
+    oa, lsea = hip.attn_fwd_noalias(q, k, v, 128 ** -0.5)
+    assert torch.equal(oa, o) and torch.equal(lsea, lse)
+    ga = hip.attn_bwd_dq_alias(do, q, k, v, o, lse, 128 ** -0.5)
+    for name, a, b in zip(("dq", "dk", "dv"), ga, g):
+        assert torch.equal(a, b), name
+
+
+@pytest.mark.parametrize("B,H,Hkv,S", CASES + [(1, 32, 8, 8192)])
+def test_noalias_kernels_match_the_round3_kernels_bitwise(fused, B, H, Hkv, S):
+    """fwd2n / dq2n (LDS images as __restrict__ tile parameters: no mid-tile DMA wait) against fwd2 /
+    dq2 (one LDS array, the compiler's wait) at every test shape, including the causal diagonal's
+    peeled tiles: bit-identical."""
+    torch.manual_seed(B * 1000 + S)
+    q = torch.randn(B, H, S, 128, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
+    do = torch.randn(B, S, H, 128, device="cuda", dtype=torch.bfloat16)
+    hip = fused.hip()
+    o, lse = hip.attn_fwd(q, k, v, 128 ** -0.5)
+    oa, lsea = hip.attn_fwd_noalias(q, k, v, 128 ** -0.5)
+    assert torch.equal(o, oa) and torch.equal(lse, lsea)
+    dq = hip.attn_bwd(do, q, k, v, o, lse, 128 ** -0.5)[0]
+    dqa = hip.attn_bwd_dq_alias(do, q, k, v, o, lse, 128 ** -0.5)[0]
+    assert torch.equal(dq, dqa)

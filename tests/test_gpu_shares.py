@@ -268,6 +268,7 @@ class Pitched(ctypes.Structure):
     _fields_ = [("ptr", ctypes.c_void_p), ("pitch", ctypes.c_size_t), ("xsize", ctypes.c_size_t), ("ysize", ctypes.c_size_t)]
 big, small = Pitched(), Pitched()
 e_big = hip.hipMalloc3D(ctypes.byref(big), Extent(1 << 20, 20 << 10, 1))     # 20 GiB of 3D array: past the share
+hip.hipGetLastError()                             # consume the expected OOM (HIP keeps it as the thread's last error)
 e_small = hip.hipMalloc3D(ctypes.byref(small), Extent(1 << 20, 1 << 10, 1))  # 1 GiB: inside it
 g = ctypes.CDLL(None)
 g.gtk_vgpu_used.restype = ctypes.c_longlong

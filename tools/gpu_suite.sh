@@ -66,6 +66,13 @@ c = probe.copy_bw(0, 0, 512 << 20, 5, 1)
 print(json.dumps({"tflops": round(float(w["tflops"]), 1), "hbm_copy_gbps": round(float(c["gbps"]), 1)}))' >> "$out/cumask.log" 2>&1 || exit 1
     done
     ;;
+  attn)
+    # attention kernels: bit-identity / determinism tests, interleaved A/B timings, MFMA-busy counters
+    step pytest_attn 600 python -u -m pytest tests/test_attention_gpu.py -x -v --timeout 300 --timeout-method thread
+    step ab_b4 300 python -u bench/attn_bench.py --b 4 --s 4096 --iters 5 --ab 30
+    step ab_b2 300 python -u bench/attn_bench.py --b 2 --s 4096 --iters 5 --ab 30
+    step pmc_attn 120 timeout -s KILL 100 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_INST_LDS --kernel-trace -d "$out/pmc_attn" -o run -- python3 tools/pmc_attn.py
+    ;;
   *) echo "unknown mode $mode"; exit 2 ;;
 esac
 echo "[gpu_suite] done"

@@ -29,6 +29,10 @@ def main():
     for _ in range(3):
         o, lse = hip.attn_fwd(q, k, v, D ** -0.5)
         hip.attn_bwd(do, q, k, v, o, lse, D ** -0.5)
+    if hasattr(hip, "attn_fwd_noalias"):  # fwd2n / dq2: the A/B variants, same pass: per-kernel counters of both
+        for _ in range(3):
+            o, lse = hip.attn_fwd_noalias(q, k, v, D ** -0.5)
+            hip.attn_bwd_dq_alias(do, q, k, v, o, lse, D ** -0.5)
     torch.cuda.synchronize()
     print("pmc_attn done", flush=True)
 
