@@ -47,6 +47,7 @@ __device__ __forceinline__ float wave_max(float v) {
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 
 #define CHECK_BF16(t) TORCH_CHECK((t).is_cuda() && (t).scalar_type() == at::kBFloat16 && (t).is_contiguous(), #t " must be a contiguous bf16 GPU tensor")
+#define CHECK_GRAD(t) TORCH_CHECK((t).is_cuda() && ((t).scalar_type() == at::kBFloat16 || (t).scalar_type() == at::kFloat) && (t).is_contiguous(), #t " must be a contiguous bf16 or fp32 GPU tensor")
 #define CHECK_F32(t) TORCH_CHECK((t).is_cuda() && (t).scalar_type() == at::kFloat && (t).is_contiguous(), #t " must be a contiguous fp32 GPU tensor")
 
 const u16* bp(const at::Tensor& t) { return reinterpret_cast<const u16*>(t.data_ptr()); }
@@ -645,15 +646,30 @@ void xent_bwd_inplace(at::Tensor& logits, const at::Tensor& labels, const at::Te
 // each of master/m/v, one 16-B load of the bf16 gradient; writes master/m/v and the bf16 weight.
 // hp: device fp32 [lr, beta1, beta2, eps, weight_decay, grad_scale, bias_c1, bias_c2] so a captured
 // graph replays with updated hyper-parameters.
+// 8 gradient elements of vector i as fp32: the bf16 gradient buffer, or the fp32 buffer a DP
+// all-reduce in fp32 leaves (parallel/dp.py grad_reduce="fp32")
+__device__ __forceinline__ void load_g8(const u16* __restrict__ g, size_t i, float (&out)[8]) {
+  const u16x8 gv = reinterpret_cast<const u16x8*>(g)[i];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = bf2f(gv[j]);
+}
+__device__ __forceinline__ void load_g8(const float* __restrict__ g, size_t i, float (&out)[8]) {
+  const f32x4 a = reinterpret_cast<const f32x4*>(g)[2 * i], b = reinterpret_cast<const f32x4*>(g)[2 * i + 1];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) out[j] = a[j], out[j + 4] = b[j];
+}
+
+template <typename G>
 __device__ __forceinline__ void adamw_body(float* __restrict__ master, float* __restrict__ m, float* __restrict__ v,
-                                           const u16* __restrict__ g, u16* __restrict__ w, size_t n, float lr, float b1,
+                                           const G* __restrict__ g, u16* __restrict__ w, size_t n, float lr, float b1,
                                            float b2, float eps, float wd, float gs, float bc1, float bc2) {
   const size_t nv = n >> 3;
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (size_t)gridDim.x * 256) {
     f32x4 p0 = reinterpret_cast<f32x4*>(master)[2 * i], p1 = reinterpret_cast<f32x4*>(master)[2 * i + 1];
     f32x4 m0 = reinterpret_cast<f32x4*>(m)[2 * i], m1 = reinterpret_cast<f32x4*>(m)[2 * i + 1];
     f32x4 v0 = reinterpret_cast<f32x4*>(v)[2 * i], v1 = reinterpret_cast<f32x4*>(v)[2 * i + 1];
-    const u16x8 gv = reinterpret_cast<const u16x8*>(g)[i];
+    float gf[8];
+    load_g8(g, i, gf);
     u16x8 wo;
     float p[8], mm[8], vv[8];
 #pragma unroll
@@ -664,7 +680,7 @@ __device__ __forceinline__ void adamw_body(float* __restrict__ master, float* __
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float gr = bf2f(gv[j]) * gs;
+      const float gr = gf[j] * gs;
       mm[j] = b1 * mm[j] + (1.f - b1) * gr;
       vv[j] = b2 * vv[j] + (1.f - b2) * gr * gr;
       const float upd = (mm[j] / bc1) / (sqrtf(vv[j] / bc2) + eps);
@@ -687,8 +703,9 @@ __device__ __forceinline__ void adamw_body(float* __restrict__ master, float* __
   }
 }
 
+template <typename G>
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, float* __restrict__ m, float* __restrict__ v,
-                                                    const u16* __restrict__ g, u16* __restrict__ w, const float* __restrict__ hp,
+                                                    const G* __restrict__ g, u16* __restrict__ w, const float* __restrict__ hp,
                                                     size_t n) {
   adamw_body(master, m, v, g, w, n, hp[0], hp[1], hp[2], hp[3], hp[4], hp[5], hp[6], hp[7]);
 }
@@ -699,8 +716,9 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, 
 //   part = sqnorm partials of the gradient (``sq_norm_parts``); every block reduces them itself
 //   t    = optimizer step count AFTER this step (``sq_norm_parts`` advanced it in stream order)
 // Bias corrections 1 - beta^t and the clipping factor min(1, clip / ||g * grad_scale||) follow.
+template <typename G>
 __global__ __launch_bounds__(256) void adamw_dev_kernel(float* __restrict__ master, float* __restrict__ m, float* __restrict__ v,
-                                                        const u16* __restrict__ g, u16* __restrict__ w, const float* __restrict__ hp,
+                                                        const G* __restrict__ g, u16* __restrict__ w, const float* __restrict__ hp,
                                                         const float* __restrict__ part, int nparts, const float* __restrict__ tptr,
                                                         size_t n) {
   __shared__ float red[4];
@@ -720,17 +738,16 @@ __global__ __launch_bounds__(256) void adamw_dev_kernel(float* __restrict__ mast
 }
 
 // sum of squares of a bf16 buffer -> per-block partials (fp32)
-__global__ __launch_bounds__(256) void sqnorm_kernel(const u16* __restrict__ g, float* __restrict__ part, size_t n) {
+template <typename G>
+__global__ __launch_bounds__(256) void sqnorm_kernel(const G* __restrict__ g, float* __restrict__ part, size_t n) {
   __shared__ float red[4];
   float s = 0.f;
   const size_t nv = n >> 3;
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (size_t)gridDim.x * 256) {
-    const u16x8 x = reinterpret_cast<const u16x8*>(g)[i];
+    float x[8];
+    load_g8(g, i, x);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float f = bf2f(x[j]);
-      s += f * f;
-    }
+    for (int j = 0; j < 8; ++j) s += x[j] * x[j];
   }
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
@@ -742,31 +759,35 @@ void adamw_step(at::Tensor& master, at::Tensor& m, at::Tensor& v, const at::Tens
   CHECK_F32(master);
   CHECK_F32(m);
   CHECK_F32(v);
-  CHECK_BF16(g);
+  CHECK_GRAD(g);
   CHECK_BF16(w);
   CHECK_F32(hp);
   const size_t n = master.numel();
   TORCH_CHECK(n % 8 == 0 && (size_t)m.numel() == n && (size_t)v.numel() == n && (size_t)g.numel() == n && (size_t)w.numel() == n,
               "adamw: flat buffers must have equal sizes, a multiple of 8");
   TORCH_CHECK(hp.numel() >= 8, "adamw: hp needs 8 entries");
-  if (n) hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n / 8)), dim3(256), 0, cur_stream(), master.data_ptr<float>(),
-                            m.data_ptr<float>(), v.data_ptr<float>(), bp(g), bpm(w), hp.data_ptr<float>(), n);
+  if (!n) return;
+  if (g.scalar_type() == at::kFloat)
+    hipLaunchKernelGGL(adamw_kernel<float>, dim3(grid_for(n / 8)), dim3(256), 0, cur_stream(), master.data_ptr<float>(),
+                       m.data_ptr<float>(), v.data_ptr<float>(), g.data_ptr<float>(), bpm(w), hp.data_ptr<float>(), n);
+  else
+    hipLaunchKernelGGL(adamw_kernel<u16>, dim3(grid_for(n / 8)), dim3(256), 0, cur_stream(), master.data_ptr<float>(),
+                       m.data_ptr<float>(), v.data_ptr<float>(), bp(g), bpm(w), hp.data_ptr<float>(), n);
 }
 
 // sqnorm + (optionally) the step counter: block 0 / thread 0 adds 1 to ``tick`` — nothing else in
 // this kernel reads it; the AdamW kernel after it in stream order does.
-__global__ __launch_bounds__(256) void sqnorm_tick_kernel(const u16* __restrict__ g, float* __restrict__ part, size_t n,
+template <typename G>
+__global__ __launch_bounds__(256) void sqnorm_tick_kernel(const G* __restrict__ g, float* __restrict__ part, size_t n,
                                                           float* __restrict__ tick) {
   __shared__ float red[4];
   float s = 0.f;
   const size_t nv = n >> 3;
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (size_t)gridDim.x * 256) {
-    const u16x8 x = reinterpret_cast<const u16x8*>(g)[i];
+    float x[8];
+    load_g8(g, i, x);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float f = bf2f(x[j]);
-      s += f * f;
-    }
+    for (int j = 0; j < 8; ++j) s += x[j] * x[j];
   }
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
@@ -830,7 +851,7 @@ std::vector<at::Tensor> mnist_synth(const at::Tensor& proto, int64_t batch, cons
 }
 
 at::Tensor sq_norm_parts(const at::Tensor& g, c10::optional<at::Tensor> tick) {
-  CHECK_BF16(g);
+  CHECK_GRAD(g);
   const size_t n = g.numel();
   TORCH_CHECK(n % 8 == 0, "sq_norm_parts: size must be a multiple of 8");
   float* tk = nullptr;
@@ -840,7 +861,11 @@ at::Tensor sq_norm_parts(const at::Tensor& g, c10::optional<at::Tensor> tick) {
   }
   const int grid = (int)std::max<size_t>(1, std::min<size_t>((n / 8 + 255) / 256, 1024));
   auto part = at::empty({grid}, g.options().dtype(at::kFloat));  // every slot written
-  hipLaunchKernelGGL(sqnorm_tick_kernel, dim3(grid), dim3(256), 0, cur_stream(), bp(g), part.data_ptr<float>(), n, tk);
+  if (g.scalar_type() == at::kFloat)
+    hipLaunchKernelGGL(sqnorm_tick_kernel<float>, dim3(grid), dim3(256), 0, cur_stream(), g.data_ptr<float>(), part.data_ptr<float>(), n,
+                       tk);
+  else
+    hipLaunchKernelGGL(sqnorm_tick_kernel<u16>, dim3(grid), dim3(256), 0, cur_stream(), bp(g), part.data_ptr<float>(), n, tk);
   return part;
 }
 
@@ -849,7 +874,7 @@ void adamw_step_dev(at::Tensor& master, at::Tensor& m, at::Tensor& v, const at::
   CHECK_F32(master);
   CHECK_F32(m);
   CHECK_F32(v);
-  CHECK_BF16(g);
+  CHECK_GRAD(g);
   CHECK_BF16(w);
   CHECK_F32(hp);
   CHECK_F32(t);
@@ -864,18 +889,27 @@ void adamw_step_dev(at::Tensor& master, at::Tensor& m, at::Tensor& v, const at::
     pp = part->data_ptr<float>();
     np = (int)part->numel();
   }
-  if (n) hipLaunchKernelGGL(adamw_dev_kernel, dim3(grid_for(n / 8)), dim3(256), 0, cur_stream(), master.data_ptr<float>(),
-                            m.data_ptr<float>(), v.data_ptr<float>(), bp(g), bpm(w), hp.data_ptr<float>(), pp, np,
-                            t.data_ptr<float>(), n);
+  if (!n) return;
+  if (g.scalar_type() == at::kFloat)
+    hipLaunchKernelGGL(adamw_dev_kernel<float>, dim3(grid_for(n / 8)), dim3(256), 0, cur_stream(), master.data_ptr<float>(),
+                       m.data_ptr<float>(), v.data_ptr<float>(), g.data_ptr<float>(), bpm(w), hp.data_ptr<float>(), pp, np,
+                       t.data_ptr<float>(), n);
+  else
+    hipLaunchKernelGGL(adamw_dev_kernel<u16>, dim3(grid_for(n / 8)), dim3(256), 0, cur_stream(), master.data_ptr<float>(),
+                       m.data_ptr<float>(), v.data_ptr<float>(), bp(g), bpm(w), hp.data_ptr<float>(), pp, np,
+                       t.data_ptr<float>(), n);
 }
 
 at::Tensor sq_norm(const at::Tensor& g) {
-  CHECK_BF16(g);
+  CHECK_GRAD(g);
   const size_t n = g.numel();
   TORCH_CHECK(n % 8 == 0, "sq_norm: size must be a multiple of 8");
   const int grid = 1024;
   auto part = at::zeros({grid}, g.options().dtype(at::kFloat));
-  if (n) hipLaunchKernelGGL(sqnorm_kernel, dim3(grid), dim3(256), 0, cur_stream(), bp(g), part.data_ptr<float>(), n);
+  if (n && g.scalar_type() == at::kFloat)
+    hipLaunchKernelGGL(sqnorm_kernel<float>, dim3(grid), dim3(256), 0, cur_stream(), g.data_ptr<float>(), part.data_ptr<float>(), n);
+  else if (n)
+    hipLaunchKernelGGL(sqnorm_kernel<u16>, dim3(grid), dim3(256), 0, cur_stream(), bp(g), part.data_ptr<float>(), n);
   return part.sum();
 }
 
@@ -911,7 +945,18 @@ std::vector<at::Tensor> attn_bwd_v3(const at::Tensor& dout, const at::Tensor& q,
 
 namespace gtk_xpose {  // csrc/ops/transpose.hip
 at::Tensor transpose_bf16(const at::Tensor& x);
+void transpose_bf16_out(const at::Tensor& x, at::Tensor& y);
 }  // namespace gtk_xpose
+
+namespace gtk_shadow {  // csrc/ops/comm_shadow.hip
+void comm_shadow(const at::Tensor& src, at::Tensor& dst, int64_t bytes, int64_t ctas, double micros);
+}  // namespace gtk_shadow
+
+namespace gtk_adamw {  // csrc/ops/adamw_t.hip
+void adamw_step_t(at::Tensor& master, at::Tensor& m, at::Tensor& v, const at::Tensor& g, at::Tensor& w, at::Tensor& wt,
+                  const at::Tensor& hp, const at::Tensor& mats, int64_t total_tiles, const at::Tensor& ranges,
+                  int64_t max_range, c10::optional<at::Tensor> part, c10::optional<at::Tensor> t);
+}  // namespace gtk_adamw
 
 PYBIND11_MODULE(_fused, m) {
   m.def("attn_fwd", &gtk_attn::attn_fwd, "causal GQA flash attention forward (bf16, D=128): -> (o [B,S,H,D], lse2 [B,H,S])");
@@ -946,4 +991,10 @@ PYBIND11_MODULE(_fused, m) {
   m.def("mnist_xent10_fwd", &gtk_mnist::xent10_fwd, "10-class softmax cross-entropy: mean loss + unscaled gradient");
   m.def("mnist_xent10_bwd", &gtk_mnist::xent10_bwd, "scaled logits gradient + bias gradient");
   m.def("transpose_bf16", &gtk_xpose::transpose_bf16, "contiguous [R, C] bf16 -> [C, R] (R, C multiples of 64)");
+  m.def("transpose_bf16_out", &gtk_xpose::transpose_bf16_out, "transpose [R, C] bf16 into a contiguous [C, R] buffer");
+  m.def("comm_shadow", &gtk_shadow::comm_shadow,
+        "shadow of a DP collective: `ctas` workgroups copy `bytes` src -> dst, paced over at least `micros` us");
+  m.def("adamw_step_t", &gtk_adamw::adamw_step_t,
+        "AdamW over the flat buffers that also writes W^T of the listed matrices (tile kernel) and updates the listed "
+        "ranges (flat kernel); part/t given = the device-side (graph-capturable) hyper-parameter form");
 }

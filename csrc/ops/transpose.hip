@@ -93,23 +93,32 @@ __global__ __launch_bounds__(256) void transpose128_bf16_kernel(const u16* __res
   }
 }
 
-at::Tensor transpose_bf16(const at::Tensor& x) {
+// x [R, C] -> y [C, R] into a caller-provided contiguous buffer (the persistent W^T of the NT layout)
+void transpose_bf16_out(const at::Tensor& x, at::Tensor& y) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 2,
               "transpose_bf16: x must be a contiguous 2-D bf16 GPU tensor");
   const int64_t R = x.size(0), C = x.size(1);
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16 && y.is_contiguous() && y.dim() == 2 && y.size(0) == C &&
+                  y.size(1) == R,
+              "transpose_bf16_out: y must be a contiguous [C, R] bf16 GPU tensor");
   TORCH_CHECK(R % kTile == 0 && C % kTile == 0, "transpose_bf16: both dims must be multiples of 64");
   TORCH_CHECK(R / kTile <= 65535, "transpose_bf16: too many rows for the grid");
-  auto y = at::empty({C, R}, x.options());
-  if (R == 0 || C == 0) return y;
+  if (R == 0 || C == 0) return;
   if (R % kBig == 0 && C % kBig == 0) {
     hipLaunchKernelGGL(transpose128_bf16_kernel, dim3((unsigned)(C / kBig), (unsigned)(R / kBig)), dim3(256), 0,
                        at::hip::getCurrentHIPStream().stream(), reinterpret_cast<const u16*>(x.data_ptr()),
                        reinterpret_cast<u16*>(y.data_ptr()), (int)R, (int)C);
-    return y;
+    return;
   }
   hipLaunchKernelGGL(transpose_bf16_kernel, dim3((unsigned)(C / kTile), (unsigned)(R / kTile)), dim3(256), 0,
                      at::hip::getCurrentHIPStream().stream(), reinterpret_cast<const u16*>(x.data_ptr()),
                      reinterpret_cast<u16*>(y.data_ptr()), (int)R, (int)C);
+}
+
+at::Tensor transpose_bf16(const at::Tensor& x) {
+  TORCH_CHECK(x.dim() == 2, "transpose_bf16: x must be 2-D");
+  auto y = at::empty({x.size(1), x.size(0)}, x.options());
+  transpose_bf16_out(x, y);
   return y;
 }
 

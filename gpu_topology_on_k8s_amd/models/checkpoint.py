@@ -380,6 +380,8 @@ def load_checkpoint(path: str, model, opt=None, gen: Optional[torch.Generator] =
     w = read_ranges(d, [(0, flat.numel)], ("flat",))["flat"]
     with torch.no_grad():
         flat.data.copy_(w.to(flat.data.dtype), non_blocking=False)
+        if hasattr(flat, "invalidate_t"):
+            flat.invalidate_t()  # persistent W^T is re-made from the restored weights
     if opt is not None:
         st = read_optimizer_ranges(d, opt.shards)
         dev = opt.master.device

@@ -140,6 +140,92 @@ class FlatParams:
             self.params[n] = p
         self.direct: Dict[str, bool] = {}  # name -> "fresh" (not yet written since zero_grad)
         self._ready: Dict[str, List[Callable]] = {}
+        # persistent transposed weights (enable_transposed): W^T of each listed matrix in one flat
+        # bf16 buffer, written by the optimizer's fused step or re-made lazily when stale
+        self.data_t: Optional[torch.Tensor] = None
+        self.t_offsets: Dict[str, int] = {}
+        self.t_valid: Dict[str, bool] = {}
+        self._t_ver: Dict[str, int] = {}  # data._version when each W^T was last made valid
+        self.t_refreshes = 0  # lazy W^T re-makes (transposes) since construction
+        self.eager_xt = False  # NT layout: make x^T in the forward (Llama(transpose_x="forward"))
+
+    # ---------------------------------------------------------------- persistent W^T
+    def enable_transposed(self, names) -> List[str]:
+        """Keep ``W^T`` of the listed 2-D parameters resident: the NT-layout input
+        gradient reads it every backward, and W changes only in the optimizer, which writes W^T in the
+        same pass (``FlatAdamW`` + ``adamw_step_t``).  Matrices whose dims are not multiples of 64 (the
+        fused tile kernel's unit) are left out.  -> the names kept."""
+        want = set(names)
+        keep = [n for n in self.names if n in want and len(self.shapes[n]) == 2
+                and self.shapes[n][0] % 64 == 0 and self.shapes[n][1] % 64 == 0]
+        off = 0
+        self.t_offsets = {}
+        for n in keep:
+            self.t_offsets[n] = off
+            off += (math.prod(self.shapes[n]) + _ALIGN - 1) // _ALIGN * _ALIGN
+        self.data_t = torch.empty(off, dtype=self.data.dtype, device=self.data.device) if keep else None
+        self.t_valid = {n: False for n in keep}
+        self._plan = None
+        return keep
+
+    def weight_t(self, name: str) -> Optional[torch.Tensor]:
+        """``W^T`` ([in, out], contiguous) of a transposed parameter, re-made first if stale; ``None``
+        when ``name`` keeps no transposed copy."""
+        if name not in self.t_offsets:
+            return None
+        R, C = self.shapes[name]
+        o = self.t_offsets[name]
+        view = self.data_t[o:o + R * C].view(C, R)
+        # stale if invalidated, or if torch wrote the weights in place since (copy_, add_ ... bump the
+        # flat buffer's version counter; kernels and collectives do not, so their callers invalidate)
+        if not self.t_valid[name] or self._t_ver.get(name) != self.data._version:
+            w = self.params[name].detach()
+            if view.is_cuda:
+                fused.hip().transpose_bf16_out(w.contiguous(), view)
+            else:
+                view.copy_(w.t())
+            self.t_valid[name] = True
+            self._t_ver[name] = self.data._version
+            self.t_refreshes += 1
+        return view
+
+    def invalidate_t(self) -> None:
+        """The weights changed outside the optimizer's fused step (init, broadcast, ZeRO-1 all-gather,
+        checkpoint restore, an unfused optimizer): every W^T is re-made at its next use."""
+        for n in self.t_valid:
+            self.t_valid[n] = False
+
+    def mark_t_valid(self) -> None:
+        """The optimizer's fused step just wrote every W^T from the new W."""
+        ver = self.data._version
+        for n in self.t_valid:
+            self.t_valid[n] = True
+            self._t_ver[n] = ver
+
+    def adamw_plan(self):
+        """Descriptors of ``adamw_step_t``: (mats int64 [N, 5] = (offset, W^T offset, R, C, first tile),
+        total 64x64 tiles, ranges int64 [M, 2] = the rest of the flat buffer as (start, length), longest
+        range), on the buffer's device.  Cached."""
+        if self._plan is None:
+            mats, base, spans = [], 0, []
+            for n in self.names:
+                if n in self.t_offsets:
+                    R, C = self.shapes[n]
+                    mats.append((self.offsets[n], self.t_offsets[n], R, C, base))
+                    base += (R // 64) * (C // 64)
+                    spans.append((self.offsets[n], self.offsets[n] + R * C))
+            ranges, cur = [], 0
+            for a, b in sorted(spans):
+                if a > cur:
+                    ranges.append((cur, a - cur))
+                cur = b
+            if cur < self.numel:
+                ranges.append((cur, self.numel - cur))
+            dev = self.data.device
+            mt = torch.tensor(mats or [[0] * 5], dtype=torch.int64)[: len(mats)].to(dev)
+            rt = torch.tensor(ranges or [[0, 0]], dtype=torch.int64)[: len(ranges)].to(dev)
+            self._plan = (mt, base, rt, max((ln for _, ln in ranges), default=0))
+        return self._plan
 
     def mark_direct(self, name: str) -> None:
         self.direct[name] = True
@@ -246,10 +332,12 @@ class _NTOperands:
     b4 x 4096 on one MI355X: 22.8k tok/s with overlap vs 23.0k without, and +18 GB peak (all W^T
     live through backward) -- the GEMMs hold every CU, so the side stream only contends."""
 
-    def __init__(self, x: torch.Tensor, w: torch.Tensor, overlap: bool, dgrad_nn: bool = False):
+    def __init__(self, x: torch.Tensor, w: torch.Tensor, overlap: bool, dgrad_nn: bool = False,
+                 wt_fn: Optional[Callable[[], Optional[torch.Tensor]]] = None, eager_x: bool = False):
         self.event = None
         self.dgrad_nn = dgrad_nn  # dgrad reads W as is (NN): no W^T is made
-        if overlap and x.is_cuda and not dgrad_nn:
+        self.wt_fn = None if dgrad_nn else wt_fn  # the persistent W^T (FlatParams.weight_t): no per-step transpose
+        if overlap and x.is_cuda and not dgrad_nn and self.wt_fn is None:
             main = torch.cuda.current_stream(x.device)
             side = _side_stream(x.device)
             side.wait_stream(main)  # x (and the optimizer's last write of w) are complete
@@ -260,6 +348,11 @@ class _NTOperands:
             self.event = torch.cuda.Event()
             self.event.record(side)
             self.x, self.w = None, None
+        elif eager_x and x.is_cuda:
+            # x^T made in the forward, on the main stream, right after x's producer wrote it (still in
+            # the Infinity Cache): the backward finds it ready, and x itself is not kept
+            self.x_t, self.w_t = fused.transpose(x), None
+            self.x, self.w = None, w
         else:
             self.x_t = self.w_t = None
             self.x, self.w = x, w
@@ -277,10 +370,18 @@ class _NTOperands:
             self.x_t.record_stream(main)  # allocated on the side stream, consumed on the main one
             self.w_t.record_stream(main)
             self.event = None
-        elif self.x_t is None:
-            self.x_t, self.w_t = fused.transpose(self.x), fused.transpose(self.w)
+        elif self.w_t is None:
+            if self.x_t is None:
+                self.x_t = fused.transpose(self.x)
+            self.w_t = self.wt_fn() if self.wt_fn is not None else None
+            if self.w_t is None:
+                self.w_t = fused.transpose(self.w)
             self.x = self.w = None
         return self.x_t, self.w_t
+
+
+def _wt_fn(flat: "FlatParams", name: str):
+    return (lambda: flat.weight_t(name)) if name in flat.t_offsets else None
 
 
 class _FlatLinear(torch.autograd.Function):
@@ -290,7 +391,7 @@ class _FlatLinear(torch.autograd.Function):
     def forward(ctx, x, w, flat, name, nt, overlap, dgrad_nn=False):
         ctx.flat, ctx.name, ctx.nt, ctx.dgrad_nn = flat, name, nt, dgrad_nn
         if nt:
-            ctx.ops = _NTOperands(x, w, overlap, dgrad_nn)
+            ctx.ops = _NTOperands(x, w, overlap, dgrad_nn, _wt_fn(flat, name), flat.eager_xt)
         else:
             ctx.save_for_backward(x, w)
         return F.linear(x, w)
@@ -324,7 +425,7 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
         gu = F.linear(x, w)
         ctx.flat, ctx.name, ctx.nt, ctx.dgrad_nn = flat, name, nt, dgrad_nn
         if nt:
-            ctx.ops = _NTOperands(x, w, overlap, dgrad_nn)
+            ctx.ops = _NTOperands(x, w, overlap, dgrad_nn, _wt_fn(flat, name), flat.eager_xt)
             ctx.save_for_backward(gu)
         else:
             ctx.save_for_backward(gu, x, w)
@@ -355,7 +456,7 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
 class Llama(torch.nn.Module):
     def __init__(self, cfg: LlamaConfig, device="cuda", seed: int = 0, checkpoint: bool = False, attn: str = "hip",
                  gemm_layout: str = "nt", overlap_transposes: bool = False, fuse_residual: bool = True,
-                 dgrad_nn: Tuple[str, ...] = ()):
+                 dgrad_nn: Tuple[str, ...] = (), persistent_wt: bool = True, transpose_x: str = "backward"):
         super().__init__()
         if gemm_layout not in ("nt", "native"):
             raise ValueError("gemm_layout must be 'nt' or 'native'")
@@ -380,12 +481,23 @@ class Llama(torch.nn.Module):
             if p.dim() == 2 and n != "tok_emb":
                 self.flat.mark_direct(n)
         self._init(seed)
+        # NT layout: W^T of every projection stays resident and the optimizer rewrites it with W
+        # (no per-step weight transposes); dgrad_nn projections read W itself
+        if transpose_x not in ("backward", "forward"):
+            raise ValueError("transpose_x must be 'backward' or 'forward'")
+        self.transpose_x = transpose_x
+        self.flat.eager_xt = transpose_x == "forward" and gemm_layout == "nt"
+        self.persistent_wt = persistent_wt and gemm_layout == "nt"
+        if self.persistent_wt:
+            self.flat.enable_transposed([n for n in self.flat.direct
+                                         if n.rsplit(".", 1)[-1] not in self.dgrad_nn])
         cos, sin = fused.rope_tables(cfg.max_seq, cfg.head_dim, cfg.rope_theta, device=device)
         self.register_buffer("rope_cos", cos, persistent=False)
         self.register_buffer("rope_sin", sin, persistent=False)
 
     @torch.no_grad()
     def _init(self, seed: int) -> None:
+        self.flat.invalidate_t()
         dev = self.flat.data.device
         g = torch.Generator(device=dev).manual_seed(seed)  # same seed + device type => identical replicas
         std = 0.02

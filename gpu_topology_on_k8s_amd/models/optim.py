@@ -13,6 +13,11 @@ range, and the clipping norm is the all-reduced sum of every rank's shard norms.
 ``capturable=True``: the step count and every hyper-parameter stay on the device (bias corrections
 computed there), so a whole training step including :meth:`step` can be captured into a hipGraph and
 replayed (``models/train.py --graph``); the host mirror ``t`` is advanced by :meth:`note_replay`.
+
+Persistent transposed weights (``FlatParams.enable_transposed``, the NT-layout Llama): on a GPU without
+shards the step is ``adamw_step_t`` -- the projection matrices by a 64 x 64-tile kernel that writes W
+and W^T in the same pass, the rest of the buffer by the flat kernel -- and every W^T is valid after
+it.  Any other path (ZeRO-1 shards, CPU) leaves W^T stale, and the backward re-makes it on first use.
 """
 from __future__ import annotations
 
@@ -55,6 +60,8 @@ class FlatAdamW:
                                        dtype=torch.float32).to(flat.data.device)
             self._hp_scale = 1.0
         self._deferred = []  # events the next step's writes must wait for (async checkpoint copies)
+        # the fused W + W^T step (adamw_step_t) applies on a GPU without shards
+        self.fused_t = (getattr(flat, "data_t", None) is not None and not self.sharded and flat.data.is_cuda)
 
     @property
     def t(self) -> int:
@@ -79,22 +86,25 @@ class FlatAdamW:
         return 3 * self.master.numel() * 4
 
     @torch.no_grad()
-    def step(self, grad_scale: float = 1.0, sq: Optional[torch.Tensor] = None) -> None:
+    def step(self, grad_scale: float = 1.0, sq: Optional[torch.Tensor] = None, grad: Optional[torch.Tensor] = None) -> None:
         """``sq``: this rank's precomputed sum of squared gradients over its shards (the
-        data-parallel reducer's overlapped per-bucket norms); computed here when ``None``."""
+        data-parallel reducer's overlapped per-bucket norms); computed here when ``None``.
+        ``grad``: the flat gradient to apply instead of the bf16 ``flat.grad`` -- the fp32 sum a DP
+        reduction in fp32 leaves (``BucketedAllReduce.reduced_grad``); the kernels read either type."""
+        gbuf = grad if grad is not None else self.flat.grad
         if self._deferred:
             cur = torch.cuda.current_stream(self.hp.device)
             for ev in self._deferred:
                 cur.wait_event(ev)
             self._deferred.clear()
         if self.capturable:
-            self._step_device(grad_scale, sq)
+            self._step_device(grad_scale, sq, gbuf)
             return
         self._t += 1
         b1, b2 = self.betas
         gs = torch.tensor(grad_scale, dtype=torch.float32, device=self.hp.device)
         if self.clip_norm is not None:
-            for g in ([] if sq is not None else self._views(self.flat.grad)):
+            for g in ([] if sq is not None else self._views(gbuf)):
                 part = fused.hip().sq_norm(g) if g.is_cuda else g.float().pow(2).sum()
                 sq = part if sq is None else sq + part
             if self.sharded and dist.is_initialized() and dist.get_world_size(self.group) > 1:
@@ -104,8 +114,15 @@ class FlatAdamW:
         vals = torch.tensor([self.lr, b1, b2, self.eps, self.wd, 0.0, 1 - b1 ** self.t, 1 - b2 ** self.t], dtype=torch.float32)
         self.hp.copy_(vals, non_blocking=True)
         self.hp[5:6].copy_(gs.reshape(1))
+        if self.fused_t:
+            mats, tiles, ranges, maxr = self.flat.adamw_plan()
+            fused.hip().adamw_step_t(self.master, self.m, self.v, gbuf, self.flat.data, self.flat.data_t, self.hp,
+                                     mats, tiles, ranges, maxr, None, None)
+            self.flat.mark_t_valid()
+            return
+        self._invalidate_t()
         o = 0
-        for (s, e), g, d in zip(self.shards, self._views(self.flat.grad), self._views(self.flat.data)):
+        for (s, e), g, d in zip(self.shards, self._views(gbuf), self._views(self.flat.data)):
             n = e - s
             st = (self.master[o:o + n], self.m[o:o + n], self.v[o:o + n])
             if d.is_cuda:
@@ -114,19 +131,19 @@ class FlatAdamW:
                 self._step_ref(*st, g, d)
             o += n
 
-    def _clip_sq(self, sq: Optional[torch.Tensor]) -> torch.Tensor:
-        for g in ([] if sq is not None else self._views(self.flat.grad)):
+    def _clip_sq(self, sq: Optional[torch.Tensor], gbuf: torch.Tensor) -> torch.Tensor:
+        for g in ([] if sq is not None else self._views(gbuf)):
             part = fused.hip().sq_norm(g) if g.is_cuda else g.float().pow(2).sum()
             sq = part if sq is None else sq + part
         if self.sharded and dist.is_initialized() and dist.get_world_size(self.group) > 1:
             dist.all_reduce(sq, group=self.group)
         return sq
 
-    def _step_device(self, grad_scale: float, sq: Optional[torch.Tensor]) -> None:
+    def _step_device(self, grad_scale: float, sq: Optional[torch.Tensor], gbuf: torch.Tensor) -> None:
         """Host-sync-free step: no host->device copies, so it captures.  On a GPU without shards it
         is two HIP launches — ``sq_norm_parts`` (clipping partials, step counter += 1) and
         ``adamw_step_dev`` (bias corrections and clip factor derived in-kernel)."""
-        g, d = self.flat.grad, self.flat.data
+        g, d = gbuf, self.flat.data
         if d.is_cuda and not self.sharded and sq is None:
             hip = fused.hip()
             if grad_scale != self._hp_scale:  # constant per run (1/world): set once, persists across replays
@@ -139,7 +156,14 @@ class FlatAdamW:
                 self.t_dev.add_(1.0)
             if not torch.cuda.is_current_stream_capturing():
                 self._t += 1
+            if self.fused_t:
+                mats, tiles, ranges, maxr = self.flat.adamw_plan()
+                hip.adamw_step_t(self.master, self.m, self.v, g, d, self.flat.data_t, self.hp_dev, mats, tiles, ranges, maxr,
+                                 part, self.t_dev)
+                self.flat.mark_t_valid()
+                return
             hip.adamw_step_dev(self.master, self.m, self.v, g, d, self.hp_dev, part, self.t_dev)
+            self._invalidate_t()
             return
         b1, b2 = self.betas
         self.t_dev.add_(1.0)
@@ -148,12 +172,13 @@ class FlatAdamW:
         self.hp[6:7].copy_(1.0 - torch.pow(b1, self.t_dev))
         self.hp[7:8].copy_(1.0 - torch.pow(b2, self.t_dev))
         if self.clip_norm is not None:
-            norm = self._clip_sq(sq).sqrt() * grad_scale
+            norm = self._clip_sq(sq, gbuf).sqrt() * grad_scale
             self.hp[5:6].copy_((torch.clamp(self.clip_norm / (norm + 1e-6), max=1.0) * grad_scale).reshape(1))
         else:
             self.hp[5:6].fill_(grad_scale)
+        self._invalidate_t()
         o = 0
-        for (s, e), g, d in zip(self.shards, self._views(self.flat.grad), self._views(self.flat.data)):
+        for (s, e), g, d in zip(self.shards, self._views(gbuf), self._views(self.flat.data)):
             n = e - s
             st = (self.master[o:o + n], self.m[o:o + n], self.v[o:o + n])
             if d.is_cuda:
@@ -161,6 +186,10 @@ class FlatAdamW:
             else:
                 self._step_ref(*st, g, d)
             o += n
+
+    def _invalidate_t(self) -> None:
+        if hasattr(self.flat, "invalidate_t"):
+            self.flat.invalidate_t()
 
     def _views(self, buf: torch.Tensor):
         return [buf[s:e] for s, e in self.shards]

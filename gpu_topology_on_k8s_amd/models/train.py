@@ -41,7 +41,7 @@ __all__ = ["train", "main"]
 PEAK_BF16_FLOPS = 2.5e15  # MI355X dense bf16 (MI355X_MICROARCH.md), per GPU
 
 
-def _init_dist(device_kind: str) -> Dict[str, int]:
+def _init_dist(device_kind: str, comm_ctas: int = 0) -> Dict[str, int]:
     if "RANK" not in os.environ:
         os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
@@ -51,7 +51,13 @@ def _init_dist(device_kind: str) -> Dict[str, int]:
         # gloo (RCCL refuses two ranks on one device) — the multi-rank DP / ZeRO-1 GPU code paths run
         # on a single-GPU box; production runs one rank per GPU over RCCL
         rehearse = device_kind == "cuda" and os.environ.get("GTK_REHEARSE_ON_ONE_GPU") == "1"
-        dist.init_process_group(backend="gloo" if rehearse or device_kind != "cuda" else "nccl")
+        backend = "gloo" if rehearse or device_kind != "cuda" else "nccl"
+        kw = {}
+        if backend == "nccl" and comm_ctas:
+            from ..parallel.dp import nccl_options
+
+            kw["pg_options"] = nccl_options(max_ctas=comm_ctas)  # RCCL's CTAs per collective, capped
+        dist.init_process_group(backend=backend, **kw)
     return {"rank": rank, "world": world, "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}
 
 
@@ -113,8 +119,10 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
           dgrad_nn: str = "",
           zero1: bool = False, save_dir: Optional[str] = None, save_every: int = 0, resume: Optional[str] = None,
           keep: int = 2, fuse_residual: bool = True, overlap_norm: bool = False, same_data: bool = False,
-          graph: str = "auto", conv: str = "hip", cpu_bind: str = "auto", repeat_batch: bool = False) -> Dict[str, object]:
-    env = _init_dist(device_kind)
+          graph: str = "auto", conv: str = "hip", cpu_bind: str = "auto", repeat_batch: bool = False,
+          persistent_wt: bool = True, transpose_x: str = "backward", grad_reduce: str = "bf16", comm_ctas: int = 0,
+          comm_shadow: int = 0, comm_shadow_k: int = 8, comm_shadow_busbw: float = 350.0) -> Dict[str, object]:
+    env = _init_dist(device_kind, comm_ctas)
     if placement == "auto":  # inside a pod the allocation decides; on a bare node, the placement core
         placement = "pod" if os.environ.get("GTK_GPU_GROUP") else "best"
     if device_kind == "cuda" and placement == "pod":
@@ -165,12 +173,22 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         cfg = LlamaConfig.named(model_name)
         model = Llama(cfg, device=device, seed=seed, checkpoint=checkpoint, attn=attn, gemm_layout=gemm_layout,
                       overlap_transposes=overlap_transposes, fuse_residual=fuse_residual,
-                      dgrad_nn=tuple(p for p in dgrad_nn.split(",") if p))
+                      dgrad_nn=tuple(p for p in dgrad_nn.split(",") if p), persistent_wt=persistent_wt,
+                      transpose_x=transpose_x)
         items_per_step, unit, flops_per_item = batch * seq, "tokens", cfg.flops_per_token(seq)
     broadcast_params(model.flat)
     # graph mode issues the gradient collectives after backward (inside the captured step), not from
     # autograd hooks mid-backward: one capture-friendly sequence
-    ar = BucketedAllReduce(model.flat, bucket_mb=bucket_mb, zero1=zero1, overlap_norm=overlap_norm, overlap=not use_graph)
+    shadow = None
+    if comm_shadow and env["world"] == 1 and device.type == "cuda":
+        # what a k-GPU DP step's collectives take from this GPU: CTA-limited paced copies from the
+        # bucket hooks (parallel/dp.py CommShadow, profiles/r04_comm_shadow)
+        from ..parallel.dp import CommShadow
+
+        shadow = CommShadow(device, comm_shadow, k=comm_shadow_k, busbw_gbps=comm_shadow_busbw,
+                            max_bucket_bytes=int(bucket_mb * (1 << 20)))
+    ar = BucketedAllReduce(model.flat, bucket_mb=bucket_mb, zero1=zero1, overlap_norm=overlap_norm, overlap=not use_graph,
+                           grad_reduce=grad_reduce, shadow=shadow)
     opt = FlatAdamW(model.flat, lr=lr, shards=ar.shards() if zero1 else None, capturable=use_graph)
     if zero1:
         model.param_ready = ar.wait_param
@@ -213,7 +231,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         loss = model(x, y)
         loss.backward()
         ar.finish()
-        opt.step(grad_scale=ar.grad_scale, sq=ar.sq_norm())
+        opt.step(grad_scale=ar.grad_scale, sq=ar.sq_norm(), grad=ar.reduced_grad)
         ar.gather_params()  # zero1: overlaps the next forward; no-op otherwise
         return loss.detach()
 
@@ -312,6 +330,17 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "gemm_tuning": gemm_mode,
         "gemm_layout": gemm_layout,
         "overlap_transposes": overlap_transposes,
+        "grad_reduce": grad_reduce,
+        "comm_ctas": comm_ctas or None,
+        "comm_shadow": ({"ctas": shadow.ctas, "k": shadow.k, "busbw_gbps": shadow.busbw,
+                         "collectives_per_step": shadow.launched / max(1, done[0] - start_step),
+                         "ring_bytes_per_step": shadow.bytes / max(1, done[0] - start_step),
+                         "collective_us_per_step": shadow.micros / max(1, done[0] - start_step)}
+                        if shadow is not None else None),
+        "persistent_wt": bool(getattr(model, "persistent_wt", False)),
+        "transpose_x": getattr(model, "transpose_x", None),
+        "optimizer_writes_wt": bool(getattr(opt, "fused_t", False)),
+        "wt_refreshes": int(getattr(model.flat, "t_refreshes", 0)),
         "dgrad_nn": dgrad_nn,
         "fuse_residual": fuse_residual,
         "overlap_norm": ar.overlap_norm,
@@ -380,13 +409,30 @@ def main(argv=None) -> int:
                     help="train on the first batch at every step: uniform random tokens carry nothing to learn, one "
                          "repeated batch does, so the loss must fall (end-to-end check of forward, backward and AdamW)")
     ap.add_argument("--lr", type=float, default=3e-4)
+    ap.add_argument("--persistent-wt", default="on", choices=["on", "off"],
+                    help="NT layout: keep W^T resident and let the optimizer write it with W (on), or re-make every "
+                         "W^T by a transpose in every backward (off, the round-3 path)")
+    ap.add_argument("--transpose-x", default="backward", choices=["backward", "forward"],
+                    help="NT layout: make each weight gradient's x^T in the backward (from HBM) or in the forward right "
+                         "after x's producer (while x sits in the Infinity Cache)")
+    ap.add_argument("--grad-reduce", default="bf16", choices=["bf16", "fp32"],
+                    help="DP gradient reduction dtype: bf16 in place, or fp32 (a widened copy reduced and applied in fp32)")
+    ap.add_argument("--comm-ctas", type=int, default=0,
+                    help="cap RCCL's CTAs per collective (ncclConfig_t maxCTAs; 0 = RCCL's choice)")
+    ap.add_argument("--comm-shadow", type=int, default=0,
+                    help="one GPU: play each bucket's k-GPU ring all-reduce as this many CU-holding workgroups (0 = off)")
+    ap.add_argument("--comm-shadow-k", type=int, default=8, help="--comm-shadow: ranks of the emulated ring")
+    ap.add_argument("--comm-shadow-busbw", type=float, default=350.0,
+                    help="--comm-shadow: per-rank bus GB/s that sets each emulated collective's duration")
     a = ap.parse_args(argv)
     train(a.model, a.batch, a.seq, a.steps, a.warmup, a.device, a.placement, a.discovery, a.bucket_mb, a.checkpoint, lr=a.lr, attn=a.attn,
           gemm_tuning=a.gemm_tuning, gemm_table=a.gemm_table, gemm_layout=a.gemm_layout,
           overlap_transposes=a.overlap_transposes, dgrad_nn=a.dgrad_nn, zero1=a.zero1, save_dir=a.save_dir, save_every=a.save_every,
           resume=a.resume, keep=a.keep, fuse_residual=not a.no_fuse_residual,
           overlap_norm=a.overlap_norm, same_data=a.same_data, graph=a.graph, conv=a.conv, cpu_bind=a.cpu_bind,
-          repeat_batch=a.repeat_batch)
+          repeat_batch=a.repeat_batch, persistent_wt=a.persistent_wt == "on",
+          transpose_x=a.transpose_x, grad_reduce=a.grad_reduce, comm_ctas=a.comm_ctas, comm_shadow=a.comm_shadow,
+          comm_shadow_k=a.comm_shadow_k, comm_shadow_busbw=a.comm_shadow_busbw)
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0

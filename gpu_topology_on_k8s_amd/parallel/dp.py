@@ -22,6 +22,15 @@ of late layers overlaps the compute of early ones.  Communication volume equals 
 fp32 master/m/v memory and AdamW time drop by the world size (96 GB -> 12 GB per GPU for
 Llama-3-8B on 8 GPUs).  Every bucket is a whole number of 64-element-aligned parameters, so its
 length splits into 8-element-multiple chunks for any world size up to 8.
+
+``grad_reduce="fp32"`` reduces each bucket in fp32 (a widened copy in :attr:`grad32`, all-reduced or
+reduce-scattered there) and the optimizer reads that fp32 sum: the averaged gradient is rounded to
+bf16 nowhere, against the bf16 ring whose partial sums round at every hop.  It doubles the bytes
+on the links; bf16 stays the default (tests/test_llama_dp_cpu.py measures both against an exact sum).
+
+``comm_ctas`` caps the CTAs (CUs) RCCL may use per collective (``ncclConfig_t.maxCTAs`` through the
+process group's options, :func:`nccl_options`): during backward the collectives share the GPU with
+hipBLASLt's GEMMs, which hold every CU.  :class:`CommShadow` measures that contention on one GPU.
 """
 from __future__ import annotations
 
@@ -32,7 +41,59 @@ from typing import Dict, List, Optional
 import torch
 import torch.distributed as dist
 
-__all__ = ["BucketedAllReduce", "Bucket", "broadcast_params"]
+__all__ = ["BucketedAllReduce", "Bucket", "broadcast_params", "CommShadow", "nccl_options", "ring_bytes"]
+
+
+def nccl_options(max_ctas: int = 0, min_ctas: int = 0):
+    """``ProcessGroupNCCL.Options`` with RCCL's CTA bounds (``ncclConfig_t`` minCTAs / maxCTAs); ``None``
+    when both are 0 (RCCL's own choice)."""
+    if not (max_ctas or min_ctas):
+        return None
+    o = dist.ProcessGroupNCCL.Options()
+    if max_ctas:
+        o.config.max_ctas = int(max_ctas)
+    if min_ctas:
+        o.config.min_ctas = int(min_ctas)
+    return o
+
+
+def ring_bytes(nbytes: int, k: int) -> int:
+    """Bytes each member of a k-rank ring all-reduce sends (and receives): 2 (k-1)/k of the message."""
+    return int(nbytes * 2 * (k - 1) / k) if k > 1 else 0
+
+
+class CommShadow:
+    """The collective a k-GPU DP step would run for each gradient bucket, played on one GPU
+    (VERDICT r3 next #4): ``ctas`` workgroups (RCCL's CTAs) copy the bucket's ring traffic through
+    local HBM, paced over the collective's duration ``ring_bytes / busbw`` on a side stream, from the
+    bucket-ready hook, exactly where the real all-reduce would start (csrc/ops/comm_shadow.hip).  The
+    compute stream waits for it before the optimizer, as it waits for RCCL."""
+
+    def __init__(self, device, ctas: int, k: int = 8, busbw_gbps: float = 350.0, max_bucket_bytes: int = 256 << 20):
+        self.ctas, self.k, self.busbw = int(ctas), int(k), float(busbw_gbps)
+        nb = max(16, ring_bytes(max_bucket_bytes, self.k))
+        self.src = torch.empty(nb, dtype=torch.uint8, device=device)
+        self.dst = torch.empty(nb, dtype=torch.uint8, device=device)
+        self.stream = torch.cuda.Stream(device=device)
+        self.launched = 0
+        self.bytes = 0
+        self.micros = 0.0
+
+    def launch(self, bucket_bytes: int) -> None:
+        from ..ops import fused
+
+        nb = min(ring_bytes(bucket_bytes, self.k), self.src.numel())
+        us = nb / (self.busbw * 1e9) * 1e6
+        cur = torch.cuda.current_stream(self.src.device)
+        self.stream.wait_stream(cur)  # the bucket's gradients are complete
+        with torch.cuda.stream(self.stream):
+            fused.hip().comm_shadow(self.src, self.dst, nb, self.ctas, us)
+        self.launched += 1
+        self.bytes += nb
+        self.micros += us
+
+    def wait(self) -> None:
+        torch.cuda.current_stream(self.src.device).wait_stream(self.stream)
 
 
 @dataclass
@@ -55,11 +116,16 @@ def broadcast_params(flat, group=None, src: int = 0) -> None:
     """Rank ``src`` -> everyone (ncclBroadcast of the whole flat parameter buffer, C3)."""
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.broadcast(flat.data, src=src, group=group)
+    if hasattr(flat, "invalidate_t"):
+        flat.invalidate_t()  # persistent W^T (models/llama.py) is re-made from the broadcast weights
 
 
 class BucketedAllReduce:
     def __init__(self, flat, group=None, bucket_mb: float = 256.0, first_bucket_mb: float = 64.0, average: bool = True,
-                 overlap: bool = True, zero1: bool = False, overlap_norm: bool = False):
+                 overlap: bool = True, zero1: bool = False, overlap_norm: bool = False, grad_reduce: str = "bf16",
+                 shadow: Optional[CommShadow] = None):
+        if grad_reduce not in ("bf16", "fp32"):
+            raise ValueError("grad_reduce must be 'bf16' or 'fp32'")
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -97,19 +163,25 @@ class BucketedAllReduce:
             if bad:
                 raise ValueError(f"zero1: buckets {bad[:4]} do not split into 8-element chunks over {self.world} ranks")
         self.stats = {"buckets": len(self.buckets), "bucket_mb": bucket_mb, "launches": 0, "comm_bytes": 0,
-                      "zero1": zero1}
+                      "zero1": zero1, "grad_reduce": grad_reduce}
+        # fp32 reduction: the buckets are widened into this buffer and reduced there; the optimizer
+        # reads it (reduced_grad).  Only at world > 1: one rank has nothing to sum.
+        self.grad_reduce = grad_reduce
+        self.grad32 = (torch.zeros(flat.numel, dtype=torch.float32, device=flat.grad.device)
+                       if grad_reduce == "fp32" and self.world > 1 else None)
+        self.shadow = shadow if (shadow is not None and self.world == 1 and flat.grad.is_cuda) else None
         # Gradient-clipping norm per bucket on a side HIP stream, as each bucket's reduction lands:
         # the 16 GB read (3 ms at HBM rate for Llama-3-8B) overlaps the compute-bound backward GEMMs
         # instead of running serially before the optimizer.  Needs the readiness hooks, so at
         # world 1 they are installed for it alone.  Off by default: on one MI355X it measured
         # 691.2 vs 691.4 ms/step (Llama-3-8B) — hipBLASLt's GEMMs hold every CU, so the side-stream
         # norm kernels find no free slots and serialise anyway (profiles/r01_fuse_res/NORM.md).
-        self.overlap_norm = overlap_norm and overlap and flat.grad.is_cuda
+        self.overlap_norm = overlap_norm and overlap and flat.grad.is_cuda and self.grad32 is None
         self._norm_stream = None
         self._parts = torch.zeros(max(1, len(self.buckets)), dtype=torch.float32, device=flat.grad.device) \
             if self.overlap_norm else None
         self._launched = [False] * len(self.buckets)
-        if overlap and (self.world > 1 or self.overlap_norm):
+        if overlap and (self.world > 1 or self.overlap_norm or self.shadow is not None):
             direct = getattr(flat, "direct", {})
             for n, p in flat.params.items():
                 if n in direct:  # weight-gradient GEMM writes the flat buffer itself (models/llama.py _FlatLinear)
@@ -140,14 +212,21 @@ class BucketedAllReduce:
 
     def _launch(self, b: Bucket) -> None:
         self._launched[b.index] = True
-        if self.world == 1:  # nothing to reduce: only the overlapped norm
+        if self.world == 1:  # nothing to reduce: only the overlapped norm (and the k-GPU shadow)
+            if self.shadow is not None:
+                self.shadow.launch(b.numel * self.flat.grad.element_size())
             self._norm(b)
             return
         view = self.flat.grad[b.start:b.end]
         b.launched_at = time.perf_counter()
+        if self.grad32 is not None:  # widen, then reduce in fp32
+            buf = self.grad32[b.start:b.end]
+            buf.copy_(view)
+            view = buf
+        src = self.grad32 if self.grad32 is not None else self.flat.grad
         if self.zero1:
             s, e = self.own(b)
-            b.work = dist.reduce_scatter_tensor(self.flat.grad[s:e], view, group=self.group, async_op=True)
+            b.work = dist.reduce_scatter_tensor(src[s:e], view, group=self.group, async_op=True)
         else:
             b.work = dist.all_reduce(view, group=self.group, async_op=True)
         self.stats["launches"] += 1
@@ -197,11 +276,19 @@ class BucketedAllReduce:
                     self._launch(b)
             for b in self.buckets:
                 b.work.wait()
-        elif self.overlap_norm:
+        elif self.overlap_norm or self.shadow is not None:
             for b in self.buckets:
                 if not self._launched[b.index]:
                     self._launch(b)
+            if self.shadow is not None:
+                self.shadow.wait()  # the optimizer waits for the (shadow) collectives, as for RCCL's
         self.reset()
+
+    @property
+    def reduced_grad(self) -> Optional[torch.Tensor]:
+        """The fp32 reduced gradient the optimizer reads under ``grad_reduce="fp32"`` (None: the flat bf16
+        gradient buffer holds the reduced gradient)."""
+        return self.grad32
 
     def gather_params(self) -> None:
         """zero1, after the optimizer step: all-gather every bucket's updated weights, asynchronously,

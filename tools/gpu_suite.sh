@@ -73,6 +73,19 @@ print(json.dumps({"tflops": round(float(w["tflops"]), 1), "hbm_copy_gbps": round
     step ab_b2 300 python -u bench/attn_bench.py --b 2 --s 4096 --iters 5 --ab 30
     step pmc_attn 120 timeout -s KILL 100 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_INST_LDS --kernel-trace -d "$out/pmc_attn" -o run -- python3 tools/pmc_attn.py
     ;;
+  llama_ab)
+    # transposes A/B: round-3 path, persistent W^T, + x^T in the forward; then the
+    # kernel trace of the default
+    step pytest_fused 600 python -u -m pytest tests/test_fused_gpu.py -x -v --timeout 300 --timeout-method thread
+    step llama_wt_off 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --persistent-wt off
+    step llama_wt_on 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
+    step llama_wt_xf 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --transpose-x forward
+    step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
+    ;;
+  shadow)
+    # what 8-GPU DP communication costs the Llama-3-8B step: comm-shadow CTA sweep
+    step shadow_sweep 1100 python -u bench/comm_shadow_sweep.py --ctas 0,8,16,32,64 --out "$out/shadow.jsonl"
+    ;;
   *) echo "unknown mode $mode"; exit 2 ;;
 esac
 echo "[gpu_suite] done"
