@@ -36,6 +36,7 @@ Engine::Engine(const Problem& p, const Policy& pol) : p_(p), pol_(pol) {
     }
     lv.sorted_free = lv.free;
     std::sort(lv.sorted_free.begin(), lv.sorted_free.end(), std::greater<int>());
+
     lv_.push_back(std::move(lv));
   }
   if (!p_.nic.empty()) {
@@ -214,6 +215,19 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
   }
   std::vector<int> mg(lv_.size());
   for (size_t l = 0; l < lv_.size(); ++l) mg[l] = min_groups(lv_[l], k);
+  // suf[l][start * G + g]: free devices of group g (level l) at positions >= start of F
+  std::vector<std::vector<int>> suf(lv_.size());
+  size_t gmax = 1;
+  for (size_t l = 0; l < lv_.size(); ++l) {
+    const int G = (int)lv_[l].free.size();
+    gmax = std::max(gmax, (size_t)G);
+    suf[l].assign((size_t)(m + 1) * G, 0);
+    for (int a = m - 1; a >= 0; --a) {
+      for (int g = 0; g < G; ++g) suf[l][(size_t)a * G + g] = suf[l][(size_t)(a + 1) * G + g];
+      suf[l][(size_t)a * G + lv_[l].gid[F[a]]] += 1;
+    }
+  }
+  std::vector<int> ucap(gmax);
   const double pairs_k = k >= 2 ? 0.5 * k * (k - 1) : 1.0;
 
   // ---- exact symmetry breaking.  Free devices a and b are interchangeable when they sit in the same
@@ -338,6 +352,32 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
     std::vector<int> g;
     double gj = std::numeric_limits<double>::infinity();
     greedy(k, F, &g, &gj, false, &cls_of);
+    // packing seeds: whole groups first, fullest first -- within the fullest outer group first, or
+    // ignoring the outer levels.  Greedy growth from the cheapest pair can straddle groups on a
+    // partitioned node (a 40-XCP request ending up over 6 packages where 5 whole ones exist), and a
+    // poor incumbent leaves the bound nothing to cut.
+    for (int outer = 0; outer < 2 && !lv_.empty(); ++outer) {
+      std::vector<int> order = F;
+      const auto& in = lv_[0];
+      const Level* out = (outer && lv_.size() > 1) ? &lv_.back() : nullptr;
+      std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+        if (out) {
+          const int fa = out->free[out->gid[a]], fb = out->free[out->gid[b]];
+          if (fa != fb) return fa > fb;
+          if (out->gid[a] != out->gid[b]) return out->gid[a] < out->gid[b];
+        }
+        const int fa = in.free[in.gid[a]], fb = in.free[in.gid[b]];
+        if (fa != fb) return fa > fb;
+        return in.gid[a] < in.gid[b];
+      });
+      std::vector<int> cand(order.begin(), order.begin() + k);
+      std::sort(cand.begin(), cand.end());
+      const double cj = evaluate(cand, nullptr);
+      if (cj < gj - kEps) {
+        gj = cj;
+        g = cand;
+      }
+    }
     best_j = gj;
     for (int dev : g) best_pos.push_back((int)(std::lower_bound(F.begin(), F.end(), dev) - F.begin()));
   }
@@ -375,8 +415,32 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
         comm_lb = (pairsum + std::max(add, 0.0)) / pairs_k;
         bott_lb = std::max(pairmax, comm_lb);  // the costliest pair is at least the mean
       }
+      // span look-ahead: the r devices still to choose come from positions >= start; they fit into
+      // the touched groups' reachable free devices plus whole untouched groups, taken largest first,
+      // so a completion touches at least that many more groups.  This is what lets packing problems
+      // prune: on a CPX node (64 XCPs in 8 packages) a 24-XCP request that cannot avoid a fourth
+      // package is worse than any three-package incumbent, and is cut as soon as that is certain.
       double span_lb = 0;
-      for (size_t l = 0; l < lv_.size(); ++l) span_lb += std::max(0, touched[l] - mg[l]);
+      for (size_t l = 0; l < lv_.size(); ++l) {
+        const auto& lv = lv_[l];
+        const int G = (int)lv.free.size();
+        const int* reach = &suf[l][(size_t)start * G];  // free devices of each group at positions >= start
+        int spare = 0, nun = 0;
+        for (int g = 0; g < G; ++g) {
+          if (take[l][g] > 0) spare += reach[g];
+          else if (reach[g] > 0) ucap[nun++] = reach[g];
+        }
+        int extra = 0;
+        if (r > spare) {
+          std::sort(ucap.begin(), ucap.begin() + nun, std::greater<int>());
+          int need = r - spare;
+          for (int i = 0; i < nun && need > 0; ++i) {
+            need -= ucap[i];
+            ++extra;
+          }
+        }
+        span_lb += std::max(0, touched[l] + extra - mg[l]);
+      }
       double lb = (1.0 - wb) * comm_lb + wb * bott_lb + pol_.w_span * span_lb + pol_.w_access * ((accsum + r * amin) / k);
       if (collect_ties ? lb > best_j + kEps : lb >= best_j - kEps) return;
     }
