@@ -507,6 +507,57 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const u16* __restrict
   }
 }
 
+// Forward with a transposed copy of the output: hT [F, T] is the B operand of the w2 weight-gradient
+// GEMM in NT layout, written from the LDS tile here (Llama(transpose_x="forward")) instead of by a
+// transpose pass over the 2*T*F-byte output in the backward.  Same tiling and swizzle as
+// swiglu_bwd_t_kernel, same expression as swiglu_fwd_kernel (identical h bits).  T, F multiples of 64.
+__global__ __launch_bounds__(256) void swiglu_fwd_t_kernel(const u16* __restrict__ gu, u16* __restrict__ h,
+                                                           u16* __restrict__ hT, int T, int F) {
+  __shared__ u16x8 tile[64][8];
+  const int t = threadIdx.x;
+  const size_t r0 = (size_t)blockIdx.y * 64, c0 = (size_t)blockIdx.x * 64;
+  const size_t F2 = 2 * (size_t)F;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (t >> 3) + 32 * i, v = t & 7;
+    const size_t row = r0 + r;
+    const u16x8 g = *reinterpret_cast<const u16x8*>(gu + row * F2 + c0 + 8 * v);
+    const u16x8 u = *reinterpret_cast<const u16x8*>(gu + row * F2 + F + c0 + 8 * v);
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gf = bf2f(g[j]);
+      o[j] = f2bf(gf / (1.f + __expf(-gf)) * bf2f(u[j]));
+    }
+    *reinterpret_cast<u16x8*>(h + row * F + c0 + 8 * v) = o;
+    tile[r][v ^ ((r >> 3) & 7)] = o;
+  }
+  __syncthreads();
+  const u16* lds = reinterpret_cast<const u16*>(&tile[0][0]);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = t + 256 * i;
+    const int c = idx >> 3, p = idx & 7;
+    const int pv = (c >> 3) ^ p;
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = lds[(8 * p + j) * 64 + pv * 8 + (c & 7)];
+    *reinterpret_cast<u16x8*>(hT + (c0 + c) * T + r0 + 8 * p) = o;
+  }
+}
+
+std::vector<at::Tensor> swiglu_fwd_t(const at::Tensor& gu) {
+  CHECK_BF16(gu);
+  TORCH_CHECK(gu.dim() == 2, "swiglu_fwd_t: gu must be [T, 2F]");
+  const int64_t T = gu.size(0), F = gu.size(1) / 2;
+  TORCH_CHECK(T % 64 == 0 && F % 64 == 0 && T / 64 <= 65535, "swiglu_fwd_t: T and F must be multiples of 64");
+  auto h = at::empty({T, F}, gu.options());
+  auto hT = at::empty({F, T}, gu.options());
+  if (T && F) hipLaunchKernelGGL(swiglu_fwd_t_kernel, dim3((unsigned)(F / 64), (unsigned)(T / 64)), dim3(256), 0, cur_stream(), bp(gu),
+                           bpm(h), bpm(hT), (int)T, (int)F);
+  return {h, hT};
+}
+
 at::Tensor swiglu_fwd(const at::Tensor& gu) {
   CHECK_BF16(gu);
   const int64_t F2 = gu.size(-1);
@@ -975,6 +1026,7 @@ PYBIND11_MODULE(_fused, m) {
   m.def("rope_split_bwd", &rope_split_bwd);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("swiglu_fwd_t", &swiglu_fwd_t, "swiglu forward -> (h [T, F], h^T [F, T]); T, F multiples of 64");
   m.def("swiglu_bwd_t", &swiglu_bwd_t, "swiglu backward -> (dgu [T, 2F], dgu^T [2F, T]); T, F multiples of 64");
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd_inplace", &xent_bwd_inplace);

@@ -333,7 +333,8 @@ class _NTOperands:
     live through backward) -- the GEMMs hold every CU, so the side stream only contends."""
 
     def __init__(self, x: torch.Tensor, w: torch.Tensor, overlap: bool, dgrad_nn: bool = False,
-                 wt_fn: Optional[Callable[[], Optional[torch.Tensor]]] = None, eager_x: bool = False):
+                 wt_fn: Optional[Callable[[], Optional[torch.Tensor]]] = None, eager_x: bool = False,
+                 x_t: Optional[torch.Tensor] = None):
         self.event = None
         self.dgrad_nn = dgrad_nn  # dgrad reads W as is (NN): no W^T is made
         self.wt_fn = None if dgrad_nn else wt_fn  # the persistent W^T (FlatParams.weight_t): no per-step transpose
@@ -348,6 +349,9 @@ class _NTOperands:
             self.event = torch.cuda.Event()
             self.event.record(side)
             self.x, self.w = None, None
+        elif x_t is not None:  # its producer wrote x^T too (SwiGLU forward)
+            self.x_t, self.w_t = x_t, None
+            self.x, self.w = None, w
         elif eager_x and x.is_cuda:
             # x^T made in the forward, on the main stream, right after x's producer wrote it (still in
             # the Infinity Cache): the backward finds it ready, and x itself is not kept
@@ -388,10 +392,10 @@ class _FlatLinear(torch.autograd.Function):
     """``y = x W^T`` whose weight gradient is written in place into the flat buffer."""
 
     @staticmethod
-    def forward(ctx, x, w, flat, name, nt, overlap, dgrad_nn=False):
+    def forward(ctx, x, w, flat, name, nt, overlap, dgrad_nn=False, x_t=None):
         ctx.flat, ctx.name, ctx.nt, ctx.dgrad_nn = flat, name, nt, dgrad_nn
         if nt:
-            ctx.ops = _NTOperands(x, w, overlap, dgrad_nn, _wt_fn(flat, name), flat.eager_xt)
+            ctx.ops = _NTOperands(x, w, overlap, dgrad_nn, _wt_fn(flat, name), flat.eager_xt, x_t=x_t)
         else:
             ctx.save_for_backward(x, w)
         return F.linear(x, w)
@@ -412,7 +416,7 @@ class _FlatLinear(torch.autograd.Function):
             x, w = ctx.saved_tensors
             dx = dy.mm(w) if ctx.needs_input_grad[0] else None
             ctx.flat.write_grad(ctx.name, dy, x)
-        return dx, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None
 
 
 class _FlatLinearSwiGLU(torch.autograd.Function):
@@ -429,10 +433,19 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
             ctx.save_for_backward(gu)
         else:
             ctx.save_for_backward(gu, x, w)
-        return fused.hip().swiglu_fwd(gu) if gu.is_cuda else fused.swiglu_ref(gu)
+        a_t = None
+        if not gu.is_cuda:
+            a = fused.swiglu_ref(gu)
+        elif nt and flat.eager_xt and gu.size(0) % 64 == 0 and (gu.size(1) // 2) % 64 == 0:
+            # the next projection's x^T from the same kernel (transpose_x="forward")
+            a, a_t = fused.hip().swiglu_fwd_t(gu)
+            ctx.mark_non_differentiable(a_t)
+        else:
+            a = fused.hip().swiglu_fwd(gu)
+        return a, a_t
 
     @staticmethod
-    def backward(ctx, da):
+    def backward(ctx, da, _da_t=None):
         gu = ctx.saved_tensors[0]
         if ctx.nt:
             dgu, dgu_t = fused.swiglu_bwd_t(da, gu)
@@ -518,10 +531,10 @@ class Llama(torch.nn.Module):
             self.param_ready(name)
         return self.flat.params[name]
 
-    def _linear(self, x: torch.Tensor, name: str) -> torch.Tensor:
+    def _linear(self, x: torch.Tensor, name: str, x_t: Optional[torch.Tensor] = None) -> torch.Tensor:
         nt = self.gemm_layout == "nt"
         return _FlatLinear.apply(x, self.P(name).detach(), self.flat, name, nt, self.overlap_transposes,
-                                 name.rsplit(".", 1)[-1] in self.dgrad_nn)
+                                 name.rsplit(".", 1)[-1] in self.dgrad_nn, x_t)
 
     # ---------------------------------------------------------------- blocks
     def _attention(self, q, k, v):
@@ -558,9 +571,9 @@ class Llama(torch.nn.Module):
         q, k, v = fused.rope_split(qkv, self.rope_cos, self.rope_sin, B, S, H, Hkv, Dh)
         o = self._attention(q, k, v).reshape(B * S, H * Dh)  # [B, S, H, Dh] -> [B*S, H*Dh]
         x, h = self._norm(x, self._linear(o, f"l{i}.wo"), f"l{i}.ffn_norm")
-        a = _FlatLinearSwiGLU.apply(h, self.P(f"l{i}.w13").detach(), self.flat, f"l{i}.w13", self.gemm_layout == "nt",
-                                    self.overlap_transposes, "w13" in self.dgrad_nn)
-        return x, self._linear(a, f"l{i}.w2")
+        a, a_t = _FlatLinearSwiGLU.apply(h, self.P(f"l{i}.w13").detach(), self.flat, f"l{i}.w13", self.gemm_layout == "nt",
+                                         self.overlap_transposes, "w13" in self.dgrad_nn)
+        return x, self._linear(a, f"l{i}.w2", x_t=a_t)
 
     def forward(self, tokens: torch.Tensor, labels: Optional[torch.Tensor] = None) -> torch.Tensor:
         B, S = tokens.shape

@@ -241,6 +241,14 @@ def test_swiglu_bwd_t_matches_bwd_and_transpose(hip, T, F):
     assert dgu_t.shape == (2 * F, T) and torch.equal(dgu_t, dgu.t().contiguous())
 
 
+@pytest.mark.parametrize("T,F", [(64, 64), (256, 512), (16384 // 8, 14336 // 8)])
+def test_swiglu_fwd_t_matches_fwd_and_transpose(hip, T, F):
+    gu = torch.randn(T, 2 * F, device="cuda", dtype=torch.bfloat16)
+    h, ht = hip.swiglu_fwd_t(gu)
+    ref = hip.swiglu_fwd(gu)
+    assert torch.equal(h, ref) and torch.equal(ht, ref.t().contiguous())
+
+
 def test_transpose_wrapper_fallback_shapes():
     from gpu_topology_on_k8s_amd.ops import fused
 
