@@ -351,11 +351,11 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
   if (log_space > std::log(2.0e5)) {  // (with collect_ties the DFS re-finds the seed and lists it)
     std::vector<int> g;
     double gj = std::numeric_limits<double>::infinity();
-    greedy(k, F, &g, &gj, false, &cls_of);
     // packing seeds: whole groups first, fullest first -- within the fullest outer group first, or
     // ignoring the outer levels.  Greedy growth from the cheapest pair can straddle groups on a
     // partitioned node (a 40-XCP request ending up over 6 packages where 5 whole ones exist), and a
     // poor incumbent leaves the bound nothing to cut.
+    double seed_span = std::numeric_limits<double>::infinity();
     for (int outer = 0; outer < 2 && !lv_.empty(); ++outer) {
       std::vector<int> order = F;
       const auto& in = lv_[0];
@@ -372,10 +372,24 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
       });
       std::vector<int> cand(order.begin(), order.begin() + k);
       std::sort(cand.begin(), cand.end());
-      const double cj = evaluate(cand, nullptr);
+      Terms tm;
+      const double cj = evaluate(cand, &tm);
       if (cj < gj - kEps) {
         gj = cj;
         g = cand;
+        seed_span = tm.span;
+      }
+    }
+    // The greedy + 1-swap seed (O(k m) evaluations per pass) only when packing left groups
+    // straddled: a span-0 packing is already the kind of set the bound needs, and the search below
+    // proves or improves it either way.
+    if (!(seed_span <= 0.0)) {
+      std::vector<int> gg;
+      double ggj = std::numeric_limits<double>::infinity();
+      greedy(k, F, &gg, &ggj, false, &cls_of);
+      if (ggj < gj - kEps || g.empty()) {
+        gj = ggj;
+        g = gg;
       }
     }
     best_j = gj;
@@ -479,11 +493,11 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
   std::vector<int> ids;
   for (int pos : best_pos) ids.push_back(F[pos]);
   res.exact = !aborted;
-  if (aborted && best_pos.size() != (size_t)k) {
+  if (aborted) {  // the node budget ran out: the better of the search's best and greedy + 1-swap
     double gj = std::numeric_limits<double>::infinity();
     std::vector<int> g;
     greedy(k, F, &g, &gj, false, &cls_of);
-    ids = g;
+    if (best_pos.size() != (size_t)k || gj < evaluate(ids, nullptr) - kEps) ids = g;
   }
   res.ids = ids;
   res.objective = evaluate(ids, &res.terms);
