@@ -6,12 +6,11 @@
 // optimizer, which streams every weight anyway (master/m/v/grad in, master/m/v/W out), writes W^T in
 // the same pass: +2 B per element on top of its 28 B, and the backward finds W^T ready.
 //
-//   adamw_tiles_kernel   one 64 x 64 tile of one projection matrix per loop trip (grid-stride over
+//   adamw_tiles_kernel   one 64 x 256 tile of one projection matrix per loop trip (grid-stride over
 //                        every matrix's tiles: the persistent grid ends when the tile index passes the
-//                        total, so every wave exits).  Thread t updates 8 consecutive elements of rows
-//                        t/8 and t/8 + 32 (the transpose kernel's 64-tile load pattern), stages the new
-//                        bf16 row segments in an XOR-swizzled LDS tile and writes 8 consecutive rows of
-//                        one column of W^T per 16-B store (csrc/ops/transpose.hip: conflict-free).
+//                        total, so every wave exits).  The update walks 1 KiB row segments like the
+//                        flat kernel, stages the new bf16 rows in an XOR-swizzled LDS tile, and writes
+//                        8 consecutive rows of one column of W^T per 16-B store (conflict-free).
 //   adamw_ranges_kernel  the parameters that are not transposed (embedding, norms): blockIdx.y picks a
 //                        range, grid-stride over its 16-B vectors.
 // Both apply exactly adamw_body's arithmetic (csrc/ops/fused_ops.hip), in the same per-element order,
@@ -123,7 +122,11 @@ struct Mat {
   int64_t off, toff, R, C, tile_base;
 };
 
-constexpr int kT = 64;
+// Tile = 64 rows x 256 columns.  The fp32 master/m/v streams are read and written in 1 KiB
+// contiguous row segments (a wave covers two rows: 64 lanes x 8 elements x 4 B), the access shape of
+// the flat kernel; a 64 x 64 tile's 256-B segments ran the step at 5.45 TB/s against the flat
+// kernel's 5.97 (profiles/r04_llama).  W^T leaves as 256 output rows x 128 B.
+constexpr int kTR = 64, kTC = 256;
 
 template <bool DEV, typename G>
 __global__ __launch_bounds__(256) void adamw_tiles_kernel(float* __restrict__ master, float* __restrict__ m, float* __restrict__ v,
@@ -131,9 +134,11 @@ __global__ __launch_bounds__(256) void adamw_tiles_kernel(float* __restrict__ ma
                                                           const Mat* __restrict__ mats, int nmats, int64_t total_tiles,
                                                           const float* __restrict__ hp, const float* __restrict__ part, int nparts,
                                                           const float* __restrict__ tptr) {
-  __shared__ u16x8 tile[kT][8];
+  // [row][16-B vector]: vector v of row r at slot v ^ ((r >> 3) & 7) -- the XOR touches the low 3 bits
+  // only, so a row's 32 vectors stay a permutation of its own 512 B
+  __shared__ u16x8 tile[kTR][kTC / 8];
   const Hyper h = hyper<DEV>(hp, part, nparts, tptr);
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const u16* lds = reinterpret_cast<const u16*>(&tile[0][0]);
   for (int64_t ti = blockIdx.x; ti < total_tiles; ti += gridDim.x) {
     int lo = 0, hi = nmats - 1;  // last matrix whose tile_base <= ti (block-uniform)
@@ -143,23 +148,28 @@ __global__ __launch_bounds__(256) void adamw_tiles_kernel(float* __restrict__ ma
       else hi = mid - 1;
     }
     const Mat mt = mats[lo];
-    const int64_t local = ti - mt.tile_base, tiles_c = mt.C / kT;
-    const int64_t r0 = (local / tiles_c) * kT, c0 = (local % tiles_c) * kT;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = (t >> 3) + 32 * i, vv = t & 7;
+    const int64_t local = ti - mt.tile_base, tiles_c = mt.C / kTC;
+    const int64_t r0 = (local / tiles_c) * kTR, c0 = (local % tiles_c) * kTC;
+    // update: 8 passes of 8 rows; thread t takes vector t & 31 of row 8 * pass + t / 32
+#pragma unroll 4
+    for (int pass = 0; pass < kTR / 8; ++pass) {
+      const int r = 8 * pass + (t >> 5), vv = t & 31;
       const u16x8 wo = adam8(master, m, v, g, w, (size_t)(mt.off + (r0 + r) * mt.C + c0 + 8 * vv), h);
       tile[r][vv ^ ((r >> 3) & 7)] = wo;
     }
     __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int idx = t + 256 * i;
-      const int c = idx >> 3, p = idx & 7;
-      const int pv = (c >> 3) ^ p;  // ((r >> 3) & 7) == p for every r in 8p..8p+7
+    // transposed write: per instruction a wave takes one 16-B column vector vc (8 columns) x the 8
+    // row groups p, lanes (p, column & 7): the row groups sit on 8 different slots, the 8 columns in
+    // one slot's 4 dwords -- 32 banks, no conflicts; each output row gets 8 x 16 B = 128 B
+    const int p = lane >> 3, cl = lane & 7;
+#pragma unroll 4
+    for (int i = 0; i < kTC / 32; ++i) {
+      const int vc = 4 * i + wv;
+      const int c = 8 * vc + cl;
+      const int slot = vc ^ p;
       u16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = lds[(8 * p + j) * 64 + pv * 8 + (c & 7)];
+      for (int j = 0; j < 8; ++j) o[j] = lds[((8 * p + j) * (kTC / 8) + slot) * 8 + cl];
       *reinterpret_cast<u16x8*>(wt + mt.toff + (c0 + c) * mt.R + r0 + 8 * p) = o;
     }
     __syncthreads();  // the tile is free for the next trip

@@ -147,17 +147,18 @@ class FlatParams:
         self.t_valid: Dict[str, bool] = {}
         self._t_ver: Dict[str, int] = {}  # data._version when each W^T was last made valid
         self.t_refreshes = 0  # lazy W^T re-makes (transposes) since construction
+        self._plan = None  # adamw_plan() cache
         self.eager_xt = False  # NT layout: make x^T in the forward (Llama(transpose_x="forward"))
 
     # ---------------------------------------------------------------- persistent W^T
     def enable_transposed(self, names) -> List[str]:
         """Keep ``W^T`` of the listed 2-D parameters resident: the NT-layout input
         gradient reads it every backward, and W changes only in the optimizer, which writes W^T in the
-        same pass (``FlatAdamW`` + ``adamw_step_t``).  Matrices whose dims are not multiples of 64 (the
-        fused tile kernel's unit) are left out.  -> the names kept."""
+        same pass (``FlatAdamW`` + ``adamw_step_t``).  Matrices whose dims are not multiples of the fused
+        tile kernel's 64 x 256 tile are left out.  -> the names kept."""
         want = set(names)
         keep = [n for n in self.names if n in want and len(self.shapes[n]) == 2
-                and self.shapes[n][0] % 64 == 0 and self.shapes[n][1] % 64 == 0]
+                and self.shapes[n][0] % 64 == 0 and self.shapes[n][1] % 256 == 0]
         off = 0
         self.t_offsets = {}
         for n in keep:
@@ -204,7 +205,7 @@ class FlatParams:
 
     def adamw_plan(self):
         """Descriptors of ``adamw_step_t``: (mats int64 [N, 5] = (offset, W^T offset, R, C, first tile),
-        total 64x64 tiles, ranges int64 [M, 2] = the rest of the flat buffer as (start, length), longest
+        total 64x256 tiles, ranges int64 [M, 2] = the rest of the flat buffer as (start, length), longest
         range), on the buffer's device.  Cached."""
         if self._plan is None:
             mats, base, spans = [], 0, []
@@ -212,7 +213,7 @@ class FlatParams:
                 if n in self.t_offsets:
                     R, C = self.shapes[n]
                     mats.append((self.offsets[n], self.t_offsets[n], R, C, base))
-                    base += (R // 64) * (C // 64)
+                    base += (R // 64) * (C // 256)
                     spans.append((self.offsets[n], self.offsets[n] + R * C))
             ranges, cur = [], 0
             for a, b in sorted(spans):

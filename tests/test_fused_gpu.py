@@ -187,7 +187,13 @@ def test_adamw_and_sqnorm(hip, gdtype):
     hip.adamw_step(master, m, v, g, w, hp)
     assert torch.allclose(m, rm, atol=1e-6, rtol=1e-5) and torch.allclose(v, rv, atol=1e-7, rtol=1e-5)
     assert torch.allclose(master, rp, atol=1e-6, rtol=1e-5)
-    assert torch.equal(w, rp.to(torch.bfloat16))
+    # W is the kernel's own master rounded once; against torch's op-by-op reference it may differ by
+    # one bf16 ulp where an fp32 gradient's update lands next to a rounding boundary (FMA contraction)
+    assert torch.equal(w, master.to(torch.bfloat16))
+    if gdtype == torch.bfloat16:
+        assert torch.equal(w, rp.to(torch.bfloat16))
+    else:
+        assert (w.float() - rp.to(torch.bfloat16).float()).abs().max() <= 2 ** -7 * rp.abs().max()
     sq = hip.sq_norm(g)
     assert math.isclose(sq.item(), g.float().pow(2).sum().item(), rel_tol=1e-4)
 
@@ -349,7 +355,7 @@ def _adamw_t_case(seed=7):
     it out, plus its adamw_step_t plan."""
     from gpu_topology_on_k8s_amd.models.llama import FlatParams
 
-    shapes = [("a", (128,)), ("w1", (192, 256)), ("b", (64,)), ("w2", (64, 64)), ("w3", (256, 128))]
+    shapes = [("a", (128,)), ("w1", (192, 256)), ("b", (64,)), ("w2", (64, 512)), ("w3", (256, 768))]
     flat = FlatParams(shapes, "cuda")
     assert flat.enable_transposed(["w1", "w2", "w3"]) == ["w1", "w2", "w3"]
     torch.manual_seed(seed)
@@ -366,7 +372,7 @@ def test_adamw_step_t_matches_flat_kernel_and_writes_wt(hip, dev):
     W^T of every planned matrix; the ranges kernel covers the rest (VERDICT r3 next #3)."""
     flat, st = _adamw_t_case()
     mats, tiles, ranges, maxr = flat.adamw_plan()
-    assert tiles == 3 * 4 + 1 + 4 * 2 and ranges.shape[0] >= 2
+    assert tiles == 3 * 1 + 1 * 2 + 4 * 3 and ranges.shape[0] >= 2
     ref = {k: v.clone() for k, v in st.items()}
     got = {k: v.clone() for k, v in st.items()}
     wt = torch.full_like(flat.data_t, float("nan"))

@@ -73,6 +73,13 @@ print(json.dumps({"tflops": round(float(w["tflops"]), 1), "hbm_copy_gbps": round
     step ab_b2 300 python -u bench/attn_bench.py --b 2 --s 4096 --iters 5 --ab 30
     step pmc_attn 120 timeout -s KILL 100 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_INST_LDS --kernel-trace -d "$out/pmc_attn" -o run -- python3 tools/pmc_attn.py
     ;;
+  adamw_t)
+    # the AdamW-T tile kernel against the flat kernel: bitwise tests, then the step with and without W^T
+    step pytest_adamw 300 python -u -m pytest tests/test_fused_gpu.py -x -v --timeout 200 --timeout-method thread -k "adamw or persistent_wt or transpose"
+    step llama_wt_off 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --persistent-wt off
+    step llama_wt_on 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
+    step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
+    ;;
   llama_ab)
     # transposes A/B: round-3 path, persistent W^T, + x^T in the forward; then the
     # kernel trace of the default
