@@ -558,6 +558,69 @@ std::vector<at::Tensor> swiglu_fwd_t(const at::Tensor& gu) {
   return {h, hT};
 }
 
+// swiglu_bwd_t with 64-token x 128-feature tiles: 256-B row segments of dh / gate / up (the 64 x 64
+// tile reads 128-B segments and ran at 4.96 TB/s in the Llama step, profiles/r04_llama) and 128-B
+// segments of the transposed rows.  Lanes of one transposed-store instruction take one 16-B column
+// vector x 8 row groups (the swizzle puts the row groups on 8 slots): conflict-free.  Same arithmetic
+// as swiglu_bwd_kernel (bit-identical).  T multiple of 64, F multiple of 128.
+__global__ __launch_bounds__(256) void swiglu_bwd_t128_kernel(const u16* __restrict__ dh, const u16* __restrict__ gu,
+                                                              u16* __restrict__ dgu, u16* __restrict__ dguT, int T, int F) {
+  __shared__ u16x8 tile[2][64][16];  // [gate | up][token][feature vector, swizzled]
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const size_t r0 = (size_t)blockIdx.y * 64, c0 = (size_t)blockIdx.x * 128;
+  const size_t F2 = 2 * (size_t)F;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (t >> 4) + 16 * i, v = t & 15;
+    const size_t row = r0 + r;
+    const u16x8 g = *reinterpret_cast<const u16x8*>(gu + row * F2 + c0 + 8 * v);
+    const u16x8 u = *reinterpret_cast<const u16x8*>(gu + row * F2 + F + c0 + 8 * v);
+    const u16x8 d = *reinterpret_cast<const u16x8*>(dh + row * F + c0 + 8 * v);
+    u16x8 og, ou;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gf = bf2f(g[j]), uf = bf2f(u[j]), df = bf2f(d[j]);
+      const float sg = 1.f / (1.f + __expf(-gf));
+      const float silu = gf * sg;
+      ou[j] = f2bf(df * silu);
+      og[j] = f2bf(df * uf * sg * (1.f + gf * (1.f - sg)));
+    }
+    *reinterpret_cast<u16x8*>(dgu + row * F2 + c0 + 8 * v) = og;
+    *reinterpret_cast<u16x8*>(dgu + row * F2 + F + c0 + 8 * v) = ou;
+    tile[0][r][v ^ ((r >> 3) & 7)] = og;
+    tile[1][r][v ^ ((r >> 3) & 7)] = ou;
+  }
+  __syncthreads();
+  const int p = lane >> 3, cl = lane & 7;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const u16* lds = reinterpret_cast<const u16*>(&tile[h][0][0]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int vc = 4 * i + wv;
+      const int c = 8 * vc + cl;
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = lds[((8 * p + j) * 16 + (vc ^ p)) * 8 + cl];
+      *reinterpret_cast<u16x8*>(dguT + ((size_t)h * F + c0 + c) * T + r0 + 8 * p) = o;
+    }
+  }
+}
+
+std::vector<at::Tensor> swiglu_bwd_t128(const at::Tensor& dh, const at::Tensor& gu) {
+  CHECK_BF16(dh);
+  CHECK_BF16(gu);
+  TORCH_CHECK(gu.dim() == 2, "swiglu_bwd_t128: gu must be [T, 2F]");
+  const int64_t T = gu.size(0), F = gu.size(1) / 2;
+  TORCH_CHECK(dh.numel() == T * F, "swiglu_bwd_t128: shape mismatch");
+  TORCH_CHECK(T % 64 == 0 && F % 128 == 0 && T / 64 <= 65535, "swiglu_bwd_t128: T multiple of 64, F of 128");
+  auto dgu = at::empty_like(gu);
+  auto dguT = at::empty({2 * F, T}, gu.options());
+  if (T && F) hipLaunchKernelGGL(swiglu_bwd_t128_kernel, dim3((unsigned)(F / 128), (unsigned)(T / 64)), dim3(256), 0, cur_stream(),
+                           bp(dh), bp(gu), bpm(dgu), bpm(dguT), (int)T, (int)F);
+  return {dgu, dguT};
+}
+
 at::Tensor swiglu_fwd(const at::Tensor& gu) {
   CHECK_BF16(gu);
   const int64_t F2 = gu.size(-1);
@@ -1026,6 +1089,7 @@ PYBIND11_MODULE(_fused, m) {
   m.def("rope_split_bwd", &rope_split_bwd);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("swiglu_bwd_t128", &swiglu_bwd_t128, "swiglu_bwd_t with 64 x 128 tiles (bit-identical)");
   m.def("swiglu_fwd_t", &swiglu_fwd_t, "swiglu forward -> (h [T, F], h^T [F, T]); T, F multiples of 64");
   m.def("swiglu_bwd_t", &swiglu_bwd_t, "swiglu backward -> (dgu [T, 2F], dgu^T [2F, T]); T, F multiples of 64");
   m.def("xent_fwd", &xent_fwd);

@@ -255,6 +255,15 @@ def test_swiglu_fwd_t_matches_fwd_and_transpose(hip, T, F):
     assert torch.equal(h, ref) and torch.equal(ht, ref.t().contiguous())
 
 
+@pytest.mark.parametrize("T,F", [(64, 128), (256, 512), (16384 // 8, 14336 // 8)])
+def test_swiglu_bwd_t128_is_bit_identical(hip, T, F):
+    gu = torch.randn(T, 2 * F, device="cuda", dtype=torch.bfloat16)
+    dh = torch.randn(T, F, device="cuda", dtype=torch.bfloat16)
+    a, at = hip.swiglu_bwd_t(dh, gu)
+    b, bt = hip.swiglu_bwd_t128(dh, gu)
+    assert torch.equal(a, b) and torch.equal(at, bt)
+
+
 def test_transpose_wrapper_fallback_shapes():
     from gpu_topology_on_k8s_amd.ops import fused
 

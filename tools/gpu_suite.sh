@@ -75,7 +75,8 @@ print(json.dumps({"tflops": round(float(w["tflops"]), 1), "hbm_copy_gbps": round
     ;;
   adamw_t)
     # the AdamW-T tile kernel against the flat kernel: bitwise tests, then the step with and without W^T
-    step pytest_adamw 300 python -u -m pytest tests/test_fused_gpu.py -x -v --timeout 200 --timeout-method thread -k "adamw or persistent_wt or transpose"
+    step pytest_adamw 300 python -u -m pytest tests/test_fused_gpu.py -x -v --timeout 200 --timeout-method thread -k "adamw or persistent_wt or transpose or swiglu"
+    step swiglu_ab 120 python -u bench/swiglu_t_ab.py
     step llama_wt_off 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --persistent-wt off
     step llama_wt_on 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
     step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
