@@ -54,6 +54,8 @@ def main():
         line = {"ctas": n, "ms_per_step": round(ms, 2), "tokens_per_s": round(r["tokens_per_s"], 1),
                 "inflation": round(ms / base - 1, 4) if base else None,
                 "collective_ms_per_step": round(sh.get("collective_us_per_step", 0) / 1e3, 2),
+                "achieved_ms_per_step": round(sh.get("achieved_ms_per_step", 0), 2),
+                "exposed_ms_per_step": round(sh.get("exposed_ms_per_step", 0), 2),
                 "collectives_per_step": sh.get("collectives_per_step"), "ring_gb_per_step": round(sh.get("ring_bytes_per_step", 0) / 1e9, 2),
                 "k": a.k, "busbw_gbps": a.busbw, "model": a.model, "batch": a.batch, "seq": a.seq}
         print(json.dumps(line), flush=True)

@@ -33,7 +33,7 @@ from .mnist import EPOCH_IMAGES, MnistCNN, MnistConfig
 from .gemm_tuning import setup_gemm_tuning
 from .optim import FlatAdamW
 from .checkpoint import CheckpointWriter, load_checkpoint
-from ..parallel.dp import BucketedAllReduce, broadcast_params
+from ..parallel.dp import DEFAULT_COMM_CTAS, BucketedAllReduce, broadcast_params
 from ..topology.cpus import bind_workload
 
 __all__ = ["train", "main"]
@@ -120,7 +120,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
           zero1: bool = False, save_dir: Optional[str] = None, save_every: int = 0, resume: Optional[str] = None,
           keep: int = 2, fuse_residual: bool = True, overlap_norm: bool = False, same_data: bool = False,
           graph: str = "auto", conv: str = "hip", cpu_bind: str = "auto", repeat_batch: bool = False,
-          persistent_wt: bool = True, transpose_x: str = "backward", grad_reduce: str = "bf16", comm_ctas: int = 0,
+          persistent_wt: bool = True, transpose_x: str = "backward", grad_reduce: str = "bf16", comm_ctas: int = DEFAULT_COMM_CTAS,
           comm_shadow: int = 0, comm_shadow_k: int = 8, comm_shadow_busbw: float = 350.0) -> Dict[str, object]:
     env = _init_dist(device_kind, comm_ctas)
     if placement == "auto":  # inside a pod the allocation decides; on a bare node, the placement core
@@ -273,6 +273,8 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
     sync()
     dist.barrier()
     sync()
+    if shadow is not None:
+        shadow.reset_timing()
     t0 = time.perf_counter()
     for _ in range(steps):
         losses.append(step())
@@ -335,7 +337,8 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "comm_shadow": ({"ctas": shadow.ctas, "k": shadow.k, "busbw_gbps": shadow.busbw,
                          "collectives_per_step": shadow.launched / max(1, done[0] - start_step),
                          "ring_bytes_per_step": shadow.bytes / max(1, done[0] - start_step),
-                         "collective_us_per_step": shadow.micros / max(1, done[0] - start_step)}
+                         "collective_us_per_step": shadow.micros / max(1, done[0] - start_step),
+                         **shadow.timing()}
                         if shadow is not None else None),
         "persistent_wt": bool(getattr(model, "persistent_wt", False)),
         "transpose_x": getattr(model, "transpose_x", None),
@@ -417,8 +420,9 @@ def main(argv=None) -> int:
                          "after x's producer (while x sits in the Infinity Cache)")
     ap.add_argument("--grad-reduce", default="bf16", choices=["bf16", "fp32"],
                     help="DP gradient reduction dtype: bf16 in place, or fp32 (a widened copy reduced and applied in fp32)")
-    ap.add_argument("--comm-ctas", type=int, default=0,
-                    help="cap RCCL's CTAs per collective (ncclConfig_t maxCTAs; 0 = RCCL's choice)")
+    ap.add_argument("--comm-ctas", type=int, default=DEFAULT_COMM_CTAS,
+                    help="cap RCCL's CTAs per collective (ncclConfig_t maxCTAs; 0 = RCCL's choice); the default is "
+                         "the knee of the one-GPU comm-shadow sweep (profiles/r04_comm_shadow)")
     ap.add_argument("--comm-shadow", type=int, default=0,
                     help="one GPU: play each bucket's k-GPU ring all-reduce as this many CU-holding workgroups (0 = off)")
     ap.add_argument("--comm-shadow-k", type=int, default=8, help="--comm-shadow: ranks of the emulated ring")

@@ -30,18 +30,26 @@ on the links; bf16 stays the default (tests/test_llama_dp_cpu.py measures both a
 
 ``comm_ctas`` caps the CTAs (CUs) RCCL may use per collective (``ncclConfig_t.maxCTAs`` through the
 process group's options, :func:`nccl_options`): during backward the collectives share the GPU with
-hipBLASLt's GEMMs, which hold every CU.  :class:`CommShadow` measures that contention on one GPU.
+hipBLASLt's GEMMs, which hold every CU.  :class:`CommShadow` measures that contention on one GPU
+(profiles/r04_comm_shadow): a GEMM that shares even a few CUs with a collective runs at the pace
+of its slowest CU, so the step pays for *how long* any CU is shared, not for how many are.  Too few
+CTAs stretch each collective past its link-rate duration (16 CTAs: 3x, +14 % step time); too many
+share every CU (256: +7.7 %).  :data:`DEFAULT_COMM_CTAS` = 64 is the knee at 250-350 GB/s bus
+bandwidth for Llama-3-8B's 67 buckets per step (+4.4 % / +5.9 %).
 """
 from __future__ import annotations
 
 import time
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
 
-__all__ = ["BucketedAllReduce", "Bucket", "broadcast_params", "CommShadow", "nccl_options", "ring_bytes"]
+__all__ = ["BucketedAllReduce", "Bucket", "broadcast_params", "CommShadow", "DEFAULT_COMM_CTAS", "nccl_options", "ring_bytes"]
+
+# RCCL CTAs per DP collective (profiles/r04_comm_shadow/SUMMARY.md)
+DEFAULT_COMM_CTAS = 64
 
 
 def nccl_options(max_ctas: int = 0, min_ctas: int = 0):
@@ -78,6 +86,10 @@ class CommShadow:
         self.launched = 0
         self.bytes = 0
         self.micros = 0.0
+        # per step: the (start, end) events of every collective and the compute stream's event at the
+        # point where it starts waiting for them (timing(): achieved durations and the exposed tail)
+        self.steps: List[Tuple[object, List[Tuple[object, object]]]] = []
+        self._cur: List[Tuple[object, object]] = []
 
     def launch(self, bucket_bytes: int) -> None:
         from ..ops import fused
@@ -86,14 +98,42 @@ class CommShadow:
         us = nb / (self.busbw * 1e9) * 1e6
         cur = torch.cuda.current_stream(self.src.device)
         self.stream.wait_stream(cur)  # the bucket's gradients are complete
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         with torch.cuda.stream(self.stream):
+            ev0.record(self.stream)
             fused.hip().comm_shadow(self.src, self.dst, nb, self.ctas, us)
+            ev1.record(self.stream)
+        self._cur.append((ev0, ev1))
         self.launched += 1
         self.bytes += nb
         self.micros += us
 
     def wait(self) -> None:
-        torch.cuda.current_stream(self.src.device).wait_stream(self.stream)
+        cur = torch.cuda.current_stream(self.src.device)
+        ready = torch.cuda.Event(enable_timing=True)
+        ready.record(cur)
+        cur.wait_stream(self.stream)
+        if self._cur:
+            self.steps.append((ready, self._cur))
+            self._cur = []
+
+    def reset_timing(self) -> None:
+        self.steps, self._cur = [], []
+
+    def timing(self) -> Dict[str, float]:
+        """Per step, averaged over the steps since reset_timing(): the summed collective kernel time
+        (target: the sum of ring_bytes / busBW; more means N CTAs could not move the bytes in time)
+        and the exposed tail, from the compute stream reaching the optimizer to the last collective's
+        end (what overlap could not hide)."""
+        if not self.steps:
+            return {"achieved_ms_per_step": 0.0, "exposed_ms_per_step": 0.0, "steps_timed": 0}
+        torch.cuda.synchronize(self.src.device)
+        ach = exp = 0.0
+        for ready, evs in self.steps:
+            ach += sum(a.elapsed_time(b) for a, b in evs)
+            exp += max(0.0, ready.elapsed_time(evs[-1][1]))
+        n = len(self.steps)
+        return {"achieved_ms_per_step": ach / n, "exposed_ms_per_step": exp / n, "steps_timed": n}
 
 
 @dataclass

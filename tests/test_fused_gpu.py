@@ -461,3 +461,44 @@ def test_comm_shadow_holds_its_ctas_for_the_collective_duration(hip):
     copied = nb // 16 // 32 // 16 * 16 * 32 * 16  # whole vectors per workgroup and chunk
     assert torch.equal(dst[:copied], src[:copied]) and not dst[copied + 4096:].any()
     assert 2.0 <= ms < 4.0, ms
+
+
+def test_comm_shadow_timing_reports_achieved_and_exposed_time(hip):
+    """parallel/dp.py CommShadow.timing(): per step, the summed collective time (at least the paced
+    target) and the exposed tail when the compute stream waits right after the last launch."""
+    from gpu_topology_on_k8s_amd.parallel.dp import CommShadow
+
+    sh = CommShadow(torch.device("cuda", 0), ctas=64, k=8, busbw_gbps=350.0, max_bucket_bytes=16 << 20)
+    for _ in range(2):
+        sh.launch(16 << 20)
+        sh.launch(8 << 20)
+        sh.wait()
+    t = sh.timing()
+    target_ms = sh.micros / 2 / 1e3
+    assert t["steps_timed"] == 2
+    assert target_ms <= t["achieved_ms_per_step"] < target_ms * 1.5 + 0.2, (t, target_ms)
+    # nothing else ran: the whole second collective (at least) is exposed
+    assert t["exposed_ms_per_step"] >= 0.9 * ring_ms(8 << 20), t
+
+
+def ring_ms(nbytes, k=8, busbw=350.0):
+    return nbytes * 2 * (k - 1) / k / (busbw * 1e9) * 1e3
+
+
+def test_training_with_the_default_rccl_cta_cap_initialises_its_communicator():
+    """models/train.py passes --comm-ctas (default parallel/dp.py DEFAULT_COMM_CTAS) to RCCL as
+    ncclConfig_t maxCTAs through the process group's options; at world 1 the barrier and the timing
+    all-reduce still create the communicator, so the capped config is exercised on one GPU."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd.models.train", "--model", "tiny", "--batch", "2",
+                        "--seq", "128", "--steps", "2", "--warmup", "1", "--gemm-tuning", "off"],
+                       capture_output=True, text=True, timeout=300, cwd=repo, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert r["comm_ctas"] == 64 and r["n_gpus"] == 1
