@@ -180,7 +180,8 @@ __device__ __forceinline__ float xhalf_max(float x) {  // max(x[lane], x[lane ^ 
 
 __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
                                                            const u16* __restrict__ v, u16* __restrict__ o,
-                                                           float* __restrict__ lse2, int H, int Hkv, int S, float c) {
+                                                           float* __restrict__ lse2, int H, int Hkv, int S, float c,
+                                                           u16* __restrict__ ot = nullptr) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BK * D * 2];  // [buf][K image | V image]
   const int t = threadIdx.x, lane = t & 63, r = lane & 31, hh = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -301,6 +302,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict
   }
   const float inv = 1.f / l;
   u16* orow = o + (((size_t)b * S + myq) * (size_t)(H) + hq) * D;
+  // O^T [H*D, B*S] (ot != nullptr): the o-projection's x^T for its NT-layout weight gradient, written
+  // from an LDS image of the block's [128 d][128 q] tile (the loop's last dma_sync retired every LDS
+  // read, so the K/V ring is free) as 256-B row segments, instead of by a transpose pass in the
+  // backward.  Same bf16 values as O.  Row stride 136 elements (272 B) staggers the banks.
+  constexpr int kOtStride = 136;
+  u16* otl = reinterpret_cast<u16*>(smem);
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
@@ -309,8 +316,21 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict
 #pragma unroll
       for (int e = 0; e < 4; ++e) v4[e] = f2bf(oacc[dt][4 * g4 + e] * inv);
       *reinterpret_cast<u16x4*>(orow + 32 * dt + 8 * g4 + 4 * hh) = v4;
+      if (ot) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) otl[(32 * dt + 8 * g4 + 4 * hh + e) * kOtStride + w * 32 + r] = v4[e];
+      }
     }
   if (hh == 0) lse2[(size_t)(b * H + hq) * S + myq] = m + log2f(l);
+  if (ot) {
+    __syncthreads();
+    const int d = t >> 1, half = t & 1;
+    const size_t BS = (size_t)(gridDim.x / H) * S;
+    u16* dst = ot + ((size_t)hq * D + d) * BS + (size_t)b * S + (size_t)qb * BQ + 64 * half;
+    const u16* srcl = otl + d * kOtStride + 64 * half;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) reinterpret_cast<u16x8*>(dst)[j] = reinterpret_cast<const u16x8*>(srcl)[j];
+  }
 }
 
 // ---- forward with the tile's LDS images as __restrict__ parameters (the default since round 4).
@@ -1221,19 +1241,29 @@ void check_qkv(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
 }
 
 std::vector<at::Tensor> attn_fwd_variant(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale,
-                                         bool noalias) {
+                                         bool noalias, bool with_t = false) {
   check_qkv(q, k, v);
   const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
   auto o = at::empty({B, S, H, D}, q.options());
   auto lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
   const float c = (float)(scale * 1.4426950408889634);
-  if (noalias)
+  if (noalias) {
+    TORCH_CHECK(!with_t, "attention: O^T is written by the default (fwd2) kernel only");
     hipLaunchKernelGGL(attn_fwd2n_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bpm(o),
                        lse.data_ptr<float>(), H, Hkv, S, c);
-  else
-    hipLaunchKernelGGL(attn_fwd2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bpm(o),
-                       lse.data_ptr<float>(), H, Hkv, S, c);
+    return {o, lse};
+  }
+  at::Tensor ot;
+  if (with_t) ot = at::empty({(int64_t)H * D, (int64_t)B * S}, q.options());
+  hipLaunchKernelGGL(attn_fwd2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bpm(o),
+                     lse.data_ptr<float>(), H, Hkv, S, c, with_t ? bpm(ot) : nullptr);
+  if (with_t) return {o, lse, ot};
   return {o, lse};
+}
+
+// default forward that also writes O^T [H*D, B*S] (the o-projection's NT-layout x^T): {o, lse, ot}
+std::vector<at::Tensor> attn_fwd_t(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale) {
+  return attn_fwd_variant(q, k, v, scale, false, true);
 }
 
 // default forward: fwd2.  fwd2n (no mid-tile DMA wait) computes the same bits but measured 1.4-2 %

@@ -558,6 +558,56 @@ std::vector<at::Tensor> swiglu_fwd_t(const at::Tensor& gu) {
   return {h, hT};
 }
 
+// swiglu_fwd_t with 64-token x 128-feature tiles (the swiglu_bwd_t128 layout): 256-B row segments of
+// gate / up / h, 128-B segments of the transposed rows, conflict-free transposed LDS reads.  Same
+// expression as swiglu_fwd_kernel (identical h bits).  T multiple of 64, F multiple of 128.
+__global__ __launch_bounds__(256) void swiglu_fwd_t128_kernel(const u16* __restrict__ gu, u16* __restrict__ h,
+                                                              u16* __restrict__ hT, int T, int F) {
+  __shared__ u16x8 tile[64][16];  // [token][feature vector, swizzled]
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const size_t r0 = (size_t)blockIdx.y * 64, c0 = (size_t)blockIdx.x * 128;
+  const size_t F2 = 2 * (size_t)F;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (t >> 4) + 16 * i, v = t & 15;
+    const size_t row = r0 + r;
+    const u16x8 g = *reinterpret_cast<const u16x8*>(gu + row * F2 + c0 + 8 * v);
+    const u16x8 u = *reinterpret_cast<const u16x8*>(gu + row * F2 + F + c0 + 8 * v);
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gf = bf2f(g[j]);
+      o[j] = f2bf(gf / (1.f + __expf(-gf)) * bf2f(u[j]));
+    }
+    *reinterpret_cast<u16x8*>(h + row * F + c0 + 8 * v) = o;
+    tile[r][v ^ ((r >> 3) & 7)] = o;
+  }
+  __syncthreads();
+  const int p = lane >> 3, cl = lane & 7;
+  const u16* lds = reinterpret_cast<const u16*>(&tile[0][0]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int vc = 4 * i + wv;
+    const int c = 8 * vc + cl;
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = lds[((8 * p + j) * 16 + (vc ^ p)) * 8 + cl];
+    *reinterpret_cast<u16x8*>(hT + (c0 + c) * T + r0 + 8 * p) = o;
+  }
+}
+
+std::vector<at::Tensor> swiglu_fwd_t128(const at::Tensor& gu) {
+  CHECK_BF16(gu);
+  TORCH_CHECK(gu.dim() == 2, "swiglu_fwd_t128: gu must be [T, 2F]");
+  const int64_t T = gu.size(0), F = gu.size(1) / 2;
+  TORCH_CHECK(T % 64 == 0 && F % 128 == 0 && T / 64 <= 65535, "swiglu_fwd_t128: T multiple of 64, F of 128");
+  auto h = at::empty({T, F}, gu.options());
+  auto hT = at::empty({F, T}, gu.options());
+  if (T && F) hipLaunchKernelGGL(swiglu_fwd_t128_kernel, dim3((unsigned)(F / 128), (unsigned)(T / 64)), dim3(256), 0, cur_stream(),
+                           bp(gu), bpm(h), bpm(hT), (int)T, (int)F);
+  return {h, hT};
+}
+
 // swiglu_bwd_t with 64-token x 128-feature tiles: 256-B row segments of dh / gate / up (the 64 x 64
 // tile reads 128-B segments and ran at 4.96 TB/s in the Llama step, profiles/r04_llama) and 128-B
 // segments of the transposed rows.  Lanes of one transposed-store instruction take one 16-B column
@@ -730,6 +780,52 @@ __global__ __launch_bounds__(256) void xent_bwd_kernel(u16* __restrict__ logits,
   }
 }
 
+// xent_bwd with a transposed copy: dlogits^T [V, T] is the A operand of the lm_head weight-gradient
+// GEMM in NT layout, written from the LDS tile instead of by a transpose pass that re-reads the
+// 4.2 GB gradient (Llama-3-8B, T 16384).  One 256-thread block = 64 rows x 128 vocabulary columns:
+// 256-B row segments in, 128-B transposed segments out (the swiglu_bwd_t128 tile).  Same expression
+// as xent_bwd_kernel (bit-identical dlogits).  T multiple of 64, V multiple of 128.
+__global__ __launch_bounds__(256) void xent_bwd_t_kernel(u16* __restrict__ logits, u16* __restrict__ dlT,
+                                                         const int64_t* __restrict__ labels, const float* __restrict__ lse,
+                                                         const float* __restrict__ gscale, int T, int V, int64_t ignore_index) {
+  __shared__ u16x8 tile[64][16];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const size_t r0 = (size_t)blockIdx.y * 64, c0 = (size_t)blockIdx.x * 128;
+  const float g = gscale[0];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (t >> 4) + 16 * i, v = t & 15;
+    const size_t row = r0 + r;
+    const int64_t y = labels[row];
+    const bool ignored = (y == ignore_index || y < 0 || y >= V);
+    const float l = lse[row];
+    const float sc = ignored ? 0.f : g;
+    u16x8* src = reinterpret_cast<u16x8*>(logits + row * V + c0 + 8 * v);
+    const u16x8 x = *src;
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t col = (int64_t)c0 + 8 * v + j;
+      const float p = __expf(bf2f(x[j]) - l);
+      o[j] = f2bf((p - (col == y ? 1.f : 0.f)) * sc);
+    }
+    *src = o;
+    tile[r][v ^ ((r >> 3) & 7)] = o;
+  }
+  __syncthreads();
+  const int p = lane >> 3, cl = lane & 7;
+  const u16* lds = reinterpret_cast<const u16*>(&tile[0][0]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int vc = 4 * i + wv;
+    const int c = 8 * vc + cl;
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = lds[((8 * p + j) * 16 + (vc ^ p)) * 8 + cl];
+    *reinterpret_cast<u16x8*>(dlT + (c0 + c) * T + r0 + 8 * p) = o;
+  }
+}
+
 std::vector<at::Tensor> xent_fwd(const at::Tensor& logits, const at::Tensor& labels, int64_t ignore_index) {
   CHECK_BF16(logits);
   TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous(), "labels must be int64 GPU");
@@ -753,6 +849,25 @@ void xent_bwd_inplace(at::Tensor& logits, const at::Tensor& labels, const at::Te
   const int64_t T = logits.numel() / V;
   if (T) hipLaunchKernelGGL(xent_bwd_kernel, dim3((unsigned)T), dim3(256), 0, cur_stream(), bpm(logits), labels.data_ptr<int64_t>(),
                             lse.data_ptr<float>(), gscale.data_ptr<float>(), V, ignore_index);
+}
+
+// dlogits in place over the logits AND its transpose [V, T] (returned).  T multiple of 64, V of 128.
+at::Tensor xent_bwd_t(at::Tensor& logits, const at::Tensor& labels, const at::Tensor& lse, const at::Tensor& gscale,
+                      int64_t ignore_index) {
+  CHECK_BF16(logits);
+  CHECK_F32(lse);
+  CHECK_F32(gscale);
+  TORCH_CHECK(logits.dim() == 2, "xent_bwd_t: logits must be [T, V]");
+  TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous(), "labels must be int64 GPU");
+  const int64_t T = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(labels.numel() == T && lse.numel() == T, "xent_bwd_t: labels/lse must have T entries");
+  TORCH_CHECK(T % 64 == 0 && V % 128 == 0 && T / 64 <= 65535, "xent_bwd_t: T multiple of 64, V of 128");
+  auto dlT = at::empty({V, T}, logits.options());
+  if (T && V)
+    hipLaunchKernelGGL(xent_bwd_t_kernel, dim3((unsigned)(V / 128), (unsigned)(T / 64)), dim3(256), 0, cur_stream(), bpm(logits),
+                       bpm(dlT), labels.data_ptr<int64_t>(), lse.data_ptr<float>(), gscale.data_ptr<float>(), (int)T, (int)V,
+                       ignore_index);
+  return dlT;
 }
 
 // =============================================================================== optimizer
@@ -1045,6 +1160,7 @@ at::Tensor xent10_bwd(const at::Tensor& dlog, const at::Tensor& g, at::Tensor& g
 namespace gtk_attn {  // csrc/ops/attention.hip
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale);
 std::vector<at::Tensor> attn_fwd_noalias(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale);
+std::vector<at::Tensor> attn_fwd_t(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale);
 std::vector<at::Tensor> attn_bwd_dq_alias(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                           const at::Tensor& out, const at::Tensor& lse, double scale);
 std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
@@ -1074,6 +1190,7 @@ void adamw_step_t(at::Tensor& master, at::Tensor& m, at::Tensor& v, const at::Te
 
 PYBIND11_MODULE(_fused, m) {
   m.def("attn_fwd", &gtk_attn::attn_fwd, "causal GQA flash attention forward (bf16, D=128): -> (o [B,S,H,D], lse2 [B,H,S])");
+  m.def("attn_fwd_t", &gtk_attn::attn_fwd_t, "attn_fwd that also writes O^T [H*D, B*S]: -> (o, lse2, ot)");
   m.def("attn_bwd", &gtk_attn::attn_bwd, "flash attention backward: -> (dq, dk, dv)");
   m.def("attn_fwd_noalias", &gtk_attn::attn_fwd_noalias, "forward fwd2n (no mid-tile DMA wait; A/B reference, bit-identical to the default fwd2)");
   m.def("attn_bwd_dq_alias", &gtk_attn::attn_bwd_dq_alias, "default backward with the round-3 dQ dq2 (A/B reference, bit-identical)");
@@ -1090,10 +1207,12 @@ PYBIND11_MODULE(_fused, m) {
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("swiglu_bwd_t128", &swiglu_bwd_t128, "swiglu_bwd_t with 64 x 128 tiles (bit-identical)");
+  m.def("swiglu_fwd_t128", &swiglu_fwd_t128, "swiglu_fwd_t with 64 x 128 tiles; T multiple of 64, F of 128");
   m.def("swiglu_fwd_t", &swiglu_fwd_t, "swiglu forward -> (h [T, F], h^T [F, T]); T, F multiples of 64");
   m.def("swiglu_bwd_t", &swiglu_bwd_t, "swiglu backward -> (dgu [T, 2F], dgu^T [2F, T]); T, F multiples of 64");
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd_inplace", &xent_bwd_inplace);
+  m.def("xent_bwd_t", &xent_bwd_t, "xent_bwd_inplace that also returns dlogits^T [V, T]; T multiple of 64, V of 128");
   m.def("adamw_step", &adamw_step);
   m.def("sq_norm", &sq_norm);
   m.def("sq_norm_parts", &sq_norm_parts, "sum-of-squares partials of a bf16 buffer; optionally advance a step counter");

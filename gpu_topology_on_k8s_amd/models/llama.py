@@ -149,6 +149,9 @@ class FlatParams:
         self.t_refreshes = 0  # lazy W^T re-makes (transposes) since construction
         self._plan = None  # adamw_plan() cache
         self.eager_xt = False  # NT layout: make x^T in the forward (Llama(transpose_x="forward"))
+        # NT layout: producers that hold a tile in LDS write the transposed copy too (SwiGLU h^T,
+        # cross-entropy dlogits^T; Llama(transpose_x="fused"/"forward"))
+        self.producer_xt = False
 
     # ---------------------------------------------------------------- persistent W^T
     def enable_transposed(self, names) -> List[str]:
@@ -412,7 +415,8 @@ class _FlatLinear(torch.autograd.Function):
                 dx = dy.mm(w_t)  # w_t is W here: dy W (NN)
             else:
                 dx = F.linear(dy, w_t)  # dy (W^T)^T
-            ctx.flat.write_grad(ctx.name, dy, None, nt=True, x_t=x_t)
+            # dy^T written by dy's producer kernel (cross-entropy backward for lm_head), if any
+            ctx.flat.write_grad(ctx.name, dy, None, nt=True, x_t=x_t, dy_t=fused.take_t(dy))
         else:
             x, w = ctx.saved_tensors
             dx = dy.mm(w) if ctx.needs_input_grad[0] else None
@@ -427,6 +431,7 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, flat, name, nt, overlap, dgrad_nn=False):
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for a^T (non-differentiable) in backward
         gu = F.linear(x, w)
         ctx.flat, ctx.name, ctx.nt, ctx.dgrad_nn = flat, name, nt, dgrad_nn
         if nt:
@@ -437,9 +442,9 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
         a_t = None
         if not gu.is_cuda:
             a = fused.swiglu_ref(gu)
-        elif nt and flat.eager_xt and gu.size(0) % 64 == 0 and (gu.size(1) // 2) % 64 == 0:
-            # the next projection's x^T from the same kernel (transpose_x="forward")
-            a, a_t = fused.hip().swiglu_fwd_t(gu)
+        elif nt and flat.producer_xt and gu.size(0) % 64 == 0 and (gu.size(1) // 2) % 64 == 0:
+            # the next projection's x^T from the same kernel (transpose_x="fused" / "forward")
+            a, a_t = fused.swiglu_fwd_t(gu)
             ctx.mark_non_differentiable(a_t)
         else:
             a = fused.hip().swiglu_fwd(gu)
@@ -470,7 +475,7 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
 class Llama(torch.nn.Module):
     def __init__(self, cfg: LlamaConfig, device="cuda", seed: int = 0, checkpoint: bool = False, attn: str = "hip",
                  gemm_layout: str = "nt", overlap_transposes: bool = False, fuse_residual: bool = True,
-                 dgrad_nn: Tuple[str, ...] = (), persistent_wt: bool = True, transpose_x: str = "backward"):
+                 dgrad_nn: Tuple[str, ...] = (), persistent_wt: bool = True, transpose_x: str = "fused"):
         super().__init__()
         if gemm_layout not in ("nt", "native"):
             raise ValueError("gemm_layout must be 'nt' or 'native'")
@@ -497,10 +502,11 @@ class Llama(torch.nn.Module):
         self._init(seed)
         # NT layout: W^T of every projection stays resident and the optimizer rewrites it with W
         # (no per-step weight transposes); dgrad_nn projections read W itself
-        if transpose_x not in ("backward", "forward"):
-            raise ValueError("transpose_x must be 'backward' or 'forward'")
+        if transpose_x not in ("backward", "forward", "fused"):
+            raise ValueError("transpose_x must be 'backward', 'forward' or 'fused'")
         self.transpose_x = transpose_x
         self.flat.eager_xt = transpose_x == "forward" and gemm_layout == "nt"
+        self.flat.producer_xt = transpose_x in ("forward", "fused") and gemm_layout == "nt"
         self.persistent_wt = persistent_wt and gemm_layout == "nt"
         if self.persistent_wt:
             self.flat.enable_transposed([n for n in self.flat.direct
@@ -538,9 +544,12 @@ class Llama(torch.nn.Module):
                                  name.rsplit(".", 1)[-1] in self.dgrad_nn, x_t)
 
     # ---------------------------------------------------------------- blocks
-    def _attention(self, q, k, v):
-        """q [B,H,S,Dh], k/v [B,Hkv,S,Dh] -> [B,S,H,Dh] (token-major, what the o-projection reads)."""
+    def _attention(self, q, k, v, want_t: bool = False):
+        """q [B,H,S,Dh], k/v [B,Hkv,S,Dh] -> [B,S,H,Dh] (token-major, what the o-projection reads);
+        ``want_t``: ``(o, o^T [H*Dh, B*S])`` with the transposed copy written by the forward kernel."""
         if self.attn == "hip" and (not q.is_cuda or fused.flash_attention_supported(q, k)):
+            if want_t:
+                return fused.attention_t(q, k, v)
             return fused.attention(q, k, v)  # HIP MFMA flash attention (PyTorch reference on CPU)
         if self.attn in ("hip", "sdpa"):  # library SDPA: A/B baseline, or shapes the HIP kernel does not cover
             o = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=q.size(1) != k.size(1))
@@ -550,7 +559,8 @@ class Llama(torch.nn.Module):
                 k = k.repeat_interleave(rep, dim=1)
                 v = v.repeat_interleave(rep, dim=1)
             o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
-        return o.transpose(1, 2)
+        o = o.transpose(1, 2)
+        return (o, None) if want_t else o
 
     def _norm(self, x: torch.Tensor, r: Optional[torch.Tensor], name: str):
         """``(x + r, rmsnorm(x + r))`` — the residual add fused into the norm kernel; ``r=None``
@@ -570,14 +580,21 @@ class Llama(torch.nn.Module):
         x, h = self._norm(x, r, f"l{i}.attn_norm")
         qkv = self._linear(h, f"l{i}.wqkv")
         q, k, v = fused.rope_split(qkv, self.rope_cos, self.rope_sin, B, S, H, Hkv, Dh)
-        o = self._attention(q, k, v).reshape(B * S, H * Dh)  # [B, S, H, Dh] -> [B*S, H*Dh]
-        x, h = self._norm(x, self._linear(o, f"l{i}.wo"), f"l{i}.ffn_norm")
+        if self.flat.eager_xt:
+            # o^T from the attention kernel's epilogue: 46 us per layer against the 43 us transpose it
+            # replaces (profiles/r04_fused_t), so only the all-eager "forward" mode asks for it
+            o, o_t = self._attention(q, k, v, want_t=True)
+        else:
+            o, o_t = self._attention(q, k, v), None
+        o = o.reshape(B * S, H * Dh)  # [B, S, H, Dh] -> [B*S, H*Dh]
+        x, h = self._norm(x, self._linear(o, f"l{i}.wo", x_t=o_t), f"l{i}.ffn_norm")
         a, a_t = _FlatLinearSwiGLU.apply(h, self.P(f"l{i}.w13").detach(), self.flat, f"l{i}.w13", self.gemm_layout == "nt",
                                          self.overlap_transposes, "w13" in self.dgrad_nn)
         return x, self._linear(a, f"l{i}.w2", x_t=a_t)
 
     def forward(self, tokens: torch.Tensor, labels: Optional[torch.Tensor] = None) -> torch.Tensor:
         B, S = tokens.shape
+        fused.clear_t()  # transposed gradients a previous backward offered and nobody took
         x = F.embedding(tokens.reshape(-1), self.P("tok_emb"))  # [B*S, D]
         r = None
         for i in range(self.cfg.n_layers):
@@ -589,7 +606,7 @@ class Llama(torch.nn.Module):
         logits = self._linear(x, "lm_head")  # [B*S, V]
         if labels is None:
             return logits.view(B, S, -1)
-        return fused.cross_entropy(logits, labels.reshape(-1))
+        return fused.cross_entropy(logits, labels.reshape(-1), want_t=self.flat.producer_xt)
 
 
 def smoke_step(device: str = "cuda:0") -> float:

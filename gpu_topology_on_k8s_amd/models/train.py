@@ -120,7 +120,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
           zero1: bool = False, save_dir: Optional[str] = None, save_every: int = 0, resume: Optional[str] = None,
           keep: int = 2, fuse_residual: bool = True, overlap_norm: bool = False, same_data: bool = False,
           graph: str = "auto", conv: str = "hip", cpu_bind: str = "auto", repeat_batch: bool = False,
-          persistent_wt: bool = True, transpose_x: str = "backward", grad_reduce: str = "bf16", comm_ctas: int = DEFAULT_COMM_CTAS,
+          persistent_wt: bool = True, transpose_x: str = "fused", grad_reduce: str = "bf16", comm_ctas: int = DEFAULT_COMM_CTAS,
           comm_shadow: int = 0, comm_shadow_k: int = 8, comm_shadow_busbw: float = 350.0) -> Dict[str, object]:
     env = _init_dist(device_kind, comm_ctas)
     if placement == "auto":  # inside a pod the allocation decides; on a bare node, the placement core
@@ -415,9 +415,12 @@ def main(argv=None) -> int:
     ap.add_argument("--persistent-wt", default="on", choices=["on", "off"],
                     help="NT layout: keep W^T resident and let the optimizer write it with W (on), or re-make every "
                          "W^T by a transpose in every backward (off, the round-3 path)")
-    ap.add_argument("--transpose-x", default="backward", choices=["backward", "forward"],
-                    help="NT layout: make each weight gradient's x^T in the backward (from HBM) or in the forward right "
-                         "after x's producer (while x sits in the Infinity Cache)")
+    ap.add_argument("--transpose-x", default="fused", choices=["fused", "backward", "forward"],
+                    help="NT layout: where the weight gradients' transposed operands come from. fused: written by the "
+                         "producer kernels that hold the tile in LDS (SwiGLU h^T, cross-entropy dlogits^T), the "
+                         "rest transposed in the backward; backward: every one transposed in the backward "
+                         "(round 3); forward: fused, plus attention O^T from its kernel and every other x^T made "
+                         "right after its producer")
     ap.add_argument("--grad-reduce", default="bf16", choices=["bf16", "fp32"],
                     help="DP gradient reduction dtype: bf16 in place, or fp32 (a widened copy reduced and applied in fp32)")
     ap.add_argument("--comm-ctas", type=int, default=DEFAULT_COMM_CTAS,

@@ -6,7 +6,7 @@ oracle of ``tests/test_fused_gpu.py``).
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import Dict, Optional, Tuple
 
 import torch
 
@@ -15,7 +15,7 @@ from .._native import load
 __all__ = [
     "rmsnorm", "rmsnorm_ref", "rope_tables", "rope_split", "rope_split_ref", "swiglu", "swiglu_ref", "cross_entropy",
     "cross_entropy_ref", "hip", "attention", "attention_ref", "flash_attention_supported", "transpose", "swiglu_bwd_ref",
-    "swiglu_bwd_t",
+    "swiglu_bwd_t", "swiglu_fwd_t", "attention_t", "offer_t", "take_t", "clear_t",
 ]
 
 
@@ -30,6 +30,35 @@ def transpose(x: torch.Tensor) -> torch.Tensor:
     if x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and x.size(0) % 64 == 0 and x.size(1) % 64 == 0:
         return hip().transpose_bf16(x.contiguous())
     return x.t().contiguous()
+
+
+# ----------------------------------------------------------------- transposed gradients, handed on
+# A backward kernel that already holds a gradient tile in LDS can write the gradient's transpose too
+# (xent_bwd_t: dlogits^T), which the consumer's NT-layout weight-gradient GEMM needs.  Autograd passes
+# only the gradient itself between nodes, so the producer offers the transpose here, keyed by the
+# gradient's storage, shape and version, and the consuming linear layer takes it (models/llama.py
+# _FlatLinear).  The entry holds the gradient alive, so its address cannot be reused while the entry
+# exists; a gradient that autograd summed or copied on the way has another address and simply finds
+# nothing (the consumer transposes it itself).  Llama.forward clears leftovers.
+_PENDING_T: Dict[Tuple[int, Tuple[int, ...]], Tuple[torch.Tensor, torch.Tensor, int]] = {}
+
+
+def offer_t(g: torch.Tensor, g_t: torch.Tensor) -> None:
+    _PENDING_T[(g.data_ptr(), tuple(g.shape))] = (g, g_t, g._version)
+
+
+def take_t(g: torch.Tensor) -> Optional[torch.Tensor]:
+    """The transpose a producer offered for exactly this gradient (same storage, shape, version), or None."""
+    if not _PENDING_T:
+        return None
+    e = _PENDING_T.pop((g.data_ptr(), tuple(g.shape)), None)
+    if e is None or e[2] != g._version or e[0].stride() != g.stride():
+        return None
+    return e[1]
+
+
+def clear_t() -> None:
+    _PENDING_T.clear()
 
 
 # ------------------------------------------------------------------------------------ RMSNorm
@@ -176,6 +205,17 @@ def swiglu_bwd_t(dh: torch.Tensor, gu: torch.Tensor) -> Tuple[torch.Tensor, torc
     return dgu, transpose(dgu)
 
 
+def swiglu_fwd_t(gu: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """SwiGLU forward returning ``(h [T, F], h^T [F, T])`` (no autograd): the HIP kernel writes the
+    transposed copy from its LDS tile; elsewhere the reference plus a transpose."""
+    if gu.is_cuda and gu.dim() == 2 and gu.size(0) % 64 == 0 and (gu.size(1) // 2) % 128 == 0:
+        return tuple(hip().swiglu_fwd_t128(gu.contiguous()))
+    if gu.is_cuda and gu.dim() == 2 and gu.size(0) % 64 == 0 and (gu.size(1) // 2) % 64 == 0:
+        return tuple(hip().swiglu_fwd_t(gu.contiguous()))
+    h = hip().swiglu_fwd(gu.contiguous()) if gu.is_cuda else swiglu_ref(gu)
+    return h, transpose(h)
+
+
 class _SwiGLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, gu):
@@ -201,30 +241,38 @@ def cross_entropy_ref(logits: torch.Tensor, labels: torch.Tensor, ignore_index: 
 
 
 class _CrossEntropy(torch.autograd.Function):
-    """Mean token cross-entropy; backward overwrites the (no longer needed) bf16 logits with dlogits."""
+    """Mean token cross-entropy; backward overwrites the (no longer needed) bf16 logits with dlogits.
+    ``want_t``: the backward kernel also writes dlogits^T and offers it (:func:`offer_t`) to the lm_head
+    weight gradient (xent_bwd_t, T multiple of 64, V of 128)."""
 
     @staticmethod
-    def forward(ctx, logits, labels, ignore_index):
+    def forward(ctx, logits, labels, ignore_index, want_t=False):
         V = logits.size(-1)
         lg = logits.contiguous().view(-1, V)
         lb = labels.contiguous().view(-1)
         loss_rows, lse = hip().xent_fwd(lg, lb, int(ignore_index))
         nvalid = (lb != ignore_index).sum().clamp_min(1).float()
         ctx.lg, ctx.lb, ctx.lse, ctx.nvalid, ctx.ii, ctx.shape = lg, lb, lse, nvalid, int(ignore_index), logits.shape
+        ctx.want_t = bool(want_t) and lg.size(0) % 64 == 0 and V % 128 == 0 and lg.size(0) // 64 <= 65535
         return loss_rows.sum() / nvalid
 
     @staticmethod
     def backward(ctx, g):
         scale = (g.float() / ctx.nvalid).reshape(1).contiguous()
         lg = ctx.lg
-        hip().xent_bwd_inplace(lg, ctx.lb, ctx.lse, scale, ctx.ii)
         ctx.lg = None
-        return lg.view(ctx.shape), None, None
+        if ctx.want_t:
+            lg_t = hip().xent_bwd_t(lg, ctx.lb, ctx.lse, scale, ctx.ii)
+            out = lg.view(ctx.shape)
+            offer_t(out, lg_t)
+            return out, None, None, None
+        hip().xent_bwd_inplace(lg, ctx.lb, ctx.lse, scale, ctx.ii)
+        return lg.view(ctx.shape), None, None, None
 
 
-def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int = -100, want_t: bool = False) -> torch.Tensor:
     if logits.is_cuda:
-        return _CrossEntropy.apply(logits, labels, ignore_index)
+        return _CrossEntropy.apply(logits, labels, ignore_index, want_t)
     return cross_entropy_ref(logits, labels, ignore_index)
 
 
@@ -244,29 +292,48 @@ def attention_ref(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: floa
 
 class _FlashAttention(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, scale):
+    def forward(ctx, q, k, v, scale, with_t=False):
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for O^T (non-differentiable) in backward
         q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
-        o, lse = hip().attn_fwd(q, k, v, float(scale))
+        if with_t:  # the kernel also writes O^T [H*D, B*S] (the o-projection's NT-layout x^T)
+            o, lse, o_t = hip().attn_fwd_t(q, k, v, float(scale))
+            ctx.mark_non_differentiable(o_t)
+        else:
+            o, lse = hip().attn_fwd(q, k, v, float(scale))
+            o_t = None
         ctx.save_for_backward(q, k, v, o, lse)
         ctx.scale = float(scale)
-        return o
+        return o, o_t
 
     @staticmethod
-    def backward(ctx, do):
+    def backward(ctx, do, _do_t=None):
         q, k, v, o, lse = ctx.saved_tensors
         dq, dk, dv = hip().attn_bwd(do.contiguous(), q, k, v, o, lse, ctx.scale)
-        return dq, dk, dv, None
+        return dq, dk, dv, None, None
 
 
 def flash_attention_supported(q: torch.Tensor, k: torch.Tensor) -> bool:
     return q.is_cuda and q.dtype == torch.bfloat16 and q.size(-1) == 128 and q.size(2) % 128 == 0 and q.size(1) % k.size(1) == 0
 
 
-def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | None = None) -> torch.Tensor:
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | None = None):
     """Causal GQA attention -> [B, S, H, D]; the HIP flash kernel on GPU (head dim 128, S % 128 == 0)."""
     sc = scale if scale is not None else q.size(-1) ** -0.5
     if q.is_cuda:
         if not flash_attention_supported(q, k):
             raise ValueError("HIP flash attention needs bf16, head dim 128 and S % 128 == 0")
-        return _FlashAttention.apply(q, k, v, sc)
+        return _FlashAttention.apply(q, k, v, sc, False)[0]
     return attention_ref(q, k, v, sc)
+
+
+def attention_t(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | None = None):
+    """``(o [B, S, H, D], o^T [H*D, B*S])``: on GPU the forward kernel writes the transposed copy from
+    its LDS tile (no gradient flows through it); elsewhere the reference plus a transpose."""
+    sc = scale if scale is not None else q.size(-1) ** -0.5
+    if q.is_cuda:
+        if not flash_attention_supported(q, k):
+            raise ValueError("HIP flash attention needs bf16, head dim 128 and S % 128 == 0")
+        return _FlashAttention.apply(q, k, v, sc, True)
+    o = attention_ref(q, k, v, sc)
+    B, S, H, D = o.shape
+    return o, o.detach().reshape(B * S, H * D).t().contiguous()

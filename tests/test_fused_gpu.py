@@ -502,3 +502,69 @@ def test_training_with_the_default_rccl_cta_cap_initialises_its_communicator():
     assert p.returncode == 0, p.stderr[-3000:]
     r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert r["comm_ctas"] == 64 and r["n_gpus"] == 1
+
+
+@pytest.mark.parametrize("T,F", [(64, 128), (256, 512), (16384 // 8, 14336 // 8)])
+def test_swiglu_fwd_t128_is_bit_identical(hip, T, F):
+    """64 x 128-tile forward-with-transpose: h equals swiglu_fwd's bits, h^T its transpose."""
+    gu = torch.randn(T, 2 * F, device="cuda", dtype=torch.bfloat16)
+    h, ht = hip.swiglu_fwd_t128(gu)
+    ref = hip.swiglu_fwd(gu)
+    assert torch.equal(h, ref) and torch.equal(ht, ref.t().contiguous())
+
+
+@pytest.mark.parametrize("T,V", [(64, 128), (256, 1024), (512, 128256)])
+def test_xent_bwd_t_matches_in_place_backward_and_its_transpose(hip, T, V):
+    """csrc/ops/fused_ops.hip xent_bwd_t: the same dlogits bits as xent_bwd_inplace (ignored rows
+    included) plus dlogits^T [V, T]."""
+    logits = (torch.randn(T, V, device="cuda") * 3).to(torch.bfloat16)
+    labels = torch.randint(0, V, (T,), device="cuda")
+    labels[::7] = -100
+    _, lse = hip.xent_fwd(logits, labels, -100)
+    scale = torch.tensor([0.37], device="cuda")
+    a = logits.clone()
+    hip.xent_bwd_inplace(a, labels, lse, scale, -100)
+    b = logits.clone()
+    bt = hip.xent_bwd_t(b, labels, lse, scale, -100)
+    assert torch.equal(a, b) and torch.equal(bt, a.t().contiguous())
+    assert not b[::7].any()
+
+
+@pytest.mark.parametrize("B,H,Hkv,S", [(1, 4, 2, 128), (2, 8, 2, 512)])
+def test_attention_forward_writes_o_transpose(hip, B, H, Hkv, S):
+    """attn_fwd_t: O and lse bit-identical to attn_fwd, and O^T [H*D, B*S] is O's exact transpose."""
+    q = torch.randn(B, H, S, 128, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
+    o, lse = hip.attn_fwd(q, k, v, 128 ** -0.5)
+    o2, lse2, ot = hip.attn_fwd_t(q, k, v, 128 ** -0.5)
+    assert torch.equal(o, o2) and torch.equal(lse, lse2)
+    assert torch.equal(ot, o.reshape(B * S, H * 128).t().contiguous())
+
+
+def test_llama_fused_transposes_are_bit_identical():
+    """transpose_x="fused" (SwiGLU h^T, attention O^T and dlogits^T written by their producers, the
+    dlogits^T handed to lm_head through ops/fused.py offer_t/take_t) and "forward" give the same
+    losses and gradients, bit for bit, as transposing every operand in the backward."""
+    from gpu_topology_on_k8s_amd.models import Llama, LlamaConfig
+    from gpu_topology_on_k8s_amd.ops import fused
+
+    cfg = LlamaConfig(dim=512, n_layers=2, n_heads=4, n_kv_heads=2, vocab=1024, ffn_dim=1024, max_seq=512)
+    tok = torch.randint(0, cfg.vocab, (2, 256), device="cuda")
+    out = {}
+    for mode in ("backward", "fused", "forward"):
+        m = Llama(cfg, device="cuda", seed=5, gemm_layout="nt", transpose_x=mode)
+        losses = []
+        for _ in range(2):
+            m.flat.zero_grad()
+            loss = m(tok, torch.roll(tok, -1, 1))
+            loss.backward()
+            losses.append(loss.item())
+            assert not fused._PENDING_T  # every offered transpose was taken
+            with torch.no_grad():
+                m.flat.data.add_(m.flat.grad, alpha=-1e-2)
+                m.flat.invalidate_t()
+        out[mode] = (losses, m.flat.grad.float().clone())
+    for mode in ("fused", "forward"):
+        assert out[mode][0] == out["backward"][0], mode
+        assert torch.equal(out[mode][1], out["backward"][1]), mode

@@ -383,3 +383,38 @@ def test_fp32_gradient_reduction_matches_the_exact_sum_four_ranks_gloo():
         assert res[r]["fp32"] < res[r]["bf16"], res[r]  # the bf16 ring rounds; fp32 does not
         assert res[r]["bf16"] < 2e-2, res[r]
         assert res[r]["fp32_dtype"] == "torch.float32"
+
+
+def test_transposed_gradient_hand_off_matches_only_the_same_tensor():
+    """ops/fused.py offer_t / take_t: a consumer gets the offered transpose only for the very gradient
+    it was offered for (storage, shape, strides and version), once; anything else falls back."""
+    from gpu_topology_on_k8s_amd.ops import fused
+
+    g = torch.randn(8, 4)
+    gt = g.t().contiguous()
+    fused.offer_t(g, gt)
+    assert fused.take_t(torch.randn(8, 4)) is None  # another tensor
+    assert fused.take_t(g) is gt
+    assert fused.take_t(g) is None  # taken once
+    fused.offer_t(g, gt)
+    g.add_(1.0)  # modified after the offer: the transpose is stale
+    assert fused.take_t(g) is None
+    fused.offer_t(g, gt)
+    assert fused.take_t(g.view(4, 8)) is None  # other shape
+    fused.clear_t()
+    assert not fused._PENDING_T
+
+
+def test_llama_transpose_modes_agree_on_cpu():
+    """transpose_x fused / forward / backward: the same CPU gradients (the CPU path transposes with
+    torch; the GPU kernels are checked bitwise in tests/test_fused_gpu.py)."""
+    from gpu_topology_on_k8s_amd.models import Llama, LlamaConfig
+
+    cfg = LlamaConfig.tiny()
+    tok = torch.randint(0, cfg.vocab, (2, 64))
+    grads = {}
+    for mode in ("backward", "fused", "forward"):
+        m = Llama(cfg, device="cpu", seed=3, gemm_layout="nt", transpose_x=mode)
+        m(tok, torch.roll(tok, -1, 1)).backward()
+        grads[mode] = m.flat.grad.clone()
+    assert torch.equal(grads["fused"], grads["backward"]) and torch.equal(grads["forward"], grads["backward"])

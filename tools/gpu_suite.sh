@@ -90,6 +90,16 @@ print(json.dumps({"tflops": round(float(w["tflops"]), 1), "hbm_copy_gbps": round
     step llama_wt_xf 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --transpose-x forward
     step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
     ;;
+  fused_t)
+    # producer-written transposes (SwiGLU h^T, attention O^T, dlogits^T): kernel tests, kernel A/B,
+    # step A/B against the all-in-backward path, kernel trace of the default
+    step pytest_fused 600 python -u -m pytest tests/test_fused_gpu.py -x -v --timeout 300 --timeout-method thread
+    step fused_t_ab 300 python -u bench/fused_t_ab.py
+    step llama_fused 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
+    step llama_bwd 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --transpose-x backward
+    step llama_fused2 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
+    step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
+    ;;
   shadow)
     # what 8-GPU DP communication costs the Llama-3-8B step: comm-shadow CTA sweep
     step shadow_sweep 1100 python -u bench/comm_shadow_sweep.py --ctas ${SHADOW_CTAS:-0,8,16,32,64} --busbw ${SHADOW_BUSBW:-350} --out "$out/shadow.jsonl"
