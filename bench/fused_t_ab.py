@@ -3,6 +3,7 @@
 (event-timed medians, interleaved):
   swiglu forward   T 16384, F 14336: swiglu_fwd (+ transpose) vs swiglu_fwd_t (64x64) vs swiglu_fwd_t128
   xent backward    T 16384, V 128256: xent_bwd_inplace (+ transpose) vs xent_bwd_t
+  RoPE backward    B 4, H 32, Hkv 8, S 4096: rope_split_bwd (+ transpose) vs rope_split_bwd_t
   attention fwd    B 4, H 32, Hkv 8, S 4096: attn_fwd (+ transpose of O) vs attn_fwd_t
 """
 import json
@@ -57,6 +58,16 @@ def main():
     del logits, work
     torch.cuda.empty_cache()
     B, H, Hkv, S = 4, 32, 8, 4096
+    cos, sin = fused.rope_tables(S, 128, device="cuda")
+    dq = torch.randn(B, H, S, 128, device="cuda", dtype=torch.bfloat16)
+    dk = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
+    dv = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
+    out["rope_bwd_ms"] = timed({
+        "bwd": lambda: hip.rope_split_bwd(dq, dk, dv, cos, sin, 0),
+        "bwd+transpose": lambda: hip.transpose_bf16(hip.rope_split_bwd(dq, dk, dv, cos, sin, 0)),
+        "bwd_t": lambda: hip.rope_split_bwd_t(dq, dk, dv, cos, sin, 0),
+    })
+    del dq, dk, dv
     q = torch.randn(B, H, S, 128, device="cuda", dtype=torch.bfloat16)
     k = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
     v = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)

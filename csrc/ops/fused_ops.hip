@@ -413,6 +413,98 @@ at::Tensor rope_split_bwd(const at::Tensor& dq, const at::Tensor& dk, const at::
   return dqkv;
 }
 
+// RoPE backward with a transposed copy: dqkv^T [(H+2Hkv)*128, B*S] is the A operand of the QKV
+// weight-gradient GEMM in NT layout, written from the LDS tile instead of by a transpose pass that
+// re-reads dqkv.  One 256-thread block = 64 tokens x one head (head dim 128): a thread takes 8
+// rotation pairs (lo = x[8v..8v+7], hi = x[64+8v..]) of one token, the tile is staged in LDS with the
+// swiglu_bwd_t128 swizzle and written as 128-B segments of the transposed rows.  Same expressions as
+// rope_split_kernel<true> (bit-identical dqkv).  S multiple of 64.
+__global__ __launch_bounds__(256) void rope_bwd_t_kernel(u16* __restrict__ dqkv, u16* __restrict__ dqkvT,
+                                                         const u16* __restrict__ q, const u16* __restrict__ k,
+                                                         const u16* __restrict__ v, const float* __restrict__ cosb,
+                                                         const float* __restrict__ sinb, int B, int S, int H, int Hkv,
+                                                         int pos_offset) {
+  constexpr int Dh = 128, half = 64;
+  __shared__ u16x8 tile[64][16];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int hh = blockIdx.x, heads = H + 2 * Hkv;
+  const size_t tok0 = (size_t)blockIdx.y * 64;  // never crosses a sequence (S % 64 == 0)
+  const int b = (int)(tok0 / S), s0 = (int)(tok0 % S);
+  const u16* src;
+  if (hh < H) src = q + (((size_t)b * H + hh) * S + s0) * Dh;
+  else if (hh < H + Hkv) src = k + (((size_t)b * Hkv + (hh - H)) * S + s0) * Dh;
+  else src = v + (((size_t)b * Hkv + (hh - H - Hkv)) * S + s0) * Dh;
+  const int vi = t & 7;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int r = (t >> 3) + 32 * pass;
+    const u16* fa = src + (size_t)r * Dh;
+    const int i0 = vi * 8;
+    const u16x8 lo = *reinterpret_cast<const u16x8*>(fa + i0);
+    const u16x8 hi = *reinterpret_cast<const u16x8*>(fa + half + i0);
+    u16x8 olo, ohi;
+    if (hh >= H + Hkv) {  // V: plain copy
+      olo = lo;
+      ohi = hi;
+    } else {
+      const int sp = s0 + r;
+      const float* cr = cosb + (size_t)(sp + pos_offset) * half + i0;
+      const float* sr = sinb + (size_t)(sp + pos_offset) * half + i0;
+      f32x4 c0 = *reinterpret_cast<const f32x4*>(cr), c1 = *reinterpret_cast<const f32x4*>(cr + 4);
+      f32x4 sn0 = *reinterpret_cast<const f32x4*>(sr), sn1 = *reinterpret_cast<const f32x4*>(sr + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float c = j < 4 ? c0[j] : c1[j - 4];
+        const float sn = (j < 4 ? sn0[j] : sn1[j - 4]) * -1.f;
+        const float a = bf2f(lo[j]), bb = bf2f(hi[j]);
+        olo[j] = f2bf(a * c - bb * sn);
+        ohi[j] = f2bf(bb * c + a * sn);
+      }
+    }
+    u16* ta = dqkv + (tok0 + r) * (size_t)heads * Dh + (size_t)hh * Dh;
+    *reinterpret_cast<u16x8*>(ta + i0) = olo;
+    *reinterpret_cast<u16x8*>(ta + half + i0) = ohi;
+    tile[r][vi ^ ((r >> 3) & 7)] = olo;
+    tile[r][(8 + vi) ^ ((r >> 3) & 7)] = ohi;
+  }
+  __syncthreads();
+  const size_t BS = (size_t)B * S;
+  const int p = lane >> 3, cl = lane & 7;
+  const u16* lds = reinterpret_cast<const u16*>(&tile[0][0]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int vc = 4 * i + wv;
+    const int c = 8 * vc + cl;
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = lds[((8 * p + j) * 16 + (vc ^ p)) * 8 + cl];
+    *reinterpret_cast<u16x8*>(dqkvT + ((size_t)hh * Dh + c) * BS + tok0 + 8 * p) = o;
+  }
+}
+
+// rope_split_bwd that also returns dqkv^T [(H+2Hkv)*Dh, B*S]; head dim 128, S multiple of 64
+std::vector<at::Tensor> rope_split_bwd_t(const at::Tensor& dq, const at::Tensor& dk, const at::Tensor& dv, const at::Tensor& cosb,
+                                         const at::Tensor& sinb, int64_t pos_offset) {
+  CHECK_BF16(dq);
+  CHECK_BF16(dk);
+  CHECK_BF16(dv);
+  CHECK_F32(cosb);
+  CHECK_F32(sinb);
+  const int64_t B = dq.size(0), H = dq.size(1), S = dq.size(2), Dh = dq.size(3), Hkv = dk.size(1);
+  TORCH_CHECK(Dh == 128 && S % 64 == 0, "rope_split_bwd_t: head dim 128 and S multiple of 64");
+  TORCH_CHECK(dk.sizes() == dv.sizes() && dk.size(0) == B && dk.size(2) == S && dk.size(3) == Dh, "rope_split_bwd_t: shapes");
+  TORCH_CHECK(cosb.size(-1) == Dh / 2 && cosb.size(0) >= S + pos_offset && sinb.sizes() == cosb.sizes(), "rope table shape");
+  TORCH_CHECK(B * S / 64 <= 65535, "rope_split_bwd_t: too many tokens for the grid");
+  const int64_t heads = H + 2 * Hkv;
+  auto dqkv = at::empty({B * S, heads * Dh}, dq.options());
+  auto dqkvT = at::empty({heads * Dh, B * S}, dq.options());
+  if (B * S)
+    hipLaunchKernelGGL(rope_bwd_t_kernel, dim3((unsigned)heads, (unsigned)(B * S / 64)), dim3(256), 0, cur_stream(), bpm(dqkv),
+                       bpm(dqkvT), bp(dq), bp(dk), bp(dv), cosb.data_ptr<float>(), sinb.data_ptr<float>(), (int)B, (int)S, (int)H,
+                       (int)Hkv, (int)pos_offset);
+  return {dqkv, dqkvT};
+}
+
 // =============================================================================== SwiGLU
 // gu: [T, 2F] = [gate | up]; h = silu(g) * u : [T, F]
 __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const u16* __restrict__ gu, u16* __restrict__ h, size_t T, int F) {
@@ -1211,6 +1303,7 @@ PYBIND11_MODULE(_fused, m) {
   m.def("swiglu_fwd_t", &swiglu_fwd_t, "swiglu forward -> (h [T, F], h^T [F, T]); T, F multiples of 64");
   m.def("swiglu_bwd_t", &swiglu_bwd_t, "swiglu backward -> (dgu [T, 2F], dgu^T [2F, T]); T, F multiples of 64");
   m.def("xent_fwd", &xent_fwd);
+  m.def("rope_split_bwd_t", &rope_split_bwd_t, "rope_split_bwd that also returns dqkv^T; head dim 128, S multiple of 64");
   m.def("xent_bwd_inplace", &xent_bwd_inplace);
   m.def("xent_bwd_t", &xent_bwd_t, "xent_bwd_inplace that also returns dlogits^T [V, T]; T multiple of 64, V of 128");
   m.def("adamw_step", &adamw_step);

@@ -150,7 +150,7 @@ class FlatParams:
         self._plan = None  # adamw_plan() cache
         self.eager_xt = False  # NT layout: make x^T in the forward (Llama(transpose_x="forward"))
         # NT layout: producers that hold a tile in LDS write the transposed copy too (SwiGLU h^T,
-        # cross-entropy dlogits^T; Llama(transpose_x="fused"/"forward"))
+        # RoPE-backward dqkv^T, cross-entropy dlogits^T; Llama(transpose_x="fused"/"forward"))
         self.producer_xt = False
 
     # ---------------------------------------------------------------- persistent W^T
@@ -475,7 +475,8 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
 class Llama(torch.nn.Module):
     def __init__(self, cfg: LlamaConfig, device="cuda", seed: int = 0, checkpoint: bool = False, attn: str = "hip",
                  gemm_layout: str = "nt", overlap_transposes: bool = False, fuse_residual: bool = True,
-                 dgrad_nn: Tuple[str, ...] = (), persistent_wt: bool = True, transpose_x: str = "fused"):
+                 dgrad_nn: Tuple[str, ...] = (), persistent_wt: bool = True, transpose_x: str = "fused",
+                 attn_ot: Optional[bool] = None):
         super().__init__()
         if gemm_layout not in ("nt", "native"):
             raise ValueError("gemm_layout must be 'nt' or 'native'")
@@ -507,6 +508,8 @@ class Llama(torch.nn.Module):
         self.transpose_x = transpose_x
         self.flat.eager_xt = transpose_x == "forward" and gemm_layout == "nt"
         self.flat.producer_xt = transpose_x in ("forward", "fused") and gemm_layout == "nt"
+        # attention O^T from the forward kernel's epilogue (default: with transpose_x="forward" only)
+        self.attn_ot = self.flat.eager_xt if attn_ot is None else bool(attn_ot) and self.flat.producer_xt
         self.persistent_wt = persistent_wt and gemm_layout == "nt"
         if self.persistent_wt:
             self.flat.enable_transposed([n for n in self.flat.direct
@@ -579,10 +582,10 @@ class Llama(torch.nn.Module):
         H, Hkv, Dh = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
         x, h = self._norm(x, r, f"l{i}.attn_norm")
         qkv = self._linear(h, f"l{i}.wqkv")
-        q, k, v = fused.rope_split(qkv, self.rope_cos, self.rope_sin, B, S, H, Hkv, Dh)
-        if self.flat.eager_xt:
+        q, k, v = fused.rope_split(qkv, self.rope_cos, self.rope_sin, B, S, H, Hkv, Dh, want_t=self.flat.producer_xt)
+        if self.attn_ot:
             # o^T from the attention kernel's epilogue: 46 us per layer against the 43 us transpose it
-            # replaces (profiles/r04_fused_t), so only the all-eager "forward" mode asks for it
+            # replaces (profiles/r04_fused_t), so only the all-eager "forward" mode asks for it by default
             o, o_t = self._attention(q, k, v, want_t=True)
         else:
             o, o_t = self._attention(q, k, v), None

@@ -157,24 +157,32 @@ def rope_split_ref(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, B: i
 
 class _RopeSplit(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, cos, sin, B, S, H, Hkv, Dh, pos_offset):
+    def forward(ctx, qkv, cos, sin, B, S, H, Hkv, Dh, pos_offset, want_t=False):
         q, k, v = hip().rope_split_fwd(qkv.contiguous(), cos, sin, B, S, H, Hkv, Dh, pos_offset)
         ctx.save_for_backward(cos, sin)
         ctx.meta = (pos_offset, qkv.shape)
+        # backward also writes dqkv^T for the QKV weight gradient (rope_split_bwd_t, offered via offer_t)
+        ctx.want_t = bool(want_t) and Dh == 128 and S % 64 == 0 and B * S // 64 <= 65535
         return q, k, v
 
     @staticmethod
     def backward(ctx, dq, dk, dv):
         cos, sin = ctx.saved_tensors
         pos_offset, shape = ctx.meta
+        if ctx.want_t:
+            dqkv, dqkv_t = hip().rope_split_bwd_t(dq.contiguous(), dk.contiguous(), dv.contiguous(), cos, sin, pos_offset)
+            out = dqkv.view(shape)
+            offer_t(out, dqkv_t)
+            return out, None, None, None, None, None, None, None, None, None
         dqkv = hip().rope_split_bwd(dq.contiguous(), dk.contiguous(), dv.contiguous(), cos, sin, pos_offset)
-        return dqkv.view(shape), None, None, None, None, None, None, None, None
+        return dqkv.view(shape), None, None, None, None, None, None, None, None, None
 
 
-def rope_split(qkv, cos, sin, B, S, H, Hkv, Dh, pos_offset: int = 0):
-    """Fused QKV split + RoPE: [B*S, (H+2Hkv)*Dh] -> q [B,H,S,Dh], k/v [B,Hkv,S,Dh]."""
+def rope_split(qkv, cos, sin, B, S, H, Hkv, Dh, pos_offset: int = 0, want_t: bool = False):
+    """Fused QKV split + RoPE: [B*S, (H+2Hkv)*Dh] -> q [B,H,S,Dh], k/v [B,Hkv,S,Dh].  ``want_t``: the
+    backward offers dqkv^T to the QKV projection's weight gradient (:func:`offer_t`)."""
     if qkv.is_cuda:
-        return _RopeSplit.apply(qkv, cos, sin, B, S, H, Hkv, Dh, pos_offset)
+        return _RopeSplit.apply(qkv, cos, sin, B, S, H, Hkv, Dh, pos_offset, want_t)
     return rope_split_ref(qkv, cos, sin, B, S, H, Hkv, Dh, pos_offset)
 
 

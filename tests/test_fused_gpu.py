@@ -552,8 +552,9 @@ def test_llama_fused_transposes_are_bit_identical():
     cfg = LlamaConfig(dim=512, n_layers=2, n_heads=4, n_kv_heads=2, vocab=1024, ffn_dim=1024, max_seq=512)
     tok = torch.randint(0, cfg.vocab, (2, 256), device="cuda")
     out = {}
-    for mode in ("backward", "fused", "forward"):
-        m = Llama(cfg, device="cuda", seed=5, gemm_layout="nt", transpose_x=mode)
+    for mode in ("backward", "fused", "fused+ot", "forward"):
+        m = Llama(cfg, device="cuda", seed=5, gemm_layout="nt", transpose_x=mode.split("+")[0],
+                  attn_ot=True if mode.endswith("+ot") else None)
         losses = []
         for _ in range(2):
             m.flat.zero_grad()
@@ -565,6 +566,20 @@ def test_llama_fused_transposes_are_bit_identical():
                 m.flat.data.add_(m.flat.grad, alpha=-1e-2)
                 m.flat.invalidate_t()
         out[mode] = (losses, m.flat.grad.float().clone())
-    for mode in ("fused", "forward"):
+    for mode in ("fused", "fused+ot", "forward"):
         assert out[mode][0] == out["backward"][0], mode
         assert torch.equal(out[mode][1], out["backward"][1]), mode
+
+
+@pytest.mark.parametrize("B,H,Hkv,S", [(1, 4, 2, 64), (2, 8, 2, 256), (4, 32, 8, 512)])
+def test_rope_bwd_t_is_bit_identical_and_transposed(hip, B, H, Hkv, S):
+    """rope_split_bwd_t: dqkv bit-identical to rope_split_bwd, dqkv^T its exact transpose."""
+    from gpu_topology_on_k8s_amd.ops import fused
+
+    cos, sin = fused.rope_tables(S + 8, 128, device="cuda")
+    dq = torch.randn(B, H, S, 128, device="cuda", dtype=torch.bfloat16)
+    dk = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
+    dv = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
+    ref = hip.rope_split_bwd(dq, dk, dv, cos, sin, 3)
+    got, got_t = hip.rope_split_bwd_t(dq, dk, dv, cos, sin, 3)
+    assert torch.equal(got, ref) and torch.equal(got_t, ref.t().contiguous())

@@ -97,6 +97,7 @@ print(json.dumps({"tflops": round(float(w["tflops"]), 1), "hbm_copy_gbps": round
     step fused_t_ab 300 python -u bench/fused_t_ab.py
     step llama_fused 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
     step llama_bwd 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --transpose-x backward
+    step llama_fused_ot 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --attn-ot on
     step llama_fused2 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
     step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
     ;;
