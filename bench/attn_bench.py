@@ -69,7 +69,7 @@ def main():
         t = timeit(lambda: hip.attn_bwd_v2(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
         res["hip_bwd_v2_ms"] = t * 1e3
     if a.ab:
-        variants = {n: getattr(hip, n) for n in ("attn_bwd", "attn_bwd_v6", "attn_bwd_dq_alias", "attn_bwd_v5t", "attn_bwd_v4",
+        variants = {n: getattr(hip, n) for n in ("attn_bwd", "attn_bwd_v5m0", "attn_bwd_dq_alias", "attn_bwd_v5t", "attn_bwd_v4",
                                                  "attn_bwd_v3")
                     if hasattr(hip, n)}
         times = {n: [] for n in variants}

@@ -827,7 +827,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv4_kernel(const u16* __res
 // were issued before its first MFMA; a wave has at most 15 LDS reads in flight (4-bit lgkmcnt), so
 // the MFMA pipe idled while the LDS drained ~40 of them (`s_waitcnt lgkmcnt(14)` after 56 reads in
 // the ISA).  Same MFMAs in the same order: bit-identical.
-template <bool kSFirst>
+// kMaskBranch: the causal mask runs only on the slices that need it (a wave-uniform branch around
+// it), instead of a compare + select per score on every slice.  Only the first KB/QT slices of each
+// q-head touch the block's diagonal (or lie wholly above a wave's keys): ~3 % of the slices at
+// S 4096, while the per-score select cost 16 x (v_cmp + v_cndmask) per slice on every slice of a
+// kernel whose single wave per SIMD is issue-bound (profiles/r04_dkdv6).  Masked scores still become
+// exactly 0 before dS, so the products are unchanged: bit-identical.
+template <bool kSFirst, bool kMaskBranch = true>
 __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv5_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
                                                                 const u16* __restrict__ v, const u16* __restrict__ dout,
                                                                 const float* __restrict__ lse2, const float* __restrict__ delta,
@@ -957,16 +963,31 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv5_kernel(const u16* __res
     }
     __builtin_amdgcn_sched_barrier(0);
     // (4) softmax / dS of this slice under the deferred dV/dK MFMAs of the previous one
+    if (kMaskBranch) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
+      for (int g = 0; g < 4; ++g)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int i = 4 * g + e;
-        float pv = fexp2(fmaf(sacc[i], c, -lq[g][e]));
-        pv = (mykey - crow(i, hh) > kill_from) ? 0.f : pv;
-        sacc[i] = pv;
-        dpacc[i] = pv * (dpacc[i] - dq[g][e]);
+        for (int e = 0; e < 4; ++e) sacc[4 * g + e] = fexp2(fmaf(sacc[4 * g + e], c, -lq[g][e]));
+      if (kill_from != (1 << 30)) {  // wave-uniform: a diagonal or dead slice
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[i] = (mykey - crow(i, hh) > kill_from) ? 0.f : sacc[i];
       }
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dpacc[4 * g + e] = sacc[4 * g + e] * (dpacc[4 * g + e] - dq[g][e]);
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g + e;
+          float pv = fexp2(fmaf(sacc[i], c, -lq[g][e]));
+          pv = (mykey - crow(i, hh) > kill_from) ? 0.f : pv;
+          sacc[i] = pv;
+          dpacc[i] = pv * (dpacc[i] - dq[g][e]);
+        }
+    }
     const Packs cur{pack8(sacc, 0), pack8(sacc, 8), pack8(dpacc, 0), pack8(dpacc, 8)};
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
@@ -1002,212 +1023,6 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv5_kernel(const u16* __res
       dkt[dt] = mfma(tr_frag(pbuf + SL_Q, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), prev.d1, dkt[dt]);
     }
   }
-  u16* dkrow = dk + ((size_t)(b * Hkv + hk) * S + mykey) * D;
-  u16* dvrow = dv + ((size_t)(b * Hkv + hk) * S + mykey) * D;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      u16x4 a4, b4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        a4[e] = f2bf(dkt[dt][4 * g4 + e] * scale);
-        b4[e] = f2bf(dvt[dt][4 * g4 + e]);
-      }
-      *reinterpret_cast<u16x4*>(dkrow + 32 * dt + 8 * g4 + 4 * hh) = a4;
-      *reinterpret_cast<u16x4*>(dvrow + 32 * dt + 8 * g4 + 4 * hh) = b4;
-    }
-}
-
-// dK/dV v6: v5<kSFirst=true> with a 4-slot slice ring, so that a slice's LDS-DMA gets a whole step
-// to land instead of half of one.  v5 issues slice idx+1 mid-step and waits for it (vmcnt(0)) at the
-// step's end; when Q / dO come from HBM rather than L2 that wait is exposed every step.  v6: step idx
-// reads slot idx (S, dP) and slot idx-1 (the deferred dV/dK products), issues slice idx+2 into slot
-// idx+2 (= idx-2, whose last reader was step idx-1, before the previous barrier) right after its
-// transposed reads, and ends with `s_waitcnt vmcnt(4) lgkmcnt(0); s_barrier` in one asm statement:
-// only the 4 Q/dO pieces just issued may stay in flight (every wave issues its 4-B lse/delta piece
-// first), and no workgroup-scope fence drains them (a __syncthreads() here lowered to vmcnt(0)).
-// The compiler still waits (vmcnt(0)) before the first transposed read of each step -- its LDS-DMA
-// alias tracking does not cover the ds_read_b64_tr_b16 intrinsic here -- which is where slice idx+2,
-// issued a step earlier, must have landed.  The four slots are __restrict__ parameters of one
-// inlined body, so the row reads (ds_read_b128) carry no such wait; the loop is unrolled by four so
-// every slot choice is static.  Same MFMAs in the same order per accumulator as v5: bit-identical.
-struct Dkdv6Args {
-  const u16 *q, *dout;
-  const float *lse2, *delta;
-  int H, S, G, hk, b, kb;
-  float c;
-};
-
-__device__ __forceinline__ void dkdv6_body(char* __restrict__ s0, char* __restrict__ s1, char* __restrict__ s2,
-                                           char* __restrict__ s3, const Dkdv6Args& a, const bf16x8 (&kf)[8],
-                                           const bf16x8 (&vf)[8], f32x16 (&dvt)[4], f32x16 (&dkt)[4]) {
-  const int t = threadIdx.x, lane = t & 63, r = lane & 31, hh = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int H = a.H, S = a.S, G = a.G, hk = a.hk, b = a.b, kb = a.kb;
-  const float c = a.c;
-  const int krow = w * 32 + r, mykey = kb * KB + krow, kmin = kb * KB + w * 32;
-  const int qt0 = (kb * KB) / QT, nqt = S / QT - qt0, nslice = G * nqt;
-  const uint32_t qbytes = (uint32_t)((size_t)H * S * D * 2), dbytes = (uint32_t)((size_t)S * H * D * 2);
-  const auto qrs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.q + (size_t)b * H * S * D), 0, qbytes, 0x00020000);
-  const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.dout + (size_t)b * S * H * D), 0, dbytes, 0x00020000);
-  // every wave issues one 4-B-per-lane piece first (waves 0/1: lse/delta; 2/3: lse again, unread), so
-  // the Q/dO pieces are the 4 newest vm operations of every wave
-  const auto lrs = __builtin_amdgcn_make_buffer_rsrc((void*)((w == 1 ? a.delta : a.lse2) + (size_t)b * H * S), 0,
-                                                     (uint32_t)((size_t)H * S * 4), 0x00020000);
-  uint32_t qv[2], dvo[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int R = 8 * w + 4 * i + (lane >> 4);
-    const uint32_t ch16 = 16 * ((lane & 15) ^ (((R & 3) << 2) | ((R >> 2) & 3)));
-    qv[i] = (uint32_t)(R * D * 2) + ch16;
-    dvo[i] = (uint32_t)(R * H * D * 2) + ch16;
-  }
-  auto sload = [&](int idx, char* buf) {
-    const int hq = hk * G + idx / nqt, qbase = (qt0 + idx % nqt) * QT;
-    const uint32_t qs = (uint32_t)(((size_t)hq * S + qbase) * D * 2), ds = (uint32_t)(((size_t)qbase * H + hq) * D * 2);
-    // waves 2/3 land their (unused) piece in the slot's padding after SL_DEL's 32 entries
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, (LDS_AS void*)(buf + (w == 0 ? SL_LSE : w == 1 ? SL_DEL : SL_DEL + 256)), 4,
-                                             4 * lane, (uint32_t)(((size_t)hq * S + qbase) * 4), 0, 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (LDS_AS void*)(buf + SL_Q + (8 * w + 4 * i) * 256), 16, qv[i], qs, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, (LDS_AS void*)(buf + SL_DO + (8 * w + 4 * i) * 256), 16, dvo[i], ds, 0, 0);
-    }
-  };
-  auto active = [&](int idx) {
-    const int j = idx % nqt;
-    return j >= KB / QT || (qt0 + j) * QT + QT - 1 >= kmin;
-  };
-  auto masked = [&](int idx) { return idx % nqt < KB / QT; };
-  struct Packs {
-    bf16x8 p0, p1, d0, d1;
-  };
-  Packs prev{};
-  {  // the first step's deferred products read slot 3: zeros, not stale LDS bits
-    u16x8* z = reinterpret_cast<u16x8*>(s3);
-    for (int i = t; i < SL_BYTES / 16; i += 256) z[i] = u16x8{};
-  }
-  sload(0, s0);
-  if (nslice > 1) sload(1, s1);
-  dma_sync();
-  auto step = [&](int idx, const char* buf, const char* pbuf, char* dbuf) {
-    bf16x8 ta[16], qa[8], da[8];
-    f32x4 lq[4], dq[4];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      qa[s] = lds_b128(buf + SL_Q, swz(r, 2 * s + hh));
-      da[s] = lds_b128(buf + SL_DO, swz(r, 2 * s + hh));
-    }
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      lq[g] = *reinterpret_cast<const f32x4*>(buf + SL_LSE + 4 * (8 * g + 4 * hh));
-      dq[g] = *reinterpret_cast<const f32x4*>(buf + SL_DEL + 4 * (8 * g + 4 * hh));
-    }
-    const int j = idx % nqt;
-    const int qbase = (qt0 + j) * QT;
-    const bool dead = !active(idx);
-    const int kill_from = dead ? -(1 << 30) : (masked(idx) ? qbase : 1 << 30);
-    f32x16 sacc = f32x16{}, dpacc = f32x16{};
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      sacc = mfma(qa[s], kf[s], sacc);
-      dpacc = mfma(da[s], vf[s], dpacc);
-    }
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      ta[4 * dt + 0] = tr_frag(pbuf + SL_DO, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt);
-      ta[4 * dt + 1] = tr_frag(pbuf + SL_DO, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt);
-      ta[4 * dt + 2] = tr_frag(pbuf + SL_Q, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt);
-      ta[4 * dt + 3] = tr_frag(pbuf + SL_Q, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt);
-    }
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (idx + 2 < nslice) sload(idx + 2, dbuf);  // slot idx-2: its last reader finished before the last barrier
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int i = 4 * g + e;
-        float pv = fexp2(fmaf(sacc[i], c, -lq[g][e]));
-        pv = (mykey - crow(i, hh) > kill_from) ? 0.f : pv;
-        sacc[i] = pv;
-        dpacc[i] = pv * (dpacc[i] - dq[g][e]);
-      }
-    const Packs cur{pack8(sacc, 0), pack8(sacc, 8), pack8(dpacc, 0), pack8(dpacc, 8)};
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      dvt[dt] = mfma(ta[4 * dt + 0], prev.p0, dvt[dt]);
-      dvt[dt] = mfma(ta[4 * dt + 1], prev.p1, dvt[dt]);
-      dkt[dt] = mfma(ta[4 * dt + 2], prev.d0, dkt[dt]);
-      dkt[dt] = mfma(ta[4 * dt + 3], prev.d1, dkt[dt]);
-    }
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    prev = cur;
-    // every wave's slice idx+1 has landed (slice idx+2's 4 Q/dO pieces may still fly) and every LDS
-    // read of this step has returned; then the barrier, with no fence that would drain the DMA
-    if (idx + 2 < nslice)
-      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  };
-  int idx = 0;
-  for (; idx + 4 <= nslice; idx += 4) {
-    step(idx, s0, s3, s2);
-    step(idx + 1, s1, s0, s3);
-    step(idx + 2, s2, s1, s0);
-    step(idx + 3, s3, s2, s1);
-  }
-  if (idx < nslice) step(idx, s0, s3, s2);
-  if (idx + 1 < nslice) step(idx + 1, s1, s0, s3);
-  if (idx + 2 < nslice) step(idx + 2, s2, s1, s0);
-  {  // the last slice's deferred dV/dK products
-    const int ls = (nslice - 1) & 3;
-    const char* pbuf = ls == 0 ? s0 : ls == 1 ? s1 : ls == 2 ? s2 : s3;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      dvt[dt] = mfma(tr_frag(pbuf + SL_DO, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), prev.p0, dvt[dt]);
-      dvt[dt] = mfma(tr_frag(pbuf + SL_DO, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), prev.p1, dvt[dt]);
-      dkt[dt] = mfma(tr_frag(pbuf + SL_Q, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), prev.d0, dkt[dt]);
-      dkt[dt] = mfma(tr_frag(pbuf + SL_Q, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), prev.d1, dkt[dt]);
-    }
-  }
-}
-
-constexpr int SL6_BYTES = SL_BYTES + 256;  // + the landing pad of waves 2/3's unused 4-B piece
-
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv6_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
-                                                                const u16* __restrict__ v, const u16* __restrict__ dout,
-                                                                const float* __restrict__ lse2, const float* __restrict__ delta,
-                                                                u16* __restrict__ dk, u16* __restrict__ dv, int H, int Hkv,
-                                                                int S, float c, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * SL6_BYTES];  // slice ring, 4 slots
-  const int t = threadIdx.x, lane = t & 63, r = lane & 31, hh = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int kb = blockIdx.y;
-  const int bk = xcd_head(blockIdx.x, gridDim.x), b = bk / Hkv, hk = bk % Hkv, G = H / Hkv;
-  const size_t kvoff = ((size_t)(b * Hkv + hk) * S + (size_t)kb * KB) * D;
-  const int krow = w * 32 + r, mykey = kb * KB + krow;
-  bf16x8 kf[8], vf[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    kf[s] = *reinterpret_cast<const bf16x8*>(k + kvoff + (size_t)krow * D + 16 * s + 8 * hh);
-    vf[s] = *reinterpret_cast<const bf16x8*>(v + kvoff + (size_t)krow * D + 16 * s + 8 * hh);
-  }
-  f32x16 dvt[4], dkt[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) dvt[dt] = dkt[dt] = f32x16{};
-  const Dkdv6Args args{q, dout, lse2, delta, H, S, G, hk, b, kb, c};
-  dkdv6_body(smem, smem + SL6_BYTES, smem + 2 * SL6_BYTES, smem + 3 * SL6_BYTES, args, kf, vf, dvt, dkt);
   u16* dkrow = dk + ((size_t)(b * Hkv + hk) * S + mykey) * D;
   u16* dvrow = dv + ((size_t)(b * Hkv + hk) * S + mykey) * D;
 #pragma unroll
@@ -1527,7 +1342,7 @@ std::vector<at::Tensor> attn_bwd_v4(const at::Tensor& dout, const at::Tensor& q,
 // default backward: delta, dK/dV v5 (software-pipelined slices, operands read ahead of the DMA), dQ v2
 std::vector<at::Tensor> attn_bwd_order(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                        const at::Tensor& out, const at::Tensor& lse, double scale, bool s_first,
-                                       bool dq_noalias = true) {
+                                       bool dq_noalias = true, bool mask_branch = true) {
   check_qkv(q, k, v);
   const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
   TORCH_CHECK(dout.is_contiguous() && out.is_contiguous() && dout.numel() == q.numel() && out.numel() == q.numel(),
@@ -1538,7 +1353,11 @@ std::vector<at::Tensor> attn_bwd_order(const at::Tensor& dout, const at::Tensor&
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
                      delta.data_ptr<float>(), B, H, S);
   const float c = (float)(scale * 1.4426950408889634);
-  if (s_first)
+  if (s_first && !mask_branch)
+    hipLaunchKernelGGL((attn_bwd_dkdv5_kernel<true, false>), dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k),
+                       bp(v), bp(dout), lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c,
+                       (float)scale);
+  else if (s_first)
     hipLaunchKernelGGL(attn_bwd_dkdv5_kernel<true>, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v),
                        bp(dout), lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
   else
@@ -1558,24 +1377,10 @@ std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, co
   return attn_bwd_order(dout, q, k, v, out, lse, scale, true);
 }
 
-// dK/dV v6 (4-slot ring, slices two ahead) + dQ dq2n: A/B candidate, bit-identical to the default
-std::vector<at::Tensor> attn_bwd_v6(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                    const at::Tensor& out, const at::Tensor& lse, double scale) {
-  check_qkv(q, k, v);
-  const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
-  TORCH_CHECK(dout.is_contiguous() && out.is_contiguous() && dout.numel() == q.numel() && out.numel() == q.numel(),
-              "attention bwd: dout/out must be contiguous [B, S, H, D]");
-  auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
-  auto dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
-  const int rows = B * S * H;
-  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
-                     delta.data_ptr<float>(), B, H, S);
-  const float c = (float)(scale * 1.4426950408889634);
-  hipLaunchKernelGGL(attn_bwd_dkdv6_kernel, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
-                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
-  hipLaunchKernelGGL(attn_bwd_dq2n_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
-                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
-  return {dq, dk, dv};
+// default backward with the per-score causal select on every slice (round 3 / early round 4): A/B reference, bit-identical
+std::vector<at::Tensor> attn_bwd_v5m0(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                      const at::Tensor& out, const at::Tensor& lse, double scale) {
+  return attn_bwd_order(dout, q, k, v, out, lse, scale, true, true, false);
 }
 
 // default order with the round-3 dQ (dq2: one-array images, mid-tile DMA wait): A/B reference, bit-identical.

@@ -1253,8 +1253,8 @@ namespace gtk_attn {  // csrc/ops/attention.hip
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale);
 std::vector<at::Tensor> attn_fwd_noalias(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale);
 std::vector<at::Tensor> attn_fwd_t(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale);
-std::vector<at::Tensor> attn_bwd_v6(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                    const at::Tensor& out, const at::Tensor& lse, double scale);
+std::vector<at::Tensor> attn_bwd_v5m0(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                      const at::Tensor& out, const at::Tensor& lse, double scale);
 std::vector<at::Tensor> attn_bwd_dq_alias(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                           const at::Tensor& out, const at::Tensor& lse, double scale);
 std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
@@ -1288,7 +1288,7 @@ PYBIND11_MODULE(_fused, m) {
   m.def("attn_bwd", &gtk_attn::attn_bwd, "flash attention backward: -> (dq, dk, dv)");
   m.def("attn_fwd_noalias", &gtk_attn::attn_fwd_noalias, "forward fwd2n (no mid-tile DMA wait; A/B reference, bit-identical to the default fwd2)");
   m.def("attn_bwd_dq_alias", &gtk_attn::attn_bwd_dq_alias, "default backward with the round-3 dQ dq2 (A/B reference, bit-identical)");
-  m.def("attn_bwd_v6", &gtk_attn::attn_bwd_v6, "dK/dV v6 (4-slot ring, slices two ahead) + dq2n: A/B candidate, bit-identical");
+  m.def("attn_bwd_v5m0", &gtk_attn::attn_bwd_v5m0, "default backward with the per-score causal select on every slice (A/B reference, bit-identical)");
   m.def("attn_bwd_v5t", &gtk_attn::attn_bwd_v5t, "v5 with the transposed reads issued first (A/B reference for the default order)");
   m.def("attn_bwd_v4", &gtk_attn::attn_bwd_v4, "v4 backward (dK/dV LDS operands read at their use; A/B reference for the default v5)");
   m.def("attn_bwd_v3", &gtk_attn::attn_bwd_v3, "v3 backward (dK/dV not pipelined across slices; A/B reference for v4)");

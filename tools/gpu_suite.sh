@@ -101,8 +101,8 @@ print(json.dumps({"tflops": round(float(w["tflops"]), 1), "hbm_copy_gbps": round
     step llama_fused2 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
     step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
     ;;
-  dkdv6)
-    # dK/dV v6 (4-slot ring, DMA a step ahead): bit-identity, interleaved A/B at B 4 and 2, counters
+  attn_ab)
+    # attention backward A/B (interleaved, B 4 and 2) with bit-identity tests and counters
     step pytest_attn 600 python -u -m pytest tests/test_attention_gpu.py -x -v --timeout 300 --timeout-method thread
     step ab_b4 300 python -u bench/attn_bench.py --b 4 --ab 30
     step ab_b2 300 python -u bench/attn_bench.py --b 2 --ab 30

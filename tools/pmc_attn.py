@@ -33,10 +33,6 @@ def main():
         for _ in range(3):
             o, lse = hip.attn_fwd_noalias(q, k, v, D ** -0.5)
             hip.attn_bwd_dq_alias(do, q, k, v, o, lse, D ** -0.5)
-    if hasattr(hip, "attn_bwd_v6"):  # dK/dV v6: the 4-slot ring
-        for _ in range(3):
-            o, lse = hip.attn_fwd(q, k, v, D ** -0.5)
-            hip.attn_bwd_v6(do, q, k, v, o, lse, D ** -0.5)
     torch.cuda.synchronize()
     print("pmc_attn done", flush=True)
 
