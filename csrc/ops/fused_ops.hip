@@ -271,10 +271,17 @@ void rmsnorm_bwd_launch(const at::Tensor& dy, const at::Tensor& x, const at::Ten
 }
 
 std::vector<at::Tensor> rmsnorm_bwd_impl(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, const at::Tensor& rstd,
-                                         const u16* dres);
+                                         const u16* dres, const at::Tensor* dw_out = nullptr);
 
 std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, const at::Tensor& rstd) {
   return rmsnorm_bwd_impl(dy, x, w, rstd, nullptr);
+}
+
+// the same, with dW written into `dw_out` (a contiguous bf16 view of D elements, e.g. the weight's
+// slot of the flat gradient buffer): no separate dW tensor for autograd to accumulate
+at::Tensor rmsnorm_bwd_into(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, const at::Tensor& rstd,
+                            const at::Tensor& dw_out) {
+  return rmsnorm_bwd_impl(dy, x, w, rstd, nullptr, &dw_out)[0];
 }
 
 // Backward of add_rmsnorm: dx = rmsnorm_bwd(dy) + dres, where dres is the gradient that reached h
@@ -286,8 +293,15 @@ std::vector<at::Tensor> add_rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& 
   return rmsnorm_bwd_impl(dy, h, w, rstd, bp(dres));
 }
 
+at::Tensor add_rmsnorm_bwd_into(const at::Tensor& dy, const at::Tensor& h, const at::Tensor& w, const at::Tensor& rstd,
+                                const at::Tensor& dres, const at::Tensor& dw_out) {
+  CHECK_BF16(dres);
+  TORCH_CHECK(dres.numel() == h.numel(), "add_rmsnorm_bwd_into: dres shape mismatch");
+  return rmsnorm_bwd_impl(dy, h, w, rstd, bp(dres), &dw_out)[0];
+}
+
 std::vector<at::Tensor> rmsnorm_bwd_impl(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, const at::Tensor& rstd,
-                                         const u16* dres) {
+                                         const u16* dres, const at::Tensor* dw_out) {
   CHECK_BF16(dy);
   CHECK_BF16(x);
   CHECK_BF16(w);
@@ -296,7 +310,14 @@ std::vector<at::Tensor> rmsnorm_bwd_impl(const at::Tensor& dy, const at::Tensor&
   const int M = (int)(x.numel() / D);
   TORCH_CHECK(dy.numel() == x.numel() && rstd.numel() == M, "rmsnorm_bwd: shape mismatch");
   auto dx = at::empty_like(x);
-  auto dw = at::empty({D}, w.options());
+  at::Tensor dw;
+  if (dw_out) {
+    CHECK_BF16(*dw_out);
+    TORCH_CHECK(dw_out->numel() == D, "rmsnorm_bwd: dw_out must hold D elements");
+    dw = *dw_out;
+  } else {
+    dw = at::empty({D}, w.options());
+  }
   // 1024 waves (4 per CU) fill the chip; each takes M/1024 rows so the dW partials stay at 16 MB.
   // 2048 waves measured slower for the fused (ACC) variant at [16384, 4096]: 160.4 vs 143.5 us
   // (bench/norm_bench.py; the plain variant went 197 -> 171 us incl. its separate add).
@@ -962,6 +983,52 @@ at::Tensor xent_bwd_t(at::Tensor& logits, const at::Tensor& labels, const at::Te
   return dlT;
 }
 
+// =============================================================================== embedding backward
+// dW_emb[tok] = sum of the dx rows of every position holding tok, written straight into the weight's
+// slot of the flat gradient buffer (rows no position holds are zeroed by the caller).  The positions
+// arrive sorted by token (stable: equal tokens in position order), so one wave per segment start sums
+// its segment in a fixed order in fp32 and rounds once: deterministic, no atomics.  Replaces torch's
+// embedding backward (sort + two kernels + a dense [V, D] gradient) and autograd's add of that
+// dense gradient into the flat buffer.
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restrict__ sorted, const int64_t* __restrict__ perm,
+                                                        const u16* __restrict__ dx, u16* __restrict__ out, int T, int D,
+                                                        int64_t V) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= T) return;
+  const int64_t tok = sorted[i];
+  if ((i > 0 && sorted[i - 1] == tok) || tok < 0 || tok >= V) return;
+  int end = i + 1;
+  while (end < T && sorted[end] == tok) ++end;
+  const int nvec = D >> 3;
+  for (int c = lane; c < nvec; c += 64) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = i; j < end; ++j) {
+      const u16x8 x = reinterpret_cast<const u16x8*>(dx + (size_t)perm[j] * D)[c];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += bf2f(x[e]);
+    }
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(acc[e]);
+    reinterpret_cast<u16x8*>(out + (size_t)tok * D)[c] = o;
+  }
+}
+
+// out: [V, D] bf16 (contiguous view), zeroed by the caller; sorted / perm: int64 [T]; dx: bf16 [T, D]
+void embed_bwd_into(const at::Tensor& sorted, const at::Tensor& perm, const at::Tensor& dx, at::Tensor& out) {
+  CHECK_BF16(dx);
+  CHECK_BF16(out);
+  TORCH_CHECK(sorted.is_cuda() && perm.is_cuda() && sorted.scalar_type() == at::kLong && perm.scalar_type() == at::kLong &&
+                  sorted.is_contiguous() && perm.is_contiguous(), "embed_bwd_into: sorted / perm must be contiguous int64 GPU tensors");
+  TORCH_CHECK(dx.dim() == 2 && out.dim() == 2 && dx.size(1) == out.size(1) && dx.size(1) % 8 == 0, "embed_bwd_into: shapes");
+  const int64_t T = dx.size(0);
+  TORCH_CHECK(sorted.numel() == T && perm.numel() == T && T < (int64_t(1) << 31), "embed_bwd_into: sorted / perm must have T entries");
+  if (T)
+    hipLaunchKernelGGL(embed_bwd_kernel, dim3((unsigned)((T + 3) / 4)), dim3(256), 0, cur_stream(), sorted.data_ptr<int64_t>(),
+                       perm.data_ptr<int64_t>(), bp(dx), bpm(out), (int)T, (int)dx.size(1), out.size(0));
+}
+
 // =============================================================================== optimizer
 // Flat-buffer AdamW (decoupled weight decay).  8 elements per thread per iteration: two 16-B loads
 // each of master/m/v, one 16-B load of the bf16 gradient; writes master/m/v and the bf16 weight.
@@ -1297,6 +1364,9 @@ PYBIND11_MODULE(_fused, m) {
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
   m.def("add_rmsnorm_fwd", &add_rmsnorm_fwd);
   m.def("add_rmsnorm_bwd", &add_rmsnorm_bwd);
+  m.def("embed_bwd_into", &embed_bwd_into, "embedding gradient rows summed per token (sorted positions) into a zeroed [V, D] bf16 view");
+  m.def("rmsnorm_bwd_into", &rmsnorm_bwd_into, "rmsnorm_bwd writing dW into a given bf16 view; returns dx");
+  m.def("add_rmsnorm_bwd_into", &add_rmsnorm_bwd_into, "add_rmsnorm_bwd writing dW into a given bf16 view; returns dx");
   m.def("rope_split_fwd", &rope_split_fwd);
   m.def("rope_split_bwd", &rope_split_bwd);
   m.def("swiglu_fwd", &swiglu_fwd);

@@ -472,11 +472,80 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
         return dx, None, None, None, None, None, None
 
 
+class _FlatRMSNorm(torch.autograd.Function):
+    """``rmsnorm(x) * w`` whose weight gradient the backward kernel writes straight into the weight's
+    slot of the flat gradient buffer (``rmsnorm_bwd_into``): no separate dW for autograd to add in,
+    and no zero-fill of that slot in ``zero_grad`` (the weight is a direct parameter)."""
+
+    @staticmethod
+    def forward(ctx, x, w, flat, name, eps):
+        x = x.contiguous()
+        y, rstd = fused.hip().rmsnorm_fwd(x, w, float(eps))
+        ctx.save_for_backward(x, w, rstd)
+        ctx.flat, ctx.name = flat, name
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, rstd = ctx.saved_tensors
+        dx = fused.hip().rmsnorm_bwd_into(dy.contiguous(), x, w, rstd, ctx.flat.params[ctx.name].grad)
+        ctx.flat.mark_written(ctx.name)
+        return dx, None, None, None, None
+
+
+class _FlatAddRMSNorm(torch.autograd.Function):
+    """``h = x + r; y = rmsnorm(h) * w`` (ops/fused.py ``add_rmsnorm``) with the weight gradient written
+    into the flat buffer by the backward kernel, as :class:`_FlatRMSNorm`."""
+
+    @staticmethod
+    def forward(ctx, x, r, w, flat, name, eps):
+        h, y, rstd = fused.hip().add_rmsnorm_fwd(x.contiguous(), r.contiguous(), w, float(eps))
+        ctx.save_for_backward(h, w, rstd)
+        ctx.flat, ctx.name = flat, name
+        return h, y
+
+    @staticmethod
+    def backward(ctx, dh, dy):
+        h, w, rstd = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros_like(h)
+        view = ctx.flat.params[ctx.name].grad
+        if dh is None:
+            dx = fused.hip().rmsnorm_bwd_into(dy.contiguous(), h, w, rstd, view)
+        else:
+            dx = fused.hip().add_rmsnorm_bwd_into(dy.contiguous(), h, w, rstd, dh.contiguous(), view)
+        ctx.flat.mark_written(ctx.name)
+        return dx, dx, None, None, None, None
+
+
+class _FlatEmbedding(torch.autograd.Function):
+    """Token embedding whose gradient goes straight into the flat buffer: the slot is zeroed and
+    ``embed_bwd_into`` sums each token's dx rows in position order (deterministic) -- instead of
+    torch's embedding backward building a dense [V, D] gradient that autograd then adds in.  ``w`` is
+    the Parameter itself (the only differentiable input); its autograd gradient is None."""
+
+    @staticmethod
+    def forward(ctx, tokens, w, flat, name):
+        ctx.save_for_backward(tokens)
+        ctx.flat, ctx.name = flat, name
+        return F.embedding(tokens, w.detach())
+
+    @staticmethod
+    def backward(ctx, dy):
+        (tokens,) = ctx.saved_tensors
+        view = ctx.flat.params[ctx.name].grad
+        srt, perm = torch.sort(tokens.reshape(-1), stable=True)
+        view.zero_()
+        fused.hip().embed_bwd_into(srt, perm, dy.contiguous().view(-1, view.size(1)), view)
+        ctx.flat.mark_written(ctx.name)
+        return None, None, None, None
+
+
 class Llama(torch.nn.Module):
     def __init__(self, cfg: LlamaConfig, device="cuda", seed: int = 0, checkpoint: bool = False, attn: str = "hip",
                  gemm_layout: str = "nt", overlap_transposes: bool = False, fuse_residual: bool = True,
                  dgrad_nn: Tuple[str, ...] = (), persistent_wt: bool = True, transpose_x: str = "fused",
-                 attn_ot: Optional[bool] = None):
+                 attn_ot: Optional[bool] = None, flat_grads: Optional[bool] = None):
         super().__init__()
         if gemm_layout not in ("nt", "native"):
             raise ValueError("gemm_layout must be 'nt' or 'native'")
@@ -496,9 +565,15 @@ class Llama(torch.nn.Module):
         # bucket's weight all-gather, parallel/dp.py BucketedAllReduce.wait_param)
         self.param_ready: Optional[Callable[[str], None]] = None
         self.flat = FlatParams(cfg.param_shapes(), device)
+        # on the GPU every gradient is written straight into the flat buffer by its kernel (projections:
+        # the weight-gradient GEMM; norms and the embedding: their backward kernels), so no parameter is
+        # zero-filled and then accumulated into; on the CPU reference path norms and the embedding go
+        # through autograd's accumulation
+        on_gpu = torch.device(device).type == "cuda"
+        self.flat_grads = on_gpu if flat_grads is None else bool(flat_grads) and on_gpu
         for n, p in self.flat.params.items():
             self.register_parameter(n.replace(".", "_"), p)
-            if p.dim() == 2 and n != "tok_emb":
+            if (p.dim() == 2 and n != "tok_emb") or self.flat_grads:
                 self.flat.mark_direct(n)
         self._init(seed)
         # NT layout: W^T of every projection stays resident and the optimizer rewrites it with W
@@ -512,8 +587,8 @@ class Llama(torch.nn.Module):
         self.attn_ot = self.flat.eager_xt if attn_ot is None else bool(attn_ot) and self.flat.producer_xt
         self.persistent_wt = persistent_wt and gemm_layout == "nt"
         if self.persistent_wt:
-            self.flat.enable_transposed([n for n in self.flat.direct
-                                         if n.rsplit(".", 1)[-1] not in self.dgrad_nn])
+            self.flat.enable_transposed([n for n in self.flat.direct if n != "tok_emb"
+                                         and n.rsplit(".", 1)[-1] not in self.dgrad_nn])
         cos, sin = fused.rope_tables(cfg.max_seq, cfg.head_dim, cfg.rope_theta, device=device)
         self.register_buffer("rope_cos", cos, persistent=False)
         self.register_buffer("rope_sin", sin, persistent=False)
@@ -568,6 +643,14 @@ class Llama(torch.nn.Module):
     def _norm(self, x: torch.Tensor, r: Optional[torch.Tensor], name: str):
         """``(x + r, rmsnorm(x + r))`` — the residual add fused into the norm kernel; ``r=None``
         is a plain norm of ``x`` (first layer)."""
+        if self.flat_grads:
+            w = self.P(name).detach()
+            if r is None:
+                return x, _FlatRMSNorm.apply(x, w, self.flat, name, self.cfg.norm_eps)
+            if self.fuse_residual:
+                return _FlatAddRMSNorm.apply(x, r, w, self.flat, name, self.cfg.norm_eps)
+            x = x + r
+            return x, _FlatRMSNorm.apply(x, w, self.flat, name, self.cfg.norm_eps)
         if r is None:
             return x, fused.rmsnorm(x, self.P(name), self.cfg.norm_eps)
         if self.fuse_residual:
@@ -598,7 +681,10 @@ class Llama(torch.nn.Module):
     def forward(self, tokens: torch.Tensor, labels: Optional[torch.Tensor] = None) -> torch.Tensor:
         B, S = tokens.shape
         fused.clear_t()  # transposed gradients a previous backward offered and nobody took
-        x = F.embedding(tokens.reshape(-1), self.P("tok_emb"))  # [B*S, D]
+        if self.flat_grads:
+            x = _FlatEmbedding.apply(tokens.reshape(-1), self.P("tok_emb"), self.flat, "tok_emb")  # [B*S, D]
+        else:
+            x = F.embedding(tokens.reshape(-1), self.P("tok_emb"))  # [B*S, D]
         r = None
         for i in range(self.cfg.n_layers):
             if self.checkpoint and self.training:

@@ -583,3 +583,69 @@ def test_rope_bwd_t_is_bit_identical_and_transposed(hip, B, H, Hkv, S):
     ref = hip.rope_split_bwd(dq, dk, dv, cos, sin, 3)
     got, got_t = hip.rope_split_bwd_t(dq, dk, dv, cos, sin, 3)
     assert torch.equal(got, ref) and torch.equal(got_t, ref.t().contiguous())
+
+
+def test_norm_backward_into_the_flat_slot_is_bit_identical(hip):
+    """rmsnorm_bwd_into / add_rmsnorm_bwd_into: the same dx and dW bits as the allocating kernels, dW
+    landing in the given view (a slice of a larger buffer) and nowhere else."""
+    M, D = 1024, 4096
+    x = torch.randn(M, D, device="cuda", dtype=torch.bfloat16)
+    r = torch.randn(M, D, device="cuda", dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(D, device="cuda")).to(torch.bfloat16)
+    dy = torch.randn(M, D, device="cuda", dtype=torch.bfloat16)
+    dres = torch.randn(M, D, device="cuda", dtype=torch.bfloat16)
+    h, _, rstd = hip.add_rmsnorm_fwd(x, r, w, 1e-5)
+    buf = torch.full((3 * D,), 7.0, device="cuda", dtype=torch.bfloat16)
+    view = buf[D:2 * D]
+    dx_ref, dw_ref = hip.add_rmsnorm_bwd(dy, h, w, rstd, dres)
+    dx = hip.add_rmsnorm_bwd_into(dy, h, w, rstd, dres, view)
+    assert torch.equal(dx, dx_ref) and torch.equal(view, dw_ref)
+    assert (buf[:D] == 7).all() and (buf[2 * D:] == 7).all()
+    dx_ref, dw_ref = hip.rmsnorm_bwd(dy, h, w, rstd)
+    dx = hip.rmsnorm_bwd_into(dy, h, w, rstd, view)
+    assert torch.equal(dx, dx_ref) and torch.equal(view, dw_ref)
+
+
+def test_embedding_backward_into_the_flat_slot(hip):
+    """embed_bwd_into: per-token sums of dx rows (repeated tokens, out-of-range ids skipped) match an
+    fp32 reference within one bf16 rounding, untouched rows stay zero, and two runs give the same bits."""
+    V, D, T = 1000, 512, 4096
+    tok = torch.randint(0, 64, (T,), device="cuda")  # many repeats
+    tok[::97] = torch.randint(64, V, (tok[::97].numel(),), device="cuda")
+    dx = torch.randn(T, D, device="cuda", dtype=torch.bfloat16)
+    ref = torch.zeros(V, D, device="cuda").index_add_(0, tok, dx.float())
+    outs = []
+    for _ in range(2):
+        out = torch.zeros(V, D, device="cuda", dtype=torch.bfloat16)
+        srt, perm = torch.sort(tok, stable=True)
+        hip.embed_bwd_into(srt, perm, dx, out)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+    assert torch.allclose(outs[0].float(), ref, rtol=8e-3, atol=1e-2)
+    used = torch.zeros(V, dtype=torch.bool, device="cuda")
+    used[tok] = True
+    assert not outs[0][~used].any()
+
+
+def test_llama_flat_gradients_match_autograd_accumulation():
+    """The GPU model writes the norm and embedding gradients into the flat buffer from their kernels
+    (Llama.flat_grads); the same model with those parameters left to autograd's accumulation (the
+    round-3 path) gives the same gradients: norms bit for bit, the embedding within bf16 rounding."""
+    from gpu_topology_on_k8s_amd.models import Llama, LlamaConfig
+
+    cfg = LlamaConfig(dim=512, n_layers=2, n_heads=4, n_kv_heads=2, vocab=1024, ffn_dim=1024, max_seq=512)
+    tok = torch.randint(0, cfg.vocab, (2, 256), device="cuda")
+    a = Llama(cfg, device="cuda", seed=5)
+    assert a.flat_grads and a.flat.direct["tok_emb"] and a.flat.direct["l0.attn_norm"]
+    b = Llama(cfg, device="cuda", seed=5, flat_grads=False)  # norms / embedding accumulated by autograd
+    assert not b.flat_grads and "tok_emb" not in b.flat.direct
+    for m in (a, b):
+        for _ in range(2):  # the second step checks that nothing accumulates across steps
+            m.flat.zero_grad()
+            m(tok, torch.roll(tok, -1, 1)).backward()
+    for n in a.flat.params:
+        ga, gb = a.flat.params[n].grad, b.flat.params[n].grad
+        if n == "tok_emb":
+            assert torch.allclose(ga.float(), gb.float(), rtol=1e-2, atol=1e-4), n
+        else:
+            assert torch.equal(ga, gb), n
