@@ -126,20 +126,33 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const u16* __restrict_
 #pragma unroll
     for (int j = 0; j < 8; ++j) dwacc[i][j] = 0.f;
   }
-  for (int row = gwave; row < M; row += nwaves) {
+  // one wave per SIMD walks its rows with the NEXT row's x / dy / dres loads in flight while it
+  // computes the current one (the grid is one wave per SIMD, so the second register set is free):
+  // at one outstanding row per wave the kernel was latency-bound at 4.2 TB/s (profiles/r04_norm)
+  u16x8 xv[NV], gv[NV], dv[ACC ? NV : 1];
+  u16x8 nx[NV], ng[NV], nd[ACC ? NV : 1];
+  auto load_row = [&](int row, u16x8 (&a)[NV], u16x8 (&b)[NV], u16x8 (&cc)[ACC ? NV : 1]) {
     const u16x8* xr = reinterpret_cast<const u16x8*>(x + (size_t)row * D);
     const u16x8* dyr = reinterpret_cast<const u16x8*>(dy + (size_t)row * D);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = i * 64 + lane;
+      if (c < nvec) {
+        a[i] = xr[c];
+        b[i] = dyr[c];
+        if constexpr (ACC) cc[i] = reinterpret_cast<const u16x8*>(dres + (size_t)row * D)[c];
+      }
+    }
+  };
+  if (gwave < M) load_row(gwave, xv, gv, dv);
+  for (int row = gwave; row < M; row += nwaves) {
     const float r = rstd[row];
-    u16x8 xv[NV], gv[NV], dv[ACC ? NV : 1];
+    if (row + nwaves < M) load_row(row + nwaves, nx, ng, nd);
     float dot = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = i * 64 + lane;
       if (c < nvec) {
-        xv[i] = xr[c];
-        gv[i] = dyr[c];
-        // issued with x/dy so the residual gradient's latency hides under the same wait
-        if constexpr (ACC) dv[i] = reinterpret_cast<const u16x8*>(dres + (size_t)row * D)[c];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float xf = bf2f(xv[i][j]), dyf = bf2f(gv[i][j]);
@@ -166,6 +179,12 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const u16* __restrict_
         }
         dxr[c] = o;
       }
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      xv[i] = nx[i];
+      gv[i] = ng[i];
+      if constexpr (ACC) dv[i] = nd[i];
     }
   }
   float* part = dw_part + (size_t)gwave * D;
