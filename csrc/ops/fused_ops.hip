@@ -1148,9 +1148,11 @@ __global__ __launch_bounds__(256) void adamw_dev_kernel(float* __restrict__ mast
 template <typename G>
 __global__ __launch_bounds__(256) void sqnorm_kernel(const G* __restrict__ g, float* __restrict__ part, size_t n) {
   __shared__ float red[4];
-  // four independent grid-stride streams per thread, so four 16-B loads are in flight per lane
-  // (one stream ran the 16 GB bf16 gradient at 5.3 TB/s); a fixed grid and order: deterministic
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  // each thread's grid-stride vectors are loaded four at a time (four 16-B loads in flight per lane;
+  // one at a time ran the 16 GB bf16 gradient at 5.3 TB/s) but summed in the same order into one
+  // accumulator: the partials keep their bits (the clip factor, and with it the training trajectory,
+  // is sensitive to the norm's last bits -- profiles/r04_norm)
+  float s = 0.f;
   const size_t nv = n >> 3, stride = (size_t)gridDim.x * 256;
   size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   for (; i + 3 * stride < nv; i += 4 * stride) {
@@ -1160,15 +1162,14 @@ __global__ __launch_bounds__(256) void sqnorm_kernel(const G* __restrict__ g, fl
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[u] += x[u][j] * x[u][j];
+      for (int j = 0; j < 8; ++j) s += x[u][j] * x[u][j];
   }
   for (; i < nv; i += stride) {
     float x[8];
     load_g8(g, i, x);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[0] += x[j] * x[j];
+    for (int j = 0; j < 8; ++j) s += x[j] * x[j];
   }
-  float s = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();

@@ -152,6 +152,10 @@ class FlatParams:
         # NT layout: producers that hold a tile in LDS write the transposed copy too (SwiGLU h^T,
         # RoPE-backward dqkv^T, cross-entropy dlogits^T; Llama(transpose_x="fused"/"forward"))
         self.producer_xt = False
+        # NT layout: each weight-gradient GEMM runs on a side stream, concurrently with its input-gradient
+        # GEMM on the main one (Llama(wgrad_stream=True)); joined at the end of the backward
+        self.wgrad_side: Optional["torch.cuda.Stream"] = None
+        self._join_queued = False
 
     # ---------------------------------------------------------------- persistent W^T
     def enable_transposed(self, names) -> List[str]:
@@ -259,6 +263,28 @@ class FlatParams:
             view.addmm_(a, b)
         for fn in list(self._ready.get(name, ())):
             fn(self.params[name])
+
+    def write_grad_side(self, name: str, dy: torch.Tensor, x_t: Optional[torch.Tensor], dy_t: Optional[torch.Tensor]) -> None:
+        """:meth:`write_grad` (NT) issued on :attr:`wgrad_side` after everything the main stream has
+        queued, so the weight-gradient GEMM overlaps the input-gradient GEMM issued next on the main
+        stream: two GEMMs whose tile counts leave part of the last wave idle fill each other's tails.
+        The main stream waits for the side stream at the end of the backward (autograd callback)."""
+        main = torch.cuda.current_stream(dy.device)
+        side = self.wgrad_side
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self.write_grad(name, dy, None, nt=True, x_t=x_t, dy_t=dy_t)
+        for t in (dy, x_t, dy_t):
+            if t is not None:
+                t.record_stream(side)  # freed by the main stream's owner while the side stream reads it
+        if not self._join_queued:
+            self._join_queued = True
+
+            def join():
+                main.wait_stream(side)
+                self._join_queued = False
+
+            torch.autograd.Variable._execution_engine.queue_callback(join)
 
     def mark_written(self, name: str) -> None:
         """A kernel wrote ``name``'s gradient into the flat buffer itself (not through
@@ -409,14 +435,18 @@ class _FlatLinear(torch.autograd.Function):
         if ctx.nt:
             x_t, w_t = ctx.ops.get()
             ctx.ops = None
+            dy_t = fused.take_t(dy)  # dy^T written by dy's producer kernel (xent / RoPE backward), if any
+            side = ctx.flat.wgrad_side is not None and dy.is_cuda
+            if side:  # weight gradient first, on the side stream: it overlaps the input gradient below
+                ctx.flat.write_grad_side(ctx.name, dy, x_t, dy_t)
             if not ctx.needs_input_grad[0]:
                 dx = None
             elif ctx.dgrad_nn:
                 dx = dy.mm(w_t)  # w_t is W here: dy W (NN)
             else:
                 dx = F.linear(dy, w_t)  # dy (W^T)^T
-            # dy^T written by dy's producer kernel (cross-entropy backward for lm_head), if any
-            ctx.flat.write_grad(ctx.name, dy, None, nt=True, x_t=x_t, dy_t=fused.take_t(dy))
+            if not side:
+                ctx.flat.write_grad(ctx.name, dy, None, nt=True, x_t=x_t, dy_t=dy_t)
         else:
             x, w = ctx.saved_tensors
             dx = dy.mm(w) if ctx.needs_input_grad[0] else None
@@ -457,13 +487,17 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
             dgu, dgu_t = fused.swiglu_bwd_t(da, gu)
             x_t, w_t = ctx.ops.get()
             ctx.ops = None
+            side = ctx.flat.wgrad_side is not None and dgu.is_cuda
+            if side:
+                ctx.flat.write_grad_side(ctx.name, dgu, x_t, dgu_t)
             if not ctx.needs_input_grad[0]:
                 dx = None
             elif ctx.dgrad_nn:
                 dx = dgu.mm(w_t)  # w_t is W here (NN)
             else:
                 dx = F.linear(dgu, w_t)
-            ctx.flat.write_grad(ctx.name, dgu, None, nt=True, dy_t=dgu_t, x_t=x_t)
+            if not side:
+                ctx.flat.write_grad(ctx.name, dgu, None, nt=True, dy_t=dgu_t, x_t=x_t)
         else:
             _, x, w = ctx.saved_tensors
             dgu = fused.hip().swiglu_bwd(da.contiguous(), gu) if gu.is_cuda else fused.swiglu_bwd_ref(da, gu)
@@ -545,7 +579,7 @@ class Llama(torch.nn.Module):
     def __init__(self, cfg: LlamaConfig, device="cuda", seed: int = 0, checkpoint: bool = False, attn: str = "hip",
                  gemm_layout: str = "nt", overlap_transposes: bool = False, fuse_residual: bool = True,
                  dgrad_nn: Tuple[str, ...] = (), persistent_wt: bool = True, transpose_x: str = "fused",
-                 attn_ot: Optional[bool] = None, flat_grads: Optional[bool] = None):
+                 attn_ot: Optional[bool] = None, flat_grads: Optional[bool] = None, wgrad_stream: bool = False):
         super().__init__()
         if gemm_layout not in ("nt", "native"):
             raise ValueError("gemm_layout must be 'nt' or 'native'")
@@ -583,6 +617,9 @@ class Llama(torch.nn.Module):
         self.transpose_x = transpose_x
         self.flat.eager_xt = transpose_x == "forward" and gemm_layout == "nt"
         self.flat.producer_xt = transpose_x in ("forward", "fused") and gemm_layout == "nt"
+        self.wgrad_stream = bool(wgrad_stream) and on_gpu and gemm_layout == "nt"
+        if self.wgrad_stream:
+            self.flat.wgrad_side = torch.cuda.Stream(device=torch.device(device))
         # attention O^T from the forward kernel's epilogue (default: with transpose_x="forward" only)
         self.attn_ot = self.flat.eager_xt if attn_ot is None else bool(attn_ot) and self.flat.producer_xt
         self.persistent_wt = persistent_wt and gemm_layout == "nt"

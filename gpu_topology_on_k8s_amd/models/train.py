@@ -120,7 +120,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
           zero1: bool = False, save_dir: Optional[str] = None, save_every: int = 0, resume: Optional[str] = None,
           keep: int = 2, fuse_residual: bool = True, overlap_norm: bool = False, same_data: bool = False,
           graph: str = "auto", conv: str = "hip", cpu_bind: str = "auto", repeat_batch: bool = False,
-          persistent_wt: bool = True, transpose_x: str = "fused", grad_reduce: str = "bf16", comm_ctas: int = DEFAULT_COMM_CTAS, attn_ot: Optional[bool] = None, flat_grads: bool = True,
+          persistent_wt: bool = True, transpose_x: str = "fused", grad_reduce: str = "bf16", comm_ctas: int = DEFAULT_COMM_CTAS, attn_ot: Optional[bool] = None, flat_grads: bool = True, wgrad_stream: bool = False,
           comm_shadow: int = 0, comm_shadow_k: int = 8, comm_shadow_busbw: float = 350.0) -> Dict[str, object]:
     env = _init_dist(device_kind, comm_ctas)
     if placement == "auto":  # inside a pod the allocation decides; on a bare node, the placement core
@@ -174,7 +174,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         model = Llama(cfg, device=device, seed=seed, checkpoint=checkpoint, attn=attn, gemm_layout=gemm_layout,
                       overlap_transposes=overlap_transposes, fuse_residual=fuse_residual,
                       dgrad_nn=tuple(p for p in dgrad_nn.split(",") if p), persistent_wt=persistent_wt,
-                      transpose_x=transpose_x, attn_ot=attn_ot, flat_grads=flat_grads)
+                      transpose_x=transpose_x, attn_ot=attn_ot, flat_grads=flat_grads, wgrad_stream=wgrad_stream)
         items_per_step, unit, flops_per_item = batch * seq, "tokens", cfg.flops_per_token(seq)
     broadcast_params(model.flat)
     # graph mode issues the gradient collectives after backward (inside the captured step), not from
@@ -344,6 +344,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "transpose_x": getattr(model, "transpose_x", None),
         "attn_ot": getattr(model, "attn_ot", None),
         "flat_grads": bool(getattr(model, "flat_grads", False)),
+        "wgrad_stream": bool(getattr(model, "wgrad_stream", False)),
         "optimizer_writes_wt": bool(getattr(opt, "fused_t", False)),
         "wt_refreshes": int(getattr(model.flat, "t_refreshes", 0)),
         "dgrad_nn": dgrad_nn,
@@ -429,6 +430,8 @@ def main(argv=None) -> int:
     ap.add_argument("--flat-grads", default="on", choices=["on", "off"],
                     help="GPU: norm and embedding gradients written into the flat buffer by their kernels (on), or "
                          "accumulated by autograd from separate tensors (off, the round-3 path)")
+    ap.add_argument("--wgrad-stream", default="off", choices=["on", "off"],
+                    help="NT layout: run each weight-gradient GEMM on a side stream, overlapping its input-gradient GEMM")
     ap.add_argument("--grad-reduce", default="bf16", choices=["bf16", "fp32"],
                     help="DP gradient reduction dtype: bf16 in place, or fp32 (a widened copy reduced and applied in fp32)")
     ap.add_argument("--comm-ctas", type=int, default=DEFAULT_COMM_CTAS,
@@ -446,7 +449,7 @@ def main(argv=None) -> int:
           resume=a.resume, keep=a.keep, fuse_residual=not a.no_fuse_residual,
           overlap_norm=a.overlap_norm, same_data=a.same_data, graph=a.graph, conv=a.conv, cpu_bind=a.cpu_bind,
           repeat_batch=a.repeat_batch, persistent_wt=a.persistent_wt == "on",
-          transpose_x=a.transpose_x, attn_ot={"auto": None, "on": True, "off": False}[a.attn_ot], flat_grads=a.flat_grads == "on", grad_reduce=a.grad_reduce, comm_ctas=a.comm_ctas, comm_shadow=a.comm_shadow,
+          transpose_x=a.transpose_x, attn_ot={"auto": None, "on": True, "off": False}[a.attn_ot], flat_grads=a.flat_grads == "on", wgrad_stream=a.wgrad_stream == "on", grad_reduce=a.grad_reduce, comm_ctas=a.comm_ctas, comm_shadow=a.comm_shadow,
           comm_shadow_k=a.comm_shadow_k, comm_shadow_busbw=a.comm_shadow_busbw)
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -649,3 +649,25 @@ def test_llama_flat_gradients_match_autograd_accumulation():
             assert torch.allclose(ga.float(), gb.float(), rtol=1e-2, atol=1e-4), n
         else:
             assert torch.equal(ga, gb), n
+
+
+def test_llama_side_stream_weight_gradients_are_bit_identical():
+    """wgrad_stream: every weight-gradient GEMM on a side stream, joined at the end of the backward by
+    an autograd callback -- the same gradients, bit for bit, over two steps with an update between."""
+    from gpu_topology_on_k8s_amd.models import Llama, LlamaConfig
+
+    cfg = LlamaConfig(dim=512, n_layers=2, n_heads=4, n_kv_heads=2, vocab=1024, ffn_dim=1024, max_seq=512)
+    tok = torch.randint(0, cfg.vocab, (2, 256), device="cuda")
+    out = {}
+    for ws in (False, True):
+        m = Llama(cfg, device="cuda", seed=5, wgrad_stream=ws)
+        assert m.wgrad_stream == ws
+        for _ in range(2):
+            m.flat.zero_grad()
+            m(tok, torch.roll(tok, -1, 1)).backward()
+            g = m.flat.grad.clone()  # read on the main stream right after backward: the join must hold
+            with torch.no_grad():
+                m.flat.data.add_(m.flat.grad, alpha=-1e-2)
+                m.flat.invalidate_t()
+        out[ws] = g
+    assert torch.equal(out[True], out[False])
