@@ -116,6 +116,8 @@ class CommShadow:
         if self._cur:
             self.steps.append((ready, self._cur))
             self._cur = []
+            if len(self.steps) > 64:  # a long run keeps the last 64 steps' events, not every step's
+                del self.steps[0]
 
     def reset_timing(self) -> None:
         self.steps, self._cur = [], []
