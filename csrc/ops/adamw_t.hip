@@ -116,6 +116,56 @@ __device__ __forceinline__ u16x8 adam8(float* __restrict__ master, float* __rest
   return wo;
 }
 
+// adam8 split in two: the loads of 8 elements, then the update and stores from those registers.
+// The tile kernel issues the loads of several passes before any store: through the same master/m/v
+// pointers the compiler cannot hoist a later pass's loads above an earlier pass's stores.
+struct Adam8In {
+  f32x4 p0, p1, m0, m1, v0, v1;
+  float gf[8];
+};
+template <typename G>
+__device__ __forceinline__ void adam8_load(const float* __restrict__ master, const float* __restrict__ m, const float* __restrict__ v,
+                                           const G* __restrict__ g, size_t i, Adam8In& in) {
+  const f32x4* mp = reinterpret_cast<const f32x4*>(master + i);
+  const f32x4* mm_ = reinterpret_cast<const f32x4*>(m + i);
+  const f32x4* vp = reinterpret_cast<const f32x4*>(v + i);
+  in.p0 = mp[0], in.p1 = mp[1], in.m0 = mm_[0], in.m1 = mm_[1], in.v0 = vp[0], in.v1 = vp[1];
+  load_g8(g, i, in.gf);
+}
+__device__ __forceinline__ u16x8 adam8_store(float* __restrict__ master, float* __restrict__ m, float* __restrict__ v,
+                                             u16* __restrict__ w, size_t i, const Adam8In& in, const Hyper& h) {
+  u16x8 wo;
+  float p[8], mm[8], vv[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    p[j] = in.p0[j], p[j + 4] = in.p1[j];
+    mm[j] = in.m0[j], mm[j + 4] = in.m1[j];
+    vv[j] = in.v0[j], vv[j + 4] = in.v1[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {  // adamw_body's expressions, in its order
+    const float gr = in.gf[j] * h.gs;
+    mm[j] = h.b1 * mm[j] + (1.f - h.b1) * gr;
+    vv[j] = h.b2 * vv[j] + (1.f - h.b2) * gr * gr;
+    const float upd = (mm[j] / h.bc1) / (sqrtf(vv[j] / h.bc2) + h.eps);
+    p[j] = p[j] - h.lr * (upd + h.wd * p[j]);
+    wo[j] = f2bf(p[j]);
+  }
+  f32x4 p0, p1, m0, m1, v0, v1;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    p0[j] = p[j], p1[j] = p[j + 4];
+    m0[j] = mm[j], m1[j] = mm[j + 4];
+    v0[j] = vv[j], v1[j] = vv[j + 4];
+  }
+  f32x4* mp = reinterpret_cast<f32x4*>(master + i);
+  f32x4* mmp = reinterpret_cast<f32x4*>(m + i);
+  f32x4* vp = reinterpret_cast<f32x4*>(v + i);
+  mp[0] = p0, mp[1] = p1, mmp[0] = m0, mmp[1] = m1, vp[0] = v0, vp[1] = v1;
+  *reinterpret_cast<u16x8*>(w + i) = wo;
+  return wo;
+}
+
 // one transposed matrix: rows R x cols C at flat element offset `off`, its W^T ([C, R]) at `toff` of
 // the transposed buffer, tiles [tile_base, tile_base + (R/64)(C/64)) of the global tile index
 struct Mat {
@@ -128,7 +178,7 @@ struct Mat {
 // kernel's 5.97 (profiles/r04_llama).  W^T leaves as 256 output rows x 128 B.
 constexpr int kTR = 64, kTC = 256;
 
-template <bool DEV, typename G>
+template <bool DEV, typename G, int kAhead = 1>
 __global__ __launch_bounds__(256) void adamw_tiles_kernel(float* __restrict__ master, float* __restrict__ m, float* __restrict__ v,
                                                           const G* __restrict__ g, u16* __restrict__ w, u16* __restrict__ wt,
                                                           const Mat* __restrict__ mats, int nmats, int64_t total_tiles,
@@ -151,11 +201,28 @@ __global__ __launch_bounds__(256) void adamw_tiles_kernel(float* __restrict__ ma
     const int64_t local = ti - mt.tile_base, tiles_c = mt.C / kTC;
     const int64_t r0 = (local / tiles_c) * kTR, c0 = (local % tiles_c) * kTC;
     // update: 8 passes of 8 rows; thread t takes vector t & 31 of row 8 * pass + t / 32
+    if (kAhead == 1) {
 #pragma unroll 4
-    for (int pass = 0; pass < kTR / 8; ++pass) {
-      const int r = 8 * pass + (t >> 5), vv = t & 31;
-      const u16x8 wo = adam8(master, m, v, g, w, (size_t)(mt.off + (r0 + r) * mt.C + c0 + 8 * vv), h);
-      tile[r][vv ^ ((r >> 3) & 7)] = wo;
+      for (int pass = 0; pass < kTR / 8; ++pass) {
+        const int r = 8 * pass + (t >> 5), vv = t & 31;
+        const u16x8 wo = adam8(master, m, v, g, w, (size_t)(mt.off + (r0 + r) * mt.C + c0 + 8 * vv), h);
+        tile[r][vv ^ ((r >> 3) & 7)] = wo;
+      }
+    } else {  // kAhead passes' loads in flight before their stores
+#pragma unroll 1
+      for (int p0 = 0; p0 < kTR / 8; p0 += kAhead) {
+        Adam8In in[kAhead];
+#pragma unroll
+        for (int u = 0; u < kAhead; ++u) {
+          const int r = 8 * (p0 + u) + (t >> 5), vv = t & 31;
+          adam8_load(master, m, v, g, (size_t)(mt.off + (r0 + r) * mt.C + c0 + 8 * vv), in[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kAhead; ++u) {
+          const int r = 8 * (p0 + u) + (t >> 5), vv = t & 31;
+          tile[r][vv ^ ((r >> 3) & 7)] = adam8_store(master, m, v, w, (size_t)(mt.off + (r0 + r) * mt.C + c0 + 8 * vv), in[u], h);
+        }
+      }
     }
     __syncthreads();
     // transposed write: per instruction a wave takes one 16-B column vector vc (8 columns) x the 8
@@ -194,7 +261,7 @@ __global__ __launch_bounds__(256) void adamw_ranges_kernel(float* __restrict__ m
 template <typename G>
 void launch(at::Tensor& master, at::Tensor& m, at::Tensor& v, const G* gp, at::Tensor& w, at::Tensor& wt, const at::Tensor& hp,
             const at::Tensor& mats, int64_t total_tiles, const at::Tensor& ranges, int64_t max_range,
-            const c10::optional<at::Tensor>& part, const c10::optional<at::Tensor>& t) {
+            const c10::optional<at::Tensor>& part, const c10::optional<at::Tensor>& t, int64_t ahead_arg) {
   const bool dev = t.has_value();
   const float* pp = nullptr;
   int np = 0;
@@ -213,9 +280,16 @@ void launch(at::Tensor& master, at::Tensor& m, at::Tensor& v, const G* gp, at::T
   if (mats.size(0) > 0 && total_tiles > 0) {
     const unsigned grid = (unsigned)std::min<int64_t>(total_tiles, 4096);
     const Mat* md = reinterpret_cast<const Mat*>(mats.data_ptr<int64_t>());
+    const int ahead = ahead_arg == 2 || ahead_arg == 4 ? (int)ahead_arg : 1;  // passes' loads in flight (A/B)
     if (dev)
       hipLaunchKernelGGL((adamw_tiles_kernel<true, G>), dim3(grid), dim3(256), 0, s, mp, mmp, vp, gp, wp, wtp, md, (int)mats.size(0),
                          total_tiles, hp.data_ptr<float>(), pp, np, tp);
+    else if (ahead == 4)
+      hipLaunchKernelGGL((adamw_tiles_kernel<false, G, 4>), dim3(grid), dim3(256), 0, s, mp, mmp, vp, gp, wp, wtp, md,
+                         (int)mats.size(0), total_tiles, hp.data_ptr<float>(), pp, np, tp);
+    else if (ahead == 2)
+      hipLaunchKernelGGL((adamw_tiles_kernel<false, G, 2>), dim3(grid), dim3(256), 0, s, mp, mmp, vp, gp, wp, wtp, md,
+                         (int)mats.size(0), total_tiles, hp.data_ptr<float>(), pp, np, tp);
     else
       hipLaunchKernelGGL((adamw_tiles_kernel<false, G>), dim3(grid), dim3(256), 0, s, mp, mmp, vp, gp, wp, wtp, md,
                          (int)mats.size(0), total_tiles, hp.data_ptr<float>(), pp, np, tp);
@@ -236,7 +310,7 @@ void launch(at::Tensor& master, at::Tensor& m, at::Tensor& v, const G* gp, at::T
 // part / t present = the DEV form (hp in adamw_step_dev's layout).
 void adamw_step_t(at::Tensor& master, at::Tensor& m, at::Tensor& v, const at::Tensor& g, at::Tensor& w, at::Tensor& wt,
                   const at::Tensor& hp, const at::Tensor& mats, int64_t total_tiles, const at::Tensor& ranges,
-                  int64_t max_range, c10::optional<at::Tensor> part, c10::optional<at::Tensor> t) {
+                  int64_t max_range, c10::optional<at::Tensor> part, c10::optional<at::Tensor> t, int64_t ahead) {
   CHECK_DEV(master, at::kFloat);
   CHECK_DEV(m, at::kFloat);
   CHECK_DEV(v, at::kFloat);
@@ -252,9 +326,10 @@ void adamw_step_t(at::Tensor& master, at::Tensor& m, at::Tensor& v, const at::Te
   TORCH_CHECK(mats.dim() == 2 && mats.size(1) == 5 && ranges.dim() == 2 && ranges.size(1) == 2, "adamw_step_t: bad descriptors");
   TORCH_CHECK(ranges.size(0) <= 65535, "adamw_step_t: too many ranges");
   if (g.scalar_type() == at::kFloat)
-    launch(master, m, v, g.data_ptr<float>(), w, wt, hp, mats, total_tiles, ranges, max_range, part, t);
+    launch(master, m, v, g.data_ptr<float>(), w, wt, hp, mats, total_tiles, ranges, max_range, part, t, ahead);
   else
-    launch(master, m, v, reinterpret_cast<const u16*>(g.data_ptr()), w, wt, hp, mats, total_tiles, ranges, max_range, part, t);
+    launch(master, m, v, reinterpret_cast<const u16*>(g.data_ptr()), w, wt, hp, mats, total_tiles, ranges, max_range, part, t,
+           ahead);
 }
 
 }  // namespace gtk_adamw

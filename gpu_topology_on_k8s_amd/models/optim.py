@@ -38,6 +38,9 @@ class FlatAdamW:
         self.flat = flat
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.clip_norm = clip_norm
+        # AdamW-T tile kernel: how many 8-row passes' loads it issues before their stores (1, 2 or 4);
+        # 2 measured fastest at the Llama-3-8B layout: 40.85 ms vs 42.51 (1) and 41.76 (4) (profiles/r04_memk)
+        self.adamw_ahead = 2
         self.group = group
         self.sharded = shards is not None
         self.shards: List[Tuple[int, int]] = list(shards) if shards is not None else [(0, flat.numel)]
@@ -117,7 +120,7 @@ class FlatAdamW:
         if self.fused_t:
             mats, tiles, ranges, maxr = self.flat.adamw_plan()
             fused.hip().adamw_step_t(self.master, self.m, self.v, gbuf, self.flat.data, self.flat.data_t, self.hp,
-                                     mats, tiles, ranges, maxr, None, None)
+                                     mats, tiles, ranges, maxr, None, None, self.adamw_ahead)
             self.flat.mark_t_valid()
             return
         self._invalidate_t()
@@ -159,7 +162,7 @@ class FlatAdamW:
             if self.fused_t:
                 mats, tiles, ranges, maxr = self.flat.adamw_plan()
                 hip.adamw_step_t(self.master, self.m, self.v, g, d, self.flat.data_t, self.hp_dev, mats, tiles, ranges, maxr,
-                                 part, self.t_dev)
+                                 part, self.t_dev, 1)
                 self.flat.mark_t_valid()
                 return
             hip.adamw_step_dev(self.master, self.m, self.v, g, d, self.hp_dev, part, self.t_dev)

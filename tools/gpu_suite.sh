@@ -125,6 +125,14 @@ print(json.dumps({"tflops": round(float(w["tflops"]), 1), "hbm_copy_gbps": round
     step llama_on2 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --wgrad-stream on
     step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1 --wgrad-stream on
     ;;
+  memk)
+    # memory-bound tile kernels with every load of the tile issued first: tests, kernel A/B bench, step, trace
+    step pytest_fused 600 python -u -m pytest tests/test_fused_gpu.py -x -v --timeout 300 --timeout-method thread
+    step fused_t_ab 300 python -u bench/fused_t_ab.py
+    step adamw_t_ab 300 python -u bench/adamw_t_ab.py
+    step llama 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
+    step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
+    ;;
   attn_ab)
     # attention backward A/B (interleaved, B 4 and 2) with bit-identity tests and counters
     step pytest_attn 600 python -u -m pytest tests/test_attention_gpu.py -x -v --timeout 300 --timeout-method thread
