@@ -26,7 +26,7 @@ import sys
 import sysconfig
 from dataclasses import dataclass, field
 from pathlib import Path
-from typing import Dict, List, Optional
+from typing import List, Optional
 
 HERE = Path(__file__).resolve().parent
 REPO = HERE.parent.parent
@@ -75,7 +75,6 @@ class Target:
     pybind: bool = True
     torch: bool = False
     shared: bool = True
-    src_flags: Dict[str, List[str]] = field(default_factory=dict)  # extra compile flags per source file name
 
     def command(self) -> List[str]:
         if self.compiler == "hipcc":
@@ -186,7 +185,7 @@ def _build_objects(t: Target, force: bool, verbose: bool, jobs: int) -> str:
     def one(src: Path) -> Path:
         obj = odir / (src.stem + ".o")
         if force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, dep_t):
-            _run(flags + t.src_flags.get(src.name, []) + ["-c", str(src), "-o", str(obj)], f"{t.name}:{src.name}", verbose)
+            _run(flags + ["-c", str(src), "-o", str(obj)], f"{t.name}:{src.name}", verbose)
         return obj
 
     with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(t.sources)))) as ex:
