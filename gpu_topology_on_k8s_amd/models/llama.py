@@ -150,7 +150,7 @@ class FlatParams:
         self._plan = None  # adamw_plan() cache
         self.eager_xt = False  # NT layout: make x^T in the forward (Llama(transpose_x="forward"))
         # NT layout: producers that hold a tile in LDS write the transposed copy too (SwiGLU h^T,
-        # RoPE-backward dqkv^T, cross-entropy dlogits^T; Llama(transpose_x="fused"/"forward"))
+        # attention O^T, RoPE-backward dqkv^T, cross-entropy dlogits^T; Llama(transpose_x="fused"/"forward"))
         self.producer_xt = False
         # NT layout: each weight-gradient GEMM runs on a side stream, concurrently with its input-gradient
         # GEMM on the main one (Llama(wgrad_stream=True)); joined at the end of the backward
@@ -620,8 +620,8 @@ class Llama(torch.nn.Module):
         self.wgrad_stream = bool(wgrad_stream) and on_gpu and gemm_layout == "nt"
         if self.wgrad_stream:
             self.flat.wgrad_side = torch.cuda.Stream(device=torch.device(device))
-        # attention O^T from the forward kernel's epilogue (default: with transpose_x="forward" only)
-        self.attn_ot = self.flat.eager_xt if attn_ot is None else bool(attn_ot) and self.flat.producer_xt
+        # attention O^T from the forward kernel's epilogue (default: with the producer-written transposes)
+        self.attn_ot = self.flat.producer_xt if attn_ot is None else bool(attn_ot) and self.flat.producer_xt
         self.persistent_wt = persistent_wt and gemm_layout == "nt"
         if self.persistent_wt:
             self.flat.enable_transposed([n for n in self.flat.direct if n != "tok_emb"
@@ -704,8 +704,9 @@ class Llama(torch.nn.Module):
         qkv = self._linear(h, f"l{i}.wqkv")
         q, k, v = fused.rope_split(qkv, self.rope_cos, self.rope_sin, B, S, H, Hkv, Dh, want_t=self.flat.producer_xt)
         if self.attn_ot:
-            # o^T from the attention kernel's epilogue: 46 us per layer against the 43 us transpose it
-            # replaces (profiles/r04_fused_t), so only the all-eager "forward" mode asks for it by default
+            # o^T from the attention kernel's epilogue: +47 us per layer in the kernel against the 43 us
+            # transpose it replaces, step time unchanged in an interleaved A/B, +4.3 GB kept from the
+            # forward (profiles/r04_otab)
             o, o_t = self._attention(q, k, v, want_t=True)
         else:
             o, o_t = self._attention(q, k, v), None

@@ -420,13 +420,13 @@ def main(argv=None) -> int:
                          "W^T by a transpose in every backward (off, the round-3 path)")
     ap.add_argument("--transpose-x", default="fused", choices=["fused", "backward", "forward"],
                     help="NT layout: where the weight gradients' transposed operands come from. fused: written by the "
-                         "producer kernels that hold the tile in LDS (SwiGLU h^T, cross-entropy dlogits^T), the "
-                         "rest transposed in the backward; backward: every one transposed in the backward "
-                         "(round 3); forward: fused, plus attention O^T from its kernel and every other x^T made "
-                         "right after its producer")
+                         "producer kernels that hold the tile in LDS (SwiGLU h^T, attention O^T, RoPE-backward "
+                         "dqkv^T, cross-entropy dlogits^T), the rest transposed in the backward; backward: every one "
+                         "transposed in the backward (round 3); forward: fused, plus every other x^T made right "
+                         "after its producer")
     ap.add_argument("--attn-ot", default="auto", choices=["auto", "on", "off"],
                     help="NT layout: the attention forward kernel also writes O^T for the o-projection's weight "
-                         "gradient (auto: only with --transpose-x forward)")
+                         "gradient (auto: with --transpose-x fused / forward)")
     ap.add_argument("--flat-grads", default="on", choices=["on", "off"],
                     help="GPU: norm and embedding gradients written into the flat buffer by their kernels (on), or "
                          "accumulated by autograd from separate tensors (off, the round-3 path)")

@@ -543,18 +543,20 @@ def test_attention_forward_writes_o_transpose(hip, B, H, Hkv, S):
 
 
 def test_llama_fused_transposes_are_bit_identical():
-    """transpose_x="fused" (SwiGLU h^T, attention O^T and dlogits^T written by their producers, the
-    dlogits^T handed to lm_head through ops/fused.py offer_t/take_t) and "forward" give the same
-    losses and gradients, bit for bit, as transposing every operand in the backward."""
+    """transpose_x="fused" (SwiGLU h^T, attention O^T, RoPE dqkv^T and dlogits^T written by their
+    producers; the backward ones handed on through ops/fused.py offer_t/take_t), with and without the
+    attention O^T, and "forward" give the same losses and gradients, bit for bit, as transposing every
+    operand in the backward."""
     from gpu_topology_on_k8s_amd.models import Llama, LlamaConfig
     from gpu_topology_on_k8s_amd.ops import fused
 
     cfg = LlamaConfig(dim=512, n_layers=2, n_heads=4, n_kv_heads=2, vocab=1024, ffn_dim=1024, max_seq=512)
     tok = torch.randint(0, cfg.vocab, (2, 256), device="cuda")
     out = {}
-    for mode in ("backward", "fused", "fused+ot", "forward"):
-        m = Llama(cfg, device="cuda", seed=5, gemm_layout="nt", transpose_x=mode.split("+")[0],
-                  attn_ot=True if mode.endswith("+ot") else None)
+    for mode in ("backward", "fused", "fused-no-ot", "forward"):
+        m = Llama(cfg, device="cuda", seed=5, gemm_layout="nt", transpose_x=mode.split("-")[0],
+                  attn_ot=False if mode.endswith("-no-ot") else None)
+        assert m.attn_ot == (mode in ("fused", "forward"))
         losses = []
         for _ in range(2):
             m.flat.zero_grad()
@@ -566,7 +568,7 @@ def test_llama_fused_transposes_are_bit_identical():
                 m.flat.data.add_(m.flat.grad, alpha=-1e-2)
                 m.flat.invalidate_t()
         out[mode] = (losses, m.flat.grad.float().clone())
-    for mode in ("fused", "fused+ot", "forward"):
+    for mode in ("fused", "fused-no-ot", "forward"):
         assert out[mode][0] == out["backward"][0], mode
         assert torch.equal(out[mode][1], out["backward"][1]), mode
 
