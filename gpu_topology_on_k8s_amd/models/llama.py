@@ -737,14 +737,19 @@ class Llama(torch.nn.Module):
 
 
 def smoke_step(device: str = "cuda:0") -> float:
-    """One tiny forward+backward on ``device`` through the HIP kernels (``__graft_entry__.smoke``)."""
+    """One tiny forward+backward on ``device`` through the HIP kernels (``__graft_entry__.smoke``): head
+    dim 128 and multiples of the tile sizes, so the flash attention (with its O^T epilogue), the
+    transposed-output SwiGLU / RoPE / cross-entropy kernels and the flat-gradient norm and embedding
+    kernels all run, not their fallbacks."""
     torch.manual_seed(0)
-    cfg = LlamaConfig.tiny()
+    cfg = LlamaConfig(dim=512, n_layers=2, n_heads=4, n_kv_heads=2, vocab=1024, ffn_dim=1024, max_seq=512)
     model = Llama(cfg, device=device)
-    tokens = torch.randint(0, cfg.vocab, (2, 64), device=device)
+    tokens = torch.randint(0, cfg.vocab, (2, 128), device=device)
+    assert model.attn_ot and model.flat_grads and model.persistent_wt
     loss = model(tokens, torch.roll(tokens, -1, dims=1))
     loss.backward()
     torch.cuda.synchronize()
+    assert not fused._PENDING_T  # every transposed gradient a producer offered was consumed
     g = model.flat.grad.float()
     assert torch.isfinite(g).all() and g.abs().sum() > 0
     return float(loss.item())
