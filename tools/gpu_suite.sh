@@ -141,6 +141,13 @@ print(json.dumps({"tflops": round(float(w["tflops"]), 1), "hbm_copy_gbps": round
     step llama_on2 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --attn-ot on
     step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1 --attn-ot on
     ;;
+  pmcstep)
+    # counters over one Llama-3-8B step: MFMA busy, then memory-side requests (each pass its own run),
+    # summarised on the box (the per-dispatch databases exceed what gpurun copies back)
+    step pmc_mfma 300 timeout -s KILL 290 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-trace -d "$out/mfma" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 1 --warmup 1
+    step pmc_mem 300 timeout -s KILL 290 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum GRBM_GUI_ACTIVE --kernel-trace -d "$out/mem" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 1 --warmup 1
+    step pmc_tables 120 bash -c "python tools/pmc_table.py $out/mfma/run_results.db > $out/mfma.md && python tools/pmc_table.py $out/mem/run_results.db > $out/mem.md && rm -rf $out/mfma $out/mem"
+    ;;
   attn_ab)
     # attention backward A/B (interleaved, B 4 and 2) with bit-identity tests and counters
     step pytest_attn 600 python -u -m pytest tests/test_attention_gpu.py -x -v --timeout 300 --timeout-method thread
