@@ -3,6 +3,7 @@ learnable synthetic data, the capturable AdamW against the eager one, and the be
 with two 2-rank gloo jobs on a fake 8-device node."""
 import json
 import os
+import socket
 import subprocess
 import sys
 
@@ -53,7 +54,9 @@ def test_mnist_training_learns_on_cpu():
 
     env = {k: os.environ.get(k) for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     try:
-        os.environ["MASTER_PORT"] = "29731"
+        with socket.socket() as sk:  # a fixed port collides with other tests under pytest -n
+            sk.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
         out = train("mnist-cnn", batch=32, steps=25, warmup=1, device_kind="cpu", log=False, lr=1e-3)
     finally:
         import torch.distributed as dist
