@@ -53,48 +53,33 @@ def main():
     t = timeit(lambda: hip.attn_fwd(q, k, v, Dh ** -0.5), a.iters)
     res["hip_fwd_ms"] = t * 1e3
     res["hip_fwd_tflops"] = fwd_flops / t / 1e12
-    if hasattr(hip, "attn_fwd_v1"):
-        t = timeit(lambda: hip.attn_fwd_v1(q, k, v, Dh ** -0.5), a.iters)
-        res["hip_fwd_v1_ms"] = t * 1e3
     t = timeit(lambda: hip.attn_bwd(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
     res["hip_bwd_ms"] = t * 1e3
     res["hip_bwd_tflops"] = 2.5 * fwd_flops / t / 1e12
-    if hasattr(hip, "attn_bwd_v4"):
-        t = timeit(lambda: hip.attn_bwd_v4(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
-        res["hip_bwd_v4_ms"] = t * 1e3
-    if hasattr(hip, "attn_bwd_v3"):
-        t = timeit(lambda: hip.attn_bwd_v3(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
-        res["hip_bwd_v3_ms"] = t * 1e3
-    if hasattr(hip, "attn_bwd_v2"):
-        t = timeit(lambda: hip.attn_bwd_v2(do, q, k, v, o, lse, Dh ** -0.5), a.iters)
-        res["hip_bwd_v2_ms"] = t * 1e3
     if a.ab:
-        variants = {n: getattr(hip, n) for n in ("attn_bwd", "attn_bwd_v5m0", "attn_bwd_dq_alias", "attn_bwd_v5t", "attn_bwd_v4",
-                                                 "attn_bwd_v3")
-                    if hasattr(hip, n)}
+        # interleaved A/B of the backward variants the extension exports (dK/dV v5 = the round-4 default,
+        # v7 = S / dP in VGPRs, with the dV/dK accumulators pinned to AGPRs or left to the compiler)
+        variants = {"default": lambda: hip.attn_bwd(do, q, k, v, o, lse, Dh ** -0.5)}
+        if hasattr(hip, "attn_bwd_v5"):
+            variants["v5"] = lambda: hip.attn_bwd_v5(do, q, k, v, o, lse, Dh ** -0.5)
+        if hasattr(hip, "attn_bwd_v7"):
+            variants["v7_asm"] = lambda: hip.attn_bwd_v7(do, q, k, v, o, lse, Dh ** -0.5, True)
+            variants["v7_cc"] = lambda: hip.attn_bwd_v7(do, q, k, v, o, lse, Dh ** -0.5, False)
         times = {n: [] for n in variants}
         for fn in variants.values():
-            fn(do, q, k, v, o, lse, Dh ** -0.5)
+            fn()
         for _ in range(a.ab):
             for n, fn in variants.items():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                fn(do, q, k, v, o, lse, Dh ** -0.5)
+                fn()
                 e1.record()
                 times[n].append((e0, e1))
         torch.cuda.synchronize()
         res["ab_median_ms"] = {n: sorted(x.elapsed_time(y) for x, y in ts)[len(ts) // 2] for n, ts in times.items()}
-        fvars = {n: getattr(hip, n) for n in ("attn_fwd", "attn_fwd_noalias") if hasattr(hip, n)}
-        ftimes = {n: [] for n in fvars}
-        for _ in range(a.ab):
-            for n, fn in fvars.items():
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                fn(q, k, v, Dh ** -0.5)
-                e1.record()
-                ftimes[n].append((e0, e1))
-        torch.cuda.synchronize()
-        res["ab_fwd_median_ms"] = {n: sorted(x.elapsed_time(y) for x, y in ts)[len(ts) // 2] for n, ts in ftimes.items()}
+        ref = variants["default"]()
+        res["ab_rel_vs_default"] = {n: [float(((x.float() - y.float()).norm() / y.float().norm()).item()) for x, y in zip(fn(), ref)]
+                                    for n, fn in variants.items()}
     try:
         t = timeit(lambda: F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True), a.iters)
         res["sdpa_fwd_ms"] = t * 1e3

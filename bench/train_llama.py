@@ -42,9 +42,9 @@ def run(placement: str, a) -> dict:
     cmd = ([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1",
            f"--master-port={_port()}", "-m", "gpu_topology_on_k8s_amd.models.train", "--model", a.model, "--batch", str(a.batch),
            "--seq", str(a.seq), "--steps", str(a.steps), "--warmup", str(a.warmup), "--placement", placement,
-           "--bucket-mb", str(a.bucket_mb), "--attn", a.attn, "--gemm-tuning", a.gemm_tuning, "--gemm-layout", a.gemm_layout,
+           "--bucket-mb", str(a.bucket_mb), "--attn", a.attn, "--gemm-tuning", a.gemm_tuning,
            "--device", a.device, "--discovery", a.discovery]
-           + (["--overlap-transposes"] if a.overlap_transposes else []) + (["--zero1"] if a.zero1 else [])
+           + (["--zero1"] if a.zero1 else [])
            + (["--checkpoint"] if a.checkpoint else []) + (["--gemm-table", a.gemm_table] if a.gemm_table else [])
            + ["--graph", a.graph])
     # dma-buf IPC handles for RCCL's P2P/IPC transport between the ranks (see bench.py main())
@@ -73,8 +73,6 @@ def main() -> int:
     ap.add_argument("--checkpoint", action="store_true")
     ap.add_argument("--gemm-tuning", default="auto", choices=["auto", "off", "use", "tune"])
     ap.add_argument("--gemm-table", default="")
-    ap.add_argument("--gemm-layout", default="nt", choices=["nt", "native"])
-    ap.add_argument("--overlap-transposes", action="store_true")
     ap.add_argument("--zero1", action="store_true", help="ZeRO-1: sharded AdamW, reduce-scatter grads / all-gather weights")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"], help="whole-step hipGraph (models/train.py)")
     ap.add_argument("--timeout", type=int, default=1500)

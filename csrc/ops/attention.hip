@@ -92,6 +92,27 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& acc, int base) {
   return out;
 }
 
+__device__ __forceinline__ bf16x8 pack8a(const float* x, int base) {
+  bf16x8 out;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = (__bf16)x[base + j];
+  return out;
+}
+
+// Empty asm statements that "modify" their operands: code computing those values cannot move across
+// them, and volatile asm keeps its order with the other volatile asm (the dV/dK MFMAs of dK/dV v7), so a
+// pair of pins fixes which MFMA gap a piece of VALU issues in.  No instruction is emitted.
+__device__ __forceinline__ void pin2(float& a, float& b) { asm volatile("" : "+v"(a), "+v"(b)); }
+__device__ __forceinline__ void pin4(float& a, float& b, float& c, float& d) {
+  asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
+__device__ __forceinline__ void pin16(float* x) {
+  asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]));
+  asm volatile("" : "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15]));
+}
+__device__ __forceinline__ void pin_b(bf16x8& a, bf16x8& b) { asm volatile("" : "+v"(a), "+v"(b)); }
+__device__ __forceinline__ void pin_b1(bf16x8& a) { asm volatile("" : "+v"(a)); }
+
 // raw v_exp_f32 (2^x): no denormal range reduction — softmax terms below 2^-126 are 0 either way
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -333,155 +354,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict
   }
 }
 
-// ---- forward with the tile's LDS images as __restrict__ parameters (the default since round 4).
-// fwd2's tile reads the K/V images of buffer kt&1 and issues the DMA of tile kt+1 into buffer
-// (kt+1)&1, both through pointers into ONE __shared__ array with a run-time index, so the compiler
-// cannot prove the DMA target disjoint from the images and inserts `s_waitcnt vmcnt(0)` before the
-// first transposed V read: every tile waited mid-way for the next tile's DMA.  Passing the three
-// images as __restrict__ parameters of an inlined function gives their accesses scoped-noalias
-// metadata, the LDS-DMA wait tracking sees the reads and the DMA as disjoint, and the wait goes; the
-// DMA now lands under the softmax AND the PV MFMAs.  Correctness does not rest on that analysis: the
-// only orderings the double buffer needs (tile kt+1 staged before it is read; tile kt's reads
-// returned before its buffer is refilled) are dma_sync()'s explicit vmcnt(0) lgkmcnt(0) + barrier at
-// the end of every tile.  Same instructions and order of arithmetic as fwd2: bit-identical output.
-template <bool kMasked>
-__device__ __forceinline__ void fwd_tile_na(const char* __restrict__ kimg, const char* __restrict__ vimg,
-                                            char* __restrict__ nimg, bool prefetch, const KVStage& stage, int kt,
-                                            const bf16x8 (&qf)[8], f32x16 (&oacc)[4], float& m, float& l, int lane, int r,
-                                            int hh, int myq, float c) {
-  const int key0 = kt * BK;
-  f32x16 s0 = f32x16{}, s1 = f32x16{};
-  __builtin_amdgcn_s_setprio(1);
-  {
-    bf16x8 kf0[8], kf1[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      kf0[s] = lds_b128(kimg, swz(r, 2 * s + hh));
-      kf1[s] = lds_b128(kimg, swz(32 + r, 2 * s + hh));
-    }
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      s0 = mfma(kf0[s], qf[s], s0);
-      s1 = mfma(kf1[s], qf[s], s1);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x8, 8, 0);
-  }
-  __builtin_amdgcn_s_setprio(0);
-  if (prefetch) stage.load(kt + 1, nimg);  // lands under softmax + PV
-  if (kMasked) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int k0i = key0 + crow(i, hh);
-      if (k0i > myq) s0[i] = -INFINITY;
-      if (k0i + 32 > myq) s1[i] = -INFINITY;
-    }
-  }
-  float mx = max3(s0[0], s1[0], s0[1]);
-#pragma unroll
-  for (int i = 1; i < 16; ++i) mx = max3(mx, s1[i], i + 1 < 16 ? s0[i + 1] : s1[i]);
-  const float mrow = xhalf_max(mx) * c;
-  const float mnew = mrow > m + kMaxSlack ? mrow : m;
-  const bool resc = __any(mnew != m);
-  float rs = 0.f;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    s0[i] = fexp2(fmaf(s0[i], c, -mnew));
-    s1[i] = fexp2(fmaf(s1[i], c, -mnew));
-    rs += s0[i] + s1[i];
-  }
-  rs += __shfl_xor(rs, 32, 64);
-  if (resc) {
-    const float alpha = fexp2(m - mnew);
-    l *= alpha;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
-  }
-  l += rs;
-  m = mnew;
-  const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 8), p10 = pack8(s1, 0), p11 = pack8(s1, 8);
-  __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
-    const int col0 = 32 * dt;
-    oacc[dt] = mfma(tr_frag(vimg, lane, 0 + 4 * hh, 8 + 4 * hh, col0), p00, oacc[dt]);
-    oacc[dt] = mfma(tr_frag(vimg, lane, 16 + 4 * hh, 24 + 4 * hh, col0), p01, oacc[dt]);
-    oacc[dt] = mfma(tr_frag(vimg, lane, 32 + 4 * hh, 40 + 4 * hh, col0), p10, oacc[dt]);
-    oacc[dt] = mfma(tr_frag(vimg, lane, 48 + 4 * hh, 56 + 4 * hh, col0), p11, oacc[dt]);
-  }
-  __builtin_amdgcn_s_setprio(0);
-}
-
-__global__ __launch_bounds__(256, 2) void attn_fwd2n_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
-                                                            const u16* __restrict__ v, u16* __restrict__ o,
-                                                            float* __restrict__ lse2, int H, int Hkv, int S, float c) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BK * D * 2];  // [buf][K image | V image]
-  const int t = threadIdx.x, lane = t & 63, r = lane & 31, hh = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int nqb = gridDim.y;
-  const int qb = nqb - 1 - blockIdx.y;  // heaviest first
-  const int bh = xcd_head(blockIdx.x, gridDim.x), b = bh / H, hq = bh % H, hk = hq / (H / Hkv);
-  const u16* qp = q + ((size_t)(b * H + hq) * S) * D;
-  const size_t kvoff = ((size_t)(b * Hkv + hk) * S) * D;
-  const int q0 = qb * BQ + w * 32;
-  const int myq = q0 + r;
-
-  bf16x8 qf[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + (size_t)myq * D + 16 * s + 8 * hh);
-
-  f32x16 oacc[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) oacc[dt] = f32x16{};
-  float m = -INFINITY, l = 0.f;
-
-  const int ntiles = (qb * BQ + BQ) / BK;
-  const KVStage stage(k + kvoff, v + kvoff, S, w, lane);
-  auto tile = [&](int kt, bool masked) {
-    const char* kimg = smem + (kt & 1) * (2 * BK * D * 2);
-    char* nimg = smem + ((kt + 1) & 1) * (2 * BK * D * 2);
-    if (masked)
-      fwd_tile_na<true>(kimg, kimg + BK * D * 2, nimg, kt + 1 < ntiles, stage, kt, qf, oacc, m, l, lane, r, hh, myq, c);
-    else
-      fwd_tile_na<false>(kimg, kimg + BK * D * 2, nimg, kt + 1 < ntiles, stage, kt, qf, oacc, m, l, lane, r, hh, myq, c);
-  };
-  stage.load(0, smem);
-  dma_sync();
-  int kt = 0;
-  for (; kt < ntiles - 2; ++kt) {
-    tile(kt, false);
-    dma_sync();
-  }
-  for (; kt < ntiles; ++kt) {
-    const int key0 = kt * BK;
-    if (key0 <= q0 + 31) {
-      tile(kt, key0 + BK - 1 > q0);
-    } else if (kt + 1 < ntiles) {
-      stage.load(kt + 1, smem + ((kt + 1) & 1) * (2 * BK * D * 2));
-    }
-    dma_sync();
-  }
-  const float inv = 1.f / l;
-  u16* orow = o + (((size_t)b * S + myq) * (size_t)(H) + hq) * D;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      u16x4 v4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v4[e] = f2bf(oacc[dt][4 * g4 + e] * inv);
-      *reinterpret_cast<u16x4*>(orow + 32 * dt + 8 * g4 + 4 * hh) = v4;
-    }
-  if (hh == 0) lse2[(size_t)(b * H + hq) * S + myq] = m + log2f(l);
-}
-
 // ==================================================================================== backward
 // delta[b, h, q] = sum_d dO[b, q, h, d] * O[b, q, h, d]   (one 16-lane group per row)
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
@@ -502,314 +374,40 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const u16* __restrict
   }
 }
 
-// ============================================================================ backward v2 (split)
+// delta as above, plus what dK/dV v7 starts its S / dP chains from: nls = -lse2 / c, ndl = -delta
+__global__ __launch_bounds__(256) void attn_bwd_pre7_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
+                                                            const float* __restrict__ lse2, float* __restrict__ delta,
+                                                            float* __restrict__ nls, float* __restrict__ ndl, int B, int H,
+                                                            int S, float inv_c) {
+  const int row = blockIdx.x * 16 + (threadIdx.x >> 4);  // row = (b*S + s)*H + h
+  const int i = threadIdx.x & 15;
+  if (row >= B * S * H) return;
+  const u16x8 a = reinterpret_cast<const u16x8*>(dout + (size_t)row * D)[i];
+  const u16x8 bb = reinterpret_cast<const u16x8*>(out + (size_t)row * D)[i];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += bf2f(a[j]) * bf2f(bb[j]);
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) s += __shfl_xor(s, off, 16);
+  if (i == 0) {
+    const int h = row % H, bs = row / H, sidx = bs % S, bidx = bs / S;
+    const size_t o = ((size_t)bidx * H + h) * S + sidx;
+    delta[o] = s;
+    ndl[o] = -s;
+    nls[o] = -lse2[o] * inv_c;
+  }
+}
 
-// dK/dV v3.  The split dK/dV decomposition (one workgroup = 128 keys of one (batch,
-// kv-head), sweeping every q-head of the GQA group x 32-query slices, key on the lane), with the
-// slice stream made asynchronous and the LDS footprint cut so two workgroups still share a CU:
-//   * each lane's K row (the B operand of S = Q.K^T) lives in registers for the whole kernel
-//     (32 VGPRs), so only the V image stays in LDS (32 KiB);
-//   * Q, dO, lse and delta of a slice arrive by LDS-DMA into a double buffer (2 x 16.5 KiB), issued
-//     one slice ahead: one barrier per slice, no staging registers, no ds_write pass;
-//   * lse / delta are read per accumulator quad with ds_read_b128 (crow(4g..4g+3) are 4 consecutive
-//     queries) instead of 32 cross-lane shuffles;
-//   * only the first KB/QT slices of each q-head touch the block's diagonal: mask code runs there only.
+// ============================================================================ backward dK/dV
+// The split dK/dV decomposition: one workgroup = 128 keys of one (batch, kv-head), sweeping every q-head
+// of the GQA group x 32-query slices, key on the lane; each lane's K and V rows live in registers for
+// the whole kernel.  Q, dO, lse and delta of a slice arrive by LDS-DMA into a 3-slot ring, one slice
+// ahead, with one barrier per slice; lse / delta are read per accumulator quad with ds_read_b128
+// (crow(4g..4g+3) are 4 consecutive queries).  Only the first KB/QT slices of each q-head touch the
+// block's diagonal: mask code runs there only.  Earlier generations (v3: not pipelined, v4: operands
+// read at their use) and the A/B variants of v5 were retired in round 5; their bit-identity and
+// timing records are profiles/r04_attn, r04_maskbr, r04_split, r04_vpg.
 constexpr int SL_Q = 0, SL_DO = QT * D * 2, SL_LSE = 2 * QT * D * 2, SL_DEL = SL_LSE + 256, SL_BYTES = SL_DEL + 256;
-
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv3_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
-                                                                const u16* __restrict__ v, const u16* __restrict__ dout,
-                                                                const float* __restrict__ lse2, const float* __restrict__ delta,
-                                                                u16* __restrict__ dk, u16* __restrict__ dv, int H, int Hkv,
-                                                                int S, float c, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * SL_BYTES];  // slice double buffer
-  char* sbuf = smem;
-  const int t = threadIdx.x, lane = t & 63, r = lane & 31, hh = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int kb = blockIdx.y;  // grid (B*Hkv, S/KB): key block 0 (the most query slices) of every head dispatches first
-  const int bk = xcd_head(blockIdx.x, gridDim.x), b = bk / Hkv, hk = bk % Hkv, G = H / Hkv;
-  const size_t kvoff = ((size_t)(b * Hkv + hk) * S + (size_t)kb * KB) * D;
-  const int krow = w * 32 + r, mykey = kb * KB + krow, kmin = kb * KB + w * 32;
-  bf16x8 kf[8], vf[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    kf[s] = *reinterpret_cast<const bf16x8*>(k + kvoff + (size_t)krow * D + 16 * s + 8 * hh);
-    vf[s] = *reinterpret_cast<const bf16x8*>(v + kvoff + (size_t)krow * D + 16 * s + 8 * hh);
-  }
-  f32x16 dvt[4], dkt[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) dvt[dt] = dkt[dt] = f32x16{};
-  const int qt0 = (kb * KB) / QT, nqt = S / QT - qt0, nslice = G * nqt;
-
-  // slice DMA: wave w brings rows 8w .. 8w+7 of the Q and dO images (2 + 2 x 1 KiB); waves 0 / 1 the
-  // 64 lse / delta values starting at the slice (the upper 32 are the next slice's or out of range).
-  const uint32_t qbytes = (uint32_t)((size_t)H * S * D * 2), dbytes = (uint32_t)((size_t)S * H * D * 2);
-  const auto qrs = __builtin_amdgcn_make_buffer_rsrc((void*)(q + (size_t)b * H * S * D), 0, qbytes, 0x00020000);
-  const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)(dout + (size_t)b * S * H * D), 0, dbytes, 0x00020000);
-  const auto lrs = __builtin_amdgcn_make_buffer_rsrc((void*)((w == 0 ? lse2 : delta) + (size_t)b * H * S), 0,
-                                                     (uint32_t)((size_t)H * S * 4), 0x00020000);
-  uint32_t qv[2], dvo[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int R = 8 * w + 4 * i + (lane >> 4);
-    const uint32_t ch16 = 16 * ((lane & 15) ^ (((R & 3) << 2) | ((R >> 2) & 3)));
-    qv[i] = (uint32_t)(R * D * 2) + ch16;
-    dvo[i] = (uint32_t)(R * H * D * 2) + ch16;
-  }
-  auto sload = [&](int idx, char* buf) {
-    const int hq = hk * G + idx / nqt, qbase = (qt0 + idx % nqt) * QT;
-    const uint32_t qs = (uint32_t)(((size_t)hq * S + qbase) * D * 2), ds = (uint32_t)(((size_t)qbase * H + hq) * D * 2);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (LDS_AS void*)(buf + SL_Q + (8 * w + 4 * i) * 256), 16, qv[i], qs, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, (LDS_AS void*)(buf + SL_DO + (8 * w + 4 * i) * 256), 16, dvo[i], ds, 0, 0);
-    }
-    if (w < 2)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, (LDS_AS void*)(buf + (w == 0 ? SL_LSE : SL_DEL)), 4, 4 * lane,
-                                               (uint32_t)(((size_t)hq * S + qbase) * 4), 0, 0);
-  };
-
-  auto slice = [&](int idx, char* buf, bool masked) {
-    const int qbase = (qt0 + idx % nqt) * QT;
-    const char* qimg = buf + SL_Q;
-    const char* doimg = buf + SL_DO;
-    f32x16 sacc = f32x16{}, dpacc = f32x16{};
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      sacc = mfma(lds_b128(qimg, swz(r, 2 * s + hh)), kf[s], sacc);
-      dpacc = mfma(lds_b128(doimg, swz(r, 2 * s + hh)), vf[s], dpacc);
-    }
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {  // accumulator quad g holds queries 8g + 4hh + {0..3}
-      const f32x4 lq = *reinterpret_cast<const f32x4*>(buf + SL_LSE + 4 * (8 * g + 4 * hh));
-      const f32x4 dq_ = *reinterpret_cast<const f32x4*>(buf + SL_DEL + 4 * (8 * g + 4 * hh));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int i = 4 * g + e;
-        float pv = fexp2(fmaf(sacc[i], c, -lq[e]));
-        if (masked && mykey > qbase + crow(i, hh)) pv = 0.f;
-        sacc[i] = pv;
-        dpacc[i] = pv * (dpacc[i] - dq_[e]);
-      }
-    }
-    const bf16x8 p0 = pack8(sacc, 0), p1 = pack8(sacc, 8), d0 = pack8(dpacc, 0), d1 = pack8(dpacc, 8);
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      dvt[dt] = mfma(tr_frag(doimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), p0, dvt[dt]);
-      dvt[dt] = mfma(tr_frag(doimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), p1, dvt[dt]);
-      dkt[dt] = mfma(tr_frag(qimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), d0, dkt[dt]);
-      dkt[dt] = mfma(tr_frag(qimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), d1, dkt[dt]);
-    }
-  };
-
-  sload(0, sbuf);
-  dma_sync();
-  for (int idx = 0; idx < nslice; ++idx) {
-    char* buf = sbuf + (idx & 1) * SL_BYTES;
-    if (idx + 1 < nslice) sload(idx + 1, sbuf + ((idx + 1) & 1) * SL_BYTES);  // buffer free since the last barrier
-    const int j = idx % nqt;  // scalar
-    if (j >= KB / QT) {
-      slice(idx, buf, false);  // every query of the slice is past the block's last key
-    } else if ((qt0 + j) * QT + QT - 1 >= kmin) {  // diagonal slice that reaches this wave's keys
-      slice(idx, buf, true);
-    }
-    dma_sync();
-  }
-  u16* dkrow = dk + ((size_t)(b * Hkv + hk) * S + mykey) * D;
-  u16* dvrow = dv + ((size_t)(b * Hkv + hk) * S + mykey) * D;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      u16x4 a4, b4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        a4[e] = f2bf(dkt[dt][4 * g4 + e] * scale);
-        b4[e] = f2bf(dvt[dt][4 * g4 + e]);
-      }
-      *reinterpret_cast<u16x4*>(dkrow + 32 * dt + 8 * g4 + 4 * hh) = a4;
-      *reinterpret_cast<u16x4*>(dvrow + 32 * dt + 8 * g4 + 4 * hh) = b4;
-    }
-}
-
-// dK/dV v4: dK/dV v3 software-pipelined across query slices.  PMC on v3 (profiles/r01_attention):
-// the MFMA pipe is busy ~27 % of the time and the kernel issues ~13 VALU per MFMA, because at one
-// wave per SIMD the softmax/dS VALU block of a slice sits between its S/dP MFMAs and its dV/dK
-// MFMAs with nothing to overlap it.  v4 defers each slice's dV^T/dK^T MFMAs by one slice: slice i's
-// softmax/dS VALU runs interleaved (sched_group_barrier) with slice i-1's dV/dK MFMAs, which need
-// only slice i-1's packed bf16 P/dS (16 VGPRs carried across iterations; a second S/dP accumulator
-// set would spill).  Slices rotate through a 3-buffer LDS ring (i-1 read by the deferred dV/dK
-// products, i by S/dP, i+1 in flight by LDS-DMA), still one barrier per slice.  Diagonal slices (the
-// first KB/QT of each q-head) and slices a wave skips take the unfused path.
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv4_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
-                                                                const u16* __restrict__ v, const u16* __restrict__ dout,
-                                                                const float* __restrict__ lse2, const float* __restrict__ delta,
-                                                                u16* __restrict__ dk, u16* __restrict__ dv, int H, int Hkv,
-                                                                int S, float c, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[3 * SL_BYTES];  // slice ring
-  const int t = threadIdx.x, lane = t & 63, r = lane & 31, hh = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int kb = blockIdx.y;
-  const int bk = xcd_head(blockIdx.x, gridDim.x), b = bk / Hkv, hk = bk % Hkv, G = H / Hkv;
-  const size_t kvoff = ((size_t)(b * Hkv + hk) * S + (size_t)kb * KB) * D;
-  const int krow = w * 32 + r, mykey = kb * KB + krow, kmin = kb * KB + w * 32;
-  bf16x8 kf[8], vf[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    kf[s] = *reinterpret_cast<const bf16x8*>(k + kvoff + (size_t)krow * D + 16 * s + 8 * hh);
-    vf[s] = *reinterpret_cast<const bf16x8*>(v + kvoff + (size_t)krow * D + 16 * s + 8 * hh);
-  }
-  f32x16 dvt[4], dkt[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) dvt[dt] = dkt[dt] = f32x16{};
-  const int qt0 = (kb * KB) / QT, nqt = S / QT - qt0, nslice = G * nqt;
-
-  const uint32_t qbytes = (uint32_t)((size_t)H * S * D * 2), dbytes = (uint32_t)((size_t)S * H * D * 2);
-  const auto qrs = __builtin_amdgcn_make_buffer_rsrc((void*)(q + (size_t)b * H * S * D), 0, qbytes, 0x00020000);
-  const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)(dout + (size_t)b * S * H * D), 0, dbytes, 0x00020000);
-  const auto lrs = __builtin_amdgcn_make_buffer_rsrc((void*)((w == 0 ? lse2 : delta) + (size_t)b * H * S), 0,
-                                                     (uint32_t)((size_t)H * S * 4), 0x00020000);
-  uint32_t qv[2], dvo[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int R = 8 * w + 4 * i + (lane >> 4);
-    const uint32_t ch16 = 16 * ((lane & 15) ^ (((R & 3) << 2) | ((R >> 2) & 3)));
-    qv[i] = (uint32_t)(R * D * 2) + ch16;
-    dvo[i] = (uint32_t)(R * H * D * 2) + ch16;
-  }
-  auto ring = [&](int idx) -> char* { return smem + (idx % 3) * SL_BYTES; };
-  auto sload = [&](int idx) {
-    char* buf = ring(idx);
-    const int hq = hk * G + idx / nqt, qbase = (qt0 + idx % nqt) * QT;
-    const uint32_t qs = (uint32_t)(((size_t)hq * S + qbase) * D * 2), ds = (uint32_t)(((size_t)qbase * H + hq) * D * 2);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (LDS_AS void*)(buf + SL_Q + (8 * w + 4 * i) * 256), 16, qv[i], qs, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, (LDS_AS void*)(buf + SL_DO + (8 * w + 4 * i) * 256), 16, dvo[i], ds, 0, 0);
-    }
-    if (w < 2)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, (LDS_AS void*)(buf + (w == 0 ? SL_LSE : SL_DEL)), 4, 4 * lane,
-                                               (uint32_t)(((size_t)hq * S + qbase) * 4), 0, 0);
-  };
-  // slice state: does this wave compute slice idx at all, and does it need the causal mask there
-  auto active = [&](int idx) {
-    const int j = idx % nqt;
-    return j >= KB / QT || (qt0 + j) * QT + QT - 1 >= kmin;
-  };
-  auto masked = [&](int idx) { return idx % nqt < KB / QT; };
-
-  // S and dP of one slice (key on the lane, 32 queries in registers)
-  auto sdp = [&](const char* buf, f32x16& sacc, f32x16& dpacc) {
-    const char* qimg = buf + SL_Q;
-    const char* doimg = buf + SL_DO;
-    sacc = f32x16{};
-    dpacc = f32x16{};
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      sacc = mfma(lds_b128(qimg, swz(r, 2 * s + hh)), kf[s], sacc);
-      dpacc = mfma(lds_b128(doimg, swz(r, 2 * s + hh)), vf[s], dpacc);
-    }
-  };
-  struct Packs {  // bf16 B operands of dV^T (P) and dK^T (dS) for one slice
-    bf16x8 p0, p1, d0, d1;
-  };
-  // dV^T += dO^T.P and dK^T += Q^T.dS (dO^T, Q^T by transposed LDS reads of the slice's images)
-  auto dvdk = [&](const char* buf, const Packs& pk) {
-    const char* qimg = buf + SL_Q;
-    const char* doimg = buf + SL_DO;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      dvt[dt] = mfma(tr_frag(doimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), pk.p0, dvt[dt]);
-      dvt[dt] = mfma(tr_frag(doimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), pk.p1, dvt[dt]);
-      dkt[dt] = mfma(tr_frag(qimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), pk.d0, dkt[dt]);
-      dkt[dt] = mfma(tr_frag(qimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), pk.d1, dkt[dt]);
-    }
-  };
-
-  // Iteration idx, one basic block: S/dP of slice idx (MFMA); then its softmax/dS (VALU) interleaved
-  // with the dV/dK MFMAs of slice idx-1, whose bf16 operands (16 VGPRs) were packed one iteration
-  // earlier.  No branches: a slice this wave would skip (all its queries precede the wave's keys)
-  // runs with P = 0 (adds exact zeros), the causal mask is a select, and the first iteration's
-  // deferred products use zero packs.  With one MFMA path the accumulators stay put: v3's two
-  // inlined paths made the register allocator copy all 128 dK/dV accumulators VGPR -> AGPR on
-  // every slice (v_accvgpr_write x 128 in the .s).
-  Packs prev{};
-  {  // ring(2) is what the first iteration's deferred (zero-pack) products read: make it zeros, not
-     // whatever bits the LDS held (0 x NaN would poison the accumulators)
-    u16x8* z = reinterpret_cast<u16x8*>(smem + 2 * SL_BYTES);
-    for (int i = t; i < SL_BYTES / 16; i += 256) z[i] = u16x8{};
-  }
-  __syncthreads();
-  sload(0);
-  dma_sync();
-  // One slice; `rb` = ring slot of slice idx, a constant at every call site (the loop is unrolled by
-  // the ring length), so every LDS address is a hoisted per-lane offset plus an immediate.
-  auto step = [&](int idx, const int rb) {
-    // ring slot rb landed at the last barrier; slot (rb+1)%3 = slice idx-2's, read by the dV/dK
-    // products of the previous step, takes slice idx+1; slot (rb+2)%3 (slice idx-1) stays intact
-    if (idx + 1 < nslice) sload(idx + 1);
-    const int j = idx % nqt;
-    const int qbase = (qt0 + j) * QT;
-    const bool dead = !active(idx);  // wave-uniform
-    const int kill_from = dead ? -(1 << 30) : (masked(idx) ? qbase : 1 << 30);  // key - query > kill_from -> P = 0
-    const char* buf = smem + rb * SL_BYTES;
-    f32x16 sacc, dpacc;
-    sdp(buf, sacc, dpacc);
-    __builtin_amdgcn_sched_barrier(0);
-    Packs cur;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4 lq = *reinterpret_cast<const f32x4*>(buf + SL_LSE + 4 * (8 * g + 4 * hh));
-      const f32x4 dq_ = *reinterpret_cast<const f32x4*>(buf + SL_DEL + 4 * (8 * g + 4 * hh));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int i = 4 * g + e;
-        float pv = fexp2(fmaf(sacc[i], c, -lq[e]));
-        pv = (mykey - crow(i, hh) > kill_from) ? 0.f : pv;
-        sacc[i] = pv;
-        dpacc[i] = pv * (dpacc[i] - dq_[e]);
-      }
-    }
-    cur = Packs{pack8(sacc, 0), pack8(sacc, 8), pack8(dpacc, 0), pack8(dpacc, 8)};
-    dvdk(smem + ((rb + 2) % 3) * SL_BYTES, prev);  // slice idx-1; at idx = 0 zero packs on zeros
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {  // {1 dV/dK MFMA, 2 transposed reads, 12 softmax VALU} x 16
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    prev = cur;
-    dma_sync();
-  };
-  int idx = 0;
-  for (; idx + 3 <= nslice; idx += 3) {
-    step(idx, 0);
-    step(idx + 1, 1);
-    step(idx + 2, 2);
-  }
-  if (idx < nslice) step(idx, 0);
-  if (idx + 1 < nslice) step(idx + 1, 1);
-  switch ((nslice - 1) % 3) {  // the last slice's deferred dV/dK products
-    case 0: dvdk(smem, prev); break;
-    case 1: dvdk(smem + SL_BYTES, prev); break;
-    default: dvdk(smem + 2 * SL_BYTES, prev); break;
-  }
-  u16* dkrow = dk + ((size_t)(b * Hkv + hk) * S + mykey) * D;
-  u16* dvrow = dv + ((size_t)(b * Hkv + hk) * S + mykey) * D;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      u16x4 a4, b4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        a4[e] = f2bf(dkt[dt][4 * g4 + e] * scale);
-        b4[e] = f2bf(dvt[dt][4 * g4 + e]);
-      }
-      *reinterpret_cast<u16x4*>(dkrow + 32 * dt + 8 * g4 + 4 * hh) = a4;
-      *reinterpret_cast<u16x4*>(dvrow + 32 * dt + 8 * g4 + 4 * hh) = b4;
-    }
-}
 
 // dK/dV v5: v4 with its LDS operands read AHEAD, into registers, before the next slice's LDS-DMA
 // is issued.  The v4 ISA (hipcc -S, ROCm 7.2) showed one wave per SIMD (460 VGPR+AGPR) waiting on
@@ -1040,107 +638,266 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv5_kernel(const u16* __res
     }
 }
 
-// dQ v2: the forward-shaped dQ kernel restructured like forward v2 — LDS-DMA double-buffered K/V tiles with
-// one barrier per tile, the block's diagonal tiles peeled out of a branch-free main loop, LPT +
-// XCD-grouped grid (B*H, S/128).  (Forcing the fragment reads ahead with sched_group_barrier spills
-// inside the loop here: Q, dO, 4 accumulators and dQ^T already hold 192 VGPRs.)
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
-                                                              const u16* __restrict__ v, const u16* __restrict__ dout,
-                                                              const float* __restrict__ lse2, const float* __restrict__ delta,
-                                                              u16* __restrict__ dq, int H, int Hkv, int S, float c, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BK * D * 2];  // [buf][K image | V image]
+// dK/dV v7: v5's slice pipeline with the registers re-budgeted so that S and dP accumulate in VGPRs.
+// v5 (hipcc -S, ROCm 7.2) holds ~460 registers at one wave per SIMD: past 256 the compiler selects the
+// AGPR form for EVERY MFMA, so S / dP land in AGPRs and each slice pays ~100 v_accvgpr_read / write /
+// mov to bring them to the softmax VALU and back -- ~4 cycles each, on a wave whose VALU already fills
+// the MFMA gaps (profiles/r04_attn).  Here:
+//   * -lse/c and -delta enter as the S and dP chains' initial accumulators (the pre-kernel writes them
+//     negated and pre-divided): p = 2^(c * S') and dS = p * dP' need no lse / delta registers and no
+//     subtract;
+//   * the long-lived dV^T / dK^T accumulators (128 registers) are pinned in AGPRs by their MFMAs' asm
+//     constraints (kAsmAcc), so everything else -- K / V rows, the slice's operands, S / dP, the packs
+//     -- fits the 256 VGPRs and the S / dP MFMAs stay in VGPR form: no accumulator moves.
+template <bool kAsmAcc>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv7_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
+                                                                const u16* __restrict__ v, const u16* __restrict__ dout,
+                                                                const float* __restrict__ nls, const float* __restrict__ ndl,
+                                                                u16* __restrict__ dk, u16* __restrict__ dv, int H, int Hkv,
+                                                                int S, float c, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[3 * SL_BYTES];  // slice ring
   const int t = threadIdx.x, lane = t & 63, r = lane & 31, hh = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int nqb = gridDim.y, qb = nqb - 1 - blockIdx.y;
-  const int bh = xcd_head(blockIdx.x, gridDim.x), b = bh / H, hq = bh % H, hk = hq / (H / Hkv);
-  const size_t kvoff = ((size_t)(b * Hkv + hk) * S) * D;
-  const int q0 = qb * BQ + w * 32, myq = q0 + r;
-  const u16* qrow = q + ((size_t)(b * H + hq) * S + myq) * D;
-  const u16* dorow = dout + (((size_t)b * S + myq) * H + hq) * D;
-  bf16x8 qf[8], df[8];
+  const int kb = blockIdx.y;
+  const int bk = xcd_head(blockIdx.x, gridDim.x), b = bk / Hkv, hk = bk % Hkv, G = H / Hkv;
+  const size_t kvoff = ((size_t)(b * Hkv + hk) * S + (size_t)kb * KB) * D;
+  const int krow = w * 32 + r, mykey = kb * KB + krow, kmin = kb * KB + w * 32;
+  bf16x8 kf[8], vf[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    qf[s] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s + 8 * hh);
-    df[s] = *reinterpret_cast<const bf16x8*>(dorow + 16 * s + 8 * hh);
+    kf[s] = *reinterpret_cast<const bf16x8*>(k + kvoff + (size_t)krow * D + 16 * s + 8 * hh);
+    vf[s] = *reinterpret_cast<const bf16x8*>(v + kvoff + (size_t)krow * D + 16 * s + 8 * hh);
   }
-  const float lse_q = lse2[(size_t)(b * H + hq) * S + myq], del_q = delta[(size_t)(b * H + hq) * S + myq];
-  f32x16 dqt[4];
+  f32x16 dvt[4], dkt[4];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) dqt[dt] = f32x16{};
-  const int ntiles = (qb * BQ + BQ) / BK;
-  const KVStage stage(k + kvoff, v + kvoff, S, w, lane);
+  for (int dt = 0; dt < 4; ++dt) dvt[dt] = dkt[dt] = f32x16{};
+  if (kAsmAcc)  // the zeroing writes settle before the first asm MFMA reads them as its accumulator
+    asm volatile("s_nop 1" : "+a"(dvt[0]), "+a"(dvt[1]), "+a"(dvt[2]), "+a"(dvt[3]), "+a"(dkt[0]), "+a"(dkt[1]), "+a"(dkt[2]),
+                 "+a"(dkt[3]));
+  const int qt0 = (kb * KB) / QT, nqt = S / QT - qt0, nslice = G * nqt;
 
-  auto tile = [&](int kt, bool masked) {
-    char* kimg = smem + (kt & 1) * (2 * BK * D * 2);
-    char* vimg = kimg + BK * D * 2;
-    const int key0 = kt * BK;
-    f32x16 s0 = f32x16{}, s1 = f32x16{}, e0 = f32x16{}, e1 = f32x16{};
-    __builtin_amdgcn_s_setprio(1);  // MFMA phases outrank the other wave's VALU phase (ping-pong)
+  const uint32_t qbytes = (uint32_t)((size_t)H * S * D * 2), dbytes = (uint32_t)((size_t)S * H * D * 2);
+  const auto qrs = __builtin_amdgcn_make_buffer_rsrc((void*)(q + (size_t)b * H * S * D), 0, qbytes, 0x00020000);
+  const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)(dout + (size_t)b * S * H * D), 0, dbytes, 0x00020000);
+  const auto lrs = __builtin_amdgcn_make_buffer_rsrc((void*)((w == 0 ? nls : ndl) + (size_t)b * H * S), 0,
+                                                     (uint32_t)((size_t)H * S * 4), 0x00020000);
+  uint32_t qv[2], dvo[2];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const bf16x8 k0 = lds_b128(kimg, swz(r, 2 * s + hh)), k1 = lds_b128(kimg, swz(32 + r, 2 * s + hh));
-      const bf16x8 v0 = lds_b128(vimg, swz(r, 2 * s + hh)), v1 = lds_b128(vimg, swz(32 + r, 2 * s + hh));
-      s0 = mfma(k0, qf[s], s0);
-      s1 = mfma(k1, qf[s], s1);
-      e0 = mfma(v0, df[s], e0);
-      e1 = mfma(v1, df[s], e1);
-    }
-    __builtin_amdgcn_s_setprio(0);
-    if (kt + 1 < ntiles) stage.load(kt + 1, smem + ((kt + 1) & 1) * (2 * BK * D * 2));  // lands under the dQ MFMAs
+  for (int i = 0; i < 2; ++i) {
+    const int R = 8 * w + 4 * i + (lane >> 4);
+    const uint32_t ch16 = 16 * ((lane & 15) ^ (((R & 3) << 2) | ((R >> 2) & 3)));
+    qv[i] = (uint32_t)(R * D * 2) + ch16;
+    dvo[i] = (uint32_t)(R * H * D * 2) + ch16;
+  }
+  // slices are walked in (q-head, query tile) order; (sh, sj) of a slice are stepped, not divided out
+  auto sload = [&](int sh, int sj, char* buf) {
+    const int hq = hk * G + sh, qbase = (qt0 + sj) * QT;
+    const uint32_t qs = (uint32_t)(((size_t)hq * S + qbase) * D * 2), ds = (uint32_t)(((size_t)qbase * H + hq) * D * 2);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float p0 = fexp2(fmaf(s0[i], c, -lse_q));
-      float p1 = fexp2(fmaf(s1[i], c, -lse_q));
-      if (masked) {
-        const int kk = key0 + crow(i, hh);
-        if (kk > myq) p0 = 0.f;
-        if (kk + 32 > myq) p1 = 0.f;
-      }
-      s0[i] = p0 * (e0[i] - del_q);
-      s1[i] = p1 * (e1[i] - del_q);
+    for (int i = 0; i < 2; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (LDS_AS void*)(buf + SL_Q + (8 * w + 4 * i) * 256), 16, qv[i], qs, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, (LDS_AS void*)(buf + SL_DO + (8 * w + 4 * i) * 256), 16, dvo[i], ds, 0, 0);
     }
-    const bf16x8 d00 = pack8(s0, 0), d01 = pack8(s0, 8), d10 = pack8(s1, 0), d11 = pack8(s1, 8);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      dqt[dt] = mfma(tr_frag(kimg, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), d00, dqt[dt]);
-      dqt[dt] = mfma(tr_frag(kimg, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), d01, dqt[dt]);
-      dqt[dt] = mfma(tr_frag(kimg, lane, 32 + 4 * hh, 40 + 4 * hh, 32 * dt), d10, dqt[dt]);
-      dqt[dt] = mfma(tr_frag(kimg, lane, 48 + 4 * hh, 56 + 4 * hh, 32 * dt), d11, dqt[dt]);
-    }
-    __builtin_amdgcn_s_setprio(0);
+    if (w < 2)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, (LDS_AS void*)(buf + (w == 0 ? SL_LSE : SL_DEL)), 4, 4 * lane,
+                                               (uint32_t)(((size_t)hq * S + qbase) * 4), 0, 0);
+  };
+  int cur_h = 0, cur_j = 0;  // this step's slice
+  // dV^T / dK^T += A . B: in AGPRs through the asm constraint (kAsmAcc), else the builtin
+  auto acc_mfma = [&](f32x16& acc, bf16x8 a, bf16x8 bb) {
+    if (kAsmAcc)
+      asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(bb));
+    else
+      acc = mfma(a, bb, acc);
+  };
+  struct Packs {
+    bf16x8 p0, p1, d0, d1;
   };
 
-  stage.load(0, smem);
+  Packs prev{};
+  {  // the first step's deferred products read ring(2): zeros, not stale LDS bits
+    u16x8* z = reinterpret_cast<u16x8*>(smem + 2 * SL_BYTES);
+    for (int i = t; i < SL_BYTES / 16; i += 256) z[i] = u16x8{};
+  }
+  __syncthreads();
+  sload(0, 0, smem);
   dma_sync();
-  int kt = 0;
-  for (; kt < ntiles - 2; ++kt) {
-    tile(kt, false);
-    dma_sync();
-  }
-  for (; kt < ntiles; ++kt) {
-    const int key0 = kt * BK;
-    if (key0 <= q0 + 31) {
-      tile(kt, key0 + BK - 1 > q0);
-    } else if (kt + 1 < ntiles) {
-      stage.load(kt + 1, smem + ((kt + 1) & 1) * (2 * BK * D * 2));
+  auto step = [&](int idx, const int rb) {
+    const char* buf = smem + rb * SL_BYTES;
+    const char* pbuf = smem + ((rb + 2) % 3) * SL_BYTES;  // slice idx-1 (its deferred dV/dK products)
+    // (1) this slice's rows and its -lse/c, -delta (the S / dP chains' initial accumulators)
+    bf16x8 qa[8], da[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      qa[s] = lds_b128(buf + SL_Q, swz(r, 2 * s + hh));
+      da[s] = lds_b128(buf + SL_DO, swz(r, 2 * s + hh));
     }
+    f32x16 sacc, dpacc;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(buf + SL_LSE + 4 * (8 * g + 4 * hh));
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(buf + SL_DEL + 4 * (8 * g + 4 * hh));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        sacc[4 * g + e] = l4[e];
+        dpacc[4 * g + e] = d4[e];
+      }
+    }
+    // (2) S' = S - lse/c and dP' = dP - delta, the previous slice's transposed reads between their MFMAs
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      sacc = mfma(qa[s], kf[s], sacc);
+      dpacc = mfma(da[s], vf[s], dpacc);
+    }
+    bf16x8 ta[16];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      ta[4 * dt + 0] = tr_frag(pbuf + SL_DO, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt);
+      ta[4 * dt + 1] = tr_frag(pbuf + SL_DO, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt);
+      ta[4 * dt + 2] = tr_frag(pbuf + SL_Q, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt);
+      ta[4 * dt + 3] = tr_frag(pbuf + SL_Q, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt);
+    }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // (3) the next slice's DMA: every LDS read of this step precedes it
+    const int nj = cur_j + 1 == nqt ? 0 : cur_j + 1, nh = cur_j + 1 == nqt ? cur_h + 1 : cur_h;
+    if (idx + 1 < nslice) sload(nh, nj, smem + ((rb + 1) % 3) * SL_BYTES);
+    __builtin_amdgcn_sched_barrier(0);
+    // (4) softmax / dS of this slice under the deferred dV/dK MFMAs of the previous one
+    // diagonal slices (the block's first KB/QT query tiles) mask from qbase; slices wholly above this
+    // wave's keys are dead (every score masked)
+    const int qbase = (qt0 + cur_j) * QT;
+    const bool dead = cur_j < KB / QT && qbase + QT - 1 < kmin;
+    const int kill_from = dead ? -(1 << 30) : (cur_j < KB / QT ? qbase : 1 << 30);
+    Packs cur;
+    if (kAsmAcc) {
+      // The dV/dK MFMAs are asm statements, which the scheduling-group barriers do not see; each gap's
+      // VALU is pinned between its two MFMAs instead: an empty asm right after MFMA i "writes" the
+      // gap's inputs and another right before MFMA i+1 "reads" its outputs (no instructions emitted).
+      float sp[16], dp[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sp[i] = sacc[i], dp[i] = dpacc[i];
+      auto M = [&](int i) {  // accumulators round-robin: an accumulator's two products are 4 MFMAs apart
+        const int dt = i & 3, part = i >> 2;
+        const int ti = 4 * dt + part;
+        f32x16& acc = part < 2 ? dvt[dt] : dkt[dt];
+        const bf16x8 bb = part == 0 ? prev.p0 : part == 1 ? prev.p1 : part == 2 ? prev.d0 : prev.d1;
+        acc_mfma(acc, ta[ti], bb);
+      };
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {  // gaps 0-7: p = 2^(c S') for two scores each (mul + exp: 24 cycles)
+        M(i);
+        pin2(sp[2 * i], sp[2 * i + 1]);
+        sp[2 * i] = fexp2(sp[2 * i] * c);
+        sp[2 * i + 1] = fexp2(sp[2 * i + 1] * c);
+        pin2(sp[2 * i], sp[2 * i + 1]);
+      }
+      M(8);  // gap 8: the causal mask (diagonal / dead slices only), P's two packs
+      pin16(sp);
+      if (kill_from != (1 << 30)) {  // wave-uniform
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sp[i] = (mykey - crow(i, hh) > kill_from) ? 0.f : sp[i];
+      }
+      cur.p0 = pack8a(sp, 0);
+      cur.p1 = pack8a(sp, 8);
+      pin_b(cur.p0, cur.p1);
+#pragma unroll
+      for (int i = 9; i < 13; ++i) {  // gaps 9-12: dS = p dP' for four scores each
+        M(i);
+        const int o = 4 * (i - 9);
+        pin4(dp[o], dp[o + 1], dp[o + 2], dp[o + 3]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dp[o + e] *= sp[o + e];
+        pin4(dp[o], dp[o + 1], dp[o + 2], dp[o + 3]);
+      }
+      M(13);  // gaps 13-14: dS's packs
+      pin4(dp[0], dp[1], dp[2], dp[3]);
+      pin4(dp[4], dp[5], dp[6], dp[7]);
+      cur.d0 = pack8a(dp, 0);
+      pin_b1(cur.d0);
+      M(14);
+      pin4(dp[8], dp[9], dp[10], dp[11]);
+      pin4(dp[12], dp[13], dp[14], dp[15]);
+      cur.d1 = pack8a(dp, 8);
+      pin_b1(cur.d1);
+      M(15);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[i] = fexp2(sacc[i] * c);
+      if (kill_from != (1 << 30)) {  // wave-uniform: a diagonal or dead slice
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[i] = (mykey - crow(i, hh) > kill_from) ? 0.f : sacc[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dpacc[i] = sacc[i] * dpacc[i];
+      cur = Packs{pack8(sacc, 0), pack8(sacc, 8), pack8(dpacc, 0), pack8(dpacc, 8)};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        acc_mfma(dvt[dt], ta[4 * dt + 0], prev.p0);
+        acc_mfma(dvt[dt], ta[4 * dt + 1], prev.p1);
+        acc_mfma(dkt[dt], ta[4 * dt + 2], prev.d0);
+        acc_mfma(dkt[dt], ta[4 * dt + 3], prev.d1);
+      }
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {  // {1 dV/dK MFMA, 5 softmax VALU} x 16
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    prev = cur;
+    cur_h = nh, cur_j = nj;
     dma_sync();
+  };
+  int idx = 0;
+  for (; idx + 3 <= nslice; idx += 3) {
+    step(idx, 0);
+    step(idx + 1, 1);
+    step(idx + 2, 2);
   }
-  u16* out = dq + ((size_t)(b * H + hq) * S + myq) * D;
+  if (idx < nslice) step(idx, 0);
+  if (idx + 1 < nslice) step(idx + 1, 1);
+  {  // the last slice's deferred dV/dK products
+    const char* pbuf = smem + ((nslice - 1) % 3) * SL_BYTES;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      acc_mfma(dvt[dt], tr_frag(pbuf + SL_DO, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), prev.p0);
+      acc_mfma(dvt[dt], tr_frag(pbuf + SL_DO, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), prev.p1);
+      acc_mfma(dkt[dt], tr_frag(pbuf + SL_Q, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), prev.d0);
+      acc_mfma(dkt[dt], tr_frag(pbuf + SL_Q, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), prev.d1);
+    }
+  }
+  if (kAsmAcc)  // asm MFMAs are invisible to the hazard recognizer: their results settle before the reads
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(dvt[0]), "+a"(dvt[1]), "+a"(dvt[2]), "+a"(dvt[3]), "+a"(dkt[0]),
+                 "+a"(dkt[1]), "+a"(dkt[2]), "+a"(dkt[3]));
+  u16* dkrow = dk + ((size_t)(b * Hkv + hk) * S + mykey) * D;
+  u16* dvrow = dv + ((size_t)(b * Hkv + hk) * S + mykey) * D;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
-      u16x4 a4;
+      u16x4 a4, b4;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) a4[e] = f2bf(dqt[dt][4 * g4 + e] * scale);
-      *reinterpret_cast<u16x4*>(out + 32 * dt + 8 * g4 + 4 * hh) = a4;
+      for (int e = 0; e < 4; ++e) {
+        a4[e] = f2bf(dkt[dt][4 * g4 + e] * scale);
+        b4[e] = f2bf(dvt[dt][4 * g4 + e]);
+      }
+      *reinterpret_cast<u16x4*>(dkrow + 32 * dt + 8 * g4 + 4 * hh) = a4;
+      *reinterpret_cast<u16x4*>(dvrow + 32 * dt + 8 * g4 + 4 * hh) = b4;
     }
 }
 
-// ---- dQ with the tile's LDS images as __restrict__ parameters (the default since round 4): the same
-// change as attn_fwd2n_kernel.  dq2's wait sat before the first transposed K read of the dQ MFMAs.
+// dQ: forward-shaped (query on the lane), dQ^T += K^T.dS^T accumulated in registers; LDS-DMA
+// double-buffered K/V tiles with one barrier per tile, the block's diagonal tiles peeled out of a
+// branch-free main loop, LPT + XCD-grouped grid (B*H, S/128).  The tile's LDS images are __restrict__
+// parameters of an inlined function, so the compiler's LDS-DMA wait tracking sees the reads and the
+// next tile's DMA as disjoint and puts no mid-tile wait in front of the first transposed K read (the
+// round-3 dq2 did; 1.2 % slower whole backward at B 4, profiles/r04_attn).  The ordering the double
+// buffer needs is dma_sync()'s explicit vmcnt(0) lgkmcnt(0) + barrier at the end of every tile.
 template <bool kMasked>
 __device__ __forceinline__ void dq_tile_na(const char* __restrict__ kimg, const char* __restrict__ vimg,
                                            char* __restrict__ nimg, bool prefetch, const KVStage& stage, int kt,
@@ -1261,19 +1018,14 @@ void check_qkv(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
   TORCH_CHECK(q.size(1) * q.size(2) * D * 2 < (int64_t(1) << 31), "attention: per-batch q/dO bytes must fit the 32-bit buffer offsets");
 }
 
-std::vector<at::Tensor> attn_fwd_variant(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale,
-                                         bool noalias, bool with_t = false) {
+// forward (fwd2); with_t: also O^T [H*D, B*S] (the o-projection's NT-layout x^T) from the epilogue
+std::vector<at::Tensor> attn_fwd_impl(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale,
+                                      bool with_t) {
   check_qkv(q, k, v);
   const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
   auto o = at::empty({B, S, H, D}, q.options());
   auto lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
   const float c = (float)(scale * 1.4426950408889634);
-  if (noalias) {
-    TORCH_CHECK(!with_t, "attention: O^T is written by the default (fwd2) kernel only");
-    hipLaunchKernelGGL(attn_fwd2n_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bpm(o),
-                       lse.data_ptr<float>(), H, Hkv, S, c);
-    return {o, lse};
-  }
   at::Tensor ot;
   if (with_t) ot = at::empty({(int64_t)H * D, (int64_t)B * S}, q.options());
   hipLaunchKernelGGL(attn_fwd2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bpm(o),
@@ -1282,25 +1034,17 @@ std::vector<at::Tensor> attn_fwd_variant(const at::Tensor& q, const at::Tensor& 
   return {o, lse};
 }
 
-// default forward that also writes O^T [H*D, B*S] (the o-projection's NT-layout x^T): {o, lse, ot}
+// {o, lse, ot}
 std::vector<at::Tensor> attn_fwd_t(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale) {
-  return attn_fwd_variant(q, k, v, scale, false, true);
+  return attn_fwd_impl(q, k, v, scale, true);
 }
 
-// default forward: fwd2.  fwd2n (no mid-tile DMA wait) computes the same bits but measured 1.4-2 %
-// slower on MI355X (profiles/r04_attn: the wait costs nothing -- the DMA has landed during the
-// softmax -- and fwd2n spills 9 VGPRs in its peeled diagonal tiles)
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale) {
-  return attn_fwd_variant(q, k, v, scale, false);
+  return attn_fwd_impl(q, k, v, scale, false);
 }
 
-// fwd2n (LDS images as __restrict__ tile parameters, no mid-tile DMA wait): A/B reference, bit-identical
-std::vector<at::Tensor> attn_fwd_noalias(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale) {
-  return attn_fwd_variant(q, k, v, scale, true);
-}
-
-// v3 dK/dV (kept for A/B: v4 must match it bit for bit) + dQ v2
-std::vector<at::Tensor> attn_bwd_v3(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+// backward v5: delta, dK/dV v5, dQ (round-4 default; A/B reference for v7)
+std::vector<at::Tensor> attn_bwd_v5(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                     const at::Tensor& out, const at::Tensor& lse, double scale) {
   check_qkv(q, k, v);
   const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
@@ -1312,88 +1056,43 @@ std::vector<at::Tensor> attn_bwd_v3(const at::Tensor& dout, const at::Tensor& q,
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
                      delta.data_ptr<float>(), B, H, S);
   const float c = (float)(scale * 1.4426950408889634);
-  hipLaunchKernelGGL(attn_bwd_dkdv3_kernel, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
-                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
-  hipLaunchKernelGGL(attn_bwd_dq2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
+  hipLaunchKernelGGL(attn_bwd_dkdv5_kernel<true>, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v),
+                     bp(dout), lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
+  hipLaunchKernelGGL(attn_bwd_dq2n_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
                      lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
-  return {dq, dk, dv};
-}
-
-// v4 dK/dV (LDS operands read at their use, under the next slice's DMA) + dQ v2: A/B reference for v5
-std::vector<at::Tensor> attn_bwd_v4(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                    const at::Tensor& out, const at::Tensor& lse, double scale) {
-  check_qkv(q, k, v);
-  const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
-  TORCH_CHECK(dout.is_contiguous() && out.is_contiguous() && dout.numel() == q.numel() && out.numel() == q.numel(),
-              "attention bwd: dout/out must be contiguous [B, S, H, D]");
-  auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
-  auto dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
-  const int rows = B * S * H;
-  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
-                     delta.data_ptr<float>(), B, H, S);
-  const float c = (float)(scale * 1.4426950408889634);
-  hipLaunchKernelGGL(attn_bwd_dkdv4_kernel, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
-                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
-  hipLaunchKernelGGL(attn_bwd_dq2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
-                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
-  return {dq, dk, dv};
-}
-
-// default backward: delta, dK/dV v5 (software-pipelined slices, operands read ahead of the DMA), dQ v2
-std::vector<at::Tensor> attn_bwd_order(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                       const at::Tensor& out, const at::Tensor& lse, double scale, bool s_first,
-                                       bool dq_noalias = true, bool mask_branch = true) {
-  check_qkv(q, k, v);
-  const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
-  TORCH_CHECK(dout.is_contiguous() && out.is_contiguous() && dout.numel() == q.numel() && out.numel() == q.numel(),
-              "attention bwd: dout/out must be contiguous [B, S, H, D]");
-  auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
-  auto dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
-  const int rows = B * S * H;
-  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
-                     delta.data_ptr<float>(), B, H, S);
-  const float c = (float)(scale * 1.4426950408889634);
-  if (s_first && !mask_branch)
-    hipLaunchKernelGGL((attn_bwd_dkdv5_kernel<true, false>), dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k),
-                       bp(v), bp(dout), lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c,
-                       (float)scale);
-  else if (s_first)
-    hipLaunchKernelGGL(attn_bwd_dkdv5_kernel<true>, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v),
-                       bp(dout), lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
-  else
-    hipLaunchKernelGGL(attn_bwd_dkdv5_kernel<false>, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v),
-                       bp(dout), lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
-  if (dq_noalias)
-    hipLaunchKernelGGL(attn_bwd_dq2n_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
-                       lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
-  else
-    hipLaunchKernelGGL(attn_bwd_dq2_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
-                       lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
   return {dq, dk, dv};
 }
 
 std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                  const at::Tensor& out, const at::Tensor& lse, double scale) {
-  return attn_bwd_order(dout, q, k, v, out, lse, scale, true);
+  return attn_bwd_v5(dout, q, k, v, out, lse, scale);
 }
 
-// default backward with the per-score causal select on every slice (round 3 / early round 4): A/B reference, bit-identical
-std::vector<at::Tensor> attn_bwd_v5m0(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                      const at::Tensor& out, const at::Tensor& lse, double scale) {
-  return attn_bwd_order(dout, q, k, v, out, lse, scale, true, true, false);
-}
-
-// default order with the round-3 dQ (dq2: one-array images, mid-tile DMA wait): A/B reference, bit-identical.
-// The default dQ is dq2n: 1.2 % faster whole backward at B 4 x 4096, equal at B 2 (profiles/r04_attn)
-std::vector<at::Tensor> attn_bwd_dq_alias(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                          const at::Tensor& out, const at::Tensor& lse, double scale) {
-  return attn_bwd_order(dout, q, k, v, out, lse, scale, true, false);
-}
-
-// v5 with the previous slice's transposed reads issued first (the round-3 order): A/B reference
-std::vector<at::Tensor> attn_bwd_v5t(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                     const at::Tensor& out, const at::Tensor& lse, double scale) {
-  return attn_bwd_order(dout, q, k, v, out, lse, scale, false);
+// dK/dV v7 (S / dP in VGPRs, -lse/c and -delta as their chains' initial accumulators) + dQ
+std::vector<at::Tensor> attn_bwd_v7(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                    const at::Tensor& out, const at::Tensor& lse, double scale, bool asm_acc) {
+  check_qkv(q, k, v);
+  const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
+  TORCH_CHECK(dout.is_contiguous() && out.is_contiguous() && dout.numel() == q.numel() && out.numel() == q.numel(),
+              "attention bwd: dout/out must be contiguous [B, S, H, D]");
+  TORCH_CHECK(lse.is_contiguous() && lse.numel() == (int64_t)B * H * S, "attention bwd: lse must be [B, H, S]");
+  auto fopt = q.options().dtype(at::kFloat);
+  auto delta = at::empty({B, H, S}, fopt), nls = at::empty({B, H, S}, fopt), ndl = at::empty({B, H, S}, fopt);
+  auto dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
+  const int rows = B * S * H;
+  const float c = (float)(scale * 1.4426950408889634);
+  hipLaunchKernelGGL(attn_bwd_pre7_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
+                     lse.data_ptr<float>(), delta.data_ptr<float>(), nls.data_ptr<float>(), ndl.data_ptr<float>(), B, H, S,
+                     1.f / c);
+  if (asm_acc)
+    hipLaunchKernelGGL(attn_bwd_dkdv7_kernel<true>, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v),
+                       bp(dout), nls.data_ptr<float>(), ndl.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
+  else
+    hipLaunchKernelGGL(attn_bwd_dkdv7_kernel<false>, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v),
+                       bp(dout), nls.data_ptr<float>(), ndl.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
+  hipLaunchKernelGGL(attn_bwd_dq2n_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
+                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
+  return {dq, dk, dv};
 }
 
 }  // namespace gtk_attn

@@ -1376,20 +1376,13 @@ at::Tensor xent10_bwd(const at::Tensor& dlog, const at::Tensor& g, at::Tensor& g
 
 namespace gtk_attn {  // csrc/ops/attention.hip
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale);
-std::vector<at::Tensor> attn_fwd_noalias(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale);
 std::vector<at::Tensor> attn_fwd_t(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale);
-std::vector<at::Tensor> attn_bwd_v5m0(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                      const at::Tensor& out, const at::Tensor& lse, double scale);
-std::vector<at::Tensor> attn_bwd_dq_alias(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                          const at::Tensor& out, const at::Tensor& lse, double scale);
 std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                  const at::Tensor& out, const at::Tensor& lse, double scale);
-std::vector<at::Tensor> attn_bwd_v4(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+std::vector<at::Tensor> attn_bwd_v5(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                     const at::Tensor& out, const at::Tensor& lse, double scale);
-std::vector<at::Tensor> attn_bwd_v5t(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                     const at::Tensor& out, const at::Tensor& lse, double scale);
-std::vector<at::Tensor> attn_bwd_v3(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                    const at::Tensor& out, const at::Tensor& lse, double scale);
+std::vector<at::Tensor> attn_bwd_v7(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                    const at::Tensor& out, const at::Tensor& lse, double scale, bool asm_acc);
 }  // namespace gtk_attn
 
 namespace gtk_xpose {  // csrc/ops/transpose.hip
@@ -1411,12 +1404,8 @@ PYBIND11_MODULE(_fused, m) {
   m.def("attn_fwd", &gtk_attn::attn_fwd, "causal GQA flash attention forward (bf16, D=128): -> (o [B,S,H,D], lse2 [B,H,S])");
   m.def("attn_fwd_t", &gtk_attn::attn_fwd_t, "attn_fwd that also writes O^T [H*D, B*S]: -> (o, lse2, ot)");
   m.def("attn_bwd", &gtk_attn::attn_bwd, "flash attention backward: -> (dq, dk, dv)");
-  m.def("attn_fwd_noalias", &gtk_attn::attn_fwd_noalias, "forward fwd2n (no mid-tile DMA wait; A/B reference, bit-identical to the default fwd2)");
-  m.def("attn_bwd_dq_alias", &gtk_attn::attn_bwd_dq_alias, "default backward with the round-3 dQ dq2 (A/B reference, bit-identical)");
-  m.def("attn_bwd_v5m0", &gtk_attn::attn_bwd_v5m0, "default backward with the per-score causal select on every slice (A/B reference, bit-identical)");
-  m.def("attn_bwd_v5t", &gtk_attn::attn_bwd_v5t, "v5 with the transposed reads issued first (A/B reference for the default order)");
-  m.def("attn_bwd_v4", &gtk_attn::attn_bwd_v4, "v4 backward (dK/dV LDS operands read at their use; A/B reference for the default v5)");
-  m.def("attn_bwd_v3", &gtk_attn::attn_bwd_v3, "v3 backward (dK/dV not pipelined across slices; A/B reference for v4)");
+  m.def("attn_bwd_v5", &gtk_attn::attn_bwd_v5, "backward with dK/dV v5 (round-4 default; A/B reference)");
+  m.def("attn_bwd_v7", &gtk_attn::attn_bwd_v7, "backward with dK/dV v7 (S / dP in VGPRs; asm_acc: dV/dK accumulators pinned to AGPRs)");
   m.doc() = "gfx950 fused kernels for the Llama-3 DP validation workload";
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);

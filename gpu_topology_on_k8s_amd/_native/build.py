@@ -26,7 +26,7 @@ import sys
 import sysconfig
 from dataclasses import dataclass, field
 from pathlib import Path
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 HERE = Path(__file__).resolve().parent
 REPO = HERE.parent.parent
@@ -75,6 +75,7 @@ class Target:
     pybind: bool = True
     torch: bool = False
     shared: bool = True
+    src_flags: Dict[str, List[str]] = field(default_factory=dict)  # extra compile flags per source file name
 
     def command(self) -> List[str]:
         if self.compiler == "hipcc":
@@ -157,8 +158,13 @@ def targets() -> List[Target]:
                 f"-L{HERE / 'bin' / 'fake_hip'}", "-l:libamdhip64.so", "-l:libhsa-runtime64.so", "-Wl,--disable-new-dtags",
                 f"-Wl,-rpath,{HERE / 'bin' / 'fake_hip'}"],
                deps=[HERE / "bin" / "fake_hip" / "libamdhip64.so"], pybind=False, shared=False),
+        # attention.hip: MFMAs whose accumulators the code does not pin to AGPRs take the VGPR form even in
+        # the one-wave-per-SIMD dK/dV kernel (its S / dP chains feed the softmax VALU directly; the dV/dK
+        # accumulators are pinned to AGPRs by their asm constraints).  The other kernels of the file fit
+        # 256 VGPRs and select that form anyway.
         Target("_fused", sorted((CSRC / "ops").glob("*.hip")), "hipcc", HERE / f"_fused{EXT}",
-               deps=sorted((CSRC / "ops").glob("*.h")), pybind=True, torch=True),
+               deps=sorted((CSRC / "ops").glob("*.h")), pybind=True, torch=True,
+               src_flags={"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}),
     ]
 
 
@@ -185,7 +191,7 @@ def _build_objects(t: Target, force: bool, verbose: bool, jobs: int) -> str:
     def one(src: Path) -> Path:
         obj = odir / (src.stem + ".o")
         if force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, dep_t):
-            _run(flags + ["-c", str(src), "-o", str(obj)], f"{t.name}:{src.name}", verbose)
+            _run(flags + t.src_flags.get(src.name, []) + ["-c", str(src), "-o", str(obj)], f"{t.name}:{src.name}", verbose)
         return obj
 
     with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(t.sources)))) as ex:

@@ -12,14 +12,15 @@ MI355X-first layout:
   * fused QKV and gate|up projections -> hipBLASLt GEMMs; everything between GEMMs is a fused HIP
     kernel (RMSNorm, RoPE + head split, SwiGLU, cross-entropy with in-place dlogits);
   * backward GEMMs in the forward GEMM's "NT" layout (``gemm_layout="nt"``): dgrad as
-    ``dy (W^T)^T`` and wgrad as ``(dy^T)(x^T)^T``, the operands transposed by the LDS-tiled HIP
-    kernel (``ops.fused.transpose``) — hipBLASLt runs NT 10-40 % faster than the NN / TN layouts
-    autograd would hand it (bench/gemm_layout_bench.py).  ``overlap_transposes`` makes ``x^T`` and
-    ``W^T`` in the forward on a side HIP stream instead; measured on MI355X it does not pay (22.8k
-    vs 23.0k tok/s, +18 GB): the hipBLASLt GEMMs hold every CU, so the transposes only contend.
-    ``dgrad_nn`` computes the input gradient as ``dy W`` (NN, no per-step ``W^T``) for the named
-    projections; on MI355X every projection was slower that way, 1.4-4.7 ms per step each, even with
-    the NN shapes tuned (profiles/r03_layout/SUMMARY.md), so it is an A/B knob, off by default;
+    ``dy (W^T)^T`` and wgrad as ``(dy^T)(x^T)^T`` -- hipBLASLt runs NT 10-40 % faster than the NN / TN
+    layouts autograd would hand it (bench/gemm_layout_bench.py).  ``W^T`` stays resident and the
+    optimizer rewrites it with ``W``; the transposed activations come from their producer kernels
+    (SwiGLU ``h^T``, attention ``O^T``, RoPE-backward ``dqkv^T``, cross-entropy ``dlogits^T``) or from
+    the LDS-tiled HIP transpose (``ops.fused.transpose``) for the rest.  Alternatives measured flat or
+    slower on MI355X and retired in round 5 (records in profiles/ and docs/PERFORMANCE.md): transposes
+    on a side stream in forward (r01), NN input gradients (r03_layout), x^T made in the forward and
+    weight-gradient GEMMs on a side stream (r04_llama, r04_wgs), unfused residual adds (r01_fuse_res),
+    autograd-accumulated norm / embedding gradients (r04_flatgrad);
   * Llama-3-8B = 8.03 B params: 16 GB bf16 weights + 16 GB bf16 grads + 96 GB fp32 master/m/v =
     128 GB, leaving ~160 GB of the 288 GB HBM for activations, so DP alone suffices (no TP/PP/SP).
 """
@@ -148,14 +149,9 @@ class FlatParams:
         self._t_ver: Dict[str, int] = {}  # data._version when each W^T was last made valid
         self.t_refreshes = 0  # lazy W^T re-makes (transposes) since construction
         self._plan = None  # adamw_plan() cache
-        self.eager_xt = False  # NT layout: make x^T in the forward (Llama(transpose_x="forward"))
         # NT layout: producers that hold a tile in LDS write the transposed copy too (SwiGLU h^T,
-        # attention O^T, RoPE-backward dqkv^T, cross-entropy dlogits^T; Llama(transpose_x="fused"/"forward"))
+        # attention O^T, RoPE-backward dqkv^T, cross-entropy dlogits^T)
         self.producer_xt = False
-        # NT layout: each weight-gradient GEMM runs on a side stream, concurrently with its input-gradient
-        # GEMM on the main one (Llama(wgrad_stream=True)); joined at the end of the backward
-        self.wgrad_side: Optional["torch.cuda.Stream"] = None
-        self._join_queued = False
 
     # ---------------------------------------------------------------- persistent W^T
     def enable_transposed(self, names) -> List[str]:
@@ -249,7 +245,7 @@ class FlatParams:
 
         ``nt``: compute it as ``(dy^T)(x^T)^T`` from transposed copies, the GEMM layout hipBLASLt runs
         fastest (both operands contiguous along the token dimension being reduced); ``dy_t`` / ``x_t``
-        are transposed copies made elsewhere (SwiGLU backward; the forward's side stream)."""
+        are transposed copies their producer kernels wrote (SwiGLU backward, cross-entropy, RoPE)."""
         view = self.params[name].grad
         if nt:
             a = dy_t if dy_t is not None else fused.transpose(dy)
@@ -264,31 +260,22 @@ class FlatParams:
         for fn in list(self._ready.get(name, ())):
             fn(self.params[name])
 
-    def write_grad_side(self, name: str, dy: torch.Tensor, x_t: Optional[torch.Tensor], dy_t: Optional[torch.Tensor]) -> None:
-        """:meth:`write_grad` (NT) issued on :attr:`wgrad_side` after everything the main stream has
-        queued, so the weight-gradient GEMM overlaps the input-gradient GEMM issued next on the main
-        stream: two GEMMs whose tile counts leave part of the last wave idle fill each other's tails.
-        The main stream waits for the side stream at the end of the backward (autograd callback)."""
-        main = torch.cuda.current_stream(dy.device)
-        side = self.wgrad_side
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            self.write_grad(name, dy, None, nt=True, x_t=x_t, dy_t=dy_t)
-        for t in (dy, x_t, dy_t):
-            if t is not None:
-                t.record_stream(side)  # freed by the main stream's owner while the side stream reads it
-        if not self._join_queued:
-            self._join_queued = True
+    def grad_target(self, name: str) -> Tuple[torch.Tensor, bool]:
+        """Where a kernel that writes ``name``'s whole gradient (norm / embedding backward) should write:
+        ``(view, True)`` -- the flat slot itself -- on the first write since :meth:`zero_grad`; after
+        that ``(scratch, False)``: the caller writes a scratch tensor and :meth:`mark_written` adds it
+        in, so a second backward before ``zero_grad`` accumulates as autograd would."""
+        view = self.params[name].grad
+        if self.direct.get(name, False):
+            return view, True
+        return torch.empty_like(view), False
 
-            def join():
-                main.wait_stream(side)
-                self._join_queued = False
-
-            torch.autograd.Variable._execution_engine.queue_callback(join)
-
-    def mark_written(self, name: str) -> None:
+    def mark_written(self, name: str, partial: Optional[torch.Tensor] = None) -> None:
         """A kernel wrote ``name``'s gradient into the flat buffer itself (not through
-        :meth:`write_grad`): clear its fresh flag and announce readiness (data-parallel buckets)."""
+        :meth:`write_grad`), or into ``partial`` (a :meth:`grad_target` scratch, added in here): clear
+        its fresh flag and announce readiness (data-parallel buckets)."""
+        if partial is not None:
+            self.params[name].grad.add_(partial)
         self.direct[name] = False
         for fn in list(self._ready.get(name, ())):
             fn(self.params[name])
@@ -342,76 +329,26 @@ class FlatParams:
         return o, o + math.prod(self.shapes[name])
 
 
-_SIDE_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
-
-
-def _side_stream(device: torch.device) -> "torch.cuda.Stream":
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    s = _SIDE_STREAMS.get(idx)
-    if s is None:
-        s = _SIDE_STREAMS[idx] = torch.cuda.Stream(device=idx)
-    return s
-
-
 class _NTOperands:
-    """``x^T`` and ``W^T`` of one forward GEMM for its NT-layout backward GEMMs.
+    """``x^T`` and ``W^T`` of one forward GEMM for its NT-layout backward GEMMs: ``x^T`` as its producer
+    kernel wrote it (``x_t``), else made from the kept ``x`` in backward by the HIP transpose; ``W^T``
+    the persistent copy (``wt_fn``, :meth:`FlatParams.weight_t`), else transposed in backward."""
 
-    Default: made in backward on the main stream, just before their GEMMs.  ``overlap``: issued in
-    the FORWARD on a side HIP stream right after the producer of ``x`` (memory-bound transposes
-    under the compute-bound forward GEMMs), ``x^T`` kept instead of ``x``.  Measured at Llama-3-8B
-    b4 x 4096 on one MI355X: 22.8k tok/s with overlap vs 23.0k without, and +18 GB peak (all W^T
-    live through backward) -- the GEMMs hold every CU, so the side stream only contends."""
-
-    def __init__(self, x: torch.Tensor, w: torch.Tensor, overlap: bool, dgrad_nn: bool = False,
-                 wt_fn: Optional[Callable[[], Optional[torch.Tensor]]] = None, eager_x: bool = False,
+    def __init__(self, x: torch.Tensor, w: torch.Tensor, wt_fn: Optional[Callable[[], Optional[torch.Tensor]]] = None,
                  x_t: Optional[torch.Tensor] = None):
-        self.event = None
-        self.dgrad_nn = dgrad_nn  # dgrad reads W as is (NN): no W^T is made
-        self.wt_fn = None if dgrad_nn else wt_fn  # the persistent W^T (FlatParams.weight_t): no per-step transpose
-        if overlap and x.is_cuda and not dgrad_nn and self.wt_fn is None:
-            main = torch.cuda.current_stream(x.device)
-            side = _side_stream(x.device)
-            side.wait_stream(main)  # x (and the optimizer's last write of w) are complete
-            with torch.cuda.stream(side):
-                self.x_t, self.w_t = fused.transpose(x), fused.transpose(w)
-            x.record_stream(side)  # x may be freed by the caller while the side stream still reads it
-            w.record_stream(side)
-            self.event = torch.cuda.Event()
-            self.event.record(side)
-            self.x, self.w = None, None
-        elif x_t is not None:  # its producer wrote x^T too (SwiGLU forward)
-            self.x_t, self.w_t = x_t, None
-            self.x, self.w = None, w
-        elif eager_x and x.is_cuda:
-            # x^T made in the forward, on the main stream, right after x's producer wrote it (still in
-            # the Infinity Cache): the backward finds it ready, and x itself is not kept
-            self.x_t, self.w_t = fused.transpose(x), None
-            self.x, self.w = None, w
-        else:
-            self.x_t = self.w_t = None
-            self.x, self.w = x, w
+        self.wt_fn = wt_fn
+        self.x_t = x_t
+        self.x = None if x_t is not None else x
+        self.w = w
 
     def get(self) -> Tuple[torch.Tensor, torch.Tensor]:
-        """-> (x^T, W^T), ready for use on the current stream (``W`` itself with ``dgrad_nn``)."""
-        if self.dgrad_nn:
-            if self.x_t is None:
-                self.x_t = fused.transpose(self.x)
-                self.x = None
-            return self.x_t, self.w
-        if self.event is not None:
-            main = torch.cuda.current_stream(self.x_t.device)
-            main.wait_event(self.event)
-            self.x_t.record_stream(main)  # allocated on the side stream, consumed on the main one
-            self.w_t.record_stream(main)
-            self.event = None
-        elif self.w_t is None:
-            if self.x_t is None:
-                self.x_t = fused.transpose(self.x)
-            self.w_t = self.wt_fn() if self.wt_fn is not None else None
-            if self.w_t is None:
-                self.w_t = fused.transpose(self.w)
-            self.x = self.w = None
-        return self.x_t, self.w_t
+        """-> (x^T, W^T), ready for use on the current stream."""
+        x_t = self.x_t if self.x_t is not None else fused.transpose(self.x)
+        w_t = self.wt_fn() if self.wt_fn is not None else None
+        if w_t is None:
+            w_t = fused.transpose(self.w)
+        self.x = self.w = self.x_t = None
+        return x_t, w_t
 
 
 def _wt_fn(flat: "FlatParams", name: str):
@@ -422,10 +359,10 @@ class _FlatLinear(torch.autograd.Function):
     """``y = x W^T`` whose weight gradient is written in place into the flat buffer."""
 
     @staticmethod
-    def forward(ctx, x, w, flat, name, nt, overlap, dgrad_nn=False, x_t=None):
-        ctx.flat, ctx.name, ctx.nt, ctx.dgrad_nn = flat, name, nt, dgrad_nn
+    def forward(ctx, x, w, flat, name, nt, x_t=None):
+        ctx.flat, ctx.name, ctx.nt = flat, name, nt
         if nt:
-            ctx.ops = _NTOperands(x, w, overlap, dgrad_nn, _wt_fn(flat, name), flat.eager_xt, x_t=x_t)
+            ctx.ops = _NTOperands(x, w, _wt_fn(flat, name), x_t=x_t)
         else:
             ctx.save_for_backward(x, w)
         return F.linear(x, w)
@@ -436,36 +373,28 @@ class _FlatLinear(torch.autograd.Function):
             x_t, w_t = ctx.ops.get()
             ctx.ops = None
             dy_t = fused.take_t(dy)  # dy^T written by dy's producer kernel (xent / RoPE backward), if any
-            side = ctx.flat.wgrad_side is not None and dy.is_cuda
-            if side:  # weight gradient first, on the side stream: it overlaps the input gradient below
-                ctx.flat.write_grad_side(ctx.name, dy, x_t, dy_t)
-            if not ctx.needs_input_grad[0]:
-                dx = None
-            elif ctx.dgrad_nn:
-                dx = dy.mm(w_t)  # w_t is W here: dy W (NN)
-            else:
-                dx = F.linear(dy, w_t)  # dy (W^T)^T
-            if not side:
-                ctx.flat.write_grad(ctx.name, dy, None, nt=True, x_t=x_t, dy_t=dy_t)
+            dx = F.linear(dy, w_t) if ctx.needs_input_grad[0] else None  # dy (W^T)^T
+            ctx.flat.write_grad(ctx.name, dy, None, nt=True, x_t=x_t, dy_t=dy_t)
         else:
             x, w = ctx.saved_tensors
             dx = dy.mm(w) if ctx.needs_input_grad[0] else None
             ctx.flat.write_grad(ctx.name, dy, x)
-        return dx, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None
 
 
 class _FlatLinearSwiGLU(torch.autograd.Function):
     """``silu(g) * u`` of ``[g | u] = x W13^T``: the gate|up projection and SwiGLU as one node, so the
     backward gets d[g | u] AND its transpose from one HIP kernel (``fused.swiglu_bwd_t``) and feeds
-    the transpose straight to the NT weight-gradient GEMM."""
+    the transpose straight to the NT weight-gradient GEMM; the forward kernel writes ``h^T`` for the
+    down projection's weight gradient."""
 
     @staticmethod
-    def forward(ctx, x, w, flat, name, nt, overlap, dgrad_nn=False):
+    def forward(ctx, x, w, flat, name, nt):
         ctx.set_materialize_grads(False)  # no zero-filled gradient for a^T (non-differentiable) in backward
         gu = F.linear(x, w)
-        ctx.flat, ctx.name, ctx.nt, ctx.dgrad_nn = flat, name, nt, dgrad_nn
+        ctx.flat, ctx.name, ctx.nt = flat, name, nt
         if nt:
-            ctx.ops = _NTOperands(x, w, overlap, dgrad_nn, _wt_fn(flat, name), flat.eager_xt)
+            ctx.ops = _NTOperands(x, w, _wt_fn(flat, name))
             ctx.save_for_backward(gu)
         else:
             ctx.save_for_backward(gu, x, w)
@@ -473,8 +402,7 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
         if not gu.is_cuda:
             a = fused.swiglu_ref(gu)
         elif nt and flat.producer_xt and gu.size(0) % 64 == 0 and (gu.size(1) // 2) % 64 == 0:
-            # the next projection's x^T from the same kernel (transpose_x="fused" / "forward")
-            a, a_t = fused.swiglu_fwd_t(gu)
+            a, a_t = fused.swiglu_fwd_t(gu)  # the next projection's x^T from the same kernel
             ctx.mark_non_differentiable(a_t)
         else:
             a = fused.hip().swiglu_fwd(gu)
@@ -487,23 +415,14 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
             dgu, dgu_t = fused.swiglu_bwd_t(da, gu)
             x_t, w_t = ctx.ops.get()
             ctx.ops = None
-            side = ctx.flat.wgrad_side is not None and dgu.is_cuda
-            if side:
-                ctx.flat.write_grad_side(ctx.name, dgu, x_t, dgu_t)
-            if not ctx.needs_input_grad[0]:
-                dx = None
-            elif ctx.dgrad_nn:
-                dx = dgu.mm(w_t)  # w_t is W here (NN)
-            else:
-                dx = F.linear(dgu, w_t)
-            if not side:
-                ctx.flat.write_grad(ctx.name, dgu, None, nt=True, dy_t=dgu_t, x_t=x_t)
+            dx = F.linear(dgu, w_t) if ctx.needs_input_grad[0] else None
+            ctx.flat.write_grad(ctx.name, dgu, None, nt=True, dy_t=dgu_t, x_t=x_t)
         else:
             _, x, w = ctx.saved_tensors
             dgu = fused.hip().swiglu_bwd(da.contiguous(), gu) if gu.is_cuda else fused.swiglu_bwd_ref(da, gu)
             dx = dgu.mm(w) if ctx.needs_input_grad[0] else None
             ctx.flat.write_grad(ctx.name, dgu, x)
-        return dx, None, None, None, None, None, None
+        return dx, None, None, None, None
 
 
 class _FlatRMSNorm(torch.autograd.Function):
@@ -522,8 +441,9 @@ class _FlatRMSNorm(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w, rstd = ctx.saved_tensors
-        dx = fused.hip().rmsnorm_bwd_into(dy.contiguous(), x, w, rstd, ctx.flat.params[ctx.name].grad)
-        ctx.flat.mark_written(ctx.name)
+        out, fresh = ctx.flat.grad_target(ctx.name)
+        dx = fused.hip().rmsnorm_bwd_into(dy.contiguous(), x, w, rstd, out)
+        ctx.flat.mark_written(ctx.name, None if fresh else out)
         return dx, None, None, None, None
 
 
@@ -543,12 +463,12 @@ class _FlatAddRMSNorm(torch.autograd.Function):
         h, w, rstd = ctx.saved_tensors
         if dy is None:
             dy = torch.zeros_like(h)
-        view = ctx.flat.params[ctx.name].grad
+        out, fresh = ctx.flat.grad_target(ctx.name)
         if dh is None:
-            dx = fused.hip().rmsnorm_bwd_into(dy.contiguous(), h, w, rstd, view)
+            dx = fused.hip().rmsnorm_bwd_into(dy.contiguous(), h, w, rstd, out)
         else:
-            dx = fused.hip().add_rmsnorm_bwd_into(dy.contiguous(), h, w, rstd, dh.contiguous(), view)
-        ctx.flat.mark_written(ctx.name)
+            dx = fused.hip().add_rmsnorm_bwd_into(dy.contiguous(), h, w, rstd, dh.contiguous(), out)
+        ctx.flat.mark_written(ctx.name, None if fresh else out)
         return dx, dx, None, None, None, None
 
 
@@ -567,34 +487,27 @@ class _FlatEmbedding(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (tokens,) = ctx.saved_tensors
-        view = ctx.flat.params[ctx.name].grad
+        out, fresh = ctx.flat.grad_target(ctx.name)
         srt, perm = torch.sort(tokens.reshape(-1), stable=True)
-        view.zero_()
-        fused.hip().embed_bwd_into(srt, perm, dy.contiguous().view(-1, view.size(1)), view)
-        ctx.flat.mark_written(ctx.name)
+        out.zero_()
+        fused.hip().embed_bwd_into(srt, perm, dy.contiguous().view(-1, out.size(1)), out)
+        ctx.flat.mark_written(ctx.name, None if fresh else out)
         return None, None, None, None
 
 
 class Llama(torch.nn.Module):
     def __init__(self, cfg: LlamaConfig, device="cuda", seed: int = 0, checkpoint: bool = False, attn: str = "hip",
-                 gemm_layout: str = "nt", overlap_transposes: bool = False, fuse_residual: bool = True,
-                 dgrad_nn: Tuple[str, ...] = (), persistent_wt: bool = True, transpose_x: str = "fused",
-                 attn_ot: Optional[bool] = None, flat_grads: Optional[bool] = None, wgrad_stream: bool = False):
+                 gemm_layout: str = "nt", persistent_wt: bool = True):
+        """``gemm_layout``: "nt" (the GPU default, see the module docstring) or "native" (autograd's
+        layouts: the reference the NT path is checked against).  ``persistent_wt=False`` re-makes every
+        W^T by a transpose in every backward (the round-3 path; A/B reference for the AdamW-written W^T)."""
         super().__init__()
         if gemm_layout not in ("nt", "native"):
             raise ValueError("gemm_layout must be 'nt' or 'native'")
-        bad = set(dgrad_nn) - set(PROJECTIONS)
-        if bad:
-            raise ValueError(f"dgrad_nn: unknown projections {sorted(bad)} (of {PROJECTIONS})")
-        # projections whose input gradient is dy W (NN) instead of dy (W^T)^T: no W^T per step, for
-        # the shapes where hipBLASLt's NN kernel costs less than the NT one plus the transpose
-        self.dgrad_nn = frozenset(dgrad_nn)
         self.cfg = cfg
         self.checkpoint = checkpoint
         self.attn = attn
         self.gemm_layout = gemm_layout
-        self.overlap_transposes = overlap_transposes
-        self.fuse_residual = fuse_residual  # residual add inside the RMSNorm kernels (fwd and bwd)
         # called with a parameter name before its first use in forward (ZeRO-1: wait for that
         # bucket's weight all-gather, parallel/dp.py BucketedAllReduce.wait_param)
         self.param_ready: Optional[Callable[[str], None]] = None
@@ -603,29 +516,20 @@ class Llama(torch.nn.Module):
         # the weight-gradient GEMM; norms and the embedding: their backward kernels), so no parameter is
         # zero-filled and then accumulated into; on the CPU reference path norms and the embedding go
         # through autograd's accumulation
-        on_gpu = torch.device(device).type == "cuda"
-        self.flat_grads = on_gpu if flat_grads is None else bool(flat_grads) and on_gpu
+        self.flat_grads = torch.device(device).type == "cuda"
         for n, p in self.flat.params.items():
             self.register_parameter(n.replace(".", "_"), p)
             if (p.dim() == 2 and n != "tok_emb") or self.flat_grads:
                 self.flat.mark_direct(n)
         self._init(seed)
-        # NT layout: W^T of every projection stays resident and the optimizer rewrites it with W
-        # (no per-step weight transposes); dgrad_nn projections read W itself
-        if transpose_x not in ("backward", "forward", "fused"):
-            raise ValueError("transpose_x must be 'backward', 'forward' or 'fused'")
-        self.transpose_x = transpose_x
-        self.flat.eager_xt = transpose_x == "forward" and gemm_layout == "nt"
-        self.flat.producer_xt = transpose_x in ("forward", "fused") and gemm_layout == "nt"
-        self.wgrad_stream = bool(wgrad_stream) and on_gpu and gemm_layout == "nt"
-        if self.wgrad_stream:
-            self.flat.wgrad_side = torch.cuda.Stream(device=torch.device(device))
-        # attention O^T from the forward kernel's epilogue (default: with the producer-written transposes)
-        self.attn_ot = self.flat.producer_xt if attn_ot is None else bool(attn_ot) and self.flat.producer_xt
+        # NT layout: the producers that hold a tile in LDS write the transposed activation too, the
+        # attention forward's epilogue O^T among them; W^T of every projection stays resident and the
+        # optimizer rewrites it with W (no per-step weight transposes)
+        self.flat.producer_xt = gemm_layout == "nt"
+        self.attn_ot = self.flat.producer_xt
         self.persistent_wt = persistent_wt and gemm_layout == "nt"
         if self.persistent_wt:
-            self.flat.enable_transposed([n for n in self.flat.direct if n != "tok_emb"
-                                         and n.rsplit(".", 1)[-1] not in self.dgrad_nn])
+            self.flat.enable_transposed([n for n in self.flat.direct if n != "tok_emb"])
         cos, sin = fused.rope_tables(cfg.max_seq, cfg.head_dim, cfg.rope_theta, device=device)
         self.register_buffer("rope_cos", cos, persistent=False)
         self.register_buffer("rope_sin", sin, persistent=False)
@@ -654,9 +558,7 @@ class Llama(torch.nn.Module):
         return self.flat.params[name]
 
     def _linear(self, x: torch.Tensor, name: str, x_t: Optional[torch.Tensor] = None) -> torch.Tensor:
-        nt = self.gemm_layout == "nt"
-        return _FlatLinear.apply(x, self.P(name).detach(), self.flat, name, nt, self.overlap_transposes,
-                                 name.rsplit(".", 1)[-1] in self.dgrad_nn, x_t)
+        return _FlatLinear.apply(x, self.P(name).detach(), self.flat, name, self.gemm_layout == "nt", x_t)
 
     # ---------------------------------------------------------------- blocks
     def _attention(self, q, k, v, want_t: bool = False):
@@ -684,16 +586,10 @@ class Llama(torch.nn.Module):
             w = self.P(name).detach()
             if r is None:
                 return x, _FlatRMSNorm.apply(x, w, self.flat, name, self.cfg.norm_eps)
-            if self.fuse_residual:
-                return _FlatAddRMSNorm.apply(x, r, w, self.flat, name, self.cfg.norm_eps)
-            x = x + r
-            return x, _FlatRMSNorm.apply(x, w, self.flat, name, self.cfg.norm_eps)
+            return _FlatAddRMSNorm.apply(x, r, w, self.flat, name, self.cfg.norm_eps)
         if r is None:
             return x, fused.rmsnorm(x, self.P(name), self.cfg.norm_eps)
-        if self.fuse_residual:
-            return fused.add_rmsnorm(x, r, self.P(name), self.cfg.norm_eps)
-        x = x + r
-        return x, fused.rmsnorm(x, self.P(name), self.cfg.norm_eps)
+        return fused.add_rmsnorm(x, r, self.P(name), self.cfg.norm_eps)
 
     def _layer(self, i: int, x: torch.Tensor, B: int, S: int, r: Optional[torch.Tensor] = None):
         """One block; returns ``(x, r)``: the residual stream and the block's last branch output, which
@@ -712,8 +608,7 @@ class Llama(torch.nn.Module):
             o, o_t = self._attention(q, k, v), None
         o = o.reshape(B * S, H * Dh)  # [B, S, H, Dh] -> [B*S, H*Dh]
         x, h = self._norm(x, self._linear(o, f"l{i}.wo", x_t=o_t), f"l{i}.ffn_norm")
-        a, a_t = _FlatLinearSwiGLU.apply(h, self.P(f"l{i}.w13").detach(), self.flat, f"l{i}.w13", self.gemm_layout == "nt",
-                                         self.overlap_transposes, "w13" in self.dgrad_nn)
+        a, a_t = _FlatLinearSwiGLU.apply(h, self.P(f"l{i}.w13").detach(), self.flat, f"l{i}.w13", self.gemm_layout == "nt")
         return x, self._linear(a, f"l{i}.w2", x_t=a_t)
 
     def forward(self, tokens: torch.Tensor, labels: Optional[torch.Tensor] = None) -> torch.Tensor:

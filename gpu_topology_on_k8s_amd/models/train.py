@@ -115,12 +115,11 @@ def _choose_device(env, placement: str, discovery: str, visible: Optional[int] =
 def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int = 3, warmup: int = 1, device_kind: str = "cuda",
           placement: str = "auto", discovery: str = "auto", bucket_mb: float = 256.0, checkpoint: bool = False, lr: float = 3e-4,
           attn: str = "hip", seed: int = 0, log: bool = True, gemm_tuning: str = "auto",
-          gemm_table: Optional[str] = None, gemm_layout: str = "nt", overlap_transposes: bool = False,
-          dgrad_nn: str = "",
+          gemm_table: Optional[str] = None, gemm_layout: str = "nt",
           zero1: bool = False, save_dir: Optional[str] = None, save_every: int = 0, resume: Optional[str] = None,
-          keep: int = 2, fuse_residual: bool = True, overlap_norm: bool = False, same_data: bool = False,
+          keep: int = 2, same_data: bool = False,
           graph: str = "auto", conv: str = "hip", cpu_bind: str = "auto", repeat_batch: bool = False,
-          persistent_wt: bool = True, transpose_x: str = "fused", grad_reduce: str = "bf16", comm_ctas: int = DEFAULT_COMM_CTAS, attn_ot: Optional[bool] = None, flat_grads: bool = True, wgrad_stream: bool = False,
+          persistent_wt: bool = True, grad_reduce: str = "bf16", comm_ctas: int = DEFAULT_COMM_CTAS,
           comm_shadow: int = 0, comm_shadow_k: int = 8, comm_shadow_busbw: float = 350.0) -> Dict[str, object]:
     env = _init_dist(device_kind, comm_ctas)
     if placement == "auto":  # inside a pod the allocation decides; on a bare node, the placement core
@@ -172,9 +171,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
     else:
         cfg = LlamaConfig.named(model_name)
         model = Llama(cfg, device=device, seed=seed, checkpoint=checkpoint, attn=attn, gemm_layout=gemm_layout,
-                      overlap_transposes=overlap_transposes, fuse_residual=fuse_residual,
-                      dgrad_nn=tuple(p for p in dgrad_nn.split(",") if p), persistent_wt=persistent_wt,
-                      transpose_x=transpose_x, attn_ot=attn_ot, flat_grads=flat_grads, wgrad_stream=wgrad_stream)
+                      persistent_wt=persistent_wt)
         items_per_step, unit, flops_per_item = batch * seq, "tokens", cfg.flops_per_token(seq)
     broadcast_params(model.flat)
     # graph mode issues the gradient collectives after backward (inside the captured step), not from
@@ -187,7 +184,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
 
         shadow = CommShadow(device, comm_shadow, k=comm_shadow_k, busbw_gbps=comm_shadow_busbw,
                             max_bucket_bytes=int(bucket_mb * (1 << 20)))
-    ar = BucketedAllReduce(model.flat, bucket_mb=bucket_mb, zero1=zero1, overlap_norm=overlap_norm, overlap=not use_graph,
+    ar = BucketedAllReduce(model.flat, bucket_mb=bucket_mb, zero1=zero1, overlap=not use_graph,
                            grad_reduce=grad_reduce, shadow=shadow)
     opt = FlatAdamW(model.flat, lr=lr, shards=ar.shards() if zero1 else None, capturable=use_graph)
     if zero1:
@@ -231,7 +228,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         loss = model(x, y)
         loss.backward()
         ar.finish()
-        opt.step(grad_scale=ar.grad_scale, sq=ar.sq_norm(), grad=ar.reduced_grad)
+        opt.step(grad_scale=ar.grad_scale, grad=ar.reduced_grad)
         ar.gather_params()  # zero1: overlaps the next forward; no-op otherwise
         return loss.detach()
 
@@ -331,7 +328,6 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "bucket_mb": bucket_mb,
         "gemm_tuning": gemm_mode,
         "gemm_layout": gemm_layout,
-        "overlap_transposes": overlap_transposes,
         "grad_reduce": grad_reduce,
         "comm_ctas": comm_ctas or None,
         "comm_shadow": ({"ctas": shadow.ctas, "k": shadow.k, "busbw_gbps": shadow.busbw,
@@ -341,15 +337,10 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
                          **shadow.timing()}
                         if shadow is not None else None),
         "persistent_wt": bool(getattr(model, "persistent_wt", False)),
-        "transpose_x": getattr(model, "transpose_x", None),
         "attn_ot": getattr(model, "attn_ot", None),
         "flat_grads": bool(getattr(model, "flat_grads", False)),
-        "wgrad_stream": bool(getattr(model, "wgrad_stream", False)),
         "optimizer_writes_wt": bool(getattr(opt, "fused_t", False)),
         "wt_refreshes": int(getattr(model.flat, "t_refreshes", 0)),
-        "dgrad_nn": dgrad_nn,
-        "fuse_residual": fuse_residual,
-        "overlap_norm": ar.overlap_norm,
         "step_start": start_step,
         "step_end": done[0],
         "resumed_from": resumed,
@@ -384,13 +375,6 @@ def main(argv=None) -> int:
     ap.add_argument("--gemm-tuning", default="auto", choices=["auto", "off", "use", "tune"],
                     help="TunableOp library-GEMM selection (models/gemm_tuning.py)")
     ap.add_argument("--gemm-table", default=None, help="TunableOp results table (default: the shipped MI355X table)")
-    ap.add_argument("--gemm-layout", default="nt", choices=["nt", "native"],
-                    help="backward GEMM operand layout: nt = transposed operands (HIP transpose kernel), native = as autograd issues them")
-    ap.add_argument("--dgrad-nn", default="",
-                    help="comma list of projections (wqkv,wo,w13,w2,lm_head) whose input gradient uses the NN GEMM dy W "
-                         "instead of NT with a per-step W^T (gemm layout nt)")
-    ap.add_argument("--overlap-transposes", action="store_true",
-                    help="make the NT operands' transposes on a side stream in forward (measured: no gain on MI355X)")
     ap.add_argument("--zero1", action="store_true",
                     help="shard the optimizer over the ranks: reduce-scatter grads, all-gather weights (ZeRO-1)")
     ap.add_argument("--save-dir", default=None, help="write checkpoints here (async; at the end, and every --save-every steps)")
@@ -398,8 +382,6 @@ def main(argv=None) -> int:
     ap.add_argument("--keep", type=int, default=2, help="committed checkpoints to keep")
     ap.add_argument("--resume", default=None,
                     help="checkpoint root (its latest) or step directory; any world size / --zero1 setting")
-    ap.add_argument("--no-fuse-residual", action="store_true",
-                    help="separate residual-add kernels instead of the fused add+RMSNorm (A/B)")
     ap.add_argument("--same-data", action="store_true",
                     help="every rank trains on rank 0's batches (k-rank losses must equal the 1-rank run)")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
@@ -409,29 +391,10 @@ def main(argv=None) -> int:
     ap.add_argument("--cpu-bind", default="auto", choices=["auto", "env", "off"],
                     help="Gaia B6: pin this rank to GTK_CPUSET narrowed to its device's core slice (auto; on a bare node the "
                          "slice alone), GTK_CPUSET only (env), or leave the threads unbound (off)")
-    ap.add_argument("--overlap-norm", action="store_true",
-                    help="clipping norm per bucket on a side stream as buckets complete (measured no gain at world 1)")
     ap.add_argument("--repeat-batch", action="store_true",
                     help="train on the first batch at every step: uniform random tokens carry nothing to learn, one "
                          "repeated batch does, so the loss must fall (end-to-end check of forward, backward and AdamW)")
     ap.add_argument("--lr", type=float, default=3e-4)
-    ap.add_argument("--persistent-wt", default="on", choices=["on", "off"],
-                    help="NT layout: keep W^T resident and let the optimizer write it with W (on), or re-make every "
-                         "W^T by a transpose in every backward (off, the round-3 path)")
-    ap.add_argument("--transpose-x", default="fused", choices=["fused", "backward", "forward"],
-                    help="NT layout: where the weight gradients' transposed operands come from. fused: written by the "
-                         "producer kernels that hold the tile in LDS (SwiGLU h^T, attention O^T, RoPE-backward "
-                         "dqkv^T, cross-entropy dlogits^T), the rest transposed in the backward; backward: every one "
-                         "transposed in the backward (round 3); forward: fused, plus every other x^T made right "
-                         "after its producer")
-    ap.add_argument("--attn-ot", default="auto", choices=["auto", "on", "off"],
-                    help="NT layout: the attention forward kernel also writes O^T for the o-projection's weight "
-                         "gradient (auto: with --transpose-x fused / forward)")
-    ap.add_argument("--flat-grads", default="on", choices=["on", "off"],
-                    help="GPU: norm and embedding gradients written into the flat buffer by their kernels (on), or "
-                         "accumulated by autograd from separate tensors (off, the round-3 path)")
-    ap.add_argument("--wgrad-stream", default="off", choices=["on", "off"],
-                    help="NT layout: run each weight-gradient GEMM on a side stream, overlapping its input-gradient GEMM")
     ap.add_argument("--grad-reduce", default="bf16", choices=["bf16", "fp32"],
                     help="DP gradient reduction dtype: bf16 in place, or fp32 (a widened copy reduced and applied in fp32)")
     ap.add_argument("--comm-ctas", type=int, default=DEFAULT_COMM_CTAS,
@@ -444,12 +407,9 @@ def main(argv=None) -> int:
                     help="--comm-shadow: per-rank bus GB/s that sets each emulated collective's duration")
     a = ap.parse_args(argv)
     train(a.model, a.batch, a.seq, a.steps, a.warmup, a.device, a.placement, a.discovery, a.bucket_mb, a.checkpoint, lr=a.lr, attn=a.attn,
-          gemm_tuning=a.gemm_tuning, gemm_table=a.gemm_table, gemm_layout=a.gemm_layout,
-          overlap_transposes=a.overlap_transposes, dgrad_nn=a.dgrad_nn, zero1=a.zero1, save_dir=a.save_dir, save_every=a.save_every,
-          resume=a.resume, keep=a.keep, fuse_residual=not a.no_fuse_residual,
-          overlap_norm=a.overlap_norm, same_data=a.same_data, graph=a.graph, conv=a.conv, cpu_bind=a.cpu_bind,
-          repeat_batch=a.repeat_batch, persistent_wt=a.persistent_wt == "on",
-          transpose_x=a.transpose_x, attn_ot={"auto": None, "on": True, "off": False}[a.attn_ot], flat_grads=a.flat_grads == "on", wgrad_stream=a.wgrad_stream == "on", grad_reduce=a.grad_reduce, comm_ctas=a.comm_ctas, comm_shadow=a.comm_shadow,
+          gemm_tuning=a.gemm_tuning, gemm_table=a.gemm_table, zero1=a.zero1, save_dir=a.save_dir, save_every=a.save_every,
+          resume=a.resume, keep=a.keep, same_data=a.same_data, graph=a.graph, conv=a.conv, cpu_bind=a.cpu_bind,
+          repeat_batch=a.repeat_batch, grad_reduce=a.grad_reduce, comm_ctas=a.comm_ctas, comm_shadow=a.comm_shadow,
           comm_shadow_k=a.comm_shadow_k, comm_shadow_busbw=a.comm_shadow_busbw)
     if dist.is_initialized():
         dist.destroy_process_group()

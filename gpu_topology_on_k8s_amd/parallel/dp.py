@@ -164,7 +164,7 @@ def broadcast_params(flat, group=None, src: int = 0) -> None:
 
 class BucketedAllReduce:
     def __init__(self, flat, group=None, bucket_mb: float = 256.0, first_bucket_mb: float = 64.0, average: bool = True,
-                 overlap: bool = True, zero1: bool = False, overlap_norm: bool = False, grad_reduce: str = "bf16",
+                 overlap: bool = True, zero1: bool = False, grad_reduce: str = "bf16",
                  shadow: Optional[CommShadow] = None):
         if grad_reduce not in ("bf16", "fp32"):
             raise ValueError("grad_reduce must be 'bf16' or 'fp32'")
@@ -212,18 +212,10 @@ class BucketedAllReduce:
         self.grad32 = (torch.zeros(flat.numel, dtype=torch.float32, device=flat.grad.device)
                        if grad_reduce == "fp32" and self.world > 1 else None)
         self.shadow = shadow if (shadow is not None and self.world == 1 and flat.grad.is_cuda) else None
-        # Gradient-clipping norm per bucket on a side HIP stream, as each bucket's reduction lands:
-        # the 16 GB read (3 ms at HBM rate for Llama-3-8B) overlaps the compute-bound backward GEMMs
-        # instead of running serially before the optimizer.  Needs the readiness hooks, so at
-        # world 1 they are installed for it alone.  Off by default: on one MI355X it measured
-        # 691.2 vs 691.4 ms/step (Llama-3-8B) — hipBLASLt's GEMMs hold every CU, so the side-stream
-        # norm kernels find no free slots and serialise anyway (profiles/r01_fuse_res/NORM.md).
-        self.overlap_norm = overlap_norm and overlap and flat.grad.is_cuda and self.grad32 is None
-        self._norm_stream = None
-        self._parts = torch.zeros(max(1, len(self.buckets)), dtype=torch.float32, device=flat.grad.device) \
-            if self.overlap_norm else None
+        # (A per-bucket clipping norm on a side stream as buckets land measured flat on MI355X --
+        # hipBLASLt's GEMMs hold every CU -- and was retired in round 5: profiles/r01_fuse_res/NORM.md.)
         self._launched = [False] * len(self.buckets)
-        if overlap and (self.world > 1 or self.overlap_norm or self.shadow is not None):
+        if overlap and (self.world > 1 or self.shadow is not None):
             direct = getattr(flat, "direct", {})
             for n, p in flat.params.items():
                 if n in direct:  # weight-gradient GEMM writes the flat buffer itself (models/llama.py _FlatLinear)
@@ -254,10 +246,9 @@ class BucketedAllReduce:
 
     def _launch(self, b: Bucket) -> None:
         self._launched[b.index] = True
-        if self.world == 1:  # nothing to reduce: only the overlapped norm (and the k-GPU shadow)
+        if self.world == 1:  # nothing to reduce: only the k-GPU shadow
             if self.shadow is not None:
                 self.shadow.launch(b.numel * self.flat.grad.element_size())
-            self._norm(b)
             return
         view = self.flat.grad[b.start:b.end]
         b.launched_at = time.perf_counter()
@@ -273,34 +264,6 @@ class BucketedAllReduce:
             b.work = dist.all_reduce(view, group=self.group, async_op=True)
         self.stats["launches"] += 1
         self.stats["comm_bytes"] += view.numel() * view.element_size()
-        self._norm(b)
-
-    def _norm(self, b: Bucket) -> None:
-        """Squared norm of this rank's reduced part of bucket ``b`` into ``_parts[b]``, on the side
-        stream, after the bucket's collective (or, at world 1, its gradient GEMMs)."""
-        if not self.overlap_norm:
-            return
-        from ..ops import fused
-
-        cur = torch.cuda.current_stream(self.flat.grad.device)
-        if self._norm_stream is None:
-            self._norm_stream = torch.cuda.Stream(device=self.flat.grad.device)
-        st = self._norm_stream
-        st.wait_stream(cur)
-        with torch.cuda.stream(st):
-            if b.work is not None:
-                b.work.wait()  # the side stream waits for RCCL's stream
-            s, e = self.own(b)
-            self._parts[b.index:b.index + 1].copy_(fused.hip().sq_norm(self.flat.grad[s:e]).reshape(1))
-
-    def sq_norm(self) -> Optional[torch.Tensor]:
-        """This rank's sum of squared reduced gradients (its shards under zero1) from the
-        overlapped per-bucket norms, ordered on the current stream; ``None`` when not overlapped.
-        Call after :meth:`finish`."""
-        if not self.overlap_norm:
-            return None
-        torch.cuda.current_stream(self.flat.grad.device).wait_stream(self._norm_stream)
-        return self._parts.sum()
 
     def reset(self) -> None:
         for b in self.buckets:
@@ -318,7 +281,7 @@ class BucketedAllReduce:
                     self._launch(b)
             for b in self.buckets:
                 b.work.wait()
-        elif self.overlap_norm or self.shadow is not None:
+        elif self.shadow is not None:
             for b in self.buckets:
                 if not self._launched[b.index]:
                     self._launch(b)

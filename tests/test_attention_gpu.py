@@ -60,12 +60,13 @@ def test_attention_backward(fused, B, H, Hkv, S):
     assert _rel(vh.grad, vf.grad) < 2e-2, _rel(vh.grad, vf.grad)
 
 
-@pytest.mark.parametrize("B,H,Hkv,S", [(2, 8, 2, 768), (1, 4, 4, 128), (1, 32, 8, 1024), (2, 4, 1, 384)])
-def test_attention_bwd_v4_matches_v3(fused, B, H, Hkv, S):
-    """dK/dV v4 (slices software-pipelined through a 3-buffer ring, branch-free) and v5 (the default:
-    v4 with every LDS operand read before the next slice's DMA) do v3's arithmetic in v3's order:
-    identical bits, including the all-diagonal S=128 case, MHA
-    (G=1), G=4 and G=8, and slice counts that are not multiples of the ring length."""
+@pytest.mark.parametrize("B,H,Hkv,S", [(2, 8, 2, 768), (1, 4, 4, 128), (1, 32, 8, 1024), (2, 4, 1, 384), (1, 8, 2, 640)])
+@pytest.mark.parametrize("variant", ["v5", "v7_asm", "v7_cc"])
+def test_attention_bwd_variants_match_fp32_reference(fused, B, H, Hkv, S, variant):
+    """Every dK/dV generation the extension exports (v5: the round-4 kernel; v7: S / dP accumulated in
+    VGPRs from -lse/c and -delta, its dV/dK accumulators pinned to AGPRs by asm or left to the compiler)
+    against the fp32 PyTorch reference, and within bf16 rounding of each other: the all-diagonal S=128
+    case, MHA (G=1), G=4 and G=8, slice counts that are not multiples of the 3-slot ring."""
     torch.manual_seed(5)
     q = torch.randn(B, H, S, 128, device="cuda", dtype=torch.bfloat16)
     k = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
@@ -73,16 +74,22 @@ def test_attention_bwd_v4_matches_v3(fused, B, H, Hkv, S):
     do = torch.randn(B, S, H, 128, device="cuda", dtype=torch.bfloat16)
     hip = fused.hip()
     o, lse = hip.attn_fwd(q, k, v, 128 ** -0.5)
-    g3 = hip.attn_bwd_v3(do, q, k, v, o, lse, 128 ** -0.5)
-    g5 = hip.attn_bwd(do, q, k, v, o, lse, 128 ** -0.5)  # the default, v5: operands read ahead of the DMA
-    for name, a, b in zip(("dq", "dk", "dv"), g5, g3):
-        assert torch.equal(a, b), (name, _rel(a, b))
-    g5t = hip.attn_bwd_v5t(do, q, k, v, o, lse, 128 ** -0.5)  # v5 with the transposed reads first
-    for name, a, b in zip(("dq", "dk", "dv"), g5t, g3):
-        assert torch.equal(a, b), (name, "v5t", _rel(a, b))
-    g4 = hip.attn_bwd_v4(do, q, k, v, o, lse, 128 ** -0.5)  # v4: operands read at their use
-    for name, a, b in zip(("dq", "dk", "dv"), g4, g3):
-        assert torch.equal(a, b), (name, "v4", _rel(a, b))
+    fn = {"v5": lambda: hip.attn_bwd_v5(do, q, k, v, o, lse, 128 ** -0.5),
+          "v7_asm": lambda: hip.attn_bwd_v7(do, q, k, v, o, lse, 128 ** -0.5, True),
+          "v7_cc": lambda: hip.attn_bwd_v7(do, q, k, v, o, lse, 128 ** -0.5, False)}[variant]
+    got = fn()
+    qf, kf, vf = (x.float().requires_grad_(True) for x in (q, k, v))
+    ref = fused.attention_ref(qf, kf, vf)
+    ref.backward(do.float())
+    for name, a, want in zip(("dq", "dk", "dv"), got, (qf.grad, kf.grad, vf.grad)):
+        assert torch.isfinite(a).all(), (variant, name)
+        assert _rel(a, want) < 2e-2, (variant, name, _rel(a, want))
+    base = hip.attn_bwd(do, q, k, v, o, lse, 128 ** -0.5)
+    for name, a, b in zip(("dq", "dk", "dv"), got, base):
+        assert _rel(a, b) < 1e-2, (variant, name, _rel(a, b))
+    again = fn()
+    for name, a, b in zip(("dq", "dk", "dv"), again, got):
+        assert torch.equal(a, b), (variant, name, "not deterministic")
 
 
 @pytest.mark.parametrize("B,H,Hkv,S", [(2, 8, 2, 768), (1, 4, 4, 128), (1, 2, 2, 640)])
@@ -164,45 +171,3 @@ def test_attention_is_deterministic_at_the_training_shape(fused):
         g2 = hip.attn_bwd(do, q, k, v, o, lse, 128 ** -0.5)
         for name, a, b in zip(("dq", "dk", "dv"), g2, g):
             assert torch.equal(a, b), name
-    # the A/B variants (fwd2n without the mid-tile DMA wait; the round-3 dQ dq2 with it): same bits
-    oa, lsea = hip.attn_fwd_noalias(q, k, v, 128 ** -0.5)
-    assert torch.equal(oa, o) and torch.equal(lsea, lse)
-    ga = hip.attn_bwd_dq_alias(do, q, k, v, o, lse, 128 ** -0.5)
-    for name, a, b in zip(("dq", "dk", "dv"), ga, g):
-        assert torch.equal(a, b), name
-
-
-@pytest.mark.parametrize("B,H,Hkv,S", CASES + [(1, 32, 8, 8192)])
-def test_noalias_kernels_match_the_round3_kernels_bitwise(fused, B, H, Hkv, S):
-    """fwd2n / dq2n (LDS images as __restrict__ tile parameters: no mid-tile DMA wait) against fwd2 /
-    dq2 (one LDS array, the compiler's wait) at every test shape, including the causal diagonal's
-    peeled tiles: bit-identical."""
-    torch.manual_seed(B * 1000 + S)
-    q = torch.randn(B, H, S, 128, device="cuda", dtype=torch.bfloat16)
-    k = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
-    v = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
-    do = torch.randn(B, S, H, 128, device="cuda", dtype=torch.bfloat16)
-    hip = fused.hip()
-    o, lse = hip.attn_fwd(q, k, v, 128 ** -0.5)
-    oa, lsea = hip.attn_fwd_noalias(q, k, v, 128 ** -0.5)
-    assert torch.equal(o, oa) and torch.equal(lse, lsea)
-    dq = hip.attn_bwd(do, q, k, v, o, lse, 128 ** -0.5)[0]
-    dqa = hip.attn_bwd_dq_alias(do, q, k, v, o, lse, 128 ** -0.5)[0]
-    assert torch.equal(dq, dqa)
-
-
-@pytest.mark.parametrize("B,H,Hkv,S", [(1, 4, 2, 128), (1, 8, 2, 384), (2, 32, 8, 1024), (1, 32, 8, 4096)])
-def test_mask_branch_backward_is_bit_identical(fused, B, H, Hkv, S):
-    """dK/dV v5 with the causal mask behind a wave-uniform branch (the default) against the per-score
-    select on every slice (attn_bwd_v5m0): dq, dk, dv bit-identical, diagonal and dead slices included."""
-    hip = fused.hip()
-    torch.manual_seed(11)
-    q = torch.randn(B, H, S, 128, device="cuda", dtype=torch.bfloat16)
-    k = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
-    v = torch.randn(B, Hkv, S, 128, device="cuda", dtype=torch.bfloat16)
-    do = torch.randn(B, S, H, 128, device="cuda", dtype=torch.bfloat16)
-    o, lse = hip.attn_fwd(q, k, v, 128 ** -0.5)
-    ref = hip.attn_bwd_v5m0(do, q, k, v, o, lse, 128 ** -0.5)
-    got = hip.attn_bwd(do, q, k, v, o, lse, 128 ** -0.5)
-    for a, b in zip(got, ref):
-        assert torch.equal(a, b)

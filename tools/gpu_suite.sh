@@ -73,57 +73,12 @@ print(json.dumps({"tflops": round(float(w["tflops"]), 1), "hbm_copy_gbps": round
     step ab_b2 300 python -u bench/attn_bench.py --b 2 --s 4096 --iters 5 --ab 30
     step pmc_attn 120 timeout -s KILL 100 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_INST_LDS --kernel-trace -d "$out/pmc_attn" -o run -- python3 tools/pmc_attn.py
     ;;
-  adamw_t)
-    # the AdamW-T tile kernel against the flat kernel: bitwise tests, then the step with and without W^T
-    step pytest_adamw 300 python -u -m pytest tests/test_fused_gpu.py -x -v --timeout 200 --timeout-method thread -k "adamw or persistent_wt or transpose or swiglu"
-    step swiglu_ab 120 python -u bench/swiglu_t_ab.py
-    step llama_wt_off 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --persistent-wt off
-    step llama_wt_on 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
-    step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
-    ;;
-  llama_ab)
-    # transposes A/B: round-3 path, persistent W^T, + x^T in the forward; then the
-    # kernel trace of the default
-    step pytest_fused 600 python -u -m pytest tests/test_fused_gpu.py -x -v --timeout 300 --timeout-method thread
-    step llama_wt_off 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --persistent-wt off
-    step llama_wt_on 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
-    step llama_wt_xf 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --transpose-x forward
-    step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
-    ;;
-  fused_t)
-    # producer-written transposes (SwiGLU h^T, attention O^T, dlogits^T): kernel tests, kernel A/B,
-    # step A/B against the all-in-backward path, kernel trace of the default
-    step pytest_fused 600 python -u -m pytest tests/test_fused_gpu.py -x -v --timeout 300 --timeout-method thread
-    step fused_t_ab 300 python -u bench/fused_t_ab.py
-    step llama_fused 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
-    step llama_bwd 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --transpose-x backward
-    step llama_fused_ot 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --attn-ot on
-    step llama_fused2 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
-    step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
-    ;;
-  flatgrad)
-    # norm / embedding gradients written into the flat buffer by their kernels: tests, step A/B, trace
-    step pytest_fused 600 python -u -m pytest tests/test_fused_gpu.py -x -v --timeout 300 --timeout-method thread
-    step llama_flat 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
-    step llama_noflat 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --flat-grads off
-    step llama_flat2 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
-    step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
-    ;;
   normpf)
     # RMSNorm backward with the next row prefetched: tests, norm bench, step, trace
     step pytest_fused 600 python -u -m pytest tests/test_fused_gpu.py -x -v --timeout 300 --timeout-method thread
     step norm_bench 300 python -u bench/norm_bench.py
     step llama 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
     step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
-    ;;
-  wgs)
-    # weight-gradient GEMMs on a side stream (overlapping the input-gradient GEMMs): tests, step A/B, trace
-    step pytest_fused 600 python -u -m pytest tests/test_fused_gpu.py -x -v --timeout 300 --timeout-method thread
-    step llama_off 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
-    step llama_on 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --wgrad-stream on
-    step llama_off2 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
-    step llama_on2 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --wgrad-stream on
-    step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1 --wgrad-stream on
     ;;
   memk)
     # memory-bound tile kernels with every load of the tile issued first: tests, kernel A/B bench, step, trace
@@ -132,14 +87,6 @@ print(json.dumps({"tflops": round(float(w["tflops"]), 1), "hbm_copy_gbps": round
     step adamw_t_ab 300 python -u bench/adamw_t_ab.py
     step llama 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
     step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
-    ;;
-  ot_ab)
-    # attention O^T from the forward epilogue (--attn-ot on) vs the backward transpose, interleaved, + trace of "on"
-    step llama_off 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
-    step llama_on 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --attn-ot on
-    step llama_off2 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
-    step llama_on2 600 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2 --attn-ot on
-    step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1 --attn-ot on
     ;;
   pmcstep)
     # counters over one Llama-3-8B step: MFMA busy, then memory-side requests (each pass its own run),

@@ -29,10 +29,11 @@ def main():
     for _ in range(3):
         o, lse = hip.attn_fwd(q, k, v, D ** -0.5)
         hip.attn_bwd(do, q, k, v, o, lse, D ** -0.5)
-    if hasattr(hip, "attn_fwd_noalias"):  # fwd2n / dq2: the A/B variants, same pass: per-kernel counters of both
-        for _ in range(3):
-            o, lse = hip.attn_fwd_noalias(q, k, v, D ** -0.5)
-            hip.attn_bwd_dq_alias(do, q, k, v, o, lse, D ** -0.5)
+    # the dK/dV generations the extension exports, same pass: per-kernel counters of each
+    for name, args in (("attn_bwd_v5", ()), ("attn_bwd_v7", (True,)), ("attn_bwd_v7", (False,))):
+        if hasattr(hip, name):
+            for _ in range(3):
+                getattr(hip, name)(do, q, k, v, o, lse, D ** -0.5, *args)
     torch.cuda.synchronize()
     print("pmc_attn done", flush=True)
 
