@@ -28,7 +28,7 @@ import torch.distributed as dist
 
 from ..ops import fused
 
-__all__ = ["FlatAdamW"]
+__all__ = ["FlatAdamW", "FlatSGD"]
 
 
 class FlatAdamW:
@@ -205,3 +205,75 @@ class FlatAdamW:
         upd = (m / bc1) / ((v / bc2).sqrt() + eps)
         master.sub_(lr * (upd + wd * master))
         data.copy_(master.to(data.dtype))
+
+
+class FlatSGD:
+    """Plain SGD on the flat buffer (fp32 master, no momentum, no weight decay, no clipping):
+    ``w -= lr * grad_scale * g``.  The data-parallel parity check of ``models/train.py
+    --optimizer sgd``: AdamW's update m / sqrt(v) is invariant to the scale of the
+    gradient, so a k-rank run whose reduction never ran (each rank applying its local gradient / k)
+    tracks the 1-rank run within tolerance; SGD's update is linear in the gradient, so it cannot.
+    Same interface as :class:`FlatAdamW` (``shards`` for ZeRO-1, ``capturable`` for hipGraph steps,
+    ``t_dev`` as the device step counter); not checkpointable."""
+
+    _CHUNK = 1 << 26  # elements per fp32 temporary
+
+    def __init__(self, flat, lr: float = 1e-2, shards: Optional[Sequence[Tuple[int, int]]] = None, group=None,
+                 capturable: bool = False):
+        self.flat = flat
+        self.lr = float(lr)
+        self.group = group
+        self.sharded = shards is not None
+        self.shards: List[Tuple[int, int]] = list(shards) if shards is not None else [(0, flat.numel)]
+        if self.sharded:
+            self.master = torch.cat([flat.data[s:e].float() for s, e in self.shards])
+        else:
+            self.master = flat.data.float()
+        self.capturable = capturable
+        self.t_dev = torch.zeros(1, dtype=torch.float32, device=flat.data.device) if capturable else None
+        self._t = 0
+        self._deferred = []
+        self.fused_t = False
+
+    @property
+    def t(self) -> int:
+        return self._t
+
+    @t.setter
+    def t(self, value: int) -> None:
+        self._t = int(value)
+        if self.t_dev is not None:
+            self.t_dev.fill_(float(self._t))
+
+    def note_replay(self, n: int = 1) -> None:
+        self._t += n
+
+    def defer_until(self, event) -> None:
+        self._deferred.append(event)
+
+    def state_bytes(self) -> int:
+        return self.master.numel() * 4
+
+    @torch.no_grad()
+    def step(self, grad_scale: float = 1.0, sq: Optional[torch.Tensor] = None, grad: Optional[torch.Tensor] = None) -> None:
+        gbuf = grad if grad is not None else self.flat.grad
+        if self._deferred:
+            cur = torch.cuda.current_stream(self.master.device)
+            for ev in self._deferred:
+                cur.wait_event(ev)
+            self._deferred.clear()
+        if self.t_dev is not None:
+            self.t_dev.add_(1.0)
+        if not (self.master.is_cuda and torch.cuda.is_current_stream_capturing()):
+            self._t += 1
+        alpha = -self.lr * float(grad_scale)
+        o = 0
+        for s, e in self.shards:
+            for a in range(s, e, self._CHUNK):
+                b = min(e, a + self._CHUNK)
+                m = self.master[o + a - s:o + b - s]
+                m.add_(gbuf[a:b].float(), alpha=alpha)
+                self.flat.data[a:b].copy_(m)
+            o += e - s
+        if hasattr(self.flat, "invalidate_t"):
+            self.flat.invalidate_t()

@@ -19,6 +19,7 @@ for launch-bound models such as the MNIST CNN ('auto' = on for MNIST at world 1 
 from __future__ import annotations
 
 import argparse
+import dataclasses
 import json
 import os
 import sys
@@ -31,7 +32,7 @@ import torch.distributed as dist
 from .llama import Llama, LlamaConfig
 from .mnist import EPOCH_IMAGES, MnistCNN, MnistConfig
 from .gemm_tuning import setup_gemm_tuning
-from .optim import FlatAdamW
+from .optim import FlatAdamW, FlatSGD
 from .checkpoint import CheckpointWriter, load_checkpoint
 from ..parallel.dp import DEFAULT_COMM_CTAS, BucketedAllReduce, broadcast_params
 from ..topology.cpus import bind_workload
@@ -120,7 +121,15 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
           keep: int = 2, same_data: bool = False,
           graph: str = "auto", conv: str = "hip", cpu_bind: str = "auto", repeat_batch: bool = False,
           persistent_wt: bool = True, grad_reduce: str = "bf16", comm_ctas: int = DEFAULT_COMM_CTAS,
-          comm_shadow: int = 0, comm_shadow_k: int = 8, comm_shadow_busbw: float = 350.0) -> Dict[str, object]:
+          comm_shadow: int = 0, comm_shadow_k: int = 8, comm_shadow_busbw: float = 350.0,
+          optimizer: str = "adamw", check_reduction: bool = False, data_ranks: int = 0, dropout: bool = True,
+          fingerprint: bool = False) -> Dict[str, object]:
+    """``optimizer="sgd"``, ``data_ranks``, ``fingerprint`` and ``check_reduction`` are the data-parallel
+    correctness checks (VERDICT r4 next #1); see :func:`main`'s help for each."""
+    if optimizer not in ("adamw", "sgd"):
+        raise ValueError("optimizer must be 'adamw' or 'sgd'")
+    if optimizer == "sgd" and (save_dir or resume):
+        raise ValueError("--optimizer sgd is a parity check: it is not checkpointed")
     env = _init_dist(device_kind, comm_ctas)
     if placement == "auto":  # inside a pod the allocation decides; on a bare node, the placement core
         placement = "pod" if os.environ.get("GTK_GPU_GROUP") else "best"
@@ -163,16 +172,25 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         raise ValueError("--graph on needs a GPU")
     if use_graph and zero1:
         raise ValueError("--graph does not capture ZeRO-1's per-bucket weight all-gathers")
-    data_seed = 1234 + (0 if same_data else env["rank"])
+    # data: rank r draws from seed 1234 + r (1234 for every rank with --same-data); --data-ranks K makes
+    # ONE rank draw every one of K ranks' batches and train on their concatenation -- the batch a K-rank
+    # job's gradient all-reduce averages over, for the k-rank vs 1-rank parity check
+    if data_ranks and env["world"] != 1:
+        raise ValueError("--data-ranks emulates K ranks' data on a 1-rank job")
+    seeds = [1234 + i for i in range(data_ranks)] if data_ranks else [1234 + (0 if same_data else env["rank"])]
+    data_seed = seeds[0]
+    local_batch = batch * len(seeds)
     if mnist:
         cfg = MnistConfig.named(model_name)
+        if not dropout:  # deterministic in the batch split: what the k-rank vs 1-rank parity check needs
+            cfg = dataclasses.replace(cfg, p1=0.0, p2=0.0)
         model = MnistCNN(cfg, device=device, seed=seed, conv=conv)
-        items_per_step, unit, flops_per_item = batch, "images", cfg.flops_per_image()
+        items_per_step, unit, flops_per_item = local_batch, "images", cfg.flops_per_image()
     else:
         cfg = LlamaConfig.named(model_name)
         model = Llama(cfg, device=device, seed=seed, checkpoint=checkpoint, attn=attn, gemm_layout=gemm_layout,
                       persistent_wt=persistent_wt)
-        items_per_step, unit, flops_per_item = batch * seq, "tokens", cfg.flops_per_token(seq)
+        items_per_step, unit, flops_per_item = local_batch * seq, "tokens", cfg.flops_per_token(seq)
     broadcast_params(model.flat)
     # graph mode issues the gradient collectives after backward (inside the captured step), not from
     # autograd hooks mid-backward: one capture-friendly sequence
@@ -186,7 +204,12 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
                             max_bucket_bytes=int(bucket_mb * (1 << 20)))
     ar = BucketedAllReduce(model.flat, bucket_mb=bucket_mb, zero1=zero1, overlap=not use_graph,
                            grad_reduce=grad_reduce, shadow=shadow)
-    opt = FlatAdamW(model.flat, lr=lr, shards=ar.shards() if zero1 else None, capturable=use_graph)
+    if optimizer == "sgd":
+        if use_graph and getattr(model.flat, "data_t", None) is not None:
+            raise ValueError("--optimizer sgd with --graph: the captured step would keep a stale W^T")
+        opt = FlatSGD(model.flat, lr=lr, shards=ar.shards() if zero1 else None, capturable=use_graph)
+    else:
+        opt = FlatAdamW(model.flat, lr=lr, shards=ar.shards() if zero1 else None, capturable=use_graph)
     if zero1:
         model.param_ready = ar.wait_param
     if mnist and use_graph:
@@ -198,8 +221,35 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
     if mnist and use_graph:
         torch.cuda.manual_seed(data_seed)
         gen = None
+        gens = []
     else:
-        gen = torch.Generator(device=device if mnist else "cpu").manual_seed(data_seed)
+        gens = [torch.Generator(device=device if mnist else "cpu").manual_seed(sd) for sd in seeds]
+        gen = gens[0]
+    def update_fp():
+        """Four fixed pseudo-random projections (fp64) of the fp32 master weights: every rank sums its
+        1/world partition of each bucket and the sums are all-reduced, so a k-rank job and a 1-rank job
+        produce comparable numbers.  Their change over a run fingerprints the weight update."""
+        acc = torch.zeros(4, dtype=torch.float64, device=opt.master.device)
+        base, o = {}, 0
+        for s_, e_ in opt.shards:  # flat offset -> offset in the optimizer's (concatenated) master
+            base[(s_, e_)] = o
+            o += e_ - s_
+        for b in ar.buckets:
+            lo = b.start + (b.numel * env["rank"]) // env["world"]
+            hi = b.start + (b.numel * (env["rank"] + 1)) // env["world"]
+            for (s_, e_), o_ in base.items():
+                a0, a1 = max(lo, s_), min(hi, e_)
+                for a in range(a0, a1, 1 << 24):
+                    z = min(a1, a + (1 << 24))
+                    w = opt.master[o_ + a - s_:o_ + z - s_].double()
+                    idx = torch.arange(a, z, dtype=torch.float64, device=w.device)
+                    for k in range(4):
+                        acc[k] += (w * torch.sin(idx * (0.6180339887 + 0.1 * k) + k)).sum()
+        if env["world"] > 1:
+            dist.all_reduce(acc)
+        return acc.tolist()
+
+    fp0 = update_fp() if fingerprint else None
     start_step, resumed = 0, None
     if resume:
         meta = load_checkpoint(resume, model, opt, gen)
@@ -210,27 +260,86 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
     done = [start_step]
     first: Dict[str, object] = {}
 
+    def _cat(parts):
+        return parts[0] if len(parts) == 1 else tuple(torch.cat(z) for z in zip(*parts))
+
     def batch_tokens():
-        if mnist and use_graph:  # one HIP launch, indexed by the optimizer's device step counter
-            return model.synthetic_batch_dev(batch, opt.t_dev, seed=data_seed)
+        if mnist and use_graph:  # one HIP launch per seed, indexed by the optimizer's device step counter
+            x, y = _cat([model.synthetic_batch_dev(batch, opt.t_dev, seed=sd) for sd in seeds])
+            return x.contiguous(memory_format=torch.channels_last), y
         if mnist:
-            return model.synthetic_batch(batch, gen)
+            x, y = _cat([model.synthetic_batch(batch, g) for g in gens])
+            return x.contiguous(memory_format=torch.channels_last), y
         if repeat_batch and "t" in first:  # memorisation check: the same tokens every step
             t = first["t"]
         else:
-            t = torch.randint(0, cfg.vocab, (batch, seq + 1), generator=gen)
+            t = torch.cat([torch.randint(0, cfg.vocab, (batch, seq + 1), generator=g) for g in gens])
             t = first["t"] = t.to(device, non_blocking=True)
         return t[:, :-1], t[:, 1:]
 
-    def body() -> torch.Tensor:
-        x, y = batch_tokens()
+    def body(xy=None, before_opt=None) -> torch.Tensor:
+        x, y = xy if xy is not None else batch_tokens()
         model.flat.zero_grad()
         loss = model(x, y)
         loss.backward()
         ar.finish()
+        if before_opt is not None:
+            before_opt()
         opt.step(grad_scale=ar.grad_scale, grad=ar.reduced_grad)
         ar.gather_params()  # zero1: overlaps the next forward; no-op otherwise
         return loss.detach()
+
+    # --check-reduction: the first step checks the gradient reduction with DIFFERENT data per rank.  A
+    # hook-free pass of the same batch (same dropout state) gives each rank's local gradient; the real
+    # pass then copies every bucket's input right before its collective launches.  Checked, on the
+    # stream and at the point the optimizer reads it: the reduced buffer against the fp64 sum of all
+    # ranks' local gradients (a skipped bucket, an unawaited collective, a wrong scale fail), and each
+    # launched bucket against the local gradient (a bucket whose collective started before backward
+    # finished writing it fails).  In graph mode the copies are captured with the step and the check
+    # runs after the first replay (a replay that re-ran a stale collective fails).
+    check = {"pending": bool(check_reduction), "result": None}
+    tol = 1e-3 if ar.grad32 is not None else 1e-2
+
+    def _rng():
+        st = {"cpu": torch.get_rng_state()}
+        if device.type == "cuda":
+            st["cuda"] = torch.cuda.get_rng_state(device)
+        if getattr(model, "_own_step", None) is not None:
+            st["own"] = model._own_step.clone()
+        return st
+
+    def _set_rng(st):
+        torch.set_rng_state(st["cpu"])
+        if "cuda" in st:
+            torch.cuda.set_rng_state(st["cuda"], device)
+        if "own" in st:
+            model._own_step.copy_(st["own"])
+
+    def _record(red, rdy) -> None:
+        ok = red["max_rel"] <= tol and (rdy is None or rdy["max_rel"] <= tol)
+        check["result"] = {"ok": bool(ok), "tol": tol, "reduce_max_rel": red["max_rel"],
+                           "ready_max_rel": None if rdy is None else rdy["max_rel"], "buckets": len(red["buckets"]),
+                           "worst_bucket": max(red["buckets"], key=lambda z: z["rel"])["index"] if red["buckets"] else None,
+                           "mode": "graph-replay" if use_graph else "eager", "world": env["world"]}
+
+    def checked_body() -> torch.Tensor:
+        xy = batch_tokens()
+        st = _rng()
+        ar.suspend(True)
+        model.flat.zero_grad()
+        model(*xy).backward()
+        if hasattr(model.flat, "fill_unwritten"):
+            model.flat.fill_unwritten()
+        ar.suspend(False)
+        local = model.flat.grad.clone()
+        _set_rng(st)
+        ar.capture_local(True)
+
+        def verify():
+            ar.capture_local(False)
+            _record(ar.verify(local), ar.verify(local, against=ar.snapshot) if env["world"] > 1 else None)
+
+        return body(xy, before_opt=verify)
 
     captured = {}
 
@@ -249,6 +358,12 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
             captured["g"].replay()
             opt.note_replay()
             loss = captured["loss"].clone()
+            if check["pending"]:
+                check["pending"] = False
+                _record(ar.verify(ar.snapshot if env["world"] > 1 else ar.reduced_buffer()), None)
+        elif check["pending"] and not use_graph:
+            check["pending"] = False
+            loss = checked_body()
         else:
             loss = body()
         done[0] += 1
@@ -266,6 +381,8 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         losses.append(step())
     ar.wait_all_params()
     if use_graph:
+        if check["pending"]:
+            ar.capture_local(True)  # the captured finish() copies every bucket's input before its collective
         capture()
     sync()
     dist.barrier()
@@ -282,6 +399,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
     t = torch.tensor([dt], dtype=torch.float64, device=device if device.type == "cuda" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
+    fp1 = update_fp() if fingerprint else None
     if ckpt is not None:
         if not ckpt.has(done[0]):
             ckpt.save(done[0], gen)
@@ -307,7 +425,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "worst_devices": pl.get("worst"),
         "best_score": pl.get("best_score"),
         "worst_score": pl.get("worst_score"),
-        "global_batch": batch * env["world"],
+        "global_batch": local_batch * env["world"],
         "seq_len": None if mnist else seq,
         "steps": steps,
         "warmup": warmup,
@@ -320,6 +438,11 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "loss_last": float(losses[-1]),
         "losses": [float(x) for x in losses],
         "same_data": same_data,
+        "data_ranks": data_ranks or None,
+        "optimizer": optimizer,
+        "dropout": dropout,
+        "check_reduction": check["result"] if check_reduction else None,
+        "update_fingerprint": [b - a for a, b in zip(fp0, fp1)] if fingerprint else None,
         "repeat_batch": repeat_batch,
         "lr": lr,
         "buckets": ar.stats["buckets"],
@@ -395,6 +518,21 @@ def main(argv=None) -> int:
                     help="train on the first batch at every step: uniform random tokens carry nothing to learn, one "
                          "repeated batch does, so the loss must fall (end-to-end check of forward, backward and AdamW)")
     ap.add_argument("--lr", type=float, default=3e-4)
+    ap.add_argument("--optimizer", default="adamw", choices=["adamw", "sgd"],
+                    help="sgd: plain SGD on the fp32 master (the DP parity check: unlike AdamW, its update is linear "
+                         "in the gradient, so a reduction that did not run changes it)")
+    ap.add_argument("--check-reduction", action="store_true",
+                    help="check the first step's gradient reduction with different data per rank: the buffer the "
+                         "optimizer reads against the fp64 sum of every rank's local gradient (bf16 <= 1e-2, fp32 <= "
+                         "1e-3 relative, per bucket) and each bucket's collective input against the complete local "
+                         "gradient; the job exits 3 when it fails")
+    ap.add_argument("--data-ranks", type=int, default=0,
+                    help="1-rank job: train on the concatenation of these many ranks' batches (the k-rank parity "
+                         "reference)")
+    ap.add_argument("--dropout", default="on", choices=["on", "off"],
+                    help="MNIST dropout (off: the forward does not depend on how the batch is split over ranks)")
+    ap.add_argument("--fingerprint", action="store_true",
+                    help="report update_fingerprint: fixed projections of the fp32 master weights' change over the run")
     ap.add_argument("--grad-reduce", default="bf16", choices=["bf16", "fp32"],
                     help="DP gradient reduction dtype: bf16 in place, or fp32 (a widened copy reduced and applied in fp32)")
     ap.add_argument("--comm-ctas", type=int, default=DEFAULT_COMM_CTAS,
@@ -406,13 +544,18 @@ def main(argv=None) -> int:
     ap.add_argument("--comm-shadow-busbw", type=float, default=350.0,
                     help="--comm-shadow: per-rank bus GB/s that sets each emulated collective's duration")
     a = ap.parse_args(argv)
-    train(a.model, a.batch, a.seq, a.steps, a.warmup, a.device, a.placement, a.discovery, a.bucket_mb, a.checkpoint, lr=a.lr, attn=a.attn,
+    out = train(a.model, a.batch, a.seq, a.steps, a.warmup, a.device, a.placement, a.discovery, a.bucket_mb, a.checkpoint, lr=a.lr, attn=a.attn,
           gemm_tuning=a.gemm_tuning, gemm_table=a.gemm_table, zero1=a.zero1, save_dir=a.save_dir, save_every=a.save_every,
           resume=a.resume, keep=a.keep, same_data=a.same_data, graph=a.graph, conv=a.conv, cpu_bind=a.cpu_bind,
           repeat_batch=a.repeat_batch, grad_reduce=a.grad_reduce, comm_ctas=a.comm_ctas, comm_shadow=a.comm_shadow,
-          comm_shadow_k=a.comm_shadow_k, comm_shadow_busbw=a.comm_shadow_busbw)
+          comm_shadow_k=a.comm_shadow_k, comm_shadow_busbw=a.comm_shadow_busbw, optimizer=a.optimizer,
+          check_reduction=a.check_reduction, data_ranks=a.data_ranks, dropout=a.dropout == "on", fingerprint=a.fingerprint)
     if dist.is_initialized():
         dist.destroy_process_group()
+    cr = out.get("check_reduction")
+    if a.check_reduction and not (cr and cr.get("ok")):
+        print(json.dumps({"check_reduction_failed": cr}), file=sys.stderr, flush=True)
+        return 3
     return 0
 
 

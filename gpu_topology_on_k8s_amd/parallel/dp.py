@@ -177,7 +177,7 @@ class BucketedAllReduce:
         self.overlap = overlap
         esz = flat.grad.element_size()
         cap = max(1, int(bucket_mb * (1 << 20) / esz))
-        first_cap = max(1, int(first_bucket_mb * (1 << 20) / esz))
+        first_cap = min(cap, max(1, int(first_bucket_mb * (1 << 20) / esz)))  # never larger than the others
         # Parameters sit in the flat buffer in registration order, so reverse registration order
         # (the order backward finishes gradients) walks the buffer downwards and every bucket is
         # one contiguous range.  Bucket 0 (the first to complete) is capped smaller.
@@ -215,6 +215,10 @@ class BucketedAllReduce:
         # (A per-bucket clipping norm on a side stream as buckets land measured flat on MI355X --
         # hipBLASLt's GEMMs hold every CU -- and was retired in round 5: profiles/r01_fuse_res/NORM.md.)
         self._launched = [False] * len(self.buckets)
+        # reduction check (capture_local / verify): each bucket's local gradient as its collective saw it
+        self.snapshot: Optional[torch.Tensor] = None
+        self._capture = False
+        self._suspended = False
         if overlap and (self.world > 1 or self.shadow is not None):
             direct = getattr(flat, "direct", {})
             for n, p in flat.params.items():
@@ -226,6 +230,8 @@ class BucketedAllReduce:
 
     def _make_hook(self, name: str):
         def hook(p: torch.Tensor) -> None:
+            if self._suspended:
+                return
             b = self.buckets[self.bucket_of[name]]
             b.pending -= 1
             if b.pending == 0:
@@ -252,6 +258,8 @@ class BucketedAllReduce:
             return
         view = self.flat.grad[b.start:b.end]
         b.launched_at = time.perf_counter()
+        if self._capture:  # the exact input of this bucket's collective, copied on the launching stream
+            self.snapshot[b.start:b.end].copy_(view)
         if self.grad32 is not None:  # widen, then reduce in fp32
             buf = self.grad32[b.start:b.end]
             buf.copy_(view)
@@ -264,6 +272,60 @@ class BucketedAllReduce:
             b.work = dist.all_reduce(view, group=self.group, async_op=True)
         self.stats["launches"] += 1
         self.stats["comm_bytes"] += view.numel() * view.element_size()
+
+    # ---------------------------------------------------------------- reduction check
+    def suspend(self, on: bool) -> None:
+        """While suspended the readiness hooks launch nothing (a hook-free backward: the local gradient
+        of models/train.py's --check-reduction reference pass); leaving suspension resets the counts."""
+        self._suspended = bool(on)
+        if not on:
+            self.reset()
+
+    def capture_local(self, on: bool) -> None:
+        """While on, each bucket's local gradient is copied into :attr:`snapshot` on the launching
+        stream right before its collective is issued: exactly what that collective reduced."""
+        if on and self.snapshot is None:
+            self.snapshot = torch.zeros_like(self.flat.grad)
+        self._capture = bool(on)
+
+    def reduced_buffer(self) -> torch.Tensor:
+        """The buffer the optimizer reads after :meth:`finish` (fp32 under ``grad_reduce="fp32"``)."""
+        return self.grad32 if self.grad32 is not None else self.flat.grad
+
+    def _gather(self, x: torch.Tensor) -> List[torch.Tensor]:
+        if self.world == 1:
+            return [x]
+        raw = x.contiguous()
+        if raw.dtype not in (torch.float32, torch.float64):  # bit-exact through any backend (gloo has no bf16)
+            raw = raw.view(torch.uint8)
+        parts = [torch.empty_like(raw) for _ in range(self.world)]
+        dist.all_gather(parts, raw, group=self.group)
+        return [q.view(x.dtype) for q in parts]
+
+    def verify(self, local: torch.Tensor, against: Optional[torch.Tensor] = None) -> Dict[str, object]:
+        """Per bucket: the reduced gradient the optimizer reads (this rank's own range under zero1)
+        against the exact sum over ranks of ``local`` -- every rank's local gradient, all-gathered
+        bit-exactly and summed in fp64.  ``against``: compare with this buffer instead of the
+        reduced one, rank-locally (``snapshot`` vs a hook-free pass: was each bucket complete when its
+        collective launched?).  -> ``{"max_rel": worst relative L2 error, "buckets": [...]}``."""
+        out, worst = [], 0.0
+        for b in self.buckets:
+            s, e = self.own(b)
+            if against is None:
+                parts = self._gather(local[b.start:b.end])
+                exact = torch.zeros(e - s, dtype=torch.float64, device=local.device)
+                for q in parts:
+                    exact += q[s - b.start:e - b.start].double()
+                got = self.reduced_buffer()[s:e].double()
+            else:  # the whole bucket: every rank's snapshot holds its own local bucket
+                exact = local[b.start:b.end].double()
+                got = against[b.start:b.end].double()
+            den = float(exact.norm())
+            err = float((got - exact).norm())
+            rel = err / den if den > 0 else err
+            worst = max(worst, rel)
+            out.append({"index": b.index, "rel": rel})
+        return {"max_rel": worst, "buckets": out}
 
     def reset(self) -> None:
         for b in self.buckets:
