@@ -452,6 +452,11 @@ class DevicePluginServer:
             log.warning("link re-probe produced no usable topology")
             self.metrics.reprobes.labels("failed").inc()
             return False
+        # noise-equivalent links take their class value, kept from the published matrix while the new
+        # median stays within the band (ops/checks.py band_links): a healthy node republishes nothing
+        from ..ops.checks import apply_banding
+
+        apply_banding(new, prev=self.topology)
         delta = self.link_change(self.topology, new)
         if delta <= self.cfg.reprobe_tolerance:
             log.info("link re-probe: largest change %.1f%% (within tolerance)", 100 * delta)

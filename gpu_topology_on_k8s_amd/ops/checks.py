@@ -17,9 +17,20 @@ serialises its sources.  These checks anchor to absolute rates:
 * **Ring.** Every member pulling from all others at once (K6) must keep 60 % of the pair-sum bound
   (the sum of its single-pair reads), and cannot exceed it by more than 10 %.
 
-Reference: ``/root/reference/design.md:11`` (a job using n GPUs gets affine GPUs) and
-``design.md:25-27`` (link discovery); the checks make a wrong link matrix fail loudly instead of
-steering placements.
+**Banding** (:func:`band_links`).  On a full xGMI mesh every pair is one hop and
+the links are interchangeable, yet the measured GB/s differ by a few percent of noise; with cost =
+ref / GB/s that noise alone would pick the "best" pair, rank the worst subset and change the node
+annotation at every re-probe.  The probe repeats every pair (``repeats`` per preset) and records
+each link's spread; a link within max(its spread, its class's median spread, :data:`BAND_MIN`) of its
+link class's median takes the class value, so noise-equivalent links become exactly equal (the placement engine's symmetry
+breaking then decides, deterministically).  A link outside that band, or below its pair floor,
+keeps its measured number: a degraded link is still seen.  Given the previously published matrix a
+class keeps its previous value while the new median stays within the band of it, so a re-probe of a
+healthy node republishes the same numbers (the same cost annotation).
+
+Reference: ``/root/reference/design.md:11`` (a job using n GPUs gets affine GPUs),
+``design.md:25-27`` (link discovery) and ``design.md:47`` (the link weights TODO); the checks make a
+wrong link matrix fail loudly instead of steering placements.
 """
 from __future__ import annotations
 
@@ -39,6 +50,7 @@ PAIR_MEDIAN_FRACTION = 0.5
 GATHER_FRACTION = 0.5  # of (k-1) x median single-pair read
 RING_MIN_FRACTION = 0.6  # of the pair-sum bound
 RING_MAX_FRACTION = 1.1
+BAND_MIN = 0.03  # links within 3 % of their class median (or within their own repeat spread) are equal
 
 Pair = Tuple[int, int]
 
@@ -110,3 +122,67 @@ def check_ring(ring_bound_gbps: float, pair_sum_gbps: float) -> List[str]:
         probs.append(f"ring bound {ring_bound_gbps:.1f} GB/s above {RING_MAX_FRACTION} x pair-sum {pair_sum_gbps:.1f}: "
                      "the single-pair reads under-measure the links")
     return probs
+
+
+def link_class(topo: Topology, a: int, b: int) -> Tuple[int, int, bool]:
+    """Links the probe should find interchangeable: same link type, same hop count, and both ends on
+    one package or both on different packages (XCPs of one GPU talk over Infinity Fabric)."""
+    return int(topo.link_type[a, b]), int(topo.hops[a, b]), int(topo.physical[a]) == int(topo.physical[b])
+
+
+def band_links(topo: Topology, raw: np.ndarray, spread: Optional[np.ndarray] = None,
+               prev: Optional[np.ndarray] = None) -> Tuple[np.ndarray, Dict[str, object]]:
+    """``raw``: measured per-direction GB/s (n x n, nan = unmeasured); ``spread``: each link's relative
+    repeat spread ((max - min) / median over the probe's repeats; nan / None = unknown, taken as 0);
+    ``prev``: the previously published (banded) matrix, or None.  -> (banded matrix, report)."""
+    n = topo.n
+    raw = np.asarray(raw, dtype=np.float64)
+    sp = np.zeros((n, n)) if spread is None else np.nan_to_num(np.asarray(spread, dtype=np.float64), nan=0.0)
+    out = raw.copy()
+    meas = {(a, b): float(raw[a, b]) for a in range(n) for b in range(n) if a != b and np.isfinite(raw[a, b]) and raw[a, b] > 0}
+    floors = pair_floors(topo, meas)
+    classes: Dict[Tuple[int, int, bool], List[Pair]] = {}
+    for pr in meas:
+        classes.setdefault(link_class(topo, *pr), []).append(pr)
+    report: Dict[str, object] = {"band_min": BAND_MIN, "classes": [], "kept": []}
+    for key in sorted(classes):
+        prs = classes[key]
+        med = float(np.median([meas[p] for p in prs]))
+        cls_band = max(BAND_MIN, float(np.median([sp[p] for p in prs])))
+        value, reused = med, False
+        if prev is not None:
+            pv = [float(prev[p]) for p in prs if np.isfinite(prev[p]) and prev[p] > 0]
+            if pv:
+                pmed = float(np.median(pv))
+                if abs(med - pmed) <= cls_band * pmed:
+                    value, reused = pmed, True
+        snapped = 0
+        for p in prs:
+            band = max(cls_band, float(sp[p]))  # the class's typical repeat spread, or this link's own
+            if abs(meas[p] - med) <= band * med and meas[p] >= floors[p]:
+                out[p] = value
+                snapped += 1
+            else:
+                report["kept"].append([int(p[0]), int(p[1])])
+        report["classes"].append({"link_type": key[0], "hops": key[1], "same_package": key[2], "links": len(prs),
+                                  "median_gbps": round(med, 2), "value_gbps": round(value, 2), "snapped": snapped,
+                                  "reused_previous": reused})
+    report["kept_count"] = len(report["kept"])
+    report["kept"] = report["kept"][:64]  # the node annotation carries this report: bounded
+    return out, report
+
+
+def apply_banding(topo: Topology, prev: Optional[Topology] = None) -> bool:
+    """Re-derive ``topo``'s published matrix from the raw per-link measurements its probe recorded
+    (``probe["raw_gbps"]`` / ``probe["spread"]``), banded against ``prev``'s published matrix when
+    given.  False (nothing changed) when the topology carries no raw measurements."""
+    pr = topo.probe or {}
+    if pr.get("raw_gbps") is None:
+        return False
+    raw = np.array([[np.nan if x is None else float(x) for x in row] for row in pr["raw_gbps"]], dtype=np.float64)
+    sp = pr.get("spread")
+    spread = None if sp is None else np.array([[np.nan if x is None else float(x) for x in row] for row in sp])
+    pbw = prev.bw_gbps if (prev is not None and prev.bw_gbps is not None and prev.n == topo.n) else None
+    banded, rep = band_links(topo, raw, spread, pbw)
+    topo.set_measured_bw(banded, dict(pr, banding=rep))
+    return True

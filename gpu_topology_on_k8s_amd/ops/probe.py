@@ -29,10 +29,12 @@ __all__ = ["device_count", "device_props", "warmup", "copy_bw", "gather_bw", "me
            "probe_topology", "probe_in_child", "ingress_bound", "ring_peers", "ring_bw", "measure_ring", "ring_in_child",
            "PROBE_PRESETS"]
 
-#: bytes per transfer / timed iterations; sizes exceed the 256 MiB Infinity Cache for "full".
+#: bytes per transfer / timed iterations / repeats of every pair (the link's median is published, its
+#: spread decides which links are noise-equivalent: ops/checks.py band_links); sizes exceed the 256 MiB
+#: Infinity Cache for "full".
 PROBE_PRESETS: Dict[str, Dict[str, int]] = {
-    "quick": {"bytes": 64 << 20, "iters": 3, "warmup": 1},
-    "full": {"bytes": 512 << 20, "iters": 10, "warmup": 2},
+    "quick": {"bytes": 64 << 20, "iters": 3, "warmup": 1, "repeats": 5},
+    "full": {"bytes": 512 << 20, "iters": 10, "warmup": 2, "repeats": 5},
 }
 
 
@@ -245,19 +247,26 @@ def probe_topology(topo: Topology, preset: str = "quick", devs: Optional[List[in
     t0 = time.time()
     w = warmup(m.hip(devs[0]), warm_ms)
     bw = np.full((topo.n, topo.n), np.nan)
+    spread = np.full((topo.n, topo.n), np.nan)
     hbm = np.full(topo.n, np.nan)
     pairs, rep = _probe_pairs(topo, devs, by_package)
+    reps = max(1, int(cfg.get("repeats", 1)))
     for i, j in pairs:
         hi, hj = m.hip(i), m.hip(j)
         if i != j and not bool(_p().can_access_peer(hj if mode == "read" else hi, hi if mode == "read" else hj)):
             continue
-        r = copy_bw(hi, hj, cfg["bytes"], cfg["iters"], cfg["warmup"], mode=mode, kind=kind)
-        if not r["ok"]:
-            raise RuntimeError(f"probe verification failed for {i}->{j}")
+        vals = []
+        for _ in range(reps if i != j else 1):
+            r = copy_bw(hi, hj, cfg["bytes"], cfg["iters"], cfg["warmup"], mode=mode, kind=kind)
+            if not r["ok"]:
+                raise RuntimeError(f"probe verification failed for {i}->{j}")
+            vals.append(float(r["gbps"]))
         if i == j:
-            hbm[i] = r["gbps"]
+            hbm[i] = vals[0]
         else:
-            bw[i, j] = r["gbps"]
+            med = float(np.median(vals))
+            bw[i, j] = med
+            spread[i, j] = (max(vals) - min(vals)) / med if med > 0 else np.nan
     if rep is not None:  # partitioned node: every XCP pair takes its packages' measurement
         for i in devs:
             hbm[i] = hbm[rep[(i, i)][0]] if np.isnan(hbm[i]) else hbm[i]
@@ -265,11 +274,22 @@ def probe_topology(topo: Topology, preset: str = "quick", devs: Optional[List[in
             for j in devs:
                 if i != j and np.isnan(bw[i, j]):
                     a, b = rep[(i, j)]
-                    bw[i, j] = bw[a, b]
+                    bw[i, j], spread[i, j] = bw[a, b], spread[a, b]
     topo.hbm_gbps = hbm
+    from .checks import band_links
+
+    banded, band_report = band_links(topo, bw, spread)
+
+    def _rows(x, nd):
+        return [[None if not np.isfinite(v) else round(float(v), nd) for v in row] for row in x]
+
     topo.set_measured_bw(
-        bw,
+        banded,
         {
+            "raw_gbps": _rows(bw, 2),
+            "spread": _rows(spread, 4),
+            "repeats": reps,
+            "banding": band_report,
             "method": f"p2p_{mode}_{kind}",
             "preset": preset,
             "bytes": cfg["bytes"],

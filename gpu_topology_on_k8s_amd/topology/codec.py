@@ -81,6 +81,12 @@ def encode_v2(topo) -> Dict[str, Any]:
     if topo.ref_class is not None:
         m["ref_class"] = pack_matrix(topo.ref_class, "u8")
     probe = dict(topo.probe or {})
+    for key in ("raw_gbps", "spread"):  # the probe's per-link medians and repeat spreads (ops/checks.py banding)
+        v = probe.pop(key, None)
+        if v is not None:
+            a = np.array([[np.nan if x is None else float(x) for x in row] for row in v], dtype=np.float64)
+            if a.shape == (n, n):
+                m[key] = pack_matrix(a, "f16")
     mx = probe.pop("amdsmi_max_bw_mbps", None)
     if mx is not None:
         mx = np.asarray(mx, dtype=np.float64)
@@ -123,6 +129,10 @@ def decode_v2(d: Dict[str, Any]):
         return unpack_matrix(m[key], n) if key in m else None
 
     probe = dict(d.get("probe") or {})
+    for key in ("raw_gbps", "spread"):
+        a = mat(key)
+        if a is not None:
+            probe[key] = [[None if not math.isfinite(x) else float(x) for x in row] for row in a.tolist()]
     mx = mat("max_bw_mbps")
     if mx is not None:
         probe["amdsmi_max_bw_mbps"] = mx.tolist()
