@@ -22,7 +22,7 @@ import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, Iterable, List, Optional, Set, Tuple
 
-from ..k8s.annotations import Contract, PodAssignment, decode_node_annotations, probing_until
+from ..k8s.annotations import Contract, PodAssignment, decode_node_annotations, ledger_gen, parse_ledger, probing_until
 from ..k8s.api import KubeAPI
 from ..k8s.objects import annotations as obj_annotations
 from ..k8s.objects import labels as obj_labels
@@ -30,6 +30,10 @@ from ..k8s.objects import meta, pod_gpu_request, pod_is_terminal, pod_key, pod_n
 from ..topology.model import Topology
 
 log = logging.getLogger(__name__)
+
+# a node-ledger entry whose pod no LIST has shown on the node this long after its bind is a bind that
+# failed or was lost: its devices are free again (extender/scheduler.py bind)
+LEDGER_GRACE_S = 30.0
 
 __all__ = ["Alloc", "NodeState", "ClusterCache"]
 
@@ -56,6 +60,12 @@ class NodeState:
     unknown_uids: Dict[str, str] = field(default_factory=dict)  # pod UID -> pod key of unknown_pods
     capacity: int = -1  # node.status.allocatable[resource] (-1 = unknown)
     probing_until: float = 0.0  # the device plugin's re-probe mark (<prefix>/probing): skip the node until then
+    # the node's allocation ledger (<prefix>/gpu-ledger, written by every extender's bind under a
+    # resourceVersion precondition): pod key -> (ids, bind time).  An entry covers a bind in flight;
+    # once a LIST has shown its pod on the node (`settled`) the pod's own annotation governs
+    ledger: Dict[str, Tuple[Tuple[int, ...], float]] = field(default_factory=dict)
+    ledger_gen: int = 0
+    settled: Set[str] = field(default_factory=set)
     synced_at: float = 0.0
     list_epoch: int = -1  # epoch of the newest pod LIST applied (older LISTs arriving late are stale)
     lock: threading.RLock = field(default_factory=threading.RLock, repr=False)
@@ -77,7 +87,17 @@ class NodeState:
         for a in self.allocs.values():
             if not a.assigned and now - a.assume_time <= ttl:
                 t = min(t, a.assume_time + ttl)
+        for key, (_, at) in self.ledger_live(now, ttl).items():
+            t = min(t, at + min(ttl, LEDGER_GRACE_S))
         return t
+
+    def ledger_live(self, now: float, ttl: float, grace: float = None) -> Dict[str, Tuple[Tuple[int, ...], float]]:
+        """Ledger entries that still hold their devices: binds in flight -- younger than ``grace`` (and
+        ``ttl``) and whose pod no LIST has shown on the node yet.  The rest are what the next ledger
+        write drops (a settled pod's annotation governs; an entry past the grace is a failed bind)."""
+        g_s = LEDGER_GRACE_S if grace is None else grace
+        return {k: (g, t) for k, (g, t) in self.ledger.items()
+                if now - t <= min(ttl, g_s) and k not in self.settled}
 
     @property
     def unknown(self) -> int:
@@ -89,6 +109,9 @@ class NodeState:
         for a in self.allocs.values():
             if a.assigned or (now - a.assume_time) <= ttl:
                 out.update(a.ids)
+        for key, (ids, _) in self.ledger_live(now, ttl).items():
+            if key not in self.allocs:  # being bound by another extender, not yet seen on a pod annotation
+                out.update(ids)
         return out
 
     def free_count(self, now: float, ttl: float) -> int:
@@ -145,6 +168,12 @@ class ClusterCache:
                 st.node_rv = rv
             st.labels = labels
             st.probing_until = probing_until(obj_annotations(node), self.contract)
+            ledger = parse_ledger(obj_annotations(node), self.contract)
+            st.ledger_gen = ledger_gen(obj_annotations(node), self.contract)
+            if ledger != st.ledger:
+                st.ledger = ledger
+                st.settled &= set(ledger)
+                st.bump()
             alloc = ((node.get("status") or {}).get("allocatable") or {})
             st.capacity = -1
             for r in self.resources:
@@ -221,6 +250,10 @@ class ClusterCache:
         st.allocs = allocs
         st.unknown_pods = unknown
         st.unknown_uids = unknown_uids
+        settled = st.settled | (seen & set(st.ledger))
+        if settled != st.settled:
+            st.settled = settled
+            st.bump()
         st.synced_at = now
 
     def refresh_node(self, name: str) -> NodeState:

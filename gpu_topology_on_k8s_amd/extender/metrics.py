@@ -36,6 +36,10 @@ class ExtenderMetrics:
         self.decision_cache = Counter("gtk_extender_decision_cache_total", "placement decisions served from / added to the cache",
                                       ["result"], registry=self.registry)
 
+        self.ledger_conflict = Counter("gtk_extender_ledger_conflicts_total",
+                                       "binds whose node allocation ledger changed under them (409): re-decided",
+                                       registry=self.registry)
+        self.ledger_conflicts = 0
         self.probing_skips = Counter("gtk_extender_probing_skips_total",
                                      "node evaluations skipped because the node's device plugin is re-probing its links",
                                      registry=self.registry)

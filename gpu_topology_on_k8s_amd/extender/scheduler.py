@@ -41,8 +41,8 @@ from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
-from ..k8s.annotations import ANN_ASSIGNED, ANN_ASSUME_TIME, ANN_GROUP, Contract, PodAssignment
-from ..k8s.api import ApiError, KubeAPI
+from ..k8s.annotations import ANN_ASSIGNED, ANN_ASSUME_TIME, ANN_GROUP, Contract, PodAssignment, dump_ledger
+from ..k8s.api import ApiError, Conflict, KubeAPI
 from ..k8s.events import record_event
 from ..k8s.objects import annotations as obj_annotations
 from ..k8s.objects import labels as obj_labels
@@ -87,6 +87,11 @@ class ExtenderConfig:
     # pods whose spec.schedulerName is not listed are refused at bind (empty = any scheduler)
     scheduler_names: Tuple[str, ...] = ()
     events: bool = True
+    # the node allocation ledger (Contract.ledger_key): every bind records its device set on the Node
+    # with a resourceVersion precondition, so concurrent extender instances cannot overlap; a 409
+    # re-reads the node and re-decides, up to `ledger_attempts` times
+    ledger: bool = True
+    ledger_attempts: int = 8
 
 
 @dataclass
@@ -468,45 +473,36 @@ class TopologyExtender:
             sched = (pod.get("spec") or {}).get("schedulerName") or "default-scheduler"
             if self.cfg.scheduler_names and sched not in self.cfg.scheduler_names:
                 raise ApiError(403, f"pod {namespace}/{name} uses scheduler {sched!r}, not one of {list(self.cfg.scheduler_names)}")
-            # refresh (2 API calls) BEFORE taking the node lock; the decision below uses only cached
-            # state, so a bind never holds one node's lock while waiting for another's
-            self.cache.refresh_node(node)
-            st = self.cache.get(node, sync=False)
-            with st.lock:  # serialise select+annotate+bind per node
-                d, why = self._eval_state(pod, node, st, k)
-                if d is None:
-                    raise NoFeasiblePlacement(f"bind {namespace}/{name} on {node}: {why}")
-                d = dataclasses.replace(d, cpuset=recommended_cpuset(st.topology, d.ids))  # memo entries stay unshared
-                key = pod_key(pod)
-                now = self.clock()
-                pa = PodAssignment.assumed(d.ids, now)
-                ann = pa.to_annotations()
-                t = st.topology
-                numa = sorted({t.gpus[i].numa for i in d.ids}) if t is not None else []
-                ann[self.cfg.contract.numa_key] = ",".join(str(x) for x in numa)
-                if d.cpuset:
-                    ann[self.cfg.contract.cpuset_key] = d.cpuset
-                ann[self.cfg.contract.score_key] = f"{d.score:.3f}"
-                self.cache.assume(node, key, d.ids, now, cpuset=d.cpuset, uid=uid or str(meta(pod).get("uid", "")))
-                try:
-                    self._patch_with_retry(namespace, name, ann)
-                    self.api.bind_pod(namespace, name, uid, node)
-                    self.cache.bound(node, key)
-                except Exception:
-                    self.cache.forget(node, key)
-                    try:  # roll back the annotation so a retry starts clean
-                        self.api.patch_pod_annotations(namespace, name, {ANN_GROUP: None, ANN_ASSIGNED: None, ANN_ASSUME_TIME: None,
-                                                                         self.cfg.contract.cpuset_key: None})
-                    except Exception as e2:  # pragma: no cover - best effort
-                        log.warning("rollback of %s/%s annotations failed: %s", namespace, name, e2)
-                    raise
-                self.metrics.bound(d)
-                log.info("bound %s to %s devices %s score %.2f (%s)", key, node, list(d.ids), d.score, d.policy)
-                if self.cfg.events:
-                    record_event(self.api, pod, "GPUTopologyBound",
-                                 f"assigned devices {list(d.ids)} on {node} (score {d.score:.2f}, {d.policy})",
-                                 component="gpu-topology-extender")
-                return d
+            key = pod_key(pod)
+            for attempt in range(max(1, self.cfg.ledger_attempts)):
+                # refresh (2 API calls) BEFORE taking the node lock; the decision below uses only cached
+                # state, so a bind never holds one node's lock while waiting for another's
+                self.cache.refresh_node(node)
+                st = self.cache.get(node, sync=False)
+                with st.lock:  # serialise select+annotate+bind per node (in this process)
+                    d, why = self._eval_state(pod, node, st, k)
+                    if d is None:
+                        raise NoFeasiblePlacement(f"bind {namespace}/{name} on {node}: {why}")
+                    d = dataclasses.replace(d, cpuset=recommended_cpuset(st.topology, d.ids))  # memo entries stay unshared
+                    now = self.clock()
+                    if self.cfg.ledger:
+                        # across processes: record the set on the Node, conditional on the node being
+                        # exactly what this decision saw; another extender's bind in between -> 409
+                        entries = st.ledger_live(now, self.cfg.assume_ttl)
+                        entries[key] = (tuple(d.ids), now)
+                        gen = st.ledger_gen + 1
+                        try:
+                            self.api.patch_node(node, annotations={self.cfg.contract.ledger_key: dump_ledger(entries, gen)},
+                                                resource_version=st.node_rv)
+                        except Conflict:
+                            self.metrics.ledger_conflicts += 1
+                            self.metrics.ledger_conflict.inc()
+                            log.info("bind %s on %s: node changed since the decision (attempt %d); re-deciding",
+                                     key, node, attempt + 1)
+                            continue
+                    return self._commit(pod, namespace, name, uid, node, key, d, st, now)
+            raise ApiError(409, f"bind {namespace}/{name} on {node}: the node's allocation ledger kept changing "
+                                f"({self.cfg.ledger_attempts} attempts)")
         except Exception as e:
             if self.cfg.events and pod is not None:
                 record_event(self.api, pod, "FailedGPUTopologyBind", f"bind to {node} failed: {e}", "Warning",
@@ -514,6 +510,62 @@ class TopologyExtender:
             raise
         finally:
             self.metrics.observe("bind", time.perf_counter() - t0)
+
+    def _commit(self, pod, namespace: str, name: str, uid: str, node: str, key: str, d: Decision, st: NodeState,
+                now: float) -> Decision:
+        """Under ``st.lock``, the devices recorded: annotate the pod, bind it; undo everything on failure."""
+        pa = PodAssignment.assumed(d.ids, now)
+        ann = pa.to_annotations()
+        t = st.topology
+        numa = sorted({t.gpus[i].numa for i in d.ids}) if t is not None else []
+        ann[self.cfg.contract.numa_key] = ",".join(str(x) for x in numa)
+        if d.cpuset:
+            ann[self.cfg.contract.cpuset_key] = d.cpuset
+        ann[self.cfg.contract.score_key] = f"{d.score:.3f}"
+        self.cache.assume(node, key, d.ids, now, cpuset=d.cpuset, uid=uid or str(meta(pod).get("uid", "")))
+        try:
+            self._patch_with_retry(namespace, name, ann)
+            self.api.bind_pod(namespace, name, uid, node)
+            self.cache.bound(node, key)
+        except Exception:
+            self.cache.forget(node, key)
+            try:  # roll back the annotation so a retry starts clean
+                self.api.patch_pod_annotations(namespace, name, {ANN_GROUP: None, ANN_ASSIGNED: None, ANN_ASSUME_TIME: None,
+                                                                 self.cfg.contract.cpuset_key: None})
+            except Exception as e2:  # pragma: no cover - best effort
+                log.warning("rollback of %s/%s annotations failed: %s", namespace, name, e2)
+            if self.cfg.ledger:
+                self._ledger_release(node, key)
+            raise
+        self.metrics.bound(d)
+        log.info("bound %s to %s devices %s score %.2f (%s)", key, node, list(d.ids), d.score, d.policy)
+        if self.cfg.events:
+            record_event(self.api, pod, "GPUTopologyBound",
+                         f"assigned devices {list(d.ids)} on {node} (score {d.score:.2f}, {d.policy})",
+                         component="gpu-topology-extender")
+        return d
+
+    def _ledger_release(self, node: str, key: str, attempts: int = 4) -> None:
+        """Drop ``key``'s ledger entry after a failed bind (best effort; the entry also lapses on its own
+        once older than the grace period with no such pod on the node)."""
+        from ..k8s.annotations import ledger_gen, parse_ledger
+
+        for _ in range(attempts):
+            try:
+                n = self.api.get_node(node)
+                ann = obj_annotations(n)
+                entries = parse_ledger(ann, self.cfg.contract)
+                if key not in entries:
+                    return
+                del entries[key]
+                self.api.patch_node(node, annotations={self.cfg.contract.ledger_key: dump_ledger(entries, ledger_gen(ann, self.cfg.contract) + 1)},
+                                    resource_version=str(meta(n).get("resourceVersion", "")))
+                return
+            except Conflict:
+                continue
+            except Exception as e:  # noqa: BLE001 - best effort
+                log.warning("releasing the ledger entry of %s on %s failed: %s", key, node, e)
+                return
 
     def preempt(self, pod: Dict[str, Any], victims: Dict[str, Tuple[List[str], int]],
                 max_subsets: int = 4096) -> Dict[str, Tuple[List[str], int]]:

@@ -74,6 +74,15 @@ class Contract:
         return f"{self.prefix}/probing"
 
     @property
+    def ledger_key(self) -> str:
+        """Node annotation: the device sets the extenders have bound onto the node and not yet seen
+        settle, ``{"gen": N, "a": {"<ns>/<pod>": {"g": [ids], "t": unix time}}}``.  Written in bind with
+        the node's resourceVersion as a precondition, so two extender instances (a scheduler leader
+        failover, a DaemonSet of extenders) cannot both hand out one node's free devices: the second
+        writer gets 409, re-reads and re-decides (extender/scheduler.py)."""
+        return f"{self.prefix}/gpu-ledger"
+
+    @property
     def numa_key(self) -> str:
         """Pod annotation: NUMA node(s) of the assigned devices (Gaia B6)."""
         return f"{self.prefix}/numa-nodes"
@@ -242,6 +251,31 @@ def probing_until(ann: Mapping[str, str], contract: Contract = Contract()) -> fl
         return float(raw) if raw not in (None, "") else 0.0
     except (TypeError, ValueError):
         return 0.0
+
+
+def parse_ledger(ann: Mapping[str, str], contract: Contract = Contract()) -> Dict[str, Tuple[Tuple[int, ...], float]]:
+    """Entries of a node's allocation ledger (``Contract.ledger_key``): pod key -> (device ids, unix
+    time of the bind).  A malformed ledger reads as empty (the next bind rewrites it)."""
+    raw = ann.get(contract.ledger_key)
+    if not raw:
+        return {}
+    try:
+        d = json.loads(raw)
+        return {str(k): (tuple(int(i) for i in v["g"]), float(v["t"])) for k, v in (d.get("a") or {}).items()}
+    except (ValueError, TypeError, KeyError, AttributeError):
+        return {}
+
+
+def ledger_gen(ann: Mapping[str, str], contract: Contract = Contract()) -> int:
+    try:
+        return int(json.loads(ann.get(contract.ledger_key) or "{}").get("gen", 0))
+    except (ValueError, TypeError, AttributeError):
+        return 0
+
+
+def dump_ledger(entries: Mapping[str, Tuple[Sequence[int], float]], gen: int) -> str:
+    return json.dumps({"gen": int(gen), "a": {k: {"g": [int(i) for i in g], "t": round(float(t), 3)}
+                                               for k, (g, t) in sorted(entries.items())}}, separators=(",", ":"))
 
 
 def annotations_size(ann: Mapping[str, str]) -> int:

@@ -68,8 +68,9 @@ class KubeAPI:
         raise NotImplementedError
 
     def patch_node(self, name: str, annotations: Optional[Dict[str, Optional[str]]] = None,
-                   labels: Optional[Dict[str, Optional[str]]] = None) -> Obj:
-        """JSON merge patch of node metadata (a ``None`` value deletes the key)."""
+                   labels: Optional[Dict[str, Optional[str]]] = None, resource_version: Optional[str] = None) -> Obj:
+        """JSON merge patch of node metadata (a ``None`` value deletes the key); with
+        ``resource_version`` the patch is conditional (409 when the node changed since)."""
         raise NotImplementedError
 
     def get_pod(self, namespace: str, name: str) -> Obj:
@@ -187,12 +188,14 @@ class RestKubeAPI(KubeAPI):
     def list_nodes(self, label_selector: Optional[str] = None) -> List[Obj]:
         return self._do("GET", "/api/v1/nodes" + _selector_q(label_selector)).get("items", [])
 
-    def patch_node(self, name, annotations=None, labels=None) -> Obj:
+    def patch_node(self, name, annotations=None, labels=None, resource_version=None) -> Obj:
         md: Obj = {}
         if annotations is not None:
             md["annotations"] = annotations
         if labels is not None:
             md["labels"] = labels
+        if resource_version is not None:  # the apiserver enforces it as a precondition (409 Conflict)
+            md["resourceVersion"] = str(resource_version)
         return self._do("PATCH", f"/api/v1/nodes/{quote(name)}", {"metadata": md}, "application/merge-patch+json")
 
     def get_pod(self, namespace: str, name: str) -> Obj:

@@ -231,10 +231,12 @@ class FakeAPIServer(KubeAPI):
             self._enter("list_nodes")
             return [copy.deepcopy(n) for n in self.nodes.values() if _match_labels(n, label_selector)]
 
-    def patch_node(self, name, annotations=None, labels=None) -> Obj:
+    def patch_node(self, name, annotations=None, labels=None, resource_version=None) -> Obj:
         with self._lock:
             self._enter("patch_node")
             node = self._node(name)
+            if resource_version is not None and str(resource_version) != meta(node).get("resourceVersion"):
+                raise Conflict(f"node {name}: resourceVersion {resource_version} is stale")
             md: Obj = {}
             if annotations is not None:
                 md["annotations"] = annotations
@@ -330,7 +332,8 @@ class _Handler(BaseHTTPRequestHandler):
                     return self._send(200, self.api.get_node(rest[1]))
                 if method == "PATCH":
                     md = self._body().get("metadata", {})
-                    return self._send(200, self.api.patch_node(rest[1], md.get("annotations"), md.get("labels")))
+                    return self._send(200, self.api.patch_node(rest[1], md.get("annotations"), md.get("labels"),
+                                                               md.get("resourceVersion")))
             node_name = None
             fs = (q.get("fieldSelector") or [""])[0]
             if fs.startswith("spec.nodeName="):

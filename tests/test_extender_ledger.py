@@ -1,0 +1,157 @@
+"""Bind safety across extender instances.
+
+Each :class:`TopologyExtender` serialises select -> annotate -> bind per node with an in-process lock,
+but the extender runs as several instances (a DaemonSet on the control-plane nodes; two leaders across
+a scheduler failover).  Every bind therefore records its device set in the node's allocation ledger
+(``<prefix>/gpu-ledger``) with the node's resourceVersion as a precondition; a second instance that
+decided on the same state gets 409, re-reads the node and re-decides.  Two instances share one
+FakeAPIServer here, which enforces the precondition as the apiserver does; each has its own cache.
+"""
+import threading
+
+from gpu_topology_on_k8s_amd.extender import ExtenderConfig, TopologyExtender
+from gpu_topology_on_k8s_amd.k8s import Contract, FakeAPIServer
+from gpu_topology_on_k8s_amd.k8s.annotations import encode_node_annotations, parse_ledger
+from gpu_topology_on_k8s_amd.k8s.objects import annotations as obj_annotations
+from gpu_topology_on_k8s_amd.k8s.objects import make_node, make_pod
+from gpu_topology_on_k8s_amd.topology import fixtures as fx
+
+
+class Clock:
+    def __init__(self, t=1_700_000_000.0):
+        self.t = t
+
+    def __call__(self):
+        return self.t
+
+
+def _two(ledger=True, n_pods=0, k=1):
+    api = FakeAPIServer()
+    c = Contract()
+    t = fx.f7_mi355x()
+    api.create_node(make_node("n1", labels={c.label_model: "MI355X"}, annotations=encode_node_annotations(t, c),
+                              capacity={c.resource_name: str(t.n)}))
+    clock = Clock()
+    exts = [TopologyExtender(api, ExtenderConfig(resync_s=0.0, ledger=ledger, events=False), clock=clock) for _ in range(2)]
+    for i in range(n_pods):
+        api.create_pod(make_pod(f"p{i}", gpus=k))
+    return api, exts, clock
+
+
+def _bind(api, ext, name):
+    pod = api.get_pod("default", name)
+    return ext.bind("default", name, pod["metadata"]["uid"], "n1")
+
+
+def _lockstep(exts):
+    """Both instances read the node before either writes anything (the failover window, made certain):
+    their first refresh before a bind waits for the other's."""
+    gate = threading.Barrier(2, timeout=10)
+    for e in exts:
+        real = e.cache.refresh_node
+        first = [True]
+
+        def refresh(name, _real=real, _first=first):
+            st = _real(name)
+            if _first[0]:
+                _first[0] = False
+                gate.wait()
+            return st
+
+        e.cache.refresh_node = refresh
+
+
+def _race(api, exts):
+    out = {}
+
+    def go(i):
+        out[i] = _bind(api, exts[i], f"p{i}").ids
+
+    ts = [threading.Thread(target=go, args=(i,)) for i in (0, 1)]
+    [t.start() for t in ts]
+    [t.join(timeout=30) for t in ts]
+    return out
+
+
+def test_without_the_ledger_two_instances_hand_out_the_same_device():
+    """The hazard being fixed: two instances deciding on the same state pick the same best device."""
+    api, exts, _ = _two(ledger=False, n_pods=2)
+    _lockstep(exts)
+    out = _race(api, exts)
+    assert set(out[0]) & set(out[1])
+
+
+def test_with_the_ledger_the_second_instance_redecides():
+    api, exts, _ = _two(ledger=True, n_pods=2)
+    _lockstep(exts)
+    out = _race(api, exts)
+    assert not set(out[0]) & set(out[1]), out
+    assert exts[0].metrics.ledger_conflicts + exts[1].metrics.ledger_conflicts >= 1
+    groups = [obj_annotations(api.get_pod("default", f"p{i}"))["ALIYUN_COM_GPU_GROUP"] for i in (0, 1)]
+    assert groups[0] != groups[1]
+
+
+def test_fifty_concurrent_pods_on_one_node_never_overlap():
+    api, exts, _ = _two(ledger=True, n_pods=50)
+    res = {}
+    gate = threading.Barrier(50, timeout=30)
+
+    def go(i):
+        gate.wait()
+        try:
+            res[i] = _bind(api, exts[i % 2], f"p{i}").ids
+        except Exception as e:  # noqa: BLE001 - no free device / ledger contention: kube-scheduler retries
+            res[i] = e
+
+    ts = [threading.Thread(target=go, args=(i,)) for i in range(50)]
+    [t.start() for t in ts]
+    [t.join(timeout=60) for t in ts]
+    got = [r for r in res.values() if isinstance(r, tuple)]
+    flat = [d for g in got for d in g]
+    assert len(flat) == len(set(flat)) and len(flat) <= 8, got
+    # the pods that lost retry, one at a time (what kube-scheduler does): the node fills exactly
+    for i in sorted(res):
+        if not isinstance(res[i], tuple) and len(flat) < 8:
+            res[i] = _bind(api, exts[i % 2], f"p{i}").ids
+            flat += list(res[i])
+    assert sorted(flat) == list(range(8))
+    ann = {i: obj_annotations(api.get_pod("default", f"p{i}")).get("ALIYUN_COM_GPU_GROUP") for i in range(50)}
+    held = [int(x) for v in ann.values() if v for x in v.split(",")]
+    assert sorted(held) == list(range(8))  # GROUP annotations: every device exactly once
+
+
+def test_ledger_entries_settle_and_lapse():
+    """An entry covers a bind in flight only: once a LIST shows the pod on the node its own annotation
+    governs (the next ledger write drops the entry), and an entry whose pod never appears lapses after
+    the grace period (a bind that failed after recording its devices)."""
+    from gpu_topology_on_k8s_amd.extender.cache import LEDGER_GRACE_S
+    from gpu_topology_on_k8s_amd.k8s.annotations import dump_ledger
+
+    api, exts, clock = _two(ledger=True, n_pods=3)
+    d0 = _bind(api, exts[0], "p0")
+    led = parse_ledger(obj_annotations(api.get_node("n1")))
+    assert set(led) == {"default/p0"} and led["default/p0"][0] == d0.ids
+    d1 = _bind(api, exts[1], "p1")
+    led = parse_ledger(obj_annotations(api.get_node("n1")))
+    assert set(led) == {"default/p1"}  # p0 settled (listed on the node): dropped
+    assert not set(d0.ids) & set(d1.ids)
+    # a lost bind: recorded, never annotated nor bound
+    c = Contract()
+    api.patch_node("n1", annotations={c.ledger_key: dump_ledger({"default/ghost": ((7,), clock.t)}, 99)})
+    d2 = _bind(api, exts[0], "p2")
+    assert 7 not in d2.ids
+    api.delete_pod("default", "p2")
+    clock.t += LEDGER_GRACE_S + 1
+    api.create_pod(make_pod("p3", gpus=6))
+    d3 = _bind(api, exts[1], "p3")
+    assert 7 in d3.ids  # the ghost's device is free again
+
+
+def test_failed_bind_releases_its_ledger_entry():
+    api, exts, _ = _two(ledger=True, n_pods=1)
+    api.inject("bind_pod", 500)
+    try:
+        _bind(api, exts[0], "p0")
+    except Exception:  # noqa: BLE001 - the injected apiserver failure
+        pass
+    assert "default/p0" not in parse_ledger(obj_annotations(api.get_node("n1")))
