@@ -42,7 +42,20 @@ __all__ = ["train", "main"]
 PEAK_BF16_FLOPS = 2.5e15  # MI355X dense bf16 (MI355X_MICROARCH.md), per GPU
 
 
-def _init_dist(device_kind: str, comm_ctas: int = 0) -> Dict[str, int]:
+AUTO_CTAS = (32, 64, 128)  # --comm-ctas auto: the candidates around the one-GPU shadow sweep's knee
+
+
+def _comm_group(ctas: int):
+    """A process group over every rank with RCCL's CTAs per collective capped at ``ctas`` (gloo: a
+    plain group, so the selection logic runs in CPU tests)."""
+    if dist.get_backend() == "nccl":
+        from ..parallel.dp import nccl_options
+
+        return dist.new_group(backend="nccl", pg_options=nccl_options(max_ctas=ctas))
+    return dist.new_group(backend="gloo")
+
+
+def _init_dist(device_kind: str, comm_ctas=0) -> Dict[str, int]:
     if "RANK" not in os.environ:
         os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
@@ -54,7 +67,7 @@ def _init_dist(device_kind: str, comm_ctas: int = 0) -> Dict[str, int]:
         rehearse = device_kind == "cuda" and os.environ.get("GTK_REHEARSE_ON_ONE_GPU") == "1"
         backend = "gloo" if rehearse or device_kind != "cuda" else "nccl"
         kw = {}
-        if backend == "nccl" and comm_ctas:
+        if backend == "nccl" and comm_ctas and comm_ctas != "auto":
             from ..parallel.dp import nccl_options
 
             kw["pg_options"] = nccl_options(max_ctas=comm_ctas)  # RCCL's CTAs per collective, capped
@@ -120,7 +133,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
           zero1: bool = False, save_dir: Optional[str] = None, save_every: int = 0, resume: Optional[str] = None,
           keep: int = 2, same_data: bool = False,
           graph: str = "auto", conv: str = "hip", cpu_bind: str = "auto", repeat_batch: bool = False,
-          persistent_wt: bool = True, grad_reduce: str = "bf16", comm_ctas: int = DEFAULT_COMM_CTAS,
+          persistent_wt: bool = True, grad_reduce: str = "bf16", comm_ctas="auto",
           comm_shadow: int = 0, comm_shadow_k: int = 8, comm_shadow_busbw: float = 350.0,
           optimizer: str = "adamw", check_reduction: bool = False, data_ranks: int = 0, dropout: bool = True,
           fingerprint: bool = False) -> Dict[str, object]:
@@ -202,8 +215,11 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
 
         shadow = CommShadow(device, comm_shadow, k=comm_shadow_k, busbw_gbps=comm_shadow_busbw,
                             max_bucket_bytes=int(bucket_mb * (1 << 20)))
-    ar = BucketedAllReduce(model.flat, bucket_mb=bucket_mb, zero1=zero1, overlap=not use_graph,
-                           grad_reduce=grad_reduce, shadow=shadow)
+    def make_ar(group=None) -> BucketedAllReduce:
+        return BucketedAllReduce(model.flat, group=group, bucket_mb=bucket_mb, zero1=zero1, overlap=not use_graph,
+                                 grad_reduce=grad_reduce, shadow=shadow)
+
+    ar = make_ar()
     if optimizer == "sgd":
         if use_graph and getattr(model.flat, "data_t", None) is not None:
             raise ValueError("--optimizer sgd with --graph: the captured step would keep a stale W^T")
@@ -380,6 +396,37 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
     for _ in range(max(warmup, 1) if use_graph else warmup):
         losses.append(step())
     ar.wait_all_params()
+    cta_table = None
+    if comm_ctas == "auto" and env["world"] > 1 and not use_graph:
+        # the first k >= 2 run confirms the CTA cap the one-GPU comm shadow chose:
+        # one communicator per candidate cap, a settling step and two timed steps on each (max over
+        # ranks), then the rest of the run on the fastest.  These steps train like warmup steps.
+        cta_table, groups = [], {}
+        for c in AUTO_CTAS:
+            groups[c] = _comm_group(c)
+            ar.remove()
+            ar = make_ar(groups[c])
+            if zero1:
+                model.param_ready = ar.wait_param
+            step()
+            ar.wait_all_params()
+            sync()
+            dist.barrier()
+            ta = time.perf_counter()
+            for _ in range(2):
+                step()
+            ar.wait_all_params()
+            sync()
+            tt = torch.tensor([time.perf_counter() - ta], dtype=torch.float64,
+                              device=device if device.type == "cuda" else "cpu")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            cta_table.append({"ctas": c, "ms_per_step": float(tt.item()) / 2 * 1e3})
+        best = min(cta_table, key=lambda r: r["ms_per_step"])["ctas"]
+        ar.remove()
+        ar = make_ar(groups[best])
+        if zero1:
+            model.param_ready = ar.wait_param
+        comm_ctas = best
     if use_graph:
         if check["pending"]:
             ar.capture_local(True)  # the captured finish() copies every bucket's input before its collective
@@ -453,6 +500,7 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "gemm_layout": gemm_layout,
         "grad_reduce": grad_reduce,
         "comm_ctas": comm_ctas or None,
+        "comm_ctas_tuning": cta_table,
         "comm_shadow": ({"ctas": shadow.ctas, "k": shadow.k, "busbw_gbps": shadow.busbw,
                          "collectives_per_step": shadow.launched / max(1, done[0] - start_step),
                          "ring_bytes_per_step": shadow.bytes / max(1, done[0] - start_step),
@@ -535,9 +583,11 @@ def main(argv=None) -> int:
                     help="report update_fingerprint: fixed projections of the fp32 master weights' change over the run")
     ap.add_argument("--grad-reduce", default="bf16", choices=["bf16", "fp32"],
                     help="DP gradient reduction dtype: bf16 in place, or fp32 (a widened copy reduced and applied in fp32)")
-    ap.add_argument("--comm-ctas", type=int, default=DEFAULT_COMM_CTAS,
-                    help="cap RCCL's CTAs per collective (ncclConfig_t maxCTAs; 0 = RCCL's choice); the default is "
-                         "the knee of the one-GPU comm-shadow sweep (profiles/r04_comm_shadow)")
+    ap.add_argument("--comm-ctas", default="auto", type=lambda v: v if v == "auto" else int(v),
+                    help="cap RCCL's CTAs per collective (ncclConfig_t maxCTAs; 0 = RCCL's choice; N = that cap); "
+                         f"auto (world > 1): time {'/'.join(map(str, AUTO_CTAS))} after the warmup and keep the fastest "
+                         f"(reported as comm_ctas_tuning); at world 1 nothing to cap.  {DEFAULT_COMM_CTAS} is the knee of "
+                         "the one-GPU comm-shadow sweep (profiles/r04_comm_shadow)")
     ap.add_argument("--comm-shadow", type=int, default=0,
                     help="one GPU: play each bucket's k-GPU ring all-reduce as this many CU-holding workgroups (0 = off)")
     ap.add_argument("--comm-shadow-k", type=int, default=8, help="--comm-shadow: ranks of the emulated ring")

@@ -91,10 +91,16 @@ class CommShadow:
         self.steps: List[Tuple[object, List[Tuple[object, object]]]] = []
         self._cur: List[Tuple[object, object]] = []
 
-    def launch(self, bucket_bytes: int) -> None:
+    def launch(self, bucket_bytes: int, part: str = "ar"):
+        """Play one bucket's collective: ``ar`` the all-reduce (2 (k-1)/k of the bucket through each
+        rank); under ZeRO-1 ``rs`` the reduce-scatter at the bucket hook and ``ag`` the weight
+        all-gather after the optimizer, (k-1)/k each.  Returns the collective's end event."""
         from ..ops import fused
 
-        nb = min(ring_bytes(bucket_bytes, self.k), self.src.numel())
+        nb = ring_bytes(bucket_bytes, self.k)
+        if part in ("rs", "ag"):
+            nb //= 2
+        nb = min(nb, self.src.numel())
         us = nb / (self.busbw * 1e9) * 1e6
         cur = torch.cuda.current_stream(self.src.device)
         self.stream.wait_stream(cur)  # the bucket's gradients are complete
@@ -107,6 +113,7 @@ class CommShadow:
         self.launched += 1
         self.bytes += nb
         self.micros += us
+        return ev1
 
     def wait(self) -> None:
         cur = torch.cuda.current_stream(self.src.device)
@@ -147,6 +154,7 @@ class Bucket:
     pending: int = 0
     work: Optional[object] = None
     gather_work: Optional[object] = None
+    gather_event: Optional[object] = None  # one-GPU comm shadow of the ZeRO-1 all-gather
     launched_at: float = 0.0
 
     @property
@@ -254,7 +262,7 @@ class BucketedAllReduce:
         self._launched[b.index] = True
         if self.world == 1:  # nothing to reduce: only the k-GPU shadow
             if self.shadow is not None:
-                self.shadow.launch(b.numel * self.flat.grad.element_size())
+                self.shadow.launch(b.numel * self.flat.grad.element_size(), "rs" if self.zero1 else "ar")
             return
         view = self.flat.grad[b.start:b.end]
         b.launched_at = time.perf_counter()
@@ -360,6 +368,10 @@ class BucketedAllReduce:
     def gather_params(self) -> None:
         """zero1, after the optimizer step: all-gather every bucket's updated weights, asynchronously,
         first-used bucket (highest index: the embedding end of the buffer) first."""
+        if self.zero1 and self.world == 1 and self.shadow is not None:
+            for b in reversed(self.buckets):  # the k-GPU job's all-gathers, played on the shadow stream
+                b.gather_event = self.shadow.launch(b.numel * self.flat.data.element_size(), "ag")
+            return
         if not self.zero1 or self.world == 1:
             return
         for b in reversed(self.buckets):
@@ -373,12 +385,18 @@ class BucketedAllReduce:
         if b.gather_work is not None:
             b.gather_work.wait()
             b.gather_work = None
+        if b.gather_event is not None:
+            torch.cuda.current_stream(self.flat.data.device).wait_event(b.gather_event)
+            b.gather_event = None
 
     def wait_all_params(self) -> None:
         for b in self.buckets:
             if b.gather_work is not None:
                 b.gather_work.wait()
                 b.gather_work = None
+            if b.gather_event is not None:
+                torch.cuda.current_stream(self.flat.data.device).wait_event(b.gather_event)
+                b.gather_event = None
 
     @property
     def grad_scale(self) -> float:

@@ -168,3 +168,28 @@ def test_a_missing_wait_fails_the_reduction_check():
     for r in (0, 1):
         c = res[r]["check"]
         assert not c["ok"] and c["reduce_max_rel"] > 0.1, c
+
+
+def test_comm_ctas_auto_times_each_cap_and_keeps_the_fastest():
+    """--comm-ctas auto (the default) at world > 1: after the warmup one
+    communicator per candidate cap, two timed steps each, the fastest kept and the table reported; the
+    reduction check still holds across the switch of communicators (ZeRO-1 included)."""
+    import json
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "-m", "gpu_topology_on_k8s_amd.models.train",
+                        "--model", "tiny", "--batch", "2", "--seq", "64", "--steps", "2", "--warmup", "1", "--device", "cpu",
+                        "--attn", "sdpa", "--gemm-tuning", "off", "--bucket-mb", "0.05", "--zero1", "--check-reduction"],
+                       capture_output=True, text=True, timeout=600, cwd=repo, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    table = out["comm_ctas_tuning"]
+    from gpu_topology_on_k8s_amd.models.train import AUTO_CTAS
+
+    assert [r["ctas"] for r in table] == list(AUTO_CTAS) and all(r["ms_per_step"] > 0 for r in table)
+    assert out["comm_ctas"] == min(table, key=lambda r: r["ms_per_step"])["ctas"]
+    assert out["check_reduction"]["ok"]

@@ -104,7 +104,7 @@ print(json.dumps({"tflops": round(float(w["tflops"]), 1), "hbm_copy_gbps": round
     ;;
   shadow)
     # what 8-GPU DP communication costs the Llama-3-8B step: comm-shadow CTA sweep
-    step shadow_sweep 1100 python -u bench/comm_shadow_sweep.py --ctas ${SHADOW_CTAS:-0,8,16,32,64} --busbw ${SHADOW_BUSBW:-350} --out "$out/shadow.jsonl"
+    step shadow_sweep 1100 python -u bench/comm_shadow_sweep.py --ctas ${SHADOW_CTAS:-0,8,16,32,64} --busbw ${SHADOW_BUSBW:-350} --out "$out/shadow.jsonl" ${SHADOW_ZERO1:+--zero1}
     ;;
   *) echo "unknown mode $mode"; exit 2 ;;
 esac
