@@ -399,34 +399,51 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
     cta_table = None
     if comm_ctas == "auto" and env["world"] > 1 and not use_graph:
         # the first k >= 2 run confirms the CTA cap the one-GPU comm shadow chose:
-        # one communicator per candidate cap, a settling step and two timed steps on each (max over
-        # ranks), then the rest of the run on the fastest.  These steps train like warmup steps.
+        # one communicator per candidate cap; on each a settling pass and two timed passes (max over
+        # ranks) of forward + backward with the bucketed reductions overlapped (+ ZeRO-1's all-gather
+        # of the unchanged weights) -- no optimizer update, one fixed batch, the data generators and
+        # dropout state restored after -- so training is exactly the run without the tuning.
         cta_table, groups = [], {}
+        gstates = [g.get_state() for g in gens]
+        rng0 = _rng()
+        first0 = dict(first)
+        xy = batch_tokens()
+
+        def tune_pass():
+            model.flat.zero_grad()
+            model(*xy).backward()
+            ar.finish()
+            ar.gather_params()
+            ar.wait_all_params()
+
         for c in AUTO_CTAS:
             groups[c] = _comm_group(c)
             ar.remove()
             ar = make_ar(groups[c])
             if zero1:
                 model.param_ready = ar.wait_param
-            step()
-            ar.wait_all_params()
+            tune_pass()
             sync()
             dist.barrier()
             ta = time.perf_counter()
             for _ in range(2):
-                step()
-            ar.wait_all_params()
+                tune_pass()
             sync()
             tt = torch.tensor([time.perf_counter() - ta], dtype=torch.float64,
                               device=device if device.type == "cuda" else "cpu")
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            cta_table.append({"ctas": c, "ms_per_step": float(tt.item()) / 2 * 1e3})
-        best = min(cta_table, key=lambda r: r["ms_per_step"])["ctas"]
+            cta_table.append({"ctas": c, "ms_per_pass": float(tt.item()) / 2 * 1e3})
+        best = min(cta_table, key=lambda r: r["ms_per_pass"])["ctas"]
         ar.remove()
         ar = make_ar(groups[best])
         if zero1:
             model.param_ready = ar.wait_param
         comm_ctas = best
+        for g, st_ in zip(gens, gstates):
+            g.set_state(st_)
+        _set_rng(rng0)
+        first.clear()
+        first.update(first0)
     if use_graph:
         if check["pending"]:
             ar.capture_local(True)  # the captured finish() copies every bucket's input before its collective
