@@ -63,8 +63,8 @@ def main():
         if hasattr(hip, "attn_bwd_v5"):
             variants["v5"] = lambda: hip.attn_bwd_v5(do, q, k, v, o, lse, Dh ** -0.5)
         if hasattr(hip, "attn_bwd_v7"):
-            variants["v7_asm"] = lambda: hip.attn_bwd_v7(do, q, k, v, o, lse, Dh ** -0.5, True)
-            variants["v7_cc"] = lambda: hip.attn_bwd_v7(do, q, k, v, o, lse, Dh ** -0.5, False)
+            for vi, vn in enumerate(("v7", "v7_early", "v7_stream", "v7_early_stream")):
+                variants[vn] = (lambda vi_: lambda: hip.attn_bwd_v7(do, q, k, v, o, lse, Dh ** -0.5, vi_))(vi)
         times = {n: [] for n in variants}
         for fn in variants.values():
             fn()

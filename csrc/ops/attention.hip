@@ -649,7 +649,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv5_kernel(const u16* __res
 //   * the long-lived dV^T / dK^T accumulators (128 registers) are pinned in AGPRs by their MFMAs' asm
 //     constraints (kAsmAcc), so everything else -- K / V rows, the slice's operands, S / dP, the packs
 //     -- fits the 256 VGPRs and the S / dP MFMAs stay in VGPR form: no accumulator moves.
-template <bool kAsmAcc>
+template <bool kEarlyDma, bool kStreamT>
 __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv7_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
                                                                 const u16* __restrict__ v, const u16* __restrict__ dout,
                                                                 const float* __restrict__ nls, const float* __restrict__ ndl,
@@ -671,8 +671,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv7_kernel(const u16* __res
   f32x16 dvt[4], dkt[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dvt[dt] = dkt[dt] = f32x16{};
-  if (kAsmAcc)  // the zeroing writes settle before the first asm MFMA reads them as its accumulator
-    asm volatile("s_nop 1" : "+a"(dvt[0]), "+a"(dvt[1]), "+a"(dvt[2]), "+a"(dvt[3]), "+a"(dkt[0]), "+a"(dkt[1]), "+a"(dkt[2]),
+  // the zeroing writes settle before the first asm MFMA reads them as its accumulator
+  asm volatile("s_nop 1" : "+a"(dvt[0]), "+a"(dvt[1]), "+a"(dvt[2]), "+a"(dvt[3]), "+a"(dkt[0]), "+a"(dkt[1]), "+a"(dkt[2]),
                  "+a"(dkt[3]));
   const int qt0 = (kb * KB) / QT, nqt = S / QT - qt0, nslice = G * nqt;
 
@@ -703,12 +703,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv7_kernel(const u16* __res
                                                (uint32_t)(((size_t)hq * S + qbase) * 4), 0, 0);
   };
   int cur_h = 0, cur_j = 0;  // this step's slice
-  // dV^T / dK^T += A . B: in AGPRs through the asm constraint (kAsmAcc), else the builtin
+  // dV^T / dK^T += A . B, the accumulator pinned to AGPRs by the asm constraint
   auto acc_mfma = [&](f32x16& acc, bf16x8 a, bf16x8 bb) {
-    if (kAsmAcc)
-      asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(bb));
-    else
-      acc = mfma(a, bb, acc);
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(bb));
   };
   struct Packs {
     bf16x8 p0, p1, d0, d1;
@@ -722,16 +719,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv7_kernel(const u16* __res
   __syncthreads();
   sload(0, 0, smem);
   dma_sync();
-  auto step = [&](int idx, const int rb) {
-    const char* buf = smem + rb * SL_BYTES;
-    const char* pbuf = smem + ((rb + 2) % 3) * SL_BYTES;  // slice idx-1 (its deferred dV/dK products)
-    // (1) this slice's rows and its -lse/c, -delta (the S / dP chains' initial accumulators)
-    bf16x8 qa[8], da[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      qa[s] = lds_b128(buf + SL_Q, swz(r, 2 * s + hh));
-      da[s] = lds_b128(buf + SL_DO, swz(r, 2 * s + hh));
-    }
+  // buf: this slice; pbuf: the previous one (its deferred dV/dK products); nbuf: the slot the next
+  // slice's DMA fills.  As __restrict__ parameters the three are provably disjoint, so no read of buf /
+  // pbuf waits for the DMA into nbuf (kEarlyDma issues it before them: a whole step to land)
+  auto step = [&](int idx, const char* __restrict__ buf, const char* __restrict__ pbuf, char* __restrict__ nbuf) {
+    const int nj = cur_j + 1 == nqt ? 0 : cur_j + 1, nh = cur_j + 1 == nqt ? cur_h + 1 : cur_h;
+    if (kEarlyDma && idx + 1 < nslice) sload(nh, nj, nbuf);
+    // (1) this slice's -lse/c, -delta (the S / dP chains' initial accumulators) and its rows
     f32x16 sacc, dpacc;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -743,29 +737,56 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv7_kernel(const u16* __res
         dpacc[4 * g + e] = d4[e];
       }
     }
-    // (2) S' = S - lse/c and dP' = dP - delta, the previous slice's transposed reads between their MFMAs
+    bf16x8 qa[8], da[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      qa[s] = lds_b128(buf + SL_Q, swz(r, 2 * s + hh));
+      da[s] = lds_b128(buf + SL_DO, swz(r, 2 * s + hh));
+    }
+    // the previous slice's transposed dO^T / Q^T fragment ti (A operand of dV^T / dK^T product ti)
+    auto tfrag = [&](int ti) {
+      const int dt = ti >> 2, part = ti & 3;
+      return tr_frag(pbuf + (part < 2 ? SL_DO : SL_Q), lane, (part & 1) * 16 + 4 * hh, (part & 1) * 16 + 8 + 4 * hh, 32 * dt);
+    };
+    // dV/dK product i in issue order: accumulators round-robin, so an accumulator's two products are
+    // 4 MFMAs apart
+    auto tix = [](int i) { return 4 * (i & 3) + (i >> 2); };
+    // (2) S' = S - lse/c and dP' = dP - delta.  kStreamT: the transposed fragments are read in phase
+    // (4), two products ahead of their use (12 registers instead of 64 -- what lets this slice's rows
+    // all be read ahead of the S / dP chains); else all 16 read here, between those MFMAs
+    bf16x8 ta[16];
+    if (kStreamT) {
+      ta[tix(0)] = tfrag(tix(0));
+      ta[tix(1)] = tfrag(tix(1));
+    }
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       sacc = mfma(qa[s], kf[s], sacc);
       dpacc = mfma(da[s], vf[s], dpacc);
     }
-    bf16x8 ta[16];
+    if (kStreamT) {
+      // the init quads and the first two rows of Q and dO, then one more row per MFMA: the chains start
+      // as soon as their first operands land and every later row is in flight under an MFMA
+      // (the first two transposed fragments of phase (4) with the first reads)
+      __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      ta[4 * dt + 0] = tr_frag(pbuf + SL_DO, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt);
-      ta[4 * dt + 1] = tr_frag(pbuf + SL_DO, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt);
-      ta[4 * dt + 2] = tr_frag(pbuf + SL_Q, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt);
-      ta[4 * dt + 3] = tr_frag(pbuf + SL_Q, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt);
-    }
+      for (int g = 0; g < 12; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    } else {
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      for (int ti = 0; ti < 16; ++ti) ta[ti] = tfrag(ti);
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
-    // (3) the next slice's DMA: every LDS read of this step precedes it
-    const int nj = cur_j + 1 == nqt ? 0 : cur_j + 1, nh = cur_j + 1 == nqt ? cur_h + 1 : cur_h;
-    if (idx + 1 < nslice) sload(nh, nj, smem + ((rb + 1) % 3) * SL_BYTES);
+    // (3) the next slice's DMA (late variant): every LDS read of this step precedes it
+    if (!kEarlyDma && idx + 1 < nslice) sload(nh, nj, nbuf);
     __builtin_amdgcn_sched_barrier(0);
     // (4) softmax / dS of this slice under the deferred dV/dK MFMAs of the previous one
     // diagonal slices (the block's first KB/QT query tiles) mask from qbase; slices wholly above this
@@ -774,93 +795,73 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv7_kernel(const u16* __res
     const bool dead = cur_j < KB / QT && qbase + QT - 1 < kmin;
     const int kill_from = dead ? -(1 << 30) : (cur_j < KB / QT ? qbase : 1 << 30);
     Packs cur;
-    if (kAsmAcc) {
-      // The dV/dK MFMAs are asm statements, which the scheduling-group barriers do not see; each gap's
-      // VALU is pinned between its two MFMAs instead: an empty asm right after MFMA i "writes" the
-      // gap's inputs and another right before MFMA i+1 "reads" its outputs (no instructions emitted).
-      float sp[16], dp[16];
+    // The dV/dK MFMAs are asm statements, which the scheduling-group barriers do not see; each gap's
+    // VALU is pinned between its two MFMAs instead: an empty asm right after MFMA i "writes" the gap's
+    // inputs and another right before MFMA i+1 "reads" its outputs (no instructions emitted).  LDS reads
+    // keep their source position relative to the (side-effecting) asm statements.
+    float sp[16], dp[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) sp[i] = sacc[i], dp[i] = dpacc[i];
-      auto M = [&](int i) {  // accumulators round-robin: an accumulator's two products are 4 MFMAs apart
-        const int dt = i & 3, part = i >> 2;
-        const int ti = 4 * dt + part;
-        f32x16& acc = part < 2 ? dvt[dt] : dkt[dt];
-        const bf16x8 bb = part == 0 ? prev.p0 : part == 1 ? prev.p1 : part == 2 ? prev.d0 : prev.d1;
-        acc_mfma(acc, ta[ti], bb);
-      };
+    for (int i = 0; i < 16; ++i) sp[i] = sacc[i], dp[i] = dpacc[i];
+    auto M = [&](int i) {
+      const int ti = tix(i), dt = ti >> 2, part = ti & 3;
+      f32x16& acc = part < 2 ? dvt[dt] : dkt[dt];
+      const bf16x8 bb = part == 0 ? prev.p0 : part == 1 ? prev.p1 : part == 2 ? prev.d0 : prev.d1;
+      acc_mfma(acc, ta[ti], bb);
+      if (kStreamT && i + 2 < 16) ta[tix(i + 2)] = tfrag(tix(i + 2));
+    };
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {  // gaps 0-7: p = 2^(c S') for two scores each (mul + exp: 24 cycles)
-        M(i);
-        pin2(sp[2 * i], sp[2 * i + 1]);
-        sp[2 * i] = fexp2(sp[2 * i] * c);
-        sp[2 * i + 1] = fexp2(sp[2 * i + 1] * c);
-        pin2(sp[2 * i], sp[2 * i + 1]);
-      }
-      M(8);  // gap 8: the causal mask (diagonal / dead slices only), P's two packs
-      pin16(sp);
-      if (kill_from != (1 << 30)) {  // wave-uniform
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sp[i] = (mykey - crow(i, hh) > kill_from) ? 0.f : sp[i];
-      }
-      cur.p0 = pack8a(sp, 0);
-      cur.p1 = pack8a(sp, 8);
-      pin_b(cur.p0, cur.p1);
-#pragma unroll
-      for (int i = 9; i < 13; ++i) {  // gaps 9-12: dS = p dP' for four scores each
-        M(i);
-        const int o = 4 * (i - 9);
-        pin4(dp[o], dp[o + 1], dp[o + 2], dp[o + 3]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dp[o + e] *= sp[o + e];
-        pin4(dp[o], dp[o + 1], dp[o + 2], dp[o + 3]);
-      }
-      M(13);  // gaps 13-14: dS's packs
-      pin4(dp[0], dp[1], dp[2], dp[3]);
-      pin4(dp[4], dp[5], dp[6], dp[7]);
-      cur.d0 = pack8a(dp, 0);
-      pin_b1(cur.d0);
-      M(14);
-      pin4(dp[8], dp[9], dp[10], dp[11]);
-      pin4(dp[12], dp[13], dp[14], dp[15]);
-      cur.d1 = pack8a(dp, 8);
-      pin_b1(cur.d1);
-      M(15);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sacc[i] = fexp2(sacc[i] * c);
-      if (kill_from != (1 << 30)) {  // wave-uniform: a diagonal or dead slice
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sacc[i] = (mykey - crow(i, hh) > kill_from) ? 0.f : sacc[i];
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) dpacc[i] = sacc[i] * dpacc[i];
-      cur = Packs{pack8(sacc, 0), pack8(sacc, 8), pack8(dpacc, 0), pack8(dpacc, 8)};
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        acc_mfma(dvt[dt], ta[4 * dt + 0], prev.p0);
-        acc_mfma(dvt[dt], ta[4 * dt + 1], prev.p1);
-        acc_mfma(dkt[dt], ta[4 * dt + 2], prev.d0);
-        acc_mfma(dkt[dt], ta[4 * dt + 3], prev.d1);
-      }
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {  // {1 dV/dK MFMA, 5 softmax VALU} x 16
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
-      }
+    for (int i = 0; i < 8; ++i) {  // gaps 0-7: p = 2^(c S') for two scores each (mul + exp: 24 cycles)
+      M(i);
+      pin2(sp[2 * i], sp[2 * i + 1]);
+      sp[2 * i] = fexp2(sp[2 * i] * c);
+      sp[2 * i + 1] = fexp2(sp[2 * i + 1] * c);
+      pin2(sp[2 * i], sp[2 * i + 1]);
     }
+    M(8);  // gap 8: the causal mask (diagonal / dead slices only), P's two packs
+    pin16(sp);
+    if (kill_from != (1 << 30)) {  // wave-uniform
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sp[i] = (mykey - crow(i, hh) > kill_from) ? 0.f : sp[i];
+    }
+    cur.p0 = pack8a(sp, 0);
+    cur.p1 = pack8a(sp, 8);
+    pin_b(cur.p0, cur.p1);
+#pragma unroll
+    for (int i = 9; i < 13; ++i) {  // gaps 9-12: dS = p dP' for four scores each
+      M(i);
+      const int o = 4 * (i - 9);
+      pin4(dp[o], dp[o + 1], dp[o + 2], dp[o + 3]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dp[o + e] *= sp[o + e];
+      pin4(dp[o], dp[o + 1], dp[o + 2], dp[o + 3]);
+    }
+    M(13);  // gaps 13-14: dS's packs
+    pin4(dp[0], dp[1], dp[2], dp[3]);
+    pin4(dp[4], dp[5], dp[6], dp[7]);
+    cur.d0 = pack8a(dp, 0);
+    pin_b1(cur.d0);
+    M(14);
+    pin4(dp[8], dp[9], dp[10], dp[11]);
+    pin4(dp[12], dp[13], dp[14], dp[15]);
+    cur.d1 = pack8a(dp, 8);
+    pin_b1(cur.d1);
+    M(15);
     __builtin_amdgcn_sched_barrier(0);
     prev = cur;
     cur_h = nh, cur_j = nj;
     dma_sync();
   };
   int idx = 0;
+  char* const s0 = smem;
+  char* const s1 = smem + SL_BYTES;
+  char* const s2 = smem + 2 * SL_BYTES;
   for (; idx + 3 <= nslice; idx += 3) {
-    step(idx, 0);
-    step(idx + 1, 1);
-    step(idx + 2, 2);
+    step(idx, s0, s2, s1);
+    step(idx + 1, s1, s0, s2);
+    step(idx + 2, s2, s1, s0);
   }
-  if (idx < nslice) step(idx, 0);
-  if (idx + 1 < nslice) step(idx + 1, 1);
+  if (idx < nslice) step(idx, s0, s2, s1);
+  if (idx + 1 < nslice) step(idx + 1, s1, s0, s2);
   {  // the last slice's deferred dV/dK products
     const char* pbuf = smem + ((nslice - 1) % 3) * SL_BYTES;
 #pragma unroll
@@ -871,8 +872,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv7_kernel(const u16* __res
       acc_mfma(dkt[dt], tr_frag(pbuf + SL_Q, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), prev.d1);
     }
   }
-  if (kAsmAcc)  // asm MFMAs are invisible to the hazard recognizer: their results settle before the reads
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(dvt[0]), "+a"(dvt[1]), "+a"(dvt[2]), "+a"(dvt[3]), "+a"(dkt[0]),
+  // asm MFMAs are invisible to the hazard recognizer: their results settle before the reads
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(dvt[0]), "+a"(dvt[1]), "+a"(dvt[2]), "+a"(dvt[3]), "+a"(dkt[0]),
                  "+a"(dkt[1]), "+a"(dkt[2]), "+a"(dkt[3]));
   u16* dkrow = dk + ((size_t)(b * Hkv + hk) * S + mykey) * D;
   u16* dvrow = dv + ((size_t)(b * Hkv + hk) * S + mykey) * D;
@@ -1070,7 +1071,7 @@ std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, co
 
 // dK/dV v7 (S / dP in VGPRs, -lse/c and -delta as their chains' initial accumulators) + dQ
 std::vector<at::Tensor> attn_bwd_v7(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                    const at::Tensor& out, const at::Tensor& lse, double scale, bool asm_acc) {
+                                    const at::Tensor& out, const at::Tensor& lse, double scale, int64_t variant) {
   check_qkv(q, k, v);
   const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
   TORCH_CHECK(dout.is_contiguous() && out.is_contiguous() && dout.numel() == q.numel() && out.numel() == q.numel(),
@@ -1084,12 +1085,17 @@ std::vector<at::Tensor> attn_bwd_v7(const at::Tensor& dout, const at::Tensor& q,
   hipLaunchKernelGGL(attn_bwd_pre7_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
                      lse.data_ptr<float>(), delta.data_ptr<float>(), nls.data_ptr<float>(), ndl.data_ptr<float>(), B, H, S,
                      1.f / c);
-  if (asm_acc)
-    hipLaunchKernelGGL(attn_bwd_dkdv7_kernel<true>, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v),
-                       bp(dout), nls.data_ptr<float>(), ndl.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
-  else
-    hipLaunchKernelGGL(attn_bwd_dkdv7_kernel<false>, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v),
-                       bp(dout), nls.data_ptr<float>(), ndl.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
+  // variant bit 0: the next slice's DMA at the step start; bit 1: transposed fragments streamed in phase (4)
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
+                       nls.data_ptr<float>(), ndl.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
+  };
+  switch (variant & 3) {
+    case 0: launch(attn_bwd_dkdv7_kernel<false, false>); break;
+    case 1: launch(attn_bwd_dkdv7_kernel<true, false>); break;
+    case 2: launch(attn_bwd_dkdv7_kernel<false, true>); break;
+    default: launch(attn_bwd_dkdv7_kernel<true, true>); break;
+  }
   hipLaunchKernelGGL(attn_bwd_dq2n_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
                      lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
   return {dq, dk, dv};

@@ -61,7 +61,7 @@ def test_attention_backward(fused, B, H, Hkv, S):
 
 
 @pytest.mark.parametrize("B,H,Hkv,S", [(2, 8, 2, 768), (1, 4, 4, 128), (1, 32, 8, 1024), (2, 4, 1, 384), (1, 8, 2, 640)])
-@pytest.mark.parametrize("variant", ["v5", "v7_asm", "v7_cc"])
+@pytest.mark.parametrize("variant", ["v5", "v7", "v7_early", "v7_stream", "v7_early_stream"])
 def test_attention_bwd_variants_match_fp32_reference(fused, B, H, Hkv, S, variant):
     """Every dK/dV generation the extension exports (v5: the round-4 kernel; v7: S / dP accumulated in
     VGPRs from -lse/c and -delta, its dV/dK accumulators pinned to AGPRs by asm or left to the compiler)
@@ -75,8 +75,10 @@ def test_attention_bwd_variants_match_fp32_reference(fused, B, H, Hkv, S, varian
     hip = fused.hip()
     o, lse = hip.attn_fwd(q, k, v, 128 ** -0.5)
     fn = {"v5": lambda: hip.attn_bwd_v5(do, q, k, v, o, lse, 128 ** -0.5),
-          "v7_asm": lambda: hip.attn_bwd_v7(do, q, k, v, o, lse, 128 ** -0.5, True),
-          "v7_cc": lambda: hip.attn_bwd_v7(do, q, k, v, o, lse, 128 ** -0.5, False)}[variant]
+          "v7": lambda: hip.attn_bwd_v7(do, q, k, v, o, lse, 128 ** -0.5, 0),
+          "v7_early": lambda: hip.attn_bwd_v7(do, q, k, v, o, lse, 128 ** -0.5, 1),
+          "v7_stream": lambda: hip.attn_bwd_v7(do, q, k, v, o, lse, 128 ** -0.5, 2),
+          "v7_early_stream": lambda: hip.attn_bwd_v7(do, q, k, v, o, lse, 128 ** -0.5, 3)}[variant]
     got = fn()
     qf, kf, vf = (x.float().requires_grad_(True) for x in (q, k, v))
     ref = fused.attention_ref(qf, kf, vf)
