@@ -57,14 +57,12 @@ def main():
     res["hip_bwd_ms"] = t * 1e3
     res["hip_bwd_tflops"] = 2.5 * fwd_flops / t / 1e12
     if a.ab:
-        # interleaved A/B of the backward variants the extension exports (dK/dV v5 = the round-4 default,
-        # v7 = S / dP in VGPRs, with the dV/dK accumulators pinned to AGPRs or left to the compiler)
+        # interleaved A/B of the backward variants the extension exports (one since round 5: the A/B
+        # records of the retired ones are profiles/r05_attn7)
         variants = {"default": lambda: hip.attn_bwd(do, q, k, v, o, lse, Dh ** -0.5)}
-        if hasattr(hip, "attn_bwd_v5"):
-            variants["v5"] = lambda: hip.attn_bwd_v5(do, q, k, v, o, lse, Dh ** -0.5)
-        if hasattr(hip, "attn_bwd_v7"):
-            for vi, vn in enumerate(("v7", "v7_early", "v7_stream", "v7_early_stream")):
-                variants[vn] = (lambda vi_: lambda: hip.attn_bwd_v7(do, q, k, v, o, lse, Dh ** -0.5, vi_))(vi)
+        for n in sorted(dir(hip)):
+            if n.startswith("attn_bwd_"):
+                variants[n] = (lambda fn: lambda: fn(do, q, k, v, o, lse, Dh ** -0.5))(getattr(hip, n))
         times = {n: [] for n in variants}
         for fn in variants.values():
             fn()

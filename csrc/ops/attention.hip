@@ -355,27 +355,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict
 }
 
 // ==================================================================================== backward
-// delta[b, h, q] = sum_d dO[b, q, h, d] * O[b, q, h, d]   (one 16-lane group per row)
+// delta[b, h, q] = sum_d dO[b, q, h, d] * O[b, q, h, d] (one 16-lane group per row; dQ reads it), plus
+// what dK/dV starts its S / dP chains from: nls = -lse2 / c, ndl = -delta
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
-                                                           float* __restrict__ delta, int B, int H, int S) {
-  const int row = blockIdx.x * 16 + (threadIdx.x >> 4);  // row = (b*S + s)*H + h
-  const int i = threadIdx.x & 15;
-  if (row >= B * S * H) return;
-  const u16x8 a = reinterpret_cast<const u16x8*>(dout + (size_t)row * D)[i];
-  const u16x8 bb = reinterpret_cast<const u16x8*>(out + (size_t)row * D)[i];
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s += bf2f(a[j]) * bf2f(bb[j]);
-#pragma unroll
-  for (int off = 8; off > 0; off >>= 1) s += __shfl_xor(s, off, 16);
-  if (i == 0) {
-    const int h = row % H, bs = row / H, sidx = bs % S, bidx = bs / S;
-    delta[((size_t)bidx * H + h) * S + sidx] = s;
-  }
-}
-
-// delta as above, plus what dK/dV v7 starts its S / dP chains from: nls = -lse2 / c, ndl = -delta
-__global__ __launch_bounds__(256) void attn_bwd_pre7_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
                                                             const float* __restrict__ lse2, float* __restrict__ delta,
                                                             float* __restrict__ nls, float* __restrict__ ndl, int B, int H,
                                                             int S, float inv_c) {
@@ -401,256 +383,32 @@ __global__ __launch_bounds__(256) void attn_bwd_pre7_kernel(const u16* __restric
 // ============================================================================ backward dK/dV
 // The split dK/dV decomposition: one workgroup = 128 keys of one (batch, kv-head), sweeping every q-head
 // of the GQA group x 32-query slices, key on the lane; each lane's K and V rows live in registers for
-// the whole kernel.  Q, dO, lse and delta of a slice arrive by LDS-DMA into a 3-slot ring, one slice
-// ahead, with one barrier per slice; lse / delta are read per accumulator quad with ds_read_b128
-// (crow(4g..4g+3) are 4 consecutive queries).  Only the first KB/QT slices of each q-head touch the
-// block's diagonal: mask code runs there only.  Earlier generations (v3: not pipelined, v4: operands
-// read at their use) and the A/B variants of v5 were retired in round 5; their bit-identity and
-// timing records are profiles/r04_attn, r04_maskbr, r04_split, r04_vpg.
+// the whole kernel.  Q, dO, -lse/c and -delta of a slice arrive by LDS-DMA into a 3-slot ring, one slice
+// ahead, with one barrier per slice.  Each slice's dV^T += dO^T.P and dK^T += Q^T.dS products are
+// deferred by one slice, so its softmax / dS VALU runs under the previous slice's products.  Only the
+// first KB/QT slices of each q-head touch the block's diagonal: mask code runs there only.
+//
+// Round 5 (v7) re-budgeted the registers of the round-4 kernel (v5).  v5 held ~460 registers at one
+// wave per SIMD; past 256 the compiler selects the AGPR form for EVERY MFMA, so S / dP landed in AGPRs
+// and each slice paid ~100 v_accvgpr_read / write / mov to bring them to the softmax VALU and back.
+// Now (hipcc -S: 252 VGPRs + 128 AGPRs, no accumulator moves in the loop):
+//   * -lse/c and -delta enter as the S and dP chains' initial accumulators (the pre-kernel writes them
+//     negated and pre-divided): p = 2^(c S') and dS = p dP' need no lse / delta registers, no subtract;
+//   * the long-lived dV^T / dK^T accumulators (128 registers) are pinned in AGPRs by their MFMAs' asm
+//     constraints, and the S / dP MFMAs take the VGPR form (attention.hip is built with
+//     -amdgpu-mfma-vgpr-form); each gap's softmax VALU is pinned between two of those asm MFMAs by
+//     empty asm statements on its operands;
+//   * the transposed dO^T / Q^T fragments are read two products ahead of their use (12 registers
+//     instead of 64), which leaves room to read this slice's rows and init quads ahead of the S / dP
+//     chains;
+//   * the next slice's DMA is issued at the step start, into a slot passed as a __restrict__ pointer
+//     (so no read of this step waits for it): a whole step to land.
+// Measured at B 4 x 4096 (profiles/r05_attn7): 1434 -> 1009 us per dK/dV launch, MFMA busy 39 -> 52 %,
+// whole backward -14.6 %.  v3 / v4 / v5 and the v7 A/B variants are retired; their records are
+// profiles/r04_attn, r04_maskbr, r04_split, r04_vpg, r05_attn7.
 constexpr int SL_Q = 0, SL_DO = QT * D * 2, SL_LSE = 2 * QT * D * 2, SL_DEL = SL_LSE + 256, SL_BYTES = SL_DEL + 256;
 
-// dK/dV v5: v4 with its LDS operands read AHEAD, into registers, before the next slice's LDS-DMA
-// is issued.  The v4 ISA (hipcc -S, ROCm 7.2) showed one wave per SIMD (460 VGPR+AGPR) waiting on
-// every fragment: each MFMA sat behind its own `ds_read; s_waitcnt lgkmcnt(0)`, and the compiler put
-// an `s_waitcnt vmcnt(0)` (the next slice's DMA) in front of the first transposed read of the
-// previous slot, since it cannot prove that read disjoint from the DMA target.  Here a step
-//   1. reads everything it will consume from LDS: the previous slice's dO^T / Q^T fragments (the
-//      deferred dV/dK products), this slice's lse / delta and its Q / dO fragments;
-//   2. only then issues the next slice's LDS-DMA (nothing after it reads LDS until the barrier);
-//   3. runs S and dP, then the softmax / dS VALU interleaved with the deferred dV/dK MFMAs, whose
-//      operands are all in registers already.
-// Same MFMAs in the same order per accumulator as v4, so the results are bit-identical.
-// kSFirst: read this slice's Q / dO rows (and lse / delta) first, start S / dP on them, and issue the
-// previous slice's 32 transposed reads BETWEEN those MFMAs.  In the v5 order all 56 reads of a step
-// were issued before its first MFMA; a wave has at most 15 LDS reads in flight (4-bit lgkmcnt), so
-// the MFMA pipe idled while the LDS drained ~40 of them (`s_waitcnt lgkmcnt(14)` after 56 reads in
-// the ISA).  Same MFMAs in the same order: bit-identical.
-// kMaskBranch: the causal mask runs only on the slices that need it (a wave-uniform branch around
-// it), instead of a compare + select per score on every slice.  Only the first KB/QT slices of each
-// q-head touch the block's diagonal (or lie wholly above a wave's keys): ~3 % of the slices at
-// S 4096, while the per-score select cost 16 x (v_cmp + v_cndmask) per slice on every slice of a
-// kernel whose single wave per SIMD is issue-bound (profiles/r04_dkdv6).  Masked scores still become
-// exactly 0 before dS, so the products are unchanged: bit-identical.
-template <bool kSFirst, bool kMaskBranch = true>
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv5_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
-                                                                const u16* __restrict__ v, const u16* __restrict__ dout,
-                                                                const float* __restrict__ lse2, const float* __restrict__ delta,
-                                                                u16* __restrict__ dk, u16* __restrict__ dv, int H, int Hkv,
-                                                                int S, float c, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[3 * SL_BYTES];  // slice ring
-  const int t = threadIdx.x, lane = t & 63, r = lane & 31, hh = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int kb = blockIdx.y;
-  const int bk = xcd_head(blockIdx.x, gridDim.x), b = bk / Hkv, hk = bk % Hkv, G = H / Hkv;
-  const size_t kvoff = ((size_t)(b * Hkv + hk) * S + (size_t)kb * KB) * D;
-  const int krow = w * 32 + r, mykey = kb * KB + krow, kmin = kb * KB + w * 32;
-  bf16x8 kf[8], vf[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    kf[s] = *reinterpret_cast<const bf16x8*>(k + kvoff + (size_t)krow * D + 16 * s + 8 * hh);
-    vf[s] = *reinterpret_cast<const bf16x8*>(v + kvoff + (size_t)krow * D + 16 * s + 8 * hh);
-  }
-  f32x16 dvt[4], dkt[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) dvt[dt] = dkt[dt] = f32x16{};
-  const int qt0 = (kb * KB) / QT, nqt = S / QT - qt0, nslice = G * nqt;
-
-  const uint32_t qbytes = (uint32_t)((size_t)H * S * D * 2), dbytes = (uint32_t)((size_t)S * H * D * 2);
-  const auto qrs = __builtin_amdgcn_make_buffer_rsrc((void*)(q + (size_t)b * H * S * D), 0, qbytes, 0x00020000);
-  const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)(dout + (size_t)b * S * H * D), 0, dbytes, 0x00020000);
-  const auto lrs = __builtin_amdgcn_make_buffer_rsrc((void*)((w == 0 ? lse2 : delta) + (size_t)b * H * S), 0,
-                                                     (uint32_t)((size_t)H * S * 4), 0x00020000);
-  uint32_t qv[2], dvo[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int R = 8 * w + 4 * i + (lane >> 4);
-    const uint32_t ch16 = 16 * ((lane & 15) ^ (((R & 3) << 2) | ((R >> 2) & 3)));
-    qv[i] = (uint32_t)(R * D * 2) + ch16;
-    dvo[i] = (uint32_t)(R * H * D * 2) + ch16;
-  }
-  auto sload = [&](int idx, char* buf) {
-    const int hq = hk * G + idx / nqt, qbase = (qt0 + idx % nqt) * QT;
-    const uint32_t qs = (uint32_t)(((size_t)hq * S + qbase) * D * 2), ds = (uint32_t)(((size_t)qbase * H + hq) * D * 2);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (LDS_AS void*)(buf + SL_Q + (8 * w + 4 * i) * 256), 16, qv[i], qs, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, (LDS_AS void*)(buf + SL_DO + (8 * w + 4 * i) * 256), 16, dvo[i], ds, 0, 0);
-    }
-    if (w < 2)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, (LDS_AS void*)(buf + (w == 0 ? SL_LSE : SL_DEL)), 4, 4 * lane,
-                                               (uint32_t)(((size_t)hq * S + qbase) * 4), 0, 0);
-  };
-  auto active = [&](int idx) {
-    const int j = idx % nqt;
-    return j >= KB / QT || (qt0 + j) * QT + QT - 1 >= kmin;
-  };
-  auto masked = [&](int idx) { return idx % nqt < KB / QT; };
-  struct Packs {
-    bf16x8 p0, p1, d0, d1;
-  };
-
-  Packs prev{};
-  {  // the first step's deferred products read ring(2): zeros, not stale LDS bits
-    u16x8* z = reinterpret_cast<u16x8*>(smem + 2 * SL_BYTES);
-    for (int i = t; i < SL_BYTES / 16; i += 256) z[i] = u16x8{};
-  }
-  __syncthreads();
-  sload(0, smem);
-  dma_sync();
-  auto step = [&](int idx, const int rb) {
-    const char* buf = smem + rb * SL_BYTES;
-    const char* pbuf = smem + ((rb + 2) % 3) * SL_BYTES;  // slice idx-1 (its deferred dV/dK products)
-    // (1) every LDS operand of this step, while no DMA is outstanding
-    bf16x8 ta[16], qa[8], da[8];
-    f32x4 lq[4], dq[4];
-    auto read_t = [&]() {  // the previous slice's dO^T / Q^T (the deferred dV / dK products)
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        ta[4 * dt + 0] = tr_frag(pbuf + SL_DO, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt);
-        ta[4 * dt + 1] = tr_frag(pbuf + SL_DO, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt);
-        ta[4 * dt + 2] = tr_frag(pbuf + SL_Q, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt);
-        ta[4 * dt + 3] = tr_frag(pbuf + SL_Q, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt);
-      }
-    };
-    auto read_s = [&]() {  // this slice's Q / dO rows (S and dP), then lse / delta (the softmax)
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        qa[s] = lds_b128(buf + SL_Q, swz(r, 2 * s + hh));
-        da[s] = lds_b128(buf + SL_DO, swz(r, 2 * s + hh));
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        lq[g] = *reinterpret_cast<const f32x4*>(buf + SL_LSE + 4 * (8 * g + 4 * hh));
-        dq[g] = *reinterpret_cast<const f32x4*>(buf + SL_DEL + 4 * (8 * g + 4 * hh));
-      }
-    };
-    const int j = idx % nqt;
-    const int qbase = (qt0 + j) * QT;
-    const bool dead = !active(idx);
-    const int kill_from = dead ? -(1 << 30) : (masked(idx) ? qbase : 1 << 30);
-    f32x16 sacc = f32x16{}, dpacc = f32x16{};
-    if (kSFirst) {
-      // (2') S and dP as soon as this slice's rows are in, the previous slice's 32 transposed reads
-      // issued between their MFMAs ({1 MFMA, 2 LDS reads} x 16), then the next slice's DMA: every
-      // LDS read of the step still precedes it
-      read_s();
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        sacc = mfma(qa[s], kf[s], sacc);
-        dpacc = mfma(da[s], vf[s], dpacc);
-      }
-      read_t();
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (idx + 1 < nslice) sload(idx + 1, smem + ((rb + 1) % 3) * SL_BYTES);
-    } else {
-      read_t();
-      read_s();
-      // (2) the next slice lands in slot (rb+1)%3 = slice idx-2's, read for the last time last step
-      if (idx + 1 < nslice) sload(idx + 1, smem + ((rb + 1) % 3) * SL_BYTES);
-      // (3) S and dP
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        sacc = mfma(qa[s], kf[s], sacc);
-        dpacc = mfma(da[s], vf[s], dpacc);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // (4) softmax / dS of this slice under the deferred dV/dK MFMAs of the previous one
-    if (kMaskBranch) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sacc[4 * g + e] = fexp2(fmaf(sacc[4 * g + e], c, -lq[g][e]));
-      if (kill_from != (1 << 30)) {  // wave-uniform: a diagonal or dead slice
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sacc[i] = (mykey - crow(i, hh) > kill_from) ? 0.f : sacc[i];
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dpacc[4 * g + e] = sacc[4 * g + e] * (dpacc[4 * g + e] - dq[g][e]);
-    } else {
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * g + e;
-          float pv = fexp2(fmaf(sacc[i], c, -lq[g][e]));
-          pv = (mykey - crow(i, hh) > kill_from) ? 0.f : pv;
-          sacc[i] = pv;
-          dpacc[i] = pv * (dpacc[i] - dq[g][e]);
-        }
-    }
-    const Packs cur{pack8(sacc, 0), pack8(sacc, 8), pack8(dpacc, 0), pack8(dpacc, 8)};
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      dvt[dt] = mfma(ta[4 * dt + 0], prev.p0, dvt[dt]);
-      dvt[dt] = mfma(ta[4 * dt + 1], prev.p1, dvt[dt]);
-      dkt[dt] = mfma(ta[4 * dt + 2], prev.d0, dkt[dt]);
-      dkt[dt] = mfma(ta[4 * dt + 3], prev.d1, dkt[dt]);
-    }
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {  // {1 dV/dK MFMA, 7 softmax VALU} x 16
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    prev = cur;
-    dma_sync();
-  };
-  int idx = 0;
-  for (; idx + 3 <= nslice; idx += 3) {
-    step(idx, 0);
-    step(idx + 1, 1);
-    step(idx + 2, 2);
-  }
-  if (idx < nslice) step(idx, 0);
-  if (idx + 1 < nslice) step(idx + 1, 1);
-  {  // the last slice's deferred dV/dK products
-    const char* pbuf = smem + ((nslice - 1) % 3) * SL_BYTES;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      dvt[dt] = mfma(tr_frag(pbuf + SL_DO, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), prev.p0, dvt[dt]);
-      dvt[dt] = mfma(tr_frag(pbuf + SL_DO, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), prev.p1, dvt[dt]);
-      dkt[dt] = mfma(tr_frag(pbuf + SL_Q, lane, 0 + 4 * hh, 8 + 4 * hh, 32 * dt), prev.d0, dkt[dt]);
-      dkt[dt] = mfma(tr_frag(pbuf + SL_Q, lane, 16 + 4 * hh, 24 + 4 * hh, 32 * dt), prev.d1, dkt[dt]);
-    }
-  }
-  u16* dkrow = dk + ((size_t)(b * Hkv + hk) * S + mykey) * D;
-  u16* dvrow = dv + ((size_t)(b * Hkv + hk) * S + mykey) * D;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      u16x4 a4, b4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        a4[e] = f2bf(dkt[dt][4 * g4 + e] * scale);
-        b4[e] = f2bf(dvt[dt][4 * g4 + e]);
-      }
-      *reinterpret_cast<u16x4*>(dkrow + 32 * dt + 8 * g4 + 4 * hh) = a4;
-      *reinterpret_cast<u16x4*>(dvrow + 32 * dt + 8 * g4 + 4 * hh) = b4;
-    }
-}
-
-// dK/dV v7: v5's slice pipeline with the registers re-budgeted so that S and dP accumulate in VGPRs.
-// v5 (hipcc -S, ROCm 7.2) holds ~460 registers at one wave per SIMD: past 256 the compiler selects the
-// AGPR form for EVERY MFMA, so S / dP land in AGPRs and each slice pays ~100 v_accvgpr_read / write /
-// mov to bring them to the softmax VALU and back -- ~4 cycles each, on a wave whose VALU already fills
-// the MFMA gaps (profiles/r04_attn).  Here:
-//   * -lse/c and -delta enter as the S and dP chains' initial accumulators (the pre-kernel writes them
-//     negated and pre-divided): p = 2^(c * S') and dS = p * dP' need no lse / delta registers and no
-//     subtract;
-//   * the long-lived dV^T / dK^T accumulators (128 registers) are pinned in AGPRs by their MFMAs' asm
-//     constraints (kAsmAcc), so everything else -- K / V rows, the slice's operands, S / dP, the packs
-//     -- fits the 256 VGPRs and the S / dP MFMAs stay in VGPR form: no accumulator moves.
-template <bool kEarlyDma, bool kStreamT>
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv7_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(const u16* __restrict__ q, const u16* __restrict__ k,
                                                                 const u16* __restrict__ v, const u16* __restrict__ dout,
                                                                 const float* __restrict__ nls, const float* __restrict__ ndl,
                                                                 u16* __restrict__ dk, u16* __restrict__ dv, int H, int Hkv,
@@ -721,10 +479,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv7_kernel(const u16* __res
   dma_sync();
   // buf: this slice; pbuf: the previous one (its deferred dV/dK products); nbuf: the slot the next
   // slice's DMA fills.  As __restrict__ parameters the three are provably disjoint, so no read of buf /
-  // pbuf waits for the DMA into nbuf (kEarlyDma issues it before them: a whole step to land)
+  // pbuf waits for the DMA into nbuf, issued first: it has a whole step to land
   auto step = [&](int idx, const char* __restrict__ buf, const char* __restrict__ pbuf, char* __restrict__ nbuf) {
     const int nj = cur_j + 1 == nqt ? 0 : cur_j + 1, nh = cur_j + 1 == nqt ? cur_h + 1 : cur_h;
-    if (kEarlyDma && idx + 1 < nslice) sload(nh, nj, nbuf);
+    if (idx + 1 < nslice) sload(nh, nj, nbuf);
     // (1) this slice's -lse/c, -delta (the S / dP chains' initial accumulators) and its rows
     f32x16 sacc, dpacc;
 #pragma unroll
@@ -751,44 +509,28 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv7_kernel(const u16* __res
     // dV/dK product i in issue order: accumulators round-robin, so an accumulator's two products are
     // 4 MFMAs apart
     auto tix = [](int i) { return 4 * (i & 3) + (i >> 2); };
-    // (2) S' = S - lse/c and dP' = dP - delta.  kStreamT: the transposed fragments are read in phase
-    // (4), two products ahead of their use (12 registers instead of 64 -- what lets this slice's rows
-    // all be read ahead of the S / dP chains); else all 16 read here, between those MFMAs
+    // (2) S' = S - lse/c and dP' = dP - delta.  The transposed fragments of phase (3) are read two
+    // products ahead of their use; the first two here.  16 of the step's 28 LDS reads (8 init quads, 16
+    // rows, 4 transposed halves) go before the first MFMA, then one per MFMA: every MFMA's rows were
+    // issued ~7 MFMAs earlier (fewer up front and the compiler streams the rows through one register
+    // quad, each MFMA waiting on its own read)
     bf16x8 ta[16];
-    if (kStreamT) {
-      ta[tix(0)] = tfrag(tix(0));
-      ta[tix(1)] = tfrag(tix(1));
-    }
+    ta[tix(0)] = tfrag(tix(0));
+    ta[tix(1)] = tfrag(tix(1));
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       sacc = mfma(qa[s], kf[s], sacc);
       dpacc = mfma(da[s], vf[s], dpacc);
     }
-    if (kStreamT) {
-      // the init quads and the first two rows of Q and dO, then one more row per MFMA: the chains start
-      // as soon as their first operands land and every later row is in flight under an MFMA
-      // (the first two transposed fragments of phase (4) with the first reads)
-      __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
 #pragma unroll
-      for (int g = 0; g < 12; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-    } else {
-#pragma unroll
-      for (int ti = 0; ti < 16; ++ti) ta[ti] = tfrag(ti);
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      }
+    for (int g = 0; g < 12; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
     __builtin_amdgcn_sched_barrier(0);
-    // (3) the next slice's DMA (late variant): every LDS read of this step precedes it
-    if (!kEarlyDma && idx + 1 < nslice) sload(nh, nj, nbuf);
-    __builtin_amdgcn_sched_barrier(0);
-    // (4) softmax / dS of this slice under the deferred dV/dK MFMAs of the previous one
+    // (3) softmax / dS of this slice under the deferred dV/dK MFMAs of the previous one
     // diagonal slices (the block's first KB/QT query tiles) mask from qbase; slices wholly above this
     // wave's keys are dead (every score masked)
     const int qbase = (qt0 + cur_j) * QT;
@@ -807,7 +549,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv7_kernel(const u16* __res
       f32x16& acc = part < 2 ? dvt[dt] : dkt[dt];
       const bf16x8 bb = part == 0 ? prev.p0 : part == 1 ? prev.p1 : part == 2 ? prev.d0 : prev.d1;
       acc_mfma(acc, ta[ti], bb);
-      if (kStreamT && i + 2 < 16) ta[tix(i + 2)] = tfrag(tix(i + 2));
+      if (i + 2 < 16) ta[tix(i + 2)] = tfrag(tix(i + 2));
     };
 #pragma unroll
     for (int i = 0; i < 8; ++i) {  // gaps 0-7: p = 2^(c S') for two scores each (mul + exp: 24 cycles)
@@ -1044,58 +786,25 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
   return attn_fwd_impl(q, k, v, scale, false);
 }
 
-// backward v5: delta, dK/dV v5, dQ (round-4 default; A/B reference for v7)
-std::vector<at::Tensor> attn_bwd_v5(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                    const at::Tensor& out, const at::Tensor& lse, double scale) {
-  check_qkv(q, k, v);
-  const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
-  TORCH_CHECK(dout.is_contiguous() && out.is_contiguous() && dout.numel() == q.numel() && out.numel() == q.numel(),
-              "attention bwd: dout/out must be contiguous [B, S, H, D]");
-  auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
-  auto dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
-  const int rows = B * S * H;
-  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
-                     delta.data_ptr<float>(), B, H, S);
-  const float c = (float)(scale * 1.4426950408889634);
-  hipLaunchKernelGGL(attn_bwd_dkdv5_kernel<true>, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v),
-                     bp(dout), lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
-  hipLaunchKernelGGL(attn_bwd_dq2n_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
-                     lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
-  return {dq, dk, dv};
-}
-
+// backward: delta (+ -lse/c, -delta for dK/dV), dK/dV, dQ
 std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                  const at::Tensor& out, const at::Tensor& lse, double scale) {
-  return attn_bwd_v5(dout, q, k, v, out, lse, scale);
-}
-
-// dK/dV v7 (S / dP in VGPRs, -lse/c and -delta as their chains' initial accumulators) + dQ
-std::vector<at::Tensor> attn_bwd_v7(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                    const at::Tensor& out, const at::Tensor& lse, double scale, int64_t variant) {
   check_qkv(q, k, v);
   const int B = q.size(0), H = q.size(1), S = q.size(2), Hkv = k.size(1);
   TORCH_CHECK(dout.is_contiguous() && out.is_contiguous() && dout.numel() == q.numel() && out.numel() == q.numel(),
               "attention bwd: dout/out must be contiguous [B, S, H, D]");
-  TORCH_CHECK(lse.is_contiguous() && lse.numel() == (int64_t)B * H * S, "attention bwd: lse must be [B, H, S]");
+  TORCH_CHECK(lse.is_contiguous() && lse.scalar_type() == at::kFloat && lse.numel() == (int64_t)B * H * S,
+              "attention bwd: lse must be fp32 [B, H, S]");
   auto fopt = q.options().dtype(at::kFloat);
   auto delta = at::empty({B, H, S}, fopt), nls = at::empty({B, H, S}, fopt), ndl = at::empty({B, H, S}, fopt);
   auto dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
   const int rows = B * S * H;
   const float c = (float)(scale * 1.4426950408889634);
-  hipLaunchKernelGGL(attn_bwd_pre7_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
+  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(), bp(dout), bp(out),
                      lse.data_ptr<float>(), delta.data_ptr<float>(), nls.data_ptr<float>(), ndl.data_ptr<float>(), B, H, S,
                      1.f / c);
-  // variant bit 0: the next slice's DMA at the step start; bit 1: transposed fragments streamed in phase (4)
-  auto launch = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
-                       nls.data_ptr<float>(), ndl.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
-  };
-  switch (variant & 3) {
-    case 0: launch(attn_bwd_dkdv7_kernel<false, false>); break;
-    case 1: launch(attn_bwd_dkdv7_kernel<true, false>); break;
-    case 2: launch(attn_bwd_dkdv7_kernel<false, true>); break;
-    default: launch(attn_bwd_dkdv7_kernel<true, true>); break;
-  }
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(B * Hkv, S / KB), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
+                     nls.data_ptr<float>(), ndl.data_ptr<float>(), bpm(dk), bpm(dv), H, Hkv, S, c, (float)scale);
   hipLaunchKernelGGL(attn_bwd_dq2n_kernel, dim3(B * H, S / BQ), dim3(256), 0, cur_stream(), bp(q), bp(k), bp(v), bp(dout),
                      lse.data_ptr<float>(), delta.data_ptr<float>(), bpm(dq), H, Hkv, S, c, (float)scale);
   return {dq, dk, dv};

@@ -1379,10 +1379,6 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
 std::vector<at::Tensor> attn_fwd_t(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale);
 std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                  const at::Tensor& out, const at::Tensor& lse, double scale);
-std::vector<at::Tensor> attn_bwd_v5(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                    const at::Tensor& out, const at::Tensor& lse, double scale);
-std::vector<at::Tensor> attn_bwd_v7(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                                    const at::Tensor& out, const at::Tensor& lse, double scale, int64_t variant);
 }  // namespace gtk_attn
 
 namespace gtk_xpose {  // csrc/ops/transpose.hip
@@ -1404,8 +1400,6 @@ PYBIND11_MODULE(_fused, m) {
   m.def("attn_fwd", &gtk_attn::attn_fwd, "causal GQA flash attention forward (bf16, D=128): -> (o [B,S,H,D], lse2 [B,H,S])");
   m.def("attn_fwd_t", &gtk_attn::attn_fwd_t, "attn_fwd that also writes O^T [H*D, B*S]: -> (o, lse2, ot)");
   m.def("attn_bwd", &gtk_attn::attn_bwd, "flash attention backward: -> (dq, dk, dv)");
-  m.def("attn_bwd_v5", &gtk_attn::attn_bwd_v5, "backward with dK/dV v5 (round-4 default; A/B reference)");
-  m.def("attn_bwd_v7", &gtk_attn::attn_bwd_v7, "backward with dK/dV v7 (S / dP in VGPRs; variant 0: dV/dK accumulators pinned to AGPRs, 1: + next slice's DMA at the step start, 2: accumulators left to the compiler)");
   m.doc() = "gfx950 fused kernels for the Llama-3 DP validation workload";
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);

@@ -102,6 +102,13 @@ print(json.dumps({"tflops": round(float(w["tflops"]), 1), "hbm_copy_gbps": round
     step ab_b2 300 python -u bench/attn_bench.py --b 2 --ab 30
     step pmc_attn 120 timeout -s KILL 100 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_BUSY_CYCLES --kernel-trace -d "$out/pmc_attn" -o run -- python3 tools/pmc_attn.py
     ;;
+  attn_step)
+    # round 5: attention kernel tests, the fused-op tests, then the Llama-3-8B step with this tree's
+    # attention backward against the round-4 build's (scratch/r04, interleaved), and the step's trace
+    step pytest_attn 600 python -u -m pytest tests/test_attention_gpu.py tests/test_fused_gpu.py -x -v --timeout 300 --timeout-method thread
+    step step_ab 900 python -u bench/attn_step_ab.py --so ${AB_SO:-scratch/r04/_fused.cpython-310-x86_64-linux-gnu.so} --rounds 4 --steps 3
+    step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
+    ;;
   shadow)
     # what 8-GPU DP communication costs the Llama-3-8B step: comm-shadow CTA sweep
     step shadow_sweep 1100 python -u bench/comm_shadow_sweep.py --ctas ${SHADOW_CTAS:-0,8,16,32,64} --busbw ${SHADOW_BUSBW:-350} --out "$out/shadow.jsonl" ${SHADOW_ZERO1:+--zero1}

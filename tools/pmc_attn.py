@@ -29,12 +29,6 @@ def main():
     for _ in range(3):
         o, lse = hip.attn_fwd(q, k, v, D ** -0.5)
         hip.attn_bwd(do, q, k, v, o, lse, D ** -0.5)
-    # the dK/dV generations the extension exports, same pass: per-kernel counters of each
-    for name, args in (("attn_bwd_v5", ()), ("attn_bwd_v7", (0,)), ("attn_bwd_v7", (1,)), ("attn_bwd_v7", (2,)),
-                       ("attn_bwd_v7", (3,))):
-        if hasattr(hip, name):
-            for _ in range(3):
-                getattr(hip, name)(do, q, k, v, o, lse, D ** -0.5, *args)
     torch.cuda.synchronize()
     print("pmc_attn done", flush=True)
 
