@@ -452,9 +452,10 @@ def ring_ms(nbytes, k=8, busbw=350.0):
 
 
 def test_training_with_the_default_rccl_cta_cap_initialises_its_communicator():
-    """models/train.py passes --comm-ctas (default parallel/dp.py DEFAULT_COMM_CTAS) to RCCL as
+    """models/train.py passes --comm-ctas N (here parallel/dp.py DEFAULT_COMM_CTAS) to RCCL as
     ncclConfig_t maxCTAs through the process group's options; at world 1 the barrier and the timing
-    all-reduce still create the communicator, so the capped config is exercised on one GPU."""
+    all-reduce still create the communicator, so the capped config is exercised on one GPU.  (The
+    default, auto, picks among capped communicators at world > 1: tests/test_dp_check.py.)"""
     import json
     import os
     import subprocess
@@ -463,11 +464,11 @@ def test_training_with_the_default_rccl_cta_cap_initialises_its_communicator():
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
     p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd.models.train", "--model", "tiny", "--batch", "2",
-                        "--seq", "128", "--steps", "2", "--warmup", "1", "--gemm-tuning", "off"],
+                        "--seq", "128", "--steps", "2", "--warmup", "1", "--gemm-tuning", "off", "--comm-ctas", "64"],
                        capture_output=True, text=True, timeout=300, cwd=repo, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
-    assert r["comm_ctas"] == 64 and r["n_gpus"] == 1
+    assert r["comm_ctas"] == 64 and r["n_gpus"] == 1 and r["comm_ctas_tuning"] is None
 
 
 @pytest.mark.parametrize("T,F", [(64, 128), (256, 512), (16384 // 8, 14336 // 8)])
