@@ -176,7 +176,7 @@ def main(argv=None) -> int:
         outcome, msg = repartition(api, a.node_name, contract, idle_fn, reload_driver=a.partition_driver_reload,
                                    settle_s=a.probe_settle_seconds, wait=wait, hold=hold,
                                    time_slices=node_time_slices(api, a.node_name, contract, a.time_slices))
-        if outcome in ("ok", "failed", "invalid"):
+        if outcome in ("ok", "partial", "failed", "invalid"):
             (log.warning if outcome != "ok" else log.info)("partition request: %s: %s", outcome, msg)
         return outcome, msg
 
@@ -298,7 +298,7 @@ def main(argv=None) -> int:
                     plugin.maintenance.release()
             if outcome not in ("none", "same"):
                 plugin.metrics.partition_changes.labels(outcome).inc()
-            if outcome == "ok":
+            if outcome in ("ok", "partial"):  # the device layout changed: re-register it
                 plugin.layout_change_reason = f"GPU partitions {msg} (node label)"
                 plugin.layout_change.set()
             elif outcome == "busy" and ticks % 300 == 0:

@@ -58,7 +58,10 @@ def repartition(api, node_name: str, contract: Contract, idle_fn: Callable[[], b
     """One reconciliation pass.  -> (outcome, message), outcome one of
     ``none`` (no request), ``same`` (already there), ``invalid``, ``skipped`` (this request failed
     before), ``unavailable`` (amdsmi reports no package: nothing recorded, the next pass asks again),
-    ``busy`` (pods hold devices), ``stopped`` (``wait`` returned True), ``ok``, ``failed``.
+    ``busy`` (pods hold devices), ``stopped`` (``wait`` returned True), ``ok``, ``failed`` (nothing
+    changed), ``partial`` (failed, but the device layout changed on the way -- a compute step took on
+    some packages, or a memory step and its driver reload ran before a later step failed: the plugin
+    must restart like after ``ok``).
 
     ``hold`` (``DevicePluginServer.allocation_hold``) holds the plugin's Allocate from the moment the
     node is marked until the switch is over.  An Allocate that arrives meanwhile (a bind already past
@@ -115,11 +118,12 @@ def repartition(api, node_name: str, contract: Contract, idle_fn: Callable[[], b
                 res = apply_partition(want_c, want_m, lib=lib, reload_driver=reload_driver, before_reload=still_idle)
             except Exception as e:  # noqa: BLE001 - PartitionError, or amdsmi without the setters: recorded, not retried
                 res = {"ok": False, "reason": str(e)[:500]}
+            # the old device IDs are stale exactly when the exposed devices changed: a compute step that
+            # took (even if a later one failed), a memory step only once the driver reloaded -- not a
+            # memory mode pending a reload, nor a reload held back for an arriving Allocate
+            changed = bool(res.get("layout_changed", res["ok"]))
             if h is not None:
-                # a memory step may have been applied even when a later step failed: any change of
-                # the package's modes makes the old device IDs stale
-                h.switched = bool(res["ok"] or any(st.get("set") in ("compute", "memory") and all(
-                    p.get("status") == "ok" for p in st.get("packages", [])) for st in res.get("steps", [])))
+                h.switched = changed
         if res["ok"]:
             switched = True
             api.patch_node(node_name, annotations={contract.partition_failed_key: None})
@@ -127,6 +131,9 @@ def repartition(api, node_name: str, contract: Contract, idle_fn: Callable[[], b
             return "ok", f"{before} -> {tag}"
         api.patch_node(node_name, annotations={contract.partition_failed_key: f"{tag}: {res['reason']}"[:1000]})
         _event(api, node_name, "FailedGPUPartitionChange", f"{before} -> {tag}: {res['reason']}", "Warning")
+        if changed:
+            switched = True  # keep the mark: the restarted plugin publishes the changed layout and clears it
+            return "partial", f"{before} -> {tag} partly applied: {res['reason']}"
         return "failed", res["reason"]
     finally:
         if not switched:  # after a switch the restarted plugin clears it, once the new layout is published

@@ -94,8 +94,11 @@ def _check_offered(info: Sequence[dict], compute: Optional[str], memory: Optiona
 def apply_partition(compute: Optional[str] = None, memory: Optional[str] = None, lib: Optional[str] = None,
                     reload_driver: bool = False, before_reload: Optional[Callable[[], bool]] = None) -> dict:
     """Switch every package to ``compute`` / ``memory`` (None = keep).  The caller guarantees that no
-    process uses the GPUs.  -> ``{"ok", "steps", "before", "after", "reason", "reload_required"}``;
-    ``ok`` is False (with ``reason``) when amdsmi refused a step.  Nothing is retried.
+    process uses the GPUs.  -> ``{"ok", "steps", "before", "after", "reason", "reload_required",
+    "reloaded", "layout_changed"}``; ``ok`` is False (with ``reason``) when amdsmi refused a step.
+    Nothing is retried.  ``layout_changed``: the devices the node exposes changed, whatever ``ok`` says
+    -- a compute step took effect on some package (its XCP count changed at once), or a memory step
+    was followed by a driver reload.  A memory mode only pending a reload changes nothing yet.
     ``before_reload`` is asked right before a driver reload (the most disruptive step); False stops
     the switch there (the caller saw a pod claim a device since its own idle check)."""
     compute, memory = normalise(compute, memory)
@@ -109,10 +112,13 @@ def apply_partition(compute: Optional[str] = None, memory: Optional[str] = None,
     cur_m = before[0]["memory"]
     mixed = any(p["compute"] != cur_c or p["memory"] != cur_m for p in before)
     steps = plan_steps("" if mixed else cur_c, "" if mixed else cur_m, compute, memory)
-    out = {"ok": True, "before": before, "steps": [], "reason": "", "reload_required": False, "reloaded": False}
+    out = {"ok": True, "before": before, "steps": [], "reason": "", "reload_required": False, "reloaded": False,
+           "layout_changed": False}
     for what, mode in steps:
         res = [(bdf, int(code)) for bdf, code in mod.set_partition_step(lib, what, mode)]
         out["steps"].append({"set": what, "mode": mode, "packages": [{"bdf": b, "status": status_name(c)} for b, c in res]})
+        if what == "compute" and any(c == 0 for _, c in res):
+            out["layout_changed"] = True  # effective at once on every package that accepted it
         bad = [(b, c) for b, c in res if c != 0]
         if bad:
             out["ok"] = False
@@ -139,6 +145,7 @@ def apply_partition(compute: Optional[str] = None, memory: Optional[str] = None,
                 out["reason"] = f"amdgpu driver reload: {status_name(code)}"
                 break
             out["reloaded"] = True
+            out["layout_changed"] = True
     out["after"] = partition_info(lib)
     if out["ok"]:
         wrong = [p["bdf"] for p in out["after"]

@@ -382,3 +382,67 @@ def test_driver_reload_is_held_back_when_the_node_stops_being_idle(node):
     r = apply_partition("CPX", "NPS4", reload_driver=True, before_reload=lambda: False)
     assert not r["ok"] and r["reload_required"] and "held back" in r["reason"]
     assert not any(s["set"] == "driver-reload" for s in r["steps"])
+
+
+def test_allocate_held_while_a_reload_is_held_back_proceeds(node, tmp_path, monkeypatch):
+    """ADVICE r4 (repartition.py:121): a memory mode set but pending its driver reload changes no
+    device; when the reload is held back for the very Allocate that arrived, that Allocate must
+    proceed on the (unchanged) layout instead of being refused as stale."""
+    import threading
+    import time
+
+    from gpu_topology_on_k8s_amd.deviceplugin import repartition as rp
+
+    assert apply_partition("CPX")["ok"]  # CPX/NPS1: the request below is a memory-only change
+    api, plug = _held_plugin(tmp_path)
+    c = Contract()
+    api.patch_node("w", labels={c.partition_request_label: "CPX", c.memory_partition_request_label: "NPS4"})
+    real = rp.apply_partition
+    started = threading.Event()
+
+    def apply_when_contended(*a, **kw):
+        started.set()
+        t0 = time.time()
+        while not plug._hold.contended():  # the Allocate below is waiting on the hold
+            assert time.time() - t0 < 5
+            time.sleep(0.01)
+        return real(*a, **kw)
+
+    monkeypatch.setattr(rp, "apply_partition", apply_when_contended)
+    out = {}
+    th = threading.Thread(target=lambda: out.setdefault("r", rp.repartition(
+        api, "w", c, lambda: True, settle_s=0, reload_driver=True, hold=plug.allocation_hold)))
+    th.start()
+    assert started.wait(5)
+    resp = plug.Allocate(_alloc_req(1), _Ctx())  # waits for the switch, then is served: nothing changed
+    th.join(5)
+    assert len(resp.container_responses) == 1
+    assert out["r"][0] == "failed" and "held back" in out["r"][1]
+    assert not plug._stale_layout
+    # ... and the node is not left marked: nothing to republish
+    assert c.probing_key not in (api.get_node("w")["metadata"].get("annotations") or {})
+
+
+def test_a_partial_switch_is_reported_as_a_layout_change(node, tmp_path, monkeypatch):
+    """A compute step that took before a later step failed changed the exposed devices: the pass says
+    ``partial`` (the daemon restarts for it, like after ``ok``), held Allocates are refused, and the
+    node stays marked until the restarted plugin publishes the new layout."""
+    from gpu_topology_on_k8s_amd.deviceplugin import repartition as rp
+
+    api, plug = _held_plugin(tmp_path)
+    monkeypatch.setattr(rp, "apply_partition", lambda *a, **kw: {
+        "ok": False, "layout_changed": True, "reason": "memory partition NPS4: fake refusal",
+        "steps": [{"set": "compute", "mode": "CPX", "packages": [{"bdf": "x", "status": "ok"}]}]})
+    outcome, msg = rp.repartition(api, "w", Contract(), lambda: True, settle_s=0, hold=plug.allocation_hold)
+    assert outcome == "partial" and "partly applied" in msg
+    assert plug._stale_layout
+    assert Contract().probing_key in (api.get_node("w")["metadata"].get("annotations") or {})
+
+
+def test_apply_partition_reports_whether_the_layout_changed(node):
+    r = apply_partition("CPX")
+    assert r["ok"] and r["layout_changed"]
+    r = apply_partition("CPX", "NPS4", reload_driver=False)  # pending a reload: no device changed yet
+    assert not r["ok"] and r["reload_required"] and not r["layout_changed"]
+    r = apply_partition("CPX", "NPS4", reload_driver=True)
+    assert r["ok"] and r["reloaded"] and r["layout_changed"]
