@@ -4,11 +4,15 @@
 // host allocations from the CPU pool, hipMemCreate from hsa_amd_vmem_handle_create, and a stream is
 // an HSA queue on the current GPU.  Built as bin/fake_hip/libamdhip64.so so the guard's fallback
 // lookup (a runtime loaded RTLD_LOCAL, found by name among the loaded objects) is exercised exactly
-// as with the PyTorch wheel's bundled runtime.  The current device comes from $FAKE_HIP_DEVICE; the
-// device has 64 GiB.
+// as with the PyTorch wheel's bundled runtime.  The current device comes from $FAKE_HIP_DEVICE, a HIP
+// ordinal: $HIP_VISIBLE_DEVICES maps it to a ROCr ordinal and the stand-in ROCr's $ROCR_VISIBLE_DEVICES
+// that to a physical GPU, whose PCI address hipDeviceGetPCIBusId reports.  Each device has 64 GiB.
+// hipMallocManaged returns system memory that no device pool is charged for (HMM-backed managed memory,
+// ADVICE r4), which the guard has to charge at the HIP level.
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -19,6 +23,8 @@ const char* fake_hsa_queue_mask(const hsa_queue_t* q);
 uint64_t fake_hsa_gpu_pool(int gpu);
 uint64_t fake_hsa_cpu_pool();
 uint64_t fake_hsa_gpu_agent(int gpu);
+int fake_hsa_physical(int ordinal);
+int fake_hsa_visible_count();
 
 typedef int hipError_t;
 static const unsigned long long kTotal = 64ull << 30;
@@ -32,15 +38,53 @@ struct hipPitchedPtr {
   size_t pitch, xsize, ysize;
 };
 
-static int cur() {
+// HIP ordinal -> ROCr ordinal ($HIP_VISIBLE_DEVICES), -1 when not visible
+static int rocr_ordinal(int hip) {
+  const char* v = std::getenv("HIP_VISIBLE_DEVICES");
+  if (!v || !*v) return hip;
+  int i = 0;
+  for (const char* c = v; *c; ++i) {
+    char* e = nullptr;
+    long o = std::strtol(c, &e, 10);
+    if (e == c) break;
+    if (i == hip) return (int)o;
+    c = *e == ',' ? e + 1 : e;
+  }
+  return -1;
+}
+
+static int physical(int hip) { return fake_hsa_physical(rocr_ordinal(hip)); }
+
+static int hip_device() {
   const char* e = std::getenv("FAKE_HIP_DEVICE");
   return e ? std::atoi(e) : 0;
+}
+
+static int cur() {  // the current device, as the physical GPU whose pool / agent serve it
+  const int p = physical(hip_device());
+  return p < 0 ? 0 : p;
 }
 
 static void init() { hsa_init(); }
 
 static hipError_t status(hsa_status_t s) {
   return s == HSA_STATUS_SUCCESS ? kOk : s == HSA_STATUS_ERROR_OUT_OF_RESOURCES ? kOom : kInvalid;
+}
+
+// managed blocks handed out (hipFree must tell them from pool blocks without touching memory)
+static void* g_managed[4096];
+static int g_nmanaged = 0;
+static bool g_managed_contains(void* p) {
+  for (int i = 0; i < g_nmanaged; ++i)
+    if (g_managed[i] == p) return true;
+  return false;
+}
+static void g_managed_erase(void* p) {
+  for (int i = 0; i < g_nmanaged; ++i)
+    if (g_managed[i] == p) {
+      g_managed[i] = g_managed[--g_nmanaged];
+      return;
+    }
 }
 
 static hipError_t dev_alloc(void** p, size_t n) {
@@ -62,7 +106,14 @@ __attribute__((visibility("default"))) hipError_t hipInit(unsigned int) {
 }
 __attribute__((visibility("default"))) hipError_t hipGetDeviceCount(int* n) {
   init();
-  if (n) *n = 2;
+  if (n) *n = fake_hsa_visible_count();
+  return kOk;
+}
+__attribute__((visibility("default"))) hipError_t hipDeviceGetPCIBusId(char* bus, int len, int dev) {
+  init();
+  const int p = physical(dev);
+  if (!bus || len < 13 || p < 0) return kInvalid;
+  std::snprintf(bus, (size_t)len, "0000:%02x:00.0", 0x05 + 0x10 * p);
   return kOk;
 }
 __attribute__((visibility("default"))) hipError_t hipSetDevice(int) {
@@ -71,7 +122,7 @@ __attribute__((visibility("default"))) hipError_t hipSetDevice(int) {
 }
 __attribute__((visibility("default"))) hipError_t hipGetDevice(int* d) {
   init();
-  *d = cur();
+  *d = hip_device();
   return kOk;
 }
 __attribute__((visibility("default"))) hipError_t hipRuntimeGetVersion(int* v) {
@@ -87,7 +138,17 @@ __attribute__((visibility("default"))) hipError_t hipDeviceGetAttribute(int* v, 
 
 __attribute__((visibility("default"))) hipError_t hipMalloc(void** p, size_t n) { return dev_alloc(p, n); }
 __attribute__((visibility("default"))) hipError_t hipExtMallocWithFlags(void** p, size_t n, unsigned int) { return dev_alloc(p, n); }
-__attribute__((visibility("default"))) hipError_t hipMallocManaged(void** p, size_t n, unsigned int) { return dev_alloc(p, n); }
+static const unsigned kManagedTag = 0x6d616e67;  // "mang": system memory, freed by hipFree like device memory
+__attribute__((visibility("default"))) hipError_t hipMallocManaged(void** p, size_t n, unsigned int) {
+  init();
+  if (!p) return kInvalid;
+  unsigned* b = static_cast<unsigned*>(std::malloc(32 + (n & 7)));
+  if (!b) return kOom;
+  b[0] = kManagedTag;
+  *p = b + 4;
+  if (g_nmanaged < 4096) g_managed[g_nmanaged++] = *p;
+  return kOk;
+}
 __attribute__((visibility("default"))) hipError_t hipMallocAsync(void** p, size_t n, void*) { return dev_alloc(p, n); }
 __attribute__((visibility("default"))) hipError_t hipMallocFromPoolAsync(void** p, size_t n, void*, void*) { return dev_alloc(p, n); }
 __attribute__((visibility("default"))) hipError_t hipMallocPitch(void** p, size_t* pitch, size_t w, size_t h) {
@@ -110,7 +171,13 @@ __attribute__((visibility("default"))) hipError_t hipHostMalloc(void** p, size_t
 }
 __attribute__((visibility("default"))) hipError_t hipFree(void* p) {
   init();
-  return p ? status(hsa_amd_memory_pool_free(p)) : kOk;
+  if (!p) return kOk;
+  if (g_managed_contains(p)) {
+    g_managed_erase(p);
+    std::free(static_cast<unsigned*>(p) - 4);
+    return kOk;
+  }
+  return status(hsa_amd_memory_pool_free(p));
 }
 __attribute__((visibility("default"))) hipError_t hipFreeAsync(void* p, void*) { return hipFree(p); }
 __attribute__((visibility("default"))) hipError_t hipHostFree(void* p) { return hipFree(p); }

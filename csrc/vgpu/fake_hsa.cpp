@@ -2,8 +2,10 @@
 // bin/fake_hip/libhsa-runtime64.so and linked by the stand-in HIP runtime (fake_hip.cpp) the way the
 // real libamdhip64 links libhsa-runtime64.  It models what the guard relies on:
 //   * hsa_init reads HSA_CU_MASK once, as ROCr does (fake_hsa_init_mask() returns what it read);
-//   * agents: a CPU agent first, then two GPU agents (ordinals 0 and 1) with 256 CUs each; every
-//     agent has one global memory pool; allocations are tiny host blocks (the size is bookkept);
+//   * agents: a CPU agent first, then two GPU agents with 256 CUs each, physical GPU p at PCI address
+//     0000:(05 + 0x10 p):00.0 (HSA_AMD_AGENT_INFO_BDFID / _DOMAIN); $ROCR_VISIBLE_DEVICES ("1,0", "1")
+//     selects and orders them as ROCr does, so ordinals need not be physical indices; every agent has
+//     one global memory pool; allocations are tiny host blocks (the size is bookkept);
 //   * queues: a created queue starts with the CU mask HSA_CU_MASK gave its GPU at hsa_init (all CUs
 //     when none), hsa_amd_queue_cu_set_mask replaces it; fake_hsa_queue_mask(q) renders the mask
 //     a queue runs with as a CU list ("0-63").
@@ -29,7 +31,30 @@ constexpr uint64_t kCpuPool = 0x3000, kGpuPool0 = 0x4000;
 std::mutex g_mu;
 bool g_inited = false;
 char g_init_mask[4096] = "(never initialised)";
-std::vector<uint32_t> g_env_bits[kGpus];  // HSA_CU_MASK as read at hsa_init
+std::vector<uint32_t> g_env_bits[kGpus];  // HSA_CU_MASK as read at hsa_init, by ordinal
+std::vector<int> g_visible;                // ordinal -> physical GPU ($ROCR_VISIBLE_DEVICES at hsa_init)
+
+void parse_visible() {
+  g_visible.clear();
+  const char* v = std::getenv("ROCR_VISIBLE_DEVICES");
+  if (!v || !*v) {
+    for (int p = 0; p < kGpus; ++p) g_visible.push_back(p);
+    return;
+  }
+  for (const char* c = v; *c;) {
+    char* e = nullptr;
+    long p = std::strtol(c, &e, 10);
+    if (e == c) break;
+    if (p >= 0 && p < kGpus) g_visible.push_back((int)p);
+    c = *e == ',' ? e + 1 : e;
+  }
+}
+
+int ordinal_of(int phys) {
+  for (size_t o = 0; o < g_visible.size(); ++o)
+    if (g_visible[o] == phys) return (int)o;
+  return -1;
+}
 struct FakeQueue {
   hsa_queue_t q;
   int gpu;
@@ -108,6 +133,7 @@ __attribute__((visibility("default"))) hsa_status_t hsa_init() {
   std::lock_guard<std::mutex> g(g_mu);
   if (g_inited) return HSA_STATUS_SUCCESS;
   g_inited = true;
+  parse_visible();
   const char* m = std::getenv("HSA_CU_MASK");
   std::strncpy(g_init_mask, m ? m : "", sizeof(g_init_mask) - 1);
   parse_env_mask(m);
@@ -117,14 +143,38 @@ __attribute__((visibility("default"))) hsa_status_t hsa_init() {
 __attribute__((visibility("default"))) hsa_status_t hsa_iterate_agents(hsa_status_t (*cb)(hsa_agent_t, void*), void* data) {
   hsa_agent_t a{kCpuAgent};
   hsa_status_t e = cb(a, data);
-  for (int i = 0; i < kGpus && e == HSA_STATUS_SUCCESS; ++i) e = cb(hsa_agent_t{kGpuAgent0 + (uint64_t)i}, data);
+  for (size_t o = 0; o < g_visible.size() && e == HSA_STATUS_SUCCESS; ++o)
+    e = cb(hsa_agent_t{kGpuAgent0 + (uint64_t)g_visible[o]}, data);
   return e == HSA_STATUS_INFO_BREAK ? HSA_STATUS_SUCCESS : e;
 }
 
 __attribute__((visibility("default"))) hsa_status_t hsa_agent_get_info(hsa_agent_t agent, hsa_agent_info_t attr, void* value) {
-  if (attr != HSA_AGENT_INFO_DEVICE) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
-  *static_cast<hsa_device_type_t*>(value) = agent.handle == kCpuAgent ? HSA_DEVICE_TYPE_CPU : HSA_DEVICE_TYPE_GPU;
-  return HSA_STATUS_SUCCESS;
+  const bool cpu = agent.handle == kCpuAgent;
+  if (attr == HSA_AGENT_INFO_DEVICE) {
+    *static_cast<hsa_device_type_t*>(value) = cpu ? HSA_DEVICE_TYPE_CPU : HSA_DEVICE_TYPE_GPU;
+    return HSA_STATUS_SUCCESS;
+  }
+  if ((int)attr == (int)HSA_AMD_AGENT_INFO_BDFID && !cpu) {  // bus << 8 | device << 3 | function
+    *static_cast<uint32_t*>(value) = (uint32_t)(0x05 + 0x10 * (int)(agent.handle - kGpuAgent0)) << 8;
+    return HSA_STATUS_SUCCESS;
+  }
+  if ((int)attr == (int)HSA_AMD_AGENT_INFO_DOMAIN && !cpu) {
+    *static_cast<uint32_t*>(value) = 0;
+    return HSA_STATUS_SUCCESS;
+  }
+  return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+}
+
+// ROCr ordinal -> physical GPU (for the stand-in HIP runtime's device numbering); -1 when not visible
+__attribute__((visibility("default"))) int fake_hsa_physical(int ordinal) {
+  std::lock_guard<std::mutex> g(g_mu);
+  if (!g_inited) parse_visible();
+  return ordinal >= 0 && ordinal < (int)g_visible.size() ? g_visible[ordinal] : -1;
+}
+__attribute__((visibility("default"))) int fake_hsa_visible_count() {
+  std::lock_guard<std::mutex> g(g_mu);
+  if (!g_inited) parse_visible();
+  return (int)g_visible.size();
 }
 
 __attribute__((visibility("default"))) hsa_status_t hsa_amd_agent_iterate_memory_pools(
@@ -186,7 +236,8 @@ __attribute__((visibility("default"))) hsa_status_t hsa_queue_create(hsa_agent_t
   FakeQueue* fq = new FakeQueue();
   std::memset(&fq->q, 0, sizeof(fq->q));
   fq->gpu = (int)(agent.handle - kGpuAgent0);
-  fq->mask = g_env_bits[fq->gpu].empty() ? all_cus() : g_env_bits[fq->gpu];
+  const int ord = ordinal_of(fq->gpu);  // HSA_CU_MASK names ordinals, not physical GPUs
+  fq->mask = (ord < 0 || g_env_bits[ord].empty()) ? all_cus() : g_env_bits[ord];
   g_queues[&fq->q] = fq;
   *queue = &fq->q;
   return HSA_STATUS_SUCCESS;

@@ -15,8 +15,11 @@
 //     refused with HSA_STATUS_ERROR_OUT_OF_RESOURCES beyond it (HIP turns that into
 //     hipErrorOutOfMemory).  So hipMalloc, hipMallocPitch/3D/Array, hipMallocAsync pools, hipMemCreate
 //     and the runtime's own device allocations are all charged, once.  Host pools are not counted.
-//     hipMemGetInfo reports the share as the device's total, so caching allocators size themselves
-//     to it.
+//     hipMallocManaged is the one HIP allocation that need not reach a device pool (with HMM the
+//     runtime backs it with system memory that migrates into HBM on first touch): it is charged at
+//     the HIP level, against the current device, in full, when the runtime did not already charge it
+//     through a pool (and released by hipFree).  hipMemGetInfo reports the share as the device's
+//     total, so caching allocators size themselves to it.
 //   * CUs: HSA_CU_MASK is set from the mounted config in the constructor (before main), and set back
 //     again in hsa_init, which every HIP program passes through whatever its first HIP call is, in
 //     case the program rewrote it meanwhile.  Independently of the environment, every queue the
@@ -27,9 +30,17 @@
 // The config is the read-only file the plugin mounts at /etc/gtk-vgpu.conf.  When that file exists it
 // is the only one read: $GTK_VGPU_CONFIG (which the pod spec could override) is honoured only where
 // no config is mounted (tests, hand-run jobs).  Format:
-//     hbm_limit <HIP ordinal> <bytes>
-//     cu_mask <HSA_CU_MASK value>
+//     hbm_limit_bdf <pci address> <bytes>     e.g. hbm_limit_bdf 0000:05:00.0 103079215104
+//     cu_mask_bdf <pci address> <cu list>     e.g. cu_mask_bdf 0000:05:00.0 0-127
+//     hbm_limit <ordinal> <bytes>             (hand-run jobs) ROCr enumeration order
+//     cu_mask <HSA_CU_MASK value>             (hand-run jobs) ROCr ordinals
 //     acct <path>                  (optional) pod-wide accounting file, shared read-write
+// The plugin writes the PCI-address forms: a device's ordinal depends on $ROCR_VISIBLE_DEVICES /
+// $HIP_VISIBLE_DEVICES, which the pod can set.  Addresses are resolved to ROCr ordinals
+// once the runtime has enumerated its agents (HSA_AMD_AGENT_INFO_DOMAIN / _BDFID), and HIP's device
+// numbers are mapped through hipDeviceGetPCIBusId, so a share holds whatever the process renumbers.
+// With address-keyed masks the environment mask is cleared instead of set (ROCr reads it before any
+// agent can be named by address); the per-queue mask below is then the enforcement.
 // No file: the library is inert (pure pass-through).  Without ``acct`` the limit holds per process.
 // With it, every process of the pod that maps the file draws from one budget: the file is a table of
 // per-process slots (bytes in use per device); a process owns its slot by holding an fcntl write lock
@@ -101,6 +112,9 @@ struct State {
   std::string cu_mask;                                                     // HSA_CU_MASK value
   std::vector<std::vector<uint32_t>> mask_bits;                            // per ordinal; empty = all CUs
   std::unordered_map<const hsa_queue_t*, int> queues;                      // queue -> GPU ordinal
+  std::unordered_map<void*, std::pair<int, size_t>> managed;               // hipMallocManaged charges
+  std::vector<std::pair<uint32_t, long long>> bdf_limit;                   // PCI address -> bytes
+  std::vector<std::pair<uint32_t, std::vector<uint32_t>>> bdf_mask;        // PCI address -> CU bits
   State() {
     for (int i = 0; i < kMaxDev; ++i) limit[i] = -1, used[i] = 0;
   }
@@ -148,6 +162,39 @@ Fn real(const char* name, const char* stem) {
 #define REAL_HIP(name, type) static const type real_fn = real<type>(#name, "libamdhip64");
 #define REAL_HSA(name) static const auto real_fn = real<decltype(&::name)>(#name, "libhsa-runtime64");
 
+// "<cu>[-<cu>][,...]" -> bit words
+std::vector<uint32_t> parse_cus(const char* c) {
+  std::vector<uint32_t> bits;
+  while (*c) {
+    char* e = nullptr;
+    long a = std::strtol(c, &e, 10);
+    if (e == c) break;
+    long b = a;
+    c = e;
+    if (*c == '-') {
+      b = std::strtol(c + 1, &e, 10);
+      c = e;
+    }
+    for (long cu = a; cu <= b && cu >= 0 && cu < 4096; ++cu) {
+      if ((long)bits.size() * 32 <= cu) bits.resize(cu / 32 + 1, 0u);
+      bits[cu / 32] |= 1u << (cu % 32);
+    }
+    if (*c == ',') ++c;
+  }
+  return bits;
+}
+
+// "dddd:bb:dd.f" (hex; the domain may be omitted) -> domain << 16 | bus << 8 | device << 3 | function
+bool parse_bdf(const char* t, uint32_t* key) {
+  unsigned d = 0, b = 0, v = 0, f = 0;
+  if (std::sscanf(t, "%x:%x:%x.%x", &d, &b, &v, &f) != 4) {
+    d = 0;
+    if (std::sscanf(t, "%x:%x.%x", &b, &v, &f) != 3) return false;
+  }
+  *key = (d & 0xffffu) << 16 | (b & 0xffu) << 8 | (v & 0x1fu) << 3 | (f & 7u);
+  return true;
+}
+
 // HSA_CU_MASK syntax: "<ordinal>:<cu>[-<cu>][,...]" parts separated by ';'
 std::vector<std::vector<uint32_t>> parse_mask(const std::string& v) {
   std::vector<std::vector<uint32_t>> out;
@@ -162,34 +209,33 @@ std::vector<std::vector<uint32_t>> parse_mask(const std::string& v) {
     int dev = std::atoi(part.c_str());
     if (dev < 0 || dev >= kMaxDev) continue;
     if ((int)out.size() <= dev) out.resize(dev + 1);
-    std::vector<uint32_t>& bits = out[dev];
-    const char* c = part.c_str() + colon + 1;
-    while (*c) {
-      char* e = nullptr;
-      long a = std::strtol(c, &e, 10);
-      if (e == c) break;
-      long b = a;
-      c = e;
-      if (*c == '-') {
-        b = std::strtol(c + 1, &e, 10);
-        c = e;
-      }
-      for (long cu = a; cu <= b && cu >= 0 && cu < 4096; ++cu) {
-        if ((long)bits.size() * 32 <= cu) bits.resize(cu / 32 + 1, 0u);
-        bits[cu / 32] |= 1u << (cu % 32);
-      }
-      if (*c == ',') ++c;
-    }
+    out[dev] = parse_cus(part.c_str() + colon + 1);
   }
   return out;
 }
 
-// GPU agents in ROCr's enumeration order (HSA_CU_MASK's and HIP's ordinals) and each one's global
-// memory pools.  Built once, on the first queue or allocation, from the real runtime.
+// GPU agents in ROCr's enumeration order (HSA_CU_MASK's ordinals) and each one's global memory pools
+// and PCI address.  Built once, on the first queue or allocation, from the real runtime; the
+// address-keyed limits and masks of the config are resolved to ordinals then.
 struct Agents {
   std::vector<uint64_t> gpus;                       // ordinal -> agent handle
+  std::vector<uint32_t> bdf;                        // ordinal -> PCI address key (0xffffffff: unknown)
   std::unordered_map<uint64_t, int> pool_ordinal;   // GPU global pool handle -> ordinal
 };
+
+void resolve_bdf_config(const Agents& a) {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  for (const auto& l : s.bdf_limit)
+    for (size_t o = 0; o < a.bdf.size() && o < (size_t)kMaxDev; ++o)
+      if (a.bdf[o] == l.first) s.limit[o] = l.second;
+  for (const auto& m : s.bdf_mask)
+    for (size_t o = 0; o < a.bdf.size() && o < (size_t)kMaxDev; ++o)
+      if (a.bdf[o] == m.first) {
+        if (s.mask_bits.size() <= o) s.mask_bits.resize(o + 1);
+        s.mask_bits[o] = m.second;
+      }
+}
 
 Agents& agents() {
   static Agents* a = new Agents();
@@ -205,6 +251,10 @@ Agents& agents() {
           hsa_device_type_t type{};
           if (info(ag, HSA_AGENT_INFO_DEVICE, &type) != HSA_STATUS_SUCCESS || type != HSA_DEVICE_TYPE_GPU) return HSA_STATUS_SUCCESS;
           a->gpus.push_back(ag.handle);
+          uint32_t id = 0, dom = 0;
+          const bool known = info(ag, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &id) == HSA_STATUS_SUCCESS &&
+                             info(ag, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom) == HSA_STATUS_SUCCESS;
+          a->bdf.push_back(known ? ((dom & 0xffffu) << 16 | (id & 0xffffu)) : 0xffffffffu);
           struct Ctx {
             Agents* a;
             int ordinal;
@@ -224,8 +274,31 @@ Agents& agents() {
           return HSA_STATUS_SUCCESS;
         },
         a);
+    resolve_bdf_config(*a);
   });
   return *a;
+}
+
+// ROCr ordinal of HIP device `hip` (HIP may renumber: $HIP_VISIBLE_DEVICES), by PCI address; the HIP
+// number itself when the address is unknown
+int hip_ordinal(int hip) {
+  typedef hipError_t (*F)(char*, int, int);
+  static const F bus_id = real<F>("hipDeviceGetPCIBusId", "libamdhip64");
+  const Agents& a = agents();
+  char bus[64] = {0};
+  uint32_t key = 0;
+  if (bus_id(bus, (int)sizeof bus, hip) == kSuccess && parse_bdf(bus, &key))
+    for (size_t o = 0; o < a.bdf.size(); ++o)
+      if (a.bdf[o] == key) return (int)o;
+  return hip;
+}
+
+int current_ordinal() {
+  typedef hipError_t (*G)(int*);
+  static const G get_device = real<G>("hipGetDevice", "libamdhip64");
+  int dev = 0;
+  if (get_device(&dev) != kSuccess) return -1;
+  return hip_ordinal(dev);
 }
 
 int pool_ordinal(hsa_amd_memory_pool_t pool) {
@@ -380,7 +453,11 @@ std::pair<int, size_t> untrack(void* p) {
 
 void set_cu_mask_env() {
   State& s = st();
-  if (s.active && !s.cu_mask.empty()) setenv("HSA_CU_MASK", s.cu_mask.c_str(), 1);
+  if (!s.active) return;
+  if (!s.bdf_mask.empty())
+    unsetenv("HSA_CU_MASK");  // an ordinal-keyed mask may name other devices; queues get the share's
+  else if (!s.cu_mask.empty())
+    setenv("HSA_CU_MASK", s.cu_mask.c_str(), 1);
 }
 
 const char* config_path() {
@@ -398,10 +475,15 @@ __attribute__((constructor)) void load_config() {
   State& s = st();
   char line[4096];
   while (std::fgets(line, sizeof line, f)) {
-    char key[64] = {0}, val[4000] = {0};
+    char key[64] = {0}, val[4000] = {0}, key_s[64] = {0};
     int dev = -1;
     long long bytes = -1;
-    if (std::sscanf(line, "hbm_limit %d %lld", &dev, &bytes) == 2) {
+    uint32_t addr = 0;
+    if (std::sscanf(line, "hbm_limit_bdf %63s %lld", key_s, &bytes) == 2) {
+      if (parse_bdf(key_s, &addr) && bytes >= 0) s.bdf_limit.emplace_back(addr, bytes);
+    } else if (std::sscanf(line, "cu_mask_bdf %63s %3999s", key_s, val) == 2) {
+      if (parse_bdf(key_s, &addr)) s.bdf_mask.emplace_back(addr, parse_cus(val));
+    } else if (std::sscanf(line, "hbm_limit %d %lld", &dev, &bytes) == 2) {
       if (dev >= 0 && dev < kMaxDev && bytes >= 0) s.limit[dev] = bytes;
     } else if (std::sscanf(line, "%63s %3999s", key, val) == 2 && std::strcmp(key, "cu_mask") == 0) {
       s.cu_mask = val;
@@ -422,6 +504,7 @@ __attribute__((constructor)) void load_config() {
                    c.ptrs.clear();
                    c.handles.clear();
                    c.queues.clear();
+                   c.managed.clear();
                    c.mine = -1;
                  });
   set_cu_mask_env();  // before ROCr initialises
@@ -466,8 +549,8 @@ __attribute__((visibility("default"))) hsa_status_t hsa_queue_create(
   REAL_HSA(hsa_queue_create);
   hsa_status_t e = real_fn(agent, size, type, callback, data, private_segment_size, group_segment_size, queue);
   State& s = st();
-  if (e != HSA_STATUS_SUCCESS || !queue || !*queue || !s.active || s.mask_bits.empty()) return e;
-  const int ord = agent_ordinal(agent);
+  if (e != HSA_STATUS_SUCCESS || !queue || !*queue || !s.active || (s.mask_bits.empty() && s.bdf_mask.empty())) return e;
+  const int ord = agent_ordinal(agent);  // resolves the address-keyed masks on first use
   std::vector<uint32_t> m = share_mask(ord, nullptr, 0);
   if (m.empty()) return e;
   {
@@ -599,16 +682,68 @@ __attribute__((visibility("default"))) hipError_t hipMemGetInfo(size_t* free_b, 
   hipError_t e = real_fn(free_b, total_b);
   State& s = st();
   if (e != kSuccess || !s.active) return e;
-  typedef hipError_t (*G)(int*);
-  static const G get_device = real<G>("hipGetDevice", "libamdhip64");
-  int dev = 0;
-  if (get_device(&dev) != kSuccess || dev < 0 || dev >= kMaxDev || s.limit[dev] < 0) return e;
+  const int dev = current_ordinal();
+  if (dev < 0 || dev >= kMaxDev || s.limit[dev] < 0) return e;
   std::lock_guard<std::mutex> g(s.mu);
   const long long left = s.limit[dev] - pod_used(dev);
   if (total_b && (long long)*total_b > s.limit[dev]) *total_b = (size_t)s.limit[dev];
   if (free_b && (long long)*free_b > left) *free_b = (size_t)(left > 0 ? left : 0);
   return e;
 }
+
+// Managed memory the runtime did not place in a device pool (HMM: system pages that migrate into HBM
+// when a kernel touches them) would bypass the pool hooks: charged here, in full, to the current device.
+__attribute__((visibility("default"))) hipError_t hipMallocManaged(void** ptr, size_t size, unsigned int flags) {
+  typedef hipError_t (*F)(void**, size_t, unsigned int);
+  REAL_HIP(hipMallocManaged, F);
+  State& s = st();
+  if (!s.active) return real_fn(ptr, size, flags);
+  const int dev = current_ordinal();
+  if (!reserve(dev, size)) {
+    if (ptr) *ptr = nullptr;
+    return 2;  // hipErrorOutOfMemory
+  }
+  hipError_t e = real_fn(ptr, size, flags);
+  if (dev < 0 || dev >= kMaxDev || s.limit[dev] < 0) return e;
+  bool charged = e == kSuccess && ptr && *ptr;
+  if (charged) {
+    std::lock_guard<std::mutex> g(s.mu);
+    if (s.ptrs.count(*ptr))
+      charged = false;  // the runtime took it from a device pool: already counted there
+    else
+      s.managed[*ptr] = {dev, size};
+  }
+  if (!charged) unreserve(dev, size);
+  return e;
+}
+
+__attribute__((visibility("default"))) hipError_t hipFree(void* ptr) {
+  typedef hipError_t (*F)(void*);
+  REAL_HIP(hipFree, F);
+  State& s = st();
+  std::pair<int, size_t> v{-1, 0};
+  if (s.active && ptr) {  // forget it before the address can be handed out again
+    std::lock_guard<std::mutex> g(s.mu);
+    auto it = s.managed.find(ptr);
+    if (it != s.managed.end()) {
+      v = it->second;
+      s.managed.erase(it);
+    }
+  }
+  hipError_t e = real_fn(ptr);
+  if (v.first >= 0) {
+    if (e == kSuccess) {
+      unreserve(v.first, v.second);
+    } else {
+      std::lock_guard<std::mutex> g(s.mu);
+      s.managed[ptr] = v;
+    }
+  }
+  return e;
+}
+
+// ROCr ordinal the HIP device `hip` maps to (tests: the address-keyed config under renumbering)
+__attribute__((visibility("default"))) int gtk_vgpu_hip_ordinal(int hip) { return hip_ordinal(hip); }
 
 // introspection for tests and the workload's report: bytes in use / limit on `dev` (-1: no limit)
 __attribute__((visibility("default"))) long long gtk_vgpu_used(int dev) {
@@ -625,7 +760,9 @@ __attribute__((visibility("default"))) long long gtk_vgpu_pod_used(int dev) {
 }
 
 __attribute__((visibility("default"))) long long gtk_vgpu_limit(int dev) {
-  return (dev >= 0 && dev < kMaxDev) ? st().limit[dev] : -1;
+  if (dev < 0 || dev >= kMaxDev) return -1;
+  std::lock_guard<std::mutex> g(st().mu);
+  return st().limit[dev];
 }
 
 // queues of this process the share's mask was applied to

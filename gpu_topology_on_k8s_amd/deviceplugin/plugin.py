@@ -47,7 +47,7 @@ from ..placement.core import select_with
 from ..topology.cpus import recommended_cpuset
 from ..topology.identity import ENV_BDFS, ENV_FRACTION, ENV_GROUP, ENV_SLICES
 from ..topology.model import Topology
-from ..topology.shares import cu_mask_env, physical_group, share_fractions, slices_per_gpu
+from ..topology.shares import cu_mask_env, format_cus, physical_group, share_cus, share_fractions, slices_per_gpu
 from . import proto as pb
 from .podresources import POD_RESOURCES_SOCKET, list_pod_resources
 from .metrics import PluginMetrics
@@ -799,20 +799,31 @@ class DevicePluginServer:
         return True
 
     def guard_config(self, ids: Sequence[int], mask: str, acct: bool = True) -> str:
-        """The guard's config for a container holding the time slices ``ids``: per partly held GPU (its
-        HIP ordinal in the container: position among the held physical GPUs) the HBM of the slices it
-        holds, the CU mask Allocate computed, and the accounting file every process of the pod shares
-        (one budget for the pod, not per process)."""
+        """The guard's config for a container holding the time slices ``ids``: per partly held GPU the
+        HBM of the slices it holds and their CUs, and the accounting file every process of the pod
+        shares (one budget for the pod, not per process).  GPUs are named by PCI address (an
+        ordinal moves when the pod sets ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES); only when discovery
+        found no address does the config fall back to the container ordinal (position among the held
+        physical GPUs) and the HSA_CU_MASK value Allocate computed."""
         frac = share_fractions(self.topology, ids)
+        cus = share_cus(self.topology, ids) if mask else {}
         lines = ["# gtk-vgpu: written by the device plugin at Allocate (deviceplugin/plugin.py)"]
+        partial = [p for p in sorted(frac) if frac[p] < 1.0]
+        held = {p: [self.topology.gpus[int(i)] for i in ids if self.topology.gpus[int(i)].physical == p] for p in partial}
+        by_address = all(held[p] and held[p][0].bdf for p in partial)
         for ordinal, p in enumerate(sorted(frac)):
-            if frac[p] >= 1.0:
+            if p not in held:
                 continue
-            held = [self.topology.gpus[int(i)] for i in ids if self.topology.gpus[int(i)].physical == p]
-            hbm = sum(int(g.vram_bytes) for g in held)
-            if hbm > 0:
+            hbm = sum(int(g.vram_bytes) for g in held[p])
+            if by_address:
+                bdf = held[p][0].bdf
+                if hbm > 0:
+                    lines.append(f"hbm_limit_bdf {bdf} {hbm}")
+                if p in cus:
+                    lines.append(f"cu_mask_bdf {bdf} {format_cus(cus[p])}")
+            elif hbm > 0:
                 lines.append(f"hbm_limit {ordinal} {hbm}")
-        if mask:
+        if mask and not by_address:
             lines.append(f"cu_mask {mask}")
         if acct:
             lines.append(f"acct {self.GUARD_ACCT_IN_CONTAINER}")

@@ -164,10 +164,17 @@ def cu_mask_env(topo: Topology, ids: Sequence[int]) -> str:
     if slices_per_gpu(topo) <= 1:
         return ""
     frac = share_fractions(topo, ids)
-    parts = []
-    for ordinal, p in enumerate(sorted(frac)):
-        if frac[p] >= 1.0:
-            continue
-        cus = sorted({c for i in ids if topo.gpus[int(i)].physical == p for c in slice_cus(topo, int(i))})
-        parts.append(f"{ordinal}:{_ranges(cus)}")
-    return ";".join(parts)
+    cus = share_cus(topo, ids)
+    return ";".join(f"{ordinal}:{_ranges(cus[p])}" for ordinal, p in enumerate(sorted(frac)) if p in cus)
+
+
+def share_cus(topo: Topology, ids: Sequence[int]) -> Dict[int, List[int]]:
+    """Compute units of each partly held physical GPU of the time slices ``ids`` (whole GPUs omitted)."""
+    frac = share_fractions(topo, ids)
+    return {p: sorted({c for i in ids if topo.gpus[int(i)].physical == p for c in slice_cus(topo, int(i))})
+            for p in sorted(frac) if frac[p] < 1.0}
+
+
+def format_cus(cus: Sequence[int]) -> str:
+    """CU list in HSA_CU_MASK syntax ("0-63,128-191")."""
+    return _ranges(list(cus))

@@ -155,6 +155,88 @@ def test_guard_enforces_the_mask_at_rocr_whatever_the_first_call(tmp_path, mode,
     assert out["init_mask"] == "0:0-255" and out["queues"] == ["0-255", "0-255", "0-95"]
 
 
+RENUMBER_CHILD = r"""
+import ctypes, json, os, sys
+rt = ctypes.CDLL(sys.argv[1], mode=ctypes.RTLD_LOCAL)
+g = ctypes.CDLL(None)
+GiB = 1 << 30
+def alloc(n, fn="hipMalloc"):
+    p = ctypes.c_void_p()
+    args = (ctypes.c_uint(1),) if fn == "hipMallocManaged" else ()
+    f = getattr(g, fn) if hasattr(g, fn) else getattr(rt, fn)  # global scope first, as the application links
+    return f(ctypes.byref(p), ctypes.c_size_t(n), *args), p
+n = ctypes.c_int()
+rt.hipGetDeviceCount(ctypes.byref(n))
+bus = ctypes.create_string_buffer(64)
+rt.hipDeviceGetPCIBusId(bus, 64, 0)
+e1, p1 = alloc(6 * GiB)
+e2, p2 = alloc(3 * GiB, "hipMallocManaged")   # managed memory (system pages here, as with HMM) is charged too
+e3, p3 = alloc(2 * GiB, "hipMallocManaged")
+g.gtk_vgpu_used.restype = ctypes.c_longlong
+used_full = g.gtk_vgpu_used(g.gtk_vgpu_hip_ordinal(0))
+free_, total = ctypes.c_size_t(), ctypes.c_size_t()
+g.hipMemGetInfo(ctypes.byref(free_), ctypes.byref(total))
+g.hipFree(p3)                                   # ... and given back by hipFree
+used_freed = g.gtk_vgpu_used(g.gtk_vgpu_hip_ordinal(0))
+s = ctypes.c_void_p()
+rt.hipStreamCreate(ctypes.byref(s))
+rt.fake_hip_init_mask.restype = ctypes.c_char_p
+rt.fake_hip_stream_mask.restype = ctypes.c_char_p
+out = {"count": n.value, "bus0": bus.value.decode(), "e": [e1, e2, e3], "used_full": used_full, "used_freed": used_freed,
+       "total": total.value, "free": free_.value, "queue": rt.fake_hip_stream_mask(s).decode(),
+       "init_mask": rt.fake_hip_init_mask().decode(), "rocr_ordinal": g.gtk_vgpu_hip_ordinal(0)}
+if n.value > 1:                                 # the other GPU is not the share's
+    os.environ["FAKE_HIP_DEVICE"] = "1"
+    out["other"] = alloc(40 * GiB)[0]
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("visible,rocr_ordinal", [({}, 1), ({"ROCR_VISIBLE_DEVICES": "1,0"}, 0),
+                                                  ({"HIP_VISIBLE_DEVICES": "1"}, 1), ({"ROCR_VISIBLE_DEVICES": "1"}, 0)])
+def test_address_keyed_share_holds_under_renumbering(tmp_path, visible, rocr_ordinal):
+    """ADVICE r4 (vgpu_guard.cpp ordinal keying): the plugin names the share's GPU by PCI address, so
+    a pod that reorders or hides devices with $ROCR_VISIBLE_DEVICES / $HIP_VISIBLE_DEVICES cannot move
+    its limit or mask onto another GPU.  The share is physical GPU 1 (0000:15:00.0); whichever HIP
+    number it ends up with, its allocations are capped, hipMemGetInfo reports the share, its queues
+    run on the share's CUs (an ordinal-keyed HSA_CU_MASK in the pod's environment is cleared), and the
+    other GPU, when visible, is not limited.  Managed allocations, which do not reach a device pool
+    here (system memory, as with HMM), are charged at the HIP level and released by hipFree."""
+    conf = tmp_path / "gtk-vgpu.conf"
+    conf.write_text(f"hbm_limit_bdf 0000:15:00.0 {8 * GiB}\ncu_mask_bdf 0000:15:00.0 64-127\n")
+    hip0_is_share = visible != {}
+    env = {k: v for k, v in os.environ.items() if k not in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES")}
+    env.update(GTK_VGPU_CONFIG=str(conf), HSA_CU_MASK="0:0-255", FAKE_HIP_DEVICE="0" if hip0_is_share else "1", **visible)
+    env["LD_PRELOAD"] = (env["LD_PRELOAD"] + ":" if env.get("LD_PRELOAD") else "") + str(binary("libgtk_vgpu.so"))
+    child = RENUMBER_CHILD if hip0_is_share else RENUMBER_CHILD.replace("(bus, 64, 0)", "(bus, 64, 1)").replace(
+        "hip_ordinal(0)", "hip_ordinal(1)").replace('os.environ["FAKE_HIP_DEVICE"] = "1"', 'os.environ["FAKE_HIP_DEVICE"] = "0"')
+    p = subprocess.run([sys.executable, "-c", child, _fake()], capture_output=True, text=True, timeout=60, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["bus0"] == "0000:15:00.0", out
+    assert out["e"] == [0, 2, 0] and out["used_full"] == 8 * GiB and out["used_freed"] == 6 * GiB, out
+    assert out["total"] == 8 * GiB and out["free"] == 0, out
+    assert out["queue"] == "64-127" and out["init_mask"] == "", out
+    assert out["rocr_ordinal"] == rocr_ordinal, out
+    if out["count"] > 1:
+        assert out["other"] == 0, out
+
+
+def test_ordinal_keyed_share_moves_with_renumbering(tmp_path):
+    """Why the plugin writes addresses: the same share keyed by ordinal 0 lands on whichever GPU the
+    pod's own ROCR_VISIBLE_DEVICES puts first -- here the other one, and the share's GPU is uncapped."""
+    conf = tmp_path / "gtk-vgpu.conf"
+    conf.write_text(f"hbm_limit 0 {8 * GiB}\n")
+    env = {k: v for k, v in os.environ.items() if k not in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES")}
+    env.update(GTK_VGPU_CONFIG=str(conf), FAKE_HIP_DEVICE="1", ROCR_VISIBLE_DEVICES="1,0")
+    env["LD_PRELOAD"] = (env["LD_PRELOAD"] + ":" if env.get("LD_PRELOAD") else "") + str(binary("libgtk_vgpu.so"))
+    child = RENUMBER_CHILD.replace("(bus, 64, 0)", "(bus, 64, 1)")
+    p = subprocess.run([sys.executable, "-c", child, _fake()], capture_output=True, text=True, timeout=60, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["bus0"] == "0000:05:00.0" and out["e"] == [0, 0, 0], out  # physical GPU 0, the plugin's "ordinal 0": uncapped
+
+
 def test_mounted_config_wins_over_the_pods_environment(tmp_path):
     """ADVICE r3 (vgpu_guard.cpp:322): a pod spec that points GTK_VGPU_CONFIG elsewhere does not make
     the guard inert when the plugin's config is mounted: the fixed mount path is read first.  (The
@@ -202,7 +284,11 @@ def test_allocate_mounts_the_guard_for_a_partial_gpu_only():
         assert ro and os.path.getsize(lib) == os.path.getsize(str(binary("libgtk_vgpu.so")))
         conf, ro = mounts["/etc/gtk-vgpu.conf"]
         text = open(conf).read()
-        assert ro and f"hbm_limit 0 {2 * (288_000_000_000 // 4)}" in text and f"cu_mask {envs['HSA_CU_MASK']}" in text
+        # keyed by PCI address, the CUs the same as the env's mask for that GPU
+        bdf = envs["GTK_GPU_BDFS"].split(",")[0]
+        assert ro and f"hbm_limit_bdf {bdf} {2 * (288_000_000_000 // 4)}" in text, text
+        ordinal, cus = envs["HSA_CU_MASK"].split(":")
+        assert ordinal == "0" and f"cu_mask_bdf {bdf} {cus}" in text and "hbm_limit 0" not in text, text
         acct, ro = mounts["/var/run/gtk-vgpu.acct"]  # the pod's shared budget, writable by any container user
         assert not ro and "acct /var/run/gtk-vgpu.acct" in text and os.stat(acct).st_mode & 0o666 == 0o666
         c.submit("whole", 4, slices=True)  # a whole GPU's worth of slices: no share to guard
@@ -210,6 +296,39 @@ def test_allocate_mounts_the_guard_for_a_partial_gpu_only():
         resp = c.nodes["s"].kubelet.responses["default/whole"].container_responses[0]
         assert r.node == "s" and not resp.mounts and "LD_PRELOAD" not in dict(resp.envs)
         assert "gtk_plugin_guarded_containers_total 1.0" in c.nodes["s"].plugin.metrics.exposition().decode()
+
+
+def test_plugin_config_caps_the_share_whatever_the_pod_renumbers(tmp_path):
+    """The plugin's own config for half of physical GPU 1 (slices 4, 5), read by the guard in a process
+    whose ROCR_VISIBLE_DEVICES puts that GPU first: the share's GPU is capped and masked; without an
+    address (discovery found none) the config falls back to ordinals."""
+    import dataclasses
+
+    from gpu_topology_on_k8s_amd.deviceplugin import DevicePluginServer, PluginConfig
+    from gpu_topology_on_k8s_amd.topology import fixtures as fx
+    from gpu_topology_on_k8s_amd.topology.shares import time_slice
+
+    v = time_slice(fx.f7_mi355x(n=2), 4)
+    plug = DevicePluginServer(v, PluginConfig(device_specs="stub", dev_root=str(tmp_path), share_guard="env",
+                                              guard_dir=str(tmp_path / "g")))
+    from gpu_topology_on_k8s_amd.topology.shares import cu_mask_env
+
+    text = plug.guard_config([4, 5], cu_mask_env(v, [4, 5]), acct=False)
+    assert "hbm_limit_bdf 0000:15:00.0 " in text and "cu_mask_bdf 0000:15:00.0 0-127" in text, text
+    conf = tmp_path / "gtk-vgpu.conf"
+    conf.write_text(text.replace(f" {2 * (288_000_000_000 // 4)}", f" {8 * GiB}"))
+    env = {k: val for k, val in os.environ.items() if k not in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES")}
+    env.update(GTK_VGPU_CONFIG=str(conf), HSA_CU_MASK="0:0-255", FAKE_HIP_DEVICE="0", ROCR_VISIBLE_DEVICES="1,0")
+    env["LD_PRELOAD"] = (env["LD_PRELOAD"] + ":" if env.get("LD_PRELOAD") else "") + str(binary("libgtk_vgpu.so"))
+    p = subprocess.run([sys.executable, "-c", RENUMBER_CHILD, _fake()], capture_output=True, text=True, timeout=60, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["e"] == [0, 2, 0] and out["total"] == 8 * GiB and out["queue"] == "0-127" and out["other"] == 0, out
+    bare = dataclasses.replace(v, gpus=[dataclasses.replace(g, bdf="") for g in v.gpus])
+    plug2 = DevicePluginServer(bare, PluginConfig(device_specs="stub", dev_root=str(tmp_path), share_guard="env",
+                                                  guard_dir=str(tmp_path / "g2")))
+    text = plug2.guard_config([4, 5], cu_mask_env(bare, [4, 5]), acct=False)
+    assert "hbm_limit 0 " in text and "cu_mask 0:0-127" in text and "_bdf" not in text, text
 
 
 def test_preload_mode_mounts_ld_so_preload(tmp_path):
