@@ -151,12 +151,15 @@ def check_pod(env: Dict[str, str], visible_bdfs: Optional[List[str]] = None, all
     fr = [float(x) for x in env.get("GTK_GPU_FRACTION", "").split(",") if x.strip()]
     if fr and min(fr) < 1.0:
         problems = []
-        if not env.get("HSA_CU_MASK"):
+        guarded = env.get("GTK_VGPU_ACTIVE") == "1"
+        # an address-keyed guard config clears HSA_CU_MASK and masks every queue itself (vgpu_guard.cpp)
+        mask = env.get("HSA_CU_MASK") or ("per queue, by the guard" if guarded else "")
+        if not mask:
             problems.append("no HSA_CU_MASK")
-        if env.get("GTK_VGPU_ACTIVE") != "1":
+        if not guarded:
             problems.append("the vGPU guard is not loaded (HBM share unenforced)")
         out.append(_c("pod-share", "warn" if problems else "ok",
-                      "; ".join(problems) if problems else f"share {fr}, CU mask {env.get('HSA_CU_MASK')}, guard active"))
+                      "; ".join(problems) if problems else f"share {fr}, CU mask {mask}, guard active"))
     return out
 
 

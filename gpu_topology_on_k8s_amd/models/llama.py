@@ -364,7 +364,8 @@ class _FlatLinear(torch.autograd.Function):
         if nt:
             ctx.ops = _NTOperands(x, w, _wt_fn(flat, name), x_t=x_t)
         else:
-            ctx.save_for_backward(x, w)
+            ctx.save_for_backward(x)
+            ctx.w = w  # a flat-buffer view: not version-checked (see _FlatRMSNorm)
         return F.linear(x, w)
 
     @staticmethod
@@ -376,7 +377,8 @@ class _FlatLinear(torch.autograd.Function):
             dx = F.linear(dy, w_t) if ctx.needs_input_grad[0] else None  # dy (W^T)^T
             ctx.flat.write_grad(ctx.name, dy, None, nt=True, x_t=x_t, dy_t=dy_t)
         else:
-            x, w = ctx.saved_tensors
+            (x,), w = ctx.saved_tensors, ctx.w
+            ctx.w = None
             dx = dy.mm(w) if ctx.needs_input_grad[0] else None
             ctx.flat.write_grad(ctx.name, dy, x)
         return dx, None, None, None, None, None
@@ -397,7 +399,8 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
             ctx.ops = _NTOperands(x, w, _wt_fn(flat, name))
             ctx.save_for_backward(gu)
         else:
-            ctx.save_for_backward(gu, x, w)
+            ctx.save_for_backward(gu, x)
+            ctx.w = w
         a_t = None
         if not gu.is_cuda:
             a = fused.swiglu_ref(gu)
@@ -418,7 +421,8 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
             dx = F.linear(dgu, w_t) if ctx.needs_input_grad[0] else None
             ctx.flat.write_grad(ctx.name, dgu, None, nt=True, dy_t=dgu_t, x_t=x_t)
         else:
-            _, x, w = ctx.saved_tensors
+            (_, x), w = ctx.saved_tensors, ctx.w
+            ctx.w = None
             dgu = fused.hip().swiglu_bwd(da.contiguous(), gu) if gu.is_cuda else fused.swiglu_bwd_ref(da, gu)
             dx = dgu.mm(w) if ctx.needs_input_grad[0] else None
             ctx.flat.write_grad(ctx.name, dgu, x)
@@ -428,19 +432,26 @@ class _FlatLinearSwiGLU(torch.autograd.Function):
 class _FlatRMSNorm(torch.autograd.Function):
     """``rmsnorm(x) * w`` whose weight gradient the backward kernel writes straight into the weight's
     slot of the flat gradient buffer (``rmsnorm_bwd_into``): no separate dW for autograd to add in,
-    and no zero-fill of that slot in ``zero_grad`` (the weight is a direct parameter)."""
+    and no zero-fill of that slot in ``zero_grad`` (the weight is a direct parameter).
+
+    The weight is kept on ``ctx``, not saved for backward: every parameter is a view of the flat
+    buffer and views share one version counter, so ZeRO-1's all-gather of ANOTHER bucket landing
+    during the forward (overlapped, parallel/dp.py ``gather_params``) would fail autograd's check
+    although this weight's own bucket was gathered before its first use (``wait_param``) and nothing
+    writes it again before the backward."""
 
     @staticmethod
     def forward(ctx, x, w, flat, name, eps):
         x = x.contiguous()
         y, rstd = fused.hip().rmsnorm_fwd(x, w, float(eps))
-        ctx.save_for_backward(x, w, rstd)
-        ctx.flat, ctx.name = flat, name
+        ctx.save_for_backward(x, rstd)
+        ctx.w, ctx.flat, ctx.name = w, flat, name
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w, rstd = ctx.saved_tensors
+        (x, rstd), w = ctx.saved_tensors, ctx.w
+        ctx.w = None
         out, fresh = ctx.flat.grad_target(ctx.name)
         dx = fused.hip().rmsnorm_bwd_into(dy.contiguous(), x, w, rstd, out)
         ctx.flat.mark_written(ctx.name, None if fresh else out)
@@ -454,13 +465,14 @@ class _FlatAddRMSNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, r, w, flat, name, eps):
         h, y, rstd = fused.hip().add_rmsnorm_fwd(x.contiguous(), r.contiguous(), w, float(eps))
-        ctx.save_for_backward(h, w, rstd)
-        ctx.flat, ctx.name = flat, name
+        ctx.save_for_backward(h, rstd)
+        ctx.w, ctx.flat, ctx.name = w, flat, name  # not version-checked: see _FlatRMSNorm
         return h, y
 
     @staticmethod
     def backward(ctx, dh, dy):
-        h, w, rstd = ctx.saved_tensors
+        (h, rstd), w = ctx.saved_tensors, ctx.w
+        ctx.w = None
         if dy is None:
             dy = torch.zeros_like(h)
         out, fresh = ctx.flat.grad_target(ctx.name)

@@ -42,6 +42,11 @@ def test_pod_checks_from_an_allocate_env():
     assert c["pod-share"]["status"] == "warn" and "guard" in c["pod-share"]["detail"]
     c = _by_name(check_pod(dict(env, GTK_VGPU_ACTIVE="1"), visible_bdfs=["0000:75:00.0"], allowed=range(8)))
     assert c["pod-share"]["status"] == "ok"
+    bare = {k: v for k, v in env.items() if k != "HSA_CU_MASK"}  # the guard cleared it: it masks the queues
+    c = _by_name(check_pod(dict(bare, GTK_VGPU_ACTIVE="1"), visible_bdfs=["0000:75:00.0"], allowed=range(8)))
+    assert c["pod-share"]["status"] == "ok" and "by the guard" in c["pod-share"]["detail"]
+    c = _by_name(check_pod(bare, visible_bdfs=["0000:75:00.0"], allowed=range(8)))
+    assert c["pod-share"]["status"] == "warn" and "no HSA_CU_MASK" in c["pod-share"]["detail"]
     c = _by_name(check_pod(env, visible_bdfs=["0000:05:00.0"], allowed=range(100, 108)))
     assert c["pod-group"]["status"] == "fail" and c["pod-cpuset"]["status"] == "warn"
 

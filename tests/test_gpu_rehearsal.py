@@ -26,7 +26,8 @@ def _run(args, port=None, timeout=600):
         cmd += ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1", f"--master-port={port}"]
     cmd += ["-m", "gpu_topology_on_k8s_amd.models.train", *args]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=REPO, env=e)
-    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    tb = p.stderr.find("Traceback")  # the first rank's traceback, not the launcher's summary
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[tb:tb + 4000] if tb >= 0 else p.stderr[-4000:])
     return json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
 
 

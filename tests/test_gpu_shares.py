@@ -311,6 +311,68 @@ def test_vgpu_guard_holds_whatever_the_first_hip_call(tmp_path, first):
     assert 0.15 * full < g["tflops"] < 0.40 * full, (g["tflops"], full)
 
 
+_MANAGED_CHILD = r"""
+import ctypes, json, os
+g = ctypes.CDLL(None)                              # global scope: the guard's entry points come first
+hip = ctypes.CDLL("libamdhip64.so")
+g.gtk_vgpu_used.restype = ctypes.c_longlong
+def managed(n):
+    p = ctypes.c_void_p()
+    e = g.hipMallocManaged(ctypes.byref(p), ctypes.c_size_t(n), ctypes.c_uint(1))
+    hip.hipGetLastError()
+    return e, p
+free_, total = ctypes.c_size_t(), ctypes.c_size_t()
+g.hipMemGetInfo(ctypes.byref(free_), ctypes.byref(total))
+base = g.gtk_vgpu_used(0)
+e_big, _ = managed(20 << 30)                      # past the 16 GiB share
+e_ok, p = managed(4 << 30)
+with_4 = g.gtk_vgpu_used(0)
+e_pf = hip.hipMemPrefetchAsync(p, ctypes.c_size_t(4 << 30), ctypes.c_int(0), None)   # into HBM: still one charge
+hip.hipDeviceSynchronize()
+hip.hipGetLastError()
+after_pf = g.gtk_vgpu_used(0)
+e_free = g.hipFree(p)
+freed = g.gtk_vgpu_used(0)
+from gpu_topology_on_k8s_amd.ops.probe import warmup
+r = warmup(0, 30.0)
+print(json.dumps({"total": total.value, "e": [e_big, e_ok, e_free], "prefetch": e_pf, "base": base, "with_4": with_4,
+                  "after_prefetch": after_pf, "freed": freed, "env_mask": os.environ.get("HSA_CU_MASK"),
+                  "masked_queues": g.gtk_vgpu_masked_queues(), "tflops": r["tflops"]}))
+"""
+
+
+def test_vgpu_guard_by_pci_address_charges_managed_memory(tmp_path):
+    """ADVICE r4 on the real runtime: the plugin's address-keyed config (the GPU named by its PCI
+    address, not an ordinal) caps the share and masks the queues (the pod's HSA_CU_MASK is cleared; the
+    MFMA loop still runs on 64 of 256 CUs); hipMallocManaged past the 16 GiB share is refused, one
+    inside it is charged once (a prefetch into HBM does not charge it again) and hipFree gives it back."""
+    from gpu_topology_on_k8s_amd._native import binary
+
+    base_env = {k: v for k, v in os.environ.items() if k not in _STRIP}
+    base_env.pop("HSA_CU_MASK", None)
+    q = subprocess.run([sys.executable, "-c", "import json; from gpu_topology_on_k8s_amd.topology.identity import hip_device_bdfs;"
+                        "from gpu_topology_on_k8s_amd.ops.probe import warmup;"
+                        "print(json.dumps({'bdf': hip_device_bdfs()[0], 'tflops': warmup(0, 30.0)['tflops']}))"],
+                       capture_output=True, text=True, timeout=240, cwd=REPO, env=base_env)
+    assert q.returncode == 0, q.stderr[-3000:]
+    ref = json.loads(q.stdout.strip().splitlines()[-1])
+    conf = tmp_path / "gtk-vgpu.conf"
+    conf.write_text(f"hbm_limit_bdf {ref['bdf']} {16 << 30}\ncu_mask_bdf {ref['bdf']} 0-63\n")
+    env = dict(base_env, GTK_VGPU_CONFIG=str(conf), HSA_CU_MASK="0:0-255")
+    env["LD_PRELOAD"] = (env["LD_PRELOAD"] + ":" if env.get("LD_PRELOAD") else "") + str(binary("libgtk_vgpu.so"))
+    p = subprocess.run([sys.executable, "-c", _MANAGED_CHILD], capture_output=True, text=True, timeout=240, cwd=REPO, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    g = json.loads(p.stdout.strip().splitlines()[-1])
+    print(json.dumps({"bdf": ref["bdf"], "guarded": g, "full_tflops": ref["tflops"]}))
+    assert g["total"] == 16 << 30 and g["env_mask"] is None and g["masked_queues"] > 0, g
+    assert g["e"] == [2, 0, 0], g  # hipErrorOutOfMemory past the share
+    # the prefetch does not charge the 4 GiB again; the runtime's own first-use buffers for it (4 MiB
+    # measured on the box) are device-pool allocations, charged like any other and kept after the free
+    rt_own = g["after_prefetch"] - g["with_4"]
+    assert g["with_4"] - g["base"] == 4 << 30 and 0 <= rt_own < 64 << 20 and g["freed"] - g["base"] == rt_own, g
+    assert 0.15 * ref["tflops"] < g["tflops"] < 0.40 * ref["tflops"], (g["tflops"], ref["tflops"])
+
+
 def test_doctor_inside_a_guarded_half_gpu_pod(tmp_path):
     """A whole pod start on the real GPU: the device plugin (real discovery, 2 time slices, guard on)
     allocates slice 0; a process gets exactly what the container would (the Allocate envs, the guard

@@ -109,6 +109,13 @@ print(json.dumps({"tflops": round(float(w["tflops"]), 1), "hbm_copy_gbps": round
     step step_ab 900 python -u bench/attn_step_ab.py --so ${AB_SO:-scratch/r04/_fused.cpython-310-x86_64-linux-gnu.so} --rounds 4 --steps 3
     step prof_llama 600 rocprofv3 --kernel-trace --stats -d "$out/prof_llama" -o run -- python3 -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 3 --warmup 1
     ;;
+  r05)
+    # round 5 checks: the share guard by PCI address (+ managed memory), the k >= 2 DP reduction checks
+    # rehearsed on the one GPU, and the loss lineage with this tree's and the round-4 attention backward
+    step pytest_r05 900 python -u -m pytest tests/test_gpu_shares.py tests/test_gpu_rehearsal.py tests/test_gpu_multi.py -k "guard or doctor or rehearsal or dp" -x -v --timeout 300 --timeout-method thread
+    step lineage_v7 400 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
+    step lineage_r04attn 400 python -u bench/with_attn_bwd.py --so ${AB_SO:-scratch/r04/_fused.cpython-310-x86_64-linux-gnu.so} -- --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
+    ;;
   shadow)
     # what 8-GPU DP communication costs the Llama-3-8B step: comm-shadow CTA sweep
     step shadow_sweep 1100 python -u bench/comm_shadow_sweep.py --ctas ${SHADOW_CTAS:-0,8,16,32,64} --busbw ${SHADOW_BUSBW:-350} --out "$out/shadow.jsonl" ${SHADOW_ZERO1:+--zero1}
