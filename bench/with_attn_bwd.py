@@ -12,7 +12,8 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from bench.attn_step_ab import Switch, load_other  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))  # bench/ (the repo root's bench.py shadows the dir)
+from attn_step_ab import Switch, load_other  # noqa: E402
 from gpu_topology_on_k8s_amd.models import train  # noqa: E402
 from gpu_topology_on_k8s_amd.ops import fused  # noqa: E402
 

@@ -21,7 +21,7 @@ step() {  # step <name> <seconds> <command...>
 
 case "$mode" in
   suite)
-    step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+    step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread
     step smoke 300 python -u -c 'import __graft_entry__ as g; g.smoke()'
     step bench_k1 600 python -u bench.py --gpus 1 --steps 20 --warmup 5
     ;;
@@ -112,7 +112,7 @@ print(json.dumps({"tflops": round(float(w["tflops"]), 1), "hbm_copy_gbps": round
   r05)
     # round 5 checks: the share guard by PCI address (+ managed memory), the k >= 2 DP reduction checks
     # rehearsed on the one GPU, and the loss lineage with this tree's and the round-4 attention backward
-    step pytest_r05 900 python -u -m pytest tests/test_gpu_shares.py tests/test_gpu_rehearsal.py tests/test_gpu_multi.py -k "guard or doctor or rehearsal or dp" -x -v --timeout 300 --timeout-method thread
+    step pytest_r05 900 python -u -m pytest tests/test_gpu_shares.py tests/test_gpu_rehearsal.py tests/test_gpu_multi.py -k "guard or doctor or rehearsal or dp" -x -v -rP --timeout 300 --timeout-method thread
     step lineage_v7 400 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
     step lineage_r04attn 400 python -u bench/with_attn_bwd.py --so ${AB_SO:-scratch/r04/_fused.cpython-310-x86_64-linux-gnu.so} -- --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
     ;;
