@@ -14,15 +14,17 @@
 //   * K and V tiles share one XOR-swizzled LDS image ((b) of guide T10): 16-B chunk ch of row r at
 //     256*r + 16*(ch ^ (((r&3)<<2) | ((r>>2)&3))) — conflict-free for both the ds_read_b128 row reads
 //     of K and the transposed reads of V.
-//   * register-staged K/V prefetch: the next tile's global loads are issued before this tile's MFMAs
-//     and written to LDS after the barrier (guide T14).  Query blocks are launched heaviest-first.
+//   * K/V tiles double-buffered in LDS, the next one staged by LDS-DMA (buffer_load ... lds) under
+//     the current tile's softmax and PV, one barrier per tile; query blocks launched heaviest-first,
+//     heads XCD-grouped (attn_fwd2_kernel).
 //   * output O is written token-major [B, S, H, D] (what the o-projection GEMM consumes) and the
-//     row log-sum-exp in log2 units for the backward.
-// Backward (attn_bwd): delta = rowsum(dO*O), then two kernels with no cross-workgroup sums:
-//   * dK/dV (v4): one workgroup = 128 keys of one (batch, kv-head), sweeping every q-head of the GQA
-//     group x 32-query slices; key on the lane for S = Q.K^T and dP = dO.V^T, whose P / dS
-//     accumulators feed dV^T += dO^T.P and dK^T += Q^T.dS as B operands (dO^T, Q^T by transposed LDS
-//     reads); software-pipelined slices.  v3 (attn_bwd_v3) is kept as the bit-identity oracle.
+//     row log-sum-exp in log2 units for the backward; optionally O^T from the epilogue.
+// Backward (attn_bwd): a pre-kernel (delta = rowsum(dO*O), -lse/c, -delta), then two kernels with no
+// cross-workgroup sums:
+//   * dK/dV: one workgroup = 128 keys of one (batch, kv-head), sweeping every q-head of the GQA group x
+//     32-query slices; key on the lane for S = Q.K^T and dP = dO.V^T, whose P / dS accumulators feed
+//     dV^T += dO^T.P and dK^T += Q^T.dS as B operands (dO^T, Q^T by transposed LDS reads); a 3-slot
+//     LDS-DMA slice ring, the dV/dK products of slice i under the softmax of slice i+1.
 //   * dQ: forward-shaped (query on the lane), dQ^T += K^T.dS^T accumulated in registers.
 // Earlier generations (forward v1 with one LDS buffer, backward v1 with fp32 dQ atomics, backward v2
 // with synchronous slice staging) were measured, retired, and live in git history before round 2.

@@ -26,9 +26,12 @@ def main():
     v = torch.randn(B, Hkv, S, D, device="cuda", dtype=torch.bfloat16)
     do = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
     hip = fused.hip()
+    variants = [getattr(hip, n) for n in sorted(dir(hip)) if n.startswith("attn_bwd_")]  # A/B builds only
     for _ in range(3):
         o, lse = hip.attn_fwd(q, k, v, D ** -0.5)
         hip.attn_bwd(do, q, k, v, o, lse, D ** -0.5)
+        for fn in variants:
+            fn(do, q, k, v, o, lse, D ** -0.5)
     torch.cuda.synchronize()
     print("pmc_attn done", flush=True)
 
