@@ -436,6 +436,9 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         best = min(cta_table, key=lambda r: r["ms_per_pass"])["ctas"]
         ar.remove()
         ar = make_ar(groups[best])
+        for c, grp in groups.items():  # the losers' communicators (RCCL: channel buffers per peer) go now
+            if c != best:
+                dist.destroy_process_group(grp)
         if zero1:
             model.param_ready = ar.wait_param
         comm_ctas = best
