@@ -78,6 +78,27 @@ def main():
         ref = variants["default"]()
         res["ab_rel_vs_default"] = {n: [float(((x.float() - y.float()).norm() / y.float().norm()).item()) for x, y in zip(fn(), ref)]
                                     for n, fn in variants.items()}
+        # forward variants (attn_fwdv_*), interleaved against attn_fwd the same way
+        fvars = {"fwd": lambda: hip.attn_fwd(q, k, v, Dh ** -0.5)}
+        for n in sorted(dir(hip)):
+            if n.startswith("attn_fwdv_"):
+                fvars[n] = (lambda fn: lambda: fn(q, k, v, Dh ** -0.5))(getattr(hip, n))
+        if len(fvars) > 1:
+            ft = {n: [] for n in fvars}
+            for fn in fvars.values():
+                fn()
+            for _ in range(a.ab):
+                for n, fn in fvars.items():
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    fn()
+                    e1.record()
+                    ft[n].append((e0, e1))
+            torch.cuda.synchronize()
+            res["ab_fwd_median_ms"] = {n: sorted(x.elapsed_time(y) for x, y in ts)[len(ts) // 2] for n, ts in ft.items()}
+            fref = fvars["fwd"]()
+            res["ab_fwd_rel"] = {n: [float(((x.float() - y.float()).norm() / y.float().norm()).item()) for x, y in zip(fn(), fref)]
+                                 for n, fn in fvars.items()}
     try:
         t = timeit(lambda: F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True), a.iters)
         res["sdpa_fwd_ms"] = t * 1e3

@@ -32,6 +32,9 @@ def main():
         hip.attn_bwd(do, q, k, v, o, lse, D ** -0.5)
         for fn in variants:
             fn(do, q, k, v, o, lse, D ** -0.5)
+        for n in sorted(dir(hip)):
+            if n.startswith("attn_fwdv_"):
+                getattr(hip, n)(q, k, v, D ** -0.5)
     torch.cuda.synchronize()
     print("pmc_attn done", flush=True)
 
