@@ -15,6 +15,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <unordered_set>
 
 extern "C" {
 // the stand-in ROCr's test hooks
@@ -72,19 +74,14 @@ static hipError_t status(hsa_status_t s) {
 }
 
 // managed blocks handed out (hipFree must tell them from pool blocks without touching memory)
-static void* g_managed[4096];
-static int g_nmanaged = 0;
-static bool g_managed_contains(void* p) {
-  for (int i = 0; i < g_nmanaged; ++i)
-    if (g_managed[i] == p) return true;
-  return false;
+static std::mutex g_managed_mu;
+static std::unordered_set<void*>& g_managed() {
+  static auto* m = new std::unordered_set<void*>();  // never destroyed: frees may come from exit-time code
+  return *m;
 }
-static void g_managed_erase(void* p) {
-  for (int i = 0; i < g_nmanaged; ++i)
-    if (g_managed[i] == p) {
-      g_managed[i] = g_managed[--g_nmanaged];
-      return;
-    }
+static bool g_managed_take(void* p) {  // forget p if it is a managed block; -> whether it was
+  std::lock_guard<std::mutex> g(g_managed_mu);
+  return g_managed().erase(p) != 0;
 }
 
 static hipError_t dev_alloc(void** p, size_t n) {
@@ -146,7 +143,8 @@ __attribute__((visibility("default"))) hipError_t hipMallocManaged(void** p, siz
   if (!b) return kOom;
   b[0] = kManagedTag;
   *p = b + 4;
-  if (g_nmanaged < 4096) g_managed[g_nmanaged++] = *p;
+  std::lock_guard<std::mutex> g(g_managed_mu);
+  g_managed().insert(*p);
   return kOk;
 }
 __attribute__((visibility("default"))) hipError_t hipMallocAsync(void** p, size_t n, void*) { return dev_alloc(p, n); }
@@ -172,8 +170,7 @@ __attribute__((visibility("default"))) hipError_t hipHostMalloc(void** p, size_t
 __attribute__((visibility("default"))) hipError_t hipFree(void* p) {
   init();
   if (!p) return kOk;
-  if (g_managed_contains(p)) {
-    g_managed_erase(p);
+  if (g_managed_take(p)) {
     std::free(static_cast<unsigned*>(p) - 4);
     return kOk;
   }

@@ -1,10 +1,11 @@
 // Host-only stress test of the vGPU guard (csrc/vgpu/vgpu_guard.cpp) under ThreadSanitizer and
 // AddressSanitizer/UBSan: the guard's sources are linked into this binary, the
 // stand-in HIP runtime (fake_hip.cpp) is its "libamdhip64", and many threads allocate and free
-// concurrently against one budget.  The test process sets GTK_VGPU_CONFIG before start (the guard's
-// constructor reads it before main).  Checks: no allocation ever succeeds past the limit, every byte
-// is returned, hipMemGetInfo stays consistent, and (with an ``acct`` file) forked children share the
-// parent's budget.
+// concurrently against one budget (device-pool allocations and HIP-level managed ones).  The test
+// process sets GTK_VGPU_CONFIG before start (the guard's constructor reads it before main); the config
+// may name the device by ordinal or by PCI address (resolved when the runtime first enumerates).
+// Checks: no allocation ever succeeds past the limit, every byte is returned, hipMemGetInfo stays
+// consistent, and (with an ``acct`` file) forked children share the parent's budget.
 //
 //     GTK_VGPU_CONFIG=cfg ./vgpu_selftest_tsan [threads] [iters]
 #include <sys/wait.h>
@@ -21,6 +22,7 @@ extern "C" {
 int hipMalloc(void** p, size_t n);
 int hipFree(void* p);
 int hipMallocAsync(void** p, size_t n, void* stream);
+int hipMallocManaged(void** p, size_t n, unsigned int flags);
 int hipFreeAsync(void* p, void* stream);
 int hipMemGetInfo(size_t* f, size_t* t);
 long long gtk_vgpu_used(int dev);
@@ -36,6 +38,8 @@ static int fail(const char* what) {
 int main(int argc, char** argv) {
   const int threads = argc > 1 ? std::atoi(argv[1]) : 16;
   const int iters = argc > 2 ? std::atoi(argv[2]) : 2000;
+  size_t f0 = 0, t0 = 0;
+  hipMemGetInfo(&f0, &t0);  // first runtime call: an address-keyed limit is resolved here
   const long long limit = gtk_vgpu_limit(0);
   if (limit <= 0) return fail("no hbm_limit for ordinal 0 in GTK_VGPU_CONFIG");
   std::atomic<long long> live{0}, peak{0}, ooms{0}, oks{0};
@@ -47,23 +51,29 @@ int main(int argc, char** argv) {
       started++;
       while (started.load() < threads) std::this_thread::yield();  // all threads contend from the start
       std::mt19937_64 rng(1234 + t);
-      std::vector<std::pair<void*, size_t>> held;
+      struct Held {
+        void* p;
+        size_t n;
+        bool managed;
+      };
+      std::vector<Held> held;
       for (int i = 0; i < iters; ++i) {
         if (!held.empty() && (rng() % 3 == 0 || held.size() > 16)) {
-          auto [p, n] = held.back();
+          const Held h = held.back();
           held.pop_back();
-          live -= (long long)n;
-          if ((rng() & 1) ? hipFree(p) : hipFreeAsync(p, nullptr)) bad_free++;
+          live -= (long long)h.n;
+          if ((h.managed || (rng() & 1)) ? hipFree(h.p) : hipFreeAsync(h.p, nullptr)) bad_free++;
           continue;
         }
         const size_t n = (size_t)(1 + rng() % (limit / 4));
         void* p = nullptr;
         // reserve in the shadow count first: `live` only ever overstates what the guard holds
         const long long now = (live += (long long)n);
-        const int e = (rng() & 1) ? hipMalloc(&p, n) : hipMallocAsync(&p, n, nullptr);
+        const int kind = (int)(rng() % 3);  // pool, stream-ordered pool, managed (charged at the HIP level)
+        const int e = kind == 0 ? hipMalloc(&p, n) : kind == 1 ? hipMallocAsync(&p, n, nullptr) : hipMallocManaged(&p, n, 1);
         if (e == 0) {
           oks++;
-          held.push_back({p, n});
+          held.push_back({p, n, kind == 2});
           long long pk = peak.load();
           while (now > pk && !peak.compare_exchange_weak(pk, now)) {
           }
@@ -76,9 +86,9 @@ int main(int argc, char** argv) {
           ooms++;
         }
       }
-      for (auto [p, n] : held) {
-        live -= (long long)n;
-        hipFree(p);
+      for (const Held& h : held) {
+        live -= (long long)h.n;
+        hipFree(h.p);
       }
     });
   }

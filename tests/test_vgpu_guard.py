@@ -396,16 +396,18 @@ def test_pod_wide_budget_across_processes_and_crash_release(tmp_path):
 
 
 @pytest.mark.parametrize("sanitizer", ["tsan", "asan"])
-@pytest.mark.parametrize("pod_wide", [False, True])
-def test_guard_under_sanitizers(tmp_path, sanitizer, pod_wide):
+@pytest.mark.parametrize("pod_wide,keyed", [(False, "ordinal"), (True, "ordinal"), (False, "bdf"), (True, "bdf")])
+def test_guard_under_sanitizers(tmp_path, sanitizer, pod_wide, keyed):
     """SURVEY.md §5.2 for the guard: 16 threads allocating and freeing against one budget (and, pod-wide,
     a forked child drawing from the parent's budget) under ThreadSanitizer and ASan/UBSan — no race, no
-    memory error, never past the limit, every byte returned.  (TSan found two races in the first
+    memory error, never past the limit, every byte returned; pool and managed allocations mixed, the
+    device named by ordinal or by PCI address (resolved concurrently with the first allocations).  (TSan found two races in the first
     version: a lazily resolved entry point, and an address reused between the runtime's free and the
     guard forgetting it.)"""
     exe = str(binary(f"vgpu_selftest_{sanitizer}"))
     conf = tmp_path / "c.conf"
-    conf.write_text(f"hbm_limit 0 {8 * GiB}\n" + (f"acct {tmp_path / 'pod.acct'}\n" if pod_wide else ""))
+    limit = f"hbm_limit 0 {8 * GiB}" if keyed == "ordinal" else f"hbm_limit_bdf 0000:05:00.0 {8 * GiB}"
+    conf.write_text(limit + "\n" + (f"acct {tmp_path / 'pod.acct'}\n" if pod_wide else ""))
     env = dict(os.environ, GTK_VGPU_CONFIG=str(conf))
     if pod_wide:
         env["SELFTEST_ACCT"] = "1"
