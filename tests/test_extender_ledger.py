@@ -155,3 +155,20 @@ def test_failed_bind_releases_its_ledger_entry():
     except Exception:  # noqa: BLE001 - the injected apiserver failure
         pass
     assert "default/p0" not in parse_ledger(obj_annotations(api.get_node("n1")))
+
+
+def test_malformed_or_foreign_ledger_values_do_not_break_binds():
+    """A ledger another writer mangled (not JSON, wrong shapes, device ids off the node) reads as
+    empty or is ignored where it names no device of the node; the next bind rewrites it."""
+    from gpu_topology_on_k8s_amd.k8s.annotations import dump_ledger
+
+    c = Contract()
+    bad = ["not json", "[1, 2]", '{"a": {"x/y": {"g": "zz", "t": 1}}}', '{"a": [], "gen": "q"}',
+           dump_ledger({"default/other": ((99, -3), 1_700_000_000.0)}, 5)]
+    for i, raw in enumerate(bad):
+        api, exts, _ = _two(ledger=True, n_pods=1, k=8)
+        api.patch_node("n1", annotations={c.ledger_key: raw})
+        d = _bind(api, exts[0], "p0")
+        assert sorted(d.ids) == list(range(8)), (raw, d)
+        led = parse_ledger(obj_annotations(api.get_node("n1")))
+        assert led["default/p0"][0] == tuple(d.ids)
