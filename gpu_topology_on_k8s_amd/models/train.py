@@ -352,8 +352,9 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         ar.capture_local(True)
 
         def verify():
+            frozen = ar.freeze()  # what the optimizer reads, before the check's own collectives run
             ar.capture_local(False)
-            _record(ar.verify(local), ar.verify(local, against=ar.snapshot) if env["world"] > 1 else None)
+            _record(ar.verify(local, frozen=frozen), ar.verify(local, against=ar.snapshot) if env["world"] > 1 else None)
 
         return body(xy, before_opt=verify)
 

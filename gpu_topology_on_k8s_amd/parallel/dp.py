@@ -300,6 +300,19 @@ class BucketedAllReduce:
         """The buffer the optimizer reads after :meth:`finish` (fp32 under ``grad_reduce="fp32"``)."""
         return self.grad32 if self.grad32 is not None else self.flat.grad
 
+    def freeze(self) -> torch.Tensor:
+        """A copy of the buffer the optimizer reads, taken on the current stream at the point the
+        optimizer reads it and before any verification collective: on RCCL those collectives run on
+        the communicator's stream behind the reductions, and a read after them would hide a reduction
+        the optimizer never waited for.  Host memory (pinned) for a GPU buffer."""
+        src = self.reduced_buffer()
+        if not src.is_cuda:
+            return src.clone()
+        out = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+        out.copy_(src, non_blocking=True)
+        torch.cuda.current_stream(src.device).synchronize()
+        return out
+
     def _gather(self, x: torch.Tensor) -> List[torch.Tensor]:
         if self.world == 1:
             return [x]
@@ -310,12 +323,14 @@ class BucketedAllReduce:
         dist.all_gather(parts, raw, group=self.group)
         return [q.view(x.dtype) for q in parts]
 
-    def verify(self, local: torch.Tensor, against: Optional[torch.Tensor] = None) -> Dict[str, object]:
+    def verify(self, local: torch.Tensor, against: Optional[torch.Tensor] = None,
+               frozen: Optional[torch.Tensor] = None) -> Dict[str, object]:
         """Per bucket: the reduced gradient the optimizer reads (this rank's own range under zero1)
         against the exact sum over ranks of ``local`` -- every rank's local gradient, all-gathered
         bit-exactly and summed in fp64.  ``against``: compare with this buffer instead of the
         reduced one, rank-locally (``snapshot`` vs a hook-free pass: was each bucket complete when its
-        collective launched?).  -> ``{"max_rel": worst relative L2 error, "buckets": [...]}``."""
+        collective launched?).  ``frozen``: the reduced buffer as :meth:`freeze` took it (else it is
+        read now).  -> ``{"max_rel": worst relative L2 error, "buckets": [...]}``."""
         out, worst = [], 0.0
         for b in self.buckets:
             s, e = self.own(b)
@@ -324,7 +339,7 @@ class BucketedAllReduce:
                 exact = torch.zeros(e - s, dtype=torch.float64, device=local.device)
                 for q in parts:
                     exact += q[s - b.start:e - b.start].double()
-                got = self.reduced_buffer()[s:e].double()
+                got = (frozen[s:e].to(exact.device) if frozen is not None else self.reduced_buffer()[s:e]).double()
             else:  # the whole bucket: every rank's snapshot holds its own local bucket
                 exact = local[b.start:b.end].double()
                 got = against[b.start:b.end].double()

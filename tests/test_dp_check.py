@@ -7,8 +7,8 @@ mutated one:
 
 * one bucket's collective skipped (the rank applies its local gradient for that bucket);
 * ``b.work.wait()`` removed from :meth:`BucketedAllReduce.finish` while the collectives are slow (a
-  FIFO worker thread runs each one 0.2 s late on a side gloo group, so the optimizer-side read comes
-  before the reduction lands);
+  FIFO worker thread runs each one 0.05 s late on a side gloo group, so the optimizer-side read comes
+  before the reduction lands; the check freezes the buffer at that read, before its own collectives);
 * the same slow collectives WITH the wait: the check passes, so it is the missing wait it catches.
 
 The SGD fingerprint of a 2-rank run must match a 1-rank run on the concatenated batch
@@ -55,7 +55,7 @@ class _SlowDist:
     def _loop(self):
         while True:
             t, ev = self._q.get()
-            time.sleep(0.2)
+            time.sleep(0.05)
             self._real.all_reduce(t, group=self._side)
             ev.set()
             self._q.task_done()
