@@ -141,6 +141,7 @@ __attribute__((visibility("default"))) hsa_status_t hsa_init() {
 }
 
 __attribute__((visibility("default"))) hsa_status_t hsa_iterate_agents(hsa_status_t (*cb)(hsa_agent_t, void*), void* data) {
+  if (!g_inited) return HSA_STATUS_ERROR_NOT_INITIALIZED;  // as ROCr before hsa_init
   hsa_agent_t a{kCpuAgent};
   hsa_status_t e = cb(a, data);
   for (size_t o = 0; o < g_visible.size() && e == HSA_STATUS_SUCCESS; ++o)

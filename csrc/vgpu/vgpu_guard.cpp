@@ -158,6 +158,18 @@ Fn real(const char* name, const char* stem) {
   return reinterpret_cast<Fn>(p);
 }
 
+// the same, or nullptr while the library is not loaded yet (entry points the guard calls on its own
+// initiative, which may run before the program has loaded the runtime)
+template <typename Fn>
+Fn real_opt(const char* name, const char* stem) {
+  void* p = dlsym(RTLD_NEXT, name);
+  if (!p) {
+    void* h = loaded_library(stem);
+    if (h) p = dlsym(h, name);
+  }
+  return reinterpret_cast<Fn>(p);
+}
+
 // resolved once per entry point; a function-local static is initialised thread-safely
 #define REAL_HIP(name, type) static const type real_fn = real<type>(#name, "libamdhip64");
 #define REAL_HSA(name) static const auto real_fn = real<decltype(&::name)>(#name, "libhsa-runtime64");
@@ -237,12 +249,22 @@ void resolve_bdf_config(const Agents& a) {
       }
 }
 
-Agents& agents() {
-  static Agents* a = new Agents();
-  static std::once_flag once;
-  std::call_once(once, [] {
-    REAL_HSA(hsa_iterate_agents);
-    real_fn(
+// Built once the runtime can enumerate (after hsa_init): a call that comes earlier (an exported
+// introspection entry point, a HIP call that does not initialise ROCr) gets an empty table and the next
+// call tries again, so the address-keyed config is never resolved against an empty enumeration.
+// Readers get an immutable table published with release/acquire.
+const Agents& agents() {
+  static std::atomic<const Agents*> ready{nullptr};
+  static const Agents* const empty = new Agents();
+  if (const Agents* p = ready.load(std::memory_order_acquire)) return *p;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> g(mu);
+  if (const Agents* p = ready.load(std::memory_order_acquire)) return *p;
+  const auto iterate = real_opt<decltype(&::hsa_iterate_agents)>("hsa_iterate_agents", "libhsa-runtime64");
+  if (!iterate) return *empty;  // the runtime is not even loaded yet
+  Agents* a = new Agents();
+  {
+    const hsa_status_t e = iterate(
         [](hsa_agent_t ag, void* data) -> hsa_status_t {
           static const auto info = real<decltype(&::hsa_agent_get_info)>("hsa_agent_get_info", "libhsa-runtime64");
           static const auto pools =
@@ -274,8 +296,13 @@ Agents& agents() {
           return HSA_STATUS_SUCCESS;
         },
         a);
-    resolve_bdf_config(*a);
-  });
+    if (e != HSA_STATUS_SUCCESS || a->gpus.empty()) {  // not initialised yet (or no GPU): try again later
+      delete a;
+      return *empty;
+    }
+  }
+  resolve_bdf_config(*a);
+  ready.store(a, std::memory_order_release);
   return *a;
 }
 
@@ -283,8 +310,12 @@ Agents& agents() {
 // number itself when the address is unknown
 int hip_ordinal(int hip) {
   typedef hipError_t (*F)(char*, int, int);
-  static const F bus_id = real<F>("hipDeviceGetPCIBusId", "libamdhip64");
+  static std::atomic<F> cached{nullptr};
+  F bus_id = cached.load(std::memory_order_acquire);
+  if (!bus_id && (bus_id = real_opt<F>("hipDeviceGetPCIBusId", "libamdhip64")) != nullptr)
+    cached.store(bus_id, std::memory_order_release);
   const Agents& a = agents();
+  if (!bus_id) return hip;  // no HIP runtime loaded yet
   char bus[64] = {0};
   uint32_t key = 0;
   if (bus_id(bus, (int)sizeof bus, hip) == kSuccess && parse_bdf(bus, &key))

@@ -222,6 +222,25 @@ def test_address_keyed_share_holds_under_renumbering(tmp_path, visible, rocr_ord
         assert out["other"] == 0, out
 
 
+def test_introspection_before_the_runtime_starts_does_not_disable_the_share(tmp_path):
+    """The guard's address-keyed config is resolved once ROCr can enumerate its agents.  A call into
+    the guard before the runtime is initialised (here its exported introspection entry point, first
+    thing in the process) must not freeze an empty enumeration: the share still holds afterwards."""
+    conf = tmp_path / "gtk-vgpu.conf"
+    conf.write_text(f"hbm_limit_bdf 0000:15:00.0 {8 * GiB}\ncu_mask_bdf 0000:15:00.0 64-127\n")
+    env = {k: v for k, v in os.environ.items() if k not in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES")}
+    env.update(GTK_VGPU_CONFIG=str(conf), FAKE_HIP_DEVICE="0", ROCR_VISIBLE_DEVICES="1,0")
+    env["LD_PRELOAD"] = (env["LD_PRELOAD"] + ":" if env.get("LD_PRELOAD") else "") + str(binary("libgtk_vgpu.so"))
+    early = ("import ctypes\ng0 = ctypes.CDLL(None)\ng0.gtk_vgpu_limit.restype = ctypes.c_longlong\n"
+             "early = (g0.gtk_vgpu_hip_ordinal(0), g0.gtk_vgpu_limit(0))\n")
+    child = early + RENUMBER_CHILD.replace('"rocr_ordinal": g.gtk_vgpu_hip_ordinal(0)}', '"rocr_ordinal": g.gtk_vgpu_hip_ordinal(0), "early": early}')
+    p = subprocess.run([sys.executable, "-c", child, _fake()], capture_output=True, text=True, timeout=60, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["early"] == [0, -1], out  # before the runtime: unresolved (HIP number, no limit yet)
+    assert out["e"] == [0, 2, 0] and out["total"] == 8 * GiB and out["queue"] == "64-127", out
+
+
 def test_ordinal_keyed_share_moves_with_renumbering(tmp_path):
     """Why the plugin writes addresses: the same share keyed by ordinal 0 lands on whichever GPU the
     pod's own ROCR_VISIBLE_DEVICES puts first -- here the other one, and the share's GPU is uncapped."""
