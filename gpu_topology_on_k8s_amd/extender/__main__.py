@@ -48,6 +48,10 @@ def main(argv=None) -> int:
     ap.add_argument("--client-ca", default="",
                     help="require callers to present a certificate signed by this CA (mutual TLS; kube-scheduler's "
                          "extender tlsConfig.certFile/keyFile) — needed before serving beyond loopback")
+    ap.add_argument("--bind-ledger", default="on", choices=["on", "off"],
+                    help="record every bind's devices in the node's allocation ledger (<prefix>/gpu-ledger) with the "
+                         "node's resourceVersion as a precondition, so extender replicas never hand out one GPU twice "
+                         "(needs `patch` on nodes); off = the per-process node lock only (a single extender)")
     ap.add_argument("--log-level", default="INFO")
     a = ap.parse_args(argv)
     logging.basicConfig(level=a.log_level, format='{"ts":"%(asctime)s","lvl":"%(levelname)s","mod":"%(name)s","msg":"%(message)s"}')
@@ -58,7 +62,8 @@ def main(argv=None) -> int:
     cfg = ExtenderConfig(contract=Contract(resource_name=a.resource_name, prefix=a.annotation_prefix, slice_resource=a.slice_resource_name), policy_name=a.policy,
                          policy=PlacementPolicy(tie_break=a.tie_break, partition_aware=a.partition_aware == "on"),
                          assume_ttl=a.assume_ttl, resync_s=a.resync,
-                         scheduler_names=tuple(x.strip() for x in a.scheduler_names.split(",") if x.strip()))
+                         scheduler_names=tuple(x.strip() for x in a.scheduler_names.split(",") if x.strip()),
+                         ledger=a.bind_ledger == "on")
     ext = TopologyExtender(api, cfg)
     if a.informer == "on":
         from ..k8s.informer import Informer

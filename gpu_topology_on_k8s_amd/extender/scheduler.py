@@ -500,6 +500,12 @@ class TopologyExtender:
                             log.info("bind %s on %s: node changed since the decision (attempt %d); re-deciding",
                                      key, node, attempt + 1)
                             continue
+                        except ApiError as e:
+                            if e.code == 403:  # RBAC without `patch` on nodes: say what to fix, then fail the bind
+                                raise ApiError(403, f"bind {key} on {node}: the allocation ledger needs `patch` on nodes "
+                                                    f"for the extender's service account (or run with --bind-ledger off "
+                                                    f"for a single extender): {e}") from e
+                            raise
                     return self._commit(pod, namespace, name, uid, node, key, d, st, now)
             raise ApiError(409, f"bind {namespace}/{name} on {node}: the node's allocation ledger kept changing "
                                 f"({self.cfg.ledger_attempts} attempts)")

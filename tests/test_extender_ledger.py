@@ -172,3 +172,21 @@ def test_malformed_or_foreign_ledger_values_do_not_break_binds():
         assert sorted(d.ids) == list(range(8)), (raw, d)
         led = parse_ledger(obj_annotations(api.get_node("n1")))
         assert led["default/p0"][0] == tuple(d.ids)
+
+
+def test_ledger_without_node_patch_rights_fails_the_bind_with_the_fix_and_can_be_turned_off():
+    """RBAC without `patch` on nodes: the ledger write is refused (403) and the bind fails with a
+    message naming the missing verb and --bind-ledger off; with the ledger off the same bind succeeds
+    (a single extender's node lock only)."""
+    import pytest
+
+    from gpu_topology_on_k8s_amd.extender.__main__ import main as extender_main  # noqa: F401 - the flag exists
+    from gpu_topology_on_k8s_amd.k8s.api import ApiError
+
+    api, exts, _ = _two(ledger=True, n_pods=2)
+    api.inject("patch_node", 403, times=100)
+    with pytest.raises(ApiError) as ei:
+        _bind(api, exts[0], "p0")
+    assert ei.value.code == 403 and "--bind-ledger off" in str(ei.value) and "patch" in str(ei.value)
+    off = TopologyExtender(api, ExtenderConfig(resync_s=0.0, ledger=False, events=False))
+    assert len(_bind(api, off, "p1").ids) == 1
