@@ -114,7 +114,12 @@ print(json.dumps({"tflops": round(float(w["tflops"]), 1), "hbm_copy_gbps": round
     # rehearsed on the one GPU, and the loss lineage with this tree's and the round-4 attention backward
     step pytest_r05 900 python -u -m pytest tests/test_gpu_shares.py tests/test_gpu_rehearsal.py tests/test_gpu_multi.py -k "guard or doctor or rehearsal or dp" -x -v -rP --timeout 300 --timeout-method thread
     step lineage_v7 400 python -u -m gpu_topology_on_k8s_amd.models.train --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
-    step lineage_r04attn 400 python -u bench/with_attn_bwd.py --so ${AB_SO:-scratch/r04/_fused.cpython-310-x86_64-linux-gnu.so} -- --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
+    so=${AB_SO:-scratch/r04/_fused.cpython-310-x86_64-linux-gnu.so}  # another tree's build (git-ignored)
+    if [ -f "$so" ]; then
+      step lineage_r04attn 400 python -u bench/with_attn_bwd.py --so "$so" -- --model llama3-8b --batch 4 --seq 4096 --steps 5 --warmup 2
+    else
+      echo "[gpu_suite] lineage_r04attn skipped: no $so"
+    fi
     ;;
   shadow)
     # what 8-GPU DP communication costs the Llama-3-8B step: comm-shadow CTA sweep
