@@ -1192,13 +1192,16 @@ class DevicePluginServer:
         next_health = next_reconcile = 0.0
         while not self._stop.wait(0.2):
             self._monitor_beat = time.monotonic()
-            if self.cfg.reconcile_interval > 0 and time.monotonic() >= next_reconcile:
+            # a kubelet restart first: the reconcile below talks to the kubelet's pod-resources socket,
+            # which is going away too, and could hold the beat for its RPC timeout before re-registering
+            vanished = not os.path.exists(self.cfg.socket_path)
+            if not vanished and self.cfg.reconcile_interval > 0 and time.monotonic() >= next_reconcile:
                 next_reconcile = time.monotonic() + self.cfg.reconcile_interval
                 try:
                     self.reconcile()
                 except Exception as e:  # noqa: BLE001
                     log.warning("reconcile failed: %s", e)
-            if not os.path.exists(self.cfg.socket_path):
+            if vanished:
                 log.warning("plugin socket %s vanished (kubelet restart?): re-serving and re-registering", self.cfg.socket_path)
                 try:
                     if self._server is not None:
