@@ -10,6 +10,7 @@ not JSON at all.  Binds that do go through must never hand out a device twice.
 import asyncio
 import json
 import logging
+import os
 
 from aiohttp.test_utils import TestClient, TestServer
 from hypothesis import HealthCheck, given, settings
@@ -93,7 +94,7 @@ def _check_shape(verb, status, body):
         assert isinstance(body, dict)
 
 
-@settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@settings(max_examples=int(os.environ.get("GTK_FUZZ_EXAMPLES", "150")), deadline=None, suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
 @given(calls=st.lists(st.one_of(st.tuples(st.sampled_from(["sort", "prioritize", "filter", "preempt"]), bodies),
                                 st.tuples(st.just("bind"), binds),
                                 st.tuples(st.just("raw"), st.binary(max_size=40))), min_size=1, max_size=8))
