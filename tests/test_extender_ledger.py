@@ -9,6 +9,8 @@ FakeAPIServer here, which enforces the precondition as the apiserver does; each 
 """
 import threading
 
+import pytest
+
 from gpu_topology_on_k8s_amd.extender import ExtenderConfig, TopologyExtender
 from gpu_topology_on_k8s_amd.k8s import Contract, FakeAPIServer
 from gpu_topology_on_k8s_amd.k8s.annotations import encode_node_annotations, parse_ledger
@@ -190,3 +192,52 @@ def test_ledger_without_node_patch_rights_fails_the_bind_with_the_fix_and_can_be
     assert ei.value.code == 403 and "--bind-ledger off" in str(ei.value) and "patch" in str(ei.value)
     off = TopologyExtender(api, ExtenderConfig(resync_s=0.0, ledger=False, events=False))
     assert len(_bind(api, off, "p1").ids) == 1
+
+
+@pytest.mark.parametrize("seed", [5, 7, 11])
+def test_two_extenders_under_churn_never_share_a_device(seed):
+    """Randomised churn across two extender instances on one apiserver: pods of 1-4 GPUs are bound
+    concurrently through either instance (4 workers) while others complete; after every round the live
+    pods' GROUP annotations on the node are disjoint, and every device a bind handed out is one no
+    other live pod holds."""
+    import random
+    from concurrent.futures import ThreadPoolExecutor
+
+    api, exts, clock = _two(ledger=True)
+    rng = random.Random(seed)
+    live, n, bound = {}, 0, 0
+    lock = threading.Lock()
+
+    def bind(name):
+        try:
+            ids = _bind(api, exts[rng.randrange(2)], name).ids
+            # the container starts: Allocate flips ASSIGNED (an assumption never confirmed would expire
+            # after the assume TTL by design, and this test's clock runs far past it)
+            api.patch_pod_annotations("default", name, {"ALIYUN_COM_GPU_ASSIGNED": "true"})
+            return name, ids
+        except Exception:  # noqa: BLE001 - no room / ledger contention: kube-scheduler would retry later
+            api.delete_pod("default", name)
+            return name, None
+
+    with ThreadPoolExecutor(4) as pool:
+        for _ in range(40):
+            names = []
+            for _ in range(rng.randint(1, 4)):
+                n += 1
+                api.create_pod(make_pod(f"c{n}", gpus=rng.randint(1, 4)))
+                names.append(f"c{n}")
+            for name, ids in pool.map(bind, names):
+                if ids is not None:
+                    with lock:
+                        live[name] = set(ids)
+                        bound += 1
+            held = [d for s in live.values() for d in s]
+            assert len(held) == len(set(held)), live
+            ann = [obj_annotations(api.get_pod("default", k)).get("ALIYUN_COM_GPU_GROUP") for k in live]
+            flat = [int(x) for v in ann if v for x in v.split(",")]
+            assert len(flat) == len(set(flat)), ann
+            for k in rng.sample(sorted(live), k=min(len(live), rng.randint(0, 3))):  # some pods finish
+                api.delete_pod("default", k)
+                del live[k]
+            clock.t += rng.choice([0.5, 2.0, 40.0])  # sometimes past the ledger grace
+    assert n > 60 and bound > 30, (n, bound)
