@@ -331,18 +331,31 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(const u16* __restrict
   // backward.  Same bf16 values as O.  Row stride 136 elements (272 B) staggers the banks.
   constexpr int kOtStride = 136;
   u16* otl = reinterpret_cast<u16*>(smem);
+  // T21: lane half hh holds columns 8k + 4hh .. +3 of its row; one v_permlane32_swap per dword of a
+  // pair of column groups (k, k+1) gives every lane 16 contiguous bytes (lanes 0-31: group k, lanes
+  // 32-63: group k+1): 8 dwordx4 stores per lane instead of 16 dwordx2
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      u16x4 v4;
+    for (int g4 = 0; g4 < 4; g4 += 2) {
+      u16x4 va, vb;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v4[e] = f2bf(oacc[dt][4 * g4 + e] * inv);
-      *reinterpret_cast<u16x4*>(orow + 32 * dt + 8 * g4 + 4 * hh) = v4;
+      for (int e = 0; e < 4; ++e) {
+        va[e] = f2bf(oacc[dt][4 * g4 + e] * inv);
+        vb[e] = f2bf(oacc[dt][4 * g4 + 4 + e] * inv);
+      }
       if (ot) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) otl[(32 * dt + 8 * g4 + 4 * hh + e) * kOtStride + w * 32 + r] = v4[e];
+        for (int e = 0; e < 4; ++e) {
+          otl[(32 * dt + 8 * g4 + 4 * hh + e) * kOtStride + w * 32 + r] = va[e];
+          otl[(32 * dt + 8 * g4 + 8 + 4 * hh + e) * kOtStride + w * 32 + r] = vb[e];
+        }
       }
+      const auto a = __builtin_bit_cast(uint2, va), bb = __builtin_bit_cast(uint2, vb);
+      const auto s0 = __builtin_amdgcn_permlane32_swap(a.x, bb.x, false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(a.y, bb.y, false, false);
+      const uint4 out = {s0[0], s1[0], s0[1], s1[1]};
+      *reinterpret_cast<uint4*>(orow + 32 * dt + 8 * g4 + 8 * hh) = out;
     }
   if (hh == 0) lse2[(size_t)(b * H + hq) * S + myq] = m + log2f(l);
   if (ot) {
@@ -736,14 +749,22 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq2n_kernel(const u16* __rest
     dma_sync();
   }
   u16* out = dq + ((size_t)(b * H + hq) * S + myq) * D;
+  // T21 widened stores, as the forward's
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      u16x4 a4;
+    for (int g4 = 0; g4 < 4; g4 += 2) {
+      u16x4 va, vb;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) a4[e] = f2bf(dqt[dt][4 * g4 + e] * scale);
-      *reinterpret_cast<u16x4*>(out + 32 * dt + 8 * g4 + 4 * hh) = a4;
+      for (int e = 0; e < 4; ++e) {
+        va[e] = f2bf(dqt[dt][4 * g4 + e] * scale);
+        vb[e] = f2bf(dqt[dt][4 * g4 + 4 + e] * scale);
+      }
+      const auto a = __builtin_bit_cast(uint2, va), bb = __builtin_bit_cast(uint2, vb);
+      const auto s0 = __builtin_amdgcn_permlane32_swap(a.x, bb.x, false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(a.y, bb.y, false, false);
+      const uint4 o4 = {s0[0], s1[0], s0[1], s1[1]};
+      *reinterpret_cast<uint4*>(out + 32 * dt + 8 * g4 + 8 * hh) = o4;
     }
 }
 
