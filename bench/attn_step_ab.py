@@ -36,14 +36,15 @@ def load_other(path: str):
 
 
 class Switch:
-    """``fused.hip()`` stand-in: this tree's extension, with ``attn_bwd`` from ``other`` when ``use_other``."""
+    """``fused.hip()`` stand-in: this tree's extension, with the ``swap`` entry points (default
+    ``attn_bwd``) from ``other`` when ``use_other``."""
 
-    def __init__(self, cur, other):
-        self.cur, self.other, self.use_other = cur, other, False
+    def __init__(self, cur, other, swap=("attn_bwd",)):
+        self.cur, self.other, self.use_other, self.swap = cur, other, False, tuple(swap)
 
     def __getattr__(self, name):
-        if name == "attn_bwd" and self.use_other:
-            return self.other.attn_bwd
+        if name in self.swap and self.use_other:
+            return getattr(self.other, name)
         return getattr(self.cur, name)
 
 
@@ -55,8 +56,9 @@ def main():
     ap.add_argument("--seq", type=int, default=4096)
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--swap", default="attn_bwd", help="comma-separated entry points taken from the other build")
     a = ap.parse_args()
-    sw = Switch(fused.hip(), load_other(a.so))
+    sw = Switch(fused.hip(), load_other(a.so), swap=[x for x in a.swap.split(",") if x])
     fused.hip = lambda: sw  # every call site goes through fused.hip()
     setup_gemm_tuning("auto", None, 0)
     cfg = LlamaConfig.named(a.model)
@@ -91,7 +93,7 @@ def main():
             torch.cuda.synchronize()
             times["other" if arm else "this"].append((time.perf_counter() - t0) / a.steps * 1e3)
     med = {k: statistics.median(v) for k, v in times.items()}
-    print(json.dumps({"model": a.model, "batch": a.batch, "seq": a.seq, "other_so": a.so, "ms_per_step": times,
+    print(json.dumps({"model": a.model, "batch": a.batch, "seq": a.seq, "other_so": a.so, "swap": sw.swap, "ms_per_step": times,
                       "median_ms": med, "delta_pct": 100.0 * (med["this"] / med["other"] - 1.0),
                       "tokens_per_s_this": a.batch * a.seq / med["this"] * 1e3}), flush=True)
 
