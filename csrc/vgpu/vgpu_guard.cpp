@@ -105,7 +105,7 @@ struct State {
   Table* table = nullptr;
   int mine = -1;             // this process's slot
   pid_t mine_pid = 0;        // the process that claimed `mine` (a forked child claims its own)
-  long long limit[kMaxDev];  // bytes; < 0 = no limit on that ordinal
+  std::atomic<long long> limit[kMaxDev];  // bytes; < 0 = no limit (atomic: resolved lazily, read unlocked)
   long long used[kMaxDev];
   std::unordered_map<void*, std::pair<int, size_t>> ptrs;                  // pool allocations
   std::unordered_map<uint64_t, std::pair<int, size_t>> handles;            // vmem handles
@@ -724,27 +724,32 @@ __attribute__((visibility("default"))) hipError_t hipMemGetInfo(size_t* free_b, 
 
 // Managed memory the runtime did not place in a device pool (HMM: system pages that migrate into HBM
 // when a kernel touches them) would bypass the pool hooks: charged here, in full, to the current device.
+// The charge follows the real call: a runtime that does take the block from a device pool has charged
+// (and checked) it in the pool hook already, and a charge taken beforehand would count it twice while
+// that hook decides.  A block over the share is handed back before the caller sees it.
 __attribute__((visibility("default"))) hipError_t hipMallocManaged(void** ptr, size_t size, unsigned int flags) {
   typedef hipError_t (*F)(void**, size_t, unsigned int);
+  typedef hipError_t (*FreeF)(void*);
   REAL_HIP(hipMallocManaged, F);
+  static const FreeF real_free = real<FreeF>("hipFree", "libamdhip64");
   State& s = st();
   if (!s.active) return real_fn(ptr, size, flags);
   const int dev = current_ordinal();
+  hipError_t e = real_fn(ptr, size, flags);
+  if (e != kSuccess || !ptr || !*ptr) return e;
+  {
+    std::lock_guard<std::mutex> g(s.mu);
+    if (s.ptrs.count(*ptr)) return e;  // the runtime took it from a device pool: counted there
+  }
   if (!reserve(dev, size)) {
-    if (ptr) *ptr = nullptr;
+    real_free(*ptr);
+    *ptr = nullptr;
     return 2;  // hipErrorOutOfMemory
   }
-  hipError_t e = real_fn(ptr, size, flags);
-  if (dev < 0 || dev >= kMaxDev || s.limit[dev] < 0) return e;
-  bool charged = e == kSuccess && ptr && *ptr;
-  if (charged) {
+  if (dev >= 0 && dev < kMaxDev && s.limit[dev] >= 0) {
     std::lock_guard<std::mutex> g(s.mu);
-    if (s.ptrs.count(*ptr))
-      charged = false;  // the runtime took it from a device pool: already counted there
-    else
-      s.managed[*ptr] = {dev, size};
+    s.managed[*ptr] = {dev, size};
   }
-  if (!charged) unreserve(dev, size);
   return e;
 }
 
