@@ -475,11 +475,17 @@ class TopologyExtender:
                 raise ApiError(403, f"pod {namespace}/{name} uses scheduler {sched!r}, not one of {list(self.cfg.scheduler_names)}")
             key = pod_key(pod)
             for attempt in range(max(1, self.cfg.ledger_attempts)):
-                # refresh (2 API calls) BEFORE taking the node lock; the decision below uses only cached
-                # state, so a bind never holds one node's lock while waiting for another's
-                self.cache.refresh_node(node)
                 st = self.cache.get(node, sync=False)
-                with st.lock:  # serialise select+annotate+bind per node (in this process)
+                # serialise refresh+select+annotate+bind per node (in this process).  The refresh (2 API
+                # calls) runs under this node's lock, and takes no other node's: the decision must see
+                # the node object and the pod LIST of ONE refresh.  Refreshed outside the lock, a
+                # concurrent refresh could apply a newer node object -- whose ledger has already dropped
+                # a pod its writer saw bound -- over an older LIST that does not show that pod yet; the
+                # pod's devices then look free and the resourceVersion precondition (the newer object's)
+                # passes: one device, two pods.
+                with st.lock:
+                    if self.cache.refresh_node(node) is not st:
+                        continue  # the node was dropped and re-created meanwhile: decide on the new state
                     d, why = self._eval_state(pod, node, st, k)
                     if d is None:
                         raise NoFeasiblePlacement(f"bind {namespace}/{name} on {node}: {why}")

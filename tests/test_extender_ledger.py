@@ -241,3 +241,51 @@ def test_two_extenders_under_churn_never_share_a_device(seed):
                 del live[k]
             clock.t += rng.choice([0.5, 2.0, 40.0])  # sometimes past the ledger grace
     assert n > 60 and bound > 30, (n, bound)
+
+
+def test_a_newer_node_object_never_meets_an_older_pod_list():
+    """The decision sees the node object and the pod LIST of one refresh.  Interleaving forced: B's bind
+    has refreshed (no pod bound yet) when A binds p0 and then p1 -- A's second ledger write drops p0,
+    which A's LIST showed bound -- and a concurrent refresh in B applies that newer node object.  Had B
+    decided on it with its older LIST, p0's device would look free and the newer object's
+    resourceVersion would pass the precondition; B's 7-GPU pod must not get p0's (or p1's) device."""
+    from gpu_topology_on_k8s_amd.extender.scheduler import NoFeasiblePlacement
+
+    api, exts, _ = _two(ledger=True, n_pods=2)
+    api.create_pod(make_pod("big", gpus=7))
+    a, b = exts
+    refreshed, go = threading.Event(), threading.Event()
+    real = b.cache.refresh_node
+    first = [True]
+
+    def paused_refresh(name):
+        st = real(name)
+        if first[0]:
+            first[0] = False
+            refreshed.set()
+            assert go.wait(10)
+        return st
+
+    b.cache.refresh_node = paused_refresh
+    out = {}
+
+    def bind_big():
+        try:
+            out["big"] = _bind(api, b, "big").ids
+        except NoFeasiblePlacement as e:
+            out["big"] = e
+
+    tb = threading.Thread(target=bind_big)
+    tb.start()
+    assert refreshed.wait(10)
+    d0, d1 = _bind(api, a, "p0"), _bind(api, a, "p1")
+    assert "default/p0" not in parse_ledger(obj_annotations(api.get_node("n1")))  # settled, dropped by A
+    tc = threading.Thread(target=lambda: b.cache.update_node_object(api.get_node("n1")))  # B's other refresh
+    tc.start()
+    tc.join(timeout=0.3)
+    go.set()
+    tb.join(timeout=30)
+    tc.join(timeout=30)
+    assert not tb.is_alive() and not tc.is_alive()
+    taken = set(d0.ids) | set(d1.ids)
+    assert isinstance(out["big"], NoFeasiblePlacement) or not set(out["big"]) & taken, (out, taken)
