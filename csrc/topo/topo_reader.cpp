@@ -13,8 +13,10 @@
 #include <amd_smi/amdsmi.h>
 #include <dirent.h>
 #include <dlfcn.h>
+#ifndef GTK_TOPO_NO_PYTHON  // the sanitizer self-test (topo_selftest.cpp) includes this file without Python
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+#endif
 
 #include <algorithm>
 #include <cstdint>
@@ -29,7 +31,9 @@
 #include <tuple>
 #include <vector>
 
+#ifndef GTK_TOPO_NO_PYTHON
 namespace py = pybind11;
+#endif
 
 namespace {
 
@@ -108,6 +112,7 @@ void assign_physical(Result& r) {
       }
 }
 
+#ifndef GTK_TOPO_NO_PYTHON
 py::dict to_py(const Result& r) {
   py::list gpus;
   for (const auto& d : r.devs) {
@@ -167,6 +172,7 @@ py::dict to_py(const Result& r) {
   out["warnings"] = r.warnings;
   return out;
 }
+#endif
 
 std::string fmt_bdf(uint64_t domain, uint64_t bus, uint64_t dev, uint64_t fn) {
   char buf[32];
@@ -707,6 +713,14 @@ std::map<std::string, std::string> read_props(const std::string& path) {
   return m;
 }
 
+// whole-string decimal int (sysfs names such as "12", "node3", "card1" after their prefix); false for
+// anything else, including values out of int range: a stray entry is skipped, not fatal
+bool to_int(const std::string& s, int* out) {
+  if (s.empty() || s.size() > 9 || !std::all_of(s.begin(), s.end(), ::isdigit)) return false;
+  *out = (int)std::strtol(s.c_str(), nullptr, 10);
+  return true;
+}
+
 std::vector<std::string> list_dir(const std::string& path) {
   std::vector<std::string> out;
   DIR* d = opendir(path.c_str());
@@ -719,7 +733,7 @@ std::vector<std::string> list_dir(const std::string& path) {
   std::sort(out.begin(), out.end(), [](const std::string& a, const std::string& b) {
     bool na = !a.empty() && std::all_of(a.begin(), a.end(), ::isdigit);
     bool nb = !b.empty() && std::all_of(b.begin(), b.end(), ::isdigit);
-    if (na && nb) return std::stoll(a) < std::stoll(b);
+    if (na && nb) return a.size() != b.size() ? a.size() < b.size() : a < b;  // numeric order, any length
     return a < b;
   });
   return out;
@@ -778,7 +792,8 @@ void read_host_affinity(Result& r, const std::string& pci_root, const std::strin
     std::vector<int> dist;
     int v;
     while (ss >> v) dist.push_back(v);
-    if (!dist.empty()) r.numa_distance[std::stoi(e.substr(4))] = dist;
+    int nn = 0;
+    if (!dist.empty() && to_int(e.substr(4), &nn)) r.numa_distance[nn] = dist;
   }
 }
 
@@ -853,7 +868,8 @@ Result discover_sysfs_impl(const std::string& root, const std::string& drm_root)
   std::map<int, std::vector<KfdLink>> direct, indirect;
   std::map<int, bool> is_cpu;
   for (const auto& nd : nodes) {
-    int id = std::stoi(nd);
+    int id = 0;
+    if (!to_int(nd, &id)) continue;  // not a KFD node directory
     auto p = read_props(nodes_dir + "/" + nd + "/properties");
     props[id] = p;
     is_cpu[id] = as_u64(p, "simd_count") == 0;
@@ -938,11 +954,13 @@ Result discover_sysfs_impl(const std::string& root, const std::string& drm_root)
         }
       }
       // the card minor: first cardN directory under the device's drm/
-      for (const auto& c : list_dir(dev + "drm"))
-        if (c.rfind("card", 0) == 0) {
-          d.card = std::stoi(c.substr(4));
+      for (const auto& c : list_dir(dev + "drm")) {
+        int cm = 0;
+        if (c.rfind("card", 0) == 0 && to_int(c.substr(4), &cm)) {
+          d.card = cm;
           break;
         }
+      }
     }
     idx_of[nid] = (int)i;
     r.devs.push_back(d);
@@ -991,6 +1009,7 @@ Result discover_sysfs_impl(const std::string& root, const std::string& drm_root)
 
 }  // namespace
 
+#ifndef GTK_TOPO_NO_PYTHON
 PYBIND11_MODULE(_topo, m) {
   m.doc() = "MI355X topology discovery: amdsmi (dlopen) and KFD sysfs backends";
   m.def(
@@ -1079,3 +1098,4 @@ PYBIND11_MODULE(_topo, m) {
   m.attr("HSA_IOLINK_TYPE_XGMI") = 11;
   m.attr("HSA_IOLINK_TYPE_PCIEXPRESS") = 2;
 }
+#endif  // GTK_TOPO_NO_PYTHON

@@ -5,6 +5,7 @@
 Targets (all land in ``gpu_topology_on_k8s_amd/_native/``):
   _topo       C++  (g++)    amdsmi (dlopen) + KFD sysfs topology reader
   bin/libfake_amdsmi.so     stand-in amdsmi for CPU tests of the reader's multi-GPU paths
+  bin/topo_selftest         ASan/UBSan host build of the sysfs reader, fed corrupted trees
   _placement  C++  (g++)    branch-and-bound placement engine
   bin/engine_selftest       ASan/UBSan host build of the engine checked against brute force
   _probe      HIP  (hipcc)  gfx950 link/HBM probe kernels + MFMA warm-up
@@ -120,6 +121,10 @@ def targets() -> List[Target]:
     rocm_lib = str(ROCM / "lib")
     return [
         Target("_topo", [CSRC / "topo" / "topo_reader.cpp"], "gxx", HERE / f"_topo{EXT}", ["-ldl"]),
+        # host-only sanitizer build of the sysfs reader; run by tests/test_topo_reader_asan.py
+        Target("topo_selftest", [CSRC / "topo" / "topo_selftest.cpp"], "gxx", HERE / "bin" / "topo_selftest",
+               ["-g", "-O1", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer",
+                "-ldl"], deps=[CSRC / "topo" / "topo_reader.cpp"], pybind=False, shared=False),
         Target("fake_amdsmi", [CSRC / "topo" / "fake_amdsmi.cpp"], "gxx", HERE / "bin" / "libfake_amdsmi.so",
                ["-fvisibility=default"], pybind=False),
         Target("_placement", [CSRC / "placement" / "engine.cpp", CSRC / "placement" / "engine_module.cpp"], "gxx",
