@@ -183,6 +183,13 @@ std::string fmt_bdf(uint64_t domain, uint64_t bus, uint64_t dev, uint64_t fn) {
 
 // ------------------------------------------------------------------------------------------------
 // amdsmi backend (dlopen)
+
+// a fixed-size char field a library filled: at most `cap` bytes, whether or not it wrote the NUL
+template <size_t N>
+std::string field_str(const char (&f)[N]) {
+  return std::string(f, strnlen(f, N));
+}
+
 struct AmdSmi {
   void* h = nullptr;
 // decltype of the declared prototypes: no link-time dependency on libamd_smi
@@ -300,7 +307,7 @@ Result discover_amdsmi_impl(const std::string& lib) {
   for (size_t i = 0; i < handles.size(); ++i) {
     Dev& d = devs[i];
     auto h = handles[i];
-    amdsmi_bdf_t bdf;
+    amdsmi_bdf_t bdf{};
     if (s.get_bdf(h, &bdf) == AMDSMI_STATUS_SUCCESS) {
       d.bdf = fmt_bdf(bdf.domain_number, bdf.bus_number, bdf.device_number, bdf.function_number);
       d.location = ((uint64_t)bdf.domain_number << 16) | ((uint64_t)bdf.bus_number << 8) | ((uint64_t)bdf.device_number << 3);
@@ -308,16 +315,16 @@ Result discover_amdsmi_impl(const std::string& lib) {
     if (s.get_uuid) {
       char buf[AMDSMI_MAX_STRING_LENGTH] = {0};
       unsigned int len = sizeof(buf);
-      if (s.get_uuid(h, &len, buf) == AMDSMI_STATUS_SUCCESS) d.uuid = buf;
+      if (s.get_uuid(h, &len, buf) == AMDSMI_STATUS_SUCCESS) d.uuid = field_str(buf);
     }
     if (s.get_enum) {
-      amdsmi_enumeration_info_t e;
+      amdsmi_enumeration_info_t e{};
       if (s.get_enum(h, &e) == AMDSMI_STATUS_SUCCESS) {
         d.render_minor = (int)e.drm_render;
         d.card = (int)e.drm_card;
         d.kfd_node = (int)e.hsa_id;
         d.hip_id = (int)e.hip_id;
-        if (d.uuid.empty()) d.uuid = e.hip_uuid;
+        if (d.uuid.empty()) d.uuid = field_str(e.hip_uuid);
       }
     }
     if (s.get_numa) {
@@ -326,16 +333,16 @@ Result discover_amdsmi_impl(const std::string& lib) {
     }
     if (s.get_cpart) {
       char buf[64] = {0};
-      if (s.get_cpart(h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS && buf[0]) d.partition = buf;
+      if (s.get_cpart(h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS && buf[0]) d.partition = field_str(buf);
     }
     if (s.get_mpart) {
       char buf[64] = {0};
-      if (s.get_mpart(h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS && buf[0]) d.memory_partition = buf;
+      if (s.get_mpart(h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS && buf[0]) d.memory_partition = field_str(buf);
     }
     if (s.get_asic) {
-      amdsmi_asic_info_t a;
+      amdsmi_asic_info_t a{};
       if (s.get_asic(h, &a) == AMDSMI_STATUS_SUCCESS) {
-        d.model = a.market_name;
+        d.model = field_str(a.market_name);
         if (a.num_of_compute_units != 0xFFFFFFFFu) d.cus = (int)a.num_of_compute_units;
         if (a.target_graphics_version != 0xFFFFFFFFFFFFFFFFull) {
           char gb[32];
@@ -349,7 +356,7 @@ Result discover_amdsmi_impl(const std::string& lib) {
       if (s.get_mem_total(h, AMDSMI_MEM_TYPE_VRAM, &tot) == AMDSMI_STATUS_SUCCESS) d.vram = tot;
     }
     if (s.get_xgmi_status) {
-      amdsmi_xgmi_link_status_t ls;
+      amdsmi_xgmi_link_status_t ls{};
       if (s.get_xgmi_status(h, &ls) == AMDSMI_STATUS_SUCCESS) {
         int up = 0;
         for (uint32_t l = 0; l < ls.total_links && l < AMDSMI_MAX_NUM_XGMI_LINKS; ++l)
@@ -359,7 +366,7 @@ Result discover_amdsmi_impl(const std::string& lib) {
       }
     }
     if (s.get_ecc_total) {
-      amdsmi_error_count_t ec;
+      amdsmi_error_count_t ec{};
       if (s.get_ecc_total(h, &ec) == AMDSMI_STATUS_SUCCESS) {
         d.ecc_correctable = (int64_t)ec.correctable_count;
         d.ecc_uncorrectable = (int64_t)ec.uncorrectable_count;
@@ -481,7 +488,8 @@ struct Session {
       throw std::runtime_error("socket count");
     }
     std::vector<amdsmi_socket_handle> socks(nsock);
-    if (nsock) s.get_socket_handles(&nsock, socks.data());
+    if (nsock && s.get_socket_handles(&nsock, socks.data()) != AMDSMI_STATUS_SUCCESS) nsock = 0;
+    nsock = std::min<uint32_t>(nsock, (uint32_t)socks.size());
     for (uint32_t k = 0; k < nsock; ++k) {
       uint32_t np = 0;
       if (s.get_processor_handles(socks[k], &np, nullptr) != AMDSMI_STATUS_SUCCESS || np == 0) continue;
@@ -504,7 +512,7 @@ struct Session {
   }
   ~Session() { s.shut_down(); }
   std::string bdf(amdsmi_processor_handle h) {
-    amdsmi_bdf_t b;
+    amdsmi_bdf_t b{};
     if (s.get_bdf(h, &b) != AMDSMI_STATUS_SUCCESS) return "";
     return fmt_bdf(b.domain_number, b.bus_number, b.device_number, 0);  // the package: function 0
   }
@@ -527,9 +535,9 @@ std::vector<PartInfo> partition_info_impl(const std::string& lib) {
     p.bdf = ss.bdf(h);
     p.xcps = ss.xcps[k];
     char buf[64] = {0};
-    if (s.get_cpart && s.get_cpart(h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) p.compute = buf;
-    buf[0] = 0;
-    if (s.get_mpart && s.get_mpart(h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) p.memory = buf;
+    if (s.get_cpart && s.get_cpart(h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) p.compute = field_str(buf);
+    std::memset(buf, 0, sizeof(buf));
+    if (s.get_mpart && s.get_mpart(h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) p.memory = field_str(buf);
     if (s.get_profiles) {
       // a few KiB per profile: on the heap, not the stack
       auto cfg = std::make_unique<amdsmi_accelerator_partition_profile_config_t>();
