@@ -32,8 +32,14 @@ from ..topology.model import Topology
 log = logging.getLogger(__name__)
 
 # a node-ledger entry whose pod no LIST has shown on the node this long after its bind is a bind that
-# failed or was lost: its devices are free again (extender/scheduler.py bind)
+# failed or was lost: its devices are free again (extender/scheduler.py bind).  The age is measured on
+# THIS process's clock, from when this cache first saw the entry: the entry's own timestamp comes from
+# the writer's clock, and an instance whose clock runs ahead of the writer's by more than the grace
+# would otherwise take a bind in flight for a lapsed one.  The writer's timestamp still retires an
+# entry once it is older than the grace plus LEDGER_CLOCK_SKEW_S (a ghost a restarted cache sees for
+# the first time).
 LEDGER_GRACE_S = 30.0
+LEDGER_CLOCK_SKEW_S = 120.0
 
 __all__ = ["Alloc", "NodeState", "ClusterCache"]
 
@@ -64,6 +70,7 @@ class NodeState:
     # resourceVersion precondition): pod key -> (ids, bind time).  An entry covers a bind in flight;
     # once a LIST has shown its pod on the node (`settled`) the pod's own annotation governs
     ledger: Dict[str, Tuple[Tuple[int, ...], float]] = field(default_factory=dict)
+    ledger_seen: Dict[str, Tuple[Tuple[int, ...], float]] = field(default_factory=dict)  # key -> (ids, first seen here)
     ledger_gen: int = 0
     settled: Set[str] = field(default_factory=set)
     synced_at: float = 0.0
@@ -87,17 +94,24 @@ class NodeState:
         for a in self.allocs.values():
             if not a.assigned and now - a.assume_time <= ttl:
                 t = min(t, a.assume_time + ttl)
+        g_s = min(ttl, LEDGER_GRACE_S)
         for key, (_, at) in self.ledger_live(now, ttl).items():
-            t = min(t, at + min(ttl, LEDGER_GRACE_S))
+            t = min(t, self._first_seen(key, now) + g_s, at + g_s + LEDGER_CLOCK_SKEW_S)
         return t
 
+    def _first_seen(self, key: str, now: float) -> float:
+        seen = self.ledger_seen.get(key)
+        return seen[1] if seen is not None else now
+
     def ledger_live(self, now: float, ttl: float, grace: float = None) -> Dict[str, Tuple[Tuple[int, ...], float]]:
-        """Ledger entries that still hold their devices: binds in flight -- younger than ``grace`` (and
-        ``ttl``) and whose pod no LIST has shown on the node yet.  The rest are what the next ledger
-        write drops (a settled pod's annotation governs; an entry past the grace is a failed bind)."""
-        g_s = LEDGER_GRACE_S if grace is None else grace
+        """Ledger entries that still hold their devices: binds in flight -- seen by this cache for at
+        most ``grace`` (and ``ttl``), written at most ``grace`` + LEDGER_CLOCK_SKEW_S ago by the writer's
+        clock, and whose pod no LIST has shown on the node yet.  The rest are what the next ledger write
+        drops (a settled pod's annotation governs; an entry past the grace is a failed bind)."""
+        g_s = min(ttl, LEDGER_GRACE_S if grace is None else grace)
         return {k: (g, t) for k, (g, t) in self.ledger.items()
-                if now - t <= min(ttl, g_s) and k not in self.settled}
+                if k not in self.settled and now - self._first_seen(k, now) <= g_s
+                and now - t <= g_s + LEDGER_CLOCK_SKEW_S}
 
     @property
     def unknown(self) -> int:
@@ -174,6 +188,12 @@ class ClusterCache:
                 st.ledger = ledger
                 st.settled &= set(ledger)
                 st.bump()
+            now = self.clock()
+            seen = {}
+            for k, (ids, _) in ledger.items():
+                prev = st.ledger_seen.get(k)
+                seen[k] = prev if prev is not None and prev[0] == ids else (ids, now)
+            st.ledger_seen = seen
             alloc = ((node.get("status") or {}).get("allocatable") or {})
             st.capacity = -1
             for r in self.resources:

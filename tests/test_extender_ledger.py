@@ -126,7 +126,7 @@ def test_ledger_entries_settle_and_lapse():
     """An entry covers a bind in flight only: once a LIST shows the pod on the node its own annotation
     governs (the next ledger write drops the entry), and an entry whose pod never appears lapses after
     the grace period (a bind that failed after recording its devices)."""
-    from gpu_topology_on_k8s_amd.extender.cache import LEDGER_GRACE_S
+    from gpu_topology_on_k8s_amd.extender.cache import LEDGER_CLOCK_SKEW_S, LEDGER_GRACE_S
     from gpu_topology_on_k8s_amd.k8s.annotations import dump_ledger
 
     api, exts, clock = _two(ledger=True, n_pods=3)
@@ -143,7 +143,7 @@ def test_ledger_entries_settle_and_lapse():
     d2 = _bind(api, exts[0], "p2")
     assert 7 not in d2.ids
     api.delete_pod("default", "p2")
-    clock.t += LEDGER_GRACE_S + 1
+    clock.t += LEDGER_GRACE_S + LEDGER_CLOCK_SKEW_S + 1  # old by the writers' clocks too (exts[1] never saw them)
     api.create_pod(make_pod("p3", gpus=6))
     d3 = _bind(api, exts[1], "p3")
     assert 7 in d3.ids  # the ghost's device is free again
@@ -289,3 +289,31 @@ def test_a_newer_node_object_never_meets_an_older_pod_list():
     assert not tb.is_alive() and not tc.is_alive()
     taken = set(d0.ids) | set(d1.ids)
     assert isinstance(out["big"], NoFeasiblePlacement) or not set(out["big"]) & taken, (out, taken)
+
+
+def test_an_instance_whose_clock_runs_ahead_still_honours_a_bind_in_flight():
+    """The ledger entry's timestamp is the writer's clock.  An instance 90 s ahead (more than the grace)
+    must still count a fresh entry: it ages entries from when it first saw them.  Once it has seen an
+    entry for longer than the grace with no pod behind it, the entry lapses on its own clock."""
+    from gpu_topology_on_k8s_amd.extender.cache import LEDGER_GRACE_S
+    from gpu_topology_on_k8s_amd.k8s.annotations import dump_ledger
+
+    api = FakeAPIServer()
+    c = Contract()
+    t = fx.f7_mi355x()
+    api.create_node(make_node("n1", labels={c.label_model: "MI355X"}, annotations=encode_node_annotations(t, c),
+                              capacity={c.resource_name: str(t.n)}))
+    behind, ahead = Clock(1_700_000_000.0), Clock(1_700_000_090.0)
+    a = TopologyExtender(api, ExtenderConfig(resync_s=0.0, ledger=True, events=False), clock=behind)
+    b = TopologyExtender(api, ExtenderConfig(resync_s=0.0, ledger=True, events=False), clock=ahead)
+    # A has recorded its decision (devices 0-3) but not yet annotated or bound the pod
+    api.patch_node("n1", annotations={c.ledger_key: dump_ledger({"default/inflight": ((0, 1, 2, 3), behind.t)}, 1)})
+    api.create_pod(make_pod("big", gpus=5))
+    with pytest.raises(Exception):
+        _bind(api, b, "big")  # only 4 devices are free: the in-flight entry holds 0-3
+    api.create_pod(make_pod("four", gpus=4))
+    assert not set(_bind(api, b, "four").ids) & {0, 1, 2, 3}
+    b.cache.refresh_node("n1")  # a resync LISTs "four" on the node: its own annotation governs from now on
+    ahead.t += LEDGER_GRACE_S + 1  # B has now seen the in-flight entry for longer than the grace: a lost bind
+    api.delete_pod("default", "four")
+    assert len(_bind(api, b, "big").ids) == 5
