@@ -70,7 +70,9 @@ class NodeState:
     # resourceVersion precondition): pod key -> (ids, bind time).  An entry covers a bind in flight;
     # once a LIST has shown its pod on the node (`settled`) the pod's own annotation governs
     ledger: Dict[str, Tuple[Tuple[int, ...], float]] = field(default_factory=dict)
-    ledger_seen: Dict[str, Tuple[Tuple[int, ...], float]] = field(default_factory=dict)  # key -> (ids, first seen here)
+    # key -> (ids, writer time, first seen here): a re-written entry (a new incarnation of the pod name)
+    # is a new entry and ages from when it was first seen
+    ledger_seen: Dict[str, Tuple[Tuple[int, ...], float, float]] = field(default_factory=dict)
     ledger_gen: int = 0
     settled: Set[str] = field(default_factory=set)
     synced_at: float = 0.0
@@ -101,7 +103,7 @@ class NodeState:
 
     def _first_seen(self, key: str, now: float) -> float:
         seen = self.ledger_seen.get(key)
-        return seen[1] if seen is not None else now
+        return seen[2] if seen is not None else now
 
     def ledger_live(self, now: float, ttl: float, grace: float = None) -> Dict[str, Tuple[Tuple[int, ...], float]]:
         """Ledger entries that still hold their devices: binds in flight -- seen by this cache for at
@@ -190,9 +192,9 @@ class ClusterCache:
                 st.bump()
             now = self.clock()
             seen = {}
-            for k, (ids, _) in ledger.items():
+            for k, (ids, at) in ledger.items():
                 prev = st.ledger_seen.get(k)
-                seen[k] = prev if prev is not None and prev[0] == ids else (ids, now)
+                seen[k] = prev if prev is not None and prev[:2] == (ids, at) else (ids, at, now)
             st.ledger_seen = seen
             alloc = ((node.get("status") or {}).get("allocatable") or {})
             st.capacity = -1
@@ -270,7 +272,9 @@ class ClusterCache:
         st.allocs = allocs
         st.unknown_pods = unknown
         st.unknown_uids = unknown_uids
-        settled = st.settled | (seen & set(st.ledger))
+        # a key stays settled only while the LIST shows it: a pod name that comes back (a StatefulSet
+        # pod re-created) with a new bind in flight is a new entry no LIST has shown yet
+        settled = (st.settled & seen) | (seen & set(st.ledger))
         if settled != st.settled:
             st.settled = settled
             st.bump()
@@ -427,6 +431,7 @@ class ClusterCache:
             if event == "DELETED" or pod_is_terminal(obj):
                 st.allocs.pop(key, None)
                 st.unknown_pods.pop(key, None)
+                st.settled.discard(key)
                 with self._lock:
                     self._overlay.get(node, {}).pop(key, None)
                 return

@@ -317,3 +317,83 @@ def test_an_instance_whose_clock_runs_ahead_still_honours_a_bind_in_flight():
     ahead.t += LEDGER_GRACE_S + 1  # B has now seen the in-flight entry for longer than the grace: a lost bind
     api.delete_pod("default", "four")
     assert len(_bind(api, b, "big").ids) == 5
+
+
+def test_a_reused_pod_name_in_flight_is_not_taken_for_its_settled_predecessor():
+    """StatefulSet pods come back under the same name.  B has seen "db" bound (its ledger entry settled);
+    db is deleted and re-created, and A records the new db's devices in the ledger but has not bound it
+    yet.  B, deciding in that window, must count the new entry: the old pod's settlement does not carry
+    over to a new incarnation that no LIST has shown."""
+    from gpu_topology_on_k8s_amd.extender.scheduler import NoFeasiblePlacement
+
+    api, exts, _ = _two(ledger=True)
+    a, b = exts
+    api.create_pod(make_pod("db", gpus=4))
+    first = _bind(api, a, "db")
+    b.cache.refresh_node("n1")  # B's LIST shows db on the node: settled in B's view
+    api.delete_pod("default", "db")
+    api.create_pod(make_pod("db", gpus=4))
+    api.create_pod(make_pod("all", gpus=8))
+    recorded, go = threading.Event(), threading.Event()
+    real_commit = a._commit
+
+    def paused_commit(*args, **kw):  # A: devices recorded in the ledger, pod not yet annotated or bound
+        recorded.set()
+        assert go.wait(10)
+        return real_commit(*args, **kw)
+
+    a._commit = paused_commit
+    out = {}
+    ta = threading.Thread(target=lambda: out.setdefault("db", _bind(api, a, "db")))
+    ta.start()
+    assert recorded.wait(10)
+    try:
+        out["all"] = _bind(api, b, "all").ids
+    except NoFeasiblePlacement as e:
+        out["all"] = e
+    go.set()
+    ta.join(timeout=30)
+    assert not ta.is_alive()
+    assert isinstance(out["all"], NoFeasiblePlacement), (out, first.ids)
+
+
+def test_a_reused_pod_name_on_the_same_devices_is_a_new_entry():
+    """As above, but long after the first incarnation and on the SAME devices: the new bind's entry has
+    the old key and the old device set, and is still a new entry (new bind time) that ages from when B
+    first sees it, not from when B saw the old one."""
+    from gpu_topology_on_k8s_amd.extender.cache import LEDGER_GRACE_S
+    from gpu_topology_on_k8s_amd.extender.scheduler import NoFeasiblePlacement
+
+    api, exts, clock = _two(ledger=True)
+    a, b = exts
+    api.create_pod(make_pod("db", gpus=4))
+    first = _bind(api, a, "db")
+    a.cache.refresh_node("n1")
+    b.cache.refresh_node("n1")  # both have seen db bound and its entry
+    api.delete_pod("default", "db")
+    clock.t += LEDGER_GRACE_S + 1
+    api.create_pod(make_pod("db", gpus=4))
+    api.create_pod(make_pod("all", gpus=8))
+    recorded, go = threading.Event(), threading.Event()
+    real_commit = a._commit
+    chosen = {}
+
+    def paused_commit(pod, namespace, name, uid, node, key, d, *rest):
+        chosen["ids"] = d.ids
+        recorded.set()
+        assert go.wait(10)
+        return real_commit(pod, namespace, name, uid, node, key, d, *rest)
+
+    a._commit = paused_commit
+    ta = threading.Thread(target=lambda: _bind(api, a, "db"))
+    ta.start()
+    assert recorded.wait(10)
+    assert tuple(chosen["ids"]) == tuple(first.ids)  # the same devices again
+    try:
+        got = _bind(api, b, "all").ids
+    except NoFeasiblePlacement as e:
+        got = e
+    go.set()
+    ta.join(timeout=30)
+    assert not ta.is_alive()
+    assert isinstance(got, NoFeasiblePlacement), got
