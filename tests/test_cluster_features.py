@@ -530,3 +530,66 @@ def test_strict_specs_do_not_require_card_nodes(tmp_path):
     (tmp_path / "dri" / f"card{t.gpus[1].card}").write_text("")
     r = plug.Allocate(req, None).container_responses[0]
     assert f"/dev/dri/card{t.gpus[1].card}" in [d.container_path for d in r.devices]
+
+
+def test_relist_started_during_a_bind_keeps_the_binds_devices():
+    """A relist whose LIST request goes out while a bind is in flight (after the bind's own refresh,
+    before the binding is accepted) cannot show the pod, and is newer than anything applied so far: only
+    the bind's overlay entry (its epoch assigned when the binding is accepted) keeps the devices used
+    until a LIST that started after the bind shows the pod."""
+    api = FakeAPIServer()
+    api.create_node(make_node("n", annotations=encode_node_annotations(fx.f7_mi355x(), C), capacity={C.resource_name: "8"}))
+    api.create_pod(make_pod("p", gpus=2))
+    ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+    cache = ext.cache
+    cache.sync_all()
+    real_bind_pod = api.bind_pod
+    grabbed = {}
+
+    def bind_pod(*a, **kw):  # the binding request is in flight: a relist starts now
+        grabbed["token"] = cache.begin_list("Pod")
+        grabbed["items"] = api.list_pods()
+        return real_bind_pod(*a, **kw)
+
+    api.bind_pod = bind_pod
+    d = ext.bind("default", "p", "", "n")
+    cache.on_list("Pod", grabbed["items"], grabbed["token"])  # ... and arrives after the bind
+    used = cache.get("n", sync=False).used(time.time(), 300.0)
+    assert set(d.ids) <= used, (d.ids, used)
+
+
+def test_relist_applied_while_the_binding_is_in_flight_keeps_the_assumption():
+    """A LIST applied between the assumption and the accepted binding (it cannot show the pod yet) must
+    not drop the assumption: until the binding is accepted no LIST can prove the pod gone."""
+    api = FakeAPIServer()
+    api.create_node(make_node("n", annotations=encode_node_annotations(fx.f7_mi355x(), C), capacity={C.resource_name: "8"}))
+    api.create_pod(make_pod("p", gpus=2))
+    ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+    cache = ext.cache
+    cache.sync_all()
+    real_bind_pod = api.bind_pod
+
+    def bind_pod(*a, **kw):
+        token = cache.begin_list("Pod")
+        cache.on_list("Pod", api.list_pods(), token)  # a relist lands before the binding is accepted
+        return real_bind_pod(*a, **kw)
+
+    api.bind_pod = bind_pod
+    d = ext.bind("default", "p", "", "n")
+    assert set(d.ids) <= cache.get("n", sync=False).used(time.time(), 300.0)
+
+
+def test_an_older_list_arriving_late_is_ignored():
+    """Concurrent LISTs can complete out of order: one that started before a newer one already applied
+    is dropped whole, or it would erase pods the newer one showed."""
+    api = FakeAPIServer()
+    api.create_node(make_node("n", annotations=encode_node_annotations(fx.f7_mi355x(), C), capacity={C.resource_name: "8"}))
+    api.create_pod(make_pod("q", gpus=2))
+    ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+    cache = ext.cache
+    cache.sync_all()
+    old_token, old_items = cache.begin_list("Pod"), api.list_pods()  # q not bound yet
+    ext.bind("default", "q", "", "n")
+    cache.refresh_node("n")  # a newer LIST shows q bound
+    cache.on_list("Pod", old_items, old_token)  # the older LIST completes last
+    assert "default/q" in cache.get("n", sync=False).allocs
