@@ -49,3 +49,35 @@ def test_preferred_answer_is_always_admissible(r):
     ids = [int(x) for x in resp.container_responses[0].deviceIDs]
     assert len(ids) == size and len(set(ids)) == size, (r, ids)
     assert set(ids) <= set(avail) and set(must) <= set(ids), (r, ids)
+    healthy = [a for a in avail if a not in unhealthy]
+    if group is None and set(must) <= set(healthy) and len(healthy) >= size:
+        assert set(ids) <= set(healthy), (r, ids)  # unhealthy devices only when nothing else fits
+
+
+def test_claim_rereads_when_the_pod_changed_under_it():
+    """Allocate claims the oldest pending pod of the right size with a conditional patch: if the pod was
+    changed in between (here the reconcile pass confirmed it with its own devices), the patch conflicts,
+    the candidates are re-read, and the next pending pod is claimed instead of the confirmed one being
+    overwritten."""
+    api = FakeAPIServer()
+    api.create_node(make_node("n1"))
+    for name, group, t in (("a", [0, 1], 1_700_000_000.0), ("b", [2, 3], 1_700_000_001.0)):
+        pod = make_pod(name, gpus=2, node="n1")
+        pod["metadata"].setdefault("annotations", {}).update(PodAssignment.assumed(group, t).to_annotations())
+        api.create_pod(pod)
+    plugin = DevicePluginServer(fx.f7_mi355x(), PluginConfig(resource_name="amd.com/gpu", socket_dir=_SOCK, node_name="n1"),
+                                api=api)
+    real = api.patch_pod_annotations
+    first = [True]
+
+    def patch(ns, name, ann, resource_version=None):
+        if first[0] and name == "a":
+            first[0] = False
+            real(ns, "a", {"ALIYUN_COM_GPU_ASSIGNED": "true"})  # confirmed meanwhile, on its own devices
+        return real(ns, name, ann, resource_version=resource_version)
+
+    api.patch_pod_annotations = patch
+    claimed = plugin._claim_pod([4, 5])
+    assert claimed["metadata"]["name"] == "b"
+    a = PodAssignment.from_annotations(api.get_pod("default", "a")["metadata"]["annotations"])
+    assert a.assigned and list(a.group) == [0, 1]
