@@ -178,6 +178,13 @@ def _dp_worker(rank, world, port, q):
     gathered = [torch.zeros(1) for _ in range(world)]
     dist.all_gather(gathered, t)
     out["replicas_equal"] = all(abs(g.item() - gathered[0].item()) < 1e-6 for g in gathered)
+    # stragglers: buckets no backward hook launched (parameters that got no gradient) are launched by
+    # finish() itself; here no backward runs at all, so finish() must reduce every bucket
+    before = ar.stats["launches"]
+    m.flat.grad.fill_(rank + 1)
+    ar.finish()
+    out["straggler_launches"] = ar.stats["launches"] - before
+    out["stragglers_reduced"] = bool((m.flat.grad.float() == world * (world + 1) / 2).all())
     tiles = sorted((b.start, b.end) for b in ar.buckets)
     out["tiled"] = tiles[0][0] == 0 and tiles[-1][1] == m.flat.numel and all(a[1] == b[0] for a, b in zip(tiles, tiles[1:]))
     q.put((rank, out))
@@ -202,6 +209,7 @@ def test_bucketed_allreduce_two_ranks_gloo():
         assert res[r]["launches"] == res[r]["buckets"]  # every bucket launched from a backward hook
         assert res[r]["replicas_equal"]
         assert res[r]["tiled"]
+        assert res[r]["straggler_launches"] == res[r]["buckets"] and res[r]["stragglers_reduced"], res[r]
 
 
 def _zero1_worker(rank, world, port, q):
