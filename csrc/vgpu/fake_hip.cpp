@@ -139,6 +139,9 @@ static const unsigned kManagedTag = 0x6d616e67;  // "mang": system memory, freed
 __attribute__((visibility("default"))) hipError_t hipMallocManaged(void** p, size_t n, unsigned int) {
   init();
   if (!p) return kInvalid;
+  // FAKE_HIP_MANAGED_IN_POOL=1: a runtime that backs managed memory with a device pool (no HMM): the
+  // guard's pool hook charges it, and its HIP-level hook must not charge it again
+  if (const char* v = std::getenv("FAKE_HIP_MANAGED_IN_POOL"); v && v[0] == '1') return dev_alloc(p, n);
   unsigned* b = static_cast<unsigned*>(std::malloc(32 + (n & 7)));
   if (!b) return kOom;
   b[0] = kManagedTag;

@@ -222,6 +222,23 @@ def test_address_keyed_share_holds_under_renumbering(tmp_path, visible, rocr_ord
         assert out["other"] == 0, out
 
 
+def test_pool_backed_managed_memory_is_charged_once(tmp_path):
+    """A runtime without HMM backs hipMallocManaged with a device pool: the pool hook charges the block,
+    and the HIP-level managed hook sees that and does not charge it a second time (which would refuse
+    a block that fits: 6 GiB + 2 GiB managed in an 8 GiB share)."""
+    conf = tmp_path / "gtk-vgpu.conf"
+    conf.write_text(f"hbm_limit_bdf 0000:15:00.0 {8 * GiB}\ncu_mask_bdf 0000:15:00.0 64-127\n")
+    env = {k: v for k, v in os.environ.items() if k not in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES")}
+    env.update(GTK_VGPU_CONFIG=str(conf), FAKE_HIP_DEVICE="1", FAKE_HIP_MANAGED_IN_POOL="1")
+    env["LD_PRELOAD"] = (env["LD_PRELOAD"] + ":" if env.get("LD_PRELOAD") else "") + str(binary("libgtk_vgpu.so"))
+    child = RENUMBER_CHILD.replace("(bus, 64, 0)", "(bus, 64, 1)").replace("hip_ordinal(0)", "hip_ordinal(1)").replace(
+        'os.environ["FAKE_HIP_DEVICE"] = "1"', 'os.environ["FAKE_HIP_DEVICE"] = "0"')
+    p = subprocess.run([sys.executable, "-c", child, _fake()], capture_output=True, text=True, timeout=60, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["e"] == [0, 2, 0] and out["used_full"] == 8 * GiB and out["used_freed"] == 6 * GiB, out
+
+
 def test_introspection_before_the_runtime_starts_does_not_disable_the_share(tmp_path):
     """The guard's address-keyed config is resolved once ROCr can enumerate its agents.  A call into
     the guard before the runtime is initialised (here its exported introspection entry point, first
