@@ -160,3 +160,40 @@ def test_partitioned_node_classes_are_banded_separately(seed):
     same = t.physical[:, None] == t.physical[None, :]
     off = ~np.eye(n, dtype=bool)
     assert len(set(banded[same & off].tolist())) == 1 and len(set(banded[~same].tolist())) == 1
+
+
+def test_a_link_whose_own_repeats_spread_widely_takes_its_band_from_them():
+    """Class spread 1 % (band 3 %), one link 6 % below the class median whose own repeats spread 10 %:
+    its median is as noisy as its offset, so it takes the class value; a link 6 % low with a tight 1 %
+    spread is a real difference and keeps its measurement."""
+    t = f7_mi355x()
+    raw = np.full((8, 8), LINK)
+    spread = np.full((8, 8), 0.01)
+    np.fill_diagonal(raw, np.nan)
+    raw[0, 1] = LINK * 0.94
+    spread[0, 1] = 0.10
+    raw[2, 3] = LINK * 0.94
+    banded, rep = band_links(t, raw, spread)
+    assert banded[0, 1] == pytest.approx(LINK) and banded[2, 3] == pytest.approx(LINK * 0.94)
+    assert [2, 3] in rep["kept"] and [0, 1] not in rep["kept"]
+
+
+def test_links_inside_a_package_and_across_packages_are_separate_classes():
+    """XCPs of one package talk over Infinity Fabric, others over xGMI: even when a backend reports both
+    as one-hop links of the same type, they are banded against their own class medians, not mixed."""
+    from gpu_topology_on_k8s_amd.topology.fixtures import f8_mi355x_cpx
+
+    t = f8_mi355x_cpx()
+    n = t.n
+    t.link_type[:, :] = t.link_type.max()  # one type for every pair (a backend that cannot tell them apart)
+    np.fill_diagonal(t.link_type, 0)
+    t.hops[:, :] = 1
+    np.fill_diagonal(t.hops, 0)
+    rng = np.random.default_rng(3)
+    same = np.equal.outer(t.physical, t.physical)
+    raw = np.where(same, 400.0, 60.0) * (1 + rng.uniform(-0.01, 0.01, (n, n)))
+    np.fill_diagonal(raw, np.nan)
+    banded, _ = band_links(t, raw, np.full((n, n), 0.01))
+    off = ~np.eye(n, dtype=bool)
+    assert np.unique(np.round(banded[same & off], 6)).size == 1  # every intra-package link on its class value
+    assert np.unique(np.round(banded[~same], 6)).size == 1
