@@ -146,3 +146,28 @@ def test_pair_cost_lca():
     assert t.pair_cost(0, 1) == t.lca(0, 1).link_cost
     assert t.lca(0, 6) is t.root
     assert t.pair_cost(3, 3) == 0.0
+
+
+def test_fragment_best_fit_outranks_access_cost():
+    """Alg. 2 picks the fragment whose free share is closest to the request (the author's note: least
+    fragment waste), even when another fragment sits on a cheaper GPU."""
+    t = fx.f4_tree()
+    t.mark_used([0], 0.8)  # 0.2 free, access cost 2
+    t.mark_used([2], 0.5)  # 0.5 free, access cost 1
+    assert fragment(t, 0.15) == [0]
+    assert fragment(t, 0.3) == [2]  # does not fit on GPU0
+
+
+def test_link_prefers_cheaper_access_over_a_tighter_subtree():
+    """Two same-class subtrees can host the request: the one whose GPUs are cheaper to reach wins over
+    the one it would fill exactly (TotalCost = m x children's access cost, Alg. 4 line 10)."""
+    from gpu_topology_on_k8s_amd.placement.gaia import link, tree_from_spec
+
+    spec = {"link": "SOC", "children": [
+        {"link": "PIX", "children": [{"gpu": 0, "cost": 3}, {"gpu": 1, "cost": 3}]},
+        {"link": "PIX", "children": [{"gpu": 2, "cost": 1}, {"gpu": 3, "cost": 1}, {"gpu": 4, "cost": 1}]},
+    ]}
+    assert link(tree_from_spec(spec), 2) == [2, 3]
+    # same access costs: the tighter subtree (no GPU left stranded) wins
+    spec["children"][0]["children"] = [{"gpu": 0, "cost": 1}, {"gpu": 1, "cost": 1}]
+    assert link(tree_from_spec(spec), 2) == [0, 1]
