@@ -155,6 +155,12 @@ def test_repartition_pass_marks_the_node_and_records_the_outcome(node):
     assert c.partition_failed_key not in api.get_node("w")["metadata"]["annotations"]
     api.patch_node("w", labels={c.partition_request_label: "bogus"})
     assert repartition(api, "w", c, idle)[0] == "invalid"
+    # a failure mark left from an earlier request goes once the node is in the requested mode (an operator
+    # switched it by hand): "already there" clears it
+    api.patch_node("w", labels={c.partition_request_label: "DPX"},
+                   annotations={c.partition_failed_key: "DPX/-: an earlier refusal"})
+    assert repartition(api, "w", c, idle)[0] == "same"
+    assert c.partition_failed_key not in api.get_node("w")["metadata"]["annotations"]
 
 
 def test_repartition_without_packages_is_not_already_there(node, monkeypatch):
