@@ -298,3 +298,39 @@ def test_node_label_devices_per_gpu():
         DevicePluginServer(topo, PluginConfig(node_name=name), api=api)._publish_node()
     labels = {n: api.get_node(n)["metadata"]["labels"][C.label_slices] for n in ("s", "w", "c")}
     assert labels == {"s": "4", "w": "1", "c": "8"}
+
+
+def test_gpu_memory_on_a_node_without_device_sizes_is_refused_with_the_reason():
+    """A sliced node whose topology carries no device memory sizes cannot size a ``gpu-memory`` request:
+    /filter names why for that node instead of failing the verb."""
+    from gpu_topology_on_k8s_amd.extender import ExtenderConfig, TopologyExtender
+    from gpu_topology_on_k8s_amd.k8s import FakeAPIServer
+    from gpu_topology_on_k8s_amd.k8s.objects import make_node
+
+    t = time_slice(fx.f7_mi355x(), 4)
+    for g in t.gpus:
+        g.vram_bytes = 0
+    api = FakeAPIServer()
+    api.create_node(make_node("s", annotations=encode_node_annotations(t, C), capacity={C.slice_resource: "32"}))
+    ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+    pod = api.create_pod(make_pod("m2", gpus=2, resource=C.slice_resource, annotations={C.memory_key: "100G"}))
+    ok, failed = ext.filter(pod, ["s"])
+    assert ok == [] and "cannot be sized" in failed["s"], failed
+
+
+def test_small_pods_pack_onto_the_fuller_node():
+    """Node-level best fit: with the same placement quality on both nodes, a 2-GPU pod goes to the node
+    that already runs work, keeping the empty node whole for an 8-GPU job."""
+    from gpu_topology_on_k8s_amd.extender import ExtenderConfig, TopologyExtender
+    from gpu_topology_on_k8s_amd.k8s import FakeAPIServer
+    from gpu_topology_on_k8s_amd.k8s.objects import make_node
+
+    api = FakeAPIServer()
+    for n in ("empty", "busy"):
+        api.create_node(make_node(n, annotations=encode_node_annotations(fx.f7_mi355x(), C), capacity={C.resource_name: "8"}))
+    ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+    first = api.create_pod(make_pod("first", gpus=4))
+    ext.bind("default", "first", first["metadata"]["uid"], "busy")
+    pod = api.create_pod(make_pod("small", gpus=2))
+    scores = dict(ext.prioritize(pod, ["empty", "busy"]))
+    assert scores["busy"] > scores["empty"], scores
