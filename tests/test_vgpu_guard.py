@@ -123,8 +123,11 @@ every = (ctypes.c_uint32 * 8)(*([0xFFFFFFFF] * 8))                 # a stream as
 rt.hipExtStreamCreateWithCUMask(ctypes.byref(s2), ctypes.c_uint32(8), every)
 part = (ctypes.c_uint32 * 8)(*([0xFFFFFFFF] * 3 + [0] * 5))        # ... for CUs 0-95
 rt.hipExtStreamCreateWithCUMask(ctypes.byref(s3), ctypes.c_uint32(8), part)
+s4 = ctypes.c_void_p()
+low = (ctypes.c_uint32 * 8)(*([0xFFFFFFFF] + [0] * 7))             # ... for CUs 0-31, none of them the share's
+rt.hipExtStreamCreateWithCUMask(ctypes.byref(s4), ctypes.c_uint32(8), low)
 print(json.dumps({"init_mask": rt.fake_hip_init_mask().decode(),
-                  "queues": [rt.fake_hip_stream_mask(s).decode() for s in (s1, s2, s3)]}))
+                  "queues": [rt.fake_hip_stream_mask(s).decode() for s in (s1, s2, s3, s4)]}))
 """
 
 
@@ -146,13 +149,14 @@ def test_guard_enforces_the_mask_at_rocr_whatever_the_first_call(tmp_path, mode,
     assert p.returncode == 0, p.stderr[-2000:]
     out = json.loads(p.stdout.strip().splitlines()[-1])
     assert out["init_mask"] == "0:64-127"
-    assert out["queues"] == ["64-127", "64-127", "64-95"]
+    # a stream mask with no CU of the share would stop its queue: the share's own mask applies instead
+    assert out["queues"] == ["64-127", "64-127", "64-95", "64-127"]
     env.pop("LD_PRELOAD")
     q = subprocess.run([sys.executable, "-c", REWRITE_CHILD, fake, mode, first], capture_output=True, text=True, timeout=60,
                        env=env)
     assert q.returncode == 0, q.stderr[-2000:]
     out = json.loads(q.stdout.strip().splitlines()[-1])
-    assert out["init_mask"] == "0:0-255" and out["queues"] == ["0-255", "0-255", "0-95"]
+    assert out["init_mask"] == "0:0-255" and out["queues"] == ["0-255", "0-255", "0-95", "0-31"]
 
 
 RENUMBER_CHILD = r"""
