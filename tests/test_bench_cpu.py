@@ -40,6 +40,23 @@ def test_bench_two_ranks_gloo():
     assert sw["all_exact"] and [r["bytes"] for r in sw["rows"]][:2] == [8, 64] and sw["peak"]["busbw_gbps"] > 0
 
 
+def test_bench_line_is_internally_consistent():
+    """The numbers of the JSON line agree with each other and with the timed phase: algBW is the message
+    over ms_per_step, busBW is algBW x 2(k-1)/k, the value is k x busBW, and ms_per_step x steps of the
+    timed region fits inside the headline phase (the driver checks the line against its own clock)."""
+    steps = 40
+    out = _bench("--gpus", "2", "--backend", "cpu", "--steps", str(steps), "--warmup", "1", "--size-mb", "4",
+                 "--sweep", "off", "--probe", "off")
+    k, nbytes, ms = out["n_gpus"], out["config"]["message_bytes_per_gpu"], out["ms_per_step"]
+    algbw = nbytes / (ms / 1e3) / 1e9
+    rel = 1e-4 / ms + 1e-6  # ms_per_step is printed to 4 decimals
+    assert abs(out["algbw_gbps"] - algbw) <= rel * algbw + 2e-3, out
+    assert abs(out["busbw_gbps"] - algbw * 2 * (k - 1) / k) <= rel * algbw + 2e-3, out
+    assert abs(out["value"] - k * out["busbw_gbps"]) <= 2e-2 * out["value"] + 4e-3, out
+    # the headline phase is the timed region plus its bracketing barriers, on rank 0's clock (rounded to ms)
+    assert ms * steps <= out["phase_s"]["headline"] * 1e3 + 0.5, out
+
+
 def test_bench_single_rank_cpu():
     out = _bench("--backend", "cpu", "--steps", "2", "--warmup", "1", "--size-mb", "1", "--via", "direct")
     assert out["k8s_placement"] is None
