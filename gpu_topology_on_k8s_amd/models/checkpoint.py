@@ -299,18 +299,21 @@ class CheckpointWriter:
             os.replace(os.path.join(self.root, "latest.tmp"), os.path.join(self.root, "latest"))
             if old is not None:
                 shutil.rmtree(old, ignore_errors=True)
-            self._prune()
+            self._prune(os.path.basename(final))
         self.saved.append(step)
         if dist.is_initialized():
             dist.barrier()
 
-    def _prune(self) -> None:
+    def _prune(self, current: str) -> None:
+        """Keep ``current`` (what ``latest`` now names) and the newest ``keep - 1`` other steps.  A run
+        resumed from an older step re-saves lower step numbers than the directories it left behind;
+        counting ``current`` by its number would delete it (keep = 1) and leave ``latest`` dangling."""
         if self.keep <= 0:
             return
         # numeric order: the zero padding stops sorting lexicographically past step 999999
-        steps = sorted((d for d in os.listdir(self.root) if d.startswith("step_") and d[5:].isdigit() and
+        steps = sorted((d for d in os.listdir(self.root) if d.startswith("step_") and d[5:].isdigit() and d != current and
                         os.path.exists(os.path.join(self.root, d, "meta.json"))), key=lambda d: int(d[5:]))
-        for d in steps[:-self.keep]:
+        for d in steps[:max(0, len(steps) - (self.keep - 1))]:
             shutil.rmtree(os.path.join(self.root, d), ignore_errors=True)
 
     def has(self, step: int) -> bool:

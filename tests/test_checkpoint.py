@@ -64,6 +64,24 @@ def test_keep_prunes_and_latest_points_at_newest(tmp_path):
     assert meta["numel"] == m.flat.numel and meta["layout"][0][0] == m.flat.names[0]
 
 
+def test_a_resumed_run_saving_older_steps_keeps_its_latest(tmp_path):
+    """A run resumed from an older step writes lower step numbers than the directories left behind by
+    the run it replaces: the step ``latest`` names is never the one pruned, and with keep = 1 it is the
+    only one left."""
+    cfg = LlamaConfig.tiny()
+    m = Llama(cfg, device="cpu")
+    opt = FlatAdamW(m.flat)
+    w = CheckpointWriter(str(tmp_path), m, opt, keep=1)
+    w.save(5)
+    w.close()
+    w = CheckpointWriter(str(tmp_path), m, opt, keep=1)  # resumed from an older step, saving step 3
+    w.save(3)
+    w.close()
+    assert open(tmp_path / "latest").read() == "step_000003"
+    assert sorted(d for d in os.listdir(tmp_path) if d.startswith("step_")) == ["step_000003"]
+    assert latest_checkpoint(str(tmp_path)).endswith("step_000003")
+
+
 def test_layout_mismatch_is_refused(tmp_path):
     m = Llama(LlamaConfig.tiny(), device="cpu")
     w = CheckpointWriter(str(tmp_path), m, FlatAdamW(m.flat))
