@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""Hand-made mutants of the control plane's decision code, each run against the tests that should
+catch it (a mutation-testing pass; README "Mutation testing of the control plane").
+
+    python tools/mutants.py                  # every group
+    python tools/mutants.py --only ledger    # one group (ledger, cache, plugin, dp, guard, banding, gaia,
+                                             # repartition, extender)
+
+Each mutant replaces one line (or a few) of a source file, runs the group's tests with pytest-xdist,
+and restores the file whatever happens.  ``CAUGHT`` = some test failed, ``SURVIVED`` = the tests did
+not notice: either a missing test or an equivalent mutant (listed with ``equivalent=True`` and a
+reason; they are reported, not failed).  The guard's mutants rebuild ``libgtk_vgpu.so`` and its
+sanitizer self-tests, before and after.  Refuses to run on a tree with uncommitted changes to the
+files it mutates.  Exit status 1 when a non-equivalent mutant survives.
+"""
+import argparse
+import os
+import subprocess
+import sys
+from dataclasses import dataclass
+from typing import List
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@dataclass
+class Mutant:
+    group: str
+    path: str
+    old: str
+    new: str
+    equivalent: bool = False
+    why: str = ""
+
+
+CACHE = "gpu_topology_on_k8s_amd/extender/cache.py"
+SCHED = "gpu_topology_on_k8s_amd/extender/scheduler.py"
+PLUGIN = "gpu_topology_on_k8s_amd/deviceplugin/plugin.py"
+DP = "gpu_topology_on_k8s_amd/parallel/dp.py"
+GUARD = "csrc/vgpu/vgpu_guard.cpp"
+CHECKS = "gpu_topology_on_k8s_amd/ops/checks.py"
+GAIA = "gpu_topology_on_k8s_amd/placement/gaia.py"
+REPART = "gpu_topology_on_k8s_amd/deviceplugin/repartition.py"
+
+MUTANTS: List[Mutant] = [
+    # allocation ledger (cross-extender bind safety)
+    Mutant("ledger", CACHE, "if k not in self.settled and now - self._first_seen(k, now) <= g_s",
+           "if now - self._first_seen(k, now) <= g_s"),
+    Mutant("ledger", CACHE, "            if key not in self.allocs:  # being bound by another extender",
+           "            if False:  # being bound by another extender"),
+    Mutant("ledger", SCHED, "resource_version=st.node_rv)", "resource_version=None)"),
+    Mutant("ledger", SCHED, "                        entries[key] = (tuple(d.ids), now)", "                        pass"),
+    Mutant("ledger", CACHE, "        settled = (st.settled & seen) | (seen & set(st.ledger))",
+           "        settled = st.settled | (seen & set(st.ledger))"),
+    Mutant("ledger", CACHE, "seen[k] = prev if prev is not None and prev[:2] == (ids, at) else (ids, at, now)",
+           "seen[k] = prev if prev is not None and prev[0] == ids else (ids, at, now)"),
+    Mutant("ledger", SCHED, "                self._ledger_release(node, key)", "                pass"),
+    Mutant("ledger", SCHED, "                    if self.cache.refresh_node(node) is not st:",
+           "                    if self.cache.refresh_node(node) is not st and False:", equivalent=True,
+           why="the node object is re-created only when a node is deleted and re-added mid-bind"),
+    # overlay / LIST epochs (the cache's view of this process's binds)
+    Mutant("cache", CACHE, "                after_bind = list_epoch > self._overlay_epoch.get((st.name, key), 0)",
+           "                after_bind = True"),
+    Mutant("cache", CACHE, "                elif after_bind and self.consistent_lists:", "                elif self.consistent_lists:"),
+    Mutant("cache", CACHE, "                self._overlay_epoch[(node, pod)] = self._next_epoch()",
+           "                self._overlay_epoch[(node, pod)] = 0"),
+    Mutant("cache", CACHE, "            self._overlay_epoch[(node, pod)] = math.inf", "            self._overlay_epoch[(node, pod)] = 0"),
+    Mutant("cache", CACHE, "        if list_epoch < st.list_epoch:", "        if False:"),
+    Mutant("cache", CACHE, "            if a.assigned or (now - a.assume_time) <= ttl:", "            if a.assigned:"),
+    Mutant("cache", CACHE, '        return self._next_epoch() if kind == "Pod" else None', "        return None"),
+    Mutant("cache", CACHE, "                    if after_bind:  # a LIST started after the bind: authoritative from now on",
+           "                    if True:  # a LIST started after the bind: authoritative from now on", equivalent=True,
+           why="a LIST that shows the pod carries its annotation: dropping the overlay entry early loses nothing"),
+    # device plugin
+    Mutant("plugin", PLUGIN, "            exact = [c for c in cands if sorted(set(c[1].group)) == ids]", "            exact = []"),
+    Mutant("plugin", PLUGIN, '                resource_version=md.get("resourceVersion"))', "                resource_version=None)"),
+    Mutant("plugin", PLUGIN, "            if pa is not None and pa.assigned and sorted(set(pa.group)) == ids:",
+           "            if pa is not None and pa.assigned:"),
+    Mutant("plugin", PLUGIN, "                if len(g) == size and g <= set(avail) and set(must) <= g:", "                if len(g) == size:"),
+    Mutant("plugin", PLUGIN, "        healthy = [a for a in avail if 0 <= a < self.topology.n and self._health.get(a, True)]",
+           "        healthy = [a for a in avail if 0 <= a < self.topology.n]"),
+    Mutant("plugin", PLUGIN, "            unhealthy = [i for i in ids if not self._health.get(i, True)]", "            unhealthy = []"),
+    # data-parallel reduction
+    Mutant("dp", DP, "        return b.start + self.rank * c, b.start + (self.rank + 1) * c", "        return b.start, b.start + c"),
+    Mutant("dp", DP, "                if b.work is None:\n                    self._launch(b)", "                if False:\n                    self._launch(b)"),
+    Mutant("dp", DP, "        return 1.0 / self.world if self.average else 1.0", "        return 1.0"),
+    Mutant("dp", DP, "            self.snapshot[b.start:b.end].copy_(view)", "            pass"),
+    Mutant("dp", DP, "            buf.copy_(view)", "            pass"),
+    # vGPU guard (rebuilt per mutant)
+    Mutant("guard", GUARD, "      if (total + (long long)bytes > s.limit[dev]) return false;", "      if (false) return false;"),
+    Mutant("guard", GUARD, "  if (s.used[dev] + (long long)bytes > s.limit[dev]) return false;", "  if (false) return false;"),
+    Mutant("guard", GUARD, "    if (s.ptrs.count(*ptr)) return e;  // the runtime took it from a device pool: counted there",
+           "    if (false) return e;"),
+    Mutant("guard", GUARD, "        if (i == s.mine || slot_alive(s.acct_fd, i)) total += s.table->slot[i].used[dev];",
+           "        if (i == s.mine) total += s.table->slot[i].used[dev];"),
+    Mutant("guard", GUARD, "      if (a.bdf[o] == l.first) s.limit[o] = l.second;", "      if (a.bdf[o] == l.first) s.limit[0] = l.second;"),
+    Mutant("guard", GUARD, "    if (any)  // an empty intersection would stop the queue: the share's own mask applies instead",
+           "    if (true)"),
+    # probe banding
+    Mutant("banding", CHECKS, "            if abs(meas[p] - med) <= band * med and meas[p] >= floors[p]:",
+           "            if abs(meas[p] - med) <= band * med:"),
+    Mutant("banding", CHECKS, "                if abs(med - pmed) <= cls_band * pmed:", "                if False:"),
+    Mutant("banding", CHECKS, "            band = max(cls_band, float(sp[p]))  # the class's typical repeat spread, or this link's own",
+           "            band = cls_band"),
+    Mutant("banding", CHECKS,
+           "    return int(topo.link_type[a, b]), int(topo.hops[a, b]), int(topo.physical[a]) == int(topo.physical[b])",
+           "    return int(topo.link_type[a, b]), int(topo.hops[a, b]), True"),
+    # Gaia algorithms
+    Mutant("gaia", GAIA, "        leaf = _pick(cands, lambda l: (round(l.resources, 9), l.access_cost), tie_break, rng)",
+           "        leaf = _pick(cands, lambda l: (l.access_cost,), tie_break, rng)"),
+    Mutant("gaia", GAIA, "    pool = cands if cands else leaves", "    pool = leaves"),
+    Mutant("gaia", GAIA, "        lambda c: (c.link_cost, m * (_min_access(c, m) / m), c.free_whole - m),",
+           "        lambda c: (c.link_cost, c.free_whole - m),"),
+    Mutant("gaia", GAIA, "    cands = [l for l in leaves if l.used > 1e-12 and m <= l.resources + 1e-12]",
+           "    cands = [l for l in leaves if m <= l.resources + 1e-12]", equivalent=True,
+           why="an unused leaf has resources 1.0, so best fit prefers any fitting fragment anyway"),
+    # partition switch
+    Mutant("repartition", REPART, '            changed = bool(res.get("layout_changed", res["ok"]))', '            changed = bool(res["ok"])'),
+    Mutant("repartition", REPART, "                return idle_fn() and not (h is not None and h.contended())",
+           "                return idle_fn()"),
+    Mutant("repartition", REPART, "        if contract.partition_failed_key in ann:", "        if False:"),
+    # extender node evaluation
+    Mutant("extender", SCHED, "        rank = obj + node_packing_term(free, k, t.n, self.cfg.policy)", "        rank = obj"),
+    Mutant("extender", SCHED, "                if dev_mem <= 0:", "                if False:"),
+    Mutant("extender", SCHED, '        if s > 1 and unit != "slice":', "        if False:"),
+]
+
+TESTS = {
+    "ledger": ["tests/test_extender_ledger.py", "tests/test_extender.py", "tests/test_cluster_features.py", "tests/test_churn.py"],
+    "cache": ["tests/test_cluster_features.py", "tests/test_extender.py", "tests/test_extender_ledger.py", "tests/test_churn.py"],
+    "plugin": ["tests/test_deviceplugin.py", "tests/test_cluster_features.py", "tests/test_preferred_allocation_props.py",
+               "tests/test_daemons.py", "tests/test_health.py"],
+    "dp": ["tests/test_dp_check.py", "tests/test_llama_dp_cpu.py", "tests/test_checkpoint.py"],
+    "guard": ["tests/test_vgpu_guard.py"],
+    "banding": ["tests/test_probe_banding.py", "tests/test_probe_checks.py"],
+    "gaia": ["tests/test_gaia_conformance.py", "tests/test_placement.py"],
+    "repartition": ["tests/test_partition.py", "tests/test_daemons.py"],
+    "extender": ["tests/test_shares.py", "tests/test_extender.py", "tests/test_cluster_features.py"],
+}
+
+GUARD_TARGETS = "vgpu_guard,vgpu_selftest_asan,vgpu_selftest_tsan"
+
+
+def _rebuild_guard() -> bool:
+    p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd._native.build", "--only", GUARD_TARGETS], cwd=REPO,
+                       capture_output=True, text=True, timeout=900)
+    return p.returncode == 0
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--only", default="", help="comma-separated groups")
+    ap.add_argument("-n", type=int, default=6, help="pytest-xdist workers")
+    a = ap.parse_args()
+    groups = [g for g in a.only.split(",") if g] or list(TESTS)
+    todo = [m for m in MUTANTS if m.group in groups]
+    paths = sorted({m.path for m in todo})
+    dirty = subprocess.run(["git", "status", "--porcelain", "--", *paths], cwd=REPO, capture_output=True, text=True).stdout
+    if dirty.strip():
+        print("refusing: uncommitted changes in\n" + dirty, file=sys.stderr)
+        return 2
+    bad = 0
+    for m in todo:
+        path = os.path.join(REPO, m.path)
+        src = open(path).read()
+        if m.old not in src:
+            print(f"MISSING   [{m.group}] {m.old.strip()[:90]}")
+            bad += 1
+            continue
+        try:
+            open(path, "w").write(src.replace(m.old, m.new, 1))
+            if m.path == GUARD and not _rebuild_guard():
+                print(f"NOBUILD   [{m.group}] {m.old.strip()[:90]}")
+                continue
+            p = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "-n", str(a.n), "-m", "not gpu",
+                                *TESTS[m.group]], cwd=REPO, capture_output=True, text=True, timeout=1800)
+            caught = p.returncode != 0
+            tag = "CAUGHT  " if caught else ("EQUIV   " if m.equivalent else "SURVIVED")
+            if not caught and not m.equivalent:
+                bad += 1
+            note = f"  ({m.why})" if m.equivalent and not caught else ""
+            print(f"{tag}  [{m.group}] {m.old.strip()[:90].replace(chr(10), ' ')}{note}", flush=True)
+        finally:
+            open(path, "w").write(src)
+    if any(m.path == GUARD for m in todo):
+        _rebuild_guard()
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
