@@ -129,7 +129,8 @@ TESTS = {
     "ledger": ["tests/test_extender_ledger.py", "tests/test_extender.py", "tests/test_cluster_features.py", "tests/test_churn.py"],
     "cache": ["tests/test_cluster_features.py", "tests/test_extender.py", "tests/test_extender_ledger.py", "tests/test_churn.py"],
     "plugin": ["tests/test_deviceplugin.py", "tests/test_cluster_features.py", "tests/test_preferred_allocation_props.py",
-               "tests/test_daemons.py", "tests/test_health.py"],
+               "tests/test_daemons.py", "tests/test_health.py", "tests/test_sim.py", "tests/test_churn.py",
+               "tests/test_reprobe_admission.py", "tests/test_partition.py", "tests/test_shares.py"],
     "dp": ["tests/test_dp_check.py", "tests/test_llama_dp_cpu.py", "tests/test_checkpoint.py"],
     "guard": ["tests/test_vgpu_guard.py"],
     "banding": ["tests/test_probe_banding.py", "tests/test_probe_checks.py"],
