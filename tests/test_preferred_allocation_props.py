@@ -81,3 +81,20 @@ def test_claim_rereads_when_the_pod_changed_under_it():
     assert claimed["metadata"]["name"] == "b"
     a = PodAssignment.from_annotations(api.get_pod("default", "a")["metadata"]["annotations"])
     assert a.assigned and list(a.group) == [0, 1]
+
+
+def test_claim_prefers_the_pod_whose_group_matches_exactly():
+    """The kubelet allocated exactly what the extender annotated on the NEWER of two pending pods of the
+    same size: that pod is claimed, not the older one (the oldest-same-size rule is only the fallback
+    when no GROUP matches)."""
+    api = FakeAPIServer()
+    api.create_node(make_node("n1"))
+    for name, group, t in (("old", [0, 1], 1_700_000_000.0), ("new", [2, 3], 1_700_000_005.0)):
+        pod = make_pod(name, gpus=2, node="n1")
+        pod["metadata"].setdefault("annotations", {}).update(PodAssignment.assumed(group, t).to_annotations())
+        api.create_pod(pod)
+    plugin = DevicePluginServer(fx.f7_mi355x(), PluginConfig(resource_name="amd.com/gpu", socket_dir=_SOCK, node_name="n1"),
+                                api=api)
+    assert plugin._claim_pod([2, 3])["metadata"]["name"] == "new"
+    old = PodAssignment.from_annotations(api.get_pod("default", "old")["metadata"]["annotations"])
+    assert not old.assigned and list(old.group) == [0, 1]
