@@ -80,6 +80,11 @@ MUTANTS: List[Mutant] = [
     Mutant("plugin", PLUGIN, "        healthy = [a for a in avail if 0 <= a < self.topology.n and self._health.get(a, True)]",
            "        healthy = [a for a in avail if 0 <= a < self.topology.n]"),
     Mutant("plugin", PLUGIN, "            unhealthy = [i for i in ids if not self._health.get(i, True)]", "            unhealthy = []"),
+    Mutant("plugin", PLUGIN, "            if not ids:\n                continue  # not admitted yet (or not ours)",
+           "            if False:\n                continue  # not admitted yet (or not ours)"),
+    Mutant("plugin", PLUGIN, "                ann[ANN_ASSUME_TIME] = str(int(self.clock()))", "                pass"),
+    Mutant("plugin", PLUGIN, "            if PodAssignment.from_annotations(obj_annotations(p)) is not None or pod_phase(p) != \"Pending\":",
+           "            if PodAssignment.from_annotations(obj_annotations(p)) is not None:"),
     # data-parallel reduction
     Mutant("dp", DP, "        return b.start + self.rank * c, b.start + (self.rank + 1) * c", "        return b.start, b.start + c"),
     Mutant("dp", DP, "                if b.work is None:\n                    self._launch(b)", "                if False:\n                    self._launch(b)"),
