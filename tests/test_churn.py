@@ -193,3 +193,47 @@ def test_random_churn_on_time_sliced_nodes(seed):
                 assert not (prev & cus), (key, envs["HSA_CU_MASK"])  # neighbours on one GPU never share a CU
                 prev |= cus
         assert placed > 0 and any(k in frac for k in request)  # the slice pool really was exercised
+
+
+def test_reconcile_leaves_bound_but_not_admitted_pods_alone():
+    """The kubelet has not admitted a bound pod yet (its pod-resources show no devices for it): the
+    reconcile pass must not touch the extender's assumption (stamping an empty GROUP as ASSIGNED would
+    hide the devices the extender set aside for it)."""
+    with SimCluster({"n": fx.f7_mi355x()}) as c:
+        c.submit("a", 2)
+        (r,) = c.schedule_pending(admit=False)
+        before = PodAssignment.from_annotations(obj_annotations(c.api.get_pod("default", "a")))
+        assert c.reconcile() == 0
+        after = PodAssignment.from_annotations(obj_annotations(c.api.get_pod("default", "a")))
+        assert after == before and not after.assigned and sorted(after.group) == sorted(r.devices)
+
+
+def test_reconcile_restores_a_lost_assignment_with_the_full_contract():
+    """An admitted pod whose annotations were lost (a failed patch, a user edit) gets all three back from
+    the kubelet's allocation: GROUP, ASSIGNED=true and an ASSUME_TIME."""
+    from gpu_topology_on_k8s_amd.k8s.annotations import ANN_ASSIGNED, ANN_ASSUME_TIME, ANN_GROUP
+
+    with SimCluster({"n": fx.f7_mi355x()}) as c:
+        c.submit("a", 2)
+        (r,) = c.schedule_pending()
+        c.api.patch_pod_annotations("default", "a", {ANN_GROUP: None, ANN_ASSIGNED: None, ANN_ASSUME_TIME: None})
+        assert c.reconcile() == 1
+        ann = obj_annotations(c.api.get_pod("default", "a"))
+        assert ann[ANN_GROUP] == ",".join(str(i) for i in sorted(r.allocated)) and ann[ANN_ASSIGNED] == "true"
+        assert int(ann[ANN_ASSUME_TIME]) > 0
+
+
+def test_allocate_for_an_unannotated_pod_skips_running_ones():
+    """A pod scheduled around the extender is matched by its GPU count among the node's PENDING pods
+    without a GROUP; a running pod of the same size (already admitted) is not a candidate."""
+    from gpu_topology_on_k8s_amd.k8s.objects import make_pod
+
+    with SimCluster({"n": fx.f7_mi355x()}) as c:
+        plugin = c.nodes["n"].plugin
+        old = make_pod("legacy-running", gpus=2, node="n")
+        old["status"] = {"phase": "Running"}
+        c.api.create_pod(old)
+        c.api.create_pod(make_pod("legacy-new", gpus=2, node="n"))
+        claimed = plugin._claim_pod([4, 5])
+        assert claimed["metadata"]["name"] == "legacy-new"
+        assert PodAssignment.from_annotations(obj_annotations(c.api.get_pod("default", "legacy-running"))) is None
