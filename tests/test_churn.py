@@ -230,10 +230,10 @@ def test_allocate_for_an_unannotated_pod_skips_running_ones():
 
     with SimCluster({"n": fx.f7_mi355x()}) as c:
         plugin = c.nodes["n"].plugin
-        old = make_pod("legacy-running", gpus=2, node="n")
+        old = make_pod("a-legacy-running", gpus=2, node="n")
         old["status"] = {"phase": "Running"}
         c.api.create_pod(old)
-        c.api.create_pod(make_pod("legacy-new", gpus=2, node="n"))
+        c.api.create_pod(make_pod("b-legacy-new", gpus=2, node="n"))
         claimed = plugin._claim_pod([4, 5])
-        assert claimed["metadata"]["name"] == "legacy-new"
-        assert PodAssignment.from_annotations(obj_annotations(c.api.get_pod("default", "legacy-running"))) is None
+        assert claimed["metadata"]["name"] == "b-legacy-new"
+        assert PodAssignment.from_annotations(obj_annotations(c.api.get_pod("default", "a-legacy-running"))) is None
