@@ -73,7 +73,10 @@ MUTANTS: List[Mutant] = [
            why="a LIST that shows the pod carries its annotation: dropping the overlay entry early loses nothing"),
     # device plugin
     Mutant("plugin", PLUGIN, "            exact = [c for c in cands if sorted(set(c[1].group)) == ids]", "            exact = []"),
-    Mutant("plugin", PLUGIN, '                resource_version=md.get("resourceVersion"))', "                resource_version=None)"),
+    Mutant("plugin", PLUGIN, 'return self.api.patch_pod_annotations(md.get("namespace", "default"), md["name"], ann,\n'
+                             '                                                      resource_version=md.get("resourceVersion"))',
+           'return self.api.patch_pod_annotations(md.get("namespace", "default"), md["name"], ann,\n'
+           '                                                      resource_version=None)'),
     Mutant("plugin", PLUGIN, "            if pa is not None and pa.assigned and sorted(set(pa.group)) == ids:",
            "            if pa is not None and pa.assigned:"),
     Mutant("plugin", PLUGIN, "                if len(g) == size and g <= set(avail) and set(must) <= g:", "                if len(g) == size:"),
