@@ -110,6 +110,7 @@ class Phases:
         self.s = {}
         self.skipped = []
         self.current = "setup"  # the phase in progress (the watchdog's report)
+        self.headline = None  # the measured headline line, once timed (a later hang keeps it)
 
     def elapsed(self) -> float:
         return time.perf_counter() - self.t0
@@ -152,9 +153,15 @@ def start_watchdog(seconds: float, ph: Phases, rank: int, world: int, args, exit
         e = err or sys.stderr
         msg = f"watchdog: rank {rank} still in phase '{ph.current}' after {ph.elapsed():.0f} s"
         if rank == 0:
-            print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
-                              "warmup": args.warmup, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-                              "dtype": args.dtype, "error": msg, "phase_s": ph.report()}), file=o, flush=True)
+            if ph.headline is not None:
+                # the headline was timed (max over ranks) before a supplementary phase hung: report it
+                line = dict(ph.headline, error=msg + " (after the headline was measured)", phase_s=ph.report(),
+                            skipped_phases=ph.skipped)
+            else:
+                line = {"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+                        "warmup": args.warmup, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                        "dtype": args.dtype, "error": msg, "phase_s": ph.report()}
+            print(json.dumps(line), file=o, flush=True)
         print(f"bench: {msg}; thread stacks follow", file=e, flush=True)
         try:
             faulthandler.dump_traceback(file=e, all_threads=True)
@@ -557,6 +564,15 @@ def main(argv=None) -> int:
     # nccl-tests busBW (busbw_gbps below); at k = 1 busBW is 0 and the one rank's algBW is the value
     value = busbw * env.world if env.world > 1 else algbw
     headline_bytes = runner.nbytes
+    ph.headline = {
+        "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": env.world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (rank-dependent exact pattern, verified before timing)",
+        "config": {"model": "rccl-allreduce", "op": "sum", "message_bytes_per_gpu": headline_bytes, "inplace": args.inplace,
+                   "backend": args.backend, "global_batch": None, "seq_len": None, "parallelism": f"dp{env.world}",
+                   "subset": choice.devices, "hip_devices": choice.hip_devices},
+        "algbw_gbps": round(algbw, 3), "busbw_gbps": round(busbw, 3), "scaling_comparable": env.world > 1,
+    }
     step_s = ms_per_step / 1e3
     sweep = None
     sizes = sweep_sizes(args.sweep, cpu=cpu)

@@ -256,3 +256,37 @@ def test_watchdog_reports_the_stuck_phase_and_exits():
     assert "thread stacks follow" in err.getvalue()
     t.cancel()
     assert bench.start_watchdog(0, ph, 0, 1, args) is None
+
+
+def test_watchdog_after_the_headline_keeps_the_measured_value():
+    """A supplementary phase (size sweep, fp32, graph latency, worst-subset A/B) that hangs after the
+    headline was timed must not cost the measurement: the watchdog's line carries the headline value and
+    contract fields, with the stuck phase named in ``error``."""
+    import io
+    import threading
+    import time as _time
+
+    sys.path.insert(0, REPO)
+    import bench
+
+    args = bench.parse(["--steps", "3", "--warmup", "1"])
+    ph = bench.Phases(300.0)
+    ph.headline = {"metric": bench.METRIC, "value": 1234.5, "unit": "GB/s", "n_gpus": 2, "steps": 3, "warmup": 1,
+                   "ms_per_step": 1.7, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+                   "config": {"model": "rccl-allreduce", "parallelism": "dp2"}}
+    out, err, codes = io.StringIO(), io.StringIO(), []
+    done = threading.Event()
+
+    def fake_exit(code):
+        codes.append(code)
+        done.set()
+
+    stuck = threading.Thread(target=lambda: ph.run("ab_worst", done.wait, 30), daemon=True)
+    stuck.start()
+    _time.sleep(0.05)
+    t = bench.start_watchdog(0.2, ph, 0, 2, args, exit_fn=fake_exit, out=out, err=err)
+    assert done.wait(10) and codes == [124]
+    line = json.loads(out.getvalue().strip().splitlines()[-1])
+    assert line["value"] == 1234.5 and line["ms_per_step"] == 1.7 and line["config"]["parallelism"] == "dp2"
+    assert "'ab_worst'" in line["error"] and "after the headline" in line["error"]
+    t.cancel()
