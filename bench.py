@@ -95,7 +95,8 @@ def parse(argv=None):
                          "skipped when its predicted cost would overrun it; the headline is never skipped; 0 = no limit")
     ap.add_argument("--watchdog-s", type=float, default=None,
                     help="a rank still running after this many seconds (default: budget + 300; 0 = off) reports the "
-                         "phase it is stuck in (rank 0: a JSON line with value null), dumps every thread's stack and "
+                         "phase it is stuck in (rank 0: a JSON line, value null before the headline is timed and the measured "
+                         "headline after it), dumps every thread's stack and "
                          "exits 124, so a hung collective ends the run with a diagnosis instead of a silent kill")
     return ap.parse_args(argv)
 
