@@ -41,6 +41,7 @@ GUARD = "csrc/vgpu/vgpu_guard.cpp"
 CHECKS = "gpu_topology_on_k8s_amd/ops/checks.py"
 GAIA = "gpu_topology_on_k8s_amd/placement/gaia.py"
 REPART = "gpu_topology_on_k8s_amd/deviceplugin/repartition.py"
+ANN = "gpu_topology_on_k8s_amd/k8s/annotations.py"
 
 MUTANTS: List[Mutant] = [
     # allocation ledger (cross-extender bind safety)
@@ -127,6 +128,14 @@ MUTANTS: List[Mutant] = [
     Mutant("repartition", REPART, "                return idle_fn() and not (h is not None and h.contended())",
            "                return idle_fn()"),
     Mutant("repartition", REPART, "        if contract.partition_failed_key in ann:", "        if False:"),
+    # wire contract (pod / node annotations)
+    Mutant("contract", ANN, "        if g is None or any(i < 0 for i in g):", "        if g is None:"),
+    Mutant("contract", ANN, "                g = parse_group(ann.get(ANN_GPU_ID_ALIAS))  # diagram alias, read-only", "                pass"),
+    Mutant("contract", ANN, '        assigned = str(ann.get(ANN_ASSIGNED, "false")).lower() == "true"',
+           '        assigned = str(ann.get(ANN_ASSIGNED, "false")) == "true"'),
+    Mutant("contract", ANN, '    return [int(x) for x in s.split(",") if x.strip() != ""]', '    return [int(x) for x in s.split(",")]'),
+    Mutant("contract", ANN, "    except (ValueError, TypeError, KeyError, AttributeError):\n        return {}",
+           "    except (ValueError,):\n        return {}"),
     # extender node evaluation
     Mutant("extender", SCHED, "        rank = obj + node_packing_term(free, k, t.n, self.cfg.policy)", "        rank = obj"),
     Mutant("extender", SCHED, "                if dev_mem <= 0:", "                if False:"),
@@ -145,6 +154,8 @@ TESTS = {
     "gaia": ["tests/test_gaia_conformance.py", "tests/test_placement.py"],
     "repartition": ["tests/test_partition.py", "tests/test_daemons.py"],
     "extender": ["tests/test_shares.py", "tests/test_extender.py", "tests/test_cluster_features.py"],
+    "contract": ["tests/test_k8s.py", "tests/test_extender.py", "tests/test_extender_fuzz.py", "tests/test_extender_ledger.py",
+                 "tests/test_deviceplugin.py", "tests/test_cluster_features.py"],
 }
 
 GUARD_TARGETS = "vgpu_guard,vgpu_selftest_asan,vgpu_selftest_tsan"
