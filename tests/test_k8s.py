@@ -181,3 +181,17 @@ def test_rest_client_rereads_a_rotated_token(tmp_path):
         assert ei.value.code == 401
     finally:
         srv.shutdown()
+
+
+def test_pod_assignment_parsing_edge_cases():
+    """GROUP must name device indices: a negative one makes the annotation no assignment at all (the pod
+    then counts by its resource request); ASSIGNED is read case-insensitively, as Go's strconv.ParseBool
+    accepts "True" and "TRUE" from the reference's writers."""
+    from gpu_topology_on_k8s_amd.k8s.annotations import ANN_ASSIGNED, ANN_ASSUME_TIME, ANN_GROUP, PodAssignment
+
+    assert PodAssignment.from_annotations({ANN_GROUP: "-1"}) is None
+    assert PodAssignment.from_annotations({ANN_GROUP: "0,-2"}) is None
+    for v in ("true", "True", "TRUE"):
+        pa = PodAssignment.from_annotations({ANN_GROUP: "1,3", ANN_ASSIGNED: v, ANN_ASSUME_TIME: "1561717704"})
+        assert pa.assigned and pa.group == [1, 3] and pa.assume_time == 1561717704
+    assert not PodAssignment.from_annotations({ANN_GROUP: "1", ANN_ASSIGNED: "false"}).assigned
