@@ -48,6 +48,15 @@ def parse_cpulist(s: str) -> Set[int]:
     return out
 
 
+def try_parse_cpulist(s: str) -> Optional[Set[int]]:
+    """:func:`parse_cpulist`, or None for a malformed list (a hand-edited annotation, not a crash)."""
+    try:
+        out = parse_cpulist(s)
+    except ValueError:
+        return None
+    return out if all(c >= 0 for c in out) else None
+
+
 def format_cpulist(cpus: Iterable[int]) -> str:
     xs = sorted(set(int(c) for c in cpus))
     if not xs:
@@ -119,10 +128,14 @@ def apply_cpuset(spec: Optional[str], source: str = "GTK_CPUSET", threads: bool 
     later inherit the mask), then OpenMP / torch intra-op threads are set to the core count.
     Returns ``{"applied", "source", "requested", "cpus", "n", "reason"}`` for the JSON report lines.
     ``allowed`` / ``setter`` stand in for the OS calls in tests."""
-    want = parse_cpulist(spec or "")
+    want = try_parse_cpulist(spec or "")
     have = set(os.sched_getaffinity(0)) if allowed is None else set(allowed)
-    rep: Dict[str, object] = {"applied": False, "source": source, "requested": format_cpulist(want), "cpus": "", "n": 0,
-                              "reason": ""}
+    rep: Dict[str, object] = {"applied": False, "source": source, "requested": format_cpulist(want or ()), "cpus": "",
+                              "n": 0, "reason": ""}
+    if want is None:
+        rep["requested"] = str(spec)[:200]
+        rep["reason"] = "malformed cpulist: not applied"
+        return rep
     if not want:
         rep["reason"] = "no cpuset given"
         return rep
@@ -164,11 +177,12 @@ def bind_workload(mode: str = "auto", own: str = "", env: Optional[Dict[str, str
     pod = env.get("GTK_CPUSET", "")
     if mode == "env":
         return apply_cpuset(pod, "GTK_CPUSET", **kw)
-    if pod and own and parse_cpulist(pod) & parse_cpulist(own):
-        return apply_cpuset(format_cpulist(parse_cpulist(pod) & parse_cpulist(own)), "GTK_CPUSET&device-slice", **kw)
-    if pod:
+    pod_set, own_set = try_parse_cpulist(pod), try_parse_cpulist(own)
+    if pod_set and own_set and pod_set & own_set:
+        return apply_cpuset(format_cpulist(pod_set & own_set), "GTK_CPUSET&device-slice", **kw)
+    if pod and pod_set is not None:
         return apply_cpuset(pod, "GTK_CPUSET", **kw)
-    return apply_cpuset(own, "device-slice", **kw)
+    return apply_cpuset(own, "device-slice" if not pod else "device-slice (GTK_CPUSET malformed)", **kw)
 
 
 def access_costs(topo, prefer_numa: Optional[Sequence[int]] = None) -> Optional[np.ndarray]:

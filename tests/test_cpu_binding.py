@@ -87,3 +87,16 @@ def test_train_entry_point_reports_and_applies_gtk_cpuset():
             assert parse_cpulist(rep["cpus"]) == set(allowed[:1])
         else:
             assert "disjoint" in rep["reason"]
+
+
+def test_a_malformed_cpuset_is_reported_not_fatal():
+    """GTK_CPUSET comes from a pod annotation a user can edit: a list that does not parse is reported and
+    not applied (the rank falls back to its device's own slice), never an exception at start-up."""
+    from gpu_topology_on_k8s_amd.topology.cpus import apply_cpuset, bind_workload
+
+    calls = []
+    rep = apply_cpuset("0-3,x-7", allowed=set(range(8)), setter=lambda tid, s: calls.append(s))
+    assert rep["applied"] is False and "malformed" in rep["reason"] and not calls
+    rep = bind_workload("auto", own="4-5", env={"GTK_CPUSET": "garbage"}, allowed=set(range(8)),
+                        setter=lambda tid, s: calls.append(s))
+    assert rep["applied"] and rep["cpus"] == "4-5" and "malformed" in rep["source"]
