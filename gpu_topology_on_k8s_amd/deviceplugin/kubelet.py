@@ -3,8 +3,10 @@
 It serves ``Registration`` on ``<dir>/kubelet.sock``; when a plugin registers it dials the plugin's
 endpoint, consumes ``ListAndWatch`` (updating the node's capacity/allocatable in the fake
 apiserver, as the real kubelet does — diagram step 2), and on pod admission calls
-``GetPreferredAllocation`` + ``Allocate`` exactly like the kubelet's device manager.  ``restart()``
-wipes the socket directory like a kubelet restart so plugin re-registration can be tested.
+``GetPreferredAllocation`` + ``Allocate`` the way the kubelet's device manager does: once per
+container with that container's count, init containers first, a regular init container's devices
+reused by the containers after it (``must_include``).  ``restart()`` wipes the socket directory like
+a kubelet restart so plugin re-registration can be tested.
 """
 from __future__ import annotations
 
@@ -19,7 +21,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import grpc
 
-from ..k8s.objects import meta, pod_gpu_request, pod_key
+from ..k8s.objects import meta, pod_device_steps, pod_key
 from .podresources import build_response, pod_resources_handler
 from . import proto as pb
 
@@ -55,7 +57,11 @@ class FakeKubelet:
         self.node_name = node_name
         self.api = api
         self.plugins: Dict[str, _Plugin] = {}
-        self.allocated: Dict[str, Dict[str, Tuple[str, ...]]] = {}  # resource -> pod key -> ids
+        self.allocated: Dict[str, Dict[str, Tuple[str, ...]]] = {}  # resource -> pod key -> ids (every container's)
+        # resource -> pod key -> [(container, kind, ids)] in admission order (pod-resources reports these)
+        self.containers: Dict[str, Dict[str, List[Tuple[str, str, Tuple[str, ...]]]]] = {}
+        self.allocate_calls: List[Tuple[str, str, Tuple[str, ...]]] = []  # (pod key, container, ids) per Allocate RPC
+        self.preferred_calls: List[Tuple[List[str], int]] = []  # (must_include, size) per GetPreferredAllocation RPC
         self.responses: Dict[str, object] = {}  # pod key -> AllocateResponse
         self.rejected: List[Tuple[str, str]] = []  # (pod key, reason) of pods whose admission failed
         self._server: Optional[grpc.Server] = None
@@ -134,10 +140,19 @@ class FakeKubelet:
         self._server.start()
 
     def list_pod_resources(self):
-        """What the device manager recorded: pod -> resource -> device IDs (PodResourcesLister.List)."""
+        """What the device manager reports (PodResourcesLister.List): per app container and sidecar its
+        devices.  Regular init containers are not listed (they have exited), so a pod whose init
+        container held more devices than its app containers shows fewer devices than it holds."""
         with self._lock:
-            triples = [(key, res, list(ids)) for res, per in self.allocated.items() for key, ids in per.items()]
-        return build_response(triples)
+            rows = []
+            for res, per in self.allocated.items():
+                for key, ids in per.items():
+                    cs = self.containers.get(res, {}).get(key)
+                    if cs is None:
+                        rows.append((key, "main", res, list(ids)))
+                        continue
+                    rows += [(key, name, res, list(cids)) for name, kind, cids in cs if kind != "init"]
+        return build_response(rows)
 
     def stop(self) -> None:
         self._stop.set()
@@ -188,39 +203,79 @@ class FakeKubelet:
                 pass
         return AdmissionError(f"UnexpectedAdmissionError: {msg}")
 
-    def admit(self, pod: dict, resource: str, container_split: Optional[Sequence[int]] = None,
-              allocate_timeout: float = 10.0):
-        """Allocate devices for ``pod``: GetPreferredAllocation (if offered) then Allocate.  Any error
-        of either call, or too few devices, rejects the pod for good (:meth:`_reject`) as the kubelet's
-        device manager does; a missing device node or a failed PreStartContainer only fails the
-        container start (retried by the kubelet), so the pod stays Pending."""
+    def _devices_to_allocate(self, p: _Plugin, resource: str, required: int, in_use: set, reusable: List[str]) -> List[str]:
+        """``devicesToAllocate`` of the kubelet device manager for one container (no topology-manager
+        hint, the kubelet's default ``none`` policy): devices an init container of the pod handed on
+        come first; if they do not cover the request, the plugin's ``GetPreferredAllocation`` is asked
+        with ``available ∪ reused`` and ``must_include = reused`` for the container's full count, and
+        its answer ∩ available fills the rest (then the lowest free ids)."""
+        allocated: List[str] = []
+        for d in reusable:
+            if len(allocated) == required:
+                return allocated
+            allocated.append(d)
+        if len(allocated) == required:
+            return allocated
+        avail = [d for d in self.available(resource) if d not in in_use and d not in allocated]
+        needed = required - len(allocated)
+        if len(avail) < needed:
+            raise ValueError(f"requested number of devices unavailable for {resource}. Requested: {required}, "
+                             f"Available: {len(avail) + len(allocated)}")
+        if getattr(p.options, "get_preferred_allocation_available", False):
+            req = pb.PreferredAllocationRequest()
+            req.container_requests.add(available_deviceIDs=sorted(set(avail) | set(allocated), key=int),
+                                       must_include_deviceIDs=list(allocated), allocation_size=required)
+            self.preferred_calls.append((list(allocated), required))
+            pref = self._stub(p, "GetPreferredAllocation")(req, timeout=5)
+            for d in pref.container_responses[0].deviceIDs:
+                if d in avail and d not in allocated and len(allocated) < required:
+                    allocated.append(d)
+        for d in avail:
+            if len(allocated) == required:
+                break
+            if d not in allocated:
+                allocated.append(d)
+        return allocated
+
+    def admit(self, pod: dict, resource: str, allocate_timeout: float = 10.0):
+        """Admit ``pod`` the way the kubelet's device manager does (``ManagerImpl.Allocate``): once per
+        container that requests ``resource`` — init containers first, then the app containers — one
+        ``GetPreferredAllocation`` (when the plugin offers it and reused devices do not cover the
+        request) and one ``Allocate`` with that container's devices.  A regular init container's
+        devices are reused by the containers after it; a sidecar's are not.  Any error of either call,
+        or too few devices, rejects the pod for good (:meth:`_reject`); a missing device node or a
+        failed PreStartContainer only fails the container start (retried by the kubelet), so the pod
+        stays Pending.  Returns one AllocateResponse holding every container's response, in order."""
         key = pod_key(pod)
         p = self.plugins.get(resource)
-        k = pod_gpu_request(pod, [resource] + [r for r in self.plugins if r != resource])
-        if k == 0:
+        names = [resource] + [r for r in self.plugins if r != resource]
+        steps = pod_device_steps(pod, names)
+        if not steps:
             return None
         if p is None:
             raise self._reject(pod, f"no device plugin registered for {resource}")
         with self._lock:
-            avail = self.available(resource)
-            if len(avail) < k:
-                raise self._reject(pod, f"requested {k} of {resource}, available {len(avail)}")
-            chosen: List[str] = avail[:k]
+            reuse: List[str] = []  # devicesToReuse[pod]
+            pod_ids: List[str] = []  # every device the pod holds (the device manager's podDevices)
+            per_container: List[Tuple[str, str, Tuple[str, ...]]] = []
+            resp = pb.AllocateResponse()
             try:
-                if getattr(p.options, "get_preferred_allocation_available", False):
-                    req = pb.PreferredAllocationRequest()
-                    req.container_requests.add(available_deviceIDs=avail, allocation_size=k)
-                    pref = self._stub(p, "GetPreferredAllocation")(req, timeout=5)
-                    ids = list(pref.container_responses[0].deviceIDs)
-                    if len(ids) == k and set(ids) <= set(avail):
-                        chosen = ids
-                split = list(container_split or [k])
-                areq = pb.AllocateRequest()
-                pos = 0
-                for n in split:
-                    areq.container_requests.add(devices_ids=chosen[pos:pos + n])
-                    pos += n
-                resp = self._stub(p, "Allocate")(areq, timeout=allocate_timeout)
+                for cname, n, kind in steps:
+                    try:
+                        chosen = self._devices_to_allocate(p, resource, n, set(pod_ids), reuse)
+                    except ValueError as e:
+                        raise self._reject(pod, str(e)) from e
+                    areq = pb.AllocateRequest()
+                    areq.container_requests.add(devices_ids=chosen)
+                    self.allocate_calls.append((key, cname, tuple(chosen)))
+                    r = self._stub(p, "Allocate")(areq, timeout=allocate_timeout)
+                    resp.container_responses.extend(r.container_responses)
+                    pod_ids += [d for d in chosen if d not in pod_ids]
+                    per_container.append((cname, kind, tuple(chosen)))
+                    if kind == "init":
+                        reuse += [d for d in chosen if d not in reuse]
+                    else:  # an app container or a sidecar keeps what it got
+                        reuse = [d for d in reuse if d not in chosen]
             except grpc.RpcError as e:
                 raise self._reject(pod, f"device plugin call failed: {e.code()}: {e.details()}") from e
             # what containerd does next: every DeviceSpec must name a device node that exists on the
@@ -236,14 +291,13 @@ class FakeKubelet:
             if getattr(p.options, "pre_start_required", False):
                 # the kubelet calls PreStartContainer per container before starting it; an error
                 # there fails the container start
-                pos = 0
-                for n in split:
+                for _, _, ids in per_container:
                     try:
-                        self._stub(p, "PreStartContainer")(pb.PreStartContainerRequest(devices_ids=chosen[pos:pos + n]), timeout=300)
+                        self._stub(p, "PreStartContainer")(pb.PreStartContainerRequest(devices_ids=list(ids)), timeout=300)
                     except grpc.RpcError as e:
                         raise AdmissionError(f"PreStartContainer failed: {e.details()}") from e
-                    pos += n
-            self.allocated[resource][key] = tuple(chosen)
+            self.allocated[resource][key] = tuple(sorted(pod_ids, key=int))
+            self.containers.setdefault(resource, {})[key] = per_container
             self.responses[key] = resp
         if self.api is not None and hasattr(self.api, "set_pod_phase"):
             md = meta(pod)
@@ -278,3 +332,5 @@ class FakeKubelet:
         with self._lock:
             for res in self.allocated.values():
                 res.pop(key, None)
+            for per in self.containers.values():
+                per.pop(key, None)

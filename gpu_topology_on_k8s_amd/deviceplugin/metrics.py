@@ -49,6 +49,10 @@ class PluginMetrics:
                                           buckets=(0.5, 1, 2, 5, 10, 30, 60, 120), registry=r)
         self.reconciled = Counter("gtk_plugin_reconciled_pods_total",
                                   "pod GROUP annotations corrected to the kubelet's pod-resources truth", registry=r)
+        self.container_claims = Counter(
+            "gtk_plugin_container_claims_total",
+            "per-container Allocate calls of multi-container pods and mismatches, by how they matched a pod "
+            "(partial, final, resized, unannotated)", ["how"], registry=r)
         self.annotation_bytes = Gauge("gtk_plugin_topology_annotation_bytes", "encoded size of the published node annotations",
                                       registry=r)
 

@@ -16,9 +16,16 @@ Reference behaviour:
     placement core itself.
 
 Pod <-> Allocate association (the kubelet does not say which pod it is allocating for, SURVEY §7.3
-#4): pending pods on this node with ``ASSIGNED=false`` are matched by exact device set first, then
-by size with the oldest ``ASSUME_TIME`` (the design's implicit scheme); a pod scheduled around the
-extender (no GROUP) is annotated with what the kubelet gave it so the extender sees the usage.
+#4).  The kubelet's device manager calls ``GetPreferredAllocation`` and ``Allocate`` once per
+container, with that container's count, init containers first, and hands a regular init container's
+devices on to the containers after it.  A pending pod's containers (its spec) say which count its
+next call asks for, so a request of ``n`` devices is matched to the pod whose next container asks
+``n``: a pod whose admission is under way first, then the oldest ``ASSUME_TIME`` (the design's
+implicit scheme).  ``GetPreferredAllocation`` answers with the part of that pod's GROUP the container
+should get; ``Allocate`` records the devices against the GROUP and flips ``ASSIGNED=true`` once the
+whole GROUP has been allocated.  Devices outside the GROUP rewrite it to the kubelet's choice.  A pod
+scheduled around the extender (no GROUP) is annotated with what the kubelet gave its containers, so
+the extender sees the usage.
 """
 from __future__ import annotations
 
@@ -41,7 +48,7 @@ from ..k8s.annotations import (ANN_ASSIGNED, ANN_ASSUME_TIME, ANN_GROUP, Contrac
 from ..k8s.api import Conflict, KubeAPI
 from ..k8s.events import record_event
 from ..k8s.objects import annotations as obj_annotations
-from ..k8s.objects import meta, pod_gpu_request, pod_is_terminal, pod_phase
+from ..k8s.objects import meta, pod_device_steps, pod_gpu_request, pod_is_terminal, pod_phase
 from ..placement import NoFeasiblePlacement, PlacementPolicy
 from ..placement.core import select_with
 from ..topology.cpus import recommended_cpuset
@@ -204,6 +211,33 @@ class PluginConfig:
         return os.path.join(self.socket_dir, self.socket_name)
 
 
+class _Admission:
+    """A pod the kubelet is admitting: it calls ``Allocate`` once per container, so a
+    GROUP is claimed over several calls.  Kept in memory only while the pod is Pending."""
+
+    __slots__ = ("uid", "claimed", "done")
+
+    def __init__(self, uid: str) -> None:
+        self.uid = uid
+        self.claimed: set = set()  # devices its containers got so far
+        self.done = 0  # its Allocate calls so far (containers requesting devices, kubelet order)
+
+
+class _Candidate:
+    """A pending pod an ``Allocate`` / ``GetPreferredAllocation`` may be for."""
+
+    __slots__ = ("pod", "key", "pa", "steps", "adm")
+
+    def __init__(self, pod: dict, key: str, pa: Optional[PodAssignment], steps: List[Tuple[str, int, str]],
+                 adm: Optional[_Admission]) -> None:
+        self.pod, self.key, self.pa, self.steps, self.adm = pod, key, pa, steps, adm
+
+    def next_size(self) -> Optional[int]:
+        """Devices the pod's next container asks for (None: not known from its spec, or all done)."""
+        done = self.adm.done if self.adm is not None else 0
+        return self.steps[done][1] if done < len(self.steps) else None
+
+
 class AllocationHold:
     """State shared by a partition switch and the Allocate calls it holds (``allocation_hold``)."""
 
@@ -248,6 +282,7 @@ class DevicePluginServer:
         self._stale_layout = ""  # set when a switch changed the device layout: Allocate refuses until the restart
         self._guard_ready = False  # install_guard() put libgtk_vgpu.so into cfg.guard_dir
         self.allocations: List[Tuple[str, Tuple[int, ...]]] = []  # (pod key or "", ids) log
+        self._admissions: Dict[str, _Admission] = {}  # pod key -> admission in progress (under _alloc_lock)
         self.registered = 0
         self.metrics = PluginMetrics()
         self.metrics.set_topology(topology)
@@ -512,23 +547,51 @@ class DevicePluginServer:
             yield pb.ListAndWatchResponse(devices=devs)
 
     def GetPreferredAllocation(self, request, context):
+        """The kubelet asks once per container, with that container's count.  The answer
+        is the part of the extender's GROUP this container should get: the pod whose next container
+        asks for ``size`` devices (in-progress admissions first, then the oldest ASSUME_TIME), its
+        devices the kubelet still offers, and — when the container gets only part of the GROUP — the
+        best sub-placement of them that contains the devices an init container handed on
+        (``must_include``)."""
         resp = pb.PreferredAllocationResponse()
-        pending = self._pending_assumed()
+        with self._alloc_lock:  # the admission records are Allocate's
+            cands = self._admission_candidates()
         for creq in request.container_requests:
             avail = self._ids(context, creq.available_deviceIDs)
             must = self._ids(context, creq.must_include_deviceIDs)
             size = int(creq.allocation_size)
-            ids = None
-            for _, pa, _ in pending:
-                g = set(pa.group)
-                if len(g) == size and g <= set(avail) and set(must) <= g:
-                    ids = sorted(g)
-                    self.metrics.preferred.labels("annotation").inc()
-                    break
-            if ids is None:
+            ids = self._preferred_from_group(cands, size, avail, must)
+            if ids is not None:
+                self.metrics.preferred.labels("annotation").inc()
+            else:
                 ids = self._preferred_fallback(size, avail, must)
             resp.container_responses.add(deviceIDs=[str(i) for i in ids])
         return resp
+
+    def _preferred_from_group(self, cands: List["_Candidate"], size: int, avail: Sequence[int],
+                              must: Sequence[int]) -> Optional[List[int]]:
+        avail_s, must_s = set(avail), set(must)
+        for c in cands:
+            if c.pa is None:
+                continue
+            nxt = c.next_size()
+            g = set(c.pa.group)
+            free = g & avail_s
+            if not must_s <= g or len(free) < size:
+                continue
+            if nxt is None and len(free) != size:
+                continue  # no per-container request known: only a GROUP of exactly this size
+            if nxt is not None and nxt != size:
+                continue
+            if len(free) == size:
+                return sorted(free)
+            healthy = sorted(i for i in free if self._health.get(i, True))
+            try:
+                return sorted(select_with(self.topology, size, healthy, sorted(must_s), self.cfg.policy))
+            except (NoFeasiblePlacement, ValueError, AssertionError):
+                rest = [i for i in sorted(free, key=lambda i: (i not in healthy, i)) if i not in must_s]
+                return sorted(list(must_s) + rest[: size - len(must_s)])
+        return None
 
     def _preferred_fallback(self, size: int, avail: Sequence[int], must: Sequence[int]) -> List[int]:
         """No annotated pod matches: run the placement core over the healthy available devices.  A
@@ -605,11 +668,12 @@ class DevicePluginServer:
                 if self._probing:
                     log.warning("Allocate of %s: the link probe did not yield within %.0fs; allocating anyway",
                                 sorted(set(all_ids)), self.cfg.probe_yield_s)
-            pod = self._claim_pod(sorted(set(all_ids)))
-        extra_env = self._rccl_env(pod) if pod is not None else {}
-        for creq in request.container_requests:
+            # the kubelet sends one container per call; each container request is one step of its pod
+            pods = [self._claim_pod(sorted({int(x) for x in creq.devices_ids})) for creq in request.container_requests]
+        for creq, pod in zip(request.container_requests, pods):
             ids = [int(x) for x in creq.devices_ids]
-            resp.container_responses.append(self._container_response(ids, extra_env))
+            resp.container_responses.append(self._container_response(ids, self._rccl_env(pod) if pod is not None else {}))
+        pod = next((p for p in pods if p is not None), None)
         self.allocations.append((f"{meta(pod).get('namespace')}/{meta(pod).get('name')}" if pod else "", tuple(sorted(all_ids))))
         self.metrics.allocations.labels("ok").inc()
         self.metrics.allocated_devices.inc(len(all_ids))
@@ -650,11 +714,12 @@ class DevicePluginServer:
         return pb.PreStartContainerResponse()
 
     def _assigned_pod(self, ids: Sequence[int]) -> Optional[dict]:
-        """The live pod on this node whose confirmed GROUP is exactly ``ids`` (newest ASSUME_TIME)."""
+        """The live pod on this node whose confirmed GROUP holds ``ids`` (one container's devices;
+        newest ASSUME_TIME)."""
         best = None
         for p in self._node_pods():
             pa = PodAssignment.from_annotations(obj_annotations(p))
-            if pa is not None and pa.assigned and sorted(set(pa.group)) == list(ids):
+            if pa is not None and pa.assigned and set(ids) <= set(pa.group):
                 if best is None or pa.assume_time >= best[1]:
                     best = (p, pa.assume_time)
         return best[0] if best else None
@@ -928,47 +993,122 @@ class DevicePluginServer:
             log.warning("listing pods on %s failed: %s", self.cfg.node_name, e)
             return []
 
-    def _pending_assumed(self) -> List[Tuple[dict, PodAssignment, float]]:
-        out = []
+    def _admission_candidates(self) -> List["_Candidate"]:
+        """Pending pods on this node the kubelet may be allocating for, in the order a container's
+        request is matched against them: a pod whose admission is under way (some containers got
+        devices, the kubelet admits one pod at a time), then the oldest ASSUME_TIME (the design's
+        implicit rule), then pods scheduled around the extender (no GROUP) by creation time.  Pods
+        whose GROUP is confirmed and whose containers have all been allocated are not candidates.
+        Admission records of pods that left the Pending set are dropped here."""
+        names = self._resource_names()
+        out: List[_Candidate] = []
+        pending = set()
         for p in self._node_pods():
+            if pod_phase(p) != "Pending":
+                continue
+            md = meta(p)
+            key = f"{md.get('namespace', 'default')}/{md.get('name')}"
+            adm = self._admissions.get(key)
+            if adm is not None and adm.uid != md.get("uid", ""):
+                adm = None  # a new pod of the same name
             pa = PodAssignment.from_annotations(obj_annotations(p))
-            if pa is not None and not pa.assigned and pod_phase(p) == "Pending":
-                out.append((p, pa, float(pa.assume_time)))
-        out.sort(key=lambda x: (x[2], meta(x[0]).get("creationTimestamp", ""), meta(x[0]).get("name", "")))
+            try:
+                steps = pod_device_steps(p, names)
+            except ValueError:
+                steps = []
+            if pa is None and not steps:
+                continue
+            if adm is None and pa is not None and pa.assigned:
+                continue  # admitted before (or by a previous run of this plugin)
+            pending.add(key)
+            out.append(_Candidate(p, key, pa, steps, adm))
+        for key in [k for k in self._admissions if k not in pending]:
+            del self._admissions[key]
+        out.sort(key=lambda c: (c.adm is None or c.adm.done == 0, c.pa is None,
+                                float(c.pa.assume_time) if c.pa is not None else 0.0,
+                                meta(c.pod).get("creationTimestamp", ""), meta(c.pod).get("name", "")))
         return out
 
+    def _match(self, cands: List["_Candidate"], ids: List[int]) -> Tuple[Optional["_Candidate"], str]:
+        """The candidate one container's devices are for, and how it matched: ``group`` (inside its
+        GROUP), ``resized`` (its next container asks this many, the kubelet chose other devices) or
+        ``unannotated`` (scheduled around the extender)."""
+        ids_s, n = set(ids), len(ids)
+        for c in cands:  # devices of its GROUP, for a container of this size
+            nxt = c.next_size()
+            if c.pa is not None and ids_s <= set(c.pa.group) and (nxt == n or (nxt is None and c.adm is None)):
+                return c, "group"
+        for c in cands:  # the kubelet chose outside every GROUP: the pod whose next container asks n
+            nxt = c.next_size()
+            if c.pa is not None and (nxt == n or (nxt is None and len(set(c.pa.group)) == n and c.adm is None)):
+                return c, "resized"
+        for c in cands:
+            if c.pa is None and c.next_size() == n:
+                return c, "unannotated"
+        return None, ""
+
     def _claim_pod(self, ids: List[int]) -> Optional[dict]:
-        """Find the pod these devices are for and flip it to ASSIGNED=true (conditional patch)."""
+        """One container's ``Allocate``: find the pod the devices are for, record them against its
+        GROUP, and flip it to ASSIGNED=true (conditional patch) once every device of the GROUP has been
+        allocated — with one ``Allocate`` per container (the real kubelet), a pod is claimed over
+        several calls.  A container reusing its init container's devices matches the same pod.  When
+        the kubelet chose devices outside the GROUP, the GROUP is rewritten to what it chose (the
+        extender's view must be the kubelet's truth).  -> the pod (for its RCCL env)."""
         if self.api is None or not self.cfg.node_name:
             return None
         for attempt in range(5):
-            cands = self._pending_assumed()
-            exact = [c for c in cands if sorted(set(c[1].group)) == ids]
-            sized = [c for c in cands if len(set(c[1].group)) == len(ids)]
-            pod: Optional[dict] = None
-            if exact:
-                pod = exact[0][0]
-            elif sized:
-                pod = sized[0][0]  # oldest ASSUME_TIME with the same count (design's implicit rule)
-                log.warning("kubelet allocated %s but pod %s was assumed %s; recording what the kubelet chose",
-                            ids, meta(pod).get("name"), sized[0][1].group)
-            else:
-                pod = self._unannotated_pod(len(ids))
-                if pod is None:
-                    log.warning("no pending pod on %s matches allocation %s", self.cfg.node_name, ids)
-                    return None
+            cands = self._admission_candidates()
+            c, how = self._match(cands, ids)
+            if c is None:
+                log.warning("no pending pod on %s matches allocation %s", self.cfg.node_name, ids)
+                return None
+            md = meta(c.pod)
+            adm = c.adm if c.adm is not None else _Admission(md.get("uid", ""))
+            claimed = adm.claimed | set(ids)
+            done = adm.done + 1
+            finished = done >= len(c.steps)
             now = int(self.clock())
-            ann = {ANN_GROUP: format_group(ids), ANN_ASSIGNED: "true", ANN_ASSUME_TIME: str(now)}
-            md = meta(pod)
-            try:
-                return self.api.patch_pod_annotations(md.get("namespace", "default"), md["name"], ann,
-                                                      resource_version=md.get("resourceVersion"))
-            except Conflict:
-                continue  # someone else touched the pod: re-read and retry
-            except Exception as e:
-                log.warning("flipping %s/%s to ASSIGNED=true failed: %s", md.get("namespace"), md.get("name"), e)
-                return pod
+            ann: Dict[str, Optional[str]] = {}
+            if how == "unannotated":
+                if finished or len(claimed) >= self._pod_request(c.pod):
+                    ann = {ANN_GROUP: format_group(sorted(claimed)), ANN_ASSIGNED: "true", ANN_ASSUME_TIME: str(now)}
+            else:
+                group = set(c.pa.group)
+                if how == "resized" or not set(ids) <= group:
+                    extra = set(ids) - group
+                    spare = sorted(group - claimed, reverse=True)  # GROUP devices no container got yet
+                    group = (group - set(spare[:len(extra)])) | claimed
+                    log.warning("kubelet allocated %s but pod %s was assumed %s; recording what the kubelet chose",
+                                ids, md.get("name"), c.pa.group)
+                complete = claimed >= group
+                if sorted(group) != sorted(set(c.pa.group)) or (complete and not c.pa.assigned):
+                    ann = {ANN_GROUP: format_group(sorted(group)), ANN_ASSIGNED: "true" if complete else "false"}
+                    if complete:
+                        ann[ANN_ASSUME_TIME] = str(now)
+            pod = c.pod
+            if ann:
+                try:
+                    pod = self.api.patch_pod_annotations(md.get("namespace", "default"), md["name"], ann,
+                                                         resource_version=md.get("resourceVersion"))
+                except Conflict:
+                    continue  # someone else touched the pod: re-read and retry
+                except Exception as e:  # noqa: BLE001 - the reconcile pass repairs it
+                    log.warning("recording allocation %s on %s/%s failed: %s", ids, md.get("namespace"), md.get("name"), e)
+            adm.claimed, adm.done = claimed, done
+            if finished:
+                self._admissions.pop(c.key, None)
+            else:
+                self._admissions[c.key] = adm
+            if how != "group" or not finished or len(c.steps) > 1:
+                self.metrics.container_claims.labels(how if how != "group" else ("final" if finished else "partial")).inc()
+            return pod
         return None
+
+    def _pod_request(self, pod: dict) -> int:
+        try:
+            return pod_gpu_request(pod, self._resource_names())
+        except ValueError:
+            return 0
 
     def reconcile(self) -> int:
         """Make every GPU pod's ``ALIYUN_COM_GPU_GROUP`` on this node equal the devices the kubelet
@@ -985,15 +1125,36 @@ class DevicePluginServer:
             return 0
         names = self._resource_names()
         fixed = 0
-        for p in self._node_pods():
+        pods = self._node_pods()
+        reported = {}
+        for p in pods:
             md = meta(p)
             key = f"{md.get('namespace', 'default')}/{md.get('name')}"
-            ids = sorted({int(i) for r in names for i in truth.get(key, {}).get(r, []) if str(i).isdigit()})
+            reported[key] = {int(i) for r in names for i in truth.get(key, {}).get(r, []) if str(i).isdigit()}
+        for p in pods:
+            md = meta(p)
+            key = f"{md.get('namespace', 'default')}/{md.get('name')}"
+            ids = sorted(reported[key])
             if not ids:
                 continue  # not admitted yet (or not ours)
             pa = PodAssignment.from_annotations(obj_annotations(p))
-            if pa is not None and pa.assigned and sorted(set(pa.group)) == ids:
-                continue
+            group = set(pa.group) if pa is not None else set()
+            if pa is not None and set(ids) <= group:
+                # pod-resources lists app containers and sidecars, not init containers that have exited:
+                # a GROUP larger than the listed devices holds the init devices the kubelet still counts
+                # as the pod's, and is kept.  An unconfirmed GROUP is confirmed once the listed devices
+                # are all of it or the pod runs (all its containers were allocated)
+                if pa.assigned or (set(ids) != group and pod_phase(p) != "Running"):
+                    continue
+                ids = sorted(group)
+            elif pa is not None:
+                # devices outside the GROUP: the kubelet's are the truth; GROUP devices no other pod
+                # reports may be this pod's init devices and are kept, up to the pod's request
+                others = set().union(*(v for k, v in reported.items() if k != key))
+                keep = sorted(group - set(ids) - others)
+                ids = sorted(set(ids) | set(keep[:max(0, self._pod_request(p) - len(ids))]))
+                if pa.assigned and ids == sorted(group):
+                    continue
             ann = {ANN_GROUP: format_group(ids), ANN_ASSIGNED: "true"}
             if pa is None:
                 ann[ANN_ASSUME_TIME] = str(int(self.clock()))
@@ -1010,20 +1171,6 @@ class DevicePluginServer:
                          f"GROUP {format_group(pa.group) if pa else '-'} -> {format_group(ids)} (kubelet pod-resources)",
                          "Normal", component="gpu-topology-device-plugin", host=self.cfg.node_name)
         return fixed
-
-    def _unannotated_pod(self, k: int) -> Optional[dict]:
-        names = self._resource_names()
-        cands = []
-        for p in self._node_pods():
-            if PodAssignment.from_annotations(obj_annotations(p)) is not None or pod_phase(p) != "Pending":
-                continue
-            try:
-                if pod_gpu_request(p, names) == k:
-                    cands.append(p)
-            except ValueError:
-                continue
-        cands.sort(key=lambda p: (meta(p).get("creationTimestamp", ""), meta(p).get("name", "")))
-        return cands[0] if cands else None
 
     # ------------------------------------------------------------------ lifecycle
     def _handlers(self):

@@ -79,18 +79,23 @@ def list_pod_resources(socket_path: str = POD_RESOURCES_SOCKET, timeout: float =
     return out
 
 
-def build_response(allocations: Iterable[Tuple[str, str, List[str]]]) -> "ListPodResourcesResponse":
-    """``(pod key, resource, device ids)`` triples -> a List response (one container per pod)."""
+def build_response(allocations: Iterable[Tuple]) -> "ListPodResourcesResponse":
+    """``(pod key, container, resource, device ids)`` rows (or ``(pod key, resource, ids)``, one
+    container named ``main``) -> a List response."""
     resp = ListPodResourcesResponse()
     pods: Dict[str, object] = {}
-    for key, resource, ids in allocations:
+    conts: Dict[Tuple[str, str], object] = {}
+    for row in allocations:
+        key, cname, resource, ids = row if len(row) == 4 else (row[0], "main", row[1], row[2])
         pr = pods.get(key)
         if pr is None:
             ns, name = key.split("/", 1)
             pr = resp.pod_resources.add(name=name, namespace=ns)
-            pr.containers.add(name="main")
             pods[key] = pr
-        pr.containers[0].devices.add(resource_name=resource, device_ids=list(ids))
+        c = conts.get((key, cname))
+        if c is None:
+            c = conts[(key, cname)] = pr.containers.add(name=cname)
+        c.devices.add(resource_name=resource, device_ids=list(ids))
     return resp
 
 

@@ -14,7 +14,32 @@ from gpu_topology_on_k8s_amd.sim import SimCluster
 from gpu_topology_on_k8s_amd.topology import fixtures as fx
 
 
-def _check(c, live, request):
+def _annotation_mismatches(c, live):
+    out = []
+    for key, node in live.items():
+        ns, name = key.split("/")
+        kub = c.nodes[node].kubelet.allocated[c.nodes[node].resource].get(key) or ()
+        a = PodAssignment.from_annotations(obj_annotations(c.api.get_pod(ns, name)))
+        if a is None or not a.assigned or sorted(a.group) != sorted(int(i) for i in kub):
+            out.append((key, a, kub))
+    return out
+
+
+def _shape(rng, k):
+    """Pod shape for a k-device request: one container, several app containers, or an init container
+    (smaller or as large as the pod) in front — each Allocate'd per container by the fake kubelet."""
+    r = rng.random()
+    if k < 2 or r < 0.4:
+        return {}
+    if r < 0.75:
+        cut = rng.randint(1, k - 1)
+        return {"split": [cut, k - cut]}
+    return {"split": [k], "init": [rng.randint(1, k)]}
+
+
+def _check(c, live, request, strict=False):
+    if strict:  # sequential admissions: Allocate alone must keep GROUP == the kubelet's allocation
+        assert not _annotation_mismatches(c, live)
     c.reconcile()  # the plugins' periodic pass (kubelet pod-resources -> GROUP annotations), run now
     per_node = {}
     for key, node in live.items():
@@ -36,16 +61,21 @@ def _check(c, live, request):
 def test_random_churn_keeps_allocations_consistent(seed, informer):
     rng = random.Random(seed)
     with SimCluster({f"n{i}": fx.f7_mi355x() for i in range(3)}, informer=informer) as c:
-        live, request, nxt = {}, {}, 0
+        live, request, nxt, multi = {}, {}, 0, 0
         for _ in range(36):
             op = rng.random()
+            strict = True
             if op < 0.55:
                 for _ in range(rng.randint(1, 3)):
                     k = rng.choice([1, 1, 2, 2, 4, 8])
-                    c.submit(f"p{nxt}", k)
+                    shape = _shape(rng, k)
+                    c.submit(f"p{nxt}", 0 if shape else k, **shape)
                     request[f"default/p{nxt}"] = k
+                    multi += bool(shape)
                     nxt += 1
-                for r in c.schedule_pending(concurrent=rng.random() < 0.5):
+                concurrent = rng.random() < 0.5
+                strict = not concurrent  # concurrent binds + admissions may swap same-size pods
+                for r in c.schedule_pending(concurrent=concurrent):
                     if r.node and r.allocated:
                         live[r.pod] = r.node
             elif op < 0.8 and live:
@@ -64,7 +94,8 @@ def test_random_churn_keeps_allocations_consistent(seed, informer):
                 n.kubelet.wait_for(c.resource)
             else:
                 c.api.inject("bind_pod", 500, times=1)
-            _check(c, live, request)
+            _check(c, live, request, strict=strict)
+        assert multi > 0  # multi-container / init-container pods really were in the mix
         # drain: everything finishes, every node is empty again
         for key in sorted(live):
             c.complete(key.split("/")[1])

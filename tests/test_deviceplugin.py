@@ -149,9 +149,12 @@ def test_multi_container_pod(node):
     pod = api.create_pod(pod)
     d = ext.bind("default", "mc", pod["metadata"]["uid"], "n1")
     assert len(d.ids) == 4
-    resp = kubelet.admit(api.get_pod("default", "mc"), RES, container_split=[2, 2])
+    resp = kubelet.admit(api.get_pod("default", "mc"), RES)  # one GetPreferredAllocation + Allocate per container
     assert len(resp.container_responses) == 2
-    assert PodAssignment.from_annotations(api.get_pod("default", "mc")["metadata"]["annotations"]).assigned
+    assert [len(ids) for _, _, ids in kubelet.allocate_calls] == [2, 2]
+    pa = PodAssignment.from_annotations(api.get_pod("default", "mc")["metadata"]["annotations"])
+    assert pa.assigned and sorted(pa.group) == sorted(d.ids)
+    assert sorted(int(i) for i in kubelet.allocated[RES]["default/mc"]) == sorted(d.ids)
 
 
 def test_rccl_env_passthrough(node):

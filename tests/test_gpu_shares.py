@@ -128,6 +128,45 @@ def test_cu_masked_shares_split_the_compute_units():
         assert together[n] > 0.8 * alone[n], (n, together, alone)
 
 
+def test_two_container_pod_one_slice_each_on_a_time_sliced_node():
+    """a real node advertised as 2 time slices per GPU admits a pod of two
+    containers asking one slice each through the in-process flow — the kubelet calls
+    GetPreferredAllocation + Allocate per container — with the pod-resources reconcile off.  The pod
+    gets exactly its GROUP (ASSIGNED flips on the second container), each container one slice with its
+    own half of the CUs, and both containers then run MFMA work on the GPU under their masks."""
+    from gpu_topology_on_k8s_amd.k8s import PodAssignment
+    from gpu_topology_on_k8s_amd.k8s.objects import annotations as obj_annotations
+    from gpu_topology_on_k8s_amd.sim import SimCluster
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
+    from gpu_topology_on_k8s_amd.topology.shares import time_slice
+
+    t = discover("auto")
+    t.node_name = "gpu-node"
+    v = time_slice(t, 2)
+    with SimCluster({"gpu-node": v}, reconcile_interval=0.0) as c:
+        c.submit("two-containers", 0, split=[1, 1], slices=True)
+        (r,) = c.schedule_pending()
+        assert r.error == "" and len(r.devices) == 2, r
+        kub = c.nodes["gpu-node"].kubelet
+        res = c.nodes["gpu-node"].resource
+        calls = [ids for key, _, ids in kub.allocate_calls if key == "default/two-containers"]
+        assert [len(ids) for ids in calls] == [1, 1] and sorted(int(i) for ids in calls for i in ids) == sorted(r.devices)
+        pa = PodAssignment.from_annotations(obj_annotations(c.api.get_pod("default", "two-containers")))
+        assert pa.assigned and sorted(pa.group) == sorted(r.devices)
+        assert sorted(int(i) for i in kub.allocated[res]["default/two-containers"]) == sorted(r.devices)
+        envs = [dict(cr.envs) for cr in kub.responses["default/two-containers"].container_responses]
+    masks = [e["HSA_CU_MASK"] for e in envs]
+    cus = t.gpus[0].cus if t.gpus[0].cus > 0 else 256
+    if len({int(i) // 2 for i in r.devices}) == 1:  # both slices of one GPU: disjoint halves of its CUs
+        assert sorted(masks) == sorted([f"0:0-{cus // 2 - 1}", f"0:{cus // 2}-{cus - 1}"]), masks
+    assert [e["GTK_GPU_FRACTION"] for e in envs] == ["0.5", "0.5"]
+    base = {k: v for k, v in os.environ.items() if k not in _STRIP and k != "HSA_CU_MASK"}
+    procs = [_mfma_rate(dict(base, HSA_CU_MASK=m), ms=500.0) for m in masks]
+    rates = [_rate(p) for p in procs]
+    print(json.dumps({"two_container_masks": masks, "concurrent_tflops": [round(x) for x in rates]}))
+    assert all(x > 100 for x in rates), rates
+
+
 _CENSUS = r"""
 import json
 from gpu_topology_on_k8s_amd._native import load

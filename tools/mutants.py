@@ -73,22 +73,25 @@ MUTANTS: List[Mutant] = [
            "                    if True:  # a LIST started after the bind: authoritative from now on", equivalent=True,
            why="a LIST that shows the pod carries its annotation: dropping the overlay entry early loses nothing"),
     # device plugin
-    Mutant("plugin", PLUGIN, "            exact = [c for c in cands if sorted(set(c[1].group)) == ids]", "            exact = []"),
-    Mutant("plugin", PLUGIN, 'return self.api.patch_pod_annotations(md.get("namespace", "default"), md["name"], ann,\n'
-                             '                                                      resource_version=md.get("resourceVersion"))',
-           'return self.api.patch_pod_annotations(md.get("namespace", "default"), md["name"], ann,\n'
-           '                                                      resource_version=None)'),
-    Mutant("plugin", PLUGIN, "            if pa is not None and pa.assigned and sorted(set(pa.group)) == ids:",
-           "            if pa is not None and pa.assigned:"),
-    Mutant("plugin", PLUGIN, "                if len(g) == size and g <= set(avail) and set(must) <= g:", "                if len(g) == size:"),
+    Mutant("plugin", PLUGIN,
+           "            if c.pa is not None and ids_s <= set(c.pa.group) and (nxt == n or (nxt is None and c.adm is None)):",
+           "            if c.pa is not None and (nxt == n or (nxt is None and c.adm is None)):"),
+    Mutant("plugin", PLUGIN, 'pod = self.api.patch_pod_annotations(md.get("namespace", "default"), md["name"], ann,\n'
+                             '                                                         resource_version=md.get("resourceVersion"))',
+           'pod = self.api.patch_pod_annotations(md.get("namespace", "default"), md["name"], ann,\n'
+           '                                                         resource_version=None)'),
+    Mutant("plugin", PLUGIN, "            if pa is not None and set(ids) <= group:", "            if pa is not None and set(ids) == group:"),
+    Mutant("plugin", PLUGIN, "            if nxt is not None and nxt != size:", "            if False:"),
+    Mutant("plugin", PLUGIN, "        out.sort(key=lambda c: (c.adm is None or c.adm.done == 0, c.pa is None,",
+           "        out.sort(key=lambda c: (False, c.pa is None,"),
     Mutant("plugin", PLUGIN, "        healthy = [a for a in avail if 0 <= a < self.topology.n and self._health.get(a, True)]",
            "        healthy = [a for a in avail if 0 <= a < self.topology.n]"),
     Mutant("plugin", PLUGIN, "            unhealthy = [i for i in ids if not self._health.get(i, True)]", "            unhealthy = []"),
     Mutant("plugin", PLUGIN, "            if not ids:\n                continue  # not admitted yet (or not ours)",
            "            if False:\n                continue  # not admitted yet (or not ours)"),
     Mutant("plugin", PLUGIN, "                ann[ANN_ASSUME_TIME] = str(int(self.clock()))", "                pass"),
-    Mutant("plugin", PLUGIN, "            if PodAssignment.from_annotations(obj_annotations(p)) is not None or pod_phase(p) != \"Pending\":",
-           "            if PodAssignment.from_annotations(obj_annotations(p)) is not None:"),
+    Mutant("plugin", PLUGIN, '            if pod_phase(p) != "Pending":\n                continue\n            md = meta(p)',
+           '            if False:\n                continue\n            md = meta(p)'),
     # data-parallel reduction
     Mutant("dp", DP, "        return b.start + self.rank * c, b.start + (self.rank + 1) * c", "        return b.start, b.start + c"),
     Mutant("dp", DP, "                if b.work is None:\n                    self._launch(b)", "                if False:\n                    self._launch(b)"),
@@ -147,7 +150,8 @@ TESTS = {
     "cache": ["tests/test_cluster_features.py", "tests/test_extender.py", "tests/test_extender_ledger.py", "tests/test_churn.py"],
     "plugin": ["tests/test_deviceplugin.py", "tests/test_cluster_features.py", "tests/test_preferred_allocation_props.py",
                "tests/test_daemons.py", "tests/test_health.py", "tests/test_sim.py", "tests/test_churn.py",
-               "tests/test_reprobe_admission.py", "tests/test_partition.py", "tests/test_shares.py"],
+               "tests/test_reprobe_admission.py", "tests/test_partition.py", "tests/test_shares.py",
+               "tests/test_multicontainer.py"],
     "dp": ["tests/test_dp_check.py", "tests/test_llama_dp_cpu.py", "tests/test_checkpoint.py"],
     "guard": ["tests/test_vgpu_guard.py"],
     "banding": ["tests/test_probe_banding.py", "tests/test_probe_checks.py"],
