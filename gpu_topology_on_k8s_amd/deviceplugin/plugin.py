@@ -145,7 +145,7 @@ class PluginConfig:
                  cdi_dir: str = "/var/run/cdi", cdi_kind: str = "amd.com/gpu", nic_env: bool = True,
                  share_cu_mask: bool = True, probe_mark_s: float = 300.0, probe_settle_s: float = 2.0,
                  probe_yield_s: float = 20.0, share_guard: str = "off", guard_dir: str = "/var/lib/gtk-vgpu",
-                 guard_lib: Optional[str] = None):
+                 guard_lib: Optional[str] = None, admission_settle_s: float = 5.0):
         self.resource_name = resource_name
         self.socket_dir = socket_dir
         self.socket_name = socket_name
@@ -205,6 +205,9 @@ class PluginConfig:
         # annotations are corrected to the kubelet's pod-resources API (None / "" = off)
         self.pod_resources_socket = pod_resources_socket or ""
         self.reconcile_interval = reconcile_interval
+        # the kubelet allocates a pod container by container, back to back: a Pending pod is reconciled
+        # only once no Allocate has come for this long (its calls may still be under way)
+        self.admission_settle_s = admission_settle_s
 
     @property
     def socket_path(self) -> str:
@@ -213,12 +216,12 @@ class PluginConfig:
 
 class _Admission:
     """A pod the kubelet is admitting: it calls ``Allocate`` once per container, so a
-    GROUP is claimed over several calls.  Kept in memory only while the pod is Pending."""
+    GROUP is claimed over several calls.  In memory only, while the pod is Pending."""
 
-    __slots__ = ("uid", "claimed", "done")
+    __slots__ = ("key", "uid", "claimed", "done")
 
-    def __init__(self, uid: str) -> None:
-        self.uid = uid
+    def __init__(self, key: str, uid: str) -> None:
+        self.key, self.uid = key, uid
         self.claimed: set = set()  # devices its containers got so far
         self.done = 0  # its Allocate calls so far (containers requesting devices, kubelet order)
 
@@ -283,6 +286,12 @@ class DevicePluginServer:
         self._guard_ready = False  # install_guard() put libgtk_vgpu.so into cfg.guard_dir
         self.allocations: List[Tuple[str, Tuple[int, ...]]] = []  # (pod key or "", ids) log
         self._admissions: Dict[str, _Admission] = {}  # pod key -> admission in progress (under _alloc_lock)
+        # admission units: the devices of consecutive Allocate calls linked by reuse (an init container's
+        # devices handed on), i.e. of one kubelet pod admission whichever pod the calls were matched to
+        self._unit_of: Dict[int, set] = {}  # device -> its unit (from the latest call that allocated it)
+        self._chain: Optional[Tuple[set, Optional[_Admission]]] = None  # the previous call's unit and record
+        self._last_alloc = -1e9  # monotonic time the last Allocate ended
+        self._claimed_by: Optional[_Admission] = None  # the record _claim_pod matched the current call to
         self.registered = 0
         self.metrics = PluginMetrics()
         self.metrics.set_topology(topology)
@@ -555,12 +564,12 @@ class DevicePluginServer:
         (``must_include``)."""
         resp = pb.PreferredAllocationResponse()
         with self._alloc_lock:  # the admission records are Allocate's
-            cands = self._admission_candidates()
+            cands, live = self._admission_view()
         for creq in request.container_requests:
             avail = self._ids(context, creq.available_deviceIDs)
             must = self._ids(context, creq.must_include_deviceIDs)
             size = int(creq.allocation_size)
-            ids = self._preferred_from_group(cands, size, avail, must)
+            ids = self._preferred_from_group(cands, live, size, avail, must)
             if ids is not None:
                 self.metrics.preferred.labels("annotation").inc()
             else:
@@ -568,30 +577,42 @@ class DevicePluginServer:
             resp.container_responses.add(deviceIDs=[str(i) for i in ids])
         return resp
 
-    def _preferred_from_group(self, cands: List["_Candidate"], size: int, avail: Sequence[int],
+    def _preferred_from_group(self, cands: List["_Candidate"], live: Dict[str, dict], size: int, avail: Sequence[int],
                               must: Sequence[int]) -> Optional[List[int]]:
         avail_s, must_s = set(avail), set(must)
+        rec = self._reuse(must) if must_s else None
+        if rec is not None and rec.key in live:  # reused devices: the pod of the previous call
+            pa = PodAssignment.from_annotations(obj_annotations(live[rec.key]))
+            pick = self._pick_part(set(pa.group) | rec.claimed, size, avail_s, must_s) if pa is not None else None
+            if pick is not None:
+                return pick
         for c in cands:
             if c.pa is None:
                 continue
             nxt = c.next_size()
-            g = set(c.pa.group)
-            free = g & avail_s
-            if not must_s <= g or len(free) < size:
-                continue
-            if nxt is None and len(free) != size:
+            if nxt is None and len(set(c.pa.group) & avail_s) != size:
                 continue  # no per-container request known: only a GROUP of exactly this size
             if nxt is not None and nxt != size:
                 continue
-            if len(free) == size:
-                return sorted(free)
-            healthy = sorted(i for i in free if self._health.get(i, True))
-            try:
-                return sorted(select_with(self.topology, size, healthy, sorted(must_s), self.cfg.policy))
-            except (NoFeasiblePlacement, ValueError, AssertionError):
-                rest = [i for i in sorted(free, key=lambda i: (i not in healthy, i)) if i not in must_s]
-                return sorted(list(must_s) + rest[: size - len(must_s)])
+            pick = self._pick_part(set(c.pa.group), size, avail_s, must_s)
+            if pick is not None:
+                return pick
         return None
+
+    def _pick_part(self, g: set, size: int, avail_s: set, must_s: set) -> Optional[List[int]]:
+        """``size`` devices of GROUP ``g`` the kubelet offers, ``must_s`` among them: all of them, or
+        the best sub-placement when the container gets only part of the GROUP.  None if they do not fit."""
+        free = g & avail_s
+        if not must_s <= g or len(free) < size:
+            return None
+        if len(free) == size:
+            return sorted(free)
+        healthy = sorted(i for i in free if self._health.get(i, True))
+        try:
+            return sorted(select_with(self.topology, size, healthy, sorted(must_s), self.cfg.policy))
+        except (NoFeasiblePlacement, ValueError, AssertionError):
+            rest = [i for i in sorted(free, key=lambda i: (i not in healthy, i)) if i not in must_s]
+            return sorted(list(must_s) + rest[: size - len(must_s)])
 
     def _preferred_fallback(self, size: int, avail: Sequence[int], must: Sequence[int]) -> List[int]:
         """No annotated pod matches: run the placement core over the healthy available devices.  A
@@ -669,7 +690,13 @@ class DevicePluginServer:
                     log.warning("Allocate of %s: the link probe did not yield within %.0fs; allocating anyway",
                                 sorted(set(all_ids)), self.cfg.probe_yield_s)
             # the kubelet sends one container per call; each container request is one step of its pod
-            pods = [self._claim_pod(sorted({int(x) for x in creq.devices_ids})) for creq in request.container_requests]
+            pods = []
+            for creq in request.container_requests:
+                ids = sorted({int(x) for x in creq.devices_ids})
+                self._claimed_by = None
+                pods.append(self._claim_pod(ids))
+                self._link(ids, self._claimed_by)
+            self._last_alloc = time.monotonic()
         for creq, pod in zip(request.container_requests, pods):
             ids = [int(x) for x in creq.devices_ids]
             resp.container_responses.append(self._container_response(ids, self._rccl_env(pod) if pod is not None else {}))
@@ -993,25 +1020,31 @@ class DevicePluginServer:
             log.warning("listing pods on %s failed: %s", self.cfg.node_name, e)
             return []
 
-    def _admission_candidates(self) -> List["_Candidate"]:
-        """Pending pods on this node the kubelet may be allocating for, in the order a container's
-        request is matched against them: a pod whose admission is under way (some containers got
-        devices, the kubelet admits one pod at a time), then the oldest ASSUME_TIME (the design's
-        implicit rule), then pods scheduled around the extender (no GROUP) by creation time.  Pods
-        whose GROUP is confirmed and whose containers have all been allocated are not candidates.
-        Admission records of pods that left the Pending set are dropped here."""
+    def _admission_view(self) -> Tuple[List["_Candidate"], Dict[str, dict]]:
+        """(candidates, live pods by key).  Candidates are the pending pods on this node the kubelet
+        may be allocating for, in the order a container's request is matched against them: a pod whose
+        admission is under way (some containers got devices; the kubelet admits one pod at a time),
+        then the oldest ASSUME_TIME (the design's implicit rule), then pods scheduled around the
+        extender (no GROUP) by creation time.  Pods whose GROUP is confirmed and whose containers have
+        all been allocated are not candidates.  Live pods are the node's pods that may hold devices
+        (not terminal, not being deleted).  Records of pods that are gone are dropped here."""
         names = self._resource_names()
         out: List[_Candidate] = []
-        pending = set()
+        live: Dict[str, dict] = {}
         for p in self._node_pods():
-            if pod_phase(p) != "Pending":
-                continue
             md = meta(p)
             key = f"{md.get('namespace', 'default')}/{md.get('name')}"
+            if not md.get("deletionTimestamp"):
+                live[key] = p
+            pa = PodAssignment.from_annotations(obj_annotations(p))
+            if pod_phase(p) != "Pending" and (pa is None or pa.assigned):
+                # started: its containers have their devices.  A started pod whose GROUP was never
+                # claimed stays a candidate: the kubelet admitted it with another pod's devices (out of
+                # order), so its GROUP is what the other pod's containers will be given
+                continue
             adm = self._admissions.get(key)
             if adm is not None and adm.uid != md.get("uid", ""):
                 adm = None  # a new pod of the same name
-            pa = PodAssignment.from_annotations(obj_annotations(p))
             try:
                 steps = pod_device_steps(p, names)
             except ValueError:
@@ -1020,14 +1053,41 @@ class DevicePluginServer:
                 continue
             if adm is None and pa is not None and pa.assigned:
                 continue  # admitted before (or by a previous run of this plugin)
-            pending.add(key)
             out.append(_Candidate(p, key, pa, steps, adm))
+        pending = {c.key for c in out}
         for key in [k for k in self._admissions if k not in pending]:
             del self._admissions[key]
+        if self._chain is not None:
+            # the kubelet frees a pod's devices only when the pod ends: while the pod the previous call
+            # was matched to lives, a later call holding its devices is a reuse.  Once that pod ended (or
+            # calls stopped coming) they may have been freed and handed to another pod, which is no reuse
+            rec = self._chain[1]
+            pod = live.get(rec.key) if rec is not None else None
+            over = (time.monotonic() - self._last_alloc > self.cfg.admission_settle_s
+                    or (rec is not None and (pod is None or meta(pod).get("uid", "") != rec.uid)))
+            if over:
+                self._chain = None
         out.sort(key=lambda c: (c.adm is None or c.adm.done == 0, c.pa is None,
                                 float(c.pa.assume_time) if c.pa is not None else 0.0,
                                 meta(c.pod).get("creationTimestamp", ""), meta(c.pod).get("name", "")))
-        return out
+        return out, live
+
+    def _reuse(self, ids: Sequence[int]) -> Optional[_Admission]:
+        """The record of the previous Allocate when ``ids`` reuse some of its unit's devices.  The
+        kubelet admits one pod at a time and hands a regular init container's devices only to the
+        later containers of the same pod, so such a call continues the previous call's admission —
+        whichever pod that call was matched to."""
+        if self._chain is None or not self._chain[0] & {int(d) for d in ids}:
+            return None
+        return self._chain[1]
+
+    def _link(self, ids: Sequence[int], adm: Optional[_Admission]) -> None:
+        """Record one Allocate call in the admission units (see ``_unit_of``)."""
+        ids_s = {int(d) for d in ids}
+        unit = self._chain[0] | ids_s if self._chain is not None and self._chain[0] & ids_s else set(ids_s)
+        for d in unit:
+            self._unit_of[d] = unit
+        self._chain = (unit, adm)
 
     def _match(self, cands: List["_Candidate"], ids: List[int]) -> Tuple[Optional["_Candidate"], str]:
         """The candidate one container's devices are for, and how it matched: ``group`` (inside its
@@ -1051,41 +1111,49 @@ class DevicePluginServer:
         """One container's ``Allocate``: find the pod the devices are for, record them against its
         GROUP, and flip it to ASSIGNED=true (conditional patch) once every device of the GROUP has been
         allocated — with one ``Allocate`` per container (the real kubelet), a pod is claimed over
-        several calls.  A container reusing its init container's devices matches the same pod.  When
-        the kubelet chose devices outside the GROUP, the GROUP is rewritten to what it chose (the
-        extender's view must be the kubelet's truth).  -> the pod (for its RCCL env)."""
+        several calls.  A container reusing devices of an earlier container belongs to the same pod
+        (:meth:`_reuse`).  When the kubelet chose devices outside the GROUP, the GROUP is rewritten to
+        what it chose (the extender's view must be the kubelet's truth).  -> the pod (for its env)."""
         if self.api is None or not self.cfg.node_name:
             return None
         for attempt in range(5):
-            cands = self._admission_candidates()
-            c, how = self._match(cands, ids)
-            if c is None:
-                log.warning("no pending pod on %s matches allocation %s", self.cfg.node_name, ids)
-                return None
-            md = meta(c.pod)
-            adm = c.adm if c.adm is not None else _Admission(md.get("uid", ""))
+            cands, live = self._admission_view()
+            rec = self._reuse(ids)
+            if rec is not None and rec.key in live and meta(live[rec.key]).get("uid", "") == rec.uid:
+                pod = live[rec.key]
+                c = next((x for x in cands if x.key == rec.key), None)
+                pa = PodAssignment.from_annotations(obj_annotations(pod))
+                steps = c.steps if c is not None else []
+                adm, how = rec, "reuse"
+            else:
+                c, how = self._match(cands, ids)
+                if c is None:
+                    log.warning("no pending pod on %s matches allocation %s", self.cfg.node_name, ids)
+                    return None
+                pod, pa, steps = c.pod, c.pa, c.steps
+                adm = c.adm if c.adm is not None else _Admission(c.key, meta(pod).get("uid", ""))
+            md = meta(pod)
             claimed = adm.claimed | set(ids)
             done = adm.done + 1
-            finished = done >= len(c.steps)
+            finished = done >= len(steps)
             now = int(self.clock())
             ann: Dict[str, Optional[str]] = {}
-            if how == "unannotated":
-                if finished or len(claimed) >= self._pod_request(c.pod):
+            if pa is None:
+                if finished or len(claimed) >= self._pod_request(pod):
                     ann = {ANN_GROUP: format_group(sorted(claimed)), ANN_ASSIGNED: "true", ANN_ASSUME_TIME: str(now)}
             else:
-                group = set(c.pa.group)
-                if how == "resized" or not set(ids) <= group:
-                    extra = set(ids) - group
+                group = set(pa.group)
+                if not claimed <= group:
+                    extra = claimed - group
                     spare = sorted(group - claimed, reverse=True)  # GROUP devices no container got yet
                     group = (group - set(spare[:len(extra)])) | claimed
                     log.warning("kubelet allocated %s but pod %s was assumed %s; recording what the kubelet chose",
-                                ids, md.get("name"), c.pa.group)
+                                ids, md.get("name"), pa.group)
                 complete = claimed >= group
-                if sorted(group) != sorted(set(c.pa.group)) or (complete and not c.pa.assigned):
+                if sorted(group) != sorted(set(pa.group)) or (complete and not pa.assigned):
                     ann = {ANN_GROUP: format_group(sorted(group)), ANN_ASSIGNED: "true" if complete else "false"}
                     if complete:
                         ann[ANN_ASSUME_TIME] = str(now)
-            pod = c.pod
             if ann:
                 try:
                     pod = self.api.patch_pod_annotations(md.get("namespace", "default"), md["name"], ann,
@@ -1095,11 +1163,12 @@ class DevicePluginServer:
                 except Exception as e:  # noqa: BLE001 - the reconcile pass repairs it
                     log.warning("recording allocation %s on %s/%s failed: %s", ids, md.get("namespace"), md.get("name"), e)
             adm.claimed, adm.done = claimed, done
+            self._claimed_by = adm
             if finished:
-                self._admissions.pop(c.key, None)
+                self._admissions.pop(adm.key, None)
             else:
-                self._admissions[c.key] = adm
-            if how != "group" or not finished or len(c.steps) > 1:
+                self._admissions[adm.key] = adm
+            if how != "group" or not finished or len(steps) > 1:
                 self.metrics.container_claims.labels(how if how != "group" else ("final" if finished else "partial")).inc()
             return pod
         return None
@@ -1131,15 +1200,30 @@ class DevicePluginServer:
             md = meta(p)
             key = f"{md.get('namespace', 'default')}/{md.get('name')}"
             reported[key] = {int(i) for r in names for i in truth.get(key, {}).get(r, []) if str(i).isdigit()}
+        # what this plugin saw allocated together (an admission unit: the containers of one kubelet pod
+        # admission linked by reused devices): pod-resources does not list init containers' devices
+        with self._alloc_lock:
+            settled = time.monotonic() - self._last_alloc > self.cfg.admission_settle_s
+            units: Dict[str, set] = {}
+            for key, ids in reported.items():
+                if ids and all(d in self._unit_of for d in ids):
+                    others = set().union(*(v for k, v in reported.items() if k != key))
+                    units[key] = set().union(*(self._unit_of[d] for d in ids)) - others
         for p in pods:
             md = meta(p)
             key = f"{md.get('namespace', 'default')}/{md.get('name')}"
             ids = sorted(reported[key])
             if not ids:
                 continue  # not admitted yet (or not ours)
+            if pod_phase(p) == "Pending" and not settled:
+                continue  # the kubelet may be admitting it: its Allocate calls record it
             pa = PodAssignment.from_annotations(obj_annotations(p))
             group = set(pa.group) if pa is not None else set()
-            if pa is not None and set(ids) <= group:
+            if key in units:
+                ids = sorted(units[key])
+                if pa is not None and pa.assigned and ids == sorted(group):
+                    continue
+            elif pa is not None and set(ids) <= group:
                 # pod-resources lists app containers and sidecars, not init containers that have exited:
                 # a GROUP larger than the listed devices holds the init devices the kubelet still counts
                 # as the pod's, and is kept.  An unconfirmed GROUP is confirmed once the listed devices

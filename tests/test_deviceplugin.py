@@ -362,7 +362,7 @@ def test_liveness_reports_a_wedged_monitor_and_failing_registration(sockdir):
         r = requests.get(base + "/healthz", timeout=5)
         assert r.status_code == 200 and r.text == "ok"
         wedge.set()
-        time.sleep(0.3)
+        assert _wait(lambda: not plugin.liveness(monitor_stall_s=0.1)[0], timeout=10)  # the loop enters the wedged call
         ok, why = plugin.liveness(monitor_stall_s=0.1)
         assert not ok and "monitor loop stalled" in why
         release.set()

@@ -161,15 +161,28 @@ def test_a_pod_under_admission_is_continued_before_an_older_one():
     container cannot be q's (whose next container asks 2), so p's admission is under way; p's second
     container asks 2 like q's first, and must continue p, not jump to the older q."""
     with SimCluster({"n": fx.f7_mi355x()}) as c:
-        c.submit("q", 0, split=[2, 2])
-        c.submit("p", 0, split=[1, 2])
-        rq, rp = c.schedule_pending(admit=False)
+        groups = {"q": [0, 1, 2, 3], "p": [4, 5, 6]}
+        for name, split, t in (("p", [1, 2], 200), ("q", [2, 2], 100)):  # p created first, q assumed first
+            c.api.create_pod(make_pod(name, split=split, node="n",
+                                      annotations=PodAssignment.assumed(groups[name], t).to_annotations()))
         kub = c.nodes["n"].kubelet
         kub.admit(c.api.get_pod("default", "p"), c.resource)
         kub.admit(c.api.get_pod("default", "q"), c.resource)
-        for name, r in (("p", rp), ("q", rq)):
-            assert sorted(int(i) for i in kub.allocated[RES][f"default/{name}"]) == sorted(r.devices), name
-            assert _ann(c, name).assigned and sorted(_ann(c, name).group) == sorted(r.devices), name
+        for name, g in groups.items():
+            assert sorted(int(i) for i in kub.allocated[RES][f"default/{name}"]) == g, name
+            assert _ann(c, name).assigned and sorted(_ann(c, name).group) == g, name
+
+
+def test_reconcile_leaves_pods_without_devices_alone():
+    """A pod on the node that holds no device (no GPU request, nothing in pod-resources) is not
+    stamped with an empty GROUP by the reconcile pass."""
+    with SimCluster({"n": fx.f7_mi355x()}) as c:
+        c.api.create_pod(make_pod("cpu-only", node="n"))
+        c.api.set_pod_phase("default", "cpu-only", "Running")
+        c.submit("g", 2)
+        c.schedule_pending()
+        assert c.reconcile() == 0
+        assert _ann(c, "cpu-only") is None
 
 
 def test_single_and_multi_container_pods_of_other_sizes_do_not_steal():
@@ -252,3 +265,25 @@ def test_time_sliced_pod_with_two_one_slice_containers():
         masks = [dict(cr.envs).get("HSA_CU_MASK") for cr in kub.responses["default/two-slices"].container_responses]
         if len({i // 2 for i in group}) == 1:  # both slices on one GPU: the two containers' CUs are disjoint
             assert masks[0] and masks[1] and masks[0] != masks[1]
+
+
+def test_swapped_init_container_pods_keep_every_held_device_annotated():
+    """a = init(4) + app(2) assumed first, b = 4 GPUs assumed second, and the kubelet admits b first:
+    b's call is matched to a (same count, older) and a's init call to b — the pods' annotations name
+    each other's devices.  a's app container reuses 2 of the 4 devices its init container got: that
+    call continues the same admission.  The annotations' union is the kubelet's, and the reconcile
+    pass, which sees only a's 2 app devices in pod-resources, restores all 4 for a from the admission
+    unit — no device the kubelet holds is left unannotated."""
+    with SimCluster({"n": fx.f7_mi355x()}) as c:
+        for name, kw, g, t in (("a", dict(split=[2], init=[4]), [0, 1, 2, 3], 100), ("b", dict(split=[4]), [4, 5, 6, 7], 200)):
+            c.api.create_pod(make_pod(name, node="n", annotations=PodAssignment.assumed(g, t).to_annotations(), **kw))
+        kub = c.nodes["n"].kubelet
+        kub.admit(c.api.get_pod("default", "b"), c.resource)
+        kub.admit(c.api.get_pod("default", "a"), c.resource)
+        held = {n: sorted(int(i) for i in kub.allocated[RES][f"default/{n}"]) for n in ("a", "b")}
+        assert sorted(held["a"] + held["b"]) == list(range(8))
+        union = sorted(_ann(c, "a").group + _ann(c, "b").group)
+        assert union == list(range(8))  # the extender's view covers exactly what the kubelet holds
+        c.reconcile()
+        for n in ("a", "b"):
+            assert sorted(_ann(c, n).group) == held[n], (n, _ann(c, n), held)

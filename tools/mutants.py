@@ -80,7 +80,10 @@ MUTANTS: List[Mutant] = [
                              '                                                         resource_version=md.get("resourceVersion"))',
            'pod = self.api.patch_pod_annotations(md.get("namespace", "default"), md["name"], ann,\n'
            '                                                         resource_version=None)'),
-    Mutant("plugin", PLUGIN, "            if pa is not None and set(ids) <= group:", "            if pa is not None and set(ids) == group:"),
+    Mutant("plugin", PLUGIN, "                ids = sorted(set(ids) | set(keep[:max(0, self._pod_request(p) - len(ids))]))",
+           "                ids = sorted(set(ids))"),
+    Mutant("plugin", PLUGIN, "            if pa is not None and set(ids) <= group:", "            if pa is not None and set(ids) == group:",
+           equivalent=True, why="the branch below keeps the GROUP devices no other pod reports, up to the pod's request"),
     Mutant("plugin", PLUGIN, "            if nxt is not None and nxt != size:", "            if False:"),
     Mutant("plugin", PLUGIN, "        out.sort(key=lambda c: (c.adm is None or c.adm.done == 0, c.pa is None,",
            "        out.sort(key=lambda c: (False, c.pa is None,"),
