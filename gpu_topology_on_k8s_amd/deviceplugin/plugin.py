@@ -48,7 +48,7 @@ from ..k8s.annotations import (ANN_ASSIGNED, ANN_ASSUME_TIME, ANN_GROUP, Contrac
 from ..k8s.api import Conflict, KubeAPI
 from ..k8s.events import record_event
 from ..k8s.objects import annotations as obj_annotations
-from ..k8s.objects import meta, pod_device_steps, pod_gpu_request, pod_is_terminal, pod_phase
+from ..k8s.objects import meta, pod_device_steps, pod_gpu_request, pod_is_terminal, pod_key, pod_phase
 from ..placement import NoFeasiblePlacement, PlacementPolicy
 from ..placement.core import select_with
 from ..topology.cpus import recommended_cpuset
@@ -292,6 +292,11 @@ class DevicePluginServer:
         self._chain: Optional[Tuple[set, Optional[_Admission]]] = None  # the previous call's unit and record
         self._last_alloc = -1e9  # monotonic time the last Allocate ended
         self._claimed_by: Optional[_Admission] = None  # the record _claim_pod matched the current call to
+        # must_include of the GetPreferredAllocation calls since the last Allocate (None: there was none).
+        # The kubelet asks before every container whose reused devices do not cover its request, with
+        # must_include = the reused devices, and skips the call only when they cover it: so this tells
+        # which devices of the next Allocate are reused (all of them when None)
+        self._gpa_must: Optional[set] = None
         self.registered = 0
         self.metrics = PluginMetrics()
         self.metrics.set_topology(topology)
@@ -569,6 +574,8 @@ class DevicePluginServer:
             avail = self._ids(context, creq.available_deviceIDs)
             must = self._ids(context, creq.must_include_deviceIDs)
             size = int(creq.allocation_size)
+            with self._alloc_lock:
+                self._gpa_must = (self._gpa_must or set()) | set(must)
             ids = self._preferred_from_group(cands, live, size, avail, must)
             if ids is not None:
                 self.metrics.preferred.labels("annotation").inc()
@@ -693,9 +700,11 @@ class DevicePluginServer:
             pods = []
             for creq in request.container_requests:
                 ids = sorted({int(x) for x in creq.devices_ids})
+                reused = set(ids) if self._gpa_must is None else self._gpa_must & set(ids)
                 self._claimed_by = None
-                pods.append(self._claim_pod(ids))
-                self._link(ids, self._claimed_by)
+                pods.append(self._claim_pod(ids, reused))
+                self._link(ids, self._claimed_by, reused)
+            self._gpa_must = None
             self._last_alloc = time.monotonic()
         for creq, pod in zip(request.container_requests, pods):
             ids = [int(x) for x in creq.devices_ids]
@@ -1072,19 +1081,21 @@ class DevicePluginServer:
                                 meta(c.pod).get("creationTimestamp", ""), meta(c.pod).get("name", "")))
         return out, live
 
-    def _reuse(self, ids: Sequence[int]) -> Optional[_Admission]:
-        """The record of the previous Allocate when ``ids`` reuse some of its unit's devices.  The
+    def _reuse(self, reused: Sequence[int]) -> Optional[_Admission]:
+        """The record of the previous Allocate when the devices the kubelet reused (``reused``: what
+        GetPreferredAllocation was told to include, see ``_gpa_must``) are some of its unit's.  The
         kubelet admits one pod at a time and hands a regular init container's devices only to the
         later containers of the same pod, so such a call continues the previous call's admission —
         whichever pod that call was matched to."""
-        if self._chain is None or not self._chain[0] & {int(d) for d in ids}:
+        if self._chain is None or not self._chain[0] & {int(d) for d in reused}:
             return None
         return self._chain[1]
 
-    def _link(self, ids: Sequence[int], adm: Optional[_Admission]) -> None:
+    def _link(self, ids: Sequence[int], adm: Optional[_Admission], reused: Sequence[int] = ()) -> None:
         """Record one Allocate call in the admission units (see ``_unit_of``)."""
         ids_s = {int(d) for d in ids}
-        unit = self._chain[0] | ids_s if self._chain is not None and self._chain[0] & ids_s else set(ids_s)
+        linked = self._chain is not None and self._chain[0] & {int(d) for d in reused}
+        unit = self._chain[0] | ids_s if linked else set(ids_s)
         for d in unit:
             self._unit_of[d] = unit
         self._chain = (unit, adm)
@@ -1107,7 +1118,7 @@ class DevicePluginServer:
                 return c, "unannotated"
         return None, ""
 
-    def _claim_pod(self, ids: List[int]) -> Optional[dict]:
+    def _claim_pod(self, ids: List[int], reused: Sequence[int] = ()) -> Optional[dict]:
         """One container's ``Allocate``: find the pod the devices are for, record them against its
         GROUP, and flip it to ASSIGNED=true (conditional patch) once every device of the GROUP has been
         allocated — with one ``Allocate`` per container (the real kubelet), a pod is claimed over
@@ -1118,7 +1129,7 @@ class DevicePluginServer:
             return None
         for attempt in range(5):
             cands, live = self._admission_view()
-            rec = self._reuse(ids)
+            rec = self._reuse(reused)
             if rec is not None and rec.key in live and meta(live[rec.key]).get("uid", "") == rec.uid:
                 pod = live[rec.key]
                 c = next((x for x in cands if x.key == rec.key), None)
@@ -1200,45 +1211,45 @@ class DevicePluginServer:
             md = meta(p)
             key = f"{md.get('namespace', 'default')}/{md.get('name')}"
             reported[key] = {int(i) for r in names for i in truth.get(key, {}).get(r, []) if str(i).isdigit()}
-        # what this plugin saw allocated together (an admission unit: the containers of one kubelet pod
-        # admission linked by reused devices): pod-resources does not list init containers' devices
+        # pod-resources lists app containers and sidecars, not the init containers that have exited,
+        # yet the kubelet counts an init container's devices as the pod's until it ends.  Where they
+        # went: (1) what this plugin saw allocated together (an admission unit: the calls of one kubelet
+        # pod admission, linked by reused devices); (2) after a plugin restart, the GROUPs as written:
+        # GROUP devices no pod lists go to the pod listing most of that GROUP, up to its request
         with self._alloc_lock:
             settled = time.monotonic() - self._last_alloc > self.cfg.admission_settle_s
-            units: Dict[str, set] = {}
-            for key, ids in reported.items():
-                if ids and all(d in self._unit_of for d in ids):
-                    others = set().union(*(v for k, v in reported.items() if k != key))
-                    units[key] = set().union(*(self._unit_of[d] for d in ids)) - others
+            unit_of = dict(self._unit_of)
+        listed = set().union(*reported.values()) if reported else set()
+        old = {}
+        for p in pods:
+            pa = PodAssignment.from_annotations(obj_annotations(p))
+            if pa is not None:
+                old[pod_key(p)] = set(pa.group)
+        orphans: Dict[str, set] = {}
+        for g in old.values():
+            rest = g - listed
+            if not rest:
+                continue
+            owners = sorted(reported, key=lambda k: (-len(g & reported[k]), k))
+            if owners and g & reported[owners[0]]:
+                orphans.setdefault(owners[0], set()).update(rest)
         for p in pods:
             md = meta(p)
             key = f"{md.get('namespace', 'default')}/{md.get('name')}"
-            ids = sorted(reported[key])
+            ids = set(reported[key])
             if not ids:
                 continue  # not admitted yet (or not ours)
             if pod_phase(p) == "Pending" and not settled:
                 continue  # the kubelet may be admitting it: its Allocate calls record it
             pa = PodAssignment.from_annotations(obj_annotations(p))
-            group = set(pa.group) if pa is not None else set()
-            if key in units:
-                ids = sorted(units[key])
-                if pa is not None and pa.assigned and ids == sorted(group):
-                    continue
-            elif pa is not None and set(ids) <= group:
-                # pod-resources lists app containers and sidecars, not init containers that have exited:
-                # a GROUP larger than the listed devices holds the init devices the kubelet still counts
-                # as the pod's, and is kept.  An unconfirmed GROUP is confirmed once the listed devices
-                # are all of it or the pod runs (all its containers were allocated)
-                if pa.assigned or (set(ids) != group and pod_phase(p) != "Running"):
-                    continue
-                ids = sorted(group)
-            elif pa is not None:
-                # devices outside the GROUP: the kubelet's are the truth; GROUP devices no other pod
-                # reports may be this pod's init devices and are kept, up to the pod's request
-                others = set().union(*(v for k, v in reported.items() if k != key))
-                keep = sorted(group - set(ids) - others)
-                ids = sorted(set(ids) | set(keep[:max(0, self._pod_request(p) - len(ids))]))
-                if pa.assigned and ids == sorted(group):
-                    continue
+            others = listed - ids
+            if all(d in unit_of for d in ids):
+                target = set().union(*(unit_of[d] for d in ids)) - others
+            else:
+                target = ids | set(sorted(orphans.get(key, ()))[:max(0, self._pod_request(p) - len(ids))])
+            ids = sorted(target)
+            if pa is not None and pa.assigned and ids == sorted(set(pa.group)):
+                continue
             ann = {ANN_GROUP: format_group(ids), ANN_ASSIGNED: "true"}
             if pa is None:
                 ann[ANN_ASSUME_TIME] = str(int(self.clock()))

@@ -31,6 +31,7 @@ from urllib.parse import urlsplit
 from aiohttp import web
 
 from ..deviceplugin import DevicePluginServer, FakeKubelet, PluginConfig, placeholder_dev_tree
+from ..deviceplugin.kubelet import AdmissionError
 from ..extender import ExtenderConfig, TopologyExtender
 from ..extender.server import DEFAULT_PREFIX, make_app
 from ..k8s import Contract, FakeAPIServer, PodAssignment
@@ -358,7 +359,12 @@ class SimCluster:
             t1 = time.perf_counter()
             bound = self.api.get_pod(md.get("namespace", "default"), md["name"])
             rname = self.pod_resource(bound)
-            self.nodes[res.node].kubelet.admit(bound, rname)
+            try:
+                self.nodes[res.node].kubelet.admit(bound, rname)
+            except AdmissionError as e:  # the kubelet rejected the pod (or its container did not start)
+                res.error = f"admission: {e}"
+                self.history.append(res)
+                return res
             res.admit_ms = (time.perf_counter() - t1) * 1e3
             res.allocated = tuple(int(i) for i in self.nodes[res.node].kubelet.allocated[rname][key])
         self.history.append(res)

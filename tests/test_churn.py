@@ -76,6 +76,7 @@ def test_random_churn_keeps_allocations_consistent(seed, informer):
                 concurrent = rng.random() < 0.5
                 strict = not concurrent  # concurrent binds + admissions may swap same-size pods
                 for r in c.schedule_pending(concurrent=concurrent):
+                    assert not r.error.startswith("admission"), r  # the extender never binds onto held devices
                     if r.node and r.allocated:
                         live[r.pod] = r.node
             elif op < 0.8 and live:

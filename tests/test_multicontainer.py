@@ -287,3 +287,21 @@ def test_swapped_init_container_pods_keep_every_held_device_annotated():
         c.reconcile()
         for n in ("a", "b"):
             assert sorted(_ann(c, n).group) == held[n], (n, _ann(c, n), held)
+
+
+def test_swapped_init_container_pods_after_a_plugin_restart():
+    """The same swap, but the plugin restarted before the reconcile pass (its admission units are
+    gone): the GROUPs as written are the units — the 2 devices of b's GROUP nobody lists go to the pod
+    listing the rest of it (a's app container), up to a's request of 4."""
+    with SimCluster({"n": fx.f7_mi355x()}) as c:
+        for name, kw, g, t in (("a", dict(split=[2], init=[4]), [0, 1, 2, 3], 100), ("b", dict(split=[4]), [4, 5, 6, 7], 200)):
+            c.api.create_pod(make_pod(name, node="n", annotations=PodAssignment.assumed(g, t).to_annotations(), **kw))
+        kub = c.nodes["n"].kubelet
+        kub.admit(c.api.get_pod("default", "b"), c.resource)
+        kub.admit(c.api.get_pod("default", "a"), c.resource)
+        held = {n: sorted(int(i) for i in kub.allocated[RES][f"default/{n}"]) for n in ("a", "b")}
+        c.nodes["n"].plugin._unit_of.clear()  # what a restarted plugin knows
+        c.reconcile()
+        for n in ("a", "b"):
+            assert sorted(_ann(c, n).group) == held[n], (n, _ann(c, n), held)
+        assert c.reconcile() == 0

@@ -80,10 +80,14 @@ MUTANTS: List[Mutant] = [
                              '                                                         resource_version=md.get("resourceVersion"))',
            'pod = self.api.patch_pod_annotations(md.get("namespace", "default"), md["name"], ann,\n'
            '                                                         resource_version=None)'),
-    Mutant("plugin", PLUGIN, "                ids = sorted(set(ids) | set(keep[:max(0, self._pod_request(p) - len(ids))]))",
-           "                ids = sorted(set(ids))"),
-    Mutant("plugin", PLUGIN, "            if pa is not None and set(ids) <= group:", "            if pa is not None and set(ids) == group:",
-           equivalent=True, why="the branch below keeps the GROUP devices no other pod reports, up to the pod's request"),
+    Mutant("plugin", PLUGIN, "                orphans.setdefault(owners[0], set()).update(rest)", "                pass"),
+    Mutant("plugin", PLUGIN, "                target = set().union(*(unit_of[d] for d in ids)) - others",
+           "                target = set(ids)"),
+    Mutant("plugin", PLUGIN, "        unit = self._chain[0] | ids_s if linked else set(ids_s)", "        unit = set(ids_s)"),
+    Mutant("plugin", PLUGIN, "                reused = set(ids) if self._gpa_must is None else self._gpa_must & set(ids)",
+           "                reused = set(ids)"),
+    Mutant("plugin", PLUGIN, "                    or (rec is not None and (pod is None or meta(pod).get(\"uid\", \"\") != rec.uid)))",
+           "                    or False)"),
     Mutant("plugin", PLUGIN, "            if nxt is not None and nxt != size:", "            if False:"),
     Mutant("plugin", PLUGIN, "        out.sort(key=lambda c: (c.adm is None or c.adm.done == 0, c.pa is None,",
            "        out.sort(key=lambda c: (False, c.pa is None,"),
@@ -93,8 +97,9 @@ MUTANTS: List[Mutant] = [
     Mutant("plugin", PLUGIN, "            if not ids:\n                continue  # not admitted yet (or not ours)",
            "            if False:\n                continue  # not admitted yet (or not ours)"),
     Mutant("plugin", PLUGIN, "                ann[ANN_ASSUME_TIME] = str(int(self.clock()))", "                pass"),
-    Mutant("plugin", PLUGIN, '            if pod_phase(p) != "Pending":\n                continue\n            md = meta(p)',
-           '            if False:\n                continue\n            md = meta(p)'),
+    Mutant("plugin", PLUGIN, '            if pod_phase(p) != "Pending" and (pa is None or pa.assigned):',
+           '            if pod_phase(p) != "Pending":'),
+    Mutant("plugin", PLUGIN, '            if pod_phase(p) != "Pending" and (pa is None or pa.assigned):', '            if False:'),
     # data-parallel reduction
     Mutant("dp", DP, "        return b.start + self.rank * c, b.start + (self.rank + 1) * c", "        return b.start, b.start + c"),
     Mutant("dp", DP, "                if b.work is None:\n                    self._launch(b)", "                if False:\n                    self._launch(b)"),
