@@ -449,8 +449,6 @@ def test_prestart_validation_records_busbw_on_the_pod():
     lands on the pod, and a failing validation fails the container start with an Event."""
     import json as _json
 
-    from gpu_topology_on_k8s_amd.deviceplugin import AdmissionError
-
     seen = []
 
     def fake_validate(ids):
@@ -468,8 +466,8 @@ def test_prestart_validation_records_busbw_on_the_pod():
         v = _json.loads(c.api.get_pod("default", "pair")["metadata"]["annotations"][C.validated_key])
         assert v["k"] == 2 and v["peak_busbw_gbps"] == 60.0
         c.submit("bad", 3)
-        with pytest.raises(AdmissionError, match="validation"):
-            c.schedule_pending()
+        (rb,) = c.schedule_pending()  # the sim records the failed container start as the pod's error
+        assert rb.error.startswith("admission: PreStartContainer failed") and "validation" in rb.error and not rb.allocated
         assert any(e["reason"] == "FailedGPUPlacementValidation" for e in c.api.events)
         text = c.nodes["n1"].plugin.metrics.exposition().decode()
         assert 'gtk_plugin_placement_validations_total{result="ok"} 1.0' in text
