@@ -151,8 +151,7 @@ def scale_prioritize(n_nodes: int, pods: int = 20, k: int = 4):
         sync_ms = None
         if mode == "informer":
             t0 = time.perf_counter()
-            inf = Informer(api, ext.cache.on_list, ext.cache.on_event, watch_timeout=30.0, begin_list=ext.cache.begin_list)
-            ext.cache.attach_informer(inf)
+            inf = ext.cache.make_informer(watch_timeout=30.0)
             inf.start()
             inf.wait_synced(60)
             sync_ms = round((time.perf_counter() - t0) * 1e3, 2)

@@ -34,6 +34,10 @@ def main(argv=None) -> int:
     ap.add_argument("--partition-aware", default="on", choices=["on", "off"],
                     help="CPX/DPX/QPX nodes: group XCPs by physical GPU (on) or treat each as a stand-alone GPU (off)")
     ap.add_argument("--resync", type=float, default=5.0, help="polling period without the informer")
+    ap.add_argument("--list-page-size", type=int, default=500,
+                    help="informer LIST page size (limit/continue; 0 = one unpaginated LIST)")
+    ap.add_argument("--list-from-watch-cache", default="on", choices=["on", "off"],
+                    help="first LIST with resourceVersion=0 (served by the apiserver's watch cache, no etcd quorum read)")
     ap.add_argument("--informer", default="on", choices=["on", "off"],
                     help="keep the node/pod view current with LIST+WATCH (on) or by polling every --resync s (off)")
     ap.add_argument("--scheduler-names", default="",
@@ -66,11 +70,7 @@ def main(argv=None) -> int:
                          ledger=a.bind_ledger == "on")
     ext = TopologyExtender(api, cfg)
     if a.informer == "on":
-        from ..k8s.informer import Informer
-
-        inf = Informer(api, ext.cache.on_list, ext.cache.on_event, begin_list=ext.cache.begin_list)
-        ext.cache.attach_informer(inf)
-        inf.start()
+        ext.cache.make_informer(page_size=a.list_page_size, watch_cache=a.list_from_watch_cache == "on").start()
     ssl_context = None
     if a.tls_cert or a.tls_key:
         from .server import tls_context

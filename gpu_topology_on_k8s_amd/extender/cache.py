@@ -227,11 +227,14 @@ class ClusterCache:
             self._epoch += 1
             return self._epoch
 
-    def _rebuild(self, st: NodeState, pods: List[dict], list_epoch: int) -> None:
+    def _rebuild(self, st: NodeState, pods: List[dict], list_epoch: int, consistent: Optional[bool] = None) -> None:
         """``list_epoch``: value of the epoch counter taken just before the pods were listed.  Called
         with ``st.lock`` held.  A LIST older than the one already applied is dropped: concurrent
         refreshes can finish out of order, and the older one may predate a bind the newer one
-        already made authoritative (its overlay entry is gone)."""
+        already made authoritative (its overlay entry is gone).  ``consistent``: the LIST was a quorum
+        read (default ``consistent_lists``); a watch-cache LIST (``resourceVersion=0``) may not show a
+        bind made just before it, so its absence proves nothing."""
+        consistent = self.consistent_lists if consistent is None else consistent
         if list_epoch < st.list_epoch:
             return
         st.list_epoch = list_epoch
@@ -258,7 +261,7 @@ class ClusterCache:
                         del ov[key]
                     # else: this LIST shows the pod, but a LIST started before the bind may still be
                     # applied after it; keep the entry so such a stale view cannot drop the devices
-                elif after_bind and self.consistent_lists:
+                elif after_bind and consistent:
                     del ov[key]  # listed (quorum read) after the bind and absent: the pod is gone
                 elif now - a.assume_time > min(self.ttl, self.overlay_grace):
                     del ov[key]  # cached/lagging lists: give up after the grace period
@@ -299,7 +302,7 @@ class ClusterCache:
             for gone in set(self._nodes) - names:
                 del self._nodes[gone]
 
-    def replace_pods(self, pods: List[dict], epoch: Optional[int] = None) -> None:
+    def replace_pods(self, pods: List[dict], epoch: Optional[int] = None, consistent: Optional[bool] = None) -> None:
         """A full pod LIST: rebuild every known node's usage from it."""
         epoch = self._next_epoch() if epoch is None else epoch
         by_node: Dict[str, List[dict]] = {}
@@ -312,7 +315,7 @@ class ClusterCache:
         for name in names:
             st = self._state(name)
             with st.lock:
-                self._rebuild(st, by_node.get(name, []), epoch)
+                self._rebuild(st, by_node.get(name, []), epoch, consistent)
 
     def sync_all(self) -> None:
         """Cluster-wide LIST of nodes + pods (polling mode, or the informer's safety resync).
@@ -342,11 +345,29 @@ class ClusterCache:
         pod — would drop the bind's overlay entry and free its devices until the WATCH event."""
         return self._next_epoch() if kind == "Pod" else None
 
-    def on_list(self, kind: str, items: List[dict], epoch: Optional[int] = None) -> None:
+    def make_informer(self, **kw):
+        """The LIST+WATCH informer that drives this cache in production (k8s/informer.py): paginated
+        watch-cache LISTs, pods filtered server-side to the non-terminal ones, objects trimmed to the
+        fields the cache reads, watches resumed rather than relisted.  Attached, not started."""
+        from ..k8s.informer import Informer
+        from ..k8s.objects import LIVE_POD_SELECTOR, trim_node, trim_pod
+
+        prefix = self.contract.prefix
+
+        def transform(kind: str, o: dict) -> dict:
+            return trim_pod(o, prefix) if kind == "Pod" else trim_node(o, prefix)
+
+        kw.setdefault("field_selectors", {"Pod": LIVE_POD_SELECTOR})
+        kw.setdefault("transform", transform)
+        inf = Informer(self.api, self.on_list, self.on_event, begin_list=self.begin_list, **kw)
+        self.attach_informer(inf)
+        return inf
+
+    def on_list(self, kind: str, items: List[dict], epoch: Optional[int] = None, consistent: Optional[bool] = None) -> None:
         if kind == "Node":
             self.replace_nodes(items)
         elif kind == "Pod":
-            self.replace_pods(items, epoch)
+            self.replace_pods(items, epoch, consistent)
         with self._lock:
             self._last_full = self.clock()
 

@@ -92,12 +92,22 @@ class KubeAPI:
         raise NotImplementedError
 
     def list_with_version(self, kind: str, node_name: Optional[str] = None) -> Tuple[List[Obj], str]:
-        """(items, list resourceVersion) of ``kind`` in {"Node", "Pod"}: the LIST half of an informer."""
+        """(items, list resourceVersion) of ``kind`` in {"Node", "Pod"}: one unpaginated LIST."""
+        raise NotImplementedError
+
+    def list_page(self, kind: str, limit: int = 0, continue_token: str = "", resource_version: Optional[str] = None,
+                  field_selector: Optional[str] = None) -> Tuple[List[Obj], str, str]:
+        """One page of a LIST of ``kind``: (items, list resourceVersion, continue token or "").
+        ``resource_version="0"`` lets the apiserver answer from its watch cache (no etcd quorum read,
+        possibly a little stale; older apiservers then ignore ``limit``); ``None`` is a consistent
+        read.  Pages after the first pass only ``continue_token``.  An expired continue token raises
+        :class:`Gone`."""
         raise NotImplementedError
 
     def watch_stream(self, kind: str, resource_version: str, timeout: float = 60.0,
-                     stop: Optional[threading.Event] = None) -> Iterator[Tuple[str, Obj]]:
-        """(event type, object) after ``resource_version`` until ``timeout``: the WATCH half."""
+                     stop: Optional[threading.Event] = None, field_selector: Optional[str] = None) -> Iterator[Tuple[str, Obj]]:
+        """(event type, object) after ``resource_version`` until ``timeout``: the WATCH half.  With a
+        ``field_selector`` an object that stops matching arrives as DELETED."""
         raise NotImplementedError
 
 
@@ -235,13 +245,29 @@ class RestKubeAPI(KubeAPI):
         d = self._do("GET", path)
         return d.get("items", []), str((d.get("metadata") or {}).get("resourceVersion", ""))
 
+    def list_page(self, kind, limit=0, continue_token="", resource_version=None, field_selector=None):
+        q = []
+        if limit:
+            q.append(f"limit={int(limit)}")
+        if continue_token:
+            q.append("continue=" + quote(continue_token))
+        elif resource_version is not None:
+            q.append("resourceVersion=" + quote(str(resource_version)))
+        if field_selector:
+            q.append("fieldSelector=" + quote(field_selector))
+        d = self._do("GET", self._KIND_PATH[kind] + ("?" + "&".join(q) if q else ""))
+        md = d.get("metadata") or {}
+        return d.get("items", []), str(md.get("resourceVersion", "")), str(md.get("continue") or "")
+
     def watch_stream(self, kind: str, resource_version: str, timeout: float = 60.0,
-                     stop: Optional[threading.Event] = None) -> Iterator[Tuple[str, Obj]]:
+                     stop: Optional[threading.Event] = None, field_selector: Optional[str] = None) -> Iterator[Tuple[str, Obj]]:
         """``GET {path}?watch=1&resourceVersion=..&timeoutSeconds=..&allowWatchBookmarks=true`` read
         line by line; BOOKMARKs are yielded (they carry only a resourceVersion), an ERROR 410 raises
         :class:`Gone`."""
         url = (f"{self.base}{self._KIND_PATH[kind]}?watch=1&allowWatchBookmarks=true"
                f"&resourceVersion={quote(str(resource_version))}&timeoutSeconds={int(max(1, timeout))}")
+        if field_selector:
+            url += "&fieldSelector=" + quote(field_selector)
         with self._session().get(url, stream=True, timeout=(self.timeout, timeout + 30), verify=self._verify,
                                  headers=self._auth()) as r:
             if r.status_code >= 400:

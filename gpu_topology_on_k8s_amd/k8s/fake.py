@@ -17,13 +17,13 @@ import json
 import threading
 import time
 import uuid
-from collections import defaultdict, deque
+from collections import OrderedDict, defaultdict, deque
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any, Callable, Dict, Iterator, List, Optional, Tuple
 from urllib.parse import parse_qs, unquote, urlparse
 
 from .api import ApiError, Conflict, Gone, KubeAPI, NotFound, raise_for
-from .objects import meta
+from .objects import match_fields, meta
 
 __all__ = ["FakeAPIServer", "serve_http"]
 
@@ -78,6 +78,16 @@ class FakeAPIServer(KubeAPI):
         self._history: "deque[Tuple[int, str, str, Obj]]" = deque(maxlen=history)
         self.calls: Dict[str, int] = defaultdict(int)
         self.latency_s = 0.0
+        # paginated LISTs (list_page): the rest of a LIST, serialized at the LIST's resourceVersion,
+        # by continue token; the oldest are dropped (their tokens then answer 410, as after etcd
+        # compaction).  ``watch_cache_pages``: whether a resourceVersion=0 LIST (served from the watch
+        # cache) honours ``limit`` — apiservers before the paginated watch cache ignore it
+        self._pages: "OrderedDict[str, Tuple[List[str], str]]" = OrderedDict()
+        self.max_open_lists = 64
+        self.watch_cache_pages = False
+        self.bytes_served: Dict[str, int] = defaultdict(int)  # kind -> JSON bytes of LIST responses
+        self.list_requests: Dict[str, int] = defaultdict(int)  # kind -> LIST requests (pages)
+        self._watch_cuts: Dict[str, List[int]] = defaultdict(list)  # kind -> cut the next watches after n events
 
     # ------------------------------------------------------------------ infrastructure
     def _next_rv(self) -> str:
@@ -115,22 +125,67 @@ class FakeAPIServer(KubeAPI):
     # ------------------------------------------------------------------ LIST+WATCH (informers)
     def list_with_version(self, kind: str, node_name: Optional[str] = None) -> Tuple[List[Obj], str]:
         """(items, list resourceVersion): what ``GET /api/v1/{nodes,pods}`` returns."""
+        items, rv, _ = self.list_page(kind, field_selector=f"spec.nodeName={node_name}" if node_name and kind == "Pod" else None)
+        return items, rv
+
+    def list_page(self, kind, limit=0, continue_token="", resource_version=None, field_selector=None):
+        """One page of a LIST (``GET ...?limit=&continue=&resourceVersion=&fieldSelector=``).  The
+        whole LIST is serialized at its resourceVersion on the first page (a consistent snapshot, as
+        the apiserver reads etcd at one revision); later pages are served from it."""
         with self._lock:
-            items = self.list_nodes() if kind == "Node" else self.list_pods(node_name=node_name)
-            return items, str(self._rv)
+            self._enter("list_nodes" if kind == "Node" else "list_pods")
+            if continue_token:
+                snap = self._pages.pop(continue_token, None)
+                if snap is None:
+                    raise Gone("the provided continue parameter is too old")
+                encoded, list_rv = snap
+            else:
+                src = self.nodes if kind == "Node" else self.pods
+                encoded = [json.dumps(o) for _, o in sorted(src.items()) if match_fields(o, field_selector)]
+                list_rv = str(self._rv)
+                if str(resource_version) == "0" and not self.watch_cache_pages:
+                    limit = 0
+            page, rest = (encoded[:limit], encoded[limit:]) if limit else (encoded, [])
+            token = ""
+            if rest:
+                token = uuid.uuid4().hex
+                self._pages[token] = (rest, list_rv)
+                while len(self._pages) > self.max_open_lists:
+                    self._pages.popitem(last=False)
+            self.list_requests[kind] += 1
+            self.bytes_served[kind] += sum(len(e) for e in page)
+        return [json.loads(e) for e in page], list_rv, token
+
+    def expire_continue_tokens(self) -> None:
+        """Every open paginated LIST loses its snapshot (etcd compaction): the next page answers 410."""
+        with self._lock:
+            self._pages.clear()
+
+    def cut_watch(self, kind: str, after: int = 0) -> None:
+        """A watch of ``kind`` (the one open now, else the next) breaks — a connection reset — after
+        delivering ``after`` more events."""
+        with self._lock:
+            self._watch_cuts[kind].append(after)
 
     def watch_stream(self, kind: str, resource_version: str, timeout: float = 60.0,
-                     stop: Optional[threading.Event] = None) -> Iterator[Tuple[str, Obj]]:
+                     stop: Optional[threading.Event] = None, field_selector: Optional[str] = None) -> Iterator[Tuple[str, Obj]]:
         """Changes of ``kind`` after ``resource_version``, blocking up to ``timeout`` s for new ones
-        (``GET ...?watch=1``).  Raises :class:`Gone` when the window no longer reaches back that far."""
-        self.calls[f"watch_{kind}"] += 1
+        (``GET ...?watch=1``).  Raises :class:`Gone` when the window no longer reaches back that far.
+        With ``field_selector``, a change to an object that does not match is delivered as DELETED
+        (the object left the selection) and an ADDED one is not delivered."""
+        with self._lock:
+            self._enter(f"watch_{kind}")
+        cut: Optional[int] = None
         since = int(resource_version or 0)
         deadline = time.monotonic() + timeout
+        sent = 0
         with self._lock:
             if self._history and since < self._history[0][0] - 1 and len(self._history) == self._history.maxlen:
                 raise Gone(f"resourceVersion {since} is too old")
         while stop is None or not stop.is_set():
             with self._lock:
+                if cut is None and self._watch_cuts.get(kind):  # a cut requested while this watch is open
+                    cut = sent + self._watch_cuts[kind].pop(0)
                 batch = [(t, o) for rv, t, k, o in self._history if rv > since and k == kind]
                 if self._history:
                     since = max(since, self._history[-1][0])
@@ -141,6 +196,13 @@ class FakeAPIServer(KubeAPI):
                     self._changed.wait(min(left, 0.25))
                     continue
             for t, o in batch:
+                if field_selector and not match_fields(o, field_selector):
+                    if t == "ADDED":
+                        continue
+                    t = "DELETED"
+                if cut is not None and sent >= cut:
+                    raise ConnectionResetError(f"watch of {kind} cut after {sent} events (injected)")
+                sent += 1
                 yield t, copy.deepcopy(o)
 
     def create_event(self, namespace: str, event: Obj) -> Obj:
@@ -294,6 +356,9 @@ class FakeAPIServer(KubeAPI):
 class _Handler(BaseHTTPRequestHandler):
     api: FakeAPIServer = None  # type: ignore[assignment]
     token: Optional[str] = None
+    # HTTP/1.1 as the apiserver speaks it: keep-alive, and watches streamed with chunked encoding (a
+    # client reading an unframed HTTP/1.0 body buffers events until its read size fills)
+    protocol_version = "HTTP/1.1"
 
     def log_message(self, *a):  # quiet
         pass
@@ -321,12 +386,16 @@ class _Handler(BaseHTTPRequestHandler):
                 raise NotFound(u.path)
             rest = parts[2:]
             watch = (q.get("watch") or ["0"])[0] in ("1", "true")
+            fs = (q.get("fieldSelector") or [""])[0]
             if rest in (["nodes"], ["pods"]) and method == "GET" and watch:
                 return self._watch("Node" if rest == ["nodes"] else "Pod", (q.get("resourceVersion") or ["0"])[0],
-                                   float((q.get("timeoutSeconds") or ["60"])[0]))
-            if rest == ["nodes"] and method == "GET":
-                items, rv = self.api.list_with_version("Node")
-                return self._send(200, {"kind": "NodeList", "metadata": {"resourceVersion": rv}, "items": items})
+                                   float((q.get("timeoutSeconds") or ["60"])[0]), fs or None)
+            if rest in (["nodes"], ["pods"]) and method == "GET":
+                kind = "Node" if rest == ["nodes"] else "Pod"
+                items, rv, cont = self.api.list_page(kind, int((q.get("limit") or ["0"])[0]), (q.get("continue") or [""])[0],
+                                                     (q.get("resourceVersion") or [None])[0], fs or None)
+                md = {"resourceVersion": rv, **({"continue": cont} if cont else {})}
+                return self._send(200, {"kind": f"{kind}List", "metadata": md, "items": items})
             if len(rest) == 2 and rest[0] == "nodes":
                 if method == "GET":
                     return self._send(200, self.api.get_node(rest[1]))
@@ -335,12 +404,8 @@ class _Handler(BaseHTTPRequestHandler):
                     return self._send(200, self.api.patch_node(rest[1], md.get("annotations"), md.get("labels"),
                                                                md.get("resourceVersion")))
             node_name = None
-            fs = (q.get("fieldSelector") or [""])[0]
             if fs.startswith("spec.nodeName="):
                 node_name = fs.split("=", 1)[1]
-            if rest == ["pods"] and method == "GET":
-                items, rv = self.api.list_with_version("Pod", node_name=node_name)
-                return self._send(200, {"kind": "PodList", "metadata": {"resourceVersion": rv}, "items": items})
             if len(rest) == 3 and rest[0] == "namespaces" and rest[2] == "events" and method == "POST":
                 return self._send(201, self.api.create_event(rest[1], self._body()))
             if len(rest) >= 3 and rest[0] == "namespaces" and rest[2] == "pods":
@@ -362,27 +427,36 @@ class _Handler(BaseHTTPRequestHandler):
         except ApiError as e:
             return self._send(e.code, {"kind": "Status", "status": "Failure", "code": e.code, "message": e.message})
 
-    def _watch(self, kind: str, rv: str, timeout: float) -> None:
-        """Watch response: one JSON ``{"type", "object"}`` per line until ``timeoutSeconds`` (HTTP/1.0,
-        body ends when the connection closes, as a chunked watch does for a streaming client)."""
+    def _chunk(self, data: bytes) -> None:
+        self.wfile.write(f"{len(data):x}\r\n".encode() + data + b"\r\n")
+        self.wfile.flush()
+
+    def _watch(self, kind: str, rv: str, timeout: float, field_selector: Optional[str] = None) -> None:
+        """Watch response: one JSON ``{"type", "object"}`` line per chunk (chunked transfer encoding,
+        as the apiserver streams it) until ``timeoutSeconds``.  An injected cut drops the connection
+        without the final chunk (the client sees a broken stream)."""
         try:
-            stream = self.api.watch_stream(kind, rv, timeout)
+            stream = self.api.watch_stream(kind, rv, timeout, field_selector=field_selector)
             first = next(stream, None)
         except Gone as e:
             return self._send(200, {"type": "ERROR", "object": {"kind": "Status", "code": 410, "reason": "Expired",
                                                                 "message": e.message}})
+        except ConnectionResetError:
+            self.close_connection = True
+            return
         self.send_response(200)
         self.send_header("Content-Type", "application/json")
+        self.send_header("Transfer-Encoding", "chunked")
         self.end_headers()
         try:
             if first is not None:
-                self.wfile.write((json.dumps({"type": first[0], "object": first[1]}) + "\n").encode())
-                self.wfile.flush()
+                self._chunk((json.dumps({"type": first[0], "object": first[1]}) + "\n").encode())
                 for t, o in stream:
-                    self.wfile.write((json.dumps({"type": t, "object": o}) + "\n").encode())
-                    self.wfile.flush()
+                    self._chunk((json.dumps({"type": t, "object": o}) + "\n").encode())
+            self.wfile.write(b"0\r\n\r\n")
+            self.wfile.flush()
         except (BrokenPipeError, ConnectionResetError):
-            pass
+            self.close_connection = True
 
     def do_GET(self):
         self._route("GET")

@@ -3,20 +3,31 @@
 The extender scores every candidate node of every pending pod (``design.md:118,123-129``), so its
 node/pod view must be current without a cluster-wide LIST in the request path (VERDICT r1 weak #7:
 the first ``prioritize`` at 1024 nodes cost 580 ms of LIST).  One thread per kind does what
-client-go's reflector does: LIST (remember the list ``resourceVersion``), hand the items to
-``on_list``, then WATCH from that version and hand every change to ``on_event``; a watch that times
-out is resumed from the last seen version, a 410 Gone (window expired) or any error relists after a
-back-off.  ``synced`` is set once every kind has been listed.
+client-go's reflector does:
 
-``begin_list(kind)`` (optional) is called just BEFORE each LIST request and its return value is
-passed to ``on_list(kind, items, token)``: a consumer that also writes state between the LIST request
-and its arrival (the extender's bind overlay) can order the two (extender/cache.py epochs).
+* **LIST** once, in pages of ``page_size`` (``limit``/``continue``), first from the apiserver's watch
+  cache (``resourceVersion=0``: no etcd quorum read).  Pods are filtered server-side with a field
+  selector (``status.phase!=Succeeded,status.phase!=Failed``: terminal pods never hold a device, and
+  a long-lived cluster keeps many).  Every object goes through ``transform`` before it is kept (the
+  extender keeps only the fields it reads: ``k8s.objects.trim_pod`` / ``trim_node``).  A continue token
+  that expired mid-LIST (410) restarts the LIST as a consistent read.
+* **WATCH** from the LIST's resourceVersion and hand every change to ``on_event``.  A watch that ends
+  (``timeoutSeconds``) or breaks (connection reset, apiserver 5xx/429) is **resumed from the last
+  resourceVersion seen**, after an exponential back-off with jitter; only a 410 Gone (the version
+  left the apiserver's window) relists.
+
+``begin_list(kind)`` (optional) is called just BEFORE each LIST and its return value is passed to
+``on_list(kind, items, token, consistent=...)``: a consumer that also writes state between the LIST
+request and its arrival (the extender's bind overlay) can order the two (extender/cache.py epochs),
+and learns whether the LIST was a consistent read (a watch-cache LIST may lag a bind it just made).
 """
 from __future__ import annotations
 
 import logging
+import random
 import threading
-from typing import Callable, Dict, List, Optional, Sequence
+import time
+from typing import Callable, Dict, List, Mapping, Optional, Sequence, Tuple
 
 from .api import Gone, KubeAPI
 from .objects import meta
@@ -31,7 +42,10 @@ Obj = Dict[str, object]
 class Informer:
     def __init__(self, api: KubeAPI, on_list: Callable[..., None], on_event: Callable[[str, str, Obj], None],
                  kinds: Sequence[str] = ("Node", "Pod"), watch_timeout: float = 300.0, backoff: float = 1.0,
-                 begin_list: Optional[Callable[[str], object]] = None):
+                 begin_list: Optional[Callable[[str], object]] = None, page_size: int = 500,
+                 field_selectors: Optional[Mapping[str, str]] = None,
+                 transform: Optional[Callable[[str, Obj], Obj]] = None, watch_cache: bool = True,
+                 max_backoff: float = 30.0, jitter: float = 0.2, seed: Optional[int] = None):
         self.api = api
         self.on_list = on_list
         self.begin_list = begin_list
@@ -39,12 +53,23 @@ class Informer:
         self.kinds = tuple(kinds)
         self.watch_timeout = watch_timeout
         self.backoff = backoff
+        self.max_backoff = max_backoff
+        self.jitter = jitter
+        self.page_size = int(page_size)
+        self.field_selectors = dict(field_selectors or {})
+        self.transform = transform
+        self.watch_cache = watch_cache
+        self._rng = random.Random(seed)
         self._stop = threading.Event()
         self._synced = {k: threading.Event() for k in self.kinds}
         self._all_synced = False
         self._threads: List[threading.Thread] = []
-        self.lists: Dict[str, int] = {k: 0 for k in self.kinds}  # LIST calls made (relists after the first)
+        self.lists: Dict[str, int] = {k: 0 for k in self.kinds}  # complete LISTs (relists after the first)
+        self.pages: Dict[str, int] = {k: 0 for k in self.kinds}  # LIST requests (pages)
         self.events: Dict[str, int] = {k: 0 for k in self.kinds}
+        self.watch_resumes: Dict[str, int] = {k: 0 for k in self.kinds}  # watches re-opened from the last version
+        self.watch_errors: Dict[str, int] = {k: 0 for k in self.kinds}
+        self.last_list: Dict[str, Dict[str, float]] = {}  # kind -> {"items", "pages", "seconds", "consistent"}
         self.last_error: Optional[str] = None
 
     @property
@@ -54,6 +79,11 @@ class Informer:
         if not self._all_synced:
             self._all_synced = all(e.is_set() for e in self._synced.values())
         return self._all_synced
+
+    def relists(self, kind: Optional[str] = None) -> int:
+        """LISTs after the first (per kind, or summed)."""
+        kinds = [kind] if kind else list(self.kinds)
+        return sum(max(0, self.lists[k] - 1) for k in kinds)
 
     def wait_synced(self, timeout: float = 30.0) -> bool:
         for e in self._synced.values():
@@ -75,22 +105,63 @@ class Informer:
             t.join(timeout=5)
         self._threads = []
 
+    def _delay(self, failures: int) -> float:
+        """Exponential back-off with jitter: ``backoff * 2^(failures-1)`` capped at ``max_backoff``,
+        scaled by a random factor in ``[1 - jitter, 1 + jitter]`` (replicas do not retry in step)."""
+        d = min(self.max_backoff, self.backoff * (2 ** max(0, failures - 1)))
+        return d * (1.0 + self.jitter * self._rng.uniform(-1.0, 1.0))
+
+    def _list(self, kind: str) -> Tuple[List[Obj], str, bool]:
+        """One complete LIST in pages -> (items, resourceVersion, consistent)."""
+        t0 = time.monotonic()
+        fs = self.field_selectors.get(kind)
+        rv_param: Optional[str] = "0" if self.watch_cache else None
+        items: List[Obj] = []
+        cont = ""
+        pages = 0
+        while True:
+            try:
+                page, list_rv, cont = self.api.list_page(kind, limit=self.page_size, continue_token=cont,
+                                                         resource_version=None if cont else rv_param, field_selector=fs)
+            except Gone:
+                if not cont:
+                    raise
+                # the paginated LIST's snapshot was compacted away mid-way: start over, consistently
+                log.info("informer %s: continue token expired after %d pages; relisting", kind, pages)
+                items, cont, rv_param = [], "", None
+                continue
+            pages += 1
+            self.pages[kind] += 1
+            tf = self.transform
+            items.extend(tf(kind, o) for o in page) if tf is not None else items.extend(page)
+            if not cont:
+                break
+        self.lists[kind] += 1
+        consistent = rv_param is None
+        self.last_list[kind] = {"items": float(len(items)), "pages": float(pages), "seconds": time.monotonic() - t0,
+                                "consistent": float(consistent)}
+        return items, list_rv, consistent
+
     def _run(self, kind: str) -> None:
         rv: Optional[str] = None
+        failures = 0
         while not self._stop.is_set():
             try:
                 if rv is None:
                     token = self.begin_list(kind) if self.begin_list is not None else None
-                    items, rv = self.api.list_with_version(kind)
-                    self.lists[kind] += 1
+                    items, list_rv, consistent = self._list(kind)
                     if self.begin_list is not None:
-                        self.on_list(kind, items, token)
+                        self.on_list(kind, items, token, consistent=consistent)
                     else:
                         self.on_list(kind, items)
+                    rv = list_rv
                     self._synced[kind].set()
-                for t, obj in self.api.watch_stream(kind, rv, self.watch_timeout, self._stop):
+                    failures = 0
+                for t, obj in self.api.watch_stream(kind, rv, self.watch_timeout, self._stop,
+                                                    field_selector=self.field_selectors.get(kind)):
                     if self._stop.is_set():
                         return
+                    failures = 0
                     new_rv = meta(obj).get("resourceVersion")
                     if new_rv:
                         rv = str(new_rv)
@@ -98,15 +169,22 @@ class Informer:
                         continue
                     self.events[kind] += 1
                     try:
-                        self.on_event(t, kind, obj)
+                        self.on_event(t, kind, self.transform(kind, obj) if self.transform is not None else obj)
                     except Exception as e:  # noqa: BLE001 - one bad object must not stop the stream
                         log.warning("informer %s: handler failed on %s: %s", kind, meta(obj).get("name"), e)
-                # watch ended (timeoutSeconds): resume from rv without relisting
+                # the watch ended (timeoutSeconds): resume from rv, no relist
+                self.watch_resumes[kind] += 1
             except Gone:
                 log.info("informer %s: resourceVersion %s expired; relisting", kind, rv)
                 rv = None
-            except Exception as e:  # noqa: BLE001 - network / apiserver errors: back off and relist
+            except Exception as e:  # noqa: BLE001 - network / apiserver errors: back off, then resume
+                failures += 1
                 self.last_error = str(e)
-                log.warning("informer %s: %s; relisting in %.1fs", kind, e, self.backoff)
-                rv = None
-                self._stop.wait(self.backoff)
+                delay = self._delay(failures)
+                if rv is None:
+                    log.warning("informer %s: LIST failed: %s; retrying in %.1fs", kind, e, delay)
+                else:
+                    self.watch_errors[kind] += 1
+                    self.watch_resumes[kind] += 1
+                    log.warning("informer %s: watch broke: %s; resuming from resourceVersion %s in %.1fs", kind, e, rv, delay)
+                self._stop.wait(delay)

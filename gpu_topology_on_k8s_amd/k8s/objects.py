@@ -5,7 +5,8 @@ from typing import Any, Dict, Iterable, List, Optional, Sequence, Tuple
 
 __all__ = [
     "meta", "annotations", "labels", "pod_key", "pod_node", "pod_phase", "pod_is_terminal", "pod_gpu_request",
-    "pod_device_steps", "make_pod", "make_node", "parse_quantity",
+    "pod_device_steps", "make_pod", "make_node", "parse_quantity", "field_value", "match_fields", "trim_pod",
+    "trim_node", "LIVE_POD_SELECTOR",
 ]
 
 Obj = Dict[str, Any]
@@ -109,6 +110,78 @@ def pod_device_steps(p: Obj, resource_names: Iterable[str]) -> List[Tuple[str, i
                 k = "sidecar" if kind == "init" and _is_sidecar(c) else kind
                 out.append((str(c.get("name") or f"{key}[{i}]"), r, k))
     return out
+
+
+def field_value(o: Obj, path: str) -> str:
+    """The string value of a dotted field path (``status.phase``, ``spec.nodeName``), "" if absent —
+    what a field selector compares (a missing ``status.phase`` is an empty string, as in the apiserver)."""
+    cur: Any = o
+    for part in path.split("."):
+        cur = cur.get(part) if isinstance(cur, dict) else None
+    return "" if cur is None else str(cur)
+
+
+def match_fields(o: Obj, selector: Optional[str]) -> bool:
+    """A field selector (``a.b=v``, ``a.b==v``, ``a.b!=v``, comma = AND) against an object."""
+    for term in (selector or "").split(","):
+        term = term.strip()
+        if not term:
+            continue
+        if "!=" in term:
+            k, v = term.split("!=", 1)
+            if field_value(o, k.strip()) == v.strip():
+                return False
+        else:
+            k, v = term.replace("==", "=").split("=", 1)
+            if field_value(o, k.strip()) != v.strip():
+                return False
+    return True
+
+
+#: what the extender's informer asks the apiserver for: pods that may hold devices (terminal ones
+#: never do, and a long-lived cluster keeps many of them)
+LIVE_POD_SELECTOR = "status.phase!=Succeeded,status.phase!=Failed"
+
+_META_KEEP = ("name", "namespace", "uid", "resourceVersion", "creationTimestamp", "deletionTimestamp")
+
+
+def _keep_annotation(key: str, prefix: str) -> bool:
+    return key.startswith(("ALIYUN_COM_GPU_", "GPU_", "GPUPKG_", prefix + "/")) or key == "gpu-id"
+
+
+def _trim_meta(o: Obj, prefix: str, keep_labels: bool) -> Obj:
+    md = meta(o)
+    out: Obj = {k: md[k] for k in _META_KEEP if k in md}
+    ann = md.get("annotations") or {}
+    out["annotations"] = {k: v for k, v in ann.items() if _keep_annotation(k, prefix)} if isinstance(ann, dict) else {}
+    if keep_labels:
+        out["labels"] = dict(md.get("labels") or {})
+    return out
+
+
+def trim_pod(p: Obj, prefix: str = "gputopology.amd.com") -> Obj:
+    """The parts of a Pod the extender's cache reads (the informer's transform, like client-go's
+    ``SetTransform``): identity, the GPU contract's annotations, node, phase and the containers'
+    resource requests.  ``managedFields``, env, volumes, status conditions and the rest are dropped:
+    a 100k-pod cluster is then held in tens of MB instead of GBs."""
+    spec = p.get("spec") if isinstance(p.get("spec"), dict) else {}
+    out_spec: Obj = {k: spec[k] for k in ("nodeName", "schedulerName") if k in spec}
+    for key in ("containers", "initContainers"):
+        cs = spec.get(key)
+        if isinstance(cs, list):
+            out_spec[key] = [{k: c[k] for k in ("name", "resources", "restartPolicy") if isinstance(c, dict) and k in c}
+                             for c in cs]
+    st = p.get("status") if isinstance(p.get("status"), dict) else {}
+    return {"metadata": _trim_meta(p, prefix, keep_labels=False), "spec": out_spec,
+            "status": {"phase": st["phase"]} if "phase" in st else {}}
+
+
+def trim_node(n: Obj, prefix: str = "gputopology.amd.com") -> Obj:
+    """The parts of a Node the extender's cache reads: identity, labels, the topology contract's
+    annotations and the capacity/allocatable counts (``status.images`` alone can be 100 kB a node)."""
+    st = n.get("status") if isinstance(n.get("status"), dict) else {}
+    return {"metadata": _trim_meta(n, prefix, keep_labels=True),
+            "status": {k: st[k] for k in ("capacity", "allocatable") if k in st}}
 
 
 def make_pod(

@@ -248,12 +248,7 @@ class SimCluster:
     def start_extender(self) -> None:
         self.extender = TopologyExtender(self.api, self.ext_cfg)
         if self.use_informer:
-            from ..k8s.informer import Informer
-
-            self.informer = Informer(self.api, self.extender.cache.on_list, self.extender.cache.on_event, watch_timeout=5.0,
-                                     begin_list=self.extender.cache.begin_list,
-                                     backoff=0.1)
-            self.extender.cache.attach_informer(self.informer)
+            self.informer = self.extender.cache.make_informer(watch_timeout=5.0, backoff=0.1, page_size=50)
             self.informer.start()
             self.informer.wait_synced(10.0)
         self.http = HttpExtender(self.extender)

@@ -62,7 +62,9 @@ MUTANTS: List[Mutant] = [
     # overlay / LIST epochs (the cache's view of this process's binds)
     Mutant("cache", CACHE, "                after_bind = list_epoch > self._overlay_epoch.get((st.name, key), 0)",
            "                after_bind = True"),
-    Mutant("cache", CACHE, "                elif after_bind and self.consistent_lists:", "                elif self.consistent_lists:"),
+    Mutant("cache", CACHE, "                elif after_bind and consistent:", "                elif consistent:"),
+    Mutant("cache", CACHE, "        consistent = self.consistent_lists if consistent is None else consistent",
+           "        consistent = self.consistent_lists"),
     Mutant("cache", CACHE, "                self._overlay_epoch[(node, pod)] = self._next_epoch()",
            "                self._overlay_epoch[(node, pod)] = 0"),
     Mutant("cache", CACHE, "            self._overlay_epoch[(node, pod)] = math.inf", "            self._overlay_epoch[(node, pod)] = 0"),
