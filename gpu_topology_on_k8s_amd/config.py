@@ -85,34 +85,95 @@ def scheduler_configuration(resource: str = DEFAULT_RESOURCE, url: Optional[str]
     }
 
 
+PLUGIN_SA = "gpu-topology-device-plugin"
+EXTENDER_SA = "gpu-topology-extender"
+NODE_NAME_CLAIM = "authentication.kubernetes.io/node-name"
+
+
+def rbac_manifests(namespace: str = NAMESPACE) -> List[Dict[str, Any]]:
+    """Least-privilege identities: the privileged node agent and the binder no
+    longer share one ServiceAccount.
+
+    * ``gpu-topology-device-plugin`` (every GPU node, privileged): reads pods and its node, patches pod
+      annotations (ASSIGNED / GROUP at Allocate, ``design.md:236-246``) and its node's annotations and
+      labels (topology publication, ``design.md:76-82``), records Events.  No ``pods/binding``, no
+      Leases.  A ``ValidatingAdmissionPolicy`` confines its writes to ITS node — the node named by the
+      ``authentication.kubernetes.io/node-name`` claim of its pod-bound token (k8s >= 1.30) — and the
+      pods bound there, and lets it change only the node's metadata.  A compromised GPU node can then
+      neither bind pods nor relabel, taint or annotate another node.
+    * ``gpu-topology-extender`` (control plane): reads nodes and pods, patches pod annotations,
+      creates ``pods/binding`` (``design.md:119,223-232``), records Events, and keeps the allocation
+      ledger in Leases of its own namespace (a Role there, not cluster-wide; extender/ledger.py).  It
+      holds no write access to Nodes."""
+    core, coord = "", "coordination.k8s.io"
+
+    def role(kind, name, rules, ns=None):
+        md = {"name": name, **({"namespace": ns} if ns else {})}
+        return {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": kind, "metadata": md, "rules": rules}
+
+    def binding(kind, name, role_kind, sa, ns=None):
+        md = {"name": name, **({"namespace": ns} if ns else {})}
+        return {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": kind, "metadata": md,
+                "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": role_kind, "name": name},
+                "subjects": [{"kind": "ServiceAccount", "name": sa, "namespace": namespace}]}
+
+    plugin_user = f"system:serviceaccount:{namespace}:{PLUGIN_SA}"
+    vap = {
+        "apiVersion": "admissionregistration.k8s.io/v1",
+        "kind": "ValidatingAdmissionPolicy",
+        "metadata": {"name": "gpu-topology-device-plugin-own-node"},
+        "spec": {
+            "failurePolicy": "Fail",
+            "matchConstraints": {"resourceRules": [{"apiGroups": [core], "apiVersions": ["v1"], "operations": ["UPDATE"],
+                                                    "resources": ["nodes", "pods"]}]},
+            "matchConditions": [{"name": "device-plugin", "expression": f"request.userInfo.username == '{plugin_user}'"}],
+            "validations": [
+                {"expression": f"'{NODE_NAME_CLAIM}' in request.userInfo.extra && "
+                               f"(request.kind.kind == 'Node' ? object.metadata.name : object.spec.nodeName) == "
+                               f"request.userInfo.extra['{NODE_NAME_CLAIM}'][0]",
+                 "message": "the GPU device plugin may only change its own node and the pods bound to it"},
+                {"expression": "request.kind.kind != 'Node' || object.spec == oldObject.spec",
+                 "message": "the GPU device plugin may only change node metadata (annotations, labels)"},
+            ],
+        },
+    }
+    return [
+        {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": PLUGIN_SA, "namespace": namespace}},
+        {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": EXTENDER_SA, "namespace": namespace}},
+        role("ClusterRole", PLUGIN_SA, [
+            {"apiGroups": [core], "resources": ["nodes"], "verbs": ["get", "patch"]},
+            {"apiGroups": [core], "resources": ["pods"], "verbs": ["get", "list", "watch", "patch"]},
+            {"apiGroups": [core], "resources": ["events"], "verbs": ["create", "patch"]},
+        ]),
+        binding("ClusterRoleBinding", PLUGIN_SA, "ClusterRole", PLUGIN_SA),
+        vap,
+        {"apiVersion": "admissionregistration.k8s.io/v1", "kind": "ValidatingAdmissionPolicyBinding",
+         "metadata": {"name": "gpu-topology-device-plugin-own-node"},
+         "spec": {"policyName": "gpu-topology-device-plugin-own-node", "validationActions": ["Deny"]}},
+        role("ClusterRole", EXTENDER_SA, [
+            {"apiGroups": [core], "resources": ["nodes"], "verbs": ["get", "list", "watch"]},
+            {"apiGroups": [core], "resources": ["pods"], "verbs": ["get", "list", "watch", "patch"]},
+            {"apiGroups": [core], "resources": ["pods/binding"], "verbs": ["create"]},
+            {"apiGroups": [core], "resources": ["events"], "verbs": ["create", "patch"]},
+        ]),
+        binding("ClusterRoleBinding", EXTENDER_SA, "ClusterRole", EXTENDER_SA),
+        role("Role", f"{EXTENDER_SA}-ledger", [
+            {"apiGroups": [coord], "resources": ["leases"], "verbs": ["get", "list", "watch", "create", "patch"]},
+        ], ns=namespace),
+        binding("RoleBinding", f"{EXTENDER_SA}-ledger", "Role", EXTENDER_SA, ns=namespace),
+    ]
+
+
 def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, namespace: str = NAMESPACE,
                      probe: str = "quick", policy: str = "exact", time_slices: int = 1, partition_control: bool = False) -> str:
     """The DaemonSets, RBAC and scheduler config.  ``time_slices > 1``: the device plugin advertises
     every GPU as that many time slices (fractional pods; topology/shares.py).  ``partition_control``:
     the plugin switches compute / memory partition modes on the node labels' request
     (deviceplugin/repartition.py), which writes the GPUs' sysfs, so /sys is mounted writable."""
-    sa = "gpu-topology"
     labels = {"app.kubernetes.io/part-of": "gpu-topology-amd"}
-    docs: List[Dict[str, Any]] = [
-        {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": sa, "namespace": namespace}},
-        {
-            "apiVersion": "rbac.authorization.k8s.io/v1",
-            "kind": "ClusterRole",
-            "metadata": {"name": "gpu-topology"},
-            "rules": [
-                {"apiGroups": [""], "resources": ["nodes"], "verbs": ["get", "list", "watch", "patch"]},
-                {"apiGroups": [""], "resources": ["pods"], "verbs": ["get", "list", "watch", "patch", "update"]},
-                {"apiGroups": [""], "resources": ["pods/binding", "bindings"], "verbs": ["create"]},
-                {"apiGroups": [""], "resources": ["events"], "verbs": ["create", "patch"]},
-            ],
-        },
-        {
-            "apiVersion": "rbac.authorization.k8s.io/v1",
-            "kind": "ClusterRoleBinding",
-            "metadata": {"name": "gpu-topology"},
-            "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole", "name": "gpu-topology"},
-            "subjects": [{"kind": "ServiceAccount", "name": sa, "namespace": namespace}],
-        },
+    docs: List[Dict[str, Any]] = rbac_manifests(namespace)
+    plugin_sa, ext_sa = PLUGIN_SA, EXTENDER_SA
+    docs += [
         {
             "apiVersion": "apps/v1",
             "kind": "DaemonSet",
@@ -122,7 +183,7 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
                 "template": {
                     "metadata": {"labels": {"name": "amd-gpu-topology-device-plugin", **labels}},
                     "spec": {
-                        "serviceAccountName": sa,
+                        "serviceAccountName": plugin_sa,
                         "priorityClassName": "system-node-critical",
                         "nodeSelector": {"feature.node.kubernetes.io/amd-gpu": "true"},
                         "tolerations": [{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}],
@@ -183,7 +244,7 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
                 "template": {
                     "metadata": {"labels": {"name": "gpu-topology-scheduler-extender", **labels}},
                     "spec": {
-                        "serviceAccountName": sa,
+                        "serviceAccountName": ext_sa,
                         "hostNetwork": True,  # kube-scheduler reaches it on 127.0.0.1:32743 (design.md:98)
                         "nodeSelector": {"node-role.kubernetes.io/control-plane": ""},
                         "tolerations": [{"key": "node-role.kubernetes.io/control-plane", "operator": "Exists",
@@ -193,7 +254,8 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
                             "image": image,
                             "command": ["python3", "-m", "gpu_topology_on_k8s_amd.extender", f"--resource-name={resource}",
                                         "--host=127.0.0.1", f"--port={DEFAULT_PORT}", f"--policy={policy}", "--informer=on",
-                                        "--scheduler-names=default-scheduler"],
+                                        "--scheduler-names=default-scheduler", "--ledger-store=lease",
+                                        f"--ledger-namespace={namespace}"],
                             "readinessProbe": {"httpGet": {"host": "127.0.0.1", "path": "/healthz", "port": DEFAULT_PORT}},
                             "livenessProbe": {"httpGet": {"host": "127.0.0.1", "path": "/healthz", "port": DEFAULT_PORT}},
                             "resources": {"requests": {"cpu": "200m", "memory": "256Mi"}, "limits": {"memory": "2Gi"}},

@@ -120,6 +120,9 @@ def main(argv=None) -> int:
                     help="kubelet pod-resources API; GROUP annotations are reconciled against it ('' = off)")
     ap.add_argument("--reconcile-interval", type=float, default=10.0,
                     help="seconds between pod-resources reconciliation passes (0 = off)")
+    ap.add_argument("--admission-settle", type=float, default=5.0,
+                    help="a Pending pod is reconciled only once no Allocate has come for this many seconds (the "
+                         "kubelet allocates a pod container by container)")
     ap.add_argument("--reprobe-interval", type=float, default=0.0,
                     help="re-measure the links (child process) every N s while no pod holds a device; 0 = never")
     ap.add_argument("--reprobe-tolerance", type=float, default=0.15,
@@ -238,7 +241,7 @@ def main(argv=None) -> int:
                        reprobe_tolerance=a.reprobe_tolerance, pod_resources_socket=a.pod_resources_socket,
                        probe_mark_s=a.probe_mark_seconds, probe_settle_s=a.probe_settle_seconds,
                        probe_yield_s=a.probe_yield_seconds,
-                       reconcile_interval=a.reconcile_interval, cdi_dir=a.cdi_dir, nic_env=a.nic_env == "on",
+                       reconcile_interval=a.reconcile_interval, admission_settle_s=a.admission_settle, cdi_dir=a.cdi_dir, nic_env=a.nic_env == "on",
                        share_cu_mask=a.share_cu_mask == "on", share_guard=a.share_guard, guard_dir=a.share_guard_dir,
                        policy=PlacementPolicy(partition_aware=a.partition_aware == "on"))
     events = None

@@ -8,6 +8,7 @@ in-cluster apiserver (or ``--apiserver URL``).
 from __future__ import annotations
 
 import argparse
+import os
 import logging
 import sys
 
@@ -52,10 +53,15 @@ def main(argv=None) -> int:
     ap.add_argument("--client-ca", default="",
                     help="require callers to present a certificate signed by this CA (mutual TLS; kube-scheduler's "
                          "extender tlsConfig.certFile/keyFile) — needed before serving beyond loopback")
+    ap.add_argument("--ledger-store", default="lease", choices=["lease", "node", "both"],
+                    help="where the allocation ledger lives: a coordination.k8s.io Lease per node (default), the "
+                         "round-5 Node annotation, or both during a rolling upgrade (docs/MIGRATION.md)")
+    ap.add_argument("--ledger-namespace", default=os.environ.get("POD_NAMESPACE", "kube-system"),
+                    help="namespace of the ledger Leases (the extender's own)")
     ap.add_argument("--bind-ledger", default="on", choices=["on", "off"],
-                    help="record every bind's devices in the node's allocation ledger (<prefix>/gpu-ledger) with the "
-                         "node's resourceVersion as a precondition, so extender replicas never hand out one GPU twice "
-                         "(needs `patch` on nodes); off = the per-process node lock only (a single extender)")
+                    help="record every bind's devices in the node's allocation ledger (<prefix>/gpu-ledger, see "
+                         "--ledger-store) with the ledger's resourceVersion as a precondition, so extender replicas never "
+                         "hand out one GPU twice; off = the per-process node lock only (a single extender)")
     ap.add_argument("--log-level", default="INFO")
     a = ap.parse_args(argv)
     logging.basicConfig(level=a.log_level, format='{"ts":"%(asctime)s","lvl":"%(levelname)s","mod":"%(name)s","msg":"%(message)s"}')
@@ -67,7 +73,7 @@ def main(argv=None) -> int:
                          policy=PlacementPolicy(tie_break=a.tie_break, partition_aware=a.partition_aware == "on"),
                          assume_ttl=a.assume_ttl, resync_s=a.resync,
                          scheduler_names=tuple(x.strip() for x in a.scheduler_names.split(",") if x.strip()),
-                         ledger=a.bind_ledger == "on")
+                         ledger=a.bind_ledger == "on", ledger_store=a.ledger_store, ledger_namespace=a.ledger_namespace)
     ext = TopologyExtender(api, cfg)
     if a.informer == "on":
         ext.cache.make_informer(page_size=a.list_page_size, watch_cache=a.list_from_watch_cache == "on").start()

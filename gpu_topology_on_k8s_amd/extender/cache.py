@@ -22,12 +22,14 @@ import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, Iterable, List, Optional, Set, Tuple
 
-from ..k8s.annotations import Contract, PodAssignment, decode_node_annotations, ledger_gen, parse_ledger, probing_until
+from ..k8s.annotations import (Contract, PodAssignment, decode_node_annotations, ledger_gen, ledger_uids, parse_ledger,
+                               probing_until)
 from ..k8s.api import KubeAPI
 from ..k8s.objects import annotations as obj_annotations
 from ..k8s.objects import labels as obj_labels
 from ..k8s.objects import meta, pod_gpu_request, pod_is_terminal, pod_key, pod_node
 from ..topology.model import Topology
+from .ledger import LedgerStore, lease_node
 
 log = logging.getLogger(__name__)
 
@@ -73,8 +75,43 @@ class NodeState:
     # key -> (ids, writer time, first seen here): a re-written entry (a new incarnation of the pod name)
     # is a new entry and ages from when it was first seen
     ledger_seen: Dict[str, Tuple[Tuple[int, ...], float, float]] = field(default_factory=dict)
-    ledger_gen: int = 0
-    settled: Set[str] = field(default_factory=set)
+    # the ledger's sources (extender/ledger.py): the node's Lease and/or its Node annotation; `ledger`
+    # is their union.  `lease_rv` None = no Lease for this node yet (the next bind creates it)
+    ledger_lease: Dict[str, Tuple[Tuple[int, ...], float]] = field(default_factory=dict)
+    ledger_node: Dict[str, Tuple[Tuple[int, ...], float]] = field(default_factory=dict)
+    gen_lease: int = 0
+    gen_node: int = 0
+    uid_lease: Dict[str, str] = field(default_factory=dict)
+    uid_node: Dict[str, str] = field(default_factory=dict)
+    lease_rv: Optional[str] = None
+    ledger_uid: Dict[str, str] = field(default_factory=dict)  # pod UID an entry records (extender/ledger.py)
+    # ledger entries whose pod a LIST or the watch has shown bound on this node, by key -> the entry's
+    # identity (bind time, pod UID).  An entry that records its pod's UID settles for good once THAT pod is seen (its own
+    # annotation governs from then on, also after it ends); a re-created pod of the same name is another
+    # UID and writes another entry.  An entry without a UID (a round-5 writer) is settled only while the
+    # pod is shown, as before
+    settled_at: Dict[str, Tuple[float, str]] = field(default_factory=dict)  # key -> (bind time, pod UID)
+    # pod key -> UID of the pods the last LIST / the watch show on this node: their ledger entries
+    # settle whichever arrives first (the pod's watch event or the ledger's)
+    present: Dict[str, str] = field(default_factory=dict)
+
+    @property
+    def settled(self) -> Set[str]:
+        return set(self.settled_at)
+
+    def resettle(self) -> bool:
+        """Recompute ``settled_at`` from ``ledger`` and ``present`` -> changed.  Call with ``lock`` held."""
+        new = {}
+        for k, (_, t) in self.ledger.items():
+            uid = self.ledger_uid.get(k, "")
+            if uid:
+                if self.settled_at.get(k) == (t, uid) or self.present.get(k) == uid:
+                    new[k] = (t, uid)
+            elif k in self.present:
+                new[k] = (t, "")
+        changed = new != self.settled_at
+        self.settled_at = new
+        return changed
     synced_at: float = 0.0
     list_epoch: int = -1  # epoch of the newest pod LIST applied (older LISTs arriving late are stale)
     lock: threading.RLock = field(default_factory=threading.RLock, repr=False)
@@ -105,6 +142,9 @@ class NodeState:
         seen = self.ledger_seen.get(key)
         return seen[2] if seen is not None else now
 
+    def ledger_live_uids(self, now: float, ttl: float) -> Dict[str, str]:
+        return {k: self.ledger_uid[k] for k in self.ledger_live(now, ttl) if k in self.ledger_uid}
+
     def ledger_live(self, now: float, ttl: float, grace: float = None) -> Dict[str, Tuple[Tuple[int, ...], float]]:
         """Ledger entries that still hold their devices: binds in flight -- seen by this cache for at
         most ``grace`` (and ``ttl``), written at most ``grace`` + LEDGER_CLOCK_SKEW_S ago by the writer's
@@ -112,7 +152,7 @@ class NodeState:
         drops (a settled pod's annotation governs; an entry past the grace is a failed bind)."""
         g_s = min(ttl, LEDGER_GRACE_S if grace is None else grace)
         return {k: (g, t) for k, (g, t) in self.ledger.items()
-                if k not in self.settled and now - self._first_seen(k, now) <= g_s
+                if k not in self.settled_at and now - self._first_seen(k, now) <= g_s
                 and now - t <= g_s + LEDGER_CLOCK_SKEW_S}
 
     @property
@@ -140,9 +180,10 @@ class NodeState:
 class ClusterCache:
     def __init__(self, api: KubeAPI, contract: Contract = Contract(), assume_ttl: float = 300.0,
                  resync_s: float = 5.0, clock: Callable[[], float] = time.time,
-                 resource_aliases: Iterable[str] = ()):
+                 resource_aliases: Iterable[str] = (), ledger: Optional[LedgerStore] = None):
         self.api = api
         self.contract = contract
+        self.ledger = ledger or LedgerStore("lease", contract=contract)
         self.ttl = float(assume_ttl)
         self.resync_s = float(resync_s)
         self.clock = clock
@@ -184,18 +225,10 @@ class ClusterCache:
                 st.node_rv = rv
             st.labels = labels
             st.probing_until = probing_until(obj_annotations(node), self.contract)
-            ledger = parse_ledger(obj_annotations(node), self.contract)
-            st.ledger_gen = ledger_gen(obj_annotations(node), self.contract)
-            if ledger != st.ledger:
-                st.ledger = ledger
-                st.settled &= set(ledger)
-                st.bump()
-            now = self.clock()
-            seen = {}
-            for k, (ids, at) in ledger.items():
-                prev = st.ledger_seen.get(k)
-                seen[k] = prev if prev is not None and prev[:2] == (ids, at) else (ids, at, now)
-            st.ledger_seen = seen
+            st.ledger_node = parse_ledger(obj_annotations(node), self.contract) if self.ledger.uses_node else {}
+            st.uid_node = ledger_uids(obj_annotations(node), self.contract) if self.ledger.uses_node else {}
+            st.gen_node = ledger_gen(obj_annotations(node), self.contract)
+            self._apply_ledger(st)
             alloc = ((node.get("status") or {}).get("allocatable") or {})
             st.capacity = -1
             for r in self.resources:
@@ -206,6 +239,55 @@ class ClusterCache:
                         pass
                     break
         return st
+
+    def _apply_ledger(self, st: NodeState) -> None:
+        """With ``st.lock`` held: ``st.ledger`` = the union of the ledger's sources (the newer bind of a
+        key wins), and the first-seen times of its entries (ledger_live)."""
+        ledger = dict(st.ledger_node)
+        uids = dict(st.uid_node)
+        for k, v in st.ledger_lease.items():
+            if k not in ledger or v[1] >= ledger[k][1]:
+                ledger[k] = v
+                uids.pop(k, None)
+                if k in st.uid_lease:
+                    uids[k] = st.uid_lease[k]
+        changed = ledger != st.ledger or uids != st.ledger_uid
+        st.ledger = ledger
+        st.ledger_uid = uids
+        if st.resettle() or changed:
+            st.bump()
+        now = self.clock()
+        seen = {}
+        for k, (ids, at) in ledger.items():
+            prev = st.ledger_seen.get(k)
+            seen[k] = prev if prev is not None and prev[:2] == (ids, at) else (ids, at, now)
+        st.ledger_seen = seen
+
+    def update_lease_object(self, node: str, lease: Optional[dict]) -> None:
+        """The node's ledger Lease as read or watched (None: it does not exist / was deleted)."""
+        st = self._state(node)
+        with st.lock:
+            if lease is None:
+                st.ledger_lease, st.gen_lease, st.lease_rv, st.uid_lease = {}, 0, None, {}
+            else:
+                ann = obj_annotations(lease)
+                st.ledger_lease = parse_ledger(ann, self.contract)
+                st.uid_lease = ledger_uids(ann, self.contract)
+                st.gen_lease = ledger_gen(ann, self.contract)
+                st.lease_rv = str(meta(lease).get("resourceVersion", "")) or None
+            self._apply_ledger(st)
+
+    def replace_leases(self, leases: List[dict]) -> None:
+        """A full LIST of the ledger namespace's Leases."""
+        by_node = {}
+        for lease in leases:
+            n = lease_node(lease, self.contract)
+            if n is not None:
+                by_node[n] = lease
+        with self._lock:
+            names = set(self._nodes) | set(by_node)
+        for n in names:
+            self.update_lease_object(n, by_node.get(n))
 
     # ------------------------------------------------------------------ pods -> usage
     def _pod_alloc(self, pod: dict) -> Tuple[Optional[Alloc], int]:
@@ -242,8 +324,10 @@ class ClusterCache:
         unknown: Dict[str, int] = {}
         unknown_uids: Dict[str, str] = {}
         seen = set()
+        shown: Dict[str, str] = {}
         for p in pods:
             seen.add(pod_key(p))
+            shown[pod_key(p)] = str(meta(p).get("uid", ""))
             a, u = self._pod_alloc(p)
             if u:
                 unknown[pod_key(p)] = u
@@ -277,16 +361,17 @@ class ClusterCache:
         st.unknown_uids = unknown_uids
         # a key stays settled only while the LIST shows it: a pod name that comes back (a StatefulSet
         # pod re-created) with a new bind in flight is a new entry no LIST has shown yet
-        settled = (st.settled & seen) | (seen & set(st.ledger))
-        if settled != st.settled:
-            st.settled = settled
+        st.present = shown
+        if st.resettle():
             st.bump()
         st.synced_at = now
 
     def refresh_node(self, name: str) -> NodeState:
-        """Authoritative re-read of one node and its pods (used before every bind)."""
+        """Authoritative re-read of one node, its ledger Lease and its pods (used before every bind)."""
         node = self.api.get_node(name)
         st = self.update_node_object(node)
+        if self.ledger.uses_lease:
+            self.update_lease_object(name, self.ledger.read_lease(self.api, name))
         epoch = self._next_epoch()
         pods = self.api.list_pods(node_name=name)
         with st.lock:
@@ -355,10 +440,15 @@ class ClusterCache:
         prefix = self.contract.prefix
 
         def transform(kind: str, o: dict) -> dict:
+            if kind == "Lease":
+                return o
             return trim_pod(o, prefix) if kind == "Pod" else trim_node(o, prefix)
 
         kw.setdefault("field_selectors", {"Pod": LIVE_POD_SELECTOR})
         kw.setdefault("transform", transform)
+        if self.ledger.uses_lease:  # the other extenders' binds in flight
+            kw.setdefault("kinds", ("Node", "Pod", "Lease"))
+            kw.setdefault("namespaces", {"Lease": self.ledger.namespace})
         inf = Informer(self.api, self.on_list, self.on_event, begin_list=self.begin_list, **kw)
         self.attach_informer(inf)
         return inf
@@ -368,6 +458,8 @@ class ClusterCache:
             self.replace_nodes(items)
         elif kind == "Pod":
             self.replace_pods(items, epoch, consistent)
+        elif kind == "Lease":
+            self.replace_leases(items)
         with self._lock:
             self._last_full = self.clock()
 
@@ -433,6 +525,11 @@ class ClusterCache:
 
     # ------------------------------------------------------------------ watch events (fake / informer)
     def on_event(self, event: str, kind: str, obj: dict) -> None:
+        if kind == "Lease":
+            n = lease_node(obj, self.contract)
+            if n is not None:
+                self.update_lease_object(n, None if event == "DELETED" else obj)
+            return
         if kind == "Node":
             if event == "DELETED":
                 with self._lock:
@@ -452,10 +549,14 @@ class ClusterCache:
             if event == "DELETED" or pod_is_terminal(obj):
                 st.allocs.pop(key, None)
                 st.unknown_pods.pop(key, None)
-                st.settled.discard(key)
+                st.present.pop(key, None)  # its ledger entry stays settled: the pod was seen, then ended
                 with self._lock:
                     self._overlay.get(node, {}).pop(key, None)
                 return
+            # the watch shows the pod bound on the node, as a LIST would: from now on its own annotation
+            # governs, and its ledger entry no longer holds devices once the pod ends
+            st.present[key] = str(meta(obj).get("uid", ""))
+            st.resettle()
             a, u = self._pod_alloc(obj)
             if a is not None:
                 st.allocs[key] = a  # the apiserver has the assignment: authoritative over the overlay

@@ -41,7 +41,7 @@ from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
-from ..k8s.annotations import ANN_ASSIGNED, ANN_ASSUME_TIME, ANN_GROUP, Contract, PodAssignment, dump_ledger
+from ..k8s.annotations import ANN_ASSIGNED, ANN_ASSUME_TIME, ANN_GROUP, Contract, PodAssignment
 from ..k8s.api import ApiError, Conflict, KubeAPI
 from ..k8s.events import record_event
 from ..k8s.objects import annotations as obj_annotations
@@ -55,6 +55,7 @@ from ..topology.cpus import access_costs, recommended_cpuset
 from ..topology.model import Topology
 from ..topology.shares import slices_per_gpu
 from .cache import ClusterCache, NodeState
+from .ledger import LedgerStore
 from .metrics import ExtenderMetrics
 
 log = logging.getLogger(__name__)
@@ -92,6 +93,11 @@ class ExtenderConfig:
     # re-reads the node and re-decides, up to `ledger_attempts` times
     ledger: bool = True
     ledger_attempts: int = 8
+    # where the ledger lives (extender/ledger.py): one coordination.k8s.io Lease per node in
+    # `ledger_namespace` ("lease"), the round-5 Node annotation ("node"), or both during a rolling
+    # upgrade between the two ("both"; docs/MIGRATION.md)
+    ledger_store: str = "lease"
+    ledger_namespace: str = "kube-system"
 
 
 @dataclass
@@ -127,8 +133,9 @@ class TopologyExtender:
         self.api = api
         self.cfg = config or ExtenderConfig()
         self.clock = clock
+        self.ledger = LedgerStore(self.cfg.ledger_store, self.cfg.ledger_namespace, self.cfg.contract)
         self.cache = ClusterCache(api, self.cfg.contract, self.cfg.assume_ttl, self.cfg.resync_s, clock=clock,
-                                  resource_aliases=self.cfg.resource_aliases)
+                                  resource_aliases=self.cfg.resource_aliases, ledger=self.ledger)
         self.metrics = metrics or ExtenderMetrics()
         self.metrics.attach_cache(self.cache, self.cfg.assume_ttl, clock)
         self._rng = random.Random(self.cfg.seed)
@@ -492,23 +499,30 @@ class TopologyExtender:
                     d = dataclasses.replace(d, cpuset=recommended_cpuset(st.topology, d.ids))  # memo entries stay unshared
                     now = self.clock()
                     if self.cfg.ledger:
-                        # across processes: record the set on the Node, conditional on the node being
-                        # exactly what this decision saw; another extender's bind in between -> 409
+                        # across processes: record the set in the node's ledger, conditional on the
+                        # ledger being exactly what this decision saw; another extender's bind in
+                        # between -> 409
                         entries = st.ledger_live(now, self.cfg.assume_ttl)
                         entries[key] = (tuple(d.ids), now)
-                        gen = st.ledger_gen + 1
+                        uids = st.ledger_live_uids(now, self.cfg.assume_ttl)
+                        uids[key] = uid or str(meta(pod).get("uid", ""))
                         try:
-                            self.api.patch_node(node, annotations={self.cfg.contract.ledger_key: dump_ledger(entries, gen)},
-                                                resource_version=st.node_rv)
+                            self.ledger.write(self.api, node, entries, st.lease_rv, st.gen_lease, st.node_rv, st.gen_node,
+                                              uids)
                         except Conflict:
                             self.metrics.ledger_conflicts += 1
                             self.metrics.ledger_conflict.inc()
-                            log.info("bind %s on %s: node changed since the decision (attempt %d); re-deciding",
+                            log.info("bind %s on %s: ledger changed since the decision (attempt %d); re-deciding",
                                      key, node, attempt + 1)
                             continue
                         except ApiError as e:
-                            if e.code == 403:  # RBAC without `patch` on nodes: say what to fix, then fail the bind
-                                raise ApiError(403, f"bind {key} on {node}: the allocation ledger needs `patch` on nodes "
+                            if e.code == 403:  # RBAC without the ledger's verbs: say what to fix, then fail the bind
+                                need = []
+                                if self.ledger.uses_lease:
+                                    need.append(f"`create`/`patch` on leases.coordination.k8s.io in {self.ledger.namespace}")
+                                if self.ledger.uses_node:
+                                    need.append("`patch` on nodes")
+                                raise ApiError(403, f"bind {key} on {node}: the allocation ledger needs {' and '.join(need)} "
                                                     f"for the extender's service account (or run with --bind-ledger off "
                                                     f"for a single extender): {e}") from e
                             raise
@@ -560,18 +574,9 @@ class TopologyExtender:
     def _ledger_release(self, node: str, key: str, attempts: int = 4) -> None:
         """Drop ``key``'s ledger entry after a failed bind (best effort; the entry also lapses on its own
         once older than the grace period with no such pod on the node)."""
-        from ..k8s.annotations import ledger_gen, parse_ledger
-
         for _ in range(attempts):
             try:
-                n = self.api.get_node(node)
-                ann = obj_annotations(n)
-                entries = parse_ledger(ann, self.cfg.contract)
-                if key not in entries:
-                    return
-                del entries[key]
-                self.api.patch_node(node, annotations={self.cfg.contract.ledger_key: dump_ledger(entries, ledger_gen(ann, self.cfg.contract) + 1)},
-                                    resource_version=str(meta(n).get("resourceVersion", "")))
+                self.ledger.release(self.api, node, key)
                 return
             except Conflict:
                 continue

@@ -273,8 +273,21 @@ def ledger_gen(ann: Mapping[str, str], contract: Contract = Contract()) -> int:
         return 0
 
 
-def dump_ledger(entries: Mapping[str, Tuple[Sequence[int], float]], gen: int) -> str:
-    return json.dumps({"gen": int(gen), "a": {k: {"g": [int(i) for i in g], "t": round(float(t), 3)}
+def ledger_uids(ann: Mapping[str, str], contract: Contract = Contract()) -> Dict[str, str]:
+    """Pod UID of each ledger entry that records one (``"u"``; entries of round-5 writers have none)."""
+    try:
+        d = json.loads(ann.get(contract.ledger_key) or "{}")
+        return {str(k): str(v["u"]) for k, v in (d.get("a") or {}).items() if isinstance(v, dict) and v.get("u")}
+    except (ValueError, TypeError, AttributeError):
+        return {}
+
+
+def dump_ledger(entries: Mapping[str, Tuple[Sequence[int], float]], gen: int, uids: Optional[Mapping[str, str]] = None) -> str:
+    """The ledger annotation's value; ``uids`` adds each entry's pod UID (an entry of a re-created pod
+    of the same name is then told apart from its predecessor's)."""
+    uids = uids or {}
+    return json.dumps({"gen": int(gen), "a": {k: {"g": [int(i) for i in g], "t": round(float(t), 3),
+                                                  **({"u": uids[k]} if uids.get(k) else {})}
                                                for k, (g, t) in sorted(entries.items())}}, separators=(",", ":"))
 
 

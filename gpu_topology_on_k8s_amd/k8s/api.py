@@ -95,8 +95,22 @@ class KubeAPI:
         """(items, list resourceVersion) of ``kind`` in {"Node", "Pod"}: one unpaginated LIST."""
         raise NotImplementedError
 
+    # coordination.k8s.io/v1 Lease: the extender's per-node allocation ledger lives in one Lease per node
+    # in its own namespace (extender/ledger.py), so the extender needs no write access to Node objects
+    def get_lease(self, namespace: str, name: str) -> Obj:
+        raise NotImplementedError
+
+    def create_lease(self, namespace: str, lease: Obj) -> Obj:
+        """Create a Lease; 409 Conflict (AlreadyExists) when one of that name exists."""
+        raise NotImplementedError
+
+    def patch_lease(self, namespace: str, name: str, annotations: Dict[str, Optional[str]],
+                    resource_version: Optional[str] = None) -> Obj:
+        """Merge-patch a Lease's annotations; with ``resource_version`` conditional (409 on mismatch)."""
+        raise NotImplementedError
+
     def list_page(self, kind: str, limit: int = 0, continue_token: str = "", resource_version: Optional[str] = None,
-                  field_selector: Optional[str] = None) -> Tuple[List[Obj], str, str]:
+                  field_selector: Optional[str] = None, namespace: Optional[str] = None) -> Tuple[List[Obj], str, str]:
         """One page of a LIST of ``kind``: (items, list resourceVersion, continue token or "").
         ``resource_version="0"`` lets the apiserver answer from its watch cache (no etcd quorum read,
         possibly a little stale; older apiservers then ignore ``limit``); ``None`` is a consistent
@@ -105,9 +119,11 @@ class KubeAPI:
         raise NotImplementedError
 
     def watch_stream(self, kind: str, resource_version: str, timeout: float = 60.0,
-                     stop: Optional[threading.Event] = None, field_selector: Optional[str] = None) -> Iterator[Tuple[str, Obj]]:
+                     stop: Optional[threading.Event] = None, field_selector: Optional[str] = None,
+                     namespace: Optional[str] = None) -> Iterator[Tuple[str, Obj]]:
         """(event type, object) after ``resource_version`` until ``timeout``: the WATCH half.  With a
-        ``field_selector`` an object that stops matching arrives as DELETED."""
+        ``field_selector`` an object that stops matching arrives as DELETED.  ``namespace``: for the
+        namespaced kinds (Lease), that namespace only."""
         raise NotImplementedError
 
 
@@ -238,6 +254,28 @@ class RestKubeAPI(KubeAPI):
 
     _KIND_PATH = {"Node": "/api/v1/nodes", "Pod": "/api/v1/pods"}
 
+    @staticmethod
+    def _lease_path(namespace: str, name: str = "") -> str:
+        p = f"/apis/coordination.k8s.io/v1/namespaces/{quote(namespace)}/leases"
+        return p + (f"/{quote(name)}" if name else "")
+
+    def _kind_path(self, kind: str, namespace: Optional[str]) -> str:
+        if kind == "Lease":
+            return self._lease_path(namespace or "default")
+        return self._KIND_PATH[kind]
+
+    def get_lease(self, namespace, name):
+        return self._do("GET", self._lease_path(namespace, name))
+
+    def create_lease(self, namespace, lease):
+        return self._do("POST", self._lease_path(namespace), lease)
+
+    def patch_lease(self, namespace, name, annotations, resource_version=None):
+        md: Obj = {"annotations": annotations}
+        if resource_version is not None:
+            md["resourceVersion"] = str(resource_version)
+        return self._do("PATCH", self._lease_path(namespace, name), {"metadata": md}, "application/merge-patch+json")
+
     def list_with_version(self, kind: str, node_name: Optional[str] = None) -> Tuple[List[Obj], str]:
         path = self._KIND_PATH[kind]
         if node_name and kind == "Pod":
@@ -245,7 +283,7 @@ class RestKubeAPI(KubeAPI):
         d = self._do("GET", path)
         return d.get("items", []), str((d.get("metadata") or {}).get("resourceVersion", ""))
 
-    def list_page(self, kind, limit=0, continue_token="", resource_version=None, field_selector=None):
+    def list_page(self, kind, limit=0, continue_token="", resource_version=None, field_selector=None, namespace=None):
         q = []
         if limit:
             q.append(f"limit={int(limit)}")
@@ -255,16 +293,17 @@ class RestKubeAPI(KubeAPI):
             q.append("resourceVersion=" + quote(str(resource_version)))
         if field_selector:
             q.append("fieldSelector=" + quote(field_selector))
-        d = self._do("GET", self._KIND_PATH[kind] + ("?" + "&".join(q) if q else ""))
+        d = self._do("GET", self._kind_path(kind, namespace) + ("?" + "&".join(q) if q else ""))
         md = d.get("metadata") or {}
         return d.get("items", []), str(md.get("resourceVersion", "")), str(md.get("continue") or "")
 
     def watch_stream(self, kind: str, resource_version: str, timeout: float = 60.0,
-                     stop: Optional[threading.Event] = None, field_selector: Optional[str] = None) -> Iterator[Tuple[str, Obj]]:
+                     stop: Optional[threading.Event] = None, field_selector: Optional[str] = None,
+                     namespace: Optional[str] = None) -> Iterator[Tuple[str, Obj]]:
         """``GET {path}?watch=1&resourceVersion=..&timeoutSeconds=..&allowWatchBookmarks=true`` read
         line by line; BOOKMARKs are yielded (they carry only a resourceVersion), an ERROR 410 raises
         :class:`Gone`."""
-        url = (f"{self.base}{self._KIND_PATH[kind]}?watch=1&allowWatchBookmarks=true"
+        url = (f"{self.base}{self._kind_path(kind, namespace)}?watch=1&allowWatchBookmarks=true"
                f"&resourceVersion={quote(str(resource_version))}&timeoutSeconds={int(max(1, timeout))}")
         if field_selector:
             url += "&fieldSelector=" + quote(field_selector)

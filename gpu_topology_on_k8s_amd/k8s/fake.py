@@ -71,6 +71,7 @@ class FakeAPIServer(KubeAPI):
         self._rv = 0
         self.nodes: Dict[str, Obj] = {}
         self.pods: Dict[Tuple[str, str], Obj] = {}
+        self.leases: Dict[Tuple[str, str], Obj] = {}  # coordination.k8s.io/v1 Leases by (namespace, name)
         self.events: List[Obj] = []
         self._faults: Dict[str, List[Tuple[int, int]]] = defaultdict(list)  # op -> [(code, remaining)]
         self._watchers: List[Watcher] = []
@@ -128,20 +129,21 @@ class FakeAPIServer(KubeAPI):
         items, rv, _ = self.list_page(kind, field_selector=f"spec.nodeName={node_name}" if node_name and kind == "Pod" else None)
         return items, rv
 
-    def list_page(self, kind, limit=0, continue_token="", resource_version=None, field_selector=None):
+    def list_page(self, kind, limit=0, continue_token="", resource_version=None, field_selector=None, namespace=None):
         """One page of a LIST (``GET ...?limit=&continue=&resourceVersion=&fieldSelector=``).  The
         whole LIST is serialized at its resourceVersion on the first page (a consistent snapshot, as
         the apiserver reads etcd at one revision); later pages are served from it."""
         with self._lock:
-            self._enter("list_nodes" if kind == "Node" else "list_pods")
+            self._enter({"Node": "list_nodes", "Pod": "list_pods"}.get(kind, f"list_{kind}"))
             if continue_token:
                 snap = self._pages.pop(continue_token, None)
                 if snap is None:
                     raise Gone("the provided continue parameter is too old")
                 encoded, list_rv = snap
             else:
-                src = self.nodes if kind == "Node" else self.pods
-                encoded = [json.dumps(o) for _, o in sorted(src.items()) if match_fields(o, field_selector)]
+                src = {"Node": self.nodes, "Pod": self.pods, "Lease": self.leases}[kind]
+                encoded = [json.dumps(o) for _, o in sorted(src.items()) if match_fields(o, field_selector)
+                           and (namespace is None or meta(o).get("namespace") == namespace)]
                 list_rv = str(self._rv)
                 if str(resource_version) == "0" and not self.watch_cache_pages:
                     limit = 0
@@ -168,7 +170,8 @@ class FakeAPIServer(KubeAPI):
             self._watch_cuts[kind].append(after)
 
     def watch_stream(self, kind: str, resource_version: str, timeout: float = 60.0,
-                     stop: Optional[threading.Event] = None, field_selector: Optional[str] = None) -> Iterator[Tuple[str, Obj]]:
+                     stop: Optional[threading.Event] = None, field_selector: Optional[str] = None,
+                     namespace: Optional[str] = None) -> Iterator[Tuple[str, Obj]]:
         """Changes of ``kind`` after ``resource_version``, blocking up to ``timeout`` s for new ones
         (``GET ...?watch=1``).  Raises :class:`Gone` when the window no longer reaches back that far.
         With ``field_selector``, a change to an object that does not match is delivered as DELETED
@@ -186,7 +189,8 @@ class FakeAPIServer(KubeAPI):
             with self._lock:
                 if cut is None and self._watch_cuts.get(kind):  # a cut requested while this watch is open
                     cut = sent + self._watch_cuts[kind].pop(0)
-                batch = [(t, o) for rv, t, k, o in self._history if rv > since and k == kind]
+                batch = [(t, o) for rv, t, k, o in self._history if rv > since and k == kind
+                         and (namespace is None or meta(o).get("namespace") == namespace)]
                 if self._history:
                     since = max(since, self._history[-1][0])
                 if not batch:
@@ -337,6 +341,44 @@ class FakeAPIServer(KubeAPI):
             self._emit("MODIFIED", "Pod", pod)
             return copy.deepcopy(pod)
 
+    def get_lease(self, namespace: str, name: str) -> Obj:
+        with self._lock:
+            self._enter("get_lease")
+            lease = self.leases.get((namespace, name))
+            if lease is None:
+                raise NotFound(f"lease {namespace}/{name}")
+            return copy.deepcopy(lease)
+
+    def create_lease(self, namespace: str, lease: Obj) -> Obj:
+        with self._lock:
+            self._enter("create_lease")
+            lease = copy.deepcopy(lease)
+            md = meta(lease)
+            md["namespace"] = namespace
+            key = (namespace, md["name"])
+            if key in self.leases:
+                raise Conflict(f"leases.coordination.k8s.io \"{md['name']}\" already exists")
+            lease.setdefault("apiVersion", "coordination.k8s.io/v1")
+            lease.setdefault("kind", "Lease")
+            md.setdefault("uid", str(uuid.uuid4()))
+            md["resourceVersion"] = self._next_rv()
+            self.leases[key] = lease
+            self._emit("ADDED", "Lease", lease)
+            return copy.deepcopy(lease)
+
+    def patch_lease(self, namespace, name, annotations, resource_version=None) -> Obj:
+        with self._lock:
+            self._enter("patch_lease")
+            lease = self.leases.get((namespace, name))
+            if lease is None:
+                raise NotFound(f"lease {namespace}/{name}")
+            if resource_version is not None and str(resource_version) != meta(lease).get("resourceVersion"):
+                raise Conflict(f"lease {namespace}/{name}: resourceVersion {resource_version} is stale")
+            _merge(lease, {"metadata": {"annotations": annotations}})
+            meta(lease)["resourceVersion"] = self._next_rv()
+            self._emit("MODIFIED", "Lease", lease)
+            return copy.deepcopy(lease)
+
     def bind_pod(self, namespace: str, name: str, uid: str, node: str) -> None:
         with self._lock:
             self._enter("bind_pod")
@@ -382,6 +424,8 @@ class _Handler(BaseHTTPRequestHandler):
         parts = [unquote(p) for p in u.path.strip("/").split("/")]
         q = parse_qs(u.query)
         try:
+            if parts[:4] == ["apis", "coordination.k8s.io", "v1", "namespaces"] and len(parts) >= 6 and parts[5] == "leases":
+                return self._lease_route(method, parts[4], parts[6] if len(parts) > 6 else "", q)
             if parts[:2] != ["api", "v1"]:
                 raise NotFound(u.path)
             rest = parts[2:]
@@ -427,16 +471,35 @@ class _Handler(BaseHTTPRequestHandler):
         except ApiError as e:
             return self._send(e.code, {"kind": "Status", "status": "Failure", "code": e.code, "message": e.message})
 
+    def _lease_route(self, method: str, ns: str, name: str, q: Dict[str, List[str]]) -> None:
+        if not name and method == "GET":
+            if (q.get("watch") or ["0"])[0] in ("1", "true"):
+                return self._watch("Lease", (q.get("resourceVersion") or ["0"])[0], float((q.get("timeoutSeconds") or ["60"])[0]),
+                                   namespace=ns)
+            items, rv, cont = self.api.list_page("Lease", int((q.get("limit") or ["0"])[0]), (q.get("continue") or [""])[0],
+                                                 (q.get("resourceVersion") or [None])[0], namespace=ns)
+            return self._send(200, {"kind": "LeaseList", "metadata": {"resourceVersion": rv, **({"continue": cont} if cont else {})},
+                                    "items": items})
+        if not name and method == "POST":
+            return self._send(201, self.api.create_lease(ns, self._body()))
+        if name and method == "GET":
+            return self._send(200, self.api.get_lease(ns, name))
+        if name and method == "PATCH":
+            md = self._body().get("metadata", {})
+            return self._send(200, self.api.patch_lease(ns, name, md.get("annotations") or {}, md.get("resourceVersion")))
+        raise NotFound(f"{method} leases/{name}")
+
     def _chunk(self, data: bytes) -> None:
         self.wfile.write(f"{len(data):x}\r\n".encode() + data + b"\r\n")
         self.wfile.flush()
 
-    def _watch(self, kind: str, rv: str, timeout: float, field_selector: Optional[str] = None) -> None:
+    def _watch(self, kind: str, rv: str, timeout: float, field_selector: Optional[str] = None,
+               namespace: Optional[str] = None) -> None:
         """Watch response: one JSON ``{"type", "object"}`` line per chunk (chunked transfer encoding,
         as the apiserver streams it) until ``timeoutSeconds``.  An injected cut drops the connection
         without the final chunk (the client sees a broken stream)."""
         try:
-            stream = self.api.watch_stream(kind, rv, timeout, field_selector=field_selector)
+            stream = self.api.watch_stream(kind, rv, timeout, field_selector=field_selector, namespace=namespace)
             first = next(stream, None)
         except Gone as e:
             return self._send(200, {"type": "ERROR", "object": {"kind": "Status", "code": 410, "reason": "Expired",

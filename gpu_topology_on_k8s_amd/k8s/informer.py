@@ -45,7 +45,8 @@ class Informer:
                  begin_list: Optional[Callable[[str], object]] = None, page_size: int = 500,
                  field_selectors: Optional[Mapping[str, str]] = None,
                  transform: Optional[Callable[[str, Obj], Obj]] = None, watch_cache: bool = True,
-                 max_backoff: float = 30.0, jitter: float = 0.2, seed: Optional[int] = None):
+                 max_backoff: float = 30.0, jitter: float = 0.2, seed: Optional[int] = None,
+                 namespaces: Optional[Mapping[str, str]] = None):
         self.api = api
         self.on_list = on_list
         self.begin_list = begin_list
@@ -57,6 +58,7 @@ class Informer:
         self.jitter = jitter
         self.page_size = int(page_size)
         self.field_selectors = dict(field_selectors or {})
+        self.namespaces = dict(namespaces or {})  # namespaced kinds (Lease): the one namespace watched
         self.transform = transform
         self.watch_cache = watch_cache
         self._rng = random.Random(seed)
@@ -122,7 +124,8 @@ class Informer:
         while True:
             try:
                 page, list_rv, cont = self.api.list_page(kind, limit=self.page_size, continue_token=cont,
-                                                         resource_version=None if cont else rv_param, field_selector=fs)
+                                                         resource_version=None if cont else rv_param, field_selector=fs,
+                                                         namespace=self.namespaces.get(kind))
             except Gone:
                 if not cont:
                     raise
@@ -158,7 +161,8 @@ class Informer:
                     self._synced[kind].set()
                     failures = 0
                 for t, obj in self.api.watch_stream(kind, rv, self.watch_timeout, self._stop,
-                                                    field_selector=self.field_selectors.get(kind)):
+                                                    field_selector=self.field_selectors.get(kind),
+                                                    namespace=self.namespaces.get(kind)):
                     if self._stop.is_set():
                         return
                     failures = 0

@@ -190,8 +190,13 @@ class SimCluster:
                  policy: PlacementPolicy = PlacementPolicy(), assume_ttl: float = 300.0, use_filter: bool = True,
                  node_labels: Optional[Dict[str, Dict[str, str]]] = None, device_specs: str = "strict",
                  prestart_validate: bool = False, validate_fn=None, reconcile_interval: float = 0.0,
-                 informer: bool = False, share_guard: str = "preload"):
+                 informer: bool = False, share_guard: str = "preload", rbac: bool = False):
         self.resource = resource
+        # every component talks to the apiserver as its deploy ServiceAccount (k8s/rbac.py): the
+        # plugins with their node-name claim and the own-node admission policy, the extender with its
+        # ledger Role; the fake kubelet and the mini scheduler keep full access
+        self.rbac = rbac
+        self.denied: List[str] = []
         # drive the extender's cache by LIST+WATCH (production mode) instead of a LIST per request
         self.use_informer = informer
         self.informer = None
@@ -230,6 +235,7 @@ class SimCluster:
             # a time-sliced node is its own pool: its plugin advertises the slice resource (as the
             # daemon does with --time-slices), and amd.com/gpu means whole GPUs everywhere
             res = self.contract.slice_resource if slices_per_gpu(topo) > 1 else self.resource
+            plugin_api = self._as("plugin", name)
             plugin = DevicePluginServer(topo, PluginConfig(resource_name=res, socket_dir=sockdir, node_name=name,
                                                            contract=self.contract, dev_root=dev_root,
                                                            device_specs=self.device_specs,
@@ -238,15 +244,29 @@ class SimCluster:
                                                            reconcile_interval=self.reconcile_interval,
                                                            share_guard=self.share_guard,
                                                            guard_dir=os.path.join(self._root, f"vgpu{i}")),
-                                        api=self.api, validate_fn=self.validate_fn)
+                                        api=plugin_api, validate_fn=self.validate_fn)
             plugin.start()
             kubelet.wait_for(res)
             self.nodes[name] = _Node(name, topo, sockdir, kubelet, plugin, res)
         self.start_extender()
         return self
 
+    def _as(self, who: str, node: str = ""):
+        """The apiserver as the deploy ServiceAccount of ``who`` (plugin / extender) sees it."""
+        if not self.rbac:
+            return self.api
+        import yaml
+
+        from ..config import EXTENDER_SA, NAMESPACE, PLUGIN_SA, render_manifests
+        from ..k8s.rbac import RBACView, identities_from_manifests, sa_username
+
+        ids = identities_from_manifests(yaml.safe_load_all(render_manifests()))
+        view = RBACView(self.api, ids[sa_username(NAMESPACE, PLUGIN_SA if who == "plugin" else EXTENDER_SA)], node_name=node)
+        view.denied = self.denied  # one shared log of refusals
+        return view
+
     def start_extender(self) -> None:
-        self.extender = TopologyExtender(self.api, self.ext_cfg)
+        self.extender = TopologyExtender(self._as("extender"), self.ext_cfg)
         if self.use_informer:
             self.informer = self.extender.cache.make_informer(watch_timeout=5.0, backoff=0.1, page_size=50)
             self.informer.start()

@@ -36,11 +36,14 @@ def test_scheduler_configuration():
 def test_manifests_are_valid_yaml():
     docs = list(yaml.safe_load_all(render_manifests()))
     kinds = [d["kind"] for d in docs]
-    assert kinds == ["ServiceAccount", "ClusterRole", "ClusterRoleBinding", "DaemonSet", "DaemonSet", "ConfigMap"]
-    assert docs[4]["spec"]["template"]["spec"]["nodeSelector"] == {"node-role.kubernetes.io/control-plane": ""}
-    ext = docs[4]["spec"]["template"]["spec"]["containers"][0]
+    assert kinds == ["ServiceAccount", "ServiceAccount", "ClusterRole", "ClusterRoleBinding", "ValidatingAdmissionPolicy",
+                     "ValidatingAdmissionPolicyBinding", "ClusterRole", "ClusterRoleBinding", "Role", "RoleBinding",
+                     "DaemonSet", "DaemonSet", "ConfigMap"]
+    ds, ext_ds = [d for d in docs if d["kind"] == "DaemonSet"]
+    assert ext_ds["spec"]["template"]["spec"]["nodeSelector"] == {"node-role.kubernetes.io/control-plane": ""}
+    ext = ext_ds["spec"]["template"]["spec"]["containers"][0]
     assert "--host=127.0.0.1" in ext["command"] and "ports" not in ext  # /bind is never exposed off-node
-    ds = docs[3]
+    assert "--ledger-store=lease" in ext["command"]
     c = ds["spec"]["template"]["spec"]["containers"][0]
     assert "gpu_topology_on_k8s_amd.deviceplugin" in c["command"]
     assert {"name": "device-plugins", "mountPath": "/var/lib/kubelet/device-plugins"} in c["volumeMounts"]

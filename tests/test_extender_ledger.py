@@ -1,22 +1,62 @@
-"""Bind safety across extender instances (VERDICT r4 next #5).
+"""Bind safety across extender instances (VERDICT r4 next #5, r5 next #3).
 
 Each :class:`TopologyExtender` serialises select -> annotate -> bind per node with an in-process lock,
 but the extender runs as several instances (a DaemonSet on the control-plane nodes; two leaders across
 a scheduler failover).  Every bind therefore records its device set in the node's allocation ledger
-(``<prefix>/gpu-ledger``) with the node's resourceVersion as a precondition; a second instance that
-decided on the same state gets 409, re-reads the node and re-decides.  Two instances share one
+(``<prefix>/gpu-ledger``) with the ledger object's resourceVersion as a precondition; a second instance
+that decided on the same state gets 409, re-reads and re-decides.  Two instances share one
 FakeAPIServer here, which enforces the precondition as the apiserver does; each has its own cache.
+Every test runs with the ledger in a per-node coordination.k8s.io Lease (the default) and in the
+round-5 Node annotation.
 """
 import threading
 
 import pytest
 
 from gpu_topology_on_k8s_amd.extender import ExtenderConfig, TopologyExtender
+from gpu_topology_on_k8s_amd.extender.ledger import lease_name
 from gpu_topology_on_k8s_amd.k8s import Contract, FakeAPIServer
 from gpu_topology_on_k8s_amd.k8s.annotations import encode_node_annotations, parse_ledger
+from gpu_topology_on_k8s_amd.k8s.api import NotFound
 from gpu_topology_on_k8s_amd.k8s.objects import annotations as obj_annotations
 from gpu_topology_on_k8s_amd.k8s.objects import make_node, make_pod
 from gpu_topology_on_k8s_amd.topology import fixtures as fx
+
+STORE = {"store": "lease"}
+NS = "kube-system"
+
+
+@pytest.fixture(autouse=True, params=["lease", "node"])
+def store(request):
+    STORE["store"] = request.param
+    yield request.param
+    STORE["store"] = "lease"
+
+
+def _cfg(**kw):
+    return ExtenderConfig(resync_s=0.0, events=False, ledger_store=STORE["store"], ledger_namespace=NS, **kw)
+
+
+def _ledger(api, node="n1"):
+    """The node's ledger entries where the store in use keeps them."""
+    if STORE["store"] == "node":
+        return parse_ledger(obj_annotations(api.get_node(node)))
+    try:
+        return parse_ledger(obj_annotations(api.get_lease(NS, lease_name(node))))
+    except NotFound:
+        return {}
+
+
+def _set_ledger(api, raw, node="n1"):
+    """Another writer's ledger value, written where the store in use reads it."""
+    c = Contract()
+    if STORE["store"] == "node":
+        api.patch_node(node, annotations={c.ledger_key: raw})
+        return
+    try:
+        api.patch_lease(NS, lease_name(node), {c.ledger_key: raw})
+    except NotFound:
+        api.create_lease(NS, {"metadata": {"name": lease_name(node), "annotations": {c.ledger_key: raw}}})
 
 
 class Clock:
@@ -34,7 +74,7 @@ def _two(ledger=True, n_pods=0, k=1):
     api.create_node(make_node("n1", labels={c.label_model: "MI355X"}, annotations=encode_node_annotations(t, c),
                               capacity={c.resource_name: str(t.n)}))
     clock = Clock()
-    exts = [TopologyExtender(api, ExtenderConfig(resync_s=0.0, ledger=ledger, events=False), clock=clock) for _ in range(2)]
+    exts = [TopologyExtender(api, _cfg(ledger=ledger), clock=clock) for _ in range(2)]
     for i in range(n_pods):
         api.create_pod(make_pod(f"p{i}", gpus=k))
     return api, exts, clock
@@ -131,15 +171,15 @@ def test_ledger_entries_settle_and_lapse():
 
     api, exts, clock = _two(ledger=True, n_pods=3)
     d0 = _bind(api, exts[0], "p0")
-    led = parse_ledger(obj_annotations(api.get_node("n1")))
+    led = _ledger(api)
     assert set(led) == {"default/p0"} and led["default/p0"][0] == d0.ids
     d1 = _bind(api, exts[1], "p1")
-    led = parse_ledger(obj_annotations(api.get_node("n1")))
+    led = _ledger(api)
     assert set(led) == {"default/p1"}  # p0 settled (listed on the node): dropped
     assert not set(d0.ids) & set(d1.ids)
     # a lost bind: recorded, never annotated nor bound
     c = Contract()
-    api.patch_node("n1", annotations={c.ledger_key: dump_ledger({"default/ghost": ((7,), clock.t)}, 99)})
+    _set_ledger(api, dump_ledger({"default/ghost": ((7,), clock.t)}, 99))
     d2 = _bind(api, exts[0], "p2")
     assert 7 not in d2.ids
     api.delete_pod("default", "p2")
@@ -156,7 +196,7 @@ def test_failed_bind_releases_its_ledger_entry():
         _bind(api, exts[0], "p0")
     except Exception:  # noqa: BLE001 - the injected apiserver failure
         pass
-    assert "default/p0" not in parse_ledger(obj_annotations(api.get_node("n1")))
+    assert "default/p0" not in _ledger(api)
 
 
 def test_malformed_or_foreign_ledger_values_do_not_break_binds():
@@ -169,28 +209,29 @@ def test_malformed_or_foreign_ledger_values_do_not_break_binds():
            dump_ledger({"default/other": ((99, -3), 1_700_000_000.0)}, 5)]
     for i, raw in enumerate(bad):
         api, exts, _ = _two(ledger=True, n_pods=1, k=8)
-        api.patch_node("n1", annotations={c.ledger_key: raw})
+        _set_ledger(api, raw)
         d = _bind(api, exts[0], "p0")
         assert sorted(d.ids) == list(range(8)), (raw, d)
-        led = parse_ledger(obj_annotations(api.get_node("n1")))
+        led = _ledger(api)
         assert led["default/p0"][0] == tuple(d.ids)
 
 
-def test_ledger_without_node_patch_rights_fails_the_bind_with_the_fix_and_can_be_turned_off():
-    """RBAC without `patch` on nodes: the ledger write is refused (403) and the bind fails with a
-    message naming the missing verb and --bind-ledger off; with the ledger off the same bind succeeds
-    (a single extender's node lock only)."""
+def test_ledger_without_its_rbac_verbs_fails_the_bind_with_the_fix_and_can_be_turned_off():
+    """RBAC without the ledger's verbs (`create` on leases / `patch` on nodes): the ledger write is
+    refused (403) and the bind fails with a message naming the missing verb and --bind-ledger off; with
+    the ledger off the same bind succeeds (a single extender's node lock only)."""
     import pytest
 
     from gpu_topology_on_k8s_amd.extender.__main__ import main as extender_main  # noqa: F401 - the flag exists
     from gpu_topology_on_k8s_amd.k8s.api import ApiError
 
     api, exts, _ = _two(ledger=True, n_pods=2)
-    api.inject("patch_node", 403, times=100)
+    api.inject("create_lease" if STORE["store"] == "lease" else "patch_node", 403, times=100)
     with pytest.raises(ApiError) as ei:
         _bind(api, exts[0], "p0")
-    assert ei.value.code == 403 and "--bind-ledger off" in str(ei.value) and "patch" in str(ei.value)
-    off = TopologyExtender(api, ExtenderConfig(resync_s=0.0, ledger=False, events=False))
+    want = "leases" if STORE["store"] == "lease" else "`patch` on nodes"
+    assert ei.value.code == 403 and "--bind-ledger off" in str(ei.value) and want in str(ei.value)
+    off = TopologyExtender(api, _cfg(ledger=False))
     assert len(_bind(api, off, "p1").ids) == 1
 
 
@@ -279,8 +320,13 @@ def test_a_newer_node_object_never_meets_an_older_pod_list():
     tb.start()
     assert refreshed.wait(10)
     d0, d1 = _bind(api, a, "p0"), _bind(api, a, "p1")
-    assert "default/p0" not in parse_ledger(obj_annotations(api.get_node("n1")))  # settled, dropped by A
-    tc = threading.Thread(target=lambda: b.cache.update_node_object(api.get_node("n1")))  # B's other refresh
+    assert "default/p0" not in _ledger(api)  # settled, dropped by A
+    def other_refresh():  # B's other refresh: the newer node object and ledger
+        b.cache.update_node_object(api.get_node("n1"))
+        if STORE["store"] == "lease":
+            b.cache.update_lease_object("n1", api.get_lease(NS, lease_name("n1")))
+
+    tc = threading.Thread(target=other_refresh)
     tc.start()
     tc.join(timeout=0.3)
     go.set()
@@ -304,10 +350,10 @@ def test_an_instance_whose_clock_runs_ahead_still_honours_a_bind_in_flight():
     api.create_node(make_node("n1", labels={c.label_model: "MI355X"}, annotations=encode_node_annotations(t, c),
                               capacity={c.resource_name: str(t.n)}))
     behind, ahead = Clock(1_700_000_000.0), Clock(1_700_000_090.0)
-    a = TopologyExtender(api, ExtenderConfig(resync_s=0.0, ledger=True, events=False), clock=behind)
-    b = TopologyExtender(api, ExtenderConfig(resync_s=0.0, ledger=True, events=False), clock=ahead)
+    a = TopologyExtender(api, _cfg(ledger=True), clock=behind)
+    b = TopologyExtender(api, _cfg(ledger=True), clock=ahead)
     # A has recorded its decision (devices 0-3) but not yet annotated or bound the pod
-    api.patch_node("n1", annotations={c.ledger_key: dump_ledger({"default/inflight": ((0, 1, 2, 3), behind.t)}, 1)})
+    _set_ledger(api, dump_ledger({"default/inflight": ((0, 1, 2, 3), behind.t)}, 1))
     api.create_pod(make_pod("big", gpus=5))
     with pytest.raises(Exception):
         _bind(api, b, "big")  # only 4 devices are free: the in-flight entry holds 0-3
@@ -397,3 +443,40 @@ def test_a_reused_pod_name_on_the_same_devices_is_a_new_entry():
     ta.join(timeout=30)
     assert not ta.is_alive()
     assert isinstance(got, NoFeasiblePlacement), got
+
+
+def test_an_ended_pod_s_entry_holds_nothing_once_its_pod_was_seen():
+    """The watch shows the pod bound (its entry settles, whichever of the pod's and the ledger's events
+    comes first); the pod then ends within the grace period: its devices are free at once, not after
+    the entry lapses (found under the informer, where no LIST follows a bind)."""
+    api, exts, clock = _two(ledger=True, n_pods=1, k=4)
+    a, b = exts
+    d = _bind(api, a, "p0")
+    pod = api.get_pod("default", "p0")
+    st = b.cache.get("n1")
+    b.cache.on_event("MODIFIED", "Pod", pod)  # the pod's event first, the ledger's after
+    b.cache.update_lease_object("n1", api.get_lease(NS, lease_name("n1"))) if STORE["store"] == "lease" else \
+        b.cache.update_node_object(api.get_node("n1"))
+    assert "default/p0" in st.ledger and "default/p0" in st.settled
+    api.set_pod_phase("default", "p0", "Succeeded")
+    b.cache.on_event("MODIFIED", "Pod", api.get_pod("default", "p0"))
+    assert not set(d.ids) & st.used(clock.t, 300)  # within the grace, yet free
+
+
+def test_a_mixed_fleet_during_the_ledger_migration_never_shares_a_device():
+    """docs/MIGRATION.md: a round-5 extender (Node annotation) and an upgraded one in `both` mode bind
+    on one node concurrently: each sees the other's binds in flight."""
+    api = FakeAPIServer()
+    c = Contract()
+    t = fx.f7_mi355x()
+    api.create_node(make_node("n1", labels={c.label_model: "MI355X"}, annotations=encode_node_annotations(t, c),
+                              capacity={c.resource_name: str(t.n)}))
+    old = TopologyExtender(api, ExtenderConfig(resync_s=0.0, events=False, ledger_store="node"))
+    new = TopologyExtender(api, ExtenderConfig(resync_s=0.0, events=False, ledger_store="both", ledger_namespace=NS))
+    for i in range(2):
+        api.create_pod(make_pod(f"p{i}", gpus=1))
+    _lockstep([old, new])
+    out = _race(api, [old, new])
+    assert not set(out[0]) & set(out[1]), out
+    assert parse_ledger(obj_annotations(api.get_node("n1")))  # the old writer's view is kept current
+    assert parse_ledger(obj_annotations(api.get_lease(NS, lease_name("n1"))))

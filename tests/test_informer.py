@@ -163,12 +163,12 @@ def test_gone_relists_and_expired_continue_restarts_consistently():
     real = api.list_page
     first = {"done": False}
 
-    def list_page(kind, limit=0, continue_token="", resource_version=None, field_selector=None):
+    def list_page(kind, limit=0, continue_token="", resource_version=None, field_selector=None, namespace=None):
         if kind == "Pod" and continue_token and not first["done"]:
             first["done"] = True
             api.expire_continue_tokens()  # compaction between page 1 and page 2
         lists.append((kind, bool(continue_token), resource_version))
-        return real(kind, limit, continue_token, resource_version, field_selector)
+        return real(kind, limit, continue_token, resource_version, field_selector, namespace)
 
     api.list_page = list_page
     got = {}

@@ -35,6 +35,7 @@ class Mutant:
 
 CACHE = "gpu_topology_on_k8s_amd/extender/cache.py"
 SCHED = "gpu_topology_on_k8s_amd/extender/scheduler.py"
+LEDGER = "gpu_topology_on_k8s_amd/extender/ledger.py"
 PLUGIN = "gpu_topology_on_k8s_amd/deviceplugin/plugin.py"
 DP = "gpu_topology_on_k8s_amd/parallel/dp.py"
 GUARD = "csrc/vgpu/vgpu_guard.cpp"
@@ -45,14 +46,18 @@ ANN = "gpu_topology_on_k8s_amd/k8s/annotations.py"
 
 MUTANTS: List[Mutant] = [
     # allocation ledger (cross-extender bind safety)
-    Mutant("ledger", CACHE, "if k not in self.settled and now - self._first_seen(k, now) <= g_s",
+    Mutant("ledger", CACHE, "if k not in self.settled_at and now - self._first_seen(k, now) <= g_s",
            "if now - self._first_seen(k, now) <= g_s"),
     Mutant("ledger", CACHE, "            if key not in self.allocs:  # being bound by another extender",
            "            if False:  # being bound by another extender"),
-    Mutant("ledger", SCHED, "resource_version=st.node_rv)", "resource_version=None)"),
+    Mutant("ledger", LEDGER, "                api.patch_lease(self.namespace, lease_name(node), {key: value}, resource_version=lease_rv)",
+           "                api.patch_lease(self.namespace, lease_name(node), {key: value}, resource_version=None)"),
+    Mutant("ledger", LEDGER, "            api.patch_node(node, annotations={key: dump_ledger(entries, node_gen + 1, uids)}, resource_version=node_rv)",
+           "            api.patch_node(node, annotations={key: dump_ledger(entries, node_gen + 1, uids)}, resource_version=None)"),
+    Mutant("ledger", CACHE, "            st.present[key] = str(meta(obj).get(\"uid\", \"\"))\n            st.resettle()", "            pass"),
     Mutant("ledger", SCHED, "                        entries[key] = (tuple(d.ids), now)", "                        pass"),
-    Mutant("ledger", CACHE, "        settled = (st.settled & seen) | (seen & set(st.ledger))",
-           "        settled = st.settled | (seen & set(st.ledger))"),
+    Mutant("ledger", CACHE, "                if self.settled_at.get(k) == (t, uid) or self.present.get(k) == uid:",
+           "                if k in self.settled_at or k in self.present:"),
     Mutant("ledger", CACHE, "seen[k] = prev if prev is not None and prev[:2] == (ids, at) else (ids, at, now)",
            "seen[k] = prev if prev is not None and prev[0] == ids else (ids, at, now)"),
     Mutant("ledger", SCHED, "                self._ledger_release(node, key)", "                pass"),
@@ -156,7 +161,8 @@ MUTANTS: List[Mutant] = [
 ]
 
 TESTS = {
-    "ledger": ["tests/test_extender_ledger.py", "tests/test_extender.py", "tests/test_cluster_features.py", "tests/test_churn.py"],
+    "ledger": ["tests/test_extender_ledger.py", "tests/test_extender.py", "tests/test_cluster_features.py", "tests/test_churn.py",
+               "tests/test_rbac.py"],
     "cache": ["tests/test_cluster_features.py", "tests/test_extender.py", "tests/test_extender_ledger.py", "tests/test_churn.py"],
     "plugin": ["tests/test_deviceplugin.py", "tests/test_cluster_features.py", "tests/test_preferred_allocation_props.py",
                "tests/test_daemons.py", "tests/test_health.py", "tests/test_sim.py", "tests/test_churn.py",
