@@ -73,6 +73,13 @@ def parse(argv=None):
                     help="after the headline: time the same all-reduce on the WORST k-subset the placement core found "
                          "(a second communicator on those devices) and report the placement gain; auto = whenever a "
                          "distinct worst subset exists (k < devices on the node)")
+    ap.add_argument("--ab-default", default="auto", choices=["auto", "on", "off"],
+                    help="after the headline: also time the k-subset the kubelet hands out with no extender (lowest "
+                         "free indices; the paper's default-Kubernetes comparator, p.7 Figs. 11-12) when it differs "
+                         "from the chosen one")
+    ap.add_argument("--topology-json", default="",
+                    help="place on this node model (Topology JSON, e.g. a fixture with a degraded link) instead of "
+                         "discovering one: rehearsals of the placement A/B on CPU")
     ap.add_argument("--rccl-log", default="auto", choices=["auto", "on", "off"],
                     help="capture RCCL's INIT/GRAPH log (per-rank file under /tmp) and report the transports and "
                          "channel counts it chose; auto = on for k >= 2")
@@ -353,27 +360,33 @@ def tune_ctas(env, device, nbytes, args, tdev, barrier_kw):
 
 
 def measure_worst(env, choice, nbytes, args, tdev, barrier_kw, backend, ctas):
-    """The placement A/B inside the north-star run: rank r builds a second communicator on
-    ``choice.worst_hip[r]`` (the worst-scoring k-subset of the same node), checks it exactly and times
+    """The placement A/B inside the north-star run: the worst-scoring k-subset of the same node."""
+    return measure_subset(env, "worst", choice.worst, choice.worst_hip, choice.worst_score, nbytes, args, tdev, barrier_kw,
+                          backend, ctas)
+
+
+def measure_subset(env, label, subset, hip, score, nbytes, args, tdev, barrier_kw, backend, ctas):
+    """One placement A/B arm: rank r builds a second communicator on ``hip[r]`` (another k-subset of the
+    same node: the worst one, or the kubelet's default choice), checks it exactly and times
     ``min(K, 20)`` all-reduces of the headline size (max over ranks)."""
     import torch
     import torch.distributed as dist
 
     from gpu_topology_on_k8s_amd.parallel.allreduce import AllReduceRunner, bus_factor
 
-    wdev = int((choice.worst_hip or choice.worst)[env.rank])
+    wdev = int((hip or subset)[env.rank])
     ok, r = 1, None
     try:
-        r = AllReduceRunner(env, wdev, nbytes, args.dtype, backend=backend, inplace=args.inplace, ctas=ctas, tag="/worst")
+        r = AllReduceRunner(env, wdev, nbytes, args.dtype, backend=backend, inplace=args.inplace, ctas=ctas, tag=f"/{label}")
     except Exception as e:  # noqa: BLE001 - every rank learns it through the flag below
-        print(f"bench: worst-subset communicator unavailable on rank {env.rank}: {e}", file=sys.stderr)
+        print(f"bench: {label}-subset communicator unavailable on rank {env.rank}: {e}", file=sys.stderr)
         ok = 0
     flag = torch.tensor([ok], dtype=torch.int32, device=tdev)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     if int(flag.item()) == 0:
         if r is not None:
             r.close()
-        return {"subset": choice.worst, "error": "communicator unavailable"}
+        return {"subset": subset, "error": "communicator unavailable"}
     try:
         wrong = torch.tensor([r.check()], dtype=torch.int64, device=tdev)
         dist.all_reduce(wrong)
@@ -390,11 +403,17 @@ def measure_worst(env, choice, nbytes, args, tdev, barrier_kw, backend, ctas):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms = float(t.item()) / steps * 1e3
         alg = r.nbytes / (ms / 1e3) / 1e9
-        return {"subset": choice.worst, "hip_devices": choice.worst_hip, "score": choice.worst_score, "steps": steps,
+        return {"subset": subset, "hip_devices": hip, "score": score, "steps": steps,
                 "ms_per_step": round(ms, 4), "algbw_gbps": round(alg, 3), "busbw_gbps": round(alg * bus_factor(env.world), 3),
                 "exact": int(wrong.item()) == 0}
     finally:
         r.close()
+
+
+def _gain(ours: float, arm, world: int):
+    """Headline rate over an A/B arm's (busBW at k >= 2, algBW at k = 1)."""
+    key = "busbw_gbps" if world > 1 else "algbw_gbps"
+    return round(ours / arm[key], 4) if arm and arm.get(key) else None
 
 
 def _sweep_cost(sizes, algbw_gbps: float) -> float:
@@ -456,6 +475,12 @@ def main(argv=None) -> int:
     if env.rank == 0:
         preset = {"auto": None if cpu else "quick", "off": None}.get(args.probe, args.probe)
         topo = None
+        if args.topology_json:
+            from gpu_topology_on_k8s_amd.topology.model import Topology
+
+            with open(args.topology_json) as f:
+                topo = Topology.from_json(f.read())
+            preset = None
         if preset:
             # the probe seeds the placement's cost matrix (scheduler-chosen subset): part of the
             # headline's definition, so it is bounded by the budget but never skipped
@@ -614,6 +639,19 @@ def main(argv=None) -> int:
         finally:
             if not cpu:
                 torch.cuda.set_device(device)  # the second communicator switched this thread's device
+    default_ab = None
+    want_default = args.ab_default == "on" or (args.ab_default == "auto" and bool(choice.default))
+    if want_default and choice.default and (cpu or (choice.default_hip and runner.comm is not None)) \
+            and ph.allow("ab_default", comm_s + (max(1, args.warmup // 2) + min(args.steps, 20) + 1) * step_s, agree):
+        try:  # supplementary, like the worst-subset arm
+            default_ab = ph.run("ab_default", measure_subset, env, "default", choice.default, choice.default_hip,
+                                choice.default_score, headline_bytes, args, tdev, barrier_kw, args.backend, ctas)
+        except Exception as e:  # noqa: BLE001
+            print(f"bench: default-subset A/B aborted on rank {env.rank}: {e}", file=sys.stderr)
+            default_ab = {"subset": choice.default, "error": str(e)[:300]}
+        finally:
+            if not cpu:
+                torch.cuda.set_device(device)
     runner.close()
     rccl = None
     if rccl_log and env.rank == 0:
@@ -665,6 +703,8 @@ def main(argv=None) -> int:
                 "placement_ms": choice.placement_ms,
                 "worst_subset": choice.worst,
                 "worst_score": choice.worst_score,
+                "default_subset": choice.default,
+                "default_score": choice.default_score,
                 "topology_source": choice.source,
                 "probed": choice.probed,
                 "rccl_ctas": list(ctas) if ctas else "rccl-default",
@@ -682,9 +722,12 @@ def main(argv=None) -> int:
             "graph_latency": graph,
             "rccl": rccl,
             "worst_subset_ab": worst_ab,
-            "placement_gain": (round((busbw if env.world > 1 else algbw)
-                                     / worst_ab[("busbw_gbps" if env.world > 1 else "algbw_gbps")], 4)
-                               if worst_ab and worst_ab.get(("busbw_gbps" if env.world > 1 else "algbw_gbps")) else None),
+            "placement_gain": _gain(busbw if env.world > 1 else algbw, worst_ab, env.world),
+            "default_subset_ab": default_ab,
+            "placement_gain_vs_default": _gain(busbw if env.world > 1 else algbw, default_ab, env.world),
+            # the objective's terms of the chosen, worst and default subsets, what separates them and the
+            # gain the slowest link predicts (placement/explain.py): a healthy xGMI mesh predicts 1.00
+            "placement_terms": choice.extra.get("placement_terms"),
             "value_kind": ("aggregate busbw (k x per-rank busbw_gbps)" if env.world > 1
                            else "algbw (busbw = 0 at k=1)"),
             "busbw_vs_probe_bound": round(busbw / bound, 4) if bound else None,

@@ -7,11 +7,15 @@ HTTP.  For each informer mode an extender process of its own (so its RSS is its 
 it through the REST client:
 
 * ``legacy``   — round 5: one unpaginated consistent LIST of every pod and node, objects kept whole;
-* ``clientgo`` — paginated watch-cache LIST (limit/continue), terminal pods filtered server-side,
-  objects trimmed to what the cache reads.
+* ``clientgo`` — a watch-cache LIST (``resourceVersion=0``), terminal pods filtered server-side, objects
+  trimmed to what the cache reads; the apiserver answers it whole, as apiservers before the paginated
+  watch cache ignore ``limit`` there;
+* ``paged``    — the same with an apiserver that pages it (limit/continue, 500 a page): the LIST never
+  sits in the extender's memory whole.
 
 Recorded per mode: LIST time to synced, LIST requests and JSON bytes the apiserver served, the
-extender's RSS after the sync, one /prioritize over every node.  In ``clientgo`` mode the apiserver
+extender's peak RSS and the RSS it keeps after the sync (freed heap returned with ``malloc_trim``),
+one /prioritize over every node.  In the ``clientgo`` and ``paged`` modes the apiserver
 then cuts the open pod watch and refuses the next watch attempts (503): the extender must see the
 pods created meanwhile with **zero** relists.
 
@@ -28,10 +32,32 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
-def _rss_mb() -> float:
+def _rss_mb(trim: bool = False) -> float:
+    """Resident set size; ``trim`` first hands freed heap back to the kernel (glibc ``malloc_trim``), so
+    the number is what the process keeps, not the high-water mark of a LIST it has already dropped."""
+    import gc
+
     import psutil
 
+    if trim:
+        import ctypes
+
+        gc.collect()
+        try:
+            ctypes.CDLL("libc.so.6").malloc_trim(0)
+        except OSError:
+            pass
     return psutil.Process().memory_info().rss / 2 ** 20
+
+
+def _peak_mb() -> float:
+    """This process's RSS high-water mark (``VmHWM``: reset at exec, unlike ``ru_maxrss``, which would
+    carry the parent's footprint over from the fork)."""
+    with open("/proc/self/status") as f:
+        for line in f:
+            if line.startswith("VmHWM:"):
+                return int(line.split()[1]) / 1024
+    return float("nan")
 
 
 def child(url: str, mode: str, n_nodes: int) -> None:
@@ -43,39 +69,39 @@ def child(url: str, mode: str, n_nodes: int) -> None:
     from gpu_topology_on_k8s_amd.k8s.informer import Informer
     from gpu_topology_on_k8s_amd.k8s.objects import make_pod
 
-    gc.collect()
-    rss0 = _rss_mb()
+    rss0 = _rss_mb(trim=True)
     api = RestKubeAPI(url, timeout=600.0)
     ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
     if mode == "legacy":
         inf = Informer(api, ext.cache.on_list, ext.cache.on_event, begin_list=ext.cache.begin_list, page_size=0,
                        watch_cache=False, watch_timeout=60.0)
         ext.cache.attach_informer(inf)
-    else:
+    else:  # clientgo: a watch-cache LIST the apiserver answers whole; paged: one it pages (limit/continue)
         inf = ext.cache.make_informer(page_size=500, watch_timeout=60.0, backoff=0.05, max_backoff=0.5)
     t0 = time.perf_counter()
     inf.start()
     assert inf.wait_synced(1200)
     sync_s = time.perf_counter() - t0
-    gc.collect()
-    rss = _rss_mb()
+    peak = _peak_mb()
+    rss = _rss_mb(trim=True)
     names = [f"n{i}" for i in range(n_nodes)]
     pod = make_pod("probe-pod", gpus=4)
     t1 = time.perf_counter()
     prio = ext.prioritize(pod, names)
     prio_ms = (time.perf_counter() - t1) * 1e3
-    out = {"mode": mode, "sync_s": round(sync_s, 2), "rss_mb_before": round(rss0, 1), "rss_mb_synced": round(rss, 1),
-           "rss_mb_cache": round(rss - rss0, 1), "pod_list": inf.last_list.get("Pod"), "node_list": inf.last_list.get("Node"),
+    out = {"mode": mode, "sync_s": round(sync_s, 2), "rss_mb_before": round(rss0, 1), "rss_mb_peak": round(peak, 1),
+           "rss_mb_synced": round(rss, 1), "rss_mb_cache": round(rss - rss0, 1),
+           "pod_list": inf.last_list.get("Pod"), "node_list": inf.last_list.get("Node"),
            "prioritize_all_nodes_ms": round(prio_ms, 1), "nodes_scored": len(prio),
            "nodes_with_free_4": sum(1 for _, score in prio if score > 0)}
     print("SYNCED " + json.dumps(out), flush=True)
-    if mode == "clientgo":
+    if mode != "legacy":
         line = sys.stdin.readline().strip()  # "GO <count>": the parent cut the watch and created pods
         want = int(line.split()[1])
         t2 = time.perf_counter()
         deadline = time.monotonic() + 120
         while time.monotonic() < deadline:
-            got = sum(1 for st in ext.cache.nodes() for k in st.allocs if k.startswith("default/late-"))
+            got = sum(1 for st in ext.cache.nodes() for k in st.allocs if k.startswith(f"default/late-{mode}-"))
             if got >= want:
                 break
             time.sleep(0.05)
@@ -145,7 +171,7 @@ def main() -> int:
     ap.add_argument("--nodes", type=int, default=5000)
     ap.add_argument("--pods", type=int, default=100_000)
     ap.add_argument("--terminal", type=float, default=0.25, help="fraction of pods that are Succeeded")
-    ap.add_argument("--modes", default="legacy,clientgo")
+    ap.add_argument("--modes", default="legacy,clientgo,paged")
     ap.add_argument("--late-pods", type=int, default=200, help="pods created while the watch is broken")
     ap.add_argument("--out", default="")
     ap.add_argument("--child", default="")
@@ -168,6 +194,7 @@ def main() -> int:
     srv, url = serve_http(api)
     try:
         for mode in a.modes.split(","):
+            api.watch_cache_pages = mode == "paged"  # an apiserver that pages watch-cache LISTs (k8s >= 1.31)
             b0, r0 = dict(api.bytes_served), dict(api.list_requests)
             p = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--child", mode, "--url", url, "--nodes", str(a.nodes)],
                                  stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, cwd=REPO)
@@ -177,13 +204,14 @@ def main() -> int:
                     res.update(_json.loads(line[7:]))
                     res["list_bytes"] = {k: api.bytes_served[k] - b0.get(k, 0) for k in ("Node", "Pod")}
                     res["list_requests"] = {k: api.list_requests[k] - r0.get(k, 0) for k in ("Node", "Pod")}
-                    print(f"[informer_scale] {mode}: synced in {res['sync_s']}s, cache {res['rss_mb_cache']} MB, "
-                          f"{res['list_bytes']['Pod'] / 2 ** 20:.0f} MB of pods listed", flush=True)
-                    if mode == "clientgo":
+                    print(f"[informer_scale] {mode}: synced in {res['sync_s']}s, peak RSS {res['rss_mb_peak']} MB, kept "
+                          f"{res['rss_mb_cache']} MB, {res['list_bytes']['Pod'] / 2 ** 20:.0f} MB of pods listed in "
+                          f"{res['list_requests']['Pod']} requests", flush=True)
+                    if mode != "legacy":
                         api.cut_watch("Pod", after=0)
                         api.inject("watch_Pod", 503, times=3)
                         for i in range(a.late_pods):
-                            api.create_pod(make_pod(f"late-{i}", gpus=1, node=f"n{i % a.nodes}",
+                            api.create_pod(make_pod(f"late-{mode}-{i}", gpus=1, node=f"n{i % a.nodes}",
                                                     annotations=PodAssignment([7], True, 1_700_000_000).to_annotations()))
                         p.stdin.write(f"GO {a.late_pods}\n")
                         p.stdin.flush()

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """BASELINE config 5 / Gaia Exp. 6 (paper p.7 Figs. 11-12): DP training throughput on the
-scheduler-chosen subset vs the worst subset of the same size — Llama-3 (tokens/s) or the paper's own
-workload, the MNIST CNN (images/s and the time of one 60k-image epoch, ``--model mnist-cnn``).
+scheduler-chosen subset vs the worst subset of the same size and vs the devices the kubelet hands out
+with no extender (the paper's actual comparator, default Kubernetes) — Llama-3 (tokens/s) or the
+paper's own workload, the MNIST CNN (images/s and the time of one 60k-image epoch, ``--model mnist-cnn``).
+Every run reports the placement objective's terms of the three subsets and the gain their slowest
+links predict (placement/explain.py).
 
     python bench/train_llama.py --gpus 2 --model llama3-8b --batch 2 --seq 4096 --steps 10 [--out f.json]
     python bench/train_llama.py --gpus 2 --model mnist-cnn --batch 64 --steps 300
@@ -50,6 +53,8 @@ def run(placement: str, a) -> dict:
     # dma-buf IPC handles for RCCL's P2P/IPC transport between the ranks (see bench.py main())
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""),
                **extra_env)
+    if a.topology_json:
+        env["GTK_TOPOLOGY_JSON"] = os.path.abspath(a.topology_json)
     p = subprocess.run(cmd, capture_output=True, text=True, cwd=REPO, env=env, timeout=a.timeout)
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     if p.returncode != 0 or not lines:
@@ -76,13 +81,18 @@ def main() -> int:
     ap.add_argument("--zero1", action="store_true", help="ZeRO-1: sharded AdamW, reduce-scatter grads / all-gather weights")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"], help="whole-step hipGraph (models/train.py)")
     ap.add_argument("--timeout", type=int, default=1500)
-    ap.add_argument("--placements", default="best,worst", help="comma list of best, worst, p2p-off (emulated worst link class)")
+    ap.add_argument("--placements", default="best,worst,default",
+                    help="comma list of best, worst, default (the devices the kubelet hands out with no extender: the "
+                         "paper's default-Kubernetes comparator), p2p-off (emulated worst link class)")
+    ap.add_argument("--topology-json", default="", help="place on this node model (CPU rehearsals of the A/B)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     res = {}
     for pl in a.placements.split(","):
         if pl == "worst" and "best" in res and not res["best"].get("worst_devices"):
             pl = "p2p-off"  # k == node size: best == worst device set; emulate the worst link class instead
+        if pl == "default" and "best" in res and not res["best"].get("default_devices"):
+            continue  # the kubelet would hand out the chosen devices: nothing to compare
         if pl in res:
             continue
         r = run(pl, a)
@@ -109,6 +119,14 @@ def main() -> int:
     }
     if summary["worst_throughput"]:
         summary["speedup_vs_worst"] = summary["best_throughput"] / summary["worst_throughput"]
+    dflt = res.get("default", {})
+    summary["default_devices"] = res["best"].get("default_devices")
+    summary["default_same_as_best"] = not res["best"].get("default_devices")
+    summary["default_throughput"] = dflt.get("throughput")
+    if dflt.get("throughput"):
+        summary["speedup_vs_default"] = summary["best_throughput"] / dflt["throughput"]
+    # what separates the subsets in the placement objective, and the gain their slowest links predict
+    summary["placement_terms"] = res["best"].get("placement_terms")
     print(json.dumps(summary), flush=True)
     if a.out:
         with open(a.out, "w") as f:

@@ -88,7 +88,9 @@ class FakeAPIServer(KubeAPI):
         self.watch_cache_pages = False
         self.bytes_served: Dict[str, int] = defaultdict(int)  # kind -> JSON bytes of LIST responses
         self.list_requests: Dict[str, int] = defaultdict(int)  # kind -> LIST requests (pages)
-        self._watch_cuts: Dict[str, List[int]] = defaultdict(list)  # kind -> cut the next watches after n events
+        self._watch_cuts: Dict[str, List[int]] = defaultdict(list)  # kind -> cut the next watch after n events
+        self._open_watches: Dict[str, Dict[int, List[Optional[int]]]] = defaultdict(dict)  # kind -> id -> [cut]
+        self._watch_ids = 0
 
     # ------------------------------------------------------------------ infrastructure
     def _next_rv(self) -> str:
@@ -164,10 +166,14 @@ class FakeAPIServer(KubeAPI):
             self._pages.clear()
 
     def cut_watch(self, kind: str, after: int = 0) -> None:
-        """A watch of ``kind`` (the one open now, else the next) breaks — a connection reset — after
-        delivering ``after`` more events."""
+        """Every watch of ``kind`` open now (or, with none open, the next one) breaks — a connection
+        reset — after delivering ``after`` more events."""
         with self._lock:
-            self._watch_cuts[kind].append(after)
+            if self._open_watches.get(kind):
+                for slot in self._open_watches[kind].values():
+                    slot[0] = after
+            else:
+                self._watch_cuts[kind].append(after)
 
     def watch_stream(self, kind: str, resource_version: str, timeout: float = 60.0,
                      stop: Optional[threading.Event] = None, field_selector: Optional[str] = None,
@@ -178,17 +184,26 @@ class FakeAPIServer(KubeAPI):
         (the object left the selection) and an ADDED one is not delivered."""
         with self._lock:
             self._enter(f"watch_{kind}")
+            if self._history and int(resource_version or 0) < self._history[0][0] - 1 \
+                    and len(self._history) == self._history.maxlen:
+                raise Gone(f"resourceVersion {resource_version} is too old")
+            self._watch_ids += 1
+            wid, slot = self._watch_ids, [self._watch_cuts[kind].pop(0) if self._watch_cuts.get(kind) else None]
+            self._open_watches[kind][wid] = slot
+        try:
+            yield from self._watch_events(kind, int(resource_version or 0), time.monotonic() + timeout, stop, field_selector,
+                                          namespace, slot)
+        finally:
+            with self._lock:
+                self._open_watches[kind].pop(wid, None)
+
+    def _watch_events(self, kind, since, deadline, stop, field_selector, namespace, slot):
         cut: Optional[int] = None
-        since = int(resource_version or 0)
-        deadline = time.monotonic() + timeout
         sent = 0
-        with self._lock:
-            if self._history and since < self._history[0][0] - 1 and len(self._history) == self._history.maxlen:
-                raise Gone(f"resourceVersion {since} is too old")
         while stop is None or not stop.is_set():
             with self._lock:
-                if cut is None and self._watch_cuts.get(kind):  # a cut requested while this watch is open
-                    cut = sent + self._watch_cuts[kind].pop(0)
+                if cut is None and slot[0] is not None:  # a cut requested while this watch is open
+                    cut = sent + slot[0]
                 batch = [(t, o) for rv, t, k, o in self._history if rv > since and k == kind
                          and (namespace is None or meta(o).get("namespace") == namespace)]
                 if self._history:

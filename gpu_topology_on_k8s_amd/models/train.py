@@ -115,13 +115,26 @@ def _choose_device(env, placement: str, discovery: str, visible: Optional[int] =
     if env["rank"] == 0:
         from ..parallel.allreduce import choose_subset
 
-        ch = choose_subset(env["world"], backend=discovery, visible=visible)
-        use_worst = placement == "worst" and ch.worst
-        devices = ch.worst if use_worst else ch.devices  # node-local topology indices (GROUP numbering)
-        info = {"devices": devices, "hip_devices": ch.worst_hip if use_worst else ch.hip_devices, "best": ch.devices,
-                "best_score": ch.score, "worst": ch.worst, "worst_score": ch.worst_score, "source": ch.source,
+        topo = None
+        if os.environ.get("GTK_TOPOLOGY_JSON"):  # a node model to place on (CPU rehearsals of the A/B)
+            from ..topology.model import Topology
+
+            with open(os.environ["GTK_TOPOLOGY_JSON"]) as f:
+                topo = Topology.from_json(f.read())
+        ch = choose_subset(env["world"], backend=discovery, visible=visible, topology=topo)
+        # best = the placement core; worst = its highest-objective alternative; default = what the
+        # kubelet hands out with no extender (the paper's default-Kubernetes comparator): the best set
+        # again when the kubelet would pick the same devices
+        arm = {"worst": (ch.worst, ch.worst_hip, "worst_cpusets"),
+               "default": (ch.default, ch.default_hip, "default_cpusets")}.get(placement)
+        use = arm if arm and arm[0] else None
+        devices = use[0] if use else ch.devices  # node-local topology indices (GROUP numbering)
+        info = {"devices": devices, "hip_devices": use[1] if use else ch.hip_devices, "best": ch.devices,
+                "best_score": ch.score, "worst": ch.worst, "worst_score": ch.worst_score, "default": ch.default,
+                "default_score": ch.default_score, "source": ch.source,
+                "placement_terms": ch.extra.get("placement_terms"),
                 # Gaia B6: each rank's share of the node's cores, the slice of its own device
-                "cpusets": ch.extra.get("worst_cpusets") if use_worst else ch.extra.get("cpusets")}
+                "cpusets": ch.extra.get(use[2]) if use else ch.extra.get("cpusets")}
         store.set("gtk/train_placement", json.dumps(info))
     return json.loads(store.get("gtk/train_placement").decode())
 
@@ -491,8 +504,11 @@ def train(model_name: str = "tiny", batch: int = 1, seq: int = 128, steps: int =
         "hbm_cap_fraction": pl.get("hbm_cap_fraction"),
         "best_devices": pl.get("best"),
         "worst_devices": pl.get("worst"),
+        "default_devices": pl.get("default"),
         "best_score": pl.get("best_score"),
         "worst_score": pl.get("worst_score"),
+        "default_score": pl.get("default_score"),
+        "placement_terms": pl.get("placement_terms"),
         "global_batch": local_batch * env["world"],
         "seq_len": None if mnist else seq,
         "steps": steps,
@@ -557,9 +573,10 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
-    ap.add_argument("--placement", default="auto", choices=["auto", "best", "worst", "pod"],
+    ap.add_argument("--placement", default="auto", choices=["auto", "best", "worst", "default", "pod"],
                     help="pod = the devices Allocate gave this container (GTK_GPU_GROUP/GTK_GPU_BDFS); best/worst = "
-                         "run the placement core on the node; auto = pod when GTK_GPU_GROUP is set, else best")
+                         "run the placement core on the node; default = the devices the kubelet hands out with no "
+                         "extender (lowest free indices); auto = pod when GTK_GPU_GROUP is set, else best")
     ap.add_argument("--discovery", default="auto")
     ap.add_argument("--bucket-mb", type=float, default=256.0)
     ap.add_argument("--checkpoint", action="store_true")

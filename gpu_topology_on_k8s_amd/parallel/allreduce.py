@@ -98,6 +98,11 @@ class SubsetChoice:
     hip_devices: List[int] = field(default_factory=list)  # HIP ordinal of devices[r] in this process
     worst_hip: Optional[List[int]] = None
     extra: Dict[str, object] = field(default_factory=dict)
+    # the kubelet's own choice with no extender (lowest free indices: placement/explain.py), None when
+    # it is the chosen set or no distinct k-subset exists
+    default: Optional[List[int]] = None
+    default_score: Optional[float] = None
+    default_hip: Optional[List[int]] = None
 
     def to_json(self) -> str:
         return json.dumps(self.__dict__)
@@ -277,8 +282,13 @@ def choose_subset(k: int, probe: Optional[str] = None, backend: str = "auto", vi
                 objective, _ = evaluate(Problem.from_topology(topo, []), k8s["devices"], PlacementPolicy())
                 score = score_from_objective(objective)
             devices = list(k8s["devices"])
+    from ..placement.explain import default_subset, explain_subsets
     from ..topology.cpus import recommended_cpuset
 
+    kubelet = default_subset(topo, k)
+    terms = explain_subsets(topo, {"chosen": devices, "worst": list(w.ids) if w else None, "default": kubelet})
+    # the kubelet would have chosen the same devices: explained (same_devices), nothing to time
+    dflt = kubelet if kubelet is not None and sorted(kubelet) != sorted(devices) else None
     # Gaia B6: each rank's share of the node's cores = the slice of its own device (bind_workload)
     cpusets = [recommended_cpuset(topo, [d]) for d in devices]
     return SubsetChoice(
@@ -292,7 +302,12 @@ def choose_subset(k: int, probe: Optional[str] = None, backend: str = "auto", vi
         probed=probed,
         hip_devices=[dmap.hip(i) for i in devices],
         worst_hip=[dmap.hip(i) for i in w.ids] if w else None,
+        default=dflt,
+        default_score=terms["default"]["score"] if dflt else None,
+        default_hip=[dmap.hip(i) for i in dflt] if dflt else None,
         extra={"discovery_ms": round((t1 - t0) * 1e3, 2), "node_devices": topo.n, "visible_devices": nvis,
+               "placement_terms": terms,
+               "default_cpusets": [recommended_cpuset(topo, [d]) for d in dflt] if dflt else None,
                "device_map": dmap.to_dict(), "worst_exact": bool(w.exact) if w else None, "cpusets": cpusets,
                "worst_cpusets": [recommended_cpuset(topo, [d]) for d in w.ids] if w else None,
                **({"probe": probe_summary(topo, devices)} if probed else {}),

@@ -1,0 +1,96 @@
+"""Why one k-subset beats another: the objective's terms, and the gain they predict.
+
+The placement A/B of the north-star run times the all-reduce on the scheduler's choice and on an
+alternative of the same node (``bench.py``, ``bench/train_llama.py``; paper p.7 Figs. 11-12 compare
+Gaia with the default kube-scheduler placement).  On a healthy MI355X node every xGMI link lands in one
+band (ops/checks.py), so the subsets can differ only by NUMA span and packing, terms that move the
+host side (proxies, staging buffers) and later pods, not the links a ring all-reduce runs on.  A
+reader of the JSON line must see that before comparing two busBW numbers.  So every compared subset is
+reported with:
+
+* the objective ``J`` (placement/core.py ``evaluate``) and the weighted contribution of each term:
+  ``comm`` (mean link cost), ``bottleneck`` (worst link over mean), ``span`` (NUMA / group spread
+  beyond the minimum), ``frag`` (pristine groups broken), ``fit`` (packing), ``access`` (host-core
+  affinity), ``nic_deficit``;
+* its links: the slowest measured link GB/s (or the worst link cost when nothing was measured), the
+  link classes and the NUMA nodes it uses;
+* against the chosen subset, the terms that separate the two (largest first) and the **predicted
+  gain**: the chosen subset's slowest link over the other's.  A ring all-reduce moves every byte over
+  every link of its ring, so its busBW follows the slowest one.  The prediction is 1.00 when only
+  host-side terms separate the subsets.
+
+Subsets compared: ``chosen`` (the placement core), ``worst`` (highest objective), and ``default``
+(what the kubelet's device manager hands out with no extender and no preferred allocation: it takes
+the free devices in set order, modelled here as the lowest free indices).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from ..topology.model import LinkType, Topology
+from .core import PlacementPolicy, Problem, evaluate, score_from_objective
+
+__all__ = ["explain_subsets", "default_subset", "TERMS"]
+
+TERMS = ("comm", "bottleneck", "span", "frag", "fit", "access", "nic_deficit")
+
+
+def default_subset(topo: Topology, k: int, used: Sequence[int] = ()) -> Optional[List[int]]:
+    """The kubelet's choice without the extender: ``k`` free healthy devices in index order."""
+    free = [g.index for g in topo.gpus if g.healthy and g.index not in set(used)]
+    return sorted(free)[:k] if len(free) >= k else None
+
+
+def _weighted(terms: Dict[str, float], policy: PlacementPolicy) -> Dict[str, float]:
+    return {"comm": terms["comm"], "bottleneck": policy.w_bottleneck * (terms["bottleneck"] - terms["comm"]),
+            "span": policy.w_span * terms["span"], "frag": policy.w_frag * terms["frag"], "fit": policy.w_fit * terms["fit"],
+            "access": policy.w_access * terms["access"], "nic_deficit": policy.w_nic * terms["nic_deficit"]}
+
+
+def _links(topo: Topology, ids: Sequence[int]) -> Dict[str, object]:
+    ids = list(ids)
+    pairs = [(a, b) for i, a in enumerate(ids) for b in ids[i + 1:]]
+    bw = topo.bw_gbps
+    meas = []
+    if bw is not None:
+        for a, b in pairs:
+            v = [x for x in (bw[a, b], bw[b, a]) if np.isfinite(x) and x > 0]
+            if v:
+                meas.append(min(v))
+    classes = sorted({LinkType(int(topo.link_type[a, b])).name for a, b in pairs})
+    return {"min_link_gbps": round(min(meas), 2) if meas and len(meas) == len(pairs) else None,
+            "max_link_cost": round(max((float(topo.cost[a, b]) for a, b in pairs), default=0.0), 6),
+            "link_classes": classes, "numa_nodes": sorted({int(topo.gpus[i].numa) for i in ids})}
+
+
+def explain_subsets(topo: Topology, subsets: Dict[str, Optional[Sequence[int]]], policy: PlacementPolicy = PlacementPolicy(),
+                    used: Sequence[int] = (), reference: str = "chosen") -> Dict[str, object]:
+    """``{name: {...}}`` for every non-empty subset, plus ``vs_<name>`` comparisons against
+    ``reference`` (the chosen subset): separating terms and the link-bound predicted gain."""
+    p = Problem.from_topology(topo, used)
+    out: Dict[str, object] = {}
+    for name, ids in subsets.items():
+        if not ids:
+            continue
+        j, terms = evaluate(p, list(ids), policy)
+        out[name] = {"ids": [int(i) for i in ids], "objective": round(j, 6), "score": round(score_from_objective(j), 4),
+                     "weighted": {t: round(v, 6) for t, v in _weighted(terms, policy).items()}, **_links(topo, ids)}
+    ref = out.get(reference)
+    if ref is None:
+        return out
+    for name, e in list(out.items()):
+        if name == reference or not isinstance(e, dict):
+            continue
+        delta = {t: round(e["weighted"][t] - ref["weighted"][t], 6) for t in TERMS}
+        sep = [t for t in sorted(TERMS, key=lambda t: -abs(delta[t])) if abs(delta[t]) > 1e-9]
+        if ref["min_link_gbps"] and e["min_link_gbps"]:
+            gain, basis = ref["min_link_gbps"] / e["min_link_gbps"], "slowest measured link"
+        else:
+            gain, basis = (e["max_link_cost"] / ref["max_link_cost"] if ref["max_link_cost"] else 1.0), "worst link cost"
+        out[f"vs_{name}"] = {"same_devices": sorted(e["ids"]) == sorted(ref["ids"]), "objective_delta": round(e["objective"] - ref["objective"], 6),
+                             "separating_terms": {t: delta[t] for t in sep},
+                             "predicted_gain": round(gain, 4), "predicted_basis": basis,
+                             "link_terms_separate": any(t in ("comm", "bottleneck") for t in sep)}
+    return out

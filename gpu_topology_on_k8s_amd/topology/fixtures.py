@@ -98,6 +98,19 @@ def f7_mi355x(link_gbps: Optional[float] = None, noise: float = 0.0, seed: int =
     return Topology.full_mesh(n=n, numa_split=2, link_gbps=link_gbps, noise=noise, seed=seed, node_name="f7-mi355x")
 
 
+def f7_degraded(pairs=((0, 1, 0.6),), link_gbps: float = 150.0) -> Topology:
+    """F7 with measured links, some degraded: ``(i, j, fraction)`` runs at that fraction of
+    ``link_gbps`` (an xGMI link retrained at a lower width, or a flaky one) — the node on which a
+    placement's choice is link-bound, unlike a healthy full mesh."""
+    t = f7_mi355x()
+    bw = np.where(np.eye(t.n, dtype=bool), np.nan, float(link_gbps))
+    for i, j, f in pairs:
+        bw[i, j] = bw[j, i] = float(link_gbps) * float(f)
+    t.set_measured_bw(bw, {"method": "fixture", "degraded": [list(p) for p in pairs]})
+    t.node_name = "f7-degraded"
+    return t
+
+
 def f8_mi355x_cpx(link_gbps: Optional[float] = None, noise: float = 0.0, seed: int = 0) -> Topology:
     return Topology.full_mesh(n=8, numa_split=2, link_gbps=link_gbps, noise=noise, seed=seed, node_name="f8-mi355x-cpx",
                               partitions_per_gpu=8)

@@ -1,0 +1,104 @@
+"""The placement A/B made interpretable (paper p.7 Figs. 11-12, default
+Kubernetes vs Gaia; ``design.md:11``): every compared subset — the scheduler's choice, the worst one and
+the devices the kubelet hands out with no extender — comes with the objective's terms, what separates
+it from the choice, and the gain its slowest link predicts."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from gpu_topology_on_k8s_amd.placement import select, worst
+from gpu_topology_on_k8s_amd.placement.explain import TERMS, default_subset, explain_subsets
+from gpu_topology_on_k8s_amd.topology import fixtures as fx
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _three(topo, k):
+    return explain_subsets(topo, {"chosen": list(select(topo, k).ids), "worst": list(worst(topo, k).ids),
+                                  "default": default_subset(topo, k)})
+
+
+@pytest.mark.parametrize("k", [2, 4])
+def test_healthy_mesh_predicts_no_link_gain(k):
+    """Every xGMI link alike: the worst subset differs only by host-side terms (NUMA span, packing), so
+    the predicted all-reduce gain is 1.00 — what the first k >= 2 run will print, explained."""
+    ex = _three(fx.f7_mi355x(link_gbps=150.0), k)
+    assert ex["chosen"]["objective"] <= ex["default"]["objective"] <= ex["worst"]["objective"]
+    vs = ex["vs_worst"]
+    assert not vs["link_terms_separate"] and vs["predicted_gain"] == pytest.approx(1.0)
+    assert set(vs["separating_terms"]) <= {"span", "frag", "fit", "access"} and vs["separating_terms"]
+    assert ex["vs_default"]["same_devices"]  # on an empty node the kubelet's lowest ids are the choice too
+    assert set(ex["chosen"]["weighted"]) == set(TERMS)
+
+
+@pytest.mark.parametrize("k", [2, 4])
+def test_degraded_link_separates_the_default_placement(k):
+    """Link 0-1 at 60 %: the kubelet's lowest ids use it, the choice does not; the comparison names the
+    link terms and predicts the slowest-link ratio, 1 / 0.6."""
+    t = fx.f7_degraded(((0, 1, 0.6),))
+    ex = _three(t, k)
+    chosen, dflt = ex["chosen"]["ids"], ex["default"]["ids"]
+    assert not {0, 1} <= set(chosen) and {0, 1} <= set(dflt)
+    vs = ex["vs_default"]
+    assert vs["link_terms_separate"] and "comm" in vs["separating_terms"]
+    assert vs["predicted_gain"] == pytest.approx(1 / 0.6, rel=1e-3) and vs["predicted_basis"] == "slowest measured link"
+    assert ex["chosen"]["objective"] < ex["default"]["objective"]
+    assert vs["predicted_gain"] >= ex["vs_worst"]["predicted_gain"] >= 1.0 - 1e-9
+
+
+def _bench(*args, timeout=300):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], capture_output=True, text=True, timeout=timeout,
+                       cwd=REPO, env=env)
+    assert p.returncode == 0, p.stderr[-4000:]
+    return json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+
+
+@pytest.mark.parametrize("n,fixture", [(2, "f7"), (4, "f7"), (2, "degraded"), (4, "degraded")])
+def test_bench_dry_run_reports_three_subsets_with_terms(tmp_path, n, fixture):
+    """gloo dry runs of the north-star line at N=2 and N=4 on F7 and on the one-degraded-link node: the
+    line carries chosen / worst / default with their terms and predicted gains; where the kubelet's
+    choice differs, it is timed as a third arm."""
+    t = fx.f7_mi355x(link_gbps=150.0) if fixture == "f7" else fx.f7_degraded(((0, 1, 0.6),))
+    path = tmp_path / "topo.json"
+    path.write_text(t.to_json())
+    out = _bench("--gpus", str(n), "--backend", "cpu", "--steps", "2", "--warmup", "1", "--size-mb", "1", "--sweep", "off",
+                 "--cpu-visible", "8", "--topology-json", str(path))
+    pt = out["placement_terms"]
+    assert {"chosen", "worst", "default", "vs_worst", "vs_default"} <= set(pt)
+    assert pt["chosen"]["ids"] == out["config"]["subset"]
+    for name in ("chosen", "worst", "default"):
+        assert set(pt[name]["weighted"]) == set(TERMS) and pt[name]["link_classes"] == ["XGMI"]
+    assert out["worst_subset_ab"] and out["worst_subset_ab"]["exact"]
+    if fixture == "f7":
+        assert pt["vs_default"]["same_devices"] and out["config"]["default_subset"] is None and out["default_subset_ab"] is None
+        assert pt["vs_worst"]["predicted_gain"] == pytest.approx(1.0)
+    else:
+        assert out["config"]["default_subset"] == pt["default"]["ids"]
+        ab = out["default_subset_ab"]
+        assert ab and ab["exact"] and ab["subset"] == out["config"]["default_subset"] and out["placement_gain_vs_default"] > 0
+        assert pt["vs_default"]["predicted_gain"] == pytest.approx(1 / 0.6, rel=1e-3)
+
+
+def test_train_harness_runs_the_default_arm(tmp_path):
+    """bench/train_llama.py on a degraded fake node (CPU, 2 ranks): best, worst and the kubelet's default
+    are three different device sets, each trained, and the summary carries the terms."""
+    t = fx.f7_degraded(((0, 1, 0.6),))
+    path = tmp_path / "topo.json"
+    path.write_text(t.to_json())
+    out = tmp_path / "r.json"
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench", "train_llama.py"), "--gpus", "2", "--device", "cpu",
+                        "--discovery", "fake", "--model", "tiny", "--batch", "1", "--seq", "64", "--steps", "2", "--warmup", "1",
+                        "--attn", "sdpa", "--gemm-tuning", "off", "--topology-json", str(path), "--out", str(out)],
+                       capture_output=True, text=True, timeout=900, cwd=REPO, env=dict(env, GTK_FAKE_GPUS="8"))
+    assert p.returncode == 0, p.stderr[-4000:]
+    r = json.loads(out.read_text())
+    s = r["summary"]
+    assert set(r["runs"]) == {"best", "worst", "default"}
+    assert s["default_devices"] == [0, 1] and not s["default_same_as_best"] and s["default_throughput"] > 0
+    assert len({tuple(r["runs"][k]["devices"]) for k in r["runs"]}) == 3
+    assert s["placement_terms"]["vs_default"]["link_terms_separate"]
