@@ -30,8 +30,8 @@
 // The config is the read-only file the plugin mounts at /etc/gtk-vgpu.conf.  When that file exists it
 // is the only one read: $GTK_VGPU_CONFIG (which the pod spec could override) is honoured only where
 // no config is mounted (tests, hand-run jobs).  Format:
-//     hbm_limit_bdf <pci address> <bytes>     e.g. hbm_limit_bdf 0000:05:00.0 103079215104
-//     cu_mask_bdf <pci address> <cu list>     e.g. cu_mask_bdf 0000:05:00.0 0-127
+//     hbm_limit_bdf <pci address> <bytes> [<fallback ordinal>]   e.g. hbm_limit_bdf 0000:05:00.0 103079215104 0
+//     cu_mask_bdf <pci address> <cu list> [<fallback ordinal>]   e.g. cu_mask_bdf 0000:05:00.0 0-127 0
 //     hbm_limit <ordinal> <bytes>             (hand-run jobs) ROCr enumeration order
 //     cu_mask <HSA_CU_MASK value>             (hand-run jobs) ROCr ordinals
 //     acct <path>                  (optional) pod-wide accounting file, shared read-write
@@ -113,8 +113,19 @@ struct State {
   std::vector<std::vector<uint32_t>> mask_bits;                            // per ordinal; empty = all CUs
   std::unordered_map<const hsa_queue_t*, int> queues;                      // queue -> GPU ordinal
   std::unordered_map<void*, std::pair<int, size_t>> managed;               // hipMallocManaged charges
-  std::vector<std::pair<uint32_t, long long>> bdf_limit;                   // PCI address -> bytes
-  std::vector<std::pair<uint32_t, std::vector<uint32_t>>> bdf_mask;        // PCI address -> CU bits
+  struct BdfLimit {
+    uint32_t addr;
+    long long bytes;
+    int fallback;  // ROCr ordinal to apply it to when no agent has the address (-1: none given)
+  };
+  struct BdfMask {
+    uint32_t addr;
+    std::vector<uint32_t> bits;
+    int fallback;
+  };
+  std::vector<BdfLimit> bdf_limit;                                         // PCI address -> bytes
+  std::vector<BdfMask> bdf_mask;                                           // PCI address -> CU bits
+  std::atomic<int> unmatched{-1};  // address entries no agent had (-1: not resolved yet)
   State() {
     for (int i = 0; i < kMaxDev; ++i) limit[i] = -1, used[i] = 0;
   }
@@ -235,18 +246,45 @@ struct Agents {
   std::unordered_map<uint64_t, int> pool_ordinal;   // GPU global pool handle -> ordinal
 };
 
+// An address entry no agent has (the runtime reported no BDFID / DOMAIN, or a format mismatch between
+// what amdsmi printed and what ROCr reports) must not leave the share silently unenforced:
+// it is reported on stderr, counted (gtk_vgpu_unmatched, checked by `gtk doctor --gpu`), and applied to
+// the fallback ordinal the plugin wrote next to the address (the device's position among the pod's
+// GPUs: right unless the pod renumbers its devices), when there is one.
+int unmatched_ordinal(const Agents& a, const char* what, uint32_t addr, int fallback) {
+  const bool ok = fallback >= 0 && fallback < (int)a.gpus.size() && fallback < kMaxDev;
+  std::fprintf(stderr,
+               "gtk-vgpu: %s %04x:%02x:%02x.%x matches none of the %zu GPUs the runtime enumerated%s; %s\n", what,
+               addr >> 16, (addr >> 8) & 0xffu, (addr >> 3) & 0x1fu, addr & 7u, a.gpus.size(),
+               (!a.bdf.empty() && a.bdf[0] == 0xffffffffu) ? " (the runtime reports no PCI addresses)" : "",
+               ok ? "applying it to the fallback ROCr ordinal" : "NO fallback ordinal: this limit is NOT enforced");
+  if (ok) std::fprintf(stderr, "gtk-vgpu:   fallback ordinal %d\n", fallback);
+  return ok ? fallback : -1;
+}
+
 void resolve_bdf_config(const Agents& a) {
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
-  for (const auto& l : s.bdf_limit)
+  auto where = [&](uint32_t addr) -> int {
     for (size_t o = 0; o < a.bdf.size() && o < (size_t)kMaxDev; ++o)
-      if (a.bdf[o] == l.first) s.limit[o] = l.second;
-  for (const auto& m : s.bdf_mask)
-    for (size_t o = 0; o < a.bdf.size() && o < (size_t)kMaxDev; ++o)
-      if (a.bdf[o] == m.first) {
-        if (s.mask_bits.size() <= o) s.mask_bits.resize(o + 1);
-        s.mask_bits[o] = m.second;
-      }
+      if (a.bdf[o] == addr) return (int)o;
+    return -1;
+  };
+  int unmatched = 0;
+  for (const auto& l : s.bdf_limit) {
+    int o = where(l.addr);
+    if (o < 0) ++unmatched, o = unmatched_ordinal(a, "hbm_limit_bdf", l.addr, l.fallback);
+    if (o >= 0) s.limit[o] = l.bytes;
+  }
+  for (const auto& m : s.bdf_mask) {
+    int o = where(m.addr);
+    if (o < 0) ++unmatched, o = unmatched_ordinal(a, "cu_mask_bdf", m.addr, m.fallback);
+    if (o >= 0) {
+      if ((int)s.mask_bits.size() <= o) s.mask_bits.resize(o + 1);
+      s.mask_bits[o] = m.bits;
+    }
+  }
+  s.unmatched = unmatched;
 }
 
 // Built once the runtime can enumerate (after hsa_init): a call that comes earlier (an exported
@@ -510,10 +548,11 @@ __attribute__((constructor)) void load_config() {
     int dev = -1;
     long long bytes = -1;
     uint32_t addr = 0;
-    if (std::sscanf(line, "hbm_limit_bdf %63s %lld", key_s, &bytes) == 2) {
-      if (parse_bdf(key_s, &addr) && bytes >= 0) s.bdf_limit.emplace_back(addr, bytes);
-    } else if (std::sscanf(line, "cu_mask_bdf %63s %3999s", key_s, val) == 2) {
-      if (parse_bdf(key_s, &addr)) s.bdf_mask.emplace_back(addr, parse_cus(val));
+    int fb = -1, nf = 0;
+    if ((nf = std::sscanf(line, "hbm_limit_bdf %63s %lld %d", key_s, &bytes, &fb)) >= 2) {
+      if (parse_bdf(key_s, &addr) && bytes >= 0) s.bdf_limit.push_back({addr, bytes, nf == 3 ? fb : -1});
+    } else if ((nf = std::sscanf(line, "cu_mask_bdf %63s %3999s %d", key_s, val, &fb)) >= 2) {
+      if (parse_bdf(key_s, &addr)) s.bdf_mask.push_back({addr, parse_cus(val), nf == 3 ? fb : -1});
     } else if (std::sscanf(line, "hbm_limit %d %lld", &dev, &bytes) == 2) {
       if (dev >= 0 && dev < kMaxDev && bytes >= 0) s.limit[dev] = bytes;
     } else if (std::sscanf(line, "%63s %3999s", key, val) == 2 && std::strcmp(key, "cu_mask") == 0) {
@@ -799,6 +838,13 @@ __attribute__((visibility("default"))) long long gtk_vgpu_limit(int dev) {
   if (dev < 0 || dev >= kMaxDev) return -1;
   std::lock_guard<std::mutex> g(st().mu);
   return st().limit[dev];
+}
+
+// address-keyed config entries no GPU agent had (each reported on stderr; applied to its fallback
+// ordinal when the config names one); -1 while the runtime has not enumerated its agents yet
+__attribute__((visibility("default"))) int gtk_vgpu_unmatched() {
+  agents();  // resolves the config once the runtime can enumerate
+  return st().unmatched.load();
 }
 
 // queues of this process the share's mask was applied to

@@ -917,11 +917,13 @@ class DevicePluginServer:
                 continue
             hbm = sum(int(g.vram_bytes) for g in held[p])
             if by_address:
+                # the container ordinal follows as the guard's fallback, used only when the runtime
+                # enumerates no GPU with that address (vgpu_guard.cpp: reported, never silently dropped)
                 bdf = held[p][0].bdf
                 if hbm > 0:
-                    lines.append(f"hbm_limit_bdf {bdf} {hbm}")
+                    lines.append(f"hbm_limit_bdf {bdf} {hbm} {ordinal}")
                 if p in cus:
-                    lines.append(f"cu_mask_bdf {bdf} {format_cus(cus[p])}")
+                    lines.append(f"cu_mask_bdf {bdf} {format_cus(cus[p])} {ordinal}")
             elif hbm > 0:
                 lines.append(f"hbm_limit {ordinal} {hbm}")
         if mask and not by_address:

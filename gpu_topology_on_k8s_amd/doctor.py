@@ -207,7 +207,31 @@ def run_checks(backend: str = "auto", fake_n: Optional[int] = None, gpu: bool = 
                         allowed=allowed)
     if gpu:
         checks += check_gpu()
+        checks += check_guard(env)  # after the runtime started: the guard has resolved its config
     return checks
+
+
+def check_guard(env: Dict[str, str]) -> List[Check]:
+    """Inside a guarded partial-GPU pod, once the GPU runtime has started: every address-keyed entry of
+    the guard's config matched a GPU the runtime enumerated (an unmatched one used to leave
+    the share unenforced while this doctor reported it enforced).  The guard reports each unmatched
+    entry on stderr and applies it to the fallback ordinal the plugin wrote."""
+    if env.get("GTK_VGPU_ACTIVE") != "1":
+        return []
+    import ctypes
+
+    try:
+        fn = ctypes.CDLL(None).gtk_vgpu_unmatched
+    except AttributeError:
+        return [_c("pod-guard", "fail", "GTK_VGPU_ACTIVE is set but libgtk_vgpu.so is not loaded in this process")]
+    n = int(fn())
+    if n < 0:
+        return [_c("pod-guard", "skip", "the GPU runtime has not enumerated its devices in this process")]
+    if n:
+        return [_c("pod-guard", "fail", f"{n} address-keyed guard entr{'y' if n == 1 else 'ies'} matched no GPU the runtime "
+                                        "enumerated (see the gtk-vgpu lines on stderr): applied to the plugin's fallback "
+                                        "ordinal when it wrote one, else unenforced", unmatched=n)]
+    return [_c("pod-guard", "ok", "every address-keyed guard entry matched a GPU")]
 
 
 def main(a) -> int:

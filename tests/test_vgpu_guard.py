@@ -509,3 +509,46 @@ def test_a_new_allocation_never_truncates_a_table_a_live_process_maps(tmp_path):
     assert not os.path.exists(first) and not os.path.exists(first[:-5] + ".conf")
     assert not os.path.exists(second) and os.path.exists(third)  # second was never locked: also collected
     assert os.path.getsize(third) == 0  # fresh; the guard formats it on first use
+
+
+@pytest.mark.parametrize("fallback", [True, False])
+def test_an_address_no_gpu_has_is_reported_and_falls_back(tmp_path, fallback):
+    """ADVICE r5 (vgpu_guard.cpp:238): a config address that matches no ROCr agent used to leave the share
+    silently unlimited.  Now each such entry is reported on stderr and counted (gtk_vgpu_unmatched, which
+    `gtk doctor --gpu` checks); with the fallback ordinal the plugin writes it is applied there, so the
+    share still holds."""
+    conf = tmp_path / "gtk-vgpu.conf"
+    fb = " 0" if fallback else ""
+    conf.write_text(f"hbm_limit_bdf 0000:99:00.0 {8 * GiB}{fb}\ncu_mask_bdf 0000:99:00.0 64-127{fb}\n")
+    env = {k: v for k, v in os.environ.items() if k not in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES")}
+    env.update(GTK_VGPU_CONFIG=str(conf), FAKE_HIP_DEVICE="0")
+    env["LD_PRELOAD"] = (env["LD_PRELOAD"] + ":" if env.get("LD_PRELOAD") else "") + str(binary("libgtk_vgpu.so"))
+    child = RENUMBER_CHILD.replace('"rocr_ordinal": g.gtk_vgpu_hip_ordinal(0)}',
+                                   '"rocr_ordinal": g.gtk_vgpu_hip_ordinal(0), "unmatched": g.gtk_vgpu_unmatched(), '
+                                   '"doctor": __import__("gpu_topology_on_k8s_amd.doctor", fromlist=["x"]).check_guard(os.environ)}')
+    p = subprocess.run([sys.executable, "-c", child, _fake()], capture_output=True, text=True, timeout=60, env=env, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert "0000:99:00.0 matches none of the 2 GPUs" in p.stderr
+    assert out["unmatched"] == 2 and out["doctor"][0]["status"] == "fail" and out["doctor"][0]["unmatched"] == 2
+    if fallback:
+        assert "fallback ROCr ordinal" in p.stderr
+        assert out["e"] == [0, 2, 0] and out["total"] == 8 * GiB and out["queue"] == "64-127", out  # still enforced
+    else:
+        assert "NOT enforced" in p.stderr and out["e"] == [0, 0, 0], out  # loud, not silent
+
+
+def test_doctor_passes_when_every_address_matched(tmp_path):
+    conf = tmp_path / "gtk-vgpu.conf"
+    conf.write_text(f"hbm_limit_bdf 0000:05:00.0 {8 * GiB} 0\n")
+    env = {k: v for k, v in os.environ.items() if k not in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES")}
+    env.update(GTK_VGPU_CONFIG=str(conf), FAKE_HIP_DEVICE="0")
+    env["LD_PRELOAD"] = (env["LD_PRELOAD"] + ":" if env.get("LD_PRELOAD") else "") + str(binary("libgtk_vgpu.so"))
+    code = ("import ctypes, json, os, sys\nrt = ctypes.CDLL(sys.argv[1], mode=ctypes.RTLD_LOCAL)\nn = ctypes.c_int()\n"
+            "from gpu_topology_on_k8s_amd.doctor import check_guard\nbefore = check_guard(os.environ)\n"
+            "rt.hipGetDeviceCount(ctypes.byref(n))\nprint(json.dumps([before, check_guard(os.environ)]))\n")
+    p = subprocess.run([sys.executable, "-c", code, _fake()], capture_output=True, text=True, timeout=60, env=env, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-2000:]
+    before, after = json.loads(p.stdout.strip().splitlines()[-1])
+    assert before[0]["status"] == "skip" and after[0]["status"] == "ok", (before, after)
+    assert "matches none" not in p.stderr

@@ -120,7 +120,9 @@ MUTANTS: List[Mutant] = [
            "    if (false) return e;"),
     Mutant("guard", GUARD, "        if (i == s.mine || slot_alive(s.acct_fd, i)) total += s.table->slot[i].used[dev];",
            "        if (i == s.mine) total += s.table->slot[i].used[dev];"),
-    Mutant("guard", GUARD, "      if (a.bdf[o] == l.first) s.limit[o] = l.second;", "      if (a.bdf[o] == l.first) s.limit[0] = l.second;"),
+    Mutant("guard", GUARD, "    if (o >= 0) s.limit[o] = l.bytes;", "    if (o >= 0) s.limit[0] = l.bytes;"),
+    Mutant("guard", GUARD, "    if (o < 0) ++unmatched, o = unmatched_ordinal(a, \"hbm_limit_bdf\", l.addr, l.fallback);",
+           "    if (o < 0) ++unmatched;"),
     Mutant("guard", GUARD, "    if (any)  // an empty intersection would stop the queue: the share's own mask applies instead",
            "    if (true)"),
     # probe banding
