@@ -305,15 +305,23 @@ class CheckpointWriter:
             dist.barrier()
 
     def _prune(self, current: str) -> None:
-        """Keep ``current`` (what ``latest`` now names) and the newest ``keep - 1`` other steps.  A run
-        resumed from an older step re-saves lower step numbers than the directories it left behind;
-        counting ``current`` by its number would delete it (keep = 1) and leave ``latest`` dangling."""
+        """Keep ``current`` (what ``latest`` now names) and the ``keep - 1`` newest steps before it.  A
+        run resumed from an older step re-saves lower step numbers than the directories the abandoned
+        run left behind: those (numbered above ``current``) are that run's future, not this one's past,
+        and are deleted — kept, they would crowd this run's own checkpoints out of ``keep`` and be what
+        ``latest_checkpoint``'s fallback picks if ``latest`` ever names an incomplete directory
+        (ADVICE r5).  ``current`` itself is never counted by its number (keep = 1 would delete it)."""
         if self.keep <= 0:
             return
+        cur = int(current[5:])
         # numeric order: the zero padding stops sorting lexicographically past step 999999
-        steps = sorted((d for d in os.listdir(self.root) if d.startswith("step_") and d[5:].isdigit() and d != current and
-                        os.path.exists(os.path.join(self.root, d, "meta.json"))), key=lambda d: int(d[5:]))
-        for d in steps[:max(0, len(steps) - (self.keep - 1))]:
+        steps = sorted((d for d in os.listdir(self.root) if d.startswith("step_") and d[5:].isdigit() and d != current),
+                       key=lambda d: int(d[5:]))
+        for d in steps:
+            if int(d[5:]) > cur:  # the abandoned run's (complete or not)
+                shutil.rmtree(os.path.join(self.root, d), ignore_errors=True)
+        older = [d for d in steps if int(d[5:]) < cur and os.path.exists(os.path.join(self.root, d, "meta.json"))]
+        for d in older[:max(0, len(older) - (self.keep - 1))]:
             shutil.rmtree(os.path.join(self.root, d), ignore_errors=True)
 
     def has(self, step: int) -> bool:

@@ -51,6 +51,9 @@ GATHER_FRACTION = 0.5  # of (k-1) x median single-pair read
 RING_MIN_FRACTION = 0.6  # of the pair-sum bound
 RING_MAX_FRACTION = 1.1
 BAND_MIN = 0.03  # links within 3 % of their class median (or within their own repeat spread) are equal
+# a link's own repeat spread widens its band at most this far: an unstable link (repeats spreading by
+# tens of percent, e.g. an intermittently degraded one) is never snapped onto its class's healthy value
+BAND_SPREAD_CAP = 0.10
 
 Pair = Tuple[int, int]
 
@@ -144,7 +147,8 @@ def band_links(topo: Topology, raw: np.ndarray, spread: Optional[np.ndarray] = N
     classes: Dict[Tuple[int, int, bool], List[Pair]] = {}
     for pr in meas:
         classes.setdefault(link_class(topo, *pr), []).append(pr)
-    report: Dict[str, object] = {"band_min": BAND_MIN, "classes": [], "kept": []}
+    report: Dict[str, object] = {"band_min": BAND_MIN, "band_spread_cap": BAND_SPREAD_CAP, "classes": [], "kept": [],
+                                 "unstable": []}
     for key in sorted(classes):
         prs = classes[key]
         med = float(np.median([meas[p] for p in prs]))
@@ -158,7 +162,10 @@ def band_links(topo: Topology, raw: np.ndarray, spread: Optional[np.ndarray] = N
                     value, reused = pmed, True
         snapped = 0
         for p in prs:
-            band = max(cls_band, float(sp[p]))  # the class's typical repeat spread, or this link's own
+            # the class's typical repeat spread, or this link's own up to BAND_SPREAD_CAP
+            band = max(cls_band, min(float(sp[p]), BAND_SPREAD_CAP))
+            if float(sp[p]) > BAND_SPREAD_CAP:
+                report["unstable"].append([int(p[0]), int(p[1])])
             if abs(meas[p] - med) <= band * med and meas[p] >= floors[p]:
                 out[p] = value
                 snapped += 1
@@ -169,6 +176,8 @@ def band_links(topo: Topology, raw: np.ndarray, spread: Optional[np.ndarray] = N
                                   "reused_previous": reused})
     report["kept_count"] = len(report["kept"])
     report["kept"] = report["kept"][:64]  # the node annotation carries this report: bounded
+    report["unstable_count"] = len(report["unstable"])
+    report["unstable"] = report["unstable"][:64]
     return out, report
 
 

@@ -82,6 +82,30 @@ def test_a_resumed_run_saving_older_steps_keeps_its_latest(tmp_path):
     assert latest_checkpoint(str(tmp_path)).endswith("step_000003")
 
 
+def test_a_resumed_run_keeps_its_own_checkpoints_not_the_abandoned_runs(tmp_path):
+    """ADVICE r5 (checkpoint.py:314): the abandoned run saved 100, 200 and 300; this run resumes from 100
+    with keep = 2 and saves 150, then 250.  The survivors are this run's current step and its
+    predecessor: the abandoned run's 200 and 300 are gone at the first save, so no later save deletes
+    this run's previous checkpoint to keep them, and the fallback never picks them."""
+    cfg = LlamaConfig.tiny()
+    m = Llama(cfg, device="cpu")
+    opt = FlatAdamW(m.flat)
+    w = CheckpointWriter(str(tmp_path), m, opt, keep=3)
+    for s in (100, 200, 300):
+        w.save(s)
+    w.close()
+    w = CheckpointWriter(str(tmp_path), m, opt, keep=2)  # resumed from step 100
+    w.save(150)
+    w.close()
+    assert sorted(d for d in os.listdir(tmp_path) if d.startswith("step_")) == ["step_000100", "step_000150"]
+    w = CheckpointWriter(str(tmp_path), m, opt, keep=2)
+    w.save(250)
+    w.close()
+    assert sorted(d for d in os.listdir(tmp_path) if d.startswith("step_")) == ["step_000150", "step_000250"]
+    os.unlink(tmp_path / "step_000250" / "meta.json")  # latest names an incomplete directory: the fallback
+    assert latest_checkpoint(str(tmp_path)).endswith("step_000150")  # finds this run's, not the old run's 300
+
+
 def test_layout_mismatch_is_refused(tmp_path):
     m = Llama(LlamaConfig.tiny(), device="cpu")
     w = CheckpointWriter(str(tmp_path), m, FlatAdamW(m.flat))

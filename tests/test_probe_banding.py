@@ -178,6 +178,28 @@ def test_a_link_whose_own_repeats_spread_widely_takes_its_band_from_them():
     assert [2, 3] in rep["kept"] and [0, 1] not in rep["kept"]
 
 
+def test_an_unstable_link_well_below_its_class_keeps_its_number():
+    """ADVICE r5 (checks.py:161): a link at 60 % of its class whose repeats spread 45 % (an intermittently
+    degraded link) is above the 0.5 x median floor, and its own spread alone would have widened its band
+    to 45 %; the widening is capped, so it keeps its measured value and is reported unstable."""
+    t = f7_mi355x()
+    raw = np.full((8, 8), LINK)
+    spread = np.full((8, 8), 0.01)
+    np.fill_diagonal(raw, np.nan)
+    raw[4, 6] = raw[6, 4] = LINK * 0.6
+    spread[4, 6] = spread[6, 4] = 0.45
+    banded, rep = band_links(t, raw, spread)
+    assert banded[4, 6] == pytest.approx(LINK * 0.6) and banded[6, 4] == pytest.approx(LINK * 0.6)
+    assert [4, 6] in rep["kept"] and [4, 6] in rep["unstable"] and rep["unstable_count"] == 2
+    t = _with(t, banded)
+    assert t.cost[4, 6] > t.cost[4, 5] * 1.5  # the published cost carries it: placements pay for the link
+
+
+def _with(t, bw):
+    t.set_measured_bw(bw, {"method": "banded"})
+    return t
+
+
 def test_links_inside_a_package_and_across_packages_are_separate_classes():
     """XCPs of one package talk over Infinity Fabric, others over xGMI: even when a backend reports both
     as one-hop links of the same type, they are banded against their own class medians, not mixed."""

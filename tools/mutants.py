@@ -129,8 +129,9 @@ MUTANTS: List[Mutant] = [
     Mutant("banding", CHECKS, "            if abs(meas[p] - med) <= band * med and meas[p] >= floors[p]:",
            "            if abs(meas[p] - med) <= band * med:"),
     Mutant("banding", CHECKS, "                if abs(med - pmed) <= cls_band * pmed:", "                if False:"),
-    Mutant("banding", CHECKS, "            band = max(cls_band, float(sp[p]))  # the class's typical repeat spread, or this link's own",
-           "            band = cls_band"),
+    Mutant("banding", CHECKS, "            band = max(cls_band, min(float(sp[p]), BAND_SPREAD_CAP))", "            band = cls_band"),
+    Mutant("banding", CHECKS, "            band = max(cls_band, min(float(sp[p]), BAND_SPREAD_CAP))",
+           "            band = max(cls_band, float(sp[p]))"),
     Mutant("banding", CHECKS,
            "    return int(topo.link_type[a, b]), int(topo.hops[a, b]), int(topo.physical[a]) == int(topo.physical[b])",
            "    return int(topo.link_type[a, b]), int(topo.hops[a, b]), True"),
