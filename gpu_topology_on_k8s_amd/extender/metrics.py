@@ -40,6 +40,14 @@ class ExtenderMetrics:
                                        "binds whose node allocation ledger changed under them (409): re-decided",
                                        registry=self.registry)
         self.ledger_conflicts = 0
+        self.bind_lock_seconds = Histogram("gtk_extender_bind_node_lock_seconds",
+                                           "time a bind held its node's lock (refresh + decide + ledger + annotate + bind): "
+                                           "informer events for that node wait this long",
+                                           buckets=_LAT_BUCKETS + (10.0, 30.0), registry=self.registry)
+        self.bind_aborts = Counter("gtk_extender_bind_aborts_total",
+                                   "binds given up because they ran out of time (retry budget, or too slow to finish "
+                                   "before their ledger entry could lapse in another extender's view)", ["reason"],
+                                   registry=self.registry)
         self.probing_skips = Counter("gtk_extender_probing_skips_total",
                                      "node evaluations skipped because the node's device plugin is re-probing its links",
                                      registry=self.registry)

@@ -54,7 +54,7 @@ from ..placement.legacy import design_greedy_select
 from ..topology.cpus import access_costs, recommended_cpuset
 from ..topology.model import Topology
 from ..topology.shares import slices_per_gpu
-from .cache import ClusterCache, NodeState
+from .cache import LEDGER_GRACE_S, ClusterCache, NodeState
 from .ledger import LedgerStore
 from .metrics import ExtenderMetrics
 
@@ -98,6 +98,9 @@ class ExtenderConfig:
     # upgrade between the two ("both"; docs/MIGRATION.md)
     ledger_store: str = "lease"
     ledger_namespace: str = "kube-system"
+    # a bind holds its node's lock while it refreshes, decides, records and binds, and the informer's
+    # events for that node wait on it: the ledger retry loop gives up after this long
+    bind_budget_s: float = 10.0
 
 
 @dataclass
@@ -110,6 +113,21 @@ class Decision:
     micros: float
     cpuset: str = ""
     rank: float = float("nan")  # objective + node-level packing term: what nodes are compared by
+
+
+class _held:
+    """Context manager observing how long a block ran (a lock held) into a Histogram."""
+
+    def __init__(self, hist):
+        self.hist = hist
+
+    def __enter__(self):
+        self.t0 = time.perf_counter()
+        return self
+
+    def __exit__(self, *exc):
+        self.hist.observe(time.perf_counter() - self.t0)
+        return False
 
 
 def normalized_scores(objectives: Dict[str, float], resolution: float = 0.005) -> Dict[str, int]:
@@ -481,7 +499,12 @@ class TopologyExtender:
             if self.cfg.scheduler_names and sched not in self.cfg.scheduler_names:
                 raise ApiError(403, f"pod {namespace}/{name} uses scheduler {sched!r}, not one of {list(self.cfg.scheduler_names)}")
             key = pod_key(pod)
+            started = time.monotonic()
             for attempt in range(max(1, self.cfg.ledger_attempts)):
+                if attempt and time.monotonic() - started > self.cfg.bind_budget_s:
+                    self.metrics.bind_aborts.labels("budget").inc()
+                    raise ApiError(409, f"bind {namespace}/{name} on {node}: {attempt} ledger conflicts in "
+                                        f"{time.monotonic() - started:.1f}s (budget {self.cfg.bind_budget_s:.0f}s)")
                 st = self.cache.get(node, sync=False)
                 # serialise refresh+select+annotate+bind per node (in this process).  The refresh (2 API
                 # calls) runs under this node's lock, and takes no other node's: the decision must see
@@ -490,7 +513,7 @@ class TopologyExtender:
                 # a pod its writer saw bound -- over an older LIST that does not show that pod yet; the
                 # pod's devices then look free and the resourceVersion precondition (the newer object's)
                 # passes: one device, two pods.
-                with st.lock:
+                with st.lock, _held(self.metrics.bind_lock_seconds):
                     if self.cache.refresh_node(node) is not st:
                         continue  # the node was dropped and re-created meanwhile: decide on the new state
                     d, why = self._eval_state(pod, node, st, k)
@@ -526,7 +549,7 @@ class TopologyExtender:
                                                     f"for the extender's service account (or run with --bind-ledger off "
                                                     f"for a single extender): {e}") from e
                             raise
-                    return self._commit(pod, namespace, name, uid, node, key, d, st, now)
+                    return self._commit(pod, namespace, name, uid, node, key, d, st, now, time.monotonic())
             raise ApiError(409, f"bind {namespace}/{name} on {node}: the node's allocation ledger kept changing "
                                 f"({self.cfg.ledger_attempts} attempts)")
         except Exception as e:
@@ -538,8 +561,14 @@ class TopologyExtender:
             self.metrics.observe("bind", time.perf_counter() - t0)
 
     def _commit(self, pod, namespace: str, name: str, uid: str, node: str, key: str, d: Decision, st: NodeState,
-                now: float) -> Decision:
-        """Under ``st.lock``, the devices recorded: annotate the pod, bind it; undo everything on failure."""
+                now: float, recorded: Optional[float] = None) -> Decision:
+        """Under ``st.lock``, the devices recorded: annotate the pod, bind it; undo everything on failure.
+
+        ``recorded``: when the ledger entry was written (monotonic).  Another extender counts the entry
+        for LEDGER_GRACE_S from when it first sees it, never before it was written; a bind that has not
+        reached the apiserver's binding call within half of that (a throttled or retrying apiserver) is
+        given up and rolled back rather than completed after the entry may have lapsed and the devices
+        been handed out again."""
         pa = PodAssignment.assumed(d.ids, now)
         ann = pa.to_annotations()
         t = st.topology
@@ -551,6 +580,10 @@ class TopologyExtender:
         self.cache.assume(node, key, d.ids, now, cpuset=d.cpuset, uid=uid or str(meta(pod).get("uid", "")))
         try:
             self._patch_with_retry(namespace, name, ann)
+            if self.cfg.ledger and recorded is not None and time.monotonic() - recorded > LEDGER_GRACE_S / 2:
+                self.metrics.bind_aborts.labels("ledger_grace").inc()
+                raise ApiError(503, f"bind {key} on {node}: {time.monotonic() - recorded:.1f}s after recording its devices, "
+                                    f"past half the ledger grace ({LEDGER_GRACE_S:.0f}s); rolled back for kube-scheduler to retry")
             self.api.bind_pod(namespace, name, uid, node)
             self.cache.bound(node, key)
         except Exception:

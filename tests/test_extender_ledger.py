@@ -480,3 +480,60 @@ def test_a_mixed_fleet_during_the_ledger_migration_never_shares_a_device():
     assert not set(out[0]) & set(out[1]), out
     assert parse_ledger(obj_annotations(api.get_node("n1")))  # the old writer's view is kept current
     assert parse_ledger(obj_annotations(api.get_lease(NS, lease_name("n1"))))
+
+
+def test_a_bind_too_slow_to_beat_its_ledger_grace_is_rolled_back(monkeypatch):
+    """ADVICE r5 (cache.py:41): another extender stops counting a ledger entry LEDGER_GRACE_S after it
+    first saw it, bound or not.  A bind whose pod annotation took longer than half that (a throttled
+    apiserver) must not go on to bind: it is rolled back, its entry released, and kube-scheduler retries."""
+    from gpu_topology_on_k8s_amd.extender import scheduler as sch
+    from gpu_topology_on_k8s_amd.k8s.api import ApiError
+
+    monkeypatch.setattr(sch, "LEDGER_GRACE_S", 0.2)
+    api, exts, _ = _two(ledger=True, n_pods=1)
+    real = exts[0]._patch_with_retry
+
+    def slow(*a, **kw):
+        import time as _t
+
+        _t.sleep(0.15)
+        return real(*a, **kw)
+
+    exts[0]._patch_with_retry = slow
+    with pytest.raises(ApiError) as ei:
+        _bind(api, exts[0], "p0")
+    assert ei.value.code == 503 and "ledger grace" in str(ei.value)
+    pod = api.get_pod("default", "p0")
+    assert not (pod.get("spec") or {}).get("nodeName") and "ALIYUN_COM_GPU_GROUP" not in obj_annotations(pod)
+    assert "default/p0" not in _ledger(api)
+    assert exts[0].metrics.bind_aborts.labels("ledger_grace")._value.get() == 1
+
+
+def test_the_bind_retry_loop_has_a_time_budget():
+    """ADVICE r5 (scheduler.py:487): informer events for a node wait while a bind holds its lock; a ledger
+    that keeps conflicting ends the bind after `bind_budget_s`, not after the apiserver's patience."""
+    import time as _t
+
+    from gpu_topology_on_k8s_amd.k8s.api import ApiError
+
+    api = FakeAPIServer()
+    c = Contract()
+    t = fx.f7_mi355x()
+    api.create_node(make_node("n1", labels={c.label_model: "MI355X"}, annotations=encode_node_annotations(t, c),
+                              capacity={c.resource_name: str(t.n)}))
+    ext = TopologyExtender(api, _cfg(ledger=True, bind_budget_s=0.1, ledger_attempts=100))
+    api.create_pod(make_pod("p0", gpus=1))
+    real = ext.cache.refresh_node
+
+    def slow_refresh(name):
+        _t.sleep(0.04)
+        return real(name)
+
+    ext.cache.refresh_node = slow_refresh
+    api.inject("create_lease" if STORE["store"] == "lease" else "patch_node", 409, times=1000)
+    t0 = _t.monotonic()
+    with pytest.raises(ApiError) as ei:
+        _bind(api, ext, "p0")
+    assert ei.value.code == 409 and "budget" in str(ei.value) and _t.monotonic() - t0 < 1.0
+    assert ext.metrics.bind_aborts.labels("budget")._value.get() == 1
+    assert ext.metrics.bind_lock_seconds._sum.get() > 0
