@@ -62,6 +62,9 @@ def main(argv=None) -> int:
                     help="record every bind's devices in the node's allocation ledger (<prefix>/gpu-ledger, see "
                          "--ledger-store) with the ledger's resourceVersion as a precondition, so extender replicas never "
                          "hand out one GPU twice; off = the per-process node lock only (a single extender)")
+    ap.add_argument("--bind-budget", type=float, default=10.0,
+                    help="seconds a bind may spend re-deciding on ledger conflicts before it answers 409 and lets "
+                         "kube-scheduler retry (informer events for that node wait while a bind holds its lock)")
     ap.add_argument("--log-level", default="INFO")
     a = ap.parse_args(argv)
     logging.basicConfig(level=a.log_level, format='{"ts":"%(asctime)s","lvl":"%(levelname)s","mod":"%(name)s","msg":"%(message)s"}')
@@ -73,7 +76,8 @@ def main(argv=None) -> int:
                          policy=PlacementPolicy(tie_break=a.tie_break, partition_aware=a.partition_aware == "on"),
                          assume_ttl=a.assume_ttl, resync_s=a.resync,
                          scheduler_names=tuple(x.strip() for x in a.scheduler_names.split(",") if x.strip()),
-                         ledger=a.bind_ledger == "on", ledger_store=a.ledger_store, ledger_namespace=a.ledger_namespace)
+                         ledger=a.bind_ledger == "on", ledger_store=a.ledger_store, ledger_namespace=a.ledger_namespace,
+                         bind_budget_s=a.bind_budget)
     ext = TopologyExtender(api, cfg)
     if a.informer == "on":
         ext.cache.make_informer(page_size=a.list_page_size, watch_cache=a.list_from_watch_cache == "on").start()
