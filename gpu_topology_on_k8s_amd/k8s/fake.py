@@ -138,6 +138,8 @@ class FakeAPIServer(KubeAPI):
         with self._lock:
             self._enter({"Node": "list_nodes", "Pod": "list_pods"}.get(kind, f"list_{kind}"))
             if continue_token:
+                if resource_version not in (None, ""):  # as the apiserver's validation answers
+                    raise ApiError(400, "specifying resource version is not allowed when using continue")
                 snap = self._pages.pop(continue_token, None)
                 if snap is None:
                     raise Gone("the provided continue parameter is too old")

@@ -10,12 +10,16 @@ import pytest
 from gpu_topology_on_k8s_amd.extender import ExtenderConfig, TopologyExtender
 from gpu_topology_on_k8s_amd.k8s import Contract, FakeAPIServer, PodAssignment, serve_http
 from gpu_topology_on_k8s_amd.k8s.annotations import encode_node_annotations
-from gpu_topology_on_k8s_amd.k8s.api import Gone, RestKubeAPI
+from gpu_topology_on_k8s_amd.k8s.api import ApiError, Gone, RestKubeAPI
 from gpu_topology_on_k8s_amd.k8s.informer import Informer
 from gpu_topology_on_k8s_amd.k8s.objects import LIVE_POD_SELECTOR, make_node, make_pod, match_fields, trim_node, trim_pod
 from gpu_topology_on_k8s_amd.topology import fixtures as fx
 
 C = Contract()
+
+
+def meta_name(o):
+    return o["metadata"]["name"]
 
 
 def _wait(pred, timeout=10.0):
@@ -218,3 +222,46 @@ def test_a_watch_cache_list_does_not_drop_a_bind_it_cannot_show():
     assert {2, 3} <= cache.get("n", sync=False).used(time.time(), 300)
     cache.on_list("Pod", [], cache.begin_list("Pod"), consistent=True)
     assert not {2, 3} & cache.get("n", sync=False).used(time.time(), 300)
+
+
+def test_watch_events_are_transformed_and_a_delivered_event_resets_the_backoff():
+    """Watch events go through the same trim as LIST items (a bulky pod never lands in the cache), and
+    the back-off restarts from its base once a watch delivers again: a cluster that had a bad minute
+    does not pay its longest delay on the next, unrelated disconnect."""
+    api = _cluster(n_nodes=1, pods_per_node=1)
+    got = []
+    inf = Informer(api, lambda k, items: None, lambda t, k, o: got.append((t, o)), kinds=("Pod",),
+                   transform=lambda k, o: trim_pod(o), watch_timeout=2.0, backoff=0.01, max_backoff=0.05)
+    delays = []
+    real = inf._delay
+    inf._delay = lambda f: (delays.append(f), real(f))[1]
+    api.inject("watch_Pod", 503, times=2)  # the first two watches are refused ...
+    try:
+        inf.start()
+        assert inf.wait_synced(10)
+        api.create_pod(_bulky(make_pod("late0", gpus=1, node="n0")))
+        assert _wait(lambda: any(meta_name(o) == "late0" for _, o in got))
+        api.cut_watch("Pod", after=0)  # ... then, after a delivered event, the open watch breaks
+        api.create_pod(make_pod("late1", gpus=1, node="n0"))
+        assert _wait(lambda: len(delays) >= 3)
+        assert delays[:3] == [1, 2, 1], delays
+        assert _wait(lambda: any(meta_name(o) == "late1" for _, o in got))  # resumed, not lost
+        assert inf.relists() == 0
+        o = next(o for _, o in got if meta_name(o) == "late0")
+        assert "managedFields" not in o["metadata"] and "env" not in o["spec"]["containers"][0]
+    finally:
+        inf.stop()
+
+
+def test_continue_pages_carry_no_resource_version():
+    """The apiserver refuses a page request that names both a continue token and a resourceVersion;
+    the informer sends the version on the first page only."""
+    api = _cluster()
+    api.watch_cache_pages = True
+    _, _, cont = api.list_page("Pod", limit=4, resource_version="0")
+    with pytest.raises(ApiError) as ei:
+        api.list_page("Pod", limit=4, continue_token=cont, resource_version="0")
+    assert ei.value.code == 400
+    inf = Informer(api, lambda k, items: None, lambda *a: None, kinds=("Pod",), page_size=4, watch_timeout=1.0)
+    items, _, consistent = inf._list("Pod")
+    assert len(items) == 30 and not consistent and inf.pages["Pod"] == 8

@@ -3,8 +3,8 @@
 catch it (a mutation-testing pass; README "Mutation testing of the control plane").
 
     python tools/mutants.py                  # every group
-    python tools/mutants.py --only ledger    # one group (ledger, cache, plugin, dp, guard, banding, gaia,
-                                             # repartition, extender)
+    python tools/mutants.py --only ledger    # one group (ledger, cache, plugin, informer, rbac, dp, guard,
+                                             # banding, gaia, repartition, extender, contract)
 
 Each mutant replaces one line (or a few) of a source file, runs the group's tests with pytest-xdist,
 and restores the file whatever happens.  ``CAUGHT`` = some test failed, ``SURVIVED`` = the tests did
@@ -43,6 +43,8 @@ CHECKS = "gpu_topology_on_k8s_amd/ops/checks.py"
 GAIA = "gpu_topology_on_k8s_amd/placement/gaia.py"
 REPART = "gpu_topology_on_k8s_amd/deviceplugin/repartition.py"
 ANN = "gpu_topology_on_k8s_amd/k8s/annotations.py"
+INFORMER = "gpu_topology_on_k8s_amd/k8s/informer.py"
+RBAC = "gpu_topology_on_k8s_amd/k8s/rbac.py"
 
 MUTANTS: List[Mutant] = [
     # allocation ledger (cross-extender bind safety)
@@ -64,6 +66,10 @@ MUTANTS: List[Mutant] = [
     Mutant("ledger", SCHED, "                    if self.cache.refresh_node(node) is not st:",
            "                    if self.cache.refresh_node(node) is not st and False:", equivalent=True,
            why="the node object is re-created only when a node is deleted and re-added mid-bind"),
+    Mutant("ledger", SCHED, "                if attempt and time.monotonic() - started > self.cfg.bind_budget_s:",
+           "                if False:"),
+    Mutant("ledger", SCHED, "            if self.cfg.ledger and recorded is not None and time.monotonic() - recorded > LEDGER_GRACE_S / 2:",
+           "            if False:"),
     # overlay / LIST epochs (the cache's view of this process's binds)
     Mutant("cache", CACHE, "                after_bind = list_epoch > self._overlay_epoch.get((st.name, key), 0)",
            "                after_bind = True"),
@@ -107,6 +113,22 @@ MUTANTS: List[Mutant] = [
     Mutant("plugin", PLUGIN, '            if pod_phase(p) != "Pending" and (pa is None or pa.assigned):',
            '            if pod_phase(p) != "Pending":'),
     Mutant("plugin", PLUGIN, '            if pod_phase(p) != "Pending" and (pa is None or pa.assigned):', '            if False:'),
+    # informer (client-go reflector semantics)
+    Mutant("informer", INFORMER, "                failures += 1\n                self.last_error = str(e)",
+           "                failures += 1\n                rv = None\n                self.last_error = str(e)"),
+    Mutant("informer", INFORMER, "                                                         resource_version=None if cont else rv_param,",
+           "                                                         resource_version=rv_param,"),
+    Mutant("informer", INFORMER, '                items, cont, rv_param = [], "", None', '                items, cont = [], ""'),
+    Mutant("informer", INFORMER, "        return d * (1.0 + self.jitter * self._rng.uniform(-1.0, 1.0))", "        return d"),
+    Mutant("informer", INFORMER, "        d = min(self.max_backoff, self.backoff * (2 ** max(0, failures - 1)))",
+           "        d = self.backoff * (2 ** max(0, failures - 1))"),
+    Mutant("informer", INFORMER, "self.on_event(t, kind, self.transform(kind, obj) if self.transform is not None else obj)",
+           "self.on_event(t, kind, obj)"),
+    Mutant("informer", INFORMER, "                    failures = 0\n                    new_rv", "                    new_rv"),
+    # per-identity RBAC of the deploy manifests
+    Mutant("rbac", RBAC, "        if self.identity.own_node_only and node != self.node_name:", "        if False:"),
+    Mutant("rbac", RBAC, "and (self.namespace is None or self.namespace == namespace))", ")"),
+    Mutant("rbac", RBAC, "                out[m.group(1)].own_node_only = True", "                pass"),
     # data-parallel reduction
     Mutant("dp", DP, "        return b.start + self.rank * c, b.start + (self.rank + 1) * c", "        return b.start, b.start + c"),
     Mutant("dp", DP, "                if b.work is None:\n                    self._launch(b)", "                if False:\n                    self._launch(b)"),
@@ -171,6 +193,8 @@ TESTS = {
                "tests/test_daemons.py", "tests/test_health.py", "tests/test_sim.py", "tests/test_churn.py",
                "tests/test_reprobe_admission.py", "tests/test_partition.py", "tests/test_shares.py",
                "tests/test_multicontainer.py"],
+    "informer": ["tests/test_informer.py", "tests/test_cluster_features.py", "tests/test_rbac.py"],
+    "rbac": ["tests/test_rbac.py", "tests/test_config_cli.py"],
     "dp": ["tests/test_dp_check.py", "tests/test_llama_dp_cpu.py", "tests/test_checkpoint.py"],
     "guard": ["tests/test_vgpu_guard.py"],
     "banding": ["tests/test_probe_banding.py", "tests/test_probe_checks.py"],
