@@ -101,6 +101,12 @@ def test_a_link_below_its_floor_keeps_its_number_even_inside_a_wide_band():
     spread[1, 6] = 5.0  # a spread so wide that the band alone would snap it
     banded, rep = band_links(t, raw, spread)
     assert banded[1, 6] == 30.0 and [1, 6] in rep["kept"]
+    # the class's own band can be that wide too (every repeat of a noisy probe spreading by 80 %): the
+    # floor still keeps the slow link's number, it is not smoothed into the class's healthy value
+    spread = np.where(np.isnan(spread), np.nan, 0.8)
+    banded, rep = band_links(t, raw, spread)
+    assert banded[1, 6] == 30.0 and [1, 6] in rep["kept"]
+    assert banded[0, 1] == pytest.approx(np.nanmedian(raw[~np.eye(8, dtype=bool)]), rel=0.02)
 
 
 def test_two_reprobes_of_one_node_publish_the_same_cost_annotation():

@@ -188,7 +188,8 @@ MUTANTS: List[Mutant] = [
 TESTS = {
     "ledger": ["tests/test_extender_ledger.py", "tests/test_extender.py", "tests/test_cluster_features.py", "tests/test_churn.py",
                "tests/test_rbac.py"],
-    "cache": ["tests/test_cluster_features.py", "tests/test_extender.py", "tests/test_extender_ledger.py", "tests/test_churn.py"],
+    "cache": ["tests/test_cluster_features.py", "tests/test_extender.py", "tests/test_extender_ledger.py", "tests/test_churn.py",
+              "tests/test_informer.py"],
     "plugin": ["tests/test_deviceplugin.py", "tests/test_cluster_features.py", "tests/test_preferred_allocation_props.py",
                "tests/test_daemons.py", "tests/test_health.py", "tests/test_sim.py", "tests/test_churn.py",
                "tests/test_reprobe_admission.py", "tests/test_partition.py", "tests/test_shares.py",
