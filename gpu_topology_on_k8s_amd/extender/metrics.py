@@ -7,13 +7,17 @@ Fragmentation index of a node = 1 - (free devices in its fullest group) / (free 
 group is a physical GPU on partitioned nodes and a NUMA domain otherwise: 0 when every free device
 sits in one group (the next large request gets a compact set), toward 1 as free devices scatter.
 The cluster index weights nodes by free devices.  ``gtk_extender_placeable_nodes{k}`` counts the
-nodes that can still host a k-device pod."""
+nodes that can still host a k-device pod.
+
+The informer's health (k8s/informer.py) is exported per kind: complete LISTs (a count above 1 is a
+relist, which at 100,000 pods costs tens of seconds and hundreds of MB: ``profiles/sched/INFORMER.md``),
+LIST pages, watch events, watches resumed and watch errors, and the size and duration of the last LIST."""
 from __future__ import annotations
 
 from typing import TYPE_CHECKING
 
 from prometheus_client import CollectorRegistry, Counter, Histogram, generate_latest
-from prometheus_client.core import GaugeMetricFamily
+from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily
 
 if TYPE_CHECKING:  # pragma: no cover
     from .scheduler import Decision
@@ -58,6 +62,7 @@ class ExtenderMetrics:
         """Export fragmentation gauges from ``cache`` (an :class:`~.cache.ClusterCache`) at scrape time."""
         if self._cache is None:
             self.registry.register(_FragmentationCollector(cache, ttl, clock))
+            self.registry.register(_InformerCollector(cache))
         self._cache = cache
 
     def cache(self, hit: bool, n: int = 1) -> None:
@@ -137,3 +142,34 @@ class _FragmentationCollector:
             place_g.add_metric([str(k)], c)
         cluster_g.add_metric([], (1.0 - tot_big / tot_free) if tot_free else 0.0)
         yield from (node_g, free_g, place_g, cluster_g, share_g)
+
+
+class _InformerCollector:
+    """The cache's informer counters at scrape time (nothing while the cache polls)."""
+
+    def __init__(self, cache):
+        self.cache = cache
+
+    def collect(self):
+        inf = getattr(self.cache, "informer", None)
+        if inf is None:
+            return
+        fams = [(CounterMetricFamily(f"gtk_extender_informer_{name}", help_, labels=["kind"]), getattr(inf, attr))
+                for name, attr, help_ in (
+                    ("lists", "lists", "complete LISTs (more than one per kind: relists after a 410 Gone)"),
+                    ("list_pages", "pages", "LIST requests (limit/continue pages)"),
+                    ("events", "events", "watch events handed to the cache"),
+                    ("watch_resumes", "watch_resumes", "watches re-opened from the last resourceVersion (no relist)"),
+                    ("watch_errors", "watch_errors", "watches that broke (connection reset, 5xx, 429)"))]
+        for fam, per_kind in fams:
+            for kind, v in sorted(per_kind.items()):
+                fam.add_metric([kind], float(v))
+        items = GaugeMetricFamily("gtk_extender_informer_last_list_items", "objects in the last complete LIST", labels=["kind"])
+        secs = GaugeMetricFamily("gtk_extender_informer_last_list_seconds", "duration of the last complete LIST", labels=["kind"])
+        for kind, ll in sorted(dict(inf.last_list).items()):
+            items.add_metric([kind], ll.get("items", 0.0))
+            secs.add_metric([kind], ll.get("seconds", 0.0))
+        synced = GaugeMetricFamily("gtk_extender_informer_synced", "1 once every kind has listed")
+        synced.add_metric([], 1.0 if inf.synced else 0.0)
+        yield from [f for f, _ in fams]
+        yield from (items, secs, synced)

@@ -265,3 +265,27 @@ def test_continue_pages_carry_no_resource_version():
     inf = Informer(api, lambda k, items: None, lambda *a: None, kinds=("Pod",), page_size=4, watch_timeout=1.0)
     items, _, consistent = inf._list("Pod")
     assert len(items) == 30 and not consistent and inf.pages["Pod"] == 8
+
+
+def test_informer_health_is_on_the_extenders_metrics():
+    """An operator sees a relist storm (or its absence) on /metrics: per-kind LISTs, pages, events,
+    resumed and broken watches, and the size of the last LIST."""
+    api = _cluster(n_nodes=2, pods_per_node=3)
+    api.watch_cache_pages = True
+    ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+    assert b"gtk_extender_informer_lists" not in ext.metrics.exposition()  # polling: nothing to report
+    inf = ext.cache.make_informer(page_size=2, watch_timeout=2.0, backoff=0.02, max_backoff=0.1)
+    try:
+        inf.start()
+        assert inf.wait_synced(10)
+        api.cut_watch("Pod", after=0)
+        api.create_pod(make_pod("late", gpus=1, node="n0"))
+        assert _wait(lambda: inf.watch_errors["Pod"] >= 1 and inf.events["Pod"] >= 1)
+        text = ext.metrics.exposition().decode()
+    finally:
+        inf.stop()
+    assert 'gtk_extender_informer_lists_total{kind="Pod"} 1.0' in text
+    assert 'gtk_extender_informer_list_pages_total{kind="Pod"} 2.0' in text  # 4 live pods, 2 per page
+    assert 'gtk_extender_informer_watch_errors_total{kind="Pod"} 1.0' in text
+    assert 'gtk_extender_informer_last_list_items{kind="Pod"} 4.0' in text
+    assert "gtk_extender_informer_synced 1.0" in text
