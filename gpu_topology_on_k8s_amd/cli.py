@@ -323,7 +323,8 @@ def cmd_config(a) -> int:
                              sort_keys=False), end="")
     else:
         print(render_manifests(a.resource_name, image=a.image, time_slices=a.time_slices,
-                               partition_control=a.partition_control), end="")
+                               partition_control=a.partition_control, topology_manager_policy=a.topology_manager_policy,
+                               topology_manager_scope=a.topology_manager_scope), end="")
     return 0
 
 
@@ -473,6 +474,11 @@ def main(argv=None) -> int:
     p.add_argument("--filter", action="store_true")
     p.add_argument("--image", default="rocm/gpu-topology-k8s:latest")
     p.add_argument("--time-slices", type=int, default=1, help="manifests: device plugin --time-slices (fractional GPUs on SPX nodes)")
+    p.add_argument("--topology-manager-policy", default="", choices=["", "none", "best-effort", "restricted", "single-numa-node"],
+                   help="manifests: the GPU nodes' kubelet --topology-manager-policy, published by the device plugin so the "
+                        "extender binds the devices the kubelet will allocate")
+    p.add_argument("--topology-manager-scope", default="", choices=["", "container", "pod"],
+                   help="manifests: the GPU nodes' kubelet --topology-manager-scope")
     p.add_argument("--partition-control", action="store_true",
                    help="manifests: device plugin --partition-control on (switches partition modes on node labels; /sys writable)")
     p.add_argument("--tls-dir", default="", help="scheduler: call the extender over mutual TLS with tls.crt/tls.key/ca.crt from here")

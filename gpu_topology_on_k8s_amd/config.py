@@ -165,11 +165,16 @@ def rbac_manifests(namespace: str = NAMESPACE) -> List[Dict[str, Any]]:
 
 
 def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, namespace: str = NAMESPACE,
-                     probe: str = "quick", policy: str = "exact", time_slices: int = 1, partition_control: bool = False) -> str:
+                     probe: str = "quick", policy: str = "exact", time_slices: int = 1, partition_control: bool = False,
+                     topology_manager_policy: str = "", topology_manager_scope: str = "") -> str:
     """The DaemonSets, RBAC and scheduler config.  ``time_slices > 1``: the device plugin advertises
     every GPU as that many time slices (fractional pods; topology/shares.py).  ``partition_control``:
     the plugin switches compute / memory partition modes on the node labels' request
-    (deviceplugin/repartition.py), which writes the GPUs' sysfs, so /sys is mounted writable."""
+    (deviceplugin/repartition.py), which writes the GPUs' sysfs, so /sys is mounted writable.
+    ``topology_manager_policy`` / ``_scope``: the GPU nodes' kubelet ``--topology-manager-policy`` /
+    ``--topology-manager-scope``, handed to the plugin, which publishes them for the extender
+    (placement/numa_align.py); the kubelet's own config file is not mounted (its directory holds the
+    pods' volumes)."""
     labels = {"app.kubernetes.io/part-of": "gpu-topology-amd"}
     docs: List[Dict[str, Any]] = rbac_manifests(namespace)
     plugin_sa, ext_sa = PLUGIN_SA, EXTENDER_SA
@@ -194,7 +199,9 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
                                         f"--resource-name={resource}", f"--probe={probe}", "--discovery=auto",
                                         "--reprobe-interval=3600", "--prestart-validate", f"--metrics-port={PLUGIN_METRICS_PORT}"]
                                        + ([f"--time-slices={int(time_slices)}"] if int(time_slices) > 1 else [])
-                                       + (["--partition-control=on"] if partition_control else []),
+                                       + (["--partition-control=on"] if partition_control else [])
+                                       + ([f"--topology-manager-policy={topology_manager_policy}"] if topology_manager_policy else [])
+                                       + ([f"--topology-manager-scope={topology_manager_scope}"] if topology_manager_scope else []),
                             "ports": [{"containerPort": PLUGIN_METRICS_PORT, "name": "metrics"}],
                             # /healthz fails when the gRPC server is down, the monitor loop is wedged or
                             # re-registration keeps failing (DevicePluginServer.liveness); start-up (discovery,

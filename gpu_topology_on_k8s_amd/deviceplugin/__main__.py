@@ -123,6 +123,14 @@ def main(argv=None) -> int:
     ap.add_argument("--admission-settle", type=float, default=5.0,
                     help="a Pending pod is reconciled only once no Allocate has come for this many seconds (the "
                          "kubelet allocates a pod container by container)")
+    ap.add_argument("--topology-manager-policy", default="", choices=["", "none", "best-effort", "restricted", "single-numa-node"],
+                    help="the kubelet's --topology-manager-policy, published as a node label so the extender picks "
+                         "the devices the kubelet will offer ('' = read --kubelet-config, else none)")
+    ap.add_argument("--topology-manager-scope", default="", choices=["", "container", "pod"],
+                    help="the kubelet's --topology-manager-scope ('' = read --kubelet-config, else container)")
+    ap.add_argument("--kubelet-config", default="/var/lib/kubelet/config.yaml",
+                    help="KubeletConfiguration to read topologyManagerPolicy / topologyManagerScope from when the "
+                         "flags above are not given (skipped when absent)")
     ap.add_argument("--reprobe-interval", type=float, default=0.0,
                     help="re-measure the links (child process) every N s while no pod holds a device; 0 = never")
     ap.add_argument("--reprobe-tolerance", type=float, default=0.15,
@@ -235,6 +243,7 @@ def main(argv=None) -> int:
     health = HealthMonitor(topo, node_topology, HealthPolicy(xgmi_links=a.xgmi_link_loss == "unhealthy"))
 
     specs = a.device_specs if a.device_specs != "auto" else ("stub" if a.discovery == "fake" else "strict")
+    tm = topology_manager_of(a)
     cfg = PluginConfig(resource_name=advertised, socket_dir=a.socket_dir, socket_name=a.socket_name, dev_root=a.dev_root,
                        node_name=a.node_name, contract=contract, device_specs=specs, prestart_validate=a.prestart_validate,
                        health_interval=a.health_interval, reprobe_interval=a.reprobe_interval,
@@ -243,7 +252,7 @@ def main(argv=None) -> int:
                        probe_yield_s=a.probe_yield_seconds,
                        reconcile_interval=a.reconcile_interval, admission_settle_s=a.admission_settle, cdi_dir=a.cdi_dir, nic_env=a.nic_env == "on",
                        share_cu_mask=a.share_cu_mask == "on", share_guard=a.share_guard, guard_dir=a.share_guard_dir,
-                       policy=PlacementPolicy(partition_aware=a.partition_aware == "on"))
+                       policy=PlacementPolicy(partition_aware=a.partition_aware == "on"), topology_manager=tm)
     events = None
     if a.gpu_events == "auto" and a.discovery in ("auto", "amdsmi"):
         from .events import GpuEventWatcher
@@ -317,5 +326,19 @@ def main(argv=None) -> int:
     return 0
 
 
+def topology_manager_of(a) -> "TopologyManager":
+    """The node's Topology Manager: the flags, else the kubelet's config file, else ``none``."""
+    from ..placement.numa_align import TopologyManager, read_kubelet_config
+
+    base = TopologyManager()
+    if (not a.topology_manager_policy or not a.topology_manager_scope) and a.kubelet_config and os.path.exists(a.kubelet_config):
+        try:
+            base = read_kubelet_config(a.kubelet_config)
+        except Exception as e:  # noqa: BLE001 - an unreadable or malformed file must not stop the plugin
+            logging.getLogger("gtk.deviceplugin").warning("reading the topology manager from %s failed: %s", a.kubelet_config, e)
+    return TopologyManager(a.topology_manager_policy or base.policy, a.topology_manager_scope or base.scope)
+
+
 if __name__ == "__main__":
     sys.exit(main())
+

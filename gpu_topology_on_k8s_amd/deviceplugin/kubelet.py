@@ -7,6 +7,12 @@ apiserver, as the real kubelet does — diagram step 2), and on pod admission ca
 container with that container's count, init containers first, a regular init container's devices
 reused by the containers after it (``must_include``).  ``restart()`` wipes the socket directory like
 a kubelet restart so plugin re-registration can be tested.
+
+``topology_policy`` / ``topology_scope`` run the kubelet's Topology Manager in front of the device
+manager (``--topology-manager-policy`` / ``--topology-manager-scope``): NUMA hints from the devices'
+``TopologyInfo``, merged by the policy, admission refused with ``TopologyAffinityError``, and each
+container's devices drawn from the hinted NUMA nodes first (the device manager's ``filterByAffinity``).
+The device manager is the only hint provider modelled (no CPU or memory manager).
 """
 from __future__ import annotations
 
@@ -21,13 +27,15 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import grpc
 
-from ..k8s.objects import meta, pod_device_steps, pod_key
+from ..k8s.objects import meta, pod_device_steps, pod_gpu_request, pod_key
 from .podresources import build_response, pod_resources_handler
 from . import proto as pb
 
 log = logging.getLogger(__name__)
 
-__all__ = ["FakeKubelet", "AdmissionError"]
+__all__ = ["FakeKubelet", "AdmissionError", "TOPOLOGY_POLICIES"]
+
+TOPOLOGY_POLICIES = ("none", "best-effort", "restricted", "single-numa-node")
 
 
 class AdmissionError(RuntimeError):
@@ -41,13 +49,18 @@ class _Plugin:
     channel: grpc.Channel
     options: object
     devices: Dict[str, str] = field(default_factory=dict)  # id -> health
+    numa: Dict[str, Tuple[int, ...]] = field(default_factory=dict)  # id -> NUMA nodes of its TopologyInfo
     ready: threading.Event = field(default_factory=threading.Event)
     thread: Optional[threading.Thread] = None
 
 
 class FakeKubelet:
     def __init__(self, socket_dir: str, node_name: str = "", api=None, pod_resources_socket: Optional[str] = None,
-                 cdi_dir: Optional[str] = None):
+                 cdi_dir: Optional[str] = None, topology_policy: str = "none", topology_scope: str = "container"):
+        if topology_policy not in TOPOLOGY_POLICIES or topology_scope not in ("container", "pod"):
+            raise ValueError(f"topology manager policy/scope {topology_policy}/{topology_scope} not supported")
+        self.topology_policy = topology_policy
+        self.topology_scope = topology_scope
         self.socket_dir = socket_dir
         # a CDI-enabled runtime resolves Allocate's cdi_devices against the specs in this directory
         self.cdi_dir = cdi_dir
@@ -100,6 +113,7 @@ class FakeKubelet:
             for resp in self._stub(p, "ListAndWatch")(pb.Empty()):
                 with self._lock:
                     p.devices = {d.ID: d.health for d in resp.devices}
+                    p.numa = {d.ID: tuple(int(n.ID) for n in d.topology.nodes) for d in resp.devices}
                 p.ready.set()
                 self._update_capacity(p)
                 if self._stop.is_set():
@@ -190,51 +204,154 @@ class FakeKubelet:
             used = {i for ids in self.allocated.get(resource, {}).values() for i in ids}
             return sorted((d for d, h in p.devices.items() if h == pb.HEALTHY and d not in used), key=int)
 
-    def _reject(self, pod: dict, msg: str) -> AdmissionError:
+    def _reject(self, pod: dict, msg: str, reason: str = "UnexpectedAdmissionError") -> AdmissionError:
         """Pod admission failed: like the real kubelet, the pod is terminal (``Failed``, reason
-        ``UnexpectedAdmissionError``) and is never retried on this node; a bare pod is lost."""
+        ``UnexpectedAdmissionError``, or ``TopologyAffinityError`` from the Topology Manager) and is
+        never retried on this node; a bare pod is lost."""
         self.rejected.append((pod_key(pod), msg))
         if self.api is not None and hasattr(self.api, "set_pod_phase"):
             md = meta(pod)
             try:
-                self.api.set_pod_phase(md.get("namespace", "default"), md["name"], "Failed", reason="UnexpectedAdmissionError",
-                                       message=msg)
+                self.api.set_pod_phase(md.get("namespace", "default"), md["name"], "Failed", reason=reason, message=msg)
             except Exception:  # pragma: no cover
                 pass
-        return AdmissionError(f"UnexpectedAdmissionError: {msg}")
+        return AdmissionError(f"{reason}: {msg}")
 
-    def _devices_to_allocate(self, p: _Plugin, resource: str, required: int, in_use: set, reusable: List[str]) -> List[str]:
-        """``devicesToAllocate`` of the kubelet device manager for one container (no topology-manager
-        hint, the kubelet's default ``none`` policy): devices an init container of the pod handed on
-        come first; if they do not cover the request, the plugin's ``GetPreferredAllocation`` is asked
-        with ``available ∪ reused`` and ``must_include = reused`` for the container's full count, and
-        its answer ∩ available fills the rest (then the lowest free ids)."""
+    # ------------------------------------------------------------------ topology manager
+    # NUMA sets are bitmasks (bit i = NUMA node i), as in the kubelet's bitmask package.
+    def _numa_nodes(self, p: _Plugin) -> List[int]:
+        return sorted({n for ns in p.numa.values() for n in ns})
+
+    def _device_mask(self, p: _Plugin, d: str) -> int:
+        m = 0
+        for n in p.numa.get(d, ()):
+            m |= 1 << n
+        return m
+
+    @staticmethod
+    def _iterate_masks(nodes: List[int]):
+        """``bitmask.IterateBitMasks``: every combination of ``nodes``, one bit first, in order."""
+        def rec(rest, acc, size):
+            if len(acc) == size:
+                yield sum(1 << b for b in acc)
+                return
+            for i in range(len(rest)):
+                yield from rec(rest[i + 1:], acc + [rest[i]], size)
+        for size in range(1, len(nodes) + 1):
+            yield from rec(nodes, [], size)
+
+    def _generate_hints(self, p: _Plugin, available: set, reusable: set, request: int) -> Optional[List[Tuple[int, bool]]]:
+        """``generateDeviceTopologyHints``: None = the resource has no topology (no preference); [] = no
+        NUMA combination can hold the request."""
+        nodes = self._numa_nodes(p)
+        if not nodes:
+            return None
+        if len(available | reusable) < request:
+            return []
+        min_affinity = len(nodes)
+        hints: List[Tuple[int, bool]] = []
+        for mask in self._iterate_masks(nodes):
+            in_mask = sum(1 for d in p.devices if self._device_mask(p, d) & mask)
+            if in_mask >= request and bin(mask).count("1") < min_affinity:
+                min_affinity = bin(mask).count("1")
+            matching = 0
+            fits = True
+            for d in reusable:
+                dm = self._device_mask(p, d)
+                if not dm:
+                    continue
+                if not dm & mask:
+                    fits = False
+                    break
+                matching += 1
+            if not fits:
+                continue
+            matching += sum(1 for d in available if self._device_mask(p, d) & mask)
+            if matching >= request:
+                hints.append((mask, False))
+        return [(m, bin(m).count("1") == min_affinity) for m, _ in hints]
+
+    def _merge(self, p: _Plugin, hints: Optional[List[Tuple[int, bool]]]) -> Tuple[Optional[int], bool]:
+        """The policy's ``Merge`` with the device manager as the only provider -> (mask or None, admit)."""
+        nodes = self._numa_nodes(p)
+        default = sum(1 << n for n in nodes)
+        if hints is None:
+            return None, True
+        if self.topology_policy == "single-numa-node":
+            hints = [(m, pref) for m, pref in hints if bin(m).count("1") == 1 and pref]
+        best_mask, best_pref = default, False  # mergeFilteredHints starts from {default, false}
+        for m, pref in hints:
+            if pref and not best_pref:
+                best_mask, best_pref = m, pref
+                continue
+            if best_pref and not pref:
+                continue
+            cm, cb = bin(m).count("1"), bin(best_mask).count("1")
+            narrower = cm < cb or (cm == cb and sorted(_bits(m)) < sorted(_bits(best_mask)))
+            if narrower:
+                best_mask, best_pref = m, pref
+        if self.topology_policy == "single-numa-node" and best_mask == default:
+            best_mask = None
+        admit = self.topology_policy == "best-effort" or best_pref
+        return best_mask, admit
+
+    def _hint(self, p: _Plugin, pod: dict, request: int, available: set, reusable: set) -> Optional[int]:
+        """Admit one hint request or reject the pod (``TopologyAffinityError``)."""
+        mask, admit = self._merge(p, self._generate_hints(p, available, reusable, request))
+        if not admit:
+            raise self._reject(pod, f"Resources cannot be allocated with Topology locality (policy {self.topology_policy}, "
+                                    f"scope {self.topology_scope}, {request} devices)", reason="TopologyAffinityError")
+        return mask
+
+    def _devices_to_allocate(self, p: _Plugin, resource: str, required: int, in_use: set, reusable: List[str],
+                             hint: Optional[int] = None) -> List[str]:
+        """``devicesToAllocate`` of the kubelet device manager for one container: devices an init
+        container of the pod handed on come first.  With a Topology Manager hint (``filterByAffinity``)
+        the free devices on the hinted NUMA nodes are ``aligned``: if the container needs fewer than
+        that, the plugin's ``GetPreferredAllocation`` is asked with ``aligned ∪ reused``; otherwise it
+        gets every aligned device and the plugin is asked with ``available ∪ allocated`` for the rest.
+        Without a hint it is asked with ``available ∪ reused``.  ``must_include`` is what the container
+        holds already, the size its full count; the answer ∩ the offered devices fills the request,
+        then the lowest free ids (Go's set order is unspecified)."""
         allocated: List[str] = []
-        for d in reusable:
-            if len(allocated) == required:
-                return allocated
-            allocated.append(d)
-        if len(allocated) == required:
+
+        def allocate_remaining_from(devices) -> bool:
+            for d in sorted(devices, key=int):
+                if len(allocated) == required:
+                    break
+                if d not in allocated:
+                    allocated.append(d)
+            return len(allocated) == required
+
+        if allocate_remaining_from(sorted(reusable, key=int)):
             return allocated
         avail = [d for d in self.available(resource) if d not in in_use and d not in allocated]
         needed = required - len(allocated)
         if len(avail) < needed:
             raise ValueError(f"requested number of devices unavailable for {resource}. Requested: {required}, "
                              f"Available: {len(avail) + len(allocated)}")
-        if getattr(p.options, "get_preferred_allocation_available", False):
+        aligned = [d for d in avail if hint is not None and self._device_mask(p, d) & hint]
+        unaligned = [d for d in avail if d not in aligned]
+
+        def preferred(offered) -> List[str]:
+            if not getattr(p.options, "get_preferred_allocation_available", False):
+                return []
             req = pb.PreferredAllocationRequest()
-            req.container_requests.add(available_deviceIDs=sorted(set(avail) | set(allocated), key=int),
+            req.container_requests.add(available_deviceIDs=sorted(set(offered) | set(allocated), key=int),
                                        must_include_deviceIDs=list(allocated), allocation_size=required)
             self.preferred_calls.append((list(allocated), required))
-            pref = self._stub(p, "GetPreferredAllocation")(req, timeout=5)
-            for d in pref.container_responses[0].deviceIDs:
-                if d in avail and d not in allocated and len(allocated) < required:
-                    allocated.append(d)
-        for d in avail:
-            if len(allocated) == required:
-                break
-            if d not in allocated:
-                allocated.append(d)
+            resp = self._stub(p, "GetPreferredAllocation")(req, timeout=5)
+            return [d for d in resp.container_responses[0].deviceIDs if d in offered]
+
+        if needed < len(aligned):
+            if allocate_remaining_from(preferred(aligned)) or allocate_remaining_from(aligned):
+                return allocated
+            raise ValueError(f"unexpectedly allocated less resources than required. Requested: {required}")
+        if allocate_remaining_from(aligned):
+            return allocated
+        if allocate_remaining_from(preferred(avail)):
+            return allocated
+        allocate_remaining_from(unaligned)
         return allocated
 
     def admit(self, pod: dict, resource: str, allocate_timeout: float = 10.0):
@@ -259,10 +376,17 @@ class FakeKubelet:
             pod_ids: List[str] = []  # every device the pod holds (the device manager's podDevices)
             per_container: List[Tuple[str, str, Tuple[str, ...]]] = []
             resp = pb.AllocateResponse()
+            tm = self.topology_policy != "none"
+            hint: Optional[int] = None
+            if tm and self.topology_scope == "pod":
+                hint = self._hint(p, pod, pod_gpu_request(pod, [resource]), set(self.available(resource)), set())
             try:
                 for cname, n, kind in steps:
+                    if tm and self.topology_scope == "container":
+                        free = {d for d in self.available(resource) if d not in pod_ids}
+                        hint = self._hint(p, pod, n, free, set(reuse))
                     try:
-                        chosen = self._devices_to_allocate(p, resource, n, set(pod_ids), reuse)
+                        chosen = self._devices_to_allocate(p, resource, n, set(pod_ids), reuse, hint)
                     except ValueError as e:
                         raise self._reject(pod, str(e)) from e
                     areq = pb.AllocateRequest()
@@ -334,3 +458,7 @@ class FakeKubelet:
                 res.pop(key, None)
             for per in self.containers.values():
                 per.pop(key, None)
+
+
+def _bits(mask: int) -> List[int]:
+    return [i for i in range(mask.bit_length()) if mask >> i & 1]

@@ -51,6 +51,7 @@ from ..k8s.objects import annotations as obj_annotations
 from ..k8s.objects import meta, pod_device_steps, pod_gpu_request, pod_is_terminal, pod_key, pod_phase
 from ..placement import NoFeasiblePlacement, PlacementPolicy
 from ..placement.core import select_with
+from ..placement.numa_align import TopologyManager, tm_labels
 from ..topology.cpus import recommended_cpuset
 from ..topology.identity import ENV_BDFS, ENV_FRACTION, ENV_GROUP, ENV_SLICES
 from ..topology.model import Topology
@@ -145,7 +146,8 @@ class PluginConfig:
                  cdi_dir: str = "/var/run/cdi", cdi_kind: str = "amd.com/gpu", nic_env: bool = True,
                  share_cu_mask: bool = True, probe_mark_s: float = 300.0, probe_settle_s: float = 2.0,
                  probe_yield_s: float = 20.0, share_guard: str = "off", guard_dir: str = "/var/lib/gtk-vgpu",
-                 guard_lib: Optional[str] = None, admission_settle_s: float = 5.0):
+                 guard_lib: Optional[str] = None, admission_settle_s: float = 5.0,
+                 topology_manager: Optional[TopologyManager] = None):
         self.resource_name = resource_name
         self.socket_dir = socket_dir
         self.socket_name = socket_name
@@ -208,6 +210,9 @@ class PluginConfig:
         # the kubelet allocates a pod container by container, back to back: a Pending pod is reconciled
         # only once no Allocate has come for this long (its calls may still be under way)
         self.admission_settle_s = admission_settle_s
+        # the kubelet's Topology Manager, published as node labels so the extender picks the devices the
+        # kubelet will offer (placement/numa_align.py)
+        self.topology_manager = topology_manager or TopologyManager()
 
     @property
     def socket_path(self) -> str:
@@ -533,6 +538,7 @@ class DevicePluginServer:
             c.label_partition: t.gpus[0].partition if t.gpus else "",
             c.label_gfx: t.gpus[0].gfx if t.gpus else "",
             c.label_slices: str(max((int((t.physical == p).sum()) for p in set(t.physical.tolist())), default=1)),
+            **tm_labels(self.cfg.topology_manager, c.prefix),
         }
         ann = encode_node_annotations(t, c)
         ann[c.active_slices_key] = str(slices_per_gpu(t))  # the layout a restart must keep while pods hold devices

@@ -46,9 +46,11 @@ from ..k8s.api import ApiError, Conflict, KubeAPI
 from ..k8s.events import record_event
 from ..k8s.objects import annotations as obj_annotations
 from ..k8s.objects import labels as obj_labels
-from ..k8s.objects import meta, pod_gpu_request, pod_key
+from ..k8s.objects import meta, pod_device_steps, pod_gpu_request, pod_key
 from ..placement import NoFeasiblePlacement, PlacementPolicy, place_fraction, select
-from ..placement.core import node_packing_term
+from ..placement.core import node_packing_term, select_with
+from ..placement.numa_align import plan as numa_plan
+from ..placement.numa_align import tm_from_labels
 from ..placement.gaia import gaia_schedule, tree_from_topology
 from ..placement.legacy import design_greedy_select
 from ..topology.cpus import access_costs, recommended_cpuset
@@ -285,6 +287,29 @@ class TopologyExtender:
                         ids, self.cfg.policy)
         return tuple(sorted(int(i) for i in ids)), score_from_objective(j), j
 
+    def _choose_aligned(self, t: Topology, used: Sequence[int], k: int, access, multi: bool,
+                        steps: Sequence[Tuple[int, str]], tm) -> Tuple[Optional[Tuple[int, ...]], str]:
+        """The GROUP on a node whose kubelet runs the Topology Manager: the devices the kubelet will
+        offer container by container (placement/numa_align.py), the placement core choosing wherever
+        the kubelet leaves the choice to the plugin.  (None, why) when the kubelet would reject the pod."""
+        def choose(n: int, offered: Sequence[int], must: Sequence[int]) -> Sequence[int]:
+            if must:
+                return select_with(t, n, offered, must, self.cfg.policy)
+            return select(t, n, used=[i for i in range(t.n) if i not in set(offered)], policy=self.cfg.policy,
+                          rng=self._rng, access=access, nic_aware=multi).ids
+
+        ids, why = numa_plan(t, used, steps, tm, choose)
+        if ids is not None and len(ids) != k:
+            return None, f"the kubelet's topology manager would allocate {len(ids)} devices, the pod requests {k}"
+        return ids, why
+
+    def _rate(self, t: Topology, used: Sequence[int], ids: Sequence[int], access, multi: bool) -> Tuple[float, float]:
+        from ..placement.core import Problem, evaluate, score_from_objective
+
+        j, _ = evaluate(Problem.from_topology(t, used, access, partition_aware=self.cfg.policy.partition_aware, nic_aware=multi),
+                        list(ids), self.cfg.policy)
+        return score_from_objective(j), j
+
     def request_unit(self, pod: Dict[str, Any]) -> Tuple[Optional[str], str]:
         """Which pool the pod draws from: ``"gpu"`` (whole GPUs: the resource name and its aliases) or
         ``"slice"`` (``Contract.slice_resource``, time slices of sliced nodes); (None, reason) when it
@@ -298,11 +323,14 @@ class TopologyExtender:
 
     def _pod_shape(self, pod: Dict[str, Any], k: int) -> Tuple[Optional[tuple], str]:
         """What a placement depends on from the pod: (k, fraction, NUMA preference, GPU model,
-        multi-node, memory, pool unit), parsed once per request; (None, reason) for a malformed one."""
+        multi-node, memory, pool unit, device steps), parsed once per request; (None, reason) for a
+        malformed one.  The steps (``(count, kind)`` per container, kubelet admission order) matter
+        on nodes with a Topology Manager, which aligns each container on its own."""
         try:
             fraction = self.fraction_of(pod)
             mem = self.memory_of(pod)
             unit, why = self.request_unit(pod)
+            steps = tuple((n, kind) for _, n, kind in pod_device_steps(pod, self.resources))
         except ValueError as e:
             return None, str(e)
         if unit is None:
@@ -311,7 +339,7 @@ class TopologyExtender:
             fraction = 0.0  # a memory-sized share of one GPU: the Fragment path, sized by HBM below
         numa = self.numa_preference(pod)
         want = obj_annotations(pod).get(self.cfg.contract.pod_model_key) or obj_labels(pod).get(self.cfg.contract.pod_model_key)
-        return (k, fraction, tuple(numa) if numa else None, want, self.multi_node(pod), mem, unit), ""
+        return (k, fraction, tuple(numa) if numa else None, want, self.multi_node(pod), mem, unit, steps), ""
 
     def multi_node(self, pod: Dict[str, Any]) -> bool:
         """A member of a multi-node job: ``<prefix>/multi-node: "true"``, or it requests an RDMA
@@ -337,7 +365,7 @@ class TopologyExtender:
             shape, why = self._pod_shape(pod, k)
             if shape is None:
                 return None, why
-        _, fraction, numa, want, multi, mem, unit = shape
+        _, fraction, numa, want, multi, mem, unit, steps = shape
         with st.lock:
             now = self.clock()
             if st.probing_until > now:
@@ -350,7 +378,7 @@ class TopologyExtender:
                 if hit is not None and hit[0] <= now <= hit[1]:
                     self.metrics.cache(True)
                     return hit[2], hit[3]
-            d, why = self._eval_state_uncached(st, name, k, fraction, numa, want, now, multi, mem, unit)
+            d, why = self._eval_state_uncached(st, name, k, fraction, numa, want, now, multi, mem, unit, steps)
             if self._cacheable():
                 st.memo[shape] = (now, st.valid_until(now, self.cfg.assume_ttl), d, why)
             return d, why
@@ -370,7 +398,7 @@ class TopologyExtender:
 
     def _eval_state_uncached(self, st: NodeState, name: str, k: int, fraction: Optional[float], numa, want,
                              now: float, multi: bool = False, mem: Optional[int] = None,
-                             unit: str = "gpu") -> Tuple[Optional[Decision], str]:
+                             unit: str = "gpu", steps: Sequence[Tuple[int, str]] = ()) -> Tuple[Optional[Decision], str]:
         t = st.topology
         if t is None:
             return None, "node has no GPU topology annotation"
@@ -413,8 +441,15 @@ class TopologyExtender:
             return None, f"insufficient free devices: need {k}, free {free}"
         access = access_costs(t, numa) if self.cfg.cpu_affinity else None
         t0 = time.perf_counter()
+        tm = tm_from_labels(st.labels, self.cfg.contract.prefix)
         try:
-            ids, score, obj = self._choose_cached(t, used, k, access, fraction, multi)
+            if tm.active and fraction is None and steps:
+                ids, why = self._choose_aligned(t, used, k, access, multi, steps, tm)
+                if ids is None:
+                    return None, why
+                score, obj = self._rate(t, used, ids, access, multi)
+            else:
+                ids, score, obj = self._choose_cached(t, used, k, access, fraction, multi)
         except NoFeasiblePlacement as e:
             return None, str(e)
         us = (time.perf_counter() - t0) * 1e6
@@ -658,7 +693,7 @@ class TopologyExtender:
                 freed_unknown = sum(st.unknown_pods.get(st.unknown_uids.get(u, ""), 0) for u in keep)
                 used = st.used(now, self.cfg.assume_ttl)
                 healthy = {g.index for g in t.gpus if g.healthy}
-                _, fraction, numa, _, multi, mem, unit = shape
+                _, fraction, numa, _, multi, mem, unit, _ = shape
                 if not self._pool_ok(t, unit)[0]:
                     continue
                 if fraction == 0.0 and mem is not None and len({g.physical for g in t.gpus}) == t.n:

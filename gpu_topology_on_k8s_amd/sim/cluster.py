@@ -190,8 +190,14 @@ class SimCluster:
                  policy: PlacementPolicy = PlacementPolicy(), assume_ttl: float = 300.0, use_filter: bool = True,
                  node_labels: Optional[Dict[str, Dict[str, str]]] = None, device_specs: str = "strict",
                  prestart_validate: bool = False, validate_fn=None, reconcile_interval: float = 0.0,
-                 informer: bool = False, share_guard: str = "preload", rbac: bool = False):
+                 informer: bool = False, share_guard: str = "preload", rbac: bool = False,
+                 topology_manager=None, publish_topology_manager: bool = True):
         self.resource = resource
+        # the kubelets' Topology Manager (placement/numa_align.TopologyManager, one for every node or a
+        # dict per node); the plugins publish it unless `publish_topology_manager` is off (an operator
+        # who did not tell the plugin: the extender then places as if the policy were none)
+        self.topology_manager = topology_manager
+        self.publish_topology_manager = publish_topology_manager
         # every component talks to the apiserver as its deploy ServiceAccount (k8s/rbac.py): the
         # plugins with their node-name claim and the own-node admission policy, the extender with its
         # ledger Role; the fake kubelet and the mini scheduler keep full access
@@ -225,7 +231,9 @@ class SimCluster:
         for i, (name, topo) in enumerate(self._topologies.items()):
             self.api.create_node(make_node(name, labels=self._labels.get(name)))
             sockdir = os.path.join(self._root, f"n{i}")
-            kubelet = FakeKubelet(sockdir, node_name=name, api=self.api)
+            tm = self.topology_manager.get(name) if isinstance(self.topology_manager, dict) else self.topology_manager
+            kubelet = FakeKubelet(sockdir, node_name=name, api=self.api, topology_policy=tm.policy if tm else "none",
+                                  topology_scope=tm.scope if tm else "container")
             kubelet.start()
             if self.device_specs == "strict":  # a node with (placeholder) ROCm device nodes
                 dev_root = placeholder_dev_tree(os.path.join(self._root, f"dev{i}"), topo)
@@ -243,7 +251,8 @@ class SimCluster:
                                                            pod_resources_socket=kubelet.pod_resources_socket,
                                                            reconcile_interval=self.reconcile_interval,
                                                            share_guard=self.share_guard,
-                                                           guard_dir=os.path.join(self._root, f"vgpu{i}")),
+                                                           guard_dir=os.path.join(self._root, f"vgpu{i}"),
+                                                           topology_manager=tm if self.publish_topology_manager else None),
                                         api=plugin_api, validate_fn=self.validate_fn)
             plugin.start()
             kubelet.wait_for(res)

@@ -1,0 +1,191 @@
+"""Nodes whose kubelet runs the Topology Manager (placement/numa_align.py).
+
+The kubelet offers each container the free devices of the narrowest, lowest NUMA set that fits, and a
+``restricted`` or ``single-numa-node`` kubelet rejects pods that do not align (``TopologyAffinityError``,
+pod Failed for good).  The extender replays that procedure, so the GROUP it binds is what the kubelet
+allocates, and it never binds a pod the kubelet would reject.  The fake kubelet
+(deviceplugin/kubelet.py) implements the Topology Manager separately, in the kubelet's own structure
+(bitmask hints, ``mergeFilteredHints``, ``filterByAffinity``); these tests hold the two against each
+other."""
+import random
+
+import pytest
+
+from gpu_topology_on_k8s_amd.deviceplugin.__main__ import topology_manager_of
+from gpu_topology_on_k8s_amd.k8s import Contract, PodAssignment
+from gpu_topology_on_k8s_amd.k8s.objects import annotations as obj_annotations
+from gpu_topology_on_k8s_amd.k8s.objects import labels as obj_labels
+from gpu_topology_on_k8s_amd.placement.numa_align import (TopologyManager, best_hint, plan, read_kubelet_config,
+                                                          tm_from_labels)
+from gpu_topology_on_k8s_amd.sim import SimCluster
+from gpu_topology_on_k8s_amd.topology import fixtures as fx
+
+NUMA = {i: 0 if i < 4 else 1 for i in range(8)}  # F7: GPUs 0-3 on NUMA node 0, 4-7 on node 1
+ALL = list(range(8))
+
+
+def _hint(policy, k, used, reusable=()):
+    return best_hint(policy, k, set(ALL) - set(used) - set(reusable), set(reusable), NUMA, ALL)
+
+
+@pytest.mark.parametrize("policy", ["best-effort", "restricted", "single-numa-node"])
+def test_hints_pick_the_lowest_numa_node_that_fits(policy):
+    assert _hint(policy, 2, []) == (frozenset({0}), True, True)
+    assert _hint(policy, 2, [0, 1, 2]) == (frozenset({1}), True, True)
+    assert _hint(policy, 4, [5]) == (frozenset({0}), True, True)
+
+
+def test_a_request_no_numa_node_holds_any_more_is_not_preferred():
+    used = [0, 1, 2, 4, 5, 6]  # one free GPU per NUMA node: a 2-GPU pod could sit on one node of an empty machine
+    assert _hint("best-effort", 2, used) == (frozenset({0, 1}), False, True)
+    assert _hint("restricted", 2, used)[2] is False
+    assert _hint("single-numa-node", 2, used) == (None, False, False)
+
+
+def test_a_request_wider_than_a_numa_node():
+    assert _hint("restricted", 6, []) == (frozenset({0, 1}), True, True)  # minimal width is 2: preferred
+    assert _hint("single-numa-node", 6, [])[2] is False
+
+
+def test_reused_devices_pin_the_hint():
+    # an init container's devices on NUMA node 1 are handed on: only masks holding them qualify
+    assert _hint("best-effort", 2, [], reusable=[4]) == (frozenset({1}), True, True)
+    assert _hint("single-numa-node", 2, [5, 6, 7], reusable=[4, 0])[2] is False
+
+
+def _first(n, offered, must):
+    out = sorted(must)
+    return out + [d for d in sorted(offered) if d not in out][: n - len(out)]
+
+
+def test_plan_follows_the_device_managers_two_branches():
+    t = fx.f7_mi355x()
+    tm = TopologyManager("best-effort", "container")
+    # needed < aligned: the plugin chooses among NUMA node 0's free devices only
+    assert plan(t, [0], [(2, "app")], tm, lambda n, off, must: sorted(off, reverse=True)[:n]) == ((2, 3), "")
+    # needed == aligned: every aligned device, no choice left
+    assert plan(t, [0], [(3, "app")], tm, _first) == ((1, 2, 3), "")
+    # needed > aligned (6 devices, minimal width 2): everything is aligned
+    assert plan(t, [], [(6, "app")], tm, _first) == ((0, 1, 2, 3, 4, 5), "")
+    # per container: the second container finds NUMA node 0 too full and goes to node 1
+    assert plan(t, [0], [(2, "app"), (2, "app")], tm, _first) == ((1, 2, 4, 5), "")
+    # scope pod: one hint for the pod's 4 devices, both containers inside it
+    assert plan(t, [0], [(2, "app"), (2, "app")], TopologyManager("best-effort", "pod"), _first) == ((4, 5, 6, 7), "")
+    ids, why = plan(t, [], [(6, "app")], TopologyManager("single-numa-node", "container"), _first)
+    assert ids is None and "TopologyAffinityError" in why
+
+
+def _shape(rng):
+    """A random pod: one or two app containers, sometimes an init container, 1..8 GPUs in total."""
+    r = rng.random()
+    if r < 0.5:
+        return {"gpus": rng.choice([1, 1, 2, 2, 3, 4, 6, 8])}
+    if r < 0.8:
+        a, b = rng.choice([(1, 1), (1, 2), (2, 2), (1, 3), (2, 4)])
+        return {"gpus": 0, "split": [a, b]}
+    app = rng.choice([1, 2, 3])
+    return {"gpus": 0, "split": [app], "init": [rng.choice([1, 2, app])]}
+
+
+@pytest.mark.parametrize("policy,scope", [("best-effort", "container"), ("restricted", "container"),
+                                          ("single-numa-node", "container"), ("best-effort", "pod"),
+                                          ("single-numa-node", "pod")])
+def test_groups_equal_what_the_kubelet_allocates_under_churn(policy, scope):
+    """Random pods arrive and finish on two MI355X nodes whose kubelets run the Topology Manager; the
+    reconcile pass is off.  Every pod the extender binds is admitted with exactly its GROUP, and no pod
+    is bound that the kubelet rejects."""
+    rng = random.Random(f"{policy}/{scope}")
+    tm = TopologyManager(policy, scope)
+    with SimCluster({"a": fx.f7_mi355x(), "b": fx.f7_mi355x()}, topology_manager=tm) as c:
+        live = []
+        placed = 0
+        for i in range(40):
+            if live and rng.random() < 0.4:
+                c.complete(live.pop(rng.randrange(len(live))))
+            c.submit(f"p{i}", **_shape(rng))
+            (r,) = c.schedule_pending()
+            if r.node is None:
+                assert r.error, r
+                c.delete(f"p{i}")  # infeasible now: a real scheduler would retry it later
+                continue
+            assert not r.error, r  # bound means admitted: the kubelet rejected nothing the extender bound
+            # what the extender decided at bind is what the kubelet allocated (the plugin did not have to
+            # correct the GROUP at Allocate), and the annotation says so
+            assert sorted(r.devices) == sorted(r.allocated), (i, r)
+            pa = PodAssignment.from_annotations(obj_annotations(c.api.get_pod("default", f"p{i}")))
+            assert sorted(pa.group) == sorted(r.allocated) and pa.assigned, (i, pa, r)
+            live.append(f"p{i}")
+            placed += 1
+        assert placed >= 15
+        assert not any(rej for n in c.nodes.values() for rej in n.kubelet.rejected)
+
+
+def test_an_extender_that_ignores_the_policy_loses_pods_the_aware_one_places():
+    """``single-numa-node`` kubelets, two nodes with room for 4 GPUs each, but only node b has them on
+    one NUMA node.  Unaware, the extender binds to node a, where the kubelet rejects the pod for good
+    (Failed, TopologyAffinityError); aware, it filters node a out with the reason and places the pod on b."""
+    tm = TopologyManager("single-numa-node", "container")
+    results = {}
+    for aware in (False, True):
+        with SimCluster({"a": fx.f7_mi355x(), "b": fx.f7_mi355x()}, topology_manager=tm,
+                        publish_topology_manager=aware) as c:
+            # node a: 2 GPUs used on each NUMA node (four 2-GPU pods, two of them done); node b: NUMA node 0 full
+            for node, groups, done in (("a", ([0, 1], [2, 3], [4, 5], [6, 7]), (1, 3)), ("b", ([0, 1], [2, 3]), ())):
+                for j, g in enumerate(groups):
+                    name = f"pre-{node}{j}"
+                    c.submit(name, 2)
+                    uid = c.api.get_pod("default", name)["metadata"]["uid"]
+                    c.api.patch_pod_annotations("default", name, PodAssignment(g, False, 0).to_annotations())
+                    c.api.bind_pod("default", name, uid, node)
+                    c.nodes[node].kubelet.admit(c.api.get_pod("default", name), c.resource)
+                    assert sorted(int(d) for d in c.nodes[node].kubelet.allocated[c.resource][f"default/{name}"]) == g
+                for j in done:
+                    c.complete(f"pre-{node}{j}")
+            c.extender.cache.sync_all()
+            c.submit("x", 4)
+            fr = c.extender.filter(c.api.get_pod("default", "x"), ["a", "b"])
+            (r,) = c.schedule_pending()
+            results[aware] = (r, fr, c.api.get_pod("default", "x"))
+    r, fr, pod = results[True]
+    assert r.node == "b" and not r.error and sorted(r.allocated) == [4, 5, 6, 7]
+    assert "TopologyAffinityError" in fr[1]["a"]
+    r, _, pod = results[False]  # both nodes score 10 on links alone; the tie goes to a, and the pod is lost
+    assert r.node == "a" and "TopologyAffinityError" in r.error and pod["status"]["phase"] == "Failed"
+
+
+def test_the_plugin_publishes_the_policy_from_flags_or_the_kubelet_config(tmp_path):
+    cfgfile = tmp_path / "config.yaml"
+    cfgfile.write_text("apiVersion: kubelet.config.k8s.io/v1beta1\nkind: KubeletConfiguration\n"
+                       "topologyManagerPolicy: single-numa-node\ntopologyManagerScope: pod\n")
+    assert read_kubelet_config(str(cfgfile)) == TopologyManager("single-numa-node", "pod")
+
+    class A:
+        topology_manager_policy = ""
+        topology_manager_scope = ""
+        kubelet_config = str(cfgfile)
+
+    assert topology_manager_of(A) == TopologyManager("single-numa-node", "pod")
+    A.topology_manager_policy = "restricted"
+    assert topology_manager_of(A) == TopologyManager("restricted", "pod")  # a flag beats the file
+    A.kubelet_config = str(tmp_path / "missing.yaml")
+    A.topology_manager_policy = ""
+    assert topology_manager_of(A) == TopologyManager()
+    with SimCluster({"a": fx.f7_mi355x()}, topology_manager=TopologyManager("restricted", "container")) as c:
+        labels = obj_labels(c.api.get_node("a"))
+        assert tm_from_labels(labels, Contract().prefix) == TopologyManager("restricted", "container")
+    assert tm_from_labels({f"{Contract().prefix}/topology-manager-policy": "bogus"}, Contract().prefix) == TopologyManager()
+
+
+def test_the_manifests_hand_the_policy_to_the_plugin():
+    import yaml
+
+    from gpu_topology_on_k8s_amd.config import render_manifests
+
+    def plugin_cmd(**kw):
+        docs = list(yaml.safe_load_all(render_manifests(**kw)))
+        ds = next(d for d in docs if d["kind"] == "DaemonSet" and "device-plugin" in d["metadata"]["name"])
+        return ds["spec"]["template"]["spec"]["containers"][0]["command"]
+
+    assert not any("topology-manager" in a for a in plugin_cmd())
+    cmd = plugin_cmd(topology_manager_policy="single-numa-node", topology_manager_scope="pod")
+    assert "--topology-manager-policy=single-numa-node" in cmd and "--topology-manager-scope=pod" in cmd

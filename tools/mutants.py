@@ -3,7 +3,7 @@
 catch it (a mutation-testing pass; README "Mutation testing of the control plane").
 
     python tools/mutants.py                  # every group
-    python tools/mutants.py --only ledger    # one group (ledger, cache, plugin, informer, rbac, dp, guard,
+    python tools/mutants.py --only ledger    # one group (ledger, cache, plugin, informer, rbac, numa, dp, guard,
                                              # banding, gaia, repartition, extender, contract)
 
 Each mutant replaces one line (or a few) of a source file, runs the group's tests with pytest-xdist,
@@ -45,6 +45,7 @@ REPART = "gpu_topology_on_k8s_amd/deviceplugin/repartition.py"
 ANN = "gpu_topology_on_k8s_amd/k8s/annotations.py"
 INFORMER = "gpu_topology_on_k8s_amd/k8s/informer.py"
 RBAC = "gpu_topology_on_k8s_amd/k8s/rbac.py"
+NUMA_ALIGN = "gpu_topology_on_k8s_amd/placement/numa_align.py"
 
 MUTANTS: List[Mutant] = [
     # allocation ledger (cross-extender bind safety)
@@ -129,6 +130,19 @@ MUTANTS: List[Mutant] = [
     Mutant("rbac", RBAC, "        if self.identity.own_node_only and node != self.node_name:", "        if False:"),
     Mutant("rbac", RBAC, "and (self.namespace is None or self.namespace == namespace))", ")"),
     Mutant("rbac", RBAC, "                out[m.group(1)].own_node_only = True", "                pass"),
+    # placement under the kubelet's Topology Manager
+    Mutant("numa", NUMA_ALIGN, "            if needed < len(aligned):", "            if needed <= len(aligned):", equivalent=True,
+           why="needed == aligned: the plugin, asked over exactly the aligned devices, answers all of them"),
+    Mutant("numa", NUMA_ALIGN, "            in_mask = sum(1 for d in all_devices if numa.get(d, -1) in mask)",
+           "            in_mask = sum(1 for d in available if numa.get(d, -1) in mask)"),
+    Mutant("numa", NUMA_ALIGN, "        elif pref == best[1] and (len(mask), sorted(mask)) < (len(best[0]), sorted(best[0])):",
+           "        elif pref == best[1] and len(mask) < len(best[0]):"),
+    Mutant("numa", NUMA_ALIGN, "        for combo in itertools.combinations(sorted(nodes), width):",
+           "        for combo in itertools.combinations(sorted(nodes, reverse=True), width):"),
+    Mutant("numa", NUMA_ALIGN, "            if any(numa.get(d, -1) >= 0 and numa[d] not in mask for d in reusable):", "            if False:"),
+    Mutant("numa", NUMA_ALIGN, '    admit = policy == "best-effort" or pref', "    admit = True"),
+    Mutant("numa", NUMA_ALIGN, '        if kind == "init":\n            reuse |= got', '        if False:\n            reuse |= got'),
+    Mutant("numa", SCHED, "            if tm.active and fraction is None and steps:", "            if False:"),
     # data-parallel reduction
     Mutant("dp", DP, "        return b.start + self.rank * c, b.start + (self.rank + 1) * c", "        return b.start, b.start + c"),
     Mutant("dp", DP, "                if b.work is None:\n                    self._launch(b)", "                if False:\n                    self._launch(b)"),
@@ -196,6 +210,7 @@ TESTS = {
                "tests/test_multicontainer.py"],
     "informer": ["tests/test_informer.py", "tests/test_cluster_features.py", "tests/test_rbac.py"],
     "rbac": ["tests/test_rbac.py", "tests/test_config_cli.py"],
+    "numa": ["tests/test_topology_manager.py"],
     "dp": ["tests/test_dp_check.py", "tests/test_llama_dp_cpu.py", "tests/test_checkpoint.py"],
     "guard": ["tests/test_vgpu_guard.py"],
     "banding": ["tests/test_probe_banding.py", "tests/test_probe_checks.py"],
