@@ -189,3 +189,19 @@ def test_the_manifests_hand_the_policy_to_the_plugin():
     assert not any("topology-manager" in a for a in plugin_cmd())
     cmd = plugin_cmd(topology_manager_policy="single-numa-node", topology_manager_scope="pod")
     assert "--topology-manager-policy=single-numa-node" in cmd and "--topology-manager-scope=pod" in cmd
+
+
+def test_init_container_devices_are_reused_under_the_topology_manager():
+    """An init container's devices go on to the app container (the kubelet's devicesToReuse), also
+    when its hint is computed: the pod holds max(init, app) devices, never their sum."""
+    t = fx.f7_mi355x()
+    tm = TopologyManager("single-numa-node", "container")
+    assert plan(t, [], [(2, "init"), (2, "app")], tm, _first) == ((0, 1), "")
+    assert plan(t, [], [(1, "init"), (3, "app")], tm, _first) == ((0, 1, 2), "")
+    assert plan(t, [0, 1], [(1, "sidecar"), (2, "app")], tm, _first) == ((2, 4, 5), "")  # a sidecar keeps its GPU
+    with SimCluster({"a": fx.f7_mi355x()}, topology_manager=tm) as c:
+        c.submit("warm", 0, split=[3], init=[2])
+        c.submit("side", 0, split=[2], sidecars=[1])
+        for r in c.schedule_pending():
+            assert r.node == "a" and not r.error and sorted(r.devices) == sorted(r.allocated), r
+        assert [sorted(r.allocated) for r in c.history] == [[0, 1, 2], [3, 4, 5]]

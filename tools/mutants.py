@@ -136,9 +136,11 @@ MUTANTS: List[Mutant] = [
     Mutant("numa", NUMA_ALIGN, "            in_mask = sum(1 for d in all_devices if numa.get(d, -1) in mask)",
            "            in_mask = sum(1 for d in available if numa.get(d, -1) in mask)"),
     Mutant("numa", NUMA_ALIGN, "        elif pref == best[1] and (len(mask), sorted(mask)) < (len(best[0]), sorted(best[0])):",
-           "        elif pref == best[1] and len(mask) < len(best[0]):"),
+           "        elif pref == best[1] and len(mask) < len(best[0]):", equivalent=True,
+           why="masks are iterated lowest ids first, so the first of equally narrow hints is already the lowest"),
     Mutant("numa", NUMA_ALIGN, "        for combo in itertools.combinations(sorted(nodes), width):",
-           "        for combo in itertools.combinations(sorted(nodes, reverse=True), width):"),
+           "        for combo in itertools.combinations(sorted(nodes, reverse=True), width):", equivalent=True,
+           why="the merge compares equally narrow hints by their lowest ids, whatever the iteration order"),
     Mutant("numa", NUMA_ALIGN, "            if any(numa.get(d, -1) >= 0 and numa[d] not in mask for d in reusable):", "            if False:"),
     Mutant("numa", NUMA_ALIGN, '    admit = policy == "best-effort" or pref', "    admit = True"),
     Mutant("numa", NUMA_ALIGN, '        if kind == "init":\n            reuse |= got', '        if False:\n            reuse |= got'),
