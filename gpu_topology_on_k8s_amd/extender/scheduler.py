@@ -693,9 +693,10 @@ class TopologyExtender:
                 freed_unknown = sum(st.unknown_pods.get(st.unknown_uids.get(u, ""), 0) for u in keep)
                 used = st.used(now, self.cfg.assume_ttl)
                 healthy = {g.index for g in t.gpus if g.healthy}
-                _, fraction, numa, _, multi, mem, unit, _ = shape
+                _, fraction, numa, _, multi, mem, unit, steps = shape
                 if not self._pool_ok(t, unit)[0]:
                     continue
+                tm = tm_from_labels(st.labels, self.cfg.contract.prefix)
                 if fraction == 0.0 and mem is not None and len({g.physical for g in t.gpus}) == t.n:
                     fraction = None  # memory-sized request on whole GPUs: an ordinary placement
                 access = access_costs(t, numa) if self.cfg.cpu_affinity else None
@@ -712,7 +713,14 @@ class TopologyExtender:
                         if free < k:
                             continue
                         try:
-                            _, _, obj = self._choose_cached(t, still, k, access, fraction, multi)
+                            if tm.active and fraction is None and steps:
+                                # the kubelet's Topology Manager must admit the pod on what the victims free
+                                ids, _ = self._choose_aligned(t, still, k, access, multi, steps, tm)
+                                if ids is None:
+                                    continue
+                                _, obj = self._rate(t, still, ids, access, multi)
+                            else:
+                                _, _, obj = self._choose_cached(t, still, k, access, fraction, multi)
                         except NoFeasiblePlacement:
                             continue
                         if best is None or obj < best[0] - 1e-12:

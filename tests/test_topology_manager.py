@@ -205,3 +205,30 @@ def test_init_container_devices_are_reused_under_the_topology_manager():
         for r in c.schedule_pending():
             assert r.node == "a" and not r.error and sorted(r.devices) == sorted(r.allocated), r
         assert [sorted(r.allocated) for r in c.history] == [[0, 1, 2], [3, 4, 5]]
+
+
+def test_preemption_counts_only_victims_whose_devices_the_kubelet_would_align():
+    """Victims that free one GPU on each NUMA node make room for a 2-GPU pod by count, but a
+    ``single-numa-node`` kubelet would reject it there: /preempt drops the node."""
+    import time
+
+    from gpu_topology_on_k8s_amd.extender import ExtenderConfig, TopologyExtender
+    from gpu_topology_on_k8s_amd.k8s import FakeAPIServer
+    from gpu_topology_on_k8s_amd.k8s.annotations import encode_node_annotations
+    from gpu_topology_on_k8s_amd.k8s.objects import make_node, make_pod
+    from gpu_topology_on_k8s_amd.placement.numa_align import tm_labels
+
+    c = Contract()
+    for tm, expect in ((TopologyManager(), True), (TopologyManager("single-numa-node", "container"), False)):
+        api = FakeAPIServer()
+        api.create_node(make_node("n1", labels=tm_labels(tm, c.prefix), annotations=encode_node_annotations(fx.f7_mi355x(), c),
+                                  capacity={c.resource_name: "8"}))
+        uids = {}
+        for name, ids in (("a", [0]), ("b", [4]), ("c", [1, 2, 3]), ("d", [5, 6, 7])):
+            p = api.create_pod(make_pod(name, gpus=len(ids), node="n1",
+                                        annotations=PodAssignment(ids, True, int(time.time())).to_annotations()))
+            uids[name] = p["metadata"]["uid"]
+        ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+        pod = api.create_pod(make_pod("want2", gpus=2))
+        got = ext.preempt(pod, {"n1": ([uids["a"], uids["b"]], 0)})
+        assert ("n1" in got) is expect, (tm, got)
