@@ -87,16 +87,20 @@ def _shape(rng):
     return {"gpus": 0, "split": [app], "init": [rng.choice([1, 2, app])]}
 
 
-@pytest.mark.parametrize("policy,scope", [("best-effort", "container"), ("restricted", "container"),
-                                          ("single-numa-node", "container"), ("best-effort", "pod"),
-                                          ("single-numa-node", "pod")])
-def test_groups_equal_what_the_kubelet_allocates_under_churn(policy, scope):
-    """Random pods arrive and finish on two MI355X nodes whose kubelets run the Topology Manager; the
-    reconcile pass is off.  Every pod the extender binds is admitted with exactly its GROUP, and no pod
-    is bound that the kubelet rejects."""
-    rng = random.Random(f"{policy}/{scope}")
+@pytest.mark.parametrize("policy,scope,split", [("best-effort", "container", 2), ("restricted", "container", 2),
+                                                ("single-numa-node", "container", 2), ("best-effort", "pod", 2),
+                                                ("single-numa-node", "pod", 2), ("best-effort", "container", 4),
+                                                ("restricted", "pod", 4)])
+def test_groups_equal_what_the_kubelet_allocates_under_churn(policy, scope, split):
+    """Random pods arrive and finish on two MI355X nodes whose kubelets run the Topology Manager (hosts
+    with 2 NUMA nodes, or 4 as an EPYC in NPS2/NPS4 mode); the reconcile pass is off.  Every pod the
+    extender binds is admitted with exactly its GROUP, and no pod is bound that the kubelet rejects."""
+    from gpu_topology_on_k8s_amd.topology.model import Topology
+
+    rng = random.Random(f"{policy}/{scope}/{split}")
     tm = TopologyManager(policy, scope)
-    with SimCluster({"a": fx.f7_mi355x(), "b": fx.f7_mi355x()}, topology_manager=tm) as c:
+    node = lambda: Topology.full_mesh(n=8, numa_split=split, node_name="mi355x")  # noqa: E731
+    with SimCluster({"a": node(), "b": node()}, topology_manager=tm) as c:
         live = []
         placed = 0
         for i in range(40):
@@ -232,3 +236,30 @@ def test_preemption_counts_only_victims_whose_devices_the_kubelet_would_align():
         pod = api.create_pod(make_pod("want2", gpus=2))
         got = ext.preempt(pod, {"n1": ([uids["a"], uids["b"]], 0)})
         assert ("n1" in got) is expect, (tm, got)
+
+
+@pytest.mark.parametrize("split", [2, 4, 8])
+def test_the_extenders_hints_equal_the_fake_kubelets(split):
+    """Differential check of the two implementations (placement/numa_align.best_hint against the fake
+    kubelet's bitmask hints and merge) over random states, on hosts with 2, 4 and 8 NUMA nodes (an EPYC
+    host in NPS4 mode puts one MI355X on each): same admission, same hinted NUMA nodes."""
+    from gpu_topology_on_k8s_amd.deviceplugin.kubelet import FakeKubelet, _bits, _Plugin
+    from gpu_topology_on_k8s_amd.topology.model import Topology
+
+    t = Topology.full_mesh(n=8, numa_split=split)
+    numa = {g.index: int(g.numa) for g in t.gpus}
+    assert len(set(numa.values())) == split
+    rng = random.Random(split)
+    for policy in ("best-effort", "restricted", "single-numa-node"):
+        kl = FakeKubelet("/nonexistent", topology_policy=policy)
+        p = _Plugin(resource="amd.com/gpu", endpoint="", channel=None, options=None,
+                    devices={str(i): "Healthy" for i in range(8)}, numa={str(i): (numa[i],) for i in range(8)})
+        for _ in range(300):
+            used = set(rng.sample(range(8), rng.randint(0, 7)))
+            reusable = set(rng.sample(sorted(used), rng.randint(0, min(2, len(used)))))  # the pod's own init devices
+            avail = set(range(8)) - used
+            req = rng.randint(1, 8)
+            mask, admit = kl._merge(p, kl._generate_hints(p, {str(d) for d in avail}, {str(d) for d in reusable}, req))
+            want, _, ok = best_hint(policy, req, avail, reusable, numa, list(range(8)))
+            assert ok == admit, (policy, used, reusable, req)
+            assert (None if mask is None else frozenset(_bits(mask))) == want, (policy, used, reusable, req)
