@@ -124,25 +124,31 @@ def exp2_xcp_cluster(reps: int, node: str = "xcp"):
             "sched_ms_mean": statistics.mean(sched), "paper_sched_s": PAPER_SCHED_S["exp2"]}
 
 
-def scale_prioritize(n_nodes: int, pods: int = 20, k: int = 4):
+def scale_prioritize(n_nodes: int, pods: int = 20, k: int = 4, tm_policy: str = "none", split=None):
     """kube-scheduler's sort fan-out on a large cluster: one pending k-GPU pod x every node, repeated
     for `pods` same-size pods (no binds in between), extender called in process (no HTTP) so the
-    numbers are the extender's own cost.  Decision cache off vs on (the LRU of scheduler.py)."""
+    numbers are the extender's own cost.  Decision cache off vs on (the LRU of scheduler.py).
+    ``tm_policy``: every node's kubelet runs the Topology Manager with that policy (published by its
+    plugin), so the extender replays the kubelet's NUMA alignment (placement/numa_align.py);
+    ``split`` = (a, b): the pods have two containers of a and b GPUs."""
     import time
 
     from gpu_topology_on_k8s_amd.extender import ExtenderConfig, TopologyExtender
     from gpu_topology_on_k8s_amd.k8s import Contract, FakeAPIServer
     from gpu_topology_on_k8s_amd.k8s.annotations import encode_node_annotations
     from gpu_topology_on_k8s_amd.k8s.objects import make_node, make_pod
+    from gpu_topology_on_k8s_amd.placement.numa_align import TopologyManager, tm_labels
 
     api = FakeAPIServer()
     c = Contract()
     names = [f"node{i}" for i in range(n_nodes)]
+    extra = tm_labels(TopologyManager(tm_policy, "container"), c.prefix) if tm_policy != "none" else {}
     for i, n in enumerate(names):
         t = fx.f7_mi355x(76.5, 0.03, i)
-        api.create_node(make_node(n, labels={c.label_model: "MI355X"}, annotations=encode_node_annotations(t, c),
+        api.create_node(make_node(n, labels={c.label_model: "MI355X", **extra}, annotations=encode_node_annotations(t, c),
                                   capacity={c.resource_name: "8"}))
-    out = {"experiment": f"scale-prioritize-{n_nodes}-nodes", "nodes": n_nodes, "request_gpus": k, "pods": pods}
+    out = {"experiment": f"scale-prioritize-{n_nodes}-nodes" + (f"-tm-{tm_policy}" if tm_policy != "none" else ""),
+           "nodes": n_nodes, "request_gpus": k, "pods": pods, "topology_manager": tm_policy, "containers": list(split or [k])}
     from gpu_topology_on_k8s_amd.k8s.informer import Informer
 
     for mode, cache in (("cache_off", 0), ("cache_on", 4096), ("informer", 4096)):
@@ -158,7 +164,7 @@ def scale_prioritize(n_nodes: int, pods: int = 20, k: int = 4):
         ms = []
         lists_before = api.calls.get("list_pods", 0) + api.calls.get("list_nodes", 0)
         for i in range(pods):
-            pod = api.create_pod(make_pod(f"p{mode}-{i}", gpus=k))
+            pod = api.create_pod(make_pod(f"p{mode}-{i}", gpus=0 if split else k, split=list(split) if split else None))
             t0 = time.perf_counter()
             ext.prioritize(pod, names)
             ms.append((time.perf_counter() - t0) * 1e3)
@@ -204,9 +210,12 @@ def main() -> int:
     ap.add_argument("--reps", type=int, default=500)
     ap.add_argument("--out", default="")
     ap.add_argument("--scale-nodes", type=int, default=1024, help="cluster size of the sort fan-out experiment (0: skip)")
+    ap.add_argument("--scale-topology-manager", default="",
+                    help="also run the fan-out with every kubelet's Topology Manager under this policy (single and 2+2 container pods)")
+    ap.add_argument("--skip-tables", action="store_true", help="only the scale experiments")
     a = ap.parse_args()
     random.seed(0)
-    results = [
+    results = [] if a.skip_tables else [
         run_exp("exp1-1gpu", 1, (), a.reps),
         run_exp("exp1-2gpu", 2, (), a.reps),
         exp2_fragments(a.reps),
@@ -217,9 +226,13 @@ def main() -> int:
         run_exp("mi355x-exact-4gpu", 4, (), max(50, a.reps // 5), policy="exact", topo_fn=lambda: fx.f7_mi355x(76.5, 0.03, 1)),
         run_exp("mi355x-exact-1gpu-after-2", 1, (0, 1), max(50, a.reps // 5), policy="exact", topo_fn=lambda: fx.f7_mi355x(76.5, 0.03, 1)),
     ]
-    results.append(cpx_select())
+    if not a.skip_tables:
+        results.append(cpx_select())
     if a.scale_nodes:
         results.append(scale_prioritize(a.scale_nodes))
+        if a.scale_topology_manager:
+            results.append(scale_prioritize(a.scale_nodes, tm_policy=a.scale_topology_manager))
+            results.append(scale_prioritize(a.scale_nodes, tm_policy=a.scale_topology_manager, split=(2, 2)))
     for r in results:
         print(json.dumps(r))
     if a.out:
