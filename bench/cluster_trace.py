@@ -35,7 +35,6 @@ from __future__ import annotations
 import argparse
 import heapq
 import json
-import math
 import os
 import random
 import statistics
@@ -46,7 +45,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from gpu_topology_on_k8s_amd.placement import NoFeasiblePlacement, PlacementPolicy, select  # noqa: E402
+from gpu_topology_on_k8s_amd.placement import PlacementPolicy, select  # noqa: E402
 from gpu_topology_on_k8s_amd.placement.core import Problem, evaluate, node_packing_term  # noqa: E402
 from gpu_topology_on_k8s_amd.placement.gaia import gaia_schedule, tree_from_topology  # noqa: E402
 from gpu_topology_on_k8s_amd.placement.legacy import design_greedy_select  # noqa: E402

@@ -37,7 +37,6 @@ import statistics
 import sys
 from typing import Dict, List, Optional, Tuple
 
-import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 

@@ -23,7 +23,7 @@ import threading
 import time
 from concurrent import futures
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import grpc
 

@@ -3,7 +3,6 @@ start-up probe reuse on busy nodes, compact node annotations, CPU affinity, the 
 path, normalised node scores, LIST+WATCH informer, plugin metrics/events, Gaia Fragment via XCPs,
 and the cross-node bind deadlock."""
 import itertools
-import math
 import threading
 import time
 
@@ -22,7 +21,7 @@ from gpu_topology_on_k8s_amd.k8s.api import RestKubeAPI
 from gpu_topology_on_k8s_amd.k8s.informer import Informer
 from gpu_topology_on_k8s_amd.k8s.objects import make_node, make_pod
 from gpu_topology_on_k8s_amd.parallel.allreduce import choose_subset
-from gpu_topology_on_k8s_amd.placement import PlacementPolicy, Problem, evaluate, place_fraction, select, worst
+from gpu_topology_on_k8s_amd.placement import Problem, evaluate, place_fraction, select, worst
 from gpu_topology_on_k8s_amd.sim import SimCluster
 from gpu_topology_on_k8s_amd.topology import fixtures as fx
 from gpu_topology_on_k8s_amd.topology.cpus import access_costs, device_core_slices, format_cpulist, parse_cpulist, recommended_cpuset

@@ -11,7 +11,6 @@ from gpu_topology_on_k8s_amd.k8s.annotations import encode_node_annotations
 from gpu_topology_on_k8s_amd.k8s.objects import make_node, make_pod
 from gpu_topology_on_k8s_amd.placement.defrag import plan_defrag
 from gpu_topology_on_k8s_amd.topology import fixtures as fx
-from gpu_topology_on_k8s_amd.topology.model import Topology
 from gpu_topology_on_k8s_amd.topology.shares import time_slice
 
 C = Contract()

@@ -8,7 +8,7 @@ import random
 
 import pytest
 
-from gpu_topology_on_k8s_amd.placement import CostTree, fragment, gaia_schedule, link, singular, tree_from_topology
+from gpu_topology_on_k8s_amd.placement import fragment, gaia_schedule, link, singular, tree_from_topology
 from gpu_topology_on_k8s_amd.topology import fixtures as fx
 
 REPS = 500

@@ -2,7 +2,6 @@
 ``design.md:234`` usage tracking, SURVEY §3.2 hot loop): paginated watch-cache LISTs, server-side
 filtering of terminal pods, objects trimmed to what the cache reads, watches resumed from the last
 resourceVersion after a transient error (relist only on 410 Gone), exponential back-off with jitter."""
-import threading
 import time
 
 import pytest

@@ -1,7 +1,6 @@
 """Cluster-in-a-process integration: BASELINE configs 1-4 through the full 7-step flow, restart
 recovery and fault injection (SURVEY.md §4 "Integration", §5.3)."""
 import numpy as np
-import pytest
 
 from gpu_topology_on_k8s_amd.sim import SimCluster
 from gpu_topology_on_k8s_amd.topology import fixtures as fx
