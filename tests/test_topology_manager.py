@@ -263,3 +263,30 @@ def test_the_extenders_hints_equal_the_fake_kubelets(split):
             want, _, ok = best_hint(policy, req, avail, reusable, numa, list(range(8)))
             assert ok == admit, (policy, used, reusable, req)
             assert (None if mask is None else frozenset(_bits(mask))) == want, (policy, used, reusable, req)
+
+
+@pytest.mark.gpu
+def test_a_real_node_under_single_numa_node():
+    """The MI355X of the box, discovered through amdsmi with the NUMA node its host reports (not
+    necessarily 0), advertised as 4 time slices, its kubelet under ``single-numa-node``: the devices'
+    TopologyInfo carries that NUMA node, every pod is admitted with exactly the GROUP the extender
+    bound, and the node labels name the policy."""
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
+    from gpu_topology_on_k8s_amd.topology.shares import time_slice
+
+    t = discover("auto")
+    t.node_name = "gpu-node"
+    v = time_slice(t, 4)
+    numa = {int(g.numa) for g in v.gpus}
+    tm = TopologyManager("single-numa-node", "container")
+    with SimCluster({"gpu-node": v}, topology_manager=tm, reconcile_interval=0.0) as c:
+        kub = c.nodes["gpu-node"].kubelet
+        res = c.nodes["gpu-node"].resource
+        assert {n for ns in kub.plugins[res].numa.values() for n in ns} == numa
+        assert tm_from_labels(obj_labels(c.api.get_node("gpu-node")), Contract().prefix) == tm
+        c.submit("two", 0, split=[1, 1], slices=True)
+        c.submit("pair", 2, slices=True)
+        for r in c.schedule_pending():
+            assert not r.error and sorted(r.devices) == sorted(r.allocated), r
+        assert not kub.rejected
+    print({"numa_nodes": sorted(numa), "devices": v.n})
