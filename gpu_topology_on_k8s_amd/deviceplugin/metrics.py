@@ -53,6 +53,11 @@ class PluginMetrics:
             "gtk_plugin_container_claims_total",
             "per-container Allocate calls of multi-container pods and mismatches, by how they matched a pod "
             "(partial, final, resized, unannotated)", ["how"], registry=r)
+        self.group_overridden = Counter(
+            "gtk_plugin_group_overridden_total",
+            "Allocate calls whose devices were not the pod's GROUP, recorded as the kubelet chose them: the extender "
+            "bound devices the kubelet did not offer (a Topology Manager policy the plugin was not told about, CPU or "
+            "memory manager hints)", registry=r)
         self.annotation_bytes = Gauge("gtk_plugin_topology_annotation_bytes", "encoded size of the published node annotations",
                                       registry=r)
 

@@ -1168,6 +1168,7 @@ class DevicePluginServer:
                     group = (group - set(spare[:len(extra)])) | claimed
                     log.warning("kubelet allocated %s but pod %s was assumed %s; recording what the kubelet chose",
                                 ids, md.get("name"), pa.group)
+                    self.metrics.group_overridden.inc()
                 complete = claimed >= group
                 if sorted(group) != sorted(set(pa.group)) or (complete and not pa.assigned):
                     ann = {ANN_GROUP: format_group(sorted(group)), ANN_ASSIGNED: "true" if complete else "false"}

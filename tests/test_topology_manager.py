@@ -122,6 +122,31 @@ def test_groups_equal_what_the_kubelet_allocates_under_churn(policy, scope, spli
             placed += 1
         assert placed >= 15
         assert not any(rej for n in c.nodes.values() for rej in n.kubelet.rejected)
+        assert sum(n.plugin.metrics.group_overridden._value.get() for n in c.nodes.values()) == 0
+
+
+def test_an_untold_plugin_shows_the_kubelet_overriding_groups():
+    """The operator did not tell the plugin the kubelet's ``best-effort`` policy: the extender binds
+    devices the kubelet does not offer, the plugin records what the kubelet chose, and
+    ``gtk_plugin_group_overridden_total`` says so (docs/OPERATIONS.md)."""
+    rng = random.Random("best-effort/container/2")
+    tm = TopologyManager("best-effort", "container")
+    with SimCluster({"a": fx.f7_mi355x(), "b": fx.f7_mi355x()}, topology_manager=tm, publish_topology_manager=False) as c:
+        live, differ = [], 0
+        for i in range(40):
+            if live and rng.random() < 0.4:
+                c.complete(live.pop(rng.randrange(len(live))))
+            c.submit(f"p{i}", **_shape(rng))
+            (r,) = c.schedule_pending()
+            if r.node is None or r.error:
+                c.delete(f"p{i}")
+                continue
+            differ += sorted(r.devices) != sorted(r.allocated)
+            live.append(f"p{i}")
+        overridden = sum(n.plugin.metrics.group_overridden._value.get() for n in c.nodes.values())
+        text = "".join(n.plugin.metrics.exposition().decode() for n in c.nodes.values())
+    assert differ > 0 and overridden >= differ
+    assert "gtk_plugin_group_overridden_total" in text
 
 
 def test_an_extender_that_ignores_the_policy_loses_pods_the_aware_one_places():
