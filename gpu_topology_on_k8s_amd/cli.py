@@ -504,6 +504,8 @@ def main(argv=None) -> int:
     p.add_argument("--gpu", action="store_true", help="also initialise HIP: device count, gfx950, MFMA warm-up")
     p.add_argument("--dev-root", default="/dev")
     p.add_argument("--plugin-dir", default="/var/lib/kubelet/device-plugins")
+    p.add_argument("--kubelet-config", default="/var/lib/kubelet/config.yaml",
+                   help="KubeletConfiguration whose Topology Manager policy the device plugin must be given")
     p.set_defaults(fn=lambda a: __import__("gpu_topology_on_k8s_amd.doctor", fromlist=["main"]).main(a))
     p = sub.add_parser("partition", help="GPU compute / memory partition modes: show, or set (root; the node must be idle)")
     p.add_argument("action", choices=["show", "set"])

@@ -11,7 +11,10 @@ DaemonSet's init step, an operator, or a pod's entry point can act on it.  Node 
 * ``cpu-affinity``              every GPU's local cores intersect this process's allowed CPUs (Gaia B6);
 * ``device-plugin-dir``         the kubelet's device-plugin socket directory is writable;
 * ``partition``                 each package's compute / memory partition mode and the modes it offers
-                                (amdsmi, read-only; what ``--partition-control`` may switch to).
+                                (amdsmi, read-only; what ``--partition-control`` may switch to);
+* ``topology-manager``          the kubelet's Topology Manager policy and scope (its KubeletConfiguration),
+                                which the device plugin must be given so the extender binds what the
+                                kubelet will allocate (placement/numa_align.py).
 
 Pod checks (when ``GTK_GPU_GROUP`` is set, i.e. inside a container Allocate configured):
 
@@ -118,6 +121,26 @@ def check_partition(backend: str) -> Check:
               packages=info)
 
 
+def check_topology_manager(kubelet_config: str = "/var/lib/kubelet/config.yaml") -> Check:
+    """The kubelet's ``topologyManagerPolicy`` / ``topologyManagerScope`` and the device plugin flags
+    that must carry them (skip when the file is not readable here)."""
+    from .placement.numa_align import read_kubelet_config
+
+    if not kubelet_config or not os.path.exists(kubelet_config):
+        return _c("topology-manager", "skip", f"{kubelet_config} not readable here: pass the kubelet's policy to the device "
+                                              "plugin with --topology-manager-policy / --topology-manager-scope")
+    try:
+        tm = read_kubelet_config(kubelet_config)
+    except Exception as e:  # noqa: BLE001 - the check's result
+        return _c("topology-manager", "fail", f"{kubelet_config}: {e}")
+    if not tm.active:
+        return _c("topology-manager", "ok", "policy none: the kubelet takes the plugin's preferred devices as they are",
+                  policy=tm.policy, scope=tm.scope)
+    return _c("topology-manager", "ok", f"policy {tm.policy}, scope {tm.scope}: run the device plugin with "
+                                        f"--topology-manager-policy={tm.policy} --topology-manager-scope={tm.scope} "
+                                        "(or --kubelet-config on this file)", policy=tm.policy, scope=tm.scope)
+
+
 def check_plugin_dir(path: str) -> Check:
     if not os.path.isdir(path):
         return _c("device-plugin-dir", "skip", f"{path} absent (not a kubelet node, or not mounted)")
@@ -190,7 +213,8 @@ def check_gpu() -> List[Check]:
 
 def run_checks(backend: str = "auto", fake_n: Optional[int] = None, gpu: bool = False, dev_root: str = "/dev",
                plugin_dir: str = "/var/lib/kubelet/device-plugins", env: Optional[Dict[str, str]] = None,
-               visible_bdfs: Optional[List[str]] = None, allowed=None) -> List[Check]:
+               visible_bdfs: Optional[List[str]] = None, allowed=None,
+               kubelet_config: str = "/var/lib/kubelet/config.yaml") -> List[Check]:
     env = dict(os.environ) if env is None else env
     checks: List[Check] = []
     if backend != "fake":
@@ -203,6 +227,7 @@ def run_checks(backend: str = "auto", fake_n: Optional[int] = None, gpu: bool = 
     checks += check_native()
     checks.append(check_ipc(env))
     checks.append(check_plugin_dir(plugin_dir))
+    checks.append(check_topology_manager(kubelet_config))
     checks += check_pod(env, visible_bdfs=visible_bdfs if visible_bdfs is not None else ([] if backend == "fake" else None),
                         allowed=allowed)
     if gpu:
@@ -235,7 +260,8 @@ def check_guard(env: Dict[str, str]) -> List[Check]:
 
 
 def main(a) -> int:
-    checks = run_checks(a.discovery, a.fake_gpus, a.gpu, a.dev_root, a.plugin_dir)
+    checks = run_checks(a.discovery, a.fake_gpus, a.gpu, a.dev_root, a.plugin_dir,
+                        kubelet_config=getattr(a, "kubelet_config", "/var/lib/kubelet/config.yaml"))
     for c in checks:
         print(json.dumps(c))
     worst = "fail" if any(c["status"] == "fail" for c in checks) else ("warn" if any(c["status"] == "warn" for c in checks) else "ok")

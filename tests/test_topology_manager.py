@@ -315,3 +315,15 @@ def test_a_real_node_under_single_numa_node():
             assert not r.error and sorted(r.devices) == sorted(r.allocated), r
         assert not kub.rejected
     print({"numa_nodes": sorted(numa), "devices": v.n})
+
+
+def test_doctor_names_the_plugin_flags_the_kubelet_needs(tmp_path):
+    from gpu_topology_on_k8s_amd.doctor import check_topology_manager
+
+    assert check_topology_manager(str(tmp_path / "none.yaml"))["status"] == "skip"
+    f = tmp_path / "config.yaml"
+    f.write_text("kind: KubeletConfiguration\ntopologyManagerPolicy: restricted\n")
+    c = check_topology_manager(str(f))
+    assert c["status"] == "ok" and c["policy"] == "restricted" and "--topology-manager-policy=restricted" in c["detail"]
+    f.write_text("kind: KubeletConfiguration\ntopologyManagerPolicy: bogus\n")
+    assert check_topology_manager(str(f))["status"] == "fail"
