@@ -16,7 +16,7 @@ import signal
 import sys
 import threading
 import time
-from typing import Tuple
+from typing import Optional, Tuple
 
 from ..k8s.annotations import Contract
 from ..placement import PlacementPolicy
@@ -39,13 +39,14 @@ def make_api(apiserver: str, token: str, ca_file: str = "", insecure: bool = Fal
     return None
 
 
-def node_time_slices(api, node_name: str, contract: Contract, default: int) -> int:
+def node_time_slices(api, node_name: str, contract: Contract, default: int, node: Optional[dict] = None) -> int:
     """Time slices for this node: the operator's node label ``<prefix>/time-slices`` when set (one
-    DaemonSet serves a cluster where only some nodes are shared), else ``--time-slices``."""
-    if api is None or not node_name:
+    DaemonSet serves a cluster where only some nodes are shared), else ``--time-slices``.  ``node``:
+    the Node object already read (no second GET)."""
+    if node is None and (api is None or not node_name):
         return default
     try:
-        labels = (api.get_node(node_name).get("metadata") or {}).get("labels") or {}
+        labels = ((node if node is not None else api.get_node(node_name)).get("metadata") or {}).get("labels") or {}
     except Exception as e:  # noqa: BLE001 - the flag still applies
         logging.getLogger("gtk.deviceplugin").warning("reading node %s labels failed: %s", node_name, e)
         return default
@@ -277,12 +278,15 @@ def main(argv=None) -> int:
     done = threading.Event()
     for sig in (signal.SIGINT, signal.SIGTERM):  # installed before serving: a stop never races start-up
         signal.signal(sig, lambda *_: done.set())
+    plugin.poll_node()  # a cordoned GPU is never advertised Healthy, not even until the first label check
     plugin.start()
     ticks = 0
     while not done.wait(1.0):
         ticks += 1
-        if ticks % max(1, int(a.label_check_interval)) == 0 and api is not None:  # the operator relabelled the node's time slices
-            label = node_time_slices(api, a.node_name, contract, a.time_slices)
+        if ticks % max(1, int(a.label_check_interval)) == 0 and api is not None:
+            # one GET of the node: the operator's GPU cordon (<prefix>/cordoned-gpus) and time-slice label
+            node = plugin.poll_node()
+            label = node_time_slices(api, a.node_name, contract, a.time_slices, node=node) if node is not None else a.time_slices
             want = applicable_slices(label)
             if want != label and not unapplied_warned:
                 log.warning("node label asks for %d time slices per GPU; a partitioned node cannot be sliced, "

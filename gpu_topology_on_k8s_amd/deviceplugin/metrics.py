@@ -58,6 +58,8 @@ class PluginMetrics:
             "Allocate calls whose devices were not the pod's GROUP, recorded as the kubelet chose them: the extender "
             "bound devices the kubelet did not offer (a Topology Manager policy the plugin was not told about, CPU or "
             "memory manager hints)", registry=r)
+        self.cordoned = Gauge("gtk_plugin_cordoned_devices", "devices the operator took out of service (<prefix>/cordoned-gpus)",
+                              registry=r)
         self.annotation_bytes = Gauge("gtk_plugin_topology_annotation_bytes", "encoded size of the published node annotations",
                                       registry=r)
 

@@ -38,7 +38,7 @@ import os
 import threading
 import time
 from concurrent import futures
-from typing import Callable, Dict, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Set, Tuple
 
 import grpc
 import numpy as np
@@ -332,9 +332,9 @@ class DevicePluginServer:
         """Fault injection / health monitor entry: re-advertise through every ListAndWatch stream."""
         self.set_health_many({index: healthy})
 
-    def set_health_many(self, states: Dict[int, bool]) -> None:
+    def set_health_many(self, states: Dict[int, bool], reason: str = "GPUUnhealthy", why: str = "") -> None:
         """Apply several health changes at once: one ListAndWatch update, one node publish and one
-        Event per newly unhealthy physical GPU (the time slices of a GPU flip together)."""
+        Event (``reason``) per newly unhealthy physical GPU (the time slices of a GPU flip together)."""
         changed: Dict[int, bool] = {}
         with self._cond:
             for index, healthy in states.items():
@@ -355,10 +355,88 @@ class DevicePluginServer:
             if self.api is not None and self.cfg.node_name and not healthy and g.physical not in reported:
                 reported.add(g.physical)
                 devs = sorted(i for i in changed if self.topology.gpus[i].physical == g.physical)
-                record_event(self.api, {"kind": "Node", "metadata": {"name": self.cfg.node_name}}, "GPUUnhealthy",
-                             f"device{'s' if len(devs) > 1 else ''} {format_group(devs)} ({g.bdf or 'no bdf'}) Unhealthy",
+                record_event(self.api, {"kind": "Node", "metadata": {"name": self.cfg.node_name}}, reason,
+                             f"device{'s' if len(devs) > 1 else ''} {format_group(devs)} ({g.bdf or 'no bdf'}) Unhealthy"
+                             + (f": {why}" if why else ""),
                              "Warning", component="gpu-topology-device-plugin", host=self.cfg.node_name)
         self._publish_node()
+
+    # ------------------------------------------------------------------ operator cordon
+    CORDON_HOLD = "cordoned by the operator"
+
+    def cordoned_from(self, value: str) -> Tuple[Set[int], List[str]]:
+        """Devices ``<prefix>/cordoned-gpus`` names -> (indices, tokens that name no device here).  An
+        index or a PCI address (``0000:75:00.0``, or without the domain) stands for its whole physical
+        GPU: every partition or time slice of it."""
+        t = self.topology
+        by_bdf: Dict[str, int] = {}
+        for g in t.gpus:
+            if g.bdf:
+                b = g.bdf.lower()
+                by_bdf.setdefault(b, g.index)
+                by_bdf.setdefault(b.split(":", 1)[1] if b.count(":") == 2 else b, g.index)
+        out: Set[int] = set()
+        unknown: List[str] = []
+        for tok in (x.strip() for x in str(value or "").split(",")):
+            if not tok:
+                continue
+            i: Optional[int] = None
+            if tok.isdigit() and int(tok) < t.n:
+                i = int(tok)
+            elif ":" in tok:
+                i = by_bdf.get(tok.lower())
+            if i is None:
+                unknown.append(tok)
+                continue
+            out |= {g.index for g in t.gpus if g.physical == t.gpus[i].physical}
+        return out, unknown
+
+    def apply_cordon(self, value: Optional[str]) -> Tuple[Set[int], Set[int]]:
+        """Hold the devices the annotation names Unhealthy, release the ones it no longer names ->
+        (newly cordoned, released).  A released device is Healthy again unless another hold (a GPU
+        reset) or the next health pass says otherwise."""
+        want, unknown = self.cordoned_from(value or "")
+        with self._cond:
+            have = {i for i, why in self._holds.items() if why == self.CORDON_HOLD}
+            add, drop = want - have, have - want
+            for i in add:
+                self._holds.setdefault(i, self.CORDON_HOLD)
+            for i in drop:
+                self._holds.pop(i, None)
+        node = {"kind": "Node", "metadata": {"name": self.cfg.node_name}}
+        if unknown and unknown != getattr(self, "_cordon_unknown", None) and self.api is not None and self.cfg.node_name:
+            record_event(self.api, node, "GPUCordonUnknown", f"{self.cfg.contract.cordon_key} names no device here: "
+                         f"{','.join(unknown)}", "Warning", component="gpu-topology-device-plugin", host=self.cfg.node_name)
+        self._cordon_unknown = unknown
+        if add:
+            self.set_health_many({i: False for i in add}, reason="GPUCordoned", why=self.CORDON_HOLD)
+        if drop:
+            states = {i: True for i in drop if i not in self._holds}
+            if self.health_fn is not None and states:
+                try:
+                    verdict = self.health_fn(self.topology)
+                    states = {i: bool(verdict.get(i, True)) for i in states}
+                except Exception as e:  # noqa: BLE001 - the next health pass decides
+                    log.warning("health check after an uncordon failed: %s", e)
+            self.set_health_many(states)
+            if self.api is not None and self.cfg.node_name:
+                record_event(self.api, node, "GPUUncordoned", f"devices {format_group(sorted(drop))} back in service",
+                             "Normal", component="gpu-topology-device-plugin", host=self.cfg.node_name)
+        self.metrics.cordoned.set(len(want))
+        return add, drop
+
+    def poll_node(self) -> Optional[dict]:
+        """One GET of this plugin's own Node (the daemon's periodic label check): applies the operator's
+        cordon and returns the object (None without an apiserver or on error)."""
+        if self.api is None or not self.cfg.node_name:
+            return None
+        try:
+            node = self.api.get_node(self.cfg.node_name)
+        except Exception as e:  # noqa: BLE001 - the next poll retries
+            log.warning("reading node %s failed: %s", self.cfg.node_name, e)
+            return None
+        self.apply_cordon(obj_annotations(node).get(self.cfg.contract.cordon_key))
+        return node
 
     def update_topology(self, topo: Topology) -> None:
         """New probe results / partition change: re-publish and re-advertise."""

@@ -83,6 +83,14 @@ class Contract:
         return f"{self.prefix}/gpu-ledger"
 
     @property
+    def cordon_key(self) -> str:
+        """Node annotation set by the operator: GPUs to take out of service without draining the node
+        (an RMA, a flaky HBM stack), as device indices or PCI addresses, comma-separated.  Each names
+        its whole physical GPU.  The device plugin advertises them Unhealthy (the kubelet stops counting
+        them, the extender stops choosing them); pods already on them keep running."""
+        return f"{self.prefix}/cordoned-gpus"
+
+    @property
     def numa_key(self) -> str:
         """Pod annotation: NUMA node(s) of the assigned devices (Gaia B6)."""
         return f"{self.prefix}/numa-nodes"

@@ -1,0 +1,116 @@
+"""Taking one GPU out of service without draining its node (``<prefix>/cordoned-gpus``, an operator's
+node annotation; docs/OPERATIONS.md).  The device plugin holds the named GPUs Unhealthy: the kubelet's
+allocatable shrinks, the extender never chooses them, pods already on them keep running, and removing
+the annotation puts them back."""
+import pytest
+
+from gpu_topology_on_k8s_amd.k8s import Contract
+from gpu_topology_on_k8s_amd.k8s.objects import annotations as obj_annotations
+from gpu_topology_on_k8s_amd.sim import SimCluster
+from gpu_topology_on_k8s_amd.topology import fixtures as fx
+from gpu_topology_on_k8s_amd.topology.shares import time_slice
+
+C = Contract()
+
+
+def _wait(pred, timeout=5.0):
+    import time
+
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        if pred():
+            return True
+        time.sleep(0.02)
+    return False
+
+
+def _cordon(c, node, value):
+    c.api.patch_node(node, annotations={C.cordon_key: value})
+    return c.nodes[node].plugin.poll_node()
+
+
+def test_a_cordoned_gpu_is_never_chosen_and_its_running_pod_stays():
+    t = fx.f7_mi355x()
+    t.gpus[5].bdf = "0000:75:00.0"
+    with SimCluster({"n": t}) as c:
+        c.submit("on-two", 2)
+        (r,) = c.schedule_pending()
+        held = set(r.allocated)
+        kub, res = c.nodes["n"].kubelet, c.resource
+        victim = min(held)
+        _cordon(c, "n", f"{victim},75:00.0")  # an index and a PCI address without its domain
+        assert _wait(lambda: kub.plugins[res].devices[str(victim)] != "Healthy")
+        assert _wait(lambda: c.api.get_node("n")["status"]["allocatable"][res] == "6")
+        assert set(kub.allocated[res]["default/on-two"]) == {str(i) for i in held}  # still running
+        assert c.nodes["n"].plugin.metrics.cordoned._value.get() == 2
+        reasons = [e.get("reason") for e in c.api.events]
+        assert "GPUCordoned" in reasons
+        c.extender.cache.sync_all()
+        c.submit("big", 4)
+        (r2,) = c.schedule_pending()
+        assert r2.node == "n" and not ({victim, 5} & set(r2.allocated)), r2
+        c.submit("rest", 2)
+        (r3,) = c.schedule_pending()
+        assert r3.node is None  # 8 - 2 held - 4 - 2 cordoned: nothing left
+        # back in service
+        _cordon(c, "n", "")
+        assert _wait(lambda: kub.plugins[res].devices[str(victim)] == "Healthy")
+        assert "GPUUncordoned" in [e.get("reason") for e in c.api.events]
+        c.extender.cache.sync_all()
+        c.delete("rest")
+        c.submit("rest2", 1)
+        (r4,) = c.schedule_pending()
+        assert r4.node == "n" and r4.allocated == (5,), r4
+
+
+def test_a_cordon_names_the_whole_physical_gpu_and_reports_unknown_tokens():
+    t = time_slice(fx.f7_mi355x(), 2)  # 16 slices, two per GPU
+    with SimCluster({"n": t}) as c:
+        plug = c.nodes["n"].plugin
+        got, unknown = plug.cordoned_from("3, 0000:ff:00.0, 99, gpu7")
+        assert got == {2, 3} and unknown == ["0000:ff:00.0", "99", "gpu7"]
+        add, drop = plug.apply_cordon("3,99")
+        assert add == {2, 3} and not drop
+        assert "GPUCordonUnknown" in [e.get("reason") for e in c.api.events]
+        assert not plug._health[2] and not plug._health[3]
+        # a reset hold outlives an uncordon of the same device
+        plug._holds[2] = "GPU reset in progress"
+        add, drop = plug.apply_cordon("")
+        assert drop == {3} and plug._health[3] and not plug._health[2]
+
+
+def test_the_daemon_applies_a_cordon_before_it_serves_and_follows_it():
+    """The plugin daemon (its own process, against the apiserver over HTTP): a GPU cordoned before it
+    starts is never advertised Healthy, and an uncordon is picked up by the periodic node check."""
+    import os
+    import shutil
+    import tempfile
+
+    from gpu_topology_on_k8s_amd.deviceplugin.kubelet import FakeKubelet
+    from gpu_topology_on_k8s_amd.k8s import FakeAPIServer, serve_http
+    from gpu_topology_on_k8s_amd.k8s.objects import make_node
+    from test_daemons import _spawn, _stop
+
+    api = FakeAPIServer()
+    api.create_node(make_node("worker-1", annotations={C.cordon_key: "2"}))
+    srv, url = serve_http(api)
+    sockdir = tempfile.mkdtemp(prefix="gtkc", dir="/tmp")
+    kubelet = FakeKubelet(sockdir, node_name="worker-1", api=api)
+    kubelet.start()
+    devroot = os.path.join(sockdir, "dev")
+    os.makedirs(devroot)
+    p = _spawn(["gpu_topology_on_k8s_amd.deviceplugin", "--discovery", "fake", "--fake-gpus", "4", "--apiserver", url,
+                "--node-name", "worker-1", "--socket-dir", sockdir, "--log-level", "WARNING", "--dev-root", devroot,
+                "--label-check-interval", "1"])
+    try:
+        plugin = kubelet.wait_for("amd.com/gpu", timeout=60)
+        first = dict(plugin.devices)  # the first ListAndWatch answer
+        assert first["2"] == "Unhealthy" and first["0"] == "Healthy", first
+        api.patch_node("worker-1", annotations={C.cordon_key: ""})
+        assert _wait(lambda: plugin.devices.get("2") == "Healthy", 15)
+    finally:
+        rc = _stop(p)
+        kubelet.stop()
+        srv.shutdown()
+        shutil.rmtree(sockdir, ignore_errors=True)
+    assert rc == 0

@@ -144,7 +144,10 @@ MUTANTS: List[Mutant] = [
     Mutant("numa", NUMA_ALIGN, "            if any(numa.get(d, -1) >= 0 and numa[d] not in mask for d in reusable):", "            if False:"),
     Mutant("numa", NUMA_ALIGN, '    admit = policy == "best-effort" or pref', "    admit = True"),
     Mutant("numa", NUMA_ALIGN, '        if kind == "init":\n            reuse |= got', '        if False:\n            reuse |= got'),
-    Mutant("numa", SCHED, "            if tm.active and fraction is None and steps:", "            if False:"),
+    Mutant("numa", SCHED, "            if tm.active and fraction is None and steps:\n                ids, why = self._choose_aligned(",
+           "            if False:\n                ids, why = self._choose_aligned("),
+    Mutant("numa", SCHED, "                            if tm.active and fraction is None and steps:",
+           "                            if False:"),
     # data-parallel reduction
     Mutant("dp", DP, "        return b.start + self.rank * c, b.start + (self.rank + 1) * c", "        return b.start, b.start + c"),
     Mutant("dp", DP, "                if b.work is None:\n                    self._launch(b)", "                if False:\n                    self._launch(b)"),
