@@ -3,7 +3,7 @@
 catch it (a mutation-testing pass; README "Mutation testing of the control plane").
 
     python tools/mutants.py                  # every group
-    python tools/mutants.py --only ledger    # one group (ledger, cache, plugin, informer, rbac, numa, dp, guard,
+    python tools/mutants.py --only ledger    # one group (ledger, cache, plugin, informer, rbac, numa, cordon, dp, guard,
                                              # banding, gaia, repartition, extender, contract)
 
 Each mutant replaces one line (or a few) of a source file, runs the group's tests with pytest-xdist,
@@ -46,6 +46,7 @@ ANN = "gpu_topology_on_k8s_amd/k8s/annotations.py"
 INFORMER = "gpu_topology_on_k8s_amd/k8s/informer.py"
 RBAC = "gpu_topology_on_k8s_amd/k8s/rbac.py"
 NUMA_ALIGN = "gpu_topology_on_k8s_amd/placement/numa_align.py"
+PLUGIN_MAIN = "gpu_topology_on_k8s_amd/deviceplugin/__main__.py"
 
 MUTANTS: List[Mutant] = [
     # allocation ledger (cross-extender bind safety)
@@ -148,6 +149,11 @@ MUTANTS: List[Mutant] = [
            "            if False:\n                ids, why = self._choose_aligned("),
     Mutant("numa", SCHED, "                            if tm.active and fraction is None and steps:",
            "                            if False:"),
+    # operator GPU cordon
+    Mutant("cordon", PLUGIN, "                self._holds.setdefault(i, self.CORDON_HOLD)", "                pass"),
+    Mutant("cordon", PLUGIN, "            out |= {g.index for g in t.gpus if g.physical == t.gpus[i].physical}", "            out.add(i)"),
+    Mutant("cordon", PLUGIN, "            states = {i: True for i in drop if i not in self._holds}", "            states = {i: True for i in drop}"),
+    Mutant("cordon", PLUGIN_MAIN, "    plugin.poll_node()  # a cordoned GPU is never advertised Healthy", "    pass  # a cordoned GPU is never advertised Healthy"),
     # data-parallel reduction
     Mutant("dp", DP, "        return b.start + self.rank * c, b.start + (self.rank + 1) * c", "        return b.start, b.start + c"),
     Mutant("dp", DP, "                if b.work is None:\n                    self._launch(b)", "                if False:\n                    self._launch(b)"),
@@ -216,6 +222,7 @@ TESTS = {
     "informer": ["tests/test_informer.py", "tests/test_cluster_features.py", "tests/test_rbac.py"],
     "rbac": ["tests/test_rbac.py", "tests/test_config_cli.py"],
     "numa": ["tests/test_topology_manager.py"],
+    "cordon": ["tests/test_cordon.py"],
     "dp": ["tests/test_dp_check.py", "tests/test_llama_dp_cpu.py", "tests/test_checkpoint.py"],
     "guard": ["tests/test_vgpu_guard.py"],
     "banding": ["tests/test_probe_banding.py", "tests/test_probe_checks.py"],
