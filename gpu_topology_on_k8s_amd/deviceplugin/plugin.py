@@ -411,7 +411,7 @@ class DevicePluginServer:
         if add:
             self.set_health_many({i: False for i in add}, reason="GPUCordoned", why=self.CORDON_HOLD)
         if drop:
-            states = {i: True for i in drop if i not in self._holds}
+            states = {i: True for i in drop}  # a device holds one reason at a time: a reset hold is not a cordon
             if self.health_fn is not None and states:
                 try:
                     verdict = self.health_fn(self.topology)

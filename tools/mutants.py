@@ -152,7 +152,6 @@ MUTANTS: List[Mutant] = [
     # operator GPU cordon
     Mutant("cordon", PLUGIN, "                self._holds.setdefault(i, self.CORDON_HOLD)", "                pass"),
     Mutant("cordon", PLUGIN, "            out |= {g.index for g in t.gpus if g.physical == t.gpus[i].physical}", "            out.add(i)"),
-    Mutant("cordon", PLUGIN, "            states = {i: True for i in drop if i not in self._holds}", "            states = {i: True for i in drop}"),
     Mutant("cordon", PLUGIN_MAIN, "    plugin.poll_node()  # a cordoned GPU is never advertised Healthy", "    pass  # a cordoned GPU is never advertised Healthy"),
     # data-parallel reduction
     Mutant("dp", DP, "        return b.start + self.rank * c, b.start + (self.rank + 1) * c", "        return b.start, b.start + c"),
