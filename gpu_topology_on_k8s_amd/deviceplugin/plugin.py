@@ -1493,15 +1493,17 @@ class DevicePluginServer:
         if kind == "GPU_PRE_RESET":
             log.warning("device %d (%s): GPU reset starting: %s", index, bdf, message)
             for i in same:
-                self._holds[i] = "GPU reset in progress"
+                if self._holds.get(i) != self.CORDON_HOLD:  # a cordoned GPU stays cordoned through a reset
+                    self._holds[i] = "GPU reset in progress"
             self.set_health_many({i: False for i in same})
             reason, note = "GPUReset", f"device {index} ({bdf}) is resetting; held Unhealthy"
         elif kind == "GPU_POST_RESET":
             log.warning("device %d (%s): GPU reset finished: %s", index, bdf, message)
             for i in same:
-                self._holds.pop(i, None)
+                if self._holds.get(i) != self.CORDON_HOLD:
+                    self._holds.pop(i, None)
             if self.health_fn is None:
-                self.set_health_many({i: True for i in same})
+                self.set_health_many({i: True for i in same if i not in self._holds})
             self._reprobe_now.set()
             reason, note = "GPUResetDone", f"device {index} ({bdf}) finished a reset; links re-measured when idle"
         elif kind == "VMFAULT":

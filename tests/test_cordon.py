@@ -114,3 +114,18 @@ def test_the_daemon_applies_a_cordon_before_it_serves_and_follows_it():
         srv.shutdown()
         shutil.rmtree(sockdir, ignore_errors=True)
     assert rc == 0
+
+
+def test_a_cordoned_gpu_stays_out_of_service_through_a_reset():
+    with SimCluster({"n": fx.f7_mi355x()}) as c:
+        plug = c.nodes["n"].plugin
+        plug.apply_cordon("3")
+        plug.gpu_event(3, "GPU_PRE_RESET")
+        plug.gpu_event(3, "GPU_POST_RESET")
+        assert plug._health[3] is False and plug._holds[3] == plug.CORDON_HOLD
+        plug.gpu_event(4, "GPU_PRE_RESET")  # an uncordoned GPU comes back after its reset
+        assert plug._health[4] is False
+        plug.gpu_event(4, "GPU_POST_RESET")
+        assert plug._health[4] is True
+        plug.apply_cordon("")
+        assert plug._health[3] is True
