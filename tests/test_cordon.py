@@ -129,3 +129,30 @@ def test_a_cordoned_gpu_stays_out_of_service_through_a_reset():
         assert plug._health[4] is True
         plug.apply_cordon("")
         assert plug._health[3] is True
+
+
+def test_any_annotation_text_parses_without_raising():
+    """The annotation is free text an operator types: whatever it holds, the plugin names only devices
+    it has, whole physical GPUs, and reports the rest."""
+    from hypothesis import given, settings
+    from hypothesis import strategies as st
+
+    from gpu_topology_on_k8s_amd.deviceplugin.plugin import DevicePluginServer
+
+    t = time_slice(fx.f7_mi355x(), 2)
+    for i, g in enumerate(t.gpus):
+        g.bdf = f"0000:{0x10 + g.physical:02x}:00.0"
+    plug = DevicePluginServer(t)
+    token = st.one_of(st.integers(-5, 40).map(str), st.sampled_from([g.bdf for g in t.gpus] + ["14:00.0", "0000:FF:00.0"]),
+                      st.text(max_size=8))
+
+    @settings(max_examples=300, deadline=None)
+    @given(st.lists(token, max_size=6).map(",".join))
+    def check(value):
+        got, unknown = plug.cordoned_from(value)
+        assert got <= set(range(t.n))
+        for i in got:  # whole physical GPUs
+            assert {g.index for g in t.gpus if g.physical == t.gpus[i].physical} <= got
+        assert all(isinstance(u, str) and u for u in unknown)
+
+    check()
