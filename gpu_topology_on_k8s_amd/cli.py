@@ -243,6 +243,7 @@ def cmd_status(a) -> int:
     from .extender import ExtenderConfig, TopologyExtender
     from .extender.metrics import node_fragmentation
     from .k8s.annotations import Contract
+    from .placement.numa_align import tm_from_labels
     api = make_api(a.apiserver, a.token, a.ca_file, a.insecure_skip_tls_verify)
     if api is None:
         print("gtk status: no apiserver (--apiserver URL, or run in a cluster)", file=sys.stderr)
@@ -268,6 +269,10 @@ def cmd_status(a) -> int:
                                          for p in sorted(set(t.physical.tolist()))}
         row["partition"] = f"{t.gpus[0].partition}/{t.gpus[0].memory_partition}" if t.gpus else ""
         row["probing"] = bool(getattr(st, "probing_until", 0.0) > now)  # re-probe / repartition: the extender skips it
+        row["unhealthy"] = [g.index for g in t.gpus if not g.healthy]
+        tm = tm_from_labels(st.labels, ext.cfg.contract.prefix)
+        if tm.active:  # the kubelet aligns devices to NUMA nodes: the scores below already account for it
+            row["topology_manager"] = f"{tm.policy}/{tm.scope}"
         try:  # the operator's partition request and a refusal the plugin recorded
             md = api.get_node(st.name).get("metadata") or {}
             c = ext.cfg.contract
@@ -277,6 +282,9 @@ def cmd_status(a) -> int:
             failed = (md.get("annotations") or {}).get(c.partition_failed_key)
             if failed:
                 row["partition_change_failed"] = failed
+            cordon = (md.get("annotations") or {}).get(c.cordon_key)
+            if cordon:
+                row["cordoned"] = cordon  # the operator's out-of-service GPUs (the plugin holds them Unhealthy)
         except Exception:  # noqa: BLE001 - the node vanished meanwhile: the row stands without it
             pass
         # a sliced node is scored for slice requests (its own pool), every other node for whole devices
@@ -291,11 +299,14 @@ def cmd_status(a) -> int:
     if a.output == "json":
         print(json.dumps(rows))
         return 0
-    head = f"{'NODE':<20}{'DEV':>5}{'USED':>6}{'FREE':>6}{'FRAG':>7}  " + "  ".join(f"k={k:<4}" for k in sizes)
+    head = f"{'NODE':<20}{'DEV':>5}{'USED':>6}{'FREE':>6}{'DOWN':>6}{'FRAG':>7}  " + "  ".join(f"k={k:<4}" for k in sizes) + "  NOTES"
     print(head)
     for r in rows:
         cells = "  ".join(f"{('-' if r['best_score'][str(k)] is None else format(r['best_score'][str(k)], '.2f')):<6}" for k in sizes)
-        print(f"{r['node']:<20}{r['devices']:>5}{r['used']:>6}{r['free']:>6}{r['fragmentation']:>7.3f}  {cells}")
+        notes = ", ".join(x for x in (f"cordoned {r['cordoned']}" if r.get("cordoned") else "",
+                                      f"topology-manager {r['topology_manager']}" if r.get("topology_manager") else "",
+                                      "probing" if r.get("probing") else "") if x)
+        print(f"{r['node']:<20}{r['devices']:>5}{r['used']:>6}{r['free']:>6}{len(r['unhealthy']):>6}{r['fragmentation']:>7.3f}  {cells}  {notes}")
     return 0
 
 

@@ -109,8 +109,9 @@ def test_gtk_status_reports_usage_and_scores():
     api = FakeAPIServer()
     for n in ("n0", "n1"):
         api.create_node(make_node(n, annotations=encode_node_annotations(fx.f7_mi355x(), C), capacity={C.resource_name: "8"}))
-    api.patch_node("n1", labels={C.partition_request_label: "CPX"},
-                   annotations={C.partition_failed_key: "CPX/-: compute partition CPX: 0000:05:00.0: permission denied"})
+    api.patch_node("n1", labels={C.partition_request_label: "CPX", f"{C.prefix}/topology-manager-policy": "single-numa-node"},
+                   annotations={C.partition_failed_key: "CPX/-: compute partition CPX: 0000:05:00.0: permission denied",
+                                C.cordon_key: "7"})
     api.create_pod(make_pod("a", gpus=2, node="n0", annotations=PodAssignment([0, 4], True, 1).to_annotations()))
     srv, url = serve_http(api)
     try:
@@ -123,11 +124,16 @@ def test_gtk_status_reports_usage_and_scores():
     assert p.returncode == 0, p.stderr
     rows = {r["node"]: r for r in json.loads(p.stdout)}
     assert rows["n0"]["used"] == 2 and rows["n0"]["free"] == 6 and rows["n1"]["free"] == 8
-    assert rows["n0"]["best_score"]["8"] is None and rows["n1"]["best_score"]["8"] is not None
+    assert rows["n0"]["best_score"]["8"] is None
     assert q.returncode == 0 and q.stdout.splitlines()[0].startswith("NODE") and "n1" in q.stdout
     assert "gpu_share_used" not in rows["n0"]
     assert rows["n0"]["partition"] == "SPX/NPS1" and not rows["n0"]["probing"] and "partition_request" not in rows["n0"]
     assert rows["n1"]["partition_request"] == "CPX/-" and "permission" in rows["n1"]["partition_change_failed"]
+    # the operator's cordon and the kubelet's Topology Manager: a single-numa-node kubelet can take at most
+    # one NUMA node's 4 GPUs, so an 8-GPU pod has no score there
+    assert rows["n1"]["cordoned"] == "7" and rows["n1"]["topology_manager"] == "single-numa-node/container"
+    assert rows["n1"]["best_score"]["8"] is None and rows["n1"]["best_score"]["4"] is not None and rows["n0"]["unhealthy"] == []
+    assert "cordoned 7" in q.stdout and "topology-manager single-numa-node/container" in q.stdout
 
 
 def test_gtk_status_shares_on_a_sliced_node():
