@@ -327,3 +327,26 @@ def test_doctor_names_the_plugin_flags_the_kubelet_needs(tmp_path):
     assert c["status"] == "ok" and c["policy"] == "restricted" and "--topology-manager-policy=restricted" in c["detail"]
     f.write_text("kind: KubeletConfiguration\ntopologyManagerPolicy: bogus\n")
     assert check_topology_manager(str(f))["status"] == "fail"
+
+
+@pytest.mark.parametrize("used,reusable,size,want", [
+    ((), (), 1, [({0}, True), ({1}, True), ({0, 1}, False)]),
+    ((), (), 2, [({0}, True), ({1}, True), ({0, 1}, False)]),
+    ((), (), 3, [({0, 1}, True)]),
+    (("2", "3"), (), 2, [({0, 1}, False)]),  # one free GPU per NUMA node: no narrow hint left, none preferred
+    (("1", "3"), (), 2, [({0}, True), ({0, 1}, False)]),  # node 1 full: node 0 still holds the pair
+    (("3",), ("3",), 2, [({1}, True), ({0, 1}, False)]),  # a reused GPU on node 1 pins every mask to contain 1
+    (("0", "1", "2", "3"), (), 1, []),  # nothing free: no hint at all
+])
+def test_the_fake_kubelets_hint_lists(used, reusable, size, want):
+    """The device manager's hints for 4 GPUs, two per NUMA node (``generateDeviceTopologyHints``): every
+    NUMA set whose free plus reused devices hold the request, preferred when as narrow as the narrowest
+    set whose devices, free or not, could."""
+    from gpu_topology_on_k8s_amd.deviceplugin.kubelet import FakeKubelet, _bits, _Plugin
+
+    kl = FakeKubelet("/nonexistent", topology_policy="best-effort")
+    p = _Plugin(resource="amd.com/gpu", endpoint="", channel=None, options=None, devices={str(i): "Healthy" for i in range(4)},
+                numa={"0": (0,), "1": (1,), "2": (0,), "3": (1,)})
+    avail = {str(i) for i in range(4)} - set(used)
+    hints = kl._generate_hints(p, avail - set(reusable), set(reusable), size)
+    assert [(set(_bits(m)), pref) for m, pref in hints] == want
