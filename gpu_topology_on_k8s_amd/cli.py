@@ -327,7 +327,11 @@ def cmd_config(a) -> int:
         else:
             print(out["gpu-topology-kind.yaml"], end="")
         return 0
-    if a.kind == "policy":
+    if a.kind == "alerts":
+        from .config import prometheus_rules
+
+        print(yaml.safe_dump(prometheus_rules(), sort_keys=False), end="")
+    elif a.kind == "policy":
         print(json.dumps(legacy_policy(a.resource_name, with_filter=a.filter), indent=2))
     elif a.kind == "scheduler":
         print(yaml.safe_dump(scheduler_configuration(a.resource_name, with_filter=a.filter, tls_dir=a.tls_dir or None),
@@ -479,7 +483,7 @@ def main(argv=None) -> int:
     p.add_argument("--resource-name", default="amd.com/gpu")
     p.set_defaults(fn=cmd_status)
     p = sub.add_parser("config")
-    p.add_argument("kind", choices=["scheduler", "policy", "manifests", "kind"])
+    p.add_argument("kind", choices=["scheduler", "policy", "manifests", "kind", "alerts"])
     p.add_argument("--out-dir", default="", help="kind: write every file of deploy/kind/ here")
     p.add_argument("--resource-name", default="amd.com/gpu")
     p.add_argument("--filter", action="store_true")

@@ -375,3 +375,64 @@ def render_kind(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, fake_gpus:
         "pod-half-gpu.yaml": yaml.safe_dump(half, sort_keys=False),
         "up.sh": up,
     }
+
+
+def prometheus_rules(namespace: str = NAMESPACE) -> Dict[str, Any]:
+    """A ``PrometheusRule`` (prometheus-operator) with the alerts an operator of this framework needs.
+    Every expression uses only metrics the plugin and the extender export (tests/test_alerts.py
+    checks them against live expositions)."""
+    def alert(name, expr, for_, severity, summary, action):
+        return {"alert": name, "expr": expr, "for": for_, "labels": {"severity": severity},
+                "annotations": {"summary": summary, "description": action}}
+
+    extender = [
+        alert("GPUTopologyExtenderNotSynced", "max(gtk_extender_informer_synced) == 0", "5m", "critical",
+              "The extender's informer has not listed nodes and pods",
+              "Sort and bind answer from an empty or stale view. Check the extender's apiserver access "
+              "(RBAC: nodes/pods list+watch, leases in its namespace) and its log."),
+        alert("GPUTopologyExtenderRelisting", "sum by (kind) (increase(gtk_extender_informer_lists_total[1h])) > 2", "0m",
+              "warning", "The extender relisted {{ $labels.kind }} more than twice in an hour",
+              "Each relist is a full LIST (seconds and hundreds of MB at 100,000 pods). Watches are falling out of the "
+              "apiserver's window (410): check apiserver load and --list-page-size."),
+        alert("GPUTopologyExtenderWatchErrors", "sum(rate(gtk_extender_informer_watch_errors_total[10m])) > 0.05", "15m",
+              "warning", "The extender's watches keep breaking",
+              "Watches are resumed without relisting, but a steady error rate means a flaky apiserver path (LB idle "
+              "timeouts, APF throttling)."),
+        alert("GPUTopologyBindAborts", "sum by (reason) (increase(gtk_extender_bind_aborts_total[15m])) > 0", "0m", "warning",
+              "Binds gave up ({{ $labels.reason }})",
+              "budget: ledger conflicts kept re-deciding a bind (many replicas racing on one node); ledger_grace: a pod "
+              "PATCH took longer than 15 s (apiserver throttling). kube-scheduler retries the pods."),
+        alert("GPUTopologyLedgerConflicts", "sum(rate(gtk_extender_ledger_conflicts_total[5m])) > 1", "15m", "info",
+              "Extender replicas keep colliding on the same nodes",
+              "Conflicts are safe (the loser re-decides) but cost latency; fewer replicas or a scheduler leader "
+              "election reduce them."),
+        alert("GPUTopologyFragmented",
+              "max(gtk_extender_placeable_nodes{k=\"8\"}) == 0 and sum(gtk_extender_node_free_devices) >= 8", "30m", "info",
+              "No node can host an 8-GPU pod although 8 or more GPUs are free",
+              "Free GPUs are scattered. `gtk defrag --size 8` plans the fewest pod moves that free a node."),
+    ]
+    plugin = [
+        alert("GPUTopologyKubeletOverridesGroups", "sum by (pod) (increase(gtk_plugin_group_overridden_total[1h])) > 0", "0m",
+              "warning", "The kubelet allocated other GPUs than the extender bound ({{ $labels.pod }})",
+              "Usually the node's kubelet runs a Topology Manager policy the device plugin was not told about: pass "
+              "--topology-manager-policy / --topology-manager-scope (`gtk doctor` names them)."),
+        alert("GPUTopologyDeviceUnhealthy",
+              "count by (pod) (gtk_plugin_device_healthy == 0) > on (pod) (max by (pod) (gtk_plugin_cordoned_devices))",
+              "10m", "warning", "GPUs are Unhealthy beyond the ones the operator cordoned ({{ $labels.pod }})",
+              "RAS errors, a reset in progress or a lost xGMI link (see the node's GPUUnhealthy Events)."),
+        alert("GPUTopologyAllocateRefused",
+              "sum by (pod, outcome) (increase(gtk_plugin_allocations_total{outcome=~\"invalid|unhealthy|missing|stale_layout\"}[15m])) > 0",
+              "0m", "critical", "Allocate refused pods ({{ $labels.outcome }}) on {{ $labels.pod }}",
+              "The kubelet does not retry a refused Allocate: those pods ended Failed (UnexpectedAdmissionError)."),
+        alert("GPUTopologyPlacementValidationFailed",
+              "sum by (pod) (increase(gtk_plugin_placement_validations_total{result!=\"ok\"}[1h])) > 0", "0m", "warning",
+              "The pre-start RCCL all-reduce failed on a placement ({{ $labels.pod }})",
+              "A container did not start because its GPUs failed the collective (FailedGPUPlacementValidation Events)."),
+        alert("GPUTopologyPluginNotRegistered", "max by (pod) (gtk_plugin_registrations_total) == 0", "10m", "critical",
+              "The device plugin never registered with the kubelet ({{ $labels.pod }})",
+              "The node advertises no GPUs. Check the device-plugins hostPath mount and the kubelet."),
+    ]
+    return {"apiVersion": "monitoring.coreos.com/v1", "kind": "PrometheusRule",
+            "metadata": {"name": "gpu-topology-amd", "namespace": namespace, "labels": {"app.kubernetes.io/part-of": "gpu-topology-amd"}},
+            "spec": {"groups": [{"name": "gpu-topology-extender", "rules": extender},
+                                {"name": "gpu-topology-device-plugin", "rules": plugin}]}}

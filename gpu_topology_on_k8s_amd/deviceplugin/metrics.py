@@ -60,6 +60,12 @@ class PluginMetrics:
             "memory manager hints)", registry=r)
         self.cordoned = Gauge("gtk_plugin_cordoned_devices", "devices the operator took out of service (<prefix>/cordoned-gpus)",
                               registry=r)
+        # every label value an alert watches exists from the start at 0 (deploy/prometheus-rules.yaml):
+        # increase() cannot see the first increment of a series that appears at 1
+        for outcome in ("ok", "invalid", "unhealthy", "missing", "stale_layout", "switch_wait", "probe_yield"):
+            self.allocations.labels(outcome)
+        for result in ("ok", "failed"):
+            self.validations.labels(result)
         self.annotation_bytes = Gauge("gtk_plugin_topology_annotation_bytes", "encoded size of the published node annotations",
                                       registry=r)
 

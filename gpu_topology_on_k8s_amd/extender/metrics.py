@@ -52,6 +52,8 @@ class ExtenderMetrics:
                                    "binds given up because they ran out of time (retry budget, or too slow to finish "
                                    "before their ledger entry could lapse in another extender's view)", ["reason"],
                                    registry=self.registry)
+        for reason in ("budget", "ledger_grace"):  # exported at 0 from the start (the alerts use increase())
+            self.bind_aborts.labels(reason)
         self.probing_skips = Counter("gtk_extender_probing_skips_total",
                                      "node evaluations skipped because the node's device plugin is re-probing its links",
                                      registry=self.registry)
