@@ -785,6 +785,11 @@ class DevicePluginServer:
             for creq in request.container_requests:
                 ids = sorted({int(x) for x in creq.devices_ids})
                 reused = set(ids) if self._gpa_must is None else self._gpa_must & set(ids)
+                if self._gpa_must is None and self.cfg.topology_manager.active and not self._continuing():
+                    # a Topology Manager skips GetPreferredAllocation also for a new pod whose aligned
+                    # devices are exactly its need: with no admission under way this is no reuse, even
+                    # when the GPUs are those a pod that just ended (status not updated yet) freed
+                    reused = set()
                 self._claimed_by = None
                 pods.append(self._claim_pod(ids, reused))
                 self._link(ids, self._claimed_by, reused)
@@ -1166,6 +1171,11 @@ class DevicePluginServer:
                                 float(c.pa.assume_time) if c.pa is not None else 0.0,
                                 meta(c.pod).get("creationTimestamp", ""), meta(c.pod).get("name", "")))
         return out, live
+
+    def _continuing(self) -> bool:
+        """The previous Allocate's admission still has containers to allocate."""
+        rec = self._chain[1] if self._chain is not None else None
+        return rec is not None and self._admissions.get(rec.key) is rec
 
     def _reuse(self, reused: Sequence[int]) -> Optional[_Admission]:
         """The record of the previous Allocate when the devices the kubelet reused (``reused``: what

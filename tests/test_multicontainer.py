@@ -305,3 +305,20 @@ def test_swapped_init_container_pods_after_a_plugin_restart():
         for n in ("a", "b"):
             assert sorted(_ann(c, n).group) == held[n], (n, _ann(c, n), held)
         assert c.reconcile() == 0
+
+
+def test_a_new_pod_on_gpus_freed_before_the_status_update_is_not_the_old_one():
+    """p1 ended on the kubelet (its GPUs freed) while the apiserver still shows it Running; p2, whose
+    GROUP names those GPUs, is admitted next.  The kubelet asked GetPreferredAllocation with nothing to
+    include, so the call reuses nothing: it is p2's, not a continuation of p1 (whose devices they were)."""
+    with SimCluster({"n": fx.f7_mi355x()}) as c:
+        c.api.create_pod(make_pod("p1", gpus=2, node="n", annotations=PodAssignment.assumed([2, 3], 100).to_annotations()))
+        kub = c.nodes["n"].kubelet
+        kub.admit(c.api.get_pod("default", "p1"), c.resource)
+        assert _ann(c, "p1").assigned
+        kub.release(c.api.get_pod("default", "p1"))  # the status update lags
+        c.api.create_pod(make_pod("p2", gpus=2, node="n", annotations=PodAssignment.assumed([2, 3], 200).to_annotations()))
+        kub.admit(c.api.get_pod("default", "p2"), c.resource)
+        assert sorted(int(i) for i in kub.allocated[RES]["default/p2"]) == [2, 3]
+        assert kub.preferred_calls[-1] == ([], 2)
+        assert _ann(c, "p2").assigned and sorted(_ann(c, "p2").group) == [2, 3]

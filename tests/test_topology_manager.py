@@ -350,3 +350,27 @@ def test_the_fake_kubelets_hint_lists(used, reusable, size, want):
     avail = {str(i) for i in range(4)} - set(used)
     hints = kl._generate_hints(p, avail - set(reusable), set(reusable), size)
     assert [(set(_bits(m)), pref) for m, pref in hints] == want
+
+
+def test_an_allocation_without_preferred_call_after_a_finished_pod_is_a_new_pod():
+    """Under a Topology Manager the kubelet skips GetPreferredAllocation when the aligned devices are
+    exactly what a container needs, so "no preferred call" does not mean "reused devices".  Pod p1 has
+    ended on the kubelet (its GPUs freed) while the apiserver still shows it Running; p2 gets p1's GPUs
+    with no preferred call.  The plugin must not take that call for p1 (whose admission finished): p2
+    is claimed, with the devices the kubelet gave it."""
+    tm = TopologyManager("best-effort", "container")
+    with SimCluster({"n": fx.f7_mi355x()}, topology_manager=tm) as c:
+        kub, res = c.nodes["n"].kubelet, c.resource
+        c.submit("p0", 2)
+        c.submit("p1", 2)
+        r0, r1 = c.schedule_pending()
+        assert sorted(r0.allocated) == [0, 1] and sorted(r1.allocated) == [2, 3]
+        n_pref = len(kub.preferred_calls)
+        kub.release(c.api.get_pod("default", "p1"))  # the kubelet freed p1's GPUs; its status update lags
+        c.submit("p2", 2)
+        (r2,) = c.schedule_pending()
+        assert sorted(r2.allocated) == [2, 3] and len(kub.preferred_calls) == n_pref  # aligned == needed: no preferred call
+        pa2 = PodAssignment.from_annotations(obj_annotations(c.api.get_pod("default", "p2")))
+        pa1 = PodAssignment.from_annotations(obj_annotations(c.api.get_pod("default", "p1")))
+        assert pa2.assigned and sorted(pa2.group) == [2, 3], pa2
+        assert sorted(pa1.group) == [2, 3] and pa1.assigned

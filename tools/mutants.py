@@ -102,7 +102,8 @@ MUTANTS: List[Mutant] = [
     Mutant("plugin", PLUGIN, "                reused = set(ids) if self._gpa_must is None else self._gpa_must & set(ids)",
            "                reused = set(ids)"),
     Mutant("plugin", PLUGIN, "                    or (rec is not None and (pod is None or meta(pod).get(\"uid\", \"\") != rec.uid)))",
-           "                    or False)"),
+           "                    or False)", equivalent=True,
+           why="defence in depth: a call that reuses nothing never links, and an ended pod's record leaves _admissions"),
     Mutant("plugin", PLUGIN, "            if nxt is not None and nxt != size:", "            if False:"),
     Mutant("plugin", PLUGIN, "        out.sort(key=lambda c: (c.adm is None or c.adm.done == 0, c.pa is None,",
            "        out.sort(key=lambda c: (False, c.pa is None,"),
@@ -145,6 +146,8 @@ MUTANTS: List[Mutant] = [
     Mutant("numa", NUMA_ALIGN, "            if any(numa.get(d, -1) >= 0 and numa[d] not in mask for d in reusable):", "            if False:"),
     Mutant("numa", NUMA_ALIGN, '    admit = policy == "best-effort" or pref', "    admit = True"),
     Mutant("numa", NUMA_ALIGN, '        if kind == "init":\n            reuse |= got', '        if False:\n            reuse |= got'),
+    Mutant("numa", PLUGIN, "                if self._gpa_must is None and self.cfg.topology_manager.active and not self._continuing():",
+           "                if False:"),
     Mutant("numa", SCHED, "            if tm.active and fraction is None and steps:\n                ids, why = self._choose_aligned(",
            "            if False:\n                ids, why = self._choose_aligned("),
     Mutant("numa", SCHED, "                            if tm.active and fraction is None and steps:",
