@@ -263,7 +263,8 @@ def render_manifests(resource: str = DEFAULT_RESOURCE, image: str = IMAGE, names
                                         "--host=127.0.0.1", f"--port={DEFAULT_PORT}", f"--policy={policy}", "--informer=on",
                                         "--scheduler-names=default-scheduler", "--ledger-store=lease",
                                         f"--ledger-namespace={namespace}"],
-                            "readinessProbe": {"httpGet": {"host": "127.0.0.1", "path": "/healthz", "port": DEFAULT_PORT}},
+                            # ready once the informer has listed the cluster (filter / sort decline GPU pods before)
+                            "readinessProbe": {"httpGet": {"host": "127.0.0.1", "path": "/readyz", "port": DEFAULT_PORT}},
                             "livenessProbe": {"httpGet": {"host": "127.0.0.1", "path": "/healthz", "port": DEFAULT_PORT}},
                             "resources": {"requests": {"cpu": "200m", "memory": "256Mi"}, "limits": {"memory": "2Gi"}},
                         }],

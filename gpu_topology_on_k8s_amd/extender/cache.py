@@ -477,7 +477,9 @@ class ClusterCache:
         sent full Node objects) refreshes the node's topology/labels without an API call.
         """
         stale = self.clock() - self._last_full >= self.resync_s or name not in self._nodes
-        if sync and stale and not self.informed():
+        # polling mode only: with an informer attached (synced or still listing) the cluster is never
+        # re-listed per request (the extender declines decisions until the informer has synced)
+        if sync and stale and self.informer is None:
             try:
                 self.sync_all()
             except Exception as e:
@@ -485,7 +487,7 @@ class ClusterCache:
         st = self.update_node_object(node_obj) if node_obj is not None else self._state(name)
         # node unknown to the last sync (e.g. just created): read it directly.  An informer's view is
         # authoritative: a node it has not delivered yet simply has no topology for now
-        if sync and st.synced_at == 0.0 and not self.informed():
+        if sync and st.synced_at == 0.0 and self.informer is None:
             try:
                 self.refresh_node(name)
             except Exception as e:

@@ -463,6 +463,17 @@ class TopologyExtender:
         return self._eval_state(pod, name, st, k, shape)
 
     # ------------------------------------------------------------------ verbs
+    NOT_READY = "gpu-topology extender is still listing the cluster (informer not synced); retry"
+
+    @property
+    def ready(self) -> bool:
+        """Decisions can be made: polling mode, or the informer has listed every kind once.  Until
+        then filter and sort decline GPU pods (kube-scheduler retries them) instead of deciding on an
+        empty view, and nothing falls back to cluster-wide LISTs (at 100,000 pods one takes ~50 s and
+        GBs).  Bind needs no gate: it decides on its own refresh of the node (its object, its pods, its
+        ledger Lease) under the node lock."""
+        return self.cache.informer is None or self.cache.informed()
+
     def filter(self, pod: Dict[str, Any], node_names: Sequence[str], node_objs: Optional[Dict[str, dict]] = None):
         """-> (passing node names, {failed node: reason})."""
         t0 = time.perf_counter()
@@ -470,6 +481,9 @@ class TopologyExtender:
             k = self.request_of(pod)
         except MalformedPod as e:
             return [], {n: str(e) for n in node_names}
+        if k and not self.ready:
+            self.metrics.request("filter", "not_ready")
+            return [], {n: self.NOT_READY for n in node_names}
         ok: List[str] = []
         failed: Dict[str, str] = {}
         shape, bad = self._pod_shape(pod, k) if k else (None, "")
@@ -495,6 +509,9 @@ class TopologyExtender:
         try:
             k = self.request_of(pod)
         except MalformedPod:
+            return [(n, 0) for n in node_names]
+        if k and not self.ready:
+            self.metrics.request("prioritize", "not_ready")
             return [(n, 0) for n in node_names]
         objs: Dict[str, float] = {}
         shape, _ = self._pod_shape(pod, k) if k else (None, "")

@@ -8,7 +8,7 @@ Reference endpoint (``design.md:98-100``): ``http://127.0.0.1:32743/gputopology-
   POST {prefix}/filter      ExtenderArgs -> ExtenderFilterResult       (optional)
   POST {prefix}/bind        ExtenderBindingArgs -> ExtenderBindingResult
   POST {prefix}/preempt     ExtenderPreemptionArgs -> ExtenderPreemptionResult (topology-aware victims)
-  GET  {prefix}/healthz, /metrics (Prometheus text), /version, /debug/nodes (cache snapshot),
+  GET  {prefix}/healthz, {prefix}/readyz (503 until the informer has synced), /metrics (Prometheus text), /version, /debug/nodes (cache snapshot),
        /defrag?gpus=k (the fewest pod moves after which a k-GPU pod fits well: placement/defrag.py)
 
 kube-scheduler marshals Go structs without json tags, so request keys are capitalised (``Pod``,
@@ -168,6 +168,12 @@ def make_app(ext: TopologyExtender, prefix: str = DEFAULT_PREFIX, workers: int =
     async def healthz(request: web.Request) -> web.Response:
         return web.Response(text="ok")
 
+    async def readyz(request: web.Request) -> web.Response:
+        """Ready once the informer has listed the cluster (the DaemonSet's readinessProbe)."""
+        if ext.ready:
+            return web.Response(text="ok")
+        return web.Response(status=503, text=ext.NOT_READY)
+
     async def metrics(request: web.Request) -> web.Response:
         return web.Response(body=ext.metrics.exposition(), content_type="text/plain", charset="utf-8")
 
@@ -197,6 +203,8 @@ def make_app(ext: TopologyExtender, prefix: str = DEFAULT_PREFIX, workers: int =
     app.router.add_post(f"{prefix}/preempt", preempt)
     for p in (f"{prefix}/healthz", "/healthz"):
         app.router.add_get(p, healthz)
+    for p in (f"{prefix}/readyz", "/readyz"):
+        app.router.add_get(p, readyz)
     app.router.add_get(f"{prefix}/metrics", metrics)
     app.router.add_get("/metrics", metrics)
     app.router.add_get(f"{prefix}/version", version)

@@ -288,3 +288,39 @@ def test_informer_health_is_on_the_extenders_metrics():
     assert 'gtk_extender_informer_watch_errors_total{kind="Pod"} 1.0' in text
     assert 'gtk_extender_informer_last_list_items{kind="Pod"} 4.0' in text
     assert "gtk_extender_informer_synced 1.0" in text
+
+
+def test_before_the_first_sync_nothing_relists_per_request():
+    """An extender whose informer is still listing (a restart at 100,000 pods takes ~50 s) never
+    falls back to a cluster-wide LIST per request: filter and sort decline GPU pods until it has
+    synced (kube-scheduler retries them), /readyz answers 503, bind still works on its own refresh of
+    the node, and once the informer has synced everything is served from it."""
+    import requests
+
+    from gpu_topology_on_k8s_amd.sim.cluster import HttpExtender
+
+    api = _cluster(n_nodes=2, pods_per_node=1)
+    ext = TopologyExtender(api, ExtenderConfig(resync_s=0.0))
+    inf = ext.cache.make_informer(watch_timeout=2.0)  # attached, not started yet: still listing
+    http = HttpExtender(ext)
+    http.start()
+    try:
+        lists = api.calls.get("list_pods", 0) + api.calls.get("list_nodes", 0)
+        pod = api.create_pod(make_pod("want", gpus=2))
+        ok, failed = ext.filter(pod, ["n0", "n1"])
+        assert ok == [] and set(failed.values()) == {ext.NOT_READY}
+        assert ext.prioritize(pod, ["n0", "n1"]) == [("n0", 0), ("n1", 0)]
+        assert ext.filter(make_pod("cpu", gpus=0), ["n0"])[0] == ["n0"]  # not ours: passes
+        assert api.calls.get("list_pods", 0) + api.calls.get("list_nodes", 0) == lists  # no cluster LIST
+        assert requests.get(f"{http.url}/readyz", timeout=5).status_code == 503
+        d = ext.bind("default", "want", pod["metadata"]["uid"], "n1")  # its own refresh of n1
+        assert d is not None and len(d.ids) == 2
+        inf.start()
+        assert inf.wait_synced(10)
+        assert requests.get(f"{http.url}/readyz", timeout=5).status_code == 200
+        pod2 = api.create_pod(make_pod("want2", gpus=2))
+        assert _wait(lambda: ext.filter(pod2, ["n0", "n1"])[0] == ["n0", "n1"])
+        assert "not_ready" in ext.metrics.exposition().decode()
+    finally:
+        inf.stop()
+        http.stop()
