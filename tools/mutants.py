@@ -128,6 +128,9 @@ MUTANTS: List[Mutant] = [
     Mutant("informer", INFORMER, "self.on_event(t, kind, self.transform(kind, obj) if self.transform is not None else obj)",
            "self.on_event(t, kind, obj)"),
     Mutant("informer", INFORMER, "                    failures = 0\n                    new_rv", "                    new_rv"),
+    Mutant("informer", CACHE, "        if sync and stale and self.informer is None:", "        if sync and stale and not self.informed():"),
+    Mutant("informer", SCHED, "        if k and not self.ready:\n            self.metrics.request(\"filter\", \"not_ready\")",
+           "        if False:\n            self.metrics.request(\"filter\", \"not_ready\")"),
     # per-identity RBAC of the deploy manifests
     Mutant("rbac", RBAC, "        if self.identity.own_node_only and node != self.node_name:", "        if False:"),
     Mutant("rbac", RBAC, "and (self.namespace is None or self.namespace == namespace))", ")"),
