@@ -758,8 +758,10 @@ class TopologyExtender:
         annotation) are left out: their used sets are not exact."""
         from ..placement.defrag import plan_defrag
 
-        if not self.cache.informed():
+        if self.cache.informer is None:
             self.cache.sync_all()
+        elif not self.cache.informed():
+            return None  # still listing: no plan from a partial view, and no cluster LIST per request
         now = self.clock()
         nodes: Dict[str, Topology] = {}
         pods: Dict[str, Dict[str, Tuple[int, ...]]] = {}

@@ -311,6 +311,9 @@ def test_before_the_first_sync_nothing_relists_per_request():
         assert ok == [] and set(failed.values()) == {ext.NOT_READY}
         assert ext.prioritize(pod, ["n0", "n1"]) == [("n0", 0), ("n1", 0)]
         assert ext.filter(make_pod("cpu", gpus=0), ["n0"])[0] == ["n0"]  # not ours: passes
+        ext.preempt(pod, {"n0": ([], 0)})  # the verbs that read the cache without a gate
+        ext.defrag(2)
+        ext.cache.get("n1")
         assert api.calls.get("list_pods", 0) + api.calls.get("list_nodes", 0) == lists  # no cluster LIST
         assert requests.get(f"{http.url}/readyz", timeout=5).status_code == 503
         d = ext.bind("default", "want", pod["metadata"]["uid"], "n1")  # its own refresh of n1
