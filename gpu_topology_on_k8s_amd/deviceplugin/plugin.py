@@ -1111,11 +1111,15 @@ class DevicePluginServer:
                 env[k] = v.strip()
         return env
 
-    def _node_pods(self) -> List[dict]:
+    def _node_pods(self, cached: bool = False) -> List[dict]:
+        """This node's live pods.  ``cached``: from the apiserver's watch cache, for the periodic
+        reconcile (on every node every --reconcile-interval: a consistent read would be an etcd range
+        over every pod of the cluster each time; a stale answer only delays a correction, which is a
+        conditional patch)."""
         if self.api is None or not self.cfg.node_name:
             return []
         try:
-            return [p for p in self.api.list_pods(node_name=self.cfg.node_name) if not pod_is_terminal(p)]
+            return [p for p in self.api.list_pods(node_name=self.cfg.node_name, cached=cached) if not pod_is_terminal(p)]
         except Exception as e:
             log.warning("listing pods on %s failed: %s", self.cfg.node_name, e)
             return []
@@ -1302,7 +1306,7 @@ class DevicePluginServer:
             return 0
         names = self._resource_names()
         fixed = 0
-        pods = self._node_pods()
+        pods = self._node_pods(cached=True)
         reported = {}
         for p in pods:
             md = meta(p)

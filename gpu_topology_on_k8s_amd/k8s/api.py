@@ -76,7 +76,10 @@ class KubeAPI:
     def get_pod(self, namespace: str, name: str) -> Obj:
         raise NotImplementedError
 
-    def list_pods(self, node_name: Optional[str] = None, namespace: Optional[str] = None) -> List[Obj]:
+    def list_pods(self, node_name: Optional[str] = None, namespace: Optional[str] = None, cached: bool = False) -> List[Obj]:
+        """Pods (of one node / namespace).  ``cached``: served from the apiserver's watch cache
+        (``resourceVersion=0``: no etcd range over every pod of the cluster, possibly a little stale);
+        for periodic passes that tolerate it (the device plugin's reconcile)."""
         raise NotImplementedError
 
     def patch_pod_annotations(self, namespace: str, name: str, annotations: Dict[str, Optional[str]],
@@ -227,11 +230,10 @@ class RestKubeAPI(KubeAPI):
     def get_pod(self, namespace: str, name: str) -> Obj:
         return self._do("GET", f"/api/v1/namespaces/{quote(namespace)}/pods/{quote(name)}")
 
-    def list_pods(self, node_name: Optional[str] = None, namespace: Optional[str] = None) -> List[Obj]:
+    def list_pods(self, node_name: Optional[str] = None, namespace: Optional[str] = None, cached: bool = False) -> List[Obj]:
         path = f"/api/v1/namespaces/{quote(namespace)}/pods" if namespace else "/api/v1/pods"
-        if node_name:
-            path += "?fieldSelector=" + quote(f"spec.nodeName={node_name}")
-        return self._do("GET", path).get("items", [])
+        q = ([f"fieldSelector={quote(f'spec.nodeName={node_name}')}"] if node_name else []) + (["resourceVersion=0"] if cached else [])
+        return self._do("GET", path + ("?" + "&".join(q) if q else "")).get("items", [])
 
     def patch_pod_annotations(self, namespace, name, annotations, resource_version=None) -> Obj:
         md: Obj = {"annotations": annotations}

@@ -88,6 +88,7 @@ class FakeAPIServer(KubeAPI):
         self.watch_cache_pages = False
         self.bytes_served: Dict[str, int] = defaultdict(int)  # kind -> JSON bytes of LIST responses
         self.list_requests: Dict[str, int] = defaultdict(int)  # kind -> LIST requests (pages)
+        self.cache_reads: Dict[str, int] = defaultdict(int)  # kind -> LISTs served from the watch cache (resourceVersion=0)
         self._watch_cuts: Dict[str, List[int]] = defaultdict(list)  # kind -> cut the next watch after n events
         self._open_watches: Dict[str, Dict[int, List[Optional[int]]]] = defaultdict(dict)  # kind -> id -> [cut]
         self._watch_ids = 0
@@ -149,8 +150,10 @@ class FakeAPIServer(KubeAPI):
                 encoded = [json.dumps(o) for _, o in sorted(src.items()) if match_fields(o, field_selector)
                            and (namespace is None or meta(o).get("namespace") == namespace)]
                 list_rv = str(self._rv)
-                if str(resource_version) == "0" and not self.watch_cache_pages:
-                    limit = 0
+                if str(resource_version) == "0":
+                    self.cache_reads[kind] += 1
+                    if not self.watch_cache_pages:
+                        limit = 0
             page, rest = (encoded[:limit], encoded[limit:]) if limit else (encoded, [])
             token = ""
             if rest:
@@ -335,9 +338,11 @@ class FakeAPIServer(KubeAPI):
             self._enter("get_pod")
             return copy.deepcopy(self._pod(namespace, name))
 
-    def list_pods(self, node_name: Optional[str] = None, namespace: Optional[str] = None) -> List[Obj]:
+    def list_pods(self, node_name: Optional[str] = None, namespace: Optional[str] = None, cached: bool = False) -> List[Obj]:
         with self._lock:
             self._enter("list_pods")
+            if cached:
+                self.cache_reads["Pod"] += 1
             out = []
             for (ns, _), p in self.pods.items():
                 if namespace and ns != namespace:
@@ -472,7 +477,8 @@ class _Handler(BaseHTTPRequestHandler):
             if len(rest) >= 3 and rest[0] == "namespaces" and rest[2] == "pods":
                 ns = rest[1]
                 if len(rest) == 3 and method == "GET":
-                    return self._send(200, {"kind": "PodList", "items": self.api.list_pods(node_name=node_name, namespace=ns)})
+                    return self._send(200, {"kind": "PodList", "items": self.api.list_pods(
+                        node_name=node_name, namespace=ns, cached=(q.get("resourceVersion") or [""])[0] == "0")})
                 if len(rest) == 4:
                     if method == "GET":
                         return self._send(200, self.api.get_pod(ns, rest[3]))

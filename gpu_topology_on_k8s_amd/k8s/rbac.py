@@ -139,9 +139,9 @@ class RBACView(KubeAPI):
         self._check("get", "", "pods", namespace, name)
         return self.api.get_pod(namespace, name)
 
-    def list_pods(self, node_name=None, namespace=None):
+    def list_pods(self, node_name=None, namespace=None, cached=False):
         self._check("list", "", "pods", namespace)
-        return self.api.list_pods(node_name=node_name, namespace=namespace)
+        return self.api.list_pods(node_name=node_name, namespace=namespace, cached=cached)
 
     def patch_pod_annotations(self, namespace, name, annotations, resource_version=None):
         self._check("patch", "", "pods", namespace, name)

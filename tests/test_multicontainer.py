@@ -322,3 +322,31 @@ def test_a_new_pod_on_gpus_freed_before_the_status_update_is_not_the_old_one():
         assert sorted(int(i) for i in kub.allocated[RES]["default/p2"]) == [2, 3]
         assert kub.preferred_calls[-1] == ([], 2)
         assert _ann(c, "p2").assigned and sorted(_ann(c, "p2").group) == [2, 3]
+
+
+def test_the_periodic_reconcile_reads_from_the_watch_cache():
+    """Every node's plugin reconciles every --reconcile-interval: its pod LIST is a watch-cache read
+    (resourceVersion=0), not an etcd range over all the cluster's pods; an admission still reads
+    consistently.  Over HTTP the query carries resourceVersion=0."""
+    from gpu_topology_on_k8s_amd.k8s import FakeAPIServer, serve_http
+    from gpu_topology_on_k8s_amd.k8s.api import RestKubeAPI
+
+    with SimCluster({"n": fx.f7_mi355x()}) as c:
+        c.submit("a", 2)
+        c.schedule_pending()
+        before = c.api.cache_reads["Pod"]
+        c.reconcile()
+        assert c.api.cache_reads["Pod"] == before + 1
+        c.submit("b", 2)
+        c.schedule_pending()  # GetPreferredAllocation / Allocate: consistent reads
+        assert c.api.cache_reads["Pod"] == before + 1
+    api = FakeAPIServer()
+    srv, url = serve_http(api)
+    try:
+        api.create_pod(make_pod("x", gpus=1, node="n"))
+        got = RestKubeAPI(url).list_pods(node_name="n", cached=True)
+        assert [p["metadata"]["name"] for p in got] == ["x"] and api.cache_reads["Pod"] == 1
+        RestKubeAPI(url).list_pods(node_name="n")
+        assert api.cache_reads["Pod"] == 1
+    finally:
+        srv.shutdown()
