@@ -381,7 +381,7 @@ class DevicePluginServer:
             if not tok:
                 continue
             i: Optional[int] = None
-            if tok.isdigit() and int(tok) < t.n:
+            if tok.isascii() and tok.isdigit() and int(tok) < t.n:  # not str.isdigit alone: "¹" is a digit to it
                 i = int(tok)
             elif ":" in tok:
                 i = by_bdf.get(tok.lower())
@@ -1311,7 +1311,7 @@ class DevicePluginServer:
         for p in pods:
             md = meta(p)
             key = f"{md.get('namespace', 'default')}/{md.get('name')}"
-            reported[key] = {int(i) for r in names for i in truth.get(key, {}).get(r, []) if str(i).isdigit()}
+            reported[key] = {int(i) for r in names for i in truth.get(key, {}).get(r, []) if str(i).isascii() and str(i).isdigit()}
         # pod-resources lists app containers and sidecars, not the init containers that have exited,
         # yet the kubelet counts an init container's devices as the pod's until it ends.  Where they
         # went: (1) what this plugin saw allocated together (an admission unit: the calls of one kubelet

@@ -24,7 +24,7 @@ from typing import Callable, Dict, Iterable, List, Optional, Set, Tuple
 
 from ..k8s.annotations import (Contract, PodAssignment, decode_node_annotations, ledger_gen, ledger_uids, parse_ledger,
                                probing_until)
-from ..k8s.api import KubeAPI
+from ..k8s.api import ApiError, KubeAPI
 from ..k8s.objects import annotations as obj_annotations
 from ..k8s.objects import labels as obj_labels
 from ..k8s.objects import meta, pod_gpu_request, pod_is_terminal, pod_key, pod_node
@@ -367,13 +367,34 @@ class ClusterCache:
         st.synced_at = now
 
     def refresh_node(self, name: str) -> NodeState:
-        """Authoritative re-read of one node, its ledger Lease and its pods (used before every bind)."""
+        """Authoritative re-read of one node, its ledger Lease and its pods (used before every bind).
+
+        The pods are read last, from the apiserver's watch cache but no older than the node and Lease
+        just read (``resourceVersionMatch=NotOlderThan``): an etcd range over every pod of the cluster
+        per bind is not needed for the ordering that matters.  A ledger entry is dropped only by a
+        write made after its writer saw the pod bound, so a pod LIST at least as new as the ledger
+        shows every pod whose entry is gone.  A cache that cannot catch up (504), or an apiserver that
+        refuses the parameter, gets a consistent read instead."""
         node = self.api.get_node(name)
         st = self.update_node_object(node)
+        floor = _rv_int(meta(node).get("resourceVersion"))
         if self.ledger.uses_lease:
-            self.update_lease_object(name, self.ledger.read_lease(self.api, name))
+            lease = self.ledger.read_lease(self.api, name)
+            self.update_lease_object(name, lease)
+            if lease is not None:
+                lrv = _rv_int(meta(lease).get("resourceVersion"))
+                floor = None if floor is None or lrv is None else max(floor, lrv)
         epoch = self._next_epoch()
-        pods = self.api.list_pods(node_name=name)
+        pods = None
+        if floor is not None:
+            try:
+                pods = self.api.list_pods(node_name=name, not_older_than=str(floor))
+            except ApiError as e:
+                if e.code not in (400, 422, 504):
+                    raise
+                log.info("pod LIST of %s not older than %s: %s; reading consistently", name, floor, e)
+        if pods is None:
+            pods = self.api.list_pods(node_name=name)
         with st.lock:
             self._rebuild(st, pods, epoch)
         return st
@@ -594,3 +615,11 @@ class ClusterCache:
                     "labels": st.labels,
                 }
         return out
+
+
+def _rv_int(rv) -> Optional[int]:
+    """A resourceVersion as the etcd revision it is, or None (opaque to this client: no floor)."""
+    try:
+        return int(str(rv))
+    except (TypeError, ValueError):
+        return None

@@ -76,10 +76,13 @@ class KubeAPI:
     def get_pod(self, namespace: str, name: str) -> Obj:
         raise NotImplementedError
 
-    def list_pods(self, node_name: Optional[str] = None, namespace: Optional[str] = None, cached: bool = False) -> List[Obj]:
+    def list_pods(self, node_name: Optional[str] = None, namespace: Optional[str] = None, cached: bool = False,
+                  not_older_than: Optional[str] = None) -> List[Obj]:
         """Pods (of one node / namespace).  ``cached``: served from the apiserver's watch cache
         (``resourceVersion=0``: no etcd range over every pod of the cluster, possibly a little stale);
-        for periodic passes that tolerate it (the device plugin's reconcile)."""
+        for periodic passes that tolerate it (the device plugin's reconcile).  ``not_older_than``: a
+        watch-cache read that reflects at least that resourceVersion (``resourceVersionMatch=
+        NotOlderThan``; 504 when the cache cannot catch up)."""
         raise NotImplementedError
 
     def patch_pod_annotations(self, namespace: str, name: str, annotations: Dict[str, Optional[str]],
@@ -230,9 +233,12 @@ class RestKubeAPI(KubeAPI):
     def get_pod(self, namespace: str, name: str) -> Obj:
         return self._do("GET", f"/api/v1/namespaces/{quote(namespace)}/pods/{quote(name)}")
 
-    def list_pods(self, node_name: Optional[str] = None, namespace: Optional[str] = None, cached: bool = False) -> List[Obj]:
+    def list_pods(self, node_name: Optional[str] = None, namespace: Optional[str] = None, cached: bool = False,
+                  not_older_than: Optional[str] = None) -> List[Obj]:
         path = f"/api/v1/namespaces/{quote(namespace)}/pods" if namespace else "/api/v1/pods"
         q = ([f"fieldSelector={quote(f'spec.nodeName={node_name}')}"] if node_name else []) + (["resourceVersion=0"] if cached else [])
+        if not_older_than and not cached:
+            q += [f"resourceVersion={quote(str(not_older_than))}", "resourceVersionMatch=NotOlderThan"]
         return self._do("GET", path + ("?" + "&".join(q) if q else "")).get("items", [])
 
     def patch_pod_annotations(self, namespace, name, annotations, resource_version=None) -> Obj:

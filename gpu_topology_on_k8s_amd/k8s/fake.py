@@ -89,6 +89,7 @@ class FakeAPIServer(KubeAPI):
         self.bytes_served: Dict[str, int] = defaultdict(int)  # kind -> JSON bytes of LIST responses
         self.list_requests: Dict[str, int] = defaultdict(int)  # kind -> LIST requests (pages)
         self.cache_reads: Dict[str, int] = defaultdict(int)  # kind -> LISTs served from the watch cache (resourceVersion=0)
+        self.min_rv_reads: Dict[str, int] = defaultdict(int)  # kind -> watch-cache LISTs with resourceVersionMatch=NotOlderThan
         self._watch_cuts: Dict[str, List[int]] = defaultdict(list)  # kind -> cut the next watch after n events
         self._open_watches: Dict[str, Dict[int, List[Optional[int]]]] = defaultdict(dict)  # kind -> id -> [cut]
         self._watch_ids = 0
@@ -338,9 +339,14 @@ class FakeAPIServer(KubeAPI):
             self._enter("get_pod")
             return copy.deepcopy(self._pod(namespace, name))
 
-    def list_pods(self, node_name: Optional[str] = None, namespace: Optional[str] = None, cached: bool = False) -> List[Obj]:
+    def list_pods(self, node_name: Optional[str] = None, namespace: Optional[str] = None, cached: bool = False,
+                  not_older_than: Optional[str] = None) -> List[Obj]:
         with self._lock:
             self._enter("list_pods")
+            if not_older_than is not None:
+                if int(not_older_than) > self._rv:  # the apiserver waits ~3 s for its cache, then gives up
+                    raise ApiError(504, f"Timeout: Too large resource version: {not_older_than}, current: {self._rv}")
+                self.min_rv_reads["Pod"] += 1
             if cached:
                 self.cache_reads["Pod"] += 1
             out = []
@@ -456,6 +462,10 @@ class _Handler(BaseHTTPRequestHandler):
             if rest in (["nodes"], ["pods"]) and method == "GET" and watch:
                 return self._watch("Node" if rest == ["nodes"] else "Pod", (q.get("resourceVersion") or ["0"])[0],
                                    float((q.get("timeoutSeconds") or ["60"])[0]), fs or None)
+            if rest == ["pods"] and method == "GET" and (q.get("resourceVersionMatch") or [""])[0] == "NotOlderThan":
+                node_name = fs.split("=", 1)[1] if fs.startswith("spec.nodeName=") else None
+                items = self.api.list_pods(node_name=node_name, not_older_than=(q.get("resourceVersion") or ["0"])[0])
+                return self._send(200, {"kind": "PodList", "metadata": {"resourceVersion": str(self.api._rv)}, "items": items})
             if rest in (["nodes"], ["pods"]) and method == "GET":
                 kind = "Node" if rest == ["nodes"] else "Pod"
                 items, rv, cont = self.api.list_page(kind, int((q.get("limit") or ["0"])[0]), (q.get("continue") or [""])[0],

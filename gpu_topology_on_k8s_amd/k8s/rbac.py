@@ -139,9 +139,9 @@ class RBACView(KubeAPI):
         self._check("get", "", "pods", namespace, name)
         return self.api.get_pod(namespace, name)
 
-    def list_pods(self, node_name=None, namespace=None, cached=False):
+    def list_pods(self, node_name=None, namespace=None, cached=False, not_older_than=None):
         self._check("list", "", "pods", namespace)
-        return self.api.list_pods(node_name=node_name, namespace=namespace, cached=cached)
+        return self.api.list_pods(node_name=node_name, namespace=namespace, cached=cached, not_older_than=not_older_than)
 
     def patch_pod_annotations(self, namespace, name, annotations, resource_version=None):
         self._check("patch", "", "pods", namespace, name)

@@ -122,7 +122,7 @@ def latest_checkpoint(root: str) -> Optional[str]:
     for d in (os.path.join(root, name), os.path.join(root, f".{name}.old")):
         if os.path.exists(os.path.join(d, "meta.json")):
             return d
-    done = sorted((x for x in os.listdir(root) if x.startswith("step_") and x[5:].isdigit()
+    done = sorted((x for x in os.listdir(root) if x.startswith("step_") and x[5:].isascii() and x[5:].isdigit()
                    and os.path.exists(os.path.join(root, x, "meta.json"))), key=lambda x: int(x[5:]))
     return os.path.join(root, done[-1]) if done else None
 
@@ -315,7 +315,7 @@ class CheckpointWriter:
             return
         cur = int(current[5:])
         # numeric order: the zero padding stops sorting lexicographically past step 999999
-        steps = sorted((d for d in os.listdir(self.root) if d.startswith("step_") and d[5:].isdigit() and d != current),
+        steps = sorted((d for d in os.listdir(self.root) if d.startswith("step_") and d[5:].isascii() and d[5:].isdigit() and d != current),
                        key=lambda d: int(d[5:]))
         for d in steps:
             if int(d[5:]) > cur:  # the abandoned run's (complete or not)

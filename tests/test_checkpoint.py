@@ -271,3 +271,15 @@ def test_latest_survives_crash_while_replacing_a_step(tmp_path):
     assert latest_checkpoint(str(root)).endswith(".step_1000000.old")
     (root / ".step_1000000.old" / "meta.json").unlink()
     assert latest_checkpoint(str(root)).endswith("step_999999")  # numeric, not lexicographic
+
+
+def test_stray_step_directories_are_ignored(tmp_path):
+    """A directory named like a step but not one ("step_¹": a digit to str.isdigit, not to int) is
+    neither resumed from nor pruned, and does not break either."""
+    import os
+
+    from gpu_topology_on_k8s_amd.models.checkpoint import latest_checkpoint
+
+    os.makedirs(tmp_path / "step_¹")
+    os.makedirs(tmp_path / "step_x")
+    assert latest_checkpoint(str(tmp_path)) is None

@@ -67,8 +67,8 @@ def test_a_cordon_names_the_whole_physical_gpu_and_reports_unknown_tokens():
     t = time_slice(fx.f7_mi355x(), 2)  # 16 slices, two per GPU
     with SimCluster({"n": t}) as c:
         plug = c.nodes["n"].plugin
-        got, unknown = plug.cordoned_from("3, 0000:ff:00.0, 99, gpu7")
-        assert got == {2, 3} and unknown == ["0000:ff:00.0", "99", "gpu7"]
+        got, unknown = plug.cordoned_from("3, 0000:ff:00.0, 99, gpu7, ¹")
+        assert got == {2, 3} and unknown == ["0000:ff:00.0", "99", "gpu7", "¹"]
         add, drop = plug.apply_cordon("3,99")
         assert add == {2, 3} and not drop
         assert "GPUCordonUnknown" in [e.get("reason") for e in c.api.events]

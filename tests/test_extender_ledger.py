@@ -537,3 +537,51 @@ def test_the_bind_retry_loop_has_a_time_budget():
     assert ei.value.code == 409 and "budget" in str(ei.value) and _t.monotonic() - t0 < 1.0
     assert ext.metrics.bind_aborts.labels("budget")._value.get() == 1
     assert ext.metrics.bind_lock_seconds._sum.get() > 0
+
+
+def test_a_binds_pod_list_is_a_watch_cache_read_no_older_than_its_ledger():
+    """Each bind refreshes its node: the node, the ledger, then the node's pods — read from the
+    apiserver's watch cache but no older than the ledger and node just read (resourceVersionMatch=
+    NotOlderThan), instead of an etcd range over every pod of the cluster.  A cache that cannot catch
+    up (504) gets a consistent read; over HTTP the query carries the floor."""
+    from gpu_topology_on_k8s_amd.k8s import serve_http
+    from gpu_topology_on_k8s_amd.k8s.api import ApiError, RestKubeAPI
+
+    api, exts, _ = _two(ledger=True, n_pods=3)
+    floors = []
+    real = api.list_pods
+
+    def spy(node_name=None, namespace=None, cached=False, not_older_than=None):
+        # the refresh has just read the node and the ledger: its floor is the newer of the two
+        rvs = [int(api.get_node("n1")["metadata"]["resourceVersion"])]
+        if STORE["store"] == "lease" and ("kube-system", "gpu-ledger.n1") in api.leases:
+            rvs.append(int(api.get_lease("kube-system", "gpu-ledger.n1")["metadata"]["resourceVersion"]))
+        floors.append((not_older_than, max(rvs)))
+        return real(node_name=node_name, namespace=namespace, cached=cached, not_older_than=not_older_than)
+
+    api.list_pods = spy
+    _bind(api, exts[0], "p0")
+    _bind(api, exts[1], "p1")
+    node_rv = int(api.get_node("n1")["metadata"]["resourceVersion"])
+    assert len(floors) >= 2 and all(f is not None and int(f) == want for f, want in floors), floors
+    assert api.min_rv_reads["Pod"] >= 2
+    # a watch cache that cannot catch up: the bind still decides on a consistent read
+    def too_new(node_name=None, namespace=None, cached=False, not_older_than=None):
+        if not_older_than is not None:
+            raise ApiError(504, "Timeout: Too large resource version")
+        return real(node_name=node_name, namespace=namespace, cached=cached)
+
+    api.list_pods = too_new
+    d = _bind(api, exts[0], "p2")
+    assert d is not None and len(d.ids) == 1
+    api.list_pods = real
+    srv, url = serve_http(api)
+    try:
+        before = api.min_rv_reads["Pod"]
+        got = RestKubeAPI(url).list_pods(node_name="n1", not_older_than=str(node_rv))
+        assert len(got) == 3 and api.min_rv_reads["Pod"] == before + 1
+        with pytest.raises(ApiError) as ei:
+            RestKubeAPI(url).list_pods(node_name="n1", not_older_than=str(10 ** 9))
+        assert ei.value.code == 504
+    finally:
+        srv.shutdown()

@@ -72,6 +72,8 @@ MUTANTS: List[Mutant] = [
            "                if False:"),
     Mutant("ledger", SCHED, "            if self.cfg.ledger and recorded is not None and time.monotonic() - recorded > LEDGER_GRACE_S / 2:",
            "            if False:"),
+    Mutant("ledger", CACHE, "                floor = None if floor is None or lrv is None else max(floor, lrv)",
+           "                floor = floor"),
     # overlay / LIST epochs (the cache's view of this process's binds)
     Mutant("cache", CACHE, "                after_bind = list_epoch > self._overlay_epoch.get((st.name, key), 0)",
            "                after_bind = True"),
