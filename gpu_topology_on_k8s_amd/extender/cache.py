@@ -63,6 +63,7 @@ class NodeState:
     topology: Optional[Topology] = None
     labels: Dict[str, str] = field(default_factory=dict)
     node_rv: str = ""
+    node_uid: str = ""  # owner of the node's ledger Lease (garbage-collected with the node)
     allocs: Dict[str, Alloc] = field(default_factory=dict)
     unknown_pods: Dict[str, int] = field(default_factory=dict)  # pod -> devices held without a GROUP annotation
     unknown_uids: Dict[str, str] = field(default_factory=dict)  # pod UID -> pod key of unknown_pods
@@ -224,6 +225,7 @@ class ClusterCache:
                     st.topology = None
                 st.node_rv = rv
             st.labels = labels
+            st.node_uid = str(meta(node).get("uid", "") or "")
             st.probing_until = probing_until(obj_annotations(node), self.contract)
             st.ledger_node = parse_ledger(obj_annotations(node), self.contract) if self.ledger.uses_node else {}
             st.uid_node = ledger_uids(obj_annotations(node), self.contract) if self.ledger.uses_node else {}

@@ -71,16 +71,21 @@ class LedgerStore:
         except NotFound:
             return None
 
-    def lease_object(self, node: str, value: str) -> dict:
+    def lease_object(self, node: str, value: str, node_uid: str = "") -> dict:
+        """A node's ledger Lease.  With the node's UID it is owned by the Node, so the garbage collector
+        deletes it with the node (a namespaced dependent may have a cluster-scoped owner; without
+        ``blockOwnerDeletion`` this needs no permission on the Node)."""
         c = self.contract
-        return {"apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
-                "metadata": {"name": lease_name(node), "namespace": self.namespace,
-                             "labels": {"app.kubernetes.io/part-of": "gpu-topology-amd", "app.kubernetes.io/component": "gpu-ledger"},
-                             "annotations": {c.ledger_key: value, f"{c.prefix}/node": node}},
+        md = {"name": lease_name(node), "namespace": self.namespace,
+              "labels": {"app.kubernetes.io/part-of": "gpu-topology-amd", "app.kubernetes.io/component": "gpu-ledger"},
+              "annotations": {c.ledger_key: value, f"{c.prefix}/node": node}}
+        if node_uid:
+            md["ownerReferences"] = [{"apiVersion": "v1", "kind": "Node", "name": node, "uid": node_uid}]
+        return {"apiVersion": "coordination.k8s.io/v1", "kind": "Lease", "metadata": md,
                 "spec": {"holderIdentity": "gpu-topology-extender"}}
 
     def write(self, api: KubeAPI, node: str, entries: Entries, lease_rv: Optional[str], lease_gen: int,
-              node_rv: str, node_gen: int, uids: Optional[Dict[str, str]] = None) -> None:
+              node_rv: str, node_gen: int, uids: Optional[Dict[str, str]] = None, node_uid: str = "") -> None:
         """Record ``entries`` (with their pods' ``uids``) as the node's ledger, conditional on the
         versions the decision saw.  Raises :class:`~..k8s.api.Conflict` when another writer got there
         first."""
@@ -88,7 +93,7 @@ class LedgerStore:
         if self.uses_lease:
             value = dump_ledger(entries, lease_gen + 1, uids)
             if lease_rv is None:
-                api.create_lease(self.namespace, self.lease_object(node, value))  # 409 AlreadyExists: a race lost
+                api.create_lease(self.namespace, self.lease_object(node, value, node_uid))  # 409 AlreadyExists: a race lost
             else:
                 api.patch_lease(self.namespace, lease_name(node), {key: value}, resource_version=lease_rv)
         if self.uses_node:

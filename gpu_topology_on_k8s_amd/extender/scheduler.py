@@ -583,7 +583,7 @@ class TopologyExtender:
                         uids[key] = uid or str(meta(pod).get("uid", ""))
                         try:
                             self.ledger.write(self.api, node, entries, st.lease_rv, st.gen_lease, st.node_rv, st.gen_node,
-                                              uids)
+                                              uids, node_uid=st.node_uid)
                         except Conflict:
                             self.metrics.ledger_conflicts += 1
                             self.metrics.ledger_conflict.inc()

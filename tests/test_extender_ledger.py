@@ -585,3 +585,16 @@ def test_a_binds_pod_list_is_a_watch_cache_read_no_older_than_its_ledger():
         assert ei.value.code == 504
     finally:
         srv.shutdown()
+
+
+def test_the_ledger_lease_is_owned_by_its_node():
+    """A node's ledger Lease carries an ownerReference to the Node: the garbage collector removes it
+    with the node, so Leases of deleted nodes do not pile up in the extender's namespace."""
+    if STORE["store"] != "lease":
+        pytest.skip("the Node store has no separate object")
+    api, exts, _ = _two(ledger=True, n_pods=1)
+    _bind(api, exts[0], "p0")
+    lease = api.get_lease("kube-system", "gpu-ledger.n1")
+    node = api.get_node("n1")
+    assert lease["metadata"]["ownerReferences"] == [{"apiVersion": "v1", "kind": "Node", "name": "n1",
+                                                     "uid": node["metadata"]["uid"]}]
