@@ -13,6 +13,7 @@ from gpu_topology_on_k8s_amd.k8s.objects import annotations as obj_annotations
 from gpu_topology_on_k8s_amd.placement.numa_align import TopologyManager
 from gpu_topology_on_k8s_amd.sim import SimCluster
 from gpu_topology_on_k8s_amd.topology import fixtures as fx
+from gpu_topology_on_k8s_amd.topology.shares import time_slice
 
 C = Contract()
 
@@ -29,6 +30,11 @@ def _shape(rng):
     return {"gpus": 0, "split": [rng.choice([1, 2])], "sidecars": [1]}
 
 
+def _physical(t, i):
+    """Every device of device i's physical GPU (a cordon names the whole GPU: all its slices)."""
+    return {g.index for g in t.gpus if g.physical == t.gpus[i].physical}
+
+
 def _wait(pred, timeout=5.0):
     t0 = time.time()
     while time.time() - t0 < timeout:
@@ -42,8 +48,9 @@ def _wait(pred, timeout=5.0):
 def test_everything_at_once_under_churn(seed):
     rng = random.Random(seed)
     tms = {"plain": TopologyManager(), "aligned": TopologyManager("best-effort", "container"),
-           "strict": TopologyManager("single-numa-node", "pod")}
-    with SimCluster({n: fx.f7_mi355x() for n in tms}, topology_manager=tms, informer=True, rbac=True) as c:
+           "strict": TopologyManager("single-numa-node", "pod"), "sliced": TopologyManager("best-effort", "container")}
+    nodes = {n: (time_slice(fx.f7_mi355x(), 2) if n == "sliced" else fx.f7_mi355x()) for n in tms}
+    with SimCluster(nodes, topology_manager=tms, informer=True, rbac=True) as c:
         live, cordoned, placed = [], {}, 0
         for i in range(150):
             ev = rng.random()
@@ -51,16 +58,19 @@ def test_everything_at_once_under_churn(seed):
                 c.complete(live.pop(rng.randrange(len(live))))
             elif ev < 0.38:  # the operator cordons or releases a GPU somewhere
                 node = rng.choice(list(tms))
-                want = "" if cordoned.get(node) else str(rng.randrange(8))
+                want = "" if cordoned.get(node) else str(rng.randrange(nodes[node].n))
                 c.api.patch_node(node, annotations={C.cordon_key: want})
                 c.nodes[node].plugin.poll_node()
                 cordoned[node] = want
             # the informer delivers what just changed before the next decision
             assert _wait(lambda: all(
                 {g.index for g in c.extender.cache.get(n, sync=False).topology.gpus if not g.healthy}
-                == ({int(cordoned[n])} if cordoned.get(n) else set()) for n in tms))
+                == (_physical(nodes[n], int(cordoned[n])) if cordoned.get(n) else set()) for n in tms))
             name = f"p{i}"
-            c.submit(name, **_shape(rng))
+            if rng.random() < 0.2:  # time slices: one pool of their own (the sliced node)
+                c.submit(name, **rng.choice([{"gpus": 1}, {"gpus": 2}, {"gpus": 0, "split": [1, 1]}]), slices=True)
+            else:
+                c.submit(name, **_shape(rng))
             (r,) = c.schedule_pending()
             if r.node is None:
                 c.delete(name)
@@ -70,7 +80,7 @@ def test_everything_at_once_under_churn(seed):
             pa = PodAssignment.from_annotations(obj_annotations(c.api.get_pod("default", name)))
             assert pa.assigned and sorted(pa.group) == sorted(r.allocated), (r, pa)
             if cordoned.get(r.node):
-                assert int(cordoned[r.node]) not in r.allocated, (r, cordoned)
+                assert not _physical(nodes[r.node], int(cordoned[r.node])) & set(r.allocated), (r, cordoned)
             live.append(name)
             placed += 1
         assert placed >= 40
