@@ -83,6 +83,8 @@ def test_everything_at_once_under_churn(seed):
                 assert not _physical(nodes[r.node], int(cordoned[r.node])) & set(r.allocated), (r, cordoned)
             live.append(name)
             placed += 1
+            if i % 10 == 9:  # every claim was exact: the pod-resources reconcile finds nothing to fix
+                assert c.reconcile() == 0, i
         assert placed >= 40
         assert c.denied == []
         assert not any(n.kubelet.rejected for n in c.nodes.values())
