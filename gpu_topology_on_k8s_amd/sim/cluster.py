@@ -16,6 +16,7 @@ restart recovery, fault injection and the scheduling-latency benchmark.
 from __future__ import annotations
 
 import asyncio
+import copy
 import logging
 import os
 import shutil
@@ -225,6 +226,7 @@ class SimCluster:
         self.http: Optional[HttpExtender] = None
         self._client = _ExtenderClient()
         self.history: List[ScheduleResult] = []
+        self._plugin_args: Dict[str, tuple] = {}
 
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> "SimCluster":
@@ -243,22 +245,35 @@ class SimCluster:
             # a time-sliced node is its own pool: its plugin advertises the slice resource (as the
             # daemon does with --time-slices), and amd.com/gpu means whole GPUs everywhere
             res = self.contract.slice_resource if slices_per_gpu(topo) > 1 else self.resource
-            plugin_api = self._as("plugin", name)
-            plugin = DevicePluginServer(topo, PluginConfig(resource_name=res, socket_dir=sockdir, node_name=name,
-                                                           contract=self.contract, dev_root=dev_root,
-                                                           device_specs=self.device_specs,
-                                                           prestart_validate=self.prestart_validate,
-                                                           pod_resources_socket=kubelet.pod_resources_socket,
-                                                           reconcile_interval=self.reconcile_interval,
-                                                           share_guard=self.share_guard,
-                                                           guard_dir=os.path.join(self._root, f"vgpu{i}"),
-                                                           topology_manager=tm if self.publish_topology_manager else None),
-                                        api=plugin_api, validate_fn=self.validate_fn)
+            self._plugin_args[name] = (i, copy.deepcopy(topo), sockdir, dev_root, kubelet, res, tm)  # as discovered
+            plugin = self._make_plugin(name, topo)
             plugin.start()
             kubelet.wait_for(res)
             self.nodes[name] = _Node(name, topo, sockdir, kubelet, plugin, res)
         self.start_extender()
         return self
+
+    def _make_plugin(self, name: str, topo: Optional[Topology] = None) -> DevicePluginServer:
+        """The node's plugin; a restarted one re-discovers the node (a pristine copy of its topology)."""
+        i, pristine, sockdir, dev_root, kubelet, res, tm = self._plugin_args[name]
+        return DevicePluginServer(topo if topo is not None else copy.deepcopy(pristine), PluginConfig(
+            resource_name=res, socket_dir=sockdir, node_name=name, contract=self.contract, dev_root=dev_root,
+            device_specs=self.device_specs, prestart_validate=self.prestart_validate,
+            pod_resources_socket=kubelet.pod_resources_socket, reconcile_interval=self.reconcile_interval,
+            share_guard=self.share_guard, guard_dir=os.path.join(self._root, f"vgpu{i}"),
+            topology_manager=tm if self.publish_topology_manager else None),
+            api=self._as("plugin", name), validate_fn=self.validate_fn)
+
+    def restart_plugin(self, name: str) -> None:
+        """The node's device plugin process restarts: a new one with no memory of admissions, which
+        reads its node (the operator's cordon) before serving, as the daemon does, and re-registers."""
+        n = self.nodes[name]
+        n.plugin.stop()
+        plugin = self._make_plugin(name)
+        plugin.poll_node()
+        plugin.start()
+        n.kubelet.wait_for(n.resource)
+        n.plugin = plugin
 
     def _as(self, who: str, node: str = ""):
         """The apiserver as the deploy ServiceAccount of ``who`` (plugin / extender) sees it."""

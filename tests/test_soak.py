@@ -1,6 +1,7 @@
 """Every round-6 feature at once, under random churn: nodes whose kubelets run different Topology
 Manager policies, multi-container / init / sidecar pods, operator GPU cordons coming and going, the
-extender on its informer, every component as its deploy ServiceAccount.  Invariants after every
+extender on its informer, every component as its deploy ServiceAccount, and extender and device
+plugin restarts in between.  Invariants after every
 step: a bound pod is admitted (no kubelet rejection) with exactly the GROUP the extender bound
 (reconcile off), no new pod lands on a cordoned GPU, no request is refused by RBAC."""
 import random
@@ -56,7 +57,12 @@ def test_everything_at_once_under_churn(seed):
             ev = rng.random()
             if live and ev < 0.3:
                 c.complete(live.pop(rng.randrange(len(live))))
-            elif ev < 0.38:  # the operator cordons or releases a GPU somewhere
+            elif ev < 0.34:  # a component restarts: the extender (stateless) or a node's plugin
+                if rng.random() < 0.5:
+                    c.restart_extender()
+                else:
+                    c.restart_plugin(rng.choice(list(tms)))
+            elif ev < 0.42:  # the operator cordons or releases a GPU somewhere
                 node = rng.choice(list(tms))
                 want = "" if cordoned.get(node) else str(rng.randrange(nodes[node].n))
                 c.api.patch_node(node, annotations={C.cordon_key: want})
