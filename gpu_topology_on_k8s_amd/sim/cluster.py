@@ -192,8 +192,13 @@ class SimCluster:
                  node_labels: Optional[Dict[str, Dict[str, str]]] = None, device_specs: str = "strict",
                  prestart_validate: bool = False, validate_fn=None, reconcile_interval: float = 0.0,
                  informer: bool = False, share_guard: str = "preload", rbac: bool = False,
-                 topology_manager=None, publish_topology_manager: bool = True):
+                 topology_manager=None, publish_topology_manager: bool = True, replicas: int = 1):
         self.resource = resource
+        # extender replicas (kube-scheduler HA: one extender per control-plane node, each with its own
+        # cache); the mini scheduler sends consecutive pods to them in turn
+        self.replicas = max(1, int(replicas))
+        self._extra: List[Tuple[TopologyExtender, "HttpExtender", object]] = []
+        self._turn = 0
         # the kubelets' Topology Manager (placement/numa_align.TopologyManager, one for every node or a
         # dict per node); the plugins publish it unless `publish_topology_manager` is off (an operator
         # who did not tell the plugin: the extender then places as if the policy were none)
@@ -290,13 +295,23 @@ class SimCluster:
         return view
 
     def start_extender(self) -> None:
-        self.extender = TopologyExtender(self._as("extender"), self.ext_cfg)
+        self.extender, self.http, self.informer = self._new_replica()
+        self._extra = [self._new_replica() for _ in range(self.replicas - 1)]
+
+    @property
+    def extenders(self) -> List[TopologyExtender]:
+        return [self.extender] + [e for e, _, _ in self._extra]
+
+    def _new_replica(self):
+        ext = TopologyExtender(self._as("extender"), self.ext_cfg)
+        inf = None
         if self.use_informer:
-            self.informer = self.extender.cache.make_informer(watch_timeout=5.0, backoff=0.1, page_size=50)
-            self.informer.start()
-            self.informer.wait_synced(10.0)
-        self.http = HttpExtender(self.extender)
-        self.http.start()
+            inf = ext.cache.make_informer(watch_timeout=5.0, backoff=0.1, page_size=50)
+            inf.start()
+            inf.wait_synced(10.0)
+        http = HttpExtender(ext)
+        http.start()
+        return ext, http, inf
 
     def _stop_extender(self) -> None:
         if self.http is not None:
@@ -305,6 +320,11 @@ class SimCluster:
         if self.informer is not None:
             self.informer.stop()
             self.informer = None
+        for _, http, inf in self._extra:
+            http.stop()
+            if inf is not None:
+                inf.stop()
+        self._extra = []
 
     def restart_extender(self) -> None:
         """Stateless restart: the new process rebuilds from annotations."""
@@ -364,28 +384,36 @@ class SimCluster:
                 out.append(name)
         return out
 
-    def _post(self, verb: str, body: dict):
-        assert self.http is not None
-        return self._client.post(f"{self.http.url}/{verb}", body)
+    def _post(self, verb: str, body: dict, http: Optional["HttpExtender"] = None):
+        http = http or self.http
+        assert http is not None
+        return self._client.post(f"{http.url}/{verb}", body)
+
+    def _next_http(self) -> "HttpExtender":
+        """The replica this pod goes to: the primary, then each extra one in turn."""
+        https = [self.http] + [h for _, h, _ in self._extra]
+        self._turn = (self._turn + 1) % len(https)
+        return https[self._turn]
 
     def schedule_one(self, pod: dict, admit: bool = True) -> ScheduleResult:
         key = pod_key(pod)
         t0 = time.perf_counter()
+        http = self._next_http() if self._extra else self.http  # one replica decides the whole cycle
         cands = self._fits(pod)
         res = ScheduleResult(pod=key, node=None)
         if cands and self.use_filter:
-            fr = self._post("filter", {"Pod": pod, "NodeNames": cands})
+            fr = self._post("filter", {"Pod": pod, "NodeNames": cands}, http)
             cands = fr.get("NodeNames") or []
         if not cands:
             res.error = "no feasible node"
             res.sched_ms = (time.perf_counter() - t0) * 1e3
             self.history.append(res)
             return res
-        prio = self._post("sort", {"Pod": pod, "NodeNames": cands})
+        prio = self._post("sort", {"Pod": pod, "NodeNames": cands}, http)
         best = max(prio, key=lambda h: (h["Score"], -cands.index(h["Host"])))
         md = meta(pod)
         br = self._post("bind", {"PodName": md["name"], "PodNamespace": md.get("namespace", "default"), "PodUID": md.get("uid", ""),
-                                 "Node": best["Host"]})
+                                 "Node": best["Host"]}, http)
         res.sched_ms = (time.perf_counter() - t0) * 1e3
         if br.get("Error"):
             res.error = br["Error"]

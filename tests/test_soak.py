@@ -1,7 +1,7 @@
 """Every round-6 feature at once, under random churn: nodes whose kubelets run different Topology
 Manager policies, multi-container / init / sidecar pods, operator GPU cordons coming and going, the
-extender on its informer, every component as its deploy ServiceAccount, and extender and device
-plugin restarts in between.  Invariants after every
+extender as two replicas (kube-scheduler HA) each on its own informer, every component as its deploy
+ServiceAccount, and extender and device plugin restarts in between.  Invariants after every
 step: a bound pod is admitted (no kubelet rejection) with exactly the GROUP the extender bound
 (reconcile off), no new pod lands on a cordoned GPU, no request is refused by RBAC."""
 import random
@@ -51,7 +51,7 @@ def test_everything_at_once_under_churn(seed):
     tms = {"plain": TopologyManager(), "aligned": TopologyManager("best-effort", "container"),
            "strict": TopologyManager("single-numa-node", "pod"), "sliced": TopologyManager("best-effort", "container")}
     nodes = {n: (time_slice(fx.f7_mi355x(), 2) if n == "sliced" else fx.f7_mi355x()) for n in tms}
-    with SimCluster(nodes, topology_manager=tms, informer=True, rbac=True) as c:
+    with SimCluster(nodes, topology_manager=tms, informer=True, rbac=True, replicas=2) as c:
         live, cordoned, placed = [], {}, 0
         for i in range(150):
             ev = rng.random()
@@ -70,8 +70,8 @@ def test_everything_at_once_under_churn(seed):
                 cordoned[node] = want
             # the informer delivers what just changed before the next decision
             assert _wait(lambda: all(
-                {g.index for g in c.extender.cache.get(n, sync=False).topology.gpus if not g.healthy}
-                == (_physical(nodes[n], int(cordoned[n])) if cordoned.get(n) else set()) for n in tms))
+                {g.index for g in e.cache.get(n, sync=False).topology.gpus if not g.healthy}
+                == (_physical(nodes[n], int(cordoned[n])) if cordoned.get(n) else set()) for n in tms for e in c.extenders))
             name = f"p{i}"
             if rng.random() < 0.2:  # time slices: one pool of their own (the sliced node)
                 c.submit(name, **rng.choice([{"gpus": 1}, {"gpus": 2}, {"gpus": 0, "split": [1, 1]}]), slices=True)
