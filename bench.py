@@ -641,7 +641,9 @@ def main(argv=None) -> int:
                 torch.cuda.set_device(device)  # the second communicator switched this thread's device
     default_ab = None
     want_default = args.ab_default == "on" or (args.ab_default == "auto" and bool(choice.default))
-    if want_default and choice.default and (cpu or (choice.default_hip and runner.comm is not None)) \
+    if want_default and choice.default and worst_ab and not worst_ab.get("error") and sorted(choice.default) == sorted(choice.worst or []):
+        default_ab = dict(worst_ab, same_as="worst")  # the kubelet's choice is the worst subset: measured once
+    elif want_default and choice.default and (cpu or (choice.default_hip and runner.comm is not None)) \
             and ph.allow("ab_default", comm_s + (max(1, args.warmup // 2) + min(args.steps, 20) + 1) * step_s, agree):
         try:  # supplementary, like the worst-subset arm
             default_ab = ph.run("ab_default", measure_subset, env, "default", choice.default, choice.default_hip,

@@ -93,6 +93,9 @@ def main() -> int:
             pl = "p2p-off"  # k == node size: best == worst device set; emulate the worst link class instead
         if pl == "default" and "best" in res and not res["best"].get("default_devices"):
             continue  # the kubelet would hand out the chosen devices: nothing to compare
+        if pl == "default" and "worst" in res and sorted(res["best"].get("default_devices") or []) == sorted(res["worst"].get("devices") or []):
+            res["default"] = dict(res["worst"], placement="default", same_as="worst")  # the same devices: measured once
+            continue
         if pl in res:
             continue
         r = run(pl, a)
@@ -122,6 +125,7 @@ def main() -> int:
     dflt = res.get("default", {})
     summary["default_devices"] = res["best"].get("default_devices")
     summary["default_same_as_best"] = not res["best"].get("default_devices")
+    summary["default_same_as_worst"] = dflt.get("same_as") == "worst"
     summary["default_throughput"] = dflt.get("throughput")
     if dflt.get("throughput"):
         summary["speedup_vs_default"] = summary["best_throughput"] / dflt["throughput"]

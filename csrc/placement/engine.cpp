@@ -18,6 +18,7 @@ Engine::Engine(const Problem& p, const Policy& pol) : p_(p), pol_(pol) {
   if (p_.free.size() != n) throw std::invalid_argument("free must have n entries");
   if (p_.access.empty()) p_.access.assign(n, 0.0);
   if (p_.access.size() != n) throw std::invalid_argument("access must have n entries");
+  if (!p_.deficit.empty() && p_.deficit.size() != n * n) throw std::invalid_argument("deficit must be empty or n*n");
   for (const auto& raw : p_.levels) {
     if (raw.size() != n) throw std::invalid_argument("every level needs n group ids");
     Level lv;
@@ -91,6 +92,9 @@ double Engine::evaluate(const std::vector<int>& ids, Terms* terms) const {
       }
     t.comm = 2.0 * s / ((double)k * (k - 1));
     t.bott = mx;
+    if (!p_.deficit.empty())
+      for (int a = 0; a < k; ++a)
+        for (int b = a + 1; b < k; ++b) t.deficit = std::max(t.deficit, p_.deficit[(size_t)ids[a] * n + ids[b]]);
   } else {
     t.comm = t.bott = 1.0;
   }
@@ -119,7 +123,8 @@ double Engine::evaluate(const std::vector<int>& ids, Terms* terms) const {
   t.access = k ? acc / k : 0.0;
   t.nicdef = k ? nic_deficit(ids.data(), k) : 0.0;
   if (terms) *terms = t;
-  return t.comm + pol_.w_nic * t.nicdef + pol_.w_bottleneck * (t.bott - t.comm) + pol_.w_span * t.span + pol_.w_frag * t.frag + pol_.w_fit * t.fit + pol_.w_access * t.access;
+  return t.comm + pol_.w_nic * t.nicdef + pol_.w_bottleneck * (t.bott - t.comm) + pol_.w_span * t.span + pol_.w_frag * t.frag + pol_.w_fit * t.fit + pol_.w_access * t.access +
+         pol_.w_link_deficit * t.deficit;
 }
 
 void Engine::greedy(int k, const std::vector<int>& F, std::vector<int>* best, double* best_j, bool maximise,
@@ -247,10 +252,13 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
       if (!p_.nic.empty() && p_.nic[i] != p_.nic[j]) return false;
       const double* ri = &p_.cost[(size_t)i * n];
       const double* rj = &p_.cost[(size_t)j * n];
+      const double* di = p_.deficit.empty() ? nullptr : &p_.deficit[(size_t)i * n];
+      const double* dj = p_.deficit.empty() ? nullptr : &p_.deficit[(size_t)j * n];
       for (int c = 0; c < m; ++c) {
         const int x = F[c];
         if (x == i || x == j) continue;
         if (std::fabs(ri[x] - rj[x]) > 1e-12 * std::max(1.0, std::fabs(ri[x]))) return false;
+        if (di && std::fabs(di[x] - dj[x]) > 1e-12 * std::max(1.0, std::fabs(di[x]))) return false;
       }
       return true;
     };
@@ -271,6 +279,8 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
   for (size_t l = 0; l < lv_.size(); ++l) take[l].assign(lv_[l].size.size(), 0);
   std::vector<std::vector<double>> cross(k + 1, std::vector<double>(m, 0.0));  // cross[d][c] = sum cost(F[c], P_d)
   std::vector<std::vector<double>> xmax(k + 1, std::vector<double>(m, 0.0));   // xmax[d][c] = max cost(F[c], P_d)
+  const bool has_def = !p_.deficit.empty();
+  std::vector<std::vector<double>> dmax(has_def ? k + 1 : 0, std::vector<double>(m, 0.0));  // dmax[d][c] = max deficit(F[c], P_d)
   std::vector<double> scratch(m);
 
   double best_j = std::numeric_limits<double>::infinity();
@@ -281,7 +291,7 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
 
   // Leaf objective from the incremental state.
   const double wb = pol_.w_bottleneck;
-  auto leaf_objective = [&](double pairsum, double pairmax, double accsum) {
+  auto leaf_objective = [&](double pairsum, double pairmax, double accsum, double defmax) {
     double comm = k >= 2 ? pairsum / pairs_k : 1.0;
     double bott = k >= 2 ? pairmax : 1.0;
     double span = 0, frag = 0, fit = 0;
@@ -316,7 +326,7 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
       nicdef = nic_deficit(ids, k);
     }
     return comm + wb * (bott - comm) + pol_.w_span * span + pol_.w_frag * frag + pol_.w_fit * fit +
-           pol_.w_access * (accsum / k) + pol_.w_nic * nicdef;
+           pol_.w_access * (accsum / k) + pol_.w_nic * nicdef + pol_.w_link_deficit * (k >= 2 ? defmax : 0.0);
   };
 
   // Large search spaces: seed the incumbent with greedy + 1-swap so pruning bites from the start.
@@ -396,12 +406,13 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
     for (int dev : g) best_pos.push_back((int)(std::lower_bound(F.begin(), F.end(), dev) - F.begin()));
   }
 
-  std::function<void(int, double, double, double)> dfs = [&](int start, double pairsum, double pairmax, double accsum) {
+  std::function<void(int, double, double, double, double)> dfs = [&](int start, double pairsum, double pairmax, double accsum,
+                                                                    double defmax) {
     if (aborted) return;
     const int d = (int)chosen.size();
     if (d == k) {
       ++leaves;
-      double j = leaf_objective(pairsum, pairmax, accsum);
+      double j = leaf_objective(pairsum, pairmax, accsum, defmax);
       if (j < best_j - kEps) {
         best_j = j;
         best_pos = chosen;
@@ -455,7 +466,9 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
         }
         span_lb += std::max(0, touched[l] + extra - mg[l]);
       }
-      double lb = (1.0 - wb) * comm_lb + wb * bott_lb + pol_.w_span * span_lb + pol_.w_access * ((accsum + r * amin) / k);
+      // the deficit of the pairs chosen so far can only grow
+      double lb = (1.0 - wb) * comm_lb + wb * bott_lb + pol_.w_span * span_lb + pol_.w_access * ((accsum + r * amin) / k) +
+                  pol_.w_link_deficit * (k >= 2 ? defmax : 0.0);
       if (collect_ties ? lb > best_j + kEps : lb >= best_j - kEps) return;
     }
     for (int c = start; c <= m - r; ++c) {
@@ -470,14 +483,19 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
       }
       const double add_pairs = cross[d][c];
       const double new_max = d > 0 ? std::max(pairmax, xmax[d][c]) : pairmax;
+      const double new_def = has_def && d > 0 ? std::max(defmax, dmax[d][c]) : defmax;
       if (d + 1 < k) {
         const double* row = &p_.cost[(size_t)dev * n];
         for (int q = c + 1; q < m; ++q) {
           cross[d + 1][q] = cross[d][q] + row[F[q]];
           xmax[d + 1][q] = d > 0 ? std::max(xmax[d][q], row[F[q]]) : row[F[q]];
         }
+        if (has_def) {
+          const double* drow = &p_.deficit[(size_t)dev * n];
+          for (int q = c + 1; q < m; ++q) dmax[d + 1][q] = d > 0 ? std::max(dmax[d][q], drow[F[q]]) : drow[F[q]];
+        }
       }
-      dfs(c + 1, pairsum + add_pairs, new_max, accsum + p_.access[dev]);
+      dfs(c + 1, pairsum + add_pairs, new_max, accsum + p_.access[dev], new_def);
       // pop
       for (size_t l = 0; l < lv_.size(); ++l) {
         int g = lv_[l].gid[dev];
@@ -488,7 +506,7 @@ Result Engine::select(int k, uint64_t node_limit, bool collect_ties, size_t max_
       if (aborted) return;
     }
   };
-  dfs(0, 0.0, -std::numeric_limits<double>::infinity(), 0.0);
+  dfs(0, 0.0, -std::numeric_limits<double>::infinity(), 0.0, 0.0);
 
   std::vector<int> ids;
   for (int pos : best_pos) ids.push_back(F[pos]);

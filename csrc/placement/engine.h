@@ -16,6 +16,8 @@
 //   frag = sum_levels #pristine groups left partially used
 //   fit  = sum_levels sum_touched free_after/size
 //   acc  = mean access cost of S
+//   + w_link_deficit * deficit: the largest Problem::deficit over the pairs of S (a link's shortfall
+//     against the best link of its class on the node, beyond a dead band; empty = 0 everywhere)
 //   + w_nic * nicdef (only with Problem::nic): NIC domains (device -> its nearest RDMA NIC) a
 //     multi-node pod could use but S leaves out, min(k, domains with a free device) - domains touched
 // Enumeration is lexicographic over free device ids and a candidate replaces the incumbent only if
@@ -33,6 +35,7 @@ constexpr double kEps = 1e-9;
 struct Policy {
   double w_span = 0.5, w_frag = 0.25, w_fit = 0.05, w_access = 0.1, w_bottleneck = 0.4;  // w_bottleneck in [0, 1]
   double w_nic = 1.0;
+  double w_link_deficit = 1.0;
 };
 
 struct Problem {
@@ -42,10 +45,11 @@ struct Problem {
   std::vector<std::vector<int>> levels;   // per level: group id per device (any ints)
   std::vector<double> access;             // n
   std::vector<int> nic;                   // empty, or n: NIC domain per device (-1 = none)
+  std::vector<double> deficit;            // empty (all 0), or n*n row-major, symmetric, >= 0
 };
 
 struct Terms {
-  double comm = 0, bott = 0, span = 0, frag = 0, fit = 0, access = 0, nicdef = 0;
+  double comm = 0, bott = 0, span = 0, frag = 0, fit = 0, access = 0, nicdef = 0, deficit = 0;
 };
 
 struct Result {

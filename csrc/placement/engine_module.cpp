@@ -16,10 +16,12 @@ using namespace gtk;
 
 namespace {
 
+using DArray = py::array_t<double, py::array::c_style | py::array::forcecast>;
+
 Problem make_problem(py::array_t<double, py::array::c_style | py::array::forcecast> cost,
                      py::array_t<bool, py::array::c_style | py::array::forcecast> free_mask,
                      const std::vector<std::vector<int>>& levels,
-                     py::array_t<double, py::array::c_style | py::array::forcecast> access) {
+                     py::array_t<double, py::array::c_style | py::array::forcecast> access, DArray deficit = DArray()) {
   Problem p;
   auto c = cost.unchecked<2>();
   if (c.shape(0) != c.shape(1)) throw std::invalid_argument("cost must be square");
@@ -33,6 +35,10 @@ Problem make_problem(py::array_t<double, py::array::c_style | py::array::forceca
   auto a = access.unchecked<1>();
   if (a.shape(0) != 0 && a.shape(0) != p.n) throw std::invalid_argument("access length != n");
   p.access.assign(access.data(), access.data() + a.shape(0));
+  if (deficit.size() > 0) {
+    if (deficit.ndim() != 2 || deficit.shape(0) != p.n || deficit.shape(1) != p.n) throw std::invalid_argument("deficit must be n x n");
+    p.deficit.assign(deficit.data(), deficit.data() + (size_t)p.n * p.n);
+  }
   return p;
 }
 
@@ -53,11 +59,13 @@ py::dict to_dict(const Result& r, double us) {
   t["fit"] = r.terms.fit;
   t["access"] = r.terms.access;
   t["nic_deficit"] = r.terms.nicdef;
+  t["link_deficit"] = r.terms.deficit;
   d["terms"] = t;
   return d;
 }
 
-Policy make_policy(double w_span, double w_frag, double w_fit, double w_access, double w_bottleneck, double w_nic = 1.0) {
+Policy make_policy(double w_span, double w_frag, double w_fit, double w_access, double w_bottleneck, double w_nic = 1.0,
+                   double w_link_deficit = 1.0) {
   if (!(w_bottleneck >= 0.0 && w_bottleneck <= 1.0)) throw std::invalid_argument("w_bottleneck must be in [0, 1]");
   Policy pol;
   pol.w_bottleneck = w_bottleneck;
@@ -66,6 +74,7 @@ Policy make_policy(double w_span, double w_frag, double w_fit, double w_access, 
   pol.w_frag = w_frag;
   pol.w_fit = w_fit;
   pol.w_access = w_access;
+  pol.w_link_deficit = w_link_deficit;
   return pol;
 }
 
@@ -79,15 +88,15 @@ PYBIND11_MODULE(_placement, m) {
          py::array_t<bool, py::array::c_style | py::array::forcecast> free_mask, const std::vector<std::vector<int>>& levels,
          py::array_t<double, py::array::c_style | py::array::forcecast> access, int k, double w_span, double w_frag,
          double w_fit, double w_access, uint64_t node_limit, bool collect_ties, double w_bottleneck,
-         const std::vector<int>& nic, double w_nic) {
-        Problem p = make_problem(cost, free_mask, levels, access);
+         const std::vector<int>& nic, double w_nic, DArray deficit, double w_link_deficit) {
+        Problem p = make_problem(cost, free_mask, levels, access, deficit);
         p.nic = nic;
         Result r;
         double us = 0;
         {
           py::gil_scoped_release nogil;
           auto t0 = std::chrono::steady_clock::now();
-          Engine e(p, make_policy(w_span, w_frag, w_fit, w_access, w_bottleneck, w_nic));
+          Engine e(p, make_policy(w_span, w_frag, w_fit, w_access, w_bottleneck, w_nic, w_link_deficit));
           r = e.select(k, node_limit, collect_ties);
           us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
         }
@@ -98,22 +107,23 @@ PYBIND11_MODULE(_placement, m) {
       py::arg("cost"), py::arg("free"), py::arg("levels"), py::arg("access"), py::arg("k"), py::arg("w_span") = 0.5,
       py::arg("w_frag") = 0.25, py::arg("w_fit") = 0.05, py::arg("w_access") = 0.1,
       py::arg("node_limit") = (uint64_t)2000000, py::arg("collect_ties") = false,
-      py::arg("w_bottleneck") = 0.4, py::arg("nic") = std::vector<int>{}, py::arg("w_nic") = 1.0);
+      py::arg("w_bottleneck") = 0.4, py::arg("nic") = std::vector<int>{}, py::arg("w_nic") = 1.0,
+      py::arg("deficit") = DArray(), py::arg("w_link_deficit") = 1.0);
   m.def(
       "worst",
       [](py::array_t<double, py::array::c_style | py::array::forcecast> cost,
          py::array_t<bool, py::array::c_style | py::array::forcecast> free_mask, const std::vector<std::vector<int>>& levels,
          py::array_t<double, py::array::c_style | py::array::forcecast> access, int k, double w_span, double w_frag,
          double w_fit, double w_access, uint64_t node_limit, double w_bottleneck,
-         const std::vector<int>& nic, double w_nic) {
-        Problem p = make_problem(cost, free_mask, levels, access);
+         const std::vector<int>& nic, double w_nic, DArray deficit, double w_link_deficit) {
+        Problem p = make_problem(cost, free_mask, levels, access, deficit);
         p.nic = nic;
         Result r;
         double us = 0;
         {
           py::gil_scoped_release nogil;
           auto t0 = std::chrono::steady_clock::now();
-          Engine e(p, make_policy(w_span, w_frag, w_fit, w_access, w_bottleneck, w_nic));
+          Engine e(p, make_policy(w_span, w_frag, w_fit, w_access, w_bottleneck, w_nic, w_link_deficit));
           r = e.worst(k, node_limit);
           us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
         }
@@ -122,17 +132,17 @@ PYBIND11_MODULE(_placement, m) {
       py::arg("cost"), py::arg("free"), py::arg("levels"), py::arg("access"), py::arg("k"), py::arg("w_span") = 0.5,
       py::arg("w_frag") = 0.25, py::arg("w_fit") = 0.05, py::arg("w_access") = 0.1,
       py::arg("node_limit") = (uint64_t)2000000, py::arg("w_bottleneck") = 0.4, py::arg("nic") = std::vector<int>{},
-      py::arg("w_nic") = 1.0);
+      py::arg("w_nic") = 1.0, py::arg("deficit") = DArray(), py::arg("w_link_deficit") = 1.0);
   m.def(
       "evaluate",
       [](py::array_t<double, py::array::c_style | py::array::forcecast> cost,
          py::array_t<bool, py::array::c_style | py::array::forcecast> free_mask, const std::vector<std::vector<int>>& levels,
          py::array_t<double, py::array::c_style | py::array::forcecast> access, const std::vector<int>& ids,
          double w_span, double w_frag, double w_fit, double w_access, double w_bottleneck,
-         const std::vector<int>& nic, double w_nic) {
-        Problem p = make_problem(cost, free_mask, levels, access);
+         const std::vector<int>& nic, double w_nic, DArray deficit, double w_link_deficit) {
+        Problem p = make_problem(cost, free_mask, levels, access, deficit);
         p.nic = nic;
-        Engine e(p, make_policy(w_span, w_frag, w_fit, w_access, w_bottleneck, w_nic));
+        Engine e(p, make_policy(w_span, w_frag, w_fit, w_access, w_bottleneck, w_nic, w_link_deficit));
         Result r;
         r.ids = ids;
         r.objective = e.evaluate(ids, &r.terms);
@@ -141,6 +151,7 @@ PYBIND11_MODULE(_placement, m) {
       },
       py::arg("cost"), py::arg("free"), py::arg("levels"), py::arg("access"), py::arg("ids"), py::arg("w_span") = 0.5,
       py::arg("w_frag") = 0.25, py::arg("w_fit") = 0.05, py::arg("w_access") = 0.1, py::arg("w_bottleneck") = 0.4,
-      py::arg("nic") = std::vector<int>{}, py::arg("w_nic") = 1.0);
+      py::arg("nic") = std::vector<int>{}, py::arg("w_nic") = 1.0, py::arg("deficit") = DArray(),
+      py::arg("w_link_deficit") = 1.0);
   m.attr("EPS") = kEps;
 }

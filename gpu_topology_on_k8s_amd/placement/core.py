@@ -26,6 +26,11 @@ The objective for a candidate set S (|S| = k) is::
     frag  = sum over levels of #pristine groups left partially used
     fit   = sum over levels and touched groups of free_after/size  (best-fit packing)
     acc   = mean per-device access cost (CPU/NUMA affinity hint, design.md:144-145, Gaia B6)
+    + w_link_deficit * deficit: how far the set's worst link falls below the best link of its own
+      class (link type, hops, on-package or not) on this node, beyond a LINK_DEFICIT_BAND dead band;
+      0 on a healthy (banded) node.  A degraded xGMI link slows every collective that crosses it
+      (a 2- or 3-GPU ring uses every pair), which NUMA locality (span) or packing do not make up for
+      once it is measurably slow
     + w_nic * nicdef, multi-node pods only (``Problem.nic``): NIC domains (device -> its nearest RDMA
       NIC) the set leaves out, min(k, domains with a free device) - domains touched.  A 2-GPU pod of
       a multi-node job on a node with one NIC per socket gets twice the network bandwidth across the
@@ -50,6 +55,9 @@ __all__ = ["PlacementPolicy", "Placement", "Problem", "select", "worst", "select
            "score_from_objective", "node_packing_term", "NoFeasiblePlacement"]
 
 EPS = 1e-9
+# a link costlier than the best link of its class by less than this is noise (measurement spread,
+# an unbanded matrix): its deficit is 0.  Beyond it the deficit is the excess over the band
+LINK_DEFICIT_BAND = 0.10
 
 
 class NoFeasiblePlacement(RuntimeError):
@@ -63,6 +71,7 @@ class PlacementPolicy:
     w_fit: float = 0.05
     w_access: float = 0.1
     w_bottleneck: float = 0.4  # in [0, 1]: blend of mean and worst link (bench/cluster_trace.py)
+    w_link_deficit: float = 1.0  # per unit of the worst link's shortfall against its class's best (see LINK_DEFICIT_BAND)
     w_nic: float = 1.0  # per NIC domain a multi-node pod leaves unused (only with Problem.nic)
     tie_break: str = "first"  # "first" (deterministic, lowest ids) | "random"
     exact_limit: int = 200_000  # Python path: max subsets enumerated exactly; above -> greedy + local search
@@ -79,6 +88,7 @@ class PlacementPolicy:
     def to_dict(self) -> Dict[str, object]:
         return dict(
             w_span=self.w_span, w_frag=self.w_frag, w_fit=self.w_fit, w_access=self.w_access, w_bottleneck=self.w_bottleneck, w_nic=self.w_nic,
+            w_link_deficit=self.w_link_deficit,
             w_node_fit=self.w_node_fit,
             tie_break=self.tie_break, exact_limit=self.exact_limit, node_limit=self.node_limit,
             partition_aware=self.partition_aware,
@@ -113,6 +123,7 @@ class Problem:
     levels: List[np.ndarray]  # group id per device, innermost level first
     access: np.ndarray  # float[n]
     nic: Optional[np.ndarray] = None  # int[n]: NIC domain per device (-1 none); None = not a multi-node pod
+    deficit: Optional[np.ndarray] = None  # n x n: link shortfall against its class's best (None = all 0)
 
     @classmethod
     def from_topology(cls, topo: Topology, used: Sequence[int] = (), access: Optional[Sequence[float]] = None,
@@ -136,11 +147,31 @@ class Problem:
                 cost[same] = float(np.median(cost[cross]))
         levels.append(topo.numa)
         acc = np.zeros(n) if access is None else np.asarray(access, dtype=np.float64)
-        return cls(cost=cost, free=free, levels=levels, access=acc, nic=nic_domains(topo) if nic_aware else None)
+        return cls(cost=cost, free=free, levels=levels, access=acc, nic=nic_domains(topo) if nic_aware else None,
+                   deficit=link_deficit(topo, cost))
 
     @property
     def n(self) -> int:
         return len(self.free)
+
+
+def link_deficit(topo: Topology, cost: np.ndarray) -> Optional[np.ndarray]:
+    """Per pair: how far its cost exceeds the cheapest link of the same class on this node (link type,
+    hops, both ends on one package or not), as a fraction beyond LINK_DEFICIT_BAND; None when no
+    link falls short (the common case: a healthy node, or costs from link classes only)."""
+    n = topo.n
+    if n < 2:
+        return None
+    same = topo.physical[:, None] == topo.physical[None, :]
+    key = (np.asarray(topo.link_type, dtype=np.int64) * 1024 + np.asarray(topo.hops, dtype=np.int64) * 2 + same)
+    c = np.asarray(cost, dtype=np.float64)
+    ok = np.isfinite(c) & (c > 0) & ~np.eye(n, dtype=bool)
+    out = np.zeros((n, n))
+    for k in np.unique(key[ok]):
+        m = ok & (key == k)
+        best = float(c[m].min())
+        out[m] = np.maximum(0.0, c[m] / best - 1.0 - LINK_DEFICIT_BAND)
+    return out if out.any() else None
 
 
 def nic_domains(topo: Topology) -> Optional[np.ndarray]:
@@ -215,14 +246,18 @@ def evaluate(p: Problem, ids: Sequence[int], policy: PlacementPolicy = Placement
                 frag += 1
             fit += after / size[g]
     acc = float(np.mean(p.access[ids])) if k else 0.0
+    dft = 0.0
+    if p.deficit is not None and k >= 2:
+        dft = float(p.deficit[np.ix_(ids, ids)].max())
     nicdef = 0.0
     if p.nic is not None and k:
         domains = {int(d) for d, f in zip(p.nic, p.free) if f and d >= 0}
         touched = {int(p.nic[i]) for i in ids if p.nic[i] >= 0}
         nicdef = float(max(0, min(k, len(domains)) - len(touched)))
     j = (comm + policy.w_bottleneck * (bott - comm) + policy.w_span * span + policy.w_frag * frag
-         + policy.w_fit * fit + policy.w_access * acc + policy.w_nic * nicdef)
-    return j, {"comm": comm, "bottleneck": bott, "nic_deficit": nicdef, "span": span, "frag": frag, "fit": fit, "access": acc}
+         + policy.w_fit * fit + policy.w_access * acc + policy.w_nic * nicdef + policy.w_link_deficit * dft)
+    return j, {"comm": comm, "bottleneck": bott, "nic_deficit": nicdef, "span": span, "frag": frag, "fit": fit, "access": acc,
+               "link_deficit": dft}
 
 
 def _greedy_local(p: Problem, k: int, policy: PlacementPolicy, stats) -> Tuple[List[int], float]:
@@ -272,21 +307,28 @@ def _native_engine():
         return None
 
 
+def _deficit_kw(p: Problem, policy: PlacementPolicy) -> Dict[str, object]:
+    """The link-deficit matrix and weight for the native engine (an empty matrix: no link falls short)."""
+    d = np.zeros((0, 0)) if p.deficit is None else np.ascontiguousarray(p.deficit, dtype=np.float64)
+    return {"deficit": d, "w_link_deficit": policy.w_link_deficit}
+
+
 def _select_native(mod, p: Problem, k: int, policy: PlacementPolicy, rng: Optional[random.Random] = None) -> Placement:
     args = (np.ascontiguousarray(p.cost, dtype=np.float64), np.ascontiguousarray(p.free, dtype=bool),
             [lv.astype(np.int64).tolist() for lv in p.levels], np.ascontiguousarray(p.access, dtype=np.float64))
     w = (policy.w_span, policy.w_frag, policy.w_fit, policy.w_access)
     ties = policy.tie_break == "random"
     nic = [] if p.nic is None else [int(x) for x in p.nic]
+    dk = _deficit_kw(p, policy)
     r = mod.select(*args, int(k), *w, int(policy.node_limit), ties, w_bottleneck=policy.w_bottleneck, nic=nic,
-                   w_nic=policy.w_nic)
+                   w_nic=policy.w_nic, **dk)
     if not r["feasible"]:
         raise NoFeasiblePlacement(f"need {k} free devices")
     if ties and len(r["ties"]) > 1:
         # same draw as the Python enumeration: lexicographic tie list, one rng.choice
         pick = list((rng or random).choice(r["ties"]))
         if pick != list(r["ids"]):
-            e = mod.evaluate(*args, pick, *w, w_bottleneck=policy.w_bottleneck, nic=nic, w_nic=policy.w_nic)
+            e = mod.evaluate(*args, pick, *w, w_bottleneck=policy.w_bottleneck, nic=nic, w_nic=policy.w_nic, **dk)
             r = dict(r, ids=pick, objective=e["objective"], terms=e["terms"])
     terms = dict(r["terms"])
     terms["search_nodes"] = float(r["nodes"])
@@ -412,7 +454,7 @@ def worst(topo: Topology, k: int, used: Sequence[int] = (), policy: PlacementPol
                 [lv.astype(np.int64).tolist() for lv in p.levels], np.ascontiguousarray(p.access, dtype=np.float64))
         nic = [] if p.nic is None else [int(x) for x in p.nic]
         r = mod.worst(*args, int(k), policy.w_span, policy.w_frag, policy.w_fit, policy.w_access, int(policy.exact_limit),
-                      w_bottleneck=policy.w_bottleneck, nic=nic, w_nic=policy.w_nic)
+                      w_bottleneck=policy.w_bottleneck, nic=nic, w_nic=policy.w_nic, **_deficit_kw(p, policy))
         terms = dict(r["terms"])
         terms["search_us"] = float(r["micros"])
         return Placement(ids=tuple(int(i) for i in r["ids"]), objective=float(r["objective"]),

@@ -9,7 +9,8 @@ reader of the JSON line must see that before comparing two busBW numbers.  So ev
 reported with:
 
 * the objective ``J`` (placement/core.py ``evaluate``) and the weighted contribution of each term:
-  ``comm`` (mean link cost), ``bottleneck`` (worst link over mean), ``span`` (NUMA / group spread
+  ``comm`` (mean link cost), ``bottleneck`` (worst link over mean), ``link_deficit`` (the worst
+  link's shortfall against the best of its class on the node), ``span`` (NUMA / group spread
   beyond the minimum), ``frag`` (pristine groups broken), ``fit`` (packing), ``access`` (host-core
   affinity), ``nic_deficit``;
 * its links: the slowest measured link GB/s (or the worst link cost when nothing was measured), the
@@ -34,7 +35,7 @@ from .core import PlacementPolicy, Problem, evaluate, score_from_objective
 
 __all__ = ["explain_subsets", "default_subset", "TERMS"]
 
-TERMS = ("comm", "bottleneck", "span", "frag", "fit", "access", "nic_deficit")
+TERMS = ("comm", "bottleneck", "link_deficit", "span", "frag", "fit", "access", "nic_deficit")
 
 
 def default_subset(topo: Topology, k: int, used: Sequence[int] = ()) -> Optional[List[int]]:
@@ -45,6 +46,7 @@ def default_subset(topo: Topology, k: int, used: Sequence[int] = ()) -> Optional
 
 def _weighted(terms: Dict[str, float], policy: PlacementPolicy) -> Dict[str, float]:
     return {"comm": terms["comm"], "bottleneck": policy.w_bottleneck * (terms["bottleneck"] - terms["comm"]),
+            "link_deficit": policy.w_link_deficit * terms.get("link_deficit", 0.0),
             "span": policy.w_span * terms["span"], "frag": policy.w_frag * terms["frag"], "fit": policy.w_fit * terms["fit"],
             "access": policy.w_access * terms["access"], "nic_deficit": policy.w_nic * terms["nic_deficit"]}
 
@@ -92,5 +94,5 @@ def explain_subsets(topo: Topology, subsets: Dict[str, Optional[Sequence[int]]],
         out[f"vs_{name}"] = {"same_devices": sorted(e["ids"]) == sorted(ref["ids"]), "objective_delta": round(e["objective"] - ref["objective"], 6),
                              "separating_terms": {t: delta[t] for t in sep},
                              "predicted_gain": round(gain, 4), "predicted_basis": basis,
-                             "link_terms_separate": any(t in ("comm", "bottleneck") for t in sep)}
+                             "link_terms_separate": any(t in ("comm", "bottleneck", "link_deficit") for t in sep)}
     return out

@@ -285,7 +285,8 @@ def test_partition_aware_switch_on_cpx_node():
 def test_bottleneck_term_avoids_a_slow_link_a_ring_cannot_skip(engine):
     """GPUs 5-7 are taken; links 0-1 and 0-2 run at a third of nominal.  Every ring over {0,1,2,3}
     uses one of them.  The mean pair cost alone (+2/3) keeps the job inside NUMA half 0-3 (crossing
-    to GPU 4 costs w_span + w_frag = 0.75); the bottleneck term moves it to {1,2,3,4}."""
+    to GPU 4 costs w_span + w_frag = 0.75); the bottleneck term, or the link-deficit term, moves it to
+    {1,2,3,4}."""
     if engine == "native" and not available("_placement"):
         pytest.skip("_placement not built")
     t = fx.f7_mi355x(link_gbps=76.5)  # cost 1.0 per nominal link
@@ -294,7 +295,10 @@ def test_bottleneck_term_avoids_a_slow_link_a_ring_cannot_skip(engine):
         bw[a, b] = bw[b, a] = bw[a, b] / 3.0
     t.set_measured_bw(bw, {"method": "synthetic"})
     used = [5, 6, 7]
-    assert set(select(t, 4, used=used, policy=PlacementPolicy(w_bottleneck=0.0), engine=engine).ids) == {0, 1, 2, 3}
+    assert set(select(t, 4, used=used, policy=PlacementPolicy(w_bottleneck=0.0, w_link_deficit=0.0), engine=engine).ids) == {0, 1, 2, 3}
+    # either term alone moves it: the bottleneck (worst pair), or the deficit (worst pair against the best of its class)
+    assert set(select(t, 4, used=used, policy=PlacementPolicy(w_link_deficit=0.0), engine=engine).ids) == {1, 2, 3, 4}
+    assert set(select(t, 4, used=used, policy=PlacementPolicy(w_bottleneck=0.0), engine=engine).ids) == {1, 2, 3, 4}
     pl = select(t, 4, used=used, policy=PlacementPolicy(), engine=engine)
     assert set(pl.ids) == {1, 2, 3, 4}
     assert pl.terms["bottleneck"] == pytest.approx(pl.comm)
@@ -323,3 +327,69 @@ def test_multi_node_pod_spreads_over_nic_domains(engine):
     half = select(t, 2, used=[4, 5, 6, 7], engine=engine, nic_aware=True)
     assert set(half.ids) <= {0, 1, 2, 3} and half.terms["nic_deficit"] == 0
     assert select(fx.f7_mi355x(), 2, engine=engine, nic_aware=True).ids == select(fx.f7_mi355x(), 2, engine=engine).ids
+
+
+def test_a_healthy_node_has_no_link_deficit_and_places_as_before():
+    """The link-deficit term is 0 on a healthy (banded) node, and on one whose costs come from link
+    classes: no placement changes there."""
+    from gpu_topology_on_k8s_amd.placement.core import Problem
+
+    for t in (fx.f7_mi355x(link_gbps=150.0), fx.f7_mi355x(), fx.f8_mi355x_cpx()):
+        assert Problem.from_topology(t).deficit is None
+    t = fx.f7_mi355x(link_gbps=150.0)
+    for k in (1, 2, 3, 4, 5, 8):
+        for used in ([], [0], [4, 5, 6], [1, 2, 6]):
+            if 8 - len(used) < k:
+                continue
+            a = select(t, k, used=used, engine="python")
+            b = select(t, k, used=used, policy=PlacementPolicy(w_link_deficit=0.0), engine="python")
+            assert a.ids == b.ids and a.objective == pytest.approx(b.objective)
+
+
+@pytest.mark.parametrize("engine", ["python", "native"])
+def test_a_degraded_link_outweighs_numa_locality_for_a_pair(engine):
+    """Only GPUs 0, 1 (NUMA 0) and 7 (NUMA 1) are free and link 0-1 runs at 60 %: a 2-GPU pod's one
+    link is its all-reduce's bottleneck, so the healthy cross-NUMA pair wins.  Without the deficit term
+    NUMA locality (span) kept the slow pair."""
+    if engine == "native" and not available("_placement"):
+        pytest.skip("_placement not built")
+    t = fx.f7_degraded(((0, 1, 0.6),))
+    used = [2, 3, 4, 5, 6]
+    pl = select(t, 2, used=used, engine=engine)
+    assert 7 in pl.ids and pl.terms["link_deficit"] == 0.0
+    assert select(t, 2, used=used, policy=PlacementPolicy(w_link_deficit=0.0), engine=engine).ids == (0, 1)
+    assert worst(t, 2, used=used, engine=engine).ids == (0, 1)
+
+
+def test_the_deficit_has_a_dead_band_and_keeps_link_classes_apart():
+    from gpu_topology_on_k8s_amd.placement.core import LINK_DEFICIT_BAND, Problem
+
+    for frac, want in ((0.95, 0.0), (0.85, 1 / 0.85 - 1 - LINK_DEFICIT_BAND), (0.5, 1.0 - LINK_DEFICIT_BAND)):
+        d = Problem.from_topology(fx.f7_degraded(((2, 5, frac),))).deficit
+        got = 0.0 if d is None else float(d[2, 5])
+        assert got == pytest.approx(max(0.0, want), abs=1e-6), frac
+        if d is not None:
+            assert float(np.delete(np.delete(d, [2, 5], 0), [2, 5], 1).max()) == 0.0  # the healthy links: none
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_native_and_python_agree_with_degraded_links(seed):
+    """Random noisy matrices with a few degraded links: the branch-and-bound engine (its deficit bound
+    included) finds the Python enumeration's set and objective."""
+    if not available("_placement"):
+        pytest.skip("_placement not built")
+    rng = np.random.default_rng(seed)
+    t = fx.f7_mi355x(link_gbps=150.0)
+    bw = np.array(t.bw_gbps, dtype=float) * (1 + rng.uniform(-0.04, 0.04, (8, 8)))
+    for _ in range(3):
+        a, b = rng.choice(8, 2, replace=False)
+        bw[a, b] = bw[b, a] = 150.0 * rng.uniform(0.3, 0.85)
+    np.fill_diagonal(bw, np.nan)
+    t.set_measured_bw(bw, {"method": "synthetic"})
+    for k in (2, 3, 4, 6):
+        used = sorted(rng.choice(8, int(rng.integers(0, 8 - k + 1)), replace=False).tolist())
+        a, b = select(t, k, used=used, engine="python"), select(t, k, used=used, engine="native")
+        assert a.ids == b.ids and a.objective == pytest.approx(b.objective), (seed, k, used)
+        assert a.terms["link_deficit"] == pytest.approx(b.terms["link_deficit"])
+        wa, wb = worst(t, k, used=used, engine="python"), worst(t, k, used=used, engine="native")
+        assert wa.objective == pytest.approx(wb.objective)

@@ -3,7 +3,7 @@
 catch it (a mutation-testing pass; README "Mutation testing of the control plane").
 
     python tools/mutants.py                  # every group
-    python tools/mutants.py --only ledger    # one group (ledger, cache, plugin, informer, rbac, numa, cordon, dp, guard,
+    python tools/mutants.py --only ledger    # one group (ledger, cache, plugin, informer, rbac, numa, cordon, objective, dp, guard,
                                              # banding, gaia, repartition, extender, contract)
 
 Each mutant replaces one line (or a few) of a source file, runs the group's tests with pytest-xdist,
@@ -47,6 +47,8 @@ INFORMER = "gpu_topology_on_k8s_amd/k8s/informer.py"
 RBAC = "gpu_topology_on_k8s_amd/k8s/rbac.py"
 NUMA_ALIGN = "gpu_topology_on_k8s_amd/placement/numa_align.py"
 PLUGIN_MAIN = "gpu_topology_on_k8s_amd/deviceplugin/__main__.py"
+CORE = "gpu_topology_on_k8s_amd/placement/core.py"
+ENGINE = "csrc/placement/engine.cpp"
 
 MUTANTS: List[Mutant] = [
     # allocation ledger (cross-extender bind safety)
@@ -157,6 +159,15 @@ MUTANTS: List[Mutant] = [
            "            if False:\n                ids, why = self._choose_aligned("),
     Mutant("numa", SCHED, "                            if tm.active and fraction is None and steps:",
            "                            if False:"),
+    # placement objective: the link-deficit term (Python and the native engine)
+    Mutant("objective", CORE, "        dft = float(p.deficit[np.ix_(ids, ids)].max())", "        dft = 0.0"),
+    Mutant("objective", CORE, "        out[m] = np.maximum(0.0, c[m] / best - 1.0 - LINK_DEFICIT_BAND)",
+           "        out[m] = np.maximum(0.0, c[m] / best - 1.0)"),
+    Mutant("objective", ENGINE, "          for (int q = c + 1; q < m; ++q) dmax[d + 1][q] = d > 0 ? std::max(dmax[d][q], drow[F[q]]) : drow[F[q]];",
+           "          for (int q = c + 1; q < m; ++q) dmax[d + 1][q] = 0.0;"),
+    Mutant("objective", ENGINE, "                  pol_.w_link_deficit * (k >= 2 ? defmax : 0.0);\n      if (collect_ties",
+           "                  0.0;\n      if (collect_ties", equivalent=True,
+           why="a weaker lower bound prunes less; the search stays exact"),
     # operator GPU cordon
     Mutant("cordon", PLUGIN, "                self._holds.setdefault(i, self.CORDON_HOLD)", "                pass"),
     Mutant("cordon", PLUGIN, "            out |= {g.index for g in t.gpus if g.physical == t.gpus[i].physical}", "            out.add(i)"),
@@ -230,6 +241,7 @@ TESTS = {
     "rbac": ["tests/test_rbac.py", "tests/test_config_cli.py"],
     "numa": ["tests/test_topology_manager.py"],
     "cordon": ["tests/test_cordon.py"],
+    "objective": ["tests/test_placement.py", "tests/test_placement_ab.py"],
     "dp": ["tests/test_dp_check.py", "tests/test_llama_dp_cpu.py", "tests/test_checkpoint.py"],
     "guard": ["tests/test_vgpu_guard.py"],
     "banding": ["tests/test_probe_banding.py", "tests/test_probe_checks.py"],
@@ -241,10 +253,11 @@ TESTS = {
 }
 
 GUARD_TARGETS = "vgpu_guard,vgpu_selftest_asan,vgpu_selftest_tsan"
+NATIVE_TARGETS = {GUARD: GUARD_TARGETS, ENGINE: "placement,engine_selftest"}  # mutated sources rebuilt per mutant
 
 
-def _rebuild_guard() -> bool:
-    p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd._native.build", "--only", GUARD_TARGETS], cwd=REPO,
+def _rebuild(path: str) -> bool:
+    p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd._native.build", "--only", NATIVE_TARGETS[path]], cwd=REPO,
                        capture_output=True, text=True, timeout=900)
     return p.returncode == 0
 
@@ -271,7 +284,7 @@ def main() -> int:
             continue
         try:
             open(path, "w").write(src.replace(m.old, m.new, 1))
-            if m.path == GUARD and not _rebuild_guard():
+            if m.path in NATIVE_TARGETS and not _rebuild(m.path):
                 print(f"NOBUILD   [{m.group}] {m.old.strip()[:90]}")
                 continue
             p = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "-n", str(a.n), "-m", "not gpu",
@@ -284,8 +297,8 @@ def main() -> int:
             print(f"{tag}  [{m.group}] {m.old.strip()[:90].replace(chr(10), ' ')}{note}", flush=True)
         finally:
             open(path, "w").write(src)
-    if any(m.path == GUARD for m in todo):
-        _rebuild_guard()
+    for path in sorted({m.path for m in todo if m.path in NATIVE_TARGETS}):
+        _rebuild(path)
     return 1 if bad else 0
 
 
