@@ -253,7 +253,7 @@ TESTS = {
 }
 
 GUARD_TARGETS = "vgpu_guard,vgpu_selftest_asan,vgpu_selftest_tsan"
-NATIVE_TARGETS = {GUARD: GUARD_TARGETS, ENGINE: "placement,engine_selftest"}  # mutated sources rebuilt per mutant
+NATIVE_TARGETS = {GUARD: GUARD_TARGETS, ENGINE: "_placement,engine_selftest"}  # mutated sources rebuilt per mutant
 
 
 def _rebuild(path: str) -> bool:
