@@ -129,7 +129,7 @@ def targets() -> List[Target]:
                ["-fvisibility=default"], pybind=False),
         Target("_placement", [CSRC / "placement" / "engine.cpp", CSRC / "placement" / "engine_module.cpp"], "gxx",
                HERE / f"_placement{EXT}", deps=[CSRC / "placement" / "engine.h"]),
-        # host-only sanitizer build of the engine; run by tests/test_placement_native.py
+        # host-only sanitizer build of the engine; run by tests/test_placement.py
         Target("engine_selftest", [CSRC / "placement" / "engine.cpp", CSRC / "placement" / "engine_selftest.cpp"], "gxx",
                HERE / "bin" / "engine_selftest", ["-g", "-O1", "-fsanitize=address,undefined", "-fno-omit-frame-pointer"],
                deps=[CSRC / "placement" / "engine.h"], pybind=False, shared=False),

@@ -37,7 +37,7 @@ The objective for a candidate set S (|S| = k) is::
       sockets; on a full xGMI mesh that costs its collectives nothing
 
 The C++ engine (``csrc/placement/engine.cpp``) implements the same objective with branch-and-bound;
-``tests/test_placement_native.py`` checks both agree.
+``tests/test_placement.py`` checks both agree (hypothesis: native == Python == brute force).
 """
 from __future__ import annotations
 
