@@ -16,9 +16,11 @@ reported with:
 * its links: the slowest measured link GB/s (or the worst link cost when nothing was measured), the
   link classes and the NUMA nodes it uses;
 * against the chosen subset, the terms that separate the two (largest first) and the **predicted
-  gain**: the chosen subset's slowest link over the other's.  A ring all-reduce moves every byte over
-  every link of its ring, so its busBW follows the slowest one.  The prediction is 1.00 when only
-  host-side terms separate the subsets.
+  gain**: the chosen subset's ring-bound link over the other's.  A ring all-reduce moves every byte
+  over every link of its ring, so its busBW follows the slowest one.  With 2 or 3 devices the ring
+  uses every pair; with 4 or more on a full mesh RCCL orders the ring around a slow link when it can,
+  so the bound is the slowest link of the best ring (``ring_link_gbps``; the model of
+  bench/cluster_trace.py).  The prediction is 1.00 when only host-side terms separate the subsets.
 
 Subsets compared: ``chosen`` (the placement core), ``worst`` (highest objective), and ``default``
 (what the kubelet's device manager hands out with no extender and no preferred allocation: it takes
@@ -26,6 +28,7 @@ the free devices in set order, modelled here as the lowest free indices).
 """
 from __future__ import annotations
 
+import itertools
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -51,19 +54,38 @@ def _weighted(terms: Dict[str, float], policy: PlacementPolicy) -> Dict[str, flo
             "access": policy.w_access * terms["access"], "nic_deficit": policy.w_nic * terms["nic_deficit"]}
 
 
+def _ring_bound(ids: Sequence[int], speed) -> Optional[float]:
+    """The slowest link a ring all-reduce over ``ids`` must use (``speed(a, b)``: higher is faster):
+    every pair for 2-3 devices, else the best ring's slowest link (exhaustive up to 8 devices, every
+    pair beyond that)."""
+    ids = list(ids)
+    if len(ids) < 2:
+        return None
+    if len(ids) <= 3 or len(ids) > 8:
+        return min(speed(a, b) for i, a in enumerate(ids) for b in ids[i + 1:])
+    first, rest = ids[0], ids[1:]
+    return max(min(speed(x, y) for x, y in zip((first,) + perm, perm + (first,)))
+               for perm in itertools.permutations(rest) if perm[0] < perm[-1])
+
+
 def _links(topo: Topology, ids: Sequence[int]) -> Dict[str, object]:
     ids = list(ids)
     pairs = [(a, b) for i, a in enumerate(ids) for b in ids[i + 1:]]
     bw = topo.bw_gbps
-    meas = []
+    gbps: Dict[tuple, float] = {}
     if bw is not None:
         for a, b in pairs:
             v = [x for x in (bw[a, b], bw[b, a]) if np.isfinite(x) and x > 0]
             if v:
-                meas.append(min(v))
+                gbps[(a, b)] = gbps[(b, a)] = min(v)
+    measured = len(gbps) == 2 * len(pairs)
     classes = sorted({LinkType(int(topo.link_type[a, b])).name for a, b in pairs})
-    return {"min_link_gbps": round(min(meas), 2) if meas and len(meas) == len(pairs) else None,
+    ring = _ring_bound(ids, lambda a, b: gbps[(a, b)]) if measured and pairs else None
+    ring_cost = _ring_bound(ids, lambda a, b: -float(topo.cost[a, b])) if pairs else None
+    return {"min_link_gbps": round(min(gbps.values()), 2) if measured and pairs else None,
+            "ring_link_gbps": round(ring, 2) if ring is not None else None,
             "max_link_cost": round(max((float(topo.cost[a, b]) for a, b in pairs), default=0.0), 6),
+            "ring_link_cost": round(-ring_cost, 6) if ring_cost is not None else 0.0,
             "link_classes": classes, "numa_nodes": sorted({int(topo.gpus[i].numa) for i in ids})}
 
 
@@ -87,10 +109,13 @@ def explain_subsets(topo: Topology, subsets: Dict[str, Optional[Sequence[int]]],
             continue
         delta = {t: round(e["weighted"][t] - ref["weighted"][t], 6) for t in TERMS}
         sep = [t for t in sorted(TERMS, key=lambda t: -abs(delta[t])) if abs(delta[t]) > 1e-9]
-        if ref["min_link_gbps"] and e["min_link_gbps"]:
-            gain, basis = ref["min_link_gbps"] / e["min_link_gbps"], "slowest measured link"
+        ring_k = len(e["ids"]) >= 4 and len(e["ids"]) <= 8
+        if ref["ring_link_gbps"] and e["ring_link_gbps"]:
+            gain = ref["ring_link_gbps"] / e["ring_link_gbps"]
+            basis = "slowest measured link of the best ring" if ring_k else "slowest measured link"
         else:
-            gain, basis = (e["max_link_cost"] / ref["max_link_cost"] if ref["max_link_cost"] else 1.0), "worst link cost"
+            gain = e["ring_link_cost"] / ref["ring_link_cost"] if ref["ring_link_cost"] else 1.0
+            basis = "worst link cost of the best ring" if ring_k else "worst link cost"
         out[f"vs_{name}"] = {"same_devices": sorted(e["ids"]) == sorted(ref["ids"]), "objective_delta": round(e["objective"] - ref["objective"], 6),
                              "separating_terms": {t: delta[t] for t in sep},
                              "predicted_gain": round(gain, 4), "predicted_basis": basis,
