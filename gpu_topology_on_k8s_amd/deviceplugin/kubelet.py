@@ -287,7 +287,7 @@ class FakeKubelet:
             if best_pref and not pref:
                 continue
             cm, cb = bin(m).count("1"), bin(best_mask).count("1")
-            narrower = cm < cb or (cm == cb and sorted(_bits(m)) < sorted(_bits(best_mask)))
+            narrower = cm < cb or (cm == cb and m < best_mask)  # IsNarrowerThan: equal widths compare as integers
             if narrower:
                 best_mask, best_pref = m, pref
         if self.topology_policy == "single-numa-node" and best_mask == default:

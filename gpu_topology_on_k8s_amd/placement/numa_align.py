@@ -8,7 +8,8 @@ active Topology Manager the kubelet narrows what it offers first.  For every con
 every set of NUMA nodes whose free devices, plus the devices an init container handed on, cover the
 request.  A hint is *preferred* when it is as narrow as the smallest set of NUMA nodes whose devices
 (free or not) could hold the request.  The policy merges the hints: the narrowest preferred one wins,
-and among equally narrow ones the lowest NUMA ids.  The policy also decides admission:
+and among equally narrow ones the smallest bitmask (``bitMask.IsNarrowerThan`` compares equal-width
+masks as integers, so {1,2} = 0b0110 beats {0,3} = 0b1001: the highest NUMA id decides first).  The policy also decides admission:
 
 * ``best-effort`` always admits;
 * ``restricted`` rejects when the winner is not preferred;
@@ -101,6 +102,10 @@ def _masks(nodes: Sequence[int]):
             yield frozenset(combo)
 
 
+def _mask_value(mask: FrozenSet[int]) -> int:
+    return sum(1 << n for n in mask)
+
+
 def best_hint(policy: str, request: int, available: Set[int], reusable: Set[int], numa: Mapping[int, int],
               all_devices: Sequence[int]) -> Tuple[Optional[FrozenSet[int]], bool, bool]:
     """(NUMA nodes of the merged hint or None = any, preferred, admitted) for one device request
@@ -129,7 +134,7 @@ def best_hint(policy: str, request: int, available: Set[int], reusable: Set[int]
     for mask, pref in hints:
         if pref and not best[1]:
             best = (mask, pref)
-        elif pref == best[1] and (len(mask), sorted(mask)) < (len(best[0]), sorted(best[0])):
+        elif pref == best[1] and (len(mask), _mask_value(mask)) < (len(best[0]), _mask_value(best[0])):
             best = (mask, pref)
     mask, pref = best
     if policy == "single-numa-node" and mask == everything:

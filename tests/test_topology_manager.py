@@ -290,6 +290,45 @@ def test_the_extenders_hints_equal_the_fake_kubelets(split):
             assert (None if mask is None else frozenset(_bits(mask))) == want, (policy, used, reusable, req)
 
 
+def test_equally_narrow_hints_tie_break_on_the_bitmask_value():
+    """16 devices, 4 per NUMA node on 4 nodes; free counts 1, 3, 2, 4 and a request of 5: both {0,3} and
+    {1,2} hold it, neither {0,1} nor {0,2} does.  The kubelet's IsNarrowerThan compares equal-width
+    masks as integers (0b0110 < 0b1001), so it hints {1,2}, not the lexicographically first {0,3}; the
+    extender and the fake kubelet agree with it."""
+    from gpu_topology_on_k8s_amd.deviceplugin.kubelet import FakeKubelet, _bits, _Plugin
+
+    numa = {d: d // 4 for d in range(16)}
+    free = {0} | {4, 5, 6} | {8, 9} | {12, 13, 14, 15}
+    for policy in ("best-effort", "restricted"):
+        assert best_hint(policy, 5, free, set(), numa, list(range(16))) == (frozenset({1, 2}), True, True)
+        kl = FakeKubelet("/nonexistent", topology_policy=policy)
+        p = _Plugin(resource="amd.com/gpu", endpoint="", channel=None, options=None,
+                    devices={str(i): "Healthy" for i in range(16)}, numa={str(i): (numa[i],) for i in range(16)})
+        mask, admit = kl._merge(p, kl._generate_hints(p, {str(d) for d in free}, set(), 5))
+        assert admit and set(_bits(mask)) == {1, 2}
+
+
+def test_the_hints_agree_on_sixteen_devices_over_four_numa_nodes():
+    """The differential check on 4 devices per NUMA node, where equal-width ties between masks are
+    common."""
+    from gpu_topology_on_k8s_amd.deviceplugin.kubelet import FakeKubelet, _bits, _Plugin
+
+    numa = {d: d // 4 for d in range(16)}
+    rng = random.Random(16)
+    for policy in ("best-effort", "restricted", "single-numa-node"):
+        kl = FakeKubelet("/nonexistent", topology_policy=policy)
+        p = _Plugin(resource="amd.com/gpu", endpoint="", channel=None, options=None,
+                    devices={str(i): "Healthy" for i in range(16)}, numa={str(i): (numa[i],) for i in range(16)})
+        for _ in range(300):
+            used = set(rng.sample(range(16), rng.randint(0, 15)))
+            reusable = set(rng.sample(sorted(used), rng.randint(0, min(3, len(used)))))
+            avail = set(range(16)) - used
+            req = rng.randint(1, 12)
+            mask, admit = kl._merge(p, kl._generate_hints(p, {str(d) for d in avail}, {str(d) for d in reusable}, req))
+            want, _, ok = best_hint(policy, req, avail, reusable, numa, list(range(16)))
+            assert ok == admit and (None if mask is None else frozenset(_bits(mask))) == want, (policy, used, reusable, req)
+
+
 @pytest.mark.gpu
 def test_a_real_node_under_single_numa_node():
     """The MI355X of the box, discovered through amdsmi with the NUMA node its host reports (not
