@@ -311,6 +311,9 @@ class DevicePluginServer:
         self.layout_change_reason = ""
         # devices held Unhealthy by a GPU event (reset in progress) whatever the RAS poll says
         self._holds: Dict[int, str] = {}
+        # devices the operator's cordon annotation names (held with CORDON_HOLD unless a reset holds them)
+        self._cordon_want: Set[int] = set()
+        self._cordon_unknown: List[str] = []
         self._reprobe_now = threading.Event()  # a GPU reset finished: re-measure as soon as the node is idle
         self.event_source = None  # deviceplugin.events.GpuEventWatcher (amdsmi event notification)
         # liveness (/healthz): the monitor loop's last pass, and since when re-registration has failed
@@ -397,21 +400,23 @@ class DevicePluginServer:
         reset) or the next health pass says otherwise."""
         want, unknown = self.cordoned_from(value or "")
         with self._cond:
-            have = {i for i, why in self._holds.items() if why == self.CORDON_HOLD}
-            add, drop = want - have, have - want
+            add, drop = want - self._cordon_want, self._cordon_want - want
+            self._cordon_want = set(want)
             for i in add:
-                self._holds.setdefault(i, self.CORDON_HOLD)
+                self._holds.setdefault(i, self.CORDON_HOLD)  # a reset hold stays; the reset's end turns it into this
             for i in drop:
-                self._holds.pop(i, None)
+                if self._holds.get(i) == self.CORDON_HOLD:  # a reset in progress keeps its own hold
+                    self._holds.pop(i)
+            released = {i for i in drop if i not in self._holds}
         node = {"kind": "Node", "metadata": {"name": self.cfg.node_name}}
-        if unknown and unknown != getattr(self, "_cordon_unknown", None) and self.api is not None and self.cfg.node_name:
+        if unknown and unknown != self._cordon_unknown and self.api is not None and self.cfg.node_name:
             record_event(self.api, node, "GPUCordonUnknown", f"{self.cfg.contract.cordon_key} names no device here: "
                          f"{','.join(unknown)}", "Warning", component="gpu-topology-device-plugin", host=self.cfg.node_name)
         self._cordon_unknown = unknown
         if add:
             self.set_health_many({i: False for i in add}, reason="GPUCordoned", why=self.CORDON_HOLD)
-        if drop:
-            states = {i: True for i in drop}  # a device holds one reason at a time: a reset hold is not a cordon
+        if released:
+            states = {i: True for i in released}
             if self.health_fn is not None and states:
                 try:
                     verdict = self.health_fn(self.topology)
@@ -420,10 +425,10 @@ class DevicePluginServer:
                     log.warning("health check after an uncordon failed: %s", e)
             self.set_health_many(states)
             if self.api is not None and self.cfg.node_name:
-                record_event(self.api, node, "GPUUncordoned", f"devices {format_group(sorted(drop))} back in service",
+                record_event(self.api, node, "GPUUncordoned", f"devices {format_group(sorted(released))} back in service",
                              "Normal", component="gpu-topology-device-plugin", host=self.cfg.node_name)
         self.metrics.cordoned.set(len(want))
-        return add, drop
+        return add, released
 
     def poll_node(self) -> Optional[dict]:
         """One GET of this plugin's own Node (the daemon's periodic label check): applies the operator's
@@ -1506,15 +1511,16 @@ class DevicePluginServer:
                 if slices_per_gpu(self.topology) > 1 else [index])
         if kind == "GPU_PRE_RESET":
             log.warning("device %d (%s): GPU reset starting: %s", index, bdf, message)
-            for i in same:
-                if self._holds.get(i) != self.CORDON_HOLD:  # a cordoned GPU stays cordoned through a reset
-                    self._holds[i] = "GPU reset in progress"
+            for i in same:  # a cordoned GPU goes back to its cordon when the reset ends (_cordon_want)
+                self._holds[i] = "GPU reset in progress"
             self.set_health_many({i: False for i in same})
             reason, note = "GPUReset", f"device {index} ({bdf}) is resetting; held Unhealthy"
         elif kind == "GPU_POST_RESET":
             log.warning("device %d (%s): GPU reset finished: %s", index, bdf, message)
             for i in same:
-                if self._holds.get(i) != self.CORDON_HOLD:
+                if i in self._cordon_want:  # cordoned during the reset: the operator's hold replaces it
+                    self._holds[i] = self.CORDON_HOLD
+                else:
                     self._holds.pop(i, None)
             if self.health_fn is None:
                 self.set_health_many({i: True for i in same if i not in self._holds})

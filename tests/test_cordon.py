@@ -129,6 +129,16 @@ def test_a_cordoned_gpu_stays_out_of_service_through_a_reset():
         assert plug._health[4] is True
         plug.apply_cordon("")
         assert plug._health[3] is True
+        # cordoned while a reset is in progress: the reset's end leaves it cordoned, not Healthy
+        plug.gpu_event(5, "GPU_PRE_RESET")
+        assert plug.apply_cordon("5")[0] == {5} and plug._holds[5] != plug.CORDON_HOLD
+        plug.gpu_event(5, "GPU_POST_RESET")
+        assert plug._health[5] is False and plug._holds[5] == plug.CORDON_HOLD
+        # uncordoned while a reset is in progress: the reset keeps it out until it ends
+        plug.gpu_event(5, "GPU_PRE_RESET")
+        assert plug.apply_cordon("") == (set(), set()) and plug._health[5] is False
+        plug.gpu_event(5, "GPU_POST_RESET")
+        assert plug._health[5] is True and 5 not in plug._holds
 
 
 def test_any_annotation_text_parses_without_raising():

@@ -144,12 +144,11 @@ MUTANTS: List[Mutant] = [
            why="needed == aligned: the plugin, asked over exactly the aligned devices, answers all of them"),
     Mutant("numa", NUMA_ALIGN, "            in_mask = sum(1 for d in all_devices if numa.get(d, -1) in mask)",
            "            in_mask = sum(1 for d in available if numa.get(d, -1) in mask)"),
-    Mutant("numa", NUMA_ALIGN, "        elif pref == best[1] and (len(mask), sorted(mask)) < (len(best[0]), sorted(best[0])):",
-           "        elif pref == best[1] and len(mask) < len(best[0]):", equivalent=True,
-           why="masks are iterated lowest ids first, so the first of equally narrow hints is already the lowest"),
+    Mutant("numa", NUMA_ALIGN, "        elif pref == best[1] and (len(mask), _mask_value(mask)) < (len(best[0]), _mask_value(best[0])):",
+           "        elif pref == best[1] and (len(mask), sorted(mask)) < (len(best[0]), sorted(best[0])):"),
     Mutant("numa", NUMA_ALIGN, "        for combo in itertools.combinations(sorted(nodes), width):",
            "        for combo in itertools.combinations(sorted(nodes, reverse=True), width):", equivalent=True,
-           why="the merge compares equally narrow hints by their lowest ids, whatever the iteration order"),
+           why="the merge compares equally narrow hints by their bitmask value, whatever the iteration order"),
     Mutant("numa", NUMA_ALIGN, "            if any(numa.get(d, -1) >= 0 and numa[d] not in mask for d in reusable):", "            if False:"),
     Mutant("numa", NUMA_ALIGN, '    admit = policy == "best-effort" or pref', "    admit = True"),
     Mutant("numa", NUMA_ALIGN, '        if kind == "init":\n            reuse |= got', '        if False:\n            reuse |= got'),
@@ -169,7 +168,7 @@ MUTANTS: List[Mutant] = [
            "                  0.0;\n      if (collect_ties", equivalent=True,
            why="a weaker lower bound prunes less; the search stays exact"),
     # operator GPU cordon
-    Mutant("cordon", PLUGIN, "                self._holds.setdefault(i, self.CORDON_HOLD)", "                pass"),
+    Mutant("cordon", PLUGIN, "                self._holds.setdefault(i, self.CORDON_HOLD)  #", "                pass  #"),
     Mutant("cordon", PLUGIN, "            out |= {g.index for g in t.gpus if g.physical == t.gpus[i].physical}", "            out.add(i)"),
     Mutant("cordon", PLUGIN_MAIN, "    plugin.poll_node()  # a cordoned GPU is never advertised Healthy", "    pass  # a cordoned GPU is never advertised Healthy"),
     # data-parallel reduction
