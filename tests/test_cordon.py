@@ -141,6 +141,28 @@ def test_a_cordoned_gpu_stays_out_of_service_through_a_reset():
         assert plug._health[5] is True and 5 not in plug._holds
 
 
+def test_a_cordon_outlasts_health_passes_that_find_the_gpu_healthy():
+    """The RAS poll reports every GPU healthy; a cordoned one stays out of service through its passes
+    and comes back only when the annotation lets it go."""
+    with SimCluster({"n": fx.f7_mi355x()}) as c:
+        plug = c.nodes["n"].plugin
+        kub, res = c.nodes["n"].kubelet, c.resource
+        calls = []
+
+        def all_healthy(t):
+            calls.append(1)
+            return {i: True for i in range(t.n)}
+
+        plug.cfg.health_interval = 0.05
+        plug.health_fn = all_healthy
+        _cordon(c, "n", "6")
+        n0 = len(calls)
+        assert _wait(lambda: len(calls) >= n0 + 3)
+        assert kub.plugins[res].devices["6"] == "Unhealthy" and not plug._health[6]
+        _cordon(c, "n", "")
+        assert _wait(lambda: kub.plugins[res].devices["6"] == "Healthy")
+
+
 def test_any_annotation_text_parses_without_raising():
     """The annotation is free text an operator types: whatever it holds, the plugin names only devices
     it has, whole physical GPUs, and reports the rest."""
