@@ -213,9 +213,16 @@ def cmd_select(a) -> int:
     pl = select(t, a.k, used=used, policy=PlacementPolicy())
     out = {"ids": list(pl.ids), "score": round(pl.score, 4), "objective": round(pl.objective, 6), "exact": pl.exact,
            "terms": {k: round(v, 6) for k, v in pl.terms.items()}}
-    if a.worst:
+    if a.worst or a.explain:
         w = worst(t, a.k, used=used)
         out["worst"] = {"ids": list(w.ids), "score": round(w.score, 4)}
+    if a.explain:
+        # what bench.py's placement_terms carries: the terms of the chosen, worst and kubelet-default
+        # subsets, the terms that separate each from the choice and the gain its ring-bound link predicts
+        from .placement.explain import default_subset, explain_subsets
+
+        out["explain"] = explain_subsets(t, {"chosen": pl.ids, "worst": w.ids, "default": default_subset(t, a.k, used)},
+                                         used=used)
     print(json.dumps(out))
     return 0
 
@@ -462,6 +469,9 @@ def main(argv=None) -> int:
     p.add_argument("--used", default="")
     p.add_argument("--policy", default="exact", choices=["exact", "gaia"])
     p.add_argument("--worst", action="store_true")
+    p.add_argument("--explain", action="store_true",
+                   help="the objective's terms for the chosen, worst and kubelet-default (lowest free ids) subsets, "
+                        "the terms that separate them and the gain their slowest ring link predicts")
     p.set_defaults(fn=cmd_select)
     p = sub.add_parser("defrag", help="plan pod moves that make a k-GPU pod placeable (read-only)")
     p.add_argument("-k", type=int, default=8)

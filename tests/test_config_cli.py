@@ -74,6 +74,19 @@ def test_cli_topo_select_config():
     assert p.returncode == 2 and "time-sliced" in p.stderr
 
 
+def test_cli_select_explain_on_a_degraded_link(tmp_path):
+    """``gtk select --explain``: the chosen, worst and kubelet-default subsets with their terms; with link
+    0-1 at 60 % the default (0, 1) is predicted 1 / 0.6 slower than the choice, by link terms."""
+    from gpu_topology_on_k8s_amd.topology import fixtures as fx
+
+    f = tmp_path / "t.json"
+    f.write_text(fx.f7_degraded(((0, 1, 0.6),)).to_json())
+    out = json.loads(_cli("select", "--topology", str(f), "-k", "2", "--explain"))
+    ex = out["explain"]
+    assert ex["chosen"]["ids"] == out["ids"] and ex["default"]["ids"] == [0, 1] and ex["worst"]["ids"] == out["worst"]["ids"]
+    assert ex["vs_default"]["link_terms_separate"] and abs(ex["vs_default"]["predicted_gain"] - 1 / 0.6) < 1e-3
+
+
 def test_manifests_time_slices():
     from gpu_topology_on_k8s_amd.config import render_manifests
 
