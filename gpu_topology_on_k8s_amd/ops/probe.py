@@ -37,6 +37,11 @@ PROBE_PRESETS: Dict[str, Dict[str, int]] = {
     "full": {"bytes": 512 << 20, "iters": 10, "warmup": 2, "repeats": 5},
 }
 
+#: the K3 HBM self-copy reads and writes at least this much in every preset: 2 x 1 GiB is far past the
+#: 256 MiB Infinity Cache, which a quick preset's 2 x 64 MiB would fit (profiles/r06_prof: 3.1-3.2 TB/s
+#: at 64 MiB, 2.8 TB/s at 512 MiB)
+HBM_COPY_MIN_BYTES = 1 << 30
+
 
 def _p():
     return load("_probe")
@@ -256,8 +261,9 @@ def probe_topology(topo: Topology, preset: str = "quick", devs: Optional[List[in
         if i != j and not bool(_p().can_access_peer(hj if mode == "read" else hi, hi if mode == "read" else hj)):
             continue
         vals = []
+        nbytes = cfg["bytes"] if i != j else max(cfg["bytes"], HBM_COPY_MIN_BYTES)
         for _ in range(reps if i != j else 1):
-            r = copy_bw(hi, hj, cfg["bytes"], cfg["iters"], cfg["warmup"], mode=mode, kind=kind)
+            r = copy_bw(hi, hj, nbytes, cfg["iters"], cfg["warmup"], mode=mode, kind=kind)
             if not r["ok"]:
                 raise RuntimeError(f"probe verification failed for {i}->{j}")
             vals.append(float(r["gbps"]))

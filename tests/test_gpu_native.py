@@ -134,7 +134,7 @@ def test_probe_cli_ingress_single_gpu(tmp_path):
         assert d["probe"]["ingress_all_gbps"][0] is None  # one GPU: no peers to gather from
     else:
         assert all(x is not None and x > 0 for x in d["probe"]["ingress_all_gbps"])
-    assert d["hbm_gbps"][0] > 2000  # quick preset, 64 MiB self copy: ~3.2 TB/s measured (r02)
+    assert d["hbm_gbps"][0] > 2000  # 1 GiB self copy (HBM_COPY_MIN_BYTES): ~2.8 TB/s measured (r06)
 
 
 def test_discover_real_node():
