@@ -160,9 +160,11 @@ class Sim:
 
     def link_factor(self, n: int, ids: Tuple[int, ...]) -> float:
         """How much slower than on the node's best link the job's collectives run:
-        ``ring`` = the best ring's slowest link (RCCL searches ring orders by link bandwidth, so a
-        bad link is avoided whenever a Hamiltonian cycle without it exists), ``bottleneck`` = the
-        set's slowest link, ``mean`` = mean pair cost (traffic spread over every link)."""
+        ``ring`` = the best ring's slowest link (assumes RCCL's ring order avoids a bad link whenever
+        a Hamiltonian cycle without it exists; nothing tells RCCL the measured matrix, so this is the
+        optimistic model: it credits the rival policies' placements as much as possible, so it
+        understates this framework's gain), ``bottleneck`` = the set's slowest link (RCCL's channels
+        cross every link), ``mean`` = mean pair cost (traffic spread over every link)."""
         if len(ids) < 2:
             return 1.0
         key = (n, ids, self.link_model)

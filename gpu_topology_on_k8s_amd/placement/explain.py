@@ -16,11 +16,16 @@ reported with:
 * its links: the slowest measured link GB/s (or the worst link cost when nothing was measured), the
   link classes and the NUMA nodes it uses;
 * against the chosen subset, the terms that separate the two (largest first) and the **predicted
-  gain**: the chosen subset's ring-bound link over the other's.  A ring all-reduce moves every byte
-  over every link of its ring, so its busBW follows the slowest one.  With 2 or 3 devices the ring
-  uses every pair; with 4 or more on a full mesh RCCL orders the ring around a slow link when it can,
-  so the bound is the slowest link of the best ring (``ring_link_gbps``; the model of
-  bench/cluster_trace.py).  The prediction is 1.00 when only host-side terms separate the subsets.
+  gain**, a range.  A ring all-reduce moves every byte over every link of its ring, so its busBW
+  follows the slowest one.
+  - ``predicted_gain``: the ratio of the two subsets' slowest links over all pairs.  This is the
+    expectation when RCCL's channels cross every link of the subset. Nothing hands RCCL the measured
+    matrix, so it cannot steer round a link that its own detection reports at full width.
+  - ``predicted_gain_ring`` (4 to 8 devices): the ratio of the best rings' slowest links
+    (``ring_link_gbps``). This is the expectation if RCCL's ring order does avoid the slow link, the
+    optimistic model of bench/cluster_trace.py. With 2 or 3 devices every ring uses every pair, so the
+    two are equal.
+  Both are 1.00 when only host-side terms separate the subsets.
 
 Subsets compared: ``chosen`` (the placement core), ``worst`` (highest objective), and ``default``
 (what the kubelet's device manager hands out with no extender and no preferred allocation: it takes
@@ -109,15 +114,15 @@ def explain_subsets(topo: Topology, subsets: Dict[str, Optional[Sequence[int]]],
             continue
         delta = {t: round(e["weighted"][t] - ref["weighted"][t], 6) for t in TERMS}
         sep = [t for t in sorted(TERMS, key=lambda t: -abs(delta[t])) if abs(delta[t]) > 1e-9]
-        ring_k = len(e["ids"]) >= 4 and len(e["ids"]) <= 8
-        if ref["ring_link_gbps"] and e["ring_link_gbps"]:
-            gain = ref["ring_link_gbps"] / e["ring_link_gbps"]
-            basis = "slowest measured link of the best ring" if ring_k else "slowest measured link"
+        if ref["min_link_gbps"] and e["min_link_gbps"]:
+            gain, basis = ref["min_link_gbps"] / e["min_link_gbps"], "slowest measured link"
+            ring_gain = ref["ring_link_gbps"] / e["ring_link_gbps"]
         else:
-            gain = e["ring_link_cost"] / ref["ring_link_cost"] if ref["ring_link_cost"] else 1.0
-            basis = "worst link cost of the best ring" if ring_k else "worst link cost"
+            gain = e["max_link_cost"] / ref["max_link_cost"] if ref["max_link_cost"] else 1.0
+            ring_gain = e["ring_link_cost"] / ref["ring_link_cost"] if ref["ring_link_cost"] else 1.0
+            basis = "worst link cost"
         out[f"vs_{name}"] = {"same_devices": sorted(e["ids"]) == sorted(ref["ids"]), "objective_delta": round(e["objective"] - ref["objective"], 6),
                              "separating_terms": {t: delta[t] for t in sep},
-                             "predicted_gain": round(gain, 4), "predicted_basis": basis,
+                             "predicted_gain": round(gain, 4), "predicted_gain_ring": round(ring_gain, 4), "predicted_basis": basis,
                              "link_terms_separate": any(t in ("comm", "bottleneck", "link_deficit") for t in sep)}
     return out

@@ -37,18 +37,19 @@ def test_healthy_mesh_predicts_no_link_gain(k):
 @pytest.mark.parametrize("k", [2, 4])
 def test_degraded_link_separates_the_default_placement(k):
     """Link 0-1 at 60 %: the kubelet's lowest ids use it, the choice does not; the comparison names the
-    link terms.  Two devices predict the slowest-link ratio, 1 / 0.6; four devices on a full mesh let
-    RCCL order the ring round the slow link (0-2-1-3-0), so the prediction is 1.00."""
+    link terms and predicts the slowest-link ratio, 1 / 0.6.  With four devices the ring-order bound is
+    1.00: a ring 0-2-1-3-0 avoids the slow link, if RCCL's ring order does."""
     t = fx.f7_degraded(((0, 1, 0.6),))
     ex = _three(t, k)
     chosen, dflt = ex["chosen"]["ids"], ex["default"]["ids"]
     assert not {0, 1} <= set(chosen) and {0, 1} <= set(dflt)
     vs = ex["vs_default"]
     assert vs["link_terms_separate"] and "comm" in vs["separating_terms"]
+    assert vs["predicted_gain"] == pytest.approx(1 / 0.6, rel=1e-3) and vs["predicted_basis"] == "slowest measured link"
     if k == 2:
-        assert vs["predicted_gain"] == pytest.approx(1 / 0.6, rel=1e-3) and vs["predicted_basis"] == "slowest measured link"
+        assert vs["predicted_gain_ring"] == pytest.approx(vs["predicted_gain"])
     else:
-        assert vs["predicted_gain"] == pytest.approx(1.0) and vs["predicted_basis"] == "slowest measured link of the best ring"
+        assert vs["predicted_gain_ring"] == pytest.approx(1.0)
         assert ex["default"]["ring_link_gbps"] == pytest.approx(150.0) and ex["default"]["min_link_gbps"] == pytest.approx(90.0)
     assert ex["chosen"]["objective"] < ex["default"]["objective"]
     assert vs["predicted_gain"] >= ex["vs_worst"]["predicted_gain"] >= 1.0 - 1e-9
@@ -85,17 +86,19 @@ def test_bench_dry_run_reports_three_subsets_with_terms(tmp_path, n, fixture):
         assert out["config"]["default_subset"] == pt["default"]["ids"]
         ab = out["default_subset_ab"]
         assert ab and ab["exact"] and ab["subset"] == out["config"]["default_subset"] and out["placement_gain_vs_default"] > 0
-        assert pt["vs_default"]["predicted_gain"] == pytest.approx(1 / 0.6 if n == 2 else 1.0, rel=1e-3)
+        assert pt["vs_default"]["predicted_gain"] == pytest.approx(1 / 0.6, rel=1e-3)
+        assert pt["vs_default"]["predicted_gain_ring"] == pytest.approx(1 / 0.6 if n == 2 else 1.0, rel=1e-3)
 
 
 def test_ring_cannot_route_round_two_slow_links_of_one_device():
     """Device 0 at 60 % toward both 1 and 2: any ring through {0,1,2,3} uses two of 0's three links, so
-    one slow link is unavoidable and the four-device prediction is 1 / 0.6 again."""
+    one slow link is unavoidable and even the ring-order bound is 1 / 0.6."""
     t = fx.f7_degraded(((0, 1, 0.6), (0, 2, 0.6)))
     ex = _three(t, 4)
     assert {0, 1, 2, 3} == set(ex["default"]["ids"]) and 0 not in ex["chosen"]["ids"]
     assert ex["default"]["ring_link_gbps"] == pytest.approx(90.0)
     assert ex["vs_default"]["predicted_gain"] == pytest.approx(1 / 0.6, rel=1e-3)
+    assert ex["vs_default"]["predicted_gain_ring"] == pytest.approx(1 / 0.6, rel=1e-3)
 
 
 def test_ring_bound_model():
