@@ -149,7 +149,6 @@ def scale_prioritize(n_nodes: int, pods: int = 20, k: int = 4, tm_policy: str = 
                                   capacity={c.resource_name: "8"}))
     out = {"experiment": f"scale-prioritize-{n_nodes}-nodes" + (f"-tm-{tm_policy}" if tm_policy != "none" else ""),
            "nodes": n_nodes, "request_gpus": k, "pods": pods, "topology_manager": tm_policy, "containers": list(split or [k])}
-    from gpu_topology_on_k8s_amd.k8s.informer import Informer
 
     for mode, cache in (("cache_off", 0), ("cache_on", 4096), ("informer", 4096)):
         ext = TopologyExtender(api, ExtenderConfig(resync_s=60.0 if mode != "informer" else 0.0, decision_cache=cache))
