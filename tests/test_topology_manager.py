@@ -87,19 +87,21 @@ def _shape(rng):
     return {"gpus": 0, "split": [app], "init": [rng.choice([1, 2, app])]}
 
 
-@pytest.mark.parametrize("policy,scope,split", [("best-effort", "container", 2), ("restricted", "container", 2),
-                                                ("single-numa-node", "container", 2), ("best-effort", "pod", 2),
-                                                ("single-numa-node", "pod", 2), ("best-effort", "container", 4),
-                                                ("restricted", "pod", 4)])
-def test_groups_equal_what_the_kubelet_allocates_under_churn(policy, scope, split):
+@pytest.mark.parametrize("policy,scope,split,n", [("best-effort", "container", 2, 8), ("restricted", "container", 2, 8),
+                                                  ("single-numa-node", "container", 2, 8), ("best-effort", "pod", 2, 8),
+                                                  ("single-numa-node", "pod", 2, 8), ("best-effort", "container", 4, 8),
+                                                  ("restricted", "pod", 4, 8), ("best-effort", "container", 4, 16),
+                                                  ("restricted", "container", 4, 16)])
+def test_groups_equal_what_the_kubelet_allocates_under_churn(policy, scope, split, n):
     """Random pods arrive and finish on two MI355X nodes whose kubelets run the Topology Manager (hosts
-    with 2 NUMA nodes, or 4 as an EPYC in NPS2/NPS4 mode); the reconcile pass is off.  Every pod the
-    extender binds is admitted with exactly its GROUP, and no pod is bound that the kubelet rejects."""
+    with 2 NUMA nodes, or 4 as an EPYC in NPS2/NPS4 mode; 16 devices are a node of DPX partitions, 4 per
+    NUMA node); the reconcile pass is off.  Every pod the extender binds
+    is admitted with exactly its GROUP, and no pod is bound that the kubelet rejects."""
     from gpu_topology_on_k8s_amd.topology.model import Topology
 
-    rng = random.Random(f"{policy}/{scope}/{split}")
+    rng = random.Random(f"{policy}/{scope}/{split}/{n}")
     tm = TopologyManager(policy, scope)
-    node = lambda: Topology.full_mesh(n=8, numa_split=split, node_name="mi355x")  # noqa: E731
+    node = lambda: Topology.full_mesh(n=n, numa_split=split, node_name="mi355x")  # noqa: E731
     with SimCluster({"a": node(), "b": node()}, topology_manager=tm) as c:
         live = []
         placed = 0
