@@ -33,6 +33,7 @@ the free devices in set order, modelled here as the lowest free indices).
 """
 from __future__ import annotations
 
+import functools
 import itertools
 from typing import Dict, List, Optional, Sequence
 
@@ -59,18 +60,23 @@ def _weighted(terms: Dict[str, float], policy: PlacementPolicy) -> Dict[str, flo
             "access": policy.w_access * terms["access"], "nic_deficit": policy.w_nic * terms["nic_deficit"]}
 
 
-def _ring_bound(ids: Sequence[int], speed) -> Optional[float]:
-    """The slowest link a ring all-reduce over ``ids`` must use (``speed(a, b)``: higher is faster):
-    every pair for 2-3 devices, else the best ring's slowest link (exhaustive up to 8 devices, every
-    pair beyond that)."""
-    ids = list(ids)
-    if len(ids) < 2:
+@functools.lru_cache(maxsize=None)
+def _rings(k: int) -> np.ndarray:
+    """Every ring over positions 0..k-1 once (start fixed at 0, one direction): ((k-1)!/2, k) indices."""
+    return np.array([(0,) + p for p in itertools.permutations(range(1, k)) if p[0] < p[-1]], dtype=np.intp)
+
+
+def _ring_bound(speed: np.ndarray) -> Optional[float]:
+    """The slowest link a ring all-reduce over the devices of the k x k ``speed`` matrix must use
+    (higher is faster): every pair for 2-3 devices, else the best ring's slowest link (exhaustive up to
+    8 devices, every pair beyond that)."""
+    k = speed.shape[0]
+    if k < 2:
         return None
-    if len(ids) <= 3 or len(ids) > 8:
-        return min(speed(a, b) for i, a in enumerate(ids) for b in ids[i + 1:])
-    first, rest = ids[0], ids[1:]
-    return max(min(speed(x, y) for x, y in zip((first,) + perm, perm + (first,)))
-               for perm in itertools.permutations(rest) if perm[0] < perm[-1])
+    if k <= 3 or k > 8:
+        return float(speed[~np.eye(k, dtype=bool)].min())
+    r = _rings(k)
+    return float(speed[r, np.roll(r, -1, axis=1)].min(axis=1).max())
 
 
 def _links(topo: Topology, ids: Sequence[int]) -> Dict[str, object]:
@@ -85,8 +91,10 @@ def _links(topo: Topology, ids: Sequence[int]) -> Dict[str, object]:
                 gbps[(a, b)] = gbps[(b, a)] = min(v)
     measured = len(gbps) == 2 * len(pairs)
     classes = sorted({LinkType(int(topo.link_type[a, b])).name for a, b in pairs})
-    ring = _ring_bound(ids, lambda a, b: gbps[(a, b)]) if measured and pairs else None
-    ring_cost = _ring_bound(ids, lambda a, b: -float(topo.cost[a, b])) if pairs else None
+    ring = None
+    if measured and pairs:
+        ring = _ring_bound(np.array([[gbps[(a, b)] if a != b else np.inf for b in ids] for a in ids]))
+    ring_cost = _ring_bound(-np.asarray(topo.cost, dtype=float)[np.ix_(ids, ids)]) if pairs else None
     return {"min_link_gbps": round(min(gbps.values()), 2) if measured and pairs else None,
             "ring_link_gbps": round(ring, 2) if ring is not None else None,
             "max_link_cost": round(max((float(topo.cost[a, b]) for a, b in pairs), default=0.0), 6),

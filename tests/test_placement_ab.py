@@ -103,14 +103,29 @@ def test_ring_cannot_route_round_two_slow_links_of_one_device():
 
 def test_ring_bound_model():
     """The ring bound on hand-made speeds: every pair for k <= 3, the best ring's slowest link for 4..8."""
+    import itertools
+
+    import numpy as np
+
     from gpu_topology_on_k8s_amd.placement.explain import _ring_bound
-    slow = {(0, 1), (1, 0)}
-    sp = lambda a, b: 1.0 if (a, b) in slow else 2.0
-    assert _ring_bound([0, 1, 2], sp) == 1.0
-    assert _ring_bound([0, 1, 2, 3], sp) == 2.0
-    slow |= {(2, 3), (3, 2), (0, 2), (2, 0)}
-    assert _ring_bound([0, 1, 2, 3], sp) == 1.0       # 2's only fast link left is 2-1: a ring needs two
-    assert _ring_bound([0], sp) is None
+
+    def sp(k, slow):
+        m = np.full((k, k), 2.0)
+        for a, b in slow:
+            m[a, b] = m[b, a] = 1.0
+        return m
+
+    assert _ring_bound(sp(3, [(0, 1)])) == 1.0
+    assert _ring_bound(sp(4, [(0, 1)])) == 2.0
+    assert _ring_bound(sp(4, [(0, 1), (2, 3), (0, 2)])) == 1.0  # 2's only fast link left is 2-1: a ring needs two
+    assert _ring_bound(np.zeros((1, 1))) is None
+    # against a plain enumeration, on random speeds for 4..8 devices
+    rng = np.random.default_rng(0)
+    for k in range(4, 9):
+        m = rng.uniform(1, 2, (k, k))
+        m = np.minimum(m, m.T)
+        want = max(min(m[x, y] for x, y in zip((0,) + p, p + (0,))) for p in itertools.permutations(range(1, k)))
+        assert _ring_bound(m) == want
 
 
 def test_train_harness_runs_the_default_arm(tmp_path):
