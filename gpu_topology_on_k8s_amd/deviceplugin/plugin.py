@@ -1511,17 +1511,19 @@ class DevicePluginServer:
                 if slices_per_gpu(self.topology) > 1 else [index])
         if kind == "GPU_PRE_RESET":
             log.warning("device %d (%s): GPU reset starting: %s", index, bdf, message)
-            for i in same:  # a cordoned GPU goes back to its cordon when the reset ends (_cordon_want)
-                self._holds[i] = "GPU reset in progress"
+            with self._cond:  # apply_cordon checks and releases holds under this lock
+                for i in same:  # a cordoned GPU goes back to its cordon when the reset ends (_cordon_want)
+                    self._holds[i] = "GPU reset in progress"
             self.set_health_many({i: False for i in same})
             reason, note = "GPUReset", f"device {index} ({bdf}) is resetting; held Unhealthy"
         elif kind == "GPU_POST_RESET":
             log.warning("device %d (%s): GPU reset finished: %s", index, bdf, message)
-            for i in same:
-                if i in self._cordon_want:  # cordoned during the reset: the operator's hold replaces it
-                    self._holds[i] = self.CORDON_HOLD
-                else:
-                    self._holds.pop(i, None)
+            with self._cond:
+                for i in same:
+                    if i in self._cordon_want:  # cordoned during the reset: the operator's hold replaces it
+                        self._holds[i] = self.CORDON_HOLD
+                    else:
+                        self._holds.pop(i, None)
             if self.health_fn is None:
                 self.set_health_many({i: True for i in same if i not in self._holds})
             self._reprobe_now.set()
