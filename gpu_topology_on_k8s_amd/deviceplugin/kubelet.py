@@ -185,6 +185,25 @@ class FakeKubelet:
             self.plugins.clear()
         self.start()
 
+    def restart_container(self, key: str, container: str, resource: Optional[str] = None) -> Tuple[str, ...]:
+        """A container of an admitted pod restarts (a crash, a liveness failure): like the kubelet, the
+        device manager hands it the devices it already holds.  There is no GetPreferredAllocation and no
+        Allocate; only PreStartContainer runs again when the plugin asks for it, and its failure fails
+        this start (the kubelet backs off and retries).  Returns the container's device ids."""
+        resource = resource or next(iter(self.plugins))
+        p = self.plugins[resource]
+        with self._lock:
+            held = [ids for name, _kind, ids in self.containers.get(resource, {}).get(key, ()) if name == container]
+        if not held:
+            raise KeyError(f"{key}: no container {container!r} holding {resource}")
+        ids = held[0]
+        if getattr(p.options, "pre_start_required", False):
+            try:
+                self._stub(p, "PreStartContainer")(pb.PreStartContainerRequest(devices_ids=list(ids)), timeout=300)
+            except grpc.RpcError as e:
+                raise AdmissionError(f"PreStartContainer failed: {e.details()}") from e
+        return ids
+
     def wait_for(self, resource: str, timeout: float = 10.0) -> _Plugin:
         t0 = time.time()
         while time.time() - t0 < timeout:

@@ -833,15 +833,28 @@ class DevicePluginServer:
                          "FailedGPUPlacementValidation", msg, "Warning", component="gpu-topology-device-plugin",
                          host=self.cfg.node_name)
             context.abort(grpc.StatusCode.FAILED_PRECONDITION, msg)
-        if pod is not None and self.api is not None:
+        if pod is not None and self.api is not None and self._widest_validation(pod, res):
             md = meta(pod)
-            ann = {self.cfg.contract.validated_key: json.dumps(
-                {k: res[k] for k in ("k", "peak_bytes", "peak_algbw_gbps", "peak_busbw_gbps") if k in res}, separators=(",", ":"))}
+            rec = {k: res[k] for k in ("k", "peak_bytes", "peak_algbw_gbps", "peak_busbw_gbps") if k in res}
+            rec["devices"] = format_group(ids)
+            ann = {self.cfg.contract.validated_key: json.dumps(rec, separators=(",", ":"))}
             try:
                 self.api.patch_pod_annotations(md.get("namespace", "default"), md["name"], ann)
             except Exception as e:  # noqa: BLE001 - the validation passed; the record is best effort
                 log.warning("recording validation on %s failed: %s", md.get("name"), e)
         return pb.PreStartContainerResponse()
+
+    def _widest_validation(self, pod: dict, res: Dict[str, object]) -> bool:
+        """Whether ``res`` should be the pod's validation record: each container start (a restart too)
+        validates that container's devices, and the pod keeps its widest one (ties: the latest), so a
+        one-GPU sidecar does not overwrite the all-reduce of a four-GPU container."""
+        old = obj_annotations(pod).get(self.cfg.contract.validated_key)
+        if not old:
+            return True
+        try:
+            return int(res.get("k", 0)) >= int(json.loads(old).get("k", 0))
+        except (ValueError, TypeError, AttributeError):
+            return True
 
     def _assigned_pod(self, ids: Sequence[int]) -> Optional[dict]:
         """The live pod on this node whose confirmed GROUP holds ``ids`` (one container's devices;

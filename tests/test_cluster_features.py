@@ -3,6 +3,7 @@ start-up probe reuse on busy nodes, compact node annotations, CPU affinity, the 
 path, normalised node scores, LIST+WATCH informer, plugin metrics/events, Gaia Fragment via XCPs,
 and the cross-node bind deadlock."""
 import itertools
+import json
 import threading
 import time
 
@@ -471,6 +472,40 @@ def test_prestart_validation_records_busbw_on_the_pod():
         text = c.nodes["n1"].plugin.metrics.exposition().decode()
         assert 'gtk_plugin_placement_validations_total{result="ok"} 1.0' in text
         assert 'gtk_plugin_placement_validations_total{result="failed"} 1.0' in text
+
+
+def test_a_container_restart_keeps_its_devices_and_validates_again():
+    """A restarted container gets the devices it holds, as the kubelet's device manager does: no
+    GetPreferredAllocation, no Allocate, the pod's annotations untouched; PreStartContainer (the
+    placement validation) runs again, and its failure fails only that start."""
+    seen = []
+    fail = []
+
+    def fake_validate(ids):
+        seen.append(sorted(ids))
+        return {"ok": not fail, "wrong": 1 if fail else 0, "k": len(ids)}
+
+    with SimCluster({"n1": fx.f7_mi355x()}, prestart_validate=True, validate_fn=fake_validate) as c:
+        c.submit("two", 0, split=[2, 1])
+        (r,) = c.schedule_pending()
+        assert not r.error, r
+        kub = c.nodes["n1"].kubelet
+        key = "default/two"
+        names = [name for name, _kind, _ids in kub.containers[C.resource_name][key]]
+        calls = (len(kub.allocate_calls), len(kub.preferred_calls))
+        ann = dict(c.api.get_pod("default", "two")["metadata"]["annotations"])
+        # each container start validated its own devices; the pod keeps the widest (2 GPUs, not the 1-GPU one)
+        assert json.loads(ann[C.validated_key])["k"] == 2 and len(seen) == 2
+        before = len(seen)
+        ids = kub.restart_container(key, names[0])
+        assert len(ids) == 2 and set(ids) <= {str(i) for i in r.allocated}
+        assert seen[before:] == [sorted(int(i) for i in ids)]
+        assert (len(kub.allocate_calls), len(kub.preferred_calls)) == calls
+        assert dict(c.api.get_pod("default", "two")["metadata"]["annotations"]) == ann
+        fail.append(1)
+        with pytest.raises(Exception, match="PreStartContainer failed"):
+            kub.restart_container(key, names[1])
+        assert set(kub.allocated[C.resource_name][key]) == {str(i) for i in r.allocated}  # still held
 
 
 def test_relist_racing_a_bind_keeps_the_binds_devices():
