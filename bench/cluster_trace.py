@@ -104,13 +104,14 @@ def make_trace(n_jobs: int, n_gpus: int, load: float, mean_min: float, seed: int
 
 
 class Sim:
-    def __init__(self, topos: List[Topology], policy: str, alpha: float, link_model: str = "ring"):
+    def __init__(self, topos: List[Topology], policy: str, alpha: float, link_model: str = "ring",
+                 pp: Optional[PlacementPolicy] = None):
         self.topos = topos
         self.policy = policy
         self.alpha = alpha
         self.link_model = link_model
         self._lf: Dict[tuple, float] = {}
-        self.pp = PlacementPolicy()
+        self.pp = pp or PlacementPolicy()
         self.used: List[set] = [set() for _ in topos]
         self.memo: Dict[Tuple[int, Tuple[int, ...], int], Optional[Tuple[Tuple[int, ...], float]]] = {}
 
@@ -186,8 +187,22 @@ class Sim:
         return self._lf[key]
 
 
-def run(topos: List[Topology], trace, policy: str, alpha: float, link_model: str = "ring") -> Dict[str, object]:
-    sim = Sim(topos, policy, alpha, link_model)
+def policy_from(weights: str) -> PlacementPolicy:
+    """``w_fit=0,w_frag=0.5`` -> the default PlacementPolicy with those weights replaced."""
+    import dataclasses
+
+    kw = {}
+    for item in filter(None, (x.strip() for x in weights.split(","))):
+        name, _, val = item.partition("=")
+        if not name.startswith("w_") or not hasattr(PlacementPolicy, name):
+            raise SystemExit(f"--weights: unknown weight {name!r}")
+        kw[name] = float(val)
+    return dataclasses.replace(PlacementPolicy(), **kw)
+
+
+def run(topos: List[Topology], trace, policy: str, alpha: float, link_model: str = "ring",
+        pp: Optional[PlacementPolicy] = None) -> Dict[str, object]:
+    sim = Sim(topos, policy, alpha, link_model, pp)
     n_gpus = 8 * len(topos)
     events: List[Tuple[float, int, str, int]] = []  # (time, seq, kind, job)
     seq = 0
@@ -263,8 +278,11 @@ def main() -> int:
                     help="how a placement's links slow its collectives (Sim.link_factor)")
     ap.add_argument("--seeds", default="1,2,3")
     ap.add_argument("--policies", default=",".join(POLICIES))
+    ap.add_argument("--weights", default="", help="objective weights for every policy's scoring and node ranking, "
+                                                  "e.g. w_fit=0,w_frag=0 (an ablation; default: PlacementPolicy())")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
+    pp = policy_from(a.weights)
     results = []
     summaries = {}
     for kind in a.node_kind.split(","):
@@ -272,7 +290,7 @@ def main() -> int:
             topos = make_cluster(a.nodes, a.degraded, seed, kind)
             trace = make_trace(a.jobs, 8 * a.nodes, a.load, a.mean_min, seed)
             for pol in a.policies.split(","):
-                r = run(topos, trace, pol, a.alpha, a.link_model)
+                r = run(topos, trace, pol, a.alpha, a.link_model, pp)
                 r["seed"], r["node_kind"] = seed, kind
                 print(json.dumps(r), flush=True)
                 results.append(r)
