@@ -48,7 +48,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gpu_topology_on_k8s_amd.placement import PlacementPolicy, select  # noqa: E402
 from gpu_topology_on_k8s_amd.placement.core import Problem, evaluate, node_packing_term  # noqa: E402
 from gpu_topology_on_k8s_amd.placement.gaia import gaia_schedule, tree_from_topology  # noqa: E402
-from gpu_topology_on_k8s_amd.placement.legacy import design_greedy_select  # noqa: E402
+from gpu_topology_on_k8s_amd.placement.legacy import design_farthest_single, design_greedy_select  # noqa: E402
 from gpu_topology_on_k8s_amd.topology.model import Topology  # noqa: E402
 
 POLICIES = ("exact", "gaia", "design", "k8s-spread", "k8s-binpack")
@@ -105,7 +105,8 @@ def make_trace(n_jobs: int, n_gpus: int, load: float, mean_min: float, seed: int
 
 class Sim:
     def __init__(self, topos: List[Topology], policy: str, alpha: float, link_model: str = "ring",
-                 pp: Optional[PlacementPolicy] = None):
+                 pp: Optional[PlacementPolicy] = None, single: str = "objective"):
+        self.single = single
         self.topos = topos
         self.policy = policy
         self.alpha = alpha
@@ -124,7 +125,13 @@ class Sim:
         t = self.topos[n]
         res = None
         if 8 - len(used) >= k:
-            if self.policy == "exact":
+            if self.policy == "exact" and k == 1 and self.single == "farthest":
+                # the reference design's rule for one GPU (design.md:135-147): the free device farthest
+                # from the others, so the well-linked ones stay together for multi-GPU jobs
+                i = design_farthest_single(t.cost, list(used))
+                j, _ = evaluate(Problem.from_topology(t, list(used)), [i], self.pp)
+                res = ((int(i),), j)
+            elif self.policy == "exact":
                 pl = select(t, k, used=list(used), policy=self.pp)
                 res = (tuple(pl.ids), pl.objective)
             else:
@@ -201,8 +208,8 @@ def policy_from(weights: str) -> PlacementPolicy:
 
 
 def run(topos: List[Topology], trace, policy: str, alpha: float, link_model: str = "ring",
-        pp: Optional[PlacementPolicy] = None) -> Dict[str, object]:
-    sim = Sim(topos, policy, alpha, link_model, pp)
+        pp: Optional[PlacementPolicy] = None, single: str = "objective") -> Dict[str, object]:
+    sim = Sim(topos, policy, alpha, link_model, pp, single)
     n_gpus = 8 * len(topos)
     events: List[Tuple[float, int, str, int]] = []  # (time, seq, kind, job)
     seq = 0
@@ -280,6 +287,8 @@ def main() -> int:
     ap.add_argument("--policies", default=",".join(POLICIES))
     ap.add_argument("--weights", default="", help="objective weights for every policy's scoring and node ranking, "
                                                   "e.g. w_fit=0,w_frag=0 (an ablation; default: PlacementPolicy())")
+    ap.add_argument("--single", default="objective", choices=["objective", "farthest"],
+                    help="exact's choice for 1-GPU jobs: the objective's, or the reference design's farthest device")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     pp = policy_from(a.weights)
@@ -290,7 +299,7 @@ def main() -> int:
             topos = make_cluster(a.nodes, a.degraded, seed, kind)
             trace = make_trace(a.jobs, 8 * a.nodes, a.load, a.mean_min, seed)
             for pol in a.policies.split(","):
-                r = run(topos, trace, pol, a.alpha, a.link_model, pp)
+                r = run(topos, trace, pol, a.alpha, a.link_model, pp, a.single)
                 r["seed"], r["node_kind"] = seed, kind
                 print(json.dumps(r), flush=True)
                 results.append(r)
