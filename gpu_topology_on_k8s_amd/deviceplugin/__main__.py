@@ -155,6 +155,10 @@ def main(argv=None) -> int:
                          "The node label <annotation-prefix>/time-slices overrides it per node")
     ap.add_argument("--label-check-interval", type=float, default=30.0,
                     help="seconds between checks of the node's time-slices label (a change restarts the plugin once idle)")
+    ap.add_argument("--container-ipc-mode", default=None,
+                    help="HSA_ENABLE_IPC_MODE_LEGACY for every allocated container (default: this plugin's own value, "
+                         "0 in the rendered manifests; '' to set none). 0 lets RCCL's multi-process IPC work on hosts whose "
+                         "driver exports IPC handles only as dma-bufs")
     ap.add_argument("--share-guard", default="preload", choices=["off", "env", "preload"],
                     help="--time-slices: mount and preload libgtk_vgpu.so into pods holding part of a GPU, which caps their HIP "
                          "allocations at the share's HBM and forces their CU mask (preload = an /etc/ld.so.preload mount plus "
@@ -253,7 +257,8 @@ def main(argv=None) -> int:
                        probe_yield_s=a.probe_yield_seconds,
                        reconcile_interval=a.reconcile_interval, admission_settle_s=a.admission_settle, cdi_dir=a.cdi_dir, nic_env=a.nic_env == "on",
                        share_cu_mask=a.share_cu_mask == "on", share_guard=a.share_guard, guard_dir=a.share_guard_dir,
-                       policy=PlacementPolicy(partition_aware=a.partition_aware == "on"), topology_manager=tm)
+                       policy=PlacementPolicy(partition_aware=a.partition_aware == "on"), topology_manager=tm,
+                       container_ipc_mode=a.container_ipc_mode)
     events = None
     if a.gpu_events == "auto" and a.discovery in ("auto", "amdsmi"):
         from .events import GpuEventWatcher

@@ -147,8 +147,13 @@ class PluginConfig:
                  share_cu_mask: bool = True, probe_mark_s: float = 300.0, probe_settle_s: float = 2.0,
                  probe_yield_s: float = 20.0, share_guard: str = "off", guard_dir: str = "/var/lib/gtk-vgpu",
                  guard_lib: Optional[str] = None, admission_settle_s: float = 5.0,
-                 topology_manager: Optional[TopologyManager] = None):
+                 topology_manager: Optional[TopologyManager] = None, container_ipc_mode: Optional[str] = None):
         self.resource_name = resource_name
+        # HSA_ENABLE_IPC_MODE_LEGACY handed to every allocated container (None: the plugin's own value;
+        # "": none).  On hosts whose amdgpu driver exports IPC handles only as dma-bufs, ROCr needs 0 or a
+        # multi-process RCCL job in the pod fails in hipIpcGetMemHandle (docs/OPERATIONS.md "IPC")
+        self.container_ipc_mode = (os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "") if container_ipc_mode is None
+                                   else container_ipc_mode)
         self.socket_dir = socket_dir
         self.socket_name = socket_name
         self.kubelet_socket = kubelet_socket or os.path.join(socket_dir, "kubelet.sock")
@@ -960,6 +965,8 @@ class DevicePluginServer:
         if nics:
             r.envs["GTK_NICS"] = ",".join(nics)
             r.envs["NCCL_IB_HCA"] = "=" + ",".join(nics)  # exact-name match
+        if self.cfg.container_ipc_mode:  # before the pod's own env (rccl-env), which may override it
+            r.envs["HSA_ENABLE_IPC_MODE_LEGACY"] = self.cfg.container_ipc_mode
         for k, v in extra_env.items():
             r.envs[k] = v
         if mask:  # after the pod's own RCCL/HSA env: its queues run on its slices' CUs, disjoint from its neighbours'

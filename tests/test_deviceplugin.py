@@ -169,6 +169,29 @@ def test_rccl_env_passthrough(node):
     assert "LD_PRELOAD" not in envs  # only RCCL/HIP tuning variables pass
 
 
+def test_containers_get_the_ipc_mode_rccl_needs(node, monkeypatch):
+    """Every allocated container gets HSA_ENABLE_IPC_MODE_LEGACY as the plugin has it (0 in the rendered
+    manifests: dma-buf IPC handles, which multi-process RCCL needs on these hosts); a pod's rccl-env may
+    override it, and an empty setting hands none."""
+    api, kubelet, plugin, _ = node
+    c = Contract(resource_name=RES)
+    plugin.cfg.container_ipc_mode = "0"
+    pod = api.create_pod(make_pod("ipc", gpus=2, node="n1", annotations=PodAssignment.assumed([0, 1], 1).to_annotations()))
+    assert kubelet.admit(pod, RES).container_responses[0].envs["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    pod = api.create_pod(make_pod("own", gpus=1, node="n1", annotations={
+        f"{c.prefix}/rccl-env": "HSA_ENABLE_IPC_MODE_LEGACY=1", **PodAssignment.assumed([2], 1).to_annotations()}))
+    assert kubelet.admit(pod, RES).container_responses[0].envs["HSA_ENABLE_IPC_MODE_LEGACY"] == "1"
+    plugin.cfg.container_ipc_mode = ""
+    pod = api.create_pod(make_pod("none", gpus=1, node="n1", annotations=PodAssignment.assumed([3], 1).to_annotations()))
+    assert "HSA_ENABLE_IPC_MODE_LEGACY" not in kubelet.admit(pod, RES).container_responses[0].envs
+    from gpu_topology_on_k8s_amd.deviceplugin.plugin import PluginConfig as PC
+
+    monkeypatch.setenv("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    assert PC().container_ipc_mode == "0" and PC(container_ipc_mode="").container_ipc_mode == ""
+    monkeypatch.delenv("HSA_ENABLE_IPC_MODE_LEGACY")
+    assert PC().container_ipc_mode == ""
+
+
 def test_kubelet_restart_triggers_reregistration(node):
     api, kubelet, plugin, _ = node
     assert plugin.registered == 1
