@@ -135,3 +135,29 @@ def test_pod_flow_then_training_on_the_allocated_device():
     assert p.returncode == 0, p.stderr[-3000:]
     out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
     assert out["devices"] == [r.allocated[0]] and out["images_per_s"] > 0
+
+
+def test_the_allocated_env_opens_ipc_handles_across_processes():
+    """The device plugin hands each container the IPC mode multi-process RCCL needs on these hosts
+    (HSA_ENABLE_IPC_MODE_LEGACY=0, the plugin's own setting in the manifests): a process started with
+    only the container's value exports a buffer that a second process opens and reads exactly."""
+    from gpu_topology_on_k8s_amd.sim import SimCluster
+    from gpu_topology_on_k8s_amd.topology.discovery import discover
+
+    t = discover("auto")
+    t.node_name = "gpu-node"
+    with SimCluster({"gpu-node": t}) as c:
+        c.nodes["gpu-node"].plugin.cfg.container_ipc_mode = "0"
+        c.submit("ipc", 1)
+        r = c.schedule_pending()[0]
+        assert r.error == "" and len(r.allocated) == 1
+        envs = dict(c.nodes["gpu-node"].kubelet.responses["default/ipc"].container_responses[0].envs)
+    assert envs["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "HSA_ENABLE_IPC_MODE_LEGACY")}
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = envs["HSA_ENABLE_IPC_MODE_LEGACY"]
+    p = subprocess.run([sys.executable, "-m", "gpu_topology_on_k8s_amd", "ipc", "--bytes", str(64 << 20)], capture_output=True,
+                       text=True, timeout=300, cwd=REPO, env=env)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and lines, p.stderr[-2000:]
+    out = json.loads(lines[-1])
+    assert out["ok"] and out["ipc_mode_legacy"] == "0", out
