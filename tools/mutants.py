@@ -47,6 +47,7 @@ INFORMER = "gpu_topology_on_k8s_amd/k8s/informer.py"
 RBAC = "gpu_topology_on_k8s_amd/k8s/rbac.py"
 NUMA_ALIGN = "gpu_topology_on_k8s_amd/placement/numa_align.py"
 PLUGIN_MAIN = "gpu_topology_on_k8s_amd/deviceplugin/__main__.py"
+KUBELET = "gpu_topology_on_k8s_amd/deviceplugin/kubelet.py"
 CORE = "gpu_topology_on_k8s_amd/placement/core.py"
 ENGINE = "csrc/placement/engine.cpp"
 
@@ -120,6 +121,10 @@ MUTANTS: List[Mutant] = [
     Mutant("plugin", PLUGIN, '            if pod_phase(p) != "Pending" and (pa is None or pa.assigned):',
            '            if pod_phase(p) != "Pending":'),
     Mutant("plugin", PLUGIN, '            if pod_phase(p) != "Pending" and (pa is None or pa.assigned):', '            if False:'),
+    Mutant("plugin", PLUGIN, "        if self.cfg.container_ipc_mode:  # before the pod's own env", "        if False:  # before the pod's own env"),
+    Mutant("plugin", PLUGIN, '            return int(res.get("k", 0)) >= int(json.loads(old).get("k", 0))', "            return True"),
+    Mutant("plugin", KUBELET, '        if getattr(p.options, "pre_start_required", False):\n            try:',
+           "        if False:\n            try:"),
     # informer (client-go reflector semantics)
     Mutant("informer", INFORMER, "                failures += 1\n                self.last_error = str(e)",
            "                failures += 1\n                rv = None\n                self.last_error = str(e)"),
