@@ -136,9 +136,36 @@ def check_topology_manager(kubelet_config: str = "/var/lib/kubelet/config.yaml")
     if not tm.active:
         return _c("topology-manager", "ok", "policy none: the kubelet takes the plugin's preferred devices as they are",
                   policy=tm.policy, scope=tm.scope)
+    unmodelled = _unmodelled_tm_options(kubelet_config)
+    if unmodelled:
+        return _c("topology-manager", "warn", f"policy {tm.policy}, scope {tm.scope} with topologyManagerPolicyOptions "
+                                              f"{', '.join(unmodelled)}: the extender replays the default merge (equally narrow "
+                                              "hints tie-break on the lowest NUMA bitmask), so where these options make the "
+                                              "kubelet pick other NUMA nodes the plugin's GROUP is overridden "
+                                              "(gtk_plugin_group_overridden_total) and the reconcile corrects the annotations",
+                  policy=tm.policy, scope=tm.scope, options=unmodelled)
     return _c("topology-manager", "ok", f"policy {tm.policy}, scope {tm.scope}: run the device plugin with "
                                         f"--topology-manager-policy={tm.policy} --topology-manager-scope={tm.scope} "
                                         "(or --kubelet-config on this file)", policy=tm.policy, scope=tm.scope)
+
+
+#: kubelet Topology Manager policy options that leave the device hints and their merge as the
+#: extender replays them (placement/numa_align.py); any other option enabled is reported
+_TM_OPTIONS_MODELLED = {"max-allowable-numa-nodes"}
+
+
+def _unmodelled_tm_options(kubelet_config: str) -> List[str]:
+    """``topologyManagerPolicyOptions`` the extender does not model and the file enables (e.g.
+    ``prefer-closest-numa-nodes``, which breaks ties between equally narrow hints by NUMA distance)."""
+    import yaml
+
+    with open(kubelet_config) as f:
+        cfg = yaml.safe_load(f) or {}
+    opts = cfg.get("topologyManagerPolicyOptions") or {}
+    if not isinstance(opts, dict):
+        return []
+    return sorted(str(k) for k, v in opts.items()
+                  if k not in _TM_OPTIONS_MODELLED and str(v).strip().lower() not in ("false", "0", ""))
 
 
 def check_plugin_dir(path: str) -> Check:

@@ -30,7 +30,9 @@ chooses where the kubelet leaves the choice to the plugin.  It answers the GROUP
 allocate, or why the kubelet would reject the pod.
 
 What is not modelled: hints of the CPU and memory managers (a Guaranteed pod with integer CPUs under
-the static CPU policy narrows the merged hint further), and which of several reusable devices the
+the static CPU policy narrows the merged hint further); the ``prefer-closest-numa-nodes`` policy
+option (ties between equally narrow hints broken by NUMA distance; ``gtk doctor`` warns when a
+kubelet enables it); and which of several reusable devices the
 kubelet hands a container (its set iteration order is unspecified; the lowest ids are assumed).  The
 device plugin's pod-resources reconcile corrects the annotations when the kubelet chose otherwise.
 

@@ -368,6 +368,14 @@ def test_doctor_names_the_plugin_flags_the_kubelet_needs(tmp_path):
     assert c["status"] == "ok" and c["policy"] == "restricted" and "--topology-manager-policy=restricted" in c["detail"]
     f.write_text("kind: KubeletConfiguration\ntopologyManagerPolicy: bogus\n")
     assert check_topology_manager(str(f))["status"] == "fail"
+    # policy options: prefer-closest-numa-nodes changes the hint tie-break the extender replays -> warned
+    f.write_text("kind: KubeletConfiguration\ntopologyManagerPolicy: best-effort\n"
+                 "topologyManagerPolicyOptions:\n  prefer-closest-numa-nodes: \"true\"\n  max-allowable-numa-nodes: \"16\"\n")
+    c = check_topology_manager(str(f))
+    assert c["status"] == "warn" and c["options"] == ["prefer-closest-numa-nodes"] and "overridden" in c["detail"]
+    f.write_text("kind: KubeletConfiguration\ntopologyManagerPolicy: best-effort\n"
+                 "topologyManagerPolicyOptions:\n  prefer-closest-numa-nodes: \"false\"\n  max-allowable-numa-nodes: \"16\"\n")
+    assert check_topology_manager(str(f))["status"] == "ok"
 
 
 @pytest.mark.parametrize("used,reusable,size,want", [
