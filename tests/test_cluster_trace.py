@@ -106,3 +106,23 @@ def test_bench_scripts_compile_and_document_themselves():
     for name in ("share_mnist.py", "share_neighbor.py", "share_trace.py"):
         p = subprocess.run([sys.executable, os.path.join(root, "bench", name), "--help"], capture_output=True, text=True, timeout=60)
         assert p.returncode == 0 and "usage" in p.stdout.lower(), (name, p.stderr[-500:])
+
+
+def test_weights_and_single_gpu_rule_options():
+    """The ablation knobs (profiles/sched/ablation): ``--weights`` replaces objective weights and rejects
+    unknown names; ``--single farthest`` gives exact's 1-GPU jobs the device farthest from the others."""
+    pp = ct.policy_from("w_fit=0, w_frag=0.5")
+    assert pp.w_fit == 0.0 and pp.w_frag == 0.5 and pp.w_span == PlacementPolicy().w_span
+    with pytest.raises(SystemExit):
+        ct.policy_from("bogus=1")
+    with pytest.raises(SystemExit):
+        ct.policy_from("exact_limit=5")  # not a weight
+    topos = ct.make_cluster(2, 2, seed=3)
+    sim = ct.Sim(topos, "exact", 0.5, "bottleneck", pp, single="farthest")
+    (i,), _ = sim._choose_on(0, 1)
+    c = topos[0].cost
+    far = max(range(8), key=lambda d: sum(c[d, x] for x in range(8) if x != d))
+    assert i == far
+    trace = ct.make_trace(60, 16, 0.9, 60.0, seed=3)
+    r = ct.run(topos, trace, "exact", 0.5, "bottleneck", pp, "farthest")
+    assert r["jct_mean_min"] > 0 and r["runtime_inflation_mean"] >= 1.0
